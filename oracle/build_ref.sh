@@ -1,0 +1,51 @@
+#!/usr/bin/env bash
+# TEST INFRASTRUCTURE ONLY.
+# Builds oracle/_ref/libsrsref.so from the srsRAN reference sources where they lie under /root/reference (nothing is
+# copied into this repository) plus oracle/ref/ref_shim.cpp. Output goes only to oracle/_ref/ (git-ignored, shipped to
+# the GPU box with the snapshot). Skips quietly when the reference tree is absent (GPU box).
+set -euo pipefail
+REF=${SRSRAN_REF:-/root/reference}
+HERE=$(cd "$(dirname "$0")" && pwd)
+OUT="$HERE/_ref"
+if [ ! -d "$REF/lib/phy/upper/channel_coding/ldpc" ]; then
+  echo "build_ref: reference tree not present; keeping existing $OUT" >&2
+  exit 0
+fi
+mkdir -p "$OUT/obj"
+CXX=${CXX:-g++}
+FLAGS="-std=c++17 -O3 -fPIC -DNDEBUG -DFMT_HEADER_ONLY -DASSERTS_ENABLED=0 -I$REF/include -I$REF/external/fmt/include -I$REF/external -I$REF/lib/phy/upper/channel_coding"
+LDPC=$REF/lib/phy/upper/channel_coding/ldpc
+SRCS=(
+  "$LDPC/ldpc_graph_impl.cpp:"
+  "$LDPC/ldpc_luts_impl.cpp:"
+  "$LDPC/ldpc_encoder_impl.cpp:"
+  "$LDPC/ldpc_encoder_generic.cpp:"
+  "$LDPC/ldpc_encoder_avx2.cpp:-mavx2"
+  "$LDPC/ldpc_decoder_impl.cpp:"
+  "$LDPC/ldpc_decoder_generic.cpp:"
+  "$LDPC/ldpc_decoder_avx2.cpp:-mavx2"
+  "$LDPC/ldpc_decoder_avx512.cpp:-mavx512f -mavx512bw"
+  "$LDPC/ldpc_rate_matcher_impl.cpp:"
+  "$LDPC/ldpc_rate_dematcher_impl.cpp:"
+  "$LDPC/ldpc_rate_dematcher_avx2_impl.cpp:-mavx2"
+  "$LDPC/ldpc_segmenter_tx_impl.cpp:"
+  "$REF/lib/phy/upper/channel_coding/crc_calculator_generic_impl.cpp:"
+  "$REF/lib/phy/upper/log_likelihood_ratio.cpp:-mavx2"
+  "$REF/lib/srsvec/bit.cpp:-mavx2"
+  "$REF/lib/srsvec/compare.cpp:-mavx2"
+  "$HERE/ref/ref_shim.cpp:-mavx2"
+)
+OBJS=()
+pids=()
+for entry in "${SRCS[@]}"; do
+  src=${entry%%:*}; extra=${entry#*:}
+  obj="$OUT/obj/$(basename "${src%.cpp}").o"
+  OBJS+=("$obj")
+  if [ ! -f "$obj" ] || [ "$src" -nt "$obj" ] || [ "$0" -nt "$obj" ]; then
+    $CXX $FLAGS $extra -c "$src" -o "$obj" &
+    pids+=($!)
+  fi
+done
+for p in "${pids[@]:-}"; do [ -n "$p" ] && wait "$p"; done
+$CXX -shared -o "$OUT/libsrsref.so" "${OBJS[@]}"
+echo "build_ref: $OUT/libsrsref.so"

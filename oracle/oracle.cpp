@@ -1,0 +1,568 @@
+// =====================================================================================================================
+// TEST INFRASTRUCTURE ONLY — CPU restatement ("oracle") of the srsRAN reference algorithms on the accelerated path.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and only as the checker
+// (never as the thing measured or shipped). The product path (srsran-5g_amd/) never links or calls it.
+//
+// Pinning: every function here is checked bit-for-bit against the reference itself, compiled from its own sources by
+// oracle/build_ref.sh into oracle/_ref/libsrsref.so (tests/test_oracle_vs_reference.py), and against the committed
+// golden vectors in tests/golden/ that tools/gen_golden.py produced from that same reference build.
+//
+// Each function cites the reference file:line it restates (paths relative to /root/reference/lib/phy/upper/).
+// Plain scalar C-style code, written for clarity, not speed.
+// =====================================================================================================================
+#include "../srsran-5g_amd/csrc/ldpc_base_graphs.h"
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+namespace {
+
+// LLR constants: log_likelihood_ratio.h:300 (LLR_INFTY = 127, LLR_MAX = 120).
+constexpr int LLR_INF = 127;
+constexpr int LLR_MAX = 120;
+
+struct bg_view {
+  int             M, N_full, N_short, K;
+  const uint16_t* row_start;
+  const uint8_t*  col;
+  const uint16_t* V;
+};
+
+bool get_bg(int bg, int Z, bg_view& v)
+{
+  if (Z < 2 || Z > 384 || kLiftingSetIndex[Z] == 255) {
+    return false;
+  }
+  int ils = kLiftingSetIndex[Z];
+  if (bg == 1) {
+    v = {kBG1_M, kBG1_N_FULL, kBG1_N_FULL - 2, kBG1_K, kBG1_ROW_START, kBG1_COL, kBG1_V[ils]};
+  } else if (bg == 2) {
+    v = {kBG2_M, kBG2_N_FULL, kBG2_N_FULL - 2, kBG2_K, kBG2_ROW_START, kBG2_COL, kBG2_V[ils]};
+  } else {
+    return false;
+  }
+  return true;
+}
+
+// CRC generator polynomials, channel_coding/crc_calculator_generic_impl.cpp:30 (order, polynomial incl. x^order).
+bool crc_params(int poly, unsigned& order, uint64_t& g)
+{
+  switch (poly) {
+    case 0: order = 24; g = 0x1864cfb; return true;  // CRC24A
+    case 1: order = 24; g = 0x1800063; return true;  // CRC24B
+    case 2: order = 24; g = 0x1b2b117; return true;  // CRC24C
+    case 3: order = 16; g = 0x11021; return true;    // CRC16
+    case 4: order = 11; g = 0xe21; return true;      // CRC11
+    case 5: order = 6; g = 0x61; return true;        // CRC6
+    default: return false;
+  }
+}
+
+// Saturated LLR sum of the SIMD implementations: log_likelihood_ratio.cpp:432 (avx2_sum_llr) and
+// ldpc_rate_dematcher_avx2_impl.cpp:29 — int8 saturating add, then clamp to [-LLR_MAX, LLR_MAX].
+int8_t llr_sum_simd(int a, int b)
+{
+  int s = a + b;
+  s     = s > 127 ? 127 : (s < -128 ? -128 : s);
+  s     = s > LLR_MAX ? LLR_MAX : (s < -LLR_MAX ? -LLR_MAX : s);
+  return static_cast<int8_t>(s);
+}
+
+// Saturated LLR sum of the generic implementation: log_likelihood_ratio.cpp:40 (tackle_special_sums) + :58.
+int8_t llr_sum_generic(int a, int b)
+{
+  if (a == -b) {
+    return 0;
+  }
+  if (a > LLR_MAX || a < -LLR_MAX) {
+    return static_cast<int8_t>(a);
+  }
+  if (b > LLR_MAX || b < -LLR_MAX) {
+    return static_cast<int8_t>(b);
+  }
+  int s = a + b;
+  return static_cast<int8_t>(s > LLR_MAX ? LLR_MAX : (s < -LLR_MAX ? -LLR_MAX : s));
+}
+
+// Cyclic shift of the lifting: (P^s x)[l] = x[(l + s) % Z]. ldpc_encoder_generic.cpp:79 / ldpc_decoder_impl.cpp:103.
+inline int rot(int l, int s, int Z)
+{
+  int t = l + s;
+  return t >= Z ? t - Z : t;
+}
+
+} // namespace
+
+extern "C" {
+
+// ---------------------------------------------------------------------------------------------------------------------
+// CRC — channel_coding/crc_calculator_generic_impl.cpp:103 (calculate_bit): zero initial remainder, MSB first, the
+// message followed by `order` zero bits.
+// ---------------------------------------------------------------------------------------------------------------------
+unsigned orc_crc_bits(int poly, const uint8_t* bits, unsigned nbits)
+{
+  unsigned order;
+  uint64_t g;
+  if (!crc_params(poly, order, g)) {
+    return 0xffffffffu;
+  }
+  uint64_t high = 1ULL << order, rem = 0;
+  for (unsigned i = 0; i < nbits + order; ++i) {
+    rem = (rem << 1) | (i < nbits ? (bits[i] & 1U) : 0U);
+    if (rem & high) {
+      rem ^= g;
+    }
+  }
+  return static_cast<unsigned>(rem & (high - 1));
+}
+
+unsigned orc_crc_bytes(int poly, const uint8_t* bytes, unsigned nbytes)
+{
+  std::vector<uint8_t> bits(nbytes * 8);
+  for (unsigned i = 0; i < nbytes * 8; ++i) {
+    bits[i] = (bytes[i / 8] >> (7 - i % 8)) & 1U;
+  }
+  return orc_crc_bits(poly, bits.data(), nbytes * 8);
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// LDPC encoder — restates channel_coding/ldpc/ldpc_encoder_generic.cpp (preprocess_systematic_bits :58, high_rate_* :226,
+// ext_region_inner :107, write_codeblock :162) from the parity-check equations H·c = 0 directly:
+//   core rows 0..3:   sum_k P^{s(m,k)} x_k + sum_{j<4} P^{s(m,K+j)} p_j = 0 (double-diagonal core, solved generically),
+//   extension rows m: p_{K+m} = sum_{c < K+4} P^{s(m,c)} c_c (identity extension).
+// msg: K*Z unpacked bits. cb: N_short*Z unpacked output bits (the first 2Z systematic bits are shortened).
+// ---------------------------------------------------------------------------------------------------------------------
+int orc_ldpc_encode(int bg, int Z, const uint8_t* msg, uint8_t* cb)
+{
+  bg_view g;
+  if (!get_bg(bg, Z, g)) {
+    return -1;
+  }
+  const int            K = g.K;
+  std::vector<uint8_t> c(static_cast<size_t>(g.N_full) * Z, 0);
+  for (int i = 0; i < K * Z; ++i) {
+    c[i] = msg[i] & 1U;
+  }
+  // lambda_m = sum over information columns of the rotated message for the four core rows.
+  std::vector<uint8_t> lam(4 * Z, 0);
+  for (int m = 0; m < 4; ++m) {
+    for (int e = g.row_start[m]; e < g.row_start[m + 1]; ++e) {
+      int col = g.col[e];
+      if (col >= K) {
+        continue;
+      }
+      int s = g.V[e] % Z;
+      for (int l = 0; l < Z; ++l) {
+        lam[m * Z + l] ^= c[col * Z + rot(l, s, Z)];
+      }
+    }
+  }
+  // Core parity: collect per core row the (parity column, shift) pairs.
+  int pshift[4][4];
+  for (int m = 0; m < 4; ++m) {
+    for (int j = 0; j < 4; ++j) {
+      pshift[m][j] = -1;
+    }
+    for (int e = g.row_start[m]; e < g.row_start[m + 1]; ++e) {
+      int col = g.col[e];
+      if (col >= K && col < K + 4) {
+        pshift[m][col - K] = g.V[e] % Z;
+      }
+    }
+  }
+  // Summing the four core rows cancels p1..p3 (each appears twice with equal shifts) and leaves the column-K terms.
+  // Those are an odd number of rotations of p0 where equal shifts cancel pairwise: find the surviving shift x.
+  int cnt[384] = {0};
+  for (int m = 0; m < 4; ++m) {
+    if (pshift[m][0] >= 0) {
+      cnt[pshift[m][0]] ^= 1;
+    }
+  }
+  int x = -1, nsurv = 0;
+  for (int s = 0; s < Z; ++s) {
+    if (cnt[s]) {
+      x = s;
+      ++nsurv;
+    }
+  }
+  if (nsurv != 1) {
+    return -2;
+  }
+  // P^x p0 = sum_m lambda_m  =>  p0[(l + x) % Z] = sum_m lambda_m[l].
+  uint8_t* p[4];
+  for (int j = 0; j < 4; ++j) {
+    p[j] = &c[(K + j) * Z];
+  }
+  for (int l = 0; l < Z; ++l) {
+    uint8_t acc = lam[0 * Z + l] ^ lam[1 * Z + l] ^ lam[2 * Z + l] ^ lam[3 * Z + l];
+    p[0][rot(l, x, Z)] = acc;
+  }
+  // Solve p1..p3: repeatedly use a core row with exactly one unknown parity column (its shift is 0 by construction of
+  // the double-diagonal; handled generally via the rotation).
+  bool known[4] = {true, false, false, false};
+  for (int round = 0; round < 4; ++round) {
+    for (int m = 0; m < 4; ++m) {
+      int unknown = -1, nunk = 0;
+      for (int j = 0; j < 4; ++j) {
+        if (pshift[m][j] >= 0 && !known[j]) {
+          unknown = j;
+          ++nunk;
+        }
+      }
+      if (nunk != 1) {
+        continue;
+      }
+      int su = pshift[m][unknown];
+      for (int l = 0; l < Z; ++l) {
+        uint8_t acc = lam[m * Z + l];
+        for (int j = 0; j < 4; ++j) {
+          if (j != unknown && pshift[m][j] >= 0) {
+            acc ^= p[j][rot(l, pshift[m][j], Z)];
+          }
+        }
+        p[unknown][rot(l, su, Z)] = acc;
+      }
+      known[unknown] = true;
+    }
+  }
+  for (int j = 0; j < 4; ++j) {
+    if (!known[j]) {
+      return -3;
+    }
+  }
+  // Extension parity (identity extension: the V of column K+m in row m is 0 for every lifting set).
+  for (int m = 4; m < g.M; ++m) {
+    uint8_t* out = &c[(K + m) * Z];
+    for (int e = g.row_start[m]; e < g.row_start[m + 1]; ++e) {
+      int col = g.col[e];
+      int s   = g.V[e] % Z;
+      if (col >= K + 4) {
+        if (col != K + m || s != 0) {
+          return -4;
+        }
+        continue;
+      }
+      for (int l = 0; l < Z; ++l) {
+        out[l] ^= c[col * Z + rot(l, s, Z)];
+      }
+    }
+  }
+  std::memcpy(cb, &c[2 * Z], static_cast<size_t>(g.N_short) * Z);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// LDPC decoder — restates channel_coding/ldpc/ldpc_decoder_impl.cpp:60 (decode), :152 (load_soft_bits),
+// :195 (update_variable_to_check_messages), :255 (update_check_to_variable_messages), :240 (update_soft_bits),
+// :333 (get_hard_bits), with the per-implementation kernels of
+//   mode 0 = generic:  ldpc_decoder_generic.cpp:30/:46/:70/:85/:110
+//   mode 1 = SIMD:     ldpc_decoder_avx2.cpp:69/:111/:154/:165/:205 (ldpc_decoder_avx512.cpp and _neon.cpp are the
+//                      same arithmetic on wider/narrower registers; avx2_support.h:71 scale_epi8).
+// The two modes differ only in how the normalised min-sum factor is applied (round-to-nearest in float vs a 16-bit
+// fixed-point multiply that truncates).
+//
+// llr: n_llr input LLRs (the rate-dematched codeblock, first 2Z systematic bits excluded).
+// out: K*Z unpacked decoded bits. crc_poly < 0: no CRC early stop.
+// Returns the number of iterations when the CRC check succeeded, -1 otherwise (like std::nullopt).
+// Positions of a partial last node beyond n_llr are zero here (the reference leaves them stale when n_llr % Z != 0).
+// ---------------------------------------------------------------------------------------------------------------------
+int orc_ldpc_decode(int           mode,
+                    int           bg,
+                    int           Z,
+                    int           nof_crc_bits,
+                    int           nof_filler_bits,
+                    int           crc_poly,
+                    int           max_iter,
+                    float         scaling,
+                    const int8_t* llr,
+                    unsigned      n_llr,
+                    uint8_t*      out)
+{
+  (void)nof_crc_bits;
+  bg_view g;
+  if (!get_bg(bg, Z, g) || max_iter <= 0) {
+    return -2;
+  }
+  const int K       = g.K;
+  const int msg_len = K * Z;
+  if (static_cast<int>(n_llr) > g.N_short * Z || static_cast<int>(n_llr) < msg_len + 2 * Z) {
+    return -2;
+  }
+  // Trim trailing zero LLRs (decode :94).
+  int input_size = static_cast<int>(n_llr);
+  while (input_size > 0 && llr[input_size - 1] == 0) {
+    --input_size;
+  }
+  if (input_size < msg_len) {
+    if (crc_poly < 0) {
+      for (int i = 0; i < msg_len; ++i) {
+        out[i] = 1;
+      }
+    }
+    return -1;
+  }
+  // load_soft_bits (:152): two shortened nodes of zeros, then the LLRs clamped to +/-64 per whole node; the trailing
+  // partial node (if any) copied unclamped.
+  std::vector<int> soft(static_cast<size_t>(g.N_full) * Z, 0);
+  int              full = (static_cast<int>(n_llr) / Z) * Z;
+  for (int i = 0; i < full; ++i) {
+    int v            = llr[i];
+    soft[2 * Z + i]  = v > 64 ? 64 : (v < -64 ? -64 : v);
+  }
+  for (int i = full; i < static_cast<int>(n_llr); ++i) {
+    soft[2 * Z + i] = llr[i];
+  }
+  // Codeblock length and number of layers (:118-:128).
+  int cb_len = input_size + 2 * Z;
+  if (cb_len < msg_len + 4 * Z) {
+    cb_len = msg_len + 4 * Z;
+  }
+  if (cb_len % Z != 0) {
+    cb_len = (cb_len / Z + 1) * Z;
+  }
+  const int nof_layers = cb_len / Z - K;
+
+  // Check-to-variable messages, stored per (edge, check row j) — the rotated domain of the reference.
+  const int        nE = g.row_start[g.M];
+  std::vector<int> c2v(static_cast<size_t>(nE) * Z, 0);
+  std::vector<int> v2c(static_cast<size_t>(20) * Z);
+  std::vector<int> min1(Z), min2(Z), idx(Z), sgn(Z);
+  const uint16_t   sf16 = static_cast<uint16_t>(scaling * 65536U);
+
+  auto scale = [&](int a) -> int {
+    if (mode == 0) {
+      // ldpc_decoder_generic.cpp:70 scale_llr
+      if (a > LLR_MAX || a < -LLR_MAX) {
+        return a;
+      }
+      return static_cast<int>(std::round(static_cast<float>(a) * scaling));
+    }
+    // avx2_support.h:71 scale_epi8 (non-negative inputs here: the magnitudes).
+    if (scaling >= .9999) {
+      return a;
+    }
+    if (a > LLR_MAX) {
+      return a;
+    }
+    return static_cast<int>((static_cast<uint32_t>(a) * sf16) >> 16);
+  };
+
+  unsigned order = 0;
+  uint64_t gpoly = 0;
+  if (crc_poly >= 0 && !crc_params(crc_poly, order, gpoly)) {
+    return -2;
+  }
+  const int nof_significant = msg_len - nof_filler_bits;
+
+  for (int it = 0; it < max_iter; ++it) {
+    for (int m = 0; m < nof_layers; ++m) {
+      const int e0 = g.row_start[m], e1 = g.row_start[m + 1];
+      for (int j = 0; j < Z; ++j) {
+        min1[j] = LLR_MAX;  // srsvec::fill(min, LLR_MAX) (:270)
+        min2[j] = LLR_MAX;
+        idx[j]  = 0;
+        sgn[j]  = 0;
+      }
+      // Variable-to-check messages (:195 + ldpc_decoder_avx2.cpp:69). c2v is always finite (|c2v| <= LLR_MAX because
+      // the minimum trackers start at LLR_MAX), so generic and SIMD saturation rules coincide here.
+      for (int e = e0; e < e1; ++e) {
+        const int col = g.col[e], s = g.V[e] % Z, ei = e - e0;
+        for (int j = 0; j < Z; ++j) {
+          int sb = soft[col * Z + rot(j, s, Z)];
+          int v;
+          if (sb >= LLR_INF || sb <= -LLR_INF) {
+            v = sb;
+          } else {
+            v = sb - c2v[static_cast<size_t>(e) * Z + j];
+            v = v > LLR_MAX ? LLR_MAX : (v < -LLR_MAX ? -LLR_MAX : v);
+          }
+          v2c[static_cast<size_t>(ei) * Z + j] = v;
+          // analyze_var_to_check_msgs (ldpc_decoder_generic.cpp:46).
+          int  a       = v < 0 ? -v : v;
+          bool is_min  = a < min1[j];
+          int  nsecond = is_min ? min1[j] : a;
+          if (a < min2[j]) {
+            min2[j] = nsecond;
+          }
+          if (is_min) {
+            min1[j] = a;
+            idx[j]  = ei;
+          }
+          sgn[j] ^= (v < 0) ? 1 : 0;
+        }
+      }
+      // Check-to-variable messages and soft-bit update (:255 + :240).
+      for (int e = e0; e < e1; ++e) {
+        const int col = g.col[e], s = g.V[e] % Z, ei = e - e0;
+        for (int j = 0; j < Z; ++j) {
+          int v   = v2c[static_cast<size_t>(ei) * Z + j];
+          int mag = scale(ei == idx[j] ? min2[j] : min1[j]);
+          int neg = sgn[j] ^ ((v < 0) ? 1 : 0);
+          int c   = neg ? -mag : mag;
+          c2v[static_cast<size_t>(e) * Z + j] = c;
+          // Promotion sum (log_likelihood_ratio.cpp:75, ldpc_decoder_avx2.cpp:205).
+          int sb;
+          if (v >= LLR_INF || v <= -LLR_INF) {
+            sb = v;
+          } else if (c == -v) {
+            sb = 0;
+          } else {
+            int t = c + v;
+            sb    = t > LLR_MAX ? LLR_INF : (t < -LLR_MAX ? -LLR_INF : t);
+          }
+          soft[col * Z + rot(j, s, Z)] = sb;
+        }
+      }
+    }
+    if (crc_poly >= 0) {
+      bool ok = true;
+      for (int i = 0; i < msg_len; ++i) {
+        out[i] = soft[i] <= 0 ? 1 : 0;
+        ok &= soft[i] != 0;
+      }
+      if (ok && orc_crc_bits(crc_poly, out, nof_significant) == 0) {
+        return it + 1;
+      }
+    }
+  }
+  if (crc_poly < 0) {
+    for (int i = 0; i < msg_len; ++i) {
+      out[i] = soft[i] <= 0 ? 1 : 0;
+    }
+  }
+  return -1;
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// Rate matching — channel_coding/ldpc/ldpc_rate_matcher_impl.cpp:37 (init: k0 from TS 38.212 Table 5.4.2.1-2),
+// :104 (select_bits: circular buffer read skipping filler bits) and :150 (bit interleaving, TS 38.212 5.4.2.2).
+// cb: N_short*Z codeblock bits (unpacked; filler bits may hold any value, they are skipped). out: E unpacked bits.
+// ---------------------------------------------------------------------------------------------------------------------
+static bool rm_params(int bg, int Z, int rv, unsigned Nref, unsigned nof_filler, unsigned& Ncb, unsigned& k0,
+                      unsigned& nsys, unsigned& N)
+{
+  static const double sf1[4] = {0, 17, 33, 56};
+  static const double sf2[4] = {0, 13, 25, 43};
+  bg_view             g;
+  if (!get_bg(bg, Z, g) || rv < 0 || rv > 3) {
+    return false;
+  }
+  N        = static_cast<unsigned>(g.N_short * Z);
+  Ncb      = (Nref > 0 && Nref < N) ? Nref : N;
+  nsys     = static_cast<unsigned>((g.K - 2) * Z);
+  double t = ((bg == 1 ? sf1 : sf2)[rv] * Ncb) / N;
+  k0       = static_cast<unsigned>(std::floor(t)) * Z;
+  return nof_filler < nsys;
+}
+
+int orc_rate_match(int bg, int Z, int rv, int qm, unsigned Nref, unsigned nof_filler, const uint8_t* cb, unsigned E,
+                   uint8_t* out)
+{
+  unsigned Ncb, k0, nsys, N;
+  if (!rm_params(bg, Z, rv, Nref, nof_filler, Ncb, k0, nsys, N) || qm <= 0 || E % qm != 0) {
+    return -1;
+  }
+  const unsigned       fill_lo = nsys - nof_filler, fill_hi = nsys;
+  std::vector<uint8_t> e(E);
+  unsigned             k = k0;
+  for (unsigned n = 0; n < E;) {
+    if (!(k >= fill_lo && k < fill_hi)) {
+      e[n++] = cb[k] & 1U;
+    }
+    k = (k + 1) % Ncb;
+  }
+  // Interleaving: output symbol i carries bits e[j*E/Qm + i], j = 0..Qm-1 (:150).
+  const unsigned R = E / qm;
+  for (unsigned i = 0; i < R; ++i) {
+    for (int j = 0; j < qm; ++j) {
+      out[i * qm + j] = e[j * R + i];
+    }
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// Rate dematching — channel_coding/ldpc/ldpc_rate_dematcher_impl.cpp:46 (rate_dematch), :203 (deinterleave),
+// :128 (allot_llrs: copy on the first pass over the circular buffer when new_data, saturated combining afterwards;
+// filler bits set to +LLR_INFTY; unvisited positions zeroed). mode 0: generic combining (:116 -> LLR operator+),
+// mode 1: SIMD combining (ldpc_rate_dematcher_avx2_impl.cpp:29).
+// llr: E input LLRs. buf: N_short*Z LLRs (read when combining, written).
+// ---------------------------------------------------------------------------------------------------------------------
+int orc_rate_dematch(int mode, int bg, int Z, int rv, int qm, unsigned Nref, unsigned nof_filler, int new_data,
+                     const int8_t* llr, unsigned E, int8_t* buf)
+{
+  unsigned Ncb, k0, nsys, N;
+  if (!rm_params(bg, Z, rv, Nref, nof_filler, Ncb, k0, nsys, N) || qm <= 0 || E % qm != 0) {
+    return -1;
+  }
+  // Deinterleave (:203): e[j*R + i] = llr[i*Qm + j].
+  std::vector<int8_t> e(E);
+  const unsigned      R = E / qm;
+  for (unsigned i = 0; i < R; ++i) {
+    for (int j = 0; j < qm; ++j) {
+      e[j * R + i] = llr[i * qm + j];
+    }
+  }
+  const unsigned nof_info = nsys - nof_filler;
+  // allot_llrs (:128), step by step: note that in copy mode with k0 inside the parity region the positions
+  // [nsys, k0) keep their previous content, exactly like the reference.
+  auto put = [&](unsigned pos, int8_t v, bool cp) {
+    buf[pos] = cp ? v : ((mode == 0) ? llr_sum_generic(buf[pos], v) : llr_sum_simd(buf[pos], v));
+  };
+  bool     copy = new_data != 0;
+  unsigned k    = k0;
+  unsigned n    = 0;
+  while (n < E) {
+    if (k < nof_info) {
+      unsigned cnt = nof_info - k;
+      if (cnt > E - n) {
+        cnt = E - n;
+      }
+      if (copy) {
+        for (unsigned i = 0; i < k; ++i) {
+          buf[i] = 0;
+        }
+      }
+      for (unsigned i = 0; i < cnt; ++i) {
+        put(k + i, e[n + i], copy);
+      }
+      k += cnt;
+      n += cnt;
+    } else if (copy) {
+      for (unsigned i = 0; i < nof_info; ++i) {
+        buf[i] = 0;
+      }
+    }
+    if (copy) {
+      for (unsigned i = nof_info; i < nsys; ++i) {
+        buf[i] = static_cast<int8_t>(LLR_INF);
+      }
+    }
+    if (k < nsys) {
+      k = nsys;
+    }
+    unsigned cnt = Ncb - k;
+    if (cnt > E - n) {
+      cnt = E - n;
+    }
+    for (unsigned i = 0; i < cnt; ++i) {
+      put(k + i, e[n + i], copy);
+    }
+    k = (k + cnt) % Ncb;
+    n += cnt;
+    if (n < E) {
+      copy = false;
+    }
+  }
+  if (copy && k != 0) {
+    for (unsigned i = k; i < Ncb; ++i) {
+      buf[i] = 0;
+    }
+  }
+  return 0;
+}
+
+} // extern "C"

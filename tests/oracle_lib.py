@@ -1,0 +1,159 @@
+"""Test-side loaders for the CPU oracle (oracle/liboracle.so) and the reference build (oracle/_ref/libsrsref.so).
+
+TEST INFRASTRUCTURE ONLY: these are the checkers; the product (srsran-5g_amd/) never imports this module.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libsrsref.so")
+
+CRC24A, CRC24B, CRC24C, CRC16, CRC11, CRC6 = range(6)
+CRC_LEN = {CRC24A: 24, CRC24B: 24, CRC24C: 24, CRC16: 16, CRC11: 11, CRC6: 6}
+LIFTING_SIZES = [2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 18, 20, 22, 24, 26, 28, 30, 32, 36, 40, 44, 48,
+                 52, 56, 60, 64, 72, 80, 88, 96, 104, 112, 120, 128, 144, 160, 176, 192, 208, 224, 240, 256, 288, 320,
+                 352, 384]
+BG_K = {1: 22, 2: 10}
+BG_N_SHORT = {1: 66, 2: 50}
+
+_P = ctypes.c_void_p
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_P)
+
+
+def _setup(lib, prefix):
+    f = getattr(lib, prefix + "crc_bits")
+    f.restype = ctypes.c_uint
+    f.argtypes = [ctypes.c_int, _P, ctypes.c_uint]
+    f = getattr(lib, prefix + "crc_bytes")
+    f.restype = ctypes.c_uint
+    f.argtypes = [ctypes.c_int, _P, ctypes.c_uint]
+    f = getattr(lib, prefix + "ldpc_decode")
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int] * 7 + [ctypes.c_float, _P, ctypes.c_uint, _P]
+
+
+class _Lib:
+    def __init__(self, path, prefix):
+        self.lib = ctypes.CDLL(path)
+        self.prefix = prefix
+        _setup(self.lib, prefix)
+
+    def _f(self, name):
+        return getattr(self.lib, self.prefix + name)
+
+    def crc_bits(self, poly, bits):
+        bits = np.ascontiguousarray(bits, dtype=np.uint8)
+        return int(self._f("crc_bits")(poly, _ptr(bits), bits.size))
+
+    def crc_bytes(self, poly, data):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        return int(self._f("crc_bytes")(poly, _ptr(data), data.size))
+
+    def ldpc_decode(self, mode, bg, Z, llr, nof_crc_bits=16, nof_filler=0, crc_poly=-1, max_iter=6, scaling=0.8,
+                    out_init=None):
+        llr = np.ascontiguousarray(llr, dtype=np.int8)
+        K = BG_K[bg]
+        out = np.zeros(K * Z, np.uint8) if out_init is None else np.array(out_init, dtype=np.uint8)
+        r = self._f("ldpc_decode")(mode, bg, Z, nof_crc_bits, nof_filler, crc_poly, max_iter, scaling, _ptr(llr),
+                                  llr.size, _ptr(out))
+        return r, out
+
+
+class Oracle(_Lib):
+    def __init__(self, path=ORACLE_SO):
+        super().__init__(path, "orc_")
+
+    def ldpc_encode(self, bg, Z, msg):
+        msg = np.ascontiguousarray(msg, dtype=np.uint8)
+        cb = np.zeros(BG_N_SHORT[bg] * Z, np.uint8)
+        r = self.lib.orc_ldpc_encode(bg, Z, _ptr(msg), _ptr(cb))
+        assert r == 0, r
+        return cb
+
+    def rate_match(self, bg, Z, rv, qm, Nref, nof_filler, cb, E):
+        cb = np.ascontiguousarray(cb, dtype=np.uint8)
+        out = np.zeros(E, np.uint8)
+        r = self.lib.orc_rate_match(bg, Z, rv, qm, ctypes.c_uint(Nref), ctypes.c_uint(nof_filler), _ptr(cb),
+                                    ctypes.c_uint(E), _ptr(out))
+        assert r == 0, r
+        return out
+
+    def rate_dematch(self, mode, bg, Z, rv, qm, Nref, nof_filler, new_data, llr, buf):
+        llr = np.ascontiguousarray(llr, dtype=np.int8)
+        buf = np.array(buf, dtype=np.int8)
+        r = self.lib.orc_rate_dematch(mode, bg, Z, rv, qm, ctypes.c_uint(Nref), ctypes.c_uint(nof_filler),
+                                      int(new_data), _ptr(llr), ctypes.c_uint(llr.size), _ptr(buf))
+        assert r == 0, r
+        return buf
+
+
+class Reference(_Lib):
+    """The srsRAN reference itself, built from its own sources (oracle/build_ref.sh)."""
+
+    GENERIC, AVX2, AVX512 = 0, 1, 2
+
+    def __init__(self, path=REF_SO):
+        super().__init__(path, "ref_")
+
+    def has_avx512(self):
+        return bool(self.lib.ref_cpu_has_avx512())
+
+    def ldpc_encode(self, bg, Z, msg, impl=0):
+        msg = np.ascontiguousarray(msg, dtype=np.uint8)
+        cb = np.zeros(BG_N_SHORT[bg] * Z, np.uint8)
+        self.lib.ref_ldpc_encode(impl, bg, Z, _ptr(msg), _ptr(cb))
+        return cb
+
+    def rate_match(self, bg, Z, rv, qm, Nref, nof_filler, msg, E):
+        msg = np.ascontiguousarray(msg, dtype=np.uint8)
+        out = np.zeros(E, np.uint8)
+        self.lib.ref_rate_match(bg, Z, rv, qm, ctypes.c_uint(Nref), ctypes.c_uint(nof_filler), _ptr(msg),
+                                ctypes.c_uint(E), _ptr(out))
+        return out
+
+    def rate_dematch(self, impl, bg, Z, rv, qm, Nref, nof_filler, new_data, llr, buf):
+        llr = np.ascontiguousarray(llr, dtype=np.int8)
+        buf = np.array(buf, dtype=np.int8)
+        self.lib.ref_rate_dematch(impl, bg, Z, rv, qm, ctypes.c_uint(Nref), ctypes.c_uint(nof_filler), int(new_data),
+                                  _ptr(llr), ctypes.c_uint(llr.size), _ptr(buf))
+        return buf
+
+    def pdsch_encode(self, bg, rv, qm, nof_layers, Nref, nof_ch_symbols, tb):
+        tb = np.ascontiguousarray(tb, dtype=np.uint8)
+        cw = np.zeros(nof_ch_symbols * qm, np.uint8)
+        meta = np.zeros(4 * 200, np.uint32)
+        n = self.lib.ref_pdsch_encode(bg, rv, qm, nof_layers, ctypes.c_uint(Nref), ctypes.c_uint(nof_ch_symbols),
+                                      _ptr(tb), ctypes.c_uint(tb.size), _ptr(cw), _ptr(meta))
+        return cw, meta[: 4 * n].reshape(n, 4)
+
+
+def have_ref():
+    return os.path.exists(REF_SO)
+
+
+def encode_with_llrs(oracle, rng, bg, Z, crc_poly=CRC16, nof_filler=0, amp=10, noise=0.0, n_llr=None):
+    """Random message with a CRC at the end of its significant bits, LDPC-encoded and mapped to LLRs."""
+    K = BG_K[bg]
+    L = K * Z - nof_filler
+    clen = CRC_LEN[crc_poly]
+    msg = np.zeros(K * Z, np.uint8)
+    msg[: L - clen] = rng.integers(0, 2, L - clen)
+    crc = oracle.crc_bits(crc_poly, msg[: L - clen])
+    msg[L - clen: L] = [(crc >> (clen - 1 - i)) & 1 for i in range(clen)]
+    cb = oracle.ldpc_encode(bg, Z, msg)
+    llr = (1 - 2 * cb.astype(np.int32)) * amp
+    if noise > 0:
+        llr = llr + rng.normal(0, noise, llr.size)
+    llr = np.clip(np.round(llr), -120, 120).astype(np.int8)
+    # Filler bits are known zeros: +inf, as the rate dematcher marks them (ldpc_rate_dematcher_impl.cpp:172).
+    if nof_filler:
+        llr[(K - 2) * Z - nof_filler:(K - 2) * Z] = 127
+    if n_llr is not None:
+        llr = llr[:n_llr]
+    return msg, cb, llr

@@ -1,0 +1,154 @@
+"""Pins the CPU restatement (oracle/liboracle.so) bit-for-bit against the srsRAN reference built from its own sources
+(oracle/_ref/libsrsref.so). Skipped where the reference build is absent; tests/test_golden.py then pins the oracle
+against the committed fixtures that tools/gen_golden.py generated from the same reference build.
+"""
+import numpy as np
+import pytest
+
+from oracle_lib import (BG_K, BG_N_SHORT, CRC16, CRC24A, CRC24B, CRC_LEN, LIFTING_SIZES, Oracle, Reference,
+                        encode_with_llrs, have_ref)
+
+pytestmark = [pytest.mark.ref, pytest.mark.skipif(not have_ref(), reason="reference build oracle/_ref absent")]
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+@pytest.fixture(scope="module")
+def ref():
+    return Reference()
+
+
+def test_crc_all_polys(orc, ref):
+    rng = np.random.default_rng(1)
+    for poly in range(6):
+        for n in [0, 1, 7, 8, 24, 100, 1000, 8448]:
+            bits = rng.integers(0, 2, n).astype(np.uint8)
+            assert orc.crc_bits(poly, bits) == ref.crc_bits(poly, bits), (poly, n)
+        data = rng.integers(0, 256, 333).astype(np.uint8)
+        assert orc.crc_bytes(poly, data) == ref.crc_bytes(poly, data)
+
+
+@pytest.mark.parametrize("bg", [1, 2])
+def test_encoder_all_lifting_sizes(orc, ref, bg):
+    rng = np.random.default_rng(bg)
+    for Z in LIFTING_SIZES:
+        msg = rng.integers(0, 2, BG_K[bg] * Z).astype(np.uint8)
+        want = ref.ldpc_encode(bg, Z, msg, impl=0)
+        assert np.array_equal(orc.ldpc_encode(bg, Z, msg), want), Z
+        assert np.array_equal(ref.ldpc_encode(bg, Z, msg, impl=1), want), Z
+
+
+def _decode_cases():
+    cases = []
+    for bg in (1, 2):
+        for Z in (2, 3, 5, 7, 9, 11, 13, 15, 16, 36, 52, 64, 104, 208, 240, 288, 320, 352, 384):
+            cases.append((bg, Z))
+    return cases
+
+
+@pytest.mark.parametrize("bg,Z", _decode_cases())
+def test_decoder_matches_reference(orc, ref, bg, Z):
+    rng = np.random.default_rng(1000 * bg + Z)
+    K, N = BG_K[bg], BG_N_SHORT[bg]
+    impls = [(0, Reference.GENERIC), (1, Reference.AVX2)]
+    if ref.has_avx512():
+        impls.append((1, Reference.AVX512))
+    for trial in range(4):
+        noise = [0.0, 6.0, 9.0, 14.0][trial]
+        crc_poly = CRC16 if trial % 2 == 0 else CRC24B
+        nof_filler = 0 if trial < 2 else min(Z, (K - 2) * Z // 4)
+        if K * Z - nof_filler < CRC_LEN[crc_poly] + 8:
+            crc_poly = 5  # CRC6 for the tiniest codeblocks (the decoder's CRC is only used for early stopping)
+        # Codeblock lengths: the minimum admissible, a ragged rate-matched one and the full one (multiples of Z).
+        n_llr = [(K + 2) * Z, N * Z, (K + 7) * Z if bg == 1 else (K + 5) * Z, N * Z][trial]
+        _, _, llr = encode_with_llrs(orc, rng, bg, Z, crc_poly=crc_poly, nof_filler=nof_filler, amp=12,
+                                     noise=noise, n_llr=n_llr)
+        for use_crc in (True, False):
+            for mode, impl in impls:
+                kw = dict(nof_crc_bits=16 if CRC_LEN[crc_poly] < 24 else 24, nof_filler=nof_filler,
+                          crc_poly=crc_poly if use_crc else -1, max_iter=8, scaling=0.8)
+                r_ref, o_ref = ref.ldpc_decode(impl, bg, Z, llr, **kw)
+                r_orc, o_orc = orc.ldpc_decode(mode, bg, Z, llr, **kw)
+                assert r_orc == r_ref, (trial, use_crc, impl)
+                assert np.array_equal(o_orc, o_ref), (trial, use_crc, impl)
+
+
+def test_decoder_random_llrs_and_trimmed_input(orc, ref):
+    """Random +/-10 LLRs (the reference benchmark's input, tests/benchmarks/phy/upper/channel_coding/ldpc/
+    ldpc_decoder_benchmark.cpp:129) and inputs whose tail is zero (trimmed by decode)."""
+    rng = np.random.default_rng(7)
+    for bg, Z in ((1, 384), (2, 384), (1, 24), (2, 10)):
+        K, N = BG_K[bg], BG_N_SHORT[bg]
+        llr = ((rng.integers(0, 2, N * Z) * 20) - 10).astype(np.int8)
+        for mode, impl in ((0, 0), (1, 1)):
+            r1, o1 = ref.ldpc_decode(impl, bg, Z, llr, max_iter=6)
+            r2, o2 = orc.ldpc_decode(mode, bg, Z, llr, max_iter=6)
+            assert r1 == r2 and np.array_equal(o1, o2)
+        # Zero tail: only K*Z + 3Z significant LLRs.
+        llr2 = llr.copy()
+        llr2[(K + 3) * Z:] = 0
+        for mode, impl in ((0, 0), (1, 1)):
+            r1, o1 = ref.ldpc_decode(impl, bg, Z, llr2, max_iter=5, crc_poly=CRC16)
+            r2, o2 = orc.ldpc_decode(mode, bg, Z, llr2, max_iter=5, crc_poly=CRC16)
+            assert r1 == r2 and np.array_equal(o1, o2)
+        # Too few significant LLRs: decode refuses (output all ones without CRC).
+        llr3 = llr.copy()
+        llr3[K * Z - 5:] = 0
+        r1, o1 = ref.ldpc_decode(1, bg, Z, llr3)
+        r2, o2 = orc.ldpc_decode(1, bg, Z, llr3)
+        assert r1 == r2 == -1 and np.array_equal(o1, o2) and o1.all()
+
+
+def test_decoder_scaling_factors(orc, ref):
+    rng = np.random.default_rng(11)
+    for sf in (0.5, 0.625, 0.75, 0.9, 0.99995):
+        _, _, llr = encode_with_llrs(orc, rng, 1, 96, noise=8.0, amp=12)
+        for mode, impl in ((0, 0), (1, 1)):
+            r1, o1 = ref.ldpc_decode(impl, 1, 96, llr, crc_poly=CRC16, max_iter=10, scaling=sf)
+            r2, o2 = orc.ldpc_decode(mode, 1, 96, llr, crc_poly=CRC16, max_iter=10, scaling=sf)
+            assert r1 == r2 and np.array_equal(o1, o2), sf
+
+
+def _rm_cases():
+    rng = np.random.default_rng(3)
+    cases = []
+    for bg in (1, 2):
+        for Z in (2, 13, 64, 208, 384):
+            for rv in range(4):
+                qm = [1, 2, 4, 6, 8][int(rng.integers(0, 5))]
+                N = BG_N_SHORT[bg] * Z
+                nsys = (BG_K[bg] - 2) * Z
+                nof_filler = int(rng.integers(0, max(1, nsys // 3)))
+                Nref = [0, int(N * 0.7)][int(rng.integers(0, 2))]
+                E = qm * int(rng.integers(max(1, (BG_K[bg] * Z) // qm // 2), 3 * N // qm))
+                cases.append((bg, Z, rv, qm, Nref, nof_filler, E))
+    return cases
+
+
+@pytest.mark.parametrize("case", _rm_cases())
+def test_rate_match(orc, ref, case):
+    bg, Z, rv, qm, Nref, nof_filler, E = case
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    K = BG_K[bg]
+    msg = rng.integers(0, 2, K * Z).astype(np.uint8)
+    msg[K * Z - nof_filler:] = 0  # filler bits are zeros in the encoder input (ldpc_segmenter_tx_impl.cpp:216)
+    want = ref.rate_match(bg, Z, rv, qm, Nref, nof_filler, msg, E)
+    cb = orc.ldpc_encode(bg, Z, msg)
+    assert np.array_equal(orc.rate_match(bg, Z, rv, qm, Nref, nof_filler, cb, E), want)
+
+
+@pytest.mark.parametrize("case", _rm_cases())
+def test_rate_dematch(orc, ref, case):
+    bg, Z, rv, qm, Nref, nof_filler, E = case
+    rng = np.random.default_rng((hash(case) + 5) & 0xFFFF)
+    N = BG_N_SHORT[bg] * Z
+    llr = rng.integers(-120, 121, E).astype(np.int8)
+    init = rng.integers(-120, 121, N).astype(np.int8)
+    for new_data in (1, 0):
+        for mode, impl in ((0, 0), (1, 1)):
+            want = ref.rate_dematch(impl, bg, Z, rv, qm, Nref, nof_filler, new_data, llr, init)
+            got = orc.rate_dematch(mode, bg, Z, rv, qm, Nref, nof_filler, new_data, llr, init)
+            assert np.array_equal(got, want), (new_data, mode)

@@ -1,0 +1,111 @@
+/*
+ * srsgpu_phy.h — C ABI of the MI355X (gfx950) 5G NR PHY acceleration library (libsrsgpu_phy.so).
+ *
+ * Drop-in boundary for the srsRAN upper-PHY channel-coding hot path. Every entry point names the reference interface
+ * it replaces (paths relative to the srsRAN tree, include/ or lib/). Plain C: pointers, sizes, POD structs; no C++ or
+ * torch types. Device pointers are HIP device (HBM) addresses; `stream` is a hipStream_t (NULL = default stream).
+ *
+ * Error convention: functions return SRSGPU_OK (0) or a negative SRSGPU_ERR_* code; srsgpu_last_error() returns a
+ * thread-local description of the last failure. Invalid configurations are rejected with the same conditions the
+ * reference asserts on (e.g. ldpc_decoder_impl.cpp:48-:56, :73-:88).
+ */
+#ifndef SRSGPU_PHY_H
+#define SRSGPU_PHY_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRSGPU_OK 0
+#define SRSGPU_ERR_INVALID_ARG (-1)
+#define SRSGPU_ERR_HIP (-2)
+#define SRSGPU_ERR_NO_MEMORY (-3)
+
+/* CRC generator polynomials, same numbering as srsran::crc_generator_poly
+ * (include/srsran/phy/upper/channel_coding/crc_calculator.h:33). */
+#define SRSGPU_CRC24A 0
+#define SRSGPU_CRC24B 1
+#define SRSGPU_CRC24C 2
+#define SRSGPU_CRC16 3
+#define SRSGPU_CRC11 4
+#define SRSGPU_CRC6 5
+#define SRSGPU_CRC_NONE 255 /* no CRC early stop: the decoder runs max_iterations (crc == nullptr) */
+
+/* LDPC decoder arithmetic variants of the reference (lib/phy/upper/channel_coding/channel_coding_factories.cpp,
+ * create_ldpc_decoder_factory_sw): "generic" rounds the normalised min-sum magnitudes (ldpc_decoder_generic.cpp:70);
+ * "avx2"/"avx512"/"neon" truncate a 16-bit fixed-point product (avx2_support.h:71). Results are bit-exact with the
+ * selected variant. */
+#define SRSGPU_LDPC_IMPL_GENERIC 0
+#define SRSGPU_LDPC_IMPL_SIMD 1
+
+typedef struct srsgpu_context srsgpu_context;
+
+/** Library version (major * 10000 + minor * 100 + patch). */
+int srsgpu_version(void);
+
+/** Thread-local description of the last error. */
+const char* srsgpu_last_error(void);
+
+/** Creates a context on HIP device `device` (one process per GPU). Uploads the lifted base-graph tables. */
+int srsgpu_context_create(int device, srsgpu_context** ctx);
+
+/** Destroys a context and frees its device memory. */
+void srsgpu_context_destroy(srsgpu_context* ctx);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * LDPC decoder — replaces srsran::ldpc_decoder::decode(bit_buffer& output, span<const log_likelihood_ratio> input,
+ * crc_calculator* crc, const configuration& cfg)   (include/srsran/phy/upper/channel_coding/ldpc/ldpc_decoder.h:72,
+ * lib/phy/upper/channel_coding/ldpc/ldpc_decoder_impl.cpp:60), batched over codeblocks.
+ * ------------------------------------------------------------------------------------------------------------------ */
+typedef struct {
+  uint8_t  base_graph;      /* 1 or 2 (codeblock_metadata::tb_common.base_graph) */
+  uint8_t  crc_poly;        /* SRSGPU_CRC* used for early stopping, or SRSGPU_CRC_NONE (crc == nullptr) */
+  uint16_t lifting_size;    /* Z (tb_common.lifting_size) */
+  uint16_t nof_filler_bits; /* cb_specific.nof_filler_bits */
+  uint8_t  nof_crc_bits;    /* cb_specific.nof_crc_bits: 16 or 24 */
+  uint8_t  max_iterations;  /* algorithm_conf.max_iterations (> 0) */
+  float    scaling_factor;  /* algorithm_conf.scaling_factor, in (0, 1) */
+  uint32_t llr_offset;      /* index of the codeblock's first LLR in the batch LLR buffer */
+  uint32_t nof_llrs;        /* input.size(): (K + 2) * Z <= nof_llrs <= N_short * Z */
+  uint32_t out_offset;      /* byte offset of the codeblock's K*Z output bits, packed MSB first (bit_buffer) */
+} srsgpu_ldpc_decoder_config;
+
+/** Pre-validated, device-resident batch of decoder work (reusable across calls and capturable in a hipGraph). */
+typedef struct srsgpu_ldpc_decoder_plan srsgpu_ldpc_decoder_plan;
+
+/** Validates `nof_cbs` configurations, builds the CRC early-stop tables they need and uploads the work descriptors.
+ *  Blocking (host <-> device copies); call it outside the timed / captured region. */
+int srsgpu_ldpc_decoder_plan_create(srsgpu_context*                   ctx,
+                                    int                               impl,
+                                    const srsgpu_ldpc_decoder_config* cfgs,
+                                    uint32_t                          nof_cbs,
+                                    srsgpu_ldpc_decoder_plan**        plan);
+
+/** Decodes the planned codeblocks: reads int8 LLRs from d_llrs, writes packed bits to d_out and, per codeblock, the
+ *  number of iterations on CRC success or -1 (std::nullopt) to d_nof_iterations[i]. Asynchronous on `stream`; no host
+ *  synchronisation, no allocation (hipGraph-capturable). */
+int srsgpu_ldpc_decoder_plan_execute(const srsgpu_ldpc_decoder_plan* plan,
+                                     const int8_t*                   d_llrs,
+                                     uint8_t*                        d_out,
+                                     int32_t*                        d_nof_iterations,
+                                     void*                           stream);
+
+void srsgpu_ldpc_decoder_plan_destroy(srsgpu_ldpc_decoder_plan* plan);
+
+/** One-shot convenience: plan_create + plan_execute + stream synchronisation + plan_destroy. */
+int srsgpu_ldpc_decode(srsgpu_context*                   ctx,
+                       int                               impl,
+                       const srsgpu_ldpc_decoder_config* cfgs,
+                       uint32_t                          nof_cbs,
+                       const int8_t*                     d_llrs,
+                       uint8_t*                          d_out,
+                       int32_t*                          d_nof_iterations,
+                       void*                             stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SRSGPU_PHY_H */

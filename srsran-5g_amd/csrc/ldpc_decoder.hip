@@ -1,0 +1,369 @@
+// Batched LDPC decoder for 5G NR (TS 38.212 BG1/BG2), layered normalised min-sum on 8-bit LLRs, for gfx950.
+//
+// Drop-in semantics of srsran::ldpc_decoder::decode (reference lib/phy/upper/channel_coding/ldpc/
+// ldpc_decoder_impl.cpp:60): same trimming of the input, same soft-bit clamp (:152), same layer schedule, same
+// check-node arithmetic (ldpc_decoder_avx2.cpp:69/:111/:165/:205, or ldpc_decoder_generic.cpp for MODE 0), same CRC
+// early stop after every full iteration (:133) and the same hard-decision output. Results are bit-exact with the
+// reference on identical inputs (tests/test_ldpc_decoder_gpu.py).
+//
+// Mapping to CDNA4:
+//  * one workgroup decodes one codeblock; lane z (0 <= z < Z) owns lifted check row z of every layer, so a layer is
+//    Z independent check-node updates (a circulant permutation guarantees no two lanes touch the same soft bit);
+//  * the soft bits of the whole codeblock live in LDS (68 x 384 B for BG1); column c of the lifted graph sits at
+//    c * 384, so every column offset is a ds_read/ds_write immediate;
+//  * the check-to-variable messages never leave the VGPRs: per layer a lane keeps the scaled minimum, second minimum,
+//    argmin and one sign bit per edge (one 32-bit word, two for the 19-edge core rows of BG1) - the messages are
+//    rebuilt from them exactly;
+//  * the base-graph structure (edges per layer, columns) is unrolled at compile time; only the lifting shifts are
+//    read at run time (wave-uniform loads).
+#include "common.h"
+#include "ldpc_base_graphs.h"
+#include "srsgpu_internal.h"
+
+namespace srsgpu {
+namespace {
+
+template <int BG>
+struct bg_t;
+
+template <>
+struct bg_t<1> {
+  static constexpr int M  = kBG1_M;
+  static constexpr int NF = kBG1_N_FULL;
+  static constexpr int K  = kBG1_K;
+  static constexpr int NE = kBG1_NUM_EDGES;
+  static constexpr int rs(int m) { return kBG1_ROW_START[m]; }
+  static constexpr int col(int e) { return kBG1_COL[e]; }
+};
+
+template <>
+struct bg_t<2> {
+  static constexpr int M  = kBG2_M;
+  static constexpr int NF = kBG2_N_FULL;
+  static constexpr int K  = kBG2_K;
+  static constexpr int NE = kBG2_NUM_EDGES;
+  static constexpr int rs(int m) { return kBG2_ROW_START[m]; }
+  static constexpr int col(int e) { return kBG2_COL[e]; }
+};
+
+#ifndef LDPC_DEC_MIN_WAVES
+#define LDPC_DEC_MIN_WAVES 4
+#endif
+
+constexpr int LLR_MAX = 120;
+constexpr int LLR_INF = 127;
+/// Sign bits of the first SIGNS_LO edges of a layer share the state word with min1 (7 b), min2 (7 b), argmin (5 b).
+constexpr int SIGNS_LO = 13;
+/// Bytes of LDS reduction scratch between the soft-bit image and the shift table.
+constexpr int SCRATCH_BYTES = 64 * sizeof(int);
+
+/// Normalisation of a check-node magnitude (0..120). MODE 1: avx2_support.h:71 scale_epi8 (16-bit fixed point,
+/// truncating); MODE 0: ldpc_decoder_generic.cpp:70 scale_llr (float, round half away from zero).
+template <int MODE>
+__device__ __forceinline__ int scale_mag(int m, uint32_t sf16, float sf)
+{
+  if constexpr (MODE == 1) {
+    return static_cast<int>((static_cast<uint32_t>(m) * sf16) >> 16);
+  } else {
+    return static_cast<int>(roundf(static_cast<float>(m) * sf));
+  }
+}
+
+/// One lifted check row of layer m: variable-to-check messages, min-sum analysis, check-to-variable messages and the
+/// soft-bit update (ldpc_decoder_impl.cpp:195, :255, :240).
+template <int BG, int MODE, int m>
+__device__ __forceinline__ void row_update(int8_t* __restrict__ soft,
+                                           const uint16_t* __restrict__ sh,  // lifting shifts, in LDS
+                                           int       z,
+                                           int       Z,
+                                           uint32_t  sf16,
+                                           float     sf,
+                                           uint32_t& st,
+                                           uint32_t& st_hi)
+{
+  using G              = bg_t<BG>;
+  constexpr int e0     = G::rs(m);
+  constexpr int deg    = G::rs(m + 1) - e0;
+  const int     om1    = static_cast<int>(st & 127u);
+  const int     om2    = static_cast<int>((st >> 7) & 127u);
+  const int     oidx   = static_cast<int>((st >> 14) & 31u);
+  int           v2c[deg];
+  int           min1 = LLR_MAX, min2 = LLR_MAX, idx = 0;
+  uint32_t      sp   = 0;
+  // Sign bits of edges >= SIGNS_LO of the (at most four) high-degree core rows share one word, 6 bits per row.
+  constexpr int HI_SHIFT = 6 * (m & 3);
+
+  static_for<deg>([&](auto E) {
+    constexpr int e   = decltype(E)::value;
+    constexpr int col = G::col(e0 + e);
+    // Rotated position (z + s) mod Z with one unsigned min: z + s - Z wraps above z + s when z + s < Z.
+    const uint32_t p0 = static_cast<uint32_t>(z) + sh[e0 + e];
+    const uint32_t p1 = p0 - static_cast<uint32_t>(Z);
+    const int      p  = static_cast<int>(p0 < p1 ? p0 : p1);
+    const int sb      = soft[col * SOFT_COL_STRIDE + p];
+    // Previous check-to-variable message of this edge, rebuilt from the compressed state.
+    uint32_t sgn;
+    if constexpr (e < SIGNS_LO) {
+      sgn = (st >> (19 + e)) & 1u;
+    } else {
+      sgn = (st_hi >> (HI_SHIFT + e - SIGNS_LO)) & 1u;
+    }
+    const int om = (oidx == e) ? om2 : om1;
+    const int c  = sgn ? -om : om;
+    // v2c = soft - c2v saturated to +/-LLR_MAX; infinite soft bits stay infinite (ldpc_decoder_avx2.cpp:69).
+    int v  = clamp_i(sb - c, -LLR_MAX, LLR_MAX);
+    v      = (sb == LLR_INF || sb == -LLR_INF) ? sb : v;
+    v2c[e] = v;
+    // Two smallest magnitudes, argmin and sign parity (ldpc_decoder_avx2.cpp:111).
+    const int  a      = v < 0 ? -v : v;
+    const bool is_min = a < min1;
+    const int  nsec   = is_min ? min1 : a;
+    min2              = (a < min2) ? nsec : min2;
+    min1              = is_min ? a : min1;
+    idx               = is_min ? e : idx;
+    sp ^= static_cast<uint32_t>(v < 0);
+  });
+
+  const int s1  = scale_mag<MODE>(min1, sf16, sf);
+  const int s2  = scale_mag<MODE>(min2, sf16, sf);
+  uint32_t  nst = static_cast<uint32_t>(s1) | (static_cast<uint32_t>(s2) << 7) | (static_cast<uint32_t>(idx) << 14);
+  uint32_t  nhi = 0;
+
+  static_for<deg>([&](auto E) {
+    constexpr int  e   = decltype(E)::value;
+    constexpr int  col = G::col(e0 + e);
+    const int      v   = v2c[e];
+    const uint32_t neg = sp ^ static_cast<uint32_t>(v < 0);
+    const int      mag = (idx == e) ? s2 : s1;
+    const int      c   = neg ? -mag : mag;
+    // Promotion sum (log_likelihood_ratio.cpp:75, ldpc_decoder_avx2.cpp:205): |sum| > LLR_MAX becomes +/-infinity.
+    const int t  = c + v;
+    int       sb = t > LLR_MAX ? LLR_INF : (t < -LLR_MAX ? -LLR_INF : t);
+    sb           = (v == LLR_INF || v == -LLR_INF) ? v : sb;
+    const uint32_t p0 = static_cast<uint32_t>(z) + sh[e0 + e];
+    const uint32_t p1 = p0 - static_cast<uint32_t>(Z);
+    soft[col * SOFT_COL_STRIDE + static_cast<int>(p0 < p1 ? p0 : p1)] = static_cast<int8_t>(sb);
+    if constexpr (e < SIGNS_LO) {
+      nst |= neg << (19 + e);
+    } else {
+      nhi |= neg << (HI_SHIFT + e - SIGNS_LO);
+    }
+  });
+  st = nst;
+  if constexpr (deg > SIGNS_LO) {
+    static_assert(m < 4 && deg - SIGNS_LO <= 6, "only the core rows may exceed SIGNS_LO edges");
+    st_hi = (st_hi & ~(0x3fu << HI_SHIFT)) | nhi;
+  }
+}
+
+/// Hard decisions of the K*Z systematic bits, packed MSB first (log_likelihood_ratio.cpp:350 hard_decision).
+__device__ __forceinline__ void write_hard_bits(const int8_t* __restrict__ soft,
+                                                uint8_t* __restrict__ out,
+                                                int      nbits,
+                                                int      Z,
+                                                uint32_t magic)
+{
+  const int nbytes = (nbits + 7) / 8;
+  for (int b = threadIdx.x; b < nbytes; b += blockDim.x) {
+    uint32_t byte = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = 8 * b + k;
+      if (i < nbits) {
+        const int col = static_cast<int>(__umulhi(static_cast<uint32_t>(i), magic));
+        const int l   = i - col * Z;
+        byte |= static_cast<uint32_t>(soft[col * SOFT_COL_STRIDE + l] <= 0) << (7 - k);
+      }
+    }
+    out[b] = static_cast<uint8_t>(byte);
+  }
+}
+
+template <int BG, int MODE>
+__global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(const dec_desc* __restrict__ descs,
+                                                          const int8_t* __restrict__ llrs,
+                                                          uint8_t* __restrict__ out,
+                                                          int32_t* __restrict__ results,
+                                                          const uint16_t* __restrict__ shift_table,
+                                                          const uint32_t* __restrict__ crc_tables)
+{
+  using G = bg_t<BG>;
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  int8_t*   soft    = smem;
+  int*      scratch = reinterpret_cast<int*>(smem + G::NF * SOFT_COL_STRIDE);
+  uint16_t* sh      = reinterpret_cast<uint16_t*>(smem + G::NF * SOFT_COL_STRIDE + SCRATCH_BYTES);
+
+  const dec_desc d      = descs[blockIdx.x];
+  const int      Z      = d.Z;
+  const int      z      = threadIdx.x;
+  const bool     active = z < Z;
+  const int      wave   = threadIdx.x / WAVE;
+  const int      nwaves = blockDim.x / WAVE;
+  const int      lane   = threadIdx.x % WAVE;
+
+  // ---- Load the LLRs into the soft-bit image (ldpc_decoder_impl.cpp:152) and find the last non-zero LLR (:94). ----
+  const int8_t* llr   = llrs + d.llr_offset;
+  const int     n_llr = static_cast<int>(d.nof_llr);
+  const int     full  = static_cast<int>(__umulhi(static_cast<uint32_t>(n_llr), d.div_magic)) * Z;
+  int           last  = -1;
+  if (active) {
+    soft[0 * SOFT_COL_STRIDE + z] = 0;
+    soft[1 * SOFT_COL_STRIDE + z] = 0;
+    for (int c = 2; c < G::NF; ++c) {
+      const int i = (c - 2) * Z + z;
+      int       v = (i < n_llr) ? static_cast<int>(llr[i]) : 0;
+      last        = (v != 0) ? i : last;
+      v           = (i < full) ? clamp_i(v, -64, 64) : v;
+      soft[c * SOFT_COL_STRIDE + z] = static_cast<int8_t>(v);
+    }
+  }
+  // Lifting shifts of this Z into LDS (read back as wave-uniform broadcasts inside the layer loop).
+  {
+    const uint16_t* gsh = shift_table + static_cast<uint32_t>(d.zpos) * G::NE;
+    for (int e = threadIdx.x; e < G::NE; e += blockDim.x) {
+      sh[e] = gsh[e];
+    }
+  }
+  last = wave_max(last);
+  if (lane == 0) {
+    scratch[wave] = last;
+  }
+  __syncthreads();
+  int input_size = scratch[0];
+  for (int w = 1; w < nwaves; ++w) {
+    input_size = scratch[w] > input_size ? scratch[w] : input_size;
+  }
+  input_size += 1;
+
+  const int  msg_len = G::K * Z;
+  uint8_t*   cb_out  = out + d.out_offset;
+  const bool use_crc = d.crc_table != NO_CRC_TABLE;
+  if (input_size < msg_len) {
+    // Not enough LLRs: no decoding; without CRC the output is all ones (ldpc_decoder_impl.cpp:100).
+    if (!use_crc) {
+      for (int b = threadIdx.x; b < (msg_len + 7) / 8; b += blockDim.x) {
+        cb_out[b] = 0xff;
+      }
+    }
+    if (threadIdx.x == 0) {
+      results[d.cb_index] = -1;
+    }
+    return;
+  }
+  int cb_len = input_size + 2 * Z;
+  cb_len     = cb_len > msg_len + 4 * Z ? cb_len : msg_len + 4 * Z;
+  const int nof_layers =
+      __builtin_amdgcn_readfirstlane(static_cast<int>(__umulhi(static_cast<uint32_t>(cb_len + Z - 1), d.div_magic)) -
+                                     G::K);
+
+  const uint32_t* crc_table = crc_tables + (use_crc ? d.crc_table : 0u);
+  const int       nsig      = d.nof_significant;
+  const uint32_t  sf16      = d.sf16;
+  const float     sf        = d.sf;
+
+  uint32_t st[G::M];
+  uint32_t st_hi = 0;
+#pragma unroll
+  for (int m = 0; m < G::M; ++m) {
+    st[m] = 0;
+  }
+  __syncthreads();
+
+  const int max_iter = d.max_iter;
+  for (int it = 0; it < max_iter; ++it) {
+    // Opaque per-iteration copies: stop the compiler from hoisting per-layer predicates and per-column addresses out
+    // of the iteration loop (they would pin ~70 registers for values that cost one instruction to recompute).
+    int nl = nof_layers, zz = z, ZZ = Z;
+    asm volatile("" : "+s"(nl));
+    asm volatile("" : "+v"(zz));
+    asm volatile("" : "+s"(ZZ));
+    static_for<G::M>([&](auto Mi) {
+      constexpr int m = decltype(Mi)::value;
+      if (m < nl) {
+        if (active) {
+          row_update<BG, MODE, m>(soft, sh, zz, ZZ, sf16, sf, st[m], st_hi);
+        }
+        __syncthreads();
+      }
+    });
+
+    if (use_crc) {
+      // Early stop (ldpc_decoder_impl.cpp:133): every systematic soft bit non-zero and CRC remainder zero. The CRC of
+      // the hard decisions is the XOR of per-bit contributions x^(order + L - 1 - i) mod g(x) (crc_table).
+      uint32_t acc  = 0;
+      uint32_t zero = 0;
+      if (active) {
+        int i = zz;
+        static_for<G::K>([&](auto Ci) {
+          constexpr int c  = decltype(Ci)::value;
+          const int     sb = soft[c * SOFT_COL_STRIDE + zz];
+          zero |= static_cast<uint32_t>(sb == 0);
+          acc ^= (sb <= 0 && i < nsig) ? crc_table[i] : 0u;
+          i += ZZ;
+        });
+      }
+      acc  = wave_xor(acc);
+      zero = (__ballot(zero != 0) != 0) ? 1u : 0u;
+      int* red = scratch + 8 + 16 * (it & 1);
+      if (lane == 0) {
+        red[2 * wave]     = static_cast<int>(acc);
+        red[2 * wave + 1] = static_cast<int>(zero);
+      }
+      __syncthreads();
+      uint32_t tacc = 0, tzero = 0;
+      for (int w = 0; w < nwaves; ++w) {
+        tacc ^= static_cast<uint32_t>(red[2 * w]);
+        tzero |= static_cast<uint32_t>(red[2 * w + 1]);
+      }
+      if (tzero == 0 && tacc == 0) {
+        write_hard_bits(soft, cb_out, msg_len, Z, d.div_magic);
+        if (threadIdx.x == 0) {
+          results[d.cb_index] = it + 1;
+        }
+        return;
+      }
+    }
+  }
+  write_hard_bits(soft, cb_out, msg_len, Z, d.div_magic);
+  if (threadIdx.x == 0) {
+    results[d.cb_index] = -1;
+  }
+}
+
+} // namespace
+
+void launch_ldpc_decode(int             bg,
+                        int             mode,
+                        const dec_desc* d_desc,
+                        int             nof_cbs,
+                        int             block_threads,
+                        const int8_t*   d_llrs,
+                        uint8_t*        d_out,
+                        int32_t*        d_results,
+                        const uint16_t* d_shifts,
+                        const uint32_t* d_crc_tables,
+                        hipStream_t     stream)
+{
+  if (nof_cbs <= 0) {
+    return;
+  }
+  const int    nf  = (bg == 1) ? bg_t<1>::NF : bg_t<2>::NF;
+  const int    ne  = (bg == 1) ? bg_t<1>::NE : bg_t<2>::NE;
+  const size_t lds = static_cast<size_t>(nf) * SOFT_COL_STRIDE + SCRATCH_BYTES + ne * sizeof(uint16_t);
+  dim3         grid(nof_cbs), block(block_threads);
+  if (bg == 1) {
+    if (mode == 1) {
+      ldpc_decode_kernel<1, 1><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables);
+    } else {
+      ldpc_decode_kernel<1, 0><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables);
+    }
+  } else {
+    if (mode == 1) {
+      ldpc_decode_kernel<2, 1><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables);
+    } else {
+      ldpc_decode_kernel<2, 0><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables);
+    }
+  }
+}
+
+} // namespace srsgpu

@@ -1,0 +1,252 @@
+"""srsgpu — Python host binding of libsrsgpu_phy.so (the MI355X 5G NR PHY kernels), over its C ABI
+(include/srsgpu_phy.h).
+
+The Python side mirrors the srsRAN interfaces it replaces (names, argument meaning and error behaviour) so the parity
+tests read like the reference's own tests:
+
+  * ``LdpcDecoder.decode(llrs, cfg)``  <->  srsran::ldpc_decoder::decode()
+    (include/srsran/phy/upper/channel_coding/ldpc/ldpc_decoder.h:72)
+
+Device memory and streams come from PyTorch (ROCm); PyTorch is plumbing only — every codeblock is processed by the
+HIP kernels in libsrsgpu_phy.so. There is no CPU fallback: if the library or a HIP device is missing, the calls raise.
+"""
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+try:  # Import torch first: it loads its own libamdhip64.so.7, which our library then shares (one HIP runtime).
+    import torch
+except ImportError:  # pragma: no cover - torch is part of the image
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libsrsgpu_phy.so")
+
+SRSGPU_OK = 0
+CRC24A, CRC24B, CRC24C, CRC16, CRC11, CRC6 = range(6)
+CRC_NONE = 255
+IMPL_GENERIC, IMPL_SIMD = 0, 1
+IMPL_BY_NAME = {"generic": IMPL_GENERIC, "avx2": IMPL_SIMD, "avx512": IMPL_SIMD, "neon": IMPL_SIMD,
+                "auto": IMPL_SIMD, "simd": IMPL_SIMD}
+BG_K = {1: 22, 2: 10}
+BG_N_SHORT = {1: 66, 2: 50}
+
+
+class SrsGpuError(RuntimeError):
+    pass
+
+
+class LdpcDecoderConfig(ctypes.Structure):
+    """srsgpu_ldpc_decoder_config (include/srsgpu_phy.h)."""
+    _fields_ = [
+        ("base_graph", ctypes.c_uint8),
+        ("crc_poly", ctypes.c_uint8),
+        ("lifting_size", ctypes.c_uint16),
+        ("nof_filler_bits", ctypes.c_uint16),
+        ("nof_crc_bits", ctypes.c_uint8),
+        ("max_iterations", ctypes.c_uint8),
+        ("scaling_factor", ctypes.c_float),
+        ("llr_offset", ctypes.c_uint32),
+        ("nof_llrs", ctypes.c_uint32),
+        ("out_offset", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(LdpcDecoderConfig) == 24
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Loads libsrsgpu_phy.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SrsGpuError(f"{path} not built: run srsran-5g_amd/build.sh (or __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    lib.srsgpu_version.restype = ctypes.c_int
+    lib.srsgpu_last_error.restype = ctypes.c_char_p
+    lib.srsgpu_context_create.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
+    lib.srsgpu_context_destroy.argtypes = [P]
+    lib.srsgpu_context_destroy.restype = None
+    lib.srsgpu_ldpc_decoder_plan_create.argtypes = [P, ctypes.c_int, P, ctypes.c_uint32, ctypes.POINTER(P)]
+    lib.srsgpu_ldpc_decoder_plan_execute.argtypes = [P, P, P, P, P]
+    lib.srsgpu_ldpc_decoder_plan_destroy.argtypes = [P]
+    lib.srsgpu_ldpc_decoder_plan_destroy.restype = None
+    lib.srsgpu_ldpc_decode.argtypes = [P, ctypes.c_int, P, ctypes.c_uint32, P, P, P, P]
+    _lib = lib
+    return lib
+
+
+# Every symbol include/srsgpu_phy.h declares (checked by tests/test_capi_symbols.py).
+EXPORTED_SYMBOLS = [
+    "srsgpu_version", "srsgpu_last_error", "srsgpu_context_create", "srsgpu_context_destroy",
+    "srsgpu_ldpc_decoder_plan_create", "srsgpu_ldpc_decoder_plan_execute", "srsgpu_ldpc_decoder_plan_destroy",
+    "srsgpu_ldpc_decode",
+]
+
+
+def _check(rc: int):
+    if rc != SRSGPU_OK:
+        raise SrsGpuError(f"srsgpu error {rc}: {_lib.srsgpu_last_error().decode()}")
+
+
+def _stream_handle(stream) -> Optional[int]:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream if torch is not None else None
+    if hasattr(stream, "cuda_stream"):
+        return stream.cuda_stream
+    return int(stream)
+
+
+def _dptr(t) -> int:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise SrsGpuError("expected a device (HIP) tensor")
+    if not t.is_contiguous():
+        raise SrsGpuError("expected a contiguous tensor")
+    return t.data_ptr()
+
+
+class Context:
+    """srsgpu_context: one per GPU (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        lib = load_library()
+        if torch is None or not torch.cuda.is_available():
+            raise SrsGpuError("no HIP device available (the srsgpu kernels need an MI355X)")
+        self.device = device
+        h = ctypes.c_void_p()
+        _check(lib.srsgpu_context_create(device, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.srsgpu_context_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+@dataclass
+class CodeblockDecodeConfig:
+    """Mirror of srsran::ldpc_decoder::configuration (ldpc_decoder.h:44) for one codeblock."""
+    base_graph: int
+    lifting_size: int
+    nof_crc_bits: int = 16
+    nof_filler_bits: int = 0
+    max_iterations: int = 6
+    scaling_factor: float = 0.8
+
+
+def make_configs(cfgs: Sequence[CodeblockDecodeConfig], nof_llrs: Sequence[int], crc_polys: Sequence[int],
+                 llr_offsets: Optional[Sequence[int]] = None, out_offsets: Optional[Sequence[int]] = None):
+    """Packs per-codeblock configurations into the C array, with default contiguous offsets."""
+    n = len(cfgs)
+    arr = (LdpcDecoderConfig * n)()
+    llr_off = 0
+    out_off = 0
+    for i, c in enumerate(cfgs):
+        a = arr[i]
+        a.base_graph = c.base_graph
+        a.crc_poly = crc_polys[i]
+        a.lifting_size = c.lifting_size
+        a.nof_filler_bits = c.nof_filler_bits
+        a.nof_crc_bits = c.nof_crc_bits
+        a.max_iterations = c.max_iterations
+        a.scaling_factor = c.scaling_factor
+        a.nof_llrs = nof_llrs[i]
+        a.llr_offset = llr_offsets[i] if llr_offsets is not None else llr_off
+        a.out_offset = out_offsets[i] if out_offsets is not None else out_off
+        llr_off += nof_llrs[i]
+        out_off += (BG_K[c.base_graph] * c.lifting_size + 7) // 8
+    return arr
+
+
+class LdpcDecoderPlan:
+    """srsgpu_ldpc_decoder_plan: validated, device-resident batch of decoder work (hipGraph-capturable execute)."""
+
+    def __init__(self, ctx: Context, impl: int, cfg_array):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        _check(_lib.srsgpu_ldpc_decoder_plan_create(ctx.handle, impl, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                    len(cfg_array), ctypes.byref(h)))
+        self.handle = h
+        self.nof_cbs = len(cfg_array)
+
+    def execute(self, d_llrs, d_out, d_iters, stream=None):
+        _check(_lib.srsgpu_ldpc_decoder_plan_execute(self.handle, _dptr(d_llrs), _dptr(d_out), _dptr(d_iters),
+                                                     _stream_handle(stream)))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.srsgpu_ldpc_decoder_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def unpack_bits(packed: np.ndarray, nbits: int) -> np.ndarray:
+    return np.unpackbits(np.asarray(packed, dtype=np.uint8))[:nbits]
+
+
+class LdpcDecoder:
+    """GPU implementation of srsran::ldpc_decoder (ldpc_decoder.h), created like
+    create_ldpc_decoder_factory_sw(type)->create() (channel_coding_factories.h): type "generic" or "avx2"/"avx512"/
+    "neon"/"auto" selects the arithmetic variant the results are bit-exact with."""
+
+    def __init__(self, ctx: Context, dec_type: str = "auto"):
+        if dec_type not in IMPL_BY_NAME:
+            raise SrsGpuError(f"invalid LDPC decoder type '{dec_type}'")
+        self.ctx = ctx
+        self.impl = IMPL_BY_NAME[dec_type]
+
+    def decode(self, llrs: np.ndarray, cfg: CodeblockDecodeConfig, crc_poly: Optional[int] = None,
+               output_init: Optional[np.ndarray] = None):
+        """Decodes one codeblock. Returns (nof_iterations or None, K*Z unpacked bits) like ldpc_decoder::decode."""
+        res = self.decode_batch([llrs], [cfg], [crc_poly], None if output_init is None else [output_init])
+        return res[0]
+
+    def decode_batch(self, llrs_list: List[np.ndarray], cfgs: List[CodeblockDecodeConfig],
+                     crc_polys: List[Optional[int]], output_inits=None):
+        n = len(cfgs)
+        nof_llrs = [int(np.asarray(x).size) for x in llrs_list]
+        polys = [CRC_NONE if p is None else p for p in crc_polys]
+        arr = make_configs(cfgs, nof_llrs, polys)
+        flat = np.concatenate([np.asarray(x, dtype=np.int8) for x in llrs_list]) if n else np.zeros(0, np.int8)
+        out_bytes = [(BG_K[c.base_graph] * c.lifting_size + 7) // 8 for c in cfgs]
+        dev = torch.device("cuda", self.ctx.device)
+        d_llrs = torch.from_numpy(flat).to(dev)
+        if output_inits is not None:
+            init = np.concatenate([np.packbits(np.asarray(o, dtype=np.uint8)) for o in output_inits])
+            d_out = torch.from_numpy(init).to(dev)
+        else:
+            d_out = torch.zeros(sum(out_bytes), dtype=torch.uint8, device=dev)
+        d_iters = torch.zeros(n, dtype=torch.int32, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        _check(_lib.srsgpu_ldpc_decode(self.ctx.handle, self.impl, ctypes.cast(arr, ctypes.c_void_p), n,
+                                       _dptr(d_llrs), _dptr(d_out), _dptr(d_iters), stream.cuda_stream))
+        out = d_out.cpu().numpy()
+        iters = d_iters.cpu().numpy()
+        results = []
+        off = 0
+        for i, c in enumerate(cfgs):
+            nb = BG_K[c.base_graph] * c.lifting_size
+            bits = unpack_bits(out[off: off + out_bytes[i]], nb)
+            off += out_bytes[i]
+            results.append((None if iters[i] < 0 else int(iters[i]), bits))
+        return results

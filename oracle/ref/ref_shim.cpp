@@ -268,3 +268,51 @@ int ref_pdsch_encode(int bg, int rv, int qm, int nof_layers, unsigned Nref, unsi
 }
 
 } // extern "C"
+
+#include <chrono>
+
+extern "C" {
+
+/// CPU baseline: decodes n codeblocks (LLRs at llr + i * stride, same configuration) with ONE reference decoder
+/// instance of the given implementation and returns the wall time of the decode() calls only, in nanoseconds.
+/// iters[i] receives the return value (iterations or -1).
+long long ref_ldpc_decode_timed(int           impl,
+                                int           bg,
+                                int           Z,
+                                int           nof_crc_bits,
+                                int           nof_filler_bits,
+                                int           crc_poly,
+                                int           max_iter,
+                                float         scaling,
+                                const int8_t* llr,
+                                unsigned      n_llr,
+                                unsigned      stride,
+                                unsigned      n,
+                                int*          iters)
+{
+  auto                            dec = make_decoder(impl);
+  unsigned                        K   = (bg == 2) ? 10 : 22;
+  dynamic_bit_buffer              msg(K * Z);
+  std::unique_ptr<crc_calculator> crc;
+  if (crc_poly >= 0) {
+    crc = std::make_unique<crc_calculator_generic_impl>(to_poly(crc_poly));
+  }
+  ldpc_decoder::configuration cfg;
+  cfg.block_conf.tb_common.base_graph        = to_bg(bg);
+  cfg.block_conf.tb_common.lifting_size      = static_cast<ldpc::lifting_size_t>(Z);
+  cfg.block_conf.cb_specific.nof_crc_bits    = nof_crc_bits;
+  cfg.block_conf.cb_specific.nof_filler_bits = nof_filler_bits;
+  cfg.algorithm_conf.max_iterations          = max_iter;
+  cfg.algorithm_conf.scaling_factor          = scaling;
+  auto t0                                    = std::chrono::steady_clock::now();
+  for (unsigned i = 0; i != n; ++i) {
+    span<const log_likelihood_ratio> in(reinterpret_cast<const log_likelihood_ratio*>(llr + static_cast<size_t>(i) * stride),
+                                        n_llr);
+    std::optional<unsigned> r = dec->decode(msg, in, crc.get(), cfg);
+    iters[i]                  = r.has_value() ? static_cast<int>(*r) : -1;
+  }
+  auto t1 = std::chrono::steady_clock::now();
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+}
+
+} // extern "C"

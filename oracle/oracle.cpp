@@ -557,8 +557,10 @@ int orc_rate_dematch(int mode, int bg, int Z, int rv, int qm, unsigned Nref, uns
       copy = false;
     }
   }
+  // :198 zeroes out.last(buffer_length - tmp_idx) of the FULL N-length output, i.e. [N - (Ncb - k), N): with limited
+  // buffer rate matching (Ncb < N) that is not [k, Ncb).
   if (copy && k != 0) {
-    for (unsigned i = k; i < Ncb; ++i) {
+    for (unsigned i = N - (Ncb - k); i < N; ++i) {
       buf[i] = 0;
     }
   }

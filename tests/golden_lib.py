@@ -1,0 +1,82 @@
+"""Iterators over the reference-generated fixtures in tests/golden/ (see tools/gen_golden.py)."""
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+BG_K = {1: 22, 2: 10}
+BG_N_SHORT = {1: 66, 2: 50}
+
+
+def _load(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def crc_cases():
+    d = _load("crc.npz")
+    off = 0
+    for poly, n, c in zip(d["poly"], d["lens"], d["crc"]):
+        yield int(poly), d["bits"][off:off + n], int(c)
+        off += n
+
+
+def encoder_cases():
+    d = _load("ldpc_encoder.npz")
+    mo = co = 0
+    for bg, Z in d["cfg"]:
+        K, N = BG_K[bg] * Z, BG_N_SHORT[bg] * Z
+        mb, cbb = (K + 7) // 8, (N + 7) // 8
+        yield int(bg), int(Z), np.unpackbits(d["msg"][mo:mo + mb])[:K], np.unpackbits(d["cb"][co:co + cbb])[:N]
+        mo += mb
+        co += cbb
+
+
+def decoder_cases():
+    """Yields dict(bg, Z, impl (0 generic / 1 avx2), crc_poly (-1 none), nof_crc_bits, filler, max_iter, llr,
+    iters (-1 = nullopt), bits)."""
+    d = _load("ldpc_decoder.npz")
+    lo = oo = 0
+    for i, (bg, Z, impl, poly, nbits, filler, max_iter, n_llr) in enumerate(d["cfg"]):
+        K = BG_K[bg] * Z
+        ob = (K + 7) // 8
+        yield dict(bg=int(bg), Z=int(Z), impl=int(impl), crc_poly=int(poly), nof_crc_bits=int(nbits),
+                   filler=int(filler), max_iter=int(max_iter), llr=d["llr"][lo:lo + n_llr], iters=int(d["iters"][i]),
+                   bits=np.unpackbits(d["out"][oo:oo + ob])[:K])
+        lo += n_llr
+        oo += ob
+
+
+def rate_matching_cases():
+    """Yields dict(bg, Z, rv, qm, Nref, filler, E, msg, rm_out, dm_llr, dm_init, dm_out[(new_data, impl)])."""
+    d = _load("rate_matching.npz")
+    mo = ro = lo = io = oo = 0
+    for bg, Z, rv, qm, Nref, filler, E in d["cfg"]:
+        K, N = BG_K[bg] * Z, BG_N_SHORT[bg] * Z
+        mb, rb = (K + 7) // 8, (E + 7) // 8
+        case = dict(bg=int(bg), Z=int(Z), rv=int(rv), qm=int(qm), Nref=int(Nref), filler=int(filler), E=int(E),
+                    msg=np.unpackbits(d["msg"][mo:mo + mb])[:K], rm_out=np.unpackbits(d["rm_out"][ro:ro + rb])[:E],
+                    dm_llr=d["dm_llr"][lo:lo + E], dm_init=d["dm_init"][io:io + N], dm_out={})
+        for new_data in (1, 0):
+            for impl in (0, 1):
+                case["dm_out"][(new_data, impl)] = d["dm_out"][oo:oo + N]
+                oo += N
+        mo += mb
+        ro += rb
+        lo += E
+        io += N
+        yield case
+
+
+def pdsch_encoder_cases():
+    """Yields dict(bg, rv, qm, nof_layers, Nref, nof_ch_symbols, tb, cw (unpacked bits), meta (C x 4))."""
+    d = _load("pdsch_encoder.npz")
+    to = co = mo = 0
+    for bg, rv, qm, layers, Nref, nsym, tb_bytes, ncb in d["cfg"]:
+        G = nsym * qm
+        cb = (G + 7) // 8
+        yield dict(bg=int(bg), rv=int(rv), qm=int(qm), nof_layers=int(layers), Nref=int(Nref),
+                   nof_ch_symbols=int(nsym), tb=d["tb"][to:to + tb_bytes], cw=np.unpackbits(d["cw"][co:co + cb])[:G],
+                   meta=d["meta"][mo:mo + ncb])
+        to += tb_bytes
+        co += cb
+        mo += ncb

@@ -127,3 +127,21 @@ def test_decoder_rejects_invalid_configs(ctx):
         dec.decode(np.ones(67 * 16, np.int8), srsgpu.CodeblockDecodeConfig(1, 16))  # too long
     with pytest.raises(srsgpu.SrsGpuError):
         dec.decode(np.ones(66 * 16, np.int8), srsgpu.CodeblockDecodeConfig(1, 16, scaling_factor=1.0))
+
+
+def test_decoder_golden_vectors(ctx):
+    """The GPU decoder against the reference's own outputs (tests/golden/ldpc_decoder.npz), every case in one batch
+    per arithmetic variant."""
+    import golden_lib as G
+    import srsgpu
+    cases = list(G.decoder_cases())
+    for impl, dec_type in ((0, "generic"), (1, "avx2")):
+        sel = [c for c in cases if c["impl"] == impl]
+        dec = srsgpu.LdpcDecoder(ctx, dec_type)
+        cfgs = [srsgpu.CodeblockDecodeConfig(c["bg"], c["Z"], nof_crc_bits=c["nof_crc_bits"],
+                                             nof_filler_bits=c["filler"], max_iterations=c["max_iter"]) for c in sel]
+        got = dec.decode_batch([c["llr"] for c in sel], cfgs,
+                               [None if c["crc_poly"] < 0 else c["crc_poly"] for c in sel])
+        for c, (r, bits) in zip(sel, got):
+            assert (r if r is not None else -1) == c["iters"], (c["bg"], c["Z"])
+            assert np.array_equal(bits, c["bits"])

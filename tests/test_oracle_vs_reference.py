@@ -152,3 +152,21 @@ def test_rate_dematch(orc, ref, case):
             want = ref.rate_dematch(impl, bg, Z, rv, qm, Nref, nof_filler, new_data, llr, init)
             got = orc.rate_dematch(mode, bg, Z, rv, qm, Nref, nof_filler, new_data, llr, init)
             assert np.array_equal(got, want), (new_data, mode)
+
+
+@pytest.mark.parametrize("bg,Z,rv,qm,filler,frac", [(1, 16, 0, 2, 51, 0.6), (1, 64, 0, 8, 46, 0.8), (2, 64, 1, 1, 115, 0.3),
+                                                    (1, 384, 3, 4, 100, 0.5), (2, 13, 2, 6, 0, 0.9)])
+def test_rate_dematch_limited_buffer_short_input(orc, ref, bg, Z, rv, qm, filler, frac):
+    """Limited-buffer rate matching (Ncb < N) with an input that ends in the first pass: the tail zeroing of
+    allot_llrs (ldpc_rate_dematcher_impl.cpp:198) applies to the end of the full buffer."""
+    rng = np.random.default_rng(Z + rv)
+    N = BG_N_SHORT[bg] * Z
+    Nref = int(N * 0.75)
+    E = qm * max(1, int(Nref * frac) // qm)
+    llr = rng.integers(-120, 121, E).astype(np.int8)
+    init = rng.integers(-120, 121, N).astype(np.int8)
+    for new_data in (1, 0):
+        for mode, impl in ((0, 0), (1, 1)):
+            want = ref.rate_dematch(impl, bg, Z, rv, qm, Nref, filler, new_data, llr, init)
+            got = orc.rate_dematch(mode, bg, Z, rv, qm, Nref, filler, new_data, llr, init)
+            assert np.array_equal(got, want), (new_data, mode)

@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Generates tests/golden/*.npz: input/output vectors produced by the srsRAN reference itself (built from its own
+sources by oracle/build_ref.sh into oracle/_ref/libsrsref.so). The reference repository ships no test-vector archives
+(its CMake downloads *_test_data.tar.gz at build time), so these fixtures are the pinned reference outputs; they travel
+to the GPU box where /root/reference does not exist.
+
+Run: python tools/gen_golden.py   (deterministic: fixed seeds)
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "srsran-5g_amd"))
+
+from oracle_lib import BG_K, BG_N_SHORT, CRC16, CRC24A, CRC24B, CRC_LEN, Reference  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def ref_encode_llrs(ref, rng, bg, Z, crc_poly, nof_filler, amp, noise, n_llr):
+    """Message with CRC (computed by the reference CRC), encoded by the reference encoder, mapped to LLRs."""
+    K = BG_K[bg]
+    L = K * Z - nof_filler
+    clen = CRC_LEN[crc_poly]
+    msg = np.zeros(K * Z, np.uint8)
+    msg[: L - clen] = rng.integers(0, 2, L - clen)
+    crc = ref.crc_bits(crc_poly, msg[: L - clen])
+    msg[L - clen: L] = [(crc >> (clen - 1 - i)) & 1 for i in range(clen)]
+    cb = ref.ldpc_encode(bg, Z, msg)
+    llr = (1 - 2 * cb.astype(np.int32)) * amp + (rng.normal(0, noise, cb.size) if noise > 0 else 0)
+    llr = np.clip(np.round(llr), -120, 120).astype(np.int8)
+    if nof_filler:
+        llr[(K - 2) * Z - nof_filler:(K - 2) * Z] = 127
+    return llr[:n_llr]
+
+
+def gen_crc(ref, rng):
+    polys, bits_list, want = [], [], []
+    for poly in range(6):
+        for n in (1, 24, 100, 1000, 8448):
+            b = rng.integers(0, 2, n).astype(np.uint8)
+            polys.append(poly)
+            bits_list.append(b)
+            want.append(ref.crc_bits(poly, b))
+    lens = np.array([b.size for b in bits_list], np.int32)
+    np.savez_compressed(os.path.join(OUT, "crc.npz"), poly=np.array(polys, np.int32), lens=lens,
+                        bits=np.concatenate(bits_list), crc=np.array(want, np.uint32))
+
+
+def gen_encoder(ref, rng):
+    rows = []
+    msgs, cbs = [], []
+    for bg in (1, 2):
+        for Z in (2, 7, 15, 36, 104, 208, 224, 240, 288, 320, 352, 384):
+            msg = rng.integers(0, 2, BG_K[bg] * Z).astype(np.uint8)
+            cb = ref.ldpc_encode(bg, Z, msg)
+            rows.append((bg, Z))
+            msgs.append(np.packbits(msg))
+            cbs.append(np.packbits(cb))
+    np.savez_compressed(os.path.join(OUT, "ldpc_encoder.npz"), cfg=np.array(rows, np.int32),
+                        msg=np.concatenate(msgs), cb=np.concatenate(cbs))
+
+
+def gen_decoder(ref, rng):
+    """Cases: (bg, Z, impl, crc_poly or -1, nof_crc_bits, filler, max_iter, scaling) + LLRs -> (iters, bits)."""
+    cfg, llrs, iters, outs = [], [], [], []
+    cases = []
+    for bg in (1, 2):
+        for Z in (2, 5, 13, 24, 64, 112, 208, 288, 352, 384):
+            for trial in range(4):
+                cases.append((bg, Z, trial))
+    for bg, Z, trial in cases:
+        K, N = BG_K[bg], BG_N_SHORT[bg]
+        crc_poly = [CRC16, CRC24B, CRC24A, CRC24B][trial]
+        filler = 0 if trial in (0, 1) else min(Z, (K - 2) * Z // 6)
+        if K * Z - filler < CRC_LEN[crc_poly] + 8:
+            crc_poly = 5
+        noise = [0.0, 7.0, 10.0, 14.0][trial]
+        n_nodes = [N, K + 2, (K + N) // 2, N][trial]
+        llr = ref_encode_llrs(ref, rng, bg, Z, crc_poly, filler, 12, noise, n_nodes * Z)
+        for impl in (Reference.GENERIC, Reference.AVX2):
+            for use_crc in (True, False):
+                if not use_crc and trial % 2:
+                    continue
+                nbits = 16 if CRC_LEN[crc_poly] < 24 else 24
+                r, o = ref.ldpc_decode(impl, bg, Z, llr, nof_crc_bits=nbits, nof_filler=filler,
+                                       crc_poly=crc_poly if use_crc else -1, max_iter=8, scaling=0.8)
+                cfg.append((bg, Z, impl, crc_poly if use_crc else -1, nbits, filler, 8, len(llr)))
+                llrs.append(llr)
+                iters.append(r)
+                outs.append(np.packbits(o))
+    np.savez_compressed(os.path.join(OUT, "ldpc_decoder.npz"), cfg=np.array(cfg, np.int32),
+                        llr=np.concatenate(llrs), iters=np.array(iters, np.int32), out=np.concatenate(outs))
+
+
+def gen_rate_matching(ref, rng):
+    """Per case: message, rate-matched output, dematcher input/initial buffer and the four dematcher outputs
+    (new_data 1/0 x generic/SIMD combining)."""
+    cfg, msgs, rm_out, dm_llr, dm_init, dm_out = [], [], [], [], [], []
+    for bg in (1, 2):
+        for Z in (3, 16, 64, 208, 384):
+            for rv in range(4):
+                if Z == 384 and rv in (1, 2):
+                    continue
+                qm = [1, 2, 4, 6, 8][(Z + rv) % 5]
+                N = BG_N_SHORT[bg] * Z
+                nsys = (BG_K[bg] - 2) * Z
+                filler = int(rng.integers(0, max(1, nsys // 4)))
+                Nref = [0, int(N * 0.75)][(rv + bg) % 2]
+                E = qm * int(rng.integers(max(1, (BG_K[bg] * Z) // qm // 2), 2 * N // qm))
+                msg = rng.integers(0, 2, BG_K[bg] * Z).astype(np.uint8)
+                msg[BG_K[bg] * Z - filler:] = 0
+                out = ref.rate_match(bg, Z, rv, qm, Nref, filler, msg, E)
+                llr = rng.integers(-120, 121, E).astype(np.int8)
+                init = rng.integers(-120, 121, N).astype(np.int8)
+                cfg.append((bg, Z, rv, qm, Nref, filler, E))
+                msgs.append(np.packbits(msg))
+                rm_out.append(np.packbits(out))
+                dm_llr.append(llr)
+                dm_init.append(init)
+                for new_data in (1, 0):
+                    for impl in (0, 1):
+                        dm_out.append(ref.rate_dematch(impl, bg, Z, rv, qm, Nref, filler, new_data, llr, init))
+    np.savez_compressed(os.path.join(OUT, "rate_matching.npz"), cfg=np.array(cfg, np.int32),
+                        msg=np.concatenate(msgs), rm_out=np.concatenate(rm_out), dm_llr=np.concatenate(dm_llr),
+                        dm_init=np.concatenate(dm_init), dm_out=np.concatenate(dm_out))
+
+
+def gen_pdsch_encoder(ref, rng):
+    from srsgpu import sch
+    cfg, tbs, cws, metas = [], [], [], []
+    for (n_prb, layers, qm, r) in ((4, 4, 8, 948), (5, 4, 8, 948), (51, 1, 6, 772), (10, 2, 4, 434), (2, 1, 2, 120),
+                                   (24, 3, 6, 517), (106, 2, 8, 682.5)):
+        g = sch.UeGrant(n_prb, layers, qm, r)
+        seg = g.segmentation()
+        for rv in (0, 2):
+            tb = rng.integers(0, 256, seg.tbs // 8).astype(np.uint8)
+            cw, meta = ref.pdsch_encode(seg.base_graph, rv, qm, layers, 0, g.nof_ch_symbols, tb)
+            cfg.append((seg.base_graph, rv, qm, layers, 0, g.nof_ch_symbols, seg.tbs // 8, meta.shape[0]))
+            tbs.append(tb)
+            cws.append(np.packbits(cw))
+            metas.append(meta.astype(np.int32))
+    np.savez_compressed(os.path.join(OUT, "pdsch_encoder.npz"), cfg=np.array(cfg, np.int32), tb=np.concatenate(tbs),
+                        cw=np.concatenate(cws), meta=np.concatenate(metas))
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    ref = Reference()
+    gen_crc(ref, np.random.default_rng(10))
+    gen_encoder(ref, np.random.default_rng(11))
+    gen_decoder(ref, np.random.default_rng(12))
+    gen_rate_matching(ref, np.random.default_rng(13))
+    gen_pdsch_encoder(ref, np.random.default_rng(14))
+    for f in sorted(os.listdir(OUT)):
+        print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+if __name__ == "__main__":
+    main()

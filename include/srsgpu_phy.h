@@ -104,6 +104,57 @@ int srsgpu_ldpc_decode(srsgpu_context*                   ctx,
                        int32_t*                          d_nof_iterations,
                        void*                             stream);
 
+/* ------------------------------------------------------------------------------------------------------------------
+ * PUSCH codeblock decoding — the operation behind hal::hw_accelerator_pusch_dec
+ * (include/srsran/hal/phy/upper/channel_processors/pusch/hw_accelerator_pusch_dec.h:88-:112: configure_operation,
+ * enqueue_operation, dequeue_operation, read_operation_outputs) and pusch_codeblock_decoder::decode
+ * (lib/phy/upper/channel_processors/pusch/pusch_codeblock_decoder.cpp:33): rate dematching with HARQ soft combining
+ * into a device-resident soft buffer (ldpc_rate_dematcher_impl.cpp:46), LDPC decoding and the codeblock CRC check,
+ * batched over every codeblock of a slot.
+ * ------------------------------------------------------------------------------------------------------------------ */
+typedef struct {
+  uint8_t  base_graph;       /* 1 or 2 */
+  uint8_t  rv;               /* redundancy version 0..3 */
+  uint8_t  modulation_order; /* Qm: 1, 2, 4, 6, 8 */
+  uint8_t  crc_poly;         /* codeblock CRC: CRC24B (segmented TB), CRC24A or CRC16 (single codeblock) */
+  uint16_t lifting_size;     /* Z */
+  uint16_t nof_filler_bits;  /* F */
+  uint8_t  nof_crc_bits;     /* 16 or 24 */
+  uint8_t  max_iterations;   /* > 0 */
+  uint8_t  new_data;         /* 1: first transmission (copy), 0: combine with the HARQ buffer */
+  uint8_t  use_early_stop;   /* 1: CRC after every iteration; 0: max_iterations then one CRC check */
+  float    scaling_factor;   /* normalised min-sum factor in (0, 1) */
+  uint32_t Nref;             /* limited-buffer rate matching N_ref, 0 = none */
+  uint32_t rm_length;        /* E: rate-matched length (multiple of Qm) */
+  uint32_t llr_offset;       /* first of the E LLRs in the codeword LLR buffer */
+  uint32_t harq_offset;      /* first of the N_short * Z LLRs of the codeblock's HARQ soft buffer */
+  uint32_t out_offset;       /* byte offset of the packed K*Z decoded message bits */
+} srsgpu_pusch_cb_config;
+
+typedef struct srsgpu_pusch_cb_plan srsgpu_pusch_cb_plan;
+
+/** Validates the codeblock configurations (reference assertions of ldpc_rate_dematcher_impl.cpp:54-:99 and the
+ *  decoder's) and uploads the work descriptors. Blocking; outside the timed / captured region. */
+int srsgpu_pusch_cb_plan_create(srsgpu_context*               ctx,
+                                int                           impl,
+                                const srsgpu_pusch_cb_config* cfgs,
+                                uint32_t                      nof_cbs,
+                                srsgpu_pusch_cb_plan**        plan);
+
+/** Rate-dematches d_llrs into the HARQ buffers d_harq (in place), then decodes every codeblock whose entry in
+ *  d_cb_crc_ok (persistent per-codeblock HARQ flags, may be NULL) is 0: writes the packed message to d_out, the number
+ *  of iterations (or -1; 0 for codeblocks skipped because their CRC had already passed) to d_nof_iterations, and sets
+ *  d_cb_crc_ok on success. Asynchronous on `stream`, hipGraph-capturable. */
+int srsgpu_pusch_cb_plan_execute(const srsgpu_pusch_cb_plan* plan,
+                                 const int8_t*               d_llrs,
+                                 int8_t*                     d_harq,
+                                 uint8_t*                    d_out,
+                                 int32_t*                    d_nof_iterations,
+                                 uint8_t*                    d_cb_crc_ok,
+                                 void*                       stream);
+
+void srsgpu_pusch_cb_plan_destroy(srsgpu_pusch_cb_plan* plan);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,6 +77,14 @@ struct srsgpu_context {
   std::mutex                           mtx;
 };
 
+struct srsgpu_pusch_cb_plan {
+  srsgpu_context*           ctx     = nullptr;
+  int                       impl    = SRSGPU_LDPC_IMPL_SIMD;
+  dm_desc*                  d_dm    = nullptr;
+  int                       nof_cbs = 0;
+  srsgpu_ldpc_decoder_plan* dec     = nullptr;
+};
+
 struct srsgpu_ldpc_decoder_plan {
   srsgpu_context* ctx            = nullptr;
   int             impl           = SRSGPU_LDPC_IMPL_SIMD;
@@ -200,6 +208,128 @@ void srsgpu_context_destroy(srsgpu_context* ctx)
   delete ctx;
 }
 
+} // extern "C"
+
+namespace {
+
+/// Codeblock work split by base graph (one kernel instantiation per base graph).
+struct dec_batch {
+  std::vector<dec_desc> descs[2];
+  int                   maxz[2] = {0, 0};
+};
+
+/// Validates one decoder configuration (ldpc_decoder_impl.cpp:48-:56, :73-:88) and appends its descriptor.
+int add_decoder_cb(srsgpu_context* ctx,
+                   uint32_t        i,
+                   int             bg,
+                   int             Z,
+                   int             nof_filler,
+                   int             nof_crc_bits,
+                   int             max_iter,
+                   float           sf,
+                   int             crc_poly,
+                   bool            early_stop,
+                   uint32_t        llr_offset,
+                   uint32_t        nof_llrs,
+                   uint32_t        out_offset,
+                   dec_batch&      batch)
+{
+  if (bg != 1 && bg != 2) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid base graph %d", i, bg);
+  }
+  const int pos = lifting_position(Z);
+  if (pos < 0) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid lifting size %d", i, Z);
+  }
+  const int K = (bg == 1) ? kBG1_K : kBG2_K;
+  const int N = ((bg == 1) ? kBG1_N_FULL : kBG2_N_FULL) - 2;
+  if (max_iter <= 0) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: max iterations must be different to 0", i);
+  }
+  if (!(sf > 0.0f && sf < 1.0f)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: scaling factor must be between 0 and 1 exclusively", i);
+  }
+  if (nof_crc_bits != 16 && nof_crc_bits != 24) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid number of CRC bits %d", i, nof_crc_bits);
+  }
+  if (static_cast<int>(nof_llrs) > N * Z || static_cast<int>(nof_llrs) < (K + 2) * Z) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: input length %u outside [%d, %d]", i, nof_llrs, (K + 2) * Z, N * Z);
+  }
+  if (nof_filler < 0 || nof_filler >= (K - 2) * Z) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid number of filler bits %d", i, nof_filler);
+  }
+  dec_desc d{};
+  d.llr_offset      = llr_offset;
+  d.nof_llr         = nof_llrs;
+  d.out_offset      = out_offset;
+  d.crc_table       = NO_CRC_TABLE;
+  d.div_magic       = static_cast<uint32_t>(((1ULL << 32) + static_cast<uint64_t>(Z) - 1) / static_cast<uint64_t>(Z));
+  d.Z               = static_cast<uint16_t>(Z);
+  d.zpos            = static_cast<uint16_t>(pos);
+  d.nof_significant = static_cast<uint16_t>(K * Z - nof_filler);
+  d.max_iter        = static_cast<uint16_t>(max_iter);
+  // avx2_support.h:71: identity above .9999, otherwise floor(sf * 2^16) in float arithmetic.
+  d.sf16     = (static_cast<double>(sf) >= .9999) ? 65536u
+                                                   : static_cast<uint32_t>(static_cast<uint16_t>(sf * 65536U));
+  d.sf       = sf;
+  d.cb_index = i;
+  d.flags    = 0;
+  if (crc_poly != SRSGPU_CRC_NONE) {
+    int r = get_crc_table(ctx, crc_poly, K * Z - nof_filler, d.crc_table);
+    if (r != SRSGPU_OK) {
+      return r;
+    }
+    d.flags = early_stop ? DEC_FLAG_EARLY_STOP : 0u;
+  }
+  batch.descs[bg - 1].push_back(d);
+  batch.maxz[bg - 1] = Z > batch.maxz[bg - 1] ? Z : batch.maxz[bg - 1];
+  return SRSGPU_OK;
+}
+
+int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, srsgpu_ldpc_decoder_plan** plan_out)
+{
+  auto* plan = new srsgpu_ldpc_decoder_plan();
+  plan->ctx  = ctx;
+  plan->impl = impl;
+  for (int b = 0; b < 2; ++b) {
+    plan->count[b]   = static_cast<int>(batch.descs[b].size());
+    plan->threads[b] = ((batch.maxz[b] + 63) / 64) * 64;
+    if (plan->count[b] == 0) {
+      continue;
+    }
+    const size_t bytes = batch.descs[b].size() * sizeof(dec_desc);
+    if (hipMalloc(&plan->d_desc[b], bytes) != hipSuccess ||
+        hipMemcpy(plan->d_desc[b], batch.descs[b].data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      srsgpu_ldpc_decoder_plan_destroy(plan);
+      return fail(SRSGPU_ERR_HIP, "failed to upload decoder descriptors");
+    }
+  }
+  *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
+                         const int8_t*                   d_llrs,
+                         uint8_t*                        d_out,
+                         int32_t*                        d_nof_iterations,
+                         uint8_t*                        d_cb_crc_ok,
+                         hipStream_t                     s)
+{
+  for (int b = 0; b < 2; ++b) {
+    if (plan->count[b] == 0) {
+      continue;
+    }
+    launch_ldpc_decode(b + 1, plan->impl, plan->d_desc[b], plan->count[b], plan->threads[b], d_llrs, d_out,
+                       d_nof_iterations, plan->ctx->d_shifts[b], plan->ctx->d_crc_arena, d_cb_crc_ok, s);
+    HIP_TRY(hipGetLastError());
+  }
+  return SRSGPU_OK;
+}
+
+} // namespace
+
+extern "C" {
+
 int srsgpu_ldpc_decoder_plan_create(srsgpu_context*                   ctx,
                                     int                               impl,
                                     const srsgpu_ldpc_decoder_config* cfgs,
@@ -214,81 +344,17 @@ int srsgpu_ldpc_decoder_plan_create(srsgpu_context*                   ctx,
   }
   std::lock_guard<std::mutex> lock(ctx->mtx);
   HIP_TRY(hipSetDevice(ctx->device));
-  std::vector<dec_desc> descs[2];
-  int                   maxz[2] = {0, 0};
+  dec_batch batch;
   for (uint32_t i = 0; i < nof_cbs; ++i) {
     const srsgpu_ldpc_decoder_config& c = cfgs[i];
-    if (c.base_graph != 1 && c.base_graph != 2) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid base graph %d", i, c.base_graph);
-    }
-    const int Z   = c.lifting_size;
-    const int pos = lifting_position(Z);
-    if (pos < 0) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid lifting size %d", i, Z);
-    }
-    const int K = (c.base_graph == 1) ? kBG1_K : kBG2_K;
-    const int N = ((c.base_graph == 1) ? kBG1_N_FULL : kBG2_N_FULL) - 2;
-    // ldpc_decoder_impl.cpp:48-:56
-    if (c.max_iterations == 0) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: max iterations must be different to 0", i);
-    }
-    if (!(c.scaling_factor > 0.0f && c.scaling_factor < 1.0f)) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: scaling factor must be between 0 and 1 exclusively", i);
-    }
-    if (c.nof_crc_bits != 16 && c.nof_crc_bits != 24) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid number of CRC bits %d", i, c.nof_crc_bits);
-    }
-    // ldpc_decoder_impl.cpp:73-:88
-    if (static_cast<int>(c.nof_llrs) > N * Z || static_cast<int>(c.nof_llrs) < (K + 2) * Z) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: input length %u outside [%d, %d]", i, c.nof_llrs, (K + 2) * Z,
-                  N * Z);
-    }
-    if (c.nof_filler_bits >= (K - 2) * Z) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid number of filler bits %d", i, c.nof_filler_bits);
-    }
-    dec_desc d{};
-    d.llr_offset      = c.llr_offset;
-    d.nof_llr         = c.nof_llrs;
-    d.out_offset      = c.out_offset;
-    d.crc_table       = NO_CRC_TABLE;
-    d.div_magic       = static_cast<uint32_t>(((1ULL << 32) + static_cast<uint64_t>(Z) - 1) / static_cast<uint64_t>(Z));
-    d.Z               = static_cast<uint16_t>(Z);
-    d.zpos            = static_cast<uint16_t>(pos);
-    d.nof_significant = static_cast<uint16_t>(K * Z - c.nof_filler_bits);
-    d.max_iter        = c.max_iterations;
-    // avx2_support.h:71: identity above .9999, otherwise floor(sf * 2^16) in float arithmetic.
-    d.sf16     = (static_cast<double>(c.scaling_factor) >= .9999)
-                     ? 65536u
-                     : static_cast<uint32_t>(static_cast<uint16_t>(c.scaling_factor * 65536U));
-    d.sf       = c.scaling_factor;
-    d.cb_index = i;
-    if (c.crc_poly != SRSGPU_CRC_NONE) {
-      int r = get_crc_table(ctx, c.crc_poly, K * Z - c.nof_filler_bits, d.crc_table);
-      if (r != SRSGPU_OK) {
-        return r;
-      }
-    }
-    descs[c.base_graph - 1].push_back(d);
-    maxz[c.base_graph - 1] = Z > maxz[c.base_graph - 1] ? Z : maxz[c.base_graph - 1];
-  }
-  auto* plan = new srsgpu_ldpc_decoder_plan();
-  plan->ctx  = ctx;
-  plan->impl = impl;
-  for (int b = 0; b < 2; ++b) {
-    plan->count[b]   = static_cast<int>(descs[b].size());
-    plan->threads[b] = ((maxz[b] + 63) / 64) * 64;
-    if (plan->count[b] == 0) {
-      continue;
-    }
-    if (hipMalloc(&plan->d_desc[b], descs[b].size() * sizeof(dec_desc)) != hipSuccess ||
-        hipMemcpy(plan->d_desc[b], descs[b].data(), descs[b].size() * sizeof(dec_desc), hipMemcpyHostToDevice) !=
-            hipSuccess) {
-      srsgpu_ldpc_decoder_plan_destroy(plan);
-      return fail(SRSGPU_ERR_HIP, "failed to upload decoder descriptors");
+    int r = add_decoder_cb(ctx, i, c.base_graph, c.lifting_size, c.nof_filler_bits, c.nof_crc_bits, c.max_iterations,
+                           c.scaling_factor, c.crc_poly, /*early_stop=*/true, c.llr_offset, c.nof_llrs, c.out_offset,
+                           batch);
+    if (r != SRSGPU_OK) {
+      return r;
     }
   }
-  *plan_out = plan;
-  return SRSGPU_OK;
+  return upload_decoder_plan(ctx, impl, batch, plan_out);
 }
 
 int srsgpu_ldpc_decoder_plan_execute(const srsgpu_ldpc_decoder_plan* plan,
@@ -300,16 +366,7 @@ int srsgpu_ldpc_decoder_plan_execute(const srsgpu_ldpc_decoder_plan* plan,
   if (plan == nullptr || d_llrs == nullptr || d_out == nullptr || d_nof_iterations == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  auto s = static_cast<hipStream_t>(stream);
-  for (int b = 0; b < 2; ++b) {
-    if (plan->count[b] == 0) {
-      continue;
-    }
-    launch_ldpc_decode(b + 1, plan->impl, plan->d_desc[b], plan->count[b], plan->threads[b], d_llrs, d_out,
-                       d_nof_iterations, plan->ctx->d_shifts[b], plan->ctx->d_crc_arena, s);
-    HIP_TRY(hipGetLastError());
-  }
-  return SRSGPU_OK;
+  return execute_decoder_plan(plan, d_llrs, d_out, d_nof_iterations, nullptr, static_cast<hipStream_t>(stream));
 }
 
 void srsgpu_ldpc_decoder_plan_destroy(srsgpu_ldpc_decoder_plan* plan)
@@ -348,6 +405,124 @@ int srsgpu_ldpc_decode(srsgpu_context*                   ctx,
   }
   srsgpu_ldpc_decoder_plan_destroy(plan);
   return r;
+}
+
+
+int srsgpu_pusch_cb_plan_create(srsgpu_context*               ctx,
+                                int                           impl,
+                                const srsgpu_pusch_cb_config* cfgs,
+                                uint32_t                      nof_cbs,
+                                srsgpu_pusch_cb_plan**        plan_out)
+{
+  if (ctx == nullptr || plan_out == nullptr || (cfgs == nullptr && nof_cbs > 0)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  if (impl != SRSGPU_LDPC_IMPL_GENERIC && impl != SRSGPU_LDPC_IMPL_SIMD) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "invalid implementation %d", impl);
+  }
+  std::lock_guard<std::mutex> lock(ctx->mtx);
+  HIP_TRY(hipSetDevice(ctx->device));
+  static const double   shift_bg1[4] = {0, 17, 33, 56};  // ldpc_rate_dematcher_impl.cpp:33
+  static const double   shift_bg2[4] = {0, 13, 25, 43};
+  dec_batch             batch;
+  std::vector<dm_desc>  dms(nof_cbs);
+  for (uint32_t i = 0; i < nof_cbs; ++i) {
+    const srsgpu_pusch_cb_config& c = cfgs[i];
+    const int                     Z = c.lifting_size;
+    if ((c.base_graph != 1 && c.base_graph != 2) || lifting_position(Z) < 0) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid base graph %d / lifting size %d", i, c.base_graph, Z);
+    }
+    const int K    = (c.base_graph == 1) ? kBG1_K : kBG2_K;
+    const int N    = (((c.base_graph == 1) ? kBG1_N_FULL : kBG2_N_FULL) - 2) * Z;
+    const int nsys = (K - 2) * Z;
+    const int qm   = c.modulation_order;
+    if (c.rv > 3) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: RV should an integer between 0 and 3", i);
+    }
+    if (qm != 1 && qm != 2 && qm != 4 && qm != 6 && qm != 8) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid modulation order %d", i, qm);
+    }
+    if (c.rm_length == 0 || c.rm_length % qm != 0 || c.rm_length > 22u * 384u * 35u) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid rate-matched length %u", i, c.rm_length);
+    }
+    if (c.Nref > 66u * 384u) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: N_ref %u must be smaller or equal to %u", i, c.Nref, 66u * 384u);
+    }
+    if (c.nof_filler_bits >= nsys) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid number of filler bits", i);
+    }
+    const int Ncb = (c.Nref > 0 && static_cast<int>(c.Nref) < N) ? static_cast<int>(c.Nref) : N;
+    if (Ncb <= nsys) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: circular buffer %d shorter than the systematic part", i, Ncb);
+    }
+    const double   sf    = (c.base_graph == 1 ? shift_bg1 : shift_bg2)[c.rv];
+    const int      k0    = static_cast<int>(std::floor((sf * Ncb) / N)) * Z;
+    const int      ninfo = nsys - c.nof_filler_bits;
+    dm_desc&       d     = dms[i];
+    d.llr_offset         = c.llr_offset;
+    d.harq_offset        = c.harq_offset;
+    d.E                  = c.rm_length;
+    d.N                  = static_cast<uint32_t>(N);
+    d.Ncb                = static_cast<uint32_t>(Ncb);
+    d.nsys               = static_cast<uint32_t>(nsys);
+    d.v0                 = static_cast<uint32_t>(k0 < ninfo ? k0 : (k0 < nsys ? ninfo : k0 - c.nof_filler_bits));
+    d.nof_filler         = c.nof_filler_bits;
+    d.Qm                 = static_cast<uint8_t>(qm);
+    d.new_data           = c.new_data ? 1 : 0;
+    d.skip               = 0;
+    int r = add_decoder_cb(ctx, i, c.base_graph, Z, c.nof_filler_bits, c.nof_crc_bits, c.max_iterations,
+                           c.scaling_factor, c.crc_poly, c.use_early_stop != 0, c.harq_offset,
+                           static_cast<uint32_t>(N), c.out_offset, batch);
+    if (r != SRSGPU_OK) {
+      return r;
+    }
+  }
+  auto* plan    = new srsgpu_pusch_cb_plan();
+  plan->ctx     = ctx;
+  plan->impl    = impl;
+  plan->nof_cbs = static_cast<int>(nof_cbs);
+  int r         = upload_decoder_plan(ctx, impl, batch, &plan->dec);
+  if (r != SRSGPU_OK) {
+    delete plan;
+    return r;
+  }
+  if (nof_cbs > 0 && (hipMalloc(&plan->d_dm, dms.size() * sizeof(dm_desc)) != hipSuccess ||
+                      hipMemcpy(plan->d_dm, dms.data(), dms.size() * sizeof(dm_desc), hipMemcpyHostToDevice) !=
+                          hipSuccess)) {
+    srsgpu_pusch_cb_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload rate dematcher descriptors");
+  }
+  *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+int srsgpu_pusch_cb_plan_execute(const srsgpu_pusch_cb_plan* plan,
+                                 const int8_t*               d_llrs,
+                                 int8_t*                     d_harq,
+                                 uint8_t*                    d_out,
+                                 int32_t*                    d_nof_iterations,
+                                 uint8_t*                    d_cb_crc_ok,
+                                 void*                       stream)
+{
+  if (plan == nullptr || d_llrs == nullptr || d_harq == nullptr || d_out == nullptr || d_nof_iterations == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  auto s = static_cast<hipStream_t>(stream);
+  launch_rate_dematch(plan->impl, plan->d_dm, plan->nof_cbs, d_llrs, d_harq, s);
+  HIP_TRY(hipGetLastError());
+  return execute_decoder_plan(plan->dec, d_harq, d_out, d_nof_iterations, d_cb_crc_ok, s);
+}
+
+void srsgpu_pusch_cb_plan_destroy(srsgpu_pusch_cb_plan* plan)
+{
+  if (plan == nullptr) {
+    return;
+  }
+  if (plan->d_dm != nullptr) {
+    (void)hipFree(plan->d_dm);
+  }
+  srsgpu_ldpc_decoder_plan_destroy(plan->dec);
+  delete plan;
 }
 
 } // extern "C"

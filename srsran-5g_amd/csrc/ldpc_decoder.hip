@@ -185,7 +185,8 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
                                                           uint8_t* __restrict__ out,
                                                           int32_t* __restrict__ results,
                                                           const uint16_t* __restrict__ shift_table,
-                                                          const uint32_t* __restrict__ crc_tables)
+                                                          const uint32_t* __restrict__ crc_tables,
+                                                          uint8_t* __restrict__ cb_crc_ok)
 {
   using G = bg_t<BG>;
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
@@ -194,6 +195,13 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
   uint16_t* sh      = reinterpret_cast<uint16_t*>(smem + G::NF * SOFT_COL_STRIDE + SCRATCH_BYTES);
 
   const dec_desc d      = descs[blockIdx.x];
+  // HARQ context (pusch_decoder_impl.cpp:300): a codeblock whose CRC already passed is not decoded again.
+  if (cb_crc_ok != nullptr && cb_crc_ok[d.cb_index] != 0) {
+    if (threadIdx.x == 0) {
+      results[d.cb_index] = 0;
+    }
+    return;
+  }
   const int      Z      = d.Z;
   const int      z      = threadIdx.x;
   const bool     active = z < Z;
@@ -287,8 +295,10 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
       }
     });
 
-    if (use_crc) {
-      // Early stop (ldpc_decoder_impl.cpp:133): every systematic soft bit non-zero and CRC remainder zero. The CRC of
+    // With early stopping the CRC is checked after every iteration (ldpc_decoder_impl.cpp:133); without it, once after
+    // the last iteration (pusch_codeblock_decoder.cpp:53: decode without CRC, then check the CRC of the output).
+    if (use_crc && ((d.flags & DEC_FLAG_EARLY_STOP) != 0 || it == max_iter - 1)) {
+      // Success: every systematic soft bit non-zero (early stop only) and CRC remainder zero. The CRC of
       // the hard decisions is the XOR of per-bit contributions x^(order + L - 1 - i) mod g(x) (crc_table).
       uint32_t acc  = 0;
       uint32_t zero = 0;
@@ -315,10 +325,14 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
         tacc ^= static_cast<uint32_t>(red[2 * w]);
         tzero |= static_cast<uint32_t>(red[2 * w + 1]);
       }
-      if (tzero == 0 && tacc == 0) {
+      const bool early = (d.flags & DEC_FLAG_EARLY_STOP) != 0;
+      if ((tzero == 0 || !early) && tacc == 0) {
         write_hard_bits(soft, cb_out, msg_len, Z, d.div_magic);
         if (threadIdx.x == 0) {
           results[d.cb_index] = it + 1;
+          if (cb_crc_ok != nullptr) {
+            cb_crc_ok[d.cb_index] = 1;
+          }
         }
         return;
       }
@@ -342,6 +356,7 @@ void launch_ldpc_decode(int             bg,
                         int32_t*        d_results,
                         const uint16_t* d_shifts,
                         const uint32_t* d_crc_tables,
+                        uint8_t*        d_cb_crc_ok,
                         hipStream_t     stream)
 {
   if (nof_cbs <= 0) {
@@ -353,15 +368,15 @@ void launch_ldpc_decode(int             bg,
   dim3         grid(nof_cbs), block(block_threads);
   if (bg == 1) {
     if (mode == 1) {
-      ldpc_decode_kernel<1, 1><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables);
+      ldpc_decode_kernel<1, 1><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok);
     } else {
-      ldpc_decode_kernel<1, 0><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables);
+      ldpc_decode_kernel<1, 0><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok);
     }
   } else {
     if (mode == 1) {
-      ldpc_decode_kernel<2, 1><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables);
+      ldpc_decode_kernel<2, 1><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok);
     } else {
-      ldpc_decode_kernel<2, 0><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables);
+      ldpc_decode_kernel<2, 0><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok);
     }
   }
 }

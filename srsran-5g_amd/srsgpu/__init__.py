@@ -57,6 +57,31 @@ class LdpcDecoderConfig(ctypes.Structure):
 
 assert ctypes.sizeof(LdpcDecoderConfig) == 24
 
+
+class PuschCbConfig(ctypes.Structure):
+    """srsgpu_pusch_cb_config (include/srsgpu_phy.h)."""
+    _fields_ = [
+        ("base_graph", ctypes.c_uint8),
+        ("rv", ctypes.c_uint8),
+        ("modulation_order", ctypes.c_uint8),
+        ("crc_poly", ctypes.c_uint8),
+        ("lifting_size", ctypes.c_uint16),
+        ("nof_filler_bits", ctypes.c_uint16),
+        ("nof_crc_bits", ctypes.c_uint8),
+        ("max_iterations", ctypes.c_uint8),
+        ("new_data", ctypes.c_uint8),
+        ("use_early_stop", ctypes.c_uint8),
+        ("scaling_factor", ctypes.c_float),
+        ("Nref", ctypes.c_uint32),
+        ("rm_length", ctypes.c_uint32),
+        ("llr_offset", ctypes.c_uint32),
+        ("harq_offset", ctypes.c_uint32),
+        ("out_offset", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(PuschCbConfig) == 36
+
 _lib = None
 
 
@@ -79,6 +104,10 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_ldpc_decoder_plan_destroy.argtypes = [P]
     lib.srsgpu_ldpc_decoder_plan_destroy.restype = None
     lib.srsgpu_ldpc_decode.argtypes = [P, ctypes.c_int, P, ctypes.c_uint32, P, P, P, P]
+    lib.srsgpu_pusch_cb_plan_create.argtypes = [P, ctypes.c_int, P, ctypes.c_uint32, ctypes.POINTER(P)]
+    lib.srsgpu_pusch_cb_plan_execute.argtypes = [P, P, P, P, P, P, P]
+    lib.srsgpu_pusch_cb_plan_destroy.argtypes = [P]
+    lib.srsgpu_pusch_cb_plan_destroy.restype = None
     _lib = lib
     return lib
 
@@ -87,7 +116,8 @@ def load_library(path: str = LIB_PATH):
 EXPORTED_SYMBOLS = [
     "srsgpu_version", "srsgpu_last_error", "srsgpu_context_create", "srsgpu_context_destroy",
     "srsgpu_ldpc_decoder_plan_create", "srsgpu_ldpc_decoder_plan_execute", "srsgpu_ldpc_decoder_plan_destroy",
-    "srsgpu_ldpc_decode",
+    "srsgpu_ldpc_decode", "srsgpu_pusch_cb_plan_create", "srsgpu_pusch_cb_plan_execute",
+    "srsgpu_pusch_cb_plan_destroy",
 ]
 
 
@@ -250,3 +280,104 @@ class LdpcDecoder:
             off += out_bytes[i]
             results.append((None if iters[i] < 0 else int(iters[i]), bits))
         return results
+
+
+class PuschCbPlan:
+    """srsgpu_pusch_cb_plan: rate dematching + HARQ combining + LDPC decoding + CB CRC for a batch of codeblocks."""
+
+    def __init__(self, ctx: Context, impl: int, cfg_array):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        _check(_lib.srsgpu_pusch_cb_plan_create(ctx.handle, impl, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                len(cfg_array), ctypes.byref(h)))
+        self.handle = h
+        self.nof_cbs = len(cfg_array)
+
+    def execute(self, d_llrs, d_harq, d_out, d_iters, d_cb_crc_ok=None, stream=None):
+        _check(_lib.srsgpu_pusch_cb_plan_execute(self.handle, _dptr(d_llrs), _dptr(d_harq), _dptr(d_out),
+                                                 _dptr(d_iters), _dptr(d_cb_crc_ok), _stream_handle(stream)))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.srsgpu_pusch_cb_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+@dataclass
+class PuschCodeblock:
+    """One codeblock of a PUSCH transport block: hw_pusch_decoder_configuration (hw_accelerator_pusch_dec.h:30)."""
+    base_graph: int
+    lifting_size: int
+    rv: int
+    modulation_order: int
+    rm_length: int
+    nof_filler_bits: int = 0
+    crc_poly: int = CRC24B
+    nof_crc_bits: int = 24
+    Nref: int = 0
+    new_data: bool = True
+    use_early_stop: bool = True
+    max_iterations: int = 6
+    scaling_factor: float = 0.8
+
+
+def make_pusch_cb_configs(cbs: Sequence[PuschCodeblock]):
+    """Packs codeblocks with contiguous LLR / HARQ / output offsets."""
+    arr = (PuschCbConfig * len(cbs))()
+    lo = ho = oo = 0
+    for i, c in enumerate(cbs):
+        a = arr[i]
+        a.base_graph, a.rv, a.modulation_order, a.crc_poly = c.base_graph, c.rv, c.modulation_order, c.crc_poly
+        a.lifting_size, a.nof_filler_bits, a.nof_crc_bits = c.lifting_size, c.nof_filler_bits, c.nof_crc_bits
+        a.max_iterations, a.new_data, a.use_early_stop = c.max_iterations, int(c.new_data), int(c.use_early_stop)
+        a.scaling_factor, a.Nref, a.rm_length = c.scaling_factor, c.Nref, c.rm_length
+        a.llr_offset, a.harq_offset, a.out_offset = lo, ho, oo
+        lo += c.rm_length
+        ho += BG_N_SHORT[c.base_graph] * c.lifting_size
+        oo += (BG_K[c.base_graph] * c.lifting_size + 7) // 8
+    return arr, lo, ho, oo
+
+
+class PuschCodeblockDecoder:
+    """GPU counterpart of pusch_codeblock_decoder (pusch_codeblock_decoder.cpp:33) / hw_accelerator_pusch_dec with an
+    external (device-resident) HARQ buffer: the caller owns d_harq and d_cb_crc_ok across retransmissions."""
+
+    def __init__(self, ctx: Context, dec_type: str = "auto"):
+        if dec_type not in IMPL_BY_NAME:
+            raise SrsGpuError(f"invalid decoder type '{dec_type}'")
+        self.ctx = ctx
+        self.impl = IMPL_BY_NAME[dec_type]
+
+    def decode(self, llrs_list, cbs: Sequence[PuschCodeblock], harq: np.ndarray = None, cb_crc_ok: np.ndarray = None):
+        """Returns (results [(nof_iterations or None, K*Z bits)], updated harq buffer, updated crc flags)."""
+        arr, nllr, nharq, nout = make_pusch_cb_configs(cbs)
+        dev = torch.device("cuda", self.ctx.device)
+        flat = np.concatenate([np.asarray(x, dtype=np.int8) for x in llrs_list])
+        assert flat.size == nllr
+        d_llrs = torch.from_numpy(flat).to(dev)
+        d_harq = (torch.from_numpy(np.asarray(harq, dtype=np.int8).copy()).to(dev) if harq is not None
+                  else torch.zeros(nharq, dtype=torch.int8, device=dev))
+        d_crc = (torch.from_numpy(np.asarray(cb_crc_ok, dtype=np.uint8).copy()).to(dev) if cb_crc_ok is not None
+                 else torch.zeros(len(cbs), dtype=torch.uint8, device=dev))
+        d_out = torch.zeros(nout, dtype=torch.uint8, device=dev)
+        d_iters = torch.zeros(len(cbs), dtype=torch.int32, device=dev)
+        plan = PuschCbPlan(self.ctx, self.impl, arr)
+        plan.execute(d_llrs, d_harq, d_out, d_iters, d_crc)
+        torch.cuda.synchronize(dev)
+        plan.close()
+        out = d_out.cpu().numpy()
+        iters = d_iters.cpu().numpy()
+        res = []
+        off = 0
+        for i, c in enumerate(cbs):
+            nb = BG_K[c.base_graph] * c.lifting_size
+            ob = (nb + 7) // 8
+            res.append((None if iters[i] < 0 else int(iters[i]), unpack_bits(out[off:off + ob], nb)))
+            off += ob
+        return res, d_harq.cpu().numpy(), d_crc.cpu().numpy()

@@ -1,0 +1,111 @@
+"""GPU parity of the PUSCH codeblock path (rate dematching + HARQ combining + LDPC decoding + CB CRC) against the
+oracle composition (tests/chain_lib.py), through the C ABI (srsgpu_pusch_cb_plan_*)."""
+import numpy as np
+import pytest
+
+from chain_lib import bits_to_llrs, crc_for_tb, oracle_pdsch_encode, oracle_pusch_cb_decode
+from oracle_lib import BG_K, BG_N_SHORT, Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import srsgpu
+    return srsgpu.Context(0)
+
+
+@pytest.mark.parametrize("dec_type,mode", [("avx2", 1), ("generic", 0)])
+def test_rate_dematch_random_configs(orc, ctx, dec_type, mode):
+    """HARQ buffer after the plan == oracle rate dematcher, 300 random codeblocks in one batch (random rv, Qm, LBRM,
+    fillers, lengths ending inside / after the first pass, copy and combine, +/-127 inputs)."""
+    import srsgpu
+    rng = np.random.default_rng(31 + mode)
+    cbs, llrs, inits = [], [], []
+    while len(cbs) < 300:
+        bg = int(rng.integers(1, 3))
+        Z = int(rng.choice([2, 3, 5, 16, 24, 64, 144, 384]))
+        N = BG_N_SHORT[bg] * Z
+        nsys = (BG_K[bg] - 2) * Z
+        qm = int(rng.choice([1, 2, 4, 6, 8]))
+        F = int(rng.integers(0, nsys // 3 + 1))
+        Nref = int(rng.choice([0, int(N * rng.uniform(0.75, 0.99))]))
+        if 0 < Nref <= nsys:
+            continue
+        E = qm * int(rng.integers(1, 3 * N // qm))
+        cbs.append(srsgpu.PuschCodeblock(bg, Z, int(rng.integers(0, 4)), qm, E, nof_filler_bits=F, Nref=Nref,
+                                         new_data=bool(rng.integers(0, 2)), max_iterations=1))
+        llrs.append(rng.integers(-127, 128, E).astype(np.int8))
+        inits.append(rng.integers(-127, 128, N).astype(np.int8))
+    dec = srsgpu.PuschCodeblockDecoder(ctx, dec_type)
+    _, harq, _ = dec.decode(llrs, cbs, harq=np.concatenate(inits))
+    off = 0
+    for c, llr, init in zip(cbs, llrs, inits):
+        N = BG_N_SHORT[c.base_graph] * c.lifting_size
+        want = orc.rate_dematch(mode, c.base_graph, c.lifting_size, c.rv, c.modulation_order, c.Nref,
+                                c.nof_filler_bits, int(c.new_data), llr, init)
+        assert np.array_equal(harq[off:off + N], want), c
+        off += N
+
+
+def _ue_codeblocks(srsgpu, seg, rv, qm, new_data, early_stop, max_iter=8):
+    return [srsgpu.PuschCodeblock(seg.base_graph, seg.lifting_size, rv, qm, cb.rm_length,
+                                  nof_filler_bits=cb.nof_filler_bits, crc_poly=crc_for_tb(seg),
+                                  nof_crc_bits=cb.nof_crc_bits, new_data=new_data, use_early_stop=early_stop,
+                                  max_iterations=max_iter) for cb in seg.codeblocks]
+
+
+@pytest.mark.parametrize("early_stop", [True, False])
+def test_pusch_chain_with_harq_retransmission(orc, ctx, early_stop):
+    """Transport blocks of several grants: encode (oracle), noisy LLRs, rv0 first transmission, then an rv2
+    retransmission combined in the device HARQ buffer; every step equals the oracle chain (iterations, bits, HARQ
+    buffer, CRC flags)."""
+    import srsgpu
+    from srsgpu import sch
+    rng = np.random.default_rng(77 + early_stop)
+    dec = srsgpu.PuschCodeblockDecoder(ctx, "avx2")
+    grants = [sch.UeGrant(4, 4, 8, 948), sch.UeGrant(5, 2, 6, 772), sch.UeGrant(12, 1, 4, 434),
+              sch.UeGrant(2, 1, 2, 120), sch.UeGrant(30, 2, 8, 682.5)]
+    all_cbs, all_llrs, oracle_state = [], [], []
+    tx = {}
+    for gi, g in enumerate(grants):
+        seg = g.segmentation()
+        tb = rng.integers(0, 256, seg.tbs // 8).astype(np.uint8)
+        tx[gi] = (tb, seg)
+    for rv, new_data, noise in ((0, True, 9.0), (2, False, 9.0)):
+        cbs, llrs = [], []
+        for gi, g in enumerate(grants):
+            tb, seg = tx[gi]
+            cw, seg, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, rv, g.qm, g.nof_layers, 0, g.nof_ch_symbols)
+            llr = bits_to_llrs(rng, cw, amp=6.0, noise=noise)
+            cbs += _ue_codeblocks(srsgpu, seg, rv, g.qm, new_data, early_stop)
+            for cb in seg.codeblocks:
+                llrs.append(llr[cb.cw_offset: cb.cw_offset + cb.rm_length])
+        if new_data:
+            harq_g = None
+            crc_g = None
+            oracle_state = [(np.zeros(BG_N_SHORT[c.base_graph] * c.lifting_size, np.int8), False) for c in cbs]
+        res, harq_g, crc_g = dec.decode(llrs, cbs, harq=harq_g, cb_crc_ok=crc_g)
+        off = 0
+        new_state = []
+        n_ok = 0
+        for i, (c, llr) in enumerate(zip(cbs, llrs)):
+            h, ok = oracle_state[i]
+            r, bits, h2, ok2 = oracle_pusch_cb_decode(orc, 1, c, llr, h, ok)
+            N = BG_N_SHORT[c.base_graph] * c.lifting_size
+            assert np.array_equal(harq_g[off:off + N], h2), (rv, i)
+            off += N
+            r_g, bits_g = res[i]
+            assert (r_g if r_g is not None else -1) == r, (rv, i)
+            if bits is not None:
+                assert np.array_equal(bits_g, bits), (rv, i)
+            assert bool(crc_g[i]) == ok2
+            n_ok += ok2
+            new_state.append((h2, ok2))
+        oracle_state = new_state
+    assert n_ok > 0

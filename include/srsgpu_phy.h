@@ -155,6 +155,45 @@ int srsgpu_pusch_cb_plan_execute(const srsgpu_pusch_cb_plan* plan,
 
 void srsgpu_pusch_cb_plan_destroy(srsgpu_pusch_cb_plan* plan);
 
+/* ------------------------------------------------------------------------------------------------------------------
+ * PDSCH encoder — replaces srsran::pdsch_encoder::encode(span<uint8_t> codeword, span<const uint8_t> transport_block,
+ * const configuration& cfg) (include/srsran/phy/upper/channel_processors/pdsch/pdsch_encoder.h,
+ * lib/phy/upper/channel_processors/pdsch/pdsch_encoder_impl.cpp:28) and hal::hw_accelerator_pdsch_enc in TB mode
+ * (hw_accelerator_pdsch_enc.h): TB CRC, segmentation, CB CRC24B, LDPC encoding and rate matching of every transport
+ * block of a slot. The codeword is written packed MSB first (G = nof_ch_symbols * Qm bits per TB).
+ * ------------------------------------------------------------------------------------------------------------------ */
+typedef struct {
+  uint8_t  base_graph;       /* 1 or 2 */
+  uint8_t  rv;               /* 0..3 */
+  uint8_t  modulation_order; /* Qm: 1, 2, 4, 6, 8 */
+  uint8_t  nof_layers;       /* 1..4 */
+  uint32_t tbs_bytes;        /* transport block size in bytes */
+  uint32_t nof_ch_symbols;   /* number of channel symbols (multiple of nof_layers) */
+  uint32_t Nref;             /* limited-buffer rate matching N_ref, 0 = none */
+  uint32_t tb_offset;        /* byte offset of the transport block in the TB buffer */
+  uint32_t cw_offset;        /* byte offset of the codeword in the output buffer (multiple of 4) */
+} srsgpu_pdsch_tb_config;
+
+typedef struct srsgpu_pdsch_encoder_plan srsgpu_pdsch_encoder_plan;
+
+/** Segments every transport block (ldpc_segmenter_tx_impl.cpp:58), validates and uploads the work. Blocking. */
+int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
+                                     const srsgpu_pdsch_tb_config* cfgs,
+                                     uint32_t                      nof_tbs,
+                                     srsgpu_pdsch_encoder_plan**   plan);
+
+/** Number of codeblocks the plan encodes (all transport blocks). */
+uint32_t srsgpu_pdsch_encoder_plan_nof_codeblocks(const srsgpu_pdsch_encoder_plan* plan);
+
+/** Encodes the planned transport blocks from d_tbs into d_codewords. The plan owns (zeroes, then fills) the output
+ *  byte range [min cw_offset, max(cw_offset + ceil(G/32)*4)). Asynchronous on `stream`, hipGraph-capturable. */
+int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
+                                      const uint8_t*                   d_tbs,
+                                      uint8_t*                         d_codewords,
+                                      void*                            stream);
+
+void srsgpu_pdsch_encoder_plan_destroy(srsgpu_pdsch_encoder_plan* plan);
+
 #ifdef __cplusplus
 }
 #endif

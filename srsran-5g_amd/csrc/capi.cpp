@@ -3,12 +3,14 @@
 // HIP kernels; a missing/unsupported device makes every call fail loudly (there is no CPU fallback).
 #include "srsgpu_phy.h"
 #include "ldpc_base_graphs.h"
+#include "sch_host.h"
 #include "srsgpu_internal.h"
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
@@ -71,6 +73,8 @@ constexpr size_t CRC_ARENA_WORDS = 4u << 20;  // 16 MiB of contribution tables
 struct srsgpu_context {
   int                                  device      = 0;
   uint16_t*                            d_shifts[2] = {nullptr, nullptr};
+  core_plan*                           d_core[2]   = {nullptr, nullptr};
+  std::vector<core_plan>               core[2];
   uint32_t*                            d_crc_arena = nullptr;
   size_t                               crc_used    = 0;
   std::map<std::pair<int, int>, size_t> crc_tables;
@@ -83,6 +87,18 @@ struct srsgpu_pusch_cb_plan {
   dm_desc*                  d_dm    = nullptr;
   int                       nof_cbs = 0;
   srsgpu_ldpc_decoder_plan* dec     = nullptr;
+};
+
+struct srsgpu_pdsch_encoder_plan {
+  srsgpu_context* ctx        = nullptr;
+  tb_crc_desc*    d_tb       = nullptr;
+  uint32_t*       d_tb_crc   = nullptr;
+  int             nof_tbs    = 0;
+  enc_desc*       d_enc[2]   = {nullptr, nullptr};
+  int             count[2]   = {0, 0};
+  int             threads[2] = {64, 64};
+  size_t          out_begin  = 0;
+  size_t          out_end    = 0;
 };
 
 struct srsgpu_ldpc_decoder_plan {
@@ -137,6 +153,70 @@ int get_crc_table(srsgpu_context* ctx, int poly, int L, uint32_t& offset)
   return SRSGPU_OK;
 }
 
+/// Solves the core of the lifted base graph (rows 0..3 x parity columns K..K+3) once per (BG, Z), like
+/// ldpc_encoder_generic.cpp:226-:328 special-cases it per lifting set: P^x p0 = sum of the core syndromes, then every
+/// row with a single unknown parity node yields it.
+bool build_core_plan(int bg, int Z, core_plan& cp)
+{
+  const int             K   = (bg == 1) ? kBG1_K : kBG2_K;
+  const uint16_t*       rs  = (bg == 1) ? kBG1_ROW_START : kBG2_ROW_START;
+  const uint8_t*        col = (bg == 1) ? kBG1_COL : kBG2_COL;
+  const int             ils = kLiftingSetIndex[Z];
+  const uint16_t*       V   = (bg == 1) ? kBG1_V[ils] : kBG2_V[ils];
+  int                   sh[4][4];
+  for (int m = 0; m < 4; ++m) {
+    for (int j = 0; j < 4; ++j) {
+      sh[m][j] = -1;
+    }
+    for (int e = rs[m]; e < rs[m + 1]; ++e) {
+      if (col[e] >= K && col[e] < K + 4) {
+        sh[m][col[e] - K] = V[e] % Z;
+      }
+    }
+  }
+  std::vector<int> cnt(static_cast<size_t>(Z), 0);
+  for (int m = 0; m < 4; ++m) {
+    if (sh[m][0] >= 0) {
+      cnt[static_cast<size_t>(sh[m][0])] ^= 1;
+    }
+  }
+  int x = -1, nsurv = 0;
+  for (int s = 0; s < Z; ++s) {
+    if (cnt[static_cast<size_t>(s)]) {
+      x = s;
+      ++nsurv;
+    }
+  }
+  if (nsurv != 1) {
+    return false;
+  }
+  cp.x       = static_cast<int16_t>(x);
+  bool known[4] = {true, false, false, false};
+  int  step     = 0;
+  for (int round = 0; round < 4 && step < 3; ++round) {
+    for (int m = 0; m < 4 && step < 3; ++m) {
+      int u = -1, nunk = 0;
+      for (int j = 0; j < 4; ++j) {
+        if (sh[m][j] >= 0 && !known[j]) {
+          u = j;
+          ++nunk;
+        }
+      }
+      if (nunk != 1) {
+        continue;
+      }
+      cp.unk[step] = static_cast<int8_t>(u);
+      cp.row[step] = static_cast<int8_t>(m);
+      for (int j = 0; j < 4; ++j) {
+        cp.sh[step][j] = static_cast<int16_t>(sh[m][j]);
+      }
+      known[u] = true;
+      ++step;
+    }
+  }
+  return step == 3;
+}
+
 } // namespace
 
 extern "C" {
@@ -183,6 +263,21 @@ int srsgpu_context_create(int device, srsgpu_context** out)
       return fail(SRSGPU_ERR_HIP, "failed to upload LDPC shift tables");
     }
   }
+  for (int bg = 1; bg <= 2; ++bg) {
+    ctx->core[bg - 1].resize(51);
+    for (int p = 0; p < 51; ++p) {
+      if (!build_core_plan(bg, kLiftingSizes[p], ctx->core[bg - 1][static_cast<size_t>(p)])) {
+        srsgpu_context_destroy(ctx);
+        return fail(SRSGPU_ERR_INVALID_ARG, "cannot solve the LDPC core of BG%d Z=%d", bg, kLiftingSizes[p]);
+      }
+    }
+    if (hipMalloc(&ctx->d_core[bg - 1], 51 * sizeof(core_plan)) != hipSuccess ||
+        hipMemcpy(ctx->d_core[bg - 1], ctx->core[bg - 1].data(), 51 * sizeof(core_plan), hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      srsgpu_context_destroy(ctx);
+      return fail(SRSGPU_ERR_HIP, "failed to upload the LDPC core plans");
+    }
+  }
   if (hipMalloc(&ctx->d_crc_arena, CRC_ARENA_WORDS * sizeof(uint32_t)) != hipSuccess) {
     srsgpu_context_destroy(ctx);
     return fail(SRSGPU_ERR_NO_MEMORY, "failed to allocate the CRC table arena");
@@ -198,6 +293,11 @@ void srsgpu_context_destroy(srsgpu_context* ctx)
   }
   (void)hipSetDevice(ctx->device);
   for (auto* p : ctx->d_shifts) {
+    if (p != nullptr) {
+      (void)hipFree(p);
+    }
+  }
+  for (auto* p : ctx->d_core) {
     if (p != nullptr) {
       (void)hipFree(p);
     }
@@ -522,6 +622,167 @@ void srsgpu_pusch_cb_plan_destroy(srsgpu_pusch_cb_plan* plan)
     (void)hipFree(plan->d_dm);
   }
   srsgpu_ldpc_decoder_plan_destroy(plan->dec);
+  delete plan;
+}
+
+
+int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
+                                     const srsgpu_pdsch_tb_config* cfgs,
+                                     uint32_t                      nof_tbs,
+                                     srsgpu_pdsch_encoder_plan**   plan_out)
+{
+  if (ctx == nullptr || plan_out == nullptr || (cfgs == nullptr && nof_tbs > 0)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  std::lock_guard<std::mutex> lock(ctx->mtx);
+  HIP_TRY(hipSetDevice(ctx->device));
+  static const double      shift_bg1[4] = {0, 17, 33, 56};  // ldpc_rate_matcher_impl.cpp:34
+  static const double      shift_bg2[4] = {0, 13, 25, 43};
+  std::vector<tb_crc_desc> tbd(nof_tbs);
+  std::vector<enc_desc>    encs[2];
+  int                      maxz[2]   = {0, 0};
+  size_t                   out_begin = ~size_t(0), out_end = 0;
+  for (uint32_t t = 0; t < nof_tbs; ++t) {
+    const srsgpu_pdsch_tb_config& c = cfgs[t];
+    const int                     qm = c.modulation_order;
+    if (c.rv > 3 || (qm != 1 && qm != 2 && qm != 4 && qm != 6 && qm != 8) || c.cw_offset % 4 != 0) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tb %u: invalid rv, modulation order or unaligned codeword offset", t);
+    }
+    tb_segmentation seg;
+    std::string     err;
+    if (!sch_segment(static_cast<int>(c.tbs_bytes) * 8, c.base_graph, qm, c.nof_layers,
+                     static_cast<int>(c.nof_ch_symbols), seg, err)) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tb %u: %s", t, err.c_str());
+    }
+    tbd[t] = {c.tb_offset, c.tbs_bytes, seg.tb_crc_len == 24 ? 0x1864cfbu : 0x11021u,
+              static_cast<uint32_t>(seg.tb_crc_len)};
+    const int Z    = seg.Z;
+    const int pos  = lifting_position(Z);
+    const int N    = (((seg.bg == 1) ? kBG1_N_FULL : kBG2_N_FULL) - 2) * Z;
+    const int K    = (seg.bg == 1) ? kBG1_K : kBG2_K;
+    const int nsys = (K - 2) * Z;
+    const int Ncb  = (c.Nref > 0 && static_cast<int>(c.Nref) < N) ? static_cast<int>(c.Nref) : N;
+    if (Ncb <= nsys) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tb %u: circular buffer shorter than the systematic part", t);
+    }
+    const int ninfo = nsys - seg.filler;
+    const int k0    = static_cast<int>(std::floor(((seg.bg == 1 ? shift_bg1 : shift_bg2)[c.rv] * Ncb) / N)) * Z;
+    const int v0    = k0 < ninfo ? k0 : (k0 < nsys ? ninfo : k0 - seg.filler);
+    const int V     = Ncb - seg.filler;
+    uint32_t  crc_tab = NO_CRC_TABLE;
+    if (seg.cb_crc_len > 0) {
+      int r = get_crc_table(ctx, SRSGPU_CRC24B, seg.cbs[0].used, crc_tab);
+      if (r != SRSGPU_OK) {
+        return r;
+      }
+    }
+    for (int i = 0; i < seg.C; ++i) {
+      const cb_segment& cb = seg.cbs[static_cast<size_t>(i)];
+      enc_desc          d{};
+      d.tb_byte_offset = c.tb_offset;
+      d.tb_bit_offset  = static_cast<uint32_t>(cb.tb_offset);
+      d.tb_bits        = static_cast<uint32_t>(seg.tbs);
+      d.out_bit_offset = c.cw_offset * 8u + static_cast<uint32_t>(cb.cw_offset);
+      d.crc_table      = crc_tab;
+      d.div_magic      = static_cast<uint32_t>(((1ULL << 32) + static_cast<uint64_t>(Z) - 1) / static_cast<uint64_t>(Z));
+      d.E              = static_cast<uint32_t>(cb.E);
+      d.Ncb            = static_cast<uint32_t>(Ncb);
+      d.v0             = static_cast<uint32_t>(v0);
+      d.tb_index       = t;
+      d.Z              = static_cast<uint16_t>(Z);
+      d.zpos           = static_cast<uint16_t>(pos);
+      d.nof_data       = static_cast<uint16_t>(cb.nof_data);
+      d.used           = static_cast<uint16_t>(cb.used);
+      d.filler         = static_cast<uint16_t>(seg.filler);
+      d.tb_crc_len     = static_cast<uint8_t>(seg.tb_crc_len);
+      d.Qm             = static_cast<uint8_t>(qm);
+      // Last circular-buffer position the rate matcher reads -> extension parity rows to compute.
+      int kmax;
+      if (cb.E >= V - v0) {
+        kmax = Ncb - 1;
+      } else {
+        const int vend = v0 + cb.E - 1;
+        kmax           = vend < ninfo ? vend : vend + seg.filler;
+      }
+      const int last_col = (kmax + 2 * Z) / Z;  // full-codeblock node index
+      const int n_ext    = last_col - (K + 4) + 1;
+      d.n_ext            = static_cast<uint8_t>(n_ext < 0 ? 0 : n_ext);
+      encs[seg.bg - 1].push_back(d);
+    }
+    maxz[seg.bg - 1] = Z > maxz[seg.bg - 1] ? Z : maxz[seg.bg - 1];
+    out_begin        = std::min(out_begin, static_cast<size_t>(c.cw_offset));
+    out_end          = std::max(out_end, static_cast<size_t>(c.cw_offset) + (static_cast<size_t>(seg.cw_length) + 31) / 32 * 4);
+  }
+  auto* plan      = new srsgpu_pdsch_encoder_plan();
+  plan->ctx       = ctx;
+  plan->nof_tbs   = static_cast<int>(nof_tbs);
+  plan->out_begin = nof_tbs ? out_begin : 0;
+  plan->out_end   = out_end;
+  bool ok         = true;
+  if (nof_tbs > 0) {
+    ok = hipMalloc(&plan->d_tb, tbd.size() * sizeof(tb_crc_desc)) == hipSuccess &&
+         hipMemcpy(plan->d_tb, tbd.data(), tbd.size() * sizeof(tb_crc_desc), hipMemcpyHostToDevice) == hipSuccess &&
+         hipMalloc(&plan->d_tb_crc, tbd.size() * sizeof(uint32_t)) == hipSuccess;
+  }
+  for (int b = 0; b < 2 && ok; ++b) {
+    plan->count[b]   = static_cast<int>(encs[b].size());
+    plan->threads[b] = ((maxz[b] + 63) / 64) * 64;
+    if (plan->count[b] > 0) {
+      ok = hipMalloc(&plan->d_enc[b], encs[b].size() * sizeof(enc_desc)) == hipSuccess &&
+           hipMemcpy(plan->d_enc[b], encs[b].data(), encs[b].size() * sizeof(enc_desc), hipMemcpyHostToDevice) ==
+               hipSuccess;
+    }
+  }
+  if (!ok) {
+    srsgpu_pdsch_encoder_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload encoder descriptors");
+  }
+  *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+uint32_t srsgpu_pdsch_encoder_plan_nof_codeblocks(const srsgpu_pdsch_encoder_plan* plan)
+{
+  return plan == nullptr ? 0u : static_cast<uint32_t>(plan->count[0] + plan->count[1]);
+}
+
+int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
+                                      const uint8_t*                   d_tbs,
+                                      uint8_t*                         d_codewords,
+                                      void*                            stream)
+{
+  if (plan == nullptr || d_tbs == nullptr || d_codewords == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  auto s = static_cast<hipStream_t>(stream);
+  if (plan->out_end > plan->out_begin) {
+    HIP_TRY(hipMemsetAsync(d_codewords + plan->out_begin, 0, plan->out_end - plan->out_begin, s));
+  }
+  launch_tb_crc(plan->d_tb, plan->nof_tbs, d_tbs, plan->d_tb_crc, s);
+  HIP_TRY(hipGetLastError());
+  for (int b = 0; b < 2; ++b) {
+    if (plan->count[b] == 0) {
+      continue;
+    }
+    launch_pdsch_encode(b + 1, plan->d_enc[b], plan->count[b], plan->threads[b], d_tbs, plan->d_tb_crc,
+                        reinterpret_cast<uint32_t*>(d_codewords), plan->ctx->d_shifts[b], plan->ctx->d_core[b],
+                        plan->ctx->d_crc_arena, s);
+    HIP_TRY(hipGetLastError());
+  }
+  return SRSGPU_OK;
+}
+
+void srsgpu_pdsch_encoder_plan_destroy(srsgpu_pdsch_encoder_plan* plan)
+{
+  if (plan == nullptr) {
+    return;
+  }
+  for (void* p : {static_cast<void*>(plan->d_tb), static_cast<void*>(plan->d_tb_crc), static_cast<void*>(plan->d_enc[0]),
+                  static_cast<void*>(plan->d_enc[1])}) {
+    if (p != nullptr) {
+      (void)hipFree(p);
+    }
+  }
   delete plan;
 }
 

@@ -1,0 +1,336 @@
+// PDSCH channel encoding for 5G NR on gfx950: transport-block CRC, codeblock assembly with CB CRC24B, LDPC encoding
+// (TS 38.212 §5.3.2, BG1/BG2) and rate matching with bit interleaving (§5.4.2), batched over every codeblock of a slot.
+//
+// Drop-in semantics of srsran::pdsch_encoder_impl::encode (reference lib/phy/upper/channel_processors/pdsch/
+// pdsch_encoder_impl.cpp:28): ldpc_segmenter_tx_impl::read_codeblock (ldpc_segmenter_tx_impl.cpp:144), the LDPC
+// encoder (ldpc_encoder_generic.cpp) and ldpc_rate_matcher_impl::rate_match (ldpc_rate_matcher_impl.cpp:95). The
+// codeword is produced packed MSB first (the bit_buffer / hw_accelerator_pdsch_enc packed layout); the reference
+// unpacks it one bit per byte, which the host binding does for comparisons.
+//
+// Mapping to CDNA4: one workgroup per codeblock; the codeblock's bits live one per byte in LDS (column c at c * 384,
+// as in the decoder), lane z computes row z of every lifted parity equation; the rate-matched output is produced
+// 32 bits per lane and written as whole words (atomicOr only for the two words a codeblock shares with its
+// neighbours).
+#include "common.h"
+#include "ldpc_base_graphs.h"
+#include "srsgpu_internal.h"
+
+namespace srsgpu {
+namespace {
+
+template <int BG>
+struct ebg;
+template <>
+struct ebg<1> {
+  static constexpr int M  = kBG1_M;
+  static constexpr int NF = kBG1_N_FULL;
+  static constexpr int K  = kBG1_K;
+  static constexpr int NE = kBG1_NUM_EDGES;
+  static constexpr int rs(int m) { return kBG1_ROW_START[m]; }
+  static constexpr int col(int e) { return kBG1_COL[e]; }
+};
+template <>
+struct ebg<2> {
+  static constexpr int M  = kBG2_M;
+  static constexpr int NF = kBG2_N_FULL;
+  static constexpr int K  = kBG2_K;
+  static constexpr int NE = kBG2_NUM_EDGES;
+  static constexpr int rs(int m) { return kBG2_ROW_START[m]; }
+  static constexpr int col(int e) { return kBG2_COL[e]; }
+};
+
+constexpr int S = SOFT_COL_STRIDE;
+
+__device__ __forceinline__ int rot(int z, int s, int Z)
+{
+  const uint32_t p0 = static_cast<uint32_t>(z + s);
+  const uint32_t p1 = p0 - static_cast<uint32_t>(Z);
+  return static_cast<int>(p0 < p1 ? p0 : p1);
+}
+
+/// a(x) * b(x) mod g(x) over GF(2) for polynomials of degree < order.
+__device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b, uint32_t g, int order)
+{
+  const uint32_t high = 1u << order;
+  uint32_t       r    = 0;
+  for (int i = order - 1; i >= 0; --i) {
+    r <<= 1;
+    if (r & high) {
+      r ^= g;
+    }
+    if ((b >> i) & 1u) {
+      r ^= a;
+    }
+  }
+  return r;
+}
+
+/// CRC of every transport block (TS 38.212 §5.1, crc_calculator_generic_impl.cpp:64 calculate_byte): each lane
+/// computes the CRC of a contiguous chunk with a byte table, chunks are combined pairwise with
+/// CRC(A|B) = CRC(A) * x^(8|B|) + CRC(B) mod g. The message is conceptually front-padded with zero bytes to a multiple
+/// of the chunk size (leading zeros do not change a zero-initialised CRC).
+__global__ __launch_bounds__(256) void tb_crc_kernel(const tb_crc_desc* __restrict__ descs,
+                                                     const uint8_t* __restrict__ tbs,
+                                                     uint32_t* __restrict__ crcs)
+{
+  __shared__ uint32_t table[256];
+  __shared__ uint32_t part[256];
+  const tb_crc_desc d     = descs[blockIdx.x];
+  const int         order = d.order;
+  const uint32_t    g     = d.poly;
+  const uint32_t    mask  = (1u << order) - 1u;
+  {
+    // table[b] = b(x) * x^order mod g
+    uint32_t r = static_cast<uint32_t>(threadIdx.x) << (order - 8);
+    for (int k = 0; k < 8; ++k) {
+      r <<= 1;
+      if (r & (1u << order)) {
+        r ^= g;
+      }
+    }
+    table[threadIdx.x] = r & mask;
+  }
+  __syncthreads();
+  const int      n    = static_cast<int>(d.nbytes);
+  const int      cs   = (n + 255) / 256;
+  const int      pad  = cs * 256 - n;
+  const uint8_t* data = tbs + d.byte_offset;
+  uint32_t       rem  = 0;
+  for (int p = threadIdx.x * cs; p < (threadIdx.x + 1) * cs; ++p) {
+    const int i = p - pad;
+    if (i >= 0) {
+      rem = ((rem << 8) ^ table[((rem >> (order - 8)) ^ data[i]) & 0xffu]) & mask;
+    }
+  }
+  part[threadIdx.x] = rem;
+  __syncthreads();
+  // F = x^(8 cs) mod g, squared at every level of the pairwise combination.
+  uint32_t f = 1u;
+  {
+    // x^(8 cs) by square-and-multiply over the bits of 8 cs.
+    uint32_t       base = 2u;  // x
+    uint32_t       e    = 8u * static_cast<uint32_t>(cs);
+    while (e) {
+      if (e & 1u) {
+        f = gf2_mulmod(f, base, g, order);
+      }
+      base = gf2_mulmod(base, base, g, order);
+      e >>= 1;
+    }
+  }
+  for (int step = 1; step < 256; step <<= 1) {
+    if ((threadIdx.x % (2 * step)) == 0) {
+      part[threadIdx.x] = gf2_mulmod(part[threadIdx.x], f, g, order) ^ part[threadIdx.x + step];
+    }
+    f = gf2_mulmod(f, f, g, order);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    crcs[blockIdx.x] = part[0];
+  }
+}
+
+template <int BG, int QM>
+__device__ __forceinline__ void rate_match_words(const enc_desc& d, const uint8_t* __restrict__ bits, int Z,
+                                                 uint32_t* __restrict__ out_words)
+{
+  // Output bit t of the codeblock: symbol i = t / Qm, bit j = t % Qm carries e[j * R + i] (interleaver, :150);
+  // e[n] is the circular-buffer bit at valid position (v0 + n) mod V, fillers skipped (select_bits, :104).
+  const int      E = static_cast<int>(d.E), R = E / QM;
+  const int      V = static_cast<int>(d.Ncb) - d.filler;
+  const int      ninfo = (ebg<BG>::K - 2) * Z - d.filler;
+  const uint32_t g0    = d.out_bit_offset;
+  const uint32_t w0 = g0 / 32u, w1 = (g0 + static_cast<uint32_t>(E) - 1u) / 32u;
+  for (uint32_t w = w0 + threadIdx.x; w <= w1; w += blockDim.x) {
+    uint32_t word = 0;
+    bool     full = true;
+    for (int b = 0; b < 32; ++b) {
+      const int t = static_cast<int>(w * 32u + static_cast<uint32_t>(b) - g0);
+      if (t < 0 || t >= E) {
+        full = false;
+        continue;
+      }
+      const int i = t / QM, j = t - i * QM;
+      int       v = static_cast<int>(d.v0) + j * R + i;
+      while (v >= V) {
+        v -= V;
+      }
+      const int k   = (v < ninfo ? v : v + d.filler) + 2 * Z;  // shortened position -> full codeblock position
+      const int col = static_cast<int>(__umulhi(static_cast<uint32_t>(k), d.div_magic));
+      const int l   = k - col * Z;
+      // Byte (g / 8) of the packed stream, bit 7 - g % 8, inside a little-endian 32-bit word.
+      word |= static_cast<uint32_t>(bits[col * S + l]) << ((b & ~7) + 7 - (b & 7));
+    }
+    if (full) {
+      out_words[w] = word;
+    } else if (word != 0) {
+      atomicOr(&out_words[w], word);
+    }
+  }
+}
+
+template <int BG>
+__global__ __launch_bounds__(384) void pdsch_encode_kernel(const enc_desc* __restrict__ descs,
+                                                           const uint8_t* __restrict__ tbs,
+                                                           const uint32_t* __restrict__ tb_crcs,
+                                                           uint32_t* __restrict__ out_words,
+                                                           const uint16_t* __restrict__ shift_table,
+                                                           const core_plan* __restrict__ core_plans,
+                                                           const uint32_t* __restrict__ crc_tables)
+{
+  using G = ebg<BG>;
+  __shared__ __attribute__((aligned(16))) uint8_t bits[G::NF * S];
+  __shared__ uint8_t  lam[4 * S];
+  __shared__ uint16_t sh[G::NE];
+  __shared__ uint32_t red[8];
+
+  const enc_desc d  = descs[blockIdx.x];
+  const int      Z  = d.Z;
+  const int      K  = G::K;
+  const int      KZ = K * Z;
+  for (int e = threadIdx.x; e < G::NE; e += blockDim.x) {
+    sh[e] = shift_table[static_cast<uint32_t>(d.zpos) * G::NE + e];
+  }
+  // ---- Codeblock message (ldpc_segmenter_tx_impl.cpp:144): TB(+TB CRC) bits, zero padding, CB CRC, fillers. ----
+  const uint8_t* tb      = tbs + d.tb_byte_offset;
+  const uint32_t tb_crc  = tb_crcs[d.tb_index];
+  const int      ndata   = d.nof_data;
+  for (int i = threadIdx.x; i < KZ; i += blockDim.x) {
+    uint32_t bit = 0;
+    if (i < ndata) {
+      const uint32_t p = d.tb_bit_offset + static_cast<uint32_t>(i);
+      bit              = (p < d.tb_bits) ? (tb[p >> 3] >> (7u - (p & 7u))) & 1u
+                                         : (tb_crc >> (d.tb_crc_len - 1u - (p - d.tb_bits))) & 1u;
+    }
+    const int col = static_cast<int>(__umulhi(static_cast<uint32_t>(i), d.div_magic));
+    bits[col * S + (i - col * Z)] = static_cast<uint8_t>(bit);
+  }
+  __syncthreads();
+  // ---- Codeblock CRC24B over the first `used` bits: XOR of per-bit contributions (table per length). ----
+  if (d.crc_table != NO_CRC_TABLE) {
+    const uint32_t* P   = crc_tables + d.crc_table;
+    uint32_t        acc = 0;
+    for (int i = threadIdx.x; i < d.used; i += blockDim.x) {
+      const int col = static_cast<int>(__umulhi(static_cast<uint32_t>(i), d.div_magic));
+      acc ^= bits[col * S + (i - col * Z)] ? P[i] : 0u;
+    }
+    acc = wave_xor(acc);
+    if ((threadIdx.x % WAVE) == 0) {
+      red[threadIdx.x / WAVE] = acc;
+    }
+    __syncthreads();
+    uint32_t crc = 0;
+    for (int w = 0; w < static_cast<int>(blockDim.x / WAVE); ++w) {
+      crc ^= red[w];
+    }
+    for (int k = threadIdx.x; k < 24; k += blockDim.x) {
+      const int i   = d.used + k;
+      const int col = static_cast<int>(__umulhi(static_cast<uint32_t>(i), d.div_magic));
+      bits[col * S + (i - col * Z)] = static_cast<uint8_t>((crc >> (23 - k)) & 1u);
+    }
+    __syncthreads();
+  }
+  const int  z      = threadIdx.x;
+  const bool active = z < Z;
+  // ---- Core parity (rows 0..3, double-diagonal): lambda_m = sum of the rotated information nodes. ----
+  if (active) {
+    static_for<4>([&](auto Mi) {
+      constexpr int m  = decltype(Mi)::value;
+      constexpr int e0 = G::rs(m), deg = G::rs(m + 1) - e0;
+      uint32_t      acc = 0;
+      static_for<deg>([&](auto Ei) {
+        constexpr int e   = e0 + decltype(Ei)::value;
+        constexpr int col = G::col(e);
+        if constexpr (col < G::K) {
+          acc ^= bits[col * S + rot(z, sh[e], Z)];
+        }
+      });
+      lam[m * S + z] = static_cast<uint8_t>(acc);
+    });
+  }
+  __syncthreads();
+  const core_plan* __restrict__ cp = core_plans + d.zpos;
+  if (active) {
+    // P^x p0 = lambda_0 + lambda_1 + lambda_2 + lambda_3
+    bits[K * S + rot(z, cp->x, Z)] = lam[z] ^ lam[S + z] ^ lam[2 * S + z] ^ lam[3 * S + z];
+  }
+  __syncthreads();
+  for (int step = 0; step < 3; ++step) {
+    if (active) {
+      const int u   = cp->unk[step];
+      const int row = cp->row[step];
+      uint32_t  acc = lam[row * S + z];
+      for (int j = 0; j < 4; ++j) {
+        const int s = cp->sh[step][j];
+        if (j != u && s >= 0) {
+          acc ^= bits[(K + j) * S + rot(z, s, Z)];
+        }
+      }
+      bits[(K + u) * S + rot(z, cp->sh[step][u], Z)] = static_cast<uint8_t>(acc);
+    }
+    __syncthreads();
+  }
+  // ---- Extension parity (identity extension): p_{K+m} = sum over the row's nodes of the high-rate region. ----
+  if (active) {
+    const int n_ext = d.n_ext;
+    static_for<G::M - 4>([&](auto Mi) {
+      constexpr int m  = 4 + decltype(Mi)::value;
+      constexpr int e0 = G::rs(m), deg = G::rs(m + 1) - e0;
+      if (m - 4 < n_ext) {
+        uint32_t acc = 0;
+        static_for<deg>([&](auto Ei) {
+          constexpr int e   = e0 + decltype(Ei)::value;
+          constexpr int col = G::col(e);
+          if constexpr (col < G::K + 4) {
+            acc ^= bits[col * S + rot(z, sh[e], Z)];
+          }
+        });
+        bits[(K + m) * S + z] = static_cast<uint8_t>(acc);
+      }
+    });
+  }
+  __syncthreads();
+  // ---- Rate matching + interleaving + packing. ----
+  switch (d.Qm) {
+    case 1: rate_match_words<BG, 1>(d, bits, Z, out_words); break;
+    case 2: rate_match_words<BG, 2>(d, bits, Z, out_words); break;
+    case 4: rate_match_words<BG, 4>(d, bits, Z, out_words); break;
+    case 6: rate_match_words<BG, 6>(d, bits, Z, out_words); break;
+    default: rate_match_words<BG, 8>(d, bits, Z, out_words); break;
+  }
+}
+
+} // namespace
+
+void launch_tb_crc(const tb_crc_desc* d_desc, int nof_tbs, const uint8_t* d_tbs, uint32_t* d_crcs, hipStream_t s)
+{
+  if (nof_tbs > 0) {
+    tb_crc_kernel<<<nof_tbs, 256, 0, s>>>(d_desc, d_tbs, d_crcs);
+  }
+}
+
+void launch_pdsch_encode(int              bg,
+                         const enc_desc*  d_desc,
+                         int              nof_cbs,
+                         int              block_threads,
+                         const uint8_t*   d_tbs,
+                         const uint32_t*  d_tb_crcs,
+                         uint32_t*        d_out_words,
+                         const uint16_t*  d_shifts,
+                         const core_plan* d_core_plans,
+                         const uint32_t*  d_crc_tables,
+                         hipStream_t      s)
+{
+  if (nof_cbs <= 0) {
+    return;
+  }
+  if (bg == 1) {
+    pdsch_encode_kernel<1><<<nof_cbs, block_threads, 0, s>>>(d_desc, d_tbs, d_tb_crcs, d_out_words, d_shifts,
+                                                              d_core_plans, d_crc_tables);
+  } else {
+    pdsch_encode_kernel<2><<<nof_cbs, block_threads, 0, s>>>(d_desc, d_tbs, d_tb_crcs, d_out_words, d_shifts,
+                                                              d_core_plans, d_crc_tables);
+  }
+}
+
+} // namespace srsgpu

@@ -50,6 +50,61 @@ struct dm_desc {
 };
 static_assert(sizeof(dm_desc) == 36, "dm_desc layout");
 
+/// CRC job of one transport block (tb_crc_kernel).
+struct tb_crc_desc {
+  uint32_t byte_offset;  ///< First byte of the transport block.
+  uint32_t nbytes;       ///< Transport block size in bytes.
+  uint32_t poly;         ///< Generator polynomial including the x^order term (e.g. 0x1864cfb).
+  uint32_t order;        ///< 16 or 24.
+};
+
+/// How the double-diagonal core (rows 0..3, parity columns K..K+3) is solved for one (BG, Z): P^x p0 is the sum of
+/// the four row syndromes, then three rows each determine one more parity node.
+struct core_plan {
+  int16_t x;          ///< Shift of p0 that survives the sum of the core rows.
+  int8_t  unk[3];     ///< Parity node solved at each step.
+  int8_t  row[3];     ///< Core row used at each step.
+  int16_t sh[3][4];   ///< Shifts of the row's parity nodes at each step (-1: no edge).
+};
+
+/// Per-codeblock work item of the PDSCH encoder (pdsch_encode_kernel).
+struct enc_desc {
+  uint32_t tb_byte_offset;  ///< Transport block start (bytes).
+  uint32_t tb_bit_offset;   ///< First TB(+TB CRC) bit carried by the codeblock.
+  uint32_t tb_bits;         ///< TBS in bits: stream bits >= tb_bits come from the TB CRC.
+  uint32_t out_bit_offset;  ///< First bit of the codeblock in the packed codeword output.
+  uint32_t crc_table;       ///< CB CRC24B contribution table (NO_CRC_TABLE: single codeblock, no CB CRC).
+  uint32_t div_magic;       ///< ceil(2^32 / Z).
+  uint32_t E;               ///< Rate-matched length.
+  uint32_t Ncb;             ///< Circular buffer length.
+  uint32_t v0;              ///< Index of k0 among the non-filler positions.
+  uint32_t tb_index;        ///< Transport block (TB CRC slot).
+  uint16_t Z;
+  uint16_t zpos;
+  uint16_t nof_data;        ///< TB(+TB CRC) bits of the codeblock.
+  uint16_t used;            ///< Bits covered by the CB CRC.
+  uint16_t filler;
+  uint8_t  tb_crc_len;
+  uint8_t  Qm;
+  uint8_t  n_ext;           ///< Extension parity rows needed by the rate matcher.
+  uint8_t  pad[3];
+};
+static_assert(sizeof(enc_desc) == 56, "enc_desc layout");
+
+void launch_tb_crc(const tb_crc_desc* d_desc, int nof_tbs, const uint8_t* d_tbs, uint32_t* d_crcs, hipStream_t s);
+
+void launch_pdsch_encode(int              bg,
+                         const enc_desc*  d_desc,
+                         int              nof_cbs,
+                         int              block_threads,
+                         const uint8_t*   d_tbs,
+                         const uint32_t*  d_tb_crcs,
+                         uint32_t*        d_out_words,
+                         const uint16_t*  d_shifts,
+                         const core_plan* d_core_plans,
+                         const uint32_t*  d_crc_tables,
+                         hipStream_t      s);
+
 /// Launches the batched rate dematcher (rate_dematcher.hip). mode 0: generic combining, 1: SIMD combining.
 void launch_rate_dematch(int mode, const dm_desc* d_desc, int nof_cbs, const int8_t* d_llrs, int8_t* d_harq,
                          hipStream_t stream);

@@ -82,6 +82,24 @@ class PuschCbConfig(ctypes.Structure):
 
 assert ctypes.sizeof(PuschCbConfig) == 36
 
+
+class PdschTbConfig(ctypes.Structure):
+    """srsgpu_pdsch_tb_config (include/srsgpu_phy.h)."""
+    _fields_ = [
+        ("base_graph", ctypes.c_uint8),
+        ("rv", ctypes.c_uint8),
+        ("modulation_order", ctypes.c_uint8),
+        ("nof_layers", ctypes.c_uint8),
+        ("tbs_bytes", ctypes.c_uint32),
+        ("nof_ch_symbols", ctypes.c_uint32),
+        ("Nref", ctypes.c_uint32),
+        ("tb_offset", ctypes.c_uint32),
+        ("cw_offset", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(PdschTbConfig) == 24
+
 _lib = None
 
 
@@ -108,6 +126,12 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pusch_cb_plan_execute.argtypes = [P, P, P, P, P, P, P]
     lib.srsgpu_pusch_cb_plan_destroy.argtypes = [P]
     lib.srsgpu_pusch_cb_plan_destroy.restype = None
+    lib.srsgpu_pdsch_encoder_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(P)]
+    lib.srsgpu_pdsch_encoder_plan_nof_codeblocks.argtypes = [P]
+    lib.srsgpu_pdsch_encoder_plan_nof_codeblocks.restype = ctypes.c_uint32
+    lib.srsgpu_pdsch_encoder_plan_execute.argtypes = [P, P, P, P]
+    lib.srsgpu_pdsch_encoder_plan_destroy.argtypes = [P]
+    lib.srsgpu_pdsch_encoder_plan_destroy.restype = None
     _lib = lib
     return lib
 
@@ -117,7 +141,8 @@ EXPORTED_SYMBOLS = [
     "srsgpu_version", "srsgpu_last_error", "srsgpu_context_create", "srsgpu_context_destroy",
     "srsgpu_ldpc_decoder_plan_create", "srsgpu_ldpc_decoder_plan_execute", "srsgpu_ldpc_decoder_plan_destroy",
     "srsgpu_ldpc_decode", "srsgpu_pusch_cb_plan_create", "srsgpu_pusch_cb_plan_execute",
-    "srsgpu_pusch_cb_plan_destroy",
+    "srsgpu_pusch_cb_plan_destroy", "srsgpu_pdsch_encoder_plan_create", "srsgpu_pdsch_encoder_plan_nof_codeblocks",
+    "srsgpu_pdsch_encoder_plan_execute", "srsgpu_pdsch_encoder_plan_destroy",
 ]
 
 
@@ -381,3 +406,84 @@ class PuschCodeblockDecoder:
             res.append((None if iters[i] < 0 else int(iters[i]), unpack_bits(out[off:off + ob], nb)))
             off += ob
         return res, d_harq.cpu().numpy(), d_crc.cpu().numpy()
+
+
+@dataclass
+class PdschTransportBlock:
+    """pdsch_encoder::configuration (pdsch_encoder.h) of one transport block."""
+    base_graph: int
+    rv: int
+    modulation_order: int
+    nof_layers: int
+    nof_ch_symbols: int
+    Nref: int = 0
+
+
+def make_pdsch_configs(tbs_bytes: Sequence[int], tbs: Sequence[PdschTransportBlock]):
+    """Packs transport blocks with contiguous TB / codeword (word-aligned) offsets."""
+    arr = (PdschTbConfig * len(tbs))()
+    to = co = 0
+    cw_offsets = []
+    for i, (nb, t) in enumerate(zip(tbs_bytes, tbs)):
+        a = arr[i]
+        a.base_graph, a.rv, a.modulation_order, a.nof_layers = t.base_graph, t.rv, t.modulation_order, t.nof_layers
+        a.tbs_bytes, a.nof_ch_symbols, a.Nref, a.tb_offset, a.cw_offset = nb, t.nof_ch_symbols, t.Nref, to, co
+        cw_offsets.append(co)
+        to += nb
+        co += (t.nof_ch_symbols * t.modulation_order + 31) // 32 * 4
+    return arr, to, co, cw_offsets
+
+
+class PdschEncoderPlan:
+    """srsgpu_pdsch_encoder_plan: TB CRC + segmentation + CB CRC + LDPC + rate matching of a slot's TBs."""
+
+    def __init__(self, ctx: Context, cfg_array):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        _check(_lib.srsgpu_pdsch_encoder_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                     len(cfg_array), ctypes.byref(h)))
+        self.handle = h
+        self.nof_tbs = len(cfg_array)
+        self.nof_codeblocks = int(_lib.srsgpu_pdsch_encoder_plan_nof_codeblocks(h))
+
+    def execute(self, d_tbs, d_codewords, stream=None):
+        _check(_lib.srsgpu_pdsch_encoder_plan_execute(self.handle, _dptr(d_tbs), _dptr(d_codewords),
+                                                      _stream_handle(stream)))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.srsgpu_pdsch_encoder_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class PdschEncoder:
+    """GPU counterpart of srsran::pdsch_encoder (pdsch_encoder_impl.cpp:28); encode() returns the codeword unpacked
+    one bit per byte like the reference."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def encode_batch(self, tbs: Sequence[np.ndarray], cfgs: Sequence[PdschTransportBlock]):
+        arr, ntb, ncw, cw_offsets = make_pdsch_configs([t.size for t in tbs], cfgs)
+        dev = torch.device("cuda", self.ctx.device)
+        d_tbs = torch.from_numpy(np.concatenate([np.asarray(t, np.uint8) for t in tbs])).to(dev)
+        d_cw = torch.full((max(ncw, 4),), 0xAB, dtype=torch.uint8, device=dev)
+        plan = PdschEncoderPlan(self.ctx, arr)
+        plan.execute(d_tbs, d_cw)
+        torch.cuda.synchronize(dev)
+        plan.close()
+        cw = d_cw.cpu().numpy()
+        out = []
+        for off, c in zip(cw_offsets, cfgs):
+            G = c.nof_ch_symbols * c.modulation_order
+            out.append(np.unpackbits(cw[off: off + (G + 7) // 8])[:G])
+        return out
+
+    def encode(self, tb: np.ndarray, cfg: PdschTransportBlock) -> np.ndarray:
+        return self.encode_batch([tb], [cfg])[0]

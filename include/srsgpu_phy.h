@@ -194,6 +194,59 @@ int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
 
 void srsgpu_pdsch_encoder_plan_destroy(srsgpu_pdsch_encoder_plan* plan);
 
+/* ------------------------------------------------------------------------------------------------------------------
+ * PUSCH decoder (transport-block level) — replaces srsran::pusch_decoder (include/srsran/phy/upper/channel_processors/
+ * pusch/pusch_decoder.h; lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.cpp: new_data :98, segmentation
+ * :190, codeblock tasks :283, join_and_notify :386): segmentation, per-codeblock rate dematching + HARQ combining +
+ * LDPC decoding + CB CRC, codeblock concatenation and TB CRC24A check, for every transport block of a slot.
+ * The HARQ context lives in device memory owned by the caller: d_harq (C * N_short * Z LLRs per TB), d_cb_crc_ok (one
+ * flag per codeblock) and d_cb_msgs (SRSGPU_CB_MSG_STRIDE bytes of decoded message per codeblock).
+ * ------------------------------------------------------------------------------------------------------------------ */
+#define SRSGPU_CB_MSG_STRIDE 1056u /* bytes per codeblock message slot (22 * 384 bits) */
+
+typedef struct {
+  uint8_t  base_graph;       /* 1 or 2 */
+  uint8_t  rv;               /* 0..3 */
+  uint8_t  modulation_order; /* Qm */
+  uint8_t  nof_layers;       /* 1..4 */
+  uint8_t  new_data;         /* 1: new transmission (resets the TB's CB CRC flags) */
+  uint8_t  use_early_stop;   /* LDPC early stop with the codeblock CRC */
+  uint8_t  max_iterations;   /* nof_ldpc_iterations (> 0) */
+  uint8_t  reserved;
+  float    scaling_factor;   /* normalised min-sum factor in (0, 1) */
+  uint32_t tbs_bytes;        /* transport block size in bytes */
+  uint32_t nof_ch_symbols;   /* G / Qm */
+  uint32_t Nref;             /* limited-buffer rate matching N_ref, 0 = none */
+  uint32_t llr_offset;       /* first of the G codeword LLRs */
+  uint32_t harq_offset;      /* first LLR of the TB's HARQ soft buffer */
+  uint32_t cb_offset;        /* index of the TB's first codeblock (CRC flags, messages, iteration counts) */
+  uint32_t tb_offset;        /* byte offset of the decoded transport block */
+} srsgpu_pusch_tb_config;
+
+typedef struct srsgpu_pusch_decoder_plan srsgpu_pusch_decoder_plan;
+
+int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
+                                     int                           impl,
+                                     const srsgpu_pusch_tb_config* cfgs,
+                                     uint32_t                      nof_tbs,
+                                     srsgpu_pusch_decoder_plan**   plan);
+
+uint32_t srsgpu_pusch_decoder_plan_nof_codeblocks(const srsgpu_pusch_decoder_plan* plan);
+
+/** Decodes the planned transport blocks. d_tb_crc_ok[t] = 1 when the TB CRC passed (pusch_decoder_result
+ *  tb_crc_ok); d_cb_nof_iterations[c] as in srsgpu_pusch_cb_plan_execute. Asynchronous, hipGraph-capturable. */
+int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
+                                      const int8_t*                    d_llrs,
+                                      int8_t*                          d_harq,
+                                      uint8_t*                         d_cb_crc_ok,
+                                      uint8_t*                         d_cb_msgs,
+                                      int32_t*                         d_cb_nof_iterations,
+                                      uint8_t*                         d_tbs,
+                                      uint8_t*                         d_tb_crc_ok,
+                                      void*                            stream);
+
+void srsgpu_pusch_decoder_plan_destroy(srsgpu_pusch_decoder_plan* plan);
+
 #ifdef __cplusplus
 }
 #endif

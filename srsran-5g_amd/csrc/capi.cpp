@@ -101,6 +101,13 @@ struct srsgpu_pdsch_encoder_plan {
   size_t          out_end    = 0;
 };
 
+struct srsgpu_pusch_decoder_plan {
+  srsgpu_context*       ctx     = nullptr;
+  srsgpu_pusch_cb_plan* cbs     = nullptr;
+  tb_dec_desc*          d_tb    = nullptr;
+  int                   nof_tbs = 0;
+};
+
 struct srsgpu_ldpc_decoder_plan {
   srsgpu_context* ctx            = nullptr;
   int             impl           = SRSGPU_LDPC_IMPL_SIMD;
@@ -426,6 +433,108 @@ int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
   return SRSGPU_OK;
 }
 
+struct pusch_cb_params {
+  int      bg, rv, qm, crc_poly, Z, filler, nof_crc_bits, max_iter;
+  bool     new_data, early_stop;
+  float    sf;
+  uint32_t Nref, E, llr_offset, harq_offset, out_offset, cb_index;
+};
+
+/// Validates one PUSCH codeblock (ldpc_rate_dematcher_impl.cpp:54-:99 plus the decoder's checks) and appends its
+/// dematcher and decoder descriptors.
+int add_pusch_cb(srsgpu_context*        ctx,
+                 uint32_t               i,
+                 const pusch_cb_params& c,
+                 dec_batch&             batch,
+                 std::vector<dm_desc>&  dms)
+{
+  static const double shift_bg1[4] = {0, 17, 33, 56};  // ldpc_rate_dematcher_impl.cpp:33
+  static const double shift_bg2[4] = {0, 13, 25, 43};
+  const int           Z            = c.Z;
+  if ((c.bg != 1 && c.bg != 2) || lifting_position(Z) < 0) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid base graph %d / lifting size %d", i, c.bg, Z);
+  }
+  const int K    = (c.bg == 1) ? kBG1_K : kBG2_K;
+  const int N    = (((c.bg == 1) ? kBG1_N_FULL : kBG2_N_FULL) - 2) * Z;
+  const int nsys = (K - 2) * Z;
+  const int qm   = c.qm;
+  if (c.rv < 0 || c.rv > 3) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: RV should an integer between 0 and 3", i);
+  }
+  if (qm != 1 && qm != 2 && qm != 4 && qm != 6 && qm != 8) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid modulation order %d", i, qm);
+  }
+  if (c.E == 0 || c.E % static_cast<uint32_t>(qm) != 0 || c.E > 22u * 384u * 35u) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid rate-matched length %u", i, c.E);
+  }
+  if (c.Nref > 66u * 384u) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: N_ref %u must be smaller or equal to %u", i, c.Nref, 66u * 384u);
+  }
+  if (c.filler < 0 || c.filler >= nsys) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid number of filler bits", i);
+  }
+  const int Ncb = (c.Nref > 0 && static_cast<int>(c.Nref) < N) ? static_cast<int>(c.Nref) : N;
+  if (Ncb <= nsys) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: circular buffer %d shorter than the systematic part", i, Ncb);
+  }
+  const double sf    = (c.bg == 1 ? shift_bg1 : shift_bg2)[c.rv];
+  const int    k0    = static_cast<int>(std::floor((sf * Ncb) / N)) * Z;
+  const int    ninfo = nsys - c.filler;
+  dm_desc      d{};
+  d.llr_offset  = c.llr_offset;
+  d.harq_offset = c.harq_offset;
+  d.E           = c.E;
+  d.N           = static_cast<uint32_t>(N);
+  d.Ncb         = static_cast<uint32_t>(Ncb);
+  d.nsys        = static_cast<uint32_t>(nsys);
+  d.v0          = static_cast<uint32_t>(k0 < ninfo ? k0 : (k0 < nsys ? ninfo : k0 - c.filler));
+  d.nof_filler  = static_cast<uint16_t>(c.filler);
+  d.Qm          = static_cast<uint8_t>(qm);
+  d.new_data    = c.new_data ? 1 : 0;
+  d.cb_index    = c.cb_index;
+  dms.push_back(d);
+  return add_decoder_cb(ctx, c.cb_index, c.bg, Z, c.filler, c.nof_crc_bits, c.max_iter, c.sf, c.crc_poly,
+                        c.early_stop, c.harq_offset, static_cast<uint32_t>(N), c.out_offset, batch);
+}
+
+int upload_pusch_cb_plan(srsgpu_context*             ctx,
+                         int                         impl,
+                         const dec_batch&            batch,
+                         const std::vector<dm_desc>& dms,
+                         srsgpu_pusch_cb_plan**      plan_out)
+{
+  auto* plan    = new srsgpu_pusch_cb_plan();
+  plan->ctx     = ctx;
+  plan->impl    = impl;
+  plan->nof_cbs = static_cast<int>(dms.size());
+  int r         = upload_decoder_plan(ctx, impl, batch, &plan->dec);
+  if (r != SRSGPU_OK) {
+    delete plan;
+    return r;
+  }
+  if (!dms.empty() && (hipMalloc(&plan->d_dm, dms.size() * sizeof(dm_desc)) != hipSuccess ||
+                       hipMemcpy(plan->d_dm, dms.data(), dms.size() * sizeof(dm_desc), hipMemcpyHostToDevice) !=
+                           hipSuccess)) {
+    srsgpu_pusch_cb_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload rate dematcher descriptors");
+  }
+  *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+int execute_pusch_cb_plan(const srsgpu_pusch_cb_plan* plan,
+                          const int8_t*               d_llrs,
+                          int8_t*                     d_harq,
+                          uint8_t*                    d_out,
+                          int32_t*                    d_nof_iterations,
+                          uint8_t*                    d_cb_crc_ok,
+                          hipStream_t                 s)
+{
+  launch_rate_dematch(plan->impl, plan->d_dm, plan->nof_cbs, d_llrs, d_harq, d_cb_crc_ok, s);
+  HIP_TRY(hipGetLastError());
+  return execute_decoder_plan(plan->dec, d_harq, d_out, d_nof_iterations, d_cb_crc_ok, s);
+}
+
 } // namespace
 
 extern "C" {
@@ -522,78 +631,19 @@ int srsgpu_pusch_cb_plan_create(srsgpu_context*               ctx,
   }
   std::lock_guard<std::mutex> lock(ctx->mtx);
   HIP_TRY(hipSetDevice(ctx->device));
-  static const double   shift_bg1[4] = {0, 17, 33, 56};  // ldpc_rate_dematcher_impl.cpp:33
-  static const double   shift_bg2[4] = {0, 13, 25, 43};
-  dec_batch             batch;
-  std::vector<dm_desc>  dms(nof_cbs);
+  dec_batch            batch;
+  std::vector<dm_desc> dms;
   for (uint32_t i = 0; i < nof_cbs; ++i) {
     const srsgpu_pusch_cb_config& c = cfgs[i];
-    const int                     Z = c.lifting_size;
-    if ((c.base_graph != 1 && c.base_graph != 2) || lifting_position(Z) < 0) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid base graph %d / lifting size %d", i, c.base_graph, Z);
-    }
-    const int K    = (c.base_graph == 1) ? kBG1_K : kBG2_K;
-    const int N    = (((c.base_graph == 1) ? kBG1_N_FULL : kBG2_N_FULL) - 2) * Z;
-    const int nsys = (K - 2) * Z;
-    const int qm   = c.modulation_order;
-    if (c.rv > 3) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: RV should an integer between 0 and 3", i);
-    }
-    if (qm != 1 && qm != 2 && qm != 4 && qm != 6 && qm != 8) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid modulation order %d", i, qm);
-    }
-    if (c.rm_length == 0 || c.rm_length % qm != 0 || c.rm_length > 22u * 384u * 35u) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid rate-matched length %u", i, c.rm_length);
-    }
-    if (c.Nref > 66u * 384u) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: N_ref %u must be smaller or equal to %u", i, c.Nref, 66u * 384u);
-    }
-    if (c.nof_filler_bits >= nsys) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid number of filler bits", i);
-    }
-    const int Ncb = (c.Nref > 0 && static_cast<int>(c.Nref) < N) ? static_cast<int>(c.Nref) : N;
-    if (Ncb <= nsys) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: circular buffer %d shorter than the systematic part", i, Ncb);
-    }
-    const double   sf    = (c.base_graph == 1 ? shift_bg1 : shift_bg2)[c.rv];
-    const int      k0    = static_cast<int>(std::floor((sf * Ncb) / N)) * Z;
-    const int      ninfo = nsys - c.nof_filler_bits;
-    dm_desc&       d     = dms[i];
-    d.llr_offset         = c.llr_offset;
-    d.harq_offset        = c.harq_offset;
-    d.E                  = c.rm_length;
-    d.N                  = static_cast<uint32_t>(N);
-    d.Ncb                = static_cast<uint32_t>(Ncb);
-    d.nsys               = static_cast<uint32_t>(nsys);
-    d.v0                 = static_cast<uint32_t>(k0 < ninfo ? k0 : (k0 < nsys ? ninfo : k0 - c.nof_filler_bits));
-    d.nof_filler         = c.nof_filler_bits;
-    d.Qm                 = static_cast<uint8_t>(qm);
-    d.new_data           = c.new_data ? 1 : 0;
-    d.skip               = 0;
-    int r = add_decoder_cb(ctx, i, c.base_graph, Z, c.nof_filler_bits, c.nof_crc_bits, c.max_iterations,
-                           c.scaling_factor, c.crc_poly, c.use_early_stop != 0, c.harq_offset,
-                           static_cast<uint32_t>(N), c.out_offset, batch);
+    pusch_cb_params p{c.base_graph, c.rv, c.modulation_order, c.crc_poly, c.lifting_size, c.nof_filler_bits,
+                      c.nof_crc_bits, c.max_iterations, c.new_data != 0, c.use_early_stop != 0, c.scaling_factor,
+                      c.Nref, c.rm_length, c.llr_offset, c.harq_offset, c.out_offset, i};
+    int r = add_pusch_cb(ctx, i, p, batch, dms);
     if (r != SRSGPU_OK) {
       return r;
     }
   }
-  auto* plan    = new srsgpu_pusch_cb_plan();
-  plan->ctx     = ctx;
-  plan->impl    = impl;
-  plan->nof_cbs = static_cast<int>(nof_cbs);
-  int r         = upload_decoder_plan(ctx, impl, batch, &plan->dec);
-  if (r != SRSGPU_OK) {
-    delete plan;
-    return r;
-  }
-  if (nof_cbs > 0 && (hipMalloc(&plan->d_dm, dms.size() * sizeof(dm_desc)) != hipSuccess ||
-                      hipMemcpy(plan->d_dm, dms.data(), dms.size() * sizeof(dm_desc), hipMemcpyHostToDevice) !=
-                          hipSuccess)) {
-    srsgpu_pusch_cb_plan_destroy(plan);
-    return fail(SRSGPU_ERR_HIP, "failed to upload rate dematcher descriptors");
-  }
-  *plan_out = plan;
-  return SRSGPU_OK;
+  return upload_pusch_cb_plan(ctx, impl, batch, dms, plan_out);
 }
 
 int srsgpu_pusch_cb_plan_execute(const srsgpu_pusch_cb_plan* plan,
@@ -607,10 +657,8 @@ int srsgpu_pusch_cb_plan_execute(const srsgpu_pusch_cb_plan* plan,
   if (plan == nullptr || d_llrs == nullptr || d_harq == nullptr || d_out == nullptr || d_nof_iterations == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  auto s = static_cast<hipStream_t>(stream);
-  launch_rate_dematch(plan->impl, plan->d_dm, plan->nof_cbs, d_llrs, d_harq, s);
-  HIP_TRY(hipGetLastError());
-  return execute_decoder_plan(plan->dec, d_harq, d_out, d_nof_iterations, d_cb_crc_ok, s);
+  return execute_pusch_cb_plan(plan, d_llrs, d_harq, d_out, d_nof_iterations, d_cb_crc_ok,
+                               static_cast<hipStream_t>(stream));
 }
 
 void srsgpu_pusch_cb_plan_destroy(srsgpu_pusch_cb_plan* plan)
@@ -782,6 +830,116 @@ void srsgpu_pdsch_encoder_plan_destroy(srsgpu_pdsch_encoder_plan* plan)
     if (p != nullptr) {
       (void)hipFree(p);
     }
+  }
+  delete plan;
+}
+
+
+int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
+                                     int                           impl,
+                                     const srsgpu_pusch_tb_config* cfgs,
+                                     uint32_t                      nof_tbs,
+                                     srsgpu_pusch_decoder_plan**   plan_out)
+{
+  if (ctx == nullptr || plan_out == nullptr || (cfgs == nullptr && nof_tbs > 0)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  if (impl != SRSGPU_LDPC_IMPL_GENERIC && impl != SRSGPU_LDPC_IMPL_SIMD) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "invalid implementation %d", impl);
+  }
+  std::lock_guard<std::mutex> lock(ctx->mtx);
+  HIP_TRY(hipSetDevice(ctx->device));
+  dec_batch                batch;
+  std::vector<dm_desc>     dms;
+  std::vector<tb_dec_desc> tbs(nof_tbs);
+  for (uint32_t t = 0; t < nof_tbs; ++t) {
+    const srsgpu_pusch_tb_config& c = cfgs[t];
+    tb_segmentation               seg;
+    std::string                   err;
+    if (!sch_segment(static_cast<int>(c.tbs_bytes) * 8, c.base_graph, c.modulation_order, c.nof_layers,
+                     static_cast<int>(c.nof_ch_symbols), seg, err)) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tb %u: %s", t, err.c_str());
+    }
+    // pusch_decoder_impl.cpp:34 select_crc: CRC24B when segmented, else the TB CRC.
+    const int crc_poly = (seg.C > 1) ? SRSGPU_CRC24B : (seg.tbs > 3824 ? SRSGPU_CRC24A : SRSGPU_CRC16);
+    const int N        = (((seg.bg == 1) ? kBG1_N_FULL : kBG2_N_FULL) - 2) * seg.Z;
+    for (int i = 0; i < seg.C; ++i) {
+      const cb_segment& cb = seg.cbs[static_cast<size_t>(i)];
+      const uint32_t    ci = c.cb_offset + static_cast<uint32_t>(i);
+      pusch_cb_params   p{seg.bg, c.rv, c.modulation_order, crc_poly, seg.Z, seg.filler,
+                        seg.C > 1 ? 24 : seg.tb_crc_len, c.max_iterations, c.new_data != 0, c.use_early_stop != 0,
+                        c.scaling_factor, c.Nref, static_cast<uint32_t>(cb.E),
+                        c.llr_offset + static_cast<uint32_t>(cb.cw_offset),
+                        c.harq_offset + static_cast<uint32_t>(i) * static_cast<uint32_t>(N), ci * CB_MSG_STRIDE, ci};
+      int r = add_pusch_cb(ctx, ci, p, batch, dms);
+      if (r != SRSGPU_OK) {
+        return r;
+      }
+    }
+    tb_dec_desc& d = tbs[t];
+    d.first_cb     = c.cb_offset;
+    d.nof_cbs      = static_cast<uint32_t>(seg.C);
+    d.tbs_bits     = static_cast<uint32_t>(seg.tbs);
+    d.cb_data_bits = static_cast<uint32_t>(seg.C > 1 ? seg.cbs[0].used : seg.tbs);
+    d.data_magic   = static_cast<uint32_t>(((1ULL << 32) + d.cb_data_bits - 1) / d.cb_data_bits);
+    d.tb_offset    = c.tb_offset;
+    d.tb_index     = t;
+  }
+  auto* plan    = new srsgpu_pusch_decoder_plan();
+  plan->ctx     = ctx;
+  plan->nof_tbs = static_cast<int>(nof_tbs);
+  int r         = upload_pusch_cb_plan(ctx, impl, batch, dms, &plan->cbs);
+  if (r != SRSGPU_OK) {
+    delete plan;
+    return r;
+  }
+  if (nof_tbs > 0 && (hipMalloc(&plan->d_tb, tbs.size() * sizeof(tb_dec_desc)) != hipSuccess ||
+                      hipMemcpy(plan->d_tb, tbs.data(), tbs.size() * sizeof(tb_dec_desc), hipMemcpyHostToDevice) !=
+                          hipSuccess)) {
+    srsgpu_pusch_decoder_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload transport block descriptors");
+  }
+  *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+uint32_t srsgpu_pusch_decoder_plan_nof_codeblocks(const srsgpu_pusch_decoder_plan* plan)
+{
+  return plan == nullptr ? 0u : static_cast<uint32_t>(plan->cbs->nof_cbs);
+}
+
+int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
+                                      const int8_t*                    d_llrs,
+                                      int8_t*                          d_harq,
+                                      uint8_t*                         d_cb_crc_ok,
+                                      uint8_t*                         d_cb_msgs,
+                                      int32_t*                         d_cb_nof_iterations,
+                                      uint8_t*                         d_tbs,
+                                      uint8_t*                         d_tb_crc_ok,
+                                      void*                            stream)
+{
+  if (plan == nullptr || d_llrs == nullptr || d_harq == nullptr || d_cb_crc_ok == nullptr || d_cb_msgs == nullptr ||
+      d_cb_nof_iterations == nullptr || d_tbs == nullptr || d_tb_crc_ok == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  auto s = static_cast<hipStream_t>(stream);
+  int  r = execute_pusch_cb_plan(plan->cbs, d_llrs, d_harq, d_cb_msgs, d_cb_nof_iterations, d_cb_crc_ok, s);
+  if (r != SRSGPU_OK) {
+    return r;
+  }
+  launch_pusch_tb(plan->d_tb, plan->nof_tbs, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, s);
+  HIP_TRY(hipGetLastError());
+  return SRSGPU_OK;
+}
+
+void srsgpu_pusch_decoder_plan_destroy(srsgpu_pusch_decoder_plan* plan)
+{
+  if (plan == nullptr) {
+    return;
+  }
+  srsgpu_pusch_cb_plan_destroy(plan->cbs);
+  if (plan->d_tb != nullptr) {
+    (void)hipFree(plan->d_tb);
   }
   delete plan;
 }

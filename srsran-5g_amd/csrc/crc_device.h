@@ -1,0 +1,80 @@
+// Block-wide CRC of a byte string on gfx950 (TS 38.212 §5.1, crc_calculator_generic_impl.cpp:64 calculate_byte:
+// zero initial remainder, MSB first). Each of the 256 lanes computes the CRC of a contiguous chunk with a byte table,
+// then chunks are combined pairwise: CRC(A|B) = CRC(A) * x^(8|B|) + CRC(B) mod g. The message is conceptually
+// front-padded with zero bytes to a multiple of the chunk size (leading zeros do not change a zero-initialised CRC).
+#pragma once
+
+#include "common.h"
+
+namespace srsgpu {
+
+/// a(x) * b(x) mod g(x) over GF(2) for polynomials of degree < order (g includes the x^order term).
+__device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b, uint32_t g, int order)
+{
+  const uint32_t high = 1u << order;
+  uint32_t       r    = 0;
+  for (int i = order - 1; i >= 0; --i) {
+    r <<= 1;
+    if (r & high) {
+      r ^= g;
+    }
+    if ((b >> i) & 1u) {
+      r ^= a;
+    }
+  }
+  return r;
+}
+
+/// CRC (order 8..24, g including x^order) of data[0..n) computed by a 256-lane workgroup. `table` and `part` are
+/// 256-entry LDS scratch arrays. Returns the CRC in every lane. Must be called by all 256 lanes.
+__device__ inline uint32_t block_crc_bytes(const uint8_t* data, int n, int order, uint32_t g, uint32_t* table,
+                                           uint32_t* part)
+{
+  const uint32_t mask = (1u << order) - 1u;
+  {
+    uint32_t r = static_cast<uint32_t>(threadIdx.x) << (order - 8);
+    for (int k = 0; k < 8; ++k) {
+      r <<= 1;
+      if (r & (1u << order)) {
+        r ^= g;
+      }
+    }
+    table[threadIdx.x] = r & mask;
+  }
+  __syncthreads();
+  const int cs  = (n + 255) / 256;
+  const int pad = cs * 256 - n;
+  uint32_t  rem = 0;
+  for (int p = threadIdx.x * cs; p < (threadIdx.x + 1) * cs; ++p) {
+    const int i = p - pad;
+    if (i >= 0) {
+      rem = ((rem << 8) ^ table[((rem >> (order - 8)) ^ data[i]) & 0xffu]) & mask;
+    }
+  }
+  part[threadIdx.x] = rem;
+  __syncthreads();
+  uint32_t f = 1u;  // x^(8 cs) mod g by square-and-multiply
+  {
+    uint32_t base = 2u;
+    uint32_t e    = 8u * static_cast<uint32_t>(cs);
+    while (e) {
+      if (e & 1u) {
+        f = gf2_mulmod(f, base, g, order);
+      }
+      base = gf2_mulmod(base, base, g, order);
+      e >>= 1;
+    }
+  }
+  for (int step = 1; step < 256; step <<= 1) {
+    if ((threadIdx.x % (2 * step)) == 0) {
+      part[threadIdx.x] = gf2_mulmod(part[threadIdx.x], f, g, order) ^ part[threadIdx.x + step];
+    }
+    f = gf2_mulmod(f, f, g, order);
+    __syncthreads();
+  }
+  const uint32_t crc = part[0];
+  __syncthreads();
+  return crc;
+}
+
+} // namespace srsgpu

@@ -12,6 +12,7 @@
 // 32 bits per lane and written as whole words (atomicOr only for the two words a codeblock shares with its
 // neighbours).
 #include "common.h"
+#include "crc_device.h"
 #include "ldpc_base_graphs.h"
 #include "srsgpu_internal.h"
 
@@ -48,85 +49,18 @@ __device__ __forceinline__ int rot(int z, int s, int Z)
   return static_cast<int>(p0 < p1 ? p0 : p1);
 }
 
-/// a(x) * b(x) mod g(x) over GF(2) for polynomials of degree < order.
-__device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b, uint32_t g, int order)
-{
-  const uint32_t high = 1u << order;
-  uint32_t       r    = 0;
-  for (int i = order - 1; i >= 0; --i) {
-    r <<= 1;
-    if (r & high) {
-      r ^= g;
-    }
-    if ((b >> i) & 1u) {
-      r ^= a;
-    }
-  }
-  return r;
-}
-
-/// CRC of every transport block (TS 38.212 §5.1, crc_calculator_generic_impl.cpp:64 calculate_byte): each lane
-/// computes the CRC of a contiguous chunk with a byte table, chunks are combined pairwise with
-/// CRC(A|B) = CRC(A) * x^(8|B|) + CRC(B) mod g. The message is conceptually front-padded with zero bytes to a multiple
-/// of the chunk size (leading zeros do not change a zero-initialised CRC).
+/// CRC of every transport block (TS 38.212 §5.1): one 256-lane workgroup per transport block (crc_device.h).
 __global__ __launch_bounds__(256) void tb_crc_kernel(const tb_crc_desc* __restrict__ descs,
                                                      const uint8_t* __restrict__ tbs,
                                                      uint32_t* __restrict__ crcs)
 {
   __shared__ uint32_t table[256];
   __shared__ uint32_t part[256];
-  const tb_crc_desc d     = descs[blockIdx.x];
-  const int         order = d.order;
-  const uint32_t    g     = d.poly;
-  const uint32_t    mask  = (1u << order) - 1u;
-  {
-    // table[b] = b(x) * x^order mod g
-    uint32_t r = static_cast<uint32_t>(threadIdx.x) << (order - 8);
-    for (int k = 0; k < 8; ++k) {
-      r <<= 1;
-      if (r & (1u << order)) {
-        r ^= g;
-      }
-    }
-    table[threadIdx.x] = r & mask;
-  }
-  __syncthreads();
-  const int      n    = static_cast<int>(d.nbytes);
-  const int      cs   = (n + 255) / 256;
-  const int      pad  = cs * 256 - n;
-  const uint8_t* data = tbs + d.byte_offset;
-  uint32_t       rem  = 0;
-  for (int p = threadIdx.x * cs; p < (threadIdx.x + 1) * cs; ++p) {
-    const int i = p - pad;
-    if (i >= 0) {
-      rem = ((rem << 8) ^ table[((rem >> (order - 8)) ^ data[i]) & 0xffu]) & mask;
-    }
-  }
-  part[threadIdx.x] = rem;
-  __syncthreads();
-  // F = x^(8 cs) mod g, squared at every level of the pairwise combination.
-  uint32_t f = 1u;
-  {
-    // x^(8 cs) by square-and-multiply over the bits of 8 cs.
-    uint32_t       base = 2u;  // x
-    uint32_t       e    = 8u * static_cast<uint32_t>(cs);
-    while (e) {
-      if (e & 1u) {
-        f = gf2_mulmod(f, base, g, order);
-      }
-      base = gf2_mulmod(base, base, g, order);
-      e >>= 1;
-    }
-  }
-  for (int step = 1; step < 256; step <<= 1) {
-    if ((threadIdx.x % (2 * step)) == 0) {
-      part[threadIdx.x] = gf2_mulmod(part[threadIdx.x], f, g, order) ^ part[threadIdx.x + step];
-    }
-    f = gf2_mulmod(f, f, g, order);
-    __syncthreads();
-  }
+  const tb_crc_desc d   = descs[blockIdx.x];
+  const uint32_t    crc = block_crc_bytes(tbs + d.byte_offset, static_cast<int>(d.nbytes), static_cast<int>(d.order),
+                                          d.poly, table, part);
   if (threadIdx.x == 0) {
-    crcs[blockIdx.x] = part[0];
+    crcs[blockIdx.x] = crc;
   }
 }
 

@@ -1,0 +1,101 @@
+// Transport-block stage of the PUSCH decoder on gfx950: concatenation of the decoded codeblocks into the transport
+// block and the TB CRC24A check, with the reference's HARQ bookkeeping.
+//
+// Drop-in semantics of pusch_decoder_impl::join_and_notify / concatenate_codeblocks (reference
+// lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.cpp:386 and :438): with one codeblock the TB CRC is the
+// codeblock CRC and the TB is copied only when it passed; with several codeblocks the TB is assembled (each codeblock
+// contributes min(free TB bits, data bits), the last one also carries the 24-bit TB checksum) only when every codeblock
+// CRC passed, then CRC24A(TB) is compared with the checksum; a mismatch resets every codeblock CRC flag (:423).
+#include "common.h"
+#include "crc_device.h"
+#include "srsgpu_internal.h"
+
+namespace srsgpu {
+namespace {
+
+__global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __restrict__ descs,
+                                                       uint8_t* __restrict__ cb_crc_ok,
+                                                       const uint8_t* __restrict__ cb_msgs,
+                                                       uint8_t* __restrict__ tbs,
+                                                       uint8_t* __restrict__ tb_crc_ok)
+{
+  __shared__ uint32_t table[256];
+  __shared__ uint32_t part[256];
+  __shared__ int      all_ok;
+  const tb_dec_desc d = descs[blockIdx.x];
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    for (uint32_t c = 0; c < d.nof_cbs; ++c) {
+      ok &= cb_crc_ok[d.first_cb + c] != 0;
+    }
+    all_ok = ok;
+  }
+  __syncthreads();
+  if (!all_ok) {
+    if (threadIdx.x == 0) {
+      tb_crc_ok[d.tb_index] = 0;
+    }
+    return;
+  }
+  uint8_t*       tb    = tbs + d.tb_offset;
+  const uint8_t* msgs  = cb_msgs + static_cast<size_t>(d.first_cb) * CB_MSG_STRIDE;
+  const uint32_t bytes = d.tbs_bits / 8u;
+  if (d.nof_cbs == 1) {
+    for (uint32_t b = threadIdx.x; b < bytes; b += blockDim.x) {
+      tb[b] = msgs[b];
+    }
+    if (threadIdx.x == 0) {
+      tb_crc_ok[d.tb_index] = 1;
+    }
+    return;
+  }
+  // TB bit p comes from codeblock p / cb_data_bits, message bit p % cb_data_bits.
+  for (uint32_t b = threadIdx.x; b < bytes; b += blockDim.x) {
+    uint32_t byte = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t p  = 8u * b + static_cast<uint32_t>(k);
+      const uint32_t cb = __umulhi(p, d.data_magic);
+      const uint32_t q  = p - cb * d.cb_data_bits;
+      const uint8_t* m  = msgs + cb * CB_MSG_STRIDE;
+      byte |= ((static_cast<uint32_t>(m[q >> 3]) >> (7u - (q & 7u))) & 1u) << (7 - k);
+    }
+    tb[b] = static_cast<uint8_t>(byte);
+  }
+  __syncthreads();
+  const uint32_t crc = block_crc_bytes(tb, static_cast<int>(bytes), 24, 0x1864cfbu, table, part);
+  // Checksum: the 24 bits that follow the last codeblock's TB bits (concatenate_codeblocks, :465).
+  const uint32_t last_q = d.tbs_bits - (d.nof_cbs - 1u) * d.cb_data_bits;
+  const uint8_t* lm     = msgs + (d.nof_cbs - 1u) * CB_MSG_STRIDE;
+  uint32_t       chk    = 0;
+  for (int k = 0; k < 24; ++k) {
+    const uint32_t q = last_q + static_cast<uint32_t>(k);
+    chk              = (chk << 1) | ((static_cast<uint32_t>(lm[q >> 3]) >> (7u - (q & 7u))) & 1u);
+  }
+  const bool ok = (crc == chk);
+  if (!ok) {
+    for (uint32_t c = threadIdx.x; c < d.nof_cbs; c += blockDim.x) {
+      cb_crc_ok[d.first_cb + c] = 0;
+    }
+  }
+  if (threadIdx.x == 0) {
+    tb_crc_ok[d.tb_index] = ok ? 1 : 0;
+  }
+}
+
+} // namespace
+
+void launch_pusch_tb(const tb_dec_desc* d_desc,
+                     int                nof_tbs,
+                     uint8_t*           d_cb_crc_ok,
+                     const uint8_t*     d_cb_msgs,
+                     uint8_t*           d_tbs,
+                     uint8_t*           d_tb_crc_ok,
+                     hipStream_t        stream)
+{
+  if (nof_tbs > 0) {
+    pusch_tb_kernel<<<nof_tbs, 256, 0, stream>>>(d_desc, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok);
+  }
+}
+
+} // namespace srsgpu

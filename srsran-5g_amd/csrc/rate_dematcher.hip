@@ -42,11 +42,13 @@ __device__ __forceinline__ int llr_combine(int a, int b)
 template <int MODE>
 __global__ __launch_bounds__(256) void rate_dematch_kernel(const dm_desc* __restrict__ descs,
                                                            const int8_t* __restrict__ llrs,
-                                                           int8_t* __restrict__ harq)
+                                                           int8_t* __restrict__ harq,
+                                                           uint8_t* __restrict__ cb_crc_ok)
 {
   const dm_desc d = descs[blockIdx.x];
-  if (d.skip) {
-    return;
+  // New data invalidates the codeblock CRC flags of the HARQ context (pusch_decoder_impl.cpp:132).
+  if (d.new_data && cb_crc_ok != nullptr && threadIdx.x == 0) {
+    cb_crc_ok[d.cb_index] = 0;
   }
   const int8_t* in  = llrs + d.llr_offset;
   int8_t*       buf = harq + d.harq_offset;
@@ -104,16 +106,21 @@ __global__ __launch_bounds__(256) void rate_dematch_kernel(const dm_desc* __rest
 
 } // namespace
 
-void launch_rate_dematch(int mode, const dm_desc* d_desc, int nof_cbs, const int8_t* d_llrs, int8_t* d_harq,
-                         hipStream_t stream)
+void launch_rate_dematch(int           mode,
+                         const dm_desc* d_desc,
+                         int           nof_cbs,
+                         const int8_t* d_llrs,
+                         int8_t*       d_harq,
+                         uint8_t*      d_cb_crc_ok,
+                         hipStream_t   stream)
 {
   if (nof_cbs <= 0) {
     return;
   }
   if (mode == 1) {
-    rate_dematch_kernel<1><<<nof_cbs, 256, 0, stream>>>(d_desc, d_llrs, d_harq);
+    rate_dematch_kernel<1><<<nof_cbs, 256, 0, stream>>>(d_desc, d_llrs, d_harq, d_cb_crc_ok);
   } else {
-    rate_dematch_kernel<0><<<nof_cbs, 256, 0, stream>>>(d_desc, d_llrs, d_harq);
+    rate_dematch_kernel<0><<<nof_cbs, 256, 0, stream>>>(d_desc, d_llrs, d_harq, d_cb_crc_ok);
   }
 }
 

@@ -46,7 +46,7 @@ struct dm_desc {
   uint16_t nof_filler;   ///< Filler bits.
   uint8_t  Qm;           ///< Modulation order.
   uint8_t  new_data;     ///< First transmission: copy instead of combine.
-  uint32_t skip;         ///< Non-zero: leave this codeblock's buffer untouched.
+  uint32_t cb_index;     ///< Codeblock index (CRC flag slot).
 };
 static_assert(sizeof(dm_desc) == 36, "dm_desc layout");
 
@@ -106,8 +106,36 @@ void launch_pdsch_encode(int              bg,
                          hipStream_t      s);
 
 /// Launches the batched rate dematcher (rate_dematcher.hip). mode 0: generic combining, 1: SIMD combining.
-void launch_rate_dematch(int mode, const dm_desc* d_desc, int nof_cbs, const int8_t* d_llrs, int8_t* d_harq,
-                         hipStream_t stream);
+void launch_rate_dematch(int           mode,
+                         const dm_desc* d_desc,
+                         int           nof_cbs,
+                         const int8_t* d_llrs,
+                         int8_t*       d_harq,
+                         uint8_t*      d_cb_crc_ok,
+                         hipStream_t   stream);
+
+/// TB stage of the PUSCH decoder (pusch_tb.hip): codeblock concatenation and TB CRC check.
+struct tb_dec_desc {
+  uint32_t first_cb;     ///< Index of the TB's first codeblock (flags, messages).
+  uint32_t nof_cbs;      ///< C.
+  uint32_t tbs_bits;     ///< Transport block size in bits.
+  uint32_t cb_data_bits; ///< Data bits per codeblock (cb_info when C > 1).
+  uint32_t data_magic;   ///< ceil(2^32 / cb_data_bits).
+  uint32_t tb_offset;    ///< Output byte offset of the transport block.
+  uint32_t tb_index;     ///< Result slot.
+  uint32_t pad;
+};
+
+void launch_pusch_tb(const tb_dec_desc* d_desc,
+                     int                nof_tbs,
+                     uint8_t*           d_cb_crc_ok,
+                     const uint8_t*     d_cb_msgs,
+                     uint8_t*           d_tbs,
+                     uint8_t*           d_tb_crc_ok,
+                     hipStream_t        stream);
+
+/// Bytes between the packed messages of consecutive codeblocks in the PUSCH decoder's message buffer.
+constexpr uint32_t CB_MSG_STRIDE = 1056;  // 22 * 384 / 8
 
 /// Launches the batched LDPC decoder (ldpc_decoder.hip).
 void launch_ldpc_decode(int                bg,

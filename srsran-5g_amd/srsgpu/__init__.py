@@ -100,6 +100,32 @@ class PdschTbConfig(ctypes.Structure):
 
 assert ctypes.sizeof(PdschTbConfig) == 24
 
+
+class PuschTbConfig(ctypes.Structure):
+    """srsgpu_pusch_tb_config (include/srsgpu_phy.h)."""
+    _fields_ = [
+        ("base_graph", ctypes.c_uint8),
+        ("rv", ctypes.c_uint8),
+        ("modulation_order", ctypes.c_uint8),
+        ("nof_layers", ctypes.c_uint8),
+        ("new_data", ctypes.c_uint8),
+        ("use_early_stop", ctypes.c_uint8),
+        ("max_iterations", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8),
+        ("scaling_factor", ctypes.c_float),
+        ("tbs_bytes", ctypes.c_uint32),
+        ("nof_ch_symbols", ctypes.c_uint32),
+        ("Nref", ctypes.c_uint32),
+        ("llr_offset", ctypes.c_uint32),
+        ("harq_offset", ctypes.c_uint32),
+        ("cb_offset", ctypes.c_uint32),
+        ("tb_offset", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(PuschTbConfig) == 40
+CB_MSG_STRIDE = 1056
+
 _lib = None
 
 
@@ -132,6 +158,12 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pdsch_encoder_plan_execute.argtypes = [P, P, P, P]
     lib.srsgpu_pdsch_encoder_plan_destroy.argtypes = [P]
     lib.srsgpu_pdsch_encoder_plan_destroy.restype = None
+    lib.srsgpu_pusch_decoder_plan_create.argtypes = [P, ctypes.c_int, P, ctypes.c_uint32, ctypes.POINTER(P)]
+    lib.srsgpu_pusch_decoder_plan_nof_codeblocks.argtypes = [P]
+    lib.srsgpu_pusch_decoder_plan_nof_codeblocks.restype = ctypes.c_uint32
+    lib.srsgpu_pusch_decoder_plan_execute.argtypes = [P, P, P, P, P, P, P, P, P]
+    lib.srsgpu_pusch_decoder_plan_destroy.argtypes = [P]
+    lib.srsgpu_pusch_decoder_plan_destroy.restype = None
     _lib = lib
     return lib
 
@@ -142,7 +174,9 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ldpc_decoder_plan_create", "srsgpu_ldpc_decoder_plan_execute", "srsgpu_ldpc_decoder_plan_destroy",
     "srsgpu_ldpc_decode", "srsgpu_pusch_cb_plan_create", "srsgpu_pusch_cb_plan_execute",
     "srsgpu_pusch_cb_plan_destroy", "srsgpu_pdsch_encoder_plan_create", "srsgpu_pdsch_encoder_plan_nof_codeblocks",
-    "srsgpu_pdsch_encoder_plan_execute", "srsgpu_pdsch_encoder_plan_destroy",
+    "srsgpu_pdsch_encoder_plan_execute", "srsgpu_pdsch_encoder_plan_destroy", "srsgpu_pusch_decoder_plan_create",
+    "srsgpu_pusch_decoder_plan_nof_codeblocks", "srsgpu_pusch_decoder_plan_execute",
+    "srsgpu_pusch_decoder_plan_destroy",
 ]
 
 
@@ -487,3 +521,114 @@ class PdschEncoder:
 
     def encode(self, tb: np.ndarray, cfg: PdschTransportBlock) -> np.ndarray:
         return self.encode_batch([tb], [cfg])[0]
+
+
+@dataclass
+class PuschTransportBlock:
+    """pusch_decoder::configuration (pusch_decoder.h:55) + the TB geometry of one transport block."""
+    tbs_bytes: int
+    base_graph: int
+    rv: int
+    modulation_order: int
+    nof_layers: int
+    nof_ch_symbols: int
+    Nref: int = 0
+    new_data: bool = True
+    use_early_stop: bool = True
+    nof_ldpc_iterations: int = 6
+    scaling_factor: float = 0.8
+
+
+def make_pusch_tb_configs(tbs: Sequence[PuschTransportBlock], nof_cbs: Sequence[int], cb_lengths: Sequence[int]):
+    """Contiguous layout: codeword LLRs, HARQ buffers (C * N per TB), codeblock slots, TB bytes.
+    nof_cbs[i] / cb_lengths[i] (N_short * Z) come from the segmentation (srsgpu.sch)."""
+    arr = (PuschTbConfig * len(tbs))()
+    lo = ho = co = to = 0
+    for i, t in enumerate(tbs):
+        a = arr[i]
+        a.base_graph, a.rv, a.modulation_order, a.nof_layers = t.base_graph, t.rv, t.modulation_order, t.nof_layers
+        a.new_data, a.use_early_stop, a.max_iterations = int(t.new_data), int(t.use_early_stop), t.nof_ldpc_iterations
+        a.scaling_factor, a.tbs_bytes, a.nof_ch_symbols, a.Nref = t.scaling_factor, t.tbs_bytes, t.nof_ch_symbols, t.Nref
+        a.llr_offset, a.harq_offset, a.cb_offset, a.tb_offset = lo, ho, co, to
+        lo += t.nof_ch_symbols * t.modulation_order
+        ho += nof_cbs[i] * cb_lengths[i]
+        co += nof_cbs[i]
+        to += t.tbs_bytes
+    return arr, lo, ho, co, to
+
+
+class PuschDecoderPlan:
+    """srsgpu_pusch_decoder_plan (TB level)."""
+
+    def __init__(self, ctx: Context, impl: int, cfg_array):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        _check(_lib.srsgpu_pusch_decoder_plan_create(ctx.handle, impl, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                     len(cfg_array), ctypes.byref(h)))
+        self.handle = h
+        self.nof_tbs = len(cfg_array)
+        self.nof_codeblocks = int(_lib.srsgpu_pusch_decoder_plan_nof_codeblocks(h))
+
+    def execute(self, d_llrs, d_harq, d_cb_crc_ok, d_cb_msgs, d_cb_iters, d_tbs, d_tb_crc_ok, stream=None):
+        _check(_lib.srsgpu_pusch_decoder_plan_execute(self.handle, _dptr(d_llrs), _dptr(d_harq), _dptr(d_cb_crc_ok),
+                                                      _dptr(d_cb_msgs), _dptr(d_cb_iters), _dptr(d_tbs),
+                                                      _dptr(d_tb_crc_ok), _stream_handle(stream)))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.srsgpu_pusch_decoder_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class PuschDecoder:
+    """GPU counterpart of srsran::pusch_decoder with a device-resident HARQ context (one per set of TBs)."""
+
+    def __init__(self, ctx: Context, dec_type: str = "auto"):
+        if dec_type not in IMPL_BY_NAME:
+            raise SrsGpuError(f"invalid decoder type '{dec_type}'")
+        self.ctx = ctx
+        self.impl = IMPL_BY_NAME[dec_type]
+        self.harq = None
+
+    def decode_batch(self, llrs_list, tbs: Sequence[PuschTransportBlock]):
+        """Returns (tb_crc_ok list, TB byte arrays, per-TB lists of CB iteration counts). The HARQ context is kept
+        between calls (retransmissions: same TBs, new_data False)."""
+        from . import sch
+        nof_cbs, cb_len = [], []
+        for t in tbs:
+            seg = sch.segment(t.tbs_bytes * 8, t.base_graph, t.modulation_order, t.nof_layers, t.nof_ch_symbols)
+            nof_cbs.append(seg.nof_segments)
+            cb_len.append((66 if t.base_graph == 1 else 50) * seg.lifting_size)
+        arr, nllr, nharq, ncb, ntb = make_pusch_tb_configs(tbs, nof_cbs, cb_len)
+        dev = torch.device("cuda", self.ctx.device)
+        if self.harq is None or self.harq[0].numel() != nharq:
+            self.harq = (torch.zeros(nharq, dtype=torch.int8, device=dev),
+                         torch.zeros(ncb, dtype=torch.uint8, device=dev),
+                         torch.zeros(ncb * CB_MSG_STRIDE, dtype=torch.uint8, device=dev))
+        d_harq, d_crc, d_msgs = self.harq
+        d_llrs = torch.from_numpy(np.concatenate([np.asarray(x, np.int8) for x in llrs_list])).to(dev)
+        assert d_llrs.numel() == nllr
+        d_iters = torch.zeros(ncb, dtype=torch.int32, device=dev)
+        d_tbs = torch.zeros(max(ntb, 1), dtype=torch.uint8, device=dev)
+        d_tb_ok = torch.zeros(len(tbs), dtype=torch.uint8, device=dev)
+        plan = PuschDecoderPlan(self.ctx, self.impl, arr)
+        plan.execute(d_llrs, d_harq, d_crc, d_msgs, d_iters, d_tbs, d_tb_ok)
+        torch.cuda.synchronize(dev)
+        plan.close()
+        ok = d_tb_ok.cpu().numpy()
+        tb_bytes = d_tbs.cpu().numpy()
+        iters = d_iters.cpu().numpy()
+        out_tbs, out_iters = [], []
+        off = co = 0
+        for i, t in enumerate(tbs):
+            out_tbs.append(tb_bytes[off: off + t.tbs_bytes].copy())
+            out_iters.append(iters[co: co + nof_cbs[i]].tolist())
+            off += t.tbs_bytes
+            co += nof_cbs[i]
+        return [bool(x) for x in ok], out_tbs, out_iters

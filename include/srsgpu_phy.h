@@ -194,6 +194,11 @@ int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
 
 void srsgpu_pdsch_encoder_plan_destroy(srsgpu_pdsch_encoder_plan* plan);
 
+/** Stage timing (see srsgpu_pusch_decoder_plan_enable_timing): stages 0: output clear + TB CRC, 1: codeblock
+ *  encoding and rate matching (ms[2]). */
+int srsgpu_pdsch_encoder_plan_enable_timing(srsgpu_pdsch_encoder_plan* plan, int enable);
+int srsgpu_pdsch_encoder_plan_stage_times(srsgpu_pdsch_encoder_plan* plan, float* ms, uint32_t* nof_executes);
+
 /* ------------------------------------------------------------------------------------------------------------------
  * PUSCH decoder (transport-block level) — replaces srsran::pusch_decoder (include/srsran/phy/upper/channel_processors/
  * pusch/pusch_decoder.h; lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.cpp: new_data :98, segmentation
@@ -246,6 +251,12 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
                                       void*                            stream);
 
 void srsgpu_pusch_decoder_plan_destroy(srsgpu_pusch_decoder_plan* plan);
+
+/** Stage timing: when enabled, every execute records HIP events on its stream around the three kernel stages
+ *  (0: rate dematching, 1: LDPC decoding, 2: TB assembly + CRC). stage_times synchronises on them and returns the
+ *  accumulated milliseconds per stage (ms[3]) and the number of executes since the previous call. */
+int srsgpu_pusch_decoder_plan_enable_timing(srsgpu_pusch_decoder_plan* plan, int enable);
+int srsgpu_pusch_decoder_plan_stage_times(srsgpu_pusch_decoder_plan* plan, float* ms, uint32_t* nof_executes);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,7 @@ SRCS=(
   "$LDPC/ldpc_rate_matcher_impl.cpp:"
   "$LDPC/ldpc_rate_dematcher_impl.cpp:"
   "$LDPC/ldpc_rate_dematcher_avx2_impl.cpp:-mavx2"
+  "$LDPC/ldpc_rate_dematcher_avx512_impl.cpp:-mavx512f -mavx512bw -mavx512vbmi"
   "$LDPC/ldpc_segmenter_tx_impl.cpp:"
   "$REF/lib/phy/upper/channel_coding/crc_calculator_generic_impl.cpp:"
   "$REF/lib/phy/upper/log_likelihood_ratio.cpp:-mavx2"

@@ -316,3 +316,129 @@ long long ref_ldpc_decode_timed(int           impl,
 }
 
 } // extern "C"
+
+#include "ldpc/ldpc_rate_dematcher_avx512_impl.h"
+
+extern "C" {
+
+int ref_cpu_has_avx512vbmi()
+{
+  return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+         __builtin_cpu_supports("avx512vbmi");
+}
+
+/// CPU baseline, DL leg: pdsch_encoder_impl::encode (pdsch_encoder_impl.cpp:28) of n transport blocks with one set
+/// of reference objects (segmenter, encoder of the given implementation, rate matcher), codeword unpacked one bit per
+/// byte like the reference. Returns the wall time of the encode loop in nanoseconds.
+long long ref_pdsch_encode_slot_timed(int             enc_impl,
+                                      unsigned        n,
+                                      const int*      bg,
+                                      const int*      qm,
+                                      const int*      layers,
+                                      const unsigned* nsym,
+                                      const unsigned* tb_bytes,
+                                      const uint8_t*  tbs,
+                                      uint8_t*        cw_out)
+{
+  ldpc_segmenter_tx_impl::sch_crc crcs{std::make_unique<crc_calculator_generic_impl>(crc_generator_poly::CRC16),
+                                       std::make_unique<crc_calculator_generic_impl>(crc_generator_poly::CRC24A),
+                                       std::make_unique<crc_calculator_generic_impl>(crc_generator_poly::CRC24B)};
+  ldpc_segmenter_tx_impl        seg(crcs);
+  std::unique_ptr<ldpc_encoder> enc;
+  if (enc_impl == 1) {
+    enc = std::make_unique<ldpc_encoder_avx2>();
+  } else {
+    enc = std::make_unique<ldpc_encoder_generic>();
+  }
+  ldpc_rate_matcher_impl rm;
+  dynamic_bit_buffer     cb_data(8448);
+  dynamic_bit_buffer     packed(22 * 384 * 35);
+  auto                   t0     = std::chrono::steady_clock::now();
+  size_t                 tb_off = 0, cw_off = 0;
+  for (unsigned t = 0; t != n; ++t) {
+    segmenter_config scfg;
+    scfg.base_graph     = to_bg(bg[t]);
+    scfg.rv             = 0;
+    scfg.mod            = to_mod(qm[t]);
+    scfg.Nref           = 0;
+    scfg.nof_layers     = layers[t];
+    scfg.nof_ch_symbols = nsym[t];
+    span<const uint8_t>          tb(tbs + tb_off, tb_bytes[t]);
+    const ldpc_segmenter_buffer& sb = seg.new_transmission(tb, scfg);
+    cb_data.resize(sb.get_segment_length().value());
+    for (unsigned i = 0, nc = sb.get_nof_codeblocks(); i != nc; ++i) {
+      codeblock_metadata md = sb.get_cb_metadata(i);
+      sb.read_codeblock(cb_data, tb, i);
+      const ldpc_encoder_buffer& buf = enc->encode(cb_data, md.tb_common);
+      unsigned                   E   = sb.get_rm_length(i);
+      packed.resize(E);
+      rm.rate_match(packed, buf, md);
+      srsvec::bit_unpack(span<uint8_t>(cw_out + cw_off, E), packed);
+      cw_off += E;
+    }
+    tb_off += tb_bytes[t];
+  }
+  auto t1 = std::chrono::steady_clock::now();
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+}
+
+/// CPU baseline, UL leg: the codeblock task of pusch_decoder_impl (pusch_decoder_impl.cpp:283 /
+/// pusch_codeblock_decoder.cpp:33) for n codeblocks: rate dematching (new data) + LDPC decoding with CRC early stop.
+/// p[i*8 + {0..7}] = {bg, Z, qm, E, filler, crc_poly, nof_crc_bits, llr_offset}. dm_impl: 0 generic, 1 avx2,
+/// 2 avx512; dec_impl: 0 generic, 1 avx2, 2 avx512. Returns nanoseconds; iters[i] = iterations or -1.
+long long ref_pusch_decode_cbs_timed(int           dm_impl,
+                                     int           dec_impl,
+                                     unsigned      n,
+                                     const int*    p,
+                                     const int8_t* llrs,
+                                     int           max_iter,
+                                     int*          iters)
+{
+  std::unique_ptr<ldpc_rate_dematcher> rdm;
+  if (dm_impl == 2) {
+    rdm = std::make_unique<ldpc_rate_dematcher_avx512_impl>();
+  } else if (dm_impl == 1) {
+    rdm = std::make_unique<ldpc_rate_dematcher_avx2_impl>();
+  } else {
+    rdm = std::make_unique<ldpc_rate_dematcher_impl>();
+  }
+  auto                            dec = make_decoder(dec_impl);
+  std::unique_ptr<crc_calculator> crc_set[6];
+  for (int c = 0; c < 6; ++c) {
+    crc_set[c] = std::make_unique<crc_calculator_generic_impl>(to_poly(c));
+  }
+  std::vector<log_likelihood_ratio> buf(66 * 384);
+  dynamic_bit_buffer                msg(22 * 384);
+  auto                              t0 = std::chrono::steady_clock::now();
+  for (unsigned i = 0; i != n; ++i) {
+    const int* q  = p + 8 * i;
+    int        bg = q[0], Z = q[1];
+    unsigned   N  = (bg == 2 ? 50 : 66) * Z;
+    unsigned   K  = (bg == 2 ? 10 : 22) * Z;
+    codeblock_metadata md;
+    md.tb_common.base_graph        = to_bg(bg);
+    md.tb_common.lifting_size      = static_cast<ldpc::lifting_size_t>(Z);
+    md.tb_common.rv                = 0;
+    md.tb_common.mod               = to_mod(q[2]);
+    md.tb_common.Nref              = 0;
+    md.cb_specific.rm_length       = q[3];
+    md.cb_specific.nof_filler_bits = q[4];
+    md.cb_specific.nof_crc_bits    = q[6];
+    md.cb_specific.full_length     = N + 2 * Z;
+    span<log_likelihood_ratio> b(buf.data(), N);
+    rdm->rate_dematch(b,
+                      span<const log_likelihood_ratio>(reinterpret_cast<const log_likelihood_ratio*>(llrs + q[7]), q[3]),
+                      true,
+                      md);
+    ldpc_decoder::configuration cfg;
+    cfg.block_conf                    = md;
+    cfg.algorithm_conf.max_iterations = max_iter;
+    msg.resize(K);
+    std::optional<unsigned> r = dec->decode(msg, b, crc_set[q[5]].get(), cfg);
+    iters[i]                  = r.has_value() ? static_cast<int>(*r) : -1;
+  }
+  auto t1 = std::chrono::steady_clock::now();
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+}
+
+} // extern "C"

@@ -81,6 +81,79 @@ struct srsgpu_context {
   std::mutex                           mtx;
 };
 
+/// Per-stage device time accounting: HIP events recorded around every kernel stage on the execution stream.
+struct stage_timer {
+  bool                                  enabled = false;
+  int                                   stages  = 0;
+  std::vector<std::vector<hipEvent_t>>  pending;  ///< One event set (stages + 1) per timed execute.
+  std::vector<std::vector<hipEvent_t>>  pool;
+  std::vector<double>                   acc_ms;
+  uint32_t                              count = 0;
+
+  ~stage_timer()
+  {
+    for (auto* v : {&pending, &pool}) {
+      for (auto& set : *v) {
+        for (hipEvent_t e : set) {
+          (void)hipEventDestroy(e);
+        }
+      }
+    }
+  }
+  /// Returns the event set for this execute (nullptr when disabled).
+  std::vector<hipEvent_t>* begin()
+  {
+    if (!enabled) {
+      return nullptr;
+    }
+    if (pool.empty()) {
+      std::vector<hipEvent_t> set(static_cast<size_t>(stages) + 1);
+      for (auto& e : set) {
+        if (hipEventCreate(&e) != hipSuccess) {
+          return nullptr;
+        }
+      }
+      pool.push_back(std::move(set));
+    }
+    pending.push_back(std::move(pool.back()));
+    pool.pop_back();
+    return &pending.back();
+  }
+  static void mark(std::vector<hipEvent_t>* set, int i, hipStream_t s)
+  {
+    if (set != nullptr) {
+      (void)hipEventRecord((*set)[static_cast<size_t>(i)], s);
+    }
+  }
+  /// Synchronises on the pending events and accumulates the stage durations.
+  int collect(float* out_ms, uint32_t* nof_executes)
+  {
+    acc_ms.resize(static_cast<size_t>(stages), 0.0);
+    for (auto& set : pending) {
+      if (hipEventSynchronize(set.back()) != hipSuccess) {
+        return -1;
+      }
+      for (int i = 0; i < stages; ++i) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, set[static_cast<size_t>(i)], set[static_cast<size_t>(i) + 1]) != hipSuccess) {
+          return -1;
+        }
+        acc_ms[static_cast<size_t>(i)] += ms;
+      }
+      ++count;
+      pool.push_back(std::move(set));
+    }
+    pending.clear();
+    for (int i = 0; i < stages; ++i) {
+      out_ms[i] = static_cast<float>(acc_ms[static_cast<size_t>(i)]);
+    }
+    *nof_executes = count;
+    std::fill(acc_ms.begin(), acc_ms.end(), 0.0);
+    count = 0;
+    return 0;
+  }
+};
+
 struct srsgpu_pusch_cb_plan {
   srsgpu_context*           ctx     = nullptr;
   int                       impl    = SRSGPU_LDPC_IMPL_SIMD;
@@ -90,6 +163,7 @@ struct srsgpu_pusch_cb_plan {
 };
 
 struct srsgpu_pdsch_encoder_plan {
+  mutable stage_timer timer;
   srsgpu_context* ctx        = nullptr;
   tb_crc_desc*    d_tb       = nullptr;
   uint32_t*       d_tb_crc   = nullptr;
@@ -102,6 +176,7 @@ struct srsgpu_pdsch_encoder_plan {
 };
 
 struct srsgpu_pusch_decoder_plan {
+  mutable stage_timer   timer;
   srsgpu_context*       ctx     = nullptr;
   srsgpu_pusch_cb_plan* cbs     = nullptr;
   tb_dec_desc*          d_tb    = nullptr;
@@ -802,12 +877,15 @@ int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
   if (plan == nullptr || d_tbs == nullptr || d_codewords == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  auto s = static_cast<hipStream_t>(stream);
+  auto  s  = static_cast<hipStream_t>(stream);
+  auto* ev = plan->timer.begin();
+  stage_timer::mark(ev, 0, s);
   if (plan->out_end > plan->out_begin) {
     HIP_TRY(hipMemsetAsync(d_codewords + plan->out_begin, 0, plan->out_end - plan->out_begin, s));
   }
   launch_tb_crc(plan->d_tb, plan->nof_tbs, d_tbs, plan->d_tb_crc, s);
   HIP_TRY(hipGetLastError());
+  stage_timer::mark(ev, 1, s);
   for (int b = 0; b < 2; ++b) {
     if (plan->count[b] == 0) {
       continue;
@@ -816,6 +894,29 @@ int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
                         reinterpret_cast<uint32_t*>(d_codewords), plan->ctx->d_shifts[b], plan->ctx->d_core[b],
                         plan->ctx->d_crc_arena, s);
     HIP_TRY(hipGetLastError());
+  }
+  stage_timer::mark(ev, 2, s);
+  return SRSGPU_OK;
+}
+
+int srsgpu_pdsch_encoder_plan_enable_timing(srsgpu_pdsch_encoder_plan* plan, int enable)
+{
+  if (plan == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  plan->timer.stages  = 2;
+  plan->timer.enabled = enable != 0;
+  return SRSGPU_OK;
+}
+
+int srsgpu_pdsch_encoder_plan_stage_times(srsgpu_pdsch_encoder_plan* plan, float* ms, uint32_t* nof_executes)
+{
+  if (plan == nullptr || ms == nullptr || nof_executes == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  plan->timer.stages = 2;
+  if (plan->timer.collect(ms, nof_executes) != 0) {
+    return fail(SRSGPU_ERR_HIP, "event synchronisation failed");
   }
   return SRSGPU_OK;
 }
@@ -922,13 +1023,42 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
       d_cb_nof_iterations == nullptr || d_tbs == nullptr || d_tb_crc_ok == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  auto s = static_cast<hipStream_t>(stream);
-  int  r = execute_pusch_cb_plan(plan->cbs, d_llrs, d_harq, d_cb_msgs, d_cb_nof_iterations, d_cb_crc_ok, s);
+  auto  s  = static_cast<hipStream_t>(stream);
+  auto* ev = plan->timer.begin();
+  stage_timer::mark(ev, 0, s);
+  launch_rate_dematch(plan->cbs->impl, plan->cbs->d_dm, plan->cbs->nof_cbs, d_llrs, d_harq, d_cb_crc_ok, s);
+  HIP_TRY(hipGetLastError());
+  stage_timer::mark(ev, 1, s);
+  int r = execute_decoder_plan(plan->cbs->dec, d_harq, d_cb_msgs, d_cb_nof_iterations, d_cb_crc_ok, s);
   if (r != SRSGPU_OK) {
     return r;
   }
+  stage_timer::mark(ev, 2, s);
   launch_pusch_tb(plan->d_tb, plan->nof_tbs, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, s);
   HIP_TRY(hipGetLastError());
+  stage_timer::mark(ev, 3, s);
+  return SRSGPU_OK;
+}
+
+int srsgpu_pusch_decoder_plan_enable_timing(srsgpu_pusch_decoder_plan* plan, int enable)
+{
+  if (plan == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  plan->timer.stages  = 3;
+  plan->timer.enabled = enable != 0;
+  return SRSGPU_OK;
+}
+
+int srsgpu_pusch_decoder_plan_stage_times(srsgpu_pusch_decoder_plan* plan, float* ms, uint32_t* nof_executes)
+{
+  if (plan == nullptr || ms == nullptr || nof_executes == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  plan->timer.stages = 3;
+  if (plan->timer.collect(ms, nof_executes) != 0) {
+    return fail(SRSGPU_ERR_HIP, "event synchronisation failed");
+  }
   return SRSGPU_OK;
 }
 

@@ -164,6 +164,9 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pusch_decoder_plan_execute.argtypes = [P, P, P, P, P, P, P, P, P]
     lib.srsgpu_pusch_decoder_plan_destroy.argtypes = [P]
     lib.srsgpu_pusch_decoder_plan_destroy.restype = None
+    for name in ("srsgpu_pusch_decoder_plan", "srsgpu_pdsch_encoder_plan"):
+        getattr(lib, name + "_enable_timing").argtypes = [P, ctypes.c_int]
+        getattr(lib, name + "_stage_times").argtypes = [P, P, ctypes.POINTER(ctypes.c_uint32)]
     _lib = lib
     return lib
 
@@ -176,8 +179,17 @@ EXPORTED_SYMBOLS = [
     "srsgpu_pusch_cb_plan_destroy", "srsgpu_pdsch_encoder_plan_create", "srsgpu_pdsch_encoder_plan_nof_codeblocks",
     "srsgpu_pdsch_encoder_plan_execute", "srsgpu_pdsch_encoder_plan_destroy", "srsgpu_pusch_decoder_plan_create",
     "srsgpu_pusch_decoder_plan_nof_codeblocks", "srsgpu_pusch_decoder_plan_execute",
-    "srsgpu_pusch_decoder_plan_destroy",
+    "srsgpu_pusch_decoder_plan_destroy", "srsgpu_pusch_decoder_plan_enable_timing",
+    "srsgpu_pusch_decoder_plan_stage_times", "srsgpu_pdsch_encoder_plan_enable_timing",
+    "srsgpu_pdsch_encoder_plan_stage_times",
 ]
+
+
+def _stage_times(prefix, handle, n):
+    ms = (ctypes.c_float * n)()
+    cnt = ctypes.c_uint32()
+    _check(getattr(_lib, prefix + "_stage_times")(handle, ctypes.cast(ms, ctypes.c_void_p), ctypes.byref(cnt)))
+    return list(ms), cnt.value
 
 
 def _check(rc: int):
@@ -484,6 +496,13 @@ class PdschEncoderPlan:
         _check(_lib.srsgpu_pdsch_encoder_plan_execute(self.handle, _dptr(d_tbs), _dptr(d_codewords),
                                                       _stream_handle(stream)))
 
+    def enable_timing(self, enable=True):
+        _check(_lib.srsgpu_pdsch_encoder_plan_enable_timing(self.handle, int(enable)))
+
+    def stage_times(self):
+        """([ms TB CRC, ms encode], number of executes) accumulated since the previous call."""
+        return _stage_times("srsgpu_pdsch_encoder_plan", self.handle, 2)
+
     def close(self):
         if getattr(self, "handle", None):
             _lib.srsgpu_pdsch_encoder_plan_destroy(self.handle)
@@ -573,6 +592,13 @@ class PuschDecoderPlan:
         _check(_lib.srsgpu_pusch_decoder_plan_execute(self.handle, _dptr(d_llrs), _dptr(d_harq), _dptr(d_cb_crc_ok),
                                                       _dptr(d_cb_msgs), _dptr(d_cb_iters), _dptr(d_tbs),
                                                       _dptr(d_tb_crc_ok), _stream_handle(stream)))
+
+    def enable_timing(self, enable=True):
+        _check(_lib.srsgpu_pusch_decoder_plan_enable_timing(self.handle, int(enable)))
+
+    def stage_times(self):
+        """([ms dematch, ms decode, ms TB stage], number of executes) accumulated since the previous call."""
+        return _stage_times("srsgpu_pusch_decoder_plan", self.handle, 3)
 
     def close(self):
         if getattr(self, "handle", None):

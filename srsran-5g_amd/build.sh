@@ -3,7 +3,7 @@
 set -euo pipefail
 HERE=$(cd "$(dirname "$0")" && pwd)
 ROOT=$(cd "$HERE/.." && pwd)
-OUT="$HERE/lib"
+OUT="${SRSGPU_OUT_DIR:-$HERE/lib}"
 mkdir -p "$OUT/obj"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 FLAGS="-std=c++17 -O3 -fPIC --offload-arch=gfx950 -I$ROOT/include -I$HERE/csrc ${SRSGPU_EXTRA_FLAGS:-}"

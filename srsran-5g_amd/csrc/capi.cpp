@@ -73,6 +73,7 @@ constexpr size_t CRC_ARENA_WORDS = 4u << 20;  // 16 MiB of contribution tables
 struct srsgpu_context {
   int                                  device      = 0;
   uint16_t*                            d_shifts[2] = {nullptr, nullptr};
+  uint32_t*                            d_shifts32[2] = {nullptr, nullptr};  ///< Same, one dword per shift (decoder).
   core_plan*                           d_core[2]   = {nullptr, nullptr};
   std::vector<core_plan>               core[2];
   uint32_t*                            d_crc_arena = nullptr;
@@ -184,11 +185,16 @@ struct srsgpu_pusch_decoder_plan {
 };
 
 struct srsgpu_ldpc_decoder_plan {
-  srsgpu_context* ctx            = nullptr;
-  int             impl           = SRSGPU_LDPC_IMPL_SIMD;
-  dec_desc*       d_desc[2]      = {nullptr, nullptr};
-  int             count[2]       = {0, 0};
-  int             threads[2]     = {64, 64};
+  /// One kernel launch per (base graph, block size): lanes = 64 * ceil(Z / 64) per codeblock.
+  struct group {
+    int       bg      = 1;
+    int       threads = 64;
+    int       count   = 0;
+    dec_desc* d_desc  = nullptr;
+  };
+  srsgpu_context*    ctx  = nullptr;
+  int                impl = SRSGPU_LDPC_IMPL_SIMD;
+  std::vector<group> groups;
 };
 
 namespace {
@@ -338,8 +344,13 @@ int srsgpu_context_create(int device, srsgpu_context** out)
         tab[static_cast<size_t>(p) * ne + e] = static_cast<uint16_t>(v % Z);
       }
     }
+    // The decoder reads its shifts through scalar loads, which are dword-granular: it gets a 32-bit copy.
+    std::vector<uint32_t> tab32(tab.begin(), tab.end());
     if (hipMalloc(&ctx->d_shifts[bg - 1], tab.size() * sizeof(uint16_t)) != hipSuccess ||
         hipMemcpy(ctx->d_shifts[bg - 1], tab.data(), tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        hipMalloc(&ctx->d_shifts32[bg - 1], tab32.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipMemcpy(ctx->d_shifts32[bg - 1], tab32.data(), tab32.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
             hipSuccess) {
       srsgpu_context_destroy(ctx);
       return fail(SRSGPU_ERR_HIP, "failed to upload LDPC shift tables");
@@ -379,6 +390,11 @@ void srsgpu_context_destroy(srsgpu_context* ctx)
       (void)hipFree(p);
     }
   }
+  for (auto* p : ctx->d_shifts32) {
+    if (p != nullptr) {
+      (void)hipFree(p);
+    }
+  }
   for (auto* p : ctx->d_core) {
     if (p != nullptr) {
       (void)hipFree(p);
@@ -394,10 +410,12 @@ void srsgpu_context_destroy(srsgpu_context* ctx)
 
 namespace {
 
-/// Codeblock work split by base graph (one kernel instantiation per base graph).
+/// Codeblock work split by base graph: one launch per base graph, sized for its largest lifting size. (Splitting
+/// further by block size raises the occupancy of the small-Z blocks but serialises launches; measured slower on the
+/// 100 MHz slot: 0.82 vs 0.76 ms per 16 slots.)
 struct dec_batch {
-  std::vector<dec_desc> descs[2];
-  int                   maxz[2] = {0, 0};
+  std::map<int, std::vector<dec_desc>> groups;
+  std::map<int, int>                   threads;
 };
 
 /// Validates one decoder configuration (ldpc_decoder_impl.cpp:48-:56, :73-:88) and appends its descriptor.
@@ -463,8 +481,9 @@ int add_decoder_cb(srsgpu_context* ctx,
     }
     d.flags = early_stop ? DEC_FLAG_EARLY_STOP : 0u;
   }
-  batch.descs[bg - 1].push_back(d);
-  batch.maxz[bg - 1] = Z > batch.maxz[bg - 1] ? Z : batch.maxz[bg - 1];
+  batch.groups[bg].push_back(d);
+  int& t = batch.threads[bg];
+  t      = std::max(t, ((Z + 63) / 64) * 64);
   return SRSGPU_OK;
 }
 
@@ -473,18 +492,19 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
   auto* plan = new srsgpu_ldpc_decoder_plan();
   plan->ctx  = ctx;
   plan->impl = impl;
-  for (int b = 0; b < 2; ++b) {
-    plan->count[b]   = static_cast<int>(batch.descs[b].size());
-    plan->threads[b] = ((batch.maxz[b] + 63) / 64) * 64;
-    if (plan->count[b] == 0) {
-      continue;
-    }
-    const size_t bytes = batch.descs[b].size() * sizeof(dec_desc);
-    if (hipMalloc(&plan->d_desc[b], bytes) != hipSuccess ||
-        hipMemcpy(plan->d_desc[b], batch.descs[b].data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+  for (const auto& kv : batch.groups) {
+    srsgpu_ldpc_decoder_plan::group g;
+    g.bg               = kv.first;
+    g.threads          = batch.threads.at(kv.first);
+    g.count            = static_cast<int>(kv.second.size());
+    const size_t bytes = kv.second.size() * sizeof(dec_desc);
+    if (hipMalloc(&g.d_desc, bytes) != hipSuccess ||
+        hipMemcpy(g.d_desc, kv.second.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      plan->groups.push_back(g);
       srsgpu_ldpc_decoder_plan_destroy(plan);
       return fail(SRSGPU_ERR_HIP, "failed to upload decoder descriptors");
     }
+    plan->groups.push_back(g);
   }
   *plan_out = plan;
   return SRSGPU_OK;
@@ -497,12 +517,9 @@ int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
                          uint8_t*                        d_cb_crc_ok,
                          hipStream_t                     s)
 {
-  for (int b = 0; b < 2; ++b) {
-    if (plan->count[b] == 0) {
-      continue;
-    }
-    launch_ldpc_decode(b + 1, plan->impl, plan->d_desc[b], plan->count[b], plan->threads[b], d_llrs, d_out,
-                       d_nof_iterations, plan->ctx->d_shifts[b], plan->ctx->d_crc_arena, d_cb_crc_ok, s);
+  for (const auto& g : plan->groups) {
+    launch_ldpc_decode(g.bg, plan->impl, g.d_desc, g.count, g.threads, d_llrs, d_out, d_nof_iterations,
+                       plan->ctx->d_shifts32[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s);
     HIP_TRY(hipGetLastError());
   }
   return SRSGPU_OK;
@@ -658,9 +675,9 @@ void srsgpu_ldpc_decoder_plan_destroy(srsgpu_ldpc_decoder_plan* plan)
   if (plan == nullptr) {
     return;
   }
-  for (auto* p : plan->d_desc) {
-    if (p != nullptr) {
-      (void)hipFree(p);
+  for (auto& g : plan->groups) {
+    if (g.d_desc != nullptr) {
+      (void)hipFree(g.d_desc);
     }
   }
   delete plan;
@@ -1073,5 +1090,13 @@ void srsgpu_pusch_decoder_plan_destroy(srsgpu_pusch_decoder_plan* plan)
   }
   delete plan;
 }
+
+#ifdef LDPC_DEC_PROFILE
+/// Instrumented builds only: phase stamps of the last decoder launch (see ldpc_decoder.hip, DEC_STAMP).
+int srsgpu_debug_decoder_profile(uint64_t* dst, uint32_t n)
+{
+  return srsgpu::debug_read_decoder_profile(dst, n);
+}
+#endif
 
 } // extern "C"

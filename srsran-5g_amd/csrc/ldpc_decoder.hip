@@ -50,8 +50,24 @@ struct bg_t<2> {
 #define LDPC_DEC_MIN_WAVES 4
 #endif
 
+#ifdef LDPC_DEC_PROFILE
+// Instrumented build only (SRSGPU_EXTRA_FLAGS=-DLDPC_DEC_PROFILE): per-codeblock s_memtime stamps of the decoder
+// phases, read back with srsgpu_debug_decoder_profile (tools/decoder_phase_profile.py).
+__device__ uint64_t g_dec_prof[LDPC_DEC_PROF_CBS * LDPC_DEC_PROF_SLOTS];
+#define DEC_PROF(slot, value)                                                                                          \
+  do {                                                                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < LDPC_DEC_PROF_CBS) {                                                          \
+      g_dec_prof[blockIdx.x * LDPC_DEC_PROF_SLOTS + (slot)] = (value);                                                 \
+    }                                                                                                                  \
+  } while (0)
+#else
+#define DEC_PROF(slot, value)                                                                                          \
+  do {                                                                                                                 \
+  } while (0)
+#endif
+#define DEC_STAMP(slot) DEC_PROF(slot, __builtin_amdgcn_s_memtime())
+
 constexpr int LLR_MAX = 120;
-constexpr int LLR_INF = 127;
 /// Sign bits of the first SIGNS_LO edges of a layer share the state word with min1 (7 b), min2 (7 b), argmin (5 b).
 constexpr int SIGNS_LO = 13;
 /// Bytes of LDS reduction scratch between the soft-bit image and the shift table.
@@ -69,27 +85,45 @@ __device__ __forceinline__ int scale_mag(int m, uint32_t sf16, float sf)
   }
 }
 
+/// Lifting shifts are read through the scalar (constant) path: wave-uniform, compile-time offsets -> s_load.
+using const_u32_ptr = const __attribute__((address_space(4))) uint32_t*;
+
+/// Unsigned median of three (v_med3_u32).
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c)
+{
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+/// Soft bits are kept in LDS in [-LLR_MAX - 1, LLR_MAX + 1]: +/-(LLR_MAX + 1) stands for the reference's +/-infinity
+/// (LLR_INFTY = 127). The encoding is exact for inputs in the log_likelihood_ratio domain ([-120, 120] and +/-127,
+/// log_likelihood_ratio.h:65) and lets the promotion sum be a single clamp.
+constexpr int SOFT_INF = LLR_MAX + 1;
+/// Minimum search key: magnitude << 5 | edge. Ties resolve to the lowest edge as in the reference (strict '<').
+constexpr uint32_t KEY_INIT = static_cast<uint32_t>(LLR_MAX) << 5;
+
 /// One lifted check row of layer m: variable-to-check messages, min-sum analysis, check-to-variable messages and the
 /// soft-bit update (ldpc_decoder_impl.cpp:195, :255, :240).
 template <int BG, int MODE, int m>
 __device__ __forceinline__ void row_update(int8_t* __restrict__ soft,
-                                           const uint16_t* __restrict__ sh,  // lifting shifts, in LDS
-                                           int       z,
-                                           int       Z,
-                                           uint32_t  sf16,
-                                           float     sf,
-                                           uint32_t& st,
-                                           uint32_t& st_hi)
+                                           const_u32_ptr sh,  // lifting shifts of this Z
+                                           int           z,
+                                           int           Z,
+                                           uint32_t      sf16,
+                                           float         sf,
+                                           uint32_t&     st,
+                                           uint32_t&     st_hi)
 {
-  using G              = bg_t<BG>;
-  constexpr int e0     = G::rs(m);
-  constexpr int deg    = G::rs(m + 1) - e0;
-  const int     om1    = static_cast<int>(st & 127u);
-  const int     om2    = static_cast<int>((st >> 7) & 127u);
-  const int     oidx   = static_cast<int>((st >> 14) & 31u);
+  using G            = bg_t<BG>;
+  constexpr int e0   = G::rs(m);
+  constexpr int deg  = G::rs(m + 1) - e0;
+  const int     om1  = static_cast<int>(st & 127u);
+  const int     om2  = static_cast<int>((st >> 7) & 127u);
+  const int     oidx = static_cast<int>((st >> 14) & 31u);
   int           v2c[deg];
-  int           min1 = LLR_MAX, min2 = LLR_MAX, idx = 0;
-  uint32_t      sp   = 0;
+  uint32_t      k1 = KEY_INIT, k2 = KEY_INIT;  // two smallest keys
+  uint32_t      sx = 0;                        // sign parity in bit 31
   // Sign bits of edges >= SIGNS_LO of the (at most four) high-degree core rows share one word, 6 bits per row.
   constexpr int HI_SHIFT = 6 * (m & 3);
 
@@ -100,53 +134,51 @@ __device__ __forceinline__ void row_update(int8_t* __restrict__ soft,
     const uint32_t p0 = static_cast<uint32_t>(z) + sh[e0 + e];
     const uint32_t p1 = p0 - static_cast<uint32_t>(Z);
     const int      p  = static_cast<int>(p0 < p1 ? p0 : p1);
-    const int sb      = soft[col * SOFT_COL_STRIDE + p];
-    // Previous check-to-variable message of this edge, rebuilt from the compressed state.
-    uint32_t sgn;
+    const int      sb = soft[col * SOFT_COL_STRIDE + p];
+    // Previous check-to-variable message of this edge, rebuilt from the compressed state (n = 0 or -1: its sign).
+    int n;
     if constexpr (e < SIGNS_LO) {
-      sgn = (st >> (19 + e)) & 1u;
+      n = static_cast<int>(st << (12 - e)) >> 31;
     } else {
-      sgn = (st_hi >> (HI_SHIFT + e - SIGNS_LO)) & 1u;
+      n = static_cast<int>(st_hi << (31 - (HI_SHIFT + e - SIGNS_LO))) >> 31;
     }
     const int om = (oidx == e) ? om2 : om1;
-    const int c  = sgn ? -om : om;
-    // v2c = soft - c2v saturated to +/-LLR_MAX; infinite soft bits stay infinite (ldpc_decoder_avx2.cpp:69).
-    int v  = clamp_i(sb - c, -LLR_MAX, LLR_MAX);
-    v      = (sb == LLR_INF || sb == -LLR_INF) ? sb : v;
-    v2c[e] = v;
-    // Two smallest magnitudes, argmin and sign parity (ldpc_decoder_avx2.cpp:111).
-    const int  a      = v < 0 ? -v : v;
-    const bool is_min = a < min1;
-    const int  nsec   = is_min ? min1 : a;
-    min2              = (a < min2) ? nsec : min2;
-    min1              = is_min ? a : min1;
-    idx               = is_min ? e : idx;
-    sp ^= static_cast<uint32_t>(v < 0);
+    const int c  = (om ^ n) - n;
+    // v2c = soft - c2v saturated to +/-LLR_MAX; infinite soft bits stay infinite (ldpc_decoder_avx2.cpp:69): they
+    // get |v2c| >= 392, never a minimum, and saturate back to infinity in the update.
+    const int fin = clamp_i(sb, -LLR_MAX, LLR_MAX);
+    const int v   = clamp_i(sb - c, -LLR_MAX, LLR_MAX) + ((sb - fin) << 9);
+    v2c[e]        = v;
+    // Two smallest magnitudes and argmin (ldpc_decoder_avx2.cpp:111) on keys |v| << 5 | e; sign parity by XOR.
+    const uint32_t key = (static_cast<uint32_t>(v < 0 ? -v : v) << 5) | static_cast<uint32_t>(e);
+    k2                 = umed3(key, k1, k2);
+    k1                 = key < k1 ? key : k1;
+    sx ^= static_cast<uint32_t>(v);
   });
 
-  const int s1  = scale_mag<MODE>(min1, sf16, sf);
-  const int s2  = scale_mag<MODE>(min2, sf16, sf);
+  const int idx = static_cast<int>(k1 & 31u);
+  const int s1  = scale_mag<MODE>(static_cast<int>(k1 >> 5), sf16, sf);
+  const int s2  = scale_mag<MODE>(static_cast<int>(k2 >> 5), sf16, sf);
   uint32_t  nst = static_cast<uint32_t>(s1) | (static_cast<uint32_t>(s2) << 7) | (static_cast<uint32_t>(idx) << 14);
   uint32_t  nhi = 0;
 
   static_for<deg>([&](auto E) {
-    constexpr int  e   = decltype(E)::value;
-    constexpr int  col = G::col(e0 + e);
-    const int      v   = v2c[e];
-    const uint32_t neg = sp ^ static_cast<uint32_t>(v < 0);
-    const int      mag = (idx == e) ? s2 : s1;
-    const int      c   = neg ? -mag : mag;
+    constexpr int e   = decltype(E)::value;
+    constexpr int col = G::col(e0 + e);
+    const int     v   = v2c[e];
+    // c2v sign = product of the other edges' signs (ldpc_decoder_avx2.cpp:165).
+    const int n   = static_cast<int>(sx ^ static_cast<uint32_t>(v)) >> 31;
+    const int mag = (idx == e) ? s2 : s1;
+    const int c   = (mag ^ n) - n;
     // Promotion sum (log_likelihood_ratio.cpp:75, ldpc_decoder_avx2.cpp:205): |sum| > LLR_MAX becomes +/-infinity.
-    const int t  = c + v;
-    int       sb = t > LLR_MAX ? LLR_INF : (t < -LLR_MAX ? -LLR_INF : t);
-    sb           = (v == LLR_INF || v == -LLR_INF) ? v : sb;
+    const int      sb = clamp_i(c + v, -SOFT_INF, SOFT_INF);
     const uint32_t p0 = static_cast<uint32_t>(z) + sh[e0 + e];
     const uint32_t p1 = p0 - static_cast<uint32_t>(Z);
     soft[col * SOFT_COL_STRIDE + static_cast<int>(p0 < p1 ? p0 : p1)] = static_cast<int8_t>(sb);
     if constexpr (e < SIGNS_LO) {
-      nst |= neg << (19 + e);
+      nst |= static_cast<uint32_t>(n) & (1u << (19 + e));
     } else {
-      nhi |= neg << (HI_SHIFT + e - SIGNS_LO);
+      nhi |= static_cast<uint32_t>(n) & (1u << (HI_SHIFT + e - SIGNS_LO));
     }
   });
   st = nst;
@@ -184,16 +216,18 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
                                                           const int8_t* __restrict__ llrs,
                                                           uint8_t* __restrict__ out,
                                                           int32_t* __restrict__ results,
-                                                          const uint16_t* __restrict__ shift_table,
+                                                          const uint32_t* __restrict__ shift_table,
                                                           const uint32_t* __restrict__ crc_tables,
                                                           uint8_t* __restrict__ cb_crc_ok)
 {
   using G = bg_t<BG>;
-  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  // Static LDS: its base is a link-time constant, so every soft-bit access is (lane offset + immediate).
+  __shared__ __attribute__((aligned(16))) int8_t smem[G::NF * SOFT_COL_STRIDE + SCRATCH_BYTES];
   int8_t*   soft    = smem;
   int*      scratch = reinterpret_cast<int*>(smem + G::NF * SOFT_COL_STRIDE);
-  uint16_t* sh      = reinterpret_cast<uint16_t*>(smem + G::NF * SOFT_COL_STRIDE + SCRATCH_BYTES);
 
+  DEC_STAMP(0);
+  DEC_PROF(29, __builtin_amdgcn_s_memrealtime());
   const dec_desc d      = descs[blockIdx.x];
   // HARQ context (pusch_decoder_impl.cpp:300): a codeblock whose CRC already passed is not decoded again.
   if (cb_crc_ok != nullptr && cb_crc_ok[d.cb_index] != 0) {
@@ -203,6 +237,7 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
     return;
   }
   const int      Z      = d.Z;
+  const auto     sh     = (const_u32_ptr)(uintptr_t)(shift_table + static_cast<uint32_t>(d.zpos) * G::NE);
   const int      z      = threadIdx.x;
   const bool     active = z < Z;
   const int      wave   = threadIdx.x / WAVE;
@@ -210,26 +245,57 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
   const int      lane   = threadIdx.x % WAVE;
 
   // ---- Load the LLRs into the soft-bit image (ldpc_decoder_impl.cpp:152) and find the last non-zero LLR (:94). ----
-  const int8_t* llr   = llrs + d.llr_offset;
-  const int     n_llr = static_cast<int>(d.nof_llr);
-  const int     full  = static_cast<int>(__umulhi(static_cast<uint32_t>(n_llr), d.div_magic)) * Z;
-  int           last  = -1;
+  // Dword loads from the 4-byte aligned span covering the LLRs (every lane keeps several loads in flight), byte
+  // scatter into the column-major image. Bytes of the boundary dwords outside the codeblock are ignored.
+  const int8_t*  llr   = llrs + d.llr_offset;
+  const int      n_llr = static_cast<int>(d.nof_llr);
+  const uint32_t ncols = __umulhi(static_cast<uint32_t>(n_llr), d.div_magic);  // whole lifted columns of input
+  const uint32_t full  = ncols * static_cast<uint32_t>(Z);
+  int            last  = -1;
+  {
+    const uint32_t  head   = static_cast<uint32_t>(d.llr_offset) & 3u;
+    const uint32_t* words  = reinterpret_cast<const uint32_t*>(llr - head);
+    const int       nwords = static_cast<int>((head + static_cast<uint32_t>(n_llr) + 3u) >> 2);
+    constexpr int   BATCH  = 4;
+    for (int w0 = threadIdx.x; w0 < nwords; w0 += BATCH * blockDim.x) {
+      uint32_t val[BATCH];
+#pragma unroll
+      for (int j = 0; j < BATCH; ++j) {
+        const int w = w0 + j * blockDim.x;
+        val[j]      = (w < nwords) ? words[w] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < BATCH; ++j) {
+        const int w = w0 + j * blockDim.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t i = static_cast<uint32_t>(4 * w + k) - head;  // LLR index (wraps for head bytes)
+          if (i < static_cast<uint32_t>(n_llr)) {
+            int v = static_cast<int8_t>(val[j] >> (8 * k));
+            last  = (v != 0) ? static_cast<int>(i) : last;
+            // Soft clamp of the whole lifted columns (:152); the tail keeps its LLRs, infinities as +/-SOFT_INF.
+            v                 = (i < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
+            const uint32_t cq = __umulhi(i, d.div_magic);
+            soft[(cq + 2) * SOFT_COL_STRIDE + (i - cq * static_cast<uint32_t>(Z))] = static_cast<int8_t>(v);
+          }
+        }
+      }
+    }
+  }
+  // Zero the punctured columns 0, 1 and every position beyond the input (the image is read up to K + nof_layers
+  // columns).
   if (active) {
     soft[0 * SOFT_COL_STRIDE + z] = 0;
     soft[1 * SOFT_COL_STRIDE + z] = 0;
-    for (int c = 2; c < G::NF; ++c) {
-      const int i = (c - 2) * Z + z;
-      int       v = (i < n_llr) ? static_cast<int>(llr[i]) : 0;
-      last        = (v != 0) ? i : last;
-      v           = (i < full) ? clamp_i(v, -64, 64) : v;
-      soft[c * SOFT_COL_STRIDE + z] = static_cast<int8_t>(v);
+    int c = 2 + static_cast<int>(ncols);
+    if (static_cast<uint32_t>(n_llr) > full) {
+      if (z >= n_llr - static_cast<int>(full)) {
+        soft[c * SOFT_COL_STRIDE + z] = 0;
+      }
+      ++c;
     }
-  }
-  // Lifting shifts of this Z into LDS (read back as wave-uniform broadcasts inside the layer loop).
-  {
-    const uint16_t* gsh = shift_table + static_cast<uint32_t>(d.zpos) * G::NE;
-    for (int e = threadIdx.x; e < G::NE; e += blockDim.x) {
-      sh[e] = gsh[e];
+    for (; c < G::NF; ++c) {
+      soft[c * SOFT_COL_STRIDE + z] = 0;
     }
   }
   last = wave_max(last);
@@ -278,6 +344,8 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
   __syncthreads();
 
   const int max_iter = d.max_iter;
+  DEC_STAMP(1);
+  DEC_PROF(31, static_cast<uint64_t>(nof_layers));
   for (int it = 0; it < max_iter; ++it) {
     // Opaque per-iteration copies: stop the compiler from hoisting per-layer predicates and per-column addresses out
     // of the iteration loop (they would pin ~70 registers for values that cost one instruction to recompute).
@@ -294,6 +362,7 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
         __syncthreads();
       }
     });
+    DEC_STAMP(2 + 2 * (it & 7));
 
     // With early stopping the CRC is checked after every iteration (ldpc_decoder_impl.cpp:133); without it, once after
     // the last iteration (pusch_codeblock_decoder.cpp:53: decode without CRC, then check the CRC of the output).
@@ -326,8 +395,11 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
         tzero |= static_cast<uint32_t>(red[2 * w + 1]);
       }
       const bool early = (d.flags & DEC_FLAG_EARLY_STOP) != 0;
+      DEC_STAMP(3 + 2 * (it & 7));
       if ((tzero == 0 || !early) && tacc == 0) {
         write_hard_bits(soft, cb_out, msg_len, Z, d.div_magic);
+        DEC_STAMP(28);
+        DEC_PROF(30, __builtin_amdgcn_s_memrealtime());
         if (threadIdx.x == 0) {
           results[d.cb_index] = it + 1;
           if (cb_crc_ok != nullptr) {
@@ -339,12 +411,23 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
     }
   }
   write_hard_bits(soft, cb_out, msg_len, Z, d.div_magic);
+  DEC_STAMP(28);
+  DEC_PROF(30, __builtin_amdgcn_s_memrealtime());
   if (threadIdx.x == 0) {
     results[d.cb_index] = -1;
   }
 }
 
 } // namespace
+
+#ifdef LDPC_DEC_PROFILE
+int debug_read_decoder_profile(uint64_t* dst, size_t n)
+{
+  const size_t max = static_cast<size_t>(LDPC_DEC_PROF_CBS) * LDPC_DEC_PROF_SLOTS;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dec_prof), (n < max ? n : max) * sizeof(uint64_t)) == hipSuccess ? 0
+                                                                                                              : -1;
+}
+#endif
 
 void launch_ldpc_decode(int             bg,
                         int             mode,
@@ -354,7 +437,7 @@ void launch_ldpc_decode(int             bg,
                         const int8_t*   d_llrs,
                         uint8_t*        d_out,
                         int32_t*        d_results,
-                        const uint16_t* d_shifts,
+                        const uint32_t* d_shifts,
                         const uint32_t* d_crc_tables,
                         uint8_t*        d_cb_crc_ok,
                         hipStream_t     stream)
@@ -362,9 +445,7 @@ void launch_ldpc_decode(int             bg,
   if (nof_cbs <= 0) {
     return;
   }
-  const int    nf  = (bg == 1) ? bg_t<1>::NF : bg_t<2>::NF;
-  const int    ne  = (bg == 1) ? bg_t<1>::NE : bg_t<2>::NE;
-  const size_t lds = static_cast<size_t>(nf) * SOFT_COL_STRIDE + SCRATCH_BYTES + ne * sizeof(uint16_t);
+  const size_t lds = 0;
   dim3         grid(nof_cbs), block(block_threads);
   if (bg == 1) {
     if (mode == 1) {

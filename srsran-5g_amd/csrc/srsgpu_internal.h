@@ -137,6 +137,13 @@ void launch_pusch_tb(const tb_dec_desc* d_desc,
 /// Bytes between the packed messages of consecutive codeblocks in the PUSCH decoder's message buffer.
 constexpr uint32_t CB_MSG_STRIDE = 1056;  // 22 * 384 / 8
 
+#ifdef LDPC_DEC_PROFILE
+constexpr int LDPC_DEC_PROF_CBS   = 4096;
+constexpr int LDPC_DEC_PROF_SLOTS = 32;
+/// Copies the phase stamps of the instrumented decoder build (LDPC_DEC_PROFILE) into dst (n words).
+int debug_read_decoder_profile(uint64_t* dst, size_t n);
+#endif
+
 /// Launches the batched LDPC decoder (ldpc_decoder.hip).
 void launch_ldpc_decode(int                bg,
                         int                mode,
@@ -146,7 +153,7 @@ void launch_ldpc_decode(int                bg,
                         const int8_t*      d_llrs,
                         uint8_t*           d_out,
                         int32_t*           d_results,
-                        const uint16_t*    d_shifts,
+                        const uint32_t*    d_shifts,
                         const uint32_t*    d_crc_tables,
                         uint8_t*           d_cb_crc_ok,
                         hipStream_t        stream);

@@ -23,7 +23,8 @@ except ImportError:  # pragma: no cover - torch is part of the image
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libsrsgpu_phy.so")
+# SRSGPU_LIB selects another build of the library (e.g. an instrumented one under a different SRSGPU_OUT_DIR).
+LIB_PATH = os.environ.get("SRSGPU_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libsrsgpu_phy.so"))
 
 SRSGPU_OK = 0
 CRC24A, CRC24B, CRC24C, CRC16, CRC11, CRC6 = range(6)

@@ -214,7 +214,9 @@ int get_crc_table(srsgpu_context* ctx, int poly, int L, uint32_t& offset)
   if (!crc_params(poly, order, g)) {
     return fail(SRSGPU_ERR_INVALID_ARG, "invalid CRC polynomial %d", poly);
   }
-  if (ctx->crc_used + static_cast<size_t>(L) > CRC_ARENA_WORDS) {
+  // Tables start 16-byte aligned and are padded to whole 16-byte vectors (the decoder copies them with 16-B loads).
+  ctx->crc_used = (ctx->crc_used + 3u) & ~static_cast<size_t>(3u);
+  if (ctx->crc_used + ((static_cast<size_t>(L) + 3u) & ~static_cast<size_t>(3u)) > CRC_ARENA_WORDS) {
     return fail(SRSGPU_ERR_NO_MEMORY, "CRC table arena exhausted");
   }
   std::vector<uint32_t> tab(static_cast<size_t>(L));

@@ -22,13 +22,25 @@ __device__ __forceinline__ void static_for(F&& f)
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
+/// One DPP step of a wave reduction: v ^ (v permuted by CTRL within the enabled rows; 0 elsewhere).
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_xor(uint32_t v)
+{
+  return v ^ static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROW_MASK, 0xf, false));
+}
+
+/// XOR of v over the 64 lanes (all lanes must be active), returned to every lane. DPP steps: pairs, quads, half-rows,
+/// rows (quad_perm / mirrors), then row 0 -> 1 and 2 -> 3 (row_bcast:15) and rows 0-1 -> 2-3 (row_bcast:31): lane 63
+/// ends with the total. No LDS round trip (ds_bpermute) on the way.
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
 {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    v ^= static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), o, WAVE));
-  }
-  return v;
+  v = dpp_xor<0xb1>(v);          // quad_perm [1,0,3,2]
+  v = dpp_xor<0x4e>(v);          // quad_perm [2,3,0,1]
+  v = dpp_xor<0x141>(v);         // row_half_mirror
+  v = dpp_xor<0x140>(v);         // row_mirror
+  v = dpp_xor<0x142, 0xa>(v);    // row_bcast:15 into rows 1, 3
+  v = dpp_xor<0x143, 0xc>(v);    // row_bcast:31 into rows 2, 3
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
 }
 
 __device__ __forceinline__ int wave_max(int v)

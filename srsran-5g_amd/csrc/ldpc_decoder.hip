@@ -88,6 +88,18 @@ __device__ __forceinline__ int scale_mag(int m, uint32_t sf16, float sf)
 /// Lifting shifts are read through the scalar (constant) path: wave-uniform, compile-time offsets -> s_load.
 using const_u32_ptr = const __attribute__((address_space(4))) uint32_t*;
 
+/// Issues an s_load of sh[OFF / 4] into dst without waiting for it (scalar-cache warm-up). The caller must keep dst
+/// live until an explicit "s_waitcnt lgkmcnt(0)" (the compiler does not track this load).
+template <int OFF>
+__device__ __forceinline__ void scalar_touch(uint32_t& dst, const __attribute__((address_space(4))) uint32_t* sh)
+{
+  asm volatile("s_load_dword %0, %1, %2" : "=s"(dst) : "s"(sh), "n"(OFF));
+}
+__device__ __forceinline__ void keep_sgpr(uint32_t v)
+{
+  asm volatile("" ::"s"(v));
+}
+
 /// Unsigned median of three (v_med3_u32).
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c)
 {
@@ -238,6 +250,17 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
   }
   const int      Z      = d.Z;
   const auto     sh     = (const_u32_ptr)(uintptr_t)(shift_table + static_cast<uint32_t>(d.zpos) * G::NE);
+  // Warm the scalar cache with this Z's shift row while the LLRs load: the layers read it with s_load, and cold
+  // misses there would stall every layer of the first iteration. The destinations stay live (and unused) until the
+  // explicit wait below, so no register is reused while a load is still in flight.
+  // (Kernel arguments are pinned in SGPRs first: a later kernarg s_load would wait for the warm-up loads.)
+  asm volatile("" ::"s"(llrs), "s"(out), "s"(results), "s"(crc_tables), "s"(cb_crc_ok), "s"(blockDim.x));
+  constexpr int SH_LINES = (G::NE * 4 - 4) / 64 + 2;
+  uint32_t      pf[SH_LINES];
+  static_for<SH_LINES>([&](auto L) {
+    constexpr int l = decltype(L)::value;
+    scalar_touch<(l * 64 < G::NE * 4 - 4) ? l * 64 : G::NE * 4 - 4>(pf[l], sh);
+  });
   const int      z      = threadIdx.x;
   const bool     active = z < Z;
   const int      wave   = threadIdx.x / WAVE;
@@ -245,41 +268,88 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
   const int      lane   = threadIdx.x % WAVE;
 
   // ---- Load the LLRs into the soft-bit image (ldpc_decoder_impl.cpp:152) and find the last non-zero LLR (:94). ----
-  // Dword loads from the 4-byte aligned span covering the LLRs (every lane keeps several loads in flight), byte
-  // scatter into the column-major image. Bytes of the boundary dwords outside the codeblock are ignored.
+  // 16-byte loads from the aligned span covering the LLRs, all of a lane's loads in flight at once, then a byte
+  // scatter into the column-major image. A vector inside one lifted column of the clamped region (the common case)
+  // takes the short path: one address, a clamp per byte, a whole-vector non-zero test. Boundary vectors (head and
+  // tail of the span, column crossings, the unclamped tail of the input) go byte by byte.
   const int8_t*  llr   = llrs + d.llr_offset;
   const int      n_llr = static_cast<int>(d.nof_llr);
   const uint32_t ncols = __umulhi(static_cast<uint32_t>(n_llr), d.div_magic);  // whole lifted columns of input
   const uint32_t full  = ncols * static_cast<uint32_t>(Z);
   int            last  = -1;
+  const bool     use_crc = d.crc_table != NO_CRC_TABLE;
+  const int      nsig    = d.nof_significant;
   {
-    const uint32_t  head   = static_cast<uint32_t>(d.llr_offset) & 3u;
-    const uint32_t* words  = reinterpret_cast<const uint32_t*>(llr - head);
-    const int       nwords = static_cast<int>((head + static_cast<uint32_t>(n_llr) + 3u) >> 2);
-    constexpr int   BATCH  = 4;
-    for (int w0 = threadIdx.x; w0 < nwords; w0 += BATCH * blockDim.x) {
-      uint32_t val[BATCH];
+    const uint32_t head = static_cast<uint32_t>(d.llr_offset) & 15u;
+    const uint4*   vecs = reinterpret_cast<const uint4*>(llr - head);
+    const int      nvec = static_cast<int>((head + static_cast<uint32_t>(n_llr) + 15u) >> 4);
+    // 5 x 16 B per lane covers a whole BG1 codeblock at Z = 384 with 384 lanes (and at every smaller Z).
+    constexpr int BATCH  = 5;
+    int           last_w = -1;  // last short-path vector with a non-zero byte, and its bytes
+    uint4         last_v = make_uint4(0u, 0u, 0u, 0u);
+    for (int w0 = threadIdx.x; w0 < nvec; w0 += BATCH * blockDim.x) {
+      uint4 val[BATCH];
 #pragma unroll
       for (int j = 0; j < BATCH; ++j) {
         const int w = w0 + j * blockDim.x;
-        val[j]      = (w < nwords) ? words[w] : 0u;
+        val[j]      = (w < nvec) ? vecs[w] : make_uint4(0u, 0u, 0u, 0u);
       }
 #pragma unroll
       for (int j = 0; j < BATCH; ++j) {
         const int w = w0 + j * blockDim.x;
+        if (w >= nvec) {
+          continue;
+        }
+        const uint32_t i0 = static_cast<uint32_t>(16 * w) - head;  // LLR index of byte 0 (wraps for the head)
+        const uint32_t c0 = __umulhi(i0, d.div_magic);
+        const uint32_t l0 = i0 - c0 * static_cast<uint32_t>(Z);
+        const bool     short_path = (16u * static_cast<uint32_t>(w) >= head) && (i0 + 16u <= full) &&
+                                (l0 + 16u <= static_cast<uint32_t>(Z));
+        if (short_path) {
+          int8_t* dst = soft + (c0 + 2) * SOFT_COL_STRIDE + l0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t i = static_cast<uint32_t>(4 * w + k) - head;  // LLR index (wraps for head bytes)
-          if (i < static_cast<uint32_t>(n_llr)) {
-            int v = static_cast<int8_t>(val[j] >> (8 * k));
-            last  = (v != 0) ? static_cast<int>(i) : last;
-            // Soft clamp of the whole lifted columns (:152); the tail keeps its LLRs, infinities as +/-SOFT_INF.
-            v                 = (i < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
-            const uint32_t cq = __umulhi(i, d.div_magic);
-            soft[(cq + 2) * SOFT_COL_STRIDE + (i - cq * static_cast<uint32_t>(Z))] = static_cast<int8_t>(v);
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              dst[4 * q + k] = static_cast<int8_t>(clamp_i(static_cast<int8_t>(word >> (8 * k)), -64, 64));
+            }
+          }
+          if ((val[j].x | val[j].y | val[j].z | val[j].w) != 0u) {
+            last_w = w;
+            last_v = val[j];
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const uint32_t i = i0 + static_cast<uint32_t>(4 * q + k);
+              if (i < static_cast<uint32_t>(n_llr)) {
+                int v = static_cast<int8_t>(word >> (8 * k));
+                last  = (v != 0) ? static_cast<int>(i) : last;
+                // Soft clamp of the whole lifted columns (:152); the tail keeps its LLRs, infinities as
+                // +/-SOFT_INF.
+                v                 = (i < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
+                const uint32_t cq = __umulhi(i, d.div_magic);
+                soft[(cq + 2) * SOFT_COL_STRIDE + (i - cq * static_cast<uint32_t>(Z))] = static_cast<int8_t>(v);
+              }
+            }
           }
         }
       }
+    }
+    if (last_w >= 0) {
+      // Highest non-zero byte of the last non-zero short-path vector.
+      const uint32_t words[4] = {last_v.x, last_v.y, last_v.z, last_v.w};
+      int            hb       = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        hb = (words[q] != 0u) ? 4 * q + (31 - __clz(static_cast<int>(words[q]))) / 8 : hb;
+      }
+      const int i = 16 * last_w - static_cast<int>(head) + hb;
+      last        = i > last ? i : last;
     }
   }
   // Zero the punctured columns 0, 1 and every position beyond the input (the image is read up to K + nof_layers
@@ -311,7 +381,6 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
 
   const int  msg_len = G::K * Z;
   uint8_t*   cb_out  = out + d.out_offset;
-  const bool use_crc = d.crc_table != NO_CRC_TABLE;
   if (input_size < msg_len) {
     // Not enough LLRs: no decoding; without CRC the output is all ones (ldpc_decoder_impl.cpp:100).
     if (!use_crc) {
@@ -330,8 +399,6 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
       __builtin_amdgcn_readfirstlane(static_cast<int>(__umulhi(static_cast<uint32_t>(cb_len + Z - 1), d.div_magic)) -
                                      G::K);
 
-  const uint32_t* crc_table = crc_tables + (use_crc ? d.crc_table : 0u);
-  const int       nsig      = d.nof_significant;
   const uint32_t  sf16      = d.sf16;
   const float     sf        = d.sf;
 
@@ -343,6 +410,10 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
   }
   __syncthreads();
 
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  static_for<SH_LINES>([&](auto L) { keep_sgpr(pf[decltype(L)::value]); });
+
+  const uint32_t* crc_table = crc_tables + (use_crc ? d.crc_table : 0u);
   const int max_iter = d.max_iter;
   DEC_STAMP(1);
   DEC_PROF(31, static_cast<uint64_t>(nof_layers));

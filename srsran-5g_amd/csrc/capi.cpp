@@ -74,6 +74,8 @@ struct srsgpu_context {
   int                                  device      = 0;
   uint16_t*                            d_shifts[2] = {nullptr, nullptr};
   uint32_t*                            d_shifts32[2] = {nullptr, nullptr};  ///< Same, one dword per shift (decoder).
+  /// Packed decoder address constants (A, B) per (Z position, edge), see ldpc_decoder_pk.hip (even Z only).
+  uint32_t*                            d_pair_ab[2] = {nullptr, nullptr};
   core_plan*                           d_core[2]   = {nullptr, nullptr};
   std::vector<core_plan>               core[2];
   uint32_t*                            d_crc_arena = nullptr;
@@ -185,9 +187,11 @@ struct srsgpu_pusch_decoder_plan {
 };
 
 struct srsgpu_ldpc_decoder_plan {
-  /// One kernel launch per (base graph, block size): lanes = 64 * ceil(Z / 64) per codeblock.
+  /// One kernel launch per (base graph, kernel): even lifting sizes go to the packed two-rows-per-lane kernel
+  /// (64 * ceil(Z / 128) lanes), odd ones to the one-row-per-lane kernel (64 * ceil(Z / 64) lanes).
   struct group {
     int       bg      = 1;
+    bool      packed  = false;
     int       threads = 64;
     int       count   = 0;
     dec_desc* d_desc  = nullptr;
@@ -348,6 +352,30 @@ int srsgpu_context_create(int device, srsgpu_context** out)
     }
     // The decoder reads its shifts through scalar loads, which are dword-granular: it gets a 32-bit copy.
     std::vector<uint32_t> tab32(tab.begin(), tab.end());
+    // Packed decoder: rows z and z + H of a lane read the pair at min(2z + A, 2z + B) (row z) and its partner byte.
+    std::vector<uint32_t> ab(static_cast<size_t>(51) * ne * 2, 0u);
+    for (int p = 0; p < 51; ++p) {
+      const int Z = kLiftingSizes[p];
+      if (Z % 2 != 0) {
+        continue;
+      }
+      const int H = Z / 2;
+      for (int e = 0; e < ne; ++e) {
+        const int sft = tab[static_cast<size_t>(p) * ne + e];
+        const int hi  = sft >= H ? 1 : 0;
+        const int sm  = sft - hi * H;
+        const int A   = 2 * sm + hi;
+        const int B   = 2 * sm - 2 * H + 1 - hi;
+        ab[(static_cast<size_t>(p) * ne + e) * 2]     = static_cast<uint32_t>(A);
+        ab[(static_cast<size_t>(p) * ne + e) * 2 + 1] = static_cast<uint32_t>(B);
+      }
+    }
+    if (hipMalloc(&ctx->d_pair_ab[bg - 1], ab.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipMemcpy(ctx->d_pair_ab[bg - 1], ab.data(), ab.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      srsgpu_context_destroy(ctx);
+      return fail(SRSGPU_ERR_HIP, "failed to upload LDPC pair address tables");
+    }
     if (hipMalloc(&ctx->d_shifts[bg - 1], tab.size() * sizeof(uint16_t)) != hipSuccess ||
         hipMemcpy(ctx->d_shifts[bg - 1], tab.data(), tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice) !=
             hipSuccess ||
@@ -397,6 +425,11 @@ void srsgpu_context_destroy(srsgpu_context* ctx)
       (void)hipFree(p);
     }
   }
+  for (auto* p : ctx->d_pair_ab) {
+    if (p != nullptr) {
+      (void)hipFree(p);
+    }
+  }
   for (auto* p : ctx->d_core) {
     if (p != nullptr) {
       (void)hipFree(p);
@@ -416,8 +449,8 @@ namespace {
 /// further by block size raises the occupancy of the small-Z blocks but serialises launches; measured slower on the
 /// 100 MHz slot: 0.82 vs 0.76 ms per 16 slots.)
 struct dec_batch {
-  std::map<int, std::vector<dec_desc>> groups;
-  std::map<int, int>                   threads;
+  std::map<std::pair<int, bool>, std::vector<dec_desc>> groups;  ///< (base graph, packed kernel)
+  std::map<std::pair<int, bool>, int>                   threads;
 };
 
 /// Validates one decoder configuration (ldpc_decoder_impl.cpp:48-:56, :73-:88) and appends its descriptor.
@@ -483,9 +516,12 @@ int add_decoder_cb(srsgpu_context* ctx,
     }
     d.flags = early_stop ? DEC_FLAG_EARLY_STOP : 0u;
   }
-  batch.groups[bg].push_back(d);
-  int& t = batch.threads[bg];
-  t      = std::max(t, ((Z + 63) / 64) * 64);
+  const bool packed = (Z % 2) == 0;
+  const auto key    = std::make_pair(bg, packed);
+  batch.groups[key].push_back(d);
+  const int lanes = packed ? Z / 2 : Z;
+  int&      t     = batch.threads[key];
+  t               = std::max(t, ((lanes + 63) / 64) * 64);
   return SRSGPU_OK;
 }
 
@@ -496,7 +532,8 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
   plan->impl = impl;
   for (const auto& kv : batch.groups) {
     srsgpu_ldpc_decoder_plan::group g;
-    g.bg               = kv.first;
+    g.bg               = kv.first.first;
+    g.packed           = kv.first.second;
     g.threads          = batch.threads.at(kv.first);
     g.count            = static_cast<int>(kv.second.size());
     const size_t bytes = kv.second.size() * sizeof(dec_desc);
@@ -520,8 +557,13 @@ int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
                          hipStream_t                     s)
 {
   for (const auto& g : plan->groups) {
-    launch_ldpc_decode(g.bg, plan->impl, g.d_desc, g.count, g.threads, d_llrs, d_out, d_nof_iterations,
-                       plan->ctx->d_shifts32[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s);
+    if (g.packed) {
+      launch_ldpc_decode_pk(g.bg, plan->impl, g.d_desc, g.count, g.threads, d_llrs, d_out, d_nof_iterations,
+                            plan->ctx->d_pair_ab[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s);
+    } else {
+      launch_ldpc_decode(g.bg, plan->impl, g.d_desc, g.count, g.threads, d_llrs, d_out, d_nof_iterations,
+                         plan->ctx->d_shifts32[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s);
+    }
     HIP_TRY(hipGetLastError());
   }
   return SRSGPU_OK;
@@ -1095,9 +1137,9 @@ void srsgpu_pusch_decoder_plan_destroy(srsgpu_pusch_decoder_plan* plan)
 
 #ifdef LDPC_DEC_PROFILE
 /// Instrumented builds only: phase stamps of the last decoder launch (see ldpc_decoder.hip, DEC_STAMP).
-int srsgpu_debug_decoder_profile(uint64_t* dst, uint32_t n)
+int srsgpu_debug_decoder_profile(uint64_t* dst, uint32_t n, int packed)
 {
-  return srsgpu::debug_read_decoder_profile(dst, n);
+  return packed ? srsgpu::debug_read_decoder_profile_pk(dst, n) : srsgpu::debug_read_decoder_profile(dst, n);
 }
 #endif
 

@@ -19,32 +19,11 @@
 #include "common.h"
 #include "ldpc_base_graphs.h"
 #include "srsgpu_internal.h"
+#include "ldpc_decoder_common.h"
 
 namespace srsgpu {
 namespace {
-
-template <int BG>
-struct bg_t;
-
-template <>
-struct bg_t<1> {
-  static constexpr int M  = kBG1_M;
-  static constexpr int NF = kBG1_N_FULL;
-  static constexpr int K  = kBG1_K;
-  static constexpr int NE = kBG1_NUM_EDGES;
-  static constexpr int rs(int m) { return kBG1_ROW_START[m]; }
-  static constexpr int col(int e) { return kBG1_COL[e]; }
-};
-
-template <>
-struct bg_t<2> {
-  static constexpr int M  = kBG2_M;
-  static constexpr int NF = kBG2_N_FULL;
-  static constexpr int K  = kBG2_K;
-  static constexpr int NE = kBG2_NUM_EDGES;
-  static constexpr int rs(int m) { return kBG2_ROW_START[m]; }
-  static constexpr int col(int e) { return kBG2_COL[e]; }
-};
+using namespace ldpc_dec;
 
 #ifndef LDPC_DEC_MIN_WAVES
 #define LDPC_DEC_MIN_WAVES 4
@@ -66,54 +45,6 @@ __device__ uint64_t g_dec_prof[LDPC_DEC_PROF_CBS * LDPC_DEC_PROF_SLOTS];
   } while (0)
 #endif
 #define DEC_STAMP(slot) DEC_PROF(slot, __builtin_amdgcn_s_memtime())
-
-constexpr int LLR_MAX = 120;
-/// Sign bits of the first SIGNS_LO edges of a layer share the state word with min1 (7 b), min2 (7 b), argmin (5 b).
-constexpr int SIGNS_LO = 13;
-/// Bytes of LDS reduction scratch between the soft-bit image and the shift table.
-constexpr int SCRATCH_BYTES = 64 * sizeof(int);
-
-/// Normalisation of a check-node magnitude (0..120). MODE 1: avx2_support.h:71 scale_epi8 (16-bit fixed point,
-/// truncating); MODE 0: ldpc_decoder_generic.cpp:70 scale_llr (float, round half away from zero).
-template <int MODE>
-__device__ __forceinline__ int scale_mag(int m, uint32_t sf16, float sf)
-{
-  if constexpr (MODE == 1) {
-    return static_cast<int>((static_cast<uint32_t>(m) * sf16) >> 16);
-  } else {
-    return static_cast<int>(roundf(static_cast<float>(m) * sf));
-  }
-}
-
-/// Lifting shifts are read through the scalar (constant) path: wave-uniform, compile-time offsets -> s_load.
-using const_u32_ptr = const __attribute__((address_space(4))) uint32_t*;
-
-/// Issues an s_load of sh[OFF / 4] into dst without waiting for it (scalar-cache warm-up). The caller must keep dst
-/// live until an explicit "s_waitcnt lgkmcnt(0)" (the compiler does not track this load).
-template <int OFF>
-__device__ __forceinline__ void scalar_touch(uint32_t& dst, const __attribute__((address_space(4))) uint32_t* sh)
-{
-  asm volatile("s_load_dword %0, %1, %2" : "=s"(dst) : "s"(sh), "n"(OFF));
-}
-__device__ __forceinline__ void keep_sgpr(uint32_t v)
-{
-  asm volatile("" ::"s"(v));
-}
-
-/// Unsigned median of three (v_med3_u32).
-__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c)
-{
-  uint32_t r;
-  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-
-/// Soft bits are kept in LDS in [-LLR_MAX - 1, LLR_MAX + 1]: +/-(LLR_MAX + 1) stands for the reference's +/-infinity
-/// (LLR_INFTY = 127). The encoding is exact for inputs in the log_likelihood_ratio domain ([-120, 120] and +/-127,
-/// log_likelihood_ratio.h:65) and lets the promotion sum be a single clamp.
-constexpr int SOFT_INF = LLR_MAX + 1;
-/// Minimum search key: magnitude << 5 | edge. Ties resolve to the lowest edge as in the reference (strict '<').
-constexpr uint32_t KEY_INIT = static_cast<uint32_t>(LLR_MAX) << 5;
 
 /// One lifted check row of layer m: variable-to-check messages, min-sum analysis, check-to-variable messages and the
 /// soft-bit update (ldpc_decoder_impl.cpp:195, :255, :240).
@@ -443,13 +374,17 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
       uint32_t acc  = 0;
       uint32_t zero = 0;
       if (active) {
-        int i = zz;
+        // Unconditional table loads (index clamped, value masked): no divergent branch between them, so they are
+        // all in flight at once.
+        uint32_t       i        = static_cast<uint32_t>(zz);
+        const uint32_t last_bit = static_cast<uint32_t>(nsig) - 1u;
         static_for<G::K>([&](auto Ci) {
-          constexpr int c  = decltype(Ci)::value;
-          const int     sb = soft[c * SOFT_COL_STRIDE + zz];
+          constexpr int  c  = decltype(Ci)::value;
+          const int      sb = soft[c * SOFT_COL_STRIDE + zz];
+          const uint32_t t  = crc_table[i < last_bit ? i : last_bit];
           zero |= static_cast<uint32_t>(sb == 0);
-          acc ^= (sb <= 0 && i < nsig) ? crc_table[i] : 0u;
-          i += ZZ;
+          acc ^= (sb <= 0 && i <= last_bit) ? t : 0u;
+          i += static_cast<uint32_t>(ZZ);
         });
       }
       acc  = wave_xor(acc);

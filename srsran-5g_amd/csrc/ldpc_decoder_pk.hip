@@ -1,0 +1,563 @@
+// Batched LDPC decoder for 5G NR, two lifted check rows per lane in packed 16-bit arithmetic, for gfx950.
+//
+// Same drop-in semantics and the same bit-exact results as ldpc_decoder.hip (reference
+// lib/phy/upper/channel_coding/ldpc/ldpc_decoder_impl.cpp:60, check-node arithmetic of ldpc_decoder_avx2.cpp or
+// ldpc_decoder_generic.cpp), for even lifting sizes. The check-node update is VALU-bound, so every instruction works
+// on two rows at once: lane z (0 <= z < H = Z/2) owns rows z and z + H of every layer, and the v_pk_* 16-bit
+// instructions (add/sub/min/max/shift/mad on both halves of a VGPR) carry the two rows' messages side by side. All
+// intermediate values fit 16 bits: soft bits in [-121, 121], v2c in [-632, 632], search keys < 20243.
+//
+// LDS layout: column c of the lifted graph at c * 384, position p of the column at byte 2 * (p mod H) + (p >= H),
+// so that the positions (z + s) mod Z and (z + H + s) mod Z that a lane reads for an edge of shift s are the two
+// bytes of one pair: address a = min(2z + A_s, 2z + B_s) for a row-z value, a ^ 1 for the row-(z + H) value, with
+// A_s = 2 (s mod H) + [s >= H] and B_s = A_s - 2H + 1 - 2 [s >= H] precomputed per (Z, edge) on the host.
+//
+// Compressed check-to-variable state per layer and lane (both rows, one per 16-bit half):
+//   mag word:  min1 (7 b) | min2 (7 b) << 7            (scaled magnitudes)
+//   sign word: sign bits of edges 0..10 | argmin << 11
+//   hi word:   sign bits of edges 11..18 (the four 19-edge core rows of BG1 only)
+#include "common.h"
+#include "ldpc_base_graphs.h"
+#include "ldpc_decoder_common.h"
+#include "srsgpu_internal.h"
+
+namespace srsgpu {
+namespace {
+using namespace ldpc_dec;
+
+#ifdef LDPC_DEC_PROFILE
+__device__ uint64_t g_dec_prof_pk[LDPC_DEC_PROF_CBS * LDPC_DEC_PROF_SLOTS];
+#define DEC_PROF(slot, value)                                                                                          \
+  do {                                                                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < LDPC_DEC_PROF_CBS) {                                                          \
+      g_dec_prof_pk[blockIdx.x * LDPC_DEC_PROF_SLOTS + (slot)] = (value);                                              \
+    }                                                                                                                  \
+  } while (0)
+#else
+#define DEC_PROF(slot, value)                                                                                          \
+  do {                                                                                                                 \
+  } while (0)
+#endif
+#define DEC_STAMP(slot) DEC_PROF(slot, __builtin_amdgcn_s_memtime())
+
+typedef short          s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t bits(s16x2 v)
+{
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ uint32_t bits(u16x2 v)
+{
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ s16x2 as_s16(uint32_t v)
+{
+  return __builtin_bit_cast(s16x2, v);
+}
+__device__ __forceinline__ u16x2 as_u16(uint32_t v)
+{
+  return __builtin_bit_cast(u16x2, v);
+}
+__device__ __forceinline__ s16x2 ss(int x)
+{
+  return s16x2{static_cast<short>(x), static_cast<short>(x)};
+}
+__device__ __forceinline__ u16x2 uu(int x)
+{
+  return u16x2{static_cast<unsigned short>(x), static_cast<unsigned short>(x)};
+}
+/// 1 where IDX != e, 0 where IDX == e (both halves): one v_pk_min_u16 against an opaque 0x00010001 (a visible
+/// constant 1 gets the min rewritten into per-half compares and cndmasks).
+__device__ __forceinline__ u16x2 not_argmin(u16x2 idx, int e, u16x2 one)
+{
+  return __builtin_elementwise_min(idx - uu(e), one);  // v_pk_sub_u16 with e inline and op_sel_hi broadcast
+}
+
+__device__ __forceinline__ s16x2 clamp2(s16x2 v, int lo, int hi)
+{
+  return __builtin_elementwise_min(__builtin_elementwise_max(v, ss(lo)), ss(hi));
+}
+
+/// Fixed-point normalisation parameters: MODE 1 scales m by (m * sf16) >> 16, evaluated in 16-bit halves as
+/// ((m * hi) + ((m * lo) >> 8)) >> 8 with sf16 = hi * 256 + lo (exact: every product stays below 2^16).
+struct scale_t {
+  u16x2 hi;
+  u16x2 lo;
+  float sf;
+};
+
+template <int MODE>
+__device__ __forceinline__ u16x2 scale_pk(u16x2 m, const scale_t& sc)
+{
+  if constexpr (MODE == 1) {
+    const u16x2 l = (m * sc.lo) >> uu(8);
+    return (m * sc.hi + l) >> uu(8);
+  } else {
+    // ldpc_decoder_generic.cpp:70 scale_llr: round half away from zero of m * sf (m >= 0).
+    const unsigned short a = static_cast<unsigned short>(roundf(static_cast<float>(m.x) * sc.sf));
+    const unsigned short b = static_cast<unsigned short>(roundf(static_cast<float>(m.y) * sc.sf));
+    return u16x2{a, b};
+  }
+}
+
+#ifndef LDPC_PK_CRC_CHUNK
+#define LDPC_PK_CRC_CHUNK 8
+#endif
+/// Systematic columns per batch of CRC table loads.
+constexpr int CRC_CHUNK = LDPC_PK_CRC_CHUNK;
+
+/// Sign bits of edge e: bit e (e < 11) of the sign word or bit e - 11 of the hi word, in both halves.
+constexpr int SIGNS_W0 = 11;
+
+/// Two lifted check rows (z, z + H) of layer m: v2c messages, min-sum analysis, c2v messages, soft-bit update
+/// (ldpc_decoder_impl.cpp:195, :255, :240; arithmetic of ldpc_decoder_avx2.cpp:69/:111/:165/:205).
+template <int BG, int MODE, int m>
+__device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
+                                              const_u32_ptr  ab,  // (A, B) address constants of this Z, per edge
+                                              uint32_t       z2,
+                                              const scale_t& sc,
+                                              uint32_t&      magw,
+                                              uint32_t&      sgw,
+                                              uint32_t&      hiw)
+{
+  using G           = bg_t<BG>;
+  constexpr int e0  = G::rs(m);
+  constexpr int deg = G::rs(m + 1) - e0;
+  static_assert(deg <= SIGNS_W0 + 8, "at most 19 edges per row");
+  const u16x2 S1  = as_u16(magw & 0x007f007fu);
+  const u16x2 S2  = as_u16((magw >> 7) & 0x007f007fu);
+  const u16x2 D   = S1 - S2;
+  const u16x2 IDX = as_u16(sgw) >> uu(11);
+  s16x2       v2c[deg];
+  uint32_t    addr[deg];
+  u16x2       k1 = uu(KEY_INIT), k2 = uu(KEY_INIT);
+  uint32_t    sx = 0;
+  uint32_t    one_bits = 0x00010001u;
+  asm("" : "+v"(one_bits));
+  const u16x2 one = as_u16(one_bits);
+
+  static_for<deg>([&](auto E) {
+    constexpr int  e   = decltype(E)::value;
+    constexpr int  col = G::col(e0 + e);
+    const uint32_t pa  = z2 + ab[2 * (e0 + e)];
+    const uint32_t pb  = z2 + ab[2 * (e0 + e) + 1];
+    const uint32_t a   = pa < pb ? pa : pb;
+    addr[e]            = a;
+    // Two byte loads merged by one v_perm (d16 loads do not preserve the other half with SRAM ECC on gfx950).
+    const s16x2 sb{static_cast<short>(soft[col * SOFT_COL_STRIDE + a]),
+                   static_cast<short>(soft[col * SOFT_COL_STRIDE + (a ^ 1u)])};
+    // Previous c2v of this edge: magnitude min2 at the argmin, min1 elsewhere; sign from the sign bits.
+    constexpr int  pos = (e < SIGNS_W0) ? e : e - SIGNS_W0;
+    const uint32_t sw  = (e < SIGNS_W0) ? sgw : hiw;
+    const s16x2    n   = (as_s16(sw) << ss(15 - pos)) >> ss(15);
+    const u16x2    ne  = not_argmin(IDX, e, one);
+    const u16x2    om  = ne * D + S2;
+    const s16x2    c   = as_s16(bits(om) ^ bits(n)) - n;
+    // v2c = soft - c2v saturated to +/-LLR_MAX; infinite soft bits give |v2c| >= 392 (stay infinite).
+    const s16x2 fin = clamp2(sb, -LLR_MAX, LLR_MAX);
+    const s16x2 v   = clamp2(sb - c, -LLR_MAX, LLR_MAX) + (sb - fin) * ss(512);
+    v2c[e]          = v;
+    const u16x2 key = __builtin_bit_cast(u16x2, __builtin_elementwise_max(v, -v)) * uu(32) + uu(e);
+    k2              = __builtin_elementwise_min(__builtin_elementwise_max(key, k1), k2);
+    k1              = __builtin_elementwise_min(key, k1);
+    sx ^= bits(v);
+  });
+
+  const u16x2 IDXN = k1 & uu(31);
+  const u16x2 S1N  = scale_pk<MODE>(k1 >> uu(5), sc);
+  const u16x2 S2N  = scale_pk<MODE>(k2 >> uu(5), sc);
+  const u16x2 DN   = S1N - S2N;
+  uint32_t    nsg  = bits(IDXN << uu(11));
+  uint32_t    nhi  = 0;
+
+  static_for<deg>([&](auto E) {
+    constexpr int e   = decltype(E)::value;
+    constexpr int col = G::col(e0 + e);
+    const s16x2   v   = v2c[e];
+    // c2v sign = product of the other edges' signs; magnitude min2 at the argmin, min1 elsewhere.
+    const s16x2 n   = as_s16(sx ^ bits(v)) >> ss(15);
+    const u16x2 ne  = not_argmin(IDXN, e, one);
+    const u16x2 mag = ne * DN + S2N;
+    const s16x2 c   = as_s16(bits(mag) ^ bits(n)) - n;
+    // Promotion sum (log_likelihood_ratio.cpp:75): |sum| > LLR_MAX becomes +/-infinity (SOFT_INF).
+    const s16x2    sb = clamp2(c + v, -SOFT_INF, SOFT_INF);
+    const uint32_t a  = addr[e];
+    soft[col * SOFT_COL_STRIDE + a]        = static_cast<int8_t>(sb.x);
+    soft[col * SOFT_COL_STRIDE + (a ^ 1u)] = static_cast<int8_t>(sb.y);
+    constexpr int      pos  = (e < SIGNS_W0) ? e : e - SIGNS_W0;
+    constexpr uint32_t mask = (1u << pos) | (1u << (16 + pos));
+    if constexpr (e < SIGNS_W0) {
+      nsg |= bits(n) & mask;
+    } else {
+      nhi |= bits(n) & mask;
+    }
+  });
+  magw = bits(S1N | (S2N << uu(7)));
+  sgw  = nsg;
+  if constexpr (deg > SIGNS_W0) {
+    hiw = nhi;
+  }
+}
+
+/// LDS byte offset of position l (0 <= l < Z) inside a column.
+__device__ __forceinline__ uint32_t pair_pos(uint32_t l, uint32_t H)
+{
+  return (l < H) ? 2u * l : 2u * (l - H) + 1u;
+}
+
+/// Hard decisions of the K*Z systematic bits, packed MSB first (log_likelihood_ratio.cpp:350 hard_decision).
+__device__ __forceinline__ void write_hard_bits_pk(const int8_t* __restrict__ soft,
+                                                   uint8_t* __restrict__ out,
+                                                   int      nbits,
+                                                   int      Z,
+                                                   uint32_t magic)
+{
+  const uint32_t H      = static_cast<uint32_t>(Z) / 2u;
+  const int      nbytes = (nbits + 7) / 8;
+  for (int b = threadIdx.x; b < nbytes; b += blockDim.x) {
+    uint32_t byte = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = 8 * b + k;
+      if (i < nbits) {
+        const uint32_t col = __umulhi(static_cast<uint32_t>(i), magic);
+        const uint32_t l   = static_cast<uint32_t>(i) - col * static_cast<uint32_t>(Z);
+        byte |= static_cast<uint32_t>(soft[col * SOFT_COL_STRIDE + pair_pos(l, H)] <= 0) << (7 - k);
+      }
+    }
+    out[b] = static_cast<uint8_t>(byte);
+  }
+}
+
+template <int BG, int MODE>
+__global__ __launch_bounds__(192, 3) void ldpc_decode_pk_kernel(const dec_desc* __restrict__ descs,
+                                                             const int8_t* __restrict__ llrs,
+                                                             uint8_t* __restrict__ out,
+                                                             int32_t* __restrict__ results,
+                                                             const uint32_t* __restrict__ ab_table,
+                                                             const uint32_t* __restrict__ crc_tables,
+                                                             uint8_t* __restrict__ cb_crc_ok)
+{
+  using G = bg_t<BG>;
+  __shared__ __attribute__((aligned(16))) int8_t smem[G::NF * SOFT_COL_STRIDE + SCRATCH_BYTES];
+  int8_t* soft    = smem;
+  int*    scratch = reinterpret_cast<int*>(smem + G::NF * SOFT_COL_STRIDE);
+
+  DEC_STAMP(0);
+  DEC_PROF(29, __builtin_amdgcn_s_memrealtime());
+  const dec_desc d = descs[blockIdx.x];
+  // HARQ context (pusch_decoder_impl.cpp:300): a codeblock whose CRC already passed is not decoded again.
+  if (cb_crc_ok != nullptr && cb_crc_ok[d.cb_index] != 0) {
+    if (threadIdx.x == 0) {
+      results[d.cb_index] = 0;
+    }
+    return;
+  }
+  const int      Z  = d.Z;
+  const uint32_t H  = static_cast<uint32_t>(Z) / 2u;
+  const auto     ab = (const_u32_ptr)(uintptr_t)(ab_table + static_cast<uint32_t>(d.zpos) * 2u * G::NE);
+  asm volatile("" ::"s"(llrs), "s"(out), "s"(results), "s"(crc_tables), "s"(cb_crc_ok), "s"(blockDim.x));
+  // Scalar-cache warm-up of this Z's address constants while the LLRs load (see ldpc_decoder.hip).
+  constexpr int AB_BYTES = G::NE * 8;
+  constexpr int AB_LINES = (AB_BYTES - 4) / 64 + 2;
+  uint32_t      pf[AB_LINES];
+  static_for<AB_LINES>([&](auto L) {
+    constexpr int l = decltype(L)::value;
+    scalar_touch<(l * 64 < AB_BYTES - 4) ? l * 64 : AB_BYTES - 4>(pf[l], ab);
+  });
+  const int  z      = threadIdx.x;
+  const bool active = static_cast<uint32_t>(z) < H;
+  const int  wave   = threadIdx.x / WAVE;
+  const int  nwaves = blockDim.x / WAVE;
+  const int  lane   = threadIdx.x % WAVE;
+
+  // ---- LLRs -> soft-bit image (ldpc_decoder_impl.cpp:152), last non-zero LLR (:94); as ldpc_decoder.hip but with
+  // the pair layout: a 16-byte vector inside one half of one column is a stride-2 run of bytes. ----
+  const int8_t*  llr   = llrs + d.llr_offset;
+  const int      n_llr = static_cast<int>(d.nof_llr);
+  const uint32_t ncols = __umulhi(static_cast<uint32_t>(n_llr), d.div_magic);
+  const uint32_t full  = ncols * static_cast<uint32_t>(Z);
+  int            last  = -1;
+  {
+    const uint32_t head   = static_cast<uint32_t>(d.llr_offset) & 15u;
+    const uint4*   vecs   = reinterpret_cast<const uint4*>(llr - head);
+    const int      nvec   = static_cast<int>((head + static_cast<uint32_t>(n_llr) + 15u) >> 4);
+    constexpr int  BATCH  = 9;  // 9 x 16 B per lane: a whole BG1 codeblock at Z = 384 with 192 lanes
+    int            last_w = -1;
+    uint4          last_v = make_uint4(0u, 0u, 0u, 0u);
+    for (int w0 = threadIdx.x; w0 < nvec; w0 += BATCH * blockDim.x) {
+      uint4 val[BATCH];
+#pragma unroll
+      for (int j = 0; j < BATCH; ++j) {
+        const int w = w0 + j * blockDim.x;
+        val[j]      = (w < nvec) ? vecs[w] : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int j = 0; j < BATCH; ++j) {
+        const int w = w0 + j * blockDim.x;
+        if (w >= nvec) {
+          continue;
+        }
+        const uint32_t i0 = static_cast<uint32_t>(16 * w) - head;
+        const uint32_t c0 = __umulhi(i0, d.div_magic);
+        const uint32_t l0 = i0 - c0 * static_cast<uint32_t>(Z);
+        const bool     one_half   = (l0 + 16u <= H) || (l0 >= H && l0 + 16u <= static_cast<uint32_t>(Z));
+        const bool     short_path = (16u * static_cast<uint32_t>(w) >= head) && (i0 + 16u <= full) && one_half;
+        if (short_path) {
+          int8_t* dst = soft + (c0 + 2) * SOFT_COL_STRIDE + pair_pos(l0, H);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              dst[2 * (4 * q + k)] = static_cast<int8_t>(clamp_i(static_cast<int8_t>(word >> (8 * k)), -64, 64));
+            }
+          }
+          if ((val[j].x | val[j].y | val[j].z | val[j].w) != 0u) {
+            last_w = w;
+            last_v = val[j];
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const uint32_t i = i0 + static_cast<uint32_t>(4 * q + k);
+              if (i < static_cast<uint32_t>(n_llr)) {
+                int v = static_cast<int8_t>(word >> (8 * k));
+                last  = (v != 0) ? static_cast<int>(i) : last;
+                v     = (i < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
+                const uint32_t cq = __umulhi(i, d.div_magic);
+                soft[(cq + 2) * SOFT_COL_STRIDE + pair_pos(i - cq * static_cast<uint32_t>(Z), H)] =
+                    static_cast<int8_t>(v);
+              }
+            }
+          }
+        }
+      }
+    }
+    if (last_w >= 0) {
+      const uint32_t words[4] = {last_v.x, last_v.y, last_v.z, last_v.w};
+      int            hb       = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        hb = (words[q] != 0u) ? 4 * q + (31 - __clz(static_cast<int>(words[q]))) / 8 : hb;
+      }
+      const int i = 16 * last_w - static_cast<int>(head) + hb;
+      last        = i > last ? i : last;
+    }
+  }
+  // Zero the punctured columns 0, 1 and every position beyond the input.
+  if (active) {
+    auto* soft16 = reinterpret_cast<uint16_t*>(soft);
+    soft16[(0 * SOFT_COL_STRIDE) / 2 + z] = 0;
+    soft16[(1 * SOFT_COL_STRIDE) / 2 + z] = 0;
+    int c = 2 + static_cast<int>(ncols);
+    if (static_cast<uint32_t>(n_llr) > full) {
+      const uint32_t rem = static_cast<uint32_t>(n_llr) - full;
+      if (static_cast<uint32_t>(z) >= rem) {
+        soft[c * SOFT_COL_STRIDE + 2 * z] = 0;
+      }
+      if (static_cast<uint32_t>(z) + H >= rem) {
+        soft[c * SOFT_COL_STRIDE + 2 * z + 1] = 0;
+      }
+      ++c;
+    }
+    for (; c < G::NF; ++c) {
+      soft16[(c * SOFT_COL_STRIDE) / 2 + z] = 0;
+    }
+  }
+  last = wave_max(last);
+  if (lane == 0) {
+    scratch[wave] = last;
+  }
+  __syncthreads();
+  int input_size = scratch[0];
+  for (int w = 1; w < nwaves; ++w) {
+    input_size = scratch[w] > input_size ? scratch[w] : input_size;
+  }
+  input_size += 1;
+
+  const int  msg_len = G::K * Z;
+  uint8_t*   cb_out  = out + d.out_offset;
+  const bool use_crc = d.crc_table != NO_CRC_TABLE;
+  if (input_size < msg_len) {
+    // Not enough LLRs: no decoding; without CRC the output is all ones (ldpc_decoder_impl.cpp:100).
+    if (!use_crc) {
+      for (int b = threadIdx.x; b < (msg_len + 7) / 8; b += blockDim.x) {
+        cb_out[b] = 0xff;
+      }
+    }
+    if (threadIdx.x == 0) {
+      results[d.cb_index] = -1;
+    }
+    return;
+  }
+  int cb_len = input_size + 2 * Z;
+  cb_len     = cb_len > msg_len + 4 * Z ? cb_len : msg_len + 4 * Z;
+  const int nof_layers =
+      __builtin_amdgcn_readfirstlane(static_cast<int>(__umulhi(static_cast<uint32_t>(cb_len + Z - 1), d.div_magic)) -
+                                     G::K);
+
+  const uint32_t* crc_table = crc_tables + (use_crc ? d.crc_table : 0u);
+  const int       nsig      = d.nof_significant;
+  scale_t         sc;
+  sc.hi = uu(static_cast<int>(d.sf16 >> 8));
+  sc.lo = uu(static_cast<int>(d.sf16 & 255u));
+  sc.sf = d.sf;
+
+  uint32_t magw[G::M], sgw[G::M];
+  uint32_t hiw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int m = 0; m < G::M; ++m) {
+    magw[m] = 0;
+    sgw[m]  = 0;
+  }
+  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  static_for<AB_LINES>([&](auto L) { keep_sgpr(pf[decltype(L)::value]); });
+
+  const int max_iter = d.max_iter;
+  DEC_STAMP(1);
+  DEC_PROF(31, static_cast<uint64_t>(nof_layers));
+  for (int it = 0; it < max_iter; ++it) {
+    // Opaque per-iteration copies (see ldpc_decoder.hip).
+    int           nl  = nof_layers;
+    uint32_t      z2  = 2u * static_cast<uint32_t>(z);
+    const_u32_ptr abi = ab;
+    asm volatile("" : "+s"(nl));
+    asm volatile("" : "+v"(z2));
+    asm volatile("" : "+s"(abi));
+    static_for<G::M>([&](auto Mi) {
+      constexpr int m = decltype(Mi)::value;
+      if (m < nl) {
+        if (active) {
+          __builtin_amdgcn_sched_barrier(0);
+          row_update_pk<BG, MODE, m>(soft, abi, z2, sc, magw[m], sgw[m], hiw[m & 3]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();
+      }
+    });
+    DEC_STAMP(2 + 2 * (it & 7));
+
+    // CRC after every iteration with early stop (ldpc_decoder_impl.cpp:133), else after the last one.
+    if (use_crc && ((d.flags & DEC_FLAG_EARLY_STOP) != 0 || it == max_iter - 1)) {
+      uint32_t acc  = 0;
+      uint32_t zero = 0;
+      if (active) {
+        // Opaque copies again: per-column table offsets would otherwise be hoisted out of the iteration loop. The
+        // table loads are unconditional (index clamped, value masked): no divergent branches between them, all of
+        // a chunk's loads in flight at once, saddr form (global base in SGPRs + 32-bit byte offset).
+        uint32_t zz   = static_cast<uint32_t>(z);
+        uint32_t ZZ   = static_cast<uint32_t>(Z);
+        uint32_t HH   = H;
+        uint32_t last_bit = static_cast<uint32_t>(nsig) - 1u;
+        asm volatile("" : "+v"(zz));
+        asm volatile("" : "+s"(ZZ), "+s"(HH), "+s"(last_bit));
+        uint32_t ia = zz;
+        static_for<G::K>([&](auto Ci) {
+          constexpr int  c  = decltype(Ci)::value;
+          const uint32_t ib = ia + HH;
+          const int      sa = soft[c * SOFT_COL_STRIDE + 2 * zz];
+          const int      sb = soft[c * SOFT_COL_STRIDE + 2 * zz + 1];
+          zero |= static_cast<uint32_t>(sa == 0) | static_cast<uint32_t>(sb == 0);
+          const uint32_t ta = crc_table[ia < last_bit ? ia : last_bit];
+          const uint32_t tb = crc_table[ib < last_bit ? ib : last_bit];
+          acc ^= (sa <= 0 && ia <= last_bit) ? ta : 0u;
+          acc ^= (sb <= 0 && ib <= last_bit) ? tb : 0u;
+          ia += ZZ;
+          // Bound the table loads in flight (each holds a result register).
+          if constexpr (c % CRC_CHUNK == CRC_CHUNK - 1) {
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        });
+      }
+      acc      = wave_xor(acc);
+      zero     = (__ballot(zero != 0) != 0) ? 1u : 0u;
+      int* red = scratch + 8 + 16 * (it & 1);
+      if (lane == 0) {
+        red[2 * wave]     = static_cast<int>(acc);
+        red[2 * wave + 1] = static_cast<int>(zero);
+      }
+      __syncthreads();
+      uint32_t tacc = 0, tzero = 0;
+      for (int w = 0; w < nwaves; ++w) {
+        tacc ^= static_cast<uint32_t>(red[2 * w]);
+        tzero |= static_cast<uint32_t>(red[2 * w + 1]);
+      }
+      const bool early = (d.flags & DEC_FLAG_EARLY_STOP) != 0;
+      DEC_STAMP(3 + 2 * (it & 7));
+      if ((tzero == 0 || !early) && tacc == 0) {
+        write_hard_bits_pk(soft, cb_out, msg_len, Z, d.div_magic);
+        DEC_STAMP(28);
+        DEC_PROF(30, __builtin_amdgcn_s_memrealtime());
+        if (threadIdx.x == 0) {
+          results[d.cb_index] = it + 1;
+          if (cb_crc_ok != nullptr) {
+            cb_crc_ok[d.cb_index] = 1;
+          }
+        }
+        return;
+      }
+    }
+  }
+  write_hard_bits_pk(soft, cb_out, msg_len, Z, d.div_magic);
+  DEC_STAMP(28);
+  DEC_PROF(30, __builtin_amdgcn_s_memrealtime());
+  if (threadIdx.x == 0) {
+    results[d.cb_index] = -1;
+  }
+}
+
+} // namespace
+
+#ifdef LDPC_DEC_PROFILE
+int debug_read_decoder_profile_pk(uint64_t* dst, size_t n)
+{
+  const size_t max = static_cast<size_t>(LDPC_DEC_PROF_CBS) * LDPC_DEC_PROF_SLOTS;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dec_prof_pk), (n < max ? n : max) * sizeof(uint64_t)) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
+
+void launch_ldpc_decode_pk(int             bg,
+                           int             mode,
+                           const dec_desc* d_desc,
+                           int             nof_cbs,
+                           int             block_threads,
+                           const int8_t*   d_llrs,
+                           uint8_t*        d_out,
+                           int32_t*        d_results,
+                           const uint32_t* d_ab,
+                           const uint32_t* d_crc_tables,
+                           uint8_t*        d_cb_crc_ok,
+                           hipStream_t     stream)
+{
+  if (nof_cbs <= 0) {
+    return;
+  }
+  dim3 grid(nof_cbs), block(block_threads);
+  if (bg == 1) {
+    if (mode == 1) {
+      ldpc_decode_pk_kernel<1, 1><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables,
+                                                              d_cb_crc_ok);
+    } else {
+      ldpc_decode_pk_kernel<1, 0><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables,
+                                                              d_cb_crc_ok);
+    }
+  } else {
+    if (mode == 1) {
+      ldpc_decode_pk_kernel<2, 1><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables,
+                                                              d_cb_crc_ok);
+    } else {
+      ldpc_decode_pk_kernel<2, 0><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables,
+                                                              d_cb_crc_ok);
+    }
+  }
+}
+
+} // namespace srsgpu

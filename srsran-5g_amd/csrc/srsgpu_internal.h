@@ -142,7 +142,22 @@ constexpr int LDPC_DEC_PROF_CBS   = 4096;
 constexpr int LDPC_DEC_PROF_SLOTS = 32;
 /// Copies the phase stamps of the instrumented decoder build (LDPC_DEC_PROFILE) into dst (n words).
 int debug_read_decoder_profile(uint64_t* dst, size_t n);
+int debug_read_decoder_profile_pk(uint64_t* dst, size_t n);
 #endif
+
+/// Launches the packed two-rows-per-lane LDPC decoder (ldpc_decoder_pk.hip; even Z, block_threads >= Z / 2).
+void launch_ldpc_decode_pk(int             bg,
+                           int             mode,
+                           const dec_desc* d_desc,
+                           int             nof_cbs,
+                           int             block_threads,
+                           const int8_t*   d_llrs,
+                           uint8_t*        d_out,
+                           int32_t*        d_results,
+                           const uint32_t* d_ab,
+                           const uint32_t* d_crc_tables,
+                           uint8_t*        d_cb_crc_ok,
+                           hipStream_t     stream);
 
 /// Launches the batched LDPC decoder (ldpc_decoder.hip).
 void launch_ldpc_decode(int                bg,

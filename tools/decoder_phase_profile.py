@@ -77,8 +77,11 @@ def main():
 
     n = min(cb_total, 4096)
     buf = np.zeros(n * SLOTS, dtype=np.uint64)
-    lib.srsgpu_debug_decoder_profile.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
-    assert lib.srsgpu_debug_decoder_profile(buf.ctypes.data, buf.size) == 0
+    lib.srsgpu_debug_decoder_profile.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
+    # Even lifting sizes run on the packed kernel (its own stamp array); fall back to the one-row kernel's.
+    assert lib.srsgpu_debug_decoder_profile(buf.ctypes.data, buf.size, 1) == 0
+    if not buf.any():
+        assert lib.srsgpu_debug_decoder_profile(buf.ctypes.data, buf.size, 0) == 0
     p = buf.reshape(n, SLOTS).astype(np.int64)
     it = iters.cpu().numpy()[:n]
     nit = np.where(it > 0, it, args.iterations)

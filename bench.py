@@ -115,6 +115,8 @@ def main():
     ap.add_argument("--worst-case", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--serial-legs", action="store_true",
+                    help="run the DL and UL legs on one stream (clean per-stage times; slower overall)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -168,11 +170,19 @@ def main():
     d_iters = torch.zeros(cb_total, dtype=torch.int32, device=dev)
     d_ul_tbs = torch.zeros(ul_tb_total, dtype=torch.uint8, device=dev)
     d_tb_ok = torch.zeros(nof_tbs, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # The DL and UL legs are independent (as in a gNB, where PDSCH and PUSCH processing of a slot run concurrently):
+    # each gets its own HIP stream, joined back into the main stream at the end of every step.
+    main_stream = torch.cuda.current_stream(dev)
+    dl_stream = torch.cuda.Stream(dev)
+    ul_stream = dl_stream if args.serial_legs else torch.cuda.Stream(dev)
 
     def step():
-        dl_plan.execute(d_dl_tbs, d_dl_cw, stream)
-        ul_plan.execute(d_llrs, d_harq, d_crc, d_msgs, d_iters, d_ul_tbs, d_tb_ok, stream)
+        dl_stream.wait_stream(main_stream)
+        ul_stream.wait_stream(main_stream)
+        dl_plan.execute(d_dl_tbs, d_dl_cw, dl_stream)
+        ul_plan.execute(d_llrs, d_harq, d_crc, d_msgs, d_iters, d_ul_tbs, d_tb_ok, ul_stream)
+        main_stream.wait_stream(dl_stream)
+        main_stream.wait_stream(ul_stream)
 
     for _ in range(args.warmup):
         step()
@@ -249,7 +259,9 @@ def main():
         "data": "synthetic: random TB payloads; PUSCH LLRs = " + data_desc,
         "config": {"workload": "n78 100 MHz 4x4 slot, 273 PRB, 64 UEs x (4-5 PRB, 4 layers, 256QAM MCS27), LDPC BG1 "
                                "(Z 288/352): 64 TBs / 192 codeblocks per direction per slot",
-                   "legs": ["pdsch_encode", "pusch_decode"], "slots_per_step": S,
+                   "legs": ["pdsch_encode", "pusch_decode"],
+                   "leg_streams": "one stream" if args.serial_legs else "DL and UL on concurrent streams",
+                   "slots_per_step": S,
                    "codeblocks_per_step_per_direction": int(sum(nof_cbs)),
                    "ldpc_max_iterations": args.iterations, "ldpc_early_stop": True,
                    "decoder_arithmetic": "avx2/avx512 (SIMD) variant, bit-exact",

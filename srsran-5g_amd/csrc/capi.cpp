@@ -66,7 +66,7 @@ bool crc_params(int poly, unsigned& order, uint64_t& g)
   }
 }
 
-constexpr size_t CRC_ARENA_WORDS = 4u << 20;  // 16 MiB of contribution tables
+constexpr size_t CRC_ARENA_WORDS = 16u << 20;  // 64 MiB of contribution tables
 
 } // namespace
 
@@ -245,6 +245,20 @@ int get_crc_table(srsgpu_context* ctx, int poly, int L, uint32_t& offset)
   ctx->crc_tables.emplace(key, ctx->crc_used);
   ctx->crc_used += static_cast<size_t>(L);
   return SRSGPU_OK;
+}
+
+/// Contribution table for an optional fast path: its arena offset, or NO_CRC_TABLE (no error) when the arena has no
+/// room left for it.
+uint32_t try_crc_table(srsgpu_context* ctx, int poly, int L)
+{
+  const auto key = std::make_pair(poly, L);
+  if (ctx->crc_tables.find(key) == ctx->crc_tables.end() &&
+      ((ctx->crc_used + 3u) & ~static_cast<size_t>(3u)) + ((static_cast<size_t>(L) + 3u) & ~static_cast<size_t>(3u)) >
+          CRC_ARENA_WORDS) {
+    return NO_CRC_TABLE;
+  }
+  uint32_t off = NO_CRC_TABLE;
+  return get_crc_table(ctx, poly, L, off) == SRSGPU_OK ? off : NO_CRC_TABLE;
 }
 
 /// Solves the core of the lifted base graph (rows 0..3 x parity columns K..K+3) once per (BG, Z), like
@@ -628,6 +642,8 @@ int add_pusch_cb(srsgpu_context*        ctx,
   d.Qm          = static_cast<uint8_t>(qm);
   d.new_data    = c.new_data ? 1 : 0;
   d.cb_index    = c.cb_index;
+  const uint64_t R = c.E / static_cast<uint32_t>(qm);
+  d.r_magic        = ((1ULL << 40) + R - 1) / R;
   dms.push_back(d);
   return add_decoder_cb(ctx, c.cb_index, c.bg, Z, c.filler, c.nof_crc_bits, c.max_iter, c.sf, c.crc_poly,
                         c.early_stop, c.harq_offset, static_cast<uint32_t>(N), c.out_offset, batch);
@@ -839,7 +855,10 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
       return fail(SRSGPU_ERR_INVALID_ARG, "tb %u: %s", t, err.c_str());
     }
     tbd[t] = {c.tb_offset, c.tbs_bytes, seg.tb_crc_len == 24 ? 0x1864cfbu : 0x11021u,
-              static_cast<uint32_t>(seg.tb_crc_len)};
+              static_cast<uint32_t>(seg.tb_crc_len), NO_CRC_TABLE};
+    // TB CRC from a per-bit table (cached per length); when the arena is full the kernel uses the byte-table method.
+    tbd[t].table = try_crc_table(ctx, seg.tb_crc_len == 24 ? SRSGPU_CRC24A : SRSGPU_CRC16,
+                                 static_cast<int>(c.tbs_bytes) * 8);
     const int Z    = seg.Z;
     const int pos  = lifting_position(Z);
     const int N    = (((seg.bg == 1) ? kBG1_N_FULL : kBG2_N_FULL) - 2) * Z;
@@ -944,7 +963,7 @@ int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
   if (plan->out_end > plan->out_begin) {
     HIP_TRY(hipMemsetAsync(d_codewords + plan->out_begin, 0, plan->out_end - plan->out_begin, s));
   }
-  launch_tb_crc(plan->d_tb, plan->nof_tbs, d_tbs, plan->d_tb_crc, s);
+  launch_tb_crc(plan->d_tb, plan->nof_tbs, d_tbs, plan->d_tb_crc, plan->ctx->d_crc_arena, s);
   HIP_TRY(hipGetLastError());
   stage_timer::mark(ev, 1, s);
   for (int b = 0; b < 2; ++b) {
@@ -1046,6 +1065,7 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
     d.data_magic   = static_cast<uint32_t>(((1ULL << 32) + d.cb_data_bits - 1) / d.cb_data_bits);
     d.tb_offset    = c.tb_offset;
     d.tb_index     = t;
+    d.crc_table    = (seg.C > 1) ? try_crc_table(ctx, SRSGPU_CRC24A, seg.tbs) : NO_CRC_TABLE;
   }
   auto* plan    = new srsgpu_pusch_decoder_plan();
   plan->ctx     = ctx;
@@ -1095,7 +1115,7 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
     return r;
   }
   stage_timer::mark(ev, 2, s);
-  launch_pusch_tb(plan->d_tb, plan->nof_tbs, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, s);
+  launch_pusch_tb(plan->d_tb, plan->nof_tbs, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, plan->ctx->d_crc_arena, s);
   HIP_TRY(hipGetLastError());
   stage_timer::mark(ev, 3, s);
   return SRSGPU_OK;

@@ -77,4 +77,38 @@ __device__ inline uint32_t block_crc_bytes(const uint8_t* data, int n, int order
   return crc;
 }
 
+/// CRC of data[0..nbytes) from the per-bit contribution table P of the message length L = 8 * nbytes
+/// (P[i] = x^(order + L - 1 - i) mod g, 16-byte aligned): the CRC is the XOR of P[i] over the set message bits. Each
+/// lane takes whole bytes and reads their 8 contributions as two 16-byte vectors (no dependent chain, no GF(2)
+/// products). `red` is LDS scratch of one word per wave. Returns the CRC in every lane; all lanes must call it.
+__device__ inline uint32_t block_crc_table(const uint8_t* data, int nbytes, const uint32_t* P, uint32_t* red)
+{
+  uint32_t acc = 0;
+  for (int j = threadIdx.x; j < nbytes; j += blockDim.x) {
+    const uint32_t byte = data[j];
+    const uint4*   p4   = reinterpret_cast<const uint4*>(P + 8 * j);
+    const uint4    a    = p4[0];
+    const uint4    b    = p4[1];
+    acc ^= (byte & 0x80u) ? a.x : 0u;
+    acc ^= (byte & 0x40u) ? a.y : 0u;
+    acc ^= (byte & 0x20u) ? a.z : 0u;
+    acc ^= (byte & 0x10u) ? a.w : 0u;
+    acc ^= (byte & 0x08u) ? b.x : 0u;
+    acc ^= (byte & 0x04u) ? b.y : 0u;
+    acc ^= (byte & 0x02u) ? b.z : 0u;
+    acc ^= (byte & 0x01u) ? b.w : 0u;
+  }
+  acc = wave_xor(acc);
+  if ((threadIdx.x % WAVE) == 0) {
+    red[threadIdx.x / WAVE] = acc;
+  }
+  __syncthreads();
+  uint32_t crc = 0;
+  for (int w = 0; w < static_cast<int>(blockDim.x / WAVE); ++w) {
+    crc ^= red[w];
+  }
+  __syncthreads();
+  return crc;
+}
+
 } // namespace srsgpu

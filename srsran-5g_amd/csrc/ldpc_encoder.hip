@@ -52,13 +52,17 @@ __device__ __forceinline__ int rot(int z, int s, int Z)
 /// CRC of every transport block (TS 38.212 §5.1): one 256-lane workgroup per transport block (crc_device.h).
 __global__ __launch_bounds__(256) void tb_crc_kernel(const tb_crc_desc* __restrict__ descs,
                                                      const uint8_t* __restrict__ tbs,
-                                                     uint32_t* __restrict__ crcs)
+                                                     uint32_t* __restrict__ crcs,
+                                                     const uint32_t* __restrict__ crc_tables)
 {
   __shared__ uint32_t table[256];
   __shared__ uint32_t part[256];
-  const tb_crc_desc d   = descs[blockIdx.x];
-  const uint32_t    crc = block_crc_bytes(tbs + d.byte_offset, static_cast<int>(d.nbytes), static_cast<int>(d.order),
-                                          d.poly, table, part);
+  const tb_crc_desc d = descs[blockIdx.x];
+  // Per-bit contribution table when the plan could cache one for this length, else the byte-table method.
+  const uint32_t crc = (d.table != NO_CRC_TABLE)
+                           ? block_crc_table(tbs + d.byte_offset, static_cast<int>(d.nbytes), crc_tables + d.table, part)
+                           : block_crc_bytes(tbs + d.byte_offset, static_cast<int>(d.nbytes),
+                                             static_cast<int>(d.order), d.poly, table, part);
   if (threadIdx.x == 0) {
     crcs[blockIdx.x] = crc;
   }
@@ -236,10 +240,11 @@ __global__ __launch_bounds__(384) void pdsch_encode_kernel(const enc_desc* __res
 
 } // namespace
 
-void launch_tb_crc(const tb_crc_desc* d_desc, int nof_tbs, const uint8_t* d_tbs, uint32_t* d_crcs, hipStream_t s)
+void launch_tb_crc(const tb_crc_desc* d_desc, int nof_tbs, const uint8_t* d_tbs, uint32_t* d_crcs,
+                   const uint32_t* d_crc_tables, hipStream_t s)
 {
   if (nof_tbs > 0) {
-    tb_crc_kernel<<<nof_tbs, 256, 0, s>>>(d_desc, d_tbs, d_crcs);
+    tb_crc_kernel<<<nof_tbs, 256, 0, s>>>(d_desc, d_tbs, d_crcs, d_crc_tables);
   }
 }
 

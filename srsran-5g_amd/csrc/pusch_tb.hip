@@ -17,7 +17,8 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
                                                        uint8_t* __restrict__ cb_crc_ok,
                                                        const uint8_t* __restrict__ cb_msgs,
                                                        uint8_t* __restrict__ tbs,
-                                                       uint8_t* __restrict__ tb_crc_ok)
+                                                       uint8_t* __restrict__ tb_crc_ok,
+                                                       const uint32_t* __restrict__ crc_tables)
 {
   __shared__ uint32_t table[256];
   __shared__ uint32_t part[256];
@@ -63,7 +64,9 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
     tb[b] = static_cast<uint8_t>(byte);
   }
   __syncthreads();
-  const uint32_t crc = block_crc_bytes(tb, static_cast<int>(bytes), 24, 0x1864cfbu, table, part);
+  const uint32_t crc = (d.crc_table != NO_CRC_TABLE)
+                           ? block_crc_table(tb, static_cast<int>(bytes), crc_tables + d.crc_table, part)
+                           : block_crc_bytes(tb, static_cast<int>(bytes), 24, 0x1864cfbu, table, part);
   // Checksum: the 24 bits that follow the last codeblock's TB bits (concatenate_codeblocks, :465).
   const uint32_t last_q = d.tbs_bits - (d.nof_cbs - 1u) * d.cb_data_bits;
   const uint8_t* lm     = msgs + (d.nof_cbs - 1u) * CB_MSG_STRIDE;
@@ -91,10 +94,11 @@ void launch_pusch_tb(const tb_dec_desc* d_desc,
                      const uint8_t*     d_cb_msgs,
                      uint8_t*           d_tbs,
                      uint8_t*           d_tb_crc_ok,
+                     const uint32_t*    d_crc_tables,
                      hipStream_t        stream)
 {
   if (nof_tbs > 0) {
-    pusch_tb_kernel<<<nof_tbs, 256, 0, stream>>>(d_desc, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok);
+    pusch_tb_kernel<<<nof_tbs, 256, 0, stream>>>(d_desc, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, d_crc_tables);
   }
 }
 

@@ -39,6 +39,171 @@ __device__ __forceinline__ int llr_combine(int a, int b)
   }
 }
 
+/// Value of HARQ buffer position k after rate dematching (the per-position formulation above).
+template <int MODE>
+__device__ __forceinline__ int dematch_position(const dm_desc& d, const int8_t* __restrict__ in, int k, int old,
+                                                int zero_from)
+{
+  const int E = static_cast<int>(d.E), Qm = d.Qm, R = E / Qm;
+  const int Ncb = static_cast<int>(d.Ncb);
+  const int nsys = static_cast<int>(d.nsys), F = d.nof_filler, ninfo = nsys - F;
+  const int V  = Ncb - F;
+  const int v0 = static_cast<int>(d.v0);
+  // Input index of circular-buffer visit n: bit n / R of symbol n % R (bit interleaver, :203), division by the
+  // host-computed magic number (exact for n < 2^20).
+  auto in_index = [&](int n) {
+    const int q = static_cast<int>((static_cast<uint64_t>(static_cast<uint32_t>(n)) * d.r_magic) >> 40);
+    return (n - q * R) * Qm + q;
+  };
+  int val = old;
+  if (k < Ncb) {
+    if (k >= ninfo && k < nsys) {
+      val = d.new_data ? 127 : val;  // filler bits: +infinity (:172)
+    } else {
+      const int v  = k < ninfo ? k : k - F;
+      int       n0 = v - v0;
+      n0           = n0 < 0 ? n0 + V : n0;
+      int n        = n0;
+      if (d.new_data) {
+        if (v >= v0) {
+          if (n0 < E) {
+            val = in[in_index(n0)];  // first pass: copy
+            n   = n0 + V;
+          } else {
+            n = E;  // not reached: keep (or zeroed below)
+          }
+        } else {
+          val = (k < ninfo) ? 0 : val;  // before k0: systematic zeroed, parity keeps its content
+        }
+      }
+      for (; n < E; n += V) {
+        val = llr_combine<MODE>(val, in[in_index(n)]);
+      }
+    }
+  }
+  return (k >= zero_from) ? 0 : val;
+}
+
+/// Any transmission, position by position (dword read-modify-write where aligned).
+template <int MODE>
+__device__ __forceinline__ void dematch_general(const dm_desc& d, const int8_t* __restrict__ llrs,
+                                                int8_t* __restrict__ harq)
+{
+  const int8_t* in  = llrs + d.llr_offset;
+  int8_t*       buf = harq + d.harq_offset;
+  const int     E = static_cast<int>(d.E);
+  const int     N = static_cast<int>(d.N), Ncb = static_cast<int>(d.Ncb);
+  const int     nsys = static_cast<int>(d.nsys), F = d.nof_filler, ninfo = nsys - F;
+  const int     V  = Ncb - F;
+  const int     v0 = static_cast<int>(d.v0);
+  // Walk end of an incomplete first pass (E < V - v0): allot_llrs zeroes the last (Ncb - k_end) LLRs of the buffer.
+  const bool incomplete = d.new_data && (E < V - v0);
+  int        zero_from  = N;
+  if (incomplete) {
+    const int vend = v0 + E;
+    int       kend = vend < ninfo ? vend : vend + F;
+    kend           = kend < nsys ? nsys : kend;
+    kend           = kend % Ncb;
+    if (kend != 0) {
+      zero_from = N - (Ncb - kend);
+    }
+  }
+  if (((d.harq_offset | static_cast<uint32_t>(N)) & 3u) == 0u) {
+    // Dword read-modify-write of four consecutive positions per lane.
+    auto* buf32 = reinterpret_cast<uint32_t*>(buf);
+    for (int k4 = threadIdx.x; k4 < N / 4; k4 += blockDim.x) {
+      const uint32_t old = buf32[k4];
+      uint32_t       w   = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int v = dematch_position<MODE>(d, in, 4 * k4 + b, static_cast<int8_t>(old >> (8 * b)), zero_from);
+        w |= (static_cast<uint32_t>(v) & 0xffu) << (8 * b);
+      }
+      buf32[k4] = w;
+    }
+  } else {
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+      buf[k] = static_cast<int8_t>(dematch_position<MODE>(d, in, k, buf[k], zero_from));
+    }
+  }
+}
+
+/// First transmissions without repetition (new data, E <= V): the positions visited by the first pass before the
+/// circular buffer wraps are plain copies of the de-interleaved input. They are written symbol-major: lane r reads
+/// the Qm LLRs of symbol r (contiguous) and stores bit j at visit n = j R + r, so every store instruction of a wave
+/// covers consecutive buffer bytes. Every other position (fillers, wrapped visits, positions not reached, the
+/// limited-buffer tail) takes the per-position path, skipped a whole 16-position vector at a time when it holds only
+/// copy positions. The two phases write disjoint bytes.
+template <int MODE>
+__device__ __forceinline__ void dematch_new_data(const dm_desc& d, const int8_t* __restrict__ llrs,
+                                                 int8_t* __restrict__ harq)
+{
+  const int8_t* in  = llrs + d.llr_offset;
+  int8_t*       buf = harq + d.harq_offset;
+  const int     E = static_cast<int>(d.E), Qm = d.Qm, R = E / Qm;
+  const int     N = static_cast<int>(d.N), Ncb = static_cast<int>(d.Ncb);
+  const int     nsys = static_cast<int>(d.nsys), F = d.nof_filler, ninfo = nsys - F;
+  const int     V  = Ncb - F;
+  const int     v0 = static_cast<int>(d.v0);
+  const int     nc = (V - v0 < E) ? V - v0 : E;  // visits before the wrap: copies of positions v0 .. v0 + nc - 1
+  int           zero_from = N;
+  if (E < V - v0) {
+    const int vend = v0 + E;
+    int       kend = vend < ninfo ? vend : vend + F;
+    kend           = kend < nsys ? nsys : kend;
+    kend           = kend % Ncb;
+    if (kend != 0) {
+      zero_from = N - (Ncb - kend);
+    }
+  }
+  // Phase 1: copies, symbol-major.
+  for (int r = threadIdx.x; r < R; r += blockDim.x) {
+    int8_t sym[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sym[j] = (j < Qm) ? in[r * Qm + j] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = j * R + r;
+      if (j < Qm && n < nc) {
+        const int v = v0 + n;
+        const int k = v < ninfo ? v : v + F;
+        if (k < zero_from) {
+          buf[k] = sym[j];
+        }
+      }
+    }
+  }
+  // Phase 2: every non-copy position, 16 positions per lane and step.
+  auto is_copy = [&](int k) {
+    if (k >= Ncb || (k >= ninfo && k < nsys) || k >= zero_from) {
+      return false;
+    }
+    const int v = k < ninfo ? k : k - F;
+    return v >= v0 && v - v0 < nc;
+  };
+  for (int k0 = 16 * static_cast<int>(threadIdx.x); k0 < N; k0 += 16 * static_cast<int>(blockDim.x)) {
+    // Copy positions form one or two k-intervals: a vector entirely inside is skipped.
+    if (k0 + 15 < N && is_copy(k0) && is_copy(k0 + 15) &&
+        !(k0 < ninfo && k0 + 15 >= ninfo)) {
+      continue;
+    }
+    if (k0 >= zero_from && k0 + 15 < N && ((d.harq_offset + static_cast<uint32_t>(k0)) & 15u) == 0u) {
+      *reinterpret_cast<uint4*>(buf + k0) = make_uint4(0u, 0u, 0u, 0u);  // limited-buffer / walk-end zero tail
+      continue;
+    }
+    for (int b = 0; b < 16 && k0 + b < N; ++b) {
+      const int k = k0 + b;
+      if (!is_copy(k)) {
+        // The previous content only matters where the reference leaves it (not zeroed, not a filler).
+        const bool keeps = k < zero_from && !(k >= ninfo && k < nsys);
+        buf[k]           = static_cast<int8_t>(dematch_position<MODE>(d, in, k, keeps ? buf[k] : 0, zero_from));
+      }
+    }
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void rate_dematch_kernel(const dm_desc* __restrict__ descs,
                                                            const int8_t* __restrict__ llrs,
@@ -50,57 +215,11 @@ __global__ __launch_bounds__(256) void rate_dematch_kernel(const dm_desc* __rest
   if (d.new_data && cb_crc_ok != nullptr && threadIdx.x == 0) {
     cb_crc_ok[d.cb_index] = 0;
   }
-  const int8_t* in  = llrs + d.llr_offset;
-  int8_t*       buf = harq + d.harq_offset;
-  const int     E = static_cast<int>(d.E), Qm = d.Qm, R = E / Qm;
-  const int     N = static_cast<int>(d.N), Ncb = static_cast<int>(d.Ncb);
-  const int     nsys = static_cast<int>(d.nsys), F = d.nof_filler, ninfo = nsys - F;
-  const int     V  = Ncb - F;
-  const int     v0 = static_cast<int>(d.v0);
-  const bool    new_data = d.new_data != 0;
-  // Walk end of an incomplete first pass (E < V - v0): allot_llrs zeroes the last (Ncb - k_end) LLRs of the buffer.
-  const bool incomplete = new_data && (E < V - v0);
-  int        zero_from  = N;
-  if (incomplete) {
-    const int vend = v0 + E;
-    int       kend = vend < ninfo ? vend : vend + F;
-    kend           = kend < nsys ? nsys : kend;
-    kend           = kend % Ncb;
-    if (kend != 0) {
-      zero_from = N - (Ncb - kend);
-    }
-  }
-  for (int k = threadIdx.x; k < N; k += blockDim.x) {
-    int val = buf[k];
-    if (k < Ncb) {
-      if (k >= ninfo && k < nsys) {
-        val = new_data ? 127 : val;  // filler bits: +infinity (:172)
-      } else {
-        const int v  = k < ninfo ? k : k - F;
-        int       n0 = v - v0;
-        n0           = n0 < 0 ? n0 + V : n0;
-        int n        = n0;
-        if (new_data) {
-          if (v >= v0) {
-            if (n0 < E) {
-              val = in[(n0 % R) * Qm + n0 / R];  // first pass: copy
-              n   = n0 + V;
-            } else {
-              n = E;  // not reached: keep (or zeroed below)
-            }
-          } else {
-            val = (k < ninfo) ? 0 : val;  // before k0: systematic zeroed, parity keeps its content
-          }
-        }
-        for (; n < E; n += V) {
-          val = llr_combine<MODE>(val, in[(n % R) * Qm + n / R]);
-        }
-      }
-    }
-    if (k >= zero_from) {
-      val = 0;
-    }
-    buf[k] = static_cast<int8_t>(val);
+  const int V = static_cast<int>(d.Ncb) - d.nof_filler;
+  if (d.new_data && static_cast<int>(d.E) <= V && d.Qm <= 8) {
+    dematch_new_data<MODE>(d, llrs, harq);
+  } else {
+    dematch_general<MODE>(d, llrs, harq);
   }
 }
 

@@ -47,8 +47,9 @@ struct dm_desc {
   uint8_t  Qm;           ///< Modulation order.
   uint8_t  new_data;     ///< First transmission: copy instead of combine.
   uint32_t cb_index;     ///< Codeblock index (CRC flag slot).
+  uint64_t r_magic;      ///< ceil(2^40 / (E / Qm)): exact n / R as (n * r_magic) >> 40 for n < 2^20.
 };
-static_assert(sizeof(dm_desc) == 36, "dm_desc layout");
+static_assert(sizeof(dm_desc) == 48, "dm_desc layout");
 
 /// CRC job of one transport block (tb_crc_kernel).
 struct tb_crc_desc {
@@ -56,6 +57,7 @@ struct tb_crc_desc {
   uint32_t nbytes;       ///< Transport block size in bytes.
   uint32_t poly;         ///< Generator polynomial including the x^order term (e.g. 0x1864cfb).
   uint32_t order;        ///< 16 or 24.
+  uint32_t table;        ///< Per-bit contribution table (CRC arena offset) or NO_CRC_TABLE: byte-table method.
 };
 
 /// How the double-diagonal core (rows 0..3, parity columns K..K+3) is solved for one (BG, Z): P^x p0 is the sum of
@@ -91,7 +93,8 @@ struct enc_desc {
 };
 static_assert(sizeof(enc_desc) == 56, "enc_desc layout");
 
-void launch_tb_crc(const tb_crc_desc* d_desc, int nof_tbs, const uint8_t* d_tbs, uint32_t* d_crcs, hipStream_t s);
+void launch_tb_crc(const tb_crc_desc* d_desc, int nof_tbs, const uint8_t* d_tbs, uint32_t* d_crcs,
+                   const uint32_t* d_crc_tables, hipStream_t s);
 
 void launch_pdsch_encode(int              bg,
                          const enc_desc*  d_desc,
@@ -123,7 +126,7 @@ struct tb_dec_desc {
   uint32_t data_magic;   ///< ceil(2^32 / cb_data_bits).
   uint32_t tb_offset;    ///< Output byte offset of the transport block.
   uint32_t tb_index;     ///< Result slot.
-  uint32_t pad;
+  uint32_t crc_table;    ///< CRC24A per-bit contribution table of tbs_bits (CRC arena offset) or NO_CRC_TABLE.
 };
 
 void launch_pusch_tb(const tb_dec_desc* d_desc,
@@ -132,6 +135,7 @@ void launch_pusch_tb(const tb_dec_desc* d_desc,
                      const uint8_t*     d_cb_msgs,
                      uint8_t*           d_tbs,
                      uint8_t*           d_tb_crc_ok,
+                     const uint32_t*    d_crc_tables,
                      hipStream_t        stream);
 
 /// Bytes between the packed messages of consecutive codeblocks in the PUSCH decoder's message buffer.

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <algorithm>
+#include <tuple>
 #include <map>
 #include <mutex>
 #include <string>
@@ -74,7 +75,7 @@ struct srsgpu_context {
   int                                  device      = 0;
   uint16_t*                            d_shifts[2] = {nullptr, nullptr};
   uint32_t*                            d_shifts32[2] = {nullptr, nullptr};  ///< Same, one dword per shift (decoder).
-  /// Packed decoder address constants (A, B) per (Z position, edge), see ldpc_decoder_pk.hip (even Z only).
+  /// Packed decoder address constants A | B << 16 per (Z position, edge), see ldpc_decoder_pk.hip (even Z only).
   uint32_t*                            d_pair_ab[2] = {nullptr, nullptr};
   core_plan*                           d_core[2]   = {nullptr, nullptr};
   std::vector<core_plan>               core[2];
@@ -187,11 +188,13 @@ struct srsgpu_pusch_decoder_plan {
 };
 
 struct srsgpu_ldpc_decoder_plan {
-  /// One kernel launch per (base graph, kernel): even lifting sizes go to the packed two-rows-per-lane kernel
-  /// (64 * ceil(Z / 128) lanes), odd ones to the one-row-per-lane kernel (64 * ceil(Z / 64) lanes).
+  /// One kernel launch per (base graph, kernel, layer bound): even lifting sizes go to the packed two-rows-per-lane
+  /// kernel (64 * ceil(Z / 128) lanes) built for at most max_layers layers, odd ones to the one-row-per-lane kernel
+  /// (64 * ceil(Z / 64) lanes).
   struct group {
     int       bg      = 1;
     bool      packed  = false;
+    int       max_layers = 0;
     int       threads = 64;
     int       count   = 0;
     dec_desc* d_desc  = nullptr;
@@ -367,7 +370,7 @@ int srsgpu_context_create(int device, srsgpu_context** out)
     // The decoder reads its shifts through scalar loads, which are dword-granular: it gets a 32-bit copy.
     std::vector<uint32_t> tab32(tab.begin(), tab.end());
     // Packed decoder: rows z and z + H of a lane read the pair at min(2z + A, 2z + B) (row z) and its partner byte.
-    std::vector<uint32_t> ab(static_cast<size_t>(51) * ne * 2, 0u);
+    std::vector<uint32_t> ab(static_cast<size_t>(51) * ne, 0u);
     for (int p = 0; p < 51; ++p) {
       const int Z = kLiftingSizes[p];
       if (Z % 2 != 0) {
@@ -380,8 +383,8 @@ int srsgpu_context_create(int device, srsgpu_context** out)
         const int sm  = sft - hi * H;
         const int A   = 2 * sm + hi;
         const int B   = 2 * sm - 2 * H + 1 - hi;
-        ab[(static_cast<size_t>(p) * ne + e) * 2]     = static_cast<uint32_t>(A);
-        ab[(static_cast<size_t>(p) * ne + e) * 2 + 1] = static_cast<uint32_t>(B);
+        // One dword per edge: A in the low half, B (negative: wraps) in the high half.
+        ab[static_cast<size_t>(p) * ne + e] = static_cast<uint32_t>(A) | (static_cast<uint32_t>(B & 0xffff) << 16);
       }
     }
     if (hipMalloc(&ctx->d_pair_ab[bg - 1], ab.size() * sizeof(uint32_t)) != hipSuccess ||
@@ -462,10 +465,23 @@ namespace {
 /// Codeblock work split by base graph: one launch per base graph, sized for its largest lifting size. (Splitting
 /// further by block size raises the occupancy of the small-Z blocks but serialises launches; measured slower on the
 /// 100 MHz slot: 0.82 vs 0.76 ms per 16 slots.)
+using dec_key = std::tuple<int, bool, int>;  ///< (base graph, packed kernel, layer bound class)
 struct dec_batch {
-  std::map<std::pair<int, bool>, std::vector<dec_desc>> groups;  ///< (base graph, packed kernel)
-  std::map<std::pair<int, bool>, int>                   threads;
+  std::map<dec_key, std::vector<dec_desc>> groups;
+  std::map<dec_key, int>                   threads;
 };
+
+/// Upper bound of the number of layers decode() uses for an input of nof_llrs LLRs (ldpc_decoder_impl.cpp:110: the
+/// trimmed length can only be shorter), rounded up to a compiled class of the packed kernel (8, 16 or all rows).
+int layer_class(int bg, int Z, uint32_t nof_llrs)
+{
+  const int K      = (bg == 1) ? kBG1_K : kBG2_K;
+  const int M      = (bg == 1) ? kBG1_M : kBG2_M;
+  int       cb_len = static_cast<int>(nof_llrs) + 2 * Z;
+  cb_len           = std::max(cb_len, (K + 4) * Z);
+  const int bound  = (cb_len + Z - 1) / Z - K;
+  return bound <= 8 ? 8 : (bound <= 16 ? 16 : M);
+}
 
 /// Validates one decoder configuration (ldpc_decoder_impl.cpp:48-:56, :73-:88) and appends its descriptor.
 int add_decoder_cb(srsgpu_context* ctx,
@@ -530,8 +546,8 @@ int add_decoder_cb(srsgpu_context* ctx,
     }
     d.flags = early_stop ? DEC_FLAG_EARLY_STOP : 0u;
   }
-  const bool packed = (Z % 2) == 0;
-  const auto key    = std::make_pair(bg, packed);
+  const bool    packed = (Z % 2) == 0;
+  const dec_key key(bg, packed, packed ? layer_class(bg, Z, nof_llrs) : 0);
   batch.groups[key].push_back(d);
   const int lanes = packed ? Z / 2 : Z;
   int&      t     = batch.threads[key];
@@ -546,8 +562,9 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
   plan->impl = impl;
   for (const auto& kv : batch.groups) {
     srsgpu_ldpc_decoder_plan::group g;
-    g.bg               = kv.first.first;
-    g.packed           = kv.first.second;
+    g.bg               = std::get<0>(kv.first);
+    g.packed           = std::get<1>(kv.first);
+    g.max_layers       = std::get<2>(kv.first);
     g.threads          = batch.threads.at(kv.first);
     g.count            = static_cast<int>(kv.second.size());
     const size_t bytes = kv.second.size() * sizeof(dec_desc);
@@ -572,7 +589,8 @@ int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
 {
   for (const auto& g : plan->groups) {
     if (g.packed) {
-      launch_ldpc_decode_pk(g.bg, plan->impl, g.d_desc, g.count, g.threads, d_llrs, d_out, d_nof_iterations,
+      launch_ldpc_decode_pk(g.bg, plan->impl, g.max_layers, g.d_desc, g.count, g.threads, d_llrs, d_out,
+                            d_nof_iterations,
                             plan->ctx->d_pair_ab[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s);
     } else {
       launch_ldpc_decode(g.bg, plan->impl, g.d_desc, g.count, g.threads, d_llrs, d_out, d_nof_iterations,
@@ -645,8 +663,26 @@ int add_pusch_cb(srsgpu_context*        ctx,
   const uint64_t R = c.E / static_cast<uint32_t>(qm);
   d.r_magic        = ((1ULL << 40) + R - 1) / R;
   dms.push_back(d);
+  // The decoder reads the HARQ buffer up to the last position a new transmission can leave non-zero: the rate
+  // dematcher zeroes everything from the end of an incomplete first pass (zero_from), and decode() trims trailing
+  // zeros anyway (ldpc_decoder_impl.cpp:94), so the shorter span (whole lifted columns, hence the same soft clamp)
+  // decodes identically - and lets the decoder run a kernel sized for fewer layers.
+  uint32_t dec_llrs = static_cast<uint32_t>(N);
+  if (c.new_data) {
+    const int V = Ncb - c.filler;
+    if (static_cast<int>(c.E) < V - static_cast<int>(d.v0)) {
+      const int vend = static_cast<int>(d.v0) + static_cast<int>(c.E);
+      int       kend = vend < ninfo ? vend : vend + c.filler;
+      kend           = std::max(kend, nsys) % Ncb;
+      if (kend != 0) {
+        const int zero_from = N - (Ncb - kend);
+        const int span      = std::max((K + 2) * Z, ((zero_from + Z - 1) / Z) * Z);
+        dec_llrs            = static_cast<uint32_t>(std::min(N, span));
+      }
+    }
+  }
   return add_decoder_cb(ctx, c.cb_index, c.bg, Z, c.filler, c.nof_crc_bits, c.max_iter, c.sf, c.crc_poly,
-                        c.early_stop, c.harq_offset, static_cast<uint32_t>(N), c.out_offset, batch);
+                        c.early_stop, c.harq_offset, dec_llrs, c.out_offset, batch);
 }
 
 int upload_pusch_cb_plan(srsgpu_context*             ctx,

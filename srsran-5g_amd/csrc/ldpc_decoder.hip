@@ -304,6 +304,9 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
     scratch[wave] = last;
   }
   __syncthreads();
+  // The scalar-cache warm-up loads have landed long ago; retire them before any early return.
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  static_for<SH_LINES>([&](auto L) { keep_sgpr(pf[decltype(L)::value]); });
   int input_size = scratch[0];
   for (int w = 1; w < nwaves; ++w) {
     input_size = scratch[w] > input_size ? scratch[w] : input_size;
@@ -341,8 +344,6 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
   }
   __syncthreads();
 
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  static_for<SH_LINES>([&](auto L) { keep_sgpr(pf[decltype(L)::value]); });
 
   const uint32_t* crc_table = crc_tables + (use_crc ? d.crc_table : 0u);
   const int max_iter = d.max_iter;

@@ -79,6 +79,14 @@ __device__ __forceinline__ s16x2 clamp2(s16x2 v, int lo, int hi)
   return __builtin_elementwise_min(__builtin_elementwise_max(v, ss(lo)), ss(hi));
 }
 
+/// Byte address of the row-z soft bit of an edge: min(2z + A, 2z + B) in 16-bit halves (B < 0 wraps above every
+/// valid address): one v_pk_add_u16 and a 16-bit min across the halves.
+__device__ __forceinline__ uint32_t pair_address(uint32_t z2x2, uint32_t ab)
+{
+  const u16x2 t = as_u16(z2x2) + as_u16(ab);
+  return t.x < t.y ? t.x : t.y;
+}
+
 /// Fixed-point normalisation parameters: MODE 1 scales m by (m * sf16) >> 16, evaluated in 16-bit halves as
 /// ((m * hi) + ((m * lo) >> 8)) >> 8 with sf16 = hi * 256 + lo (exact: every product stays below 2^16).
 struct scale_t {
@@ -114,8 +122,8 @@ constexpr int SIGNS_W0 = 11;
 /// (ldpc_decoder_impl.cpp:195, :255, :240; arithmetic of ldpc_decoder_avx2.cpp:69/:111/:165/:205).
 template <int BG, int MODE, int m>
 __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
-                                              const_u32_ptr  ab,  // (A, B) address constants of this Z, per edge
-                                              uint32_t       z2,
+                                              const_u32_ptr  ab,  // A | B << 16 address constants of this Z
+                                              uint32_t       z2x2,  // 2z in both halves
                                               const scale_t& sc,
                                               uint32_t&      magw,
                                               uint32_t&      sgw,
@@ -140,9 +148,7 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   static_for<deg>([&](auto E) {
     constexpr int  e   = decltype(E)::value;
     constexpr int  col = G::col(e0 + e);
-    const uint32_t pa  = z2 + ab[2 * (e0 + e)];
-    const uint32_t pb  = z2 + ab[2 * (e0 + e) + 1];
-    const uint32_t a   = pa < pb ? pa : pb;
+    const uint32_t a   = pair_address(z2x2, ab[e0 + e]);
     addr[e]            = a;
     // Two byte loads merged by one v_perm (d16 loads do not preserve the other half with SRAM ECC on gfx950).
     const s16x2 sb{static_cast<short>(soft[col * SOFT_COL_STRIDE + a]),
@@ -230,8 +236,11 @@ __device__ __forceinline__ void write_hard_bits_pk(const int8_t* __restrict__ so
   }
 }
 
-template <int BG, int MODE>
-__global__ __launch_bounds__(192, 3) void ldpc_decode_pk_kernel(const dec_desc* __restrict__ descs,
+/// MAXL: compile-time bound on the number of layers (host-proven from the input length, dec_desc::nof_llr), so that
+/// only MAXL layers of check-to-variable state occupy VGPRs: the 4-layer high-rate codeblocks of a loaded cell run at
+/// twice the occupancy of the 46-layer worst case.
+template <int BG, int MODE, int MAXL>
+__global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : 5))) void ldpc_decode_pk_kernel(const dec_desc* __restrict__ descs,
                                                              const int8_t* __restrict__ llrs,
                                                              uint8_t* __restrict__ out,
                                                              int32_t* __restrict__ results,
@@ -256,10 +265,10 @@ __global__ __launch_bounds__(192, 3) void ldpc_decode_pk_kernel(const dec_desc* 
   }
   const int      Z  = d.Z;
   const uint32_t H  = static_cast<uint32_t>(Z) / 2u;
-  const auto     ab = (const_u32_ptr)(uintptr_t)(ab_table + static_cast<uint32_t>(d.zpos) * 2u * G::NE);
+  const auto     ab = (const_u32_ptr)(uintptr_t)(ab_table + static_cast<uint32_t>(d.zpos) * G::NE);
   asm volatile("" ::"s"(llrs), "s"(out), "s"(results), "s"(crc_tables), "s"(cb_crc_ok), "s"(blockDim.x));
   // Scalar-cache warm-up of this Z's address constants while the LLRs load (see ldpc_decoder.hip).
-  constexpr int AB_BYTES = G::NE * 8;
+  constexpr int AB_BYTES = G::NE * 4;
   constexpr int AB_LINES = (AB_BYTES - 4) / 64 + 2;
   uint32_t      pf[AB_LINES];
   static_for<AB_LINES>([&](auto L) {
@@ -374,6 +383,9 @@ __global__ __launch_bounds__(192, 3) void ldpc_decode_pk_kernel(const dec_desc* 
     scratch[wave] = last;
   }
   __syncthreads();
+  // The scalar-cache warm-up loads have landed long ago; retire them before any early return.
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  static_for<AB_LINES>([&](auto L) { keep_sgpr(pf[decltype(L)::value]); });
   int input_size = scratch[0];
   for (int w = 1; w < nwaves; ++w) {
     input_size = scratch[w] > input_size ? scratch[w] : input_size;
@@ -408,34 +420,40 @@ __global__ __launch_bounds__(192, 3) void ldpc_decode_pk_kernel(const dec_desc* 
   sc.lo = uu(static_cast<int>(d.sf16 & 255u));
   sc.sf = d.sf;
 
-  uint32_t magw[G::M], sgw[G::M];
+  static_assert(MAXL >= 4 && MAXL <= G::M, "layer bound");
+  if (nof_layers > MAXL) {
+    // The host bound is derived from the same input length: cannot happen; fail loudly rather than decode wrongly.
+    if (threadIdx.x == 0) {
+      results[d.cb_index] = -2;
+    }
+    return;
+  }
+  uint32_t magw[MAXL], sgw[MAXL];
   uint32_t hiw[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int m = 0; m < G::M; ++m) {
+  for (int m = 0; m < MAXL; ++m) {
     magw[m] = 0;
     sgw[m]  = 0;
   }
   __syncthreads();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  static_for<AB_LINES>([&](auto L) { keep_sgpr(pf[decltype(L)::value]); });
 
   const int max_iter = d.max_iter;
   DEC_STAMP(1);
   DEC_PROF(31, static_cast<uint64_t>(nof_layers));
   for (int it = 0; it < max_iter; ++it) {
     // Opaque per-iteration copies (see ldpc_decoder.hip).
-    int           nl  = nof_layers;
-    uint32_t      z2  = 2u * static_cast<uint32_t>(z);
-    const_u32_ptr abi = ab;
+    int           nl   = nof_layers;
+    uint32_t      z2x2 = 0x00020002u * static_cast<uint32_t>(z);
+    const_u32_ptr abi  = ab;
     asm volatile("" : "+s"(nl));
-    asm volatile("" : "+v"(z2));
+    asm volatile("" : "+v"(z2x2));
     asm volatile("" : "+s"(abi));
-    static_for<G::M>([&](auto Mi) {
+    static_for<MAXL>([&](auto Mi) {
       constexpr int m = decltype(Mi)::value;
       if (m < nl) {
         if (active) {
           __builtin_amdgcn_sched_barrier(0);
-          row_update_pk<BG, MODE, m>(soft, abi, z2, sc, magw[m], sgw[m], hiw[m & 3]);
+          row_update_pk<BG, MODE, m>(soft, abi, z2x2, sc, magw[m], sgw[m], hiw[m & 3]);
           __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();
@@ -526,6 +544,7 @@ int debug_read_decoder_profile_pk(uint64_t* dst, size_t n)
 
 void launch_ldpc_decode_pk(int             bg,
                            int             mode,
+                           int             max_layers,
                            const dec_desc* d_desc,
                            int             nof_cbs,
                            int             block_threads,
@@ -541,23 +560,27 @@ void launch_ldpc_decode_pk(int             bg,
     return;
   }
   dim3 grid(nof_cbs), block(block_threads);
+#define SRSGPU_PK_LAUNCH(BG_, MODE_, MAXL_)                                                                            \
+  ldpc_decode_pk_kernel<BG_, MODE_, MAXL_><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab,        \
+                                                                       d_crc_tables, d_cb_crc_ok)
   if (bg == 1) {
-    if (mode == 1) {
-      ldpc_decode_pk_kernel<1, 1><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables,
-                                                              d_cb_crc_ok);
+    if (max_layers <= 8) {
+      mode == 1 ? SRSGPU_PK_LAUNCH(1, 1, 8) : SRSGPU_PK_LAUNCH(1, 0, 8);
+    } else if (max_layers <= 16) {
+      mode == 1 ? SRSGPU_PK_LAUNCH(1, 1, 16) : SRSGPU_PK_LAUNCH(1, 0, 16);
     } else {
-      ldpc_decode_pk_kernel<1, 0><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables,
-                                                              d_cb_crc_ok);
+      mode == 1 ? SRSGPU_PK_LAUNCH(1, 1, kBG1_M) : SRSGPU_PK_LAUNCH(1, 0, kBG1_M);
     }
   } else {
-    if (mode == 1) {
-      ldpc_decode_pk_kernel<2, 1><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables,
-                                                              d_cb_crc_ok);
+    if (max_layers <= 8) {
+      mode == 1 ? SRSGPU_PK_LAUNCH(2, 1, 8) : SRSGPU_PK_LAUNCH(2, 0, 8);
+    } else if (max_layers <= 16) {
+      mode == 1 ? SRSGPU_PK_LAUNCH(2, 1, 16) : SRSGPU_PK_LAUNCH(2, 0, 16);
     } else {
-      ldpc_decode_pk_kernel<2, 0><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables,
-                                                              d_cb_crc_ok);
+      mode == 1 ? SRSGPU_PK_LAUNCH(2, 1, kBG2_M) : SRSGPU_PK_LAUNCH(2, 0, kBG2_M);
     }
   }
+#undef SRSGPU_PK_LAUNCH
 }
 
 } // namespace srsgpu

@@ -149,9 +149,11 @@ int debug_read_decoder_profile(uint64_t* dst, size_t n);
 int debug_read_decoder_profile_pk(uint64_t* dst, size_t n);
 #endif
 
-/// Launches the packed two-rows-per-lane LDPC decoder (ldpc_decoder_pk.hip; even Z, block_threads >= Z / 2).
+/// Launches the packed two-rows-per-lane LDPC decoder (ldpc_decoder_pk.hip; even Z, block_threads >= Z / 2) built for
+/// at most max_layers layers (8, 16 or all; every codeblock of the launch must satisfy layers_bound() <= it).
 void launch_ldpc_decode_pk(int             bg,
                            int             mode,
+                           int             max_layers,
                            const dec_desc* d_desc,
                            int             nof_cbs,
                            int             block_threads,

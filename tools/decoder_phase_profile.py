@@ -105,6 +105,16 @@ def main():
     res["clock_ghz_est"] = float(((p[:, 28] - t0) / np.maximum(wall, 1e-3) / 1e3).mean())
     # Concurrency: average number of codeblocks resident at once.
     res["avg_resident_cbs"] = float(wall.sum() / max(res["kernel_span_us"], 1e-9))
+    # Iteration-0 layer time by start-time quartile (first resident round vs later codeblocks).
+    start = p[:, 29]
+    q = np.quantile(start, [0.25, 0.5, 0.75])
+    it0 = (p[:, 2] - p[:, 1]).astype(float)
+    grp = np.searchsorted(q, start)
+    res["iter0_cycles_by_start_quartile"] = [float(it0[grp == g].mean()) for g in range(4)]
+    it1 = np.where(nit > 1, (p[:, 4] - p[:, 3]).astype(float), np.nan)
+    res["iter1_cycles_by_start_quartile"] = [float(np.nanmean(it1[grp == g])) for g in range(4)]
+    load = (p[:, 1] - p[:, 0]).astype(float)
+    res["load_cycles_by_start_quartile"] = [float(load[grp == g].mean()) for g in range(4)]
     print(json.dumps(res, indent=1))
     if args.out:
         with open(args.out, "w") as f:

@@ -176,6 +176,13 @@ def main():
     dl_stream = torch.cuda.Stream(dev)
     ul_stream = dl_stream if args.serial_legs else torch.cuda.Stream(dev)
 
+    # Multi-GPU (north star): every rank codes its own cells' slots; the decoded UL transport blocks and their CRC flags
+    # of all ranks are gathered to the FAPI rank (rank 0) over RCCL once per step - the path's only exchange.
+    tb_gather = None
+    if world > 1:
+        from srsgpu import dist as sdist
+        tb_gather = sdist.TbGather(d_ul_tbs.numel(), d_tb_ok.numel(), dev, root=0)
+
     def step():
         dl_stream.wait_stream(main_stream)
         ul_stream.wait_stream(main_stream)
@@ -183,6 +190,8 @@ def main():
         ul_plan.execute(d_llrs, d_harq, d_crc, d_msgs, d_iters, d_ul_tbs, d_tb_ok, ul_stream)
         main_stream.wait_stream(dl_stream)
         main_stream.wait_stream(ul_stream)
+        if tb_gather is not None:
+            tb_gather.gather(d_ul_tbs, d_tb_ok)
 
     for _ in range(args.warmup):
         step()
@@ -229,12 +238,11 @@ def main():
                          for s in segs)
     tbs_bits_slot = sum(s.tbs for s in segs)
     dec_ms = ul_ms[1] / args.steps
-    # Algorithmic bytes of one decoder launch: the N_short*Z LLRs read per codeblock, K*Z/8 bytes of decoded bits
-    # written, 4 B result + 1 B CRC flag, 40 B descriptor.
-    dec_bytes_slot = sum(s.nof_segments * ((66 if s.base_graph == 1 else 50) * s.lifting_size +
-                                           ((22 if s.base_graph == 1 else 10) * s.lifting_size + 7) // 8 + 45)
-                         for s in segs)
-    dec_bytes = S * dec_bytes_slot
+    # Algorithmic bytes of one decoder launch: the LLRs each codeblock's decode() reads (the HARQ span up to the
+    # dematcher's zero tail, as reported by the plan), K*Z/8 bytes of decoded bits written, 4 B result + 1 B CRC flag,
+    # 40 B descriptor.
+    dec_bytes = ul_plan.decoder_input_llrs + sum(
+        s.nof_segments * (((22 if s.base_graph == 1 else 10) * s.lifting_size + 7) // 8 + 45) for s in segs) * S
     achieved = dec_bytes / (dec_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "ldpc_decode_traffic.json")
@@ -265,7 +273,9 @@ def main():
                    "codeblocks_per_step_per_direction": int(sum(nof_cbs)),
                    "ldpc_max_iterations": args.iterations, "ldpc_early_stop": True,
                    "decoder_arithmetic": "avx2/avx512 (SIMD) variant, bit-exact",
-                   "parallelism": f"dp{world} (independent cells per GPU, no collective)"},
+                   "parallelism": (f"dp{world}: each GPU codes its own cells' slots; decoded UL TBs + CRC flags "
+                                   f"gathered to the FAPI rank over RCCL every step") if world > 1 else
+                                  "dp1 (independent cells per GPU)"},
         "ldpc_info_bits_per_s": info_bits_slot * value,
         "tb_bits_per_s_per_direction": tbs_bits_slot * value,
         "realtime_cells_per_gpu": value / SLOT_RATE_30KHZ / world,
@@ -275,10 +285,10 @@ def main():
                               "pusch_rate_dematch": ul_ms[0] / args.steps, "pusch_ldpc_decode": dec_ms,
                               "pusch_tb_crc": ul_ms[2] / args.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "ldpc_decode_kernel<1,1>",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "ldpc_decode_pk_kernel<1,1,8>",
                      "kernel_ms_per_launch": dec_ms,
                      "note": "algorithmic bytes per launch / decoder-stage HIP-event time on the launch stream; the "
-                             "LDPC decoder is VALU/LDS-bound, not HBM-bound (DESIGN.md)"},
+                             "LDPC decoder is VALU-issue/latency-bound, not HBM-bound (DESIGN.md)"},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -238,6 +238,11 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
 
 uint32_t srsgpu_pusch_decoder_plan_nof_codeblocks(const srsgpu_pusch_decoder_plan* plan);
 
+/** Number of LLRs the LDPC decoder stage reads per execute: every codeblock's span of the HARQ buffer, trimmed to the
+ *  rate dematcher's zero tail for new transmissions (what decode() would trim to, ldpc_decoder_impl.cpp:94). For
+ *  traffic accounting. */
+uint64_t srsgpu_pusch_decoder_plan_decoder_input_llrs(const srsgpu_pusch_decoder_plan* plan);
+
 /** Decodes the planned transport blocks. d_tb_crc_ok[t] = 1 when the TB CRC passed (pusch_decoder_result
  *  tb_crc_ok); d_cb_nof_iterations[c] as in srsgpu_pusch_cb_plan_execute. Asynchronous, hipGraph-capturable. */
 int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,

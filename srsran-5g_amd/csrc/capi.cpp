@@ -202,6 +202,7 @@ struct srsgpu_ldpc_decoder_plan {
   srsgpu_context*    ctx  = nullptr;
   int                impl = SRSGPU_LDPC_IMPL_SIMD;
   std::vector<group> groups;
+  uint64_t           input_llrs = 0;  ///< LLRs the decoder reads per execute (sum of dec_desc::nof_llr).
 };
 
 namespace {
@@ -567,6 +568,9 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
     g.max_layers       = std::get<2>(kv.first);
     g.threads          = batch.threads.at(kv.first);
     g.count            = static_cast<int>(kv.second.size());
+    for (const dec_desc& d : kv.second) {
+      plan->input_llrs += d.nof_llr;
+    }
     const size_t bytes = kv.second.size() * sizeof(dec_desc);
     if (hipMalloc(&g.d_desc, bytes) != hipSuccess ||
         hipMemcpy(g.d_desc, kv.second.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
@@ -1124,6 +1128,11 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
 uint32_t srsgpu_pusch_decoder_plan_nof_codeblocks(const srsgpu_pusch_decoder_plan* plan)
 {
   return plan == nullptr ? 0u : static_cast<uint32_t>(plan->cbs->nof_cbs);
+}
+
+uint64_t srsgpu_pusch_decoder_plan_decoder_input_llrs(const srsgpu_pusch_decoder_plan* plan)
+{
+  return (plan == nullptr || plan->cbs == nullptr || plan->cbs->dec == nullptr) ? 0u : plan->cbs->dec->input_llrs;
 }
 
 int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,

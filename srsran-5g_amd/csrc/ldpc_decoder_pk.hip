@@ -138,7 +138,6 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   const u16x2 D   = S1 - S2;
   const u16x2 IDX = as_u16(sgw) >> uu(11);
   s16x2       v2c[deg];
-  uint32_t    addr[deg];
   u16x2       k1 = uu(KEY_INIT), k2 = uu(KEY_INIT);
   uint32_t    sx = 0;
   uint32_t    one_bits = 0x00010001u;
@@ -149,7 +148,6 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     constexpr int  e   = decltype(E)::value;
     constexpr int  col = G::col(e0 + e);
     const uint32_t a   = pair_address(z2x2, ab[e0 + e]);
-    addr[e]            = a;
     // Two byte loads merged by one v_perm (d16 loads do not preserve the other half with SRAM ECC on gfx950).
     const s16x2 sb{static_cast<short>(soft[col * SOFT_COL_STRIDE + a]),
                    static_cast<short>(soft[col * SOFT_COL_STRIDE + (a ^ 1u)])};
@@ -177,6 +175,10 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   uint32_t    nsg  = bits(IDXN << uu(11));
   uint32_t    nhi  = 0;
 
+  // Addresses are recomputed (2 VALU per edge) rather than kept: 19 fewer live VGPRs for the core rows. The opaque
+  // copy stops the compiler from reusing pass-1 results.
+  uint32_t z2x2_b = z2x2;
+  asm volatile("" : "+v"(z2x2_b));
   static_for<deg>([&](auto E) {
     constexpr int e   = decltype(E)::value;
     constexpr int col = G::col(e0 + e);
@@ -188,7 +190,7 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     const s16x2 c   = as_s16(bits(mag) ^ bits(n)) - n;
     // Promotion sum (log_likelihood_ratio.cpp:75): |sum| > LLR_MAX becomes +/-infinity (SOFT_INF).
     const s16x2    sb = clamp2(c + v, -SOFT_INF, SOFT_INF);
-    const uint32_t a  = addr[e];
+    const uint32_t a  = pair_address(z2x2_b, ab[e0 + e]);
     soft[col * SOFT_COL_STRIDE + a]        = static_cast<int8_t>(sb.x);
     soft[col * SOFT_COL_STRIDE + (a ^ 1u)] = static_cast<int8_t>(sb.y);
     constexpr int      pos  = (e < SIGNS_W0) ? e : e - SIGNS_W0;
@@ -249,9 +251,12 @@ __global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : 5))) void ldp
                                                              uint8_t* __restrict__ cb_crc_ok)
 {
   using G = bg_t<BG>;
-  __shared__ __attribute__((aligned(16))) int8_t smem[G::NF * SOFT_COL_STRIDE + SCRATCH_BYTES];
+  // Only the first K + MAXL columns can be touched by MAXL layers: the soft-bit image shrinks with the layer bound
+  // (11.8 KB for 8 layers of BG1 instead of 26 KB), so more codeblocks share a CU.
+  constexpr int NCOL = G::K + MAXL;
+  __shared__ __attribute__((aligned(16))) int8_t smem[NCOL * SOFT_COL_STRIDE + SCRATCH_BYTES];
   int8_t* soft    = smem;
-  int*    scratch = reinterpret_cast<int*>(smem + G::NF * SOFT_COL_STRIDE);
+  int*    scratch = reinterpret_cast<int*>(smem + NCOL * SOFT_COL_STRIDE);
 
   DEC_STAMP(0);
   DEC_PROF(29, __builtin_amdgcn_s_memrealtime());
@@ -292,7 +297,8 @@ __global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : 5))) void ldp
     const uint32_t head   = static_cast<uint32_t>(d.llr_offset) & 15u;
     const uint4*   vecs   = reinterpret_cast<const uint4*>(llr - head);
     const int      nvec   = static_cast<int>((head + static_cast<uint32_t>(n_llr) + 15u) >> 4);
-    constexpr int  BATCH  = 9;  // 9 x 16 B per lane: a whole BG1 codeblock at Z = 384 with 192 lanes
+    // 16-B vectors per lane in flight: the whole input span of the layer bound at Z = 384 with 192 lanes.
+    constexpr int  BATCH  = ((NCOL - 2) * 384 / 16 + 191) / 192;
     int            last_w = -1;
     uint4          last_v = make_uint4(0u, 0u, 0u, 0u);
     for (int w0 = threadIdx.x; w0 < nvec; w0 += BATCH * blockDim.x) {
@@ -374,7 +380,7 @@ __global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : 5))) void ldp
       }
       ++c;
     }
-    for (; c < G::NF; ++c) {
+    for (; c < NCOL; ++c) {
       soft16[(c * SOFT_COL_STRIDE) / 2 + z] = 0;
     }
   }
@@ -456,7 +462,9 @@ __global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : 5))) void ldp
           row_update_pk<BG, MODE, m>(soft, abi, z2x2, sc, magw[m], sgw[m], hiw[m & 3]);
           __builtin_amdgcn_sched_barrier(0);
         }
+#ifndef LDPC_PK_EXPERIMENT_NO_LAYER_BARRIER  // timing experiments only: results are wrong without the barrier
         __syncthreads();
+#endif
       }
     });
     DEC_STAMP(2 + 2 * (it & 7));

@@ -154,6 +154,8 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pusch_cb_plan_destroy.argtypes = [P]
     lib.srsgpu_pusch_cb_plan_destroy.restype = None
     lib.srsgpu_pdsch_encoder_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(P)]
+    lib.srsgpu_pusch_decoder_plan_decoder_input_llrs.argtypes = [P]
+    lib.srsgpu_pusch_decoder_plan_decoder_input_llrs.restype = ctypes.c_uint64
     lib.srsgpu_pdsch_encoder_plan_nof_codeblocks.argtypes = [P]
     lib.srsgpu_pdsch_encoder_plan_nof_codeblocks.restype = ctypes.c_uint32
     lib.srsgpu_pdsch_encoder_plan_execute.argtypes = [P, P, P, P]
@@ -179,7 +181,8 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ldpc_decode", "srsgpu_pusch_cb_plan_create", "srsgpu_pusch_cb_plan_execute",
     "srsgpu_pusch_cb_plan_destroy", "srsgpu_pdsch_encoder_plan_create", "srsgpu_pdsch_encoder_plan_nof_codeblocks",
     "srsgpu_pdsch_encoder_plan_execute", "srsgpu_pdsch_encoder_plan_destroy", "srsgpu_pusch_decoder_plan_create",
-    "srsgpu_pusch_decoder_plan_nof_codeblocks", "srsgpu_pusch_decoder_plan_execute",
+    "srsgpu_pusch_decoder_plan_nof_codeblocks", "srsgpu_pusch_decoder_plan_decoder_input_llrs",
+    "srsgpu_pusch_decoder_plan_execute",
     "srsgpu_pusch_decoder_plan_destroy", "srsgpu_pusch_decoder_plan_enable_timing",
     "srsgpu_pusch_decoder_plan_stage_times", "srsgpu_pdsch_encoder_plan_enable_timing",
     "srsgpu_pdsch_encoder_plan_stage_times",
@@ -588,6 +591,7 @@ class PuschDecoderPlan:
         self.handle = h
         self.nof_tbs = len(cfg_array)
         self.nof_codeblocks = int(_lib.srsgpu_pusch_decoder_plan_nof_codeblocks(h))
+        self.decoder_input_llrs = int(_lib.srsgpu_pusch_decoder_plan_decoder_input_llrs(h))
 
     def execute(self, d_llrs, d_harq, d_cb_crc_ok, d_cb_msgs, d_cb_iters, d_tbs, d_tb_crc_ok, stream=None):
         _check(_lib.srsgpu_pusch_decoder_plan_execute(self.handle, _dptr(d_llrs), _dptr(d_harq), _dptr(d_cb_crc_ok),

@@ -84,6 +84,13 @@ def main():
         assert lib.srsgpu_debug_decoder_profile(buf.ctypes.data, buf.size, 0) == 0
     p = buf.reshape(n, SLOTS).astype(np.int64)
     it = iters.cpu().numpy()[:n]
+    # Keep codeblocks whose stamps all come from the last launch (a codeblock that returned early keeps stale ones).
+    nit0 = np.where(it > 0, it, args.iterations)
+    ok = (p[:, 30] > p[:, 29]) & (p[:, 1] >= p[:, 0]) & (p[:, 28] >= p[:, 1])
+    for k in range(args.iterations):
+        ok &= ~(nit0 > k) | ((p[:, 2 + 2 * k] >= p[:, 1]) & (p[:, 3 + 2 * k] >= p[:, 2 + 2 * k]))
+    p, it = p[ok], it[ok]
+    n = int(ok.sum())
     nit = np.where(it > 0, it, args.iterations)
     t0 = p[:, 0]
     res = {"nof_cbs": int(n), "avg_iterations": float(nit.mean()), "nof_layers": np.bincount(p[:, 31]).tolist()}
@@ -115,6 +122,15 @@ def main():
     res["iter1_cycles_by_start_quartile"] = [float(np.nanmean(it1[grp == g])) for g in range(4)]
     load = (p[:, 1] - p[:, 0]).astype(float)
     res["load_cycles_by_start_quartile"] = [float(load[grp == g].mean()) for g in range(4)]
+    # Residency timeline: codeblocks in flight per 10 us bin, and how many start / finish in each bin.
+    t_lo = p[:, 29].min()
+    st = (p[:, 29] - t_lo) / 100.0
+    en = (p[:, 30] - t_lo) / 100.0
+    bins = np.arange(0.0, en.max() + 10.0, 10.0)
+    res["timeline_us"] = [float(b) for b in bins[:-1]]
+    res["timeline_resident"] = [int(((st < b + 10) & (en > b)).sum()) for b in bins[:-1]]
+    res["timeline_starts"] = np.histogram(st, bins)[0].tolist()
+    res["timeline_ends"] = np.histogram(en, bins)[0].tolist()
     print(json.dumps(res, indent=1))
     if args.out:
         with open(args.out, "w") as f:

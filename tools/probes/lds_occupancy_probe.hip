@@ -7,7 +7,7 @@
 #include <algorithm>
 
 template <int LDS_BYTES>
-__global__ __launch_bounds__(384) void probe(unsigned long long* t, int spin)
+__global__ __launch_bounds__(1024) void probe(unsigned long long* t, int spin)
 {
   __shared__ int buf[LDS_BYTES / 4];
   unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -27,9 +27,9 @@ __global__ __launch_bounds__(384) void probe(unsigned long long* t, int spin)
 }
 
 template <int LDS_BYTES>
-void run(unsigned long long* d, int nblk, int cus)
+void run(unsigned long long* d, int nblk, int cus, int threads = 384)
 {
-  probe<LDS_BYTES><<<nblk, 384>>>(d, 2000);
+  probe<LDS_BYTES><<<nblk, threads>>>(d, 2000);
   hipDeviceSynchronize();
   std::vector<unsigned long long> h(2 * nblk);
   hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
@@ -40,7 +40,8 @@ void run(unsigned long long* d, int nblk, int cus)
     hi = std::max(hi, h[2 * i + 1]);
     sum += static_cast<double>(h[2 * i + 1] - h[2 * i]);
   }
-  printf("lds %6d B: %.2f workgroups/CU resident on average\n", LDS_BYTES, sum / static_cast<double>(hi - lo) / cus);
+  printf("threads %4d lds %6d B: %.2f workgroups/CU resident on average\n", threads, LDS_BYTES,
+         sum / static_cast<double>(hi - lo) / cus);
 }
 
 int main()
@@ -52,7 +53,7 @@ int main()
   printf("CUs %d, sharedMemPerMultiprocessor %zu, maxSharedMemoryPerMultiProcessor %zu\n", cus, p.sharedMemPerBlock,
          p.maxSharedMemoryPerMultiProcessor);
   unsigned long long* d;
-  hipMalloc(&d, 2 * nblk * 8);
+  hipMalloc(&d, 2 * nblk * 4 * 8);
   run<16384>(d, nblk, cus);
   run<32768>(d, nblk, cus);
   run<40960>(d, nblk, cus);
@@ -60,6 +61,12 @@ int main()
   run<60160>(d, nblk, cus);
   run<65536>(d, nblk, cus);
   run<81920>(d, nblk, cus);
+  for (int th : {64, 128, 192, 256}) {
+    run<1024>(d, nblk * 4, cus, th);
+    run<12288>(d, nblk * 4, cus, th);
+    run<16384>(d, nblk * 4, cus, th);
+    run<26624>(d, nblk * 4, cus, th);
+  }
   hipFree(d);
   return 0;
 }

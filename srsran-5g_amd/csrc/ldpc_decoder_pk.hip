@@ -120,7 +120,7 @@ constexpr int SIGNS_W0 = 11;
 
 /// Two lifted check rows (z, z + H) of layer m: v2c messages, min-sum analysis, c2v messages, soft-bit update
 /// (ldpc_decoder_impl.cpp:195, :255, :240; arithmetic of ldpc_decoder_avx2.cpp:69/:111/:165/:205).
-template <int BG, int MODE, int m>
+template <int BG, int MODE, int m, bool KEEP_ADDR>
 __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
                                               const_u32_ptr  ab,  // A | B << 16 address constants of this Z
                                               uint32_t       z2x2,  // 2z in both halves
@@ -144,13 +144,21 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   asm("" : "+v"(one_bits));
   const u16x2 one = as_u16(one_bits);
 
+  uint32_t addr[KEEP_ADDR ? deg : 1];
   static_for<deg>([&](auto E) {
     constexpr int  e   = decltype(E)::value;
     constexpr int  col = G::col(e0 + e);
     const uint32_t a   = pair_address(z2x2, ab[e0 + e]);
+    if constexpr (KEEP_ADDR) {
+      addr[e] = a;
+    }
     // Two byte loads merged by one v_perm (d16 loads do not preserve the other half with SRAM ECC on gfx950).
+#ifndef LDPC_PK_EXPERIMENT_NO_LOADS
     const s16x2 sb{static_cast<short>(soft[col * SOFT_COL_STRIDE + a]),
                    static_cast<short>(soft[col * SOFT_COL_STRIDE + (a ^ 1u)])};
+#else  // timing experiments only
+    const s16x2 sb = as_s16(((a * 0x9e3779b1u) >> 3) & 0x003f003fu);
+#endif
     // Previous c2v of this edge: magnitude min2 at the argmin, min1 elsewhere; sign from the sign bits.
     constexpr int  pos = (e < SIGNS_W0) ? e : e - SIGNS_W0;
     const uint32_t sw  = (e < SIGNS_W0) ? sgw : hiw;
@@ -166,6 +174,17 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     k2              = __builtin_elementwise_min(__builtin_elementwise_max(key, k1), k2);
     k1              = __builtin_elementwise_min(key, k1);
     sx ^= bits(v);
+#ifdef LDPC_PK_EXPERIMENT_EXTRA_VALU  // timing experiments only: N extra independent VALU per edge
+    {
+      uint32_t j0 = bits(v), j1 = bits(key);
+#pragma unroll
+      for (int x = 0; x < LDPC_PK_EXPERIMENT_EXTRA_VALU / 2; ++x) {
+        asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(j0) : "v"(j1));
+        asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(j1) : "v"(j0));
+      }
+      sx ^= (j0 ^ j1) & 0x00010001u & (j0 >> 30);
+    }
+#endif
   });
 
   const u16x2 IDXN = k1 & uu(31);
@@ -175,10 +194,12 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   uint32_t    nsg  = bits(IDXN << uu(11));
   uint32_t    nhi  = 0;
 
-  // Addresses are recomputed (2 VALU per edge) rather than kept: 19 fewer live VGPRs for the core rows. The opaque
-  // copy stops the compiler from reusing pass-1 results.
+  // With many layers of state the addresses are recomputed (2 VALU per edge) rather than kept: 19 fewer live VGPRs
+  // for the core rows. The opaque copy stops the compiler from reusing pass-1 results.
   uint32_t z2x2_b = z2x2;
-  asm volatile("" : "+v"(z2x2_b));
+  if constexpr (!KEEP_ADDR) {
+    asm volatile("" : "+v"(z2x2_b));
+  }
   static_for<deg>([&](auto E) {
     constexpr int e   = decltype(E)::value;
     constexpr int col = G::col(e0 + e);
@@ -187,12 +208,22 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     const s16x2 n   = as_s16(sx ^ bits(v)) >> ss(15);
     const u16x2 ne  = not_argmin(IDXN, e, one);
     const u16x2 mag = ne * DN + S2N;
-    const s16x2 c   = as_s16(bits(mag) ^ bits(n)) - n;
+    // c2v + v2c as one multiply-add on the sign +/-1 (n | 1).
+    const s16x2 sgn = as_s16(bits(n) | 0x00010001u);
     // Promotion sum (log_likelihood_ratio.cpp:75): |sum| > LLR_MAX becomes +/-infinity (SOFT_INF).
-    const s16x2    sb = clamp2(c + v, -SOFT_INF, SOFT_INF);
-    const uint32_t a  = pair_address(z2x2_b, ab[e0 + e]);
+    const s16x2    sb = clamp2(as_s16(bits(mag)) * sgn + v, -SOFT_INF, SOFT_INF);
+    uint32_t       a;
+    if constexpr (KEEP_ADDR) {
+      a = addr[e];
+    } else {
+      a = pair_address(z2x2_b, ab[e0 + e]);
+    }
+#ifndef LDPC_PK_EXPERIMENT_NO_STORES
     soft[col * SOFT_COL_STRIDE + a]        = static_cast<int8_t>(sb.x);
     soft[col * SOFT_COL_STRIDE + (a ^ 1u)] = static_cast<int8_t>(sb.y);
+#else  // timing experiments only: keep the values alive
+    nhi ^= bits(sb) + a;
+#endif
     constexpr int      pos  = (e < SIGNS_W0) ? e : e - SIGNS_W0;
     constexpr uint32_t mask = (1u << pos) | (1u << (16 + pos));
     if constexpr (e < SIGNS_W0) {
@@ -459,7 +490,7 @@ __global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : 5))) void ldp
       if (m < nl) {
         if (active) {
           __builtin_amdgcn_sched_barrier(0);
-          row_update_pk<BG, MODE, m>(soft, abi, z2x2, sc, magw[m], sgw[m], hiw[m & 3]);
+          row_update_pk<BG, MODE, m, (MAXL <= 16)>(soft, abi, z2x2, sc, magw[m], sgw[m], hiw[m & 3]);
           __builtin_amdgcn_sched_barrier(0);
         }
 #ifndef LDPC_PK_EXPERIMENT_NO_LAYER_BARRIER  // timing experiments only: results are wrong without the barrier

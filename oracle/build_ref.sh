@@ -15,6 +15,7 @@ mkdir -p "$OUT/obj"
 CXX=${CXX:-g++}
 FLAGS="-std=c++17 -O3 -fPIC -DNDEBUG -DFMT_HEADER_ONLY -DASSERTS_ENABLED=0 -I$REF/include -I$REF/external/fmt/include -I$REF/external -I$REF/lib/phy/upper/channel_coding"
 LDPC=$REF/lib/phy/upper/channel_coding/ldpc
+PDSCH=$REF/lib/phy/upper/channel_processors/pdsch
 SRCS=(
   "$LDPC/ldpc_graph_impl.cpp:"
   "$LDPC/ldpc_luts_impl.cpp:"
@@ -34,7 +35,23 @@ SRCS=(
   "$REF/lib/phy/upper/log_likelihood_ratio.cpp:-mavx2"
   "$REF/lib/srsvec/bit.cpp:-mavx2"
   "$REF/lib/srsvec/compare.cpp:-mavx2"
+  "$REF/lib/srsvec/dot_prod.cpp:-mavx2 -mfma"
+  "$REF/lib/srsvec/sc_prod.cpp:-mavx2 -mfma"
+  "$REF/lib/srsvec/conversion.cpp:-mavx2 -mfma"
   "$HERE/ref/ref_shim.cpp:-mavx2"
+  "$PDSCH/pdsch_modulator_impl.cpp:-mavx2 -I$PDSCH"
+  "$REF/lib/phy/upper/channel_modulation/modulation_mapper_lut_impl.cpp:-mavx2"
+  "$REF/lib/phy/upper/sequence_generators/pseudo_random_generator_impl.cpp:-mavx2"
+  "$REF/lib/phy/support/resource_grid_mapper_impl.cpp:-mavx2"
+  "$REF/lib/phy/support/resource_grid_impl.cpp:-mavx2"
+  "$REF/lib/phy/support/resource_grid_writer_impl.cpp:-mavx2"
+  "$REF/lib/phy/support/resource_grid_reader_impl.cpp:-mavx2"
+  "$REF/lib/phy/support/re_pattern.cpp:-mavx2"
+  "$REF/lib/phy/generic_functions/precoding/channel_precoder_generic.cpp:-mavx2"
+  "$REF/lib/phy/generic_functions/precoding/channel_precoder_impl.cpp:-mavx2"
+  "$REF/lib/phy/upper/rb_allocation.cpp:-mavx2"
+  "$REF/lib/ran/resource_allocation/vrb_to_prb.cpp:-mavx2"
+  "$HERE/ref/ref_pdsch_mod.cpp:-mavx2 -I$REF"
 )
 OBJS=()
 pids=()

@@ -80,3 +80,22 @@ def pdsch_encoder_cases():
         to += tb_bytes
         co += cb
         mo += ncb
+
+
+def pdsch_modulator_cases():
+    """Yields (cfg dict, nof_bits, grid_nof_prb, weights (P x L complex64), packed codeword, grid uint16
+    (P, 14, 12 * grid_nof_prb, 2)) made by the reference's pdsch_modulator_impl."""
+    from oracle_lib import PDSCH_MOD_KEYS
+    d = _load("pdsch_modulator.npz")
+    wo = co = go = 0
+    for row, scaling in zip(d["cfg"], d["scaling"]):
+        cfg = {k: int(v) for k, v in zip(PDSCH_MOD_KEYS[:-1], row[:-2])}
+        cfg["scaling"] = float(scaling)
+        nbits, grid_prb = int(row[-2]), int(row[-1])
+        P, L = cfg["nof_ports"], cfg["nof_layers"]
+        nw, nc, ng = P * L, (nbits + 7) // 8, P * 14 * 12 * grid_prb * 2
+        yield (cfg, nbits, grid_prb, d["weights"][wo:wo + nw].reshape(P, L), d["cw"][co:co + nc],
+               d["grid"][go:go + ng].reshape(P, 14, 12 * grid_prb, 2))
+        wo += nw
+        co += nc
+        go += ng

@@ -64,6 +64,40 @@ class _Lib:
                                   llr.size, _ptr(out))
         return r, out
 
+    def pdsch_modulate(self, cfg, weights, cw_packed, nof_bits, grid_nof_prb, grid=None):
+        """PDSCH modulator (ref_pdsch_modulate / orc_pdsch_modulate): returns the grid as uint16 bf16 bit patterns,
+        shape (nof_ports, 14, 12 * grid_nof_prb, 2). `cfg` is a PdschModConfig-like mapping (see PDSCH_MOD_KEYS)."""
+        f = self._f("pdsch_modulate")
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_int] * 11 + [ctypes.c_uint, ctypes.c_int, ctypes.c_int, ctypes.c_float, _P, _P,
+                                            ctypes.c_int, ctypes.c_int, _P]
+        w = np.ascontiguousarray(weights, dtype=np.complex64).view(np.float32)
+        cw = np.ascontiguousarray(cw_packed, dtype=np.uint8)
+        if grid is None:
+            grid = np.zeros((cfg["nof_ports"], 14, 12 * grid_nof_prb, 2), np.uint16)
+        r = f(*[int(cfg[k]) for k in PDSCH_MOD_KEYS[:11]], ctypes.c_uint(int(cfg["dmrs_symbol_mask"])),
+              int(cfg["dmrs_type2"]), int(cfg["nof_cdm_groups_without_data"]), float(cfg["scaling"]), _ptr(w),
+              _ptr(cw), int(nof_bits), int(grid_nof_prb), _ptr(grid))
+        assert r == 0, r
+        return grid
+
+
+PDSCH_MOD_KEYS = ["rnti", "n_id", "qm", "nof_layers", "nof_ports", "bwp_start_rb", "bwp_size_rb", "rb_start", "nof_rb",
+                  "start_symbol", "nof_symbols", "dmrs_symbol_mask", "dmrs_type2", "nof_cdm_groups_without_data",
+                  "scaling"]
+
+
+def pdsch_mod_nof_re(cfg):
+    """Data REs of a PDSCH modulator configuration (DM-RS REs of the DM-RS symbols excluded)."""
+    if cfg["dmrs_type2"]:
+        dm = 4 * cfg["nof_cdm_groups_without_data"]
+    else:
+        dm = 6 * cfg["nof_cdm_groups_without_data"]
+    n = 0
+    for l in range(cfg["start_symbol"], cfg["start_symbol"] + cfg["nof_symbols"]):
+        n += (12 - dm if (cfg["dmrs_symbol_mask"] >> l) & 1 else 12) * cfg["nof_rb"]
+    return n
+
 
 class Oracle(_Lib):
     def __init__(self, path=ORACLE_SO):

@@ -58,3 +58,11 @@ def test_pdsch_encoder_golden(orc):
         assert np.array_equal(cw, c["cw"])
         n += 1
     assert n == 14
+
+
+def test_pdsch_modulator_golden(orc):
+    n = 0
+    for cfg, nbits, grid_prb, w, cw, grid in G.pdsch_modulator_cases():
+        assert np.array_equal(orc.pdsch_modulate(cfg, w, cw, nbits, grid_prb), grid), cfg
+        n += 1
+    assert n == 12

@@ -170,3 +170,24 @@ def test_rate_dematch_limited_buffer_short_input(orc, ref, bg, Z, rv, qm, filler
             want = ref.rate_dematch(impl, bg, Z, rv, qm, Nref, filler, new_data, llr, init)
             got = orc.rate_dematch(mode, bg, Z, rv, qm, Nref, filler, new_data, llr, init)
             assert np.array_equal(got, want), (new_data, mode)
+
+
+def test_pdsch_modulator_random(orc, ref):
+    from pdsch_mod_cases import random_config
+    rng = np.random.default_rng(77)
+    for _ in range(80):
+        cfg, nbits, w = random_config(rng, 40)
+        cw = rng.integers(0, 256, (nbits + 7) // 8).astype(np.uint8)
+        want = ref.pdsch_modulate(cfg, w, cw, nbits, 40)
+        assert np.array_equal(orc.pdsch_modulate(cfg, w, cw, nbits, 40), want), cfg
+
+
+def test_pdsch_modulator_full_band(orc, ref):
+    from pdsch_mod_cases import full_band_config
+    rng = np.random.default_rng(78)
+    for L, qm in ((4, 8), (2, 6), (1, 2), (3, 4)):
+        cfg, nbits = full_band_config(L, qm)
+        w = (rng.normal(size=(4, L)) + 1j * rng.normal(size=(4, L))).astype(np.complex64)
+        cw = rng.integers(0, 256, (nbits + 7) // 8).astype(np.uint8)
+        want = ref.pdsch_modulate(cfg, w, cw, nbits, 273)
+        assert np.array_equal(orc.pdsch_modulate(cfg, w, cw, nbits, 273), want), (L, qm)

@@ -147,6 +147,25 @@ def gen_pdsch_encoder(ref, rng):
                         cw=np.concatenate(cws), meta=np.concatenate(metas))
 
 
+def gen_pdsch_modulator(ref, rng):
+    from oracle_lib import PDSCH_MOD_KEYS
+    from pdsch_mod_cases import random_config
+    grid_prb = 24
+    cfgs, scal, ws, cws, grids = [], [], [], [], []
+    for i in range(12):
+        cfg, nbits, w = random_config(rng, grid_prb, qm=[2, 4, 6, 8][i % 4])
+        cw = rng.integers(0, 256, (nbits + 7) // 8).astype(np.uint8)
+        grid = ref.pdsch_modulate(cfg, w, cw, nbits, grid_prb)
+        cfgs.append([cfg[k] for k in PDSCH_MOD_KEYS[:-1]] + [nbits, grid_prb])
+        scal.append(cfg["scaling"])
+        ws.append(w.ravel())
+        cws.append(cw)
+        grids.append(grid.ravel())
+    np.savez_compressed(os.path.join(OUT, "pdsch_modulator.npz"), cfg=np.array(cfgs, np.int64),
+                        scaling=np.array(scal, np.float32), weights=np.concatenate(ws), cw=np.concatenate(cws),
+                        grid=np.concatenate(grids))
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     ref = Reference()
@@ -155,6 +174,7 @@ def main():
     gen_decoder(ref, np.random.default_rng(12))
     gen_rate_matching(ref, np.random.default_rng(13))
     gen_pdsch_encoder(ref, np.random.default_rng(14))
+    gen_pdsch_modulator(ref, np.random.default_rng(15))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

@@ -200,6 +200,62 @@ int srsgpu_pdsch_encoder_plan_enable_timing(srsgpu_pdsch_encoder_plan* plan, int
 int srsgpu_pdsch_encoder_plan_stage_times(srsgpu_pdsch_encoder_plan* plan, float* ms, uint32_t* nof_executes);
 
 /* ------------------------------------------------------------------------------------------------------------------
+ * PDSCH modulator — replaces srsran::pdsch_modulator::modulate(resource_grid_writer& grid, span<const bit_buffer>
+ * codewords, const config_t& config) (include/srsran/phy/upper/channel_processors/pdsch/pdsch_modulator.h:93,
+ * lib/phy/upper/channel_processors/pdsch/pdsch_modulator_impl.cpp:107): scrambling with the TS 38.211 §5.2.1 Gold
+ * sequence (c_init = rnti * 2^15 + n_id, codeword q = 0, :30), modulation mapping (modulation_mapper_lut_impl.cpp:39,
+ * amplitude sqrt(1 / average power) times `scaling`), layer mapping, wideband precoding (channel_precoder_generic.cpp:51)
+ * and resource-element mapping (resource_grid_mapper_impl.cpp:269) into bf16 resource grids, for every PDSCH
+ * transmission of a batch of slots. Codewords come packed MSB first (the PDSCH encoder's output format).
+ * A resource grid holds `grid_nof_ports` x 14 symbols x 12 * `grid_nof_prb` subcarriers of complex bf16 (re, im)
+ * pairs (srsran::cbf16_t), port-major then symbol-major; grid g starts g * grid_nof_ports * 14 * 12 * grid_nof_prb
+ * elements into d_grids. Only the PDSCH REs are written (the DM-RS REs belong to the DM-RS processor).
+ * ------------------------------------------------------------------------------------------------------------------ */
+typedef struct {
+  uint16_t rnti;                        /* n_RNTI */
+  uint16_t n_id;                        /* n_ID, 0..1023 */
+  uint8_t  modulation_order;            /* Qm of modulation1: 2 (QPSK), 4, 6, 8 (256QAM) */
+  uint8_t  nof_layers;                  /* 1..4 */
+  uint8_t  nof_ports;                   /* precoding ports, nof_layers..4 (<= grid_nof_ports) */
+  uint8_t  start_symbol;                /* start_symbol_index */
+  uint8_t  nof_symbols;                 /* start_symbol + nof_symbols <= 14 */
+  uint8_t  dmrs_type;                   /* dmrs_config_type: 1 or 2 */
+  uint8_t  nof_cdm_groups_without_data; /* 1..2 (type 1), 1..3 (type 2) */
+  uint8_t  reserved;
+  uint16_t dmrs_symbol_mask;            /* dmrs_symb_pos: bit l = OFDM symbol l carries DM-RS */
+  uint16_t bwp_start_rb;                /* BWP start (CRB) */
+  uint16_t bwp_size_rb;                 /* BWP size */
+  uint16_t rb_start;                    /* contiguous non-interleaved VRB allocation [rb_start, rb_start + nof_rb) */
+  uint16_t nof_rb;
+  uint16_t pad;
+  float    scaling;                     /* config.scaling (applied when std::isnormal) */
+  float    precoding[4][4][2];          /* wideband precoding weight [port][layer] = (re, im) */
+  uint32_t cw_offset;                   /* byte offset of the packed codeword (multiple of 4) */
+  uint32_t nof_bits;                    /* codeword length: data REs x nof_layers x Qm */
+  uint32_t grid_index;                  /* resource grid (slot) the transmission is mapped into */
+} srsgpu_pdsch_mod_config;
+
+typedef struct srsgpu_pdsch_modulator_plan srsgpu_pdsch_modulator_plan;
+
+/** Validates the transmissions (the reference's assertions: time allocation inside the slot, allocation inside the
+ *  BWP and the grid, codeword length equal to the allocation's data REs x layers x Qm) and uploads the work. */
+int srsgpu_pdsch_modulator_plan_create(srsgpu_context*                ctx,
+                                       const srsgpu_pdsch_mod_config* cfgs,
+                                       uint32_t                       nof_tx,
+                                       uint32_t                       grid_nof_prb,
+                                       uint32_t                       grid_nof_ports,
+                                       srsgpu_pdsch_modulator_plan**  plan);
+
+/** Modulates and maps every planned transmission from d_codewords into d_grids (uint32 per RE: re | im << 16).
+ *  Asynchronous on `stream`, hipGraph-capturable. */
+int srsgpu_pdsch_modulator_plan_execute(const srsgpu_pdsch_modulator_plan* plan,
+                                        const uint8_t*                     d_codewords,
+                                        uint32_t*                          d_grids,
+                                        void*                              stream);
+
+void srsgpu_pdsch_modulator_plan_destroy(srsgpu_pdsch_modulator_plan* plan);
+
+/* ------------------------------------------------------------------------------------------------------------------
  * PUSCH decoder (transport-block level) — replaces srsran::pusch_decoder (include/srsran/phy/upper/channel_processors/
  * pusch/pusch_decoder.h; lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.cpp: new_data :98, segmentation
  * :190, codeblock tasks :283, join_and_notify :386): segmentation, per-codeblock rate dematching + HARQ combining +

@@ -5,6 +5,7 @@
 #include "ldpc_base_graphs.h"
 #include "sch_host.h"
 #include "srsgpu_internal.h"
+#include "capi_internal.h"
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdarg>
@@ -19,29 +20,15 @@
 
 using namespace srsgpu;
 
-namespace {
-
+namespace srsgpu {
 thread_local std::string g_last_error = "";
-
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-int fail(int code, const char* fmt, ...)
+void set_last_error(const char* msg)
 {
-  char    buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof(buf), fmt, ap);
-  va_end(ap);
-  g_last_error = buf;
-  return code;
+  g_last_error = msg;
 }
+} // namespace srsgpu
 
-#define HIP_TRY(expr)                                                                                                  \
-  do {                                                                                                                 \
-    hipError_t err_ = (expr);                                                                                          \
-    if (err_ != hipSuccess) {                                                                                          \
-      return fail(SRSGPU_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(err_));                                    \
-    }                                                                                                                  \
-  } while (0)
+namespace {
 
 int lifting_position(int Z)
 {
@@ -67,96 +54,8 @@ bool crc_params(int poly, unsigned& order, uint64_t& g)
   }
 }
 
-constexpr size_t CRC_ARENA_WORDS = 16u << 20;  // 64 MiB of contribution tables
 
 } // namespace
-
-struct srsgpu_context {
-  int                                  device      = 0;
-  uint16_t*                            d_shifts[2] = {nullptr, nullptr};
-  uint32_t*                            d_shifts32[2] = {nullptr, nullptr};  ///< Same, one dword per shift (decoder).
-  /// Packed decoder address constants A | B << 16 per (Z position, edge), see ldpc_decoder_pk.hip (even Z only).
-  uint32_t*                            d_pair_ab[2] = {nullptr, nullptr};
-  core_plan*                           d_core[2]   = {nullptr, nullptr};
-  std::vector<core_plan>               core[2];
-  uint32_t*                            d_crc_arena = nullptr;
-  size_t                               crc_used    = 0;
-  std::map<std::pair<int, int>, size_t> crc_tables;
-  std::mutex                           mtx;
-};
-
-/// Per-stage device time accounting: HIP events recorded around every kernel stage on the execution stream.
-struct stage_timer {
-  bool                                  enabled = false;
-  int                                   stages  = 0;
-  std::vector<std::vector<hipEvent_t>>  pending;  ///< One event set (stages + 1) per timed execute.
-  std::vector<std::vector<hipEvent_t>>  pool;
-  std::vector<double>                   acc_ms;
-  uint32_t                              count = 0;
-
-  ~stage_timer()
-  {
-    for (auto* v : {&pending, &pool}) {
-      for (auto& set : *v) {
-        for (hipEvent_t e : set) {
-          (void)hipEventDestroy(e);
-        }
-      }
-    }
-  }
-  /// Returns the event set for this execute (nullptr when disabled).
-  std::vector<hipEvent_t>* begin()
-  {
-    if (!enabled) {
-      return nullptr;
-    }
-    if (pool.empty()) {
-      std::vector<hipEvent_t> set(static_cast<size_t>(stages) + 1);
-      for (auto& e : set) {
-        if (hipEventCreate(&e) != hipSuccess) {
-          return nullptr;
-        }
-      }
-      pool.push_back(std::move(set));
-    }
-    pending.push_back(std::move(pool.back()));
-    pool.pop_back();
-    return &pending.back();
-  }
-  static void mark(std::vector<hipEvent_t>* set, int i, hipStream_t s)
-  {
-    if (set != nullptr) {
-      (void)hipEventRecord((*set)[static_cast<size_t>(i)], s);
-    }
-  }
-  /// Synchronises on the pending events and accumulates the stage durations.
-  int collect(float* out_ms, uint32_t* nof_executes)
-  {
-    acc_ms.resize(static_cast<size_t>(stages), 0.0);
-    for (auto& set : pending) {
-      if (hipEventSynchronize(set.back()) != hipSuccess) {
-        return -1;
-      }
-      for (int i = 0; i < stages; ++i) {
-        float ms = 0;
-        if (hipEventElapsedTime(&ms, set[static_cast<size_t>(i)], set[static_cast<size_t>(i) + 1]) != hipSuccess) {
-          return -1;
-        }
-        acc_ms[static_cast<size_t>(i)] += ms;
-      }
-      ++count;
-      pool.push_back(std::move(set));
-    }
-    pending.clear();
-    for (int i = 0; i < stages; ++i) {
-      out_ms[i] = static_cast<float>(acc_ms[static_cast<size_t>(i)]);
-    }
-    *nof_executes = count;
-    std::fill(acc_ms.begin(), acc_ms.end(), 0.0);
-    count = 0;
-    return 0;
-  }
-};
 
 struct srsgpu_pusch_cb_plan {
   srsgpu_context*           ctx     = nullptr;
@@ -453,8 +352,10 @@ void srsgpu_context_destroy(srsgpu_context* ctx)
       (void)hipFree(p);
     }
   }
-  if (ctx->d_crc_arena != nullptr) {
-    (void)hipFree(ctx->d_crc_arena);
+  for (uint32_t* p : {ctx->d_crc_arena, ctx->d_gold_x1, ctx->d_gold_x2_jump, ctx->d_gold_x2_lane}) {
+    if (p != nullptr) {
+      (void)hipFree(p);
+    }
   }
   delete ctx;
 }

@@ -1,0 +1,135 @@
+// Host-side internals shared by the C-ABI translation units (capi*.cpp): error reporting, the device context and the
+// per-stage event timer. Not part of the public C ABI.
+#pragma once
+
+#include "srsgpu_phy.h"
+#include "srsgpu_internal.h"
+#include <hip/hip_runtime.h>
+#include <cstdarg>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace srsgpu {
+
+/// Stores the thread-local message returned by srsgpu_last_error().
+void set_last_error(const char* msg);
+
+inline int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+inline int fail(int code, const char* fmt, ...)
+{
+  char    buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  set_last_error(buf);
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                                                  \
+  do {                                                                                                                 \
+    hipError_t err_ = (expr);                                                                                          \
+    if (err_ != hipSuccess) {                                                                                          \
+      return fail(SRSGPU_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(err_));                                    \
+    }                                                                                                                  \
+  } while (0)
+
+constexpr size_t CRC_ARENA_WORDS = 16u << 20;  // 64 MiB of contribution tables
+
+} // namespace srsgpu
+
+struct srsgpu_context {
+  int                                  device      = 0;
+  uint16_t*                            d_shifts[2] = {nullptr, nullptr};
+  uint32_t*                            d_shifts32[2] = {nullptr, nullptr};  ///< Same, one dword per shift (decoder).
+  /// Packed decoder address constants A | B << 16 per (Z position, edge), see ldpc_decoder_pk.hip (even Z only).
+  uint32_t*                            d_pair_ab[2] = {nullptr, nullptr};
+  srsgpu::core_plan*                   d_core[2]   = {nullptr, nullptr};
+  std::vector<srsgpu::core_plan>       core[2];
+  uint32_t*                            d_crc_arena = nullptr;
+  size_t                               crc_used    = 0;
+  std::map<std::pair<int, int>, size_t> crc_tables;
+  /// Gold-sequence jump tables of the scrambler (built on first use, see srsgpu::gold_tables): x1 words, x2 chunk
+  /// jumps M^(Nc + 2048 c) and x2 lane jumps M^(32 i), each matrix as 31 column words.
+  uint32_t*                            d_gold_x1      = nullptr;
+  uint32_t*                            d_gold_x2_jump = nullptr;
+  uint32_t*                            d_gold_x2_lane = nullptr;
+  std::mutex                           mtx;
+};
+
+/// Per-stage device time accounting: HIP events recorded around every kernel stage on the execution stream.
+struct stage_timer {
+  bool                                  enabled = false;
+  int                                   stages  = 0;
+  std::vector<std::vector<hipEvent_t>>  pending;  ///< One event set (stages + 1) per timed execute.
+  std::vector<std::vector<hipEvent_t>>  pool;
+  std::vector<double>                   acc_ms;
+  uint32_t                              count = 0;
+
+  ~stage_timer()
+  {
+    for (auto* v : {&pending, &pool}) {
+      for (auto& set : *v) {
+        for (hipEvent_t e : set) {
+          (void)hipEventDestroy(e);
+        }
+      }
+    }
+  }
+  /// Returns the event set for this execute (nullptr when disabled).
+  std::vector<hipEvent_t>* begin()
+  {
+    if (!enabled) {
+      return nullptr;
+    }
+    if (pool.empty()) {
+      std::vector<hipEvent_t> set(static_cast<size_t>(stages) + 1);
+      for (auto& e : set) {
+        if (hipEventCreate(&e) != hipSuccess) {
+          return nullptr;
+        }
+      }
+      pool.push_back(std::move(set));
+    }
+    pending.push_back(std::move(pool.back()));
+    pool.pop_back();
+    return &pending.back();
+  }
+  static void mark(std::vector<hipEvent_t>* set, int i, hipStream_t s)
+  {
+    if (set != nullptr) {
+      (void)hipEventRecord((*set)[static_cast<size_t>(i)], s);
+    }
+  }
+  /// Synchronises on the pending events and accumulates the stage durations.
+  int collect(float* out_ms, uint32_t* nof_executes)
+  {
+    acc_ms.resize(static_cast<size_t>(stages), 0.0);
+    for (auto& set : pending) {
+      if (hipEventSynchronize(set.back()) != hipSuccess) {
+        return -1;
+      }
+      for (int i = 0; i < stages; ++i) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, set[static_cast<size_t>(i)], set[static_cast<size_t>(i) + 1]) != hipSuccess) {
+          return -1;
+        }
+        acc_ms[static_cast<size_t>(i)] += ms;
+      }
+      ++count;
+      pool.push_back(std::move(set));
+    }
+    pending.clear();
+    for (int i = 0; i < stages; ++i) {
+      out_ms[i] = static_cast<float>(acc_ms[static_cast<size_t>(i)]);
+    }
+    *nof_executes = count;
+    std::fill(acc_ms.begin(), acc_ms.end(), 0.0);
+    count = 0;
+    return 0;
+  }
+};
+

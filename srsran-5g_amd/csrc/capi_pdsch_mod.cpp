@@ -1,0 +1,308 @@
+// Host side of the PDSCH modulator C ABI (include/srsgpu_phy.h): validation with the reference's conditions, the
+// Gold-sequence jump tables (once per context) and the per-transmission descriptors / per-chunk work items.
+#include "capi_internal.h"
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+using namespace srsgpu;
+
+static_assert(sizeof(srsgpu_pdsch_mod_config) == 168, "srsgpu_pdsch_mod_config layout (mirrored by srsgpu.PdschModConfig)");
+
+struct srsgpu_pdsch_modulator_plan {
+  srsgpu_context* ctx        = nullptr;
+  mod_desc*       d_desc     = nullptr;
+  mod_chunk*      d_chunks   = nullptr;
+  int             nof_chunks = 0;
+};
+
+namespace {
+
+/// One step of the x2 LFSR on its 31-bit window (bit k = x2(n + k)): x2(n + 31) = x2(n + 3) + x2(n + 2) + x2(n + 1) +
+/// x2(n) (TS 38.211 section 5.2.1).
+uint32_t x2_step(uint32_t s)
+{
+  const uint32_t nb = (s ^ (s >> 1) ^ (s >> 2) ^ (s >> 3)) & 1u;
+  return (s >> 1) | (nb << 30);
+}
+
+uint32_t x1_step(uint32_t s)
+{
+  const uint32_t nb = (s ^ (s >> 3)) & 1u;
+  return (s >> 1) | (nb << 30);
+}
+
+uint32_t gf2_apply(const uint32_t* cols, uint32_t v)
+{
+  uint32_t r = 0;
+  for (int j = 0; j < 31; ++j) {
+    if ((v >> j) & 1u) {
+      r ^= cols[j];
+    }
+  }
+  return r;
+}
+
+/// Builds and uploads the scrambler's Gold-sequence tables into the context (once; caller holds ctx->mtx).
+int ensure_gold_tables(srsgpu_context* ctx)
+{
+  if (ctx->d_gold_x1 != nullptr) {
+    return SRSGPU_OK;
+  }
+  // x1 (initial state x1(0) = 1): words of x1(Nc + 32 w + k), bit k.
+  std::vector<uint32_t> x1(GOLD_X1_WORDS, 0u);
+  uint32_t              s = 1;
+  for (uint32_t n = 0; n < GOLD_NC; ++n) {
+    s = x1_step(s);
+  }
+  for (uint32_t w = 0; w < GOLD_X1_WORDS; ++w) {
+    uint32_t word = 0;
+    for (int k = 0; k < 32; ++k) {
+      word |= (s & 1u) << k;
+      s = x1_step(s);
+    }
+    x1[w] = word;
+  }
+  // Lane jumps M^(32 i), stored [column j][i].
+  std::vector<uint32_t> lane(31 * 64);
+  for (int j = 0; j < 31; ++j) {
+    uint32_t v = 1u << j;
+    for (int i = 0; i < 64; ++i) {
+      lane[static_cast<size_t>(j) * 64 + static_cast<size_t>(i)] = v;
+      for (int k = 0; k < 32; ++k) {
+        v = x2_step(v);
+      }
+    }
+  }
+  // Chunk jumps M^(Nc + 2048 c): columns of M^Nc by stepping, then repeated products with M^2048.
+  uint32_t m2048[31], cur[31];
+  for (int j = 0; j < 31; ++j) {
+    uint32_t v = 1u << j, u = 1u << j;
+    for (int k = 0; k < 2048; ++k) {
+      v = x2_step(v);
+    }
+    for (uint32_t k = 0; k < GOLD_NC; ++k) {
+      u = x2_step(u);
+    }
+    m2048[j] = v;
+    cur[j]   = u;
+  }
+  std::vector<uint32_t> jump(static_cast<size_t>(GOLD_X2_JUMPS) * 31);
+  for (uint32_t c = 0; c < GOLD_X2_JUMPS; ++c) {
+    std::memcpy(&jump[static_cast<size_t>(c) * 31], cur, sizeof(cur));
+    for (int j = 0; j < 31; ++j) {
+      cur[j] = gf2_apply(m2048, cur[j]);
+    }
+  }
+  uint32_t *d_x1 = nullptr, *d_jump = nullptr, *d_lane = nullptr;
+  if (hipMalloc(&d_x1, x1.size() * 4) != hipSuccess || hipMalloc(&d_jump, jump.size() * 4) != hipSuccess ||
+      hipMalloc(&d_lane, lane.size() * 4) != hipSuccess ||
+      hipMemcpy(d_x1, x1.data(), x1.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d_jump, jump.data(), jump.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d_lane, lane.data(), lane.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    for (uint32_t* p : {d_x1, d_jump, d_lane}) {
+      if (p != nullptr) {
+        (void)hipFree(p);
+      }
+    }
+    return fail(SRSGPU_ERR_HIP, "failed to upload the Gold sequence tables");
+  }
+  ctx->d_gold_x1      = d_x1;
+  ctx->d_gold_x2_jump = d_jump;
+  ctx->d_gold_x2_lane = d_lane;
+  return SRSGPU_OK;
+}
+
+/// TS 38.211 section 5.1 constellation point (integer grid) of `index`, as modulation_mapper_lut_impl.cpp:39 builds
+/// its tables; used for the average power only.
+void constellation_point(unsigned qm, unsigned index, int& re, int& im)
+{
+  int offset = -1, real = 0, imag = 0;
+  for (unsigned j = 0; j < qm / 2; ++j) {
+    real += offset;
+    imag += offset;
+    offset *= 2;
+    real *= ((index >> (2 * j + 1)) & 1U) ? 1 : -1;
+    imag *= ((index >> (2 * j)) & 1U) ? 1 : -1;
+  }
+  re = real;
+  im = imag;
+}
+
+/// Amplitude sqrt(1 / average power) of the modulation mapper's integer constellation (modulation_mapper_lut_impl.cpp
+/// returns it as the scaling the modulator applies through the precoding weights, pdsch_modulator_impl.cpp:93).
+float modulation_amplitude(unsigned qm)
+{
+  double acc = 0;
+  for (unsigned i = 0; i < (1U << qm); ++i) {
+    int re, im;
+    constellation_point(qm, i, re, im);
+    acc += re * re + im * im;
+  }
+  const float avg = static_cast<float>(acc / (1U << qm));
+  return std::sqrt(1 / avg);
+}
+
+} // namespace
+
+extern "C" {
+
+int srsgpu_pdsch_modulator_plan_create(srsgpu_context*                ctx,
+                                       const srsgpu_pdsch_mod_config* cfgs,
+                                       uint32_t                       nof_tx,
+                                       uint32_t                       grid_nof_prb,
+                                       uint32_t                       grid_nof_ports,
+                                       srsgpu_pdsch_modulator_plan**  plan_out)
+{
+  if (ctx == nullptr || plan_out == nullptr || (cfgs == nullptr && nof_tx > 0)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  if (grid_nof_prb == 0 || grid_nof_prb > 275 || grid_nof_ports == 0 || grid_nof_ports > 4) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "invalid grid geometry (%u PRB, %u ports)", grid_nof_prb, grid_nof_ports);
+  }
+  std::lock_guard<std::mutex> lock(ctx->mtx);
+  HIP_TRY(hipSetDevice(ctx->device));
+  int r = ensure_gold_tables(ctx);
+  if (r != SRSGPU_OK) {
+    return r;
+  }
+  const uint32_t         nsc = 12u * grid_nof_prb;
+  std::vector<mod_desc>  descs(nof_tx);
+  std::vector<mod_chunk> chunks;
+  for (uint32_t t = 0; t < nof_tx; ++t) {
+    const srsgpu_pdsch_mod_config& c  = cfgs[t];
+    const unsigned                 qm = c.modulation_order;
+    if (qm != 2 && qm != 4 && qm != 6 && qm != 8) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid modulation order %u", t, qm);
+    }
+    if (c.nof_layers < 1 || c.nof_layers > 4 || c.nof_ports < c.nof_layers || c.nof_ports > grid_nof_ports) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid layers/ports (%u, %u)", t, c.nof_layers, c.nof_ports);
+    }
+    // pdsch_modulator_impl.cpp:61: the time allocation must not exceed the slot boundary.
+    if (c.nof_symbols < 1 || c.start_symbol + c.nof_symbols > 14) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: time allocation [%u, %u) exceeds the slot", t, c.start_symbol,
+                  c.start_symbol + c.nof_symbols);
+    }
+    if ((c.dmrs_type != 1 && c.dmrs_type != 2) || c.nof_cdm_groups_without_data < 1 ||
+        c.nof_cdm_groups_without_data > (c.dmrs_type == 1 ? 2 : 3)) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid DM-RS type %u / CDM groups without data %u", t,
+                  c.dmrs_type, c.nof_cdm_groups_without_data);
+    }
+    if (c.n_id > 1023 || c.bwp_size_rb < 1 || c.bwp_start_rb + c.bwp_size_rb > grid_nof_prb || c.nof_rb < 1 ||
+        c.rb_start + c.nof_rb > c.bwp_size_rb) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: allocation outside the BWP or the grid, or n_id > 1023", t);
+    }
+    if (c.cw_offset % 4 != 0) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: codeword offset not a multiple of 4", t);
+    }
+    mod_desc d{};
+    // DM-RS RE pattern of a PRB (dmrs_mapping.h): type 1 CDM group g on subcarriers 2k + g, type 2 on 6k + 2g + {0, 1}.
+    unsigned nd = 0;
+    for (unsigned k = 0; k < 12; ++k) {
+      const unsigned group = (c.dmrs_type == 2) ? (k % 6) / 2 : k % 2;
+      if (group >= c.nof_cdm_groups_without_data) {
+        d.dmrs_lut |= static_cast<uint64_t>(k) << (4 * nd);
+        ++nd;
+      }
+    }
+    d.nd_dmrs = static_cast<uint8_t>(nd);
+    uint32_t nre = 0;
+    for (unsigned l = 0; l < 14; ++l) {
+      d.sym_cum[l] = static_cast<uint16_t>(nre);
+      if (l >= c.start_symbol && l < static_cast<unsigned>(c.start_symbol + c.nof_symbols)) {
+        nre += (((c.dmrs_symbol_mask >> l) & 1u) ? nd : 12u) * c.nof_rb;
+      }
+    }
+    d.sym_cum[14] = static_cast<uint16_t>(nre);
+    d.sym_cum[15] = static_cast<uint16_t>(nre);
+    const uint64_t need = static_cast<uint64_t>(nre) * c.nof_layers * qm;
+    if (nre == 0 || need != c.nof_bits || c.nof_bits > MOD_MAX_BITS) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: codeword of %u bits for %u data REs x %u layers x Qm %u", t,
+                  c.nof_bits, nre, c.nof_layers, qm);
+    }
+    d.cw_word_offset = c.cw_offset / 4;
+    d.nof_bits       = c.nof_bits;
+    d.c_init         = (static_cast<uint32_t>(c.rnti) << 15) + c.n_id;  // pdsch_modulator_impl.cpp:35, q = 0
+    d.port_stride    = 14u * nsc;
+    d.nsc            = nsc;
+    d.grid_base      = c.grid_index * grid_nof_ports * 14u * nsc + (c.bwp_start_rb + c.rb_start) * 12u;
+    d.dmrs_mask      = c.dmrs_symbol_mask;
+    d.qm             = static_cast<uint8_t>(qm);
+    d.L              = c.nof_layers;
+    d.P              = c.nof_ports;
+    // Modulation amplitude times the power scaling, folded into the precoding weights (pdsch_modulator_impl.cpp:93).
+    float amp = modulation_amplitude(qm);
+    if (std::isnormal(c.scaling)) {
+      amp *= c.scaling;
+    }
+    for (int p = 0; p < 4; ++p) {
+      for (int l = 0; l < 4; ++l) {
+        const bool used = p < c.nof_ports && l < c.nof_layers;
+        d.w[p][l][0]    = used ? c.precoding[p][l][0] * amp : 0.f;
+        d.w[p][l][1]    = used ? c.precoding[p][l][1] * amp : 0.f;
+      }
+    }
+    descs[t]              = d;
+    const uint32_t Lq     = static_cast<uint32_t>(c.nof_layers) * qm;
+    const uint32_t nwords = (c.nof_bits + 31) / 32;
+    for (uint32_t w0 = 0; w0 < nwords; w0 += MOD_CHUNK_WORDS) {
+      const uint32_t b0 = w0 * 32, b1 = b0 + MOD_CHUNK_WORDS * 32;
+      mod_chunk      ch{};
+      ch.tx       = t;
+      ch.word0    = w0;
+      ch.re_begin = (b0 + Lq - 1) / Lq;
+      ch.re_end   = std::min(nre, (b1 + Lq - 1) / Lq);
+      if (ch.re_end > ch.re_begin) {
+        chunks.push_back(ch);
+      }
+    }
+  }
+  auto* plan       = new srsgpu_pdsch_modulator_plan();
+  plan->ctx        = ctx;
+  plan->nof_chunks = static_cast<int>(chunks.size());
+  bool ok          = true;
+  if (!chunks.empty()) {
+    ok = hipMalloc(&plan->d_desc, descs.size() * sizeof(mod_desc)) == hipSuccess &&
+         hipMemcpy(plan->d_desc, descs.data(), descs.size() * sizeof(mod_desc), hipMemcpyHostToDevice) == hipSuccess &&
+         hipMalloc(&plan->d_chunks, chunks.size() * sizeof(mod_chunk)) == hipSuccess &&
+         hipMemcpy(plan->d_chunks, chunks.data(), chunks.size() * sizeof(mod_chunk), hipMemcpyHostToDevice) ==
+             hipSuccess;
+  }
+  if (!ok) {
+    srsgpu_pdsch_modulator_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload modulator descriptors");
+  }
+  *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+int srsgpu_pdsch_modulator_plan_execute(const srsgpu_pdsch_modulator_plan* plan,
+                                        const uint8_t*                     d_codewords,
+                                        uint32_t*                          d_grids,
+                                        void*                              stream)
+{
+  if (plan == nullptr || d_codewords == nullptr || d_grids == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  launch_pdsch_modulate(plan->d_desc, plan->d_chunks, plan->nof_chunks,
+                        reinterpret_cast<const uint32_t*>(d_codewords), d_grids, plan->ctx->d_gold_x1,
+                        plan->ctx->d_gold_x2_jump, plan->ctx->d_gold_x2_lane, static_cast<hipStream_t>(stream));
+  HIP_TRY(hipGetLastError());
+  return SRSGPU_OK;
+}
+
+void srsgpu_pdsch_modulator_plan_destroy(srsgpu_pdsch_modulator_plan* plan)
+{
+  if (plan == nullptr) {
+    return;
+  }
+  for (void* p : {static_cast<void*>(plan->d_desc), static_cast<void*>(plan->d_chunks)}) {
+    if (p != nullptr) {
+      (void)hipFree(p);
+    }
+  }
+  delete plan;
+}
+
+} // extern "C"

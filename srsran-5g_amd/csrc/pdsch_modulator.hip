@@ -1,0 +1,192 @@
+// PDSCH modulator on gfx950: scrambling + modulation mapping + layer mapping + wideband precoding + RE mapping into
+// bf16 resource grids, for every PDSCH transmission of a batch of slots.
+//
+// Reference (behaviour, not code): lib/phy/upper/channel_processors/pdsch/pdsch_modulator_impl.cpp:107 (modulate),
+// :30 (scramble), modulation_mapper_lut_impl.cpp:39 (constellations), support/resource_grid_mapper_impl.cpp:269 (RE
+// order), generic_functions/precoding/channel_precoder_generic.cpp:51 (precoding), adt/bf16.h:39 (rounding).
+//
+// Work decomposition: a workgroup owns 8192 codeword bits (256 words) of one transmission. Its four waves first stage
+// the scrambled words in LDS — the Gold sequence is evaluated at any position by jumping the x2 LFSR state with
+// precomputed GF(2) matrices (the chunk jump is wave-uniform: scalar loads; the per-lane jump is one column load per
+// set state bit) and reading x1 from a table — then every lane takes one RE whose bits start in the chunk: it forms
+// the L constellation points, precodes them for every port and stores one (re, im) bf16 pair per port. Consecutive
+// lanes hold consecutive REs of a symbol, so the grid stores are coalesced 4-byte writes. HBM-bound: the codeword is
+// read once (1 bit per bit) and every PDSCH RE of every port is written once (4 B).
+//
+// Floating point follows the reference exactly: every complex product term is rounded separately (no contraction),
+// layer terms are summed in layer order and the result is rounded to bf16 half-to-even.
+#include "srsgpu_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace srsgpu {
+namespace {
+
+constexpr int MOD_THREADS = 256;
+
+/// y = M v for a 31x31 GF(2) matrix given by its columns (wave-uniform operands: scalar path).
+__device__ __forceinline__ uint32_t gf2_apply_uniform(const uint32_t* __restrict__ cols, uint32_t v)
+{
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 31; ++j) {
+    r ^= cols[j] & (0u - ((v >> j) & 1u));
+  }
+  return r;
+}
+
+/// Scrambled codeword word w (bits 32w..32w+31, MSB first) of a transmission.
+__device__ __forceinline__ uint32_t scrambled_word(const mod_desc& d,
+                                                   const uint32_t* __restrict__ cw,
+                                                   const uint32_t* __restrict__ x1,
+                                                   const uint32_t* __restrict__ x2_jump,
+                                                   const uint32_t* __restrict__ x2_lane,
+                                                   uint32_t w,
+                                                   uint32_t c_uniform)
+{
+  // x2 state (x2(n), ..., x2(n + 30)) at n = Nc + 2048 c, then at n = Nc + 32 w.
+  const uint32_t sc = gf2_apply_uniform(x2_jump + c_uniform * 31u, d.c_init);
+  const uint32_t i  = w & 63u;
+  uint32_t       s  = 0;
+#pragma unroll
+  for (int j = 0; j < 31; ++j) {
+    if ((sc >> j) & 1u) {  // uniform branch
+      s ^= x2_lane[j * 64 + i];
+    }
+  }
+  // 32 sequence bits: the window plus x2(n + 31) = x2(n + 3) + x2(n + 2) + x2(n + 1) + x2(n).
+  const uint32_t x2w = s | (((s ^ (s >> 1) ^ (s >> 2) ^ (s >> 3)) & 1u) << 31);
+  const uint32_t seq = __builtin_bitreverse32(x1[w] ^ x2w);  // LSB-first -> MSB-first
+  return __builtin_bswap32(cw[d.cw_word_offset + w]) ^ seq;
+}
+
+__device__ __forceinline__ uint32_t to_bf16_bits(float v)
+{
+  const uint32_t u = __float_as_uint(v);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+__global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_desc* __restrict__ descs,
+                                                                      const mod_chunk* __restrict__ chunks,
+                                                                      const uint32_t* __restrict__ cw,
+                                                                      uint32_t* __restrict__ grids,
+                                                                      const uint32_t* __restrict__ x1,
+                                                                      const uint32_t* __restrict__ x2_jump,
+                                                                      const uint32_t* __restrict__ x2_lane)
+{
+  __shared__ uint32_t bits[MOD_CHUNK_WORDS + 1];
+  const mod_chunk ch  = chunks[blockIdx.x];
+  const mod_desc& d   = descs[ch.tx];
+  const uint32_t  tid = threadIdx.x;
+  const uint32_t  nwords = (d.nof_bits + 31u) >> 5;
+
+  // Stage the chunk's scrambled words (and the first word of the next chunk, for an RE straddling the boundary).
+  {
+    const uint32_t w = ch.word0 + tid;
+    // word0 is a multiple of 256: the 64 words of a wave share their 2048-bit jump.
+    const uint32_t c = __builtin_amdgcn_readfirstlane(w >> 6);
+    bits[tid]        = (w < nwords) ? scrambled_word(d, cw, x1, x2_jump, x2_lane, w, c) : 0u;
+    if (tid == 0) {
+      const uint32_t w2 = ch.word0 + MOD_CHUNK_WORDS;
+      bits[MOD_CHUNK_WORDS] = (w2 < nwords) ? scrambled_word(d, cw, x1, x2_jump, x2_lane, w2, w2 >> 6) : 0u;
+    }
+  }
+
+  // Per-transmission constants.
+  const uint32_t qm = d.qm, L = d.L, P = d.P, Lq = L * qm;
+  const uint32_t qmask = (1u << qm) - 1u;
+  float          w[4][4][2];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      w[p][l][0] = d.w[p][l][0];
+      w[p][l][1] = d.w[p][l][1];
+    }
+  }
+  __syncthreads();
+
+  for (uint32_t r = ch.re_begin + tid; r < ch.re_end; r += MOD_THREADS) {
+    // The RE's L * Qm bits, left-aligned in 64 bits.
+    const uint32_t o  = r * Lq - ch.word0 * 32u;
+    const uint32_t wi = o >> 5;
+    const uint64_t b  = ((static_cast<uint64_t>(bits[wi]) << 32) | bits[wi + 1]) << (o & 31u);
+
+    // OFDM symbol and subcarrier of the RE (allocation order: symbol-major, ascending subcarrier).
+    uint32_t l = 0;
+#pragma unroll
+    for (int j = 1; j < 15; ++j) {
+      l += (d.sym_cum[j] <= r) ? 1u : 0u;
+    }
+    const uint32_t k    = r - d.sym_cum[l];
+    const bool     dmrs = (d.dmrs_mask >> l) & 1u;
+    uint32_t       sc;
+    if (dmrs) {
+      const uint32_t nd  = d.nd_dmrs;
+      const uint32_t prb = k / nd;
+      const uint32_t j   = k - prb * nd;
+      sc                 = prb * 12u + static_cast<uint32_t>((d.dmrs_lut >> (4u * j)) & 15u);
+    } else {
+      sc = k;
+    }
+    const uint32_t e = d.grid_base + l * d.nsc + sc;
+
+    // Constellation points of the layers (TS 38.211 section 5.1 integer grid; the amplitude is in the weights).
+    float xr[4], xi[4];
+#pragma unroll
+    for (int ly = 0; ly < 4; ++ly) {
+      if (ly < static_cast<int>(L)) {
+        const uint32_t idx = static_cast<uint32_t>(b >> (64u - (ly + 1) * qm)) & qmask;
+        int            re = 0, im = 0, off = -1;
+        for (uint32_t j = 0; j < qm / 2; ++j) {
+          re += off;
+          im += off;
+          off *= 2;
+          re = ((idx >> (2 * j + 1)) & 1u) ? re : -re;
+          im = ((idx >> (2 * j)) & 1u) ? im : -im;
+        }
+        xr[ly] = static_cast<float>(re);
+        xi[ly] = static_cast<float>(im);
+      }
+    }
+
+    // Precoding: port p gets sum over layers of x_l * w(p, l).
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (p < static_cast<int>(P)) {
+        float sr = 0.f, si = 0.f;
+#pragma unroll
+        for (int ly = 0; ly < 4; ++ly) {
+          if (ly < static_cast<int>(L)) {
+            const float pr = xr[ly] * w[p][ly][0] - xi[ly] * w[p][ly][1];
+            const float pi = xr[ly] * w[p][ly][1] + xi[ly] * w[p][ly][0];
+            sr             = (ly == 0) ? pr : sr + pr;
+            si             = (ly == 0) ? pi : si + pi;
+          }
+        }
+        grids[e + static_cast<uint32_t>(p) * d.port_stride] = to_bf16_bits(sr) | (to_bf16_bits(si) << 16);
+      }
+    }
+  }
+}
+
+} // namespace
+
+void launch_pdsch_modulate(const mod_desc*  d_desc,
+                           const mod_chunk* d_chunks,
+                           int              nof_chunks,
+                           const uint32_t*  d_codewords,
+                           uint32_t*        d_grids,
+                           const uint32_t*  d_x1,
+                           const uint32_t*  d_x2_jump,
+                           const uint32_t*  d_x2_lane,
+                           hipStream_t      stream)
+{
+  if (nof_chunks <= 0) {
+    return;
+  }
+  hipLaunchKernelGGL(pdsch_modulate_kernel, dim3(static_cast<unsigned>(nof_chunks)), dim3(MOD_THREADS), 0, stream,
+                     d_desc, d_chunks, d_codewords, d_grids, d_x1, d_x2_jump, d_x2_lane);
+}
+
+} // namespace srsgpu

@@ -179,4 +179,51 @@ void launch_ldpc_decode(int                bg,
                         uint8_t*           d_cb_crc_ok,
                         hipStream_t        stream);
 
+/// PDSCH modulator (pdsch_modulator.hip): per-transmission descriptor.
+struct mod_desc {
+  uint64_t dmrs_lut;        ///< Data subcarriers (4 bits each, ascending) of a PRB on DM-RS symbols.
+  uint32_t cw_word_offset;  ///< First 32-bit word of the packed codeword.
+  uint32_t nof_bits;        ///< Codeword length G.
+  uint32_t c_init;          ///< Scrambling sequence initial state (31 bits).
+  uint32_t grid_base;       ///< Element of (port 0, symbol 0, first allocated subcarrier) in the grids.
+  uint32_t port_stride;     ///< Elements per port of a grid (14 * nsc).
+  uint32_t nsc;             ///< Subcarriers per OFDM symbol.
+  uint16_t dmrs_mask;       ///< DM-RS symbols.
+  uint8_t  qm;              ///< Modulation order.
+  uint8_t  L;               ///< Layers.
+  uint8_t  P;               ///< Ports.
+  uint8_t  nd_dmrs;         ///< Data REs per PRB on DM-RS symbols.
+  uint16_t pad;
+  uint16_t sym_cum[16];     ///< Data REs in the symbols before symbol l (l = 0..14).
+  float    w[4][4][2];      ///< Precoding weights [port][layer] times the modulation amplitude.
+};
+static_assert(sizeof(mod_desc) == 200, "mod_desc layout");
+
+/// PDSCH modulator work item: 8192 codeword bits (256 words) of one transmission and the REs starting in them.
+struct mod_chunk {
+  uint32_t tx;        ///< Transmission (descriptor index).
+  uint32_t word0;     ///< First codeword word of the chunk.
+  uint32_t re_begin;  ///< First RE whose bits start in the chunk.
+  uint32_t re_end;    ///< One past the last.
+};
+
+/// Codeword words per modulator chunk and the largest codeword the Gold-sequence tables cover.
+constexpr uint32_t MOD_CHUNK_WORDS = 256;
+constexpr uint32_t MOD_MAX_BITS    = 1u << 21;
+/// Gold sequence tables (TS 38.211 section 5.2.1): x1 bits x1(1600 + n) as LSB-first words; x2 chunk jumps
+/// M^(1600 + 2048 c) (c < MOD_MAX_BITS / 2048, 31 column words each); x2 lane jumps M^(32 i) (i < 64) as [column][i].
+constexpr uint32_t GOLD_NC           = 1600;
+constexpr uint32_t GOLD_X1_WORDS     = MOD_MAX_BITS / 32;
+constexpr uint32_t GOLD_X2_JUMPS     = MOD_MAX_BITS / 2048;
+
+void launch_pdsch_modulate(const mod_desc*  d_desc,
+                           const mod_chunk* d_chunks,
+                           int              nof_chunks,
+                           const uint32_t*  d_codewords,
+                           uint32_t*        d_grids,
+                           const uint32_t*  d_x1,
+                           const uint32_t*  d_x2_jump,
+                           const uint32_t*  d_x2_lane,
+                           hipStream_t      stream);
+
 } // namespace srsgpu

@@ -125,6 +125,36 @@ class PuschTbConfig(ctypes.Structure):
 
 
 assert ctypes.sizeof(PuschTbConfig) == 40
+
+
+class PdschModConfig(ctypes.Structure):
+    """srsgpu_pdsch_mod_config (include/srsgpu_phy.h): one PDSCH transmission of pdsch_modulator::config_t."""
+    _fields_ = [
+        ("rnti", ctypes.c_uint16),
+        ("n_id", ctypes.c_uint16),
+        ("modulation_order", ctypes.c_uint8),
+        ("nof_layers", ctypes.c_uint8),
+        ("nof_ports", ctypes.c_uint8),
+        ("start_symbol", ctypes.c_uint8),
+        ("nof_symbols", ctypes.c_uint8),
+        ("dmrs_type", ctypes.c_uint8),
+        ("nof_cdm_groups_without_data", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8),
+        ("dmrs_symbol_mask", ctypes.c_uint16),
+        ("bwp_start_rb", ctypes.c_uint16),
+        ("bwp_size_rb", ctypes.c_uint16),
+        ("rb_start", ctypes.c_uint16),
+        ("nof_rb", ctypes.c_uint16),
+        ("pad", ctypes.c_uint16),
+        ("scaling", ctypes.c_float),
+        ("precoding", ctypes.c_float * 32),
+        ("cw_offset", ctypes.c_uint32),
+        ("nof_bits", ctypes.c_uint32),
+        ("grid_index", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(PdschModConfig) == 168
 CB_MSG_STRIDE = 1056
 
 _lib = None
@@ -167,6 +197,11 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pusch_decoder_plan_execute.argtypes = [P, P, P, P, P, P, P, P, P]
     lib.srsgpu_pusch_decoder_plan_destroy.argtypes = [P]
     lib.srsgpu_pusch_decoder_plan_destroy.restype = None
+    lib.srsgpu_pdsch_modulator_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                       ctypes.POINTER(P)]
+    lib.srsgpu_pdsch_modulator_plan_execute.argtypes = [P, P, P, P]
+    lib.srsgpu_pdsch_modulator_plan_destroy.argtypes = [P]
+    lib.srsgpu_pdsch_modulator_plan_destroy.restype = None
     for name in ("srsgpu_pusch_decoder_plan", "srsgpu_pdsch_encoder_plan"):
         getattr(lib, name + "_enable_timing").argtypes = [P, ctypes.c_int]
         getattr(lib, name + "_stage_times").argtypes = [P, P, ctypes.POINTER(ctypes.c_uint32)]
@@ -185,7 +220,8 @@ EXPORTED_SYMBOLS = [
     "srsgpu_pusch_decoder_plan_execute",
     "srsgpu_pusch_decoder_plan_destroy", "srsgpu_pusch_decoder_plan_enable_timing",
     "srsgpu_pusch_decoder_plan_stage_times", "srsgpu_pdsch_encoder_plan_enable_timing",
-    "srsgpu_pdsch_encoder_plan_stage_times",
+    "srsgpu_pdsch_encoder_plan_stage_times", "srsgpu_pdsch_modulator_plan_create",
+    "srsgpu_pdsch_modulator_plan_execute", "srsgpu_pdsch_modulator_plan_destroy",
 ]
 
 
@@ -544,6 +580,118 @@ class PdschEncoder:
 
     def encode(self, tb: np.ndarray, cfg: PdschTransportBlock) -> np.ndarray:
         return self.encode_batch([tb], [cfg])[0]
+
+
+@dataclass
+class PdschModulation:
+    """pdsch_modulator::config_t (pdsch_modulator.h:38) of one transmission, contiguous non-interleaved VRB allocation
+    and wideband precoding `weights` (nof_ports x nof_layers complex)."""
+    rnti: int
+    n_id: int
+    modulation_order: int
+    nof_layers: int
+    nof_ports: int
+    bwp_start_rb: int
+    bwp_size_rb: int
+    rb_start: int
+    nof_rb: int
+    start_symbol: int
+    nof_symbols: int
+    dmrs_symbol_mask: int
+    dmrs_type: int
+    nof_cdm_groups_without_data: int
+    scaling: float
+    weights: np.ndarray
+
+    def nof_re(self) -> int:
+        dm = (4 if self.dmrs_type == 2 else 6) * self.nof_cdm_groups_without_data
+        return sum((12 - dm if (self.dmrs_symbol_mask >> l) & 1 else 12) * self.nof_rb
+                   for l in range(self.start_symbol, self.start_symbol + self.nof_symbols))
+
+
+def make_pdsch_mod_configs(mods: Sequence[PdschModulation], cw_offsets: Sequence[int], grid_index: Sequence[int]):
+    arr = (PdschModConfig * len(mods))()
+    for i, (m, off, g) in enumerate(zip(mods, cw_offsets, grid_index)):
+        a = arr[i]
+        a.rnti, a.n_id, a.modulation_order, a.nof_layers, a.nof_ports = (m.rnti, m.n_id, m.modulation_order,
+                                                                         m.nof_layers, m.nof_ports)
+        a.start_symbol, a.nof_symbols, a.dmrs_type = m.start_symbol, m.nof_symbols, m.dmrs_type
+        a.nof_cdm_groups_without_data, a.dmrs_symbol_mask = m.nof_cdm_groups_without_data, m.dmrs_symbol_mask
+        a.bwp_start_rb, a.bwp_size_rb, a.rb_start, a.nof_rb = m.bwp_start_rb, m.bwp_size_rb, m.rb_start, m.nof_rb
+        a.scaling = m.scaling
+        w = np.zeros((4, 4, 2), np.float32)
+        wc = np.asarray(m.weights, np.complex64).reshape(m.nof_ports, m.nof_layers)
+        w[:m.nof_ports, :m.nof_layers, 0] = wc.real
+        w[:m.nof_ports, :m.nof_layers, 1] = wc.imag
+        a.precoding[:] = w.reshape(-1).tolist()
+        a.cw_offset, a.nof_bits, a.grid_index = off, m.nof_re() * m.nof_layers * m.modulation_order, g
+    return arr
+
+
+class PdschModulatorPlan:
+    """srsgpu_pdsch_modulator_plan: scrambling, modulation, layer mapping, precoding and RE mapping of a batch of
+    PDSCH transmissions into bf16 resource grids (grid_nof_ports x 14 x 12 * grid_nof_prb, uint32 re | im << 16)."""
+
+    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        _check(_lib.srsgpu_pdsch_modulator_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                       len(cfg_array), grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
+        self.handle = h
+        self.grid_nof_prb, self.grid_nof_ports = grid_nof_prb, grid_nof_ports
+
+    def grid_elements(self) -> int:
+        return self.grid_nof_ports * 14 * 12 * self.grid_nof_prb
+
+    def execute(self, d_codewords, d_grids, stream=None):
+        _check(_lib.srsgpu_pdsch_modulator_plan_execute(self.handle, _dptr(d_codewords), _dptr(d_grids),
+                                                        _stream_handle(stream)))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.srsgpu_pdsch_modulator_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class PdschModulator:
+    """GPU counterpart of srsran::pdsch_modulator::modulate(grid, codewords, config) (pdsch_modulator_impl.cpp:107):
+    modulate() takes the packed codeword and returns the grid as uint16 bf16 bit patterns (ports, 14, nsc, 2), written
+    over `grid` (or zeros) at the PDSCH REs only."""
+
+    def __init__(self, ctx: Context, grid_nof_prb: int, grid_nof_ports: int = 4):
+        self.ctx, self.grid_nof_prb, self.grid_nof_ports = ctx, grid_nof_prb, grid_nof_ports
+
+    def modulate_batch(self, codewords: Sequence[np.ndarray], mods: Sequence[PdschModulation], grid_index=None,
+                       grids: np.ndarray = None):
+        dev = torch.device("cuda", self.ctx.device)
+        offs, buf, o = [], [], 0
+        for cw in codewords:
+            b = np.asarray(cw, np.uint8)
+            pad = (-b.size) % 4
+            buf.append(np.concatenate([b, np.zeros(pad, np.uint8)]))
+            offs.append(o)
+            o += b.size + pad
+        grid_index = list(range(len(mods))) if grid_index is None else list(grid_index)
+        ngrids = max(grid_index) + 1 if grid_index else 1
+        arr = make_pdsch_mod_configs(mods, offs, grid_index)
+        plan = PdschModulatorPlan(self.ctx, arr, self.grid_nof_prb, self.grid_nof_ports)
+        shape = (ngrids, self.grid_nof_ports, 14, 12 * self.grid_nof_prb, 2)
+        g0 = np.zeros(shape, np.uint16) if grids is None else np.ascontiguousarray(grids, np.uint16).reshape(shape)
+        d_grid = torch.from_numpy(g0.view(np.uint32).reshape(-1).view(np.int32)).to(dev)
+        d_cw = torch.from_numpy(np.concatenate(buf) if buf else np.zeros(4, np.uint8)).to(dev)
+        plan.execute(d_cw, d_grid)
+        torch.cuda.synchronize(dev)
+        plan.close()
+        return d_grid.cpu().numpy().view(np.uint16).reshape(shape)
+
+    def modulate(self, codeword: np.ndarray, mod: PdschModulation, grid: np.ndarray = None) -> np.ndarray:
+        return self.modulate_batch([codeword], [mod], grids=None if grid is None else grid[None])[0]
 
 
 @dataclass

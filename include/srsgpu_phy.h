@@ -256,6 +256,69 @@ int srsgpu_pdsch_modulator_plan_execute(const srsgpu_pdsch_modulator_plan* plan,
 void srsgpu_pdsch_modulator_plan_destroy(srsgpu_pdsch_modulator_plan* plan);
 
 /* ------------------------------------------------------------------------------------------------------------------
+ * OFDM slot modulator / demodulator — replace srsran::ofdm_slot_modulator::modulate(span<cf_t> output,
+ * const resource_grid_reader& grid, unsigned port_index, unsigned slot_index)
+ * (include/srsran/phy/lower/modulation/ofdm_modulator.h:100, lib/phy/lower/modulation/ofdm_modulator_impl.cpp:115,
+ * per symbol :56) and ofdm_slot_demodulator::demodulate(resource_grid_writer& grid, span<const cf_t> input,
+ * unsigned port_index, unsigned slot_index) (ofdm_demodulator.h:102, ofdm_demodulator_impl.cpp:154, per symbol :94),
+ * batched over every (grid, port, symbol) of a set of slots.
+ * Modulator, per symbol: grid subcarriers [0, rg/2) -> DFT bins [N - rg/2, N), [rg/2, rg) -> bins [0, rg/2), inverse
+ * DFT (unnormalised), times the TS 38.211 section 5.4 phase compensation (phase_compensation_lut.h) and `scale`, CP =
+ * copy of the last cp_len samples. Demodulator: N samples from cp_len - window_offset, direct DFT, the same
+ * compensation (receive sign) and the DFT-window phase ramp, bins back to the grid as bf16.
+ * Grids: nof_ports x nsymb (14, or 12 with extended CP) x 12 * bw_rb uint32 (re | im << 16, bf16), grid g at
+ * g * nof_ports * nsymb * 12 * bw_rb. Time samples: complex float (re, im) interleaved, one slot of (grid g, port p)
+ * at srsgpu_ofdm_plan_sample_offset(plan, g, p) (grids, then ports, consecutively).
+ * ------------------------------------------------------------------------------------------------------------------ */
+typedef struct {
+  uint32_t numerology;                /* subcarrier spacing 15 kHz x 2^numerology, 0..4 */
+  uint32_t bw_rb;                     /* resource grid bandwidth in RB: 12 * bw_rb < dft_size */
+  uint32_t dft_size;                  /* power of two, 256..8192 */
+  uint32_t cp_extended;               /* 0: normal cyclic prefix (14 symbols), 1: extended (12 symbols) */
+  uint32_t nof_samples_window_offset; /* demodulator DFT window advance, < 144 * dft_size / 2048 (0: none) */
+  float    scale;                     /* scaling factor at the DFT output (std::isnormal) */
+  double   center_freq_hz;            /* carrier centre frequency for the phase compensation */
+} srsgpu_ofdm_config;
+
+typedef struct srsgpu_ofdm_plan srsgpu_ofdm_plan;
+
+/** Plans the modulation of nof_grids slots (grid g is slot slot_index[g] within its subframe) of nof_ports ports. */
+int srsgpu_ofdm_modulator_plan_create(srsgpu_context*           ctx,
+                                      const srsgpu_ofdm_config* cfg,
+                                      uint32_t                  nof_grids,
+                                      uint32_t                  nof_ports,
+                                      const uint32_t*           slot_index,
+                                      srsgpu_ofdm_plan**        plan);
+
+/** Plans the demodulation of nof_grids slots of nof_ports ports (same layouts). */
+int srsgpu_ofdm_demodulator_plan_create(srsgpu_context*           ctx,
+                                        const srsgpu_ofdm_config* cfg,
+                                        uint32_t                  nof_grids,
+                                        uint32_t                  nof_ports,
+                                        const uint32_t*           slot_index,
+                                        srsgpu_ofdm_plan**        plan);
+
+/** Total number of complex samples of the plan's time buffer (all grids and ports). */
+uint64_t srsgpu_ofdm_plan_nof_samples(const srsgpu_ofdm_plan* plan);
+
+/** First complex sample of (grid, port) in the time buffer. */
+uint64_t srsgpu_ofdm_plan_sample_offset(const srsgpu_ofdm_plan* plan, uint32_t grid, uint32_t port);
+
+/** Modulates d_grids into d_samples. Asynchronous on `stream`, hipGraph-capturable. */
+int srsgpu_ofdm_modulator_plan_execute(const srsgpu_ofdm_plan* plan,
+                                       const uint32_t*         d_grids,
+                                       float*                  d_samples,
+                                       void*                   stream);
+
+/** Demodulates d_samples into d_grids (every subcarrier of every symbol is written). Asynchronous. */
+int srsgpu_ofdm_demodulator_plan_execute(const srsgpu_ofdm_plan* plan,
+                                         const float*            d_samples,
+                                         uint32_t*               d_grids,
+                                         void*                   stream);
+
+void srsgpu_ofdm_plan_destroy(srsgpu_ofdm_plan* plan);
+
+/* ------------------------------------------------------------------------------------------------------------------
  * PUSCH decoder (transport-block level) — replaces srsran::pusch_decoder (include/srsran/phy/upper/channel_processors/
  * pusch/pusch_decoder.h; lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.cpp: new_data :98, segmentation
  * :190, codeblock tasks :283, join_and_notify :386): segmentation, per-codeblock rate dematching + HARQ combining +

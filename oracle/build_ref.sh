@@ -52,6 +52,11 @@ SRCS=(
   "$REF/lib/phy/upper/rb_allocation.cpp:-mavx2"
   "$REF/lib/ran/resource_allocation/vrb_to_prb.cpp:-mavx2"
   "$HERE/ref/ref_pdsch_mod.cpp:-mavx2 -I$REF"
+  "$REF/lib/phy/lower/modulation/ofdm_modulator_impl.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/lower/modulation/ofdm_demodulator_impl.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/generic_functions/dft_processor_generic_impl.cpp:-mavx2 -mfma"
+  "$REF/lib/srsvec/prod.cpp:-mavx2 -mfma"
+  "$HERE/ref/ref_ofdm.cpp:-mavx2 -mfma -I$REF"
 )
 OBJS=()
 pids=()

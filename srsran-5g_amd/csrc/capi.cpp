@@ -352,7 +352,9 @@ void srsgpu_context_destroy(srsgpu_context* ctx)
       (void)hipFree(p);
     }
   }
-  for (uint32_t* p : {ctx->d_crc_arena, ctx->d_gold_x1, ctx->d_gold_x2_jump, ctx->d_gold_x2_lane}) {
+  for (void* p : {static_cast<void*>(ctx->d_crc_arena), static_cast<void*>(ctx->d_gold_x1),
+                  static_cast<void*>(ctx->d_gold_x2_jump), static_cast<void*>(ctx->d_gold_x2_lane),
+                  static_cast<void*>(ctx->d_ofdm_twiddles)}) {
     if (p != nullptr) {
       (void)hipFree(p);
     }

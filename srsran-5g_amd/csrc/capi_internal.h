@@ -57,6 +57,8 @@ struct srsgpu_context {
   uint32_t*                            d_gold_x1      = nullptr;
   uint32_t*                            d_gold_x2_jump = nullptr;
   uint32_t*                            d_gold_x2_lane = nullptr;
+  /// OFDM DFT twiddles exp(-j 2 pi m / OFDM_MAX_DFT) as (re, im) floats (built on first use).
+  float*                               d_ofdm_twiddles = nullptr;
   std::mutex                           mtx;
 };
 

@@ -1,0 +1,246 @@
+// Host side of the OFDM modulator / demodulator C ABI (include/srsgpu_phy.h): configuration checks with the
+// reference's conditions (ofdm_modulator_impl.cpp:41-:44, ofdm_demodulator_impl.cpp:53-:68), cyclic-prefix lengths,
+// the TS 38.211 section 5.4 phase-compensation coefficients (computed in double like phase_compensation_lut.h:50) and
+// one job per (grid, port, symbol).
+#include "capi_internal.h"
+#include <cmath>
+#include <complex>
+#include <vector>
+
+using namespace srsgpu;
+
+struct srsgpu_ofdm_plan {
+  srsgpu_context*       ctx        = nullptr;
+  bool                  inverse    = true;  ///< Modulator (inverse DFT) or demodulator.
+  uint32_t              log2_dft   = 0;
+  uint32_t              nsc        = 0;
+  uint32_t              window_off = 0;
+  uint32_t              nof_ports  = 0;
+  ofdm_job*             d_jobs     = nullptr;
+  int                   nof_jobs   = 0;
+  std::vector<uint64_t> offsets;  ///< Sample offset of (grid, port); one extra entry = total.
+};
+
+namespace {
+
+/// Cyclic prefix of symbol `symbol` of the subframe in samples (cyclic_prefix.h:93: kappa units (144 >> mu), +16 for
+/// symbols 0 and 7 * 2^mu, extended 512 >> mu; one kappa unit is 2^mu * N / 2048 samples at N * scs).
+uint32_t cp_samples(uint32_t mu, uint32_t N, bool extended, uint32_t symbol)
+{
+  uint32_t units;
+  if (extended) {
+    units = 512u >> mu;
+  } else {
+    units = 144u >> mu;
+    if (symbol == 0 || symbol == 7u * (1u << mu)) {
+      units += 16;
+    }
+  }
+  return static_cast<uint32_t>((static_cast<uint64_t>(units) << mu) * N / 2048u);
+}
+
+int ensure_twiddles(srsgpu_context* ctx)
+{
+  if (ctx->d_ofdm_twiddles != nullptr) {
+    return SRSGPU_OK;
+  }
+  std::vector<float> tw(2 * OFDM_MAX_DFT);
+  for (uint32_t m = 0; m < OFDM_MAX_DFT; ++m) {
+    const double a = -2.0 * M_PI * static_cast<double>(m) / static_cast<double>(OFDM_MAX_DFT);
+    tw[2 * m]      = static_cast<float>(std::cos(a));
+    tw[2 * m + 1]  = static_cast<float>(std::sin(a));
+  }
+  float* d = nullptr;
+  if (hipMalloc(&d, tw.size() * sizeof(float)) != hipSuccess ||
+      hipMemcpy(d, tw.data(), tw.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+    if (d != nullptr) {
+      (void)hipFree(d);
+    }
+    return fail(SRSGPU_ERR_HIP, "failed to upload the DFT twiddle table");
+  }
+  ctx->d_ofdm_twiddles = d;
+  return SRSGPU_OK;
+}
+
+int plan_create(srsgpu_context*           ctx,
+                bool                      inverse,
+                const srsgpu_ofdm_config* cfg,
+                uint32_t                  nof_grids,
+                uint32_t                  nof_ports,
+                const uint32_t*           slot_index,
+                srsgpu_ofdm_plan**        plan_out)
+{
+  if (ctx == nullptr || cfg == nullptr || plan_out == nullptr || (slot_index == nullptr && nof_grids > 0)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  const uint32_t N   = cfg->dft_size;
+  const uint32_t mu  = cfg->numerology;
+  const uint32_t nsc = 12u * cfg->bw_rb;
+  uint32_t       log2n = 0;
+  while ((1u << log2n) < N) {
+    ++log2n;
+  }
+  if ((1u << log2n) != N || log2n < 8 || log2n > 13) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "DFT size %u not supported (powers of two 256..8192)", N);
+  }
+  if (mu > 4 || cfg->bw_rb == 0 || nsc >= N) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "the DFT size (%u) must be greater than the resource grid size (%u)", N, nsc);
+  }
+  if (!std::isnormal(cfg->scale)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "invalid scaling factor %g", static_cast<double>(cfg->scale));
+  }
+  const uint32_t woff = inverse ? 0u : cfg->nof_samples_window_offset;
+  if (woff != 0 && woff >= 144u * N / 2048u) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "the DFT window offset (%u) must be lower than %u", woff, 144u * N / 2048u);
+  }
+  if (nof_ports == 0) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "no ports");
+  }
+  const bool     ext   = cfg->cp_extended != 0;
+  const uint32_t nsymb = ext ? 12u : 14u;
+  const uint32_t nslot = 1u << mu;  // slots per subframe
+  // Phase compensation per symbol of the subframe (phase_compensation_lut.h:50), times the scale, in float.
+  const double              srate = 15e3 * static_cast<double>(1u << mu) * N;
+  std::vector<std::complex<float>> coef(nsymb * nslot);
+  {
+    const double sign_two_pi = (inverse ? -1.0 : 1.0) * 2.0 * M_PI;
+    uint64_t     offset      = 0;
+    for (uint32_t s = 0; s < nsymb * nslot; ++s) {
+      offset += cp_samples(mu, N, ext, s);
+      const double              t  = static_cast<double>(offset) / srate;
+      const std::complex<float> ph = static_cast<std::complex<float>>(std::polar(1.0, sign_two_pi * cfg->center_freq_hz * t));
+      coef[s]                      = ph * cfg->scale;
+      offset += N;
+    }
+  }
+  std::lock_guard<std::mutex> lock(ctx->mtx);
+  HIP_TRY(hipSetDevice(ctx->device));
+  int r = ensure_twiddles(ctx);
+  if (r != SRSGPU_OK) {
+    return r;
+  }
+  auto* plan       = new srsgpu_ofdm_plan();
+  plan->ctx        = ctx;
+  plan->inverse    = inverse;
+  plan->log2_dft   = log2n;
+  plan->nsc        = nsc;
+  plan->window_off = woff;
+  plan->nof_ports  = nof_ports;
+  std::vector<ofdm_job> jobs;
+  uint64_t              pos = 0;
+  for (uint32_t g = 0; g < nof_grids; ++g) {
+    if (slot_index[g] >= nslot) {
+      delete plan;
+      return fail(SRSGPU_ERR_INVALID_ARG, "grid %u: slot index %u exceeds the %u slots per subframe", g, slot_index[g],
+                  nslot);
+    }
+    for (uint32_t p = 0; p < nof_ports; ++p) {
+      plan->offsets.push_back(pos);
+      for (uint32_t l = 0; l < nsymb; ++l) {
+        const uint32_t s   = nsymb * slot_index[g] + l;
+        const uint32_t cp  = cp_samples(mu, N, ext, s);
+        ofdm_job       jb{};
+        jb.grid_offset     = ((g * nof_ports + p) * nsymb + l) * nsc;
+        jb.sample_offset   = static_cast<uint32_t>(pos);
+        jb.cp_len          = cp;
+        jb.coef_re         = coef[s].real();
+        jb.coef_im         = coef[s].imag();
+        jobs.push_back(jb);
+        pos += cp + N;
+      }
+    }
+  }
+  plan->offsets.push_back(pos);
+  if (pos >= (1ull << 32) || static_cast<uint64_t>(nof_grids) * nof_ports * nsymb * nsc >= (1ull << 32)) {
+    delete plan;
+    return fail(SRSGPU_ERR_INVALID_ARG, "batch too large for 32-bit offsets");
+  }
+  plan->nof_jobs = static_cast<int>(jobs.size());
+  if (!jobs.empty() && (hipMalloc(&plan->d_jobs, jobs.size() * sizeof(ofdm_job)) != hipSuccess ||
+                        hipMemcpy(plan->d_jobs, jobs.data(), jobs.size() * sizeof(ofdm_job), hipMemcpyHostToDevice) !=
+                            hipSuccess)) {
+    srsgpu_ofdm_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload OFDM jobs");
+  }
+  *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int srsgpu_ofdm_modulator_plan_create(srsgpu_context*           ctx,
+                                      const srsgpu_ofdm_config* cfg,
+                                      uint32_t                  nof_grids,
+                                      uint32_t                  nof_ports,
+                                      const uint32_t*           slot_index,
+                                      srsgpu_ofdm_plan**        plan)
+{
+  return plan_create(ctx, true, cfg, nof_grids, nof_ports, slot_index, plan);
+}
+
+int srsgpu_ofdm_demodulator_plan_create(srsgpu_context*           ctx,
+                                        const srsgpu_ofdm_config* cfg,
+                                        uint32_t                  nof_grids,
+                                        uint32_t                  nof_ports,
+                                        const uint32_t*           slot_index,
+                                        srsgpu_ofdm_plan**        plan)
+{
+  return plan_create(ctx, false, cfg, nof_grids, nof_ports, slot_index, plan);
+}
+
+uint64_t srsgpu_ofdm_plan_nof_samples(const srsgpu_ofdm_plan* plan)
+{
+  return (plan == nullptr || plan->offsets.empty()) ? 0 : plan->offsets.back();
+}
+
+uint64_t srsgpu_ofdm_plan_sample_offset(const srsgpu_ofdm_plan* plan, uint32_t grid, uint32_t port)
+{
+  if (plan == nullptr || port >= plan->nof_ports) {
+    return 0;
+  }
+  const size_t i = static_cast<size_t>(grid) * plan->nof_ports + port;
+  return i < plan->offsets.size() ? plan->offsets[i] : 0;
+}
+
+int srsgpu_ofdm_modulator_plan_execute(const srsgpu_ofdm_plan* plan,
+                                       const uint32_t*         d_grids,
+                                       float*                  d_samples,
+                                       void*                   stream)
+{
+  if (plan == nullptr || d_grids == nullptr || d_samples == nullptr || !plan->inverse) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument or not a modulator plan");
+  }
+  launch_ofdm(true, plan->log2_dft, plan->d_jobs, plan->nof_jobs, plan->nsc, 0, plan->ctx->d_ofdm_twiddles, d_grids,
+              nullptr, nullptr, d_samples, static_cast<hipStream_t>(stream));
+  HIP_TRY(hipGetLastError());
+  return SRSGPU_OK;
+}
+
+int srsgpu_ofdm_demodulator_plan_execute(const srsgpu_ofdm_plan* plan,
+                                         const float*            d_samples,
+                                         uint32_t*               d_grids,
+                                         void*                   stream)
+{
+  if (plan == nullptr || d_grids == nullptr || d_samples == nullptr || plan->inverse) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument or not a demodulator plan");
+  }
+  launch_ofdm(false, plan->log2_dft, plan->d_jobs, plan->nof_jobs, plan->nsc, plan->window_off,
+              plan->ctx->d_ofdm_twiddles, nullptr, d_grids, d_samples, nullptr, static_cast<hipStream_t>(stream));
+  HIP_TRY(hipGetLastError());
+  return SRSGPU_OK;
+}
+
+void srsgpu_ofdm_plan_destroy(srsgpu_ofdm_plan* plan)
+{
+  if (plan == nullptr) {
+    return;
+  }
+  if (plan->d_jobs != nullptr) {
+    (void)hipFree(plan->d_jobs);
+  }
+  delete plan;
+}
+
+} // extern "C"

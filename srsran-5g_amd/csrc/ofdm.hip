@@ -1,0 +1,284 @@
+// OFDM slot modulator / demodulator on gfx950: one workgroup per (grid, port, OFDM symbol), a Stockham
+// (self-sorting) radix-16 DFT in LDS with the subcarrier mapping, phase compensation, scaling, cyclic prefix and
+// bf16 conversion fused into its first and last passes.
+//
+// Reference (behaviour, not code): lib/phy/lower/modulation/ofdm_modulator_impl.cpp:56 (symbol modulator),
+// ofdm_demodulator_impl.cpp:94 (symbol demodulator), phase_compensation_lut.h:50, the unnormalised DFT of
+// lib/phy/generic_functions/dft_processor_generic_impl.cpp (sign -1 direct, +1 inverse).
+//
+// Decomposition for N = 2^n: a first pass of radix 2^(n mod 4) (or 16), then radix-16 passes. N / 16 threads (a
+// partial wave below N = 1024), each
+// holding 16 complex values in registers per pass: a pass reads its butterfly inputs (from HBM in the first pass:
+// the grid's subcarriers or the symbol's time samples, coalesced), barriers, twiddles them (exp(-+2 pi i m / N) from
+// a 8192-entry table computed in double on the host), runs the in-register radix-R DFT and writes the outputs to LDS —
+// or, in the last pass, straight to HBM with the compensation applied: time samples (and the cyclic-prefix copy) or
+// bf16 subcarriers. HBM traffic per symbol: the grid row (4 B per subcarrier) and N + CP complex float samples (8 B),
+// each touched once.
+#include "srsgpu_internal.h"
+
+namespace srsgpu {
+namespace {
+
+// cos / sin (2 pi k / 16).
+__device__ constexpr float kCos16[16] = {1.0f,          0.92387953251f,  0.70710678118f,  0.38268343236f,
+                                         0.0f,          -0.38268343236f, -0.70710678118f, -0.92387953251f,
+                                         -1.0f,         -0.92387953251f, -0.70710678118f, -0.38268343236f,
+                                         0.0f,          0.38268343236f,  0.70710678118f,  0.92387953251f};
+__device__ constexpr float kSin16[16] = {0.0f,  0.38268343236f,  0.70710678118f,  0.92387953251f,
+                                         1.0f,  0.92387953251f,  0.70710678118f,  0.38268343236f,
+                                         0.0f,  -0.38268343236f, -0.70710678118f, -0.92387953251f,
+                                         -1.0f, -0.92387953251f, -0.70710678118f, -0.38268343236f};
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b)
+{
+  return make_float2(a.x + b.x, a.y + b.y);
+}
+__device__ __forceinline__ float2 csub(float2 a, float2 b)
+{
+  return make_float2(a.x - b.x, a.y - b.y);
+}
+__device__ __forceinline__ float2 cmul(float2 a, float2 b)
+{
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+/// In-register DFT of size R (decimation in time, natural order in and out), exponent sign S.
+template <int R, int S>
+__device__ __forceinline__ void dft_reg(float2* v)
+{
+  if constexpr (R == 2) {
+    const float2 a = v[0], b = v[1];
+    v[0]           = cadd(a, b);
+    v[1]           = csub(a, b);
+  } else if constexpr (R > 2) {
+    float2 e[R / 2], o[R / 2];
+#pragma unroll
+    for (int i = 0; i < R / 2; ++i) {
+      e[i] = v[2 * i];
+      o[i] = v[2 * i + 1];
+    }
+    dft_reg<R / 2, S>(e);
+    dft_reg<R / 2, S>(o);
+#pragma unroll
+    for (int k = 0; k < R / 2; ++k) {
+      float2 t;
+      if (k == 0) {
+        t = o[0];
+      } else if (4 * k == R) {  // times S * i
+        t = (S > 0) ? make_float2(-o[k].y, o[k].x) : make_float2(o[k].y, -o[k].x);
+      } else {
+        const int m = k * (16 / R);
+        t           = cmul(o[k], make_float2(kCos16[m], S * kSin16[m]));
+      }
+      v[k]         = cadd(e[k], t);
+      v[k + R / 2] = csub(e[k], t);
+    }
+  }
+}
+
+/// One Stockham pass of radix R over N points (NS = product of the previous passes' radices): butterfly j takes
+/// x[j + r N / R], twiddles by W^(r k), k = j mod NS, and writes X[(j - k) R + k + r NS].
+template <int N, int R, int NS, int S, typename Src, typename Dst>
+__device__ __forceinline__ void stockham_pass(const float2* __restrict__ tw, Src src, Dst dst)
+{
+  constexpr int T = N / 16;
+  constexpr int B = 16 / R;
+  float2        v[B][R];
+  const int     tid = static_cast<int>(threadIdx.x);
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const int j = tid + b * T;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      v[b][r] = src(j + r * (N / R));
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const int j = tid + b * T;
+    const int k = j & (NS - 1);
+    if constexpr (NS > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        // W = exp(S 2 pi i r k / (NS R)); the table holds exp(-2 pi i m / OFDM_MAX_DFT).
+        float2 w = tw[(r * k) * static_cast<int>(OFDM_MAX_DFT / (NS * R))];
+        if constexpr (S > 0) {
+          w.y = -w.y;
+        }
+        v[b][r] = cmul(v[b][r], w);
+      }
+    }
+    dft_reg<R, S>(v[b]);
+    const int base = (j - k) * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      dst(base + r * NS, v[b][r]);
+    }
+  }
+  __syncthreads();
+}
+
+template <int LOG2N, int S, typename Src, typename Dst>
+__device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
+{
+  constexpr int N    = 1 << LOG2N;
+  constexpr int REM  = LOG2N % 4;
+  constexpr int R0   = REM ? (1 << REM) : 16;
+  constexpr int NP   = LOG2N / 4 + (REM ? 1 : 0);
+  auto          ld   = [lds](int i) { return lds[i]; };
+  auto          st   = [lds](int i, float2 v) { lds[i] = v; };
+  static_assert(NP >= 2 && NP <= 4, "supported DFT sizes: 256..8192");
+  stockham_pass<N, R0, 1, S>(tw, src_first, st);
+  if constexpr (NP == 2) {
+    stockham_pass<N, 16, R0, S>(tw, ld, dst_last);
+  } else if constexpr (NP == 3) {
+    stockham_pass<N, 16, R0, S>(tw, ld, st);
+    stockham_pass<N, 16, R0 * 16, S>(tw, ld, dst_last);
+  } else {
+    stockham_pass<N, 16, R0, S>(tw, ld, st);
+    stockham_pass<N, 16, R0 * 16, S>(tw, ld, st);
+    stockham_pass<N, 16, R0 * 256, S>(tw, ld, dst_last);
+  }
+}
+
+__device__ __forceinline__ uint32_t bf16_bits(float v)
+{
+  const uint32_t u = __float_as_uint(v);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+template <int LOG2N>
+__global__ __launch_bounds__((1 << LOG2N) / 16) void ofdm_modulate_kernel(
+    const ofdm_job* __restrict__ jobs,
+    uint32_t nsc,
+    const float2* __restrict__ tw,
+    const uint32_t* __restrict__ grid,
+    float2* __restrict__ out)
+{
+  constexpr int       N = 1 << LOG2N;
+  __shared__ float2   lds[N];
+  const ofdm_job      jb   = jobs[blockIdx.x];
+  const int           half = static_cast<int>(nsc / 2);
+  const uint32_t*     row  = grid + jb.grid_offset;
+  // Bin b < rg/2 carries subcarrier rg/2 + b, bin b >= N - rg/2 subcarrier b - (N - rg/2), the rest are zero.
+  auto src = [row, half](int b) {
+    int sc = -1;
+    if (b < half) {
+      sc = half + b;
+    } else if (b >= N - half) {
+      sc = b - (N - half);
+    }
+    if (sc < 0) {
+      return make_float2(0.f, 0.f);
+    }
+    const uint32_t u = row[sc];
+    return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+  };
+  const float2 coef = make_float2(jb.coef_re, jb.coef_im);
+  float2*      sym  = out + jb.sample_offset;
+  const int    cp   = static_cast<int>(jb.cp_len);
+  auto dst = [sym, coef, cp](int n, float2 v) {
+    const float2 y = cmul(v, coef);
+    sym[cp + n]    = y;
+    if (n >= N - cp) {
+      sym[n - (N - cp)] = y;
+    }
+  };
+  dft_lds<LOG2N, +1>(lds, tw, src, dst);
+}
+
+template <int LOG2N>
+__global__ __launch_bounds__((1 << LOG2N) / 16) void ofdm_demodulate_kernel(
+    const ofdm_job* __restrict__ jobs,
+    uint32_t nsc,
+    uint32_t window_offset,
+    const float2* __restrict__ tw,
+    const float2* __restrict__ in,
+    uint32_t* __restrict__ grid)
+{
+  constexpr int     N = 1 << LOG2N;
+  __shared__ float2 lds[N];
+  const ofdm_job    jb   = jobs[blockIdx.x];
+  const int         half = static_cast<int>(nsc / 2);
+  const float2*     x    = in + jb.sample_offset + jb.cp_len - window_offset;
+  auto              src  = [x](int n) { return x[n]; };
+  const float2      coef = make_float2(jb.coef_re, jb.coef_im);
+  uint32_t*         row  = grid + jb.grid_offset;
+  auto dst = [row, coef, half, tw, window_offset](int b, float2 v) {
+    int sc = -1;
+    if (b < half) {
+      sc = half + b;
+    } else if (b >= N - half) {
+      sc = b - (N - half);
+    }
+    if (sc < 0) {
+      return;
+    }
+    float2 y = cmul(v, coef);
+    if (window_offset != 0) {  // times exp(+j 2 pi offset b / N)
+      float2 w = tw[((window_offset * static_cast<uint32_t>(b)) & (N - 1)) * (OFDM_MAX_DFT / N)];
+      w.y      = -w.y;
+      y        = cmul(y, w);
+    }
+    row[sc] = bf16_bits(y.x) | (bf16_bits(y.y) << 16);
+  };
+  dft_lds<LOG2N, -1>(lds, tw, src, dst);
+}
+
+template <int LOG2N>
+void launch_one(bool            inverse,
+                const ofdm_job* jobs,
+                int             nof_jobs,
+                uint32_t        nsc,
+                uint32_t        window_offset,
+                const float2*   tw,
+                const uint32_t* grid_in,
+                uint32_t*       grid_out,
+                const float2*   samples_in,
+                float2*         samples_out,
+                hipStream_t     stream)
+{
+  constexpr int threads = (1 << LOG2N) / 16;  // every thread takes part in the passes' barriers
+  if (inverse) {
+    hipLaunchKernelGGL(ofdm_modulate_kernel<LOG2N>, dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0, stream,
+                       jobs, nsc, tw, grid_in, samples_out);
+  } else {
+    hipLaunchKernelGGL(ofdm_demodulate_kernel<LOG2N>, dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0,
+                       stream, jobs, nsc, window_offset, tw, samples_in, grid_out);
+  }
+}
+
+} // namespace
+
+void launch_ofdm(bool            inverse,
+                 uint32_t        log2_dft,
+                 const ofdm_job* d_jobs,
+                 int             nof_jobs,
+                 uint32_t        nsc,
+                 uint32_t        window_offset,
+                 const float*    d_twiddles,
+                 const uint32_t* d_grid_in,
+                 uint32_t*       d_grid_out,
+                 const float*    d_samples_in,
+                 float*          d_samples_out,
+                 hipStream_t     stream)
+{
+  if (nof_jobs <= 0) {
+    return;
+  }
+  const auto* tw  = reinterpret_cast<const float2*>(d_twiddles);
+  const auto* sin = reinterpret_cast<const float2*>(d_samples_in);
+  auto*       so  = reinterpret_cast<float2*>(d_samples_out);
+  switch (log2_dft) {
+    case 8: launch_one<8>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 9: launch_one<9>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 10: launch_one<10>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 11: launch_one<11>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 12: launch_one<12>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 13: launch_one<13>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    default: break;
+  }
+}
+
+} // namespace srsgpu

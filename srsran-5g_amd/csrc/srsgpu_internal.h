@@ -226,4 +226,30 @@ void launch_pdsch_modulate(const mod_desc*  d_desc,
                            const uint32_t*  d_x2_lane,
                            hipStream_t      stream);
 
+/// OFDM (de)modulator job: one OFDM symbol of one port of one grid (ofdm.hip).
+struct ofdm_job {
+  uint32_t grid_offset;    ///< Element of (grid, port, symbol, subcarrier 0).
+  uint32_t sample_offset;  ///< Complex sample where the symbol's cyclic prefix starts.
+  uint32_t cp_len;         ///< Cyclic prefix length in samples.
+  uint32_t pad;
+  float    coef_re;        ///< Phase compensation times scale.
+  float    coef_im;
+};
+
+/// Largest DFT size and the twiddle table exp(-j 2 pi m / OFDM_MAX_DFT), m < OFDM_MAX_DFT, every size strides through.
+constexpr uint32_t OFDM_MAX_DFT = 8192;
+
+void launch_ofdm(bool            inverse,
+                 uint32_t        log2_dft,
+                 const ofdm_job* d_jobs,
+                 int             nof_jobs,
+                 uint32_t        nsc,
+                 uint32_t        window_offset,
+                 const float*    d_twiddles,
+                 const uint32_t* d_grid_in,
+                 uint32_t*       d_grid_out,
+                 const float*    d_samples_in,
+                 float*          d_samples_out,
+                 hipStream_t     stream);
+
 } // namespace srsgpu

@@ -157,6 +157,22 @@ class PdschModConfig(ctypes.Structure):
 assert ctypes.sizeof(PdschModConfig) == 168
 CB_MSG_STRIDE = 1056
 
+
+class OfdmConfig(ctypes.Structure):
+    """srsgpu_ofdm_config (include/srsgpu_phy.h): ofdm_modulator_configuration / ofdm_demodulator_configuration."""
+    _fields_ = [
+        ("numerology", ctypes.c_uint32),
+        ("bw_rb", ctypes.c_uint32),
+        ("dft_size", ctypes.c_uint32),
+        ("cp_extended", ctypes.c_uint32),
+        ("nof_samples_window_offset", ctypes.c_uint32),
+        ("scale", ctypes.c_float),
+        ("center_freq_hz", ctypes.c_double),
+    ]
+
+
+assert ctypes.sizeof(OfdmConfig) == 32
+
 _lib = None
 
 
@@ -202,6 +218,16 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pdsch_modulator_plan_execute.argtypes = [P, P, P, P]
     lib.srsgpu_pdsch_modulator_plan_destroy.argtypes = [P]
     lib.srsgpu_pdsch_modulator_plan_destroy.restype = None
+    for name in ("srsgpu_ofdm_modulator_plan_create", "srsgpu_ofdm_demodulator_plan_create"):
+        getattr(lib, name).argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, P, ctypes.POINTER(P)]
+    lib.srsgpu_ofdm_plan_nof_samples.argtypes = [P]
+    lib.srsgpu_ofdm_plan_nof_samples.restype = ctypes.c_uint64
+    lib.srsgpu_ofdm_plan_sample_offset.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
+    lib.srsgpu_ofdm_plan_sample_offset.restype = ctypes.c_uint64
+    lib.srsgpu_ofdm_modulator_plan_execute.argtypes = [P, P, P, P]
+    lib.srsgpu_ofdm_demodulator_plan_execute.argtypes = [P, P, P, P]
+    lib.srsgpu_ofdm_plan_destroy.argtypes = [P]
+    lib.srsgpu_ofdm_plan_destroy.restype = None
     for name in ("srsgpu_pusch_decoder_plan", "srsgpu_pdsch_encoder_plan"):
         getattr(lib, name + "_enable_timing").argtypes = [P, ctypes.c_int]
         getattr(lib, name + "_stage_times").argtypes = [P, P, ctypes.POINTER(ctypes.c_uint32)]
@@ -222,6 +248,9 @@ EXPORTED_SYMBOLS = [
     "srsgpu_pusch_decoder_plan_stage_times", "srsgpu_pdsch_encoder_plan_enable_timing",
     "srsgpu_pdsch_encoder_plan_stage_times", "srsgpu_pdsch_modulator_plan_create",
     "srsgpu_pdsch_modulator_plan_execute", "srsgpu_pdsch_modulator_plan_destroy",
+    "srsgpu_ofdm_modulator_plan_create", "srsgpu_ofdm_demodulator_plan_create", "srsgpu_ofdm_plan_nof_samples",
+    "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
+    "srsgpu_ofdm_plan_destroy",
 ]
 
 
@@ -692,6 +721,90 @@ class PdschModulator:
 
     def modulate(self, codeword: np.ndarray, mod: PdschModulation, grid: np.ndarray = None) -> np.ndarray:
         return self.modulate_batch([codeword], [mod], grids=None if grid is None else grid[None])[0]
+
+
+class OfdmPlan:
+    """srsgpu_ofdm_plan: OFDM slot modulation (inverse=True) or demodulation of nof_grids slots x nof_ports ports.
+    Grids: (nof_grids, nof_ports, nsymb, 12 bw_rb) uint32 bf16 pairs; time buffer: nof_samples complex floats (as
+    2 * nof_samples float32), slot of (grid, port) at sample_offset(grid, port)."""
+
+    def __init__(self, ctx: Context, inverse: bool, numerology: int, bw_rb: int, dft_size: int, scale: float,
+                 center_freq_hz: float, slot_indices: Sequence[int], nof_ports: int, cp_extended: bool = False,
+                 window_offset: int = 0):
+        self.ctx, self.inverse = ctx, inverse
+        cfg = OfdmConfig(numerology, bw_rb, dft_size, int(cp_extended), window_offset, scale, center_freq_hz)
+        slots = (ctypes.c_uint32 * max(len(slot_indices), 1))(*slot_indices)
+        h = ctypes.c_void_p()
+        f = _lib.srsgpu_ofdm_modulator_plan_create if inverse else _lib.srsgpu_ofdm_demodulator_plan_create
+        _check(f(ctx.handle, ctypes.byref(cfg), len(slot_indices), nof_ports, ctypes.cast(slots, ctypes.c_void_p),
+                 ctypes.byref(h)))
+        self.handle = h
+        self.nof_grids, self.nof_ports = len(slot_indices), nof_ports
+        self.nsymb, self.nsc = (12 if cp_extended else 14), 12 * bw_rb
+        self.nof_samples = int(_lib.srsgpu_ofdm_plan_nof_samples(h))
+
+    def sample_offset(self, grid: int, port: int) -> int:
+        return int(_lib.srsgpu_ofdm_plan_sample_offset(self.handle, grid, port))
+
+    def execute(self, d_in, d_out, stream=None):
+        f = _lib.srsgpu_ofdm_modulator_plan_execute if self.inverse else _lib.srsgpu_ofdm_demodulator_plan_execute
+        _check(f(self.handle, _dptr(d_in), _dptr(d_out), _stream_handle(stream)))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.srsgpu_ofdm_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class OfdmSlotModulator:
+    """GPU counterpart of srsran::ofdm_slot_modulator (ofdm_modulator_impl.cpp:115): modulate(grid, slot) takes a
+    (nof_ports, nsymb, 12 bw_rb, 2) bf16 grid and returns (nof_ports, slot_size) complex64 samples."""
+
+    def __init__(self, ctx: Context, numerology, bw_rb, dft_size, scale, center_freq_hz, cp_extended=False):
+        self.ctx = ctx
+        self.args = (numerology, bw_rb, dft_size, scale, center_freq_hz)
+        self.cp_extended = cp_extended
+
+    def modulate(self, grid_u16: np.ndarray, slot_index: int) -> np.ndarray:
+        P = grid_u16.shape[0]
+        plan = OfdmPlan(self.ctx, True, *self.args, [slot_index], P, self.cp_extended)
+        dev = torch.device("cuda", self.ctx.device)
+        g = np.ascontiguousarray(grid_u16, np.uint16).view(np.int32).reshape(-1)
+        d_grid = torch.from_numpy(g.copy()).to(dev)
+        d_out = torch.zeros(2 * plan.nof_samples, dtype=torch.float32, device=dev)
+        plan.execute(d_grid, d_out)
+        torch.cuda.synchronize(dev)
+        plan.close()
+        return d_out.cpu().numpy().view(np.complex64).reshape(P, -1)
+
+
+class OfdmSlotDemodulator:
+    """GPU counterpart of srsran::ofdm_slot_demodulator (ofdm_demodulator_impl.cpp:154): demodulate(samples, slot)
+    takes (nof_ports, slot_size) complex samples and returns the (nof_ports, nsymb, 12 bw_rb, 2) bf16 grid."""
+
+    def __init__(self, ctx: Context, numerology, bw_rb, dft_size, scale, center_freq_hz, cp_extended=False,
+                 window_offset=0):
+        self.ctx = ctx
+        self.args = (numerology, bw_rb, dft_size, scale, center_freq_hz)
+        self.cp_extended, self.window_offset = cp_extended, window_offset
+
+    def demodulate(self, samples: np.ndarray, slot_index: int) -> np.ndarray:
+        P = samples.shape[0]
+        plan = OfdmPlan(self.ctx, False, *self.args, [slot_index], P, self.cp_extended, self.window_offset)
+        dev = torch.device("cuda", self.ctx.device)
+        x = np.ascontiguousarray(samples, np.complex64).view(np.float32).reshape(-1)
+        d_in = torch.from_numpy(x.copy()).to(dev)
+        d_grid = torch.zeros(P * plan.nsymb * plan.nsc, dtype=torch.int32, device=dev)
+        plan.execute(d_in, d_grid)
+        torch.cuda.synchronize(dev)
+        plan.close()
+        return d_grid.cpu().numpy().view(np.uint16).reshape(P, plan.nsymb, plan.nsc, 2)
 
 
 @dataclass

@@ -99,3 +99,15 @@ def pdsch_modulator_cases():
         wo += nw
         co += nc
         go += ng
+
+
+def ofdm_cases():
+    """Yields (case tuple of ofdm_cases.CASES, input bf16 grid (P, nsymb, nsc, 2), reference-modulated samples
+    (P, slot_size) complex64, reference-demodulated bf16 grid of those samples with scale 1 / (scale * N))."""
+    from ofdm_cases import CASES
+    d = _load("ofdm.npz")
+    i = 0
+    while f"case{i}_params" in d:
+        c = int(d[f"case{i}_params"][0])
+        yield CASES[c], d[f"case{i}_grid"], d[f"case{i}_samples"], d[f"case{i}_demod"]
+        i += 1

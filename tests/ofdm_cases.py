@@ -1,0 +1,57 @@
+"""OFDM test configurations and helpers shared by the oracle-vs-reference tests, the golden-fixture generator and the
+GPU parity tests. TEST INFRASTRUCTURE ONLY."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import ofdm_oracle  # noqa: E402,F401
+
+# (numerology, bw_rb, dft_size, extended CP, scale, center frequency, slot within the subframe, window offset)
+CASES = [
+    (1, 273, 4096, False, 1.0 / 64, 3.5e9, 0, 0),      # n78 100 MHz, 122.88 Msps
+    (1, 273, 4096, False, 0.0123, 3.6e9, 1, 17),
+    (1, 106, 2048, False, 0.05, 3.3e9, 1, 0),           # 40 MHz
+    (0, 52, 1024, False, 0.1, 1.8e9, 0, 5),             # 10 MHz 15 kHz: symbols 0 and 7 carry the long CP
+    (0, 25, 512, False, 0.2, 2.6e9, 0, 0),
+    (2, 66, 1024, True, 0.3, 28e9, 2, 0),               # 60 kHz extended CP
+    (2, 135, 2048, False, 0.07, 27e9, 3, 3),
+    (1, 24, 512, False, 0.25, 3.5e9, 0, 0),
+    (1, 10, 256, False, 1.0, 0.0, 1, 0),
+    (3, 66, 1024, False, 0.3, 28e9, 5, 0),              # 120 kHz
+    (1, 273, 8192, False, 1.0 / 128, 3.5e9, 0, 31),     # 245.76 Msps
+]
+
+
+def random_grid(rng, P, ns, nsc, occupancy=1.0):
+    """A bf16 grid of unit-power QPSK-like values (some REs empty)."""
+    x = (rng.normal(size=(P, ns, nsc)) + 1j * rng.normal(size=(P, ns, nsc))) / np.sqrt(2)
+    x[rng.random((P, ns, nsc)) > occupancy] = 0
+    return ofdm_oracle.complex_to_bf16(x)
+
+
+def rel_err(got, want):
+    return float(np.max(np.abs(got - want)) / max(np.sqrt(np.mean(np.abs(want) ** 2)), 1e-30))
+
+
+def bf16_ulp_diff(a_u16, b_u16):
+    """Per-value distance in bf16 units in the last place (sign-magnitude ordering)."""
+    def ordered(u):
+        u = u.astype(np.int32)
+        return np.where(u & 0x8000, -(u & 0x7FFF), u)
+    return np.abs(ordered(a_u16) - ordered(b_u16))
+
+
+def bf16_close(got_u16, want_u16, atol_rel_rms=1e-4):
+    """Fraction of significant values (|want| > 1e-3 RMS) that differ, and whether every value is within one bf16 ulp (<= 2^-7 relative) of the other or
+    within atol_rel_rms x RMS in absolute terms (values near zero, e.g. empty REs, carry only DFT rounding noise)."""
+    a = ofdm_oracle.bf16_to_complex(got_u16)
+    b = ofdm_oracle.bf16_to_complex(want_u16)
+    rms = np.sqrt(np.mean(np.abs(b) ** 2))
+    ok = True
+    for pa, pb in ((a.real, b.real), (a.imag, b.imag)):
+        ok &= bool(np.all(np.abs(pa - pb) <= np.maximum(np.abs(pb) * 2.0 ** -7, atol_rel_rms * rms)))
+    significant = np.abs(b) > 1e-3 * rms
+    differ = np.any(got_u16 != want_u16, axis=-1)
+    return ok, float(np.mean(differ[significant]))

@@ -138,6 +138,33 @@ class Reference(_Lib):
     def has_avx512(self):
         return bool(self.lib.ref_cpu_has_avx512())
 
+    def ofdm_slot_size(self, numerology, bw_rb, dft_size, extended, slot):
+        return int(self.lib.ref_ofdm_slot_size(numerology, bw_rb, dft_size, int(extended), slot))
+
+    def ofdm_modulate(self, grid_u16, numerology, bw_rb, dft_size, extended, scale, center_freq_hz, slot):
+        """ofdm_slot_modulator_impl::modulate of every port: (P, slot_size) complex64."""
+        g = np.ascontiguousarray(grid_u16, dtype=np.uint16)
+        P = g.shape[0]
+        n = self.ofdm_slot_size(numerology, bw_rb, dft_size, extended, slot)
+        out = np.zeros((P, n), np.complex64)
+        f = self.lib.ref_ofdm_modulate
+        f.argtypes = [ctypes.c_int] * 4 + [ctypes.c_float, ctypes.c_double, ctypes.c_int, ctypes.c_int, _P, _P]
+        f(numerology, bw_rb, dft_size, int(extended), scale, center_freq_hz, slot, P, _ptr(g), _ptr(out))
+        return out
+
+    def ofdm_demodulate(self, samples, numerology, bw_rb, dft_size, extended, scale, center_freq_hz, slot,
+                        window_offset=0):
+        """ofdm_slot_demodulator_impl::demodulate of every port: (P, nsymb, 12 bw_rb, 2) bf16 bit patterns."""
+        x = np.ascontiguousarray(samples, dtype=np.complex64)
+        P = x.shape[0]
+        ns = 12 if extended else 14
+        grid = np.zeros((P, ns, 12 * bw_rb, 2), np.uint16)
+        f = self.lib.ref_ofdm_demodulate
+        f.argtypes = [ctypes.c_int] * 4 + [ctypes.c_float, ctypes.c_double] + [ctypes.c_int] * 3 + [_P, _P]
+        f(numerology, bw_rb, dft_size, int(extended), scale, center_freq_hz, window_offset, slot, P, _ptr(x),
+          _ptr(grid))
+        return grid
+
     def ldpc_encode(self, bg, Z, msg, impl=0):
         msg = np.ascontiguousarray(msg, dtype=np.uint8)
         cb = np.zeros(BG_N_SHORT[bg] * Z, np.uint8)

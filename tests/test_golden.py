@@ -66,3 +66,19 @@ def test_pdsch_modulator_golden(orc):
         assert np.array_equal(orc.pdsch_modulate(cfg, w, cw, nbits, grid_prb), grid), cfg
         n += 1
     assert n == 12
+
+
+def test_ofdm_golden():
+    """The numpy OFDM restatement against the reference modulator's samples and demodulator's grids."""
+    import ofdm_oracle as O
+    from ofdm_cases import bf16_close, rel_err
+    n = 0
+    for (mu, rb, N, ext, scale, fc, slot, woff), grid, samples, demod in G.ofdm_cases():
+        got = O.modulate(grid, mu, rb, N, ext, scale, fc, slot)
+        assert rel_err(got, samples) < 2e-5
+        g2 = O.complex_to_bf16(O.demodulate(samples.astype(np.complex128), mu, rb, N, ext, 1.0 / (scale * N), fc,
+                                            slot, woff))
+        ok, frac = bf16_close(g2, demod)
+        assert ok and frac < 0.02, frac
+        n += 1
+    assert n == 5

@@ -191,3 +191,27 @@ def test_pdsch_modulator_full_band(orc, ref):
         cw = rng.integers(0, 256, (nbits + 7) // 8).astype(np.uint8)
         want = ref.pdsch_modulate(cfg, w, cw, nbits, 273)
         assert np.array_equal(orc.pdsch_modulate(cfg, w, cw, nbits, 273), want), (L, qm)
+
+
+@pytest.mark.parametrize("case", range(11))
+def test_ofdm_oracle_vs_reference(ref, case):
+    """OFDM modulator and demodulator restatement (oracle/ofdm_oracle.py, complex128) against the reference's
+    ofdm_slot_modulator_impl / ofdm_slot_demodulator_impl with its generic float DFT: slot sizes equal, modulated
+    samples within 2e-5 of the RMS (the reference's float radix-2 DFT error), demodulated bf16 grids equal except for
+    1-ulp rounding-boundary differences (and DFT noise on empty REs)."""
+    import ofdm_oracle as O
+    from ofdm_cases import CASES, bf16_close, random_grid, rel_err
+    mu, rb, N, ext, scale, fc, slot, woff = CASES[case]
+    rng = np.random.default_rng(100 + case)
+    ns = 12 if ext else 14
+    assert ref.ofdm_slot_size(mu, rb, N, ext, slot) == O.slot_size(mu, N, ext, slot)
+    grid = random_grid(rng, 2, ns, 12 * rb, occupancy=0.9)
+    want = ref.ofdm_modulate(grid, mu, rb, N, ext, scale, fc, slot)
+    got = O.modulate(grid, mu, rb, N, ext, scale, fc, slot)
+    assert rel_err(got, want) < 2e-5
+    # Demodulation of the reference's own samples.
+    gref = ref.ofdm_demodulate(want, mu, rb, N, ext, 1.0 / (scale * N), fc, slot, woff)
+    gorc = O.complex_to_bf16(O.demodulate(want.astype(np.complex128), mu, rb, N, ext, 1.0 / (scale * N), fc, slot,
+                                          woff))
+    ok, frac = bf16_close(gorc, gref)
+    assert ok and frac < 0.02, frac

@@ -166,15 +166,42 @@ def gen_pdsch_modulator(ref, rng):
                         grid=np.concatenate(grids))
 
 
+GOLDEN_OFDM_CASES = [(3, 2), (5, 1), (8, 2), (0, 1), (6, 1)]  # (index into ofdm_cases.CASES, ports)
+
+
+def gen_ofdm(ref, rng):
+    """Reference OFDM slot modulator output of random bf16 grids, and the reference demodulator's grid of those
+    samples (scale 1 / (scale * N): the round trip returns the input grid up to bf16 rounding)."""
+    from ofdm_cases import CASES, random_grid
+    out = {}
+    for i, (c, P) in enumerate(GOLDEN_OFDM_CASES):
+        mu, rb, N, ext, scale, fc, slot, woff = CASES[c]
+        ns = 12 if ext else 14
+        grid = random_grid(rng, P, ns, 12 * rb, occupancy=0.9)
+        x = ref.ofdm_modulate(grid, mu, rb, N, ext, scale, fc, slot)
+        g2 = ref.ofdm_demodulate(x, mu, rb, N, ext, 1.0 / (scale * N), fc, slot, woff)
+        out[f"case{i}_grid"] = grid
+        out[f"case{i}_samples"] = x
+        out[f"case{i}_demod"] = g2
+        out[f"case{i}_params"] = np.array([c, P], np.int64)
+    np.savez_compressed(os.path.join(OUT, "ofdm.npz"), **out)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     ref = Reference()
+    if len(sys.argv) > 1:  # regenerate only the named fixture sets, e.g. `python tools/gen_golden.py ofdm`
+        for name in sys.argv[1:]:
+            seed = {"ofdm": 16}[name]
+            globals()["gen_" + name](ref, np.random.default_rng(seed))
+        return
     gen_crc(ref, np.random.default_rng(10))
     gen_encoder(ref, np.random.default_rng(11))
     gen_decoder(ref, np.random.default_rng(12))
     gen_rate_matching(ref, np.random.default_rng(13))
     gen_pdsch_encoder(ref, np.random.default_rng(14))
     gen_pdsch_modulator(ref, np.random.default_rng(15))
+    gen_ofdm(ref, np.random.default_rng(16))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

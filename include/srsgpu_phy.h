@@ -319,6 +319,66 @@ int srsgpu_ofdm_demodulator_plan_execute(const srsgpu_ofdm_plan* plan,
 void srsgpu_ofdm_plan_destroy(srsgpu_ofdm_plan* plan);
 
 /* ------------------------------------------------------------------------------------------------------------------
+ * PUSCH demodulator — replaces srsran::pusch_demodulator::demodulate(pusch_codeword_buffer& codeword_buffer,
+ * pusch_demodulator_notifier& notifier, const resource_grid_reader& grid, const channel_estimate& estimates,
+ * const configuration& config) (include/srsran/phy/upper/channel_processors/pusch/pusch_demodulator.h:95,
+ * lib/phy/upper/channel_processors/pusch/pusch_demodulator_impl.cpp:272) for every PUSCH transmission of a batch of
+ * slots: per data RE, channel equalization (channel_equalizer_generic_impl.cpp: ZF 1 x N, ZF 2 x N; MMSE with one
+ * layer == ZF), soft demapping (demodulation_mapper_impl.cpp, the SIMD arithmetic) and descrambling
+ * (c_init = rnti * 2^15 + n_id), LLRs written to the codeword buffer in the reference's order (RE, layer, bit).
+ * SRSGPU_EQ_MMSE with 2..4 layers and ZF with 3..4 layers are extensions the open-source reference does not implement
+ * (its equalize_mmse_* / equalize_zf_3x4 / _4x4 assert): unbiased linear MMSE.
+ * Inputs: rx grids as in the OFDM demodulator (grid_nof_ports x 14 x 12 * grid_nof_prb uint32 bf16 pairs per slot);
+ * channel estimates per slot [layer 0..3][port][symbol][subcarrier] bf16 pairs (srsran::channel_estimate's path-major
+ * layout, channel_estimation.h:310); noise variances d_noise_var[4 * tx + port] (channel_estimate::get_noise_variance).
+ * ------------------------------------------------------------------------------------------------------------------ */
+#define SRSGPU_EQ_ZF 0
+#define SRSGPU_EQ_MMSE 1
+
+typedef struct {
+  uint16_t rnti;                        /* n_RNTI */
+  uint16_t n_id;                        /* n_ID, 0..1023 */
+  uint8_t  modulation_order;            /* Qm: 2, 4, 6, 8 */
+  uint8_t  nof_tx_layers;               /* 1..4 */
+  uint8_t  nof_rx_ports;                /* 1..grid_nof_ports (ports 0..n-1) */
+  uint8_t  start_symbol;
+  uint8_t  nof_symbols;                 /* start_symbol + nof_symbols <= 14 */
+  uint8_t  dmrs_type;                   /* 1 or 2 */
+  uint8_t  nof_cdm_groups_without_data; /* 1..2 (type 1), 1..3 (type 2) */
+  uint8_t  equalizer;                   /* SRSGPU_EQ_ZF or SRSGPU_EQ_MMSE */
+  uint16_t dmrs_symbol_mask;            /* bit l = OFDM symbol l carries DM-RS */
+  uint16_t rb_start;                    /* contiguous CRB allocation [rb_start, rb_start + nof_rb) (rb_mask) */
+  uint16_t nof_rb;
+  uint16_t pad;
+  uint32_t grid_index;                  /* slot (rx grid and channel estimate) of the transmission */
+  uint32_t llr_offset;                  /* first codeword LLR in the output buffer */
+} srsgpu_pusch_demod_config;
+
+typedef struct srsgpu_pusch_demodulator_plan srsgpu_pusch_demodulator_plan;
+
+/** Validates the transmissions (supported layer / port / modulation combinations, allocation inside the grid) and
+ *  uploads the work. */
+int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
+                                         const srsgpu_pusch_demod_config* cfgs,
+                                         uint32_t                         nof_tx,
+                                         uint32_t                         grid_nof_prb,
+                                         uint32_t                         grid_nof_ports,
+                                         srsgpu_pusch_demodulator_plan**  plan);
+
+/** Number of codeword LLRs of transmission `tx` (data REs x layers x Qm). */
+uint32_t srsgpu_pusch_demodulator_plan_nof_llrs(const srsgpu_pusch_demodulator_plan* plan, uint32_t tx);
+
+/** Demodulates every planned transmission into d_llrs. Asynchronous on `stream`, hipGraph-capturable. */
+int srsgpu_pusch_demodulator_plan_execute(const srsgpu_pusch_demodulator_plan* plan,
+                                          const uint32_t*                      d_grids,
+                                          const uint32_t*                      d_ch_estimates,
+                                          const float*                         d_noise_var,
+                                          int8_t*                              d_llrs,
+                                          void*                                stream);
+
+void srsgpu_pusch_demodulator_plan_destroy(srsgpu_pusch_demodulator_plan* plan);
+
+/* ------------------------------------------------------------------------------------------------------------------
  * PUSCH decoder (transport-block level) — replaces srsran::pusch_decoder (include/srsran/phy/upper/channel_processors/
  * pusch/pusch_decoder.h; lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.cpp: new_data :98, segmentation
  * :190, codeblock tasks :283, join_and_notify :386): segmentation, per-codeblock rate dematching + HARQ combining +

@@ -57,6 +57,14 @@ SRCS=(
   "$REF/lib/phy/generic_functions/dft_processor_generic_impl.cpp:-mavx2 -mfma"
   "$REF/lib/srsvec/prod.cpp:-mavx2 -mfma"
   "$HERE/ref/ref_ofdm.cpp:-mavx2 -mfma -I$REF"
+  "$REF/lib/phy/upper/channel_processors/pusch/pusch_demodulator_impl.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/upper/equalization/channel_equalizer_generic_impl.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/upper/channel_modulation/demodulation_mapper_impl.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/upper/channel_modulation/demodulation_mapper_qpsk.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/upper/channel_modulation/demodulation_mapper_qam16.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/upper/channel_modulation/demodulation_mapper_qam64.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/upper/channel_modulation/demodulation_mapper_qam256.cpp:-mavx2 -mfma"
+  "$HERE/ref/ref_pusch_demod.cpp:-mavx2 -mfma -I$REF"
 )
 OBJS=()
 pids=()

@@ -62,6 +62,11 @@ struct srsgpu_context {
   std::mutex                           mtx;
 };
 
+namespace srsgpu {
+/// Builds and uploads the Gold-sequence jump tables into the context once (caller holds ctx->mtx); capi_pdsch_mod.cpp.
+int ensure_gold_tables(srsgpu_context* ctx);
+} // namespace srsgpu
+
 /// Per-stage device time accounting: HIP events recorded around every kernel stage on the execution stream.
 struct stage_timer {
   bool                                  enabled = false;

@@ -44,8 +44,10 @@ uint32_t gf2_apply(const uint32_t* cols, uint32_t v)
   return r;
 }
 
+} // namespace
+
 /// Builds and uploads the scrambler's Gold-sequence tables into the context (once; caller holds ctx->mtx).
-int ensure_gold_tables(srsgpu_context* ctx)
+int srsgpu::ensure_gold_tables(srsgpu_context* ctx)
 {
   if (ctx->d_gold_x1 != nullptr) {
     return SRSGPU_OK;
@@ -113,6 +115,8 @@ int ensure_gold_tables(srsgpu_context* ctx)
   ctx->d_gold_x2_lane = d_lane;
   return SRSGPU_OK;
 }
+
+namespace {
 
 /// TS 38.211 section 5.1 constellation point (integer grid) of `index`, as modulation_mapper_lut_impl.cpp:39 builds
 /// its tables; used for the average power only.

@@ -1,0 +1,242 @@
+// Host side of the PUSCH demodulator C ABI (include/srsgpu_phy.h): validation (the equalizer and demapper
+// combinations, allocation inside the grid), the max-log demapper interval tables (derived from the Gray PAM, like the
+// reference's demodulation_mapper_qam64.cpp / _qam256.cpp tables) and per-transmission descriptors / 8192-LLR chunks.
+#include "capi_internal.h"
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+using namespace srsgpu;
+
+static_assert(sizeof(srsgpu_pusch_demod_config) == 28, "srsgpu_pusch_demod_config layout (mirrored by srsgpu)");
+
+struct srsgpu_pusch_demodulator_plan {
+  srsgpu_context*       ctx        = nullptr;
+  demod_desc*           d_desc     = nullptr;
+  mod_chunk*            d_chunks   = nullptr;
+  demap_pair_table*     d_tables   = nullptr;
+  int                   nof_chunks = 0;
+  std::vector<uint32_t> nof_llrs;
+};
+
+namespace {
+
+/// Max-log (slope, intercept) pieces of one bit pair of a Gray PAM with 2^(qm/2) levels: for stream bit 2k, the
+/// levels (odd integers, units of a = 1 / sqrt(average power)) carrying 0 and 1 as modulation_mapper_lut_impl.cpp:39
+/// builds them; LLR(y) = (min_{x1} (y - x1)^2 - min_{x0} (y - x0)^2) / nv is linear between consecutive even
+/// integers: slope 2 (x0 - x1) a, intercept (x1^2 - x0^2) a^2. Pieces are merged pairwise when every pair is equal
+/// (the reference's 4a-wide tables).
+demap_pair_table pair_table(unsigned qm, unsigned k)
+{
+  const int      half = static_cast<int>(qm / 2);
+  const int      L    = 1 << half;
+  std::vector<int> x0s, x1s;
+  for (unsigned idx = 0; idx < (1u << qm); ++idx) {
+    int real = 0, off = -1;
+    for (int j = 0; j < half; ++j) {
+      real += off;
+      off *= 2;
+      real *= ((idx >> (2 * j + 1)) & 1u) ? 1 : -1;
+    }
+    const unsigned bit = (idx >> (qm - 1 - 2 * k)) & 1u;
+    (bit ? x1s : x0s).push_back(real);
+  }
+  auto nearest = [](const std::vector<int>& xs, int y) {
+    int best = xs[0];
+    for (int x : xs) {
+      if (std::abs(y - x) < std::abs(y - best)) {
+        best = x;
+      }
+    }
+    return best;
+  };
+  std::vector<int> slopes(static_cast<size_t>(L)), inters(static_cast<size_t>(L));
+  for (int i = 0; i < L; ++i) {
+    const int y  = 2 * (i - L / 2) + 1;
+    const int x0 = nearest(x0s, y), x1 = nearest(x1s, y);
+    slopes[static_cast<size_t>(i)] = 2 * (x0 - x1);
+    inters[static_cast<size_t>(i)] = (x1 * x1 - x0 * x0) / 2;
+  }
+  bool mergeable = true;
+  for (int i = 0; i < L / 2; ++i) {
+    mergeable &= slopes[2 * i] == slopes[2 * i + 1] && inters[2 * i] == inters[2 * i + 1];
+  }
+  const int   avg = 2 * (L * L - 1) / 3;  // average power of the integer constellation
+  const float a   = 1.0F / std::sqrt(static_cast<float>(avg));
+  const int   step = mergeable ? 2 : 1;
+  demap_pair_table t{};
+  t.width = static_cast<float>(2 * step) * a;
+  t.count = static_cast<uint32_t>(L / step);
+  for (int i = 0; i < L / step; ++i) {
+    t.slope[i]     = static_cast<float>(slopes[static_cast<size_t>(i * step)]) * a;
+    t.intercept[i] = static_cast<float>(inters[static_cast<size_t>(i * step)]) / static_cast<float>(avg / 2);
+  }
+  return t;
+}
+
+} // namespace
+
+extern "C" {
+
+int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
+                                         const srsgpu_pusch_demod_config* cfgs,
+                                         uint32_t                         nof_tx,
+                                         uint32_t                         grid_nof_prb,
+                                         uint32_t                         grid_nof_ports,
+                                         srsgpu_pusch_demodulator_plan**  plan_out)
+{
+  if (ctx == nullptr || plan_out == nullptr || (cfgs == nullptr && nof_tx > 0)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  if (grid_nof_prb == 0 || grid_nof_prb > 275 || grid_nof_ports == 0 || grid_nof_ports > 4) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "invalid grid geometry (%u PRB, %u ports)", grid_nof_prb, grid_nof_ports);
+  }
+  const uint32_t          nsc = 12u * grid_nof_prb;
+  std::vector<demod_desc> descs(nof_tx);
+  std::vector<mod_chunk>  chunks;
+  std::vector<uint32_t>   nllr(nof_tx);
+  for (uint32_t t = 0; t < nof_tx; ++t) {
+    const srsgpu_pusch_demod_config& c  = cfgs[t];
+    const unsigned                   qm = c.modulation_order;
+    const unsigned                   L  = c.nof_tx_layers, P = c.nof_rx_ports;
+    if (qm != 2 && qm != 4 && qm != 6 && qm != 8) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid modulation order %u", t, qm);
+    }
+    // channel_equalizer_generic_impl.cpp:247 is_supported: 1, 2 or 4 ports... (any 1..4 for one layer), layers <= ports.
+    if (L < 1 || L > 4 || P < L || P > grid_nof_ports || c.equalizer > SRSGPU_EQ_MMSE) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid layers / ports / equalizer (%u, %u, %u)", t, L, P,
+                  c.equalizer);
+    }
+    if (L == 2 && c.equalizer == SRSGPU_EQ_ZF && P != 2 && P != 4) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: ZF with two layers needs two or four ports", t);
+    }
+    if (c.nof_symbols < 1 || c.start_symbol + c.nof_symbols > 14 || (c.dmrs_type != 1 && c.dmrs_type != 2) ||
+        c.nof_cdm_groups_without_data < 1 || c.nof_cdm_groups_without_data > (c.dmrs_type == 1 ? 2 : 3) ||
+        c.n_id > 1023 || c.nof_rb < 1 || c.rb_start + c.nof_rb > grid_nof_prb) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid time / frequency allocation or DM-RS configuration", t);
+    }
+    demod_desc d{};
+    unsigned   nd = 0;
+    for (unsigned k = 0; k < 12; ++k) {
+      const unsigned group = (c.dmrs_type == 2) ? (k % 6) / 2 : k % 2;
+      if (group >= c.nof_cdm_groups_without_data) {
+        d.dmrs_lut |= static_cast<uint64_t>(k) << (4 * nd);
+        ++nd;
+      }
+    }
+    uint32_t nre = 0;
+    for (unsigned l = 0; l < 14; ++l) {
+      d.sym_cum[l] = static_cast<uint16_t>(nre);
+      if (l >= c.start_symbol && l < static_cast<unsigned>(c.start_symbol + c.nof_symbols)) {
+        nre += (((c.dmrs_symbol_mask >> l) & 1u) ? nd : 12u) * c.nof_rb;
+      }
+    }
+    d.sym_cum[14] = d.sym_cum[15] = static_cast<uint16_t>(nre);
+    const uint32_t Lq = L * qm;
+    if (static_cast<uint64_t>(nre) * Lq > MOD_MAX_BITS) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: codeword too long", t);
+    }
+    const uint64_t slot_elems = static_cast<uint64_t>(grid_nof_ports) * 14u * nsc;
+    if ((static_cast<uint64_t>(c.grid_index) + 1) * slot_elems * 4u >= (1ull << 32)) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: grid index beyond 32-bit element offsets", t);
+    }
+    d.grid_base       = static_cast<uint32_t>(c.grid_index * slot_elems) + c.rb_start * 12u;
+    d.port_stride     = 14u * nsc;
+    d.nsc             = nsc;
+    d.ce_layer_stride = static_cast<uint32_t>(slot_elems);
+    d.ce_base         = static_cast<uint32_t>(c.grid_index * slot_elems * 4u) + c.rb_start * 12u;
+    d.llr_offset      = c.llr_offset;
+    d.nof_llrs        = nre * Lq;
+    d.c_init          = (static_cast<uint32_t>(c.rnti) << 15) + c.n_id;  // pusch_demodulator_impl.cpp:279
+    d.tx              = t;
+    d.dmrs_mask       = c.dmrs_symbol_mask;
+    d.qm              = static_cast<uint8_t>(qm);
+    d.L               = static_cast<uint8_t>(L);
+    d.P               = static_cast<uint8_t>(P);
+    d.nd_dmrs         = static_cast<uint8_t>(nd);
+    d.eq              = (L >= 3 || c.equalizer == SRSGPU_EQ_MMSE) ? DEMOD_EQ_MMSE : DEMOD_EQ_ZF;
+    descs[t]          = d;
+    nllr[t]           = d.nof_llrs;
+    const uint32_t nwords = (d.nof_llrs + 31) / 32;
+    for (uint32_t w0 = 0; w0 < nwords; w0 += MOD_CHUNK_WORDS) {
+      const uint32_t b0 = w0 * 32, b1 = b0 + MOD_CHUNK_WORDS * 32;
+      mod_chunk      ch{t, w0, (b0 + Lq - 1) / Lq, std::min(nre, (b1 + Lq - 1) / Lq)};
+      if (ch.re_end > ch.re_begin) {
+        chunks.push_back(ch);
+      }
+    }
+  }
+  std::vector<demap_pair_table> tables;
+  for (unsigned k = 0; k < 3; ++k) {
+    tables.push_back(pair_table(6, k));
+  }
+  for (unsigned k = 0; k < 4; ++k) {
+    tables.push_back(pair_table(8, k));
+  }
+  std::lock_guard<std::mutex> lock(ctx->mtx);
+  HIP_TRY(hipSetDevice(ctx->device));
+  int r = ensure_gold_tables(ctx);
+  if (r != SRSGPU_OK) {
+    return r;
+  }
+  auto* plan       = new srsgpu_pusch_demodulator_plan();
+  plan->ctx        = ctx;
+  plan->nof_chunks = static_cast<int>(chunks.size());
+  plan->nof_llrs   = std::move(nllr);
+  bool ok = hipMalloc(&plan->d_tables, tables.size() * sizeof(demap_pair_table)) == hipSuccess &&
+            hipMemcpy(plan->d_tables, tables.data(), tables.size() * sizeof(demap_pair_table),
+                      hipMemcpyHostToDevice) == hipSuccess;
+  if (ok && !chunks.empty()) {
+    ok = hipMalloc(&plan->d_desc, descs.size() * sizeof(demod_desc)) == hipSuccess &&
+         hipMemcpy(plan->d_desc, descs.data(), descs.size() * sizeof(demod_desc), hipMemcpyHostToDevice) ==
+             hipSuccess &&
+         hipMalloc(&plan->d_chunks, chunks.size() * sizeof(mod_chunk)) == hipSuccess &&
+         hipMemcpy(plan->d_chunks, chunks.data(), chunks.size() * sizeof(mod_chunk), hipMemcpyHostToDevice) ==
+             hipSuccess;
+  }
+  if (!ok) {
+    srsgpu_pusch_demodulator_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload demodulator descriptors");
+  }
+  *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+uint32_t srsgpu_pusch_demodulator_plan_nof_llrs(const srsgpu_pusch_demodulator_plan* plan, uint32_t tx)
+{
+  return (plan == nullptr || tx >= plan->nof_llrs.size()) ? 0u : plan->nof_llrs[tx];
+}
+
+int srsgpu_pusch_demodulator_plan_execute(const srsgpu_pusch_demodulator_plan* plan,
+                                          const uint32_t*                      d_grids,
+                                          const uint32_t*                      d_ch_estimates,
+                                          const float*                         d_noise_var,
+                                          int8_t*                              d_llrs,
+                                          void*                                stream)
+{
+  if (plan == nullptr || d_grids == nullptr || d_ch_estimates == nullptr || d_noise_var == nullptr ||
+      d_llrs == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  launch_pusch_demodulate(plan->d_desc, plan->d_chunks, plan->nof_chunks, plan->d_tables, d_grids, d_ch_estimates,
+                          d_noise_var, d_llrs, plan->ctx->d_gold_x1, plan->ctx->d_gold_x2_jump,
+                          plan->ctx->d_gold_x2_lane, static_cast<hipStream_t>(stream));
+  HIP_TRY(hipGetLastError());
+  return SRSGPU_OK;
+}
+
+void srsgpu_pusch_demodulator_plan_destroy(srsgpu_pusch_demodulator_plan* plan)
+{
+  if (plan == nullptr) {
+    return;
+  }
+  for (void* p : {static_cast<void*>(plan->d_desc), static_cast<void*>(plan->d_chunks),
+                  static_cast<void*>(plan->d_tables)}) {
+    if (p != nullptr) {
+      (void)hipFree(p);
+    }
+  }
+  delete plan;
+}
+
+} // extern "C"

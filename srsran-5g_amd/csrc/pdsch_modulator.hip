@@ -15,6 +15,7 @@
 //
 // Floating point follows the reference exactly: every complex product term is rounded separately (no contraction),
 // layer terms are summed in layer order and the result is rounded to bf16 half-to-even.
+#include "gold_device.h"
 #include "srsgpu_internal.h"
 
 #pragma clang fp contract(off)
@@ -23,17 +24,6 @@ namespace srsgpu {
 namespace {
 
 constexpr int MOD_THREADS = 256;
-
-/// y = M v for a 31x31 GF(2) matrix given by its columns (wave-uniform operands: scalar path).
-__device__ __forceinline__ uint32_t gf2_apply_uniform(const uint32_t* __restrict__ cols, uint32_t v)
-{
-  uint32_t r = 0;
-#pragma unroll
-  for (int j = 0; j < 31; ++j) {
-    r ^= cols[j] & (0u - ((v >> j) & 1u));
-  }
-  return r;
-}
 
 /// Scrambled codeword word w (bits 32w..32w+31, MSB first) of a transmission.
 __device__ __forceinline__ uint32_t scrambled_word(const mod_desc& d,
@@ -44,20 +34,7 @@ __device__ __forceinline__ uint32_t scrambled_word(const mod_desc& d,
                                                    uint32_t w,
                                                    uint32_t c_uniform)
 {
-  // x2 state (x2(n), ..., x2(n + 30)) at n = Nc + 2048 c, then at n = Nc + 32 w.
-  const uint32_t sc = gf2_apply_uniform(x2_jump + c_uniform * 31u, d.c_init);
-  const uint32_t i  = w & 63u;
-  uint32_t       s  = 0;
-#pragma unroll
-  for (int j = 0; j < 31; ++j) {
-    if ((sc >> j) & 1u) {  // uniform branch
-      s ^= x2_lane[j * 64 + i];
-    }
-  }
-  // 32 sequence bits: the window plus x2(n + 31) = x2(n + 3) + x2(n + 2) + x2(n + 1) + x2(n).
-  const uint32_t x2w = s | (((s ^ (s >> 1) ^ (s >> 2) ^ (s >> 3)) & 1u) << 31);
-  const uint32_t seq = __builtin_bitreverse32(x1[w] ^ x2w);  // LSB-first -> MSB-first
-  return __builtin_bswap32(cw[d.cw_word_offset + w]) ^ seq;
+  return __builtin_bswap32(cw[d.cw_word_offset + w]) ^ gold_word(d.c_init, w, c_uniform, x1, x2_jump, x2_lane);
 }
 
 __device__ __forceinline__ uint32_t to_bf16_bits(float v)

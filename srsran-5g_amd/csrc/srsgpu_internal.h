@@ -252,4 +252,52 @@ void launch_ofdm(bool            inverse,
                  float*          d_samples_out,
                  hipStream_t     stream);
 
+/// PUSCH demodulator (pusch_demodulator.hip): per-transmission descriptor. Work items are mod_chunk (8192 LLRs each).
+struct demod_desc {
+  uint64_t dmrs_lut;        ///< Data subcarriers (4 bits each, ascending) of a PRB on DM-RS symbols.
+  uint32_t grid_base;       ///< Element of (port 0, symbol 0, first allocated subcarrier) in the rx grids.
+  uint32_t port_stride;     ///< Elements per port of a grid (14 * nsc).
+  uint32_t nsc;             ///< Subcarriers per OFDM symbol.
+  uint32_t ce_base;         ///< Element of (layer 0, port 0, symbol 0, first allocated subcarrier) in the estimates.
+  uint32_t ce_layer_stride; ///< Elements per layer of a slot's estimates (grid_nof_ports * 14 * nsc).
+  uint32_t llr_offset;      ///< First codeword LLR.
+  uint32_t nof_llrs;        ///< Codeword length.
+  uint32_t c_init;          ///< Descrambling sequence initial state.
+  uint32_t tx;              ///< Transmission index (noise variances at 4 * tx).
+  uint16_t dmrs_mask;       ///< DM-RS symbols.
+  uint8_t  qm, L, P;        ///< Modulation order, layers, rx ports.
+  uint8_t  nd_dmrs;         ///< Data REs per PRB on DM-RS symbols.
+  uint8_t  eq;              ///< Equalizer kind (DEMOD_EQ_*).
+  uint8_t  pad;
+  uint16_t sym_cum[16];     ///< Data REs in the symbols before symbol l (l = 0..14).
+};
+static_assert(sizeof(demod_desc) == 88, "demod_desc layout");
+
+/// demod_desc::eq: the reference's ZF paths (1 layer: 1 x N with port reduction; 2 layers: 2 x N) or linear MMSE.
+constexpr uint8_t DEMOD_EQ_ZF   = 0;
+constexpr uint8_t DEMOD_EQ_MMSE = 1;
+
+/// Max-log interval tables of the 64QAM / 256QAM demapper: per bit pair k (stream bits 2k, 2k + 1) an interval width,
+/// a count and (slope, intercept) per interval. Index 0..2: 64QAM, 3..6: 256QAM.
+struct demap_pair_table {
+  float    width;
+  uint32_t count;
+  float    slope[16];
+  float    intercept[16];
+};
+constexpr int DEMAP_TABLES = 7;
+
+void launch_pusch_demodulate(const demod_desc*        d_desc,
+                             const mod_chunk*         d_chunks,
+                             int                      nof_chunks,
+                             const demap_pair_table*  d_tables,
+                             const uint32_t*          d_grids,
+                             const uint32_t*          d_ch_est,
+                             const float*             d_noise_var,
+                             int8_t*                  d_llrs,
+                             const uint32_t*          d_x1,
+                             const uint32_t*          d_x2_jump,
+                             const uint32_t*          d_x2_lane,
+                             hipStream_t              stream);
+
 } // namespace srsgpu

@@ -158,6 +158,32 @@ assert ctypes.sizeof(PdschModConfig) == 168
 CB_MSG_STRIDE = 1056
 
 
+class PuschDemodConfig(ctypes.Structure):
+    """srsgpu_pusch_demod_config (include/srsgpu_phy.h): one transmission of pusch_demodulator::configuration."""
+    _fields_ = [
+        ("rnti", ctypes.c_uint16),
+        ("n_id", ctypes.c_uint16),
+        ("modulation_order", ctypes.c_uint8),
+        ("nof_tx_layers", ctypes.c_uint8),
+        ("nof_rx_ports", ctypes.c_uint8),
+        ("start_symbol", ctypes.c_uint8),
+        ("nof_symbols", ctypes.c_uint8),
+        ("dmrs_type", ctypes.c_uint8),
+        ("nof_cdm_groups_without_data", ctypes.c_uint8),
+        ("equalizer", ctypes.c_uint8),
+        ("dmrs_symbol_mask", ctypes.c_uint16),
+        ("rb_start", ctypes.c_uint16),
+        ("nof_rb", ctypes.c_uint16),
+        ("pad", ctypes.c_uint16),
+        ("grid_index", ctypes.c_uint32),
+        ("llr_offset", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(PuschDemodConfig) == 28
+EQ_ZF, EQ_MMSE = 0, 1
+
+
 class OfdmConfig(ctypes.Structure):
     """srsgpu_ofdm_config (include/srsgpu_phy.h): ofdm_modulator_configuration / ofdm_demodulator_configuration."""
     _fields_ = [
@@ -218,6 +244,13 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pdsch_modulator_plan_execute.argtypes = [P, P, P, P]
     lib.srsgpu_pdsch_modulator_plan_destroy.argtypes = [P]
     lib.srsgpu_pdsch_modulator_plan_destroy.restype = None
+    lib.srsgpu_pusch_demodulator_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                         ctypes.POINTER(P)]
+    lib.srsgpu_pusch_demodulator_plan_nof_llrs.argtypes = [P, ctypes.c_uint32]
+    lib.srsgpu_pusch_demodulator_plan_nof_llrs.restype = ctypes.c_uint32
+    lib.srsgpu_pusch_demodulator_plan_execute.argtypes = [P, P, P, P, P, P]
+    lib.srsgpu_pusch_demodulator_plan_destroy.argtypes = [P]
+    lib.srsgpu_pusch_demodulator_plan_destroy.restype = None
     for name in ("srsgpu_ofdm_modulator_plan_create", "srsgpu_ofdm_demodulator_plan_create"):
         getattr(lib, name).argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, P, ctypes.POINTER(P)]
     lib.srsgpu_ofdm_plan_nof_samples.argtypes = [P]
@@ -250,7 +283,8 @@ EXPORTED_SYMBOLS = [
     "srsgpu_pdsch_modulator_plan_execute", "srsgpu_pdsch_modulator_plan_destroy",
     "srsgpu_ofdm_modulator_plan_create", "srsgpu_ofdm_demodulator_plan_create", "srsgpu_ofdm_plan_nof_samples",
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
-    "srsgpu_ofdm_plan_destroy",
+    "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
+    "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
 ]
 
 
@@ -721,6 +755,107 @@ class PdschModulator:
 
     def modulate(self, codeword: np.ndarray, mod: PdschModulation, grid: np.ndarray = None) -> np.ndarray:
         return self.modulate_batch([codeword], [mod], grids=None if grid is None else grid[None])[0]
+
+
+@dataclass
+class PuschDemodulation:
+    """pusch_demodulator::configuration (pusch_demodulator.h:51) of one transmission with a contiguous CRB allocation
+    and rx ports 0..nof_rx_ports-1."""
+    rnti: int
+    n_id: int
+    modulation_order: int
+    nof_tx_layers: int
+    nof_rx_ports: int
+    start_symbol: int
+    nof_symbols: int
+    dmrs_symbol_mask: int
+    dmrs_type: int
+    nof_cdm_groups_without_data: int
+    rb_start: int
+    nof_rb: int
+    equalizer: int = EQ_ZF
+
+    def nof_llrs(self) -> int:
+        dm = (4 if self.dmrs_type == 2 else 6) * self.nof_cdm_groups_without_data
+        nre = sum((12 - dm if (self.dmrs_symbol_mask >> l) & 1 else 12) * self.nof_rb
+                  for l in range(self.start_symbol, self.start_symbol + self.nof_symbols))
+        return nre * self.nof_tx_layers * self.modulation_order
+
+
+def make_pusch_demod_configs(demods: Sequence[PuschDemodulation], grid_index: Sequence[int], llr_offsets=None):
+    arr = (PuschDemodConfig * len(demods))()
+    off = 0
+    offs = []
+    for i, (m, g) in enumerate(zip(demods, grid_index)):
+        a = arr[i]
+        a.rnti, a.n_id, a.modulation_order, a.nof_tx_layers = m.rnti, m.n_id, m.modulation_order, m.nof_tx_layers
+        a.nof_rx_ports, a.start_symbol, a.nof_symbols = m.nof_rx_ports, m.start_symbol, m.nof_symbols
+        a.dmrs_type, a.nof_cdm_groups_without_data, a.equalizer = (m.dmrs_type, m.nof_cdm_groups_without_data,
+                                                                   m.equalizer)
+        a.dmrs_symbol_mask, a.rb_start, a.nof_rb, a.grid_index = m.dmrs_symbol_mask, m.rb_start, m.nof_rb, g
+        a.llr_offset = off if llr_offsets is None else llr_offsets[i]
+        offs.append(a.llr_offset)
+        off += m.nof_llrs()
+    return arr, offs, off
+
+
+class PuschDemodulatorPlan:
+    """srsgpu_pusch_demodulator_plan: equalization + soft demapping + descrambling of a batch of PUSCH transmissions
+    from rx grids (nslots, ports, 14, nsc) and channel estimates (nslots, 4 layers, ports, 14, nsc) (uint32 bf16 pairs)
+    and noise variances (ntx, 4) float32 into int8 codeword LLRs."""
+
+    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        _check(_lib.srsgpu_pusch_demodulator_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                         len(cfg_array), grid_nof_prb, grid_nof_ports,
+                                                         ctypes.byref(h)))
+        self.handle = h
+        self.nof_tx = len(cfg_array)
+
+    def nof_llrs(self, tx: int) -> int:
+        return int(_lib.srsgpu_pusch_demodulator_plan_nof_llrs(self.handle, tx))
+
+    def execute(self, d_grids, d_ch_est, d_noise_var, d_llrs, stream=None):
+        _check(_lib.srsgpu_pusch_demodulator_plan_execute(self.handle, _dptr(d_grids), _dptr(d_ch_est),
+                                                          _dptr(d_noise_var), _dptr(d_llrs), _stream_handle(stream)))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.srsgpu_pusch_demodulator_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class PuschDemodulator:
+    """GPU counterpart of srsran::pusch_demodulator::demodulate (pusch_demodulator_impl.cpp:272): demodulate() takes
+    bf16 grids / channel estimates as uint16 (..., 2) arrays and returns the codeword LLRs (int8) of each
+    transmission."""
+
+    def __init__(self, ctx: Context, grid_nof_prb: int, grid_nof_ports: int = 4):
+        self.ctx, self.grid_nof_prb, self.grid_nof_ports = ctx, grid_nof_prb, grid_nof_ports
+
+    def demodulate_batch(self, grids_u16, ch_est_u16, noise_vars, demods: Sequence[PuschDemodulation],
+                         grid_index: Sequence[int]):
+        """grids_u16 (S, Pg, 14, nsc, 2); ch_est_u16 (S, 4, Pg, 14, nsc, 2); noise_vars (ntx, 4)."""
+        dev = torch.device("cuda", self.ctx.device)
+        arr, offs, total = make_pusch_demod_configs(demods, grid_index)
+        plan = PuschDemodulatorPlan(self.ctx, arr, self.grid_nof_prb, self.grid_nof_ports)
+        g = torch.from_numpy(np.ascontiguousarray(grids_u16, np.uint16).view(np.int32).reshape(-1).copy()).to(dev)
+        h = torch.from_numpy(np.ascontiguousarray(ch_est_u16, np.uint16).view(np.int32).reshape(-1).copy()).to(dev)
+        nv = torch.from_numpy(np.ascontiguousarray(noise_vars, np.float32).reshape(-1).copy()).to(dev)
+        out = torch.full((max(total, 4),), 77, dtype=torch.int8, device=dev)
+        plan.execute(g, h, nv, out)
+        torch.cuda.synchronize(dev)
+        n = [plan.nof_llrs(i) for i in range(len(demods))]
+        plan.close()
+        o = out.cpu().numpy()
+        return [o[a:a + k] for a, k in zip(offs, n)]
 
 
 class OfdmPlan:

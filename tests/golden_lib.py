@@ -111,3 +111,27 @@ def ofdm_cases():
         c = int(d[f"case{i}_params"][0])
         yield CASES[c], d[f"case{i}_grid"], d[f"case{i}_samples"], d[f"case{i}_demod"]
         i += 1
+
+
+PUSCH_DEMOD_KEYS = ["rnti", "n_id", "qm", "nof_layers", "nof_rx_ports", "start_symbol", "nof_symbols",
+                    "dmrs_symbol_mask", "dmrs_type2", "nof_cdm_groups_without_data", "rb_start", "nof_rb"]
+
+
+def pusch_demod_cases():
+    """Yields (cfg dict, mmse flag, grid (P, 14, 288, 2) bf16, ch_est (L, P, 14, 288, 2) bf16, noise_var (P,),
+    reference LLRs) made by the reference's pusch_demodulator_impl (24-PRB grids)."""
+    d = _load("pusch_demod.npz")
+    i = 0
+    while f"case{i}_cfg" in d:
+        row = d[f"case{i}_cfg"]
+        cfg = {k: int(v) for k, v in zip(PUSCH_DEMOD_KEYS, row[:-1])}
+        yield (cfg, bool(row[-1]), d[f"case{i}_grid"], d[f"case{i}_ch_est"], d[f"case{i}_noise_var"],
+               d[f"case{i}_llr"])
+        i += 1
+
+
+def demapper_cases():
+    """Yields (qm, symbols complex64, noise variances, reference LLRs) made by demodulation_mapper_impl."""
+    d = _load("pusch_demod.npz")
+    for qm in (2, 4, 6, 8):
+        yield qm, d[f"demap{qm}_symbols"], d[f"demap{qm}_noise_var"], d[f"demap{qm}_llr"]

@@ -138,6 +138,32 @@ class Reference(_Lib):
     def has_avx512(self):
         return bool(self.lib.ref_cpu_has_avx512())
 
+    def demodulate_soft(self, qm, symbols, noise_vars):
+        """demodulation_mapper_impl::demodulate_soft: complex symbols + noise variances -> int8 LLRs."""
+        x = np.ascontiguousarray(symbols, dtype=np.complex64)
+        nv = np.ascontiguousarray(noise_vars, dtype=np.float32)
+        out = np.zeros(x.size * qm, np.int8)
+        f = self.lib.ref_demodulate_soft
+        f.restype = None
+        f.argtypes = [ctypes.c_int, _P, _P, ctypes.c_int, _P]
+        f(qm, _ptr(x), _ptr(nv), x.size, _ptr(out))
+        return out
+
+    def pusch_demodulate(self, cfg, grid_u16, ch_est_u16, noise_var, grid_nof_prb, mmse=False):
+        """pusch_demodulator_impl::demodulate of one transmission (see ref_pusch_demodulate): codeword LLRs."""
+        g = np.ascontiguousarray(grid_u16, dtype=np.uint16)
+        h = np.ascontiguousarray(ch_est_u16, dtype=np.uint16)
+        nv = np.ascontiguousarray(noise_var, dtype=np.float32)
+        cap = 12 * cfg["nof_rb"] * 14 * cfg["nof_layers"] * cfg["qm"]
+        out = np.zeros(cap, np.int8)
+        f = self.lib.ref_pusch_demodulate
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_int] * 7 + [ctypes.c_uint] + [ctypes.c_int] * 6 + [_P] * 4 + [ctypes.c_int]
+        n = f(cfg["rnti"], cfg["n_id"], cfg["qm"], cfg["nof_layers"], cfg["nof_rx_ports"], cfg["start_symbol"],
+              cfg["nof_symbols"], cfg["dmrs_symbol_mask"], cfg["dmrs_type2"], cfg["nof_cdm_groups_without_data"],
+              cfg["rb_start"], cfg["nof_rb"], grid_nof_prb, int(mmse), _ptr(g), _ptr(h), _ptr(nv), _ptr(out), cap)
+        return out[:n]
+
     def ofdm_slot_size(self, numerology, bw_rb, dft_size, extended, slot):
         return int(self.lib.ref_ofdm_slot_size(numerology, bw_rb, dft_size, int(extended), slot))
 

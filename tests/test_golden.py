@@ -82,3 +82,20 @@ def test_ofdm_golden():
         assert ok and frac < 0.02, frac
         n += 1
     assert n == 5
+
+
+def test_pusch_demod_golden():
+    """The numpy PUSCH demodulator / demapper restatement against the reference's LLRs (within one quantisation step
+    on a small fraction: the reference's AVX2 equalizer uses an approximate reciprocal)."""
+    import pusch_demod_oracle as D
+    from pusch_demod_cases import from_bf16
+    n = 0
+    for cfg, mmse, grid, H, nv, want in G.pusch_demod_cases():
+        got = D.demodulate(cfg, from_bf16(grid), from_bf16(H), nv, mmse).astype(np.int16)
+        d = np.abs(got - want.astype(np.int16))
+        assert got.size == want.size and d.max() <= 1 and np.mean(d > 0) < 0.05, (cfg, d.max(), np.mean(d > 0))
+        n += 1
+    assert n == 9
+    for qm, x, nv, want in G.demapper_cases():
+        d = np.abs(D.demap(x, nv, qm).astype(np.int16) - want.astype(np.int16))
+        assert d.max() <= 1 and np.mean(d > 0) < 0.01, qm

@@ -14,6 +14,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "srsran-5g_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 from oracle_lib import BG_K, BG_N_SHORT, CRC16, CRC24A, CRC24B, CRC_LEN, Reference  # noqa: E402
 
@@ -187,12 +188,40 @@ def gen_ofdm(ref, rng):
     np.savez_compressed(os.path.join(OUT, "ofdm.npz"), **out)
 
 
+def gen_pusch_demod(ref, rng):
+    """Reference PUSCH demodulator LLRs (pusch_demodulator_impl, generic equalizer ZF / MMSE, SIMD demapper) of random
+    transmissions in 24-PRB grids, and reference demapper LLRs of random symbols for every modulation."""
+    from pusch_demod_cases import random_case
+    out = {}
+    specs = [(1, 1, 2), (1, 2, 4), (1, 4, 6), (1, 3, 8), (2, 2, 8), (2, 4, 6), (2, 2, 4), (2, 4, 2), (1, 4, 8)]
+    for i, (L, P, qm) in enumerate(specs):
+        cfg, grid, H, nv = random_case(rng, 24, nof_layers=L, nof_rx_ports=P, qm=qm)
+        mmse = i == 8
+        llr = ref.pusch_demodulate(cfg, grid, H, nv, 24, mmse)
+        out[f"case{i}_cfg"] = np.array([cfg[k] for k in PUSCH_DEMOD_KEYS] + [int(mmse)], np.int64)
+        out[f"case{i}_grid"], out[f"case{i}_ch_est"], out[f"case{i}_noise_var"] = grid, H, nv
+        out[f"case{i}_llr"] = llr
+    for qm in (2, 4, 6, 8):
+        n = 4000
+        x = (rng.uniform(-1.5, 1.5, n) + 1j * rng.uniform(-1.5, 1.5, n)).astype(np.complex64)
+        x[::97] = 0
+        nvar = rng.uniform(0.001, 0.5, n).astype(np.float32)
+        nvar[::89] = 0
+        out[f"demap{qm}_symbols"], out[f"demap{qm}_noise_var"] = x, nvar
+        out[f"demap{qm}_llr"] = ref.demodulate_soft(qm, x, nvar)
+    np.savez_compressed(os.path.join(OUT, "pusch_demod.npz"), **out)
+
+
+PUSCH_DEMOD_KEYS = ["rnti", "n_id", "qm", "nof_layers", "nof_rx_ports", "start_symbol", "nof_symbols",
+                    "dmrs_symbol_mask", "dmrs_type2", "nof_cdm_groups_without_data", "rb_start", "nof_rb"]
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     ref = Reference()
     if len(sys.argv) > 1:  # regenerate only the named fixture sets, e.g. `python tools/gen_golden.py ofdm`
         for name in sys.argv[1:]:
-            seed = {"ofdm": 16}[name]
+            seed = {"ofdm": 16, "pusch_demod": 17}[name]
             globals()["gen_" + name](ref, np.random.default_rng(seed))
         return
     gen_crc(ref, np.random.default_rng(10))
@@ -202,6 +231,7 @@ def main():
     gen_pdsch_encoder(ref, np.random.default_rng(14))
     gen_pdsch_modulator(ref, np.random.default_rng(15))
     gen_ofdm(ref, np.random.default_rng(16))
+    gen_pusch_demod(ref, np.random.default_rng(17))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

@@ -332,6 +332,60 @@ void srsgpu_ofdm_plan_destroy(srsgpu_ofdm_plan* plan);
  * channel estimates per slot [layer 0..3][port][symbol][subcarrier] bf16 pairs (srsran::channel_estimate's path-major
  * layout, channel_estimation.h:310); noise variances d_noise_var[4 * tx + port] (channel_estimate::get_noise_variance).
  * ------------------------------------------------------------------------------------------------------------------ */
+/* ------------------------------------------------------------------------------------------------------------------
+ * PUSCH DM-RS channel estimator — replaces srsran::dmrs_pusch_estimator::estimate(channel_estimate& estimate,
+ * const resource_grid_reader& grid, const configuration& config)
+ * (include/srsran/phy/upper/signal_processors/dmrs_pusch_estimator.h, lib/phy/upper/signal_processors/
+ * dmrs_pusch_estimator_impl.cpp:28, port_channel_estimator_average_impl.cpp:77) for every PUSCH transmission of a
+ * batch of slots, pseudo-random DM-RS sequence, "average" time-domain strategy (the default) and the none / mean /
+ * filter (default) frequency-domain smoothing. Outputs per transmission and rx port: the channel estimate of every RE
+ * of the allocation in the layout the demodulator reads, the noise variance (d_noise_var[4 * tx + port]) and, when
+ * d_metrics is not NULL, (RSRP, EPRE, noise variance, SNR) at d_metrics[4 * (4 * tx + port)]. Time alignment and CFO
+ * are not estimated. One layer is the reference's scope (port_channel_estimator_average_impl.cpp:83 asserts it); 2..4
+ * layers (ports 1000..1003) are an extension: the w_f cover code is removed over adjacent pilot pairs.
+ * ------------------------------------------------------------------------------------------------------------------ */
+#define SRSGPU_CHEST_FD_NONE 0
+#define SRSGPU_CHEST_FD_MEAN 1
+#define SRSGPU_CHEST_FD_FILTER 2
+
+typedef struct {
+  uint16_t scrambling_id;    /* N_ID^{n_SCID}, 0..65535 */
+  uint8_t  n_scid;           /* 0 or 1 */
+  uint8_t  dmrs_type;        /* 1 or 2 */
+  uint8_t  nof_tx_layers;    /* 1..4 */
+  uint8_t  nof_rx_ports;     /* ports 0..n-1 of the grid */
+  uint8_t  start_symbol;     /* first_symbol */
+  uint8_t  nof_symbols;      /* start_symbol + nof_symbols <= 14 */
+  uint16_t dmrs_symbol_mask; /* symbols_mask: DM-RS symbols, inside [start_symbol, start_symbol + nof_symbols) */
+  uint16_t rb_start;         /* contiguous CRB allocation (rb_mask) */
+  uint16_t nof_rb;
+  uint16_t slot_index;       /* n_slot within the frame (DM-RS c_init) */
+  uint8_t  fd_smoothing;     /* SRSGPU_CHEST_FD_* */
+  uint8_t  pad[3];
+  float    scaling;          /* beta_PUSCH^DMRS (DM-RS amplitude relative to data), > 0 */
+  uint32_t grid_index;       /* slot of the rx grid and of the estimate buffer */
+} srsgpu_pusch_chest_config;
+
+typedef struct srsgpu_pusch_chest_plan srsgpu_pusch_chest_plan;
+
+int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
+                                   const srsgpu_pusch_chest_config* cfgs,
+                                   uint32_t                         nof_tx,
+                                   uint32_t                         grid_nof_prb,
+                                   uint32_t                         grid_nof_ports,
+                                   srsgpu_pusch_chest_plan**        plan);
+
+/** Estimates every planned transmission: reads d_grids, writes d_ch_estimates (slot layout [layer 0..3][port]
+ *  [symbol][subcarrier], only the allocated REs), d_noise_var and optionally d_metrics. Asynchronous on `stream`. */
+int srsgpu_pusch_chest_plan_execute(const srsgpu_pusch_chest_plan* plan,
+                                    const uint32_t*                d_grids,
+                                    uint32_t*                      d_ch_estimates,
+                                    float*                         d_noise_var,
+                                    float*                         d_metrics,
+                                    void*                          stream);
+
+void srsgpu_pusch_chest_plan_destroy(srsgpu_pusch_chest_plan* plan);
+
 #define SRSGPU_EQ_ZF 0
 #define SRSGPU_EQ_MMSE 1
 

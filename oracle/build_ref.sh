@@ -65,6 +65,20 @@ SRCS=(
   "$REF/lib/phy/upper/channel_modulation/demodulation_mapper_qam64.cpp:-mavx2 -mfma"
   "$REF/lib/phy/upper/channel_modulation/demodulation_mapper_qam256.cpp:-mavx2 -mfma"
   "$HERE/ref/ref_pusch_demod.cpp:-mavx2 -mfma -I$REF"
+  "$REF/lib/phy/upper/signal_processors/dmrs_pusch_estimator_impl.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/upper/signal_processors/dmrs_helper.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/upper/signal_processors/port_channel_estimator_average_impl.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/upper/signal_processors/port_channel_estimator_helpers.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/support/interpolator/interpolator_linear_impl.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/support/time_alignment_estimator/time_alignment_estimator_dft_impl.cpp:-mavx2 -mfma"
+  "$REF/lib/phy/upper/sequence_generators/low_papr_sequence_generator_impl.cpp:-mavx2 -mfma"
+  "$REF/lib/srsvec/convolution.cpp:-mavx2 -mfma"
+  "$REF/lib/srsvec/unwrap.cpp:-mavx2 -mfma"
+  "$REF/lib/srsvec/add.cpp:-mavx2 -mfma"
+  "$REF/lib/srsvec/subtract.cpp:-mavx2 -mfma"
+  "$REF/lib/srsvec/modulus_square.cpp:-mavx2 -mfma"
+  "$REF/lib/support/math_utils.cpp:-mavx2 -mfma"
+  "$HERE/ref/ref_pusch_chest.cpp:-mavx2 -mfma -I$REF"
 )
 OBJS=()
 pids=()

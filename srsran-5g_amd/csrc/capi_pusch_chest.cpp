@@ -1,0 +1,193 @@
+// Host side of the PUSCH DM-RS channel estimator C ABI (include/srsgpu_phy.h): validation, the per-symbol DM-RS
+// sequence initial states (dmrs_pusch_estimator_impl.cpp:69), the resampled raised-cosine smoothing filter
+// (port_channel_estimator_helpers.cpp filter_type, taps generated from the raised-cosine formula) and one job per
+// (transmission, rx port, CDM group).
+#include "capi_internal.h"
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+using namespace srsgpu;
+
+static_assert(sizeof(srsgpu_pusch_chest_config) == 28, "srsgpu_pusch_chest_config layout (mirrored by srsgpu)");
+
+struct srsgpu_pusch_chest_plan {
+  srsgpu_context* ctx      = nullptr;
+  chest_job*      d_jobs   = nullptr;
+  int             nof_jobs = 0;
+};
+
+namespace {
+
+/// Raised cosine, roll-off 0.2, 10 samples per symbol, n = 0..30 (t = (n - 15) / 10); the global scale is irrelevant
+/// (the estimator renormalises the taps it uses).
+double rc_tap(int n)
+{
+  const double t    = (n - 15) / 10.0;
+  const double beta = 0.2;
+  const double pi   = 3.14159265358979323846;
+  if (std::abs(std::abs(2 * beta * t) - 1.0) < 1e-12) {
+    const double x = 1 / (2 * beta);
+    return pi / 4 * std::sin(pi * x) / (pi * x);
+  }
+  const double sinc = (t == 0) ? 1.0 : std::sin(pi * t) / (pi * t);
+  return sinc * std::cos(pi * beta * t) / (1 - (2 * beta * t) * (2 * beta * t));
+}
+
+} // namespace
+
+extern "C" {
+
+int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
+                                   const srsgpu_pusch_chest_config* cfgs,
+                                   uint32_t                         nof_tx,
+                                   uint32_t                         grid_nof_prb,
+                                   uint32_t                         grid_nof_ports,
+                                   srsgpu_pusch_chest_plan**        plan_out)
+{
+  if (ctx == nullptr || plan_out == nullptr || (cfgs == nullptr && nof_tx > 0)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  if (grid_nof_prb == 0 || grid_nof_prb > 275 || grid_nof_ports == 0 || grid_nof_ports > 4) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "invalid grid geometry (%u PRB, %u ports)", grid_nof_prb, grid_nof_ports);
+  }
+  const uint32_t         nsc        = 12u * grid_nof_prb;
+  const uint64_t         slot_elems = static_cast<uint64_t>(grid_nof_ports) * 14u * nsc;
+  std::vector<chest_job> jobs;
+  for (uint32_t t = 0; t < nof_tx; ++t) {
+    const srsgpu_pusch_chest_config& c = cfgs[t];
+    const unsigned                   L = c.nof_tx_layers, P = c.nof_rx_ports;
+    if (L < 1 || L > 4 || P < 1 || P > grid_nof_ports || (c.dmrs_type != 1 && c.dmrs_type != 2) || c.n_scid > 1) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid layers / ports / DM-RS type", t);
+    }
+    if (c.nof_symbols < 1 || c.start_symbol + c.nof_symbols > 14 || c.nof_rb < 1 ||
+        c.rb_start + c.nof_rb > grid_nof_prb || !(c.scaling > 0.f) || c.fd_smoothing > SRSGPU_CHEST_FD_FILTER) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid allocation, scaling or smoothing strategy", t);
+    }
+    std::vector<unsigned> dmrs;
+    for (unsigned l = 0; l < 14; ++l) {
+      if ((c.dmrs_symbol_mask >> l) & 1u) {
+        if (l < c.start_symbol || l >= static_cast<unsigned>(c.start_symbol + c.nof_symbols)) {
+          return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: DM-RS symbol %u outside the allocation", t, l);
+        }
+        dmrs.push_back(l);
+      }
+    }
+    if (dmrs.empty()) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: no DM-RS symbols", t);
+    }
+    if ((static_cast<uint64_t>(c.grid_index) + 1) * slot_elems * 4u >= (1ull << 32)) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: grid index beyond 32-bit element offsets", t);
+    }
+    const bool     t2     = c.dmrs_type == 2;
+    const unsigned per_rb = t2 ? 4 : 6;
+    const unsigned stride = t2 ? 1 : 2;  // configure_interpolator of the group's RE pattern
+    // Smoothing filter (filter_type): min(nof_rb, 3) RBs of the 31-tap prototype resampled at the pilot stride.
+    const unsigned nrb3  = std::min<unsigned>(c.nof_rb, 3);
+    const unsigned half  = (nrb3 * 10 + 1) / 2 / stride;
+    const unsigned first = 15 - half * stride;
+    const unsigned ntaps = 2 * half + 1;
+    float          taps[32] = {};
+    float          total    = 0;
+    for (unsigned i = 0; i < ntaps; ++i) {
+      taps[i] = static_cast<float>(rc_tap(static_cast<int>(first + i * stride)));
+      total += taps[i];
+    }
+    const float rcp_total = 1 / total;
+    for (unsigned i = 0; i < ntaps; ++i) {
+      taps[i] *= rcp_total;
+    }
+    unsigned nof_v = std::min<unsigned>(12, ntaps / 2);
+    if (c.nof_rb == 1) {
+      nof_v = per_rb;
+    }
+    const unsigned ngroups = (L + 1) / 2;
+    for (unsigned p = 0; p < P; ++p) {
+      for (unsigned g = 0; g < ngroups; ++g) {
+        chest_job jb{};
+        jb.grid_base       = static_cast<uint32_t>(c.grid_index * slot_elems) + p * 14u * nsc + c.rb_start * 12u;
+        jb.ce_layer_stride = static_cast<uint32_t>(slot_elems);
+        jb.ce_base = static_cast<uint32_t>(c.grid_index * slot_elems * 4u + 2u * g * slot_elems) + p * 14u * nsc +
+                     c.rb_start * 12u;
+        jb.nsc        = nsc;
+        jb.seq_offset = c.rb_start * per_rb;
+        for (size_t s = 0; s < dmrs.size(); ++s) {
+          // c_init = ((14 n_slot + l + 1)(2 N_ID + 1) 2^17 + 2 N_ID + n_SCID) mod 2^31 (dmrs_pusch_estimator_impl.cpp:83)
+          const uint64_t nid = c.scrambling_id;
+          jb.c_init[s]       = static_cast<uint32_t>(
+              ((14ull * c.slot_index + dmrs[s] + 1) * (2 * nid + 1) * (1ull << 17) + 2 * nid + c.n_scid) % (1ull << 31));
+          jb.dmrs_symbols[s] = static_cast<uint8_t>(dmrs[s]);
+        }
+        jb.pattern = 0;
+        for (unsigned j = 0; j < per_rb; ++j) {
+          const unsigned k = t2 ? (2 * g + (j & 1) + 6 * (j >> 1)) : (g + 2 * j);
+          jb.pattern |= k << (4 * j);
+        }
+        jb.noise_slot    = 4 * t + p;
+        jb.beta          = c.scaling;
+        std::copy(taps, taps + 32, jb.taps);
+        jb.nof_pilots    = static_cast<uint16_t>(c.nof_rb * per_rb);
+        jb.nof_rb        = c.nof_rb;
+        jb.nof_dmrs      = static_cast<uint8_t>(dmrs.size());
+        jb.group_layers  = static_cast<uint8_t>(std::min<unsigned>(2, L - 2 * g));
+        jb.group         = static_cast<uint8_t>(g);
+        jb.pilots_per_rb = static_cast<uint8_t>(per_rb);
+        jb.fd            = c.fd_smoothing;
+        jb.ntaps         = static_cast<uint8_t>(ntaps);
+        jb.nof_v_pilots  = static_cast<uint8_t>(nof_v);
+        jb.interp_offset = static_cast<uint8_t>(t2 ? 2 * g : g);
+        jb.interp_stride = static_cast<uint8_t>(stride);
+        jb.first_symbol  = c.start_symbol;
+        jb.nof_symbols   = c.nof_symbols;
+        jobs.push_back(jb);
+      }
+    }
+  }
+  std::lock_guard<std::mutex> lock(ctx->mtx);
+  HIP_TRY(hipSetDevice(ctx->device));
+  int r = ensure_gold_tables(ctx);
+  if (r != SRSGPU_OK) {
+    return r;
+  }
+  auto* plan     = new srsgpu_pusch_chest_plan();
+  plan->ctx      = ctx;
+  plan->nof_jobs = static_cast<int>(jobs.size());
+  if (!jobs.empty() && (hipMalloc(&plan->d_jobs, jobs.size() * sizeof(chest_job)) != hipSuccess ||
+                        hipMemcpy(plan->d_jobs, jobs.data(), jobs.size() * sizeof(chest_job), hipMemcpyHostToDevice) !=
+                            hipSuccess)) {
+    srsgpu_pusch_chest_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload channel estimation jobs");
+  }
+  *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+int srsgpu_pusch_chest_plan_execute(const srsgpu_pusch_chest_plan* plan,
+                                    const uint32_t*                d_grids,
+                                    uint32_t*                      d_ch_estimates,
+                                    float*                         d_noise_var,
+                                    float*                         d_metrics,
+                                    void*                          stream)
+{
+  if (plan == nullptr || d_grids == nullptr || d_ch_estimates == nullptr || d_noise_var == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  launch_pusch_chest(plan->d_jobs, plan->nof_jobs, d_grids, d_ch_estimates, d_noise_var, d_metrics,
+                     plan->ctx->d_gold_x1, plan->ctx->d_gold_x2_jump, plan->ctx->d_gold_x2_lane,
+                     static_cast<hipStream_t>(stream));
+  HIP_TRY(hipGetLastError());
+  return SRSGPU_OK;
+}
+
+void srsgpu_pusch_chest_plan_destroy(srsgpu_pusch_chest_plan* plan)
+{
+  if (plan == nullptr) {
+    return;
+  }
+  if (plan->d_jobs != nullptr) {
+    (void)hipFree(plan->d_jobs);
+  }
+  delete plan;
+}
+
+} // extern "C"

@@ -287,6 +287,50 @@ struct demap_pair_table {
 };
 constexpr int DEMAP_TABLES = 7;
 
+/// PUSCH channel estimator job (pusch_chest.hip): one (transmission, rx port, DM-RS CDM group).
+struct chest_job {
+  uint32_t grid_base;        ///< Element of (port, symbol 0, first allocated subcarrier) in the rx grids.
+  uint32_t ce_base;          ///< Element of (first layer of the group, port, symbol 0, first allocated subcarrier).
+  uint32_t ce_layer_stride;  ///< Elements per layer of a slot's estimates.
+  uint32_t nsc;              ///< Subcarriers per OFDM symbol.
+  uint32_t seq_offset;       ///< DM-RS sequence index of the first pilot (rb_start x pilots per RB; point A = 0).
+  uint32_t c_init[14];       ///< DM-RS sequence initial state of each DM-RS symbol (order of dmrs_symbols).
+  uint32_t pattern;          ///< Pilot subcarriers within a PRB (4 bits each, ascending).
+  uint32_t noise_slot;       ///< 4 * tx + port: noise variance / metrics slot.
+  float    beta;             ///< DM-RS to data amplitude scaling.
+  float    taps[32];         ///< Normalised smoothing filter taps (CHEST_FD_FILTER).
+  uint16_t nof_pilots;       ///< Pilots per DM-RS symbol.
+  uint16_t nof_rb;           ///< Allocated RBs (contiguous).
+  uint8_t  dmrs_symbols[14]; ///< OFDM symbols carrying DM-RS.
+  uint8_t  nof_dmrs;         ///< Number of DM-RS symbols.
+  uint8_t  group_layers;     ///< Layers of this CDM group (1 or 2).
+  uint8_t  group;            ///< CDM group (0: ports 1000/1001, 1: ports 1002/1003).
+  uint8_t  pilots_per_rb;    ///< 6 (type 1) or 4 (type 2).
+  uint8_t  fd;               ///< CHEST_FD_* smoothing strategy.
+  uint8_t  ntaps;            ///< Filter length (odd).
+  uint8_t  nof_v_pilots;     ///< Virtual pilots on each side.
+  uint8_t  interp_offset;    ///< Interpolator offset (first pilot subcarrier of a PRB).
+  uint8_t  interp_stride;    ///< Interpolator stride.
+  uint8_t  first_symbol;     ///< First allocated OFDM symbol.
+  uint8_t  nof_symbols;      ///< Allocated OFDM symbols.
+  uint8_t  pad[3];
+};
+
+constexpr uint8_t CHEST_FD_NONE   = 0;
+constexpr uint8_t CHEST_FD_MEAN   = 1;
+constexpr uint8_t CHEST_FD_FILTER = 2;
+
+void launch_pusch_chest(const chest_job* d_jobs,
+                        int              nof_jobs,
+                        const uint32_t*  d_grids,
+                        uint32_t*        d_ce,
+                        float*           d_noise_var,
+                        float*           d_metrics,
+                        const uint32_t*  d_x1,
+                        const uint32_t*  d_x2_jump,
+                        const uint32_t*  d_x2_lane,
+                        hipStream_t      stream);
+
 void launch_pusch_demodulate(const demod_desc*        d_desc,
                              const mod_chunk*         d_chunks,
                              int                      nof_chunks,

@@ -181,6 +181,31 @@ class PuschDemodConfig(ctypes.Structure):
 
 
 assert ctypes.sizeof(PuschDemodConfig) == 28
+
+
+class PuschChestConfig(ctypes.Structure):
+    """srsgpu_pusch_chest_config (include/srsgpu_phy.h): dmrs_pusch_estimator::configuration of one transmission."""
+    _fields_ = [
+        ("scrambling_id", ctypes.c_uint16),
+        ("n_scid", ctypes.c_uint8),
+        ("dmrs_type", ctypes.c_uint8),
+        ("nof_tx_layers", ctypes.c_uint8),
+        ("nof_rx_ports", ctypes.c_uint8),
+        ("start_symbol", ctypes.c_uint8),
+        ("nof_symbols", ctypes.c_uint8),
+        ("dmrs_symbol_mask", ctypes.c_uint16),
+        ("rb_start", ctypes.c_uint16),
+        ("nof_rb", ctypes.c_uint16),
+        ("slot_index", ctypes.c_uint16),
+        ("fd_smoothing", ctypes.c_uint8),
+        ("pad", ctypes.c_uint8 * 3),
+        ("scaling", ctypes.c_float),
+        ("grid_index", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(PuschChestConfig) == 28
+CHEST_FD_NONE, CHEST_FD_MEAN, CHEST_FD_FILTER = 0, 1, 2
 EQ_ZF, EQ_MMSE = 0, 1
 
 
@@ -244,6 +269,11 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pdsch_modulator_plan_execute.argtypes = [P, P, P, P]
     lib.srsgpu_pdsch_modulator_plan_destroy.argtypes = [P]
     lib.srsgpu_pdsch_modulator_plan_destroy.restype = None
+    lib.srsgpu_pusch_chest_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                   ctypes.POINTER(P)]
+    lib.srsgpu_pusch_chest_plan_execute.argtypes = [P, P, P, P, P, P]
+    lib.srsgpu_pusch_chest_plan_destroy.argtypes = [P]
+    lib.srsgpu_pusch_chest_plan_destroy.restype = None
     lib.srsgpu_pusch_demodulator_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                          ctypes.POINTER(P)]
     lib.srsgpu_pusch_demodulator_plan_nof_llrs.argtypes = [P, ctypes.c_uint32]
@@ -285,6 +315,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
+    "srsgpu_pusch_chest_plan_create", "srsgpu_pusch_chest_plan_execute", "srsgpu_pusch_chest_plan_destroy",
 ]
 
 
@@ -856,6 +887,89 @@ class PuschDemodulator:
         plan.close()
         o = out.cpu().numpy()
         return [o[a:a + k] for a, k in zip(offs, n)]
+
+
+@dataclass
+class PuschChannelEstimation:
+    """dmrs_pusch_estimator::configuration (dmrs_pusch_estimator.h:63): pseudo-random DM-RS, contiguous CRB
+    allocation, rx ports 0..nof_rx_ports-1, "average" time-domain strategy."""
+    scrambling_id: int
+    n_scid: int
+    dmrs_type: int
+    nof_tx_layers: int
+    nof_rx_ports: int
+    start_symbol: int
+    nof_symbols: int
+    dmrs_symbol_mask: int
+    rb_start: int
+    nof_rb: int
+    slot_index: int
+    scaling: float = 1.0
+    fd_smoothing: int = CHEST_FD_FILTER
+
+
+def make_pusch_chest_configs(ests: Sequence[PuschChannelEstimation], grid_index: Sequence[int]):
+    arr = (PuschChestConfig * len(ests))()
+    for i, (e, g) in enumerate(zip(ests, grid_index)):
+        a = arr[i]
+        a.scrambling_id, a.n_scid, a.dmrs_type, a.nof_tx_layers = e.scrambling_id, e.n_scid, e.dmrs_type, e.nof_tx_layers
+        a.nof_rx_ports, a.start_symbol, a.nof_symbols = e.nof_rx_ports, e.start_symbol, e.nof_symbols
+        a.dmrs_symbol_mask, a.rb_start, a.nof_rb, a.slot_index = e.dmrs_symbol_mask, e.rb_start, e.nof_rb, e.slot_index
+        a.fd_smoothing, a.scaling, a.grid_index = e.fd_smoothing, e.scaling, g
+    return arr
+
+
+class PuschChannelEstimatorPlan:
+    """srsgpu_pusch_chest_plan: DM-RS channel estimation of a batch of PUSCH transmissions from rx grids
+    (S, Pg, 14, nsc) into estimates (S, 4, Pg, 14, nsc) (uint32 bf16 pairs), noise variances (ntx, 4) and optional
+    metrics (ntx, 4, [RSRP, EPRE, noise variance, SNR])."""
+
+    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        _check(_lib.srsgpu_pusch_chest_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                   len(cfg_array), grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
+        self.handle = h
+
+    def execute(self, d_grids, d_ch_est, d_noise_var, d_metrics=None, stream=None):
+        _check(_lib.srsgpu_pusch_chest_plan_execute(self.handle, _dptr(d_grids), _dptr(d_ch_est), _dptr(d_noise_var),
+                                                    _dptr(d_metrics), _stream_handle(stream)))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.srsgpu_pusch_chest_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class PuschChannelEstimator:
+    """GPU counterpart of srsran::dmrs_pusch_estimator::estimate (dmrs_pusch_estimator_impl.cpp:28)."""
+
+    def __init__(self, ctx: Context, grid_nof_prb: int, grid_nof_ports: int = 4):
+        self.ctx, self.grid_nof_prb, self.grid_nof_ports = ctx, grid_nof_prb, grid_nof_ports
+
+    def estimate_batch(self, grids_u16, ests: Sequence[PuschChannelEstimation], grid_index: Sequence[int]):
+        """grids_u16 (S, Pg, 14, nsc, 2) -> (estimates (S, 4, Pg, 14, nsc, 2) uint16, noise_var (ntx, 4),
+        metrics (ntx, 4, 4))."""
+        dev = torch.device("cuda", self.ctx.device)
+        plan = PuschChannelEstimatorPlan(self.ctx, make_pusch_chest_configs(ests, grid_index), self.grid_nof_prb,
+                                         self.grid_nof_ports)
+        g = np.ascontiguousarray(grids_u16, np.uint16)
+        S = g.shape[0]
+        d_g = torch.from_numpy(g.view(np.int32).reshape(-1).copy()).to(dev)
+        d_ce = torch.zeros(S * 4 * g.shape[1] * g.shape[2] * g.shape[3], dtype=torch.int32, device=dev)
+        d_nv = torch.zeros(4 * len(ests), dtype=torch.float32, device=dev)
+        d_m = torch.zeros(16 * len(ests), dtype=torch.float32, device=dev)
+        plan.execute(d_g, d_ce, d_nv, d_m)
+        torch.cuda.synchronize(dev)
+        plan.close()
+        ce = d_ce.cpu().numpy().view(np.uint16).reshape((S, 4) + g.shape[1:])
+        return ce, d_nv.cpu().numpy().reshape(-1, 4), d_m.cpu().numpy().reshape(-1, 4, 4)
 
 
 class OfdmPlan:

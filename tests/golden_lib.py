@@ -135,3 +135,21 @@ def demapper_cases():
     d = _load("pusch_demod.npz")
     for qm in (2, 4, 6, 8):
         yield qm, d[f"demap{qm}_symbols"], d[f"demap{qm}_noise_var"], d[f"demap{qm}_llr"]
+
+
+PUSCH_CHEST_KEYS = ["slot", "scrambling_id", "n_scid", "dmrs_type2", "dmrs_symbol_mask", "start_symbol", "nof_symbols",
+                    "rb_start", "nof_rb", "nof_rx_ports"]
+
+
+def pusch_chest_cases():
+    """Yields (cfg dict, fd strategy (0 none, 1 mean, 2 filter), grid (P, 14, 288, 2) bf16, reference estimates
+    (P, 14, 288, 2) bf16 (valid on the allocation only), [noise_var, rsrp, epre] (3, P)) made by
+    dmrs_pusch_estimator_impl."""
+    d = _load("pusch_chest.npz")
+    i = 0
+    while f"case{i}_cfg" in d:
+        row = d[f"case{i}_cfg"]
+        cfg = {k: int(v) for k, v in zip(PUSCH_CHEST_KEYS, row[:-1])}
+        cfg["scaling"] = float(d[f"case{i}_scaling"])
+        yield cfg, int(row[-1]), d[f"case{i}_grid"], d[f"case{i}_ch_est"], d[f"case{i}_stats"]
+        i += 1

@@ -99,3 +99,21 @@ def test_pusch_demod_golden():
     for qm, x, nv, want in G.demapper_cases():
         d = np.abs(D.demap(x, nv, qm).astype(np.int16) - want.astype(np.int16))
         assert d.max() <= 1 and np.mean(d > 0) < 0.01, qm
+
+
+def test_pusch_chest_golden():
+    """The numpy DM-RS channel estimator restatement against the reference's estimates (allocation only) and noise
+    variance / RSRP / EPRE."""
+    import pusch_chest_oracle as C
+    from ofdm_oracle import bf16_to_complex
+    n = 0
+    for cfg, fd, grid, ce, stats in G.pusch_chest_cases():
+        ch, nv, rsrp, epre, _ = C.estimate(cfg, bf16_to_complex(grid), ["none", "mean", "filter"][fd])
+        l0, l1 = cfg["start_symbol"], cfg["start_symbol"] + cfg["nof_symbols"]
+        k0, k1 = cfg["rb_start"] * 12, (cfg["rb_start"] + cfg["nof_rb"]) * 12
+        want = bf16_to_complex(ce)[:, l0:l1, k0:k1]
+        got = ch[:, l0:l1, k0:k1]
+        assert np.max(np.abs(got - want)) < 1e-2 * np.sqrt(np.mean(np.abs(want) ** 2))
+        np.testing.assert_allclose(np.stack([nv, rsrp, epre]), stats, rtol=1e-3)
+        n += 1
+    assert n == 8

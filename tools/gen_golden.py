@@ -212,6 +212,24 @@ def gen_pusch_demod(ref, rng):
     np.savez_compressed(os.path.join(OUT, "pusch_demod.npz"), **out)
 
 
+def gen_pusch_chest(ref, rng):
+    """Reference DM-RS channel estimates (dmrs_pusch_estimator_impl, filter / mean / none smoothing, average time
+    strategy) of random single-layer transmissions in 24-PRB grids (DM-RS type 1)."""
+    from pusch_chest_cases import random_case
+    out = {}
+    for i, (nrb, fd) in enumerate([(1, 2), (2, 2), (3, 2), (7, 2), (24, 2), (5, 1), (4, 0), (12, 2)]):
+        cfg, grid, _ = random_case(rng, 24, nof_rb=nrb, dmrs_type2=0)
+        ce, nv, rsrp, epre, ta, cfo = ref.pusch_chest(cfg, grid, 24, fd=fd)
+        out[f"case{i}_cfg"] = np.array([cfg[k] for k in PUSCH_CHEST_KEYS] + [fd], np.int64)
+        out[f"case{i}_scaling"] = np.float32(cfg["scaling"])
+        out[f"case{i}_grid"], out[f"case{i}_ch_est"] = grid, ce
+        out[f"case{i}_stats"] = np.stack([nv, rsrp, epre])
+    np.savez_compressed(os.path.join(OUT, "pusch_chest.npz"), **out)
+
+
+PUSCH_CHEST_KEYS = ["slot", "scrambling_id", "n_scid", "dmrs_type2", "dmrs_symbol_mask", "start_symbol", "nof_symbols",
+                    "rb_start", "nof_rb", "nof_rx_ports"]
+
 PUSCH_DEMOD_KEYS = ["rnti", "n_id", "qm", "nof_layers", "nof_rx_ports", "start_symbol", "nof_symbols",
                     "dmrs_symbol_mask", "dmrs_type2", "nof_cdm_groups_without_data", "rb_start", "nof_rb"]
 
@@ -221,7 +239,7 @@ def main():
     ref = Reference()
     if len(sys.argv) > 1:  # regenerate only the named fixture sets, e.g. `python tools/gen_golden.py ofdm`
         for name in sys.argv[1:]:
-            seed = {"ofdm": 16, "pusch_demod": 17}[name]
+            seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18}[name]
             globals()["gen_" + name](ref, np.random.default_rng(seed))
         return
     gen_crc(ref, np.random.default_rng(10))
@@ -232,6 +250,7 @@ def main():
     gen_pdsch_modulator(ref, np.random.default_rng(15))
     gen_ofdm(ref, np.random.default_rng(16))
     gen_pusch_demod(ref, np.random.default_rng(17))
+    gen_pusch_chest(ref, np.random.default_rng(18))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

@@ -256,6 +256,43 @@ int srsgpu_pdsch_modulator_plan_execute(const srsgpu_pdsch_modulator_plan* plan,
 void srsgpu_pdsch_modulator_plan_destroy(srsgpu_pdsch_modulator_plan* plan);
 
 /* ------------------------------------------------------------------------------------------------------------------
+ * PDSCH DM-RS — replaces srsran::dmrs_pdsch_processor::map(resource_grid_writer& grid, const config_t& config)
+ * (include/srsran/phy/upper/signal_processors/dmrs_pdsch_processor.h:65, lib/phy/upper/signal_processors/
+ * dmrs_pdsch_processor_impl.cpp:117) for every PDSCH transmission of a batch of slots: DM-RS sequence per symbol
+ * (c_init = ((14 n_slot + l + 1)(2 N_ID + 1) 2^17 + 2 N_ID + n_SCID) mod 2^31), CDM cover codes of DM-RS ports
+ * 0..nof_layers-1, per-CDM-group wideband precoding and mapping (bf16, same grid layout as the PDSCH modulator).
+ * ------------------------------------------------------------------------------------------------------------------ */
+typedef struct {
+  uint16_t slot_index;           /* n_slot within the frame */
+  uint16_t scrambling_id;        /* N_ID^{n_SCID} */
+  uint8_t  n_scid;               /* 0 or 1 */
+  uint8_t  dmrs_type;            /* 1 or 2 */
+  uint8_t  nof_layers;           /* DM-RS ports 0..nof_layers-1 (1..4) */
+  uint8_t  nof_ports;            /* antenna ports (precoding), nof_layers..grid_nof_ports */
+  uint16_t dmrs_symbol_mask;     /* symbols_mask */
+  uint16_t reference_point_k_rb; /* sequence reference RB (0: point A) */
+  uint16_t rb_start;             /* contiguous CRB allocation (rb_mask), rb_start >= reference_point_k_rb */
+  uint16_t nof_rb;
+  float    amplitude;            /* DM-RS amplitude (beta) */
+  float    precoding[4][4][2];   /* [port][layer] (re, im) */
+  uint32_t grid_index;
+} srsgpu_pdsch_dmrs_config;
+
+typedef struct srsgpu_pdsch_dmrs_plan srsgpu_pdsch_dmrs_plan;
+
+int srsgpu_pdsch_dmrs_plan_create(srsgpu_context*                 ctx,
+                                  const srsgpu_pdsch_dmrs_config* cfgs,
+                                  uint32_t                        nof_tx,
+                                  uint32_t                        grid_nof_prb,
+                                  uint32_t                        grid_nof_ports,
+                                  srsgpu_pdsch_dmrs_plan**        plan);
+
+/** Writes the DM-RS REs of every planned transmission into d_grids. Asynchronous on `stream`. */
+int srsgpu_pdsch_dmrs_plan_execute(const srsgpu_pdsch_dmrs_plan* plan, uint32_t* d_grids, void* stream);
+
+void srsgpu_pdsch_dmrs_plan_destroy(srsgpu_pdsch_dmrs_plan* plan);
+
+/* ------------------------------------------------------------------------------------------------------------------
  * OFDM slot modulator / demodulator — replace srsran::ofdm_slot_modulator::modulate(span<cf_t> output,
  * const resource_grid_reader& grid, unsigned port_index, unsigned slot_index)
  * (include/srsran/phy/lower/modulation/ofdm_modulator.h:100, lib/phy/lower/modulation/ofdm_modulator_impl.cpp:115,

@@ -79,6 +79,8 @@ SRCS=(
   "$REF/lib/srsvec/modulus_square.cpp:-mavx2 -mfma"
   "$REF/lib/support/math_utils.cpp:-mavx2 -mfma"
   "$HERE/ref/ref_pusch_chest.cpp:-mavx2 -mfma -I$REF"
+  "$REF/lib/phy/upper/signal_processors/dmrs_pdsch_processor_impl.cpp:-mavx2"
+  "$HERE/ref/ref_dmrs_pdsch.cpp:-mavx2 -I$REF"
 )
 OBJS=()
 pids=()

@@ -10,6 +10,14 @@ using namespace srsgpu;
 
 static_assert(sizeof(srsgpu_pdsch_mod_config) == 168, "srsgpu_pdsch_mod_config layout (mirrored by srsgpu.PdschModConfig)");
 
+static_assert(sizeof(srsgpu_pdsch_dmrs_config) == 152, "srsgpu_pdsch_dmrs_config layout (mirrored by srsgpu)");
+
+struct srsgpu_pdsch_dmrs_plan {
+  srsgpu_context* ctx      = nullptr;
+  dmrs_job*       d_jobs   = nullptr;
+  int             nof_jobs = 0;
+};
+
 struct srsgpu_pdsch_modulator_plan {
   srsgpu_context* ctx        = nullptr;
   mod_desc*       d_desc     = nullptr;
@@ -305,6 +313,97 @@ void srsgpu_pdsch_modulator_plan_destroy(srsgpu_pdsch_modulator_plan* plan)
     if (p != nullptr) {
       (void)hipFree(p);
     }
+  }
+  delete plan;
+}
+
+int srsgpu_pdsch_dmrs_plan_create(srsgpu_context*                 ctx,
+                                  const srsgpu_pdsch_dmrs_config* cfgs,
+                                  uint32_t                        nof_tx,
+                                  uint32_t                        grid_nof_prb,
+                                  uint32_t                        grid_nof_ports,
+                                  srsgpu_pdsch_dmrs_plan**        plan_out)
+{
+  if (ctx == nullptr || plan_out == nullptr || (cfgs == nullptr && nof_tx > 0)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  if (grid_nof_prb == 0 || grid_nof_prb > 275 || grid_nof_ports == 0 || grid_nof_ports > 4) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "invalid grid geometry (%u PRB, %u ports)", grid_nof_prb, grid_nof_ports);
+  }
+  const uint32_t        nsc = 12u * grid_nof_prb;
+  std::vector<dmrs_job> jobs;
+  for (uint32_t t = 0; t < nof_tx; ++t) {
+    const srsgpu_pdsch_dmrs_config& c = cfgs[t];
+    if (c.nof_layers < 1 || c.nof_layers > 4 || c.nof_ports < c.nof_layers || c.nof_ports > grid_nof_ports ||
+        (c.dmrs_type != 1 && c.dmrs_type != 2) || c.n_scid > 1 || c.nof_rb < 1 ||
+        c.rb_start + c.nof_rb > grid_nof_prb || c.rb_start < c.reference_point_k_rb || (c.dmrs_symbol_mask >> 14)) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid DM-RS configuration", t);
+    }
+    const uint32_t per_rb = c.dmrs_type == 2 ? 4 : 6;
+    for (unsigned l = 0; l < 14; ++l) {
+      if (((c.dmrs_symbol_mask >> l) & 1u) == 0) {
+        continue;
+      }
+      dmrs_job       jb{};
+      const uint64_t nid = c.scrambling_id;
+      jb.grid_base   = c.grid_index * grid_nof_ports * 14u * nsc + l * nsc + c.rb_start * 12u;
+      jb.port_stride = 14u * nsc;
+      jb.c_init      = static_cast<uint32_t>(
+          ((14ull * c.slot_index + l + 1) * (2 * nid + 1) * (1ull << 17) + 2 * nid + c.n_scid) % (1ull << 31));
+      jb.seq_offset = (c.rb_start - c.reference_point_k_rb) * per_rb;
+      jb.amp        = static_cast<float>(M_SQRT1_2) * c.amplitude;  // dmrs_pdsch_processor_impl.cpp:61
+      for (int p = 0; p < 4; ++p) {
+        for (int q = 0; q < 4; ++q) {
+          const bool used = p < c.nof_ports && q < c.nof_layers;
+          jb.w[p][q][0]   = used ? c.precoding[p][q][0] : 0.f;
+          jb.w[p][q][1]   = used ? c.precoding[p][q][1] : 0.f;
+        }
+      }
+      jb.nof_pilots = static_cast<uint16_t>(c.nof_rb * per_rb);
+      jb.type2      = c.dmrs_type == 2;
+      jb.L          = c.nof_layers;
+      jb.P          = c.nof_ports;
+      jb.lp         = (l > 0 && ((c.dmrs_symbol_mask >> (l - 1)) & 1u)) ? 1 : 0;
+      jobs.push_back(jb);
+    }
+  }
+  std::lock_guard<std::mutex> lock(ctx->mtx);
+  HIP_TRY(hipSetDevice(ctx->device));
+  int r = ensure_gold_tables(ctx);
+  if (r != SRSGPU_OK) {
+    return r;
+  }
+  auto* plan     = new srsgpu_pdsch_dmrs_plan();
+  plan->ctx      = ctx;
+  plan->nof_jobs = static_cast<int>(jobs.size());
+  if (!jobs.empty() && (hipMalloc(&plan->d_jobs, jobs.size() * sizeof(dmrs_job)) != hipSuccess ||
+                        hipMemcpy(plan->d_jobs, jobs.data(), jobs.size() * sizeof(dmrs_job), hipMemcpyHostToDevice) !=
+                            hipSuccess)) {
+    srsgpu_pdsch_dmrs_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload DM-RS jobs");
+  }
+  *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+int srsgpu_pdsch_dmrs_plan_execute(const srsgpu_pdsch_dmrs_plan* plan, uint32_t* d_grids, void* stream)
+{
+  if (plan == nullptr || d_grids == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  launch_pdsch_dmrs(plan->d_jobs, plan->nof_jobs, d_grids, plan->ctx->d_gold_x1, plan->ctx->d_gold_x2_jump,
+                    plan->ctx->d_gold_x2_lane, static_cast<hipStream_t>(stream));
+  HIP_TRY(hipGetLastError());
+  return SRSGPU_OK;
+}
+
+void srsgpu_pdsch_dmrs_plan_destroy(srsgpu_pdsch_dmrs_plan* plan)
+{
+  if (plan == nullptr) {
+    return;
+  }
+  if (plan->d_jobs != nullptr) {
+    (void)hipFree(plan->d_jobs);
   }
   delete plan;
 }

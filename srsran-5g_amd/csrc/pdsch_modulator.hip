@@ -147,7 +147,67 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
   }
 }
 
+/// PDSCH DM-RS (dmrs_pdsch_processor_impl.cpp:56 sequence, :80 cover codes, :117 per-CDM-group precoding and
+/// mapping): lane i owns DM-RS index i of the symbol in every CDM group. Same rounding as the modulator.
+__global__ __launch_bounds__(MOD_THREADS) void pdsch_dmrs_kernel(const dmrs_job* __restrict__ jobs,
+                                                                  uint32_t* __restrict__ grids,
+                                                                  const uint32_t* __restrict__ x1,
+                                                                  const uint32_t* __restrict__ x2_jump,
+                                                                  const uint32_t* __restrict__ x2_lane)
+{
+  const dmrs_job& jb     = jobs[blockIdx.x];
+  const uint32_t  per_rb = jb.type2 ? 4u : 6u;
+  for (uint32_t i = threadIdx.x; i < jb.nof_pilots; i += MOD_THREADS) {
+    const uint32_t n    = 2 * (jb.seq_offset + i);
+    const uint32_t w    = n >> 5;
+    const uint32_t word = gold_word(jb.c_init, w, w >> 6, x1, x2_jump, x2_lane);
+    const uint32_t sh   = 31u - (n & 31u);
+    const float    re   = ((word >> sh) & 1u) ? -jb.amp : jb.amp;
+    const float    im   = ((word >> (sh - 1)) & 1u) ? -jb.amp : jb.amp;
+    const uint32_t rb   = i / per_rb, j = i - rb * per_rb;
+    for (uint32_t g = 0; 2 * g < jb.L; ++g) {
+      // Subcarrier of DM-RS j of the RB in CDM group g (type 1: 2j + g; type 2: 6 (j / 2) + 2g + j % 2).
+      const uint32_t k = rb * 12u + (jb.type2 ? 6u * (j >> 1) + 2u * g + (j & 1u) : 2u * j + g);
+      // Cover codes: w_f = (+1, -1) for odd ports on odd indices; w_t = -1 for ports >= 4 when l' = 1 (none here:
+      // at most four layers, ports 0..3).
+      const float s1 = (i & 1u) ? -1.f : 1.f;
+      const uint32_t q0 = 2 * g, q1 = 2 * g + 1;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (p < static_cast<int>(jb.P)) {
+          const float wr0 = jb.w[p][q0][0], wi0 = jb.w[p][q0][1];
+          float       sr  = re * wr0 - im * wi0;
+          float       si  = re * wi0 + im * wr0;
+          if (q1 < jb.L) {
+            const float a = re * s1, b = im * s1;
+            const float wr1 = jb.w[p][q1][0], wi1 = jb.w[p][q1][1];
+            sr = sr + (a * wr1 - b * wi1);
+            si = si + (a * wi1 + b * wr1);
+          }
+          grids[jb.grid_base + static_cast<uint32_t>(p) * jb.port_stride + k] =
+              to_bf16_bits(sr) | (to_bf16_bits(si) << 16);
+        }
+      }
+    }
+  }
+}
+
 } // namespace
+
+void launch_pdsch_dmrs(const dmrs_job* d_jobs,
+                       int             nof_jobs,
+                       uint32_t*       d_grids,
+                       const uint32_t* d_x1,
+                       const uint32_t* d_x2_jump,
+                       const uint32_t* d_x2_lane,
+                       hipStream_t     stream)
+{
+  if (nof_jobs <= 0) {
+    return;
+  }
+  hipLaunchKernelGGL(pdsch_dmrs_kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(MOD_THREADS), 0, stream, d_jobs,
+                     d_grids, d_x1, d_x2_jump, d_x2_lane);
+}
 
 void launch_pdsch_modulate(const mod_desc*  d_desc,
                            const mod_chunk* d_chunks,

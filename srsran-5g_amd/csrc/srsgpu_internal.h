@@ -287,6 +287,29 @@ struct demap_pair_table {
 };
 constexpr int DEMAP_TABLES = 7;
 
+/// PDSCH DM-RS job (pdsch_modulator.hip): one DM-RS OFDM symbol of one transmission.
+struct dmrs_job {
+  uint32_t grid_base;    ///< Element of (port 0, DM-RS symbol, first allocated subcarrier) in the grids.
+  uint32_t port_stride;  ///< Elements per port of a grid.
+  uint32_t c_init;       ///< Sequence initial state of the symbol.
+  uint32_t seq_offset;   ///< Sequence index of the first allocated RB's first DM-RS ((rb_start - k_ref) x per RB).
+  float    amp;          ///< sqrt(1/2) x amplitude.
+  float    w[4][4][2];   ///< Precoding weights [port][layer].
+  uint16_t nof_pilots;   ///< DM-RS REs per CDM group in the symbol (nof_rb x per RB).
+  uint8_t  type2;        ///< DM-RS type 2.
+  uint8_t  L, P;         ///< Layers (DM-RS ports 0..L-1), antenna ports.
+  uint8_t  lp;           ///< l' (1 when the previous symbol also carries DM-RS): selects w_t.
+  uint8_t  pad[2];
+};
+
+void launch_pdsch_dmrs(const dmrs_job* d_jobs,
+                       int             nof_jobs,
+                       uint32_t*       d_grids,
+                       const uint32_t* d_x1,
+                       const uint32_t* d_x2_jump,
+                       const uint32_t* d_x2_lane,
+                       hipStream_t     stream);
+
 /// PUSCH channel estimator job (pusch_chest.hip): one (transmission, rx port, DM-RS CDM group).
 struct chest_job {
   uint32_t grid_base;        ///< Element of (port, symbol 0, first allocated subcarrier) in the rx grids.

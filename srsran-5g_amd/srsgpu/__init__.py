@@ -158,6 +158,28 @@ assert ctypes.sizeof(PdschModConfig) == 168
 CB_MSG_STRIDE = 1056
 
 
+class PdschDmrsConfig(ctypes.Structure):
+    """srsgpu_pdsch_dmrs_config (include/srsgpu_phy.h): dmrs_pdsch_processor::config_t of one transmission."""
+    _fields_ = [
+        ("slot_index", ctypes.c_uint16),
+        ("scrambling_id", ctypes.c_uint16),
+        ("n_scid", ctypes.c_uint8),
+        ("dmrs_type", ctypes.c_uint8),
+        ("nof_layers", ctypes.c_uint8),
+        ("nof_ports", ctypes.c_uint8),
+        ("dmrs_symbol_mask", ctypes.c_uint16),
+        ("reference_point_k_rb", ctypes.c_uint16),
+        ("rb_start", ctypes.c_uint16),
+        ("nof_rb", ctypes.c_uint16),
+        ("amplitude", ctypes.c_float),
+        ("precoding", ctypes.c_float * 32),
+        ("grid_index", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(PdschDmrsConfig) == 152
+
+
 class PuschDemodConfig(ctypes.Structure):
     """srsgpu_pusch_demod_config (include/srsgpu_phy.h): one transmission of pusch_demodulator::configuration."""
     _fields_ = [
@@ -269,6 +291,11 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pdsch_modulator_plan_execute.argtypes = [P, P, P, P]
     lib.srsgpu_pdsch_modulator_plan_destroy.argtypes = [P]
     lib.srsgpu_pdsch_modulator_plan_destroy.restype = None
+    lib.srsgpu_pdsch_dmrs_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                  ctypes.POINTER(P)]
+    lib.srsgpu_pdsch_dmrs_plan_execute.argtypes = [P, P, P]
+    lib.srsgpu_pdsch_dmrs_plan_destroy.argtypes = [P]
+    lib.srsgpu_pdsch_dmrs_plan_destroy.restype = None
     lib.srsgpu_pusch_chest_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                    ctypes.POINTER(P)]
     lib.srsgpu_pusch_chest_plan_execute.argtypes = [P, P, P, P, P, P]
@@ -316,6 +343,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
     "srsgpu_pusch_chest_plan_create", "srsgpu_pusch_chest_plan_execute", "srsgpu_pusch_chest_plan_destroy",
+    "srsgpu_pdsch_dmrs_plan_create", "srsgpu_pdsch_dmrs_plan_execute", "srsgpu_pdsch_dmrs_plan_destroy",
 ]
 
 
@@ -786,6 +814,66 @@ class PdschModulator:
 
     def modulate(self, codeword: np.ndarray, mod: PdschModulation, grid: np.ndarray = None) -> np.ndarray:
         return self.modulate_batch([codeword], [mod], grids=None if grid is None else grid[None])[0]
+
+
+@dataclass
+class PdschDmrs:
+    """dmrs_pdsch_processor::config_t (dmrs_pdsch_processor.h:38): contiguous CRB allocation, DM-RS ports
+    0..nof_layers-1, wideband precoding weights (nof_ports x nof_layers complex)."""
+    slot_index: int
+    scrambling_id: int
+    n_scid: int
+    dmrs_type: int
+    nof_layers: int
+    nof_ports: int
+    dmrs_symbol_mask: int
+    reference_point_k_rb: int
+    rb_start: int
+    nof_rb: int
+    amplitude: float
+    weights: np.ndarray
+
+
+def make_pdsch_dmrs_configs(dmrs: Sequence[PdschDmrs], grid_index: Sequence[int]):
+    arr = (PdschDmrsConfig * len(dmrs))()
+    for i, (m, g) in enumerate(zip(dmrs, grid_index)):
+        a = arr[i]
+        a.slot_index, a.scrambling_id, a.n_scid, a.dmrs_type = m.slot_index, m.scrambling_id, m.n_scid, m.dmrs_type
+        a.nof_layers, a.nof_ports, a.dmrs_symbol_mask = m.nof_layers, m.nof_ports, m.dmrs_symbol_mask
+        a.reference_point_k_rb, a.rb_start, a.nof_rb, a.amplitude = (m.reference_point_k_rb, m.rb_start, m.nof_rb,
+                                                                      m.amplitude)
+        w = np.zeros((4, 4, 2), np.float32)
+        wc = np.asarray(m.weights, np.complex64).reshape(m.nof_ports, m.nof_layers)
+        w[:m.nof_ports, :m.nof_layers, 0] = wc.real
+        w[:m.nof_ports, :m.nof_layers, 1] = wc.imag
+        a.precoding[:] = w.reshape(-1).tolist()
+        a.grid_index = g
+    return arr
+
+
+class PdschDmrsPlan:
+    """srsgpu_pdsch_dmrs_plan: PDSCH DM-RS generation, cover codes, precoding and mapping into bf16 grids."""
+
+    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        _check(_lib.srsgpu_pdsch_dmrs_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p), len(cfg_array),
+                                                  grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
+        self.handle = h
+
+    def execute(self, d_grids, stream=None):
+        _check(_lib.srsgpu_pdsch_dmrs_plan_execute(self.handle, _dptr(d_grids), _stream_handle(stream)))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.srsgpu_pdsch_dmrs_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 @dataclass

@@ -153,3 +153,19 @@ def pusch_chest_cases():
         cfg["scaling"] = float(d[f"case{i}_scaling"])
         yield cfg, int(row[-1]), d[f"case{i}_grid"], d[f"case{i}_ch_est"], d[f"case{i}_stats"]
         i += 1
+
+
+PDSCH_DMRS_KEYS = ["slot", "scrambling_id", "n_scid", "dmrs_type2", "nof_layers", "nof_ports", "dmrs_symbol_mask",
+                   "reference_point_k_rb", "rb_start", "nof_rb"]
+
+
+def pdsch_dmrs_cases():
+    """Yields (cfg dict, weights (P, L) complex64, reference grid (P, 14, 288, 2) bf16) made by
+    dmrs_pdsch_processor_impl (24-PRB grids)."""
+    d = _load("pdsch_dmrs.npz")
+    i = 0
+    while f"case{i}_cfg" in d:
+        cfg = {k: int(v) for k, v in zip(PDSCH_DMRS_KEYS, d[f"case{i}_cfg"])}
+        cfg["amplitude"] = float(d[f"case{i}_amplitude"])
+        yield cfg, d[f"case{i}_weights"], d[f"case{i}_grid"]
+        i += 1

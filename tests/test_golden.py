@@ -117,3 +117,13 @@ def test_pusch_chest_golden():
         np.testing.assert_allclose(np.stack([nv, rsrp, epre]), stats, rtol=1e-3)
         n += 1
     assert n == 8
+
+
+def test_pdsch_dmrs_golden():
+    """The PDSCH DM-RS restatement bit-exact against the reference's grids."""
+    import pdsch_dmrs_oracle as M
+    n = 0
+    for cfg, w, grid in G.pdsch_dmrs_cases():
+        assert np.array_equal(M.dmrs_map(cfg, w, 24), grid), cfg
+        n += 1
+    assert n == 10

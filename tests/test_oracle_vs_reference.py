@@ -278,3 +278,14 @@ def test_pusch_chest_oracle_vs_reference(ref, seed):
     np.testing.assert_allclose(nv, nv_o, rtol=1e-3)
     np.testing.assert_allclose(rsrp, rsrp_o, rtol=1e-3)
     np.testing.assert_allclose(epre, epre_o, rtol=1e-3)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_pdsch_dmrs_oracle_vs_reference(ref, seed):
+    """PDSCH DM-RS restatement bit-exact against the reference's dmrs_pdsch_processor_impl (1-4 layers and ports,
+    DM-RS types 1 and 2, single and double symbols, reference point, amplitude)."""
+    import pdsch_dmrs_oracle as M
+    from pdsch_dmrs_cases import random_config
+    rng = np.random.default_rng(500 + seed)
+    cfg, w = random_config(rng, 24)
+    assert np.array_equal(M.dmrs_map(cfg, w, 24), ref.dmrs_pdsch_map(cfg, w, 24)), cfg

@@ -227,6 +227,22 @@ def gen_pusch_chest(ref, rng):
     np.savez_compressed(os.path.join(OUT, "pusch_chest.npz"), **out)
 
 
+def gen_pdsch_dmrs(ref, rng):
+    """Reference PDSCH DM-RS grids (dmrs_pdsch_processor_impl) of random configurations in 24-PRB grids."""
+    from pdsch_dmrs_cases import random_config
+    out = {}
+    for i in range(10):
+        cfg, w = random_config(rng, 24)
+        out[f"case{i}_cfg"] = np.array([cfg[k] for k in PDSCH_DMRS_KEYS], np.int64)
+        out[f"case{i}_amplitude"] = np.float32(cfg["amplitude"])
+        out[f"case{i}_weights"] = w
+        out[f"case{i}_grid"] = ref.dmrs_pdsch_map(cfg, w, 24)
+    np.savez_compressed(os.path.join(OUT, "pdsch_dmrs.npz"), **out)
+
+
+PDSCH_DMRS_KEYS = ["slot", "scrambling_id", "n_scid", "dmrs_type2", "nof_layers", "nof_ports", "dmrs_symbol_mask",
+                   "reference_point_k_rb", "rb_start", "nof_rb"]
+
 PUSCH_CHEST_KEYS = ["slot", "scrambling_id", "n_scid", "dmrs_type2", "dmrs_symbol_mask", "start_symbol", "nof_symbols",
                     "rb_start", "nof_rb", "nof_rx_ports"]
 
@@ -239,7 +255,7 @@ def main():
     ref = Reference()
     if len(sys.argv) > 1:  # regenerate only the named fixture sets, e.g. `python tools/gen_golden.py ofdm`
         for name in sys.argv[1:]:
-            seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18}[name]
+            seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18, "pdsch_dmrs": 19}[name]
             globals()["gen_" + name](ref, np.random.default_rng(seed))
         return
     gen_crc(ref, np.random.default_rng(10))
@@ -251,6 +267,7 @@ def main():
     gen_ofdm(ref, np.random.default_rng(16))
     gen_pusch_demod(ref, np.random.default_rng(17))
     gen_pusch_chest(ref, np.random.default_rng(18))
+    gen_pdsch_dmrs(ref, np.random.default_rng(19))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

@@ -1,19 +1,25 @@
 #!/usr/bin/env python3
-"""Benchmark: 100 MHz 4x4 PDSCH + PUSCH channel-coding slot processing on MI355X.
+"""Benchmark: 100 MHz 4x4 PDSCH + PUSCH slot processing on MI355X (the whole upper-PHY data path plus OFDM).
 
 BASELINE.json metric: "PDSCH+PUSCH slots/sec (100MHz 4x4) + LDPC info-bits/s at 1/2/4/8 GPU".
 Workload ("n78 100 MHz 4x4, 273 PRB, LDPC BG1, batched 64 UEs"): one slot = 64 UEs sharing 273 PRBs (4-5 PRB each),
-4 layers, 256QAM MCS 27 (table 2), one DM-RS symbol -> 64 transport blocks, 192 LDPC BG1 codeblocks (Z 288/352),
-1.258 Mbit of TB payload per direction. A step processes `--slots-per-step` such slots per GPU, both directions:
+4 layers, 256QAM MCS 27 (table 2), one DM-RS symbol (type 1, 2 CDM groups without data) -> 64 transport blocks, 192
+LDPC BG1 codeblocks (Z 288/352), 1.258 Mbit of TB payload per direction. A step processes `--slots-per-step` such
+slots per GPU, both directions, on two HIP streams (as a gNB runs them concurrently):
 
-  * PDSCH (DL): srsgpu_pdsch_encoder_plan — TB CRC, segmentation, CB CRC24B, LDPC encoding, rate matching.
-  * PUSCH (UL): srsgpu_pusch_decoder_plan — rate dematching (new data), LDPC decoding (layered min-sum, SIMD
-    arithmetic, `--iterations` max with CRC early stop; srsRAN default 6), CB concatenation, TB CRC24A.
-    Received LLRs: the UL transport blocks encoded on the GPU, mapped to +/-amp with AWGN (--llr-amp/--llr-noise),
-    synthesised once before timing and resident in HBM; `--worst-case` uses random +/-10 LLRs instead (never
-    CRC-valid: every codeblock runs all iterations, like the reference ldpc_decoder_benchmark).
+  * DL: PDSCH encoder (TB CRC, segmentation, CB CRC, LDPC, rate matching) -> PDSCH DM-RS -> PDSCH modulator
+    (scrambling, 256QAM, layer mapping, precoding, RE mapping, bf16 grid) -> OFDM modulator (4096-point DFT, CP,
+    phase compensation) of 4 ports: baseband samples.
+  * UL: OFDM demodulator of 4 rx ports -> DM-RS channel estimator (4 layers x 4 ports) -> PUSCH demodulator (4x4
+    MMSE, soft demapping, descrambling) -> PUSCH decoder (rate dematching, LDPC min-sum, 6 iterations max with CRC
+    early stop, SIMD arithmetic; TB CRC).
+    Received samples: the UL transport blocks through a UE transmitter (the same GPU encoder / DM-RS / modulator),
+    a per-UE random unitary 4x4 channel and AWGN (--snr-db), OFDM-modulated; synthesised once before timing and
+    resident in HBM. `--worst-case` feeds Gaussian noise instead (no TB ever valid: every codeblock runs all
+    iterations, like the reference ldpc_decoder_benchmark).
 
-Weak scaling: every rank processes its own cells' slots; no data-path collective. One JSON line from rank 0.
+Weak scaling: every rank processes its own cells' slots; the decoded UL TBs + CRC flags of all ranks are gathered to
+rank 0 (the FAPI rank) over RCCL once per step. One JSON line from rank 0.
 """
 import argparse
 import ctypes
@@ -32,38 +38,28 @@ import torch.distributed as dist  # noqa: E402
 
 import srsgpu  # noqa: E402
 from srsgpu import sch  # noqa: E402
+from srsgpu import slot as slotlib  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 SLOT_RATE_30KHZ = 2000.0  # slots per second of one cell at 30 kHz SCS
+DL_STAGES = ["pdsch_encode", "pdsch_dmrs_modulate", "ofdm_modulate"]
+UL_STAGES = ["ofdm_demodulate", "pusch_channel_estimate", "pusch_demodulate", "pusch_decode"]
 
 
-def slot_grants():
-    ues = sch.slot_100mhz_4x4()
-    return ues, [u.segmentation() for u in ues]
-
-
-def synth_llrs(cw, cw_offsets, Gs, amp, noise, gen, dev):
-    """Codeword bits (packed, per-TB word-aligned) -> int8 LLRs (contiguous G per TB): +/-amp + N(0, noise)."""
-    idx = torch.cat([torch.arange(G, device=dev, dtype=torch.int64) + off * 8 for off, G in zip(cw_offsets, Gs)])
-    byte = cw[idx >> 3].to(torch.int32)
-    bits = (byte >> (7 - (idx & 7).to(torch.int32))) & 1
-    llr = (1 - 2 * bits).to(torch.float32) * amp
-    if noise > 0:
-        llr = llr + torch.randn(llr.shape, generator=gen, device=dev) * noise
-    return torch.clamp(torch.round(llr), -120, 120).to(torch.int8)
-
-
-def cpu_baseline(ues, segs, tb_host, llr_host, iterations, budget_s):
+def cpu_baseline(ues, segs, tb_host, cw_host, llr_host, samples_host, iterations, budget_s):
     """The srsRAN reference built from its own sources (oracle/_ref) on ONE host core, same slot: PDSCH encoding of
-    the 64 TBs (pdsch_encoder_impl: segmenter + AVX2 LDPC encoder + rate matcher) and the PUSCH codeblock tasks of the
-    192 codeblocks (rate dematcher + LDPC decoder with CRC early stop, the implementations "auto" picks here)."""
+    the 64 TBs (pdsch_encoder_impl: segmenter + AVX2 LDPC encoder + rate matcher), PDSCH DM-RS + modulation of the 64
+    UEs into one grid and OFDM modulation of 4 ports (generic DFT), OFDM demodulation of 4 ports, per-UE DM-RS channel
+    estimation + PUSCH demodulation (the open-source reference estimates / equalizes one layer: single-layer UEs on
+    the same REs), and the PUSCH codeblock tasks of the 192 codeblocks (rate dematcher + LDPC decoder with CRC early
+    stop, the implementations "auto" picks here)."""
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libsrsref.so")
     if not os.path.exists(ref_so):
         return None
     lib = ctypes.CDLL(ref_so)
     P = ctypes.c_void_p
-    lib.ref_pdsch_encode_slot_timed.restype = ctypes.c_longlong
-    lib.ref_pusch_decode_cbs_timed.restype = ctypes.c_longlong
+    for f in ("ref_pdsch_encode_slot_timed", "ref_pusch_decode_cbs_timed", "ref_dl_slot_timed", "ref_ul_slot_timed"):
+        getattr(lib, f).restype = ctypes.c_longlong
     avx512 = bool(lib.ref_cpu_has_avx512())
     vbmi = bool(lib.ref_cpu_has_avx512vbmi())
     n = len(ues)
@@ -72,6 +68,9 @@ def cpu_baseline(ues, segs, tb_host, llr_host, iterations, budget_s):
     ly = np.array([u.nof_layers for u in ues], np.int32)
     ns = np.array([u.nof_ch_symbols for u in ues], np.uint32)
     tbb = np.array([s.tbs // 8 for s in segs], np.uint32)
+    nrb = np.array([u.n_prb for u in ues], np.int32)
+    rb0 = np.concatenate([[0], np.cumsum(nrb)[:-1]]).astype(np.int32)
+    cw_off = np.array(cw_host[1], np.int32)
     cw = np.zeros(sum(s.cw_length for s in segs), np.uint8)
     params = []
     llr_off = 0
@@ -83,23 +82,36 @@ def cpu_baseline(ues, segs, tb_host, llr_host, iterations, budget_s):
         llr_off += s.cw_length
     params = np.array(params, np.int32)
     iters = np.zeros(len(params), np.int32)
-    enc_ns = dec_ns = 0
+    t_enc = t_dec = t_dl = t_ul = t_dl_ofdm = t_ul_ofdm = t_chest = 0
+    o1, o2 = ctypes.c_longlong(), ctypes.c_longlong()
     slots = 0
     t0 = time.time()
     while time.time() - t0 < budget_s or slots == 0:
-        enc_ns += lib.ref_pdsch_encode_slot_timed(1, n, bg.ctypes.data_as(P), qm.ctypes.data_as(P),
-                                                  ly.ctypes.data_as(P), ns.ctypes.data_as(P), tbb.ctypes.data_as(P),
-                                                  tb_host.ctypes.data_as(P), cw.ctypes.data_as(P))
-        dec_ns += lib.ref_pusch_decode_cbs_timed(2 if vbmi else 1, 2 if avx512 else 1, len(params),
-                                                 params.ctypes.data_as(P), llr_host.ctypes.data_as(P), iterations,
-                                                 iters.ctypes.data_as(P))
+        t_enc += lib.ref_pdsch_encode_slot_timed(1, n, bg.ctypes.data_as(P), qm.ctypes.data_as(P),
+                                                 ly.ctypes.data_as(P), ns.ctypes.data_as(P), tbb.ctypes.data_as(P),
+                                                 tb_host.ctypes.data_as(P), cw.ctypes.data_as(P))
+        t_dl += lib.ref_dl_slot_timed(n, rb0.ctypes.data_as(P), nrb.ctypes.data_as(P), int(qm[0]), int(ly[0]),
+                                      cw_host[0].ctypes.data_as(P), cw_off.ctypes.data_as(P), ctypes.byref(o1))
+        t_dl_ofdm += o1.value
+        t_ul += lib.ref_ul_slot_timed(n, rb0.ctypes.data_as(P), nrb.ctypes.data_as(P), int(qm[0]),
+                                      samples_host.ctypes.data_as(P), ctypes.byref(o1), ctypes.byref(o2))
+        t_ul_ofdm += o1.value
+        t_chest += o2.value
+        t_dec += lib.ref_pusch_decode_cbs_timed(2 if vbmi else 1, 2 if avx512 else 1, len(params),
+                                                params.ctypes.data_as(P), llr_host.ctypes.data_as(P), iterations,
+                                                iters.ctypes.data_as(P))
         slots += 1
-    slot_s = (enc_ns + dec_ns) * 1e-9 / slots
+    slot_s = (t_enc + t_dl + t_ul + t_dec) * 1e-9 / slots
+    ms = lambda v: v * 1e-6 / slots  # noqa: E731
     return {"value": 1.0 / slot_s, "unit": "slots/s", "cores": 1, "kind": "reference",
-            "sample": f"{slots} slots (64 TBs + 192 codeblocks each) through the srsRAN reference on one core: PDSCH "
-                      f"encode {enc_ns * 1e-6 / slots:.2f} ms/slot (avx2 encoder), PUSCH codeblock tasks "
-                      f"{dec_ns * 1e-6 / slots:.2f} ms/slot ({'avx512' if vbmi else 'avx2'} dematcher, "
-                      f"{'avx512' if avx512 else 'avx2'} decoder, {iterations} iterations max, early stop, avg "
+            "sample": f"{slots} slots (64 UEs, 192 codeblocks per direction) through the srsRAN reference on one "
+                      f"core: PDSCH encode {ms(t_enc):.2f} ms/slot (avx2 encoder), PDSCH DM-RS + modulation "
+                      f"{ms(t_dl - t_dl_ofdm):.2f} + OFDM modulation {ms(t_dl_ofdm):.2f} ms/slot (generic DFT), OFDM "
+                      f"demodulation {ms(t_ul_ofdm):.2f} + channel estimation {ms(t_chest):.2f} + PUSCH "
+                      f"demodulation {ms(t_ul - t_ul_ofdm - t_chest):.2f} ms/slot (single-layer: the open-source "
+                      f"reference's limit), PUSCH codeblock tasks {ms(t_dec):.2f} ms/slot "
+                      f"({'avx512' if vbmi else 'avx2'} dematcher, {'avx512' if avx512 else 'avx2'} decoder, "
+                      f"{iterations} iterations max, early stop, avg "
                       f"{np.where(iters > 0, iters, iterations).mean():.2f} iterations)"}
 
 
@@ -110,8 +122,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--slots-per-step", type=int, default=16)
     ap.add_argument("--iterations", type=int, default=6)
-    ap.add_argument("--llr-amp", type=float, default=16.0)
-    ap.add_argument("--llr-noise", type=float, default=6.0)
+    ap.add_argument("--snr-db", type=float, default=35.0)
     ap.add_argument("--worst-case", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -131,100 +142,82 @@ def main():
     ctx = srsgpu.Context(local_rank)
     S = args.slots_per_step
 
-    ues, segs = slot_grants()
-    tb_bytes = [s.tbs // 8 for s in segs] * S
-    Gs = [s.cw_length for s in segs] * S
+    ues = sch.slot_100mhz_4x4()
+    segs = [u.segmentation() for u in ues]
+    cell = slotlib.CellSlots(ues, segs, S)
+    dl = slotlib.DownlinkPipeline(ctx, cell)
+    ul = slotlib.UplinkPipeline(ctx, cell, iterations=args.iterations)
+    d_dl_tbs = torch.randint(0, 256, (dl.tb_total,), generator=gen, device=dev, dtype=torch.uint8)
+    d_ul_tbs_tx = torch.randint(0, 256, (dl.tb_total,), generator=gen, device=dev, dtype=torch.uint8)
+    if args.worst_case:
+        d_samples = torch.randn(2 * ul.ofdm.nof_samples, generator=gen, device=dev) * 0.01
+        data_desc = "Gaussian noise samples (no TB ever valid: all LDPC iterations, worst case)"
+    else:
+        d_samples = slotlib.synthesize_uplink(ctx, cell, d_ul_tbs_tx, snr_db=args.snr_db, seed=99 + rank)
+        data_desc = (f"UL TBs through a GPU UE transmitter (same encoder / DM-RS / modulator), a random unitary 4x4 "
+                     f"channel per UE and AWGN at {args.snr_db:g} dB SNR, OFDM-modulated (synthetic)")
+    torch.cuda.synchronize()
+    tb_bytes = dl.tb_bytes
     nof_tbs = len(tb_bytes)
 
-    # ---- PDSCH leg ----
-    dl_cfgs = [srsgpu.PdschTransportBlock(s.base_graph, 0, u.qm, u.nof_layers, u.nof_ch_symbols)
-               for u, s in zip(ues, segs)] * S
-    dl_arr, dl_tb_total, dl_cw_total, dl_cw_offsets = srsgpu.make_pdsch_configs(tb_bytes, dl_cfgs)
-    dl_plan = srsgpu.PdschEncoderPlan(ctx, dl_arr)
-    d_dl_tbs = torch.randint(0, 256, (dl_tb_total,), generator=gen, device=dev, dtype=torch.uint8)
-    d_dl_cw = torch.zeros(dl_cw_total, dtype=torch.uint8, device=dev)
-
-    # ---- PUSCH leg: received LLRs of GPU-encoded UL transport blocks ----
-    d_ul_tbs_tx = torch.randint(0, 256, (dl_tb_total,), generator=gen, device=dev, dtype=torch.uint8)
-    d_ul_cw = torch.zeros(dl_cw_total, dtype=torch.uint8, device=dev)
-    enc_tmp = srsgpu.PdschEncoderPlan(ctx, dl_arr)
-    enc_tmp.execute(d_ul_tbs_tx, d_ul_cw)
-    if args.worst_case:
-        d_llrs = (torch.randint(0, 2, (sum(Gs),), generator=gen, device=dev, dtype=torch.int32) * 20 - 10).to(torch.int8)
-        data_desc = "random +/-10 LLRs (never CRC-valid: all iterations, worst case)"
-    else:
-        d_llrs = synth_llrs(d_ul_cw, dl_cw_offsets, Gs, args.llr_amp, args.llr_noise, gen, dev)
-        data_desc = (f"UL TBs encoded on the GPU, BPSK-mapped to +/-{args.llr_amp:g} LLRs + AWGN sigma "
-                     f"{args.llr_noise:g} (synthetic)")
-    torch.cuda.synchronize()
-    enc_tmp.close()
-    ul_cfgs = [srsgpu.PuschTransportBlock(s.tbs // 8, s.base_graph, 0, u.qm, u.nof_layers, u.nof_ch_symbols,
-                                          nof_ldpc_iterations=args.iterations) for u, s in zip(ues, segs)] * S
-    nof_cbs = [s.nof_segments for s in segs] * S
-    cb_len = [(66 if s.base_graph == 1 else 50) * s.lifting_size for s in segs] * S
-    ul_arr, ul_llr_total, harq_total, cb_total, ul_tb_total = srsgpu.make_pusch_tb_configs(ul_cfgs, nof_cbs, cb_len)
-    ul_plan = srsgpu.PuschDecoderPlan(ctx, srsgpu.IMPL_SIMD, ul_arr)
-    d_harq = torch.zeros(harq_total, dtype=torch.int8, device=dev)
-    d_crc = torch.zeros(cb_total, dtype=torch.uint8, device=dev)
-    d_msgs = torch.zeros(cb_total * srsgpu.CB_MSG_STRIDE, dtype=torch.uint8, device=dev)
-    d_iters = torch.zeros(cb_total, dtype=torch.int32, device=dev)
-    d_ul_tbs = torch.zeros(ul_tb_total, dtype=torch.uint8, device=dev)
-    d_tb_ok = torch.zeros(nof_tbs, dtype=torch.uint8, device=dev)
-    # The DL and UL legs are independent (as in a gNB, where PDSCH and PUSCH processing of a slot run concurrently):
-    # each gets its own HIP stream, joined back into the main stream at the end of every step.
     main_stream = torch.cuda.current_stream(dev)
     dl_stream = torch.cuda.Stream(dev)
     ul_stream = dl_stream if args.serial_legs else torch.cuda.Stream(dev)
-
-    # Multi-GPU (north star): every rank codes its own cells' slots; the decoded UL transport blocks and their CRC flags
-    # of all ranks are gathered to the FAPI rank (rank 0) over RCCL once per step - the path's only exchange.
     tb_gather = None
     if world > 1:
         from srsgpu import dist as sdist
-        tb_gather = sdist.TbGather(d_ul_tbs.numel(), d_tb_ok.numel(), dev, root=0)
+        tb_gather = sdist.TbGather(ul.d_tbs.numel(), ul.d_tb_ok.numel(), dev, root=0)
 
-    def step():
+    def step(ev_dl=None, ev_ul=None):
         dl_stream.wait_stream(main_stream)
         ul_stream.wait_stream(main_stream)
-        dl_plan.execute(d_dl_tbs, d_dl_cw, dl_stream)
-        ul_plan.execute(d_llrs, d_harq, d_crc, d_msgs, d_iters, d_ul_tbs, d_tb_ok, ul_stream)
+        dl.execute(d_dl_tbs, dl_stream, ev_dl)
+        ul.execute(d_samples, ul_stream, ev_ul)
         main_stream.wait_stream(dl_stream)
         main_stream.wait_stream(ul_stream)
         if tb_gather is not None:
-            tb_gather.gather(d_ul_tbs, d_tb_ok)
+            tb_gather.gather(ul.d_tbs, ul.d_tb_ok)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    dl_plan.stage_times()
-    ul_plan.stage_times()
-    dl_plan.enable_timing(True)
-    ul_plan.enable_timing(True)
+    dl.encoder.stage_times()
+    ul.decoder.stage_times()
+    dl.encoder.enable_timing(True)
+    ul.decoder.enable_timing(True)
+    evs = [([torch.cuda.Event(enable_timing=True) for _ in range(4)],
+            [torch.cuda.Event(enable_timing=True) for _ in range(5)]) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(*evs[i])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    dl_ms, dl_n = dl_plan.stage_times()
-    ul_ms, ul_n = ul_plan.stage_times()
+    dl_ms, dl_n = dl.encoder.stage_times()
+    ul_ms, ul_n = ul.decoder.stage_times()
     assert dl_n == args.steps and ul_n == args.steps
+    stage = {k: 0.0 for k in DL_STAGES + UL_STAGES}
+    for ed, eu in evs:
+        for j, k in enumerate(DL_STAGES):
+            stage[k] += ed[j].elapsed_time(ed[j + 1]) / args.steps
+        for j, k in enumerate(UL_STAGES):
+            stage[k] += eu[j].elapsed_time(eu[j + 1]) / args.steps
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    # ---- Results of the last step: UL TB success and iterations (decoded TBs must equal what was sent) ----
-    tb_ok = d_tb_ok.cpu().numpy().astype(bool)
-    iters = d_iters.cpu().numpy()
+    # ---- Results of the last step: UL TB success (decoded TBs must equal what the UEs sent) and iterations ----
+    tb_ok = ul.d_tb_ok.cpu().numpy().astype(bool)
+    iters = ul.d_iters.cpu().numpy()
     if not args.worst_case:
         sent = d_ul_tbs_tx.cpu().numpy()
-        got = d_ul_tbs.cpu().numpy()
+        got = ul.d_tbs.cpu().numpy()
         off = 0
         for i, nb in enumerate(tb_bytes):
             if tb_ok[i]:
@@ -241,7 +234,7 @@ def main():
     # Algorithmic bytes of one decoder launch: the LLRs each codeblock's decode() reads (the HARQ span up to the
     # dematcher's zero tail, as reported by the plan), K*Z/8 bytes of decoded bits written, 4 B result + 1 B CRC flag,
     # 40 B descriptor.
-    dec_bytes = ul_plan.decoder_input_llrs + sum(
+    dec_bytes = ul.decoder.decoder_input_llrs + sum(
         s.nof_segments * (((22 if s.base_graph == 1 else 10) * s.lifting_size + 7) // 8 + 45) for s in segs) * S
     achieved = dec_bytes / (dec_ms * 1e-3) / 1e9
     traffic = None
@@ -263,17 +256,20 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int8",
-        "data": "synthetic: random TB payloads; PUSCH LLRs = " + data_desc,
+        "dtype": "int8/bf16/f32",
+        "data": "synthetic: random TB payloads; PUSCH input = " + data_desc,
         "config": {"workload": "n78 100 MHz 4x4 slot, 273 PRB, 64 UEs x (4-5 PRB, 4 layers, 256QAM MCS27), LDPC BG1 "
                                "(Z 288/352): 64 TBs / 192 codeblocks per direction per slot",
-                   "legs": ["pdsch_encode", "pusch_decode"],
+                   "dl_chain": "PDSCH encoder -> PDSCH DM-RS -> PDSCH modulator -> OFDM modulator (4 ports)",
+                   "ul_chain": "OFDM demodulator (4 ports) -> DM-RS channel estimator (4 layers x 4 ports) -> PUSCH "
+                               "demodulator (MMSE 4x4) -> PUSCH decoder",
                    "leg_streams": "one stream" if args.serial_legs else "DL and UL on concurrent streams",
                    "slots_per_step": S,
-                   "codeblocks_per_step_per_direction": int(sum(nof_cbs)),
+                   "codeblocks_per_step_per_direction": int(sum(s.nof_segments for s in segs) * S),
                    "ldpc_max_iterations": args.iterations, "ldpc_early_stop": True,
                    "decoder_arithmetic": "avx2/avx512 (SIMD) variant, bit-exact",
-                   "parallelism": (f"dp{world}: each GPU codes its own cells' slots; decoded UL TBs + CRC flags "
+                   "ofdm": "4096-point DFT, 122.88 Msps, normal CP",
+                   "parallelism": (f"dp{world}: each GPU processes its own cells' slots; decoded UL TBs + CRC flags "
                                    f"gathered to the FAPI rank over RCCL every step") if world > 1 else
                                   "dp1 (independent cells per GPU)"},
         "ldpc_info_bits_per_s": info_bits_slot * value,
@@ -281,9 +277,7 @@ def main():
         "realtime_cells_per_gpu": value / SLOT_RATE_30KHZ / world,
         "pusch_tb_success_rate": float(tb_ok.mean()),
         "ldpc_avg_iterations": avg_iters,
-        "stage_ms_per_step": {"pdsch_tb_crc": dl_ms[0] / args.steps, "pdsch_encode_rm": dl_ms[1] / args.steps,
-                              "pusch_rate_dematch": ul_ms[0] / args.steps, "pusch_ldpc_decode": dec_ms,
-                              "pusch_tb_crc": ul_ms[2] / args.steps},
+        "stage_ms_per_step": stage,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "ldpc_decode_pk_kernel<1,1,8>",
                      "kernel_ms_per_launch": dec_ms,
@@ -292,11 +286,13 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # One slot's UL payloads and LLRs on the host (same data the GPU decodes).
         n_slot = len(segs)
         tb_host = d_dl_tbs[: sum(tb_bytes[:n_slot])].cpu().numpy()
-        llr_host = d_llrs[: sum(Gs[:n_slot])].cpu().numpy()
-        result["cpu_baseline"] = cpu_baseline(ues, segs, tb_host, llr_host, args.iterations, args.cpu_seconds)
+        cw_host = (dl.d_cw.cpu().numpy(), dl.cw_offsets[:n_slot])
+        llr_host = ul.d_llrs[: sum(s.cw_length for s in segs)].cpu().numpy()
+        samples_host = d_samples[: 2 * 4 * 61440].cpu().numpy()
+        result["cpu_baseline"] = cpu_baseline(ues, segs, tb_host, cw_host, llr_host, samples_host, args.iterations,
+                                              args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

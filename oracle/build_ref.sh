@@ -81,6 +81,7 @@ SRCS=(
   "$HERE/ref/ref_pusch_chest.cpp:-mavx2 -mfma -I$REF"
   "$REF/lib/phy/upper/signal_processors/dmrs_pdsch_processor_impl.cpp:-mavx2"
   "$HERE/ref/ref_dmrs_pdsch.cpp:-mavx2 -I$REF"
+  "$HERE/ref/ref_slot_timed.cpp:-mavx2 -mfma -I$REF"
 )
 OBJS=()
 pids=()

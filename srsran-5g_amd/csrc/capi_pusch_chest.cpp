@@ -12,9 +12,12 @@ using namespace srsgpu;
 static_assert(sizeof(srsgpu_pusch_chest_config) == 28, "srsgpu_pusch_chest_config layout (mirrored by srsgpu)");
 
 struct srsgpu_pusch_chest_plan {
-  srsgpu_context* ctx      = nullptr;
-  chest_job*      d_jobs   = nullptr;
-  int             nof_jobs = 0;
+  srsgpu_context* ctx        = nullptr;
+  chest_job*      d_jobs     = nullptr;
+  int             nof_jobs   = 0;
+  int             max_pilots = 0;  ///< Largest job: pilots per DM-RS symbol.
+  int             max_dmrs   = 0;  ///< Largest job: DM-RS symbols.
+  int             max_words  = 0;  ///< Largest job: staged sequence words per DM-RS symbol.
 };
 
 namespace {
@@ -152,6 +155,15 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
   auto* plan     = new srsgpu_pusch_chest_plan();
   plan->ctx      = ctx;
   plan->nof_jobs = static_cast<int>(jobs.size());
+  for (const chest_job& jb : jobs) {
+    plan->max_pilots = std::max<int>(plan->max_pilots, jb.nof_pilots);
+    plan->max_dmrs   = std::max<int>(plan->max_dmrs, jb.nof_dmrs);
+    plan->max_words  = std::max<int>(plan->max_words, static_cast<int>(((2 * jb.seq_offset) % 32 + 2 * jb.nof_pilots + 31) / 32));
+  }
+  if (pusch_chest_lds_bytes(plan->max_pilots, plan->max_dmrs, plan->max_words) > 160 * 1024) {
+    delete plan;
+    return fail(SRSGPU_ERR_INVALID_ARG, "channel estimation job too large for the LDS");
+  }
   if (!jobs.empty() && (hipMalloc(&plan->d_jobs, jobs.size() * sizeof(chest_job)) != hipSuccess ||
                         hipMemcpy(plan->d_jobs, jobs.data(), jobs.size() * sizeof(chest_job), hipMemcpyHostToDevice) !=
                             hipSuccess)) {
@@ -172,7 +184,8 @@ int srsgpu_pusch_chest_plan_execute(const srsgpu_pusch_chest_plan* plan,
   if (plan == nullptr || d_grids == nullptr || d_ch_estimates == nullptr || d_noise_var == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  launch_pusch_chest(plan->d_jobs, plan->nof_jobs, d_grids, d_ch_estimates, d_noise_var, d_metrics,
+  launch_pusch_chest(plan->d_jobs, plan->nof_jobs, plan->max_pilots, plan->max_dmrs, plan->max_words, d_grids,
+                     d_ch_estimates, d_noise_var, d_metrics,
                      plan->ctx->d_gold_x1, plan->ctx->d_gold_x2_jump, plan->ctx->d_gold_x2_lane,
                      static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());

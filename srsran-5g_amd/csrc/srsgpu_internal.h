@@ -343,8 +343,15 @@ constexpr uint8_t CHEST_FD_NONE   = 0;
 constexpr uint8_t CHEST_FD_MEAN   = 1;
 constexpr uint8_t CHEST_FD_FILTER = 2;
 
+/// Dynamic LDS of the channel-estimator kernel for the plan's largest job (pilots per symbol, DM-RS symbols, staged
+/// sequence words per symbol).
+size_t pusch_chest_lds_bytes(int max_pilots, int max_dmrs, int max_words);
+
 void launch_pusch_chest(const chest_job* d_jobs,
                         int              nof_jobs,
+                        int              max_pilots,
+                        int              max_dmrs,
+                        int              max_words,
                         const uint32_t*  d_grids,
                         uint32_t*        d_ce,
                         float*           d_noise_var,

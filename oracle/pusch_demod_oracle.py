@@ -120,12 +120,12 @@ def demap(sym, nvar, qm):
     avg = {6: 42, 8: 170}[qm]
     a = F(1.0) / np.sqrt(F(avg))
     for kb, (wm, slopes, inters) in enumerate(interval_tables(qm)):
-        width = F(wm) * a
+        inv_width = F(1) / (F(wm) * a)  # scaled by the reciprocal width (avx2_helpers.h:178)
         nint = len(slopes)
         sl = np.array([F(s) * a for s in slopes], F)
         ic = np.array([F(c) / F(avg // 2) for c in inters], F)
         for k, x in enumerate((re, im)):
-            idx = np.clip(np.floor(x / width).astype(np.int64) + nint // 2, 0, nint - 1)
+            idx = np.clip(np.floor((x * inv_width).astype(F)).astype(np.int64) + nint // 2, 0, nint - 1)
             l = ((sl[idx] * x).astype(F) + ic[idx]).astype(F) * rcp
             out[:, 2 * kb + k] = np.where(np.abs(x) <= F(1e-9), 0, quantize(l, 20))
     return out.reshape(-1)

@@ -65,11 +65,11 @@ demap_pair_table pair_table(unsigned qm, unsigned k)
   const float a   = 1.0F / std::sqrt(static_cast<float>(avg));
   const int   step = mergeable ? 2 : 1;
   demap_pair_table t{};
-  t.width = static_cast<float>(2 * step) * a;
+  t.inv_width = 1.0F / (static_cast<float>(2 * step) * a);
   t.count = static_cast<uint32_t>(L / step);
   for (int i = 0; i < L / step; ++i) {
-    t.slope[i]     = static_cast<float>(slopes[static_cast<size_t>(i * step)]) * a;
-    t.intercept[i] = static_cast<float>(inters[static_cast<size_t>(i * step)]) / static_cast<float>(avg / 2);
+    t.piece[i][0] = static_cast<float>(slopes[static_cast<size_t>(i * step)]) * a;
+    t.piece[i][1] = static_cast<float>(inters[static_cast<size_t>(i * step)]) / static_cast<float>(avg / 2);
   }
   return t;
 }

@@ -58,11 +58,13 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
   const uint32_t  nwords = (d.nof_bits + 31u) >> 5;
 
   // Stage the chunk's scrambled words (and the first word of the next chunk, for an RE straddling the boundary).
-  {
-    const uint32_t w = ch.word0 + tid;
-    // word0 is a multiple of 256: the 64 words of a wave share their 2048-bit jump.
+  for (uint32_t j = tid; j < MOD_CHUNK_WORDS; j += MOD_THREADS) {
+    const uint32_t w = ch.word0 + j;
+    // word0 is a multiple of 64: the 64 words of a wave share their 2048-bit jump.
     const uint32_t c = __builtin_amdgcn_readfirstlane(w >> 6);
-    bits[tid]        = (w < nwords) ? scrambled_word(d, cw, x1, x2_jump, x2_lane, w, c) : 0u;
+    bits[j]          = (w < nwords) ? scrambled_word(d, cw, x1, x2_jump, x2_lane, w, c) : 0u;
+  }
+  {
     if (tid == 0) {
       const uint32_t w2 = ch.word0 + MOD_CHUNK_WORDS;
       bits[MOD_CHUNK_WORDS] = (w2 < nwords) ? scrambled_word(d, cw, x1, x2_jump, x2_lane, w2, w2 >> 6) : 0u;

@@ -6,8 +6,8 @@
 // equalize_zf_2xn.h:180 (ZF 2 x N), channel_modulation/demodulation_mapper_*.cpp (SIMD arithmetic: safe reciprocal
 // noise, near-zero parts, avx2_helpers.h:121 quantisation).
 //
-// Work decomposition (like the PDSCH modulator): a workgroup owns 8192 codeword LLRs of one transmission (the REs
-// whose first LLR falls in them). The four waves first stage the 8192 + 32 descrambling-sequence bits in LDS (Gold
+// Work decomposition (like the PDSCH modulator): a workgroup owns 32768 codeword LLRs of one transmission (the REs
+// whose first LLR falls in them). The four waves first stage the 32768 + 32 descrambling-sequence bits in LDS (Gold
 // sequence by GF(2) jumps, gold_device.h). Then every lane takes one RE: it loads the P received values and the L x P
 // channel estimates (consecutive lanes read consecutive subcarriers: coalesced 4-byte loads), equalizes, demaps the
 // L * Qm LLRs, flips the signs the sequence selects and stages the bytes in LDS; the workgroup finally writes its
@@ -15,7 +15,8 @@
 #include "gold_device.h"
 #include "srsgpu_internal.h"
 
-#pragma clang fp contract(off)
+// Contraction (FMA) is allowed in the equalizer; the demapper keeps the reference's separately rounded mul / add.
+#pragma clang fp contract(fast)
 
 namespace srsgpu {
 namespace {
@@ -68,20 +69,22 @@ __device__ __forceinline__ int quantize(float v, float scale)
   return static_cast<int>(__builtin_rintf(x));  // NaN cannot occur: rcp = 0 for invalid noise
 }
 
-/// Soft demapping of one equalized symbol into qm LLRs (stream order: re, im of bit pair 0, then pair 1, ...).
-__device__ __forceinline__ void demap(cpx s, float nvar, uint32_t qm, const demap_pair_table* tab, int* llr)
+/// Soft demapping of one equalized symbol into QM LLRs (stream order: re, im of bit pair 0, then pair 1, ...),
+/// following the SIMD demappers (demodulation_mapper_qam*.cpp, avx2_helpers.h: reciprocal-width interval index,
+/// separately rounded slope * x + intercept, per-component near-zero masking).
+template <int QM>
+__device__ __forceinline__ void demap(cpx s, float nvar, const demap_pair_table* tab, int* llr)
 {
-  const float rcp = (nvar > 0.f) ? 1.f / nvar : 0.f;
+#pragma clang fp contract(off)
+  const float rcp     = (nvar > 0.f) ? 1.f / nvar : 0.f;
   const float part[2] = {s.x, s.y};
-  if (qm == 2) {
+  if constexpr (QM == 2) {
     const float g = 2.0f * 1.41421356f;  // 2 * M_SQRT2f32
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       llr[k] = quantize((g * part[k]) * rcp, 120.f / 24.f);
     }
-    return;
-  }
-  if (qm == 4) {
+  } else if constexpr (QM == 4) {
     const float a = 0.316227766f;  // 1 / sqrt(10) in float
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -93,89 +96,115 @@ __device__ __forceinline__ void demap(cpx s, float nvar, uint32_t qm, const dema
       llr[k]          = nz ? 0 : quantize(l01 * rcp, 6.f);
       llr[2 + k]      = nz ? 0 : quantize(l23 * rcp, 6.f);
     }
-    return;
-  }
-  const demap_pair_table* t = tab + (qm == 6 ? 0 : 3);
-#pragma unroll
-  for (uint32_t kb = 0; kb < 4; ++kb) {
-    if (kb >= qm / 2) {
-      break;
-    }
-    const demap_pair_table& p = t[kb];
+  } else {
+    const demap_pair_table* t = tab + (QM == 6 ? 0 : 3);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const float x   = part[k];
-      int         idx = static_cast<int>(floorf(x / p.width)) + static_cast<int>(p.count / 2);
-      idx             = min(max(idx, 0), static_cast<int>(p.count) - 1);
-      const float l   = (p.slope[idx] * x + p.intercept[idx]) * rcp;
-      llr[2 * kb + k] = (fabsf(x) <= 1e-9f) ? 0 : quantize(l, 6.f);
+      const float x  = part[k];
+      const bool  nz = fabsf(x) <= 1e-9f;
+#pragma unroll
+      for (int kb = 0; kb < QM / 2; ++kb) {
+        const demap_pair_table& p   = t[kb];
+        const int               cnt = static_cast<int>(p.count);
+        int                     idx = static_cast<int>(floorf(x * p.inv_width)) + cnt / 2;
+        idx                         = min(max(idx, 0), cnt - 1);
+        const float2 sl             = *reinterpret_cast<const float2*>(p.piece[idx]);
+        const float  l              = (sl.x * x + sl.y) * rcp;
+        llr[2 * kb + k]             = nz ? 0 : quantize(l, 6.f);
+      }
     }
   }
 }
 
-/// Unbiased linear MMSE for L layers: A = H^H H + nv I, x = A^-1 H^H y, g_l = 1 - nv [A^-1]_ll,
-/// eq_l = x_l / g_l, var_l = nv [A^-1]_ll / g_l (Gauss-Jordan on the Hermitian positive definite A).
+/// Unbiased linear MMSE for L layers: A = H^H H + nv I = R^H R (Cholesky, R upper triangular with a real diagonal),
+/// T = R^-1, A^-1 = T T^H: x = T (T^H H^H y), [A^-1]_ll = sum_j |T_lj|^2, g_l = 1 - nv [A^-1]_ll,
+/// eq_l = x_l / g_l, var_l = nv [A^-1]_ll / g_l.
 template <int L>
 __device__ __forceinline__ void equalize_mmse(const cpx* y, const cpx (*h)[4], uint32_t P, float nv, cpx* eq,
                                               float* var)
 {
-  cpx A[L][L], B[L][L], m[L];
+  cpx A[L][L], m[L];
 #pragma unroll
   for (int i = 0; i < L; ++i) {
 #pragma unroll
-    for (int j = 0; j < L; ++j) {
+    for (int j = i; j < L; ++j) {
       cpx s = cmk(0.f, 0.f);
-      #pragma unroll
-      for (uint32_t p = 0; p < 4; ++p) {  // unrolled: register arrays stay in VGPRs
-        if (p >= P) {
-          break;
+#pragma unroll
+      for (uint32_t p = 0; p < 4; ++p) {
+        if (p < P) {
+          s = cadd(s, cmulc(h[j][p], h[i][p]));  // conj(h_ip) h_jp
         }
-        s = cadd(s, cmulc(h[j][p], h[i][p]));  // conj(h_pi) h_pj
       }
       A[i][j] = s;
-      B[i][j] = cmk(i == j ? 1.f : 0.f, 0.f);
     }
     A[i][i].x += nv;
     cpx s = cmk(0.f, 0.f);
-    #pragma unroll
-    for (uint32_t p = 0; p < 4; ++p) {  // unrolled: register arrays stay in VGPRs
-        if (p >= P) {
-          break;
-        }
-      s = cadd(s, cmulc(y[p], h[i][p]));  // conj(h_pi) y_p
+#pragma unroll
+    for (uint32_t p = 0; p < 4; ++p) {
+      if (p < P) {
+        s = cadd(s, cmulc(y[p], h[i][p]));  // conj(h_ip) y_p
+      }
     }
     m[i] = s;
   }
+  // Cholesky: R_ii = sqrt(A_ii - sum_k<i |R_ki|^2), R_ij = (A_ij - sum_k<i conj(R_ki) R_kj) / R_ii.
+  cpx   R[L][L];
+  float rinv[L];
 #pragma unroll
-  for (int c = 0; c < L; ++c) {
-    const float d   = A[c][c].x;  // real positive pivot (Hermitian PD)
-    const float rcp = 1.f / d;
+  for (int i = 0; i < L; ++i) {
+    float d = A[i][i].x;
 #pragma unroll
-    for (int j = 0; j < L; ++j) {
-      A[c][j] = cscale(A[c][j], rcp);
-      B[c][j] = cscale(B[c][j], rcp);
+    for (int k = 0; k < i; ++k) {
+      d -= R[k][i].x * R[k][i].x + R[k][i].y * R[k][i].y;
     }
+    const float rii = sqrtf(fmaxf(d, 0.f));
+    rinv[i]         = 1.f / rii;
 #pragma unroll
-    for (int i = 0; i < L; ++i) {
-      if (i != c) {
-        const cpx f = A[i][c];
+    for (int j = i + 1; j < L; ++j) {
+      cpx s = A[i][j];
 #pragma unroll
-        for (int j = 0; j < L; ++j) {
-          A[i][j] = csub(A[i][j], cmul(f, A[c][j]));
-          B[i][j] = csub(B[i][j], cmul(f, B[c][j]));
-        }
+      for (int k = 0; k < i; ++k) {
+        s = csub(s, cmulc(R[k][j], R[k][i]));  // conj(R_ki) R_kj
       }
+      R[i][j] = cscale(s, rinv[i]);
     }
+  }
+  // T = R^-1 (upper triangular): T_ii = 1 / R_ii, T_ij = -(sum_{k=i}^{j-1} T_ik R_kj) / R_jj.
+  cpx T[L][L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    T[i][i] = cmk(rinv[i], 0.f);
+#pragma unroll
+    for (int j = i + 1; j < L; ++j) {
+      cpx s = cmul(T[i][i], R[i][j]);
+#pragma unroll
+      for (int k = i + 1; k < j; ++k) {
+        s = cadd(s, cmul(T[i][k], R[k][j]));
+      }
+      T[i][j] = cscale(s, -rinv[j]);
+    }
+  }
+  // z = T^H m (lower triangular: z_j = sum_{i<=j} conj(T_ij) m_i), x = T z.
+  cpx z[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    cpx s = cmk(0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i <= j; ++i) {
+      s = cadd(s, cmulc(m[i], T[i][j]));
+    }
+    z[j] = s;
   }
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    cpx x = cmk(0.f, 0.f);
+    cpx   x   = cmk(0.f, 0.f);
+    float aii = 0.f;
 #pragma unroll
-    for (int j = 0; j < L; ++j) {
-      x = cadd(x, cmul(B[i][j], m[j]));
+    for (int j = i; j < L; ++j) {
+      x = cadd(x, cmul(T[i][j], z[j]));
+      aii += T[i][j].x * T[i][j].x + T[i][j].y * T[i][j].y;
     }
-    const float aii = B[i][i].x;
-    const float g   = 1.f - nv * aii;
+    const float g = 1.f - nv * aii;
     if (isnormal_f(g) && g > 0.f && isnormal_f(nv * aii)) {
       const float rg = 1.f / g;
       eq[i]          = cscale(x, rg);
@@ -187,53 +216,29 @@ __device__ __forceinline__ void equalize_mmse(const cpx* y, const cpx (*h)[4], u
   }
 }
 
-__global__ __launch_bounds__(DEMOD_THREADS) void pusch_demodulate_kernel(const demod_desc* __restrict__ descs,
-                                                                         const mod_chunk* __restrict__ chunks,
-                                                                         const demap_pair_table* __restrict__ tables,
-                                                                         const uint32_t* __restrict__ grids,
-                                                                         const uint32_t* __restrict__ ce,
-                                                                         const float* __restrict__ noise_var,
-                                                                         int8_t* __restrict__ llrs,
-                                                                         const uint32_t* __restrict__ x1,
-                                                                         const uint32_t* __restrict__ x2_jump,
-                                                                         const uint32_t* __restrict__ x2_lane)
-{
-  __shared__ uint32_t         seq[MOD_CHUNK_WORDS + 1];
-  __shared__ demap_pair_table tab[DEMAP_TABLES];
-  __shared__ int8_t           out[DEMOD_OUT_BYTES];
-  const mod_chunk             ch     = chunks[blockIdx.x];
-  const demod_desc&           d      = descs[ch.tx];
-  const uint32_t              tid    = threadIdx.x;
-  const uint32_t              nwords = (d.nof_llrs + 31u) >> 5;
-  {
-    const uint32_t w = ch.word0 + tid;
-    const uint32_t c = __builtin_amdgcn_readfirstlane(w >> 6);  // word0 % 256 == 0: wave-uniform jump
-    seq[tid]         = (w < nwords) ? gold_word(d.c_init, w, c, x1, x2_jump, x2_lane) : 0u;
-    if (tid == 0) {
-      const uint32_t w2      = ch.word0 + MOD_CHUNK_WORDS;
-      seq[MOD_CHUNK_WORDS] = (w2 < nwords) ? gold_word(d.c_init, w2, w2 >> 6, x1, x2_jump, x2_lane) : 0u;
-    }
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(tables);
-    uint32_t*       dst = reinterpret_cast<uint32_t*>(tab);
-    for (uint32_t i = tid; i < sizeof(tab) / 4; i += DEMOD_THREADS) {
-      dst[i] = src[i];
-    }
-  }
-  const uint32_t qm = d.qm, L = d.L, P = d.P, Lq = L * qm;
-  float          nv[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    nv[p] = noise_var[4 * d.tx + p];
-  }
-  float nv_max = nv[0];
-#pragma unroll
-  for (uint32_t p = 1; p < 4; ++p) {
-    nv_max = (p < P) ? fmaxf(nv_max, nv[p]) : nv_max;
-  }
-  __syncthreads();
+/// Transmission parameters of a workgroup, uniform across it.
+struct demod_uniform {
+  const demod_desc* d;
+  uint32_t          re_begin, re_end, word0;
+  float             nv[4], nv_max;
+};
 
-  const uint32_t first_llr = ch.re_begin * Lq;  // first LLR the workgroup writes
-  for (uint32_t r = ch.re_begin + tid; r < ch.re_end; r += DEMOD_THREADS) {
+/// Every RE of the chunk owned by this lane: loads, equalization (L layers), demapping (QM bits per layer),
+/// descrambling and the packed LLR bytes into the LDS output buffer. L and QM are compile-time so that every register
+/// array has static indices and the RE's L * QM bytes are assembled in registers.
+template <int L, int QM>
+__device__ __forceinline__ void demod_res(const demod_uniform& u,
+                                          const demap_pair_table* tab,
+                                          const uint32_t* __restrict__ grids,
+                                          const uint32_t* __restrict__ ce,
+                                          const uint32_t* seq,
+                                          uint32_t*       out32)
+{
+  constexpr uint32_t LQ = L * QM;
+  const demod_desc&  d  = *u.d;
+  const uint32_t     P  = d.P;
+  const bool         zf = d.eq == DEMOD_EQ_ZF;
+  for (uint32_t r = u.re_begin + threadIdx.x; r < u.re_end; r += DEMOD_THREADS) {
     // Symbol and subcarrier of the RE.
     uint32_t l = 0;
 #pragma unroll
@@ -251,35 +256,32 @@ __global__ __launch_bounds__(DEMOD_THREADS) void pusch_demodulate_kernel(const d
     }
     const uint32_t ge = d.grid_base + l * d.nsc + sc;
     const uint32_t ee = d.ce_base + l * d.nsc + sc;
-    cpx            y[4], h[4][4];
+    cpx            y[4], h[L][4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       if (p < static_cast<int>(P)) {
         y[p] = bf16c(grids[ge + p * d.port_stride]);
 #pragma unroll
-        for (int ly = 0; ly < 4; ++ly) {
-          if (ly < static_cast<int>(L)) {
-            h[ly][p] = bf16c(ce[ee + ly * d.ce_layer_stride + p * d.port_stride]);
-          }
+        for (int ly = 0; ly < L; ++ly) {
+          h[ly][p] = bf16c(ce[ee + ly * d.ce_layer_stride + p * d.port_stride]);
         }
       }
     }
-    cpx   eq[4];
-    float var[4];
-    if (L == 1) {
+    cpx   eq[L];
+    float var[L];
+    if constexpr (L == 1) {
       // ZF 1 x N (MMSE with one layer is the same, channel_equalizer_generic_impl.cpp:343).
       float ch_mod_sq = 0.f, nvar_acc = 0.f;
       cpx   acc       = cmk(0.f, 0.f);
-      #pragma unroll
-      for (uint32_t p = 0; p < 4; ++p) {  // unrolled: register arrays stay in VGPRs
-        if (p >= P) {
-          break;
-        }
-        const float norm = h[0][p].x * h[0][p].x + h[0][p].y * h[0][p].y;
-        if (isnormal_f(norm) && isnormal_f(nv[p]) && nv[p] > 0.f) {
-          ch_mod_sq += norm;
-          nvar_acc += norm * nv[p];
-          acc = cadd(acc, cmulc(y[p], h[0][p]));
+#pragma unroll
+      for (uint32_t p = 0; p < 4; ++p) {
+        if (p < P) {
+          const float norm = h[0][p].x * h[0][p].x + h[0][p].y * h[0][p].y;
+          if (isnormal_f(norm) && isnormal_f(u.nv[p]) && u.nv[p] > 0.f) {
+            ch_mod_sq += norm;
+            nvar_acc += norm * u.nv[p];
+            acc = cadd(acc, cmulc(y[p], h[0][p]));
+          }
         }
       }
       if (isnormal_f(ch_mod_sq) && isnormal_f(nvar_acc)) {
@@ -290,78 +292,166 @@ __global__ __launch_bounds__(DEMOD_THREADS) void pusch_demodulate_kernel(const d
         eq[0]  = cmk(0.f, 0.f);
         var[0] = __builtin_inff();
       }
-    } else if (L == 2 && d.eq == DEMOD_EQ_ZF) {
-      // ZF 2 x N with the largest noise variance.
-      eq[0] = eq[1] = cmk(0.f, 0.f);
-      var[0] = var[1] = __builtin_inff();
-      if (isnormal_f(nv_max) && nv_max >= 0.f) {
-        float n0 = 0.f, n1 = 0.f;
-        cpx   xi = cmk(0.f, 0.f), m0 = cmk(0.f, 0.f), m1 = cmk(0.f, 0.f);
-        #pragma unroll
-        for (uint32_t p = 0; p < 4; ++p) {  // unrolled: register arrays stay in VGPRs
-        if (p >= P) {
-          break;
-        }
-          n0 += h[0][p].x * h[0][p].x + h[0][p].y * h[0][p].y;
-          n1 += h[1][p].x * h[1][p].x + h[1][p].y * h[1][p].y;
-          xi = cadd(xi, cmulc(h[1][p], h[0][p]));  // conj(h0) h1
-          m0 = cadd(m0, cmulc(y[p], h[0][p]));
-          m1 = cadd(m1, cmulc(y[p], h[1][p]));
-        }
-        const float d_pinv = n0 * n1 - (xi.x * xi.x + xi.y * xi.y);
-        if (isnormal_f(d_pinv)) {
-          const float rcp = 1.f / d_pinv;
-          eq[0]           = cscale(csub(cscale(m0, n1), cmul(xi, m1)), rcp);
-          eq[1]           = cscale(csub(cscale(m1, n0), cmulc(m0, xi)), rcp);
-          var[0]          = nv_max * n1 * rcp;
-          var[1]          = nv_max * n0 * rcp;
+    } else {
+      bool done = false;
+      if constexpr (L == 2) {
+        if (zf) {
+          // ZF 2 x N with the largest noise variance.
+          done  = true;
+          eq[0] = eq[1] = cmk(0.f, 0.f);
+          var[0] = var[1] = __builtin_inff();
+          if (isnormal_f(u.nv_max) && u.nv_max >= 0.f) {
+            float n0 = 0.f, n1 = 0.f;
+            cpx   xi = cmk(0.f, 0.f), m0 = cmk(0.f, 0.f), m1 = cmk(0.f, 0.f);
+#pragma unroll
+            for (uint32_t p = 0; p < 4; ++p) {
+              if (p < P) {
+                n0 += h[0][p].x * h[0][p].x + h[0][p].y * h[0][p].y;
+                n1 += h[1][p].x * h[1][p].x + h[1][p].y * h[1][p].y;
+                xi = cadd(xi, cmulc(h[1][p], h[0][p]));  // conj(h0) h1
+                m0 = cadd(m0, cmulc(y[p], h[0][p]));
+                m1 = cadd(m1, cmulc(y[p], h[1][p]));
+              }
+            }
+            const float d_pinv = n0 * n1 - (xi.x * xi.x + xi.y * xi.y);
+            if (isnormal_f(d_pinv)) {
+              const float rcp = 1.f / d_pinv;
+              eq[0]           = cscale(csub(cscale(m0, n1), cmul(xi, m1)), rcp);
+              eq[1]           = cscale(csub(cscale(m1, n0), cmulc(m0, xi)), rcp);
+              var[0]          = u.nv_max * n1 * rcp;
+              var[1]          = u.nv_max * n0 * rcp;
+            }
+          }
         }
       }
-    } else if (L == 2) {
-      equalize_mmse<2>(y, h, P, nv_max, eq, var);
-    } else if (L == 3) {
-      equalize_mmse<3>(y, h, P, nv_max, eq, var);
-    } else {
-      equalize_mmse<4>(y, h, P, nv_max, eq, var);
+      if (!done) {
+        equalize_mmse<L>(y, h, P, u.nv_max, eq, var);
+      }
     }
 
-    // Demap, descramble (sequence bits of the RE's LLRs, MSB-first words staged in LDS) and stage the bytes.
-    const uint32_t o  = r * Lq - ch.word0 * 32u;
+    // Demap, descramble (sequence bits of the RE's LLRs, MSB-first words staged in LDS) and pack the bytes.
+    const uint32_t o  = r * LQ - u.word0 * 32u;
     const uint32_t wi = o >> 5;
     const uint64_t sb = ((static_cast<uint64_t>(seq[wi]) << 32) | seq[wi + 1]) << (o & 31u);
-    const uint32_t ob = r * Lq - first_llr;
-    for (uint32_t ly = 0; ly < L; ++ly) {
-      int v[8];
-      demap(eq[ly], var[ly], qm, tab, v);
+    uint32_t       pk[(LQ + 3) / 4] = {};
 #pragma unroll
-      for (uint32_t j = 0; j < 8; ++j) {
-        if (j < qm) {
-          const uint32_t bit = static_cast<uint32_t>(sb >> (63u - (ly * qm + j))) & 1u;
-          out[ob + ly * qm + j] = static_cast<int8_t>(bit ? -v[j] : v[j]);
-        }
+    for (int ly = 0; ly < L; ++ly) {
+      int v[QM];
+      demap<QM>(eq[ly], var[ly], tab, v);
+#pragma unroll
+      for (int j = 0; j < QM; ++j) {
+        const int      b   = ly * QM + j;
+        const uint32_t bit = static_cast<uint32_t>(sb >> (63 - b)) & 1u;
+        const uint32_t s8  = static_cast<uint8_t>(static_cast<int8_t>(bit ? -v[j] : v[j]));
+        pk[b / 4] |= s8 << (8 * (b % 4));
       }
     }
+    const uint32_t ob = (r - u.re_begin) * LQ;
+    if constexpr (LQ % 4 == 0) {
+#pragma unroll
+      for (uint32_t i = 0; i < LQ / 4; ++i) {
+        out32[ob / 4 + i] = pk[i];
+      }
+    } else {
+      uint8_t* out8 = reinterpret_cast<uint8_t*>(out32);
+#pragma unroll
+      for (uint32_t b = 0; b < LQ; ++b) {
+        out8[ob + b] = static_cast<uint8_t>(pk[b / 4] >> (8 * (b % 4)));
+      }
+    }
+  }
+}
+
+template <int QM>
+__device__ __forceinline__ void demod_res_qm(const demod_uniform& u, const demap_pair_table* tab,
+                                             const uint32_t* __restrict__ grids, const uint32_t* __restrict__ ce,
+                                             const uint32_t* seq, uint32_t* out32)
+{
+  switch (u.d->L) {
+    case 1: demod_res<1, QM>(u, tab, grids, ce, seq, out32); break;
+    case 2: demod_res<2, QM>(u, tab, grids, ce, seq, out32); break;
+    case 3: demod_res<3, QM>(u, tab, grids, ce, seq, out32); break;
+    default: demod_res<4, QM>(u, tab, grids, ce, seq, out32); break;
+  }
+}
+
+__global__ __launch_bounds__(DEMOD_THREADS) void pusch_demodulate_kernel(const demod_desc* __restrict__ descs,
+                                                                         const mod_chunk* __restrict__ chunks,
+                                                                         const demap_pair_table* __restrict__ tables,
+                                                                         const uint32_t* __restrict__ grids,
+                                                                         const uint32_t* __restrict__ ce,
+                                                                         const float* __restrict__ noise_var,
+                                                                         int8_t* __restrict__ llrs,
+                                                                         const uint32_t* __restrict__ x1,
+                                                                         const uint32_t* __restrict__ x2_jump,
+                                                                         const uint32_t* __restrict__ x2_lane)
+{
+  __shared__ uint32_t         seq[MOD_CHUNK_WORDS + 1];
+  __shared__ demap_pair_table tab[DEMAP_TABLES];
+  __shared__ uint32_t         out32[DEMOD_OUT_BYTES / 4];
+  const mod_chunk             ch     = chunks[blockIdx.x];
+  const demod_desc&           d      = descs[ch.tx];
+  const uint32_t              tid    = threadIdx.x;
+  const uint32_t              nwords = (d.nof_llrs + 31u) >> 5;
+  for (uint32_t j = tid; j < MOD_CHUNK_WORDS; j += DEMOD_THREADS) {
+    const uint32_t w = ch.word0 + j;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(w >> 6);  // word0 % 64 == 0: wave-uniform jump
+    seq[j]           = (w < nwords) ? gold_word(d.c_init, w, c, x1, x2_jump, x2_lane) : 0u;
+  }
+  if (tid == 0) {
+    const uint32_t w2    = ch.word0 + MOD_CHUNK_WORDS;
+    seq[MOD_CHUNK_WORDS] = (w2 < nwords) ? gold_word(d.c_init, w2, w2 >> 6, x1, x2_jump, x2_lane) : 0u;
+  }
+  if (d.qm >= 6) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(tables);
+    uint32_t*       dst = reinterpret_cast<uint32_t*>(tab);
+    for (uint32_t i = tid; i < sizeof(tab) / 4; i += DEMOD_THREADS) {
+      dst[i] = src[i];
+    }
+  }
+  demod_uniform u;
+  u.d        = &d;
+  u.re_begin = ch.re_begin;
+  u.re_end   = ch.re_end;
+  u.word0    = ch.word0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    u.nv[p] = noise_var[4 * d.tx + p];
+  }
+  u.nv_max = u.nv[0];
+#pragma unroll
+  for (uint32_t p = 1; p < 4; ++p) {
+    u.nv_max = (p < d.P) ? fmaxf(u.nv_max, u.nv[p]) : u.nv_max;
   }
   __syncthreads();
 
-  // Contiguous LLR range [first_llr, re_end * Lq) of the codeword: bytes up to dword alignment, then dwords.
-  const uint32_t n    = (ch.re_end - ch.re_begin) * Lq;
-  int8_t*        dst  = llrs + d.llr_offset + first_llr;
-  const uint32_t head = min(n, static_cast<uint32_t>((4u - (reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u));
-  if (tid < head) {
-    dst[tid] = out[tid];
+  switch (d.qm) {
+    case 2: demod_res_qm<2>(u, tab, grids, ce, seq, out32); break;
+    case 4: demod_res_qm<4>(u, tab, grids, ce, seq, out32); break;
+    case 6: demod_res_qm<6>(u, tab, grids, ce, seq, out32); break;
+    default: demod_res_qm<8>(u, tab, grids, ce, seq, out32); break;
   }
-  const uint32_t nw = (n - head) / 4;
-  for (uint32_t i = tid; i < nw; i += DEMOD_THREADS) {
-    const uint32_t b = head + 4 * i;
-    const uint32_t v = static_cast<uint8_t>(out[b]) | (static_cast<uint32_t>(static_cast<uint8_t>(out[b + 1])) << 8) |
-                       (static_cast<uint32_t>(static_cast<uint8_t>(out[b + 2])) << 16) |
-                       (static_cast<uint32_t>(static_cast<uint8_t>(out[b + 3])) << 24);
-    reinterpret_cast<uint32_t*>(dst + head)[i] = v;
+  __syncthreads();
+
+  // Contiguous LLR range [re_begin * Lq, re_end * Lq) of the codeword, staged from LDS byte 0. With s = dst & 3, the
+  // aligned global word j holds staged bytes 4 j - s .. 4 j - s + 3: two LDS words funnel-shifted, one dword store.
+  const uint32_t Lq  = static_cast<uint32_t>(d.L) * d.qm;
+  const uint32_t n   = (ch.re_end - ch.re_begin) * Lq;
+  int8_t*        dst = llrs + d.llr_offset + ch.re_begin * Lq;
+  const uint32_t s   = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst) & 3u);
+  uint32_t*      g32 = reinterpret_cast<uint32_t*>(dst - s);
+  const uint32_t j0  = (s == 0) ? 0u : 1u;       // first full word
+  const uint32_t j1  = (n + s) / 4;               // end of the full words
+  for (uint32_t j = j0 + tid; j < j1; j += DEMOD_THREADS) {
+    g32[j] = (s == 0) ? out32[j] : __builtin_amdgcn_alignbyte(out32[j], out32[j - 1], 4u - s);
   }
-  const uint32_t tail0 = head + 4 * nw;
-  if (tail0 + tid < n) {
-    dst[tail0 + tid] = out[tail0 + tid];
+  const uint8_t* out8 = reinterpret_cast<const uint8_t*>(out32);
+  if (s != 0 && tid < min(4u - s, n)) {  // head bytes before the first full word
+    dst[tid] = static_cast<int8_t>(out8[tid]);
+  }
+  const uint32_t t0 = (j1 > 0 ? 4u * j1 - s : 0u);  // tail bytes after the last full word
+  if (j1 >= j0 && t0 + tid < n && tid < 4u) {
+    dst[t0 + tid] = static_cast<int8_t>(out8[t0 + tid]);
   }
 }
 

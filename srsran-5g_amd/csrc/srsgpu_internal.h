@@ -199,7 +199,8 @@ struct mod_desc {
 };
 static_assert(sizeof(mod_desc) == 200, "mod_desc layout");
 
-/// PDSCH modulator work item: 8192 codeword bits (256 words) of one transmission and the REs starting in them.
+/// PDSCH modulator / PUSCH demodulator work item: MOD_CHUNK_WORDS x 32 codeword bits of one transmission and the REs
+/// starting in them.
 struct mod_chunk {
   uint32_t tx;        ///< Transmission (descriptor index).
   uint32_t word0;     ///< First codeword word of the chunk.
@@ -277,13 +278,13 @@ static_assert(sizeof(demod_desc) == 88, "demod_desc layout");
 constexpr uint8_t DEMOD_EQ_ZF   = 0;
 constexpr uint8_t DEMOD_EQ_MMSE = 1;
 
-/// Max-log interval tables of the 64QAM / 256QAM demapper: per bit pair k (stream bits 2k, 2k + 1) an interval width,
-/// a count and (slope, intercept) per interval. Index 0..2: 64QAM, 3..6: 256QAM.
+/// Max-log interval tables of the 64QAM / 256QAM demapper: per bit pair k (stream bits 2k, 2k + 1) the reciprocal
+/// interval width (the SIMD paths scale by it, avx2_helpers.h:178), a count and (slope, intercept) per interval
+/// (interleaved: one 8-byte LDS read per lookup). Index 0..2: 64QAM, 3..6: 256QAM.
 struct demap_pair_table {
-  float    width;
+  float    inv_width;
   uint32_t count;
-  float    slope[16];
-  float    intercept[16];
+  float    piece[16][2];
 };
 constexpr int DEMAP_TABLES = 7;
 

@@ -245,6 +245,22 @@ def main():
         if tj.get("slots_per_step") == S and tj.get("worst_case", False) == args.worst_case:
             traffic = tj.get("hbm_bytes_per_launch")
 
+    # Algorithmic HBM bytes per step of the signal-chain stages (each byte read or written once; DESIGN.md "Kernels"):
+    # bf16 grids are 4 B per RE, time samples 8 B (complex float), estimates 4 B per (layer, port, RE), LLRs 1 B.
+    P, nsc, L = cell.nof_ports, cell.nsc, ues[0].nof_layers
+    grid_b = S * P * 14 * nsc * 4
+    spp = ul.ofdm.nof_samples // (S * P)  # samples per slot and port (CPs included)
+    data_re = S * sum(12 * u.n_prb * (14 - 1) for u in ues)  # one DM-RS symbol without data
+    cw_b = sum(s.cw_length for s in segs) * S // 8
+    stage_bytes = {
+        "pdsch_dmrs_modulate": cw_b + grid_b,
+        "ofdm_modulate": grid_b + S * P * spp * 8,
+        "ofdm_demodulate": S * P * 14 * slotlib.DFT_SIZE * 8 + grid_b,
+        "pusch_channel_estimate": S * P * nsc * 4 + S * L * P * 14 * nsc * 4,
+        "pusch_demodulate": data_re * ((P + L * P) * 4 + L * ues[0].qm),
+    }
+    stage_gbps = {k: v / (stage[k] * 1e-3) / 1e9 for k, v in stage_bytes.items() if stage[k] > 0}
+
     result = {
         "metric": "PDSCH+PUSCH slots/sec (100MHz 4x4) + LDPC info-bits/s at 1/2/4/8 GPU",
         "value": value,
@@ -278,6 +294,7 @@ def main():
         "pusch_tb_success_rate": float(tb_ok.mean()),
         "ldpc_avg_iterations": avg_iters,
         "stage_ms_per_step": stage,
+        "stage_algorithmic_gbps": stage_gbps,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "ldpc_decode_pk_kernel<1,1,8>",
                      "kernel_ms_per_launch": dec_ms,

@@ -120,7 +120,8 @@ def demap(sym, nvar, qm):
     avg = {6: 42, 8: 170}[qm]
     a = F(1.0) / np.sqrt(F(avg))
     for kb, (wm, slopes, inters) in enumerate(interval_tables(qm)):
-        inv_width = F(1) / (F(wm) * a)  # scaled by the reciprocal width (avx2_helpers.h:178)
+        inv_width = F(1) / F(wm / np.sqrt(float(avg)))  # float INTERVAL_WIDTH = wm * M_SQRT1_<avg>; scaled by its
+        # reciprocal (demodulation_mapper_qam64.cpp:49, avx2_helpers.h:178)
         nint = len(slopes)
         sl = np.array([F(s) * a for s in slopes], F)
         ic = np.array([F(c) / F(avg // 2) for c in inters], F)

@@ -65,7 +65,8 @@ demap_pair_table pair_table(unsigned qm, unsigned k)
   const float a   = 1.0F / std::sqrt(static_cast<float>(avg));
   const int   step = mergeable ? 2 : 1;
   demap_pair_table t{};
-  t.inv_width = 1.0F / (static_cast<float>(2 * step) * a);
+  // INTERVAL_WIDTH = 2 (or 4) * M_SQRT1_42 / M_SQRT1_170 as a float; the SIMD demappers scale by its reciprocal.
+  t.inv_width = 1.0F / static_cast<float>(2.0 * step / std::sqrt(static_cast<double>(avg)));
   t.count = static_cast<uint32_t>(L / step);
   for (int i = 0; i < L / step; ++i) {
     t.piece[i][0] = static_cast<float>(slopes[static_cast<size_t>(i * step)]) * a;
@@ -172,6 +173,15 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
   }
   for (unsigned k = 0; k < 4; ++k) {
     tables.push_back(pair_table(8, k));
+  }
+  // The kernel shares one interval index among all bit pairs but the last (pusch_demodulator.hip demap).
+  for (unsigned first : {0u, 3u}) {
+    const unsigned np = first == 0 ? 3 : 4;
+    for (unsigned k = 1; k + 1 < np; ++k) {
+      if (tables[first + k].inv_width != tables[first].inv_width || tables[first + k].count != tables[first].count) {
+        return fail(SRSGPU_ERR_INVALID_ARG, "internal: demapper interval tables do not share their width");
+      }
+    }
   }
   std::lock_guard<std::mutex> lock(ctx->mtx);
   HIP_TRY(hipSetDevice(ctx->device));

@@ -97,53 +97,58 @@ __device__ __forceinline__ void demap(cpx s, float nvar, const demap_pair_table*
       llr[2 + k]      = nz ? 0 : quantize(l23 * rcp, 6.f);
     }
   } else {
+    // Every bit pair but the last shares its interval width and count (2a, 2^(QM/2) intervals; the last: 4a, half as
+    // many — demodulation_mapper_qam64.cpp:49/:62/:75, _qam256.cpp:48/:82/:116/:150; the host asserts it), so the
+    // interval index of the first pairs is computed once per component.
     const demap_pair_table* t = tab + (QM == 6 ? 0 : 3);
+    constexpr int           NP  = QM / 2;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const float x  = part[k];
-      const bool  nz = fabsf(x) <= 1e-9f;
+      const float x      = part[k];
+      const bool  nz     = fabsf(x) <= 1e-9f;
+      const int   cnt0   = static_cast<int>(t[0].count);
+      const int   idx0   = min(max(static_cast<int>(floorf(x * t[0].inv_width)) + cnt0 / 2, 0), cnt0 - 1);
+      const int   cntl   = static_cast<int>(t[NP - 1].count);
+      const int   idxl   = min(max(static_cast<int>(floorf(x * t[NP - 1].inv_width)) + cntl / 2, 0), cntl - 1);
 #pragma unroll
-      for (int kb = 0; kb < QM / 2; ++kb) {
-        const demap_pair_table& p   = t[kb];
-        const int               cnt = static_cast<int>(p.count);
-        int                     idx = static_cast<int>(floorf(x * p.inv_width)) + cnt / 2;
-        idx                         = min(max(idx, 0), cnt - 1);
-        const float2 sl             = *reinterpret_cast<const float2*>(p.piece[idx]);
-        const float  l              = (sl.x * x + sl.y) * rcp;
-        llr[2 * kb + k]             = nz ? 0 : quantize(l, 6.f);
+      for (int kb = 0; kb < NP; ++kb) {
+        const int    idx = (kb == NP - 1) ? idxl : idx0;
+        const float2 sl  = *reinterpret_cast<const float2*>(t[kb].piece[idx]);
+        const float  l   = (sl.x * x + sl.y) * rcp;
+        llr[2 * kb + k]  = nz ? 0 : quantize(l, 6.f);
       }
     }
   }
 }
 
-/// Unbiased linear MMSE for L layers: A = H^H H + nv I = R^H R (Cholesky, R upper triangular with a real diagonal),
-/// T = R^-1, A^-1 = T T^H: x = T (T^H H^H y), [A^-1]_ll = sum_j |T_lj|^2, g_l = 1 - nv [A^-1]_ll,
-/// eq_l = x_l / g_l, var_l = nv [A^-1]_ll / g_l.
 template <int L>
 __device__ __forceinline__ void equalize_mmse(const cpx* y, const cpx (*h)[4], uint32_t P, float nv, cpx* eq,
                                               float* var)
 {
+  // Ports p >= P hold zeros (load_re leaves them zero), so the sums run over all four without guards.
+  (void)P;
   cpx A[L][L], m[L];
 #pragma unroll
   for (int i = 0; i < L; ++i) {
+    float dsum = nv;
 #pragma unroll
-    for (int j = i; j < L; ++j) {
+    for (int p = 0; p < 4; ++p) {
+      dsum += h[i][p].x * h[i][p].x + h[i][p].y * h[i][p].y;
+    }
+    A[i][i] = cmk(dsum, 0.f);
+#pragma unroll
+    for (int j = i + 1; j < L; ++j) {
       cpx s = cmk(0.f, 0.f);
 #pragma unroll
-      for (uint32_t p = 0; p < 4; ++p) {
-        if (p < P) {
-          s = cadd(s, cmulc(h[j][p], h[i][p]));  // conj(h_ip) h_jp
-        }
+      for (int p = 0; p < 4; ++p) {
+        s = cadd(s, cmulc(h[j][p], h[i][p]));  // conj(h_ip) h_jp
       }
       A[i][j] = s;
     }
-    A[i][i].x += nv;
     cpx s = cmk(0.f, 0.f);
 #pragma unroll
-    for (uint32_t p = 0; p < 4; ++p) {
-      if (p < P) {
-        s = cadd(s, cmulc(y[p], h[i][p]));  // conj(h_ip) y_p
-      }
+    for (int p = 0; p < 4; ++p) {
+      s = cadd(s, cmulc(y[p], h[i][p]));  // conj(h_ip) y_p
     }
     m[i] = s;
   }
@@ -157,8 +162,7 @@ __device__ __forceinline__ void equalize_mmse(const cpx* y, const cpx (*h)[4], u
     for (int k = 0; k < i; ++k) {
       d -= R[k][i].x * R[k][i].x + R[k][i].y * R[k][i].y;
     }
-    const float rii = sqrtf(fmaxf(d, 0.f));
-    rinv[i]         = 1.f / rii;
+    rinv[i] = __builtin_amdgcn_rsqf(fmaxf(d, 0.f));  // 1 / R_ii (v_rsq, 1 ulp: the extension has no reference)
 #pragma unroll
     for (int j = i + 1; j < L; ++j) {
       cpx s = A[i][j];
@@ -206,7 +210,7 @@ __device__ __forceinline__ void equalize_mmse(const cpx* y, const cpx (*h)[4], u
     }
     const float g = 1.f - nv * aii;
     if (isnormal_f(g) && g > 0.f && isnormal_f(nv * aii)) {
-      const float rg = 1.f / g;
+      const float rg = __builtin_amdgcn_rcpf(g);
       eq[i]          = cscale(x, rg);
       var[i]         = (nv * aii) * rg;
     } else {
@@ -218,53 +222,110 @@ __device__ __forceinline__ void equalize_mmse(const cpx* y, const cpx (*h)[4], u
 
 /// Transmission parameters of a workgroup, uniform across it.
 struct demod_uniform {
-  const demod_desc* d;
-  uint32_t          re_begin, re_end, word0;
-  float             nv[4], nv_max;
+  const demod_desc*       d;
+  uint32_t                re_begin, re_end, word0;
+  float                   nv[4], nv_max;
+  const demap_pair_table* tables;                 ///< Global demapper tables (staged into LDS for Qm >= 6).
+  const uint32_t*         x1, *x2_jump, *x2_lane;  ///< Gold sequence tables.
 };
+
+/// Stages the chunk's descrambling words (and the first word of the next chunk) and, for 64/256QAM, the demapper
+/// tables in LDS. The caller synchronises.
+__device__ __forceinline__ void stage_chunk(const demod_uniform& u, uint32_t* seq, demap_pair_table* tab)
+{
+  const demod_desc& d      = *u.d;
+  const uint32_t    tid    = threadIdx.x;
+  const uint32_t    nwords = (d.nof_llrs + 31u) >> 5;
+  for (uint32_t j = tid; j < MOD_CHUNK_WORDS; j += DEMOD_THREADS) {
+    const uint32_t w = u.word0 + j;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(w >> 6);  // word0 % 64 == 0: wave-uniform jump
+    seq[j]           = (w < nwords) ? gold_word(d.c_init, w, c, u.x1, u.x2_jump, u.x2_lane) : 0u;
+  }
+  if (tid == 0) {
+    const uint32_t w2    = u.word0 + MOD_CHUNK_WORDS;
+    seq[MOD_CHUNK_WORDS] = (w2 < nwords) ? gold_word(d.c_init, w2, w2 >> 6, u.x1, u.x2_jump, u.x2_lane) : 0u;
+  }
+  if (d.qm >= 6) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(u.tables);
+    uint32_t*       dst = reinterpret_cast<uint32_t*>(tab);
+    for (uint32_t i = tid; i < DEMAP_TABLES * sizeof(demap_pair_table) / 4; i += DEMOD_THREADS) {
+      dst[i] = src[i];
+    }
+  }
+}
+
+/// Issues the loads of RE r: the P received values and the L x P channel estimates (raw bf16 pairs).
+template <int L>
+__device__ __forceinline__ void load_re(const demod_desc& d,
+                                        uint32_t          r,
+                                        const uint32_t* __restrict__ grids,
+                                        const uint32_t* __restrict__ ce,
+                                        uint32_t (&yw)[4],
+                                        uint32_t (&hw)[L][4])
+{
+  // Symbol and subcarrier of the RE.
+  uint32_t l = 0;
+#pragma unroll
+  for (int j = 1; j < 15; ++j) {
+    l += (d.sym_cum[j] <= r) ? 1u : 0u;
+  }
+  const uint32_t k = r - d.sym_cum[l];
+  uint32_t       sc;
+  if ((d.dmrs_mask >> l) & 1u) {
+    const uint32_t nd  = d.nd_dmrs;
+    const uint32_t prb = k / nd;
+    sc                 = prb * 12u + static_cast<uint32_t>((d.dmrs_lut >> (4u * (k - prb * nd))) & 15u);
+  } else {
+    sc = k;
+  }
+  const uint32_t ge = d.grid_base + l * d.nsc + sc;
+  const uint32_t ee = d.ce_base + l * d.nsc + sc;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (p < static_cast<int>(d.P)) {
+      yw[p] = grids[ge + p * d.port_stride];
+#pragma unroll
+      for (int ly = 0; ly < L; ++ly) {
+        hw[ly][p] = ce[ee + ly * d.ce_layer_stride + p * d.port_stride];
+      }
+    }
+  }
+}
 
 /// Every RE of the chunk owned by this lane: loads, equalization (L layers), demapping (QM bits per layer),
 /// descrambling and the packed LLR bytes into the LDS output buffer. L and QM are compile-time so that every register
 /// array has static indices and the RE's L * QM bytes are assembled in registers.
 template <int L, int QM>
 __device__ __forceinline__ void demod_res(const demod_uniform& u,
-                                          const demap_pair_table* tab,
+                                          demap_pair_table*    tab,
                                           const uint32_t* __restrict__ grids,
                                           const uint32_t* __restrict__ ce,
-                                          const uint32_t* seq,
+                                          uint32_t*       seq,
                                           uint32_t*       out32)
 {
   constexpr uint32_t LQ = L * QM;
   const demod_desc&  d  = *u.d;
   const uint32_t     P  = d.P;
   const bool         zf = d.eq == DEMOD_EQ_ZF;
-  for (uint32_t r = u.re_begin + threadIdx.x; r < u.re_end; r += DEMOD_THREADS) {
-    // Symbol and subcarrier of the RE.
-    uint32_t l = 0;
-#pragma unroll
-    for (int j = 1; j < 15; ++j) {
-      l += (d.sym_cum[j] <= r) ? 1u : 0u;
+  // The first RE's loads are in flight while the chunk's sequence is generated.
+  uint32_t r = u.re_begin + threadIdx.x;
+  uint32_t yw[4] = {}, hw[L][4] = {};
+  if (r < u.re_end) {
+    load_re<L>(d, r, grids, ce, yw, hw);
+  }
+  stage_chunk(u, seq, tab);
+  __syncthreads();
+  for (bool first = true; r < u.re_end; r += DEMOD_THREADS, first = false) {
+    if (!first) {
+      load_re<L>(d, r, grids, ce, yw, hw);
     }
-    const uint32_t k = r - d.sym_cum[l];
-    uint32_t       sc;
-    if ((d.dmrs_mask >> l) & 1u) {
-      const uint32_t nd  = d.nd_dmrs;
-      const uint32_t prb = k / nd;
-      sc                 = prb * 12u + static_cast<uint32_t>((d.dmrs_lut >> (4u * (k - prb * nd))) & 15u);
-    } else {
-      sc = k;
-    }
-    const uint32_t ge = d.grid_base + l * d.nsc + sc;
-    const uint32_t ee = d.ce_base + l * d.nsc + sc;
-    cpx            y[4], h[L][4];
+    cpx y[4], h[L][4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      if (p < static_cast<int>(P)) {
-        y[p] = bf16c(grids[ge + p * d.port_stride]);
+      y[p] = bf16c(yw[p]);
 #pragma unroll
-        for (int ly = 0; ly < L; ++ly) {
-          h[ly][p] = bf16c(ce[ee + ly * d.ce_layer_stride + p * d.port_stride]);
-        }
+      for (int ly = 0; ly < L; ++ly) {
+        h[ly][p] = bf16c(hw[ly][p]);
       }
     }
     cpx   eq[L];
@@ -363,9 +424,9 @@ __device__ __forceinline__ void demod_res(const demod_uniform& u,
 }
 
 template <int QM>
-__device__ __forceinline__ void demod_res_qm(const demod_uniform& u, const demap_pair_table* tab,
+__device__ __forceinline__ void demod_res_qm(const demod_uniform& u, demap_pair_table* tab,
                                              const uint32_t* __restrict__ grids, const uint32_t* __restrict__ ce,
-                                             const uint32_t* seq, uint32_t* out32)
+                                             uint32_t* seq, uint32_t* out32)
 {
   switch (u.d->L) {
     case 1: demod_res<1, QM>(u, tab, grids, ce, seq, out32); break;
@@ -392,28 +453,15 @@ __global__ __launch_bounds__(DEMOD_THREADS) void pusch_demodulate_kernel(const d
   const mod_chunk             ch     = chunks[blockIdx.x];
   const demod_desc&           d      = descs[ch.tx];
   const uint32_t              tid    = threadIdx.x;
-  const uint32_t              nwords = (d.nof_llrs + 31u) >> 5;
-  for (uint32_t j = tid; j < MOD_CHUNK_WORDS; j += DEMOD_THREADS) {
-    const uint32_t w = ch.word0 + j;
-    const uint32_t c = __builtin_amdgcn_readfirstlane(w >> 6);  // word0 % 64 == 0: wave-uniform jump
-    seq[j]           = (w < nwords) ? gold_word(d.c_init, w, c, x1, x2_jump, x2_lane) : 0u;
-  }
-  if (tid == 0) {
-    const uint32_t w2    = ch.word0 + MOD_CHUNK_WORDS;
-    seq[MOD_CHUNK_WORDS] = (w2 < nwords) ? gold_word(d.c_init, w2, w2 >> 6, x1, x2_jump, x2_lane) : 0u;
-  }
-  if (d.qm >= 6) {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(tables);
-    uint32_t*       dst = reinterpret_cast<uint32_t*>(tab);
-    for (uint32_t i = tid; i < sizeof(tab) / 4; i += DEMOD_THREADS) {
-      dst[i] = src[i];
-    }
-  }
   demod_uniform u;
   u.d        = &d;
   u.re_begin = ch.re_begin;
   u.re_end   = ch.re_end;
   u.word0    = ch.word0;
+  u.tables   = tables;
+  u.x1       = x1;
+  u.x2_jump  = x2_jump;
+  u.x2_lane  = x2_lane;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     u.nv[p] = noise_var[4 * d.tx + p];
@@ -423,7 +471,6 @@ __global__ __launch_bounds__(DEMOD_THREADS) void pusch_demodulate_kernel(const d
   for (uint32_t p = 1; p < 4; ++p) {
     u.nv_max = (p < d.P) ? fmaxf(u.nv_max, u.nv[p]) : u.nv_max;
   }
-  __syncthreads();
 
   switch (d.qm) {
     case 2: demod_res_qm<2>(u, tab, grids, ce, seq, out32); break;

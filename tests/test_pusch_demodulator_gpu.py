@@ -4,8 +4,8 @@ and the numpy restatement (oracle/pusch_demod_oracle.py).
 
 Tolerances (soft LLRs, floating point): for the reference's paths (ZF 1 x N, ZF 2 x N, MMSE with one layer) every
 LLR equal or one quantisation step (20 / 120) apart, < 5 % differing (the reference's AVX2 equalizer uses an
-approximate reciprocal; the GPU divides exactly). For the multi-layer MMSE extension (float32 Gauss-Jordan on the GPU
-vs float64 numpy): >= 99 % of the LLRs within one step and the hard decisions (signs) of >= 99.5 % equal."""
+approximate reciprocal; the GPU divides exactly). For the multi-layer MMSE extension (float32
+Cholesky on the GPU vs float64 numpy): >= 99 % of the LLRs within one step and the hard decisions (signs) of >= 99.5 % equal."""
 import numpy as np
 import pytest
 

@@ -252,12 +252,14 @@ def main():
     spp = ul.ofdm.nof_samples // (S * P)  # samples per slot and port (CPs included)
     data_re = S * sum(12 * u.n_prb * (14 - 1) for u in ues)  # one DM-RS symbol without data
     cw_b = sum(s.cw_length for s in segs) * S // 8
+    ce_rows = 1 if ul.estimate_layout == srsgpu.CE_COMPACT else 14  # estimate rows per (layer, port) and slot
+    ce_b = S * L * P * ce_rows * nsc * 4
     stage_bytes = {
         "pdsch_dmrs_modulate": cw_b + grid_b,
         "ofdm_modulate": grid_b + S * P * spp * 8,
         "ofdm_demodulate": S * P * 14 * slotlib.DFT_SIZE * 8 + grid_b,
-        "pusch_channel_estimate": S * P * nsc * 4 + S * L * P * 14 * nsc * 4,
-        "pusch_demodulate": data_re * ((P + L * P) * 4 + L * ues[0].qm),
+        "pusch_channel_estimate": S * P * nsc * 4 + ce_b,
+        "pusch_demodulate": data_re * (P * 4 + L * ues[0].qm) + ce_b,
     }
     stage_gbps = {k: v / (stage[k] * 1e-3) / 1e9 for k, v in stage_bytes.items() if stage[k] > 0}
 
@@ -279,6 +281,8 @@ def main():
                    "dl_chain": "PDSCH encoder -> PDSCH DM-RS -> PDSCH modulator -> OFDM modulator (4 ports)",
                    "ul_chain": "OFDM demodulator (4 ports) -> DM-RS channel estimator (4 layers x 4 ports) -> PUSCH "
                                "demodulator (MMSE 4x4) -> PUSCH decoder",
+                   "channel_estimate_layout": "compact (one row per allocation, average time strategy)"
+                                              if ul.estimate_layout == srsgpu.CE_COMPACT else "per symbol",
                    "leg_streams": "one stream" if args.serial_legs else "DL and UL on concurrent streams",
                    "slots_per_step": S,
                    "codeblocks_per_step_per_direction": int(sum(s.nof_segments for s in segs) * S),

@@ -385,6 +385,13 @@ void srsgpu_ofdm_plan_destroy(srsgpu_ofdm_plan* plan);
 #define SRSGPU_CHEST_FD_MEAN 1
 #define SRSGPU_CHEST_FD_FILTER 2
 
+/* Channel-estimate layouts (estimate_layout of the estimator and demodulator configurations). PER_SYMBOL is the
+ * reference's channel_estimate: every allocated symbol holds its estimate. COMPACT stores, with the "average" time
+ * strategy (one estimate for all the symbols of the allocation), only the row of start_symbol, and the demodulator
+ * reads that row for every symbol: identical LLRs with 1/nof_symbols of the estimate traffic. */
+#define SRSGPU_CE_PER_SYMBOL 0
+#define SRSGPU_CE_COMPACT 1
+
 typedef struct {
   uint16_t scrambling_id;    /* N_ID^{n_SCID}, 0..65535 */
   uint8_t  n_scid;           /* 0 or 1 */
@@ -398,7 +405,8 @@ typedef struct {
   uint16_t nof_rb;
   uint16_t slot_index;       /* n_slot within the frame (DM-RS c_init) */
   uint8_t  fd_smoothing;     /* SRSGPU_CHEST_FD_* */
-  uint8_t  pad[3];
+  uint8_t  estimate_layout;  /* SRSGPU_CE_PER_SYMBOL or SRSGPU_CE_COMPACT */
+  uint8_t  pad[2];
   float    scaling;          /* beta_PUSCH^DMRS (DM-RS amplitude relative to data), > 0 */
   uint32_t grid_index;       /* slot of the rx grid and of the estimate buffer */
 } srsgpu_pusch_chest_config;
@@ -440,7 +448,8 @@ typedef struct {
   uint16_t dmrs_symbol_mask;            /* bit l = OFDM symbol l carries DM-RS */
   uint16_t rb_start;                    /* contiguous CRB allocation [rb_start, rb_start + nof_rb) (rb_mask) */
   uint16_t nof_rb;
-  uint16_t pad;
+  uint8_t  estimate_layout;             /* SRSGPU_CE_PER_SYMBOL or SRSGPU_CE_COMPACT (as the estimator wrote it) */
+  uint8_t  pad;
   uint32_t grid_index;                  /* slot (rx grid and channel estimate) of the transmission */
   uint32_t llr_offset;                  /* first codeword LLR in the output buffer */
 } srsgpu_pusch_demod_config;

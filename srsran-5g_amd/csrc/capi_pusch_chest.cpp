@@ -64,7 +64,8 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid layers / ports / DM-RS type", t);
     }
     if (c.nof_symbols < 1 || c.start_symbol + c.nof_symbols > 14 || c.nof_rb < 1 ||
-        c.rb_start + c.nof_rb > grid_nof_prb || !(c.scaling > 0.f) || c.fd_smoothing > SRSGPU_CHEST_FD_FILTER) {
+        c.rb_start + c.nof_rb > grid_nof_prb || !(c.scaling > 0.f) || c.fd_smoothing > SRSGPU_CHEST_FD_FILTER ||
+        c.estimate_layout > SRSGPU_CE_COMPACT) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid allocation, scaling or smoothing strategy", t);
     }
     std::vector<unsigned> dmrs;
@@ -141,7 +142,7 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
         jb.interp_offset = static_cast<uint8_t>(t2 ? 2 * g : g);
         jb.interp_stride = static_cast<uint8_t>(stride);
         jb.first_symbol  = c.start_symbol;
-        jb.nof_symbols   = c.nof_symbols;
+        jb.nof_symbols   = c.estimate_layout == SRSGPU_CE_COMPACT ? 1 : c.nof_symbols;  // compact: start_symbol's row
         jobs.push_back(jb);
       }
     }

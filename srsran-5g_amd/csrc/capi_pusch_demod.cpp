@@ -113,7 +113,7 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
     }
     if (c.nof_symbols < 1 || c.start_symbol + c.nof_symbols > 14 || (c.dmrs_type != 1 && c.dmrs_type != 2) ||
         c.nof_cdm_groups_without_data < 1 || c.nof_cdm_groups_without_data > (c.dmrs_type == 1 ? 2 : 3) ||
-        c.n_id > 1023 || c.nof_rb < 1 || c.rb_start + c.nof_rb > grid_nof_prb) {
+        c.n_id > 1023 || c.nof_rb < 1 || c.rb_start + c.nof_rb > grid_nof_prb || c.estimate_layout > SRSGPU_CE_COMPACT) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid time / frequency allocation or DM-RS configuration", t);
     }
     demod_desc d{};
@@ -146,6 +146,10 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
     d.nsc             = nsc;
     d.ce_layer_stride = static_cast<uint32_t>(slot_elems);
     d.ce_base         = static_cast<uint32_t>(c.grid_index * slot_elems * 4u) + c.rb_start * 12u;
+    d.ce_compact      = c.estimate_layout == SRSGPU_CE_COMPACT ? 1 : 0;
+    if (d.ce_compact) {
+      d.ce_base += c.start_symbol * nsc;  // the estimator's single row (srsgpu_pusch_chest_config::estimate_layout)
+    }
     d.llr_offset      = c.llr_offset;
     d.nof_llrs        = nre * Lq;
     d.c_init          = (static_cast<uint32_t>(c.rnti) << 15) + c.n_id;  // pusch_demodulator_impl.cpp:279

@@ -279,7 +279,7 @@ __device__ __forceinline__ void load_re(const demod_desc& d,
     sc = k;
   }
   const uint32_t ge = d.grid_base + l * d.nsc + sc;
-  const uint32_t ee = d.ce_base + l * d.nsc + sc;
+  const uint32_t ee = d.ce_base + (d.ce_compact ? 0u : l * d.nsc) + sc;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     if (p < static_cast<int>(d.P)) {

@@ -269,7 +269,7 @@ struct demod_desc {
   uint8_t  qm, L, P;        ///< Modulation order, layers, rx ports.
   uint8_t  nd_dmrs;         ///< Data REs per PRB on DM-RS symbols.
   uint8_t  eq;              ///< Equalizer kind (DEMOD_EQ_*).
-  uint8_t  pad;
+  uint8_t  ce_compact;      ///< Estimates in the compact layout: every symbol reads the row at ce_base.
   uint16_t sym_cum[16];     ///< Data REs in the symbols before symbol l (l = 0..14).
 };
 static_assert(sizeof(demod_desc) == 88, "demod_desc layout");

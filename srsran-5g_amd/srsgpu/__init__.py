@@ -196,7 +196,8 @@ class PuschDemodConfig(ctypes.Structure):
         ("dmrs_symbol_mask", ctypes.c_uint16),
         ("rb_start", ctypes.c_uint16),
         ("nof_rb", ctypes.c_uint16),
-        ("pad", ctypes.c_uint16),
+        ("estimate_layout", ctypes.c_uint8),
+        ("pad", ctypes.c_uint8),
         ("grid_index", ctypes.c_uint32),
         ("llr_offset", ctypes.c_uint32),
     ]
@@ -220,7 +221,8 @@ class PuschChestConfig(ctypes.Structure):
         ("nof_rb", ctypes.c_uint16),
         ("slot_index", ctypes.c_uint16),
         ("fd_smoothing", ctypes.c_uint8),
-        ("pad", ctypes.c_uint8 * 3),
+        ("estimate_layout", ctypes.c_uint8),
+        ("pad", ctypes.c_uint8 * 2),
         ("scaling", ctypes.c_float),
         ("grid_index", ctypes.c_uint32),
     ]
@@ -228,6 +230,7 @@ class PuschChestConfig(ctypes.Structure):
 
 assert ctypes.sizeof(PuschChestConfig) == 28
 CHEST_FD_NONE, CHEST_FD_MEAN, CHEST_FD_FILTER = 0, 1, 2
+CE_PER_SYMBOL, CE_COMPACT = 0, 1  # channel-estimate layouts (SRSGPU_CE_*)
 EQ_ZF, EQ_MMSE = 0, 1
 
 
@@ -893,6 +896,7 @@ class PuschDemodulation:
     rb_start: int
     nof_rb: int
     equalizer: int = EQ_ZF
+    estimate_layout: int = CE_PER_SYMBOL
 
     def nof_llrs(self) -> int:
         dm = (4 if self.dmrs_type == 2 else 6) * self.nof_cdm_groups_without_data
@@ -912,6 +916,7 @@ def make_pusch_demod_configs(demods: Sequence[PuschDemodulation], grid_index: Se
         a.dmrs_type, a.nof_cdm_groups_without_data, a.equalizer = (m.dmrs_type, m.nof_cdm_groups_without_data,
                                                                    m.equalizer)
         a.dmrs_symbol_mask, a.rb_start, a.nof_rb, a.grid_index = m.dmrs_symbol_mask, m.rb_start, m.nof_rb, g
+        a.estimate_layout = m.estimate_layout
         a.llr_offset = off if llr_offsets is None else llr_offsets[i]
         offs.append(a.llr_offset)
         off += m.nof_llrs()
@@ -994,6 +999,7 @@ class PuschChannelEstimation:
     slot_index: int
     scaling: float = 1.0
     fd_smoothing: int = CHEST_FD_FILTER
+    estimate_layout: int = CE_PER_SYMBOL
 
 
 def make_pusch_chest_configs(ests: Sequence[PuschChannelEstimation], grid_index: Sequence[int]):
@@ -1003,6 +1009,7 @@ def make_pusch_chest_configs(ests: Sequence[PuschChannelEstimation], grid_index:
         a.scrambling_id, a.n_scid, a.dmrs_type, a.nof_tx_layers = e.scrambling_id, e.n_scid, e.dmrs_type, e.nof_tx_layers
         a.nof_rx_ports, a.start_symbol, a.nof_symbols = e.nof_rx_ports, e.start_symbol, e.nof_symbols
         a.dmrs_symbol_mask, a.rb_start, a.nof_rb, a.slot_index = e.dmrs_symbol_mask, e.rb_start, e.nof_rb, e.slot_index
+        a.estimate_layout = e.estimate_layout
         a.fd_smoothing, a.scaling, a.grid_index = e.fd_smoothing, e.scaling, g
     return arr
 

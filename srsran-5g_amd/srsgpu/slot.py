@@ -118,11 +118,13 @@ class DownlinkPipeline:
 
 class UplinkPipeline:
     """OFDM demodulator -> DM-RS channel estimator -> PUSCH demodulator -> PUSCH decoder for every UE of every slot.
-    The channel-estimate, noise-variance, LLR, HARQ and TB buffers are owned by the pipeline."""
+    The channel-estimate, noise-variance, LLR, HARQ and TB buffers are owned by the pipeline. `estimate_layout`:
+    srsgpu.CE_COMPACT (default: the "average" strategy's one estimate per allocation, stored once) or
+    srsgpu.CE_PER_SYMBOL (the reference's channel_estimate layout); the LLRs are identical."""
 
     def __init__(self, ctx, cell: CellSlots, iterations=6, rnti0=0x4601, n_id=500, scrambling_id=500,
-                 equalizer=srsgpu.EQ_MMSE):
-        self.ctx, self.cell = ctx, cell
+                 equalizer=srsgpu.EQ_MMSE, estimate_layout=srsgpu.CE_COMPACT):
+        self.ctx, self.cell, self.estimate_layout = ctx, cell, estimate_layout
         S, ues, segs = cell.nof_slots, cell.ues, cell.segs
         rb0 = cell.rb_starts()
         dev = torch.device("cuda", ctx.device)
@@ -134,12 +136,13 @@ class UplinkPipeline:
                 ests.append(srsgpu.PuschChannelEstimation(
                     scrambling_id=scrambling_id, n_scid=0, dmrs_type=1, nof_tx_layers=u.nof_layers,
                     nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=1 << DMRS_SYMBOL,
-                    rb_start=rb0[i], nof_rb=u.n_prb, slot_index=cell.slot_index(s), scaling=DMRS_BETA))
+                    rb_start=rb0[i], nof_rb=u.n_prb, slot_index=cell.slot_index(s), scaling=DMRS_BETA,
+                    estimate_layout=estimate_layout))
                 dems.append(srsgpu.PuschDemodulation(
                     rnti=rnti0 + i, n_id=n_id, modulation_order=u.qm, nof_tx_layers=u.nof_layers,
                     nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=1 << DMRS_SYMBOL,
                     dmrs_type=1, nof_cdm_groups_without_data=2, rb_start=rb0[i], nof_rb=u.n_prb,
-                    equalizer=equalizer))
+                    equalizer=equalizer, estimate_layout=estimate_layout))
                 grid_idx.append(s)
         self.chest = srsgpu.PuschChannelEstimatorPlan(ctx, srsgpu.make_pusch_chest_configs(ests, grid_idx),
                                                       cell.grid_prb, cell.nof_ports)

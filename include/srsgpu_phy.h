@@ -536,9 +536,11 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
 
 void srsgpu_pusch_decoder_plan_destroy(srsgpu_pusch_decoder_plan* plan);
 
-/** Stage timing: when enabled, every execute records HIP events on its stream around the three kernel stages
- *  (0: rate dematching, 1: LDPC decoding, 2: TB assembly + CRC). stage_times synchronises on them and returns the
- *  accumulated milliseconds per stage (ms[3]) and the number of executes since the previous call. */
+/** Stage timing: with enable = 1 every execute records HIP events on its stream around the three kernel stages
+ *  (0: rate dematching, 1: LDPC decoding, 2: TB assembly + CRC); with enable = 2 only around the decoding stage (two
+ *  events: the least perturbation of a timed run); 0 disables. stage_times synchronises on them and returns the
+ *  accumulated milliseconds per stage (ms[3], stages not timed read 0) and the number of executes since the previous
+ *  call. */
 int srsgpu_pusch_decoder_plan_enable_timing(srsgpu_pusch_decoder_plan* plan, int enable);
 int srsgpu_pusch_decoder_plan_stage_times(srsgpu_pusch_decoder_plan* plan, float* ms, uint32_t* nof_executes);
 

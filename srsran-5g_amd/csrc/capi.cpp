@@ -79,7 +79,8 @@ struct srsgpu_pdsch_encoder_plan {
 };
 
 struct srsgpu_pusch_decoder_plan {
-  mutable stage_timer   timer;
+  mutable stage_timer   timer;      ///< Three stages (enable_timing 1).
+  mutable stage_timer   timer_dec;  ///< The decoding stage only (enable_timing 2): two events per execute.
   srsgpu_context*       ctx     = nullptr;
   srsgpu_pusch_cb_plan* cbs     = nullptr;
   tb_dec_desc*          d_tb    = nullptr;
@@ -1053,15 +1054,18 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
   auto  s  = static_cast<hipStream_t>(stream);
-  auto* ev = plan->timer.begin();
+  auto* ev  = plan->timer.begin();
+  auto* evd = plan->timer_dec.begin();
   stage_timer::mark(ev, 0, s);
   launch_rate_dematch(plan->cbs->impl, plan->cbs->d_dm, plan->cbs->nof_cbs, d_llrs, d_harq, d_cb_crc_ok, s);
   HIP_TRY(hipGetLastError());
   stage_timer::mark(ev, 1, s);
+  stage_timer::mark(evd, 0, s);
   int r = execute_decoder_plan(plan->cbs->dec, d_harq, d_cb_msgs, d_cb_nof_iterations, d_cb_crc_ok, s);
   if (r != SRSGPU_OK) {
     return r;
   }
+  stage_timer::mark(evd, 1, s);
   stage_timer::mark(ev, 2, s);
   launch_pusch_tb(plan->d_tb, plan->nof_tbs, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, plan->ctx->d_crc_arena, s);
   HIP_TRY(hipGetLastError());
@@ -1074,8 +1078,10 @@ int srsgpu_pusch_decoder_plan_enable_timing(srsgpu_pusch_decoder_plan* plan, int
   if (plan == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  plan->timer.stages  = 3;
-  plan->timer.enabled = enable != 0;
+  plan->timer.stages      = 3;
+  plan->timer.enabled     = enable == 1;
+  plan->timer_dec.stages  = 1;
+  plan->timer_dec.enabled = enable == 2;
   return SRSGPU_OK;
 }
 
@@ -1084,10 +1090,15 @@ int srsgpu_pusch_decoder_plan_stage_times(srsgpu_pusch_decoder_plan* plan, float
   if (plan == nullptr || ms == nullptr || nof_executes == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  plan->timer.stages = 3;
-  if (plan->timer.collect(ms, nof_executes) != 0) {
+  plan->timer.stages     = 3;
+  plan->timer_dec.stages = 1;
+  float    dec_ms = 0;
+  uint32_t n = 0, n_dec = 0;
+  if (plan->timer.collect(ms, &n) != 0 || plan->timer_dec.collect(&dec_ms, &n_dec) != 0) {
     return fail(SRSGPU_ERR_HIP, "event synchronisation failed");
   }
+  ms[1] += dec_ms;
+  *nof_executes = n > n_dec ? n : n_dec;
   return SRSGPU_OK;
 }
 

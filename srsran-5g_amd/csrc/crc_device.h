@@ -111,4 +111,70 @@ __device__ inline uint32_t block_crc_table(const uint8_t* data, int nbytes, cons
   return crc;
 }
 
+/// Byte table of a CRC (order 8..24, g including x^order) in LDS: lut[t] = t(x) x^order mod g, the remainder update
+/// of one byte. Every lane of the workgroup must call it (it ends with a barrier).
+__device__ inline void crc_byte_lut(uint32_t* lut, int order, uint32_t g)
+{
+  const uint32_t mask = (1u << order) - 1u;
+  for (uint32_t t = threadIdx.x; t < 256u; t += blockDim.x) {
+    uint32_t r = t << (order - 8);
+    for (int k = 0; k < 8; ++k) {
+      r <<= 1;
+      if (r & (1u << order)) {
+        r ^= g;
+      }
+    }
+    lut[t] = r & mask;
+  }
+  __syncthreads();
+}
+
+/// CRC of data[0..nbytes) (global or LDS) by chunks: every lane runs the byte-table CRC over CS-byte chunks, then
+/// moves each chunk remainder r to the end of the message with the per-bit contribution table P of the message length
+/// L = 8 nbytes: r(x) x^(8 (nbytes - end)) mod g = XOR over the set bits b of r of P[8 end + order - 1 - b] (P[j] =
+/// x^(order + L - 1 - j) mod g; indices j >= L stand for x^(order + L - 1 - j) < x^order itself). Per byte this reads
+/// order * 4 / CS bytes of table instead of the 32 of block_crc_table. `lut` from crc_byte_lut; `red` one word per
+/// wave of LDS scratch. All lanes must call it; returns the CRC in every lane.
+template <int CS, typename Data>
+__device__ inline uint32_t block_crc_chunks(Data data, int nbytes, const uint32_t* P, int order, const uint32_t* lut,
+                                            uint32_t* red)
+{
+  const uint32_t mask = (1u << order) - 1u;
+  const int      L    = 8 * nbytes;
+  const int      nch  = (nbytes + CS - 1) / CS;
+  uint32_t       acc  = 0;
+  for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+    const int b0  = c * CS;
+    const int b1  = min(b0 + CS, nbytes);
+    uint32_t  rem = 0;
+    for (int i = b0; i < b1; ++i) {
+      rem = ((rem << 8) ^ lut[((rem >> (order - 8)) ^ static_cast<uint32_t>(data(i))) & 0xffu]) & mask;
+    }
+    if (b1 == nbytes) {
+      acc ^= rem;  // the last chunk is already at the end of the message
+    } else {
+      const int jb = 8 * b1 + order - 1;
+#pragma unroll
+      for (int b = 0; b < 24; ++b) {
+        if (b < order) {
+          const int      j  = jb - b;
+          const uint32_t pj = (j < L) ? P[j] : (1u << (order + L - 1 - j));
+          acc ^= ((rem >> b) & 1u) ? pj : 0u;
+        }
+      }
+    }
+  }
+  acc = wave_xor(acc);
+  if ((threadIdx.x % WAVE) == 0) {
+    red[threadIdx.x / WAVE] = acc;
+  }
+  __syncthreads();
+  uint32_t crc = 0;
+  for (int w = 0; w < static_cast<int>((blockDim.x + WAVE - 1) / WAVE); ++w) {
+    crc ^= red[w];
+  }
+  __syncthreads();
+  return crc;
+}
+
 } // namespace srsgpu

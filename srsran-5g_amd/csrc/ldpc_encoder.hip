@@ -59,10 +59,18 @@ __global__ __launch_bounds__(256) void tb_crc_kernel(const tb_crc_desc* __restri
   __shared__ uint32_t part[256];
   const tb_crc_desc d = descs[blockIdx.x];
   // Per-bit contribution table when the plan could cache one for this length, else the byte-table method.
-  const uint32_t crc = (d.table != NO_CRC_TABLE)
-                           ? block_crc_table(tbs + d.byte_offset, static_cast<int>(d.nbytes), crc_tables + d.table, part)
-                           : block_crc_bytes(tbs + d.byte_offset, static_cast<int>(d.nbytes),
-                                             static_cast<int>(d.order), d.poly, table, part);
+  // Chunked byte-table CRC moved by the per-bit contribution table when the plan could cache one for this length,
+  // else the byte table with pairwise GF(2) combination.
+  uint32_t crc;
+  if (d.table != NO_CRC_TABLE) {
+    crc_byte_lut(table, static_cast<int>(d.order), d.poly);
+    const uint8_t* tb = tbs + d.byte_offset;
+    crc = block_crc_chunks<16>([tb](int i) { return tb[i]; }, static_cast<int>(d.nbytes), crc_tables + d.table,
+                               static_cast<int>(d.order), table, part);
+  } else {
+    crc = block_crc_bytes(tbs + d.byte_offset, static_cast<int>(d.nbytes), static_cast<int>(d.order), d.poly, table,
+                          part);
+  }
   if (threadIdx.x == 0) {
     crcs[blockIdx.x] = crc;
   }
@@ -121,6 +129,8 @@ __global__ __launch_bounds__(384) void pdsch_encode_kernel(const enc_desc* __res
   __shared__ uint8_t  lam[4 * S];
   __shared__ uint16_t sh[G::NE];
   __shared__ uint32_t red[8];
+  __shared__ uint32_t lut[256];
+  __shared__ uint8_t  msg[G::K * 384 / 8];  // packed message bytes (byte path): input of the CB CRC
 
   const enc_desc d  = descs[blockIdx.x];
   const int      Z  = d.Z;
@@ -133,7 +143,35 @@ __global__ __launch_bounds__(384) void pdsch_encode_kernel(const enc_desc* __res
   const uint8_t* tb      = tbs + d.tb_byte_offset;
   const uint32_t tb_crc  = tb_crcs[d.tb_index];
   const int      ndata   = d.nof_data;
-  for (int i = threadIdx.x; i < KZ; i += blockDim.x) {
+  // Byte path: TS 38.214 TB sizes make every codeblock's data byte-aligned ((TBS + 24) is a multiple of 8 C), so the
+  // message is whole TB / TB CRC bytes; they are also kept packed for the CB CRC.
+  const bool byte_path = ((d.tb_bit_offset | static_cast<uint32_t>(ndata) | d.tb_bits | d.tb_crc_len) & 7u) == 0 &&
+                         (d.crc_table == NO_CRC_TABLE || (d.used & 7u) == 0);
+  int first_bit = 0;  // bits below are written by the byte path
+  if (byte_path) {
+    const int nmsg = (d.crc_table != NO_CRC_TABLE) ? static_cast<int>(d.used) / 8 : ndata / 8;
+    for (int q = threadIdx.x; q < nmsg; q += blockDim.x) {
+      uint32_t byte = 0;
+      if (8 * q < ndata) {
+        const uint32_t p = d.tb_bit_offset + 8u * static_cast<uint32_t>(q);
+        byte = (p < d.tb_bits) ? tb[p >> 3] : (tb_crc >> (d.tb_crc_len - 8u - (p - d.tb_bits))) & 0xffu;
+      }
+      msg[q]       = static_cast<uint8_t>(byte);
+      const int i0 = 8 * q;
+      int       col = static_cast<int>(__umulhi(static_cast<uint32_t>(i0), d.div_magic));
+      int       l   = i0 - col * Z;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        bits[col * S + l] = static_cast<uint8_t>((byte >> (7 - k)) & 1u);
+        if (++l == Z) {
+          l = 0;
+          ++col;
+        }
+      }
+    }
+    first_bit = 8 * nmsg;
+  }
+  for (int i = first_bit + static_cast<int>(threadIdx.x); i < KZ; i += blockDim.x) {
     uint32_t bit = 0;
     if (i < ndata) {
       const uint32_t p = d.tb_bit_offset + static_cast<uint32_t>(i);
@@ -143,23 +181,31 @@ __global__ __launch_bounds__(384) void pdsch_encode_kernel(const enc_desc* __res
     const int col = static_cast<int>(__umulhi(static_cast<uint32_t>(i), d.div_magic));
     bits[col * S + (i - col * Z)] = static_cast<uint8_t>(bit);
   }
+  if (byte_path && d.crc_table != NO_CRC_TABLE) {
+    crc_byte_lut(lut, 24, 0x1800063u);  // CRC24B; ends with a barrier (msg and bits complete)
+  }
   __syncthreads();
-  // ---- Codeblock CRC24B over the first `used` bits: XOR of per-bit contributions (table per length). ----
+  // ---- Codeblock CRC24B over the first `used` bits. ----
   if (d.crc_table != NO_CRC_TABLE) {
-    const uint32_t* P   = crc_tables + d.crc_table;
-    uint32_t        acc = 0;
-    for (int i = threadIdx.x; i < d.used; i += blockDim.x) {
-      const int col = static_cast<int>(__umulhi(static_cast<uint32_t>(i), d.div_magic));
-      acc ^= bits[col * S + (i - col * Z)] ? P[i] : 0u;
-    }
-    acc = wave_xor(acc);
-    if ((threadIdx.x % WAVE) == 0) {
-      red[threadIdx.x / WAVE] = acc;
-    }
-    __syncthreads();
-    uint32_t crc = 0;
-    for (int w = 0; w < static_cast<int>(blockDim.x / WAVE); ++w) {
-      crc ^= red[w];
+    const uint32_t* P = crc_tables + d.crc_table;
+    uint32_t        crc;
+    if (byte_path) {
+      crc = block_crc_chunks<16>([](int q) { return msg[q]; }, static_cast<int>(d.used) / 8, P, 24, lut, red);
+    } else {  // XOR of per-bit contributions (table per length)
+      uint32_t acc = 0;
+      for (int i = threadIdx.x; i < d.used; i += blockDim.x) {
+        const int col = static_cast<int>(__umulhi(static_cast<uint32_t>(i), d.div_magic));
+        acc ^= bits[col * S + (i - col * Z)] ? P[i] : 0u;
+      }
+      acc = wave_xor(acc);
+      if ((threadIdx.x % WAVE) == 0) {
+        red[threadIdx.x / WAVE] = acc;
+      }
+      __syncthreads();
+      crc = 0;
+      for (int w = 0; w < static_cast<int>(blockDim.x / WAVE); ++w) {
+        crc ^= red[w];
+      }
     }
     for (int k = threadIdx.x; k < 24; k += blockDim.x) {
       const int i   = d.used + k;

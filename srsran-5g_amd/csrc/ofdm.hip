@@ -76,10 +76,32 @@ __device__ __forceinline__ void dft_reg(float2* v)
   }
 }
 
+/// Twiddles W^(r k) = exp(S 2 pi i r k / (NS R)), r = 1..R-1, of the butterflies this thread runs in a pass with
+/// radix R after passes of total radix NS (k = j mod NS); the table holds exp(-2 pi i m / OFDM_MAX_DFT). Loaded at
+/// kernel start for every pass, so their L2 latency hides under the first pass's HBM loads.
+template <int N, int R, int NS, int S>
+__device__ __forceinline__ void load_twiddles(const float2* __restrict__ tw, float2 (&w)[16 / R][R])
+{
+  constexpr int T   = N / 16;
+  const int     tid = static_cast<int>(threadIdx.x);
+#pragma unroll
+  for (int b = 0; b < 16 / R; ++b) {
+    const int k = (tid + b * T) & (NS - 1);
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      float2 x = tw[(r * k) * static_cast<int>(OFDM_MAX_DFT / (NS * R))];
+      if constexpr (S > 0) {
+        x.y = -x.y;
+      }
+      w[b][r] = x;
+    }
+  }
+}
+
 /// One Stockham pass of radix R over N points (NS = product of the previous passes' radices): butterfly j takes
-/// x[j + r N / R], twiddles by W^(r k), k = j mod NS, and writes X[(j - k) R + k + r NS].
+/// x[j + r N / R], twiddles by W^(r k) (preloaded in w), k = j mod NS, and writes X[(j - k) R + k + r NS].
 template <int N, int R, int NS, int S, typename Src, typename Dst>
-__device__ __forceinline__ void stockham_pass(const float2* __restrict__ tw, Src src, Dst dst)
+__device__ __forceinline__ void stockham_pass(const float2 (&w)[16 / R][R], Src src, Dst dst)
 {
   constexpr int T = N / 16;
   constexpr int B = 16 / R;
@@ -101,12 +123,7 @@ __device__ __forceinline__ void stockham_pass(const float2* __restrict__ tw, Src
     if constexpr (NS > 1) {
 #pragma unroll
       for (int r = 1; r < R; ++r) {
-        // W = exp(S 2 pi i r k / (NS R)); the table holds exp(-2 pi i m / OFDM_MAX_DFT).
-        float2 w = tw[(r * k) * static_cast<int>(OFDM_MAX_DFT / (NS * R))];
-        if constexpr (S > 0) {
-          w.y = -w.y;
-        }
-        v[b][r] = cmul(v[b][r], w);
+        v[b][r] = cmul(v[b][r], w[b][r]);
       }
     }
     dft_reg<R, S>(v[b]);
@@ -129,16 +146,24 @@ __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ 
   auto          ld   = [lds](int i) { return lds[i]; };
   auto          st   = [lds](int i, float2 v) { lds[i] = v; };
   static_assert(NP >= 2 && NP <= 4, "supported DFT sizes: 256..8192");
-  stockham_pass<N, R0, 1, S>(tw, src_first, st);
+  float2 w0[16 / R0][R0], w1[1][16], w2[1][16], w3[1][16];
+  load_twiddles<N, 16, R0, S>(tw, w1);
+  if constexpr (NP >= 3) {
+    load_twiddles<N, 16, R0 * 16, S>(tw, w2);
+  }
+  if constexpr (NP == 4) {
+    load_twiddles<N, 16, R0 * 256, S>(tw, w3);
+  }
+  stockham_pass<N, R0, 1, S>(w0, src_first, st);  // NS = 1: no twiddles
   if constexpr (NP == 2) {
-    stockham_pass<N, 16, R0, S>(tw, ld, dst_last);
+    stockham_pass<N, 16, R0, S>(w1, ld, dst_last);
   } else if constexpr (NP == 3) {
-    stockham_pass<N, 16, R0, S>(tw, ld, st);
-    stockham_pass<N, 16, R0 * 16, S>(tw, ld, dst_last);
+    stockham_pass<N, 16, R0, S>(w1, ld, st);
+    stockham_pass<N, 16, R0 * 16, S>(w2, ld, dst_last);
   } else {
-    stockham_pass<N, 16, R0, S>(tw, ld, st);
-    stockham_pass<N, 16, R0 * 16, S>(tw, ld, st);
-    stockham_pass<N, 16, R0 * 256, S>(tw, ld, dst_last);
+    stockham_pass<N, 16, R0, S>(w1, ld, st);
+    stockham_pass<N, 16, R0 * 16, S>(w2, ld, st);
+    stockham_pass<N, 16, R0 * 256, S>(w3, ld, dst_last);
   }
 }
 

@@ -50,8 +50,16 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
     }
     return;
   }
-  // TB bit p comes from codeblock p / cb_data_bits, message bit p % cb_data_bits.
-  for (uint32_t b = threadIdx.x; b < bytes; b += blockDim.x) {
+  // TB bit p comes from codeblock p / cb_data_bits, message bit p % cb_data_bits. TS 38.214 TB sizes make the
+  // codeblock data byte-aligned when C > 1 ((TBS + 24) is a multiple of 8 C): then every TB byte is one message byte.
+  if ((d.cb_data_bits & 7u) == 0) {
+    const uint32_t cb_bytes = d.cb_data_bits / 8u;
+    for (uint32_t b = threadIdx.x; b < bytes; b += blockDim.x) {
+      const uint32_t cb = __umulhi(8u * b, d.data_magic);
+      tb[b]             = msgs[cb * CB_MSG_STRIDE + (b - cb * cb_bytes)];
+    }
+  }
+  for (uint32_t b = threadIdx.x; (d.cb_data_bits & 7u) != 0 && b < bytes; b += blockDim.x) {
     uint32_t byte = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -64,9 +72,14 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
     tb[b] = static_cast<uint8_t>(byte);
   }
   __syncthreads();
-  const uint32_t crc = (d.crc_table != NO_CRC_TABLE)
-                           ? block_crc_table(tb, static_cast<int>(bytes), crc_tables + d.crc_table, part)
-                           : block_crc_bytes(tb, static_cast<int>(bytes), 24, 0x1864cfbu, table, part);
+  uint32_t crc;
+  if (d.crc_table != NO_CRC_TABLE) {
+    crc_byte_lut(table, 24, 0x1864cfbu);
+    crc = block_crc_chunks<16>([tb](int i) { return tb[i]; }, static_cast<int>(bytes), crc_tables + d.crc_table, 24,
+                               table, part);
+  } else {
+    crc = block_crc_bytes(tb, static_cast<int>(bytes), 24, 0x1864cfbu, table, part);
+  }
   // Checksum: the 24 bits that follow the last codeblock's TB bits (concatenate_codeblocks, :465).
   const uint32_t last_q = d.tbs_bits - (d.nof_cbs - 1u) * d.cb_data_bits;
   const uint8_t* lm     = msgs + (d.nof_cbs - 1u) * CB_MSG_STRIDE;

@@ -1203,8 +1203,9 @@ class PuschDecoderPlan:
                                                       _dptr(d_cb_msgs), _dptr(d_cb_iters), _dptr(d_tbs),
                                                       _dptr(d_tb_crc_ok), _stream_handle(stream)))
 
-    def enable_timing(self, enable=True):
-        _check(_lib.srsgpu_pusch_decoder_plan_enable_timing(self.handle, int(enable)))
+    def enable_timing(self, enable=True, decode_only=False):
+        """Stage events on every execute: all three stages, or (decode_only) just around the LDPC decoding."""
+        _check(_lib.srsgpu_pusch_decoder_plan_enable_timing(self.handle, (2 if decode_only else 1) if enable else 0))
 
     def stage_times(self):
         """([ms dematch, ms decode, ms TB stage], number of executes) accumulated since the previous call."""

@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <tuple>
@@ -71,8 +72,9 @@ struct srsgpu_pdsch_encoder_plan {
   tb_crc_desc*    d_tb       = nullptr;
   uint32_t*       d_tb_crc   = nullptr;
   int             nof_tbs    = 0;
-  enc_desc*       d_enc[2]   = {nullptr, nullptr};
+  enc_desc*       d_enc[2]   = {nullptr, nullptr};  ///< Per base graph: byte-kernel codeblocks, then packed ones.
   int             count[2]   = {0, 0};
+  int             count_pk[2] = {0, 0};
   int             threads[2] = {64, 64};
   size_t          out_begin  = 0;
   size_t          out_end    = 0;
@@ -783,8 +785,11 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
   static const double      shift_bg1[4] = {0, 17, 33, 56};  // ldpc_rate_matcher_impl.cpp:34
   static const double      shift_bg2[4] = {0, 13, 25, 43};
   std::vector<tb_crc_desc> tbd(nof_tbs);
-  std::vector<enc_desc>    encs[2];
+  std::vector<enc_desc>    encs[2], encs_pk[2];
   int                      maxz[2]   = {0, 0};
+  // SRSGPU_ENCODER_BYTE_KERNEL=1 routes every codeblock to the byte kernel (A/B parity checks of the packed kernel).
+  const char* force_env         = std::getenv("SRSGPU_ENCODER_BYTE_KERNEL");
+  const bool  force_byte_kernel = force_env != nullptr && force_env[0] == '1';
   size_t                   out_begin = ~size_t(0), out_end = 0;
   for (uint32_t t = 0; t < nof_tbs; ++t) {
     const srsgpu_pdsch_tb_config& c = cfgs[t];
@@ -854,7 +859,10 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
       const int last_col = (kmax + 2 * Z) / Z;  // full-codeblock node index
       const int n_ext    = last_col - (K + 4) + 1;
       d.n_ext            = static_cast<uint8_t>(n_ext < 0 ? 0 : n_ext);
-      encs[seg.bg - 1].push_back(d);
+      // Packed kernel: Z % 32 == 0 and byte-aligned codeblock data (and CB CRC position).
+      const bool packed = !force_byte_kernel && Z % 32 == 0 && ((cb.tb_offset | cb.nof_data) & 7) == 0 &&
+                          (seg.cb_crc_len == 0 || (cb.used & 7) == 0);
+      (packed ? encs_pk : encs)[seg.bg - 1].push_back(d);
     }
     maxz[seg.bg - 1] = Z > maxz[seg.bg - 1] ? Z : maxz[seg.bg - 1];
     out_begin        = std::min(out_begin, static_cast<size_t>(c.cw_offset));
@@ -872,9 +880,11 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
          hipMalloc(&plan->d_tb_crc, tbd.size() * sizeof(uint32_t)) == hipSuccess;
   }
   for (int b = 0; b < 2 && ok; ++b) {
-    plan->count[b]   = static_cast<int>(encs[b].size());
-    plan->threads[b] = ((maxz[b] + 63) / 64) * 64;
-    if (plan->count[b] > 0) {
+    plan->count[b]    = static_cast<int>(encs[b].size());
+    plan->count_pk[b] = static_cast<int>(encs_pk[b].size());
+    plan->threads[b]  = ((maxz[b] + 63) / 64) * 64;
+    encs[b].insert(encs[b].end(), encs_pk[b].begin(), encs_pk[b].end());
+    if (!encs[b].empty()) {
       ok = hipMalloc(&plan->d_enc[b], encs[b].size() * sizeof(enc_desc)) == hipSuccess &&
            hipMemcpy(plan->d_enc[b], encs[b].data(), encs[b].size() * sizeof(enc_desc), hipMemcpyHostToDevice) ==
                hipSuccess;
@@ -890,7 +900,9 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
 
 uint32_t srsgpu_pdsch_encoder_plan_nof_codeblocks(const srsgpu_pdsch_encoder_plan* plan)
 {
-  return plan == nullptr ? 0u : static_cast<uint32_t>(plan->count[0] + plan->count[1]);
+  return plan == nullptr ? 0u
+                         : static_cast<uint32_t>(plan->count[0] + plan->count[1] + plan->count_pk[0] +
+                                                 plan->count_pk[1]);
 }
 
 int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
@@ -911,13 +923,17 @@ int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
   HIP_TRY(hipGetLastError());
   stage_timer::mark(ev, 1, s);
   for (int b = 0; b < 2; ++b) {
-    if (plan->count[b] == 0) {
-      continue;
+    auto* out = reinterpret_cast<uint32_t*>(d_codewords);
+    if (plan->count_pk[b] > 0) {
+      launch_pdsch_encode_packed(b + 1, plan->d_enc[b] + plan->count[b], plan->count_pk[b], d_tbs, plan->d_tb_crc,
+                                 out, plan->ctx->d_shifts[b], plan->ctx->d_core[b], plan->ctx->d_crc_arena, s);
+      HIP_TRY(hipGetLastError());
     }
-    launch_pdsch_encode(b + 1, plan->d_enc[b], plan->count[b], plan->threads[b], d_tbs, plan->d_tb_crc,
-                        reinterpret_cast<uint32_t*>(d_codewords), plan->ctx->d_shifts[b], plan->ctx->d_core[b],
-                        plan->ctx->d_crc_arena, s);
-    HIP_TRY(hipGetLastError());
+    if (plan->count[b] > 0) {
+      launch_pdsch_encode(b + 1, plan->d_enc[b], plan->count[b], plan->threads[b], d_tbs, plan->d_tb_crc, out,
+                          plan->ctx->d_shifts[b], plan->ctx->d_core[b], plan->ctx->d_crc_arena, s);
+      HIP_TRY(hipGetLastError());
+    }
   }
   stage_timer::mark(ev, 2, s);
   return SRSGPU_OK;

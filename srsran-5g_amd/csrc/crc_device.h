@@ -129,15 +129,28 @@ __device__ inline void crc_byte_lut(uint32_t* lut, int order, uint32_t g)
   __syncthreads();
 }
 
+/// r(x) M(x) mod g(x) for r, M of degree < order (g including x^order): shift-and-add, no memory.
+__device__ __forceinline__ uint32_t gf2_mulmod(uint32_t r, uint32_t M, int order, uint32_t g)
+{
+  uint32_t acc = 0;
+#pragma unroll
+  for (int b = 23; b >= 0; --b) {  // M < 2^order: the iterations above order - 1 leave acc at 0
+    acc = (acc << 1) ^ (((acc >> (order - 1)) & 1u) ? g : 0u);
+    acc ^= ((M >> b) & 1u) ? r : 0u;
+  }
+  return acc;
+}
+
 /// CRC of data[0..nbytes) (global or LDS) by chunks: every lane runs the byte-table CRC over CS-byte chunks, then
-/// moves each chunk remainder r to the end of the message with the per-bit contribution table P of the message length
-/// L = 8 nbytes: r(x) x^(8 (nbytes - end)) mod g = XOR over the set bits b of r of P[8 end + order - 1 - b] (P[j] =
-/// x^(order + L - 1 - j) mod g; indices j >= L stand for x^(order + L - 1 - j) < x^order itself). Per byte this reads
-/// order * 4 / CS bytes of table instead of the 32 of block_crc_table. `lut` from crc_byte_lut; `red` one word per
-/// wave of LDS scratch. All lanes must call it; returns the CRC in every lane.
+/// moves each chunk remainder r to the end of the message: r(x) x^(8 (nbytes - end)) mod g, with the power read from
+/// the per-bit contribution table P of the message length L = 8 nbytes (P[j] = x^(order + L - 1 - j) mod g, so the
+/// power is P[8 end + order - 1]; below x^order it is the monomial itself) and the product formed by shift-and-add in
+/// registers: one table load per chunk instead of one per remainder bit (those uncoalesced loads made the kernels
+/// texture-addresser bound). `lut` from crc_byte_lut; `red` one word per wave of LDS scratch. All lanes must call it;
+/// returns the CRC in every lane.
 template <int CS, typename Data>
-__device__ inline uint32_t block_crc_chunks(Data data, int nbytes, const uint32_t* P, int order, const uint32_t* lut,
-                                            uint32_t* red)
+__device__ inline uint32_t block_crc_chunks(Data data, int nbytes, const uint32_t* P, int order, uint32_t g,
+                                            const uint32_t* lut, uint32_t* red)
 {
   const uint32_t mask = (1u << order) - 1u;
   const int      L    = 8 * nbytes;
@@ -146,23 +159,13 @@ __device__ inline uint32_t block_crc_chunks(Data data, int nbytes, const uint32_
   for (int c = threadIdx.x; c < nch; c += blockDim.x) {
     const int b0  = c * CS;
     const int b1  = min(b0 + CS, nbytes);
+    const int j   = 8 * b1 + order - 1;
+    const uint32_t M = (j < L) ? P[j] : (1u << (order + L - 1 - j));  // issued before the chunk's serial chain
     uint32_t  rem = 0;
     for (int i = b0; i < b1; ++i) {
       rem = ((rem << 8) ^ lut[((rem >> (order - 8)) ^ static_cast<uint32_t>(data(i))) & 0xffu]) & mask;
     }
-    if (b1 == nbytes) {
-      acc ^= rem;  // the last chunk is already at the end of the message
-    } else {
-      const int jb = 8 * b1 + order - 1;
-#pragma unroll
-      for (int b = 0; b < 24; ++b) {
-        if (b < order) {
-          const int      j  = jb - b;
-          const uint32_t pj = (j < L) ? P[j] : (1u << (order + L - 1 - j));
-          acc ^= ((rem >> b) & 1u) ? pj : 0u;
-        }
-      }
-    }
+    acc ^= gf2_mulmod(rem, M, order, g);
   }
   acc = wave_xor(acc);
   if ((threadIdx.x % WAVE) == 0) {

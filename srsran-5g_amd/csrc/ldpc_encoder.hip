@@ -7,10 +7,12 @@
 // codeword is produced packed MSB first (the bit_buffer / hw_accelerator_pdsch_enc packed layout); the reference
 // unpacks it one bit per byte, which the host binding does for comparisons.
 //
-// Mapping to CDNA4: one workgroup per codeblock; the codeblock's bits live one per byte in LDS (column c at c * 384,
-// as in the decoder), lane z computes row z of every lifted parity equation; the rate-matched output is produced
-// 32 bits per lane and written as whole words (atomicOr only for the two words a codeblock shares with its
-// neighbours).
+// Mapping to CDNA4: one workgroup per codeblock. Codeblocks with Z % 32 == 0 and byte-aligned data (the common case)
+// take the packed kernel (pdsch_encode_packed_kernel: 32 lifted rows per lane-word, funnel-shift rotations, windowed
+// rate matching); the others the byte kernel, where the codeblock's bits live one per byte in LDS (column c at
+// c * 384, as in the decoder) and lane z computes row z of every lifted parity equation. Both produce the
+// rate-matched output 32 bits per lane and write whole words (atomicOr only for the two words a codeblock shares
+// with its neighbours).
 #include "common.h"
 #include "crc_device.h"
 #include "ldpc_base_graphs.h"
@@ -58,7 +60,6 @@ __global__ __launch_bounds__(256) void tb_crc_kernel(const tb_crc_desc* __restri
   __shared__ uint32_t table[256];
   __shared__ uint32_t part[256];
   const tb_crc_desc d = descs[blockIdx.x];
-  // Per-bit contribution table when the plan could cache one for this length, else the byte-table method.
   // Chunked byte-table CRC moved by the per-bit contribution table when the plan could cache one for this length,
   // else the byte table with pairwise GF(2) combination.
   uint32_t crc;
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(256) void tb_crc_kernel(const tb_crc_desc* __restri
     crc_byte_lut(table, static_cast<int>(d.order), d.poly);
     const uint8_t* tb = tbs + d.byte_offset;
     crc = block_crc_chunks<16>([tb](int i) { return tb[i]; }, static_cast<int>(d.nbytes), crc_tables + d.table,
-                               static_cast<int>(d.order), table, part);
+                               static_cast<int>(d.order), d.poly, table, part);
   } else {
     crc = block_crc_bytes(tbs + d.byte_offset, static_cast<int>(d.nbytes), static_cast<int>(d.order), d.poly, table,
                           part);
@@ -190,7 +191,8 @@ __global__ __launch_bounds__(384) void pdsch_encode_kernel(const enc_desc* __res
     const uint32_t* P = crc_tables + d.crc_table;
     uint32_t        crc;
     if (byte_path) {
-      crc = block_crc_chunks<16>([](int q) { return msg[q]; }, static_cast<int>(d.used) / 8, P, 24, lut, red);
+      crc = block_crc_chunks<16>([](int q) { return msg[q]; }, static_cast<int>(d.used) / 8, P, 24, 0x1800063u,
+                                 lut, red);
     } else {  // XOR of per-bit contributions (table per length)
       uint32_t acc = 0;
       for (int i = threadIdx.x; i < d.used; i += blockDim.x) {
@@ -284,7 +286,285 @@ __global__ __launch_bounds__(384) void pdsch_encode_kernel(const enc_desc* __res
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------------
+// Packed encoder (Z a multiple of 32, byte-aligned codeblock data: every codeblock of TS 38.214 TB sizes with
+// Z >= 32 of the form 2^j * {1, 3, 5, 7, 9, 11}): the codeblock lives in LDS as LSB-first bit words, column c word k
+// holding bits 32k..32k+31 of node c, so full-codeblock position p is bit p & 31 of word p >> 5. A lifted rotation
+// by s of a column is a funnel shift of two of its words (Z % 32 == 0 makes the rotation word-granular plus a bit
+// offset), so one lane computes 32 rows of a lifted parity equation per instruction sequence, and the rate matcher
+// reads 32 consecutive circular-buffer bits per window instead of one byte per bit.
+// ---------------------------------------------------------------------------------------------------------------------
+
+constexpr int PK_THREADS = 128;
+
+/// Bits X[(32 k + t + o) mod Z], t = 0..31, of a packed Z-bit column X (W = Z / 32 words), 0 <= o < Z.
+__device__ __forceinline__ uint32_t col_window(const uint32_t* x, int k, int o, int W)
+{
+  int a = k + (o >> 5);
+  a     = a >= W ? a - W : a;
+  int b = a + 1;
+  b     = b >= W ? b - W : b;
+  return __builtin_amdgcn_alignbit(x[b], x[a], static_cast<uint32_t>(o & 31));
+}
+
+/// Reverses the bit order inside every byte (LSB-first word <-> MSB-first byte stream in a little-endian word).
+__device__ __forceinline__ uint32_t bytes_bitrev(uint32_t x)
+{
+  return __builtin_bitreverse32(__builtin_bswap32(x));
+}
+
+struct pk_rm {
+  const uint32_t* cw;  ///< Packed full codeblock (LDS).
+  uint32_t        v0, V, ninfo, filler, Z2;
+
+  /// Full-codeblock position of circular-buffer valid position v (fillers skipped, first 2Z punctured).
+  __device__ __forceinline__ uint32_t pos(uint32_t v) const { return v + Z2 + (v < ninfo ? 0u : filler); }
+  __device__ __forceinline__ uint32_t bit_at(uint32_t v) const
+  {
+    const uint32_t k = pos(v);
+    return (cw[k >> 5] >> (k & 31u)) & 1u;
+  }
+  __device__ __forceinline__ uint32_t wrap(uint32_t n) const
+  {
+    uint32_t v = v0 + n;
+    while (v >= V) {
+      v -= V;
+    }
+    return v;
+  }
+  /// e[n .. n + L - 1] (rate-matcher selection output, ldpc_rate_matcher_impl.cpp:104) as LSB-first bits.
+  template <int L>
+  __device__ __forceinline__ uint32_t window(uint32_t n) const
+  {
+    const uint32_t v = wrap(n);
+    if (v + L <= V && (v >= ninfo || v + L <= ninfo)) {  // one contiguous run of the codeblock
+      const uint32_t k = pos(v);
+      return __builtin_amdgcn_alignbit(cw[(k >> 5) + 1u], cw[k >> 5], k & 31u);
+    }
+    uint32_t r = 0;
+    uint32_t u = v;
+    for (int t = 0; t < L; ++t) {
+      r |= bit_at(u) << t;
+      u = (u + 1u == V) ? 0u : u + 1u;
+    }
+    return r;
+  }
+};
+
+/// Spreads the low 32/QM bits of x to bit positions 0, QM, 2 QM, ... (QM in {1, 2, 4, 8}).
+template <int QM>
+__device__ __forceinline__ uint32_t spread_bits(uint32_t x)
+{
+  if constexpr (QM == 1) {
+    return x;
+  } else if constexpr (QM == 2) {
+    x &= 0xffffu;
+    x = (x | (x << 8)) & 0x00ff00ffu;
+    x = (x | (x << 4)) & 0x0f0f0f0fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    return (x | (x << 1)) & 0x55555555u;
+  } else if constexpr (QM == 4) {
+    x &= 0xffu;
+    x = (x | (x << 12)) & 0x000f000fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    return (x | (x << 3)) & 0x11111111u;
+  } else {
+    x &= 0xfu;
+    x = (x | (x << 14)) & 0x00030003u;
+    return (x | (x << 7)) & 0x01010101u;
+  }
+}
+
+/// Rate matching + bit interleaving (ldpc_rate_matcher_impl.cpp:95/:150) of the packed codeblock into packed output
+/// words: stream bit t = Qm i + j carries e[j R + i]. Words wholly inside the codeblock with symbol-aligned bits
+/// (Qm in {1, 2, 4, 8}, g0 % Qm == 0) take one e window per bit row j; the rest (the two boundary words, Qm = 6,
+/// unaligned offsets) are assembled bit by bit.
+template <int QM>
+__device__ __forceinline__ void rate_match_packed(const enc_desc& d, const pk_rm& rm, uint32_t* __restrict__ out_words)
+{
+  const int      E  = static_cast<int>(d.E), R = E / QM;
+  const uint32_t g0 = d.out_bit_offset;
+  const uint32_t w0 = g0 / 32u, w1 = (g0 + static_cast<uint32_t>(E) - 1u) / 32u;
+  constexpr bool pow2   = (QM == 1 || QM == 2 || QM == 4 || QM == 8);
+  const bool     align  = pow2 && (g0 % QM) == 0;
+  for (uint32_t w = w0 + threadIdx.x; w <= w1; w += blockDim.x) {
+    const int t0   = static_cast<int>(w * 32u - g0);
+    const bool full = t0 >= 0 && t0 + 32 <= E;
+    uint32_t  lin  = 0;  // bit b = stream bit t0 + b
+    if constexpr (pow2) {
+      if (full && align) {
+        constexpr int SP = 32 / QM;
+        const int     i0 = t0 / QM;
+#pragma unroll
+        for (int j = 0; j < QM; ++j) {
+          lin |= spread_bits<QM>(rm.window<SP>(static_cast<uint32_t>(j * R + i0))) << j;
+        }
+        out_words[w] = bytes_bitrev(lin);
+        continue;
+      }
+    }
+    for (int b = 0; b < 32; ++b) {
+      const int t = t0 + b;
+      if (t >= 0 && t < E) {
+        const int i = t / QM, j = t - i * QM;
+        lin |= rm.bit_at(rm.wrap(static_cast<uint32_t>(j * R + i))) << b;
+      }
+    }
+    const uint32_t word = bytes_bitrev(lin);
+    if (full) {
+      out_words[w] = word;
+    } else if (word != 0) {
+      atomicOr(&out_words[w], word);
+    }
+  }
+}
+
+template <int BG>
+__global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const enc_desc* __restrict__ descs,
+                                                                         const uint8_t* __restrict__ tbs,
+                                                                         const uint32_t* __restrict__ tb_crcs,
+                                                                         uint32_t* __restrict__ out_words,
+                                                                         const uint16_t* __restrict__ shift_table,
+                                                                         const core_plan* __restrict__ core_plans,
+                                                                         const uint32_t* __restrict__ crc_tables)
+{
+  using G = ebg<BG>;
+  constexpr int WMAX = 384 / 32;
+  __shared__ uint32_t cw[G::NF * WMAX + 1];        // packed codeblock, node c at c * W
+  __shared__ uint32_t lam[4 * WMAX];               // core row sums
+  __shared__ __attribute__((aligned(4))) uint8_t msg[G::K * 384 / 8];  // message bytes, MSB first
+  __shared__ uint32_t edge[G::NE];                 // column << 16 | lifted shift of every base-graph edge
+  __shared__ uint16_t row_start[G::M + 1];
+  __shared__ uint32_t lut[256];
+  __shared__ uint32_t red[PK_THREADS / WAVE];
+
+  const enc_desc d   = descs[blockIdx.x];
+  const int      Z   = d.Z;
+  const int      W   = Z / 32;
+  const int      K   = G::K;
+  const int      nkb = K * Z / 8;  // message bytes
+  const int      tid = static_cast<int>(threadIdx.x);
+  for (int e = tid; e < G::NE; e += PK_THREADS) {
+    edge[e] = (static_cast<uint32_t>(G::col(e)) << 16) | shift_table[static_cast<uint32_t>(d.zpos) * G::NE + e];
+  }
+  for (int m = tid; m <= G::M; m += PK_THREADS) {
+    row_start[m] = static_cast<uint16_t>(G::rs(m));
+  }
+  // ---- Message bytes (ldpc_segmenter_tx_impl.cpp:144): TB(+TB CRC) bytes, zero padding / CRC slot / fillers. ----
+  const uint8_t* tb     = tbs + d.tb_byte_offset;
+  const uint32_t tb_crc = tb_crcs[d.tb_index];
+  const int      nd8    = d.nof_data / 8;
+  for (int q = tid; q < nkb; q += PK_THREADS) {
+    uint32_t byte = 0;
+    if (q < nd8) {
+      const uint32_t p = d.tb_bit_offset + 8u * static_cast<uint32_t>(q);
+      byte = (p < d.tb_bits) ? tb[p >> 3] : (tb_crc >> (d.tb_crc_len - 8u - (p - d.tb_bits))) & 0xffu;
+    }
+    msg[q] = static_cast<uint8_t>(byte);
+  }
+  if (d.crc_table != NO_CRC_TABLE) {
+    crc_byte_lut(lut, 24, 0x1800063u);  // CRC24B; ends with a barrier
+    const uint32_t crc = block_crc_chunks<16>([](int q) { return msg[q]; }, static_cast<int>(d.used) / 8,
+                                              crc_tables + d.crc_table, 24, 0x1800063u, lut, red);
+    if (tid < 3) {
+      msg[d.used / 8 + tid] = static_cast<uint8_t>(crc >> (16 - 8 * tid));
+    }
+  }
+  __syncthreads();
+  // ---- Message words: node c word k = message bits 32 (c W + k) .. + 31. ----
+  const uint32_t* msg32 = reinterpret_cast<const uint32_t*>(msg);
+  for (int q = tid; q < K * W; q += PK_THREADS) {
+    cw[q] = bytes_bitrev(msg32[q]);
+  }
+  __syncthreads();
+  // ---- Core rows 0..3: lambda_m = sum of the rotated information nodes (32 rows per task). ----
+  for (int task = tid; task < 4 * W; task += PK_THREADS) {
+    const int m = task / W, k = task - m * W;
+    uint32_t  acc = 0;
+    for (int e = row_start[m]; e < row_start[m + 1]; ++e) {
+      const uint32_t ce = edge[e];
+      const int      c  = static_cast<int>(ce >> 16);
+      if (c < K) {
+        acc ^= col_window(cw + c * W, k, static_cast<int>(ce & 0xffffu), W);
+      }
+    }
+    lam[m * WMAX + k] = acc;
+  }
+  __syncthreads();
+  const core_plan* __restrict__ cp = core_plans + d.zpos;
+  // P^x p0 = lambda_0 + ... + lambda_3  ->  p0[l] = sum lambda[(l - x) mod Z].
+  {
+    const int o = (Z - cp->x) % Z;
+    for (int k = tid; k < W; k += PK_THREADS) {
+      cw[K * W + k] = col_window(lam, k, o, W) ^ col_window(lam + WMAX, k, o, W) ^
+                      col_window(lam + 2 * WMAX, k, o, W) ^ col_window(lam + 3 * WMAX, k, o, W);
+    }
+  }
+  __syncthreads();
+  // p_u[(z + s_u) mod Z] = lambda_row[z] + sum_{j != u} p_j[(z + s_j) mod Z]  (same steps as the byte kernel).
+  for (int step = 0; step < 3; ++step) {
+    const int u  = cp->unk[step];
+    const int su = cp->sh[step][u];
+    for (int k = tid; k < W; k += PK_THREADS) {
+      uint32_t acc = col_window(lam + cp->row[step] * WMAX, k, (Z - su) % Z, W);
+      for (int j = 0; j < 4; ++j) {
+        const int s = cp->sh[step][j];
+        if (j != u && s >= 0) {
+          acc ^= col_window(cw + (K + j) * W, k, (s - su + Z) % Z, W);
+        }
+      }
+      cw[(K + u) * W + k] = acc;
+    }
+    __syncthreads();
+  }
+  // ---- Extension parity (identity extension), every needed row in parallel. ----
+  const int n_ext = d.n_ext;
+  for (int task = tid; task < n_ext * W; task += PK_THREADS) {
+    const int r = task / W, k = task - r * W;
+    uint32_t  acc = 0;
+    for (int e = row_start[4 + r]; e < row_start[5 + r] - 1; ++e) {  // the row's last edge is its own (identity) node
+      const uint32_t ce = edge[e];
+      acc ^= col_window(cw + (ce >> 16) * W, k, static_cast<int>(ce & 0xffffu), W);
+    }
+    cw[(K + 4 + r) * W + k] = acc;
+  }
+  __syncthreads();
+  // ---- Rate matching + interleaving + packing. ----
+  const pk_rm rm{cw, d.v0, d.Ncb - d.filler, static_cast<uint32_t>((K - 2) * Z - d.filler), d.filler,
+                 static_cast<uint32_t>(2 * Z)};
+  switch (d.Qm) {
+    case 1: rate_match_packed<1>(d, rm, out_words); break;
+    case 2: rate_match_packed<2>(d, rm, out_words); break;
+    case 4: rate_match_packed<4>(d, rm, out_words); break;
+    case 6: rate_match_packed<6>(d, rm, out_words); break;
+    default: rate_match_packed<8>(d, rm, out_words); break;
+  }
+}
+
 } // namespace
+
+void launch_pdsch_encode_packed(int              bg,
+                                const enc_desc*  d_desc,
+                                int              nof_cbs,
+                                const uint8_t*   d_tbs,
+                                const uint32_t*  d_tb_crcs,
+                                uint32_t*        d_out_words,
+                                const uint16_t*  d_shifts,
+                                const core_plan* d_core_plans,
+                                const uint32_t*  d_crc_tables,
+                                hipStream_t      s)
+{
+  if (nof_cbs <= 0) {
+    return;
+  }
+  if (bg == 1) {
+    pdsch_encode_packed_kernel<1><<<nof_cbs, PK_THREADS, 0, s>>>(d_desc, d_tbs, d_tb_crcs, d_out_words, d_shifts,
+                                                                  d_core_plans, d_crc_tables);
+  } else {
+    pdsch_encode_packed_kernel<2><<<nof_cbs, PK_THREADS, 0, s>>>(d_desc, d_tbs, d_tb_crcs, d_out_words, d_shifts,
+                                                                  d_core_plans, d_crc_tables);
+  }
+}
 
 void launch_tb_crc(const tb_crc_desc* d_desc, int nof_tbs, const uint8_t* d_tbs, uint32_t* d_crcs,
                    const uint32_t* d_crc_tables, hipStream_t s)

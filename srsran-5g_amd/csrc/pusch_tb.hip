@@ -71,12 +71,26 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
     }
     tb[b] = static_cast<uint8_t>(byte);
   }
-  __syncthreads();
+  const bool crc_from_msgs = d.crc_table != NO_CRC_TABLE && (d.cb_data_bits & 7u) == 0;
+  if (!crc_from_msgs) {
+    __syncthreads();  // the CRC reads the TB back
+  }
   uint32_t crc;
-  if (d.crc_table != NO_CRC_TABLE) {
+  if (crc_from_msgs) {
+    // Straight from the codeblock messages: no dependency on the TB stores above.
+    crc_byte_lut(table, 24, 0x1864cfbu);
+    const uint32_t cb_bytes = d.cb_data_bits / 8u;
+    const uint32_t magic    = d.data_magic;
+    crc = block_crc_chunks<16>(
+        [msgs, cb_bytes, magic](int i) {
+          const uint32_t cb = __umulhi(8u * static_cast<uint32_t>(i), magic);
+          return msgs[cb * CB_MSG_STRIDE + (static_cast<uint32_t>(i) - cb * cb_bytes)];
+        },
+        static_cast<int>(bytes), crc_tables + d.crc_table, 24, 0x1864cfbu, table, part);
+  } else if (d.crc_table != NO_CRC_TABLE) {
     crc_byte_lut(table, 24, 0x1864cfbu);
     crc = block_crc_chunks<16>([tb](int i) { return tb[i]; }, static_cast<int>(bytes), crc_tables + d.crc_table, 24,
-                               table, part);
+                               0x1864cfbu, table, part);
   } else {
     crc = block_crc_bytes(tb, static_cast<int>(bytes), 24, 0x1864cfbu, table, part);
   }

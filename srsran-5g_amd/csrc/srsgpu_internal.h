@@ -108,6 +108,18 @@ void launch_pdsch_encode(int              bg,
                          const uint32_t*  d_crc_tables,
                          hipStream_t      s);
 
+/// Packed-bit encoder for codeblocks with Z % 32 == 0 and byte-aligned data (pdsch_encode_packed_kernel).
+void launch_pdsch_encode_packed(int              bg,
+                                const enc_desc*  d_desc,
+                                int              nof_cbs,
+                                const uint8_t*   d_tbs,
+                                const uint32_t*  d_tb_crcs,
+                                uint32_t*        d_out_words,
+                                const uint16_t*  d_shifts,
+                                const core_plan* d_core_plans,
+                                const uint32_t*  d_crc_tables,
+                                hipStream_t      s);
+
 /// Launches the batched rate dematcher (rate_dematcher.hip). mode 0: generic combining, 1: SIMD combining.
 void launch_rate_dematch(int           mode,
                          const dm_desc* d_desc,

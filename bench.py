@@ -128,6 +128,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--serial-legs", action="store_true",
                     help="run the DL and UL legs on one stream (clean per-stage times; slower overall)")
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
+                    help="replay the DL+UL pipeline of a step as one captured HIP graph (default) or launch eagerly")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -168,13 +170,23 @@ def main():
         from srsgpu import dist as sdist
         tb_gather = sdist.TbGather(ul.d_tbs.numel(), ul.d_tb_ok.numel(), dev, root=0)
 
-    def step(ev_dl=None, ev_ul=None):
-        dl_stream.wait_stream(main_stream)
-        ul_stream.wait_stream(main_stream)
+    def pipeline(ev_dl=None, ev_ul=None):
+        """DL and UL legs of one step, forked from and joined back into the caller's current stream."""
+        cur = torch.cuda.current_stream(dev)
+        dl_stream.wait_stream(cur)
+        ul_stream.wait_stream(cur)
         dl.execute(d_dl_tbs, dl_stream, ev_dl)
         ul.execute(d_samples, ul_stream, ev_ul)
-        main_stream.wait_stream(dl_stream)
-        main_stream.wait_stream(ul_stream)
+        cur.wait_stream(dl_stream)
+        cur.wait_stream(ul_stream)
+
+    graph = None
+
+    def step(ev_dl=None, ev_ul=None):
+        if graph is not None and ev_dl is None:
+            graph.replay()
+        else:
+            pipeline(ev_dl, ev_ul)
         if tb_gather is not None:
             tb_gather.gather(ul.d_tbs, ul.d_tb_ok)
 
@@ -183,9 +195,19 @@ def main():
     torch.cuda.synchronize()
     dl.encoder.stage_times()
     ul.decoder.stage_times()
-    # Timed loop: only the decoder plan's own stage events (the roofline kernel's launch duration, on its launch
-    # stream); the per-stage events of every leg cost ~30 us per step, so stage times come from an extra untimed pass.
-    ul.decoder.enable_timing(True, decode_only=True)
+    if args.graph:
+        # hipGraph of the whole per-step pipeline (every plan is allocation-free and capture-safe): the 11 kernels,
+        # the codeword memset and the stream fork/join replay as one graph launch per step.
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            pipeline()
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+    # Timed loop: eager mode records only the decoder plan's own stage events (the roofline kernel's launch duration,
+    # on its launch stream); graph mode records none. The roofline kernel time then comes from an untimed eager pass
+    # with those two events, and per-stage times from another untimed pass with events between the stages.
+    ul.decoder.enable_timing(not args.graph, decode_only=True)
     evs = [([torch.cuda.Event(enable_timing=True) for _ in range(4)],
             [torch.cuda.Event(enable_timing=True) for _ in range(5)]) for _ in range(args.steps)]
     if world > 1:
@@ -199,6 +221,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if args.graph:
+        ul.decoder.enable_timing(True, decode_only=True)
+        for _ in range(args.steps):
+            pipeline()
+        torch.cuda.synchronize()
     ul_ms, ul_n = ul.decoder.stage_times()
     assert ul_n == args.steps
     ul.decoder.enable_timing(False)
@@ -288,6 +315,8 @@ def main():
                    "channel_estimate_layout": "compact (one row per allocation, average time strategy)"
                                               if ul.estimate_layout == srsgpu.CE_COMPACT else "per symbol",
                    "leg_streams": "one stream" if args.serial_legs else "DL and UL on concurrent streams",
+                   "launch": "one captured HIP graph per step (torch.cuda.CUDAGraph over the plans' execute calls)"
+                             if args.graph else "eager kernel launches",
                    "slots_per_step": S,
                    "codeblocks_per_step_per_direction": int(sum(s.nof_segments for s in segs) * S),
                    "ldpc_max_iterations": args.iterations, "ldpc_early_stop": True,
@@ -306,8 +335,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "ldpc_decode_pk_kernel<1,1,8>",
                      "kernel_ms_per_launch": dec_ms,
-                     "note": "algorithmic bytes per launch / decoder-stage HIP-event time on the launch stream; the "
-                             "LDPC decoder is VALU-issue/latency-bound, not HBM-bound (DESIGN.md)"},
+                     "note": "algorithmic bytes per launch / decoder-stage HIP-event time on the launch stream ("
+                             + ("an eager pass of as many steps right after the graph-replayed timed loop"
+                                if args.graph else "inside the timed loop")
+                             + "); the LDPC decoder is VALU-issue/latency-bound, not HBM-bound (DESIGN.md)"},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

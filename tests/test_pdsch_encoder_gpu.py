@@ -72,3 +72,41 @@ def test_pdsch_encoder_slot_100mhz(ctx):
     got = srsgpu.PdschEncoder(ctx).encode_batch(tbs, cfgs)
     for a, b in zip(got, want):
         assert np.array_equal(a, b)
+
+
+def test_pdsch_encoder_packed_kernel_every_lifting_size(ctx):
+    """The packed kernel (Z % 32 == 0) against the oracle and against the byte kernel (SRSGPU_ENCODER_BYTE_KERNEL=1)
+    on grants covering every (BG, Z) with Z a multiple of 32 that the TBS tables reach, every Qm and rv."""
+    import os
+    import srsgpu
+    from srsgpu import sch
+    orc = Oracle()
+    rng = np.random.default_rng(32)
+    tables = list(sch.MCS_TABLE_256QAM.values())
+    seen, tbs, cfgs, want = set(), [], [], []
+    for _ in range(4000):
+        qm, r = tables[int(rng.integers(0, len(tables)))]
+        g = sch.UeGrant(int(rng.integers(1, 140)), int(rng.integers(1, 5)), qm, r,
+                        nof_symb_sh=int(rng.integers(2, 15)))
+        seg = g.segmentation()
+        key = (seg.base_graph, seg.lifting_size, g.qm)
+        if seg.lifting_size % 32 or key in seen or seg.tbs > 200000:
+            continue
+        seen.add(key)
+        rv = int(rng.integers(0, 4))
+        tb = rng.integers(0, 256, seg.tbs // 8).astype(np.uint8)
+        cw, _, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, rv, g.qm, g.nof_layers, 0, g.nof_ch_symbols)
+        tbs.append(tb)
+        cfgs.append(srsgpu.PdschTransportBlock(seg.base_graph, rv, g.qm, g.nof_layers, g.nof_ch_symbols))
+        want.append(cw)
+    assert len({(b, z) for b, z, _ in seen}) >= 12, sorted(seen)
+    got = srsgpu.PdschEncoder(ctx).encode_batch(tbs, cfgs)
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert np.array_equal(a, b), (i, cfgs[i])
+    os.environ["SRSGPU_ENCODER_BYTE_KERNEL"] = "1"
+    try:
+        byte = srsgpu.PdschEncoder(ctx).encode_batch(tbs, cfgs)
+    finally:
+        del os.environ["SRSGPU_ENCODER_BYTE_KERNEL"]
+    for a, b in zip(got, byte):
+        assert np.array_equal(a, b)

@@ -98,3 +98,50 @@ def test_uplink_compact_estimates_match_per_symbol_layout(ctx):
     for l in range(14):
         assert np.array_equal(ce_full[:, :, l], ce_comp[:, :, 0])
     assert compact.d_tb_ok.cpu().numpy().all()
+
+
+def test_pipelines_replay_as_hip_graph(ctx):
+    """The DL and UL plans are allocation-free and capture-safe: both legs captured once into one HIP graph (forked
+    onto two streams) and replayed give the same codewords, grids, samples, LLRs and decoded TBs as eager launches."""
+    import torch
+    from srsgpu import sch
+    from srsgpu import slot as slotlib
+    ues = sch.slot_100mhz_4x4()
+    segs = [u.segmentation() for u in ues]
+    cell = slotlib.CellSlots(ues, segs, 2)
+    dl = slotlib.DownlinkPipeline(ctx, cell)
+    ul = slotlib.UplinkPipeline(ctx, cell)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(9)
+    dl_tbs = torch.randint(0, 256, (dl.tb_total,), generator=gen, device="cuda", dtype=torch.uint8)
+    ul_tbs = torch.randint(0, 256, (dl.tb_total,), generator=gen, device="cuda", dtype=torch.uint8)
+    samples = slotlib.synthesize_uplink(ctx, cell, ul_tbs, snr_db=35.0, seed=11)
+    s_dl, s_ul = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def pipeline():
+        cur = torch.cuda.current_stream()
+        s_dl.wait_stream(cur)
+        s_ul.wait_stream(cur)
+        dl.execute(dl_tbs, s_dl)
+        ul.execute(samples, s_ul)
+        cur.wait_stream(s_dl)
+        cur.wait_stream(s_ul)
+
+    pipeline()
+    torch.cuda.synchronize()
+    outs = [dl.d_cw, dl.d_grid, dl.d_samples, ul.d_llrs, ul.d_tbs, ul.d_tb_ok, ul.d_iters]
+    eager = [t.clone() for t in outs]
+    for t in outs:
+        t.zero_()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        pipeline()
+    for t in outs:  # capture does not execute: clear again and replay twice
+        t.zero_()
+    graph.replay()
+    graph.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(eager, outs):
+        assert torch.equal(a, b)
+    assert ul.d_tb_ok.cpu().numpy().all()
+    assert torch.equal(ul.d_tbs, ul_tbs)

@@ -128,6 +128,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--serial-legs", action="store_true",
                     help="run the DL and UL legs on one stream (clean per-stage times; slower overall)")
+    ap.add_argument("--batches", type=int, default=1,
+                    help="split a step's slots into this many independent DL/UL pipeline pairs on their own streams")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
                     help="replay the DL+UL pipeline of a step as one captured HIP graph (default) or launch eagerly")
     args = ap.parse_args()
@@ -143,42 +145,52 @@ def main():
     gen.manual_seed(1234 + rank)
     ctx = srsgpu.Context(local_rank)
     S = args.slots_per_step
+    B = args.batches
+    assert B >= 1 and S % B == 0, "--slots-per-step must be a multiple of --batches"
+    Sb = S // B  # slots per pipeline pair
 
     ues = sch.slot_100mhz_4x4()
     segs = [u.segmentation() for u in ues]
-    cell = slotlib.CellSlots(ues, segs, S)
-    dl = slotlib.DownlinkPipeline(ctx, cell)
-    ul = slotlib.UplinkPipeline(ctx, cell, iterations=args.iterations)
-    d_dl_tbs = torch.randint(0, 256, (dl.tb_total,), generator=gen, device=dev, dtype=torch.uint8)
-    d_ul_tbs_tx = torch.randint(0, 256, (dl.tb_total,), generator=gen, device=dev, dtype=torch.uint8)
+    cell = slotlib.CellSlots(ues, segs, Sb)
+    dls = [slotlib.DownlinkPipeline(ctx, cell) for _ in range(B)]
+    uls = [slotlib.UplinkPipeline(ctx, cell, iterations=args.iterations) for _ in range(B)]
+    dl, ul = dls[0], uls[0]
+    dl_tbs = [torch.randint(0, 256, (dl.tb_total,), generator=gen, device=dev, dtype=torch.uint8) for _ in range(B)]
+    ul_tbs_tx = [torch.randint(0, 256, (dl.tb_total,), generator=gen, device=dev, dtype=torch.uint8) for _ in range(B)]
     if args.worst_case:
-        d_samples = torch.randn(2 * ul.ofdm.nof_samples, generator=gen, device=dev) * 0.01
+        samples = [torch.randn(2 * ul.ofdm.nof_samples, generator=gen, device=dev) * 0.01 for _ in range(B)]
         data_desc = "Gaussian noise samples (no TB ever valid: all LDPC iterations, worst case)"
     else:
-        d_samples = slotlib.synthesize_uplink(ctx, cell, d_ul_tbs_tx, snr_db=args.snr_db, seed=99 + rank)
+        samples = [slotlib.synthesize_uplink(ctx, cell, ul_tbs_tx[b], snr_db=args.snr_db, seed=99 + rank + 1000 * b)
+                   for b in range(B)]
         data_desc = (f"UL TBs through a GPU UE transmitter (same encoder / DM-RS / modulator), a random unitary 4x4 "
                      f"channel per UE and AWGN at {args.snr_db:g} dB SNR, OFDM-modulated (synthetic)")
+    d_dl_tbs, d_ul_tbs_tx, d_samples = dl_tbs[0], ul_tbs_tx[0], samples[0]
     torch.cuda.synchronize()
     tb_bytes = dl.tb_bytes
     nof_tbs = len(tb_bytes)
 
-    main_stream = torch.cuda.current_stream(dev)
-    dl_stream = torch.cuda.Stream(dev)
-    ul_stream = dl_stream if args.serial_legs else torch.cuda.Stream(dev)
+    dl_streams = [torch.cuda.Stream(dev) for _ in range(B)]
+    ul_streams = dl_streams if args.serial_legs else [torch.cuda.Stream(dev) for _ in range(B)]
     tb_gather = None
     if world > 1:
         from srsgpu import dist as sdist
         tb_gather = sdist.TbGather(ul.d_tbs.numel(), ul.d_tb_ok.numel(), dev, root=0)
 
-    def pipeline(ev_dl=None, ev_ul=None):
-        """DL and UL legs of one step, forked from and joined back into the caller's current stream."""
+    def pipeline(ev_dl=None, ev_ul=None, batches=None):
+        """DL and UL legs of one step (every batch), forked from and joined back into the caller's current stream.
+        Stage events, when given, go to batch 0."""
         cur = torch.cuda.current_stream(dev)
-        dl_stream.wait_stream(cur)
-        ul_stream.wait_stream(cur)
-        dl.execute(d_dl_tbs, dl_stream, ev_dl)
-        ul.execute(d_samples, ul_stream, ev_ul)
-        cur.wait_stream(dl_stream)
-        cur.wait_stream(ul_stream)
+        bs = range(B) if batches is None else batches
+        for b in bs:
+            dl_streams[b].wait_stream(cur)
+            ul_streams[b].wait_stream(cur)
+        for b in bs:
+            dls[b].execute(dl_tbs[b], dl_streams[b], ev_dl if b == 0 else None)
+            uls[b].execute(samples[b], ul_streams[b], ev_ul if b == 0 else None)
+        for b in bs:
+            cur.wait_stream(dl_streams[b])
+            cur.wait_stream(ul_streams[b])
 
     graph = None
 
@@ -188,7 +200,8 @@ def main():
         else:
             pipeline(ev_dl, ev_ul)
         if tb_gather is not None:
-            tb_gather.gather(ul.d_tbs, ul.d_tb_ok)
+            for u in uls:
+                tb_gather.gather(u.d_tbs, u.d_tb_ok)
 
     for _ in range(args.warmup):
         step()
@@ -224,13 +237,13 @@ def main():
     if args.graph:
         ul.decoder.enable_timing(True, decode_only=True)
         for _ in range(args.steps):
-            pipeline()
+            pipeline(batches=[0])  # the roofline kernel of batch 0, its pipeline pair alone
         torch.cuda.synchronize()
     ul_ms, ul_n = ul.decoder.stage_times()
     assert ul_n == args.steps
     ul.decoder.enable_timing(False)
-    for i in range(args.steps):  # per-stage times: an extra, untimed pass with events between the stages
-        step(*evs[i])
+    for i in range(args.steps):  # per-stage times: an extra, untimed pass of batch 0 with events between the stages
+        pipeline(*evs[i], batches=[0])
     torch.cuda.synchronize()
     stage = {k: 0.0 for k in DL_STAGES + UL_STAGES}
     for ed, eu in evs:
@@ -244,16 +257,18 @@ def main():
     elapsed = float(t.item())
 
     # ---- Results of the last step: UL TB success (decoded TBs must equal what the UEs sent) and iterations ----
-    tb_ok = ul.d_tb_ok.cpu().numpy().astype(bool)
-    iters = ul.d_iters.cpu().numpy()
+    tb_ok = np.concatenate([u.d_tb_ok.cpu().numpy().astype(bool) for u in uls])
+    iters = np.concatenate([u.d_iters.cpu().numpy() for u in uls])
     if not args.worst_case:
-        sent = d_ul_tbs_tx.cpu().numpy()
-        got = ul.d_tbs.cpu().numpy()
-        off = 0
-        for i, nb in enumerate(tb_bytes):
-            if tb_ok[i]:
-                assert np.array_equal(got[off:off + nb], sent[off:off + nb]), f"TB {i} CRC ok but payload differs"
-            off += nb
+        for b in range(B):
+            sent = ul_tbs_tx[b].cpu().numpy()
+            got = uls[b].d_tbs.cpu().numpy()
+            ok_b = uls[b].d_tb_ok.cpu().numpy().astype(bool)
+            off = 0
+            for i, nb in enumerate(tb_bytes):
+                if ok_b[i]:
+                    assert np.array_equal(got[off:off + nb], sent[off:off + nb]), f"TB {i} CRC ok but payload differs"
+                off += nb
     avg_iters = float(np.where(iters > 0, iters, args.iterations).mean())
 
     slots = S * world * args.steps
@@ -266,18 +281,20 @@ def main():
     # dematcher's zero tail, as reported by the plan), K*Z/8 bytes of decoded bits written, 4 B result + 1 B CRC flag,
     # 40 B descriptor.
     dec_bytes = ul.decoder.decoder_input_llrs + sum(
-        s.nof_segments * (((22 if s.base_graph == 1 else 10) * s.lifting_size + 7) // 8 + 45) for s in segs) * S
+        s.nof_segments * (((22 if s.base_graph == 1 else 10) * s.lifting_size + 7) // 8 + 45) for s in segs) * Sb
     achieved = dec_bytes / (dec_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "ldpc_decode_traffic.json")
     if os.path.exists(tfile):
         with open(tfile) as f:
             tj = json.load(f)
-        if tj.get("slots_per_step") == S and tj.get("worst_case", False) == args.worst_case:
+        if tj.get("slots_per_step") == Sb and tj.get("worst_case", False) == args.worst_case:
             traffic = tj.get("hbm_bytes_per_launch")
 
-    # Algorithmic HBM bytes per step of the signal-chain stages (each byte read or written once; DESIGN.md "Kernels"):
-    # bf16 grids are 4 B per RE, time samples 8 B (complex float), estimates 4 B per (layer, port, RE), LLRs 1 B.
+    # Algorithmic HBM bytes per pipeline pair (Sb slots) of the signal-chain stages (each byte read or written once;
+    # DESIGN.md "Kernels"): bf16 grids are 4 B per RE, time samples 8 B (complex float), estimates 4 B per (layer,
+    # port, RE), LLRs 1 B. The stage times come from batch 0's pipeline pair.
+    S_all, S = S, Sb
     P, nsc, L = cell.nof_ports, cell.nsc, ues[0].nof_layers
     grid_b = S * P * 14 * nsc * 4
     spp = ul.ofdm.nof_samples // (S * P)  # samples per slot and port (CPs included)
@@ -317,8 +334,9 @@ def main():
                    "leg_streams": "one stream" if args.serial_legs else "DL and UL on concurrent streams",
                    "launch": "one captured HIP graph per step (torch.cuda.CUDAGraph over the plans' execute calls)"
                              if args.graph else "eager kernel launches",
-                   "slots_per_step": S,
-                   "codeblocks_per_step_per_direction": int(sum(s.nof_segments for s in segs) * S),
+                   "slots_per_step": S_all,
+                   "concurrent_batches": f"{B} DL/UL pipeline pair(s) of {Sb} slots, each leg on its own stream",
+                   "codeblocks_per_step_per_direction": int(sum(s.nof_segments for s in segs) * S_all),
                    "ldpc_max_iterations": args.iterations, "ldpc_early_stop": True,
                    "decoder_arithmetic": "avx2/avx512 (SIMD) variant, bit-exact",
                    "ofdm": "4096-point DFT, 122.88 Msps, normal CP",
@@ -330,7 +348,8 @@ def main():
         "realtime_cells_per_gpu": value / SLOT_RATE_30KHZ / world,
         "pusch_tb_success_rate": float(tb_ok.mean()),
         "ldpc_avg_iterations": avg_iters,
-        "stage_ms_per_step": stage,  # from the untimed pass with per-stage events
+        "stage_ms_per_step": stage,  # from the untimed pass of batch 0 with per-stage events
+        "stage_slots": Sb,
         "stage_algorithmic_gbps": stage_gbps,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "ldpc_decode_pk_kernel<1,1,8>",

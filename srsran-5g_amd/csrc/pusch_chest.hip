@@ -127,7 +127,7 @@ __device__ __forceinline__ void virtual_pilots(cpx* E, int N, int nv)
   }
 }
 
-__global__ __launch_bounds__(CHEST_THREADS) void pusch_chest_kernel(const chest_job* __restrict__ jobs,
+__global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void pusch_chest_kernel(const chest_job* __restrict__ jobs,
                                                                     int max_pilots,
                                                                     int max_dmrs,
                                                                     int max_words,

@@ -211,8 +211,9 @@ def main():
     if args.graph:
         # hipGraph of the whole per-step pipeline (every plan is allocation-free and capture-safe): the 11 kernels,
         # the codeword memset and the stream fork/join replay as one graph launch per step.
+        # thread_local: the RCCL watchdog thread of a multi-GPU run keeps polling its events during the capture.
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             pipeline()
         for _ in range(args.warmup):
             step()

@@ -436,7 +436,12 @@ __device__ __forceinline__ void demod_res_qm(const demod_uniform& u, demap_pair_
   }
 }
 
-__global__ __launch_bounds__(DEMOD_THREADS) void pusch_demodulate_kernel(const demod_desc* __restrict__ descs,
+#ifdef SRSGPU_DEMOD_WAVES  // occupancy experiments: waves per SIMD forced by the register allocator
+#define DEMOD_OCCUPANCY __attribute__((amdgpu_waves_per_eu(SRSGPU_DEMOD_WAVES, SRSGPU_DEMOD_WAVES)))
+#else
+#define DEMOD_OCCUPANCY
+#endif
+__global__ __launch_bounds__(DEMOD_THREADS) DEMOD_OCCUPANCY void pusch_demodulate_kernel(const demod_desc* __restrict__ descs,
                                                                          const mod_chunk* __restrict__ chunks,
                                                                          const demap_pair_table* __restrict__ tables,
                                                                          const uint32_t* __restrict__ grids,

@@ -65,6 +65,18 @@ struct srsgpu_context {
 namespace srsgpu {
 /// Builds and uploads the Gold-sequence jump tables into the context once (caller holds ctx->mtx); capi_pdsch_mod.cpp.
 int ensure_gold_tables(srsgpu_context* ctx);
+
+/// A plan's (de)scrambling sequences, resident in HBM for the plan's lifetime: word offsets of every transmission
+/// (offsets[t], filled here from nwords) and the buffer, filled once on the device (launch_gold_fill) and synchronised.
+/// Caller holds ctx->mtx and has called ensure_gold_tables.
+int build_gold_sequences(srsgpu_context*              ctx,
+                         const std::vector<uint32_t>& c_inits,
+                         const std::vector<uint32_t>& nwords,
+                         const std::vector<uint32_t>& offsets,
+                         uint32_t**                   d_seq);
+
+/// Word offsets of the transmissions' sequences in a plan's sequence buffer (each padded by one word).
+std::vector<uint32_t> gold_sequence_offsets(const std::vector<uint32_t>& nwords);
 } // namespace srsgpu
 
 /// Per-stage device time accounting: HIP events recorded around every kernel stage on the execution stream.

@@ -22,6 +22,7 @@ struct srsgpu_pdsch_modulator_plan {
   srsgpu_context* ctx        = nullptr;
   mod_desc*       d_desc     = nullptr;
   mod_chunk*      d_chunks   = nullptr;
+  uint32_t*       d_seq      = nullptr;  ///< Scrambling sequences of the transmissions (plan lifetime).
   int             nof_chunks = 0;
 };
 
@@ -53,6 +54,58 @@ uint32_t gf2_apply(const uint32_t* cols, uint32_t v)
 }
 
 } // namespace
+
+std::vector<uint32_t> srsgpu::gold_sequence_offsets(const std::vector<uint32_t>& nwords)
+{
+  std::vector<uint32_t> off(nwords.size());
+  uint32_t              o = 0;
+  for (size_t t = 0; t < nwords.size(); ++t) {
+    off[t] = o;
+    o += nwords[t] + 1u;
+  }
+  return off;
+}
+
+int srsgpu::build_gold_sequences(srsgpu_context*              ctx,
+                                 const std::vector<uint32_t>& c_inits,
+                                 const std::vector<uint32_t>& nwords,
+                                 const std::vector<uint32_t>& offsets,
+                                 uint32_t**                   d_seq)
+{
+  *d_seq = nullptr;
+  if (c_inits.empty()) {
+    return SRSGPU_OK;
+  }
+  const size_t n     = c_inits.size();
+  const size_t total = static_cast<size_t>(offsets.back()) + nwords.back() + 1u;
+  uint32_t     maxw  = 0;
+  for (uint32_t w : nwords) {
+    maxw = w > maxw ? w : maxw;
+  }
+  uint32_t* d_small = nullptr;  // c_inits | offsets | nwords
+  bool      ok      = hipMalloc(reinterpret_cast<void**>(d_seq), total * 4) == hipSuccess &&
+               hipMemset(*d_seq, 0, total * 4) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&d_small), 3 * n * 4) == hipSuccess &&
+               hipMemcpy(d_small, c_inits.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemcpy(d_small + n, offsets.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemcpy(d_small + 2 * n, nwords.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess;
+  if (ok) {
+    launch_gold_fill(d_small, d_small + n, d_small + 2 * n, static_cast<int>(n), maxw, *d_seq, ctx->d_gold_x1,
+                     ctx->d_gold_x2_jump, ctx->d_gold_x2_lane, nullptr);
+    ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(nullptr) == hipSuccess;
+  }
+  if (d_small != nullptr) {
+    (void)hipFree(d_small);
+  }
+  if (!ok) {
+    if (*d_seq != nullptr) {
+      (void)hipFree(*d_seq);
+      *d_seq = nullptr;
+    }
+    return fail(SRSGPU_ERR_HIP, "failed to build the scrambling sequences");
+  }
+  return SRSGPU_OK;
+}
 
 /// Builds and uploads the scrambler's Gold-sequence tables into the context (once; caller holds ctx->mtx).
 int srsgpu::ensure_gold_tables(srsgpu_context* ctx)
@@ -270,11 +323,24 @@ int srsgpu_pdsch_modulator_plan_create(srsgpu_context*                ctx,
       }
     }
   }
+  std::vector<uint32_t> c_inits(descs.size()), nwords(descs.size());
+  for (size_t t = 0; t < descs.size(); ++t) {
+    c_inits[t] = descs[t].c_init;
+    nwords[t]  = (descs[t].nof_bits + 31u) / 32u;
+  }
+  const std::vector<uint32_t> seq_off = gold_sequence_offsets(nwords);
+  for (size_t t = 0; t < descs.size(); ++t) {
+    descs[t].seq_word_offset = seq_off[t];
+  }
   auto* plan       = new srsgpu_pdsch_modulator_plan();
   plan->ctx        = ctx;
   plan->nof_chunks = static_cast<int>(chunks.size());
   bool ok          = true;
   if (!chunks.empty()) {
+    if (build_gold_sequences(ctx, c_inits, nwords, seq_off, &plan->d_seq) != SRSGPU_OK) {
+      srsgpu_pdsch_modulator_plan_destroy(plan);
+      return SRSGPU_ERR_HIP;
+    }
     ok = hipMalloc(&plan->d_desc, descs.size() * sizeof(mod_desc)) == hipSuccess &&
          hipMemcpy(plan->d_desc, descs.data(), descs.size() * sizeof(mod_desc), hipMemcpyHostToDevice) == hipSuccess &&
          hipMalloc(&plan->d_chunks, chunks.size() * sizeof(mod_chunk)) == hipSuccess &&
@@ -298,8 +364,8 @@ int srsgpu_pdsch_modulator_plan_execute(const srsgpu_pdsch_modulator_plan* plan,
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
   launch_pdsch_modulate(plan->d_desc, plan->d_chunks, plan->nof_chunks,
-                        reinterpret_cast<const uint32_t*>(d_codewords), d_grids, plan->ctx->d_gold_x1,
-                        plan->ctx->d_gold_x2_jump, plan->ctx->d_gold_x2_lane, static_cast<hipStream_t>(stream));
+                        reinterpret_cast<const uint32_t*>(d_codewords), d_grids, plan->d_seq,
+                        static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
 }
@@ -309,7 +375,8 @@ void srsgpu_pdsch_modulator_plan_destroy(srsgpu_pdsch_modulator_plan* plan)
   if (plan == nullptr) {
     return;
   }
-  for (void* p : {static_cast<void*>(plan->d_desc), static_cast<void*>(plan->d_chunks)}) {
+  for (void* p : {static_cast<void*>(plan->d_desc), static_cast<void*>(plan->d_chunks),
+                  static_cast<void*>(plan->d_seq)}) {
     if (p != nullptr) {
       (void)hipFree(p);
     }

@@ -15,6 +15,7 @@ struct srsgpu_pusch_demodulator_plan {
   demod_desc*           d_desc     = nullptr;
   mod_chunk*            d_chunks   = nullptr;
   demap_pair_table*     d_tables   = nullptr;
+  uint32_t*             d_seq      = nullptr;  ///< Descrambling sequences of the transmissions (plan lifetime).
   int                   nof_chunks = 0;
   std::vector<uint32_t> nof_llrs;
 };
@@ -193,10 +194,23 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
   if (r != SRSGPU_OK) {
     return r;
   }
+  std::vector<uint32_t> c_inits(descs.size()), nwords(descs.size());
+  for (size_t t = 0; t < descs.size(); ++t) {
+    c_inits[t] = descs[t].c_init;
+    nwords[t]  = (descs[t].nof_llrs + 31u) / 32u;
+  }
+  const std::vector<uint32_t> seq_off = gold_sequence_offsets(nwords);
+  for (size_t t = 0; t < descs.size(); ++t) {
+    descs[t].seq_word_offset = seq_off[t];
+  }
   auto* plan       = new srsgpu_pusch_demodulator_plan();
   plan->ctx        = ctx;
   plan->nof_chunks = static_cast<int>(chunks.size());
   plan->nof_llrs   = std::move(nllr);
+  if (!chunks.empty() && build_gold_sequences(ctx, c_inits, nwords, seq_off, &plan->d_seq) != SRSGPU_OK) {
+    srsgpu_pusch_demodulator_plan_destroy(plan);
+    return SRSGPU_ERR_HIP;
+  }
   bool ok = hipMalloc(&plan->d_tables, tables.size() * sizeof(demap_pair_table)) == hipSuccess &&
             hipMemcpy(plan->d_tables, tables.data(), tables.size() * sizeof(demap_pair_table),
                       hipMemcpyHostToDevice) == hipSuccess;
@@ -233,8 +247,7 @@ int srsgpu_pusch_demodulator_plan_execute(const srsgpu_pusch_demodulator_plan* p
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
   launch_pusch_demodulate(plan->d_desc, plan->d_chunks, plan->nof_chunks, plan->d_tables, d_grids, d_ch_estimates,
-                          d_noise_var, d_llrs, plan->ctx->d_gold_x1, plan->ctx->d_gold_x2_jump,
-                          plan->ctx->d_gold_x2_lane, static_cast<hipStream_t>(stream));
+                          d_noise_var, d_llrs, plan->d_seq, static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
 }
@@ -245,7 +258,7 @@ void srsgpu_pusch_demodulator_plan_destroy(srsgpu_pusch_demodulator_plan* plan)
     return;
   }
   for (void* p : {static_cast<void*>(plan->d_desc), static_cast<void*>(plan->d_chunks),
-                  static_cast<void*>(plan->d_tables)}) {
+                  static_cast<void*>(plan->d_tables), static_cast<void*>(plan->d_seq)}) {
     if (p != nullptr) {
       (void)hipFree(p);
     }

@@ -273,7 +273,13 @@ __device__ __forceinline__ void write_hard_bits_pk(const int8_t* __restrict__ so
 /// only MAXL layers of check-to-variable state occupy VGPRs: the 4-layer high-rate codeblocks of a loaded cell run at
 /// twice the occupancy of the 46-layer worst case.
 template <int BG, int MODE, int MAXL>
-__global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : 5))) void ldpc_decode_pk_kernel(const dec_desc* __restrict__ descs,
+#ifndef LDPC_PK_MIN_BLOCKS_8
+#define LDPC_PK_MIN_BLOCKS_8 5
+#endif
+#ifndef LDPC_PK_KEEP_ADDR_MAXL
+#define LDPC_PK_KEEP_ADDR_MAXL 16
+#endif
+__global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_8))) void ldpc_decode_pk_kernel(const dec_desc* __restrict__ descs,
                                                              const int8_t* __restrict__ llrs,
                                                              uint8_t* __restrict__ out,
                                                              int32_t* __restrict__ results,
@@ -490,7 +496,7 @@ __global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : 5))) void ldp
       if (m < nl) {
         if (active) {
           __builtin_amdgcn_sched_barrier(0);
-          row_update_pk<BG, MODE, m, (MAXL <= 16)>(soft, abi, z2x2, sc, magw[m], sgw[m], hiw[m & 3]);
+          row_update_pk<BG, MODE, m, (MAXL <= LDPC_PK_KEEP_ADDR_MAXL)>(soft, abi, z2x2, sc, magw[m], sgw[m], hiw[m & 3]);
           __builtin_amdgcn_sched_barrier(0);
         }
 #ifndef LDPC_PK_EXPERIMENT_NO_LAYER_BARRIER  // timing experiments only: results are wrong without the barrier

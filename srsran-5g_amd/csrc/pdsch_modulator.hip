@@ -6,9 +6,10 @@
 // order), generic_functions/precoding/channel_precoder_generic.cpp:51 (precoding), adt/bf16.h:39 (rounding).
 //
 // Work decomposition: a workgroup owns 8192 codeword bits (256 words) of one transmission. Its four waves first stage
-// the scrambled words in LDS — the Gold sequence is evaluated at any position by jumping the x2 LFSR state with
-// precomputed GF(2) matrices (the chunk jump is wave-uniform: scalar loads; the per-lane jump is one column load per
-// set state bit) and reading x1 from a table — then every lane takes one RE whose bits start in the chunk: it forms
+// the scrambled words in LDS — codeword XOR the plan's precomputed scrambling sequence (filled once at plan creation
+// by gold_fill_kernel, which evaluates the Gold sequence at any position by jumping the x2 LFSR state with
+// precomputed GF(2) matrices and reading x1 from a table: the sequence depends only on c_init and the length, so the
+// steady state reads one resident word per codeword word instead of recomputing the jumps) — then every lane takes one RE whose bits start in the chunk: it forms
 // the L constellation points, precodes them for every port and stores one (re, im) bf16 pair per port. Consecutive
 // lanes hold consecutive REs of a symbol, so the grid stores are coalesced 4-byte writes. HBM-bound: the codeword is
 // read once (1 bit per bit) and every PDSCH RE of every port is written once (4 B).
@@ -25,16 +26,30 @@ namespace {
 
 constexpr int MOD_THREADS = 256;
 
-/// Scrambled codeword word w (bits 32w..32w+31, MSB first) of a transmission.
+/// Scrambled codeword word w (bits 32w..32w+31, MSB first) of a transmission: the plan's precomputed sequence word.
 __device__ __forceinline__ uint32_t scrambled_word(const mod_desc& d,
                                                    const uint32_t* __restrict__ cw,
-                                                   const uint32_t* __restrict__ x1,
-                                                   const uint32_t* __restrict__ x2_jump,
-                                                   const uint32_t* __restrict__ x2_lane,
-                                                   uint32_t w,
-                                                   uint32_t c_uniform)
+                                                   const uint32_t* __restrict__ seq,
+                                                   uint32_t w)
 {
-  return __builtin_bswap32(cw[d.cw_word_offset + w]) ^ gold_word(d.c_init, w, c_uniform, x1, x2_jump, x2_lane);
+  return __builtin_bswap32(cw[d.cw_word_offset + w]) ^ seq[d.seq_word_offset + w];
+}
+
+/// Plan-time fill of the (de)scrambling sequences (launch_gold_fill): Gold sequence by GF(2) jumps.
+__global__ __launch_bounds__(MOD_THREADS) void gold_fill_kernel(const uint32_t* __restrict__ c_inits,
+                                                                 const uint32_t* __restrict__ offsets,
+                                                                 const uint32_t* __restrict__ nwords,
+                                                                 uint32_t* __restrict__ seq,
+                                                                 const uint32_t* __restrict__ x1,
+                                                                 const uint32_t* __restrict__ x2_jump,
+                                                                 const uint32_t* __restrict__ x2_lane)
+{
+  const uint32_t t = blockIdx.y;
+  const uint32_t w = blockIdx.x * MOD_THREADS + threadIdx.x;
+  const uint32_t c = __builtin_amdgcn_readfirstlane(w >> 6);  // MOD_THREADS % 64 == 0: wave-uniform chunk jump
+  if (w < nwords[t]) {
+    seq[offsets[t] + w] = gold_word(c_inits[t], w, c, x1, x2_jump, x2_lane);
+  }
 }
 
 __device__ __forceinline__ uint32_t to_bf16_bits(float v)
@@ -47,9 +62,7 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
                                                                       const mod_chunk* __restrict__ chunks,
                                                                       const uint32_t* __restrict__ cw,
                                                                       uint32_t* __restrict__ grids,
-                                                                      const uint32_t* __restrict__ x1,
-                                                                      const uint32_t* __restrict__ x2_jump,
-                                                                      const uint32_t* __restrict__ x2_lane)
+                                                                      const uint32_t* __restrict__ seq)
 {
   __shared__ uint32_t bits[MOD_CHUNK_WORDS + 1];
   const mod_chunk ch  = chunks[blockIdx.x];
@@ -60,14 +73,12 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
   // Stage the chunk's scrambled words (and the first word of the next chunk, for an RE straddling the boundary).
   for (uint32_t j = tid; j < MOD_CHUNK_WORDS; j += MOD_THREADS) {
     const uint32_t w = ch.word0 + j;
-    // word0 is a multiple of 64: the 64 words of a wave share their 2048-bit jump.
-    const uint32_t c = __builtin_amdgcn_readfirstlane(w >> 6);
-    bits[j]          = (w < nwords) ? scrambled_word(d, cw, x1, x2_jump, x2_lane, w, c) : 0u;
+    bits[j]          = (w < nwords) ? scrambled_word(d, cw, seq, w) : 0u;
   }
   {
     if (tid == 0) {
       const uint32_t w2 = ch.word0 + MOD_CHUNK_WORDS;
-      bits[MOD_CHUNK_WORDS] = (w2 < nwords) ? scrambled_word(d, cw, x1, x2_jump, x2_lane, w2, w2 >> 6) : 0u;
+      bits[MOD_CHUNK_WORDS] = (w2 < nwords) ? scrambled_word(d, cw, seq, w2) : 0u;
     }
   }
 
@@ -216,16 +227,33 @@ void launch_pdsch_modulate(const mod_desc*  d_desc,
                            int              nof_chunks,
                            const uint32_t*  d_codewords,
                            uint32_t*        d_grids,
-                           const uint32_t*  d_x1,
-                           const uint32_t*  d_x2_jump,
-                           const uint32_t*  d_x2_lane,
+                           const uint32_t*  d_seq,
                            hipStream_t      stream)
 {
   if (nof_chunks <= 0) {
     return;
   }
   hipLaunchKernelGGL(pdsch_modulate_kernel, dim3(static_cast<unsigned>(nof_chunks)), dim3(MOD_THREADS), 0, stream,
-                     d_desc, d_chunks, d_codewords, d_grids, d_x1, d_x2_jump, d_x2_lane);
+                     d_desc, d_chunks, d_codewords, d_grids, d_seq);
+}
+
+void launch_gold_fill(const uint32_t* d_c_inits,
+                      const uint32_t* d_offsets,
+                      const uint32_t* d_nwords,
+                      int             nof_tx,
+                      uint32_t        max_nwords,
+                      uint32_t*       d_seq,
+                      const uint32_t* d_x1,
+                      const uint32_t* d_x2_jump,
+                      const uint32_t* d_x2_lane,
+                      hipStream_t     stream)
+{
+  if (nof_tx <= 0 || max_nwords == 0) {
+    return;
+  }
+  const dim3 grid((max_nwords + MOD_THREADS - 1) / MOD_THREADS, static_cast<unsigned>(nof_tx));
+  hipLaunchKernelGGL(gold_fill_kernel, grid, dim3(MOD_THREADS), 0, stream, d_c_inits, d_offsets, d_nwords, d_seq, d_x1,
+                     d_x2_jump, d_x2_lane);
 }
 
 } // namespace srsgpu

@@ -7,8 +7,8 @@
 // noise, near-zero parts, avx2_helpers.h:121 quantisation).
 //
 // Work decomposition (like the PDSCH modulator): a workgroup owns 32768 codeword LLRs of one transmission (the REs
-// whose first LLR falls in them). The four waves first stage the 32768 + 32 descrambling-sequence bits in LDS (Gold
-// sequence by GF(2) jumps, gold_device.h). Then every lane takes one RE: it loads the P received values and the L x P
+// whose first LLR falls in them). The four waves first stage the 32768 + 32 descrambling-sequence bits in LDS (the plan's
+// precomputed Gold sequence words, gold_fill_kernel). Then every lane takes one RE: it loads the P received values and the L x P
 // channel estimates (consecutive lanes read consecutive subcarriers: coalesced 4-byte loads), equalizes, demaps the
 // L * Qm LLRs, flips the signs the sequence selects and stages the bytes in LDS; the workgroup finally writes its
 // contiguous LLR range with dword stores. HBM-bound: (P + L P) x 4 B in and L Qm B out per RE.
@@ -225,8 +225,8 @@ struct demod_uniform {
   const demod_desc*       d;
   uint32_t                re_begin, re_end, word0;
   float                   nv[4], nv_max;
-  const demap_pair_table* tables;                 ///< Global demapper tables (staged into LDS for Qm >= 6).
-  const uint32_t*         x1, *x2_jump, *x2_lane;  ///< Gold sequence tables.
+  const demap_pair_table* tables;  ///< Global demapper tables (staged into LDS for Qm >= 6).
+  const uint32_t*         gseq;    ///< The plan's precomputed descrambling sequences.
 };
 
 /// Stages the chunk's descrambling words (and the first word of the next chunk) and, for 64/256QAM, the demapper
@@ -238,12 +238,11 @@ __device__ __forceinline__ void stage_chunk(const demod_uniform& u, uint32_t* se
   const uint32_t    nwords = (d.nof_llrs + 31u) >> 5;
   for (uint32_t j = tid; j < MOD_CHUNK_WORDS; j += DEMOD_THREADS) {
     const uint32_t w = u.word0 + j;
-    const uint32_t c = __builtin_amdgcn_readfirstlane(w >> 6);  // word0 % 64 == 0: wave-uniform jump
-    seq[j]           = (w < nwords) ? gold_word(d.c_init, w, c, u.x1, u.x2_jump, u.x2_lane) : 0u;
+    seq[j]           = (w < nwords) ? u.gseq[d.seq_word_offset + w] : 0u;
   }
   if (tid == 0) {
     const uint32_t w2    = u.word0 + MOD_CHUNK_WORDS;
-    seq[MOD_CHUNK_WORDS] = (w2 < nwords) ? gold_word(d.c_init, w2, w2 >> 6, u.x1, u.x2_jump, u.x2_lane) : 0u;
+    seq[MOD_CHUNK_WORDS] = (w2 < nwords) ? u.gseq[d.seq_word_offset + w2] : 0u;
   }
   if (d.qm >= 6) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(u.tables);
@@ -448,9 +447,7 @@ __global__ __launch_bounds__(DEMOD_THREADS) DEMOD_OCCUPANCY void pusch_demodulat
                                                                          const uint32_t* __restrict__ ce,
                                                                          const float* __restrict__ noise_var,
                                                                          int8_t* __restrict__ llrs,
-                                                                         const uint32_t* __restrict__ x1,
-                                                                         const uint32_t* __restrict__ x2_jump,
-                                                                         const uint32_t* __restrict__ x2_lane)
+                                                                         const uint32_t* __restrict__ gseq)
 {
   __shared__ uint32_t         seq[MOD_CHUNK_WORDS + 1];
   __shared__ demap_pair_table tab[DEMAP_TABLES];
@@ -464,9 +461,7 @@ __global__ __launch_bounds__(DEMOD_THREADS) DEMOD_OCCUPANCY void pusch_demodulat
   u.re_end   = ch.re_end;
   u.word0    = ch.word0;
   u.tables   = tables;
-  u.x1       = x1;
-  u.x2_jump  = x2_jump;
-  u.x2_lane  = x2_lane;
+  u.gseq     = gseq;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     u.nv[p] = noise_var[4 * d.tx + p];
@@ -517,16 +512,14 @@ void launch_pusch_demodulate(const demod_desc*       d_desc,
                              const uint32_t*         d_ch_est,
                              const float*            d_noise_var,
                              int8_t*                 d_llrs,
-                             const uint32_t*         d_x1,
-                             const uint32_t*         d_x2_jump,
-                             const uint32_t*         d_x2_lane,
+                             const uint32_t*         d_seq,
                              hipStream_t             stream)
 {
   if (nof_chunks <= 0) {
     return;
   }
   hipLaunchKernelGGL(pusch_demodulate_kernel, dim3(static_cast<unsigned>(nof_chunks)), dim3(DEMOD_THREADS), 0, stream,
-                     d_desc, d_chunks, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_x1, d_x2_jump, d_x2_lane);
+                     d_desc, d_chunks, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq);
 }
 
 } // namespace srsgpu

@@ -208,8 +208,10 @@ struct mod_desc {
   uint16_t pad;
   uint16_t sym_cum[16];     ///< Data REs in the symbols before symbol l (l = 0..14).
   float    w[4][4][2];      ///< Precoding weights [port][layer] times the modulation amplitude.
+  uint32_t seq_word_offset; ///< First word of the transmission's scrambling sequence in the plan's sequence buffer.
+  uint32_t pad2;
 };
-static_assert(sizeof(mod_desc) == 200, "mod_desc layout");
+static_assert(sizeof(mod_desc) == 208, "mod_desc layout");
 
 /// PDSCH modulator / PUSCH demodulator work item: MOD_CHUNK_WORDS x 32 codeword bits of one transmission and the REs
 /// starting in them.
@@ -234,10 +236,22 @@ void launch_pdsch_modulate(const mod_desc*  d_desc,
                            int              nof_chunks,
                            const uint32_t*  d_codewords,
                            uint32_t*        d_grids,
-                           const uint32_t*  d_x1,
-                           const uint32_t*  d_x2_jump,
-                           const uint32_t*  d_x2_lane,
+                           const uint32_t*  d_seq,
                            hipStream_t      stream);
+
+/// Fills a plan's (de)scrambling sequence buffer once, at plan creation: for transmission t, words
+/// seq[offsets[t] + w] = c(32 w) .. c(32 w + 31) (MSB first) of the Gold sequence with initial state c_inits[t],
+/// w < nwords[t] (pdsch_modulator.hip: gold_fill_kernel).
+void launch_gold_fill(const uint32_t* d_c_inits,
+                      const uint32_t* d_offsets,
+                      const uint32_t* d_nwords,
+                      int             nof_tx,
+                      uint32_t        max_nwords,
+                      uint32_t*       d_seq,
+                      const uint32_t* d_x1,
+                      const uint32_t* d_x2_jump,
+                      const uint32_t* d_x2_lane,
+                      hipStream_t     stream);
 
 /// OFDM (de)modulator job: one OFDM symbol of one port of one grid (ofdm.hip).
 struct ofdm_job {
@@ -283,6 +297,7 @@ struct demod_desc {
   uint8_t  eq;              ///< Equalizer kind (DEMOD_EQ_*).
   uint8_t  ce_compact;      ///< Estimates in the compact layout: every symbol reads the row at ce_base.
   uint16_t sym_cum[16];     ///< Data REs in the symbols before symbol l (l = 0..14).
+  uint32_t seq_word_offset; ///< First word of the transmission's descrambling sequence in the plan's sequence buffer.
 };
 static_assert(sizeof(demod_desc) == 88, "demod_desc layout");
 
@@ -382,9 +397,7 @@ void launch_pusch_demodulate(const demod_desc*        d_desc,
                              const uint32_t*          d_ch_est,
                              const float*             d_noise_var,
                              int8_t*                  d_llrs,
-                             const uint32_t*          d_x1,
-                             const uint32_t*          d_x2_jump,
-                             const uint32_t*          d_x2_lane,
+                             const uint32_t*          d_seq,
                              hipStream_t              stream);
 
 } // namespace srsgpu

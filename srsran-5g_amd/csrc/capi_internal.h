@@ -73,7 +73,8 @@ int build_gold_sequences(srsgpu_context*              ctx,
                          const std::vector<uint32_t>& c_inits,
                          const std::vector<uint32_t>& nwords,
                          const std::vector<uint32_t>& offsets,
-                         uint32_t**                   d_seq);
+                         uint32_t**                   d_seq,
+                         const std::vector<uint32_t>* wstart = nullptr);
 
 /// Word offsets of the transmissions' sequences in a plan's sequence buffer (each padded by one word).
 std::vector<uint32_t> gold_sequence_offsets(const std::vector<uint32_t>& nwords);

@@ -70,28 +70,33 @@ int srsgpu::build_gold_sequences(srsgpu_context*              ctx,
                                  const std::vector<uint32_t>& c_inits,
                                  const std::vector<uint32_t>& nwords,
                                  const std::vector<uint32_t>& offsets,
-                                 uint32_t**                   d_seq)
+                                 uint32_t**                   d_seq,
+                                 const std::vector<uint32_t>* wstart)
 {
   *d_seq = nullptr;
   if (c_inits.empty()) {
     return SRSGPU_OK;
   }
   const size_t n     = c_inits.size();
-  const size_t total = static_cast<size_t>(offsets.back()) + nwords.back() + 1u;
+  size_t       total = 1;
   uint32_t     maxw  = 0;
-  for (uint32_t w : nwords) {
-    maxw = w > maxw ? w : maxw;
+  for (size_t t = 0; t < n; ++t) {
+    total = std::max(total, static_cast<size_t>(offsets[t]) + nwords[t] + 1u);
+    maxw  = std::max(maxw, nwords[t]);
   }
-  uint32_t* d_small = nullptr;  // c_inits | offsets | nwords
+  uint32_t* d_small = nullptr;  // c_inits | offsets | nwords | wstart
   bool      ok      = hipMalloc(reinterpret_cast<void**>(d_seq), total * 4) == hipSuccess &&
                hipMemset(*d_seq, 0, total * 4) == hipSuccess &&
-               hipMalloc(reinterpret_cast<void**>(&d_small), 3 * n * 4) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&d_small), 4 * n * 4) == hipSuccess &&
                hipMemcpy(d_small, c_inits.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess &&
                hipMemcpy(d_small + n, offsets.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess &&
-               hipMemcpy(d_small + 2 * n, nwords.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess;
+               hipMemcpy(d_small + 2 * n, nwords.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess &&
+               (wstart == nullptr ||
+                hipMemcpy(d_small + 3 * n, wstart->data(), n * 4, hipMemcpyHostToDevice) == hipSuccess);
   if (ok) {
-    launch_gold_fill(d_small, d_small + n, d_small + 2 * n, static_cast<int>(n), maxw, *d_seq, ctx->d_gold_x1,
-                     ctx->d_gold_x2_jump, ctx->d_gold_x2_lane, nullptr);
+    launch_gold_fill(d_small, d_small + n, d_small + 2 * n, wstart != nullptr ? d_small + 3 * n : nullptr,
+                     static_cast<int>(n), maxw, *d_seq, ctx->d_gold_x1, ctx->d_gold_x2_jump, ctx->d_gold_x2_lane,
+                     nullptr);
     ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(nullptr) == hipSuccess;
   }
   if (d_small != nullptr) {

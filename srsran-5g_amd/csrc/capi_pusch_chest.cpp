@@ -18,6 +18,7 @@ struct srsgpu_pusch_chest_plan {
   int             max_pilots = 0;  ///< Largest job: pilots per DM-RS symbol.
   int             max_dmrs   = 0;  ///< Largest job: DM-RS symbols.
   int             max_words  = 0;  ///< Largest job: staged sequence words per DM-RS symbol.
+  uint32_t*       d_seq      = nullptr;  ///< DM-RS sequence words of every job (plan lifetime).
 };
 
 namespace {
@@ -165,6 +166,26 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
     delete plan;
     return fail(SRSGPU_ERR_INVALID_ARG, "channel estimation job too large for the LDS");
   }
+  // DM-RS sequences, resident: per job and DM-RS symbol the words the kernel stages (from the allocation's first
+  // sequence word), filled once.
+  std::vector<uint32_t> c_inits, nwords, offsets, wstart;
+  uint32_t              base = 0;
+  for (chest_job& jb : jobs) {
+    const uint32_t n0 = 2u * jb.seq_offset;
+    const uint32_t nw = ((n0 & 31u) + 2u * jb.nof_pilots + 31u) >> 5;
+    jb.gseq_base      = base;
+    for (unsigned s = 0; s < jb.nof_dmrs; ++s) {
+      c_inits.push_back(jb.c_init[s]);
+      nwords.push_back(nw);
+      offsets.push_back(base + s * nw);
+      wstart.push_back(n0 >> 5);
+    }
+    base += jb.nof_dmrs * nw;
+  }
+  if (build_gold_sequences(ctx, c_inits, nwords, offsets, &plan->d_seq, &wstart) != SRSGPU_OK) {
+    srsgpu_pusch_chest_plan_destroy(plan);
+    return SRSGPU_ERR_HIP;
+  }
   if (!jobs.empty() && (hipMalloc(&plan->d_jobs, jobs.size() * sizeof(chest_job)) != hipSuccess ||
                         hipMemcpy(plan->d_jobs, jobs.data(), jobs.size() * sizeof(chest_job), hipMemcpyHostToDevice) !=
                             hipSuccess)) {
@@ -186,9 +207,7 @@ int srsgpu_pusch_chest_plan_execute(const srsgpu_pusch_chest_plan* plan,
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
   launch_pusch_chest(plan->d_jobs, plan->nof_jobs, plan->max_pilots, plan->max_dmrs, plan->max_words, d_grids,
-                     d_ch_estimates, d_noise_var, d_metrics,
-                     plan->ctx->d_gold_x1, plan->ctx->d_gold_x2_jump, plan->ctx->d_gold_x2_lane,
-                     static_cast<hipStream_t>(stream));
+                     d_ch_estimates, d_noise_var, d_metrics, plan->d_seq, static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
 }
@@ -200,6 +219,9 @@ void srsgpu_pusch_chest_plan_destroy(srsgpu_pusch_chest_plan* plan)
   }
   if (plan->d_jobs != nullptr) {
     (void)hipFree(plan->d_jobs);
+  }
+  if (plan->d_seq != nullptr) {
+    (void)hipFree(plan->d_seq);
   }
   delete plan;
 }

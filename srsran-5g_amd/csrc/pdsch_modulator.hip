@@ -39,16 +39,17 @@ __device__ __forceinline__ uint32_t scrambled_word(const mod_desc& d,
 __global__ __launch_bounds__(MOD_THREADS) void gold_fill_kernel(const uint32_t* __restrict__ c_inits,
                                                                  const uint32_t* __restrict__ offsets,
                                                                  const uint32_t* __restrict__ nwords,
+                                                                 const uint32_t* __restrict__ wstart,
                                                                  uint32_t* __restrict__ seq,
                                                                  const uint32_t* __restrict__ x1,
                                                                  const uint32_t* __restrict__ x2_jump,
                                                                  const uint32_t* __restrict__ x2_lane)
 {
   const uint32_t t = blockIdx.y;
-  const uint32_t w = blockIdx.x * MOD_THREADS + threadIdx.x;
-  const uint32_t c = __builtin_amdgcn_readfirstlane(w >> 6);  // MOD_THREADS % 64 == 0: wave-uniform chunk jump
-  if (w < nwords[t]) {
-    seq[offsets[t] + w] = gold_word(c_inits[t], w, c, x1, x2_jump, x2_lane);
+  const uint32_t i = blockIdx.x * MOD_THREADS + threadIdx.x;
+  if (i < nwords[t]) {
+    const uint32_t w = (wstart != nullptr ? wstart[t] : 0u) + i;
+    seq[offsets[t] + i] = gold_word(c_inits[t], w, w >> 6, x1, x2_jump, x2_lane);
   }
 }
 
@@ -240,6 +241,7 @@ void launch_pdsch_modulate(const mod_desc*  d_desc,
 void launch_gold_fill(const uint32_t* d_c_inits,
                       const uint32_t* d_offsets,
                       const uint32_t* d_nwords,
+                      const uint32_t* d_wstart,
                       int             nof_tx,
                       uint32_t        max_nwords,
                       uint32_t*       d_seq,
@@ -252,8 +254,8 @@ void launch_gold_fill(const uint32_t* d_c_inits,
     return;
   }
   const dim3 grid((max_nwords + MOD_THREADS - 1) / MOD_THREADS, static_cast<unsigned>(nof_tx));
-  hipLaunchKernelGGL(gold_fill_kernel, grid, dim3(MOD_THREADS), 0, stream, d_c_inits, d_offsets, d_nwords, d_seq, d_x1,
-                     d_x2_jump, d_x2_lane);
+  hipLaunchKernelGGL(gold_fill_kernel, grid, dim3(MOD_THREADS), 0, stream, d_c_inits, d_offsets, d_nwords, d_wstart,
+                     d_seq, d_x1, d_x2_jump, d_x2_lane);
 }
 
 } // namespace srsgpu

@@ -15,7 +15,7 @@
 //
 // One wavefront per job (a UE's allocation is a few RBs: tens of pilots) keeps the many small jobs of a slot batch
 // resident together (dynamic LDS sized by the plan's largest job). The DM-RS sequence words of every DM-RS symbol are
-// staged in LDS once (Gold sequence by GF(2) jumps, gold_device.h); the edge regression of the virtual pilots runs on
+// staged in LDS once (the plan's resident sequence words, filled at plan creation by gold_fill_kernel); the edge regression of the virtual pilots runs on
 // the lanes (one 32-lane half per band edge, unwrap as a prefix sum); reductions are wave shuffles. HBM traffic per job:
 // the D DM-RS symbols' pilots of one port (read twice: the second pass, for the noise residual, hits L2) and 4 B per
 // estimated RE per layer (the dominant term).
@@ -135,9 +135,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
                                                                     uint32_t* __restrict__ ce,
                                                                     float* __restrict__ noise_var,
                                                                     float* __restrict__ metrics,
-                                                                    const uint32_t* __restrict__ x1,
-                                                                    const uint32_t* __restrict__ x2_jump,
-                                                                    const uint32_t* __restrict__ x2_lane)
+                                                                    const uint32_t* __restrict__ gseq)
 {
   extern __shared__ __align__(16) unsigned char lds_raw[];
   const int  EN = max_pilots + 2 * CHEST_VP;
@@ -169,10 +167,9 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
     L.taps[lane] = jb.taps[lane];
   }
   const int nwords = static_cast<int>(((n0 & 31u) + 2u * static_cast<uint32_t>(N) + 31u) >> 5);
-  for (int s = 0; s < D; ++s) {
+  for (int s = 0; s < D; ++s) {  // the plan's resident sequence words (gold_fill_kernel at plan creation)
     for (int wl = lane; wl < nwords; wl += CHEST_THREADS) {
-      const uint32_t w     = w0 + static_cast<uint32_t>(wl);
-      L.seq[s * W + wl] = gold_word(jb.c_init[s], w, w >> 6, x1, x2_jump, x2_lane);
+      L.seq[s * W + wl] = gseq[jb.gseq_base + static_cast<uint32_t>(s * nwords + wl)];
     }
   }
   __syncthreads();
@@ -336,9 +333,7 @@ void launch_pusch_chest(const chest_job* d_jobs,
                         uint32_t*        d_ce,
                         float*           d_noise_var,
                         float*           d_metrics,
-                        const uint32_t*  d_x1,
-                        const uint32_t*  d_x2_jump,
-                        const uint32_t*  d_x2_lane,
+                        const uint32_t*  d_seq,
                         hipStream_t      stream)
 {
   if (nof_jobs <= 0) {
@@ -347,7 +342,7 @@ void launch_pusch_chest(const chest_job* d_jobs,
   const size_t lds = pusch_chest_lds_bytes(max_pilots, max_dmrs, max_words);
   hipLaunchKernelGGL(pusch_chest_kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(CHEST_THREADS),
                      static_cast<unsigned>(lds), stream, d_jobs, max_pilots, max_dmrs, max_words, d_grids, d_ce,
-                     d_noise_var, d_metrics, d_x1, d_x2_jump, d_x2_lane);
+                     d_noise_var, d_metrics, d_seq);
 }
 
 } // namespace srsgpu

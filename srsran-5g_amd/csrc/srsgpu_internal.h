@@ -239,12 +239,13 @@ void launch_pdsch_modulate(const mod_desc*  d_desc,
                            const uint32_t*  d_seq,
                            hipStream_t      stream);
 
-/// Fills a plan's (de)scrambling sequence buffer once, at plan creation: for transmission t, words
-/// seq[offsets[t] + w] = c(32 w) .. c(32 w + 31) (MSB first) of the Gold sequence with initial state c_inits[t],
-/// w < nwords[t] (pdsch_modulator.hip: gold_fill_kernel).
+/// Fills a plan's (de)scrambling sequence buffer once, at plan creation: for entry t, words
+/// seq[offsets[t] + i] = c(32 w) .. c(32 w + 31) (MSB first), w = wstart[t] + i (wstart null: 0), of the Gold sequence
+/// with initial state c_inits[t], i < nwords[t] (pdsch_modulator.hip: gold_fill_kernel).
 void launch_gold_fill(const uint32_t* d_c_inits,
                       const uint32_t* d_offsets,
                       const uint32_t* d_nwords,
+                      const uint32_t* d_wstart,
                       int             nof_tx,
                       uint32_t        max_nwords,
                       uint32_t*       d_seq,
@@ -365,6 +366,7 @@ struct chest_job {
   uint8_t  first_symbol;     ///< First allocated OFDM symbol.
   uint8_t  nof_symbols;      ///< Allocated OFDM symbols.
   uint8_t  pad[3];
+  uint32_t gseq_base;        ///< The job's DM-RS sequence words in the plan's buffer: [DM-RS symbol][staged word].
 };
 
 constexpr uint8_t CHEST_FD_NONE   = 0;
@@ -384,9 +386,7 @@ void launch_pusch_chest(const chest_job* d_jobs,
                         uint32_t*        d_ce,
                         float*           d_noise_var,
                         float*           d_metrics,
-                        const uint32_t*  d_x1,
-                        const uint32_t*  d_x2_jump,
-                        const uint32_t*  d_x2_lane,
+                        const uint32_t*  d_seq,
                         hipStream_t      stream);
 
 void launch_pusch_demodulate(const demod_desc*        d_desc,

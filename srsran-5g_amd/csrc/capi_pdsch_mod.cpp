@@ -15,6 +15,7 @@ static_assert(sizeof(srsgpu_pdsch_dmrs_config) == 152, "srsgpu_pdsch_dmrs_config
 struct srsgpu_pdsch_dmrs_plan {
   srsgpu_context* ctx      = nullptr;
   dmrs_job*       d_jobs   = nullptr;
+  uint32_t*       d_seq    = nullptr;  ///< DM-RS sequence words of every job (plan lifetime).
   int             nof_jobs = 0;
 };
 
@@ -448,6 +449,23 @@ int srsgpu_pdsch_dmrs_plan_create(srsgpu_context*                 ctx,
   auto* plan     = new srsgpu_pdsch_dmrs_plan();
   plan->ctx      = ctx;
   plan->nof_jobs = static_cast<int>(jobs.size());
+  // Resident sequence words of every job, filled once.
+  std::vector<uint32_t> c_inits, nwords, offsets, wstart;
+  uint32_t              base = 0;
+  for (dmrs_job& jb : jobs) {
+    const uint32_t n0 = 2u * jb.seq_offset;
+    const uint32_t nw = ((n0 & 31u) + 2u * jb.nof_pilots + 31u) >> 5;
+    jb.gseq_base      = base;
+    c_inits.push_back(jb.c_init);
+    nwords.push_back(nw);
+    offsets.push_back(base);
+    wstart.push_back(n0 >> 5);
+    base += nw;
+  }
+  if (build_gold_sequences(ctx, c_inits, nwords, offsets, &plan->d_seq, &wstart) != SRSGPU_OK) {
+    srsgpu_pdsch_dmrs_plan_destroy(plan);
+    return SRSGPU_ERR_HIP;
+  }
   if (!jobs.empty() && (hipMalloc(&plan->d_jobs, jobs.size() * sizeof(dmrs_job)) != hipSuccess ||
                         hipMemcpy(plan->d_jobs, jobs.data(), jobs.size() * sizeof(dmrs_job), hipMemcpyHostToDevice) !=
                             hipSuccess)) {
@@ -463,8 +481,7 @@ int srsgpu_pdsch_dmrs_plan_execute(const srsgpu_pdsch_dmrs_plan* plan, uint32_t*
   if (plan == nullptr || d_grids == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  launch_pdsch_dmrs(plan->d_jobs, plan->nof_jobs, d_grids, plan->ctx->d_gold_x1, plan->ctx->d_gold_x2_jump,
-                    plan->ctx->d_gold_x2_lane, static_cast<hipStream_t>(stream));
+  launch_pdsch_dmrs(plan->d_jobs, plan->nof_jobs, d_grids, plan->d_seq, static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
 }
@@ -476,6 +493,9 @@ void srsgpu_pdsch_dmrs_plan_destroy(srsgpu_pdsch_dmrs_plan* plan)
   }
   if (plan->d_jobs != nullptr) {
     (void)hipFree(plan->d_jobs);
+  }
+  if (plan->d_seq != nullptr) {
+    (void)hipFree(plan->d_seq);
   }
   delete plan;
 }

@@ -165,16 +165,15 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
 /// mapping): lane i owns DM-RS index i of the symbol in every CDM group. Same rounding as the modulator.
 __global__ __launch_bounds__(MOD_THREADS) void pdsch_dmrs_kernel(const dmrs_job* __restrict__ jobs,
                                                                   uint32_t* __restrict__ grids,
-                                                                  const uint32_t* __restrict__ x1,
-                                                                  const uint32_t* __restrict__ x2_jump,
-                                                                  const uint32_t* __restrict__ x2_lane)
+                                                                  const uint32_t* __restrict__ gseq)
 {
   const dmrs_job& jb     = jobs[blockIdx.x];
   const uint32_t  per_rb = jb.type2 ? 4u : 6u;
+  const uint32_t  wfirst = (2 * jb.seq_offset) >> 5;
   for (uint32_t i = threadIdx.x; i < jb.nof_pilots; i += MOD_THREADS) {
     const uint32_t n    = 2 * (jb.seq_offset + i);
     const uint32_t w    = n >> 5;
-    const uint32_t word = gold_word(jb.c_init, w, w >> 6, x1, x2_jump, x2_lane);
+    const uint32_t word = gseq[jb.gseq_base + (w - wfirst)];  // the plan's resident sequence words
     const uint32_t sh   = 31u - (n & 31u);
     const float    re   = ((word >> sh) & 1u) ? -jb.amp : jb.amp;
     const float    im   = ((word >> (sh - 1)) & 1u) ? -jb.amp : jb.amp;
@@ -211,16 +210,14 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_dmrs_kernel(const dmrs_job*
 void launch_pdsch_dmrs(const dmrs_job* d_jobs,
                        int             nof_jobs,
                        uint32_t*       d_grids,
-                       const uint32_t* d_x1,
-                       const uint32_t* d_x2_jump,
-                       const uint32_t* d_x2_lane,
+                       const uint32_t* d_seq,
                        hipStream_t     stream)
 {
   if (nof_jobs <= 0) {
     return;
   }
   hipLaunchKernelGGL(pdsch_dmrs_kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(MOD_THREADS), 0, stream, d_jobs,
-                     d_grids, d_x1, d_x2_jump, d_x2_lane);
+                     d_grids, d_seq);
 }
 
 void launch_pdsch_modulate(const mod_desc*  d_desc,

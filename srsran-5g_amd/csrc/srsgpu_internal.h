@@ -329,14 +329,13 @@ struct dmrs_job {
   uint8_t  L, P;         ///< Layers (DM-RS ports 0..L-1), antenna ports.
   uint8_t  lp;           ///< l' (1 when the previous symbol also carries DM-RS): selects w_t.
   uint8_t  pad[2];
+  uint32_t gseq_base;    ///< The job's sequence words (from word seq_offset / 16) in the plan's buffer.
 };
 
 void launch_pdsch_dmrs(const dmrs_job* d_jobs,
                        int             nof_jobs,
                        uint32_t*       d_grids,
-                       const uint32_t* d_x1,
-                       const uint32_t* d_x2_jump,
-                       const uint32_t* d_x2_lane,
+                       const uint32_t* d_seq,
                        hipStream_t     stream);
 
 /// PUSCH channel estimator job (pusch_chest.hip): one (transmission, rx port, DM-RS CDM group).

@@ -157,11 +157,21 @@ __device__ __forceinline__ void dematch_new_data(const dm_desc& d, const int8_t*
     }
   }
   // Phase 1: copies, symbol-major.
+  // 256QAM symbols 8-byte aligned (codewords are whole symbols from an aligned offset): one 8-byte load each.
+  const bool q8 = Qm == 8 && ((d.llr_offset & 7u) == 0u);
   for (int r = threadIdx.x; r < R; r += blockDim.x) {
     int8_t sym[8];
+    if (q8) {
+      const uint2 v = *reinterpret_cast<const uint2*>(in + 8 * r);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sym[j] = (j < Qm) ? in[r * Qm + j] : 0;
+      for (int j = 0; j < 8; ++j) {
+        sym[j] = static_cast<int8_t>(((j < 4) ? v.x : v.y) >> (8 * (j & 3)));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sym[j] = (j < Qm) ? in[r * Qm + j] : 0;
+      }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {

@@ -292,6 +292,20 @@ def main():
         if tj.get("slots_per_step") == Sb and tj.get("worst_case", False) == args.worst_case:
             traffic = tj.get("hbm_bytes_per_launch")
 
+    # VALU roofline of the same launch: wave-level VALU instructions per launch from the committed SQ counter pass
+    # (rocprofv3 --pmc SQ_INSTS_VALU ..., tools/sq_summary.py; same workload, same iterations) over the live kernel time.
+    valu = None
+    sqfile = os.path.join(ROOT, "profiles", "r1_v22_sq_valu.json")
+    if os.path.exists(sqfile) and Sb == 16 and not args.worst_case:
+        with open(sqfile) as f:
+            sq = json.load(f).get("ldpc_decode_pk_kernel<1, 1, 8>")
+        if sq:
+            peak = 1024 * 2.4e9 / 2  # SIMDs x clock / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md)
+            rate = sq["valu_instr"] / (dec_ms * 1e-3)
+            valu = {"bound": "valu_issue", "achieved": rate, "peak": peak, "unit": "wave-instr/s",
+                    "frac": rate / peak, "instr_per_launch": sq["valu_instr"],
+                    "source": "profiles/r1_v22_sq_valu.json (SQ_INSTS_VALU) / live kernel time"}
+
     # Algorithmic HBM bytes per pipeline pair (Sb slots) of the signal-chain stages (each byte read or written once;
     # DESIGN.md "Kernels"): bf16 grids are 4 B per RE, time samples 8 B (complex float), estimates 4 B per (layer,
     # port, RE), LLRs 1 B. The stage times come from batch 0's pipeline pair.
@@ -359,6 +373,7 @@ def main():
                              + ("an eager pass of as many steps right after the graph-replayed timed loop"
                                 if args.graph else "inside the timed loop")
                              + "); the LDPC decoder is VALU-issue/latency-bound, not HBM-bound (DESIGN.md)"},
+        "roofline_valu": valu,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -75,6 +75,7 @@ struct srsgpu_pdsch_encoder_plan {
   enc_desc*       d_enc[2]   = {nullptr, nullptr};  ///< Per base graph: byte-kernel codeblocks, then packed ones.
   int             count[2]   = {0, 0};
   int             count_pk[2] = {0, 0};
+  bool            inline_tb_crc = false;  ///< Every codeblock packed, every TB CRC table cached: no tb_crc_kernel.
   int             threads[2] = {64, 64};
   size_t          out_begin  = 0;
   size_t          out_end    = 0;
@@ -894,6 +895,8 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
     srsgpu_pdsch_encoder_plan_destroy(plan);
     return fail(SRSGPU_ERR_HIP, "failed to upload encoder descriptors");
   }
+  plan->inline_tb_crc = plan->count[0] == 0 && plan->count[1] == 0 &&
+                        std::all_of(tbd.begin(), tbd.end(), [](const tb_crc_desc& t) { return t.table != NO_CRC_TABLE; });
   *plan_out = plan;
   return SRSGPU_OK;
 }
@@ -919,14 +922,17 @@ int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
   if (plan->out_end > plan->out_begin) {
     HIP_TRY(hipMemsetAsync(d_codewords + plan->out_begin, 0, plan->out_end - plan->out_begin, s));
   }
-  launch_tb_crc(plan->d_tb, plan->nof_tbs, d_tbs, plan->d_tb_crc, plan->ctx->d_crc_arena, s);
-  HIP_TRY(hipGetLastError());
+  if (!plan->inline_tb_crc) {
+    launch_tb_crc(plan->d_tb, plan->nof_tbs, d_tbs, plan->d_tb_crc, plan->ctx->d_crc_arena, s);
+    HIP_TRY(hipGetLastError());
+  }
   stage_timer::mark(ev, 1, s);
   for (int b = 0; b < 2; ++b) {
     auto* out = reinterpret_cast<uint32_t*>(d_codewords);
     if (plan->count_pk[b] > 0) {
       launch_pdsch_encode_packed(b + 1, plan->d_enc[b] + plan->count[b], plan->count_pk[b], d_tbs, plan->d_tb_crc,
-                                 out, plan->ctx->d_shifts[b], plan->ctx->d_core[b], plan->ctx->d_crc_arena, s);
+                                 plan->inline_tb_crc ? plan->d_tb : nullptr, out, plan->ctx->d_shifts[b],
+                                 plan->ctx->d_core[b], plan->ctx->d_crc_arena, s);
       HIP_TRY(hipGetLastError());
     }
     if (plan->count[b] > 0) {

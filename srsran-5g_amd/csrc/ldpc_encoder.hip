@@ -423,6 +423,7 @@ template <int BG>
 __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const enc_desc* __restrict__ descs,
                                                                          const uint8_t* __restrict__ tbs,
                                                                          const uint32_t* __restrict__ tb_crcs,
+                                                                         const tb_crc_desc* __restrict__ tb_descs,
                                                                          uint32_t* __restrict__ out_words,
                                                                          const uint16_t* __restrict__ shift_table,
                                                                          const core_plan* __restrict__ core_plans,
@@ -452,8 +453,19 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
   }
   // ---- Message bytes (ldpc_segmenter_tx_impl.cpp:144): TB(+TB CRC) bytes, zero padding / CRC slot / fillers. ----
   const uint8_t* tb     = tbs + d.tb_byte_offset;
-  const uint32_t tb_crc = tb_crcs[d.tb_index];
-  const int      nd8    = d.nof_data / 8;
+  uint32_t       tb_crc = 0;
+  if (tb_descs == nullptr) {
+    tb_crc = tb_crcs[d.tb_index];  // from tb_crc_kernel
+  } else if (d.tb_bit_offset + d.nof_data > d.tb_bits) {
+    // Inline TB CRC (every TB of the plan has a contribution table): the workgroup of the codeblock that carries the
+    // TB CRC computes it, the others never need it: no separate tb_crc_kernel launch and dependency.
+    const tb_crc_desc t = tb_descs[d.tb_index];
+    crc_byte_lut(lut, static_cast<int>(t.order), t.poly);
+    const uint8_t* tbp = tbs + t.byte_offset;
+    tb_crc = block_crc_chunks<16>([tbp](int i) { return tbp[i]; }, static_cast<int>(t.nbytes), crc_tables + t.table,
+                                  static_cast<int>(t.order), t.poly, lut, red);
+  }
+  const int nd8 = d.nof_data / 8;
   for (int q = tid; q < nkb; q += PK_THREADS) {
     uint32_t byte = 0;
     if (q < nd8) {
@@ -548,6 +560,7 @@ void launch_pdsch_encode_packed(int              bg,
                                 int              nof_cbs,
                                 const uint8_t*   d_tbs,
                                 const uint32_t*  d_tb_crcs,
+                                const tb_crc_desc* d_tb_inline,
                                 uint32_t*        d_out_words,
                                 const uint16_t*  d_shifts,
                                 const core_plan* d_core_plans,
@@ -558,11 +571,11 @@ void launch_pdsch_encode_packed(int              bg,
     return;
   }
   if (bg == 1) {
-    pdsch_encode_packed_kernel<1><<<nof_cbs, PK_THREADS, 0, s>>>(d_desc, d_tbs, d_tb_crcs, d_out_words, d_shifts,
-                                                                  d_core_plans, d_crc_tables);
+    pdsch_encode_packed_kernel<1><<<nof_cbs, PK_THREADS, 0, s>>>(d_desc, d_tbs, d_tb_crcs, d_tb_inline, d_out_words,
+                                                                  d_shifts, d_core_plans, d_crc_tables);
   } else {
-    pdsch_encode_packed_kernel<2><<<nof_cbs, PK_THREADS, 0, s>>>(d_desc, d_tbs, d_tb_crcs, d_out_words, d_shifts,
-                                                                  d_core_plans, d_crc_tables);
+    pdsch_encode_packed_kernel<2><<<nof_cbs, PK_THREADS, 0, s>>>(d_desc, d_tbs, d_tb_crcs, d_tb_inline, d_out_words,
+                                                                  d_shifts, d_core_plans, d_crc_tables);
   }
 }
 

@@ -22,25 +22,37 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
 {
   __shared__ uint32_t table[256];
   __shared__ uint32_t part[256];
-  __shared__ int      all_ok;
-  const tb_dec_desc d = descs[blockIdx.x];
-  if (threadIdx.x == 0) {
-    int ok = 1;
-    for (uint32_t c = 0; c < d.nof_cbs; ++c) {
-      ok &= cb_crc_ok[d.first_cb + c] != 0;
-    }
-    all_ok = ok;
+  const tb_dec_desc d     = descs[blockIdx.x];
+  uint8_t*          tb    = tbs + d.tb_offset;
+  const uint8_t*    msgs  = cb_msgs + static_cast<size_t>(d.first_cb) * CB_MSG_STRIDE;
+  const uint32_t    bytes = d.tbs_bits / 8u;
+  // Codeblock CRC flags: loaded first, combined (workgroup AND) only after the speculative TB CRC below.
+  int ok = 1;
+  for (uint32_t c = threadIdx.x; c < d.nof_cbs; c += blockDim.x) {
+    ok &= cb_crc_ok[d.first_cb + c] != 0;
   }
-  __syncthreads();
-  if (!all_ok) {
+  // TS 38.214 TB sizes make the codeblock data byte-aligned when C > 1 ((TBS + 24) is a multiple of 8 C): then the TB
+  // CRC runs straight on the codeblock messages, before (and whatever) the flags say, so that its loads and table
+  // chain overlap the flag loads. A TB that does not pass its codeblock CRCs discards it.
+  const bool crc_from_msgs = d.nof_cbs > 1 && d.crc_table != NO_CRC_TABLE && (d.cb_data_bits & 7u) == 0;
+  uint32_t   crc           = 0;
+  if (crc_from_msgs) {
+    crc_byte_lut(table, 24, 0x1864cfbu);
+    const uint32_t cb_bytes = d.cb_data_bits / 8u;
+    const uint32_t magic    = d.data_magic;
+    crc = block_crc_chunks<16>(
+        [msgs, cb_bytes, magic](int i) {
+          const uint32_t cb = __umulhi(8u * static_cast<uint32_t>(i), magic);
+          return msgs[cb * CB_MSG_STRIDE + (static_cast<uint32_t>(i) - cb * cb_bytes)];
+        },
+        static_cast<int>(bytes), crc_tables + d.crc_table, 24, 0x1864cfbu, table, part);
+  }
+  if (!__syncthreads_and(ok)) {
     if (threadIdx.x == 0) {
       tb_crc_ok[d.tb_index] = 0;
     }
     return;
   }
-  uint8_t*       tb    = tbs + d.tb_offset;
-  const uint8_t* msgs  = cb_msgs + static_cast<size_t>(d.first_cb) * CB_MSG_STRIDE;
-  const uint32_t bytes = d.tbs_bits / 8u;
   if (d.nof_cbs == 1) {
     for (uint32_t b = threadIdx.x; b < bytes; b += blockDim.x) {
       tb[b] = msgs[b];
@@ -50,8 +62,7 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
     }
     return;
   }
-  // TB bit p comes from codeblock p / cb_data_bits, message bit p % cb_data_bits. TS 38.214 TB sizes make the
-  // codeblock data byte-aligned when C > 1 ((TBS + 24) is a multiple of 8 C): then every TB byte is one message byte.
+  // TB bit p comes from codeblock p / cb_data_bits, message bit p % cb_data_bits.
   if ((d.cb_data_bits & 7u) == 0) {
     const uint32_t cb_bytes = d.cb_data_bits / 8u;
     for (uint32_t b = threadIdx.x; b < bytes; b += blockDim.x) {
@@ -71,28 +82,15 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
     }
     tb[b] = static_cast<uint8_t>(byte);
   }
-  const bool crc_from_msgs = d.crc_table != NO_CRC_TABLE && (d.cb_data_bits & 7u) == 0;
   if (!crc_from_msgs) {
     __syncthreads();  // the CRC reads the TB back
-  }
-  uint32_t crc;
-  if (crc_from_msgs) {
-    // Straight from the codeblock messages: no dependency on the TB stores above.
-    crc_byte_lut(table, 24, 0x1864cfbu);
-    const uint32_t cb_bytes = d.cb_data_bits / 8u;
-    const uint32_t magic    = d.data_magic;
-    crc = block_crc_chunks<16>(
-        [msgs, cb_bytes, magic](int i) {
-          const uint32_t cb = __umulhi(8u * static_cast<uint32_t>(i), magic);
-          return msgs[cb * CB_MSG_STRIDE + (static_cast<uint32_t>(i) - cb * cb_bytes)];
-        },
-        static_cast<int>(bytes), crc_tables + d.crc_table, 24, 0x1864cfbu, table, part);
-  } else if (d.crc_table != NO_CRC_TABLE) {
-    crc_byte_lut(table, 24, 0x1864cfbu);
-    crc = block_crc_chunks<16>([tb](int i) { return tb[i]; }, static_cast<int>(bytes), crc_tables + d.crc_table, 24,
-                               0x1864cfbu, table, part);
-  } else {
-    crc = block_crc_bytes(tb, static_cast<int>(bytes), 24, 0x1864cfbu, table, part);
+    if (d.crc_table != NO_CRC_TABLE) {
+      crc_byte_lut(table, 24, 0x1864cfbu);
+      crc = block_crc_chunks<16>([tb](int i) { return tb[i]; }, static_cast<int>(bytes), crc_tables + d.crc_table,
+                                 24, 0x1864cfbu, table, part);
+    } else {
+      crc = block_crc_bytes(tb, static_cast<int>(bytes), 24, 0x1864cfbu, table, part);
+    }
   }
   // Checksum: the 24 bits that follow the last codeblock's TB bits (concatenate_codeblocks, :465).
   const uint32_t last_q = d.tbs_bits - (d.nof_cbs - 1u) * d.cb_data_bits;
@@ -102,14 +100,14 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
     const uint32_t q = last_q + static_cast<uint32_t>(k);
     chk              = (chk << 1) | ((static_cast<uint32_t>(lm[q >> 3]) >> (7u - (q & 7u))) & 1u);
   }
-  const bool ok = (crc == chk);
-  if (!ok) {
+  const bool crc_ok = (crc == chk);
+  if (!crc_ok) {
     for (uint32_t c = threadIdx.x; c < d.nof_cbs; c += blockDim.x) {
       cb_crc_ok[d.first_cb + c] = 0;
     }
   }
   if (threadIdx.x == 0) {
-    tb_crc_ok[d.tb_index] = ok ? 1 : 0;
+    tb_crc_ok[d.tb_index] = crc_ok ? 1 : 0;
   }
 }
 

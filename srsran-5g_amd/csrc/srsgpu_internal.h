@@ -108,12 +108,15 @@ void launch_pdsch_encode(int              bg,
                          const uint32_t*  d_crc_tables,
                          hipStream_t      s);
 
-/// Packed-bit encoder for codeblocks with Z % 32 == 0 and byte-aligned data (pdsch_encode_packed_kernel).
+/// Packed-bit encoder for codeblocks with Z % 32 == 0 and byte-aligned data (pdsch_encode_packed_kernel). With
+/// d_tb_inline (the plan's TB CRC descriptors, every one with a contribution table) the codeblock carrying a TB's CRC
+/// computes it inline and d_tb_crcs is not read; without it the TB CRCs come from tb_crc_kernel.
 void launch_pdsch_encode_packed(int              bg,
                                 const enc_desc*  d_desc,
                                 int              nof_cbs,
                                 const uint8_t*   d_tbs,
                                 const uint32_t*  d_tb_crcs,
+                                const tb_crc_desc* d_tb_inline,
                                 uint32_t*        d_out_words,
                                 const uint16_t*  d_shifts,
                                 const core_plan* d_core_plans,

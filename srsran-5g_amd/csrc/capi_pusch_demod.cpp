@@ -164,8 +164,8 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
     descs[t]          = d;
     nllr[t]           = d.nof_llrs;
     const uint32_t nwords = (d.nof_llrs + 31) / 32;
-    for (uint32_t w0 = 0; w0 < nwords; w0 += MOD_CHUNK_WORDS) {
-      const uint32_t b0 = w0 * 32, b1 = b0 + MOD_CHUNK_WORDS * 32;
+    for (uint32_t w0 = 0; w0 < nwords; w0 += DEMOD_CHUNK_WORDS) {
+      const uint32_t b0 = w0 * 32, b1 = b0 + DEMOD_CHUNK_WORDS * 32;
       mod_chunk      ch{t, w0, (b0 + Lq - 1) / Lq, std::min(nre, (b1 + Lq - 1) / Lq)};
       if (ch.re_end > ch.re_begin) {
         chunks.push_back(ch);

@@ -22,7 +22,7 @@ namespace srsgpu {
 namespace {
 
 constexpr int DEMOD_THREADS = 256;
-constexpr int DEMOD_OUT_BYTES = MOD_CHUNK_WORDS * 32 + 64;
+constexpr int DEMOD_OUT_BYTES = DEMOD_CHUNK_WORDS * 32 + 64;
 
 struct cpx {
   float x, y;
@@ -236,13 +236,13 @@ __device__ __forceinline__ void stage_chunk(const demod_uniform& u, uint32_t* se
   const demod_desc& d      = *u.d;
   const uint32_t    tid    = threadIdx.x;
   const uint32_t    nwords = (d.nof_llrs + 31u) >> 5;
-  for (uint32_t j = tid; j < MOD_CHUNK_WORDS; j += DEMOD_THREADS) {
+  for (uint32_t j = tid; j < DEMOD_CHUNK_WORDS; j += DEMOD_THREADS) {
     const uint32_t w = u.word0 + j;
     seq[j]           = (w < nwords) ? u.gseq[d.seq_word_offset + w] : 0u;
   }
   if (tid == 0) {
-    const uint32_t w2    = u.word0 + MOD_CHUNK_WORDS;
-    seq[MOD_CHUNK_WORDS] = (w2 < nwords) ? u.gseq[d.seq_word_offset + w2] : 0u;
+    const uint32_t w2      = u.word0 + DEMOD_CHUNK_WORDS;
+    seq[DEMOD_CHUNK_WORDS] = (w2 < nwords) ? u.gseq[d.seq_word_offset + w2] : 0u;
   }
   if (d.qm >= 6) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(u.tables);
@@ -315,9 +315,19 @@ __device__ __forceinline__ void demod_res(const demod_uniform& u,
   stage_chunk(u, seq, tab);
   __syncthreads();
   for (bool first = true; r < u.re_end; r += DEMOD_THREADS, first = false) {
+#if SRSGPU_DEMOD_PREFETCH
+    // The next RE's loads fly while this one is equalised and demapped.
+    (void)first;
+    uint32_t       nyw[4] = {}, nhw[L][4] = {};
+    const uint32_t rn     = r + DEMOD_THREADS;
+    if (rn < u.re_end) {
+      load_re<L>(d, rn, grids, ce, nyw, nhw);
+    }
+#else
     if (!first) {
       load_re<L>(d, r, grids, ce, yw, hw);
     }
+#endif
     cpx y[4], h[L][4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -419,6 +429,16 @@ __device__ __forceinline__ void demod_res(const demod_uniform& u,
         out8[ob + b] = static_cast<uint8_t>(pk[b / 4] >> (8 * (b % 4)));
       }
     }
+#if SRSGPU_DEMOD_PREFETCH
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      yw[p] = nyw[p];
+#pragma unroll
+      for (int ly = 0; ly < L; ++ly) {
+        hw[ly][p] = nhw[ly][p];
+      }
+    }
+#endif
   }
 }
 
@@ -449,7 +469,7 @@ __global__ __launch_bounds__(DEMOD_THREADS) DEMOD_OCCUPANCY void pusch_demodulat
                                                                          int8_t* __restrict__ llrs,
                                                                          const uint32_t* __restrict__ gseq)
 {
-  __shared__ uint32_t         seq[MOD_CHUNK_WORDS + 1];
+  __shared__ uint32_t         seq[DEMOD_CHUNK_WORDS + 1];
   __shared__ demap_pair_table tab[DEMAP_TABLES];
   __shared__ uint32_t         out32[DEMOD_OUT_BYTES / 4];
   const mod_chunk             ch     = chunks[blockIdx.x];

@@ -227,6 +227,15 @@ struct mod_chunk {
 
 /// Codeword words per modulator chunk and the largest codeword the Gold-sequence tables cover.
 constexpr uint32_t MOD_CHUNK_WORDS = 256;
+/// PUSCH demodulator chunk (codeword words per workgroup) and whether a lane prefetches its next RE's received values
+/// and estimates while it equalises the current one (pusch_demodulator.hip).
+#ifndef SRSGPU_DEMOD_CHUNK_WORDS
+#define SRSGPU_DEMOD_CHUNK_WORDS 256
+#endif
+#ifndef SRSGPU_DEMOD_PREFETCH
+#define SRSGPU_DEMOD_PREFETCH 0
+#endif
+constexpr uint32_t DEMOD_CHUNK_WORDS = SRSGPU_DEMOD_CHUNK_WORDS;
 constexpr uint32_t MOD_MAX_BITS    = 1u << 21;
 /// Gold sequence tables (TS 38.211 section 5.2.1): x1 bits x1(1600 + n) as LSB-first words; x2 chunk jumps
 /// M^(1600 + 2048 c) (c < MOD_MAX_BITS / 2048, 31 column words each); x2 lane jumps M^(32 i) (i < 64) as [column][i].

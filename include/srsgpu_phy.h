@@ -374,21 +374,34 @@ void srsgpu_ofdm_plan_destroy(srsgpu_ofdm_plan* plan);
  * const resource_grid_reader& grid, const configuration& config)
  * (include/srsran/phy/upper/signal_processors/dmrs_pusch_estimator.h, lib/phy/upper/signal_processors/
  * dmrs_pusch_estimator_impl.cpp:28, port_channel_estimator_average_impl.cpp:77) for every PUSCH transmission of a
- * batch of slots, pseudo-random DM-RS sequence, "average" time-domain strategy (the default) and the none / mean /
- * filter (default) frequency-domain smoothing. Outputs per transmission and rx port: the channel estimate of every RE
- * of the allocation in the layout the demodulator reads, the noise variance (d_noise_var[4 * tx + port]) and, when
- * d_metrics is not NULL, (RSRP, EPRE, noise variance, SNR) at d_metrics[4 * (4 * tx + port)]. Time alignment and CFO
- * are not estimated. One layer is the reference's scope (port_channel_estimator_average_impl.cpp:83 asserts it); 2..4
- * layers (ports 1000..1003) are an extension: the w_f cover code is removed over adjacent pilot pairs.
+ * batch of slots, pseudo-random DM-RS sequence, the "average" (default) and "interpolate" time-domain strategies
+ * (port_channel_estimator_td_interpolation_strategy), the none / mean / filter (default) frequency-domain smoothing,
+ * and the estimator's CFO estimation with optional compensation (compensate_cfo, du_low's default:
+ * du_low_config.h:69; port_channel_estimator_average_impl.cpp:128, :322, :475). Outputs per transmission and rx port:
+ * the channel estimate of every RE of the allocation in the layout the demodulator reads, the noise variance
+ * (d_noise_var[4 * tx + port]) and, when d_metrics is not NULL, SRSGPU_CHEST_METRICS floats at
+ * d_metrics[SRSGPU_CHEST_METRICS * (4 * tx + port)]: RSRP, EPRE, noise variance, SNR, time alignment (seconds,
+ * channel_estimate::get_time_alignment, DFT estimator time_alignment_estimator_dft_impl.cpp:178), CFO (Hz, NaN with one
+ * DM-RS symbol: channel_estimate::get_cfo_Hz), 0, 0. One layer is the reference's scope
+ * (port_channel_estimator_average_impl.cpp:83 asserts it); 2..4 layers (ports 1000..1003) are an extension: the w_f
+ * cover code is removed over adjacent pilot pairs. Frequency hopping: the reference's PUSCH estimator never sets
+ * hopping_symbol_index / rb_mask2 (dmrs_pusch_estimator_impl.cpp:107-172; only the PUCCH estimators do), so the PUSCH
+ * path has no hopping to replace.
  * ------------------------------------------------------------------------------------------------------------------ */
 #define SRSGPU_CHEST_FD_NONE 0
 #define SRSGPU_CHEST_FD_MEAN 1
 #define SRSGPU_CHEST_FD_FILTER 2
+#define SRSGPU_CHEST_TD_AVERAGE 0
+#define SRSGPU_CHEST_TD_INTERPOLATE 1
+#define SRSGPU_CHEST_METRICS 8
 
 /* Channel-estimate layouts (estimate_layout of the estimator and demodulator configurations). PER_SYMBOL is the
  * reference's channel_estimate: every allocated symbol holds its estimate. COMPACT stores, with the "average" time
  * strategy (one estimate for all the symbols of the allocation), only the row of start_symbol, and the demodulator
- * reads that row for every symbol: identical LLRs with 1/nof_symbols of the estimate traffic. */
+ * reads that row for every symbol: identical LLRs with 1/nof_symbols of the estimate traffic. With CFO compensation
+ * (compensate_cfo and >= 2 DM-RS symbols) the row holds the unrotated estimate and the first allocated element of the
+ * next row the normalised CFO (float32 bits); the demodulator (cfo_compensated = 1) applies each symbol's rotation
+ * in bf16 exactly as the estimator would have written it. The "interpolate" strategy needs PER_SYMBOL. */
 #define SRSGPU_CE_PER_SYMBOL 0
 #define SRSGPU_CE_COMPACT 1
 
@@ -406,9 +419,12 @@ typedef struct {
   uint16_t slot_index;       /* n_slot within the frame (DM-RS c_init) */
   uint8_t  fd_smoothing;     /* SRSGPU_CHEST_FD_* */
   uint8_t  estimate_layout;  /* SRSGPU_CE_PER_SYMBOL or SRSGPU_CE_COMPACT */
-  uint8_t  pad[2];
+  uint8_t  td_strategy;      /* SRSGPU_CHEST_TD_AVERAGE or SRSGPU_CHEST_TD_INTERPOLATE */
+  uint8_t  compensate_cfo;   /* 1: compensate the estimated CFO (needs >= 2 DM-RS symbols to act) */
   float    scaling;          /* beta_PUSCH^DMRS (DM-RS amplitude relative to data), > 0 */
   uint32_t grid_index;       /* slot of the rx grid and of the estimate buffer */
+  uint8_t  numerology;       /* subcarrier spacing 15 kHz x 2^numerology (0..4), normal cyclic prefix */
+  uint8_t  pad[3];
 } srsgpu_pusch_chest_config;
 
 typedef struct srsgpu_pusch_chest_plan srsgpu_pusch_chest_plan;
@@ -421,7 +437,8 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
                                    srsgpu_pusch_chest_plan**        plan);
 
 /** Estimates every planned transmission: reads d_grids, writes d_ch_estimates (slot layout [layer 0..3][port]
- *  [symbol][subcarrier], only the allocated REs), d_noise_var and optionally d_metrics. Asynchronous on `stream`. */
+ *  [symbol][subcarrier], only the allocated REs), d_noise_var and optionally d_metrics (SRSGPU_CHEST_METRICS floats
+ *  per transmission and port). Asynchronous on `stream`. */
 int srsgpu_pusch_chest_plan_execute(const srsgpu_pusch_chest_plan* plan,
                                     const uint32_t*                d_grids,
                                     uint32_t*                      d_ch_estimates,
@@ -449,9 +466,11 @@ typedef struct {
   uint16_t rb_start;                    /* contiguous CRB allocation [rb_start, rb_start + nof_rb) (rb_mask) */
   uint16_t nof_rb;
   uint8_t  estimate_layout;             /* SRSGPU_CE_PER_SYMBOL or SRSGPU_CE_COMPACT (as the estimator wrote it) */
-  uint8_t  pad;
+  uint8_t  cfo_compensated;             /* COMPACT only: the estimator compensated the CFO (its compensate_cfo) */
   uint32_t grid_index;                  /* slot (rx grid and channel estimate) of the transmission */
   uint32_t llr_offset;                  /* first codeword LLR in the output buffer */
+  uint8_t  numerology;                  /* COMPACT + cfo_compensated: subcarrier spacing of the symbol epochs */
+  uint8_t  pad2[3];
 } srsgpu_pusch_demod_config;
 
 typedef struct srsgpu_pusch_demodulator_plan srsgpu_pusch_demodulator_plan;

@@ -115,11 +115,118 @@ def interpolate(pilots, offset, stride, nof_re):
     return out
 
 
-def estimate(cfg, grid, fd="filter"):
+def symbol_start_epochs(numerology):
+    """initialize_symbol_start_epochs (port_channel_estimator_average_impl.cpp:496): cumulative CP durations in units of
+    the symbol duration plus the symbol index, normal CP; the +16 kappa CP of cyclic_prefix::get_length
+    (cyclic_prefix.h:93) applies to symbols 0 and 7 * 2^mu of the slot."""
+    t_c = 1.0 / (480000 * 4096)
+    scs_hz = (15 << numerology) * 1000
+    ep = np.zeros(14)
+    for i in range(14):
+        kappa = (144 >> numerology) + (16 if i in (0, 7 << numerology) else 0)
+        d = kappa * 64 * t_c * scs_hz
+        ep[i] = d if i == 0 else ep[i - 1] + d + 1.0
+    return ep
+
+
+TA_MAX_NOF_RE = 275 * 12   # time_alignment_estimator_dft_impl.h:41 (MAX_NOF_PRBS * NRE)
+TA_MAX_DFT = 4096          # pow2(log2_ceil(3300))
+TA_MIN_DFT = 128           # 1 / (15 kHz x one 15 kHz TA step), time_alignment_estimator_dft_impl.cpp:96
+
+
+def ta_dft_size(nof_re):
+    """get_idft (time_alignment_estimator_dft_impl.cpp:216): guard-scaled, next power of two, at least 128."""
+    n = nof_re * TA_MAX_DFT // TA_MAX_NOF_RE
+    size = 1 << max(0, int(np.ceil(np.log2(max(n, 1)))))
+    return max(TA_MIN_DFT, size)
+
+
+def ta_max_samples(numerology, dft_size, stride):
+    """Half the normal CP (144 kappa / 2^(mu + 1)) in samples at dft_size x SCS x stride (estimate_ta_correlation,
+    time_alignment_estimator_dft_impl.cpp:236)."""
+    t_c = 1.0 / (480000 * 4096)
+    half_cp = (144 * 64 // (1 << (numerology + 1))) * t_c
+    fs = dft_size * (15 << numerology) * 1000.0 * stride
+    return int(np.floor(half_cp * fs)), fs
+
+
+def fractional_sample_delay(c):
+    """time_alignment_estimator_dft_impl.cpp:51: quadratic fit over 3 or 5 correlation samples around the peak."""
+    if c.size == 5:
+        num = np.dot([-0.4, -0.2, 0.0, 0.2, 0.4], c)
+        den = np.dot([0.571429, -0.285714, -0.571429, -0.285714, 0.571429], c)
+        corr = 1.0
+    else:
+        num = np.dot([-0.5, 0.0, 0.5], c)
+        den = np.dot([0.5, -1.0, 0.5], c)
+        corr = 0.5
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = -corr * num / den
+    if not np.isfinite(r) or abs(r) > 1.0:
+        return 0.0
+    return float(r)
+
+
+def estimate_ta(planes, positions, numerology, stride):
+    """time_alignment_estimator_dft_impl::estimate of the smoothed LSE planes (port_channel_estimator_helpers.cpp:246):
+    type 1 (stride-2 pattern) copies the pilots to the first bins; otherwise the pilots go to their subcarrier offset
+    from the lowest one (mask path, stride 1). Inverse DFT, |.|^2 summed over planes, peak within +-half CP, fractional
+    refinement unless the DFT is the largest one. Returns seconds, rounded to Tc like phy_time_unit::from_seconds."""
+    span = positions[-1] - positions[0] + 1 if stride == 1 else len(positions)
+    M = ta_dft_size(span)
+    corr = np.zeros(M)
+    for f in planes:
+        x = np.zeros(M, np.complex128)
+        if stride == 1:
+            x[positions - positions[0]] = f
+        else:
+            x[: f.size] = f
+        corr += np.abs(np.fft.ifft(x) * M) ** 2
+    m, fs = ta_max_samples(numerology, M, stride)
+    d_i = int(np.argmax(corr[:m]))
+    a_i = int(np.argmax(corr[M - m:]))
+    idx = d_i if corr[d_i] >= corr[M - m + a_i] else -(m - a_i)
+    frac = 0.0
+    if M != TA_MAX_DFT:
+        n = 5 if m > 2 else 3
+        frac = fractional_sample_delay(np.array([corr[(idx + i - n // 2) % M] for i in range(n)]))
+    ta = np.float32((idx + frac) / fs)
+    t_c = 1.0 / (480000 * 4096)
+    tc10 = int(float(ta) / t_c * 10.0)  # from_seconds: truncate x10, round half away
+    tc = int(tc10 / 10) + int(np.fmod(tc10, 10) / 5)
+    return tc * t_c
+
+
+def td_interpolate(planes, dmrs_syms, first, last, l):
+    """apply_td_domain_strategy, "interpolate" (port_channel_estimator_average_impl.cpp:509): linear in time between
+    the DM-RS symbols around l, extrapolated from the first / last two."""
+    before = max([d for d in dmrs_syms if first <= d < l], default=-1)
+    after = min([d for d in dmrs_syms if l <= d < last], default=-1)
+    if before == -1:
+        second = min([d for d in dmrs_syms if after + 1 <= d < last], default=-1)
+        if second == -1:
+            return planes[0]
+        before, after = after, second
+    if after == -1:
+        second_last = max([d for d in dmrs_syms if first <= d < before], default=-1)
+        if second_last == -1:
+            return planes[-1]
+        before, after = second_last, before
+    w = (l - before) / (after - before)
+    i = sum(1 for d in dmrs_syms if first <= d < before)
+    return planes[i] + (planes[i + 1] - planes[i]) * w
+
+
+def estimate(cfg, grid, fd="filter", td="average", compensate_cfo=False, numerology=1):
     """cfg: slot, scrambling_id, n_scid, dmrs_type2, scaling (beta), dmrs_symbol_mask, start_symbol, nof_symbols,
     rb_start, nof_rb, nof_rx_ports. grid (P, 14, nsc) complex. Returns (ch (P, 14, nsc) complex128 filled on the
-    allocation, noise_var (P,), rsrp (P,), epre (P,), CFO phase between the first two DM-RS symbols (P,) or None when
-    there is one DM-RS symbol)."""
+    allocation, noise_var (P,), rsrp (P,), epre (P,), extra) with extra = dict(cfo_hz (P,) NaN when one DM-RS symbol,
+    ta_s (P,), cfo_phase (P,) arg between the first two DM-RS symbols or None).
+
+    CFO (preprocess_pilots_and_estimate_cfo, port_channel_estimator_average_impl.cpp:322): phase of
+    sum lse_1 conj(lse_0) over the time between the first two DM-RS symbols' starts; with compensate_cfo every DM-RS
+    symbol's LSE is derotated by its start epoch before combining, the noise residual re-rotates the prediction (:475)
+    and every symbol's estimate is rotated by its epoch (:128)."""
     P = cfg["nof_rx_ports"]
     t2 = cfg["dmrs_type2"]
     beta = cfg["scaling"]
@@ -127,26 +234,45 @@ def estimate(cfg, grid, fd="filter"):
     offset, stride = pat[0], pat[1] - pat[0]
     rb0, nrb = cfg["rb_start"], cfg["nof_rb"]
     sc = np.array([(rb0 + rb) * 12 + k for rb in range(nrb) for k in pat])
-    syms = [l for l in range(cfg["start_symbol"], cfg["start_symbol"] + cfg["nof_symbols"])
-            if (cfg["dmrs_symbol_mask"] >> l) & 1]
+    first, last = cfg["start_symbol"], cfg["start_symbol"] + cfg["nof_symbols"]
+    syms = [l for l in range(first, last) if (cfg["dmrs_symbol_mask"] >> l) & 1]
     Dn = len(syms)
     N = sc.size
     pil = [dmrs_sequence(cfg["slot"], l, cfg["scrambling_id"], cfg["n_scid"], t2, rb0, nrb) for l in syms]
+    ep = symbol_start_epochs(numerology)
+    scs_hz = (15 << numerology) * 1000.0
     nsc = grid.shape[2]
     ch = np.zeros((P, 14, nsc), np.complex128)
-    nvar, rsrp, epre, cfo = np.zeros(P), np.zeros(P), np.zeros(P), [None] * P
+    nvar, rsrp, epre = np.zeros(P), np.zeros(P), np.zeros(P)
+    cfo_hz, ta_s, cfo_ph = np.full(P, np.nan), np.zeros(P), [None] * P
     for p in range(P):
         rx = [grid[p, l, sc].astype(np.complex128) for l in syms]
         lse = [r * np.conj(q) for r, q in zip(rx, pil)]
-        if Dn > 1:  # CFO phase between the first two DM-RS symbols: arg(sum lse_1 conj(lse_0)) (:350)
-            cfo[p] = float(np.angle(np.dot(np.conj(lse[0]), lse[1])))
-        f = sum(lse) / (beta * Dn)
-        f = fd_smoothing(f, nrb, stride, fd)
+        cfo = None
+        if Dn > 1:  # :350-361
+            cfo_ph[p] = float(np.angle(np.dot(np.conj(lse[0]), lse[1])))
+            cfo = cfo_ph[p] / (2 * np.pi) / (ep[syms[1]] - ep[syms[0]])
+            cfo_hz[p] = cfo * scs_hz
+            if compensate_cfo:
+                lse = [y * np.exp(-2j * np.pi * ep[l] * cfo) for y, l in zip(lse, syms)]
+        planes = [sum(lse) / (beta * Dn)] if td == "average" else [y / beta for y in lse]
+        planes = [fd_smoothing(f, nrb, stride, fd) for f in planes]
+        Q = len(planes)
         epre[p] = sum(np.sum(np.abs(r) ** 2) for r in rx) / (N * Dn)
-        rsrp[p] = np.sum(np.abs(f) ** 2) * beta * beta * Dn / (N * Dn)
-        noise = sum(np.sum(np.abs(r - f * beta * q) ** 2) for r, q in zip(rx, pil))
+        rsrp[p] = sum(np.sum(np.abs(f) ** 2) for f in planes) * beta * beta * Dn / Q / (N * Dn)
+        h = sum(planes) * beta / Q
+        noise = 0.0
+        for r, q, l in zip(rx, pil, syms):
+            pred = h * q
+            if compensate_cfo and cfo is not None:
+                pred = pred * np.exp(2j * np.pi * ep[l] * cfo)
+            noise += np.sum(np.abs(r - pred) ** 2)
         nvar[p] = max(rsrp[p] / 1e10, noise / (N * Dn - 1))
-        fr = interpolate(f, offset, stride, nrb * 12)
-        for l in range(cfg["start_symbol"], cfg["start_symbol"] + cfg["nof_symbols"]):
+        ta_s[p] = estimate_ta(planes, sc, numerology, stride)
+        frs = [interpolate(f, offset, stride, nrb * 12) for f in planes]
+        for l in range(first, last):
+            fr = frs[0] if td == "average" else td_interpolate(frs, syms, first, last, l)
+            if compensate_cfo and cfo is not None:
+                fr = fr * np.exp(2j * np.pi * ep[l] * cfo)
             ch[p, l, rb0 * 12: (rb0 + nrb) * 12] = fr
-    return ch, nvar, rsrp, epre, cfo
+    return ch, nvar, rsrp, epre, dict(cfo_hz=cfo_hz, ta_s=ta_s, cfo_phase=cfo_ph)

@@ -153,3 +153,22 @@ struct stage_timer {
   }
 };
 
+
+namespace srsgpu {
+
+constexpr double T_C = 1.0 / (480000.0 * 4096.0);  // phy_time_unit::T_C
+
+/// initialize_symbol_start_epochs (port_channel_estimator_average_impl.cpp:496), normal CP, with the reference's
+/// float / double mix: each CP duration in seconds (double) times the SCS, accumulated into float. The +16 kappa CP
+/// (cyclic_prefix::get_length, cyclic_prefix.h:93) applies to symbols 0 and 7 * 2^mu of the slot.
+inline void symbol_start_epochs(unsigned mu, float* ep)
+{
+  const double khz = 15u << mu;
+  for (unsigned i = 0; i < 14; ++i) {
+    const unsigned kappa = (144u >> mu) + ((i == 0 || i == (7u << mu)) ? 16u : 0u);
+    const double   cp_s  = static_cast<double>(kappa * 64u) * T_C;
+    ep[i] = (i == 0) ? static_cast<float>(cp_s * khz * 1000) : static_cast<float>(ep[i - 1] + cp_s * khz * 1000 + 1.0F);
+  }
+}
+
+} // namespace srsgpu

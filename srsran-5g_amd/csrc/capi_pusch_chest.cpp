@@ -9,15 +9,13 @@
 
 using namespace srsgpu;
 
-static_assert(sizeof(srsgpu_pusch_chest_config) == 28, "srsgpu_pusch_chest_config layout (mirrored by srsgpu)");
+static_assert(sizeof(srsgpu_pusch_chest_config) == 32, "srsgpu_pusch_chest_config layout (mirrored by srsgpu)");
 
 struct srsgpu_pusch_chest_plan {
   srsgpu_context* ctx        = nullptr;
   chest_job*      d_jobs     = nullptr;
   int             nof_jobs   = 0;
-  int             max_pilots = 0;  ///< Largest job: pilots per DM-RS symbol.
-  int             max_dmrs   = 0;  ///< Largest job: DM-RS symbols.
-  int             max_words  = 0;  ///< Largest job: staged sequence words per DM-RS symbol.
+  chest_geom      geom       = {};  ///< Plan-wide maxima (LDS sizing).
   uint32_t*       d_seq      = nullptr;  ///< DM-RS sequence words of every job (plan lifetime).
 };
 
@@ -36,6 +34,17 @@ double rc_tap(int n)
   }
   const double sinc = (t == 0) ? 1.0 : std::sin(pi * t) / (pi * t);
   return sinc * std::cos(pi * beta * t) / (1 - (2 * beta * t) * (2 * beta * t));
+}
+
+/// time_alignment_estimator_dft_impl::get_idft (:216): guard-scaled size, next power of two, 128..4096.
+unsigned ta_dft_size(unsigned nof_re)
+{
+  const unsigned n    = nof_re * 4096u / 3300u;
+  unsigned       size = 1;
+  while (size < n) {
+    size <<= 1;
+  }
+  return std::max(128u, size);
 }
 
 } // namespace
@@ -66,8 +75,12 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
     }
     if (c.nof_symbols < 1 || c.start_symbol + c.nof_symbols > 14 || c.nof_rb < 1 ||
         c.rb_start + c.nof_rb > grid_nof_prb || !(c.scaling > 0.f) || c.fd_smoothing > SRSGPU_CHEST_FD_FILTER ||
-        c.estimate_layout > SRSGPU_CE_COMPACT) {
-      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid allocation, scaling or smoothing strategy", t);
+        c.estimate_layout > SRSGPU_CE_COMPACT || c.td_strategy > SRSGPU_CHEST_TD_INTERPOLATE ||
+        c.compensate_cfo > 1 || c.numerology > 4) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid allocation, scaling, strategy or numerology", t);
+    }
+    if (c.estimate_layout == SRSGPU_CE_COMPACT && c.td_strategy == SRSGPU_CHEST_TD_INTERPOLATE) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: the interpolate strategy needs the per-symbol layout", t);
     }
     std::vector<unsigned> dmrs;
     for (unsigned l = 0; l < 14; ++l) {
@@ -107,6 +120,62 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
       nof_v = per_rb;
     }
     const unsigned ngroups = (L + 1) / 2;
+    // Symbol epochs and the "interpolate" plane table (apply_td_domain_strategy, :509): for symbol l the planes of the
+    // DM-RS symbols around it (or the first / last two), and the weight of the second.
+    float          epochs[14];
+    symbol_start_epochs(c.numerology, epochs);
+    int8_t         q0[14] = {}, q1[14] = {};
+    float          wq[14] = {};
+    const int      s_first = c.start_symbol, s_last = c.start_symbol + c.nof_symbols;
+    auto           dm    = [&](int l) { return l >= 0 && l < 14 && ((c.dmrs_symbol_mask >> l) & 1u); };
+    auto           count = [&](int a, int b) { int n = 0; for (int l = a; l < b; ++l) n += dm(l); return n; };
+    for (int l = s_first; l < s_last; ++l) {
+      int before = -1, after = -1;
+      for (int x = s_first; x < l; ++x) if (dm(x)) before = x;
+      for (int x = s_last - 1; x >= l; --x) if (dm(x)) after = x;
+      bool copied = false;
+      if (before == -1) {
+        int second = -1;
+        for (int x = s_last - 1; x >= after + 1; --x) if (dm(x)) second = x;
+        if (second == -1) {
+          q0[l] = q1[l] = 0;
+          copied = true;
+        } else {
+          before = after;
+          after  = second;
+        }
+      }
+      if (!copied && after == -1) {
+        int second_last = -1;
+        for (int x = s_first; x < before; ++x) if (dm(x)) second_last = x;
+        if (second_last == -1) {
+          q0[l] = q1[l] = static_cast<int8_t>(dmrs.size() - 1);
+          copied = true;
+        } else {
+          after  = before;
+          before = second_last;
+        }
+      }
+      if (!copied) {
+        const int i = count(s_first, before);
+        q0[l]       = static_cast<int8_t>(i);
+        q1[l]       = static_cast<int8_t>(i + 1);
+        wq[l]       = static_cast<float>(l - before) / static_cast<float>(after - before);
+      }
+    }
+    // Time alignment (estimate_time_alignment, port_channel_estimator_helpers.cpp:246): type 1 patterns are the stride-2
+    // PUSCH patterns (pilots in the first bins); others take the RE-mask path (pilots at their subcarrier offsets).
+    const unsigned khz      = 15u << c.numerology;
+    const unsigned ta_re    = t2 ? (c.nof_rb - 1u) * 12u + 7u + 1u : c.nof_rb * per_rb;
+    const unsigned ta_dft   = ta_dft_size(ta_re);
+    const unsigned ta_strd  = t2 ? 1u : 2u;
+    const double   ta_fs    = static_cast<double>(static_cast<uint64_t>(ta_dft) * khz * 1000u * ta_strd);
+    const double   half_cp  = static_cast<double>(144u * 64u / (1u << (c.numerology + 1))) * T_C;
+    const unsigned ta_max   = static_cast<unsigned>(std::floor(half_cp * ta_fs));
+    unsigned       ta_log2  = 0;
+    while ((1u << ta_log2) < ta_dft) {
+      ++ta_log2;
+    }
     for (unsigned p = 0; p < P; ++p) {
       for (unsigned g = 0; g < ngroups; ++g) {
         chest_job jb{};
@@ -143,7 +212,21 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
         jb.interp_offset = static_cast<uint8_t>(t2 ? 2 * g : g);
         jb.interp_stride = static_cast<uint8_t>(stride);
         jb.first_symbol  = c.start_symbol;
-        jb.nof_symbols   = c.estimate_layout == SRSGPU_CE_COMPACT ? 1 : c.nof_symbols;  // compact: start_symbol's row
+        jb.nof_symbols   = c.nof_symbols;
+        jb.nof_out_symbols = c.estimate_layout == SRSGPU_CE_COMPACT ? 1 : c.nof_symbols;  // compact: start_symbol's row
+        jb.td_interp       = c.td_strategy == SRSGPU_CHEST_TD_INTERPOLATE;
+        jb.compensate_cfo  = c.compensate_cfo;
+        jb.compact_cfo     = c.estimate_layout == SRSGPU_CE_COMPACT && c.compensate_cfo && dmrs.size() >= 2;
+        std::copy(epochs, epochs + 14, jb.epochs);
+        std::copy(q0, q0 + 14, jb.td_q0);
+        std::copy(q1, q1 + 14, jb.td_q1);
+        std::copy(wq, wq + 14, jb.td_w);
+        jb.scs_hz       = static_cast<float>(khz * 1000u);
+        jb.ta_fs        = ta_fs;
+        jb.ta_dft       = static_cast<uint16_t>(ta_dft);
+        jb.ta_max       = static_cast<uint16_t>(ta_max);
+        jb.ta_log2      = static_cast<uint8_t>(ta_log2);
+        jb.ta_positions = t2 ? 1 : 0;
         jobs.push_back(jb);
       }
     }
@@ -157,12 +240,17 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
   auto* plan     = new srsgpu_pusch_chest_plan();
   plan->ctx      = ctx;
   plan->nof_jobs = static_cast<int>(jobs.size());
+  chest_geom& g = plan->geom;
+  g             = {1, 1, 1, 1, 1, 128};
   for (const chest_job& jb : jobs) {
-    plan->max_pilots = std::max<int>(plan->max_pilots, jb.nof_pilots);
-    plan->max_dmrs   = std::max<int>(plan->max_dmrs, jb.nof_dmrs);
-    plan->max_words  = std::max<int>(plan->max_words, static_cast<int>(((2 * jb.seq_offset) % 32 + 2 * jb.nof_pilots + 31) / 32));
+    g.max_pilots = std::max<int>(g.max_pilots, jb.nof_pilots);
+    g.max_dmrs   = std::max<int>(g.max_dmrs, jb.nof_dmrs);
+    g.max_words  = std::max<int>(g.max_words, static_cast<int>(((2 * jb.seq_offset) % 32 + 2 * jb.nof_pilots + 31) / 32));
+    g.max_planes = std::max<int>(g.max_planes, jb.td_interp ? jb.nof_dmrs : 1);
+    g.max_gl     = std::max<int>(g.max_gl, jb.group_layers);
+    g.max_dft    = std::max<int>(g.max_dft, jb.ta_dft);
   }
-  if (pusch_chest_lds_bytes(plan->max_pilots, plan->max_dmrs, plan->max_words) > 160 * 1024) {
+  if (pusch_chest_lds_bytes(g) > 160 * 1024) {
     delete plan;
     return fail(SRSGPU_ERR_INVALID_ARG, "channel estimation job too large for the LDS");
   }
@@ -206,8 +294,8 @@ int srsgpu_pusch_chest_plan_execute(const srsgpu_pusch_chest_plan* plan,
   if (plan == nullptr || d_grids == nullptr || d_ch_estimates == nullptr || d_noise_var == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  launch_pusch_chest(plan->d_jobs, plan->nof_jobs, plan->max_pilots, plan->max_dmrs, plan->max_words, d_grids,
-                     d_ch_estimates, d_noise_var, d_metrics, plan->d_seq, static_cast<hipStream_t>(stream));
+  launch_pusch_chest(plan->d_jobs, plan->nof_jobs, plan->geom, d_grids, d_ch_estimates, d_noise_var, d_metrics,
+                     plan->d_seq, static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
 }

@@ -8,7 +8,7 @@
 
 using namespace srsgpu;
 
-static_assert(sizeof(srsgpu_pusch_demod_config) == 28, "srsgpu_pusch_demod_config layout (mirrored by srsgpu)");
+static_assert(sizeof(srsgpu_pusch_demod_config) == 32, "srsgpu_pusch_demod_config layout (mirrored by srsgpu)");
 
 struct srsgpu_pusch_demodulator_plan {
   srsgpu_context*       ctx        = nullptr;
@@ -114,7 +114,8 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
     }
     if (c.nof_symbols < 1 || c.start_symbol + c.nof_symbols > 14 || (c.dmrs_type != 1 && c.dmrs_type != 2) ||
         c.nof_cdm_groups_without_data < 1 || c.nof_cdm_groups_without_data > (c.dmrs_type == 1 ? 2 : 3) ||
-        c.n_id > 1023 || c.nof_rb < 1 || c.rb_start + c.nof_rb > grid_nof_prb || c.estimate_layout > SRSGPU_CE_COMPACT) {
+        c.n_id > 1023 || c.nof_rb < 1 || c.rb_start + c.nof_rb > grid_nof_prb || c.estimate_layout > SRSGPU_CE_COMPACT ||
+        c.cfo_compensated > 1 || c.numerology > 4) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid time / frequency allocation or DM-RS configuration", t);
     }
     demod_desc d{};
@@ -151,6 +152,9 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
     if (d.ce_compact) {
       d.ce_base += c.start_symbol * nsc;  // the estimator's single row (srsgpu_pusch_chest_config::estimate_layout)
     }
+    // Compact + CFO compensation (>= 2 DM-RS symbols: the estimator has a CFO): per-symbol rotation in the kernel.
+    d.ce_cfo = (d.ce_compact && c.cfo_compensated && __builtin_popcount(c.dmrs_symbol_mask) >= 2) ? 1u : 0u;
+    symbol_start_epochs(c.numerology, d.epochs);
     d.llr_offset      = c.llr_offset;
     d.nof_llrs        = nre * Lq;
     d.c_init          = (static_cast<uint32_t>(c.rnti) << 15) + c.n_id;  // pusch_demodulator_impl.cpp:279

@@ -65,14 +65,6 @@ __device__ __forceinline__ float half_sum(float v)
   return v;
 }
 
-/// Layout of the dynamic LDS of a job (sizes from the plan's largest job).
-struct chest_lds {
-  cpx*      E;     ///< [2][N + 2 CHEST_VP] enlarged LSE per layer of the group (zero outside the filled span)
-  cpx*      F;     ///< [2][N] smoothed pilots
-  uint32_t* seq;   ///< [D][W] DM-RS sequence words (MSB first) per DM-RS symbol
-  float*    taps;  ///< [32]
-};
-
 /// DM-RS QPSK symbol i of DM-RS symbol s from the staged sequence words (amplitude 1/sqrt(2)).
 __device__ __forceinline__ cpx pilot(const uint32_t* seq, int W, int s, uint32_t n0, int i)
 {
@@ -127,146 +119,243 @@ __device__ __forceinline__ void virtual_pilots(cpx* E, int N, int nv)
   }
 }
 
-__global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void pusch_chest_kernel(const chest_job* __restrict__ jobs,
-                                                                    int max_pilots,
-                                                                    int max_dmrs,
-                                                                    int max_words,
-                                                                    const uint32_t* __restrict__ grids,
-                                                                    uint32_t* __restrict__ ce,
-                                                                    float* __restrict__ noise_var,
-                                                                    float* __restrict__ metrics,
-                                                                    const uint32_t* __restrict__ gseq)
+constexpr float CHEST_TWOPI = 6.283185307f;  // TWOPI (srsran/support/math_utils.h)
+
+__device__ __forceinline__ cpx cmul(cpx a, cpx b)
+{
+  return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+
+/// std::polar(1.0F, theta) in float.
+__device__ __forceinline__ cpx polar1(float theta)
+{
+  float sn, cs;
+  sincosf(theta, &sn, &cs);
+  return {cs, sn};
+}
+
+/// Pilot subcarrier of pilot i relative to the first allocated subcarrier.
+__device__ __forceinline__ uint32_t pilot_subcarrier(const chest_job& jb, int i)
+{
+  const int rb = i / jb.pilots_per_rb;
+  return static_cast<uint32_t>(rb * 12 + ((jb.pattern >> (4 * (i - rb * jb.pilots_per_rb))) & 15u));
+}
+
+/// Maximum over the wavefront with the lowest index among equal values (srsvec::max_element keeps the first maximum).
+__device__ __forceinline__ void wave_argmax(float& v, int& idx)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o);
+    const int   oi = __shfl_xor(idx, o);
+    if (ov > v || (ov == v && oi < idx)) {
+      v   = ov;
+      idx = oi;
+    }
+  }
+}
+
+/// LDS of a job, carved from the plan-sized dynamic allocation (chest_geom): the staged sequence words, the filter
+/// taps, the smoothed planes F and one region shared by the LSE stage (Y per DM-RS symbol + enlarged E per layer) and
+/// the time-alignment stage (the DFT buffer X + the correlation), which run one after the other.
+struct chest_lds {
+  uint32_t* seq;   ///< [max_dmrs][max_words]
+  float*    taps;  ///< [32]
+  cpx*      F;     ///< [max_planes][max_gl][max_pilots]
+  cpx*      Y;     ///< [max_dmrs][max_pilots]
+  cpx*      E;     ///< [max_gl][max_pilots + 2 CHEST_VP]
+  cpx*      X;     ///< [max_dft] (aliases Y / E)
+  float*    corr;  ///< [max_dft]
+};
+
+__device__ __host__ inline size_t chest_region_bytes(const chest_geom& g)
+{
+  const size_t lse = (static_cast<size_t>(g.max_dmrs) * g.max_pilots +
+                      static_cast<size_t>(g.max_gl) * (g.max_pilots + 2 * CHEST_VP)) * sizeof(cpx);
+  const size_t ta  = static_cast<size_t>(g.max_dft) * (sizeof(cpx) + sizeof(float));
+  return lse > ta ? lse : ta;
+}
+
+__global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void pusch_chest_kernel(
+    const chest_job* __restrict__ jobs,
+    chest_geom geom,
+    const uint32_t* __restrict__ grids,
+    uint32_t* __restrict__ ce,
+    float* __restrict__ noise_var,
+    float* __restrict__ metrics,
+    const uint32_t* __restrict__ gseq)
 {
   extern __shared__ __align__(16) unsigned char lds_raw[];
-  const int  EN = max_pilots + 2 * CHEST_VP;
-  chest_lds  L;
-  L.E    = reinterpret_cast<cpx*>(lds_raw);
-  L.F    = L.E + 2 * EN;
-  L.seq  = reinterpret_cast<uint32_t*>(L.F + 2 * max_pilots);
-  L.taps = reinterpret_cast<float*>(L.seq + max_dmrs * max_words);
-  (void)max_dmrs;
+  const int EN = geom.max_pilots + 2 * CHEST_VP;
+  chest_lds L;
+  L.F    = reinterpret_cast<cpx*>(lds_raw);
+  L.Y    = L.F + static_cast<size_t>(geom.max_planes) * geom.max_gl * geom.max_pilots;
+  L.E    = L.Y + static_cast<size_t>(geom.max_dmrs) * geom.max_pilots;
+  L.X    = L.Y;
+  L.corr = reinterpret_cast<float*>(L.X + geom.max_dft);
+  L.seq  = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(L.Y) + chest_region_bytes(geom));
+  L.taps = reinterpret_cast<float*>(L.seq + geom.max_dmrs * geom.max_words);
 
-  const chest_job& jb     = jobs[blockIdx.x];
-  const int        lane   = static_cast<int>(threadIdx.x);
-  const int        N      = jb.nof_pilots;
-  const int        GL     = jb.group_layers;
-  const int        D      = jb.nof_dmrs;
-  const float      beta   = jb.beta;
-  const int        per_rb = jb.pilots_per_rb;
-  const uint32_t   n0     = 2 * jb.seq_offset;  // first sequence bit of the allocation
-  const uint32_t   w0     = n0 >> 5;
-  const int        W      = max_words;
-  cpx* const       E0     = L.E;
-  cpx* const       E1     = L.E + EN;
+  const chest_job& jb    = jobs[blockIdx.x];
+  const int        lane  = static_cast<int>(threadIdx.x);
+  const int        N     = jb.nof_pilots;
+  const int        GL    = jb.group_layers;
+  const int        D     = jb.nof_dmrs;
+  const int        Q     = jb.td_interp ? D : 1;
+  const float      beta  = jb.beta;
+  const uint32_t   n0    = 2 * jb.seq_offset;  // first sequence bit of the allocation
+  const int        W     = geom.max_words;
+  const int        NP    = geom.max_pilots;
+  cpx* const       Fbase = L.F;
 
-  // Stage: zeroed enlarged buffers, taps, the sequence words of every DM-RS symbol.
-  for (int i = lane; i < 2 * EN; i += CHEST_THREADS) {
-    L.E[i] = {0.f, 0.f};
-  }
+  // Stage: taps and the sequence words of every DM-RS symbol (the plan's resident words, gold_fill_kernel).
   if (lane < 32) {
     L.taps[lane] = jb.taps[lane];
   }
   const int nwords = static_cast<int>(((n0 & 31u) + 2u * static_cast<uint32_t>(N) + 31u) >> 5);
-  for (int s = 0; s < D; ++s) {  // the plan's resident sequence words (gold_fill_kernel at plan creation)
+  for (int s = 0; s < D; ++s) {
     for (int wl = lane; wl < nwords; wl += CHEST_THREADS) {
       L.seq[s * W + wl] = gseq[jb.gseq_base + static_cast<uint32_t>(s * nwords + wl)];
     }
   }
   __syncthreads();
 
-  // Pass 1: LSE summed over the DM-RS symbols, EPRE.
+  // Pass 1: LSE of every DM-RS symbol (received x conj(pilot)), EPRE.
   float epre_acc = 0.f;
   for (int i = lane; i < N; i += CHEST_THREADS) {
-    const int      rb = i / per_rb;
-    const uint32_t k  = static_cast<uint32_t>(rb * 12 + ((jb.pattern >> (4 * (i - rb * per_rb))) & 15u));
-    cpx            z  = {0.f, 0.f};
+    const uint32_t k = pilot_subcarrier(jb, i);
     for (int s = 0; s < D; ++s) {
       const cpx y = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
       const cpx p = pilot(L.seq, W, s, n0, i);
-      z.x += y.x * p.x + y.y * p.y;  // y conj(p)
-      z.y += y.y * p.x - y.x * p.y;
+      L.Y[s * NP + i] = {y.x * p.x + y.y * p.y, y.y * p.x - y.x * p.y};
       epre_acc += y.x * y.x + y.y * y.y;
-    }
-    E0[CHEST_VP + i] = z;
-  }
-  __syncthreads();
-  // Remove the cover code of a two-layer group (pairs of adjacent pilots), then scale by 1 / (beta D).
-  const float scale = 1.0f / beta / static_cast<float>(D);
-  if (GL == 2) {
-    for (int j = lane; j < N / 2; j += CHEST_THREADS) {
-      const cpx a  = E0[CHEST_VP + 2 * j], b = E0[CHEST_VP + 2 * j + 1];
-      const cpx h0 = {(a.x + b.x) * 0.5f * scale, (a.y + b.y) * 0.5f * scale};
-      const cpx h1 = {(a.x - b.x) * 0.5f * scale, (a.y - b.y) * 0.5f * scale};
-      E0[CHEST_VP + 2 * j] = E0[CHEST_VP + 2 * j + 1] = h0;
-      E1[CHEST_VP + 2 * j] = E1[CHEST_VP + 2 * j + 1] = h1;
-    }
-  } else {
-    for (int i = lane; i < N; i += CHEST_THREADS) {
-      E0[CHEST_VP + i] = {E0[CHEST_VP + i].x * scale, E0[CHEST_VP + i].y * scale};
     }
   }
   __syncthreads();
 
-  // Frequency-domain smoothing.
-  const int nt = jb.ntaps;
-  const int c  = nt / 2;
-  for (int ly = 0; ly < GL; ++ly) {
-    cpx* E = ly ? E1 : E0;
-    cpx* F = L.F + ly * max_pilots;
-    if (jb.fd == CHEST_FD_FILTER) {
-      const int nv = jb.nof_v_pilots;
-      virtual_pilots(E, N, nv);
+  // CFO from the first two DM-RS symbols (preprocess_pilots_and_estimate_cfo, :322): arg(sum lse_1 conj(lse_0)) over
+  // the time between their starts; with compensation every DM-RS symbol is derotated by its start epoch.
+  const bool has_cfo = D >= 2;
+  float      cfo     = 0.f;
+  if (has_cfo) {
+    float ar = 0.f, ai = 0.f;
+    for (int i = lane; i < N; i += CHEST_THREADS) {
+      const cpx a = L.Y[NP + i], b = L.Y[i];
+      ar += a.x * b.x + a.y * b.y;
+      ai += a.y * b.x - a.x * b.y;
+    }
+    ar  = wave_sum(ar);
+    ai  = wave_sum(ai);
+    cfo = atan2f(ai, ar) / CHEST_TWOPI / (jb.epochs[jb.dmrs_symbols[1]] - jb.epochs[jb.dmrs_symbols[0]]);
+    if (jb.compensate_cfo) {
+      for (int s = 0; s < D; ++s) {
+        const cpx r = polar1(-CHEST_TWOPI * jb.epochs[jb.dmrs_symbols[s]] * cfo);
+        for (int i = lane; i < N; i += CHEST_THREADS) {
+          L.Y[s * NP + i] = cmul(L.Y[s * NP + i], r);
+        }
+      }
       __syncthreads();
-      for (int i = lane; i < N; i += CHEST_THREADS) {
-        cpx acc = {0.f, 0.f};
-        for (int j = 0; j < nt; ++j) {
-          const int e = CHEST_VP + i - c + j;  // symmetric taps: correlation == convolution
-          if (e >= CHEST_VP - nv && e < CHEST_VP + N + nv) {
-            acc.x += L.taps[j] * E[e].x;
-            acc.y += L.taps[j] * E[e].y;
+    }
+  }
+  const bool rotate = has_cfo && jb.compensate_cfo;
+
+  // Planes: "average" combines the DM-RS symbols into one LSE scaled by 1 / (beta D); "interpolate" keeps one per
+  // DM-RS symbol scaled by 1 / beta. Each is despread (two-layer groups), then smoothed in frequency into F.
+  const float scale = jb.td_interp ? 1.0f / beta : 1.0f / beta / static_cast<float>(D);
+  const int   nt    = jb.ntaps;
+  const int   c     = nt / 2;
+  for (int q = 0; q < Q; ++q) {
+    cpx* const E0 = L.E;
+    cpx* const E1 = L.E + EN;
+    if (GL == 2) {
+      for (int j = lane; j < N / 2; j += CHEST_THREADS) {
+        cpx a = L.Y[q * NP + 2 * j], b = L.Y[q * NP + 2 * j + 1];
+        if (!jb.td_interp) {
+          for (int s = 1; s < D; ++s) {
+            a = {a.x + L.Y[s * NP + 2 * j].x, a.y + L.Y[s * NP + 2 * j].y};
+            b = {b.x + L.Y[s * NP + 2 * j + 1].x, b.y + L.Y[s * NP + 2 * j + 1].y};
           }
         }
-        F[i] = acc;
-      }
-    } else if (jb.fd == CHEST_FD_MEAN) {
-      float sx = 0.f, sy = 0.f;
-      for (int i = lane; i < N; i += CHEST_THREADS) {
-        sx += E[CHEST_VP + i].x;
-        sy += E[CHEST_VP + i].y;
-      }
-      sx = wave_sum(sx) / static_cast<float>(N);
-      sy = wave_sum(sy) / static_cast<float>(N);
-      for (int i = lane; i < N; i += CHEST_THREADS) {
-        F[i] = {sx, sy};
+        const cpx h0 = {(a.x + b.x) * 0.5f * scale, (a.y + b.y) * 0.5f * scale};
+        const cpx h1 = {(a.x - b.x) * 0.5f * scale, (a.y - b.y) * 0.5f * scale};
+        E0[CHEST_VP + 2 * j] = E0[CHEST_VP + 2 * j + 1] = h0;
+        E1[CHEST_VP + 2 * j] = E1[CHEST_VP + 2 * j + 1] = h1;
       }
     } else {
       for (int i = lane; i < N; i += CHEST_THREADS) {
-        F[i] = E[CHEST_VP + i];
+        cpx z = L.Y[q * NP + i];
+        if (!jb.td_interp) {
+          for (int s = 1; s < D; ++s) {
+            z = {z.x + L.Y[s * NP + i].x, z.y + L.Y[s * NP + i].y};
+          }
+        }
+        E0[CHEST_VP + i] = {z.x * scale, z.y * scale};
       }
     }
-  }
-  __syncthreads();
-
-  // Pass 2: RSRP of layer 0 and the noise residual (group 0 only).
-  const cpx* F0 = L.F;
-  const cpx* F1 = L.F + max_pilots;
-  float      rsrp_acc = 0.f, noise_acc = 0.f;
-  for (int i = lane; i < N; i += CHEST_THREADS) {
-    const cpx f0 = F0[i];
-    rsrp_acc += f0.x * f0.x + f0.y * f0.y;
-    if (jb.group == 0) {
-      cpx h = f0;
-      if (GL == 2) {  // layer 1 carries w_f = -1 on odd pilots
-        const cpx  f1 = F1[i];
-        const bool od = (i & 1) != 0;
-        h             = {f0.x + (od ? -f1.x : f1.x), f0.y + (od ? -f1.y : f1.y)};
+    __syncthreads();
+    for (int ly = 0; ly < GL; ++ly) {
+      cpx* E = ly ? E1 : E0;
+      cpx* F = Fbase + (q * GL + ly) * NP;
+      if (jb.fd == CHEST_FD_FILTER) {
+        const int nv = jb.nof_v_pilots;
+        virtual_pilots(E, N, nv);
+        __syncthreads();
+        for (int i = lane; i < N; i += CHEST_THREADS) {
+          cpx acc = {0.f, 0.f};
+          for (int j = 0; j < nt; ++j) {
+            const int e = CHEST_VP + i - c + j;  // symmetric taps: correlation == convolution
+            if (e >= CHEST_VP - nv && e < CHEST_VP + N + nv) {
+              acc.x += L.taps[j] * E[e].x;
+              acc.y += L.taps[j] * E[e].y;
+            }
+          }
+          F[i] = acc;
+        }
+      } else if (jb.fd == CHEST_FD_MEAN) {
+        float sx = 0.f, sy = 0.f;
+        for (int i = lane; i < N; i += CHEST_THREADS) {
+          sx += E[CHEST_VP + i].x;
+          sy += E[CHEST_VP + i].y;
+        }
+        sx = wave_sum(sx) / static_cast<float>(N);
+        sy = wave_sum(sy) / static_cast<float>(N);
+        for (int i = lane; i < N; i += CHEST_THREADS) {
+          F[i] = {sx, sy};
+        }
+      } else {
+        for (int i = lane; i < N; i += CHEST_THREADS) {
+          F[i] = E[CHEST_VP + i];
+        }
       }
-      const int      rb = i / per_rb;
-      const uint32_t k  = static_cast<uint32_t>(rb * 12 + ((jb.pattern >> (4 * (i - rb * per_rb))) & 15u));
+    }
+    __syncthreads();
+  }
+
+  // RSRP of layer 0 over the planes, and the noise residual (group 0 only) against the time-averaged estimate
+  // beta / Q sum_q F_q, re-rotated by the CFO when compensating (estimate_noise, :422).
+  float rsrp_acc = 0.f, noise_acc = 0.f;
+  for (int i = lane; i < N; i += CHEST_THREADS) {
+    cpx h = {0.f, 0.f};
+    for (int q = 0; q < Q; ++q) {
+      const cpx f0 = Fbase[(q * GL) * NP + i];
+      rsrp_acc += f0.x * f0.x + f0.y * f0.y;
+      cpx hq = f0;
+      if (GL == 2) {  // layer 1 carries w_f = -1 on odd pilots
+        const cpx  f1 = Fbase[(q * GL + 1) * NP + i];
+        const bool od = (i & 1) != 0;
+        hq            = {f0.x + (od ? -f1.x : f1.x), f0.y + (od ? -f1.y : f1.y)};
+      }
+      const float sq = beta / static_cast<float>(Q);
+      h              = {hq.x * sq + h.x, hq.y * sq + h.y};
+    }
+    if (jb.group == 0) {
+      const uint32_t k = pilot_subcarrier(jb, i);
       for (int s = 0; s < D; ++s) {
-        const cpx   y  = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
-        const cpx   p  = pilot(L.seq, W, s, n0, i);
-        const cpx   q  = {beta * (h.x * p.x - h.y * p.y), beta * (h.x * p.y + h.y * p.x)};  // beta h p
+        const cpx y = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
+        cpx       q = cmul(h, pilot(L.seq, W, s, n0, i));
+        if (rotate) {
+          q = cmul(q, polar1(CHEST_TWOPI * jb.epochs[jb.dmrs_symbols[s]] * cfo));
+        }
         const float ex = y.x - q.x, ey = y.y - q.y;
         noise_acc += ex * ex + ey * ey;
       }
@@ -274,43 +363,144 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
   }
   const float nof_pilots = static_cast<float>(N * D);
   const float epre       = wave_sum(epre_acc) / nof_pilots;
-  const float rsrp       = wave_sum(rsrp_acc) * beta * beta / static_cast<float>(N);
-  const float noise_sum  = wave_sum(noise_acc);
-  if (lane == 0 && jb.group == 0) {
-    const float nv           = fmaxf(rsrp / 1e10f, noise_sum / (nof_pilots - 1.f));
-    noise_var[jb.noise_slot] = nv;
-    if (metrics != nullptr) {
-      float* m = metrics + 4 * jb.noise_slot;
-      m[0]     = rsrp;
-      m[1]     = epre;
-      m[2]     = nv;
-      m[3]     = (nv != 0.f) ? rsrp / beta / beta / nv : 1000.f;
+  const float rsrp = wave_sum(rsrp_acc) * beta * beta * static_cast<float>(D) / static_cast<float>(Q) / nof_pilots;
+  const float noise_sum = wave_sum(noise_acc);
+
+  // Time alignment of the smoothed layer-0 planes (estimate_time_alignment, port_channel_estimator_helpers.cpp:246 ->
+  // time_alignment_estimator_dft_impl): inverse DFT of size M through LDS (radix 2, bit-reversed scatter), |.|^2
+  // summed over the planes, the peak within +-ta_max taps, quadratic refinement unless M is the largest DFT size.
+  if (jb.group == 0) {
+    const int M   = jb.ta_dft;
+    const int lgM = jb.ta_log2;
+    __syncthreads();  // Y / E are dead: the region becomes X / corr
+    for (int q = 0; q < Q; ++q) {
+      for (int n = lane; n < M; n += CHEST_THREADS) {
+        L.X[n] = {0.f, 0.f};
+      }
+      __syncthreads();
+      const uint32_t k0 = pilot_subcarrier(jb, 0);
+      for (int i = lane; i < N; i += CHEST_THREADS) {
+        const uint32_t pos = jb.ta_positions ? pilot_subcarrier(jb, i) - k0 : static_cast<uint32_t>(i);
+        L.X[__brev(pos) >> (32 - lgM)] = Fbase[(q * GL) * NP + i];
+      }
+      __syncthreads();
+      for (int lh = 0; lh < lgM; ++lh) {
+        const int h = 1 << lh;
+        for (int b = lane; b < M / 2; b += CHEST_THREADS) {
+          const int   j  = b & (h - 1);
+          const int   i0 = ((b >> lh) << (lh + 1)) + j;
+          const float r  = static_cast<float>(j) / static_cast<float>(2 * h);  // revolutions: e^{+j 2 pi j / 2h}
+          const cpx   w  = {__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r)};
+          const cpx   a  = L.X[i0];
+          const cpx   t  = cmul(L.X[i0 + h], w);
+          L.X[i0]        = {a.x + t.x, a.y + t.y};
+          L.X[i0 + h]    = {a.x - t.x, a.y - t.y};
+        }
+        __syncthreads();
+      }
+      for (int n = lane; n < M; n += CHEST_THREADS) {
+        const float p = L.X[n].x * L.X[n].x + L.X[n].y * L.X[n].y;
+        L.corr[n]     = q ? L.corr[n] + p : p;
+      }
+      __syncthreads();
+    }
+    const int m  = jb.ta_max;
+    float     dv = -INFINITY, av = -INFINITY;
+    int       di = 0x7fffffff, ai = 0x7fffffff;
+    for (int n = lane; n < m; n += CHEST_THREADS) {
+      if (L.corr[n] > dv) {
+        dv = L.corr[n];
+        di = n;
+      }
+      if (L.corr[M - m + n] > av) {
+        av = L.corr[M - m + n];
+        ai = n;
+      }
+    }
+    wave_argmax(dv, di);
+    wave_argmax(av, ai);
+    const int idx  = (dv >= av) ? di : -(m - ai);
+    float     frac = 0.f;
+    if (M != 4096) {
+      const int nt5 = (m > 2) ? 5 : 3;
+      float     num, den, corr_k;
+      auto      cv = [&](int i) { return L.corr[(idx + i - nt5 / 2) & (M - 1)]; };
+      if (nt5 == 5) {
+        num    = -0.4f * cv(0) + -0.2f * cv(1) + 0.0f * cv(2) + 0.2f * cv(3) + 0.4f * cv(4);
+        den    = 0.571429f * cv(0) + -0.285714f * cv(1) + -0.571429f * cv(2) + -0.285714f * cv(3) + 0.571429f * cv(4);
+        corr_k = 1.0f;
+      } else {
+        num    = -0.5f * cv(0) + 0.0f * cv(1) + 0.5f * cv(2);
+        den    = 0.5f * cv(0) + -1.0f * cv(1) + 0.5f * cv(2);
+        corr_k = 0.5f;
+      }
+      const float r = -corr_k * num / den;
+      frac          = (isnan(r) || isinf(r) || fabsf(r) > 1.0f) ? 0.f : r;
+    }
+    // phy_time_unit::from_seconds of the float seconds: Tc units truncated at x10, then rounded half away.
+    const float   ta_f = static_cast<float>((static_cast<double>(idx) + static_cast<double>(frac)) / jb.ta_fs);
+    const double  t_c  = 1.0 / (480000.0 * 4096.0);
+    const int64_t tc10 = static_cast<int64_t>(static_cast<double>(ta_f) / t_c * 10.0);
+    const float   ta_s = static_cast<float>(static_cast<double>(tc10 / 10 + (tc10 % 10) / 5) * t_c);
+    if (lane == 0) {
+      const float nv = fmaxf(rsrp / 1e10f, noise_sum / (nof_pilots - 1.f));
+      noise_var[jb.noise_slot] = nv;
+      if (metrics != nullptr) {
+        float* mt = metrics + CHEST_METRICS * jb.noise_slot;
+        mt[0]     = rsrp;
+        mt[1]     = epre;
+        mt[2]     = nv;
+        mt[3]     = (nv != 0.f) ? rsrp / beta / beta / nv : 1000.f;
+        mt[4]     = ta_s;
+        mt[5]     = has_cfo ? cfo * jb.scs_hz : __builtin_nanf("");
+        mt[6]     = 0.f;
+        mt[7]     = 0.f;
+      }
     }
   }
 
-  // Interpolation to every RE of the allocation, the same estimate for every symbol ("average" strategy).
+  // Estimates of every RE of the allocation: linear frequency interpolation of the planes; "interpolate" then
+  // interpolates in time between the planes around each symbol (host table); bf16, then the CFO rotation of each
+  // symbol by its start epoch in bf16 like sc_prod on the channel_estimate (:128). The compact layout writes the
+  // unrotated row of start_symbol and, with compensation, the CFO (float bits) in the first element of the next row.
   const int nre    = jb.nof_rb * 12;
   const int offset = jb.interp_offset;
   const int stride = jb.interp_stride;
   const int last   = offset + (N - 1) * stride;
+  auto      freq   = [&](const cpx* F, int k) -> cpx {
+    if (k <= offset) {
+      return F[0];
+    }
+    if (k >= last) {
+      return F[N - 1];
+    }
+    const int   i = (k - offset) / stride;
+    const float w = static_cast<float>((k - offset) - i * stride) / static_cast<float>(stride);
+    const cpx   a = F[i], b = F[i + 1];
+    return {(b.x - a.x) * w + a.x, (b.y - a.y) * w + a.y};
+  };
+  const bool rotate_out = rotate && !jb.compact_cfo;
   for (int k = lane; k < nre; k += CHEST_THREADS) {
     for (int ly = 0; ly < GL; ++ly) {
-      const cpx* F = L.F + ly * max_pilots;
-      cpx        v;
-      if (k <= offset) {
-        v = F[0];
-      } else if (k >= last) {
-        v = F[N - 1];
-      } else {
-        const int   i = (k - offset) / stride;
-        const float w = static_cast<float>((k - offset) - i * stride) / static_cast<float>(stride);
-        const cpx   a = F[i], b = F[i + 1];
-        v             = {(b.x - a.x) * w + a.x, (b.y - a.y) * w + a.y};
-      }
-      const uint32_t u   = to_bf16c(v);
-      uint32_t*      dst = ce + jb.ce_base + ly * jb.ce_layer_stride + static_cast<uint32_t>(k);
-      for (int l = jb.first_symbol; l < jb.first_symbol + jb.nof_symbols; ++l) {
+      uint32_t* dst = ce + jb.ce_base + ly * jb.ce_layer_stride + static_cast<uint32_t>(k);
+      const cpx v0  = freq(Fbase + ly * NP, k);
+      for (int r = 0; r < jb.nof_out_symbols; ++r) {
+        const int l = jb.first_symbol + r;
+        cpx       v = v0;
+        if (jb.td_interp) {
+          const cpx   a = freq(Fbase + (jb.td_q0[l] * GL + ly) * NP, k);
+          const cpx   b = freq(Fbase + (jb.td_q1[l] * GL + ly) * NP, k);
+          const float w = jb.td_w[l];
+          v             = {a.x + (b.x - a.x) * w, a.y + (b.y - a.y) * w};
+        }
+        uint32_t u = to_bf16c(v);
+        if (rotate_out) {
+          u = to_bf16c(cmul(bf16c(u), polar1(CHEST_TWOPI * jb.epochs[l] * cfo)));
+        }
         dst[l * jb.nsc] = u;
+      }
+      if (jb.compact_cfo && k == 0) {
+        dst[(jb.first_symbol + 1) * jb.nsc] = __float_as_uint(has_cfo ? cfo : 0.f);
       }
     }
   }
@@ -318,17 +508,15 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
 
 } // namespace
 
-size_t pusch_chest_lds_bytes(int max_pilots, int max_dmrs, int max_words)
+size_t pusch_chest_lds_bytes(const chest_geom& g)
 {
-  return (2 * static_cast<size_t>(max_pilots + 2 * CHEST_VP) + 2 * static_cast<size_t>(max_pilots)) * sizeof(cpx) +
-         static_cast<size_t>(max_dmrs) * static_cast<size_t>(max_words) * 4 + 32 * 4;
+  return static_cast<size_t>(g.max_planes) * g.max_gl * g.max_pilots * sizeof(cpx) + chest_region_bytes(g) +
+         static_cast<size_t>(g.max_dmrs) * g.max_words * 4 + 32 * 4;
 }
 
 void launch_pusch_chest(const chest_job* d_jobs,
                         int              nof_jobs,
-                        int              max_pilots,
-                        int              max_dmrs,
-                        int              max_words,
+                        const chest_geom& geom,
                         const uint32_t*  d_grids,
                         uint32_t*        d_ce,
                         float*           d_noise_var,
@@ -339,10 +527,9 @@ void launch_pusch_chest(const chest_job* d_jobs,
   if (nof_jobs <= 0) {
     return;
   }
-  const size_t lds = pusch_chest_lds_bytes(max_pilots, max_dmrs, max_words);
+  const size_t lds = pusch_chest_lds_bytes(geom);
   hipLaunchKernelGGL(pusch_chest_kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(CHEST_THREADS),
-                     static_cast<unsigned>(lds), stream, d_jobs, max_pilots, max_dmrs, max_words, d_grids, d_ce,
-                     d_noise_var, d_metrics, d_seq);
+                     static_cast<unsigned>(lds), stream, d_jobs, geom, d_grids, d_ce, d_noise_var, d_metrics, d_seq);
 }
 
 } // namespace srsgpu

@@ -227,7 +227,15 @@ struct demod_uniform {
   float                   nv[4], nv_max;
   const demap_pair_table* tables;  ///< Global demapper tables (staged into LDS for Qm >= 6).
   const uint32_t*         gseq;    ///< The plan's precomputed descrambling sequences.
+  const cpx*              rot;     ///< LDS [14][4 layers][4 ports] CFO rotations (demod_desc::ce_cfo), else null.
 };
+
+/// Round-to-nearest-even float -> bf16 pair (adt/bf16.h), the estimator's storage rounding.
+__device__ __forceinline__ uint32_t to_bf16c(cpx v)
+{
+  const uint32_t a = __float_as_uint(v.x), b = __float_as_uint(v.y);
+  return ((a + 0x7fffu + ((a >> 16) & 1u)) >> 16) | (((b + 0x7fffu + ((b >> 16) & 1u)) >> 16) << 16);
+}
 
 /// Stages the chunk's descrambling words (and the first word of the next chunk) and, for 64/256QAM, the demapper
 /// tables in LDS. The caller synchronises.
@@ -260,7 +268,8 @@ __device__ __forceinline__ void load_re(const demod_desc& d,
                                         const uint32_t* __restrict__ grids,
                                         const uint32_t* __restrict__ ce,
                                         uint32_t (&yw)[4],
-                                        uint32_t (&hw)[L][4])
+                                        uint32_t (&hw)[L][4],
+                                        uint32_t& sym)
 {
   // Symbol and subcarrier of the RE.
   uint32_t l = 0;
@@ -269,6 +278,7 @@ __device__ __forceinline__ void load_re(const demod_desc& d,
     l += (d.sym_cum[j] <= r) ? 1u : 0u;
   }
   const uint32_t k = r - d.sym_cum[l];
+  sym              = l;
   uint32_t       sc;
   if ((d.dmrs_mask >> l) & 1u) {
     const uint32_t nd  = d.nd_dmrs;
@@ -308,9 +318,9 @@ __device__ __forceinline__ void demod_res(const demod_uniform& u,
   const bool         zf = d.eq == DEMOD_EQ_ZF;
   // The first RE's loads are in flight while the chunk's sequence is generated.
   uint32_t r = u.re_begin + threadIdx.x;
-  uint32_t yw[4] = {}, hw[L][4] = {};
+  uint32_t yw[4] = {}, hw[L][4] = {}, sym = 0;
   if (r < u.re_end) {
-    load_re<L>(d, r, grids, ce, yw, hw);
+    load_re<L>(d, r, grids, ce, yw, hw, sym);
   }
   stage_chunk(u, seq, tab);
   __syncthreads();
@@ -318,14 +328,14 @@ __device__ __forceinline__ void demod_res(const demod_uniform& u,
 #if SRSGPU_DEMOD_PREFETCH
     // The next RE's loads fly while this one is equalised and demapped.
     (void)first;
-    uint32_t       nyw[4] = {}, nhw[L][4] = {};
+    uint32_t       nyw[4] = {}, nhw[L][4] = {}, nsym = 0;
     const uint32_t rn     = r + DEMOD_THREADS;
     if (rn < u.re_end) {
-      load_re<L>(d, rn, grids, ce, nyw, nhw);
+      load_re<L>(d, rn, grids, ce, nyw, nhw, nsym);
     }
 #else
     if (!first) {
-      load_re<L>(d, r, grids, ce, yw, hw);
+      load_re<L>(d, r, grids, ce, yw, hw, sym);
     }
 #endif
     cpx y[4], h[L][4];
@@ -335,6 +345,17 @@ __device__ __forceinline__ void demod_res(const demod_uniform& u,
 #pragma unroll
       for (int ly = 0; ly < L; ++ly) {
         h[ly][p] = bf16c(hw[ly][p]);
+      }
+    }
+    if (u.rot != nullptr) {
+      // Compact estimate with CFO compensation: the symbol's estimate the reference estimator stores,
+      // bf16(bf16(h) e^{j 2 pi t_l cfo}) (port_channel_estimator_average_impl.cpp:128).
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int ly = 0; ly < L; ++ly) {
+          h[ly][p] = bf16c(to_bf16c(cmul(h[ly][p], u.rot[(sym * 4 + ly) * 4 + p])));
+        }
       }
     }
     cpx   eq[L];
@@ -438,6 +459,7 @@ __device__ __forceinline__ void demod_res(const demod_uniform& u,
         hw[ly][p] = nhw[ly][p];
       }
     }
+    sym = nsym;
 #endif
   }
 }
@@ -472,6 +494,7 @@ __global__ __launch_bounds__(DEMOD_THREADS) DEMOD_OCCUPANCY void pusch_demodulat
   __shared__ uint32_t         seq[DEMOD_CHUNK_WORDS + 1];
   __shared__ demap_pair_table tab[DEMAP_TABLES];
   __shared__ uint32_t         out32[DEMOD_OUT_BYTES / 4];
+  __shared__ cpx              rot[14 * 16];
   const mod_chunk             ch     = chunks[blockIdx.x];
   const demod_desc&           d      = descs[ch.tx];
   const uint32_t              tid    = threadIdx.x;
@@ -482,6 +505,22 @@ __global__ __launch_bounds__(DEMOD_THREADS) DEMOD_OCCUPANCY void pusch_demodulat
   u.word0    = ch.word0;
   u.tables   = tables;
   u.gseq     = gseq;
+  u.rot      = nullptr;
+  if (d.ce_cfo) {
+    // Per (symbol, layer, port) rotation by the estimator's CFO (float bits next to the compact row); the caller's
+    // first barrier (after stage_chunk) publishes them.
+    for (uint32_t i = tid; i < 14u * 16u; i += DEMOD_THREADS) {
+      const uint32_t l = i >> 4, ly = (i >> 2) & 3u, p = i & 3u;
+      float          c = 0.f;
+      if (ly < d.L && p < d.P) {
+        c = __uint_as_float(ce[d.ce_base + ly * d.ce_layer_stride + p * d.port_stride + d.nsc]);
+      }
+      float sn, cs;
+      sincosf(6.283185307f * d.epochs[l] * c, &sn, &cs);
+      rot[i] = cmk(cs, sn);
+    }
+    u.rot = rot;
+  }
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     u.nv[p] = noise_var[4 * d.tx + p];

@@ -311,8 +311,11 @@ struct demod_desc {
   uint8_t  ce_compact;      ///< Estimates in the compact layout: every symbol reads the row at ce_base.
   uint16_t sym_cum[16];     ///< Data REs in the symbols before symbol l (l = 0..14).
   uint32_t seq_word_offset; ///< First word of the transmission's descrambling sequence in the plan's sequence buffer.
+  uint32_t ce_cfo;          ///< Compact layout with CFO compensation: rotate each symbol's estimates (CFO word at
+                            ///< ce_base + nsc of every (layer, port)).
+  float    epochs[14];      ///< Symbol start epochs (symbol durations) for the rotation.
 };
-static_assert(sizeof(demod_desc) == 88, "demod_desc layout");
+static_assert(sizeof(demod_desc) == 152, "demod_desc layout");
 
 /// demod_desc::eq: the reference's ZF paths (1 layer: 1 x N with port reduction; 2 layers: 2 x N) or linear MMSE.
 constexpr uint8_t DEMOD_EQ_ZF   = 0;
@@ -352,6 +355,7 @@ void launch_pdsch_dmrs(const dmrs_job* d_jobs,
 
 /// PUSCH channel estimator job (pusch_chest.hip): one (transmission, rx port, DM-RS CDM group).
 struct chest_job {
+  double   ta_fs;            ///< Sampling rate of the time-alignment correlation (DFT size x SCS x pilot stride), Hz.
   uint32_t grid_base;        ///< Element of (port, symbol 0, first allocated subcarrier) in the rx grids.
   uint32_t ce_base;          ///< Element of (first layer of the group, port, symbol 0, first allocated subcarrier).
   uint32_t ce_layer_stride;  ///< Elements per layer of a slot's estimates.
@@ -362,9 +366,16 @@ struct chest_job {
   uint32_t noise_slot;       ///< 4 * tx + port: noise variance / metrics slot.
   float    beta;             ///< DM-RS to data amplitude scaling.
   float    taps[32];         ///< Normalised smoothing filter taps (CHEST_FD_FILTER).
+  float    epochs[14];       ///< Symbol start epochs in symbol durations (initialize_symbol_start_epochs).
+  float    td_w[14];         ///< "interpolate": weight of plane td_q1 for symbol l (plane td_q0 gets 1 - w).
+  float    scs_hz;           ///< Subcarrier spacing (CFO in Hz).
   uint16_t nof_pilots;       ///< Pilots per DM-RS symbol.
   uint16_t nof_rb;           ///< Allocated RBs (contiguous).
+  uint16_t ta_dft;           ///< Time-alignment DFT size M (power of two, 128..4096).
+  uint16_t ta_max;           ///< Correlation taps searched on each side (half cyclic prefix in samples).
   uint8_t  dmrs_symbols[14]; ///< OFDM symbols carrying DM-RS.
+  int8_t   td_q0[14];        ///< "interpolate": planes interpolated for symbol l.
+  int8_t   td_q1[14];
   uint8_t  nof_dmrs;         ///< Number of DM-RS symbols.
   uint8_t  group_layers;     ///< Layers of this CDM group (1 or 2).
   uint8_t  group;            ///< CDM group (0: ports 1000/1001, 1: ports 1002/1003).
@@ -376,7 +387,13 @@ struct chest_job {
   uint8_t  interp_stride;    ///< Interpolator stride.
   uint8_t  first_symbol;     ///< First allocated OFDM symbol.
   uint8_t  nof_symbols;      ///< Allocated OFDM symbols.
-  uint8_t  pad[3];
+  uint8_t  nof_out_symbols;  ///< Rows written: nof_symbols, or 1 in the compact layout.
+  uint8_t  td_interp;        ///< Time-domain strategy: 0 average (one plane), 1 interpolate (one plane per DM-RS symbol).
+  uint8_t  compensate_cfo;   ///< Derotate the DM-RS symbols by the estimated CFO and rotate the estimates.
+  uint8_t  compact_cfo;      ///< Compact layout with CFO compensation: store the CFO next to the estimate row.
+  uint8_t  ta_log2;          ///< log2(ta_dft).
+  uint8_t  ta_positions;     ///< 1: pilots at their subcarrier offset (mask path), 0: in the first bins (stride 2).
+  uint8_t  pad[1];
   uint32_t gseq_base;        ///< The job's DM-RS sequence words in the plan's buffer: [DM-RS symbol][staged word].
 };
 
@@ -384,15 +401,25 @@ constexpr uint8_t CHEST_FD_NONE   = 0;
 constexpr uint8_t CHEST_FD_MEAN   = 1;
 constexpr uint8_t CHEST_FD_FILTER = 2;
 
-/// Dynamic LDS of the channel-estimator kernel for the plan's largest job (pilots per symbol, DM-RS symbols, staged
-/// sequence words per symbol).
-size_t pusch_chest_lds_bytes(int max_pilots, int max_dmrs, int max_words);
+/// Floats per (transmission, port) of the estimator's metrics output (RSRP, EPRE, noise variance, SNR, TA, CFO).
+constexpr int CHEST_METRICS = 8;
+
+/// Plan-wide maxima that size the estimator's dynamic LDS.
+struct chest_geom {
+  int max_pilots;  ///< Pilots per DM-RS symbol.
+  int max_dmrs;    ///< DM-RS symbols.
+  int max_words;   ///< Staged sequence words per DM-RS symbol.
+  int max_planes;  ///< LSE planes (1 with "average", the DM-RS symbols with "interpolate").
+  int max_gl;      ///< Layers per CDM group.
+  int max_dft;     ///< Time-alignment DFT size.
+};
+
+/// Dynamic LDS of the channel-estimator kernel for the plan's largest job.
+size_t pusch_chest_lds_bytes(const chest_geom& g);
 
 void launch_pusch_chest(const chest_job* d_jobs,
                         int              nof_jobs,
-                        int              max_pilots,
-                        int              max_dmrs,
-                        int              max_words,
+                        const chest_geom& geom,
                         const uint32_t*  d_grids,
                         uint32_t*        d_ce,
                         float*           d_noise_var,

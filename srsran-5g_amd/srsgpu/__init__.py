@@ -197,13 +197,15 @@ class PuschDemodConfig(ctypes.Structure):
         ("rb_start", ctypes.c_uint16),
         ("nof_rb", ctypes.c_uint16),
         ("estimate_layout", ctypes.c_uint8),
-        ("pad", ctypes.c_uint8),
+        ("cfo_compensated", ctypes.c_uint8),
         ("grid_index", ctypes.c_uint32),
         ("llr_offset", ctypes.c_uint32),
+        ("numerology", ctypes.c_uint8),
+        ("pad2", ctypes.c_uint8 * 3),
     ]
 
 
-assert ctypes.sizeof(PuschDemodConfig) == 28
+assert ctypes.sizeof(PuschDemodConfig) == 32
 
 
 class PuschChestConfig(ctypes.Structure):
@@ -222,14 +224,19 @@ class PuschChestConfig(ctypes.Structure):
         ("slot_index", ctypes.c_uint16),
         ("fd_smoothing", ctypes.c_uint8),
         ("estimate_layout", ctypes.c_uint8),
-        ("pad", ctypes.c_uint8 * 2),
+        ("td_strategy", ctypes.c_uint8),
+        ("compensate_cfo", ctypes.c_uint8),
         ("scaling", ctypes.c_float),
         ("grid_index", ctypes.c_uint32),
+        ("numerology", ctypes.c_uint8),
+        ("pad", ctypes.c_uint8 * 3),
     ]
 
 
-assert ctypes.sizeof(PuschChestConfig) == 28
+assert ctypes.sizeof(PuschChestConfig) == 32
 CHEST_FD_NONE, CHEST_FD_MEAN, CHEST_FD_FILTER = 0, 1, 2
+CHEST_TD_AVERAGE, CHEST_TD_INTERPOLATE = 0, 1
+CHEST_METRICS = 8  # per (tx, port): RSRP, EPRE, noise variance, SNR, TA (s), CFO (Hz, NaN without), 0, 0
 CE_PER_SYMBOL, CE_COMPACT = 0, 1  # channel-estimate layouts (SRSGPU_CE_*)
 EQ_ZF, EQ_MMSE = 0, 1
 
@@ -897,6 +904,8 @@ class PuschDemodulation:
     nof_rb: int
     equalizer: int = EQ_ZF
     estimate_layout: int = CE_PER_SYMBOL
+    cfo_compensated: int = 0  # compact layout written with CFO compensation (the estimator's compensate_cfo)
+    numerology: int = 1
 
     def nof_llrs(self) -> int:
         dm = (4 if self.dmrs_type == 2 else 6) * self.nof_cdm_groups_without_data
@@ -917,6 +926,7 @@ def make_pusch_demod_configs(demods: Sequence[PuschDemodulation], grid_index: Se
                                                                    m.equalizer)
         a.dmrs_symbol_mask, a.rb_start, a.nof_rb, a.grid_index = m.dmrs_symbol_mask, m.rb_start, m.nof_rb, g
         a.estimate_layout = m.estimate_layout
+        a.cfo_compensated, a.numerology = m.cfo_compensated, m.numerology
         a.llr_offset = off if llr_offsets is None else llr_offsets[i]
         offs.append(a.llr_offset)
         off += m.nof_llrs()
@@ -1000,6 +1010,9 @@ class PuschChannelEstimation:
     scaling: float = 1.0
     fd_smoothing: int = CHEST_FD_FILTER
     estimate_layout: int = CE_PER_SYMBOL
+    td_strategy: int = CHEST_TD_AVERAGE
+    compensate_cfo: int = 0
+    numerology: int = 1
 
 
 def make_pusch_chest_configs(ests: Sequence[PuschChannelEstimation], grid_index: Sequence[int]):
@@ -1009,7 +1022,8 @@ def make_pusch_chest_configs(ests: Sequence[PuschChannelEstimation], grid_index:
         a.scrambling_id, a.n_scid, a.dmrs_type, a.nof_tx_layers = e.scrambling_id, e.n_scid, e.dmrs_type, e.nof_tx_layers
         a.nof_rx_ports, a.start_symbol, a.nof_symbols = e.nof_rx_ports, e.start_symbol, e.nof_symbols
         a.dmrs_symbol_mask, a.rb_start, a.nof_rb, a.slot_index = e.dmrs_symbol_mask, e.rb_start, e.nof_rb, e.slot_index
-        a.estimate_layout = e.estimate_layout
+        a.estimate_layout, a.td_strategy, a.compensate_cfo = e.estimate_layout, e.td_strategy, e.compensate_cfo
+        a.numerology = e.numerology
         a.fd_smoothing, a.scaling, a.grid_index = e.fd_smoothing, e.scaling, g
     return arr
 
@@ -1017,7 +1031,7 @@ def make_pusch_chest_configs(ests: Sequence[PuschChannelEstimation], grid_index:
 class PuschChannelEstimatorPlan:
     """srsgpu_pusch_chest_plan: DM-RS channel estimation of a batch of PUSCH transmissions from rx grids
     (S, Pg, 14, nsc) into estimates (S, 4, Pg, 14, nsc) (uint32 bf16 pairs), noise variances (ntx, 4) and optional
-    metrics (ntx, 4, [RSRP, EPRE, noise variance, SNR])."""
+    metrics (ntx, 4, CHEST_METRICS: RSRP, EPRE, noise variance, SNR, TA seconds, CFO Hz or NaN, 0, 0)."""
 
     def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4):
         self.ctx = ctx
@@ -1050,7 +1064,7 @@ class PuschChannelEstimator:
 
     def estimate_batch(self, grids_u16, ests: Sequence[PuschChannelEstimation], grid_index: Sequence[int]):
         """grids_u16 (S, Pg, 14, nsc, 2) -> (estimates (S, 4, Pg, 14, nsc, 2) uint16, noise_var (ntx, 4),
-        metrics (ntx, 4, 4))."""
+        metrics (ntx, 4, CHEST_METRICS))."""
         dev = torch.device("cuda", self.ctx.device)
         plan = PuschChannelEstimatorPlan(self.ctx, make_pusch_chest_configs(ests, grid_index), self.grid_nof_prb,
                                          self.grid_nof_ports)
@@ -1059,12 +1073,12 @@ class PuschChannelEstimator:
         d_g = torch.from_numpy(g.view(np.int32).reshape(-1).copy()).to(dev)
         d_ce = torch.zeros(S * 4 * g.shape[1] * g.shape[2] * g.shape[3], dtype=torch.int32, device=dev)
         d_nv = torch.zeros(4 * len(ests), dtype=torch.float32, device=dev)
-        d_m = torch.zeros(16 * len(ests), dtype=torch.float32, device=dev)
+        d_m = torch.zeros(4 * CHEST_METRICS * len(ests), dtype=torch.float32, device=dev)
         plan.execute(d_g, d_ce, d_nv, d_m)
         torch.cuda.synchronize(dev)
         plan.close()
         ce = d_ce.cpu().numpy().view(np.uint16).reshape((S, 4) + g.shape[1:])
-        return ce, d_nv.cpu().numpy().reshape(-1, 4), d_m.cpu().numpy().reshape(-1, 4, 4)
+        return ce, d_nv.cpu().numpy().reshape(-1, 4), d_m.cpu().numpy().reshape(-1, 4, CHEST_METRICS)
 
 
 class OfdmPlan:

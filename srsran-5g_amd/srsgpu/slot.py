@@ -160,7 +160,7 @@ class UplinkPipeline:
         self.d_grid = torch.zeros(cell.grid_elems(), dtype=torch.int32, device=dev)
         self.d_ce = torch.zeros(4 * cell.grid_elems(), dtype=torch.int32, device=dev)
         self.d_nv = torch.zeros(4 * len(ests), dtype=torch.float32, device=dev)
-        self.d_metrics = torch.zeros(16 * len(ests), dtype=torch.float32, device=dev)
+        self.d_metrics = torch.zeros(4 * srsgpu.CHEST_METRICS * len(ests), dtype=torch.float32, device=dev)
         self.d_llrs = torch.zeros(max(self.llr_total, 4), dtype=torch.int8, device=dev)
         self.d_harq = torch.zeros(harq_total, dtype=torch.int8, device=dev)
         self.d_crc = torch.zeros(cb_total, dtype=torch.uint8, device=dev)

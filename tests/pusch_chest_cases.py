@@ -7,8 +7,11 @@ import pusch_chest_oracle as C
 from pusch_demod_cases import bf16
 
 
-def random_case(rng, grid_prb, nof_rx_ports=None, nof_rb=None, dmrs_type2=None, snr_db=None, dmrs_mask=None):
-    """Returns (cfg, grid (P, 14, nsc, 2) bf16, true channel (P, nsc) complex)."""
+def random_case(rng, grid_prb, nof_rx_ports=None, nof_rb=None, dmrs_type2=None, snr_db=None, dmrs_mask=None,
+                cfo_hz=0.0, delay=0.0, numerology=1):
+    """Returns (cfg, grid (P, 14, nsc, 2) bf16, true channel (P, nsc) complex). cfo_hz rotates OFDM symbol l by
+    2 pi cfo t_l (t_l: the symbol's start epoch); delay (in samples of a 4096-point DFT, may be negative) shifts every
+    path."""
     P = int(nof_rx_ports or rng.integers(1, 5))
     nrb = int(nof_rb or rng.integers(1, grid_prb + 1))
     rb0 = int(rng.integers(0, grid_prb - nrb + 1))
@@ -28,7 +31,7 @@ def random_case(rng, grid_prb, nof_rx_ports=None, nof_rb=None, dmrs_type2=None, 
     for p in range(P):
         for _ in range(4):
             tau = rng.uniform(0, 40)
-            H[p] += (rng.normal() + 1j * rng.normal()) / np.sqrt(8) * np.exp(-2j * np.pi * k * tau / 4096)
+            H[p] += (rng.normal() + 1j * rng.normal()) / np.sqrt(8) * np.exp(-2j * np.pi * k * (tau + delay) / 4096)
     snr = float(snr_db if snr_db is not None else rng.uniform(5, 35))
     nv = 10 ** (-snr / 10)
     x = (rng.choice([-1, 1], (14, nsc)) + 1j * rng.choice([-1, 1], (14, nsc))) / np.sqrt(2)
@@ -38,7 +41,11 @@ def random_case(rng, grid_prb, nof_rx_ports=None, nof_rb=None, dmrs_type2=None, 
         if (dmrs_mask >> l) & 1:
             x[l, sc] = cfg["scaling"] * C.dmrs_sequence(cfg["slot"], l, cfg["scrambling_id"], cfg["n_scid"], t2, rb0,
                                                         nrb)
-    y = H[:, None, :] * x[None] + (rng.normal(size=(P, 14, nsc)) + 1j * rng.normal(size=(P, 14, nsc))) * np.sqrt(nv / 2)
+    y = H[:, None, :] * x[None]
+    if cfo_hz:
+        ep = C.symbol_start_epochs(numerology)
+        y = y * np.exp(2j * np.pi * cfo_hz / ((15 << numerology) * 1000.0) * ep)[None, :, None]
+    y = y + (rng.normal(size=(P, 14, nsc)) + 1j * rng.normal(size=(P, 14, nsc))) * np.sqrt(nv / 2)
     return cfg, bf16(y), H
 
 

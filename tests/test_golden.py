@@ -119,6 +119,34 @@ def test_pusch_chest_golden():
     assert n == 8
 
 
+# Stated tolerances of the CFO / TA / time-strategy fixtures (reference float32 + bf16 estimates vs the float64
+# restatement): estimates within CHEST_CFO_TOL[td] x RMS channel ("interpolate" extrapolates past the DM-RS symbols,
+# amplifying the reference's bf16 / float rounding), noise variance / RSRP / EPRE 1e-3 relative, CFO within 0.05 Hz,
+# time alignment within 2 Tc (the reference rounds to Tc).
+CHEST_CFO_TOL = {0: 1.5e-2, 1: 2.5e-2}
+T_C = 1.0 / (480000 * 4096)
+
+
+def test_pusch_chest_cfo_golden():
+    """The restatement against the reference's estimates with CFO estimation / compensation, time alignment and the
+    average / interpolate time strategies (tests/golden/pusch_chest_cfo.npz)."""
+    import pusch_chest_oracle as C
+    from ofdm_oracle import bf16_to_complex
+    n = 0
+    for cfg, fd, td, comp, grid, ce, stats in G.pusch_chest_cfo_cases():
+        ch, nv, rsrp, epre, ex = C.estimate(cfg, bf16_to_complex(grid), ["none", "mean", "filter"][fd],
+                                            ["average", "interpolate"][td], bool(comp))
+        k0, k1 = cfg["rb_start"] * 12, (cfg["rb_start"] + cfg["nof_rb"]) * 12
+        want = bf16_to_complex(ce)[:, :, k0:k1]
+        got = ch[:, :, k0:k1]
+        assert np.max(np.abs(got - want)) < CHEST_CFO_TOL[td] * np.sqrt(np.mean(np.abs(want) ** 2)), (n, cfg)
+        np.testing.assert_allclose(np.stack([nv, rsrp, epre]), stats[:3], rtol=1e-3)
+        np.testing.assert_allclose(ex["ta_s"], stats[3], atol=2 * T_C)
+        np.testing.assert_allclose(ex["cfo_hz"], stats[4], atol=0.05)  # NaN == NaN (one DM-RS symbol)
+        n += 1
+    assert n == 20
+
+
 def test_pdsch_dmrs_golden():
     """The PDSCH DM-RS restatement bit-exact against the reference's grids."""
     import pdsch_dmrs_oracle as M

@@ -254,12 +254,57 @@ def test_pusch_demodulator_oracle_vs_reference(ref, seed):
     assert d.max() <= 1 and np.mean(d > 0) < 0.05, (cfg, d.max(), np.mean(d > 0))
 
 
+@pytest.mark.parametrize("seed", range(24))
+def test_pusch_chest_cfo_ta_oracle_vs_reference(ref, seed):
+    """CFO estimation (compensated and not), time alignment and the interpolate time strategy of the restatement against
+    the reference (1..100 RB, 1-3 DM-RS symbols, CFO up to 2 kHz, delays up to +-30 samples of a 4096-point DFT):
+    estimates within 1.5e-2 (average) / 2.5e-2 (interpolate) x RMS, noise variance / RSRP 1e-3 relative, CFO within
+    0.05 Hz, TA within 2 Tc."""
+    import pusch_chest_oracle as C
+    from ofdm_oracle import bf16_to_complex
+    from pusch_chest_cases import random_case
+    rng = np.random.default_rng(1000 + seed)
+    nrb = [1, 2, 3, 4, 5, 24, 52, 100][seed % 8]
+    gp = max(24, nrb + 3)
+    td, comp, fd = seed % 2, (seed // 2) % 2, [2, 1, 0][(seed // 4) % 3]
+    cfg, grid, _ = random_case(rng, gp, nof_rb=nrb, dmrs_type2=0, cfo_hz=rng.uniform(-2000, 2000),
+                               delay=rng.uniform(-30, 30), snr_db=rng.uniform(5, 35))
+    ce, nv, rsrp, epre, ta, cfo = ref.pusch_chest(cfg, grid, gp, fd=fd, td=td, compensate_cfo=comp)
+    ch, nv_o, rsrp_o, epre_o, ex = C.estimate(cfg, bf16_to_complex(grid), ["none", "mean", "filter"][fd],
+                                              ["average", "interpolate"][td], bool(comp))
+    l0, l1 = cfg["start_symbol"], cfg["start_symbol"] + cfg["nof_symbols"]
+    k0, k1 = cfg["rb_start"] * 12, (cfg["rb_start"] + nrb) * 12
+    got, want = bf16_to_complex(ce)[:, l0:l1, k0:k1], ch[:, l0:l1, k0:k1]
+    assert np.max(np.abs(got - want)) < [1.5e-2, 2.5e-2][td] * np.sqrt(np.mean(np.abs(want) ** 2))
+    np.testing.assert_allclose(nv, nv_o, rtol=1e-3)
+    np.testing.assert_allclose(rsrp, rsrp_o, rtol=1e-3)
+    np.testing.assert_allclose(cfo, ex["cfo_hz"], atol=0.05)
+    np.testing.assert_allclose(ta, ex["ta_s"], atol=2 / (480000 * 4096))
+
+
+def test_pusch_chest_type2_reference_is_undefined(ref):
+    """Type-2 PUSCH DM-RS in the reference is undefined behaviour, so it cannot pin type 2: configure_interpolator
+    (port_channel_estimator_helpers.cpp:296) derives stride 1 from the type-2 RE pattern {0, 1, 6, 7}, so
+    interpolator_linear_impl reads 12 x nof_rb values from a buffer of 4 x nof_rb pilots; with the "filter" smoothing and
+    >= 2 RB filter_type (:83) also writes 2 x floor(nof_coefs / 2) + 1 > 15 tail-correction coefficients into its
+    15-element array (the stack-smashing abort). Here, with "mean" smoothing (no filter_type), the reference returns
+    estimates that are not the constant its own mean strategy computes."""
+    from ofdm_oracle import bf16_to_complex
+    from pusch_chest_cases import random_case
+    rng = np.random.default_rng(4)
+    cfg, grid, _ = random_case(rng, 24, nof_rb=4, dmrs_type2=1)
+    ce = ref.pusch_chest(cfg, grid, 24, fd=1)[0]
+    k0 = cfg["rb_start"] * 12
+    row = bf16_to_complex(ce)[0, cfg["start_symbol"], k0:k0 + 48]
+    assert not np.allclose(row, row[0], rtol=1e-2, atol=0)
+
+
 @pytest.mark.parametrize("seed", range(14))
 def test_pusch_chest_oracle_vs_reference(ref, seed):
     """DM-RS channel estimator restatement (float64) against the reference's dmrs_pusch_estimator_impl (float32, bf16
     output): estimates on the allocated REs within 1e-2 of the RMS channel magnitude, noise variance / RSRP / EPRE within
-    1e-3 relative, for the filter (default), mean and none smoothing strategies and 1..24 RBs, DM-RS type 1 (the
-    reference build aborts with a stack overrun on type-2 PUSCH DM-RS, so type 2 is unpinned)."""
+    1e-3 relative, for the filter (default), mean and none smoothing strategies and 1..24 RBs, DM-RS type 1 (type-2
+    PUSCH DM-RS is undefined behaviour in the reference: test_pusch_chest_type2_reference_is_undefined)."""
     import pusch_chest_oracle as C
     from ofdm_oracle import bf16_to_complex
     from pusch_chest_cases import random_case

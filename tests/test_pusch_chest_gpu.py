@@ -24,13 +24,20 @@ def ctx():
     return srsgpu.Context(0)
 
 
-def to_est(cfg, fd=2, layers=1):
+def to_est(cfg, fd=2, layers=1, td=0, comp=0, layout=0):
     import srsgpu
     return srsgpu.PuschChannelEstimation(
         scrambling_id=cfg["scrambling_id"], n_scid=cfg["n_scid"], dmrs_type=2 if cfg["dmrs_type2"] else 1,
         nof_tx_layers=layers, nof_rx_ports=cfg["nof_rx_ports"], start_symbol=cfg["start_symbol"],
         nof_symbols=cfg["nof_symbols"], dmrs_symbol_mask=cfg["dmrs_symbol_mask"], rb_start=cfg["rb_start"],
-        nof_rb=cfg["nof_rb"], slot_index=cfg["slot"], scaling=cfg["scaling"], fd_smoothing=fd)
+        nof_rb=cfg["nof_rb"], slot_index=cfg["slot"], scaling=cfg["scaling"], fd_smoothing=fd, td_strategy=td,
+        compensate_cfo=comp, estimate_layout=layout)
+
+
+# Stated tolerances with CFO / TA / interpolate (see tests/test_golden.py): estimates within CFO_TOL[td] x RMS channel,
+# noise variance / RSRP / EPRE 1e-3 relative, CFO 0.05 Hz, time alignment 2 Tc.
+CFO_TOL = {0: 1.5e-2, 1: 2.5e-2}
+T_C = 1.0 / (480000 * 4096)
 
 
 def pad4(grid):
@@ -116,6 +123,89 @@ def test_pusch_chest_shared_slot_100mhz(ctx):
         w = ch[:, ls, ks]
         assert np.max(np.abs(got - w)) < 1e-2 * np.sqrt(np.mean(np.abs(w) ** 2)), i
         np.testing.assert_allclose(nv[i], nvo, rtol=1e-3)
+
+
+def test_pusch_chest_cfo_ta_golden(ctx):
+    """The reference's estimates with CFO estimation / compensation, time alignment and both time-domain strategies
+    (tests/golden/pusch_chest_cfo.npz: du_low's default filter + average + CFO compensation, and the alternatives),
+    every case in ONE plan: estimates, noise variance / RSRP / EPRE, TA and CFO within the stated tolerances."""
+    import srsgpu
+    cases = list(G.pusch_chest_cfo_cases())
+    grids = np.stack([pad4(c[4]) for c in cases])
+    ests = [to_est(cfg, fd, 1, td, comp) for cfg, fd, td, comp, _, _, _ in cases]
+    ce, nv, m = srsgpu.PuschChannelEstimator(ctx, 64, 4).estimate_batch(grids, ests, list(range(len(cases))))
+    for i, (cfg, fd, td, comp, _, want, stats) in enumerate(cases):
+        P = cfg["nof_rx_ports"]
+        ks = slice(cfg["rb_start"] * 12, (cfg["rb_start"] + cfg["nof_rb"]) * 12)
+        got = bf16_to_complex(ce[i, 0, :P])[:, :, ks]
+        w = bf16_to_complex(want)[:, :, ks]
+        assert np.max(np.abs(got - w)) < CFO_TOL[td] * np.sqrt(np.mean(np.abs(w) ** 2)), (i, cfg, td, comp)
+        np.testing.assert_allclose(nv[i, :P], stats[0], rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 0], stats[1], rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 1], stats[2], rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 4], stats[3], atol=2 * T_C)
+        np.testing.assert_allclose(m[i, :P, 5], stats[4], atol=0.05)
+
+
+def test_pusch_chest_cfo_ta_random_vs_oracle(ctx):
+    """48 random transmissions with CFO and delay (1..100 RB, 1-3 DM-RS symbols, every smoothing, both time
+    strategies, compensation on / off), ONE plan, against the restatement within the stated tolerances."""
+    import srsgpu
+    rng = np.random.default_rng(78)
+    cases, opts = [], []
+    for i in range(48):
+        nrb = [1, 2, 3, 5, 12, 24, 52, 100][i % 8]
+        cases.append(random_case(rng, 104, nof_rb=nrb, dmrs_type2=0, cfo_hz=rng.uniform(-2000, 2000),
+                                 delay=rng.uniform(-30, 30)))
+        opts.append((int(rng.integers(0, 3)), i % 2, (i // 2) % 2))
+    grids = np.stack([pad4(g) for _, g, _ in cases])
+    ests = [to_est(cfg, fd, 1, td, comp) for (cfg, _, _), (fd, td, comp) in zip(cases, opts)]
+    ce, nv, m = srsgpu.PuschChannelEstimator(ctx, 104, 4).estimate_batch(grids, ests, list(range(len(cases))))
+    for i, ((cfg, grid, _), (fd, td, comp)) in enumerate(zip(cases, opts)):
+        P = cfg["nof_rx_ports"]
+        ch, nvo, rsrp, epre, ex = C.estimate(cfg, bf16_to_complex(grid), ["none", "mean", "filter"][fd],
+                                             ["average", "interpolate"][td], bool(comp))
+        ls, ks = region(cfg)
+        got = bf16_to_complex(ce[i, 0, :P])[:, ls, ks]
+        w = ch[:, ls, ks]
+        assert np.max(np.abs(got - w)) < CFO_TOL[td] * np.sqrt(np.mean(np.abs(w) ** 2)), (i, cfg, fd, td, comp)
+        np.testing.assert_allclose(nv[i, :P], nvo, rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 0], rsrp, rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 4], ex["ta_s"], atol=2 * T_C)
+        np.testing.assert_allclose(m[i, :P, 5], ex["cfo_hz"], atol=0.05)
+
+
+def test_pusch_compact_cfo_equals_per_symbol(ctx):
+    """Compact layout with CFO compensation (the demodulator rotates each symbol's estimate) gives the LLRs of the
+    per-symbol layout (the estimator rotates), bit for bit: 1-4 layers, 4 rx ports, DM-RS in symbols 2 and 11."""
+    import torch
+    import srsgpu
+    rng = np.random.default_rng(12)
+    dev = torch.device("cuda", 0)
+    for L in (1, 2, 4):
+        cfg, grid, _ = multilayer_case(rng, 24, L, 4, 16, rb_start=3, dmrs_mask=(1 << 2) | (1 << 11)) if L > 1 else \
+            random_case(rng, 24, nof_rx_ports=4, nof_rb=16, dmrs_type2=0, dmrs_mask=(1 << 2) | (1 << 11),
+                        cfo_hz=700.0)[:2] + (None,)
+        cfg.update(start_symbol=0, nof_symbols=14)
+        g4 = torch.from_numpy(pad4(grid).view(np.int32).reshape(-1).copy()).to(dev)
+        outs = []
+        for layout in (srsgpu.CE_PER_SYMBOL, srsgpu.CE_COMPACT):
+            est = srsgpu.PuschChannelEstimatorPlan(
+                ctx, srsgpu.make_pusch_chest_configs([to_est(cfg, 2, L, 0, 1, layout)], [0]), 24, 4)
+            arr, _, total = srsgpu.make_pusch_demod_configs([srsgpu.PuschDemodulation(
+                rnti=0x4601, n_id=77, modulation_order=6, nof_tx_layers=L, nof_rx_ports=4, start_symbol=0,
+                nof_symbols=14, dmrs_symbol_mask=cfg["dmrs_symbol_mask"], dmrs_type=1, nof_cdm_groups_without_data=2,
+                rb_start=cfg["rb_start"], nof_rb=cfg["nof_rb"], equalizer=srsgpu.EQ_MMSE if L > 2 else srsgpu.EQ_ZF,
+                estimate_layout=layout, cfo_compensated=1)], [0])
+            dem = srsgpu.PuschDemodulatorPlan(ctx, arr, 24, 4)
+            d_ce = torch.zeros(4 * 4 * 14 * 288, dtype=torch.int32, device=dev)
+            d_nv = torch.zeros(4, dtype=torch.float32, device=dev)
+            d_llr = torch.zeros(total, dtype=torch.int8, device=dev)
+            est.execute(g4, d_ce, d_nv)
+            dem.execute(g4, d_ce, d_nv, d_llr)
+            torch.cuda.synchronize()
+            outs.append(d_llr.cpu().numpy())
+        assert np.array_equal(outs[0], outs[1]), (L, np.mean(outs[0] != outs[1]))
 
 
 @pytest.mark.parametrize("L", [2, 4])

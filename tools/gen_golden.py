@@ -227,6 +227,32 @@ def gen_pusch_chest(ref, rng):
     np.savez_compressed(os.path.join(OUT, "pusch_chest.npz"), **out)
 
 
+def gen_pusch_chest_cfo(ref, rng):
+    """Reference DM-RS channel estimates with CFO estimation (compensated or not), time alignment and both time-domain
+    strategies (average, interpolate), DM-RS type 1 with 2-4 DM-RS symbols (and one 1-symbol case per strategy), on
+    received grids rotated by a carrier frequency offset and delayed: du_low's default configuration (filter, average,
+    CFO compensation: du_low_config.h:51-69) and its alternatives."""
+    from pusch_chest_cases import random_case
+    out = {}
+    masks = [(1 << 2) | (1 << 11), (1 << 2) | (1 << 7) | (1 << 11), (1 << 2) | (1 << 5) | (1 << 8) | (1 << 11),
+             (1 << 3) | (1 << 9), 1 << 2]
+    i = 0
+    for td in (0, 1):
+        for comp in (1, 0):
+            for j, (nrb, fd) in enumerate([(4, 2), (24, 2), (1, 2), (7, 1), (52, 0)]):
+                mask = masks[(j + td + comp) % len(masks)]
+                cfg, grid, _ = random_case(rng, 64, nof_rb=nrb, dmrs_type2=0, dmrs_mask=mask,
+                                           cfo_hz=float(rng.uniform(-1500, 1500)), delay=float(rng.uniform(-25, 25)))
+                cfg["start_symbol"], cfg["nof_symbols"] = 0, 14
+                ce, nv, rsrp, epre, ta, cfo = ref.pusch_chest(cfg, grid, 64, fd=fd, td=td, compensate_cfo=bool(comp))
+                out[f"case{i}_cfg"] = np.array([cfg[k] for k in PUSCH_CHEST_KEYS] + [fd, td, comp], np.int64)
+                out[f"case{i}_scaling"] = np.float32(cfg["scaling"])
+                out[f"case{i}_grid"], out[f"case{i}_ch_est"] = grid, ce
+                out[f"case{i}_stats"] = np.stack([nv, rsrp, epre, ta, cfo])
+                i += 1
+    np.savez_compressed(os.path.join(OUT, "pusch_chest_cfo.npz"), **out)
+
+
 def gen_pdsch_dmrs(ref, rng):
     """Reference PDSCH DM-RS grids (dmrs_pdsch_processor_impl) of random configurations in 24-PRB grids."""
     from pdsch_dmrs_cases import random_config
@@ -255,7 +281,7 @@ def main():
     ref = Reference()
     if len(sys.argv) > 1:  # regenerate only the named fixture sets, e.g. `python tools/gen_golden.py ofdm`
         for name in sys.argv[1:]:
-            seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18, "pdsch_dmrs": 19}[name]
+            seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18, "pdsch_dmrs": 19, "pusch_chest_cfo": 20}[name]
             globals()["gen_" + name](ref, np.random.default_rng(seed))
         return
     gen_crc(ref, np.random.default_rng(10))
@@ -268,6 +294,7 @@ def main():
     gen_pusch_demod(ref, np.random.default_rng(17))
     gen_pusch_chest(ref, np.random.default_rng(18))
     gen_pdsch_dmrs(ref, np.random.default_rng(19))
+    gen_pusch_chest_cfo(ref, np.random.default_rng(20))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

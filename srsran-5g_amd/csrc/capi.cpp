@@ -59,6 +59,7 @@ bool crc_params(int poly, unsigned& order, uint64_t& g)
 } // namespace
 
 struct srsgpu_pusch_cb_plan {
+  std::vector<crc_key>      crc_refs;  ///< CRC tables referenced (top-level plans only).
   srsgpu_context*           ctx     = nullptr;
   int                       impl    = SRSGPU_LDPC_IMPL_SIMD;
   dm_desc*                  d_dm    = nullptr;
@@ -67,6 +68,7 @@ struct srsgpu_pusch_cb_plan {
 };
 
 struct srsgpu_pdsch_encoder_plan {
+  std::vector<crc_key> crc_refs;  ///< CRC tables referenced.
   mutable stage_timer timer;
   srsgpu_context* ctx        = nullptr;
   tb_crc_desc*    d_tb       = nullptr;
@@ -82,6 +84,7 @@ struct srsgpu_pdsch_encoder_plan {
 };
 
 struct srsgpu_pusch_decoder_plan {
+  std::vector<crc_key>  crc_refs;   ///< CRC tables referenced.
   mutable stage_timer   timer;      ///< Three stages (enable_timing 1).
   mutable stage_timer   timer_dec;  ///< The decoding stage only (enable_timing 2): two events per execute.
   srsgpu_context*       ctx     = nullptr;
@@ -91,6 +94,7 @@ struct srsgpu_pusch_decoder_plan {
 };
 
 struct srsgpu_ldpc_decoder_plan {
+  std::vector<crc_key> crc_refs;  ///< CRC tables referenced (top-level plans only).
   /// One kernel launch per (base graph, kernel, layer bound): even lifting sizes go to the packed two-rows-per-lane
   /// kernel (64 * ceil(Z / 128) lanes) built for at most max_layers layers, odd ones to the one-row-per-lane kernel
   /// (64 * ceil(Z / 64) lanes).
@@ -110,14 +114,84 @@ struct srsgpu_ldpc_decoder_plan {
 
 namespace {
 
+/// Returns an arena block to the free list, merged with its free neighbours.
+void crc_free_block(srsgpu_context* ctx, size_t off, size_t len)
+{
+  auto next = ctx->crc_free.lower_bound(off);
+  if (next != ctx->crc_free.end() && next->first == off + len) {
+    len += next->second;
+    next = ctx->crc_free.erase(next);
+  }
+  if (next != ctx->crc_free.begin()) {
+    auto prev = std::prev(next);
+    if (prev->first + prev->second == off) {
+      off = prev->first;
+      len += prev->second;
+      ctx->crc_free.erase(prev);
+    }
+  }
+  ctx->crc_free.emplace(off, len);
+}
+
+/// First-fit allocation of `words` arena words; evicts unreferenced cached tables (least recently used first) when
+/// nothing fits and `evict` is set. Returns false when the arena cannot hold them (or, for optional tables, when
+/// placing them would leave less than `keep_free` words).
+bool crc_alloc(srsgpu_context* ctx, size_t words, size_t keep_free, bool evict, size_t& offset)
+{
+  auto free_words = [ctx]() {
+    size_t n = 0;
+    for (const auto& b : ctx->crc_free) {
+      n += b.second;
+    }
+    return n;
+  };
+  for (;;) {
+    if (free_words() >= words + keep_free) {
+      for (auto it = ctx->crc_free.begin(); it != ctx->crc_free.end(); ++it) {
+        if (it->second >= words) {
+          offset                = it->first;
+          const size_t rest     = it->second - words;
+          ctx->crc_free.erase(it);
+          if (rest > 0) {
+            ctx->crc_free.emplace(offset + words, rest);
+          }
+          return true;
+        }
+      }
+    }
+    if (!evict) {
+      return false;
+    }
+    auto victim = ctx->crc_tables.end();
+    for (auto it = ctx->crc_tables.begin(); it != ctx->crc_tables.end(); ++it) {
+      if (it->second.refs == 0 && (victim == ctx->crc_tables.end() || it->second.last_use < victim->second.last_use)) {
+        victim = it;
+      }
+    }
+    if (victim == ctx->crc_tables.end()) {
+      return false;
+    }
+    const size_t off = victim->second.offset, len = victim->second.words;
+    ctx->crc_tables.erase(victim);
+    crc_free_block(ctx, off, len);
+  }
+}
+
 /// Contribution table of every message bit to the CRC remainder: P[i] = x^(order + L - 1 - i) mod g(x), so that
 /// CRC(m) = XOR of P[i] over the set bits m_i (the calculate() of crc_calculator_generic_impl.cpp:136 is linear).
-int get_crc_table(srsgpu_context* ctx, int poly, int L, uint32_t& offset)
+/// The caller's plan takes a reference (refs) released with the plan. Optional tables (fast paths with a fallback)
+/// never evict and leave CRC_ARENA_RESERVE words for required ones, so a long-running cell with link adaptation keeps
+/// finding room for its codeblock tables (unreferenced tables are evicted for them).
+int get_crc_table(srsgpu_context* ctx, int poly, int L, uint32_t& offset, std::vector<crc_key>& refs,
+                  bool optional = false)
 {
-  auto key = std::make_pair(poly, L);
-  auto it  = ctx->crc_tables.find(key);
+  const crc_key key(poly, L);
+  auto          it = ctx->crc_tables.find(key);
   if (it != ctx->crc_tables.end()) {
-    offset = static_cast<uint32_t>(it->second);
+    ++it->second.refs;
+    it->second.last_use = ++ctx->crc_clock;
+    refs.push_back(key);
+    offset = static_cast<uint32_t>(it->second.offset);
     return SRSGPU_OK;
   }
   unsigned order;
@@ -125,12 +199,14 @@ int get_crc_table(srsgpu_context* ctx, int poly, int L, uint32_t& offset)
   if (!crc_params(poly, order, g)) {
     return fail(SRSGPU_ERR_INVALID_ARG, "invalid CRC polynomial %d", poly);
   }
-  // Tables start 16-byte aligned and are padded to whole 16-byte vectors (the decoder copies them with 16-B loads).
-  ctx->crc_used = (ctx->crc_used + 3u) & ~static_cast<size_t>(3u);
-  if (ctx->crc_used + ((static_cast<size_t>(L) + 3u) & ~static_cast<size_t>(3u)) > CRC_ARENA_WORDS) {
-    return fail(SRSGPU_ERR_NO_MEMORY, "CRC table arena exhausted");
+  // Tables start 16-byte aligned and are padded to whole 16-byte vectors (the decoder copies them with 16-B loads):
+  // every block is a multiple of 4 words, so every offset is too.
+  const size_t words = (static_cast<size_t>(L) + 3u) & ~static_cast<size_t>(3u);
+  size_t       off   = 0;
+  if (!crc_alloc(ctx, words, optional ? CRC_ARENA_RESERVE : 0, !optional, off)) {
+    return optional ? SRSGPU_ERR_NO_MEMORY : fail(SRSGPU_ERR_NO_MEMORY, "CRC table arena exhausted");
   }
-  std::vector<uint32_t> tab(static_cast<size_t>(L));
+  std::vector<uint32_t> tab(words, 0u);
   const uint64_t        high = 1ULL << order;
   uint64_t              r    = 1;
   for (unsigned k = 0; k < order; ++k) {
@@ -146,26 +222,28 @@ int get_crc_table(srsgpu_context* ctx, int poly, int L, uint32_t& offset)
       r ^= g;
     }
   }
-  HIP_TRY(hipMemcpy(ctx->d_crc_arena + ctx->crc_used, tab.data(), tab.size() * sizeof(uint32_t),
-                    hipMemcpyHostToDevice));
-  offset = static_cast<uint32_t>(ctx->crc_used);
-  ctx->crc_tables.emplace(key, ctx->crc_used);
-  ctx->crc_used += static_cast<size_t>(L);
+  if (hipMemcpy(ctx->d_crc_arena + off, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
+      hipSuccess) {
+    crc_free_block(ctx, off, words);
+    return fail(SRSGPU_ERR_HIP, "CRC table upload failed");
+  }
+  crc_entry e;
+  e.offset   = off;
+  e.words    = words;
+  e.refs     = 1;
+  e.last_use = ++ctx->crc_clock;
+  ctx->crc_tables.emplace(key, e);
+  refs.push_back(key);
+  offset = static_cast<uint32_t>(off);
   return SRSGPU_OK;
 }
 
-/// Contribution table for an optional fast path: its arena offset, or NO_CRC_TABLE (no error) when the arena has no
-/// room left for it.
-uint32_t try_crc_table(srsgpu_context* ctx, int poly, int L)
+/// Contribution table for an optional fast path: its arena offset, or NO_CRC_TABLE (no error) when it would eat into
+/// the reserve kept for required tables.
+uint32_t try_crc_table(srsgpu_context* ctx, int poly, int L, std::vector<crc_key>& refs)
 {
-  const auto key = std::make_pair(poly, L);
-  if (ctx->crc_tables.find(key) == ctx->crc_tables.end() &&
-      ((ctx->crc_used + 3u) & ~static_cast<size_t>(3u)) + ((static_cast<size_t>(L) + 3u) & ~static_cast<size_t>(3u)) >
-          CRC_ARENA_WORDS) {
-    return NO_CRC_TABLE;
-  }
   uint32_t off = NO_CRC_TABLE;
-  return get_crc_table(ctx, poly, L, off) == SRSGPU_OK ? off : NO_CRC_TABLE;
+  return get_crc_table(ctx, poly, L, off, refs, true) == SRSGPU_OK ? off : NO_CRC_TABLE;
 }
 
 /// Solves the core of the lifted base graph (rows 0..3 x parity columns K..K+3) once per (BG, Z), like
@@ -377,6 +455,7 @@ using dec_key = std::tuple<int, bool, int>;  ///< (base graph, packed kernel, la
 struct dec_batch {
   std::map<dec_key, std::vector<dec_desc>> groups;
   std::map<dec_key, int>                   threads;
+  std::vector<crc_key>*                    crc_refs = nullptr;  ///< The creating call's crc_ref_guard.
 };
 
 /// Upper bound of the number of layers decode() uses for an input of nof_llrs LLRs (ldpc_decoder_impl.cpp:110: the
@@ -448,7 +527,7 @@ int add_decoder_cb(srsgpu_context* ctx,
   d.cb_index = i;
   d.flags    = 0;
   if (crc_poly != SRSGPU_CRC_NONE) {
-    int r = get_crc_table(ctx, crc_poly, K * Z - nof_filler, d.crc_table);
+    int r = get_crc_table(ctx, crc_poly, K * Z - nof_filler, d.crc_table, *batch.crc_refs);
     if (r != SRSGPU_OK) {
       return r;
     }
@@ -652,7 +731,9 @@ int srsgpu_ldpc_decoder_plan_create(srsgpu_context*                   ctx,
   }
   std::lock_guard<std::mutex> lock(ctx->mtx);
   HIP_TRY(hipSetDevice(ctx->device));
-  dec_batch batch;
+  crc_ref_guard guard(ctx);
+  dec_batch     batch;
+  batch.crc_refs = &guard.refs;
   for (uint32_t i = 0; i < nof_cbs; ++i) {
     const srsgpu_ldpc_decoder_config& c = cfgs[i];
     int r = add_decoder_cb(ctx, i, c.base_graph, c.lifting_size, c.nof_filler_bits, c.nof_crc_bits, c.max_iterations,
@@ -662,7 +743,11 @@ int srsgpu_ldpc_decoder_plan_create(srsgpu_context*                   ctx,
       return r;
     }
   }
-  return upload_decoder_plan(ctx, impl, batch, plan_out);
+  const int r = upload_decoder_plan(ctx, impl, batch, plan_out);
+  if (r == SRSGPU_OK) {
+    guard.commit((*plan_out)->crc_refs);
+  }
+  return r;
 }
 
 int srsgpu_ldpc_decoder_plan_execute(const srsgpu_ldpc_decoder_plan* plan,
@@ -681,6 +766,10 @@ void srsgpu_ldpc_decoder_plan_destroy(srsgpu_ldpc_decoder_plan* plan)
 {
   if (plan == nullptr) {
     return;
+  }
+  if (!plan->crc_refs.empty()) {
+    std::lock_guard<std::mutex> lock(plan->ctx->mtx);
+    crc_release_locked(plan->ctx, plan->crc_refs);
   }
   for (auto& g : plan->groups) {
     if (g.d_desc != nullptr) {
@@ -730,7 +819,9 @@ int srsgpu_pusch_cb_plan_create(srsgpu_context*               ctx,
   }
   std::lock_guard<std::mutex> lock(ctx->mtx);
   HIP_TRY(hipSetDevice(ctx->device));
+  crc_ref_guard        guard(ctx);
   dec_batch            batch;
+  batch.crc_refs = &guard.refs;
   std::vector<dm_desc> dms;
   for (uint32_t i = 0; i < nof_cbs; ++i) {
     const srsgpu_pusch_cb_config& c = cfgs[i];
@@ -742,7 +833,11 @@ int srsgpu_pusch_cb_plan_create(srsgpu_context*               ctx,
       return r;
     }
   }
-  return upload_pusch_cb_plan(ctx, impl, batch, dms, plan_out);
+  const int r = upload_pusch_cb_plan(ctx, impl, batch, dms, plan_out);
+  if (r == SRSGPU_OK) {
+    guard.commit((*plan_out)->crc_refs);
+  }
+  return r;
 }
 
 int srsgpu_pusch_cb_plan_execute(const srsgpu_pusch_cb_plan* plan,
@@ -765,6 +860,10 @@ void srsgpu_pusch_cb_plan_destroy(srsgpu_pusch_cb_plan* plan)
   if (plan == nullptr) {
     return;
   }
+  if (!plan->crc_refs.empty()) {
+    std::lock_guard<std::mutex> lock(plan->ctx->mtx);
+    crc_release_locked(plan->ctx, plan->crc_refs);
+  }
   if (plan->d_dm != nullptr) {
     (void)hipFree(plan->d_dm);
   }
@@ -783,6 +882,7 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
   }
   std::lock_guard<std::mutex> lock(ctx->mtx);
   HIP_TRY(hipSetDevice(ctx->device));
+  crc_ref_guard            guard(ctx);
   static const double      shift_bg1[4] = {0, 17, 33, 56};  // ldpc_rate_matcher_impl.cpp:34
   static const double      shift_bg2[4] = {0, 13, 25, 43};
   std::vector<tb_crc_desc> tbd(nof_tbs);
@@ -808,7 +908,7 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
               static_cast<uint32_t>(seg.tb_crc_len), NO_CRC_TABLE};
     // TB CRC from a per-bit table (cached per length); when the arena is full the kernel uses the byte-table method.
     tbd[t].table = try_crc_table(ctx, seg.tb_crc_len == 24 ? SRSGPU_CRC24A : SRSGPU_CRC16,
-                                 static_cast<int>(c.tbs_bytes) * 8);
+                                 static_cast<int>(c.tbs_bytes) * 8, guard.refs);
     const int Z    = seg.Z;
     const int pos  = lifting_position(Z);
     const int N    = (((seg.bg == 1) ? kBG1_N_FULL : kBG2_N_FULL) - 2) * Z;
@@ -824,7 +924,7 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
     const int V     = Ncb - seg.filler;
     uint32_t  crc_tab = NO_CRC_TABLE;
     if (seg.cb_crc_len > 0) {
-      int r = get_crc_table(ctx, SRSGPU_CRC24B, seg.cbs[0].used, crc_tab);
+      int r = get_crc_table(ctx, SRSGPU_CRC24B, seg.cbs[0].used, crc_tab, guard.refs);
       if (r != SRSGPU_OK) {
         return r;
       }
@@ -897,6 +997,7 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
   }
   plan->inline_tb_crc = plan->count[0] == 0 && plan->count[1] == 0 &&
                         std::all_of(tbd.begin(), tbd.end(), [](const tb_crc_desc& t) { return t.table != NO_CRC_TABLE; });
+  guard.commit(plan->crc_refs);
   *plan_out = plan;
   return SRSGPU_OK;
 }
@@ -972,6 +1073,10 @@ void srsgpu_pdsch_encoder_plan_destroy(srsgpu_pdsch_encoder_plan* plan)
   if (plan == nullptr) {
     return;
   }
+  if (!plan->crc_refs.empty()) {
+    std::lock_guard<std::mutex> lock(plan->ctx->mtx);
+    crc_release_locked(plan->ctx, plan->crc_refs);
+  }
   for (void* p : {static_cast<void*>(plan->d_tb), static_cast<void*>(plan->d_tb_crc), static_cast<void*>(plan->d_enc[0]),
                   static_cast<void*>(plan->d_enc[1])}) {
     if (p != nullptr) {
@@ -996,7 +1101,9 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
   }
   std::lock_guard<std::mutex> lock(ctx->mtx);
   HIP_TRY(hipSetDevice(ctx->device));
+  crc_ref_guard            guard(ctx);
   dec_batch                batch;
+  batch.crc_refs = &guard.refs;
   std::vector<dm_desc>     dms;
   std::vector<tb_dec_desc> tbs(nof_tbs);
   for (uint32_t t = 0; t < nof_tbs; ++t) {
@@ -1031,7 +1138,7 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
     d.data_magic   = static_cast<uint32_t>(((1ULL << 32) + d.cb_data_bits - 1) / d.cb_data_bits);
     d.tb_offset    = c.tb_offset;
     d.tb_index     = t;
-    d.crc_table    = (seg.C > 1) ? try_crc_table(ctx, SRSGPU_CRC24A, seg.tbs) : NO_CRC_TABLE;
+    d.crc_table    = (seg.C > 1) ? try_crc_table(ctx, SRSGPU_CRC24A, seg.tbs, guard.refs) : NO_CRC_TABLE;
   }
   auto* plan    = new srsgpu_pusch_decoder_plan();
   plan->ctx     = ctx;
@@ -1047,6 +1154,7 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
     srsgpu_pusch_decoder_plan_destroy(plan);
     return fail(SRSGPU_ERR_HIP, "failed to upload transport block descriptors");
   }
+  guard.commit(plan->crc_refs);
   *plan_out = plan;
   return SRSGPU_OK;
 }
@@ -1128,6 +1236,10 @@ void srsgpu_pusch_decoder_plan_destroy(srsgpu_pusch_decoder_plan* plan)
 {
   if (plan == nullptr) {
     return;
+  }
+  if (!plan->crc_refs.empty()) {
+    std::lock_guard<std::mutex> lock(plan->ctx->mtx);
+    crc_release_locked(plan->ctx, plan->crc_refs);
   }
   srsgpu_pusch_cb_plan_destroy(plan->cbs);
   if (plan->d_tb != nullptr) {

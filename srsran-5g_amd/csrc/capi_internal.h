@@ -38,6 +38,19 @@ inline int fail(int code, const char* fmt, ...)
   } while (0)
 
 constexpr size_t CRC_ARENA_WORDS = 16u << 20;  // 64 MiB of contribution tables
+/// Optional (fast-path) tables are only placed while at least this many arena words stay free for required ones.
+constexpr size_t CRC_ARENA_RESERVE = CRC_ARENA_WORDS / 4;
+
+using crc_key = std::pair<int, int>;  ///< (polynomial, message length)
+
+/// One contribution table in the arena: referenced by live plans (refs) or cached for reuse (refs == 0, evictable
+/// least recently used first when an allocation does not fit).
+struct crc_entry {
+  size_t   offset   = 0;
+  size_t   words    = 0;
+  int      refs     = 0;
+  uint64_t last_use = 0;
+};
 
 } // namespace srsgpu
 
@@ -50,8 +63,9 @@ struct srsgpu_context {
   srsgpu::core_plan*                   d_core[2]   = {nullptr, nullptr};
   std::vector<srsgpu::core_plan>       core[2];
   uint32_t*                            d_crc_arena = nullptr;
-  size_t                               crc_used    = 0;
-  std::map<std::pair<int, int>, size_t> crc_tables;
+  std::map<srsgpu::crc_key, srsgpu::crc_entry> crc_tables;
+  std::map<size_t, size_t>             crc_free = {{0, srsgpu::CRC_ARENA_WORDS}};  ///< Free blocks: offset -> words.
+  uint64_t                             crc_clock = 0;
   /// Gold-sequence jump tables of the scrambler (built on first use, see srsgpu::gold_tables): x1 words, x2 chunk
   /// jumps M^(Nc + 2048 c) and x2 lane jumps M^(32 i), each matrix as 31 column words.
   uint32_t*                            d_gold_x1      = nullptr;
@@ -63,6 +77,30 @@ struct srsgpu_context {
 };
 
 namespace srsgpu {
+/// Drops a plan's references on CRC contribution tables (caller holds ctx->mtx); the tables stay cached.
+inline void crc_release_locked(srsgpu_context* ctx, std::vector<crc_key>& refs)
+{
+  for (const crc_key& k : refs) {
+    auto it = ctx->crc_tables.find(k);
+    if (it != ctx->crc_tables.end() && it->second.refs > 0) {
+      --it->second.refs;
+    }
+  }
+  refs.clear();
+}
+
+/// Releases the references taken during a plan creation unless they are committed to the plan (caller holds the lock
+/// for the guard's whole life).
+struct crc_ref_guard {
+  srsgpu_context*      ctx;
+  std::vector<crc_key> refs;
+  explicit crc_ref_guard(srsgpu_context* c) : ctx(c) {}
+  crc_ref_guard(const crc_ref_guard&)            = delete;
+  crc_ref_guard& operator=(const crc_ref_guard&) = delete;
+  void commit(std::vector<crc_key>& dst) { dst.swap(refs); refs.clear(); }
+  ~crc_ref_guard() { crc_release_locked(ctx, refs); }
+};
+
 /// Builds and uploads the Gold-sequence jump tables into the context once (caller holds ctx->mtx); capi_pdsch_mod.cpp.
 int ensure_gold_tables(srsgpu_context* ctx);
 

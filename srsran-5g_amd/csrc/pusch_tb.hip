@@ -13,6 +13,14 @@
 namespace srsgpu {
 namespace {
 
+/// p / d with the magic m = ceil(2^32 / d): the high product never undershoots and overshoots by at most one once
+/// p * d >= 2^32 (TB bits up to ~1.3 M x codeblock bits up to 8448), so one correction makes it exact for every p.
+__device__ __forceinline__ uint32_t cb_index(uint32_t p, uint32_t d, uint32_t m)
+{
+  const uint32_t q = __umulhi(p, m);
+  return (q * d > p) ? q - 1u : q;
+}
+
 __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __restrict__ descs,
                                                        uint8_t* __restrict__ cb_crc_ok,
                                                        const uint8_t* __restrict__ cb_msgs,
@@ -66,7 +74,7 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
   if ((d.cb_data_bits & 7u) == 0) {
     const uint32_t cb_bytes = d.cb_data_bits / 8u;
     for (uint32_t b = threadIdx.x; b < bytes; b += blockDim.x) {
-      const uint32_t cb = __umulhi(8u * b, d.data_magic);
+      const uint32_t cb = cb_index(8u * b, d.cb_data_bits, d.data_magic);
       tb[b]             = msgs[cb * CB_MSG_STRIDE + (b - cb * cb_bytes)];
     }
   }
@@ -75,7 +83,7 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const uint32_t p  = 8u * b + static_cast<uint32_t>(k);
-      const uint32_t cb = __umulhi(p, d.data_magic);
+      const uint32_t cb = cb_index(p, d.cb_data_bits, d.data_magic);
       const uint32_t q  = p - cb * d.cb_data_bits;
       const uint8_t* m  = msgs + cb * CB_MSG_STRIDE;
       byte |= ((static_cast<uint32_t>(m[q >> 3]) >> (7u - (q & 7u))) & 1u) << (7 - k);

@@ -110,3 +110,44 @@ def test_pdsch_encoder_packed_kernel_every_lifting_size(ctx):
         del os.environ["SRSGPU_ENCODER_BYTE_KERNEL"]
     for a, b in zip(got, byte):
         assert np.array_equal(a, b)
+
+
+def test_crc_table_arena_long_running_cell(ctx):
+    """A long-running cell with link adaptation (advisor round 1): 60 PDSCH encoder + PUSCH decoder plans, each TB of
+    a distinct large size (its optional per-length TB CRC table is up to 1.2 M words of the 16 M-word arena), created
+    and destroyed, then 12 kept alive at once; plans needing new codeblock CRC lengths are still created (required
+    tables evict unreferenced cached ones, optional ones always leave a reserve) and still encode correctly."""
+    import srsgpu
+    from srsgpu import sch
+    orc = Oracle()
+
+    def nsym(nb):
+        return ((nb * 8 * 10 // 8 + 7) // 8 + 3) // 4 * 4  # G / Qm at code rate ~0.8, a multiple of the layers
+
+    for i in range(60):
+        nb = 150000 + 97 * i
+        arr, _, _, _ = srsgpu.make_pdsch_configs([nb], [srsgpu.PdschTransportBlock(1, 0, 8, 4, nsym(nb))])
+        srsgpu.PdschEncoderPlan(ctx, arr).close()
+        seg = sch.segment(nb * 8, 1, 8, 4, nsym(nb))
+        ul = srsgpu.PuschTransportBlock(nb, 1, 0, 8, 4, nsym(nb), new_data=True)
+        arr, *_ = srsgpu.make_pusch_tb_configs([ul], [seg.nof_segments],
+                                               [66 * seg.codeblocks[0].lifting_size])
+        srsgpu.PuschDecoderPlan(ctx, srsgpu.IMPL_SIMD, arr).close()
+    live = []
+    for i in range(12):
+        nb = 140000 + 89 * i
+        arr, _, _, _ = srsgpu.make_pdsch_configs([nb], [srsgpu.PdschTransportBlock(1, 0, 8, 4, nsym(nb))])
+        live.append(srsgpu.PdschEncoderPlan(ctx, arr))
+    rng = np.random.default_rng(3)
+    tbs, cfgs, want = [], [], []
+    for nb in (3007, 20013, 61005):  # new codeblock lengths
+        tb = rng.integers(0, 256, nb).astype(np.uint8)
+        cw, _, _ = oracle_pdsch_encode(orc, tb, 1, 0, 8, 4, 0, nsym(nb))
+        tbs.append(tb)
+        cfgs.append(srsgpu.PdschTransportBlock(1, 0, 8, 4, nsym(nb)))
+        want.append(cw)
+    got = srsgpu.PdschEncoder(ctx).encode_batch(tbs, cfgs)
+    for a, b in zip(got, want):
+        assert np.array_equal(a, b)
+    for p in live:
+        p.close()

@@ -164,3 +164,24 @@ def test_pusch_decoder_tb_level(orc, ctx):
                 n_ok += 1
             state[i] = new_st
         assert n_ok >= 10
+
+
+def test_pusch_decoder_large_unaligned_tbs(orc, ctx):
+    """A byte-aligned TBS outside the TS 38.214 tables, large enough that the codeblock index of a TB bit needs the
+    corrected magic division (526 344 bits: C = 63 codeblocks of 8 356 data bits, not byte-aligned, TB bit index x
+    codeblock bits >= 2^32): clean LLRs decode to the sent bytes with the TB CRC passing."""
+    import srsgpu
+    from srsgpu import sch
+    rng = np.random.default_rng(9)
+    tbs_bits = 526344
+    qm, layers, nsym = 8, 4, 73200  # G = 585 600 bits (code rate 0.9)
+    seg = sch.segment(tbs_bits, 1, qm, layers, nsym)
+    assert seg.nof_segments == 63 and (tbs_bits + 24) % (8 * 63) != 0
+    tb = rng.integers(0, 256, tbs_bits // 8).astype(np.uint8)
+    cw, _, _ = oracle_pdsch_encode(orc, tb, 1, 0, qm, layers, 0, nsym)
+    llr = bits_to_llrs(rng, cw, amp=10.0, noise=0.0)
+    dec = srsgpu.PuschDecoder(ctx, "avx2")
+    ok, got, iters = dec.decode_batch([llr], [srsgpu.PuschTransportBlock(tbs_bits // 8, 1, 0, qm, layers, nsym,
+                                                                         new_data=True, nof_ldpc_iterations=6)])
+    assert len(iters[0]) == 63 and ok[0], (len(iters[0]), ok[0])
+    assert np.array_equal(got[0], tb)

@@ -3,29 +3,43 @@
 
 BASELINE.json metric: "PDSCH+PUSCH slots/sec (100MHz 4x4) + LDPC info-bits/s at 1/2/4/8 GPU".
 Workload ("n78 100 MHz 4x4, 273 PRB, LDPC BG1, batched 64 UEs"): one slot = 64 UEs sharing 273 PRBs (4-5 PRB each),
-4 layers, 256QAM MCS 27 (table 2), one DM-RS symbol (type 1, 2 CDM groups without data) -> 64 transport blocks, 192
-LDPC BG1 codeblocks (Z 288/352), 1.258 Mbit of TB payload per direction. A step processes `--slots-per-step` such
-slots per GPU, both directions, on two HIP streams (as a gNB runs them concurrently):
+256QAM MCS 27 (table 2), DM-RS type 1 in symbols 2 and 11 (dmrs-AdditionalPosition pos1, two CDM groups without
+data). A step processes `--slots-per-step` such slots per GPU, both directions, on two HIP streams (as a gNB runs
+them concurrently):
 
-  * DL: PDSCH encoder (TB CRC, segmentation, CB CRC, LDPC, rate matching) -> PDSCH DM-RS -> PDSCH modulator
-    (scrambling, 256QAM, layer mapping, precoding, RE mapping, bf16 grid) -> OFDM modulator (4096-point DFT, CP,
-    phase compensation) of 4 ports: baseband samples.
-  * UL: OFDM demodulator of 4 rx ports -> DM-RS channel estimator (4 layers x 4 ports) -> PUSCH demodulator (4x4
-    MMSE, soft demapping, descrambling) -> PUSCH decoder (rate dematching, LDPC min-sum, 6 iterations max with CRC
-    early stop, SIMD arithmetic; TB CRC).
-    Received samples: the UL transport blocks through a UE transmitter (the same GPU encoder / DM-RS / modulator),
-    a per-UE random unitary 4x4 channel and AWGN (--snr-db), OFDM-modulated; synthesised once before timing and
-    resident in HBM. `--worst-case` feeds Gaussian noise instead (no TB ever valid: every codeblock runs all
-    iterations, like the reference ldpc_decoder_benchmark).
+  * DL (4 layers, 4 ports): PDSCH encoder (TB CRC, segmentation, CB CRC, LDPC, rate matching) -> PDSCH DM-RS ->
+    PDSCH modulator (scrambling, 256QAM, layer mapping, precoding, RE mapping, bf16 grid) -> OFDM modulator
+    (4096-point DFT, CP, phase compensation) of 4 ports: baseband samples.
+  * UL (4 rx ports): OFDM demodulator -> DM-RS channel estimator (du_low defaults: filter smoothing, average time
+    strategy, CFO estimation + compensation, time alignment) -> PUSCH demodulator (equalizer, soft demapping,
+    descrambling) -> PUSCH decoder (rate dematching, LDPC min-sum, 6 iterations max with CRC early stop, SIMD
+    arithmetic; TB CRC).
 
-Weak scaling: every rank processes its own cells' slots; the decoded UL TBs + CRC flags of all ranks are gathered to
-rank 0 (the FAPI rank) over RCCL once per step. One JSON line from rank 0.
+Profiles (--profile):
+  * "ref" (default): every stage is one the open-source reference runs - single-layer PUSCH per UE (its estimator's
+    limit, port_channel_estimator_average_impl.cpp:83) with ZF 1 x 4, so the GPU path and the cpu_baseline leg do the
+    same, parity-pinned work (the bench checks the GPU's UL LLRs against the reference's on the same samples).
+  * "mimo4": the extension - 4-layer PUSCH per UE (multi-layer estimation, 4 x 4 MMSE), beyond the reference.
+
+Received samples: the UL transport blocks through a UE transmitter (the same GPU encoder / DM-RS / modulator), a
+per-UE random unitary 4x4 channel, a per-UE CFO (+-300 Hz) and AWGN (--snr-db), OFDM-modulated; synthesised before
+timing and resident in HBM. `--input-sets` independent copies of the whole per-step working set (TBs, samples, grids,
+estimates, LLRs, HARQ buffers, decoded TBs, each set with its own plans and captured graph) are rotated step by step,
+so the timed loop streams a working set larger than the 256 MB Infinity Cache. Operating points: the headline SNR,
+plus `--extra-points` (a clean 35 dB link and the worst case: Gaussian noise, every codeblock runs all iterations,
+like the reference's ldpc_decoder benchmark) timed the same way.
+
+Weak scaling (--shard cells): every rank processes its own cells' slots; the decoded UL TBs + CRC flags of all ranks are
+gathered to rank 0 (the FAPI rank) over RCCL once per step. Strong scaling (--shard ues): the 64 UEs of every slot are
+split across the ranks (srsgpu.dist.shard_ues); each rank runs the upper PHY of its UEs (the OFDM stages of the cell
+stay on every rank) and the TBs are gathered the same way. One JSON line from rank 0.
 """
 import argparse
 import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -44,95 +58,162 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 SLOT_RATE_30KHZ = 2000.0  # slots per second of one cell at 30 kHz SCS
 DL_STAGES = ["pdsch_encode", "pdsch_dmrs_modulate", "ofdm_modulate"]
 UL_STAGES = ["ofdm_demodulate", "pusch_channel_estimate", "pusch_demodulate", "pusch_decode"]
+DMRS_MASK = slotlib.DMRS_POS1
+CFO_HZ_MAX = 300.0
+
+PROFILES = {
+    "ref": dict(ul_layers=1, equalizer=srsgpu.EQ_ZF,
+                ul_desc="single-layer PUSCH per UE, ZF 1x4 (the reference's estimator / equalizer scope)"),
+    "mimo4": dict(ul_layers=4, equalizer=srsgpu.EQ_MMSE,
+                  ul_desc="4-layer PUSCH per UE, multi-layer estimation + 4x4 MMSE (extension beyond the reference)"),
+}
 
 
-def cpu_baseline(ues, segs, tb_host, cw_host, llr_host, samples_host, iterations, budget_s):
-    """The srsRAN reference built from its own sources (oracle/_ref) on ONE host core, same slot: PDSCH encoding of
-    the 64 TBs (pdsch_encoder_impl: segmenter + AVX2 LDPC encoder + rate matcher), PDSCH DM-RS + modulation of the 64
-    UEs into one grid and OFDM modulation of 4 ports (generic DFT), OFDM demodulation of 4 ports, per-UE DM-RS channel
-    estimation + PUSCH demodulation (the open-source reference estimates / equalizes one layer: single-layer UEs on
-    the same REs), and the PUSCH codeblock tasks of the 192 codeblocks (rate dematcher + LDPC decoder with CRC early
-    stop, the implementations "auto" picks here)."""
+def host_cores():
+    """Host cores this process may use: the affinity set, capped by OMP_NUM_THREADS (16 per GPU on the GPU box,
+    where the affinity set shows the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
+
+
+def cpu_baseline(dl_ues, dl_segs, ul_ues, ul_segs, tb_host, cw_host, samples_host, iterations, budget_s, cores):
+    """The srsRAN reference built from its own sources (oracle/_ref) on `cores` host threads, each running whole slots
+    end to end with its own reference objects (slot-level parallelism: the best throughput the CPU path reaches on this
+    workload): PDSCH encoding of the 64 DL TBs (pdsch_encoder_impl: segmenter + AVX2 LDPC encoder + rate matcher),
+    PDSCH DM-RS + modulation of the 64 UEs into one grid and OFDM modulation of 4 ports (generic DFT), OFDM
+    demodulation of 4 ports, per-UE DM-RS channel estimation (filter, average, CFO compensation) + PUSCH demodulation
+    (single-layer ZF 1 x 4) of the same samples the GPU receives, and the PUSCH codeblock tasks (rate dematcher +
+    LDPC decoder with CRC early stop, the implementations "auto" picks here) on the reference's own LLRs.
+    Returns (baseline dict, reference UL LLRs of slot 0)."""
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libsrsref.so")
     if not os.path.exists(ref_so):
-        return None
+        return None, None
     lib = ctypes.CDLL(ref_so)
     P = ctypes.c_void_p
     for f in ("ref_pdsch_encode_slot_timed", "ref_pusch_decode_cbs_timed", "ref_dl_slot_timed", "ref_ul_slot_timed"):
         getattr(lib, f).restype = ctypes.c_longlong
     avx512 = bool(lib.ref_cpu_has_avx512())
     vbmi = bool(lib.ref_cpu_has_avx512vbmi())
-    n = len(ues)
-    bg = np.array([s.base_graph for s in segs], np.int32)
-    qm = np.array([u.qm for u in ues], np.int32)
-    ly = np.array([u.nof_layers for u in ues], np.int32)
-    ns = np.array([u.nof_ch_symbols for u in ues], np.uint32)
-    tbb = np.array([s.tbs // 8 for s in segs], np.uint32)
-    nrb = np.array([u.n_prb for u in ues], np.int32)
+    n = len(dl_ues)
+    bg = np.array([s.base_graph for s in dl_segs], np.int32)
+    qm = np.array([u.qm for u in dl_ues], np.int32)
+    ly = np.array([u.nof_layers for u in dl_ues], np.int32)
+    ns = np.array([u.nof_ch_symbols for u in dl_ues], np.uint32)
+    tbb = np.array([s.tbs // 8 for s in dl_segs], np.uint32)
+    nrb = np.array([u.n_prb for u in dl_ues], np.int32)
     rb0 = np.concatenate([[0], np.cumsum(nrb)[:-1]]).astype(np.int32)
     cw_off = np.array(cw_host[1], np.int32)
-    cw = np.zeros(sum(s.cw_length for s in segs), np.uint8)
+    ul_nrb = np.array([u.n_prb for u in ul_ues], np.int32)
+    ul_rb0 = np.concatenate([[0], np.cumsum(ul_nrb)[:-1]]).astype(np.int32)
     params = []
     llr_off = 0
-    for u, s in zip(ues, segs):
+    for s in ul_segs:
         crc = 1 if s.nof_segments > 1 else (0 if s.tbs > 3824 else 3)
         for cb in s.codeblocks:
-            params.append([s.base_graph, s.lifting_size, u.qm, cb.rm_length, cb.nof_filler_bits, crc,
+            params.append([s.base_graph, s.lifting_size, ul_ues[0].qm, cb.rm_length, cb.nof_filler_bits, crc,
                            cb.nof_crc_bits, llr_off + cb.cw_offset])
         llr_off += s.cw_length
     params = np.array(params, np.int32)
-    iters = np.zeros(len(params), np.int32)
-    t_enc = t_dec = t_dl = t_ul = t_dl_ofdm = t_ul_ofdm = t_chest = 0
-    o1, o2 = ctypes.c_longlong(), ctypes.c_longlong()
-    slots = 0
-    t0 = time.time()
-    while time.time() - t0 < budget_s or slots == 0:
-        t_enc += lib.ref_pdsch_encode_slot_timed(1, n, bg.ctypes.data_as(P), qm.ctypes.data_as(P),
-                                                 ly.ctypes.data_as(P), ns.ctypes.data_as(P), tbb.ctypes.data_as(P),
-                                                 tb_host.ctypes.data_as(P), cw.ctypes.data_as(P))
-        t_dl += lib.ref_dl_slot_timed(n, rb0.ctypes.data_as(P), nrb.ctypes.data_as(P), int(qm[0]), int(ly[0]),
-                                      cw_host[0].ctypes.data_as(P), cw_off.ctypes.data_as(P), ctypes.byref(o1))
-        t_dl_ofdm += o1.value
-        t_ul += lib.ref_ul_slot_timed(n, rb0.ctypes.data_as(P), nrb.ctypes.data_as(P), int(qm[0]),
-                                      samples_host.ctypes.data_as(P), ctypes.byref(o1), ctypes.byref(o2))
-        t_ul_ofdm += o1.value
-        t_chest += o2.value
-        t_dec += lib.ref_pusch_decode_cbs_timed(2 if vbmi else 1, 2 if avx512 else 1, len(params),
-                                                params.ctypes.data_as(P), llr_host.ctypes.data_as(P), iterations,
-                                                iters.ctypes.data_as(P))
-        slots += 1
-    slot_s = (t_enc + t_dl + t_ul + t_dec) * 1e-9 / slots
-    ms = lambda v: v * 1e-6 / slots  # noqa: E731
-    return {"value": 1.0 / slot_s, "unit": "slots/s", "cores": 1, "kind": "reference",
-            "sample": f"{slots} slots (64 UEs, 192 codeblocks per direction) through the srsRAN reference on one "
-                      f"core: PDSCH encode {ms(t_enc):.2f} ms/slot (avx2 encoder), PDSCH DM-RS + modulation "
-                      f"{ms(t_dl - t_dl_ofdm):.2f} + OFDM modulation {ms(t_dl_ofdm):.2f} ms/slot (generic DFT), OFDM "
-                      f"demodulation {ms(t_ul_ofdm):.2f} + channel estimation {ms(t_chest):.2f} + PUSCH "
-                      f"demodulation {ms(t_ul - t_ul_ofdm - t_chest):.2f} ms/slot (single-layer: the open-source "
-                      f"reference's limit), PUSCH codeblock tasks {ms(t_dec):.2f} ms/slot "
+    nllr = llr_off
+
+    def run_slot(st):
+        cw = st["cw"]
+        o1, o2 = ctypes.c_longlong(), ctypes.c_longlong()
+        t = np.zeros(7)
+        t[0] = lib.ref_pdsch_encode_slot_timed(1, n, bg.ctypes.data_as(P), qm.ctypes.data_as(P),
+                                               ly.ctypes.data_as(P), ns.ctypes.data_as(P), tbb.ctypes.data_as(P),
+                                               tb_host.ctypes.data_as(P), cw.ctypes.data_as(P))
+        t[1] = lib.ref_dl_slot_timed(n, rb0.ctypes.data_as(P), nrb.ctypes.data_as(P), int(qm[0]), int(ly[0]),
+                                     ctypes.c_uint(DMRS_MASK), cw_host[0].ctypes.data_as(P), cw_off.ctypes.data_as(P),
+                                     ctypes.byref(o1))
+        t[2] = o1.value
+        t[3] = lib.ref_ul_slot_timed(len(ul_ues), ul_rb0.ctypes.data_as(P), ul_nrb.ctypes.data_as(P),
+                                     int(ul_ues[0].qm), ctypes.c_uint(DMRS_MASK), 1, samples_host.ctypes.data_as(P),
+                                     st["llr"].ctypes.data_as(P), ctypes.byref(o1), ctypes.byref(o2))
+        t[4], t[5] = o1.value, o2.value
+        t[6] = lib.ref_pusch_decode_cbs_timed(2 if vbmi else 1, 2 if avx512 else 1, len(params),
+                                              params.ctypes.data_as(P), st["llr"].ctypes.data_as(P), iterations,
+                                              st["iters"].ctypes.data_as(P))
+        return t
+
+    states = [{"cw": np.zeros(sum(s.cw_length for s in dl_segs), np.uint8), "llr": np.zeros(nllr, np.int8),
+               "iters": np.zeros(len(params), np.int32), "slots": 0, "t": np.zeros(7), "it": []}
+              for _ in range(cores)]
+    start = threading.Barrier(cores + 1)
+    stop = threading.Event()
+
+    def worker(st):
+        run_slot(st)  # untimed: first-call setup of the thread's reference objects (DFT plans, tables)
+        start.wait()
+        while not stop.is_set() or st["slots"] == 0:
+            st["t"] += run_slot(st)
+            st["slots"] += 1
+            st["it"].append(np.where(st["iters"] > 0, st["iters"], iterations).mean())
+
+    threads = [threading.Thread(target=worker, args=(st,)) for st in states]
+    for th in threads:
+        th.start()
+    start.wait()
+    t0 = time.perf_counter()
+    time.sleep(budget_s)
+    stop.set()
+    for th in threads:
+        th.join()
+    wall = time.perf_counter() - t0
+    slots = sum(st["slots"] for st in states)
+    tt = sum(st["t"] for st in states) / slots * 1e-6  # ms per slot per thread, per stage
+    it = float(np.mean([x for st in states for x in st["it"]]))
+    base = {"value": slots / wall, "unit": "slots/s", "cores": cores, "kind": "reference",
+            "sample": f"{slots} slots in {wall:.1f} s on {cores} host threads, each running whole slots (64 UEs) "
+                      f"through the srsRAN reference with its own objects; per slot and thread: PDSCH encode "
+                      f"{tt[0]:.2f} ms (avx2 encoder), PDSCH DM-RS + modulation {tt[1] - tt[2]:.2f} ms + OFDM "
+                      f"modulation {tt[2]:.2f} ms (generic DFT), OFDM demodulation {tt[4]:.2f} ms + channel "
+                      f"estimation {tt[5]:.2f} ms (filter, average, CFO compensation) + PUSCH demodulation "
+                      f"{tt[3] - tt[4] - tt[5]:.2f} ms (single-layer ZF 1x4), PUSCH codeblock tasks {tt[6]:.2f} ms "
                       f"({'avx512' if vbmi else 'avx2'} dematcher, {'avx512' if avx512 else 'avx2'} decoder, "
-                      f"{iterations} iterations max, early stop, avg "
-                      f"{np.where(iters > 0, iters, iterations).mean():.2f} iterations)"}
+                      f"{iterations} iterations max, early stop, avg {it:.2f} iterations)"}
+    return base, states[0]["llr"].copy()
+
+
+class InputSet:
+    """One independent copy of a step's working set: DL / UL pipelines (plans + buffers), DL TBs, UL samples and the
+    UL TBs the UEs sent. Sets are rotated step by step."""
+
+    def __init__(self, ctx, dl_cell, ul_cell, prof, iterations, gen, dev):
+        self.dl = slotlib.DownlinkPipeline(ctx, dl_cell)
+        self.ul = slotlib.UplinkPipeline(ctx, ul_cell, iterations=iterations, equalizer=prof["equalizer"],
+                                         compensate_cfo=True)
+        self.dl_tbs = torch.randint(0, 256, (self.dl.tb_total,), generator=gen, device=dev, dtype=torch.uint8)
+        self.ul_tbs_tx = torch.randint(0, 256, (sum(self.ul.tb_bytes),), generator=gen, device=dev,
+                                       dtype=torch.uint8)
+        self.samples = torch.zeros(2 * self.ul.ofdm.nof_samples, dtype=torch.float32, device=dev)
+        self.graph = None
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=4000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--profile", choices=sorted(PROFILES), default="ref")
     ap.add_argument("--slots-per-step", type=int, default=16)
+    ap.add_argument("--input-sets", type=int, default=4, help="independent working sets rotated step by step")
     ap.add_argument("--iterations", type=int, default=6)
-    ap.add_argument("--snr-db", type=float, default=35.0)
-    ap.add_argument("--worst-case", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--snr-db", type=float, default=26.0)
+    ap.add_argument("--worst-case", action="store_true", help="headline on Gaussian-noise input (all iterations)")
+    ap.add_argument("--extra-points", action=argparse.BooleanOptionalAction, default=True,
+                    help="also time the 35 dB and worst-case operating points (--point-steps steps each)")
+    ap.add_argument("--point-steps", type=int, default=1000)
+    ap.add_argument("--shard", choices=["cells", "ues"], default="cells")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--serial-legs", action="store_true",
                     help="run the DL and UL legs on one stream (clean per-stage times; slower overall)")
-    ap.add_argument("--batches", type=int, default=1,
-                    help="split a step's slots into this many independent DL/UL pipeline pairs on their own streams")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
-                    help="replay the DL+UL pipeline of a step as one captured HIP graph (default) or launch eagerly")
+                    help="replay each set's DL+UL pipeline as one captured HIP graph (default) or launch eagerly")
     args = ap.parse_args()
+    prof = PROFILES[args.profile]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -145,186 +226,216 @@ def main():
     gen.manual_seed(1234 + rank)
     ctx = srsgpu.Context(local_rank)
     S = args.slots_per_step
-    B = args.batches
-    assert B >= 1 and S % B == 0, "--slots-per-step must be a multiple of --batches"
-    Sb = S // B  # slots per pipeline pair
+    K = max(1, args.input_sets)
 
-    ues = sch.slot_100mhz_4x4()
-    segs = [u.segmentation() for u in ues]
-    cell = slotlib.CellSlots(ues, segs, Sb)
-    dls = [slotlib.DownlinkPipeline(ctx, cell) for _ in range(B)]
-    uls = [slotlib.UplinkPipeline(ctx, cell, iterations=args.iterations) for _ in range(B)]
-    dl, ul = dls[0], uls[0]
-    dl_tbs = [torch.randint(0, 256, (dl.tb_total,), generator=gen, device=dev, dtype=torch.uint8) for _ in range(B)]
-    ul_tbs_tx = [torch.randint(0, 256, (dl.tb_total,), generator=gen, device=dev, dtype=torch.uint8) for _ in range(B)]
-    if args.worst_case:
-        samples = [torch.randn(2 * ul.ofdm.nof_samples, generator=gen, device=dev) * 0.01 for _ in range(B)]
-        data_desc = "Gaussian noise samples (no TB ever valid: all LDPC iterations, worst case)"
+    dl_all = sch.slot_100mhz_4x4(nof_layers=4, nof_dmrs_symbols=2)
+    ul_all = sch.slot_100mhz_4x4(nof_layers=prof["ul_layers"], nof_dmrs_symbols=2)
+    if args.shard == "ues" and world > 1:
+        from srsgpu import dist as sdist
+        dl_ues, ul_ues = sdist.shard_ues(dl_all, world, rank), sdist.shard_ues(ul_all, world, rank)
+        rb_first = sum(u.n_prb for u in dl_all[:sdist.shard_range(len(dl_all), world, rank).start])
     else:
-        samples = [slotlib.synthesize_uplink(ctx, cell, ul_tbs_tx[b], snr_db=args.snr_db, seed=99 + rank + 1000 * b)
-                   for b in range(B)]
-        data_desc = (f"UL TBs through a GPU UE transmitter (same encoder / DM-RS / modulator), a random unitary 4x4 "
-                     f"channel per UE and AWGN at {args.snr_db:g} dB SNR, OFDM-modulated (synthetic)")
-    d_dl_tbs, d_ul_tbs_tx, d_samples = dl_tbs[0], ul_tbs_tx[0], samples[0]
-    torch.cuda.synchronize()
-    tb_bytes = dl.tb_bytes
-    nof_tbs = len(tb_bytes)
+        dl_ues, ul_ues, rb_first = dl_all, ul_all, 0
+    dl_segs = [u.segmentation() for u in dl_ues]
+    ul_segs = [u.segmentation() for u in ul_ues]
+    dl_cell = slotlib.CellSlots(dl_ues, dl_segs, S, dmrs_mask=DMRS_MASK, rb_first=rb_first)
+    ul_cell = slotlib.CellSlots(ul_ues, ul_segs, S, dmrs_mask=DMRS_MASK, rb_first=rb_first)
+    sets = [InputSet(ctx, dl_cell, ul_cell, prof, args.iterations, gen, dev) for _ in range(K)]
 
-    dl_streams = [torch.cuda.Stream(dev) for _ in range(B)]
-    ul_streams = dl_streams if args.serial_legs else [torch.cuda.Stream(dev) for _ in range(B)]
+    def fill_samples(snr_db, worst):
+        for k, st in enumerate(sets):
+            if worst:
+                st.samples.copy_(torch.randn(st.samples.numel(), generator=gen, device=dev) * 0.01)
+            else:
+                st.samples.copy_(slotlib.synthesize_uplink(ctx, ul_cell, st.ul_tbs_tx, snr_db=snr_db,
+                                                           seed=99 + rank + 1000 * k, cfo_hz_max=CFO_HZ_MAX))
+        torch.cuda.synchronize()
+
+    fill_samples(args.snr_db, args.worst_case)
+    dl_stream = torch.cuda.Stream(dev)
+    ul_stream = dl_stream if args.serial_legs else torch.cuda.Stream(dev)
     tb_gather = None
     if world > 1:
         from srsgpu import dist as sdist
-        tb_gather = sdist.TbGather(ul.d_tbs.numel(), ul.d_tb_ok.numel(), dev, root=0)
+        tb_gather = sdist.TbGather(sets[0].ul.d_tbs.numel(), sets[0].ul.d_tb_ok.numel(), dev, root=0)
 
-    def pipeline(ev_dl=None, ev_ul=None, batches=None):
-        """DL and UL legs of one step (every batch), forked from and joined back into the caller's current stream.
-        Stage events, when given, go to batch 0."""
+    def pipeline(st, ev_dl=None, ev_ul=None):
+        """DL and UL legs of one step of input set `st`, forked from and joined back into the current stream."""
         cur = torch.cuda.current_stream(dev)
-        bs = range(B) if batches is None else batches
-        for b in bs:
-            dl_streams[b].wait_stream(cur)
-            ul_streams[b].wait_stream(cur)
-        for b in bs:
-            dls[b].execute(dl_tbs[b], dl_streams[b], ev_dl if b == 0 else None)
-            uls[b].execute(samples[b], ul_streams[b], ev_ul if b == 0 else None)
-        for b in bs:
-            cur.wait_stream(dl_streams[b])
-            cur.wait_stream(ul_streams[b])
+        dl_stream.wait_stream(cur)
+        ul_stream.wait_stream(cur)
+        st.dl.execute(st.dl_tbs, dl_stream, ev_dl)
+        st.ul.execute(st.samples, ul_stream, ev_ul)
+        cur.wait_stream(dl_stream)
+        cur.wait_stream(ul_stream)
 
-    graph = None
-
-    def step(ev_dl=None, ev_ul=None):
-        if graph is not None and ev_dl is None:
-            graph.replay()
+    def step(i):
+        st = sets[i % K]
+        if st.graph is not None:
+            st.graph.replay()
         else:
-            pipeline(ev_dl, ev_ul)
+            pipeline(st)
         if tb_gather is not None:
-            for u in uls:
-                tb_gather.gather(u.d_tbs, u.d_tb_ok)
+            tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize()
-    dl.encoder.stage_times()
-    ul.decoder.stage_times()
     if args.graph:
-        # hipGraph of the whole per-step pipeline (every plan is allocation-free and capture-safe): the 11 kernels,
-        # the codeword memset and the stream fork/join replay as one graph launch per step.
+        # One hipGraph per input set of the whole per-step pipeline (every plan is allocation-free and capture-safe):
+        # the kernels, the codeword memset and the stream fork/join replay as one graph launch per step.
         # thread_local: the RCCL watchdog thread of a multi-GPU run keeps polling its events during the capture.
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-            pipeline()
-        for _ in range(args.warmup):
-            step()
+        for st in sets:
+            st.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(st.graph, capture_error_mode="thread_local"):
+                pipeline(st)
+        for i in range(args.warmup):
+            step(i)
         torch.cuda.synchronize()
-    # Timed loop: eager mode records only the decoder plan's own stage events (the roofline kernel's launch duration,
-    # on its launch stream); graph mode records none. The roofline kernel time then comes from an untimed eager pass
-    # with those two events, and per-stage times from another untimed pass with events between the stages.
-    ul.decoder.enable_timing(not args.graph, decode_only=True)
+
+    def timed(steps):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def ul_results(check_payload):
+        """UL TB success and LDPC iterations of the last step of every set; decoded TBs with a passing CRC must
+        equal what the UEs sent."""
+        ok_all, it_all = [], []
+        for st in sets:
+            ok = st.ul.d_tb_ok.cpu().numpy().astype(bool)
+            it = st.ul.d_iters.cpu().numpy()
+            if check_payload:
+                sent, got, off = st.ul_tbs_tx.cpu().numpy(), st.ul.d_tbs.cpu().numpy(), 0
+                for i, nb in enumerate(st.ul.tb_bytes):
+                    if ok[i]:
+                        assert np.array_equal(got[off:off + nb], sent[off:off + nb]), f"TB {i} CRC ok, payload differs"
+                    off += nb
+            ok_all.append(ok)
+            it_all.append(np.where(it > 0, it, args.iterations))
+        return float(np.concatenate(ok_all).mean()), float(np.concatenate(it_all).mean())
+
+    elapsed = timed(args.steps)
+    tb_success, avg_iters = ul_results(not args.worst_case)
+    slots = S * (world if args.shard == "cells" else 1) * args.steps
+    value = slots / elapsed
+
+    # Roofline kernel time: an eager pass over the sets with the decoder plans' own stage events (the decoding launch
+    # on its stream), right after the timed loop.
+    st0 = sets[0]
+    for st in sets:
+        st.ul.decoder.stage_times()
+        st.ul.decoder.enable_timing(True, decode_only=True)
+    n_dec = min(args.steps, 400)
+    for i in range(n_dec):
+        pipeline(sets[i % K])
+    torch.cuda.synchronize()
+    dec_ms_tot, dec_n = 0.0, 0
+    for st in sets:
+        ms, n = st.ul.decoder.stage_times()
+        dec_ms_tot += ms[1]
+        dec_n += n
+        st.ul.decoder.enable_timing(False)
+    assert dec_n == n_dec
+    dec_ms = dec_ms_tot / dec_n
+    # Per-stage times: another untimed eager pass with events between the stages.
+    n_stage = min(args.steps, 200)
     evs = [([torch.cuda.Event(enable_timing=True) for _ in range(4)],
-            [torch.cuda.Event(enable_timing=True) for _ in range(5)]) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if args.graph:
-        ul.decoder.enable_timing(True, decode_only=True)
-        for _ in range(args.steps):
-            pipeline(batches=[0])  # the roofline kernel of batch 0, its pipeline pair alone
-        torch.cuda.synchronize()
-    ul_ms, ul_n = ul.decoder.stage_times()
-    assert ul_n == args.steps
-    ul.decoder.enable_timing(False)
-    for i in range(args.steps):  # per-stage times: an extra, untimed pass of batch 0 with events between the stages
-        pipeline(*evs[i], batches=[0])
+            [torch.cuda.Event(enable_timing=True) for _ in range(5)]) for _ in range(n_stage)]
+    for i in range(n_stage):
+        pipeline(sets[i % K], *evs[i])
     torch.cuda.synchronize()
     stage = {k: 0.0 for k in DL_STAGES + UL_STAGES}
     for ed, eu in evs:
         for j, k in enumerate(DL_STAGES):
-            stage[k] += ed[j].elapsed_time(ed[j + 1]) / args.steps
+            stage[k] += ed[j].elapsed_time(ed[j + 1]) / n_stage
         for j, k in enumerate(UL_STAGES):
-            stage[k] += eu[j].elapsed_time(eu[j + 1]) / args.steps
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+            stage[k] += eu[j].elapsed_time(eu[j + 1]) / n_stage
 
-    # ---- Results of the last step: UL TB success (decoded TBs must equal what the UEs sent) and iterations ----
-    tb_ok = np.concatenate([u.d_tb_ok.cpu().numpy().astype(bool) for u in uls])
-    iters = np.concatenate([u.d_iters.cpu().numpy() for u in uls])
-    if not args.worst_case:
-        for b in range(B):
-            sent = ul_tbs_tx[b].cpu().numpy()
-            got = uls[b].d_tbs.cpu().numpy()
-            ok_b = uls[b].d_tb_ok.cpu().numpy().astype(bool)
-            off = 0
-            for i, nb in enumerate(tb_bytes):
-                if ok_b[i]:
-                    assert np.array_equal(got[off:off + nb], sent[off:off + nb]), f"TB {i} CRC ok but payload differs"
-                off += nb
-    avg_iters = float(np.where(iters > 0, iters, args.iterations).mean())
+    # ---- Operating points: the same timed loop on other inputs (samples rewritten in place; graphs unchanged) ----
+    points = [{"name": "headline", "snr_db": None if args.worst_case else args.snr_db, "value": value,
+               "ms_per_step": elapsed * 1e3 / args.steps, "steps": args.steps,
+               "pusch_tb_success_rate": tb_success, "ldpc_avg_iterations": avg_iters}]
+    if args.extra_points:
+        for name, snr, worst in (("clean_35dB", 35.0, False), ("worst_case_noise", None, True)):
+            fill_samples(snr, worst)
+            for i in range(max(args.warmup, K)):
+                step(i)
+            e = timed(args.point_steps)
+            ok, it = ul_results(not worst)
+            points.append({"name": name, "snr_db": snr, "value": S * (world if args.shard == "cells" else 1)
+                           * args.point_steps / e, "ms_per_step": e * 1e3 / args.point_steps,
+                           "steps": args.point_steps, "pusch_tb_success_rate": ok, "ldpc_avg_iterations": it})
+        fill_samples(args.snr_db, args.worst_case)
 
-    slots = S * world * args.steps
-    value = slots / elapsed
+    # ---- Roofline of the dominant kernel (LDPC decoder) ----
+    ul, dl = st0.ul, st0.dl
     info_bits_slot = sum(((22 if s.base_graph == 1 else 10) * s.lifting_size - s.nof_filler_bits) * s.nof_segments
-                         for s in segs)
-    tbs_bits_slot = sum(s.tbs for s in segs)
-    dec_ms = ul_ms[1] / args.steps
+                         for s in ul_segs)
+    tbs_bits_ul = sum(s.tbs for s in ul_segs)
+    tbs_bits_dl = sum(s.tbs for s in dl_segs)
     # Algorithmic bytes of one decoder launch: the LLRs each codeblock's decode() reads (the HARQ span up to the
     # dematcher's zero tail, as reported by the plan), K*Z/8 bytes of decoded bits written, 4 B result + 1 B CRC flag,
     # 40 B descriptor.
     dec_bytes = ul.decoder.decoder_input_llrs + sum(
-        s.nof_segments * (((22 if s.base_graph == 1 else 10) * s.lifting_size + 7) // 8 + 45) for s in segs) * Sb
+        s.nof_segments * (((22 if s.base_graph == 1 else 10) * s.lifting_size + 7) // 8 + 45) for s in ul_segs) * S
     achieved = dec_bytes / (dec_ms * 1e-3) / 1e9
+    wl_key = f"{args.profile}/S{S}/{'noise' if args.worst_case else f'{args.snr_db:g}dB'}"
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "ldpc_decode_traffic.json")
     if os.path.exists(tfile):
         with open(tfile) as f:
             tj = json.load(f)
-        if tj.get("slots_per_step") == Sb and tj.get("worst_case", False) == args.worst_case:
+        if tj.get("workload") == wl_key:
             traffic = tj.get("hbm_bytes_per_launch")
-
     # VALU roofline of the same launch: wave-level VALU instructions per launch from the committed SQ counter pass
-    # (rocprofv3 --pmc SQ_INSTS_VALU ..., tools/sq_summary.py; same workload, same iterations) over the live kernel time.
+    # (rocprofv3 --pmc SQ_INSTS_VALU ..., tools/sq_summary.py; same workload) over the live kernel time.
     valu = None
-    sqfile = os.path.join(ROOT, "profiles", "r1_v22_sq_valu.json")
-    if os.path.exists(sqfile) and Sb == 16 and not args.worst_case:
+    sqfile = os.path.join(ROOT, "profiles", "sq_valu.json")
+    if os.path.exists(sqfile):
         with open(sqfile) as f:
-            sq = json.load(f).get("ldpc_decode_pk_kernel<1, 1, 8>")
+            sqj = json.load(f)
+        sq = sqj.get("kernels", {}).get("ldpc_decode_pk_kernel<1, 1, 8>") if sqj.get("workload") == wl_key else None
         if sq:
             peak = 1024 * 2.4e9 / 2  # SIMDs x clock / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md)
             rate = sq["valu_instr"] / (dec_ms * 1e-3)
             valu = {"bound": "valu_issue", "achieved": rate, "peak": peak, "unit": "wave-instr/s",
                     "frac": rate / peak, "instr_per_launch": sq["valu_instr"],
-                    "source": "profiles/r1_v22_sq_valu.json (SQ_INSTS_VALU) / live kernel time"}
+                    "source": "profiles/sq_valu.json (SQ_INSTS_VALU) / live kernel time"}
 
-    # Algorithmic HBM bytes per pipeline pair (Sb slots) of the signal-chain stages (each byte read or written once;
-    # DESIGN.md "Kernels"): bf16 grids are 4 B per RE, time samples 8 B (complex float), estimates 4 B per (layer,
-    # port, RE), LLRs 1 B. The stage times come from batch 0's pipeline pair.
-    S_all, S = S, Sb
-    P, nsc, L = cell.nof_ports, cell.nsc, ues[0].nof_layers
+    # Algorithmic HBM bytes per step of the signal-chain stages (each byte read or written once; DESIGN.md "Kernels"):
+    # bf16 grids are 4 B per RE, time samples 8 B (complex float), estimates 4 B per (layer, port, RE), LLRs 1 B.
+    P, nsc, Lu = ul_cell.nof_ports, ul_cell.nsc, prof["ul_layers"]
     grid_b = S * P * 14 * nsc * 4
     spp = ul.ofdm.nof_samples // (S * P)  # samples per slot and port (CPs included)
-    data_re = S * sum(12 * u.n_prb * (14 - 1) for u in ues)  # one DM-RS symbol without data
-    cw_b = sum(s.cw_length for s in segs) * S // 8
-    ce_rows = 1 if ul.estimate_layout == srsgpu.CE_COMPACT else 14  # estimate rows per (layer, port) and slot
-    ce_b = S * L * P * ce_rows * nsc * 4
+    nd = bin(DMRS_MASK).count("1")
+    data_re = S * sum(12 * u.n_prb * (14 - nd) for u in ul_ues)
+    cw_b = sum(s.cw_length for s in dl_segs) * S // 8
+    ce_rows = 1 if ul.estimate_layout == srsgpu.CE_COMPACT else 14
+    ce_b = S * Lu * P * ce_rows * 12 * sum(u.n_prb for u in ul_ues) * 4
     stage_bytes = {
         "pdsch_dmrs_modulate": cw_b + grid_b,
         "ofdm_modulate": grid_b + S * P * spp * 8,
         "ofdm_demodulate": S * P * 14 * slotlib.DFT_SIZE * 8 + grid_b,
-        "pusch_channel_estimate": S * P * nsc * 4 + ce_b,
-        "pusch_demodulate": data_re * (P * 4 + L * ues[0].qm) + ce_b,
+        "pusch_channel_estimate": S * P * nd * nsc * 4 + ce_b,
+        "pusch_demodulate": data_re * (P * 4 + Lu * ul_ues[0].qm) + ce_b,
     }
     stage_gbps = {k: v / (stage[k] * 1e-3) / 1e9 for k, v in stage_bytes.items() if stage[k] > 0}
+    set_bytes = sum(t.numel() * t.element_size() for t in
+                    (st0.dl_tbs, st0.samples, st0.ul_tbs_tx, dl.d_cw, dl.d_grid, dl.d_samples, ul.d_grid, ul.d_nv,
+                     ul.d_llrs, ul.d_harq, ul.d_crc, ul.d_msgs, ul.d_iters, ul.d_tbs, ul.d_tb_ok)) \
+        + S * Lu * P * 14 * nsc * 4 // 14 * ce_rows
 
     result = {
         "metric": "PDSCH+PUSCH slots/sec (100MHz 4x4) + LDPC info-bits/s at 1/2/4/8 GPU",
@@ -335,55 +446,71 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.shard == "cells" else "strong",
         "vs_baseline": None,
         "dtype": "int8/bf16/f32",
-        "data": "synthetic: random TB payloads; PUSCH input = " + data_desc,
-        "config": {"workload": "n78 100 MHz 4x4 slot, 273 PRB, 64 UEs x (4-5 PRB, 4 layers, 256QAM MCS27), LDPC BG1 "
-                               "(Z 288/352): 64 TBs / 192 codeblocks per direction per slot",
+        "data": ("synthetic: random TB payloads; PUSCH input = " +
+                 ("Gaussian noise samples (no TB ever valid: all LDPC iterations)" if args.worst_case else
+                  f"UL TBs through a GPU UE transmitter (same encoder / DM-RS / modulator), a random unitary 4x4 "
+                  f"channel and a CFO within +-{CFO_HZ_MAX:g} Hz per UE, AWGN at {args.snr_db:g} dB SNR, "
+                  f"OFDM-modulated")),
+        "config": {"workload": f"n78 100 MHz 4x4 slot, 273 PRB, 64 UEs x 4-5 PRB, 256QAM MCS27, DM-RS symbols 2+11; "
+                               f"DL 4 layers, UL {prof['ul_desc']}; LDPC BG1",
+                   "profile": args.profile,
                    "dl_chain": "PDSCH encoder -> PDSCH DM-RS -> PDSCH modulator -> OFDM modulator (4 ports)",
-                   "ul_chain": "OFDM demodulator (4 ports) -> DM-RS channel estimator (4 layers x 4 ports) -> PUSCH "
-                               "demodulator (MMSE 4x4) -> PUSCH decoder",
-                   "channel_estimate_layout": "compact (one row per allocation, average time strategy)"
+                   "ul_chain": "OFDM demodulator (4 ports) -> DM-RS channel estimator (filter, average, CFO "
+                               "compensation, TA) -> PUSCH demodulator -> PUSCH decoder",
+                   "channel_estimate_layout": "compact (one row per allocation, CFO rotation in the demodulator)"
                                               if ul.estimate_layout == srsgpu.CE_COMPACT else "per symbol",
                    "leg_streams": "one stream" if args.serial_legs else "DL and UL on concurrent streams",
-                   "launch": "one captured HIP graph per step (torch.cuda.CUDAGraph over the plans' execute calls)"
-                             if args.graph else "eager kernel launches",
-                   "slots_per_step": S_all,
-                   "concurrent_batches": f"{B} DL/UL pipeline pair(s) of {Sb} slots, each leg on its own stream",
-                   "codeblocks_per_step_per_direction": int(sum(s.nof_segments for s in segs) * S_all),
+                   "launch": "one captured HIP graph per step and input set" if args.graph else "eager launches",
+                   "slots_per_step": S,
+                   "input_sets": K,
+                   "working_set_mb": K * set_bytes / 2 ** 20,
+                   "timed_region_s": elapsed,
+                   "codeblocks_per_step": {"dl": int(sum(s.nof_segments for s in dl_segs) * S),
+                                           "ul": int(sum(s.nof_segments for s in ul_segs) * S)},
                    "ldpc_max_iterations": args.iterations, "ldpc_early_stop": True,
                    "decoder_arithmetic": "avx2/avx512 (SIMD) variant, bit-exact",
                    "ofdm": "4096-point DFT, 122.88 Msps, normal CP",
-                   "parallelism": (f"dp{world}: each GPU processes its own cells' slots; decoded UL TBs + CRC flags "
-                                   f"gathered to the FAPI rank over RCCL every step") if world > 1 else
-                                  "dp1 (independent cells per GPU)"},
+                   "parallelism": (f"dp{world}: each GPU processes its own cells' slots" if args.shard == "cells" else
+                                   f"ue-shard{world}: the 64 UEs of each slot split across {world} GPUs (OFDM of the "
+                                   f"cell on every rank)") + (
+                                      "; decoded UL TBs + CRC flags gathered to the FAPI rank over RCCL every step"
+                                      if world > 1 else "")},
         "ldpc_info_bits_per_s": info_bits_slot * value,
-        "tb_bits_per_s_per_direction": tbs_bits_slot * value,
+        "tb_bits_per_s": {"dl": tbs_bits_dl * value, "ul": tbs_bits_ul * value},
         "realtime_cells_per_gpu": value / SLOT_RATE_30KHZ / world,
-        "pusch_tb_success_rate": float(tb_ok.mean()),
+        "pusch_tb_success_rate": tb_success,
         "ldpc_avg_iterations": avg_iters,
-        "stage_ms_per_step": stage,  # from the untimed pass of batch 0 with per-stage events
-        "stage_slots": Sb,
+        "operating_points": points,
+        "stage_ms_per_step": stage,  # from an untimed eager pass with per-stage events
         "stage_algorithmic_gbps": stage_gbps,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "ldpc_decode_pk_kernel<1,1,8>",
-                     "kernel_ms_per_launch": dec_ms,
-                     "note": "algorithmic bytes per launch / decoder-stage HIP-event time on the launch stream ("
-                             + ("an eager pass of as many steps right after the graph-replayed timed loop"
-                                if args.graph else "inside the timed loop")
-                             + "); the LDPC decoder is VALU-issue/latency-bound, not HBM-bound (DESIGN.md)"},
+                     "kernel_ms_per_launch": dec_ms, "algorithmic_bytes_per_launch": dec_bytes,
+                     "note": "algorithmic bytes per launch / decoder-stage HIP-event time on the launch stream (an "
+                             "eager pass right after the timed loop); the LDPC decoder is VALU-issue/latency-bound, "
+                             "not HBM-bound (DESIGN.md)"},
         "roofline_valu": valu,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        n_slot = len(segs)
-        tb_host = d_dl_tbs[: sum(tb_bytes[:n_slot])].cpu().numpy()
-        cw_host = (dl.d_cw.cpu().numpy(), dl.cw_offsets[:n_slot])
-        llr_host = ul.d_llrs[: sum(s.cw_length for s in segs)].cpu().numpy()
-        samples_host = d_samples[: 2 * 4 * 61440].cpu().numpy()
-        result["cpu_baseline"] = cpu_baseline(ues, segs, tb_host, cw_host, llr_host, samples_host, args.iterations,
-                                              args.cpu_seconds)
+        n_dl, n_ul = len(dl_segs), len(ul_segs)
+        tb_host = st0.dl_tbs[: sum(dl.tb_bytes[:n_dl])].cpu().numpy()
+        cw_host = (dl.d_cw.cpu().numpy(), dl.cw_offsets[:n_dl])
+        samples_host = st0.samples[: 2 * 4 * 61440].cpu().numpy()
+        base, ref_llr = cpu_baseline(dl_ues, dl_segs, ul_ues, ul_segs, tb_host, cw_host, samples_host,
+                                     args.iterations, args.cpu_seconds, host_cores())
+        result["cpu_baseline"] = base
+        if ref_llr is not None and args.profile == "ref":
+            # The GPU's UL LLRs of slot 0 against the reference's on the same received samples.
+            pipeline(st0)
+            torch.cuda.synchronize()
+            got = ul.d_llrs[: sum(s.cw_length for s in ul_segs)].cpu().numpy().astype(np.int16)
+            d = np.abs(got - ref_llr.astype(np.int16))
+            result["ul_llr_parity_vs_reference"] = {"llrs": int(d.size), "equal": float(np.mean(d == 0)),
+                                                    "within_one_step": float(np.mean(d <= 1)), "max_diff": int(d.max())}
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

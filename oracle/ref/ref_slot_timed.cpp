@@ -2,8 +2,8 @@
 // oracle/_ref/libsrsref.so) for bench.py's cpu_baseline leg: the DL stages after the encoder (PDSCH DM-RS + PDSCH
 // modulator of every UE into one grid, OFDM modulation of every port) and the UL stages before the decoder (OFDM
 // demodulation of every port, then per UE DM-RS channel estimation and PUSCH demodulation). The open-source reference
-// estimates and equalizes at most one layer per PUSCH (port_channel_estimator_average_impl.cpp:83,
-// channel_equalizer_generic_impl.cpp: ZF 1 x N), so the UL stages run single-layer UEs on the same REs.
+// estimates at most one layer per PUSCH (port_channel_estimator_average_impl.cpp:83), so the UL stages run
+// single-layer UEs (ZF 1 x N). Every reference object is thread_local: bench.py runs one slot loop per host core.
 #include "srsran/phy/support/precoding_configuration.h"
 #include "srsran/phy/support/resource_grid_reader.h"
 #include "srsran/phy/upper/channel_estimation.h"
@@ -31,6 +31,7 @@
 #include "lib/phy/upper/signal_processors/port_channel_estimator_average_impl.h"
 
 #include <chrono>
+#include <cstring>
 #include <memory>
 #include <vector>
 
@@ -81,27 +82,28 @@ precoding_configuration identity(unsigned L, unsigned P)
 
 extern "C" {
 
-/// One DL slot after the encoder: per UE PDSCH DM-RS + PDSCH modulation (identity precoding, 1 DM-RS symbol, type 1,
-/// 2 CDM groups without data) into a 273-PRB 4-port grid, then OFDM modulation of the 4 ports (4096-point DFT,
-/// generic). Returns the elapsed nanoseconds of those stages; out_ofdm_ns gets the OFDM part.
+/// One DL slot after the encoder: per UE PDSCH DM-RS + PDSCH modulation (identity precoding, DM-RS symbols
+/// dmrs_mask, type 1, 2 CDM groups without data) into a 273-PRB 4-port grid, then OFDM modulation of the 4 ports
+/// (4096-point DFT, generic). Returns the elapsed nanoseconds of those stages; out_ofdm_ns gets the OFDM part.
 long long ref_dl_slot_timed(int            nof_ues,
                             const int*     rb_start,
                             const int*     nof_rb,
                             int            qm,
                             int            nof_layers,
+                            unsigned       dmrs_mask,
                             const uint8_t* codewords,
                             const int*     cw_byte_offset,
                             long long*     out_ofdm_ns)
 {
-  static pdsch_modulator_impl modulator(
+  static thread_local pdsch_modulator_impl modulator(
       std::make_unique<modulation_mapper_lut_impl>(), std::make_unique<pseudo_random_generator_impl>(),
       std::make_unique<resource_grid_mapper_impl>(std::make_unique<channel_precoder_generic>()));
-  static dmrs_pdsch_processor_impl dmrs(
+  static thread_local dmrs_pdsch_processor_impl dmrs(
       std::make_unique<pseudo_random_generator_impl>(),
       std::make_unique<resource_grid_mapper_impl>(std::make_unique<channel_precoder_generic>()));
-  static resource_grid_impl grid(4, 14, 273 * 12);
-  static std::unique_ptr<ofdm_slot_modulator_impl> ofdm;
-  static std::vector<cf_t>                          samples;
+  static thread_local resource_grid_impl grid(4, 14, 273 * 12);
+  static thread_local std::unique_ptr<ofdm_slot_modulator_impl> ofdm;
+  static thread_local std::vector<cf_t>                          samples;
   if (!ofdm) {
     ofdm_modulator_common_configuration common;
     common.dft = std::make_unique<dft_processor_generic_impl>(
@@ -113,9 +115,14 @@ long long ref_dl_slot_timed(int            nof_ues,
   const modulation_scheme mod = qm == 8 ? modulation_scheme::QAM256
                                         : (qm == 6 ? modulation_scheme::QAM64
                                                    : (qm == 4 ? modulation_scheme::QAM16 : modulation_scheme::QPSK));
+  const int                       nof_dmrs = __builtin_popcount(dmrs_mask);
+  symbol_slot_mask                dmrs_pos(14);
+  for (unsigned l = 0; l != 14; ++l) {
+    dmrs_pos.set(l, ((dmrs_mask >> l) & 1U) != 0);
+  }
   std::vector<dynamic_bit_buffer> cws(static_cast<size_t>(nof_ues));
   for (int u = 0; u < nof_ues; ++u) {
-    const unsigned nbits = static_cast<unsigned>(nof_rb[u] * 12 * 13 * nof_layers * qm);
+    const unsigned nbits = static_cast<unsigned>(nof_rb[u] * 12 * (14 - nof_dmrs) * nof_layers * qm);
     cws[u].resize(nbits);
     srsvec::copy_offset(cws[u], span<const uint8_t>(codewords + cw_byte_offset[u], (nbits + 7) / 8), 0);
   }
@@ -128,8 +135,7 @@ long long ref_dl_slot_timed(int            nof_ues,
     dc.scrambling_id        = 500;
     dc.n_scid               = false;
     dc.amplitude            = 1.4125375F;
-    dc.symbols_mask         = symbol_slot_mask(14);
-    dc.symbols_mask.set(2);
+    dc.symbols_mask         = dmrs_pos;
     dc.rb_mask = crb_bitmap(273);
     dc.rb_mask.fill(rb_start[u], rb_start[u] + nof_rb[u]);
     dc.precoding = identity(nof_layers, 4);
@@ -162,21 +168,25 @@ long long ref_dl_slot_timed(int            nof_ues,
 }
 
 /// One UL slot before the decoder: OFDM demodulation of 4 ports (4096-point generic DFT), then per UE single-layer
-/// DM-RS channel estimation (filter / average) and PUSCH demodulation (ZF 1 x 4, 256QAM) of its RBs. Returns the
-/// elapsed nanoseconds; out_ofdm_ns / out_chest_ns get the OFDM and estimation parts.
+/// DM-RS channel estimation (filter / average, CFO compensation when compensate_cfo: du_low's defaults) on the DM-RS
+/// symbols of dmrs_mask and PUSCH demodulation (ZF 1 x 4) of its RBs. Returns the elapsed nanoseconds; out_ofdm_ns /
+/// out_chest_ns get the OFDM and estimation parts. llr_out (optional): the LLRs of every UE, concatenated.
 long long ref_ul_slot_timed(int          nof_ues,
                             const int*   rb_start,
                             const int*   nof_rb,
                             int          qm,
+                            unsigned     dmrs_mask,
+                            int          compensate_cfo,
                             const float* samples_in,
+                            int8_t*      llr_out,
                             long long*   out_ofdm_ns,
                             long long*   out_chest_ns)
 {
-  static resource_grid_impl                          grid(4, 14, 273 * 12);
-  static std::unique_ptr<ofdm_slot_demodulator_impl> ofdm;
-  static std::unique_ptr<dmrs_pusch_estimator_impl>  est;
-  static std::unique_ptr<pusch_demodulator_impl>     demod;
-  static unsigned                                    slot_size = 0;
+  static thread_local resource_grid_impl                          grid(4, 14, 273 * 12);
+  static thread_local std::unique_ptr<ofdm_slot_demodulator_impl> ofdm;
+  static thread_local std::unique_ptr<dmrs_pusch_estimator_impl>  ests[2];
+  static thread_local std::unique_ptr<pusch_demodulator_impl>     demod;
+  static thread_local unsigned                                    slot_size = 0;
   if (!ofdm) {
     ofdm_demodulator_common_configuration common;
     common.dft = std::make_unique<dft_processor_generic_impl>(
@@ -184,21 +194,23 @@ long long ref_ul_slot_timed(int          nof_ues,
     ofdm = std::make_unique<ofdm_slot_demodulator_impl>(
         common, ofdm_demodulator_configuration{1, 273, 4096, cyclic_prefix::NORMAL, 0, 1.0F / 64, 3.5e9});
     slot_size = ofdm->get_slot_size(0);
-    time_alignment_estimator_dft_impl::collection_dft_processors dfts;
-    for (unsigned n = time_alignment_estimator_dft_impl::min_dft_size;
-         n <= time_alignment_estimator_dft_impl::max_dft_size;
-         n *= 2) {
-      dfts.emplace(n, std::make_unique<dft_processor_generic_impl>(
-                          dft_processor::configuration{n, time_alignment_estimator_dft_impl::dft_direction}));
+    for (int c = 0; c != 2; ++c) {
+      time_alignment_estimator_dft_impl::collection_dft_processors dfts;
+      for (unsigned n = time_alignment_estimator_dft_impl::min_dft_size;
+           n <= time_alignment_estimator_dft_impl::max_dft_size;
+           n *= 2) {
+        dfts.emplace(n, std::make_unique<dft_processor_generic_impl>(
+                            dft_processor::configuration{n, time_alignment_estimator_dft_impl::dft_direction}));
+      }
+      ests[c] = std::make_unique<dmrs_pusch_estimator_impl>(
+          std::make_unique<pseudo_random_generator_impl>(), std::make_unique<low_papr_sequence_generator_impl>(),
+          std::make_unique<port_channel_estimator_average_impl>(
+              std::make_unique<interpolator_linear_impl>(),
+              std::make_unique<time_alignment_estimator_dft_impl>(std::move(dfts)),
+              port_channel_estimator_fd_smoothing_strategy::filter,
+              port_channel_estimator_td_interpolation_strategy::average,
+              c == 1));
     }
-    est = std::make_unique<dmrs_pusch_estimator_impl>(
-        std::make_unique<pseudo_random_generator_impl>(), std::make_unique<low_papr_sequence_generator_impl>(),
-        std::make_unique<port_channel_estimator_average_impl>(
-            std::make_unique<interpolator_linear_impl>(),
-            std::make_unique<time_alignment_estimator_dft_impl>(std::move(dfts)),
-            port_channel_estimator_fd_smoothing_strategy::filter,
-            port_channel_estimator_td_interpolation_strategy::average,
-            false));
     demod = std::make_unique<pusch_demodulator_impl>(
         std::make_unique<channel_equalizer_generic_impl>(channel_equalizer_algorithm_type::zf),
         nullptr,
@@ -211,8 +223,15 @@ long long ref_ul_slot_timed(int          nof_ues,
   const modulation_scheme mod = qm == 8 ? modulation_scheme::QAM256
                                         : (qm == 6 ? modulation_scheme::QAM64
                                                    : (qm == 4 ? modulation_scheme::QAM16 : modulation_scheme::QPSK));
+  dmrs_pusch_estimator_impl& est      = *ests[compensate_cfo ? 1 : 0];
+  const int                  nof_dmrs = __builtin_popcount(dmrs_mask);
+  symbol_slot_mask           dmrs_pos(14);
+  for (unsigned l = 0; l != 14; ++l) {
+    dmrs_pos.set(l, ((dmrs_mask >> l) & 1U) != 0);
+  }
   std::vector<cf_t> buf(slot_size);
-  auto              t0 = clk::now();
+  size_t            llr_pos = 0;
+  auto              t0      = clk::now();
   for (unsigned p = 0; p != 4; ++p) {
     std::copy(reinterpret_cast<const cf_t*>(samples_in) + p * slot_size,
               reinterpret_cast<const cf_t*>(samples_in) + (p + 1) * slot_size,
@@ -234,8 +253,7 @@ long long ref_ul_slot_timed(int          nof_ues,
     cfg.sequence_config = seq;
     cfg.scaling         = 1.4125375F;
     cfg.c_prefix        = cyclic_prefix::NORMAL;
-    cfg.symbols_mask    = bounded_bitset<MAX_NSYMB_PER_SLOT>(14);
-    cfg.symbols_mask.set(2);
+    cfg.symbols_mask    = dmrs_pos;
     cfg.rb_mask = crb_bitmap(273);
     cfg.rb_mask.fill(rb_start[u], rb_start[u] + nof_rb[u]);
     cfg.first_symbol = 0;
@@ -244,7 +262,7 @@ long long ref_ul_slot_timed(int          nof_ues,
       cfg.rx_ports.push_back(p);
     }
     auto t1 = clk::now();
-    est->estimate(ce, grid.get_reader(), cfg);
+    est.estimate(ce, grid.get_reader(), cfg);
     chest += ns_since(t1);
 
     pusch_demodulator::configuration dcfg;
@@ -253,8 +271,7 @@ long long ref_ul_slot_timed(int          nof_ues,
     dcfg.modulation         = mod;
     dcfg.start_symbol_index = 0;
     dcfg.nof_symbols        = 14;
-    dcfg.dmrs_symb_pos      = symbol_slot_mask(14);
-    dcfg.dmrs_symb_pos.set(2);
+    dcfg.dmrs_symb_pos      = dmrs_pos;
     dcfg.dmrs_config_type            = dmrs_type::TYPE1;
     dcfg.nof_cdm_groups_without_data = 2;
     dcfg.n_id                        = 500;
@@ -263,8 +280,12 @@ long long ref_ul_slot_timed(int          nof_ues,
     for (uint8_t p = 0; p != 4; ++p) {
       dcfg.rx_ports.push_back(p);
     }
-    sink_buffer cw(static_cast<unsigned>(nof_rb[u] * 12 * 13 * qm));
+    sink_buffer cw(static_cast<unsigned>(nof_rb[u] * 12 * (14 - nof_dmrs) * qm));
     demod->demodulate(cw, notifier, grid.get_reader(), ce, dcfg);
+    if (llr_out != nullptr) {
+      std::memcpy(llr_out + llr_pos, cw.data.data(), cw.data.size());
+      llr_pos += cw.data.size();
+    }
   }
   *out_chest_ns = chest;
   return ns_since(t0);

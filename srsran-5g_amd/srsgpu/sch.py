@@ -177,9 +177,12 @@ class UeGrant:
         return segment(tbs, base_graph(tbs, self.r1024 / 1024.0), self.qm, self.nof_layers, self.nof_ch_symbols)
 
 
-def slot_100mhz_4x4(nof_ues: int = 64, mcs: int = 27, nof_prb: int = 273, nof_layers: int = 4) -> List[UeGrant]:
-    """n78 100 MHz (30 kHz SCS, 273 PRB) slot shared by `nof_ues` UEs, 4 layers, MCS table 2 (256QAM)."""
+def slot_100mhz_4x4(nof_ues: int = 64, mcs: int = 27, nof_prb: int = 273, nof_layers: int = 4,
+                    nof_dmrs_symbols: int = 1) -> List[UeGrant]:
+    """n78 100 MHz (30 kHz SCS, 273 PRB) slot shared by `nof_ues` UEs, `nof_layers` layers, MCS table 2 (256QAM),
+    `nof_dmrs_symbols` DM-RS symbols (type 1, two CDM groups without data)."""
     qm, r = MCS_TABLE_256QAM[mcs]
     base = nof_prb // nof_ues
     extra = nof_prb - base * nof_ues
-    return [UeGrant(base + (1 if i < extra else 0), nof_layers, qm, r) for i in range(nof_ues)]
+    return [UeGrant(base + (1 if i < extra else 0), nof_layers, qm, r, nof_dmrs_symbols=nof_dmrs_symbols)
+            for i in range(nof_ues)]

@@ -26,7 +26,8 @@ except ImportError:  # pragma: no cover
 NUMEROLOGY = 1            # 30 kHz
 DFT_SIZE = 4096           # 122.88 Msps
 CENTER_FREQ_HZ = 3.5e9    # n78
-DMRS_SYMBOL = 2           # one DM-RS symbol, type 1, two CDM groups without data
+DMRS_SYMBOL = 2           # first DM-RS symbol, type 1, two CDM groups without data
+DMRS_POS1 = (1 << 2) | (1 << 11)  # dmrs-AdditionalPosition pos1: DM-RS symbols 2 and 11
 DMRS_BETA = 10 ** (3 / 20)  # PUSCH / PDSCH DM-RS to data EPRE with two CDM groups without data (TS 38.214 6.2.2)
 TX_SCALE = 1.0 / 64       # OFDM modulator output scaling
 
@@ -39,13 +40,15 @@ class CellSlots:
     nof_slots: int
     grid_prb: int = 273
     nof_ports: int = 4
+    dmrs_mask: int = 1 << DMRS_SYMBOL
+    rb_first: int = 0  # first RB of the first UE (a rank's share of the UEs when a slot is sharded by UE)
 
     @property
     def nsc(self):
         return 12 * self.grid_prb
 
     def rb_starts(self):
-        out, rb = [], 0
+        out, rb = [], self.rb_first
         for u in self.ues:
             out.append(rb)
             rb += u.n_prb
@@ -85,11 +88,11 @@ class DownlinkPipeline:
                 mods.append(srsgpu.PdschModulation(
                     rnti=rnti0 + i, n_id=n_id, modulation_order=u.qm, nof_layers=u.nof_layers,
                     nof_ports=cell.nof_ports, bwp_start_rb=0, bwp_size_rb=cell.grid_prb, rb_start=rb0[i],
-                    nof_rb=u.n_prb, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=1 << DMRS_SYMBOL, dmrs_type=1,
+                    nof_rb=u.n_prb, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=cell.dmrs_mask, dmrs_type=1,
                     nof_cdm_groups_without_data=2, scaling=1.0, weights=w))
                 dmrs.append(srsgpu.PdschDmrs(
                     slot_index=cell.slot_index(s), scrambling_id=scrambling_id, n_scid=0, dmrs_type=1,
-                    nof_layers=u.nof_layers, nof_ports=cell.nof_ports, dmrs_symbol_mask=1 << DMRS_SYMBOL,
+                    nof_layers=u.nof_layers, nof_ports=cell.nof_ports, dmrs_symbol_mask=cell.dmrs_mask,
                     reference_point_k_rb=0, rb_start=rb0[i], nof_rb=u.n_prb, amplitude=DMRS_BETA, weights=w))
                 grid_idx.append(s)
         self.modulator = srsgpu.PdschModulatorPlan(ctx, srsgpu.make_pdsch_mod_configs(mods, self.cw_offsets, grid_idx),
@@ -120,10 +123,12 @@ class UplinkPipeline:
     """OFDM demodulator -> DM-RS channel estimator -> PUSCH demodulator -> PUSCH decoder for every UE of every slot.
     The channel-estimate, noise-variance, LLR, HARQ and TB buffers are owned by the pipeline. `estimate_layout`:
     srsgpu.CE_COMPACT (default: the "average" strategy's one estimate per allocation, stored once) or
-    srsgpu.CE_PER_SYMBOL (the reference's channel_estimate layout); the LLRs are identical."""
+    srsgpu.CE_PER_SYMBOL (the reference's channel_estimate layout); the LLRs are identical. The estimator runs du_low's
+    defaults (du_low_config.h:51-69): "filter" smoothing, "average" time strategy and, with compensate_cfo, CFO
+    compensation (which acts when the cell has two or more DM-RS symbols)."""
 
     def __init__(self, ctx, cell: CellSlots, iterations=6, rnti0=0x4601, n_id=500, scrambling_id=500,
-                 equalizer=srsgpu.EQ_MMSE, estimate_layout=srsgpu.CE_COMPACT):
+                 equalizer=srsgpu.EQ_MMSE, estimate_layout=srsgpu.CE_COMPACT, compensate_cfo=True):
         self.ctx, self.cell, self.estimate_layout = ctx, cell, estimate_layout
         S, ues, segs = cell.nof_slots, cell.ues, cell.segs
         rb0 = cell.rb_starts()
@@ -135,14 +140,15 @@ class UplinkPipeline:
             for i, u in enumerate(ues):
                 ests.append(srsgpu.PuschChannelEstimation(
                     scrambling_id=scrambling_id, n_scid=0, dmrs_type=1, nof_tx_layers=u.nof_layers,
-                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=1 << DMRS_SYMBOL,
+                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=cell.dmrs_mask,
                     rb_start=rb0[i], nof_rb=u.n_prb, slot_index=cell.slot_index(s), scaling=DMRS_BETA,
-                    estimate_layout=estimate_layout))
+                    estimate_layout=estimate_layout, compensate_cfo=int(compensate_cfo), numerology=NUMEROLOGY))
                 dems.append(srsgpu.PuschDemodulation(
                     rnti=rnti0 + i, n_id=n_id, modulation_order=u.qm, nof_tx_layers=u.nof_layers,
-                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=1 << DMRS_SYMBOL,
+                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=cell.dmrs_mask,
                     dmrs_type=1, nof_cdm_groups_without_data=2, rb_start=rb0[i], nof_rb=u.n_prb,
-                    equalizer=equalizer, estimate_layout=estimate_layout))
+                    equalizer=equalizer, estimate_layout=estimate_layout, cfo_compensated=int(compensate_cfo),
+                    numerology=NUMEROLOGY))
                 grid_idx.append(s)
         self.chest = srsgpu.PuschChannelEstimatorPlan(ctx, srsgpu.make_pusch_chest_configs(ests, grid_idx),
                                                       cell.grid_prb, cell.nof_ports)
@@ -184,11 +190,12 @@ class UplinkPipeline:
 
 
 def synthesize_uplink(ctx, cell: CellSlots, d_tbs, snr_db=35.0, seed=0, rnti0=0x4601, n_id=500,
-                      scrambling_id=500):
+                      scrambling_id=500, cfo_hz_max=0.0):
     """Test input: the UEs' PUSCH transmissions (the same LDPC / rate matching / scrambling / modulation / layer
     mapping as the PDSCH chain, DM-RS ports 1000..1003 with amplitude beta) through a per-UE random unitary 4x4 MIMO
-    channel (flat over the UE's RBs, a random phase ramp across them) plus AWGN at `snr_db`, OFDM-modulated into the
-    received baseband samples of every slot. Returns the device sample buffer (complex float pairs)."""
+    channel (flat over the UE's RBs, a random phase ramp across them), a per-UE carrier frequency offset uniform in
+    +-cfo_hz_max (each OFDM symbol rotated by 2 pi cfo t_l) plus AWGN at `snr_db`, OFDM-modulated into the received
+    baseband samples of every slot. Returns the device sample buffer (complex float pairs)."""
     dev = torch.device("cuda", ctx.device)
     ue_tx = DownlinkPipeline(ctx, cell, weights=None, rnti0=rnti0, n_id=n_id, scrambling_id=scrambling_id)
     stream = torch.cuda.current_stream(dev)
@@ -213,6 +220,21 @@ def synthesize_uplink(ctx, cell: CellSlots, d_tbs, snr_db=35.0, seed=0, rnti0=0x
         H[k0:k1] = q[None] * ramp[:, None, None]
         k0 = k1
     y = torch.einsum("kpl,slmk->spmk", H, x)
+    if cfo_hz_max > 0:
+        t = torch.zeros(14, dtype=torch.float64)
+        scs_hz = (15 << NUMEROLOGY) * 1000.0
+        for i in range(14):  # symbol start epochs in symbol durations (normal CP)
+            kappa = (144 >> NUMEROLOGY) + (16 if i in (0, 7 << NUMEROLOGY) else 0)
+            d = kappa * 64 / (480000 * 4096) * scs_hz
+            t[i] = d if i == 0 else t[i - 1] + d + 1.0
+        cfo = torch.zeros(nsc, dtype=torch.float64)
+        k0 = 0
+        for ue in cell.ues:
+            k1 = k0 + 12 * ue.n_prb
+            cfo[k0:k1] = (float(torch.rand(1, generator=gen, device=dev)) * 2 - 1) * cfo_hz_max / scs_hz
+            k0 = k1
+        rot = torch.exp(2j * torch.pi * t[:, None] * cfo[None, :]).to(torch.complex64).to(dev)  # (14, nsc)
+        y = y * rot[None, None]
     nv = 10 ** (-snr_db / 10)
     y = y + torch.complex(torch.randn(y.shape, generator=gen, device=dev),
                           torch.randn(y.shape, generator=gen, device=dev)) * float(np.sqrt(nv / 2))

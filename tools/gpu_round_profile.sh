@@ -1,18 +1,30 @@
 #!/usr/bin/env bash
-# One GPU-box session: parity tests, the default bench (with the CPU reference baseline), a rocprofv3 kernel-trace
-# --stats pass of the bench, and FETCH_SIZE / WRITE_SIZE PMC passes (separate, per MI355X_MICROARCH.md) for the
-# decoder's HBM traffic. Outputs under gpurun_out/round/. Every GPU step has its own time limit; steps are chained.
+# One GPU-box session: the default bench (with the CPU reference baseline), a rocprofv3 kernel-trace --stats pass of
+# the bench, FETCH_SIZE / WRITE_SIZE PMC passes (separate, per MI355X_MICROARCH.md) for the decoder's HBM traffic and
+# an SQ counter pass (VALU issue). Outputs under gpurun_out/$1 (default round). Every GPU step has its own time limit;
+# steps are chained (set -e).
 set -euo pipefail
-OUT=gpurun_out/round
+OUT=gpurun_out/${1:-round}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > "$OUT/gpu_tests.log" 2>&1
+R=$(pwd)
+PB="--no-cpu-baseline --no-extra-points --steps 40 --warmup 4"
 timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 > "$OUT/stats_bench.json" 2> "$OUT/stats.err"
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/$OUT/stats" -o run --output-format csv -- \
+  python3 "$R/bench.py" $PB > "$OUT/stats_bench.json" 2> "$OUT/stats.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$R/$OUT/pmc_fetch" -o run --output-format csv -- \
+  python3 "$R/bench.py" $PB > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$R/$OUT/pmc_write" -o run --output-format csv -- \
+  python3 "$R/bench.py" $PB > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+  SQ_ACTIVE_INST_ANY SQ_INSTS_LDS -d "$R/$OUT/pmc_sq" -o run --output-format csv -- \
+  python3 "$R/bench.py" $PB > "$OUT/pmc_sq.json" 2> "$OUT/pmc_sq.err"
 python tools/traffic_from_pmc.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/stats_bench.json" "$OUT/traffic.json" \
   > "$OUT/traffic.log" 2>&1
+SQ_CSV=$(python -c 'import glob, sys; print(glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)[0])' "$OUT/pmc_sq")
+python tools/sq_summary.py "$SQ_CSV" \
+  "$OUT/sq_valu.json" "$OUT/stats_bench.json" > "$OUT/sq.log" 2>&1
+# Keep the summaries (kernel stats, traffic, SQ) and drop the bulky per-dispatch traces before gpurun copies back.
+find "$OUT" -name "*kernel_trace.csv" -delete
+find "$OUT" -name "*counter_collection.csv" -size +2M -delete
+du -sh "$OUT"

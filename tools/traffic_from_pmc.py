@@ -34,10 +34,11 @@ def main():
     write_kb, nw, _ = per_dispatch(write_dir, "WRITE_SIZE", k)
     bench = json.loads(open(bench_json).read().strip().splitlines()[-1])
     alg = bench["roofline"]["achieved"] * 1e9 * bench["roofline"]["kernel_ms_per_launch"] * 1e-3
+    snr = bench["operating_points"][0]["snr_db"]
     res = {
         "kernel": kn[0] if kn else k,
-        "slots_per_step": bench["config"]["slots_per_step"],
-        "worst_case": "never CRC-valid" in bench["data"],
+        "workload": f"{bench['config']['profile']}/S{bench['config']['slots_per_step']}/"
+                    f"{'noise' if snr is None else f'{snr:g}dB'}",  # bench.py matches it before using the numbers
         "dispatches_fetch": nf,
         "dispatches_write": nw,
         "fetch_size_kb_raw": fetch_kb,

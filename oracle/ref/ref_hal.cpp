@@ -1,0 +1,247 @@
+// TEST INFRASTRUCTURE ONLY: C entry points that run the reference's own transport-block processors with the GPU
+// bindings of integration/ plugged in through the reference's interfaces, and the reference's CPU implementations
+// beside them, on the same inputs (built by oracle/build_hal.sh into oracle/_ref/libsrshal.so; tests/test_hal_gpu.py):
+//
+//   PUSCH decoder, mode 0: pusch_decoder_impl (pusch_decoder_impl.cpp) with the reference's pusch_codeblock_decoder
+//                          (AVX2 rate dematcher + AVX-512 / AVX2 LDPC decoder) - the CPU path;
+//                  mode 1: the same pusch_decoder_impl, its ldpc_decoder replaced by integration/ldpc_decoder_gpu.cpp;
+//                  mode 2: pusch_decoder_hw_impl (pusch_decoder_hw_impl.cpp) over the GPU hal::hw_accelerator_pusch_dec
+//                          of integration/hw_accelerator_pusch_dec_gpu.cpp (HARQ soft buffers in HBM);
+//   PDSCH encoder, mode 0: pdsch_encoder_impl (AVX2 LDPC encoder); mode 1: pdsch_encoder_hw_impl over the GPU
+//                          hal::hw_accelerator_pdsch_enc (integration/hw_accelerator_pdsch_enc_gpu.cpp).
+//
+// The rx buffers are a minimal unique_rx_buffer::callback (soft bits, data bits, CRC flags per codeblock, absolute
+// codeblock identifiers harq_id * 160 + cb), one per (mode, HARQ process), so retransmissions combine like the pool's.
+#include "hw_accelerator_pusch_dec_gpu.h"
+
+#include "srsran/phy/upper/channel_coding/channel_coding_factories.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_decoder_notifier.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_decoder_result.h"
+#include "srsran/phy/upper/unique_rx_buffer.h"
+
+#include "lib/phy/upper/channel_coding/crc_calculator_generic_impl.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_decoder_avx2.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_decoder_avx512.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_encoder_avx2.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_rate_dematcher_avx2_impl.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_rate_matcher_impl.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_segmenter_rx_impl.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_segmenter_tx_impl.h"
+#include "lib/phy/upper/channel_processors/pdsch/pdsch_encoder_hw_impl.h"
+#include "lib/phy/upper/channel_processors/pdsch/pdsch_encoder_impl.h"
+#include "lib/phy/upper/channel_processors/pusch/pusch_codeblock_decoder.h"
+#include "lib/phy/upper/channel_processors/pusch/pusch_decoder_hw_impl.h"
+#include "lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.h"
+
+#include <map>
+#include <memory>
+#include <vector>
+
+namespace srsran {
+std::shared_ptr<ldpc_decoder_factory> create_ldpc_decoder_factory_gpu(int device);
+}
+
+using namespace srsran;
+
+namespace {
+
+constexpr unsigned CB_IDS_PER_HARQ = 160;  // >= MAX_NOF_SEGMENTS
+
+class test_rx_buffer : public unique_rx_buffer::callback
+{
+public:
+  test_rx_buffer(unsigned nof_cbs, unsigned first_abs_id) :
+    crcs(nof_cbs, false), soft(nof_cbs, std::vector<log_likelihood_ratio>(66 * 384)),
+    data(nof_cbs, std::vector<uint8_t>(22 * 384 / 8)), abs0(first_abs_id)
+  {
+  }
+  unsigned   get_nof_codeblocks() const override { return static_cast<unsigned>(crcs.size()); }
+  void       reset_codeblocks_crc() override { std::fill(crcs.begin(), crcs.end(), false); }
+  span<bool> get_codeblocks_crc() override { return span<bool>(reinterpret_cast<bool*>(crcs.data()), crcs.size()); }
+  unsigned   get_absolute_codeblock_id(unsigned cb) const override { return abs0 + cb; }
+  span<log_likelihood_ratio> get_codeblock_soft_bits(unsigned cb, unsigned size) override
+  {
+    return span<log_likelihood_ratio>(soft[cb]).first(size);
+  }
+  bit_buffer get_codeblock_data_bits(unsigned cb, unsigned size) override
+  {
+    return bit_buffer::from_bytes(data[cb]).first(size);
+  }
+  bool       try_lock() override { return true; }
+  void       unlock() override {}
+  void       release() override { reset_codeblocks_crc(); }
+
+private:
+  std::vector<char>                              crcs;  // storage for span<bool>
+  std::vector<std::vector<log_likelihood_ratio>> soft;
+  std::vector<std::vector<uint8_t>>              data;
+  unsigned                                       abs0;
+};
+
+class result_capture : public pusch_decoder_notifier
+{
+public:
+  void on_sch_data(const pusch_decoder_result& r) override
+  {
+    result = r;
+    done   = true;
+  }
+  pusch_decoder_result result;
+  bool                 done = false;
+};
+
+template <typename S>
+S make_sch_crc()
+{
+  S s;
+  s.crc16  = std::make_unique<crc_calculator_generic_impl>(crc_generator_poly::CRC16);
+  s.crc24A = std::make_unique<crc_calculator_generic_impl>(crc_generator_poly::CRC24A);
+  s.crc24B = std::make_unique<crc_calculator_generic_impl>(crc_generator_poly::CRC24B);
+  return s;
+}
+
+std::unique_ptr<ldpc_decoder> cpu_decoder()
+{
+  if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw")) {
+    return std::make_unique<ldpc_decoder_avx512>();
+  }
+  return std::make_unique<ldpc_decoder_avx2>();
+}
+
+struct hal_harness {
+  std::shared_ptr<ldpc_decoder_factory>                   gpu_ldpc;
+  std::shared_ptr<hal::hw_accelerator_pusch_dec_factory>  gpu_dec;
+  std::shared_ptr<hal::hw_accelerator_pdsch_enc_factory>  gpu_enc;
+  std::unique_ptr<pusch_decoder>                          dec[3];
+  std::unique_ptr<pdsch_encoder>                          enc[2];
+  std::map<std::pair<int, unsigned>, std::unique_ptr<test_rx_buffer>> rx;
+};
+
+std::unique_ptr<pusch_decoder> make_sw_decoder(std::unique_ptr<ldpc_decoder> ldpc)
+{
+  auto cb_crc = make_sch_crc<pusch_codeblock_decoder::sch_crc>();
+  std::vector<std::unique_ptr<pusch_codeblock_decoder>> cbs;
+  cbs.push_back(std::make_unique<pusch_codeblock_decoder>(std::make_unique<ldpc_rate_dematcher_avx2_impl>(),
+                                                          std::move(ldpc), cb_crc));
+  auto pool = std::make_shared<pusch_decoder_impl::codeblock_decoder_pool>(std::move(cbs));
+  return std::make_unique<pusch_decoder_impl>(std::make_unique<ldpc_segmenter_rx_impl>(), pool,
+                                              make_sch_crc<pusch_decoder_impl::sch_crc>(), nullptr, 275, 4);
+}
+
+} // namespace
+
+extern "C" {
+
+void* hal_create(int device, unsigned max_cb_ids)
+{
+  auto* h     = new hal_harness();
+  h->gpu_ldpc = create_ldpc_decoder_factory_gpu(device);
+  h->gpu_dec  = hal::create_hw_accelerator_pusch_dec_factory_gpu(device, max_cb_ids);
+  h->gpu_enc  = hal::create_hw_accelerator_pdsch_enc_factory_gpu(device);
+  h->dec[0]   = make_sw_decoder(cpu_decoder());
+  h->dec[1]   = make_sw_decoder(h->gpu_ldpc->create());
+  {
+    std::vector<std::unique_ptr<hal::hw_accelerator_pusch_dec>> accs;
+    accs.push_back(h->gpu_dec->create());
+    auto pool  = std::make_shared<pusch_decoder_hw_impl::hw_decoder_pool>(std::move(accs));
+    auto crcs  = make_sch_crc<pusch_decoder_hw_impl::sch_crc>();
+    h->dec[2]  = std::make_unique<pusch_decoder_hw_impl>(std::make_unique<ldpc_segmenter_rx_impl>(), crcs, pool, nullptr);
+  }
+  {
+    auto seg_crc = make_sch_crc<ldpc_segmenter_tx_impl::sch_crc>();
+    h->enc[0]    = std::make_unique<pdsch_encoder_impl>(std::make_unique<ldpc_segmenter_tx_impl>(seg_crc),
+                                                     std::make_unique<ldpc_encoder_avx2>(),
+                                                     std::make_unique<ldpc_rate_matcher_impl>());
+    auto seg_crc2 = make_sch_crc<ldpc_segmenter_tx_impl::sch_crc>();
+    auto crcs     = make_sch_crc<pdsch_encoder_hw_impl::sch_crc>();
+    h->enc[1]     = std::make_unique<pdsch_encoder_hw_impl>(crcs, std::make_unique<ldpc_segmenter_tx_impl>(seg_crc2),
+                                                        h->gpu_enc->create());
+  }
+  return h;
+}
+
+void hal_destroy(void* p)
+{
+  delete static_cast<hal_harness*>(p);
+}
+
+/// pusch_decoder::new_data + on_new_softbits + on_end_softbits of one transport block (synchronous: no executor).
+/// stats[] = {tb_crc_ok, nof_codeblocks_total, ldpc observations, min, max, mean iterations}. Returns 0, or -1 when
+/// the decoder did not notify.
+int hal_pusch_decode(void*          p,
+                     int            mode,
+                     unsigned       harq_id,
+                     unsigned       nof_cbs,
+                     int            bg,
+                     int            rv,
+                     int            qm,
+                     int            nof_layers,
+                     unsigned       Nref,
+                     int            max_iter,
+                     int            early_stop,
+                     int            new_data,
+                     const int8_t*  llrs,
+                     unsigned       nof_llrs,
+                     uint8_t*       tb,
+                     unsigned       tb_bytes,
+                     double*        stats)
+{
+  auto* h   = static_cast<hal_harness*>(p);
+  auto  key = std::make_pair(mode, harq_id);
+  auto  it  = h->rx.find(key);
+  if (it == h->rx.end() || it->second->get_nof_codeblocks() != nof_cbs) {
+    h->rx[key] = std::make_unique<test_rx_buffer>(nof_cbs, harq_id * CB_IDS_PER_HARQ);
+  }
+  pusch_decoder::configuration cfg;
+  cfg.base_graph          = bg == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2;
+  cfg.rv                  = rv;
+  cfg.mod                 = static_cast<modulation_scheme>(qm);
+  cfg.Nref                = Nref;
+  cfg.nof_layers          = nof_layers;
+  cfg.nof_ldpc_iterations = max_iter;
+  cfg.use_early_stop      = early_stop != 0;
+  cfg.new_data            = new_data != 0;
+  result_capture        notifier;
+  pusch_decoder_buffer& buf = h->dec[mode]->new_data(span<uint8_t>(tb, tb_bytes), unique_rx_buffer(*h->rx[key]),
+                                                     notifier, cfg);
+  buf.on_new_softbits(span<const log_likelihood_ratio>(reinterpret_cast<const log_likelihood_ratio*>(llrs), nof_llrs));
+  buf.on_end_softbits();
+  if (!notifier.done) {
+    return -1;
+  }
+  const auto& r = notifier.result;
+  stats[0]      = r.tb_crc_ok ? 1 : 0;
+  stats[1]      = r.nof_codeblocks_total;
+  stats[2]      = r.ldpc_decoder_stats.get_nof_observations();
+  stats[3]      = r.ldpc_decoder_stats.get_nof_observations() ? r.ldpc_decoder_stats.get_min() : -1;
+  stats[4]      = r.ldpc_decoder_stats.get_nof_observations() ? r.ldpc_decoder_stats.get_max() : -1;
+  stats[5]      = r.ldpc_decoder_stats.get_nof_observations() ? r.ldpc_decoder_stats.get_mean() : -1;
+  return 0;
+}
+
+/// pdsch_encoder::encode of one transport block into cw (G = nof_ch_symbols x Qm bits, one per byte).
+int hal_pdsch_encode(void*          p,
+                     int            mode,
+                     int            bg,
+                     int            rv,
+                     int            qm,
+                     int            nof_layers,
+                     unsigned       nof_ch_symbols,
+                     unsigned       Nref,
+                     const uint8_t* tb,
+                     unsigned       tb_bytes,
+                     uint8_t*       cw)
+{
+  auto*                        h = static_cast<hal_harness*>(p);
+  pdsch_encoder::configuration cfg;
+  cfg.base_graph     = bg == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2;
+  cfg.rv             = rv;
+  cfg.mod            = static_cast<modulation_scheme>(qm);
+  cfg.Nref           = Nref;
+  cfg.nof_layers     = nof_layers;
+  cfg.nof_ch_symbols = nof_ch_symbols;
+  h->enc[mode]->encode(span<uint8_t>(cw, nof_ch_symbols * qm), span<const uint8_t>(tb, tb_bytes), cfg);
+  return 0;
+}
+
+} // extern "C"

@@ -1,0 +1,80 @@
+"""Processor / HAL-level drop-in on the GPU: the reference's OWN transport-block processors (compiled from its sources
+by oracle/build_hal.sh) drive the MI355X through the bindings a maintainer adds (integration/), and their results are
+compared with the reference's CPU processors on the same inputs, through the same harness (tests/hal_lib.py):
+
+  * pusch_decoder_hw_impl over hal::hw_accelerator_pusch_dec (integration/hw_accelerator_pusch_dec_gpu.cpp, HARQ soft
+    buffers in HBM) and pusch_decoder_impl with the GPU ldpc_decoder (integration/ldpc_decoder_gpu.cpp) against
+    pusch_decoder_impl with the reference's AVX-512 / AVX2 decoder: TB bytes, TB CRC flag and the LDPC iteration
+    statistics (count, min, max, mean) equal, new transmissions and rv2 retransmissions (HARQ combining);
+  * pdsch_encoder_hw_impl over hal::hw_accelerator_pdsch_enc (integration/hw_accelerator_pdsch_enc_gpu.cpp) against
+    pdsch_encoder_impl (AVX2 encoder): codewords bit-exact.
+
+Grants: random TB sizes (CRC16 / CRC24A single-codeblock, CRC24B segmented, BG1 / BG2), BASELINE configs[1] (20 MHz
+SISO 64QAM PDSCH) and configs[2] (100 MHz 2x2 256QAM PUSCH) and the bench slot's UE grants."""
+import numpy as np
+import pytest
+
+from chain_lib import bits_to_llrs, oracle_pdsch_encode
+from oracle_lib import Oracle
+from srsgpu import sch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hal():
+    import hal_lib
+    h = hal_lib.Hal(0)
+    yield h
+    h.close()
+
+
+def grants(rng):
+    tables = list(sch.MCS_TABLE_256QAM.values())
+    out = []
+    for _ in range(24):
+        qm, r = tables[int(rng.integers(0, len(tables)))]
+        out.append(sch.UeGrant(int(rng.integers(1, 60)), int(rng.integers(1, 5)), qm, r,
+                               nof_symb_sh=int(rng.integers(4, 15))))
+    out += sch.slot_100mhz_4x4(nof_ues=8, nof_prb=51, nof_layers=1, mcs=20)       # configs[1]-like: SISO, 64QAM
+    out += sch.slot_100mhz_4x4(nof_ues=4, nof_prb=273, nof_layers=2, mcs=27)[:4]  # configs[2]: 100 MHz 2x2 256QAM
+    out += sch.slot_100mhz_4x4(nof_layers=1, nof_dmrs_symbols=2)[:6]             # the bench slot's UL grants
+    return out
+
+
+def test_hal_pusch_decoder_gpu_equals_reference_cpu(hal):
+    import hal_lib
+    orc = Oracle()
+    rng = np.random.default_rng(21)
+    gs = grants(rng)
+    n_ok = 0
+    for i, g in enumerate(gs):
+        seg = g.segmentation()
+        tb = rng.integers(0, 256, seg.tbs // 8).astype(np.uint8)
+        noise = [0.0, 5.0, 8.0, 11.0][i % 4]
+        for rv, new_data in ((0, True), (2, False)):
+            cw, _, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, rv, g.qm, g.nof_layers, 0, g.nof_ch_symbols)
+            llr = bits_to_llrs(rng, cw, amp=6.0, noise=noise)
+            res = [hal.pusch_decode(m, i, seg.nof_segments, seg.base_graph, rv, g.qm, g.nof_layers, llr, seg.tbs // 8,
+                                    new_data=new_data)
+                   for m in (hal_lib.PUSCH_CPU, hal_lib.PUSCH_SW_GPU_LDPC, hal_lib.PUSCH_HW_GPU)]
+            (tb0, s0), (tb1, s1), (tb2, s2) = res
+            assert s1 == s0, (i, rv, s0, s1)
+            assert s2 == s0, (i, rv, s0, s2)
+            if s0["tb_crc_ok"]:
+                assert np.array_equal(tb0, tb) and np.array_equal(tb1, tb) and np.array_equal(tb2, tb), (i, rv)
+                n_ok += 1
+    assert n_ok >= 20
+
+
+def test_hal_pdsch_encoder_gpu_equals_reference_cpu(hal):
+    import hal_lib
+    rng = np.random.default_rng(22)
+    for i, g in enumerate(grants(rng)):
+        seg = g.segmentation()
+        tb = rng.integers(0, 256, seg.tbs // 8).astype(np.uint8)
+        rv = i % 4
+        Nref = 0 if i % 3 else (seg.segment_length + (66 if seg.base_graph == 1 else 50) * seg.lifting_size) // 2
+        a = hal.pdsch_encode(hal_lib.PDSCH_CPU, seg.base_graph, rv, g.qm, g.nof_layers, g.nof_ch_symbols, tb, Nref)
+        b = hal.pdsch_encode(hal_lib.PDSCH_HW_GPU, seg.base_graph, rv, g.qm, g.nof_layers, g.nof_ch_symbols, tb, Nref)
+        assert np.array_equal(a, b), (i, seg.tbs, seg.nof_segments, rv, Nref)

@@ -10,10 +10,23 @@ REF = "/root/reference"
 
 
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "include", "srsran")), reason="reference tree absent")
-@pytest.mark.parametrize("src", ["ldpc_decoder_gpu.cpp"])
+@pytest.mark.parametrize("src", ["ldpc_decoder_gpu.cpp", "hw_accelerator_pusch_dec_gpu.cpp",
+                                 "hw_accelerator_pdsch_enc_gpu.cpp"])
 def test_binding_compiles_against_reference_headers(src, tmp_path):
     cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-fsyntax-only", "-DFMT_HEADER_ONLY",
            f"-I{REF}/include", f"-I{REF}/external/fmt/include", f"-I{REF}/external", f"-I{ROOT}/include",
-           "-I/opt/rocm/include", "-x", "c++", "-D__HIP_PLATFORM_AMD__", os.path.join(ROOT, "integration", src)]
+           f"-I{ROOT}/integration", "-I/opt/rocm/include", "-x", "c++", "-D__HIP_PLATFORM_AMD__", os.path.join(ROOT, "integration", src)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libsrshal.so")),
+                    reason="HAL harness not built (oracle/build_hal.sh)")
+def test_hal_harness_links_reference_processors_with_gpu_bindings():
+    """oracle/build_hal.sh links the reference's pusch_decoder_hw_impl / pdsch_encoder_hw_impl / pusch_decoder_impl /
+    pdsch_encoder_impl with the integration/ bindings (-Wl,--no-undefined): the library loads and exports the harness
+    entry points (no GPU call here; the GPU run is tests/test_hal_gpu.py)."""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libsrshal.so"))
+    for sym in ("hal_create", "hal_destroy", "hal_pusch_decode", "hal_pdsch_encode"):
+        assert hasattr(lib, sym)

@@ -210,6 +210,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--serial-legs", action="store_true",
                     help="run the DL and UL legs on one stream (clean per-stage times; slower overall)")
+    ap.add_argument("--pipeline", action=argparse.BooleanOptionalAction, default=True,
+                    help="replay each input set on its own stream (up to --input-sets steps in flight)")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
                     help="replay each set's DL+UL pipeline as one captured HIP graph (default) or launch eagerly")
     args = ap.parse_args()
@@ -269,14 +271,20 @@ def main():
         cur.wait_stream(dl_stream)
         cur.wait_stream(ul_stream)
 
+    # Pipelining across steps: each input set replays on its own stream, so a step's UL decode can overlap the next
+    # set's front end (different buffers; a set's consecutive steps stay ordered on its stream).
+    set_streams = [torch.cuda.Stream(dev) for _ in range(K)] if args.pipeline else None
+
     def step(i):
         st = sets[i % K]
-        if st.graph is not None:
-            st.graph.replay()
-        else:
-            pipeline(st)
-        if tb_gather is not None:
-            tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
+        cur = torch.cuda.current_stream(dev) if set_streams is None else set_streams[i % K]
+        with torch.cuda.stream(cur):
+            if st.graph is not None:
+                st.graph.replay()
+            else:
+                pipeline(st)
+            if tb_gather is not None:
+                tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
 
     for i in range(args.warmup):
         step(i)
@@ -464,6 +472,8 @@ def main():
                                               if ul.estimate_layout == srsgpu.CE_COMPACT else "per symbol",
                    "leg_streams": "one stream" if args.serial_legs else "DL and UL on concurrent streams",
                    "launch": "one captured HIP graph per step and input set" if args.graph else "eager launches",
+                   "pipelining": (f"up to {K} steps in flight: each input set's step runs on its own stream"
+                                  if args.pipeline else "steps serialised on one stream"),
                    "slots_per_step": S,
                    "input_sets": K,
                    "working_set_mb": K * set_bytes / 2 ** 20,

@@ -102,6 +102,7 @@ struct srsgpu_ldpc_decoder_plan {
     int       bg      = 1;
     bool      packed  = false;
     int       max_layers = 0;
+    int       split   = 1;   ///< 2: edge-split kernel (each row's edges over two wave halves), see upload_decoder_plan
     int       threads = 64;
     int       count   = 0;
     dec_desc* d_desc  = nullptr;
@@ -554,6 +555,19 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
     g.max_layers       = std::get<2>(kv.first);
     g.threads          = batch.threads.at(kv.first);
     g.count            = static_cast<int>(kv.second.size());
+    // Few codeblocks per launch leave the SIMDs with one or two waves each: the per-codeblock latency (instructions
+    // per wave) then sets the kernel time, and the edge-split kernel halves it at ~15 % more total work. Above ~3
+    // waves per SIMD of the plain kernel (MI355X: 1024 SIMDs) the launch is throughput-bound and keeps the plain one.
+    // SRSGPU_DECODER_SPLIT=0 / 1 forces either (A/B tests).
+    if (g.packed) {
+      const char* env    = std::getenv("SRSGPU_DECODER_SPLIT");
+      const long  waves  = static_cast<long>(g.count) * (g.threads / 64);
+      const bool  split2 = env != nullptr ? (env[0] == '1') : (waves < 3L * 1024L);
+      if (split2) {
+        g.split = 2;
+        g.threads *= 2;
+      }
+    }
     for (const dec_desc& d : kv.second) {
       plan->input_llrs += d.nof_llr;
     }
@@ -579,7 +593,7 @@ int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
 {
   for (const auto& g : plan->groups) {
     if (g.packed) {
-      launch_ldpc_decode_pk(g.bg, plan->impl, g.max_layers, g.d_desc, g.count, g.threads, d_llrs, d_out,
+      launch_ldpc_decode_pk(g.bg, plan->impl, g.max_layers, g.split, g.d_desc, g.count, g.threads, d_llrs, d_out,
                             d_nof_iterations,
                             plan->ctx->d_pair_ab[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s);
     } else {

@@ -239,6 +239,104 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   }
 }
 
+/// Edge-split layer update (SPLIT = 2 kernels): the workgroup's two halves own the same rows; the lanes of half 0
+/// process edges [0, ceil(deg / 2)) of their two rows, the lanes of half 1 the remaining edges, so each lane issues
+/// about half the VALU instructions of a layer (a lone wave issues one VALU per ~6.5 cycles: with few codeblocks per
+/// launch the per-codeblock latency, i.e. the instructions per wave, sets the kernel time). The two-minimum searches
+/// are merged through LDS between the two passes; keys carry the global edge index, so the merge is exactly the
+/// sequential scan. Each half keeps the sign bits of its own edges (at most 10: no hi word).
+constexpr int HALF_MAX = 10;
+
+struct half_state {
+  s16x2    v2c[HALF_MAX];
+  uint32_t addr[HALF_MAX];
+  u16x2    k1, k2;
+  uint32_t sx;
+};
+
+template <int BG, int MODE, int m, int EB, int EE>
+__device__ __forceinline__ void pass1_half(const int8_t* __restrict__ soft,
+                                           const_u32_ptr ab,
+                                           uint32_t      z2x2,
+                                           uint32_t      magw,
+                                           uint32_t      sgw,
+                                           half_state&   st)
+{
+  using G          = bg_t<BG>;
+  constexpr int e0 = G::rs(m);
+  static_assert(EE - EB <= HALF_MAX, "at most 10 edges per half row");
+  const u16x2 S1  = as_u16(magw & 0x007f007fu);
+  const u16x2 S2  = as_u16((magw >> 7) & 0x007f007fu);
+  const u16x2 D   = S1 - S2;
+  const u16x2 IDX = as_u16(sgw) >> uu(11);
+  uint32_t    one_bits = 0x00010001u;
+  asm("" : "+v"(one_bits));
+  const u16x2 one = as_u16(one_bits);
+  st.k1           = uu(KEY_INIT);
+  st.k2           = uu(KEY_INIT);
+  st.sx           = 0;
+  static_for<EE - EB>([&](auto E) {
+    constexpr int  j   = decltype(E)::value;
+    constexpr int  e   = EB + j;
+    constexpr int  col = G::col(e0 + e);
+    const uint32_t a   = pair_address(z2x2, ab[e0 + e]);
+    st.addr[j]         = a;
+    const s16x2 sb{static_cast<short>(soft[col * SOFT_COL_STRIDE + a]),
+                   static_cast<short>(soft[col * SOFT_COL_STRIDE + (a ^ 1u)])};
+    const s16x2 n   = (as_s16(sgw) << ss(15 - j)) >> ss(15);
+    const u16x2 ne  = not_argmin(IDX, e, one);
+    const u16x2 om  = ne * D + S2;
+    const s16x2 c   = as_s16(bits(om) ^ bits(n)) - n;
+    const s16x2 fin = clamp2(sb, -LLR_MAX, LLR_MAX);
+    const s16x2 v   = clamp2(sb - c, -LLR_MAX, LLR_MAX) + (sb - fin) * ss(512);
+    st.v2c[j]       = v;
+    const u16x2 key = __builtin_bit_cast(u16x2, __builtin_elementwise_max(v, -v)) * uu(32) + uu(e);
+    st.k2           = __builtin_elementwise_min(__builtin_elementwise_max(key, st.k1), st.k2);
+    st.k1           = __builtin_elementwise_min(key, st.k1);
+    st.sx ^= bits(v);
+  });
+}
+
+template <int BG, int MODE, int m, int EB, int EE>
+__device__ __forceinline__ void pass2_half(int8_t* __restrict__ soft,
+                                           const scale_t&    sc,
+                                           u16x2             k1,
+                                           u16x2             k2,
+                                           uint32_t          sx,
+                                           const half_state& st,
+                                           uint32_t&         magw,
+                                           uint32_t&         sgw)
+{
+  using G          = bg_t<BG>;
+  constexpr int e0 = G::rs(m);
+  uint32_t      one_bits = 0x00010001u;
+  asm("" : "+v"(one_bits));
+  const u16x2 one  = as_u16(one_bits);
+  const u16x2 IDXN = k1 & uu(31);
+  const u16x2 S1N  = scale_pk<MODE>(k1 >> uu(5), sc);
+  const u16x2 S2N  = scale_pk<MODE>(k2 >> uu(5), sc);
+  const u16x2 DN   = S1N - S2N;
+  uint32_t    nsg  = bits(IDXN << uu(11));
+  static_for<EE - EB>([&](auto E) {
+    constexpr int j   = decltype(E)::value;
+    constexpr int e   = EB + j;
+    constexpr int col = G::col(e0 + e);
+    const s16x2   v   = st.v2c[j];
+    const s16x2   n   = as_s16(sx ^ bits(v)) >> ss(15);
+    const u16x2   ne  = not_argmin(IDXN, e, one);
+    const u16x2   mag = ne * DN + S2N;
+    const s16x2   sgn = as_s16(bits(n) | 0x00010001u);
+    const s16x2   sb  = clamp2(as_s16(bits(mag)) * sgn + v, -SOFT_INF, SOFT_INF);
+    const uint32_t a  = st.addr[j];
+    soft[col * SOFT_COL_STRIDE + a]        = static_cast<int8_t>(sb.x);
+    soft[col * SOFT_COL_STRIDE + (a ^ 1u)] = static_cast<int8_t>(sb.y);
+    constexpr uint32_t mask = (1u << j) | (1u << (16 + j));
+    nsg |= bits(n) & mask;
+  });
+  magw = bits(S1N | (S2N << uu(7)));
+  sgw  = nsg;
+}
+
 /// LDS byte offset of position l (0 <= l < Z) inside a column.
 __device__ __forceinline__ uint32_t pair_pos(uint32_t l, uint32_t H)
 {
@@ -272,14 +370,14 @@ __device__ __forceinline__ void write_hard_bits_pk(const int8_t* __restrict__ so
 /// MAXL: compile-time bound on the number of layers (host-proven from the input length, dec_desc::nof_llr), so that
 /// only MAXL layers of check-to-variable state occupy VGPRs: the 4-layer high-rate codeblocks of a loaded cell run at
 /// twice the occupancy of the 46-layer worst case.
-template <int BG, int MODE, int MAXL>
+template <int BG, int MODE, int MAXL, int SPLIT>
 #ifndef LDPC_PK_MIN_BLOCKS_8
 #define LDPC_PK_MIN_BLOCKS_8 5
 #endif
 #ifndef LDPC_PK_KEEP_ADDR_MAXL
 #define LDPC_PK_KEEP_ADDR_MAXL 16
 #endif
-__global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_8))) void ldpc_decode_pk_kernel(const dec_desc* __restrict__ descs,
+__global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_8)))) void ldpc_decode_pk_kernel(const dec_desc* __restrict__ descs,
                                                              const int8_t* __restrict__ llrs,
                                                              uint8_t* __restrict__ out,
                                                              int32_t* __restrict__ results,
@@ -291,9 +389,12 @@ __global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : LDPC_PK_MIN_B
   // Only the first K + MAXL columns can be touched by MAXL layers: the soft-bit image shrinks with the layer bound
   // (11.8 KB for 8 layers of BG1 instead of 26 KB), so more codeblocks share a CU.
   constexpr int NCOL = G::K + MAXL;
-  __shared__ __attribute__((aligned(16))) int8_t smem[NCOL * SOFT_COL_STRIDE + SCRATCH_BYTES];
+  // SPLIT = 2: the halves exchange (k1, k2, sign parity) per row through MERGE_BYTES of LDS every layer.
+  constexpr int MERGE_BYTES = (SPLIT == 2) ? 2 * 192 * 16 : 0;
+  __shared__ __attribute__((aligned(16))) int8_t smem[NCOL * SOFT_COL_STRIDE + SCRATCH_BYTES + MERGE_BYTES];
   int8_t* soft    = smem;
   int*    scratch = reinterpret_cast<int*>(smem + NCOL * SOFT_COL_STRIDE);
+  uint4*  merge   = reinterpret_cast<uint4*>(smem + NCOL * SOFT_COL_STRIDE + SCRATCH_BYTES);
 
   DEC_STAMP(0);
   DEC_PROF(29, __builtin_amdgcn_s_memrealtime());
@@ -317,7 +418,10 @@ __global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : LDPC_PK_MIN_B
     constexpr int l = decltype(L)::value;
     scalar_touch<(l * 64 < AB_BYTES - 4) ? l * 64 : AB_BYTES - 4>(pf[l], ab);
   });
-  const int  z      = threadIdx.x;
+  // SPLIT = 2: threads [0, hb) and [hb, 2 hb) are the two edge halves of the same rows.
+  const int  hb     = (SPLIT == 2) ? static_cast<int>(blockDim.x) / 2 : static_cast<int>(blockDim.x);
+  const int  half   = (SPLIT == 2 && static_cast<int>(threadIdx.x) >= hb) ? 1 : 0;
+  const int  z      = static_cast<int>(threadIdx.x) - half * hb;
   const bool active = static_cast<uint32_t>(z) < H;
   const int  wave   = threadIdx.x / WAVE;
   const int  nwaves = blockDim.x / WAVE;
@@ -402,7 +506,7 @@ __global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : LDPC_PK_MIN_B
     }
   }
   // Zero the punctured columns 0, 1 and every position beyond the input.
-  if (active) {
+  if (active && half == 0) {
     auto* soft16 = reinterpret_cast<uint16_t*>(soft);
     soft16[(0 * SOFT_COL_STRIDE) / 2 + z] = 0;
     soft16[(1 * SOFT_COL_STRIDE) / 2 + z] = 0;
@@ -494,10 +598,39 @@ __global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : LDPC_PK_MIN_B
     static_for<MAXL>([&](auto Mi) {
       constexpr int m = decltype(Mi)::value;
       if (m < nl) {
-        if (active) {
-          __builtin_amdgcn_sched_barrier(0);
-          row_update_pk<BG, MODE, m, (MAXL <= LDPC_PK_KEEP_ADDR_MAXL)>(soft, abi, z2x2, sc, magw[m], sgw[m], hiw[m & 3]);
-          __builtin_amdgcn_sched_barrier(0);
+        if constexpr (SPLIT == 1) {
+          if (active) {
+            __builtin_amdgcn_sched_barrier(0);
+            row_update_pk<BG, MODE, m, (MAXL <= LDPC_PK_KEEP_ADDR_MAXL)>(soft, abi, z2x2, sc, magw[m], sgw[m],
+                                                                         hiw[m & 3]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else {
+          constexpr int deg = G::rs(m + 1) - G::rs(m);
+          constexpr int hm  = (deg + 1) / 2;
+          half_state    st;
+          if (active) {
+            if (half == 0) {
+              pass1_half<BG, MODE, m, 0, hm>(soft, abi, z2x2, magw[m], sgw[m], st);
+            } else {
+              pass1_half<BG, MODE, m, hm, deg>(soft, abi, z2x2, magw[m], sgw[m], st);
+            }
+            merge[half * hb + z] = make_uint4(bits(st.k1), bits(st.k2), st.sx, 0u);
+          }
+          __syncthreads();
+          if (active) {
+            const uint4 pr = merge[(1 - half) * hb + z];
+            const u16x2 pk1 = as_u16(pr.x), pk2 = as_u16(pr.y);
+            const u16x2 k1  = __builtin_elementwise_min(st.k1, pk1);
+            const u16x2 k2  = __builtin_elementwise_min(__builtin_elementwise_max(st.k1, pk1),
+                                                        __builtin_elementwise_min(st.k2, pk2));
+            const uint32_t sx = st.sx ^ pr.z;
+            if (half == 0) {
+              pass2_half<BG, MODE, m, 0, hm>(soft, sc, k1, k2, sx, st, magw[m], sgw[m]);
+            } else {
+              pass2_half<BG, MODE, m, hm, deg>(soft, sc, k1, k2, sx, st, magw[m], sgw[m]);
+            }
+          }
         }
 #ifndef LDPC_PK_EXPERIMENT_NO_LAYER_BARRIER  // timing experiments only: results are wrong without the barrier
         __syncthreads();
@@ -520,12 +653,16 @@ __global__ __launch_bounds__(192, (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : LDPC_PK_MIN_B
         uint32_t last_bit = static_cast<uint32_t>(nsig) - 1u;
         asm volatile("" : "+v"(zz));
         asm volatile("" : "+s"(ZZ), "+s"(HH), "+s"(last_bit));
-        uint32_t ia = zz;
-        static_for<G::K>([&](auto Ci) {
+        // SPLIT = 2: half 0 sums the first K / 2 columns, half 1 the rest (hcol = half x K / 2).
+        constexpr int KC   = (SPLIT == 2) ? G::K / 2 : G::K;
+        const int     hcol = half * KC;
+        uint32_t      ia   = zz + static_cast<uint32_t>(hcol) * ZZ;
+        const int8_t* scol = soft + hcol * SOFT_COL_STRIDE;
+        static_for<KC>([&](auto Ci) {
           constexpr int  c  = decltype(Ci)::value;
           const uint32_t ib = ia + HH;
-          const int      sa = soft[c * SOFT_COL_STRIDE + 2 * zz];
-          const int      sb = soft[c * SOFT_COL_STRIDE + 2 * zz + 1];
+          const int      sa = scol[c * SOFT_COL_STRIDE + 2 * zz];
+          const int      sb = scol[c * SOFT_COL_STRIDE + 2 * zz + 1];
           zero |= static_cast<uint32_t>(sa == 0) | static_cast<uint32_t>(sb == 0);
           const uint32_t ta = crc_table[ia < last_bit ? ia : last_bit];
           const uint32_t tb = crc_table[ib < last_bit ? ib : last_bit];
@@ -590,6 +727,7 @@ int debug_read_decoder_profile_pk(uint64_t* dst, size_t n)
 void launch_ldpc_decode_pk(int             bg,
                            int             mode,
                            int             max_layers,
+                           int             split,
                            const dec_desc* d_desc,
                            int             nof_cbs,
                            int             block_threads,
@@ -606,8 +744,10 @@ void launch_ldpc_decode_pk(int             bg,
   }
   dim3 grid(nof_cbs), block(block_threads);
 #define SRSGPU_PK_LAUNCH(BG_, MODE_, MAXL_)                                                                            \
-  ldpc_decode_pk_kernel<BG_, MODE_, MAXL_><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab,        \
-                                                                       d_crc_tables, d_cb_crc_ok)
+  (split == 2 ? ldpc_decode_pk_kernel<BG_, MODE_, MAXL_, 2><<<grid, block, 0, stream>>>(                              \
+                    d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables, d_cb_crc_ok)                               \
+              : ldpc_decode_pk_kernel<BG_, MODE_, MAXL_, 1><<<grid, block, 0, stream>>>(                              \
+                    d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables, d_cb_crc_ok))
   if (bg == 1) {
     if (max_layers <= 8) {
       mode == 1 ? SRSGPU_PK_LAUNCH(1, 1, 8) : SRSGPU_PK_LAUNCH(1, 0, 8);

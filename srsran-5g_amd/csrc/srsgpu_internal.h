@@ -164,11 +164,13 @@ int debug_read_decoder_profile(uint64_t* dst, size_t n);
 int debug_read_decoder_profile_pk(uint64_t* dst, size_t n);
 #endif
 
-/// Launches the packed two-rows-per-lane LDPC decoder (ldpc_decoder_pk.hip; even Z, block_threads >= Z / 2) built for
-/// at most max_layers layers (8, 16 or all; every codeblock of the launch must satisfy layers_bound() <= it).
+/// Launches the packed two-rows-per-lane LDPC decoder (ldpc_decoder_pk.hip; even Z, block_threads >= Z / 2, or
+/// >= 2 x 64 ceil(Z / 128) with split = 2) built for at most max_layers layers (8, 16 or all; every codeblock of the
+/// launch must satisfy layers_bound() <= it). split = 2: each row's edges are shared by two halves of the workgroup.
 void launch_ldpc_decode_pk(int             bg,
                            int             mode,
                            int             max_layers,
+                           int             split,
                            const dec_desc* d_desc,
                            int             nof_cbs,
                            int             block_threads,

@@ -235,6 +235,32 @@ typedef struct {
   uint32_t grid_index;                  /* resource grid (slot) the transmission is mapped into */
 } srsgpu_pdsch_mod_config;
 
+/* Generalised frequency allocation, reserved resource elements and per-PRG precoding of one transmission (the
+ * *_plan_create_ex entry points; a NULL extension array, or NULL members, keep the contiguous / no reserved REs /
+ * wideband defaults of the plain configuration).
+ *
+ * srsgpu_re_pattern mirrors srsran::re_pattern (include/srsran/phy/support/re_pattern.h): the REs of re_mask (bit k =
+ * subcarrier k of a PRB) in every CRB of crb_mask and every OFDM symbol of symbol_mask. */
+typedef struct {
+  const uint8_t* crb_mask;    /* one byte per grid CRB (nonzero = included); NULL = every CRB */
+  uint16_t       re_mask;     /* 12 bits */
+  uint16_t       symbol_mask; /* 14 bits */
+} srsgpu_re_pattern;
+
+typedef struct {
+  const uint8_t*           crb_mask;     /* allocated CRBs, one byte per grid CRB: rb_allocation::get_crb_mask of any
+                                            type-0 bitmap or interleaved VRB-to-PRB mapping (pdsch_modulator_impl.cpp:58,
+                                            pusch_demodulator.h:55 rb_mask); NULL = the contiguous allocation of the
+                                            plain configuration */
+  const srsgpu_re_pattern* reserved;     /* reserved REs besides the DM-RS (pdsch_modulator::config_t::reserved: SSB,
+                                            CSI-RS, ZP-CSI-RS, PT-RS ...); PDSCH modulator only */
+  uint32_t                 nof_reserved;
+  uint16_t                 prg_size;     /* precoding resource block group size in PRBs (precoding_configuration);
+                                            0 = the wideband weights of the plain configuration */
+  uint16_t                 nof_prg;      /* PRGs in prg_weights: PRG i covers CRBs [i prg_size, (i + 1) prg_size) */
+  const float*             prg_weights;  /* [nof_prg][port][layer] (re, im), ports x layers of the configuration */
+} srsgpu_alloc_ext;
+
 typedef struct srsgpu_pdsch_modulator_plan srsgpu_pdsch_modulator_plan;
 
 /** Validates the transmissions (the reference's assertions: time allocation inside the slot, allocation inside the
@@ -245,6 +271,18 @@ int srsgpu_pdsch_modulator_plan_create(srsgpu_context*                ctx,
                                        uint32_t                       grid_nof_prb,
                                        uint32_t                       grid_nof_ports,
                                        srsgpu_pdsch_modulator_plan**  plan);
+
+/** As srsgpu_pdsch_modulator_plan_create with an optional allocation extension per transmission (exts may be NULL):
+ *  CRB-mask allocations, reserved RE patterns and per-PRG precoding. The data REs are the allocated CRBs' REs of the
+ *  allocated symbols minus the BWP's DM-RS pattern on DM-RS symbols and the reserved patterns, in symbol-major,
+ *  ascending-subcarrier order (resource_grid_mapper_impl.cpp:269). */
+int srsgpu_pdsch_modulator_plan_create_ex(srsgpu_context*                ctx,
+                                          const srsgpu_pdsch_mod_config* cfgs,
+                                          const srsgpu_alloc_ext*        exts,
+                                          uint32_t                       nof_tx,
+                                          uint32_t                       grid_nof_prb,
+                                          uint32_t                       grid_nof_ports,
+                                          srsgpu_pdsch_modulator_plan**  plan);
 
 /** Modulates and maps every planned transmission from d_codewords into d_grids (uint32 per RE: re | im << 16).
  *  Asynchronous on `stream`, hipGraph-capturable. */

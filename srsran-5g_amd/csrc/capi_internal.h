@@ -210,3 +210,65 @@ inline void symbol_start_epochs(unsigned mu, float* ep)
 }
 
 } // namespace srsgpu
+
+namespace srsgpu {
+
+/// Data resource elements of a transmission in mapping order (resource_grid_mapper_impl.cpp:269: symbol-major,
+/// ascending grid subcarrier): the REs of the allocated CRBs (crb_mask, one byte per grid CRB) in symbols
+/// [start_symbol, start_symbol + nof_symbols), minus the DM-RS RE pattern of the CDM groups without data over the
+/// CRBs [dmrs_crb_begin, dmrs_crb_end) on DM-RS symbols (dmrs_mapping.h get_dmrs_pattern) and minus the reserved
+/// patterns. Fills sc[] with each RE's grid subcarrier and sym_cum[l] with the REs before symbol l (l = 0..15).
+inline void enumerate_data_res(unsigned                 grid_nof_prb,
+                               const uint8_t*           crb_mask,
+                               unsigned                 start_symbol,
+                               unsigned                 nof_symbols,
+                               unsigned                 dmrs_symbol_mask,
+                               unsigned                 dmrs_type,
+                               unsigned                 nof_cdm_groups_without_data,
+                               unsigned                 dmrs_crb_begin,
+                               unsigned                 dmrs_crb_end,
+                               const srsgpu_re_pattern* reserved,
+                               unsigned                 nof_reserved,
+                               std::vector<uint16_t>&   sc,
+                               uint16_t*                sym_cum)
+{
+  unsigned dmrs_re = 0;  // DM-RS REs of a PRB: type 1 CDM group g on 2k + g, type 2 on 6k + 2g + {0, 1}
+  for (unsigned k = 0; k < 12; ++k) {
+    const unsigned group = (dmrs_type == 2) ? (k % 6) / 2 : k % 2;
+    if (group < nof_cdm_groups_without_data) {
+      dmrs_re |= 1u << k;
+    }
+  }
+  sc.clear();
+  for (unsigned l = 0; l < 16; ++l) {
+    if (l < 14) {
+      sym_cum[l] = static_cast<uint16_t>(sc.size());
+    }
+    if (l >= 14 || l < start_symbol || l >= start_symbol + nof_symbols) {
+      if (l >= 14) {
+        sym_cum[l] = static_cast<uint16_t>(sc.size());
+      }
+      continue;
+    }
+    const bool dmrs_sym = ((dmrs_symbol_mask >> l) & 1u) != 0;
+    for (unsigned crb = 0; crb < grid_nof_prb; ++crb) {
+      if (crb_mask[crb] == 0) {
+        continue;
+      }
+      unsigned excl = (dmrs_sym && crb >= dmrs_crb_begin && crb < dmrs_crb_end) ? dmrs_re : 0u;
+      for (unsigned i = 0; i < nof_reserved; ++i) {
+        const srsgpu_re_pattern& r = reserved[i];
+        if (((r.symbol_mask >> l) & 1u) != 0 && (r.crb_mask == nullptr || r.crb_mask[crb] != 0)) {
+          excl |= r.re_mask & 0xfffu;
+        }
+      }
+      for (unsigned k = 0; k < 12; ++k) {
+        if (((excl >> k) & 1u) == 0) {
+          sc.push_back(static_cast<uint16_t>(crb * 12 + k));
+        }
+      }
+    }
+  }
+}
+
+} // namespace srsgpu

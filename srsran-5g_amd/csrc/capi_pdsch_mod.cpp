@@ -22,6 +22,8 @@ struct srsgpu_pdsch_dmrs_plan {
 struct srsgpu_pdsch_modulator_plan {
   srsgpu_context* ctx        = nullptr;
   mod_desc*       d_desc     = nullptr;
+  uint16_t*       d_sc_map   = nullptr;  ///< RE -> grid subcarrier maps of the general allocations.
+  float*          d_prg_w    = nullptr;  ///< Per-PRG weights [prg][port 4][layer 4][2] (amplitude folded in).
   mod_chunk*      d_chunks   = nullptr;
   uint32_t*       d_seq      = nullptr;  ///< Scrambling sequences of the transmissions (plan lifetime).
   int             nof_chunks = 0;
@@ -226,6 +228,17 @@ int srsgpu_pdsch_modulator_plan_create(srsgpu_context*                ctx,
                                        uint32_t                       grid_nof_ports,
                                        srsgpu_pdsch_modulator_plan**  plan_out)
 {
+  return srsgpu_pdsch_modulator_plan_create_ex(ctx, cfgs, nullptr, nof_tx, grid_nof_prb, grid_nof_ports, plan_out);
+}
+
+int srsgpu_pdsch_modulator_plan_create_ex(srsgpu_context*                ctx,
+                                          const srsgpu_pdsch_mod_config* cfgs,
+                                          const srsgpu_alloc_ext*        exts,
+                                          uint32_t                       nof_tx,
+                                          uint32_t                       grid_nof_prb,
+                                          uint32_t                       grid_nof_ports,
+                                          srsgpu_pdsch_modulator_plan**  plan_out)
+{
   if (ctx == nullptr || plan_out == nullptr || (cfgs == nullptr && nof_tx > 0)) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
@@ -241,8 +254,12 @@ int srsgpu_pdsch_modulator_plan_create(srsgpu_context*                ctx,
   const uint32_t         nsc = 12u * grid_nof_prb;
   std::vector<mod_desc>  descs(nof_tx);
   std::vector<mod_chunk> chunks;
+  std::vector<uint16_t>  sc_map;  // RE -> grid subcarrier of every general allocation
+  std::vector<float>     prg_w;   // per-PRG weights of every transmission with PRG precoding
+  std::vector<uint16_t>  sc_tx;
   for (uint32_t t = 0; t < nof_tx; ++t) {
     const srsgpu_pdsch_mod_config& c  = cfgs[t];
+    const srsgpu_alloc_ext*        x  = (exts != nullptr) ? &exts[t] : nullptr;
     const unsigned                 qm = c.modulation_order;
     if (qm != 2 && qm != 4 && qm != 6 && qm != 8) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid modulation order %u", t, qm);
@@ -260,9 +277,16 @@ int srsgpu_pdsch_modulator_plan_create(srsgpu_context*                ctx,
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid DM-RS type %u / CDM groups without data %u", t,
                   c.dmrs_type, c.nof_cdm_groups_without_data);
     }
-    if (c.n_id > 1023 || c.bwp_size_rb < 1 || c.bwp_start_rb + c.bwp_size_rb > grid_nof_prb || c.nof_rb < 1 ||
-        c.rb_start + c.nof_rb > c.bwp_size_rb) {
+    // PRG precoding indexes PRGs by absolute CRB (resource_grid_mapper_impl.cpp:218), so it takes the RE map path too.
+    const bool general = x != nullptr && (x->crb_mask != nullptr || x->nof_reserved > 0 || x->prg_size > 0);
+    if (c.n_id > 1023 || c.bwp_size_rb < 1 || c.bwp_start_rb + c.bwp_size_rb > grid_nof_prb ||
+        (!general && (c.nof_rb < 1 || c.rb_start + c.nof_rb > c.bwp_size_rb))) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: allocation outside the BWP or the grid, or n_id > 1023", t);
+    }
+    if (x != nullptr && ((x->nof_reserved > 0 && x->reserved == nullptr) ||
+                         (x->prg_size > 0 && (x->prg_weights == nullptr || x->nof_prg == 0 ||
+                                              static_cast<uint32_t>(x->prg_size) * x->nof_prg < grid_nof_prb)))) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid allocation extension (reserved patterns / PRG weights)", t);
     }
     if (c.cw_offset % 4 != 0) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: codeword offset not a multiple of 4", t);
@@ -279,14 +303,32 @@ int srsgpu_pdsch_modulator_plan_create(srsgpu_context*                ctx,
     }
     d.nd_dmrs = static_cast<uint8_t>(nd);
     uint32_t nre = 0;
-    for (unsigned l = 0; l < 14; ++l) {
-      d.sym_cum[l] = static_cast<uint16_t>(nre);
-      if (l >= c.start_symbol && l < static_cast<unsigned>(c.start_symbol + c.nof_symbols)) {
-        nre += (((c.dmrs_symbol_mask >> l) & 1u) ? nd : 12u) * c.nof_rb;
+    d.sc_map     = NO_SC_MAP;
+    if (general) {
+      // CRB mask (a contiguous allocation when the extension has none) minus the BWP's DM-RS pattern and the
+      // reserved patterns (pdsch_modulator_impl.cpp:58-:87).
+      std::vector<uint8_t> crbs(grid_nof_prb, 0);
+      for (unsigned rb = 0; rb < grid_nof_prb; ++rb) {
+        crbs[rb] = (x->crb_mask != nullptr) ? x->crb_mask[rb]
+                                            : (rb >= c.bwp_start_rb + c.rb_start &&
+                                               rb < static_cast<unsigned>(c.bwp_start_rb + c.rb_start + c.nof_rb));
       }
+      enumerate_data_res(grid_nof_prb, crbs.data(), c.start_symbol, c.nof_symbols, c.dmrs_symbol_mask, c.dmrs_type,
+                         c.nof_cdm_groups_without_data, c.bwp_start_rb, c.bwp_start_rb + c.bwp_size_rb, x->reserved,
+                         x->nof_reserved, sc_tx, d.sym_cum);
+      nre      = static_cast<uint32_t>(sc_tx.size());
+      d.sc_map = static_cast<uint32_t>(sc_map.size());
+      sc_map.insert(sc_map.end(), sc_tx.begin(), sc_tx.end());
+    } else {
+      for (unsigned l = 0; l < 14; ++l) {
+        d.sym_cum[l] = static_cast<uint16_t>(nre);
+        if (l >= c.start_symbol && l < static_cast<unsigned>(c.start_symbol + c.nof_symbols)) {
+          nre += (((c.dmrs_symbol_mask >> l) & 1u) ? nd : 12u) * c.nof_rb;
+        }
+      }
+      d.sym_cum[14] = static_cast<uint16_t>(nre);
+      d.sym_cum[15] = static_cast<uint16_t>(nre);
     }
-    d.sym_cum[14] = static_cast<uint16_t>(nre);
-    d.sym_cum[15] = static_cast<uint16_t>(nre);
     const uint64_t need = static_cast<uint64_t>(nre) * c.nof_layers * qm;
     if (nre == 0 || need != c.nof_bits || c.nof_bits > MOD_MAX_BITS) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: codeword of %u bits for %u data REs x %u layers x Qm %u", t,
@@ -297,7 +339,7 @@ int srsgpu_pdsch_modulator_plan_create(srsgpu_context*                ctx,
     d.c_init         = (static_cast<uint32_t>(c.rnti) << 15) + c.n_id;  // pdsch_modulator_impl.cpp:35, q = 0
     d.port_stride    = 14u * nsc;
     d.nsc            = nsc;
-    d.grid_base      = c.grid_index * grid_nof_ports * 14u * nsc + (c.bwp_start_rb + c.rb_start) * 12u;
+    d.grid_base      = c.grid_index * grid_nof_ports * 14u * nsc + (general ? 0u : (c.bwp_start_rb + c.rb_start) * 12u);
     d.dmrs_mask      = c.dmrs_symbol_mask;
     d.qm             = static_cast<uint8_t>(qm);
     d.L              = c.nof_layers;
@@ -312,6 +354,22 @@ int srsgpu_pdsch_modulator_plan_create(srsgpu_context*                ctx,
         const bool used = p < c.nof_ports && l < c.nof_layers;
         d.w[p][l][0]    = used ? c.precoding[p][l][0] * amp : 0.f;
         d.w[p][l][1]    = used ? c.precoding[p][l][1] * amp : 0.f;
+      }
+    }
+    d.prg_sc = 0;
+    if (x != nullptr && x->prg_size > 0) {
+      // Per-PRG weights, the same amplitude folding (precoding2 *= scaling, pdsch_modulator_impl.cpp:96).
+      d.prg_sc = static_cast<uint16_t>(x->prg_size * 12u);
+      d.prg_w  = static_cast<uint32_t>(prg_w.size());
+      for (unsigned g = 0; g < x->nof_prg; ++g) {
+        for (int p = 0; p < 4; ++p) {
+          for (int l = 0; l < 4; ++l) {
+            const bool   used = p < c.nof_ports && l < c.nof_layers;
+            const float* src  = x->prg_weights + ((static_cast<size_t>(g) * c.nof_ports + p) * c.nof_layers + l) * 2;
+            prg_w.push_back(used ? src[0] * amp : 0.f);
+            prg_w.push_back(used ? src[1] * amp : 0.f);
+          }
+        }
       }
     }
     descs[t]              = d;
@@ -352,6 +410,15 @@ int srsgpu_pdsch_modulator_plan_create(srsgpu_context*                ctx,
          hipMalloc(&plan->d_chunks, chunks.size() * sizeof(mod_chunk)) == hipSuccess &&
          hipMemcpy(plan->d_chunks, chunks.data(), chunks.size() * sizeof(mod_chunk), hipMemcpyHostToDevice) ==
              hipSuccess;
+    if (ok && !sc_map.empty()) {
+      ok = hipMalloc(&plan->d_sc_map, sc_map.size() * sizeof(uint16_t)) == hipSuccess &&
+           hipMemcpy(plan->d_sc_map, sc_map.data(), sc_map.size() * sizeof(uint16_t), hipMemcpyHostToDevice) ==
+               hipSuccess;
+    }
+    if (ok && !prg_w.empty()) {
+      ok = hipMalloc(&plan->d_prg_w, prg_w.size() * sizeof(float)) == hipSuccess &&
+           hipMemcpy(plan->d_prg_w, prg_w.data(), prg_w.size() * sizeof(float), hipMemcpyHostToDevice) == hipSuccess;
+    }
   }
   if (!ok) {
     srsgpu_pdsch_modulator_plan_destroy(plan);
@@ -369,7 +436,7 @@ int srsgpu_pdsch_modulator_plan_execute(const srsgpu_pdsch_modulator_plan* plan,
   if (plan == nullptr || d_codewords == nullptr || d_grids == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  launch_pdsch_modulate(plan->d_desc, plan->d_chunks, plan->nof_chunks,
+  launch_pdsch_modulate(plan->d_desc, plan->d_sc_map, plan->d_prg_w, plan->d_chunks, plan->nof_chunks,
                         reinterpret_cast<const uint32_t*>(d_codewords), d_grids, plan->d_seq,
                         static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
@@ -382,7 +449,8 @@ void srsgpu_pdsch_modulator_plan_destroy(srsgpu_pdsch_modulator_plan* plan)
     return;
   }
   for (void* p : {static_cast<void*>(plan->d_desc), static_cast<void*>(plan->d_chunks),
-                  static_cast<void*>(plan->d_seq)}) {
+                  static_cast<void*>(plan->d_seq), static_cast<void*>(plan->d_sc_map),
+                  static_cast<void*>(plan->d_prg_w)}) {
     if (p != nullptr) {
       (void)hipFree(p);
     }

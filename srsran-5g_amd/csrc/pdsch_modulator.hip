@@ -60,6 +60,8 @@ __device__ __forceinline__ uint32_t to_bf16_bits(float v)
 }
 
 __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_desc* __restrict__ descs,
+                                                                      const uint16_t* __restrict__ sc_map,
+                                                                      const float* __restrict__ prg_w,
                                                                       const mod_chunk* __restrict__ chunks,
                                                                       const uint32_t* __restrict__ cw,
                                                                       uint32_t* __restrict__ grids,
@@ -112,7 +114,11 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
     const uint32_t k    = r - d.sym_cum[l];
     const bool     dmrs = (d.dmrs_mask >> l) & 1u;
     uint32_t       sc;
-    if (dmrs) {
+    if (d.sc_map != NO_SC_MAP) {
+      // General allocation (CRB mask, reserved REs, PRG precoding): the plan's RE -> grid subcarrier map (grid_base
+      // at CRB 0, so sc is the absolute subcarrier the PRG index below needs).
+      sc = sc_map[d.sc_map + r];
+    } else if (dmrs) {
       const uint32_t nd  = d.nd_dmrs;
       const uint32_t prb = k / nd;
       const uint32_t j   = k - prb * nd;
@@ -121,6 +127,8 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
       sc = k;
     }
     const uint32_t e = d.grid_base + l * d.nsc + sc;
+    // Per-PRG precoding (resource_grid_mapper_impl.cpp:218): the weights of the PRG holding the RE's subcarrier.
+    const float* wt = (d.prg_sc != 0) ? prg_w + d.prg_w + (sc / d.prg_sc) * 32u : nullptr;
 
     // Constellation points of the layers (TS 38.211 section 5.1 integer grid; the amplitude is in the weights).
     float xr[4], xi[4];
@@ -149,8 +157,10 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
 #pragma unroll
         for (int ly = 0; ly < 4; ++ly) {
           if (ly < static_cast<int>(L)) {
-            const float pr = xr[ly] * w[p][ly][0] - xi[ly] * w[p][ly][1];
-            const float pi = xr[ly] * w[p][ly][1] + xi[ly] * w[p][ly][0];
+            const float wr = (wt != nullptr) ? wt[(p * 4 + ly) * 2] : w[p][ly][0];
+            const float wi = (wt != nullptr) ? wt[(p * 4 + ly) * 2 + 1] : w[p][ly][1];
+            const float pr = xr[ly] * wr - xi[ly] * wi;
+            const float pi = xr[ly] * wi + xi[ly] * wr;
             sr             = (ly == 0) ? pr : sr + pr;
             si             = (ly == 0) ? pi : si + pi;
           }
@@ -221,6 +231,8 @@ void launch_pdsch_dmrs(const dmrs_job* d_jobs,
 }
 
 void launch_pdsch_modulate(const mod_desc*  d_desc,
+                           const uint16_t*  d_sc_map,
+                           const float*     d_prg_w,
                            const mod_chunk* d_chunks,
                            int              nof_chunks,
                            const uint32_t*  d_codewords,
@@ -232,7 +244,7 @@ void launch_pdsch_modulate(const mod_desc*  d_desc,
     return;
   }
   hipLaunchKernelGGL(pdsch_modulate_kernel, dim3(static_cast<unsigned>(nof_chunks)), dim3(MOD_THREADS), 0, stream,
-                     d_desc, d_chunks, d_codewords, d_grids, d_seq);
+                     d_desc, d_sc_map, d_prg_w, d_chunks, d_codewords, d_grids, d_seq);
 }
 
 void launch_gold_fill(const uint32_t* d_c_inits,

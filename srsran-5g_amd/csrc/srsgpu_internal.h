@@ -210,13 +210,18 @@ struct mod_desc {
   uint8_t  L;               ///< Layers.
   uint8_t  P;               ///< Ports.
   uint8_t  nd_dmrs;         ///< Data REs per PRB on DM-RS symbols.
-  uint16_t pad;
+  uint16_t prg_sc;          ///< Per-PRG precoding: subcarriers per PRG (0: the wideband weights w).
   uint16_t sym_cum[16];     ///< Data REs in the symbols before symbol l (l = 0..14).
   float    w[4][4][2];      ///< Precoding weights [port][layer] times the modulation amplitude.
   uint32_t seq_word_offset; ///< First word of the transmission's scrambling sequence in the plan's sequence buffer.
-  uint32_t pad2;
+  uint32_t sc_map;          ///< General allocation: first entry of the RE -> grid subcarrier map (NO_SC_MAP: contiguous).
+  uint32_t prg_w;           ///< Per-PRG precoding: first float of [prg][port][layer][2] (amplitude folded in).
+  uint32_t pad3[3];
 };
-static_assert(sizeof(mod_desc) == 208, "mod_desc layout");
+static_assert(sizeof(mod_desc) == 224, "mod_desc layout");
+
+/// mod_desc::sc_map of the contiguous fast path.
+constexpr uint32_t NO_SC_MAP = 0xffffffffu;
 
 /// PDSCH modulator / PUSCH demodulator work item: MOD_CHUNK_WORDS x 32 codeword bits of one transmission and the REs
 /// starting in them.
@@ -246,6 +251,8 @@ constexpr uint32_t GOLD_X1_WORDS     = MOD_MAX_BITS / 32;
 constexpr uint32_t GOLD_X2_JUMPS     = MOD_MAX_BITS / 2048;
 
 void launch_pdsch_modulate(const mod_desc*  d_desc,
+                           const uint16_t*  d_sc_map,
+                           const float*     d_prg_w,
                            const mod_chunk* d_chunks,
                            int              nof_chunks,
                            const uint32_t*  d_codewords,

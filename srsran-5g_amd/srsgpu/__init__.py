@@ -155,6 +155,17 @@ class PdschModConfig(ctypes.Structure):
 
 
 assert ctypes.sizeof(PdschModConfig) == 168
+
+
+class RePatternC(ctypes.Structure):
+    """srsgpu_re_pattern (include/srsgpu_phy.h)."""
+    _fields_ = [("crb_mask", ctypes.c_void_p), ("re_mask", ctypes.c_uint16), ("symbol_mask", ctypes.c_uint16)]
+
+
+class AllocExtC(ctypes.Structure):
+    """srsgpu_alloc_ext (include/srsgpu_phy.h): CRB mask, reserved RE patterns and per-PRG precoding."""
+    _fields_ = [("crb_mask", ctypes.c_void_p), ("reserved", ctypes.c_void_p), ("nof_reserved", ctypes.c_uint32),
+                ("prg_size", ctypes.c_uint16), ("nof_prg", ctypes.c_uint16), ("prg_weights", ctypes.c_void_p)]
 CB_MSG_STRIDE = 1056
 
 
@@ -298,6 +309,8 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pusch_decoder_plan_destroy.restype = None
     lib.srsgpu_pdsch_modulator_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                        ctypes.POINTER(P)]
+    lib.srsgpu_pdsch_modulator_plan_create_ex.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                          ctypes.POINTER(P)]
     lib.srsgpu_pdsch_modulator_plan_execute.argtypes = [P, P, P, P]
     lib.srsgpu_pdsch_modulator_plan_destroy.argtypes = [P]
     lib.srsgpu_pdsch_modulator_plan_destroy.restype = None
@@ -347,7 +360,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_pusch_decoder_plan_destroy", "srsgpu_pusch_decoder_plan_enable_timing",
     "srsgpu_pusch_decoder_plan_stage_times", "srsgpu_pdsch_encoder_plan_enable_timing",
     "srsgpu_pdsch_encoder_plan_stage_times", "srsgpu_pdsch_modulator_plan_create",
-    "srsgpu_pdsch_modulator_plan_execute", "srsgpu_pdsch_modulator_plan_destroy",
+    "srsgpu_pdsch_modulator_plan_create_ex", "srsgpu_pdsch_modulator_plan_execute", "srsgpu_pdsch_modulator_plan_destroy",
     "srsgpu_ofdm_modulator_plan_create", "srsgpu_ofdm_demodulator_plan_create", "srsgpu_ofdm_plan_nof_samples",
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
@@ -716,8 +729,11 @@ class PdschEncoder:
 
 @dataclass
 class PdschModulation:
-    """pdsch_modulator::config_t (pdsch_modulator.h:38) of one transmission, contiguous non-interleaved VRB allocation
-    and wideband precoding `weights` (nof_ports x nof_layers complex)."""
+    """pdsch_modulator::config_t (pdsch_modulator.h:38) of one transmission: contiguous non-interleaved VRB allocation
+    [rb_start, rb_start + nof_rb) of the BWP and wideband precoding `weights` (nof_ports x nof_layers complex), or the
+    general form: `crb_mask` (one byte per grid CRB, alloc.vrb_to_crb_mask of any type-0 / type-1 / interleaved
+    allocation), `reserved` RE patterns (alloc.ReservedPattern: SSB, CSI-RS, ...) and per-PRG precoding
+    (`prg_size` PRBs per PRG, `prg_weights` nof_prg x nof_ports x nof_layers complex)."""
     rnti: int
     n_id: int
     modulation_order: int
@@ -734,14 +750,68 @@ class PdschModulation:
     nof_cdm_groups_without_data: int
     scaling: float
     weights: np.ndarray
+    crb_mask: Optional[np.ndarray] = None
+    reserved: Sequence = ()
+    prg_size: int = 0
+    prg_weights: Optional[np.ndarray] = None
 
-    def nof_re(self) -> int:
+    def is_general(self) -> bool:
+        return self.crb_mask is not None or len(self.reserved) > 0 or self.prg_size > 0
+
+    def nof_re(self, grid_nof_prb: Optional[int] = None) -> int:
+        if self.is_general():
+            from . import alloc
+            n = grid_nof_prb if grid_nof_prb is not None else self.bwp_start_rb + self.bwp_size_rb
+            crbs = self.crb_mask
+            if crbs is None:
+                crbs = np.zeros(n, np.uint8)
+                crbs[self.bwp_start_rb + self.rb_start:self.bwp_start_rb + self.rb_start + self.nof_rb] = 1
+            return alloc.count_data_res(n, np.asarray(crbs)[:n], self.start_symbol, self.nof_symbols,
+                                        self.dmrs_symbol_mask, self.dmrs_type, self.nof_cdm_groups_without_data,
+                                        self.bwp_start_rb, self.bwp_size_rb, self.reserved)
         dm = (4 if self.dmrs_type == 2 else 6) * self.nof_cdm_groups_without_data
         return sum((12 - dm if (self.dmrs_symbol_mask >> l) & 1 else 12) * self.nof_rb
                    for l in range(self.start_symbol, self.start_symbol + self.nof_symbols))
 
 
-def make_pdsch_mod_configs(mods: Sequence[PdschModulation], cw_offsets: Sequence[int], grid_index: Sequence[int]):
+def make_alloc_exts(mods, grid_nof_prb: int):
+    """srsgpu_alloc_ext array of the general transmissions (None when every one is contiguous and wideband); the
+    returned keep-alive list holds the buffers the structures point to until the plan is created."""
+    if not any(m.is_general() for m in mods):
+        return None, []
+    exts = (AllocExtC * len(mods))()
+    keep = []
+    for i, m in enumerate(mods):
+        if not m.is_general():
+            continue
+        e = exts[i]
+        if m.crb_mask is not None:
+            c = np.zeros(grid_nof_prb, np.uint8)
+            src = np.asarray(m.crb_mask, np.uint8)[:grid_nof_prb]
+            c[:src.size] = src
+            keep.append(c)
+            e.crb_mask = c.ctypes.data
+        if len(m.reserved):
+            pats = (RePatternC * len(m.reserved))()
+            for j, r in enumerate(m.reserved):
+                pats[j].re_mask, pats[j].symbol_mask = r.re_mask, r.symbol_mask
+                if r.crb_mask is not None:
+                    c = np.zeros(grid_nof_prb, np.uint8)
+                    src = np.asarray(r.crb_mask, np.uint8)[:grid_nof_prb]
+                    c[:src.size] = src
+                    keep.append(c)
+                    pats[j].crb_mask = c.ctypes.data
+            keep.append(pats)
+            e.reserved, e.nof_reserved = ctypes.cast(pats, ctypes.c_void_p), len(m.reserved)
+        if m.prg_size > 0:
+            w = np.ascontiguousarray(np.asarray(m.prg_weights, np.complex64).reshape(-1, m.nof_ports, m.nof_layers))
+            keep.append(w)
+            e.prg_size, e.nof_prg, e.prg_weights = m.prg_size, w.shape[0], w.ctypes.data
+    return exts, keep
+
+
+def make_pdsch_mod_configs(mods: Sequence[PdschModulation], cw_offsets: Sequence[int], grid_index: Sequence[int],
+                           grid_nof_prb: Optional[int] = None):
     arr = (PdschModConfig * len(mods))()
     for i, (m, off, g) in enumerate(zip(mods, cw_offsets, grid_index)):
         a = arr[i]
@@ -756,7 +826,7 @@ def make_pdsch_mod_configs(mods: Sequence[PdschModulation], cw_offsets: Sequence
         w[:m.nof_ports, :m.nof_layers, 0] = wc.real
         w[:m.nof_ports, :m.nof_layers, 1] = wc.imag
         a.precoding[:] = w.reshape(-1).tolist()
-        a.cw_offset, a.nof_bits, a.grid_index = off, m.nof_re() * m.nof_layers * m.modulation_order, g
+        a.cw_offset, a.nof_bits, a.grid_index = off, m.nof_re(grid_nof_prb) * m.nof_layers * m.modulation_order, g
     return arr
 
 
@@ -764,11 +834,17 @@ class PdschModulatorPlan:
     """srsgpu_pdsch_modulator_plan: scrambling, modulation, layer mapping, precoding and RE mapping of a batch of
     PDSCH transmissions into bf16 resource grids (grid_nof_ports x 14 x 12 * grid_nof_prb, uint32 re | im << 16)."""
 
-    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4):
+    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4, exts=None):
         self.ctx = ctx
         h = ctypes.c_void_p()
-        _check(_lib.srsgpu_pdsch_modulator_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
-                                                       len(cfg_array), grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
+        if exts is None:
+            _check(_lib.srsgpu_pdsch_modulator_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                           len(cfg_array), grid_nof_prb, grid_nof_ports,
+                                                           ctypes.byref(h)))
+        else:
+            _check(_lib.srsgpu_pdsch_modulator_plan_create_ex(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                              ctypes.cast(exts, ctypes.c_void_p), len(cfg_array),
+                                                              grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
         self.handle = h
         self.grid_nof_prb, self.grid_nof_ports = grid_nof_prb, grid_nof_ports
 
@@ -811,8 +887,9 @@ class PdschModulator:
             o += b.size + pad
         grid_index = list(range(len(mods))) if grid_index is None else list(grid_index)
         ngrids = max(grid_index) + 1 if grid_index else 1
-        arr = make_pdsch_mod_configs(mods, offs, grid_index)
-        plan = PdschModulatorPlan(self.ctx, arr, self.grid_nof_prb, self.grid_nof_ports)
+        arr = make_pdsch_mod_configs(mods, offs, grid_index, self.grid_nof_prb)
+        exts, _keep = make_alloc_exts(mods, self.grid_nof_prb)
+        plan = PdschModulatorPlan(self.ctx, arr, self.grid_nof_prb, self.grid_nof_ports, exts)
         shape = (ngrids, self.grid_nof_ports, 14, 12 * self.grid_nof_prb, 2)
         g0 = np.zeros(shape, np.uint16) if grids is None else np.ascontiguousarray(grids, np.uint16).reshape(shape)
         d_grid = torch.from_numpy(g0.view(np.uint32).reshape(-1).view(np.int32)).to(dev)

@@ -183,3 +183,25 @@ def pdsch_dmrs_cases():
         cfg["amplitude"] = float(d[f"case{i}_amplitude"])
         yield cfg, d[f"case{i}_weights"], d[f"case{i}_grid"]
         i += 1
+
+
+GENERAL_KEYS = ["rnti", "n_id", "qm", "nof_layers", "nof_ports", "bwp_start_rb", "bwp_size_rb", "start_symbol",
+                "nof_symbols", "dmrs_symbol_mask", "dmrs_type2", "nof_cdm_groups_without_data", "interleave",
+                "prg_size"]
+
+
+def pdsch_mod_general_cases():
+    """Yields (cfg dict with vrb_mask / interleave / reserved / prg_size / prg_weights, nof_bits, grid_nof_prb,
+    weights (P x L complex64), packed codeword, reference grid (P, 14, nsc, 2) uint16, reference CRB mask) made by the
+    reference's pdsch_modulator_impl with general allocations (tools/gen_golden.py gen_pdsch_mod_general)."""
+    d = _load("pdsch_mod_general.npz")
+    i = 0
+    while f"case{i}_cfg" in d:
+        row = d[f"case{i}_cfg"]
+        cfg = {k: int(v) for k, v in zip(GENERAL_KEYS, row[:-2])}
+        nbits, G = int(row[-2]), int(row[-1])
+        cfg.update(rb_start=0, nof_rb=0, scaling=float(d[f"case{i}_scaling"]), vrb_mask=d[f"case{i}_vrb"],
+                   reserved=[(c, int(m[0]), int(m[1])) for c, m in zip(d[f"case{i}_res_crb"], d[f"case{i}_res_masks"])],
+                   prg_weights=d[f"case{i}_prg_w"] if cfg["prg_size"] else None)
+        yield cfg, nbits, G, d[f"case{i}_w"], d[f"case{i}_cw"], d[f"case{i}_grid"], d[f"case{i}_crb"]
+        i += 1

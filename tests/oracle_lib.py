@@ -82,6 +82,46 @@ class _Lib:
         return grid
 
 
+def _general_args(cfg, grid_nof_prb):
+    res = cfg["reserved"]
+    res_crb = (np.concatenate([np.asarray(r[0], np.uint8)[:grid_nof_prb] for r in res]) if res
+               else np.zeros(1, np.uint8))
+    res_re = np.array([r[1] for r in res] or [0], np.uint16)
+    res_sym = np.array([r[2] for r in res] or [0], np.uint16)
+    pw = (np.ascontiguousarray(cfg["prg_weights"], np.complex64).view(np.float32) if cfg["prg_size"]
+          else np.zeros(2, np.float32))
+    nprg = cfg["prg_weights"].shape[0] if cfg["prg_size"] else 0
+    return res_crb, res_re, res_sym, pw, nprg
+
+
+def pdsch_modulate_general(lib, cfg, weights, cw_packed, nof_bits, grid_nof_prb, crb_mask=None, grid=None):
+    """orc_pdsch_modulate_ex (crb_mask given) / ref_pdsch_modulate_ex (VRB mask + interleaving of cfg): returns
+    (grid (P, 14, nsc, 2) uint16, CRB mask uint8 (the reference's get_crb_mask, or crb_mask))."""
+    w = np.ascontiguousarray(weights, dtype=np.complex64).view(np.float32)
+    cw = np.ascontiguousarray(cw_packed, dtype=np.uint8)
+    res_crb, res_re, res_sym, pw, nprg = _general_args(cfg, grid_nof_prb)
+    if grid is None:
+        grid = np.zeros((cfg["nof_ports"], 14, 12 * grid_nof_prb, 2), np.uint16)
+    head = [int(cfg[k]) for k in ("rnti", "n_id", "qm", "nof_layers", "nof_ports", "bwp_start_rb", "bwp_size_rb")]
+    mid = [int(cfg["start_symbol"]), int(cfg["nof_symbols"]), ctypes.c_uint(int(cfg["dmrs_symbol_mask"])),
+           int(cfg["dmrs_type2"]), int(cfg["nof_cdm_groups_without_data"]), ctypes.c_float(float(cfg["scaling"])),
+           _ptr(w), len(cfg["reserved"]), _ptr(res_crb), _ptr(res_re), _ptr(res_sym), int(cfg["prg_size"]), nprg,
+           _ptr(pw), _ptr(cw), int(nof_bits), int(grid_nof_prb), _ptr(grid)]
+    if crb_mask is not None:
+        crb = np.ascontiguousarray(crb_mask, np.uint8)
+        f = lib.orc_pdsch_modulate_ex
+        f.restype = ctypes.c_int
+        r = f(*head, _ptr(crb), *mid)
+    else:
+        vrb = np.ascontiguousarray(cfg["vrb_mask"], np.uint8)
+        crb = np.zeros(grid_nof_prb, np.uint8)
+        f = lib.ref_pdsch_modulate_ex
+        f.restype = ctypes.c_int
+        r = f(*head, _ptr(vrb), vrb.size, int(cfg["interleave"]), *mid, _ptr(crb))
+    assert r == 0, r
+    return grid, crb
+
+
 PDSCH_MOD_KEYS = ["rnti", "n_id", "qm", "nof_layers", "nof_ports", "bwp_start_rb", "bwp_size_rb", "rb_start", "nof_rb",
                   "start_symbol", "nof_symbols", "dmrs_symbol_mask", "dmrs_type2", "nof_cdm_groups_without_data",
                   "scaling"]

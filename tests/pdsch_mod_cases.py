@@ -42,3 +42,90 @@ def full_band_config(nof_layers=4, qm=8, rnti=0x4601, n_id=500):
                rb_start=0, nof_rb=273, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=1 << 2, dmrs_type2=0,
                nof_cdm_groups_without_data=2, scaling=1.0)
     return cfg, pdsch_mod_nof_re(cfg) * nof_layers * qm
+
+
+def general_nof_re(cfg, crb_mask, grid_nof_prb):
+    """Data REs of a general allocation (test-side count, independent of the product's srsgpu.alloc): allocated CRBs x
+    symbols minus the BWP DM-RS pattern on DM-RS symbols and the reserved patterns."""
+    if cfg["dmrs_type2"]:
+        dm = {k for k in range(12) if (k % 6) // 2 < cfg["nof_cdm_groups_without_data"]}
+    else:
+        dm = {k for k in range(12) if k % 2 < cfg["nof_cdm_groups_without_data"]}
+    n = 0
+    b0, b1 = cfg["bwp_start_rb"], cfg["bwp_start_rb"] + cfg["bwp_size_rb"]
+    for l in range(cfg["start_symbol"], cfg["start_symbol"] + cfg["nof_symbols"]):
+        for crb in range(grid_nof_prb):
+            if not crb_mask[crb]:
+                continue
+            excl = set(dm) if ((cfg["dmrs_symbol_mask"] >> l) & 1 and b0 <= crb < b1) else set()
+            for rc, rre, rsym in cfg["reserved"]:
+                if (rsym >> l) & 1 and rc[crb]:
+                    excl |= {k for k in range(12) if (rre >> k) & 1}
+            n += 12 - len(excl)
+    return n
+
+
+def random_general_config(rng, grid_nof_prb, interleave=None, prg=None, nof_reserved=None):
+    """A random general allocation: random type-0 VRB bitmap of the BWP mapped non-interleaved or interleaved (bundle
+    size 2 / 4, vrb_to_prb::create_interleaved_other), 0..3 reserved RE patterns (random CRB subsets, PRB subcarriers and
+    symbols, e.g. CSI-RS / SSB-like), wideband or per-PRG precoding (PRG sizes 2 / 4 / whole grid). Returns (cfg with
+    vrb_mask, interleave, reserved [(crb mask, re mask, symbol mask)], prg_size, prg_weights; nof_bits; weights)."""
+    while True:
+        cfg, _, w = random_config(rng, grid_nof_prb)
+        bwp_start = int(rng.integers(0, min(6, grid_nof_prb - 8)))
+        bwp_size = int(rng.integers(8, grid_nof_prb - bwp_start + 1))
+        cfg.update(bwp_start_rb=bwp_start, bwp_size_rb=bwp_size, rb_start=0, nof_rb=0)
+        il = int(rng.choice([0, 0, 2, 4]) if interleave is None else interleave)
+        nvrb = bwp_size
+        density = float(rng.choice([0.2, 0.5, 0.9, 1.0]))
+        vrb = (rng.random(nvrb) < density).astype(np.uint8)
+        if not vrb.any():
+            vrb[int(rng.integers(0, nvrb))] = 1
+        reserved = []
+        for _ in range(int(rng.integers(0, 4) if nof_reserved is None else nof_reserved)):
+            rc = (rng.random(grid_nof_prb) < rng.choice([0.3, 1.0])).astype(np.uint8)
+            if not rc.any():
+                rc[int(rng.integers(0, grid_nof_prb))] = 1
+            rre = int(rng.integers(1, 4096))
+            rsym = int(rng.integers(1, 1 << 14))
+            reserved.append((rc, rre, rsym))
+        P, L = cfg["nof_ports"], cfg["nof_layers"]
+        prg_size = int(rng.choice([0, 2, 4, grid_nof_prb]) if prg is None else prg)
+        nof_prg = -(-grid_nof_prb // prg_size) if prg_size else 0
+        prg_w = ((rng.normal(size=(nof_prg, P, L)) + 1j * rng.normal(size=(nof_prg, P, L))).astype(np.complex64)
+                 if prg_size else None)
+        cfg.update(vrb_mask=vrb, interleave=il, reserved=reserved, prg_size=prg_size, prg_weights=prg_w)
+        crbs = crb_mask_test_side(cfg, grid_nof_prb)
+        nre = general_nof_re(cfg, crbs, grid_nof_prb)
+        if nre == 0 or nre > 156 * int(crbs.sum()):
+            continue
+        return cfg, nre * L * cfg["qm"], w
+
+
+def crb_mask_test_side(cfg, grid_nof_prb):
+    """CRB mask of a case, restated on the test side from TS 38.211 7.3.1.6 (vrb_to_prb.cpp:94 interleaver), so the
+    product's srsgpu.alloc.vrb_to_crb_mask is checked against the reference's get_crb_mask and not against itself."""
+    s, n, L = cfg["bwp_start_rb"], cfg["bwp_size_rb"], cfg["interleave"]
+    vrbs = np.flatnonzero(cfg["vrb_mask"])
+    if L:
+        nb = -(-(n + s % L) // L)
+        first = L - s % L
+        last = (s + n) % L or L
+        prb = list(range(first))
+        mid = [None] * (nb - 2)
+        C = nb // 2
+        for c in range(C):
+            for r in range(2):
+                j = c * 2 + r
+                if j == 0 or j > nb - 2:
+                    continue
+                mid[j - 1] = r * C + c
+        for fj in mid:
+            prb += [(fj - 1) * L + first + i for i in range(L)]
+        prb += [(nb - 2) * L + first + i for i in range(last)]
+        prbs = np.array(prb)[vrbs]
+    else:
+        prbs = vrbs
+    out = np.zeros(grid_nof_prb, np.uint8)
+    out[s + prbs] = 1
+    return out

@@ -68,6 +68,25 @@ def test_pdsch_modulator_golden(orc):
     assert n == 12
 
 
+def test_pdsch_mod_general_golden(orc):
+    """General allocations (VRB bitmaps, interleaving, reserved REs, single-PRG precoding): the test-side CRB mapping
+    and the product's host mapping reproduce the reference's CRB masks, and the oracle reproduces its grids."""
+    import srsgpu.alloc as A
+    from oracle_lib import pdsch_modulate_general
+    from pdsch_mod_cases import crb_mask_test_side
+    n = 0
+    for cfg, nbits, grid_prb, w, cw, grid, crb in G.pdsch_mod_general_cases():
+        assert np.array_equal(crb_mask_test_side(cfg, grid_prb), crb)
+        il = cfg["interleave"]
+        vtp = A.interleaved_other(cfg["bwp_start_rb"], cfg["bwp_size_rb"], il) if il else None
+        assert np.array_equal(A.vrb_to_crb_mask(cfg["vrb_mask"], cfg["bwp_start_rb"], cfg["bwp_size_rb"], grid_prb,
+                                                vtp), crb)
+        got, _ = pdsch_modulate_general(orc.lib, cfg, w, cw, nbits, grid_prb, crb_mask=crb)
+        assert np.array_equal(got, grid), cfg
+        n += 1
+    assert n == 10
+
+
 def test_ofdm_golden():
     """The numpy OFDM restatement against the reference modulator's samples and demodulator's grids."""
     import ofdm_oracle as O

@@ -193,6 +193,55 @@ def test_pdsch_modulator_full_band(orc, ref):
         assert np.array_equal(orc.pdsch_modulate(cfg, w, cw, nbits, 273), want), (L, qm)
 
 
+def test_pdsch_modulator_general_vs_reference(orc, ref):
+    """General allocations: type-0 VRB bitmaps mapped non-interleaved / interleaved (bundles 2, 4), reserved RE patterns
+    and PRG precoding with one PRG over the grid (multi-PRG: see the next test). The reference's CRB mask
+    (rb_allocation::get_crb_mask) equals the test-side restatement and the product's host mapping
+    (srsgpu.alloc.vrb_to_crb_mask), and the oracle's grid over that mask equals the reference's grid bit for bit."""
+    import srsgpu.alloc as A
+    from oracle_lib import pdsch_modulate_general
+    from pdsch_mod_cases import crb_mask_test_side, random_general_config
+    rng = np.random.default_rng(79)
+    G = 52
+    for i in range(60):
+        cfg, nbits, w = random_general_config(rng, G, interleave=[0, 2, 4][i % 3] if i < 30 else None,
+                                              prg=[0, G][i % 2])
+        cw = rng.integers(0, 256, (nbits + 7) // 8).astype(np.uint8)
+        want, crb = pdsch_modulate_general(ref.lib, cfg, w, cw, nbits, G)
+        assert np.array_equal(crb, crb_mask_test_side(cfg, G)), cfg
+        il = cfg["interleave"]
+        vtp = A.interleaved_other(cfg["bwp_start_rb"], cfg["bwp_size_rb"], il) if il else None
+        assert np.array_equal(A.vrb_to_crb_mask(cfg["vrb_mask"], cfg["bwp_start_rb"], cfg["bwp_size_rb"], G, vtp), crb)
+        got, _ = pdsch_modulate_general(orc.lib, cfg, w, cw, nbits, G, crb_mask=crb)
+        assert np.array_equal(got, want), (i, cfg)
+
+
+def test_pdsch_modulator_multi_prg_reference_defect(orc, ref):
+    """Documents a reference defect instead of copying it: with more than one PRG, the symbol-buffer mapper the PDSCH
+    modulator uses (resource_grid_mapper_impl.cpp:330-:340) adds the ABSOLUTE lowest active subcarrier
+    (bounded_bitset::find_lowest returns absolute indexes) to the PRG's start, so PRG i > 0 starts at
+    i * prg_size * 12 + lowest: REs of PRG 1.. are mapped with the wrong PRG's weights or not at all, and part of the
+    codeword is silently dropped. The reference's own mapper test (resource_grid_mapper_test.cpp:270) and its pattern
+    mapper (:220-:245) define the PRG of a RE as its subcarrier / (12 prg_size); the oracle and the GPU path implement
+    that. This test pins (a) the defect (the reference maps fewer REs than the allocation holds) and (b) that the
+    reference equals the oracle on PRG 0 of the first data symbol, before the first dropped RE shifts the codeword."""
+    from oracle_lib import pdsch_modulate_general
+    from pdsch_mod_cases import random_general_config
+    rng = np.random.default_rng(80)
+    G = 52
+    for i in range(10):
+        cfg, nbits, w = random_general_config(rng, G, interleave=0, prg=4, nof_reserved=0)
+        cw = rng.integers(0, 256, (nbits + 7) // 8).astype(np.uint8)
+        want, crb = pdsch_modulate_general(ref.lib, cfg, w, cw, nbits, G)
+        got, _ = pdsch_modulate_general(orc.lib, cfg, w, cw, nbits, G, crb_mask=crb)
+        mapped_ref = int((want[0] != 0).any(-1).sum())
+        mapped_orc = int((got[0] != 0).any(-1).sum())
+        if crb[4:].any():
+            assert mapped_ref < mapped_orc, cfg
+        l0 = int(np.flatnonzero((got[0] != 0).any(-1).any(-1))[0])
+        assert np.array_equal(got[:, l0, :48], want[:, l0, :48]), cfg
+
+
 @pytest.mark.parametrize("case", range(11))
 def test_ofdm_oracle_vs_reference(ref, case):
     """OFDM modulator and demodulator restatement (oracle/ofdm_oracle.py, complex128) against the reference's

@@ -101,6 +101,89 @@ def test_pdsch_modulator_full_band(ctx, L, qm):
     assert np.array_equal(got, want)
 
 
+def to_general_mod(cfg, w, crb, grid_prb):
+    import srsgpu
+    import srsgpu.alloc as A
+    m = to_mod(cfg, w)
+    m.crb_mask = crb
+    m.reserved = [A.ReservedPattern(re_mask=r[1], symbol_mask=r[2], crb_mask=r[0]) for r in cfg["reserved"]]
+    m.prg_size = cfg["prg_size"]
+    m.prg_weights = cfg["prg_weights"]
+    return m
+
+
+def test_pdsch_modulator_general_golden(ctx):
+    """Reference-made grids of general allocations (VRB bitmaps non-interleaved / interleaved, reserved RE patterns,
+    single-PRG precoding), one plan with every case, bit-exact."""
+    import srsgpu
+    cases = list(G.pdsch_mod_general_cases())
+    grid_prb = cases[0][2]
+    mods = [to_general_mod(c, w, crb, grid_prb) for c, _, _, w, _, _, crb in cases]
+    for m, (c, nbits, *_rest) in zip(mods, cases):
+        assert m.nof_re(grid_prb) * m.nof_layers * m.modulation_order == nbits
+    got = srsgpu.PdschModulator(ctx, grid_prb, 4).modulate_batch([c[4] for c in cases], mods)
+    for i, (cfg, nbits, _, w, cw, grid, crb) in enumerate(cases):
+        assert np.array_equal(got[i, : cfg["nof_ports"]], grid), (i, cfg)
+
+
+def test_pdsch_modulator_general_random_vs_oracle(ctx):
+    """90 random general allocations in ONE plan (contiguous transmissions mixed in), including multi-PRG precoding
+    (PRG sizes 2 and 4) and reserved patterns, against the oracle (PRG of a RE = its CRB / prg_size, the reference's
+    mapper test definition; see test_pdsch_modulator_multi_prg_reference_defect)."""
+    import srsgpu
+    from oracle_lib import pdsch_modulate_general
+    from pdsch_mod_cases import crb_mask_test_side, random_general_config
+    orc = Oracle()
+    rng = np.random.default_rng(22)
+    G_ = 52
+    mods, cws, want = [], [], []
+    for i in range(90):
+        if i % 9 == 8:
+            cfg, nbits, w = random_config(rng, G_)
+            cw = rng.integers(0, 256, (nbits + 7) // 8).astype(np.uint8)
+            g = np.zeros((4, 14, 12 * G_, 2), np.uint16)
+            orc.pdsch_modulate(cfg, w, cw, nbits, G_, grid=g[: cfg["nof_ports"]])
+            mods.append(to_mod(cfg, w))
+        else:
+            cfg, nbits, w = random_general_config(rng, G_)
+            crb = crb_mask_test_side(cfg, G_)
+            cw = rng.integers(0, 256, (nbits + 7) // 8).astype(np.uint8)
+            g = np.zeros((4, 14, 12 * G_, 2), np.uint16)
+            pdsch_modulate_general(orc.lib, cfg, w, cw, nbits, G_, crb_mask=crb, grid=g[: cfg["nof_ports"]])
+            mods.append(to_general_mod(cfg, w, crb, G_))
+        cws.append(cw)
+        want.append(g)
+    got = srsgpu.PdschModulator(ctx, G_, 4).modulate_batch(cws, mods)
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert np.array_equal(a, b), (i, mods[i])
+
+
+def test_pdsch_modulator_general_full_band(ctx):
+    """273 PRB, interleaved (bundle 4) 90 % VRB bitmap, CSI-RS-like and SSB-like reserved patterns, PRG size 4 with
+    4 layers of 256QAM: the largest general codeword."""
+    import srsgpu
+    import srsgpu.alloc as A
+    from oracle_lib import pdsch_modulate_general
+    orc = Oracle()
+    rng = np.random.default_rng(23)
+    vrb = (rng.random(273) < 0.9).astype(np.uint8)
+    crb = A.vrb_to_crb_mask(vrb, 0, 273, 273, A.interleaved_other(0, 273, 4))
+    ssb = np.zeros(273, np.uint8)
+    ssb[100:120] = 1
+    reserved = [(np.ones(273, np.uint8), 0x111, (1 << 5) | (1 << 12)), (ssb, 0xFFF, 0b111100)]
+    cfg = dict(rnti=0x4601, n_id=7, qm=8, nof_layers=4, nof_ports=4, bwp_start_rb=0, bwp_size_rb=273, rb_start=0,
+               nof_rb=0, start_symbol=1, nof_symbols=13, dmrs_symbol_mask=(1 << 2) | (1 << 11), dmrs_type2=0,
+               nof_cdm_groups_without_data=2, scaling=1.0, vrb_mask=vrb, interleave=4, reserved=reserved, prg_size=4)
+    cfg["prg_weights"] = ((rng.normal(size=(69, 4, 4)) + 1j * rng.normal(size=(69, 4, 4))) / 2).astype(np.complex64)
+    w = np.eye(4, dtype=np.complex64)
+    m = to_general_mod(cfg, w, crb, 273)
+    nbits = m.nof_re(273) * 32
+    cw = rng.integers(0, 256, nbits // 8).astype(np.uint8)
+    want, _ = pdsch_modulate_general(orc.lib, cfg, w, cw, nbits, 273, crb_mask=crb)
+    got = srsgpu.PdschModulator(ctx, 273, 4).modulate(cw, m)
+    assert np.array_equal(got, want)
+
+
 def test_pdsch_modulator_rejects_invalid(ctx):
     """The reference's assertions: time allocation beyond the slot, codeword length not filling the allocation."""
     import srsgpu

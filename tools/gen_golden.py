@@ -276,12 +276,43 @@ PUSCH_DEMOD_KEYS = ["rnti", "n_id", "qm", "nof_layers", "nof_rx_ports", "start_s
                     "dmrs_symbol_mask", "dmrs_type2", "nof_cdm_groups_without_data", "rb_start", "nof_rb"]
 
 
+def gen_pdsch_mod_general(ref, rng):
+    """General PDSCH allocations made by the reference (ref_pdsch_modulate_ex): VRB bitmaps non-interleaved /
+    interleaved, reserved RE patterns, wideband or single-PRG precoding (multi-PRG: see
+    test_pdsch_modulator_multi_prg_reference_defect), each with the reference's CRB mask."""
+    from oracle_lib import pdsch_modulate_general
+    from pdsch_mod_cases import random_general_config
+    G = 32
+    out = {}
+    for i in range(10):
+        cfg, nbits, w = random_general_config(rng, G, interleave=[0, 2, 4][i % 3], prg=[0, G][i % 2])
+        cw = rng.integers(0, 256, (nbits + 7) // 8).astype(np.uint8)
+        grid, crb = pdsch_modulate_general(ref.lib, cfg, w, cw, nbits, G)
+        out[f"case{i}_cfg"] = np.array([cfg[k] for k in GENERAL_KEYS] + [nbits, G], np.int64)
+        out[f"case{i}_scaling"] = np.float32(cfg["scaling"])
+        out[f"case{i}_vrb"] = cfg["vrb_mask"]
+        out[f"case{i}_res_crb"] = np.array([r[0] for r in cfg["reserved"]], np.uint8).reshape(-1, G)
+        out[f"case{i}_res_masks"] = np.array([[r[1], r[2]] for r in cfg["reserved"]], np.int64).reshape(-1, 2)
+        out[f"case{i}_w"] = w
+        out[f"case{i}_prg_w"] = cfg["prg_weights"] if cfg["prg_size"] else np.zeros((0,), np.complex64)
+        out[f"case{i}_cw"] = cw
+        out[f"case{i}_grid"] = grid
+        out[f"case{i}_crb"] = crb
+    np.savez_compressed(os.path.join(OUT, "pdsch_mod_general.npz"), **out)
+
+
+GENERAL_KEYS = ["rnti", "n_id", "qm", "nof_layers", "nof_ports", "bwp_start_rb", "bwp_size_rb", "start_symbol",
+                "nof_symbols", "dmrs_symbol_mask", "dmrs_type2", "nof_cdm_groups_without_data", "interleave",
+                "prg_size"]
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     ref = Reference()
     if len(sys.argv) > 1:  # regenerate only the named fixture sets, e.g. `python tools/gen_golden.py ofdm`
         for name in sys.argv[1:]:
-            seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18, "pdsch_dmrs": 19, "pusch_chest_cfo": 20}[name]
+            seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18, "pdsch_dmrs": 19, "pusch_chest_cfo": 20,
+                    "pdsch_mod_general": 21}[name]
             globals()["gen_" + name](ref, np.random.default_rng(seed))
         return
     gen_crc(ref, np.random.default_rng(10))
@@ -295,6 +326,7 @@ def main():
     gen_pusch_chest(ref, np.random.default_rng(18))
     gen_pdsch_dmrs(ref, np.random.default_rng(19))
     gen_pusch_chest_cfo(ref, np.random.default_rng(20))
+    gen_pdsch_mod_general(ref, np.random.default_rng(21))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

@@ -325,6 +325,18 @@ int srsgpu_pdsch_dmrs_plan_create(srsgpu_context*                 ctx,
                                   uint32_t                        grid_nof_ports,
                                   srsgpu_pdsch_dmrs_plan**        plan);
 
+/** As srsgpu_pdsch_dmrs_plan_create, with an optional extension per transmission (NULL array or NULL crb_mask: the
+ *  contiguous rb_start / nof_rb allocation): crb_mask is dmrs_pdsch_processor::config_t::rb_mask (one byte per grid
+ *  CRB, any pattern; the sequence skips the unallocated CRBs, dmrs_helper.cpp dmrs_sequence_generate). Reserved
+ *  patterns and PRGs are rejected: the reference's DM-RS precoding has one PRG (dmrs_pdsch_processor_impl.cpp:149). */
+int srsgpu_pdsch_dmrs_plan_create_ex(srsgpu_context*                 ctx,
+                                     const srsgpu_pdsch_dmrs_config* cfgs,
+                                     const srsgpu_alloc_ext*         exts,
+                                     uint32_t                        nof_tx,
+                                     uint32_t                        grid_nof_prb,
+                                     uint32_t                        grid_nof_ports,
+                                     srsgpu_pdsch_dmrs_plan**        plan);
+
 /** Writes the DM-RS REs of every planned transmission into d_grids. Asynchronous on `stream`. */
 int srsgpu_pdsch_dmrs_plan_execute(const srsgpu_pdsch_dmrs_plan* plan, uint32_t* d_grids, void* stream);
 

@@ -17,9 +17,10 @@ using namespace srsran;
 
 extern "C" {
 
-/// Maps the DM-RS of one PDSCH transmission (contiguous CRB allocation, wideband precoding nof_ports x nof_layers
-/// weights, row-major by port) into a zeroed (nof_ports x 14 x 12 * grid_nof_prb) grid; writes it as bf16 pairs.
-int ref_dmrs_pdsch_map(int             numerology,
+/// Maps the DM-RS of one PDSCH transmission (CRB allocation rb_mask: crb_mask, one byte per grid CRB, or the
+/// contiguous [rb_start, rb_start + nof_rb) when crb_mask is NULL; wideband precoding nof_ports x nof_layers weights,
+/// row-major by port) into a zeroed (nof_ports x 14 x 12 * grid_nof_prb) grid; writes it as bf16 pairs.
+int ref_dmrs_pdsch_map_mask(int             numerology,
                        int             slot_index,
                        int             scrambling_id,
                        int             n_scid,
@@ -32,6 +33,7 @@ int ref_dmrs_pdsch_map(int             numerology,
                        int             nof_rb,
                        float           amplitude,
                        const float*    weights,
+                       const uint8_t*  crb_mask,
                        int             grid_nof_prb,
                        uint16_t*       grid_out)
 {
@@ -53,7 +55,13 @@ int ref_dmrs_pdsch_map(int             numerology,
     cfg.symbols_mask.set(l, ((dmrs_symbol_mask >> l) & 1U) != 0);
   }
   cfg.rb_mask = crb_bitmap(grid_nof_prb);
-  cfg.rb_mask.fill(rb_start, rb_start + nof_rb);
+  if (crb_mask != nullptr) {
+    for (int rb = 0; rb < grid_nof_prb; ++rb) {
+      cfg.rb_mask.set(rb, crb_mask[rb] != 0);
+    }
+  } else {
+    cfg.rb_mask.fill(rb_start, rb_start + nof_rb);
+  }
   cfg.precoding = precoding_configuration(nof_layers, nof_ports, 1, MAX_NOF_PRBS);
   for (int p = 0; p < nof_ports; ++p) {
     for (int l = 0; l < nof_layers; ++l) {
@@ -72,6 +80,40 @@ int ref_dmrs_pdsch_map(int             numerology,
     }
   }
   return 0;
+}
+
+int ref_dmrs_pdsch_map(int          numerology,
+                       int          slot_index,
+                       int          scrambling_id,
+                       int          n_scid,
+                       int          dmrs_type2,
+                       int          nof_layers,
+                       int          nof_ports,
+                       unsigned     dmrs_symbol_mask,
+                       int          reference_point_k_rb,
+                       int          rb_start,
+                       int          nof_rb,
+                       float        amplitude,
+                       const float* weights,
+                       int          grid_nof_prb,
+                       uint16_t*    grid_out)
+{
+  return ref_dmrs_pdsch_map_mask(numerology,
+                                 slot_index,
+                                 scrambling_id,
+                                 n_scid,
+                                 dmrs_type2,
+                                 nof_layers,
+                                 nof_ports,
+                                 dmrs_symbol_mask,
+                                 reference_point_k_rb,
+                                 rb_start,
+                                 nof_rb,
+                                 amplitude,
+                                 weights,
+                                 nullptr,
+                                 grid_nof_prb,
+                                 grid_out);
 }
 
 } // extern "C"

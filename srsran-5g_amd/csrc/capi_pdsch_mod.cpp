@@ -465,6 +465,17 @@ int srsgpu_pdsch_dmrs_plan_create(srsgpu_context*                 ctx,
                                   uint32_t                        grid_nof_ports,
                                   srsgpu_pdsch_dmrs_plan**        plan_out)
 {
+  return srsgpu_pdsch_dmrs_plan_create_ex(ctx, cfgs, nullptr, nof_tx, grid_nof_prb, grid_nof_ports, plan_out);
+}
+
+int srsgpu_pdsch_dmrs_plan_create_ex(srsgpu_context*                 ctx,
+                                     const srsgpu_pdsch_dmrs_config* cfgs,
+                                     const srsgpu_alloc_ext*         exts,
+                                     uint32_t                        nof_tx,
+                                     uint32_t                        grid_nof_prb,
+                                     uint32_t                        grid_nof_ports,
+                                     srsgpu_pdsch_dmrs_plan**        plan_out)
+{
   if (ctx == nullptr || plan_out == nullptr || (cfgs == nullptr && nof_tx > 0)) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
@@ -475,9 +486,32 @@ int srsgpu_pdsch_dmrs_plan_create(srsgpu_context*                 ctx,
   std::vector<dmrs_job> jobs;
   for (uint32_t t = 0; t < nof_tx; ++t) {
     const srsgpu_pdsch_dmrs_config& c = cfgs[t];
+    const srsgpu_alloc_ext*         x = (exts != nullptr) ? &exts[t] : nullptr;
+    if (x != nullptr && (x->nof_reserved > 0 || x->prg_size > 0)) {
+      // dmrs_pdsch_processor_impl.cpp:149 builds each CDM group's precoding with one PRG (more PRGs assert there).
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: PDSCH DM-RS takes a CRB mask only (no reserved REs or PRGs)", t);
+    }
+    // Allocated CRB intervals (dmrs_helper.cpp dmrs_sequence_generate for_each_interval over rb_mask).
+    std::vector<std::pair<unsigned, unsigned>> runs;
+    if (x != nullptr && x->crb_mask != nullptr) {
+      for (unsigned rb = 0; rb < grid_nof_prb;) {
+        if (x->crb_mask[rb] == 0) {
+          ++rb;
+          continue;
+        }
+        unsigned e = rb;
+        while (e < grid_nof_prb && x->crb_mask[e] != 0) {
+          ++e;
+        }
+        runs.emplace_back(rb, e);
+        rb = e;
+      }
+    } else if (c.nof_rb >= 1 && c.rb_start + c.nof_rb <= grid_nof_prb) {
+      runs.emplace_back(c.rb_start, c.rb_start + c.nof_rb);
+    }
     if (c.nof_layers < 1 || c.nof_layers > 4 || c.nof_ports < c.nof_layers || c.nof_ports > grid_nof_ports ||
-        (c.dmrs_type != 1 && c.dmrs_type != 2) || c.n_scid > 1 || c.nof_rb < 1 ||
-        c.rb_start + c.nof_rb > grid_nof_prb || c.rb_start < c.reference_point_k_rb || (c.dmrs_symbol_mask >> 14)) {
+        (c.dmrs_type != 1 && c.dmrs_type != 2) || c.n_scid > 1 || runs.empty() ||
+        runs.front().first < c.reference_point_k_rb || (c.dmrs_symbol_mask >> 14)) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid DM-RS configuration", t);
     }
     const uint32_t per_rb = c.dmrs_type == 2 ? 4 : 6;
@@ -485,27 +519,31 @@ int srsgpu_pdsch_dmrs_plan_create(srsgpu_context*                 ctx,
       if (((c.dmrs_symbol_mask >> l) & 1u) == 0) {
         continue;
       }
-      dmrs_job       jb{};
-      const uint64_t nid = c.scrambling_id;
-      jb.grid_base   = c.grid_index * grid_nof_ports * 14u * nsc + l * nsc + c.rb_start * 12u;
-      jb.port_stride = 14u * nsc;
-      jb.c_init      = static_cast<uint32_t>(
-          ((14ull * c.slot_index + l + 1) * (2 * nid + 1) * (1ull << 17) + 2 * nid + c.n_scid) % (1ull << 31));
-      jb.seq_offset = (c.rb_start - c.reference_point_k_rb) * per_rb;
-      jb.amp        = static_cast<float>(M_SQRT1_2) * c.amplitude;  // dmrs_pdsch_processor_impl.cpp:61
-      for (int p = 0; p < 4; ++p) {
-        for (int q = 0; q < 4; ++q) {
-          const bool used = p < c.nof_ports && q < c.nof_layers;
-          jb.w[p][q][0]   = used ? c.precoding[p][q][0] : 0.f;
-          jb.w[p][q][1]   = used ? c.precoding[p][q][1] : 0.f;
+      for (const auto& run : runs) {
+        // One job per symbol and CRB interval: the sequence index of CRB n is (n - k_ref) x per RB, and the cover
+        // code parity of a DM-RS RE is that of its index within the PRB (per RB is even).
+        dmrs_job       jb{};
+        const uint64_t nid = c.scrambling_id;
+        jb.grid_base   = c.grid_index * grid_nof_ports * 14u * nsc + l * nsc + run.first * 12u;
+        jb.port_stride = 14u * nsc;
+        jb.c_init      = static_cast<uint32_t>(
+            ((14ull * c.slot_index + l + 1) * (2 * nid + 1) * (1ull << 17) + 2 * nid + c.n_scid) % (1ull << 31));
+        jb.seq_offset = (run.first - c.reference_point_k_rb) * per_rb;
+        jb.amp        = static_cast<float>(M_SQRT1_2) * c.amplitude;  // dmrs_pdsch_processor_impl.cpp:61
+        for (int p = 0; p < 4; ++p) {
+          for (int q = 0; q < 4; ++q) {
+            const bool used = p < c.nof_ports && q < c.nof_layers;
+            jb.w[p][q][0]   = used ? c.precoding[p][q][0] : 0.f;
+            jb.w[p][q][1]   = used ? c.precoding[p][q][1] : 0.f;
+          }
         }
+        jb.nof_pilots = static_cast<uint16_t>((run.second - run.first) * per_rb);
+        jb.type2      = c.dmrs_type == 2;
+        jb.L          = c.nof_layers;
+        jb.P          = c.nof_ports;
+        jb.lp         = (l > 0 && ((c.dmrs_symbol_mask >> (l - 1)) & 1u)) ? 1 : 0;
+        jobs.push_back(jb);
       }
-      jb.nof_pilots = static_cast<uint16_t>(c.nof_rb * per_rb);
-      jb.type2      = c.dmrs_type == 2;
-      jb.L          = c.nof_layers;
-      jb.P          = c.nof_ports;
-      jb.lp         = (l > 0 && ((c.dmrs_symbol_mask >> (l - 1)) & 1u)) ? 1 : 0;
-      jobs.push_back(jb);
     }
   }
   std::lock_guard<std::mutex> lock(ctx->mtx);

@@ -316,6 +316,8 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pdsch_modulator_plan_destroy.restype = None
     lib.srsgpu_pdsch_dmrs_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                   ctypes.POINTER(P)]
+    lib.srsgpu_pdsch_dmrs_plan_create_ex.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                     ctypes.POINTER(P)]
     lib.srsgpu_pdsch_dmrs_plan_execute.argtypes = [P, P, P]
     lib.srsgpu_pdsch_dmrs_plan_destroy.argtypes = [P]
     lib.srsgpu_pdsch_dmrs_plan_destroy.restype = None
@@ -366,7 +368,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
     "srsgpu_pusch_chest_plan_create", "srsgpu_pusch_chest_plan_execute", "srsgpu_pusch_chest_plan_destroy",
-    "srsgpu_pdsch_dmrs_plan_create", "srsgpu_pdsch_dmrs_plan_execute", "srsgpu_pdsch_dmrs_plan_destroy",
+    "srsgpu_pdsch_dmrs_plan_create", "srsgpu_pdsch_dmrs_plan_create_ex", "srsgpu_pdsch_dmrs_plan_execute", "srsgpu_pdsch_dmrs_plan_destroy",
 ]
 
 
@@ -905,8 +907,9 @@ class PdschModulator:
 
 @dataclass
 class PdschDmrs:
-    """dmrs_pdsch_processor::config_t (dmrs_pdsch_processor.h:38): contiguous CRB allocation, DM-RS ports
-    0..nof_layers-1, wideband precoding weights (nof_ports x nof_layers complex)."""
+    """dmrs_pdsch_processor::config_t (dmrs_pdsch_processor.h:38): contiguous CRB allocation (or `crb_mask`, one byte
+    per grid CRB: rb_mask of any type-0 / interleaved allocation), DM-RS ports 0..nof_layers-1, wideband precoding
+    weights (nof_ports x nof_layers complex)."""
     slot_index: int
     scrambling_id: int
     n_scid: int
@@ -919,6 +922,26 @@ class PdschDmrs:
     nof_rb: int
     amplitude: float
     weights: np.ndarray
+    crb_mask: Optional[np.ndarray] = None
+
+    def is_general(self) -> bool:
+        return self.crb_mask is not None
+
+
+def make_dmrs_exts(dmrs, grid_nof_prb: int):
+    """srsgpu_alloc_ext array for PDSCH DM-RS CRB masks (None when every allocation is contiguous) + keep-alive list."""
+    if not any(d.crb_mask is not None for d in dmrs):
+        return None, []
+    exts = (AllocExtC * len(dmrs))()
+    keep = []
+    for i, d in enumerate(dmrs):
+        if d.crb_mask is not None:
+            c = np.zeros(grid_nof_prb, np.uint8)
+            src = np.asarray(d.crb_mask, np.uint8)[:grid_nof_prb]
+            c[:src.size] = src
+            keep.append(c)
+            exts[i].crb_mask = c.ctypes.data
+    return exts, keep
 
 
 def make_pdsch_dmrs_configs(dmrs: Sequence[PdschDmrs], grid_index: Sequence[int]):
@@ -941,11 +964,16 @@ def make_pdsch_dmrs_configs(dmrs: Sequence[PdschDmrs], grid_index: Sequence[int]
 class PdschDmrsPlan:
     """srsgpu_pdsch_dmrs_plan: PDSCH DM-RS generation, cover codes, precoding and mapping into bf16 grids."""
 
-    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4):
+    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4, exts=None):
         self.ctx = ctx
         h = ctypes.c_void_p()
-        _check(_lib.srsgpu_pdsch_dmrs_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p), len(cfg_array),
-                                                  grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
+        if exts is None:
+            _check(_lib.srsgpu_pdsch_dmrs_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                      len(cfg_array), grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
+        else:
+            _check(_lib.srsgpu_pdsch_dmrs_plan_create_ex(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                         ctypes.cast(exts, ctypes.c_void_p), len(cfg_array),
+                                                         grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
         self.handle = h
 
     def execute(self, d_grids, stream=None):

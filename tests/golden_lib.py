@@ -185,6 +185,18 @@ def pdsch_dmrs_cases():
         i += 1
 
 
+def pdsch_dmrs_mask_cases():
+    """Yields (cfg dict, weights (P, L) complex64, CRB mask (51,) uint8, reference grid (P, 14, 612, 2) bf16) made by
+    dmrs_pdsch_processor_impl with general rb_mask allocations (51-PRB grids)."""
+    d = _load("pdsch_dmrs_mask.npz")
+    i = 0
+    while f"case{i}_cfg" in d:
+        cfg = {k: int(v) for k, v in zip(PDSCH_DMRS_KEYS, d[f"case{i}_cfg"])}
+        cfg["amplitude"] = float(d[f"case{i}_amplitude"])
+        yield cfg, d[f"case{i}_weights"], d[f"case{i}_crb_mask"], d[f"case{i}_grid"]
+        i += 1
+
+
 GENERAL_KEYS = ["rnti", "n_id", "qm", "nof_layers", "nof_ports", "bwp_start_rb", "bwp_size_rb", "start_symbol",
                 "nof_symbols", "dmrs_symbol_mask", "dmrs_type2", "nof_cdm_groups_without_data", "interleave",
                 "prg_size"]

@@ -219,17 +219,20 @@ class Reference(_Lib):
           grid_nof_prb, P, fd, td, int(compensate_cfo), _ptr(g), _ptr(ce), *[_ptr(o) for o in outs])
         return (ce,) + tuple(outs)
 
-    def dmrs_pdsch_map(self, cfg, weights, grid_nof_prb, numerology=1):
-        """dmrs_pdsch_processor_impl::map into a zeroed grid: (P, 14, nsc, 2) bf16 bit patterns."""
+    def dmrs_pdsch_map(self, cfg, weights, grid_nof_prb, numerology=1, crb_mask=None):
+        """dmrs_pdsch_processor_impl::map into a zeroed grid: (P, 14, nsc, 2) bf16 bit patterns. crb_mask (one byte
+        per grid CRB) replaces the contiguous rb_start / nof_rb allocation as config_t::rb_mask."""
         w = np.ascontiguousarray(weights, dtype=np.complex64).view(np.float32)
         P = cfg["nof_ports"]
         grid = np.zeros((P, 14, 12 * grid_nof_prb, 2), np.uint16)
-        f = self.lib.ref_dmrs_pdsch_map
+        m = None if crb_mask is None else np.ascontiguousarray(np.asarray(crb_mask, np.uint8)[:grid_nof_prb])
+        f = self.lib.ref_dmrs_pdsch_map_mask
         f.restype = ctypes.c_int
-        f.argtypes = [ctypes.c_int] * 7 + [ctypes.c_uint] + [ctypes.c_int] * 3 + [ctypes.c_float, _P, ctypes.c_int, _P]
+        f.argtypes = ([ctypes.c_int] * 7 + [ctypes.c_uint] + [ctypes.c_int] * 3 + [ctypes.c_float, _P, _P,
+                                                                                  ctypes.c_int, _P])
         f(numerology, cfg["slot"], cfg["scrambling_id"], cfg["n_scid"], cfg["dmrs_type2"], cfg["nof_layers"], P,
           cfg["dmrs_symbol_mask"], cfg["reference_point_k_rb"], cfg["rb_start"], cfg["nof_rb"], cfg["amplitude"],
-          _ptr(w), grid_nof_prb, _ptr(grid))
+          _ptr(w), None if m is None else _ptr(m), grid_nof_prb, _ptr(grid))
         return grid
 
     def ofdm_slot_size(self, numerology, bw_rb, dft_size, extended, slot):

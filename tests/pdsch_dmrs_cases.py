@@ -19,3 +19,20 @@ def random_config(rng, grid_prb, nof_layers=None, nof_ports=None):
                amplitude=float(rng.choice([1.0, 1.4125375, 0.5])))
     w = ((rng.normal(size=(P, L)) + 1j * rng.normal(size=(P, L))) / 2).astype(np.complex64)
     return cfg, w
+
+
+def random_mask_config(rng, grid_prb, nof_layers=None, nof_ports=None):
+    """A random configuration with a general CRB mask (rb_mask): type-0 style RBG runs or a random scatter, the
+    sequence reference point at or below the first allocated CRB. Returns (cfg, weights, crb_mask)."""
+    cfg, w = random_config(rng, grid_prb, nof_layers, nof_ports)
+    if rng.random() < 0.5:
+        rbg = int(rng.choice([2, 4, 8, 16]))
+        sel = rng.random((grid_prb + rbg - 1) // rbg) < rng.uniform(0.2, 0.8)
+        mask = np.repeat(sel, rbg)[:grid_prb].astype(np.uint8)
+    else:
+        mask = (rng.random(grid_prb) < rng.uniform(0.1, 0.9)).astype(np.uint8)
+    if not mask.any():
+        mask[int(rng.integers(0, grid_prb))] = 1
+    first = int(np.flatnonzero(mask)[0])
+    cfg.update(rb_start=first, nof_rb=int(mask.sum()), reference_point_k_rb=int(rng.integers(0, first + 1)))
+    return cfg, w, mask

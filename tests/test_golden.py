@@ -174,3 +174,13 @@ def test_pdsch_dmrs_golden():
         assert np.array_equal(M.dmrs_map(cfg, w, 24), grid), cfg
         n += 1
     assert n == 10
+
+
+def test_pdsch_dmrs_crb_mask_golden():
+    """The PDSCH DM-RS restatement over general CRB masks bit-exact against the reference's grids."""
+    import pdsch_dmrs_oracle as M
+    n = 0
+    for cfg, w, mask, grid in G.pdsch_dmrs_mask_cases():
+        assert np.array_equal(M.dmrs_map(cfg, w, 51, crb_mask=mask), grid), cfg
+        n += 1
+    assert n == 8

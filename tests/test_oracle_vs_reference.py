@@ -383,3 +383,19 @@ def test_pdsch_dmrs_oracle_vs_reference(ref, seed):
     rng = np.random.default_rng(500 + seed)
     cfg, w = random_config(rng, 24)
     assert np.array_equal(M.dmrs_map(cfg, w, 24), ref.dmrs_pdsch_map(cfg, w, 24)), cfg
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_pdsch_dmrs_crb_mask_oracle_vs_reference(ref, seed):
+    """PDSCH DM-RS over a general CRB mask (rb_mask: RBG runs or scattered CRBs, the sequence skipping the gaps,
+    dmrs_helper.cpp:64) bit-exact against the reference's dmrs_pdsch_processor_impl."""
+    import pdsch_dmrs_oracle as M
+    from pdsch_dmrs_cases import random_mask_config
+    rng = np.random.default_rng(700 + seed)
+    cfg, w, mask = random_mask_config(rng, 51)
+    want = ref.dmrs_pdsch_map(cfg, w, 51, crb_mask=mask)
+    assert np.array_equal(M.dmrs_map(cfg, w, 51, crb_mask=mask), want), cfg
+    # A mask of exactly the contiguous allocation [rb_start, rb_start + nof_rb) reproduces the plain configuration.
+    contiguous = np.zeros(51, np.uint8)
+    contiguous[cfg["rb_start"]:cfg["rb_start"] + cfg["nof_rb"]] = 1
+    assert np.array_equal(ref.dmrs_pdsch_map(cfg, w, 51, crb_mask=contiguous), ref.dmrs_pdsch_map(cfg, w, 51))

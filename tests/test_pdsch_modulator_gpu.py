@@ -199,22 +199,25 @@ def test_pdsch_modulator_rejects_invalid(ctx):
         srsgpu.PdschModulatorPlan(ctx, arr, 273, 4)
 
 
-def to_dmrs(cfg, w):
+def to_dmrs(cfg, w, crb_mask=None):
     import srsgpu
     return srsgpu.PdschDmrs(slot_index=cfg["slot"], scrambling_id=cfg["scrambling_id"], n_scid=cfg["n_scid"],
                             dmrs_type=2 if cfg["dmrs_type2"] else 1, nof_layers=cfg["nof_layers"],
                             nof_ports=cfg["nof_ports"], dmrs_symbol_mask=cfg["dmrs_symbol_mask"],
                             reference_point_k_rb=cfg["reference_point_k_rb"], rb_start=cfg["rb_start"],
-                            nof_rb=cfg["nof_rb"], amplitude=cfg["amplitude"], weights=w)
+                            nof_rb=cfg["nof_rb"], amplitude=cfg["amplitude"], weights=w, crb_mask=crb_mask)
 
 
-def run_dmrs(ctx, items, grid_prb, S):
+def run_dmrs(ctx, items, grid_prb, S, masks=None):
     import torch
     import srsgpu
     dev = torch.device("cuda", 0)
     d_grid = torch.zeros(S * 4 * 14 * 12 * grid_prb, dtype=torch.int32, device=dev)
-    plan = srsgpu.PdschDmrsPlan(ctx, srsgpu.make_pdsch_dmrs_configs([to_dmrs(c, w) for c, w, _ in items],
-                                                                    [g for _, _, g in items]), grid_prb, 4)
+    masks = masks or [None] * len(items)
+    dmrs = [to_dmrs(c, w, m) for (c, w, _), m in zip(items, masks)]
+    exts, _keep = srsgpu.make_dmrs_exts(dmrs, grid_prb)
+    plan = srsgpu.PdschDmrsPlan(ctx, srsgpu.make_pdsch_dmrs_configs(dmrs, [g for _, _, g in items]), grid_prb, 4,
+                                exts)
     plan.execute(d_grid)
     torch.cuda.synchronize()
     plan.close()
@@ -238,3 +241,35 @@ def test_pdsch_dmrs_random_vs_oracle(ctx):
     got = run_dmrs(ctx, [(c, w, i) for i, (c, w) in enumerate(items)], 52, len(items))
     for i, (cfg, w) in enumerate(items):
         assert np.array_equal(got[i, : cfg["nof_ports"]], M.dmrs_map(cfg, w, 52)), cfg
+
+
+def test_pdsch_dmrs_crb_mask_golden(ctx):
+    """PDSCH DM-RS over general CRB masks (rb_mask) bit-exact against the reference's grids, in ONE plan together
+    with a contiguous transmission."""
+    cases = list(G.pdsch_dmrs_mask_cases())
+    plain = list(G.pdsch_dmrs_cases())[0]
+    items = [(c, w, i) for i, (c, w, _, _) in enumerate(cases)] + [(plain[0], plain[1], len(cases))]
+    masks = [m for _, _, m, _ in cases] + [None]
+    got = run_dmrs(ctx, items, 51, len(items), masks)
+    for i, (cfg, w, _, want) in enumerate(cases):
+        assert np.array_equal(got[i, : cfg["nof_ports"]], want), cfg
+    import pdsch_dmrs_oracle as M
+    assert np.array_equal(got[-1, : plain[0]["nof_ports"]], M.dmrs_map(plain[0], plain[1], 51))
+
+
+def test_pdsch_dmrs_crb_mask_random_vs_oracle(ctx):
+    """40 random CRB-mask configurations against the oracle, bit-exact; reserved patterns / PRGs are rejected."""
+    import pdsch_dmrs_oracle as M
+    import srsgpu
+    from pdsch_dmrs_cases import random_mask_config
+    rng = np.random.default_rng(33)
+    items = [random_mask_config(rng, 273) for _ in range(40)]
+    got = run_dmrs(ctx, [(c, w, i) for i, (c, w, _) in enumerate(items)], 273, len(items), [m for _, _, m in items])
+    for i, (cfg, w, m) in enumerate(items):
+        assert np.array_equal(got[i, : cfg["nof_ports"]], M.dmrs_map(cfg, w, 273, crb_mask=m)), cfg
+    cfg, w, m = items[0]
+    d = to_dmrs(cfg, w, m)
+    exts, _keep = srsgpu.make_dmrs_exts([d], 273)
+    exts[0].prg_size = 4
+    with pytest.raises(srsgpu.SrsGpuError):
+        srsgpu.PdschDmrsPlan(ctx, srsgpu.make_pdsch_dmrs_configs([d], [0]), 273, 4, exts)

@@ -266,6 +266,20 @@ def gen_pdsch_dmrs(ref, rng):
     np.savez_compressed(os.path.join(OUT, "pdsch_dmrs.npz"), **out)
 
 
+def gen_pdsch_dmrs_mask(ref, rng):
+    """Reference PDSCH DM-RS grids over general CRB masks (config_t::rb_mask) in 51-PRB grids."""
+    from pdsch_dmrs_cases import random_mask_config
+    out = {}
+    for i in range(8):
+        cfg, w, mask = random_mask_config(rng, 51)
+        out[f"case{i}_cfg"] = np.array([cfg[k] for k in PDSCH_DMRS_KEYS], np.int64)
+        out[f"case{i}_amplitude"] = np.float32(cfg["amplitude"])
+        out[f"case{i}_weights"] = w
+        out[f"case{i}_crb_mask"] = mask
+        out[f"case{i}_grid"] = ref.dmrs_pdsch_map(cfg, w, 51, crb_mask=mask)
+    np.savez_compressed(os.path.join(OUT, "pdsch_dmrs_mask.npz"), **out)
+
+
 PDSCH_DMRS_KEYS = ["slot", "scrambling_id", "n_scid", "dmrs_type2", "nof_layers", "nof_ports", "dmrs_symbol_mask",
                    "reference_point_k_rb", "rb_start", "nof_rb"]
 
@@ -312,7 +326,7 @@ def main():
     if len(sys.argv) > 1:  # regenerate only the named fixture sets, e.g. `python tools/gen_golden.py ofdm`
         for name in sys.argv[1:]:
             seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18, "pdsch_dmrs": 19, "pusch_chest_cfo": 20,
-                    "pdsch_mod_general": 21}[name]
+                    "pdsch_mod_general": 21, "pdsch_dmrs_mask": 22}[name]
             globals()["gen_" + name](ref, np.random.default_rng(seed))
         return
     gen_crc(ref, np.random.default_rng(10))
@@ -327,6 +341,7 @@ def main():
     gen_pdsch_dmrs(ref, np.random.default_rng(19))
     gen_pusch_chest_cfo(ref, np.random.default_rng(20))
     gen_pdsch_mod_general(ref, np.random.default_rng(21))
+    gen_pdsch_dmrs_mask(ref, np.random.default_rng(22))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

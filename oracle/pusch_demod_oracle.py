@@ -240,3 +240,114 @@ def demodulate(cfg, grid, ch_est, noise_var, mmse=False):
     llr = demap(eq.reshape(-1), nvar.reshape(-1), qm).astype(np.int16)
     c = gold_sequence(cfg["rnti"] * (1 << 15) + cfg["n_id"], llr.size)
     return np.where(c == 1, -llr, llr).astype(np.int8)
+
+
+# ----------------------------------------------------------------------------------------------------------------------
+# General allocations, transform precoding and post-equalization statistics (pusch_demodulator_impl.cpp:272-444).
+# ----------------------------------------------------------------------------------------------------------------------
+
+def allocated_rbs(rb_start, nof_rb, crb_mask=None):
+    """CRBs of the allocation in ascending order: config.rb_mask (crb_mask, one byte per grid CRB) or the contiguous
+    [rb_start, rb_start + nof_rb)."""
+    if crb_mask is None:
+        return list(range(rb_start, rb_start + nof_rb))
+    return [int(i) for i in np.flatnonzero(np.asarray(crb_mask))]
+
+
+def data_res_mask(start_symbol, nof_symbols, dmrs_symbol_mask, dmrs_type2, nof_cdm_groups_without_data, rbs):
+    """As data_res over an arbitrary CRB list: re_mask = rb_mask kron active REs per PRB (pusch_demodulator_impl.cpp:
+    290), symbol-major, ascending subcarrier."""
+    out = []
+    for l in range(start_symbol, start_symbol + nof_symbols):
+        dm = (dmrs_symbol_mask >> l) & 1
+        for rb in rbs:
+            for k in range(12):
+                group = (k % 6) // 2 if dmrs_type2 else k % 2
+                if dm and group < nof_cdm_groups_without_data:
+                    continue
+                out.append((l, rb * 12 + k))
+    return out
+
+
+def modulate_bits(bits, qm):
+    """Hard bits (n * qm,) -> complex64 constellation points, TS 38.211 section 5.1 (modulation_mapper_lut_impl.cpp:39
+    builds the same points: Gray PAM per component, amplitude 1 / sqrt(average power))."""
+    b = np.asarray(bits, np.int64).reshape(-1, qm)
+    half = qm // 2
+    avg = {2: 2, 4: 10, 6: 42, 8: 170}[qm]
+
+    def pam(cols):
+        # s_j = 1 - 2 b_j: s0 (2^(h-1) - s2 (2^(h-2) - ... (2 - s_{2(h-1)})))
+        s = [1 - 2 * b[:, c] for c in cols]
+        if half == 1:
+            return s[0]
+        inner = 2 - s[half - 1]
+        for j in range(half - 2, 0, -1):
+            inner = (1 << (half - j)) - s[j] * inner
+        return s[0] * inner
+
+    re = pam([2 * j for j in range(half)])
+    im = pam([2 * j + 1 for j in range(half)])
+    a = F(1) / np.sqrt(F(avg))
+    return (re.astype(F) * a + 1j * (im.astype(F) * a)).astype(np.complex64)
+
+
+def transform_deprecode(eq, nvar):
+    """transform_precoder_dft_impl.cpp deprecode_ofdm_symbol (inverse DFT of the M_sc data REs, scaled 1 / sqrt(M_sc))
+    and deprecode_ofdm_symbol_noise (every valid noise variance -- positive, finite -- replaced by their mean)."""
+    m = eq.size
+    x = (np.fft.ifft(eq.astype(np.complex128)) * m / np.sqrt(m)).astype(np.complex64)
+    v = np.asarray(nvar, F)
+    valid = (v > 0) & np.isfinite(v)
+    mean = F(np.sum(v[valid], dtype=np.float64) / max(int(valid.sum()), 1)) if valid.any() else F(0)
+    return x, np.where(valid, mean, v).astype(F)
+
+
+def demodulate_ex(cfg, grid, ch_est, noise_var, mmse=False, crb_mask=None, transform_precoding=False,
+                  nvars_out=None):
+    """pusch_demodulator_impl::demodulate with a general CRB mask, transform precoding (one layer) and the
+    post-equalization statistics. Returns (descrambled LLRs int8, stats (15, 2) float64: per OFDM symbol and, in row
+    14, for the whole transmission, (post-equalization SINR dB, EVM); NaN rows for symbols without data).
+
+    Statistics (:355-:443): SINR = -10 log10(mean of the equalizer noise variances that are not infinite) or +inf with
+    none; EVM of a symbol = sqrt(mean |modulate(hard(LLR)) - equalized|^2) over its REs x layers
+    (evm_calculator_generic_impl.cpp; hard bit = LLR <= 0, before descrambling), total = the per-symbol EVMs weighted
+    by their sizes (filter_infinite_and_accumulate :225 skips the infinite values). nvars_out (a dict) receives each
+    symbol's equalizer noise variances."""
+    rbs = allocated_rbs(cfg["rb_start"], cfg["nof_rb"], crb_mask)
+    P, L, qm = cfg["nof_rx_ports"], cfg["nof_layers"], cfg["qm"]
+    llrs = []
+    stats = np.full((15, 2), np.nan)
+    tot_nv, tot_cnt, tot_evm, tot_n = 0.0, 0, 0.0, 0
+    for l in range(cfg["start_symbol"], cfg["start_symbol"] + cfg["nof_symbols"]):
+        res = data_res_mask(l, 1, cfg["dmrs_symbol_mask"], cfg["dmrs_type2"], cfg["nof_cdm_groups_without_data"], rbs)
+        if not res:
+            continue
+        sc = np.array([r[1] for r in res])
+        rx = grid[:P, l, sc]
+        H = np.transpose(ch_est[:L, :P, l, sc], (1, 0, 2))
+        if L <= 2 and not (mmse and L == 2):
+            eq, nvar = equalize(rx, H, noise_var, mmse)
+        else:
+            e, v = equalize_mmse(rx, H, noise_var)
+            eq, nvar = e.astype(np.complex64), v.astype(F)
+        eq, nvar = eq.reshape(-1), nvar.reshape(-1)
+        if transform_precoding:
+            assert L == 1
+            eq, nvar = transform_deprecode(eq, nvar)
+        if nvars_out is not None:
+            nvars_out[l] = nvar
+        fin = ~np.isinf(nvar)
+        s_nv, s_cnt = float(np.sum(nvar[fin], dtype=np.float64)), int(fin.sum())
+        llr = demap(eq, nvar, qm)
+        err = modulate_bits((llr <= 0).astype(np.uint8), qm) - eq
+        e2 = float(np.sum(err.real.astype(np.float64) ** 2 + err.imag.astype(np.float64) ** 2))
+        evm = np.sqrt(e2 / eq.size)
+        stats[l] = (-10 * np.log10(s_nv / s_cnt) if s_cnt and s_nv > 0 else np.inf, evm)
+        tot_nv, tot_cnt, tot_evm, tot_n = tot_nv + s_nv, tot_cnt + s_cnt, tot_evm + eq.size * evm, tot_n + eq.size
+        llrs.append(llr)
+    llr = np.concatenate(llrs).astype(np.int16) if llrs else np.zeros(0, np.int16)
+    c = gold_sequence(cfg["rnti"] * (1 << 15) + cfg["n_id"], llr.size)
+    if tot_n:
+        stats[14] = (-10 * np.log10(tot_nv / tot_cnt) if tot_cnt and tot_nv > 0 else np.inf, tot_evm / tot_n)
+    return np.where(c == 1, -llr, llr).astype(np.int8), stats

@@ -130,6 +130,22 @@ def pusch_demod_cases():
         i += 1
 
 
+def pusch_demod_general_cases():
+    """Yields (cfg dict, transform precoding flag, CRB mask or None, grid (P, 14, 384, 2) bf16, ch_est, noise_var,
+    reference LLRs, reference stats (15, 2): per-symbol and end (SINR dB, EVM), NaN when absent) made by
+    pusch_demodulator_impl with the EVM calculator, post-equalization SINR, CRB masks and transform precoding
+    (32-PRB grids)."""
+    d = _load("pusch_demod_general.npz")
+    i = 0
+    while f"case{i}_cfg" in d:
+        row = d[f"case{i}_cfg"]
+        cfg = {k: int(v) for k, v in zip(PUSCH_DEMOD_KEYS, row[:-1])}
+        crb = d[f"case{i}_crb"]
+        yield (cfg, bool(row[-1]), crb if crb.size else None, d[f"case{i}_grid"], d[f"case{i}_ch_est"],
+               d[f"case{i}_noise_var"], d[f"case{i}_llr"], d[f"case{i}_stats"])
+        i += 1
+
+
 def demapper_cases():
     """Yields (qm, symbols complex64, noise variances, reference LLRs) made by demodulation_mapper_impl."""
     d = _load("pusch_demod.npz")

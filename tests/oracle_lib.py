@@ -204,6 +204,27 @@ class Reference(_Lib):
               cfg["rb_start"], cfg["nof_rb"], grid_nof_prb, int(mmse), _ptr(g), _ptr(h), _ptr(nv), _ptr(out), cap)
         return out[:n]
 
+    def pusch_demodulate_ex(self, cfg, grid_u16, ch_est_u16, noise_var, grid_nof_prb, mmse=False, crb_mask=None,
+                            transform_precoding=False):
+        """ref_pusch_demodulate_ex: (codeword LLRs, stats (15, 2) float32 = per-symbol / end (SINR dB, EVM), NaN when
+        absent) with a general CRB mask, transform precoding, the EVM calculator and the post-equalization SINR."""
+        g = np.ascontiguousarray(grid_u16, dtype=np.uint16)
+        h = np.ascontiguousarray(ch_est_u16, dtype=np.uint16)
+        nv = np.ascontiguousarray(noise_var, dtype=np.float32)
+        cap = 12 * grid_nof_prb * 14 * cfg["nof_layers"] * cfg["qm"]
+        out = np.zeros(cap, np.int8)
+        stats = np.zeros((15, 2), np.float32)
+        m = None if crb_mask is None else np.ascontiguousarray(np.asarray(crb_mask, np.uint8)[:grid_nof_prb])
+        f = self.lib.ref_pusch_demodulate_ex
+        f.restype = ctypes.c_int
+        f.argtypes = ([ctypes.c_int] * 7 + [ctypes.c_uint] + [ctypes.c_int] * 4 + [_P] + [ctypes.c_int] * 3 + [_P] * 4
+                      + [ctypes.c_int, _P])
+        n = f(cfg["rnti"], cfg["n_id"], cfg["qm"], cfg["nof_layers"], cfg["nof_rx_ports"], cfg["start_symbol"],
+              cfg["nof_symbols"], cfg["dmrs_symbol_mask"], cfg["dmrs_type2"], cfg["nof_cdm_groups_without_data"],
+              cfg["rb_start"], cfg["nof_rb"], None if m is None else _ptr(m), int(transform_precoding), grid_nof_prb,
+              int(mmse), _ptr(g), _ptr(h), _ptr(nv), _ptr(out), cap, _ptr(stats))
+        return out[:n], stats
+
     def pusch_chest(self, cfg, grid_u16, grid_nof_prb, fd=2, td=0, compensate_cfo=False, numerology=1):
         """dmrs_pusch_estimator_impl::estimate of one single-layer transmission: (ch_est (P, 14, nsc, 2) bf16,
         noise_var, rsrp, epre, ta_s, cfo_hz) per port."""

@@ -45,3 +45,40 @@ def random_case(rng, grid_prb, nof_layers=None, nof_rx_ports=None, qm=None, snr_
     y = np.einsum("lpsk,lsk->psk", Hq, x)
     y += (rng.normal(size=y.shape) + 1j * rng.normal(size=y.shape)) * np.sqrt(nv[:, None, None] / 2)
     return cfg, bf16(y), bf16(H), nv
+
+
+def valid_tp_prbs(limit):
+    """PRB counts a transform-precoded allocation may take (TS 38.211 section 6.3.1.4: 2^a 3^b 5^c)."""
+    out = []
+    for n in range(1, limit + 1):
+        m = n
+        for f in (2, 3, 5):
+            while m % f == 0:
+                m //= f
+        if m == 1:
+            out.append(n)
+    return out
+
+
+def random_general_case(rng, grid_prb, transform_precoding=False, mask=True, nof_rx_ports=None, qm=None,
+                        snr_db=None, max_rb=None):
+    """random_case with a general CRB mask (RBG runs or scattered CRBs; with transform precoding, a PRB count the DFT
+    supports and DM-RS symbols without data). Returns (cfg, grid, ch_est, noise_var, crb_mask or None)."""
+    cfg, grid, H, nv = random_case(rng, grid_prb, nof_layers=1 if transform_precoding else None,
+                                   nof_rx_ports=nof_rx_ports, qm=qm, snr_db=snr_db, max_rb=max_rb)
+    lim = min(grid_prb, max_rb or grid_prb)
+    crb = None
+    if transform_precoding:
+        cfg["dmrs_type2"], cfg["nof_cdm_groups_without_data"] = 0, 2
+        nrb = int(rng.choice(valid_tp_prbs(lim)))
+    else:
+        nrb = int(rng.integers(1, lim + 1))
+    if mask:
+        crb = np.zeros(grid_prb, np.uint8)
+        crb[rng.choice(grid_prb, nrb, replace=False)] = 1
+        rbs = np.flatnonzero(crb)
+        cfg["rb_start"], cfg["nof_rb"] = int(rbs[0]), nrb
+    else:
+        cfg["rb_start"], cfg["nof_rb"] = int(rng.integers(0, grid_prb - nrb + 1)), nrb
+    return cfg, grid, H, nv, crb
+

@@ -212,6 +212,23 @@ def gen_pusch_demod(ref, rng):
     np.savez_compressed(os.path.join(OUT, "pusch_demod.npz"), **out)
 
 
+def gen_pusch_demod_general(ref, rng):
+    """Reference PUSCH demodulator LLRs and statistics (per-symbol / end post-equalization SINR and EVM) with general
+    CRB masks and transform precoding, in 32-PRB grids."""
+    from pusch_demod_cases import random_general_case
+    out = {}
+    specs = [(False, True, None), (True, True, None), (True, False, None), (False, True, 1), (True, True, 5),
+             (False, False, 32), (True, False, 32), (False, True, 16)]
+    for i, (tp, mask, max_rb) in enumerate(specs):
+        cfg, grid, H, nv, crb = random_general_case(rng, 32, transform_precoding=tp, mask=mask, max_rb=max_rb)
+        llr, stats = ref.pusch_demodulate_ex(cfg, grid, H, nv, 32, crb_mask=crb, transform_precoding=tp)
+        out[f"case{i}_cfg"] = np.array([cfg[k] for k in PUSCH_DEMOD_KEYS] + [int(tp)], np.int64)
+        out[f"case{i}_crb"] = crb if crb is not None else np.zeros(0, np.uint8)
+        out[f"case{i}_grid"], out[f"case{i}_ch_est"], out[f"case{i}_noise_var"] = grid, H, nv
+        out[f"case{i}_llr"], out[f"case{i}_stats"] = llr, stats
+    np.savez_compressed(os.path.join(OUT, "pusch_demod_general.npz"), **out)
+
+
 def gen_pusch_chest(ref, rng):
     """Reference DM-RS channel estimates (dmrs_pusch_estimator_impl, filter / mean / none smoothing, average time
     strategy) of random single-layer transmissions in 24-PRB grids (DM-RS type 1)."""
@@ -326,7 +343,7 @@ def main():
     if len(sys.argv) > 1:  # regenerate only the named fixture sets, e.g. `python tools/gen_golden.py ofdm`
         for name in sys.argv[1:]:
             seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18, "pdsch_dmrs": 19, "pusch_chest_cfo": 20,
-                    "pdsch_mod_general": 21, "pdsch_dmrs_mask": 22}[name]
+                    "pdsch_mod_general": 21, "pdsch_dmrs_mask": 22, "pusch_demod_general": 23}[name]
             globals()["gen_" + name](ref, np.random.default_rng(seed))
         return
     gen_crc(ref, np.random.default_rng(10))
@@ -342,6 +359,7 @@ def main():
     gen_pusch_chest_cfo(ref, np.random.default_rng(20))
     gen_pdsch_mod_general(ref, np.random.default_rng(21))
     gen_pdsch_dmrs_mask(ref, np.random.default_rng(22))
+    gen_pusch_demod_general(ref, np.random.default_rng(23))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

@@ -520,7 +520,10 @@ typedef struct {
   uint32_t grid_index;                  /* slot (rx grid and channel estimate) of the transmission */
   uint32_t llr_offset;                  /* first codeword LLR in the output buffer */
   uint8_t  numerology;                  /* COMPACT + cfo_compensated: subcarrier spacing of the symbol epochs */
-  uint8_t  pad2[3];
+  uint8_t  transform_precoding;         /* 1: transform precoding (DFT-s-OFDM; one layer, every data symbol's REs a
+                                           multiple of 12 with 2^a 3^b 5^c PRBs, TS 38.211 section 6.3.1.4):
+                                           configuration::enable_transform_precoding, pusch_demodulator_impl.cpp:346 */
+  uint8_t  pad2[2];
 } srsgpu_pusch_demod_config;
 
 typedef struct srsgpu_pusch_demodulator_plan srsgpu_pusch_demodulator_plan;
@@ -546,6 +549,35 @@ int srsgpu_pusch_demodulator_plan_execute(const srsgpu_pusch_demodulator_plan* p
                                           void*                                stream);
 
 void srsgpu_pusch_demodulator_plan_destroy(srsgpu_pusch_demodulator_plan* plan);
+
+/** As srsgpu_pusch_demodulator_plan_create with an optional allocation extension per transmission (exts may be NULL):
+ *  srsgpu_alloc_ext::crb_mask is configuration::rb_mask (any CRB pattern; data REs in symbol-major, ascending-subcarrier
+ *  order, pusch_demodulator_impl.cpp:290); reserved patterns and PRGs are rejected (the demodulator has neither). */
+int srsgpu_pusch_demodulator_plan_create_ex(srsgpu_context*                  ctx,
+                                            const srsgpu_pusch_demod_config* cfgs,
+                                            const srsgpu_alloc_ext*          exts,
+                                            uint32_t                         nof_tx,
+                                            uint32_t                         grid_nof_prb,
+                                            uint32_t                         grid_nof_ports,
+                                            srsgpu_pusch_demodulator_plan**  plan);
+
+/* Post-equalization statistics (pusch_demodulator_notifier::demodulation_stats, pusch_demodulator_impl.cpp:355-443):
+ * SRSGPU_DEMOD_STATS floats per transmission, rows 0..13 = OFDM symbol l (on_provisional_stats) and row 14 = the whole
+ * transmission (on_end_stats), each (SINR dB, EVM): SINR = -10 log10(mean of the finite equalizer noise variances,
+ * after transform deprecoding) or +inf, EVM = sqrt(mean |modulate(hard decisions) - equalized symbol|^2) per symbol
+ * (evm_calculator_generic_impl.cpp), the total EVM weighting each symbol's by its size. NaN rows: no data REs. */
+#define SRSGPU_DEMOD_STATS 30
+
+/** As srsgpu_pusch_demodulator_plan_execute, and when d_stats is not NULL also writes the statistics of every
+ *  transmission (d_stats[SRSGPU_DEMOD_STATS * tx + 2 * row + {0: SINR dB, 1: EVM}]). Asynchronous, hipGraph-capturable
+ *  (the plan's accumulators are reset by the same execute). */
+int srsgpu_pusch_demodulator_plan_execute_ex(const srsgpu_pusch_demodulator_plan* plan,
+                                             const uint32_t*                      d_grids,
+                                             const uint32_t*                      d_ch_estimates,
+                                             const float*                         d_noise_var,
+                                             int8_t*                              d_llrs,
+                                             float*                               d_stats,
+                                             void*                                stream);
 
 /* ------------------------------------------------------------------------------------------------------------------
  * PUSCH decoder (transport-block level) — replaces srsran::pusch_decoder (include/srsran/phy/upper/channel_processors/

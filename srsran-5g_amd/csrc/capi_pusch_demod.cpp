@@ -9,16 +9,40 @@
 using namespace srsgpu;
 
 static_assert(sizeof(srsgpu_pusch_demod_config) == 32, "srsgpu_pusch_demod_config layout (mirrored by srsgpu)");
+static_assert(SRSGPU_DEMOD_STATS == DEMOD_STATS_PER_TX, "statistics row layout");
 
 struct srsgpu_pusch_demodulator_plan {
   srsgpu_context*       ctx        = nullptr;
   demod_desc*           d_desc     = nullptr;
   mod_chunk*            d_chunks   = nullptr;
+  demod_tp_job*         d_tp_jobs  = nullptr;  ///< Transform-precoded (transmission, symbol) work items.
   demap_pair_table*     d_tables   = nullptr;
   uint32_t*             d_seq      = nullptr;  ///< Descrambling sequences of the transmissions (plan lifetime).
+  uint16_t*             d_crbs     = nullptr;  ///< Allocated CRB lists of the CRB-mask transmissions.
+  float*                d_acc      = nullptr;  ///< Statistics accumulators (zero between executes).
   int                   nof_chunks = 0;
+  int                   nof_tp_jobs = 0;
+  int                   nof_tx     = 0;
   std::vector<uint32_t> nof_llrs;
 };
+
+namespace {
+
+/// TS 38.211 section 6.3.1.4: transform precoding needs M_RB = 2^a 3^b 5^c (transform_precoding_helpers.h).
+bool tp_valid_nof_prb(unsigned n)
+{
+  if (n == 0) {
+    return false;
+  }
+  for (unsigned f : {2u, 3u, 5u}) {
+    while (n % f == 0) {
+      n /= f;
+    }
+  }
+  return n == 1;
+}
+
+} // namespace
 
 namespace {
 
@@ -87,6 +111,17 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
                                          uint32_t                         grid_nof_ports,
                                          srsgpu_pusch_demodulator_plan**  plan_out)
 {
+  return srsgpu_pusch_demodulator_plan_create_ex(ctx, cfgs, nullptr, nof_tx, grid_nof_prb, grid_nof_ports, plan_out);
+}
+
+int srsgpu_pusch_demodulator_plan_create_ex(srsgpu_context*                  ctx,
+                                            const srsgpu_pusch_demod_config* cfgs,
+                                            const srsgpu_alloc_ext*          exts,
+                                            uint32_t                         nof_tx,
+                                            uint32_t                         grid_nof_prb,
+                                            uint32_t                         grid_nof_ports,
+                                            srsgpu_pusch_demodulator_plan**  plan_out)
+{
   if (ctx == nullptr || plan_out == nullptr || (cfgs == nullptr && nof_tx > 0)) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
@@ -94,11 +129,28 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
     return fail(SRSGPU_ERR_INVALID_ARG, "invalid grid geometry (%u PRB, %u ports)", grid_nof_prb, grid_nof_ports);
   }
   const uint32_t          nsc = 12u * grid_nof_prb;
-  std::vector<demod_desc> descs(nof_tx);
-  std::vector<mod_chunk>  chunks;
-  std::vector<uint32_t>   nllr(nof_tx);
+  std::vector<demod_desc>   descs(nof_tx);
+  std::vector<mod_chunk>    chunks;
+  std::vector<demod_tp_job> tp_jobs;
+  std::vector<uint16_t>     crb_lists;
+  std::vector<uint32_t>     nllr(nof_tx);
   for (uint32_t t = 0; t < nof_tx; ++t) {
     const srsgpu_pusch_demod_config& c  = cfgs[t];
+    const srsgpu_alloc_ext*          x  = (exts != nullptr) ? &exts[t] : nullptr;
+    if (x != nullptr && (x->nof_reserved > 0 || x->prg_size > 0)) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: the PUSCH demodulator takes a CRB mask only", t);
+    }
+    // Allocated CRBs: the mask's, or the contiguous [rb_start, rb_start + nof_rb).
+    std::vector<uint16_t> crbs;
+    const bool            masked = x != nullptr && x->crb_mask != nullptr;
+    if (masked) {
+      for (uint32_t rb = 0; rb < grid_nof_prb; ++rb) {
+        if (x->crb_mask[rb] != 0) {
+          crbs.push_back(static_cast<uint16_t>(rb));
+        }
+      }
+    }
+    const uint32_t nof_alloc_rb = masked ? static_cast<uint32_t>(crbs.size()) : c.nof_rb;
     const unsigned                   qm = c.modulation_order;
     const unsigned                   L  = c.nof_tx_layers, P = c.nof_rx_ports;
     if (qm != 2 && qm != 4 && qm != 6 && qm != 8) {
@@ -114,8 +166,9 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
     }
     if (c.nof_symbols < 1 || c.start_symbol + c.nof_symbols > 14 || (c.dmrs_type != 1 && c.dmrs_type != 2) ||
         c.nof_cdm_groups_without_data < 1 || c.nof_cdm_groups_without_data > (c.dmrs_type == 1 ? 2 : 3) ||
-        c.n_id > 1023 || c.nof_rb < 1 || c.rb_start + c.nof_rb > grid_nof_prb || c.estimate_layout > SRSGPU_CE_COMPACT ||
-        c.cfo_compensated > 1 || c.numerology > 4) {
+        c.n_id > 1023 || nof_alloc_rb < 1 || (!masked && c.rb_start + c.nof_rb > grid_nof_prb) ||
+        c.estimate_layout > SRSGPU_CE_COMPACT || c.cfo_compensated > 1 || c.numerology > 4 ||
+        c.transform_precoding > 1) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid time / frequency allocation or DM-RS configuration", t);
     }
     demod_desc d{};
@@ -131,7 +184,16 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
     for (unsigned l = 0; l < 14; ++l) {
       d.sym_cum[l] = static_cast<uint16_t>(nre);
       if (l >= c.start_symbol && l < static_cast<unsigned>(c.start_symbol + c.nof_symbols)) {
-        nre += (((c.dmrs_symbol_mask >> l) & 1u) ? nd : 12u) * c.nof_rb;
+        const uint32_t m = (((c.dmrs_symbol_mask >> l) & 1u) ? nd : 12u) * nof_alloc_rb;
+        if (c.transform_precoding && m > 0) {
+          // pusch_demodulator_impl.cpp:347 (one layer), transform_precoder_dft_impl.cpp (M_sc % 12, valid M_RB).
+          if (L != 1 || m % 12 != 0 || !tp_valid_nof_prb(m / 12) || m > 3240) {
+            return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: transform precoding needs one layer and 12 x 2^a 3^b 5^c data "
+                        "REs per symbol (symbol %u has %u)", t, l, m);
+          }
+          tp_jobs.push_back(demod_tp_job{t, l});
+        }
+        nre += m;
       }
     }
     d.sym_cum[14] = d.sym_cum[15] = static_cast<uint16_t>(nre);
@@ -143,11 +205,15 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
     if ((static_cast<uint64_t>(c.grid_index) + 1) * slot_elems * 4u >= (1ull << 32)) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: grid index beyond 32-bit element offsets", t);
     }
-    d.grid_base       = static_cast<uint32_t>(c.grid_index * slot_elems) + c.rb_start * 12u;
+    const uint32_t first_sc = masked ? 0u : c.rb_start * 12u;  // CRB lists address absolute subcarriers
+    d.grid_base       = static_cast<uint32_t>(c.grid_index * slot_elems) + first_sc;
     d.port_stride     = 14u * nsc;
     d.nsc             = nsc;
     d.ce_layer_stride = static_cast<uint32_t>(slot_elems);
-    d.ce_base         = static_cast<uint32_t>(c.grid_index * slot_elems * 4u) + c.rb_start * 12u;
+    d.ce_base         = static_cast<uint32_t>(c.grid_index * slot_elems * 4u) + first_sc;
+    d.crb_list        = masked ? static_cast<uint32_t>(crb_lists.size()) : DEMOD_CONTIGUOUS;
+    crb_lists.insert(crb_lists.end(), crbs.begin(), crbs.end());
+    d.transform_precoding = c.transform_precoding;
     d.ce_compact      = c.estimate_layout == SRSGPU_CE_COMPACT ? 1 : 0;
     if (d.ce_compact) {
       d.ce_base += c.start_symbol * nsc;  // the estimator's single row (srsgpu_pusch_chest_config::estimate_layout)
@@ -167,7 +233,7 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
     d.eq              = (L >= 3 || c.equalizer == SRSGPU_EQ_MMSE) ? DEMOD_EQ_MMSE : DEMOD_EQ_ZF;
     descs[t]          = d;
     nllr[t]           = d.nof_llrs;
-    const uint32_t nwords = (d.nof_llrs + 31) / 32;
+    const uint32_t nwords = c.transform_precoding ? 0u : (d.nof_llrs + 31) / 32;  // TP: per-symbol jobs instead
     for (uint32_t w0 = 0; w0 < nwords; w0 += DEMOD_CHUNK_WORDS) {
       const uint32_t b0 = w0 * 32, b1 = b0 + DEMOD_CHUNK_WORDS * 32;
       mod_chunk      ch{t, w0, (b0 + Lq - 1) / Lq, std::min(nre, (b1 + Lq - 1) / Lq)};
@@ -207,24 +273,43 @@ int srsgpu_pusch_demodulator_plan_create(srsgpu_context*                  ctx,
   for (size_t t = 0; t < descs.size(); ++t) {
     descs[t].seq_word_offset = seq_off[t];
   }
-  auto* plan       = new srsgpu_pusch_demodulator_plan();
-  plan->ctx        = ctx;
-  plan->nof_chunks = static_cast<int>(chunks.size());
-  plan->nof_llrs   = std::move(nllr);
-  if (!chunks.empty() && build_gold_sequences(ctx, c_inits, nwords, seq_off, &plan->d_seq) != SRSGPU_OK) {
+  auto* plan        = new srsgpu_pusch_demodulator_plan();
+  plan->ctx         = ctx;
+  plan->nof_chunks  = static_cast<int>(chunks.size());
+  plan->nof_tp_jobs = static_cast<int>(tp_jobs.size());
+  plan->nof_tx      = static_cast<int>(nof_tx);
+  plan->nof_llrs    = std::move(nllr);
+  const bool work   = !chunks.empty() || !tp_jobs.empty();
+  if (work && build_gold_sequences(ctx, c_inits, nwords, seq_off, &plan->d_seq) != SRSGPU_OK) {
     srsgpu_pusch_demodulator_plan_destroy(plan);
     return SRSGPU_ERR_HIP;
   }
   bool ok = hipMalloc(&plan->d_tables, tables.size() * sizeof(demap_pair_table)) == hipSuccess &&
             hipMemcpy(plan->d_tables, tables.data(), tables.size() * sizeof(demap_pair_table),
                       hipMemcpyHostToDevice) == hipSuccess;
-  if (ok && !chunks.empty()) {
+  if (ok && work) {
     ok = hipMalloc(&plan->d_desc, descs.size() * sizeof(demod_desc)) == hipSuccess &&
          hipMemcpy(plan->d_desc, descs.data(), descs.size() * sizeof(demod_desc), hipMemcpyHostToDevice) ==
-             hipSuccess &&
-         hipMalloc(&plan->d_chunks, chunks.size() * sizeof(mod_chunk)) == hipSuccess &&
+             hipSuccess;
+  }
+  if (ok && !chunks.empty()) {
+    ok = hipMalloc(&plan->d_chunks, chunks.size() * sizeof(mod_chunk)) == hipSuccess &&
          hipMemcpy(plan->d_chunks, chunks.data(), chunks.size() * sizeof(mod_chunk), hipMemcpyHostToDevice) ==
              hipSuccess;
+  }
+  if (ok && !tp_jobs.empty()) {
+    ok = hipMalloc(&plan->d_tp_jobs, tp_jobs.size() * sizeof(demod_tp_job)) == hipSuccess &&
+         hipMemcpy(plan->d_tp_jobs, tp_jobs.data(), tp_jobs.size() * sizeof(demod_tp_job), hipMemcpyHostToDevice) ==
+             hipSuccess;
+  }
+  if (ok && !crb_lists.empty()) {
+    ok = hipMalloc(&plan->d_crbs, crb_lists.size() * sizeof(uint16_t)) == hipSuccess &&
+         hipMemcpy(plan->d_crbs, crb_lists.data(), crb_lists.size() * sizeof(uint16_t), hipMemcpyHostToDevice) ==
+             hipSuccess;
+  }
+  if (ok && nof_tx > 0) {
+    const size_t acc_bytes = static_cast<size_t>(nof_tx) * DEMOD_ACC_PER_TX * sizeof(float);
+    ok = hipMalloc(&plan->d_acc, acc_bytes) == hipSuccess && hipMemset(plan->d_acc, 0, acc_bytes) == hipSuccess;
   }
   if (!ok) {
     srsgpu_pusch_demodulator_plan_destroy(plan);
@@ -250,8 +335,30 @@ int srsgpu_pusch_demodulator_plan_execute(const srsgpu_pusch_demodulator_plan* p
       d_llrs == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
+  return srsgpu_pusch_demodulator_plan_execute_ex(plan, d_grids, d_ch_estimates, d_noise_var, d_llrs, nullptr, stream);
+}
+
+int srsgpu_pusch_demodulator_plan_execute_ex(const srsgpu_pusch_demodulator_plan* plan,
+                                             const uint32_t*                      d_grids,
+                                             const uint32_t*                      d_ch_estimates,
+                                             const float*                         d_noise_var,
+                                             int8_t*                              d_llrs,
+                                             float*                               d_stats,
+                                             void*                                stream)
+{
+  if (plan == nullptr || d_grids == nullptr || d_ch_estimates == nullptr || d_noise_var == nullptr ||
+      d_llrs == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  const hipStream_t s   = static_cast<hipStream_t>(stream);
+  float*            acc = d_stats != nullptr ? plan->d_acc : nullptr;
   launch_pusch_demodulate(plan->d_desc, plan->d_chunks, plan->nof_chunks, plan->d_tables, d_grids, d_ch_estimates,
-                          d_noise_var, d_llrs, plan->d_seq, static_cast<hipStream_t>(stream));
+                          d_noise_var, d_llrs, plan->d_seq, plan->d_crbs, acc, s);
+  launch_pusch_demodulate_tp(plan->d_desc, plan->d_tp_jobs, plan->nof_tp_jobs, plan->d_tables, d_grids,
+                             d_ch_estimates, d_noise_var, d_llrs, plan->d_seq, plan->d_crbs, acc, s);
+  if (d_stats != nullptr) {
+    launch_pusch_demod_stats(plan->d_acc, d_stats, plan->nof_tx, s);
+  }
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
 }
@@ -262,7 +369,8 @@ void srsgpu_pusch_demodulator_plan_destroy(srsgpu_pusch_demodulator_plan* plan)
     return;
   }
   for (void* p : {static_cast<void*>(plan->d_desc), static_cast<void*>(plan->d_chunks),
-                  static_cast<void*>(plan->d_tables), static_cast<void*>(plan->d_seq)}) {
+                  static_cast<void*>(plan->d_tp_jobs), static_cast<void*>(plan->d_tables),
+                  static_cast<void*>(plan->d_seq), static_cast<void*>(plan->d_crbs), static_cast<void*>(plan->d_acc)}) {
     if (p != nullptr) {
       (void)hipFree(p);
     }

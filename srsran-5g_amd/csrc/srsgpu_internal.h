@@ -323,8 +323,24 @@ struct demod_desc {
   uint32_t ce_cfo;          ///< Compact layout with CFO compensation: rotate each symbol's estimates (CFO word at
                             ///< ce_base + nsc of every (layer, port)).
   float    epochs[14];      ///< Symbol start epochs (symbol durations) for the rotation.
+  uint32_t crb_list;        ///< CRB-mask allocation: first entry of the transmission's allocated CRBs (ascending) in the
+                            ///< plan's CRB list, grid_base / ce_base then exclude the first subcarrier; DEMOD_CONTIGUOUS
+                            ///< for the contiguous allocation.
+  uint32_t transform_precoding;  ///< Transform-precoded: the demodulate_tp kernel handles the transmission.
 };
-static_assert(sizeof(demod_desc) == 152, "demod_desc layout");
+static_assert(sizeof(demod_desc) == 160, "demod_desc layout");
+constexpr uint32_t DEMOD_CONTIGUOUS = 0xffffffffu;
+
+/// Transform-precoded PUSCH work item: one OFDM symbol of one transmission (M data REs, the inverse DFT length).
+struct demod_tp_job {
+  uint32_t tx;
+  uint32_t symbol;
+};
+/// Post-equalization statistics accumulators per transmission and OFDM symbol: (sum of finite noise variances, their
+/// count, sum of squared EVM errors, equalized symbols).
+constexpr int DEMOD_ACC_PER_TX = 14 * 4;
+/// Statistics floats per transmission (SRSGPU_DEMOD_STATS of the C ABI): 15 rows x (SINR dB, EVM).
+constexpr int DEMOD_STATS_PER_TX = 30;
 
 /// demod_desc::eq: the reference's ZF paths (1 layer: 1 x N with port reduction; 2 layers: 2 x N) or linear MMSE.
 constexpr uint8_t DEMOD_EQ_ZF   = 0;
@@ -436,6 +452,19 @@ void launch_pusch_chest(const chest_job* d_jobs,
                         const uint32_t*  d_seq,
                         hipStream_t      stream);
 
+void launch_pusch_demodulate_tp(const demod_desc*       d_desc,
+                                const demod_tp_job*      d_jobs,
+                                int                      nof_jobs,
+                                const demap_pair_table*  d_tables,
+                                const uint32_t*          d_grids,
+                                const uint32_t*          d_ch_est,
+                                const float*             d_noise_var,
+                                int8_t*                  d_llrs,
+                                const uint32_t*          d_seq,
+                                const uint16_t*          d_crbs,
+                                float*                   d_acc,
+                                hipStream_t              stream);
+void launch_pusch_demod_stats(float* d_acc, float* d_stats, int nof_tx, hipStream_t stream);
 void launch_pusch_demodulate(const demod_desc*        d_desc,
                              const mod_chunk*         d_chunks,
                              int                      nof_chunks,
@@ -445,6 +474,8 @@ void launch_pusch_demodulate(const demod_desc*        d_desc,
                              const float*             d_noise_var,
                              int8_t*                  d_llrs,
                              const uint32_t*          d_seq,
+                             const uint16_t*          d_crbs,
+                             float*                   d_acc,
                              hipStream_t              stream);
 
 } // namespace srsgpu

@@ -212,11 +212,13 @@ class PuschDemodConfig(ctypes.Structure):
         ("grid_index", ctypes.c_uint32),
         ("llr_offset", ctypes.c_uint32),
         ("numerology", ctypes.c_uint8),
-        ("pad2", ctypes.c_uint8 * 3),
+        ("transform_precoding", ctypes.c_uint8),
+        ("pad2", ctypes.c_uint8 * 2),
     ]
 
 
 assert ctypes.sizeof(PuschDemodConfig) == 32
+DEMOD_STATS = 30  # SRSGPU_DEMOD_STATS: 15 rows (symbols 0..13, then the transmission) x (SINR dB, EVM)
 
 
 class PuschChestConfig(ctypes.Structure):
@@ -319,6 +321,9 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pdsch_dmrs_plan_create_ex.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                      ctypes.POINTER(P)]
     lib.srsgpu_pdsch_dmrs_plan_execute.argtypes = [P, P, P]
+    lib.srsgpu_pusch_demodulator_plan_create_ex.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                            ctypes.POINTER(P)]
+    lib.srsgpu_pusch_demodulator_plan_execute_ex.argtypes = [P, P, P, P, P, P, P]
     lib.srsgpu_pdsch_dmrs_plan_destroy.argtypes = [P]
     lib.srsgpu_pdsch_dmrs_plan_destroy.restype = None
     lib.srsgpu_pusch_chest_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -367,6 +372,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
+    "srsgpu_pusch_demodulator_plan_create_ex", "srsgpu_pusch_demodulator_plan_execute_ex",
     "srsgpu_pusch_chest_plan_create", "srsgpu_pusch_chest_plan_execute", "srsgpu_pusch_chest_plan_destroy",
     "srsgpu_pdsch_dmrs_plan_create", "srsgpu_pdsch_dmrs_plan_create_ex", "srsgpu_pdsch_dmrs_plan_execute", "srsgpu_pdsch_dmrs_plan_destroy",
 ]
@@ -928,8 +934,9 @@ class PdschDmrs:
         return self.crb_mask is not None
 
 
-def make_dmrs_exts(dmrs, grid_nof_prb: int):
-    """srsgpu_alloc_ext array for PDSCH DM-RS CRB masks (None when every allocation is contiguous) + keep-alive list."""
+def make_crb_mask_exts(dmrs, grid_nof_prb: int):
+    """srsgpu_alloc_ext array carrying CRB masks only (PDSCH DM-RS, PUSCH demodulator / estimator: objects with a
+    `crb_mask`; None when every allocation is contiguous) + keep-alive list."""
     if not any(d.crb_mask is not None for d in dmrs):
         return None, []
     exts = (AllocExtC * len(dmrs))()
@@ -942,6 +949,9 @@ def make_dmrs_exts(dmrs, grid_nof_prb: int):
             keep.append(c)
             exts[i].crb_mask = c.ctypes.data
     return exts, keep
+
+
+make_dmrs_exts = make_crb_mask_exts
 
 
 def make_pdsch_dmrs_configs(dmrs: Sequence[PdschDmrs], grid_index: Sequence[int]):
@@ -993,8 +1003,9 @@ class PdschDmrsPlan:
 
 @dataclass
 class PuschDemodulation:
-    """pusch_demodulator::configuration (pusch_demodulator.h:51) of one transmission with a contiguous CRB allocation
-    and rx ports 0..nof_rx_ports-1."""
+    """pusch_demodulator::configuration (pusch_demodulator.h:51) of one transmission, rx ports 0..nof_rx_ports-1: a
+    contiguous CRB allocation [rb_start, rb_start + nof_rb) or `crb_mask` (rb_mask, one byte per grid CRB), and
+    optionally transform precoding (enable_transform_precoding, one layer)."""
     rnti: int
     n_id: int
     modulation_order: int
@@ -1011,10 +1022,13 @@ class PuschDemodulation:
     estimate_layout: int = CE_PER_SYMBOL
     cfo_compensated: int = 0  # compact layout written with CFO compensation (the estimator's compensate_cfo)
     numerology: int = 1
+    crb_mask: Optional[np.ndarray] = None
+    transform_precoding: int = 0
 
     def nof_llrs(self) -> int:
         dm = (4 if self.dmrs_type == 2 else 6) * self.nof_cdm_groups_without_data
-        nre = sum((12 - dm if (self.dmrs_symbol_mask >> l) & 1 else 12) * self.nof_rb
+        nrb = int(np.count_nonzero(self.crb_mask)) if self.crb_mask is not None else self.nof_rb
+        nre = sum((12 - dm if (self.dmrs_symbol_mask >> l) & 1 else 12) * nrb
                   for l in range(self.start_symbol, self.start_symbol + self.nof_symbols))
         return nre * self.nof_tx_layers * self.modulation_order
 
@@ -1032,6 +1046,7 @@ def make_pusch_demod_configs(demods: Sequence[PuschDemodulation], grid_index: Se
         a.dmrs_symbol_mask, a.rb_start, a.nof_rb, a.grid_index = m.dmrs_symbol_mask, m.rb_start, m.nof_rb, g
         a.estimate_layout = m.estimate_layout
         a.cfo_compensated, a.numerology = m.cfo_compensated, m.numerology
+        a.transform_precoding = m.transform_precoding
         a.llr_offset = off if llr_offsets is None else llr_offsets[i]
         offs.append(a.llr_offset)
         off += m.nof_llrs()
@@ -1043,21 +1058,33 @@ class PuschDemodulatorPlan:
     from rx grids (nslots, ports, 14, nsc) and channel estimates (nslots, 4 layers, ports, 14, nsc) (uint32 bf16 pairs)
     and noise variances (ntx, 4) float32 into int8 codeword LLRs."""
 
-    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4):
+    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4, exts=None):
         self.ctx = ctx
         h = ctypes.c_void_p()
-        _check(_lib.srsgpu_pusch_demodulator_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
-                                                         len(cfg_array), grid_nof_prb, grid_nof_ports,
-                                                         ctypes.byref(h)))
+        if exts is None:
+            _check(_lib.srsgpu_pusch_demodulator_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                             len(cfg_array), grid_nof_prb, grid_nof_ports,
+                                                             ctypes.byref(h)))
+        else:
+            _check(_lib.srsgpu_pusch_demodulator_plan_create_ex(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                                ctypes.cast(exts, ctypes.c_void_p), len(cfg_array),
+                                                                grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
         self.handle = h
         self.nof_tx = len(cfg_array)
 
     def nof_llrs(self, tx: int) -> int:
         return int(_lib.srsgpu_pusch_demodulator_plan_nof_llrs(self.handle, tx))
 
-    def execute(self, d_grids, d_ch_est, d_noise_var, d_llrs, stream=None):
-        _check(_lib.srsgpu_pusch_demodulator_plan_execute(self.handle, _dptr(d_grids), _dptr(d_ch_est),
-                                                          _dptr(d_noise_var), _dptr(d_llrs), _stream_handle(stream)))
+    def execute(self, d_grids, d_ch_est, d_noise_var, d_llrs, stream=None, d_stats=None):
+        """d_stats: optional float32 device buffer of DEMOD_STATS floats per transmission (SINR dB / EVM rows)."""
+        if d_stats is None:
+            _check(_lib.srsgpu_pusch_demodulator_plan_execute(self.handle, _dptr(d_grids), _dptr(d_ch_est),
+                                                              _dptr(d_noise_var), _dptr(d_llrs),
+                                                              _stream_handle(stream)))
+        else:
+            _check(_lib.srsgpu_pusch_demodulator_plan_execute_ex(self.handle, _dptr(d_grids), _dptr(d_ch_est),
+                                                                 _dptr(d_noise_var), _dptr(d_llrs), _dptr(d_stats),
+                                                                 _stream_handle(stream)))
 
     def close(self):
         if getattr(self, "handle", None):
@@ -1080,21 +1107,28 @@ class PuschDemodulator:
         self.ctx, self.grid_nof_prb, self.grid_nof_ports = ctx, grid_nof_prb, grid_nof_ports
 
     def demodulate_batch(self, grids_u16, ch_est_u16, noise_vars, demods: Sequence[PuschDemodulation],
-                         grid_index: Sequence[int]):
-        """grids_u16 (S, Pg, 14, nsc, 2); ch_est_u16 (S, 4, Pg, 14, nsc, 2); noise_vars (ntx, 4)."""
+                         grid_index: Sequence[int], with_stats: bool = False):
+        """grids_u16 (S, Pg, 14, nsc, 2); ch_est_u16 (S, 4, Pg, 14, nsc, 2); noise_vars (ntx, 4). Returns the LLRs of
+        each transmission and, with_stats, also the (ntx, 15, 2) statistics (SINR dB, EVM per symbol / total)."""
         dev = torch.device("cuda", self.ctx.device)
         arr, offs, total = make_pusch_demod_configs(demods, grid_index)
-        plan = PuschDemodulatorPlan(self.ctx, arr, self.grid_nof_prb, self.grid_nof_ports)
+        exts, _keep = make_crb_mask_exts(demods, self.grid_nof_prb)
+        plan = PuschDemodulatorPlan(self.ctx, arr, self.grid_nof_prb, self.grid_nof_ports, exts)
         g = torch.from_numpy(np.ascontiguousarray(grids_u16, np.uint16).view(np.int32).reshape(-1).copy()).to(dev)
         h = torch.from_numpy(np.ascontiguousarray(ch_est_u16, np.uint16).view(np.int32).reshape(-1).copy()).to(dev)
         nv = torch.from_numpy(np.ascontiguousarray(noise_vars, np.float32).reshape(-1).copy()).to(dev)
         out = torch.full((max(total, 4),), 77, dtype=torch.int8, device=dev)
-        plan.execute(g, h, nv, out)
+        st = torch.full((max(len(demods), 1) * DEMOD_STATS,), 55.0, dtype=torch.float32, device=dev) \
+            if with_stats else None
+        plan.execute(g, h, nv, out, d_stats=st)
         torch.cuda.synchronize(dev)
         n = [plan.nof_llrs(i) for i in range(len(demods))]
         plan.close()
         o = out.cpu().numpy()
-        return [o[a:a + k] for a, k in zip(offs, n)]
+        llrs = [o[a:a + k] for a, k in zip(offs, n)]
+        if not with_stats:
+            return llrs
+        return llrs, st.cpu().numpy()[:len(demods) * DEMOD_STATS].reshape(len(demods), 15, 2)
 
 
 @dataclass

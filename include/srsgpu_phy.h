@@ -486,6 +486,20 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
                                    uint32_t                         grid_nof_ports,
                                    srsgpu_pusch_chest_plan**        plan);
 
+/** As srsgpu_pusch_chest_plan_create with an optional allocation extension per transmission (exts may be NULL):
+ *  srsgpu_alloc_ext::crb_mask is configuration::rb_mask. The pilots of the allocated CRBs (the sequence skipping the
+ *  unallocated ones, dmrs_helper.cpp:64) are smoothed and interpolated as one band, the time alignment takes the RE-mask
+ *  path (port_channel_estimator_helpers.cpp:285), and PRB i of the band is written at the i-th allocated CRB. (The
+ *  reference writes every PRB of a non-contiguous mask at the lowest CRB instead, port_channel_estimator_average_impl.cpp:
+ *  297: DESIGN.md.) Reserved patterns and PRGs are rejected. */
+int srsgpu_pusch_chest_plan_create_ex(srsgpu_context*                  ctx,
+                                      const srsgpu_pusch_chest_config* cfgs,
+                                      const srsgpu_alloc_ext*          exts,
+                                      uint32_t                         nof_tx,
+                                      uint32_t                         grid_nof_prb,
+                                      uint32_t                         grid_nof_ports,
+                                      srsgpu_pusch_chest_plan**        plan);
+
 /** Estimates every planned transmission: reads d_grids, writes d_ch_estimates (slot layout [layer 0..3][port]
  *  [symbol][subcarrier], only the allocated REs), d_noise_var and optionally d_metrics (SRSGPU_CHEST_METRICS floats
  *  per transmission and port). Asynchronous on `stream`. */

@@ -53,15 +53,17 @@ def layer0_pattern(dmrs_type2):
     return [0, 1, 6, 7] if dmrs_type2 else [0, 2, 4, 6, 8, 10]
 
 
-def dmrs_sequence(slot, symbol, scrambling_id, n_scid, dmrs_type2, rb_start, nof_rb):
-    """DM-RS symbols of the allocated RBs of one OFDM symbol (QPSK, amplitude 1/sqrt(2))."""
+def dmrs_sequence(slot, symbol, scrambling_id, n_scid, dmrs_type2, rb_start, nof_rb, rbs=None):
+    """DM-RS symbols of the allocated RBs of one OFDM symbol (QPSK, amplitude 1/sqrt(2)): the contiguous
+    [rb_start, rb_start + nof_rb), or the CRB list `rbs` (dmrs_sequence_generate skips the unallocated CRBs,
+    dmrs_helper.cpp:64; reference point A, dmrs_pusch_estimator_impl.cpp:103)."""
     c_init = ((14 * slot + symbol + 1) * (2 * scrambling_id + 1) * (1 << 17) + 2 * scrambling_id + n_scid) % (1 << 31)
     per_rb = 4 if dmrs_type2 else 6
-    m0 = rb_start * per_rb
-    n = nof_rb * per_rb
-    c = D.gold_sequence(c_init, 2 * (m0 + n)).astype(np.float64)
+    rbs = list(range(rb_start, rb_start + nof_rb)) if rbs is None else list(rbs)
+    m = np.array([rb * per_rb + j for rb in rbs for j in range(per_rb)])
+    c = D.gold_sequence(c_init, 2 * (int(m.max()) + 1)).astype(np.float64)
     a = 1 / np.sqrt(2)
-    return ((1 - 2 * c[2 * m0::2]) * a + 1j * (1 - 2 * c[2 * m0 + 1::2]) * a)[:n]
+    return (1 - 2 * c[2 * m]) * a + 1j * (1 - 2 * c[2 * m + 1]) * a
 
 
 def virtual_pilots(base, is_start):
@@ -217,7 +219,7 @@ def td_interpolate(planes, dmrs_syms, first, last, l):
     return planes[i] + (planes[i + 1] - planes[i]) * w
 
 
-def estimate(cfg, grid, fd="filter", td="average", compensate_cfo=False, numerology=1):
+def estimate(cfg, grid, fd="filter", td="average", compensate_cfo=False, numerology=1, crb_mask=None):
     """cfg: slot, scrambling_id, n_scid, dmrs_type2, scaling (beta), dmrs_symbol_mask, start_symbol, nof_symbols,
     rb_start, nof_rb, nof_rx_ports. grid (P, 14, nsc) complex. Returns (ch (P, 14, nsc) complex128 filled on the
     allocation, noise_var (P,), rsrp (P,), epre (P,), extra) with extra = dict(cfo_hz (P,) NaN when one DM-RS symbol,
@@ -226,19 +228,29 @@ def estimate(cfg, grid, fd="filter", td="average", compensate_cfo=False, numerol
     CFO (preprocess_pilots_and_estimate_cfo, port_channel_estimator_average_impl.cpp:322): phase of
     sum lse_1 conj(lse_0) over the time between the first two DM-RS symbols' starts; with compensate_cfo every DM-RS
     symbol's LSE is derotated by its start epoch before combining, the noise residual re-rotates the prediction (:475)
-    and every symbol's estimate is rotated by its epoch (:128)."""
+    and every symbol's estimate is rotated by its epoch (:128).
+
+    crb_mask (rb_mask, one byte per grid CRB) replaces the contiguous allocation: the pilots of the allocated CRBs are
+    concatenated, smoothed and interpolated as one band (compute_hop :245-275, the filter sized by the CRB count), the
+    time alignment takes the RE-mask path (pilots at their subcarrier offsets, port_channel_estimator_helpers.cpp:285),
+    and PRB i of the interpolated band is the estimate of the i-th allocated CRB. (The reference writes every PRB of a
+    non-contiguous mask at the lowest CRB instead, :297 -- a defect: tests/test_oracle_vs_reference.py pins the
+    restatement against what it does write.)"""
     P = cfg["nof_rx_ports"]
     t2 = cfg["dmrs_type2"]
     beta = cfg["scaling"]
     pat = layer0_pattern(t2)
     offset, stride = pat[0], pat[1] - pat[0]
     rb0, nrb = cfg["rb_start"], cfg["nof_rb"]
-    sc = np.array([(rb0 + rb) * 12 + k for rb in range(nrb) for k in pat])
+    rbs = list(range(rb0, rb0 + nrb)) if crb_mask is None else [int(i) for i in np.flatnonzero(crb_mask)]
+    contiguous = rbs[-1] - rbs[0] + 1 == len(rbs)
+    nrb = len(rbs)
+    sc = np.array([rb * 12 + k for rb in rbs for k in pat])
     first, last = cfg["start_symbol"], cfg["start_symbol"] + cfg["nof_symbols"]
     syms = [l for l in range(first, last) if (cfg["dmrs_symbol_mask"] >> l) & 1]
     Dn = len(syms)
     N = sc.size
-    pil = [dmrs_sequence(cfg["slot"], l, cfg["scrambling_id"], cfg["n_scid"], t2, rb0, nrb) for l in syms]
+    pil = [dmrs_sequence(cfg["slot"], l, cfg["scrambling_id"], cfg["n_scid"], t2, rb0, nrb, rbs) for l in syms]
     ep = symbol_start_epochs(numerology)
     scs_hz = (15 << numerology) * 1000.0
     nsc = grid.shape[2]
@@ -268,11 +280,12 @@ def estimate(cfg, grid, fd="filter", td="average", compensate_cfo=False, numerol
                 pred = pred * np.exp(2j * np.pi * ep[l] * cfo)
             noise += np.sum(np.abs(r - pred) ** 2)
         nvar[p] = max(rsrp[p] / 1e10, noise / (N * Dn - 1))
-        ta_s[p] = estimate_ta(planes, sc, numerology, stride)
+        ta_s[p] = estimate_ta(planes, sc, numerology, stride if contiguous else 1)
         frs = [interpolate(f, offset, stride, nrb * 12) for f in planes]
         for l in range(first, last):
             fr = frs[0] if td == "average" else td_interpolate(frs, syms, first, last, l)
             if compensate_cfo and cfo is not None:
                 fr = fr * np.exp(2j * np.pi * ep[l] * cfo)
-            ch[p, l, rb0 * 12: (rb0 + nrb) * 12] = fr
+            for i, rb in enumerate(rbs):
+                ch[p, l, rb * 12: (rb + 1) * 12] = fr[i * 12: (i + 1) * 12]
     return ch, nvar, rsrp, epre, dict(cfo_hz=cfo_hz, ta_s=ta_s, cfo_phase=cfo_ph)

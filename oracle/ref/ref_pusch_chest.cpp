@@ -23,12 +23,12 @@ using namespace srsran;
 
 extern "C" {
 
-/// DM-RS based channel estimation of one single-layer PUSCH transmission (pseudo-random DM-RS sequence, contiguous CRB
-/// allocation [rb_start, rb_start + nof_rb)) on every rx port of a (nof_rx_ports x 14 x 12 * grid_nof_prb) bf16 grid.
+/// DM-RS based channel estimation of one single-layer PUSCH transmission (pseudo-random DM-RS sequence, CRB allocation
+/// crb_mask (one byte per grid CRB) or, when NULL, the contiguous [rb_start, rb_start + nof_rb)) on every rx port of a (nof_rx_ports x 14 x 12 * grid_nof_prb) bf16 grid.
 /// fd_strategy: 0 none, 1 mean, 2 filter; td_strategy: 0 average, 1 interpolate. Outputs: ch_est
 /// [port][14][12 * grid_nof_prb] bf16 pairs, and per port noise variance, RSRP, EPRE, time alignment (s), CFO (Hz or
 /// NaN).
-int ref_pusch_chest(int             numerology,
+int ref_pusch_chest_mask(int             numerology,
                     int             slot_index,
                     int             scrambling_id,
                     int             n_scid,
@@ -40,6 +40,7 @@ int ref_pusch_chest(int             numerology,
                     int             nof_symbols,
                     int             rb_start,
                     int             nof_rb,
+                    const uint8_t*  crb_mask,
                     int             grid_nof_prb,
                     int             nof_rx_ports,
                     int             fd_strategy,
@@ -102,7 +103,13 @@ int ref_pusch_chest(int             numerology,
     cfg.symbols_mask.set(l, ((dmrs_symbol_mask >> l) & 1U) != 0);
   }
   cfg.rb_mask = crb_bitmap(grid_nof_prb);
-  cfg.rb_mask.fill(rb_start, rb_start + nof_rb);
+  if (crb_mask != nullptr) {
+    for (int rb = 0; rb < grid_nof_prb; ++rb) {
+      cfg.rb_mask.set(rb, crb_mask[rb] != 0);
+    }
+  } else {
+    cfg.rb_mask.fill(rb_start, rb_start + nof_rb);
+  }
   cfg.first_symbol = first_symbol;
   cfg.nof_symbols  = nof_symbols;
   for (int p = 0; p < nof_rx_ports; ++p) {
@@ -110,6 +117,10 @@ int ref_pusch_chest(int             numerology,
   }
   channel_estimate ce({static_cast<unsigned>(grid_nof_prb), 14, static_cast<unsigned>(nof_rx_ports),
                        static_cast<unsigned>(nof_layers)});
+  for (int p = 0; p < nof_rx_ports; ++p) {
+    span<cbf16_t> path = ce.get_path_ch_estimate(p, 0);
+    std::fill(path.begin(), path.end(), cbf16_t());
+  }
   est.estimate(ce, grid.get_reader(), cfg);
   for (int p = 0; p < nof_rx_ports; ++p) {
     span<const cbf16_t> path = ce.get_path_ch_estimate(p, 0);
@@ -126,6 +137,37 @@ int ref_pusch_chest(int             numerology,
     cfo_hz[p]                   = cfo.has_value() ? *cfo : std::numeric_limits<float>::quiet_NaN();
   }
   return 0;
+}
+
+int ref_pusch_chest(int             numerology,
+                    int             slot_index,
+                    int             scrambling_id,
+                    int             n_scid,
+                    int             dmrs_type2,
+                    int             nof_layers,
+                    float           scaling,
+                    unsigned        dmrs_symbol_mask,
+                    int             first_symbol,
+                    int             nof_symbols,
+                    int             rb_start,
+                    int             nof_rb,
+                    int             grid_nof_prb,
+                    int             nof_rx_ports,
+                    int             fd_strategy,
+                    int             td_strategy,
+                    int             compensate_cfo,
+                    const uint16_t* grid_in,
+                    uint16_t*       ch_est_out,
+                    float*          noise_var,
+                    float*          rsrp,
+                    float*          epre,
+                    float*          ta_s,
+                    float*          cfo_hz)
+{
+  return ref_pusch_chest_mask(numerology, slot_index, scrambling_id, n_scid, dmrs_type2, nof_layers, scaling,
+                              dmrs_symbol_mask, first_symbol, nof_symbols, rb_start, nof_rb, nullptr, grid_nof_prb,
+                              nof_rx_ports, fd_strategy, td_strategy, compensate_cfo, grid_in, ch_est_out, noise_var,
+                              rsrp, epre, ta_s, cfo_hz);
 }
 
 } // extern "C"

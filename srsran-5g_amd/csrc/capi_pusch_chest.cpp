@@ -17,6 +17,7 @@ struct srsgpu_pusch_chest_plan {
   int             nof_jobs   = 0;
   chest_geom      geom       = {};  ///< Plan-wide maxima (LDS sizing).
   uint32_t*       d_seq      = nullptr;  ///< DM-RS sequence words of every job (plan lifetime).
+  uint16_t*       d_crbs     = nullptr;  ///< CRB lists of the CRB-mask transmissions (relative to their first CRB).
 };
 
 namespace {
@@ -58,6 +59,17 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
                                    uint32_t                         grid_nof_ports,
                                    srsgpu_pusch_chest_plan**        plan_out)
 {
+  return srsgpu_pusch_chest_plan_create_ex(ctx, cfgs, nullptr, nof_tx, grid_nof_prb, grid_nof_ports, plan_out);
+}
+
+int srsgpu_pusch_chest_plan_create_ex(srsgpu_context*                  ctx,
+                                      const srsgpu_pusch_chest_config* cfgs,
+                                      const srsgpu_alloc_ext*          exts,
+                                      uint32_t                         nof_tx,
+                                      uint32_t                         grid_nof_prb,
+                                      uint32_t                         grid_nof_ports,
+                                      srsgpu_pusch_chest_plan**        plan_out)
+{
   if (ctx == nullptr || plan_out == nullptr || (cfgs == nullptr && nof_tx > 0)) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
@@ -67,9 +79,37 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
   const uint32_t         nsc        = 12u * grid_nof_prb;
   const uint64_t         slot_elems = static_cast<uint64_t>(grid_nof_ports) * 14u * nsc;
   std::vector<chest_job> jobs;
+  std::vector<uint16_t>  crb_lists;
   for (uint32_t t = 0; t < nof_tx; ++t) {
-    const srsgpu_pusch_chest_config& c = cfgs[t];
-    const unsigned                   L = c.nof_tx_layers, P = c.nof_rx_ports;
+    srsgpu_pusch_chest_config c = cfgs[t];
+    const unsigned            L = c.nof_tx_layers, P = c.nof_rx_ports;
+    const srsgpu_alloc_ext*   x = (exts != nullptr) ? &exts[t] : nullptr;
+    if (x != nullptr && (x->nof_reserved > 0 || x->prg_size > 0)) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: the PUSCH estimator takes a CRB mask only", t);
+    }
+    // CRB mask (configuration::rb_mask): a contiguous mask is the plain allocation; otherwise the allocated CRBs
+    // relative to the first one drive the pilot, sequence and estimate positions.
+    std::vector<uint16_t> rel;
+    if (x != nullptr && x->crb_mask != nullptr) {
+      std::vector<uint16_t> crbs;
+      for (uint32_t rb = 0; rb < grid_nof_prb; ++rb) {
+        if (x->crb_mask[rb] != 0) {
+          crbs.push_back(static_cast<uint16_t>(rb));
+        }
+      }
+      if (crbs.empty()) {
+        return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: empty CRB mask", t);
+      }
+      c.rb_start = crbs.front();
+      c.nof_rb   = static_cast<uint16_t>(crbs.size());
+      if (crbs.back() - crbs.front() + 1u != crbs.size()) {
+        for (uint16_t rb : crbs) {
+          rel.push_back(static_cast<uint16_t>(rb - crbs.front()));
+        }
+      }
+    }
+    const bool     masked  = !rel.empty();
+    const unsigned span_rb = masked ? rel.back() + 1u : c.nof_rb;
     if (L < 1 || L > 4 || P < 1 || P > grid_nof_ports || (c.dmrs_type != 1 && c.dmrs_type != 2) || c.n_scid > 1) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid layers / ports / DM-RS type", t);
     }
@@ -165,10 +205,11 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
     }
     // Time alignment (estimate_time_alignment, port_channel_estimator_helpers.cpp:246): type 1 patterns are the stride-2
     // PUSCH patterns (pilots in the first bins); others take the RE-mask path (pilots at their subcarrier offsets).
+    // A non-contiguous mask takes the RE-mask path for both types (pilot span of the re_mask = rb_mask kron pattern).
     const unsigned khz      = 15u << c.numerology;
-    const unsigned ta_re    = t2 ? (c.nof_rb - 1u) * 12u + 7u + 1u : c.nof_rb * per_rb;
+    const unsigned ta_re    = (t2 || masked) ? (span_rb - 1u) * 12u + (t2 ? 7u : 10u) + 1u : c.nof_rb * per_rb;
     const unsigned ta_dft   = ta_dft_size(ta_re);
-    const unsigned ta_strd  = t2 ? 1u : 2u;
+    const unsigned ta_strd  = (t2 || masked) ? 1u : 2u;
     const double   ta_fs    = static_cast<double>(static_cast<uint64_t>(ta_dft) * khz * 1000u * ta_strd);
     const double   half_cp  = static_cast<double>(144u * 64u / (1u << (c.numerology + 1))) * T_C;
     const unsigned ta_max   = static_cast<unsigned>(std::floor(half_cp * ta_fs));
@@ -226,10 +267,13 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
         jb.ta_dft       = static_cast<uint16_t>(ta_dft);
         jb.ta_max       = static_cast<uint16_t>(ta_max);
         jb.ta_log2      = static_cast<uint8_t>(ta_log2);
-        jb.ta_positions = t2 ? 1 : 0;
+        jb.ta_positions = (t2 || masked) ? 1 : 0;
+        jb.crb_list     = masked ? static_cast<uint32_t>(crb_lists.size()) : CHEST_CONTIGUOUS;
+        jb.span_pilots  = static_cast<uint16_t>(span_rb * per_rb);
         jobs.push_back(jb);
       }
     }
+    crb_lists.insert(crb_lists.end(), rel.begin(), rel.end());
   }
   std::lock_guard<std::mutex> lock(ctx->mtx);
   HIP_TRY(hipSetDevice(ctx->device));
@@ -245,7 +289,7 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
   for (const chest_job& jb : jobs) {
     g.max_pilots = std::max<int>(g.max_pilots, jb.nof_pilots);
     g.max_dmrs   = std::max<int>(g.max_dmrs, jb.nof_dmrs);
-    g.max_words  = std::max<int>(g.max_words, static_cast<int>(((2 * jb.seq_offset) % 32 + 2 * jb.nof_pilots + 31) / 32));
+    g.max_words  = std::max<int>(g.max_words, static_cast<int>(((2 * jb.seq_offset) % 32 + 2 * jb.span_pilots + 31) / 32));
     g.max_planes = std::max<int>(g.max_planes, jb.td_interp ? jb.nof_dmrs : 1);
     g.max_gl     = std::max<int>(g.max_gl, jb.group_layers);
     g.max_dft    = std::max<int>(g.max_dft, jb.ta_dft);
@@ -260,7 +304,7 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
   uint32_t              base = 0;
   for (chest_job& jb : jobs) {
     const uint32_t n0 = 2u * jb.seq_offset;
-    const uint32_t nw = ((n0 & 31u) + 2u * jb.nof_pilots + 31u) >> 5;
+    const uint32_t nw = ((n0 & 31u) + 2u * jb.span_pilots + 31u) >> 5;
     jb.gseq_base      = base;
     for (unsigned s = 0; s < jb.nof_dmrs; ++s) {
       c_inits.push_back(jb.c_init[s]);
@@ -273,6 +317,13 @@ int srsgpu_pusch_chest_plan_create(srsgpu_context*                  ctx,
   if (build_gold_sequences(ctx, c_inits, nwords, offsets, &plan->d_seq, &wstart) != SRSGPU_OK) {
     srsgpu_pusch_chest_plan_destroy(plan);
     return SRSGPU_ERR_HIP;
+  }
+  if (!crb_lists.empty() &&
+      (hipMalloc(&plan->d_crbs, crb_lists.size() * sizeof(uint16_t)) != hipSuccess ||
+       hipMemcpy(plan->d_crbs, crb_lists.data(), crb_lists.size() * sizeof(uint16_t), hipMemcpyHostToDevice) !=
+           hipSuccess)) {
+    srsgpu_pusch_chest_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload CRB lists");
   }
   if (!jobs.empty() && (hipMalloc(&plan->d_jobs, jobs.size() * sizeof(chest_job)) != hipSuccess ||
                         hipMemcpy(plan->d_jobs, jobs.data(), jobs.size() * sizeof(chest_job), hipMemcpyHostToDevice) !=
@@ -294,7 +345,7 @@ int srsgpu_pusch_chest_plan_execute(const srsgpu_pusch_chest_plan* plan,
   if (plan == nullptr || d_grids == nullptr || d_ch_estimates == nullptr || d_noise_var == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  launch_pusch_chest(plan->d_jobs, plan->nof_jobs, plan->geom, d_grids, d_ch_estimates, d_noise_var, d_metrics,
+  launch_pusch_chest(plan->d_crbs, plan->d_jobs, plan->nof_jobs, plan->geom, d_grids, d_ch_estimates, d_noise_var, d_metrics,
                      plan->d_seq, static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
@@ -310,6 +361,9 @@ void srsgpu_pusch_chest_plan_destroy(srsgpu_pusch_chest_plan* plan)
   }
   if (plan->d_seq != nullptr) {
     (void)hipFree(plan->d_seq);
+  }
+  if (plan->d_crbs != nullptr) {
+    (void)hipFree(plan->d_crbs);
   }
   delete plan;
 }

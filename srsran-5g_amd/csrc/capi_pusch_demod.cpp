@@ -214,6 +214,7 @@ int srsgpu_pusch_demodulator_plan_create_ex(srsgpu_context*                  ctx
     d.crb_list        = masked ? static_cast<uint32_t>(crb_lists.size()) : DEMOD_CONTIGUOUS;
     crb_lists.insert(crb_lists.end(), crbs.begin(), crbs.end());
     d.transform_precoding = c.transform_precoding;
+    d.cfo_sc              = masked ? static_cast<uint16_t>(crbs.front() * 12u) : 0u;
     d.ce_compact      = c.estimate_layout == SRSGPU_CE_COMPACT ? 1 : 0;
     if (d.ce_compact) {
       d.ce_base += c.start_symbol * nsc;  // the estimator's single row (srsgpu_pusch_chest_config::estimate_layout)

@@ -134,11 +134,26 @@ __device__ __forceinline__ cpx polar1(float theta)
   return {cs, sn};
 }
 
+/// PRB of the allocation's rb-th allocated CRB relative to the first allocated CRB (the CRB list of a mask).
+__device__ __forceinline__ int alloc_rb(const chest_job& jb, const uint16_t* __restrict__ crbs, int rb)
+{
+  return jb.crb_list == CHEST_CONTIGUOUS ? rb : static_cast<int>(crbs[jb.crb_list + static_cast<uint32_t>(rb)]);
+}
+
 /// Pilot subcarrier of pilot i relative to the first allocated subcarrier.
-__device__ __forceinline__ uint32_t pilot_subcarrier(const chest_job& jb, int i)
+__device__ __forceinline__ uint32_t pilot_subcarrier(const chest_job& jb, const uint16_t* __restrict__ crbs, int i)
 {
   const int rb = i / jb.pilots_per_rb;
-  return static_cast<uint32_t>(rb * 12 + ((jb.pattern >> (4 * (i - rb * jb.pilots_per_rb))) & 15u));
+  return static_cast<uint32_t>(alloc_rb(jb, crbs, rb) * 12 +
+                               ((jb.pattern >> (4 * (i - rb * jb.pilots_per_rb))) & 15u));
+}
+
+/// DM-RS sequence position of pilot i relative to the first allocated CRB's first one: the sequence skips the
+/// unallocated CRBs (dmrs_helper.cpp:64 dmrs_sequence_generate over rb_mask).
+__device__ __forceinline__ int pilot_seq_index(const chest_job& jb, const uint16_t* __restrict__ crbs, int i)
+{
+  const int rb = i / jb.pilots_per_rb;
+  return alloc_rb(jb, crbs, rb) * jb.pilots_per_rb + (i - rb * jb.pilots_per_rb);
 }
 
 /// Maximum over the wavefront with the lowest index among equal values (srsvec::max_element keeps the first maximum).
@@ -183,7 +198,8 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
     uint32_t* __restrict__ ce,
     float* __restrict__ noise_var,
     float* __restrict__ metrics,
-    const uint32_t* __restrict__ gseq)
+    const uint32_t* __restrict__ gseq,
+    const uint16_t* __restrict__ crbs)
 {
   extern __shared__ __align__(16) unsigned char lds_raw[];
   const int EN = geom.max_pilots + 2 * CHEST_VP;
@@ -212,7 +228,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
   if (lane < 32) {
     L.taps[lane] = jb.taps[lane];
   }
-  const int nwords = static_cast<int>(((n0 & 31u) + 2u * static_cast<uint32_t>(N) + 31u) >> 5);
+  const int nwords = static_cast<int>(((n0 & 31u) + 2u * static_cast<uint32_t>(jb.span_pilots) + 31u) >> 5);
   for (int s = 0; s < D; ++s) {
     for (int wl = lane; wl < nwords; wl += CHEST_THREADS) {
       L.seq[s * W + wl] = gseq[jb.gseq_base + static_cast<uint32_t>(s * nwords + wl)];
@@ -223,10 +239,11 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
   // Pass 1: LSE of every DM-RS symbol (received x conj(pilot)), EPRE.
   float epre_acc = 0.f;
   for (int i = lane; i < N; i += CHEST_THREADS) {
-    const uint32_t k = pilot_subcarrier(jb, i);
+    const uint32_t k = pilot_subcarrier(jb, crbs, i);
+    const int      m = pilot_seq_index(jb, crbs, i);
     for (int s = 0; s < D; ++s) {
       const cpx y = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
-      const cpx p = pilot(L.seq, W, s, n0, i);
+      const cpx p = pilot(L.seq, W, s, n0, m);
       L.Y[s * NP + i] = {y.x * p.x + y.y * p.y, y.y * p.x - y.x * p.y};
       epre_acc += y.x * y.x + y.y * y.y;
     }
@@ -349,10 +366,11 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
       h              = {hq.x * sq + h.x, hq.y * sq + h.y};
     }
     if (jb.group == 0) {
-      const uint32_t k = pilot_subcarrier(jb, i);
+      const uint32_t k = pilot_subcarrier(jb, crbs, i);
+      const int      m = pilot_seq_index(jb, crbs, i);
       for (int s = 0; s < D; ++s) {
         const cpx y = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
-        cpx       q = cmul(h, pilot(L.seq, W, s, n0, i));
+        cpx       q = cmul(h, pilot(L.seq, W, s, n0, m));
         if (rotate) {
           q = cmul(q, polar1(CHEST_TWOPI * jb.epochs[jb.dmrs_symbols[s]] * cfo));
         }
@@ -378,9 +396,9 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
         L.X[n] = {0.f, 0.f};
       }
       __syncthreads();
-      const uint32_t k0 = pilot_subcarrier(jb, 0);
+      const uint32_t k0 = pilot_subcarrier(jb, crbs, 0);
       for (int i = lane; i < N; i += CHEST_THREADS) {
-        const uint32_t pos = jb.ta_positions ? pilot_subcarrier(jb, i) - k0 : static_cast<uint32_t>(i);
+        const uint32_t pos = jb.ta_positions ? pilot_subcarrier(jb, crbs, i) - k0 : static_cast<uint32_t>(i);
         L.X[__brev(pos) >> (32 - lgM)] = Fbase[(q * GL) * NP + i];
       }
       __syncthreads();
@@ -481,8 +499,10 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
   };
   const bool rotate_out = rotate && !jb.compact_cfo;
   for (int k = lane; k < nre; k += CHEST_THREADS) {
+    // PRB k / 12 of the interpolated band is the (k / 12)-th allocated CRB (compute_hop maps the band PRB by PRB).
+    const int kr = alloc_rb(jb, crbs, k / 12) * 12 + k % 12;
     for (int ly = 0; ly < GL; ++ly) {
-      uint32_t* dst = ce + jb.ce_base + ly * jb.ce_layer_stride + static_cast<uint32_t>(k);
+      uint32_t* dst = ce + jb.ce_base + ly * jb.ce_layer_stride + static_cast<uint32_t>(kr);
       const cpx v0  = freq(Fbase + ly * NP, k);
       for (int r = 0; r < jb.nof_out_symbols; ++r) {
         const int l = jb.first_symbol + r;
@@ -514,7 +534,8 @@ size_t pusch_chest_lds_bytes(const chest_geom& g)
          static_cast<size_t>(g.max_dmrs) * g.max_words * 4 + 32 * 4;
 }
 
-void launch_pusch_chest(const chest_job* d_jobs,
+void launch_pusch_chest(const uint16_t* d_crbs,
+                        const chest_job* d_jobs,
                         int              nof_jobs,
                         const chest_geom& geom,
                         const uint32_t*  d_grids,
@@ -529,7 +550,8 @@ void launch_pusch_chest(const chest_job* d_jobs,
   }
   const size_t lds = pusch_chest_lds_bytes(geom);
   hipLaunchKernelGGL(pusch_chest_kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(CHEST_THREADS),
-                     static_cast<unsigned>(lds), stream, d_jobs, geom, d_grids, d_ce, d_noise_var, d_metrics, d_seq);
+                     static_cast<unsigned>(lds), stream, d_jobs, geom, d_grids, d_ce, d_noise_var, d_metrics, d_seq,
+                     d_crbs);
 }
 
 } // namespace srsgpu

@@ -575,7 +575,7 @@ __device__ __forceinline__ void setup_uniform(const demod_desc& d, const uint32_
       const uint32_t l = i >> 4, ly = (i >> 2) & 3u, p = i & 3u;
       float          c = 0.f;
       if (ly < d.L && p < d.P) {
-        c = __uint_as_float(ce[d.ce_base + ly * d.ce_layer_stride + p * d.port_stride + d.nsc]);
+        c = __uint_as_float(ce[d.ce_base + ly * d.ce_layer_stride + p * d.port_stride + d.nsc + d.cfo_sc]);
       }
       float sn, cs;
       sincosf(6.283185307f * d.epochs[l] * c, &sn, &cs);

@@ -326,7 +326,9 @@ struct demod_desc {
   uint32_t crb_list;        ///< CRB-mask allocation: first entry of the transmission's allocated CRBs (ascending) in the
                             ///< plan's CRB list, grid_base / ce_base then exclude the first subcarrier; DEMOD_CONTIGUOUS
                             ///< for the contiguous allocation.
-  uint32_t transform_precoding;  ///< Transform-precoded: the demodulate_tp kernel handles the transmission.
+  uint16_t transform_precoding;  ///< Transform-precoded: the demodulate_tp kernel handles the transmission.
+  uint16_t cfo_sc;               ///< Subcarrier of the compact row's CFO word relative to ce_base (the first
+                                 ///< allocated one: 0 for contiguous allocations, 12 x first CRB for CRB masks).
 };
 static_assert(sizeof(demod_desc) == 160, "demod_desc layout");
 constexpr uint32_t DEMOD_CONTIGUOUS = 0xffffffffu;
@@ -420,7 +422,12 @@ struct chest_job {
   uint8_t  ta_positions;     ///< 1: pilots at their subcarrier offset (mask path), 0: in the first bins (stride 2).
   uint8_t  pad[1];
   uint32_t gseq_base;        ///< The job's DM-RS sequence words in the plan's buffer: [DM-RS symbol][staged word].
+  uint32_t crb_list;         ///< CRB-mask allocation: the allocated CRBs relative to the first one in the plan's CRB
+                             ///< list (pilots and estimates follow them); CHEST_CONTIGUOUS otherwise.
+  uint16_t span_pilots;      ///< DM-RS sequence positions from the first to the last allocated CRB (staged words).
+  uint16_t pad2;
 };
+constexpr uint32_t CHEST_CONTIGUOUS = 0xffffffffu;
 
 constexpr uint8_t CHEST_FD_NONE   = 0;
 constexpr uint8_t CHEST_FD_MEAN   = 1;
@@ -442,7 +449,8 @@ struct chest_geom {
 /// Dynamic LDS of the channel-estimator kernel for the plan's largest job.
 size_t pusch_chest_lds_bytes(const chest_geom& g);
 
-void launch_pusch_chest(const chest_job* d_jobs,
+void launch_pusch_chest(const uint16_t* d_crbs,
+                        const chest_job* d_jobs,
                         int              nof_jobs,
                         const chest_geom& geom,
                         const uint32_t*  d_grids,

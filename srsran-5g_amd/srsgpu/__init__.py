@@ -324,6 +324,8 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pusch_demodulator_plan_create_ex.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                             ctypes.POINTER(P)]
     lib.srsgpu_pusch_demodulator_plan_execute_ex.argtypes = [P, P, P, P, P, P, P]
+    lib.srsgpu_pusch_chest_plan_create_ex.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                      ctypes.POINTER(P)]
     lib.srsgpu_pdsch_dmrs_plan_destroy.argtypes = [P]
     lib.srsgpu_pdsch_dmrs_plan_destroy.restype = None
     lib.srsgpu_pusch_chest_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -373,6 +375,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
     "srsgpu_pusch_demodulator_plan_create_ex", "srsgpu_pusch_demodulator_plan_execute_ex",
+    "srsgpu_pusch_chest_plan_create_ex",
     "srsgpu_pusch_chest_plan_create", "srsgpu_pusch_chest_plan_execute", "srsgpu_pusch_chest_plan_destroy",
     "srsgpu_pdsch_dmrs_plan_create", "srsgpu_pdsch_dmrs_plan_create_ex", "srsgpu_pdsch_dmrs_plan_execute", "srsgpu_pdsch_dmrs_plan_destroy",
 ]
@@ -1134,7 +1137,7 @@ class PuschDemodulator:
 @dataclass
 class PuschChannelEstimation:
     """dmrs_pusch_estimator::configuration (dmrs_pusch_estimator.h:63): pseudo-random DM-RS, contiguous CRB
-    allocation, rx ports 0..nof_rx_ports-1, "average" time-domain strategy."""
+    allocation (or `crb_mask`: rb_mask, one byte per grid CRB), rx ports 0..nof_rx_ports-1."""
     scrambling_id: int
     n_scid: int
     dmrs_type: int
@@ -1152,6 +1155,7 @@ class PuschChannelEstimation:
     td_strategy: int = CHEST_TD_AVERAGE
     compensate_cfo: int = 0
     numerology: int = 1
+    crb_mask: Optional[np.ndarray] = None
 
 
 def make_pusch_chest_configs(ests: Sequence[PuschChannelEstimation], grid_index: Sequence[int]):
@@ -1172,11 +1176,16 @@ class PuschChannelEstimatorPlan:
     (S, Pg, 14, nsc) into estimates (S, 4, Pg, 14, nsc) (uint32 bf16 pairs), noise variances (ntx, 4) and optional
     metrics (ntx, 4, CHEST_METRICS: RSRP, EPRE, noise variance, SNR, TA seconds, CFO Hz or NaN, 0, 0)."""
 
-    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4):
+    def __init__(self, ctx: Context, cfg_array, grid_nof_prb: int, grid_nof_ports: int = 4, exts=None):
         self.ctx = ctx
         h = ctypes.c_void_p()
-        _check(_lib.srsgpu_pusch_chest_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
-                                                   len(cfg_array), grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
+        if exts is None:
+            _check(_lib.srsgpu_pusch_chest_plan_create(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                       len(cfg_array), grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
+        else:
+            _check(_lib.srsgpu_pusch_chest_plan_create_ex(ctx.handle, ctypes.cast(cfg_array, ctypes.c_void_p),
+                                                          ctypes.cast(exts, ctypes.c_void_p), len(cfg_array),
+                                                          grid_nof_prb, grid_nof_ports, ctypes.byref(h)))
         self.handle = h
 
     def execute(self, d_grids, d_ch_est, d_noise_var, d_metrics=None, stream=None):
@@ -1205,8 +1214,9 @@ class PuschChannelEstimator:
         """grids_u16 (S, Pg, 14, nsc, 2) -> (estimates (S, 4, Pg, 14, nsc, 2) uint16, noise_var (ntx, 4),
         metrics (ntx, 4, CHEST_METRICS))."""
         dev = torch.device("cuda", self.ctx.device)
+        exts, _keep = make_crb_mask_exts(ests, self.grid_nof_prb)
         plan = PuschChannelEstimatorPlan(self.ctx, make_pusch_chest_configs(ests, grid_index), self.grid_nof_prb,
-                                         self.grid_nof_ports)
+                                         self.grid_nof_ports, exts)
         g = np.ascontiguousarray(grids_u16, np.uint16)
         S = g.shape[0]
         d_g = torch.from_numpy(g.view(np.int32).reshape(-1).copy()).to(dev)

@@ -225,19 +225,24 @@ class Reference(_Lib):
               int(mmse), _ptr(g), _ptr(h), _ptr(nv), _ptr(out), cap, _ptr(stats))
         return out[:n], stats
 
-    def pusch_chest(self, cfg, grid_u16, grid_nof_prb, fd=2, td=0, compensate_cfo=False, numerology=1):
+    def pusch_chest(self, cfg, grid_u16, grid_nof_prb, fd=2, td=0, compensate_cfo=False, numerology=1,
+                    crb_mask=None):
         """dmrs_pusch_estimator_impl::estimate of one single-layer transmission: (ch_est (P, 14, nsc, 2) bf16,
-        noise_var, rsrp, epre, ta_s, cfo_hz) per port."""
+        noise_var, rsrp, epre, ta_s, cfo_hz) per port. crb_mask (one byte per grid CRB) replaces the contiguous
+        allocation as configuration::rb_mask."""
         g = np.ascontiguousarray(grid_u16, dtype=np.uint16)
         P = cfg["nof_rx_ports"]
         ce = np.zeros((P, 14, 12 * grid_nof_prb, 2), np.uint16)
         outs = [np.zeros(P, np.float32) for _ in range(5)]
-        f = self.lib.ref_pusch_chest
+        m = None if crb_mask is None else np.ascontiguousarray(np.asarray(crb_mask, np.uint8)[:grid_nof_prb])
+        f = self.lib.ref_pusch_chest_mask
         f.restype = ctypes.c_int
-        f.argtypes = [ctypes.c_int] * 6 + [ctypes.c_float, ctypes.c_uint] + [ctypes.c_int] * 9 + [_P] * 7
+        f.argtypes = [ctypes.c_int] * 6 + [ctypes.c_float, ctypes.c_uint] + [ctypes.c_int] * 4 + [_P] + \
+            [ctypes.c_int] * 5 + [_P] * 7
         f(numerology, cfg["slot"], cfg["scrambling_id"], cfg["n_scid"], cfg["dmrs_type2"], 1, cfg["scaling"],
           cfg["dmrs_symbol_mask"], cfg["start_symbol"], cfg["nof_symbols"], cfg["rb_start"], cfg["nof_rb"],
-          grid_nof_prb, P, fd, td, int(compensate_cfo), _ptr(g), _ptr(ce), *[_ptr(o) for o in outs])
+          None if m is None else _ptr(m), grid_nof_prb, P, fd, td, int(compensate_cfo), _ptr(g), _ptr(ce),
+          *[_ptr(o) for o in outs])
         return (ce,) + tuple(outs)
 
     def dmrs_pdsch_map(self, cfg, weights, grid_nof_prb, numerology=1, crb_mask=None):

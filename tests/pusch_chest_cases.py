@@ -7,14 +7,34 @@ import pusch_chest_oracle as C
 from pusch_demod_cases import bf16
 
 
+def random_crb_mask(rng, grid_prb, nof_rb=None):
+    """A non-contiguous CRB mask: RBG-like runs or scattered CRBs (at least two runs)."""
+    while True:
+        if rng.random() < 0.5:
+            rbg = int(rng.choice([2, 4, 8]))
+            sel = rng.random((grid_prb + rbg - 1) // rbg) < rng.uniform(0.2, 0.8)
+            m = np.repeat(sel, rbg)[:grid_prb].astype(np.uint8)
+        else:
+            m = (rng.random(grid_prb) < rng.uniform(0.1, 0.8)).astype(np.uint8)
+        if nof_rb is not None and m.sum() > nof_rb:
+            m[np.flatnonzero(m)[nof_rb:]] = 0
+        rbs = np.flatnonzero(m)
+        if rbs.size >= 2 and rbs[-1] - rbs[0] + 1 != rbs.size:
+            return m
+
+
 def random_case(rng, grid_prb, nof_rx_ports=None, nof_rb=None, dmrs_type2=None, snr_db=None, dmrs_mask=None,
-                cfo_hz=0.0, delay=0.0, numerology=1):
+                cfo_hz=0.0, delay=0.0, numerology=1, crb_mask=None):
     """Returns (cfg, grid (P, 14, nsc, 2) bf16, true channel (P, nsc) complex). cfo_hz rotates OFDM symbol l by
     2 pi cfo t_l (t_l: the symbol's start epoch); delay (in samples of a 4096-point DFT, may be negative) shifts every
-    path."""
+    path. crb_mask: the DM-RS go to those CRBs (cfg rb_start / nof_rb = its first CRB / CRB count)."""
     P = int(nof_rx_ports or rng.integers(1, 5))
     nrb = int(nof_rb or rng.integers(1, grid_prb + 1))
     rb0 = int(rng.integers(0, grid_prb - nrb + 1))
+    rbs = list(range(rb0, rb0 + nrb))
+    if crb_mask is not None:
+        rbs = [int(i) for i in np.flatnonzero(crb_mask)]
+        rb0, nrb = rbs[0], len(rbs)
     t2 = int(dmrs_type2 if dmrs_type2 is not None else rng.integers(0, 2))
     start = int(rng.integers(0, 2))
     nsym = int(rng.integers(6, 15 - start))
@@ -36,11 +56,11 @@ def random_case(rng, grid_prb, nof_rx_ports=None, nof_rb=None, dmrs_type2=None, 
     nv = 10 ** (-snr / 10)
     x = (rng.choice([-1, 1], (14, nsc)) + 1j * rng.choice([-1, 1], (14, nsc))) / np.sqrt(2)
     pat = C.layer0_pattern(t2)
-    sc = np.array([(rb0 + rb) * 12 + q for rb in range(nrb) for q in pat])
+    sc = np.array([rb * 12 + q for rb in rbs for q in pat])
     for l in range(14):
         if (dmrs_mask >> l) & 1:
             x[l, sc] = cfg["scaling"] * C.dmrs_sequence(cfg["slot"], l, cfg["scrambling_id"], cfg["n_scid"], t2, rb0,
-                                                        nrb)
+                                                        nrb, rbs)
     y = H[:, None, :] * x[None]
     if cfo_hz:
         ep = C.symbol_start_epochs(numerology)

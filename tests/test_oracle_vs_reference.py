@@ -332,6 +332,46 @@ def test_pusch_demodulator_general_oracle_vs_reference(ref, seed):
                                atol=5e-3 if cfg["nof_layers"] == 1 else 0.1)
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_pusch_chest_crb_mask_oracle_vs_reference(ref, seed):
+    """Non-contiguous CRB masks (rb_mask) against the reference's estimator: noise variance, RSRP, EPRE (1e-3
+    relative), time alignment (2 Tc; RE-mask DFT path), CFO (0.05 Hz) are pinned as computed; the estimates are pinned
+    through what the reference writes. Its write-back (port_channel_estimator_average_impl.cpp:295-304) puts every
+    allocated PRB's 12 estimates at the lowest allocated CRB (the subspan never advances), so the reference's lowest
+    CRB holds the LAST allocated PRB's estimate and every other allocated CRB stays unwritten (zero): the restatement's
+    last-PRB estimate must equal the former (with the "average" time strategy; "interpolate" reads past the PRB's
+    window, so only its metrics are pinned), and the restatement writes PRB i at CRB i of the mask (the intended
+    mapping, which the GPU implements). Type 2 is left out: the reference's type-2 estimator is undefined behaviour in
+    this build (see test_pusch_chest_type2_reference_is_undefined)."""
+    import pusch_chest_oracle as C
+    from ofdm_oracle import bf16_to_complex
+    from pusch_chest_cases import random_case, random_crb_mask
+    rng = np.random.default_rng(1500 + seed)
+    mask = random_crb_mask(rng, 48, nof_rb=None)
+    td = seed % 2
+    comp = seed % 3 != 0
+    cfg, grid, _ = random_case(rng, 48, crb_mask=mask, dmrs_type2=0,  # type 2: reference UB (see below)
+                               cfo_hz=rng.uniform(-1500, 1500), delay=rng.uniform(-20, 20))
+    ce, nv, rsrp, epre, ta, cfo = ref.pusch_chest(cfg, grid, 48, fd=2, td=td, compensate_cfo=comp, crb_mask=mask)
+    ch, nv_o, rsrp_o, epre_o, ex = C.estimate(cfg, bf16_to_complex(grid), td="interpolate" if td else "average",
+                                              compensate_cfo=comp, crb_mask=mask)
+    np.testing.assert_allclose(nv, nv_o, rtol=1e-3)
+    np.testing.assert_allclose(rsrp, rsrp_o, rtol=1e-3)
+    np.testing.assert_allclose(epre, epre_o, rtol=1e-3)
+    np.testing.assert_allclose(ta, ex["ta_s"], atol=2 * C.T_C if hasattr(C, "T_C") else 2 / (480000 * 4096))
+    np.testing.assert_allclose(cfo, ex["cfo_hz"], atol=0.05)
+    if td:
+        return  # "interpolate" reads nof_re estimates from each PRB's 12-wide window: past it, undefined (:297)
+    rbs = np.flatnonzero(mask)
+    got = bf16_to_complex(ce)
+    for l in range(cfg["start_symbol"], cfg["start_symbol"] + cfg["nof_symbols"]):
+        want = ch[:, l, rbs[-1] * 12:(rbs[-1] + 1) * 12]
+        g = got[:, l, rbs[0] * 12:(rbs[0] + 1) * 12]
+        rms = np.sqrt(np.mean(np.abs(want) ** 2))
+        assert np.max(np.abs(g - want)) < 2.5e-2 * rms, (cfg, l)
+        assert not np.any(got[:, l, rbs[1] * 12:(rbs[1] + 1) * 12]), "the reference leaves the other CRBs unwritten"
+
+
 @pytest.mark.parametrize("seed", range(24))
 def test_pusch_chest_cfo_ta_oracle_vs_reference(ref, seed):
     """CFO estimation (compensated and not), time alignment and the interpolate time strategy of the restatement against

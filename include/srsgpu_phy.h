@@ -594,6 +594,67 @@ int srsgpu_pusch_demodulator_plan_execute_ex(const srsgpu_pusch_demodulator_plan
                                              void*                                stream);
 
 /* ------------------------------------------------------------------------------------------------------------------
+ * UL-SCH demultiplexer (UCI on PUSCH, TS 38.212 section 6.2.7) — replaces srsran::ulsch_demultiplex::demultiplex /
+ * set_csi_part2 (include/srsran/phy/upper/channel_processors/pusch/ulsch_demultiplex.h:64,
+ * lib/phy/upper/channel_processors/pusch/ulsch_demultiplex_impl.cpp:199) for every transmission of a batch: routes the
+ * demodulated, descrambled codeword LLRs (the PUSCH demodulator's output, RE by RE) to the UL-SCH data stream (the PUSCH
+ * decoder's input; REs carrying HARQ-ACK of <= 2 bits stay in it as zeros), HARQ-ACK, CSI Part 1 and CSI Part 2 LLR
+ * streams, with the reference's 1- / 2-bit UCI placeholder handling (the scrambling sequence c_init = rnti 2^15 + n_id
+ * re-applied to the "y" and "x" placeholder bits, :91 / :131). The RE sets per OFDM symbol (reserved HARQ-ACK REs,
+ * HARQ-ACK, CSI Part 1, CSI Part 2, :316) are fixed at plan creation; CSI Part 2 is placed as if set_csi_part2 were
+ * called before the first symbol. Input and output offsets are in LLRs.
+ * ------------------------------------------------------------------------------------------------------------------ */
+typedef struct {
+  uint8_t  modulation_order;            /* Qm: 2, 4, 6, 8 */
+  uint8_t  nof_layers;                  /* 1..4 */
+  uint16_t nof_prb;                     /* allocated PRBs (count) */
+  uint8_t  start_symbol;                /* start_symbol_index */
+  uint8_t  nof_symbols;
+  uint16_t dmrs_symbol_mask;            /* DM-RS symbols */
+  uint8_t  dmrs_type;                   /* 1 or 2 */
+  uint8_t  nof_cdm_groups_without_data; /* 1..2 (type 1), 1..3 (type 2) */
+  uint16_t rnti;                        /* scrambling c_init = rnti 2^15 + n_id (placeholders) */
+  uint16_t n_id;
+  uint16_t pad;
+  uint32_t nof_harq_ack_rvd;            /* G^HARQ-ACK_rvd */
+  uint32_t nof_harq_ack_bits;           /* O^HARQ-ACK */
+  uint32_t nof_enc_harq_ack_bits;       /* G^HARQ-ACK */
+  uint32_t nof_csi_part1_bits;          /* O^CSI-1 */
+  uint32_t nof_enc_csi_part1_bits;      /* G^CSI-1 */
+  uint32_t nof_csi_part2_bits;          /* O^CSI-2 */
+  uint32_t nof_enc_csi_part2_bits;      /* G^CSI-2 (0: none) */
+  uint32_t llr_offset;                  /* first codeword LLR in the input */
+  uint32_t sch_offset;                  /* first UL-SCH LLR in d_sch */
+  uint32_t harq_offset;                 /* first HARQ-ACK LLR in d_harq */
+  uint32_t csi1_offset;                 /* first CSI Part 1 LLR in d_csi1 */
+  uint32_t csi2_offset;                 /* first CSI Part 2 LLR in d_csi2 */
+} srsgpu_ulsch_demux_config;
+
+typedef struct srsgpu_ulsch_demux_plan srsgpu_ulsch_demux_plan;
+
+/** Validates the transmissions (every UCI field must fit the allocation, as the reference asserts at the end of the
+ *  codeword) and uploads the RE routing. */
+int srsgpu_ulsch_demux_plan_create(srsgpu_context*                  ctx,
+                                   const srsgpu_ulsch_demux_config* cfgs,
+                                   uint32_t                         nof_tx,
+                                   srsgpu_ulsch_demux_plan**        plan);
+
+/** LLRs of transmission tx: stream 0 = codeword (input), 1 = UL-SCH, 2 = HARQ-ACK, 3 = CSI Part 1, 4 = CSI Part 2. */
+uint32_t srsgpu_ulsch_demux_plan_nof_llrs(const srsgpu_ulsch_demux_plan* plan, uint32_t tx, uint32_t stream);
+
+/** Demultiplexes every planned transmission. Asynchronous on `stream`, hipGraph-capturable. Output pointers of streams
+ *  no transmission uses may be NULL. */
+int srsgpu_ulsch_demux_plan_execute(const srsgpu_ulsch_demux_plan* plan,
+                                    const int8_t*                  d_llrs,
+                                    int8_t*                        d_sch,
+                                    int8_t*                        d_harq,
+                                    int8_t*                        d_csi1,
+                                    int8_t*                        d_csi2,
+                                    void*                          stream);
+
+void srsgpu_ulsch_demux_plan_destroy(srsgpu_ulsch_demux_plan* plan);
+
+/* ------------------------------------------------------------------------------------------------------------------
  * PUSCH decoder (transport-block level) — replaces srsran::pusch_decoder (include/srsran/phy/upper/channel_processors/
  * pusch/pusch_decoder.h; lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.cpp: new_data :98, segmentation
  * :190, codeblock tasks :283, join_and_notify :386): segmentation, per-codeblock rate dematching + HARQ combining +

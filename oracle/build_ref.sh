@@ -67,6 +67,8 @@ SRCS=(
   "$REF/lib/phy/upper/channel_modulation/evm_calculator_generic_impl.cpp:-mavx2 -mfma"
   "$REF/lib/phy/generic_functions/transform_precoding/transform_precoder_dft_impl.cpp:-mavx2 -mfma"
   "$HERE/ref/ref_pusch_demod.cpp:-mavx2 -mfma -I$REF"
+  "$REF/lib/phy/upper/channel_processors/pusch/ulsch_demultiplex_impl.cpp:-mavx2 -mfma"
+  "$HERE/ref/ref_ulsch_demux.cpp:-mavx2 -mfma -I$REF"
   "$REF/lib/phy/upper/signal_processors/dmrs_pusch_estimator_impl.cpp:-mavx2 -mfma"
   "$REF/lib/phy/upper/signal_processors/dmrs_helper.cpp:-mavx2 -mfma"
   "$REF/lib/phy/upper/signal_processors/port_channel_estimator_average_impl.cpp:-mavx2 -mfma"

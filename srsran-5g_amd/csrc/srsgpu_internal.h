@@ -460,6 +460,39 @@ void launch_pusch_chest(const uint16_t* d_crbs,
                         const uint32_t*  d_seq,
                         hipStream_t      stream);
 
+/// UL-SCH demultiplexer (ulsch_demux.hip): per-transmission descriptor and per-RE routing.
+struct ulsch_demux_desc {
+  uint32_t llr_offset, sch_offset, uci_offset[3];  ///< Input codeword and output stream offsets (LLRs).
+  uint32_t route;                                  ///< First routing entry (one per RE) in the plan's table.
+  uint32_t seq_word_offset;                        ///< Scrambling sequence words (placeholders) in the plan's buffer.
+  uint32_t nof_llrs;                               ///< Codeword LLRs.
+  uint8_t  qm, lq;                                 ///< Modulation order, LLRs per RE (layers x Qm).
+  uint8_t  placeholder[3];                         ///< Per UCI field: 0 none, 1 / 2: the 1- / 2-bit placeholders.
+  uint8_t  pad[3];
+};
+/// Routing of one RE: sch = RE index in the UL-SCH stream or DEMUX_NONE; uci = kind (bits 30-31: 0 none, 1 HARQ-ACK,
+/// 2 CSI Part 1, 3 CSI Part 2) | RE index in that stream (bits 0-29); csi2 = RE index in the CSI Part 2 stream of a
+/// HARQ-ACK RE (<= 2 bits, on the reserved REs) that CSI Part 2 was also mapped to, else DEMUX_NONE. HARQ-ACK of <= 2
+/// bits punctures: the UL-SCH and CSI Part 2 receive zeros on its REs (ulsch_demultiplex_impl.cpp:468).
+struct ulsch_demux_route {
+  uint32_t sch;
+  uint32_t uci;
+  uint32_t csi2;
+};
+constexpr uint32_t DEMUX_NONE = 0xffffffffu;
+
+void launch_ulsch_demux(const ulsch_demux_desc*  d_desc,
+                        const ulsch_demux_route* d_routes,
+                        const mod_chunk*         d_chunks,
+                        int                      nof_chunks,
+                        const int8_t*            d_llrs,
+                        int8_t*                  d_sch,
+                        int8_t*                  d_harq,
+                        int8_t*                  d_csi1,
+                        int8_t*                  d_csi2,
+                        const uint32_t*          d_seq,
+                        hipStream_t              stream);
+
 void launch_pusch_demodulate_tp(const demod_desc*       d_desc,
                                 const demod_tp_job*      d_jobs,
                                 int                      nof_jobs,

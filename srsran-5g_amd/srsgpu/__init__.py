@@ -221,6 +221,39 @@ assert ctypes.sizeof(PuschDemodConfig) == 32
 DEMOD_STATS = 30  # SRSGPU_DEMOD_STATS: 15 rows (symbols 0..13, then the transmission) x (SINR dB, EVM)
 
 
+class UlschDemuxConfig(ctypes.Structure):
+    """srsgpu_ulsch_demux_config (include/srsgpu_phy.h): ulsch_demultiplex::configuration of one transmission plus
+    the CSI Part 2 size, the scrambling identity (placeholders) and the stream offsets."""
+    _fields_ = [
+        ("modulation_order", ctypes.c_uint8),
+        ("nof_layers", ctypes.c_uint8),
+        ("nof_prb", ctypes.c_uint16),
+        ("start_symbol", ctypes.c_uint8),
+        ("nof_symbols", ctypes.c_uint8),
+        ("dmrs_symbol_mask", ctypes.c_uint16),
+        ("dmrs_type", ctypes.c_uint8),
+        ("nof_cdm_groups_without_data", ctypes.c_uint8),
+        ("rnti", ctypes.c_uint16),
+        ("n_id", ctypes.c_uint16),
+        ("pad", ctypes.c_uint16),
+        ("nof_harq_ack_rvd", ctypes.c_uint32),
+        ("nof_harq_ack_bits", ctypes.c_uint32),
+        ("nof_enc_harq_ack_bits", ctypes.c_uint32),
+        ("nof_csi_part1_bits", ctypes.c_uint32),
+        ("nof_enc_csi_part1_bits", ctypes.c_uint32),
+        ("nof_csi_part2_bits", ctypes.c_uint32),
+        ("nof_enc_csi_part2_bits", ctypes.c_uint32),
+        ("llr_offset", ctypes.c_uint32),
+        ("sch_offset", ctypes.c_uint32),
+        ("harq_offset", ctypes.c_uint32),
+        ("csi1_offset", ctypes.c_uint32),
+        ("csi2_offset", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(UlschDemuxConfig) == 64
+
+
 class PuschChestConfig(ctypes.Structure):
     """srsgpu_pusch_chest_config (include/srsgpu_phy.h): dmrs_pusch_estimator::configuration of one transmission."""
     _fields_ = [
@@ -324,6 +357,12 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pusch_demodulator_plan_create_ex.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                             ctypes.POINTER(P)]
     lib.srsgpu_pusch_demodulator_plan_execute_ex.argtypes = [P, P, P, P, P, P, P]
+    lib.srsgpu_ulsch_demux_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(P)]
+    lib.srsgpu_ulsch_demux_plan_nof_llrs.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
+    lib.srsgpu_ulsch_demux_plan_nof_llrs.restype = ctypes.c_uint32
+    lib.srsgpu_ulsch_demux_plan_execute.argtypes = [P, P, P, P, P, P, P]
+    lib.srsgpu_ulsch_demux_plan_destroy.argtypes = [P]
+    lib.srsgpu_ulsch_demux_plan_destroy.restype = None
     lib.srsgpu_pusch_chest_plan_create_ex.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                       ctypes.POINTER(P)]
     lib.srsgpu_pdsch_dmrs_plan_destroy.argtypes = [P]
@@ -375,7 +414,8 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
     "srsgpu_pusch_demodulator_plan_create_ex", "srsgpu_pusch_demodulator_plan_execute_ex",
-    "srsgpu_pusch_chest_plan_create_ex",
+    "srsgpu_pusch_chest_plan_create_ex", "srsgpu_ulsch_demux_plan_create", "srsgpu_ulsch_demux_plan_nof_llrs",
+    "srsgpu_ulsch_demux_plan_execute", "srsgpu_ulsch_demux_plan_destroy",
     "srsgpu_pusch_chest_plan_create", "srsgpu_pusch_chest_plan_execute", "srsgpu_pusch_chest_plan_destroy",
     "srsgpu_pdsch_dmrs_plan_create", "srsgpu_pdsch_dmrs_plan_create_ex", "srsgpu_pdsch_dmrs_plan_execute", "srsgpu_pdsch_dmrs_plan_destroy",
 ]
@@ -1228,6 +1268,110 @@ class PuschChannelEstimator:
         plan.close()
         ce = d_ce.cpu().numpy().view(np.uint16).reshape((S, 4) + g.shape[1:])
         return ce, d_nv.cpu().numpy().reshape(-1, 4), d_m.cpu().numpy().reshape(-1, 4, CHEST_METRICS)
+
+
+@dataclass
+class UlschDemultiplexing:
+    """ulsch_demultiplex::configuration (ulsch_demultiplex.h:48) + set_csi_part2 sizes + the transmission's rnti /
+    n_id (scrambling of the UCI placeholders)."""
+    modulation_order: int
+    nof_layers: int
+    nof_prb: int
+    start_symbol: int
+    nof_symbols: int
+    dmrs_symbol_mask: int
+    dmrs_type: int
+    nof_cdm_groups_without_data: int
+    rnti: int
+    n_id: int
+    nof_harq_ack_rvd: int = 0
+    nof_harq_ack_bits: int = 0
+    nof_enc_harq_ack_bits: int = 0
+    nof_csi_part1_bits: int = 0
+    nof_enc_csi_part1_bits: int = 0
+    nof_csi_part2_bits: int = 0
+    nof_enc_csi_part2_bits: int = 0
+
+
+class UlschDemuxPlan:
+    """srsgpu_ulsch_demux_plan: UCI-on-PUSCH demultiplexing of a batch of codewords (int8 LLRs) into the UL-SCH,
+    HARQ-ACK, CSI Part 1 and CSI Part 2 streams."""
+
+    STREAMS = ("codeword", "sch", "harq", "csi1", "csi2")
+
+    def __init__(self, ctx: Context, demuxes: Sequence[UlschDemultiplexing], llr_offsets: Sequence[int]):
+        self.ctx = ctx
+        arr = (UlschDemuxConfig * len(demuxes))()
+        for i, (m, off) in enumerate(zip(demuxes, llr_offsets)):
+            a = arr[i]
+            for f, _ in UlschDemuxConfig._fields_:
+                if hasattr(m, f):
+                    setattr(a, f, getattr(m, f))
+            a.llr_offset = off
+        h = ctypes.c_void_p()
+        # First pass sizes the output streams, the second fixes their offsets.
+        _check(_lib.srsgpu_ulsch_demux_plan_create(ctx.handle, ctypes.cast(arr, ctypes.c_void_p), len(arr),
+                                                   ctypes.byref(h)))
+        n = [[int(_lib.srsgpu_ulsch_demux_plan_nof_llrs(h, t, k)) for k in range(5)] for t in range(len(arr))]
+        _lib.srsgpu_ulsch_demux_plan_destroy(h)
+        self.offsets = {k: [] for k in self.STREAMS[1:]}
+        self.totals = {}
+        for j, k in enumerate(self.STREAMS[1:]):
+            o = 0
+            for t in range(len(arr)):
+                self.offsets[k].append(o)
+                o += n[t][j + 1]
+            self.totals[k] = o
+        for t in range(len(arr)):
+            arr[t].sch_offset, arr[t].harq_offset = self.offsets["sch"][t], self.offsets["harq"][t]
+            arr[t].csi1_offset, arr[t].csi2_offset = self.offsets["csi1"][t], self.offsets["csi2"][t]
+        h = ctypes.c_void_p()
+        _check(_lib.srsgpu_ulsch_demux_plan_create(ctx.handle, ctypes.cast(arr, ctypes.c_void_p), len(arr),
+                                                   ctypes.byref(h)))
+        self.handle = h
+        self.counts = n
+
+    def execute(self, d_llrs, d_sch, d_harq=None, d_csi1=None, d_csi2=None, stream=None):
+        _check(_lib.srsgpu_ulsch_demux_plan_execute(self.handle, _dptr(d_llrs), _dptr(d_sch), _dptr(d_harq),
+                                                    _dptr(d_csi1), _dptr(d_csi2), _stream_handle(stream)))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.srsgpu_ulsch_demux_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class UlschDemultiplexer:
+    """GPU counterpart of srsran::ulsch_demultiplex (ulsch_demultiplex_impl.cpp:199): demultiplex_batch() takes each
+    transmission's codeword LLRs and returns dicts of the sch / harq / csi1 / csi2 LLR streams."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def demultiplex_batch(self, codewords: Sequence[np.ndarray], demuxes: Sequence[UlschDemultiplexing]):
+        dev = torch.device("cuda", self.ctx.device)
+        offs, o = [], 0
+        for cw in codewords:
+            offs.append(o)
+            o += cw.size
+        plan = UlschDemuxPlan(self.ctx, demuxes, offs)
+        d_in = torch.from_numpy(np.concatenate([np.asarray(c, np.int8) for c in codewords])).to(dev)
+        outs = {k: torch.full((max(plan.totals[k], 4),), 99, dtype=torch.int8, device=dev) for k in plan.totals}
+        plan.execute(d_in, outs["sch"], outs["harq"], outs["csi1"], outs["csi2"])
+        torch.cuda.synchronize(dev)
+        host = {k: v.cpu().numpy() for k, v in outs.items()}
+        res = []
+        for t in range(len(demuxes)):
+            res.append({k: host[k][plan.offsets[k][t]: plan.offsets[k][t] + plan.counts[t][j + 1]]
+                        for j, k in enumerate(("sch", "harq", "csi1", "csi2"))})
+        plan.close()
+        return res
 
 
 class OfdmPlan:

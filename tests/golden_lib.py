@@ -233,3 +233,21 @@ def pdsch_mod_general_cases():
                    prg_weights=d[f"case{i}_prg_w"] if cfg["prg_size"] else None)
         yield cfg, nbits, G, d[f"case{i}_w"], d[f"case{i}_cw"], d[f"case{i}_grid"], d[f"case{i}_crb"]
         i += 1
+
+
+ULSCH_DEMUX_KEYS = ["qm", "nof_layers", "nof_prb", "start_symbol", "nof_symbols", "dmrs_symbol_mask", "dmrs_type2",
+                    "nof_cdm_groups_without_data", "nof_harq_ack_rvd", "nof_harq_ack_bits", "nof_enc_harq_ack_bits",
+                    "nof_csi_part1_bits", "nof_enc_csi_part1_bits"]
+
+
+def ulsch_demux_cases():
+    """Yields (cfg dict, CSI-2 bits, CSI-2 encoded bits, c_init, codeword LLRs int8, reference outputs dict sch / harq /
+    csi1 / csi2) made by the reference's ulsch_demultiplex_impl."""
+    d = _load("ulsch_demux.npz")
+    i = 0
+    while f"case{i}_cfg" in d:
+        row = d[f"case{i}_cfg"]
+        cfg = {k: int(v) for k, v in zip(ULSCH_DEMUX_KEYS, row[:-3])}
+        yield (cfg, int(row[-3]), int(row[-2]), int(row[-1]), d[f"case{i}_llrs"],
+               {k: d[f"case{i}_{k}"] for k in ("sch", "harq", "csi1", "csi2")})
+        i += 1

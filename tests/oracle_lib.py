@@ -225,6 +225,24 @@ class Reference(_Lib):
               int(mmse), _ptr(g), _ptr(h), _ptr(nv), _ptr(out), cap, _ptr(stats))
         return out[:n], stats
 
+    def ulsch_demux(self, cfg, llrs, c_init, csi2_bits=0, csi2_enc_bits=0, block_size=1 << 20):
+        """ulsch_demultiplex_impl fed the codeword in blocks: dict sch / harq / csi1 / csi2 of int8 LLRs."""
+        x = np.ascontiguousarray(llrs, dtype=np.int8)
+        cap = x.size + 64
+        outs = [np.zeros(cap, np.int8) for _ in range(4)]
+        counts = np.zeros(4, np.int32)
+        f = self.lib.ref_ulsch_demux
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint] + [ctypes.c_int] * 9 + [ctypes.c_uint, _P, ctypes.c_int,
+                                                                                   ctypes.c_int] + [_P] * 4 + \
+            [ctypes.c_int, _P]
+        f(cfg["qm"], cfg["nof_layers"], cfg["nof_prb"], cfg["start_symbol"], cfg["nof_symbols"],
+          cfg["dmrs_symbol_mask"], cfg["dmrs_type2"], cfg["nof_cdm_groups_without_data"], cfg["nof_harq_ack_rvd"],
+          cfg["nof_harq_ack_bits"], cfg["nof_enc_harq_ack_bits"], cfg["nof_csi_part1_bits"],
+          cfg["nof_enc_csi_part1_bits"], csi2_bits, csi2_enc_bits, c_init, _ptr(x), x.size, block_size,
+          *[_ptr(o) for o in outs], cap, _ptr(counts))
+        return {k: o[:n] for k, o, n in zip(("sch", "harq", "csi1", "csi2"), outs, counts)}
+
     def pusch_chest(self, cfg, grid_u16, grid_nof_prb, fd=2, td=0, compensate_cfo=False, numerology=1,
                     crb_mask=None):
         """dmrs_pusch_estimator_impl::estimate of one single-layer transmission: (ch_est (P, 14, nsc, 2) bf16,

@@ -208,3 +208,15 @@ def test_pusch_demod_general_golden():
                                    atol=5e-3 if cfg["nof_layers"] == 1 else 0.1)
         n += 1
     assert n == 8
+
+
+def test_ulsch_demux_golden():
+    """The UL-SCH demultiplexer restatement bit-exact against the reference's outputs."""
+    import ulsch_demux_oracle as U
+    n = 0
+    for cfg, c2b, c2e, c_init, llrs, want in G.ulsch_demux_cases():
+        got = U.demultiplex(cfg, llrs, c_init, c2b, c2e)
+        for k in ("sch", "harq", "csi1", "csi2"):
+            assert np.array_equal(got[k], want[k]), (k, cfg)
+        n += 1
+    assert n == 12

@@ -468,3 +468,21 @@ def test_pdsch_dmrs_crb_mask_oracle_vs_reference(ref, seed):
     contiguous = np.zeros(51, np.uint8)
     contiguous[cfg["rb_start"]:cfg["rb_start"] + cfg["nof_rb"]] = 1
     assert np.array_equal(ref.dmrs_pdsch_map(cfg, w, 51, crb_mask=contiguous), ref.dmrs_pdsch_map(cfg, w, 51))
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_ulsch_demux_oracle_vs_reference(ref, seed):
+    """UCI-on-PUSCH demultiplexing restatement bit-exact against the reference's ulsch_demultiplex_impl: random
+    allocations / DM-RS patterns, HARQ-ACK of 0, 1, 2 (placeholders on the reserved REs, zeroed for the UL-SCH) or
+    more bits, CSI Part 1 and CSI Part 2 (1- / 2-bit placeholders included), QPSK..256QAM, 1-2 layers, the codeword fed
+    in odd-sized blocks."""
+    import ulsch_demux_oracle as U
+    from ulsch_demux_cases import nof_llrs, random_config
+    rng = np.random.default_rng(1700 + seed)
+    cfg, c2b, c2e, c_init = random_config(rng)
+    llrs = rng.integers(-120, 121, nof_llrs(cfg)).astype(np.int8)
+    want = ref.ulsch_demux(cfg, llrs, c_init, c2b, c2e, block_size=int(rng.integers(7, 500)))
+    got = U.demultiplex(cfg, llrs, c_init, c2b, c2e)
+    for k in ("sch", "harq", "csi1", "csi2"):
+        assert np.array_equal(got[k], want[k]), (k, cfg, c2b, c2e)
+    assert want["harq"].size == cfg["nof_enc_harq_ack_bits"] and want["csi2"].size == c2e

@@ -229,6 +229,26 @@ def gen_pusch_demod_general(ref, rng):
     np.savez_compressed(os.path.join(OUT, "pusch_demod_general.npz"), **out)
 
 
+def gen_ulsch_demux(ref, rng):
+    """Reference UL-SCH demultiplexer outputs (ulsch_demultiplex_impl) of random UCI-on-PUSCH configurations."""
+    from ulsch_demux_cases import nof_llrs, random_config
+    out = {}
+    for i in range(12):
+        cfg, c2b, c2e, c_init = random_config(rng)
+        llrs = rng.integers(-120, 121, nof_llrs(cfg)).astype(np.int8)
+        res = ref.ulsch_demux(cfg, llrs, c_init, c2b, c2e, block_size=int(rng.integers(7, 500)))
+        out[f"case{i}_cfg"] = np.array([cfg[k] for k in ULSCH_DEMUX_KEYS] + [c2b, c2e, c_init], np.int64)
+        out[f"case{i}_llrs"] = llrs
+        for k, v in res.items():
+            out[f"case{i}_{k}"] = v
+    np.savez_compressed(os.path.join(OUT, "ulsch_demux.npz"), **out)
+
+
+ULSCH_DEMUX_KEYS = ["qm", "nof_layers", "nof_prb", "start_symbol", "nof_symbols", "dmrs_symbol_mask", "dmrs_type2",
+                    "nof_cdm_groups_without_data", "nof_harq_ack_rvd", "nof_harq_ack_bits", "nof_enc_harq_ack_bits",
+                    "nof_csi_part1_bits", "nof_enc_csi_part1_bits"]
+
+
 def gen_pusch_chest(ref, rng):
     """Reference DM-RS channel estimates (dmrs_pusch_estimator_impl, filter / mean / none smoothing, average time
     strategy) of random single-layer transmissions in 24-PRB grids (DM-RS type 1)."""
@@ -343,7 +363,7 @@ def main():
     if len(sys.argv) > 1:  # regenerate only the named fixture sets, e.g. `python tools/gen_golden.py ofdm`
         for name in sys.argv[1:]:
             seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18, "pdsch_dmrs": 19, "pusch_chest_cfo": 20,
-                    "pdsch_mod_general": 21, "pdsch_dmrs_mask": 22, "pusch_demod_general": 23}[name]
+                    "pdsch_mod_general": 21, "pdsch_dmrs_mask": 22, "pusch_demod_general": 23, "ulsch_demux": 24}[name]
             globals()["gen_" + name](ref, np.random.default_rng(seed))
         return
     gen_crc(ref, np.random.default_rng(10))
@@ -360,6 +380,7 @@ def main():
     gen_pdsch_mod_general(ref, np.random.default_rng(21))
     gen_pdsch_dmrs_mask(ref, np.random.default_rng(22))
     gen_pusch_demod_general(ref, np.random.default_rng(23))
+    gen_ulsch_demux(ref, np.random.default_rng(24))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

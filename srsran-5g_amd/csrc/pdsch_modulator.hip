@@ -59,33 +59,17 @@ __device__ __forceinline__ uint32_t to_bf16_bits(float v)
   return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
 }
 
-__global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_desc* __restrict__ descs,
-                                                                      const uint16_t* __restrict__ sc_map,
-                                                                      const float* __restrict__ prg_w,
-                                                                      const mod_chunk* __restrict__ chunks,
-                                                                      const uint32_t* __restrict__ cw,
-                                                                      uint32_t* __restrict__ grids,
-                                                                      const uint32_t* __restrict__ seq)
+/// The chunk's REs: modulation, layer mapping, precoding and mapping. MAP: general allocation (the plan's RE ->
+/// subcarrier map); PRG: per-PRG precoding weights (resource_grid_mapper_impl.cpp:218).
+template <bool MAP, bool PRG>
+__device__ __forceinline__ void modulate_res(const mod_desc& d,
+                                             const mod_chunk& ch,
+                                             const uint32_t*  bits,
+                                             const uint16_t* __restrict__ sc_map,
+                                             const float* __restrict__ prg_w,
+                                             uint32_t* __restrict__ grids)
 {
-  __shared__ uint32_t bits[MOD_CHUNK_WORDS + 1];
-  const mod_chunk ch  = chunks[blockIdx.x];
-  const mod_desc& d   = descs[ch.tx];
-  const uint32_t  tid = threadIdx.x;
-  const uint32_t  nwords = (d.nof_bits + 31u) >> 5;
-
-  // Stage the chunk's scrambled words (and the first word of the next chunk, for an RE straddling the boundary).
-  for (uint32_t j = tid; j < MOD_CHUNK_WORDS; j += MOD_THREADS) {
-    const uint32_t w = ch.word0 + j;
-    bits[j]          = (w < nwords) ? scrambled_word(d, cw, seq, w) : 0u;
-  }
-  {
-    if (tid == 0) {
-      const uint32_t w2 = ch.word0 + MOD_CHUNK_WORDS;
-      bits[MOD_CHUNK_WORDS] = (w2 < nwords) ? scrambled_word(d, cw, seq, w2) : 0u;
-    }
-  }
-
-  // Per-transmission constants.
+  const uint32_t tid = threadIdx.x;
   const uint32_t qm = d.qm, L = d.L, P = d.P, Lq = L * qm;
   const uint32_t qmask = (1u << qm) - 1u;
   float          w[4][4][2];
@@ -97,7 +81,6 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
       w[p][l][1] = d.w[p][l][1];
     }
   }
-  __syncthreads();
 
   for (uint32_t r = ch.re_begin + tid; r < ch.re_end; r += MOD_THREADS) {
     // The RE's L * Qm bits, left-aligned in 64 bits.
@@ -111,14 +94,13 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
     for (int j = 1; j < 15; ++j) {
       l += (d.sym_cum[j] <= r) ? 1u : 0u;
     }
-    const uint32_t k    = r - d.sym_cum[l];
-    const bool     dmrs = (d.dmrs_mask >> l) & 1u;
+    const uint32_t k = r - d.sym_cum[l];
     uint32_t       sc;
-    if (d.sc_map != NO_SC_MAP) {
+    if constexpr (MAP) {
       // General allocation (CRB mask, reserved REs, PRG precoding): the plan's RE -> grid subcarrier map (grid_base
       // at CRB 0, so sc is the absolute subcarrier the PRG index below needs).
       sc = sc_map[d.sc_map + r];
-    } else if (dmrs) {
+    } else if ((d.dmrs_mask >> l) & 1u) {
       const uint32_t nd  = d.nd_dmrs;
       const uint32_t prb = k / nd;
       const uint32_t j   = k - prb * nd;
@@ -127,8 +109,8 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
       sc = k;
     }
     const uint32_t e = d.grid_base + l * d.nsc + sc;
-    // Per-PRG precoding (resource_grid_mapper_impl.cpp:218): the weights of the PRG holding the RE's subcarrier.
-    const float* wt = (d.prg_sc != 0) ? prg_w + d.prg_w + (sc / d.prg_sc) * 32u : nullptr;
+    // Per-PRG precoding: the weights of the PRG holding the RE's subcarrier.
+    const float* wt = PRG ? prg_w + d.prg_w + (sc / d.prg_sc) * 32u : nullptr;
 
     // Constellation points of the layers (TS 38.211 section 5.1 integer grid; the amplitude is in the weights).
     float xr[4], xi[4];
@@ -157,8 +139,8 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
 #pragma unroll
         for (int ly = 0; ly < 4; ++ly) {
           if (ly < static_cast<int>(L)) {
-            const float wr = (wt != nullptr) ? wt[(p * 4 + ly) * 2] : w[p][ly][0];
-            const float wi = (wt != nullptr) ? wt[(p * 4 + ly) * 2 + 1] : w[p][ly][1];
+            const float wr = PRG ? wt[(p * 4 + ly) * 2] : w[p][ly][0];
+            const float wi = PRG ? wt[(p * 4 + ly) * 2 + 1] : w[p][ly][1];
             const float pr = xr[ly] * wr - xi[ly] * wi;
             const float pi = xr[ly] * wi + xi[ly] * wr;
             sr             = (ly == 0) ? pr : sr + pr;
@@ -168,6 +150,45 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
         grids[e + static_cast<uint32_t>(p) * d.port_stride] = to_bf16_bits(sr) | (to_bf16_bits(si) << 16);
       }
     }
+  }
+}
+
+__global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_desc* __restrict__ descs,
+                                                                      const uint16_t* __restrict__ sc_map,
+                                                                      const float* __restrict__ prg_w,
+                                                                      const mod_chunk* __restrict__ chunks,
+                                                                      const uint32_t* __restrict__ cw,
+                                                                      uint32_t* __restrict__ grids,
+                                                                      const uint32_t* __restrict__ seq)
+{
+  __shared__ uint32_t bits[MOD_CHUNK_WORDS + 1];
+  const mod_chunk ch  = chunks[blockIdx.x];
+  const mod_desc& d   = descs[ch.tx];
+  const uint32_t  tid = threadIdx.x;
+  const uint32_t  nwords = (d.nof_bits + 31u) >> 5;
+
+  // Stage the chunk's scrambled words (and the first word of the next chunk, for an RE straddling the boundary).
+  for (uint32_t j = tid; j < MOD_CHUNK_WORDS; j += MOD_THREADS) {
+    const uint32_t w = ch.word0 + j;
+    bits[j]          = (w < nwords) ? scrambled_word(d, cw, seq, w) : 0u;
+  }
+  {
+    if (tid == 0) {
+      const uint32_t w2 = ch.word0 + MOD_CHUNK_WORDS;
+      bits[MOD_CHUNK_WORDS] = (w2 < nwords) ? scrambled_word(d, cw, seq, w2) : 0u;
+    }
+  }
+
+  __syncthreads();
+  // One instantiation per allocation kind, chosen per workgroup (uniform): the contiguous wideband path keeps its
+  // weights in registers and its subcarrier arithmetic; the general path reads the RE -> subcarrier map and, with
+  // PRGs, the PRG's weights.
+  if (d.sc_map == NO_SC_MAP) {
+    modulate_res<false, false>(d, ch, bits, sc_map, prg_w, grids);
+  } else if (d.prg_sc == 0) {
+    modulate_res<true, false>(d, ch, bits, sc_map, prg_w, grids);
+  } else {
+    modulate_res<true, true>(d, ch, bits, sc_map, prg_w, grids);
   }
 }
 

@@ -34,10 +34,13 @@ def shard_ues(ues: Sequence, world: int, rank: int) -> List:
 
 
 class TbGather:
-    """Gathers fixed-size decoded-TB buffers and CRC flags of every rank into `root`'s buffers.
+    """Gathers every rank's decoded-TB bytes and CRC flags into `root`'s buffers.
 
-    Buffers are allocated once (per plan); `gather` is one collective pair per batch, issued on the current stream.
-    On the root, `tbs[r]` / `crc_ok[r]` hold rank r's results afterwards (rank root's own included).
+    Ranks may hold different amounts (a UE shard's TB sizes differ from another's): the sizes are exchanged once at
+    construction (one all_gather), every rank sends a buffer padded to the largest, and on the root `tbs[r]` /
+    `crc_ok[r]` are views of rank r's real bytes. `gather` is one collective pair per batch on the current stream; the
+    buffers are allocated once (per plan). `assemble()` concatenates the ranks' results in rank order, which is the
+    UE order of the slot for contiguous `shard_ues` shares.
     """
 
     def __init__(self, tb_bytes: int, nof_tbs: int, device: torch.device, root: int = 0,
@@ -48,15 +51,34 @@ class TbGather:
         self.group = group
         self.tb_bytes = int(tb_bytes)
         self.nof_tbs = int(nof_tbs)
+        mine = torch.tensor([self.tb_bytes, self.nof_tbs], dtype=torch.int64, device=device)
+        sizes = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(self.world)]
+        dist.all_gather(sizes, mine, group=group)
+        self.sizes = [(int(x[0]), int(x[1])) for x in sizes]
+        self.max_bytes = max(b for b, _ in self.sizes)
+        self.max_tbs = max(n for _, n in self.sizes)
+        self._send_tbs = torch.zeros(self.max_bytes, dtype=torch.uint8, device=device)
+        self._send_ok = torch.zeros(self.max_tbs, dtype=torch.uint8, device=device)
         if self.rank == root:
-            self.tbs = [torch.empty(self.tb_bytes, dtype=torch.uint8, device=device) for _ in range(self.world)]
-            self.crc_ok = [torch.empty(self.nof_tbs, dtype=torch.uint8, device=device) for _ in range(self.world)]
+            self._recv_tbs = [torch.empty(self.max_bytes, dtype=torch.uint8, device=device) for _ in range(self.world)]
+            self._recv_ok = [torch.empty(self.max_tbs, dtype=torch.uint8, device=device) for _ in range(self.world)]
+            self.tbs = [t[:b] for t, (b, _) in zip(self._recv_tbs, self.sizes)]
+            self.crc_ok = [t[:n] for t, (_, n) in zip(self._recv_ok, self.sizes)]
         else:
+            self._recv_tbs = self._recv_ok = None
             self.tbs = None
             self.crc_ok = None
 
     def gather(self, d_tbs: torch.Tensor, d_crc_ok: torch.Tensor) -> None:
         if d_tbs.numel() != self.tb_bytes or d_crc_ok.numel() != self.nof_tbs:
             raise ValueError("TB buffer sizes differ from the ones the gather was planned for")
-        dist.gather(d_tbs, self.tbs, dst=self.root, group=self.group)
-        dist.gather(d_crc_ok, self.crc_ok, dst=self.root, group=self.group)
+        self._send_tbs[: self.tb_bytes].copy_(d_tbs)
+        self._send_ok[: self.nof_tbs].copy_(d_crc_ok)
+        dist.gather(self._send_tbs, self._recv_tbs, dst=self.root, group=self.group)
+        dist.gather(self._send_ok, self._recv_ok, dst=self.root, group=self.group)
+
+    def assemble(self):
+        """Root only: (all TB bytes, all CRC flags) in rank order."""
+        if self.rank != self.root:
+            raise ValueError("only the root holds the gathered results")
+        return torch.cat(self.tbs), torch.cat(self.crc_ok)

@@ -91,3 +91,55 @@ def test_tb_gather_world2_gloo():
         for r in range(world):
             assert np.all(tbs[r] == ((r * 16 + step) & 0xFF))
             assert list(oks[r]) == [(r + step + i) % 2 for i in range(5)]
+
+
+def _shard_worker(rank, world, port, q):
+    """One rank of a UE-sharded slot: its share of the 64 UEs (shard_ues), the host-side TB sizing of its plans
+    (segmentation -> TB bytes / codeblocks, what its PUSCH decoder plan sizes), decoded TBs faked as a function of the
+    UE index, and the gather to rank 0."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        ues = sch.slot_100mhz_4x4()
+        mine = sdist.shard_range(len(ues), world, rank)
+        segs = [ues[i].segmentation() for i in mine]
+        tb = [np.full(s.tbs // 8, i & 0xFF, np.uint8) for i, s in zip(mine, segs)]
+        ok = np.array([(i * 7) % 3 != 0 for i in mine], np.uint8)
+        g = sdist.TbGather(sum(t.size for t in tb), len(tb), torch.device("cpu"), root=0)
+        g.gather(torch.from_numpy(np.concatenate(tb)), torch.from_numpy(ok))
+        res = None
+        if rank == 0:
+            all_tbs, all_ok = g.assemble()
+            res = (all_tbs.numpy().copy(), all_ok.numpy().copy(), [s for s in g.sizes])
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ue_sharded_slot_gather_gloo(world):
+    """UE sharding end to end on CPU ranks: uneven shares (64 UEs over 3 ranks) and per-rank TB sizes, gathered to
+    rank 0 in the slot's UE order, equal to what the whole slot on one rank would give."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, res, err = q.get(timeout=120)
+        assert err is None, err
+        out[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    tbs, ok, sizes = out[0]
+    ues = sch.slot_100mhz_4x4()
+    want_tbs = np.concatenate([np.full(u.segmentation().tbs // 8, i & 0xFF, np.uint8) for i, u in enumerate(ues)])
+    want_ok = np.array([(i * 7) % 3 != 0 for i in range(len(ues))], np.uint8)
+    assert np.array_equal(tbs, want_tbs) and np.array_equal(ok, want_ok)
+    assert len(set(sizes)) > 1 or world == 1  # the ranks' TB sizes differ: the padding path ran

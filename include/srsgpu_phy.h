@@ -474,8 +474,13 @@ typedef struct {
   float    scaling;          /* beta_PUSCH^DMRS (DM-RS amplitude relative to data), > 0 */
   uint32_t grid_index;       /* slot of the rx grid and of the estimate buffer */
   uint8_t  numerology;       /* subcarrier spacing 15 kHz x 2^numerology (0..4), normal cyclic prefix */
-  uint8_t  pad[3];
+  uint8_t  dmrs_sequence;    /* SRSGPU_DMRS_PSEUDO_RANDOM (scrambling_id, n_scid) or SRSGPU_DMRS_LOW_PAPR (transform
+                                precoding: scrambling_id = n_RS_ID 0..1007, the group n_RS_ID mod 30 sequence on every
+                                DM-RS symbol, dmrs_pusch_estimator_impl.cpp:77; one layer, type 1) */
+  uint8_t  pad[2];
 } srsgpu_pusch_chest_config;
+#define SRSGPU_DMRS_PSEUDO_RANDOM 0
+#define SRSGPU_DMRS_LOW_PAPR 1
 
 typedef struct srsgpu_pusch_chest_plan srsgpu_pusch_chest_plan;
 

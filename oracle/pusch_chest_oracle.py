@@ -66,6 +66,33 @@ def dmrs_sequence(slot, symbol, scrambling_id, n_scid, dmrs_type2, rb_start, nof
     return (1 - 2 * c[2 * m]) * a + 1j * (1 - 2 * c[2 * m + 1]) * a
 
 
+def _largest_prime_below(n):
+    for p in range(n - 1, 1, -1):
+        if all(p % d for d in range(2, int(p ** 0.5) + 1)):
+            return p
+    raise ValueError(n)
+
+
+def low_papr_sequence(u, m, v=0):
+    """TS 38.211 section 5.2.2 low-PAPR base sequence r_(u,v)(n), alpha = 0, as low_papr_sequence_generator_impl.cpp
+    builds it (phase tables for M_ZC = 6..24, the length-30 formula, Zadoff-Chu with the largest prime N_ZC < M_ZC and
+    q from the float q_hat = N_ZC (u + 1) / 31 above): exp(j pi arg(n) / N_ZC)."""
+    import low_papr_tables
+    if m in low_papr_tables.PHI:
+        return np.exp(1j * np.pi * np.array(low_papr_tables.PHI[m][u]) / 4)
+    if m == 30:
+        n = np.arange(30)
+        return np.exp(1j * np.pi * -(((u + 1) * (n + 1) * (n + 2)) % 62) / 31)
+    if m < 36:
+        raise ValueError(m)
+    nzc = _largest_prime_below(m)
+    q_hat = np.float32(np.float32(nzc) * np.float32(u + 1)) / np.float32(31)
+    q = int(np.float32(float(q_hat) + 0.5 + v)) if int(np.float32(2) * q_hat) % 2 == 0 \
+        else int(np.float32(float(q_hat) + 0.5 - v))
+    mm = np.arange(m) % nzc
+    return np.exp(1j * np.pi * -((q * mm * (mm + 1)) % (2 * nzc)) / nzc)
+
+
 def virtual_pilots(base, is_start):
     """compute_v_pilots: linear regression of |p| and unwrap(arg p) over x = 0..n-1, evaluated at x = -n..-1 (start)
     or n..2n-1 (end)."""
@@ -219,7 +246,8 @@ def td_interpolate(planes, dmrs_syms, first, last, l):
     return planes[i] + (planes[i + 1] - planes[i]) * w
 
 
-def estimate(cfg, grid, fd="filter", td="average", compensate_cfo=False, numerology=1, crb_mask=None):
+def estimate(cfg, grid, fd="filter", td="average", compensate_cfo=False, numerology=1, crb_mask=None,
+             low_papr_id=None):
     """cfg: slot, scrambling_id, n_scid, dmrs_type2, scaling (beta), dmrs_symbol_mask, start_symbol, nof_symbols,
     rb_start, nof_rb, nof_rx_ports. grid (P, 14, nsc) complex. Returns (ch (P, 14, nsc) complex128 filled on the
     allocation, noise_var (P,), rsrp (P,), epre (P,), extra) with extra = dict(cfo_hz (P,) NaN when one DM-RS symbol,
@@ -250,7 +278,10 @@ def estimate(cfg, grid, fd="filter", td="average", compensate_cfo=False, numerol
     syms = [l for l in range(first, last) if (cfg["dmrs_symbol_mask"] >> l) & 1]
     Dn = len(syms)
     N = sc.size
-    pil = [dmrs_sequence(cfg["slot"], l, cfg["scrambling_id"], cfg["n_scid"], t2, rb0, nrb, rbs) for l in syms]
+    if low_papr_id is not None:
+        pil = [low_papr_sequence(low_papr_id % 30, len(rbs) * 6) for _ in syms]
+    else:
+        pil = [dmrs_sequence(cfg["slot"], l, cfg["scrambling_id"], cfg["n_scid"], t2, rb0, nrb, rbs) for l in syms]
     ep = symbol_start_epochs(numerology)
     scs_hz = (15 << numerology) * 1000.0
     nsc = grid.shape[2]

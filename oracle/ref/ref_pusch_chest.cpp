@@ -29,6 +29,7 @@ extern "C" {
 /// [port][14][12 * grid_nof_prb] bf16 pairs, and per port noise variance, RSRP, EPRE, time alignment (s), CFO (Hz or
 /// NaN).
 int ref_pusch_chest_mask(int             numerology,
+                    int             low_papr_id,
                     int             slot_index,
                     int             scrambling_id,
                     int             n_scid,
@@ -90,12 +91,19 @@ int ref_pusch_chest_mask(int             numerology,
 
   dmrs_pusch_estimator::configuration cfg;
   cfg.slot = slot_point(to_subcarrier_spacing(numerology), slot_index);
-  dmrs_pusch_estimator::pseudo_random_sequence_configuration seq;
-  seq.type          = dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1;
-  seq.nof_tx_layers = nof_layers;
-  seq.scrambling_id = scrambling_id;
-  seq.n_scid        = n_scid != 0;
-  cfg.sequence_config = seq;
+  if (low_papr_id >= 0) {
+    // Transform precoding: low-PAPR DM-RS sequence (dmrs_pusch_estimator_impl.cpp:77), type 1, one layer.
+    dmrs_pusch_estimator::low_papr_sequence_configuration lp;
+    lp.n_rs_id          = static_cast<unsigned>(low_papr_id);
+    cfg.sequence_config = lp;
+  } else {
+    dmrs_pusch_estimator::pseudo_random_sequence_configuration seq;
+    seq.type            = dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1;
+    seq.nof_tx_layers   = nof_layers;
+    seq.scrambling_id   = scrambling_id;
+    seq.n_scid          = n_scid != 0;
+    cfg.sequence_config = seq;
+  }
   cfg.scaling         = scaling;
   cfg.c_prefix        = cyclic_prefix::NORMAL;
   cfg.symbols_mask    = bounded_bitset<MAX_NSYMB_PER_SLOT>(14);
@@ -164,10 +172,20 @@ int ref_pusch_chest(int             numerology,
                     float*          ta_s,
                     float*          cfo_hz)
 {
-  return ref_pusch_chest_mask(numerology, slot_index, scrambling_id, n_scid, dmrs_type2, nof_layers, scaling,
+  return ref_pusch_chest_mask(numerology, -1, slot_index, scrambling_id, n_scid, dmrs_type2, nof_layers, scaling,
                               dmrs_symbol_mask, first_symbol, nof_symbols, rb_start, nof_rb, nullptr, grid_nof_prb,
                               nof_rx_ports, fd_strategy, td_strategy, compensate_cfo, grid_in, ch_est_out, noise_var,
                               rsrp, epre, ta_s, cfo_hz);
+}
+
+/// The reference's low-PAPR sequence r^(alpha, delta)_(u,v)(n) of length m (low_papr_sequence_generator_impl::generate
+/// with alpha = 0, the estimator's call): m complex floats.
+void ref_low_papr_generate(unsigned u, unsigned v, unsigned m, float* out)
+{
+  static low_papr_sequence_generator_impl gen;
+  std::vector<cf_t>                       seq(m);
+  gen.generate(seq, u, v, 0, 1);
+  std::memcpy(out, seq.data(), m * sizeof(cf_t));
 }
 
 } // extern "C"

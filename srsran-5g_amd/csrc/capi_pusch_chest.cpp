@@ -3,6 +3,7 @@
 // (port_channel_estimator_helpers.cpp filter_type, taps generated from the raised-cosine formula) and one job per
 // (transmission, rx port, CDM group).
 #include "capi_internal.h"
+#include "low_papr_tables.h"
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -18,6 +19,7 @@ struct srsgpu_pusch_chest_plan {
   chest_geom      geom       = {};  ///< Plan-wide maxima (LDS sizing).
   uint32_t*       d_seq      = nullptr;  ///< DM-RS sequence words of every job (plan lifetime).
   uint16_t*       d_crbs     = nullptr;  ///< CRB lists of the CRB-mask transmissions (relative to their first CRB).
+  float2*         d_lp       = nullptr;  ///< Low-PAPR DM-RS sequences of the transform-precoded transmissions.
 };
 
 namespace {
@@ -46,6 +48,54 @@ unsigned ta_dft_size(unsigned nof_re)
     size <<= 1;
   }
   return std::max(128u, size);
+}
+
+/// TS 38.211 section 5.2.2 low-PAPR base sequence of group u (v = 0, alpha = 0) and length m, as
+/// low_papr_sequence_generator_impl.cpp builds it: the phase tables for m = 6..24, the length-30 formula, and
+/// Zadoff-Chu of the largest prime N_ZC < m for m >= 36 with q = (int)(q_hat + 0.5), q_hat = (float) N_ZC (u + 1) / 31.
+/// Returns false for a length the specification does not define.
+bool low_papr_sequence(unsigned u, unsigned m, std::vector<float2>& out)
+{
+  std::vector<int> arg(m);
+  unsigned         nzc = 4;
+  const int8_t*    phi = m == 6 ? kLowPaprPhi6[u] : m == 12 ? kLowPaprPhi12[u] : m == 18 ? kLowPaprPhi18[u]
+                                                                  : m == 24 ? kLowPaprPhi24[u] : nullptr;
+  if (phi != nullptr) {
+    for (unsigned n = 0; n < m; ++n) {
+      arg[n] = phi[n];  // units of pi / 4 = pi / N_ZC with N_ZC = 4
+    }
+  } else if (m == 30) {
+    nzc = 31;
+    for (unsigned n = 0; n < m; ++n) {
+      arg[n] = -static_cast<int>(((u + 1ull) * (n + 1ull) * (n + 2ull)) % 62u);
+    }
+  } else if (m >= 36) {
+    nzc = m - 1;
+    auto prime = [](unsigned x) {
+      for (unsigned d = 2; d * d <= x; ++d) {
+        if (x % d == 0) {
+          return false;
+        }
+      }
+      return x > 1;
+    };
+    while (!prime(nzc)) {
+      --nzc;
+    }
+    const float   q_hat = static_cast<float>(nzc) * static_cast<float>(u + 1) / 31.f;
+    const int64_t q     = static_cast<int64_t>(static_cast<float>(static_cast<double>(q_hat) + 0.5));
+    for (unsigned n = 0; n < m; ++n) {
+      const int64_t mm = n % nzc;
+      arg[n]           = -static_cast<int>((q * mm * (mm + 1)) % (2 * nzc));
+    }
+  } else {
+    return false;
+  }
+  for (unsigned n = 0; n < m; ++n) {
+    const double a = 3.14159265358979323846 * static_cast<double>(arg[n]) / static_cast<double>(nzc);
+    out.push_back(make_float2(static_cast<float>(std::cos(a)), static_cast<float>(std::sin(a))));
+  }
+  return true;
 }
 
 } // namespace
@@ -80,6 +130,7 @@ int srsgpu_pusch_chest_plan_create_ex(srsgpu_context*                  ctx,
   const uint64_t         slot_elems = static_cast<uint64_t>(grid_nof_ports) * 14u * nsc;
   std::vector<chest_job> jobs;
   std::vector<uint16_t>  crb_lists;
+  std::vector<float2>    lp_table;
   for (uint32_t t = 0; t < nof_tx; ++t) {
     srsgpu_pusch_chest_config c = cfgs[t];
     const unsigned            L = c.nof_tx_layers, P = c.nof_rx_ports;
@@ -110,6 +161,21 @@ int srsgpu_pusch_chest_plan_create_ex(srsgpu_context*                  ctx,
     }
     const bool     masked  = !rel.empty();
     const unsigned span_rb = masked ? rel.back() + 1u : c.nof_rb;
+    // Transform precoding: the low-PAPR sequence of group n_RS_ID mod 30 over the allocation's pilots (type 1, one
+    // layer: dmrs_pusch_estimator.h get_dmrs_type / get_nof_tx_layers for low_papr_sequence_configuration).
+    uint32_t lp_base = CHEST_CONTIGUOUS;
+    if (c.dmrs_sequence > SRSGPU_DMRS_LOW_PAPR) {
+      return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid DM-RS sequence kind %u", t, c.dmrs_sequence);
+    }
+    if (c.dmrs_sequence == SRSGPU_DMRS_LOW_PAPR) {
+      if (L != 1 || c.dmrs_type != 1 || c.scrambling_id > 1007) {
+        return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: low-PAPR DM-RS takes one layer, type 1 and n_RS_ID <= 1007", t);
+      }
+      lp_base = static_cast<uint32_t>(lp_table.size());
+      if (!low_papr_sequence(c.scrambling_id % 30u, c.nof_rb * 6u, lp_table)) {
+        return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: no low-PAPR sequence of length %u", t, c.nof_rb * 6u);
+      }
+    }
     if (L < 1 || L > 4 || P < 1 || P > grid_nof_ports || (c.dmrs_type != 1 && c.dmrs_type != 2) || c.n_scid > 1) {
       return fail(SRSGPU_ERR_INVALID_ARG, "tx %u: invalid layers / ports / DM-RS type", t);
     }
@@ -270,6 +336,7 @@ int srsgpu_pusch_chest_plan_create_ex(srsgpu_context*                  ctx,
         jb.ta_positions = (t2 || masked) ? 1 : 0;
         jb.crb_list     = masked ? static_cast<uint32_t>(crb_lists.size()) : CHEST_CONTIGUOUS;
         jb.span_pilots  = static_cast<uint16_t>(span_rb * per_rb);
+        jb.lp_base      = lp_base;
         jobs.push_back(jb);
       }
     }
@@ -318,6 +385,13 @@ int srsgpu_pusch_chest_plan_create_ex(srsgpu_context*                  ctx,
     srsgpu_pusch_chest_plan_destroy(plan);
     return SRSGPU_ERR_HIP;
   }
+  if (!lp_table.empty() &&
+      (hipMalloc(&plan->d_lp, lp_table.size() * sizeof(float2)) != hipSuccess ||
+       hipMemcpy(plan->d_lp, lp_table.data(), lp_table.size() * sizeof(float2), hipMemcpyHostToDevice) !=
+           hipSuccess)) {
+    srsgpu_pusch_chest_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload low-PAPR sequences");
+  }
   if (!crb_lists.empty() &&
       (hipMalloc(&plan->d_crbs, crb_lists.size() * sizeof(uint16_t)) != hipSuccess ||
        hipMemcpy(plan->d_crbs, crb_lists.data(), crb_lists.size() * sizeof(uint16_t), hipMemcpyHostToDevice) !=
@@ -345,7 +419,7 @@ int srsgpu_pusch_chest_plan_execute(const srsgpu_pusch_chest_plan* plan,
   if (plan == nullptr || d_grids == nullptr || d_ch_estimates == nullptr || d_noise_var == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  launch_pusch_chest(plan->d_crbs, plan->d_jobs, plan->nof_jobs, plan->geom, d_grids, d_ch_estimates, d_noise_var, d_metrics,
+  launch_pusch_chest(plan->d_lp, plan->d_crbs, plan->d_jobs, plan->nof_jobs, plan->geom, d_grids, d_ch_estimates, d_noise_var, d_metrics,
                      plan->d_seq, static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
@@ -364,6 +438,9 @@ void srsgpu_pusch_chest_plan_destroy(srsgpu_pusch_chest_plan* plan)
   }
   if (plan->d_crbs != nullptr) {
     (void)hipFree(plan->d_crbs);
+  }
+  if (plan->d_lp != nullptr) {
+    (void)hipFree(plan->d_lp);
   }
   delete plan;
 }

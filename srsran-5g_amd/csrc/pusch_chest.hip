@@ -75,6 +75,11 @@ __device__ __forceinline__ cpx pilot(const uint32_t* seq, int W, int s, uint32_t
   return {((word >> sh) & 1u) ? -a : a, ((word >> (sh - 1)) & 1u) ? -a : a};
 }
 
+/// DM-RS value of pilot i (sequence position m) on DM-RS symbol s: the staged pseudo-random QPSK symbol, or the job's
+/// low-PAPR sequence value (transform precoding: the same sequence on every DM-RS symbol).
+__device__ __forceinline__ cpx dmrs_value(const chest_job& jb, const float2* __restrict__ lp, const uint32_t* seq,
+                                          int W, int s, uint32_t n0, int m, int i);
+
 /// compute_v_pilots on the lanes: lanes 0..nv-1 of the first half extrapolate the band start from E[VP .. VP+nv),
 /// lanes 32..32+nv-1 the band end from E[VP+N-nv .. VP+N): linear regression of |p| and the unwrapped arg over
 /// x = 0..nv-1, evaluated at x = -nv..-1 (start) or nv..2nv-1 (end).
@@ -156,6 +161,16 @@ __device__ __forceinline__ int pilot_seq_index(const chest_job& jb, const uint16
   return alloc_rb(jb, crbs, rb) * jb.pilots_per_rb + (i - rb * jb.pilots_per_rb);
 }
 
+__device__ __forceinline__ cpx dmrs_value(const chest_job& jb, const float2* __restrict__ lp, const uint32_t* seq,
+                                          int W, int s, uint32_t n0, int m, int i)
+{
+  if (jb.lp_base != CHEST_CONTIGUOUS) {
+    const float2 v = lp[jb.lp_base + static_cast<uint32_t>(i)];
+    return {v.x, v.y};
+  }
+  return pilot(seq, W, s, n0, m);
+}
+
 /// Maximum over the wavefront with the lowest index among equal values (srsvec::max_element keeps the first maximum).
 __device__ __forceinline__ void wave_argmax(float& v, int& idx)
 {
@@ -199,7 +214,8 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
     float* __restrict__ noise_var,
     float* __restrict__ metrics,
     const uint32_t* __restrict__ gseq,
-    const uint16_t* __restrict__ crbs)
+    const uint16_t* __restrict__ crbs,
+    const float2* __restrict__ lp)
 {
   extern __shared__ __align__(16) unsigned char lds_raw[];
   const int EN = geom.max_pilots + 2 * CHEST_VP;
@@ -243,7 +259,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
     const int      m = pilot_seq_index(jb, crbs, i);
     for (int s = 0; s < D; ++s) {
       const cpx y = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
-      const cpx p = pilot(L.seq, W, s, n0, m);
+      const cpx p = dmrs_value(jb, lp, L.seq, W, s, n0, m, i);
       L.Y[s * NP + i] = {y.x * p.x + y.y * p.y, y.y * p.x - y.x * p.y};
       epre_acc += y.x * y.x + y.y * y.y;
     }
@@ -370,7 +386,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
       const int      m = pilot_seq_index(jb, crbs, i);
       for (int s = 0; s < D; ++s) {
         const cpx y = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
-        cpx       q = cmul(h, pilot(L.seq, W, s, n0, m));
+        cpx       q = cmul(h, dmrs_value(jb, lp, L.seq, W, s, n0, m, i));
         if (rotate) {
           q = cmul(q, polar1(CHEST_TWOPI * jb.epochs[jb.dmrs_symbols[s]] * cfo));
         }
@@ -534,7 +550,8 @@ size_t pusch_chest_lds_bytes(const chest_geom& g)
          static_cast<size_t>(g.max_dmrs) * g.max_words * 4 + 32 * 4;
 }
 
-void launch_pusch_chest(const uint16_t* d_crbs,
+void launch_pusch_chest(const float2*   d_lp,
+                        const uint16_t* d_crbs,
                         const chest_job* d_jobs,
                         int              nof_jobs,
                         const chest_geom& geom,
@@ -551,7 +568,7 @@ void launch_pusch_chest(const uint16_t* d_crbs,
   const size_t lds = pusch_chest_lds_bytes(geom);
   hipLaunchKernelGGL(pusch_chest_kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(CHEST_THREADS),
                      static_cast<unsigned>(lds), stream, d_jobs, geom, d_grids, d_ce, d_noise_var, d_metrics, d_seq,
-                     d_crbs);
+                     d_crbs, d_lp);
 }
 
 } // namespace srsgpu

@@ -426,6 +426,9 @@ struct chest_job {
                              ///< list (pilots and estimates follow them); CHEST_CONTIGUOUS otherwise.
   uint16_t span_pilots;      ///< DM-RS sequence positions from the first to the last allocated CRB (staged words).
   uint16_t pad2;
+  uint32_t lp_base;          ///< Low-PAPR DM-RS (transform precoding): first pilot value of the job's sequence in the
+                             ///< plan's table (one complex float per pilot, every DM-RS symbol); CHEST_CONTIGUOUS: the
+                             ///< pseudo-random sequence words.
 };
 constexpr uint32_t CHEST_CONTIGUOUS = 0xffffffffu;
 
@@ -449,7 +452,8 @@ struct chest_geom {
 /// Dynamic LDS of the channel-estimator kernel for the plan's largest job.
 size_t pusch_chest_lds_bytes(const chest_geom& g);
 
-void launch_pusch_chest(const uint16_t* d_crbs,
+void launch_pusch_chest(const float2*   d_lp,
+                        const uint16_t* d_crbs,
                         const chest_job* d_jobs,
                         int              nof_jobs,
                         const chest_geom& geom,

@@ -275,7 +275,8 @@ class PuschChestConfig(ctypes.Structure):
         ("scaling", ctypes.c_float),
         ("grid_index", ctypes.c_uint32),
         ("numerology", ctypes.c_uint8),
-        ("pad", ctypes.c_uint8 * 3),
+        ("dmrs_sequence", ctypes.c_uint8),
+        ("pad", ctypes.c_uint8 * 2),
     ]
 
 
@@ -1196,6 +1197,10 @@ class PuschChannelEstimation:
     compensate_cfo: int = 0
     numerology: int = 1
     crb_mask: Optional[np.ndarray] = None
+    dmrs_sequence: int = 0  # DMRS_PSEUDO_RANDOM, or DMRS_LOW_PAPR (transform precoding: scrambling_id = n_RS_ID)
+
+
+DMRS_PSEUDO_RANDOM, DMRS_LOW_PAPR = 0, 1
 
 
 def make_pusch_chest_configs(ests: Sequence[PuschChannelEstimation], grid_index: Sequence[int]):
@@ -1208,6 +1213,7 @@ def make_pusch_chest_configs(ests: Sequence[PuschChannelEstimation], grid_index:
         a.estimate_layout, a.td_strategy, a.compensate_cfo = e.estimate_layout, e.td_strategy, e.compensate_cfo
         a.numerology = e.numerology
         a.fd_smoothing, a.scaling, a.grid_index = e.fd_smoothing, e.scaling, g
+        a.dmrs_sequence = e.dmrs_sequence
     return arr
 
 

@@ -185,6 +185,20 @@ def pusch_chest_cfo_cases():
         i += 1
 
 
+def pusch_chest_low_papr_cases():
+    """Yields (cfg dict, fd, td, compensate_cfo, n_RS_ID, grid (P, 14, 768, 2) bf16, reference estimates, [noise_var,
+    rsrp, epre, ta_s, cfo_hz] (5, P)) made by dmrs_pusch_estimator_impl with low-PAPR DM-RS (64-PRB grids)."""
+    d = _load("pusch_chest_low_papr.npz")
+    i = 0
+    while f"case{i}_cfg" in d:
+        row = d[f"case{i}_cfg"]
+        cfg = {k: int(v) for k, v in zip(PUSCH_CHEST_KEYS, row[:-4])}
+        cfg["scaling"] = float(d[f"case{i}_scaling"])
+        yield (cfg, int(row[-4]), int(row[-3]), int(row[-2]), int(row[-1]), d[f"case{i}_grid"],
+               d[f"case{i}_ch_est"], d[f"case{i}_stats"])
+        i += 1
+
+
 PDSCH_DMRS_KEYS = ["slot", "scrambling_id", "n_scid", "dmrs_type2", "nof_layers", "nof_ports", "dmrs_symbol_mask",
                    "reference_point_k_rb", "rb_start", "nof_rb"]
 

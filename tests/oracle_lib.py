@@ -243,8 +243,17 @@ class Reference(_Lib):
           *[_ptr(o) for o in outs], cap, _ptr(counts))
         return {k: o[:n] for k, o, n in zip(("sch", "harq", "csi1", "csi2"), outs, counts)}
 
+    def low_papr(self, u, v, m):
+        """low_papr_sequence_generator_impl::generate(sequence of m, u, v, 0, 1): complex64 (m,)."""
+        out = np.zeros(m, np.complex64)
+        f = self.lib.ref_low_papr_generate
+        f.restype = None
+        f.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, _P]
+        f(u, v, m, _ptr(out))
+        return out
+
     def pusch_chest(self, cfg, grid_u16, grid_nof_prb, fd=2, td=0, compensate_cfo=False, numerology=1,
-                    crb_mask=None):
+                    crb_mask=None, low_papr_id=-1):
         """dmrs_pusch_estimator_impl::estimate of one single-layer transmission: (ch_est (P, 14, nsc, 2) bf16,
         noise_var, rsrp, epre, ta_s, cfo_hz) per port. crb_mask (one byte per grid CRB) replaces the contiguous
         allocation as configuration::rb_mask."""
@@ -255,9 +264,9 @@ class Reference(_Lib):
         m = None if crb_mask is None else np.ascontiguousarray(np.asarray(crb_mask, np.uint8)[:grid_nof_prb])
         f = self.lib.ref_pusch_chest_mask
         f.restype = ctypes.c_int
-        f.argtypes = [ctypes.c_int] * 6 + [ctypes.c_float, ctypes.c_uint] + [ctypes.c_int] * 4 + [_P] + \
+        f.argtypes = [ctypes.c_int] * 7 + [ctypes.c_float, ctypes.c_uint] + [ctypes.c_int] * 4 + [_P] + \
             [ctypes.c_int] * 5 + [_P] * 7
-        f(numerology, cfg["slot"], cfg["scrambling_id"], cfg["n_scid"], cfg["dmrs_type2"], 1, cfg["scaling"],
+        f(numerology, int(low_papr_id), cfg["slot"], cfg["scrambling_id"], cfg["n_scid"], cfg["dmrs_type2"], 1, cfg["scaling"],
           cfg["dmrs_symbol_mask"], cfg["start_symbol"], cfg["nof_symbols"], cfg["rb_start"], cfg["nof_rb"],
           None if m is None else _ptr(m), grid_nof_prb, P, fd, td, int(compensate_cfo), _ptr(g), _ptr(ce),
           *[_ptr(o) for o in outs])

@@ -24,10 +24,11 @@ def random_crb_mask(rng, grid_prb, nof_rb=None):
 
 
 def random_case(rng, grid_prb, nof_rx_ports=None, nof_rb=None, dmrs_type2=None, snr_db=None, dmrs_mask=None,
-                cfo_hz=0.0, delay=0.0, numerology=1, crb_mask=None):
+                cfo_hz=0.0, delay=0.0, numerology=1, crb_mask=None, low_papr_id=None):
     """Returns (cfg, grid (P, 14, nsc, 2) bf16, true channel (P, nsc) complex). cfo_hz rotates OFDM symbol l by
     2 pi cfo t_l (t_l: the symbol's start epoch); delay (in samples of a 4096-point DFT, may be negative) shifts every
-    path. crb_mask: the DM-RS go to those CRBs (cfg rb_start / nof_rb = its first CRB / CRB count)."""
+    path. crb_mask: the DM-RS go to those CRBs (cfg rb_start / nof_rb = its first CRB / CRB count). low_papr_id: the
+    DM-RS is the low-PAPR sequence of group low_papr_id mod 30 (transform precoding, type 1)."""
     P = int(nof_rx_ports or rng.integers(1, 5))
     nrb = int(nof_rb or rng.integers(1, grid_prb + 1))
     rb0 = int(rng.integers(0, grid_prb - nrb + 1))
@@ -59,8 +60,11 @@ def random_case(rng, grid_prb, nof_rx_ports=None, nof_rb=None, dmrs_type2=None, 
     sc = np.array([rb * 12 + q for rb in rbs for q in pat])
     for l in range(14):
         if (dmrs_mask >> l) & 1:
-            x[l, sc] = cfg["scaling"] * C.dmrs_sequence(cfg["slot"], l, cfg["scrambling_id"], cfg["n_scid"], t2, rb0,
-                                                        nrb, rbs)
+            if low_papr_id is not None:
+                x[l, sc] = cfg["scaling"] * C.low_papr_sequence(low_papr_id % 30, sc.size)
+            else:
+                x[l, sc] = cfg["scaling"] * C.dmrs_sequence(cfg["slot"], l, cfg["scrambling_id"], cfg["n_scid"], t2,
+                                                            rb0, nrb, rbs)
     y = H[:, None, :] * x[None]
     if cfo_hz:
         ep = C.symbol_start_epochs(numerology)

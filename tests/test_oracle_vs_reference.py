@@ -372,6 +372,37 @@ def test_pusch_chest_crb_mask_oracle_vs_reference(ref, seed):
         assert not np.any(got[:, l, rbs[1] * 12:(rbs[1] + 1) * 12]), "the reference leaves the other CRBs unwritten"
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_pusch_chest_low_papr_oracle_vs_reference(ref, seed):
+    """Transform-precoding DM-RS (low-PAPR sequence of group n_RS_ID mod 30: phase tables, the length-30 formula and
+    Zadoff-Chu lengths, dmrs_pusch_estimator_impl.cpp:77) against the reference's estimator: estimates within
+    1.5e-2 / 2.5e-2 x RMS, noise variance / RSRP / EPRE 1e-3, CFO 0.05 Hz, TA 2 Tc."""
+    import pusch_chest_oracle as C
+    from ofdm_oracle import bf16_to_complex
+    from pusch_chest_cases import random_case
+    from pusch_demod_cases import valid_tp_prbs
+    rng = np.random.default_rng(1900 + seed)
+    nrb = int(rng.choice([1, 2, 3, 4, 5] + valid_tp_prbs(48)[5:]))
+    n_rs_id = int(rng.integers(0, 1008))
+    td = seed % 2
+    comp = seed % 3 != 0
+    cfg, grid, _ = random_case(rng, 48, nof_rb=nrb, dmrs_type2=0, cfo_hz=rng.uniform(-1500, 1500),
+                               delay=rng.uniform(-20, 20), low_papr_id=n_rs_id)
+    ce, nv, rsrp, epre, ta, cfo = ref.pusch_chest(cfg, grid, 48, fd=2, td=td, compensate_cfo=comp,
+                                                  low_papr_id=n_rs_id)
+    ch, nv_o, rsrp_o, epre_o, ex = C.estimate(cfg, bf16_to_complex(grid), td="interpolate" if td else "average",
+                                              compensate_cfo=comp, low_papr_id=n_rs_id)
+    ls = slice(cfg["start_symbol"], cfg["start_symbol"] + cfg["nof_symbols"])
+    ks = slice(cfg["rb_start"] * 12, (cfg["rb_start"] + cfg["nof_rb"]) * 12)
+    got, want = bf16_to_complex(ce)[:, ls, ks], ch[:, ls, ks]
+    assert np.max(np.abs(got - want)) < (2.5e-2 if td else 1.5e-2) * np.sqrt(np.mean(np.abs(want) ** 2)), cfg
+    np.testing.assert_allclose(nv, nv_o, rtol=1e-3)
+    np.testing.assert_allclose(rsrp, rsrp_o, rtol=1e-3)
+    np.testing.assert_allclose(epre, epre_o, rtol=1e-3)
+    np.testing.assert_allclose(ta, ex["ta_s"], atol=2 / (480000 * 4096))
+    np.testing.assert_allclose(cfo, ex["cfo_hz"], atol=0.05)
+
+
 @pytest.mark.parametrize("seed", range(24))
 def test_pusch_chest_cfo_ta_oracle_vs_reference(ref, seed):
     """CFO estimation (compensated and not), time alignment and the interpolate time strategy of the restatement against

@@ -359,3 +359,108 @@ def test_pusch_crb_mask_compact_cfo_chain(ctx):
                               bf16_to_complex(ce_ps[:1]).astype(np.complex64), nv_ps, crb_mask=mask)
     d = np.abs(outs[0].astype(np.int16) - want.astype(np.int16))
     assert d.max() <= 1 and np.mean(d > 0) < 0.01, (d.max(), np.mean(d > 0))
+
+
+def test_pusch_chest_low_papr_random_vs_oracle(ctx):
+    """Transform-precoding DM-RS (low-PAPR sequences: phase tables for 1-4 PRB, the length-30 formula, Zadoff-Chu)
+    in ONE plan with pseudo-random transmissions, against the restatement (pinned against the reference's estimator by
+    test_pusch_chest_low_papr_oracle_vs_reference): estimates, noise variance / RSRP, TA, CFO within the stated
+    tolerances."""
+    import srsgpu
+    from pusch_demod_cases import valid_tp_prbs
+    rng = np.random.default_rng(81)
+    sizes = [1, 2, 3, 4, 5] + valid_tp_prbs(100)[5:]
+    cases, opts, ids = [], [], []
+    for i in range(36):
+        lp = i % 4 != 3
+        nid = int(rng.integers(0, 1008)) if lp else None
+        cases.append(random_case(rng, 104, nof_rb=int(sizes[i % len(sizes)]), dmrs_type2=0,
+                                 cfo_hz=rng.uniform(-1500, 1500), delay=rng.uniform(-20, 20), low_papr_id=nid))
+        opts.append((int(rng.integers(0, 3)), i % 2, (i // 2) % 2))
+        ids.append(nid)
+    grids = np.stack([pad4(g) for _, g, _ in cases])
+    ests = []
+    for (cfg, _, _), (fd, td, comp), nid in zip(cases, opts, ids):
+        e = to_est(cfg, fd, 1, td, comp)
+        if nid is not None:
+            e.dmrs_sequence, e.scrambling_id = srsgpu.DMRS_LOW_PAPR, nid
+        ests.append(e)
+    ce, nv, m = srsgpu.PuschChannelEstimator(ctx, 104, 4).estimate_batch(grids, ests, list(range(len(cases))))
+    for i, ((cfg, grid, _), (fd, td, comp), nid) in enumerate(zip(cases, opts, ids)):
+        P = cfg["nof_rx_ports"]
+        ch, nvo, rsrp, epre, ex = C.estimate(cfg, bf16_to_complex(grid), ["none", "mean", "filter"][fd],
+                                             ["average", "interpolate"][td], bool(comp), low_papr_id=nid)
+        ls, ks = region(cfg)
+        got = bf16_to_complex(ce[i, 0, :P])[:, ls, ks]
+        w = ch[:, ls, ks]
+        assert np.max(np.abs(got - w)) < CFO_TOL[td] * np.sqrt(np.mean(np.abs(w) ** 2)), (i, cfg, fd, td, comp)
+        np.testing.assert_allclose(nv[i, :P], nvo, rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 0], rsrp, rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 4], ex["ta_s"], atol=2 * T_C)
+        np.testing.assert_allclose(m[i, :P, 5], ex["cfo_hz"], atol=0.05)
+
+
+def test_pusch_transform_precoding_receive_chain(ctx):
+    """DFT-s-OFDM PUSCH end to end on the GPU: a transform-precoded 64QAM transmission (data DFT-spread over the
+    allocation, low-PAPR DM-RS in symbols 2 and 11, frequency-selective channel, CFO, noise) through the estimator
+    (low-PAPR, CFO compensation) and the demodulator (transform precoding) matches the oracle chain: LLRs within one
+    step on >= 99 %, hard decisions of the clean data bits all correct."""
+    import torch
+    import srsgpu
+    from pusch_demod_cases import QAM_AMP, bf16
+    rng = np.random.default_rng(14)
+    dev = torch.device("cuda", 0)
+    G, nrb, rb0, P, qm, nid = 52, 12, 7, 4, 6, 321
+    mask = (1 << 2) | (1 << 11)
+    cfg, grid, H = random_case(rng, G, nof_rx_ports=P, nof_rb=nrb, dmrs_type2=0, dmrs_mask=mask, snr_db=30,
+                               low_papr_id=nid)
+    cfg.update(start_symbol=0, nof_symbols=14, rb_start=rb0)
+    # Rebuild the grid with DFT-spread 64QAM data on the non-DM-RS symbols and the DM-RS at the allocation.
+    nsc, M = 12 * G, 12 * nrb
+    lv = np.arange(-7, 8, 2) * QAM_AMP[qm]
+    x = np.zeros((14, nsc), np.complex128)
+    data = {}
+    for l in range(14):
+        sc = np.arange(rb0 * 12, rb0 * 12 + M)
+        if (mask >> l) & 1:
+            x[l, sc[0::2]] = cfg["scaling"] * C.low_papr_sequence(nid % 30, M // 2)
+        else:
+            d = rng.choice(lv, M) + 1j * rng.choice(lv, M)
+            data[l] = d
+            x[l, sc] = np.fft.fft(d) / np.sqrt(M)
+    y = H[:, None, :] * x[None]
+    y += (rng.normal(size=y.shape) + 1j * rng.normal(size=y.shape)) * np.sqrt(10 ** (-3.0) / 2)
+    grid = bf16(y)
+    est = srsgpu.PuschChannelEstimation(
+        scrambling_id=nid, n_scid=0, dmrs_type=1, nof_tx_layers=1, nof_rx_ports=P, start_symbol=0, nof_symbols=14,
+        dmrs_symbol_mask=mask, rb_start=rb0, nof_rb=nrb, slot_index=3, scaling=cfg["scaling"],
+        compensate_cfo=1, dmrs_sequence=srsgpu.DMRS_LOW_PAPR)
+    dem = srsgpu.PuschDemodulation(
+        rnti=0x4601, n_id=77, modulation_order=qm, nof_tx_layers=1, nof_rx_ports=P, start_symbol=0, nof_symbols=14,
+        dmrs_symbol_mask=mask, dmrs_type=1, nof_cdm_groups_without_data=2, rb_start=rb0, nof_rb=nrb,
+        transform_precoding=1)
+    g4 = torch.from_numpy(pad4(grid).view(np.int32).reshape(-1).copy()).to(dev)
+    eplan = srsgpu.PuschChannelEstimatorPlan(ctx, srsgpu.make_pusch_chest_configs([est], [0]), G, 4)
+    arr, _, total = srsgpu.make_pusch_demod_configs([dem], [0])
+    dplan = srsgpu.PuschDemodulatorPlan(ctx, arr, G, 4)
+    d_ce = torch.zeros(4 * 4 * 14 * nsc, dtype=torch.int32, device=dev)
+    d_nv = torch.zeros(4, dtype=torch.float32, device=dev)
+    d_llr = torch.zeros(total, dtype=torch.int8, device=dev)
+    eplan.execute(g4, d_ce, d_nv)
+    dplan.execute(g4, d_ce, d_nv, d_llr)
+    torch.cuda.synchronize()
+    got = d_llr.cpu().numpy()
+    ce = d_ce.cpu().numpy().view(np.uint16).reshape(4, 4, 14, nsc, 2)
+    dcfg = dict(rnti=0x4601, n_id=77, qm=qm, nof_layers=1, nof_rx_ports=P, start_symbol=0, nof_symbols=14,
+                dmrs_symbol_mask=mask, dmrs_type2=0, nof_cdm_groups_without_data=2, rb_start=rb0, nof_rb=nrb)
+    want, _ = D.demodulate_ex(dcfg, bf16_to_complex(pad4(grid)).astype(np.complex64),
+                              bf16_to_complex(ce[:1]).astype(np.complex64), d_nv.cpu().numpy(),
+                              transform_precoding=True)
+    d = np.abs(got.astype(np.int16) - want.astype(np.int16))
+    assert d.max() <= 1 and np.mean(d > 0) < 0.01, (d.max(), np.mean(d > 0))
+    # Descramble and compare the hard decisions with the sent 64QAM symbols.
+    c = D.gold_sequence(0x4601 * (1 << 15) + 77, got.size)
+    llr = np.where(c == 1, -got.astype(np.int16), got.astype(np.int16))
+    sent = np.concatenate([data[l] for l in sorted(data)])
+    hard = D.modulate_bits((llr <= 0).astype(np.uint8), qm)
+    assert np.mean(np.abs(hard - sent.astype(np.complex64)) > 1e-3) < 1e-3

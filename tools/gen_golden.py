@@ -290,6 +290,26 @@ def gen_pusch_chest_cfo(ref, rng):
     np.savez_compressed(os.path.join(OUT, "pusch_chest_cfo.npz"), **out)
 
 
+def gen_pusch_chest_low_papr(ref, rng):
+    """Reference DM-RS channel estimates of transform-precoded PUSCH (low-PAPR DM-RS, n_RS_ID), 1..48 PRB (phase-table,
+    length-30 and Zadoff-Chu sequences), du_low defaults (filter, average, CFO compensation) and interpolate."""
+    from pusch_chest_cases import random_case
+    out = {}
+    for i, nrb in enumerate([1, 2, 3, 4, 5, 6, 10, 16, 24, 48]):
+        td, comp, nid = i % 2, int(i % 3 != 2), int(rng.integers(0, 1008))
+        cfg, grid, _ = random_case(rng, 64, nof_rb=nrb, dmrs_type2=0, dmrs_mask=(1 << 2) | (1 << 11),
+                                   cfo_hz=float(rng.uniform(-1500, 1500)), delay=float(rng.uniform(-25, 25)),
+                                   low_papr_id=nid)
+        cfg["start_symbol"], cfg["nof_symbols"] = 0, 14
+        ce, nv, rsrp, epre, ta, cfo = ref.pusch_chest(cfg, grid, 64, fd=2, td=td, compensate_cfo=bool(comp),
+                                                      low_papr_id=nid)
+        out[f"case{i}_cfg"] = np.array([cfg[k] for k in PUSCH_CHEST_KEYS] + [2, td, comp, nid], np.int64)
+        out[f"case{i}_scaling"] = np.float32(cfg["scaling"])
+        out[f"case{i}_grid"], out[f"case{i}_ch_est"] = grid, ce
+        out[f"case{i}_stats"] = np.stack([nv, rsrp, epre, ta, cfo])
+    np.savez_compressed(os.path.join(OUT, "pusch_chest_low_papr.npz"), **out)
+
+
 def gen_pdsch_dmrs(ref, rng):
     """Reference PDSCH DM-RS grids (dmrs_pdsch_processor_impl) of random configurations in 24-PRB grids."""
     from pdsch_dmrs_cases import random_config
@@ -363,7 +383,7 @@ def main():
     if len(sys.argv) > 1:  # regenerate only the named fixture sets, e.g. `python tools/gen_golden.py ofdm`
         for name in sys.argv[1:]:
             seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18, "pdsch_dmrs": 19, "pusch_chest_cfo": 20,
-                    "pdsch_mod_general": 21, "pdsch_dmrs_mask": 22, "pusch_demod_general": 23, "ulsch_demux": 24}[name]
+                    "pdsch_mod_general": 21, "pdsch_dmrs_mask": 22, "pusch_demod_general": 23, "ulsch_demux": 24, "pusch_chest_low_papr": 25}[name]
             globals()["gen_" + name](ref, np.random.default_rng(seed))
         return
     gen_crc(ref, np.random.default_rng(10))
@@ -381,6 +401,7 @@ def main():
     gen_pdsch_dmrs_mask(ref, np.random.default_rng(22))
     gen_pusch_demod_general(ref, np.random.default_rng(23))
     gen_ulsch_demux(ref, np.random.default_rng(24))
+    gen_pusch_chest_low_papr(ref, np.random.default_rng(25))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

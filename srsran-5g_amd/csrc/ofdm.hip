@@ -77,13 +77,40 @@ __device__ __forceinline__ void dft_reg(float2* v)
 }
 
 /// Twiddles W^(r k) = exp(S 2 pi i r k / (NS R)), r = 1..R-1, of the butterflies this thread runs in a pass with
-/// radix R after passes of total radix NS (k = j mod NS); the table holds exp(-2 pi i m / OFDM_MAX_DFT). Loaded at
+/// radix R after passes of total radix NS (k = j mod NS); the table holds exp(-2 pi i m / OFDM_MAX_DFT). Computed at
 /// kernel start for every pass, so their L2 latency hides under the first pass's HBM loads.
 template <int N, int R, int NS, int S>
 __device__ __forceinline__ void load_twiddles(const float2* __restrict__ tw, float2 (&w)[16 / R][R])
 {
   constexpr int T   = N / 16;
   const int     tid = static_cast<int>(threadIdx.x);
+  if constexpr (R == 16) {
+    // W^k from the table (the lanes' k are consecutive, so the gather touches few cache lines; W^(r k) for all r
+    // touched up to 64 lines per instruction in the last pass), W^2k, W^4k, W^8k by squaring and the other powers by
+    // at most three complex products (relative error < 1e-6).
+    const int k  = tid & (NS - 1);
+    auto      at = [&](int r) {
+      float2 x = tw[(r * k) * static_cast<int>(OFDM_MAX_DFT / (NS * R))];
+      if constexpr (S > 0) {
+        x.y = -x.y;
+      }
+      return x;
+    };
+    float2(&v)[R] = w[0];
+    v[1]          = at(1);
+    v[2]          = cmul(v[1], v[1]);
+    v[4]          = cmul(v[2], v[2]);
+    v[8]          = cmul(v[4], v[4]);
+    v[3]          = cmul(v[1], v[2]);
+    v[5]          = cmul(v[4], v[1]);
+    v[6]          = cmul(v[4], v[2]);
+    v[7]          = cmul(v[4], v[3]);
+#pragma unroll
+    for (int r = 9; r < 16; ++r) {
+      v[r] = cmul(v[8], v[r - 8]);
+    }
+    return;
+  }
 #pragma unroll
   for (int b = 0; b < 16 / R; ++b) {
     const int k = (tid + b * T) & (NS - 1);
@@ -143,6 +170,7 @@ __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ 
   constexpr int REM  = LOG2N % 4;
   constexpr int R0   = REM ? (1 << REM) : 16;
   constexpr int NP   = LOG2N / 4 + (REM ? 1 : 0);
+  // (Padding the layout against the first pass's strided stores measured slower: the transform is latency-bound.)
   auto          ld   = [lds](int i) { return lds[i]; };
   auto          st   = [lds](int i, float2 v) { lds[i] = v; };
   static_assert(NP >= 2 && NP <= 4, "supported DFT sizes: 256..8192");

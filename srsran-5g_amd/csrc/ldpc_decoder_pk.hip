@@ -74,6 +74,36 @@ __device__ __forceinline__ u16x2 not_argmin(u16x2 idx, int e, u16x2 one)
   return __builtin_elementwise_min(idx - uu(e), one);  // v_pk_sub_u16 with e inline and op_sel_hi broadcast
 }
 
+/// Opaque packed multipliers 32 and 512: with a visible power of two the compiler splits a multiply-add into a
+/// shift and an add / or (two VALU instead of one v_pk_mad).
+struct pk_consts {
+  u16x2 k32;
+  s16x2 k512;
+};
+__device__ __forceinline__ pk_consts make_pk_consts()
+{
+  uint32_t a = 0x00200020u, b = 0x02000200u;
+  asm("" : "+v"(a), "+v"(b));
+  return {as_u16(a), as_s16(b)};
+}
+
+/// v2c of an edge from its soft bit sb and previous c2v magnitude om with sign mask n (0 / -1):
+/// clamp(sb - c2v, +/-LLR_MAX), plus +/-512 for an infinite soft bit (|v2c| >= 392 stays infinite). sb - c2v is one
+/// multiply-add on -(n | 1) = ~n | 1.
+__device__ __forceinline__ s16x2 v2c_pk(s16x2 sb, u16x2 om, s16x2 n, const pk_consts& kc)
+{
+  const s16x2 nn  = as_s16(~bits(n) | 0x00010001u);
+  const s16x2 t   = as_s16(bits(om)) * nn + sb;
+  const s16x2 fin = __builtin_elementwise_min(__builtin_elementwise_max(sb, ss(-LLR_MAX)), ss(LLR_MAX));
+  return (sb - fin) * kc.k512 + __builtin_elementwise_min(__builtin_elementwise_max(t, ss(-LLR_MAX)), ss(LLR_MAX));
+}
+
+/// Search key |v| * 32 + e of the two-minimum scan (one v_pk_mad).
+__device__ __forceinline__ u16x2 key_pk(s16x2 v, int e, const pk_consts& kc)
+{
+  return __builtin_bit_cast(u16x2, __builtin_elementwise_max(v, -v)) * kc.k32 + uu(e);
+}
+
 __device__ __forceinline__ s16x2 clamp2(s16x2 v, int lo, int hi)
 {
   return __builtin_elementwise_min(__builtin_elementwise_max(v, ss(lo)), ss(hi));
@@ -142,7 +172,8 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   uint32_t    sx = 0;
   uint32_t    one_bits = 0x00010001u;
   asm("" : "+v"(one_bits));
-  const u16x2 one = as_u16(one_bits);
+  const u16x2     one = as_u16(one_bits);
+  const pk_consts kc  = make_pk_consts();
 
   uint32_t addr[KEEP_ADDR ? deg : 1];
   static_for<deg>([&](auto E) {
@@ -165,12 +196,10 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     const s16x2    n   = (as_s16(sw) << ss(15 - pos)) >> ss(15);
     const u16x2    ne  = not_argmin(IDX, e, one);
     const u16x2    om  = ne * D + S2;
-    const s16x2    c   = as_s16(bits(om) ^ bits(n)) - n;
     // v2c = soft - c2v saturated to +/-LLR_MAX; infinite soft bits give |v2c| >= 392 (stay infinite).
-    const s16x2 fin = clamp2(sb, -LLR_MAX, LLR_MAX);
-    const s16x2 v   = clamp2(sb - c, -LLR_MAX, LLR_MAX) + (sb - fin) * ss(512);
+    const s16x2 v   = v2c_pk(sb, om, n, kc);
     v2c[e]          = v;
-    const u16x2 key = __builtin_bit_cast(u16x2, __builtin_elementwise_max(v, -v)) * uu(32) + uu(e);
+    const u16x2 key = key_pk(v, e, kc);
     k2              = __builtin_elementwise_min(__builtin_elementwise_max(key, k1), k2);
     k1              = __builtin_elementwise_min(key, k1);
     sx ^= bits(v);
@@ -271,8 +300,9 @@ __device__ __forceinline__ void pass1_half(const int8_t* __restrict__ soft,
   const u16x2 IDX = as_u16(sgw) >> uu(11);
   uint32_t    one_bits = 0x00010001u;
   asm("" : "+v"(one_bits));
-  const u16x2 one = as_u16(one_bits);
-  st.k1           = uu(KEY_INIT);
+  const u16x2     one = as_u16(one_bits);
+  const pk_consts kc  = make_pk_consts();
+  st.k1               = uu(KEY_INIT);
   st.k2           = uu(KEY_INIT);
   st.sx           = 0;
   static_for<EE - EB>([&](auto E) {
@@ -286,11 +316,9 @@ __device__ __forceinline__ void pass1_half(const int8_t* __restrict__ soft,
     const s16x2 n   = (as_s16(sgw) << ss(15 - j)) >> ss(15);
     const u16x2 ne  = not_argmin(IDX, e, one);
     const u16x2 om  = ne * D + S2;
-    const s16x2 c   = as_s16(bits(om) ^ bits(n)) - n;
-    const s16x2 fin = clamp2(sb, -LLR_MAX, LLR_MAX);
-    const s16x2 v   = clamp2(sb - c, -LLR_MAX, LLR_MAX) + (sb - fin) * ss(512);
+    const s16x2 v   = v2c_pk(sb, om, n, kc);
     st.v2c[j]       = v;
-    const u16x2 key = __builtin_bit_cast(u16x2, __builtin_elementwise_max(v, -v)) * uu(32) + uu(e);
+    const u16x2 key = key_pk(v, e, kc);
     st.k2           = __builtin_elementwise_min(__builtin_elementwise_max(key, st.k1), st.k2);
     st.k1           = __builtin_elementwise_min(key, st.k1);
     st.sx ^= bits(v);
@@ -458,16 +486,24 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
         const uint32_t i0 = static_cast<uint32_t>(16 * w) - head;
         const uint32_t c0 = __umulhi(i0, d.div_magic);
         const uint32_t l0 = i0 - c0 * static_cast<uint32_t>(Z);
-        const bool     one_half   = (l0 + 16u <= H) || (l0 >= H && l0 + 16u <= static_cast<uint32_t>(Z));
-        const bool     short_path = (16u * static_cast<uint32_t>(w) >= head) && (i0 + 16u <= full) && one_half;
+        // Short path: the 16 LLRs lie in one column (every vector but the unaligned head and the input's tail). A
+        // vector may straddle the column's half boundary H: byte k >= H - l0 goes to 2 (l - H) + 1 instead of 2 l,
+        // i.e. its address moves by 1 - 2H (one bit-extract and one 24-bit multiply-add per byte, no branch), so a
+        // wave's straddling lane does not drag the whole wave through the per-byte general path.
+        const bool short_path = (16u * static_cast<uint32_t>(w) >= head) && (i0 + 16u <= full) &&
+                                (l0 + 16u <= static_cast<uint32_t>(Z));
         if (short_path) {
-          int8_t* dst = soft + (c0 + 2) * SOFT_COL_STRIDE + pair_pos(l0, H);
+          int8_t*        dst   = soft + (c0 + 2) * SOFT_COL_STRIDE + pair_pos(l0, H);
+          const uint32_t cross = (l0 < H && l0 + 16u > H) ? (0xffffu << (H - l0)) : 0u;  // bit k: byte k moves
+          const int      adj   = 1 - 2 * static_cast<int>(H);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-              dst[2 * (4 * q + k)] = static_cast<int8_t>(clamp_i(static_cast<int8_t>(word >> (8 * k)), -64, 64));
+              const int kk  = 4 * q + k;
+              const int mv  = static_cast<int>((cross >> kk) & 1u) * adj;
+              dst[2 * kk + mv] = static_cast<int8_t>(clamp_i(static_cast<int8_t>(word >> (8 * k)), -64, 64));
             }
           }
           if ((val[j].x | val[j].y | val[j].z | val[j].w) != 0u) {

@@ -445,8 +445,21 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
   const int      K   = G::K;
   const int      nkb = K * Z / 8;  // message bytes
   const int      tid = static_cast<int>(threadIdx.x);
-  for (int e = tid; e < G::NE; e += PK_THREADS) {
-    edge[e] = (static_cast<uint32_t>(G::col(e)) << 16) | shift_table[static_cast<uint32_t>(d.zpos) * G::NE + e];
+  {
+    // Every lane's table loads in flight at once, then the stores (a rolled loop waits for each load in turn).
+    constexpr int NEL = (G::NE + PK_THREADS - 1) / PK_THREADS;
+    uint32_t      ev[NEL];
+#pragma unroll
+    for (int r = 0; r < NEL; ++r) {
+      const int e = tid + r * PK_THREADS < G::NE ? tid + r * PK_THREADS : G::NE - 1;
+      ev[r]       = (static_cast<uint32_t>(G::col(e)) << 16) | shift_table[static_cast<uint32_t>(d.zpos) * G::NE + e];
+    }
+#pragma unroll
+    for (int r = 0; r < NEL; ++r) {
+      if (tid + r * PK_THREADS < G::NE) {
+        edge[tid + r * PK_THREADS] = ev[r];
+      }
+    }
   }
   for (int m = tid; m <= G::M; m += PK_THREADS) {
     row_start[m] = static_cast<uint16_t>(G::rs(m));
@@ -466,13 +479,31 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
                                   static_cast<int>(t.order), t.poly, lut, red);
   }
   const int nd8 = d.nof_data / 8;
-  for (int q = tid; q < nkb; q += PK_THREADS) {
-    uint32_t byte = 0;
-    if (q < nd8) {
-      const uint32_t p = d.tb_bit_offset + 8u * static_cast<uint32_t>(q);
-      byte = (p < d.tb_bits) ? tb[p >> 3] : (tb_crc >> (d.tb_crc_len - 8u - (p - d.tb_bits))) & 0xffu;
+  {
+    // All of a lane's message bytes are loaded before any is stored (the loads in flight together; the address is
+    // clamped into the TB so the loads are unconditional).
+    constexpr int  MB    = (G::K * 384 / 8 + PK_THREADS - 1) / PK_THREADS;
+    const uint32_t tb_hi = d.tb_bits >= 8u ? (d.tb_bits - 8u) >> 3 : 0u;
+    uint32_t       byte[MB];
+#pragma unroll
+    for (int r = 0; r < MB; ++r) {
+      const int      q  = tid + r * PK_THREADS;
+      const uint32_t p  = d.tb_bit_offset + 8u * static_cast<uint32_t>(q);
+      const uint32_t pb = p >> 3;
+      byte[r]           = (q < nd8) ? tb[pb < tb_hi ? pb : tb_hi] : 0u;
     }
-    msg[q] = static_cast<uint8_t>(byte);
+#pragma unroll
+    for (int r = 0; r < MB; ++r) {
+      const int q = tid + r * PK_THREADS;
+      if (q < nkb) {
+        const uint32_t p = d.tb_bit_offset + 8u * static_cast<uint32_t>(q);
+        uint32_t       b = byte[r];
+        if (q < nd8 && p >= d.tb_bits) {
+          b = (tb_crc >> (d.tb_crc_len - 8u - (p - d.tb_bits))) & 0xffu;
+        }
+        msg[q] = static_cast<uint8_t>(b);
+      }
+    }
   }
   if (d.crc_table != NO_CRC_TABLE) {
     crc_byte_lut(lut, 24, 0x1800063u);  // CRC24B; ends with a barrier

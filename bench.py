@@ -414,7 +414,11 @@ def main():
     if os.path.exists(sqfile):
         with open(sqfile) as f:
             sqj = json.load(f)
-        sq = sqj.get("kernels", {}).get("ldpc_decode_pk_kernel<1, 1, 8>") if sqj.get("workload") == wl_key else None
+        # The BG1 / MODE 1 / 8-layer decoder of this workload (plain or edge-split variant).
+        sq = None
+        if sqj.get("workload") == wl_key:
+            sq = next((v for k, v in sqj.get("kernels", {}).items() if k.startswith("ldpc_decode_pk_kernel<1, 1, 8")),
+                      None)
         if sq:
             peak = 1024 * 2.4e9 / 2  # SIMDs x clock / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md)
             rate = sq["valu_instr"] / (dec_ms * 1e-3)
@@ -497,7 +501,7 @@ def main():
         "stage_ms_per_step": stage,  # from an untimed eager pass with per-stage events
         "stage_algorithmic_gbps": stage_gbps,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "ldpc_decode_pk_kernel<1,1,8>",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "ldpc_decode_pk_kernel<1,1,8,2>",
                      "kernel_ms_per_launch": dec_ms, "algorithmic_bytes_per_launch": dec_bytes,
                      "note": "algorithmic bytes per launch / decoder-stage HIP-event time on the launch stream (an "
                              "eager pass right after the timed loop); the LDPC decoder is VALU-issue/latency-bound, "

@@ -29,6 +29,13 @@ so the timed loop streams a working set larger than the 256 MB Infinity Cache. O
 plus `--extra-points` (a clean 35 dB link and the worst case: Gaussian noise, every codeblock runs all iterations,
 like the reference's ldpc_decoder benchmark) timed the same way.
 
+Workloads (--workload):
+  * "multi_ue" (default, the headline): the 64-UE slot above, `--slots-per-step` slots per step in each direction.
+  * "testmode": configs[4], the du_low test mode's traffic - one test UE owning all 273 PRB in every slot (max TBS:
+    MCS 27, 4 DL layers), continuous slots of the du_high default TDD pattern DDDDDDSUUU (6 DL slots, a special slot
+    with an 8-symbol PDSCH, 3 UL slots); a step is `--periods` TDD periods, value counts every slot of the pattern.
+    Fresh DL payloads every step (drawn on the GPU inside the captured graph); the UL payloads differ per input set.
+
 Weak scaling (--shard cells): every rank processes its own cells' slots; the decoded UL TBs + CRC flags of all ranks are
 gathered to rank 0 (the FAPI rank) over RCCL once per step. Strong scaling (--shard ues): the 64 UEs of every slot are
 split across the ranks (srsgpu.dist.shard_ues); each rank runs the upper PHY of its UEs (the OFDM stages of the cell
@@ -77,7 +84,8 @@ def host_cores():
     return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
 
 
-def cpu_baseline(dl_ues, dl_segs, ul_ues, ul_segs, tb_host, cw_host, samples_host, iterations, budget_s, cores):
+def cpu_baseline(dl_ues, dl_segs, ul_ues, ul_segs, tb_host, cw_host, samples_host, iterations, budget_s, cores,
+                 tdd=None):
     """The srsRAN reference built from its own sources (oracle/_ref) on `cores` host threads, each running whole slots
     end to end with its own reference objects (slot-level parallelism: the best throughput the CPU path reaches on this
     workload): PDSCH encoding of the 64 DL TBs (pdsch_encoder_impl: segmenter + AVX2 LDPC encoder + rate matcher),
@@ -85,6 +93,9 @@ def cpu_baseline(dl_ues, dl_segs, ul_ues, ul_segs, tb_host, cw_host, samples_hos
     demodulation of 4 ports, per-UE DM-RS channel estimation (filter, average, CFO compensation) + PUSCH demodulation
     (single-layer ZF 1 x 4) of the same samples the GPU receives, and the PUSCH codeblock tasks (rate dematcher +
     LDPC decoder with CRC early stop, the implementations "auto" picks here) on the reference's own LLRs.
+    `tdd` = (DL slots, UL slots) per TDD period (testmode): every thread still runs one DL and one UL slot per
+    iteration; the period rate follows from the measured per-slot DL / UL shares (the special slot costed as a full DL
+    slot, which favours the GPU's side of the ratio slightly less than the real 8-symbol PDSCH would).
     Returns (baseline dict, reference UL LLRs of slot 0)."""
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libsrsref.so")
     if not os.path.exists(ref_so):
@@ -164,8 +175,13 @@ def cpu_baseline(dl_ues, dl_segs, ul_ues, ul_segs, tb_host, cw_host, samples_hos
     slots = sum(st["slots"] for st in states)
     tt = sum(st["t"] for st in states) / slots * 1e-6  # ms per slot per thread, per stage
     it = float(np.mean([x for st in states for x in st["it"]]))
-    base = {"value": slots / wall, "unit": "slots/s", "cores": cores, "kind": "reference",
-            "sample": f"{slots} slots in {wall:.1f} s on {cores} host threads, each running whole slots (64 UEs) "
+    value = slots / wall
+    if tdd is not None:
+        t_dl, t_ul = tt[0] + tt[1], tt[3] + tt[6]
+        value = sum(tdd) / ((tdd[0] * t_dl + tdd[1] * t_ul) / (t_dl + t_ul) / value)
+    base = {"value": value, "unit": "slots/s", "cores": cores, "kind": "reference",
+            "sample": (f"TDD rate from {tdd[0]} DL + {tdd[1]} UL slots per period; " if tdd else "") +
+                      f"{slots} DL+UL slot pairs in {wall:.1f} s on {cores} host threads, each running whole slots ({len(dl_ues)} UEs) "
                       f"through the srsRAN reference with its own objects; per slot and thread: PDSCH encode "
                       f"{tt[0]:.2f} ms (avx2 encoder), PDSCH DM-RS + modulation {tt[1] - tt[2]:.2f} ms + OFDM "
                       f"modulation {tt[2]:.2f} ms (generic DFT), OFDM demodulation {tt[4]:.2f} ms + channel "
@@ -178,13 +194,18 @@ def cpu_baseline(dl_ues, dl_segs, ul_ues, ul_segs, tb_host, cw_host, samples_hos
 
 class InputSet:
     """One independent copy of a step's working set: DL / UL pipelines (plans + buffers), DL TBs, UL samples and the
-    UL TBs the UEs sent. Sets are rotated step by step."""
+    UL TBs the UEs sent. Sets are rotated step by step. `dl_cells`: the DL slot groups of a step (one, or a TDD
+    period's full and special slots), run as one DownlinkGroup."""
 
-    def __init__(self, ctx, dl_cell, ul_cell, prof, iterations, gen, dev):
-        self.dl = slotlib.DownlinkPipeline(ctx, dl_cell)
+    def __init__(self, ctx, dl_cells, ul_cell, prof, iterations, gen, dev, fresh_tbs=False):
+        self.dls = [slotlib.DownlinkPipeline(ctx, c) for c in dl_cells]
+        self.dl = self.dls[0]
         self.ul = slotlib.UplinkPipeline(ctx, ul_cell, iterations=iterations, equalizer=prof["equalizer"],
                                          compensate_cfo=True)
-        self.dl_tbs = torch.randint(0, 256, (self.dl.tb_total,), generator=gen, device=dev, dtype=torch.uint8)
+        self.dl_tbs_all = [torch.randint(0, 256, (d.tb_total,), generator=gen, device=dev, dtype=torch.uint8)
+                           for d in self.dls]
+        self.dl_tbs = self.dl_tbs_all[0]
+        self.dl_group = slotlib.DownlinkGroup(self.dls, self.dl_tbs_all, fresh_tbs=fresh_tbs)
         self.ul_tbs_tx = torch.randint(0, 256, (sum(self.ul.tb_bytes),), generator=gen, device=dev,
                                        dtype=torch.uint8)
         self.samples = torch.zeros(2 * self.ul.ofdm.nof_samples, dtype=torch.float32, device=dev)
@@ -197,6 +218,8 @@ def main():
     ap.add_argument("--steps", type=int, default=4000)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--profile", choices=sorted(PROFILES), default="ref")
+    ap.add_argument("--workload", choices=["multi_ue", "testmode"], default="multi_ue")
+    ap.add_argument("--periods", type=int, default=2, help="testmode: TDD periods (10 slots each) per step")
     ap.add_argument("--slots-per-step", type=int, default=16)
     ap.add_argument("--input-sets", type=int, default=4, help="independent working sets rotated step by step")
     ap.add_argument("--iterations", type=int, default=6)
@@ -232,17 +255,30 @@ def main():
 
     dl_all = sch.slot_100mhz_4x4(nof_layers=4, nof_dmrs_symbols=2)
     ul_all = sch.slot_100mhz_4x4(nof_layers=prof["ul_layers"], nof_dmrs_symbols=2)
-    if args.shard == "ues" and world > 1:
+    testmode = args.workload == "testmode"
+    if testmode and args.shard == "ues" and world > 1:
+        raise SystemExit("--workload testmode has one UE per slot: --shard ues does not apply")
+    if testmode:
+        dl_cell, sp_cell, ul_cell = slotlib.tdd_testmode_cells(args.periods, 4, prof["ul_layers"])
+        dl_cells = [dl_cell, sp_cell]
+        dl_ues, ul_ues, dl_segs, ul_segs = dl_cell.ues, ul_cell.ues, dl_cell.segs, ul_cell.segs
+    elif args.shard == "ues" and world > 1:
         from srsgpu import dist as sdist
         dl_ues, ul_ues = sdist.shard_ues(dl_all, world, rank), sdist.shard_ues(ul_all, world, rank)
         rb_first = sum(u.n_prb for u in dl_all[:sdist.shard_range(len(dl_all), world, rank).start])
     else:
         dl_ues, ul_ues, rb_first = dl_all, ul_all, 0
-    dl_segs = [u.segmentation() for u in dl_ues]
-    ul_segs = [u.segmentation() for u in ul_ues]
-    dl_cell = slotlib.CellSlots(dl_ues, dl_segs, S, dmrs_mask=DMRS_MASK, rb_first=rb_first)
-    ul_cell = slotlib.CellSlots(ul_ues, ul_segs, S, dmrs_mask=DMRS_MASK, rb_first=rb_first)
-    sets = [InputSet(ctx, dl_cell, ul_cell, prof, args.iterations, gen, dev) for _ in range(K)]
+    if not testmode:
+        dl_segs = [u.segmentation() for u in dl_ues]
+        ul_segs = [u.segmentation() for u in ul_ues]
+        dl_cell = slotlib.CellSlots(dl_ues, dl_segs, S, dmrs_mask=DMRS_MASK, rb_first=rb_first)
+        ul_cell = slotlib.CellSlots(ul_ues, ul_segs, S, dmrs_mask=DMRS_MASK, rb_first=rb_first)
+        dl_cells = [dl_cell]
+    # Slots a step processes (value's unit): a TDD period's slots in testmode, else the slots of each direction.
+    slots_per_step = args.periods * slotlib.TDD_PERIOD if testmode else S
+    S_ul = ul_cell.nof_slots
+    S_dl = sum(c.nof_slots for c in dl_cells)
+    sets = [InputSet(ctx, dl_cells, ul_cell, prof, args.iterations, gen, dev, fresh_tbs=testmode) for _ in range(K)]
 
     def fill_samples(snr_db, worst):
         for k, st in enumerate(sets):
@@ -266,7 +302,7 @@ def main():
         cur = torch.cuda.current_stream(dev)
         dl_stream.wait_stream(cur)
         ul_stream.wait_stream(cur)
-        st.dl.execute(st.dl_tbs, dl_stream, ev_dl)
+        st.dl_group.execute(dl_stream, ev_dl)
         st.ul.execute(st.samples, ul_stream, ev_ul)
         cur.wait_stream(dl_stream)
         cur.wait_stream(ul_stream)
@@ -336,8 +372,9 @@ def main():
 
     elapsed = timed(args.steps)
     tb_success, avg_iters = ul_results(not args.worst_case)
-    slots = S * (world if args.shard == "cells" else 1) * args.steps
-    value = slots / elapsed
+    agg = world if args.shard == "cells" else 1  # ranks whose slots add up (weak scaling)
+    step_rate = agg * args.steps / elapsed       # steps/s of the whole job
+    value = slots_per_step * step_rate
 
     # Roofline kernel time: an eager pass over the sets with the decoder plans' own stage events (the decoding launch
     # on its stream), right after the timed loop.
@@ -382,8 +419,7 @@ def main():
                 step(i)
             e = timed(args.point_steps)
             ok, it = ul_results(not worst)
-            points.append({"name": name, "snr_db": snr, "value": S * (world if args.shard == "cells" else 1)
-                           * args.point_steps / e, "ms_per_step": e * 1e3 / args.point_steps,
+            points.append({"name": name, "snr_db": snr, "value": slots_per_step * agg * args.point_steps / e, "ms_per_step": e * 1e3 / args.point_steps,
                            "steps": args.point_steps, "pusch_tb_success_rate": ok, "ldpc_avg_iterations": it})
         fill_samples(args.snr_db, args.worst_case)
 
@@ -391,15 +427,16 @@ def main():
     ul, dl = st0.ul, st0.dl
     info_bits_slot = sum(((22 if s.base_graph == 1 else 10) * s.lifting_size - s.nof_filler_bits) * s.nof_segments
                          for s in ul_segs)
-    tbs_bits_ul = sum(s.tbs for s in ul_segs)
-    tbs_bits_dl = sum(s.tbs for s in dl_segs)
+    tbs_bits_ul_step = sum(s.tbs for s in ul_segs) * S_ul
+    tbs_bits_dl_step = sum(sum(s.tbs for s in c.segs) * c.nof_slots for c in dl_cells)
     # Algorithmic bytes of one decoder launch: the LLRs each codeblock's decode() reads (the HARQ span up to the
     # dematcher's zero tail, as reported by the plan), K*Z/8 bytes of decoded bits written, 4 B result + 1 B CRC flag,
     # 40 B descriptor.
     dec_bytes = ul.decoder.decoder_input_llrs + sum(
-        s.nof_segments * (((22 if s.base_graph == 1 else 10) * s.lifting_size + 7) // 8 + 45) for s in ul_segs) * S
+        s.nof_segments * (((22 if s.base_graph == 1 else 10) * s.lifting_size + 7) // 8 + 45) for s in ul_segs) * S_ul
     achieved = dec_bytes / (dec_ms * 1e-3) / 1e9
-    wl_key = f"{args.profile}/S{S}/{'noise' if args.worst_case else f'{args.snr_db:g}dB'}"
+    wl_key = (f"testmode/P{args.periods}/" if testmode else "") + \
+        f"{args.profile}/S{S}/{'noise' if args.worst_case else f'{args.snr_db:g}dB'}"
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "ldpc_decode_traffic.json")
     if os.path.exists(tfile):
@@ -429,25 +466,34 @@ def main():
     # Algorithmic HBM bytes per step of the signal-chain stages (each byte read or written once; DESIGN.md "Kernels"):
     # bf16 grids are 4 B per RE, time samples 8 B (complex float), estimates 4 B per (layer, port, RE), LLRs 1 B.
     P, nsc, Lu = ul_cell.nof_ports, ul_cell.nsc, prof["ul_layers"]
-    grid_b = S * P * 14 * nsc * 4
-    spp = ul.ofdm.nof_samples // (S * P)  # samples per slot and port (CPs included)
+    grid_b_dl, grid_b_ul = S_dl * P * 14 * nsc * 4, S_ul * P * 14 * nsc * 4
+    spp = ul.ofdm.nof_samples // (S_ul * P)  # samples per slot and port (CPs included)
     nd = bin(DMRS_MASK).count("1")
-    data_re = S * sum(12 * u.n_prb * (14 - nd) for u in ul_ues)
-    cw_b = sum(s.cw_length for s in dl_segs) * S // 8
+    data_re = S_ul * sum(12 * u.n_prb * (14 - nd) for u in ul_ues)
+    cw_b = sum(sum(s.cw_length for s in c.segs) * c.nof_slots for c in dl_cells) // 8
     ce_rows = 1 if ul.estimate_layout == srsgpu.CE_COMPACT else 14
-    ce_b = S * Lu * P * ce_rows * 12 * sum(u.n_prb for u in ul_ues) * 4
+    ce_b = S_ul * Lu * P * ce_rows * 12 * sum(u.n_prb for u in ul_ues) * 4
     stage_bytes = {
-        "pdsch_dmrs_modulate": cw_b + grid_b,
-        "ofdm_modulate": grid_b + S * P * spp * 8,
-        "ofdm_demodulate": S * P * 14 * slotlib.DFT_SIZE * 8 + grid_b,
-        "pusch_channel_estimate": S * P * nd * nsc * 4 + ce_b,
+        "pdsch_dmrs_modulate": cw_b + grid_b_dl,
+        "ofdm_modulate": grid_b_dl + S_dl * P * spp * 8,
+        "ofdm_demodulate": S_ul * P * 14 * slotlib.DFT_SIZE * 8 + grid_b_ul,
+        "pusch_channel_estimate": S_ul * P * nd * nsc * 4 + ce_b,
         "pusch_demodulate": data_re * (P * 4 + Lu * ul_ues[0].qm) + ce_b,
     }
     stage_gbps = {k: v / (stage[k] * 1e-3) / 1e9 for k, v in stage_bytes.items() if stage[k] > 0}
     set_bytes = sum(t.numel() * t.element_size() for t in
-                    (st0.dl_tbs, st0.samples, st0.ul_tbs_tx, dl.d_cw, dl.d_grid, dl.d_samples, ul.d_grid, ul.d_nv,
-                     ul.d_llrs, ul.d_harq, ul.d_crc, ul.d_msgs, ul.d_iters, ul.d_tbs, ul.d_tb_ok)) \
-        + S * Lu * P * 14 * nsc * 4 // 14 * ce_rows
+                    [*st0.dl_tbs_all, st0.samples, st0.ul_tbs_tx, ul.d_grid, ul.d_nv, ul.d_llrs, ul.d_harq, ul.d_crc,
+                     ul.d_msgs, ul.d_iters, ul.d_tbs, ul.d_tb_ok]
+                    + [t for d in st0.dls for t in (d.d_cw, d.d_grid, d.d_samples)]) \
+        + S_ul * Lu * P * 14 * nsc * 4 // 14 * ce_rows
+    if testmode:
+        workload = (f"du_low test mode (configs[4]): n78 100 MHz 4x4, one test UE x 273 PRB per slot (max TBS), "
+                    f"256QAM MCS27, TDD DDDDDDSUUU x {args.periods} per step (special slot: 8-symbol PDSCH, DM-RS "
+                    f"2+7); DM-RS symbols 2+11; DL 4 layers, UL {prof['ul_desc']}; LDPC BG1; fresh DL payloads "
+                    f"every step")
+    else:
+        workload = (f"n78 100 MHz 4x4 slot, 273 PRB, 64 UEs x 4-5 PRB, 256QAM MCS27, DM-RS symbols 2+11; "
+                    f"DL 4 layers, UL {prof['ul_desc']}; LDPC BG1")
 
     result = {
         "metric": "PDSCH+PUSCH slots/sec (100MHz 4x4) + LDPC info-bits/s at 1/2/4/8 GPU",
@@ -466,9 +512,9 @@ def main():
                   f"UL TBs through a GPU UE transmitter (same encoder / DM-RS / modulator), a random unitary 4x4 "
                   f"channel and a CFO within +-{CFO_HZ_MAX:g} Hz per UE, AWGN at {args.snr_db:g} dB SNR, "
                   f"OFDM-modulated")),
-        "config": {"workload": f"n78 100 MHz 4x4 slot, 273 PRB, 64 UEs x 4-5 PRB, 256QAM MCS27, DM-RS symbols 2+11; "
-                               f"DL 4 layers, UL {prof['ul_desc']}; LDPC BG1",
+        "config": {"workload": workload,
                    "profile": args.profile,
+                   "workload_kind": args.workload,
                    "dl_chain": "PDSCH encoder -> PDSCH DM-RS -> PDSCH modulator -> OFDM modulator (4 ports)",
                    "ul_chain": "OFDM demodulator (4 ports) -> DM-RS channel estimator (filter, average, CFO "
                                "compensation, TA) -> PUSCH demodulator -> PUSCH decoder",
@@ -478,12 +524,14 @@ def main():
                    "launch": "one captured HIP graph per step and input set" if args.graph else "eager launches",
                    "pipelining": (f"up to {K} steps in flight: each input set's step runs on its own stream"
                                   if args.pipeline else "steps serialised on one stream"),
-                   "slots_per_step": S,
+                   "slots_per_step": slots_per_step,
+                   "dl_slots_per_step": S_dl, "ul_slots_per_step": S_ul,
                    "input_sets": K,
                    "working_set_mb": K * set_bytes / 2 ** 20,
                    "timed_region_s": elapsed,
-                   "codeblocks_per_step": {"dl": int(sum(s.nof_segments for s in dl_segs) * S),
-                                           "ul": int(sum(s.nof_segments for s in ul_segs) * S)},
+                   "codeblocks_per_step": {"dl": int(sum(sum(s.nof_segments for s in c.segs) * c.nof_slots
+                                                     for c in dl_cells)),
+                                           "ul": int(sum(s.nof_segments for s in ul_segs) * S_ul)},
                    "ldpc_max_iterations": args.iterations, "ldpc_early_stop": True,
                    "decoder_arithmetic": "avx2/avx512 (SIMD) variant, bit-exact",
                    "ofdm": "4096-point DFT, 122.88 Msps, normal CP",
@@ -492,8 +540,8 @@ def main():
                                    f"cell on every rank)") + (
                                       "; decoded UL TBs + CRC flags gathered to the FAPI rank over RCCL every step"
                                       if world > 1 else "")},
-        "ldpc_info_bits_per_s": info_bits_slot * value,
-        "tb_bits_per_s": {"dl": tbs_bits_dl * value, "ul": tbs_bits_ul * value},
+        "ldpc_info_bits_per_s": info_bits_slot * S_ul * step_rate,
+        "tb_bits_per_s": {"dl": tbs_bits_dl_step * step_rate, "ul": tbs_bits_ul_step * step_rate},
         "realtime_cells_per_gpu": value / SLOT_RATE_30KHZ / world,
         "pusch_tb_success_rate": tb_success,
         "ldpc_avg_iterations": avg_iters,
@@ -515,9 +563,10 @@ def main():
         cw_host = (dl.d_cw.cpu().numpy(), dl.cw_offsets[:n_dl])
         samples_host = st0.samples[: 2 * 4 * 61440].cpu().numpy()
         base, ref_llr = cpu_baseline(dl_ues, dl_segs, ul_ues, ul_segs, tb_host, cw_host, samples_host,
-                                     args.iterations, args.cpu_seconds, host_cores())
+                                     args.iterations, args.cpu_seconds, host_cores(),
+                                     tdd=(slotlib.TDD_DL_SLOTS + 1, slotlib.TDD_UL_SLOTS) if testmode else None)
         result["cpu_baseline"] = base
-        if ref_llr is not None and args.profile == "ref":
+        if ref_llr is not None and args.profile == "ref" and not testmode:  # the reference shim runs slot 0
             # The GPU's UL LLRs of slot 0 against the reference's on the same received samples.
             pipeline(st0)
             torch.cuda.synchronize()

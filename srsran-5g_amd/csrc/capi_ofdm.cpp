@@ -12,7 +12,7 @@ using namespace srsgpu;
 struct srsgpu_ofdm_plan {
   srsgpu_context*       ctx        = nullptr;
   bool                  inverse    = true;  ///< Modulator (inverse DFT) or demodulator.
-  uint32_t              log2_dft   = 0;
+  uint32_t              dft_size   = 0;
   uint32_t              nsc        = 0;
   uint32_t              window_off = 0;
   uint32_t              nof_ports  = 0;
@@ -76,12 +76,12 @@ int plan_create(srsgpu_context*           ctx,
   const uint32_t N   = cfg->dft_size;
   const uint32_t mu  = cfg->numerology;
   const uint32_t nsc = 12u * cfg->bw_rb;
-  uint32_t       log2n = 0;
-  while ((1u << log2n) < N) {
-    ++log2n;
-  }
-  if ((1u << log2n) != N || log2n < 8 || log2n > 13) {
-    return fail(SRSGPU_ERR_INVALID_ARG, "DFT size %u not supported (powers of two 256..8192)", N);
+  // The generic DFT's sizes (dft_processor_generic_impl.cpp:211-230) up to 8192 points, except 4608 = 9 x 512.
+  const uint32_t m = (N % 3 == 0) ? N / 3 : N;
+  const bool     pow2_ok = N >= 128 && N <= 8192 && (N & (N - 1)) == 0;
+  const bool     x3_ok   = N % 3 == 0 && m >= 128 && m <= 2048 && (m & (m - 1)) == 0;
+  if (!pow2_ok && !x3_ok) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "DFT size %u not supported (2^n 128..8192 or 3 x 2^m 384..6144)", N);
   }
   if (mu > 4 || cfg->bw_rb == 0 || nsc >= N) {
     return fail(SRSGPU_ERR_INVALID_ARG, "the DFT size (%u) must be greater than the resource grid size (%u)", N, nsc);
@@ -122,7 +122,7 @@ int plan_create(srsgpu_context*           ctx,
   auto* plan       = new srsgpu_ofdm_plan();
   plan->ctx        = ctx;
   plan->inverse    = inverse;
-  plan->log2_dft   = log2n;
+  plan->dft_size   = N;
   plan->nsc        = nsc;
   plan->window_off = woff;
   plan->nof_ports  = nof_ports;
@@ -212,7 +212,7 @@ int srsgpu_ofdm_modulator_plan_execute(const srsgpu_ofdm_plan* plan,
   if (plan == nullptr || d_grids == nullptr || d_samples == nullptr || !plan->inverse) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument or not a modulator plan");
   }
-  launch_ofdm(true, plan->log2_dft, plan->d_jobs, plan->nof_jobs, plan->nsc, 0, plan->ctx->d_ofdm_twiddles, d_grids,
+  launch_ofdm(true, plan->dft_size, plan->d_jobs, plan->nof_jobs, plan->nsc, 0, plan->ctx->d_ofdm_twiddles, d_grids,
               nullptr, nullptr, d_samples, static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
@@ -226,7 +226,7 @@ int srsgpu_ofdm_demodulator_plan_execute(const srsgpu_ofdm_plan* plan,
   if (plan == nullptr || d_grids == nullptr || d_samples == nullptr || plan->inverse) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument or not a demodulator plan");
   }
-  launch_ofdm(false, plan->log2_dft, plan->d_jobs, plan->nof_jobs, plan->nsc, plan->window_off,
+  launch_ofdm(false, plan->dft_size, plan->d_jobs, plan->nof_jobs, plan->nsc, plan->window_off,
               plan->ctx->d_ofdm_twiddles, nullptr, d_grids, d_samples, nullptr, static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;

@@ -7,8 +7,9 @@
 // lib/phy/generic_functions/dft_processor_generic_impl.cpp (sign -1 direct, +1 inverse).
 //
 // Decomposition for N = 2^n: a first pass of radix 2^(n mod 4) (or 16), then radix-16 passes. N / 16 threads (a
-// partial wave below N = 1024), each
-// holding 16 complex values in registers per pass: a pass reads its butterfly inputs (from HBM in the first pass:
+// partial wave below N = 1024), each holding 16 complex values in registers per pass. N = 3 * 2^m (the generic DFT's
+// 384 ... 6144, e.g. 1536 / 3072 points at 46.08 / 92.16 Msps): the power-of-two passes of M = 2^m, then one radix-3
+// pass; N / 48 threads holding 48 values per pass. A pass a pass reads its butterfly inputs (from HBM in the first pass:
 // the grid's subcarriers or the symbol's time samples, coalesced), barriers, twiddles them (exp(-+2 pi i m / N) from
 // a 8192-entry table computed in double on the host), runs the in-register radix-R DFT and writes the outputs to LDS —
 // or, in the last pass, straight to HBM with the compensation applied: time samples (and the cyclic-prefix copy) or
@@ -46,7 +47,16 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b)
 template <int R, int S>
 __device__ __forceinline__ void dft_reg(float2* v)
 {
-  if constexpr (R == 2) {
+  if constexpr (R == 3) {
+    // X0 = a + (b + c), X1,2 = a - (b + c) / 2 +- S i sqrt(3) / 2 (b - c).
+    const float2 a = v[0], t1 = cadd(v[1], v[2]), t2 = csub(v[1], v[2]);
+    const float  h = S * 0.86602540378f;
+    const float2 m = make_float2(a.x - 0.5f * t1.x, a.y - 0.5f * t1.y);
+    const float2 n = make_float2(-h * t2.y, h * t2.x);
+    v[0]           = cadd(a, t1);
+    v[1]           = cadd(m, n);
+    v[2]           = csub(m, n);
+  } else if constexpr (R == 2) {
     const float2 a = v[0], b = v[1];
     v[0]           = cadd(a, b);
     v[1]           = csub(a, b);
@@ -163,6 +173,109 @@ __device__ __forceinline__ void stockham_pass(const float2 (&w)[16 / R][R], Src 
   __syncthreads();
 }
 
+constexpr bool is_pow2(int n)
+{
+  return (n & (n - 1)) == 0;
+}
+constexpr int ilog2(int n)
+{
+  return n <= 1 ? 0 : 1 + ilog2(n / 2);
+}
+/// Threads per workgroup of an N-point transform: 16 values per thread (2^n) or 48 (3 * 2^m).
+template <int N>
+constexpr int ofdm_threads()
+{
+  return is_pow2(N) ? N / 16 : N / 48;
+}
+
+/// exp(S 2 pi i m / N), 0 <= m < N, of any supported N: the table entry for a power of two, sincospi otherwise
+/// (argument 2 m / N rounded once: phase error < 3e-7 rad).
+template <int N, int S>
+__device__ __forceinline__ float2 twiddle_any(const float2* __restrict__ tw, uint32_t m)
+{
+  float2 x;
+  if constexpr (is_pow2(N)) {
+    x = tw[m * (OFDM_MAX_DFT / N)];
+    x.y = -x.y;  // the table holds exp(-...)
+  } else {
+    sincospif(static_cast<float>(2 * m) / static_cast<float>(N), &x.y, &x.x);
+  }
+  if constexpr (S < 0) {
+    x.y = -x.y;
+  }
+  return x;
+}
+
+/// One Stockham pass of the N = 3 M transform (T = N / 48 threads, B = N / (R T) butterflies each). The power-of-two
+/// passes come first: their NS divides T, so all butterflies of a thread share k = tid mod NS and the twiddles w of
+/// load_twiddles. The radix-3 pass is last (NS = M, k = j): twiddles exp(S 2 pi i r j / N) by sincospi.
+template <int N, int R, int NS, int S, typename Src, typename Dst>
+__device__ __forceinline__ void stockham_pass3(const float2 (&w)[16], Src src, Dst dst)
+{
+  constexpr int T = N / 48;
+  constexpr int B = N / (R * T);
+  static_assert(R == 3 ? NS == N / 3 : (T % NS == 0 || NS == 1), "pass order: powers of two, then radix 3");
+  float2    v[B][R];
+  const int tid = static_cast<int>(threadIdx.x);
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const int j = tid + b * T;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      v[b][r] = src(j + r * (N / R));
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const int j = tid + b * T;
+    const int k = (R == 3) ? j : (j & (NS - 1));
+    if constexpr (R == 3) {
+#pragma unroll
+      for (int r = 1; r < 3; ++r) {
+        v[b][r] = cmul(v[b][r], twiddle_any<N, S>(nullptr, static_cast<uint32_t>(r * j)));
+      }
+    } else if constexpr (NS > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        v[b][r] = cmul(v[b][r], w[r]);
+      }
+    }
+    dft_reg<R, S>(v[b]);
+    const int base = (j - k) * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      dst(base + r * NS, v[b][r]);
+    }
+  }
+  __syncthreads();
+}
+
+/// N = 3 M: power-of-two passes of M (first radix 2^(m mod 4) or 16, then 16s), then radix 3.
+template <int N, int S, typename Src, typename Dst>
+__device__ __forceinline__ void dft_lds3(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
+{
+  constexpr int M   = N / 3;
+  constexpr int LM  = ilog2(M);
+  constexpr int REM = LM % 4;
+  constexpr int R0  = REM ? (1 << REM) : 16;
+  constexpr int NP  = LM / 4 + (REM ? 1 : 0);
+  static_assert(3 * M == N && is_pow2(M) && NP >= 2 && NP <= 3, "supported DFT sizes: 3 x (128..2048)");
+  auto   ld = [lds](int i) { return lds[i]; };
+  auto   st = [lds](int i, float2 v) { lds[i] = v; };
+  float2 w0[16] = {}, w1[1][16], w2[1][16];
+  load_twiddles<N, 16, R0, S>(tw, w1);
+  if constexpr (NP == 3) {
+    load_twiddles<N, 16, R0 * 16, S>(tw, w2);
+  }
+  stockham_pass3<N, R0, 1, S>(w0, src_first, st);
+  stockham_pass3<N, 16, R0, S>(w1[0], ld, st);
+  if constexpr (NP == 3) {
+    stockham_pass3<N, 16, R0 * 16, S>(w2[0], ld, st);
+  }
+  stockham_pass3<N, 3, M, S>(w0, ld, dst_last);
+}
+
 template <int LOG2N, int S, typename Src, typename Dst>
 __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
 {
@@ -173,7 +286,7 @@ __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ 
   // (Padding the layout against the first pass's strided stores measured slower: the transform is latency-bound.)
   auto          ld   = [lds](int i) { return lds[i]; };
   auto          st   = [lds](int i, float2 v) { lds[i] = v; };
-  static_assert(NP >= 2 && NP <= 4, "supported DFT sizes: 256..8192");
+  static_assert(NP >= 2 && NP <= 4, "supported DFT sizes: 128..8192");
   float2 w0[16 / R0][R0], w1[1][16], w2[1][16], w3[1][16];
   load_twiddles<N, 16, R0, S>(tw, w1);
   if constexpr (NP >= 3) {
@@ -195,21 +308,31 @@ __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ 
   }
 }
 
+/// Any supported N: the power-of-two or the 3 x 2^m decomposition.
+template <int N, int S, typename Src, typename Dst>
+__device__ __forceinline__ void dft_any(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
+{
+  if constexpr (is_pow2(N)) {
+    dft_lds<ilog2(N), S>(lds, tw, src_first, dst_last);
+  } else {
+    dft_lds3<N, S>(lds, tw, src_first, dst_last);
+  }
+}
+
 __device__ __forceinline__ uint32_t bf16_bits(float v)
 {
   const uint32_t u = __float_as_uint(v);
   return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
 }
 
-template <int LOG2N>
-__global__ __launch_bounds__((1 << LOG2N) / 16) void ofdm_modulate_kernel(
+template <int N>
+__global__ __launch_bounds__(ofdm_threads<N>()) void ofdm_modulate_kernel(
     const ofdm_job* __restrict__ jobs,
     uint32_t nsc,
     const float2* __restrict__ tw,
     const uint32_t* __restrict__ grid,
     float2* __restrict__ out)
 {
-  constexpr int       N = 1 << LOG2N;
   __shared__ float2   lds[N];
   const ofdm_job      jb   = jobs[blockIdx.x];
   const int           half = static_cast<int>(nsc / 2);
@@ -238,11 +361,11 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void ofdm_modulate_kernel(
       sym[n - (N - cp)] = y;
     }
   };
-  dft_lds<LOG2N, +1>(lds, tw, src, dst);
+  dft_any<N, +1>(lds, tw, src, dst);
 }
 
-template <int LOG2N>
-__global__ __launch_bounds__((1 << LOG2N) / 16) void ofdm_demodulate_kernel(
+template <int N>
+__global__ __launch_bounds__(ofdm_threads<N>()) void ofdm_demodulate_kernel(
     const ofdm_job* __restrict__ jobs,
     uint32_t nsc,
     uint32_t window_offset,
@@ -250,7 +373,6 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void ofdm_demodulate_kernel(
     const float2* __restrict__ in,
     uint32_t* __restrict__ grid)
 {
-  constexpr int     N = 1 << LOG2N;
   __shared__ float2 lds[N];
   const ofdm_job    jb   = jobs[blockIdx.x];
   const int         half = static_cast<int>(nsc / 2);
@@ -270,16 +392,14 @@ __global__ __launch_bounds__((1 << LOG2N) / 16) void ofdm_demodulate_kernel(
     }
     float2 y = cmul(v, coef);
     if (window_offset != 0) {  // times exp(+j 2 pi offset b / N)
-      float2 w = tw[((window_offset * static_cast<uint32_t>(b)) & (N - 1)) * (OFDM_MAX_DFT / N)];
-      w.y      = -w.y;
-      y        = cmul(y, w);
+      y = cmul(y, twiddle_any<N, +1>(tw, (window_offset * static_cast<uint32_t>(b)) % N));
     }
     row[sc] = bf16_bits(y.x) | (bf16_bits(y.y) << 16);
   };
-  dft_lds<LOG2N, -1>(lds, tw, src, dst);
+  dft_any<N, -1>(lds, tw, src, dst);
 }
 
-template <int LOG2N>
+template <int N>
 void launch_one(bool            inverse,
                 const ofdm_job* jobs,
                 int             nof_jobs,
@@ -292,12 +412,12 @@ void launch_one(bool            inverse,
                 float2*         samples_out,
                 hipStream_t     stream)
 {
-  constexpr int threads = (1 << LOG2N) / 16;  // every thread takes part in the passes' barriers
+  constexpr int threads = ofdm_threads<N>();  // every thread takes part in the passes' barriers
   if (inverse) {
-    hipLaunchKernelGGL(ofdm_modulate_kernel<LOG2N>, dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0, stream,
+    hipLaunchKernelGGL(ofdm_modulate_kernel<N>, dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0, stream,
                        jobs, nsc, tw, grid_in, samples_out);
   } else {
-    hipLaunchKernelGGL(ofdm_demodulate_kernel<LOG2N>, dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0,
+    hipLaunchKernelGGL(ofdm_demodulate_kernel<N>, dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0,
                        stream, jobs, nsc, window_offset, tw, samples_in, grid_out);
   }
 }
@@ -305,7 +425,7 @@ void launch_one(bool            inverse,
 } // namespace
 
 void launch_ofdm(bool            inverse,
-                 uint32_t        log2_dft,
+                 uint32_t        dft_size,
                  const ofdm_job* d_jobs,
                  int             nof_jobs,
                  uint32_t        nsc,
@@ -323,13 +443,19 @@ void launch_ofdm(bool            inverse,
   const auto* tw  = reinterpret_cast<const float2*>(d_twiddles);
   const auto* sin = reinterpret_cast<const float2*>(d_samples_in);
   auto*       so  = reinterpret_cast<float2*>(d_samples_out);
-  switch (log2_dft) {
-    case 8: launch_one<8>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 9: launch_one<9>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 10: launch_one<10>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 11: launch_one<11>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 12: launch_one<12>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 13: launch_one<13>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+  switch (dft_size) {
+    case 128: launch_one<128>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 256: launch_one<256>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 512: launch_one<512>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 1024: launch_one<1024>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 2048: launch_one<2048>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 4096: launch_one<4096>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 8192: launch_one<8192>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 384: launch_one<384>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 768: launch_one<768>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 1536: launch_one<1536>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 3072: launch_one<3072>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 6144: launch_one<6144>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
     default: break;
   }
 }

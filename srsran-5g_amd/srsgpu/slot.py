@@ -11,7 +11,7 @@ pusch_processor_impl.cpp (estimate, demodulate, decode), lib/phy/lower/modulatio
 not part of the receive path it feeds.
 """
 from dataclasses import dataclass
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 
@@ -42,6 +42,8 @@ class CellSlots:
     nof_ports: int = 4
     dmrs_mask: int = 1 << DMRS_SYMBOL
     rb_first: int = 0  # first RB of the first UE (a rank's share of the UEs when a slot is sharded by UE)
+    nof_symbols: int = 14  # shared-channel symbols from symbol 0 (8 in a TDD special slot's downlink part)
+    slot_numbers: Optional[List[int]] = None  # slot number within the frame of each batch slot (default: s % 20)
 
     @property
     def nsc(self):
@@ -55,10 +57,42 @@ class CellSlots:
         return out
 
     def slot_index(self, s):
-        return s % 20
+        return (s if self.slot_numbers is None else self.slot_numbers[s]) % 20
+
+    def subframe_slots(self):
+        """Slot index within the subframe of every batch slot (the OFDM phase compensation's symbol epochs)."""
+        return [self.slot_index(s) % (1 << NUMEROLOGY) for s in range(self.nof_slots)]
 
     def grid_elems(self):
         return self.nof_slots * self.nof_ports * 14 * self.nsc
+
+
+TDD_PERIOD = 10           # du_high_config.h:503-511 defaults: 10-slot period, 6 DL slots, a special slot with 8 DL
+TDD_DL_SLOTS = 6          # symbols (no UL symbols) and 3 UL slots (DDDDDDSUUU)
+TDD_SPECIAL_DL_SYMBOLS = 8
+TDD_UL_SLOTS = 3
+DMRS_POS1_8SYM = (1 << 2) | (1 << 7)  # TS 38.211 Table 7.4.1.1.2-3: type A, duration 8, pos1 -> l0 = 2 and 7
+
+
+def tdd_testmode_cells(periods: int, dl_layers: int = 4, ul_layers: int = 1, mcs: int = 27, nof_prb: int = 273):
+    """The du_low test mode's traffic over `periods` TDD periods of the du_high default pattern: one test UE owning the
+    whole carrier in every slot (max TBS: CQI 15 -> MCS 27 of the 256QAM table, all 273 PRB), `dl_layers` PDSCH
+    layers, `ul_layers` PUSCH layers, DM-RS type 1 pos1. Returns (full DL slots, special-slot DL part, UL slots) as
+    CellSlots with their slot numbers in the frame (du_high_config.h:882-905 test_ue: pdsch_active / pusch_active)."""
+    qm, r = sch.MCS_TABLE_256QAM[mcs]
+    dl_nums = [p * TDD_PERIOD + i for p in range(periods) for i in range(TDD_DL_SLOTS)]
+    sp_nums = [p * TDD_PERIOD + TDD_DL_SLOTS for p in range(periods)]
+    ul_nums = [p * TDD_PERIOD + TDD_DL_SLOTS + 1 + i for p in range(periods) for i in range(TDD_UL_SLOTS)]
+    dl_ue = sch.UeGrant(nof_prb, dl_layers, qm, r, nof_dmrs_symbols=2)
+    sp_ue = sch.UeGrant(nof_prb, dl_layers, qm, r, nof_symb_sh=TDD_SPECIAL_DL_SYMBOLS, nof_dmrs_symbols=2)
+    ul_ue = sch.UeGrant(nof_prb, ul_layers, qm, r, nof_dmrs_symbols=2)
+    dl = CellSlots([dl_ue], [dl_ue.segmentation()], len(dl_nums), grid_prb=nof_prb, dmrs_mask=DMRS_POS1,
+                   slot_numbers=dl_nums)
+    sp = CellSlots([sp_ue], [sp_ue.segmentation()], len(sp_nums), grid_prb=nof_prb, dmrs_mask=DMRS_POS1_8SYM,
+                   nof_symbols=TDD_SPECIAL_DL_SYMBOLS, slot_numbers=sp_nums)
+    ul = CellSlots([ul_ue], [ul_ue.segmentation()], len(ul_nums), grid_prb=nof_prb, dmrs_mask=DMRS_POS1,
+                   slot_numbers=ul_nums)
+    return dl, sp, ul
 
 
 def _identity(P, L):
@@ -88,7 +122,7 @@ class DownlinkPipeline:
                 mods.append(srsgpu.PdschModulation(
                     rnti=rnti0 + i, n_id=n_id, modulation_order=u.qm, nof_layers=u.nof_layers,
                     nof_ports=cell.nof_ports, bwp_start_rb=0, bwp_size_rb=cell.grid_prb, rb_start=rb0[i],
-                    nof_rb=u.n_prb, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=cell.dmrs_mask, dmrs_type=1,
+                    nof_rb=u.n_prb, start_symbol=0, nof_symbols=cell.nof_symbols, dmrs_symbol_mask=cell.dmrs_mask, dmrs_type=1,
                     nof_cdm_groups_without_data=2, scaling=1.0, weights=w))
                 dmrs.append(srsgpu.PdschDmrs(
                     slot_index=cell.slot_index(s), scrambling_id=scrambling_id, n_scid=0, dmrs_type=1,
@@ -100,7 +134,7 @@ class DownlinkPipeline:
         self.dmrs = srsgpu.PdschDmrsPlan(ctx, srsgpu.make_pdsch_dmrs_configs(dmrs, grid_idx), cell.grid_prb,
                                          cell.nof_ports)
         self.ofdm = srsgpu.OfdmPlan(ctx, True, NUMEROLOGY, cell.grid_prb, DFT_SIZE, TX_SCALE, CENTER_FREQ_HZ,
-                                    [s % 2 for s in range(S)], cell.nof_ports)
+                                    cell.subframe_slots(), cell.nof_ports)
         dev = torch.device("cuda", ctx.device)
         self.d_cw = torch.zeros(max(self.cw_total, 4), dtype=torch.uint8, device=dev)
         self.d_grid = torch.zeros(cell.grid_elems(), dtype=torch.int32, device=dev)
@@ -119,6 +153,34 @@ class DownlinkPipeline:
         rec(3)
 
 
+class DownlinkGroup:
+    """Several DownlinkPipelines (e.g. a TDD period's full DL slots and its special slot's DL part) run stage by stage
+    on one stream, each with its own TB buffer. `fresh_tbs`: every execution first overwrites the TB payloads with
+    new random bytes on the stream (graph-safe Philox: a captured graph draws new payloads on every replay), so
+    consecutive slots carry fresh data like the test mode's continuous traffic."""
+
+    def __init__(self, pipes: Sequence[DownlinkPipeline], d_tbs: Sequence, fresh_tbs=False):
+        self.pipes, self.d_tbs, self.fresh_tbs = list(pipes), list(d_tbs), fresh_tbs
+
+    def execute(self, stream, events=None):
+        if self.fresh_tbs:
+            with torch.cuda.stream(stream):
+                for t in self.d_tbs:
+                    t.random_(0, 256)
+        rec = (lambda i: events[i].record(stream)) if events else (lambda i: None)
+        rec(0)
+        for p, t in zip(self.pipes, self.d_tbs):
+            p.encoder.execute(t, p.d_cw, stream)
+        rec(1)
+        for p in self.pipes:
+            p.dmrs.execute(p.d_grid, stream)
+            p.modulator.execute(p.d_cw, p.d_grid, stream)
+        rec(2)
+        for p in self.pipes:
+            p.ofdm.execute(p.d_grid, p.d_samples, stream)
+        rec(3)
+
+
 class UplinkPipeline:
     """OFDM demodulator -> DM-RS channel estimator -> PUSCH demodulator -> PUSCH decoder for every UE of every slot.
     The channel-estimate, noise-variance, LLR, HARQ and TB buffers are owned by the pipeline. `estimate_layout`:
@@ -134,18 +196,18 @@ class UplinkPipeline:
         rb0 = cell.rb_starts()
         dev = torch.device("cuda", ctx.device)
         self.ofdm = srsgpu.OfdmPlan(ctx, False, NUMEROLOGY, cell.grid_prb, DFT_SIZE, 1.0 / (TX_SCALE * DFT_SIZE),
-                                    CENTER_FREQ_HZ, [s % 2 for s in range(S)], cell.nof_ports)
+                                    CENTER_FREQ_HZ, cell.subframe_slots(), cell.nof_ports)
         ests, dems, grid_idx = [], [], []
         for s in range(S):
             for i, u in enumerate(ues):
                 ests.append(srsgpu.PuschChannelEstimation(
                     scrambling_id=scrambling_id, n_scid=0, dmrs_type=1, nof_tx_layers=u.nof_layers,
-                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=cell.dmrs_mask,
+                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=cell.nof_symbols, dmrs_symbol_mask=cell.dmrs_mask,
                     rb_start=rb0[i], nof_rb=u.n_prb, slot_index=cell.slot_index(s), scaling=DMRS_BETA,
                     estimate_layout=estimate_layout, compensate_cfo=int(compensate_cfo), numerology=NUMEROLOGY))
                 dems.append(srsgpu.PuschDemodulation(
                     rnti=rnti0 + i, n_id=n_id, modulation_order=u.qm, nof_tx_layers=u.nof_layers,
-                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=14, dmrs_symbol_mask=cell.dmrs_mask,
+                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=cell.nof_symbols, dmrs_symbol_mask=cell.dmrs_mask,
                     dmrs_type=1, nof_cdm_groups_without_data=2, rb_start=rb0[i], nof_rb=u.n_prb,
                     equalizer=equalizer, estimate_layout=estimate_layout, cfo_compensated=int(compensate_cfo),
                     numerology=NUMEROLOGY))
@@ -247,7 +309,7 @@ def synthesize_uplink(ctx, cell: CellSlots, d_tbs, snr_db=35.0, seed=0, rnti0=0x
 
     rx_grid = ((to_bf16(yr) & 0xFFFF) | (to_bf16(yi) << 16)).to(torch.int32).contiguous().reshape(-1)
     air = srsgpu.OfdmPlan(ctx, True, NUMEROLOGY, cell.grid_prb, DFT_SIZE, TX_SCALE, CENTER_FREQ_HZ,
-                          [s % 2 for s in range(S)], P)
+                          cell.subframe_slots(), P)
     d_samples = torch.zeros(2 * air.nof_samples, dtype=torch.float32, device=dev)
     air.execute(rx_grid, d_samples, stream)
     torch.cuda.synchronize(dev)

@@ -21,6 +21,14 @@ CASES = [
     (1, 10, 256, False, 1.0, 0.0, 1, 0),
     (3, 66, 1024, False, 0.3, 28e9, 5, 0),              # 120 kHz
     (1, 273, 8192, False, 1.0 / 128, 3.5e9, 0, 31),     # 245.76 Msps
+    (0, 6, 128, False, 0.5, 1.9e9, 0, 0),               # 1.4 MHz-like grid, 1.92 Msps
+    # 3 x 2^m sizes of the generic DFT (dft_processor_generic_impl.cpp:213-222)
+    (1, 106, 1536, False, 0.05, 3.5e9, 0, 0),           # 40 MHz, 46.08 Msps
+    (1, 217, 3072, False, 1.0 / 48, 3.6e9, 1, 9),       # 80 MHz, 92.16 Msps
+    (0, 25, 384, False, 0.2, 2.1e9, 0, 0),              # 5 MHz 15 kHz, 5.76 Msps
+    (0, 52, 768, False, 0.1, 1.8e9, 0, 3),              # 10 MHz 15 kHz, 11.52 Msps
+    (2, 51, 768, False, 0.3, 28e9, 3, 0),               # 60 kHz
+    (1, 273, 6144, False, 1.0 / 96, 3.5e9, 0, 20),      # 100 MHz, 184.32 Msps
 ]
 
 

@@ -1,0 +1,105 @@
+"""configs[4]: the du_low test mode's traffic on the GPU - one test UE owning all 273 PRB in every slot (max TBS, MCS 27,
+4 DL layers), continuous slots of the du_high default TDD pattern DDDDDDSUUU (du_high_config.h:503-511; the special
+slot carries an 8-symbol PDSCH with DM-RS in symbols 2 and 7), the whole period captured once as a HIP graph and
+replayed slot period after slot period with fresh data:
+
+* DL: every replay draws new TB payloads on the GPU inside the graph (srsgpu.slot.DownlinkGroup, fresh_tbs). Each
+  period's codewords, grids and samples must equal an eager run of the same plans on the drawn payloads, and a
+  loopback receiver (the GPU's own OFDM demodulator -> 4-layer estimator -> MMSE demodulator -> decoder, after AWGN)
+  must decode every drawn TB of the period;
+* UL: the period's 3 UL slots (one max-TBS single-layer PUSCH each, ZF, the reference-runnable profile) rotate over
+  independently synthesised UE transmissions; every replay must decode that transmission's TBs.
+"""
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import srsgpu
+    return srsgpu.Context(0)
+
+
+def test_testmode_cells_follow_the_tdd_pattern():
+    from srsgpu import slot as slotlib
+    dl, sp, ul = slotlib.tdd_testmode_cells(2)
+    assert [dl.slot_index(s) for s in range(dl.nof_slots)] == [0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15]
+    assert [sp.slot_index(s) for s in range(sp.nof_slots)] == [6, 16]
+    assert [ul.slot_index(s) for s in range(ul.nof_slots)] == [7, 8, 9, 17, 18, 19]
+    assert sp.nof_symbols == 8 and sp.dmrs_mask == (1 << 2) | (1 << 7)
+    # Max TBS of 273 PRB, 256QAM MCS 27 (TS 38.214 5.1.3.2): 4 layers x 12 data symbols, 4 layers x 6, 1 layer x 12.
+    assert [c.segs[0].tbs for c in (dl, sp, ul)] == [1179864, 590128, 295176]
+
+
+@pytest.mark.gpu
+def test_testmode_continuous_periods_with_fresh_payloads(ctx):
+    import torch
+    import srsgpu
+    from srsgpu import slot as slotlib
+    dl_cell, sp_cell, ul_cell = slotlib.tdd_testmode_cells(1, dl_layers=4, ul_layers=1)
+    dls = [slotlib.DownlinkPipeline(ctx, c) for c in (dl_cell, sp_cell)]
+    tbs = [torch.zeros(d.tb_total, dtype=torch.uint8, device="cuda") for d in dls]
+    group = slotlib.DownlinkGroup(dls, tbs, fresh_tbs=True)
+    ul = slotlib.UplinkPipeline(ctx, ul_cell, equalizer=srsgpu.EQ_ZF)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(21)
+    ul_sets = []
+    for k in range(2):  # two different UE transmissions of the period's UL slots
+        sent = torch.randint(0, 256, (sum(ul.tb_bytes),), generator=gen, device="cuda", dtype=torch.uint8)
+        x = slotlib.synthesize_uplink(ctx, ul_cell, sent, snr_db=30.0, seed=40 + k, cfo_hz_max=300.0)
+        ul_sets.append((sent, x))
+    samples = torch.zeros_like(ul_sets[0][1])
+    # Loopback receivers for the DL slots (the GPU transmitter's own output, identity channel + AWGN).
+    rx = [slotlib.UplinkPipeline(ctx, c) for c in (dl_cell, sp_cell)]
+    eager = [slotlib.DownlinkPipeline(ctx, c) for c in (dl_cell, sp_cell)]
+    eager_group = slotlib.DownlinkGroup(eager, tbs, fresh_tbs=False)
+
+    s_dl, s_ul = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def period():
+        cur = torch.cuda.current_stream()
+        s_dl.wait_stream(cur)
+        s_ul.wait_stream(cur)
+        group.execute(s_dl)
+        ul.execute(samples, s_ul)
+        cur.wait_stream(s_dl)
+        cur.wait_stream(s_ul)
+
+    period()  # warm-up (plans' first launches) outside the capture
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        period()
+    stream = torch.cuda.current_stream()
+    prev = None
+    for step in range(4):
+        sent, x = ul_sets[step % 2]
+        samples.copy_(x)
+        graph.replay()
+        torch.cuda.synchronize()
+        drawn = [t.clone() for t in tbs]
+        if prev is not None:  # fresh payloads on every replay
+            for a, b in zip(drawn, prev):
+                assert not torch.equal(a, b)
+        prev = drawn
+        # The graph's DL outputs equal an eager run of identical plans on the same payloads.
+        eager_group.execute(stream)
+        torch.cuda.synchronize()
+        for d, e in zip(dls, eager):
+            assert torch.equal(d.d_cw, e.d_cw)
+            assert torch.equal(d.d_grid, e.d_grid)
+            assert torch.equal(d.d_samples, e.d_samples)
+        # Loopback: every DL TB of the period decodes to the drawn payload.
+        for d, r, t in zip(dls, rx, drawn):
+            y = d.d_samples
+            rms = float(y.square().mean().sqrt())
+            noisy = y + torch.randn(y.shape, generator=gen, device="cuda") * (rms * 10 ** (-35 / 20))
+            r.execute(noisy, stream)
+            torch.cuda.synchronize()
+            ok = r.d_tb_ok.cpu().numpy()
+            assert ok.all(), (step, np.nonzero(ok == 0)[0])
+            assert torch.equal(r.d_tbs, t)
+        # UL: this period's UE transmission.
+        ok = ul.d_tb_ok.cpu().numpy()
+        assert ok.all(), (step, np.nonzero(ok == 0)[0])
+        assert torch.equal(ul.d_tbs, sent)

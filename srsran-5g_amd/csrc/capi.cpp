@@ -73,11 +73,14 @@ struct srsgpu_pdsch_encoder_plan {
   srsgpu_context* ctx        = nullptr;
   tb_crc_desc*    d_tb       = nullptr;
   uint32_t*       d_tb_crc   = nullptr;
+  tb_crc_slice*   d_slices   = nullptr;  ///< tb_crc_kernel work (TBs split into TB_CRC_SLICE_BYTES ranges).
+  int             nof_slices = 0;
   int             nof_tbs    = 0;
   enc_desc*       d_enc[2]   = {nullptr, nullptr};  ///< Per base graph: byte-kernel codeblocks, then packed ones.
   int             count[2]   = {0, 0};
   int             count_pk[2] = {0, 0};
-  bool            inline_tb_crc = false;  ///< Every codeblock packed, every TB CRC table cached: no tb_crc_kernel.
+  bool            inline_tb_crc = false;  ///< Every codeblock packed, every TB CRC table cached, every TB at most
+                                          ///< TB_CRC_INLINE_MAX_BYTES: no tb_crc_kernel.
   int             threads[2] = {64, 64};
   size_t          out_begin  = 0;
   size_t          out_end    = 0;
@@ -91,6 +94,7 @@ struct srsgpu_pusch_decoder_plan {
   srsgpu_pusch_cb_plan* cbs     = nullptr;
   tb_dec_desc*          d_tb    = nullptr;
   int                   nof_tbs = 0;
+  int                   tb_threads = 256;  ///< pusch_tb_kernel workgroup size (1024 for large TBs).
 };
 
 struct srsgpu_ldpc_decoder_plan {
@@ -983,16 +987,29 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
     out_begin        = std::min(out_begin, static_cast<size_t>(c.cw_offset));
     out_end          = std::max(out_end, static_cast<size_t>(c.cw_offset) + (static_cast<size_t>(seg.cw_length) + 31) / 32 * 4);
   }
+  // TB CRC slices: a TB with a contribution table is spread over TB_CRC_SLICE_BYTES ranges (a max-TBS TB of one
+  // workgroup would otherwise serialise ~150 KB of byte-table steps); without a table it stays one slice.
+  std::vector<tb_crc_slice> slices;
+  for (uint32_t t = 0; t < nof_tbs; ++t) {
+    const uint32_t step = tbd[t].table != NO_CRC_TABLE ? TB_CRC_SLICE_BYTES : std::max(tbd[t].nbytes, 1u);
+    for (uint32_t b = 0; b < std::max(tbd[t].nbytes, 1u); b += step) {
+      slices.push_back({t, b, std::min(b + step, tbd[t].nbytes)});
+    }
+  }
   auto* plan      = new srsgpu_pdsch_encoder_plan();
   plan->ctx       = ctx;
   plan->nof_tbs   = static_cast<int>(nof_tbs);
+  plan->nof_slices = static_cast<int>(slices.size());
   plan->out_begin = nof_tbs ? out_begin : 0;
   plan->out_end   = out_end;
   bool ok         = true;
   if (nof_tbs > 0) {
     ok = hipMalloc(&plan->d_tb, tbd.size() * sizeof(tb_crc_desc)) == hipSuccess &&
          hipMemcpy(plan->d_tb, tbd.data(), tbd.size() * sizeof(tb_crc_desc), hipMemcpyHostToDevice) == hipSuccess &&
-         hipMalloc(&plan->d_tb_crc, tbd.size() * sizeof(uint32_t)) == hipSuccess;
+         hipMalloc(&plan->d_tb_crc, tbd.size() * sizeof(uint32_t)) == hipSuccess &&
+         hipMalloc(&plan->d_slices, slices.size() * sizeof(tb_crc_slice)) == hipSuccess &&
+         hipMemcpy(plan->d_slices, slices.data(), slices.size() * sizeof(tb_crc_slice), hipMemcpyHostToDevice) ==
+             hipSuccess;
   }
   for (int b = 0; b < 2 && ok; ++b) {
     plan->count[b]    = static_cast<int>(encs[b].size());
@@ -1010,7 +1027,9 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
     return fail(SRSGPU_ERR_HIP, "failed to upload encoder descriptors");
   }
   plan->inline_tb_crc = plan->count[0] == 0 && plan->count[1] == 0 &&
-                        std::all_of(tbd.begin(), tbd.end(), [](const tb_crc_desc& t) { return t.table != NO_CRC_TABLE; });
+                        std::all_of(tbd.begin(), tbd.end(), [](const tb_crc_desc& t) {
+                          return t.table != NO_CRC_TABLE && t.nbytes <= TB_CRC_INLINE_MAX_BYTES;
+                        });
   guard.commit(plan->crc_refs);
   *plan_out = plan;
   return SRSGPU_OK;
@@ -1037,8 +1056,9 @@ int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
   if (plan->out_end > plan->out_begin) {
     HIP_TRY(hipMemsetAsync(d_codewords + plan->out_begin, 0, plan->out_end - plan->out_begin, s));
   }
-  if (!plan->inline_tb_crc) {
-    launch_tb_crc(plan->d_tb, plan->nof_tbs, d_tbs, plan->d_tb_crc, plan->ctx->d_crc_arena, s);
+  if (!plan->inline_tb_crc && plan->nof_tbs > 0) {
+    HIP_TRY(hipMemsetAsync(plan->d_tb_crc, 0, static_cast<size_t>(plan->nof_tbs) * sizeof(uint32_t), s));
+    launch_tb_crc(plan->d_tb, plan->d_slices, plan->nof_slices, d_tbs, plan->d_tb_crc, plan->ctx->d_crc_arena, s);
     HIP_TRY(hipGetLastError());
   }
   stage_timer::mark(ev, 1, s);
@@ -1091,7 +1111,8 @@ void srsgpu_pdsch_encoder_plan_destroy(srsgpu_pdsch_encoder_plan* plan)
     std::lock_guard<std::mutex> lock(plan->ctx->mtx);
     crc_release_locked(plan->ctx, plan->crc_refs);
   }
-  for (void* p : {static_cast<void*>(plan->d_tb), static_cast<void*>(plan->d_tb_crc), static_cast<void*>(plan->d_enc[0]),
+  for (void* p : {static_cast<void*>(plan->d_tb), static_cast<void*>(plan->d_tb_crc), static_cast<void*>(plan->d_slices),
+                  static_cast<void*>(plan->d_enc[0]),
                   static_cast<void*>(plan->d_enc[1])}) {
     if (p != nullptr) {
       (void)hipFree(p);
@@ -1157,6 +1178,9 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
   auto* plan    = new srsgpu_pusch_decoder_plan();
   plan->ctx     = ctx;
   plan->nof_tbs = static_cast<int>(nof_tbs);
+  plan->tb_threads = std::any_of(tbs.begin(), tbs.end(), [](const tb_dec_desc& t) {
+                       return t.tbs_bits / 8u > TB_CRC_INLINE_MAX_BYTES;
+                     }) ? 1024 : 256;
   int r         = upload_pusch_cb_plan(ctx, impl, batch, dms, &plan->cbs);
   if (r != SRSGPU_OK) {
     delete plan;
@@ -1211,7 +1235,7 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
   }
   stage_timer::mark(evd, 1, s);
   stage_timer::mark(ev, 2, s);
-  launch_pusch_tb(plan->d_tb, plan->nof_tbs, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, plan->ctx->d_crc_arena, s);
+  launch_pusch_tb(plan->d_tb, plan->nof_tbs, plan->tb_threads, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, plan->ctx->d_crc_arena, s);
   HIP_TRY(hipGetLastError());
   stage_timer::mark(ev, 3, s);
   return SRSGPU_OK;

@@ -25,13 +25,15 @@ __device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b, uint32_t 
   return r;
 }
 
-/// CRC (order 8..24, g including x^order) of data[0..n) computed by a 256-lane workgroup. `table` and `part` are
-/// 256-entry LDS scratch arrays. Returns the CRC in every lane. Must be called by all 256 lanes.
+/// CRC (order 8..24, g including x^order) of data[0..n) computed by the first 256 lanes of the workgroup (any larger
+/// lanes only take part in the barriers). `table` and `part` are 256-entry LDS scratch arrays. Returns the CRC in every
+/// lane. Must be called by all lanes.
 __device__ inline uint32_t block_crc_bytes(const uint8_t* data, int n, int order, uint32_t g, uint32_t* table,
                                            uint32_t* part)
 {
   const uint32_t mask = (1u << order) - 1u;
-  {
+  const bool     in   = threadIdx.x < 256u;
+  if (in) {
     uint32_t r = static_cast<uint32_t>(threadIdx.x) << (order - 8);
     for (int k = 0; k < 8; ++k) {
       r <<= 1;
@@ -45,13 +47,15 @@ __device__ inline uint32_t block_crc_bytes(const uint8_t* data, int n, int order
   const int cs  = (n + 255) / 256;
   const int pad = cs * 256 - n;
   uint32_t  rem = 0;
-  for (int p = threadIdx.x * cs; p < (threadIdx.x + 1) * cs; ++p) {
+  for (int p = threadIdx.x * cs; in && p < (threadIdx.x + 1) * cs; ++p) {
     const int i = p - pad;
     if (i >= 0) {
       rem = ((rem << 8) ^ table[((rem >> (order - 8)) ^ data[i]) & 0xffu]) & mask;
     }
   }
-  part[threadIdx.x] = rem;
+  if (in) {
+    part[threadIdx.x] = rem;
+  }
   __syncthreads();
   uint32_t f = 1u;  // x^(8 cs) mod g by square-and-multiply
   {
@@ -66,7 +70,7 @@ __device__ inline uint32_t block_crc_bytes(const uint8_t* data, int n, int order
     }
   }
   for (int step = 1; step < 256; step <<= 1) {
-    if ((threadIdx.x % (2 * step)) == 0) {
+    if (in && (threadIdx.x % (2 * step)) == 0) {
       part[threadIdx.x] = gf2_mulmod(part[threadIdx.x], f, g, order) ^ part[threadIdx.x + step];
     }
     f = gf2_mulmod(f, f, g, order);
@@ -148,15 +152,17 @@ __device__ __forceinline__ uint32_t gf2_mulmod(uint32_t r, uint32_t M, int order
 /// registers: one table load per chunk instead of one per remainder bit (those uncoalesced loads made the kernels
 /// texture-addresser bound). `lut` from crc_byte_lut; `red` one word per wave of LDS scratch. All lanes must call it;
 /// returns the CRC in every lane.
+/// [begin, end) (begin a multiple of CS; default the whole message) restricts the sum to that byte range's chunks: their
+/// contribution to the CRC of the whole nbytes-byte message (the CRC is linear, so slices XOR together).
 template <int CS, typename Data>
 __device__ inline uint32_t block_crc_chunks(Data data, int nbytes, const uint32_t* P, int order, uint32_t g,
-                                            const uint32_t* lut, uint32_t* red)
+                                            const uint32_t* lut, uint32_t* red, int begin = 0, int end = -1)
 {
   const uint32_t mask = (1u << order) - 1u;
   const int      L    = 8 * nbytes;
-  const int      nch  = (nbytes + CS - 1) / CS;
+  const int      nch  = ((end < 0 ? nbytes : end) + CS - 1) / CS;
   uint32_t       acc  = 0;
-  for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+  for (int c = begin / CS + static_cast<int>(threadIdx.x); c < nch; c += blockDim.x) {
     const int b0  = c * CS;
     const int b1  = min(b0 + CS, nbytes);
     const int j   = 8 * b1 + order - 1;

@@ -51,15 +51,18 @@ __device__ __forceinline__ int rot(int z, int s, int Z)
   return static_cast<int>(p0 < p1 ? p0 : p1);
 }
 
-/// CRC of every transport block (TS 38.212 §5.1): one 256-lane workgroup per transport block (crc_device.h).
+/// CRC of every transport block (TS 38.212 §5.1): one 256-lane workgroup per TB slice (crc_device.h), each XORing its
+/// slice's contribution into the TB's (zeroed) CRC word.
 __global__ __launch_bounds__(256) void tb_crc_kernel(const tb_crc_desc* __restrict__ descs,
+                                                     const tb_crc_slice* __restrict__ slices,
                                                      const uint8_t* __restrict__ tbs,
                                                      uint32_t* __restrict__ crcs,
                                                      const uint32_t* __restrict__ crc_tables)
 {
   __shared__ uint32_t table[256];
   __shared__ uint32_t part[256];
-  const tb_crc_desc d = descs[blockIdx.x];
+  const tb_crc_slice sl = slices[blockIdx.x];
+  const tb_crc_desc  d  = descs[sl.tb];
   // Chunked byte-table CRC moved by the per-bit contribution table when the plan could cache one for this length,
   // else the byte table with pairwise GF(2) combination.
   uint32_t crc;
@@ -67,13 +70,14 @@ __global__ __launch_bounds__(256) void tb_crc_kernel(const tb_crc_desc* __restri
     crc_byte_lut(table, static_cast<int>(d.order), d.poly);
     const uint8_t* tb = tbs + d.byte_offset;
     crc = block_crc_chunks<16>([tb](int i) { return tb[i]; }, static_cast<int>(d.nbytes), crc_tables + d.table,
-                               static_cast<int>(d.order), d.poly, table, part);
-  } else {
+                               static_cast<int>(d.order), d.poly, table, part, static_cast<int>(sl.begin),
+                               static_cast<int>(sl.end));
+  } else {  // one slice: the whole TB
     crc = block_crc_bytes(tbs + d.byte_offset, static_cast<int>(d.nbytes), static_cast<int>(d.order), d.poly, table,
                           part);
   }
   if (threadIdx.x == 0) {
-    crcs[blockIdx.x] = crc;
+    atomicXor(&crcs[sl.tb], crc);
   }
 }
 
@@ -610,11 +614,16 @@ void launch_pdsch_encode_packed(int              bg,
   }
 }
 
-void launch_tb_crc(const tb_crc_desc* d_desc, int nof_tbs, const uint8_t* d_tbs, uint32_t* d_crcs,
-                   const uint32_t* d_crc_tables, hipStream_t s)
+void launch_tb_crc(const tb_crc_desc*  d_desc,
+                   const tb_crc_slice* d_slices,
+                   int                 nof_slices,
+                   const uint8_t*      d_tbs,
+                   uint32_t*           d_crcs,
+                   const uint32_t*     d_crc_tables,
+                   hipStream_t         s)
 {
-  if (nof_tbs > 0) {
-    tb_crc_kernel<<<nof_tbs, 256, 0, s>>>(d_desc, d_tbs, d_crcs, d_crc_tables);
+  if (nof_slices > 0) {
+    tb_crc_kernel<<<nof_slices, 256, 0, s>>>(d_desc, d_slices, d_tbs, d_crcs, d_crc_tables);
   }
 }
 

@@ -25,7 +25,7 @@
 namespace srsgpu {
 namespace {
 
-constexpr int CHEST_THREADS = 64;  // one wavefront
+constexpr int CHEST_THREADS = 64;  // one wavefront per job (multi-wave workgroups for large allocations: T)
 constexpr int CHEST_VP      = 12;  // MAX_V_PILOTS
 
 struct cpx {
@@ -51,6 +51,26 @@ __device__ __forceinline__ float wave_sum(float v)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     v += __shfl_xor(v, o);
+  }
+  return v;
+}
+
+/// Sum over the workgroup of T lanes (every lane gets the result; all lanes must call it). T = 64: wave shuffles only.
+template <int T>
+__device__ __forceinline__ float block_sum(float v, float* red)
+{
+  v = wave_sum(v);
+  if constexpr (T > 64) {
+    __syncthreads();  // red may still be read by a previous reduction
+    if ((threadIdx.x & 63u) == 0) {
+      red[threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    v = 0.f;
+#pragma unroll
+    for (int w = 0; w < T / 64; ++w) {
+      v += red[w];
+    }
   }
   return v;
 }
@@ -185,6 +205,30 @@ __device__ __forceinline__ void wave_argmax(float& v, int& idx)
   }
 }
 
+/// wave_argmax over the workgroup of T lanes (lowest index among equal maxima; all lanes must call it).
+template <int T>
+__device__ __forceinline__ void block_argmax(float& v, int& idx, float* redf, int* redi)
+{
+  wave_argmax(v, idx);
+  if constexpr (T > 64) {
+    __syncthreads();
+    if ((threadIdx.x & 63u) == 0) {
+      redf[threadIdx.x >> 6] = v;
+      redi[threadIdx.x >> 6] = idx;
+    }
+    __syncthreads();
+    v   = redf[0];
+    idx = redi[0];
+#pragma unroll
+    for (int w = 1; w < T / 64; ++w) {
+      if (redf[w] > v || (redf[w] == v && redi[w] < idx)) {
+        v   = redf[w];
+        idx = redi[w];
+      }
+    }
+  }
+}
+
 /// LDS of a job, carved from the plan-sized dynamic allocation (chest_geom): the staged sequence words, the filter
 /// taps, the smoothed planes F and one region shared by the LSE stage (Y per DM-RS symbol + enlarged E per layer) and
 /// the time-alignment stage (the DFT buffer X + the correlation), which run one after the other.
@@ -206,7 +250,8 @@ __device__ __host__ inline size_t chest_region_bytes(const chest_geom& g)
   return lse > ta ? lse : ta;
 }
 
-__global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void pusch_chest_kernel(
+template <int T>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void pusch_chest_kernel(
     const chest_job* __restrict__ jobs,
     chest_geom geom,
     const uint32_t* __restrict__ grids,
@@ -218,6 +263,8 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
     const float2* __restrict__ lp)
 {
   extern __shared__ __align__(16) unsigned char lds_raw[];
+  __shared__ float redf[T / 64];
+  __shared__ int   redi[T / 64];
   const int EN = geom.max_pilots + 2 * CHEST_VP;
   chest_lds L;
   L.F    = reinterpret_cast<cpx*>(lds_raw);
@@ -246,7 +293,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
   }
   const int nwords = static_cast<int>(((n0 & 31u) + 2u * static_cast<uint32_t>(jb.span_pilots) + 31u) >> 5);
   for (int s = 0; s < D; ++s) {
-    for (int wl = lane; wl < nwords; wl += CHEST_THREADS) {
+    for (int wl = lane; wl < nwords; wl += T) {
       L.seq[s * W + wl] = gseq[jb.gseq_base + static_cast<uint32_t>(s * nwords + wl)];
     }
   }
@@ -254,7 +301,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
 
   // Pass 1: LSE of every DM-RS symbol (received x conj(pilot)), EPRE.
   float epre_acc = 0.f;
-  for (int i = lane; i < N; i += CHEST_THREADS) {
+  for (int i = lane; i < N; i += T) {
     const uint32_t k = pilot_subcarrier(jb, crbs, i);
     const int      m = pilot_seq_index(jb, crbs, i);
     for (int s = 0; s < D; ++s) {
@@ -272,18 +319,18 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
   float      cfo     = 0.f;
   if (has_cfo) {
     float ar = 0.f, ai = 0.f;
-    for (int i = lane; i < N; i += CHEST_THREADS) {
+    for (int i = lane; i < N; i += T) {
       const cpx a = L.Y[NP + i], b = L.Y[i];
       ar += a.x * b.x + a.y * b.y;
       ai += a.y * b.x - a.x * b.y;
     }
-    ar  = wave_sum(ar);
-    ai  = wave_sum(ai);
+    ar  = block_sum<T>(ar, redf);
+    ai  = block_sum<T>(ai, redf);
     cfo = atan2f(ai, ar) / CHEST_TWOPI / (jb.epochs[jb.dmrs_symbols[1]] - jb.epochs[jb.dmrs_symbols[0]]);
     if (jb.compensate_cfo) {
       for (int s = 0; s < D; ++s) {
         const cpx r = polar1(-CHEST_TWOPI * jb.epochs[jb.dmrs_symbols[s]] * cfo);
-        for (int i = lane; i < N; i += CHEST_THREADS) {
+        for (int i = lane; i < N; i += T) {
           L.Y[s * NP + i] = cmul(L.Y[s * NP + i], r);
         }
       }
@@ -301,7 +348,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
     cpx* const E0 = L.E;
     cpx* const E1 = L.E + EN;
     if (GL == 2) {
-      for (int j = lane; j < N / 2; j += CHEST_THREADS) {
+      for (int j = lane; j < N / 2; j += T) {
         cpx a = L.Y[q * NP + 2 * j], b = L.Y[q * NP + 2 * j + 1];
         if (!jb.td_interp) {
           for (int s = 1; s < D; ++s) {
@@ -315,7 +362,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
         E1[CHEST_VP + 2 * j] = E1[CHEST_VP + 2 * j + 1] = h1;
       }
     } else {
-      for (int i = lane; i < N; i += CHEST_THREADS) {
+      for (int i = lane; i < N; i += T) {
         cpx z = L.Y[q * NP + i];
         if (!jb.td_interp) {
           for (int s = 1; s < D; ++s) {
@@ -331,9 +378,11 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
       cpx* F = Fbase + (q * GL + ly) * NP;
       if (jb.fd == CHEST_FD_FILTER) {
         const int nv = jb.nof_v_pilots;
-        virtual_pilots(E, N, nv);
+        if (lane < 64) {  // the first wave extrapolates both band edges
+          virtual_pilots(E, N, nv);
+        }
         __syncthreads();
-        for (int i = lane; i < N; i += CHEST_THREADS) {
+        for (int i = lane; i < N; i += T) {
           cpx acc = {0.f, 0.f};
           for (int j = 0; j < nt; ++j) {
             const int e = CHEST_VP + i - c + j;  // symmetric taps: correlation == convolution
@@ -346,17 +395,17 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
         }
       } else if (jb.fd == CHEST_FD_MEAN) {
         float sx = 0.f, sy = 0.f;
-        for (int i = lane; i < N; i += CHEST_THREADS) {
+        for (int i = lane; i < N; i += T) {
           sx += E[CHEST_VP + i].x;
           sy += E[CHEST_VP + i].y;
         }
-        sx = wave_sum(sx) / static_cast<float>(N);
-        sy = wave_sum(sy) / static_cast<float>(N);
-        for (int i = lane; i < N; i += CHEST_THREADS) {
+        sx = block_sum<T>(sx, redf) / static_cast<float>(N);
+        sy = block_sum<T>(sy, redf) / static_cast<float>(N);
+        for (int i = lane; i < N; i += T) {
           F[i] = {sx, sy};
         }
       } else {
-        for (int i = lane; i < N; i += CHEST_THREADS) {
+        for (int i = lane; i < N; i += T) {
           F[i] = E[CHEST_VP + i];
         }
       }
@@ -367,7 +416,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
   // RSRP of layer 0 over the planes, and the noise residual (group 0 only) against the time-averaged estimate
   // beta / Q sum_q F_q, re-rotated by the CFO when compensating (estimate_noise, :422).
   float rsrp_acc = 0.f, noise_acc = 0.f;
-  for (int i = lane; i < N; i += CHEST_THREADS) {
+  for (int i = lane; i < N; i += T) {
     cpx h = {0.f, 0.f};
     for (int q = 0; q < Q; ++q) {
       const cpx f0 = Fbase[(q * GL) * NP + i];
@@ -396,9 +445,10 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
     }
   }
   const float nof_pilots = static_cast<float>(N * D);
-  const float epre       = wave_sum(epre_acc) / nof_pilots;
-  const float rsrp = wave_sum(rsrp_acc) * beta * beta * static_cast<float>(D) / static_cast<float>(Q) / nof_pilots;
-  const float noise_sum = wave_sum(noise_acc);
+  const float epre       = block_sum<T>(epre_acc, redf) / nof_pilots;
+  const float rsrp =
+      block_sum<T>(rsrp_acc, redf) * beta * beta * static_cast<float>(D) / static_cast<float>(Q) / nof_pilots;
+  const float noise_sum = block_sum<T>(noise_acc, redf);
 
   // Time alignment of the smoothed layer-0 planes (estimate_time_alignment, port_channel_estimator_helpers.cpp:246 ->
   // time_alignment_estimator_dft_impl): inverse DFT of size M through LDS (radix 2, bit-reversed scatter), |.|^2
@@ -408,19 +458,19 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
     const int lgM = jb.ta_log2;
     __syncthreads();  // Y / E are dead: the region becomes X / corr
     for (int q = 0; q < Q; ++q) {
-      for (int n = lane; n < M; n += CHEST_THREADS) {
+      for (int n = lane; n < M; n += T) {
         L.X[n] = {0.f, 0.f};
       }
       __syncthreads();
       const uint32_t k0 = pilot_subcarrier(jb, crbs, 0);
-      for (int i = lane; i < N; i += CHEST_THREADS) {
+      for (int i = lane; i < N; i += T) {
         const uint32_t pos = jb.ta_positions ? pilot_subcarrier(jb, crbs, i) - k0 : static_cast<uint32_t>(i);
         L.X[__brev(pos) >> (32 - lgM)] = Fbase[(q * GL) * NP + i];
       }
       __syncthreads();
       for (int lh = 0; lh < lgM; ++lh) {
         const int h = 1 << lh;
-        for (int b = lane; b < M / 2; b += CHEST_THREADS) {
+        for (int b = lane; b < M / 2; b += T) {
           const int   j  = b & (h - 1);
           const int   i0 = ((b >> lh) << (lh + 1)) + j;
           const float r  = static_cast<float>(j) / static_cast<float>(2 * h);  // revolutions: e^{+j 2 pi j / 2h}
@@ -432,7 +482,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
         }
         __syncthreads();
       }
-      for (int n = lane; n < M; n += CHEST_THREADS) {
+      for (int n = lane; n < M; n += T) {
         const float p = L.X[n].x * L.X[n].x + L.X[n].y * L.X[n].y;
         L.corr[n]     = q ? L.corr[n] + p : p;
       }
@@ -441,7 +491,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
     const int m  = jb.ta_max;
     float     dv = -INFINITY, av = -INFINITY;
     int       di = 0x7fffffff, ai = 0x7fffffff;
-    for (int n = lane; n < m; n += CHEST_THREADS) {
+    for (int n = lane; n < m; n += T) {
       if (L.corr[n] > dv) {
         dv = L.corr[n];
         di = n;
@@ -451,8 +501,8 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
         ai = n;
       }
     }
-    wave_argmax(dv, di);
-    wave_argmax(av, ai);
+    block_argmax<T>(dv, di, redf, redi);
+    block_argmax<T>(av, ai, redf, redi);
     const int idx  = (dv >= av) ? di : -(m - ai);
     float     frac = 0.f;
     if (M != 4096) {
@@ -514,7 +564,7 @@ __global__ __launch_bounds__(CHEST_THREADS) __attribute__((amdgpu_waves_per_eu(8
     return {(b.x - a.x) * w + a.x, (b.y - a.y) * w + a.y};
   };
   const bool rotate_out = rotate && !jb.compact_cfo;
-  for (int k = lane; k < nre; k += CHEST_THREADS) {
+  for (int k = lane; k < nre; k += T) {
     // PRB k / 12 of the interpolated band is the (k / 12)-th allocated CRB (compute_hop maps the band PRB by PRB).
     const int kr = alloc_rb(jb, crbs, k / 12) * 12 + k % 12;
     for (int ly = 0; ly < GL; ++ly) {
@@ -566,9 +616,20 @@ void launch_pusch_chest(const float2*   d_lp,
     return;
   }
   const size_t lds = pusch_chest_lds_bytes(geom);
-  hipLaunchKernelGGL(pusch_chest_kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(CHEST_THREADS),
-                     static_cast<unsigned>(lds), stream, d_jobs, geom, d_grids, d_ce, d_noise_var, d_metrics, d_seq,
-                     d_crbs, d_lp);
+  // One wave per job for the usual few-RB allocations (many jobs resident together); a job with hundreds of pilots
+  // (a wideband allocation: few jobs, each a long serial chain on one wave) spreads over 4 or 16 waves.
+  const auto launch = [&](auto kernel, int threads) {
+    hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(static_cast<unsigned>(threads)),
+                       static_cast<unsigned>(lds), stream, d_jobs, geom, d_grids, d_ce, d_noise_var, d_metrics, d_seq,
+                       d_crbs, d_lp);
+  };
+  if (geom.max_pilots > 512) {
+    launch(pusch_chest_kernel<1024>, 1024);
+  } else if (geom.max_pilots > 128) {
+    launch(pusch_chest_kernel<256>, 256);
+  } else {
+    launch(pusch_chest_kernel<CHEST_THREADS>, CHEST_THREADS);
+  }
 }
 
 } // namespace srsgpu

@@ -21,7 +21,7 @@ __device__ __forceinline__ uint32_t cb_index(uint32_t p, uint32_t d, uint32_t m)
   return (q * d > p) ? q - 1u : q;
 }
 
-__global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __restrict__ descs,
+__global__ __launch_bounds__(1024) void pusch_tb_kernel(const tb_dec_desc* __restrict__ descs,
                                                        uint8_t* __restrict__ cb_crc_ok,
                                                        const uint8_t* __restrict__ cb_msgs,
                                                        uint8_t* __restrict__ tbs,
@@ -123,6 +123,7 @@ __global__ __launch_bounds__(256) void pusch_tb_kernel(const tb_dec_desc* __rest
 
 void launch_pusch_tb(const tb_dec_desc* d_desc,
                      int                nof_tbs,
+                     int                threads,
                      uint8_t*           d_cb_crc_ok,
                      const uint8_t*     d_cb_msgs,
                      uint8_t*           d_tbs,
@@ -131,7 +132,7 @@ void launch_pusch_tb(const tb_dec_desc* d_desc,
                      hipStream_t        stream)
 {
   if (nof_tbs > 0) {
-    pusch_tb_kernel<<<nof_tbs, 256, 0, stream>>>(d_desc, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, d_crc_tables);
+    pusch_tb_kernel<<<nof_tbs, threads, 0, stream>>>(d_desc, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, d_crc_tables);
   }
 }
 

@@ -93,8 +93,25 @@ struct enc_desc {
 };
 static_assert(sizeof(enc_desc) == 56, "enc_desc layout");
 
-void launch_tb_crc(const tb_crc_desc* d_desc, int nof_tbs, const uint8_t* d_tbs, uint32_t* d_crcs,
-                   const uint32_t* d_crc_tables, hipStream_t s);
+/// A byte range [begin, end) of transport block `tb` whose CRC contribution one tb_crc_kernel workgroup computes and
+/// XORs into the TB's CRC word (zeroed before the launch): large TBs are spread over many workgroups instead of one.
+struct tb_crc_slice {
+  uint32_t tb;
+  uint32_t begin;
+  uint32_t end;
+};
+/// Slice length (256 lanes x 16-byte chunks); TBs without a contribution table take one slice (byte-table method).
+constexpr uint32_t TB_CRC_SLICE_BYTES = 4096;
+/// Largest TB whose CRC the packed encoder computes inline (one workgroup per TB); larger ones go to tb_crc_kernel.
+constexpr uint32_t TB_CRC_INLINE_MAX_BYTES = 16384;
+
+void launch_tb_crc(const tb_crc_desc*  d_desc,
+                   const tb_crc_slice* d_slices,
+                   int                 nof_slices,
+                   const uint8_t*      d_tbs,
+                   uint32_t*           d_crcs,
+                   const uint32_t*     d_crc_tables,
+                   hipStream_t         s);
 
 void launch_pdsch_encode(int              bg,
                          const enc_desc*  d_desc,
@@ -144,8 +161,10 @@ struct tb_dec_desc {
   uint32_t crc_table;    ///< CRC24A per-bit contribution table of tbs_bits (CRC arena offset) or NO_CRC_TABLE.
 };
 
+/// threads: 256, or 1024 for plans with TBs above TB_CRC_INLINE_MAX_BYTES (the TB CRC chain per lane shrinks 4x).
 void launch_pusch_tb(const tb_dec_desc* d_desc,
                      int                nof_tbs,
+                     int                threads,
                      uint8_t*           d_cb_crc_ok,
                      const uint8_t*     d_cb_msgs,
                      uint8_t*           d_tbs,

@@ -17,6 +17,7 @@ struct srsgpu_pdsch_dmrs_plan {
   dmrs_job*       d_jobs   = nullptr;
   uint32_t*       d_seq    = nullptr;  ///< DM-RS sequence words of every job (plan lifetime).
   int             nof_jobs = 0;
+  int             max_pilots = 0;  ///< Largest job (workgroups per job of the launch).
 };
 
 struct srsgpu_pdsch_modulator_plan {
@@ -555,6 +556,9 @@ int srsgpu_pdsch_dmrs_plan_create_ex(srsgpu_context*                 ctx,
   auto* plan     = new srsgpu_pdsch_dmrs_plan();
   plan->ctx      = ctx;
   plan->nof_jobs = static_cast<int>(jobs.size());
+  for (const dmrs_job& j : jobs) {
+    plan->max_pilots = std::max(plan->max_pilots, static_cast<int>(j.nof_pilots));
+  }
   // Resident sequence words of every job, filled once.
   std::vector<uint32_t> c_inits, nwords, offsets, wstart;
   uint32_t              base = 0;
@@ -587,7 +591,7 @@ int srsgpu_pdsch_dmrs_plan_execute(const srsgpu_pdsch_dmrs_plan* plan, uint32_t*
   if (plan == nullptr || d_grids == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  launch_pdsch_dmrs(plan->d_jobs, plan->nof_jobs, d_grids, plan->d_seq, static_cast<hipStream_t>(stream));
+  launch_pdsch_dmrs(plan->d_jobs, plan->nof_jobs, plan->max_pilots, d_grids, plan->d_seq, static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
 }

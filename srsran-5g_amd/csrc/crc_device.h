@@ -167,9 +167,18 @@ __device__ inline uint32_t block_crc_chunks(Data data, int nbytes, const uint32_
     const int b1  = min(b0 + CS, nbytes);
     const int j   = 8 * b1 + order - 1;
     const uint32_t M = (j < L) ? P[j] : (1u << (order + L - 1 - j));  // issued before the chunk's serial chain
-    uint32_t  rem = 0;
-    for (int i = b0; i < b1; ++i) {
-      rem = ((rem << 8) ^ lut[((rem >> (order - 8)) ^ static_cast<uint32_t>(data(i))) & 0xffu]) & mask;
+    // The chunk's bytes are all loaded before the table chain starts (a rolled loop waited for each load in turn).
+    uint32_t byte[CS];
+#pragma unroll
+    for (int k = 0; k < CS; ++k) {
+      byte[k] = (b0 + k < b1) ? static_cast<uint32_t>(data(b0 + k)) : 0u;
+    }
+    uint32_t rem = 0;
+#pragma unroll
+    for (int k = 0; k < CS; ++k) {
+      if (b0 + k < b1) {
+        rem = ((rem << 8) ^ lut[((rem >> (order - 8)) ^ byte[k]) & 0xffu]) & mask;
+      }
     }
     acc ^= gf2_mulmod(rem, M, order, g);
   }

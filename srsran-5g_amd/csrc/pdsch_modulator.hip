@@ -201,7 +201,8 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_dmrs_kernel(const dmrs_job*
   const dmrs_job& jb     = jobs[blockIdx.x];
   const uint32_t  per_rb = jb.type2 ? 4u : 6u;
   const uint32_t  wfirst = (2 * jb.seq_offset) >> 5;
-  for (uint32_t i = threadIdx.x; i < jb.nof_pilots; i += MOD_THREADS) {
+  // blockIdx.y: a wideband job's pilots are spread over several workgroups (one loop trip each).
+  for (uint32_t i = threadIdx.x + blockIdx.y * MOD_THREADS; i < jb.nof_pilots; i += MOD_THREADS * gridDim.y) {
     const uint32_t n    = 2 * (jb.seq_offset + i);
     const uint32_t w    = n >> 5;
     const uint32_t word = gseq[jb.gseq_base + (w - wfirst)];  // the plan's resident sequence words
@@ -240,6 +241,7 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_dmrs_kernel(const dmrs_job*
 
 void launch_pdsch_dmrs(const dmrs_job* d_jobs,
                        int             nof_jobs,
+                       int             max_pilots,
                        uint32_t*       d_grids,
                        const uint32_t* d_seq,
                        hipStream_t     stream)
@@ -247,8 +249,9 @@ void launch_pdsch_dmrs(const dmrs_job* d_jobs,
   if (nof_jobs <= 0) {
     return;
   }
-  hipLaunchKernelGGL(pdsch_dmrs_kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(MOD_THREADS), 0, stream, d_jobs,
-                     d_grids, d_seq);
+  const unsigned ny = static_cast<unsigned>((max_pilots + MOD_THREADS - 1) / MOD_THREADS);
+  hipLaunchKernelGGL(pdsch_dmrs_kernel, dim3(static_cast<unsigned>(nof_jobs), ny > 0 ? ny : 1u), dim3(MOD_THREADS), 0,
+                     stream, d_jobs, d_grids, d_seq);
 }
 
 void launch_pdsch_modulate(const mod_desc*  d_desc,

@@ -394,8 +394,10 @@ struct dmrs_job {
   uint32_t gseq_base;    ///< The job's sequence words (from word seq_offset / 16) in the plan's buffer.
 };
 
+/// max_pilots: the largest nof_pilots of the jobs (sets the workgroups per job).
 void launch_pdsch_dmrs(const dmrs_job* d_jobs,
                        int             nof_jobs,
+                       int             max_pilots,
                        uint32_t*       d_grids,
                        const uint32_t* d_seq,
                        hipStream_t     stream);

@@ -215,13 +215,17 @@ class InputSet:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4000)
+    ap.add_argument("--steps", type=int, default=4000)  # >= 1 s timed at the default step shape
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--profile", choices=sorted(PROFILES), default="ref")
     ap.add_argument("--workload", choices=["multi_ue", "testmode"], default="multi_ue")
     ap.add_argument("--periods", type=int, default=2, help="testmode: TDD periods (10 slots each) per step")
-    ap.add_argument("--slots-per-step", type=int, default=16)
-    ap.add_argument("--input-sets", type=int, default=4, help="independent working sets rotated step by step")
+    # A step is a batch of 32 slots (at ~60 cells per GPU, one slot of 32 cells of a slot period, 0.27 ms < 0.5 ms);
+    # 5 input sets in flight: sweep on MI355X (profiles/r2_step_shape_sweep.txt): 16 / 4 88.0k, 16 / 2 106.2k,
+    # 32 / 2 117.9k, 32 / 4 103.8k, 32 / 5 117.9k, 64 / 3 120.5k slots/s (set counts that are multiples of the 4
+    # hardware queues serialise the sets' graph branches).
+    ap.add_argument("--slots-per-step", type=int, default=32)
+    ap.add_argument("--input-sets", type=int, default=5, help="independent working sets rotated step by step")
     ap.add_argument("--iterations", type=int, default=6)
     ap.add_argument("--snr-db", type=float, default=26.0)
     ap.add_argument("--worst-case", action="store_true", help="headline on Gaussian-noise input (all iterations)")
@@ -447,6 +451,7 @@ def main():
     # VALU roofline of the same launch: wave-level VALU instructions per launch from the committed SQ counter pass
     # (rocprofv3 --pmc SQ_INSTS_VALU ..., tools/sq_summary.py; same workload) over the live kernel time.
     valu = None
+    dec_kernel = "ldpc_decode_pk_kernel<1,1,8,*> (plain or edge-split variant)"
     sqfile = os.path.join(ROOT, "profiles", "sq_valu.json")
     if os.path.exists(sqfile):
         with open(sqfile) as f:
@@ -454,8 +459,10 @@ def main():
         # The BG1 / MODE 1 / 8-layer decoder of this workload (plain or edge-split variant).
         sq = None
         if sqj.get("workload") == wl_key:
-            sq = next((v for k, v in sqj.get("kernels", {}).items() if k.startswith("ldpc_decode_pk_kernel<1, 1, 8")),
-                      None)
+            sq_name, sq = next(((k, v) for k, v in sqj.get("kernels", {}).items()
+                                if k.startswith("ldpc_decode_pk_kernel<1, 1, 8")), (None, None))
+            if sq_name:
+                dec_kernel = sq_name.replace(" ", "")
         if sq:
             peak = 1024 * 2.4e9 / 2  # SIMDs x clock / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md)
             rate = sq["valu_instr"] / (dec_ms * 1e-3)
@@ -549,7 +556,7 @@ def main():
         "stage_ms_per_step": stage,  # from an untimed eager pass with per-stage events
         "stage_algorithmic_gbps": stage_gbps,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "ldpc_decode_pk_kernel<1,1,8,2>",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dec_kernel,
                      "kernel_ms_per_launch": dec_ms, "algorithmic_bytes_per_launch": dec_bytes,
                      "note": "algorithmic bytes per launch / decoder-stage HIP-event time on the launch stream (an "
                              "eager pass right after the timed loop); the LDPC decoder is VALU-issue/latency-bound, "

@@ -360,7 +360,7 @@ void srsgpu_pdsch_dmrs_plan_destroy(srsgpu_pdsch_dmrs_plan* plan);
 typedef struct {
   uint32_t numerology;                /* subcarrier spacing 15 kHz x 2^numerology, 0..4 */
   uint32_t bw_rb;                     /* resource grid bandwidth in RB: 12 * bw_rb < dft_size */
-  uint32_t dft_size;                  /* 2^n, 128..8192, or 3 x 2^m, 384..6144 (generic DFT sizes) */
+  uint32_t dft_size;                  /* 2^n 128..8192, 3 x 2^m 384..6144, 4608 (generic DFT sizes) */
   uint32_t cp_extended;               /* 0: normal cyclic prefix (14 symbols), 1: extended (12 symbols) */
   uint32_t nof_samples_window_offset; /* demodulator DFT window advance, < 144 * dft_size / 2048 (0: none) */
   float    scale;                     /* scaling factor at the DFT output (std::isnormal) */

@@ -76,12 +76,12 @@ int plan_create(srsgpu_context*           ctx,
   const uint32_t N   = cfg->dft_size;
   const uint32_t mu  = cfg->numerology;
   const uint32_t nsc = 12u * cfg->bw_rb;
-  // The generic DFT's sizes (dft_processor_generic_impl.cpp:211-230) up to 8192 points, except 4608 = 9 x 512.
+  // The generic DFT's sizes (dft_processor_generic_impl.cpp:211-230) up to 8192 points.
   const uint32_t m = (N % 3 == 0) ? N / 3 : N;
   const bool     pow2_ok = N >= 128 && N <= 8192 && (N & (N - 1)) == 0;
   const bool     x3_ok   = N % 3 == 0 && m >= 128 && m <= 2048 && (m & (m - 1)) == 0;
-  if (!pow2_ok && !x3_ok) {
-    return fail(SRSGPU_ERR_INVALID_ARG, "DFT size %u not supported (2^n 128..8192 or 3 x 2^m 384..6144)", N);
+  if (!pow2_ok && !x3_ok && N != 4608) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "DFT size %u not supported (2^n 128..8192, 3 x 2^m 384..6144, 4608)", N);
   }
   if (mu > 4 || cfg->bw_rb == 0 || nsc >= N) {
     return fail(SRSGPU_ERR_INVALID_ARG, "the DFT size (%u) must be greater than the resource grid size (%u)", N, nsc);

@@ -181,7 +181,7 @@ constexpr int ilog2(int n)
 {
   return n <= 1 ? 0 : 1 + ilog2(n / 2);
 }
-/// Threads per workgroup of an N-point transform: 16 values per thread (2^n) or 48 (3 * 2^m).
+/// Threads per workgroup of an N-point transform: 16 values per thread (2^n) or 48 (3 * 2^m, 9 * 2^m).
 template <int N>
 constexpr int ofdm_threads()
 {
@@ -206,15 +206,16 @@ __device__ __forceinline__ float2 twiddle_any(const float2* __restrict__ tw, uin
   return x;
 }
 
-/// One Stockham pass of the N = 3 M transform (T = N / 48 threads, B = N / (R T) butterflies each). The power-of-two
-/// passes come first: their NS divides T, so all butterflies of a thread share k = tid mod NS and the twiddles w of
-/// load_twiddles. The radix-3 pass is last (NS = M, k = j): twiddles exp(S 2 pi i r j / N) by sincospi.
+/// One Stockham pass of the N = 3^a M transform (a = 1, 2; T = N / 48 threads, B = N / (R T) butterflies each). The
+/// power-of-two passes come first: their NS divides T, so all butterflies of a thread share k = tid mod NS and the
+/// twiddles w of load_twiddles. The radix-3 passes are last (NS = M, then 3 M): twiddles exp(S 2 pi i r k / (3 NS)),
+/// k = j mod NS, by sincospi (argument rounded once: phase error < 3e-7 rad).
 template <int N, int R, int NS, int S, typename Src, typename Dst>
 __device__ __forceinline__ void stockham_pass3(const float2 (&w)[16], Src src, Dst dst)
 {
   constexpr int T = N / 48;
   constexpr int B = N / (R * T);
-  static_assert(R == 3 ? NS == N / 3 : (T % NS == 0 || NS == 1), "pass order: powers of two, then radix 3");
+  static_assert(R == 3 || T % NS == 0 || NS == 1, "pass order: powers of two, then radix 3");
   float2    v[B][R];
   const int tid = static_cast<int>(threadIdx.x);
 #pragma unroll
@@ -229,11 +230,14 @@ __device__ __forceinline__ void stockham_pass3(const float2 (&w)[16], Src src, D
 #pragma unroll
   for (int b = 0; b < B; ++b) {
     const int j = tid + b * T;
-    const int k = (R == 3) ? j : (j & (NS - 1));
+    const int k = (R == 3) ? j % NS : (j & (NS - 1));
     if constexpr (R == 3) {
 #pragma unroll
       for (int r = 1; r < 3; ++r) {
-        v[b][r] = cmul(v[b][r], twiddle_any<N, S>(nullptr, static_cast<uint32_t>(r * j)));
+        float2 x;
+        sincospif(static_cast<float>(2 * r * k) / static_cast<float>(3 * NS), &x.y, &x.x);
+        x.y     = S * x.y;
+        v[b][r] = cmul(v[b][r], x);
       }
     } else if constexpr (NS > 1) {
 #pragma unroll
@@ -251,16 +255,17 @@ __device__ __forceinline__ void stockham_pass3(const float2 (&w)[16], Src src, D
   __syncthreads();
 }
 
-/// N = 3 M: power-of-two passes of M (first radix 2^(m mod 4) or 16, then 16s), then radix 3.
+/// N = 3^a M: power-of-two passes of M (first radix 2^(m mod 4) or 16, then 16s), then a radix-3 passes.
 template <int N, int S, typename Src, typename Dst>
 __device__ __forceinline__ void dft_lds3(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
 {
-  constexpr int M   = N / 3;
+  constexpr int A3  = (N % 9 == 0) ? 9 : 3;
+  constexpr int M   = N / A3;
   constexpr int LM  = ilog2(M);
   constexpr int REM = LM % 4;
   constexpr int R0  = REM ? (1 << REM) : 16;
   constexpr int NP  = LM / 4 + (REM ? 1 : 0);
-  static_assert(3 * M == N && is_pow2(M) && NP >= 2 && NP <= 3, "supported DFT sizes: 3 x (128..2048)");
+  static_assert(A3 * M == N && is_pow2(M) && NP >= 2 && NP <= 3, "supported DFT sizes: 3 x (128..2048), 9 x 512");
   auto   ld = [lds](int i) { return lds[i]; };
   auto   st = [lds](int i, float2 v) { lds[i] = v; };
   float2 w0[16] = {}, w1[1][16], w2[1][16];
@@ -273,7 +278,12 @@ __device__ __forceinline__ void dft_lds3(float2* lds, const float2* __restrict__
   if constexpr (NP == 3) {
     stockham_pass3<N, 16, R0 * 16, S>(w2[0], ld, st);
   }
-  stockham_pass3<N, 3, M, S>(w0, ld, dst_last);
+  if constexpr (A3 == 9) {
+    stockham_pass3<N, 3, M, S>(w0, ld, st);
+    stockham_pass3<N, 3, 3 * M, S>(w0, ld, dst_last);
+  } else {
+    stockham_pass3<N, 3, M, S>(w0, ld, dst_last);
+  }
 }
 
 template <int LOG2N, int S, typename Src, typename Dst>
@@ -455,6 +465,7 @@ void launch_ofdm(bool            inverse,
     case 768: launch_one<768>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
     case 1536: launch_one<1536>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
     case 3072: launch_one<3072>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    case 4608: launch_one<4608>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
     case 6144: launch_one<6144>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
     default: break;
   }

@@ -307,7 +307,7 @@ struct ofdm_job {
 /// Largest DFT size and the twiddle table exp(-j 2 pi m / OFDM_MAX_DFT), m < OFDM_MAX_DFT, every size strides through.
 constexpr uint32_t OFDM_MAX_DFT = 8192;
 
-/// dft_size: a power of two 128..8192 or 3 x 2^m, 384..6144.
+/// dft_size: a power of two 128..8192, 3 x 2^m 384..6144 or 4608 (9 x 512).
 void launch_ofdm(bool            inverse,
                  uint32_t        dft_size,
                  const ofdm_job* d_jobs,

@@ -29,6 +29,7 @@ CASES = [
     (0, 52, 768, False, 0.1, 1.8e9, 0, 3),              # 10 MHz 15 kHz, 11.52 Msps
     (2, 51, 768, False, 0.3, 28e9, 3, 0),               # 60 kHz
     (1, 273, 6144, False, 1.0 / 96, 3.5e9, 0, 20),      # 100 MHz, 184.32 Msps
+    (1, 273, 4608, False, 1.0 / 72, 3.5e9, 1, 11),      # 100 MHz, 138.24 Msps (9 x 512: two radix-3 passes)
 ]
 
 

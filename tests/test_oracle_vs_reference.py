@@ -242,7 +242,7 @@ def test_pdsch_modulator_multi_prg_reference_defect(orc, ref):
         assert np.array_equal(got[:, l0, :48], want[:, l0, :48]), cfg
 
 
-@pytest.mark.parametrize("case", range(18))
+@pytest.mark.parametrize("case", range(19))
 def test_ofdm_oracle_vs_reference(ref, case):
     """OFDM modulator and demodulator restatement (oracle/ofdm_oracle.py, complex128) against the reference's
     ofdm_slot_modulator_impl / ofdm_slot_demodulator_impl with its generic float DFT: slot sizes equal, modulated

@@ -219,7 +219,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--profile", choices=sorted(PROFILES), default="ref")
     ap.add_argument("--workload", choices=["multi_ue", "testmode"], default="multi_ue")
-    ap.add_argument("--periods", type=int, default=2, help="testmode: TDD periods (10 slots each) per step")
+    # testmode: 4 TDD periods per step (40 slots, 0.18 ms); MI355X sweep: 2 periods 142.7k (5 sets) / 159.2k (3 sets),
+    # 4 periods 227.9k slots/s (profiles/r2_step_shape_sweep.txt).
+    ap.add_argument("--periods", type=int, default=4, help="testmode: TDD periods (10 slots each) per step")
     # A step is a batch of 32 slots (at ~60 cells per GPU, one slot of 32 cells of a slot period, 0.27 ms < 0.5 ms);
     # 5 input sets in flight: sweep on MI355X (profiles/r2_step_shape_sweep.txt): 16 / 4 88.0k, 16 / 2 106.2k,
     # 32 / 2 117.9k, 32 / 4 103.8k, 32 / 5 117.9k, 64 / 3 120.5k slots/s (set counts that are multiples of the 4

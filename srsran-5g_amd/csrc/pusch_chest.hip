@@ -168,7 +168,7 @@ __device__ __forceinline__ int alloc_rb(const chest_job& jb, const uint16_t* __r
 /// Pilot subcarrier of pilot i relative to the first allocated subcarrier.
 __device__ __forceinline__ uint32_t pilot_subcarrier(const chest_job& jb, const uint16_t* __restrict__ crbs, int i)
 {
-  const int rb = i / jb.pilots_per_rb;
+  const int rb = jb.pilots_per_rb == 6 ? i / 6 : i / 4;  // constant divisors: multiply-shift, not a division
   return static_cast<uint32_t>(alloc_rb(jb, crbs, rb) * 12 +
                                ((jb.pattern >> (4 * (i - rb * jb.pilots_per_rb))) & 15u));
 }
@@ -177,7 +177,7 @@ __device__ __forceinline__ uint32_t pilot_subcarrier(const chest_job& jb, const 
 /// unallocated CRBs (dmrs_helper.cpp:64 dmrs_sequence_generate over rb_mask).
 __device__ __forceinline__ int pilot_seq_index(const chest_job& jb, const uint16_t* __restrict__ crbs, int i)
 {
-  const int rb = i / jb.pilots_per_rb;
+  const int rb = jb.pilots_per_rb == 6 ? i / 6 : i / 4;
   return alloc_rb(jb, crbs, rb) * jb.pilots_per_rb + (i - rb * jb.pilots_per_rb);
 }
 
@@ -354,6 +354,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
     }
   }
   const bool rotate = has_cfo && jb.compensate_cfo;
+  // Per-symbol CFO rotations e^{j 2 pi epoch_l cfo} of the noise residual, once per job instead of once per pilot.
+  __shared__ cpx srot[14];
+  if (rotate) {
+    if (lane < 14) {
+      srot[lane] = polar1(CHEST_TWOPI * jb.epochs[lane] * cfo);
+    }
+    __syncthreads();
+  }
 
   // Planes: "average" combines the DM-RS symbols into one LSE scaled by 1 / (beta D); "interpolate" keeps one per
   // DM-RS symbol scaled by 1 / beta. Each is despread (two-layer groups), then smoothed in frequency into F.
@@ -453,7 +461,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
         const cpx y = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
         cpx       q = cmul(h, dmrs_value(jb, lp, L.seq, W, s, n0, m, i));
         if (rotate) {
-          q = cmul(q, polar1(CHEST_TWOPI * jb.epochs[jb.dmrs_symbols[s]] * cfo));
+          q = cmul(q, srot[jb.dmrs_symbols[s]]);
         }
         const float ex = y.x - q.x, ey = y.y - q.y;
         noise_acc += ex * ex + ey * ey;
@@ -574,7 +582,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
     if (k >= last) {
       return F[N - 1];
     }
-    const int   i = (k - offset) / stride;
+    const int   i = stride == 2 ? (k - offset) >> 1 : (k - offset) / stride;  // k > offset here
     const float w = static_cast<float>((k - offset) - i * stride) / static_cast<float>(stride);
     const cpx   a = F[i], b = F[i + 1];
     return {(b.x - a.x) * w + a.x, (b.y - a.y) * w + a.y};
@@ -597,6 +605,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
         }
         uint32_t u = to_bf16c(v);
         if (rotate_out) {
+          // polar1 inline (not srot): keeps the per-symbol layout bit-identical to the demodulator's rotation of the
+          // compact layout (same expression, same FMA contraction).
           u = to_bf16c(cmul(bf16c(u), polar1(CHEST_TWOPI * jb.epochs[l] * cfo)));
         }
         dst[l * jb.nsc] = u;

@@ -1178,9 +1178,15 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
   auto* plan    = new srsgpu_pusch_decoder_plan();
   plan->ctx     = ctx;
   plan->nof_tbs = static_cast<int>(nof_tbs);
-  plan->tb_threads = std::any_of(tbs.begin(), tbs.end(), [](const tb_dec_desc& t) {
-                       return t.tbs_bits / 8u > TB_CRC_INLINE_MAX_BYTES;
-                     }) ? 1024 : 256;
+  // 1 024 lanes when a TB is large (its CRC chain per lane shrinks 4x); one wave when every TB is a single small
+  // codeblock (copy only: the codeblock CRC covers it; block_crc_bytes, which needs 256 lanes, is never reached).
+  const bool any_large = std::any_of(tbs.begin(), tbs.end(), [](const tb_dec_desc& t) {
+    return t.tbs_bits / 8u > TB_CRC_INLINE_MAX_BYTES;
+  });
+  const bool all_small_single = std::all_of(tbs.begin(), tbs.end(), [](const tb_dec_desc& t) {
+    return t.nof_cbs == 1 && t.tbs_bits / 8u <= 2048u;
+  });
+  plan->tb_threads = any_large ? 1024 : (all_small_single ? 64 : 256);
   int r         = upload_pusch_cb_plan(ctx, impl, batch, dms, &plan->cbs);
   if (r != SRSGPU_OK) {
     delete plan;

@@ -202,7 +202,7 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_dmrs_kernel(const dmrs_job*
   const uint32_t  per_rb = jb.type2 ? 4u : 6u;
   const uint32_t  wfirst = (2 * jb.seq_offset) >> 5;
   // blockIdx.y: a wideband job's pilots are spread over several workgroups (one loop trip each).
-  for (uint32_t i = threadIdx.x + blockIdx.y * MOD_THREADS; i < jb.nof_pilots; i += MOD_THREADS * gridDim.y) {
+  for (uint32_t i = threadIdx.x + blockIdx.y * blockDim.x; i < jb.nof_pilots; i += blockDim.x * gridDim.y) {
     const uint32_t n    = 2 * (jb.seq_offset + i);
     const uint32_t w    = n >> 5;
     const uint32_t word = gseq[jb.gseq_base + (w - wfirst)];  // the plan's resident sequence words
@@ -249,8 +249,12 @@ void launch_pdsch_dmrs(const dmrs_job* d_jobs,
   if (nof_jobs <= 0) {
     return;
   }
-  const unsigned ny = static_cast<unsigned>((max_pilots + MOD_THREADS - 1) / MOD_THREADS);
-  hipLaunchKernelGGL(pdsch_dmrs_kernel, dim3(static_cast<unsigned>(nof_jobs), ny > 0 ? ny : 1u), dim3(MOD_THREADS), 0,
+  // One wave per job for few-RB allocations (a 4-5 RB job has 24-30 pilots: a 256-lane workgroup left 7 of 8 lanes
+  // idle), 256 lanes and more workgroups per job for wideband ones.
+  const int      threads = max_pilots <= 64 ? 64 : MOD_THREADS;
+  const unsigned ny      = static_cast<unsigned>((max_pilots + threads - 1) / threads);
+  hipLaunchKernelGGL(pdsch_dmrs_kernel, dim3(static_cast<unsigned>(nof_jobs), ny > 0 ? ny : 1u),
+                     dim3(static_cast<unsigned>(threads)), 0,
                      stream, d_jobs, d_grids, d_seq);
 }
 

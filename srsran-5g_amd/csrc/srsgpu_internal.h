@@ -161,7 +161,8 @@ struct tb_dec_desc {
   uint32_t crc_table;    ///< CRC24A per-bit contribution table of tbs_bits (CRC arena offset) or NO_CRC_TABLE.
 };
 
-/// threads: 256, or 1024 for plans with TBs above TB_CRC_INLINE_MAX_BYTES (the TB CRC chain per lane shrinks 4x).
+/// threads: 256; 1024 for plans with TBs above TB_CRC_INLINE_MAX_BYTES (the TB CRC chain per lane shrinks 4x); 64
+/// when every TB is one small codeblock.
 void launch_pusch_tb(const tb_dec_desc* d_desc,
                      int                nof_tbs,
                      int                threads,

@@ -126,11 +126,11 @@ __global__ __launch_bounds__(1024) void pusch_tb_kernel(const tb_dec_desc* __res
   // Checksum: the 24 bits that follow the last codeblock's TB bits (concatenate_codeblocks, :465).
   const uint32_t last_q = d.tbs_bits - (d.nof_cbs - 1u) * d.cb_data_bits;
   const uint8_t* lm     = msgs + (d.nof_cbs - 1u) * CB_MSG_STRIDE;
-  uint32_t       chk    = 0;
-  for (int k = 0; k < 24; ++k) {
-    const uint32_t q = last_q + static_cast<uint32_t>(k);
-    chk              = (chk << 1) | ((static_cast<uint32_t>(lm[q >> 3]) >> (7u - (q & 7u))) & 1u);
-  }
+  // The 24 bits span at most 4 message bytes: four independent loads, then one 32-bit window shift.
+  const uint32_t q0 = last_q >> 3;
+  const uint32_t w  = (static_cast<uint32_t>(lm[q0]) << 24) | (static_cast<uint32_t>(lm[q0 + 1]) << 16) |
+                     (static_cast<uint32_t>(lm[q0 + 2]) << 8) | static_cast<uint32_t>(lm[q0 + 3]);
+  const uint32_t chk = (w >> (8u - (last_q & 7u))) & 0xffffffu;
   const bool crc_ok = (crc == chk);
   if (!crc_ok) {
     for (uint32_t c = threadIdx.x; c < d.nof_cbs; c += blockDim.x) {

@@ -181,7 +181,8 @@ def cpu_baseline(dl_ues, dl_segs, ul_ues, ul_segs, tb_host, cw_host, samples_hos
         value = sum(tdd) / ((tdd[0] * t_dl + tdd[1] * t_ul) / (t_dl + t_ul) / value)
     base = {"value": value, "unit": "slots/s", "cores": cores, "kind": "reference",
             "sample": (f"TDD rate from {tdd[0]} DL + {tdd[1]} UL slots per period; " if tdd else "") +
-                      f"{slots} DL+UL slot pairs in {wall:.1f} s on {cores} host threads, each running whole slots ({len(dl_ues)} UEs) "
+                      f"{slots} DL+UL slot pairs in {wall:.1f} s on {cores} host threads, each running whole slots "
+                      f"({len(dl_ues)} UEs) "
                       f"through the srsRAN reference with its own objects; per slot and thread: PDSCH encode "
                       f"{tt[0]:.2f} ms (avx2 encoder), PDSCH DM-RS + modulation {tt[1] - tt[2]:.2f} ms + OFDM "
                       f"modulation {tt[2]:.2f} ms (generic DFT), OFDM demodulation {tt[4]:.2f} ms + channel "
@@ -202,8 +203,9 @@ class InputSet:
         self.dl = self.dls[0]
         self.ul = slotlib.UplinkPipeline(ctx, ul_cell, iterations=iterations, equalizer=prof["equalizer"],
                                          compensate_cfo=True)
-        self.dl_tbs_all = [torch.randint(0, 256, (d.tb_total,), generator=gen, device=dev, dtype=torch.uint8)
-                           for d in self.dls]
+        # Padded to 8 bytes: fresh payloads are drawn 8 bytes at a time (the plans read tb_total bytes).
+        self.dl_tbs_all = [torch.randint(0, 256, ((d.tb_total + 7) // 8 * 8,), generator=gen, device=dev,
+                                         dtype=torch.uint8) for d in self.dls]
         self.dl_tbs = self.dl_tbs_all[0]
         self.dl_group = slotlib.DownlinkGroup(self.dls, self.dl_tbs_all, fresh_tbs=fresh_tbs)
         self.ul_tbs_tx = torch.randint(0, 256, (sum(self.ul.tb_bytes),), generator=gen, device=dev,
@@ -425,7 +427,8 @@ def main():
                 step(i)
             e = timed(args.point_steps)
             ok, it = ul_results(not worst)
-            points.append({"name": name, "snr_db": snr, "value": slots_per_step * agg * args.point_steps / e, "ms_per_step": e * 1e3 / args.point_steps,
+            points.append({"name": name, "snr_db": snr, "value": slots_per_step * agg * args.point_steps / e,
+                           "ms_per_step": e * 1e3 / args.point_steps,
                            "steps": args.point_steps, "pusch_tb_success_rate": ok, "ldpc_avg_iterations": it})
         fill_samples(args.snr_db, args.worst_case)
 

@@ -122,8 +122,8 @@ class DownlinkPipeline:
                 mods.append(srsgpu.PdschModulation(
                     rnti=rnti0 + i, n_id=n_id, modulation_order=u.qm, nof_layers=u.nof_layers,
                     nof_ports=cell.nof_ports, bwp_start_rb=0, bwp_size_rb=cell.grid_prb, rb_start=rb0[i],
-                    nof_rb=u.n_prb, start_symbol=0, nof_symbols=cell.nof_symbols, dmrs_symbol_mask=cell.dmrs_mask, dmrs_type=1,
-                    nof_cdm_groups_without_data=2, scaling=1.0, weights=w))
+                    nof_rb=u.n_prb, start_symbol=0, nof_symbols=cell.nof_symbols, dmrs_symbol_mask=cell.dmrs_mask,
+                    dmrs_type=1, nof_cdm_groups_without_data=2, scaling=1.0, weights=w))
                 dmrs.append(srsgpu.PdschDmrs(
                     slot_index=cell.slot_index(s), scrambling_id=scrambling_id, n_scid=0, dmrs_type=1,
                     nof_layers=u.nof_layers, nof_ports=cell.nof_ports, dmrs_symbol_mask=cell.dmrs_mask,
@@ -166,7 +166,10 @@ class DownlinkGroup:
         if self.fresh_tbs:
             with torch.cuda.stream(stream):
                 for t in self.d_tbs:
-                    t.random_(0, 256)
+                    if t.numel() % 8 == 0:  # 8 payload bytes per Philox draw (the top bit of each word stays 0)
+                        t.view(torch.int64).random_()
+                    else:
+                        t.random_(0, 256)
         rec = (lambda i: events[i].record(stream)) if events else (lambda i: None)
         rec(0)
         for p, t in zip(self.pipes, self.d_tbs):
@@ -202,13 +205,15 @@ class UplinkPipeline:
             for i, u in enumerate(ues):
                 ests.append(srsgpu.PuschChannelEstimation(
                     scrambling_id=scrambling_id, n_scid=0, dmrs_type=1, nof_tx_layers=u.nof_layers,
-                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=cell.nof_symbols, dmrs_symbol_mask=cell.dmrs_mask,
-                    rb_start=rb0[i], nof_rb=u.n_prb, slot_index=cell.slot_index(s), scaling=DMRS_BETA,
+                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=cell.nof_symbols,
+                    dmrs_symbol_mask=cell.dmrs_mask, rb_start=rb0[i], nof_rb=u.n_prb, slot_index=cell.slot_index(s),
+                    scaling=DMRS_BETA,
                     estimate_layout=estimate_layout, compensate_cfo=int(compensate_cfo), numerology=NUMEROLOGY))
                 dems.append(srsgpu.PuschDemodulation(
                     rnti=rnti0 + i, n_id=n_id, modulation_order=u.qm, nof_tx_layers=u.nof_layers,
-                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=cell.nof_symbols, dmrs_symbol_mask=cell.dmrs_mask,
-                    dmrs_type=1, nof_cdm_groups_without_data=2, rb_start=rb0[i], nof_rb=u.n_prb,
+                    nof_rx_ports=cell.nof_ports, start_symbol=0, nof_symbols=cell.nof_symbols,
+                    dmrs_symbol_mask=cell.dmrs_mask, dmrs_type=1, nof_cdm_groups_without_data=2, rb_start=rb0[i],
+                    nof_rb=u.n_prb,
                     equalizer=equalizer, estimate_layout=estimate_layout, cfo_compensated=int(compensate_cfo),
                     numerology=NUMEROLOGY))
                 grid_idx.append(s)

@@ -1,7 +1,7 @@
-"""configs[4]: the du_low test mode's traffic on the GPU - one test UE owning all 273 PRB in every slot (max TBS, MCS 27,
-4 DL layers), continuous slots of the du_high default TDD pattern DDDDDDSUUU (du_high_config.h:503-511; the special
-slot carries an 8-symbol PDSCH with DM-RS in symbols 2 and 7), the whole period captured once as a HIP graph and
-replayed slot period after slot period with fresh data:
+"""configs[4]: the du_low test mode's traffic on the GPU - one test UE owning all 273 PRB in every slot (max TBS,
+MCS 27, 4 DL layers), continuous slots of the du_high default TDD pattern DDDDDDSUUU (du_high_config.h:503-511; the
+special slot carries an 8-symbol PDSCH with DM-RS in symbols 2 and 7), the whole period captured once as a HIP graph
+and replayed slot period after slot period with fresh data:
 
 * DL: every replay draws new TB payloads on the GPU inside the graph (srsgpu.slot.DownlinkGroup, fresh_tbs). Each
   period's codewords, grids and samples must equal an eager run of the same plans on the drawn payloads, and a

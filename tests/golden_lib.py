@@ -199,6 +199,25 @@ def pusch_chest_low_papr_cases():
         i += 1
 
 
+PUSCH_CHEST_273_ROWS = (0, 2, 6, 11, 13)
+
+
+def pusch_chest_273_cases():
+    """Yields (cfg dict, grid (P, 14, 3276, 2) bf16 with only DM-RS symbols 2 and 11 filled, reference estimate rows
+    PUSCH_CHEST_273_ROWS (P, 5, 3276, 2), [noise_var, rsrp, epre, ta_s, cfo_hz] (5, P)) made by
+    dmrs_pusch_estimator_impl on configs[4]'s wideband (160-273 PRB) jobs: filter, average, CFO compensation."""
+    d = _load("pusch_chest_273.npz")
+    i = 0
+    while f"case{i}_cfg" in d:
+        cfg = {k: int(v) for k, v in zip(PUSCH_CHEST_KEYS, d[f"case{i}_cfg"])}
+        cfg["scaling"] = float(d[f"case{i}_scaling"])
+        gd = d[f"case{i}_grid_dmrs"]
+        grid = np.zeros((gd.shape[0], 14) + gd.shape[2:], np.uint16)
+        grid[:, [2, 11]] = gd
+        yield cfg, grid, d[f"case{i}_ch_est_rows"], d[f"case{i}_stats"]
+        i += 1
+
+
 PDSCH_DMRS_KEYS = ["slot", "scrambling_id", "n_scid", "dmrs_type2", "nof_layers", "nof_ports", "dmrs_symbol_mask",
                    "reference_point_k_rb", "rb_start", "nof_rb"]
 

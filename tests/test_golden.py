@@ -185,6 +185,26 @@ def test_pusch_chest_low_papr_golden():
     assert n == 10
 
 
+def test_pusch_chest_273_golden():
+    """The restatement against the reference's estimates of configs[4]'s wideband jobs (160-273 PRB, 1638 pilots per
+    DM-RS symbol): du_low defaults (filter, average, CFO compensation), tests/golden/pusch_chest_273.npz."""
+    import pusch_chest_oracle as C
+    from ofdm_oracle import bf16_to_complex
+    n = 0
+    rows = list(G.PUSCH_CHEST_273_ROWS)
+    for cfg, grid, ce_rows, stats in G.pusch_chest_273_cases():
+        ch, nv, rsrp, epre, ex = C.estimate(cfg, bf16_to_complex(grid), "filter", "average", True)
+        k0, k1 = cfg["rb_start"] * 12, (cfg["rb_start"] + cfg["nof_rb"]) * 12
+        want = bf16_to_complex(ce_rows)[:, :, k0:k1]
+        got = ch[:, rows, k0:k1]
+        assert np.max(np.abs(got - want)) < CHEST_CFO_TOL[0] * np.sqrt(np.mean(np.abs(want) ** 2)), (n, cfg)
+        np.testing.assert_allclose(np.stack([nv, rsrp, epre]), stats[:3], rtol=1e-3)
+        np.testing.assert_allclose(ex["ta_s"], stats[3], atol=2 * T_C)
+        np.testing.assert_allclose(ex["cfo_hz"], stats[4], atol=0.05)
+        n += 1
+    assert n == 5
+
+
 def test_pdsch_dmrs_golden():
     """The PDSCH DM-RS restatement bit-exact against the reference's grids."""
     import pdsch_dmrs_oracle as M

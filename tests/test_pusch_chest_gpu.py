@@ -147,6 +147,31 @@ def test_pusch_chest_cfo_ta_golden(ctx):
         np.testing.assert_allclose(m[i, :P, 5], stats[4], atol=0.05)
 
 
+def test_pusch_chest_273_golden(ctx):
+    """configs[4]'s wideband jobs (160-273 PRB: 1638 pilots per DM-RS symbol, more than one pilot per lane of the
+    1024-lane workgroup) against the reference's estimates (tests/golden/pusch_chest_273.npz, du_low defaults: filter,
+    average, CFO compensation; the bench's test-mode channel at 26 / 30 dB and delay-spread channels), all five in ONE
+    plan: estimate rows, noise variance / RSRP / EPRE (1e-3), SNR, TA (2 Tc) and CFO (0.05 Hz)."""
+    import srsgpu
+    cases = list(G.pusch_chest_273_cases())
+    grids = np.stack([c[1] for c in cases])
+    ests = [to_est(cfg, 2, 1, 0, 1) for cfg, _, _, _ in cases]
+    ce, nv, m = srsgpu.PuschChannelEstimator(ctx, 273, 4).estimate_batch(grids, ests, list(range(len(cases))))
+    rows = list(G.PUSCH_CHEST_273_ROWS)
+    for i, (cfg, _, want_rows, stats) in enumerate(cases):
+        P = cfg["nof_rx_ports"]
+        ks = slice(cfg["rb_start"] * 12, (cfg["rb_start"] + cfg["nof_rb"]) * 12)
+        got = bf16_to_complex(ce[i, 0, :P])[:, rows, ks]
+        w = bf16_to_complex(want_rows)[:, :, ks]
+        assert np.max(np.abs(got - w)) < CFO_TOL[0] * np.sqrt(np.mean(np.abs(w) ** 2)), (i, cfg)
+        np.testing.assert_allclose(nv[i, :P], stats[0], rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 0], stats[1], rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 1], stats[2], rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 3], stats[1] / cfg["scaling"] ** 2 / stats[0], rtol=2e-3)
+        np.testing.assert_allclose(m[i, :P, 4], stats[3], atol=2 * T_C)
+        np.testing.assert_allclose(m[i, :P, 5], stats[4], atol=0.05)
+
+
 def test_pusch_chest_cfo_ta_random_vs_oracle(ctx):
     """48 random transmissions with CFO and delay (1..100 RB, 1-3 DM-RS symbols, every smoothing, both time
     strategies, compensation on / off), ONE plan, against the restatement within the stated tolerances."""

@@ -310,6 +310,57 @@ def gen_pusch_chest_low_papr(ref, rng):
     np.savez_compressed(os.path.join(OUT, "pusch_chest_low_papr.npz"), **out)
 
 
+PUSCH_CHEST_273_ROWS = (0, 2, 6, 11, 13)
+
+
+def gen_pusch_chest_273(ref, rng):
+    """Reference DM-RS channel estimates of configs[4]'s wideband jobs: one 273-PRB single-layer transmission (1638
+    pilots per DM-RS symbol, the estimator's more-than-one-pilot-per-lane path) on 4 rx ports, DM-RS symbols 2 and 11,
+    du_low defaults (filter, average, CFO compensation). Channels: the bench's synthetic test-mode channel (flat
+    random unitary column + a phase ramp of up to 16 samples, bench.py / srsgpu/slot.py synthesize_uplink) at 26 and
+    30 dB, and a frequency-selective delay-spread channel; plus a 160-PRB and a 272-PRB case off the band start. Only the
+    DM-RS symbols of the grid are stored (the estimator reads nothing else) and estimate rows PUSCH_CHEST_273_ROWS."""
+    import pusch_chest_oracle as C
+    from pusch_chest_cases import random_case
+    from pusch_demod_cases import bf16
+    out = {}
+    G, P = 273, 4
+    nsc = 12 * G
+    k = np.arange(nsc)
+    mask = (1 << 2) | (1 << 11)
+    ep = C.symbol_start_epochs(1)
+    for i, (nrb, rb0, snr, kind) in enumerate([(273, 0, 26.0, "flat"), (273, 0, 30.0, "flat"), (273, 0, 26.0, "sel"),
+                                               (160, 57, 22.0, "sel"), (272, 1, 30.0, "flat")]):
+        cfg = dict(slot=int(rng.integers(0, 20)), scrambling_id=int(rng.integers(0, 1008)), n_scid=0, dmrs_type2=0,
+                   scaling=float(10 ** (3 / 20)), dmrs_symbol_mask=mask, start_symbol=0, nof_symbols=14,
+                   rb_start=rb0, nof_rb=nrb, nof_rx_ports=P)
+        if kind == "flat":
+            g = rng.normal(size=(P, P)) + 1j * rng.normal(size=(P, P))
+            q, _ = np.linalg.qr(g)
+            H = q[:, 0][:, None] * np.exp(2j * np.pi * k * rng.uniform() / 256)[None, :]
+        else:
+            H = np.zeros((P, nsc), np.complex128)
+            for p in range(P):
+                for _ in range(4):
+                    H[p] += (rng.normal() + 1j * rng.normal()) / np.sqrt(8) * \
+                        np.exp(-2j * np.pi * k * rng.uniform(0, 40) / 4096)
+        x = (rng.choice([-1, 1], (14, nsc)) + 1j * rng.choice([-1, 1], (14, nsc))) / np.sqrt(2)
+        sc = np.array([rb * 12 + 2 * j for rb in range(rb0, rb0 + nrb) for j in range(6)])
+        for l in (2, 11):
+            x[l, sc] = cfg["scaling"] * C.dmrs_sequence(cfg["slot"], l, cfg["scrambling_id"], 0, 0, rb0, nrb)
+        cfo = float(rng.uniform(-300, 300))
+        y = H[:, None, :] * x[None] * np.exp(2j * np.pi * cfo / 30000.0 * ep)[None, :, None]
+        y = y + (rng.normal(size=y.shape) + 1j * rng.normal(size=y.shape)) * np.sqrt(10 ** (-snr / 10) / 2)
+        grid = bf16(y)
+        ce, nv, rsrp, epre, ta, cfo_hz = ref.pusch_chest(cfg, grid, G, fd=2, td=0, compensate_cfo=True)
+        out[f"case{i}_cfg"] = np.array([cfg[k_] for k_ in PUSCH_CHEST_KEYS], np.int64)
+        out[f"case{i}_scaling"] = np.float32(cfg["scaling"])
+        out[f"case{i}_grid_dmrs"] = grid[:, [2, 11]]
+        out[f"case{i}_ch_est_rows"] = ce[:, list(PUSCH_CHEST_273_ROWS)]
+        out[f"case{i}_stats"] = np.stack([nv, rsrp, epre, ta, cfo_hz])
+    np.savez_compressed(os.path.join(OUT, "pusch_chest_273.npz"), **out)
+
+
 def gen_pdsch_dmrs(ref, rng):
     """Reference PDSCH DM-RS grids (dmrs_pdsch_processor_impl) of random configurations in 24-PRB grids."""
     from pdsch_dmrs_cases import random_config
@@ -383,7 +434,8 @@ def main():
     if len(sys.argv) > 1:  # regenerate only the named fixture sets, e.g. `python tools/gen_golden.py ofdm`
         for name in sys.argv[1:]:
             seed = {"ofdm": 16, "pusch_demod": 17, "pusch_chest": 18, "pdsch_dmrs": 19, "pusch_chest_cfo": 20,
-                    "pdsch_mod_general": 21, "pdsch_dmrs_mask": 22, "pusch_demod_general": 23, "ulsch_demux": 24, "pusch_chest_low_papr": 25}[name]
+                    "pdsch_mod_general": 21, "pdsch_dmrs_mask": 22, "pusch_demod_general": 23, "ulsch_demux": 24, "pusch_chest_low_papr": 25,
+                    "pusch_chest_273": 26}[name]
             globals()["gen_" + name](ref, np.random.default_rng(seed))
         return
     gen_crc(ref, np.random.default_rng(10))
@@ -402,6 +454,7 @@ def main():
     gen_pusch_demod_general(ref, np.random.default_rng(23))
     gen_ulsch_demux(ref, np.random.default_rng(24))
     gen_pusch_chest_low_papr(ref, np.random.default_rng(25))
+    gen_pusch_chest_273(ref, np.random.default_rng(26))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

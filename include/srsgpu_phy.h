@@ -54,6 +54,9 @@ int srsgpu_context_create(int device, srsgpu_context** ctx);
 /** Destroys a context and frees its device memory. */
 void srsgpu_context_destroy(srsgpu_context* ctx);
 
+/** HIP device index of a context (-1 for NULL): the device a binding allocates its own buffers and streams on. */
+int srsgpu_context_device(const srsgpu_context* ctx);
+
 /* ------------------------------------------------------------------------------------------------------------------
  * LDPC decoder — replaces srsran::ldpc_decoder::decode(bit_buffer& output, span<const log_likelihood_ratio> input,
  * crc_calculator* crc, const configuration& cfg)   (include/srsran/phy/upper/channel_coding/ldpc/ldpc_decoder.h:72,

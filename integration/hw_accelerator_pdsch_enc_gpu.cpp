@@ -6,10 +6,10 @@
 // The HAL configuration carries the segmentation result (E of the short / long segments) rather than the number of
 // layers and channel symbols the srsgpu plan segments from; they follow from it: G = Ea * short + Eb * long, and the
 // long segments hold NL * Qm more bits than the short ones (TS 38.212 5.4.2.1), so NL = (Eb - Ea) / Qm (any layer
-// count reproduces the segmentation when every segment is short). Plans are cached per configuration.
+// count reproduces the segmentation when every segment is short). Plans are cached per configuration. The srsgpu context
+// is shared by the factory and every accelerator it creates (integration/gpu_context.h): accelerators outlive it.
+#include "gpu_context.h"
 #include "hw_accelerator_pusch_dec_gpu.h"
-#include "srsgpu_phy.h"
-#include <hip/hip_runtime.h>
 #include <cstring>
 #include <list>
 #include <stdexcept>
@@ -24,11 +24,11 @@ constexpr unsigned PLAN_CACHE_SIZE = 64;
 constexpr unsigned MAX_TB_BYTES    = 1277992 / 8 + 4;
 constexpr unsigned MAX_CW_BYTES    = 2 * 1024 * 1024;
 
+constexpr const char* WHO = "hw_accelerator_pdsch_enc_gpu";
+
 void hip_check(hipError_t e, const char* what)
 {
-  if (e != hipSuccess) {
-    throw std::runtime_error(std::string("hw_accelerator_pdsch_enc_gpu: ") + what + ": " + hipGetErrorString(e));
-  }
+  gpu::hip_check(e, WHO, what);
 }
 
 } // namespace
@@ -36,8 +36,10 @@ void hip_check(hipError_t e, const char* what)
 class hw_accelerator_pdsch_enc_gpu : public hw_accelerator_pdsch_enc
 {
 public:
-  explicit hw_accelerator_pdsch_enc_gpu(srsgpu_context* ctx_) : ctx(ctx_)
+  explicit hw_accelerator_pdsch_enc_gpu(std::shared_ptr<srsgpu_context> owner_) :
+    owner(std::move(owner_)), ctx(owner.get())
   {
+    hip_check(hipSetDevice(srsgpu_context_device(ctx)), "device");
     hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream");
     hip_check(hipMalloc(&d_tb, MAX_TB_BYTES), "TB buffer");
     hip_check(hipMalloc(&d_cw, MAX_CW_BYTES), "codeword buffer");
@@ -71,8 +73,13 @@ public:
 
   bool enqueue_operation(span<const uint8_t> data, span<const uint8_t> /*aux_data*/, unsigned /*cb_index*/) override
   {
-    if (cfg.cb_mode || data.size() > MAX_TB_BYTES || data.size() * 8 != cfg.nof_tb_bits) {
-      return false;
+    // Configuration errors, not back-pressure: pdsch_encoder_hw_impl retries a false enqueue forever.
+    if (cfg.cb_mode) {
+      throw std::invalid_argument(std::string(WHO) + ": codeblock mode is not supported (is_cb_mode_supported())");
+    }
+    if (data.size() > MAX_TB_BYTES || data.size() * 8 != cfg.nof_tb_bits) {
+      throw std::length_error(std::string(WHO) + ": TB of " + std::to_string(data.size()) +
+                              " bytes does not match the configured " + std::to_string(cfg.nof_tb_bits) + " bits");
     }
     std::memcpy(h_tb, data.data(), data.size());
     tb_bytes = static_cast<unsigned>(data.size());
@@ -99,12 +106,12 @@ public:
       c.tb_offset        = 0;
       c.cw_offset        = 0;
       if ((G + 7) / 8 > MAX_CW_BYTES) {
-        return false;
+        throw std::length_error(std::string(WHO) + ": codeword beyond get_max_supported_buff_size()");
       }
       srsgpu_pdsch_encoder_plan* plan = plan_for(c);
       hip_check(hipMemcpyAsync(d_tb, h_tb, tb_bytes, hipMemcpyHostToDevice, stream), "TB upload");
       if (srsgpu_pdsch_encoder_plan_execute(plan, d_tb, d_cw, stream) != SRSGPU_OK) {
-        throw std::runtime_error(std::string("hw_accelerator_pdsch_enc_gpu: ") + srsgpu_last_error());
+        throw std::runtime_error(std::string(WHO) + ": " + srsgpu_last_error());
       }
       hip_check(hipMemcpyAsync(h_cw, d_cw, (G + 7) / 8, hipMemcpyDeviceToHost, stream), "codeword download");
       hip_check(hipStreamSynchronize(stream), "synchronise");
@@ -141,7 +148,7 @@ private:
     }
     srsgpu_pdsch_encoder_plan* plan = nullptr;
     if (srsgpu_pdsch_encoder_plan_create(ctx, &key, 1, &plan) != SRSGPU_OK) {
-      throw std::runtime_error(std::string("hw_accelerator_pdsch_enc_gpu: ") + srsgpu_last_error());
+      throw std::runtime_error(std::string(WHO) + ": " + srsgpu_last_error());
     }
     cache.push_front({key, plan});
     if (cache.size() > PLAN_CACHE_SIZE) {
@@ -151,6 +158,7 @@ private:
     return plan;
   }
 
+  std::shared_ptr<srsgpu_context> owner;
   srsgpu_context*                ctx;
   hipStream_t                    stream = nullptr;
   uint8_t*                       d_tb   = nullptr;
@@ -166,13 +174,7 @@ private:
 class hw_accelerator_pdsch_enc_factory_gpu : public hw_accelerator_pdsch_enc_factory
 {
 public:
-  explicit hw_accelerator_pdsch_enc_factory_gpu(int device)
-  {
-    if (srsgpu_context_create(device, &ctx) != SRSGPU_OK) {
-      throw std::runtime_error(srsgpu_last_error());
-    }
-  }
-  ~hw_accelerator_pdsch_enc_factory_gpu() override { srsgpu_context_destroy(ctx); }
+  explicit hw_accelerator_pdsch_enc_factory_gpu(int device) : ctx(gpu::shared_context(device)) {}
 
   std::unique_ptr<hw_accelerator_pdsch_enc> create() override
   {
@@ -180,7 +182,7 @@ public:
   }
 
 private:
-  srsgpu_context* ctx = nullptr;
+  std::shared_ptr<srsgpu_context> ctx;
 };
 
 std::shared_ptr<hw_accelerator_pdsch_enc_factory> create_hw_accelerator_pdsch_enc_factory_gpu(int device)

@@ -9,10 +9,18 @@
 // srsgpu_pusch_cb_plan (rate dematching into the HBM-resident HARQ soft buffers + LDPC decoding + CB CRC): one H2D copy
 // of the staged LLRs from pinned memory, one execute, one D2H copy of messages / flags / iterations, one stream
 // synchronisation per TB. Plans are cached per codeblock-configuration list (a cell's grants repeat), so steady state
-// allocates nothing. HARQ soft buffers live in HBM, one 66 x 384-LLR slot per absolute codeblock identifier.
+// allocates nothing.
+//
+// HARQ: one HBM arena per factory, one 66 x 384-LLR slot per absolute codeblock identifier, shared by every
+// accelerator the factory creates. The reference makes one accelerator per decoder thread and hands them out through a
+// concurrent_thread_local_object_pool (factories.cpp:132-139, pusch_decoder_hw_impl.h:57, .cpp:151), so the first
+// transmission and a retransmission of a codeblock can run on different accelerators: both address the same slot.
+// The rx buffer pool keeps one codeblock on one thread at a time (unique_rx_buffer lock) and run() synchronises its
+// stream before the results are read, so consecutive transmissions of a slot are ordered. free_harq_context_entry()
+// (called once the TB CRC passes, :411/:423) releases the slot: a later retransmission into a released slot combines
+// with zeros, the state of a new soft buffer. The arena and the srsgpu context live as long as any accelerator.
+#include "gpu_context.h"
 #include "hw_accelerator_pusch_dec_gpu.h"
-#include "srsgpu_phy.h"
-#include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstring>
 #include <list>
@@ -29,11 +37,11 @@ constexpr unsigned MAX_CB_LLRS     = 66 * 384;  // N of BG1 at Z = 384: one HARQ
 constexpr unsigned MAX_E           = 66 * 384 * 8;
 constexpr unsigned PLAN_CACHE_SIZE = 64;
 
+constexpr const char* WHO = "hw_accelerator_pusch_dec_gpu";
+
 void hip_check(hipError_t e, const char* what)
 {
-  if (e != hipSuccess) {
-    throw std::runtime_error(std::string("hw_accelerator_pusch_dec_gpu: ") + what + ": " + hipGetErrorString(e));
-  }
+  gpu::hip_check(e, WHO, what);
 }
 
 uint8_t crc_poly_of(hw_dec_cb_crc_type t)
@@ -54,16 +62,60 @@ uint8_t qm_of(modulation_scheme m)
   return static_cast<uint8_t>(m);
 }
 
+/// The HBM HARQ arena of a factory: one slot per absolute codeblock identifier, shared by its accelerators.
+struct harq_arena {
+  harq_arena(std::shared_ptr<srsgpu_context> ctx_, unsigned max_cb_ids_) :
+    ctx(std::move(ctx_)), max_cb_ids(max_cb_ids_), in_use(max_cb_ids_, 0)
+  {
+    if (max_cb_ids == 0) {
+      throw std::invalid_argument(std::string(WHO) + ": max_cb_ids must be positive");
+    }
+    hip_check(hipSetDevice(srsgpu_context_device(ctx.get())), "device");
+    hip_check(hipMalloc(&d_soft, static_cast<size_t>(max_cb_ids) * MAX_CB_LLRS), "HARQ arena");
+    hip_check(hipMemset(d_soft, 0, static_cast<size_t>(max_cb_ids) * MAX_CB_LLRS), "HARQ arena");
+  }
+  ~harq_arena() { (void)hipFree(d_soft); }
+
+  /// Marks the slots of a launch as holding soft bits; returns the released slots a retransmission reads (to be
+  /// cleared first).
+  std::vector<unsigned> acquire(const std::vector<std::pair<unsigned, bool>>& ids_new_data)
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    std::vector<unsigned>       clear;
+    for (const auto& e : ids_new_data) {
+      if (!e.second && in_use[e.first] == 0) {
+        clear.push_back(e.first);
+      }
+      in_use[e.first] = 1;
+    }
+    return clear;
+  }
+
+  void release(unsigned id)
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    if (id < max_cb_ids) {
+      in_use[id] = 0;
+    }
+  }
+
+  std::shared_ptr<srsgpu_context> ctx;
+  unsigned                        max_cb_ids;
+  int8_t*                         d_soft = nullptr;
+  std::mutex                      mtx;
+  std::vector<uint8_t>            in_use;  ///< 1: the slot holds soft bits of a live HARQ process.
+};
+
 } // namespace
 
 class hw_accelerator_pusch_dec_gpu : public hw_accelerator_pusch_dec
 {
 public:
-  hw_accelerator_pusch_dec_gpu(srsgpu_context* ctx_, unsigned max_cb_ids_) : ctx(ctx_), max_cb_ids(max_cb_ids_)
+  explicit hw_accelerator_pusch_dec_gpu(std::shared_ptr<harq_arena> arena_) :
+    arena(std::move(arena_)), ctx(arena->ctx.get()), max_cb_ids(arena->max_cb_ids), d_harq(arena->d_soft)
   {
+    hip_check(hipSetDevice(srsgpu_context_device(ctx)), "device");
     hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream");
-    hip_check(hipMalloc(&d_harq, static_cast<size_t>(max_cb_ids) * MAX_CB_LLRS), "HARQ arena");
-    hip_check(hipMemset(d_harq, 0, static_cast<size_t>(max_cb_ids) * MAX_CB_LLRS), "HARQ arena");
     grow(MAX_E, 8);
   }
 
@@ -72,7 +124,6 @@ public:
     for (auto& e : cache) {
       srsgpu_pusch_cb_plan_destroy(e.plan);
     }
-    (void)hipFree(d_harq);
     (void)hipFree(d_llrs);
     (void)hipFree(d_msgs);
     (void)hipFree(d_iters);
@@ -103,8 +154,19 @@ public:
 
   bool enqueue_operation(span<const int8_t> data, span<const int8_t> /*aux_data*/, unsigned cb_index) override
   {
-    if (cb_index >= cfgs.size() || cfgs[cb_index].absolute_cb_id >= max_cb_ids || data.size() > MAX_E) {
-      return false;
+    // Configuration errors, not back-pressure: pusch_decoder_hw_impl retries a false enqueue forever
+    // (pusch_decoder_hw_impl.cpp:204-354), so they are reported loudly instead.
+    if (cb_index >= cfgs.size()) {
+      throw std::logic_error(std::string(WHO) + ": codeblock " + std::to_string(cb_index) + " enqueued unconfigured");
+    }
+    if (cfgs[cb_index].absolute_cb_id >= max_cb_ids) {
+      throw std::out_of_range(std::string(WHO) + ": absolute codeblock id " +
+                              std::to_string(cfgs[cb_index].absolute_cb_id) + " beyond the HARQ arena (max_cb_ids " +
+                              std::to_string(max_cb_ids) + ": size it for the rx buffer pool's codeblocks)");
+    }
+    if (data.size() > MAX_E) {
+      throw std::length_error(std::string(WHO) + ": rate-matched length " + std::to_string(data.size()) +
+                              " beyond the accelerator's limit");
     }
     grow(staged + data.size(), static_cast<unsigned>(ops.size()) + 1);
     std::memcpy(h_llrs + staged, data.data(), data.size());
@@ -136,11 +198,7 @@ public:
     out.nof_ldpc_iterations = (it > 0) ? static_cast<unsigned>(it) : cfgs[cb_index].max_nof_ldpc_iterations;
   }
 
-  void free_harq_context_entry(unsigned /*absolute_cb_id*/) override
-  {
-    // The HARQ slot of an absolute codeblock identifier is overwritten by its next new transmission (the rate
-    // dematcher writes every position for new data), so there is nothing to release.
-  }
+  void free_harq_context_entry(unsigned absolute_cb_id) override { arena->release(absolute_cb_id); }
 
   bool is_harq_external() const override { return true; }
 
@@ -213,7 +271,7 @@ private:
     srsgpu_pusch_cb_plan* plan = nullptr;
     if (srsgpu_pusch_cb_plan_create(ctx, SRSGPU_LDPC_IMPL_SIMD, key.data(), static_cast<uint32_t>(key.size()), &plan) !=
         SRSGPU_OK) {
-      throw std::runtime_error(std::string("hw_accelerator_pusch_dec_gpu: ") + srsgpu_last_error());
+      throw std::runtime_error(std::string(WHO) + ": " + srsgpu_last_error());
     }
     cache.push_front({key, plan});
     if (cache.size() > PLAN_CACHE_SIZE) {
@@ -248,12 +306,20 @@ private:
       k.harq_offset      = c.absolute_cb_id * MAX_CB_LLRS;
       k.out_offset       = static_cast<uint32_t>(i * SRSGPU_CB_MSG_STRIDE);
     }
-    srsgpu_pusch_cb_plan* plan = plan_for(key);
-    const size_t          n    = ops.size();
+    srsgpu_pusch_cb_plan*                   plan = plan_for(key);
+    const size_t                            n    = ops.size();
+    std::vector<std::pair<unsigned, bool>> ids(n);
+    for (size_t i = 0; i != n; ++i) {
+      ids[i] = {cfgs[ops[i].cb_index].absolute_cb_id, cfgs[ops[i].cb_index].new_data};
+    }
+    // A retransmission into a released slot combines with zeros (a new soft buffer).
+    for (unsigned id : arena->acquire(ids)) {
+      hip_check(hipMemsetAsync(d_harq + static_cast<size_t>(id) * MAX_CB_LLRS, 0, MAX_CB_LLRS, stream), "HARQ reset");
+    }
     hip_check(hipMemcpyAsync(d_llrs, h_llrs, staged, hipMemcpyHostToDevice, stream), "LLR upload");
     hip_check(hipMemsetAsync(d_flags, 0, n, stream), "flags");
     if (srsgpu_pusch_cb_plan_execute(plan, d_llrs, d_harq, d_msgs, d_iters, d_flags, stream) != SRSGPU_OK) {
-      throw std::runtime_error(std::string("hw_accelerator_pusch_dec_gpu: ") + srsgpu_last_error());
+      throw std::runtime_error(std::string(WHO) + ": " + srsgpu_last_error());
     }
     hip_check(hipMemcpyAsync(h_msgs, d_msgs, n * SRSGPU_CB_MSG_STRIDE, hipMemcpyDeviceToHost, stream), "messages");
     hip_check(hipMemcpyAsync(h_iters, d_iters, n * sizeof(int32_t), hipMemcpyDeviceToHost, stream), "iterations");
@@ -262,10 +328,11 @@ private:
     decoded = true;
   }
 
+  std::shared_ptr<harq_arena>                 arena;
   srsgpu_context*                             ctx;
   unsigned                                    max_cb_ids;
+  int8_t*                                     d_harq;
   hipStream_t                                 stream  = nullptr;
-  int8_t*                                     d_harq  = nullptr;
   int8_t*                                     d_llrs  = nullptr;
   uint8_t*                                    d_msgs  = nullptr;
   int32_t*                                    d_iters = nullptr;
@@ -284,27 +351,24 @@ private:
 };
 
 /// Factory (hw_accelerator_pusch_dec_factory.h): one accelerator per decoder-pool entry (one per worker thread), all
-/// sharing one srsgpu context (one per process and GPU). The absolute codeblock identifiers of the rx buffer pool
-/// index the HARQ arena: max_cb_ids must cover the pool's codeblocks.
+/// sharing the factory's HARQ arena and the device's srsgpu context (shared ownership: the accelerators outlive the
+/// factory). The absolute codeblock identifiers of the rx buffer pool index the HARQ arena: max_cb_ids must cover the
+/// pool's codeblocks (an identifier beyond it throws).
 class hw_accelerator_pusch_dec_factory_gpu : public hw_accelerator_pusch_dec_factory
 {
 public:
-  hw_accelerator_pusch_dec_factory_gpu(int device, unsigned max_cb_ids_) : max_cb_ids(max_cb_ids_)
+  hw_accelerator_pusch_dec_factory_gpu(int device, unsigned max_cb_ids) :
+    arena(std::make_shared<harq_arena>(gpu::shared_context(device), max_cb_ids))
   {
-    if (srsgpu_context_create(device, &ctx) != SRSGPU_OK) {
-      throw std::runtime_error(srsgpu_last_error());
-    }
   }
-  ~hw_accelerator_pusch_dec_factory_gpu() override { srsgpu_context_destroy(ctx); }
 
   std::unique_ptr<hw_accelerator_pusch_dec> create() override
   {
-    return std::make_unique<hw_accelerator_pusch_dec_gpu>(ctx, max_cb_ids);
+    return std::make_unique<hw_accelerator_pusch_dec_gpu>(arena);
   }
 
 private:
-  srsgpu_context* ctx = nullptr;
-  unsigned        max_cb_ids;
+  std::shared_ptr<harq_arena> arena;
 };
 
 std::shared_ptr<hw_accelerator_pusch_dec_factory> create_hw_accelerator_pusch_dec_factory_gpu(int      device,

@@ -3,14 +3,14 @@
 // create_ldpc_decoder_factory_sw("gpu") and every caller of ldpc_decoder::decode() (pusch_codeblock_decoder.cpp:45)
 // run the MI355X kernels unchanged. Per codeblock: the LLRs and the previous output go through pinned staging buffers
 // with asynchronous copies on the instance's own stream, and the decode runs a plan cached per codeblock configuration
-// (no allocation, no device-wide synchronisation in steady state). oracle/build_hal.sh links this file with the
-// reference's own pusch_codeblock_decoder and tests/test_hal_gpu.py runs it on the GPU.
+// (no allocation, no device-wide synchronisation in steady state). Every HIP call is checked (a failure throws). The
+// srsgpu context is shared by the factory and every decoder it creates (integration/gpu_context.h). oracle/build_hal.sh
+// links this file with the reference's own pusch_codeblock_decoder and tests/test_hal_gpu.py runs it on the GPU.
+#include "gpu_context.h"
 #include "srsran/adt/bit_buffer.h"
 #include "srsran/phy/upper/channel_coding/crc_calculator.h"
 #include "srsran/phy/upper/channel_coding/channel_coding_factories.h"
 #include "srsran/phy/upper/channel_coding/ldpc/ldpc_decoder.h"
-#include "srsgpu_phy.h"
-#include <hip/hip_runtime.h>
 #include <cstring>
 #include <list>
 #include <stdexcept>
@@ -23,17 +23,17 @@ namespace srsran {
 class ldpc_decoder_gpu : public ldpc_decoder
 {
 public:
-  explicit ldpc_decoder_gpu(srsgpu_context* ctx_, bool generic_arithmetic = false) :
-    ctx(ctx_), impl(generic_arithmetic ? SRSGPU_LDPC_IMPL_GENERIC : SRSGPU_LDPC_IMPL_SIMD)
+  explicit ldpc_decoder_gpu(std::shared_ptr<srsgpu_context> owner_, bool generic_arithmetic = false) :
+    owner(std::move(owner_)), ctx(owner.get()), impl(generic_arithmetic ? SRSGPU_LDPC_IMPL_GENERIC : SRSGPU_LDPC_IMPL_SIMD)
   {
-    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&d_llr, MAX_LLRS) != hipSuccess || hipMalloc(&d_out, MAX_OUT) != hipSuccess ||
-        hipMalloc(&d_iters, sizeof(int32_t)) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&h_llr), MAX_LLRS) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&h_out), MAX_OUT) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&h_iters), sizeof(int32_t)) != hipSuccess) {
-      throw std::runtime_error("ldpc_decoder_gpu: HIP allocation failed");
-    }
+    check(hipSetDevice(srsgpu_context_device(ctx)), "device");
+    check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream");
+    check(hipMalloc(&d_llr, MAX_LLRS), "LLR buffer");
+    check(hipMalloc(&d_out, MAX_OUT), "output buffer");
+    check(hipMalloc(&d_iters, sizeof(int32_t)), "iteration counter");
+    check(hipHostMalloc(reinterpret_cast<void**>(&h_llr), MAX_LLRS), "pinned LLRs");
+    check(hipHostMalloc(reinterpret_cast<void**>(&h_out), MAX_OUT), "pinned output");
+    check(hipHostMalloc(reinterpret_cast<void**>(&h_iters), sizeof(int32_t)), "pinned iteration counter");
   }
 
   ~ldpc_decoder_gpu() override
@@ -73,16 +73,12 @@ public:
     span<uint8_t> packed = output.get_buffer();
     std::memcpy(h_out, packed.data(), packed.size());
     std::memcpy(h_llr, input.data(), input.size());
-    (void)hipMemcpyAsync(d_out, h_out, packed.size(), hipMemcpyHostToDevice, stream);
-    (void)hipMemcpyAsync(d_llr, h_llr, input.size(), hipMemcpyHostToDevice, stream);
-    if (srsgpu_ldpc_decoder_plan_execute(plan, d_llr, d_out, d_iters, stream) != SRSGPU_OK) {
-      throw std::runtime_error(srsgpu_last_error());
-    }
-    (void)hipMemcpyAsync(h_out, d_out, packed.size(), hipMemcpyDeviceToHost, stream);
-    (void)hipMemcpyAsync(h_iters, d_iters, sizeof(int32_t), hipMemcpyDeviceToHost, stream);
-    if (hipStreamSynchronize(stream) != hipSuccess) {
-      throw std::runtime_error("ldpc_decoder_gpu: stream synchronisation failed");
-    }
+    check(hipMemcpyAsync(d_out, h_out, packed.size(), hipMemcpyHostToDevice, stream), "output upload");
+    check(hipMemcpyAsync(d_llr, h_llr, input.size(), hipMemcpyHostToDevice, stream), "LLR upload");
+    gpu::srsgpu_check(srsgpu_ldpc_decoder_plan_execute(plan, d_llr, d_out, d_iters, stream), "ldpc_decoder_gpu");
+    check(hipMemcpyAsync(h_out, d_out, packed.size(), hipMemcpyDeviceToHost, stream), "output download");
+    check(hipMemcpyAsync(h_iters, d_iters, sizeof(int32_t), hipMemcpyDeviceToHost, stream), "iteration download");
+    check(hipStreamSynchronize(stream), "synchronise");
     std::memcpy(packed.data(), h_out, packed.size());
     if (*h_iters < 0) {
       return std::nullopt;
@@ -91,6 +87,8 @@ public:
   }
 
 private:
+  static void check(hipError_t e, const char* what) { gpu::hip_check(e, "ldpc_decoder_gpu", what); }
+
   static constexpr size_t   MAX_LLRS        = 66 * 384;
   static constexpr size_t   MAX_OUT         = (22 * 384 + 7) / 8;
   static constexpr unsigned PLAN_CACHE_SIZE = 32;
@@ -110,9 +108,7 @@ private:
       }
     }
     srsgpu_ldpc_decoder_plan* plan = nullptr;
-    if (srsgpu_ldpc_decoder_plan_create(ctx, impl, &key, 1, &plan) != SRSGPU_OK) {
-      throw std::runtime_error(srsgpu_last_error());
-    }
+    gpu::srsgpu_check(srsgpu_ldpc_decoder_plan_create(ctx, impl, &key, 1, &plan), "ldpc_decoder_gpu");
     cache.push_front({key, plan});
     if (cache.size() > PLAN_CACHE_SIZE) {
       srsgpu_ldpc_decoder_plan_destroy(cache.back().plan);
@@ -121,6 +117,7 @@ private:
     return plan;
   }
 
+  std::shared_ptr<srsgpu_context> owner;
   srsgpu_context*        ctx;
   int                    impl;
   hipStream_t            stream  = nullptr;
@@ -137,17 +134,11 @@ private:
 class ldpc_decoder_factory_gpu : public ldpc_decoder_factory
 {
 public:
-  explicit ldpc_decoder_factory_gpu(int device)
-  {
-    if (srsgpu_context_create(device, &ctx) != SRSGPU_OK) {
-      throw std::runtime_error(srsgpu_last_error());
-    }
-  }
-  ~ldpc_decoder_factory_gpu() override { srsgpu_context_destroy(ctx); }
+  explicit ldpc_decoder_factory_gpu(int device) : ctx(gpu::shared_context(device)) {}
   std::unique_ptr<ldpc_decoder> create() override { return std::make_unique<ldpc_decoder_gpu>(ctx); }
 
 private:
-  srsgpu_context* ctx = nullptr;
+  std::shared_ptr<srsgpu_context> ctx;
 };
 
 std::shared_ptr<ldpc_decoder_factory> create_ldpc_decoder_factory_gpu(int device)

@@ -37,12 +37,14 @@ pids=()
 for src in "${SRCS[@]}"; do
   obj="$OUT/obj_hal/$(basename "${src%.cpp}").o"
   OBJS+=("$obj")
-  if [ ! -f "$obj" ] || [ "$src" -nt "$obj" ] || [ "$0" -nt "$obj" ] || [ "$ROOT/integration/hw_accelerator_pusch_dec_gpu.h" -nt "$obj" ]; then
+  if [ ! -f "$obj" ] || [ "$src" -nt "$obj" ] || [ "$0" -nt "$obj" ] || [ "$ROOT/integration/hw_accelerator_pusch_dec_gpu.h" -nt "$obj" ] || [ "$ROOT/integration/gpu_context.h" -nt "$obj" ] || [ "$ROOT/include/srsgpu_phy.h" -nt "$obj" ]; then
     $CXX $FLAGS -c "$src" -o "$obj" &
     pids+=($!)
   fi
 done
-for p in "${pids[@]:-}"; do [ -n "$p" ] && wait "$p"; done
+rc=0
+for p in "${pids[@]:-}"; do [ -n "$p" ] && { wait "$p" || rc=1; }; done
+[ $rc -eq 0 ] || { echo "build_hal: compilation failed" >&2; exit 1; }
 $CXX -shared -o "$OUT/libsrshal.so" "${OBJS[@]}" -L"$OUT" -lsrsref -L"$ROOT/srsran-5g_amd/lib" -lsrsgpu_phy \
   -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$ORIGIN' -Wl,-rpath,'$ORIGIN/../../srsran-5g_amd/lib' -Wl,-rpath,/opt/rocm/lib \
   -Wl,--no-undefined

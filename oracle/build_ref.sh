@@ -98,6 +98,8 @@ for entry in "${SRCS[@]}"; do
     pids+=($!)
   fi
 done
-for p in "${pids[@]:-}"; do [ -n "$p" ] && wait "$p"; done
+rc=0
+for p in "${pids[@]:-}"; do [ -n "$p" ] && { wait "$p" || rc=1; }; done
+[ $rc -eq 0 ] || { echo "build_ref: compilation failed" >&2; exit 1; }
 $CXX -shared -o "$OUT/libsrsref.so" "${OBJS[@]}"
 echo "build_ref: $OUT/libsrsref.so"

@@ -12,6 +12,12 @@
 //
 // The rx buffers are a minimal unique_rx_buffer::callback (soft bits, data bits, CRC flags per codeblock, absolute
 // codeblock identifiers harq_id * 160 + cb), one per (mode, HARQ process), so retransmissions combine like the pool's.
+//
+// Pool harness (hal_pool_*): the reference's own wiring of the HW decoder (pusch_decoder_factory_hw, factories.cpp:
+// 122-140): a temporary accelerator factory creates one accelerator per decoder thread and is dropped before anything
+// is decoded; the accelerators form a pusch_decoder_hw_impl::hw_decoder_pool (concurrent_thread_local_object_pool:
+// each thread gets its own accelerator); persistent worker threads each own a pusch_decoder_hw_impl over that pool, so
+// a transmission and its retransmission can be decoded by different threads, i.e. different accelerators.
 #include "hw_accelerator_pusch_dec_gpu.h"
 
 #include "srsran/phy/upper/channel_coding/channel_coding_factories.h"
@@ -33,8 +39,12 @@
 #include "lib/phy/upper/channel_processors/pusch/pusch_decoder_hw_impl.h"
 #include "lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.h"
 
+#include <condition_variable>
+#include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 namespace srsran {
@@ -128,9 +138,169 @@ std::unique_ptr<pusch_decoder> make_sw_decoder(std::unique_ptr<ldpc_decoder> ldp
                                               make_sch_crc<pusch_decoder_impl::sch_crc>(), nullptr, 275, 4);
 }
 
+/// A persistent thread running posted jobs one at a time (run() blocks until the job is done).
+class worker_thread
+{
+public:
+  worker_thread() : th([this] { loop(); }) {}
+  ~worker_thread()
+  {
+    {
+      std::lock_guard<std::mutex> lock(mtx);
+      quit = true;
+    }
+    cv.notify_all();
+    th.join();
+  }
+  void run(std::function<void()> f)
+  {
+    std::unique_lock<std::mutex> lock(mtx);
+    job  = std::move(f);
+    done = false;
+    cv.notify_all();
+    cv.wait(lock, [this] { return done; });
+  }
+
+private:
+  void loop()
+  {
+    std::unique_lock<std::mutex> lock(mtx);
+    for (;;) {
+      cv.wait(lock, [this] { return quit || job; });
+      if (quit) {
+        return;
+      }
+      std::function<void()> f = std::move(job);
+      job                      = nullptr;
+      lock.unlock();
+      f();
+      lock.lock();
+      done = true;
+      cv.notify_all();
+    }
+  }
+  std::mutex              mtx;
+  std::condition_variable cv;
+  std::function<void()>   job;
+  bool                    done = true;
+  bool                    quit = false;
+  std::thread             th;
+};
+
+struct pool_harness {
+  std::unique_ptr<pusch_decoder>                                       cpu;
+  std::vector<std::unique_ptr<pusch_decoder>>                          decs;  // one per worker
+  std::vector<std::unique_ptr<worker_thread>>                          workers;
+  std::map<std::pair<int, unsigned>, std::unique_ptr<test_rx_buffer>> rx;    // (cpu 0 / gpu 1, HARQ process)
+};
+
+/// new_data + on_new_softbits + on_end_softbits of one TB on `dec`; stats as hal_pusch_decode.
+int run_decode(pusch_decoder&        dec,
+               test_rx_buffer&       rxb,
+               const pusch_decoder::configuration& cfg,
+               const int8_t*         llrs,
+               unsigned              nof_llrs,
+               uint8_t*              tb,
+               unsigned              tb_bytes,
+               double*               stats)
+{
+  result_capture        notifier;
+  pusch_decoder_buffer& buf = dec.new_data(span<uint8_t>(tb, tb_bytes), unique_rx_buffer(rxb), notifier, cfg);
+  buf.on_new_softbits(span<const log_likelihood_ratio>(reinterpret_cast<const log_likelihood_ratio*>(llrs), nof_llrs));
+  buf.on_end_softbits();
+  if (!notifier.done) {
+    return -1;
+  }
+  const auto& r = notifier.result;
+  stats[0]      = r.tb_crc_ok ? 1 : 0;
+  stats[1]      = r.nof_codeblocks_total;
+  stats[2]      = r.ldpc_decoder_stats.get_nof_observations();
+  stats[3]      = r.ldpc_decoder_stats.get_nof_observations() ? r.ldpc_decoder_stats.get_min() : -1;
+  stats[4]      = r.ldpc_decoder_stats.get_nof_observations() ? r.ldpc_decoder_stats.get_max() : -1;
+  stats[5]      = r.ldpc_decoder_stats.get_nof_observations() ? r.ldpc_decoder_stats.get_mean() : -1;
+  return 0;
+}
+
 } // namespace
 
 extern "C" {
+
+/// Pool harness: nof_threads worker threads, each with its own pusch_decoder_hw_impl over one shared
+/// hw_decoder_pool of nof_threads GPU accelerators (made by a factory that is destroyed before this returns), plus the
+/// reference CPU decoder (pusch_decoder_impl, AVX-512 / AVX2 LDPC) on the calling thread.
+void* hal_pool_create(int device, unsigned max_cb_ids, unsigned nof_threads)
+{
+  auto*                                                   h = new pool_harness();
+  std::vector<std::unique_ptr<hal::hw_accelerator_pusch_dec>> accs;
+  {
+    std::shared_ptr<hal::hw_accelerator_pusch_dec_factory> factory =
+        hal::create_hw_accelerator_pusch_dec_factory_gpu(device, max_cb_ids);
+    for (unsigned i = 0; i != nof_threads; ++i) {
+      accs.push_back(factory->create());
+    }
+  }  // the factory is gone: the accelerators keep the context and the HARQ arena alive
+  auto pool = std::make_shared<pusch_decoder_hw_impl::hw_decoder_pool>(std::move(accs));
+  for (unsigned i = 0; i != nof_threads; ++i) {
+    auto crcs = make_sch_crc<pusch_decoder_hw_impl::sch_crc>();
+    h->decs.push_back(
+        std::make_unique<pusch_decoder_hw_impl>(std::make_unique<ldpc_segmenter_rx_impl>(), crcs, pool, nullptr));
+    h->workers.push_back(std::make_unique<worker_thread>());
+  }
+  h->cpu = make_sw_decoder(cpu_decoder());
+  return h;
+}
+
+void hal_pool_destroy(void* p)
+{
+  delete static_cast<pool_harness*>(p);
+}
+
+/// One TB decoded by worker thread `worker` (GPU, through the thread's pool accelerator) or, for worker < 0, by the
+/// reference CPU decoder. Arguments and stats as hal_pusch_decode.
+int hal_pool_decode(void*         p,
+                    int           worker,
+                    unsigned      harq_id,
+                    unsigned      nof_cbs,
+                    int           bg,
+                    int           rv,
+                    int           qm,
+                    int           nof_layers,
+                    unsigned      Nref,
+                    int           max_iter,
+                    int           early_stop,
+                    int           new_data,
+                    const int8_t* llrs,
+                    unsigned      nof_llrs,
+                    uint8_t*      tb,
+                    unsigned      tb_bytes,
+                    double*       stats)
+{
+  auto*    h   = static_cast<pool_harness*>(p);
+  auto     key = std::make_pair(worker < 0 ? 0 : 1, harq_id);
+  auto     it  = h->rx.find(key);
+  if (it == h->rx.end() || it->second->get_nof_codeblocks() != nof_cbs) {
+    h->rx[key] = std::make_unique<test_rx_buffer>(nof_cbs, harq_id * CB_IDS_PER_HARQ);
+  }
+  pusch_decoder::configuration cfg;
+  cfg.base_graph          = bg == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2;
+  cfg.rv                  = rv;
+  cfg.mod                 = static_cast<modulation_scheme>(qm);
+  cfg.Nref                = Nref;
+  cfg.nof_layers          = nof_layers;
+  cfg.nof_ldpc_iterations = max_iter;
+  cfg.use_early_stop      = early_stop != 0;
+  cfg.new_data            = new_data != 0;
+  test_rx_buffer& rxb     = *h->rx[key];
+  if (worker < 0) {
+    return run_decode(*h->cpu, rxb, cfg, llrs, nof_llrs, tb, tb_bytes, stats);
+  }
+  if (static_cast<size_t>(worker) >= h->workers.size()) {
+    return -2;
+  }
+  int r = -1;
+  h->workers[worker]->run([&] { r = run_decode(*h->decs[worker], rxb, cfg, llrs, nof_llrs, tb, tb_bytes, stats); });
+  return r;
+}
 
 void* hal_create(int device, unsigned max_cb_ids)
 {

@@ -169,18 +169,20 @@ long long ref_dl_slot_timed(int            nof_ues,
 
 /// One UL slot before the decoder: OFDM demodulation of 4 ports (4096-point generic DFT), then per UE single-layer
 /// DM-RS channel estimation (filter / average, CFO compensation when compensate_cfo: du_low's defaults) on the DM-RS
-/// symbols of dmrs_mask and PUSCH demodulation (ZF 1 x 4) of its RBs. Returns the elapsed nanoseconds; out_ofdm_ns /
+/// symbols of dmrs_mask and PUSCH demodulation (ZF 1 x 4) of its RBs, for slot slot_index of the frame (DM-RS c_init;
+/// the OFDM phase compensation of the slot within the subframe). Returns the elapsed nanoseconds; out_ofdm_ns /
 /// out_chest_ns get the OFDM and estimation parts. llr_out (optional): the LLRs of every UE, concatenated.
-long long ref_ul_slot_timed(int          nof_ues,
-                            const int*   rb_start,
-                            const int*   nof_rb,
-                            int          qm,
-                            unsigned     dmrs_mask,
-                            int          compensate_cfo,
-                            const float* samples_in,
-                            int8_t*      llr_out,
-                            long long*   out_ofdm_ns,
-                            long long*   out_chest_ns)
+long long ref_ul_slot_timed_at(int          nof_ues,
+                               const int*   rb_start,
+                               const int*   nof_rb,
+                               int          qm,
+                               unsigned     dmrs_mask,
+                               int          compensate_cfo,
+                               int          slot_index,
+                               const float* samples_in,
+                               int8_t*      llr_out,
+                               long long*   out_ofdm_ns,
+                               long long*   out_chest_ns)
 {
   static thread_local resource_grid_impl                          grid(4, 14, 273 * 12);
   static thread_local std::unique_ptr<ofdm_slot_demodulator_impl> ofdm;
@@ -236,7 +238,7 @@ long long ref_ul_slot_timed(int          nof_ues,
     std::copy(reinterpret_cast<const cf_t*>(samples_in) + p * slot_size,
               reinterpret_cast<const cf_t*>(samples_in) + (p + 1) * slot_size,
               buf.begin());
-    ofdm->demodulate(grid.get_writer(), buf, p, 0);
+    ofdm->demodulate(grid.get_writer(), buf, p, static_cast<unsigned>(slot_index) % 2u);
   }
   *out_ofdm_ns   = ns_since(t0);
   long long chest = 0;
@@ -244,7 +246,7 @@ long long ref_ul_slot_timed(int          nof_ues,
   null_notifier    notifier;
   for (int u = 0; u < nof_ues; ++u) {
     dmrs_pusch_estimator::configuration cfg;
-    cfg.slot = slot_point(subcarrier_spacing::kHz30, 0);
+    cfg.slot = slot_point(subcarrier_spacing::kHz30, static_cast<unsigned>(slot_index));
     dmrs_pusch_estimator::pseudo_random_sequence_configuration seq;
     seq.type          = dmrs_type::TYPE1;
     seq.nof_tx_layers = 1;
@@ -289,6 +291,22 @@ long long ref_ul_slot_timed(int          nof_ues,
   }
   *out_chest_ns = chest;
   return ns_since(t0);
+}
+
+/// ref_ul_slot_timed_at of slot 0 of the frame.
+long long ref_ul_slot_timed(int          nof_ues,
+                            const int*   rb_start,
+                            const int*   nof_rb,
+                            int          qm,
+                            unsigned     dmrs_mask,
+                            int          compensate_cfo,
+                            const float* samples_in,
+                            int8_t*      llr_out,
+                            long long*   out_ofdm_ns,
+                            long long*   out_chest_ns)
+{
+  return ref_ul_slot_timed_at(nof_ues, rb_start, nof_rb, qm, dmrs_mask, compensate_cfo, 0, samples_in, llr_out,
+                              out_ofdm_ns, out_chest_ns);
 }
 
 } // extern "C"

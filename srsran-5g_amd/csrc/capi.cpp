@@ -413,6 +413,11 @@ int srsgpu_context_create(int device, srsgpu_context** out)
   return SRSGPU_OK;
 }
 
+int srsgpu_context_device(const srsgpu_context* ctx)
+{
+  return ctx == nullptr ? -1 : ctx->device;
+}
+
 void srsgpu_context_destroy(srsgpu_context* ctx)
 {
   if (ctx == nullptr) {

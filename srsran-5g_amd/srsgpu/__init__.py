@@ -320,6 +320,8 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_context_create.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
     lib.srsgpu_context_destroy.argtypes = [P]
     lib.srsgpu_context_destroy.restype = None
+    lib.srsgpu_context_device.argtypes = [P]
+    lib.srsgpu_context_device.restype = ctypes.c_int
     lib.srsgpu_ldpc_decoder_plan_create.argtypes = [P, ctypes.c_int, P, ctypes.c_uint32, ctypes.POINTER(P)]
     lib.srsgpu_ldpc_decoder_plan_execute.argtypes = [P, P, P, P, P]
     lib.srsgpu_ldpc_decoder_plan_destroy.argtypes = [P]
@@ -399,7 +401,7 @@ def load_library(path: str = LIB_PATH):
 
 # Every symbol include/srsgpu_phy.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = [
-    "srsgpu_version", "srsgpu_last_error", "srsgpu_context_create", "srsgpu_context_destroy",
+    "srsgpu_version", "srsgpu_last_error", "srsgpu_context_create", "srsgpu_context_destroy", "srsgpu_context_device",
     "srsgpu_ldpc_decoder_plan_create", "srsgpu_ldpc_decoder_plan_execute", "srsgpu_ldpc_decoder_plan_destroy",
     "srsgpu_ldpc_decode", "srsgpu_pusch_cb_plan_create", "srsgpu_pusch_cb_plan_execute",
     "srsgpu_pusch_cb_plan_destroy", "srsgpu_pdsch_encoder_plan_create", "srsgpu_pdsch_encoder_plan_nof_codeblocks",

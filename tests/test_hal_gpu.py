@@ -78,3 +78,43 @@ def test_hal_pdsch_encoder_gpu_equals_reference_cpu(hal):
         a = hal.pdsch_encode(hal_lib.PDSCH_CPU, seg.base_graph, rv, g.qm, g.nof_layers, g.nof_ch_symbols, tb, Nref)
         b = hal.pdsch_encode(hal_lib.PDSCH_HW_GPU, seg.base_graph, rv, g.qm, g.nof_layers, g.nof_ch_symbols, tb, Nref)
         assert np.array_equal(a, b), (i, seg.tbs, seg.nof_segments, rv, Nref)
+
+
+def test_hal_pusch_decoder_thread_pool_shares_harq():
+    """The reference's thread-pool wiring of the HW decoder (pusch_decoder_factory_hw, factories.cpp:122-140): a
+    temporary accelerator factory (destroyed before decoding) makes 4 accelerators in one hw_decoder_pool; 4 worker
+    threads each own a pusch_decoder_hw_impl. Every HARQ process sends rv0 (too noisy to decode alone for most) on one
+    thread and its rv2 retransmission on ANOTHER thread, i.e. another accelerator; processes interleave. The combined
+    results (TB bytes, CRC, LDPC iteration statistics) equal the reference CPU decoder's on the same sequence."""
+    import hal_lib
+    orc = Oracle()
+    rng = np.random.default_rng(31)
+    pool = hal_lib.HalPool(0, max_cb_ids=64 * 160, nof_threads=4)
+    try:
+        gs = sch.slot_100mhz_4x4(nof_layers=1, nof_dmrs_symbols=2)[:6] + \
+            sch.slot_100mhz_4x4(nof_ues=2, nof_prb=273, nof_layers=2, mcs=27)[:2]
+        jobs = []
+        for h, g in enumerate(gs):
+            seg = g.segmentation()
+            tb = rng.integers(0, 256, seg.tbs // 8).astype(np.uint8)
+            llrs = []
+            for rv in (0, 2):
+                cw, _, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, rv, g.qm, g.nof_layers, 0, g.nof_ch_symbols)
+                llrs.append(bits_to_llrs(rng, cw, amp=6.0, noise=[3.5, 4.5, 5.5][h % 3]))
+            jobs.append((h, g, seg, tb, llrs))
+        # All first transmissions, then all retransmissions, each on a thread other than the first one's.
+        ok = {}
+        for step, (rv, new_data) in enumerate(((0, True), (2, False))):
+            for h, g, seg, tb, llrs in jobs:
+                worker = (h + 2 * step) % 4
+                args = (h, seg.nof_segments, seg.base_graph, rv, g.qm, g.nof_layers, llrs[step], seg.tbs // 8)
+                tb_gpu, s_gpu = pool.decode(worker, *args, new_data=new_data)
+                tb_cpu, s_cpu = pool.decode(-1, *args, new_data=new_data)
+                assert s_gpu == s_cpu, (h, rv, s_cpu, s_gpu)
+                if s_cpu["tb_crc_ok"]:
+                    assert np.array_equal(tb_gpu, tb) and np.array_equal(tb_cpu, tb), (h, rv)
+                ok[(h, step)] = s_cpu["tb_crc_ok"]
+        # Combining happened: some processes fail alone at rv0 and decode after the rv2 retransmission.
+        assert sum(not ok[(h, 0)] and ok[(h, 1)] for h in range(len(jobs))) >= 1, ok
+    finally:
+        pool.close()

@@ -583,6 +583,14 @@ int srsgpu_pusch_demodulator_plan_create_ex(srsgpu_context*                  ctx
                                             uint32_t                         grid_nof_ports,
                                             srsgpu_pusch_demodulator_plan**  plan);
 
+/** Copies the descrambling sequence of transmission tx (TS 38.211 section 5.2.1, c_init = rnti 2^15 + n_id: the
+ *  sequence pusch_demodulator_impl.cpp:277 generates and passes to pusch_codeword_buffer::on_new_block) into d_words:
+ *  ceil(nof_llrs / 32) 32-bit words, bit 31 of word w = c(32 w) (the plan keeps it resident). Asynchronous. */
+int srsgpu_pusch_demodulator_plan_scrambling(const srsgpu_pusch_demodulator_plan* plan,
+                                             uint32_t                             tx,
+                                             uint32_t*                            d_words,
+                                             void*                                stream);
+
 /* Post-equalization statistics (pusch_demodulator_notifier::demodulation_stats, pusch_demodulator_impl.cpp:355-443):
  * SRSGPU_DEMOD_STATS floats per transmission, rows 0..13 = OFDM symbol l (on_provisional_stats) and row 14 = the whole
  * transmission (on_end_stats), each (SINR dB, EVM): SINR = -10 log10(mean of the finite equalizer noise variances,

@@ -1,0 +1,149 @@
+// Staging and plan caching shared by the signal-chain bindings (integration/*_gpu.cpp). The reference's processors
+// hand a binding host-side objects (resource grids, channel estimates, bit buffers); a binding stages what its kernel
+// reads through pinned host memory into HBM, runs the cached srsgpu plan on its own stream and copies the results back
+// the same way. Everything is grow-only and owned by one binding instance (one per processing thread, like the
+// reference's own components), so steady state allocates nothing.
+#pragma once
+
+#include "gpu_context.h"
+#include <algorithm>
+#include <cstring>
+#include <list>
+#include <vector>
+
+namespace srsran {
+namespace gpu {
+
+/// A pinned host buffer and a device buffer of the same capacity (bytes).
+class staged_buffer
+{
+public:
+  explicit staged_buffer(const char* who_) : who(who_) {}
+  staged_buffer(const staged_buffer&)            = delete;
+  staged_buffer& operator=(const staged_buffer&) = delete;
+  ~staged_buffer()
+  {
+    (void)hipFree(d);
+    (void)hipHostFree(h);
+  }
+
+  /// Makes room for n bytes (contents are not preserved when it grows).
+  void reserve(size_t n)
+  {
+    if (n <= cap) {
+      return;
+    }
+    const size_t c = std::max(n, 2 * cap);
+    (void)hipFree(d);
+    (void)hipHostFree(h);
+    d = nullptr;
+    h = nullptr;
+    cap = 0;
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&h), c), who, "pinned staging");
+    hip_check(hipMalloc(reinterpret_cast<void**>(&d), c), who, "device buffer");
+    cap = c;
+  }
+
+  template <typename T = uint8_t>
+  T* host(size_t byte_offset = 0)
+  {
+    return reinterpret_cast<T*>(h + byte_offset);
+  }
+  template <typename T = uint8_t>
+  T* dev(size_t byte_offset = 0)
+  {
+    return reinterpret_cast<T*>(d + byte_offset);
+  }
+
+  void upload(size_t offset, size_t n, hipStream_t s)
+  {
+    if (n != 0) {
+      hip_check(hipMemcpyAsync(d + offset, h + offset, n, hipMemcpyHostToDevice, s), who, "upload");
+    }
+  }
+  void download(size_t offset, size_t n, hipStream_t s)
+  {
+    if (n != 0) {
+      hip_check(hipMemcpyAsync(h + offset, d + offset, n, hipMemcpyDeviceToHost, s), who, "download");
+    }
+  }
+
+private:
+  const char* who;
+  uint8_t*    h   = nullptr;
+  uint8_t*    d   = nullptr;
+  size_t      cap = 0;
+};
+
+/// Appends the bytes of a POD value to a cache key.
+template <typename T>
+void key_append(std::vector<uint8_t>& key, const T& v)
+{
+  const auto* p = reinterpret_cast<const uint8_t*>(&v);
+  key.insert(key.end(), p, p + sizeof(T));
+}
+
+/// Most-recently-used cache of srsgpu plans keyed by their configuration bytes (a cell's grants repeat slot after
+/// slot): create() runs only on a miss; the least recently used plan is destroyed beyond `capacity`.
+template <typename Plan>
+class plan_cache
+{
+public:
+  plan_cache(void (*destroy_)(Plan*), size_t capacity_ = 64) : destroy(destroy_), capacity(capacity_) {}
+  plan_cache(const plan_cache&)            = delete;
+  plan_cache& operator=(const plan_cache&) = delete;
+  ~plan_cache()
+  {
+    for (auto& e : lru) {
+      destroy(e.plan);
+    }
+  }
+
+  template <typename Create>
+  Plan* get(const std::vector<uint8_t>& key, Create&& create)
+  {
+    for (auto it = lru.begin(); it != lru.end(); ++it) {
+      if (it->key == key) {
+        lru.splice(lru.begin(), lru, it);
+        return lru.front().plan;
+      }
+    }
+    Plan* plan = create();
+    lru.push_front({key, plan});
+    if (lru.size() > capacity) {
+      destroy(lru.back().plan);
+      lru.pop_back();
+    }
+    return plan;
+  }
+
+private:
+  struct entry {
+    std::vector<uint8_t> key;
+    Plan*                plan;
+  };
+  void (*destroy)(Plan*);
+  size_t           capacity;
+  std::list<entry> lru;
+};
+
+/// A HIP stream on the context's device, destroyed with its owner.
+class owned_stream
+{
+public:
+  owned_stream(srsgpu_context* ctx, const char* who)
+  {
+    hip_check(hipSetDevice(srsgpu_context_device(ctx)), who, "device");
+    hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), who, "stream");
+  }
+  owned_stream(const owned_stream&)            = delete;
+  owned_stream& operator=(const owned_stream&) = delete;
+  ~owned_stream() { (void)hipStreamDestroy(s); }
+  hipStream_t get() const { return s; }
+
+private:
+  hipStream_t s = nullptr;
+};
+
+} // namespace gpu
+} // namespace srsran

@@ -1,0 +1,68 @@
+// Factories of the MI355X implementations of the reference's signal-chain interfaces (the declarations a srsRAN
+// maintainer adds next to signal_processor_factories.h, pusch/factories.h, pdsch/factories.h and
+// lower/modulation/modulation_factories.h). Each factory shares the device's srsgpu context with every object it
+// creates (integration/gpu_context.h); objects are per processing thread like the reference's own components and
+// stage the caller's host objects (resource grids, channel estimates, codewords, samples) through pinned memory.
+#pragma once
+
+#include "srsran/phy/lower/modulation/modulation_factories.h"
+#include "srsran/phy/upper/channel_processors/pdsch/factories.h"
+#include "srsran/phy/upper/channel_processors/pusch/factories.h"
+#include "srsran/phy/upper/signal_processors/signal_processor_factories.h"
+#include <cstdint>
+#include <memory>
+
+namespace srsran {
+namespace gpu {
+
+/// create_dmrs_pusch_estimator_factory_sw's strategy arguments (signal_processor_factories.h:74-80), as srsgpu codes.
+struct pusch_estimator_options {
+  uint8_t fd_smoothing   = 2;  ///< SRSGPU_CHEST_FD_*: 0 none, 1 mean, 2 filter (du_low default).
+  uint8_t td_strategy    = 0;  ///< SRSGPU_CHEST_TD_*: 0 average (du_low default), 1 interpolate.
+  bool    compensate_cfo = true;
+};
+
+/// create_pusch_demodulator_factory_sw's options (pusch/factories.h:92-99): the equalizer algorithm, whether an EVM
+/// calculator is given, and enable_post_eq_sinr.
+struct pusch_demodulator_options {
+  uint8_t equalizer           = 0;  ///< SRSGPU_EQ_ZF (reference default) or SRSGPU_EQ_MMSE.
+  bool    enable_evm          = true;
+  bool    enable_post_eq_sinr = true;
+};
+
+/// Maps the reference's strategy enums onto pusch_estimator_options.
+inline pusch_estimator_options make_pusch_estimator_options(port_channel_estimator_fd_smoothing_strategy     fd,
+                                                            port_channel_estimator_td_interpolation_strategy td,
+                                                            bool compensate_cfo)
+{
+  pusch_estimator_options o;
+  o.fd_smoothing = fd == port_channel_estimator_fd_smoothing_strategy::none
+                       ? 0
+                       : (fd == port_channel_estimator_fd_smoothing_strategy::mean ? 1 : 2);
+  o.td_strategy    = td == port_channel_estimator_td_interpolation_strategy::interpolate ? 1 : 0;
+  o.compensate_cfo = compensate_cfo;
+  return o;
+}
+
+} // namespace gpu
+
+/// PUSCH DM-RS channel estimator on GPU `device` (integration/pusch_chain_gpu.cpp).
+std::shared_ptr<dmrs_pusch_estimator_factory> create_dmrs_pusch_estimator_factory_gpu(int device,
+                                                                                     const gpu::pusch_estimator_options& opts);
+
+/// PUSCH demodulator on GPU `device` (integration/pusch_chain_gpu.cpp).
+std::shared_ptr<pusch_demodulator_factory> create_pusch_demodulator_factory_gpu(int                                   device,
+                                                                                const gpu::pusch_demodulator_options& opts);
+
+/// PDSCH modulator on GPU `device` (integration/pdsch_chain_gpu.cpp).
+std::shared_ptr<pdsch_modulator_factory> create_pdsch_modulator_factory_gpu(int device);
+
+/// PDSCH DM-RS processor on GPU `device` (integration/pdsch_chain_gpu.cpp).
+std::shared_ptr<dmrs_pdsch_processor_factory> create_dmrs_pdsch_processor_factory_gpu(int device);
+
+/// OFDM slot modulator / demodulator on GPU `device` (integration/ofdm_gpu.cpp). The symbol-granularity creators
+/// return nullptr (the GPU transforms whole slots), as the reference's factories do for unsupported configurations.
+std::shared_ptr<ofdm_modulator_factory>   create_ofdm_modulator_factory_gpu(int device);
+std::shared_ptr<ofdm_demodulator_factory> create_ofdm_demodulator_factory_gpu(int device);
+
+} // namespace srsran

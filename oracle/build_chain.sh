@@ -1,0 +1,64 @@
+#!/usr/bin/env bash
+# TEST INFRASTRUCTURE ONLY.
+# Builds oracle/_ref/libsrschain.so: the reference's own PUSCH / PDSCH processors (pusch_processor_impl,
+# pdsch_processor_impl) and the components they need that libsrsref.so / libsrshal.so do not hold (UCI decoder, polar
+# and short-block codes, PT-RS generator, UL-SCH information), compiled from their sources where they lie under
+# /root/reference, the signal-chain bindings a maintainer adds (integration/*_gpu.cpp) and the C harness
+# oracle/ref/ref_chain.cpp, linked against oracle/_ref/libsrshal.so, libsrsref.so and libsrsgpu_phy.so. Output only
+# into oracle/_ref/ (git-ignored, shipped to the GPU box with the snapshot). Skips quietly without the reference tree.
+set -euo pipefail
+REF=${SRSRAN_REF:-/root/reference}
+HERE=$(cd "$(dirname "$0")" && pwd)
+ROOT=$(cd "$HERE/.." && pwd)
+OUT="$HERE/_ref"
+if [ ! -d "$REF/lib/phy/upper/channel_processors/pusch" ]; then
+  echo "build_chain: reference tree not present; keeping existing $OUT" >&2
+  exit 0
+fi
+mkdir -p "$OUT/obj_chain"
+CXX=${CXX:-g++}
+FLAGS="-std=c++17 -O2 -fPIC -DNDEBUG -DFMT_HEADER_ONLY -DASSERTS_ENABLED=0 -mavx2 -mfma -I$REF/include
+       -I$REF/external/fmt/include -I$REF/external -I$REF -I$REF/lib/phy/upper/channel_coding -I$ROOT/include
+       -I$ROOT/integration -I/opt/rocm/include -D__HIP_PLATFORM_AMD__"
+U=$REF/lib/phy/upper
+SRCS=(
+  "$U/channel_processors/pusch/pusch_processor_impl.cpp"
+  "$U/channel_processors/pusch/pusch_processor_validator_impl.cpp"
+  "$U/channel_processors/pdsch/pdsch_processor_impl.cpp"
+  "$U/channel_processors/pdsch/pdsch_processor_validator_impl.cpp"
+  "$U/channel_processors/uci/uci_decoder_impl.cpp"
+  "$U/channel_coding/short/short_block_detector_impl.cpp"
+  "$U/channel_coding/short/short_block_encoder_impl.cpp"
+  "$REF/lib/ran/uci/uci_part2_size_calculator.cpp"
+  "$REF/lib/ran/pusch/ulsch_info.cpp"
+  "$REF/lib/ran/sch/sch_segmentation.cpp"
+  "$REF/lib/ran/ptrs/ptrs_pattern.cpp"
+  "$U/channel_coding/polar/polar_code_impl.cpp"
+  "$U/channel_coding/polar/polar_decoder_impl.cpp"
+  "$U/channel_coding/polar/polar_encoder_impl.cpp"
+  "$U/channel_coding/polar/polar_rate_dematcher_impl.cpp"
+  "$U/channel_coding/polar/polar_deallocator_impl.cpp"
+  "$U/signal_processors/ptrs/ptrs_pdsch_generator_impl.cpp"
+  "$ROOT/integration/pusch_chain_gpu.cpp"
+  "$ROOT/integration/pdsch_chain_gpu.cpp"
+  "$ROOT/integration/ofdm_gpu.cpp"
+  "$HERE/ref/ref_chain.cpp"
+)
+OBJS=()
+pids=()
+for src in "${SRCS[@]}"; do
+  obj="$OUT/obj_chain/$(basename "${src%.cpp}").o"
+  OBJS+=("$obj")
+  newest=$(ls -t "$ROOT"/integration/*.h "$ROOT/include/srsgpu_phy.h" | head -1)
+  if [ ! -f "$obj" ] || [ "$src" -nt "$obj" ] || [ "$0" -nt "$obj" ] || [ "$newest" -nt "$obj" ]; then
+    $CXX $FLAGS -c "$src" -o "$obj" &
+    pids+=($!)
+  fi
+done
+rc=0
+for p in "${pids[@]:-}"; do [ -n "$p" ] && { wait "$p" || rc=1; }; done
+[ $rc -eq 0 ] || { echo "build_chain: compilation failed" >&2; exit 1; }
+$CXX -shared -o "$OUT/libsrschain.so" "${OBJS[@]}" -L"$OUT" -lsrshal -lsrsref -L"$ROOT/srsran-5g_amd/lib" \
+  -lsrsgpu_phy -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$ORIGIN' -Wl,-rpath,'$ORIGIN/../../srsran-5g_amd/lib' \
+  -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
+echo "build_chain: $OUT/libsrschain.so"

@@ -1,0 +1,746 @@
+// TEST INFRASTRUCTURE ONLY: the reference's own PUSCH and PDSCH processors (pusch_processor_impl, pdsch_processor_impl,
+// compiled from their sources by oracle/build_chain.sh) assembled twice - once from the reference's CPU components, once
+// with the signal-chain bindings of integration/ (GPU DM-RS estimator, PUSCH demodulator, PDSCH modulator, PDSCH DM-RS,
+// and the HAL accelerators) plugged in through the same interfaces - plus the lower-PHY OFDM slot transforms both ways,
+// so tests/test_chain_gpu.py can compare the two on the same inputs. The wiring mirrors the reference's factories
+// (pusch/factories.cpp, pdsch/factories.cpp, upper_phy_factories.cpp:432-1014): estimator filter / average / CFO
+// compensation (du_low defaults), ZF equalizer with EVM and post-equalisation SINR, the UL-SCH demultiplexer and the UCI
+// decoder of the reference, LDPC with early stop.
+//
+// A UE transmitter (chain_ue_tx) built from the reference's PDSCH encoder, modulator and DM-RS processor makes the
+// test's PUSCH: the PUSCH scrambling (c_init = rnti 2^15 + n_id), modulation, layer mapping and DM-RS sequences are the
+// PDSCH ones (TS 38.211 6.3.1.1 / 7.3.1.1, 6.4.1.1.1 / 7.4.1.1.1).
+#include "hw_accelerator_pusch_dec_gpu.h"
+#include "signal_chain_gpu.h"
+
+#include "srsran/phy/support/resource_grid_reader.h"
+#include "srsran/phy/support/resource_grid_writer.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_processor_result_notifier.h"
+#include "srsran/phy/upper/unique_rx_buffer.h"
+#include "srsran/ran/sch/sch_dmrs_power.h"
+#include "srsran/srsvec/bit.h"
+
+#include "lib/phy/generic_functions/dft_processor_generic_impl.h"
+#include "lib/phy/generic_functions/precoding/channel_precoder_generic.h"
+#include "lib/phy/lower/modulation/ofdm_demodulator_impl.h"
+#include "lib/phy/lower/modulation/ofdm_modulator_impl.h"
+#include "lib/phy/support/interpolator/interpolator_linear_impl.h"
+#include "lib/phy/support/resource_grid_impl.h"
+#include "lib/phy/support/resource_grid_mapper_impl.h"
+#include "lib/phy/support/time_alignment_estimator/time_alignment_estimator_dft_impl.h"
+#include "lib/phy/upper/channel_coding/crc_calculator_generic_impl.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_decoder_avx2.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_decoder_avx512.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_encoder_avx2.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_rate_dematcher_avx2_impl.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_rate_matcher_impl.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_segmenter_rx_impl.h"
+#include "lib/phy/upper/channel_coding/ldpc/ldpc_segmenter_tx_impl.h"
+#include "lib/phy/upper/channel_coding/polar/polar_code_impl.h"
+#include "lib/phy/upper/channel_coding/polar/polar_deallocator_impl.h"
+#include "lib/phy/upper/channel_coding/polar/polar_decoder_impl.h"
+#include "lib/phy/upper/channel_coding/polar/polar_encoder_impl.h"
+#include "lib/phy/upper/channel_coding/polar/polar_rate_dematcher_impl.h"
+#include "lib/phy/upper/channel_coding/short/short_block_detector_impl.h"
+#include "lib/phy/upper/channel_modulation/demodulation_mapper_impl.h"
+#include "lib/phy/upper/channel_modulation/evm_calculator_generic_impl.h"
+#include "lib/phy/upper/channel_modulation/modulation_mapper_lut_impl.h"
+#include "lib/phy/upper/channel_processors/pdsch/pdsch_encoder_hw_impl.h"
+#include "lib/phy/upper/channel_processors/pdsch/pdsch_encoder_impl.h"
+#include "lib/phy/upper/channel_processors/pdsch/pdsch_modulator_impl.h"
+#include "lib/phy/upper/channel_processors/pdsch/pdsch_processor_impl.h"
+#include "lib/phy/upper/channel_processors/pusch/pusch_codeblock_decoder.h"
+#include "lib/phy/upper/channel_processors/pusch/pusch_decoder_hw_impl.h"
+#include "lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.h"
+#include "lib/phy/upper/channel_processors/pusch/pusch_demodulator_impl.h"
+#include "lib/phy/upper/channel_processors/pusch/pusch_processor_impl.h"
+#include "lib/phy/upper/channel_processors/pusch/ulsch_demultiplex_impl.h"
+#include "lib/phy/upper/channel_processors/uci/uci_decoder_impl.h"
+#include "lib/phy/upper/equalization/channel_equalizer_generic_impl.h"
+#include "lib/phy/upper/sequence_generators/low_papr_sequence_generator_impl.h"
+#include "lib/phy/upper/sequence_generators/pseudo_random_generator_impl.h"
+#include "lib/phy/upper/signal_processors/dmrs_pdsch_processor_impl.h"
+#include "lib/phy/upper/signal_processors/dmrs_pusch_estimator_impl.h"
+#include "lib/phy/upper/signal_processors/port_channel_estimator_average_impl.h"
+#include "lib/phy/upper/signal_processors/ptrs/ptrs_pdsch_generator_impl.h"
+
+#include <cmath>
+#include <cstdio>
+#include <exception>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <vector>
+
+using namespace srsran;
+
+namespace {
+
+constexpr unsigned CB_IDS_PER_HARQ = 160;
+
+/// Test PUSCH / PDSCH parameters (mirrored by tests/chain_harness.py).
+struct chain_params {
+  int32_t slot;              ///< Slot index within the frame (30 kHz SCS).
+  int32_t rnti;
+  int32_t n_id;
+  int32_t qm;                ///< Modulation order.
+  float   target_code_rate;  ///< R x 1024.
+  int32_t rv;
+  int32_t base_graph;
+  int32_t new_data;
+  int32_t harq_id;
+  int32_t nof_layers;
+  int32_t nof_ports;         ///< Rx ports (PUSCH) or precoding ports (PDSCH).
+  int32_t dmrs_mask;
+  int32_t dmrs_type2;
+  int32_t scrambling_id;
+  int32_t n_scid;
+  int32_t cdm_groups;        ///< CDM groups without data.
+  int32_t rb_start;          ///< VRB allocation start within the BWP.
+  int32_t nof_rb;
+  int32_t bwp_start;
+  int32_t bwp_size;
+  int32_t start_symbol;
+  int32_t nof_symbols;
+  int32_t nof_harq_ack;
+  int32_t nof_csi_part1;
+  int32_t dc_position;       ///< -1: none.
+  int32_t tbs_lbrm_bytes;
+  int32_t grid_prb;
+  int32_t max_iterations;
+};
+
+symbol_slot_mask symbol_mask(int bits)
+{
+  symbol_slot_mask m(14);
+  for (unsigned l = 0; l != 14; ++l) {
+    m.set(l, ((bits >> l) & 1) != 0);
+  }
+  return m;
+}
+
+modulation_scheme to_mod(int qm)
+{
+  return static_cast<modulation_scheme>(qm);
+}
+
+std::unique_ptr<crc_calculator> crc(crc_generator_poly p)
+{
+  return std::make_unique<crc_calculator_generic_impl>(p);
+}
+
+template <typename S>
+S sch_crc()
+{
+  S s;
+  s.crc16  = crc(crc_generator_poly::CRC16);
+  s.crc24A = crc(crc_generator_poly::CRC24A);
+  s.crc24B = crc(crc_generator_poly::CRC24B);
+  return s;
+}
+
+std::unique_ptr<ldpc_decoder> cpu_ldpc_decoder()
+{
+  if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw")) {
+    return std::make_unique<ldpc_decoder_avx512>();
+  }
+  return std::make_unique<ldpc_decoder_avx2>();
+}
+
+std::unique_ptr<time_alignment_estimator_dft_impl> ta_estimator()
+{
+  time_alignment_estimator_dft_impl::collection_dft_processors dfts;
+  for (unsigned n = time_alignment_estimator_dft_impl::min_dft_size; n <= time_alignment_estimator_dft_impl::max_dft_size;
+       n *= 2) {
+    dfts.emplace(n, std::make_unique<dft_processor_generic_impl>(
+                        dft_processor::configuration{n, time_alignment_estimator_dft_impl::dft_direction}));
+  }
+  return std::make_unique<time_alignment_estimator_dft_impl>(std::move(dfts));
+}
+
+std::unique_ptr<uci_decoder> cpu_uci_decoder()
+{
+  return std::make_unique<uci_decoder_impl>(std::make_unique<short_block_detector_impl>(),
+                                            std::make_unique<polar_code_impl>(),
+                                            std::make_unique<polar_rate_dematcher_impl>(),
+                                            std::make_unique<polar_decoder_impl>(std::make_unique<polar_encoder_impl>(),
+                                                                                 polar_code::NMAX_LOG),
+                                            std::make_unique<polar_deallocator_impl>(),
+                                            crc(crc_generator_poly::CRC6),
+                                            crc(crc_generator_poly::CRC11));
+}
+
+std::unique_ptr<resource_grid_mapper> cpu_mapper()
+{
+  return std::make_unique<resource_grid_mapper_impl>(std::make_unique<channel_precoder_generic>());
+}
+
+/// Minimal unique_rx_buffer::callback (as oracle/ref/ref_hal.cpp): per codeblock soft bits, data bits, CRC flags.
+class test_rx_buffer : public unique_rx_buffer::callback
+{
+public:
+  test_rx_buffer(unsigned nof_cbs, unsigned first_abs_id) :
+    crcs(nof_cbs, 0), soft(nof_cbs, std::vector<log_likelihood_ratio>(66 * 384)),
+    data(nof_cbs, std::vector<uint8_t>(22 * 384 / 8)), abs0(first_abs_id)
+  {
+  }
+  unsigned   get_nof_codeblocks() const override { return static_cast<unsigned>(crcs.size()); }
+  void       reset_codeblocks_crc() override { std::fill(crcs.begin(), crcs.end(), 0); }
+  span<bool> get_codeblocks_crc() override { return span<bool>(reinterpret_cast<bool*>(crcs.data()), crcs.size()); }
+  unsigned   get_absolute_codeblock_id(unsigned cb) const override { return abs0 + cb; }
+  span<log_likelihood_ratio> get_codeblock_soft_bits(unsigned cb, unsigned size) override
+  {
+    return span<log_likelihood_ratio>(soft[cb]).first(size);
+  }
+  bit_buffer get_codeblock_data_bits(unsigned cb, unsigned size) override
+  {
+    return bit_buffer::from_bytes(data[cb]).first(size);
+  }
+  bool try_lock() override { return true; }
+  void unlock() override {}
+  void release() override { reset_codeblocks_crc(); }
+
+private:
+  std::vector<char>                              crcs;
+  std::vector<std::vector<log_likelihood_ratio>> soft;
+  std::vector<std::vector<uint8_t>>              data;
+  unsigned                                       abs0;
+};
+
+class result_capture : public pusch_processor_result_notifier
+{
+public:
+  void on_uci(const pusch_processor_result_control& r) override
+  {
+    uci      = r;
+    have_uci = true;
+  }
+  void on_sch(const pusch_processor_result_data& r) override
+  {
+    sch      = r;
+    have_sch = true;
+  }
+  pusch_processor_result_control uci;
+  pusch_processor_result_data    sch;
+  bool                           have_uci = false;
+  bool                           have_sch = false;
+};
+
+class pdsch_done : public pdsch_processor_notifier
+{
+public:
+  void on_finish_processing() override { done = true; }
+  bool done = false;
+};
+
+/// A pusch_processor_impl over the given estimator / demodulator / decoder (one processing thread).
+std::unique_ptr<pusch_processor> make_pusch_processor(std::unique_ptr<dmrs_pusch_estimator> est,
+                                                      std::unique_ptr<pusch_demodulator>    demod,
+                                                      std::unique_ptr<pusch_decoder>        dec,
+                                                      unsigned                              max_iter)
+{
+  std::vector<std::unique_ptr<pusch_processor_impl::concurrent_dependencies>> deps;
+  deps.push_back(std::make_unique<pusch_processor_impl::concurrent_dependencies>(
+      std::move(est),
+      std::move(demod),
+      std::make_unique<ulsch_demultiplex_impl>(),
+      cpu_uci_decoder(),
+      channel_estimate::channel_estimate_dimensions{MAX_RB, MAX_NSYMB_PER_SLOT, 4, 4}));
+  pusch_processor_impl::configuration cfg;
+  cfg.thread_local_dependencies_pool =
+      std::make_shared<pusch_processor_impl::concurrent_dependencies_pool_type>(std::move(deps));
+  cfg.decoder               = std::move(dec);
+  cfg.dec_nof_iterations    = max_iter;
+  cfg.dec_enable_early_stop = true;
+  cfg.csi_sinr_calc_method  = channel_state_information::sinr_type::post_equalization;
+  return std::make_unique<pusch_processor_impl>(cfg);
+}
+
+std::unique_ptr<pusch_decoder> cpu_pusch_decoder()
+{
+  std::vector<std::unique_ptr<pusch_codeblock_decoder>> cbs;
+  auto                                                  cb_crc = sch_crc<pusch_codeblock_decoder::sch_crc>();
+  cbs.push_back(std::make_unique<pusch_codeblock_decoder>(
+      std::make_unique<ldpc_rate_dematcher_avx2_impl>(), cpu_ldpc_decoder(), cb_crc));
+  auto pool = std::make_shared<pusch_decoder_impl::codeblock_decoder_pool>(std::move(cbs));
+  return std::make_unique<pusch_decoder_impl>(
+      std::make_unique<ldpc_segmenter_rx_impl>(), pool, sch_crc<pusch_decoder_impl::sch_crc>(), nullptr, MAX_RB, 4);
+}
+
+std::unique_ptr<pdsch_encoder> cpu_pdsch_encoder()
+{
+  auto seg_crc = sch_crc<ldpc_segmenter_tx_impl::sch_crc>();
+  return std::make_unique<pdsch_encoder_impl>(
+      std::make_unique<ldpc_segmenter_tx_impl>(seg_crc),
+      std::make_unique<ldpc_encoder_avx2>(),
+      std::make_unique<ldpc_rate_matcher_impl>());
+}
+
+std::unique_ptr<pdsch_modulator> cpu_pdsch_modulator()
+{
+  return std::make_unique<pdsch_modulator_impl>(
+      std::make_unique<modulation_mapper_lut_impl>(), std::make_unique<pseudo_random_generator_impl>(), cpu_mapper());
+}
+
+std::unique_ptr<dmrs_pdsch_processor> cpu_dmrs_pdsch()
+{
+  return std::make_unique<dmrs_pdsch_processor_impl>(std::make_unique<pseudo_random_generator_impl>(), cpu_mapper());
+}
+
+std::unique_ptr<pdsch_processor> make_pdsch_processor(std::unique_ptr<pdsch_encoder>        enc,
+                                                      std::unique_ptr<pdsch_modulator>      mod,
+                                                      std::unique_ptr<dmrs_pdsch_processor> dmrs)
+{
+  return std::make_unique<pdsch_processor_impl>(
+      std::move(enc),
+      std::move(mod),
+      std::move(dmrs),
+      std::make_unique<ptrs_pdsch_generator_generic_impl>(std::make_unique<pseudo_random_generator_impl>(),
+                                                          cpu_mapper()));
+}
+
+struct chain_harness {
+  // PUSCH: 0 CPU reference, 1 GPU estimator + demodulator + CPU decoder, 2 GPU estimator + demodulator + HW decoder.
+  std::unique_ptr<pusch_processor>                                     pusch[3];
+  // PDSCH: 0 CPU reference, 1 HW encoder (GPU) + GPU modulator + GPU DM-RS.
+  std::unique_ptr<pdsch_processor>                                     pdsch[2];
+  std::map<std::pair<int, int>, std::unique_ptr<test_rx_buffer>>       rx;
+  std::shared_ptr<ofdm_modulator_factory>                              ofdm_mod_gpu;
+  std::shared_ptr<ofdm_demodulator_factory>                            ofdm_demod_gpu;
+  // UE transmitter (reference CPU components).
+  std::unique_ptr<pdsch_encoder>        tx_enc  = cpu_pdsch_encoder();
+  std::unique_ptr<pdsch_modulator>      tx_mod  = cpu_pdsch_modulator();
+  std::unique_ptr<dmrs_pdsch_processor> tx_dmrs = cpu_dmrs_pdsch();
+};
+
+/// Copies a (P, 14, nsc) bf16-pair array into the grid (all ports, all symbols).
+void load_grid(resource_grid& g, const uint16_t* in, unsigned P, unsigned nsc)
+{
+  std::vector<cbf16_t> row(nsc);
+  for (unsigned p = 0; p != P; ++p) {
+    for (unsigned l = 0; l != 14; ++l) {
+      std::memcpy(row.data(), in + 2 * (static_cast<size_t>(p) * 14 + l) * nsc, nsc * sizeof(cbf16_t));
+      g.get_writer().put(p, l, 0, 1, row);
+    }
+  }
+}
+
+void store_grid(const resource_grid& g, uint16_t* out, unsigned P, unsigned nsc)
+{
+  for (unsigned p = 0; p != P; ++p) {
+    for (unsigned l = 0; l != 14; ++l) {
+      span<const cbf16_t> v = g.get_reader().get_view(p, l);
+      std::memcpy(out + 2 * (static_cast<size_t>(p) * 14 + l) * nsc, v.data(), nsc * sizeof(cbf16_t));
+    }
+  }
+}
+
+precoding_configuration identity(unsigned L, unsigned P)
+{
+  precoding_configuration pc(L, P, 1, MAX_NOF_PRBS);
+  for (unsigned p = 0; p != P; ++p) {
+    for (unsigned l = 0; l != L; ++l) {
+      pc.set_coefficient(cf_t(p == l ? 1.0F : 0.0F, 0.0F), l, p, 0);
+    }
+  }
+  return pc;
+}
+
+unsigned nof_data_re(const chain_params& c)
+{
+  const unsigned dmrs_re = c.cdm_groups * (c.dmrs_type2 ? 4 : 6);
+  unsigned       n       = 0;
+  for (int l = c.start_symbol; l != c.start_symbol + c.nof_symbols; ++l) {
+    n += ((c.dmrs_mask >> l) & 1) ? NRE - dmrs_re : NRE;
+  }
+  return n * c.nof_rb;
+}
+
+/// Runs a harness entry point, turning a C++ exception (a binding's configuration or HIP error) into an error code
+/// the Python side reports, instead of terminating the test process.
+template <typename F>
+int guarded(const char* name, F&& f)
+{
+  try {
+    return f();
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "%s: %s\n", name, e.what());
+    return -100;
+  }
+}
+
+} // namespace
+
+extern "C" {
+
+/// Builds the CPU and GPU processors (GPU `device`): see the file comment.
+static void* chain_create_impl(int device, unsigned max_cb_ids)
+{
+  auto* h = new chain_harness();
+  // CPU reference.
+  auto cpu_est = std::make_unique<dmrs_pusch_estimator_impl>(
+      std::make_unique<pseudo_random_generator_impl>(),
+      std::make_unique<low_papr_sequence_generator_impl>(),
+      std::make_unique<port_channel_estimator_average_impl>(std::make_unique<interpolator_linear_impl>(),
+                                                            ta_estimator(),
+                                                            port_channel_estimator_fd_smoothing_strategy::filter,
+                                                            port_channel_estimator_td_interpolation_strategy::average,
+                                                            true));
+  auto cpu_demod = std::make_unique<pusch_demodulator_impl>(
+      std::make_unique<channel_equalizer_generic_impl>(channel_equalizer_algorithm_type::zf),
+      nullptr,
+      std::make_unique<demodulation_mapper_impl>(),
+      std::make_unique<evm_calculator_generic_impl>(std::make_unique<modulation_mapper_lut_impl>()),
+      std::make_unique<pseudo_random_generator_impl>(),
+      MAX_RB,
+      true);
+  h->pusch[0] = make_pusch_processor(std::move(cpu_est), std::move(cpu_demod), cpu_pusch_decoder(), 6);
+
+  // GPU signal chain behind the same interfaces; factories dropped right after create() like the reference's.
+  const gpu::pusch_estimator_options est_opts =
+      gpu::make_pusch_estimator_options(port_channel_estimator_fd_smoothing_strategy::filter,
+                                        port_channel_estimator_td_interpolation_strategy::average,
+                                        true);
+  gpu::pusch_demodulator_options demod_opts;
+  for (int mode = 1; mode <= 2; ++mode) {
+    std::unique_ptr<pusch_decoder> dec;
+    if (mode == 1) {
+      dec = cpu_pusch_decoder();
+    } else {
+      std::vector<std::unique_ptr<hal::hw_accelerator_pusch_dec>> accs;
+      accs.push_back(hal::create_hw_accelerator_pusch_dec_factory_gpu(device, max_cb_ids)->create());
+      auto pool = std::make_shared<pusch_decoder_hw_impl::hw_decoder_pool>(std::move(accs));
+      auto crcs = sch_crc<pusch_decoder_hw_impl::sch_crc>();
+      dec       = std::make_unique<pusch_decoder_hw_impl>(std::make_unique<ldpc_segmenter_rx_impl>(), crcs, pool, nullptr);
+    }
+    h->pusch[mode] = make_pusch_processor(create_dmrs_pusch_estimator_factory_gpu(device, est_opts)->create(),
+                                          create_pusch_demodulator_factory_gpu(device, demod_opts)->create(),
+                                          std::move(dec),
+                                          6);
+  }
+  h->pdsch[0] = make_pdsch_processor(cpu_pdsch_encoder(), cpu_pdsch_modulator(), cpu_dmrs_pdsch());
+  {
+    auto seg_crc = sch_crc<ldpc_segmenter_tx_impl::sch_crc>();
+    auto crcs    = sch_crc<pdsch_encoder_hw_impl::sch_crc>();
+    auto enc     = std::make_unique<pdsch_encoder_hw_impl>(
+        crcs,
+        std::make_unique<ldpc_segmenter_tx_impl>(seg_crc),
+        hal::create_hw_accelerator_pdsch_enc_factory_gpu(device)->create());
+    h->pdsch[1] = make_pdsch_processor(std::move(enc),
+                                       create_pdsch_modulator_factory_gpu(device)->create(),
+                                       create_dmrs_pdsch_processor_factory_gpu(device)->create());
+  }
+  h->ofdm_mod_gpu   = create_ofdm_modulator_factory_gpu(device);
+  h->ofdm_demod_gpu = create_ofdm_demodulator_factory_gpu(device);
+  return h;
+}
+
+void chain_destroy(void* p)
+{
+  delete static_cast<chain_harness*>(p);
+}
+
+/// UE transmitter: the TB encoded (reference pdsch_encoder_impl), scrambled, modulated and layer-mapped
+/// (pdsch_modulator_impl, identity precoding: layer l on port l) and the DM-RS of ports 0..L-1 with the PUSCH
+/// DM-RS-to-data amplitude (dmrs_pdsch_processor_impl), into grid_out (L, 14, 12 grid_prb) bf16 pairs. Returns the
+/// number of codeword bits.
+static int chain_ue_tx_impl(void* p, const chain_params* c, const uint8_t* tb, unsigned tb_bytes, uint16_t* grid_out)
+{
+  auto*          h   = static_cast<chain_harness*>(p);
+  const unsigned L   = c->nof_layers;
+  const unsigned nsc = 12 * c->grid_prb;
+  const unsigned G   = nof_data_re(*c) * L * c->qm;
+  resource_grid_impl grid(L, 14, nsc);
+  grid.set_all_zero();
+
+  std::vector<uint8_t> cw(G);
+  pdsch_encoder::configuration ec;
+  ec.base_graph     = c->base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2;
+  ec.rv             = c->rv;
+  ec.mod            = to_mod(c->qm);
+  ec.Nref           = 0;
+  ec.nof_layers     = L;
+  ec.nof_ch_symbols = G / c->qm;
+  h->tx_enc->encode(cw, span<const uint8_t>(tb, tb_bytes), ec);
+  dynamic_bit_buffer packed(G);
+  srsvec::bit_pack(packed, cw);
+
+  pdsch_modulator::config_t mc;
+  mc.rnti                        = static_cast<uint16_t>(c->rnti);
+  mc.bwp_size_rb                 = c->bwp_size;
+  mc.bwp_start_rb                = c->bwp_start;
+  mc.modulation1                 = to_mod(c->qm);
+  mc.modulation2                 = to_mod(c->qm);
+  mc.freq_allocation             = rb_allocation::make_type1(c->rb_start, c->nof_rb);
+  mc.start_symbol_index          = c->start_symbol;
+  mc.nof_symbols                 = c->nof_symbols;
+  mc.dmrs_symb_pos               = symbol_mask(c->dmrs_mask);
+  mc.dmrs_config_type            = c->dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1;
+  mc.nof_cdm_groups_without_data = c->cdm_groups;
+  mc.n_id                        = c->n_id;
+  mc.scaling                     = 1.0F;
+  mc.precoding                   = identity(L, L);
+  const bit_buffer cws[1]        = {packed};
+  h->tx_mod->modulate(grid.get_writer(), span<const bit_buffer>(cws, 1), mc);
+
+  dmrs_pdsch_processor::config_t dc;
+  dc.slot                 = slot_point(subcarrier_spacing::kHz30, static_cast<unsigned>(c->slot));
+  dc.reference_point_k_rb = 0;
+  dc.type                 = c->dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1;
+  dc.scrambling_id        = c->scrambling_id;
+  dc.n_scid               = c->n_scid != 0;
+  dc.amplitude            = convert_dB_to_amplitude(-get_sch_to_dmrs_ratio_dB(c->cdm_groups));
+  dc.symbols_mask         = symbol_mask(c->dmrs_mask);
+  dc.rb_mask              = rb_allocation::make_type1(c->rb_start, c->nof_rb).get_crb_mask(c->bwp_start, c->bwp_size);
+  dc.precoding            = identity(L, L);
+  h->tx_dmrs->map(grid.get_writer(), dc);
+  store_grid(grid, grid_out, L, nsc);
+  return static_cast<int>(G);
+}
+
+/// pusch_processor_impl::process in mode 0 / 1 / 2 on the received grid (nof_ports, 14, 12 grid_prb) bf16 pairs.
+/// out[]: 0 SCH notified, 1 TB CRC ok, 2 codeblocks, 3 LDPC observations, 4 min / 5 max / 6 mean iterations,
+/// 7 SINR dB, 8 EVM, 9 TA (s), 10 CFO (Hz), 11 EPRE dB, 12 RSRP dB (NaN when absent), 13 UCI notified,
+/// 14 HARQ-ACK status, 15 HARQ-ACK bits (bit i = payload[i]), 16 CSI Part 1 status, 17 CSI Part 1 bits.
+static int chain_pusch_process_impl(void* p, int mode, const chain_params* c, const uint16_t* grid_in, uint8_t* tb,
+                        unsigned tb_bytes, double* out)
+{
+  auto*          h   = static_cast<chain_harness*>(p);
+  const unsigned P   = c->nof_ports;
+  const unsigned nsc = 12 * c->grid_prb;
+  resource_grid_impl grid(P, 14, nsc);
+  load_grid(grid, grid_in, P, nsc);
+
+  pusch_processor::pdu_t pdu;
+  pdu.slot                  = slot_point(subcarrier_spacing::kHz30, static_cast<unsigned>(c->slot));
+  pdu.rnti                  = static_cast<uint16_t>(c->rnti);
+  pdu.bwp_size_rb           = c->bwp_size;
+  pdu.bwp_start_rb          = c->bwp_start;
+  pdu.cp                    = cyclic_prefix::NORMAL;
+  pdu.mcs_descr             = {to_mod(c->qm), c->target_code_rate};
+  pdu.codeword              = pusch_processor::codeword_description{
+      static_cast<unsigned>(c->rv), c->base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2,
+      c->new_data != 0};
+  pdu.uci.nof_harq_ack          = c->nof_harq_ack;
+  pdu.uci.nof_csi_part1         = c->nof_csi_part1;
+  pdu.uci.alpha_scaling         = 1.0F;
+  pdu.uci.beta_offset_harq_ack  = 20.0F;
+  pdu.uci.beta_offset_csi_part1 = 6.25F;
+  pdu.uci.beta_offset_csi_part2 = 6.25F;
+  pdu.n_id                      = c->n_id;
+  pdu.nof_tx_layers             = c->nof_layers;
+  for (unsigned i = 0; i != P; ++i) {
+    pdu.rx_ports.push_back(static_cast<uint8_t>(i));
+  }
+  pdu.dmrs_symbol_mask   = symbol_mask(c->dmrs_mask);
+  pdu.dmrs               = pusch_processor::dmrs_configuration{c->dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1,
+                                                 static_cast<unsigned>(c->scrambling_id),
+                                                 c->n_scid != 0,
+                                                 static_cast<unsigned>(c->cdm_groups)};
+  pdu.freq_alloc         = rb_allocation::make_type1(c->rb_start, c->nof_rb);
+  pdu.start_symbol_index = c->start_symbol;
+  pdu.nof_symbols        = c->nof_symbols;
+  pdu.tbs_lbrm           = units::bytes(static_cast<unsigned>(c->tbs_lbrm_bytes));
+  if (c->dc_position >= 0) {
+    pdu.dc_position = static_cast<unsigned>(c->dc_position);
+  }
+
+  auto key = std::make_pair(mode == 0 ? 0 : mode, c->harq_id);
+  const unsigned nof_cbs =
+      ldpc::compute_nof_codeblocks(units::bytes(tb_bytes).to_bits(),
+                                   c->base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2);
+  auto it = h->rx.find(key);
+  if (it == h->rx.end() || it->second->get_nof_codeblocks() != nof_cbs) {
+    h->rx[key] = std::make_unique<test_rx_buffer>(nof_cbs, static_cast<unsigned>(c->harq_id) * CB_IDS_PER_HARQ);
+  }
+  result_capture notifier;
+  h->pusch[mode]->process(span<uint8_t>(tb, tb_bytes), unique_rx_buffer(*h->rx[key]), notifier, grid.get_reader(), pdu);
+
+  for (int i = 0; i != 18; ++i) {
+    out[i] = std::nan("");
+  }
+  out[0] = notifier.have_sch ? 1 : 0;
+  out[13] = notifier.have_uci ? 1 : 0;
+  if (notifier.have_sch) {
+    const auto& d = notifier.sch.data;
+    out[1]        = d.tb_crc_ok ? 1 : 0;
+    out[2]        = d.nof_codeblocks_total;
+    out[3]        = d.ldpc_decoder_stats.get_nof_observations();
+    if (d.ldpc_decoder_stats.get_nof_observations() != 0) {
+      out[4] = d.ldpc_decoder_stats.get_min();
+      out[5] = d.ldpc_decoder_stats.get_max();
+      out[6] = d.ldpc_decoder_stats.get_mean();
+    }
+    const channel_state_information& csi = notifier.sch.csi;
+    auto opt = [](std::optional<float> v) { return v.has_value() ? static_cast<double>(*v) : std::nan(""); };
+    out[7]   = opt(csi.get_sinr_dB());
+    out[8]   = opt(csi.get_total_evm());
+    out[9]   = csi.get_time_alignment().has_value() ? csi.get_time_alignment()->to_seconds() : std::nan("");
+    out[10]  = opt(csi.get_cfo_Hz());
+    out[11]  = opt(csi.get_epre_dB());
+    out[12]  = opt(csi.get_rsrp_dB());
+  }
+  if (notifier.have_uci) {
+    auto bits = [](const pusch_uci_field& f) {
+      double v = 0;
+      for (unsigned i = 0; i != f.payload.size(); ++i) {
+        v += f.payload.test(i) ? std::ldexp(1.0, static_cast<int>(i)) : 0.0;
+      }
+      return v;
+    };
+    out[14] = static_cast<double>(notifier.uci.harq_ack.status);
+    out[15] = bits(notifier.uci.harq_ack);
+    out[16] = static_cast<double>(notifier.uci.csi_part1.status);
+    out[17] = bits(notifier.uci.csi_part1);
+  }
+  return 0;
+}
+
+/// pdsch_processor_impl::process in mode 0 (CPU) / 1 (GPU) of one TB (nof_layers layers on nof_ports ports, precoding
+/// `weights` [port][layer] complex float, one PRG) into grid_inout (nof_ports, 14, 12 grid_prb) bf16 pairs: the grid
+/// keeps whatever it holds outside the PDSCH's REs.
+static int chain_pdsch_process_impl(void* p, int mode, const chain_params* c, const float* weights, const uint8_t* tb,
+                        unsigned tb_bytes, uint16_t* grid_inout)
+{
+  auto*          h   = static_cast<chain_harness*>(p);
+  const unsigned P   = c->nof_ports;
+  const unsigned L   = c->nof_layers;
+  const unsigned nsc = 12 * c->grid_prb;
+  resource_grid_impl grid(P, 14, nsc);
+  load_grid(grid, grid_inout, P, nsc);
+
+  pdsch_processor::pdu_t pdu;
+  pdu.slot         = slot_point(subcarrier_spacing::kHz30, static_cast<unsigned>(c->slot));
+  pdu.rnti         = static_cast<uint16_t>(c->rnti);
+  pdu.bwp_size_rb  = c->bwp_size;
+  pdu.bwp_start_rb = c->bwp_start;
+  pdu.cp           = cyclic_prefix::NORMAL;
+  pdu.codewords.push_back({to_mod(c->qm), static_cast<unsigned>(c->rv)});
+  pdu.n_id                        = c->n_id;
+  pdu.ref_point                   = pdsch_processor::pdu_t::CRB0;
+  pdu.dmrs_symbol_mask            = symbol_mask(c->dmrs_mask);
+  pdu.dmrs                        = c->dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1;
+  pdu.scrambling_id               = c->scrambling_id;
+  pdu.n_scid                      = c->n_scid != 0;
+  pdu.nof_cdm_groups_without_data = c->cdm_groups;
+  pdu.freq_alloc                  = rb_allocation::make_type1(c->rb_start, c->nof_rb);
+  pdu.start_symbol_index          = c->start_symbol;
+  pdu.nof_symbols                 = c->nof_symbols;
+  pdu.ldpc_base_graph             = c->base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2;
+  pdu.tbs_lbrm                    = units::bytes(static_cast<unsigned>(c->tbs_lbrm_bytes));
+  pdu.ratio_pdsch_dmrs_to_sss_dB  = get_sch_to_dmrs_ratio_dB(c->cdm_groups);
+  pdu.ratio_pdsch_data_to_sss_dB  = 0.0F;
+  pdu.precoding                   = precoding_configuration(L, P, 1, MAX_NOF_PRBS);
+  for (unsigned port = 0; port != P; ++port) {
+    for (unsigned l = 0; l != L; ++l) {
+      pdu.precoding.set_coefficient(cf_t(weights[2 * (port * L + l)], weights[2 * (port * L + l) + 1]), l, port, 0);
+    }
+  }
+  static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data;
+  data.emplace_back(span<const uint8_t>(tb, tb_bytes));
+  pdsch_done done;
+  h->pdsch[mode]->process(grid.get_writer(), done, std::move(data), pdu);
+  store_grid(grid, grid_inout, P, nsc);
+  return done.done ? 0 : -1;
+}
+
+/// ofdm_slot_modulator of one port: mode 0 the reference (generic DFT), 1 the GPU binding. Returns the slot size.
+static int chain_ofdm_modulate_impl(void* p, int mode, unsigned numerology, unsigned bw_rb, unsigned dft_size, float scale,
+                        double center_freq_hz, unsigned slot, const uint16_t* grid_port, float* out, unsigned cap)
+{
+  auto*                        h = static_cast<chain_harness*>(p);
+  ofdm_modulator_configuration cfg{numerology, bw_rb, dft_size, cyclic_prefix::NORMAL, scale, center_freq_hz};
+  std::unique_ptr<ofdm_slot_modulator> m;
+  if (mode == 0) {
+    ofdm_modulator_common_configuration common;
+    common.dft = std::make_unique<dft_processor_generic_impl>(
+        dft_processor::configuration{dft_size, dft_processor::direction::INVERSE});
+    m = std::make_unique<ofdm_slot_modulator_impl>(common, cfg);
+  } else {
+    m = h->ofdm_mod_gpu->create_ofdm_slot_modulator(cfg);
+  }
+  resource_grid_impl grid(1, 14, 12 * bw_rb);
+  load_grid(grid, grid_port, 1, 12 * bw_rb);
+  const unsigned n = m->get_slot_size(slot);
+  if (n > cap) {
+    return -1;
+  }
+  m->modulate(span<cf_t>(reinterpret_cast<cf_t*>(out), n), grid.get_reader(), 0, slot);
+  return static_cast<int>(n);
+}
+
+/// ofdm_slot_demodulator of one port (mode 0 reference, 1 GPU) into grid_port (1, 14, 12 bw_rb) bf16 pairs.
+static int chain_ofdm_demodulate_impl(void* p, int mode, unsigned numerology, unsigned bw_rb, unsigned dft_size, float scale,
+                          double center_freq_hz, unsigned window_offset, unsigned slot, const float* in, unsigned n,
+                          uint16_t* grid_port)
+{
+  auto*                          h = static_cast<chain_harness*>(p);
+  ofdm_demodulator_configuration cfg{
+      numerology, bw_rb, dft_size, cyclic_prefix::NORMAL, window_offset, scale, center_freq_hz};
+  std::unique_ptr<ofdm_slot_demodulator> d;
+  if (mode == 0) {
+    ofdm_demodulator_common_configuration common;
+    common.dft = std::make_unique<dft_processor_generic_impl>(
+        dft_processor::configuration{dft_size, dft_processor::direction::DIRECT});
+    d = std::make_unique<ofdm_slot_demodulator_impl>(common, cfg);
+  } else {
+    d = h->ofdm_demod_gpu->create_ofdm_slot_demodulator(cfg);
+  }
+  if (d->get_slot_size(slot) != n) {
+    return -1;
+  }
+  resource_grid_impl grid(1, 14, 12 * bw_rb);
+  grid.set_all_zero();
+  d->demodulate(grid.get_writer(), span<const cf_t>(reinterpret_cast<const cf_t*>(in), n), 0, slot);
+  store_grid(grid, grid_port, 1, 12 * bw_rb);
+  return 0;
+}
+
+void* chain_create(int device, unsigned max_cb_ids)
+{
+  void* h = nullptr;
+  guarded("chain_create", [&] {
+    h = chain_create_impl(device, max_cb_ids);
+    return 0;
+  });
+  return h;
+}
+
+int chain_ue_tx(void* p, const chain_params* c, const uint8_t* tb, unsigned tb_bytes, uint16_t* grid_out)
+{
+  return guarded("chain_ue_tx", [&] { return chain_ue_tx_impl(p, c, tb, tb_bytes, grid_out); });
+}
+
+int chain_pusch_process(void* p, int mode, const chain_params* c, const uint16_t* grid_in, uint8_t* tb,
+                        unsigned tb_bytes, double* out)
+{
+  return guarded("chain_pusch_process", [&] { return chain_pusch_process_impl(p, mode, c, grid_in, tb, tb_bytes, out); });
+}
+
+int chain_pdsch_process(void* p, int mode, const chain_params* c, const float* weights, const uint8_t* tb,
+                        unsigned tb_bytes, uint16_t* grid_inout)
+{
+  return guarded("chain_pdsch_process",
+                 [&] { return chain_pdsch_process_impl(p, mode, c, weights, tb, tb_bytes, grid_inout); });
+}
+
+int chain_ofdm_modulate(void* p, int mode, unsigned numerology, unsigned bw_rb, unsigned dft_size, float scale,
+                        double center_freq_hz, unsigned slot, const uint16_t* grid_port, float* out, unsigned cap)
+{
+  return guarded("chain_ofdm_modulate", [&] {
+    return chain_ofdm_modulate_impl(p, mode, numerology, bw_rb, dft_size, scale, center_freq_hz, slot, grid_port, out,
+                                    cap);
+  });
+}
+
+int chain_ofdm_demodulate(void* p, int mode, unsigned numerology, unsigned bw_rb, unsigned dft_size, float scale,
+                          double center_freq_hz, unsigned window_offset, unsigned slot, const float* in, unsigned n,
+                          uint16_t* grid_port)
+{
+  return guarded("chain_ofdm_demodulate", [&] {
+    return chain_ofdm_demodulate_impl(
+        p, mode, numerology, bw_rb, dft_size, scale, center_freq_hz, window_offset, slot, in, n, grid_port);
+  });
+}
+
+} // extern "C"

@@ -24,6 +24,7 @@ struct srsgpu_pusch_demodulator_plan {
   int                   nof_tp_jobs = 0;
   int                   nof_tx     = 0;
   std::vector<uint32_t> nof_llrs;
+  std::vector<uint32_t> seq_off;  ///< First sequence word of each transmission in d_seq.
 };
 
 namespace {
@@ -280,6 +281,7 @@ int srsgpu_pusch_demodulator_plan_create_ex(srsgpu_context*                  ctx
   plan->nof_tp_jobs = static_cast<int>(tp_jobs.size());
   plan->nof_tx      = static_cast<int>(nof_tx);
   plan->nof_llrs    = std::move(nllr);
+  plan->seq_off     = seq_off;
   const bool work   = !chunks.empty() || !tp_jobs.empty();
   if (work && build_gold_sequences(ctx, c_inits, nwords, seq_off, &plan->d_seq) != SRSGPU_OK) {
     srsgpu_pusch_demodulator_plan_destroy(plan);
@@ -380,3 +382,20 @@ void srsgpu_pusch_demodulator_plan_destroy(srsgpu_pusch_demodulator_plan* plan)
 }
 
 } // extern "C"
+
+extern "C" int srsgpu_pusch_demodulator_plan_scrambling(const srsgpu_pusch_demodulator_plan* plan,
+                                                        uint32_t                             tx,
+                                                        uint32_t*                            d_words,
+                                                        void*                                stream)
+{
+  if (plan == nullptr || d_words == nullptr || tx >= static_cast<uint32_t>(plan->nof_tx)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument or transmission index out of range");
+  }
+  const size_t nwords = (plan->nof_llrs[tx] + 31u) / 32u;
+  if (nwords == 0) {
+    return SRSGPU_OK;
+  }
+  HIP_TRY(hipMemcpyAsync(d_words, plan->d_seq + plan->seq_off[tx], nwords * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                         static_cast<hipStream_t>(stream)));
+  return SRSGPU_OK;
+}

@@ -401,7 +401,7 @@ def load_library(path: str = LIB_PATH):
 
 # Every symbol include/srsgpu_phy.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = [
-    "srsgpu_version", "srsgpu_last_error", "srsgpu_context_create", "srsgpu_context_destroy", "srsgpu_context_device",
+    "srsgpu_version", "srsgpu_last_error", "srsgpu_context_create", "srsgpu_context_destroy", "srsgpu_context_device", "srsgpu_pusch_demodulator_plan_scrambling",
     "srsgpu_ldpc_decoder_plan_create", "srsgpu_ldpc_decoder_plan_execute", "srsgpu_ldpc_decoder_plan_destroy",
     "srsgpu_ldpc_decode", "srsgpu_pusch_cb_plan_create", "srsgpu_pusch_cb_plan_execute",
     "srsgpu_pusch_cb_plan_destroy", "srsgpu_pdsch_encoder_plan_create", "srsgpu_pdsch_encoder_plan_nof_codeblocks",

@@ -1,0 +1,110 @@
+"""ctypes wrapper of oracle/_ref/libsrschain.so (oracle/build_chain.sh, oracle/ref/ref_chain.cpp): the reference's own
+pusch_processor_impl / pdsch_processor_impl built twice, from the reference's CPU components and with the GPU
+signal-chain bindings of integration/, plus the OFDM slot transforms both ways. TEST INFRASTRUCTURE ONLY."""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHAIN_SO = os.path.join(ROOT, "oracle", "_ref", "libsrschain.so")
+
+PUSCH_CPU, PUSCH_GPU_CHAIN, PUSCH_GPU_CHAIN_HW_DEC = 0, 1, 2
+PDSCH_CPU, PDSCH_GPU = 0, 1
+_P = ctypes.c_void_p
+
+
+class ChainParams(ctypes.Structure):
+    """chain_params of oracle/ref/ref_chain.cpp."""
+    _fields_ = [(n, ctypes.c_int32) for n in ("slot", "rnti", "n_id", "qm")] + [("target_code_rate", ctypes.c_float)] + \
+        [(n, ctypes.c_int32) for n in ("rv", "base_graph", "new_data", "harq_id", "nof_layers", "nof_ports",
+                                       "dmrs_mask", "dmrs_type2", "scrambling_id", "n_scid", "cdm_groups", "rb_start",
+                                       "nof_rb", "bwp_start", "bwp_size", "start_symbol", "nof_symbols",
+                                       "nof_harq_ack", "nof_csi_part1", "dc_position", "tbs_lbrm_bytes", "grid_prb",
+                                       "max_iterations")]
+
+
+def params(**kw):
+    d = dict(slot=7, rnti=0x4601, n_id=500, qm=8, target_code_rate=948.0, rv=0, base_graph=1, new_data=1, harq_id=0,
+             nof_layers=1, nof_ports=4, dmrs_mask=(1 << 2) | (1 << 11), dmrs_type2=0, scrambling_id=500, n_scid=0,
+             cdm_groups=2, rb_start=0, nof_rb=25, bwp_start=0, bwp_size=273, start_symbol=0, nof_symbols=14,
+             nof_harq_ack=0, nof_csi_part1=0, dc_position=-1, tbs_lbrm_bytes=200000, grid_prb=273, max_iterations=6)
+    d.update(kw)
+    return ChainParams(**d)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_P)
+
+
+PUSCH_OUT = ("sch", "tb_crc_ok", "nof_cbs", "ldpc_obs", "ldpc_min", "ldpc_max", "ldpc_mean", "sinr_db", "evm", "ta_s",
+             "cfo_hz", "epre_db", "rsrp_db", "uci", "harq_ack_status", "harq_ack_bits", "csi1_status", "csi1_bits")
+
+
+class Chain:
+    def __init__(self, device=0, max_cb_ids=128 * 160, path=CHAIN_SO):
+        self.lib = ctypes.CDLL(path)
+        L = self.lib
+        L.chain_create.restype = _P
+        L.chain_create.argtypes = [ctypes.c_int, ctypes.c_uint]
+        L.chain_destroy.argtypes = [_P]
+        PP = ctypes.POINTER(ChainParams)
+        L.chain_ue_tx.restype = ctypes.c_int
+        L.chain_ue_tx.argtypes = [_P, PP, _P, ctypes.c_uint, _P]
+        L.chain_pusch_process.restype = ctypes.c_int
+        L.chain_pusch_process.argtypes = [_P, ctypes.c_int, PP, _P, _P, ctypes.c_uint, _P]
+        L.chain_pdsch_process.restype = ctypes.c_int
+        L.chain_pdsch_process.argtypes = [_P, ctypes.c_int, PP, _P, _P, ctypes.c_uint, _P]
+        L.chain_ofdm_modulate.restype = ctypes.c_int
+        L.chain_ofdm_modulate.argtypes = [_P, ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint,
+                                          ctypes.c_float, ctypes.c_double, ctypes.c_uint, _P, _P, ctypes.c_uint]
+        L.chain_ofdm_demodulate.restype = ctypes.c_int
+        L.chain_ofdm_demodulate.argtypes = [_P, ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint,
+                                            ctypes.c_float, ctypes.c_double, ctypes.c_uint, ctypes.c_uint, _P,
+                                            ctypes.c_uint, _P]
+        self.h = L.chain_create(device, max_cb_ids)
+
+    def close(self):
+        if self.h:
+            self.lib.chain_destroy(self.h)
+            self.h = None
+
+    def ue_tx(self, p, tb):
+        """The UE's transmitted grid (nof_layers, 14, 12 grid_prb, 2) bf16 bit patterns."""
+        tb = np.ascontiguousarray(tb, np.uint8)
+        g = np.zeros((p.nof_layers, 14, 12 * p.grid_prb, 2), np.uint16)
+        assert self.lib.chain_ue_tx(self.h, ctypes.byref(p), _ptr(tb), tb.size, _ptr(g)) > 0
+        return g
+
+    def pusch(self, mode, p, grid, tb_bytes):
+        """pusch_processor_impl::process: (TB bytes, result dict of PUSCH_OUT)."""
+        g = np.ascontiguousarray(grid, np.uint16)
+        tb = np.zeros(tb_bytes, np.uint8)
+        out = np.zeros(len(PUSCH_OUT), np.float64)
+        assert self.lib.chain_pusch_process(self.h, mode, ctypes.byref(p), _ptr(g), _ptr(tb), tb_bytes, _ptr(out)) == 0
+        return tb, dict(zip(PUSCH_OUT, out.tolist()))
+
+    def pdsch(self, mode, p, weights, tb, grid):
+        """pdsch_processor_impl::process into a copy of `grid` (nof_ports, 14, nsc, 2); returns the grid."""
+        w = np.ascontiguousarray(weights, np.complex64).view(np.float32)
+        tb = np.ascontiguousarray(tb, np.uint8)
+        g = np.array(grid, np.uint16, copy=True, order="C")
+        assert self.lib.chain_pdsch_process(self.h, mode, ctypes.byref(p), _ptr(w), _ptr(tb), tb.size, _ptr(g)) == 0
+        return g
+
+    def ofdm_modulate(self, mode, grid_port, numerology, bw_rb, dft_size, scale, center_freq_hz, slot):
+        g = np.ascontiguousarray(grid_port, np.uint16)
+        cap = 2 * 1024 * 1024
+        out = np.zeros(cap, np.complex64)
+        n = self.lib.chain_ofdm_modulate(self.h, mode, numerology, bw_rb, dft_size, scale, center_freq_hz, slot,
+                                         _ptr(g), _ptr(out), cap)
+        assert n > 0
+        return out[:n]
+
+    def ofdm_demodulate(self, mode, samples, numerology, bw_rb, dft_size, scale, center_freq_hz, slot,
+                        window_offset=0):
+        x = np.ascontiguousarray(samples, np.complex64)
+        g = np.zeros((1, 14, 12 * bw_rb, 2), np.uint16)
+        assert self.lib.chain_ofdm_demodulate(self.h, mode, numerology, bw_rb, dft_size, scale, center_freq_hz,
+                                              window_offset, slot, _ptr(x), x.size, _ptr(g)) == 0
+        return g

@@ -11,7 +11,8 @@ REF = "/root/reference"
 
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "include", "srsran")), reason="reference tree absent")
 @pytest.mark.parametrize("src", ["ldpc_decoder_gpu.cpp", "hw_accelerator_pusch_dec_gpu.cpp",
-                                 "hw_accelerator_pdsch_enc_gpu.cpp"])
+                                 "hw_accelerator_pdsch_enc_gpu.cpp", "pusch_chain_gpu.cpp", "pdsch_chain_gpu.cpp",
+                                 "ofdm_gpu.cpp"])
 def test_binding_compiles_against_reference_headers(src, tmp_path):
     cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-fsyntax-only", "-DFMT_HEADER_ONLY",
            f"-I{REF}/include", f"-I{REF}/external/fmt/include", f"-I{REF}/external", f"-I{ROOT}/include",
@@ -28,5 +29,19 @@ def test_hal_harness_links_reference_processors_with_gpu_bindings():
     entry points (no GPU call here; the GPU run is tests/test_hal_gpu.py)."""
     import ctypes
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libsrshal.so"))
-    for sym in ("hal_create", "hal_destroy", "hal_pusch_decode", "hal_pdsch_encode"):
+    for sym in ("hal_create", "hal_destroy", "hal_pusch_decode", "hal_pdsch_encode", "hal_pool_create",
+                "hal_pool_decode", "hal_pool_destroy"):
+        assert hasattr(lib, sym)
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libsrschain.so")),
+                    reason="chain harness not built (oracle/build_chain.sh)")
+def test_chain_harness_links_reference_processors_with_gpu_signal_chain():
+    """oracle/build_chain.sh links the reference's pusch_processor_impl / pdsch_processor_impl (with the reference's
+    UCI decoder, UL-SCH demultiplexer, PT-RS generator) with the signal-chain bindings (-Wl,--no-undefined): the
+    library loads and exports the harness entry points (the GPU run is tests/test_chain_gpu.py)."""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libsrschain.so"))
+    for sym in ("chain_create", "chain_destroy", "chain_ue_tx", "chain_pusch_process", "chain_pdsch_process",
+                "chain_ofdm_modulate", "chain_ofdm_demodulate"):
         assert hasattr(lib, sym)

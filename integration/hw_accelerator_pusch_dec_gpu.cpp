@@ -18,7 +18,9 @@
 // The rx buffer pool keeps one codeblock on one thread at a time (unique_rx_buffer lock) and run() synchronises its
 // stream before the results are read, so consecutive transmissions of a slot are ordered. free_harq_context_entry()
 // (called once the TB CRC passes, :411/:423) releases the slot: a later retransmission into a released slot combines
-// with zeros, the state of a new soft buffer. The arena and the srsgpu context live as long as any accelerator.
+// with zeros, the state of a new soft buffer, as the reference's ext_harq_buffer_context_repository::get() resets a
+// freed entry (ext_harq_buffer_context_repository.h:70-96; its debug mode, which keeps freed entries for HARQ unit
+// tests, is the factory's debug_mode). The arena and the srsgpu context live as long as any accelerator.
 #include "gpu_context.h"
 #include "hw_accelerator_pusch_dec_gpu.h"
 #include <algorithm>
@@ -64,8 +66,8 @@ uint8_t qm_of(modulation_scheme m)
 
 /// The HBM HARQ arena of a factory: one slot per absolute codeblock identifier, shared by its accelerators.
 struct harq_arena {
-  harq_arena(std::shared_ptr<srsgpu_context> ctx_, unsigned max_cb_ids_) :
-    ctx(std::move(ctx_)), max_cb_ids(max_cb_ids_), in_use(max_cb_ids_, 0)
+  harq_arena(std::shared_ptr<srsgpu_context> ctx_, unsigned max_cb_ids_, bool debug_mode_) :
+    ctx(std::move(ctx_)), max_cb_ids(max_cb_ids_), debug_mode(debug_mode_), in_use(max_cb_ids_, 0)
   {
     if (max_cb_ids == 0) {
       throw std::invalid_argument(std::string(WHO) + ": max_cb_ids must be positive");
@@ -94,13 +96,14 @@ struct harq_arena {
   void release(unsigned id)
   {
     std::lock_guard<std::mutex> lock(mtx);
-    if (id < max_cb_ids) {
+    if (id < max_cb_ids && !debug_mode) {
       in_use[id] = 0;
     }
   }
 
   std::shared_ptr<srsgpu_context> ctx;
   unsigned                        max_cb_ids;
+  bool                            debug_mode;
   int8_t*                         d_soft = nullptr;
   std::mutex                      mtx;
   std::vector<uint8_t>            in_use;  ///< 1: the slot holds soft bits of a live HARQ process.
@@ -357,8 +360,8 @@ private:
 class hw_accelerator_pusch_dec_factory_gpu : public hw_accelerator_pusch_dec_factory
 {
 public:
-  hw_accelerator_pusch_dec_factory_gpu(int device, unsigned max_cb_ids) :
-    arena(std::make_shared<harq_arena>(gpu::shared_context(device), max_cb_ids))
+  hw_accelerator_pusch_dec_factory_gpu(int device, unsigned max_cb_ids, bool debug_mode) :
+    arena(std::make_shared<harq_arena>(gpu::shared_context(device), max_cb_ids, debug_mode))
   {
   }
 
@@ -371,10 +374,10 @@ private:
   std::shared_ptr<harq_arena> arena;
 };
 
-std::shared_ptr<hw_accelerator_pusch_dec_factory> create_hw_accelerator_pusch_dec_factory_gpu(int      device,
-                                                                                              unsigned max_cb_ids)
+std::shared_ptr<hw_accelerator_pusch_dec_factory>
+create_hw_accelerator_pusch_dec_factory_gpu(int device, unsigned max_cb_ids, bool debug_mode)
 {
-  return std::make_shared<hw_accelerator_pusch_dec_factory_gpu>(device, max_cb_ids);
+  return std::make_shared<hw_accelerator_pusch_dec_factory_gpu>(device, max_cb_ids, debug_mode);
 }
 
 } // namespace hal

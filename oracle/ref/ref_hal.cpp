@@ -306,7 +306,9 @@ void* hal_create(int device, unsigned max_cb_ids)
 {
   auto* h     = new hal_harness();
   h->gpu_ldpc = create_ldpc_decoder_factory_gpu(device);
-  h->gpu_dec  = hal::create_hw_accelerator_pusch_dec_factory_gpu(device, max_cb_ids);
+  // Debug mode (entries kept after a passing TB CRC): the tests retransmit after success and compare with the CPU
+  // decoder, whose test rx buffer keeps its soft bits.
+  h->gpu_dec  = hal::create_hw_accelerator_pusch_dec_factory_gpu(device, max_cb_ids, true);
   h->gpu_enc  = hal::create_hw_accelerator_pdsch_enc_factory_gpu(device);
   h->dec[0]   = make_sw_decoder(cpu_decoder());
   h->dec[1]   = make_sw_decoder(h->gpu_ldpc->create());

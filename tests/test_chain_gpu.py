@@ -117,23 +117,24 @@ def test_pusch_processor_gpu_chain_equals_reference(chain, mode):
 
 def test_pusch_processor_gpu_chain_harq_retransmission(chain):
     """rv0 too noisy to decode alone, then rv2 (new_data = false) combines with it: the GPU chain with the HW decoder
-    (HARQ in HBM) and with the CPU decoder give the reference's outcomes."""
+    (HARQ in HBM) and with the CPU decoder give the reference's outcomes. (A process whose rv0 decodes is released by
+    the reference, pusch_decoder_hw_impl.cpp:411: its retransmission is not a combining case and is skipped.)"""
     import chain_harness as H
     rng = np.random.default_rng(47)
     outcomes = []
-    for h, snr in enumerate((17.0, 17.5, 18.0)):
-        p0 = H.params(nof_rb=30, rb_start=40, qm=8, target_code_rate=797.0, harq_id=100 + h)
-        seg = ue_grant(p0).segmentation()
-        p0.base_graph = seg.base_graph
+    for h, snr in enumerate((5.0, 5.5, 6.0, 6.5, 7.0, 7.5)):
+        kw = dict(nof_rb=30, rb_start=40, qm=6, target_code_rate=772.0, harq_id=100 + h)
+        seg = ue_grant(H.params(**kw)).segmentation()
         tb = rng.integers(0, 256, seg.tbs // 8).astype(np.uint8)
         for rv, new_data in ((0, 1), (2, 0)):
-            p = H.params(nof_rb=30, rb_start=40, qm=8, target_code_rate=797.0, harq_id=100 + h, rv=rv,
-                         new_data=new_data, base_graph=seg.base_graph)
+            p = H.params(rv=rv, new_data=new_data, base_graph=seg.base_graph, **kw)
             rx = receive(rng, chain.ue_tx(p, tb), 4, snr)
             ref = chain.pusch(H.PUSCH_CPU, p, rx, seg.tbs // 8)
             for mode in (1, 2):
                 check_pusch_equal(ref, chain.pusch(mode, p, rx, seg.tbs // 8), (h, rv, mode))
             outcomes.append((h, rv, ref[1]["tb_crc_ok"]))
+            if ref[1]["tb_crc_ok"]:
+                break
     assert any(ok for (_, rv, ok) in outcomes if rv == 2), outcomes
 
 
@@ -142,10 +143,12 @@ PDSCH_CASES = [
                                            target_code_rate=772.0, nof_layers=1, nof_ports=1, dmrs_mask=1 << 2)),
     ("100 MHz 4 layers 256QAM pos1", dict(nof_rb=273, rb_start=0, qm=8, target_code_rate=948.0, nof_layers=4,
                                           nof_ports=4)),
-    ("2 layers on 4 ports, offset, type 2, 1 CDM group", dict(nof_rb=40, rb_start=17, qm=4, target_code_rate=616.0,
-                                                              nof_layers=2, nof_ports=4, dmrs_type2=1, cdm_groups=1,
-                                                              start_symbol=1, nof_symbols=12,
-                                                              dmrs_mask=(1 << 2) | (1 << 8))),
+    # Type 1 only at the processor level: pdsch_processor_impl::modulate never sets the modulator's dmrs_config_type
+    # (pdsch_processor_impl.cpp:180-196), so a type-2 PDU reaches the modulator as type 1 (reference defect; the GPU
+    # modulator's type-2 mapping is pinned at component level, tests/test_pdsch_modulator_gpu.py).
+    ("2 layers on 4 ports, offset, 1 CDM group (data on DM-RS symbols)",
+     dict(nof_rb=40, rb_start=17, qm=4, target_code_rate=616.0, nof_layers=2, nof_ports=4, cdm_groups=1,
+          start_symbol=1, nof_symbols=12, dmrs_mask=(1 << 2) | (1 << 8))),
     ("special slot: 8 symbols DM-RS 2+7", dict(nof_rb=273, rb_start=0, qm=8, target_code_rate=948.0, nof_layers=4,
                                                nof_ports=4, nof_symbols=8, dmrs_mask=(1 << 2) | (1 << 7))),
 ]
@@ -185,5 +188,8 @@ def test_ofdm_bindings_equal_reference(chain, slot):
     assert np.max(np.abs(a - b)) < 2e-5 * rms, np.max(np.abs(a - b)) / rms
     ga = chain.ofdm_demodulate(0, a, 1, bw, N, 1.0 / (N / 64), 3.5e9, slot, window_offset=72)
     gb = chain.ofdm_demodulate(1, a, 1, bw, N, 1.0 / (N / 64), 3.5e9, slot, window_offset=72)
-    va, vb = ga.astype(np.int32), gb.astype(np.int32)
-    assert np.max(np.abs(va - vb)) <= 1, np.max(np.abs(va - vb))
+    # Within one bf16 ulp (2^-7 relative) or 1e-4 x RMS absolute (tests/test_ofdm_gpu.py's tolerance).
+    va, vb = bf16_to_complex(ga), bf16_to_complex(gb)
+    ref_rms = np.sqrt(np.mean(np.abs(va) ** 2))
+    err = np.abs(va - vb)
+    assert np.all(err <= np.maximum(2.0 ** -7 * np.abs(va), 1e-4 * ref_rms)), float(np.max(err / ref_rms))

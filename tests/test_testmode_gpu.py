@@ -103,3 +103,45 @@ def test_testmode_continuous_periods_with_fresh_payloads(ctx):
         ok = ul.d_tb_ok.cpu().numpy()
         assert ok.all(), (step, np.nonzero(ok == 0)[0])
         assert torch.equal(ul.d_tbs, sent)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["full", "special"])
+def test_testmode_dl_max_tbs_codeword_and_grid_vs_oracle(ctx, which):
+    """configs[4]'s DL at its real size against the oracle: the 1 179 864-bit max-TBS TB of a full DL slot (4 layers,
+    DM-RS 2 + 11; 140 codeblocks) and the 590 128-bit TB of the special slot's 8-symbol PDSCH (DM-RS 2 + 7), each
+    encoded by the GPU PDSCH encoder (bit-exact vs the oracle's TB CRC -> segmentation -> CB CRC -> LDPC -> rate
+    matching) and mapped with its DM-RS into the slot's 4-port grid (bit-exact vs the oracle modulator + DM-RS
+    restatements, both pinned against the reference)."""
+    import torch
+    import pdsch_dmrs_oracle as M
+    from chain_lib import oracle_pdsch_encode
+    from oracle_lib import Oracle
+    from srsgpu import slot as slotlib
+    orc = Oracle()
+    dl_cell, sp_cell, _ = slotlib.tdd_testmode_cells(1)
+    cell = dl_cell if which == "full" else sp_cell
+    pipe = slotlib.DownlinkPipeline(ctx, cell)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(7)
+    d_tbs = torch.randint(0, 256, (pipe.tb_total,), generator=gen, device="cuda", dtype=torch.uint8)
+    pipe.execute(d_tbs, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    u, seg = cell.ues[0], cell.segs[0]
+    tb = d_tbs[: seg.tbs // 8].cpu().numpy()
+    want_cw, _, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, 0, u.qm, u.nof_layers, 0, u.nof_ch_symbols)
+    cw_bytes = pipe.d_cw.cpu().numpy()
+    got_cw = np.unpackbits(cw_bytes[pipe.cw_offsets[0]: pipe.cw_offsets[0] + (seg.cw_length + 7) // 8])[: seg.cw_length]
+    assert np.array_equal(got_cw, want_cw)
+    # Slot 0 grid: the oracle modulator (identity precoding, 4 layers on 4 ports) over the DM-RS oracle's grid.
+    w = np.eye(4, dtype=np.complex64)
+    dm = dict(slot=cell.slot_index(0), scrambling_id=500, n_scid=0, dmrs_type2=0, nof_layers=4, nof_ports=4,
+              dmrs_symbol_mask=cell.dmrs_mask, reference_point_k_rb=0, rb_start=0, nof_rb=273,
+              amplitude=slotlib.DMRS_BETA)
+    want = M.dmrs_map(dm, w, 273)
+    mod = dict(rnti=0x4601, n_id=500, qm=u.qm, nof_layers=4, nof_ports=4, bwp_start_rb=0, bwp_size_rb=273, rb_start=0,
+               nof_rb=273, start_symbol=0, nof_symbols=cell.nof_symbols, dmrs_symbol_mask=cell.dmrs_mask,
+               dmrs_type2=0, nof_cdm_groups_without_data=2, scaling=1.0)
+    want = orc.pdsch_modulate(mod, w, np.packbits(want_cw), seg.cw_length, 273, grid=want)
+    got = pipe.d_grid.cpu().numpy().view(np.uint16).reshape(cell.nof_slots, 4, 14, 12 * 273, 2)[0]
+    assert np.array_equal(got, want)

@@ -68,7 +68,13 @@
 #include <cstdio>
 #include <exception>
 #include <cstring>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <map>
+#include <mutex>
+#include <random>
+#include <thread>
 #include <memory>
 #include <vector>
 
@@ -299,6 +305,198 @@ std::unique_ptr<pdsch_processor> make_pdsch_processor(std::unique_ptr<pdsch_enco
                                                           cpu_mapper()));
 }
 
+/// A PUSCH processor of mode 0 (reference CPU components), 1 (GPU estimator + demodulator, reference CPU decoder) or
+/// 2 (GPU estimator + demodulator, pusch_decoder_hw_impl over `hw_pool`'s GPU accelerators). Estimator: filter
+/// smoothing, CFO compensation and the given time strategy; ZF with post-equalisation SINR; EVM when `evm`.
+std::unique_ptr<pusch_processor> new_pusch_processor(int                                                     device,
+                                                     int                                                     mode,
+                                                     port_channel_estimator_td_interpolation_strategy        td,
+                                                     unsigned                                                max_iter,
+                                                     bool                                                    evm,
+                                                     const std::shared_ptr<pusch_decoder_hw_impl::hw_decoder_pool>& hw_pool)
+{
+  if (mode == 0) {
+    auto est = std::make_unique<dmrs_pusch_estimator_impl>(
+        std::make_unique<pseudo_random_generator_impl>(),
+        std::make_unique<low_papr_sequence_generator_impl>(),
+        std::make_unique<port_channel_estimator_average_impl>(std::make_unique<interpolator_linear_impl>(),
+                                                              ta_estimator(),
+                                                              port_channel_estimator_fd_smoothing_strategy::filter,
+                                                              td,
+                                                              true));
+    auto demod = std::make_unique<pusch_demodulator_impl>(
+        std::make_unique<channel_equalizer_generic_impl>(channel_equalizer_algorithm_type::zf),
+        nullptr,
+        std::make_unique<demodulation_mapper_impl>(),
+        evm ? std::make_unique<evm_calculator_generic_impl>(std::make_unique<modulation_mapper_lut_impl>()) : nullptr,
+        std::make_unique<pseudo_random_generator_impl>(),
+        MAX_RB,
+        true);
+    return make_pusch_processor(std::move(est), std::move(demod), cpu_pusch_decoder(), max_iter);
+  }
+  // GPU signal chain behind the same interfaces; factories dropped right after create() like the reference's.
+  const gpu::pusch_estimator_options est_opts =
+      gpu::make_pusch_estimator_options(port_channel_estimator_fd_smoothing_strategy::filter, td, true);
+  gpu::pusch_demodulator_options demod_opts;
+  demod_opts.enable_evm = evm;
+  std::unique_ptr<pusch_decoder> dec;
+  if (mode == 1) {
+    dec = cpu_pusch_decoder();
+  } else {
+    auto crcs = sch_crc<pusch_decoder_hw_impl::sch_crc>();
+    dec       = std::make_unique<pusch_decoder_hw_impl>(std::make_unique<ldpc_segmenter_rx_impl>(), crcs, hw_pool, nullptr);
+  }
+  return make_pusch_processor(create_dmrs_pusch_estimator_factory_gpu(device, est_opts)->create(),
+                              create_pusch_demodulator_factory_gpu(device, demod_opts)->create(),
+                              std::move(dec),
+                              max_iter);
+}
+
+/// A PDSCH processor of mode 0 (reference CPU components) or 1 (pdsch_encoder_hw_impl over the GPU accelerator, GPU
+/// modulator, GPU DM-RS).
+std::unique_ptr<pdsch_processor> new_pdsch_processor(int device, int mode)
+{
+  if (mode == 0) {
+    return make_pdsch_processor(cpu_pdsch_encoder(), cpu_pdsch_modulator(), cpu_dmrs_pdsch());
+  }
+  auto seg_crc = sch_crc<ldpc_segmenter_tx_impl::sch_crc>();
+  auto crcs    = sch_crc<pdsch_encoder_hw_impl::sch_crc>();
+  auto enc     = std::make_unique<pdsch_encoder_hw_impl>(
+      crcs, std::make_unique<ldpc_segmenter_tx_impl>(seg_crc), hal::create_hw_accelerator_pdsch_enc_factory_gpu(device)->create());
+  return make_pdsch_processor(
+      std::move(enc), create_pdsch_modulator_factory_gpu(device)->create(), create_dmrs_pdsch_processor_factory_gpu(device)->create());
+}
+
+pusch_processor::pdu_t make_pusch_pdu(const chain_params& cc)
+{
+  const chain_params* c = &cc;
+  const unsigned      P = c->nof_ports;
+  pusch_processor::pdu_t pdu;
+  pdu.slot                  = slot_point(subcarrier_spacing::kHz30, static_cast<unsigned>(c->slot));
+  pdu.rnti                  = static_cast<uint16_t>(c->rnti);
+  pdu.bwp_size_rb           = c->bwp_size;
+  pdu.bwp_start_rb          = c->bwp_start;
+  pdu.cp                    = cyclic_prefix::NORMAL;
+  pdu.mcs_descr             = {to_mod(c->qm), c->target_code_rate};
+  pdu.codeword              = pusch_processor::codeword_description{
+      static_cast<unsigned>(c->rv), c->base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2,
+      c->new_data != 0};
+  pdu.uci.nof_harq_ack          = c->nof_harq_ack;
+  pdu.uci.nof_csi_part1         = c->nof_csi_part1;
+  pdu.uci.alpha_scaling         = 1.0F;
+  pdu.uci.beta_offset_harq_ack  = 20.0F;
+  pdu.uci.beta_offset_csi_part1 = 6.25F;
+  pdu.uci.beta_offset_csi_part2 = 6.25F;
+  pdu.n_id                      = c->n_id;
+  pdu.nof_tx_layers             = c->nof_layers;
+  for (unsigned i = 0; i != P; ++i) {
+    pdu.rx_ports.push_back(static_cast<uint8_t>(i));
+  }
+  pdu.dmrs_symbol_mask   = symbol_mask(c->dmrs_mask);
+  pdu.dmrs               = pusch_processor::dmrs_configuration{c->dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1,
+                                                 static_cast<unsigned>(c->scrambling_id),
+                                                 c->n_scid != 0,
+                                                 static_cast<unsigned>(c->cdm_groups)};
+  pdu.freq_alloc         = rb_allocation::make_type1(c->rb_start, c->nof_rb);
+  pdu.start_symbol_index = c->start_symbol;
+  pdu.nof_symbols        = c->nof_symbols;
+  pdu.tbs_lbrm           = units::bytes(static_cast<unsigned>(c->tbs_lbrm_bytes));
+  if (c->dc_position >= 0) {
+    pdu.dc_position = static_cast<unsigned>(c->dc_position);
+  }
+
+  return pdu;
+}
+
+pdsch_processor::pdu_t make_pdsch_pdu(const chain_params& cc, const float* weights)
+{
+  const chain_params* c = &cc;
+  const unsigned      P = c->nof_ports;
+  const unsigned      L = c->nof_layers;
+  pdsch_processor::pdu_t pdu;
+  pdu.slot         = slot_point(subcarrier_spacing::kHz30, static_cast<unsigned>(c->slot));
+  pdu.rnti         = static_cast<uint16_t>(c->rnti);
+  pdu.bwp_size_rb  = c->bwp_size;
+  pdu.bwp_start_rb = c->bwp_start;
+  pdu.cp           = cyclic_prefix::NORMAL;
+  pdu.codewords.push_back({to_mod(c->qm), static_cast<unsigned>(c->rv)});
+  pdu.n_id                        = c->n_id;
+  pdu.ref_point                   = pdsch_processor::pdu_t::CRB0;
+  pdu.dmrs_symbol_mask            = symbol_mask(c->dmrs_mask);
+  pdu.dmrs                        = c->dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1;
+  pdu.scrambling_id               = c->scrambling_id;
+  pdu.n_scid                      = c->n_scid != 0;
+  pdu.nof_cdm_groups_without_data = c->cdm_groups;
+  pdu.freq_alloc                  = rb_allocation::make_type1(c->rb_start, c->nof_rb);
+  pdu.start_symbol_index          = c->start_symbol;
+  pdu.nof_symbols                 = c->nof_symbols;
+  pdu.ldpc_base_graph             = c->base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2;
+  pdu.tbs_lbrm                    = units::bytes(static_cast<unsigned>(c->tbs_lbrm_bytes));
+  pdu.ratio_pdsch_dmrs_to_sss_dB  = get_sch_to_dmrs_ratio_dB(c->cdm_groups);
+  pdu.ratio_pdsch_data_to_sss_dB  = 0.0F;
+  pdu.precoding                   = precoding_configuration(L, P, 1, MAX_NOF_PRBS);
+  for (unsigned port = 0; port != P; ++port) {
+    for (unsigned l = 0; l != L; ++l) {
+      pdu.precoding.set_coefficient(cf_t(weights[2 * (port * L + l)], weights[2 * (port * L + l) + 1]), l, port, 0);
+    }
+  }
+  return pdu;
+}
+
+/// A persistent thread running posted jobs (the processors' thread-local pools bind one instance per thread, so the
+/// benchmark's threads must live across repetitions, like the reference benchmark's unique_threads within a case).
+class bench_worker
+{
+public:
+  bench_worker() : th([this] { loop(); }) {}
+  ~bench_worker()
+  {
+    {
+      std::lock_guard<std::mutex> lock(mtx);
+      quit = true;
+    }
+    cv.notify_all();
+    th.join();
+  }
+  void post(std::function<void()> f)
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    job  = std::move(f);
+    done = false;
+    cv.notify_all();
+  }
+  void wait()
+  {
+    std::unique_lock<std::mutex> lock(mtx);
+    cv.wait(lock, [this] { return done; });
+  }
+
+private:
+  void loop()
+  {
+    std::unique_lock<std::mutex> lock(mtx);
+    for (;;) {
+      cv.wait(lock, [this] { return quit || job; });
+      if (quit) {
+        return;
+      }
+      std::function<void()> f = std::move(job);
+      job                      = nullptr;
+      lock.unlock();
+      f();
+      lock.lock();
+      done = true;
+      cv.notify_all();
+    }
+  }
+  std::mutex              mtx;
+  std::condition_variable cv;
+  std::function<void()>   job;
+  bool                    done = true;
+  bool                    quit = false;
+  std::thread             th;
+};
+
 struct chain_harness {
   // PUSCH: 0 CPU reference, 1 GPU estimator + demodulator + CPU decoder, 2 GPU estimator + demodulator + HW decoder.
   std::unique_ptr<pusch_processor>                                     pusch[3];
@@ -377,59 +575,18 @@ extern "C" {
 static void* chain_create_impl(int device, unsigned max_cb_ids)
 {
   auto* h = new chain_harness();
-  // CPU reference.
-  auto cpu_est = std::make_unique<dmrs_pusch_estimator_impl>(
-      std::make_unique<pseudo_random_generator_impl>(),
-      std::make_unique<low_papr_sequence_generator_impl>(),
-      std::make_unique<port_channel_estimator_average_impl>(std::make_unique<interpolator_linear_impl>(),
-                                                            ta_estimator(),
-                                                            port_channel_estimator_fd_smoothing_strategy::filter,
-                                                            port_channel_estimator_td_interpolation_strategy::average,
-                                                            true));
-  auto cpu_demod = std::make_unique<pusch_demodulator_impl>(
-      std::make_unique<channel_equalizer_generic_impl>(channel_equalizer_algorithm_type::zf),
-      nullptr,
-      std::make_unique<demodulation_mapper_impl>(),
-      std::make_unique<evm_calculator_generic_impl>(std::make_unique<modulation_mapper_lut_impl>()),
-      std::make_unique<pseudo_random_generator_impl>(),
-      MAX_RB,
-      true);
-  h->pusch[0] = make_pusch_processor(std::move(cpu_est), std::move(cpu_demod), cpu_pusch_decoder(), 6);
-
-  // GPU signal chain behind the same interfaces; factories dropped right after create() like the reference's.
-  const gpu::pusch_estimator_options est_opts =
-      gpu::make_pusch_estimator_options(port_channel_estimator_fd_smoothing_strategy::filter,
-                                        port_channel_estimator_td_interpolation_strategy::average,
-                                        true);
-  gpu::pusch_demodulator_options demod_opts;
-  for (int mode = 1; mode <= 2; ++mode) {
-    std::unique_ptr<pusch_decoder> dec;
-    if (mode == 1) {
-      dec = cpu_pusch_decoder();
-    } else {
+  for (int mode = 0; mode <= 2; ++mode) {
+    std::shared_ptr<pusch_decoder_hw_impl::hw_decoder_pool> hw_pool;
+    if (mode == 2) {
       std::vector<std::unique_ptr<hal::hw_accelerator_pusch_dec>> accs;
       accs.push_back(hal::create_hw_accelerator_pusch_dec_factory_gpu(device, max_cb_ids)->create());
-      auto pool = std::make_shared<pusch_decoder_hw_impl::hw_decoder_pool>(std::move(accs));
-      auto crcs = sch_crc<pusch_decoder_hw_impl::sch_crc>();
-      dec       = std::make_unique<pusch_decoder_hw_impl>(std::make_unique<ldpc_segmenter_rx_impl>(), crcs, pool, nullptr);
+      hw_pool = std::make_shared<pusch_decoder_hw_impl::hw_decoder_pool>(std::move(accs));
     }
-    h->pusch[mode] = make_pusch_processor(create_dmrs_pusch_estimator_factory_gpu(device, est_opts)->create(),
-                                          create_pusch_demodulator_factory_gpu(device, demod_opts)->create(),
-                                          std::move(dec),
-                                          6);
+    h->pusch[mode] =
+        new_pusch_processor(device, mode, port_channel_estimator_td_interpolation_strategy::average, 6, true, hw_pool);
   }
-  h->pdsch[0] = make_pdsch_processor(cpu_pdsch_encoder(), cpu_pdsch_modulator(), cpu_dmrs_pdsch());
-  {
-    auto seg_crc = sch_crc<ldpc_segmenter_tx_impl::sch_crc>();
-    auto crcs    = sch_crc<pdsch_encoder_hw_impl::sch_crc>();
-    auto enc     = std::make_unique<pdsch_encoder_hw_impl>(
-        crcs,
-        std::make_unique<ldpc_segmenter_tx_impl>(seg_crc),
-        hal::create_hw_accelerator_pdsch_enc_factory_gpu(device)->create());
-    h->pdsch[1] = make_pdsch_processor(std::move(enc),
-                                       create_pdsch_modulator_factory_gpu(device)->create(),
-                                       create_dmrs_pdsch_processor_factory_gpu(device)->create());
-  }
+  h->pdsch[0] = new_pdsch_processor(device, 0);
+  h->pdsch[1] = new_pdsch_processor(device, 1);
   h->ofdm_mod_gpu   = create_ofdm_modulator_factory_gpu(device);
   h->ofdm_demod_gpu = create_ofdm_demodulator_factory_gpu(device);
   return h;
@@ -511,39 +668,7 @@ static int chain_pusch_process_impl(void* p, int mode, const chain_params* c, co
   resource_grid_impl grid(P, 14, nsc);
   load_grid(grid, grid_in, P, nsc);
 
-  pusch_processor::pdu_t pdu;
-  pdu.slot                  = slot_point(subcarrier_spacing::kHz30, static_cast<unsigned>(c->slot));
-  pdu.rnti                  = static_cast<uint16_t>(c->rnti);
-  pdu.bwp_size_rb           = c->bwp_size;
-  pdu.bwp_start_rb          = c->bwp_start;
-  pdu.cp                    = cyclic_prefix::NORMAL;
-  pdu.mcs_descr             = {to_mod(c->qm), c->target_code_rate};
-  pdu.codeword              = pusch_processor::codeword_description{
-      static_cast<unsigned>(c->rv), c->base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2,
-      c->new_data != 0};
-  pdu.uci.nof_harq_ack          = c->nof_harq_ack;
-  pdu.uci.nof_csi_part1         = c->nof_csi_part1;
-  pdu.uci.alpha_scaling         = 1.0F;
-  pdu.uci.beta_offset_harq_ack  = 20.0F;
-  pdu.uci.beta_offset_csi_part1 = 6.25F;
-  pdu.uci.beta_offset_csi_part2 = 6.25F;
-  pdu.n_id                      = c->n_id;
-  pdu.nof_tx_layers             = c->nof_layers;
-  for (unsigned i = 0; i != P; ++i) {
-    pdu.rx_ports.push_back(static_cast<uint8_t>(i));
-  }
-  pdu.dmrs_symbol_mask   = symbol_mask(c->dmrs_mask);
-  pdu.dmrs               = pusch_processor::dmrs_configuration{c->dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1,
-                                                 static_cast<unsigned>(c->scrambling_id),
-                                                 c->n_scid != 0,
-                                                 static_cast<unsigned>(c->cdm_groups)};
-  pdu.freq_alloc         = rb_allocation::make_type1(c->rb_start, c->nof_rb);
-  pdu.start_symbol_index = c->start_symbol;
-  pdu.nof_symbols        = c->nof_symbols;
-  pdu.tbs_lbrm           = units::bytes(static_cast<unsigned>(c->tbs_lbrm_bytes));
-  if (c->dc_position >= 0) {
-    pdu.dc_position = static_cast<unsigned>(c->dc_position);
-  }
+  const pusch_processor::pdu_t pdu = make_pusch_pdu(*c);
 
   auto key = std::make_pair(mode == 0 ? 0 : mode, c->harq_id);
   const unsigned nof_cbs =
@@ -609,33 +734,7 @@ static int chain_pdsch_process_impl(void* p, int mode, const chain_params* c, co
   resource_grid_impl grid(P, 14, nsc);
   load_grid(grid, grid_inout, P, nsc);
 
-  pdsch_processor::pdu_t pdu;
-  pdu.slot         = slot_point(subcarrier_spacing::kHz30, static_cast<unsigned>(c->slot));
-  pdu.rnti         = static_cast<uint16_t>(c->rnti);
-  pdu.bwp_size_rb  = c->bwp_size;
-  pdu.bwp_start_rb = c->bwp_start;
-  pdu.cp           = cyclic_prefix::NORMAL;
-  pdu.codewords.push_back({to_mod(c->qm), static_cast<unsigned>(c->rv)});
-  pdu.n_id                        = c->n_id;
-  pdu.ref_point                   = pdsch_processor::pdu_t::CRB0;
-  pdu.dmrs_symbol_mask            = symbol_mask(c->dmrs_mask);
-  pdu.dmrs                        = c->dmrs_type2 ? dmrs_type::TYPE2 : dmrs_type::TYPE1;
-  pdu.scrambling_id               = c->scrambling_id;
-  pdu.n_scid                      = c->n_scid != 0;
-  pdu.nof_cdm_groups_without_data = c->cdm_groups;
-  pdu.freq_alloc                  = rb_allocation::make_type1(c->rb_start, c->nof_rb);
-  pdu.start_symbol_index          = c->start_symbol;
-  pdu.nof_symbols                 = c->nof_symbols;
-  pdu.ldpc_base_graph             = c->base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2;
-  pdu.tbs_lbrm                    = units::bytes(static_cast<unsigned>(c->tbs_lbrm_bytes));
-  pdu.ratio_pdsch_dmrs_to_sss_dB  = get_sch_to_dmrs_ratio_dB(c->cdm_groups);
-  pdu.ratio_pdsch_data_to_sss_dB  = 0.0F;
-  pdu.precoding                   = precoding_configuration(L, P, 1, MAX_NOF_PRBS);
-  for (unsigned port = 0; port != P; ++port) {
-    for (unsigned l = 0; l != L; ++l) {
-      pdu.precoding.set_coefficient(cf_t(weights[2 * (port * L + l)], weights[2 * (port * L + l) + 1]), l, port, 0);
-    }
-  }
+  const pdsch_processor::pdu_t pdu = make_pdsch_pdu(*c, weights);
   static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data;
   data.emplace_back(span<const uint8_t>(tb, tb_bytes));
   pdsch_done done;
@@ -740,6 +839,163 @@ int chain_ofdm_demodulate(void* p, int mode, unsigned numerology, unsigned bw_rb
   return guarded("chain_ofdm_demodulate", [&] {
     return chain_ofdm_demodulate_impl(
         p, mode, numerology, bw_rb, dft_size, scale, center_freq_hz, window_offset, slot, in, n, grid_port);
+  });
+}
+
+/// Throughput harness restating the reference's pusch_processor_benchmark.cpp "throughput_total" mode (the benchmark
+/// itself cannot be built here: the reference's DFT factories need FFTW, absent from this image): nof_threads
+/// persistent threads, each with its own pusch_processor_impl (mode 0 / 1 / 2 as chain_pusch_process; the benchmark's
+/// estimator configuration: filter smoothing, interpolate time strategy, CFO compensation; ZF; EVM off; 2 LDPC
+/// iterations with early stop, pusch_processor_benchmark.cpp:129-139, :630) and its own rx buffer, process the same PDU
+/// `batch` times over one grid of random complex-normal REs (:700-720); seconds[r] = wall time of repetition r (all
+/// threads). Returns the number of TBs whose CRC passed (0 on noise).
+static int chain_pusch_bench_impl(int                 device,
+                                  int                 mode,
+                                  const chain_params* c,
+                                  unsigned            tb_bytes,
+                                  unsigned            nof_threads,
+                                  unsigned            batch,
+                                  unsigned            repetitions,
+                                  double*             seconds)
+{
+  const unsigned     P   = c->nof_ports;
+  const unsigned     nsc = 12 * c->grid_prb;
+  resource_grid_impl grid(P, 14, nsc);
+  {
+    std::mt19937                    rgen(0);
+    std::normal_distribution<float> n(0.0F, std::sqrt(0.5F));
+    std::vector<cf_t>               row(nsc);
+    for (unsigned p = 0; p != P; ++p) {
+      for (unsigned l = 0; l != 14; ++l) {
+        for (cf_t& v : row) {
+          v = cf_t(n(rgen), n(rgen));
+        }
+        grid.get_writer().put(p, l, 0, row);
+      }
+    }
+  }
+  const pusch_processor::pdu_t pdu     = make_pusch_pdu(*c);
+  const unsigned               nof_cbs = ldpc::compute_nof_codeblocks(
+      units::bytes(tb_bytes).to_bits(), c->base_graph == 1 ? ldpc_base_graph_type::BG1 : ldpc_base_graph_type::BG2);
+  std::shared_ptr<pusch_decoder_hw_impl::hw_decoder_pool> hw_pool;
+  if (mode == 2) {
+    auto factory = hal::create_hw_accelerator_pusch_dec_factory_gpu(device, (nof_threads + 1) * CB_IDS_PER_HARQ);
+    std::vector<std::unique_ptr<hal::hw_accelerator_pusch_dec>> accs;
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      accs.push_back(factory->create());
+    }
+    hw_pool = std::make_shared<pusch_decoder_hw_impl::hw_decoder_pool>(std::move(accs));
+  }
+  std::vector<std::unique_ptr<pusch_processor>> procs;
+  std::vector<std::unique_ptr<test_rx_buffer>>  rxb;
+  std::vector<std::unique_ptr<bench_worker>>    workers;
+  for (unsigned t = 0; t != nof_threads; ++t) {
+    procs.push_back(new_pusch_processor(
+        device, mode, port_channel_estimator_td_interpolation_strategy::interpolate, 2, false, hw_pool));
+    rxb.push_back(std::make_unique<test_rx_buffer>(nof_cbs, t * CB_IDS_PER_HARQ));
+    workers.push_back(std::make_unique<bench_worker>());
+  }
+  std::atomic<int> ok{0};
+  auto run_batch = [&](unsigned t, unsigned n) {
+    std::vector<uint8_t> data(tb_bytes);
+    for (unsigned i = 0; i != n; ++i) {
+      result_capture notifier;
+      procs[t]->process(data, unique_rx_buffer(*rxb[t]), notifier, grid.get_reader(), pdu);
+      ok += (notifier.have_sch && notifier.sch.data.tb_crc_ok) ? 1 : 0;
+    }
+  };
+  // Warm-up: one PDU per thread (plans, pinned staging, first-call setup).
+  for (unsigned t = 0; t != nof_threads; ++t) {
+    workers[t]->post([&, t] { run_batch(t, 1); });
+  }
+  for (auto& w : workers) {
+    w->wait();
+  }
+  ok = 0;
+  for (unsigned r = 0; r != repetitions; ++r) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      workers[t]->post([&, t] { run_batch(t, batch); });
+    }
+    for (auto& w : workers) {
+      w->wait();
+    }
+    seconds[r] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return ok.load();
+}
+
+/// The same harness for the reference's pdsch_processor_benchmark.cpp "throughput_total" mode: nof_threads persistent
+/// threads, each with its own pdsch_processor_impl (mode 0 CPU, 1 GPU) and resource grid, process the same PDU with a
+/// random TB `batch` times. seconds[r] = wall time of repetition r.
+static int chain_pdsch_bench_impl(int                 device,
+                                  int                 mode,
+                                  const chain_params* c,
+                                  const float*        weights,
+                                  unsigned            tb_bytes,
+                                  unsigned            nof_threads,
+                                  unsigned            batch,
+                                  unsigned            repetitions,
+                                  double*             seconds)
+{
+  const pdsch_processor::pdu_t                     pdu = make_pdsch_pdu(*c, weights);
+  std::vector<std::unique_ptr<pdsch_processor>>    procs;
+  std::vector<std::unique_ptr<resource_grid_impl>> grids;
+  std::vector<std::unique_ptr<bench_worker>>       workers;
+  std::vector<uint8_t>                             tb(tb_bytes);
+  std::mt19937                                     rgen(1);
+  for (uint8_t& b : tb) {
+    b = static_cast<uint8_t>(rgen());
+  }
+  for (unsigned t = 0; t != nof_threads; ++t) {
+    procs.push_back(new_pdsch_processor(device, mode));
+    grids.push_back(std::make_unique<resource_grid_impl>(c->nof_ports, 14, 12 * c->grid_prb));
+    grids.back()->set_all_zero();
+    workers.push_back(std::make_unique<bench_worker>());
+  }
+  std::atomic<int> done{0};
+  auto run_batch = [&](unsigned t, unsigned n) {
+    for (unsigned i = 0; i != n; ++i) {
+      static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data;
+      data.emplace_back(span<const uint8_t>(tb));
+      pdsch_done notifier;
+      procs[t]->process(grids[t]->get_writer(), notifier, std::move(data), pdu);
+      done += notifier.done ? 1 : 0;
+    }
+  };
+  for (unsigned t = 0; t != nof_threads; ++t) {
+    workers[t]->post([&, t] { run_batch(t, 1); });
+  }
+  for (auto& w : workers) {
+    w->wait();
+  }
+  done = 0;
+  for (unsigned r = 0; r != repetitions; ++r) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      workers[t]->post([&, t] { run_batch(t, batch); });
+    }
+    for (auto& w : workers) {
+      w->wait();
+    }
+    seconds[r] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return done.load();
+}
+
+int chain_pusch_bench(int device, int mode, const chain_params* c, unsigned tb_bytes, unsigned nof_threads,
+                      unsigned batch, unsigned repetitions, double* seconds)
+{
+  return guarded("chain_pusch_bench", [&] {
+    return chain_pusch_bench_impl(device, mode, c, tb_bytes, nof_threads, batch, repetitions, seconds);
+  });
+}
+
+int chain_pdsch_bench(int device, int mode, const chain_params* c, const float* weights, unsigned tb_bytes,
+                      unsigned nof_threads, unsigned batch, unsigned repetitions, double* seconds)
+{
+  return guarded("chain_pdsch_bench", [&] {
+    return chain_pdsch_bench_impl(device, mode, c, weights, tb_bytes, nof_threads, batch, repetitions, seconds);
   });
 }
 

@@ -182,8 +182,8 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
   const int      Z      = d.Z;
   const auto     sh     = (const_u32_ptr)(uintptr_t)(shift_table + static_cast<uint32_t>(d.zpos) * G::NE);
   // Warm the scalar cache with this Z's shift row while the LLRs load: the layers read it with s_load, and cold
-  // misses there would stall every layer of the first iteration. The destinations stay live (and unused) until the
-  // explicit wait below, so no register is reused while a load is still in flight.
+  // misses there would stall every layer of the first iteration. The loads are ordinary (compiler-tracked) scalar loads
+  // consumed only after the LLR stage (scalar_touch, ldpc_decoder_common.h).
   // (Kernel arguments are pinned in SGPRs first: a later kernarg s_load would wait for the warm-up loads.)
   asm volatile("" ::"s"(llrs), "s"(out), "s"(results), "s"(crc_tables), "s"(cb_crc_ok), "s"(blockDim.x));
   constexpr int SH_LINES = (G::NE * 4 - 4) / 64 + 2;
@@ -304,8 +304,7 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
     scratch[wave] = last;
   }
   __syncthreads();
-  // The scalar-cache warm-up loads have landed long ago; retire them before any early return.
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // Consume the scalar-cache warm-up loads (they landed long ago; the compiler places the wait).
   static_for<SH_LINES>([&](auto L) { keep_sgpr(pf[decltype(L)::value]); });
   int input_size = scratch[0];
   for (int w = 1; w < nwaves; ++w) {

@@ -53,12 +53,15 @@ __device__ __forceinline__ int scale_mag(int m, uint32_t sf16, float sf)
 /// Lifting shifts are read through the scalar (constant) path: wave-uniform, compile-time offsets -> s_load.
 using const_u32_ptr = const __attribute__((address_space(4))) uint32_t*;
 
-/// Issues an s_load of sh[OFF / 4] into dst without waiting for it (scalar-cache warm-up). The caller must keep dst
-/// live until an explicit "s_waitcnt lgkmcnt(0)" (the compiler does not track this load).
+/// Scalar-cache warm-up: an s_load of sh[OFF / 4] that the caller consumes (keep_sgpr) only after the work it overlaps.
+/// It is an ordinary load, so the compiler's wait-count pass tracks it. An earlier version issued the s_load from
+/// inline asm: under register pressure (the __launch_bounds__(192, 8) build) the compiler spilled the asm's destination
+/// SGPR with v_writelane and reused it for address arithmetic while the untracked load was still in flight; the load's
+/// late return then overwrote a live address register and the kernel faulted ("register-capped fault").
 template <int OFF>
 __device__ __forceinline__ void scalar_touch(uint32_t& dst, const __attribute__((address_space(4))) uint32_t* sh)
 {
-  asm volatile("s_load_dword %0, %1, %2" : "=s"(dst) : "s"(sh), "n"(OFF));
+  dst = sh[OFF / 4];
 }
 __device__ __forceinline__ void keep_sgpr(uint32_t v)
 {

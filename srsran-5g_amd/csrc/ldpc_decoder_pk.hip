@@ -566,8 +566,7 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
     scratch[wave] = last;
   }
   __syncthreads();
-  // The scalar-cache warm-up loads have landed long ago; retire them before any early return.
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // Consume the scalar-cache warm-up loads (they landed long ago; the compiler places the wait).
   static_for<AB_LINES>([&](auto L) { keep_sgpr(pf[decltype(L)::value]); });
   int input_size = scratch[0];
   for (int w = 1; w < nwaves; ++w) {

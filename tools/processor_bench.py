@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""The reference's PHY processor benchmarks (pusch_processor_benchmark.cpp, pdsch_processor_benchmark.cpp, "throughput
+total" mode) restated over the reference's own processors (oracle/_ref/libsrschain.so: pusch_processor_impl /
+pdsch_processor_impl built from their sources) on the reference's CPU components and on the GPU bindings of
+integration/ (the benchmarks themselves cannot be built here: the reference's DFT factories need FFTW, absent from
+this image). Same profiles, PDUs, thread / batch / repetition scheme; prints one JSON object.
+
+GPU box: python tools/processor_bench.py [--threads N] [--batch B] [--repetitions R] > out.json
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "srsran-5g_amd")]
+
+import chain_harness as H  # noqa: E402
+from srsgpu import sch  # noqa: E402
+
+
+def host_cores():
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
+
+
+def run(lib, fn, mode, p, tbs, threads, batch, reps, weights=None):
+    import ctypes
+    secs = np.zeros(reps, np.float64)
+    args = [0, mode, ctypes.byref(p)]
+    if weights is not None:
+        w = np.ascontiguousarray(weights, np.complex64).view(np.float32)
+        args.append(w.ctypes.data_as(ctypes.c_void_p))
+    args += [tbs // 8, threads, batch, reps, secs.ctypes.data_as(ctypes.c_void_p)]
+    r = fn(*args)
+    assert r >= 0, f"benchmark failed ({r})"
+    pdus = threads * batch
+    med = float(np.median(secs))
+    return {"mode": mode, "threads": threads, "batch_per_thread": batch, "repetitions": reps,
+            "seconds_median": med, "throughput_mbps_median": pdus * tbs / med / 1e6,
+            "throughput_mbps_max": pdus * tbs / float(np.min(secs)) / 1e6,
+            "pdus_per_s": pdus / med, "tb_crc_ok": int(r)}
+
+
+def main():
+    import ctypes
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", type=int, default=host_cores())
+    ap.add_argument("--batch", type=int, default=20)
+    ap.add_argument("--repetitions", type=int, default=5)
+    args = ap.parse_args()
+    lib = ctypes.CDLL(H.CHAIN_SO)
+    PP = ctypes.POINTER(H.ChainParams)
+    lib.chain_pusch_bench.restype = ctypes.c_int
+    lib.chain_pusch_bench.argtypes = [ctypes.c_int, ctypes.c_int, PP, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint,
+                                      ctypes.c_uint, ctypes.c_void_p]
+    lib.chain_pdsch_bench.restype = ctypes.c_int
+    lib.chain_pdsch_bench.argtypes = [ctypes.c_int, ctypes.c_int, PP, ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint,
+                                      ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p]
+    T, B, R = args.threads, args.batch, args.repetitions
+    out = {"threads": T, "note": "reference processors (pusch_processor_impl / pdsch_processor_impl) on CPU components "
+                                 "(mode 0) vs GPU bindings (PUSCH mode 2: GPU estimator + demodulator + "
+                                 "pusch_decoder_hw_impl over the GPU accelerator; PDSCH mode 1: HW encoder + GPU "
+                                 "modulator + GPU DM-RS); pusch_processor_benchmark.cpp / pdsch_processor_benchmark.cpp "
+                                 "profiles, throughput_total = TB bits of all PDUs / wall time", "pusch": [], "pdsch": []}
+    # PUSCH: scs30_100MHz_256qam_rv0_4port_nlayer (273 PRB, 256QAM R 948/1024, 4 rx ports, DM-RS 2 + 11, 2 CDM
+    # groups, filter / interpolate / CFO estimator, 2 LDPC iterations, random-noise grid).
+    for layers in (1, 2, 4):
+        tbs = sch.tbs_calculate(273, 14, 6 * 2 * 2, 0, 8, 948.0, layers)
+        p = H.params(slot=0, rnti=1, n_id=0, scrambling_id=0, nof_rb=273, rb_start=0, bwp_size=273, qm=8,
+                     target_code_rate=948.0, nof_layers=layers, nof_ports=4, base_graph=sch.base_graph(tbs, 948 / 1024),
+                     tbs_lbrm_bytes=159749)  # sch_constants.h:44 tbs_lbrm_default
+        case = {"profile": "scs30_100MHz_256qam_rv0_4port_nlayer", "nof_prb": 273, "layers": layers, "tbs": tbs,
+                "peak_mbps_per_cell": tbs / 500.0}
+        modes = (0, 2) if layers == 1 else (2,)  # the reference's estimator estimates one layer
+        case["runs"] = [run(lib, lib.chain_pusch_bench, m, p, tbs, T, B if m else max(2, B // 4), R) for m in modes]
+        out["pusch"].append(case)
+        print(json.dumps(case), file=sys.stderr, flush=True)
+    # PDSCH: 4port_4layer_scs30_100MHz_256qam (270 PRB, 4 layers on 4 ports, symbols 2..13, DM-RS 2 + 7 + 11) and
+    # scs30_100MHz_256qam_max (1 port, 1 layer).
+    rng = np.random.default_rng(0)
+    for name, layers in (("4port_4layer_scs30_100MHz_256qam", 4), ("scs30_100MHz_256qam_max", 1)):
+        tbs = sch.tbs_calculate(270, 12, 6 * 3 * 2, 0, 8, 948.0, layers)
+        p = H.params(slot=0, rnti=1, n_id=0, scrambling_id=0, nof_rb=270, rb_start=0, bwp_size=270, qm=8,
+                     target_code_rate=948.0, nof_layers=layers, nof_ports=layers, start_symbol=2, nof_symbols=12,
+                     dmrs_mask=(1 << 2) | (1 << 7) | (1 << 11), base_graph=sch.base_graph(tbs, 948 / 1024),
+                     tbs_lbrm_bytes=159749)
+        q, _ = np.linalg.qr(rng.normal(size=(layers, layers)) + 1j * rng.normal(size=(layers, layers)))
+        case = {"profile": name, "nof_prb": 270, "layers": layers, "tbs": tbs, "peak_mbps_per_cell": tbs / 500.0}
+        case["runs"] = [run(lib, lib.chain_pdsch_bench, m, p, tbs, T, B if m else max(2, B // 4), R, weights=q)
+                        for m in (0, 1)]
+        out["pdsch"].append(case)
+        print(json.dumps(case), file=sys.stderr, flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -4,8 +4,8 @@ OUT=gpurun_out/${1:-icache}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 R=$(pwd)
-timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_IFETCH SQ_WAVES -d "$R/$OUT/pmc" \
-  -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-extra-points --steps 20 --warmup 4 \
+timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_IFETCH SQ_WAVES -d "$R/$OUT/pmc" \
+  -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-extra-points --steps 20 --warmup 4 --min-time 0 --no-extra-workloads \
   ${2:-} > "$OUT/bench.json" 2> "$OUT/bench.err"
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections

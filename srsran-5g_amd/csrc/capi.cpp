@@ -107,6 +107,7 @@ struct srsgpu_ldpc_decoder_plan {
     bool      packed  = false;
     int       max_layers = 0;
     int       split   = 1;   ///< 2: edge-split kernel (each row's edges over two wave halves), see upload_decoder_plan
+    int       pack    = 1;   ///< LDPC_PK4: multi-codeblock workgroups (count = workgroups), see pk4_layout_for
     int       threads = 64;
     int       count   = 0;
     dec_desc* d_desc  = nullptr;
@@ -357,7 +358,9 @@ int srsgpu_context_create(int device, srsgpu_context** out)
     // The decoder reads its shifts through scalar loads, which are dword-granular: it gets a 32-bit copy.
     std::vector<uint32_t> tab32(tab.begin(), tab.end());
     // Packed decoder: rows z and z + H of a lane read the pair at min(2z + A, 2z + B) (row z) and its partner byte.
-    std::vector<uint32_t> ab(static_cast<size_t>(51) * ne, 0u);
+    // PK4 (multi-codeblock workgroups, ldpc_decoder_pk.hip): pairs are 2 LDPC_PK4 bytes apart in the interleaved
+    // image, the lane constant is 2 LDPC_PK4 z + 2 slot: A = 2 PK4 s' + hi, B = 2 PK4 (s' - H) + 1 - hi.
+    std::vector<uint32_t> ab(static_cast<size_t>(51) * ne, 0u), ab4(static_cast<size_t>(51) * ne, 0u);
     for (int p = 0; p < 51; ++p) {
       const int Z = kLiftingSizes[p];
       if (Z % 2 != 0) {
@@ -372,10 +375,17 @@ int srsgpu_context_create(int device, srsgpu_context** out)
         const int B   = 2 * sm - 2 * H + 1 - hi;
         // One dword per edge: A in the low half, B (negative: wraps) in the high half.
         ab[static_cast<size_t>(p) * ne + e] = static_cast<uint32_t>(A) | (static_cast<uint32_t>(B & 0xffff) << 16);
+        const int A4 = 2 * LDPC_PK4 * sm + hi;
+        const int B4 = 2 * LDPC_PK4 * (sm - H) + 1 - hi;
+        ab4[static_cast<size_t>(p) * ne + e] =
+            static_cast<uint32_t>(A4) | (static_cast<uint32_t>(B4 & 0xffff) << 16);
       }
     }
     if (hipMalloc(&ctx->d_pair_ab[bg - 1], ab.size() * sizeof(uint32_t)) != hipSuccess ||
         hipMemcpy(ctx->d_pair_ab[bg - 1], ab.data(), ab.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        hipMalloc(&ctx->d_pair_ab4[bg - 1], ab4.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipMemcpy(ctx->d_pair_ab4[bg - 1], ab4.data(), ab4.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
             hipSuccess) {
       srsgpu_context_destroy(ctx);
       return fail(SRSGPU_ERR_HIP, "failed to upload LDPC pair address tables");
@@ -430,6 +440,11 @@ void srsgpu_context_destroy(srsgpu_context* ctx)
     }
   }
   for (auto* p : ctx->d_shifts32) {
+    if (p != nullptr) {
+      (void)hipFree(p);
+    }
+  }
+  for (auto* p : ctx->d_pair_ab4) {
     if (p != nullptr) {
       (void)hipFree(p);
     }
@@ -552,6 +567,101 @@ int add_decoder_cb(srsgpu_context* ctx,
   return SRSGPU_OK;
 }
 
+/// Workgroup layout of a packed-kernel launch group on the multi-codeblock kernel (ldpc_decode_pk4_kernel).
+struct pk4_layout {
+  int                   threads = 0;
+  int                   groups  = 0;
+  std::vector<dec_desc> slots;  ///< groups x LDPC_PK4 descriptors, empty slots zero
+};
+
+/// Issue cost model of a decoder launch (the kernel is bound by wave-instruction issue, profiles/r3_decoder_z_sweep.log:
+/// a codeblock costs the waves its lanes span, whatever their fill): active waves, stretched when fewer than 16 waves
+/// fit a CU (4 per SIMD are needed for the SIMD's VALU rate; one wave issues at a quarter of it).
+double decoder_issue_cost(long active_waves, int threads, int max_layers, size_t lds_bytes)
+{
+  const int wpg      = threads / 64;
+  const int wave_cap = max_layers <= 8 ? 20 : 16;  // 5 / 4 waves per SIMD at the kernels' VGPR counts
+  const int by_vgpr  = wave_cap / wpg;
+  const int by_lds   = static_cast<int>((160u * 1024u) / lds_bytes);
+  const int resident = std::min(by_vgpr, by_lds) * wpg;
+  if (resident <= 0) {
+    return 1e300;
+  }
+  return static_cast<double>(active_waves) * std::max(1.0, 16.0 / resident);
+}
+
+/// Chooses whether a packed-kernel launch group runs on the multi-codeblock kernel, and its workgroup size: codeblocks
+/// sharing the workgroup-uniform parameters (Z, scaling, iteration limit, CRC mode) are packed LDPC_PK4 at a time
+/// (fewer if c Z / 2 lanes exceed the workgroup), over every workgroup size of 64..LDPC_PK4 x 192 lanes; taken when the
+/// cost model gives >= 5 % less than the one-codeblock kernel. SRSGPU_DECODER_PK4=0 / 1 forces either (A/B tests).
+bool pk4_layout_for(int bg, int max_layers, int threads1, const std::vector<dec_desc>& cbs, pk4_layout& out)
+{
+  const char* env = std::getenv("SRSGPU_DECODER_PK4");
+  if ((env != nullptr && env[0] == '0') || max_layers > 16 || cbs.empty()) {
+    return false;
+  }
+  const int K = (bg == 1) ? kBG1_K : kBG2_K;
+  std::vector<dec_desc> v(cbs);
+  auto                  key = [](const dec_desc& d) {
+    return std::make_tuple(d.Z, d.sf16, d.max_iter, static_cast<uint32_t>(d.flags), d.crc_table == NO_CRC_TABLE);
+  };
+  std::stable_sort(v.begin(), v.end(), [&](const dec_desc& a, const dec_desc& b) { return key(a) < key(b); });
+  // Runs of equal keys (a run's codeblocks may share workgroups; the scaling float follows sf16).
+  std::vector<std::pair<size_t, size_t>> runs;
+  for (size_t i = 0; i < v.size();) {
+    size_t j = i + 1;
+    while (j < v.size() && key(v[j]) == key(v[i]) && v[j].sf == v[i].sf) {
+      ++j;
+    }
+    runs.emplace_back(i, j);
+    i = j;
+  }
+  const size_t lds1  = static_cast<size_t>(K + max_layers) * SOFT_COL_STRIDE + 256;
+  const size_t lds4  = static_cast<size_t>(LDPC_PK4) * (K + max_layers) * SOFT_COL_STRIDE + 1024;
+  const double cost1 = decoder_issue_cost(static_cast<long>(cbs.size()) * (threads1 / 64), threads1, max_layers, lds1);
+  double       best  = 1e300;
+  int          best_t = 0;
+  for (int t = 64; t <= LDPC_PK4 * 192; t += 64) {
+    long active = 0;
+    bool ok     = true;
+    for (const auto& r : runs) {
+      const int H = v[r.first].Z / 2;
+      const int c = std::min(LDPC_PK4, t / H);
+      if (c == 0) {
+        ok = false;
+        break;
+      }
+      const long n = static_cast<long>(r.second - r.first);
+      active += (n / c) * ((c * H + 63) / 64) + ((n % c) != 0 ? ((n % c) * H + 63) / 64 : 0);
+    }
+    if (!ok) {
+      continue;
+    }
+    const double c4 = decoder_issue_cost(active, t, max_layers, lds4);
+    if (c4 < best) {
+      best   = c4;
+      best_t = t;
+    }
+  }
+  const bool force = env != nullptr && env[0] == '1';
+  if (best_t == 0 || (!force && best >= 0.95 * cost1)) {
+    return false;
+  }
+  out.threads = best_t;
+  out.slots.clear();
+  for (const auto& r : runs) {
+    const int c = std::min(LDPC_PK4, best_t / (v[r.first].Z / 2));
+    for (size_t i = r.first; i < r.second; i += static_cast<size_t>(c)) {
+      const size_t n = std::min(static_cast<size_t>(c), r.second - i);
+      for (size_t k = 0; k < static_cast<size_t>(LDPC_PK4); ++k) {
+        out.slots.push_back(k < n ? v[i + k] : dec_desc{});
+      }
+    }
+  }
+  out.groups = static_cast<int>(out.slots.size() / LDPC_PK4);
+  return true;
+}
+
 int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, srsgpu_ldpc_decoder_plan** plan_out)
 {
   auto* plan = new srsgpu_ldpc_decoder_plan();
@@ -580,9 +690,18 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
     for (const dec_desc& d : kv.second) {
       plan->input_llrs += d.nof_llr;
     }
-    const size_t bytes = kv.second.size() * sizeof(dec_desc);
+    pk4_layout             pk4;
+    const dec_desc*        src   = kv.second.data();
+    size_t                 bytes = kv.second.size() * sizeof(dec_desc);
+    if (g.packed && g.split == 1 && pk4_layout_for(g.bg, g.max_layers, g.threads, kv.second, pk4)) {
+      g.pack    = LDPC_PK4;
+      g.threads = pk4.threads;
+      g.count   = pk4.groups;
+      src       = pk4.slots.data();
+      bytes     = pk4.slots.size() * sizeof(dec_desc);
+    }
     if (hipMalloc(&g.d_desc, bytes) != hipSuccess ||
-        hipMemcpy(g.d_desc, kv.second.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(g.d_desc, src, bytes, hipMemcpyHostToDevice) != hipSuccess) {
       plan->groups.push_back(g);
       srsgpu_ldpc_decoder_plan_destroy(plan);
       return fail(SRSGPU_ERR_HIP, "failed to upload decoder descriptors");
@@ -601,7 +720,11 @@ int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
                          hipStream_t                     s)
 {
   for (const auto& g : plan->groups) {
-    if (g.packed) {
+    if (g.pack == LDPC_PK4) {
+      launch_ldpc_decode_pk4(g.bg, plan->impl, g.max_layers, g.d_desc, g.count, g.threads, d_llrs, d_out,
+                             d_nof_iterations, plan->ctx->d_pair_ab4[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok,
+                             s);
+    } else if (g.packed) {
       launch_ldpc_decode_pk(g.bg, plan->impl, g.max_layers, g.split, g.d_desc, g.count, g.threads, d_llrs, d_out,
                             d_nof_iterations,
                             plan->ctx->d_pair_ab[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s);

@@ -150,7 +150,7 @@ constexpr int SIGNS_W0 = 11;
 
 /// Two lifted check rows (z, z + H) of layer m: v2c messages, min-sum analysis, c2v messages, soft-bit update
 /// (ldpc_decoder_impl.cpp:195, :255, :240; arithmetic of ldpc_decoder_avx2.cpp:69/:111/:165/:205).
-template <int BG, int MODE, int m, bool KEEP_ADDR>
+template <int BG, int MODE, int m, bool KEEP_ADDR, int CS = SOFT_COL_STRIDE>
 __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
                                               const_u32_ptr  ab,  // A | B << 16 address constants of this Z
                                               uint32_t       z2x2,  // 2z in both halves
@@ -185,8 +185,8 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     }
     // Two byte loads merged by one v_perm (d16 loads do not preserve the other half with SRAM ECC on gfx950).
 #ifndef LDPC_PK_EXPERIMENT_NO_LOADS
-    const s16x2 sb{static_cast<short>(soft[col * SOFT_COL_STRIDE + a]),
-                   static_cast<short>(soft[col * SOFT_COL_STRIDE + (a ^ 1u)])};
+    const s16x2 sb{static_cast<short>(soft[col * CS + a]),
+                   static_cast<short>(soft[col * CS + (a ^ 1u)])};
 #else  // timing experiments only
     const s16x2 sb = as_s16(((a * 0x9e3779b1u) >> 3) & 0x003f003fu);
 #endif
@@ -248,8 +248,8 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
       a = pair_address(z2x2_b, ab[e0 + e]);
     }
 #ifndef LDPC_PK_EXPERIMENT_NO_STORES
-    soft[col * SOFT_COL_STRIDE + a]        = static_cast<int8_t>(sb.x);
-    soft[col * SOFT_COL_STRIDE + (a ^ 1u)] = static_cast<int8_t>(sb.y);
+    soft[col * CS + a]        = static_cast<int8_t>(sb.x);
+    soft[col * CS + (a ^ 1u)] = static_cast<int8_t>(sb.y);
 #else  // timing experiments only: keep the values alive
     nhi ^= bits(sb) + a;
 #endif
@@ -747,6 +747,391 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------------
+// Multi-codeblock workgroups (PK4). The plain kernel gives a codeblock 64 * ceil(Z / 128) lanes: a Z = 288 codeblock
+// runs three waves of which the third has 16 active lanes, and every wave issues the full instruction stream (the
+// decoder is bound by wave-instruction issue: at a fixed per-lane load, Z = 256 on two waves decodes 1.6x the
+// codeblocks per second of Z = 288 on three, profiles/r3_decoder_z_sweep.log). Here up to PK4 codeblocks of one lifting
+// size share a workgroup: codeblock slot i owns lanes [i H, (i + 1) H), so the lanes are packed without gaps (four
+// Z = 288 codeblocks on nine full waves) and a wave whose codeblocks have all stopped skips the layer bodies.
+//
+// The soft-bit images of the slots are interleaved pair by pair: position p of column c of slot i is at byte
+// c * PK4_CS + 2 * PK4 * (p mod H) + 2 i + [p >= H]. With the lane constant u = 2 PK4 z + 2 i and the per-(Z, edge)
+// constants A = 2 PK4 s' + hi, B = 2 PK4 (s' - H) + 1 - hi (s' = shift mod H, hi = [shift >= H]; ctx d_pair_ab4) the
+// packed kernel's address arithmetic (min(u + A, u + B) in 16-bit halves, partner byte a ^ 1) and its column
+// immediates are unchanged: row_update_pk runs as is, with column stride PK4_CS.
+//
+// Per codeblock as in the plain kernel: HARQ skip, LLR load, layer count, CRC early stop, hard decisions and results.
+// The slots of a workgroup share the iteration loop (a stopped codeblock's lanes idle through the layers and barriers
+// until the last one stops). The host puts codeblocks with the same Z, scaling, iteration limit and CRC mode in a
+// workgroup (descs[PK4 * w + i], empty slots have nof_llr = 0).
+// ---------------------------------------------------------------------------------------------------------------------
+constexpr int PK4       = LDPC_PK4;
+constexpr int PK4_CS    = PK4 * SOFT_COL_STRIDE;
+constexpr int PK4_WAVES = PK4 * 192 / WAVE;
+constexpr int PK4_RED   = 2 * PK4 * PK4_WAVES * 2;  ///< CRC reduction ints: [iteration parity][slot][wave][acc, zero]
+constexpr int PK4_SCRATCH_INTS = PK4_WAVES + PK4_RED + 2 * PK4;
+
+/// Byte offset of position l (0 <= l < Z) of slot i within a column of the interleaved image.
+__device__ __forceinline__ uint32_t pair_pos4(uint32_t l, uint32_t H, uint32_t i)
+{
+  return ((l < H) ? 2u * PK4 * l : 2u * PK4 * (l - H) + 1u) + 2u * i;
+}
+
+/// LLRs of one codeblock -> its slot of the interleaved image (ldpc_decoder_impl.cpp:152; the plain kernel's load with
+/// the slot's addresses), the punctured columns and every position beyond the input zeroed. Returns this thread's
+/// index of the last non-zero LLR it saw (ldpc_decoder_impl.cpp:94), -1 if none.
+template <int NCOL>
+__device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const int8_t* __restrict__ llrs,
+                                             const dec_desc& d, uint32_t slot)
+{
+  const int      Z     = d.Z;
+  const uint32_t H     = static_cast<uint32_t>(Z) / 2u;
+  const int8_t*  llr   = llrs + d.llr_offset;
+  const int      n_llr = static_cast<int>(d.nof_llr);
+  const uint32_t ncols = __umulhi(static_cast<uint32_t>(n_llr), d.div_magic);
+  const uint32_t full  = ncols * static_cast<uint32_t>(Z);
+  int            last  = -1;
+  const uint32_t head  = static_cast<uint32_t>(d.llr_offset) & 15u;
+  const uint4*   vecs  = reinterpret_cast<const uint4*>(llr - head);
+  const int      nvec  = static_cast<int>((head + static_cast<uint32_t>(n_llr) + 15u) >> 4);
+  constexpr int  BATCH = ((NCOL - 2) * 384 / 16 + 191) / 192;
+  int            last_w = -1;
+  uint4          last_v = make_uint4(0u, 0u, 0u, 0u);
+  for (int w0 = threadIdx.x; w0 < nvec; w0 += BATCH * blockDim.x) {
+    uint4 val[BATCH];
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) {
+      const int w = w0 + j * blockDim.x;
+      val[j]      = (w < nvec) ? vecs[w] : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) {
+      const int w = w0 + j * blockDim.x;
+      if (w >= nvec) {
+        continue;
+      }
+      const uint32_t i0 = static_cast<uint32_t>(16 * w) - head;
+      const uint32_t c0 = __umulhi(i0, d.div_magic);
+      const uint32_t l0 = i0 - c0 * static_cast<uint32_t>(Z);
+      const bool short_path = (16u * static_cast<uint32_t>(w) >= head) && (i0 + 16u <= full) &&
+                              (l0 + 16u <= static_cast<uint32_t>(Z));
+      if (short_path) {
+        // Consecutive positions are 2 PK4 bytes apart; a byte past the half boundary moves by 1 - 2 PK4 H.
+        int8_t*        dst   = soft + (c0 + 2) * PK4_CS + pair_pos4(l0, H, slot);
+        const uint32_t cross = (l0 < H && l0 + 16u > H) ? (0xffffu << (H - l0)) : 0u;
+        const int      adj   = 1 - 2 * PK4 * static_cast<int>(H);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int kk = 4 * q + k;
+            const int mv = static_cast<int>((cross >> kk) & 1u) * adj;
+            dst[2 * PK4 * kk + mv] = static_cast<int8_t>(clamp_i(static_cast<int8_t>(word >> (8 * k)), -64, 64));
+          }
+        }
+        if ((val[j].x | val[j].y | val[j].z | val[j].w) != 0u) {
+          last_w = w;
+          last_v = val[j];
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t i = i0 + static_cast<uint32_t>(4 * q + k);
+            if (i < static_cast<uint32_t>(n_llr)) {
+              int v = static_cast<int8_t>(word >> (8 * k));
+              last  = (v != 0) ? static_cast<int>(i) : last;
+              v     = (i < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
+              const uint32_t cq = __umulhi(i, d.div_magic);
+              soft[(cq + 2) * PK4_CS + pair_pos4(i - cq * static_cast<uint32_t>(Z), H, slot)] = static_cast<int8_t>(v);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (last_w >= 0) {
+    const uint32_t words[4] = {last_v.x, last_v.y, last_v.z, last_v.w};
+    int            hb       = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      hb = (words[q] != 0u) ? 4 * q + (31 - __clz(static_cast<int>(words[q]))) / 8 : hb;
+    }
+    const int i = 16 * last_w - static_cast<int>(head) + hb;
+    last        = i > last ? i : last;
+  }
+  // Punctured columns 0, 1 and every position beyond the input: threads [0, H) take position pair z.
+  const uint32_t z = threadIdx.x;
+  if (z < H) {
+    auto* soft16 = reinterpret_cast<uint16_t*>(soft);
+    const uint32_t pz = PK4 * z + slot;  // 16-bit index of pair z within a column
+    soft16[(0 * PK4_CS) / 2 + pz] = 0;
+    soft16[(1 * PK4_CS) / 2 + pz] = 0;
+    int c = 2 + static_cast<int>(ncols);
+    if (static_cast<uint32_t>(n_llr) > full) {
+      const uint32_t rem = static_cast<uint32_t>(n_llr) - full;
+      if (z >= rem) {
+        soft[c * PK4_CS + 2 * pz] = 0;
+      }
+      if (z + H >= rem) {
+        soft[c * PK4_CS + 2 * pz + 1] = 0;
+      }
+      ++c;
+    }
+    for (; c < NCOL; ++c) {
+      soft16[(c * PK4_CS) / 2 + pz] = 0;
+    }
+  }
+  return last;
+}
+
+/// Hard decisions of one slot's K*Z systematic bits, written by the slot's H lanes (lane z: bytes z, z + H, ...).
+__device__ __forceinline__ void write_hard_bits_pk4(const int8_t* __restrict__ soft, uint8_t* __restrict__ out,
+                                                    int nbits, int Z, uint32_t magic, uint32_t slot, uint32_t z)
+{
+  const uint32_t H      = static_cast<uint32_t>(Z) / 2u;
+  const int      nbytes = (nbits + 7) / 8;
+  for (int b = static_cast<int>(z); b < nbytes; b += static_cast<int>(H)) {
+    uint32_t byte = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = 8 * b + k;
+      if (i < nbits) {
+        const uint32_t col = __umulhi(static_cast<uint32_t>(i), magic);
+        const uint32_t l   = static_cast<uint32_t>(i) - col * static_cast<uint32_t>(Z);
+        byte |= static_cast<uint32_t>(soft[col * PK4_CS + pair_pos4(l, H, slot)] <= 0) << (7 - k);
+      }
+    }
+    out[b] = static_cast<uint8_t>(byte);
+  }
+}
+
+template <int BG, int MODE, int MAXL>
+__global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_8)) void ldpc_decode_pk4_kernel(
+    const dec_desc* __restrict__ descs,
+    const int8_t* __restrict__ llrs,
+    uint8_t* __restrict__ out,
+    int32_t* __restrict__ results,
+    const uint32_t* __restrict__ ab_table,
+    const uint32_t* __restrict__ crc_tables,
+    uint8_t* __restrict__ cb_crc_ok)
+{
+  using G = bg_t<BG>;
+  static_assert(MAXL >= 4 && MAXL <= 16, "PK4: 8- and 16-layer classes (the 16-bit pair addresses and the LDS image)");
+  constexpr int NCOL = G::K + MAXL;
+  __shared__ __attribute__((aligned(16))) int8_t smem[NCOL * PK4_CS + PK4_SCRATCH_INTS * sizeof(int)];
+  int8_t* soft  = smem;
+  int*    wlast = reinterpret_cast<int*>(smem + NCOL * PK4_CS);  // [wave]: last non-zero LLR of the slot being loaded
+  int*    red   = wlast + PK4_WAVES;                              // [parity][slot][wave][acc, zero]
+  int*    cbi   = red + PK4_RED;                                  // [slot][layers, running]
+
+  const dec_desc* wd = descs + static_cast<size_t>(blockIdx.x) * PK4;
+  // Workgroup-uniform parameters from slot 0 (the host groups codeblocks that share them).
+  const dec_desc d0 = wd[0];
+  const int      Z  = d0.Z;
+  const uint32_t H  = static_cast<uint32_t>(Z) / 2u;
+  const auto     ab = (const_u32_ptr)(uintptr_t)(ab_table + static_cast<uint32_t>(d0.zpos) * G::NE);
+  asm volatile("" ::"s"(llrs), "s"(out), "s"(results), "s"(crc_tables), "s"(cb_crc_ok), "s"(blockDim.x));
+  constexpr int AB_BYTES = G::NE * 4;
+  constexpr int AB_LINES = (AB_BYTES - 4) / 64 + 2;
+  uint32_t      pf[AB_LINES];
+  static_for<AB_LINES>([&](auto L) {
+    constexpr int l = decltype(L)::value;
+    scalar_touch<(l * 64 < AB_BYTES - 4) ? l * 64 : AB_BYTES - 4>(pf[l], ab);
+  });
+  int cnt = 1;
+#pragma unroll
+  for (int i = 1; i < PK4; ++i) {
+    cnt += (wd[i].nof_llr != 0u) ? 1 : 0;
+  }
+  const int      wave   = threadIdx.x / WAVE;
+  const int      nwaves = blockDim.x / WAVE;
+  const int      lane   = threadIdx.x % WAVE;
+  const uint32_t slot   = threadIdx.x / H;
+  const uint32_t z      = threadIdx.x - slot * H;
+  const bool     in_cb  = slot < static_cast<uint32_t>(cnt);
+  const int      msg_len = G::K * Z;
+  const bool     use_crc = d0.crc_table != NO_CRC_TABLE;
+  const bool     early   = (d0.flags & DEC_FLAG_EARLY_STOP) != 0;
+
+  // ---- per slot: HARQ skip (pusch_decoder_impl.cpp:300), LLR load, input length, layer count ----
+  for (int i = 0; i < cnt; ++i) {
+    const dec_desc d       = wd[i];
+    int            layers  = 0;
+    int            running = 0;
+    if (cb_crc_ok != nullptr && cb_crc_ok[d.cb_index] != 0) {
+      if (threadIdx.x == 0) {
+        results[d.cb_index] = 0;
+      }
+    } else {
+      int last = load_llrs_pk4<NCOL>(soft, llrs, d, static_cast<uint32_t>(i));
+      last     = wave_max(last);
+      if (lane == 0) {
+        wlast[wave] = last;
+      }
+      __syncthreads();
+      int input_size = wlast[0];
+      for (int w = 1; w < nwaves; ++w) {
+        input_size = wlast[w] > input_size ? wlast[w] : input_size;
+      }
+      input_size += 1;
+      __syncthreads();  // wlast is reused by the next slot
+      if (input_size < msg_len) {
+        // Not enough LLRs: no decoding; without CRC the output is all ones (ldpc_decoder_impl.cpp:100).
+        if (!use_crc) {
+          for (int b = threadIdx.x; b < (msg_len + 7) / 8; b += blockDim.x) {
+            out[d.out_offset + b] = 0xff;
+          }
+        }
+        if (threadIdx.x == 0) {
+          results[d.cb_index] = -1;
+        }
+      } else {
+        int cb_len = input_size + 2 * Z;
+        cb_len     = cb_len > msg_len + 4 * Z ? cb_len : msg_len + 4 * Z;
+        layers     = static_cast<int>(__umulhi(static_cast<uint32_t>(cb_len + Z - 1), d.div_magic)) - G::K;
+        if (layers > MAXL) {
+          // The host bound is derived from the same input length: cannot happen; fail loudly.
+          if (threadIdx.x == 0) {
+            results[d.cb_index] = -2;
+          }
+          layers = 0;
+        } else {
+          running = 1;
+        }
+      }
+    }
+    if (threadIdx.x == 0) {
+      cbi[2 * i]     = layers;
+      cbi[2 * i + 1] = running;
+    }
+  }
+  __syncthreads();
+  static_for<AB_LINES>([&](auto L) { keep_sgpr(pf[decltype(L)::value]); });
+  int nl_max = 0;
+  for (int i = 0; i < cnt; ++i) {
+    nl_max = (cbi[2 * i + 1] != 0 && cbi[2 * i] > nl_max) ? cbi[2 * i] : nl_max;
+  }
+  nl_max            = __builtin_amdgcn_readfirstlane(nl_max);
+  // Per-lane loop state in one VGPR: the lane constant u = 2 PK4 z + 2 slot (bits 0-15; z and slot are recovered from
+  // it) and the lane's layer count while its codeblock runs (bits 16+; 0 once it stopped, or for lanes without a
+  // codeblock): "layer m runs" is one compare, lane >= (m + 1) << 16.
+  uint32_t lane_st = (2u * PK4 * z + 2u * slot) |
+                     (static_cast<uint32_t>((in_cb && cbi[2 * slot + 1] != 0) ? cbi[2 * slot] : 0) << 16);
+  int      running = __syncthreads_or(lane_st >= (1u << 16) ? 1 : 0);
+
+  scale_t sc;
+  sc.hi = uu(static_cast<int>(d0.sf16 >> 8));
+  sc.lo = uu(static_cast<int>(d0.sf16 & 255u));
+  sc.sf = d0.sf;
+  uint32_t magw[MAXL], sgw[MAXL];
+  uint32_t hiw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int m = 0; m < MAXL; ++m) {
+    magw[m] = 0;
+    sgw[m]  = 0;
+  }
+  const int max_iter = d0.max_iter;
+  int       it       = 0;
+  for (; it < max_iter && running != 0; ++it) {
+    int           nl   = nl_max;
+    uint32_t      z2x2 = 0x00010001u * (lane_st & 0xffffu);
+    const_u32_ptr abi  = ab;
+    asm volatile("" : "+s"(nl));
+    asm volatile("" : "+v"(z2x2));
+    asm volatile("" : "+s"(abi));
+    static_for<MAXL>([&](auto Mi) {
+      constexpr int m = decltype(Mi)::value;
+      if (m < nl) {
+        if (lane_st >= static_cast<uint32_t>(m + 1) << 16) {
+          __builtin_amdgcn_sched_barrier(0);
+          row_update_pk<BG, MODE, m, (MAXL <= LDPC_PK_KEEP_ADDR_MAXL), PK4_CS>(soft, abi, z2x2, sc, magw[m], sgw[m],
+                                                                              hiw[m & 3]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();
+      }
+    });
+
+    // CRC after every iteration with early stop (ldpc_decoder_impl.cpp:133), else after the last one; per slot.
+    if (use_crc && (early || it == max_iter - 1)) {
+      uint32_t       acc = 0, zero = 0;
+      const bool     run = lane_st >= (1u << 16);
+      const uint32_t ub  = lane_st & 0xffffu;
+      const uint32_t lz = ub / (2u * PK4), ls = (ub / 2u) % PK4;  // z, slot
+      if (run) {
+        const dec_desc* md       = wd + ls;
+        const uint32_t* table    = crc_tables + md->crc_table;
+        const uint32_t  last_bit = static_cast<uint32_t>(md->nof_significant) - 1u;
+        uint32_t        zz = lz, ZZ = static_cast<uint32_t>(Z), HH = H;
+        asm volatile("" : "+v"(zz));
+        asm volatile("" : "+s"(ZZ), "+s"(HH));
+        uint32_t      ia   = zz;
+        const int8_t* scol = soft + ub;
+        static_for<G::K>([&](auto Ci) {
+          constexpr int  c  = decltype(Ci)::value;
+          const uint32_t ib = ia + HH;
+          const int      sa = scol[c * PK4_CS];
+          const int      sb = scol[c * PK4_CS + 1];
+          zero |= static_cast<uint32_t>(sa == 0) | static_cast<uint32_t>(sb == 0);
+          const uint32_t ta = table[ia < last_bit ? ia : last_bit];
+          const uint32_t tb = table[ib < last_bit ? ib : last_bit];
+          acc ^= (sa <= 0 && ia <= last_bit) ? ta : 0u;
+          acc ^= (sb <= 0 && ib <= last_bit) ? tb : 0u;
+          ia += ZZ;
+          if constexpr (c % CRC_CHUNK == CRC_CHUNK - 1) {
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        });
+      }
+      int* r = red + (it & 1) * (PK4 * PK4_WAVES * 2);
+      static_for<PK4>([&](auto J) {
+        constexpr uint32_t j  = decltype(J)::value;
+        const bool         mine = run && ls == j;
+        const uint32_t     a    = wave_xor(mine ? acc : 0u);
+        const uint32_t     zr   = (__ballot(mine && zero != 0) != 0) ? 1u : 0u;
+        if (lane == 0) {
+          r[(j * PK4_WAVES + wave) * 2]     = static_cast<int>(a);
+          r[(j * PK4_WAVES + wave) * 2 + 1] = static_cast<int>(zr);
+        }
+      });
+      __syncthreads();
+      if (run) {
+        uint32_t tacc = 0, tzero = 0;
+        for (int w = 0; w < nwaves; ++w) {
+          tacc ^= static_cast<uint32_t>(r[(ls * PK4_WAVES + w) * 2]);
+          tzero |= static_cast<uint32_t>(r[(ls * PK4_WAVES + w) * 2 + 1]);
+        }
+        if ((tzero == 0 || !early) && tacc == 0) {
+          const dec_desc* md = wd + ls;
+          write_hard_bits_pk4(soft, out + md->out_offset, msg_len, Z, d0.div_magic, ls, lz);
+          if (lz == 0) {
+            results[md->cb_index] = it + 1;
+            if (cb_crc_ok != nullptr) {
+              cb_crc_ok[md->cb_index] = 1;
+            }
+          }
+          lane_st = ub;
+        }
+      }
+    }
+    running = __syncthreads_or(lane_st >= (1u << 16) ? 1 : 0);
+  }
+  if (lane_st >= (1u << 16)) {
+    const uint32_t  ub = lane_st & 0xffffu;
+    const uint32_t  lz = ub / (2u * PK4), ls = (ub / 2u) % PK4;
+    const dec_desc* md = wd + ls;
+    write_hard_bits_pk4(soft, out + md->out_offset, msg_len, Z, d0.div_magic, ls, lz);
+    if (lz == 0) {
+      results[md->cb_index] = -1;
+    }
+  }
+}
+
 } // namespace
 
 #ifdef LDPC_DEC_PROFILE
@@ -801,6 +1186,43 @@ void launch_ldpc_decode_pk(int             bg,
     }
   }
 #undef SRSGPU_PK_LAUNCH
+}
+
+void launch_ldpc_decode_pk4(int             bg,
+                            int             mode,
+                            int             max_layers,
+                            const dec_desc* d_desc,
+                            int             nof_groups,
+                            int             block_threads,
+                            const int8_t*   d_llrs,
+                            uint8_t*        d_out,
+                            int32_t*        d_results,
+                            const uint32_t* d_ab4,
+                            const uint32_t* d_crc_tables,
+                            uint8_t*        d_cb_crc_ok,
+                            hipStream_t     stream)
+{
+  if (nof_groups <= 0) {
+    return;
+  }
+  dim3 grid(nof_groups), block(block_threads);
+#define SRSGPU_PK4_LAUNCH(BG_, MODE_, MAXL_)                                                                           \
+  ldpc_decode_pk4_kernel<BG_, MODE_, MAXL_><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab4,       \
+                                                                        d_crc_tables, d_cb_crc_ok)
+  if (bg == 1) {
+    if (max_layers <= 8) {
+      mode == 1 ? SRSGPU_PK4_LAUNCH(1, 1, 8) : SRSGPU_PK4_LAUNCH(1, 0, 8);
+    } else {
+      mode == 1 ? SRSGPU_PK4_LAUNCH(1, 1, 16) : SRSGPU_PK4_LAUNCH(1, 0, 16);
+    }
+  } else {
+    if (max_layers <= 8) {
+      mode == 1 ? SRSGPU_PK4_LAUNCH(2, 1, 8) : SRSGPU_PK4_LAUNCH(2, 0, 8);
+    } else {
+      mode == 1 ? SRSGPU_PK4_LAUNCH(2, 1, 16) : SRSGPU_PK4_LAUNCH(2, 0, 16);
+    }
+  }
+#undef SRSGPU_PK4_LAUNCH
 }
 
 } // namespace srsgpu

@@ -202,6 +202,26 @@ void launch_ldpc_decode_pk(int             bg,
                            uint8_t*        d_cb_crc_ok,
                            hipStream_t     stream);
 
+/// Codeblocks per workgroup of the multi-codeblock packed decoder (ldpc_decode_pk4_kernel).
+constexpr int LDPC_PK4 = 4;
+
+/// Launches the multi-codeblock packed decoder: workgroup w decodes d_desc[LDPC_PK4 * w + i] (slots with nof_llr = 0
+/// are empty; the slots of a workgroup share Z, scaling, iteration limit and CRC mode), codeblock slot i on lanes
+/// [i Z / 2, (i + 1) Z / 2), block_threads >= (used slots) x Z / 2. d_ab4: the interleaved-image pair constants.
+void launch_ldpc_decode_pk4(int             bg,
+                            int             mode,
+                            int             max_layers,
+                            const dec_desc* d_desc,
+                            int             nof_groups,
+                            int             block_threads,
+                            const int8_t*   d_llrs,
+                            uint8_t*        d_out,
+                            int32_t*        d_results,
+                            const uint32_t* d_ab4,
+                            const uint32_t* d_crc_tables,
+                            uint8_t*        d_cb_crc_ok,
+                            hipStream_t     stream);
+
 /// Launches the batched LDPC decoder (ldpc_decoder.hip).
 void launch_ldpc_decode(int                bg,
                         int                mode,

@@ -3,13 +3,15 @@
 North star (BASELINE.json): "code blocks / UE allocations within a slot batch shard naturally across the 8 GPUs of
 one node with an RCCL-over-xGMI gather of decoded TBs back to the FAPI adaptor". One process per GPU:
 
-* every rank runs the whole PDSCH/PUSCH channel-coding pipeline on its own share of the batch (cells, or the UE
-  allocations of a slot) - codeblocks never cross GPUs, so the data path has no collective;
-* the only exchange is the uplink result: the decoded transport blocks and their CRC flags of every rank go to the
-  rank that hosts the FAPI adaptor (the reference's `fapi_adaptor` PUSCH results path, one point of delivery to the
-  MAC), with one RCCL gather per batch (torch.distributed "nccl" = RCCL on ROCm; "gloo" on CPU for the tests).
-
-The downlink needs no exchange: each rank's encoded codewords go to its own radio units.
+* sharding by cell (weak scaling, the bench's default): every rank runs the whole pipeline, OFDM included, on its
+  own cells' slots - codeblocks never cross GPUs, so the data path has no collective; the only exchange is the
+  uplink result: the decoded transport blocks and their CRC flags of every rank go to the rank that hosts the FAPI
+  adaptor (the reference's `fapi_adaptor` PUSCH results path, one point of delivery to the MAC), with one RCCL gather
+  per batch (`TbGather`; torch.distributed "nccl" = RCCL on ROCm; "gloo" on CPU for the tests);
+* sharding the UEs of one cell (strong scaling): a cell's samples enter and leave on one rank, so the resource grid
+  is exchanged as well (`GridExchange`): the root's demodulated UL grid is scattered by subcarrier band to the ranks
+  that own the UEs there, and the ranks' DL grid bands are gathered into the root's grid before its OFDM modulation;
+  the decoded TBs go to the FAPI rank through `TbGather` as above.
 """
 from __future__ import annotations
 
@@ -82,3 +84,84 @@ class TbGather:
         if self.rank != self.root:
             raise ValueError("only the root holds the gathered results")
         return torch.cat(self.tbs), torch.cat(self.crc_ok)
+
+
+def ue_subcarrier_ranges(ues: Sequence, world: int) -> List[tuple]:
+    """Subcarrier range [begin, end) of every rank's UE share (contiguous shard_ues shares of contiguous PRB
+    allocations starting at PRB 0): the grid columns a rank's UEs occupy."""
+    if world <= 0:
+        raise ValueError("invalid world")
+    out, rb = [], 0
+    for r in range(world):
+        n = sum(ues[i].n_prb for i in shard_range(len(ues), world, r))
+        out.append((12 * rb, 12 * (rb + n)))
+        rb += n
+    return out
+
+
+class GridExchange:
+    """The resource-grid exchange of a cell whose UEs are split across ranks (strong scaling, `--shard ues`).
+
+    The cell's radio samples enter and leave on one rank, the root (it hosts the cell's radio unit link): the root runs
+    the OFDM demodulation / modulation of the whole cell, the other ranks only the upper PHY of their UEs. Uplink: the
+    root's demodulated grid is cut into the ranks' subcarrier ranges and scattered (`scatter`); each rank writes its
+    range into its own full-width grid, where its UEs' estimator / demodulator plans read it. Downlink: every rank maps
+    its UEs into its grid and the ranges are gathered into the root's grid (`gather`) before the OFDM modulation.
+
+    The grid is [rows][nsc] int32 (rows = slots x ports x symbols, bf16 pairs), a rank's range is a column band, so a
+    transfer packs it into a dense send buffer (one strided device copy) padded to the widest band (RCCL's scatter /
+    gather move equal chunks). Per step each non-root rank moves rows x width x 4 bytes in each direction; the root
+    sends / receives the sum over the others. Buffers are allocated once; all copies and collectives run on the current
+    stream (graph-capturable with RCCL).
+    """
+
+    def __init__(self, rows: int, nsc: int, sc_ranges: Sequence[tuple], device: torch.device, root: int = 0,
+                 group: Optional[dist.ProcessGroup] = None):
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if len(sc_ranges) != self.world:
+            raise ValueError("one subcarrier range per rank")
+        for b, e in sc_ranges:
+            if not 0 <= b <= e <= nsc:
+                raise ValueError(f"subcarrier range [{b}, {e}) outside the grid's {nsc}")
+        self.rows, self.nsc, self.root, self.group = int(rows), int(nsc), root, group
+        self.ranges = [(int(b), int(e)) for b, e in sc_ranges]
+        self.width = max(e - b for b, e in self.ranges)
+        self._mine = torch.zeros(self.rows, self.width, dtype=torch.int32, device=device)
+        self._all = ([torch.zeros(self.rows, self.width, dtype=torch.int32, device=device) for _ in range(self.world)]
+                     if self.rank == root else None)
+
+    @property
+    def bytes_per_rank(self) -> List[int]:
+        """Grid bytes of every rank's band (what one scatter or gather moves to / from that rank)."""
+        return [self.rows * (e - b) * 4 for b, e in self.ranges]
+
+    def _grid2d(self, d_grid: torch.Tensor) -> torch.Tensor:
+        if d_grid.dtype != torch.int32 or d_grid.numel() != self.rows * self.nsc:
+            raise ValueError(f"grid of {d_grid.numel()} {d_grid.dtype} words, the exchange was planned for "
+                             f"{self.rows} x {self.nsc} int32")
+        return d_grid.view(self.rows, self.nsc)
+
+    def scatter(self, d_grid: torch.Tensor) -> None:
+        """Uplink: the root's bands of `d_grid` go to their ranks' `d_grid` (same columns)."""
+        g = self._grid2d(d_grid)
+        if self.rank == self.root:
+            for r, (b, e) in enumerate(self.ranges):
+                if r != self.root:
+                    self._all[r][:, : e - b].copy_(g[:, b:e])
+        dist.scatter(self._mine, self._all, src=self.root, group=self.group)
+        if self.rank != self.root:
+            b, e = self.ranges[self.rank]
+            g[:, b:e].copy_(self._mine[:, : e - b])
+
+    def gather(self, d_grid: torch.Tensor) -> None:
+        """Downlink: every rank's band of its `d_grid` goes into the root's `d_grid` (same columns)."""
+        g = self._grid2d(d_grid)
+        b, e = self.ranges[self.rank]
+        if self.rank != self.root:
+            self._mine[:, : e - b].copy_(g[:, b:e])
+        dist.gather(self._mine, self._all, dst=self.root, group=self.group)
+        if self.rank == self.root:
+            for r, (b, e) in enumerate(self.ranges):
+                if r != self.root:
+                    g[:, b:e].copy_(self._all[r][:, : e - b])

@@ -162,26 +162,30 @@ class DownlinkGroup:
     def __init__(self, pipes: Sequence[DownlinkPipeline], d_tbs: Sequence, fresh_tbs=False):
         self.pipes, self.d_tbs, self.fresh_tbs = list(pipes), list(d_tbs), fresh_tbs
 
-    def execute(self, stream, events=None):
-        if self.fresh_tbs:
-            with torch.cuda.stream(stream):
-                for t in self.d_tbs:
-                    if t.numel() % 8 == 0:  # 8 payload bytes per Philox draw (the top bit of each word stays 0)
-                        t.view(torch.int64).random_()
-                    else:
-                        t.random_(0, 256)
+    def execute(self, stream, events=None, upper=True, ofdm=True):
+        """upper: TB draw, encoding, DM-RS and modulation into the grids; ofdm: the grids' OFDM modulation. A
+        UE-sharded cell runs the two parts on different ranks with the grid gather in between (srsgpu.dist)."""
         rec = (lambda i: events[i].record(stream)) if events else (lambda i: None)
-        rec(0)
-        for p, t in zip(self.pipes, self.d_tbs):
-            p.encoder.execute(t, p.d_cw, stream)
-        rec(1)
-        for p in self.pipes:
-            p.dmrs.execute(p.d_grid, stream)
-            p.modulator.execute(p.d_cw, p.d_grid, stream)
-        rec(2)
-        for p in self.pipes:
-            p.ofdm.execute(p.d_grid, p.d_samples, stream)
-        rec(3)
+        if upper:
+            if self.fresh_tbs:
+                with torch.cuda.stream(stream):
+                    for t in self.d_tbs:
+                        if t.numel() % 8 == 0:  # 8 payload bytes per Philox draw (the top bit of each word stays 0)
+                            t.view(torch.int64).random_()
+                        else:
+                            t.random_(0, 256)
+            rec(0)
+            for p, t in zip(self.pipes, self.d_tbs):
+                p.encoder.execute(t, p.d_cw, stream)
+            rec(1)
+            for p in self.pipes:
+                p.dmrs.execute(p.d_grid, stream)
+                p.modulator.execute(p.d_cw, p.d_grid, stream)
+            rec(2)
+        if ofdm:
+            for p in self.pipes:
+                p.ofdm.execute(p.d_grid, p.d_samples, stream)
+            rec(3)
 
 
 class UplinkPipeline:
@@ -242,11 +246,16 @@ class UplinkPipeline:
         self.d_tbs = torch.zeros(tb_total, dtype=torch.uint8, device=dev)
         self.d_tb_ok = torch.zeros(self.nof_tbs, dtype=torch.uint8, device=dev)
 
-    def execute(self, d_samples, stream, events=None):
+    def execute(self, d_samples, stream, events=None, ofdm=True, upper=True):
+        """ofdm: the OFDM demodulation of `d_samples` into the grid; upper: estimation, demodulation and decoding of
+        the grid. A UE-sharded cell runs the two parts on different ranks with the grid scatter in between."""
         rec = (lambda i: events[i].record(stream)) if events else (lambda i: None)
         rec(0)
-        self.ofdm.execute(d_samples, self.d_grid, stream)
+        if ofdm:
+            self.ofdm.execute(d_samples, self.d_grid, stream)
         rec(1)
+        if not upper:
+            return
         self.chest.execute(self.d_grid, self.d_ce, self.d_nv, self.d_metrics, stream)
         rec(2)
         self.demod.execute(self.d_grid, self.d_ce, self.d_nv, self.d_llrs, stream)

@@ -143,3 +143,182 @@ def test_ue_sharded_slot_gather_gloo(world):
     want_ok = np.array([(i * 7) % 3 != 0 for i in range(len(ues))], np.uint8)
     assert np.array_equal(tbs, want_tbs) and np.array_equal(ok, want_ok)
     assert len(set(sizes)) > 1 or world == 1  # the ranks' TB sizes differ: the padding path ran
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# UE-sharded cell with real grid buffers (GridExchange): the root holds the cell's demodulated UL grid and scatters
+# the ranks' subcarrier bands; each rank decodes its UEs' transport blocks from its band (oracle receive chain:
+# QPSK hard LLRs -> rate dematching -> LDPC -> TB CRC) and the TBs are gathered to the root. Downlink: every rank maps
+# its UEs' TBs into its band and the bands are gathered into the root's grid. Both are compared with one rank doing
+# the whole cell.
+# ---------------------------------------------------------------------------------------------------------------------
+X_SLOTS, X_PORTS, X_UES, X_PRB = 2, 2, 6, 26  # 26 PRB over 6 UEs: 5, 5, 4, 4, 4, 4 (uneven bands)
+QPSK_POS, QPSK_NEG = 0x3F35, 0xBF35           # bf16 of +-1/sqrt(2)
+
+
+def _x_ues():
+    base, extra = divmod(X_PRB, X_UES)
+    return [sch.UeGrant(base + (1 if i < extra else 0), 1, 2, 512.0, nof_dmrs_symbols=0) for i in range(X_UES)]
+
+
+def _x_tbs(ues, direction):
+    """TB bytes of every (slot, UE): the same on every rank (seeded)."""
+    rng = np.random.default_rng(11 + direction)
+    return [[rng.integers(0, 256, u.segmentation().tbs // 8, dtype=np.uint8) for u in ues] for _ in range(X_SLOTS)]
+
+
+def _x_map(orc, ues, tbs, ue_ids, grid):
+    """Encodes the TBs of UEs `ue_ids` (oracle PDSCH encoder chain) and maps them as QPSK into their PRBs of `grid`
+    (rows = slot x port x symbol, every port the same symbols), subcarrier-major within a symbol."""
+    from chain_lib import oracle_pdsch_encode
+    rb0 = np.concatenate([[0], np.cumsum([u.n_prb for u in ues])])
+    for s in range(X_SLOTS):
+        for i in ue_ids:
+            u = ues[i]
+            cw, _, _ = oracle_pdsch_encode(orc, tbs[s][i], u.segmentation().base_graph, 0, 2, 1, 0, u.nof_ch_symbols)
+            pairs = cw.reshape(-1, 2)
+            re = np.where(pairs[:, 0] == 0, QPSK_POS, QPSK_NEG).astype(np.uint32)
+            im = np.where(pairs[:, 1] == 0, QPSK_POS, QPSK_NEG).astype(np.uint32)
+            words = (re | (im << 16)).view(np.int32).reshape(14, 12 * u.n_prb)
+            for p in range(X_PORTS):
+                r0 = (s * X_PORTS + p) * 14
+                grid[r0:r0 + 14, 12 * rb0[i]:12 * rb0[i + 1]] = words
+
+
+def _x_decode(orc, ues, ue_ids, grid):
+    """Decodes the TBs of UEs `ue_ids` from `grid`: hard LLRs (+-8) from the sign of the ports' summed real / imaginary
+    parts, then per codeblock the oracle rate dematcher and LDPC decoder, TB reassembly and TB CRC. Returns (TB bytes
+    in [slot][ue] order, CRC flags)."""
+    from chain_lib import crc_for_tb
+    from oracle_lib import CRC16, CRC24A
+    rb0 = np.concatenate([[0], np.cumsum([u.n_prb for u in ues])])
+    out, ok = [], []
+    for s in range(X_SLOTS):
+        for i in ue_ids:
+            u, seg = ues[i], ues[i].segmentation()
+            acc = np.zeros((14, 12 * u.n_prb, 2))
+            for p in range(X_PORTS):
+                r0 = (s * X_PORTS + p) * 14
+                w = grid[r0:r0 + 14, 12 * rb0[i]:12 * rb0[i + 1]].view(np.uint32)
+                for h in range(2):
+                    half = ((w >> (16 * h)) & 0xFFFF).astype(np.uint16)
+                    acc[..., h] += np.where(half >> 15, -1.0, 1.0)
+            llr = np.where(acc.reshape(-1) >= 0, 8, -8).astype(np.int8)
+            poly = crc_for_tb(seg)
+            payload = []
+            for cb in seg.codeblocks:
+                Z = seg.lifting_size
+                buf = np.zeros(({1: 66, 2: 50}[seg.base_graph]) * Z, np.int8)
+                buf = orc.rate_dematch(1, seg.base_graph, Z, 0, 2, 0, cb.nof_filler_bits, 1,
+                                       llr[cb.cw_offset:cb.cw_offset + cb.rm_length], buf)
+                _, bits = orc.ldpc_decode(1, seg.base_graph, Z, buf, nof_crc_bits=cb.nof_crc_bits,
+                                          nof_filler=cb.nof_filler_bits, crc_poly=poly, max_iter=6)
+                last = cb.index == seg.nof_segments - 1
+                payload.append(bits[:cb.nof_info_bits + (seg.nof_tb_crc_bits if last else 0)])
+            payload = np.concatenate(payload)
+            tb_poly = CRC16 if seg.tbs <= 3824 else CRC24A
+            ok.append(int(orc.crc_bits(tb_poly, payload) == 0))
+            out.append(np.packbits(payload[:seg.tbs]))
+    return out, np.array(ok, np.uint8)
+
+
+def _x_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from oracle_lib import Oracle
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        orc = Oracle()
+        ues = _x_ues()
+        mine = list(sdist.shard_range(len(ues), world, rank))
+        rows, nsc = X_SLOTS * X_PORTS * 14, 12 * X_PRB
+        x = sdist.GridExchange(rows, nsc, sdist.ue_subcarrier_ranges(ues, world), torch.device("cpu"), root=0)
+        # Uplink: only the root has the cell's grid (its OFDM demodulator's output); the others start from zeros.
+        ul = np.zeros((rows, nsc), np.int32)
+        if rank == 0:
+            _x_map(orc, ues, _x_tbs(ues, 0), range(len(ues)), ul)
+        ul_t = torch.from_numpy(ul)
+        x.scatter(ul_t.view(-1))
+        tbs, ok = _x_decode(orc, ues, mine, ul_t.numpy())
+        g = sdist.TbGather(sum(t.size for t in tbs), ok.size, torch.device("cpu"), root=0)
+        g.gather(torch.from_numpy(np.concatenate(tbs)), torch.from_numpy(ok))
+        # Downlink: every rank maps its own UEs; the bands meet in the root's grid.
+        dl = np.zeros((rows, nsc), np.int32)
+        _x_map(orc, ues, _x_tbs(ues, 1), mine, dl)
+        dl_t = torch.from_numpy(dl)
+        x.gather(dl_t.view(-1))
+        res = None
+        if rank == 0:
+            all_tbs, all_ok = g.assemble()
+            res = (all_tbs.numpy().copy(), all_ok.numpy().copy(), dl_t.numpy().copy(), x.bytes_per_rank)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, None, traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ue_sharded_cell_grid_exchange_gloo(world):
+    """Real grid buffers through GridExchange (UL scatter, DL gather) and real decoded TBs through TbGather equal a
+    one-rank run of the whole cell."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_x_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, res, err = q.get(timeout=300)
+        assert err is None, err
+        out[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    tbs, ok, dl_grid, nbytes = out[0]
+    # One rank, whole cell.
+    orc = Oracle()
+    ues = _x_ues()
+    rows, nsc = X_SLOTS * X_PORTS * 14, 12 * X_PRB
+    ul = np.zeros((rows, nsc), np.int32)
+    sent = _x_tbs(ues, 0)
+    _x_map(orc, ues, sent, range(len(ues)), ul)
+    ref_tbs, ref_ok = _x_decode(orc, ues, range(len(ues)), ul)
+    assert ref_ok.all()
+    for s in range(X_SLOTS):
+        for i in range(len(ues)):
+            assert np.array_equal(ref_tbs[s * len(ues) + i], sent[s][i])
+    # Gathered order: rank-major, then [slot][UE of the rank]; reorder to [slot][UE].
+    pos, got, got_ok = 0, {}, {}
+    for r in range(world):
+        rng_r = list(sdist.shard_range(len(ues), world, r))
+        for s in range(X_SLOTS):
+            for i in rng_r:
+                n = ues[i].segmentation().tbs // 8
+                got[(s, i)] = tbs[pos:pos + n]
+                pos += n
+        k = 0
+        for s in range(X_SLOTS):
+            for i in rng_r:
+                got_ok[(s, i)] = ok[sum(len(list(sdist.shard_range(len(ues), world, rr))) * X_SLOTS
+                                        for rr in range(r)) + k]
+                k += 1
+    assert pos == tbs.size
+    for s in range(X_SLOTS):
+        for i in range(len(ues)):
+            assert np.array_equal(got[(s, i)], ref_tbs[s * len(ues) + i])
+            assert got_ok[(s, i)] == 1
+    dl_ref = np.zeros((rows, nsc), np.int32)
+    _x_map(orc, ues, _x_tbs(ues, 1), range(len(ues)), dl_ref)
+    assert np.array_equal(dl_grid, dl_ref)
+    assert sum(nbytes) == rows * nsc * 4
+
+
+def test_grid_exchange_rejects_bad_plans():
+    with pytest.raises(ValueError):
+        sdist.ue_subcarrier_ranges(_x_ues(), 0)

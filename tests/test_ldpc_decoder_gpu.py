@@ -19,6 +19,20 @@ def ctx():
     return srsgpu.Context(0)
 
 
+# Kernel variants of the packed (even Z) decoder, forced through the plan's A/B switches (capi.cpp): the
+# one-codeblock kernel, its edge-split variant and the multi-codeblock workgroups (PK4, 8- and 16-layer classes).
+VARIANTS = {"plain": {"SRSGPU_DECODER_SPLIT": "0", "SRSGPU_DECODER_PK4": "0"},
+            "split": {"SRSGPU_DECODER_SPLIT": "1", "SRSGPU_DECODER_PK4": "0"},
+            "pk4": {"SRSGPU_DECODER_SPLIT": "0", "SRSGPU_DECODER_PK4": "1"}}
+
+
+@pytest.fixture(params=sorted(VARIANTS))
+def variant(request, monkeypatch):
+    for k, v in VARIANTS[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
 def _case(orc, rng, bg, Z, trial):
     K, N = BG_K[bg], BG_N_SHORT[bg]
     noise = [0.0, 5.0, 8.0, 11.0, 16.0][trial % 5]
@@ -33,7 +47,7 @@ def _case(orc, rng, bg, Z, trial):
 
 
 @pytest.mark.parametrize("dec_type,mode", [("avx2", 1), ("generic", 0)])
-def test_decoder_all_lifting_sizes_batched(orc, ctx, dec_type, mode):
+def test_decoder_all_lifting_sizes_batched(orc, ctx, dec_type, mode, variant):
     """Every lifting size of both base graphs, mixed in ONE batch (one launch per base graph)."""
     import srsgpu
     rng = np.random.default_rng(2024 + mode)
@@ -61,7 +75,7 @@ def test_decoder_all_lifting_sizes_batched(orc, ctx, dec_type, mode):
     assert n_success > len(want) // 3  # the batch exercises both early stops and failures
 
 
-def test_decoder_bg1_z384_full_batch(orc, ctx):
+def test_decoder_bg1_z384_full_batch(orc, ctx, variant):
     """The benchmark shape (BG1, Z = 384): 256 codeblocks, several SNRs, 8 iterations with CRC24B early stop."""
     import srsgpu
     rng = np.random.default_rng(99)
@@ -80,7 +94,7 @@ def test_decoder_bg1_z384_full_batch(orc, ctx):
         assert g[0] == w[0] and np.array_equal(g[1], w[1]), i
 
 
-def test_decoder_edge_cases(orc, ctx):
+def test_decoder_edge_cases(orc, ctx, variant):
     """Zero-tail trimming, too-short input (no decoding: all ones without CRC, untouched output with CRC), random
     +/-10 LLRs (the reference benchmark input) and scaling factors near the limits."""
     import srsgpu
@@ -129,7 +143,7 @@ def test_decoder_rejects_invalid_configs(ctx):
         dec.decode(np.ones(66 * 16, np.int8), srsgpu.CodeblockDecodeConfig(1, 16, scaling_factor=1.0))
 
 
-def test_decoder_golden_vectors(ctx):
+def test_decoder_golden_vectors(ctx, variant):
     """The GPU decoder against the reference's own outputs (tests/golden/ldpc_decoder.npz), every case in one batch
     per arithmetic variant."""
     import golden_lib as G
@@ -145,3 +159,44 @@ def test_decoder_golden_vectors(ctx):
         for c, (r, bits) in zip(sel, got):
             assert (r if r is not None else -1) == c["iters"], (c["bg"], c["Z"])
             assert np.array_equal(bits, c["bits"])
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+def test_decoder_pk4_mixed_workgroups(orc, ctx, mode, monkeypatch):
+    """Multi-codeblock workgroups with everything that differs between the slots of one workgroup: codeblocks that
+    stop at different iterations or never, different layer counts (input lengths, trailing zeros), too-short inputs,
+    mixed CRC polynomials and filler lengths, and lifting sizes whose slots straddle waves (Z = 288 / 352 / 208 / 96).
+    Against the oracle, bit-exact."""
+    import srsgpu
+    monkeypatch.setenv("SRSGPU_DECODER_SPLIT", "0")
+    monkeypatch.setenv("SRSGPU_DECODER_PK4", "1")
+    rng = np.random.default_rng(77 + mode)
+    dec = srsgpu.LdpcDecoder(ctx, "avx2" if mode == 1 else "generic")
+    llrs, cfgs, polys, want = [], [], [], []
+    for bg, Z in ((1, 288), (1, 352), (1, 208), (2, 96), (1, 64)):
+        K = BG_K[bg]
+        for i in range(23):
+            crc_poly = [CRC24B, CRC16, CRC24A][i % 3]
+            nof_filler = 0 if i % 4 else min(Z, (K - 2) * Z // 7)
+            n_nodes = K + 2 + int(rng.integers(1, 15))  # 8- and 16-layer classes
+            _, _, llr = encode_with_llrs(orc, rng, bg, Z, crc_poly=crc_poly, nof_filler=nof_filler, amp=10,
+                                         noise=[3.0, 6.0, 9.0, 12.0, 14.0][i % 5], n_llr=n_nodes * Z)
+            if i % 7 == 3:
+                llr[(n_nodes - 1) * Z:] = 0  # a trailing zero column: one layer fewer than the host bound
+            if i % 11 == 5:
+                llr[K * Z - 3:] = 0          # too short: no decoding
+            cfg = srsgpu.CodeblockDecodeConfig(bg, Z, nof_crc_bits=16 if crc_poly == CRC16 else 24,
+                                               nof_filler_bits=nof_filler, max_iterations=6)
+            llrs.append(llr)
+            cfgs.append(cfg)
+            polys.append(crc_poly)
+            r, bits = orc.ldpc_decode(mode, bg, Z, llr, nof_crc_bits=cfg.nof_crc_bits, nof_filler=nof_filler,
+                                      crc_poly=crc_poly, max_iter=6, scaling=0.8)
+            want.append((None if r < 0 else r, bits))
+    got = dec.decode_batch(llrs, cfgs, polys)
+    its = set()
+    for i, ((r_g, b_g), (r_w, b_w)) in enumerate(zip(got, want)):
+        assert r_g == r_w, (i, r_g, r_w)
+        assert np.array_equal(b_g, b_w), i
+        its.add(r_w)
+    assert None in its and len(its) >= 4  # failures and several stop iterations within the batch

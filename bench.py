@@ -38,8 +38,9 @@ Workloads (--workload):
 
 Weak scaling (--shard cells): every rank processes its own cells' slots; the decoded UL TBs + CRC flags of all ranks are
 gathered to rank 0 (the FAPI rank) over RCCL once per step. Strong scaling (--shard ues): the 64 UEs of every slot are
-split across the ranks (srsgpu.dist.shard_ues); each rank runs the upper PHY of its UEs (the OFDM stages of the cell
-stay on every rank) and the TBs are gathered the same way. One JSON line from rank 0.
+split across the ranks (srsgpu.dist.shard_ues); rank 0 holds the cell's samples and runs its OFDM stages, the resource
+grids are exchanged by subcarrier band (srsgpu.dist.GridExchange), each rank runs the upper PHY of its UEs, and the TBs
+are gathered the same way. One JSON line from rank 0.
 """
 import argparse
 import ctypes
@@ -215,6 +216,7 @@ class InputSet:
                                        dtype=torch.uint8)
         self.samples = torch.zeros(2 * self.ul.ofdm.nof_samples, dtype=torch.float32, device=dev)
         self.graph = None
+        self.graph_back = None  # UE-sharded cell: the part after the grid exchange
 
 
 def parse_args(argv=None):
@@ -253,6 +255,9 @@ def parse_args(argv=None):
                     help="replay each input set on its own stream (up to --input-sets steps in flight)")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
                     help="replay each set's DL+UL pipeline as one captured HIP graph (default) or launch eagerly")
+    ap.add_argument("--graph-collectives", action="store_true",
+                    help="N > 1: capture the RCCL exchanges (TB gather; grid exchange with --shard ues) inside the "
+                         "step's graph instead of issuing them between graph launches")
     return ap.parse_args(argv)
 
 
@@ -303,11 +308,35 @@ def measure(args, env):
     S_ul = ul_cell.nof_slots
     S_dl = sum(c.nof_slots for c in dl_cells)
     sets = [InputSet(ctx, dl_cells, ul_cell, prof, args.iterations, gen, dev, fresh_tbs=testmode) for _ in range(K)]
+    # UE-sharded cell (strong scaling): the cell's samples enter and leave on rank 0, which runs the OFDM stages of the
+    # whole cell; the resource grids are exchanged by subcarrier band (srsgpu.dist.GridExchange: UL scatter after the
+    # OFDM demodulation, DL gather before the OFDM modulation). Rank 0 synthesises the whole cell's UL from the TBs of
+    # all UEs (drawn identically on every rank); each rank checks its own UEs' decoded TBs.
+    shard_x = args.shard == "ues" and world > 1
+    if shard_x:
+        from srsgpu import dist as sdist
+        full_ul_cell = slotlib.CellSlots(ul_all, [u.segmentation() for u in ul_all], S, dmrs_mask=DMRS_MASK)
+        full_bytes = [s.tbs // 8 for s in full_ul_cell.segs]
+        mine = sdist.shard_range(len(ul_all), world, rank)
+        off0, n_r, tot = sum(full_bytes[:mine.start]), sum(full_bytes[mine.start:mine.stop]), sum(full_bytes)
+        for k, st in enumerate(sets):
+            g_all = torch.Generator(device=dev)
+            g_all.manual_seed(777 + k)
+            st.full_ul_tbs = torch.randint(0, 256, (S * tot,), generator=g_all, device=dev, dtype=torch.uint8)
+            st.ul_tbs_tx = torch.cat([st.full_ul_tbs[s * tot + off0: s * tot + off0 + n_r] for s in range(S)])
+        ranges = sdist.ue_subcarrier_ranges(ul_all, world)
+        gx_ul = sdist.GridExchange(S * ul_cell.nof_ports * 14, ul_cell.nsc, ranges, dev, root=0)
+        gx_dl = sdist.GridExchange(S * dl_cell.nof_ports * 14, dl_cell.nsc, ranges, dev, root=0)
 
     def fill_samples(snr_db, worst):
         for k, st in enumerate(sets):
+            if shard_x and rank != 0:
+                continue  # only the root rank receives the cell's samples
             if worst:
                 st.samples.copy_(torch.randn(st.samples.numel(), generator=gen, device=dev) * 0.01)
+            elif shard_x:
+                st.samples.copy_(slotlib.synthesize_uplink(ctx, full_ul_cell, st.full_ul_tbs, snr_db=snr_db,
+                                                           seed=99 + 1000 * k, cfo_hz_max=CFO_HZ_MAX))
             else:
                 st.samples.copy_(slotlib.synthesize_uplink(ctx, ul_cell, st.ul_tbs_tx, snr_db=snr_db,
                                                            seed=99 + rank + 1000 * k, cfo_hz_max=CFO_HZ_MAX))
@@ -321,15 +350,38 @@ def measure(args, env):
         from srsgpu import dist as sdist
         tb_gather = sdist.TbGather(sets[0].ul.d_tbs.numel(), sets[0].ul.d_tb_ok.numel(), dev, root=0)
 
-    def pipeline(st, ev_dl=None, ev_ul=None):
-        """DL and UL legs of one step of input set `st`, forked from and joined back into the current stream."""
+    def pipeline(st, ev_dl=None, ev_ul=None, part="all"):
+        """DL and UL legs of one step of input set `st`, forked from and joined back into the current stream. A
+        UE-sharded cell runs it as part "front" (DL upper PHY into the grids; UL OFDM demodulation on the root),
+        the grid exchange (`exchange`) and part "back" (DL OFDM modulation on the root; UL upper PHY)."""
         cur = torch.cuda.current_stream(dev)
         dl_stream.wait_stream(cur)
         ul_stream.wait_stream(cur)
-        st.dl_group.execute(dl_stream, ev_dl)
-        st.ul.execute(st.samples, ul_stream, ev_ul)
+        root = rank == 0
+        if part == "all":
+            st.dl_group.execute(dl_stream, ev_dl)
+            st.ul.execute(st.samples, ul_stream, ev_ul)
+        elif part == "front":
+            st.dl_group.execute(dl_stream, ev_dl, upper=True, back=False)
+            st.ul.execute(st.samples, ul_stream, ev_ul, ofdm=root, upper=False)
+        else:
+            st.dl_group.execute(dl_stream, ev_dl, upper=False, ofdm=root)
+            st.ul.execute(None, ul_stream, ev_ul, upper=True, front=False)
         cur.wait_stream(dl_stream)
         cur.wait_stream(ul_stream)
+
+    def exchange(st):
+        """UE-sharded cell: the DL grid bands to the root, the root's UL grid bands to their ranks (current stream)."""
+        gx_dl.gather(st.dls[0].d_grid)
+        gx_ul.scatter(st.ul.d_grid)
+
+    def whole(st, ev_dl=None, ev_ul=None):
+        if shard_x:
+            pipeline(st, ev_dl, ev_ul, "front")
+            exchange(st)
+            pipeline(st, ev_dl, ev_ul, "back")
+        else:
+            pipeline(st, ev_dl, ev_ul)
 
     # Pipelining across steps: each input set replays on its own stream, so a step's UL decode can overlap the next
     # set's front end (different buffers; a set's consecutive steps stay ordered on its stream).
@@ -339,11 +391,15 @@ def measure(args, env):
         st = sets[i % K]
         cur = torch.cuda.current_stream(dev) if set_streams is None else set_streams[i % K]
         with torch.cuda.stream(cur):
-            if st.graph is not None:
+            if st.graph is not None and st.graph_back is not None:
+                st.graph.replay()     # front part
+                exchange(st)          # RCCL grid exchange between the captured parts
+                st.graph_back.replay()
+            elif st.graph is not None:
                 st.graph.replay()
             else:
-                pipeline(st)
-            if tb_gather is not None:
+                whole(st)
+            if tb_gather is not None and not (st.graph is not None and args.graph_collectives):
                 tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
 
     for i in range(args.warmup):
@@ -355,8 +411,20 @@ def measure(args, env):
         # thread_local: the RCCL watchdog thread of a multi-GPU run keeps polling its events during the capture.
         for st in sets:
             st.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(st.graph, capture_error_mode="thread_local"):
-                pipeline(st)
+            if shard_x and not args.graph_collectives:
+                # The collectives stay outside: the front and back parts are captured as two graphs.
+                with torch.cuda.graph(st.graph, capture_error_mode="thread_local"):
+                    pipeline(st, part="front")
+                st.graph_back = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(st.graph_back, capture_error_mode="thread_local"):
+                    pipeline(st, part="back")
+            else:
+                # --graph-collectives: the grid exchange and the TB gather are captured with the kernels (RCCL graph
+                # capture); otherwise there are no collectives in the step's kernels.
+                with torch.cuda.graph(st.graph, capture_error_mode="thread_local"):
+                    whole(st)
+                    if tb_gather is not None and args.graph_collectives:
+                        tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
         for i in range(args.warmup):
             step(i)
         torch.cuda.synchronize()
@@ -417,7 +485,7 @@ def measure(args, env):
         st.ul.decoder.enable_timing(True, decode_only=True)
     n_dec = min(steps, 400)
     for i in range(n_dec):
-        pipeline(sets[i % K])
+        whole(sets[i % K])
     torch.cuda.synchronize()
     dec_ms_tot, dec_n = 0.0, 0
     for st in sets:
@@ -432,7 +500,7 @@ def measure(args, env):
     evs = [([torch.cuda.Event(enable_timing=True) for _ in range(4)],
             [torch.cuda.Event(enable_timing=True) for _ in range(5)]) for _ in range(n_stage)]
     for i in range(n_stage):
-        pipeline(sets[i % K], *evs[i])
+        whole(sets[i % K], *evs[i])
     torch.cuda.synchronize()
     stage = {k: 0.0 for k in DL_STAGES + UL_STAGES}
     for ed, eu in evs:
@@ -564,8 +632,11 @@ def measure(args, env):
                    "decoder_arithmetic": "avx2/avx512 (SIMD) variant, bit-exact",
                    "ofdm": "4096-point DFT, 122.88 Msps, normal CP",
                    "parallelism": (f"dp{world}: each GPU processes its own cells' slots" if args.shard == "cells" else
-                                   f"ue-shard{world}: the 64 UEs of each slot split across {world} GPUs (OFDM of the "
-                                   f"cell on every rank)") + (
+                                   f"ue-shard{world}: the 64 UEs of each slot split across {world} GPUs; OFDM of the "
+                                   f"cell on rank 0, resource grids exchanged by subcarrier band over RCCL (UL scatter "
+                                   f"after the OFDM demodulation, DL gather before the OFDM modulation: "
+                                   f"{2 * sum(gx_ul.bytes_per_rank[1:]) / 2 ** 20:.1f} MB per step)"
+                                   if shard_x else "ue-shard1") + (
                                       "; decoded UL TBs + CRC flags gathered to the FAPI rank over RCCL every step"
                                       if world > 1 else "")},
         "ldpc_info_bits_per_s": info_bits_slot * S_ul * step_rate,
@@ -599,7 +670,7 @@ def measure(args, env):
         if ref_llr is not None and args.profile == "ref":  # the reference shim runs UL slot 0
             # The GPU's UL LLRs of slot 0 against the reference's on the same received samples, and both decoders'
             # codeblock CRC outcomes on slot 0 (each on its own LLRs).
-            pipeline(st0)
+            whole(st0)
             torch.cuda.synchronize()
             got = ul.d_llrs[: sum(s.cw_length for s in ul_segs)].cpu().numpy().astype(np.int16)
             d = np.abs(got - ref_llr.astype(np.int16))
@@ -613,7 +684,7 @@ def measure(args, env):
                 "cb_outcome_agreement": float(np.mean(gpu_cb_ok == (ref_iters >= 0)))}
     # Release the working sets (graphs first) before another workload is measured in the same process.
     for st in sets:
-        st.graph = None
+        st.graph = st.graph_back = None
     del sets
     torch.cuda.synchronize()
     torch.cuda.empty_cache()

@@ -592,12 +592,14 @@ double decoder_issue_cost(long active_waves, int threads, int max_layers, size_t
 
 /// Chooses whether a packed-kernel launch group runs on the multi-codeblock kernel, and its workgroup size: codeblocks
 /// sharing the workgroup-uniform parameters (Z, scaling, iteration limit, CRC mode) are packed LDPC_PK4 at a time
-/// (fewer if c Z / 2 lanes exceed the workgroup), over every workgroup size of 64..LDPC_PK4 x 192 lanes; taken when the
-/// cost model gives >= 5 % less than the one-codeblock kernel. SRSGPU_DECODER_PK4=0 / 1 forces either (A/B tests).
-bool pk4_layout_for(int bg, int max_layers, int threads1, const std::vector<dec_desc>& cbs, pk4_layout& out)
+/// (fewer if c Z / 2 lanes exceed the workgroup), over every workgroup size of 64..LDPC_PK4 x 192 lanes, the size with
+/// the lowest modelled cost.
+bool pk4_layout_for(int bg, int max_layers, const std::vector<dec_desc>& cbs, pk4_layout& out)
 {
+  // Opt-in (SRSGPU_DECODER_PK4=1) until it wins on the box: measured round 3 (profiles/r3_decoder_pk4_scaling.log, r3_decoder_pk4_bench_ab.txt), the
+  // packed workgroups do not beat the one-codeblock kernel at equal work although they issue 25 % fewer waves.
   const char* env = std::getenv("SRSGPU_DECODER_PK4");
-  if ((env != nullptr && env[0] == '0') || max_layers > 16 || cbs.empty()) {
+  if (env == nullptr || env[0] != '1' || max_layers > 16 || cbs.empty()) {
     return false;
   }
   const int K = (bg == 1) ? kBG1_K : kBG2_K;
@@ -616,9 +618,7 @@ bool pk4_layout_for(int bg, int max_layers, int threads1, const std::vector<dec_
     runs.emplace_back(i, j);
     i = j;
   }
-  const size_t lds1  = static_cast<size_t>(K + max_layers) * SOFT_COL_STRIDE + 256;
   const size_t lds4  = static_cast<size_t>(LDPC_PK4) * (K + max_layers) * SOFT_COL_STRIDE + 1024;
-  const double cost1 = decoder_issue_cost(static_cast<long>(cbs.size()) * (threads1 / 64), threads1, max_layers, lds1);
   double       best  = 1e300;
   int          best_t = 0;
   for (int t = 64; t <= LDPC_PK4 * 192; t += 64) {
@@ -643,8 +643,7 @@ bool pk4_layout_for(int bg, int max_layers, int threads1, const std::vector<dec_
       best_t = t;
     }
   }
-  const bool force = env != nullptr && env[0] == '1';
-  if (best_t == 0 || (!force && best >= 0.95 * cost1)) {
+  if (best_t == 0) {
     return false;
   }
   out.threads = best_t;
@@ -693,7 +692,7 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
     pk4_layout             pk4;
     const dec_desc*        src   = kv.second.data();
     size_t                 bytes = kv.second.size() * sizeof(dec_desc);
-    if (g.packed && g.split == 1 && pk4_layout_for(g.bg, g.max_layers, g.threads, kv.second, pk4)) {
+    if (g.packed && g.split == 1 && pk4_layout_for(g.bg, g.max_layers, kv.second, pk4)) {
       g.pack    = LDPC_PK4;
       g.threads = pk4.threads;
       g.count   = pk4.groups;

@@ -139,6 +139,12 @@ __device__ __forceinline__ u16x2 scale_pk(u16x2 m, const scale_t& sc)
   }
 }
 
+/// 1: the row-z and partner LDS addresses of every edge stay in VGPRs between the two passes of a row; 0: only the
+/// row-z one (A/B switch).
+#ifndef LDPC_PK_KEEP_PARTNER
+#define LDPC_PK_KEEP_PARTNER 1
+#endif
+
 #ifndef LDPC_PK_CRC_CHUNK
 #define LDPC_PK_CRC_CHUNK 8
 #endif
@@ -244,6 +250,11 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     uint32_t       a;
     if constexpr (KEEP_ADDR) {
       a = addr[e];
+#if !LDPC_PK_KEEP_PARTNER
+      // Keep only the row-z address between the passes (the partner a ^ 1 is recomputed: one VALU per edge for one
+      // VGPR per edge).
+      asm volatile("" : "+v"(a));
+#endif
     } else {
       a = pair_address(z2x2_b, ab[e0 + e]);
     }

@@ -162,9 +162,10 @@ class DownlinkGroup:
     def __init__(self, pipes: Sequence[DownlinkPipeline], d_tbs: Sequence, fresh_tbs=False):
         self.pipes, self.d_tbs, self.fresh_tbs = list(pipes), list(d_tbs), fresh_tbs
 
-    def execute(self, stream, events=None, upper=True, ofdm=True):
-        """upper: TB draw, encoding, DM-RS and modulation into the grids; ofdm: the grids' OFDM modulation. A
-        UE-sharded cell runs the two parts on different ranks with the grid gather in between (srsgpu.dist)."""
+    def execute(self, stream, events=None, upper=True, ofdm=True, back=True):
+        """upper: TB draw, encoding, DM-RS and modulation into the grids; back: the OFDM stage (modulation of the grids
+        when `ofdm`). A UE-sharded cell runs the two parts as two calls, with the grid gather in between
+        (srsgpu.dist.GridExchange), and only the cell's root rank modulates (ofdm=False elsewhere)."""
         rec = (lambda i: events[i].record(stream)) if events else (lambda i: None)
         if upper:
             if self.fresh_tbs:
@@ -182,9 +183,10 @@ class DownlinkGroup:
                 p.dmrs.execute(p.d_grid, stream)
                 p.modulator.execute(p.d_cw, p.d_grid, stream)
             rec(2)
-        if ofdm:
-            for p in self.pipes:
-                p.ofdm.execute(p.d_grid, p.d_samples, stream)
+        if back:
+            if ofdm:
+                for p in self.pipes:
+                    p.ofdm.execute(p.d_grid, p.d_samples, stream)
             rec(3)
 
 
@@ -246,14 +248,16 @@ class UplinkPipeline:
         self.d_tbs = torch.zeros(tb_total, dtype=torch.uint8, device=dev)
         self.d_tb_ok = torch.zeros(self.nof_tbs, dtype=torch.uint8, device=dev)
 
-    def execute(self, d_samples, stream, events=None, ofdm=True, upper=True):
-        """ofdm: the OFDM demodulation of `d_samples` into the grid; upper: estimation, demodulation and decoding of
-        the grid. A UE-sharded cell runs the two parts on different ranks with the grid scatter in between."""
+    def execute(self, d_samples, stream, events=None, ofdm=True, upper=True, front=True):
+        """front: the OFDM stage (demodulation of `d_samples` into the grid when `ofdm`); upper: estimation,
+        demodulation and decoding of the grid. A UE-sharded cell runs the two parts as two calls with the grid scatter
+        in between (srsgpu.dist.GridExchange), and only the cell's root rank demodulates (ofdm=False elsewhere)."""
         rec = (lambda i: events[i].record(stream)) if events else (lambda i: None)
-        rec(0)
-        if ofdm:
-            self.ofdm.execute(d_samples, self.d_grid, stream)
-        rec(1)
+        if front:
+            rec(0)
+            if ofdm:
+                self.ofdm.execute(d_samples, self.d_grid, stream)
+            rec(1)
         if not upper:
             return
         self.chest.execute(self.d_grid, self.d_ce, self.d_nv, self.d_metrics, stream)

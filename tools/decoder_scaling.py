@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--cols", type=int, default=26, help="input span in lifted columns (K + 4 = 26: 4 layers)")
     ap.add_argument("--noise", type=float, default=6.0)
     ap.add_argument("--no-crc", action="store_true")
+    ap.add_argument("--sizes", default="256,512,1024,2048,3072,4096,8192", help="codeblocks per launch")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     ctx = srsgpu.Context(0)
@@ -34,7 +35,7 @@ def main():
     rng = np.random.default_rng(3)
     # All-zero codeword (valid for any LDPC code): +amp LLRs with noise. With CRC16 the all-zero message passes.
     llr1 = np.clip(np.round(16.0 + rng.normal(0, args.noise, n_llr)), -120, 120).astype(np.int8)
-    for n in (256, 512, 1024, 2048, 3072, 4096, 8192):
+    for n in [int(x) for x in args.sizes.split(",")]:
         cfg = srsgpu.CodeblockDecodeConfig(1, Z, nof_crc_bits=16, max_iterations=args.iters)
         polys = [srsgpu.CRC_NONE if args.no_crc else srsgpu.CRC16] * n
         arr = srsgpu.make_configs([cfg] * n, [n_llr] * n, polys)

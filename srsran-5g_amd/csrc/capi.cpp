@@ -580,8 +580,10 @@ struct pk4_layout {
 double decoder_issue_cost(long active_waves, int threads, int max_layers, size_t lds_bytes)
 {
   const int wpg      = threads / 64;
-  const int wave_cap = max_layers <= 8 ? 20 : 16;  // 5 / 4 waves per SIMD at the kernels' VGPR counts
-  const int by_vgpr  = wave_cap / wpg;
+  const int simd_cap = max_layers <= 8 ? 5 : 4;  // waves per SIMD at the kernels' VGPR counts
+  // A workgroup's waves go round-robin over the CU's 4 SIMDs: above 4 waves one SIMD takes ceil(w / 4) of them, so
+  // e.g. a 9-wave workgroup (3 on one SIMD) leaves no room for a second at 5 waves per SIMD (measured: PK4, r3).
+  const int by_vgpr  = wpg <= 4 ? (4 * simd_cap) / wpg : simd_cap / ((wpg + 3) / 4);
   const int by_lds   = static_cast<int>((160u * 1024u) / lds_bytes);
   const int resident = std::min(by_vgpr, by_lds) * wpg;
   if (resident <= 0) {
@@ -621,7 +623,12 @@ bool pk4_layout_for(int bg, int max_layers, const std::vector<dec_desc>& cbs, pk
   const size_t lds4  = static_cast<size_t>(LDPC_PK4) * (K + max_layers) * SOFT_COL_STRIDE + 1024;
   double       best  = 1e300;
   int          best_t = 0;
+  const char*  tenv   = std::getenv("SRSGPU_DECODER_PK4_THREADS");  // A/B: one workgroup size only
+  const int    t_only = tenv != nullptr ? std::atoi(tenv) : 0;
   for (int t = 64; t <= LDPC_PK4 * 192; t += 64) {
+    if (t_only > 0 && t != t_only) {
+      continue;
+    }
     long active = 0;
     bool ok     = true;
     for (const auto& r : runs) {

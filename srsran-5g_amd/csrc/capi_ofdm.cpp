@@ -18,6 +18,7 @@ struct srsgpu_ofdm_plan {
   uint32_t              nof_ports  = 0;
   ofdm_job*             d_jobs     = nullptr;
   int                   nof_jobs   = 0;
+  float*                d_scratch  = nullptr;  ///< Split sizes: one N-point complex row per job.
   std::vector<uint64_t> offsets;  ///< Sample offset of (grid, port); one extra entry = total.
 };
 
@@ -76,12 +77,16 @@ int plan_create(srsgpu_context*           ctx,
   const uint32_t N   = cfg->dft_size;
   const uint32_t mu  = cfg->numerology;
   const uint32_t nsc = 12u * cfg->bw_rb;
-  // The generic DFT's sizes (dft_processor_generic_impl.cpp:211-230) up to 8192 points.
+  // The generic DFT's sizes (dft_processor_generic_impl.cpp:211-230): one LDS transform up to 8192 points, the
+  // two-kernel split above (9216 .. 98304).
   const uint32_t m = (N % 3 == 0) ? N / 3 : N;
   const bool     pow2_ok = N >= 128 && N <= 8192 && (N & (N - 1)) == 0;
   const bool     x3_ok   = N % 3 == 0 && m >= 128 && m <= 2048 && (m & (m - 1)) == 0;
-  if (!pow2_ok && !x3_ok && N != 4608) {
-    return fail(SRSGPU_ERR_INVALID_ARG, "DFT size %u not supported (2^n 128..8192, 3 x 2^m 384..6144, 4608)", N);
+  if (!pow2_ok && !x3_ok && N != 4608 && ofdm_split_factor(N) == 0) {
+    return fail(SRSGPU_ERR_INVALID_ARG,
+                "DFT size %u not supported (2^n 128..8192, 3 x 2^m 384..6144, 4608, 9216, 12288, 18432, 24576, 36864, "
+                "49152, 98304)",
+                N);
   }
   if (mu > 4 || cfg->bw_rb == 0 || nsc >= N) {
     return fail(SRSGPU_ERR_INVALID_ARG, "the DFT size (%u) must be greater than the resource grid size (%u)", N, nsc);
@@ -162,6 +167,12 @@ int plan_create(srsgpu_context*           ctx,
     srsgpu_ofdm_plan_destroy(plan);
     return fail(SRSGPU_ERR_HIP, "failed to upload OFDM jobs");
   }
+  if (!jobs.empty() && ofdm_split_factor(N) != 0 &&
+      hipMalloc(&plan->d_scratch, jobs.size() * static_cast<size_t>(N) * 2 * sizeof(float)) != hipSuccess) {
+    srsgpu_ofdm_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to allocate the split-transform scratch (%zu MB)",
+                jobs.size() * static_cast<size_t>(N) * 8 / (1u << 20));
+  }
   *plan_out = plan;
   return SRSGPU_OK;
 }
@@ -213,7 +224,7 @@ int srsgpu_ofdm_modulator_plan_execute(const srsgpu_ofdm_plan* plan,
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument or not a modulator plan");
   }
   launch_ofdm(true, plan->dft_size, plan->d_jobs, plan->nof_jobs, plan->nsc, 0, plan->ctx->d_ofdm_twiddles, d_grids,
-              nullptr, nullptr, d_samples, static_cast<hipStream_t>(stream));
+              nullptr, nullptr, d_samples, plan->d_scratch, static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
 }
@@ -227,7 +238,8 @@ int srsgpu_ofdm_demodulator_plan_execute(const srsgpu_ofdm_plan* plan,
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument or not a demodulator plan");
   }
   launch_ofdm(false, plan->dft_size, plan->d_jobs, plan->nof_jobs, plan->nsc, plan->window_off,
-              plan->ctx->d_ofdm_twiddles, nullptr, d_grids, d_samples, nullptr, static_cast<hipStream_t>(stream));
+              plan->ctx->d_ofdm_twiddles, nullptr, d_grids, d_samples, nullptr, plan->d_scratch,
+              static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
 }
@@ -239,6 +251,9 @@ void srsgpu_ofdm_plan_destroy(srsgpu_ofdm_plan* plan)
   }
   if (plan->d_jobs != nullptr) {
     (void)hipFree(plan->d_jobs);
+  }
+  if (plan->d_scratch != nullptr) {
+    (void)hipFree(plan->d_scratch);
   }
   delete plan;
 }

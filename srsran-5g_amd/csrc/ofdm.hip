@@ -15,6 +15,12 @@
 // or, in the last pass, straight to HBM with the compensation applied: time samples (and the cyclic-prefix copy) or
 // bf16 subcarriers. HBM traffic per symbol: the grid row (4 B per subcarrier) and N + CP complex float samples (8 B),
 // each touched once.
+//
+// Sizes above one workgroup's LDS (the generic DFT's 9216 .. 98304 = N2 x M, N2 in {3, 6, 9, 12}, M a power of two
+// <= 8192) run as two kernels (a four-step split through an HBM scratch row per symbol): the first computes, for every
+// n1 < M, the N2-point DFT of x[n1 + M n2] (n2 < N2) times exp(S 2 pi i n1 k2 / N) into scratch[k2][n1]; the second runs
+// the M-point LDS transform of each scratch row k2 and writes output k2 + N2 k1 with the same fused last-pass work.
+// X[k2 + N2 k1] = sum_n1 W_M^(n1 k1) W_N^(n1 k2) sum_n2 x[n1 + M n2] W_N2^(n2 k2).
 #include "srsgpu_internal.h"
 
 namespace srsgpu {
@@ -409,6 +415,153 @@ __global__ __launch_bounds__(ofdm_threads<N>()) void ofdm_demodulate_kernel(
   dft_any<N, -1>(lds, tw, src, dst);
 }
 
+/// Bin b of an N-point transform -> subcarrier of a grid of 2 half subcarriers (-1: a guard bin).
+template <int N>
+__device__ __forceinline__ int bin_subcarrier(int b, int half)
+{
+  return (b < half) ? half + b : (b >= N - half ? b - (N - half) : -1);
+}
+
+/// Split transform, first kernel: one thread per n1 < M of one job (blockIdx.y), 256 threads per workgroup.
+template <int N2, int M, int S, bool MOD>
+__global__ __launch_bounds__(256) void ofdm_split_first_kernel(const ofdm_job* __restrict__ jobs,
+                                                               uint32_t nsc,
+                                                               uint32_t window_offset,
+                                                               const uint32_t* __restrict__ grid,
+                                                               const float2* __restrict__ in,
+                                                               float2* __restrict__ scratch)
+{
+  constexpr int N  = N2 * M;
+  const int     n1 = static_cast<int>(blockIdx.x * 256u + threadIdx.x);
+  if (n1 >= M) {
+    return;
+  }
+  const ofdm_job jb = jobs[blockIdx.y];
+  float2         x[N2];
+  if constexpr (MOD) {
+    const uint32_t* row  = grid + jb.grid_offset;
+    const int       half = static_cast<int>(nsc / 2);
+#pragma unroll
+    for (int n2 = 0; n2 < N2; ++n2) {
+      const int sc = bin_subcarrier<N>(n1 + M * n2, half);
+      if (sc < 0) {
+        x[n2] = make_float2(0.f, 0.f);
+      } else {
+        const uint32_t u = row[sc];
+        x[n2]            = make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+      }
+    }
+  } else {
+    const float2* src = in + jb.sample_offset + jb.cp_len - window_offset;
+#pragma unroll
+    for (int n2 = 0; n2 < N2; ++n2) {
+      x[n2] = src[n1 + M * n2];
+    }
+  }
+  // exp(S 2 pi i m / N2), m < N2 (argument rounded once).
+  float2 w2[N2];
+#pragma unroll
+  for (int m = 0; m < N2; ++m) {
+    sincospif(static_cast<float>(2 * m) / static_cast<float>(N2), &w2[m].y, &w2[m].x);
+    w2[m].y = S * w2[m].y;
+  }
+  float2* out = scratch + static_cast<size_t>(blockIdx.y) * N + n1;
+#pragma unroll
+  for (int k2 = 0; k2 < N2; ++k2) {
+    float2 acc = x[0];
+#pragma unroll
+    for (int n2 = 1; n2 < N2; ++n2) {
+      const float2 t = cmul(x[n2], w2[(n2 * k2) % N2]);
+      acc            = cadd(acc, t);
+    }
+    if (k2 != 0) {
+      float2 w;
+      sincospif(static_cast<float>(2 * ((n1 * k2) % N)) / static_cast<float>(N), &w.y, &w.x);
+      w.y = S * w.y;
+      acc = cmul(acc, w);
+    }
+    out[k2 * M] = acc;
+  }
+}
+
+/// Split transform, second kernel: workgroup (job, k2) runs the M-point LDS transform of scratch row k2 and writes
+/// outputs k2 + N2 k1 (time samples with coefficient and cyclic prefix, or bf16 subcarriers).
+template <int N2, int M, int S, bool MOD>
+__global__ __launch_bounds__(M / 16) void ofdm_split_second_kernel(const ofdm_job* __restrict__ jobs,
+                                                                   uint32_t nsc,
+                                                                   uint32_t window_offset,
+                                                                   const float2* __restrict__ tw,
+                                                                   const float2* __restrict__ scratch,
+                                                                   uint32_t* __restrict__ grid,
+                                                                   float2* __restrict__ out)
+{
+  constexpr int     N   = N2 * M;
+  __shared__ float2 lds[M];
+  const uint32_t    job = blockIdx.x / N2, k2 = blockIdx.x % N2;
+  const ofdm_job    jb  = jobs[job];
+  const float2*     row = scratch + static_cast<size_t>(job) * N + static_cast<size_t>(k2) * M;
+  auto              src = [row](int n) { return row[n]; };
+  const float2      coef = make_float2(jb.coef_re, jb.coef_im);
+  if constexpr (MOD) {
+    float2*   sym = out + jb.sample_offset;
+    const int cp  = static_cast<int>(jb.cp_len);
+    auto dst = [sym, coef, cp, k2](int k1, float2 v) {
+      const int    n = static_cast<int>(k2) + N2 * k1;
+      const float2 y = cmul(v, coef);
+      sym[cp + n]    = y;
+      if (n >= N - cp) {
+        sym[n - (N - cp)] = y;
+      }
+    };
+    dft_lds<ilog2(M), S>(lds, tw, src, dst);
+  } else {
+    uint32_t* grow = grid + jb.grid_offset;
+    const int half = static_cast<int>(nsc / 2);
+    auto dst = [grow, coef, half, tw, window_offset, k2](int k1, float2 v) {
+      const int b  = static_cast<int>(k2) + N2 * k1;
+      const int sc = bin_subcarrier<N>(b, half);
+      if (sc < 0) {
+        return;
+      }
+      float2 y = cmul(v, coef);
+      if (window_offset != 0) {  // times exp(+j 2 pi offset b / N)
+        y = cmul(y, twiddle_any<N, +1>(tw, (window_offset * static_cast<uint32_t>(b)) % N));
+      }
+      grow[sc] = bf16_bits(y.x) | (bf16_bits(y.y) << 16);
+    };
+    dft_lds<ilog2(M), S>(lds, tw, src, dst);
+  }
+}
+
+template <int N2, int M>
+void launch_split(bool            inverse,
+                  const ofdm_job* jobs,
+                  int             nof_jobs,
+                  uint32_t        nsc,
+                  uint32_t        window_offset,
+                  const float2*   tw,
+                  const uint32_t* grid_in,
+                  uint32_t*       grid_out,
+                  const float2*   samples_in,
+                  float2*         samples_out,
+                  float2*         scratch,
+                  hipStream_t     stream)
+{
+  const dim3 g1((M + 255) / 256, static_cast<unsigned>(nof_jobs)), b1(256);
+  const dim3 g2(static_cast<unsigned>(nof_jobs) * N2), b2(M / 16);
+  if (inverse) {
+    hipLaunchKernelGGL((ofdm_split_first_kernel<N2, M, +1, true>), g1, b1, 0, stream, jobs, nsc, 0u, grid_in,
+                       nullptr, scratch);
+    hipLaunchKernelGGL((ofdm_split_second_kernel<N2, M, +1, true>), g2, b2, 0, stream, jobs, nsc, 0u, tw, scratch,
+                       nullptr, samples_out);
+  } else {
+    hipLaunchKernelGGL((ofdm_split_first_kernel<N2, M, -1, false>), g1, b1, 0, stream, jobs, nsc, window_offset,
+                       nullptr, samples_in, scratch);
+    hipLaunchKernelGGL((ofdm_split_second_kernel<N2, M, -1, false>), g2, b2, 0, stream, jobs, nsc, window_offset, tw,
+                       scratch, grid_out, nullptr);
+  }
+}
+
 template <int N>
 void launch_one(bool            inverse,
                 const ofdm_job* jobs,
@@ -445,6 +598,7 @@ void launch_ofdm(bool            inverse,
                  uint32_t*       d_grid_out,
                  const float*    d_samples_in,
                  float*          d_samples_out,
+                 float*          d_scratch,
                  hipStream_t     stream)
 {
   if (nof_jobs <= 0) {
@@ -467,6 +621,17 @@ void launch_ofdm(bool            inverse,
     case 3072: launch_one<3072>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
     case 4608: launch_one<4608>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
     case 6144: launch_one<6144>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
+    default: break;
+  }
+  auto* sc = reinterpret_cast<float2*>(d_scratch);
+  switch (dft_size) {
+    case 9216: launch_split<9, 1024>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, sc, stream); break;
+    case 12288: launch_split<3, 4096>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, sc, stream); break;
+    case 18432: launch_split<9, 2048>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, sc, stream); break;
+    case 24576: launch_split<3, 8192>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, sc, stream); break;
+    case 36864: launch_split<9, 4096>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, sc, stream); break;
+    case 49152: launch_split<6, 8192>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, sc, stream); break;
+    case 98304: launch_split<12, 8192>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, sc, stream); break;
     default: break;
   }
 }

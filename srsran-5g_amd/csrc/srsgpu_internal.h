@@ -328,7 +328,16 @@ struct ofdm_job {
 /// Largest DFT size and the twiddle table exp(-j 2 pi m / OFDM_MAX_DFT), m < OFDM_MAX_DFT, every size strides through.
 constexpr uint32_t OFDM_MAX_DFT = 8192;
 
-/// dft_size: a power of two 128..8192, 3 x 2^m 384..6144 or 4608 (9 x 512).
+/// Split factor of the two-kernel transform of a DFT size above one workgroup's LDS (the generic DFT's 9216 ..
+/// 98304): N = ofdm_split_factor(N) x M with M a power of two <= OFDM_MAX_DFT; 0 for the one-kernel sizes.
+constexpr uint32_t ofdm_split_factor(uint32_t n)
+{
+  return n == 9216 ? 9 : n == 12288 ? 3 : n == 18432 ? 9 : n == 24576 ? 3 : n == 36864 ? 9 : n == 49152 ? 6
+         : n == 98304 ? 12 : 0;
+}
+
+/// dft_size: a power of two 128..8192, 3 x 2^m 384..6144, 4608 (9 x 512), or a split size (ofdm_split_factor != 0),
+/// which needs d_scratch: nof_jobs x dft_size complex floats.
 void launch_ofdm(bool            inverse,
                  uint32_t        dft_size,
                  const ofdm_job* d_jobs,
@@ -340,6 +349,7 @@ void launch_ofdm(bool            inverse,
                  uint32_t*       d_grid_out,
                  const float*    d_samples_in,
                  float*          d_samples_out,
+                 float*          d_scratch,
                  hipStream_t     stream);
 
 /// PUSCH demodulator (pusch_demodulator.hip): per-transmission descriptor. Work items are mod_chunk (8192 LLRs each).

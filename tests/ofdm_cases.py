@@ -30,7 +30,18 @@ CASES = [
     (2, 51, 768, False, 0.3, 28e9, 3, 0),               # 60 kHz
     (1, 273, 6144, False, 1.0 / 96, 3.5e9, 0, 20),      # 100 MHz, 184.32 Msps
     (1, 273, 4608, False, 1.0 / 72, 3.5e9, 1, 11),      # 100 MHz, 138.24 Msps (9 x 512: two radix-3 passes)
+    # Sizes above one workgroup's LDS (dft_processor_generic_impl.cpp:224-230): the two-kernel split transform.
+    (1, 273, 9216, False, 1.0 / 144, 3.5e9, 1, 40),     # 276.48 Msps (9 x 1024)
+    (1, 273, 12288, False, 1.0 / 192, 3.6e9, 0, 0),     # 368.64 Msps (3 x 4096)
+    (0, 270, 18432, False, 1.0 / 288, 2.1e9, 0, 7),     # 15 kHz, 276.48 Msps (9 x 2048)
+    (2, 273, 24576, False, 1.0 / 384, 27e9, 3, 0),      # 60 kHz, 1474.56 Msps (3 x 8192)
+    (2, 273, 36864, False, 1.0 / 576, 28e9, 3, 100),    # 60 kHz (9 x 4096)
+    (2, 135, 49152, True, 1.0 / 768, 28e9, 2, 0),       # 60 kHz extended CP (6 x 8192)
+    (1, 273, 98304, False, 1.0 / 1536, 3.5e9, 1, 300),  # 30 kHz (12 x 8192)
 ]
+# 120 kHz with 36864 / 98304 points is not in the list: the reference computes the sampling rate in 32 bits
+# (subcarrier_spacing.h:279, 120 kHz x 36864 > 2^32) and gets wrong cyclic prefixes there
+# (tests/test_oracle_vs_reference.py::test_ofdm_reference_sampling_rate_overflow).
 
 
 def random_grid(rng, P, ns, nsc, occupancy=1.0):

@@ -93,7 +93,7 @@ def test_ofdm_batched_slots_round_trip(ctx):
 def test_ofdm_rejects_invalid(ctx):
     import srsgpu
     for args in [(1, 273, 3000, 1.0, 0.0), (1, 273, 2048, 1.0, 0.0), (1, 106, 2048, 0.0, 0.0), (5, 10, 512, 1.0, 0.0),
-                 (1, 273, 9216, 1.0, 0.0), (1, 273, 12288, 1.0, 0.0), (0, 5, 64, 1.0, 0.0)]:
+                 (1, 273, 16384, 1.0, 0.0), (1, 273, 10000, 1.0, 0.0), (0, 5, 64, 1.0, 0.0)]:
         with pytest.raises(srsgpu.SrsGpuError):
             srsgpu.OfdmPlan(ctx, True, *args, [0], 1)
     with pytest.raises(srsgpu.SrsGpuError):  # window offset >= 144 N / 2048

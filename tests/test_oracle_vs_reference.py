@@ -242,7 +242,7 @@ def test_pdsch_modulator_multi_prg_reference_defect(orc, ref):
         assert np.array_equal(got[:, l0, :48], want[:, l0, :48]), cfg
 
 
-@pytest.mark.parametrize("case", range(19))
+@pytest.mark.parametrize("case", range(26))
 def test_ofdm_oracle_vs_reference(ref, case):
     """OFDM modulator and demodulator restatement (oracle/ofdm_oracle.py, complex128) against the reference's
     ofdm_slot_modulator_impl / ofdm_slot_demodulator_impl with its generic float DFT: slot sizes equal, modulated
@@ -262,8 +262,23 @@ def test_ofdm_oracle_vs_reference(ref, case):
     gref = ref.ofdm_demodulate(want, mu, rb, N, ext, 1.0 / (scale * N), fc, slot, woff)
     gorc = O.complex_to_bf16(O.demodulate(want.astype(np.complex128), mu, rb, N, ext, 1.0 / (scale * N), fc, slot,
                                           woff))
-    ok, frac = bf16_close(gorc, gref)
+    # Above 8192 points the reference's own float error grows (its DFT-window phase ramp exp(j 2 pi woff b / N) is
+    # evaluated in float for b up to N: ~1e-4 rad at 98304 points, woff 300): 3e-4 x RMS absolute there.
+    ok, frac = bf16_close(gorc, gref, atol_rel_rms=1e-4 if N <= 8192 else 3e-4)
     assert ok and frac < 0.02, frac
+
+
+def test_ofdm_reference_sampling_rate_overflow(ref):
+    """Reference defect: to_sampling_rate_Hz<unsigned> (subcarrier_spacing.h:279) multiplies in 32 bits, so at 120 kHz
+    the generic DFT's 36864- and 98304-point sizes overflow (4.42 / 11.8 GHz) and the slot is sized with wrong cyclic
+    prefixes. The oracle (and the GPU plans) keep the TS 38.211 section 5.3.1 lengths; below 2^32 both agree."""
+    import ofdm_oracle as O
+    for mu, N, slot in ((3, 36864, 5), (3, 98304, 7)):
+        assert 15000 * (1 << mu) * N >= 1 << 32
+        assert ref.ofdm_slot_size(mu, 264, N, False, slot) != O.slot_size(mu, N, False, slot)
+        cp = (144 >> mu) * (1 << mu) * N // 2048  # kappa units -> samples at N x scs
+        assert O.slot_size(mu, N, False, slot) == 14 * (N + cp)
+    assert ref.ofdm_slot_size(2, 264, 36864, False, 3) == O.slot_size(2, 36864, False, 3)
 
 
 @pytest.mark.parametrize("qm", [2, 4, 6, 8])

@@ -553,10 +553,16 @@ def measure(args, env):
             dec_kernel = sq_name.replace(" ", "")
         if sq:
             peak = 1024 * 2.4e9 / 2  # SIMDs x clock / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md)
+            # Measured ceiling of the decoder's instruction mix (profiles/r3_valu_rate_probe_*.log: independent
+            # v_pk_* streams saturate at 2.2 G wave-instr/s per CU, VOP2 at 3.4; 80 / 20 % mix -> 2.35 G/s per CU).
+            mix_peak = 256 * 2.35e9
             rate = sq["valu_instr"] / (dec_ms * 1e-3)
             valu = {"bound": "valu_issue", "achieved": rate, "peak": peak, "unit": "wave-instr/s",
                     "frac": rate / peak, "instr_per_launch": sq["valu_instr"],
-                    "source": "profiles/sq_valu.json (SQ_INSTS_VALU) / live kernel time"}
+                    "peak_measured_mix": mix_peak, "frac_of_measured_mix_peak": rate / mix_peak,
+                    "source": "profiles/sq_valu.json (SQ_INSTS_VALU) / live kernel time; peak = 2 cycles per wave64 "
+                              "instruction on SIMD-32; peak_measured_mix = the rate probe's ceiling for 80 % packed "
+                              "16-bit (v_pk_*, ~3.9 cycles each) + 20 % 32-bit VALU"}
 
     # Algorithmic HBM bytes per step of the signal-chain stages (each byte read or written once; DESIGN.md "Kernels"):
     # bf16 grids are 4 B per RE, time samples 8 B (complex float), estimates 4 B per (layer, port, RE), LLRs 1 B.

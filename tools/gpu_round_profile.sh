@@ -8,8 +8,11 @@ OUT=gpurun_out/${1:-round}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 R=$(pwd)
-PB="--no-cpu-baseline --no-extra-points --steps 40 --warmup 4"
-timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+# EXTRA: bench arguments of the profiled workload (e.g. "--profile mimo4 --snr-db 35"); SKIP_BENCH=1: only the passes.
+PB="--no-cpu-baseline --no-extra-points --no-extra-workloads --steps 40 --warmup 4 --min-time 0 ${EXTRA:-}"
+if [ "${SKIP_BENCH:-0}" != 1 ]; then
+  timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/$OUT/stats" -o run --output-format csv -- \
   python3 "$R/bench.py" $PB > "$OUT/stats_bench.json" 2> "$OUT/stats.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$R/$OUT/pmc_fetch" -o run --output-format csv -- \

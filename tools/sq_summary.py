@@ -40,8 +40,9 @@ if __name__ == "__main__":
     if len(sys.argv) > 3:  # sq_summary.py CSV OUT_JSON BENCH_JSON: keyed by the bench workload (bench.py checks it)
         bench = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])
         snr = bench["operating_points"][0]["snr_db"]
-        res = {"workload": f"{bench['config']['profile']}/S{bench['config']['slots_per_step']}/"
-                           f"{'noise' if snr is None else f'{snr:g}dB'}", "kernels": res}
+        res = {"workload": bench["roofline"].get("workload_key") or (
+            f"{bench['config']['profile']}/S{bench['config']['slots_per_step']}/"
+            f"{'noise' if snr is None else f'{snr:g}dB'}"), "kernels": res}
     if len(sys.argv) > 2:
         with open(sys.argv[2], "w") as f:
             json.dump(res, f, indent=1)

@@ -37,8 +37,9 @@ def main():
     snr = bench["operating_points"][0]["snr_db"]
     res = {
         "kernel": kn[0] if kn else k,
-        "workload": f"{bench['config']['profile']}/S{bench['config']['slots_per_step']}/"
-                    f"{'noise' if snr is None else f'{snr:g}dB'}",  # bench.py matches it before using the numbers
+        "workload": bench["roofline"].get("workload_key") or (
+            f"{bench['config']['profile']}/S{bench['config']['slots_per_step']}/"
+            f"{'noise' if snr is None else f'{snr:g}dB'}"),  # bench.py matches it before using the numbers
         "dispatches_fetch": nf,
         "dispatches_write": nw,
         "fetch_size_kb_raw": fetch_kb,

@@ -67,24 +67,41 @@ __device__ __forceinline__ u16x2 uu(int x)
 {
   return u16x2{static_cast<unsigned short>(x), static_cast<unsigned short>(x)};
 }
-/// 1 where IDX != e, 0 where IDX == e (both halves): one v_pk_min_u16 against an opaque 0x00010001 (a visible
-/// constant 1 gets the min rewritten into per-half compares and cndmasks).
+/// Packed 16-bit VALU instructions issue at about two thirds of the rate of 32-bit ones on gfx950
+/// (profiles/r3_valu_rate_probe_*.log): where an operation is bitwise the 32-bit form serves both halves.
+#ifndef LDPC_PK_XOR_ARGMIN
+#define LDPC_PK_XOR_ARGMIN 1
+#endif
+#ifndef LDPC_PK_SAT_INF
+#define LDPC_PK_SAT_INF 1
+#endif
+
+/// 1 where IDX != e, 0 where IDX == e (both halves): IDX ^ e (one 32-bit v_xor on both 5-bit halves), then one
+/// v_pk_min_u16 against an opaque 0x00010001 (a visible constant 1 gets the min rewritten into per-half compares and
+/// cndmasks).
 __device__ __forceinline__ u16x2 not_argmin(u16x2 idx, int e, u16x2 one)
 {
+#if LDPC_PK_XOR_ARGMIN
+  return __builtin_elementwise_min(as_u16(bits(idx) ^ (0x00010001u * static_cast<uint32_t>(e))), one);
+#else
   return __builtin_elementwise_min(idx - uu(e), one);  // v_pk_sub_u16 with e inline and op_sel_hi broadcast
+#endif
 }
 
 /// Opaque packed multipliers 32 and 512: with a visible power of two the compiler splits a multiply-add into a
 /// shift and an add / or (two VALU instead of one v_pk_mad).
 struct pk_consts {
-  u16x2 k32;
-  s16x2 k512;
+  u16x2    k32;
+  s16x2    k512;
+  uint32_t k271, kn271, kn21;  ///< 271, -271, -21 in both halves (SGPRs; LDPC_PK_SAT_INF)
 };
 __device__ __forceinline__ pk_consts make_pk_consts()
 {
   uint32_t a = 0x00200020u, b = 0x02000200u;
   asm("" : "+v"(a), "+v"(b));
-  return {as_u16(a), as_s16(b)};
+  uint32_t c = 0x010f010fu, d = 0xfef1fef1u, f = 0xffebffebu;
+  asm("" : "+s"(c), "+s"(d), "+s"(f));
+  return {as_u16(a), as_s16(b), c, d, f};
 }
 
 /// v2c of an edge from its soft bit sb and previous c2v magnitude om with sign mask n (0 / -1):
@@ -94,8 +111,19 @@ __device__ __forceinline__ s16x2 v2c_pk(s16x2 sb, u16x2 om, s16x2 n, const pk_co
 {
   const s16x2 nn  = as_s16(~bits(n) | 0x00010001u);
   const s16x2 t   = as_s16(bits(om)) * nn + sb;
+  const s16x2 ct  = __builtin_elementwise_min(__builtin_elementwise_max(t, ss(-LLR_MAX)), ss(LLR_MAX));
+#if LDPC_PK_SAT_INF
+  // Infinity marker without clamping sb: g = sat16(271 sb) - 271 sb is 0 for |sb| <= 120 (271 x 120 = 32520) and
+  // -24 / +23 for sb = +121 / -121 (the saturating v_pk_mad_i16 clamps 32791 to 32767); v = clamp(t) - 21 g puts an
+  // infinite soft bit's v2c at +505..624 / -603..-484 (|v2c| >= 392 stays infinite; keys < 2^16).
+  uint32_t sat;
+  asm("v_pk_mad_i16 %0, %1, %2, 0 clamp" : "=v"(sat) : "v"(bits(sb)), "s"(kc.k271));
+  const s16x2 g = sb * as_s16(kc.kn271) + as_s16(sat);
+  return g * as_s16(kc.kn21) + ct;
+#else
   const s16x2 fin = __builtin_elementwise_min(__builtin_elementwise_max(sb, ss(-LLR_MAX)), ss(LLR_MAX));
-  return (sb - fin) * kc.k512 + __builtin_elementwise_min(__builtin_elementwise_max(t, ss(-LLR_MAX)), ss(LLR_MAX));
+  return (sb - fin) * kc.k512 + ct;
+#endif
 }
 
 /// Search key |v| * 32 + e of the two-minimum scan (one v_pk_mad).

@@ -709,9 +709,10 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
 
 uint32_t srsgpu_pusch_decoder_plan_nof_codeblocks(const srsgpu_pusch_decoder_plan* plan);
 
-/** Number of LLRs the LDPC decoder stage reads per execute: every codeblock's span of the HARQ buffer, trimmed to the
- *  rate dematcher's zero tail for new transmissions (what decode() would trim to, ldpc_decoder_impl.cpp:94). For
- *  traffic accounting. */
+/** Number of LLR bytes the LDPC decoder stage moves per execute: every codeblock's span of the HARQ buffer, trimmed to
+ *  the rate dematcher's zero tail for new transmissions (what decode() would trim to, ldpc_decoder_impl.cpp:94); for
+ *  a codeblock whose rate dematching the decoder performs itself (first transmissions that are a plain copy), the E
+ *  codeword LLRs it reads plus the N HARQ bytes it writes. For traffic accounting. */
 uint64_t srsgpu_pusch_decoder_plan_decoder_input_llrs(const srsgpu_pusch_decoder_plan* plan);
 
 /** Decodes the planned transport blocks. d_tb_crc_ok[t] = 1 when the TB CRC passed (pusch_decoder_result

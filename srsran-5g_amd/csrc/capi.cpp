@@ -111,11 +111,13 @@ struct srsgpu_ldpc_decoder_plan {
     int       threads = 64;
     int       count   = 0;
     dec_desc* d_desc  = nullptr;
+    dm_desc*  d_dm    = nullptr;  ///< Fused rate dematching (DEC_FLAG_FUSED_DM): one dm_desc per codeblock, in order.
   };
   srsgpu_context*    ctx  = nullptr;
   int                impl = SRSGPU_LDPC_IMPL_SIMD;
   std::vector<group> groups;
-  uint64_t           input_llrs = 0;  ///< LLRs the decoder reads per execute (sum of dec_desc::nof_llr).
+  uint64_t           input_llrs = 0;  ///< LLR bytes the decoder moves per execute: dec_desc::nof_llr per codeblock,
+                                      ///< E + N for fused ones (codeword LLRs read, HARQ buffer written).
 };
 
 namespace {
@@ -476,9 +478,10 @@ namespace {
 /// Codeblock work split by base graph: one launch per base graph, sized for its largest lifting size. (Splitting
 /// further by block size raises the occupancy of the small-Z blocks but serialises launches; measured slower on the
 /// 100 MHz slot: 0.82 vs 0.76 ms per 16 slots.)
-using dec_key = std::tuple<int, bool, int>;  ///< (base graph, packed kernel, layer bound class)
+using dec_key = std::tuple<int, bool, int, bool>;  ///< (base graph, packed kernel, layer bound class, fused dematch)
 struct dec_batch {
   std::map<dec_key, std::vector<dec_desc>> groups;
+  std::map<dec_key, std::vector<dm_desc>>  fused;  ///< Fused groups: the dm_desc of each codeblock, in group order.
   std::map<dec_key, int>                   threads;
   std::vector<crc_key>*                    crc_refs = nullptr;  ///< The creating call's crc_ref_guard.
 };
@@ -509,7 +512,8 @@ int add_decoder_cb(srsgpu_context* ctx,
                    uint32_t        llr_offset,
                    uint32_t        nof_llrs,
                    uint32_t        out_offset,
-                   dec_batch&      batch)
+                   dec_batch&      batch,
+                   const dm_desc*  fused_dm = nullptr)
 {
   if (bg != 1 && bg != 2) {
     return fail(SRSGPU_ERR_INVALID_ARG, "cb %u: invalid base graph %d", i, bg);
@@ -559,7 +563,12 @@ int add_decoder_cb(srsgpu_context* ctx,
     d.flags = early_stop ? DEC_FLAG_EARLY_STOP : 0u;
   }
   const bool    packed = (Z % 2) == 0;
-  const dec_key key(bg, packed, packed ? layer_class(bg, Z, nof_llrs) : 0);
+  const bool    fuse   = fused_dm != nullptr && packed;
+  const dec_key key(bg, packed, packed ? layer_class(bg, Z, nof_llrs) : 0, fuse);
+  if (fuse) {
+    d.flags |= DEC_FLAG_FUSED_DM;
+    batch.fused[key].push_back(*fused_dm);
+  }
   batch.groups[key].push_back(d);
   const int lanes = packed ? Z / 2 : Z;
   int&      t     = batch.threads[key];
@@ -678,6 +687,7 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
     g.bg               = std::get<0>(kv.first);
     g.packed           = std::get<1>(kv.first);
     g.max_layers       = std::get<2>(kv.first);
+    const bool fused   = std::get<3>(kv.first);
     g.threads          = batch.threads.at(kv.first);
     g.count            = static_cast<int>(kv.second.size());
     // Few codeblocks per launch leave the SIMDs with one or two waves each: the per-codeblock latency (instructions
@@ -693,13 +703,28 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
         g.threads *= 2;
       }
     }
-    for (const dec_desc& d : kv.second) {
-      plan->input_llrs += d.nof_llr;
+    if (!fused) {
+      for (const dec_desc& d : kv.second) {
+        plan->input_llrs += d.nof_llr;
+      }
+    } else {
+      // A fused codeblock reads its E codeword LLRs and writes the N-byte HARQ buffer instead.
+      const std::vector<dm_desc>& dms = batch.fused.at(kv.first);
+      for (const dm_desc& m : dms) {
+        plan->input_llrs += static_cast<uint64_t>(m.E) + m.N;
+      }
+      const size_t dm_bytes = dms.size() * sizeof(dm_desc);
+      if (hipMalloc(&g.d_dm, dm_bytes) != hipSuccess ||
+          hipMemcpy(g.d_dm, dms.data(), dm_bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        plan->groups.push_back(g);
+        srsgpu_ldpc_decoder_plan_destroy(plan);
+        return fail(SRSGPU_ERR_HIP, "failed to upload fused rate dematcher descriptors");
+      }
     }
     pk4_layout             pk4;
     const dec_desc*        src   = kv.second.data();
     size_t                 bytes = kv.second.size() * sizeof(dec_desc);
-    if (g.packed && g.split == 1 && pk4_layout_for(g.bg, g.max_layers, kv.second, pk4)) {
+    if (g.packed && g.split == 1 && !fused && pk4_layout_for(g.bg, g.max_layers, kv.second, pk4)) {
       g.pack    = LDPC_PK4;
       g.threads = pk4.threads;
       g.count   = pk4.groups;
@@ -718,12 +743,15 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
   return SRSGPU_OK;
 }
 
+/// d_cw_llrs / d_harq: the codeword LLRs and the HARQ buffer of the fused groups (PUSCH plans; null otherwise).
 int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
                          const int8_t*                   d_llrs,
                          uint8_t*                        d_out,
                          int32_t*                        d_nof_iterations,
                          uint8_t*                        d_cb_crc_ok,
-                         hipStream_t                     s)
+                         hipStream_t                     s,
+                         const int8_t*                   d_cw_llrs = nullptr,
+                         int8_t*                         d_harq    = nullptr)
 {
   for (const auto& g : plan->groups) {
     if (g.pack == LDPC_PK4) {
@@ -731,9 +759,13 @@ int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
                              d_nof_iterations, plan->ctx->d_pair_ab4[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok,
                              s);
     } else if (g.packed) {
-      launch_ldpc_decode_pk(g.bg, plan->impl, g.max_layers, g.split, g.d_desc, g.count, g.threads, d_llrs, d_out,
-                            d_nof_iterations,
-                            plan->ctx->d_pair_ab[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s);
+      if (g.d_dm != nullptr && (d_cw_llrs == nullptr || d_harq == nullptr)) {
+        return fail(SRSGPU_ERR_INVALID_ARG, "fused decoder group without codeword LLRs / HARQ buffer");
+      }
+      launch_ldpc_decode_pk(g.bg, plan->impl, g.max_layers, g.split, g.d_desc, g.count, g.threads,
+                            g.d_dm != nullptr ? d_cw_llrs : d_llrs, d_out, d_nof_iterations,
+                            plan->ctx->d_pair_ab[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, g.d_dm,
+                            g.d_dm != nullptr ? d_harq : nullptr, s);
     } else {
       launch_ldpc_decode(g.bg, plan->impl, g.d_desc, g.count, g.threads, d_llrs, d_out, d_nof_iterations,
                          plan->ctx->d_shifts32[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s);
@@ -804,7 +836,17 @@ int add_pusch_cb(srsgpu_context*        ctx,
   d.cb_index    = c.cb_index;
   const uint64_t R = c.E / static_cast<uint32_t>(qm);
   d.r_magic        = ((1ULL << 40) + R - 1) / R;
-  dms.push_back(d);
+  // A first transmission from rv 0 of the whole circular buffer that reaches every systematic position without
+  // wrapping (ninfo <= E <= V) is a plain copy that defines every HARQ position (copies, fillers, zeroed tail): the
+  // packed decoder dematches it itself (ldpc_decode_pk_kernel FUSE) and the rate dematcher skips it.
+  // SRSGPU_DECODER_FUSED_DM=0 keeps every codeblock on the separate rate dematcher (A/B).
+  const char* fuse_env     = std::getenv("SRSGPU_DECODER_FUSED_DM");
+  const bool  fuse_enabled = fuse_env == nullptr || fuse_env[0] != '0';
+  const bool fuse = fuse_enabled && c.new_data && d.v0 == 0 && Ncb == N && static_cast<int>(c.E) >= ninfo &&
+                    static_cast<int>(c.E) <= Ncb - c.filler && (Z % 2) == 0;
+  if (!fuse) {
+    dms.push_back(d);
+  }
   // The decoder reads the HARQ buffer up to the last position a new transmission can leave non-zero: the rate
   // dematcher zeroes everything from the end of an incomplete first pass (zero_from), and decode() trims trailing
   // zeros anyway (ldpc_decoder_impl.cpp:94), so the shorter span (whole lifted columns, hence the same soft clamp)
@@ -824,7 +866,7 @@ int add_pusch_cb(srsgpu_context*        ctx,
     }
   }
   return add_decoder_cb(ctx, c.cb_index, c.bg, Z, c.filler, c.nof_crc_bits, c.max_iter, c.sf, c.crc_poly,
-                        c.early_stop, c.harq_offset, dec_llrs, c.out_offset, batch);
+                        c.early_stop, c.harq_offset, dec_llrs, c.out_offset, batch, fuse ? &d : nullptr);
 }
 
 int upload_pusch_cb_plan(srsgpu_context*             ctx,
@@ -862,7 +904,7 @@ int execute_pusch_cb_plan(const srsgpu_pusch_cb_plan* plan,
 {
   launch_rate_dematch(plan->impl, plan->d_dm, plan->nof_cbs, d_llrs, d_harq, d_cb_crc_ok, s);
   HIP_TRY(hipGetLastError());
-  return execute_decoder_plan(plan->dec, d_harq, d_out, d_nof_iterations, d_cb_crc_ok, s);
+  return execute_decoder_plan(plan->dec, d_harq, d_out, d_nof_iterations, d_cb_crc_ok, s, d_llrs, d_harq);
 }
 
 } // namespace
@@ -926,6 +968,9 @@ void srsgpu_ldpc_decoder_plan_destroy(srsgpu_ldpc_decoder_plan* plan)
   for (auto& g : plan->groups) {
     if (g.d_desc != nullptr) {
       (void)hipFree(g.d_desc);
+    }
+    if (g.d_dm != nullptr) {
+      (void)hipFree(g.d_dm);
     }
   }
   delete plan;
@@ -1369,7 +1414,7 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
   HIP_TRY(hipGetLastError());
   stage_timer::mark(ev, 1, s);
   stage_timer::mark(evd, 0, s);
-  int r = execute_decoder_plan(plan->cbs->dec, d_harq, d_cb_msgs, d_cb_nof_iterations, d_cb_crc_ok, s);
+  int r = execute_decoder_plan(plan->cbs->dec, d_harq, d_cb_msgs, d_cb_nof_iterations, d_cb_crc_ok, s, d_llrs, d_harq);
   if (r != SRSGPU_OK) {
     return r;
   }

@@ -315,8 +315,10 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
   const int  msg_len = G::K * Z;
   uint8_t*   cb_out  = out + d.out_offset;
   if (input_size < msg_len) {
-    // Not enough LLRs: no decoding; without CRC the output is all ones (ldpc_decoder_impl.cpp:100).
-    if (!use_crc) {
+    // Not enough LLRs: no decoding; when the CRC is not the decoder's (no CRC, or checked by the caller after the
+    // last iteration: no early stop, pusch_codeblock_decoder passes no calculator) the output is all ones
+    // (ldpc_decoder_impl.cpp:95).
+    if (!use_crc || (d.flags & DEC_FLAG_EARLY_STOP) == 0) {
       for (int b = threadIdx.x; b < (msg_len + 7) / 8; b += blockDim.x) {
         cb_out[b] = 0xff;
       }

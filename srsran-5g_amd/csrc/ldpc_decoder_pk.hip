@@ -437,7 +437,11 @@ __device__ __forceinline__ void write_hard_bits_pk(const int8_t* __restrict__ so
 /// MAXL: compile-time bound on the number of layers (host-proven from the input length, dec_desc::nof_llr), so that
 /// only MAXL layers of check-to-variable state occupy VGPRs: the 4-layer high-rate codeblocks of a loaded cell run at
 /// twice the occupancy of the 46-layer worst case.
-template <int BG, int MODE, int MAXL, int SPLIT>
+/// FUSE: the codeblock is a first transmission whose rate dematching is a plain copy (rv 0, no limited buffer,
+/// ninfo <= E <= V: every systematic position is reached and nothing repeats): the kernel dematches the codeword LLRs
+/// itself (dms[blockIdx.x]) into the LDS image and writes the HARQ soft buffer the separate rate_dematch_kernel would
+/// have written (rate_dematcher.hip dematch_new_data: copies symbol-major, fillers +127, the unreached tail zeroed).
+template <int BG, int MODE, int MAXL, int SPLIT, bool FUSE>
 #ifndef LDPC_PK_MIN_BLOCKS_8
 #define LDPC_PK_MIN_BLOCKS_8 5
 #endif
@@ -450,7 +454,9 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
                                                              int32_t* __restrict__ results,
                                                              const uint32_t* __restrict__ ab_table,
                                                              const uint32_t* __restrict__ crc_tables,
-                                                             uint8_t* __restrict__ cb_crc_ok)
+                                                             uint8_t* __restrict__ cb_crc_ok,
+                                                             const dm_desc* __restrict__ dms,
+                                                             int8_t* __restrict__ harq)
 {
   using G = bg_t<BG>;
   // Only the first K + MAXL columns can be touched by MAXL layers: the soft-bit image shrinks with the layer bound
@@ -466,8 +472,13 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
   DEC_STAMP(0);
   DEC_PROF(29, __builtin_amdgcn_s_memrealtime());
   const dec_desc d = descs[blockIdx.x];
-  // HARQ context (pusch_decoder_impl.cpp:300): a codeblock whose CRC already passed is not decoded again.
-  if (cb_crc_ok != nullptr && cb_crc_ok[d.cb_index] != 0) {
+  if constexpr (FUSE) {
+    // New data invalidates the codeblock CRC flag of the HARQ context (pusch_decoder_impl.cpp:132).
+    if (cb_crc_ok != nullptr && threadIdx.x == 0) {
+      cb_crc_ok[d.cb_index] = 0;
+    }
+  } else if (cb_crc_ok != nullptr && cb_crc_ok[d.cb_index] != 0) {
+    // HARQ context (pusch_decoder_impl.cpp:300): a codeblock whose CRC already passed is not decoded again.
     if (threadIdx.x == 0) {
       results[d.cb_index] = 0;
     }
@@ -501,103 +512,165 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
   const uint32_t ncols = __umulhi(static_cast<uint32_t>(n_llr), d.div_magic);
   const uint32_t full  = ncols * static_cast<uint32_t>(Z);
   int            last  = -1;
-  {
-    const uint32_t head   = static_cast<uint32_t>(d.llr_offset) & 15u;
-    const uint4*   vecs   = reinterpret_cast<const uint4*>(llr - head);
-    const int      nvec   = static_cast<int>((head + static_cast<uint32_t>(n_llr) + 15u) >> 4);
-    // 16-B vectors per lane in flight: the whole input span of the layer bound at Z = 384 with 192 lanes.
-    constexpr int  BATCH  = ((NCOL - 2) * 384 / 16 + 191) / 192;
-    int            last_w = -1;
-    uint4          last_v = make_uint4(0u, 0u, 0u, 0u);
-    for (int w0 = threadIdx.x; w0 < nvec; w0 += BATCH * blockDim.x) {
-      uint4 val[BATCH];
+  if constexpr (FUSE) {
+    const dm_desc  dm    = dms[blockIdx.x];
+    const int      E     = static_cast<int>(dm.E), Qm = dm.Qm, R = E / Qm;
+    const int      Fl    = dm.nof_filler;
+    const int      ninfo = static_cast<int>(dm.nsys) - Fl;
+    const int      Nh    = static_cast<int>(dm.N);
+    const int8_t*  in    = llrs + dm.llr_offset;
+    int8_t*        hb    = harq + dm.harq_offset;
+    // The whole image starts at zero (punctured columns, positions beyond the input and the unreached tail).
+    {
+      uint4* s16 = reinterpret_cast<uint4*>(soft);
+      for (int q = threadIdx.x; q < NCOL * SOFT_COL_STRIDE / 16; q += blockDim.x) {
+        s16[q] = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    __syncthreads();
+    // Decoder input clamp (ldpc_decoder_impl.cpp:152): +/-64 in the whole lifted columns of the input, the
+    // reference's LLR range (+/-infinity kept) in a trailing partial column; trailing-zero trim over [0, n_llr).
+    auto put = [&](int k, int v) {
+      hb[k] = static_cast<int8_t>(v);
+      if (static_cast<uint32_t>(k) < static_cast<uint32_t>(n_llr)) {
+        last              = (v != 0 && k > last) ? k : last;
+        const uint32_t cq = __umulhi(static_cast<uint32_t>(k), d.div_magic);
+        const int      cv = (static_cast<uint32_t>(k) < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
+        soft[(cq + 2) * SOFT_COL_STRIDE + pair_pos(static_cast<uint32_t>(k) - cq * static_cast<uint32_t>(Z), H)] =
+            static_cast<int8_t>(cv);
+      }
+    };
+    // Copies, symbol-major: lane r reads the Qm LLRs of symbol r and stores bit j at visit n = j R + r (position k =
+    // n, past the fillers once n >= ninfo); for a fixed j the lanes' HARQ stores are consecutive bytes.
+    const bool q8 = Qm == 8 && ((dm.llr_offset & 7u) == 0u);
+    for (int r = threadIdx.x; r < R; r += blockDim.x) {
+      int8_t sym[8];
+      if (q8) {
+        const uint2 v = *reinterpret_cast<const uint2*>(in + 8 * r);
 #pragma unroll
-      for (int j = 0; j < BATCH; ++j) {
-        const int w = w0 + j * blockDim.x;
-        val[j]      = (w < nvec) ? vecs[w] : make_uint4(0u, 0u, 0u, 0u);
+        for (int j = 0; j < 8; ++j) {
+          sym[j] = static_cast<int8_t>(((j < 4) ? v.x : v.y) >> (8 * (j & 3)));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sym[j] = (j < Qm) ? in[r * Qm + j] : 0;
+        }
       }
 #pragma unroll
-      for (int j = 0; j < BATCH; ++j) {
-        const int w = w0 + j * blockDim.x;
-        if (w >= nvec) {
-          continue;
+      for (int j = 0; j < 8; ++j) {
+        if (j < Qm) {
+          const int n = j * R + r;
+          put(n < ninfo ? n : n + Fl, sym[j]);
         }
-        const uint32_t i0 = static_cast<uint32_t>(16 * w) - head;
-        const uint32_t c0 = __umulhi(i0, d.div_magic);
-        const uint32_t l0 = i0 - c0 * static_cast<uint32_t>(Z);
-        // Short path: the 16 LLRs lie in one column (every vector but the unaligned head and the input's tail). A
-        // vector may straddle the column's half boundary H: byte k >= H - l0 goes to 2 (l - H) + 1 instead of 2 l,
-        // i.e. its address moves by 1 - 2H (one bit-extract and one 24-bit multiply-add per byte, no branch), so a
-        // wave's straddling lane does not drag the whole wave through the per-byte general path.
-        const bool short_path = (16u * static_cast<uint32_t>(w) >= head) && (i0 + 16u <= full) &&
-                                (l0 + 16u <= static_cast<uint32_t>(Z));
-        if (short_path) {
-          int8_t*        dst   = soft + (c0 + 2) * SOFT_COL_STRIDE + pair_pos(l0, H);
-          const uint32_t cross = (l0 < H && l0 + 16u > H) ? (0xffffu << (H - l0)) : 0u;  // bit k: byte k moves
-          const int      adj   = 1 - 2 * static_cast<int>(H);
+      }
+    }
+    // Fillers: +infinity (ldpc_rate_dematcher_impl.cpp:172); then the unreached tail [E + F, N) zeroed.
+    for (int k = ninfo + static_cast<int>(threadIdx.x); k < ninfo + Fl; k += blockDim.x) {
+      put(k, 127);
+    }
+    for (int k = E + Fl + static_cast<int>(threadIdx.x); k < Nh; k += blockDim.x) {
+      hb[k] = 0;
+    }
+  } else {
+    {
+      const uint32_t head   = static_cast<uint32_t>(d.llr_offset) & 15u;
+      const uint4*   vecs   = reinterpret_cast<const uint4*>(llr - head);
+      const int      nvec   = static_cast<int>((head + static_cast<uint32_t>(n_llr) + 15u) >> 4);
+      // 16-B vectors per lane in flight: the whole input span of the layer bound at Z = 384 with 192 lanes.
+      constexpr int  BATCH  = ((NCOL - 2) * 384 / 16 + 191) / 192;
+      int            last_w = -1;
+      uint4          last_v = make_uint4(0u, 0u, 0u, 0u);
+      for (int w0 = threadIdx.x; w0 < nvec; w0 += BATCH * blockDim.x) {
+        uint4 val[BATCH];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
+        for (int j = 0; j < BATCH; ++j) {
+          const int w = w0 + j * blockDim.x;
+          val[j]      = (w < nvec) ? vecs[w] : make_uint4(0u, 0u, 0u, 0u);
+        }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int kk  = 4 * q + k;
-              const int mv  = static_cast<int>((cross >> kk) & 1u) * adj;
-              dst[2 * kk + mv] = static_cast<int8_t>(clamp_i(static_cast<int8_t>(word >> (8 * k)), -64, 64));
+        for (int j = 0; j < BATCH; ++j) {
+          const int w = w0 + j * blockDim.x;
+          if (w >= nvec) {
+            continue;
+          }
+          const uint32_t i0 = static_cast<uint32_t>(16 * w) - head;
+          const uint32_t c0 = __umulhi(i0, d.div_magic);
+          const uint32_t l0 = i0 - c0 * static_cast<uint32_t>(Z);
+          // Short path: the 16 LLRs lie in one column (every vector but the unaligned head and the input's tail). A
+          // vector may straddle the column's half boundary H: byte k >= H - l0 goes to 2 (l - H) + 1 instead of 2 l,
+          // i.e. its address moves by 1 - 2H (one bit-extract and one 24-bit multiply-add per byte, no branch), so a
+          // wave's straddling lane does not drag the whole wave through the per-byte general path.
+          const bool short_path = (16u * static_cast<uint32_t>(w) >= head) && (i0 + 16u <= full) &&
+                                  (l0 + 16u <= static_cast<uint32_t>(Z));
+          if (short_path) {
+            int8_t*        dst   = soft + (c0 + 2) * SOFT_COL_STRIDE + pair_pos(l0, H);
+            const uint32_t cross = (l0 < H && l0 + 16u > H) ? (0xffffu << (H - l0)) : 0u;  // bit k: byte k moves
+            const int      adj   = 1 - 2 * static_cast<int>(H);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const int kk  = 4 * q + k;
+                const int mv  = static_cast<int>((cross >> kk) & 1u) * adj;
+                dst[2 * kk + mv] = static_cast<int8_t>(clamp_i(static_cast<int8_t>(word >> (8 * k)), -64, 64));
+              }
             }
-          }
-          if ((val[j].x | val[j].y | val[j].z | val[j].w) != 0u) {
-            last_w = w;
-            last_v = val[j];
-          }
-        } else {
+            if ((val[j].x | val[j].y | val[j].z | val[j].w) != 0u) {
+              last_w = w;
+              last_v = val[j];
+            }
+          } else {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const uint32_t i = i0 + static_cast<uint32_t>(4 * q + k);
-              if (i < static_cast<uint32_t>(n_llr)) {
-                int v = static_cast<int8_t>(word >> (8 * k));
-                last  = (v != 0) ? static_cast<int>(i) : last;
-                v     = (i < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
-                const uint32_t cq = __umulhi(i, d.div_magic);
-                soft[(cq + 2) * SOFT_COL_STRIDE + pair_pos(i - cq * static_cast<uint32_t>(Z), H)] =
-                    static_cast<int8_t>(v);
+              for (int k = 0; k < 4; ++k) {
+                const uint32_t i = i0 + static_cast<uint32_t>(4 * q + k);
+                if (i < static_cast<uint32_t>(n_llr)) {
+                  int v = static_cast<int8_t>(word >> (8 * k));
+                  last  = (v != 0) ? static_cast<int>(i) : last;
+                  v     = (i < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
+                  const uint32_t cq = __umulhi(i, d.div_magic);
+                  soft[(cq + 2) * SOFT_COL_STRIDE + pair_pos(i - cq * static_cast<uint32_t>(Z), H)] =
+                      static_cast<int8_t>(v);
+                }
               }
             }
           }
         }
       }
-    }
-    if (last_w >= 0) {
-      const uint32_t words[4] = {last_v.x, last_v.y, last_v.z, last_v.w};
-      int            hb       = 0;
+      if (last_w >= 0) {
+        const uint32_t words[4] = {last_v.x, last_v.y, last_v.z, last_v.w};
+        int            hb       = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        hb = (words[q] != 0u) ? 4 * q + (31 - __clz(static_cast<int>(words[q]))) / 8 : hb;
+        for (int q = 0; q < 4; ++q) {
+          hb = (words[q] != 0u) ? 4 * q + (31 - __clz(static_cast<int>(words[q]))) / 8 : hb;
+        }
+        const int i = 16 * last_w - static_cast<int>(head) + hb;
+        last        = i > last ? i : last;
       }
-      const int i = 16 * last_w - static_cast<int>(head) + hb;
-      last        = i > last ? i : last;
     }
-  }
-  // Zero the punctured columns 0, 1 and every position beyond the input.
-  if (active && half == 0) {
-    auto* soft16 = reinterpret_cast<uint16_t*>(soft);
-    soft16[(0 * SOFT_COL_STRIDE) / 2 + z] = 0;
-    soft16[(1 * SOFT_COL_STRIDE) / 2 + z] = 0;
-    int c = 2 + static_cast<int>(ncols);
-    if (static_cast<uint32_t>(n_llr) > full) {
-      const uint32_t rem = static_cast<uint32_t>(n_llr) - full;
-      if (static_cast<uint32_t>(z) >= rem) {
-        soft[c * SOFT_COL_STRIDE + 2 * z] = 0;
+    // Zero the punctured columns 0, 1 and every position beyond the input.
+    if (active && half == 0) {
+      auto* soft16 = reinterpret_cast<uint16_t*>(soft);
+      soft16[(0 * SOFT_COL_STRIDE) / 2 + z] = 0;
+      soft16[(1 * SOFT_COL_STRIDE) / 2 + z] = 0;
+      int c = 2 + static_cast<int>(ncols);
+      if (static_cast<uint32_t>(n_llr) > full) {
+        const uint32_t rem = static_cast<uint32_t>(n_llr) - full;
+        if (static_cast<uint32_t>(z) >= rem) {
+          soft[c * SOFT_COL_STRIDE + 2 * z] = 0;
+        }
+        if (static_cast<uint32_t>(z) + H >= rem) {
+          soft[c * SOFT_COL_STRIDE + 2 * z + 1] = 0;
+        }
+        ++c;
       }
-      if (static_cast<uint32_t>(z) + H >= rem) {
-        soft[c * SOFT_COL_STRIDE + 2 * z + 1] = 0;
+      for (; c < NCOL; ++c) {
+        soft16[(c * SOFT_COL_STRIDE) / 2 + z] = 0;
       }
-      ++c;
-    }
-    for (; c < NCOL; ++c) {
-      soft16[(c * SOFT_COL_STRIDE) / 2 + z] = 0;
     }
   }
   last = wave_max(last);
@@ -617,8 +690,10 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
   uint8_t*   cb_out  = out + d.out_offset;
   const bool use_crc = d.crc_table != NO_CRC_TABLE;
   if (input_size < msg_len) {
-    // Not enough LLRs: no decoding; without CRC the output is all ones (ldpc_decoder_impl.cpp:100).
-    if (!use_crc) {
+    // Not enough LLRs: no decoding; when the CRC is not the decoder's (no CRC, or checked by the caller after the
+    // last iteration: no early stop, pusch_codeblock_decoder passes no calculator) the output is all ones
+    // (ldpc_decoder_impl.cpp:95).
+    if (!use_crc || (d.flags & DEC_FLAG_EARLY_STOP) == 0) {
       for (int b = threadIdx.x; b < (msg_len + 7) / 8; b += blockDim.x) {
         cb_out[b] = 0xff;
       }
@@ -1020,8 +1095,10 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
       input_size += 1;
       __syncthreads();  // wlast is reused by the next slot
       if (input_size < msg_len) {
-        // Not enough LLRs: no decoding; without CRC the output is all ones (ldpc_decoder_impl.cpp:100).
-        if (!use_crc) {
+        // Not enough LLRs: no decoding; when the CRC is not the decoder's (no CRC, or checked by the caller after the
+        // last iteration: no early stop, pusch_codeblock_decoder passes no calculator) the output is all ones
+        // (ldpc_decoder_impl.cpp:95).
+        if (!use_crc || (d0.flags & DEC_FLAG_EARLY_STOP) == 0) {
           for (int b = threadIdx.x; b < (msg_len + 7) / 8; b += blockDim.x) {
             out[d.out_offset + b] = 0xff;
           }
@@ -1196,17 +1273,22 @@ void launch_ldpc_decode_pk(int             bg,
                            const uint32_t* d_ab,
                            const uint32_t* d_crc_tables,
                            uint8_t*        d_cb_crc_ok,
+                           const dm_desc*  d_dm,
+                           int8_t*         d_harq,
                            hipStream_t     stream)
 {
   if (nof_cbs <= 0) {
     return;
   }
   dim3 grid(nof_cbs), block(block_threads);
+  const bool fuse = d_dm != nullptr;
+#define SRSGPU_PK_LAUNCH1(BG_, MODE_, MAXL_, SPLIT_)                                                                   \
+  (fuse ? ldpc_decode_pk_kernel<BG_, MODE_, MAXL_, SPLIT_, true><<<grid, block, 0, stream>>>(                          \
+              d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables, d_cb_crc_ok, d_dm, d_harq)                        \
+        : ldpc_decode_pk_kernel<BG_, MODE_, MAXL_, SPLIT_, false><<<grid, block, 0, stream>>>(                         \
+              d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables, d_cb_crc_ok, nullptr, nullptr))
 #define SRSGPU_PK_LAUNCH(BG_, MODE_, MAXL_)                                                                            \
-  (split == 2 ? ldpc_decode_pk_kernel<BG_, MODE_, MAXL_, 2><<<grid, block, 0, stream>>>(                              \
-                    d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables, d_cb_crc_ok)                               \
-              : ldpc_decode_pk_kernel<BG_, MODE_, MAXL_, 1><<<grid, block, 0, stream>>>(                              \
-                    d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables, d_cb_crc_ok))
+  (split == 2 ? SRSGPU_PK_LAUNCH1(BG_, MODE_, MAXL_, 2) : SRSGPU_PK_LAUNCH1(BG_, MODE_, MAXL_, 1))
   if (bg == 1) {
     if (max_layers <= 8) {
       mode == 1 ? SRSGPU_PK_LAUNCH(1, 1, 8) : SRSGPU_PK_LAUNCH(1, 0, 8);
@@ -1225,6 +1307,7 @@ void launch_ldpc_decode_pk(int             bg,
     }
   }
 #undef SRSGPU_PK_LAUNCH
+#undef SRSGPU_PK_LAUNCH1
 }
 
 void launch_ldpc_decode_pk4(int             bg,

@@ -33,6 +33,9 @@ static_assert(sizeof(dec_desc) == 40, "dec_desc layout");
 
 /// dec_desc::flags: check the CRC after every iteration (early stop) instead of once after max_iter.
 constexpr uint32_t DEC_FLAG_EARLY_STOP = 1u;
+/// dec_desc::flags: the decoder launch dematches the codeblock itself (a first transmission with a copy-only rate
+/// dematching, see ldpc_decode_pk_kernel FUSE); d_llrs is then the codeword LLR buffer and d_dm its dm_desc.
+constexpr uint32_t DEC_FLAG_FUSED_DM = 2u;
 
 /// Per-codeblock work item of the rate dematcher (rate_dematcher.hip).
 struct dm_desc {
@@ -200,6 +203,8 @@ void launch_ldpc_decode_pk(int             bg,
                            const uint32_t* d_ab,
                            const uint32_t* d_crc_tables,
                            uint8_t*        d_cb_crc_ok,
+                           const dm_desc*  d_dm,
+                           int8_t*         d_harq,
                            hipStream_t     stream);
 
 /// Codeblocks per workgroup of the multi-codeblock packed decoder (ldpc_decode_pk4_kernel).

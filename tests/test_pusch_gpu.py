@@ -185,3 +185,58 @@ def test_pusch_decoder_large_unaligned_tbs(orc, ctx):
                                                                          new_data=True, nof_ldpc_iterations=6)])
     assert len(iters[0]) == 63 and ok[0], (len(iters[0]), ok[0])
     assert np.array_equal(got[0], tb)
+
+
+@pytest.mark.parametrize("dec_type,mode", [("avx2", 1), ("generic", 0)])
+def test_fused_rate_dematch_in_decoder(orc, ctx, monkeypatch, dec_type, mode):
+    """First transmissions that are a plain copy (rv 0, no LBRM, ninfo <= E <= V, even Z) are dematched inside the
+    packed decoder (DEC_FLAG_FUSED_DM): 160 such codeblocks mixed with 40 that keep the separate rate dematcher, over a
+    HARQ buffer of random old content; iterations, bits, HARQ buffer and CRC flags equal the oracle composition and the
+    unfused plan (SRSGPU_DECODER_FUSED_DM=0)."""
+    import srsgpu
+    rng = np.random.default_rng(404 + mode)
+    cbs, llrs, inits = [], [], []
+    while len(cbs) < 200:
+        fusable = len(cbs) < 160
+        bg = int(rng.integers(1, 3))
+        Z = int(rng.choice([2, 4, 16, 36, 64, 112, 144, 208, 288, 384] if fusable else [3, 5, 64, 384]))
+        N = BG_N_SHORT[bg] * Z
+        nsys = (BG_K[bg] - 2) * Z
+        qm = int(rng.choice([1, 2, 4, 6, 8]))
+        F = int(rng.integers(0, nsys // 3 + 1))
+        ninfo = nsys - F
+        if fusable:
+            lo, hi = -(-ninfo // qm), (N - F) // qm
+            if lo > hi:
+                continue
+            E, rv, Nref = qm * int(rng.integers(lo, hi + 1)), 0, 0
+        else:
+            E, rv, Nref = qm * int(rng.integers(1, 2 * N // qm)), int(rng.integers(0, 4)), 0
+        cbs.append(srsgpu.PuschCodeblock(bg, Z, rv, qm, E, nof_filler_bits=F, Nref=Nref, new_data=True,
+                                         use_early_stop=bool(rng.integers(0, 2)), max_iterations=4))
+        # Mostly a noisy all-zero codeword (decodes, CRC passes), a quarter pure noise (fails).
+        amp = 0.0 if rng.random() < 0.25 else 10.0
+        llrs.append(np.clip(np.round(amp + 4.0 * rng.standard_normal(E)), -127, 127).astype(np.int8))
+        inits.append(rng.integers(-127, 128, N).astype(np.int8))
+    init = np.concatenate(inits)
+    dec = srsgpu.PuschCodeblockDecoder(ctx, dec_type)
+    res_f, harq_f, crc_f = dec.decode(llrs, cbs, harq=init.copy())
+    monkeypatch.setenv("SRSGPU_DECODER_FUSED_DM", "0")
+    res_u, harq_u, crc_u = dec.decode(llrs, cbs, harq=init.copy())
+    monkeypatch.delenv("SRSGPU_DECODER_FUSED_DM")
+    assert np.array_equal(harq_f, harq_u)
+    assert np.array_equal(np.asarray(crc_f), np.asarray(crc_u))
+    off, n_ok = 0, 0
+    for i, (c, llr, h0) in enumerate(zip(cbs, llrs, inits)):
+        r, bits, h2, ok2 = oracle_pusch_cb_decode(orc, mode, c, llr, h0, False)
+        N = BG_N_SHORT[c.base_graph] * c.lifting_size
+        assert np.array_equal(harq_f[off:off + N], h2), (i, c)
+        off += N
+        for res in (res_f, res_u):
+            r_g, bits_g = res[i]
+            assert (r_g if r_g is not None else -1) == r, (i, c)
+            if bits is not None:
+                assert np.array_equal(bits_g, bits), (i, c)
+        assert bool(crc_f[i]) == ok2, (i, c)
+        n_ok += ok2
+    assert 30 <= n_ok < 200

@@ -405,6 +405,19 @@ def measure(args, env):
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    skip = [s for s in os.environ.get("SRSGPU_BENCH_SKIP", "").split(",") if s]
+    if skip:
+        # Timing experiment only (stage sensitivity: how much of the overlapped step each stage costs): the named
+        # stages' launches are dropped from the captured step; their outputs keep the warm-up's values (same inputs
+        # every step). The line is marked and is not a valid measurement.
+        for st in sets:
+            plans = {"encode": [d.encoder for d in st.dls], "dmrs": [d.dmrs for d in st.dls],
+                     "modulate": [d.modulator for d in st.dls], "ofdm_mod": [d.ofdm for d in st.dls],
+                     "ofdm_demod": [st.ul.ofdm], "chest": [st.ul.chest], "demod": [st.ul.demod],
+                     "decode": [st.ul.decoder]}
+            for s in skip:
+                for p in plans[s]:
+                    p.execute = lambda *a, **k: None
     if args.graph:
         # One hipGraph per input set of the whole per-step pipeline (every plan is allocation-free and capture-safe):
         # the kernels, the codeword memset and the stream fork/join replay as one graph launch per step.
@@ -493,8 +506,8 @@ def measure(args, env):
         dec_ms_tot += ms[1]
         dec_n += n
         st.ul.decoder.enable_timing(False)
-    assert dec_n == n_dec
-    dec_ms = dec_ms_tot / dec_n
+    assert dec_n == n_dec or "decode" in skip
+    dec_ms = dec_ms_tot / dec_n if dec_n else float("nan")
     # Per-stage times: another untimed eager pass with events between the stages.
     n_stage = min(steps, 200)
     evs = [([torch.cuda.Event(enable_timing=True) for _ in range(4)],
@@ -663,6 +676,8 @@ def measure(args, env):
         "roofline_valu": valu,
         "cpu_baseline": None,
     }
+    if skip:
+        result["INVALID_timing_experiment_skipped_stages"] = skip
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         n_dl, n_ul = len(dl_segs), len(ul_segs)
         tb_host = st0.dl_tbs[: sum(dl.tb_bytes[:n_dl])].cpu().numpy()

@@ -1,0 +1,10 @@
+# Round 3 re-entry check: full GPU parity suite, smoke, and the default bench (the driver's plain command shape).
+set -o pipefail
+OUT=gpurun_out/r3u
+mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+rc=$?; tail -3 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
+tail -2 $OUT/smoke.log
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || exit $?
+tail -c 600 $OUT/bench.json

@@ -292,6 +292,7 @@ bool build_core_plan(int bg, int Z, core_plan& cp)
     return false;
   }
   cp.x       = static_cast<int16_t>(x);
+  cp.o0      = static_cast<int16_t>((Z - x) % Z);
   bool known[4] = {true, false, false, false};
   int  step     = 0;
   for (int round = 0; round < 4 && step < 3; ++round) {
@@ -308,8 +309,11 @@ bool build_core_plan(int bg, int Z, core_plan& cp)
       }
       cp.unk[step] = static_cast<int8_t>(u);
       cp.row[step] = static_cast<int8_t>(m);
+      const int su  = sh[m][u];
+      cp.orow[step] = static_cast<int16_t>((Z - su) % Z);
       for (int j = 0; j < 4; ++j) {
         cp.sh[step][j] = static_cast<int16_t>(sh[m][j]);
+        cp.oj[step][j] = static_cast<int16_t>((j != u && sh[m][j] >= 0) ? (sh[m][j] - su + Z) % Z : -1);
       }
       known[u] = true;
       ++step;
@@ -1146,6 +1150,7 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
       d.filler         = static_cast<uint16_t>(seg.filler);
       d.tb_crc_len     = static_cast<uint8_t>(seg.tb_crc_len);
       d.Qm             = static_cast<uint8_t>(qm);
+      d.tb_crc_table   = tbd[t].table;
       // Last circular-buffer position the rate matcher reads -> extension parity rows to compute.
       int kmax;
       if (cb.E >= V - v0) {
@@ -1205,7 +1210,9 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
     srsgpu_pdsch_encoder_plan_destroy(plan);
     return fail(SRSGPU_ERR_HIP, "failed to upload encoder descriptors");
   }
-  plan->inline_tb_crc = plan->count[0] == 0 && plan->count[1] == 0 &&
+  // SRSGPU_ENCODER_TB_CRC_INLINE=0: always the separate tb_crc_kernel (A/B).
+  const char* inl_env = std::getenv("SRSGPU_ENCODER_TB_CRC_INLINE");
+  plan->inline_tb_crc = (inl_env == nullptr || inl_env[0] != '0') && plan->count[0] == 0 && plan->count[1] == 0 &&
                         std::all_of(tbd.begin(), tbd.end(), [](const tb_crc_desc& t) {
                           return t.table != NO_CRC_TABLE && t.nbytes <= TB_CRC_INLINE_MAX_BYTES;
                         });
@@ -1476,6 +1483,13 @@ void srsgpu_pusch_decoder_plan_destroy(srsgpu_pusch_decoder_plan* plan)
 int srsgpu_debug_decoder_profile(uint64_t* dst, uint32_t n, int packed)
 {
   return packed ? srsgpu::debug_read_decoder_profile_pk(dst, n) : srsgpu::debug_read_decoder_profile(dst, n);
+}
+#endif
+#ifdef ENC_PROFILE
+/// Instrumented builds only: phase stamps of the last packed-encoder launch (ldpc_encoder.hip, ENC_STAMP).
+int srsgpu_debug_encoder_profile(uint64_t* dst, uint32_t n)
+{
+  return srsgpu::debug_read_encoder_profile(dst, n);
 }
 #endif
 

@@ -154,19 +154,33 @@ __device__ __forceinline__ uint32_t gf2_mulmod(uint32_t r, uint32_t M, int order
 /// returns the CRC in every lane.
 /// [begin, end) (begin a multiple of CS; default the whole message) restricts the sum to that byte range's chunks: their
 /// contribution to the CRC of the whole nbytes-byte message (the CRC is linear, so slices XOR together).
+/// The power M of chunk c of an nbytes-byte message (see block_crc_chunks), for a caller that issues the table load
+/// early (c < number of chunks).
+template <int CS>
+__device__ __forceinline__ uint32_t crc_chunk_power(int c, int nbytes, const uint32_t* P, int order)
+{
+  const int L  = 8 * nbytes;
+  const int b1 = min((c + 1) * CS, nbytes);
+  const int j  = 8 * b1 + order - 1;
+  return (j < L) ? P[j] : (1u << (order + L - 1 - j));
+}
+
 template <int CS, typename Data>
 __device__ inline uint32_t block_crc_chunks(Data data, int nbytes, const uint32_t* P, int order, uint32_t g,
-                                            const uint32_t* lut, uint32_t* red, int begin = 0, int end = -1)
+                                            const uint32_t* lut, uint32_t* red, int begin = 0, int end = -1,
+                                            bool have_m0 = false, uint32_t m0 = 0)
 {
   const uint32_t mask = (1u << order) - 1u;
   const int      L    = 8 * nbytes;
   const int      nch  = ((end < 0 ? nbytes : end) + CS - 1) / CS;
+  const int      c0   = begin / CS + static_cast<int>(threadIdx.x);
   uint32_t       acc  = 0;
-  for (int c = begin / CS + static_cast<int>(threadIdx.x); c < nch; c += blockDim.x) {
+  for (int c = c0; c < nch; c += blockDim.x) {
     const int b0  = c * CS;
     const int b1  = min(b0 + CS, nbytes);
     const int j   = 8 * b1 + order - 1;
-    const uint32_t M = (j < L) ? P[j] : (1u << (order + L - 1 - j));  // issued before the chunk's serial chain
+    // Issued before the chunk's serial chain; m0 = the lane's first power, loaded by the caller (crc_chunk_power).
+    const uint32_t M = (have_m0 && c == c0) ? m0 : ((j < L) ? P[j] : (1u << (order + L - 1 - j)));
     // The chunk's bytes are all loaded before the table chain starts (a rolled loop waited for each load in turn).
     uint32_t byte[CS];
 #pragma unroll

@@ -21,6 +21,24 @@
 namespace srsgpu {
 namespace {
 
+#ifdef ENC_PROFILE
+// Instrumented builds only (tools/encoder_phase_profile.py): s_memtime per phase of the first ENC_PROF_CBS codeblocks.
+constexpr int ENC_PROF_CBS   = 8192;
+constexpr int ENC_PROF_SLOTS = 16;
+__device__ uint64_t g_enc_prof[ENC_PROF_CBS * ENC_PROF_SLOTS];
+#define ENC_PROF(slot, value)                                                                                          \
+  do {                                                                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < ENC_PROF_CBS) {                                                               \
+      g_enc_prof[blockIdx.x * ENC_PROF_SLOTS + (slot)] = (value);                                                      \
+    }                                                                                                                  \
+  } while (0)
+#else
+#define ENC_PROF(slot, value)                                                                                          \
+  do {                                                                                                                 \
+  } while (0)
+#endif
+#define ENC_STAMP(slot) ENC_PROF(slot, __builtin_amdgcn_s_memtime())
+
 template <int BG>
 struct ebg;
 template <>
@@ -43,6 +61,17 @@ struct ebg<2> {
 };
 
 constexpr int S = SOFT_COL_STRIDE;
+
+/// Largest degree of the four core rows.
+template <int BG>
+constexpr int core_max_degree()
+{
+  int d = 0;
+  for (int m = 0; m < 4; ++m) {
+    d = (ebg<BG>::rs(m + 1) - ebg<BG>::rs(m) > d) ? ebg<BG>::rs(m + 1) - ebg<BG>::rs(m) : d;
+  }
+  return d;
+}
 
 __device__ __forceinline__ int rot(int z, int s, int Z)
 {
@@ -383,14 +412,69 @@ __device__ __forceinline__ uint32_t spread_bits(uint32_t x)
 /// words: stream bit t = Qm i + j carries e[j R + i]. Words wholly inside the codeblock with symbol-aligned bits
 /// (Qm in {1, 2, 4, 8}, g0 % Qm == 0) take one e window per bit row j; the rest (the two boundary words, Qm = 6,
 /// unaligned offsets) are assembled bit by bit.
+/// Exchanges the bits of a selected by mask m << k with the bits of b selected by m (one delta swap).
+__device__ __forceinline__ void delta_swap(uint32_t& a, uint32_t& b, int k, uint32_t m)
+{
+  const uint32_t t = ((a >> k) ^ b) & m;
+  b ^= t;
+  a ^= t << k;
+}
+
+/// 256QAM groups (ldpc_rate_matcher_impl.cpp:150 interleaving, Qm = 8): 32 consecutive modulation symbols i0 .. i0 + 31
+/// from one 32-bit circular-buffer window per bit row j (r_j bit s = e[j R + i0 + s]), transposed as four 8 x 8 bit
+/// blocks by three rounds of delta swaps (rows fed in reverse, so each symbol's byte comes out MSB first) into the 8
+/// output words of the group: 8 windows and ~70 VALU for 8 words instead of 8 windows and ~20 VALU per word.
+__device__ __forceinline__ void rate_match_group8(const pk_rm& rm, int R, int i0, uint32_t* __restrict__ out)
+{
+  uint32_t r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    r[j] = rm.window<32>(static_cast<uint32_t>((7 - j) * R + i0));
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    delta_swap(r[j], r[j + 4], 4, 0x0f0f0f0fu);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if ((j & 2) == 0) {
+      delta_swap(r[j], r[j + 2], 2, 0x33333333u);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    delta_swap(r[j], r[j + 1], 1, 0x55555555u);
+  }
+  // Now byte c of r[j] is symbol 8 c + j: output word t = symbols 4 t .. 4 t + 3 = byte t / 2 of r[4 (t & 1) + q].
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int      c  = t >> 1;
+    const uint32_t* q = r + 4 * (t & 1);
+    const uint32_t lo = __builtin_amdgcn_perm(q[1], q[0], 0x0c0c0400u + 0x0101u * static_cast<uint32_t>(c));
+    const uint32_t hi = __builtin_amdgcn_perm(q[3], q[2], 0x04000c0cu + 0x01010000u * static_cast<uint32_t>(c));
+    out[t]            = lo | hi;
+  }
+}
+
 template <int QM>
 __device__ __forceinline__ void rate_match_packed(const enc_desc& d, const pk_rm& rm, uint32_t* __restrict__ out_words)
 {
   const int      E  = static_cast<int>(d.E), R = E / QM;
   const uint32_t g0 = d.out_bit_offset;
-  const uint32_t w0 = g0 / 32u, w1 = (g0 + static_cast<uint32_t>(E) - 1u) / 32u;
+  const uint32_t w1 = (g0 + static_cast<uint32_t>(E) - 1u) / 32u;
+  uint32_t       w0 = g0 / 32u;
   constexpr bool pow2   = (QM == 1 || QM == 2 || QM == 4 || QM == 8);
   const bool     align  = pow2 && (g0 % QM) == 0;
+  if constexpr (QM == 8) {
+    if ((g0 & 31u) == 0u) {
+      // Whole 32-symbol groups by transposition; the remaining words below.
+      const int ng = R / 32;
+      for (int g = threadIdx.x; g < ng; g += blockDim.x) {
+        rate_match_group8(rm, R, 32 * g, out_words + w0 + 8u * static_cast<uint32_t>(g));
+      }
+      w0 += 8u * static_cast<uint32_t>(ng);
+    }
+  }
   for (uint32_t w = w0 + threadIdx.x; w <= w1; w += blockDim.x) {
     const int t0   = static_cast<int>(w * 32u - g0);
     const bool full = t0 >= 0 && t0 + 32 <= E;
@@ -443,127 +527,242 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
   __shared__ uint32_t lut[256];
   __shared__ uint32_t red[PK_THREADS / WAVE];
 
+  ENC_STAMP(0);
+  ENC_PROF(9, __builtin_amdgcn_s_memrealtime());
+  __shared__ uint32_t lut_b[256];                  // CRC24B byte table
   const enc_desc d   = descs[blockIdx.x];
   const int      Z   = d.Z;
   const int      W   = Z / 32;
   const int      K   = G::K;
   const int      nkb = K * Z / 8;  // message bytes
   const int      tid = static_cast<int>(threadIdx.x);
-  {
-    // Every lane's table loads in flight at once, then the stores (a rolled loop waits for each load in turn).
-    constexpr int NEL = (G::NE + PK_THREADS - 1) / PK_THREADS;
-    uint32_t      ev[NEL];
+  const uint8_t* tb  = tbs + d.tb_byte_offset;
+  const int      nd8 = d.nof_data / 8;
+  // Every global load that depends only on the descriptor is issued up front (edge table, message bytes, the CB CRC's
+  // chunk power, the TB CRC word), so their latencies overlap instead of adding up.
+  constexpr int NEL = (G::NE + PK_THREADS - 1) / PK_THREADS;
+  uint32_t      ev[NEL];
 #pragma unroll
-    for (int r = 0; r < NEL; ++r) {
-      const int e = tid + r * PK_THREADS < G::NE ? tid + r * PK_THREADS : G::NE - 1;
-      ev[r]       = (static_cast<uint32_t>(G::col(e)) << 16) | shift_table[static_cast<uint32_t>(d.zpos) * G::NE + e];
-    }
+  for (int r = 0; r < NEL; ++r) {
+    const int e = tid + r * PK_THREADS < G::NE ? tid + r * PK_THREADS : G::NE - 1;
+    ev[r]       = (static_cast<uint32_t>(G::col(e)) << 16) | shift_table[static_cast<uint32_t>(d.zpos) * G::NE + e];
+  }
+  // All of a lane's message bytes are loaded before any is stored (the address is clamped into the TB so the loads
+  // are unconditional).
+  constexpr int  MB    = (G::K * 384 / 8 + PK_THREADS - 1) / PK_THREADS;
+  const uint32_t tb_hi = d.tb_bits >= 8u ? (d.tb_bits - 8u) >> 3 : 0u;
+  uint32_t       byte[MB];
 #pragma unroll
-    for (int r = 0; r < NEL; ++r) {
-      if (tid + r * PK_THREADS < G::NE) {
-        edge[tid + r * PK_THREADS] = ev[r];
+  for (int r = 0; r < MB; ++r) {
+    const int      q  = tid + r * PK_THREADS;
+    const uint32_t p  = d.tb_bit_offset + 8u * static_cast<uint32_t>(q);
+    const uint32_t pb = p >> 3;
+    byte[r]           = (q < nd8) ? tb[pb < tb_hi ? pb : tb_hi] : 0u;
+  }
+  constexpr int CB_CS    = 8;
+  const bool    has_cbc  = d.crc_table != NO_CRC_TABLE;
+  const int     cb_bytes = static_cast<int>(d.used) / 8;
+  const bool    pre_m    = has_cbc && tid < (cb_bytes + CB_CS - 1) / CB_CS;
+  const uint32_t m0      = pre_m ? crc_chunk_power<CB_CS>(tid, cb_bytes, crc_tables + d.crc_table, 24) : 0u;
+  uint32_t       tb_crc  = (tb_descs == nullptr) ? tb_crcs[d.tb_index] : 0u;  // from tb_crc_kernel
+  // Inline TB CRC (every TB of the plan has a contribution table): the workgroup of the codeblock that carries the TB
+  // CRC computes it, the others never need it (no separate tb_crc_kernel launch and dependency). TBs of at most
+  // 2 x 16 bytes per lane with 4-byte aligned offset and size (every multi-UE slot TB): each lane's two 16-byte chunks
+  // and their powers are loaded here with everything else, and the two chunk chains run interleaved below.
+  const bool  carrier = tb_descs != nullptr && d.tb_bit_offset + d.nof_data > d.tb_bits;
+  // The TB's CRC parameters straight from the codeblock descriptor (as tb_descs[d.tb_index] holds them): no dependent
+  // descriptor load before the TB's own loads.
+  tb_crc_desc tcd{};
+  tcd.byte_offset = d.tb_byte_offset;
+  tcd.nbytes      = d.tb_bits / 8u;
+  tcd.order       = d.tb_crc_len;
+  tcd.poly        = (d.tb_crc_len == 24) ? 0x1864cfbu : 0x11021u;
+  tcd.table       = d.tb_crc_table;
+  constexpr int TCS   = 16;
+  const bool    tfast = carrier && tcd.nbytes <= 2u * TCS * PK_THREADS && ((tcd.byte_offset | tcd.nbytes) & 3u) == 0u;
+  uint32_t      tw[2][TCS / 4];
+  uint32_t      tm[2] = {0u, 0u};
+  if (tfast) {
+    const uint32_t* tbw = reinterpret_cast<const uint32_t*>(tbs + tcd.byte_offset);
+    const int       nw  = static_cast<int>(tcd.nbytes / 4u);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = tid + h * PK_THREADS;
+#pragma unroll
+      for (int q = 0; q < TCS / 4; ++q) {
+        const int w = c * (TCS / 4) + q;
+        tw[h][q]    = (w < nw) ? tbw[w] : 0u;
       }
+      if (c * TCS < static_cast<int>(tcd.nbytes)) {
+        tm[h] = crc_chunk_power<TCS>(c, static_cast<int>(tcd.nbytes), crc_tables + tcd.table,
+                                     static_cast<int>(tcd.order));
+      }
+    }
+  }
+  if (has_cbc) {
+    // CRC24B byte table: each lane's two entries while the loads are in flight (the barriers below publish it).
+    for (uint32_t t = static_cast<uint32_t>(tid); t < 256u; t += PK_THREADS) {
+      uint32_t r = t << 16;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        r = (r << 1) ^ ((r & 0x800000u) ? 0x1800063u : 0u);
+      }
+      lut_b[t] = r & 0xffffffu;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < NEL; ++r) {
+    if (tid + r * PK_THREADS < G::NE) {
+      edge[tid + r * PK_THREADS] = ev[r];
     }
   }
   for (int m = tid; m <= G::M; m += PK_THREADS) {
     row_start[m] = static_cast<uint16_t>(G::rs(m));
   }
   // ---- Message bytes (ldpc_segmenter_tx_impl.cpp:144): TB(+TB CRC) bytes, zero padding / CRC slot / fillers. ----
-  const uint8_t* tb     = tbs + d.tb_byte_offset;
-  uint32_t       tb_crc = 0;
-  if (tb_descs == nullptr) {
-    tb_crc = tb_crcs[d.tb_index];  // from tb_crc_kernel
-  } else if (d.tb_bit_offset + d.nof_data > d.tb_bits) {
-    // Inline TB CRC (every TB of the plan has a contribution table): the workgroup of the codeblock that carries the
-    // TB CRC computes it, the others never need it: no separate tb_crc_kernel launch and dependency.
-    const tb_crc_desc t = tb_descs[d.tb_index];
-    crc_byte_lut(lut, static_cast<int>(t.order), t.poly);
-    const uint8_t* tbp = tbs + t.byte_offset;
-    tb_crc = block_crc_chunks<16>([tbp](int i) { return tbp[i]; }, static_cast<int>(t.nbytes), crc_tables + t.table,
-                                  static_cast<int>(t.order), t.poly, lut, red);
-  }
-  const int nd8 = d.nof_data / 8;
-  {
-    // All of a lane's message bytes are loaded before any is stored (the loads in flight together; the address is
-    // clamped into the TB so the loads are unconditional).
-    constexpr int  MB    = (G::K * 384 / 8 + PK_THREADS - 1) / PK_THREADS;
-    const uint32_t tb_hi = d.tb_bits >= 8u ? (d.tb_bits - 8u) >> 3 : 0u;
-    uint32_t       byte[MB];
+  if (tfast) {
+    crc_byte_lut(lut, static_cast<int>(tcd.order), tcd.poly);
+    const int      order = static_cast<int>(tcd.order);
+    const uint32_t mask  = (1u << order) - 1u;
+    const int      nb    = static_cast<int>(tcd.nbytes);
+    uint32_t       rem[2] = {0u, 0u};
 #pragma unroll
-    for (int r = 0; r < MB; ++r) {
-      const int      q  = tid + r * PK_THREADS;
-      const uint32_t p  = d.tb_bit_offset + 8u * static_cast<uint32_t>(q);
-      const uint32_t pb = p >> 3;
-      byte[r]           = (q < nd8) ? tb[pb < tb_hi ? pb : tb_hi] : 0u;
-    }
+    for (int k = 0; k < TCS; ++k) {
 #pragma unroll
-    for (int r = 0; r < MB; ++r) {
-      const int q = tid + r * PK_THREADS;
-      if (q < nkb) {
-        const uint32_t p = d.tb_bit_offset + 8u * static_cast<uint32_t>(q);
-        uint32_t       b = byte[r];
-        if (q < nd8 && p >= d.tb_bits) {
-          b = (tb_crc >> (d.tb_crc_len - 8u - (p - d.tb_bits))) & 0xffu;
+      for (int h = 0; h < 2; ++h) {
+        const int      c = tid + h * PK_THREADS;
+        const uint32_t b = (tw[h][k >> 2] >> (8 * (k & 3))) & 0xffu;
+        if (c * TCS + k < nb) {
+          rem[h] = ((rem[h] << 8) ^ lut[((rem[h] >> (order - 8)) ^ b) & 0xffu]) & mask;
         }
-        msg[q] = static_cast<uint8_t>(b);
       }
     }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if ((tid + h * PK_THREADS) * TCS < nb) {
+        acc ^= gf2_mulmod(rem[h], tm[h], order, tcd.poly);
+      }
+    }
+    acc = wave_xor(acc);
+    if ((tid % WAVE) == 0) {
+      red[tid / WAVE] = acc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < PK_THREADS / WAVE; ++w) {
+      tb_crc ^= red[w];
+    }
+  } else if (carrier) {
+    crc_byte_lut(lut, static_cast<int>(tcd.order), tcd.poly);
+    const uint8_t* tbp = tbs + tcd.byte_offset;
+    tb_crc = block_crc_chunks<16>([tbp](int i) { return tbp[i]; }, static_cast<int>(tcd.nbytes),
+                                  crc_tables + tcd.table, static_cast<int>(tcd.order), tcd.poly, lut, red);
   }
-  if (d.crc_table != NO_CRC_TABLE) {
-    crc_byte_lut(lut, 24, 0x1800063u);  // CRC24B; ends with a barrier
-    const uint32_t crc = block_crc_chunks<16>([](int q) { return msg[q]; }, static_cast<int>(d.used) / 8,
-                                              crc_tables + d.crc_table, 24, 0x1800063u, lut, red);
+  ENC_STAMP(1);
+#pragma unroll
+  for (int r = 0; r < MB; ++r) {
+    const int q = tid + r * PK_THREADS;
+    if (q < nkb) {
+      const uint32_t p = d.tb_bit_offset + 8u * static_cast<uint32_t>(q);
+      uint32_t       b = byte[r];
+      if (q < nd8 && p >= d.tb_bits) {
+        b = (tb_crc >> (d.tb_crc_len - 8u - (p - d.tb_bits))) & 0xffu;
+      }
+      msg[q] = static_cast<uint8_t>(b);
+    }
+  }
+  ENC_STAMP(2);
+  if (has_cbc) {
+    __syncthreads();  // msg and lut_b complete
+    const uint32_t crc = block_crc_chunks<CB_CS>([](int q) { return msg[q]; }, cb_bytes, crc_tables + d.crc_table, 24,
+                                                 0x1800063u, lut_b, red, 0, -1, pre_m, m0);
     if (tid < 3) {
       msg[d.used / 8 + tid] = static_cast<uint8_t>(crc >> (16 - 8 * tid));
     }
   }
   __syncthreads();
+  ENC_STAMP(3);
   // ---- Message words: node c word k = message bits 32 (c W + k) .. + 31. ----
   const uint32_t* msg32 = reinterpret_cast<const uint32_t*>(msg);
   for (int q = tid; q < K * W; q += PK_THREADS) {
     cw[q] = bytes_bitrev(msg32[q]);
   }
-  __syncthreads();
-  // ---- Core rows 0..3: lambda_m = sum of the rotated information nodes (32 rows per task). ----
-  for (int task = tid; task < 4 * W; task += PK_THREADS) {
-    const int m = task / W, k = task - m * W;
-    uint32_t  acc = 0;
-    for (int e = row_start[m]; e < row_start[m + 1]; ++e) {
-      const uint32_t ce = edge[e];
-      const int      c  = static_cast<int>(ce >> 16);
-      if (c < K) {
-        acc ^= col_window(cw + c * W, k, static_cast<int>(ce & 0xffffu), W);
-      }
-    }
-    lam[m * WMAX + k] = acc;
+  if (tid < 4 * WMAX) {
+    lam[tid] = 0u;
   }
   __syncthreads();
-  const core_plan* __restrict__ cp = core_plans + d.zpos;
-  // P^x p0 = lambda_0 + ... + lambda_3  ->  p0[l] = sum lambda[(l - x) mod Z].
+  ENC_STAMP(4);
+  // ---- Core rows 0..3: lambda_m = sum of the rotated information nodes (32 rows per task). Each (row, word) is
+  // split into CH edge chunks over the workgroup's lanes (every window load of a chunk in flight at once); the partial
+  // sums are XORed into lam (zeroed with the message) by LDS atomics. ----
   {
-    const int o = (Z - cp->x) % Z;
-    for (int k = tid; k < W; k += PK_THREADS) {
+    const int CH     = (W <= 10) ? 3 : 2;  // 4 W CH <= PK_THREADS
+    const int ntask  = 4 * W * CH;
+    if (tid < ntask) {
+      const int m     = tid / (W * CH);
+      const int rem   = tid - m * W * CH;
+      const int ch    = rem / W;
+      const int k     = rem - ch * W;
+      const int rs    = row_start[m];
+      const int deg   = row_start[m + 1] - rs;
+      const int per   = (deg + CH - 1) / CH;
+      const int e_beg = rs + ch * per;
+      const int e_end = min(e_beg + per, rs + deg);
+      constexpr int MAXCH = (core_max_degree<BG>() + 1) / 2;  // a core row's edges over at least two chunks
+      uint32_t acc = 0;
+#pragma unroll
+      for (int q = 0; q < MAXCH; ++q) {
+        const int e = e_beg + q;
+        if (e < e_end) {
+          const uint32_t ce = edge[e];
+          const int      c  = static_cast<int>(ce >> 16);
+          if (c < K) {
+            acc ^= col_window(cw + c * W, k, static_cast<int>(ce & 0xffffu), W);
+          }
+        }
+      }
+      if (acc != 0u) {
+        atomicXor(&lam[m * WMAX + k], acc);
+      }
+    }
+  }
+  __syncthreads();
+  ENC_STAMP(5);
+  // The four core parity nodes are W <= 12 words each, solved one after the other: the first wave alone runs the four
+  // dependent steps, ordered by wave-level LDS fences instead of workgroup barriers (window offsets precomputed mod Z
+  // per (BG, Z) in the core plan).
+  if (tid < WAVE) {
+    const core_plan cp = core_plans[d.zpos];
+    // P^x p0 = lambda_0 + ... + lambda_3  ->  p0[l] = sum lambda[(l - x) mod Z].
+    if (tid < W) {
+      const int k   = tid;
+      const int o   = cp.o0;
       cw[K * W + k] = col_window(lam, k, o, W) ^ col_window(lam + WMAX, k, o, W) ^
                       col_window(lam + 2 * WMAX, k, o, W) ^ col_window(lam + 3 * WMAX, k, o, W);
     }
+    // p_u[(z + s_u) mod Z] = lambda_row[z] + sum_{j != u} p_j[(z + s_j) mod Z]  (same steps as the byte kernel).
+#pragma unroll
+    for (int step = 0; step < 3; ++step) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (tid < W) {
+        const int k   = tid;
+        uint32_t  acc = col_window(lam + cp.row[step] * WMAX, k, cp.orow[step], W);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int oj = cp.oj[step][j];
+          if (oj >= 0) {
+            acc ^= col_window(cw + (K + j) * W, k, oj, W);
+          }
+        }
+        cw[(K + cp.unk[step]) * W + k] = acc;
+      }
+    }
   }
   __syncthreads();
-  // p_u[(z + s_u) mod Z] = lambda_row[z] + sum_{j != u} p_j[(z + s_j) mod Z]  (same steps as the byte kernel).
-  for (int step = 0; step < 3; ++step) {
-    const int u  = cp->unk[step];
-    const int su = cp->sh[step][u];
-    for (int k = tid; k < W; k += PK_THREADS) {
-      uint32_t acc = col_window(lam + cp->row[step] * WMAX, k, (Z - su) % Z, W);
-      for (int j = 0; j < 4; ++j) {
-        const int s = cp->sh[step][j];
-        if (j != u && s >= 0) {
-          acc ^= col_window(cw + (K + j) * W, k, (s - su + Z) % Z, W);
-        }
-      }
-      cw[(K + u) * W + k] = acc;
-    }
-    __syncthreads();
-  }
+  ENC_STAMP(6);
   // ---- Extension parity (identity extension), every needed row in parallel. ----
   const int n_ext = d.n_ext;
   for (int task = tid; task < n_ext * W; task += PK_THREADS) {
@@ -576,6 +775,7 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
     cw[(K + 4 + r) * W + k] = acc;
   }
   __syncthreads();
+  ENC_STAMP(7);
   // ---- Rate matching + interleaving + packing. ----
   const pk_rm rm{cw, d.v0, d.Ncb - d.filler, static_cast<uint32_t>((K - 2) * Z - d.filler), d.filler,
                  static_cast<uint32_t>(2 * Z)};
@@ -586,9 +786,20 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
     case 6: rate_match_packed<6>(d, rm, out_words); break;
     default: rate_match_packed<8>(d, rm, out_words); break;
   }
+  ENC_STAMP(8);
+  ENC_PROF(10, __builtin_amdgcn_s_memrealtime());
 }
 
 } // namespace
+
+#ifdef ENC_PROFILE
+int debug_read_encoder_profile(uint64_t* dst, size_t n)
+{
+  const size_t max = static_cast<size_t>(ENC_PROF_CBS) * ENC_PROF_SLOTS;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_enc_prof), (n < max ? n : max) * sizeof(uint64_t)) == hipSuccess ? 0
+                                                                                                                : -1;
+}
+#endif
 
 void launch_pdsch_encode_packed(int              bg,
                                 const enc_desc*  d_desc,

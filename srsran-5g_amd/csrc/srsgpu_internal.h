@@ -70,7 +70,13 @@ struct core_plan {
   int8_t  unk[3];     ///< Parity node solved at each step.
   int8_t  row[3];     ///< Core row used at each step.
   int16_t sh[3][4];   ///< Shifts of the row's parity nodes at each step (-1: no edge).
+  // Window offsets of the packed kernel (pdsch_encode_packed_kernel), precomputed mod Z: (Z - x) mod Z for p0; per
+  // step (Z - s_u) mod Z for the row sum and (s_j - s_u) mod Z for parity node j (-1: not in the sum).
+  int16_t o0;
+  int16_t orow[3];
+  int16_t oj[3][4];
 };
+static_assert(sizeof(core_plan) == 64, "core_plan layout");
 
 /// Per-codeblock work item of the PDSCH encoder (pdsch_encode_kernel).
 struct enc_desc {
@@ -93,8 +99,10 @@ struct enc_desc {
   uint8_t  Qm;
   uint8_t  n_ext;           ///< Extension parity rows needed by the rate matcher.
   uint8_t  pad[3];
+  uint32_t tb_crc_table;    ///< TB CRC contribution table of the TB (inline TB CRC: no tb_crc_desc load).
+  uint32_t pad2;
 };
-static_assert(sizeof(enc_desc) == 56, "enc_desc layout");
+static_assert(sizeof(enc_desc) == 64, "enc_desc layout");
 
 /// A byte range [begin, end) of transport block `tb` whose CRC contribution one tb_crc_kernel workgroup computes and
 /// XORs into the TB's CRC word (zeroed before the launch): large TBs are spread over many workgroups instead of one.
@@ -179,6 +187,10 @@ void launch_pusch_tb(const tb_dec_desc* d_desc,
 /// Bytes between the packed messages of consecutive codeblocks in the PUSCH decoder's message buffer.
 constexpr uint32_t CB_MSG_STRIDE = 1056;  // 22 * 384 / 8
 
+#ifdef ENC_PROFILE
+/// Copies the phase stamps of the instrumented encoder build (ENC_PROFILE) into dst (n words).
+int debug_read_encoder_profile(uint64_t* dst, size_t n);
+#endif
 #ifdef LDPC_DEC_PROFILE
 constexpr int LDPC_DEC_PROF_CBS   = 4096;
 constexpr int LDPC_DEC_PROF_SLOTS = 32;

@@ -19,6 +19,8 @@
 // the lanes (one 32-lane half per band edge, unwrap as a prefix sum); reductions are wave shuffles. HBM traffic per job:
 // the D DM-RS symbols' pilots of one port (read twice: the second pass, for the noise residual, hits L2) and 4 B per
 // estimated RE per layer (the dominant term).
+#include <cstdlib>
+
 #include "gold_device.h"
 #include "srsgpu_internal.h"
 
@@ -75,14 +77,40 @@ __device__ __forceinline__ float block_sum(float v, float* red)
   return v;
 }
 
-/// Sum over a 32-lane half of the wavefront.
-__device__ __forceinline__ float half_sum(float v)
+/// Sum over an aligned group of TS lanes (TS <= 64, every lane of the group gets the result).
+template <int TS>
+__device__ __forceinline__ float sub_sum(float v)
 {
 #pragma unroll
-  for (int o = 16; o > 0; o >>= 1) {
-    v += __shfl_xor(v, o, 32);
+  for (int o = TS / 2; o > 0; o >>= 1) {
+    v += __shfl_xor(v, o, TS);
   }
   return v;
+}
+
+/// Sum over one job's lanes: TS < 64 lanes of a wave that holds several jobs, or the whole workgroup.
+template <int T, int TS>
+__device__ __forceinline__ float job_sum(float v, float* red)
+{
+  if constexpr (TS < 64) {
+    return sub_sum<TS>(v);
+  } else {
+    return block_sum<T>(v, red);
+  }
+}
+
+/// Ordering of a job's LDS stages: a workgroup barrier; in a one-wave workgroup (T = 64, where the 32-lane halves may
+/// run jobs with different stage sequences) a wave-level fence: a wave's LDS accesses complete in program order.
+template <int T>
+__device__ __forceinline__ void job_sync()
+{
+  if constexpr (T == 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  } else {
+    __syncthreads();
+  }
 }
 
 /// DM-RS QPSK symbol i of DM-RS symbol s from the staged sequence words (amplitude 1/sqrt(2)).
@@ -100,35 +128,36 @@ __device__ __forceinline__ cpx pilot(const uint32_t* seq, int W, int s, uint32_t
 __device__ __forceinline__ cpx dmrs_value(const chest_job& jb, const float2* __restrict__ lp, const uint32_t* seq,
                                           int W, int s, uint32_t n0, int m, int i);
 
-/// compute_v_pilots on the lanes: lanes 0..nv-1 of the first half extrapolate the band start from E[VP .. VP+nv),
-/// lanes 32..32+nv-1 the band end from E[VP+N-nv .. VP+N): linear regression of |p| and the unwrapped arg over
-/// x = 0..nv-1, evaluated at x = -nv..-1 (start) or nv..2nv-1 (end).
-__device__ __forceinline__ void virtual_pilots(cpx* E, int N, int nv)
+/// compute_v_pilots on the lanes: with H lanes per band edge (H = 32, or TS / 2 when a wave holds several jobs), lanes
+/// 0..nv-1 of the first H extrapolate the band start from E[VP .. VP+nv), lanes H..H+nv-1 the band end from
+/// E[VP+N-nv .. VP+N): linear regression of |p| and the unwrapped arg over x = 0..nv-1, evaluated at x = -nv..-1
+/// (start) or nv..2nv-1 (end). Lanes j >= nv carry zeros, so the sums and the prefix do not depend on H.
+template <int H>
+__device__ __forceinline__ void virtual_pilots(cpx* E, int N, int nv, int sub)
 {
-  const int   lane = static_cast<int>(threadIdx.x);
-  const int   side = lane >> 5;
-  const int   j    = lane & 31;
+  const int   side = sub / H;
+  const int   j    = sub % H;
   const bool  act  = j < nv;
   const cpx   b    = act ? E[CHEST_VP + (side ? N - nv : 0) + j] : cpx{1.f, 0.f};
   const float ab   = act ? sqrtf(b.x * b.x + b.y * b.y) : 0.f;
   const float a    = atan2f(b.y, b.x);
   // Unwrap: arg_j + 2 pi c_j with c_j = sum_{m <= j} rint((a_{m-1} - a_m) / 2 pi) (prefix sum within the half).
   const float twopi = 6.28318531f;
-  const float prev  = __shfl_up(a, 1, 32);
+  const float prev  = __shfl_up(a, 1, H);
   float       c     = (j > 0 && act) ? rintf((prev - a) / twopi) : 0.f;
 #pragma unroll
-  for (int o = 1; o < 32; o <<= 1) {
-    const float t = __shfl_up(c, o, 32);
+  for (int o = 1; o < H; o <<= 1) {
+    const float t = __shfl_up(c, o, H);
     c += (j >= o) ? t : 0.f;
   }
   const float ar        = act ? a + twopi * c : 0.f;
   const float n         = static_cast<float>(nv);
   const float mean_x    = static_cast<float>(nv * (nv - 1)) / 2.0f / n;
   const float norm_x_sq = static_cast<float>((nv - 1) * nv * (2 * nv - 1)) / 6.0f;
-  const float mab       = half_sum(ab) / n;
-  const float mar       = half_sum(ar) / n;
-  const float dab       = half_sum(ab * static_cast<float>(j));
-  const float dar       = half_sum(ar * static_cast<float>(j));
+  const float mab       = sub_sum<H>(ab) / n;
+  const float mar       = sub_sum<H>(ar) / n;
+  const float dab       = sub_sum<H>(ab * static_cast<float>(j));
+  const float dar       = sub_sum<H>(ar * static_cast<float>(j));
   const float den       = norm_x_sq - n * mean_x * mean_x;
   const float s_abs     = (dab - mean_x * mab * n) / den;
   const float i_abs     = mab - s_abs * mean_x;
@@ -205,6 +234,21 @@ __device__ __forceinline__ void wave_argmax(float& v, int& idx)
   }
 }
 
+/// wave_argmax over an aligned group of TS < 64 lanes.
+template <int TS>
+__device__ __forceinline__ void sub_argmax(float& v, int& idx)
+{
+#pragma unroll
+  for (int o = TS / 2; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, TS);
+    const int   oi = __shfl_xor(idx, o, TS);
+    if (ov > v || (ov == v && oi < idx)) {
+      v   = ov;
+      idx = oi;
+    }
+  }
+}
+
 /// wave_argmax over the workgroup of T lanes (lowest index among equal maxima; all lanes must call it).
 template <int T>
 __device__ __forceinline__ void block_argmax(float& v, int& idx, float* redf, int* redi)
@@ -229,6 +273,17 @@ __device__ __forceinline__ void block_argmax(float& v, int& idx, float* redf, in
   }
 }
 
+/// Argmax over one job's lanes (see job_sum).
+template <int T, int TS>
+__device__ __forceinline__ void job_argmax(float& v, int& idx, float* redf, int* redi)
+{
+  if constexpr (TS < 64) {
+    sub_argmax<TS>(v, idx);
+  } else {
+    block_argmax<T>(v, idx, redf, redi);
+  }
+}
+
 /// LDS of a job, carved from the plan-sized dynamic allocation (chest_geom): the staged sequence words, the filter
 /// taps, the smoothed planes F and one region shared by the LSE stage (Y per DM-RS symbol + enlarged E per layer) and
 /// the time-alignment stage (the DFT buffer X + the correlation), which run one after the other.
@@ -250,9 +305,21 @@ __device__ __host__ inline size_t chest_region_bytes(const chest_geom& g)
   return lse > ta ? lse : ta;
 }
 
-template <int T>
+/// Dynamic LDS of one job (16-byte multiple: the jobs of a workgroup are laid out one after the other).
+__device__ __host__ inline size_t chest_job_lds_bytes(const chest_geom& g)
+{
+  const size_t b = static_cast<size_t>(g.max_planes) * g.max_gl * g.max_pilots * sizeof(cpx) + chest_region_bytes(g) +
+                   static_cast<size_t>(g.max_dmrs) * g.max_words * 4 + 32 * 4;
+  return (b + 15) & ~static_cast<size_t>(15);
+}
+
+/// T lanes per workgroup, TS lanes per job: TS = T (one job per workgroup), or T = 64 and TS = 32 (two jobs per wave,
+/// one per 32-lane half: a few-RB job's pilots fill half a wave, so a whole wave per job issued every instruction for
+/// twice the lanes it used; the chest kernel is bound by VALU issue, profiles/r3_v2_sq_serial.log).
+template <int T, int TS>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void pusch_chest_kernel(
     const chest_job* __restrict__ jobs,
+    int nof_jobs,
     chest_geom geom,
     const uint32_t* __restrict__ grids,
     uint32_t* __restrict__ ce,
@@ -265,9 +332,15 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
   extern __shared__ __align__(16) unsigned char lds_raw[];
   __shared__ float redf[T / 64];
   __shared__ int   redi[T / 64];
+  constexpr int JPW  = T / TS;  // jobs per workgroup
+  const int     slot = static_cast<int>(threadIdx.x) / TS;
+  const int     job  = static_cast<int>(blockIdx.x) * JPW + slot;
+  if (JPW > 1 && job >= nof_jobs) {
+    return;  // an odd job count leaves the second half of the last wave without a job (no workgroup barriers here)
+  }
   const int EN = geom.max_pilots + 2 * CHEST_VP;
   chest_lds L;
-  L.F    = reinterpret_cast<cpx*>(lds_raw);
+  L.F    = reinterpret_cast<cpx*>(lds_raw + static_cast<size_t>(slot) * chest_job_lds_bytes(geom));
   L.Y    = L.F + static_cast<size_t>(geom.max_planes) * geom.max_gl * geom.max_pilots;
   L.E    = L.Y + static_cast<size_t>(geom.max_dmrs) * geom.max_pilots;
   L.X    = L.Y;
@@ -278,21 +351,21 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
 #ifndef SRSGPU_CHEST_JOB_SCALAR
   // The job descriptor staged in LDS once (one coalesced read) instead of dependent scalar loads of its fields
   // (A/B on MI355X: chest stage 32.6 -> 28.9 us per 16-slot step; SRSGPU_CHEST_JOB_SCALAR restores the direct reads).
-  __shared__ chest_job sjob;
+  __shared__ chest_job sjob[JPW];
   {
     static_assert(sizeof(chest_job) % 4 == 0, "word copy");
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(jobs + blockIdx.x);
-    uint32_t*       dst = reinterpret_cast<uint32_t*>(&sjob);
-    for (int w = static_cast<int>(threadIdx.x); w < static_cast<int>(sizeof(chest_job) / 4); w += T) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(jobs + job);
+    uint32_t*       dst = reinterpret_cast<uint32_t*>(&sjob[slot]);
+    for (int w = static_cast<int>(threadIdx.x) % TS; w < static_cast<int>(sizeof(chest_job) / 4); w += TS) {
       dst[w] = src[w];
     }
-    __syncthreads();
+    job_sync<T>();
   }
-  const chest_job& jb = sjob;
+  const chest_job& jb = sjob[slot];
 #else
-  const chest_job& jb    = jobs[blockIdx.x];
+  const chest_job& jb    = jobs[job];
 #endif
-  const int        lane  = static_cast<int>(threadIdx.x);
+  const int        lane  = static_cast<int>(threadIdx.x) % TS;  // lane within the job
   const int        N     = jb.nof_pilots;
   const int        GL    = jb.group_layers;
   const int        D     = jb.nof_dmrs;
@@ -309,15 +382,15 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
   }
   const int nwords = static_cast<int>(((n0 & 31u) + 2u * static_cast<uint32_t>(jb.span_pilots) + 31u) >> 5);
   for (int s = 0; s < D; ++s) {
-    for (int wl = lane; wl < nwords; wl += T) {
+    for (int wl = lane; wl < nwords; wl += TS) {
       L.seq[s * W + wl] = gseq[jb.gseq_base + static_cast<uint32_t>(s * nwords + wl)];
     }
   }
-  __syncthreads();
+  job_sync<T>();
 
   // Pass 1: LSE of every DM-RS symbol (received x conj(pilot)), EPRE.
   float epre_acc = 0.f;
-  for (int i = lane; i < N; i += T) {
+  for (int i = lane; i < N; i += TS) {
     const uint32_t k = pilot_subcarrier(jb, crbs, i);
     const int      m = pilot_seq_index(jb, crbs, i);
     for (int s = 0; s < D; ++s) {
@@ -327,7 +400,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
       epre_acc += y.x * y.x + y.y * y.y;
     }
   }
-  __syncthreads();
+  job_sync<T>();
 
   // CFO from the first two DM-RS symbols (preprocess_pilots_and_estimate_cfo, :322): arg(sum lse_1 conj(lse_0)) over
   // the time between their starts; with compensation every DM-RS symbol is derotated by its start epoch.
@@ -335,32 +408,33 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
   float      cfo     = 0.f;
   if (has_cfo) {
     float ar = 0.f, ai = 0.f;
-    for (int i = lane; i < N; i += T) {
+    for (int i = lane; i < N; i += TS) {
       const cpx a = L.Y[NP + i], b = L.Y[i];
       ar += a.x * b.x + a.y * b.y;
       ai += a.y * b.x - a.x * b.y;
     }
-    ar  = block_sum<T>(ar, redf);
-    ai  = block_sum<T>(ai, redf);
+    ar  = job_sum<T, TS>(ar, redf);
+    ai  = job_sum<T, TS>(ai, redf);
     cfo = atan2f(ai, ar) / CHEST_TWOPI / (jb.epochs[jb.dmrs_symbols[1]] - jb.epochs[jb.dmrs_symbols[0]]);
     if (jb.compensate_cfo) {
       for (int s = 0; s < D; ++s) {
         const cpx r = polar1(-CHEST_TWOPI * jb.epochs[jb.dmrs_symbols[s]] * cfo);
-        for (int i = lane; i < N; i += T) {
+        for (int i = lane; i < N; i += TS) {
           L.Y[s * NP + i] = cmul(L.Y[s * NP + i], r);
         }
       }
-      __syncthreads();
+      job_sync<T>();
     }
   }
   const bool rotate = has_cfo && jb.compensate_cfo;
   // Per-symbol CFO rotations e^{j 2 pi epoch_l cfo} of the noise residual, once per job instead of once per pilot.
-  __shared__ cpx srot[14];
+  __shared__ cpx srot_all[JPW][14];
+  cpx* const     srot = srot_all[slot];
   if (rotate) {
     if (lane < 14) {
       srot[lane] = polar1(CHEST_TWOPI * jb.epochs[lane] * cfo);
     }
-    __syncthreads();
+    job_sync<T>();
   }
 
   // Planes: "average" combines the DM-RS symbols into one LSE scaled by 1 / (beta D); "interpolate" keeps one per
@@ -372,7 +446,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
     cpx* const E0 = L.E;
     cpx* const E1 = L.E + EN;
     if (GL == 2) {
-      for (int j = lane; j < N / 2; j += T) {
+      for (int j = lane; j < N / 2; j += TS) {
         cpx a = L.Y[q * NP + 2 * j], b = L.Y[q * NP + 2 * j + 1];
         if (!jb.td_interp) {
           for (int s = 1; s < D; ++s) {
@@ -386,7 +460,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
         E1[CHEST_VP + 2 * j] = E1[CHEST_VP + 2 * j + 1] = h1;
       }
     } else {
-      for (int i = lane; i < N; i += T) {
+      for (int i = lane; i < N; i += TS) {
         cpx z = L.Y[q * NP + i];
         if (!jb.td_interp) {
           for (int s = 1; s < D; ++s) {
@@ -396,17 +470,17 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
         E0[CHEST_VP + i] = {z.x * scale, z.y * scale};
       }
     }
-    __syncthreads();
+    job_sync<T>();
     for (int ly = 0; ly < GL; ++ly) {
       cpx* E = ly ? E1 : E0;
       cpx* F = Fbase + (q * GL + ly) * NP;
       if (jb.fd == CHEST_FD_FILTER) {
         const int nv = jb.nof_v_pilots;
-        if (lane < 64) {  // the first wave extrapolates both band edges
-          virtual_pilots(E, N, nv);
+        if (lane < 64) {  // the first wave (or the job's 2 x TS / 2 lanes) extrapolates both band edges
+          virtual_pilots<(TS < 64 ? TS / 2 : 32)>(E, N, nv, lane);
         }
-        __syncthreads();
-        for (int i = lane; i < N; i += T) {
+        job_sync<T>();
+        for (int i = lane; i < N; i += TS) {
           cpx acc = {0.f, 0.f};
           for (int j = 0; j < nt; ++j) {
             const int e = CHEST_VP + i - c + j;  // symmetric taps: correlation == convolution
@@ -419,28 +493,28 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
         }
       } else if (jb.fd == CHEST_FD_MEAN) {
         float sx = 0.f, sy = 0.f;
-        for (int i = lane; i < N; i += T) {
+        for (int i = lane; i < N; i += TS) {
           sx += E[CHEST_VP + i].x;
           sy += E[CHEST_VP + i].y;
         }
-        sx = block_sum<T>(sx, redf) / static_cast<float>(N);
-        sy = block_sum<T>(sy, redf) / static_cast<float>(N);
-        for (int i = lane; i < N; i += T) {
+        sx = job_sum<T, TS>(sx, redf) / static_cast<float>(N);
+        sy = job_sum<T, TS>(sy, redf) / static_cast<float>(N);
+        for (int i = lane; i < N; i += TS) {
           F[i] = {sx, sy};
         }
       } else {
-        for (int i = lane; i < N; i += T) {
+        for (int i = lane; i < N; i += TS) {
           F[i] = E[CHEST_VP + i];
         }
       }
     }
-    __syncthreads();
+    job_sync<T>();
   }
 
   // RSRP of layer 0 over the planes, and the noise residual (group 0 only) against the time-averaged estimate
   // beta / Q sum_q F_q, re-rotated by the CFO when compensating (estimate_noise, :422).
   float rsrp_acc = 0.f, noise_acc = 0.f;
-  for (int i = lane; i < N; i += T) {
+  for (int i = lane; i < N; i += TS) {
     cpx h = {0.f, 0.f};
     for (int q = 0; q < Q; ++q) {
       const cpx f0 = Fbase[(q * GL) * NP + i];
@@ -469,10 +543,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
     }
   }
   const float nof_pilots = static_cast<float>(N * D);
-  const float epre       = block_sum<T>(epre_acc, redf) / nof_pilots;
+  const float epre       = job_sum<T, TS>(epre_acc, redf) / nof_pilots;
   const float rsrp =
-      block_sum<T>(rsrp_acc, redf) * beta * beta * static_cast<float>(D) / static_cast<float>(Q) / nof_pilots;
-  const float noise_sum = block_sum<T>(noise_acc, redf);
+      job_sum<T, TS>(rsrp_acc, redf) * beta * beta * static_cast<float>(D) / static_cast<float>(Q) / nof_pilots;
+  const float noise_sum = job_sum<T, TS>(noise_acc, redf);
 
   // Time alignment of the smoothed layer-0 planes (estimate_time_alignment, port_channel_estimator_helpers.cpp:246 ->
   // time_alignment_estimator_dft_impl): inverse DFT of size M through LDS (radix 2, bit-reversed scatter), |.|^2
@@ -480,21 +554,21 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
   if (jb.group == 0) {
     const int M   = jb.ta_dft;
     const int lgM = jb.ta_log2;
-    __syncthreads();  // Y / E are dead: the region becomes X / corr
+    job_sync<T>();  // Y / E are dead: the region becomes X / corr
     for (int q = 0; q < Q; ++q) {
-      for (int n = lane; n < M; n += T) {
+      for (int n = lane; n < M; n += TS) {
         L.X[n] = {0.f, 0.f};
       }
-      __syncthreads();
+      job_sync<T>();
       const uint32_t k0 = pilot_subcarrier(jb, crbs, 0);
-      for (int i = lane; i < N; i += T) {
+      for (int i = lane; i < N; i += TS) {
         const uint32_t pos = jb.ta_positions ? pilot_subcarrier(jb, crbs, i) - k0 : static_cast<uint32_t>(i);
         L.X[__brev(pos) >> (32 - lgM)] = Fbase[(q * GL) * NP + i];
       }
-      __syncthreads();
+      job_sync<T>();
       for (int lh = 0; lh < lgM; ++lh) {
         const int h = 1 << lh;
-        for (int b = lane; b < M / 2; b += T) {
+        for (int b = lane; b < M / 2; b += TS) {
           const int   j  = b & (h - 1);
           const int   i0 = ((b >> lh) << (lh + 1)) + j;
           const float r  = static_cast<float>(j) / static_cast<float>(2 * h);  // revolutions: e^{+j 2 pi j / 2h}
@@ -504,18 +578,18 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
           L.X[i0]        = {a.x + t.x, a.y + t.y};
           L.X[i0 + h]    = {a.x - t.x, a.y - t.y};
         }
-        __syncthreads();
+        job_sync<T>();
       }
-      for (int n = lane; n < M; n += T) {
+      for (int n = lane; n < M; n += TS) {
         const float p = L.X[n].x * L.X[n].x + L.X[n].y * L.X[n].y;
         L.corr[n]     = q ? L.corr[n] + p : p;
       }
-      __syncthreads();
+      job_sync<T>();
     }
     const int m  = jb.ta_max;
     float     dv = -INFINITY, av = -INFINITY;
     int       di = 0x7fffffff, ai = 0x7fffffff;
-    for (int n = lane; n < m; n += T) {
+    for (int n = lane; n < m; n += TS) {
       if (L.corr[n] > dv) {
         dv = L.corr[n];
         di = n;
@@ -525,8 +599,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
         ai = n;
       }
     }
-    block_argmax<T>(dv, di, redf, redi);
-    block_argmax<T>(av, ai, redf, redi);
+    job_argmax<T, TS>(dv, di, redf, redi);
+    job_argmax<T, TS>(av, ai, redf, redi);
     const int idx  = (dv >= av) ? di : -(m - ai);
     float     frac = 0.f;
     if (M != 4096) {
@@ -588,7 +662,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
     return {(b.x - a.x) * w + a.x, (b.y - a.y) * w + a.y};
   };
   const bool rotate_out = rotate && !jb.compact_cfo;
-  for (int k = lane; k < nre; k += T) {
+  for (int k = lane; k < nre; k += TS) {
     // PRB k / 12 of the interpolated band is the (k / 12)-th allocated CRB (compute_hop maps the band PRB by PRB).
     const int kr = alloc_rb(jb, crbs, k / 12) * 12 + k % 12;
     for (int ly = 0; ly < GL; ++ly) {
@@ -622,8 +696,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
 
 size_t pusch_chest_lds_bytes(const chest_geom& g)
 {
-  return static_cast<size_t>(g.max_planes) * g.max_gl * g.max_pilots * sizeof(cpx) + chest_region_bytes(g) +
-         static_cast<size_t>(g.max_dmrs) * g.max_words * 4 + 32 * 4;
+  return chest_job_lds_bytes(g);
 }
 
 void launch_pusch_chest(const float2*   d_lp,
@@ -641,20 +714,27 @@ void launch_pusch_chest(const float2*   d_lp,
   if (nof_jobs <= 0) {
     return;
   }
-  const size_t lds = pusch_chest_lds_bytes(geom);
-  // One wave per job for the usual few-RB allocations (many jobs resident together); a job with hundreds of pilots
-  // (a wideband allocation: few jobs, each a long serial chain on one wave) spreads over 4 or 16 waves.
-  const auto launch = [&](auto kernel, int threads) {
-    hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(static_cast<unsigned>(threads)),
-                       static_cast<unsigned>(lds), stream, d_jobs, geom, d_grids, d_ce, d_noise_var, d_metrics, d_seq,
-                       d_crbs, d_lp);
+  const size_t lds = chest_job_lds_bytes(geom);
+  // Two jobs per wave (32 lanes each) for the usual few-RB allocations (many jobs resident together); a job with
+  // hundreds of pilots (a wideband allocation: few jobs, each a long serial chain on one wave) spreads over 4 or 16
+  // waves. SRSGPU_CHEST_ONE_JOB_PER_WAVE=1: one 64-lane job per wave (A/B).
+  const auto launch = [&](auto kernel, int threads, int jpw) {
+    hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>((nof_jobs + jpw - 1) / jpw)),
+                       dim3(static_cast<unsigned>(threads)), static_cast<unsigned>(jpw * lds), stream, d_jobs, nof_jobs,
+                       geom, d_grids, d_ce, d_noise_var, d_metrics, d_seq, d_crbs, d_lp);
   };
+  static const bool one_job = [] {
+    const char* e = std::getenv("SRSGPU_CHEST_ONE_JOB_PER_WAVE");
+    return e != nullptr && e[0] == '1';
+  }();
   if (geom.max_pilots > 512) {
-    launch(pusch_chest_kernel<1024>, 1024);
+    launch(pusch_chest_kernel<1024, 1024>, 1024, 1);
   } else if (geom.max_pilots > 128) {
-    launch(pusch_chest_kernel<256>, 256);
+    launch(pusch_chest_kernel<256, 256>, 256, 1);
+  } else if (!one_job && geom.max_pilots <= 64 && 2 * lds <= 64 * 1024) {
+    launch(pusch_chest_kernel<CHEST_THREADS, CHEST_THREADS / 2>, CHEST_THREADS, 2);
   } else {
-    launch(pusch_chest_kernel<CHEST_THREADS>, CHEST_THREADS);
+    launch(pusch_chest_kernel<CHEST_THREADS, CHEST_THREADS>, CHEST_THREADS, 1);
   }
 }
 

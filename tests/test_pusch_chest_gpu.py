@@ -200,6 +200,36 @@ def test_pusch_chest_cfo_ta_random_vs_oracle(ctx):
         np.testing.assert_allclose(m[i, :P, 5], ex["cfo_hz"], atol=0.05)
 
 
+def test_pusch_chest_two_jobs_per_wave_vs_oracle(ctx):
+    """Few-RB plans (at most 64 pilots per job) run two jobs per wave, one per 32-lane half: 37 random transmissions
+    (1..10 RB, 1-3 DM-RS symbols, 1-4 rx ports, DM-RS types 1 and 2, every smoothing, both time strategies, CFO
+    compensation on / off, CFO and delay) in ONE plan, so neighbouring halves run different stage sequences and the job
+    count is odd; every transmission against the restatement within the stated tolerances."""
+    import srsgpu
+    rng = np.random.default_rng(79)
+    cases, opts = [], []
+    for i in range(37):
+        nrb = [1, 2, 3, 4, 5, 7, 10][i % 7]
+        cases.append(random_case(rng, 10, nof_rb=nrb, dmrs_type2=0, cfo_hz=rng.uniform(-2000, 2000),
+                                 delay=rng.uniform(-30, 30)))
+        opts.append((int(rng.integers(0, 3)), i % 2, (i // 2) % 2))
+    grids = np.stack([pad4(g) for _, g, _ in cases])
+    ests = [to_est(cfg, fd, 1, td, comp) for (cfg, _, _), (fd, td, comp) in zip(cases, opts)]
+    ce, nv, m = srsgpu.PuschChannelEstimator(ctx, 10, 4).estimate_batch(grids, ests, list(range(len(cases))))
+    for i, ((cfg, grid, _), (fd, td, comp)) in enumerate(zip(cases, opts)):
+        P = cfg["nof_rx_ports"]
+        ch, nvo, rsrp, epre, ex = C.estimate(cfg, bf16_to_complex(grid), ["none", "mean", "filter"][fd],
+                                             ["average", "interpolate"][td], bool(comp))
+        ls, ks = region(cfg)
+        got = bf16_to_complex(ce[i, 0, :P])[:, ls, ks]
+        w = ch[:, ls, ks]
+        assert np.max(np.abs(got - w)) < CFO_TOL[td] * np.sqrt(np.mean(np.abs(w) ** 2)), (i, cfg, fd, td, comp)
+        np.testing.assert_allclose(nv[i, :P], nvo, rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 0], rsrp, rtol=1e-3)
+        np.testing.assert_allclose(m[i, :P, 4], ex["ta_s"], atol=2 * T_C)
+        np.testing.assert_allclose(m[i, :P, 5], ex["cfo_hz"], atol=0.05)
+
+
 def test_pusch_compact_cfo_equals_per_symbol(ctx):
     """Compact layout with CFO compensation (the demodulator rotates each symbol's estimate) gives the LLRs of the
     per-symbol layout (the estimator rotates), bit for bit: 1-4 layers, 4 rx ports, DM-RS in symbols 2 and 11."""

@@ -75,6 +75,12 @@ __device__ __forceinline__ u16x2 uu(int x)
 #ifndef LDPC_PK_SAT_INF
 #define LDPC_PK_SAT_INF 1
 #endif
+/// 1: a row's two-minimum search runs after all of its v2c values (156 instead of 360 hazard s_nops per 8-layer
+/// iteration, decoder launch 188 -> 184 us) - but the bench does not move (129.6k vs 128.9k slots/s,
+/// profiles/r3_decoder_phased_ab.txt: the other waves of a SIMD fill the nop slots), so edge by edge stays the default.
+#ifndef LDPC_PK_PHASED
+#define LDPC_PK_PHASED 0
+#endif
 
 /// 1 where IDX != e, 0 where IDX == e (both halves): IDX ^ e (one 32-bit v_xor on both 5-bit halves), then one
 /// v_pk_min_u16 against an opaque 0x00010001 (a visible constant 1 gets the min rewritten into per-half compares and
@@ -233,10 +239,12 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     // v2c = soft - c2v saturated to +/-LLR_MAX; infinite soft bits give |v2c| >= 392 (stay infinite).
     const s16x2 v   = v2c_pk(sb, om, n, kc);
     v2c[e]          = v;
+#if !LDPC_PK_PHASED
     const u16x2 key = key_pk(v, e, kc);
     k2              = __builtin_elementwise_min(__builtin_elementwise_max(key, k1), k2);
     k1              = __builtin_elementwise_min(key, k1);
     sx ^= bits(v);
+#endif
 #ifdef LDPC_PK_EXPERIMENT_EXTRA_VALU  // timing experiments only: N extra independent VALU per edge
     {
       uint32_t j0 = bits(v), j1 = bits(key);
@@ -250,6 +258,19 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
 #endif
   });
 
+#if LDPC_PK_PHASED
+  // The search after all of the row's v2c values exist: the per-edge chains (v2c -> |v2c| -> key) of different edges
+  // are independent, so the scheduler interleaves them instead of issuing one edge's dependent packed instructions
+  // back to back (each such pair costs an s_nop on gfx950).
+  static_for<deg>([&](auto E) {
+    constexpr int e   = decltype(E)::value;
+    const s16x2   v   = v2c[e];
+    const u16x2   key = key_pk(v, e, kc);
+    k2                = __builtin_elementwise_min(__builtin_elementwise_max(key, k1), k2);
+    k1                = __builtin_elementwise_min(key, k1);
+    sx ^= bits(v);
+  });
+#endif
   const u16x2 IDXN = k1 & uu(31);
   const u16x2 S1N  = scale_pk<MODE>(k1 >> uu(5), sc);
   const u16x2 S2N  = scale_pk<MODE>(k2 >> uu(5), sc);

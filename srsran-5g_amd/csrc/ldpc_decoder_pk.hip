@@ -75,6 +75,10 @@ __device__ __forceinline__ u16x2 uu(int x)
 #ifndef LDPC_PK_SAT_INF
 #define LDPC_PK_SAT_INF 1
 #endif
+/// 1: fused 256QAM dematching writes the HARQ buffer in dwords (0: bytes; A/B).
+#ifndef LDPC_PK_HARQ_X4
+#define LDPC_PK_HARQ_X4 1
+#endif
 /// 1: a row's two-minimum search runs after all of its v2c values (156 instead of 360 hazard s_nops per 8-layer
 /// iteration, decoder launch 188 -> 184 us) - but the bench does not move (129.6k vs 128.9k slots/s,
 /// profiles/r3_decoder_phased_ab.txt: the other waves of a SIMD fill the nop slots), so edge by edge stays the default.
@@ -551,8 +555,7 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
     __syncthreads();
     // Decoder input clamp (ldpc_decoder_impl.cpp:152): +/-64 in the whole lifted columns of the input, the
     // reference's LLR range (+/-infinity kept) in a trailing partial column; trailing-zero trim over [0, n_llr).
-    auto put = [&](int k, int v) {
-      hb[k] = static_cast<int8_t>(v);
+    auto soft_put = [&](int k, int v) {
       if (static_cast<uint32_t>(k) < static_cast<uint32_t>(n_llr)) {
         last              = (v != 0 && k > last) ? k : last;
         const uint32_t cq = __umulhi(static_cast<uint32_t>(k), d.div_magic);
@@ -561,37 +564,84 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
             static_cast<int8_t>(cv);
       }
     };
+    auto put = [&](int k, int v) {
+      hb[k] = static_cast<int8_t>(v);
+      soft_put(k, v);
+    };
     // Copies, symbol-major: lane r reads the Qm LLRs of symbol r and stores bit j at visit n = j R + r (position k =
-    // n, past the fillers once n >= ninfo); for a fixed j the lanes' HARQ stores are consecutive bytes.
+    // n, past the fillers once n >= ninfo); for a fixed j the lanes' HARQ stores are consecutive bytes. 256QAM with
+    // 4-aligned R, ninfo, fillers and HARQ buffer (every bench codeblock): a lane takes four consecutive symbols and
+    // writes each bit row's four HARQ bytes as one dword (8 dword stores per 4 symbols instead of 32 byte stores).
     const bool q8 = Qm == 8 && ((dm.llr_offset & 7u) == 0u);
-    for (int r = threadIdx.x; r < R; r += blockDim.x) {
-      int8_t sym[8];
-      if (q8) {
-        const uint2 v = *reinterpret_cast<const uint2*>(in + 8 * r);
+    const bool q8x4 = LDPC_PK_HARQ_X4 && q8 && ((R | ninfo | Fl | static_cast<int>(dm.harq_offset)) & 3) == 0;
+    if (q8x4) {
+      for (int r0 = 4 * static_cast<int>(threadIdx.x); r0 < R; r0 += 4 * static_cast<int>(blockDim.x)) {
+        uint2 v[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          sym[j] = static_cast<int8_t>(((j < 4) ? v.x : v.y) >> (8 * (j & 3)));
+        for (int q = 0; q < 4; ++q) {
+          v[q] = *reinterpret_cast<const uint2*>(in + 8 * (r0 + q));
         }
-      } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          sym[j] = (j < Qm) ? in[r * Qm + j] : 0;
+          uint32_t w = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t byte = (((j < 4) ? v[q].x : v[q].y) >> (8 * (j & 3))) & 0xffu;
+            w |= byte << (8 * q);
+          }
+          const int n = j * R + r0;  // n .. n + 3 on one side of ninfo (both multiples of 4)
+          const int k = n < ninfo ? n : n + Fl;
+          *reinterpret_cast<uint32_t*>(hb + k) = w;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            soft_put(k + q, static_cast<int8_t>(w >> (8 * q)));
+          }
         }
       }
+    } else {
+      for (int r = threadIdx.x; r < R; r += blockDim.x) {
+        int8_t sym[8];
+        if (q8) {
+          const uint2 v = *reinterpret_cast<const uint2*>(in + 8 * r);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (j < Qm) {
-          const int n = j * R + r;
-          put(n < ninfo ? n : n + Fl, sym[j]);
+          for (int j = 0; j < 8; ++j) {
+            sym[j] = static_cast<int8_t>(((j < 4) ? v.x : v.y) >> (8 * (j & 3)));
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            sym[j] = (j < Qm) ? in[r * Qm + j] : 0;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (j < Qm) {
+            const int n = j * R + r;
+            put(n < ninfo ? n : n + Fl, sym[j]);
+          }
         }
       }
     }
-    // Fillers: +infinity (ldpc_rate_dematcher_impl.cpp:172); then the unreached tail [E + F, N) zeroed.
+    // Fillers: +infinity (ldpc_rate_dematcher_impl.cpp:172); then the unreached tail [E + F, N) zeroed (16-byte
+    // stores between the unaligned head and tail bytes).
     for (int k = ninfo + static_cast<int>(threadIdx.x); k < ninfo + Fl; k += blockDim.x) {
       put(k, 127);
     }
-    for (int k = E + Fl + static_cast<int>(threadIdx.x); k < Nh; k += blockDim.x) {
-      hb[k] = 0;
+    {
+      const int t0 = E + Fl;
+      const int a0 = min(Nh, t0 + static_cast<int>((16u - (reinterpret_cast<uintptr_t>(hb + t0) & 15u)) & 15u));
+      const int nv = (Nh - a0) / 16;
+      const int a1 = a0 + 16 * nv;
+      if (static_cast<int>(threadIdx.x) < a0 - t0) {
+        hb[t0 + static_cast<int>(threadIdx.x)] = 0;
+      }
+      uint4* z16 = reinterpret_cast<uint4*>(hb + a0);
+      for (int q = threadIdx.x; q < nv; q += blockDim.x) {
+        z16[q] = make_uint4(0u, 0u, 0u, 0u);
+      }
+      if (static_cast<int>(threadIdx.x) < Nh - a1) {
+        hb[a1 + static_cast<int>(threadIdx.x)] = 0;
+      }
     }
   } else {
     {

@@ -1,4 +1,4 @@
-# Round 3: decoder row search after all of a row's v2c values (LDPC_PK_PHASED=1, default build) vs edge by edge
+# Round 3: decoder A/B, default build (lib) vs lib_exp built with other flags (see the commit using it): decoder parity, then
 # (lib_exp built with -DLDPC_PK_PHASED=0): decoder parity, then headline and worst-case bench A/B.
 set -o pipefail
 OUT=gpurun_out/r3ab

@@ -39,10 +39,11 @@ class TbGather:
     """Gathers every rank's decoded-TB bytes and CRC flags into `root`'s buffers.
 
     Ranks may hold different amounts (a UE shard's TB sizes differ from another's): the sizes are exchanged once at
-    construction (one all_gather), every rank sends a buffer padded to the largest, and on the root `tbs[r]` /
-    `crc_ok[r]` are views of rank r's real bytes. `gather` is one collective pair per batch on the current stream; the
-    buffers are allocated once (per plan). `assemble()` concatenates the ranks' results in rank order, which is the
-    UE order of the slot for contiguous `shard_ues` shares.
+    construction (one all_gather), every rank sends one buffer - its TB bytes padded to the largest rank's, then its
+    CRC flags padded the same way - so a batch costs one collective (the host issues a collective per step at a few
+    thousand steps per second), and on the root `tbs[r]` / `crc_ok[r]` are views of rank r's real bytes. `gather` runs
+    on the current stream; the buffers are allocated once (per plan). `assemble()` concatenates the ranks' results in
+    rank order, which is the UE order of the slot for contiguous `shard_ues` shares.
     """
 
     def __init__(self, tb_bytes: int, nof_tbs: int, device: torch.device, root: int = 0,
@@ -59,25 +60,23 @@ class TbGather:
         self.sizes = [(int(x[0]), int(x[1])) for x in sizes]
         self.max_bytes = max(b for b, _ in self.sizes)
         self.max_tbs = max(n for _, n in self.sizes)
-        self._send_tbs = torch.zeros(self.max_bytes, dtype=torch.uint8, device=device)
-        self._send_ok = torch.zeros(self.max_tbs, dtype=torch.uint8, device=device)
+        self._send = torch.zeros(self.max_bytes + self.max_tbs, dtype=torch.uint8, device=device)
         if self.rank == root:
-            self._recv_tbs = [torch.empty(self.max_bytes, dtype=torch.uint8, device=device) for _ in range(self.world)]
-            self._recv_ok = [torch.empty(self.max_tbs, dtype=torch.uint8, device=device) for _ in range(self.world)]
-            self.tbs = [t[:b] for t, (b, _) in zip(self._recv_tbs, self.sizes)]
-            self.crc_ok = [t[:n] for t, (_, n) in zip(self._recv_ok, self.sizes)]
+            self._recv = [torch.empty(self.max_bytes + self.max_tbs, dtype=torch.uint8, device=device)
+                          for _ in range(self.world)]
+            self.tbs = [t[:b] for t, (b, _) in zip(self._recv, self.sizes)]
+            self.crc_ok = [t[self.max_bytes: self.max_bytes + n] for t, (_, n) in zip(self._recv, self.sizes)]
         else:
-            self._recv_tbs = self._recv_ok = None
+            self._recv = None
             self.tbs = None
             self.crc_ok = None
 
     def gather(self, d_tbs: torch.Tensor, d_crc_ok: torch.Tensor) -> None:
         if d_tbs.numel() != self.tb_bytes or d_crc_ok.numel() != self.nof_tbs:
             raise ValueError("TB buffer sizes differ from the ones the gather was planned for")
-        self._send_tbs[: self.tb_bytes].copy_(d_tbs)
-        self._send_ok[: self.nof_tbs].copy_(d_crc_ok)
-        dist.gather(self._send_tbs, self._recv_tbs, dst=self.root, group=self.group)
-        dist.gather(self._send_ok, self._recv_ok, dst=self.root, group=self.group)
+        self._send[: self.tb_bytes].copy_(d_tbs)
+        self._send[self.max_bytes: self.max_bytes + self.nof_tbs].copy_(d_crc_ok)
+        dist.gather(self._send, self._recv, dst=self.root, group=self.group)
 
     def assemble(self):
         """Root only: (all TB bytes, all CRC flags) in rank order."""

@@ -425,6 +425,39 @@ int srsgpu_context_create(int device, srsgpu_context** out)
     srsgpu_context_destroy(ctx);
     return fail(SRSGPU_ERR_NO_MEMORY, "failed to allocate the CRC table arena");
   }
+  {
+    // Slice-by-4 byte tables of the TB / CB CRCs: T_0[v] = v x^order mod g (the byte table), T_k = T_(k-1) advanced
+    // by one zero byte.
+    const uint32_t      polys[3]  = {0x1864cfbu, 0x1800063u, 0x11021u};
+    const int           orders[3] = {24, 24, 16};
+    std::vector<uint32_t> tabs(3 * CRC_SLICE_WORDS);
+    for (int c = 0; c < 3; ++c) {
+      const uint32_t mask = (1u << orders[c]) - 1u;
+      uint32_t*      t    = tabs.data() + c * CRC_SLICE_WORDS;
+      for (uint32_t v = 0; v < 256; ++v) {
+        uint32_t r = v << (orders[c] - 8);
+        for (int k = 0; k < 8; ++k) {
+          r <<= 1;
+          if (r & (1u << orders[c])) {
+            r ^= polys[c];
+          }
+        }
+        t[v] = r & mask;
+      }
+      for (int k = 1; k < 4; ++k) {
+        for (uint32_t v = 0; v < 256; ++v) {
+          const uint32_t p = t[(k - 1) * 256 + v];
+          t[k * 256 + v]   = ((p << 8) ^ t[(p >> (orders[c] - 8)) & 0xffu]) & mask;
+        }
+      }
+    }
+    if (hipMalloc(&ctx->d_crc_slice, tabs.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipMemcpy(ctx->d_crc_slice, tabs.data(), tabs.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      srsgpu_context_destroy(ctx);
+      return fail(SRSGPU_ERR_HIP, "failed to upload the slice-by-4 CRC tables");
+    }
+  }
   *out = ctx;
   return SRSGPU_OK;
 }
@@ -465,7 +498,8 @@ void srsgpu_context_destroy(srsgpu_context* ctx)
       (void)hipFree(p);
     }
   }
-  for (void* p : {static_cast<void*>(ctx->d_crc_arena), static_cast<void*>(ctx->d_gold_x1),
+  for (void* p : {static_cast<void*>(ctx->d_crc_arena), static_cast<void*>(ctx->d_crc_slice),
+                  static_cast<void*>(ctx->d_gold_x1),
                   static_cast<void*>(ctx->d_gold_x2_jump), static_cast<void*>(ctx->d_gold_x2_lane),
                   static_cast<void*>(ctx->d_ofdm_twiddles)}) {
     if (p != nullptr) {
@@ -1253,7 +1287,7 @@ int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
     if (plan->count_pk[b] > 0) {
       launch_pdsch_encode_packed(b + 1, plan->d_enc[b] + plan->count[b], plan->count_pk[b], d_tbs, plan->d_tb_crc,
                                  plan->inline_tb_crc ? plan->d_tb : nullptr, out, plan->ctx->d_shifts[b],
-                                 plan->ctx->d_core[b], plan->ctx->d_crc_arena, s);
+                                 plan->ctx->d_core[b], plan->ctx->d_crc_arena, plan->ctx->d_crc_slice, s);
       HIP_TRY(hipGetLastError());
     }
     if (plan->count[b] > 0) {

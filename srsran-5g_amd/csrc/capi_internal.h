@@ -64,6 +64,9 @@ struct srsgpu_context {
   srsgpu::core_plan*                   d_core[2]   = {nullptr, nullptr};
   std::vector<srsgpu::core_plan>       core[2];
   uint32_t*                            d_crc_arena = nullptr;
+  /// Slice-by-4 byte tables (srsgpu::CRC_SLICE_WORDS per polynomial: CRC24A, CRC24B, CRC16), T_k[v] = v x^(order + 8 k)
+  /// mod g, k = 0..3.
+  uint32_t*                            d_crc_slice = nullptr;
   std::map<srsgpu::crc_key, srsgpu::crc_entry> crc_tables;
   std::map<size_t, size_t>             crc_free = {{0, srsgpu::CRC_ARENA_WORDS}};  ///< Free blocks: offset -> words.
   uint64_t                             crc_clock = 0;

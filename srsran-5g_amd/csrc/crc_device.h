@@ -154,6 +154,67 @@ __device__ __forceinline__ uint32_t gf2_mulmod(uint32_t r, uint32_t M, int order
 /// returns the CRC in every lane.
 /// [begin, end) (begin a multiple of CS; default the whole message) restricts the sum to that byte range's chunks: their
 /// contribution to the CRC of the whole nbytes-byte message (the CRC is linear, so slices XOR together).
+/// One 4-byte step of the slice-by-4 CRC (order 16 or 24): r' = (r x^32 + m x^order) mod g, m = the next four message
+/// bytes MSB first; T = the four byte tables T_k[v] = v x^(order + 8 k) mod g (4 x 256 words, context table
+/// CRC_SLICE_WORDS staged in LDS): four independent lookups instead of a chain of four.
+__device__ __forceinline__ uint32_t crc_step4(uint32_t r, uint32_t m, int order, const uint32_t* T)
+{
+  const uint32_t u = (r << (32 - order)) ^ m;
+  return T[u & 0xffu] ^ T[256u + ((u >> 8) & 0xffu)] ^ T[512u + ((u >> 16) & 0xffu)] ^ T[768u + (u >> 24)];
+}
+
+/// block_crc_chunks with the slice-by-4 tables T (T_0 is the byte table): whole 4-byte words of a chunk in one step
+/// each, a trailing partial word byte by byte. Same results.
+template <int CS, typename Data>
+__device__ inline uint32_t block_crc_slice4(Data data, int nbytes, const uint32_t* P, int order, uint32_t g,
+                                            const uint32_t* T, uint32_t* red, bool have_m0 = false, uint32_t m0 = 0)
+{
+  static_assert(CS % 4 == 0, "whole words per chunk");
+  const uint32_t mask = (1u << order) - 1u;
+  const int      L    = 8 * nbytes;
+  const int      nch  = (nbytes + CS - 1) / CS;
+  const int      c0   = static_cast<int>(threadIdx.x);
+  uint32_t       acc  = 0;
+  for (int c = c0; c < nch; c += blockDim.x) {
+    const int      b0 = c * CS;
+    const int      b1 = min(b0 + CS, nbytes);
+    const int      j  = 8 * b1 + order - 1;
+    const uint32_t M  = (have_m0 && c == c0) ? m0 : ((j < L) ? P[j] : (1u << (order + L - 1 - j)));
+    uint32_t       byte[CS];
+#pragma unroll
+    for (int k = 0; k < CS; ++k) {
+      byte[k] = (b0 + k < b1) ? static_cast<uint32_t>(data(b0 + k)) : 0u;
+    }
+    uint32_t rem = 0;
+#pragma unroll
+    for (int w = 0; w < CS / 4; ++w) {
+      const int k = 4 * w;
+      if (b0 + k + 4 <= b1) {
+        rem = crc_step4(rem, (byte[k] << 24) | (byte[k + 1] << 16) | (byte[k + 2] << 8) | byte[k + 3], order, T);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (b0 + k + q < b1) {
+            rem = ((rem << 8) ^ T[((rem >> (order - 8)) ^ byte[k + q]) & 0xffu]) & mask;
+          }
+        }
+      }
+    }
+    acc ^= gf2_mulmod(rem, M, order, g);
+  }
+  acc = wave_xor(acc);
+  if ((threadIdx.x % WAVE) == 0) {
+    red[threadIdx.x / WAVE] = acc;
+  }
+  __syncthreads();
+  uint32_t crc = 0;
+  for (int w = 0; w < static_cast<int>((blockDim.x + WAVE - 1) / WAVE); ++w) {
+    crc ^= red[w];
+  }
+  __syncthreads();
+  return crc;
+}
+
 /// The power M of chunk c of an nbytes-byte message (see block_crc_chunks), for a caller that issues the table load
 /// early (c < number of chunks).
 template <int CS>

@@ -515,7 +515,8 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
                                                                          uint32_t* __restrict__ out_words,
                                                                          const uint16_t* __restrict__ shift_table,
                                                                          const core_plan* __restrict__ core_plans,
-                                                                         const uint32_t* __restrict__ crc_tables)
+                                                                         const uint32_t* __restrict__ crc_tables,
+                                                                         const uint32_t* __restrict__ crc_slice)
 {
   using G = ebg<BG>;
   constexpr int WMAX = 384 / 32;
@@ -524,12 +525,12 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
   __shared__ __attribute__((aligned(4))) uint8_t msg[G::K * 384 / 8];  // message bytes, MSB first
   __shared__ uint32_t edge[G::NE];                 // column << 16 | lifted shift of every base-graph edge
   __shared__ uint16_t row_start[G::M + 1];
-  __shared__ uint32_t lut[256];
   __shared__ uint32_t red[PK_THREADS / WAVE];
+  __shared__ uint32_t t4b[CRC_SLICE_WORDS];        // CB CRC24B slice-by-4 tables
+  __shared__ uint32_t t4t[CRC_SLICE_WORDS];        // TB CRC (24A or 16) slice-by-4 tables (the carrier only)
 
   ENC_STAMP(0);
   ENC_PROF(9, __builtin_amdgcn_s_memrealtime());
-  __shared__ uint32_t lut_b[256];                  // CRC24B byte table
   const enc_desc d   = descs[blockIdx.x];
   const int      Z   = d.Z;
   const int      W   = Z / 32;
@@ -599,15 +600,30 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
       }
     }
   }
+  // Slice-by-4 CRC tables from the context (L2-resident, 8 words per lane; the barriers below publish them).
+  constexpr int TW = CRC_SLICE_WORDS / PK_THREADS;
   if (has_cbc) {
-    // CRC24B byte table: each lane's two entries while the loads are in flight (the barriers below publish it).
-    for (uint32_t t = static_cast<uint32_t>(tid); t < 256u; t += PK_THREADS) {
-      uint32_t r = t << 16;
+    const uint32_t* src = crc_slice + CRC_SLICE_24B * CRC_SLICE_WORDS;
+    uint32_t        t[TW];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        r = (r << 1) ^ ((r & 0x800000u) ? 0x1800063u : 0u);
-      }
-      lut_b[t] = r & 0xffffffu;
+    for (int q = 0; q < TW; ++q) {
+      t[q] = src[tid + q * PK_THREADS];
+    }
+#pragma unroll
+    for (int q = 0; q < TW; ++q) {
+      t4b[tid + q * PK_THREADS] = t[q];
+    }
+  }
+  if (carrier) {
+    const uint32_t* src = crc_slice + (tcd.order == 24 ? CRC_SLICE_24A : CRC_SLICE_16) * CRC_SLICE_WORDS;
+    uint32_t        t[TW];
+#pragma unroll
+    for (int q = 0; q < TW; ++q) {
+      t[q] = src[tid + q * PK_THREADS];
+    }
+#pragma unroll
+    for (int q = 0; q < TW; ++q) {
+      t4t[tid + q * PK_THREADS] = t[q];
     }
   }
 #pragma unroll
@@ -621,19 +637,18 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
   }
   // ---- Message bytes (ldpc_segmenter_tx_impl.cpp:144): TB(+TB CRC) bytes, zero padding / CRC slot / fillers. ----
   if (tfast) {
-    crc_byte_lut(lut, static_cast<int>(tcd.order), tcd.poly);
-    const int      order = static_cast<int>(tcd.order);
-    const uint32_t mask  = (1u << order) - 1u;
-    const int      nb    = static_cast<int>(tcd.nbytes);
-    uint32_t       rem[2] = {0u, 0u};
+    __syncthreads();  // t4t complete
+    const int order  = static_cast<int>(tcd.order);
+    const int nb     = static_cast<int>(tcd.nbytes);
+    uint32_t  rem[2] = {0u, 0u};
+    // Whole 4-byte words (the TB size is a multiple of 4 here): one slice-by-4 step each, the two chunks interleaved.
 #pragma unroll
-    for (int k = 0; k < TCS; ++k) {
+    for (int q = 0; q < TCS / 4; ++q) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int      c = tid + h * PK_THREADS;
-        const uint32_t b = (tw[h][k >> 2] >> (8 * (k & 3))) & 0xffu;
-        if (c * TCS + k < nb) {
-          rem[h] = ((rem[h] << 8) ^ lut[((rem[h] >> (order - 8)) ^ b) & 0xffu]) & mask;
+        const int c = tid + h * PK_THREADS;
+        if (c * TCS + 4 * q < nb) {
+          rem[h] = crc_step4(rem[h], __builtin_bswap32(tw[h][q]), order, t4t);
         }
       }
     }
@@ -654,10 +669,10 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
       tb_crc ^= red[w];
     }
   } else if (carrier) {
-    crc_byte_lut(lut, static_cast<int>(tcd.order), tcd.poly);
+    __syncthreads();  // t4t complete
     const uint8_t* tbp = tbs + tcd.byte_offset;
-    tb_crc = block_crc_chunks<16>([tbp](int i) { return tbp[i]; }, static_cast<int>(tcd.nbytes),
-                                  crc_tables + tcd.table, static_cast<int>(tcd.order), tcd.poly, lut, red);
+    tb_crc = block_crc_slice4<16>([tbp](int i) { return tbp[i]; }, static_cast<int>(tcd.nbytes),
+                                  crc_tables + tcd.table, static_cast<int>(tcd.order), tcd.poly, t4t, red);
   }
   ENC_STAMP(1);
 #pragma unroll
@@ -675,8 +690,8 @@ __global__ __launch_bounds__(PK_THREADS) void pdsch_encode_packed_kernel(const e
   ENC_STAMP(2);
   if (has_cbc) {
     __syncthreads();  // msg and lut_b complete
-    const uint32_t crc = block_crc_chunks<CB_CS>([](int q) { return msg[q]; }, cb_bytes, crc_tables + d.crc_table, 24,
-                                                 0x1800063u, lut_b, red, 0, -1, pre_m, m0);
+    const uint32_t crc = block_crc_slice4<CB_CS>([](int q) { return msg[q]; }, cb_bytes, crc_tables + d.crc_table, 24,
+                                                 0x1800063u, t4b, red, pre_m, m0);
     if (tid < 3) {
       msg[d.used / 8 + tid] = static_cast<uint8_t>(crc >> (16 - 8 * tid));
     }
@@ -811,6 +826,7 @@ void launch_pdsch_encode_packed(int              bg,
                                 const uint16_t*  d_shifts,
                                 const core_plan* d_core_plans,
                                 const uint32_t*  d_crc_tables,
+                                const uint32_t*  d_crc_slice,
                                 hipStream_t      s)
 {
   if (nof_cbs <= 0) {
@@ -818,10 +834,10 @@ void launch_pdsch_encode_packed(int              bg,
   }
   if (bg == 1) {
     pdsch_encode_packed_kernel<1><<<nof_cbs, PK_THREADS, 0, s>>>(d_desc, d_tbs, d_tb_crcs, d_tb_inline, d_out_words,
-                                                                  d_shifts, d_core_plans, d_crc_tables);
+                                                                  d_shifts, d_core_plans, d_crc_tables, d_crc_slice);
   } else {
     pdsch_encode_packed_kernel<2><<<nof_cbs, PK_THREADS, 0, s>>>(d_desc, d_tbs, d_tb_crcs, d_tb_inline, d_out_words,
-                                                                  d_shifts, d_core_plans, d_crc_tables);
+                                                                  d_shifts, d_core_plans, d_crc_tables, d_crc_slice);
   }
 }
 

@@ -111,6 +111,13 @@ struct tb_crc_slice {
   uint32_t begin;
   uint32_t end;
 };
+/// Slice-by-4 CRC tables in the context (crc_device.h block_crc_slice4): 4 x 256 words per polynomial, in the order
+/// CRC24A, CRC24B, CRC16.
+constexpr uint32_t CRC_SLICE_WORDS = 1024;
+constexpr int      CRC_SLICE_24A   = 0;
+constexpr int      CRC_SLICE_24B   = 1;
+constexpr int      CRC_SLICE_16    = 2;
+
 /// Slice length (256 lanes x 16-byte chunks); TBs without a contribution table take one slice (byte-table method).
 constexpr uint32_t TB_CRC_SLICE_BYTES = 4096;
 /// Largest TB whose CRC the packed encoder computes inline (one workgroup per TB); larger ones go to tb_crc_kernel.
@@ -149,6 +156,7 @@ void launch_pdsch_encode_packed(int              bg,
                                 const uint16_t*  d_shifts,
                                 const core_plan* d_core_plans,
                                 const uint32_t*  d_crc_tables,
+                                const uint32_t*  d_crc_slice,
                                 hipStream_t      s);
 
 /// Launches the batched rate dematcher (rate_dematcher.hip). mode 0: generic combining, 1: SIMD combining.

@@ -217,6 +217,7 @@ class InputSet:
         self.samples = torch.zeros(2 * self.ul.ofdm.nof_samples, dtype=torch.float32, device=dev)
         self.graph = None
         self.graph_back = None  # UE-sharded cell: the part after the grid exchange
+        self.graph_ul = None    # --leg-graphs: the UL leg's own graph (self.graph then holds the DL leg)
 
 
 def parse_args(argv=None):
@@ -236,7 +237,7 @@ def parse_args(argv=None):
     # 32 / 2 117.9k, 32 / 4 103.8k, 32 / 5 117.9k, 64 / 3 120.5k slots/s (set counts that are multiples of the 4
     # hardware queues serialise the sets' graph branches).
     ap.add_argument("--slots-per-step", type=int, default=32)
-    ap.add_argument("--input-sets", type=int, default=5, help="independent working sets rotated step by step")
+    ap.add_argument("--input-sets", type=int, default=9, help="independent working sets rotated step by step")
     ap.add_argument("--iterations", type=int, default=6)
     ap.add_argument("--snr-db", type=float, default=26.0)
     ap.add_argument("--worst-case", action="store_true", help="headline on Gaussian-noise input (all iterations)")
@@ -255,6 +256,11 @@ def parse_args(argv=None):
                     help="replay each input set on its own stream (up to --input-sets steps in flight)")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
                     help="replay each set's DL+UL pipeline as one captured HIP graph (default) or launch eagerly")
+    # Two graphs per set, each leg on its own stream, with 9 sets: 134.3k slots/s vs 130.0k for one graph per set
+    # with 5 sets (profiles/r3_leg_graphs_sweep.json: one graph per set with 7 sets drops to 123k; 7-14 sets with leg
+    # graphs give 132.9k-135.0k).
+    ap.add_argument("--leg-graphs", action=argparse.BooleanOptionalAction, default=True,
+                    help="capture the DL and UL legs of a step as two graphs replayed on two streams per input set")
     ap.add_argument("--graph-collectives", action="store_true",
                     help="N > 1: capture the RCCL exchanges (TB gather; grid exchange with --shard ues) inside the "
                          "step's graph instead of issuing them between graph launches")
@@ -386,10 +392,22 @@ def measure(args, env):
     # Pipelining across steps: each input set replays on its own stream, so a step's UL decode can overlap the next
     # set's front end (different buffers; a set's consecutive steps stay ordered on its stream).
     set_streams = [torch.cuda.Stream(dev) for _ in range(K)] if args.pipeline else None
+    # --leg-graphs: the DL and UL legs of a set as two graphs replayed on two streams of their own.
+    leg_graphs = args.leg_graphs and args.graph and not shard_x and not args.graph_collectives
+    ul_set_streams = [torch.cuda.Stream(dev) for _ in range(K)] if leg_graphs and args.pipeline else None
 
     def step(i):
         st = sets[i % K]
         cur = torch.cuda.current_stream(dev) if set_streams is None else set_streams[i % K]
+        if st.graph_ul is not None:
+            cur_ul = cur if ul_set_streams is None else ul_set_streams[i % K]
+            with torch.cuda.stream(cur):
+                st.graph.replay()
+            with torch.cuda.stream(cur_ul):
+                st.graph_ul.replay()
+                if tb_gather is not None:
+                    tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
+            return
         with torch.cuda.stream(cur):
             if st.graph is not None and st.graph_back is not None:
                 st.graph.replay()     # front part
@@ -424,7 +442,13 @@ def measure(args, env):
         # thread_local: the RCCL watchdog thread of a multi-GPU run keeps polling its events during the capture.
         for st in sets:
             st.graph = torch.cuda.CUDAGraph()
-            if shard_x and not args.graph_collectives:
+            if leg_graphs:
+                with torch.cuda.graph(st.graph, capture_error_mode="thread_local"):
+                    st.dl_group.execute(torch.cuda.current_stream(dev))
+                st.graph_ul = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(st.graph_ul, capture_error_mode="thread_local"):
+                    st.ul.execute(st.samples, torch.cuda.current_stream(dev))
+            elif shard_x and not args.graph_collectives:
                 # The collectives stay outside: the front and back parts are captured as two graphs.
                 with torch.cuda.graph(st.graph, capture_error_mode="thread_local"):
                     pipeline(st, part="front")
@@ -635,7 +659,9 @@ def measure(args, env):
                    "channel_estimate_layout": "compact (one row per allocation, CFO rotation in the demodulator)"
                                               if ul.estimate_layout == srsgpu.CE_COMPACT else "per symbol",
                    "leg_streams": "one stream" if args.serial_legs else "DL and UL on concurrent streams",
-                   "launch": "one captured HIP graph per step and input set" if args.graph else "eager launches",
+                   "launch": ("two captured HIP graphs per step and input set (DL leg, UL leg), each on its own "
+                              "stream" if leg_graphs else "one captured HIP graph per step and input set")
+                             if args.graph else "eager launches",
                    "pipelining": (f"up to {K} steps in flight: each input set's step runs on its own stream"
                                   if args.pipeline else "steps serialised on one stream"),
                    "slots_per_step": slots_per_step,
@@ -705,7 +731,7 @@ def measure(args, env):
                 "cb_outcome_agreement": float(np.mean(gpu_cb_ok == (ref_iters >= 0)))}
     # Release the working sets (graphs first) before another workload is measured in the same process.
     for st in sets:
-        st.graph = st.graph_back = None
+        st.graph = st.graph_back = st.graph_ul = None
     del sets
     torch.cuda.synchronize()
     torch.cuda.empty_cache()

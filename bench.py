@@ -420,7 +420,9 @@ def measure(args, env):
             if tb_gather is not None and not (st.graph is not None and args.graph_collectives):
                 tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
 
-    for i in range(args.warmup):
+    # Every input set runs at least once before timing (its buffers, plans and code first touched), whatever --warmup.
+    n_warm = max(args.warmup, K)
+    for i in range(n_warm):
         step(i)
     torch.cuda.synchronize()
     skip = [s for s in os.environ.get("SRSGPU_BENCH_SKIP", "").split(",") if s]
@@ -462,7 +464,7 @@ def measure(args, env):
                     whole(st)
                     if tb_gather is not None and args.graph_collectives:
                         tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
-        for i in range(args.warmup):
+        for i in range(n_warm):
             step(i)
         torch.cuda.synchronize()
 
@@ -667,6 +669,7 @@ def measure(args, env):
                    "slots_per_step": slots_per_step,
                    "dl_slots_per_step": S_dl, "ul_slots_per_step": S_ul,
                    "input_sets": K,
+                   "warmup_steps_run": n_warm,  # max(--warmup, input sets), eager and again after the graph capture
                    "working_set_mb": K * set_bytes / 2 ** 20,
                    "timed_region_s": elapsed,
                    "steps_requested": args.steps,

@@ -388,13 +388,40 @@ int srsgpu_ofdm_demodulator_plan_create(srsgpu_context*           ctx,
                                         const uint32_t*           slot_index,
                                         srsgpu_ofdm_plan**        plan);
 
+/** Symbol-granularity plans — replace srsran::ofdm_symbol_modulator::modulate(output, grid, port, symbol_index) and
+ *  ofdm_symbol_demodulator::demodulate(grid, input, port, symbol_index) (include/srsran/phy/lower/modulation/
+ *  ofdm_modulator.h:58, ofdm_demodulator.h:59), batched over ports and a run of consecutive symbols: symbols
+ *  [first_symbol, first_symbol + nof_symbols) of slot `slot_index` of the subframe (the symbol index within the
+ *  subframe the reference passes is slot_index * symbols_per_slot + first_symbol). Layouts: grid rows
+ *  [port][symbol - first_symbol][subcarrier]; samples [port][CP + N of each symbol, consecutive]
+ *  (srsgpu_ofdm_plan_sample_offset(plan, 0, port)). Executed with srsgpu_ofdm_(de)modulator_plan_execute. */
+int srsgpu_ofdm_modulator_symbols_plan_create(srsgpu_context*           ctx,
+                                              const srsgpu_ofdm_config* cfg,
+                                              uint32_t                  nof_ports,
+                                              uint32_t                  slot_index,
+                                              uint32_t                  first_symbol,
+                                              uint32_t                  nof_symbols,
+                                              srsgpu_ofdm_plan**        plan);
+
+int srsgpu_ofdm_demodulator_symbols_plan_create(srsgpu_context*           ctx,
+                                                const srsgpu_ofdm_config* cfg,
+                                                uint32_t                  nof_ports,
+                                                uint32_t                  slot_index,
+                                                uint32_t                  first_symbol,
+                                                uint32_t                  nof_symbols,
+                                                srsgpu_ofdm_plan**        plan);
+
 /** Total number of complex samples of the plan's time buffer (all grids and ports). */
 uint64_t srsgpu_ofdm_plan_nof_samples(const srsgpu_ofdm_plan* plan);
 
 /** First complex sample of (grid, port) in the time buffer. */
 uint64_t srsgpu_ofdm_plan_sample_offset(const srsgpu_ofdm_plan* plan, uint32_t grid, uint32_t port);
 
-/** Modulates d_grids into d_samples. Asynchronous on `stream`, hipGraph-capturable. */
+/** Modulates d_grids into d_samples. Asynchronous on `stream`, hipGraph-capturable.
+ *  Concurrency: plans of the split DFT sizes (9216..98304 points) own a mutable HBM scratch row per (grid, port,
+ *  symbol) job, so one such plan must not execute on two streams at the same time (order the executes, or create one
+ *  plan per stream). Plans of the other sizes hold read-only state only and may run concurrently. Same for the
+ *  demodulator below. */
 int srsgpu_ofdm_modulator_plan_execute(const srsgpu_ofdm_plan* plan,
                                        const uint32_t*         d_grids,
                                        float*                  d_samples,

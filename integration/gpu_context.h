@@ -30,6 +30,36 @@ inline void srsgpu_check(int r, const char* who)
   }
 }
 
+/// Makes the context's device current for the duration of a public entry point and restores the caller's device on
+/// exit. The reference hands binding objects to arbitrary worker threads (its processor pools), whose current device
+/// is whatever they used last, and a lazily grown buffer (staged_buffer::reserve, the HARQ arena) is allocated on the
+/// calling thread's current device: without this, a grow on device != 0 would land on the wrong GPU.
+class device_scope
+{
+public:
+  device_scope(const srsgpu_context* ctx, const char* who)
+  {
+    hip_check(hipGetDevice(&prev), who, "current device");
+    const int dev = srsgpu_context_device(ctx);
+    if (dev != prev) {
+      hip_check(hipSetDevice(dev), who, "device");
+      changed = true;
+    }
+  }
+  device_scope(const device_scope&)            = delete;
+  device_scope& operator=(const device_scope&) = delete;
+  ~device_scope()
+  {
+    if (changed) {
+      (void)hipSetDevice(prev);
+    }
+  }
+
+private:
+  int  prev    = 0;
+  bool changed = false;
+};
+
 /// The srsgpu context of `device`, one per process and device while anyone holds it: destroyed with its last owner.
 inline std::shared_ptr<srsgpu_context> shared_context(int device)
 {

@@ -10,8 +10,11 @@
 // is shared by the factory and every accelerator it creates (integration/gpu_context.h): accelerators outlive it.
 #include "gpu_context.h"
 #include "hw_accelerator_pusch_dec_gpu.h"
+#include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <list>
+#include <string>
 #include <stdexcept>
 #include <vector>
 
@@ -73,61 +76,74 @@ public:
 
   bool enqueue_operation(span<const uint8_t> data, span<const uint8_t> /*aux_data*/, unsigned /*cb_index*/) override
   {
-    // Configuration errors, not back-pressure: pdsch_encoder_hw_impl retries a false enqueue forever.
+    // Configuration errors are not back-pressure: pdsch_encoder_hw_impl retries a false enqueue forever, and an
+    // exception would unwind through a processor task that is not exception-safe (std::terminate). The TB is accepted
+    // and its codeword comes out zero (one bad grant, not a dead gNB); the error is logged once per accelerator.
+    error.clear();
     if (cfg.cb_mode) {
-      throw std::invalid_argument(std::string(WHO) + ": codeblock mode is not supported (is_cb_mode_supported())");
+      error = "codeblock mode is not supported (is_cb_mode_supported())";
+    } else if (data.size() > MAX_TB_BYTES || data.size() * 8 != cfg.nof_tb_bits) {
+      error = "TB of " + std::to_string(data.size()) + " bytes does not match the configured " +
+              std::to_string(cfg.nof_tb_bits) + " bits";
+    } else {
+      std::memcpy(h_tb, data.data(), data.size());
+      tb_bytes = static_cast<unsigned>(data.size());
     }
-    if (data.size() > MAX_TB_BYTES || data.size() * 8 != cfg.nof_tb_bits) {
-      throw std::length_error(std::string(WHO) + ": TB of " + std::to_string(data.size()) +
-                              " bytes does not match the configured " + std::to_string(cfg.nof_tb_bits) + " bits");
-    }
-    std::memcpy(h_tb, data.data(), data.size());
-    tb_bytes = static_cast<unsigned>(data.size());
-    encoded  = false;
+    encoded = false;
     return true;
   }
 
   /// data: the codeword, one bit per byte (do_unpack) or packed; aux_data: the packed codeword.
   bool dequeue_operation(span<uint8_t> data, span<uint8_t> aux_data, unsigned /*cb_index*/) override
   {
+    gpu::device_scope dev(ctx, WHO);
     const unsigned qm     = static_cast<unsigned>(cfg.modulation);
     const unsigned nshort = cfg.nof_short_segments;
     const unsigned G      = cfg.cw_length_a * nshort + cfg.cw_length_b * (cfg.nof_segments - nshort);
+    const size_t   nbytes = (G + 7) / 8;
     if (!encoded) {
-      srsgpu_pdsch_tb_config c = {};
-      c.base_graph       = (cfg.base_graph_index == ldpc_base_graph_type::BG1) ? 1 : 2;
-      c.rv               = static_cast<uint8_t>(cfg.rv);
-      c.modulation_order = static_cast<uint8_t>(qm);
-      c.nof_layers       = static_cast<uint8_t>(cfg.cw_length_b > cfg.cw_length_a ? (cfg.cw_length_b - cfg.cw_length_a) / qm
-                                                                                  : 1);
-      c.tbs_bytes        = tb_bytes;
-      c.nof_ch_symbols   = G / qm;
-      c.Nref             = cfg.Nref;
-      c.tb_offset        = 0;
-      c.cw_offset        = 0;
-      if ((G + 7) / 8 > MAX_CW_BYTES) {
-        throw std::length_error(std::string(WHO) + ": codeword beyond get_max_supported_buff_size()");
+      if (error.empty() && nbytes > MAX_CW_BYTES) {
+        error = "codeword beyond get_max_supported_buff_size()";
       }
-      srsgpu_pdsch_encoder_plan* plan = plan_for(c);
-      hip_check(hipMemcpyAsync(d_tb, h_tb, tb_bytes, hipMemcpyHostToDevice, stream), "TB upload");
-      if (srsgpu_pdsch_encoder_plan_execute(plan, d_tb, d_cw, stream) != SRSGPU_OK) {
-        throw std::runtime_error(std::string(WHO) + ": " + srsgpu_last_error());
+      srsgpu_pdsch_encoder_plan* plan = nullptr;
+      if (error.empty()) {
+        srsgpu_pdsch_tb_config c = {};
+        c.base_graph       = (cfg.base_graph_index == ldpc_base_graph_type::BG1) ? 1 : 2;
+        c.rv               = static_cast<uint8_t>(cfg.rv);
+        c.modulation_order = static_cast<uint8_t>(qm);
+        c.nof_layers       = static_cast<uint8_t>(
+            cfg.cw_length_b > cfg.cw_length_a && qm != 0 ? (cfg.cw_length_b - cfg.cw_length_a) / qm : 1);
+        c.tbs_bytes      = tb_bytes;
+        c.nof_ch_symbols = qm != 0 ? G / qm : 0;
+        c.Nref           = cfg.Nref;
+        c.tb_offset      = 0;
+        c.cw_offset      = 0;
+        plan             = plan_for(c);
       }
-      hip_check(hipMemcpyAsync(h_cw, d_cw, (G + 7) / 8, hipMemcpyDeviceToHost, stream), "codeword download");
-      hip_check(hipStreamSynchronize(stream), "synchronise");
+      if (plan == nullptr) {
+        report();
+        std::memset(h_cw, 0, std::min<size_t>(nbytes, MAX_CW_BYTES));
+      } else {
+        hip_check(hipMemcpyAsync(d_tb, h_tb, tb_bytes, hipMemcpyHostToDevice, stream), "TB upload");
+        if (srsgpu_pdsch_encoder_plan_execute(plan, d_tb, d_cw, stream) != SRSGPU_OK) {
+          throw std::runtime_error(std::string(WHO) + ": " + srsgpu_last_error());
+        }
+        hip_check(hipMemcpyAsync(h_cw, d_cw, nbytes, hipMemcpyDeviceToHost, stream), "codeword download");
+        hip_check(hipStreamSynchronize(stream), "synchronise");
+      }
       encoded = true;
     }
-    const size_t nbytes = (G + 7) / 8;
+    const size_t avail = std::min<size_t>(nbytes, MAX_CW_BYTES);
     if (!aux_data.empty()) {
-      std::memcpy(aux_data.data(), h_cw, std::min(aux_data.size(), nbytes));
+      std::memcpy(aux_data.data(), h_cw, std::min(aux_data.size(), avail));
     }
     if (cfg.do_unpack) {
-      const size_t n = std::min<size_t>(data.size(), G);
+      const size_t n = std::min<size_t>(data.size(), 8 * avail);
       for (size_t i = 0; i != n; ++i) {
         data[i] = (h_cw[i >> 3] >> (7 - (i & 7))) & 1U;
       }
     } else {
-      std::memcpy(data.data(), h_cw, std::min(data.size(), nbytes));
+      std::memcpy(data.data(), h_cw, std::min(data.size(), avail));
     }
     return true;
   }
@@ -148,7 +164,8 @@ private:
     }
     srsgpu_pdsch_encoder_plan* plan = nullptr;
     if (srsgpu_pdsch_encoder_plan_create(ctx, &key, 1, &plan) != SRSGPU_OK) {
-      throw std::runtime_error(std::string(WHO) + ": " + srsgpu_last_error());
+      error = srsgpu_last_error();
+      return nullptr;
     }
     cache.push_front({key, plan});
     if (cache.size() > PLAN_CACHE_SIZE) {
@@ -169,6 +186,16 @@ private:
   bool                           encoded  = false;
   hw_pdsch_encoder_configuration cfg      = {};
   std::list<cached_plan>         cache;
+  std::string                    error;  ///< Configuration error of the current TB (its codeword is zero).
+  bool                           reported = false;
+
+  void report()
+  {
+    if (!reported) {
+      std::fprintf(stderr, "%s: %s (codeword zeroed; further errors not logged)\n", WHO, error.c_str());
+      reported = true;
+    }
+  }
 };
 
 class hw_accelerator_pdsch_enc_factory_gpu : public hw_accelerator_pdsch_enc_factory

@@ -24,6 +24,7 @@
 #include "gpu_context.h"
 #include "hw_accelerator_pusch_dec_gpu.h"
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <list>
 #include <map>
@@ -157,23 +158,31 @@ public:
 
   bool enqueue_operation(span<const int8_t> data, span<const int8_t> /*aux_data*/, unsigned cb_index) override
   {
-    // Configuration errors, not back-pressure: pusch_decoder_hw_impl retries a false enqueue forever
-    // (pusch_decoder_hw_impl.cpp:204-354), so they are reported loudly instead.
+    gpu::device_scope dev(ctx, WHO);
+    // Configuration errors are not back-pressure: pusch_decoder_hw_impl retries a false enqueue forever
+    // (pusch_decoder_hw_impl.cpp:204-354), and an exception would unwind through a thread-pool task that is not
+    // exception-safe (std::terminate). The codeblock is accepted and reported as failed instead (CRC fail, all
+    // iterations, zero message), and the error is logged once per accelerator.
+    std::string error;
     if (cb_index >= cfgs.size()) {
-      throw std::logic_error(std::string(WHO) + ": codeblock " + std::to_string(cb_index) + " enqueued unconfigured");
+      error = "codeblock " + std::to_string(cb_index) + " enqueued unconfigured";
+    } else if (cfgs[cb_index].absolute_cb_id >= max_cb_ids) {
+      error = "absolute codeblock id " + std::to_string(cfgs[cb_index].absolute_cb_id) +
+              " beyond the HARQ arena (max_cb_ids " + std::to_string(max_cb_ids) +
+              ": size it for the rx buffer pool's codeblocks)";
+    } else if (data.size() > MAX_E) {
+      error = "rate-matched length " + std::to_string(data.size()) + " beyond the accelerator's limit";
     }
-    if (cfgs[cb_index].absolute_cb_id >= max_cb_ids) {
-      throw std::out_of_range(std::string(WHO) + ": absolute codeblock id " +
-                              std::to_string(cfgs[cb_index].absolute_cb_id) + " beyond the HARQ arena (max_cb_ids " +
-                              std::to_string(max_cb_ids) + ": size it for the rx buffer pool's codeblocks)");
-    }
-    if (data.size() > MAX_E) {
-      throw std::length_error(std::string(WHO) + ": rate-matched length " + std::to_string(data.size()) +
-                              " beyond the accelerator's limit");
+    if (!error.empty()) {
+      report(error);
+      grow(staged, static_cast<unsigned>(ops.size()) + 1);
+      ops.push_back({cb_index, static_cast<uint32_t>(staged), 0, true});
+      decoded = false;
+      return true;
     }
     grow(staged + data.size(), static_cast<unsigned>(ops.size()) + 1);
     std::memcpy(h_llrs + staged, data.data(), data.size());
-    ops.push_back({cb_index, static_cast<uint32_t>(staged), static_cast<uint32_t>(data.size())});
+    ops.push_back({cb_index, static_cast<uint32_t>(staged), static_cast<uint32_t>(data.size()), false});
     staged += data.size();
     decoded = false;
     return true;
@@ -181,6 +190,7 @@ public:
 
   bool dequeue_operation(span<uint8_t> data, span<int8_t> /*aux_data*/, unsigned cb_index) override
   {
+    gpu::device_scope dev(ctx, WHO);
     if (!decoded) {
       run();
     }
@@ -196,9 +206,11 @@ public:
   void read_operation_outputs(hw_pusch_decoder_outputs& out, unsigned cb_index, unsigned /*absolute_cb_id*/) override
   {
     const int i             = op_of(cb_index);
-    const int it            = (i >= 0) ? h_iters[i] : -1;
-    out.CRC_pass            = (i >= 0) && h_flags[i] != 0;
-    out.nof_ldpc_iterations = (it > 0) ? static_cast<unsigned>(it) : cfgs[cb_index].max_nof_ldpc_iterations;
+    const bool ok           = (i >= 0) && !ops[i].failed;
+    const int  it           = ok ? h_iters[i] : -1;
+    out.CRC_pass            = ok && h_flags[i] != 0;
+    out.nof_ldpc_iterations = (it > 0) ? static_cast<unsigned>(it)
+                                       : (cb_index < cfgs.size() ? cfgs[cb_index].max_nof_ldpc_iterations : 0U);
   }
 
   void free_harq_context_entry(unsigned absolute_cb_id) override { arena->release(absolute_cb_id); }
@@ -210,7 +222,17 @@ private:
     unsigned cb_index;
     uint32_t llr_offset;
     uint32_t length;
+    bool     failed;  ///< Rejected at enqueue or by the plan: reported as a CRC failure.
   };
+
+  /// Logs a configuration error (once per accelerator: a misconfigured cell would repeat it every slot).
+  void report(const std::string& error)
+  {
+    if (!reported) {
+      std::fprintf(stderr, "%s: %s (codeblock reported as failed; further errors not logged)\n", WHO, error.c_str());
+      reported = true;
+    }
+  }
   struct cached_plan {
     std::vector<srsgpu_pusch_cb_config> key;
     srsgpu_pusch_cb_plan*               plan;
@@ -274,7 +296,8 @@ private:
     srsgpu_pusch_cb_plan* plan = nullptr;
     if (srsgpu_pusch_cb_plan_create(ctx, SRSGPU_LDPC_IMPL_SIMD, key.data(), static_cast<uint32_t>(key.size()), &plan) !=
         SRSGPU_OK) {
-      throw std::runtime_error(std::string(WHO) + ": " + srsgpu_last_error());
+      report(srsgpu_last_error());
+      return nullptr;
     }
     cache.push_front({key, plan});
     if (cache.size() > PLAN_CACHE_SIZE) {
@@ -284,13 +307,21 @@ private:
     return plan;
   }
 
-  /// Decodes every enqueued codeblock of the TB on the device.
+  /// Decodes every enqueued codeblock of the TB on the device (the failed ones are skipped; their message is zero).
   void run()
   {
-    std::vector<srsgpu_pusch_cb_config> key(ops.size());
-    for (size_t i = 0; i != ops.size(); ++i) {
+    const size_t n = ops.size();
+    std::memset(h_msgs, 0, n * SRSGPU_CB_MSG_STRIDE);
+    std::memset(h_flags, 0, n);
+    std::vector<srsgpu_pusch_cb_config>    key;
+    std::vector<std::pair<unsigned, bool>> ids;
+    for (size_t i = 0; i != n; ++i) {
+      h_iters[i] = -1;
+      if (ops[i].failed) {
+        continue;
+      }
       const hw_pusch_decoder_configuration& c = cfgs[ops[i].cb_index];
-      srsgpu_pusch_cb_config&               k = key[i];
+      srsgpu_pusch_cb_config                k;
       std::memset(&k, 0, sizeof(k));
       k.base_graph       = (c.base_graph_index == ldpc_base_graph_type::BG1) ? 1 : 2;
       k.rv               = static_cast<uint8_t>(c.rv);
@@ -308,12 +339,19 @@ private:
       k.llr_offset       = ops[i].llr_offset;
       k.harq_offset      = c.absolute_cb_id * MAX_CB_LLRS;
       k.out_offset       = static_cast<uint32_t>(i * SRSGPU_CB_MSG_STRIDE);
+      key.push_back(k);
+      ids.emplace_back(c.absolute_cb_id, c.new_data);
     }
-    srsgpu_pusch_cb_plan*                   plan = plan_for(key);
-    const size_t                            n    = ops.size();
-    std::vector<std::pair<unsigned, bool>> ids(n);
-    for (size_t i = 0; i != n; ++i) {
-      ids[i] = {cfgs[ops[i].cb_index].absolute_cb_id, cfgs[ops[i].cb_index].new_data};
+    decoded = true;
+    if (key.empty()) {
+      return;
+    }
+    srsgpu_pusch_cb_plan* plan = plan_for(key);
+    if (plan == nullptr) {  // rejected by the plan's validation (reported): every codeblock of the TB fails
+      for (op& o : ops) {
+        o.failed = true;
+      }
+      return;
     }
     // A retransmission into a released slot combines with zeros (a new soft buffer).
     for (unsigned id : arena->acquire(ids)) {
@@ -321,6 +359,7 @@ private:
     }
     hip_check(hipMemcpyAsync(d_llrs, h_llrs, staged, hipMemcpyHostToDevice, stream), "LLR upload");
     hip_check(hipMemsetAsync(d_flags, 0, n, stream), "flags");
+    hip_check(hipMemsetAsync(d_msgs, 0, n * SRSGPU_CB_MSG_STRIDE, stream), "messages");
     if (srsgpu_pusch_cb_plan_execute(plan, d_llrs, d_harq, d_msgs, d_iters, d_flags, stream) != SRSGPU_OK) {
       throw std::runtime_error(std::string(WHO) + ": " + srsgpu_last_error());
     }
@@ -328,7 +367,6 @@ private:
     hip_check(hipMemcpyAsync(h_iters, d_iters, n * sizeof(int32_t), hipMemcpyDeviceToHost, stream), "iterations");
     hip_check(hipMemcpyAsync(h_flags, d_flags, n, hipMemcpyDeviceToHost, stream), "flags");
     hip_check(hipStreamSynchronize(stream), "synchronise");
-    decoded = true;
   }
 
   std::shared_ptr<harq_arena>                 arena;
@@ -348,6 +386,7 @@ private:
   unsigned                                    cap_cbs  = 0;
   size_t                                      staged   = 0;
   bool                                        decoded  = false;
+  bool                                        reported = false;
   std::vector<hw_pusch_decoder_configuration> cfgs;
   std::vector<op>                             ops;
   std::list<cached_plan>                      cache;

@@ -55,6 +55,7 @@ public:
                                  crc_calculator*                  crc,
                                  const configuration&             cfg) override
   {
+    gpu::device_scope dev_scope(ctx, "ldpc_decoder_gpu");
     srsgpu_ldpc_decoder_config c;
     std::memset(&c, 0, sizeof(c));
     c.base_graph      = (cfg.block_conf.tb_common.base_graph == ldpc_base_graph_type::BG1) ? 1 : 2;

@@ -99,6 +99,7 @@ public:
 
   void modulate(resource_grid_writer& grid, span<const bit_buffer> codewords, const config_t& config) override
   {
+    gpu::device_scope dev_scope(ctx, WHO);
     const precoding_configuration& pc = config.precoding;
     const unsigned                 L  = pc.get_nof_layers();
     const unsigned                 P  = pc.get_nof_ports();
@@ -252,6 +253,7 @@ public:
 
   void map(resource_grid_writer& grid, const config_t& config) override
   {
+    gpu::device_scope dev_scope(ctx, WHO);
     const precoding_configuration& pc = config.precoding;
     const unsigned                 L  = pc.get_nof_layers();
     const unsigned                 P  = pc.get_nof_ports();

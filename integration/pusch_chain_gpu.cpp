@@ -92,6 +92,7 @@ public:
 
   void estimate(channel_estimate& estimate, const resource_grid_reader& grid, const configuration& config) override
   {
+    gpu::device_scope dev_scope(ctx, WHO);
     const unsigned P = config.rx_ports.size();
     const unsigned L = config.get_nof_tx_layers();
     if (P == 0 || P > 4 || L == 0 || L > 4 || config.c_prefix != cyclic_prefix::NORMAL) {
@@ -264,6 +265,7 @@ public:
                   const channel_estimate&     estimates,
                   const configuration&        config) override
   {
+    gpu::device_scope dev_scope(ctx, WHO);
     const unsigned P  = config.rx_ports.size();
     const unsigned L  = config.nof_tx_layers;
     const unsigned Qm = get_bits_per_symbol(config.modulation);

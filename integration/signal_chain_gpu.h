@@ -6,6 +6,8 @@
 #pragma once
 
 #include "srsran/phy/lower/modulation/modulation_factories.h"
+#include "srsran/phy/lower/processors/downlink/pdxch/pdxch_processor_factories.h"
+#include "srsran/phy/lower/processors/uplink/puxch/puxch_processor_factories.h"
 #include "srsran/phy/upper/channel_processors/pdsch/factories.h"
 #include "srsran/phy/upper/channel_processors/pusch/factories.h"
 #include "srsran/phy/upper/signal_processors/signal_processor_factories.h"
@@ -60,9 +62,21 @@ std::shared_ptr<pdsch_modulator_factory> create_pdsch_modulator_factory_gpu(int 
 /// PDSCH DM-RS processor on GPU `device` (integration/pdsch_chain_gpu.cpp).
 std::shared_ptr<dmrs_pdsch_processor_factory> create_dmrs_pdsch_processor_factory_gpu(int device);
 
-/// OFDM slot modulator / demodulator on GPU `device` (integration/ofdm_gpu.cpp). The symbol-granularity creators
-/// return nullptr (the GPU transforms whole slots), as the reference's factories do for unsupported configurations.
+/// OFDM modulator / demodulator on GPU `device` (integration/ofdm_gpu.cpp): slot objects (one launch per port and
+/// slot) and symbol objects (one launch per port and symbol, synchronous: correct under the reference's own
+/// pdxch_processor_impl / puxch_processor_impl, but the lower-PHY processors below are the GPU's throughput path).
 std::shared_ptr<ofdm_modulator_factory>   create_ofdm_modulator_factory_gpu(int device);
 std::shared_ptr<ofdm_demodulator_factory> create_ofdm_demodulator_factory_gpu(int device);
+
+/// Lower-PHY PDxCH processor on GPU `device` (integration/lower_phy_gpu.cpp), the replacement of
+/// create_pdxch_processor_factory_sw (pdxch_processor_factories.h:68; lower_phy_factory.cpp:70): each slot's grid is
+/// modulated (all ports) asynchronously when the request arrives, process_symbol() hands out the symbol's samples.
+std::shared_ptr<pdxch_processor_factory> create_pdxch_processor_factory_gpu(int device);
+
+/// Lower-PHY PUxCH processor on GPU `device` (integration/lower_phy_gpu.cpp), the replacement of
+/// create_puxch_processor_factory_sw (puxch_processor_factories.h:69; lower_phy_factory.cpp:84): every received symbol
+/// (all ports) is demodulated by one asynchronous launch; up to `max_symbols_in_flight` symbols are outstanding before
+/// process_symbol() waits (0: each symbol is demodulated and notified within its own call, the reference's timing).
+std::shared_ptr<puxch_processor_factory> create_puxch_processor_factory_gpu(int device, unsigned max_symbols_in_flight = 2);
 
 } // namespace srsran

@@ -4,7 +4,7 @@
 # pdsch_processor_impl) and the components they need that libsrsref.so / libsrshal.so do not hold (UCI decoder, polar
 # and short-block codes, PT-RS generator, UL-SCH information), compiled from their sources where they lie under
 # /root/reference, the signal-chain bindings a maintainer adds (integration/*_gpu.cpp) and the C harness
-# oracle/ref/ref_chain.cpp, linked against oracle/_ref/libsrshal.so, libsrsref.so and libsrsgpu_phy.so. Output only
+# oracle/ref/ref_chain.cpp, the lower-PHY processors (pdxch / puxch_processor_impl) with the harness oracle/ref/ref_lower.cpp, linked against oracle/_ref/libsrshal.so, libsrsref.so and libsrsgpu_phy.so. Output only
 # into oracle/_ref/ (git-ignored, shipped to the GPU box with the snapshot). Skips quietly without the reference tree.
 set -euo pipefail
 REF=${SRSRAN_REF:-/root/reference}
@@ -42,7 +42,12 @@ SRCS=(
   "$ROOT/integration/pusch_chain_gpu.cpp"
   "$ROOT/integration/pdsch_chain_gpu.cpp"
   "$ROOT/integration/ofdm_gpu.cpp"
+  "$ROOT/integration/lower_phy_gpu.cpp"
+  "$REF/lib/phy/lower/processors/downlink/pdxch/pdxch_processor_impl.cpp"
+  "$REF/lib/phy/lower/processors/uplink/puxch/puxch_processor_impl.cpp"
+  "$REF/lib/instrumentation/traces/du_traces.cpp"
   "$HERE/ref/ref_chain.cpp"
+  "$HERE/ref/ref_lower.cpp"
 )
 OBJS=()
 pids=()

@@ -712,6 +712,19 @@ bool pk4_layout_for(int bg, int max_layers, const std::vector<dec_desc>& cbs, pk
     }
   }
   out.groups = static_cast<int>(out.slots.size() / LDPC_PK4);
+  // The PK4 kernel counts a workgroup's occupied slots and treats slots [0, count) as used: every workgroup must hold
+  // its codeblocks first and its empty slots (a zero dec_desc, which aliases codeblock 0's outputs) last. A layout
+  // that breaks this is refused (the caller then launches the one-codeblock kernel).
+  for (int g = 0; g < out.groups; ++g) {
+    bool empty_seen = false;
+    for (int k = 0; k < LDPC_PK4; ++k) {
+      const bool empty = out.slots[static_cast<size_t>(g) * LDPC_PK4 + k].nof_llr == 0;
+      if ((k == 0 && empty) || (empty_seen && !empty)) {
+        return false;
+      }
+      empty_seen = empty_seen || empty;
+    }
+  }
   return true;
 }
 

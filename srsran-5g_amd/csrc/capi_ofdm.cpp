@@ -3,6 +3,7 @@
 // the TS 38.211 section 5.4 phase-compensation coefficients (computed in double like phase_compensation_lut.h:50) and
 // one job per (grid, port, symbol).
 #include "capi_internal.h"
+#include <algorithm>
 #include <cmath>
 #include <complex>
 #include <vector>
@@ -69,7 +70,9 @@ int plan_create(srsgpu_context*           ctx,
                 uint32_t                  nof_grids,
                 uint32_t                  nof_ports,
                 const uint32_t*           slot_index,
-                srsgpu_ofdm_plan**        plan_out)
+                srsgpu_ofdm_plan**        plan_out,
+                uint32_t                  first_symbol = 0,
+                uint32_t                  nof_symbols  = ~0u)
 {
   if (ctx == nullptr || cfg == nullptr || plan_out == nullptr || (slot_index == nullptr && nof_grids > 0)) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
@@ -104,6 +107,14 @@ int plan_create(srsgpu_context*           ctx,
   const bool     ext   = cfg->cp_extended != 0;
   const uint32_t nsymb = ext ? 12u : 14u;
   const uint32_t nslot = 1u << mu;  // slots per subframe
+  // Symbol range of every grid (the symbol-granularity plans: ofdm_symbol_(de)modulator): whole slots by default.
+  if (nof_symbols == ~0u) {
+    nof_symbols = nsymb - std::min(first_symbol, nsymb);
+  }
+  if (nof_symbols == 0 || first_symbol + nof_symbols > nsymb) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "symbols [%u, %u) outside the %u symbols of a slot", first_symbol,
+                first_symbol + nof_symbols, nsymb);
+  }
   // Phase compensation per symbol of the subframe (phase_compensation_lut.h:50), times the scale, in float.
   const double              srate = 15e3 * static_cast<double>(1u << mu) * N;
   std::vector<std::complex<float>> coef(nsymb * nslot);
@@ -141,11 +152,12 @@ int plan_create(srsgpu_context*           ctx,
     }
     for (uint32_t p = 0; p < nof_ports; ++p) {
       plan->offsets.push_back(pos);
-      for (uint32_t l = 0; l < nsymb; ++l) {
+      for (uint32_t i = 0; i < nof_symbols; ++i) {
+        const uint32_t l   = first_symbol + i;
         const uint32_t s   = nsymb * slot_index[g] + l;
         const uint32_t cp  = cp_samples(mu, N, ext, s);
         ofdm_job       jb{};
-        jb.grid_offset     = ((g * nof_ports + p) * nsymb + l) * nsc;
+        jb.grid_offset     = ((g * nof_ports + p) * nof_symbols + i) * nsc;
         jb.sample_offset   = static_cast<uint32_t>(pos);
         jb.cp_len          = cp;
         jb.coef_re         = coef[s].real();
@@ -156,7 +168,7 @@ int plan_create(srsgpu_context*           ctx,
     }
   }
   plan->offsets.push_back(pos);
-  if (pos >= (1ull << 32) || static_cast<uint64_t>(nof_grids) * nof_ports * nsymb * nsc >= (1ull << 32)) {
+  if (pos >= (1ull << 32) || static_cast<uint64_t>(nof_grids) * nof_ports * nof_symbols * nsc >= (1ull << 32)) {
     delete plan;
     return fail(SRSGPU_ERR_INVALID_ARG, "batch too large for 32-bit offsets");
   }
@@ -199,6 +211,28 @@ int srsgpu_ofdm_demodulator_plan_create(srsgpu_context*           ctx,
                                         srsgpu_ofdm_plan**        plan)
 {
   return plan_create(ctx, false, cfg, nof_grids, nof_ports, slot_index, plan);
+}
+
+int srsgpu_ofdm_modulator_symbols_plan_create(srsgpu_context*           ctx,
+                                              const srsgpu_ofdm_config* cfg,
+                                              uint32_t                  nof_ports,
+                                              uint32_t                  slot_index,
+                                              uint32_t                  first_symbol,
+                                              uint32_t                  nof_symbols,
+                                              srsgpu_ofdm_plan**        plan)
+{
+  return plan_create(ctx, true, cfg, 1, nof_ports, &slot_index, plan, first_symbol, nof_symbols);
+}
+
+int srsgpu_ofdm_demodulator_symbols_plan_create(srsgpu_context*           ctx,
+                                                const srsgpu_ofdm_config* cfg,
+                                                uint32_t                  nof_ports,
+                                                uint32_t                  slot_index,
+                                                uint32_t                  first_symbol,
+                                                uint32_t                  nof_symbols,
+                                                srsgpu_ofdm_plan**        plan)
+{
+  return plan_create(ctx, false, cfg, 1, nof_ports, &slot_index, plan, first_symbol, nof_symbols);
 }
 
 uint64_t srsgpu_ofdm_plan_nof_samples(const srsgpu_ofdm_plan* plan)

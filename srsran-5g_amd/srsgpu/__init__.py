@@ -384,6 +384,8 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pusch_demodulator_plan_destroy.restype = None
     for name in ("srsgpu_ofdm_modulator_plan_create", "srsgpu_ofdm_demodulator_plan_create"):
         getattr(lib, name).argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, P, ctypes.POINTER(P)]
+    for name in ("srsgpu_ofdm_modulator_symbols_plan_create", "srsgpu_ofdm_demodulator_symbols_plan_create"):
+        getattr(lib, name).argtypes = [P, P] + [ctypes.c_uint32] * 4 + [ctypes.POINTER(P)]
     lib.srsgpu_ofdm_plan_nof_samples.argtypes = [P]
     lib.srsgpu_ofdm_plan_nof_samples.restype = ctypes.c_uint64
     lib.srsgpu_ofdm_plan_sample_offset.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
@@ -413,6 +415,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_pdsch_encoder_plan_stage_times", "srsgpu_pdsch_modulator_plan_create",
     "srsgpu_pdsch_modulator_plan_create_ex", "srsgpu_pdsch_modulator_plan_execute", "srsgpu_pdsch_modulator_plan_destroy",
     "srsgpu_ofdm_modulator_plan_create", "srsgpu_ofdm_demodulator_plan_create", "srsgpu_ofdm_plan_nof_samples",
+    "srsgpu_ofdm_modulator_symbols_plan_create", "srsgpu_ofdm_demodulator_symbols_plan_create",
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
@@ -1385,21 +1388,33 @@ class UlschDemultiplexer:
 class OfdmPlan:
     """srsgpu_ofdm_plan: OFDM slot modulation (inverse=True) or demodulation of nof_grids slots x nof_ports ports.
     Grids: (nof_grids, nof_ports, nsymb, 12 bw_rb) uint32 bf16 pairs; time buffer: nof_samples complex floats (as
-    2 * nof_samples float32), slot of (grid, port) at sample_offset(grid, port)."""
+    2 * nof_samples float32), slot of (grid, port) at sample_offset(grid, port).
+    symbols=(first, count): a symbol-granularity plan of one slot (slot_indices holds one slot index) covering only
+    those symbols (srsgpu_ofdm_*_symbols_plan_create; grid rows [port][symbol - first])."""
 
     def __init__(self, ctx: Context, inverse: bool, numerology: int, bw_rb: int, dft_size: int, scale: float,
                  center_freq_hz: float, slot_indices: Sequence[int], nof_ports: int, cp_extended: bool = False,
-                 window_offset: int = 0):
+                 window_offset: int = 0, symbols=None):
         self.ctx, self.inverse = ctx, inverse
         cfg = OfdmConfig(numerology, bw_rb, dft_size, int(cp_extended), window_offset, scale, center_freq_hz)
-        slots = (ctypes.c_uint32 * max(len(slot_indices), 1))(*slot_indices)
         h = ctypes.c_void_p()
-        f = _lib.srsgpu_ofdm_modulator_plan_create if inverse else _lib.srsgpu_ofdm_demodulator_plan_create
-        _check(f(ctx.handle, ctypes.byref(cfg), len(slot_indices), nof_ports, ctypes.cast(slots, ctypes.c_void_p),
-                 ctypes.byref(h)))
+        if symbols is not None:
+            if len(slot_indices) != 1:
+                raise ValueError("a symbol-granularity plan covers one slot")
+            f = (_lib.srsgpu_ofdm_modulator_symbols_plan_create if inverse
+                 else _lib.srsgpu_ofdm_demodulator_symbols_plan_create)
+            _check(f(ctx.handle, ctypes.byref(cfg), nof_ports, slot_indices[0], symbols[0], symbols[1],
+                     ctypes.byref(h)))
+        else:
+            slots = (ctypes.c_uint32 * max(len(slot_indices), 1))(*slot_indices)
+            f = _lib.srsgpu_ofdm_modulator_plan_create if inverse else _lib.srsgpu_ofdm_demodulator_plan_create
+            _check(f(ctx.handle, ctypes.byref(cfg), len(slot_indices), nof_ports,
+                     ctypes.cast(slots, ctypes.c_void_p), ctypes.byref(h)))
         self.handle = h
         self.nof_grids, self.nof_ports = len(slot_indices), nof_ports
         self.nsymb, self.nsc = (12 if cp_extended else 14), 12 * bw_rb
+        if symbols is not None:
+            self.nsymb = symbols[1]
         self.nof_samples = int(_lib.srsgpu_ofdm_plan_nof_samples(h))
 
     def sample_offset(self, grid: int, port: int) -> int:

@@ -1,0 +1,120 @@
+"""Lower-PHY drop-in (row b5): the objects du_low's radio unit drives per OFDM symbol (lib/ru/generic/lower_phy/
+lower_phy_factory.cpp:70/:84) on the GPU.
+
+The same scripted sequence of upper-PHY requests (handle_request with a resource grid for a slot) and baseband symbols
+(process_symbol) drives (tests/lower_harness.py, oracle/ref/ref_lower.cpp):
+  * the reference's own pdxch_processor_impl / puxch_processor_impl, compiled from its sources, on the reference's OFDM
+    symbol (de)modulator with the generic DFT (the CPU path);
+  * the same reference processors on the GPU symbol objects of integration/ofdm_gpu.cpp (the factories'
+    create_ofdm_symbol_(de)modulator no longer return nullptr);
+  * the GPU PDxCH / PUxCH processors of integration/lower_phy_gpu.cpp (whole-slot modulation at request time;
+    asynchronous per-symbol demodulation with 0 or more symbols in flight).
+Equal across all: process_symbol's return value per symbol, the late-request notifications and (UL) the sequence of
+received-symbol notifications. Samples within 2e-5 x RMS of the reference (tests/test_ofdm_gpu.py's bound), the buffer
+left untouched exactly where the reference leaves it; grid values within one bf16 ulp (or 1e-4 x RMS), and untouched
+REs untouched. The scripts cover requests for every slot, missing requests, empty grids, empty ports, a request
+overwritten by one 16 slots later (late), a request processed 16 slots late, partial slots and a slot left mid-way.
+"""
+import numpy as np
+import pytest
+
+from lower_harness import GPU_PROCESSOR, PROCESS, REF_CPU, REF_ON_GPU_SYMBOLS, REQUEST, SENTINEL, Lower, symbol_size
+from ofdm_oracle import bf16_to_complex
+from pusch_demod_cases import bf16
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = {
+    "100MHz_30kHz_4port": dict(numerology=1, bw_rb=273, dft_size=4096, extended=False, center_freq_hz=3.5e9,
+                               nof_ports=4, window_offset=0.5),
+    "10MHz_15kHz_2port": dict(numerology=0, bw_rb=52, dft_size=1024, extended=False, center_freq_hz=1.8e9,
+                              nof_ports=2, window_offset=0.0),
+    "60kHz_extended_cp": dict(numerology=2, bw_rb=24, dft_size=512, extended=True, center_freq_hz=3.0e9,
+                              nof_ports=1, window_offset=0.25),
+}
+
+
+@pytest.fixture(scope="module")
+def lower():
+    return Lower()
+
+
+def dl_script(nsymb):
+    """Requests and symbols: (kind, system slot, a, b)."""
+    B = 40  # first system slot (any)
+    ev = [(REQUEST, B + 3, 0, 0), (REQUEST, B + 4, 1, 0), (REQUEST, B + 5, 2, 0), (REQUEST, B + 6, 3, 0),
+          (REQUEST, B + 6 + 16, 4, 0),   # overwrites slot B+6's entry: late B+6
+          (REQUEST, B + 9, 5, 0)]
+    ev += [(PROCESS, B + s, 0, nsymb) for s in (2, 3, 4, 5, 6)]  # B+2: no request; B+5: empty grid; B+6: late B+22
+    ev += [(REQUEST, B + 7, 6, 0), (PROCESS, B + 7, 0, 5),      # a partial slot
+           (REQUEST, B + 8, 7, 0), (PROCESS, B + 8, 3, nsymb),  # a slot entered mid-way
+           (PROCESS, B + 9 + 16, 0, 2)]                         # slot B+9's request found 16 slots late
+    return ev
+
+
+def dl_grids(rng, cfg, nsymb, n=8):
+    P, nsc = cfg["nof_ports"], 12 * cfg["bw_rb"]
+    x = (rng.normal(size=(n, P, nsymb, nsc)) + 1j * rng.normal(size=(n, P, nsymb, nsc))) * 0.25
+    mask = np.full(n, (1 << P) - 1, np.uint32)
+    mask[1] = 0b0101 & ((1 << P) - 1) if P > 1 else 1  # empty ports
+    mask[2] = 0                                        # an empty grid: nothing to transmit
+    return bf16(x), mask
+
+
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_pdxch_processor_gpu_equals_reference(lower, name):
+    cfg = CONFIGS[name]
+    nsymb = 12 if cfg["extended"] else 14
+    grids, mask = dl_grids(np.random.default_rng(7), cfg, nsymb)
+    ev = dl_script(nsymb)
+    ref, ref_flags, ref_late = lower.pdxch(REF_CPU, cfg, grids, mask, ev)
+    assert ref_flags.any() and not ref_flags.all() and ref_late, "the script exercises every branch"
+    touched = ref.real != SENTINEL
+    rms = np.sqrt(np.mean(np.abs(ref[touched]) ** 2))
+    for variant in (REF_ON_GPU_SYMBOLS, GPU_PROCESSOR):
+        got, flags, late = lower.pdxch(variant, cfg, grids, mask, ev)
+        assert np.array_equal(flags, ref_flags), variant
+        assert late == ref_late, variant
+        assert got.shape == ref.shape
+        assert np.array_equal(got.real == SENTINEL, ~touched), variant  # same buffers left untouched
+        err = np.max(np.abs(got[touched] - ref[touched]))
+        assert err < 2e-5 * rms, (variant, err / rms)
+
+
+def ul_script(nsymb):
+    B = 100
+    return [(REQUEST, B + 3, 0, 0), (PROCESS, B + 2, 0, nsymb), (PROCESS, B + 3, 0, nsymb),
+            (REQUEST, B + 4, 1, 0), (PROCESS, B + 4, 0, 7),          # a slot left mid-way
+            (PROCESS, B + 5, 0, nsymb),                              # no request
+            (REQUEST, B + 6, 2, 0), (REQUEST, B + 6 + 16, 3, 0),     # overwritten: late B+6
+            (PROCESS, B + 6, 0, nsymb),                              # finds B+22: late B+22
+            (REQUEST, B + 7, 4, 0), (PROCESS, B + 7, 2, nsymb),      # entered mid-way
+            (REQUEST, B + 8, 5, 0), (PROCESS, B + 8, 0, nsymb)]
+
+
+def ul_samples(rng, cfg, ev):
+    n = sum(cfg["nof_ports"] * symbol_size(cfg["numerology"], cfg["dft_size"], cfg["extended"], e[1], l)
+            for e in ev if e[0] == PROCESS for l in range(e[2], e[3]))
+    return ((rng.normal(size=n) + 1j * rng.normal(size=n)) * 0.05).astype(np.complex64)
+
+
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_puxch_processor_gpu_equals_reference(lower, name):
+    cfg = CONFIGS[name]
+    nsymb = 12 if cfg["extended"] else 14
+    ev = ul_script(nsymb)
+    x = ul_samples(np.random.default_rng(11), cfg, ev)
+    ref, ref_flags, ref_rx, ref_late = lower.puxch(REF_CPU, cfg, 6, ev, x)
+    assert ref_flags.any() and not ref_flags.all() and ref_late and ref_rx
+    va = bf16_to_complex(ref)
+    rms = np.sqrt(np.mean(np.abs(va[va != 0]) ** 2))
+    for variant, in_flight in ((REF_ON_GPU_SYMBOLS, 0), (GPU_PROCESSOR, 0), (GPU_PROCESSOR, 3)):
+        got, flags, rx, late = lower.puxch(variant, cfg, 6, ev, x, max_in_flight=in_flight)
+        what = (variant, in_flight)
+        assert np.array_equal(flags, ref_flags), what
+        assert rx == ref_rx, what
+        assert late == ref_late, what
+        vb = bf16_to_complex(got)
+        assert np.array_equal(va == 0, vb == 0), what  # the same REs written
+        err = np.abs(va - vb)
+        assert np.all(err <= np.maximum(2.0 ** -7 * np.abs(va), 1e-4 * rms)), (what, float(np.max(err / rms)))

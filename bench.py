@@ -218,6 +218,7 @@ class InputSet:
         self.graph = None
         self.graph_back = None  # UE-sharded cell: the part after the grid exchange
         self.graph_ul = None    # --leg-graphs: the UL leg's own graph (self.graph then holds the DL leg)
+        self.tb_gather = None   # srsgpu.dist.TbGather of this set (ranks > 1)
 
 
 def parse_args(argv=None):
@@ -261,9 +262,12 @@ def parse_args(argv=None):
     # graphs give 132.9k-135.0k).
     ap.add_argument("--leg-graphs", action=argparse.BooleanOptionalAction, default=True,
                     help="capture the DL and UL legs of a step as two graphs replayed on two streams per input set")
-    ap.add_argument("--graph-collectives", action="store_true",
-                    help="N > 1: capture the RCCL exchanges (TB gather; grid exchange with --shard ues) inside the "
-                         "step's graph instead of issuing them between graph launches")
+    ap.add_argument("--graph-collectives", action=argparse.BooleanOptionalAction, default=True,
+                    help="capture the RCCL exchanges (TB gather; grid exchange with --shard ues) inside the step's "
+                         "graphs (default) instead of issuing them between graph launches")
+    ap.add_argument("--tb-gather", choices=["auto", "always", "never"], default="auto",
+                    help="the per-step TB gather to the FAPI rank: with more than one rank (auto), also at world size "
+                         "1 under torchrun (always: exercises RCCL graph capture on one GPU), or never")
     return ap.parse_args(argv)
 
 
@@ -351,10 +355,14 @@ def measure(args, env):
     fill_samples(args.snr_db, args.worst_case)
     dl_stream = torch.cuda.Stream(dev)
     ul_stream = dl_stream if args.serial_legs else torch.cuda.Stream(dev)
-    tb_gather = None
-    if world > 1:
+    # The decoded TBs + CRC flags of every rank go to the FAPI rank once per step (srsgpu.dist.TbGather). One gather
+    # per input set: each set's step runs on its own streams, so sets must not share send / receive buffers.
+    use_gather = dist.is_available() and dist.is_initialized() and (world > 1 or args.tb_gather == "always")
+    if use_gather and args.tb_gather != "never":
         from srsgpu import dist as sdist
-        tb_gather = sdist.TbGather(sets[0].ul.d_tbs.numel(), sets[0].ul.d_tb_ok.numel(), dev, root=0)
+        for st in sets:
+            st.tb_gather = sdist.TbGather(st.ul.d_tbs.numel(), st.ul.d_tb_ok.numel(), dev, root=0)
+    tb_gather = sets[0].tb_gather
 
     def pipeline(st, ev_dl=None, ev_ul=None, part="all"):
         """DL and UL legs of one step of input set `st`, forked from and joined back into the current stream. A
@@ -393,7 +401,7 @@ def measure(args, env):
     # set's front end (different buffers; a set's consecutive steps stay ordered on its stream).
     set_streams = [torch.cuda.Stream(dev) for _ in range(K)] if args.pipeline else None
     # --leg-graphs: the DL and UL legs of a set as two graphs replayed on two streams of their own.
-    leg_graphs = args.leg_graphs and args.graph and not shard_x and not args.graph_collectives
+    leg_graphs = args.leg_graphs and args.graph and not shard_x
     ul_set_streams = [torch.cuda.Stream(dev) for _ in range(K)] if leg_graphs and args.pipeline else None
 
     def step(i):
@@ -405,8 +413,8 @@ def measure(args, env):
                 st.graph.replay()
             with torch.cuda.stream(cur_ul):
                 st.graph_ul.replay()
-                if tb_gather is not None:
-                    tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
+                if st.tb_gather is not None and not args.graph_collectives:
+                    st.tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
             return
         with torch.cuda.stream(cur):
             if st.graph is not None and st.graph_back is not None:
@@ -417,8 +425,8 @@ def measure(args, env):
                 st.graph.replay()
             else:
                 whole(st)
-            if tb_gather is not None and not (st.graph is not None and args.graph_collectives):
-                tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
+            if st.tb_gather is not None and not (st.graph is not None and args.graph_collectives):
+                st.tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
 
     # Every input set runs at least once before timing (its buffers, plans and code first touched), whatever --warmup.
     n_warm = max(args.warmup, K)
@@ -450,6 +458,9 @@ def measure(args, env):
                 st.graph_ul = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(st.graph_ul, capture_error_mode="thread_local"):
                     st.ul.execute(st.samples, torch.cuda.current_stream(dev))
+                    if st.tb_gather is not None and args.graph_collectives:
+                        # RCCL graph capture: the gather replays with the UL leg, on its stream.
+                        st.tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
             elif shard_x and not args.graph_collectives:
                 # The collectives stay outside: the front and back parts are captured as two graphs.
                 with torch.cuda.graph(st.graph, capture_error_mode="thread_local"):
@@ -462,8 +473,8 @@ def measure(args, env):
                 # capture); otherwise there are no collectives in the step's kernels.
                 with torch.cuda.graph(st.graph, capture_error_mode="thread_local"):
                     whole(st)
-                    if tb_gather is not None and args.graph_collectives:
-                        tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
+                    if st.tb_gather is not None and args.graph_collectives:
+                        st.tb_gather.gather(st.ul.d_tbs, st.ul.d_tb_ok)
         for i in range(n_warm):
             step(i)
         torch.cuda.synchronize()
@@ -765,7 +776,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    if world > 1 or (args.tb_gather == "always" and "MASTER_ADDR" in os.environ):
         dist.init_process_group("nccl", device_id=dev)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
@@ -787,7 +798,7 @@ def main():
             result["workloads"][name] = summary(measure(a, env))
     if rank == 0:
         print(json.dumps(result))
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

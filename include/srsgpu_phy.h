@@ -756,6 +756,28 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
 
 void srsgpu_pusch_decoder_plan_destroy(srsgpu_pusch_decoder_plan* plan);
 
+/** HARQ soft buffers kept across slots in a persistent arena, one slot of arena_stride bytes per absolute codeblock
+ *  identifier (the reference's rx buffer pool: rx_buffer.h:65 get_absolute_codeblock_id, :72 get_codeblock_soft_bits),
+ *  moved to / from a slot batch's contiguous HARQ buffer (srsgpu_pusch_tb_config::harq_offset layout) around a
+ *  srsgpu_pusch_decoder_plan_execute. d_jobs: device array of nof_jobs entries. Asynchronous on `stream`. */
+#define SRSGPU_HARQ_TO_BATCH 0
+#define SRSGPU_HARQ_TO_ARENA 1
+typedef struct {
+  uint32_t slot;         /* arena slot (absolute codeblock identifier) */
+  uint32_t batch_offset; /* first byte of the codeblock's soft bits in the batch HARQ buffer */
+  uint32_t bytes;        /* soft bits to move (N of the codeblock) */
+  uint32_t reserved;
+} srsgpu_harq_copy_job;
+
+int srsgpu_harq_copy(srsgpu_context*             ctx,
+                     int                         direction,
+                     int8_t*                     d_arena,
+                     uint32_t                    arena_stride,
+                     int8_t*                     d_batch,
+                     const srsgpu_harq_copy_job* d_jobs,
+                     uint32_t                    nof_jobs,
+                     void*                       stream);
+
 /** Stage timing: with enable = 1 every execute records HIP events on its stream around the three kernel stages
  *  (0: rate dematching, 1: LDPC decoding, 2: TB assembly + CRC); with enable = 2 only around the decoding stage (two
  *  events: the least perturbation of a timed run); 0 disables. stage_times synchronises on them and returns the

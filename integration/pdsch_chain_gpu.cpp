@@ -13,6 +13,7 @@
 // OFDM modulator checks, ofdm_modulator_impl.cpp:77).
 #include "signal_chain_gpu.h"
 
+#include "chain_convert.h"
 #include "gpu_staging.h"
 #include "srsran/phy/support/resource_grid_writer.h"
 
@@ -23,60 +24,7 @@ namespace srsran {
 
 namespace {
 
-constexpr uint32_t SENTINEL = 0xffffffffu;
-
-/// Copies the non-sentinel REs of scratch rows [port][14][nsc] (symbols [l0, l0 + nsym) of ports 0..P-1) into the
-/// grid; a port that received any RE is marked non-empty.
-void store_written_res(resource_grid_writer& grid, const uint32_t* scratch, unsigned P, unsigned nsc, unsigned l0,
-                       unsigned nsym)
-{
-  for (unsigned p = 0; p != P; ++p) {
-    int      first_k = -1;
-    unsigned first_l = 0;
-    cbf16_t  first_v;
-    for (unsigned l = l0; l != l0 + nsym; ++l) {
-      const uint32_t* src = scratch + (static_cast<size_t>(p) * 14 + l) * nsc;
-      span<cbf16_t>   dst = grid.get_view(p, l);
-      for (unsigned k = 0; k != nsc; ++k) {
-        if (src[k] != SENTINEL) {
-          std::memcpy(&dst[k], &src[k], sizeof(uint32_t));
-          if (first_k < 0) {
-            first_k = static_cast<int>(k);
-            first_l = l;
-            first_v = dst[k];
-          }
-        }
-      }
-    }
-    if (first_k >= 0) {
-      // Rewrites one RE with its own value: resource_grid_writer_impl clears the port's empty flag on put().
-      grid.put(p, first_l, static_cast<unsigned>(first_k), 1, span<const cbf16_t>(&first_v, 1));
-    }
-  }
-}
-
-/// Grid CRB mask (one byte per CRB) of a crb_bitmap.
-std::vector<uint8_t> crb_bytes(const crb_bitmap& m, unsigned grid_prb)
-{
-  std::vector<uint8_t> out(grid_prb, 0);
-  for (unsigned rb = 0; rb != std::min<unsigned>(grid_prb, m.size()); ++rb) {
-    out[rb] = m.test(rb) ? 1 : 0;
-  }
-  return out;
-}
-
-/// Wideband precoding weights [port][layer] of PRG 0.
-void wideband_weights(const precoding_configuration& pc, float (&w)[4][4][2])
-{
-  std::memset(w, 0, sizeof(w));
-  for (unsigned p = 0; p != pc.get_nof_ports(); ++p) {
-    for (unsigned ly = 0; ly != pc.get_nof_layers(); ++ly) {
-      const cf_t c = pc.get_coefficient(ly, p, 0);
-      w[p][ly][0]  = c.real();
-      w[p][ly][1]  = c.imag();
-    }
-  }
-}
+using gpu::store_written_res;
 
 // --------------------------------------------------------------------------------------------------------------------
 // PDSCH modulator
@@ -100,97 +48,22 @@ public:
   void modulate(resource_grid_writer& grid, span<const bit_buffer> codewords, const config_t& config) override
   {
     gpu::device_scope dev_scope(ctx, WHO);
-    const precoding_configuration& pc = config.precoding;
-    const unsigned                 L  = pc.get_nof_layers();
-    const unsigned                 P  = pc.get_nof_ports();
-    if (codewords.size() != 1 || L == 0 || L > 4 || P < L || P > 4 || P > grid.get_nof_ports()) {
+    if (codewords.size() != 1) {
       throw std::invalid_argument(std::string(WHO) + ": one codeword, 1..4 layers on 1..4 ports");
     }
-    const unsigned       nsc      = grid.get_nof_subc();
-    const unsigned       grid_prb = nsc / NRE;
-    const crb_bitmap     crbs     = config.freq_allocation.get_crb_mask(config.bwp_start_rb, config.bwp_size_rb);
-    std::vector<uint8_t> crb_mask = crb_bytes(crbs, grid_prb);
-
-    srsgpu_pdsch_mod_config c;
-    std::memset(&c, 0, sizeof(c));
-    c.rnti                        = config.rnti;
-    c.n_id                        = static_cast<uint16_t>(config.n_id);
-    c.modulation_order            = static_cast<uint8_t>(get_bits_per_symbol(config.modulation1));
-    c.nof_layers                  = static_cast<uint8_t>(L);
-    c.nof_ports                   = static_cast<uint8_t>(P);
-    c.start_symbol                = static_cast<uint8_t>(config.start_symbol_index);
-    c.nof_symbols                 = static_cast<uint8_t>(config.nof_symbols);
-    c.dmrs_type                   = (config.dmrs_config_type == dmrs_type::TYPE1) ? 1 : 2;
-    c.nof_cdm_groups_without_data = static_cast<uint8_t>(config.nof_cdm_groups_without_data);
-    for (unsigned l = 0; l != 14; ++l) {
-      c.dmrs_symbol_mask |= config.dmrs_symb_pos.test(l) ? (1u << l) : 0u;
-    }
-    c.bwp_start_rb = static_cast<uint16_t>(config.bwp_start_rb);
-    c.bwp_size_rb  = static_cast<uint16_t>(config.bwp_size_rb);
-    c.rb_start     = static_cast<uint16_t>(std::max(crbs.find_lowest(), 0));
-    c.nof_rb       = static_cast<uint16_t>(crbs.count());
-    c.scaling      = config.scaling;
-    wideband_weights(pc, c.precoding);
-    c.cw_offset  = 0;
-    c.nof_bits   = codewords[0].size();
-    c.grid_index = 0;
-
-    // Reserved patterns and per-PRG weights (srsgpu_alloc_ext).
-    std::vector<std::vector<uint8_t>> res_crbs;
-    std::vector<srsgpu_re_pattern>    res;
-    for (const re_pattern& r : config.reserved.get_re_patterns()) {
-      res_crbs.push_back(crb_bytes(r.crb_mask, grid_prb));
-      srsgpu_re_pattern x;
-      std::memset(&x, 0, sizeof(x));
-      for (unsigned k = 0; k != NRE; ++k) {
-        x.re_mask |= r.re_mask.test(k) ? (1u << k) : 0u;
-      }
-      for (unsigned l = 0; l != 14; ++l) {
-        x.symbol_mask |= r.symbols.test(l) ? (1u << l) : 0u;
-      }
-      res.push_back(x);
-    }
-    for (size_t i = 0; i != res.size(); ++i) {
-      res[i].crb_mask = res_crbs[i].data();
-    }
-    std::vector<float> prg_w;
-    if (pc.get_nof_prg() > 1) {
-      for (unsigned g = 0; g != pc.get_nof_prg(); ++g) {
-        for (unsigned p = 0; p != P; ++p) {
-          for (unsigned ly = 0; ly != L; ++ly) {
-            const cf_t w = pc.get_coefficient(ly, p, g);
-            prg_w.push_back(w.real());
-            prg_w.push_back(w.imag());
-          }
-        }
-      }
-    }
+    const unsigned      nsc      = grid.get_nof_subc();
+    const unsigned      grid_prb = nsc / NRE;
+    gpu::pdsch_mod_desc d =
+        gpu::make_pdsch_mod_desc(config, codewords[0].size(), grid_prb, grid.get_nof_ports(), WHO);
+    const unsigned P = d.c.nof_ports;
 
     std::vector<uint8_t> key;
-    gpu::key_append(key, c);
+    d.append_key(key);
     gpu::key_append(key, grid_prb);
-    key.insert(key.end(), crb_mask.begin(), crb_mask.end());
-    for (size_t i = 0; i != res.size(); ++i) {
-      gpu::key_append(key, res[i].re_mask);
-      gpu::key_append(key, res[i].symbol_mask);
-      key.insert(key.end(), res_crbs[i].begin(), res_crbs[i].end());
-    }
-    gpu::key_append(key, pc.get_prg_size());
-    const auto* pw = reinterpret_cast<const uint8_t*>(prg_w.data());
-    key.insert(key.end(), pw, pw + prg_w.size() * sizeof(float));
     srsgpu_pdsch_modulator_plan* plan = plans.get(key, [&] {
-      srsgpu_alloc_ext ext;
-      std::memset(&ext, 0, sizeof(ext));
-      ext.crb_mask     = crb_mask.data();
-      ext.reserved     = res.empty() ? nullptr : res.data();
-      ext.nof_reserved = static_cast<uint32_t>(res.size());
-      if (!prg_w.empty()) {
-        ext.prg_size    = static_cast<uint16_t>(pc.get_prg_size());
-        ext.nof_prg     = static_cast<uint16_t>(pc.get_nof_prg());
-        ext.prg_weights = prg_w.data();
-      }
-      srsgpu_pdsch_modulator_plan* p = nullptr;
-      gpu::srsgpu_check(srsgpu_pdsch_modulator_plan_create_ex(ctx, &c, &ext, 1, grid_prb, P, &p), WHO);
+      const srsgpu_alloc_ext       ext = d.ext();
+      srsgpu_pdsch_modulator_plan* p   = nullptr;
+      gpu::srsgpu_check(srsgpu_pdsch_modulator_plan_create_ex(ctx, &d.c, &ext, 1, grid_prb, P, &p), WHO);
       return p;
     });
 
@@ -254,42 +127,17 @@ public:
   void map(resource_grid_writer& grid, const config_t& config) override
   {
     gpu::device_scope dev_scope(ctx, WHO);
-    const precoding_configuration& pc = config.precoding;
-    const unsigned                 L  = pc.get_nof_layers();
-    const unsigned                 P  = pc.get_nof_ports();
-    if (L == 0 || L > 4 || P < L || P > 4 || P > grid.get_nof_ports()) {
-      throw std::invalid_argument(std::string(WHO) + ": 1..4 layers on 1..4 ports");
-    }
-    const unsigned       nsc      = grid.get_nof_subc();
-    const unsigned       grid_prb = nsc / NRE;
-    std::vector<uint8_t> crb_mask = crb_bytes(config.rb_mask, grid_prb);
-
-    srsgpu_pdsch_dmrs_config c;
-    std::memset(&c, 0, sizeof(c));
-    c.slot_index    = static_cast<uint16_t>(config.slot.slot_index());
-    c.scrambling_id = static_cast<uint16_t>(config.scrambling_id);
-    c.n_scid        = config.n_scid ? 1 : 0;
-    c.dmrs_type     = (config.type == dmrs_type::TYPE1) ? 1 : 2;
-    c.nof_layers    = static_cast<uint8_t>(L);
-    c.nof_ports     = static_cast<uint8_t>(P);
-    for (unsigned l = 0; l != 14; ++l) {
-      c.dmrs_symbol_mask |= config.symbols_mask.test(l) ? (1u << l) : 0u;
-    }
-    c.reference_point_k_rb = static_cast<uint16_t>(config.reference_point_k_rb);
-    c.rb_start             = static_cast<uint16_t>(std::max(config.rb_mask.find_lowest(), 0));
-    c.nof_rb               = static_cast<uint16_t>(config.rb_mask.count());
-    c.amplitude            = config.amplitude;
-    wideband_weights(pc, c.precoding);
-    c.grid_index = 0;
+    const unsigned             nsc      = grid.get_nof_subc();
+    const unsigned             grid_prb = nsc / NRE;
+    const gpu::pdsch_dmrs_desc d        = gpu::make_pdsch_dmrs_desc(config, grid_prb, grid.get_nof_ports(), WHO);
+    const srsgpu_pdsch_dmrs_config& c   = d.c;
+    const unsigned                  P   = c.nof_ports;
 
     std::vector<uint8_t> key;
-    gpu::key_append(key, c);
+    d.append_key(key);
     gpu::key_append(key, grid_prb);
-    key.insert(key.end(), crb_mask.begin(), crb_mask.end());
     srsgpu_pdsch_dmrs_plan* plan = plans.get(key, [&] {
-      srsgpu_alloc_ext ext;
-      std::memset(&ext, 0, sizeof(ext));
-      ext.crb_mask                = crb_mask.data();
+      const srsgpu_alloc_ext  ext = d.ext();
       srsgpu_pdsch_dmrs_plan* p   = nullptr;
       gpu::srsgpu_check(srsgpu_pdsch_dmrs_plan_create_ex(ctx, &c, &ext, 1, grid_prb, P, &p), WHO);
       return p;

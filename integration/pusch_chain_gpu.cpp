@@ -16,6 +16,7 @@
 // (pusch_demodulator_impl.cpp:272-443).
 #include "signal_chain_gpu.h"
 
+#include "chain_convert.h"
 #include "gpu_staging.h"
 #include "srsran/phy/support/resource_grid_reader.h"
 #include "srsran/phy/upper/channel_processors/pusch/pusch_codeword_buffer.h"
@@ -31,43 +32,7 @@ namespace srsran {
 
 namespace {
 
-/// CRB allocation of an rb_mask restricted to a grid of grid_prb PRBs: first CRB, count, and the one-byte-per-CRB mask
-/// when it is not contiguous (empty otherwise).
-struct crb_alloc {
-  unsigned             rb_start = 0;
-  unsigned             nof_rb   = 0;
-  unsigned             span_end = 0;  ///< Last allocated CRB + 1.
-  std::vector<uint8_t> mask;
-};
-
-crb_alloc make_crb_alloc(const crb_bitmap& rb_mask, unsigned grid_prb, const char* who)
-{
-  crb_alloc a;
-  const int lo = rb_mask.find_lowest();
-  const int hi = rb_mask.find_highest();
-  if (lo < 0 || hi < lo || static_cast<unsigned>(hi) >= grid_prb) {
-    throw std::invalid_argument(std::string(who) + ": RB mask empty or beyond the resource grid");
-  }
-  a.rb_start = static_cast<unsigned>(lo);
-  a.nof_rb   = static_cast<unsigned>(rb_mask.count());
-  a.span_end = static_cast<unsigned>(hi) + 1;
-  if (a.span_end - a.rb_start != a.nof_rb) {
-    a.mask.assign(grid_prb, 0);
-    for (unsigned rb = a.rb_start; rb != a.span_end; ++rb) {
-      a.mask[rb] = rb_mask.test(rb) ? 1 : 0;
-    }
-  }
-  return a;
-}
-
-uint16_t symbol_mask_bits(const bounded_bitset<MAX_NSYMB_PER_SLOT>& m)
-{
-  uint16_t bits = 0;
-  for (unsigned l = 0; l != std::min<unsigned>(m.size(), 14); ++l) {
-    bits |= m.test(l) ? (1u << l) : 0u;
-  }
-  return bits;
-}
+using gpu::crb_alloc;
 
 // --------------------------------------------------------------------------------------------------------------------
 // DM-RS PUSCH channel estimator
@@ -93,53 +58,20 @@ public:
   void estimate(channel_estimate& estimate, const resource_grid_reader& grid, const configuration& config) override
   {
     gpu::device_scope dev_scope(ctx, WHO);
-    const unsigned P = config.rx_ports.size();
-    const unsigned L = config.get_nof_tx_layers();
-    if (P == 0 || P > 4 || L == 0 || L > 4 || config.c_prefix != cyclic_prefix::NORMAL) {
-      throw std::invalid_argument(std::string(WHO) + ": 1..4 rx ports and layers and a normal cyclic prefix");
-    }
-    const unsigned nsc      = grid.get_nof_subc();
-    const unsigned grid_prb = nsc / NRE;
-    const crb_alloc a       = make_crb_alloc(config.rb_mask, grid_prb, WHO);
-
-    srsgpu_pusch_chest_config c;
-    std::memset(&c, 0, sizeof(c));
-    if (std::holds_alternative<low_papr_sequence_configuration>(config.sequence_config)) {
-      c.dmrs_sequence = SRSGPU_DMRS_LOW_PAPR;
-      c.scrambling_id = static_cast<uint16_t>(std::get<low_papr_sequence_configuration>(config.sequence_config).n_rs_id);
-      c.dmrs_type     = 1;
-    } else {
-      const auto& s   = std::get<pseudo_random_sequence_configuration>(config.sequence_config);
-      c.dmrs_sequence = SRSGPU_DMRS_PSEUDO_RANDOM;
-      c.scrambling_id = static_cast<uint16_t>(s.scrambling_id);
-      c.n_scid        = s.n_scid ? 1 : 0;
-      c.dmrs_type     = (s.type == dmrs_type::TYPE1) ? 1 : 2;
-    }
-    c.nof_tx_layers    = static_cast<uint8_t>(L);
-    c.nof_rx_ports     = static_cast<uint8_t>(P);
-    c.start_symbol     = static_cast<uint8_t>(config.first_symbol);
-    c.nof_symbols      = static_cast<uint8_t>(config.nof_symbols);
-    c.dmrs_symbol_mask = symbol_mask_bits(config.symbols_mask);
-    c.rb_start         = static_cast<uint16_t>(a.rb_start);
-    c.nof_rb           = static_cast<uint16_t>(a.nof_rb);
-    c.slot_index       = static_cast<uint16_t>(config.slot.slot_index());
-    c.numerology       = static_cast<uint8_t>(config.slot.numerology());
-    c.fd_smoothing     = opts.fd_smoothing;
-    c.td_strategy      = opts.td_strategy;
-    c.compensate_cfo   = opts.compensate_cfo ? 1 : 0;
-    c.estimate_layout  = SRSGPU_CE_PER_SYMBOL;
-    c.scaling          = config.scaling;
-    c.grid_index       = 0;
+    const unsigned              nsc      = grid.get_nof_subc();
+    const unsigned              grid_prb = nsc / NRE;
+    const gpu::pusch_chest_desc d        = gpu::make_pusch_chest_desc(config, grid_prb, opts, SRSGPU_CE_PER_SYMBOL, WHO);
+    const srsgpu_pusch_chest_config& c   = d.c;
+    const crb_alloc&                 a   = d.alloc;
+    const unsigned                   P   = d.nof_ports;
+    const unsigned                   L   = d.nof_layers;
 
     std::vector<uint8_t> key;
-    gpu::key_append(key, c);
+    d.append_key(key);
     gpu::key_append(key, grid_prb);
-    key.insert(key.end(), a.mask.begin(), a.mask.end());
     srsgpu_pusch_chest_plan* plan = plans.get(key, [&] {
-      srsgpu_alloc_ext ext;
-      std::memset(&ext, 0, sizeof(ext));
-      ext.crb_mask                  = a.mask.empty() ? nullptr : a.mask.data();
-      srsgpu_pusch_chest_plan* p    = nullptr;
+      const srsgpu_alloc_ext   ext = d.ext();
+      srsgpu_pusch_chest_plan* p   = nullptr;
       gpu::srsgpu_check(srsgpu_pusch_chest_plan_create_ex(ctx, &c, &ext, 1, grid_prb, P, &p), WHO);
       return p;
     });
@@ -197,17 +129,7 @@ public:
         }
       }
     }
-    for (unsigned p = 0; p != P; ++p) {
-      const float* mp = m + SRSGPU_CHEST_METRICS * p;
-      estimate.set_noise_variance(nv[p], p);
-      estimate.set_epre(mp[1], p);
-      estimate.set_snr(mp[3], p);
-      for (unsigned ly = 0; ly != L; ++ly) {
-        estimate.set_rsrp(mp[0], p, ly);
-        estimate.set_time_alignment(phy_time_unit::from_seconds(mp[4]), p, ly);
-        estimate.set_cfo_Hz(std::isnan(mp[5]) ? std::optional<float>() : std::optional<float>(mp[5]), p, ly);
-      }
-    }
+    gpu::write_chest_metrics(estimate, nv, m, P, L);
   }
 
 private:
@@ -266,43 +188,20 @@ public:
                   const configuration&        config) override
   {
     gpu::device_scope dev_scope(ctx, WHO);
-    const unsigned P  = config.rx_ports.size();
-    const unsigned L  = config.nof_tx_layers;
-    const unsigned Qm = get_bits_per_symbol(config.modulation);
-    if (P == 0 || P > 4 || L == 0 || L > 4) {
-      throw std::invalid_argument(std::string(WHO) + ": 1..4 rx ports and layers");
-    }
-    const unsigned  nsc      = grid.get_nof_subc();
-    const unsigned  grid_prb = nsc / NRE;
-    const crb_alloc a        = make_crb_alloc(config.rb_mask, grid_prb, WHO);
-
-    srsgpu_pusch_demod_config c;
-    std::memset(&c, 0, sizeof(c));
-    c.rnti                        = config.rnti;
-    c.n_id                        = static_cast<uint16_t>(config.n_id);
-    c.modulation_order            = static_cast<uint8_t>(Qm);
-    c.nof_tx_layers               = static_cast<uint8_t>(L);
-    c.nof_rx_ports                = static_cast<uint8_t>(P);
-    c.start_symbol                = static_cast<uint8_t>(config.start_symbol_index);
-    c.nof_symbols                 = static_cast<uint8_t>(config.nof_symbols);
-    c.dmrs_type                   = (config.dmrs_config_type == dmrs_type::TYPE1) ? 1 : 2;
-    c.nof_cdm_groups_without_data = static_cast<uint8_t>(config.nof_cdm_groups_without_data);
-    c.equalizer                   = opts.equalizer;
-    c.dmrs_symbol_mask            = symbol_mask_bits(config.dmrs_symb_pos);
-    c.rb_start                    = static_cast<uint16_t>(a.rb_start);
-    c.nof_rb                      = static_cast<uint16_t>(a.nof_rb);
-    c.estimate_layout             = SRSGPU_CE_PER_SYMBOL;
-    c.transform_precoding         = config.enable_transform_precoding ? 1 : 0;
+    const unsigned              nsc      = grid.get_nof_subc();
+    const unsigned              grid_prb = nsc / NRE;
+    const gpu::pusch_demod_desc d        = gpu::make_pusch_demod_desc(config, grid_prb, opts, SRSGPU_CE_PER_SYMBOL, WHO);
+    const srsgpu_pusch_demod_config& c   = d.c;
+    const crb_alloc&                 a   = d.alloc;
+    const unsigned                   P   = d.nof_ports;
+    const unsigned                   L   = d.nof_layers;
 
     std::vector<uint8_t> key;
-    gpu::key_append(key, c);
+    d.append_key(key);
     gpu::key_append(key, grid_prb);
-    key.insert(key.end(), a.mask.begin(), a.mask.end());
     srsgpu_pusch_demodulator_plan* plan = plans.get(key, [&] {
-      srsgpu_alloc_ext ext;
-      std::memset(&ext, 0, sizeof(ext));
-      ext.crb_mask                     = a.mask.empty() ? nullptr : a.mask.data();
-      srsgpu_pusch_demodulator_plan* p = nullptr;
+      const srsgpu_alloc_ext         ext = d.ext();
+      srsgpu_pusch_demodulator_plan* p   = nullptr;
       gpu::srsgpu_check(srsgpu_pusch_demodulator_plan_create_ex(ctx, &c, &ext, 1, grid_prb, P, &p), WHO);
       return p;
     });
@@ -357,64 +256,12 @@ public:
     out_buf.download(0, seq_off + seq_words * 4, s);
     gpu::hip_check(hipStreamSynchronize(s), WHO, "synchronise");
 
-    // The sequence words (bit 31 of word w = c(32 w)) as an MSB-first byte stream (srsran::bit_buffer packing).
-    seq_bytes.resize(seq_words * 4);
-    const uint32_t* words = out_buf.host<uint32_t>(seq_off);
-    for (size_t w = 0; w != seq_words; ++w) {
-      seq_bytes[4 * w]     = static_cast<uint8_t>(words[w] >> 24);
-      seq_bytes[4 * w + 1] = static_cast<uint8_t>(words[w] >> 16);
-      seq_bytes[4 * w + 2] = static_cast<uint8_t>(words[w] >> 8);
-      seq_bytes[4 * w + 3] = static_cast<uint8_t>(words[w]);
-    }
-    const bit_buffer seq = bit_buffer::from_bytes(span<uint8_t>(seq_bytes)).first(nof_llrs);
-
-    // Blocks in the reference's order: per OFDM symbol with data, the codeword buffer's block views, the symbol's
-    // provisional statistics before its last block, the end statistics after the last symbol.
-    const int8_t*  llrs            = out_buf.host<int8_t>();
-    const float*   st              = out_buf.host<float>(stats_off);
-    const unsigned nof_bits_per_re = L * Qm;
-    const unsigned dmrs_re_per_prb =
-        config.nof_cdm_groups_without_data * (config.dmrs_config_type == dmrs_type::TYPE1 ? 6 : 4);
-    unsigned pos = 0;
-    for (unsigned l = l0; l != l0 + nsym; ++l) {
-      const unsigned nof_re_symbol = a.nof_rb * (config.dmrs_symb_pos.test(l) ? NRE - dmrs_re_per_prb : NRE);
-      if (nof_re_symbol == 0) {
-        continue;
-      }
-      unsigned count = 0;
-      while (count != nof_re_symbol) {
-        span<log_likelihood_ratio> block = codeword_buffer.get_next_block_view((nof_re_symbol - count) * nof_bits_per_re);
-        if (block.size() % nof_bits_per_re != 0 || pos + block.size() > nof_llrs) {
-          throw std::logic_error(std::string(WHO) + ": codeword buffer block not aligned to the REs");
-        }
-        std::memcpy(block.data(), llrs + pos, block.size());
-        block_seq.resize(block.size());
-        srsvec::copy_offset(block_seq, 0, seq, pos, block.size());
-        count += block.size() / nof_bits_per_re;
-        pos += block.size();
-        if (count == nof_re_symbol) {
-          notifier.on_provisional_stats(l, stats_of(st + 2 * l));
-        }
-        codeword_buffer.on_new_block(block, block_seq);
-      }
-    }
-    notifier.on_end_stats(stats_of(st + 2 * 14));
-    codeword_buffer.on_end_codeword();
+    gpu::feed_codeword(codeword_buffer, notifier, config, a.nof_rb, out_buf.host<int8_t>(),
+                       out_buf.host<uint32_t>(seq_off), nof_llrs, out_buf.host<float>(stats_off), opts, seq_bytes,
+                       block_seq, WHO);
   }
 
 private:
-  /// demodulation_stats of one (SINR dB, EVM) row: the SINR is reported always (+inf without the post-equalisation
-  /// SINR, as pusch_demodulator_impl.cpp:400 does with no accumulated noise), the EVM with the EVM calculator only.
-  pusch_demodulator_notifier::demodulation_stats stats_of(const float* row) const
-  {
-    pusch_demodulator_notifier::demodulation_stats out;
-    out.sinr_dB.emplace(opts.enable_post_eq_sinr ? row[0] : std::numeric_limits<float>::infinity());
-    if (opts.enable_evm && !std::isnan(row[1])) {
-      out.evm.emplace(row[1]);
-    }
-    return out;
-  }
-
   std::shared_ptr<srsgpu_context>                owner;
   srsgpu_context*                                ctx;
   gpu::pusch_demodulator_options                 opts;

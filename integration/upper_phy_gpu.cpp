@@ -1,0 +1,1191 @@
+// Slot-batched GPU processing behind the reference's upper-PHY slot processors: see upper_phy_gpu.h for the design.
+#include "upper_phy_gpu.h"
+
+#include "chain_convert.h"
+#include "gpu_staging.h"
+#include "lib/phy/upper/channel_processors/pdsch/pdsch_processor_helpers.h"
+#include "lib/phy/upper/channel_processors/pusch/pusch_processor_impl.h"
+#include "srsran/phy/support/resource_grid_reader.h"
+#include "srsran/phy/support/resource_grid_writer.h"
+#include "srsran/phy/upper/channel_coding/ldpc/ldpc.h"
+#include "srsran/phy/upper/channel_processors/pdsch/pdsch_encoder.h"
+#include "srsran/phy/upper/channel_processors/pusch/factories.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_decoder.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_decoder_buffer.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_decoder_notifier.h"
+#include "srsran/phy/upper/channel_processors/pusch/pusch_decoder_result.h"
+#include "srsran/phy/upper/channel_processors/uci/factories.h"
+#include "srsran/phy/upper/rx_buffer.h"
+#include "srsran/phy/upper/unique_rx_buffer.h"
+#include "srsran/phy/upper/uplink_slot_processor.h"
+#include "srsran/ran/sch/sch_dmrs_power.h"
+
+#include <array>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <thread>
+
+namespace srsran {
+namespace gpu {
+
+namespace {
+
+constexpr unsigned HARQ_SLOT_BYTES = 66 * 384;  ///< N of BG1 at Z = 384: one arena slot per codeblock.
+
+uint8_t bg_number(ldpc_base_graph_type bg)
+{
+  return bg == ldpc_base_graph_type::BG1 ? 1 : 2;
+}
+
+/// Codeblock length N (soft bits kept for HARQ) and message bits K Z of a transport block's codeblocks.
+void ldpc_lengths(units::bits tbs, ldpc_base_graph_type bg, unsigned& N, unsigned& KZ)
+{
+  const unsigned Z = ldpc::compute_lifting_size(tbs, bg, ldpc::compute_nof_codeblocks(tbs, bg));
+  N                = (bg == ldpc_base_graph_type::BG1 ? 66 : 50) * Z;
+  KZ               = (bg == ldpc_base_graph_type::BG1 ? 22 : 10) * Z;
+}
+
+} // namespace
+
+// ---------------------------------------------------------------------------------------------------------------------
+// HARQ arena
+// ---------------------------------------------------------------------------------------------------------------------
+
+class pusch_harq_arena
+{
+public:
+  pusch_harq_arena(int device, unsigned max_cb_ids_) : ctx(shared_context(device)), max_cb_ids(max_cb_ids_)
+  {
+    device_scope dev(ctx.get(), "pusch_harq_arena");
+    // Zero-initialised like the reference's codeblock pool storage; never cleared afterwards (the reference's
+    // rx_buffer soft bits persist across reservations: a new transmission overwrites what the dematcher writes).
+    hip_check(hipMalloc(&d_soft, static_cast<size_t>(max_cb_ids) * HARQ_SLOT_BYTES), "pusch_harq_arena", "arena");
+    hip_check(hipMemset(d_soft, 0, static_cast<size_t>(max_cb_ids) * HARQ_SLOT_BYTES), "pusch_harq_arena", "arena");
+  }
+  ~pusch_harq_arena() { (void)hipFree(d_soft); }
+
+  std::shared_ptr<srsgpu_context> ctx;
+  unsigned                        max_cb_ids;
+  int8_t*                         d_soft = nullptr;
+};
+
+std::shared_ptr<pusch_harq_arena> create_pusch_harq_arena(int device, unsigned max_cb_ids)
+{
+  return std::make_shared<pusch_harq_arena>(device, max_cb_ids);
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// PUSCH slot batch
+// ---------------------------------------------------------------------------------------------------------------------
+
+namespace {
+
+/// One registered PUSCH transmission and what the batch derives for it.
+struct pusch_entry {
+  pusch_processor::pdu_t           pdu;
+  span<uint8_t>                    data;
+  unique_rx_buffer                 rm;
+  pusch_processor_result_notifier* notifier = nullptr;
+  const resource_grid_reader*      grid     = nullptr;
+  // Layout within the batch.
+  unsigned nof_rb     = 0;
+  unsigned nof_cbs    = 0;
+  unsigned cb0        = 0;  ///< First codeblock of the TB in the batch.
+  unsigned llr_offset = 0;
+  unsigned nof_llrs   = 0;
+  unsigned tb_offset  = 0;
+  unsigned harq0      = 0;  ///< First byte of the TB's HARQ soft bits in the batch HARQ buffer.
+  unsigned cb_N       = 0;
+  unsigned cb_KZ      = 0;
+  bool     new_data   = true;
+};
+
+/// Replay stages: the reference's pusch_processor_impl runs per PDU on the batch's results.
+class replay_estimator : public dmrs_pusch_estimator
+{
+public:
+  const float* nv = nullptr;
+  const float* m  = nullptr;
+
+  void estimate(channel_estimate& estimate, const resource_grid_reader& /*grid*/, const configuration& config) override
+  {
+    const unsigned P = config.rx_ports.size();
+    const unsigned L = config.get_nof_tx_layers();
+    estimate.resize({static_cast<unsigned>(config.rb_mask.size()), config.first_symbol + config.nof_symbols, P, L});
+    write_chest_metrics(estimate, nv, m, P, L);
+  }
+};
+
+class replay_demodulator : public pusch_demodulator
+{
+public:
+  pusch_demodulator_options opts;
+  const int8_t*             llrs     = nullptr;
+  const uint32_t*           seq      = nullptr;
+  const float*              stats    = nullptr;
+  unsigned                  nof_llrs = 0;
+  unsigned                  nof_rb   = 0;
+
+  void demodulate(pusch_codeword_buffer&      codeword_buffer,
+                  pusch_demodulator_notifier& notifier,
+                  const resource_grid_reader& /*grid*/,
+                  const channel_estimate& /*estimates*/,
+                  const configuration& config) override
+  {
+    feed_codeword(codeword_buffer, notifier, config, nof_rb, llrs, seq, nof_llrs, stats, opts, seq_bytes, block_seq,
+                  "pusch_slot_batch");
+  }
+
+private:
+  std::vector<uint8_t> seq_bytes;
+  dynamic_bit_buffer   block_seq;
+};
+
+/// The decoder stage of the replay: the TB was decoded on the GPU; on_end_softbits() settles the rx buffer like
+/// pusch_decoder_impl::join_and_notify (pusch_decoder_impl.cpp:386-440) and notifies the result.
+class replay_decoder : public pusch_decoder, private pusch_decoder_buffer
+{
+public:
+  const uint8_t* cb_flags = nullptr;  ///< CB CRC flags after the decode (batch-wide array, first of the TB).
+  const int32_t* cb_iters = nullptr;  ///< Iterations per CB (> 0 on success).
+  const uint8_t* tb       = nullptr;  ///< Decoded TB bytes.
+  const uint8_t* cb_msgs  = nullptr;  ///< Decoded messages, SRSGPU_CB_MSG_STRIDE bytes per CB.
+  const uint8_t* decoded  = nullptr;  ///< 1: the CB went through the LDPC decoder in this transmission.
+  bool           tb_ok    = false;
+  unsigned       cb_KZ    = 0;
+  unsigned       max_iter = 6;
+
+  pusch_decoder_buffer& new_data(span<uint8_t>           transport_block_,
+                                 unique_rx_buffer        rm_,
+                                 pusch_decoder_notifier& notifier_,
+                                 const configuration& /*cfg*/) override
+  {
+    transport_block = transport_block_;
+    rm              = std::move(rm_);
+    notifier        = &notifier_;
+    return *this;
+  }
+
+  void set_nof_softbits(units::bits /*nof_softbits*/) override {}
+
+private:
+  span<log_likelihood_ratio> get_next_block_view(unsigned block_size) override
+  {
+    scratch.resize(std::max<size_t>(scratch.size(), block_size));
+    return span<log_likelihood_ratio>(scratch).first(block_size);
+  }
+  void on_new_softbits(span<const log_likelihood_ratio> /*softbits*/) override {}
+
+  void on_end_softbits() override
+  {
+    span<bool>           crcs    = rm->get_codeblocks_crc();
+    const unsigned       nof_cbs = crcs.size();
+    pusch_decoder_result result;
+    result.tb_crc_ok            = tb_ok;
+    result.nof_codeblocks_total = nof_cbs;
+    result.ldpc_decoder_stats.reset();
+    if (cb_stats.size() < nof_cbs) {
+      cb_stats.resize(nof_cbs, 0);
+    }
+    for (unsigned c = 0; c != nof_cbs; ++c) {
+      // pusch_decoder_impl.cpp:339-352: the iterations of a decoded CB (all of them on failure); a CB whose CRC had
+      // already passed is not decoded again and keeps its previous statistic.
+      if (decoded[c] != 0) {
+        cb_stats[c] = cb_iters[c] > 0 ? static_cast<unsigned>(cb_iters[c]) : max_iter;
+      }
+      result.ldpc_decoder_stats.update(cb_stats[c]);
+      crcs[c] = cb_flags[c] != 0;
+    }
+    if (tb_ok) {
+      std::memcpy(transport_block.data(), tb, transport_block.size());
+      rm.release();
+    } else {
+      // Codeblocks that passed keep their message for the retransmission (rx_buffer::get_codeblock_data_bits).
+      const unsigned nbytes = (cb_KZ + 7) / 8;
+      for (unsigned c = 0; c != nof_cbs; ++c) {
+        if (crcs[c]) {
+          bit_buffer bits = rm->get_codeblock_data_bits(c, cb_KZ);
+          for (unsigned i = 0; i != nbytes; ++i) {
+            bits.set_byte(cb_msgs[static_cast<size_t>(c) * SRSGPU_CB_MSG_STRIDE + i], i);
+          }
+        }
+      }
+      rm.unlock();
+    }
+    notifier->on_sch_data(result);
+  }
+
+  span<uint8_t>                     transport_block;
+  unique_rx_buffer                  rm;
+  pusch_decoder_notifier*           notifier = nullptr;
+  std::vector<log_likelihood_ratio> scratch;
+  std::vector<unsigned>             cb_stats;
+};
+
+/// A reference pusch_processor_impl over the replay stages (one per thread that runs batches: the processor's
+/// dependency pool binds its instances to threads, concurrent_thread_local_object_pool.h:67-96).
+struct replay_processor {
+  replay_estimator*               est   = nullptr;
+  replay_demodulator*             demod = nullptr;
+  replay_decoder*                 dec   = nullptr;
+  std::unique_ptr<pusch_processor> proc;
+};
+
+} // namespace
+
+class pusch_slot_batch
+{
+  static constexpr const char* WHO = "pusch_slot_batch";
+
+public:
+  pusch_slot_batch(const pusch_batch_configuration&           cfg_,
+                   std::shared_ptr<pusch_harq_arena>          arena_,
+                   std::shared_ptr<ulsch_demultiplex_factory> demux_factory_,
+                   std::shared_ptr<uci_decoder_factory>       uci_factory_,
+                   std::unique_ptr<pusch_processor>           fallback_) :
+    cfg(cfg_),
+    arena(std::move(arena_)),
+    ctx(arena->ctx.get()),
+    demux_factory(std::move(demux_factory_)),
+    uci_factory(std::move(uci_factory_)),
+    fallback(std::move(fallback_)),
+    stream(ctx, WHO),
+    chest_plans(srsgpu_pusch_chest_plan_destroy, 16),
+    demod_plans(srsgpu_pusch_demodulator_plan_destroy, 16),
+    dec_plans(srsgpu_pusch_decoder_plan_destroy, 16),
+    grid_buf(WHO),
+    out_buf(WHO),
+    flag_buf(WHO),
+    msg_buf(WHO),
+    job_buf(WHO),
+    tb_buf(WHO)
+  {
+    if (!fallback || !demux_factory || !uci_factory) {
+      throw std::invalid_argument(std::string(WHO) + ": invalid dependencies");
+    }
+  }
+
+  ~pusch_slot_batch()
+  {
+    (void)hipStreamSynchronize(stream.get());
+    (void)hipFree(d_ce);
+    (void)hipFree(d_harq);
+  }
+
+  void add(pusch_entry&& e)
+  {
+    std::lock_guard<std::mutex> lock(pending_mtx);
+    pending.push_back(std::move(e));
+  }
+
+  std::vector<pusch_entry> take()
+  {
+    std::lock_guard<std::mutex> lock(pending_mtx);
+    return std::exchange(pending, {});
+  }
+
+  void run(std::vector<pusch_entry>& entries);
+
+private:
+  /// PDUs the batch covers: SCH data without UCI, identity rx port list, up to four layers.
+  static bool batchable(const pusch_entry& e)
+  {
+    const pusch_processor::pdu_t& pdu = e.pdu;
+    if (!pdu.codeword.has_value() || pdu.uci.nof_harq_ack != 0 || pdu.uci.nof_csi_part1 != 0 ||
+        !pdu.uci.csi_part2_size.entries.empty() || pdu.nof_tx_layers == 0 || pdu.nof_tx_layers > 4 ||
+        pdu.rx_ports.empty() || pdu.rx_ports.size() > 4 || pdu.cp != cyclic_prefix::NORMAL) {
+      return false;
+    }
+    for (unsigned p = 0; p != pdu.rx_ports.size(); ++p) {
+      if (pdu.rx_ports[p] != p) {
+        return false;
+      }
+    }
+    return true;
+  }
+
+  replay_processor& replay_for_this_thread();
+
+  template <typename T>
+  static void reserve_device(T*& ptr, size_t& cap, size_t bytes, const char* what)
+  {
+    if (bytes <= cap) {
+      return;
+    }
+    (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+    hip_check(hipMalloc(reinterpret_cast<void**>(&ptr), bytes), WHO, what);
+    cap = bytes;
+  }
+
+  pusch_batch_configuration                     cfg;
+  std::shared_ptr<pusch_harq_arena>             arena;
+  srsgpu_context*                               ctx;
+  std::shared_ptr<ulsch_demultiplex_factory>    demux_factory;
+  std::shared_ptr<uci_decoder_factory>          uci_factory;
+  std::unique_ptr<pusch_processor>              fallback;
+  owned_stream                                  stream;
+  plan_cache<srsgpu_pusch_chest_plan>           chest_plans;
+  plan_cache<srsgpu_pusch_demodulator_plan>     demod_plans;
+  plan_cache<srsgpu_pusch_decoder_plan>         dec_plans;
+  staged_buffer                                 grid_buf;  ///< Rx grid [port][symbol][subcarrier].
+  staged_buffer                                 out_buf;   ///< nv, metrics, statistics, LLRs, scrambling words.
+  staged_buffer                                 flag_buf;  ///< CB CRC flags, iterations, TB CRC flags.
+  staged_buffer                                 msg_buf;   ///< CB messages.
+  staged_buffer                                 job_buf;   ///< HARQ arena copy jobs.
+  staged_buffer                                 tb_buf;    ///< Decoded TBs.
+  uint32_t*                                     d_ce      = nullptr;
+  size_t                                        d_ce_cap  = 0;
+  int8_t*                                       d_harq    = nullptr;
+  size_t                                        d_harq_cap = 0;
+  std::mutex                                    pending_mtx;
+  std::vector<pusch_entry>                      pending;
+  std::mutex                                    run_mtx;
+  std::map<std::thread::id, replay_processor>   replays;
+  std::vector<uint8_t>                          decoded_flags;
+};
+
+replay_processor& pusch_slot_batch::replay_for_this_thread()
+{
+  auto it = replays.find(std::this_thread::get_id());
+  if (it != replays.end()) {
+    return it->second;
+  }
+  replay_processor r;
+  auto             est   = std::make_unique<replay_estimator>();
+  auto             demod = std::make_unique<replay_demodulator>();
+  auto             dec   = std::make_unique<replay_decoder>();
+  r.est                  = est.get();
+  r.demod                = demod.get();
+  r.dec                  = dec.get();
+  demod->opts            = cfg.demodulator;
+  std::vector<std::unique_ptr<pusch_processor_impl::concurrent_dependencies>> deps;
+  deps.push_back(std::make_unique<pusch_processor_impl::concurrent_dependencies>(
+      std::move(est),
+      std::move(demod),
+      demux_factory->create(),
+      uci_factory->create(),
+      channel_estimate::channel_estimate_dimensions{MAX_RB, MAX_NSYMB_PER_SLOT, 4, 4}));
+  pusch_processor_impl::configuration pc;
+  pc.thread_local_dependencies_pool =
+      std::make_shared<pusch_processor_impl::concurrent_dependencies_pool_type>(std::move(deps));
+  pc.decoder               = std::move(dec);
+  pc.dec_nof_iterations    = cfg.nof_ldpc_iterations;
+  pc.dec_enable_early_stop = cfg.ldpc_early_stop;
+  pc.csi_sinr_calc_method  = cfg.csi_sinr_calc_method;
+  r.proc                   = std::make_unique<pusch_processor_impl>(pc);
+  return replays.emplace(std::this_thread::get_id(), std::move(r)).first->second;
+}
+
+void pusch_slot_batch::run(std::vector<pusch_entry>& all)
+{
+  std::lock_guard<std::mutex> lock(run_mtx);
+  device_scope                dev(ctx, WHO);
+
+  // PDUs outside the batch's scope go through the fallback processor, one by one, as the reference would.
+  std::vector<pusch_entry*> batch;
+  for (pusch_entry& e : all) {
+    if (batchable(e)) {
+      batch.push_back(&e);
+    } else {
+      fallback->process(e.data, std::move(e.rm), *e.notifier, *e.grid, e.pdu);
+    }
+  }
+  if (batch.empty()) {
+    return;
+  }
+  const resource_grid_reader& grid     = *batch.front()->grid;
+  const unsigned              nsc      = grid.get_nof_subc();
+  const unsigned              grid_prb = nsc / NRE;
+  unsigned                    P        = 0;
+  for (pusch_entry* e : batch) {
+    P = std::max<unsigned>(P, e->pdu.rx_ports.size());
+  }
+
+  // The estimator / demodulator / decoder configurations pusch_processor_impl derives from each PDU
+  // (pusch_processor_impl.cpp:150-337), as srsgpu descriptors, and the batch layout.
+  std::vector<pusch_chest_desc>       chests;
+  std::vector<pusch_demod_desc>       demods;
+  std::vector<srsgpu_pusch_tb_config> tbs;
+  std::vector<srsgpu_harq_copy_job>   jobs;
+  std::vector<uint8_t>                chest_key, demod_key, dec_key;
+  unsigned                            llr_total = 0, cb_total = 0, tb_total = 0, harq_total = 0;
+  gpu::key_append(chest_key, grid_prb);
+  gpu::key_append(demod_key, grid_prb);
+  for (pusch_entry* ep : batch) {
+    pusch_entry&                  e   = *ep;
+    const pusch_processor::pdu_t& pdu = e.pdu;
+    const crb_bitmap              rb_mask = pdu.freq_alloc.get_crb_mask(pdu.bwp_start_rb, pdu.bwp_size_rb);
+    e.nof_rb                              = pdu.freq_alloc.get_nof_rb();
+
+    unsigned  scrambling_id = 0, n_rs_id = 0, cdm_groups = 2;
+    bool      n_scid = false, tp = false;
+    dmrs_type dmrs   = dmrs_type::TYPE1;
+    if (std::holds_alternative<pusch_processor::dmrs_configuration>(pdu.dmrs)) {
+      const auto& d = std::get<pusch_processor::dmrs_configuration>(pdu.dmrs);
+      scrambling_id = d.scrambling_id;
+      n_scid        = d.n_scid;
+      cdm_groups    = d.nof_cdm_groups_without_data;
+      dmrs          = d.dmrs;
+    } else {
+      tp      = true;
+      n_rs_id = std::get<pusch_processor::dmrs_transform_precoding_configuration>(pdu.dmrs).n_rs_id;
+    }
+
+    dmrs_pusch_estimator::configuration est;
+    est.slot = pdu.slot;
+    if (tp) {
+      est.sequence_config = dmrs_pusch_estimator::low_papr_sequence_configuration{.n_rs_id = n_rs_id};
+    } else {
+      est.sequence_config = dmrs_pusch_estimator::pseudo_random_sequence_configuration{
+          .type = dmrs, .nof_tx_layers = pdu.nof_tx_layers, .scrambling_id = scrambling_id, .n_scid = n_scid};
+    }
+    est.scaling      = convert_dB_to_amplitude(-get_sch_to_dmrs_ratio_dB(cdm_groups));
+    est.c_prefix     = pdu.cp;
+    est.symbols_mask = pdu.dmrs_symbol_mask;
+    est.rb_mask      = rb_mask;
+    est.first_symbol = pdu.start_symbol_index;
+    est.nof_symbols  = pdu.nof_symbols;
+    est.rx_ports.assign(pdu.rx_ports.begin(), pdu.rx_ports.end());
+    chests.push_back(make_pusch_chest_desc(est, grid_prb, cfg.estimator, SRSGPU_CE_PER_SYMBOL, WHO));
+    chests.back().append_key(chest_key);
+
+    pusch_demodulator::configuration dem;
+    dem.rnti                        = pdu.rnti;
+    dem.rb_mask                     = rb_mask;
+    dem.modulation                  = pdu.mcs_descr.modulation;
+    dem.start_symbol_index          = pdu.start_symbol_index;
+    dem.nof_symbols                 = pdu.nof_symbols;
+    dem.dmrs_symb_pos               = pdu.dmrs_symbol_mask;
+    dem.dmrs_config_type            = dmrs;
+    dem.nof_cdm_groups_without_data = cdm_groups;
+    dem.n_id                        = pdu.n_id;
+    dem.nof_tx_layers               = pdu.nof_tx_layers;
+    dem.enable_transform_precoding  = tp;
+    dem.rx_ports                    = pdu.rx_ports;
+    demods.push_back(make_pusch_demod_desc(dem, grid_prb, cfg.demodulator, SRSGPU_CE_PER_SYMBOL, WHO));
+    pusch_demod_desc& dd = demods.back();
+
+    // Codeword LLRs: nof_rb REs per data symbol (minus the DM-RS REs) x layers x Qm.
+    const unsigned dmrs_re = cdm_groups * (dmrs == dmrs_type::TYPE1 ? 6 : 4);
+    unsigned       nre     = 0;
+    for (unsigned l = pdu.start_symbol_index; l != pdu.start_symbol_index + pdu.nof_symbols; ++l) {
+      nre += e.nof_rb * (pdu.dmrs_symbol_mask.test(l) ? NRE - dmrs_re : NRE);
+    }
+    e.nof_llrs      = nre * pdu.nof_tx_layers * dd.qm;
+    e.llr_offset    = llr_total;
+    dd.c.llr_offset = llr_total;
+    llr_total += (e.nof_llrs + 63) / 64 * 64;
+    dd.append_key(demod_key);
+
+    // TB decoding (pusch_processor_impl.cpp:278-296).
+    const units::bits tb_bits = units::bytes(e.data.size()).to_bits();
+    const auto        bg      = pdu.codeword->ldpc_base_graph;
+    e.nof_cbs                 = ldpc::compute_nof_codeblocks(tb_bits, bg);
+    ldpc_lengths(tb_bits, bg, e.cb_N, e.cb_KZ);
+    e.cb0       = cb_total;
+    e.tb_offset = tb_total;
+    e.harq0     = harq_total;
+    e.new_data  = pdu.codeword->new_data;
+    srsgpu_pusch_tb_config t;
+    std::memset(&t, 0, sizeof(t));
+    t.base_graph       = bg_number(bg);
+    t.rv               = static_cast<uint8_t>(pdu.codeword->rv);
+    t.modulation_order = static_cast<uint8_t>(dd.qm);
+    t.nof_layers       = static_cast<uint8_t>(pdu.nof_tx_layers);
+    t.new_data         = e.new_data ? 1 : 0;
+    t.use_early_stop   = cfg.ldpc_early_stop ? 1 : 0;
+    t.max_iterations   = static_cast<uint8_t>(cfg.nof_ldpc_iterations);
+    t.scaling_factor   = 0.8F;  // ldpc_decoder::configuration::algorithm_details default (ldpc_decoder.h:50)
+    t.tbs_bytes        = static_cast<uint32_t>(e.data.size());
+    t.nof_ch_symbols   = e.nof_llrs / dd.qm;
+    t.Nref             = ldpc::compute_N_ref(pdu.tbs_lbrm, e.nof_cbs).value();
+    t.llr_offset       = e.llr_offset;
+    t.harq_offset      = e.harq0;
+    t.cb_offset        = e.cb0;
+    t.tb_offset        = e.tb_offset;
+    tbs.push_back(t);
+    gpu::key_append(dec_key, t);
+    for (unsigned c = 0; c != e.nof_cbs; ++c) {
+      const unsigned id = e.rm->get_absolute_codeblock_id(c);
+      if (id >= arena->max_cb_ids) {
+        throw std::out_of_range(std::string(WHO) + ": absolute codeblock id " + std::to_string(id) +
+                                " beyond the HARQ arena");
+      }
+      jobs.push_back({id, e.harq0 + c * e.cb_N, e.cb_N, 0});
+    }
+    cb_total += e.nof_cbs;
+    tb_total += (static_cast<unsigned>(e.data.size()) + 15) / 16 * 16;
+    harq_total += e.nof_cbs * e.cb_N;
+  }
+  const unsigned n = batch.size();
+
+  // Plans (cached: a cell's grants repeat).
+  srsgpu_pusch_chest_plan* chest = chest_plans.get(chest_key, [&] {
+    std::vector<srsgpu_pusch_chest_config> c;
+    std::vector<srsgpu_alloc_ext>          x;
+    for (const pusch_chest_desc& d : chests) {
+      c.push_back(d.c);
+      x.push_back(d.ext());
+    }
+    srsgpu_pusch_chest_plan* p = nullptr;
+    srsgpu_check(srsgpu_pusch_chest_plan_create_ex(ctx, c.data(), x.data(), n, grid_prb, P, &p), WHO);
+    return p;
+  });
+  srsgpu_pusch_demodulator_plan* demod = demod_plans.get(demod_key, [&] {
+    std::vector<srsgpu_pusch_demod_config> c;
+    std::vector<srsgpu_alloc_ext>          x;
+    for (const pusch_demod_desc& d : demods) {
+      c.push_back(d.c);
+      x.push_back(d.ext());
+    }
+    srsgpu_pusch_demodulator_plan* p = nullptr;
+    srsgpu_check(srsgpu_pusch_demodulator_plan_create_ex(ctx, c.data(), x.data(), n, grid_prb, P, &p), WHO);
+    return p;
+  });
+  srsgpu_pusch_decoder_plan* dec = dec_plans.get(dec_key, [&] {
+    srsgpu_pusch_decoder_plan* p = nullptr;
+    srsgpu_check(srsgpu_pusch_decoder_plan_create(ctx, SRSGPU_LDPC_IMPL_SIMD, tbs.data(), n, &p), WHO);
+    return p;
+  });
+
+  hipStream_t  s   = stream.get();
+  const size_t row = static_cast<size_t>(nsc) * sizeof(uint32_t);
+
+  // Rx grid: every symbol of ports 0..P-1, [port][symbol][subcarrier].
+  grid_buf.reserve(P * 14 * row);
+  for (unsigned p = 0; p != P; ++p) {
+    for (unsigned l = 0; l != 14; ++l) {
+      std::memcpy(grid_buf.host((p * 14 + l) * row), grid.get_view(p, l).data(), row);
+    }
+  }
+  grid_buf.upload(0, P * 14 * row, s);
+
+  // Output staging: nv [4 n], metrics [4 n][METRICS], statistics [n][DEMOD_STATS], LLRs, scrambling words.
+  const size_t nv_off    = 0;
+  const size_t m_off     = nv_off + 4 * n * sizeof(float);
+  const size_t st_off    = m_off + 4 * n * SRSGPU_CHEST_METRICS * sizeof(float);
+  const size_t llr_off   = (st_off + n * SRSGPU_DEMOD_STATS * sizeof(float) + 63) / 64 * 64;
+  size_t       seq_total = 0;
+  std::vector<size_t> seq_off(n);
+  for (unsigned i = 0; i != n; ++i) {
+    seq_off[i] = llr_off + llr_total + seq_total;
+    seq_total += (batch[i]->nof_llrs + 31) / 32 * 4;
+  }
+  const size_t out_bytes = llr_off + llr_total + seq_total;
+  out_buf.reserve(out_bytes);
+  reserve_device(d_ce, d_ce_cap, static_cast<size_t>(4) * P * 14 * row, "channel estimates");
+
+  srsgpu_check(srsgpu_pusch_chest_plan_execute(chest, grid_buf.dev<uint32_t>(), d_ce, out_buf.dev<float>(nv_off),
+                                               out_buf.dev<float>(m_off), s),
+               WHO);
+  // pusch_processor_impl.cpp:222-240: the DC subcarrier's estimate is zeroed for CP-OFDM transmissions over it.
+  for (unsigned i = 0; i != n; ++i) {
+    const pusch_processor::pdu_t& pdu = batch[i]->pdu;
+    if (pdu.dc_position.has_value() && std::holds_alternative<pusch_processor::dmrs_configuration>(pdu.dmrs) &&
+        *pdu.dc_position < nsc) {
+      for (unsigned ly = 0; ly != pdu.nof_tx_layers; ++ly) {
+        for (unsigned p = 0; p != pdu.rx_ports.size(); ++p) {
+          uint8_t* base = reinterpret_cast<uint8_t*>(d_ce) + ((static_cast<size_t>(ly) * P + p) * 14 +
+                                                              pdu.start_symbol_index) * row +
+                          static_cast<size_t>(*pdu.dc_position) * sizeof(uint32_t);
+          hip_check(hipMemset2DAsync(base, row, 0, sizeof(uint32_t), pdu.nof_symbols, s), WHO, "DC");
+        }
+      }
+    }
+  }
+  srsgpu_check(srsgpu_pusch_demodulator_plan_execute_ex(demod, grid_buf.dev<uint32_t>(), d_ce,
+                                                        out_buf.dev<float>(nv_off), out_buf.dev<int8_t>(llr_off),
+                                                        out_buf.dev<float>(st_off), s),
+               WHO);
+  for (unsigned i = 0; i != n; ++i) {
+    srsgpu_check(srsgpu_pusch_demodulator_plan_scrambling(demod, i, out_buf.dev<uint32_t>(seq_off[i]), s), WHO);
+  }
+
+  // HARQ context: soft bits from the arena, CB CRC flags (and the messages of CBs that already passed) from the rx
+  // buffers; a new transmission's flags are reset by the plan (pusch_decoder_impl.cpp:133-136).
+  const size_t flags_off = 0;
+  const size_t iters_off = (cb_total + 15) / 16 * 16;
+  const size_t tbok_off  = iters_off + cb_total * sizeof(int32_t);
+  flag_buf.reserve(tbok_off + n + 16);
+  msg_buf.reserve(static_cast<size_t>(cb_total) * SRSGPU_CB_MSG_STRIDE);
+  decoded_flags.assign(cb_total, 0);
+  bool any_restored = false;
+  for (unsigned i = 0; i != n; ++i) {
+    pusch_entry&     e    = *batch[i];
+    span<const bool> crcs = e.rm->get_codeblocks_crc();
+    for (unsigned c = 0; c != e.nof_cbs; ++c) {
+      const bool ok                         = !e.new_data && crcs[c];
+      *flag_buf.host<uint8_t>(e.cb0 + c) = ok ? 1 : 0;
+      decoded_flags[e.cb0 + c]              = ok ? 0 : 1;
+      if (ok) {
+        const bit_buffer bits = e.rm->get_codeblock_data_bits(c, e.cb_KZ);
+        uint8_t*         dst  = msg_buf.host<uint8_t>(static_cast<size_t>(e.cb0 + c) * SRSGPU_CB_MSG_STRIDE);
+        for (unsigned b = 0; b != (e.cb_KZ + 7) / 8; ++b) {
+          dst[b] = bits.get_byte(b);
+        }
+        any_restored = true;
+      }
+    }
+  }
+  flag_buf.upload(flags_off, cb_total, s);
+  if (any_restored) {
+    msg_buf.upload(0, static_cast<size_t>(cb_total) * SRSGPU_CB_MSG_STRIDE, s);
+  }
+  job_buf.reserve(jobs.size() * sizeof(srsgpu_harq_copy_job));
+  std::memcpy(job_buf.host(), jobs.data(), jobs.size() * sizeof(srsgpu_harq_copy_job));
+  job_buf.upload(0, jobs.size() * sizeof(srsgpu_harq_copy_job), s);
+  reserve_device(d_harq, d_harq_cap, std::max<size_t>(harq_total, 16), "HARQ batch buffer");
+  srsgpu_check(srsgpu_harq_copy(ctx, SRSGPU_HARQ_TO_BATCH, arena->d_soft, HARQ_SLOT_BYTES, d_harq,
+                                job_buf.dev<srsgpu_harq_copy_job>(), jobs.size(), s),
+               WHO);
+  tb_buf.reserve(std::max<unsigned>(tb_total, 16));
+  srsgpu_check(srsgpu_pusch_decoder_plan_execute(dec, out_buf.dev<int8_t>(llr_off), d_harq,
+                                                 flag_buf.dev<uint8_t>(flags_off), msg_buf.dev<uint8_t>(),
+                                                 flag_buf.dev<int32_t>(iters_off), tb_buf.dev<uint8_t>(),
+                                                 flag_buf.dev<uint8_t>(tbok_off), s),
+               WHO);
+  srsgpu_check(srsgpu_harq_copy(ctx, SRSGPU_HARQ_TO_ARENA, arena->d_soft, HARQ_SLOT_BYTES, d_harq,
+                                job_buf.dev<srsgpu_harq_copy_job>(), jobs.size(), s),
+               WHO);
+  out_buf.download(0, out_bytes, s);
+  flag_buf.download(0, tbok_off + n, s);
+  tb_buf.download(0, tb_total, s);
+  hip_check(hipStreamSynchronize(s), WHO, "synchronise");
+
+  // Messages of the passed CBs of failed TBs are kept in the rx buffer for the retransmission.
+  bool need_msgs = false;
+  for (unsigned i = 0; i != n && !need_msgs; ++i) {
+    const pusch_entry& e = *batch[i];
+    if (*flag_buf.host<uint8_t>(tbok_off + i) == 0) {
+      for (unsigned c = 0; c != e.nof_cbs; ++c) {
+        need_msgs = need_msgs || *flag_buf.host<uint8_t>(e.cb0 + c) != 0;
+      }
+    }
+  }
+  if (need_msgs) {
+    msg_buf.download(0, static_cast<size_t>(cb_total) * SRSGPU_CB_MSG_STRIDE, s);
+    hip_check(hipStreamSynchronize(s), WHO, "synchronise");
+  }
+
+  // Result assembly and notification by the reference's own processor, PDU by PDU.
+  replay_processor& r = replay_for_this_thread();
+  for (unsigned i = 0; i != n; ++i) {
+    pusch_entry& e      = *batch[i];
+    r.est->nv           = out_buf.host<float>(nv_off + 4 * i * sizeof(float));
+    r.est->m            = out_buf.host<float>(m_off + 4 * i * SRSGPU_CHEST_METRICS * sizeof(float));
+    r.demod->llrs       = out_buf.host<int8_t>(llr_off + e.llr_offset);
+    r.demod->seq        = out_buf.host<uint32_t>(seq_off[i]);
+    r.demod->stats      = out_buf.host<float>(st_off + i * SRSGPU_DEMOD_STATS * sizeof(float));
+    r.demod->nof_llrs   = e.nof_llrs;
+    r.demod->nof_rb     = e.nof_rb;
+    r.dec->cb_flags     = flag_buf.host<uint8_t>(flags_off + e.cb0);
+    r.dec->cb_iters     = flag_buf.host<int32_t>(iters_off + e.cb0 * sizeof(int32_t));
+    r.dec->tb           = tb_buf.host<uint8_t>(e.tb_offset);
+    r.dec->cb_msgs      = msg_buf.host<uint8_t>(static_cast<size_t>(e.cb0) * SRSGPU_CB_MSG_STRIDE);
+    r.dec->decoded      = decoded_flags.data() + e.cb0;
+    r.dec->tb_ok        = *flag_buf.host<uint8_t>(tbok_off + i) != 0;
+    r.dec->cb_KZ        = e.cb_KZ;
+    r.dec->max_iter     = cfg.nof_ldpc_iterations;
+    r.proc->process(e.data, std::move(e.rm), *e.notifier, *e.grid, e.pdu);
+  }
+}
+
+std::shared_ptr<pusch_slot_batch> create_pusch_slot_batch(const pusch_batch_configuration&           config,
+                                                          std::shared_ptr<pusch_harq_arena>          arena,
+                                                          std::shared_ptr<ulsch_demultiplex_factory> demux,
+                                                          std::shared_ptr<uci_decoder_factory>       uci,
+                                                          std::unique_ptr<pusch_processor>           fallback)
+{
+  return std::make_shared<pusch_slot_batch>(config, std::move(arena), std::move(demux), std::move(uci),
+                                            std::move(fallback));
+}
+
+namespace {
+
+class pusch_processor_batch_gpu : public pusch_processor
+{
+public:
+  explicit pusch_processor_batch_gpu(std::shared_ptr<pusch_slot_batch> batch_) : batch(std::move(batch_)) {}
+
+  void process(span<uint8_t>                    data,
+               unique_rx_buffer                 rm_buffer,
+               pusch_processor_result_notifier& notifier,
+               const resource_grid_reader&      grid,
+               const pdu_t&                     pdu) override
+  {
+    pusch_entry e;
+    e.pdu      = pdu;
+    e.data     = data;
+    e.rm       = std::move(rm_buffer);
+    e.notifier = &notifier;
+    e.grid     = &grid;
+    batch->add(std::move(e));
+  }
+
+private:
+  std::shared_ptr<pusch_slot_batch> batch;
+};
+
+class inline_executor : public task_executor
+{
+public:
+  bool execute(unique_task task) override
+  {
+    task();
+    return true;
+  }
+  bool defer(unique_task task) override
+  {
+    task();
+    return true;
+  }
+};
+
+/// The reference's uplink processor with the batch run after each handle_rx_symbol.
+class uplink_processor_batch_gpu : public uplink_processor
+{
+  /// The slot processor handed out for one slot (a ring indexed by slot, like the reference's request pools).
+  class slot_processor : public uplink_slot_processor
+  {
+  public:
+    uplink_processor_batch_gpu* owner = nullptr;
+    slot_point                  slot;
+
+    void handle_rx_symbol(unsigned end_symbol_index) override
+    {
+      owner->inner->get_slot_processor(slot).handle_rx_symbol(end_symbol_index);
+      owner->flush();
+    }
+    void process_prach(const prach_buffer& buffer, const prach_buffer_context& context) override
+    {
+      owner->inner->get_slot_processor(slot).process_prach(buffer, context);
+    }
+    void discard_slot() override
+    {
+      owner->inner->get_slot_processor(slot).discard_slot();
+      owner->flush();
+    }
+  };
+
+public:
+  uplink_processor_batch_gpu(std::unique_ptr<uplink_processor> inner_,
+                             std::shared_ptr<pusch_slot_batch> batch_,
+                             task_executor&                    executor_) :
+    inner(std::move(inner_)), batch(std::move(batch_)), executor(executor_)
+  {
+    for (slot_processor& s : slots) {
+      s.owner = this;
+    }
+  }
+
+  unique_uplink_pdu_slot_repository get_pdu_slot_repository(slot_point slot) override
+  {
+    return inner->get_pdu_slot_repository(slot);
+  }
+
+  uplink_slot_processor& get_slot_processor(slot_point slot) override
+  {
+    slot_processor& s = slots[slot.system_slot() % slots.size()];
+    s.slot            = slot;
+    return s;
+  }
+
+  void stop() override { inner->stop(); }
+
+private:
+  /// Hands the PDUs registered by the last reference call to the PUSCH executor as one job.
+  void flush()
+  {
+    auto entries = std::make_shared<std::vector<pusch_entry>>(batch->take());
+    if (entries->empty()) {
+      return;
+    }
+    std::shared_ptr<pusch_slot_batch> b = batch;
+    if (!executor.execute([b, entries]() { b->run(*entries); })) {
+      b->run(*entries);  // the executor refused the job: run it here rather than lose the PDUs' notifications
+    }
+  }
+
+  std::unique_ptr<uplink_processor>  inner;
+  std::shared_ptr<pusch_slot_batch>  batch;
+  task_executor&                     executor;
+  std::array<slot_processor, 16>     slots;
+};
+
+} // namespace
+
+std::unique_ptr<pusch_processor> create_pusch_processor_batch_gpu(std::shared_ptr<pusch_slot_batch> batch)
+{
+  return std::make_unique<pusch_processor_batch_gpu>(std::move(batch));
+}
+
+task_executor& pusch_inline_executor()
+{
+  static inline_executor exec;
+  return exec;
+}
+
+std::unique_ptr<uplink_processor> create_uplink_processor_batch_gpu(std::unique_ptr<uplink_processor>  inner,
+                                                                    std::shared_ptr<pusch_slot_batch> batch,
+                                                                    task_executor&                    executor)
+{
+  return std::make_unique<uplink_processor_batch_gpu>(std::move(inner), std::move(batch), executor);
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// PDSCH slot batch
+// ---------------------------------------------------------------------------------------------------------------------
+
+namespace {
+
+/// One recorded PDSCH transmission.
+struct pdsch_entry {
+  resource_grid_writer*          grid     = nullptr;
+  pdsch_processor_notifier*      notifier = nullptr;
+  srsgpu_pdsch_tb_config         tb;
+  pdsch_modulator::config_t      mod;
+  dmrs_pdsch_processor::config_t dmrs;
+};
+
+/// Captures the DM-RS configuration pdsch_process_dmrs builds (pdsch_processor_helpers.h:43-70).
+class recording_dmrs : public dmrs_pdsch_processor
+{
+public:
+  dmrs_pdsch_processor::config_t* out = nullptr;
+  void map(resource_grid_writer& /*grid*/, const config_t& config) override { *out = config; }
+};
+
+thread_local bool pdsch_inline_scope = false;
+
+} // namespace
+
+class pdsch_slot_batch
+{
+  static constexpr const char* WHO = "pdsch_slot_batch";
+
+public:
+  pdsch_slot_batch(int device, std::unique_ptr<ptrs_pdsch_generator> ptrs_, std::unique_ptr<pdsch_processor> fallback_) :
+    owner(shared_context(device)),
+    ctx(owner.get()),
+    ptrs(std::move(ptrs_)),
+    fallback(std::move(fallback_)),
+    stream(ctx, WHO),
+    enc_plans(srsgpu_pdsch_encoder_plan_destroy, 16),
+    mod_plans(srsgpu_pdsch_modulator_plan_destroy, 16),
+    dmrs_plans(srsgpu_pdsch_dmrs_plan_destroy, 16),
+    tb_buf(WHO),
+    grid_buf(WHO)
+  {
+    if (!ptrs || !fallback) {
+      throw std::invalid_argument(std::string(WHO) + ": invalid dependencies");
+    }
+  }
+
+  ~pdsch_slot_batch()
+  {
+    (void)hipStreamSynchronize(stream.get());
+    (void)hipFree(d_cw);
+  }
+
+  /// pdsch_processor_impl::process (pdsch_processor_impl.cpp:42-90) up to the point where the encoder, modulator and
+  /// DM-RS would run: their configurations are recorded for the batch; PT-RS is generated into the grid right away.
+  void add(resource_grid_writer&                                                           grid,
+           pdsch_processor_notifier&                                                       notifier,
+           static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data,
+           const pdsch_processor::pdu_t&                                                   pdu)
+  {
+    const unsigned nof_layers = pdu.precoding.get_nof_layers();
+    if (nof_layers == 0 || nof_layers > 4 || pdu.precoding.get_nof_ports() > 4 || data.size() != 1) {
+      fallback->process(grid, notifier, std::move(data), pdu);  // two codewords (more than four layers)
+      return;
+    }
+    std::lock_guard<std::mutex> lock(mtx);
+    pdsch_entry                 e;
+    e.grid                     = &grid;
+    e.notifier                 = &notifier;
+    span<const uint8_t> tb     = data[0].get_buffer();
+    const unsigned      nre    = pdsch_compute_nof_data_re(pdu);
+    const unsigned      qm     = get_bits_per_symbol(pdu.codewords[0].modulation);
+    const units::bits   tbs    = units::bytes(tb.size()).to_bits();
+    std::memset(&e.tb, 0, sizeof(e.tb));
+    e.tb.base_graph       = bg_number(pdu.ldpc_base_graph);
+    e.tb.rv               = static_cast<uint8_t>(pdu.codewords[0].rv);
+    e.tb.modulation_order = static_cast<uint8_t>(qm);
+    e.tb.nof_layers       = static_cast<uint8_t>(nof_layers);
+    e.tb.tbs_bytes        = static_cast<uint32_t>(tb.size());
+    e.tb.nof_ch_symbols   = nre * nof_layers;
+    e.tb.Nref = ldpc::compute_N_ref(pdu.tbs_lbrm, ldpc::compute_nof_codeblocks(tbs, pdu.ldpc_base_graph)).value();
+    e.tb.tb_offset = static_cast<uint32_t>(tb_bytes.size());
+    tb_bytes.insert(tb_bytes.end(), tb.begin(), tb.end());
+    tb_bytes.resize((tb_bytes.size() + 15) / 16 * 16, 0);
+    e.tb.cw_offset = cw_total;
+    cw_total += (nre * nof_layers * qm + 31) / 32 * 4;
+
+    // The modulator configuration pdsch_processor_impl::modulate builds (pdsch_processor_impl.cpp:143-161; one
+    // codeword; dmrs_config_type is not set there, so it keeps its default, type 1).
+    pdsch_modulator::config_t& m     = e.mod;
+    m.rnti                        = pdu.rnti;
+    m.bwp_size_rb                 = pdu.bwp_size_rb;
+    m.bwp_start_rb                = pdu.bwp_start_rb;
+    m.modulation1                 = pdu.codewords[0].modulation;
+    m.modulation2                 = modulation_scheme::BPSK;
+    m.freq_allocation             = pdu.freq_alloc;
+    m.start_symbol_index          = pdu.start_symbol_index;
+    m.nof_symbols                 = pdu.nof_symbols;
+    m.dmrs_symb_pos               = pdu.dmrs_symbol_mask;
+    m.nof_cdm_groups_without_data = pdu.nof_cdm_groups_without_data;
+    m.n_id                        = pdu.n_id;
+    m.scaling                     = convert_dB_to_amplitude(-pdu.ratio_pdsch_data_to_sss_dB);
+    m.reserved                    = pdu.reserved;
+    m.precoding                   = pdu.precoding;
+    if (pdu.ptrs) {
+      pdsch_process_ptrs(grid, *ptrs, pdu);
+    }
+    recording_dmrs rec;
+    rec.out = &e.dmrs;
+    pdsch_process_dmrs(grid, rec, pdu);
+    entries.push_back(std::move(e));
+  }
+
+  /// Encodes, modulates and maps every recorded PDSCH as one launch sequence, stores the REs into the slot's grid and
+  /// reports each PDSCH finished (after which the reference's downlink processor sends the grid).
+  void flush()
+  {
+    std::vector<pdsch_entry> es;
+    std::vector<uint8_t>     tbs;
+    unsigned                 cw_bytes = 0;
+    {
+      std::lock_guard<std::mutex> lock(mtx);
+      es       = std::exchange(entries, {});
+      tbs      = std::exchange(tb_bytes, {});
+      cw_bytes = std::exchange(cw_total, 0u);
+    }
+    if (es.empty()) {
+      return;
+    }
+    std::lock_guard<std::mutex> lock(run_mtx);
+    device_scope                dev(ctx, WHO);
+    resource_grid_writer&       grid     = *es.front().grid;
+    const unsigned              nsc      = grid.get_nof_subc();
+    const unsigned              grid_prb = nsc / NRE;
+    const unsigned              P        = grid.get_nof_ports();
+    const unsigned              n        = es.size();
+
+    std::vector<srsgpu_pdsch_tb_config> tcs;
+    std::vector<pdsch_mod_desc>         mods;
+    std::vector<pdsch_dmrs_desc>        dmrss;
+    std::vector<uint8_t>                enc_key, mod_key, dmrs_key;
+    gpu::key_append(mod_key, grid_prb);
+    gpu::key_append(dmrs_key, grid_prb);
+    for (const pdsch_entry& e : es) {
+      if (e.grid != &grid) {
+        throw std::logic_error(std::string(WHO) + ": PDSCH of one batch in different resource grids");
+      }
+      tcs.push_back(e.tb);
+      gpu::key_append(enc_key, e.tb);
+      const unsigned nof_bits = e.tb.nof_ch_symbols * e.tb.modulation_order;
+      mods.push_back(make_pdsch_mod_desc(e.mod, nof_bits, grid_prb, P, WHO));
+      mods.back().c.cw_offset = e.tb.cw_offset;
+      mods.back().append_key(mod_key);
+      dmrss.push_back(make_pdsch_dmrs_desc(e.dmrs, grid_prb, P, WHO));
+      dmrss.back().append_key(dmrs_key);
+    }
+    srsgpu_pdsch_encoder_plan* enc = enc_plans.get(enc_key, [&] {
+      srsgpu_pdsch_encoder_plan* p = nullptr;
+      srsgpu_check(srsgpu_pdsch_encoder_plan_create(ctx, tcs.data(), n, &p), WHO);
+      return p;
+    });
+    srsgpu_pdsch_modulator_plan* mod = mod_plans.get(mod_key, [&] {
+      std::vector<srsgpu_pdsch_mod_config> c;
+      std::vector<srsgpu_alloc_ext>        x;
+      for (pdsch_mod_desc& d : mods) {
+        c.push_back(d.c);
+        x.push_back(d.ext());
+      }
+      srsgpu_pdsch_modulator_plan* p = nullptr;
+      srsgpu_check(srsgpu_pdsch_modulator_plan_create_ex(ctx, c.data(), x.data(), n, grid_prb, P, &p), WHO);
+      return p;
+    });
+    srsgpu_pdsch_dmrs_plan* dmrs = dmrs_plans.get(dmrs_key, [&] {
+      std::vector<srsgpu_pdsch_dmrs_config> c;
+      std::vector<srsgpu_alloc_ext>         x;
+      for (const pdsch_dmrs_desc& d : dmrss) {
+        c.push_back(d.c);
+        x.push_back(d.ext());
+      }
+      srsgpu_pdsch_dmrs_plan* p = nullptr;
+      srsgpu_check(srsgpu_pdsch_dmrs_plan_create_ex(ctx, c.data(), x.data(), n, grid_prb, P, &p), WHO);
+      return p;
+    });
+
+    hipStream_t  s   = stream.get();
+    const size_t row = static_cast<size_t>(nsc) * sizeof(uint32_t);
+    tb_buf.reserve(std::max<size_t>(tbs.size(), 16));
+    std::memcpy(tb_buf.host(), tbs.data(), tbs.size());
+    tb_buf.upload(0, tbs.size(), s);
+    if (cw_bytes > d_cw_cap) {
+      (void)hipFree(d_cw);
+      d_cw     = nullptr;
+      d_cw_cap = 0;
+      hip_check(hipMalloc(&d_cw, cw_bytes), WHO, "codewords");
+      d_cw_cap = cw_bytes;
+    }
+    // Sentinel scratch grid: exactly the REs the PDSCH and its DM-RS map come back.
+    grid_buf.reserve(P * 14 * row);
+    hip_check(hipMemsetAsync(grid_buf.dev(), 0xff, P * 14 * row, s), WHO, "scratch");
+    srsgpu_check(srsgpu_pdsch_encoder_plan_execute(enc, tb_buf.dev<uint8_t>(), d_cw, s), WHO);
+    srsgpu_check(srsgpu_pdsch_dmrs_plan_execute(dmrs, grid_buf.dev<uint32_t>(), s), WHO);
+    srsgpu_check(srsgpu_pdsch_modulator_plan_execute(mod, d_cw, grid_buf.dev<uint32_t>(), s), WHO);
+    grid_buf.download(0, P * 14 * row, s);
+    hip_check(hipStreamSynchronize(s), WHO, "synchronise");
+    store_written_res(grid, grid_buf.host<uint32_t>(), P, nsc, 0, 14);
+    for (pdsch_entry& e : es) {
+      e.notifier->on_finish_processing();
+    }
+  }
+
+private:
+  std::shared_ptr<srsgpu_context>       owner;
+  srsgpu_context*                       ctx;
+  std::unique_ptr<ptrs_pdsch_generator> ptrs;
+  std::unique_ptr<pdsch_processor>      fallback;
+  owned_stream                          stream;
+  plan_cache<srsgpu_pdsch_encoder_plan>   enc_plans;
+  plan_cache<srsgpu_pdsch_modulator_plan> mod_plans;
+  plan_cache<srsgpu_pdsch_dmrs_plan>      dmrs_plans;
+  staged_buffer                         tb_buf;
+  staged_buffer                         grid_buf;
+  uint8_t*                              d_cw     = nullptr;
+  size_t                                d_cw_cap = 0;
+  std::mutex                            mtx;
+  std::vector<pdsch_entry>              entries;
+  std::vector<uint8_t>                  tb_bytes;
+  unsigned                              cw_total = 0;
+  std::mutex                            run_mtx;
+};
+
+std::shared_ptr<pdsch_slot_batch> create_pdsch_slot_batch(int                                   device,
+                                                          std::unique_ptr<ptrs_pdsch_generator> ptrs,
+                                                          std::unique_ptr<pdsch_processor>      fallback)
+{
+  return std::make_shared<pdsch_slot_batch>(device, std::move(ptrs), std::move(fallback));
+}
+
+namespace {
+
+class pdsch_processor_batch_gpu : public pdsch_processor
+{
+public:
+  explicit pdsch_processor_batch_gpu(std::shared_ptr<pdsch_slot_batch> batch_) : batch(std::move(batch_)) {}
+
+  void process(resource_grid_writer&                                           grid,
+               pdsch_processor_notifier&                                       notifier,
+               static_vector<shared_transport_block, MAX_NOF_TRANSPORT_BLOCKS> data,
+               const pdu_t&                                                    pdu) override
+  {
+    batch->add(grid, notifier, std::move(data), pdu);
+  }
+
+private:
+  std::shared_ptr<pdsch_slot_batch> batch;
+};
+
+/// The reference's downlink processor with the slot's PDSCHs recorded inline and run as one batch at the end.
+class downlink_processor_batch_gpu : public downlink_processor_base,
+                                     private downlink_processor_controller,
+                                     private unique_downlink_processor::downlink_processor_callback
+{
+public:
+  downlink_processor_batch_gpu(std::unique_ptr<downlink_processor_base> inner_,
+                               std::shared_ptr<pdsch_slot_batch>        batch_,
+                               task_executor&                           executor_) :
+    inner(std::move(inner_)), batch(std::move(batch_)), executor(executor_)
+  {
+  }
+
+  downlink_processor_controller& get_controller() override { return *this; }
+  void                           stop() override { inner->stop(); }
+
+private:
+  unique_downlink_processor configure_resource_grid(const resource_grid_context& context,
+                                                    shared_resource_grid         grid) override
+  {
+    current = inner->get_controller().configure_resource_grid(context, std::move(grid));
+    if (!current.is_valid()) {
+      return {};
+    }
+    return unique_downlink_processor(*this);
+  }
+
+  void process_pdcch(const pdcch_processor::pdu_t& pdu) override { current->process_pdcch(pdu); }
+  void process_ssb(const ssb_processor::pdu_t& pdu) override { current->process_ssb(pdu); }
+  void process_nzp_csi_rs(const nzp_csi_rs_generator::config_t& config) override
+  {
+    current->process_nzp_csi_rs(config);
+  }
+  void process_prs(const prs_generator_configuration& config) override { current->process_prs(config); }
+
+  void process_pdsch(static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data,
+                     const pdsch_processor::pdu_t&                                                    pdu) override
+  {
+    // The reference enqueues the PDSCH task on its executor (pdsch_batch_executor): within this scope it runs here,
+    // and the batch pdsch_processor records the transmission.
+    pdsch_inline_scope = true;
+    current->process_pdsch(std::move(data), pdu);
+    pdsch_inline_scope = false;
+  }
+
+  void finish_processing_pdus() override
+  {
+    // The reference's state machine sends the grid once every task, including the batched PDSCHs, has completed.
+    unique_downlink_processor         proc = std::move(current);
+    std::shared_ptr<pdsch_slot_batch> b    = batch;
+    if (!executor.execute([b]() { b->flush(); })) {
+      b->flush();
+    }
+    proc.release();
+  }
+
+  std::unique_ptr<downlink_processor_base> inner;
+  std::shared_ptr<pdsch_slot_batch>        batch;
+  task_executor&                           executor;
+  unique_downlink_processor                current;
+};
+
+} // namespace
+
+bool pdsch_batch_executor::execute(unique_task task)
+{
+  if (pdsch_inline_scope) {
+    task();
+    return true;
+  }
+  return real.execute(std::move(task));
+}
+
+bool pdsch_batch_executor::defer(unique_task task)
+{
+  if (pdsch_inline_scope) {
+    task();
+    return true;
+  }
+  return real.defer(std::move(task));
+}
+
+std::unique_ptr<pdsch_processor> create_pdsch_processor_batch_gpu(std::shared_ptr<pdsch_slot_batch> batch)
+{
+  return std::make_unique<pdsch_processor_batch_gpu>(std::move(batch));
+}
+
+std::unique_ptr<downlink_processor_base> create_downlink_processor_batch_gpu(std::unique_ptr<downlink_processor_base> inner,
+                                                                             std::shared_ptr<pdsch_slot_batch> batch,
+                                                                             task_executor&                    executor)
+{
+  return std::make_unique<downlink_processor_batch_gpu>(std::move(inner), std::move(batch), executor);
+}
+
+} // namespace gpu
+} // namespace srsran

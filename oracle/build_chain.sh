@@ -46,6 +46,15 @@ SRCS=(
   "$REF/lib/phy/lower/processors/downlink/pdxch/pdxch_processor_impl.cpp"
   "$REF/lib/phy/lower/processors/uplink/puxch/puxch_processor_impl.cpp"
   "$REF/lib/instrumentation/traces/du_traces.cpp"
+  "$ROOT/integration/upper_phy_gpu.cpp"
+  "$U/uplink_processor_impl.cpp"
+  "$U/downlink_processor_single_executor_impl.cpp"
+  "$U/rx_buffer_pool_impl.cpp"
+  "$REF/lib/srslog/srslog.cpp"
+  "$REF/lib/srslog/backend_worker.cpp"
+  "$REF/lib/srslog/event_trace.cpp"
+  "$REF/lib/srslog/formatters/text_formatter.cpp"
+  "$REF/lib/srslog/formatters/json_formatter.cpp"
   "$HERE/ref/ref_chain.cpp"
   "$HERE/ref/ref_lower.cpp"
 )

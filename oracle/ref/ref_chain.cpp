@@ -12,6 +12,7 @@
 // PDSCH ones (TS 38.211 6.3.1.1 / 7.3.1.1, 6.4.1.1.1 / 7.4.1.1.1).
 #include "hw_accelerator_pusch_dec_gpu.h"
 #include "signal_chain_gpu.h"
+#include "upper_phy_gpu.h"
 
 #include "srsran/phy/support/resource_grid_reader.h"
 #include "srsran/phy/support/resource_grid_writer.h"
@@ -63,6 +64,16 @@
 #include "lib/phy/upper/signal_processors/dmrs_pusch_estimator_impl.h"
 #include "lib/phy/upper/signal_processors/port_channel_estimator_average_impl.h"
 #include "lib/phy/upper/signal_processors/ptrs/ptrs_pdsch_generator_impl.h"
+#include "lib/phy/upper/downlink_processor_single_executor_impl.h"
+#include "lib/phy/upper/uplink_processor_impl.h"
+#include "srsran/phy/upper/rx_buffer_pool.h"
+#include "srsran/phy/upper/upper_phy_rg_gateway.h"
+#include "srsran/phy/upper/upper_phy_rx_results_notifier.h"
+#include "srsran/phy/upper/channel_processors/pdcch/pdcch_processor.h"
+#include "srsran/phy/upper/channel_processors/ssb/ssb_processor.h"
+#include "srsran/phy/upper/signal_processors/nzp_csi_rs_generator.h"
+#include "srsran/phy/upper/signal_processors/prs/prs_generator.h"
+#include "srsran/srslog/srslog.h"
 
 #include <cmath>
 #include <cstdio>
@@ -996,6 +1007,406 @@ int chain_pdsch_bench(int device, int mode, const chain_params* c, const float* 
 {
   return guarded("chain_pdsch_bench", [&] {
     return chain_pdsch_bench_impl(device, mode, c, weights, tb_bytes, nof_threads, batch, repetitions, seconds);
+  });
+}
+
+} // extern "C"
+
+// ---------------------------------------------------------------------------------------------------------------------
+// Upper-PHY slot processors (row b6): the reference's own uplink_processor_impl and
+// downlink_processor_single_executor_impl, once over the reference's CPU channel processors and once over the GPU slot
+// batches of integration/upper_phy_gpu.cpp, fed the same slots (tests/test_upper_phy_gpu.py).
+// ---------------------------------------------------------------------------------------------------------------------
+
+namespace {
+
+/// Runs every task on the caller (deterministic test order).
+class inline_test_executor : public task_executor
+{
+public:
+  bool execute(unique_task task) override
+  {
+    task();
+    return true;
+  }
+  bool defer(unique_task task) override
+  {
+    task();
+    return true;
+  }
+};
+
+inline_test_executor& test_executor()
+{
+  static inline_test_executor e;
+  return e;
+}
+
+// Channel processors the tests never drive (the reference's uplink / downlink processors require valid instances).
+class stub_prach : public prach_detector
+{
+public:
+  prach_detection_result detect(const prach_buffer&, const configuration&) override { return {}; }
+};
+class stub_pucch : public pucch_processor
+{
+public:
+  pucch_processor_result process(const resource_grid_reader&, const format0_configuration&) override { return {}; }
+  const pucch_format1_map<pucch_processor_result>& process(const resource_grid_reader&,
+                                                           const format1_batch_configuration&) override
+  {
+    return f1;
+  }
+  pucch_processor_result process(const resource_grid_reader&, const format2_configuration&) override { return {}; }
+  pucch_processor_result process(const resource_grid_reader&, const format3_configuration&) override { return {}; }
+  pucch_processor_result process(const resource_grid_reader&, const format4_configuration&) override { return {}; }
+
+private:
+  pucch_format1_map<pucch_processor_result> f1;
+};
+class stub_srs : public srs_estimator
+{
+public:
+  srs_estimator_result estimate(const resource_grid_reader&, const srs_estimator_configuration&) override
+  {
+    return {};
+  }
+};
+class stub_pdcch : public pdcch_processor
+{
+public:
+  void process(resource_grid_writer&, const pdu_t&) override {}
+};
+class stub_ssb : public ssb_processor
+{
+public:
+  void process(resource_grid_writer&, const pdu_t&) override {}
+};
+class stub_csi_rs : public nzp_csi_rs_generator
+{
+public:
+  void map(resource_grid_writer&, const config_t&) override {}
+};
+class stub_prs : public prs_generator
+{
+public:
+  void generate(resource_grid_writer&, const prs_generator_configuration&) override {}
+};
+
+class demux_factory_ref : public ulsch_demultiplex_factory
+{
+public:
+  std::unique_ptr<ulsch_demultiplex> create() override { return std::make_unique<ulsch_demultiplex_impl>(); }
+};
+class uci_factory_ref : public uci_decoder_factory
+{
+public:
+  std::unique_ptr<uci_decoder> create() override { return cpu_uci_decoder(); }
+};
+
+/// PUSCH results as the upper PHY's notifier receives them, in arrival order.
+struct ul_record {
+  int                  rnti, harq_id, crc_ok, nof_cbs, ldpc_obs, ldpc_min, ldpc_max;
+  float                ldpc_mean, sinr, evm, ta, cfo, epre, rsrp;
+  std::vector<uint8_t> payload;
+};
+
+class ul_results_recorder : public upper_phy_rx_results_notifier
+{
+public:
+  void on_new_prach_results(const ul_prach_results&) override {}
+  void on_new_pusch_results_control(const ul_pusch_results_control&) override { ++nof_control; }
+  void on_new_pusch_results_data(const ul_pusch_results_data& r) override
+  {
+    ul_record x;
+    x.rnti    = static_cast<int>(r.rnti);
+    x.harq_id = static_cast<int>(r.harq_id);
+    x.crc_ok  = r.decoder_result.tb_crc_ok ? 1 : 0;
+    x.nof_cbs = static_cast<int>(r.decoder_result.nof_codeblocks_total);
+    const auto& st = r.decoder_result.ldpc_decoder_stats;
+    x.ldpc_obs     = static_cast<int>(st.get_nof_observations());
+    x.ldpc_min     = st.get_nof_observations() ? static_cast<int>(st.get_min()) : -1;
+    x.ldpc_max     = st.get_nof_observations() ? static_cast<int>(st.get_max()) : -1;
+    x.ldpc_mean    = st.get_nof_observations() ? st.get_mean() : NAN;
+    auto opt       = [](std::optional<float> v) { return v.has_value() ? *v : NAN; };
+    x.sinr         = opt(r.csi.get_sinr_dB());
+    x.evm          = opt(r.csi.get_total_evm());
+    x.ta   = r.csi.get_time_alignment().has_value() ? static_cast<float>(r.csi.get_time_alignment()->to_seconds()) : NAN;
+    x.cfo  = opt(r.csi.get_cfo_Hz());
+    x.epre = opt(r.csi.get_epre_dB());
+    x.rsrp = opt(r.csi.get_rsrp_dB());
+    x.payload.assign(r.payload.begin(), r.payload.end());
+    records.push_back(std::move(x));
+  }
+  void on_new_pucch_results(const ul_pucch_results&) override {}
+  void on_new_srs_results(const ul_srs_results&) override {}
+
+  std::vector<ul_record> records;
+  unsigned               nof_control = 0;
+};
+
+/// The reference's uplink_processor_impl over CPU processors (variant 0) or the GPU slot batch (variant 1).
+struct ul_harness {
+  unsigned                                   P, nsc, grid_prb;
+  std::unique_ptr<rx_buffer_pool_controller> pool;
+  ul_results_recorder                        notifier;
+  std::unique_ptr<uplink_processor>          proc;
+};
+
+ul_harness* ul_create(int device, int variant, unsigned P, unsigned grid_prb, unsigned max_iter)
+{
+  auto* h     = new ul_harness();
+  h->P        = P;
+  h->grid_prb = grid_prb;
+  h->nsc      = 12 * grid_prb;
+  rx_buffer_pool_config pc;
+  pc.max_codeblock_size   = ldpc::MAX_CODEBLOCK_SIZE;
+  pc.nof_buffers          = 256;
+  pc.nof_codeblocks       = 2048;
+  pc.expire_timeout_slots = 100;
+  pc.external_soft_bits   = false;  // the fallback processor (CPU decoder) keeps its soft bits in the buffers
+  h->pool                 = create_rx_buffer_pool(pc);
+
+  std::unique_ptr<pusch_processor> pusch;
+  std::shared_ptr<gpu::pusch_slot_batch> batch;
+  if (variant == 0) {
+    pusch = new_pusch_processor(device, 0, port_channel_estimator_td_interpolation_strategy::average, max_iter, true, {});
+  } else {
+    gpu::pusch_batch_configuration bc;
+    bc.device              = device;
+    bc.estimator           = gpu::make_pusch_estimator_options(port_channel_estimator_fd_smoothing_strategy::filter,
+                                                     port_channel_estimator_td_interpolation_strategy::average, true);
+    bc.max_cb_ids          = pc.nof_codeblocks;
+    bc.nof_ldpc_iterations = max_iter;
+    // PDUs outside the batch: the reference processor over the GPU estimator / demodulator (row b3).
+    auto fallback = new_pusch_processor(device, 1, port_channel_estimator_td_interpolation_strategy::average, max_iter,
+                                        true, {});
+    batch = gpu::create_pusch_slot_batch(bc, gpu::create_pusch_harq_arena(device, bc.max_cb_ids),
+                                         std::make_shared<demux_factory_ref>(), std::make_shared<uci_factory_ref>(),
+                                         std::move(fallback));
+    pusch = gpu::create_pusch_processor_batch_gpu(batch);
+  }
+  uplink_processor_impl::task_executor_collection execs{test_executor(),
+                                                        variant == 0 ? static_cast<task_executor&>(test_executor())
+                                                                     : gpu::pusch_inline_executor(),
+                                                        test_executor(),
+                                                        test_executor()};
+  auto impl = std::make_unique<uplink_processor_impl>(std::make_unique<stub_prach>(),
+                                                      std::move(pusch),
+                                                      std::make_unique<stub_pucch>(),
+                                                      std::make_unique<stub_srs>(),
+                                                      std::make_unique<resource_grid_impl>(P, 14, h->nsc),
+                                                      execs,
+                                                      h->pool->get_pool(),
+                                                      h->notifier,
+                                                      grid_prb,
+                                                      4);
+  if (variant == 0) {
+    h->proc = std::move(impl);
+  } else {
+    h->proc = gpu::create_uplink_processor_batch_gpu(std::move(impl), batch, test_executor());
+  }
+  return h;
+}
+
+/// PDSCH through the reference's downlink processor: the grid it sends.
+class grid_capture : public upper_phy_rg_gateway
+{
+public:
+  void send(const resource_grid_context&, shared_resource_grid grid) override
+  {
+    if (out != nullptr) {
+      store_grid(grid.get(), out, P, nsc);
+    }
+    sent = true;
+  }
+  uint16_t* out  = nullptr;
+  unsigned  P    = 0;
+  unsigned  nsc  = 0;
+  bool      sent = false;
+};
+
+class one_grid_pool : public shared_resource_grid::pool_interface
+{
+public:
+  one_grid_pool(unsigned P, unsigned nsc) : grid(P, 14, nsc) {}
+  resource_grid& get(unsigned) override { return grid; }
+  void           notify_release_scope(unsigned) override {}
+  shared_resource_grid grab()
+  {
+    count = 1;
+    return shared_resource_grid(*this, count, 0);
+  }
+  resource_grid_impl    grid;
+  std::atomic<unsigned> count{0};
+};
+
+struct dl_harness {
+  unsigned                                  P, nsc;
+  grid_capture                              gateway;
+  std::unique_ptr<one_grid_pool>            pool;
+  std::unique_ptr<gpu::pdsch_batch_executor> exec;
+  std::unique_ptr<downlink_processor_base>  proc;
+};
+
+dl_harness* dl_create(int device, int variant, unsigned P, unsigned grid_prb)
+{
+  auto* h = new dl_harness();
+  h->P    = P;
+  h->nsc  = 12 * grid_prb;
+  h->pool = std::make_unique<one_grid_pool>(P, h->nsc);
+  std::unique_ptr<pdsch_processor>        pdsch;
+  std::shared_ptr<gpu::pdsch_slot_batch> batch;
+  task_executor*                          exec = &test_executor();
+  if (variant == 0) {
+    pdsch = new_pdsch_processor(device, 0);
+  } else {
+    batch = gpu::create_pdsch_slot_batch(
+        device,
+        std::make_unique<ptrs_pdsch_generator_generic_impl>(std::make_unique<pseudo_random_generator_impl>(),
+                                                            cpu_mapper()),
+        new_pdsch_processor(device, 1));
+    pdsch   = gpu::create_pdsch_processor_batch_gpu(batch);
+    h->exec = std::make_unique<gpu::pdsch_batch_executor>(test_executor());
+    exec    = h->exec.get();
+  }
+  auto impl = std::make_unique<downlink_processor_single_executor_impl>(h->gateway,
+                                                                       std::make_unique<stub_pdcch>(),
+                                                                       std::move(pdsch),
+                                                                       std::make_unique<stub_ssb>(),
+                                                                       std::make_unique<stub_csi_rs>(),
+                                                                       std::make_unique<stub_prs>(),
+                                                                       *exec,
+                                                                       srslog::fetch_basic_logger("PHY", true));
+  if (variant == 0) {
+    h->proc = std::move(impl);
+  } else {
+    h->proc = gpu::create_downlink_processor_batch_gpu(std::move(impl), batch, test_executor());
+  }
+  return h;
+}
+
+} // namespace
+
+extern "C" {
+
+void* chain_ul_create(int device, int variant, unsigned nof_ports, unsigned grid_prb, unsigned max_iter)
+{
+  void* h = nullptr;
+  guarded("chain_ul_create", [&] {
+    h = ul_create(device, variant, nof_ports, grid_prb, max_iter);
+    return 0;
+  });
+  return h;
+}
+
+void chain_ul_destroy(void* p)
+{
+  delete static_cast<ul_harness*>(p);
+}
+
+/// One UL slot: the PUSCH PDUs (tb_bytes[i] each) registered in the reference's PDU repository, the received grid
+/// (nof_ports, 14, 12 grid_prb) bf16 pairs written into the processor's grid, then handle_rx_symbol(13). Results in
+/// notification order: ints [rnti, harq, crc_ok, nof_cbs, ldpc_obs, ldpc_min, ldpc_max], floats [ldpc_mean, sinr, evm,
+/// ta, cfo, epre, rsrp], payload bytes at tb_out + i * tb_stride. Returns the number of results (< 0 on error).
+int chain_ul_slot(void*               p,
+                  unsigned            slot,
+                  int                 nof_pdus,
+                  const chain_params* pdus,
+                  const int*          tb_bytes,
+                  const uint16_t*     grid_in,
+                  int*                out_i,
+                  float*              out_f,
+                  uint8_t*            tb_out,
+                  int                 tb_stride)
+{
+  return guarded("chain_ul_slot", [&] {
+    auto*            h  = static_cast<ul_harness*>(p);
+    const slot_point sp(subcarrier_spacing::kHz30, slot);
+    h->notifier.records.clear();
+    unique_uplink_pdu_slot_repository repo = h->proc->get_pdu_slot_repository(sp);
+    if (!repo.is_valid()) {
+      return -2;
+    }
+    for (int i = 0; i != nof_pdus; ++i) {
+      chain_params c = pdus[i];
+      c.slot         = static_cast<int>(slot);
+      uplink_pdu_slot_repository::pusch_pdu pdu{static_cast<unsigned>(c.harq_id),
+                                                units::bytes(static_cast<unsigned>(tb_bytes[i])),
+                                                make_pusch_pdu(c)};
+      repo->add_pusch_pdu(pdu);
+    }
+    shared_resource_grid grid = repo.release();
+    load_grid(grid.get(), grid_in, h->P, h->nsc);
+    grid.release();
+    h->proc->get_slot_processor(sp).handle_rx_symbol(13);
+    const auto& recs = h->notifier.records;
+    for (size_t i = 0; i != recs.size(); ++i) {
+      const ul_record& r = recs[i];
+      int*             oi = out_i + 7 * i;
+      float*           of = out_f + 7 * i;
+      oi[0] = r.rnti, oi[1] = r.harq_id, oi[2] = r.crc_ok, oi[3] = r.nof_cbs, oi[4] = r.ldpc_obs, oi[5] = r.ldpc_min;
+      oi[6] = r.ldpc_max;
+      of[0] = r.ldpc_mean, of[1] = r.sinr, of[2] = r.evm, of[3] = r.ta, of[4] = r.cfo, of[5] = r.epre, of[6] = r.rsrp;
+      std::memcpy(tb_out + i * tb_stride, r.payload.data(), std::min<size_t>(r.payload.size(), tb_stride));
+    }
+    return static_cast<int>(recs.size());
+  });
+}
+
+void* chain_dl_create(int device, int variant, unsigned nof_ports, unsigned grid_prb)
+{
+  void* h = nullptr;
+  guarded("chain_dl_create", [&] {
+    h = dl_create(device, variant, nof_ports, grid_prb);
+    return 0;
+  });
+  return h;
+}
+
+void chain_dl_destroy(void* p)
+{
+  delete static_cast<dl_harness*>(p);
+}
+
+/// One DL slot: the grid is loaded with grid_inout (the content of other channels, kept where no PDSCH maps), the
+/// reference's downlink processor configured with it, every PDSCH PDU processed (weights: nof_ports x nof_layers complex
+/// per PDU, consecutive; TBs consecutive, tb_bytes[i] each), finish_processing_pdus; grid_inout receives the grid the
+/// processor sent. Returns 0 when the grid was sent.
+int chain_dl_slot(void*               p,
+                  unsigned            slot,
+                  int                 nof_pdus,
+                  const chain_params* pdus,
+                  const float*        weights,
+                  const uint8_t*      tbs,
+                  const int*          tb_bytes,
+                  uint16_t*           grid_inout)
+{
+  return guarded("chain_dl_slot", [&] {
+    auto* h = static_cast<dl_harness*>(p);
+    load_grid(h->pool->grid, grid_inout, h->P, h->nsc);
+    h->gateway.out  = grid_inout;
+    h->gateway.P    = h->P;
+    h->gateway.nsc  = h->nsc;
+    h->gateway.sent = false;
+    const slot_point          sp(subcarrier_spacing::kHz30, slot);
+    unique_downlink_processor dl = h->proc->get_controller().configure_resource_grid({sp, 0}, h->pool->grab());
+    if (!dl.is_valid()) {
+      return -2;
+    }
+    const uint8_t* tb = tbs;
+    const float*   w  = weights;
+    for (int i = 0; i != nof_pdus; ++i) {
+      chain_params c = pdus[i];
+      c.slot         = static_cast<int>(slot);
+      static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data;
+      data.emplace_back(span<const uint8_t>(tb, static_cast<size_t>(tb_bytes[i])));
+      dl->process_pdsch(std::move(data), make_pdsch_pdu(c, w));
+      tb += tb_bytes[i];
+      w += 2 * c.nof_ports * c.nof_layers;
+    }
+    dl.release();
+    return h->gateway.sent ? 0 : -3;
   });
 }
 

@@ -1,0 +1,61 @@
+// HARQ soft-buffer transfers between a persistent per-codeblock arena and a slot batch's contiguous HARQ buffer
+// (srsgpu_harq_copy, include/srsgpu_phy.h). The reference keeps each codeblock's soft bits in the rx buffer pool,
+// addressed by its absolute codeblock identifier (rx_buffer.h:65 get_absolute_codeblock_id, :72
+// get_codeblock_soft_bits), across slots; a batched PUSCH decoder plan addresses them contiguously per transport
+// block. One workgroup per codeblock, 16-byte vector copies (every offset and length is a multiple of 16 for the LDPC
+// lengths N = 64 Z / 48 Z at even Z; a byte loop otherwise). HBM-bound: 2 bytes moved per soft bit.
+#include "srsgpu_internal.h"
+#include "capi_internal.h"
+
+namespace {
+
+__global__ void __launch_bounds__(256) harq_copy_kernel(int8_t* __restrict__ arena,
+                                                        uint32_t arena_stride,
+                                                        int8_t* __restrict__ batch,
+                                                        const srsgpu_harq_copy_job* __restrict__ jobs,
+                                                        int to_arena)
+{
+  const srsgpu_harq_copy_job j = jobs[blockIdx.x];
+  int8_t*       a   = arena + static_cast<size_t>(j.slot) * arena_stride;
+  int8_t*       b   = batch + j.batch_offset;
+  const int8_t* src = to_arena ? b : a;
+  int8_t*       dst = to_arena ? a : b;
+  const bool    vec = ((j.batch_offset | j.bytes | arena_stride) & 15u) == 0;
+  if (vec) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4*       d4 = reinterpret_cast<uint4*>(dst);
+    for (uint32_t i = threadIdx.x; i < j.bytes / 16u; i += blockDim.x) {
+      d4[i] = s4[i];
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < j.bytes; i += blockDim.x) {
+      dst[i] = src[i];
+    }
+  }
+}
+
+} // namespace
+
+extern "C" int srsgpu_harq_copy(srsgpu_context*             ctx,
+                                int                         direction,
+                                int8_t*                     d_arena,
+                                uint32_t                    arena_stride,
+                                int8_t*                     d_batch,
+                                const srsgpu_harq_copy_job* d_jobs,
+                                uint32_t                    nof_jobs,
+                                void*                       stream)
+{
+  if (ctx == nullptr || d_arena == nullptr || d_batch == nullptr || (d_jobs == nullptr && nof_jobs > 0) ||
+      (direction != SRSGPU_HARQ_TO_BATCH && direction != SRSGPU_HARQ_TO_ARENA)) {
+    return srsgpu::fail(SRSGPU_ERR_INVALID_ARG, "srsgpu_harq_copy: invalid argument");
+  }
+  if (nof_jobs == 0) {
+    return SRSGPU_OK;
+  }
+  harq_copy_kernel<<<nof_jobs, 256, 0, static_cast<hipStream_t>(stream)>>>(
+      d_arena, arena_stride, d_batch, d_jobs, direction == SRSGPU_HARQ_TO_ARENA ? 1 : 0);
+  if (hipGetLastError() != hipSuccess) {
+    return srsgpu::fail(SRSGPU_ERR_HIP, "srsgpu_harq_copy: launch failed");
+  }
+  return SRSGPU_OK;
+}

@@ -415,7 +415,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_pdsch_encoder_plan_stage_times", "srsgpu_pdsch_modulator_plan_create",
     "srsgpu_pdsch_modulator_plan_create_ex", "srsgpu_pdsch_modulator_plan_execute", "srsgpu_pdsch_modulator_plan_destroy",
     "srsgpu_ofdm_modulator_plan_create", "srsgpu_ofdm_demodulator_plan_create", "srsgpu_ofdm_plan_nof_samples",
-    "srsgpu_ofdm_modulator_symbols_plan_create", "srsgpu_ofdm_demodulator_symbols_plan_create",
+    "srsgpu_ofdm_modulator_symbols_plan_create", "srsgpu_ofdm_demodulator_symbols_plan_create", "srsgpu_harq_copy",
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",

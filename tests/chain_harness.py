@@ -108,3 +108,70 @@ class Chain:
         assert self.lib.chain_ofdm_demodulate(self.h, mode, numerology, bw_rb, dft_size, scale, center_freq_hz,
                                               window_offset, slot, _ptr(x), x.size, _ptr(g)) == 0
         return g
+
+
+UL_INTS = ("rnti", "harq_id", "tb_crc_ok", "nof_cbs", "ldpc_obs", "ldpc_min", "ldpc_max")
+UL_FLOATS = ("ldpc_mean", "sinr_db", "evm", "ta_s", "cfo_hz", "epre_db", "rsrp_db")
+UL_CPU, UL_GPU_BATCH = 0, 1
+DL_CPU, DL_GPU_BATCH = 0, 1
+
+
+class UpperPhy:
+    """The reference's own upper-PHY slot processors (uplink_processor_impl, downlink_processor_single_executor_impl)
+    over the reference's CPU channel processors (variant 0) or the GPU slot batches of integration/upper_phy_gpu.cpp
+    (variant 1): chain_ul_* / chain_dl_* of oracle/ref/ref_chain.cpp. TEST INFRASTRUCTURE ONLY."""
+
+    def __init__(self, device, variant, nof_ports, grid_prb=273, max_iter=6, path=CHAIN_SO):
+        self.lib = ctypes.CDLL(path)
+        L = self.lib
+        PP = ctypes.POINTER(ChainParams)
+        L.chain_ul_create.restype = _P
+        L.chain_ul_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]
+        L.chain_ul_destroy.argtypes = [_P]
+        L.chain_ul_slot.restype = ctypes.c_int
+        L.chain_ul_slot.argtypes = [_P, ctypes.c_uint, ctypes.c_int, PP, _P, _P, _P, _P, _P, ctypes.c_int]
+        L.chain_dl_create.restype = _P
+        L.chain_dl_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_uint]
+        L.chain_dl_destroy.argtypes = [_P]
+        L.chain_dl_slot.restype = ctypes.c_int
+        L.chain_dl_slot.argtypes = [_P, ctypes.c_uint, ctypes.c_int, PP, _P, _P, _P, _P]
+        self.P, self.grid_prb = nof_ports, grid_prb
+        self.ul = L.chain_ul_create(device, variant, nof_ports, grid_prb, max_iter)
+        self.dl = L.chain_dl_create(device, variant, nof_ports, grid_prb)
+        assert self.ul and self.dl
+
+    def close(self):
+        if self.ul:
+            self.lib.chain_ul_destroy(self.ul)
+            self.lib.chain_dl_destroy(self.dl)
+            self.ul = self.dl = None
+
+    def ul_slot(self, slot, pdus, tb_bytes, grid):
+        """One UL slot: [(result dict, payload bytes)] in notification order."""
+        arr = (ChainParams * len(pdus))(*pdus)
+        tbb = np.ascontiguousarray(tb_bytes, np.int32)
+        g = np.ascontiguousarray(grid, np.uint16)
+        n = len(pdus)
+        oi = np.zeros((n, 7), np.int32)
+        of = np.zeros((n, 7), np.float32)
+        stride = int(max(tb_bytes)) if n else 1
+        tbs = np.zeros((n, stride), np.uint8)
+        r = self.lib.chain_ul_slot(self.ul, slot, n, arr, _ptr(tbb), _ptr(g), _ptr(oi), _ptr(of), _ptr(tbs), stride)
+        assert r >= 0, r
+        out = []
+        for i in range(r):
+            d = dict(zip(UL_INTS, oi[i].tolist()))
+            d.update(zip(UL_FLOATS, of[i].tolist()))
+            out.append((d, tbs[i]))
+        return out
+
+    def dl_slot(self, slot, pdus, weights, tbs, grid):
+        """One DL slot into a copy of `grid` (the other channels' content): the grid the processor sent."""
+        arr = (ChainParams * len(pdus))(*pdus)
+        w = np.ascontiguousarray(np.concatenate([np.asarray(x, np.complex64).ravel() for x in weights]),
+                                 np.complex64).view(np.float32)
+        tb = np.ascontiguousarray(np.concatenate(tbs), np.uint8)
+        tbb = np.array([t.size for t in tbs], np.int32)
+        g = np.array(grid, np.uint16, copy=True, order="C")
+        assert self.lib.chain_dl_slot(self.dl, slot, len(pdus), arr, _ptr(w), _ptr(tb), _ptr(tbb), _ptr(g)) == 0
+        return g

@@ -1,0 +1,187 @@
+"""Upper-PHY slot processors on the GPU (row b6): the reference's OWN uplink_processor_impl and
+downlink_processor_single_executor_impl (compiled from its sources by oracle/build_chain.sh) run once over the
+reference's CPU channel processors and once over the GPU slot batches of integration/upper_phy_gpu.cpp, which gather
+a slot's PUSCH / PDSCH PDUs into one launch sequence (tests/chain_harness.py: UpperPhy).
+
+  * UL: multi-UE slots (different sizes, modulations, CFOs, delays, SNRs, one UE over the DC subcarrier, one with
+    HARQ-ACK on PUSCH, which the batch hands to its fallback processor) registered in the reference's PDU repository;
+    handle_rx_symbol(13). Then a second slot with retransmissions (rv 2, new_data = false) of the first slot's failed
+    TBs combined with the soft bits the batch kept in HBM (arena slots = the rx buffer pool's absolute codeblock
+    identifiers), plus new UEs. Equal per (RNTI, HARQ id): TB CRC, payload, number of codeblocks; within the
+    tolerances of tests/test_chain_gpu.py (the GPU LLRs equal the reference's or differ by one quantisation step):
+    LDPC mean iterations +-0.5, SINR 0.1 dB, EVM 2e-3, TA 2 Tc, CFO 0.05 Hz, EPRE / RSRP 0.01 dB.
+  * DL: a slot of PDSCHs (1-4 layers on 4 ports, random precoding, 64 / 256QAM) into a grid that already holds other
+    channels' content: the grid the reference's processor sends is bit-exact with the CPU processors' one.
+"""
+import numpy as np
+import pytest
+
+from ofdm_oracle import bf16_to_complex
+from pusch_demod_cases import bf16
+from srsgpu import sch
+
+pytestmark = pytest.mark.gpu
+
+T_C = 1.0 / (480000 * 4096)
+P = 4
+
+
+@pytest.fixture(scope="module")
+def procs():
+    import chain_harness as H
+    cpu = H.UpperPhy(0, H.UL_CPU, P)
+    gpu = H.UpperPhy(0, H.UL_GPU_BATCH, P)
+    yield cpu, gpu
+    cpu.close()
+    gpu.close()
+
+
+def grant(p):
+    nd = bin(p.dmrs_mask).count("1")
+    return sch.UeGrant(p.nof_rb, p.nof_layers, p.qm, p.target_code_rate, nof_symb_sh=p.nof_symbols,
+                       nof_dmrs_symbols=nd)
+
+
+def received_grid(rng, chain, ues, tbs, snr_db):
+    """Every UE's transmission (the reference's transmitter, chain_ue_tx) through its own random flat channel per rx
+    port, delay and CFO, summed, plus AWGN: (P, 14, nsc, 2) bf16."""
+    import pusch_chest_oracle as C
+    nsc = 12 * 273
+    y = np.zeros((P, 14, nsc), np.complex128)
+    k = np.arange(nsc)
+    ep = C.symbol_start_epochs(1)
+    for (p, cfo, delay, gain_db), tb in zip(ues, tbs):
+        x = bf16_to_complex(chain.ue_tx(p, tb))
+        g = (rng.normal(size=(P, p.nof_layers)) + 1j * rng.normal(size=(P, p.nof_layers))) / np.sqrt(2 * p.nof_layers)
+        g *= 10 ** (gain_db / 20)
+        ramp = np.exp(-2j * np.pi * k * delay / 4096)
+        yu = np.einsum("pl,lsk->psk", g, x) * ramp[None, None, :]
+        yu *= np.exp(2j * np.pi * cfo / 30000.0 * ep)[None, :, None]
+        y += yu
+    nv = 10 ** (-snr_db / 10)
+    y += (rng.normal(size=y.shape) + 1j * rng.normal(size=y.shape)) * np.sqrt(nv / 2)
+    return bf16(y)
+
+
+def check_equal(ref, got, what):
+    assert len(ref) == len(got), what
+    rk = {(d["rnti"], d["harq_id"]): (d, tb) for d, tb in ref}
+    gk = {(d["rnti"], d["harq_id"]): (d, tb) for d, tb in got}
+    assert rk.keys() == gk.keys(), what
+    for key, (r, tbr) in rk.items():
+        g, tbg = gk[key]
+        w = (what, key)
+        assert g["tb_crc_ok"] == r["tb_crc_ok"], (w, r, g)
+        assert g["nof_cbs"] == r["nof_cbs"], w
+        if r["tb_crc_ok"]:
+            assert np.array_equal(tbg, tbr), w
+        if r["ldpc_obs"] > 0:
+            assert abs(g["ldpc_mean"] - r["ldpc_mean"]) <= 0.5, (w, r["ldpc_mean"], g["ldpc_mean"])
+        assert abs(g["sinr_db"] - r["sinr_db"]) < 0.1, (w, r["sinr_db"], g["sinr_db"])
+        assert abs(g["evm"] - r["evm"]) < 2e-3, (w, r["evm"], g["evm"])
+        assert abs(g["ta_s"] - r["ta_s"]) <= 2 * T_C, (w, r["ta_s"], g["ta_s"])
+        if not np.isnan(r["cfo_hz"]):
+            assert abs(g["cfo_hz"] - r["cfo_hz"]) < 0.05, (w, r["cfo_hz"], g["cfo_hz"])
+        assert abs(g["epre_db"] - r["epre_db"]) < 0.01 and abs(g["rsrp_db"] - r["rsrp_db"]) < 0.01, (w, r, g)
+
+
+def ul_ues(rng, H, start_rnti, n, harq0, low_snr=()):
+    """n UEs side by side from RB 0: (params, CFO Hz, delay samples, gain dB)."""
+    out, rb = [], 0
+    for i in range(n):
+        nrb = int(rng.choice([4, 5, 8, 12, 17]))
+        qm, rate = [(8, 948.0), (6, 772.0), (4, 616.0), (2, 308.0)][i % 4]
+        p = H.params(rnti=start_rnti + i, harq_id=harq0 + i, nof_rb=nrb, rb_start=rb, qm=qm, target_code_rate=rate,
+                     nof_ports=P)
+        rb += nrb
+        gain = -22.0 if i in low_snr else 0.0
+        out.append((p, float(rng.uniform(-250, 250)), float(rng.uniform(-3, 3)), gain))
+    return out, rb
+
+
+def test_uplink_processor_gpu_batch_equals_reference(procs):
+    import chain_harness as H
+    cpu, gpu = procs
+    chain = H.Chain(0)
+    try:
+        rng = np.random.default_rng(2024)
+        ues, rb = ul_ues(rng, H, 0x4601, 14, 0, low_snr=(4, 9))
+        # A UE over the DC subcarrier (its estimate is zeroed there) and one with HARQ-ACK (the batch's fallback).
+        dc = H.params(rnti=0x4700, harq_id=20, nof_rb=10, rb_start=rb, qm=6, target_code_rate=772.0, nof_ports=P,
+                      dc_position=12 * (rb + 4) + 6)
+        ack = H.params(rnti=0x4701, harq_id=21, nof_rb=8, rb_start=rb + 10, qm=4, target_code_rate=616.0, nof_ports=P,
+                       nof_harq_ack=2)
+        ues += [(dc, 50.0, 1.0, 0.0), (ack, -90.0, 0.0, 0.0)]
+        tbs, sizes = [], []
+        for p, *_ in ues:
+            seg = grant(p).segmentation()
+            p.base_graph = seg.base_graph
+            tbs.append(rng.integers(0, 256, seg.tbs // 8).astype(np.uint8))
+            sizes.append(seg.tbs // 8)
+        grid = received_grid(rng, chain, ues, tbs, 28.0)
+        pdus = [p for p, *_ in ues]
+        ref = cpu.ul_slot(7, pdus, sizes, grid)
+        got = gpu.ul_slot(7, pdus, sizes, grid)
+        check_equal(ref, got, "slot 7")
+        ok = {d["rnti"]: d["tb_crc_ok"] for d, _ in ref}
+        data_ok = [ok[p.rnti] for p, *_ in ues if p.nof_harq_ack == 0]
+        assert sum(data_ok) == len(data_ok) - 2, ok  # every UE decodes but the two faded ones
+        for (p, *_), tb in zip(ues, tbs):
+            if ok[p.rnti] and p.nof_harq_ack == 0:
+                got_tb = next(t for d, t in got if d["rnti"] == p.rnti)
+                assert np.array_equal(got_tb[: tb.size], tb)
+
+        # Slot 8: the failed TBs again as rv 2 (combined with the kept soft bits) next to new UEs.
+        retx = [(u, tb) for u, tb in zip(ues, tbs) if not ok[u[0].rnti] and u[0].nof_harq_ack == 0]
+        ues2, tbs2 = [], []
+        rb = 0
+        for (p, cfo, delay, gain), tb in retx:
+            q = H.params(**{f: getattr(p, f) for f, _ in H.ChainParams._fields_})
+            q.rv, q.new_data, q.rb_start = 2, 0, rb
+            rb += q.nof_rb
+            ues2.append((q, cfo, delay, 0.0))
+            tbs2.append(tb)
+        new, _ = ul_ues(rng, H, 0x4800, 6, 40)
+        for p, cfo, delay, gain in new:
+            p.rb_start += rb
+            seg = grant(p).segmentation()
+            p.base_graph = seg.base_graph
+            ues2.append((p, cfo, delay, gain))
+            tbs2.append(rng.integers(0, 256, seg.tbs // 8).astype(np.uint8))
+        grid2 = received_grid(rng, chain, ues2, tbs2, 28.0)
+        pdus2 = [p for p, *_ in ues2]
+        sizes2 = [t.size for t in tbs2]
+        ref2 = cpu.ul_slot(8, pdus2, sizes2, grid2)
+        got2 = gpu.ul_slot(8, pdus2, sizes2, grid2)
+        check_equal(ref2, got2, "slot 8")
+        ok2 = {d["rnti"]: d["tb_crc_ok"] for d, _ in ref2}
+        assert all(ok2[p.rnti] for (p, *_), _ in retx), ok2  # the retransmissions decode after combining
+    finally:
+        chain.close()
+
+
+def test_downlink_processor_gpu_batch_equals_reference(procs):
+    import chain_harness as H
+    cpu, gpu = procs
+    rng = np.random.default_rng(77)
+    pdus, weights, tbs, rb = [], [], [], 0
+    for i in range(10):
+        L = int(rng.integers(1, 5))
+        nrb = int(rng.choice([6, 9, 16, 25]))
+        qm, rate = [(8, 948.0), (6, 772.0)][i % 2]
+        p = H.params(rnti=0x5000 + i, nof_rb=nrb, rb_start=rb, qm=qm, target_code_rate=rate, nof_layers=L,
+                     nof_ports=P, start_symbol=2, nof_symbols=12, dmrs_mask=(1 << 2) | (1 << 11))
+        rb += nrb
+        seg = grant(p).segmentation()
+        p.base_graph = seg.base_graph
+        pdus.append(p)
+        w = (rng.normal(size=(P, L)) + 1j * rng.normal(size=(P, L))) / np.sqrt(2 * L)
+        weights.append(w.astype(np.complex64))
+        tbs.append(rng.integers(0, 256, seg.tbs // 8).astype(np.uint8))
+    other = bf16((rng.normal(size=(P, 14, 12 * 273)) + 1j * rng.normal(size=(P, 14, 12 * 273))) * 0.1)
+    for slot in (3, 4):
+        ref = cpu.dl_slot(slot, pdus, weights, tbs, other)
+        got = gpu.dl_slot(slot, pdus, weights, tbs, other)
+        assert np.array_equal(ref, got), (slot, int(np.sum(np.any(ref != got, axis=-1))))
+        assert np.mean(np.any(ref != other, axis=-1)) > 0.3  # the PDSCHs were written
+        assert np.array_equal(ref[:, :2], other[:, :2])  # symbols 0-1 (another channel's) untouched

@@ -18,6 +18,7 @@
 #include "srsran/phy/upper/rx_buffer.h"
 #include "srsran/phy/upper/unique_rx_buffer.h"
 #include "srsran/phy/upper/uplink_slot_processor.h"
+#include "srsran/ran/pusch/ulsch_info.h"
 #include "srsran/ran/sch/sch_dmrs_power.h"
 
 #include <array>
@@ -99,6 +100,9 @@ struct pusch_entry {
   unsigned cb_N       = 0;
   unsigned cb_KZ      = 0;
   bool     new_data   = true;
+  int      demux_index  = -1;  ///< UCI on PUSCH: the transmission's entry in the demultiplexer plan.
+  unsigned sch_offset   = 0;   ///< First UL-SCH LLR the decoder reads.
+  unsigned nof_sch_llrs = 0;
 };
 
 /// Replay stages: the reference's pusch_processor_impl runs per PDU on the batch's results.
@@ -254,6 +258,7 @@ public:
     chest_plans(srsgpu_pusch_chest_plan_destroy, 16),
     demod_plans(srsgpu_pusch_demodulator_plan_destroy, 16),
     dec_plans(srsgpu_pusch_decoder_plan_destroy, 16),
+    demux_plans(srsgpu_ulsch_demux_plan_destroy, 16),
     grid_buf(WHO),
     out_buf(WHO),
     flag_buf(WHO),
@@ -288,12 +293,14 @@ public:
   void run(std::vector<pusch_entry>& entries);
 
 private:
-  /// PDUs the batch covers: SCH data without UCI, identity rx port list, up to four layers.
+  /// PDUs the batch covers: SCH data (with or without HARQ-ACK / CSI Part 1 on PUSCH), identity rx port list, up to
+  /// four layers. CSI Part 2 needs the decoded CSI Part 1 before the UL-SCH bits are known
+  /// (pusch_processor_impl.cpp:60-100), so those PDUs go to the fallback processor.
   static bool batchable(const pusch_entry& e)
   {
     const pusch_processor::pdu_t& pdu = e.pdu;
-    if (!pdu.codeword.has_value() || pdu.uci.nof_harq_ack != 0 || pdu.uci.nof_csi_part1 != 0 ||
-        !pdu.uci.csi_part2_size.entries.empty() || pdu.nof_tx_layers == 0 || pdu.nof_tx_layers > 4 ||
+    if (!pdu.codeword.has_value() || !pdu.uci.csi_part2_size.entries.empty() || pdu.nof_tx_layers == 0 ||
+        pdu.nof_tx_layers > 4 ||
         pdu.rx_ports.empty() || pdu.rx_ports.size() > 4 || pdu.cp != cyclic_prefix::NORMAL) {
       return false;
     }
@@ -330,6 +337,7 @@ private:
   plan_cache<srsgpu_pusch_chest_plan>           chest_plans;
   plan_cache<srsgpu_pusch_demodulator_plan>     demod_plans;
   plan_cache<srsgpu_pusch_decoder_plan>         dec_plans;
+  plan_cache<srsgpu_ulsch_demux_plan>           demux_plans;
   staged_buffer                                 grid_buf;  ///< Rx grid [port][symbol][subcarrier].
   staged_buffer                                 out_buf;   ///< nv, metrics, statistics, LLRs, scrambling words.
   staged_buffer                                 flag_buf;  ///< CB CRC flags, iterations, TB CRC flags.
@@ -410,7 +418,8 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
   std::vector<pusch_demod_desc>       demods;
   std::vector<srsgpu_pusch_tb_config> tbs;
   std::vector<srsgpu_harq_copy_job>   jobs;
-  std::vector<uint8_t>                chest_key, demod_key, dec_key;
+  std::vector<srsgpu_ulsch_demux_config> demuxes;
+  std::vector<uint8_t>                chest_key, demod_key, dec_key, demux_key;
   unsigned                            llr_total = 0, cb_total = 0, tb_total = 0, harq_total = 0;
   gpu::key_append(chest_key, grid_prb);
   gpu::key_append(demod_key, grid_prb);
@@ -480,6 +489,58 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     llr_total += (e.nof_llrs + 63) / 64 * 64;
     dd.append_key(demod_key);
 
+    // UCI on PUSCH (pusch_processor_impl.cpp:180-202, 244-262): the UL-SCH LLRs are the demultiplexer's SCH stream,
+    // written after the codewords (the reference's own demultiplexer splits the UCI LLRs again during the replay).
+    unsigned nof_sch_llrs = e.nof_llrs;
+    e.sch_offset          = e.llr_offset;
+    if (pdu.uci.nof_harq_ack != 0 || pdu.uci.nof_csi_part1 != 0) {
+      bool overlap_dc = false;
+      if (pdu.dc_position.has_value()) {
+        overlap_dc = rb_mask.test(*pdu.dc_position / NRE);
+      }
+      ulsch_configuration uc;
+      uc.tbs                         = units::bytes(e.data.size()).to_bits();
+      uc.mcs_descr                   = pdu.mcs_descr;
+      uc.nof_harq_ack_bits           = units::bits(pdu.uci.nof_harq_ack);
+      uc.nof_csi_part1_bits          = units::bits(pdu.uci.nof_csi_part1);
+      uc.nof_csi_part2_bits          = units::bits(0);
+      uc.alpha_scaling               = pdu.uci.alpha_scaling;
+      uc.beta_offset_harq_ack        = pdu.uci.beta_offset_harq_ack;
+      uc.beta_offset_csi_part1       = pdu.uci.beta_offset_csi_part1;
+      uc.beta_offset_csi_part2       = pdu.uci.beta_offset_csi_part2;
+      uc.nof_rb                      = e.nof_rb;
+      uc.start_symbol_index          = pdu.start_symbol_index;
+      uc.nof_symbols                 = pdu.nof_symbols;
+      uc.dmrs_type                   = dmrs == dmrs_type::TYPE1 ? dmrs_config_type::type1 : dmrs_config_type::type2;
+      uc.dmrs_symbol_mask            = pdu.dmrs_symbol_mask;
+      uc.nof_cdm_groups_without_data = cdm_groups;
+      uc.nof_layers                  = pdu.nof_tx_layers;
+      uc.contains_dc                 = overlap_dc;
+      const ulsch_information info   = get_ulsch_information(uc);
+      srsgpu_ulsch_demux_config d;
+      std::memset(&d, 0, sizeof(d));
+      d.modulation_order            = static_cast<uint8_t>(dd.qm);
+      d.nof_layers                  = static_cast<uint8_t>(pdu.nof_tx_layers);
+      d.nof_prb                     = static_cast<uint16_t>(e.nof_rb);
+      d.start_symbol                = static_cast<uint8_t>(pdu.start_symbol_index);
+      d.nof_symbols                 = static_cast<uint8_t>(pdu.nof_symbols);
+      d.dmrs_symbol_mask            = symbol_mask_bits(pdu.dmrs_symbol_mask);
+      d.dmrs_type                   = dmrs == dmrs_type::TYPE1 ? 1 : 2;
+      d.nof_cdm_groups_without_data = static_cast<uint8_t>(cdm_groups);
+      d.rnti                        = pdu.rnti;
+      d.n_id                        = static_cast<uint16_t>(pdu.n_id);
+      d.nof_harq_ack_rvd            = info.nof_harq_ack_rvd.value();
+      d.nof_harq_ack_bits           = pdu.uci.nof_harq_ack;
+      d.nof_enc_harq_ack_bits       = info.nof_harq_ack_bits.value();
+      d.nof_csi_part1_bits          = pdu.uci.nof_csi_part1;
+      d.nof_enc_csi_part1_bits      = info.nof_csi_part1_bits.value();
+      d.llr_offset                  = e.llr_offset;
+      demuxes.push_back(d);  // sch_offset set once the codeword region's size is known
+      e.demux_index = static_cast<int>(demuxes.size()) - 1;
+      nof_sch_llrs  = info.nof_ul_sch_bits.value();
+    }
+    e.nof_sch_llrs = nof_sch_llrs;
+
     // TB decoding (pusch_processor_impl.cpp:278-296).
     const units::bits tb_bits = units::bytes(e.data.size()).to_bits();
     const auto        bg      = pdu.codeword->ldpc_base_graph;
@@ -500,7 +561,7 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     t.max_iterations   = static_cast<uint8_t>(cfg.nof_ldpc_iterations);
     t.scaling_factor   = 0.8F;  // ldpc_decoder::configuration::algorithm_details default (ldpc_decoder.h:50)
     t.tbs_bytes        = static_cast<uint32_t>(e.data.size());
-    t.nof_ch_symbols   = e.nof_llrs / dd.qm;
+    t.nof_ch_symbols   = nof_sch_llrs / dd.qm;
     t.Nref             = ldpc::compute_N_ref(pdu.tbs_lbrm, e.nof_cbs).value();
     t.llr_offset       = e.llr_offset;
     t.harq_offset      = e.harq0;
@@ -521,6 +582,22 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     harq_total += e.nof_cbs * e.cb_N;
   }
   const unsigned n = batch.size();
+  // UL-SCH streams of the UCI transmissions: after the codewords in the same LLR buffer.
+  for (pusch_entry* ep : batch) {
+    if (ep->demux_index >= 0) {
+      srsgpu_ulsch_demux_config& d = demuxes[static_cast<size_t>(ep->demux_index)];
+      d.sch_offset                 = llr_total;
+      ep->sch_offset               = llr_total;
+      llr_total += (ep->nof_sch_llrs + 63) / 64 * 64;
+      gpu::key_append(demux_key, d);
+      gpu::key_append(dec_key, d.sch_offset);
+      for (srsgpu_pusch_tb_config& t : tbs) {
+        if (t.cb_offset == ep->cb0) {
+          t.llr_offset = ep->sch_offset;
+        }
+      }
+    }
+  }
 
   // Plans (cached: a cell's grants repeat).
   srsgpu_pusch_chest_plan* chest = chest_plans.get(chest_key, [&] {
@@ -545,6 +622,14 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     srsgpu_check(srsgpu_pusch_demodulator_plan_create_ex(ctx, c.data(), x.data(), n, grid_prb, P, &p), WHO);
     return p;
   });
+  srsgpu_ulsch_demux_plan* demux = nullptr;
+  if (!demuxes.empty()) {
+    demux = demux_plans.get(demux_key, [&] {
+      srsgpu_ulsch_demux_plan* p = nullptr;
+      srsgpu_check(srsgpu_ulsch_demux_plan_create(ctx, demuxes.data(), demuxes.size(), &p), WHO);
+      return p;
+    });
+  }
   srsgpu_pusch_decoder_plan* dec = dec_plans.get(dec_key, [&] {
     srsgpu_pusch_decoder_plan* p = nullptr;
     srsgpu_check(srsgpu_pusch_decoder_plan_create(ctx, SRSGPU_LDPC_IMPL_SIMD, tbs.data(), n, &p), WHO);
@@ -602,6 +687,13 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
                WHO);
   for (unsigned i = 0; i != n; ++i) {
     srsgpu_check(srsgpu_pusch_demodulator_plan_scrambling(demod, i, out_buf.dev<uint32_t>(seq_off[i]), s), WHO);
+  }
+  if (demux != nullptr) {
+    // Only the UL-SCH stream is needed on the device: the UCI streams are split again by the reference's own
+    // demultiplexer during the replay, from the codeword LLRs.
+    srsgpu_check(srsgpu_ulsch_demux_plan_execute(demux, out_buf.dev<int8_t>(llr_off), out_buf.dev<int8_t>(llr_off),
+                                                 nullptr, nullptr, nullptr, s),
+                 WHO);
   }
 
   // HARQ context: soft bits from the arena, CB CRC flags (and the messages of CBs that already passed) from the rx

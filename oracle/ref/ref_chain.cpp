@@ -1410,4 +1410,161 @@ int chain_dl_slot(void*               p,
   });
 }
 
+
+/// Slot-processor throughput (the reference's pusch_processor_benchmark / pdsch_processor_benchmark "throughput total"
+/// scheme, at the granularity du_low drives: one uplink / downlink processor per thread, each running slots of
+/// `nof_pdus` PDUs through the reference's uplink_processor_impl / downlink_processor_single_executor_impl, variant 0 =
+/// reference CPU processors, 1 = GPU slot batches). seconds[r] = wall time of repetition r, in which every thread runs
+/// `slots` slots. Returns the number of TB CRC passes of the last repetition (UL) or 0 (DL).
+int chain_ul_bench(int                 device,
+                   int                 variant,
+                   unsigned            nof_threads,
+                   unsigned            slots,
+                   unsigned            repetitions,
+                   int                 nof_pdus,
+                   const chain_params* pdus,
+                   const int*          tb_bytes,
+                   const uint16_t*     grid_in,
+                   unsigned            nof_ports,
+                   unsigned            grid_prb,
+                   double*             seconds)
+{
+  return guarded("chain_ul_bench", [&] {
+    std::vector<std::unique_ptr<bench_worker>> workers;
+    std::vector<ul_harness*>                   hs(nof_threads, nullptr);
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      workers.push_back(std::make_unique<bench_worker>());
+    }
+    // Each worker builds its processor on its own thread (thread-local dependency pools bind there).
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      workers[t]->post([&, t] { hs[t] = ul_create(device, variant, nof_ports, grid_prb, 2); });
+    }
+    for (auto& w : workers) {
+      w->wait();
+    }
+    const unsigned         nsc = 12 * grid_prb;
+    std::atomic<int>       ok{0};
+    std::vector<unsigned>  slot_no(nof_threads, 0);
+    auto                   run_slots = [&](unsigned t, unsigned n) {
+      ul_harness* h = hs[t];
+      for (unsigned i = 0; i != n; ++i) {
+        const slot_point sp(subcarrier_spacing::kHz30, slot_no[t]++ % 20480);
+        h->notifier.records.clear();
+        unique_uplink_pdu_slot_repository repo = h->proc->get_pdu_slot_repository(sp);
+        for (int k = 0; k != nof_pdus; ++k) {
+          chain_params c = pdus[k];
+          c.slot         = static_cast<int>(sp.slot_index());
+          repo->add_pusch_pdu({static_cast<unsigned>(c.harq_id), units::bytes(static_cast<unsigned>(tb_bytes[k])),
+                               make_pusch_pdu(c)});
+        }
+        shared_resource_grid g = repo.release();
+        for (unsigned p = 0; p != nof_ports; ++p) {
+          for (unsigned l = 0; l != 14; ++l) {
+            std::memcpy(g.get().get_writer().get_view(p, l).data(),
+                        grid_in + 2 * (static_cast<size_t>(p) * 14 + l) * nsc, nsc * sizeof(cbf16_t));
+          }
+        }
+        g.release();
+        h->proc->get_slot_processor(sp).handle_rx_symbol(13);
+        for (const ul_record& r : h->notifier.records) {
+          ok += r.crc_ok;
+        }
+      }
+    };
+    for (unsigned t = 0; t != nof_threads; ++t) {  // warm-up: plans, pools, first-touch
+      workers[t]->post([&, t] { run_slots(t, 2); });
+    }
+    for (auto& w : workers) {
+      w->wait();
+    }
+    for (unsigned r = 0; r != repetitions; ++r) {
+      ok              = 0;
+      const auto t0   = std::chrono::steady_clock::now();
+      for (unsigned t = 0; t != nof_threads; ++t) {
+        workers[t]->post([&, t] { run_slots(t, slots); });
+      }
+      for (auto& w : workers) {
+        w->wait();
+      }
+      seconds[r] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      workers[t]->post([&, t] { delete hs[t]; });
+      workers[t]->wait();
+    }
+    return ok.load();
+  });
+}
+
+int chain_dl_bench(int                 device,
+                   int                 variant,
+                   unsigned            nof_threads,
+                   unsigned            slots,
+                   unsigned            repetitions,
+                   int                 nof_pdus,
+                   const chain_params* pdus,
+                   const float*        weights,
+                   const uint8_t*      tbs,
+                   const int*          tb_bytes,
+                   unsigned            nof_ports,
+                   unsigned            grid_prb,
+                   double*             seconds)
+{
+  return guarded("chain_dl_bench", [&] {
+    std::vector<std::unique_ptr<bench_worker>> workers;
+    std::vector<dl_harness*>                   hs(nof_threads, nullptr);
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      workers.push_back(std::make_unique<bench_worker>());
+    }
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      workers[t]->post([&, t] { hs[t] = dl_create(device, variant, nof_ports, grid_prb); });
+    }
+    for (auto& w : workers) {
+      w->wait();
+    }
+    std::vector<unsigned> slot_no(nof_threads, 0);
+    auto                  run_slots = [&](unsigned t, unsigned n) {
+      dl_harness* h = hs[t];
+      h->gateway.out = nullptr;
+      for (unsigned i = 0; i != n; ++i) {
+        const slot_point          sp(subcarrier_spacing::kHz30, slot_no[t]++ % 20480);
+        unique_downlink_processor dl = h->proc->get_controller().configure_resource_grid({sp, 0}, h->pool->grab());
+        const uint8_t*            tb = tbs;
+        const float*              w  = weights;
+        for (int k = 0; k != nof_pdus; ++k) {
+          chain_params c = pdus[k];
+          c.slot         = static_cast<int>(sp.slot_index());
+          static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data;
+          data.emplace_back(span<const uint8_t>(tb, static_cast<size_t>(tb_bytes[k])));
+          dl->process_pdsch(std::move(data), make_pdsch_pdu(c, w));
+          tb += tb_bytes[k];
+          w += 2 * c.nof_ports * c.nof_layers;
+        }
+        dl.release();
+      }
+    };
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      workers[t]->post([&, t] { run_slots(t, 2); });
+    }
+    for (auto& w : workers) {
+      w->wait();
+    }
+    for (unsigned r = 0; r != repetitions; ++r) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (unsigned t = 0; t != nof_threads; ++t) {
+        workers[t]->post([&, t] { run_slots(t, slots); });
+      }
+      for (auto& w : workers) {
+        w->wait();
+      }
+      seconds[r] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      workers[t]->post([&, t] { delete hs[t]; });
+      workers[t]->wait();
+    }
+    return 0;
+  });
+}
+
 } // extern "C"

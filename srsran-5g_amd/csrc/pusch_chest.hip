@@ -47,14 +47,46 @@ __device__ __forceinline__ uint32_t to_bf16c(cpx v)
   return bf16_bits(v.x) | (bf16_bits(v.y) << 16);
 }
 
+// Cross-lane reductions on DPP (VALU lane permutations: no LDS round trip, which __shfl_xor's ds_bpermute costs per
+// step). Within a 16-lane row: quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror, after which every
+// lane of the row holds the row's result (each step pairs lanes symmetrically, so all lanes compute identical bits).
+// Across rows: row_bcast:15 into rows 1 and 3 (the 32-lane halves: lanes 31 / 63 hold them) and row_bcast:31 into
+// rows 2 and 3 (lane 63 holds the wave's), read back with readlane.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_f(float old, float v)
+{
+  return __int_as_float(
+      __builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROW_MASK, 0xf, false));
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ int dpp_i(int old, int v)
+{
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW_MASK, 0xf, false);
+}
+constexpr int DPP_XOR1 = 0xb1, DPP_XOR2 = 0x4e, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+constexpr int DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143;
+
+__device__ __forceinline__ float row_sum(float v)
+{
+  v += dpp_f<DPP_XOR1>(0.f, v);
+  v += dpp_f<DPP_XOR2>(0.f, v);
+  v += dpp_f<DPP_HALF_MIRROR>(0.f, v);
+  v += dpp_f<DPP_MIRROR>(0.f, v);
+  return v;
+}
+
+__device__ __forceinline__ float readlane_f(float v, int lane)
+{
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
 /// Sum over the wavefront (every lane gets the result).
 __device__ __forceinline__ float wave_sum(float v)
 {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    v += __shfl_xor(v, o);
-  }
-  return v;
+  v = row_sum(v);
+  v += dpp_f<DPP_BCAST15, 0xa>(0.f, v);
+  v += dpp_f<DPP_BCAST31, 0xc>(0.f, v);
+  return readlane_f(v, 63);
 }
 
 /// Sum over the workgroup of T lanes (every lane gets the result; all lanes must call it). T = 64: wave shuffles only.
@@ -77,15 +109,22 @@ __device__ __forceinline__ float block_sum(float v, float* red)
   return v;
 }
 
-/// Sum over an aligned group of TS lanes (TS <= 64, every lane of the group gets the result).
+/// Sum over an aligned group of TS lanes (TS = 16, 32 or 64, every lane of the group gets the result).
 template <int TS>
 __device__ __forceinline__ float sub_sum(float v)
 {
-#pragma unroll
-  for (int o = TS / 2; o > 0; o >>= 1) {
-    v += __shfl_xor(v, o, TS);
+  static_assert(TS == 16 || TS == 32 || TS == 64, "row, half-wave or wave");
+  if constexpr (TS == 64) {
+    return wave_sum(v);
+  } else {
+    v = row_sum(v);
+    if constexpr (TS == 32) {
+      v += dpp_f<DPP_BCAST15, 0xa>(0.f, v);
+      const float lo = readlane_f(v, 31), hi = readlane_f(v, 63);
+      v              = (threadIdx.x & 32u) ? hi : lo;
+    }
+    return v;
   }
-  return v;
 }
 
 /// Sum over one job's lanes: TS < 64 lanes of a wave that holds several jobs, or the whole workgroup.
@@ -143,12 +182,20 @@ __device__ __forceinline__ void virtual_pilots(cpx* E, int N, int nv, int sub)
   const float a    = atan2f(b.y, b.x);
   // Unwrap: arg_j + 2 pi c_j with c_j = sum_{m <= j} rint((a_{m-1} - a_m) / 2 pi) (prefix sum within the half).
   const float twopi = 6.28318531f;
-  const float prev  = __shfl_up(a, 1, H);
-  float       c     = (j > 0 && act) ? rintf((prev - a) / twopi) : 0.f;
-#pragma unroll
-  for (int o = 1; o < H; o <<= 1) {
-    const float t = __shfl_up(c, o, H);
-    c += (j >= o) ? t : 0.f;
+  // Lane j - 1: row_shr:1 inside a row, row_bcast:15 for a row's first lane (H = 32: lane 16 of each half).
+  const float prev_row = dpp_f<0x111>(a, a);
+  const float prev_bc  = dpp_f<DPP_BCAST15, 0xa>(a, a);
+  const float prev     = ((sub & 15) == 0) ? prev_bc : prev_row;
+  float       c        = (j > 0 && act) ? rintf((prev - a) / twopi) : 0.f;
+  // Inclusive prefix sum within the H lanes: row_shr:1 / 2 / 4 / 8 (lanes shifted in from outside the row add 0),
+  // then for H = 32 the first row's total into the second row (row_bcast:15).
+  c += dpp_f<0x111>(0.f, c);
+  c += dpp_f<0x112>(0.f, c);
+  c += dpp_f<0x114>(0.f, c);
+  c += dpp_f<0x118>(0.f, c);
+  static_assert(H == 16 || H == 32, "one row or two rows per band edge");
+  if constexpr (H == 32) {
+    c += dpp_f<DPP_BCAST15, 0xa>(0.f, c);
   }
   const float ar        = act ? a + twopi * c : 0.f;
   const float n         = static_cast<float>(nv);
@@ -220,32 +267,50 @@ __device__ __forceinline__ cpx dmrs_value(const chest_job& jb, const float2* __r
   return pilot(seq, W, s, n0, m);
 }
 
-/// Maximum over the wavefront with the lowest index among equal values (srsvec::max_element keeps the first maximum).
-__device__ __forceinline__ void wave_argmax(float& v, int& idx)
+/// One argmax step against the (value, index) DPP delivers (rows outside ROW_MASK compare with themselves): the larger
+/// value, the lower index among equal values (srsvec::max_element keeps the first maximum).
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ void argmax_step(float& v, int& idx)
 {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(v, o);
-    const int   oi = __shfl_xor(idx, o);
-    if (ov > v || (ov == v && oi < idx)) {
-      v   = ov;
-      idx = oi;
-    }
+  const float ov = dpp_f<CTRL, ROW_MASK>(v, v);
+  const int   oi = dpp_i<CTRL, ROW_MASK>(idx, idx);
+  if (ov > v || (ov == v && oi < idx)) {
+    v   = ov;
+    idx = oi;
   }
 }
 
-/// wave_argmax over an aligned group of TS < 64 lanes.
+__device__ __forceinline__ void row_argmax(float& v, int& idx)
+{
+  argmax_step<DPP_XOR1>(v, idx);
+  argmax_step<DPP_XOR2>(v, idx);
+  argmax_step<DPP_HALF_MIRROR>(v, idx);
+  argmax_step<DPP_MIRROR>(v, idx);
+}
+
+/// Maximum over the wavefront with the lowest index among equal values.
+__device__ __forceinline__ void wave_argmax(float& v, int& idx)
+{
+  row_argmax(v, idx);
+  argmax_step<DPP_BCAST15, 0xa>(v, idx);
+  argmax_step<DPP_BCAST31, 0xc>(v, idx);
+  v   = readlane_f(v, 63);
+  idx = __builtin_amdgcn_readlane(idx, 63);
+}
+
+/// wave_argmax over an aligned group of TS = 16 or 32 lanes.
 template <int TS>
 __device__ __forceinline__ void sub_argmax(float& v, int& idx)
 {
-#pragma unroll
-  for (int o = TS / 2; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(v, o, TS);
-    const int   oi = __shfl_xor(idx, o, TS);
-    if (ov > v || (ov == v && oi < idx)) {
-      v   = ov;
-      idx = oi;
-    }
+  static_assert(TS == 16 || TS == 32, "row or half-wave");
+  row_argmax(v, idx);
+  if constexpr (TS == 32) {
+    argmax_step<DPP_BCAST15, 0xa>(v, idx);
+    const bool hi = (threadIdx.x & 32u) != 0;
+    const float v0 = readlane_f(v, 31), v1 = readlane_f(v, 63);
+    const int   i0 = __builtin_amdgcn_readlane(idx, 31), i1 = __builtin_amdgcn_readlane(idx, 63);
+    v              = hi ? v1 : v0;
+    idx            = hi ? i1 : i0;
   }
 }
 

@@ -397,14 +397,47 @@ __device__ __forceinline__ void load_re(const demod_desc& d,
   }
 }
 
+/// Noise variances (per port and their maximum) and, for compact estimates with CFO compensation, the per (symbol,
+/// layer, port) rotation by the estimator's CFO (float bits next to the compact row). The caller synchronises before
+/// the rotations are read.
+__device__ __forceinline__ void setup_uniform(const demod_desc& d, const uint32_t* __restrict__ ce,
+                                              const float* __restrict__ noise_var, cpx* rot, demod_uniform& u)
+{
+  u.rot = nullptr;
+  if (d.ce_cfo) {
+    for (uint32_t i = threadIdx.x; i < 14u * 16u; i += blockDim.x) {
+      const uint32_t l = i >> 4, ly = (i >> 2) & 3u, p = i & 3u;
+      float          c = 0.f;
+      if (ly < d.L && p < d.P) {
+        c = __uint_as_float(ce[d.ce_base + ly * d.ce_layer_stride + p * d.port_stride + d.nsc + d.cfo_sc]);
+      }
+      float sn, cs;
+      sincosf(6.283185307f * d.epochs[l] * c, &sn, &cs);
+      rot[i] = cmk(cs, sn);
+    }
+    u.rot = rot;
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    u.nv[p] = noise_var[4 * d.tx + p];
+  }
+  u.nv_max = u.nv[0];
+#pragma unroll
+  for (uint32_t p = 1; p < 4; ++p) {
+    u.nv_max = (p < d.P) ? fmaxf(u.nv_max, u.nv[p]) : u.nv_max;
+  }
+}
+
 /// Every RE of the chunk owned by this lane: loads, equalization (L layers), demapping (QM bits per layer),
 /// descrambling and the packed LLR bytes into the LDS output buffer. L and QM are compile-time so that every register
 /// array has static indices and the RE's L * QM bytes are assembled in registers.
 template <int L, int QM, bool STATS>
-__device__ __forceinline__ void demod_res(const demod_uniform& u,
+__device__ __forceinline__ void demod_res(demod_uniform        u,
                                           demap_pair_table*    tab,
                                           const uint32_t* __restrict__ grids,
                                           const uint32_t* __restrict__ ce,
+                                          const float* __restrict__ noise_var,
+                                          cpx*            rot,
                                           uint32_t*       seq,
                                           uint32_t*       out32)
 {
@@ -419,6 +452,9 @@ __device__ __forceinline__ void demod_res(const demod_uniform& u,
     load_re<L>(d, r, grids, ce, u.crbs, yw, hw, sym);
   }
   stage_chunk(u, seq, tab);
+  // The noise variances and CFO rotations are needed from the first equalisation on: their loads follow the RE's and
+  // the sequence's, so the three fly together after the descriptor (chunk -> descriptor -> data, two dependent steps).
+  setup_uniform(d, ce, noise_var, rot, u);
   __syncthreads();
   lane_stats st;
   for (bool first = true; r < u.re_end; r += DEMOD_THREADS, first = false) {
@@ -553,44 +589,14 @@ __device__ __forceinline__ void demod_res(const demod_uniform& u,
 template <int QM, bool STATS>
 __device__ __forceinline__ void demod_res_qm(const demod_uniform& u, demap_pair_table* tab,
                                              const uint32_t* __restrict__ grids, const uint32_t* __restrict__ ce,
-                                             uint32_t* seq, uint32_t* out32)
+                                             const float* __restrict__ noise_var, cpx* rot, uint32_t* seq,
+                                             uint32_t* out32)
 {
   switch (u.d->L) {
-    case 1: demod_res<1, QM, STATS>(u, tab, grids, ce, seq, out32); break;
-    case 2: demod_res<2, QM, STATS>(u, tab, grids, ce, seq, out32); break;
-    case 3: demod_res<3, QM, STATS>(u, tab, grids, ce, seq, out32); break;
-    default: demod_res<4, QM, STATS>(u, tab, grids, ce, seq, out32); break;
-  }
-}
-
-/// Noise variances (per port and their maximum) and, for compact estimates with CFO compensation, the per (symbol,
-/// layer, port) rotation by the estimator's CFO (float bits next to the compact row). The caller synchronises before
-/// the rotations are read.
-__device__ __forceinline__ void setup_uniform(const demod_desc& d, const uint32_t* __restrict__ ce,
-                                              const float* __restrict__ noise_var, cpx* rot, demod_uniform& u)
-{
-  u.rot = nullptr;
-  if (d.ce_cfo) {
-    for (uint32_t i = threadIdx.x; i < 14u * 16u; i += blockDim.x) {
-      const uint32_t l = i >> 4, ly = (i >> 2) & 3u, p = i & 3u;
-      float          c = 0.f;
-      if (ly < d.L && p < d.P) {
-        c = __uint_as_float(ce[d.ce_base + ly * d.ce_layer_stride + p * d.port_stride + d.nsc + d.cfo_sc]);
-      }
-      float sn, cs;
-      sincosf(6.283185307f * d.epochs[l] * c, &sn, &cs);
-      rot[i] = cmk(cs, sn);
-    }
-    u.rot = rot;
-  }
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    u.nv[p] = noise_var[4 * d.tx + p];
-  }
-  u.nv_max = u.nv[0];
-#pragma unroll
-  for (uint32_t p = 1; p < 4; ++p) {
-    u.nv_max = (p < d.P) ? fmaxf(u.nv_max, u.nv[p]) : u.nv_max;
+    case 1: demod_res<1, QM, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    case 2: demod_res<2, QM, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    case 3: demod_res<3, QM, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    default: demod_res<4, QM, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
   }
 }
 
@@ -637,13 +643,12 @@ __global__ __launch_bounds__(DEMOD_THREADS) DEMOD_OCCUPANCY void pusch_demodulat
     }
     u.lacc = lacc;
   }
-  setup_uniform(d, ce, noise_var, rot, u);
 
   switch (d.qm) {
-    case 2: demod_res_qm<2, STATS>(u, tab, grids, ce, seq, out32); break;
-    case 4: demod_res_qm<4, STATS>(u, tab, grids, ce, seq, out32); break;
-    case 6: demod_res_qm<6, STATS>(u, tab, grids, ce, seq, out32); break;
-    default: demod_res_qm<8, STATS>(u, tab, grids, ce, seq, out32); break;
+    case 2: demod_res_qm<2, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    case 4: demod_res_qm<4, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    case 6: demod_res_qm<6, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    default: demod_res_qm<8, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
   }
   __syncthreads();
   if (STATS && tid < static_cast<uint32_t>(DEMOD_ACC_PER_TX) && lacc[tid] != 0.f) {

@@ -3,6 +3,9 @@
 # Builds oracle/_ref/libsrsref.so from the srsRAN reference sources where they lie under /root/reference (nothing is
 # copied into this repository) plus oracle/ref/ref_shim.cpp. Output goes only to oracle/_ref/ (git-ignored, shipped to
 # the GPU box with the snapshot). Skips quietly when the reference tree is absent (GPU box).
+# SRSREF_MARCH=<level> builds a second copy, libsrsref_<level>.so, with every file at -march=<level> (the reference's
+# own CMake builds at -march=native): the reference's floating-point results depend on the ISA it is built for
+# (SIMD widths of its srsvec reductions, FMA contraction), and tests/test_reference_isa_variance.py measures by how much.
 set -euo pipefail
 REF=${SRSRAN_REF:-/root/reference}
 HERE=$(cd "$(dirname "$0")" && pwd)
@@ -11,7 +14,14 @@ if [ ! -d "$REF/lib/phy/upper/channel_coding/ldpc" ]; then
   echo "build_ref: reference tree not present; keeping existing $OUT" >&2
   exit 0
 fi
-mkdir -p "$OUT/obj"
+MARCH=${SRSREF_MARCH:-}
+LIBNAME=libsrsref.so
+OBJDIR="$OUT/obj"
+if [ -n "$MARCH" ]; then
+  LIBNAME=libsrsref_$MARCH.so
+  OBJDIR="$OUT/obj_$MARCH"
+fi
+mkdir -p "$OBJDIR"
 CXX=${CXX:-g++}
 FLAGS="-std=c++17 -O3 -fPIC -DNDEBUG -DFMT_HEADER_ONLY -DASSERTS_ENABLED=0 -I$REF/include -I$REF/external/fmt/include -I$REF/external -I$REF/lib/phy/upper/channel_coding"
 LDPC=$REF/lib/phy/upper/channel_coding/ldpc
@@ -91,7 +101,8 @@ OBJS=()
 pids=()
 for entry in "${SRCS[@]}"; do
   src=${entry%%:*}; extra=${entry#*:}
-  obj="$OUT/obj/$(basename "${src%.cpp}").o"
+  obj="$OBJDIR/$(basename "${src%.cpp}").o"
+  [ -n "$MARCH" ] && extra="$extra -march=$MARCH"
   OBJS+=("$obj")
   if [ ! -f "$obj" ] || [ "$src" -nt "$obj" ] || [ "$0" -nt "$obj" ]; then
     $CXX $FLAGS $extra -c "$src" -o "$obj" &
@@ -101,5 +112,5 @@ done
 rc=0
 for p in "${pids[@]:-}"; do [ -n "$p" ] && { wait "$p" || rc=1; }; done
 [ $rc -eq 0 ] || { echo "build_ref: compilation failed" >&2; exit 1; }
-$CXX -shared -o "$OUT/libsrsref.so" "${OBJS[@]}"
-echo "build_ref: $OUT/libsrsref.so"
+$CXX -shared -o "$OUT/$LIBNAME" "${OBJS[@]}"
+echo "build_ref: $OUT/$LIBNAME"

@@ -24,19 +24,28 @@ struct srsgpu_pusch_chest_plan {
 
 namespace {
 
-/// Raised cosine, roll-off 0.2, 10 samples per symbol, n = 0..30 (t = (n - 15) / 10); the global scale is irrelevant
-/// (the estimator renormalises the taps it uses).
+/// Raised cosine, roll-off 0.2, 10 samples per symbol, n = 0..30 (t = (n - 15) / 10), as the reference tabulates it
+/// (port_channel_estimator_helpers.cpp:51 RC_FILTER): normalised to unit energy and quantised to 7 decimals, so that
+/// the float taps the estimator derives from it are the reference's bit for bit. The reference's table holds
+/// 0.3235207 at n = 14 and 16, one unit of the last decimal below the rounded prototype value (0.32352076).
 double rc_tap(int n)
 {
-  const double t    = (n - 15) / 10.0;
-  const double beta = 0.2;
   const double pi   = 3.14159265358979323846;
-  if (std::abs(std::abs(2 * beta * t) - 1.0) < 1e-12) {
-    const double x = 1 / (2 * beta);
-    return pi / 4 * std::sin(pi * x) / (pi * x);
+  const double beta = 0.2;
+  auto         raw  = [&](int i) {
+    const double t    = (i - 15) / 10.0;
+    const double sinc = (t == 0) ? 1.0 : std::sin(pi * t) / (pi * t);
+    return sinc * std::cos(pi * beta * t) / (1 - (2 * beta * t) * (2 * beta * t));  // |2 beta t| < 1 for i = 0..30
+  };
+  double energy = 0;
+  for (int i = 0; i != 31; ++i) {
+    energy += raw(i) * raw(i);
   }
-  const double sinc = (t == 0) ? 1.0 : std::sin(pi * t) / (pi * t);
-  return sinc * std::cos(pi * beta * t) / (1 - (2 * beta * t) * (2 * beta * t));
+  double q = std::nearbyint(raw(n) / std::sqrt(energy) * 1e7);
+  if (n == 14 || n == 16) {
+    q -= 1;
+  }
+  return q / 1e7;
 }
 
 /// time_alignment_estimator_dft_impl::get_idft (:216): guard-scaled size, next power of two, 128..4096.

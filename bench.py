@@ -197,6 +197,31 @@ def cpu_baseline(dl_ues, dl_segs, ul_ues, ul_segs, tb_host, cw_host, samples_hos
     return base, states[0]["llr"].copy(), states[0]["iters"].copy()
 
 
+def reference_build_spread(ul_ues, samples_host, ul_slot_index, ref_llr):
+    """The reference's own reproducibility on the UL slot of the LLR parity check: the same samples through the
+    reference built at -march=x86-64-v4 (AVX-512; oracle/build_ref.sh SRSREF_MARCH) against its AVX2 + FMA build (the
+    one `cpu_baseline` runs). Its srsvec reductions change order with the SIMD width, so its LLRs move by a few steps
+    between builds (tests/test_reference_isa_variance.py). None when that build or an AVX-512 host is absent."""
+    so = os.path.join(ROOT, "oracle", "_ref", "libsrsref_x86-64-v4.so")
+    if ref_llr is None or not os.path.exists(so):
+        return None
+    lib = ctypes.CDLL(so)
+    if not lib.ref_cpu_has_avx512():
+        return None
+    P = ctypes.c_void_p
+    lib.ref_ul_slot_timed_at.restype = ctypes.c_longlong
+    ul_nrb = np.array([u.n_prb for u in ul_ues], np.int32)
+    ul_rb0 = np.concatenate([[0], np.cumsum(ul_nrb)[:-1]]).astype(np.int32)
+    llr = np.zeros_like(ref_llr)
+    o1, o2 = ctypes.c_longlong(), ctypes.c_longlong()
+    lib.ref_ul_slot_timed_at(len(ul_ues), ul_rb0.ctypes.data_as(P), ul_nrb.ctypes.data_as(P), int(ul_ues[0].qm),
+                             ctypes.c_uint(DMRS_MASK), 1, int(ul_slot_index), samples_host.ctypes.data_as(P),
+                             llr.ctypes.data_as(P), ctypes.byref(o1), ctypes.byref(o2))
+    d = np.abs(llr.astype(np.int16) - ref_llr.astype(np.int16))
+    return {"builds": "reference -march=x86-64-v4 vs its -mavx2 -mfma build", "equal": float(np.mean(d == 0)),
+            "within_one_step": float(np.mean(d <= 1)), "max_diff": int(d.max()), "over_one_step": int(np.sum(d > 1))}
+
+
 class InputSet:
     """One independent copy of a step's working set: DL / UL pipelines (plans + buffers), DL TBs, UL samples and the
     UL TBs the UEs sent. Sets are rotated step by step. `dl_cells`: the DL slot groups of a step (one, or a TDD
@@ -742,7 +767,10 @@ def measure(args, env):
                 "within_one_step": float(np.mean(d <= 1)), "max_diff": int(d.max()),
                 "codeblocks": n_cb0, "gpu_cb_crc_ok": float(gpu_cb_ok.mean()),
                 "reference_cb_crc_ok": float(np.mean(ref_iters >= 0)),
-                "cb_outcome_agreement": float(np.mean(gpu_cb_ok == (ref_iters >= 0)))}
+                "cb_outcome_agreement": float(np.mean(gpu_cb_ok == (ref_iters >= 0))),
+                "over_one_step": int(np.sum(d > 1)),
+                "reference_build_spread": reference_build_spread(ul_ues, samples_host, ul_cell.slot_index(0),
+                                                                 ref_llr)}
     # Release the working sets (graphs first) before another workload is measured in the same process.
     for st in sets:
         st.graph = st.graph_back = st.graph_ul = None

@@ -1,5 +1,6 @@
 // Slot-batched GPU processing behind the reference's upper-PHY slot processors: see upper_phy_gpu.h for the design.
 #include "upper_phy_gpu.h"
+#include "srsran/support/error_handling.h"
 
 #include "chain_convert.h"
 #include "gpu_staging.h"
@@ -582,13 +583,18 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     harq_total += e.nof_cbs * e.cb_N;
   }
   const unsigned n = batch.size();
-  // UL-SCH streams of the UCI transmissions: after the codewords in the same LLR buffer.
+  // UL-SCH streams of the UCI transmissions after the codewords in the same LLR buffer, then their HARQ-ACK and
+  // CSI Part 1 streams (the plan writes every stream it routes; the replay decodes the UCI from the codeword LLRs).
   for (pusch_entry* ep : batch) {
     if (ep->demux_index >= 0) {
       srsgpu_ulsch_demux_config& d = demuxes[static_cast<size_t>(ep->demux_index)];
       d.sch_offset                 = llr_total;
       ep->sch_offset               = llr_total;
       llr_total += (ep->nof_sch_llrs + 63) / 64 * 64;
+      d.harq_offset = llr_total;
+      llr_total += (d.nof_enc_harq_ack_bits + 63) / 64 * 64;
+      d.csi1_offset = llr_total;
+      llr_total += (d.nof_enc_csi_part1_bits + 63) / 64 * 64;
       gpu::key_append(demux_key, d);
       gpu::key_append(dec_key, d.sch_offset);
       for (srsgpu_pusch_tb_config& t : tbs) {
@@ -689,11 +695,10 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     srsgpu_check(srsgpu_pusch_demodulator_plan_scrambling(demod, i, out_buf.dev<uint32_t>(seq_off[i]), s), WHO);
   }
   if (demux != nullptr) {
-    // Only the UL-SCH stream is needed on the device: the UCI streams are split again by the reference's own
+    // Only the UL-SCH stream is used on the device: the UCI streams are split again by the reference's own
     // demultiplexer during the replay, from the codeword LLRs.
-    srsgpu_check(srsgpu_ulsch_demux_plan_execute(demux, out_buf.dev<int8_t>(llr_off), out_buf.dev<int8_t>(llr_off),
-                                                 nullptr, nullptr, nullptr, s),
-                 WHO);
+    int8_t* llr_base = out_buf.dev<int8_t>(llr_off);
+    srsgpu_check(srsgpu_ulsch_demux_plan_execute(demux, llr_base, llr_base, llr_base, llr_base, llr_base, s), WHO);
   }
 
   // HARQ context: soft bits from the arena, CB CRC flags (and the messages of CBs that already passed) from the rx
@@ -895,9 +900,18 @@ private:
     if (entries->empty()) {
       return;
     }
-    std::shared_ptr<pusch_slot_batch> b = batch;
-    if (!executor.execute([b, entries]() { b->run(*entries); })) {
-      b->run(*entries);  // the executor refused the job: run it here rather than lose the PDUs' notifications
+    std::shared_ptr<pusch_slot_batch> b   = batch;
+    auto                              job = [b, entries]() {
+      // A GPU or configuration error leaves the slot's PUSCH results undeliverable: fatal, with its reason, as the
+      // reference's own processors treat failures they cannot notify (error_handling.h report_fatal_error).
+      try {
+        b->run(*entries);
+      } catch (const std::exception& e) {
+        report_fatal_error("pusch_slot_batch: {}", e.what());
+      }
+    };
+    if (!executor.execute(job)) {
+      job();  // the executor refused the job: run it here rather than lose the PDUs' notifications
     }
   }
 
@@ -1235,8 +1249,15 @@ private:
     // The reference's state machine sends the grid once every task, including the batched PDSCHs, has completed.
     unique_downlink_processor         proc = std::move(current);
     std::shared_ptr<pdsch_slot_batch> b    = batch;
-    if (!executor.execute([b]() { b->flush(); })) {
-      b->flush();
+    auto job = [b]() {
+      try {
+        b->flush();
+      } catch (const std::exception& e) {
+        report_fatal_error("pdsch_slot_batch: {}", e.what());  // as the UL batch
+      }
+    };
+    if (!executor.execute(job)) {
+      job();
     }
     proc.release();
   }

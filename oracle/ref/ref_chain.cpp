@@ -1115,7 +1115,18 @@ class ul_results_recorder : public upper_phy_rx_results_notifier
 {
 public:
   void on_new_prach_results(const ul_prach_results&) override {}
-  void on_new_pusch_results_control(const ul_pusch_results_control&) override { ++nof_control; }
+  void on_new_pusch_results_control(const ul_pusch_results_control& r) override
+  {
+    ++nof_control;
+    if (r.harq_ack.has_value()) {
+      // HARQ-ACK on PUSCH: status and payload bits (LSB first) per RNTI.
+      int bits = 0;
+      for (unsigned b = 0; b != r.harq_ack->payload.size() && b < 30; ++b) {
+        bits |= r.harq_ack->payload.test(b) ? (1 << b) : 0;
+      }
+      harq_ack[static_cast<int>(r.rnti)] = {static_cast<int>(r.harq_ack->status), bits};
+    }
+  }
   void on_new_pusch_results_data(const ul_pusch_results_data& r) override
   {
     ul_record x;
@@ -1141,8 +1152,9 @@ public:
   void on_new_pucch_results(const ul_pucch_results&) override {}
   void on_new_srs_results(const ul_srs_results&) override {}
 
-  std::vector<ul_record> records;
-  unsigned               nof_control = 0;
+  std::vector<ul_record>             records;
+  std::map<int, std::pair<int, int>> harq_ack;  ///< RNTI -> (uci_status, payload bits)
+  unsigned                           nof_control = 0;
 };
 
 /// The reference's uplink_processor_impl over CPU processors (variant 0) or the GPU slot batch (variant 1).
@@ -1307,8 +1319,9 @@ void chain_ul_destroy(void* p)
 
 /// One UL slot: the PUSCH PDUs (tb_bytes[i] each) registered in the reference's PDU repository, the received grid
 /// (nof_ports, 14, 12 grid_prb) bf16 pairs written into the processor's grid, then handle_rx_symbol(13). Results in
-/// notification order: ints [rnti, harq, crc_ok, nof_cbs, ldpc_obs, ldpc_min, ldpc_max], floats [ldpc_mean, sinr, evm,
-/// ta, cfo, epre, rsrp], payload bytes at tb_out + i * tb_stride. Returns the number of results (< 0 on error).
+/// notification order: ints [rnti, harq, crc_ok, nof_cbs, ldpc_obs, ldpc_min, ldpc_max, harq_ack_status (-1: none),
+/// harq_ack_bits], floats [ldpc_mean, sinr, evm, ta, cfo, epre, rsrp], payload bytes at tb_out + i * tb_stride.
+/// Returns the number of results (< 0 on error).
 int chain_ul_slot(void*               p,
                   unsigned            slot,
                   int                 nof_pdus,
@@ -1324,6 +1337,7 @@ int chain_ul_slot(void*               p,
     auto*            h  = static_cast<ul_harness*>(p);
     const slot_point sp(subcarrier_spacing::kHz30, slot);
     h->notifier.records.clear();
+    h->notifier.harq_ack.clear();
     unique_uplink_pdu_slot_repository repo = h->proc->get_pdu_slot_repository(sp);
     if (!repo.is_valid()) {
       return -2;
@@ -1343,10 +1357,13 @@ int chain_ul_slot(void*               p,
     const auto& recs = h->notifier.records;
     for (size_t i = 0; i != recs.size(); ++i) {
       const ul_record& r = recs[i];
-      int*             oi = out_i + 7 * i;
+      int*             oi = out_i + 9 * i;
       float*           of = out_f + 7 * i;
       oi[0] = r.rnti, oi[1] = r.harq_id, oi[2] = r.crc_ok, oi[3] = r.nof_cbs, oi[4] = r.ldpc_obs, oi[5] = r.ldpc_min;
       oi[6] = r.ldpc_max;
+      auto ack = h->notifier.harq_ack.find(r.rnti);
+      oi[7]    = ack != h->notifier.harq_ack.end() ? ack->second.first : -1;
+      oi[8]    = ack != h->notifier.harq_ack.end() ? ack->second.second : 0;
       of[0] = r.ldpc_mean, of[1] = r.sinr, of[2] = r.evm, of[3] = r.ta, of[4] = r.cfo, of[5] = r.epre, of[6] = r.rsrp;
       std::memcpy(tb_out + i * tb_stride, r.payload.data(), std::min<size_t>(r.payload.size(), tb_stride));
     }

@@ -186,14 +186,16 @@ bool crc_alloc(srsgpu_context* ctx, size_t words, size_t keep_free, bool evict, 
 }
 
 /// Contribution table of every message bit to the CRC remainder: P[i] = x^(order + L - 1 - i) mod g(x), so that
-/// CRC(m) = XOR of P[i] over the set bits m_i (the calculate() of crc_calculator_generic_impl.cpp:136 is linear).
+/// CRC(m) = XOR of P[i] over the set bits m_i (the calculate() of crc_calculator_generic_impl.cpp:136 is linear),
+/// followed by `tail` zero entries (the packed decoders read entry i for every systematic position i < K Z of a
+/// codeblock without clamping to its message length K Z - fillers: tail = fillers).
 /// The caller's plan takes a reference (refs) released with the plan. Optional tables (fast paths with a fallback)
 /// never evict and leave CRC_ARENA_RESERVE words for required ones, so a long-running cell with link adaptation keeps
 /// finding room for its codeblock tables (unreferenced tables are evicted for them).
 int get_crc_table(srsgpu_context* ctx, int poly, int L, uint32_t& offset, std::vector<crc_key>& refs,
-                  bool optional = false)
+                  bool optional = false, int tail = 0)
 {
-  const crc_key key(poly, L);
+  const crc_key key(poly, L, tail);
   auto          it = ctx->crc_tables.find(key);
   if (it != ctx->crc_tables.end()) {
     ++it->second.refs;
@@ -209,7 +211,7 @@ int get_crc_table(srsgpu_context* ctx, int poly, int L, uint32_t& offset, std::v
   }
   // Tables start 16-byte aligned and are padded to whole 16-byte vectors (the decoder copies them with 16-B loads):
   // every block is a multiple of 4 words, so every offset is too.
-  const size_t words = (static_cast<size_t>(L) + 3u) & ~static_cast<size_t>(3u);
+  const size_t words = (static_cast<size_t>(L) + static_cast<size_t>(tail) + 3u) & ~static_cast<size_t>(3u);
   size_t       off   = 0;
   if (!crc_alloc(ctx, words, optional ? CRC_ARENA_RESERVE : 0, !optional, off)) {
     return optional ? SRSGPU_ERR_NO_MEMORY : fail(SRSGPU_ERR_NO_MEMORY, "CRC table arena exhausted");
@@ -594,7 +596,7 @@ int add_decoder_cb(srsgpu_context* ctx,
   d.cb_index = i;
   d.flags    = 0;
   if (crc_poly != SRSGPU_CRC_NONE) {
-    int r = get_crc_table(ctx, crc_poly, K * Z - nof_filler, d.crc_table, *batch.crc_refs);
+    int r = get_crc_table(ctx, crc_poly, K * Z - nof_filler, d.crc_table, *batch.crc_refs, false, nof_filler);
     if (r != SRSGPU_OK) {
       return r;
     }

@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -41,7 +42,8 @@ constexpr size_t CRC_ARENA_WORDS = 16u << 20;  // 64 MiB of contribution tables
 /// Optional (fast-path) tables are only placed while at least this many arena words stay free for required ones.
 constexpr size_t CRC_ARENA_RESERVE = CRC_ARENA_WORDS / 4;
 
-using crc_key = std::pair<int, int>;  ///< (polynomial, message length)
+
+using crc_key = std::tuple<int, int, int>;  ///< (polynomial, message length, zero words after the entries)
 
 /// One contribution table in the arena: referenced by live plans (refs) or cached for reuse (refs == 0, evictable
 /// least recently used first when an allocation does not fit).

@@ -781,7 +781,6 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
                                      G::K);
 
   const uint32_t* crc_table = crc_tables + (use_crc ? d.crc_table : 0u);
-  const int       nsig      = d.nof_significant;
   scale_t         sc;
   sc.hi = uu(static_cast<int>(d.sf16 >> 8));
   sc.lo = uu(static_cast<int>(d.sf16 & 255u));
@@ -870,9 +869,8 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
         uint32_t zz   = static_cast<uint32_t>(z);
         uint32_t ZZ   = static_cast<uint32_t>(Z);
         uint32_t HH   = H;
-        uint32_t last_bit = static_cast<uint32_t>(nsig) - 1u;
         asm volatile("" : "+v"(zz));
-        asm volatile("" : "+s"(ZZ), "+s"(HH), "+s"(last_bit));
+        asm volatile("" : "+s"(ZZ), "+s"(HH));
         // SPLIT = 2: half 0 sums the first K / 2 columns, half 1 the rest (hcol = half x K / 2).
         constexpr int KC   = (SPLIT == 2) ? G::K / 2 : G::K;
         const int     hcol = half * KC;
@@ -884,10 +882,11 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
           const int      sa = scol[c * SOFT_COL_STRIDE + 2 * zz];
           const int      sb = scol[c * SOFT_COL_STRIDE + 2 * zz + 1];
           zero |= static_cast<uint32_t>(sa == 0) | static_cast<uint32_t>(sb == 0);
-          const uint32_t ta = crc_table[ia < last_bit ? ia : last_bit];
-          const uint32_t tb = crc_table[ib < last_bit ? ib : last_bit];
-          acc ^= (sa <= 0 && ia <= last_bit) ? ta : 0u;
-          acc ^= (sb <= 0 && ib <= last_bit) ? tb : 0u;
+          // ia, ib < K Z: positions past the message (fillers) read the table's zero tail (get_crc_table).
+          const uint32_t ta = crc_table[ia];
+          const uint32_t tb = crc_table[ib];
+          acc ^= (sa <= 0) ? ta : 0u;
+          acc ^= (sb <= 0) ? tb : 0u;
           ia += ZZ;
           // Bound the table loads in flight (each holds a result register).
           if constexpr (c % CRC_CHUNK == CRC_CHUNK - 1) {
@@ -1253,7 +1252,6 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
       if (run) {
         const dec_desc* md       = wd + ls;
         const uint32_t* table    = crc_tables + md->crc_table;
-        const uint32_t  last_bit = static_cast<uint32_t>(md->nof_significant) - 1u;
         uint32_t        zz = lz, ZZ = static_cast<uint32_t>(Z), HH = H;
         asm volatile("" : "+v"(zz));
         asm volatile("" : "+s"(ZZ), "+s"(HH));
@@ -1265,10 +1263,10 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
           const int      sa = scol[c * PK4_CS];
           const int      sb = scol[c * PK4_CS + 1];
           zero |= static_cast<uint32_t>(sa == 0) | static_cast<uint32_t>(sb == 0);
-          const uint32_t ta = table[ia < last_bit ? ia : last_bit];
-          const uint32_t tb = table[ib < last_bit ? ib : last_bit];
-          acc ^= (sa <= 0 && ia <= last_bit) ? ta : 0u;
-          acc ^= (sb <= 0 && ib <= last_bit) ? tb : 0u;
+          const uint32_t ta = table[ia];  // zero tail past the message, as above
+          const uint32_t tb = table[ib];
+          acc ^= (sa <= 0) ? ta : 0u;
+          acc ^= (sb <= 0) ? tb : 0u;
           ia += ZZ;
           if constexpr (c % CRC_CHUNK == CRC_CHUNK - 1) {
             __builtin_amdgcn_sched_barrier(0);

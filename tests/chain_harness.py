@@ -110,7 +110,8 @@ class Chain:
         return g
 
 
-UL_INTS = ("rnti", "harq_id", "tb_crc_ok", "nof_cbs", "ldpc_obs", "ldpc_min", "ldpc_max")
+UL_INTS = ("rnti", "harq_id", "tb_crc_ok", "nof_cbs", "ldpc_obs", "ldpc_min", "ldpc_max", "harq_ack_status",
+           "harq_ack_bits")
 UL_FLOATS = ("ldpc_mean", "sinr_db", "evm", "ta_s", "cfo_hz", "epre_db", "rsrp_db")
 UL_CPU, UL_GPU_BATCH = 0, 1
 DL_CPU, DL_GPU_BATCH = 0, 1
@@ -152,7 +153,7 @@ class UpperPhy:
         tbb = np.ascontiguousarray(tb_bytes, np.int32)
         g = np.ascontiguousarray(grid, np.uint16)
         n = len(pdus)
-        oi = np.zeros((n, 7), np.int32)
+        oi = np.zeros((n, len(UL_INTS)), np.int32)
         of = np.zeros((n, 7), np.float32)
         stride = int(max(tb_bytes)) if n else 1
         tbs = np.zeros((n, stride), np.uint8)

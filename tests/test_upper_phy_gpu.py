@@ -4,7 +4,7 @@ reference's CPU channel processors and once over the GPU slot batches of integra
 a slot's PUSCH / PDSCH PDUs into one launch sequence (tests/chain_harness.py: UpperPhy).
 
   * UL: multi-UE slots (different sizes, modulations, CFOs, delays, SNRs, one UE over the DC subcarrier, one with
-    HARQ-ACK on PUSCH, which the batch hands to its fallback processor) registered in the reference's PDU repository;
+    HARQ-ACK on PUSCH, whose UL-SCH stream the batch demultiplexes on the GPU) registered in the reference's PDU repository;
     handle_rx_symbol(13). Then a second slot with retransmissions (rv 2, new_data = false) of the first slot's failed
     TBs combined with the soft bits the batch kept in HBM (arena slots = the rx buffer pool's absolute codeblock
     identifiers), plus new UEs. Equal per (RNTI, HARQ id): TB CRC, payload, number of codeblocks; within the
@@ -83,6 +83,7 @@ def check_equal(ref, got, what):
         if not np.isnan(r["cfo_hz"]):
             assert abs(g["cfo_hz"] - r["cfo_hz"]) < 0.05, (w, r["cfo_hz"], g["cfo_hz"])
         assert abs(g["epre_db"] - r["epre_db"]) < 0.01 and abs(g["rsrp_db"] - r["rsrp_db"]) < 0.01, (w, r, g)
+        assert (g["harq_ack_status"], g["harq_ack_bits"]) == (r["harq_ack_status"], r["harq_ack_bits"]), (w, r, g)
 
 
 def ul_ues(rng, H, start_rnti, n, harq0, low_snr=()):
@@ -106,7 +107,7 @@ def test_uplink_processor_gpu_batch_equals_reference(procs):
     try:
         rng = np.random.default_rng(2024)
         ues, rb = ul_ues(rng, H, 0x4601, 14, 0, low_snr=(4, 9))
-        # A UE over the DC subcarrier (its estimate is zeroed there) and one with HARQ-ACK (the batch's fallback).
+        # A UE over the DC subcarrier (its estimate is zeroed there) and one with HARQ-ACK on PUSCH.
         dc = H.params(rnti=0x4700, harq_id=20, nof_rb=10, rb_start=rb, qm=6, target_code_rate=772.0, nof_ports=P,
                       dc_position=12 * (rb + 4) + 6)
         ack = H.params(rnti=0x4701, harq_id=21, nof_rb=8, rb_start=rb + 10, qm=4, target_code_rate=616.0, nof_ports=P,
@@ -124,6 +125,8 @@ def test_uplink_processor_gpu_batch_equals_reference(procs):
         got = gpu.ul_slot(7, pdus, sizes, grid)
         check_equal(ref, got, "slot 7")
         ok = {d["rnti"]: d["tb_crc_ok"] for d, _ in ref}
+        ack_res = next(d for d, _ in got if d["rnti"] == ack.rnti)
+        assert ack_res["harq_ack_status"] >= 0, ack_res  # the HARQ-ACK field was reported
         data_ok = [ok[p.rnti] for p, *_ in ues if p.nof_harq_ack == 0]
         assert sum(data_ok) == len(data_ok) - 2, ok  # every UE decodes but the two faded ones
         for (p, *_), tb in zip(ues, tbs):
@@ -137,13 +140,14 @@ def test_uplink_processor_gpu_batch_equals_reference(procs):
         rb = 0
         for (p, cfo, delay, gain), tb in retx:
             q = H.params(**{f: getattr(p, f) for f, _ in H.ChainParams._fields_})
-            q.rv, q.new_data, q.rb_start = 2, 0, rb
+            q.rv, q.new_data, q.rb_start, q.slot = 2, 0, rb, 8
             rb += q.nof_rb
             ues2.append((q, cfo, delay, 0.0))
             tbs2.append(tb)
         new, _ = ul_ues(rng, H, 0x4800, 6, 40)
         for p, cfo, delay, gain in new:
             p.rb_start += rb
+            p.slot = 8  # the UE's DM-RS and scrambling of slot 8 (the processor's slot)
             seg = grant(p).segmentation()
             p.base_graph = seg.base_graph
             ues2.append((p, cfo, delay, gain))
@@ -155,7 +159,9 @@ def test_uplink_processor_gpu_batch_equals_reference(procs):
         got2 = gpu.ul_slot(8, pdus2, sizes2, grid2)
         check_equal(ref2, got2, "slot 8")
         ok2 = {d["rnti"]: d["tb_crc_ok"] for d, _ in ref2}
-        assert all(ok2[p.rnti] for (p, *_), _ in retx), ok2  # the retransmissions decode after combining
+        # The 64QAM retransmission decodes after combining; the 256QAM rate-0.93 one does not (rv 2 carries almost no
+        # systematic bits and its first transmission was faded) - on the reference as on the GPU (check_equal above).
+        assert sum(ok2[p.rnti] for (p, *_), _ in retx) >= 1, ok2
     finally:
         chain.close()
 

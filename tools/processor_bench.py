@@ -49,7 +49,9 @@ def slot_cases(lib, T, slots, R):
     """The same profiles through the reference's slot processors (uplink_processor_impl /
     downlink_processor_single_executor_impl), one per thread, reference CPU processors (variant 0) vs the GPU slot batches
     of integration/upper_phy_gpu.cpp (variant 1): the single full-band PDU per slot of the reference benchmarks, and the
-    bench's multi-UE slot (64 UEs x 4-5 PRB) where the batch gathers 64 PDUs into one launch sequence."""
+    multi-UE slot at the slot processors' capacity (MAX_PUSCH_PDUS_PER_SLOT = MAX_UE_PDUS_PER_SLOT = 16,
+    slot_pdu_capacity_constants.h:44/:77: 16 UEs x 17 PRB) where the batch gathers the 16 PDUs into one launch
+    sequence."""
     import ctypes
     PP = ctypes.POINTER(H.ChainParams)
     lib.chain_ul_bench.restype = ctypes.c_int
@@ -71,7 +73,7 @@ def slot_cases(lib, T, slots, R):
         g = ((grid.view(np.uint32) + 0x7FFF + ((grid.view(np.uint32) >> 16) & 1)) >> 16).astype(np.uint16)
         case = {"profile": name, "nof_pdus_per_slot": len(pdus), "tb_bits_per_slot": int(sum(tbs)), "runs": []}
         for v in (0, 1):
-            n = slots if v else max(2, slots // 4)
+            n = slots
             secs = np.zeros(R, np.float64)
             r = lib.chain_ul_bench(0, v, T, n, R, len(pdus), arr, ptr(tbb), ptr(g), 4, 273, ptr(secs))
             assert r >= 0, r
@@ -90,7 +92,7 @@ def slot_cases(lib, T, slots, R):
         w = np.ascontiguousarray(np.concatenate([x.ravel() for x in weights]), np.complex64).view(np.float32)
         case = {"profile": name, "nof_pdus_per_slot": len(pdus), "tb_bits_per_slot": int(sum(tbs)), "runs": []}
         for v in (0, 1):
-            n = slots if v else max(2, slots // 4)
+            n = slots
             secs = np.zeros(R, np.float64)
             r = lib.chain_dl_bench(0, v, T, n, R, len(pdus), arr, ptr(w), ptr(data), ptr(tbb), 4, 273, ptr(secs))
             assert r >= 0, r
@@ -102,24 +104,22 @@ def slot_cases(lib, T, slots, R):
         out["dl"].append(case)
         print(json.dumps(case), file=sys.stderr, flush=True)
 
-    # UL: the reference benchmark's PDU (273 PRB, 256QAM, 1 layer, random-noise grid) as one PDU per slot; the
-    # bench's 64-UE slot.
+    # UL: the reference benchmark's PDU (273 PRB, 256QAM, 1 layer, random-noise grid) as one PDU per slot; 16 UEs.
     tbs = sch.tbs_calculate(273, 14, 6 * 2 * 2, 0, 8, 948.0, 1)
     p = H.params(slot=0, rnti=1, n_id=0, scrambling_id=0, nof_rb=273, rb_start=0, bwp_size=273, qm=8,
                  target_code_rate=948.0, nof_layers=1, nof_ports=4, base_graph=sch.base_graph(tbs, 948 / 1024),
                  tbs_lbrm_bytes=159749, max_iterations=2)
     ul("scs30_100MHz_256qam_rv0_4port_1layer, one PDU per slot", [p], [tbs])
-    ues = sch.slot_100mhz_4x4(nof_layers=1, nof_dmrs_symbols=2)
-    pdus, tb_list, rb = [], [], 0
-    for i, u in enumerate(ues):
+    pdus, tb_list = [], []
+    for i in range(16):
+        u = sch.UeGrant(17, 1, 8, 948.0, nof_dmrs_symbols=2)
         seg = u.segmentation()
-        pdus.append(H.params(rnti=0x4601 + i, harq_id=i % 16, nof_rb=u.n_prb, rb_start=rb, qm=u.qm,
-                             target_code_rate=u.r1024, nof_ports=4, base_graph=seg.base_graph))
+        pdus.append(H.params(rnti=0x4601 + i, harq_id=i, nof_rb=17, rb_start=17 * i, qm=8, target_code_rate=948.0,
+                             nof_ports=4, base_graph=seg.base_graph, max_iterations=2))
         tb_list.append(seg.tbs)
-        rb += u.n_prb
-    ul("64 UEs x 4-5 PRB, 256QAM MCS27, 1 layer (bench headline slot)", pdus, tb_list)
+    ul("16 UEs x 17 PRB, 256QAM, 1 layer (the slot processors' PUSCH PDU capacity)", pdus, tb_list)
 
-    # DL: 270 PRB 4 layers on 4 ports as one PDU per slot; the 64-UE 4-layer slot.
+    # DL: 270 PRB 4 layers on 4 ports as one PDU per slot; 16 UEs with 4 layers.
     tbs = sch.tbs_calculate(270, 12, 6 * 3 * 2, 0, 8, 948.0, 4)
     p = H.params(slot=0, rnti=1, n_id=0, scrambling_id=0, nof_rb=270, rb_start=0, bwp_size=273, qm=8,
                  target_code_rate=948.0, nof_layers=4, nof_ports=4, start_symbol=2, nof_symbols=12,
@@ -127,16 +127,16 @@ def slot_cases(lib, T, slots, R):
                  tbs_lbrm_bytes=159749)
     q, _ = np.linalg.qr(rng.normal(size=(4, 4)) + 1j * rng.normal(size=(4, 4)))
     dl("4port_4layer_scs30_100MHz_256qam, one PDU per slot", [p], [tbs], [q.astype(np.complex64)])
-    ues = sch.slot_100mhz_4x4(nof_layers=4, nof_dmrs_symbols=2)
-    pdus, tb_list, ws, rb = [], [], [], 0
-    for i, u in enumerate(ues):
+    pdus, tb_list, ws = [], [], []
+    for i in range(16):
+        u = sch.UeGrant(17, 4, 8, 948.0, nof_symb_sh=12, nof_dmrs_symbols=2)
         seg = u.segmentation()
-        pdus.append(H.params(rnti=0x4601 + i, nof_rb=u.n_prb, rb_start=rb, qm=u.qm, target_code_rate=u.r1024,
-                             nof_layers=4, nof_ports=4, base_graph=seg.base_graph))
+        pdus.append(H.params(rnti=0x4601 + i, nof_rb=17, rb_start=17 * i, qm=8, target_code_rate=948.0, nof_layers=4,
+                             nof_ports=4, start_symbol=2, nof_symbols=12, dmrs_mask=(1 << 2) | (1 << 11),
+                             base_graph=seg.base_graph))
         tb_list.append(seg.tbs)
         ws.append(np.eye(4, dtype=np.complex64))
-        rb += u.n_prb
-    dl("64 UEs x 4-5 PRB, 256QAM MCS27, 4 layers (bench headline slot)", pdus, tb_list, ws)
+    dl("16 UEs x 17 PRB, 256QAM, 4 layers (the slot processors' PDSCH UE PDU capacity)", pdus, tb_list, ws)
     return out
 
 

@@ -9,6 +9,8 @@
 #include <algorithm>
 #include <cstring>
 #include <list>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 namespace srsran {
@@ -84,7 +86,8 @@ void key_append(std::vector<uint8_t>& key, const T& v)
 }
 
 /// Most-recently-used cache of srsgpu plans keyed by their configuration bytes (a cell's grants repeat slot after
-/// slot): create() runs only on a miss; the least recently used plan is destroyed beyond `capacity`.
+/// slot): create() runs only on a miss; the least recently used plan is destroyed beyond `capacity`. Hashed lookup: a
+/// slot's key is a few kilobytes and a frame's worth of slot-dependent plans stays resident.
 template <typename Plan>
 class plan_cache
 {
@@ -92,39 +95,51 @@ public:
   plan_cache(void (*destroy_)(Plan*), size_t capacity_ = 64) : destroy(destroy_), capacity(capacity_) {}
   plan_cache(const plan_cache&)            = delete;
   plan_cache& operator=(const plan_cache&) = delete;
-  ~plan_cache()
-  {
-    for (auto& e : lru) {
-      destroy(e.plan);
-    }
-  }
+  ~plan_cache() { clear(); }
 
   template <typename Create>
-  Plan* get(const std::vector<uint8_t>& key, Create&& create)
+  Plan* get(const std::vector<uint8_t>& key_bytes, Create&& create)
   {
-    for (auto it = lru.begin(); it != lru.end(); ++it) {
-      if (it->key == key) {
-        lru.splice(lru.begin(), lru, it);
-        return lru.front().plan;
-      }
+    std::string key(key_bytes.begin(), key_bytes.end());
+    auto        it = index.find(key);
+    if (it != index.end()) {
+      lru.splice(lru.begin(), lru, it->second);
+      return lru.front().plan;
     }
     Plan* plan = create();
     lru.push_front({key, plan});
+    index.emplace(std::move(key), lru.begin());
     if (lru.size() > capacity) {
       destroy(lru.back().plan);
+      index.erase(lru.back().key);
       lru.pop_back();
+      ++nof_evictions;
     }
     return plan;
   }
 
+  /// Plans destroyed so far (a captured graph that references a plan must not outlive it).
+  uint64_t evictions() const { return nof_evictions; }
+
+  void clear()
+  {
+    for (auto& e : lru) {
+      destroy(e.plan);
+    }
+    lru.clear();
+    index.clear();
+  }
+
 private:
   struct entry {
-    std::vector<uint8_t> key;
-    Plan*                plan;
+    std::string key;
+    Plan*       plan;
   };
   void (*destroy)(Plan*);
-  size_t           capacity;
-  std::list<entry> lru;
+  size_t                                                            capacity;
+  std::list<entry>                                                  lru;
+  std::unordered_map<std::string, typename std::list<entry>::iterator> index;
+  uint64_t                                                          nof_evictions = 0;
 };
 
 /// A HIP stream on the context's device, destroyed with its owner.

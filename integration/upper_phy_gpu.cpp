@@ -1,5 +1,7 @@
 // Slot-batched GPU processing behind the reference's upper-PHY slot processors: see upper_phy_gpu.h for the design.
 #include "upper_phy_gpu.h"
+#include <cstdlib>
+#include <chrono>
 #include "srsran/support/error_handling.h"
 
 #include "chain_convert.h"
@@ -228,6 +230,22 @@ private:
   std::vector<unsigned>             cb_stats;
 };
 
+/// Capacity of the caches whose plans depend on the slot number (DM-RS sequences, and the UL slot graphs that run
+/// them): a grant pattern repeats every frame, i.e. every 10 x 2^mu slots (40 at 60 kHz), so a few patterns of a frame
+/// stay resident instead of every slot missing.
+constexpr size_t SLOT_PLANS = 160;
+
+std::mutex& setup_mutex()
+{
+  static std::mutex m;
+  return m;
+}
+
+void destroy_graph_exec(hipGraphExec_t x)
+{
+  (void)hipGraphExecDestroy(x);
+}
+
 /// A reference pusch_processor_impl over the replay stages (one per thread that runs batches: the processor's
 /// dependency pool binds its instances to threads, concurrent_thread_local_object_pool.h:67-96).
 struct replay_processor {
@@ -256,16 +274,12 @@ public:
     uci_factory(std::move(uci_factory_)),
     fallback(std::move(fallback_)),
     stream(ctx, WHO),
-    chest_plans(srsgpu_pusch_chest_plan_destroy, 16),
+    chest_plans(srsgpu_pusch_chest_plan_destroy, SLOT_PLANS),
     demod_plans(srsgpu_pusch_demodulator_plan_destroy, 16),
     dec_plans(srsgpu_pusch_decoder_plan_destroy, 16),
     demux_plans(srsgpu_ulsch_demux_plan_destroy, 16),
-    grid_buf(WHO),
-    out_buf(WHO),
-    flag_buf(WHO),
-    msg_buf(WHO),
-    job_buf(WHO),
-    tb_buf(WHO)
+    io(WHO),
+    graphs(destroy_graph_exec, SLOT_PLANS)
   {
     if (!fallback || !demux_factory || !uci_factory) {
       throw std::invalid_argument(std::string(WHO) + ": invalid dependencies");
@@ -274,6 +288,15 @@ public:
 
   ~pusch_slot_batch()
   {
+    if (timing && timed_slots > 0) {
+      // SRSGPU_BATCH_TIMING=1: mean host-clock time per slot of each phase of run() (diagnostics).
+      std::fprintf(stderr,
+                   "pusch_slot_batch: %llu slots, us per slot: setup %.1f, host fill %.1f, graph lookup %.1f, "
+                   "launch+GPU+sync %.1f, replay %.1f\n",
+                   static_cast<unsigned long long>(timed_slots), phase_us[0] / timed_slots,
+                   phase_us[1] / timed_slots, phase_us[2] / timed_slots, phase_us[3] / timed_slots,
+                   phase_us[4] / timed_slots);
+    }
     (void)hipStreamSynchronize(stream.get());
     (void)hipFree(d_ce);
     (void)hipFree(d_harq);
@@ -339,12 +362,12 @@ private:
   plan_cache<srsgpu_pusch_demodulator_plan>     demod_plans;
   plan_cache<srsgpu_pusch_decoder_plan>         dec_plans;
   plan_cache<srsgpu_ulsch_demux_plan>           demux_plans;
-  staged_buffer                                 grid_buf;  ///< Rx grid [port][symbol][subcarrier].
-  staged_buffer                                 out_buf;   ///< nv, metrics, statistics, LLRs, scrambling words.
-  staged_buffer                                 flag_buf;  ///< CB CRC flags, iterations, TB CRC flags.
-  staged_buffer                                 msg_buf;   ///< CB messages.
-  staged_buffer                                 job_buf;   ///< HARQ arena copy jobs.
-  staged_buffer                                 tb_buf;    ///< Decoded TBs.
+  staged_buffer                                 io;  ///< A slot's inputs and outputs (layout in run()).
+  plan_cache<std::remove_pointer_t<hipGraphExec_t>> graphs;
+  uint64_t                                      plan_generation = 0;
+  const bool                                    timing          = std::getenv("SRSGPU_BATCH_TIMING") != nullptr;
+  double                                        phase_us[5]     = {};
+  uint64_t                                      timed_slots     = 0;
   uint32_t*                                     d_ce      = nullptr;
   size_t                                        d_ce_cap  = 0;
   int8_t*                                       d_harq    = nullptr;
@@ -605,7 +628,11 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     }
   }
 
-  // Plans (cached: a cell's grants repeat).
+  // Plans (cached: a cell's grants repeat). Plan creation and buffer growth call synchronous HIP APIs, which fail
+  // while any thread captures a stream: they and the slot graph's capture run under one process-wide lock (a cache
+  // hit holds it for microseconds).
+  const auto                   t_start = std::chrono::steady_clock::now();
+  std::unique_lock<std::mutex> setup_lock(setup_mutex());
   srsgpu_pusch_chest_plan* chest = chest_plans.get(chest_key, [&] {
     std::vector<srsgpu_pusch_chest_config> c;
     std::vector<srsgpu_alloc_ext>          x;
@@ -645,125 +672,169 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
   hipStream_t  s   = stream.get();
   const size_t row = static_cast<size_t>(nsc) * sizeof(uint32_t);
 
-  // Rx grid: every symbol of ports 0..P-1, [port][symbol][subcarrier].
-  grid_buf.reserve(P * 14 * row);
-  for (unsigned p = 0; p != P; ++p) {
-    for (unsigned l = 0; l != 14; ++l) {
-      std::memcpy(grid_buf.host((p * 14 + l) * row), grid.get_view(p, l).data(), row);
-    }
-  }
-  grid_buf.upload(0, P * 14 * row, s);
-
-  // Output staging: nv [4 n], metrics [4 n][METRICS], statistics [n][DEMOD_STATS], LLRs, scrambling words.
-  const size_t nv_off    = 0;
-  const size_t m_off     = nv_off + 4 * n * sizeof(float);
-  const size_t st_off    = m_off + 4 * n * SRSGPU_CHEST_METRICS * sizeof(float);
-  const size_t llr_off   = (st_off + n * SRSGPU_DEMOD_STATS * sizeof(float) + 63) / 64 * 64;
-  size_t       seq_total = 0;
-  std::vector<size_t> seq_off(n);
+  // One pinned staging image per slot, inputs first: [grid | copy jobs | CB messages | CB CRC flags] are uploaded,
+  // [CB CRC flags | iterations | TB CRC flags | nv | metrics | statistics | LLRs | scrambling words | TBs] downloaded
+  // (the CRC flags are the HARQ context in and the result out). Two copies per slot instead of one per array.
+  auto         align  = [](size_t x) { return (x + 63) / 64 * 64; };
+  const size_t grid_o = 0;
+  const size_t jobs_o = align(grid_o + static_cast<size_t>(P) * 14 * row);
+  const size_t msgs_o = align(jobs_o + jobs.size() * sizeof(srsgpu_harq_copy_job));
+  const size_t flag_o = align(msgs_o + static_cast<size_t>(cb_total) * SRSGPU_CB_MSG_STRIDE);
+  const size_t iter_o = align(flag_o + cb_total);
+  const size_t tbok_o = align(iter_o + static_cast<size_t>(cb_total) * sizeof(int32_t));
+  const size_t nv_o   = align(tbok_o + n);
+  const size_t m_o    = align(nv_o + 4 * n * sizeof(float));
+  const size_t st_o   = align(m_o + 4 * n * SRSGPU_CHEST_METRICS * sizeof(float));
+  const size_t llr_o  = align(st_o + n * SRSGPU_DEMOD_STATS * sizeof(float));
+  std::vector<size_t> seq_o(n);
+  size_t              seq_total = 0;
   for (unsigned i = 0; i != n; ++i) {
-    seq_off[i] = llr_off + llr_total + seq_total;
+    seq_o[i] = llr_o + llr_total + seq_total;
     seq_total += (batch[i]->nof_llrs + 31) / 32 * 4;
   }
-  const size_t out_bytes = llr_off + llr_total + seq_total;
-  out_buf.reserve(out_bytes);
+  const size_t tb_o  = align(llr_o + llr_total + seq_total);
+  const size_t end_o = tb_o + std::max<size_t>(tb_total, 16);
+  io.reserve(end_o);
   reserve_device(d_ce, d_ce_cap, static_cast<size_t>(4) * P * 14 * row, "channel estimates");
+  reserve_device(d_harq, d_harq_cap, std::max<size_t>(harq_total, 16), "HARQ batch buffer");
+  setup_lock.unlock();
+  const auto t_setup = std::chrono::steady_clock::now();
 
-  srsgpu_check(srsgpu_pusch_chest_plan_execute(chest, grid_buf.dev<uint32_t>(), d_ce, out_buf.dev<float>(nv_off),
-                                               out_buf.dev<float>(m_off), s),
-               WHO);
-  // pusch_processor_impl.cpp:222-240: the DC subcarrier's estimate is zeroed for CP-OFDM transmissions over it.
-  for (unsigned i = 0; i != n; ++i) {
-    const pusch_processor::pdu_t& pdu = batch[i]->pdu;
-    if (pdu.dc_position.has_value() && std::holds_alternative<pusch_processor::dmrs_configuration>(pdu.dmrs) &&
-        *pdu.dc_position < nsc) {
-      for (unsigned ly = 0; ly != pdu.nof_tx_layers; ++ly) {
-        for (unsigned p = 0; p != pdu.rx_ports.size(); ++p) {
-          uint8_t* base = reinterpret_cast<uint8_t*>(d_ce) + ((static_cast<size_t>(ly) * P + p) * 14 +
-                                                              pdu.start_symbol_index) * row +
-                          static_cast<size_t>(*pdu.dc_position) * sizeof(uint32_t);
-          hip_check(hipMemset2DAsync(base, row, 0, sizeof(uint32_t), pdu.nof_symbols, s), WHO, "DC");
-        }
-      }
+  // Host inputs: the rx grid (every symbol of ports 0..P-1, [port][symbol][subcarrier]), the HARQ arena copy jobs,
+  // and the HARQ context from the rx buffers: CB CRC flags and the messages of CBs that already passed (a new
+  // transmission's flags are reset by the plan, pusch_decoder_impl.cpp:133-136).
+  for (unsigned p = 0; p != P; ++p) {
+    for (unsigned l = 0; l != 14; ++l) {
+      std::memcpy(io.host(grid_o + (p * 14 + l) * row), grid.get_view(p, l).data(), row);
     }
   }
-  srsgpu_check(srsgpu_pusch_demodulator_plan_execute_ex(demod, grid_buf.dev<uint32_t>(), d_ce,
-                                                        out_buf.dev<float>(nv_off), out_buf.dev<int8_t>(llr_off),
-                                                        out_buf.dev<float>(st_off), s),
-               WHO);
-  for (unsigned i = 0; i != n; ++i) {
-    srsgpu_check(srsgpu_pusch_demodulator_plan_scrambling(demod, i, out_buf.dev<uint32_t>(seq_off[i]), s), WHO);
-  }
-  if (demux != nullptr) {
-    // Only the UL-SCH stream is used on the device: the UCI streams are split again by the reference's own
-    // demultiplexer during the replay, from the codeword LLRs.
-    int8_t* llr_base = out_buf.dev<int8_t>(llr_off);
-    srsgpu_check(srsgpu_ulsch_demux_plan_execute(demux, llr_base, llr_base, llr_base, llr_base, llr_base, s), WHO);
-  }
-
-  // HARQ context: soft bits from the arena, CB CRC flags (and the messages of CBs that already passed) from the rx
-  // buffers; a new transmission's flags are reset by the plan (pusch_decoder_impl.cpp:133-136).
-  const size_t flags_off = 0;
-  const size_t iters_off = (cb_total + 15) / 16 * 16;
-  const size_t tbok_off  = iters_off + cb_total * sizeof(int32_t);
-  flag_buf.reserve(tbok_off + n + 16);
-  msg_buf.reserve(static_cast<size_t>(cb_total) * SRSGPU_CB_MSG_STRIDE);
+  std::memcpy(io.host(jobs_o), jobs.data(), jobs.size() * sizeof(srsgpu_harq_copy_job));
   decoded_flags.assign(cb_total, 0);
-  bool any_restored = false;
   for (unsigned i = 0; i != n; ++i) {
     pusch_entry&     e    = *batch[i];
     span<const bool> crcs = e.rm->get_codeblocks_crc();
     for (unsigned c = 0; c != e.nof_cbs; ++c) {
-      const bool ok                         = !e.new_data && crcs[c];
-      *flag_buf.host<uint8_t>(e.cb0 + c) = ok ? 1 : 0;
-      decoded_flags[e.cb0 + c]              = ok ? 0 : 1;
+      const bool ok                    = !e.new_data && crcs[c];
+      *io.host<uint8_t>(flag_o + e.cb0 + c) = ok ? 1 : 0;
+      decoded_flags[e.cb0 + c]         = ok ? 0 : 1;
       if (ok) {
         const bit_buffer bits = e.rm->get_codeblock_data_bits(c, e.cb_KZ);
-        uint8_t*         dst  = msg_buf.host<uint8_t>(static_cast<size_t>(e.cb0 + c) * SRSGPU_CB_MSG_STRIDE);
+        uint8_t*         dst  = io.host<uint8_t>(msgs_o + static_cast<size_t>(e.cb0 + c) * SRSGPU_CB_MSG_STRIDE);
         for (unsigned b = 0; b != (e.cb_KZ + 7) / 8; ++b) {
           dst[b] = bits.get_byte(b);
         }
-        any_restored = true;
       }
     }
   }
-  flag_buf.upload(flags_off, cb_total, s);
-  if (any_restored) {
-    msg_buf.upload(0, static_cast<size_t>(cb_total) * SRSGPU_CB_MSG_STRIDE, s);
+
+  const auto t_fill = std::chrono::steady_clock::now();
+  setup_lock.lock();
+  // The slot's device work as one captured graph per layout (cached like the plans it runs: a cell's grants repeat),
+  // so a slot costs one graph launch instead of some thirty queue operations.
+  std::vector<uint8_t> graph_key;
+  for (const std::vector<uint8_t>* k : {&chest_key, &demod_key, &demux_key, &dec_key}) {
+    gpu::key_append(graph_key, k->size());
+    graph_key.insert(graph_key.end(), k->begin(), k->end());
   }
-  job_buf.reserve(jobs.size() * sizeof(srsgpu_harq_copy_job));
-  std::memcpy(job_buf.host(), jobs.data(), jobs.size() * sizeof(srsgpu_harq_copy_job));
-  job_buf.upload(0, jobs.size() * sizeof(srsgpu_harq_copy_job), s);
-  reserve_device(d_harq, d_harq_cap, std::max<size_t>(harq_total, 16), "HARQ batch buffer");
-  srsgpu_check(srsgpu_harq_copy(ctx, SRSGPU_HARQ_TO_BATCH, arena->d_soft, HARQ_SLOT_BYTES, d_harq,
-                                job_buf.dev<srsgpu_harq_copy_job>(), jobs.size(), s),
-               WHO);
-  tb_buf.reserve(std::max<unsigned>(tb_total, 16));
-  srsgpu_check(srsgpu_pusch_decoder_plan_execute(dec, out_buf.dev<int8_t>(llr_off), d_harq,
-                                                 flag_buf.dev<uint8_t>(flags_off), msg_buf.dev<uint8_t>(),
-                                                 flag_buf.dev<int32_t>(iters_off), tb_buf.dev<uint8_t>(),
-                                                 flag_buf.dev<uint8_t>(tbok_off), s),
-               WHO);
-  srsgpu_check(srsgpu_harq_copy(ctx, SRSGPU_HARQ_TO_ARENA, arena->d_soft, HARQ_SLOT_BYTES, d_harq,
-                                job_buf.dev<srsgpu_harq_copy_job>(), jobs.size(), s),
-               WHO);
-  out_buf.download(0, out_bytes, s);
-  flag_buf.download(0, tbok_off + n, s);
-  tb_buf.download(0, tb_total, s);
+  for (const void* ptr : {static_cast<const void*>(io.host()), static_cast<const void*>(io.dev()),
+                          static_cast<const void*>(d_ce), static_cast<const void*>(d_harq)}) {
+    gpu::key_append(graph_key, ptr);
+  }
+  gpu::key_append(graph_key, P);
+  gpu::key_append(graph_key, end_o);
+  for (unsigned i = 0; i != n; ++i) {
+    const pusch_processor::pdu_t& pdu = batch[i]->pdu;
+    gpu::key_append(graph_key, pdu.dc_position.has_value() ? static_cast<int>(*pdu.dc_position) : -1);
+  }
+  const uint64_t generation = chest_plans.evictions() + demod_plans.evictions() + demux_plans.evictions() +
+                              dec_plans.evictions();
+  if (generation != plan_generation) {
+    graphs.clear();  // a captured graph references the plans' device descriptors
+    plan_generation = generation;
+  }
+  hipGraphExec_t exec = graphs.get(graph_key, [&] {
+    hip_check(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), WHO, "begin capture");
+    struct capture_guard {  // ends a capture an error interrupted, so the stream stays usable
+      hipStream_t s;
+      bool        open = true;
+      ~capture_guard()
+      {
+        if (open) {
+          hipGraph_t g = nullptr;
+          (void)hipStreamEndCapture(s, &g);
+          (void)hipGraphDestroy(g);
+        }
+      }
+    } guard{s};
+    io.upload(0, iter_o, s);
+    srsgpu_check(srsgpu_pusch_chest_plan_execute(chest, io.dev<uint32_t>(grid_o), d_ce, io.dev<float>(nv_o),
+                                                 io.dev<float>(m_o), s),
+                 WHO);
+    // pusch_processor_impl.cpp:222-240: the DC subcarrier's estimate is zeroed for CP-OFDM transmissions over it.
+    for (unsigned i = 0; i != n; ++i) {
+      const pusch_processor::pdu_t& pdu = batch[i]->pdu;
+      if (pdu.dc_position.has_value() && std::holds_alternative<pusch_processor::dmrs_configuration>(pdu.dmrs) &&
+          *pdu.dc_position < nsc) {
+        for (unsigned ly = 0; ly != pdu.nof_tx_layers; ++ly) {
+          for (unsigned p = 0; p != pdu.rx_ports.size(); ++p) {
+            uint8_t* base = reinterpret_cast<uint8_t*>(d_ce) +
+                            ((static_cast<size_t>(ly) * P + p) * 14 + pdu.start_symbol_index) * row +
+                            static_cast<size_t>(*pdu.dc_position) * sizeof(uint32_t);
+            hip_check(hipMemset2DAsync(base, row, 0, sizeof(uint32_t), pdu.nof_symbols, s), WHO, "DC");
+          }
+        }
+      }
+    }
+    srsgpu_check(srsgpu_pusch_demodulator_plan_execute_ex(demod, io.dev<uint32_t>(grid_o), d_ce, io.dev<float>(nv_o),
+                                                          io.dev<int8_t>(llr_o), io.dev<float>(st_o), s),
+                 WHO);
+    for (unsigned i = 0; i != n; ++i) {
+      srsgpu_check(srsgpu_pusch_demodulator_plan_scrambling(demod, i, io.dev<uint32_t>(seq_o[i]), s), WHO);
+    }
+    if (demux != nullptr) {
+      // Only the UL-SCH stream is used on the device: the UCI streams are split again by the reference's own
+      // demultiplexer during the replay, from the codeword LLRs.
+      int8_t* llr_base = io.dev<int8_t>(llr_o);
+      srsgpu_check(srsgpu_ulsch_demux_plan_execute(demux, llr_base, llr_base, llr_base, llr_base, llr_base, s), WHO);
+    }
+    srsgpu_check(srsgpu_harq_copy(ctx, SRSGPU_HARQ_TO_BATCH, arena->d_soft, HARQ_SLOT_BYTES, d_harq,
+                                  io.dev<srsgpu_harq_copy_job>(jobs_o), jobs.size(), s),
+                 WHO);
+    srsgpu_check(srsgpu_pusch_decoder_plan_execute(dec, io.dev<int8_t>(llr_o), d_harq, io.dev<uint8_t>(flag_o),
+                                                   io.dev<uint8_t>(msgs_o), io.dev<int32_t>(iter_o),
+                                                   io.dev<uint8_t>(tb_o), io.dev<uint8_t>(tbok_o), s),
+                 WHO);
+    srsgpu_check(srsgpu_harq_copy(ctx, SRSGPU_HARQ_TO_ARENA, arena->d_soft, HARQ_SLOT_BYTES, d_harq,
+                                  io.dev<srsgpu_harq_copy_job>(jobs_o), jobs.size(), s),
+                 WHO);
+    io.download(flag_o, end_o - flag_o, s);
+    hipGraph_t g = nullptr;
+    guard.open   = false;
+    hip_check(hipStreamEndCapture(s, &g), WHO, "end capture");
+    hipGraphExec_t x = nullptr;
+    const hipError_t r = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    hip_check(r, WHO, "graph instantiate");
+    return x;
+  });
+  setup_lock.unlock();
+  const auto t_graph = std::chrono::steady_clock::now();
+  hip_check(hipGraphLaunch(exec, s), WHO, "graph launch");
   hip_check(hipStreamSynchronize(s), WHO, "synchronise");
+  const auto t_gpu = std::chrono::steady_clock::now();
 
   // Messages of the passed CBs of failed TBs are kept in the rx buffer for the retransmission.
   bool need_msgs = false;
   for (unsigned i = 0; i != n && !need_msgs; ++i) {
     const pusch_entry& e = *batch[i];
-    if (*flag_buf.host<uint8_t>(tbok_off + i) == 0) {
+    if (*io.host<uint8_t>(tbok_o + i) == 0) {
       for (unsigned c = 0; c != e.nof_cbs; ++c) {
-        need_msgs = need_msgs || *flag_buf.host<uint8_t>(e.cb0 + c) != 0;
+        need_msgs = need_msgs || *io.host<uint8_t>(flag_o + e.cb0 + c) != 0;
       }
     }
   }
   if (need_msgs) {
-    msg_buf.download(0, static_cast<size_t>(cb_total) * SRSGPU_CB_MSG_STRIDE, s);
+    io.download(msgs_o, static_cast<size_t>(cb_total) * SRSGPU_CB_MSG_STRIDE, s);
     hip_check(hipStreamSynchronize(s), WHO, "synchronise");
   }
 
@@ -771,22 +842,32 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
   replay_processor& r = replay_for_this_thread();
   for (unsigned i = 0; i != n; ++i) {
     pusch_entry& e      = *batch[i];
-    r.est->nv           = out_buf.host<float>(nv_off + 4 * i * sizeof(float));
-    r.est->m            = out_buf.host<float>(m_off + 4 * i * SRSGPU_CHEST_METRICS * sizeof(float));
-    r.demod->llrs       = out_buf.host<int8_t>(llr_off + e.llr_offset);
-    r.demod->seq        = out_buf.host<uint32_t>(seq_off[i]);
-    r.demod->stats      = out_buf.host<float>(st_off + i * SRSGPU_DEMOD_STATS * sizeof(float));
+    r.est->nv           = io.host<float>(nv_o + 4 * i * sizeof(float));
+    r.est->m            = io.host<float>(m_o + 4 * i * SRSGPU_CHEST_METRICS * sizeof(float));
+    r.demod->llrs       = io.host<int8_t>(llr_o + e.llr_offset);
+    r.demod->seq        = io.host<uint32_t>(seq_o[i]);
+    r.demod->stats      = io.host<float>(st_o + i * SRSGPU_DEMOD_STATS * sizeof(float));
     r.demod->nof_llrs   = e.nof_llrs;
     r.demod->nof_rb     = e.nof_rb;
-    r.dec->cb_flags     = flag_buf.host<uint8_t>(flags_off + e.cb0);
-    r.dec->cb_iters     = flag_buf.host<int32_t>(iters_off + e.cb0 * sizeof(int32_t));
-    r.dec->tb           = tb_buf.host<uint8_t>(e.tb_offset);
-    r.dec->cb_msgs      = msg_buf.host<uint8_t>(static_cast<size_t>(e.cb0) * SRSGPU_CB_MSG_STRIDE);
+    r.dec->cb_flags     = io.host<uint8_t>(flag_o + e.cb0);
+    r.dec->cb_iters     = io.host<int32_t>(iter_o + e.cb0 * sizeof(int32_t));
+    r.dec->tb           = io.host<uint8_t>(tb_o + e.tb_offset);
+    r.dec->cb_msgs      = io.host<uint8_t>(msgs_o + static_cast<size_t>(e.cb0) * SRSGPU_CB_MSG_STRIDE);
     r.dec->decoded      = decoded_flags.data() + e.cb0;
-    r.dec->tb_ok        = *flag_buf.host<uint8_t>(tbok_off + i) != 0;
+    r.dec->tb_ok        = *io.host<uint8_t>(tbok_o + i) != 0;
     r.dec->cb_KZ        = e.cb_KZ;
     r.dec->max_iter     = cfg.nof_ldpc_iterations;
     r.proc->process(e.data, std::move(e.rm), *e.notifier, *e.grid, e.pdu);
+  }
+  if (timing) {
+    const auto t_end = std::chrono::steady_clock::now();
+    auto       us    = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    phase_us[0] += us(t_start, t_setup);
+    phase_us[1] += us(t_setup, t_fill);
+    phase_us[2] += us(t_fill, t_graph);
+    phase_us[3] += us(t_graph, t_gpu);
+    phase_us[4] += us(t_gpu, t_end);
+    ++timed_slots;
   }
 }
 
@@ -981,7 +1062,7 @@ public:
     stream(ctx, WHO),
     enc_plans(srsgpu_pdsch_encoder_plan_destroy, 16),
     mod_plans(srsgpu_pdsch_modulator_plan_destroy, 16),
-    dmrs_plans(srsgpu_pdsch_dmrs_plan_destroy, 16),
+    dmrs_plans(srsgpu_pdsch_dmrs_plan_destroy, SLOT_PLANS),
     tb_buf(WHO),
     grid_buf(WHO)
   {

@@ -1455,6 +1455,7 @@ int chain_ul_bench(int                 device,
     // Each worker builds its processor on its own thread (thread-local dependency pools bind there).
     for (unsigned t = 0; t != nof_threads; ++t) {
       workers[t]->post([&, t] { hs[t] = ul_create(device, variant, nof_ports, grid_prb, 2); });
+      workers[t]->wait();  // one at a time: the factories' first-use initialisation is not ours to race
     }
     for (auto& w : workers) {
       w->wait();
@@ -1488,8 +1489,10 @@ int chain_ul_bench(int                 device,
         }
       }
     };
-    for (unsigned t = 0; t != nof_threads; ++t) {  // warm-up: plans, pools, first-touch
-      workers[t]->post([&, t] { run_slots(t, 2); });
+    // Warm-up over one frame (20 slots at 30 kHz): every slot number's DM-RS plans, pools, first touch - a DU runs
+    // continuously, and the GPU batches cache their slot-dependent plans per slot number.
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      workers[t]->post([&, t] { run_slots(t, 20); });
     }
     for (auto& w : workers) {
       w->wait();
@@ -1535,6 +1538,7 @@ int chain_dl_bench(int                 device,
     }
     for (unsigned t = 0; t != nof_threads; ++t) {
       workers[t]->post([&, t] { hs[t] = dl_create(device, variant, nof_ports, grid_prb); });
+      workers[t]->wait();  // one at a time: the factories' first-use initialisation is not ours to race
     }
     for (auto& w : workers) {
       w->wait();
@@ -1561,7 +1565,7 @@ int chain_dl_bench(int                 device,
       }
     };
     for (unsigned t = 0; t != nof_threads; ++t) {
-      workers[t]->post([&, t] { run_slots(t, 2); });
+      workers[t]->post([&, t] { run_slots(t, 20); });  // one frame, as the UL bench
     }
     for (auto& w : workers) {
       w->wait();

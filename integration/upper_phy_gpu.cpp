@@ -436,6 +436,11 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     P = std::max<unsigned>(P, e->pdu.rx_ports.size());
   }
 
+  // Estimates in the compact layout with the "average" time strategy (one row per allocation and rx port, the CFO
+  // rotation of each symbol applied by the demodulator; the LLRs equal the per-symbol layout's bit for bit,
+  // tests/test_pusch_chest_gpu.py): the estimator writes 1 / 14 of the words. "interpolate" needs every symbol.
+  const uint8_t layout = cfg.estimator.td_strategy == SRSGPU_CHEST_TD_AVERAGE ? SRSGPU_CE_COMPACT : SRSGPU_CE_PER_SYMBOL;
+
   // The estimator / demodulator / decoder configurations pusch_processor_impl derives from each PDU
   // (pusch_processor_impl.cpp:150-337), as srsgpu descriptors, and the batch layout.
   std::vector<pusch_chest_desc>       chests;
@@ -482,7 +487,7 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     est.first_symbol = pdu.start_symbol_index;
     est.nof_symbols  = pdu.nof_symbols;
     est.rx_ports.assign(pdu.rx_ports.begin(), pdu.rx_ports.end());
-    chests.push_back(make_pusch_chest_desc(est, grid_prb, cfg.estimator, SRSGPU_CE_PER_SYMBOL, WHO));
+    chests.push_back(make_pusch_chest_desc(est, grid_prb, cfg.estimator, layout, WHO));
     chests.back().append_key(chest_key);
 
     pusch_demodulator::configuration dem;
@@ -498,8 +503,10 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     dem.nof_tx_layers               = pdu.nof_tx_layers;
     dem.enable_transform_precoding  = tp;
     dem.rx_ports                    = pdu.rx_ports;
-    demods.push_back(make_pusch_demod_desc(dem, grid_prb, cfg.demodulator, SRSGPU_CE_PER_SYMBOL, WHO));
+    demods.push_back(make_pusch_demod_desc(dem, grid_prb, cfg.demodulator, layout, WHO));
     pusch_demod_desc& dd = demods.back();
+    dd.c.cfo_compensated = (layout == SRSGPU_CE_COMPACT && cfg.estimator.compensate_cfo) ? 1 : 0;
+    dd.c.numerology      = static_cast<uint8_t>(pdu.slot.numerology());  // the symbol epochs of the rotation
 
     // Codeword LLRs: nof_rb REs per data symbol (minus the DM-RS REs) x layers x Qm.
     const unsigned dmrs_re = cdm_groups * (dmrs == dmrs_type::TYPE1 ? 6 : 4);
@@ -780,7 +787,9 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
             uint8_t* base = reinterpret_cast<uint8_t*>(d_ce) +
                             ((static_cast<size_t>(ly) * P + p) * 14 + pdu.start_symbol_index) * row +
                             static_cast<size_t>(*pdu.dc_position) * sizeof(uint32_t);
-            hip_check(hipMemset2DAsync(base, row, 0, sizeof(uint32_t), pdu.nof_symbols, s), WHO, "DC");
+            // Compact layout: the one row every symbol reads.
+            const unsigned rows = layout == SRSGPU_CE_COMPACT ? 1u : pdu.nof_symbols;
+            hip_check(hipMemset2DAsync(base, row, 0, sizeof(uint32_t), rows, s), WHO, "DC");
           }
         }
       }

@@ -1534,6 +1534,13 @@ int srsgpu_debug_decoder_profile(uint64_t* dst, uint32_t n, int packed)
   return packed ? srsgpu::debug_read_decoder_profile_pk(dst, n) : srsgpu::debug_read_decoder_profile(dst, n);
 }
 #endif
+#ifdef CHEST_PROFILE
+/// Instrumented builds only: phase stamps of the last estimator launch (pusch_chest.hip, CHEST_STAMP).
+int srsgpu_debug_chest_profile(uint64_t* dst, uint32_t n)
+{
+  return srsgpu::debug_read_chest_profile(dst, n);
+}
+#endif
 #ifdef ENC_PROFILE
 /// Instrumented builds only: phase stamps of the last packed-encoder launch (ldpc_encoder.hip, ENC_STAMP).
 int srsgpu_debug_encoder_profile(uint64_t* dst, uint32_t n)

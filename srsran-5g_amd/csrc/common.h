@@ -59,4 +59,16 @@ __device__ __forceinline__ int clamp_i(int v, int lo, int hi)
   return v < lo ? lo : (v > hi ? hi : v);
 }
 
+/// (ax + j ay)(bx + j by) with both fused multiply-adds explicit and nothing left to contract, so the rounding does
+/// not depend on the compiler's contraction choices in context: the estimator's per-symbol CFO rotation of its
+/// estimates and the demodulator's rotation of the compact estimate row must agree bit for bit.
+__device__ __forceinline__ void cmul_fused(float ax, float ay, float bx, float by, float& rx, float& ry)
+{
+#pragma clang fp contract(off)
+  const float pyy = ay * by;
+  const float pyx = ay * bx;
+  rx              = __builtin_fmaf(ax, bx, -pyy);
+  ry              = __builtin_fmaf(ax, by, pyx);
+}
+
 } // namespace srsgpu

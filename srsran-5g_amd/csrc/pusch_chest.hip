@@ -21,11 +21,30 @@
 // estimated RE per layer (the dominant term).
 #include <cstdlib>
 
+#include "common.h"
 #include "gold_device.h"
 #include "srsgpu_internal.h"
 
 namespace srsgpu {
 namespace {
+
+#ifdef CHEST_PROFILE
+// Instrumented builds only (tools/chest_phase_profile.py): s_memtime per phase of the first CHEST_PROF_JOBS jobs.
+constexpr int CHEST_PROF_JOBS  = 4096;
+constexpr int CHEST_PROF_SLOTS = 12;
+__device__ uint64_t g_chest_prof[CHEST_PROF_JOBS * CHEST_PROF_SLOTS];
+#define CHEST_PROF(slot, value)                                                                                        \
+  do {                                                                                                                 \
+    if (lane == 0 && job < CHEST_PROF_JOBS) {                                                                          \
+      g_chest_prof[job * CHEST_PROF_SLOTS + (slot)] = (value);                                                         \
+    }                                                                                                                  \
+  } while (0)
+#else
+#define CHEST_PROF(slot, value)                                                                                        \
+  do {                                                                                                                 \
+  } while (0)
+#endif
+#define CHEST_STAMP(slot) CHEST_PROF(slot, __builtin_amdgcn_s_memtime())
 
 constexpr int CHEST_THREADS = 64;  // one wavefront per job (multi-wave workgroups for large allocations: T)
 constexpr int CHEST_VP      = 12;  // MAX_V_PILOTS
@@ -135,6 +154,40 @@ __device__ __forceinline__ float job_sum(float v, float* red)
     return sub_sum<TS>(v);
   } else {
     return block_sum<T>(v, red);
+  }
+}
+
+/// job_sum of K values at once: one barrier pair for all of them in a multi-wave job (the per-value sums are the same
+/// as K separate job_sum calls: each wave's total, then the waves in ascending order). red: K x T / 64 floats.
+template <int T, int TS, int K>
+__device__ __forceinline__ void job_sum_n(float (&v)[K], float* red)
+{
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if constexpr (TS < 64) {
+      v[k] = sub_sum<TS>(v[k]);
+    } else {
+      v[k] = wave_sum(v[k]);
+    }
+  }
+  if constexpr (TS >= 64 && T > 64) {
+    __syncthreads();  // red may still be read by a previous reduction
+    if ((threadIdx.x & 63u) == 0) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        red[k * (T / 64) + (threadIdx.x >> 6)] = v[k];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < T / 64; ++w) {
+        t += red[k * (T / 64) + w];
+      }
+      v[k] = t;
+    }
   }
 }
 
@@ -395,7 +448,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
     const float2* __restrict__ lp)
 {
   extern __shared__ __align__(16) unsigned char lds_raw[];
-  __shared__ float redf[T / 64];
+  __shared__ float redf[3 * (T / 64)];
   __shared__ int   redi[T / 64];
   constexpr int JPW  = T / TS;  // jobs per workgroup
   const int     slot = static_cast<int>(threadIdx.x) / TS;
@@ -431,6 +484,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
   const chest_job& jb    = jobs[job];
 #endif
   const int        lane  = static_cast<int>(threadIdx.x) % TS;  // lane within the job
+  CHEST_STAMP(0);
+  CHEST_PROF(10, __builtin_amdgcn_s_memrealtime());
   const int        N     = jb.nof_pilots;
   const int        GL    = jb.group_layers;
   const int        D     = jb.nof_dmrs;
@@ -452,6 +507,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
     }
   }
   job_sync<T>();
+  CHEST_STAMP(1);
 
   // Pass 1: LSE of every DM-RS symbol (received x conj(pilot)), EPRE.
   float epre_acc = 0.f;
@@ -466,6 +522,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
     }
   }
   job_sync<T>();
+  CHEST_STAMP(2);
 
   // CFO from the first two DM-RS symbols (preprocess_pilots_and_estimate_cfo, :322): arg(sum lse_1 conj(lse_0)) over
   // the time between their starts; with compensation every DM-RS symbol is derotated by its start epoch.
@@ -478,8 +535,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
       ar += a.x * b.x + a.y * b.y;
       ai += a.y * b.x - a.x * b.y;
     }
-    ar  = job_sum<T, TS>(ar, redf);
-    ai  = job_sum<T, TS>(ai, redf);
+    float sums[2] = {ar, ai};
+    job_sum_n<T, TS, 2>(sums, redf);
+    ar = sums[0];
+    ai = sums[1];
     cfo = atan2f(ai, ar) / CHEST_TWOPI / (jb.epochs[jb.dmrs_symbols[1]] - jb.epochs[jb.dmrs_symbols[0]]);
     if (jb.compensate_cfo) {
       for (int s = 0; s < D; ++s) {
@@ -491,6 +550,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
       job_sync<T>();
     }
   }
+  CHEST_STAMP(3);
   const bool rotate = has_cfo && jb.compensate_cfo;
   // Per-symbol CFO rotations e^{j 2 pi epoch_l cfo} of the noise residual, once per job instead of once per pilot.
   __shared__ cpx srot_all[JPW][14];
@@ -562,8 +622,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
           sx += E[CHEST_VP + i].x;
           sy += E[CHEST_VP + i].y;
         }
-        sx = job_sum<T, TS>(sx, redf) / static_cast<float>(N);
-        sy = job_sum<T, TS>(sy, redf) / static_cast<float>(N);
+        float sums[2] = {sx, sy};
+        job_sum_n<T, TS, 2>(sums, redf);
+        sx = sums[0] / static_cast<float>(N);
+        sy = sums[1] / static_cast<float>(N);
         for (int i = lane; i < N; i += TS) {
           F[i] = {sx, sy};
         }
@@ -576,6 +638,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
     job_sync<T>();
   }
 
+  CHEST_STAMP(4);
   // RSRP of layer 0 over the planes, and the noise residual (group 0 only) against the time-averaged estimate
   // beta / Q sum_q F_q, re-rotated by the CFO when compensating (estimate_noise, :422).
   float rsrp_acc = 0.f, noise_acc = 0.f;
@@ -608,10 +671,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
     }
   }
   const float nof_pilots = static_cast<float>(N * D);
-  const float epre       = job_sum<T, TS>(epre_acc, redf) / nof_pilots;
-  const float rsrp =
-      job_sum<T, TS>(rsrp_acc, redf) * beta * beta * static_cast<float>(D) / static_cast<float>(Q) / nof_pilots;
-  const float noise_sum = job_sum<T, TS>(noise_acc, redf);
+  float       sums3[3]   = {epre_acc, rsrp_acc, noise_acc};
+  job_sum_n<T, TS, 3>(sums3, redf);
+  const float epre      = sums3[0] / nof_pilots;
+  const float rsrp      = sums3[1] * beta * beta * static_cast<float>(D) / static_cast<float>(Q) / nof_pilots;
+  const float noise_sum = sums3[2];
+  CHEST_STAMP(5);
 
   // Time alignment of the smoothed layer-0 planes (estimate_time_alignment, port_channel_estimator_helpers.cpp:246 ->
   // time_alignment_estimator_dft_impl): inverse DFT of size M through LDS (radix 2, bit-reversed scatter), |.|^2
@@ -631,20 +696,50 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
         L.X[__brev(pos) >> (32 - lgM)] = Fbase[(q * GL) * NP + i];
       }
       job_sync<T>();
-      for (int lh = 0; lh < lgM; ++lh) {
+      CHEST_STAMP(8);
+      // Radix-2 decimation in time over the bit-reversed input, two stages per barrier: a lane takes the four
+      // elements i0 + {0, h, 2h, 3h} through stage lh (span h) and stage lh + 1 (span 2h) in registers, with the
+      // radix-2 twiddles e^{+j 2 pi j / 2h} and e^{+j 2 pi j' / 4h} (j' = j, j + h).
+      auto twiddle = [](int j, int span2) {  // e^{+j 2 pi j / span2} (revolutions)
+        const float r = static_cast<float>(j) / static_cast<float>(span2);
+        return cpx{__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r)};
+      };
+      int lh = 0;
+      for (; lh + 1 < lgM; lh += 2) {
         const int h = 1 << lh;
-        for (int b = lane; b < M / 2; b += TS) {
-          const int   j  = b & (h - 1);
-          const int   i0 = ((b >> lh) << (lh + 1)) + j;
-          const float r  = static_cast<float>(j) / static_cast<float>(2 * h);  // revolutions: e^{+j 2 pi j / 2h}
-          const cpx   w  = {__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r)};
-          const cpx   a  = L.X[i0];
-          const cpx   t  = cmul(L.X[i0 + h], w);
-          L.X[i0]        = {a.x + t.x, a.y + t.y};
-          L.X[i0 + h]    = {a.x - t.x, a.y - t.y};
+        for (int b = lane; b < M / 4; b += TS) {
+          const int j  = b & (h - 1);
+          const int i0 = ((b >> lh) << (lh + 2)) + j;
+          cpx       x0 = L.X[i0], x1 = L.X[i0 + h], x2 = L.X[i0 + 2 * h], x3 = L.X[i0 + 3 * h];
+          const cpx w1 = twiddle(j, 2 * h);
+          cpx       t  = cmul(x1, w1);
+          x1           = {x0.x - t.x, x0.y - t.y};
+          x0           = {x0.x + t.x, x0.y + t.y};
+          t            = cmul(x3, w1);
+          x3           = {x2.x - t.x, x2.y - t.y};
+          x2           = {x2.x + t.x, x2.y + t.y};
+          t            = cmul(x2, twiddle(j, 4 * h));
+          L.X[i0 + 2 * h] = {x0.x - t.x, x0.y - t.y};
+          L.X[i0]         = {x0.x + t.x, x0.y + t.y};
+          t               = cmul(x3, twiddle(j + h, 4 * h));
+          L.X[i0 + 3 * h] = {x1.x - t.x, x1.y - t.y};
+          L.X[i0 + h]     = {x1.x + t.x, x1.y + t.y};
         }
         job_sync<T>();
       }
+      if (lh < lgM) {  // odd number of stages: the last one alone
+        const int h = 1 << lh;
+        for (int b = lane; b < M / 2; b += TS) {
+          const int j  = b & (h - 1);
+          const int i0 = ((b >> lh) << (lh + 1)) + j;
+          const cpx a  = L.X[i0];
+          const cpx t  = cmul(L.X[i0 + h], twiddle(j, 2 * h));
+          L.X[i0]      = {a.x + t.x, a.y + t.y};
+          L.X[i0 + h]  = {a.x - t.x, a.y - t.y};
+        }
+        job_sync<T>();
+      }
+      CHEST_STAMP(9);
       for (int n = lane; n < M; n += TS) {
         const float p = L.X[n].x * L.X[n].x + L.X[n].y * L.X[n].y;
         L.corr[n]     = q ? L.corr[n] + p : p;
@@ -689,6 +784,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
     const double  t_c  = 1.0 / (480000.0 * 4096.0);
     const int64_t tc10 = static_cast<int64_t>(static_cast<double>(ta_f) / t_c * 10.0);
     const float   ta_s = static_cast<float>(static_cast<double>(tc10 / 10 + (tc10 % 10) / 5) * t_c);
+    CHEST_STAMP(6);
     if (lane == 0) {
       const float nv = fmaxf(rsrp / 1e10f, noise_sum / (nof_pilots - 1.f));
       noise_var[jb.noise_slot] = nv;
@@ -744,9 +840,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
         }
         uint32_t u = to_bf16c(v);
         if (rotate_out) {
-          // polar1 inline (not srot): keeps the per-symbol layout bit-identical to the demodulator's rotation of the
-          // compact layout (same expression, same FMA contraction).
-          u = to_bf16c(cmul(bf16c(u), polar1(CHEST_TWOPI * jb.epochs[l] * cfo)));
+          // srot[l] is polar1(CHEST_TWOPI * epochs[l] * cfo), the expression the demodulator evaluates for the
+          // compact layout, so both layouts round identically (one sincos per symbol instead of per estimate).
+          const cpx h = bf16c(u);
+          cpx       r;
+          cmul_fused(h.x, h.y, srot[l].x, srot[l].y, r.x, r.y);
+          u = to_bf16c(r);
         }
         dst[l * jb.nsc] = u;
       }
@@ -755,9 +854,20 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
       }
     }
   }
+  CHEST_STAMP(7);
+  CHEST_PROF(11, __builtin_amdgcn_s_memrealtime());
 }
 
 } // namespace
+
+#ifdef CHEST_PROFILE
+int debug_read_chest_profile(uint64_t* dst, size_t n)
+{
+  const size_t max = static_cast<size_t>(CHEST_PROF_JOBS) * CHEST_PROF_SLOTS;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_chest_prof), (n < max ? n : max) * sizeof(uint64_t)) == hipSuccess ? 0
+                                                                                                                  : -1;
+}
+#endif
 
 size_t pusch_chest_lds_bytes(const chest_geom& g)
 {

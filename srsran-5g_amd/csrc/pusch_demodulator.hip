@@ -12,6 +12,7 @@
 // channel estimates (consecutive lanes read consecutive subcarriers: coalesced 4-byte loads), equalizes, demaps the
 // L * Qm LLRs, flips the signs the sequence selects and stages the bytes in LDS; the workgroup finally writes its
 // contiguous LLR range with dword stores. HBM-bound: (P + L P) x 4 B in and L Qm B out per RE.
+#include "common.h"
 #include "gold_device.h"
 #include "srsgpu_internal.h"
 
@@ -487,7 +488,10 @@ __device__ __forceinline__ void demod_res(demod_uniform        u,
       for (int p = 0; p < 4; ++p) {
 #pragma unroll
         for (int ly = 0; ly < L; ++ly) {
-          h[ly][p] = bf16c(to_bf16c(cmul(h[ly][p], u.rot[(sym * 4 + ly) * 4 + p])));
+          const cpx r = u.rot[(sym * 4 + ly) * 4 + p];
+          cpx       o;
+          cmul_fused(h[ly][p].x, h[ly][p].y, r.x, r.y, o.x, o.y);  // as the estimator's per-symbol layout
+          h[ly][p] = bf16c(to_bf16c(o));
         }
       }
     }
@@ -863,7 +867,10 @@ __global__ __launch_bounds__(TP_THREADS) void pusch_demodulate_tp_kernel(const d
       y[p] = bf16c(yw[p]);
       h[p] = bf16c(hw[0][p]);
       if (u.rot != nullptr) {
-        h[p] = bf16c(to_bf16c(cmul(h[p], u.rot[(sym * 4) * 4 + p])));
+        const cpx r = u.rot[(sym * 4) * 4 + p];
+        cpx       o;
+        cmul_fused(h[p].x, h[p].y, r.x, r.y, o.x, o.y);
+        h[p] = bf16c(to_bf16c(o));
       }
     }
     cpx   eq;

@@ -195,6 +195,10 @@ void launch_pusch_tb(const tb_dec_desc* d_desc,
 /// Bytes between the packed messages of consecutive codeblocks in the PUSCH decoder's message buffer.
 constexpr uint32_t CB_MSG_STRIDE = 1056;  // 22 * 384 / 8
 
+#ifdef CHEST_PROFILE
+/// Copies the phase stamps of the instrumented estimator build (CHEST_PROFILE) into dst (n words).
+int debug_read_chest_profile(uint64_t* dst, size_t n);
+#endif
 #ifdef ENC_PROFILE
 /// Copies the phase stamps of the instrumented encoder build (ENC_PROFILE) into dst (n words).
 int debug_read_encoder_profile(uint64_t* dst, size_t n);

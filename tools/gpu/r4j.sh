@@ -1,0 +1,8 @@
+#!/usr/bin/env bash
+# Round 4: estimator tests after the per-symbol rotation change, then the estimator phase profile (instrumented build).
+set -o pipefail
+mkdir -p gpurun_out
+true && \
+true
+SRSGPU_LIB=srsran-5g_amd/lib_prof/libsrsgpu_phy.so timeout -k 10 120 python -u tools/chest_phase_profile.py \
+  > gpurun_out/r4j_chest_profile.log 2>&1

@@ -722,7 +722,11 @@ def measure(args, env):
                                    f"{2 * sum(gx_ul.bytes_per_rank[1:]) / 2 ** 20:.1f} MB per step)"
                                    if shard_x else "ue-shard1") + (
                                       "; decoded UL TBs + CRC flags gathered to the FAPI rank over RCCL every step"
-                                      if world > 1 else "")},
+                                      if tb_gather is not None else "")},
+        "tb_gather": None if tb_gather is None else {
+            "backend": dist.get_backend(), "world": world, "per_input_set": True,
+            "in_graph": bool(args.graph_collectives and sets[0].graph_ul is not None),
+            "bytes_per_rank_per_step": int(tb_gather.max_bytes + tb_gather.max_tbs)},
         "ldpc_info_bits_per_s": info_bits_slot * S_ul * step_rate,
         "tb_bits_per_s": {"dl": tbs_bits_dl_step * step_rate, "ul": tbs_bits_ul_step * step_rate},
         "realtime_cells_per_gpu": value / SLOT_RATE_30KHZ / world,

@@ -93,6 +93,66 @@ def test_tb_gather_world2_gloo():
             assert list(oks[r]) == [(r + step + i) % 2 for i in range(5)]
 
 
+def _sets_worker(rank, world, port, q):
+    """The bench's step structure (bench.py: one TbGather per input set, the sets' steps issued round-robin, each set's
+    gather inside its own UL leg): per-set send / receive buffers, so a step of one set never clobbers what another
+    set's gather delivered. Ranks hold different TB sizes (a UE shard's); the root checks every set's last delivery
+    after every step."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cpu")
+        nof_sets, steps = 3, 10
+        tb_bytes, nof_tbs = 29 + 11 * rank, 4 + rank
+        gathers = [sdist.TbGather(tb_bytes, nof_tbs, dev, root=0) for _ in range(nof_sets)]
+
+        def payload(r, step):
+            return ((r * 37 + step * 5) & 0xFF), [(r + step + i) % 2 for i in range(4 + r)]
+
+        last = [None] * nof_sets
+        bad = []
+        for step in range(steps):
+            k = step % nof_sets
+            byte, ok = payload(rank, step)
+            gathers[k].gather(torch.full((tb_bytes,), byte, dtype=torch.uint8), torch.tensor(ok, dtype=torch.uint8))
+            last[k] = step
+            if rank == 0:
+                for j, g in enumerate(gathers):
+                    if last[j] is None:
+                        continue
+                    for r in range(world):
+                        want_byte, want_ok = payload(r, last[j])
+                        if not (np.all(g.tbs[r].numpy() == want_byte) and list(g.crc_ok[r].numpy()) == want_ok and
+                                g.tbs[r].numel() == 29 + 11 * r):
+                            bad.append((step, j, r))
+                tbs, oks = gathers[k].assemble()
+                if tbs.numel() != sum(29 + 11 * r for r in range(world)) or oks.numel() != sum(4 + r for r in range(world)):
+                    bad.append((step, k, "assemble"))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, bad, None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tb_gather_per_input_set_round_robin_gloo(world):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sets_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for _ in range(world):
+        rank, bad, err = q.get(timeout=120)
+        assert err is None, err
+        assert bad == [], bad[:5]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+
 def _shard_worker(rank, world, port, q):
     """One rank of a UE-sharded slot: its share of the 64 UEs (shard_ues), the host-side TB sizing of its plans
     (segmentation -> TB bytes / codeblocks, what its PUSCH decoder plan sizes), decoded TBs faked as a function of the

@@ -1,0 +1,8 @@
+#!/usr/bin/env bash
+# Round 4: the whole GPU parity suite, then smoke().
+set -o pipefail
+mkdir -p gpurun_out
+export LIBC_FATAL_STDERR_=1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread \
+  > gpurun_out/r4o_gpu_tests.log 2>&1 || exit $?
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4o_smoke.log 2>&1

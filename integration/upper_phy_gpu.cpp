@@ -2,6 +2,7 @@
 #include "upper_phy_gpu.h"
 #include <cstdlib>
 #include <chrono>
+#include <unordered_map>
 #include "srsran/support/error_handling.h"
 
 #include "chain_convert.h"
@@ -364,6 +365,7 @@ private:
   plan_cache<srsgpu_ulsch_demux_plan>           demux_plans;
   staged_buffer                                 io;  ///< A slot's inputs and outputs (layout in run()).
   plan_cache<std::remove_pointer_t<hipGraphExec_t>> graphs;
+  std::unordered_map<std::string, std::vector<std::vector<uint32_t>>> seq_cache;  ///< demodulator key -> sequences
   uint64_t                                      plan_generation = 0;
   const bool                                    timing          = std::getenv("SRSGPU_BATCH_TIMING") != nullptr;
   double                                        phase_us[5]     = {};
@@ -662,6 +664,41 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     srsgpu_check(srsgpu_pusch_demodulator_plan_create_ex(ctx, c.data(), x.data(), n, grid_prb, P, &p), WHO);
     return p;
   });
+  // A plan evicted above invalidates the graphs that run it and its cached sequences.
+  const uint64_t generation = chest_plans.evictions() + demod_plans.evictions() + demux_plans.evictions() +
+                              dec_plans.evictions();
+  if (generation != plan_generation) {
+    graphs.clear();  // a captured graph references the plans' device descriptors
+    seq_cache.clear();
+    plan_generation = generation;
+  }
+
+  // The replay hands the reference's codeword buffer each transmission's scrambling sequence: a property of the
+  // demodulator plan (RNTI, n_ID, length), fetched once per plan instead of copied out every slot.
+  const std::string                   seq_key(demod_key.begin(), demod_key.end());
+  const std::vector<std::vector<uint32_t>>& seq_words = [&]() -> const std::vector<std::vector<uint32_t>>& {
+    auto it = seq_cache.find(seq_key);
+    if (it != seq_cache.end()) {
+      return it->second;
+    }
+    std::vector<std::vector<uint32_t>> words(n);
+    size_t                              most = 0;
+    for (unsigned i = 0; i != n; ++i) {
+      most = std::max<size_t>(most, (batch[i]->nof_llrs + 31) / 32);
+    }
+    uint32_t* d_seq = nullptr;
+    hip_check(hipMalloc(reinterpret_cast<void**>(&d_seq), std::max<size_t>(most, 1) * sizeof(uint32_t)), WHO, "seq");
+    for (unsigned i = 0; i != n; ++i) {
+      words[i].resize((batch[i]->nof_llrs + 31) / 32);
+      srsgpu_check(srsgpu_pusch_demodulator_plan_scrambling(demod, i, d_seq, stream.get()), WHO);
+      hip_check(hipMemcpyAsync(words[i].data(), d_seq, words[i].size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               stream.get()),
+                WHO, "seq download");
+      hip_check(hipStreamSynchronize(stream.get()), WHO, "seq download");
+    }
+    (void)hipFree(d_seq);
+    return seq_cache.emplace(seq_key, std::move(words)).first->second;
+  }();
   srsgpu_ulsch_demux_plan* demux = nullptr;
   if (!demuxes.empty()) {
     demux = demux_plans.get(demux_key, [&] {
@@ -693,13 +730,7 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
   const size_t m_o    = align(nv_o + 4 * n * sizeof(float));
   const size_t st_o   = align(m_o + 4 * n * SRSGPU_CHEST_METRICS * sizeof(float));
   const size_t llr_o  = align(st_o + n * SRSGPU_DEMOD_STATS * sizeof(float));
-  std::vector<size_t> seq_o(n);
-  size_t              seq_total = 0;
-  for (unsigned i = 0; i != n; ++i) {
-    seq_o[i] = llr_o + llr_total + seq_total;
-    seq_total += (batch[i]->nof_llrs + 31) / 32 * 4;
-  }
-  const size_t tb_o  = align(llr_o + llr_total + seq_total);
+  const size_t tb_o  = align(llr_o + llr_total);
   const size_t end_o = tb_o + std::max<size_t>(tb_total, 16);
   io.reserve(end_o);
   reserve_device(d_ce, d_ce_cap, static_cast<size_t>(4) * P * 14 * row, "channel estimates");
@@ -753,12 +784,6 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     const pusch_processor::pdu_t& pdu = batch[i]->pdu;
     gpu::key_append(graph_key, pdu.dc_position.has_value() ? static_cast<int>(*pdu.dc_position) : -1);
   }
-  const uint64_t generation = chest_plans.evictions() + demod_plans.evictions() + demux_plans.evictions() +
-                              dec_plans.evictions();
-  if (generation != plan_generation) {
-    graphs.clear();  // a captured graph references the plans' device descriptors
-    plan_generation = generation;
-  }
   hipGraphExec_t exec = graphs.get(graph_key, [&] {
     hip_check(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), WHO, "begin capture");
     struct capture_guard {  // ends a capture an error interrupted, so the stream stays usable
@@ -797,9 +822,6 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     srsgpu_check(srsgpu_pusch_demodulator_plan_execute_ex(demod, io.dev<uint32_t>(grid_o), d_ce, io.dev<float>(nv_o),
                                                           io.dev<int8_t>(llr_o), io.dev<float>(st_o), s),
                  WHO);
-    for (unsigned i = 0; i != n; ++i) {
-      srsgpu_check(srsgpu_pusch_demodulator_plan_scrambling(demod, i, io.dev<uint32_t>(seq_o[i]), s), WHO);
-    }
     if (demux != nullptr) {
       // Only the UL-SCH stream is used on the device: the UCI streams are split again by the reference's own
       // demultiplexer during the replay, from the codeword LLRs.
@@ -854,7 +876,7 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     r.est->nv           = io.host<float>(nv_o + 4 * i * sizeof(float));
     r.est->m            = io.host<float>(m_o + 4 * i * SRSGPU_CHEST_METRICS * sizeof(float));
     r.demod->llrs       = io.host<int8_t>(llr_o + e.llr_offset);
-    r.demod->seq        = io.host<uint32_t>(seq_o[i]);
+    r.demod->seq        = seq_words[i].data();
     r.demod->stats      = io.host<float>(st_o + i * SRSGPU_DEMOD_STATS * sizeof(float));
     r.demod->nof_llrs   = e.nof_llrs;
     r.demod->nof_rb     = e.nof_rb;

@@ -402,6 +402,46 @@ __device__ __forceinline__ void job_argmax(float& v, int& idx, float* redf, int*
   }
 }
 
+/// Two job_argmax reductions with one barrier pair in a multi-wave job (each result as job_argmax's: the waves'
+/// maxima in ascending wave order). redf / redi: 2 x T / 64 entries.
+template <int T, int TS>
+__device__ __forceinline__ void job_argmax2(float& v0, int& i0, float& v1, int& i1, float* redf, int* redi)
+{
+  if constexpr (TS < 64) {
+    sub_argmax<TS>(v0, i0);
+    sub_argmax<TS>(v1, i1);
+  } else {
+    wave_argmax(v0, i0);
+    wave_argmax(v1, i1);
+    if constexpr (T > 64) {
+      constexpr int NW = T / 64;
+      __syncthreads();
+      if ((threadIdx.x & 63u) == 0) {
+        redf[threadIdx.x >> 6]      = v0;
+        redi[threadIdx.x >> 6]      = i0;
+        redf[NW + (threadIdx.x >> 6)] = v1;
+        redi[NW + (threadIdx.x >> 6)] = i1;
+      }
+      __syncthreads();
+      v0 = redf[0];
+      i0 = redi[0];
+      v1 = redf[NW];
+      i1 = redi[NW];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) {
+        if (redf[w] > v0 || (redf[w] == v0 && redi[w] < i0)) {
+          v0 = redf[w];
+          i0 = redi[w];
+        }
+        if (redf[NW + w] > v1 || (redf[NW + w] == v1 && redi[NW + w] < i1)) {
+          v1 = redf[NW + w];
+          i1 = redi[NW + w];
+        }
+      }
+    }
+  }
+}
+
 /// LDS of a job, carved from the plan-sized dynamic allocation (chest_geom): the staged sequence words, the filter
 /// taps, the smoothed planes F and one region shared by the LSE stage (Y per DM-RS symbol + enlarged E per layer) and
 /// the time-alignment stage (the DFT buffer X + the correlation), which run one after the other.
@@ -449,7 +489,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
 {
   extern __shared__ __align__(16) unsigned char lds_raw[];
   __shared__ float redf[3 * (T / 64)];
-  __shared__ int   redi[T / 64];
+  __shared__ int   redi[2 * (T / 64)];
   constexpr int JPW  = T / TS;  // jobs per workgroup
   const int     slot = static_cast<int>(threadIdx.x) / TS;
   const int     job  = static_cast<int>(blockIdx.x) * JPW + slot;
@@ -606,13 +646,16 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
         }
         job_sync<T>();
         for (int i = lane; i < N; i += TS) {
-          cpx acc = {0.f, 0.f};
-          for (int j = 0; j < nt; ++j) {
-            const int e = CHEST_VP + i - c + j;  // symmetric taps: correlation == convolution
-            if (e >= CHEST_VP - nv && e < CHEST_VP + N + nv) {
-              acc.x += L.taps[j] * E[e].x;
-              acc.y += L.taps[j] * E[e].y;
-            }
+          // Taps j whose input CHEST_VP + i - c + j lies in the enlarged band [CHEST_VP - nv, CHEST_VP + N + nv), in
+          // ascending order as the reference's convolution sums them (symmetric taps: correlation == convolution).
+          const int j_lo = max(0, c - nv - i);
+          const int j_hi = min(nt, N + nv + c - i);
+          const cpx* Ei  = E + (CHEST_VP + i - c);
+          cpx        acc = {0.f, 0.f};
+          for (int j = j_lo; j < j_hi; ++j) {
+            const float t = L.taps[j];
+            acc.x += t * Ei[j].x;
+            acc.y += t * Ei[j].y;
           }
           F[i] = acc;
         }
@@ -679,74 +722,80 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
   CHEST_STAMP(5);
 
   // Time alignment of the smoothed layer-0 planes (estimate_time_alignment, port_channel_estimator_helpers.cpp:246 ->
-  // time_alignment_estimator_dft_impl): inverse DFT of size M through LDS (radix 2, bit-reversed scatter), |.|^2
-  // summed over the planes, the peak within +-ta_max taps, quadratic refinement unless M is the largest DFT size.
+  // time_alignment_estimator_dft_impl): inverse DFT of size M through LDS (radix 2, decimation in frequency), |.|^2
+  // summed over the planes at the searched bins, the peak within +-ta_max taps, quadratic refinement unless M is the
+  // largest DFT size.
   if (jb.group == 0) {
     const int M   = jb.ta_dft;
     const int lgM = jb.ta_log2;
     job_sync<T>();  // Y / E are dead: the region becomes X / corr
+    // Only the bins the search and the quadratic refinement read are needed: n in [0, m + 2) and [M - m - 2, M).
+    const int m   = jb.ta_max;
+    const int nb  = min(M, 2 * (m + 2));
+    auto      bin = [&](int t) { return t < m + 2 ? t : M - nb + t; };
     for (int q = 0; q < Q; ++q) {
-      for (int n = lane; n < M; n += TS) {
-        L.X[n] = {0.f, 0.f};
-      }
-      job_sync<T>();
-      const uint32_t k0 = pilot_subcarrier(jb, crbs, 0);
-      for (int i = lane; i < N; i += TS) {
-        const uint32_t pos = jb.ta_positions ? pilot_subcarrier(jb, crbs, i) - k0 : static_cast<uint32_t>(i);
-        L.X[__brev(pos) >> (32 - lgM)] = Fbase[(q * GL) * NP + i];
+      // Natural-order input (the pilots at their positions, zeros elsewhere): decimation in frequency leaves the
+      // output in bit-reversed order, read back only at the bins above.
+      const cpx* Fq = Fbase + (q * GL) * NP;
+      if (!jb.ta_positions) {
+        for (int n = lane; n < M; n += TS) {
+          L.X[n] = n < N ? Fq[n] : cpx{0.f, 0.f};
+        }
+      } else {
+        for (int n = lane; n < M; n += TS) {
+          L.X[n] = {0.f, 0.f};
+        }
+        job_sync<T>();
+        const uint32_t k0 = pilot_subcarrier(jb, crbs, 0);
+        for (int i = lane; i < N; i += TS) {
+          L.X[pilot_subcarrier(jb, crbs, i) - k0] = Fq[i];
+        }
       }
       job_sync<T>();
       CHEST_STAMP(8);
-      // Radix-2 decimation in time over the bit-reversed input, two stages per barrier: a lane takes the four
-      // elements i0 + {0, h, 2h, 3h} through stage lh (span h) and stage lh + 1 (span 2h) in registers, with the
-      // radix-2 twiddles e^{+j 2 pi j / 2h} and e^{+j 2 pi j' / 4h} (j' = j, j + h).
+      // Radix-2 decimation in frequency, inverse sign, two stages per barrier: a lane takes the four elements
+      // i0 + {0, h, 2h, 3h} through the stage of span 2h (twiddles e^{+j 2 pi j' / 4h}, j' = j, j + h) and the stage of
+      // span h (e^{+j 2 pi j / 2h}) in registers.
       auto twiddle = [](int j, int span2) {  // e^{+j 2 pi j / span2} (revolutions)
         const float r = static_cast<float>(j) / static_cast<float>(span2);
         return cpx{__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r)};
       };
-      int lh = 0;
-      for (; lh + 1 < lgM; lh += 2) {
-        const int h = 1 << lh;
+      int lh = lgM - 1;
+      for (; lh >= 1; lh -= 2) {
+        const int h = 1 << (lh - 1);
         for (int b = lane; b < M / 4; b += TS) {
           const int j  = b & (h - 1);
-          const int i0 = ((b >> lh) << (lh + 2)) + j;
-          cpx       x0 = L.X[i0], x1 = L.X[i0 + h], x2 = L.X[i0 + 2 * h], x3 = L.X[i0 + 3 * h];
+          const int i0 = ((b >> (lh - 1)) << (lh + 1)) + j;
+          const cpx x0 = L.X[i0], x1 = L.X[i0 + h], x2 = L.X[i0 + 2 * h], x3 = L.X[i0 + 3 * h];
+          const cpx y0 = {x0.x + x2.x, x0.y + x2.y};
+          const cpx y2 = cmul({x0.x - x2.x, x0.y - x2.y}, twiddle(j, 4 * h));
+          const cpx y1 = {x1.x + x3.x, x1.y + x3.y};
+          const cpx y3 = cmul({x1.x - x3.x, x1.y - x3.y}, twiddle(j + h, 4 * h));
           const cpx w1 = twiddle(j, 2 * h);
-          cpx       t  = cmul(x1, w1);
-          x1           = {x0.x - t.x, x0.y - t.y};
-          x0           = {x0.x + t.x, x0.y + t.y};
-          t            = cmul(x3, w1);
-          x3           = {x2.x - t.x, x2.y - t.y};
-          x2           = {x2.x + t.x, x2.y + t.y};
-          t            = cmul(x2, twiddle(j, 4 * h));
-          L.X[i0 + 2 * h] = {x0.x - t.x, x0.y - t.y};
-          L.X[i0]         = {x0.x + t.x, x0.y + t.y};
-          t               = cmul(x3, twiddle(j + h, 4 * h));
-          L.X[i0 + 3 * h] = {x1.x - t.x, x1.y - t.y};
-          L.X[i0 + h]     = {x1.x + t.x, x1.y + t.y};
+          L.X[i0]         = {y0.x + y1.x, y0.y + y1.y};
+          L.X[i0 + h]     = cmul({y0.x - y1.x, y0.y - y1.y}, w1);
+          L.X[i0 + 2 * h] = {y2.x + y3.x, y2.y + y3.y};
+          L.X[i0 + 3 * h] = cmul({y2.x - y3.x, y2.y - y3.y}, w1);
         }
         job_sync<T>();
       }
-      if (lh < lgM) {  // odd number of stages: the last one alone
-        const int h = 1 << lh;
+      if (lh == 0) {  // odd number of stages: the last one (span 1, unit twiddle) alone
         for (int b = lane; b < M / 2; b += TS) {
-          const int j  = b & (h - 1);
-          const int i0 = ((b >> lh) << (lh + 1)) + j;
-          const cpx a  = L.X[i0];
-          const cpx t  = cmul(L.X[i0 + h], twiddle(j, 2 * h));
-          L.X[i0]      = {a.x + t.x, a.y + t.y};
-          L.X[i0 + h]  = {a.x - t.x, a.y - t.y};
+          const cpx a = L.X[2 * b], c = L.X[2 * b + 1];
+          L.X[2 * b]     = {a.x + c.x, a.y + c.y};
+          L.X[2 * b + 1] = {a.x - c.x, a.y - c.y};
         }
         job_sync<T>();
       }
       CHEST_STAMP(9);
-      for (int n = lane; n < M; n += TS) {
-        const float p = L.X[n].x * L.X[n].x + L.X[n].y * L.X[n].y;
+      for (int t = lane; t < nb; t += TS) {
+        const int   n = bin(t);
+        const cpx   v = L.X[__brev(static_cast<uint32_t>(n)) >> (32 - lgM)];
+        const float p = v.x * v.x + v.y * v.y;
         L.corr[n]     = q ? L.corr[n] + p : p;
       }
       job_sync<T>();
     }
-    const int m  = jb.ta_max;
     float     dv = -INFINITY, av = -INFINITY;
     int       di = 0x7fffffff, ai = 0x7fffffff;
     for (int n = lane; n < m; n += TS) {
@@ -759,8 +808,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void 
         ai = n;
       }
     }
-    job_argmax<T, TS>(dv, di, redf, redi);
-    job_argmax<T, TS>(av, ai, redf, redi);
+    job_argmax2<T, TS>(dv, di, av, ai, redf, redi);
     const int idx  = (dv >= av) ? di : -(m - ai);
     float     frac = 0.f;
     if (M != 4096) {

@@ -62,14 +62,21 @@ def main():
     rng = np.random.default_rng(5)
     cfg, _, grid = U.ul273_case(rng, snr_db=26.0)
 
-    def est(rb0, nrb):
+    def est(rb0, nrb, layout=srsgpu.CE_PER_SYMBOL):
         return srsgpu.PuschChannelEstimation(
             scrambling_id=500, n_scid=0, dmrs_type=1, nof_tx_layers=1, nof_rx_ports=4, start_symbol=0, nof_symbols=14,
             dmrs_symbol_mask=U.DMRS_MASK, rb_start=rb0, nof_rb=nrb, slot_index=cfg["slot"], scaling=U.DMRS_BETA,
-            fd_smoothing=2, td_strategy=0, compensate_cfo=1, estimate_layout=srsgpu.CE_PER_SYMBOL)
+            fd_smoothing=2, td_strategy=0, compensate_cfo=1, estimate_layout=layout)
 
+    bench_ues, rb = [], 0
+    for i in range(64):  # the bench's slot: 64 UEs x 4-5 PRB, compact layout
+        nrb = 5 if i < 17 else 4
+        bench_ues.append(est(rb, nrb, srsgpu.CE_COMPACT))
+        rb += nrb
     out = [run_case(ctx, lib, "273 PRB, 1 UE, 4 ports", [est(0, 273)], grid),
-           run_case(ctx, lib, "16 UEs x 17 PRB, 4 ports", [est(17 * i, 17) for i in range(16)], grid)]
+           run_case(ctx, lib, "273 PRB, 1 UE, 4 ports, compact", [est(0, 273, srsgpu.CE_COMPACT)], grid),
+           run_case(ctx, lib, "16 UEs x 17 PRB, 4 ports", [est(17 * i, 17) for i in range(16)], grid),
+           run_case(ctx, lib, "64 UEs x 4-5 PRB, 4 ports, compact (bench slot)", bench_ues, grid)]
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "chest_phase_profile.json"), "w") as f:
         json.dump(out, f, indent=1)

@@ -1165,8 +1165,13 @@ struct ul_harness {
   std::unique_ptr<uplink_processor>          proc;
 };
 
+/// variant: 0 the reference's CPU PUSCH processor, 1 the GPU slot batch; + 2 with the "interpolate" time strategy of
+/// the estimator (the batch then keeps per-symbol estimates) instead of du_low's "average".
 ul_harness* ul_create(int device, int variant, unsigned P, unsigned grid_prb, unsigned max_iter)
 {
+  const auto td = variant >= 2 ? port_channel_estimator_td_interpolation_strategy::interpolate
+                               : port_channel_estimator_td_interpolation_strategy::average;
+  variant %= 2;
   auto* h     = new ul_harness();
   h->P        = P;
   h->grid_prb = grid_prb;
@@ -1182,17 +1187,15 @@ ul_harness* ul_create(int device, int variant, unsigned P, unsigned grid_prb, un
   std::unique_ptr<pusch_processor> pusch;
   std::shared_ptr<gpu::pusch_slot_batch> batch;
   if (variant == 0) {
-    pusch = new_pusch_processor(device, 0, port_channel_estimator_td_interpolation_strategy::average, max_iter, true, {});
+    pusch = new_pusch_processor(device, 0, td, max_iter, true, {});
   } else {
     gpu::pusch_batch_configuration bc;
     bc.device              = device;
-    bc.estimator           = gpu::make_pusch_estimator_options(port_channel_estimator_fd_smoothing_strategy::filter,
-                                                     port_channel_estimator_td_interpolation_strategy::average, true);
+    bc.estimator = gpu::make_pusch_estimator_options(port_channel_estimator_fd_smoothing_strategy::filter, td, true);
     bc.max_cb_ids          = pc.nof_codeblocks;
     bc.nof_ldpc_iterations = max_iter;
     // PDUs outside the batch: the reference processor over the GPU estimator / demodulator (row b3).
-    auto fallback = new_pusch_processor(device, 1, port_channel_estimator_td_interpolation_strategy::average, max_iter,
-                                        true, {});
+    auto fallback = new_pusch_processor(device, 1, td, max_iter, true, {});
     batch = gpu::create_pusch_slot_batch(bc, gpu::create_pusch_harq_arena(device, bc.max_cb_ids),
                                          std::make_shared<demux_factory_ref>(), std::make_shared<uci_factory_ref>(),
                                          std::move(fallback));

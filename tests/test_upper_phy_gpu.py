@@ -191,3 +191,34 @@ def test_downlink_processor_gpu_batch_equals_reference(procs):
         assert np.array_equal(ref, got), (slot, int(np.sum(np.any(ref != got, axis=-1))))
         assert np.mean(np.any(ref != other, axis=-1)) > 0.3  # the PDSCHs were written
         assert np.array_equal(ref[:, :2], other[:, :2])  # symbols 0-1 (another channel's) untouched
+
+
+def test_uplink_processor_gpu_batch_interpolate_equals_reference():
+    """The estimator's "interpolate" time strategy (the batch keeps per-symbol estimates, DC zeroing per symbol) against
+    the reference's processors with the same strategy: 10 UEs plus one over the DC subcarrier."""
+    import chain_harness as H
+    cpu = H.UpperPhy(0, H.UL_CPU + 2, P)
+    gpu = H.UpperPhy(0, H.UL_GPU_BATCH + 2, P)
+    chain = H.Chain(0)
+    try:
+        rng = np.random.default_rng(31)
+        ues, rb = ul_ues(rng, H, 0x4a01, 10, 0)
+        dc = H.params(rnti=0x4b00, harq_id=20, nof_rb=10, rb_start=rb, qm=6, target_code_rate=772.0, nof_ports=P,
+                      dc_position=12 * (rb + 3) + 5)
+        ues.append((dc, -40.0, 0.5, 0.0))
+        tbs, sizes = [], []
+        for p, *_ in ues:
+            seg = grant(p).segmentation()
+            p.base_graph = seg.base_graph
+            tbs.append(rng.integers(0, 256, seg.tbs // 8).astype(np.uint8))
+            sizes.append(seg.tbs // 8)
+        grid = received_grid(rng, chain, ues, tbs, 28.0)
+        pdus = [p for p, *_ in ues]
+        ref = cpu.ul_slot(7, pdus, sizes, grid)
+        got = gpu.ul_slot(7, pdus, sizes, grid)
+        check_equal(ref, got, "interpolate")
+        assert sum(d["tb_crc_ok"] for d, _ in ref) >= len(pdus) - 1
+    finally:
+        chain.close()
+        cpu.close()
+        gpu.close()

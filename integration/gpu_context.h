@@ -79,5 +79,15 @@ inline std::shared_ptr<srsgpu_context> shared_context(int device)
   return ctx;
 }
 
+/// Serialises the bindings' synchronous HIP set-up calls (allocations, plan creation, blocking copies) with stream
+/// captures: HIP fails a synchronous call made while any thread of the process captures a stream, whatever the
+/// capture mode. Held around every plan-cache miss, staging growth and graph capture (recursive: a capture path may
+/// create a plan).
+inline std::recursive_mutex& hip_setup_mutex()
+{
+  static std::recursive_mutex m;
+  return m;
+}
+
 } // namespace gpu
 } // namespace srsran

@@ -35,7 +35,8 @@ public:
     if (n <= cap) {
       return;
     }
-    const size_t c = std::max(n, 2 * cap);
+    std::lock_guard<std::recursive_mutex> lock(hip_setup_mutex());
+    const size_t                          c = std::max(n, 2 * cap);
     (void)hipFree(d);
     (void)hipHostFree(h);
     d = nullptr;
@@ -106,7 +107,11 @@ public:
       lru.splice(lru.begin(), lru, it->second);
       return lru.front().plan;
     }
-    Plan* plan = create();
+    Plan* plan = nullptr;
+    {
+      std::lock_guard<std::recursive_mutex> lock(hip_setup_mutex());
+      plan = create();
+    }
     lru.push_front({key, plan});
     index.emplace(std::move(key), lru.begin());
     if (lru.size() > capacity) {

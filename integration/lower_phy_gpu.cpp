@@ -375,6 +375,7 @@ public:
         plans.push_back(p);
       }
     }
+    graphs.assign(plans.size(), nullptr);
     unsigned max_size = 0;
     for (unsigned n : geo.size) {
       max_size = std::max(max_size, n);
@@ -390,6 +391,11 @@ public:
   ~puxch_processor_gpu() override
   {
     (void)hipStreamSynchronize(stream.get());
+    for (hipGraphExec_t g : graphs) {
+      if (g != nullptr) {
+        (void)hipGraphExecDestroy(g);
+      }
+    }
     for (srsgpu_ofdm_plan* p : plans) {
       srsgpu_ofdm_plan_destroy(p);
     }
@@ -434,10 +440,29 @@ private:
       srsran_assert(in.size() == n, "The input buffer size ({}) does not match the symbol size ({}).", in.size(), n);
       std::memcpy(st.in.host<cf_t>(static_cast<size_t>(p) * n * sizeof(cf_t)), in.data(), n * sizeof(cf_t));
     }
-    st.in.upload(0, static_cast<size_t>(nof_ports) * n * sizeof(cf_t), hs);
-    gpu::srsgpu_check(srsgpu_ofdm_demodulator_plan_execute(plans[s], st.in.dev<float>(), st.out.dev<uint32_t>(), hs),
-                      WHO);
-    st.out.download(0, static_cast<size_t>(nof_ports) * nsc * sizeof(uint32_t), hs);
+    // Upload, demodulation and download of this symbol position as one captured graph (built on first use): a
+    // symbol costs one launch instead of three dependent queue operations (~9 us apart each).
+    hipGraphExec_t& exec = graphs[s];
+    if (exec == nullptr) {
+      std::lock_guard<std::recursive_mutex> lock(gpu::hip_setup_mutex());
+      gpu::hip_check(hipStreamBeginCapture(hs, hipStreamCaptureModeRelaxed), WHO, "begin capture");
+      hipGraph_t graph = nullptr;
+      try {
+        st.in.upload(0, static_cast<size_t>(nof_ports) * n * sizeof(cf_t), hs);
+        gpu::srsgpu_check(
+            srsgpu_ofdm_demodulator_plan_execute(plans[s], st.in.dev<float>(), st.out.dev<uint32_t>(), hs), WHO);
+        st.out.download(0, static_cast<size_t>(nof_ports) * nsc * sizeof(uint32_t), hs);
+      } catch (...) {
+        (void)hipStreamEndCapture(hs, &graph);
+        (void)hipGraphDestroy(graph);
+        throw;
+      }
+      gpu::hip_check(hipStreamEndCapture(hs, &graph), WHO, "end capture");
+      const hipError_t r = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      gpu::hip_check(r, WHO, "graph instantiate");
+    }
+    gpu::hip_check(hipGraphLaunch(exec, hs), WHO, "graph launch");
     gpu::hip_check(hipEventRecord(st.done, hs), WHO, "event");
     pending.push_back({l, context});
     // Deliver what has finished; bound the symbols in flight; the slot's last symbol drains the slot.
@@ -500,6 +525,7 @@ private:
   unsigned                                   nsc;
   unsigned                                   max_symbols_in_flight;
   std::vector<srsgpu_ofdm_plan*>             plans;  ///< One plan (all ports) per symbol of the subframe.
+  std::vector<hipGraphExec_t>                graphs;  ///< per plan: upload + demodulation + download
   std::vector<std::unique_ptr<symbol_stage>> stages;
   std::deque<pending_symbol>                 pending;
   std::atomic<bool>                          stopped  = false;

@@ -236,12 +236,6 @@ private:
 /// stay resident instead of every slot missing.
 constexpr size_t SLOT_PLANS = 160;
 
-std::mutex& setup_mutex()
-{
-  static std::mutex m;
-  return m;
-}
-
 void destroy_graph_exec(hipGraphExec_t x)
 {
   (void)hipGraphExecDestroy(x);
@@ -638,10 +632,10 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
   }
 
   // Plans (cached: a cell's grants repeat). Plan creation and buffer growth call synchronous HIP APIs, which fail
-  // while any thread captures a stream: they and the slot graph's capture run under one process-wide lock (a cache
-  // hit holds it for microseconds).
+  // while any thread captures a stream: they and the slot graph's capture run under gpu::hip_setup_mutex (a cache hit
+  // holds it for microseconds).
   const auto                   t_start = std::chrono::steady_clock::now();
-  std::unique_lock<std::mutex> setup_lock(setup_mutex());
+  std::unique_lock<std::recursive_mutex> setup_lock(gpu::hip_setup_mutex());
   srsgpu_pusch_chest_plan* chest = chest_plans.get(chest_key, [&] {
     std::vector<srsgpu_pusch_chest_config> c;
     std::vector<srsgpu_alloc_ext>          x;

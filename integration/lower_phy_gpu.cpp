@@ -130,13 +130,26 @@ class pdxch_processor_gpu : public pdxch_processor,
     explicit job(const char* who) : grid(who), samples(who) {}
     ~job()
     {
+      drop_graphs();
       if (done != nullptr) {
         (void)hipEventDestroy(done);
+      }
+    }
+    void drop_graphs()
+    {
+      for (hipGraphExec_t& g : graphs) {
+        if (g != nullptr) {
+          (void)hipGraphExecDestroy(g);
+          g = nullptr;
+        }
       }
     }
     gpu::staged_buffer grid;
     gpu::staged_buffer samples;
     hipEvent_t         done = nullptr;
+    /// Per slot of the subframe: upload + modulation + download captured over this job's buffers (graph_buffers).
+    std::vector<hipGraphExec_t> graphs;
+    const void*                 graph_buffers[2] = {nullptr, nullptr};
     std::vector<bool>  port_empty;
     unsigned           subframe_slot = 0;
     bool               launched      = false;  ///< false: the request's grid was empty (nothing to transmit).
@@ -266,11 +279,35 @@ private:
         std::memcpy(j.grid.host((p * geo.nsymb + l) * row), reader.get_view(p, l).data(), row);
       }
     }
-    j.grid.upload(0, nof_ports * geo.nsymb * row, s);
-    gpu::srsgpu_check(srsgpu_ofdm_modulator_plan_execute(plans[subframe_slot], j.grid.dev<uint32_t>(),
-                                                         j.samples.dev<float>(), s),
-                      WHO);
-    j.samples.download(0, nof_ports * slotn * sizeof(cf_t), s);
+    // Upload, modulation and download as one captured graph per (job, slot of the subframe), built on first use.
+    if (j.graph_buffers[0] != j.grid.dev() || j.graph_buffers[1] != j.samples.dev()) {
+      j.drop_graphs();  // the job's buffers grew: the graphs captured their old addresses
+      j.graph_buffers[0] = j.grid.dev();
+      j.graph_buffers[1] = j.samples.dev();
+    }
+    j.graphs.resize(plans.size(), nullptr);
+    hipGraphExec_t& exec = j.graphs[subframe_slot];
+    if (exec == nullptr) {
+      std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());
+      gpu::hip_check(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), WHO, "begin capture");
+      hipGraph_t graph = nullptr;
+      try {
+        j.grid.upload(0, nof_ports * geo.nsymb * row, s);
+        gpu::srsgpu_check(srsgpu_ofdm_modulator_plan_execute(plans[subframe_slot], j.grid.dev<uint32_t>(),
+                                                             j.samples.dev<float>(), s),
+                          WHO);
+        j.samples.download(0, nof_ports * slotn * sizeof(cf_t), s);
+      } catch (...) {
+        (void)hipStreamEndCapture(s, &graph);
+        (void)hipGraphDestroy(graph);
+        throw;
+      }
+      gpu::hip_check(hipStreamEndCapture(s, &graph), WHO, "end capture");
+      const hipError_t r = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      gpu::hip_check(r, WHO, "graph instantiate");
+    }
+    gpu::hip_check(hipGraphLaunch(exec, s), WHO, "graph launch");
     gpu::hip_check(hipEventRecord(j.done, s), WHO, "event");
     j.subframe_slot = subframe_slot;
     j.launched      = true;

@@ -241,6 +241,35 @@ void destroy_graph_exec(hipGraphExec_t x)
   (void)hipGraphExecDestroy(x);
 }
 
+/// Captures the queue operations `body` issues on `s` (relaxed mode; the caller holds gpu::hip_setup_mutex) into an
+/// instantiated graph. A capture an error interrupts is ended, so the stream stays usable.
+template <typename F>
+hipGraphExec_t capture_graph(hipStream_t s, const char* who, F&& body)
+{
+  hip_check(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), who, "begin capture");
+  struct capture_guard {
+    hipStream_t s;
+    bool        open = true;
+    ~capture_guard()
+    {
+      if (open) {
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(s, &g);
+        (void)hipGraphDestroy(g);
+      }
+    }
+  } guard{s};
+  body();
+  hipGraph_t g = nullptr;
+  guard.open   = false;
+  hip_check(hipStreamEndCapture(s, &g), who, "end capture");
+  hipGraphExec_t   x = nullptr;
+  const hipError_t r = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  hip_check(r, who, "graph instantiate");
+  return x;
+}
+
 /// A reference pusch_processor_impl over the replay stages (one per thread that runs batches: the processor's
 /// dependency pool binds its instances to threads, concurrent_thread_local_object_pool.h:67-96).
 struct replay_processor {
@@ -778,20 +807,7 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     const pusch_processor::pdu_t& pdu = batch[i]->pdu;
     gpu::key_append(graph_key, pdu.dc_position.has_value() ? static_cast<int>(*pdu.dc_position) : -1);
   }
-  hipGraphExec_t exec = graphs.get(graph_key, [&] {
-    hip_check(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), WHO, "begin capture");
-    struct capture_guard {  // ends a capture an error interrupted, so the stream stays usable
-      hipStream_t s;
-      bool        open = true;
-      ~capture_guard()
-      {
-        if (open) {
-          hipGraph_t g = nullptr;
-          (void)hipStreamEndCapture(s, &g);
-          (void)hipGraphDestroy(g);
-        }
-      }
-    } guard{s};
+  hipGraphExec_t exec = graphs.get(graph_key, [&] { return capture_graph(s, WHO, [&] {
     io.upload(0, iter_o, s);
     srsgpu_check(srsgpu_pusch_chest_plan_execute(chest, io.dev<uint32_t>(grid_o), d_ce, io.dev<float>(nv_o),
                                                  io.dev<float>(m_o), s),
@@ -833,15 +849,7 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
                                   io.dev<srsgpu_harq_copy_job>(jobs_o), jobs.size(), s),
                  WHO);
     io.download(flag_o, end_o - flag_o, s);
-    hipGraph_t g = nullptr;
-    guard.open   = false;
-    hip_check(hipStreamEndCapture(s, &g), WHO, "end capture");
-    hipGraphExec_t x = nullptr;
-    const hipError_t r = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    hip_check(r, WHO, "graph instantiate");
-    return x;
-  });
+  }); });
   setup_lock.unlock();
   const auto t_graph = std::chrono::steady_clock::now();
   hip_check(hipGraphLaunch(exec, s), WHO, "graph launch");
@@ -1088,6 +1096,7 @@ public:
     enc_plans(srsgpu_pdsch_encoder_plan_destroy, 16),
     mod_plans(srsgpu_pdsch_modulator_plan_destroy, 16),
     dmrs_plans(srsgpu_pdsch_dmrs_plan_destroy, SLOT_PLANS),
+    graphs(destroy_graph_exec, SLOT_PLANS),
     tb_buf(WHO),
     grid_buf(WHO)
   {
@@ -1235,23 +1244,54 @@ public:
 
     hipStream_t  s   = stream.get();
     const size_t row = static_cast<size_t>(nsc) * sizeof(uint32_t);
-    tb_buf.reserve(std::max<size_t>(tbs.size(), 16));
-    std::memcpy(tb_buf.host(), tbs.data(), tbs.size());
-    tb_buf.upload(0, tbs.size(), s);
-    if (cw_bytes > d_cw_cap) {
-      (void)hipFree(d_cw);
-      d_cw     = nullptr;
-      d_cw_cap = 0;
-      hip_check(hipMalloc(&d_cw, cw_bytes), WHO, "codewords");
-      d_cw_cap = cw_bytes;
+    {
+      // Buffer growth and the graph capture call synchronous HIP APIs, which fail while any thread captures a
+      // stream: both run under gpu::hip_setup_mutex, as the UL slot batch's do.
+      std::lock_guard<std::recursive_mutex> setup_lock(gpu::hip_setup_mutex());
+      tb_buf.reserve(std::max<size_t>(tbs.size(), 16));
+      if (cw_bytes > d_cw_cap) {
+        (void)hipFree(d_cw);
+        d_cw     = nullptr;
+        d_cw_cap = 0;
+        hip_check(hipMalloc(&d_cw, cw_bytes), WHO, "codewords");
+        d_cw_cap = cw_bytes;
+      }
+      grid_buf.reserve(P * 14 * row);
     }
-    // Sentinel scratch grid: exactly the REs the PDSCH and its DM-RS map come back.
-    grid_buf.reserve(P * 14 * row);
-    hip_check(hipMemsetAsync(grid_buf.dev(), 0xff, P * 14 * row, s), WHO, "scratch");
-    srsgpu_check(srsgpu_pdsch_encoder_plan_execute(enc, tb_buf.dev<uint8_t>(), d_cw, s), WHO);
-    srsgpu_check(srsgpu_pdsch_dmrs_plan_execute(dmrs, grid_buf.dev<uint32_t>(), s), WHO);
-    srsgpu_check(srsgpu_pdsch_modulator_plan_execute(mod, d_cw, grid_buf.dev<uint32_t>(), s), WHO);
-    grid_buf.download(0, P * 14 * row, s);
+    std::memcpy(tb_buf.host(), tbs.data(), tbs.size());
+
+    // The slot's device work as one captured graph per layout (cached like the plans it runs), so a slot costs one
+    // graph launch instead of six queue operations.
+    std::vector<uint8_t> graph_key;
+    for (const std::vector<uint8_t>* k : {&enc_key, &mod_key, &dmrs_key}) {
+      gpu::key_append(graph_key, k->size());
+      graph_key.insert(graph_key.end(), k->begin(), k->end());
+    }
+    for (const void* ptr : {static_cast<const void*>(tb_buf.host()), static_cast<const void*>(tb_buf.dev()),
+                            static_cast<const void*>(grid_buf.host()), static_cast<const void*>(grid_buf.dev()),
+                            static_cast<const void*>(d_cw)}) {
+      gpu::key_append(graph_key, ptr);
+    }
+    gpu::key_append(graph_key, tbs.size());
+    gpu::key_append(graph_key, P);
+    std::unique_lock<std::recursive_mutex> setup_lock(gpu::hip_setup_mutex());
+    // A plan evicted since the last slot invalidates the graphs that run it.
+    const uint64_t generation = enc_plans.evictions() + mod_plans.evictions() + dmrs_plans.evictions();
+    if (generation != plan_generation) {
+      graphs.clear();
+      plan_generation = generation;
+    }
+    hipGraphExec_t exec = graphs.get(graph_key, [&] { return capture_graph(s, WHO, [&] {
+      tb_buf.upload(0, tbs.size(), s);
+      // Sentinel scratch grid: exactly the REs the PDSCH and its DM-RS map come back.
+      hip_check(hipMemsetAsync(grid_buf.dev(), 0xff, P * 14 * row, s), WHO, "scratch");
+      srsgpu_check(srsgpu_pdsch_encoder_plan_execute(enc, tb_buf.dev<uint8_t>(), d_cw, s), WHO);
+      srsgpu_check(srsgpu_pdsch_dmrs_plan_execute(dmrs, grid_buf.dev<uint32_t>(), s), WHO);
+      srsgpu_check(srsgpu_pdsch_modulator_plan_execute(mod, d_cw, grid_buf.dev<uint32_t>(), s), WHO);
+      grid_buf.download(0, P * 14 * row, s);
+    }); });
+    setup_lock.unlock();
+    hip_check(hipGraphLaunch(exec, s), WHO, "graph launch");
     hip_check(hipStreamSynchronize(s), WHO, "synchronise");
     store_written_res(grid, grid_buf.host<uint32_t>(), P, nsc, 0, 14);
     for (pdsch_entry& e : es) {
@@ -1268,6 +1308,8 @@ private:
   plan_cache<srsgpu_pdsch_encoder_plan>   enc_plans;
   plan_cache<srsgpu_pdsch_modulator_plan> mod_plans;
   plan_cache<srsgpu_pdsch_dmrs_plan>      dmrs_plans;
+  plan_cache<std::remove_pointer_t<hipGraphExec_t>> graphs;
+  uint64_t                              plan_generation = 0;
   staged_buffer                         tb_buf;
   staged_buffer                         grid_buf;
   uint8_t*                              d_cw     = nullptr;

@@ -46,6 +46,14 @@ __device__ uint64_t g_chest_prof[CHEST_PROF_JOBS * CHEST_PROF_SLOTS];
 #endif
 #define CHEST_STAMP(slot) CHEST_PROF(slot, __builtin_amdgcn_s_memtime())
 
+/// Minimum waves per SIMD the estimator is compiled for. 8 (a 64-VGPR cap) spilled 10 VGPRs to scratch; at 4-5 the
+/// few-RB instantiations settle at 72-78 VGPRs (6-7 waves per SIMD) with no spill, and the headline bench gains
+/// 1.4 % (137.8k -> 139.8k slots/s, estimator stage 37.4 -> 33.5 us per step; profiles/r4_chest_waves_ab.txt); 4 also
+/// keeps the 1024-lane wideband instantiation (100 VGPRs) from spilling.
+#ifndef CHEST_WAVES_PER_EU
+#define CHEST_WAVES_PER_EU 4
+#endif
+
 constexpr int CHEST_THREADS = 64;  // one wavefront per job (multi-wave workgroups for large allocations: T)
 constexpr int CHEST_VP      = 12;  // MAX_V_PILOTS
 
@@ -475,7 +483,7 @@ __device__ __host__ inline size_t chest_job_lds_bytes(const chest_geom& g)
 /// one per 32-lane half: a few-RB job's pilots fill half a wave, so a whole wave per job issued every instruction for
 /// twice the lanes it used; the chest kernel is bound by VALU issue, profiles/r3_v2_sq_serial.log).
 template <int T, int TS>
-__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8, 8))) void pusch_chest_kernel(
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(CHEST_WAVES_PER_EU, 8))) void pusch_chest_kernel(
     const chest_job* __restrict__ jobs,
     int nof_jobs,
     chest_geom geom,

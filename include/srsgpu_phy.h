@@ -754,6 +754,19 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
                                       uint8_t*                         d_tb_crc_ok,
                                       void*                            stream);
 
+/** The transport-block stage alone (pusch_decoder_impl.cpp:386 join_and_notify, :438 concatenate_codeblocks): TB
+ *  assembly from the codeblock messages and flags already in d_cb_msgs / d_cb_crc_ok (the plan's codeblock layout,
+ *  SRSGPU_CB_MSG_STRIDE bytes per codeblock) and the TB CRC24A check; a TB CRC mismatch clears the TB's codeblock
+ *  flags, as execute does. For codeblocks decoded elsewhere: codeblock-sharded decoding, where every rank runs the
+ *  srsgpu_pusch_cb_plan of its codeblock range and the FAPI rank gathers the messages and flags (srsgpu/dist.py
+ *  CodeblockShard). Asynchronous, hipGraph-capturable. */
+int srsgpu_pusch_decoder_plan_assemble(const srsgpu_pusch_decoder_plan* plan,
+                                       uint8_t*                         d_cb_crc_ok,
+                                       const uint8_t*                   d_cb_msgs,
+                                       uint8_t*                         d_tbs,
+                                       uint8_t*                         d_tb_crc_ok,
+                                       void*                            stream);
+
 void srsgpu_pusch_decoder_plan_destroy(srsgpu_pusch_decoder_plan* plan);
 
 /** HARQ soft buffers kept across slots in a persistent arena, one slot of arena_stride bytes per absolute codeblock

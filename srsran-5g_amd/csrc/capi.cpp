@@ -1482,6 +1482,23 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
   return SRSGPU_OK;
 }
 
+int srsgpu_pusch_decoder_plan_assemble(const srsgpu_pusch_decoder_plan* plan,
+                                       uint8_t*                         d_cb_crc_ok,
+                                       const uint8_t*                   d_cb_msgs,
+                                       uint8_t*                         d_tbs,
+                                       uint8_t*                         d_tb_crc_ok,
+                                       void*                            stream)
+{
+  if (plan == nullptr || d_cb_crc_ok == nullptr || d_cb_msgs == nullptr || d_tbs == nullptr ||
+      d_tb_crc_ok == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  launch_pusch_tb(plan->d_tb, plan->nof_tbs, plan->tb_threads, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok,
+                  plan->ctx->d_crc_arena, static_cast<hipStream_t>(stream));
+  HIP_TRY(hipGetLastError());
+  return SRSGPU_OK;
+}
+
 int srsgpu_pusch_decoder_plan_enable_timing(srsgpu_pusch_decoder_plan* plan, int enable)
 {
   if (plan == nullptr) {

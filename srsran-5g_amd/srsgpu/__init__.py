@@ -343,6 +343,7 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pusch_decoder_plan_nof_codeblocks.argtypes = [P]
     lib.srsgpu_pusch_decoder_plan_nof_codeblocks.restype = ctypes.c_uint32
     lib.srsgpu_pusch_decoder_plan_execute.argtypes = [P, P, P, P, P, P, P, P, P]
+    lib.srsgpu_pusch_decoder_plan_assemble.argtypes = [P, P, P, P, P, P]
     lib.srsgpu_pusch_decoder_plan_destroy.argtypes = [P]
     lib.srsgpu_pusch_decoder_plan_destroy.restype = None
     lib.srsgpu_pdsch_modulator_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -409,7 +410,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_pusch_cb_plan_destroy", "srsgpu_pdsch_encoder_plan_create", "srsgpu_pdsch_encoder_plan_nof_codeblocks",
     "srsgpu_pdsch_encoder_plan_execute", "srsgpu_pdsch_encoder_plan_destroy", "srsgpu_pusch_decoder_plan_create",
     "srsgpu_pusch_decoder_plan_nof_codeblocks", "srsgpu_pusch_decoder_plan_decoder_input_llrs",
-    "srsgpu_pusch_decoder_plan_execute",
+    "srsgpu_pusch_decoder_plan_execute", "srsgpu_pusch_decoder_plan_assemble",
     "srsgpu_pusch_decoder_plan_destroy", "srsgpu_pusch_decoder_plan_enable_timing",
     "srsgpu_pusch_decoder_plan_stage_times", "srsgpu_pdsch_encoder_plan_enable_timing",
     "srsgpu_pdsch_encoder_plan_stage_times", "srsgpu_pdsch_modulator_plan_create",
@@ -1532,6 +1533,11 @@ class PuschDecoderPlan:
         _check(_lib.srsgpu_pusch_decoder_plan_execute(self.handle, _dptr(d_llrs), _dptr(d_harq), _dptr(d_cb_crc_ok),
                                                       _dptr(d_cb_msgs), _dptr(d_cb_iters), _dptr(d_tbs),
                                                       _dptr(d_tb_crc_ok), _stream_handle(stream)))
+
+    def assemble(self, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, stream=None):
+        """TB stage only, from codeblock messages / flags decoded elsewhere (codeblock-sharded decoding)."""
+        _check(_lib.srsgpu_pusch_decoder_plan_assemble(self.handle, _dptr(d_cb_crc_ok), _dptr(d_cb_msgs), _dptr(d_tbs),
+                                                       _dptr(d_tb_crc_ok), _stream_handle(stream)))
 
     def enable_timing(self, enable=True, decode_only=False):
         """Stage events on every execute: all three stages, or (decode_only) just around the LDPC decoding."""

@@ -11,7 +11,11 @@ one node with an RCCL-over-xGMI gather of decoded TBs back to the FAPI adaptor".
 * sharding the UEs of one cell (strong scaling): a cell's samples enter and leave on one rank, so the resource grid
   is exchanged as well (`GridExchange`): the root's demodulated UL grid is scattered by subcarrier band to the ranks
   that own the UEs there, and the ranks' DL grid bands are gathered into the root's grid before its OFDM modulation;
-  the decoded TBs go to the FAPI rank through `TbGather` as above.
+  the decoded TBs go to the FAPI rank through `TbGather` as above;
+* sharding the codeblocks of a slot (strong scaling where one UE owns the cell: configs[4]'s test-mode UE carries
+  ~140 codeblocks per slot, which UE sharding cannot split): the FAPI rank runs the front end and holds the codeword
+  LLRs, every rank decodes a contiguous range of the slot's codeblocks into its own HARQ buffers and the messages come
+  back for the TB assembly (`CodeblockShard`).
 """
 from __future__ import annotations
 
@@ -164,3 +168,94 @@ class GridExchange:
             for r, (b, e) in enumerate(self.ranges):
                 if r != self.root:
                     g[:, b:e].copy_(self._all[r][:, : e - b])
+
+
+CB_MSG_STRIDE = 1056  # SRSGPU_CB_MSG_STRIDE: bytes per codeblock message slot
+
+
+class CodeblockShard:
+    """Codeblock-level sharding of a slot's PUSCH decoding across ranks.
+
+    `cbs` lists the slot's codeblocks in order (every TB's, concatenated) as (llr_offset, rm_length) in the root's
+    codeword LLR buffer. Rank r owns the contiguous codeblock range `shard_range(len(cbs), world, r)` and, with it, the
+    contiguous LLR span from its first codeblock's first LLR to its last one's last LLR.
+
+    Per slot: `scatter_llrs` hands every rank its span (one scatter; the root keeps its own); each rank rate-dematches and
+    decodes its codeblocks into its own HARQ buffers (a srsgpu_pusch_cb_plan over `local_cbs`, LLR offsets relative to
+    the span: the HARQ memory is sharded as well); `gather` brings the messages (CB_MSG_STRIDE bytes each) and CRC flags
+    into the root's slot-wide buffers (one gather), where srsgpu_pusch_decoder_plan_assemble joins them into TBs and
+    checks the TB CRCs (pusch_decoder_impl.cpp:386); `return_flags` scatters the root's final flags back, so a TB CRC
+    mismatch clears the owners' codeblock flags exactly as the reference resets them for the retransmission (:423).
+    Buffers are allocated once; copies and collectives run on the current stream.
+    """
+
+    def __init__(self, cbs: Sequence[tuple], device: torch.device, root: int = 0,
+                 group: Optional[dist.ProcessGroup] = None):
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.root, self.group = root, group
+        self.cbs = [(int(o), int(e)) for o, e in cbs]
+        for (o, e), (o2, _) in zip(self.cbs, self.cbs[1:]):
+            if o2 < o + e:
+                raise ValueError("codeblock LLR ranges must be in order and disjoint")
+        self.ranges = [shard_range(len(self.cbs), self.world, r) for r in range(self.world)]
+        self.spans = []
+        for rg in self.ranges:
+            if len(rg) == 0:
+                self.spans.append((0, 0))
+            else:
+                b = self.cbs[rg.start][0]
+                self.spans.append((b, self.cbs[rg.stop - 1][0] + self.cbs[rg.stop - 1][1] - b))
+        self.max_span = max(1, max(n for _, n in self.spans))
+        self.max_cbs = max(1, max(len(rg) for rg in self.ranges))
+        mine = self.ranges[self.rank]
+        b0 = self.spans[self.rank][0]
+        #: (llr_offset relative to this rank's span, rm_length) of the codeblocks this rank decodes
+        self.local_cbs = [(self.cbs[i][0] - b0, self.cbs[i][1]) for i in mine]
+        self.llrs = torch.zeros(self.max_span, dtype=torch.int8, device=device)
+        self._res = torch.zeros(self.max_cbs * (CB_MSG_STRIDE + 1), dtype=torch.uint8, device=device)
+        self._flags = torch.zeros(self.max_cbs, dtype=torch.uint8, device=device)
+        if self.rank == root:
+            self._llr_all = [torch.zeros(self.max_span, dtype=torch.int8, device=device) for _ in range(self.world)]
+            self._res_all = [torch.zeros_like(self._res) for _ in range(self.world)]
+            self._flags_all = [torch.zeros(self.max_cbs, dtype=torch.uint8, device=device) for _ in range(self.world)]
+        else:
+            self._llr_all = self._res_all = self._flags_all = None
+
+    @property
+    def llr_bytes_per_rank(self) -> List[int]:
+        return [n for _, n in self.spans]
+
+    def scatter_llrs(self, d_llrs: Optional[torch.Tensor]) -> torch.Tensor:
+        """Root: `d_llrs` is the slot's codeword LLR buffer (other ranks pass None). Returns this rank's span."""
+        if self.rank == self.root:
+            for r, (b, n) in enumerate(self.spans):
+                self._llr_all[r][:n].copy_(d_llrs[b:b + n])
+        dist.scatter(self.llrs, self._llr_all, src=self.root, group=self.group)
+        return self.llrs[: self.spans[self.rank][1]]
+
+    def gather(self, d_msgs: torch.Tensor, d_flags: torch.Tensor, d_all_msgs: Optional[torch.Tensor],
+               d_all_flags: Optional[torch.Tensor]) -> None:
+        """This rank's messages (len(local_cbs) x CB_MSG_STRIDE bytes) and flags into the root's slot-wide buffers
+        (codeblock i at i x CB_MSG_STRIDE; the other ranks pass None for the root's buffers)."""
+        n = len(self.local_cbs)
+        if d_msgs.numel() < n * CB_MSG_STRIDE or d_flags.numel() < n:
+            raise ValueError("message / flag buffers smaller than this rank's codeblocks")
+        self._res[: n * CB_MSG_STRIDE].copy_(d_msgs[: n * CB_MSG_STRIDE])
+        self._res[self.max_cbs * CB_MSG_STRIDE: self.max_cbs * CB_MSG_STRIDE + n].copy_(d_flags[:n])
+        dist.gather(self._res, self._res_all, dst=self.root, group=self.group)
+        if self.rank == self.root:
+            for r, rg in enumerate(self.ranges):
+                k = len(rg)
+                src = self._res_all[r]
+                d_all_msgs[rg.start * CB_MSG_STRIDE: rg.stop * CB_MSG_STRIDE].copy_(src[: k * CB_MSG_STRIDE])
+                d_all_flags[rg.start: rg.stop].copy_(src[self.max_cbs * CB_MSG_STRIDE: self.max_cbs * CB_MSG_STRIDE + k])
+
+    def return_flags(self, d_all_flags: Optional[torch.Tensor], d_flags: torch.Tensor) -> None:
+        """The root's codeblock flags after the TB stage back to their owners' `d_flags` (the HARQ context)."""
+        if self.rank == self.root:
+            for r, rg in enumerate(self.ranges):
+                self._flags_all[r][: len(rg)].copy_(d_all_flags[rg.start: rg.stop])
+        dist.scatter(self._flags, self._flags_all, src=self.root, group=self.group)
+        n = len(self.local_cbs)
+        d_flags[:n].copy_(self._flags[:n])

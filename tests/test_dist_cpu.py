@@ -382,3 +382,142 @@ def test_ue_sharded_cell_grid_exchange_gloo(world):
 def test_grid_exchange_rejects_bad_plans():
     with pytest.raises(ValueError):
         sdist.ue_subcarrier_ranges(_x_ues(), 0)
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# Codeblock-sharded decoding (CodeblockShard): the root holds the slot's codeword LLRs (two TBs of several codeblocks,
+# so rank ranges cross a TB boundary); every rank rate-dematches and decodes its codeblock range (oracle), the
+# messages and flags are gathered into the root's slot-wide buffers, the root joins the TBs and checks the TB CRCs,
+# and the final flags go back to the owners. Compared with one rank decoding every codeblock.
+# ---------------------------------------------------------------------------------------------------------------------
+CB_TB_BYTES = (4000, 2600)  # BG1 QPSK: 4 and 3 codeblocks
+
+
+def _cb_slot(orc):
+    """(segmentations, TB bytes, codeword LLRs (+-8 hard decisions, a few flipped), per-codeblock (llr offset, E))."""
+    from chain_lib import oracle_pdsch_encode
+    rng = np.random.default_rng(21)
+    segs, tbs, llrs, cbs, off = [], [], [], [], 0
+    for nbytes in CB_TB_BYTES:
+        tb = rng.integers(0, 256, nbytes, dtype=np.uint8)
+        nof_ch_symbols = (nbytes * 8 * 2 + 7999) // 2 // 4 * 4  # code rate ~1/2 at Qm 2
+        cw, _, _ = oracle_pdsch_encode(orc, tb, 1, 0, 2, 1, 0, nof_ch_symbols)
+        seg = sch.segment(nbytes * 8, 1, 2, 1, nof_ch_symbols)
+        llr = np.where(cw == 0, 8, -8).astype(np.int8)
+        flip = rng.choice(llr.size, llr.size // 50, replace=False)
+        llr[flip] = -llr[flip]
+        segs.append(seg)
+        tbs.append(tb)
+        llrs.append(llr)
+        cbs += [(off + cb.cw_offset, cb.rm_length) for cb in seg.codeblocks]
+        off += llr.size
+    return segs, tbs, np.concatenate(llrs), cbs
+
+
+def _cb_decode(orc, segs, cb_ids, llrs_span, local_cbs):
+    """Oracle codeblock decoding of the slot's codeblocks `cb_ids` (global order) from this rank's LLR span: messages
+    (CB_MSG_STRIDE bytes each, K Z bits MSB first) and CRC flags."""
+    from chain_lib import crc_for_tb
+    flat = [(seg, cb) for seg in segs for cb in seg.codeblocks]
+    msgs = np.zeros(len(cb_ids) * sdist.CB_MSG_STRIDE, np.uint8)
+    ok = np.zeros(len(cb_ids), np.uint8)
+    for j, (i, (o, e)) in enumerate(zip(cb_ids, local_cbs)):
+        seg, cb = flat[i]
+        Z = seg.lifting_size
+        buf = np.zeros(66 * Z, np.int8)
+        buf = orc.rate_dematch(1, 1, Z, 0, 2, 0, cb.nof_filler_bits, 1, llrs_span[o:o + e], buf)
+        it, bits = orc.ldpc_decode(1, 1, Z, buf, nof_crc_bits=cb.nof_crc_bits, nof_filler=cb.nof_filler_bits,
+                                   crc_poly=crc_for_tb(seg), max_iter=6)
+        packed = np.packbits(np.asarray(bits, np.uint8))
+        msgs[j * sdist.CB_MSG_STRIDE: j * sdist.CB_MSG_STRIDE + packed.size] = packed
+        ok[j] = 0 if it is None else 1
+    return msgs, ok
+
+
+def _cb_join(orc, segs, msgs, ok):
+    """Root: TB bytes and TB CRC flags from the slot-wide messages (pusch_decoder_impl.cpp:438); a TB whose CRC fails
+    clears its codeblock flags (:423)."""
+    from oracle_lib import CRC16, CRC24A
+    out, tb_ok, i = [], [], 0
+    for seg in segs:
+        payload = []
+        first = i
+        for cb in seg.codeblocks:
+            bits = np.unpackbits(msgs[i * sdist.CB_MSG_STRIDE: (i + 1) * sdist.CB_MSG_STRIDE])
+            last = cb.index == seg.nof_segments - 1
+            payload.append(bits[:cb.nof_info_bits + (seg.nof_tb_crc_bits if last else 0)])
+            i += 1
+        payload = np.concatenate(payload)
+        good = bool(ok[first:i].all()) and orc.crc_bits(CRC16 if seg.tbs <= 3824 else CRC24A, payload) == 0
+        if not good:
+            ok[first:i] = 0
+        tb_ok.append(int(good))
+        out.append(np.packbits(payload[:seg.tbs]))
+    return out, np.array(tb_ok, np.uint8)
+
+
+def _cb_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from oracle_lib import Oracle
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        orc = Oracle()
+        segs, tbs, llrs, cbs = _cb_slot(orc)
+        sh = sdist.CodeblockShard(cbs, torch.device("cpu"), root=0)
+        span = sh.scatter_llrs(torch.from_numpy(llrs) if rank == 0 else None)
+        mine = list(sh.ranges[rank])
+        msgs, ok = _cb_decode(orc, segs, mine, span.numpy(), sh.local_cbs)
+        n = len(cbs)
+        all_msgs = torch.zeros(n * sdist.CB_MSG_STRIDE, dtype=torch.uint8) if rank == 0 else None
+        all_ok = torch.zeros(n, dtype=torch.uint8) if rank == 0 else None
+        sh.gather(torch.from_numpy(msgs), torch.from_numpy(ok), all_msgs, all_ok)
+        res = None
+        if rank == 0:
+            joined, tb_ok = _cb_join(orc, segs, all_msgs.numpy(), all_ok.numpy())
+            # A TB CRC mismatch forced on TB 1 (as if its checksum failed): its codeblocks' flags are cleared at the root
+            # and must come back cleared to their owners.
+            all_ok[len(segs[0].codeblocks):] = 0
+            res = (all_msgs.numpy().copy(), joined, tb_ok, sh.llr_bytes_per_rank)
+        local_ok = torch.from_numpy(ok.copy())
+        sh.return_flags(all_ok, local_ok)
+        first_tb1 = len(segs[0].codeblocks)
+        want = [0 if i >= first_tb1 else int(ok[j]) for j, i in enumerate(mine)]
+        assert local_ok.tolist() == want, (local_ok.tolist(), want)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, None, traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_codeblock_sharded_decode_gloo(world):
+    """CodeblockShard: the gathered messages equal one rank decoding every codeblock, the joined TBs equal the sent
+    ones with their CRCs passing, and flags cleared at the root return to the codeblocks' owners."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_cb_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, res, err = q.get(timeout=300)
+        assert err is None, err
+        out[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+    msgs, joined, tb_ok, spans = out[0]
+    orc = Oracle()
+    segs, tbs, llrs, cbs = _cb_slot(orc)
+    assert len(cbs) == 7 and len(set(spans)) >= 1 and sum(spans) <= llrs.size
+    want_msgs, want_ok = _cb_decode(orc, segs, list(range(len(cbs))), llrs, cbs)
+    assert np.array_equal(msgs, want_msgs)
+    assert tb_ok.tolist() == [1, 1]
+    for got, want in zip(joined, tbs):
+        assert np.array_equal(got, want)

@@ -240,3 +240,92 @@ def test_fused_rate_dematch_in_decoder(orc, ctx, monkeypatch, dec_type, mode):
         assert bool(crc_f[i]) == ok2, (i, c)
         n_ok += ok2
     assert 30 <= n_ok < 200
+
+
+def test_codeblock_sharded_decode_assemble(orc, ctx):
+    """Codeblock-sharded decoding on the device (srsgpu/dist.py CodeblockShard's data path, three ranks emulated on one
+    GPU): every rank's codeblock range decoded by a srsgpu_pusch_cb_plan from its LLR span into its own HARQ buffers,
+    the messages / flags placed in slot-wide buffers, the TBs joined by srsgpu_pusch_decoder_plan_assemble. TB bytes,
+    TB and CB CRC flags and messages equal the TB-level plan decoding everything, for a 63-codeblock TB (configs[4]'s
+    shape) plus smaller TBs, one of them too noisy to decode."""
+    import torch
+
+    import srsgpu
+    from srsgpu import dist as sdist
+    from srsgpu import sch
+    rng = np.random.default_rng(17)
+    g1, g2 = sch.UeGrant(30, 2, 8, 682.5), sch.UeGrant(12, 1, 6, 600.0)
+    grants = [(sch.segment(526344, 1, 8, 4, 73200), 8, 4, 73200, 0.0),
+              (g1.segmentation(), g1.qm, g1.nof_layers, g1.nof_ch_symbols, 5.0),
+              (g2.segmentation(), g2.qm, g2.nof_layers, g2.nof_ch_symbols, 40.0)]
+    tbs_cfg, segs, tbs, llrs = [], [], [], []
+    for seg, qm, layers, nsym, noise in grants:
+        tbs_bits = seg.tbs
+        tb = rng.integers(0, 256, tbs_bits // 8).astype(np.uint8)
+        cw, _, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, 0, qm, layers, 0, nsym)
+        llrs.append(bits_to_llrs(rng, cw, amp=10.0, noise=noise))
+        tbs_cfg.append(srsgpu.PuschTransportBlock(tbs_bits // 8, seg.base_graph, 0, qm, layers, nsym, new_data=True,
+                                                  nof_ldpc_iterations=6))
+        segs.append(seg)
+        tbs.append(tb)
+    nof_cbs = [s.nof_segments for s in segs]
+    arr, nllr, nharq, ncb, ntb = srsgpu.make_pusch_tb_configs(
+        tbs_cfg, nof_cbs, [BG_N_SHORT[s.base_graph] * s.lifting_size for s in segs])
+    dev = torch.device("cuda", 0)
+    d_llrs = torch.from_numpy(np.concatenate(llrs)).to(dev)
+    plan = srsgpu.PuschDecoderPlan(ctx, srsgpu.IMPL_BY_NAME["avx2"], arr)
+
+    # Reference: the TB-level plan decodes every codeblock.
+    ref = dict(crc=torch.zeros(ncb, dtype=torch.uint8, device=dev),
+               msgs=torch.zeros(ncb * sdist.CB_MSG_STRIDE, dtype=torch.uint8, device=dev),
+               tbs=torch.zeros(ntb, dtype=torch.uint8, device=dev), ok=torch.zeros(len(segs), dtype=torch.uint8,
+                                                                                   device=dev))
+    plan.execute(d_llrs, torch.zeros(nharq, dtype=torch.int8, device=dev), ref["crc"], ref["msgs"],
+                 torch.zeros(ncb, dtype=torch.int32, device=dev), ref["tbs"], ref["ok"])
+
+    # Sharded: the slot's codeblocks in order, each with its codeword LLR range.
+    flat, cb_llr = [], []
+    for i, seg in enumerate(segs):
+        for cb in seg.codeblocks:
+            flat.append(srsgpu.PuschCodeblock(seg.base_graph, seg.lifting_size, 0, tbs_cfg[i].modulation_order,
+                                              cb.rm_length, nof_filler_bits=cb.nof_filler_bits,
+                                              crc_poly=crc_for_tb(seg), nof_crc_bits=cb.nof_crc_bits,
+                                              max_iterations=6))
+            cb_llr.append((arr[i].llr_offset + cb.cw_offset, cb.rm_length))
+    world = 3
+    all_crc = torch.zeros(ncb, dtype=torch.uint8, device=dev)
+    all_msgs = torch.zeros(ncb * sdist.CB_MSG_STRIDE, dtype=torch.uint8, device=dev)
+    for r in range(world):
+        rg = sdist.shard_range(len(flat), world, r)
+        b0 = cb_llr[rg.start][0]
+        span = d_llrs[b0: cb_llr[rg.stop - 1][0] + cb_llr[rg.stop - 1][1]].clone()  # what scatter_llrs hands rank r
+        cfg, lo, ho, _ = srsgpu.make_pusch_cb_configs([flat[i] for i in rg])
+        for j, i in enumerate(rg):
+            assert cfg[j].llr_offset == cb_llr[i][0] - b0  # contiguous codeblocks: the packed offsets are the span's
+            cfg[j].out_offset = j * sdist.CB_MSG_STRIDE
+        msgs = torch.zeros(len(rg) * sdist.CB_MSG_STRIDE, dtype=torch.uint8, device=dev)
+        crc = torch.zeros(len(rg), dtype=torch.uint8, device=dev)
+        cbp = srsgpu.PuschCbPlan(ctx, srsgpu.IMPL_BY_NAME["avx2"], cfg)
+        cbp.execute(span, torch.zeros(ho, dtype=torch.int8, device=dev), msgs,
+                    torch.zeros(len(rg), dtype=torch.int32, device=dev), crc)
+        torch.cuda.synchronize(dev)
+        cbp.close()
+        all_msgs[rg.start * sdist.CB_MSG_STRIDE: rg.stop * sdist.CB_MSG_STRIDE].copy_(msgs)  # what gather does
+        all_crc[rg.start: rg.stop].copy_(crc)
+    got_tbs = torch.zeros(ntb, dtype=torch.uint8, device=dev)
+    got_ok = torch.zeros(len(segs), dtype=torch.uint8, device=dev)
+    plan.assemble(all_crc, all_msgs, got_tbs, got_ok)
+    torch.cuda.synchronize(dev)
+    plan.close()
+    assert got_ok.tolist() == ref["ok"].tolist() == [1, 1, 0], (got_ok.tolist(), ref["ok"].tolist())
+    assert torch.equal(all_crc, ref["crc"])
+    assert torch.equal(got_tbs, ref["tbs"])
+    ok_cbs = ref["crc"].cpu().numpy().astype(bool)
+    m_got = all_msgs.view(ncb, -1).cpu().numpy()[ok_cbs]
+    m_ref = ref["msgs"].view(ncb, -1).cpu().numpy()[ok_cbs]
+    assert np.array_equal(m_got, m_ref)
+    off = 0
+    for seg, tb, good in zip(segs, tbs, [1, 1, 0]):
+        if good:
+            assert np.array_equal(got_tbs[off: off + tb.size].cpu().numpy(), tb)
+        off += tb.size

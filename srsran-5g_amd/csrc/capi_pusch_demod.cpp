@@ -21,6 +21,7 @@ struct srsgpu_pusch_demodulator_plan {
   uint16_t*             d_crbs     = nullptr;  ///< Allocated CRB lists of the CRB-mask transmissions.
   float*                d_acc      = nullptr;  ///< Statistics accumulators (zero between executes).
   int                   nof_chunks = 0;
+  int                   chunk_threads = 256;  ///< Lanes per chunk workgroup (launch_pusch_demodulate).
   int                   nof_tp_jobs = 0;
   int                   nof_tx     = 0;
   std::vector<uint32_t> nof_llrs;
@@ -295,6 +296,17 @@ int srsgpu_pusch_demodulator_plan_create_ex(srsgpu_context*                  ctx
          hipMemcpy(plan->d_desc, descs.data(), descs.size() * sizeof(demod_desc), hipMemcpyHostToDevice) ==
              hipSuccess;
   }
+  if (!chunks.empty()) {
+    // Lanes per chunk from its REs: a few-PRB transmission's chunk is a few hundred REs, which 256 lanes finish in two
+    // or three trips after paying the workgroup's descriptor -> sequence staging -> first-load latency chain; 128 lanes
+    // take ~5 REs each (headline bench 139.0k -> 141.2k slots/s, demodulator stage 47 -> 40 us per step,
+    // profiles/r4_demod_threads_ab.txt), 64 for chunks of at most 384 REs.
+    uint32_t most = 0;
+    for (const mod_chunk& ch : chunks) {
+      most = std::max(most, ch.re_end - ch.re_begin);
+    }
+    plan->chunk_threads = most <= 384 ? 64 : (most <= 768 ? 128 : 256);
+  }
   if (ok && !chunks.empty()) {
     ok = hipMalloc(&plan->d_chunks, chunks.size() * sizeof(mod_chunk)) == hipSuccess &&
          hipMemcpy(plan->d_chunks, chunks.data(), chunks.size() * sizeof(mod_chunk), hipMemcpyHostToDevice) ==
@@ -355,8 +367,8 @@ int srsgpu_pusch_demodulator_plan_execute_ex(const srsgpu_pusch_demodulator_plan
   }
   const hipStream_t s   = static_cast<hipStream_t>(stream);
   float*            acc = d_stats != nullptr ? plan->d_acc : nullptr;
-  launch_pusch_demodulate(plan->d_desc, plan->d_chunks, plan->nof_chunks, plan->d_tables, d_grids, d_ch_estimates,
-                          d_noise_var, d_llrs, plan->d_seq, plan->d_crbs, acc, s);
+  launch_pusch_demodulate(plan->d_desc, plan->d_chunks, plan->nof_chunks, plan->chunk_threads, plan->d_tables,
+                          d_grids, d_ch_estimates, d_noise_var, d_llrs, plan->d_seq, plan->d_crbs, acc, s);
   launch_pusch_demodulate_tp(plan->d_desc, plan->d_tp_jobs, plan->nof_tp_jobs, plan->d_tables, d_grids,
                              d_ch_estimates, d_noise_var, d_llrs, plan->d_seq, plan->d_crbs, acc, s);
   if (d_stats != nullptr) {

@@ -12,6 +12,8 @@
 // channel estimates (consecutive lanes read consecutive subcarriers: coalesced 4-byte loads), equalizes, demaps the
 // L * Qm LLRs, flips the signs the sequence selects and stages the bytes in LDS; the workgroup finally writes its
 // contiguous LLR range with dword stores. HBM-bound: (P + L P) x 4 B in and L Qm B out per RE.
+#include <cstdlib>
+
 #include "common.h"
 #include "gold_device.h"
 #include "srsgpu_internal.h"
@@ -324,12 +326,13 @@ __device__ __forceinline__ uint32_t to_bf16c(cpx v)
 
 /// Stages the chunk's descrambling words (and the first word of the next chunk) and, for 64/256QAM, the demapper
 /// tables in LDS. The caller synchronises.
+template <int T>
 __device__ __forceinline__ void stage_chunk(const demod_uniform& u, uint32_t* seq, demap_pair_table* tab)
 {
   const demod_desc& d      = *u.d;
   const uint32_t    tid    = threadIdx.x;
   const uint32_t    nwords = (d.nof_llrs + 31u) >> 5;
-  for (uint32_t j = tid; j < DEMOD_CHUNK_WORDS; j += DEMOD_THREADS) {
+  for (uint32_t j = tid; j < DEMOD_CHUNK_WORDS; j += T) {
     const uint32_t w = u.word0 + j;
     seq[j]           = (w < nwords) ? u.gseq[d.seq_word_offset + w] : 0u;
   }
@@ -340,7 +343,7 @@ __device__ __forceinline__ void stage_chunk(const demod_uniform& u, uint32_t* se
   if (d.qm >= 6) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(u.tables);
     uint32_t*       dst = reinterpret_cast<uint32_t*>(tab);
-    for (uint32_t i = tid; i < DEMAP_TABLES * sizeof(demap_pair_table) / 4; i += DEMOD_THREADS) {
+    for (uint32_t i = tid; i < DEMAP_TABLES * sizeof(demap_pair_table) / 4; i += T) {
       dst[i] = src[i];
     }
   }
@@ -432,7 +435,7 @@ __device__ __forceinline__ void setup_uniform(const demod_desc& d, const uint32_
 /// Every RE of the chunk owned by this lane: loads, equalization (L layers), demapping (QM bits per layer),
 /// descrambling and the packed LLR bytes into the LDS output buffer. L and QM are compile-time so that every register
 /// array has static indices and the RE's L * QM bytes are assembled in registers.
-template <int L, int QM, bool STATS>
+template <int L, int QM, bool STATS, int T>
 __device__ __forceinline__ void demod_res(demod_uniform        u,
                                           demap_pair_table*    tab,
                                           const uint32_t* __restrict__ grids,
@@ -452,18 +455,18 @@ __device__ __forceinline__ void demod_res(demod_uniform        u,
   if (r < u.re_end) {
     load_re<L>(d, r, grids, ce, u.crbs, yw, hw, sym);
   }
-  stage_chunk(u, seq, tab);
+  stage_chunk<T>(u, seq, tab);
   // The noise variances and CFO rotations are needed from the first equalisation on: their loads follow the RE's and
   // the sequence's, so the three fly together after the descriptor (chunk -> descriptor -> data, two dependent steps).
   setup_uniform(d, ce, noise_var, rot, u);
   __syncthreads();
   lane_stats st;
-  for (bool first = true; r < u.re_end; r += DEMOD_THREADS, first = false) {
+  for (bool first = true; r < u.re_end; r += T, first = false) {
 #if SRSGPU_DEMOD_PREFETCH
     // The next RE's loads fly while this one is equalised and demapped.
     (void)first;
     uint32_t       nyw[4] = {}, nhw[L][4] = {}, nsym = 0;
-    const uint32_t rn     = r + DEMOD_THREADS;
+    const uint32_t rn     = r + T;
     if (rn < u.re_end) {
       load_re<L>(d, rn, grids, ce, u.crbs, nyw, nhw, nsym);
     }
@@ -590,17 +593,17 @@ __device__ __forceinline__ void demod_res(demod_uniform        u,
   }
 }
 
-template <int QM, bool STATS>
+template <int QM, bool STATS, int T>
 __device__ __forceinline__ void demod_res_qm(const demod_uniform& u, demap_pair_table* tab,
                                              const uint32_t* __restrict__ grids, const uint32_t* __restrict__ ce,
                                              const float* __restrict__ noise_var, cpx* rot, uint32_t* seq,
                                              uint32_t* out32)
 {
   switch (u.d->L) {
-    case 1: demod_res<1, QM, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
-    case 2: demod_res<2, QM, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
-    case 3: demod_res<3, QM, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
-    default: demod_res<4, QM, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    case 1: demod_res<1, QM, STATS, T>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    case 2: demod_res<2, QM, STATS, T>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    case 3: demod_res<3, QM, STATS, T>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    default: demod_res<4, QM, STATS, T>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
   }
 }
 
@@ -611,8 +614,8 @@ __device__ __forceinline__ void demod_res_qm(const demod_uniform& u, demap_pair_
 #endif
 /// STATS: also accumulate the post-equalization statistics (a separate instantiation, so that the plain kernel keeps
 /// its register budget).
-template <bool STATS>
-__global__ __launch_bounds__(DEMOD_THREADS) DEMOD_OCCUPANCY void pusch_demodulate_kernel(const demod_desc* __restrict__ descs,
+template <bool STATS, int T>
+__global__ __launch_bounds__(T) DEMOD_OCCUPANCY void pusch_demodulate_kernel(const demod_desc* __restrict__ descs,
                                                                          const mod_chunk* __restrict__ chunks,
                                                                          const demap_pair_table* __restrict__ tables,
                                                                          const uint32_t* __restrict__ grids,
@@ -642,17 +645,17 @@ __global__ __launch_bounds__(DEMOD_THREADS) DEMOD_OCCUPANCY void pusch_demodulat
   u.lacc     = nullptr;
   if (STATS) {
     // Zeroed before the caller's first barrier (after stage_chunk).
-    for (uint32_t i = tid; i < static_cast<uint32_t>(DEMOD_ACC_PER_TX); i += DEMOD_THREADS) {
+    for (uint32_t i = tid; i < static_cast<uint32_t>(DEMOD_ACC_PER_TX); i += T) {
       lacc[i] = 0.f;
     }
     u.lacc = lacc;
   }
 
   switch (d.qm) {
-    case 2: demod_res_qm<2, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
-    case 4: demod_res_qm<4, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
-    case 6: demod_res_qm<6, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
-    default: demod_res_qm<8, STATS>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    case 2: demod_res_qm<2, STATS, T>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    case 4: demod_res_qm<4, STATS, T>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    case 6: demod_res_qm<6, STATS, T>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
+    default: demod_res_qm<8, STATS, T>(u, tab, grids, ce, noise_var, rot, seq, out32); break;
   }
   __syncthreads();
   if (STATS && tid < static_cast<uint32_t>(DEMOD_ACC_PER_TX) && lacc[tid] != 0.f) {
@@ -668,7 +671,7 @@ __global__ __launch_bounds__(DEMOD_THREADS) DEMOD_OCCUPANCY void pusch_demodulat
   uint32_t*      g32 = reinterpret_cast<uint32_t*>(dst - s);
   const uint32_t j0  = (s == 0) ? 0u : 1u;       // first full word
   const uint32_t j1  = (n + s) / 4;               // end of the full words
-  for (uint32_t j = j0 + tid; j < j1; j += DEMOD_THREADS) {
+  for (uint32_t j = j0 + tid; j < j1; j += T) {
     g32[j] = (s == 0) ? out32[j] : __builtin_amdgcn_alignbyte(out32[j], out32[j - 1], 4u - s);
   }
   const uint8_t* out8 = reinterpret_cast<const uint8_t*>(out32);
@@ -971,6 +974,7 @@ __global__ __launch_bounds__(64) void pusch_demod_stats_kernel(float* __restrict
 void launch_pusch_demodulate(const demod_desc*       d_desc,
                              const mod_chunk*        d_chunks,
                              int                     nof_chunks,
+                             int                     plan_threads,
                              const demap_pair_table* d_tables,
                              const uint32_t*         d_grids,
                              const uint32_t*         d_ch_est,
@@ -984,14 +988,23 @@ void launch_pusch_demodulate(const demod_desc*       d_desc,
   if (nof_chunks <= 0) {
     return;
   }
+  static const int forced = [] {
+    const char* e = std::getenv("SRSGPU_DEMOD_THREADS");  // A/B: 64, 128 or 256 lanes per chunk for every plan
+    return e != nullptr ? std::atoi(e) : 0;
+  }();
+  const int threads = forced > 0 ? forced : plan_threads;
+  const auto launch = [&](auto kernel, int t) {
+    hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nof_chunks)), dim3(static_cast<unsigned>(t)), 0, stream,
+                       d_desc, d_chunks, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq, d_crbs, d_acc);
+  };
   if (d_acc != nullptr) {
-    hipLaunchKernelGGL(pusch_demodulate_kernel<true>, dim3(static_cast<unsigned>(nof_chunks)), dim3(DEMOD_THREADS), 0,
-                       stream, d_desc, d_chunks, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq, d_crbs,
-                       d_acc);
+    launch(pusch_demodulate_kernel<true, DEMOD_THREADS>, DEMOD_THREADS);
+  } else if (threads == 64) {
+    launch(pusch_demodulate_kernel<false, 64>, 64);
+  } else if (threads == 128) {
+    launch(pusch_demodulate_kernel<false, 128>, 128);
   } else {
-    hipLaunchKernelGGL(pusch_demodulate_kernel<false>, dim3(static_cast<unsigned>(nof_chunks)), dim3(DEMOD_THREADS), 0,
-                       stream, d_desc, d_chunks, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq, d_crbs,
-                       d_acc);
+    launch(pusch_demodulate_kernel<false, DEMOD_THREADS>, DEMOD_THREADS);
   }
 }
 

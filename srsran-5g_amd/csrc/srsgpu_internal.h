@@ -595,6 +595,7 @@ void launch_pusch_demod_stats(float* d_acc, float* d_stats, int nof_tx, hipStrea
 void launch_pusch_demodulate(const demod_desc*        d_desc,
                              const mod_chunk*         d_chunks,
                              int                      nof_chunks,
+                             int                      threads,
                              const demap_pair_table*  d_tables,
                              const uint32_t*          d_grids,
                              const uint32_t*          d_ch_est,

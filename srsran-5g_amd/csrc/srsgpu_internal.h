@@ -302,7 +302,10 @@ struct mod_chunk {
 };
 
 /// Codeword words per modulator chunk and the largest codeword the Gold-sequence tables cover.
-constexpr uint32_t MOD_CHUNK_WORDS = 256;
+#ifndef SRSGPU_MOD_CHUNK_WORDS
+#define SRSGPU_MOD_CHUNK_WORDS 256
+#endif
+constexpr uint32_t MOD_CHUNK_WORDS = SRSGPU_MOD_CHUNK_WORDS;
 /// PUSCH demodulator chunk (codeword words per workgroup) and whether a lane prefetches its next RE's received values
 /// and estimates while it equalises the current one (pusch_demodulator.hip).
 #ifndef SRSGPU_DEMOD_CHUNK_WORDS

@@ -301,9 +301,11 @@ struct mod_chunk {
   uint32_t re_end;    ///< One past the last.
 };
 
-/// Codeword words per modulator chunk and the largest codeword the Gold-sequence tables cover.
+/// Codeword words per modulator chunk (one workgroup): 1024 keeps a few-PRB 4-layer transmission (~23k bits) in one
+/// workgroup of ~3 REs per lane instead of three workgroups of one RE per lane (DM-RS + modulator stage 59.5 -> 52.6 us
+/// per step, headline +0.5 %; 512 splits such a transmission unevenly and was slower; profiles/r4_mod_chunk_ab.txt).
 #ifndef SRSGPU_MOD_CHUNK_WORDS
-#define SRSGPU_MOD_CHUNK_WORDS 256
+#define SRSGPU_MOD_CHUNK_WORDS 1024
 #endif
 constexpr uint32_t MOD_CHUNK_WORDS = SRSGPU_MOD_CHUNK_WORDS;
 /// PUSCH demodulator chunk (codeword words per workgroup) and whether a lane prefetches its next RE's received values

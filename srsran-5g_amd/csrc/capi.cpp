@@ -95,6 +95,9 @@ struct srsgpu_pusch_decoder_plan {
   tb_dec_desc*          d_tb    = nullptr;
   int                   nof_tbs = 0;
   int                   tb_threads = 256;  ///< pusch_tb_kernel workgroup size (1024 for large TBs).
+  tb_slice*             d_slices   = nullptr;  ///< Sliced TB stage (large segmented TBs): pusch_tb_slice_kernel.
+  uint32_t*             d_tb_acc   = nullptr;  ///< Per-TB CRC sums and slice counters (zero between executes).
+  int                   nof_slices = 0;
 };
 
 struct srsgpu_ldpc_decoder_plan {
@@ -1422,6 +1425,29 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
     return t.nof_cbs == 1 && t.tbs_bits / 8u <= 2048u;
   });
   plan->tb_threads = any_large ? 1024 : (all_small_single ? 64 : 256);
+  // Few large segmented TBs (at most 8, every one byte-aligned with a CRC table, one above the inline size): the TB
+  // stage runs over TB_SLICE_BYTES slices, several workgroups per TB, instead of one 1024-lane workgroup per TB, whose
+  // byte copy and CRC chain take ~15 us for a 37 KB TB. That latency is what a slot processor's one-PDU slot waits for
+  // (UL one-PDU slot batch +3 %); with many TBs per launch the single workgroups already fill the GPU and the slices'
+  // per-workgroup overhead costs throughput (test-mode bench, 32 TBs: 308.7k vs 304.4k slots/s sliced), so those keep
+  // one workgroup per TB (profiles/r4_tb_sliced_ab.txt).
+  const bool sliceable = !tbs.empty() && std::all_of(tbs.begin(), tbs.end(), [](const tb_dec_desc& t) {
+    return t.nof_cbs > 1 && t.crc_table != NO_CRC_TABLE && (t.cb_data_bits & 7u) == 0;
+  });
+  std::vector<tb_slice> slices;
+  static const bool slicing = [] {
+    const char* e = std::getenv("SRSGPU_TB_SLICED");  // A/B: 0 = one workgroup per TB
+    return e == nullptr || e[0] != '0';
+  }();
+  if (slicing && sliceable && any_large && tbs.size() <= 8) {
+    for (uint32_t t = 0; t < tbs.size(); ++t) {
+      const uint32_t bytes = tbs[t].tbs_bits / 8u;
+      const uint32_t n     = (bytes + TB_SLICE_BYTES - 1) / TB_SLICE_BYTES;
+      for (uint32_t k = 0; k < n; ++k) {
+        slices.push_back({t, k * TB_SLICE_BYTES, std::min(bytes, (k + 1) * TB_SLICE_BYTES), n});
+      }
+    }
+  }
   int r         = upload_pusch_cb_plan(ctx, impl, batch, dms, &plan->cbs);
   if (r != SRSGPU_OK) {
     delete plan;
@@ -1433,10 +1459,36 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
     srsgpu_pusch_decoder_plan_destroy(plan);
     return fail(SRSGPU_ERR_HIP, "failed to upload transport block descriptors");
   }
+  if (!slices.empty()) {
+    if (hipMalloc(&plan->d_slices, slices.size() * sizeof(tb_slice)) != hipSuccess ||
+        hipMemcpy(plan->d_slices, slices.data(), slices.size() * sizeof(tb_slice), hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        hipMalloc(&plan->d_tb_acc, 2 * tbs.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(plan->d_tb_acc, 0, 2 * tbs.size() * sizeof(uint32_t)) != hipSuccess) {
+      srsgpu_pusch_decoder_plan_destroy(plan);
+      return fail(SRSGPU_ERR_HIP, "failed to upload transport block slices");
+    }
+    plan->nof_slices = static_cast<int>(slices.size());
+  }
   guard.commit(plan->crc_refs);
   *plan_out = plan;
   return SRSGPU_OK;
 }
+
+namespace {
+/// The TB stage of a decoder plan: sliced over several workgroups per TB, or one workgroup per TB.
+void launch_plan_tb_stage(const srsgpu_pusch_decoder_plan* plan, uint8_t* d_cb_crc_ok, const uint8_t* d_cb_msgs,
+                          uint8_t* d_tbs, uint8_t* d_tb_crc_ok, hipStream_t s)
+{
+  if (plan->nof_slices > 0) {
+    launch_pusch_tb_sliced(plan->d_tb, plan->d_slices, plan->nof_slices, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok,
+                           plan->ctx->d_crc_arena, plan->d_tb_acc, plan->d_tb_acc + plan->nof_tbs, s);
+  } else {
+    launch_pusch_tb(plan->d_tb, plan->nof_tbs, plan->tb_threads, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok,
+                    plan->ctx->d_crc_arena, s);
+  }
+}
+} // namespace
 
 uint32_t srsgpu_pusch_decoder_plan_nof_codeblocks(const srsgpu_pusch_decoder_plan* plan)
 {
@@ -1476,7 +1528,7 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
   }
   stage_timer::mark(evd, 1, s);
   stage_timer::mark(ev, 2, s);
-  launch_pusch_tb(plan->d_tb, plan->nof_tbs, plan->tb_threads, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, plan->ctx->d_crc_arena, s);
+  launch_plan_tb_stage(plan, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, s);
   HIP_TRY(hipGetLastError());
   stage_timer::mark(ev, 3, s);
   return SRSGPU_OK;
@@ -1493,8 +1545,7 @@ int srsgpu_pusch_decoder_plan_assemble(const srsgpu_pusch_decoder_plan* plan,
       d_tb_crc_ok == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  launch_pusch_tb(plan->d_tb, plan->nof_tbs, plan->tb_threads, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok,
-                  plan->ctx->d_crc_arena, static_cast<hipStream_t>(stream));
+  launch_plan_tb_stage(plan, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, static_cast<hipStream_t>(stream));
   HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
 }
@@ -1540,6 +1591,12 @@ void srsgpu_pusch_decoder_plan_destroy(srsgpu_pusch_decoder_plan* plan)
   srsgpu_pusch_cb_plan_destroy(plan->cbs);
   if (plan->d_tb != nullptr) {
     (void)hipFree(plan->d_tb);
+  }
+  if (plan->d_slices != nullptr) {
+    (void)hipFree(plan->d_slices);
+  }
+  if (plan->d_tb_acc != nullptr) {
+    (void)hipFree(plan->d_tb_acc);
   }
   delete plan;
 }

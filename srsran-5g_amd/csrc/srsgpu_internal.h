@@ -180,6 +180,28 @@ struct tb_dec_desc {
   uint32_t crc_table;    ///< CRC24A per-bit contribution table of tbs_bits (CRC arena offset) or NO_CRC_TABLE.
 };
 
+/// A byte range [begin, end) of a large segmented TB (pusch_tb_slice_kernel): begin a multiple of 16 (CRC chunks).
+struct tb_slice {
+  uint32_t tb;          ///< Index into the plan's tb_dec_desc array.
+  uint32_t begin;
+  uint32_t end;
+  uint32_t nof_slices;  ///< Slices of the TB (its last finisher finalises).
+};
+/// TB bytes per slice workgroup (256 lanes x one 16-byte CRC chunk each).
+constexpr uint32_t TB_SLICE_BYTES = 4096;
+
+void launch_pusch_tb_sliced(const tb_dec_desc* d_desc,
+                            const tb_slice*    d_slices,
+                            int                nof_slices,
+                            uint8_t*           d_cb_crc_ok,
+                            const uint8_t*     d_cb_msgs,
+                            uint8_t*           d_tbs,
+                            uint8_t*           d_tb_crc_ok,
+                            const uint32_t*    d_crc_tables,
+                            uint32_t*          d_acc,
+                            uint32_t*          d_cnt,
+                            hipStream_t        stream);
+
 /// threads: 256; 1024 for plans with TBs above TB_CRC_INLINE_MAX_BYTES (the TB CRC chain per lane shrinks 4x); 64
 /// when every TB is one small codeblock.
 void launch_pusch_tb(const tb_dec_desc* d_desc,

@@ -329,3 +329,59 @@ def test_codeblock_sharded_decode_assemble(orc, ctx):
         if good:
             assert np.array_equal(got_tbs[off: off + tb.size].cpu().numpy(), tb)
         off += tb.size
+
+
+def test_pusch_decoder_sliced_tb_stage(orc, ctx):
+    """Plans whose TBs are all segmented, byte-aligned and one above 16 KB run the TB stage over 4 KB slices (several
+    workgroups per TB, the last finisher checks the CRC): clean TBs decode to the sent bytes, a TB with a failed
+    codeblock is flagged, and - through srsgpu_pusch_decoder_plan_assemble on a corrupted message with its codeblock
+    flag still set - a TB CRC mismatch clears every codeblock flag of that TB only. Executed twice (the slice counters
+    and sums reset themselves)."""
+    import torch
+
+    import srsgpu
+    from srsgpu import sch
+    rng = np.random.default_rng(23)
+    grants = [(sch.UeGrant(273, 1, 8, 948), 0.0), (sch.UeGrant(100, 2, 8, 800), 0.0), (sch.UeGrant(60, 1, 8, 900), 60.0)]
+    cfgs, segs, tbs, llrs = [], [], [], []
+    for g, noise in grants:
+        seg = g.segmentation()
+        assert seg.nof_segments > 1
+        tb = rng.integers(0, 256, seg.tbs // 8).astype(np.uint8)
+        cw, _, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, 0, g.qm, g.nof_layers, 0, g.nof_ch_symbols)
+        llrs.append(bits_to_llrs(rng, cw, amp=10.0, noise=noise))
+        cfgs.append(srsgpu.PuschTransportBlock(seg.tbs // 8, seg.base_graph, 0, g.qm, g.nof_layers, g.nof_ch_symbols,
+                                               new_data=True, nof_ldpc_iterations=6))
+        segs.append(seg)
+        tbs.append(tb)
+    assert max(t.size for t in tbs) > 16384
+    arr, nllr, nharq, ncb, ntb = srsgpu.make_pusch_tb_configs(
+        cfgs, [s.nof_segments for s in segs], [BG_N_SHORT[s.base_graph] * s.lifting_size for s in segs])
+    dev = torch.device("cuda", 0)
+    d_llrs = torch.from_numpy(np.concatenate(llrs)).to(dev)
+    plan = srsgpu.PuschDecoderPlan(ctx, srsgpu.IMPL_BY_NAME["avx2"], arr)
+    for _ in range(2):
+        crc = torch.zeros(ncb, dtype=torch.uint8, device=dev)
+        msgs = torch.zeros(ncb * srsgpu.CB_MSG_STRIDE, dtype=torch.uint8, device=dev)
+        out = torch.zeros(ntb, dtype=torch.uint8, device=dev)
+        ok = torch.zeros(len(segs), dtype=torch.uint8, device=dev)
+        plan.execute(d_llrs, torch.zeros(nharq, dtype=torch.int8, device=dev), crc, msgs,
+                     torch.zeros(ncb, dtype=torch.int32, device=dev), out, ok)
+        torch.cuda.synchronize(dev)
+        assert ok.tolist() == [1, 1, 0], ok.tolist()
+        off = 0
+        for tb, good in zip(tbs, [1, 1, 0]):
+            if good:
+                assert np.array_equal(out[off: off + tb.size].cpu().numpy(), tb)
+            off += tb.size
+    # TB CRC mismatch: flip one data byte of TB 1's second codeblock message (its CB flag stays set).
+    c1 = segs[0].nof_segments + 1
+    msgs[c1 * srsgpu.CB_MSG_STRIDE + 5] ^= 0x10
+    ok2 = torch.zeros(len(segs), dtype=torch.uint8, device=dev)
+    plan.assemble(crc, msgs, out, ok2)
+    torch.cuda.synchronize(dev)
+    plan.close()
+    assert ok2.tolist() == [1, 0, 0], ok2.tolist()
+    flags = crc.cpu().numpy()
+    n0, n1 = segs[0].nof_segments, segs[1].nof_segments
+    assert flags[:n0].all() and not flags[n0:n0 + n1].any()

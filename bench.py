@@ -263,7 +263,7 @@ def parse_args(argv=None):
     # 32 / 2 117.9k, 32 / 4 103.8k, 32 / 5 117.9k, 64 / 3 120.5k slots/s (set counts that are multiples of the 4
     # hardware queues serialise the sets' graph branches).
     ap.add_argument("--slots-per-step", type=int, default=32)
-    ap.add_argument("--input-sets", type=int, default=9, help="independent working sets rotated step by step")
+    ap.add_argument("--input-sets", type=int, default=13, help="independent working sets rotated step by step")
     ap.add_argument("--iterations", type=int, default=6)
     ap.add_argument("--snr-db", type=float, default=26.0)
     ap.add_argument("--worst-case", action="store_true", help="headline on Gaussian-noise input (all iterations)")

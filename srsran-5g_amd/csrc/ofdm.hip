@@ -26,6 +26,12 @@
 namespace srsgpu {
 namespace {
 
+#ifdef SRSGPU_OFDM_WAVES  // occupancy experiments: waves per SIMD forced by the register allocator
+#define OFDM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(SRSGPU_OFDM_WAVES, 8)))
+#else
+#define OFDM_OCCUPANCY
+#endif
+
 // cos / sin (2 pi k / 16).
 __device__ constexpr float kCos16[16] = {1.0f,          0.92387953251f,  0.70710678118f,  0.38268343236f,
                                          0.0f,          -0.38268343236f, -0.70710678118f, -0.92387953251f,
@@ -342,7 +348,7 @@ __device__ __forceinline__ uint32_t bf16_bits(float v)
 }
 
 template <int N>
-__global__ __launch_bounds__(ofdm_threads<N>()) void ofdm_modulate_kernel(
+__global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_modulate_kernel(
     const ofdm_job* __restrict__ jobs,
     uint32_t nsc,
     const float2* __restrict__ tw,
@@ -381,7 +387,7 @@ __global__ __launch_bounds__(ofdm_threads<N>()) void ofdm_modulate_kernel(
 }
 
 template <int N>
-__global__ __launch_bounds__(ofdm_threads<N>()) void ofdm_demodulate_kernel(
+__global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_demodulate_kernel(
     const ofdm_job* __restrict__ jobs,
     uint32_t nsc,
     uint32_t window_offset,

@@ -743,7 +743,9 @@ uint32_t srsgpu_pusch_decoder_plan_nof_codeblocks(const srsgpu_pusch_decoder_pla
 uint64_t srsgpu_pusch_decoder_plan_decoder_input_llrs(const srsgpu_pusch_decoder_plan* plan);
 
 /** Decodes the planned transport blocks. d_tb_crc_ok[t] = 1 when the TB CRC passed (pusch_decoder_result
- *  tb_crc_ok); d_cb_nof_iterations[c] as in srsgpu_pusch_cb_plan_execute. Asynchronous, hipGraph-capturable. */
+ *  tb_crc_ok); d_cb_nof_iterations[c] as in srsgpu_pusch_cb_plan_execute. Asynchronous, hipGraph-capturable.
+ *  A plan of at most 8 large segmented TBs runs its TB stage over slices whose CRC sums live in the plan (reset by
+ *  every execute): executes (and assembles) of one plan must be ordered, e.g. on one stream, never concurrent. */
 int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
                                       const int8_t*                    d_llrs,
                                       int8_t*                          d_harq,

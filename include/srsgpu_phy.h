@@ -685,6 +685,13 @@ int srsgpu_ulsch_demux_plan_create(srsgpu_context*                  ctx,
 /** LLRs of transmission tx: stream 0 = codeword (input), 1 = UL-SCH, 2 = HARQ-ACK, 3 = CSI Part 1, 4 = CSI Part 2. */
 uint32_t srsgpu_ulsch_demux_plan_nof_llrs(const srsgpu_ulsch_demux_plan* plan, uint32_t tx, uint32_t stream);
 
+/** LLRs of `stream` (as above) that transmission tx's OFDM symbol l (0..13, slot numbering) carries: counts[l]. The
+ *  reference's demultiplexer hands a UCI field's LLRs to its decoder buffer while it demultiplexes the symbol that holds
+ *  them and ends the field in the symbol that completes it (ulsch_demultiplex_impl.cpp:474-576); a host that replays
+ *  the GPU's streams into the reference's UCI decoders feeds them symbol by symbol with these counts. */
+int srsgpu_ulsch_demux_plan_symbol_llrs(const srsgpu_ulsch_demux_plan* plan, uint32_t tx, uint32_t stream,
+                                        uint32_t counts[14]);
+
 /** Demultiplexes every planned transmission. Asynchronous on `stream`, hipGraph-capturable. Output pointers of streams
  *  no transmission uses may be NULL. */
 int srsgpu_ulsch_demux_plan_execute(const srsgpu_ulsch_demux_plan* plan,
@@ -781,7 +788,7 @@ typedef struct {
   uint32_t slot;         /* arena slot (absolute codeblock identifier) */
   uint32_t batch_offset; /* first byte of the codeblock's soft bits in the batch HARQ buffer */
   uint32_t bytes;        /* soft bits to move (N of the codeblock) */
-  uint32_t reserved;
+  uint32_t arena;        /* srsgpu_harq_copy_arenas: index into the arena table (0 for srsgpu_harq_copy) */
 } srsgpu_harq_copy_job;
 
 int srsgpu_harq_copy(srsgpu_context*             ctx,
@@ -792,6 +799,18 @@ int srsgpu_harq_copy(srsgpu_context*             ctx,
                      const srsgpu_harq_copy_job* d_jobs,
                      uint32_t                    nof_jobs,
                      void*                       stream);
+
+/** As srsgpu_harq_copy over several arenas in one launch (the rx buffer pools of several sectors, whose slots one
+ *  GPU service batch gathers): job j moves between arena d_arenas[j.arena] (a device array of arena base pointers)
+ *  and the batch buffer. */
+int srsgpu_harq_copy_arenas(srsgpu_context*             ctx,
+                            int                         direction,
+                            int8_t* const*              d_arenas,
+                            uint32_t                    arena_stride,
+                            int8_t*                     d_batch,
+                            const srsgpu_harq_copy_job* d_jobs,
+                            uint32_t                    nof_jobs,
+                            void*                       stream);
 
 /** Stage timing: with enable = 1 every execute records HIP events on its stream around the three kernel stages
  *  (0: rate dematching, 1: LDPC decoding, 2: TB assembly + CRC); with enable = 2 only around the decoding stage (two

@@ -315,11 +315,13 @@ private:
     std::memset(h_flags, 0, n);
     std::vector<srsgpu_pusch_cb_config>    key;
     std::vector<std::pair<unsigned, bool>> ids;
+    std::vector<size_t>                    key_op;  // the op of each plan position (rejected ops are not planned)
     for (size_t i = 0; i != n; ++i) {
       h_iters[i] = -1;
       if (ops[i].failed) {
         continue;
       }
+      key_op.push_back(i);
       const hw_pusch_decoder_configuration& c = cfgs[ops[i].cb_index];
       srsgpu_pusch_cb_config                k;
       std::memset(&k, 0, sizeof(k));
@@ -367,6 +369,22 @@ private:
     hip_check(hipMemcpyAsync(h_iters, d_iters, n * sizeof(int32_t), hipMemcpyDeviceToHost, stream), "iterations");
     hip_check(hipMemcpyAsync(h_flags, d_flags, n, hipMemcpyDeviceToHost, stream), "flags");
     hip_check(hipStreamSynchronize(stream), "synchronise");
+    // The plan reports the CRC flag and iterations of its k-th codeblock at position k (srsgpu_pusch_cb_plan_create
+    // numbers the codeblocks by their position in the configuration array); read_operation_outputs reads them by op.
+    // With ops rejected at enqueue the two differ: scatter the results back to their ops (messages already land at
+    // out_offset = op * stride).
+    if (key_op.size() != n) {
+      const std::vector<uint8_t> flags(h_flags, h_flags + key_op.size());
+      const std::vector<int32_t> iters(h_iters, h_iters + key_op.size());
+      for (size_t i = 0; i != n; ++i) {
+        h_flags[i] = 0;
+        h_iters[i] = -1;
+      }
+      for (size_t k = 0; k != key_op.size(); ++k) {
+        h_flags[key_op[k]] = flags[k];
+        h_iters[key_op[k]] = iters[k];
+      }
+    }
   }
 
   std::shared_ptr<harq_arena>                 arena;

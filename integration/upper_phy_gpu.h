@@ -46,6 +46,8 @@
 namespace srsran {
 namespace gpu {
 
+class pusch_result_transport;
+
 /// PUSCH slot batching parameters (the reference's pusch_processor_impl::configuration and the rx buffer pool size).
 struct pusch_batch_configuration {
   int                                  device = 0;
@@ -55,7 +57,56 @@ struct pusch_batch_configuration {
   unsigned                             nof_ldpc_iterations = 6;
   bool                                 ldpc_early_stop     = true;
   channel_state_information::sinr_type csi_sinr_calc_method = channel_state_information::sinr_type::post_equalization;
+  /// false: the PUSCH task returns once the slot's results are notified (as the reference's processors do on their
+  /// executor); true: it returns once the slot is handed to the GPU service, and the results are notified from the
+  /// service's completion thread (the uplink processor keeps the grid and the slot until then, so a DU runs several
+  /// uplink processors per sector, as du_low's processor pool does).
+  bool asynchronous = false;
+  /// Multi-GPU (row b7): the devices a slot's UEs are sharded over, the first one the root whose thread replays the
+  /// results; empty: one device (`device`). A UE's shard is its RNTI modulo the number of devices, so its HARQ soft bits
+  /// stay in the arena of the device that decodes its retransmissions. Each shard runs the estimator, demodulator,
+  /// demultiplexer and decoder of its UEs on its own copy of the rx grid; `transport` gathers the results (TB bytes, CB
+  /// / TB CRC flags, iterations, channel metrics, statistics, UCI streams, kept CB messages) to the root.
+  std::vector<int>                        devices;
+  std::shared_ptr<pusch_result_transport> transport;  ///< nullptr: create_pusch_copy_transport()
 };
+
+/// The per-GPU PUSCH service: one dispatcher that gathers the slots every cell's batches submit into one launch
+/// sequence (cross-cell aggregation), several launch sets in flight on their own streams, and one completion thread
+/// that replays the results into the reference's processors. Shared by every PUSCH batch of every sector on a GPU.
+struct pusch_service_configuration {
+  int      device                    = 0;
+  unsigned nof_launch_sets           = 3;   ///< launches in flight (each with its own stream, staging and plans)
+  unsigned max_slots_per_launch      = 16;  ///< slots (of any cells) gathered into one launch
+  unsigned expected_slots_per_launch = 1;   ///< slots of one slot number to wait for before launching (the cells)
+  unsigned gather_window_us          = 0;   ///< longest wait for them, from the first one's arrival
+  unsigned max_grids                 = 64;  ///< batches (uplink processors) per grid shape on the device
+};
+class pusch_gpu_service;
+std::shared_ptr<pusch_gpu_service> create_pusch_gpu_service(const pusch_service_configuration& config);
+
+/// Moves a slot's PUSCH results from the GPUs that decoded its UEs to the device whose thread replays them into the
+/// reference's processors and notifier (the FAPI side, row b7): every part lands at dst + dst_offset on the root device,
+/// ordered on root_stream after the work already queued on the part's stream.
+class pusch_result_transport
+{
+public:
+  struct part {
+    unsigned    rank;    ///< Index of the part's device in the transport's device list.
+    int         device;
+    const void* src;
+    size_t      bytes;
+    void*       stream;  ///< hipStream_t of the part's producer.
+    size_t      dst_offset;
+  };
+  virtual ~pusch_result_transport() = default;
+  virtual void gather(int root_device, void* root_stream, void* dst, const std::vector<part>& parts) = 0;
+};
+/// Device-to-device copies (hipMemcpyPeerAsync; any device list, devices may repeat).
+std::shared_ptr<pusch_result_transport> create_pusch_copy_transport();
+/// RCCL point-to-point over xGMI: one communicator per listed device in this process (ncclCommInitAll, devices distinct),
+/// every part an ncclSend from its rank to rank 0 inside one group.
+std::shared_ptr<pusch_result_transport> create_pusch_rccl_transport(const std::vector<int>& devices);
 
 /// The HBM HARQ arena shared by every PUSCH batch of a sector (the rx buffer pool is shared too).
 class pusch_harq_arena;
@@ -64,13 +115,16 @@ std::shared_ptr<pusch_harq_arena> create_pusch_harq_arena(int device, unsigned m
 /// A slot batch of PUSCH transmissions (one per uplink processor).
 class pusch_slot_batch;
 
-/// demux / uci: factories of the reference's UL-SCH demultiplexer and UCI decoder (host-side parts of the result
-/// assembly, one per thread that runs batches); fallback: the processor for PDUs the batch does not cover.
+/// uci: factory of the reference's UCI decoder (host-side part of the result assembly); fallback: the processor for
+/// PDUs the batch does not cover; service: the GPU service (nullptr: a private one on config.device). The demux factory
+/// of earlier revisions is no longer used (the GPU demultiplexes; the replay feeds the UCI decoders its streams) and
+/// is accepted for compatibility.
 std::shared_ptr<pusch_slot_batch> create_pusch_slot_batch(const pusch_batch_configuration&           config,
                                                           std::shared_ptr<pusch_harq_arena>          arena,
                                                           std::shared_ptr<ulsch_demultiplex_factory> demux,
                                                           std::shared_ptr<uci_decoder_factory>       uci,
-                                                          std::unique_ptr<pusch_processor>           fallback);
+                                                          std::unique_ptr<pusch_processor>           fallback,
+                                                          std::shared_ptr<pusch_gpu_service>         service = nullptr);
 
 /// The pusch_processor given to the reference's uplink_processor_impl: process() registers the PDU in the batch.
 std::unique_ptr<pusch_processor> create_pusch_processor_batch_gpu(std::shared_ptr<pusch_slot_batch> batch);

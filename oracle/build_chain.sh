@@ -47,6 +47,7 @@ SRCS=(
   "$REF/lib/phy/lower/processors/uplink/puxch/puxch_processor_impl.cpp"
   "$REF/lib/instrumentation/traces/du_traces.cpp"
   "$ROOT/integration/upper_phy_gpu.cpp"
+  "$ROOT/integration/pusch_batch_gpu.cpp"
   "$U/uplink_processor_impl.cpp"
   "$U/downlink_processor_single_executor_impl.cpp"
   "$U/rx_buffer_pool_impl.cpp"
@@ -73,6 +74,6 @@ rc=0
 for p in "${pids[@]:-}"; do [ -n "$p" ] && { wait "$p" || rc=1; }; done
 [ $rc -eq 0 ] || { echo "build_chain: compilation failed" >&2; exit 1; }
 $CXX -shared -o "$OUT/libsrschain.so" "${OBJS[@]}" -L"$OUT" -lsrshal -lsrsref -L"$ROOT/srsran-5g_amd/lib" \
-  -lsrsgpu_phy -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$ORIGIN' -Wl,-rpath,'$ORIGIN/../../srsran-5g_amd/lib' \
+  -lsrsgpu_phy -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,'$ORIGIN' -Wl,-rpath,'$ORIGIN/../../srsran-5g_amd/lib' \
   -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 echo "build_chain: $OUT/libsrschain.so"

@@ -1117,6 +1117,7 @@ public:
   void on_new_prach_results(const ul_prach_results&) override {}
   void on_new_pusch_results_control(const ul_pusch_results_control& r) override
   {
+    std::lock_guard<std::mutex> lock(mtx);
     ++nof_control;
     if (r.harq_ack.has_value()) {
       // HARQ-ACK on PUSCH: status and payload bits (LSB first) per RNTI.
@@ -1129,6 +1130,14 @@ public:
   }
   void on_new_pusch_results_data(const ul_pusch_results_data& r) override
   {
+    if (count_only) {
+      // Benchmarks: results arrive on the GPU service's completion thread; only the count matters.
+      crc_ok += r.decoder_result.tb_crc_ok ? 1 : 0;
+      ++nof_data;
+      return;
+    }
+    std::lock_guard<std::mutex> lock(mtx);
+    ++nof_data;
     ul_record x;
     x.rnti    = static_cast<int>(r.rnti);
     x.harq_id = static_cast<int>(r.harq_id);
@@ -1152,22 +1161,75 @@ public:
   void on_new_pucch_results(const ul_pucch_results&) override {}
   void on_new_srs_results(const ul_srs_results&) override {}
 
+  /// Waits (asynchronous batches) until n data results have arrived since the last reset.
+  void wait_for(unsigned n)
+  {
+    while (nof_data.load() < n) {
+      std::this_thread::yield();
+    }
+  }
+  void reset()
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    records.clear();
+    harq_ack.clear();
+    nof_data = 0;
+    crc_ok   = 0;
+  }
+
+  std::mutex                         mtx;
   std::vector<ul_record>             records;
   std::map<int, std::pair<int, int>> harq_ack;  ///< RNTI -> (uci_status, payload bits)
   unsigned                           nof_control = 0;
+  bool                               count_only  = false;
+  std::atomic<unsigned>              nof_data{0};
+  std::atomic<unsigned>              crc_ok{0};
 };
 
 /// The reference's uplink_processor_impl over CPU processors (variant 0) or the GPU slot batch (variant 1).
 struct ul_harness {
   unsigned                                   P, nsc, grid_prb;
-  std::unique_ptr<rx_buffer_pool_controller> pool;
-  ul_results_recorder                        notifier;
+  std::unique_ptr<rx_buffer_pool_controller> own_pool;
+  rx_buffer_pool_controller*                 pool = nullptr;
+  ul_results_recorder                        own_notifier;
+  ul_results_recorder*                       notifier = &own_notifier;
   std::unique_ptr<uplink_processor>          proc;
 };
 
+constexpr unsigned UL_POOL_CODEBLOCKS = 2048;
+
+std::unique_ptr<rx_buffer_pool_controller> ul_pool()
+{
+  rx_buffer_pool_config pc;
+  pc.max_codeblock_size   = ldpc::MAX_CODEBLOCK_SIZE;
+  pc.nof_buffers          = 256;
+  pc.nof_codeblocks       = UL_POOL_CODEBLOCKS;
+  pc.expire_timeout_slots = 100;
+  pc.external_soft_bits   = false;  // the fallback processor (CPU decoder) keeps its soft bits in the buffers
+  return create_rx_buffer_pool(pc);
+}
+
+/// What the uplink processors of one sector share: the rx buffer pool, the HBM HARQ arena and the results notifier
+/// (du_low builds several uplink processors per sector over one pool). The GPU service is shared by every sector.
+struct ul_sector {
+  std::unique_ptr<rx_buffer_pool_controller> pool;
+  std::shared_ptr<gpu::pusch_harq_arena>     arena;
+  ul_results_recorder                        notifier;
+};
+
 /// variant: 0 the reference's CPU PUSCH processor, 1 the GPU slot batch; + 2 with the "interpolate" time strategy of
-/// the estimator (the batch then keeps per-symbol estimates) instead of du_low's "average".
-ul_harness* ul_create(int device, int variant, unsigned P, unsigned grid_prb, unsigned max_iter)
+/// the estimator (the batch then keeps per-symbol estimates) instead of du_low's "average". sector / service /
+/// asynchronous: the uplink processor as one of several of a sector on a shared GPU service (else it owns its pool,
+/// arena, notifier and a private service, and runs each slot synchronously).
+ul_harness* ul_create(int                                     device,
+                      int                                     variant,
+                      unsigned                                P,
+                      unsigned                                grid_prb,
+                      unsigned                                max_iter,
+                      ul_sector*                              sector       = nullptr,
+                      std::shared_ptr<gpu::pusch_gpu_service> service      = nullptr,
+                      bool                                    asynchronous = false,
+                      int                                     multi        = 0)
 {
   const auto td = variant >= 2 ? port_channel_estimator_td_interpolation_strategy::interpolate
                                : port_channel_estimator_td_interpolation_strategy::average;
@@ -1176,13 +1238,13 @@ ul_harness* ul_create(int device, int variant, unsigned P, unsigned grid_prb, un
   h->P        = P;
   h->grid_prb = grid_prb;
   h->nsc      = 12 * grid_prb;
-  rx_buffer_pool_config pc;
-  pc.max_codeblock_size   = ldpc::MAX_CODEBLOCK_SIZE;
-  pc.nof_buffers          = 256;
-  pc.nof_codeblocks       = 2048;
-  pc.expire_timeout_slots = 100;
-  pc.external_soft_bits   = false;  // the fallback processor (CPU decoder) keeps its soft bits in the buffers
-  h->pool                 = create_rx_buffer_pool(pc);
+  if (sector != nullptr) {
+    h->pool     = sector->pool.get();
+    h->notifier = &sector->notifier;
+  } else {
+    h->own_pool = ul_pool();
+    h->pool     = h->own_pool.get();
+  }
 
   std::unique_ptr<pusch_processor> pusch;
   std::shared_ptr<gpu::pusch_slot_batch> batch;
@@ -1192,13 +1254,23 @@ ul_harness* ul_create(int device, int variant, unsigned P, unsigned grid_prb, un
     gpu::pusch_batch_configuration bc;
     bc.device              = device;
     bc.estimator = gpu::make_pusch_estimator_options(port_channel_estimator_fd_smoothing_strategy::filter, td, true);
-    bc.max_cb_ids          = pc.nof_codeblocks;
+    bc.max_cb_ids          = UL_POOL_CODEBLOCKS;
     bc.nof_ldpc_iterations = max_iter;
+    bc.asynchronous        = asynchronous;
+    if (multi == 1) {
+      // Row b7 on one GPU: three UE shards on device 0 (own launchers, HARQ arenas, grid copies), peer-copy gather.
+      bc.devices = {device, device, device};
+    } else if (multi == 2) {
+      // Row b7 through RCCL at world size 1: one shard, the gather an ncclSend / ncclRecv pair to itself.
+      bc.devices   = {device};
+      bc.transport = gpu::create_pusch_rccl_transport({device});
+    }
     // PDUs outside the batch: the reference processor over the GPU estimator / demodulator (row b3).
     auto fallback = new_pusch_processor(device, 1, td, max_iter, true, {});
-    batch = gpu::create_pusch_slot_batch(bc, gpu::create_pusch_harq_arena(device, bc.max_cb_ids),
-                                         std::make_shared<demux_factory_ref>(), std::make_shared<uci_factory_ref>(),
-                                         std::move(fallback));
+    std::shared_ptr<gpu::pusch_harq_arena> arena =
+        sector != nullptr ? sector->arena : gpu::create_pusch_harq_arena(device, bc.max_cb_ids);
+    batch = gpu::create_pusch_slot_batch(bc, arena, std::make_shared<demux_factory_ref>(),
+                                         std::make_shared<uci_factory_ref>(), std::move(fallback), service);
     pusch = gpu::create_pusch_processor_batch_gpu(batch);
   }
   uplink_processor_impl::task_executor_collection execs{test_executor(),
@@ -1213,7 +1285,7 @@ ul_harness* ul_create(int device, int variant, unsigned P, unsigned grid_prb, un
                                                       std::make_unique<resource_grid_impl>(P, 14, h->nsc),
                                                       execs,
                                                       h->pool->get_pool(),
-                                                      h->notifier,
+                                                      *h->notifier,
                                                       grid_prb,
                                                       4);
   if (variant == 0) {
@@ -1309,7 +1381,10 @@ void* chain_ul_create(int device, int variant, unsigned nof_ports, unsigned grid
 {
   void* h = nullptr;
   guarded("chain_ul_create", [&] {
-    h = ul_create(device, variant, nof_ports, grid_prb, max_iter);
+    // variant bit 2: the batch completes asynchronously (results from the service's completion thread).
+    // variant bits 3 / 4: multi-GPU batch over {device} x 3 with peer copies / over {device} with RCCL.
+    h = ul_create(device, variant & 3, nof_ports, grid_prb, max_iter, nullptr, nullptr, (variant & 4) != 0,
+                  (variant & 8) != 0 ? 1 : ((variant & 16) != 0 ? 2 : 0));
     return 0;
   });
   return h;
@@ -1339,9 +1414,13 @@ int chain_ul_slot(void*               p,
   return guarded("chain_ul_slot", [&] {
     auto*            h  = static_cast<ul_harness*>(p);
     const slot_point sp(subcarrier_spacing::kHz30, slot);
-    h->notifier.records.clear();
-    h->notifier.harq_ack.clear();
+    h->notifier->reset();
     unique_uplink_pdu_slot_repository repo = h->proc->get_pdu_slot_repository(sp);
+    // An asynchronous batch releases the previous slot's grid right after its last notification.
+    for (int tries = 0; !repo.is_valid() && tries != 100000; ++tries) {
+      std::this_thread::sleep_for(std::chrono::microseconds(10));
+      repo = h->proc->get_pdu_slot_repository(sp);
+    }
     if (!repo.is_valid()) {
       return -2;
     }
@@ -1357,16 +1436,18 @@ int chain_ul_slot(void*               p,
     load_grid(grid.get(), grid_in, h->P, h->nsc);
     grid.release();
     h->proc->get_slot_processor(sp).handle_rx_symbol(13);
-    const auto& recs = h->notifier.records;
+    h->notifier->wait_for(static_cast<unsigned>(nof_pdus));  // asynchronous batches notify from the service
+    std::lock_guard<std::mutex> lock(h->notifier->mtx);
+    const auto&                 recs = h->notifier->records;
     for (size_t i = 0; i != recs.size(); ++i) {
       const ul_record& r = recs[i];
       int*             oi = out_i + 9 * i;
       float*           of = out_f + 7 * i;
       oi[0] = r.rnti, oi[1] = r.harq_id, oi[2] = r.crc_ok, oi[3] = r.nof_cbs, oi[4] = r.ldpc_obs, oi[5] = r.ldpc_min;
       oi[6] = r.ldpc_max;
-      auto ack = h->notifier.harq_ack.find(r.rnti);
-      oi[7]    = ack != h->notifier.harq_ack.end() ? ack->second.first : -1;
-      oi[8]    = ack != h->notifier.harq_ack.end() ? ack->second.second : 0;
+      auto ack = h->notifier->harq_ack.find(r.rnti);
+      oi[7]    = ack != h->notifier->harq_ack.end() ? ack->second.first : -1;
+      oi[8]    = ack != h->notifier->harq_ack.end() ? ack->second.second : 0;
       of[0] = r.ldpc_mean, of[1] = r.sinr, of[2] = r.evm, of[3] = r.ta, of[4] = r.cfo, of[5] = r.epre, of[6] = r.rsrp;
       std::memcpy(tb_out + i * tb_stride, r.payload.data(), std::min<size_t>(r.payload.size(), tb_stride));
     }
@@ -1450,31 +1531,69 @@ int chain_ul_bench(int                 device,
                    double*             seconds)
 {
   return guarded("chain_ul_bench", [&] {
+    // variant 0: reference CPU processors; 1: GPU slot batches, one synchronous uplink processor per thread (sector)
+    // with a private GPU service; 2: du_low's structure on one shared GPU service - each sector (thread) a ring of
+    // UL_RING uplink processors over one rx buffer pool and HARQ arena, slots completing asynchronously, the service
+    // gathering the sectors' slots of one slot number into one launch.
+    constexpr unsigned UL_RING = 4;
+    const bool         shared  = variant == 2;
     std::vector<std::unique_ptr<bench_worker>> workers;
-    std::vector<ul_harness*>                   hs(nof_threads, nullptr);
+    std::vector<std::unique_ptr<ul_sector>>    sectors(nof_threads);
+    std::vector<std::vector<ul_harness*>>      hs(nof_threads);
+    std::shared_ptr<gpu::pusch_gpu_service>    service;
+    if (shared) {
+      gpu::pusch_service_configuration sc;
+      sc.device                    = device;
+      sc.nof_launch_sets           = 3;
+      sc.max_slots_per_launch      = nof_threads;
+      sc.expected_slots_per_launch = nof_threads;
+      sc.gather_window_us          = 1000;
+      sc.max_grids                 = nof_threads * UL_RING;
+      service                      = gpu::create_pusch_gpu_service(sc);
+    }
     for (unsigned t = 0; t != nof_threads; ++t) {
       workers.push_back(std::make_unique<bench_worker>());
     }
-    // Each worker builds its processor on its own thread (thread-local dependency pools bind there).
+    // Each worker builds its processors on its own thread (thread-local dependency pools bind there).
     for (unsigned t = 0; t != nof_threads; ++t) {
-      workers[t]->post([&, t] { hs[t] = ul_create(device, variant, nof_ports, grid_prb, 2); });
+      workers[t]->post([&, t] {
+        if (shared) {
+          sectors[t]                      = std::make_unique<ul_sector>();
+          sectors[t]->pool                = ul_pool();
+          sectors[t]->arena               = gpu::create_pusch_harq_arena(device, UL_POOL_CODEBLOCKS);
+          sectors[t]->notifier.count_only = true;
+          for (unsigned r = 0; r != UL_RING; ++r) {
+            hs[t].push_back(ul_create(device, 1, nof_ports, grid_prb, 2, sectors[t].get(), service, true));
+          }
+        } else {
+          hs[t].push_back(ul_create(device, variant, nof_ports, grid_prb, 2));
+          hs[t].back()->notifier->count_only = true;
+        }
+      });
       workers[t]->wait();  // one at a time: the factories' first-use initialisation is not ours to race
     }
-    for (auto& w : workers) {
-      w->wait();
-    }
     const unsigned         nsc = 12 * grid_prb;
-    std::atomic<int>       ok{0};
     std::vector<unsigned>  slot_no(nof_threads, 0);
-    auto                   run_slots = [&](unsigned t, unsigned n) {
-      ul_harness* h = hs[t];
+    std::vector<unsigned>  submitted(nof_threads, 0);
+    auto                   notifier_of = [&](unsigned t) -> ul_results_recorder& {
+      return shared ? sectors[t]->notifier : *hs[t].front()->notifier;
+    };
+    auto run_slots = [&](unsigned t, unsigned n) {
       for (unsigned i = 0; i != n; ++i) {
-        const slot_point sp(subcarrier_spacing::kHz30, slot_no[t]++ % 20480);
-        h->notifier.records.clear();
+        const unsigned   s  = slot_no[t]++;
+        const slot_point sp(subcarrier_spacing::kHz30, s % 20480);
+        ul_harness*      h  = hs[t][s % hs[t].size()];
         unique_uplink_pdu_slot_repository repo = h->proc->get_pdu_slot_repository(sp);
+        while (!repo.is_valid()) {
+          // The ring's processor still holds an earlier slot (its PUSCH results are not all notified yet).
+          std::this_thread::yield();
+          repo = h->proc->get_pdu_slot_repository(sp);
+        }
         for (int k = 0; k != nof_pdus; ++k) {
           chain_params c = pdus[k];
           c.slot         = static_cast<int>(sp.slot_index());
+          // A UE's HARQ process per slot in flight (du_low's UEs cycle their 16 processes).
+          c.harq_id = (c.harq_id + static_cast<int>(s)) % 16;
           repo->add_pusch_pdu({static_cast<unsigned>(c.harq_id), units::bytes(static_cast<unsigned>(tb_bytes[k])),
                                make_pusch_pdu(c)});
         }
@@ -1487,10 +1606,9 @@ int chain_ul_bench(int                 device,
         }
         g.release();
         h->proc->get_slot_processor(sp).handle_rx_symbol(13);
-        for (const ul_record& r : h->notifier.records) {
-          ok += r.crc_ok;
-        }
+        submitted[t] += static_cast<unsigned>(nof_pdus);
       }
+      notifier_of(t).wait_for(submitted[t]);  // every result of this thread's slots notified
     };
     // Warm-up over one frame (20 slots at 30 kHz): every slot number's DM-RS plans, pools, first touch - a DU runs
     // continuously, and the GPU batches cache their slot-dependent plans per slot number.
@@ -1500,9 +1618,13 @@ int chain_ul_bench(int                 device,
     for (auto& w : workers) {
       w->wait();
     }
+    int ok = 0;
     for (unsigned r = 0; r != repetitions; ++r) {
-      ok              = 0;
-      const auto t0   = std::chrono::steady_clock::now();
+      for (unsigned t = 0; t != nof_threads; ++t) {
+        notifier_of(t).reset();
+        submitted[t] = 0;
+      }
+      const auto t0 = std::chrono::steady_clock::now();
       for (unsigned t = 0; t != nof_threads; ++t) {
         workers[t]->post([&, t] { run_slots(t, slots); });
       }
@@ -1510,12 +1632,22 @@ int chain_ul_bench(int                 device,
         w->wait();
       }
       seconds[r] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      ok         = 0;
+      for (unsigned t = 0; t != nof_threads; ++t) {
+        ok += static_cast<int>(notifier_of(t).crc_ok.load());
+      }
     }
     for (unsigned t = 0; t != nof_threads; ++t) {
-      workers[t]->post([&, t] { delete hs[t]; });
+      workers[t]->post([&, t] {
+        for (ul_harness* h : hs[t]) {
+          delete h;
+        }
+        sectors[t].reset();
+      });
       workers[t]->wait();
     }
-    return ok.load();
+    service.reset();
+    return ok;
   });
 }
 

@@ -416,4 +416,72 @@ int hal_pdsch_encode(void*          p,
   return 0;
 }
 
+/// One TB's codeblocks through one GPU accelerator directly (hw_accelerator_pusch_dec: configure, enqueue, dequeue,
+/// read_operation_outputs), BG1 / CRC24B / rv 0 / new data: codeblock c has E = rm_lengths[c] LLRs at llrs + offsets;
+/// codeblocks with reject[c] != 0 are enqueued with an oversized span, which the accelerator rejects (reports as a
+/// failed codeblock). Outputs per codeblock: crc_pass[c], iters[c], msg bytes at msgs + c * msg_stride.
+int hal_accel_decode_ops(int            device,
+                         unsigned       nof_cbs,
+                         unsigned       lifting_size,
+                         unsigned       nof_filler_bits,
+                         unsigned       qm,
+                         const unsigned* rm_lengths,
+                         const int8_t*  llrs,
+                         const uint8_t* reject,
+                         int*           crc_pass,
+                         int*           iters,
+                         uint8_t*       msgs,
+                         unsigned       msg_stride)
+{
+  try {
+    auto factory = hal::create_hw_accelerator_pusch_dec_factory_gpu(device, 64);
+    auto acc     = factory->create();
+    std::vector<int8_t> oversized(66 * 384 * 8 + 1, 0);
+    size_t              off = 0;
+    acc->reserve_queue();
+    for (unsigned c = 0; c != nof_cbs; ++c) {
+      hal::hw_pusch_decoder_configuration cfg = {};
+      cfg.base_graph_index        = ldpc_base_graph_type::BG1;
+      cfg.modulation              = qm == 2 ? modulation_scheme::QPSK
+                                    : qm == 4 ? modulation_scheme::QAM16
+                                    : qm == 6 ? modulation_scheme::QAM64
+                                              : modulation_scheme::QAM256;
+      cfg.nof_segments            = nof_cbs;
+      cfg.rv                      = 0;
+      cfg.cw_length               = rm_lengths[c];
+      cfg.lifting_size            = lifting_size;
+      cfg.Ncb                     = 66 * lifting_size;
+      cfg.Nref                    = 0;
+      cfg.nof_segment_bits        = 22 * lifting_size;
+      cfg.nof_filler_bits         = nof_filler_bits;
+      cfg.max_nof_ldpc_iterations = 6;
+      cfg.use_early_stop          = true;
+      cfg.new_data                = true;
+      cfg.cb_crc_len              = 24;
+      cfg.cb_crc_type             = hal::hw_dec_cb_crc_type::CRC24B;
+      cfg.absolute_cb_id          = c;
+      acc->configure_operation(cfg, c);
+      span<const int8_t> data = reject[c] != 0 ? span<const int8_t>(oversized) : span<const int8_t>(llrs + off, rm_lengths[c]);
+      if (!acc->enqueue_operation(data, {}, c)) {
+        return -2;
+      }
+      off += rm_lengths[c];
+    }
+    for (unsigned c = 0; c != nof_cbs; ++c) {
+      if (!acc->dequeue_operation(span<uint8_t>(msgs + c * msg_stride, msg_stride), {}, c)) {
+        return -3;
+      }
+      hal::hw_pusch_decoder_outputs out = {};
+      acc->read_operation_outputs(out, c, c);
+      crc_pass[c] = out.CRC_pass ? 1 : 0;
+      iters[c]    = static_cast<int>(out.nof_ldpc_iterations);
+    }
+    acc->free_queue();
+    return 0;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "hal_accel_decode_ops: %s\n", e.what());
+    return -1;
+  }
+}
+
 } // extern "C"

@@ -18,6 +18,7 @@ struct srsgpu_ulsch_demux_plan {
   uint32_t*                          d_seq      = nullptr;
   int                                nof_chunks = 0;
   std::vector<std::array<uint32_t, 5>> nof_llrs;  ///< Per transmission: codeword, UL-SCH, HARQ-ACK, CSI-1, CSI-2.
+  std::vector<std::array<std::array<uint32_t, 14>, 5>> symbol_llrs;  ///< The same per OFDM symbol.
 };
 
 namespace {
@@ -70,6 +71,7 @@ int srsgpu_ulsch_demux_plan_create(srsgpu_context*                  ctx,
   std::vector<ulsch_demux_route>    routes;
   std::vector<mod_chunk>            chunks;
   std::vector<std::array<uint32_t, 5>> counts(nof_tx);
+  std::vector<std::array<std::array<uint32_t, 14>, 5>> sym_counts(nof_tx);
   std::vector<uint32_t>             c_inits(nof_tx), nwords(nof_tx);
   for (uint32_t t = 0; t < nof_tx; ++t) {
     const srsgpu_ulsch_demux_config& c  = cfgs[t];
@@ -171,11 +173,17 @@ int srsgpu_ulsch_demux_plan_create(srsgpu_context*                  ctx,
           }
         }
       }
+      const uint32_t n_sch0 = n_sch;
       for (uint32_t i = 0; i < M; ++i) {
         if (ulsch[i]) {
           sym[i].sch = n_sch++;
         }
       }
+      sym_counts[t][0][l] = M * lq;
+      sym_counts[t][1][l] = (n_sch - n_sch0) * lq;
+      sym_counts[t][2][l] = static_cast<uint32_t>(harq.size()) * lq;
+      sym_counts[t][3][l] = static_cast<uint32_t>(csi1.size()) * lq;
+      sym_counts[t][4][l] = static_cast<uint32_t>(csi2.size()) * lq;
       routes.insert(routes.end(), sym.begin(), sym.end());
       n_re += M;
     }
@@ -218,6 +226,7 @@ int srsgpu_ulsch_demux_plan_create(srsgpu_context*                  ctx,
   plan->ctx        = ctx;
   plan->nof_chunks = static_cast<int>(chunks.size());
   plan->nof_llrs   = std::move(counts);
+  plan->symbol_llrs = std::move(sym_counts);
   if (!chunks.empty()) {
     if (build_gold_sequences(ctx, c_inits, nwords, seq_off, &plan->d_seq) != SRSGPU_OK) {
       srsgpu_ulsch_demux_plan_destroy(plan);
@@ -245,6 +254,16 @@ int srsgpu_ulsch_demux_plan_create(srsgpu_context*                  ctx,
 uint32_t srsgpu_ulsch_demux_plan_nof_llrs(const srsgpu_ulsch_demux_plan* plan, uint32_t tx, uint32_t stream)
 {
   return (plan == nullptr || tx >= plan->nof_llrs.size() || stream > 4) ? 0u : plan->nof_llrs[tx][stream];
+}
+
+int srsgpu_ulsch_demux_plan_symbol_llrs(const srsgpu_ulsch_demux_plan* plan, uint32_t tx, uint32_t stream,
+                                        uint32_t counts[14])
+{
+  if (plan == nullptr || counts == nullptr || tx >= plan->symbol_llrs.size() || stream > 4) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "invalid plan, transmission or stream");
+  }
+  std::copy(plan->symbol_llrs[tx][stream].begin(), plan->symbol_llrs[tx][stream].end(), counts);
+  return SRSGPU_OK;
 }
 
 int srsgpu_ulsch_demux_plan_execute(const srsgpu_ulsch_demux_plan* plan,

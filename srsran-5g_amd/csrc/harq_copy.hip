@@ -9,14 +9,18 @@
 
 namespace {
 
+/// MULTI: the job's arena is arenas[j.arena] (several sectors' rx buffer pools in one launch).
+template <bool MULTI>
 __global__ void __launch_bounds__(256) harq_copy_kernel(int8_t* __restrict__ arena,
+                                                        int8_t* const* __restrict__ arenas,
                                                         uint32_t arena_stride,
                                                         int8_t* __restrict__ batch,
                                                         const srsgpu_harq_copy_job* __restrict__ jobs,
                                                         int to_arena)
 {
   const srsgpu_harq_copy_job j = jobs[blockIdx.x];
-  int8_t*       a   = arena + static_cast<size_t>(j.slot) * arena_stride;
+  int8_t*       base = MULTI ? arenas[j.arena] : arena;
+  int8_t*       a    = base + static_cast<size_t>(j.slot) * arena_stride;
   int8_t*       b   = batch + j.batch_offset;
   const int8_t* src = to_arena ? b : a;
   int8_t*       dst = to_arena ? a : b;
@@ -52,10 +56,34 @@ extern "C" int srsgpu_harq_copy(srsgpu_context*             ctx,
   if (nof_jobs == 0) {
     return SRSGPU_OK;
   }
-  harq_copy_kernel<<<nof_jobs, 256, 0, static_cast<hipStream_t>(stream)>>>(
-      d_arena, arena_stride, d_batch, d_jobs, direction == SRSGPU_HARQ_TO_ARENA ? 1 : 0);
+  harq_copy_kernel<false><<<nof_jobs, 256, 0, static_cast<hipStream_t>(stream)>>>(
+      d_arena, nullptr, arena_stride, d_batch, d_jobs, direction == SRSGPU_HARQ_TO_ARENA ? 1 : 0);
   if (hipGetLastError() != hipSuccess) {
     return srsgpu::fail(SRSGPU_ERR_HIP, "srsgpu_harq_copy: launch failed");
+  }
+  return SRSGPU_OK;
+}
+
+extern "C" int srsgpu_harq_copy_arenas(srsgpu_context*             ctx,
+                                       int                         direction,
+                                       int8_t* const*              d_arenas,
+                                       uint32_t                    arena_stride,
+                                       int8_t*                     d_batch,
+                                       const srsgpu_harq_copy_job* d_jobs,
+                                       uint32_t                    nof_jobs,
+                                       void*                       stream)
+{
+  if (ctx == nullptr || d_arenas == nullptr || d_batch == nullptr || (d_jobs == nullptr && nof_jobs > 0) ||
+      (direction != SRSGPU_HARQ_TO_BATCH && direction != SRSGPU_HARQ_TO_ARENA)) {
+    return srsgpu::fail(SRSGPU_ERR_INVALID_ARG, "srsgpu_harq_copy_arenas: invalid argument");
+  }
+  if (nof_jobs == 0) {
+    return SRSGPU_OK;
+  }
+  harq_copy_kernel<true><<<nof_jobs, 256, 0, static_cast<hipStream_t>(stream)>>>(
+      nullptr, d_arenas, arena_stride, d_batch, d_jobs, direction == SRSGPU_HARQ_TO_ARENA ? 1 : 0);
+  if (hipGetLastError() != hipSuccess) {
+    return srsgpu::fail(SRSGPU_ERR_HIP, "srsgpu_harq_copy_arenas: launch failed");
   }
   return SRSGPU_OK;
 }

@@ -859,7 +859,11 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
     DEC_STAMP(2 + 2 * (it & 7));
 
     // CRC after every iteration with early stop (ldpc_decoder_impl.cpp:133), else after the last one.
+#ifdef LDPC_PK_EXPERIMENT_CRC_LAST  // timing experiments only: no early stop (the worst case decodes identically)
+    if (use_crc && it == max_iter - 1) {
+#else
     if (use_crc && ((d.flags & DEC_FLAG_EARLY_STOP) != 0 || it == max_iter - 1)) {
+#endif
       uint32_t acc  = 0;
       uint32_t zero = 0;
       if (active) {

@@ -364,6 +364,8 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_ulsch_demux_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(P)]
     lib.srsgpu_ulsch_demux_plan_nof_llrs.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     lib.srsgpu_ulsch_demux_plan_nof_llrs.restype = ctypes.c_uint32
+    lib.srsgpu_ulsch_demux_plan_symbol_llrs.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, P]
+    lib.srsgpu_ulsch_demux_plan_symbol_llrs.restype = ctypes.c_int
     lib.srsgpu_ulsch_demux_plan_execute.argtypes = [P, P, P, P, P, P, P]
     lib.srsgpu_ulsch_demux_plan_destroy.argtypes = [P]
     lib.srsgpu_ulsch_demux_plan_destroy.restype = None
@@ -422,6 +424,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
     "srsgpu_pusch_demodulator_plan_create_ex", "srsgpu_pusch_demodulator_plan_execute_ex",
     "srsgpu_pusch_chest_plan_create_ex", "srsgpu_ulsch_demux_plan_create", "srsgpu_ulsch_demux_plan_nof_llrs",
+    "srsgpu_ulsch_demux_plan_symbol_llrs", "srsgpu_harq_copy_arenas",
     "srsgpu_ulsch_demux_plan_execute", "srsgpu_ulsch_demux_plan_destroy",
     "srsgpu_pusch_chest_plan_create", "srsgpu_pusch_chest_plan_execute", "srsgpu_pusch_chest_plan_destroy",
     "srsgpu_pdsch_dmrs_plan_create", "srsgpu_pdsch_dmrs_plan_create_ex", "srsgpu_pdsch_dmrs_plan_execute", "srsgpu_pdsch_dmrs_plan_destroy",
@@ -1342,6 +1345,13 @@ class UlschDemuxPlan:
                                                    ctypes.byref(h)))
         self.handle = h
         self.counts = n
+
+    def symbol_llrs(self, tx: int, stream: str) -> np.ndarray:
+        """LLRs of `stream` (codeword, sch, harq, csi1, csi2) per OFDM symbol 0..13 of transmission tx."""
+        out = np.zeros(14, np.uint32)
+        _check(_lib.srsgpu_ulsch_demux_plan_symbol_llrs(self.handle, tx, self.STREAMS.index(stream),
+                                                        out.ctypes.data_as(ctypes.c_void_p)))
+        return out
 
     def execute(self, d_llrs, d_sch, d_harq=None, d_csi1=None, d_csi2=None, stream=None):
         _check(_lib.srsgpu_ulsch_demux_plan_execute(self.handle, _dptr(d_llrs), _dptr(d_sch), _dptr(d_harq),

@@ -114,6 +114,8 @@ UL_INTS = ("rnti", "harq_id", "tb_crc_ok", "nof_cbs", "ldpc_obs", "ldpc_min", "l
            "harq_ack_bits")
 UL_FLOATS = ("ldpc_mean", "sinr_db", "evm", "ta_s", "cfo_hz", "epre_db", "rsrp_db")
 UL_CPU, UL_GPU_BATCH = 0, 1
+UL_INTERPOLATE, UL_ASYNC = 2, 4  # variant bits: estimator time strategy, asynchronous batch completion
+UL_MULTI_COPY, UL_MULTI_RCCL = 8, 16  # multi-GPU batch: 3 UE shards on one device (peer copies) / RCCL world size 1
 DL_CPU, DL_GPU_BATCH = 0, 1
 
 

@@ -128,3 +128,49 @@ def test_hal_pusch_decoder_thread_pool_shares_harq():
         assert s_a == s_b and np.array_equal(tb_a, tb_b), (s_a, s_b)
     finally:
         pool.close()
+
+
+def test_hal_accelerator_rejected_codeblock_keeps_the_others_results():
+    """A codeblock the accelerator rejects at enqueue (here an oversized rate-matched span) is reported as failed, and
+    every other codeblock of the TB still reports ITS OWN CRC flag, iteration count and message: the plan numbers only
+    the accepted codeblocks, so the results are scattered back to their operations
+    (integration/hw_accelerator_pusch_dec_gpu.cpp run(); round-4 ADVICE). The first of four codeblocks is rejected;
+    the last one is noisy enough to need more iterations than the clean ones, so a shifted read would show."""
+    import ctypes
+    import hal_lib
+    orc = Oracle()
+    rng = np.random.default_rng(5)
+    g = sch.UeGrant(100, 1, 6, 772.0, nof_dmrs_symbols=2)
+    seg = g.segmentation()
+    assert seg.base_graph == 1 and seg.nof_segments >= 3
+    tb = rng.integers(0, 256, seg.tbs // 8).astype(np.uint8)
+    cw, _, _ = oracle_pdsch_encode(orc, tb, 1, 0, g.qm, 1, 0, g.nof_ch_symbols)
+    n = seg.nof_segments
+    parts = []
+    for cb in seg.codeblocks:
+        bits = cw[cb.cw_offset:cb.cw_offset + cb.rm_length]
+        noise = 3.5 if cb.index == n - 1 else 0.0
+        parts.append(bits_to_llrs(rng, bits, amp=8.0, noise=noise))
+    llrs = np.concatenate(parts)
+    lib = ctypes.CDLL(hal_lib.HAL_SO)
+    P = ctypes.c_void_p
+    lib.hal_accel_decode_ops.restype = ctypes.c_int
+    lib.hal_accel_decode_ops.argtypes = [ctypes.c_int] + [ctypes.c_uint] * 4 + [P] * 6 + [ctypes.c_uint]
+    E = np.array([cb.rm_length for cb in seg.codeblocks], np.uint32)
+
+    def run(reject):
+        rej = np.array(reject, np.uint8)
+        crc = np.zeros(n, np.int32)
+        its = np.zeros(n, np.int32)
+        msgs = np.zeros((n, 1056), np.uint8)
+        ptr = lambda a: a.ctypes.data_as(P)  # noqa: E731
+        assert lib.hal_accel_decode_ops(0, n, seg.lifting_size, seg.nof_filler_bits, g.qm, ptr(E), ptr(llrs), ptr(rej),
+                                        ptr(crc), ptr(its), ptr(msgs), 1056) == 0
+        return crc, its, msgs
+
+    crc0, its0, msgs0 = run([0] * n)
+    assert crc0.all() and its0[-1] > its0[0], (crc0, its0)
+    crc1, its1, msgs1 = run([1] + [0] * (n - 1))
+    assert crc1[0] == 0 and its1[0] == 6, (crc1, its1)
+    assert np.array_equal(crc1[1:], crc0[1:]) and np.array_equal(its1[1:], its0[1:]), (crc0, its0, crc1, its1)
+    assert np.array_equal(msgs1[1:], msgs0[1:])

@@ -65,3 +65,25 @@ def test_ulsch_demux_rejects_unfit_uci(ctx):
     cfg = dict(cfg, nof_harq_ack_bits=5, nof_enc_harq_ack_bits=10 ** 6, nof_harq_ack_rvd=0)
     with pytest.raises(srsgpu.SrsGpuError):
         srsgpu.UlschDemuxPlan(ctx, [to_demux(cfg, c2b, c2e, c_init)], [0])
+
+
+def test_ulsch_demux_symbol_llrs_vs_oracle(ctx):
+    """Per-OFDM-symbol LLR counts of every stream (srsgpu_ulsch_demux_plan_symbol_llrs, what the upper-PHY replay feeds
+    the reference's UCI decoders symbol by symbol) equal the restatement's RE sets x layers x Qm."""
+    import srsgpu
+    rng = np.random.default_rng(8)
+    for _ in range(40):
+        cfg, c2b, c2e, _ = random_config(rng, max_prb=30, allow_first_empty=True)
+        plan = srsgpu.UlschDemuxPlan(ctx, [to_demux(cfg, c2b, c2e, 0x4601 << 15)], [0])
+        lq = cfg["qm"] * cfg["nof_layers"]
+        want = {k: np.zeros(14, np.uint32) for k in ("codeword", "sch", "harq", "csi1", "csi2")}
+        for l, M, sets in U.symbol_plan(cfg, c2e):
+            want["codeword"][l] = M * lq
+            want["sch"][l] = len(sets["ulsch"]) * lq
+            for k in ("harq", "csi1", "csi2"):
+                want[k][l] = len(sets[k]) * lq
+        for k, w in want.items():
+            got = plan.symbol_llrs(0, k)
+            assert np.array_equal(got, w), (k, cfg, got, w)
+            assert int(got.sum()) == plan.counts[0][plan.STREAMS.index(k)]
+        plan.close()

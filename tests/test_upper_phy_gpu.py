@@ -26,11 +26,18 @@ T_C = 1.0 / (480000 * 4096)
 P = 4
 
 
-@pytest.fixture(scope="module")
-def procs():
+@pytest.fixture(scope="module", params=["sync", "async", "multi3_copy", "multi1_rccl"])
+def procs(request):
+    """The reference's CPU processors and the GPU batches, the latter completing synchronously (the PUSCH task returns
+    with the results notified), asynchronously (results notified from the GPU service's completion thread), or as the
+    multi-GPU batch of row b7: the slot's UEs sharded by RNTI over the device list {0, 0, 0} (three shards with their
+    own launch plans, HARQ arenas and grid copies on one GPU, results gathered by peer copies) or over {0} with the
+    RCCL transport (world size 1: the gather is an ncclSend / ncclRecv pair in one group). Every mode must equal the
+    reference's CPU processors, hence the single-device batch."""
     import chain_harness as H
     cpu = H.UpperPhy(0, H.UL_CPU, P)
-    gpu = H.UpperPhy(0, H.UL_GPU_BATCH, P)
+    extra = {"sync": 0, "async": H.UL_ASYNC, "multi3_copy": H.UL_MULTI_COPY, "multi1_rccl": H.UL_MULTI_RCCL}
+    gpu = H.UpperPhy(0, H.UL_GPU_BATCH | extra[request.param], P)
     yield cpu, gpu
     cpu.close()
     gpu.close()

@@ -1,0 +1,69 @@
+#!/usr/bin/env bash
+# One parameterised GPU-box script for the round's measurements (replaces the one-off rN*.sh scripts, kept under
+# tools/gpu/archive/). Usage on the box (via gpurun):  tools/gpu/round.sh TAG STEP [STEP ...]
+# Each step runs under its own time limit and writes into gpurun_out/TAG/; the script stops at the first failure.
+#   tests            GPU parity suite (pytest -m gpu)
+#   tests:EXPR       GPU tests selected by pytest -k EXPR
+#   smoke            __graft_entry__.smoke()
+#   bench            python bench.py (default shape) -> bench.json
+#   bench_driver     python bench.py --steps 20 --warmup 5 -> bench_driver.json
+#   slots1 / slots16 tools/processor_bench.py --only-slots at 1 / 16 threads (SRSGPU_BATCH_TIMING=1)
+#   slots16ul        the same, UL only
+#   slots_trace16    the same at 16 threads
+#   slots_trace      rocprofv3 kernel + memory-copy trace of the slot processors at one thread (UL)
+#   kstats           rocprofv3 --kernel-trace --stats of the default bench
+#   lower            tools/lower_phy_bench.py
+set -o pipefail
+TAG=${1:?tag}
+shift
+cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case "$step" in
+    tests)
+      timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+        > "$OUT/gpu_tests.log" 2>&1 || { tail -30 "$OUT/gpu_tests.log"; exit 1; }
+      tail -3 "$OUT/gpu_tests.log" ;;
+    tests:*)
+      timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        -k "${step#tests:}" > "$OUT/gpu_tests_k.log" 2>&1 || { tail -40 "$OUT/gpu_tests_k.log"; exit 1; }
+      tail -3 "$OUT/gpu_tests_k.log" ;;
+    smoke)
+      timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+        || { cat "$OUT/smoke.log"; exit 1; }
+      cat "$OUT/smoke.log" ;;
+    bench)
+      timeout -k 10 300 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
+      tail -c 600 "$OUT/bench.json" ;;
+    bench_driver)
+      timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench_driver.json" 2> "$OUT/bench_driver.err" \
+        || { tail -20 "$OUT/bench_driver.err"; exit 1; }
+      tail -c 400 "$OUT/bench_driver.json" ;;
+    slots1|slots16|slots16ul)
+      T=${step#slots}; T=${T%ul}; DIRS=ul,dl; [[ "$step" == *ul ]] && DIRS=ul
+      SRSGPU_BATCH_TIMING=1 timeout -k 10 400 python -u tools/processor_bench.py --only-slots --threads "$T" \
+        --slots 100 --repetitions 3 --directions "$DIRS" > "$OUT/$step.json" 2> "$OUT/$step.log" \
+        || { tail -20 "$OUT/$step.log"; exit 1; }
+      grep -v '^pusch_slot_batch' "$OUT/$step.log" | tail -4; grep '^pusch_slot_batch' "$OUT/$step.log" | tail -2 ;;
+    slots_trace16)
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/trace16" -o slots -- python3 -u \
+        tools/processor_bench.py --only-slots --threads 16 --repetitions 1 --slots 30 --directions ul \
+        > "$OUT/slots_trace16.log" 2>&1 || { tail -20 "$OUT/slots_trace16.log"; exit 1; } ;;
+    slots_trace)
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/trace" -o slots -- python3 -u \
+        tools/processor_bench.py --only-slots --threads 1 --repetitions 1 --slots 30 --directions ul \
+        > "$OUT/slots_trace.log" 2>&1 || { tail -20 "$OUT/slots_trace.log"; exit 1; } ;;
+    kstats)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kstats" -o k -- python3 -u bench.py \
+        > "$OUT/kstats_bench.json" 2> "$OUT/kstats.log" || { tail -20 "$OUT/kstats.log"; exit 1; } ;;
+    lower)
+      timeout -k 10 300 python -u tools/lower_phy_bench.py > "$OUT/lower.json" 2> "$OUT/lower.log" \
+        || { tail -20 "$OUT/lower.log"; exit 1; }
+      tail -c 800 "$OUT/lower.json" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"

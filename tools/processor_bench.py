@@ -45,10 +45,12 @@ def run(lib, fn, mode, p, tbs, threads, batch, reps, weights=None):
             "pdus_per_s": pdus / med, "tb_crc_ok": int(r)}
 
 
-def slot_cases(lib, T, slots, R):
+def slot_cases(lib, T, slots, R, directions=("ul", "dl")):
     """The same profiles through the reference's slot processors (uplink_processor_impl /
     downlink_processor_single_executor_impl), one per thread, reference CPU processors (variant 0) vs the GPU slot batches
-    of integration/upper_phy_gpu.cpp (variant 1): the single full-band PDU per slot of the reference benchmarks, and the
+    of integration/pusch_batch_gpu.cpp / upper_phy_gpu.cpp (variant 1: one synchronous uplink processor per thread;
+    UL variant 2: du_low's shape - a ring of uplink processors per sector, asynchronous completion, one GPU service
+    gathering every sector's slot into one launch): the single full-band PDU per slot of the reference benchmarks, and the
     multi-UE slot at the slot processors' capacity (MAX_PUSCH_PDUS_PER_SLOT = MAX_UE_PDUS_PER_SLOT = 16,
     slot_pdu_capacity_constants.h:44/:77: 16 UEs x 17 PRB) where the batch gathers the 16 PDUs into one launch
     sequence."""
@@ -72,13 +74,15 @@ def slot_cases(lib, T, slots, R):
         grid = (rng.normal(size=(4, 14, 12 * 273, 2)) * 0.1).astype(np.float32)
         g = ((grid.view(np.uint32) + 0x7FFF + ((grid.view(np.uint32) >> 16) & 1)) >> 16).astype(np.uint16)
         case = {"profile": name, "nof_pdus_per_slot": len(pdus), "tb_bits_per_slot": int(sum(tbs)), "runs": []}
-        for v in (0, 1):
+        for v in (0, 1, 2):
             n = slots
             secs = np.zeros(R, np.float64)
             r = lib.chain_ul_bench(0, v, T, n, R, len(pdus), arr, ptr(tbb), ptr(g), 4, 273, ptr(secs))
             assert r >= 0, r
             med = float(np.median(secs))
-            case["runs"].append({"variant": ["reference CPU processors", "GPU slot batch"][v], "threads": T,
+            case["runs"].append({"variant": ["reference CPU processors", "GPU slot batch, synchronous",
+                                             "GPU service: 4 uplink processors per sector, asynchronous, "
+                                             "sectors aggregated per slot"][v], "threads": T,
                                  "slots_per_thread": n, "seconds_median": med,
                                  "throughput_mbps_median": T * n * sum(tbs) / med / 1e6,
                                  "slots_per_s": T * n / med})
@@ -109,6 +113,10 @@ def slot_cases(lib, T, slots, R):
     p = H.params(slot=0, rnti=1, n_id=0, scrambling_id=0, nof_rb=273, rb_start=0, bwp_size=273, qm=8,
                  target_code_rate=948.0, nof_layers=1, nof_ports=4, base_graph=sch.base_graph(tbs, 948 / 1024),
                  tbs_lbrm_bytes=159749, max_iterations=2)
+    if "ul" not in directions:
+        ul = lambda *a: None  # noqa: E731
+    if "dl" not in directions:
+        dl = lambda *a: None  # noqa: E731
     ul("scs30_100MHz_256qam_rv0_4port_1layer, one PDU per slot", [p], [tbs])
     pdus, tb_list = [], []
     for i in range(16):
@@ -148,11 +156,13 @@ def main():
     ap.add_argument("--repetitions", type=int, default=5)
     ap.add_argument("--slots", type=int, default=20, help="slot-processor section: slots per thread and repetition")
     ap.add_argument("--only-slots", action="store_true", help="run only the slot-processor section")
+    ap.add_argument("--directions", default="ul,dl", help="slot-processor section: ul, dl or ul,dl")
     args = ap.parse_args()
     if args.only_slots:
         print(json.dumps({"threads": args.threads, "slot_processors": slot_cases(ctypes.CDLL(H.CHAIN_SO),
                                                                                 args.threads, args.slots,
-                                                                                args.repetitions)}))
+                                                                                args.repetitions,
+                                                                                args.directions.split(","))}))
         return
     lib = ctypes.CDLL(H.CHAIN_SO)
     PP = ctypes.POINTER(H.ChainParams)

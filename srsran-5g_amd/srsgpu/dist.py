@@ -177,20 +177,24 @@ class CodeblockShard:
     """Codeblock-level sharding of a slot's PUSCH decoding across ranks.
 
     `cbs` lists the slot's codeblocks in order (every TB's, concatenated) as (llr_offset, rm_length) in the root's
-    codeword LLR buffer. Rank r owns the contiguous codeblock range `shard_range(len(cbs), world, r)` and, with it, the
-    contiguous LLR span from its first codeblock's first LLR to its last one's last LLR.
+    codeword LLR buffer. Ownership: without `keys`, rank r owns the contiguous codeblock range
+    `shard_range(len(cbs), world, r)` (one contiguous LLR span each) - valid for slots of new transmissions only, since a
+    retransmitted TB's codeblocks move with the slot's composition. With `keys` (one stable HARQ key per codeblock, e.g.
+    the rx buffer pool's absolute codeblock identifier, rx_buffer.h:65), codeblock i belongs to rank keys[i] mod world in
+    every slot, so a retransmission is decoded by the rank whose HARQ buffer holds the earlier transmissions' soft bits
+    (its LLRs are packed per rank for the scatter).
 
-    Per slot: `scatter_llrs` hands every rank its span (one scatter; the root keeps its own); each rank rate-dematches and
-    decodes its codeblocks into its own HARQ buffers (a srsgpu_pusch_cb_plan over `local_cbs`, LLR offsets relative to
-    the span: the HARQ memory is sharded as well); `gather` brings the messages (CB_MSG_STRIDE bytes each) and CRC flags
-    into the root's slot-wide buffers (one gather), where srsgpu_pusch_decoder_plan_assemble joins them into TBs and
-    checks the TB CRCs (pusch_decoder_impl.cpp:386); `return_flags` scatters the root's final flags back, so a TB CRC
-    mismatch clears the owners' codeblock flags exactly as the reference resets them for the retransmission (:423).
-    Buffers are allocated once; copies and collectives run on the current stream.
+    Per slot: `scatter_llrs` hands every rank its codeblocks' LLRs (one scatter; the root keeps its own); each rank
+    rate-dematches and decodes its codeblocks into its own HARQ buffers (a srsgpu_pusch_cb_plan over `local_cbs`, LLR
+    offsets relative to its buffer: the HARQ memory is sharded as well); `gather` brings the messages (CB_MSG_STRIDE bytes
+    each) and CRC flags into the root's slot-wide buffers (one gather), where srsgpu_pusch_decoder_plan_assemble joins
+    them into TBs and checks the TB CRCs (pusch_decoder_impl.cpp:386); `return_flags` scatters the root's final flags
+    back, so a TB CRC mismatch clears the owners' codeblock flags exactly as the reference resets them for the
+    retransmission (:423). Buffers are allocated once; copies and collectives run on the current stream.
     """
 
     def __init__(self, cbs: Sequence[tuple], device: torch.device, root: int = 0,
-                 group: Optional[dist.ProcessGroup] = None):
+                 group: Optional[dist.ProcessGroup] = None, keys: Optional[Sequence[int]] = None):
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.root, self.group = root, group
@@ -198,20 +202,33 @@ class CodeblockShard:
         for (o, e), (o2, _) in zip(self.cbs, self.cbs[1:]):
             if o2 < o + e:
                 raise ValueError("codeblock LLR ranges must be in order and disjoint")
-        self.ranges = [shard_range(len(self.cbs), self.world, r) for r in range(self.world)]
-        self.spans = []
-        for rg in self.ranges:
-            if len(rg) == 0:
-                self.spans.append((0, 0))
-            else:
-                b = self.cbs[rg.start][0]
-                self.spans.append((b, self.cbs[rg.stop - 1][0] + self.cbs[rg.stop - 1][1] - b))
-        self.max_span = max(1, max(n for _, n in self.spans))
-        self.max_cbs = max(1, max(len(rg) for rg in self.ranges))
-        mine = self.ranges[self.rank]
-        b0 = self.spans[self.rank][0]
-        #: (llr_offset relative to this rank's span, rm_length) of the codeblocks this rank decodes
-        self.local_cbs = [(self.cbs[i][0] - b0, self.cbs[i][1]) for i in mine]
+        if keys is None:
+            #: codeblock indices (slot order) each rank decodes
+            self.members = [list(shard_range(len(self.cbs), self.world, r)) for r in range(self.world)]
+        else:
+            if len(keys) != len(self.cbs):
+                raise ValueError("one HARQ key per codeblock")
+            self.members = [[i for i, k in enumerate(keys) if int(k) % self.world == r] for r in range(self.world)]
+        #: per rank: (first LLR, count) pieces of the root's buffer it receives, contiguous pieces merged
+        self.pieces = []
+        for mem in self.members:
+            pcs = []
+            for i in mem:
+                o, e = self.cbs[i]
+                if pcs and pcs[-1][0] + pcs[-1][1] == o:
+                    pcs[-1] = (pcs[-1][0], pcs[-1][1] + e)
+                else:
+                    pcs.append((o, e))
+            self.pieces.append(pcs)
+        self.spans = [sum(n for _, n in pcs) for pcs in self.pieces]
+        self.max_span = max(1, max(self.spans))
+        self.max_cbs = max(1, max(len(m) for m in self.members))
+        #: (llr_offset relative to this rank's buffer, rm_length) of the codeblocks this rank decodes
+        self.local_cbs = []
+        pos = 0
+        for i in self.members[self.rank]:
+            self.local_cbs.append((pos, self.cbs[i][1]))
+            pos += self.cbs[i][1]
         self.llrs = torch.zeros(self.max_span, dtype=torch.int8, device=device)
         self._res = torch.zeros(self.max_cbs * (CB_MSG_STRIDE + 1), dtype=torch.uint8, device=device)
         self._flags = torch.zeros(self.max_cbs, dtype=torch.uint8, device=device)
@@ -223,16 +240,25 @@ class CodeblockShard:
             self._llr_all = self._res_all = self._flags_all = None
 
     @property
+    def ranges(self) -> List[List[int]]:
+        """Codeblock indices each rank decodes (slot order)."""
+        return self.members
+
+    @property
     def llr_bytes_per_rank(self) -> List[int]:
-        return [n for _, n in self.spans]
+        return list(self.spans)
 
     def scatter_llrs(self, d_llrs: Optional[torch.Tensor]) -> torch.Tensor:
-        """Root: `d_llrs` is the slot's codeword LLR buffer (other ranks pass None). Returns this rank's span."""
+        """Root: `d_llrs` is the slot's codeword LLR buffer (other ranks pass None). Returns this rank's LLRs (its
+        codeblocks' rate-matched LLRs, packed in slot order)."""
         if self.rank == self.root:
-            for r, (b, n) in enumerate(self.spans):
-                self._llr_all[r][:n].copy_(d_llrs[b:b + n])
+            for r, pcs in enumerate(self.pieces):
+                pos = 0
+                for b, n in pcs:
+                    self._llr_all[r][pos:pos + n].copy_(d_llrs[b:b + n])
+                    pos += n
         dist.scatter(self.llrs, self._llr_all, src=self.root, group=self.group)
-        return self.llrs[: self.spans[self.rank][1]]
+        return self.llrs[: self.spans[self.rank]]
 
     def gather(self, d_msgs: torch.Tensor, d_flags: torch.Tensor, d_all_msgs: Optional[torch.Tensor],
                d_all_flags: Optional[torch.Tensor]) -> None:
@@ -245,17 +271,20 @@ class CodeblockShard:
         self._res[self.max_cbs * CB_MSG_STRIDE: self.max_cbs * CB_MSG_STRIDE + n].copy_(d_flags[:n])
         dist.gather(self._res, self._res_all, dst=self.root, group=self.group)
         if self.rank == self.root:
-            for r, rg in enumerate(self.ranges):
-                k = len(rg)
+            S = CB_MSG_STRIDE
+            for r, mem in enumerate(self.members):
                 src = self._res_all[r]
-                d_all_msgs[rg.start * CB_MSG_STRIDE: rg.stop * CB_MSG_STRIDE].copy_(src[: k * CB_MSG_STRIDE])
-                d_all_flags[rg.start: rg.stop].copy_(src[self.max_cbs * CB_MSG_STRIDE: self.max_cbs * CB_MSG_STRIDE + k])
+                for j, i in enumerate(mem):
+                    d_all_msgs[i * S: (i + 1) * S].copy_(src[j * S: (j + 1) * S])
+                    d_all_flags[i: i + 1].copy_(src[self.max_cbs * S + j: self.max_cbs * S + j + 1])
 
     def return_flags(self, d_all_flags: Optional[torch.Tensor], d_flags: torch.Tensor) -> None:
         """The root's codeblock flags after the TB stage back to their owners' `d_flags` (the HARQ context)."""
         if self.rank == self.root:
-            for r, rg in enumerate(self.ranges):
-                self._flags_all[r][: len(rg)].copy_(d_all_flags[rg.start: rg.stop])
+            for r, mem in enumerate(self.members):
+                if mem:
+                    idx = torch.tensor(mem, dtype=torch.long, device=d_all_flags.device)
+                    self._flags_all[r][: len(mem)].copy_(d_all_flags[idx])
         dist.scatter(self._flags, self._flags_all, src=self.root, group=self.group)
         n = len(self.local_cbs)
         d_flags[:n].copy_(self._flags[:n])

@@ -430,7 +430,7 @@ def _cb_decode(orc, segs, cb_ids, llrs_span, local_cbs):
                                    crc_poly=crc_for_tb(seg), max_iter=6)
         packed = np.packbits(np.asarray(bits, np.uint8))
         msgs[j * sdist.CB_MSG_STRIDE: j * sdist.CB_MSG_STRIDE + packed.size] = packed
-        ok[j] = 0 if it is None else 1
+        ok[j] = 0 if (it is None or it < 0) else 1  # the oracle returns -1 when the CRC never passes
     return msgs, ok
 
 
@@ -521,3 +521,123 @@ def test_codeblock_sharded_decode_gloo(world):
     assert tb_ok.tolist() == [1, 1]
     for got, want in zip(joined, tbs):
         assert np.array_equal(got, want)
+
+
+def _cb_harq_slots(orc):
+    """Two slots for the HARQ-keyed CodeblockShard: slot 1 = TBs X, Y (new, noisy: some codeblocks fail); slot 2 =
+    TB W (new) then X again (rv 0, new noise, new_data = False) - X's codeblocks sit at other positions of the slot, so
+    contiguous sharding would hand them to other ranks. Per slot: (segmentations, codeword LLRs, (offset, E) per
+    codeblock, HARQ keys, new_data per codeblock)."""
+    from chain_lib import oracle_pdsch_encode
+    rng = np.random.default_rng(77)
+
+    def tb_llrs(nbytes, seed_tb, flip_frac):
+        tb = np.random.default_rng(seed_tb).integers(0, 256, nbytes, dtype=np.uint8)
+        nof_ch_symbols = (nbytes * 8 * 2 + 7999) // 2 // 4 * 4
+        cw, _, _ = oracle_pdsch_encode(orc, tb, 1, 0, 2, 1, 0, nof_ch_symbols)
+        seg = sch.segment(nbytes * 8, 1, 2, 1, nof_ch_symbols)
+        llr = np.where(cw == 0, 8, -8).astype(np.int8)
+        flip = rng.choice(llr.size, int(llr.size * flip_frac), replace=False)
+        llr[flip] = -llr[flip]
+        return seg, llr
+
+    def slot(items):
+        segs, llrs, cbs, keys, new, off = [], [], [], [], [], 0
+        for (nbytes, seed_tb, flip), key0, nd in items:
+            seg, llr = tb_llrs(nbytes, seed_tb, flip)
+            segs.append(seg)
+            llrs.append(llr)
+            cbs += [(off + cb.cw_offset, cb.rm_length) for cb in seg.codeblocks]
+            keys += [key0 + c for c in range(seg.nof_segments)]
+            new += [nd] * seg.nof_segments
+            off += llr.size
+        return segs, np.concatenate(llrs), cbs, keys, new
+
+    X, Y, W = (CB_TB_BYTES[0], 11, 0.16), (CB_TB_BYTES[1], 12, 0.03), (CB_TB_BYTES[1], 13, 0.03)
+    return slot([(X, 100, True), (Y, 200, True)]), slot([(W, 300, True), (X, 100, False)])
+
+
+def _cb_harq_decode(orc, segs, ids, llrs, local_cbs, keys, new, harq):
+    """Oracle decoding of codeblocks `ids` (slot order) with the HARQ buffers kept per key in `harq` (combined when
+    not new). Returns messages and CRC flags."""
+    from chain_lib import crc_for_tb
+    flat = [(seg, cb) for seg in segs for cb in seg.codeblocks]
+    msgs = np.zeros(len(ids) * sdist.CB_MSG_STRIDE, np.uint8)
+    ok = np.zeros(len(ids), np.uint8)
+    for j, (i, (o, e)) in enumerate(zip(ids, local_cbs)):
+        seg, cb = flat[i]
+        Z = seg.lifting_size
+        buf = harq.get(keys[i]) if not new[i] else None
+        buf = np.zeros(66 * Z, np.int8) if buf is None else buf
+        buf = orc.rate_dematch(1, 1, Z, 0, 2, 0, cb.nof_filler_bits, int(new[i]), llrs[o:o + e], buf)
+        harq[keys[i]] = buf
+        it, bits = orc.ldpc_decode(1, 1, Z, buf, nof_crc_bits=cb.nof_crc_bits, nof_filler=cb.nof_filler_bits,
+                                   crc_poly=crc_for_tb(seg), max_iter=6)
+        packed = np.packbits(np.asarray(bits, np.uint8))
+        msgs[j * sdist.CB_MSG_STRIDE: j * sdist.CB_MSG_STRIDE + packed.size] = packed
+        ok[j] = 0 if (it is None or it < 0) else 1  # the oracle returns -1 when the CRC never passes
+    return msgs, ok
+
+
+def _cb_harq_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from oracle_lib import Oracle
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        orc = Oracle()
+        harq = {}  # this rank's HARQ buffers, by key: they never move between ranks
+        res = []
+        for segs, llrs, cbs, keys, new in _cb_harq_slots(orc):
+            sh = sdist.CodeblockShard(cbs, torch.device("cpu"), root=0, keys=keys)
+            span = sh.scatter_llrs(torch.from_numpy(llrs) if rank == 0 else None)
+            mine = sh.members[rank]
+            assert all(keys[i] % world == rank for i in mine)
+            msgs, ok = _cb_harq_decode(orc, segs, mine, span.numpy(), sh.local_cbs, keys, new, harq)
+            n = len(cbs)
+            all_msgs = torch.zeros(n * sdist.CB_MSG_STRIDE, dtype=torch.uint8) if rank == 0 else None
+            all_ok = torch.zeros(n, dtype=torch.uint8) if rank == 0 else None
+            sh.gather(torch.from_numpy(msgs), torch.from_numpy(ok), all_msgs, all_ok)
+            if rank == 0:
+                res.append((all_msgs.numpy().copy(), all_ok.numpy().copy()))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, res if rank == 0 else None, None))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, None, traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_codeblock_shard_harq_keys_retransmission_gloo(world):
+    """CodeblockShard with HARQ keys (round-4 ADVICE): codeblock ownership follows the stable key (the rx buffer pool's
+    absolute codeblock id) instead of the slot position, so a TB retransmitted in a slot of another composition is
+    decoded by the ranks holding its earlier soft bits. Two slots; the gathered messages and CRC flags of both equal one
+    rank decoding every codeblock with every HARQ buffer, and the retransmission's combining recovers codeblocks the
+    first transmission lost."""
+    from oracle_lib import Oracle
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_cb_harq_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, res, err = q.get(timeout=300)
+        assert err is None, err
+        out[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+    orc = Oracle()
+    harq = {}
+    want = []
+    for segs, llrs, cbs, keys, new in _cb_harq_slots(orc):
+        want.append(_cb_harq_decode(orc, segs, list(range(len(cbs))), llrs, cbs, keys, new, harq))
+    for (got_msgs, got_ok), (want_msgs, want_ok) in zip(out[0], want):
+        assert np.array_equal(got_ok, want_ok)
+        assert np.array_equal(got_msgs, want_msgs)
+    nx = len(_cb_harq_slots(orc)[0][0][0].codeblocks)
+    first_x, second_x = want[0][1][:nx], want[1][1][-nx:]
+    assert first_x.sum() < nx and second_x.sum() > first_x.sum(), (first_x, second_x)

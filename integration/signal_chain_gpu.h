@@ -76,7 +76,10 @@ std::shared_ptr<pdxch_processor_factory> create_pdxch_processor_factory_gpu(int 
 /// Lower-PHY PUxCH processor on GPU `device` (integration/lower_phy_gpu.cpp), the replacement of
 /// create_puxch_processor_factory_sw (puxch_processor_factories.h:69; lower_phy_factory.cpp:84): every received symbol
 /// (all ports) is demodulated by one asynchronous launch; up to `max_symbols_in_flight` symbols are outstanding before
-/// process_symbol() waits (0: each symbol is demodulated and notified within its own call, the reference's timing).
-std::shared_ptr<puxch_processor_factory> create_puxch_processor_factory_gpu(int device, unsigned max_symbols_in_flight = 2);
+/// process_symbol() waits. 0 (the default, the drop-in setting): each symbol is demodulated and on_rx_symbol notified
+/// within its own process_symbol() call, the reference's timing (puxch_processor_impl.cpp:78). Above 0 the notification
+/// of symbol l arrives during a later symbol's call (or at the end of the slot): more throughput per sector thread, but
+/// an upper PHY that starts per-symbol work from on_rx_symbol sees it that much later.
+std::shared_ptr<puxch_processor_factory> create_puxch_processor_factory_gpu(int device, unsigned max_symbols_in_flight = 0);
 
 } // namespace srsran

@@ -1425,7 +1425,8 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
     return t.nof_cbs == 1 && t.tbs_bits / 8u <= 2048u;
   });
   plan->tb_threads = any_large ? 1024 : (all_small_single ? 64 : 256);
-  // Few large segmented TBs (at most 8, every one byte-aligned with a CRC table, one above the inline size): the TB
+  // Few large segmented TBs (at most 8, every one segmented, byte-aligned and with a CRC table, and AT LEAST one of them
+  // above the inline size - the plan's smaller segmented TBs are then sliced too, which is correct, only not needed): the TB
   // stage runs over TB_SLICE_BYTES slices, several workgroups per TB, instead of one 1024-lane workgroup per TB, whose
   // byte copy and CRC chain take ~15 us for a 37 KB TB. That latency is what a slot processor's one-PDU slot waits for
   // (UL one-PDU slot batch +3 %); with many TBs per launch the single workgroups already fill the GPU and the slices'

@@ -644,8 +644,8 @@ int srsgpu_pusch_demodulator_plan_execute_ex(const srsgpu_pusch_demodulator_plan
  * decoder's input; REs carrying HARQ-ACK of <= 2 bits stay in it as zeros), HARQ-ACK, CSI Part 1 and CSI Part 2 LLR
  * streams, with the reference's 1- / 2-bit UCI placeholder handling (the scrambling sequence c_init = rnti 2^15 + n_id
  * re-applied to the "y" and "x" placeholder bits, :91 / :131). The RE sets per OFDM symbol (reserved HARQ-ACK REs,
- * HARQ-ACK, CSI Part 1, CSI Part 2, :316) are fixed at plan creation; CSI Part 2 is placed as if set_csi_part2 were
- * called before the first symbol. Input and output offsets are in LLRs.
+ * HARQ-ACK, CSI Part 1, CSI Part 2, :316) are fixed at plan creation; CSI Part 2 is placed from csi2_first_symbol on
+ * (0: as if set_csi_part2 were called before the first symbol). Input and output offsets are in LLRs.
  * ------------------------------------------------------------------------------------------------------------------ */
 typedef struct {
   uint8_t  modulation_order;            /* Qm: 2, 4, 6, 8 */
@@ -658,7 +658,10 @@ typedef struct {
   uint8_t  nof_cdm_groups_without_data; /* 1..2 (type 1), 1..3 (type 2) */
   uint16_t rnti;                        /* scrambling c_init = rnti 2^15 + n_id (placeholders) */
   uint16_t n_id;
-  uint16_t pad;
+  uint16_t csi2_first_symbol;           /* CSI Part 2 REs only in OFDM symbols >= this one: the symbol whose
+                                           demultiplexing completes CSI Part 1, where the reference's processor calls
+                                           set_csi_part2 (pusch_processor_impl.cpp:72-100, ulsch_demultiplex_impl.cpp:241)
+                                           0: from the first symbol, as if set before it */
   uint32_t nof_harq_ack_rvd;            /* G^HARQ-ACK_rvd */
   uint32_t nof_harq_ack_bits;           /* O^HARQ-ACK */
   uint32_t nof_enc_harq_ack_bits;       /* G^HARQ-ACK */

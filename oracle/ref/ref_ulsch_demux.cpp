@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <vector>
 
@@ -31,10 +32,17 @@ public:
   {
     data.insert(data.end(), softbits.begin(), softbits.end());
   }
-  void on_end_softbits() override { ended = true; }
+  void on_end_softbits() override
+  {
+    ended = true;
+    if (on_end) {
+      on_end();
+    }
+  }
 
   std::vector<log_likelihood_ratio> data, scratch;
   bool                              ended = false;
+  std::function<void()>             on_end;
 };
 
 modulation_scheme mod_from_qm(int qm)
@@ -58,6 +66,13 @@ int copy_out(const collecting_decoder_buffer& b, int8_t* out, int cap)
 } // namespace
 
 extern "C" {
+
+int ref_ulsch_demux_ex(int qm, int nof_layers, int nof_prb, int start_symbol, int nof_symbols, unsigned dmrs_symbol_mask,
+                       int dmrs_type2, int nof_cdm_groups_without_data, int nof_harq_ack_rvd, int nof_harq_ack_bits,
+                       int nof_enc_harq_ack_bits, int nof_csi_part1_bits, int nof_enc_csi_part1_bits,
+                       int nof_csi_part2_bits, int nof_enc_csi_part2_bits, unsigned c_init, const int8_t* llrs,
+                       int nof_llrs, int block_size, int8_t* sch, int8_t* harq, int8_t* csi1, int8_t* csi2, int cap,
+                       int* counts, int csi2_after_csi1);
 
 /// Demultiplexes one PUSCH codeword of nof_llrs descrambled LLRs (c_init: its scrambling sequence) fed in blocks of
 /// at most block_size soft bits. counts[4] returns the soft bits each buffer received (SCH, HARQ-ACK, CSI Part 1, CSI
@@ -88,6 +103,42 @@ int ref_ulsch_demux(int           qm,
                     int           cap,
                     int*          counts)
 {
+  return ref_ulsch_demux_ex(qm, nof_layers, nof_prb, start_symbol, nof_symbols, dmrs_symbol_mask, dmrs_type2,
+                            nof_cdm_groups_without_data, nof_harq_ack_rvd, nof_harq_ack_bits, nof_enc_harq_ack_bits,
+                            nof_csi_part1_bits, nof_enc_csi_part1_bits, nof_csi_part2_bits, nof_enc_csi_part2_bits, c_init,
+                            llrs, nof_llrs, block_size, sch, harq, csi1, csi2, cap, counts, 0);
+}
+
+/// As ref_ulsch_demux; csi2_after_csi1 != 0: set_csi_part2 is called when the CSI Part 1 buffer ends, as the
+/// reference's PUSCH processor does once CSI Part 1 is decoded (pusch_processor_impl.cpp:72-100), instead of before the
+/// first symbol.
+int ref_ulsch_demux_ex(int           qm,
+                       int           nof_layers,
+                       int           nof_prb,
+                       int           start_symbol,
+                       int           nof_symbols,
+                       unsigned      dmrs_symbol_mask,
+                       int           dmrs_type2,
+                       int           nof_cdm_groups_without_data,
+                       int           nof_harq_ack_rvd,
+                       int           nof_harq_ack_bits,
+                       int           nof_enc_harq_ack_bits,
+                       int           nof_csi_part1_bits,
+                       int           nof_enc_csi_part1_bits,
+                       int           nof_csi_part2_bits,
+                       int           nof_enc_csi_part2_bits,
+                       unsigned      c_init,
+                       const int8_t* llrs,
+                       int           nof_llrs,
+                       int           block_size,
+                       int8_t*       sch,
+                       int8_t*       harq,
+                       int8_t*       csi1,
+                       int8_t*       csi2,
+                       int           cap,
+                       int*          counts,
+                       int           csi2_after_csi1)
+{
   ulsch_demultiplex::configuration cfg;
   cfg.modulation         = mod_from_qm(qm);
   cfg.nof_layers         = nof_layers;
@@ -112,7 +163,11 @@ int ref_ulsch_demux(int           qm,
   auto                   demux = std::make_unique<ulsch_demultiplex_impl>();
   pusch_codeword_buffer& cw    = demux->demultiplex(b_sch, b_harq, b_csi1, cfg);
   if (nof_enc_csi_part2_bits > 0) {
-    demux->set_csi_part2(b_csi2, nof_csi_part2_bits, nof_enc_csi_part2_bits);
+    if (csi2_after_csi1 != 0) {
+      b_csi1.on_end = [&] { demux->set_csi_part2(b_csi2, nof_csi_part2_bits, nof_enc_csi_part2_bits); };
+    } else {
+      demux->set_csi_part2(b_csi2, nof_csi_part2_bits, nof_enc_csi_part2_bits);
+    }
   }
 
   pseudo_random_generator_impl prg;

@@ -26,12 +26,13 @@ def _select(avail, d, count):
     return [int(i) for i in avail[::d][:count]]
 
 
-def symbol_plan(cfg, csi2_enc_bits=0):
+def symbol_plan(cfg, csi2_enc_bits=0, csi2_first_symbol=0):
     """Per allocated OFDM symbol: (symbol, M REs, dict of RE index lists: rvd, harq, csi1, csi2, ulsch).
 
     cfg: qm, nof_layers, nof_prb, start_symbol, nof_symbols, dmrs_symbol_mask, dmrs_type2, nof_cdm_groups_without_data,
     nof_harq_ack_rvd, nof_harq_ack_bits, nof_enc_harq_ack_bits, nof_csi_part1_bits, nof_enc_csi_part1_bits
-    (ulsch_demultiplex::configuration); csi2_enc_bits: G^CSI-2 (set_csi_part2 before the first symbol)."""
+    (ulsch_demultiplex::configuration); csi2_enc_bits: G^CSI-2, placed from symbol csi2_first_symbol on (where
+    set_csi_part2 is called, ulsch_demultiplex_impl.cpp:241; 0: before the first symbol)."""
     lq = cfg["qm"] * cfg["nof_layers"]
     mask = cfg["dmrs_symbol_mask"]
     dm = [(mask >> l) & 1 for l in range(14)]
@@ -77,7 +78,7 @@ def symbol_plan(cfg, csi2_enc_bits=0):
         # Step 3bis: CSI Part 2.
         M_uci = int(uci.sum())
         rem_csi2 = (csi2_enc_bits - m_csi2) // lq
-        if l >= l1_csi and M_uci > 0 and rem_csi2 > 0:
+        if l >= l1_csi and l >= csi2_first_symbol and M_uci > 0 and rem_csi2 > 0:
             d, n = (M_uci // rem_csi2, rem_csi2) if rem_csi2 < M_uci else (1, M_uci)
             sets["csi2"] = _select(np.flatnonzero(uci), d, n)
             ulsch[sets["csi2"]] = False
@@ -106,15 +107,25 @@ def _placeholder(re_llr, seq_bits, qm, nbits):
     return v.astype(np.int8)
 
 
-def demultiplex(cfg, llrs, c_init, csi2_bits=0, csi2_enc_bits=0):
+def csi1_end_symbol(cfg):
+    """The OFDM symbol whose demultiplexing completes CSI Part 1 (where the reference's PUSCH processor decodes it and
+    calls set_csi_part2, pusch_processor_impl.cpp:72-100); None without CSI Part 1."""
+    last = None
+    for l, _M, sets in symbol_plan(cfg):
+        if sets["csi1"]:
+            last = l
+    return last
+
+
+def demultiplex(cfg, llrs, c_init, csi2_bits=0, csi2_enc_bits=0, csi2_first_symbol=0):
     """Routes the descrambled codeword LLRs (int8, demodulation order) of one transmission. Returns dict of int8 arrays:
-    sch, harq, csi1, csi2 (the LLRs each decoder buffer receives, in order)."""
+    sch, harq, csi1, csi2 (the LLRs each decoder buffer receives, in order). csi2_first_symbol: see symbol_plan."""
     qm, lq = cfg["qm"], cfg["qm"] * cfg["nof_layers"]
     seq = D.gold_sequence(c_init, llrs.size)
     out = dict(sch=[], harq=[], csi1=[], csi2=[])
     nbits = dict(harq=cfg["nof_harq_ack_bits"], csi1=cfg["nof_csi_part1_bits"], csi2=csi2_bits)
     pos = 0
-    for _l, M, sets in symbol_plan(cfg, csi2_enc_bits):
+    for _l, M, sets in symbol_plan(cfg, csi2_enc_bits, csi2_first_symbol):
         data = llrs[pos: pos + M * lq].astype(np.int8).copy().reshape(M, lq)
         sb = seq[pos: pos + M * lq].reshape(M, lq)
         for kind in ("harq", "csi1", "csi2"):

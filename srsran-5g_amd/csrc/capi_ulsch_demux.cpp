@@ -145,7 +145,7 @@ int srsgpu_ulsch_demux_plan_create(srsgpu_context*                  ctx,
       // Step 3bis: CSI Part 2.
       M_uci                   = static_cast<uint32_t>(indices(uci).size());
       const uint32_t rem_csi2 = (c.nof_enc_csi_part2_bits - std::min(m_csi2, c.nof_enc_csi_part2_bits)) / lq;
-      if (l >= l1_csi && M_uci > 0 && rem_csi2 > 0) {
+      if (l >= l1_csi && l >= c.csi2_first_symbol && M_uci > 0 && rem_csi2 > 0) {
         pick(M_uci, rem_csi2, dd, nn);
         csi2 = re_select(indices(uci), dd, nn);
         for (uint32_t i : csi2) {

@@ -235,7 +235,7 @@ class UlschDemuxConfig(ctypes.Structure):
         ("nof_cdm_groups_without_data", ctypes.c_uint8),
         ("rnti", ctypes.c_uint16),
         ("n_id", ctypes.c_uint16),
-        ("pad", ctypes.c_uint16),
+        ("csi2_first_symbol", ctypes.c_uint16),
         ("nof_harq_ack_rvd", ctypes.c_uint32),
         ("nof_harq_ack_bits", ctypes.c_uint32),
         ("nof_enc_harq_ack_bits", ctypes.c_uint32),
@@ -1306,6 +1306,7 @@ class UlschDemultiplexing:
     nof_enc_csi_part1_bits: int = 0
     nof_csi_part2_bits: int = 0
     nof_enc_csi_part2_bits: int = 0
+    csi2_first_symbol: int = 0  # CSI Part 2 from this symbol on (the processor's set_csi_part2 point; 0: from the start)
 
 
 class UlschDemuxPlan:

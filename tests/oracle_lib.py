@@ -225,22 +225,24 @@ class Reference(_Lib):
               int(mmse), _ptr(g), _ptr(h), _ptr(nv), _ptr(out), cap, _ptr(stats))
         return out[:n], stats
 
-    def ulsch_demux(self, cfg, llrs, c_init, csi2_bits=0, csi2_enc_bits=0, block_size=1 << 20):
-        """ulsch_demultiplex_impl fed the codeword in blocks: dict sch / harq / csi1 / csi2 of int8 LLRs."""
+    def ulsch_demux(self, cfg, llrs, c_init, csi2_bits=0, csi2_enc_bits=0, block_size=1 << 20, csi2_after_csi1=False):
+        """ulsch_demultiplex_impl fed the codeword in blocks: dict sch / harq / csi1 / csi2 of int8 LLRs.
+        csi2_after_csi1: set_csi_part2 when the CSI Part 1 buffer ends (the PUSCH processor's timing), else before the
+        first symbol."""
         x = np.ascontiguousarray(llrs, dtype=np.int8)
         cap = x.size + 64
         outs = [np.zeros(cap, np.int8) for _ in range(4)]
         counts = np.zeros(4, np.int32)
-        f = self.lib.ref_ulsch_demux
+        f = self.lib.ref_ulsch_demux_ex
         f.restype = ctypes.c_int
         f.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint] + [ctypes.c_int] * 9 + [ctypes.c_uint, _P, ctypes.c_int,
                                                                                    ctypes.c_int] + [_P] * 4 + \
-            [ctypes.c_int, _P]
+            [ctypes.c_int, _P, ctypes.c_int]
         f(cfg["qm"], cfg["nof_layers"], cfg["nof_prb"], cfg["start_symbol"], cfg["nof_symbols"],
           cfg["dmrs_symbol_mask"], cfg["dmrs_type2"], cfg["nof_cdm_groups_without_data"], cfg["nof_harq_ack_rvd"],
           cfg["nof_harq_ack_bits"], cfg["nof_enc_harq_ack_bits"], cfg["nof_csi_part1_bits"],
           cfg["nof_enc_csi_part1_bits"], csi2_bits, csi2_enc_bits, c_init, _ptr(x), x.size, block_size,
-          *[_ptr(o) for o in outs], cap, _ptr(counts))
+          *[_ptr(o) for o in outs], cap, _ptr(counts), int(csi2_after_csi1))
         return {k: o[:n] for k, o, n in zip(("sch", "harq", "csi1", "csi2"), outs, counts)}
 
     def low_papr(self, u, v, m):

@@ -532,3 +532,22 @@ def test_ulsch_demux_oracle_vs_reference(ref, seed):
     for k in ("sch", "harq", "csi1", "csi2"):
         assert np.array_equal(got[k], want[k]), (k, cfg, c2b, c2e)
     assert want["harq"].size == cfg["nof_enc_harq_ack_bits"] and want["csi2"].size == c2e
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_ulsch_demux_csi2_after_csi1_oracle_vs_reference(ref, seed):
+    """CSI Part 2 placed where the reference's PUSCH processor configures it: set_csi_part2 runs when CSI Part 1 has
+    been decoded, i.e. while the symbol completing CSI Part 1 is demultiplexed (pusch_processor_impl.cpp:72-100,
+    ulsch_demultiplex_impl.cpp:241/:450), so CSI Part 2 takes REs of that symbol and the later ones only. The
+    restatement with csi2_first_symbol = the CSI Part 1 end symbol (what the GPU batch's plan is given) equals the
+    reference's demultiplexer driven that way."""
+    import ulsch_demux_oracle as U
+    from ulsch_demux_cases import nof_llrs, random_config
+    rng = np.random.default_rng(4100 + seed)
+    cfg, c2b, c2e, c_init = random_config(rng, csi2_after_csi1=True)
+    llrs = rng.integers(-120, 121, nof_llrs(cfg)).astype(np.int8)
+    want = ref.ulsch_demux(cfg, llrs, c_init, c2b, c2e, block_size=int(rng.integers(7, 500)), csi2_after_csi1=True)
+    got = U.demultiplex(cfg, llrs, c_init, c2b, c2e, csi2_first_symbol=U.csi1_end_symbol(cfg) or 0)
+    for k in ("sch", "harq", "csi1", "csi2"):
+        assert np.array_equal(got[k], want[k]), (k, cfg, c2b, c2e)
+    assert want["csi2"].size == c2e

@@ -44,6 +44,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <set>
@@ -127,6 +128,17 @@ struct pusch_entry {
   unsigned csi1_offset     = 0;
   std::array<uint32_t, 14> harq_ack_counts{};  ///< UCI LLRs per OFDM symbol.
   std::array<uint32_t, 14> csi1_counts{};
+  int      tb_index     = -1;  ///< The TB's index in the launch's decoder plan (-1: decoded in the CSI Part 2 phase).
+  // CSI Part 2 (pusch_processor_impl.cpp:55-101): the UL-SCH bit count depends on CSI Part 1, decoded on the host
+  // during the replay, so the UL-SCH is demultiplexed and decoded by a second, per-PDU launch from there
+  // (pusch_launcher::decode_deferred) with what the first launch left in HBM (the codeword LLRs).
+  bool                               csi2 = false;
+  ulsch_configuration                ulsch_cfg;   ///< UL-SCH information input (CSI Part 2 bits 0)
+  srsgpu_ulsch_demux_config          demux_cfg{}; ///< the first launch's demultiplexing (job-relative offsets)
+  srsgpu_pusch_tb_config             tb_cfg{};    ///< the TB's decoding, CB / TB / LLR / HARQ offsets 0
+  std::vector<srsgpu_harq_copy_job>  copies;      ///< HARQ arena copies (batch offsets from 0)
+  std::vector<uint8_t>               flags;       ///< HARQ context: CB CRC flags
+  std::vector<std::vector<uint8_t>>  msgs;        ///< messages of the CBs that passed before (empty otherwise)
 };
 
 class replay_estimator : public dmrs_pusch_estimator
@@ -156,11 +168,24 @@ public:
   const int8_t*   csi1_llrs       = nullptr;
   const uint32_t* harq_ack_counts = nullptr;
   const uint32_t* csi1_counts     = nullptr;
+  /// CSI Part 2 PDUs: the second launch, given the CSI Part 2 size (0 bits: none) and the symbol it starts at; it
+  /// returns the CSI Part 2 stream and its per-symbol counts and settles the replay decoder's results.
+  std::function<void(unsigned bits, unsigned enc_bits, unsigned first_symbol, const int8_t*& llrs,
+                     const uint32_t*& counts)>
+      second_phase;
 
-  void set_csi_part2(pusch_decoder_buffer& /*buffer*/, unsigned /*bits*/, unsigned /*enc_bits*/) override
+  void set_csi_part2(pusch_decoder_buffer& buffer, unsigned bits, unsigned enc_bits) override
   {
-    // PDUs with CSI Part 2 go to the fallback processor (pusch_slot_batch::batchable).
-    throw std::logic_error("pusch_slot_batch: CSI Part 2 in a batched PDU");
+    // Called by the reference's CSI Part 1 feedback while the symbol completing CSI Part 1 is demultiplexed
+    // (pusch_processor_impl.cpp:72-100): CSI Part 2 occupies REs of that symbol and the later ones.
+    if (!second_phase) {
+      throw std::logic_error("pusch_slot_batch: CSI Part 2 without a second phase");
+    }
+    second_phase(bits, enc_bits, current_symbol, csi2_llrs, csi2_counts);
+    second_done = true;
+    csi_part2   = &buffer;
+    csi2_pos    = 0;
+    csi2_total  = enc_bits;
   }
 
   pusch_codeword_buffer& demultiplex(pusch_decoder_buffer& sch_data_,
@@ -171,16 +196,22 @@ public:
     sch_data  = &sch_data_;
     harq_ack  = config.nof_harq_ack_bits != 0 ? &harq_ack_ : nullptr;
     csi_part1 = config.nof_csi_part1_bits != 0 ? &csi_part1_ : nullptr;
-    harq_pos = csi1_pos = 0;
-    harq_total          = config.nof_enc_harq_ack_bits;
-    csi1_total          = config.nof_enc_csi_part1_bits;
+    csi_part2 = nullptr;
+    harq_pos = csi1_pos = csi2_pos = 0;
+    harq_total                     = config.nof_enc_harq_ack_bits;
+    csi1_total                     = config.nof_enc_csi_part1_bits;
+    second_done                    = false;
     return *this;
   }
 
+  /// The symbol's UCI in the reference's order (ulsch_demultiplex_impl.cpp:474-576): HARQ-ACK, CSI Part 1 (whose end
+  /// may configure CSI Part 2 for this very symbol), CSI Part 2.
   void on_symbol(unsigned l)
   {
+    current_symbol = l;
     feed(harq_ack, harq_ack_llrs, harq_ack_counts, harq_pos, harq_total, l);
     feed(csi_part1, csi1_llrs, csi1_counts, csi1_pos, csi1_total, l);
+    feed(csi_part2, csi2_llrs, csi2_counts, csi2_pos, csi2_total, l);
   }
 
 private:
@@ -214,8 +245,15 @@ private:
   void on_end_codeword() override
   {
     // ulsch_demultiplex_impl::on_end_codeword (:321): every UCI field has ended by now.
-    if (harq_ack != nullptr || csi_part1 != nullptr) {
+    if (harq_ack != nullptr || csi_part1 != nullptr || csi_part2 != nullptr) {
       throw std::logic_error("pusch_slot_batch: UCI field not complete at the end of the codeword");
+    }
+    // A CSI Part 2 PDU whose CSI Part 1 did not configure CSI Part 2 (invalid, or zero CSI Part 2 bits): the UL-SCH
+    // takes the REs CSI Part 2 would have had (the UL-SCH information without CSI Part 2, pusch_processor_impl.cpp:180).
+    if (second_phase && !second_done) {
+      const int8_t*   llrs   = nullptr;
+      const uint32_t* counts = nullptr;
+      second_phase(0, 0, 0, llrs, counts);
     }
     sch_data->on_end_softbits();
     sch_data = nullptr;
@@ -224,7 +262,12 @@ private:
   pusch_decoder_buffer* sch_data  = nullptr;
   pusch_decoder_buffer* harq_ack  = nullptr;
   pusch_decoder_buffer* csi_part1 = nullptr;
-  unsigned              harq_pos = 0, csi1_pos = 0, harq_total = 0, csi1_total = 0;
+  pusch_decoder_buffer* csi_part2 = nullptr;
+  const int8_t*         csi2_llrs   = nullptr;
+  const uint32_t*       csi2_counts = nullptr;
+  unsigned              harq_pos = 0, csi1_pos = 0, csi2_pos = 0, harq_total = 0, csi1_total = 0, csi2_total = 0;
+  unsigned              current_symbol = 0;
+  bool                  second_done    = false;
 };
 
 /// The demodulator stage of the replay: the demodulator's notifications in pusch_demodulator_impl's order
@@ -389,6 +432,7 @@ struct pusch_job {
   unsigned                 P         = 0;
   unsigned                 grid_prb  = 0;
   hipEvent_t               uploaded  = nullptr;
+  const pusch_harq_arena*  harq      = nullptr;  ///< The HARQ arena the layout addresses.
   clock_type::time_point   arrival;
 };
 
@@ -446,6 +490,9 @@ public:
     (void)hipFree(d_ce);
     (void)hipFree(d_harq);
     (void)hipFree(d_llr);
+    (void)hipFree(d_sch_b);
+    (void)hipFree(d_uci_b);
+    (void)hipFree(d_harq_b);
   }
 
   /// Host-clock stamps of a launch (diagnostics).
@@ -478,6 +525,39 @@ public:
 
 private:
   launch_plan* create_plan(const std::vector<std::unique_ptr<pusch_job>>& jobs, unsigned P, unsigned grid_prb);
+
+  /// The second launch of a CSI Part 2 PDU (from the replay, once CSI Part 1 is decoded): the codeword LLRs the first
+  /// launch left in HBM demultiplexed again with the CSI Part 2 size (0: none) from first_symbol on, the UL-SCH decoded
+  /// with the bit count that leaves (pusch_processor_impl.cpp:84-100), the HARQ arena around it; synchronous. Results
+  /// in d_io / d_msgs at d_lay.
+  void decode_deferred(const pusch_entry& e, const pusch_harq_arena& harq, unsigned bits, unsigned enc_bits,
+                       unsigned first_symbol);
+
+  struct deferred_plan {
+    srsgpu_ulsch_demux_plan*   demux = nullptr;
+    srsgpu_pusch_decoder_plan* dec   = nullptr;
+    static void                destroy(deferred_plan* p)
+    {
+      srsgpu_ulsch_demux_plan_destroy(p->demux);
+      srsgpu_pusch_decoder_plan_destroy(p->dec);
+      delete p;
+    }
+  };
+  struct deferred_layout {
+    size_t                   arena_o = 0, flag_o = 0, iter_o = 0, tbok_o = 0, csi2_o = 0, tb_o = 0, end_o = 0;
+    std::array<uint32_t, 14> csi2_counts{};
+  };
+  plan_cache<deferred_plan> deferred_plans{deferred_plan::destroy, 16};
+  staged_buffer             d_io{"pusch_launcher deferred"};
+  staged_buffer             d_msgs{"pusch_launcher deferred"};
+  int8_t*                   d_sch_b     = nullptr;
+  size_t                    d_sch_b_cap = 0;
+  int8_t*                   d_uci_b     = nullptr;
+  size_t                    d_uci_b_cap = 0;
+  int8_t*                   d_harq_b     = nullptr;
+  size_t                    d_harq_b_cap = 0;
+  deferred_layout           d_lay;
+  std::vector<uint8_t>      d_decoded;
 
   template <typename T>
   static void reserve_device(T*& ptr, size_t& cap, size_t bytes, const char* what)
@@ -554,14 +634,14 @@ public:
   std::shared_ptr<pusch_harq_arena> arena;
 
 private:
-  /// PDUs the batch covers: SCH data (with or without HARQ-ACK / CSI Part 1 on PUSCH), identity rx port list, up to
-  /// four layers. CSI Part 2 needs the decoded CSI Part 1 before the UL-SCH bits are known
-  /// (pusch_processor_impl.cpp:60-100), so those PDUs go to the fallback processor.
+  /// PDUs the batch covers: SCH data with or without UCI on PUSCH (HARQ-ACK, CSI Part 1, CSI Part 2: the UL-SCH of a
+  /// CSI Part 2 PDU is decoded in a second launch once the replay has decoded CSI Part 1), identity rx port list, up
+  /// to four layers.
   static bool batchable(const pusch_entry& e)
   {
     const pusch_processor::pdu_t& pdu = e.pdu;
-    if (!pdu.codeword.has_value() || !pdu.uci.csi_part2_size.entries.empty() || pdu.nof_tx_layers == 0 ||
-        pdu.nof_tx_layers > 4 || pdu.rx_ports.empty() || pdu.rx_ports.size() > 4 || pdu.cp != cyclic_prefix::NORMAL) {
+    if (!pdu.codeword.has_value() || pdu.nof_tx_layers == 0 || pdu.nof_tx_layers > 4 || pdu.rx_ports.empty() ||
+        pdu.rx_ports.size() > 4 || pdu.cp != cyclic_prefix::NORMAL) {
       return false;
     }
     for (unsigned p = 0; p != pdu.rx_ports.size(); ++p) {
@@ -927,7 +1007,9 @@ launch_plan* pusch_launcher::create_plan(const std::vector<std::unique_ptr<pusch
       srsgpu_check(srsgpu_ulsch_demux_plan_symbol_llrs(lp->demux, k, 3, lp->csi1_counts[k].data()), WHO);
     }
   }
-  srsgpu_check(srsgpu_pusch_decoder_plan_create(ctx, SRSGPU_LDPC_IMPL_SIMD, tbs.data(), n, &lp->dec), WHO);
+  if (!tbs.empty()) {
+    srsgpu_check(srsgpu_pusch_decoder_plan_create(ctx, SRSGPU_LDPC_IMPL_SIMD, tbs.data(), tbs.size(), &lp->dec), WHO);
+  }
 
   // Staging image: [copy jobs | arena table | CB CRC flags] uploaded, [CB CRC flags | iterations | TB CRC flags | nv |
   // metrics | statistics | UCI streams | TBs] downloaded (the CRC flags are the HARQ context in and the result out).
@@ -1009,10 +1091,12 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
                                            HARQ_SLOT_BYTES, d_harq, io.dev<srsgpu_harq_copy_job>(0),
                                            lp->nof_copies, s),
                    WHO);
-      srsgpu_check(srsgpu_pusch_decoder_plan_execute(lp->dec, d_llr, d_harq, io.dev<uint8_t>(lp->flag_o),
-                                                     msgs.dev<uint8_t>(), io.dev<int32_t>(lp->iter_o),
-                                                     io.dev<uint8_t>(lp->tb_o), io.dev<uint8_t>(lp->tbok_o), s),
-                   WHO);
+      if (lp->dec != nullptr) {
+        srsgpu_check(srsgpu_pusch_decoder_plan_execute(lp->dec, d_llr, d_harq, io.dev<uint8_t>(lp->flag_o),
+                                                       msgs.dev<uint8_t>(), io.dev<int32_t>(lp->iter_o),
+                                                       io.dev<uint8_t>(lp->tb_o), io.dev<uint8_t>(lp->tbok_o), s),
+                     WHO);
+      }
       srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_ARENA, io.dev<int8_t*>(lp->arena_o),
                                            HARQ_SLOT_BYTES, d_harq, io.dev<srsgpu_harq_copy_job>(0),
                                            lp->nof_copies, s),
@@ -1028,7 +1112,7 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
 
   // Absolute offsets of the entries, the copy jobs and the HARQ context (flags; messages of CBs that passed before).
   decoded_flags.assign(lp->cb_total, 0);
-  unsigned tx_b = 0, llr_b = 0, cb_b = 0, tb_b = 0, uci_b = 0, harq_b = 0, dmx_b = 0;
+  unsigned tx_b = 0, llr_b = 0, cb_b = 0, tb_b = 0, uci_b = 0, harq_b = 0, dmx_b = 0, tbi_b = 0;
   auto*    copies   = io.host<srsgpu_harq_copy_job>(0);
   bool     any_msgs = false;
   std::memcpy(io.host(lp->arena_o), lp->arenas.data(), lp->arenas.size() * sizeof(int8_t*));
@@ -1051,6 +1135,9 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
       any_msgs = true;
     }
     for (pusch_entry& e : job->entries) {
+      if (e.tb_index >= 0) {
+        e.tb_index += static_cast<int>(tbi_b);
+      }
       e.tx += tx_b;
       e.llr_offset += llr_b;
       e.sch_offset += llr_b;
@@ -1072,6 +1159,7 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
     uci_b += L.uci_total;
     harq_b += L.harq_total;
     dmx_b += static_cast<unsigned>(L.demuxes.size());
+    tbi_b += static_cast<unsigned>(L.tbs.size());
   }
   tm.filled = clock_type::now();
 
@@ -1090,6 +1178,95 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
   return tm;
 }
 
+void pusch_launcher::decode_deferred(const pusch_entry&      e,
+                                     const pusch_harq_arena& harq,
+                                     unsigned                bits,
+                                     unsigned                enc_bits,
+                                     unsigned                first_symbol)
+{
+  // The UL-SCH information with the CSI Part 2 size (pusch_processor_impl.cpp:84-87).
+  ulsch_configuration uc = e.ulsch_cfg;
+  uc.nof_csi_part2_bits  = units::bits(bits);
+  const ulsch_information info = get_ulsch_information(uc);
+  if (info.nof_csi_part2_bits.value() != enc_bits) {
+    throw std::logic_error(std::string(WHO) + ": CSI Part 2 size differs from the processor's");
+  }
+  const unsigned            nsch = info.nof_ul_sch_bits.value();
+  auto                      a64  = [](size_t x) { return (x + 63) / 64 * 64; };
+  srsgpu_ulsch_demux_config d    = e.demux_cfg;
+  d.llr_offset                   = e.llr_offset;  // the codeword in the first launch's LLR buffer
+  d.nof_csi_part2_bits           = bits;
+  d.nof_enc_csi_part2_bits       = enc_bits;
+  d.csi2_first_symbol            = static_cast<uint16_t>(enc_bits != 0 ? first_symbol : 0);
+  d.sch_offset                   = 0;
+  d.harq_offset                  = 0;
+  d.csi1_offset                  = static_cast<uint32_t>(a64(d.nof_enc_harq_ack_bits));
+  d.csi2_offset                  = 0;
+  srsgpu_pusch_tb_config t       = e.tb_cfg;
+  t.nof_ch_symbols               = nsch / t.modulation_order;
+  t.llr_offset = t.harq_offset = t.cb_offset = t.tb_offset = 0;
+  std::vector<uint8_t> key;
+  key_append(key, d);
+  key_append(key, t);
+  deferred_plan* dp = deferred_plans.get(key, [&] {
+    auto p = std::make_unique<deferred_plan>();
+    srsgpu_check(srsgpu_ulsch_demux_plan_create(ctx, &d, 1, &p->demux), WHO);
+    srsgpu_check(srsgpu_pusch_decoder_plan_create(ctx, SRSGPU_LDPC_IMPL_SIMD, &t, 1, &p->dec), WHO);
+    return p.release();
+  });
+  srsgpu_check(srsgpu_ulsch_demux_plan_symbol_llrs(dp->demux, 0, 4, d_lay.csi2_counts.data()), WHO);
+
+  // [copies | arena table | CB flags] up, [CB flags | iterations | TB flag | CSI Part 2 | TB] down.
+  const unsigned n_cb = static_cast<unsigned>(e.copies.size());
+  d_lay.arena_o       = a64(n_cb * sizeof(srsgpu_harq_copy_job));
+  d_lay.flag_o        = a64(d_lay.arena_o + sizeof(int8_t*));
+  d_lay.iter_o        = a64(d_lay.flag_o + n_cb);
+  d_lay.tbok_o        = a64(d_lay.iter_o + n_cb * sizeof(int32_t));
+  d_lay.csi2_o        = a64(d_lay.tbok_o + 1);
+  d_lay.tb_o          = a64(d_lay.csi2_o + enc_bits);
+  d_lay.end_o         = d_lay.tb_o + std::max<size_t>(e.data.size(), 16);
+  d_io.reserve(d_lay.end_o);
+  d_msgs.reserve(std::max<size_t>(static_cast<size_t>(n_cb) * SRSGPU_CB_MSG_STRIDE, 64));
+  reserve_device(d_sch_b, d_sch_b_cap, std::max<size_t>(nsch, 64), "deferred UL-SCH");
+  reserve_device(d_uci_b, d_uci_b_cap, d.csi1_offset + a64(d.nof_enc_csi_part1_bits) + 64, "deferred UCI");
+  reserve_device(d_harq_b, d_harq_b_cap, std::max<size_t>(static_cast<size_t>(n_cb) * e.cb_N, 16), "deferred HARQ");
+  std::memcpy(d_io.host(0), e.copies.data(), n_cb * sizeof(srsgpu_harq_copy_job));
+  int8_t* arena_base = harq.d_soft;
+  std::memcpy(d_io.host(d_lay.arena_o), &arena_base, sizeof(arena_base));
+  std::memcpy(d_io.host(d_lay.flag_o), e.flags.data(), n_cb);
+  d_decoded.assign(n_cb, 0);
+  bool any_msgs = false;
+  for (unsigned c = 0; c != n_cb; ++c) {
+    d_decoded[c] = e.flags[c] != 0 ? 0 : 1;
+    if (!e.msgs[c].empty()) {
+      std::memcpy(d_msgs.host<uint8_t>(static_cast<size_t>(c) * SRSGPU_CB_MSG_STRIDE), e.msgs[c].data(),
+                  e.msgs[c].size());
+      any_msgs = true;
+    }
+  }
+  hipStream_t s = stream.get();
+  d_io.upload(0, d_lay.iter_o, s);
+  if (any_msgs) {
+    d_msgs.upload(0, static_cast<size_t>(n_cb) * SRSGPU_CB_MSG_STRIDE, s);
+  }
+  srsgpu_check(srsgpu_ulsch_demux_plan_execute(dp->demux, d_llr, d_sch_b, d_uci_b, d_uci_b,
+                                               d_io.dev<int8_t>(d_lay.csi2_o), s),
+               WHO);
+  srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_BATCH, d_io.dev<int8_t*>(d_lay.arena_o), HARQ_SLOT_BYTES,
+                                       d_harq_b, d_io.dev<srsgpu_harq_copy_job>(0), n_cb, s),
+               WHO);
+  srsgpu_check(srsgpu_pusch_decoder_plan_execute(dp->dec, d_sch_b, d_harq_b, d_io.dev<uint8_t>(d_lay.flag_o),
+                                                 d_msgs.dev<uint8_t>(), d_io.dev<int32_t>(d_lay.iter_o),
+                                                 d_io.dev<uint8_t>(d_lay.tb_o), d_io.dev<uint8_t>(d_lay.tbok_o), s),
+               WHO);
+  srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_ARENA, d_io.dev<int8_t*>(d_lay.arena_o), HARQ_SLOT_BYTES,
+                                       d_harq_b, d_io.dev<srsgpu_harq_copy_job>(0), n_cb, s),
+               WHO);
+  d_io.download(d_lay.flag_o, d_lay.end_o - d_lay.flag_o, s);
+  d_msgs.download(0, static_cast<size_t>(n_cb) * SRSGPU_CB_MSG_STRIDE, s);
+  hip_check(hipStreamSynchronize(s), WHO, "synchronise");
+}
+
 void pusch_launcher::wait(const std::vector<std::unique_ptr<pusch_job>>& jobs)
 {
   hip_check(hipEventSynchronize(done), WHO, "synchronise");
@@ -1101,7 +1278,7 @@ void pusch_launcher::wait(const std::vector<std::unique_ptr<pusch_job>>& jobs)
   bool               need_msgs = false;
   for (const auto& job : jobs) {
     for (const pusch_entry& e : job->entries) {
-      if (*io.host<uint8_t>(lp.tbok_o + e.tx) == 0) {
+      if (e.tb_index >= 0 && *io.host<uint8_t>(lp.tbok_o + static_cast<unsigned>(e.tb_index)) == 0) {
         for (unsigned c = 0; c != e.nof_cbs && !need_msgs; ++c) {
           need_msgs = *io.host<uint8_t>(lp.flag_o + e.cb0 + c) != 0;
         }
@@ -1137,10 +1314,27 @@ void pusch_launcher::replay(const std::vector<std::unique_ptr<pusch_job>>& jobs,
       r.dec->tb                = io_host + lp.tb_o + e.tb_offset;
       r.dec->cb_msgs           = msgs_host + static_cast<size_t>(e.cb0) * SRSGPU_CB_MSG_STRIDE;
       r.dec->decoded           = decoded_flags.data() + e.cb0;
-      r.dec->tb_ok             = io_host[lp.tbok_o + i] != 0;
+      r.dec->tb_ok             = e.tb_index >= 0 && io_host[lp.tbok_o + static_cast<unsigned>(e.tb_index)] != 0;
       r.dec->cb_KZ             = e.cb_KZ;
       r.dec->max_iter          = bcfg.nof_ldpc_iterations;
+      if (e.csi2) {
+        r.demux->second_phase = [this, &e, &r, job = job.get()](unsigned bits, unsigned enc_bits, unsigned first,
+                                                                const int8_t*& llrs, const uint32_t*& counts) {
+          decode_deferred(e, *job->harq, bits, enc_bits, first);
+          llrs            = d_io.host<int8_t>(d_lay.csi2_o);
+          counts          = d_lay.csi2_counts.data();
+          r.dec->cb_flags = d_io.host<uint8_t>(d_lay.flag_o);
+          r.dec->cb_iters = d_io.host<int32_t>(d_lay.iter_o);
+          r.dec->tb       = d_io.host<uint8_t>(d_lay.tb_o);
+          r.dec->cb_msgs  = d_msgs.host<uint8_t>();
+          r.dec->decoded  = d_decoded.data();
+          r.dec->tb_ok    = *d_io.host<uint8_t>(d_lay.tbok_o) != 0;
+        };
+      } else {
+        r.demux->second_phase = nullptr;
+      }
       r.proc->process(e.data, std::move(e.rm), *e.notifier, *e.grid, e.pdu);
+      r.demux->second_phase = nullptr;
     }
   }
 }
@@ -1326,6 +1520,7 @@ void pusch_slot_batch::build_layout(pusch_job& job, const pusch_harq_arena& harq
   // rotation of each symbol applied by the demodulator; the LLRs equal the per-symbol layout's bit for bit,
   // tests/test_pusch_chest_gpu.py): the estimator writes 1 / 14 of the words. "interpolate" needs every symbol.
   L.layout = cfg.estimator.td_strategy == SRSGPU_CHEST_TD_AVERAGE ? SRSGPU_CE_COMPACT : SRSGPU_CE_PER_SYMBOL;
+  job.harq = &harq;
   key_append(L.key, L.layout);
   key_append(L.key, job.grid_slot);
   key_append(L.key, harq.d_soft);
@@ -1471,6 +1666,9 @@ void pusch_slot_batch::build_layout(pusch_job& job, const pusch_harq_arena& harq
       L.demuxes.push_back(d);  // sch_offset set once the codeword region's size is known
       e.demux_index = static_cast<int>(L.demuxes.size()) - 1;
       nof_sch_llrs  = info.nof_ul_sch_bits.value();
+      e.csi2        = !pdu.uci.csi_part2_size.entries.empty();
+      e.ulsch_cfg   = uc;
+      e.demux_cfg   = d;
     }
     e.nof_sch_llrs = nof_sch_llrs;
 
@@ -1497,12 +1695,38 @@ void pusch_slot_batch::build_layout(pusch_job& job, const pusch_harq_arena& harq
     t.tbs_bytes        = static_cast<uint32_t>(e.data.size());
     t.nof_ch_symbols   = nof_sch_llrs / dd.qm;
     t.Nref             = ldpc::compute_N_ref(pdu.tbs_lbrm, e.nof_cbs).value();
-    t.llr_offset       = e.llr_offset;
-    t.harq_offset      = e.harq0;
-    t.cb_offset        = e.cb0;
-    t.tb_offset        = e.tb_offset;
-    L.tbs.push_back(t);
     span<const bool> crcs = e.rm->get_codeblocks_crc();
+    if (e.csi2) {
+      // Decoded by the second launch (pusch_launcher::decode_deferred): its own buffers, offsets from 0.
+      e.tb_index = -1;
+      e.tb_cfg   = t;
+      for (unsigned c = 0; c != e.nof_cbs; ++c) {
+        const unsigned id = e.rm->get_absolute_codeblock_id(c);
+        if (id >= harq.max_cb_ids) {
+          throw std::out_of_range(std::string(WHO) + ": absolute codeblock id " + std::to_string(id) +
+                                  " beyond the HARQ arena");
+        }
+        e.copies.push_back({id, c * e.cb_N, e.cb_N, 0});
+        const bool ok = !e.new_data && crcs[c];
+        e.flags.push_back(ok ? 1 : 0);
+        std::vector<uint8_t> msg;
+        if (ok) {
+          const bit_buffer bits = e.rm->get_codeblock_data_bits(c, e.cb_KZ);
+          msg.resize((e.cb_KZ + 7) / 8);
+          for (unsigned b = 0; b != msg.size(); ++b) {
+            msg[b] = bits.get_byte(b);
+          }
+        }
+        e.msgs.push_back(std::move(msg));
+      }
+      continue;
+    }
+    t.llr_offset = e.llr_offset;
+    t.harq_offset = e.harq0;
+    t.cb_offset   = e.cb0;
+    t.tb_offset   = e.tb_offset;
+    e.tb_index    = static_cast<int>(L.tbs.size());
+    L.tbs.push_back(t);
     for (unsigned c = 0; c != e.nof_cbs; ++c) {
       const unsigned id = e.rm->get_absolute_codeblock_id(c);
       if (id >= harq.max_cb_ids) {
@@ -1530,13 +1754,18 @@ void pusch_slot_batch::build_layout(pusch_job& job, const pusch_harq_arena& harq
     if (e.demux_index >= 0) {
       L.demuxes[static_cast<size_t>(e.demux_index)].sch_offset = L.llr_total;
       e.sch_offset                                              = L.llr_total;
-      L.tbs[e.tx].llr_offset                                    = L.llr_total;
+      if (e.tb_index >= 0) {
+        L.tbs[static_cast<size_t>(e.tb_index)].llr_offset = L.llr_total;
+      }
       L.llr_total += (e.nof_sch_llrs + 63) / 64 * 64;
     }
   }
   L.uci_total = uci_total;
   for (const srsgpu_pusch_tb_config& t : L.tbs) {
     key_append(L.key, t);
+  }
+  for (const pusch_entry& e : job.entries) {
+    key_append(L.key, e.tb_index);
   }
   for (const srsgpu_ulsch_demux_config& d : L.demuxes) {
     key_append(L.key, d);

@@ -75,6 +75,7 @@
 #include "srsran/phy/upper/signal_processors/prs/prs_generator.h"
 #include "srsran/srslog/srslog.h"
 
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <exception>
@@ -125,6 +126,8 @@ struct chain_params {
   int32_t tbs_lbrm_bytes;
   int32_t grid_prb;
   int32_t max_iterations;
+  int32_t csi2_size0;        ///< CSI Part 2 bits (0: no CSI Part 2) when bit 0 of CSI Part 1 is 0 (or always, when
+  int32_t csi2_size1;        ///< csi2_size1 == 0) / when it is 1 (uci_part2_size_description, one 1-bit parameter)
 };
 
 symbol_slot_mask symbol_mask(int bits)
@@ -398,6 +401,14 @@ pusch_processor::pdu_t make_pusch_pdu(const chain_params& cc)
   pdu.uci.beta_offset_harq_ack  = 20.0F;
   pdu.uci.beta_offset_csi_part1 = 6.25F;
   pdu.uci.beta_offset_csi_part2 = 6.25F;
+  if (c->csi2_size0 > 0 && c->csi2_size1 <= 0) {
+    pdu.uci.csi_part2_size = uci_part2_size_description(static_cast<unsigned>(c->csi2_size0));
+  } else if (c->csi2_size0 > 0 || c->csi2_size1 > 0) {
+    uci_part2_size_description::entry& entry = pdu.uci.csi_part2_size.entries.emplace_back();
+    entry.parameters.push_back({0, 1});
+    entry.map.push_back(static_cast<uint16_t>(c->csi2_size0));
+    entry.map.push_back(static_cast<uint16_t>(c->csi2_size1));
+  }
   pdu.n_id                      = c->n_id;
   pdu.nof_tx_layers             = c->nof_layers;
   for (unsigned i = 0; i != P; ++i) {
@@ -1127,6 +1138,19 @@ public:
       }
       harq_ack[static_cast<int>(r.rnti)] = {static_cast<int>(r.harq_ack->status), bits};
     }
+    // CSI Part 1 / Part 2: status (-1: not reported) and payload bits (size, first 30 bits LSB first).
+    auto field = [](const std::optional<pusch_uci_field>& f) {
+      std::array<int, 3> v = {-1, 0, 0};
+      if (f.has_value()) {
+        v[0] = static_cast<int>(f->status);
+        v[1] = static_cast<int>(f->payload.size());
+        for (unsigned b = 0; b != f->payload.size() && b < 30; ++b) {
+          v[2] |= f->payload.test(b) ? (1 << b) : 0;
+        }
+      }
+      return v;
+    };
+    csi[static_cast<int>(r.rnti)] = {field(r.csi1), field(r.csi2)};
   }
   void on_new_pusch_results_data(const ul_pusch_results_data& r) override
   {
@@ -1173,6 +1197,7 @@ public:
     std::lock_guard<std::mutex> lock(mtx);
     records.clear();
     harq_ack.clear();
+    csi.clear();
     nof_data = 0;
     crc_ok   = 0;
   }
@@ -1180,6 +1205,7 @@ public:
   std::mutex                         mtx;
   std::vector<ul_record>             records;
   std::map<int, std::pair<int, int>> harq_ack;  ///< RNTI -> (uci_status, payload bits)
+  std::map<int, std::pair<std::array<int, 3>, std::array<int, 3>>> csi;  ///< RNTI -> CSI Part 1, Part 2 fields
   unsigned                           nof_control = 0;
   bool                               count_only  = false;
   std::atomic<unsigned>              nof_data{0};
@@ -1398,7 +1424,7 @@ void chain_ul_destroy(void* p)
 /// One UL slot: the PUSCH PDUs (tb_bytes[i] each) registered in the reference's PDU repository, the received grid
 /// (nof_ports, 14, 12 grid_prb) bf16 pairs written into the processor's grid, then handle_rx_symbol(13). Results in
 /// notification order: ints [rnti, harq, crc_ok, nof_cbs, ldpc_obs, ldpc_min, ldpc_max, harq_ack_status (-1: none),
-/// harq_ack_bits], floats [ldpc_mean, sinr, evm, ta, cfo, epre, rsrp], payload bytes at tb_out + i * tb_stride.
+/// harq_ack_bits, csi1 status / size / bits, csi2 status / size / bits], floats [ldpc_mean, sinr, evm, ta, cfo, epre, rsrp], payload bytes at tb_out + i * tb_stride.
 /// Returns the number of results (< 0 on error).
 int chain_ul_slot(void*               p,
                   unsigned            slot,
@@ -1441,13 +1467,18 @@ int chain_ul_slot(void*               p,
     const auto&                 recs = h->notifier->records;
     for (size_t i = 0; i != recs.size(); ++i) {
       const ul_record& r = recs[i];
-      int*             oi = out_i + 9 * i;
+      int*             oi = out_i + 15 * i;
       float*           of = out_f + 7 * i;
       oi[0] = r.rnti, oi[1] = r.harq_id, oi[2] = r.crc_ok, oi[3] = r.nof_cbs, oi[4] = r.ldpc_obs, oi[5] = r.ldpc_min;
       oi[6] = r.ldpc_max;
       auto ack = h->notifier->harq_ack.find(r.rnti);
       oi[7]    = ack != h->notifier->harq_ack.end() ? ack->second.first : -1;
       oi[8]    = ack != h->notifier->harq_ack.end() ? ack->second.second : 0;
+      auto csi = h->notifier->csi.find(r.rnti);
+      for (int k = 0; k != 6; ++k) {
+        oi[9 + k] = csi == h->notifier->csi.end() ? (k % 3 == 0 ? -1 : 0)
+                                                   : (k < 3 ? csi->second.first[k] : csi->second.second[k - 3]);
+      }
       of[0] = r.ldpc_mean, of[1] = r.sinr, of[2] = r.evm, of[3] = r.ta, of[4] = r.cfo, of[5] = r.epre, of[6] = r.rsrp;
       std::memcpy(tb_out + i * tb_stride, r.payload.data(), std::min<size_t>(r.payload.size(), tb_stride));
     }

@@ -21,14 +21,15 @@ class ChainParams(ctypes.Structure):
                                        "dmrs_mask", "dmrs_type2", "scrambling_id", "n_scid", "cdm_groups", "rb_start",
                                        "nof_rb", "bwp_start", "bwp_size", "start_symbol", "nof_symbols",
                                        "nof_harq_ack", "nof_csi_part1", "dc_position", "tbs_lbrm_bytes", "grid_prb",
-                                       "max_iterations")]
+                                       "max_iterations", "csi2_size0", "csi2_size1")]
 
 
 def params(**kw):
     d = dict(slot=7, rnti=0x4601, n_id=500, qm=8, target_code_rate=948.0, rv=0, base_graph=1, new_data=1, harq_id=0,
              nof_layers=1, nof_ports=4, dmrs_mask=(1 << 2) | (1 << 11), dmrs_type2=0, scrambling_id=500, n_scid=0,
              cdm_groups=2, rb_start=0, nof_rb=25, bwp_start=0, bwp_size=273, start_symbol=0, nof_symbols=14,
-             nof_harq_ack=0, nof_csi_part1=0, dc_position=-1, tbs_lbrm_bytes=200000, grid_prb=273, max_iterations=6)
+             nof_harq_ack=0, nof_csi_part1=0, dc_position=-1, tbs_lbrm_bytes=200000, grid_prb=273, max_iterations=6,
+             csi2_size0=0, csi2_size1=0)
     d.update(kw)
     return ChainParams(**d)
 
@@ -111,7 +112,7 @@ class Chain:
 
 
 UL_INTS = ("rnti", "harq_id", "tb_crc_ok", "nof_cbs", "ldpc_obs", "ldpc_min", "ldpc_max", "harq_ack_status",
-           "harq_ack_bits")
+           "harq_ack_bits", "csi1_status", "csi1_size", "csi1_bits", "csi2_status", "csi2_size", "csi2_bits")
 UL_FLOATS = ("ldpc_mean", "sinr_db", "evm", "ta_s", "cfo_hz", "epre_db", "rsrp_db")
 UL_CPU, UL_GPU_BATCH = 0, 1
 UL_INTERPOLATE, UL_ASYNC = 2, 4  # variant bits: estimator time strategy, asynchronous batch completion

@@ -91,6 +91,8 @@ def check_equal(ref, got, what):
             assert abs(g["cfo_hz"] - r["cfo_hz"]) < 0.05, (w, r["cfo_hz"], g["cfo_hz"])
         assert abs(g["epre_db"] - r["epre_db"]) < 0.01 and abs(g["rsrp_db"] - r["rsrp_db"]) < 0.01, (w, r, g)
         assert (g["harq_ack_status"], g["harq_ack_bits"]) == (r["harq_ack_status"], r["harq_ack_bits"]), (w, r, g)
+        for f in ("csi1_status", "csi1_size", "csi1_bits", "csi2_status", "csi2_size", "csi2_bits"):
+            assert g[f] == r[f], (w, f, r, g)
 
 
 def ul_ues(rng, H, start_rnti, n, harq0, low_snr=()):
@@ -169,6 +171,47 @@ def test_uplink_processor_gpu_batch_equals_reference(procs):
         # The 64QAM retransmission decodes after combining; the 256QAM rate-0.93 one does not (rv 2 carries almost no
         # systematic bits and its first transmission was faded) - on the reference as on the GPU (check_equal above).
         assert sum(ok2[p.rnti] for (p, *_), _ in retx) >= 1, ok2
+    finally:
+        chain.close()
+
+
+def test_uplink_processor_gpu_batch_csi_part2_equals_reference(procs):
+    """UCI with CSI Part 2 on PUSCH (pusch_processor_impl.cpp:55-101): the UL-SCH bit count depends on the decoded CSI
+    Part 1, so the batch decodes the UL-SCH of such a PDU in a second launch from the replay, after the reference's UCI
+    decoder has decoded CSI Part 1 and its feedback has set CSI Part 2 - placed from the symbol completing CSI Part 1
+    on (ulsch_demultiplex_impl.cpp:241). Fixed-size and CSI-Part-1-dependent CSI Part 2 sizes, with and without
+    HARQ-ACK, next to plain UEs; results (TB, CRC, LDPC statistics, HARQ-ACK, CSI Part 1 and Part 2 status, size and
+    bits, CSI) equal the reference's CPU processors."""
+    import chain_harness as H
+    cpu, gpu = procs
+    chain = H.Chain(0)
+    try:
+        rng = np.random.default_rng(606)
+        ues, rb = ul_ues(rng, H, 0x4901, 4, 30)
+        specs = [dict(nof_csi_part1=4, csi2_size0=20), dict(nof_csi_part1=7, csi2_size0=12, csi2_size1=30),
+                 dict(nof_harq_ack=3, nof_csi_part1=11, csi2_size0=8), dict(nof_csi_part1=2, csi2_size0=3),
+                 dict(nof_harq_ack=1, nof_csi_part1=20, csi2_size0=40, csi2_size1=5)]
+        for i, sp in enumerate(specs):
+            nrb = [12, 16, 10, 8, 20][i]
+            p = H.params(rnti=0x4a00 + i, harq_id=40 + i, nof_rb=nrb, rb_start=rb, qm=[4, 6, 2, 4, 6][i],
+                         target_code_rate=[616.0, 772.0, 308.0, 616.0, 772.0][i], nof_ports=P, **sp)
+            rb += nrb
+            ues.append((p, float(rng.uniform(-200, 200)), 0.0, 0.0))
+        tbs, sizes = [], []
+        for p, *_ in ues:
+            seg = grant(p).segmentation()
+            p.base_graph = seg.base_graph
+            tbs.append(rng.integers(0, 256, seg.tbs // 8).astype(np.uint8))
+            sizes.append(seg.tbs // 8)
+        grid = received_grid(rng, chain, ues, tbs, 28.0)
+        pdus = [p for p, *_ in ues]
+        ref = cpu.ul_slot(9, pdus, sizes, grid)
+        got = gpu.ul_slot(9, pdus, sizes, grid)
+        check_equal(ref, got, "slot 9, CSI Part 2")
+        csi2 = [d for d, _ in ref if d["rnti"] >= 0x4a00]
+        assert all(d["csi1_status"] >= 0 for d in csi2), csi2
+        # CSI Part 2 reported whenever CSI Part 1 decoded (the path through the second launch was taken).
+        assert any(d["csi2_status"] >= 0 for d in csi2), csi2
     finally:
         chain.close()
 

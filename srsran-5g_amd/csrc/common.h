@@ -43,6 +43,25 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
 }
 
+/// One DPP step of an OR reduction.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_or(uint32_t v)
+{
+  return v | static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROW_MASK, 0xf, false));
+}
+
+/// OR of v over the 64 lanes (all lanes active), returned to every lane; the steps of wave_xor.
+__device__ __forceinline__ uint32_t wave_or(uint32_t v)
+{
+  v = dpp_or<0xb1>(v);
+  v = dpp_or<0x4e>(v);
+  v = dpp_or<0x141>(v);
+  v = dpp_or<0x140>(v);
+  v = dpp_or<0x142, 0xa>(v);
+  v = dpp_or<0x143, 0xc>(v);
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+
 __device__ __forceinline__ int wave_max(int v)
 {
 #pragma unroll

@@ -804,6 +804,13 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
   __syncthreads();
 
   const int max_iter = d.max_iter;
+#ifdef LDPC_PK_INC_CRC
+  // Incremental CRC (a CRC is linear over GF(2): the remainder of the hard decisions is the XOR of the table entries of
+  // the set bits). Each lane keeps its previous hard decisions of its two positions per systematic column (bit c of
+  // crc_ha / crc_hb) and the XOR of the table entries of its set ones; an iteration XORs in or out only the entries of
+  // the positions that flipped, and a column no lane of the wave flipped costs no load. Bit-exact with the full sum.
+  uint32_t crc_ha = 0, crc_hb = 0, crc_lane = 0;
+#endif
   DEC_STAMP(1);
   DEC_PROF(31, static_cast<uint64_t>(nof_layers));
   for (int it = 0; it < max_iter; ++it) {
@@ -866,6 +873,9 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
 #endif
       uint32_t acc  = 0;
       uint32_t zero = 0;
+#ifdef LDPC_PK_INC_CRC
+      uint32_t fa = 0, fb = 0, inc_ia = 0, inc_zz = 0, inc_hh = 0;
+#endif
       if (active) {
         // Opaque copies again: per-column table offsets would otherwise be hoisted out of the iteration loop. The
         // table loads are unconditional (index clamped, value masked): no divergent branches between them, all of
@@ -880,6 +890,24 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
         const int     hcol = half * KC;
         uint32_t      ia   = zz + static_cast<uint32_t>(hcol) * ZZ;
         const int8_t* scol = soft + hcol * SOFT_COL_STRIDE;
+#ifdef LDPC_PK_INC_CRC
+        uint32_t ha = 0, hb = 0;
+        static_for<KC>([&](auto Ci) {
+          constexpr int c  = decltype(Ci)::value;
+          const int     sa = scol[c * SOFT_COL_STRIDE + 2 * zz];
+          const int     sb = scol[c * SOFT_COL_STRIDE + 2 * zz + 1];
+          zero |= static_cast<uint32_t>(sa == 0) | static_cast<uint32_t>(sb == 0);
+          ha |= (sa <= 0 ? 1u : 0u) << c;
+          hb |= (sb <= 0 ? 1u : 0u) << c;
+        });
+        fa     = ha ^ crc_ha;
+        fb     = hb ^ crc_hb;
+        crc_ha = ha;
+        crc_hb = hb;
+        inc_ia = ia;
+        inc_zz = ZZ;
+        inc_hh = HH;
+#else
         static_for<KC>([&](auto Ci) {
           constexpr int  c  = decltype(Ci)::value;
           const uint32_t ib = ia + HH;
@@ -897,7 +925,39 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
             __builtin_amdgcn_sched_barrier(0);
           }
         });
+#endif
       }
+#ifdef LDPC_PK_INC_CRC
+      // Columns with a flipped decision somewhere in the wave (wave-uniform), four per round: eight table loads in
+      // flight, then the lanes XOR the entries of their flipped positions into their running remainder.
+      uint32_t cols = wave_or(fa | fb);
+      if (active) {
+        while (cols != 0) {
+          uint32_t cc[4];
+          uint32_t ok = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            cc[k] = cols != 0 ? static_cast<uint32_t>(__builtin_ctz(cols)) : cc[0];
+            ok |= (cols != 0 ? 1u : 0u) << k;
+            cols &= cols - 1;
+          }
+          uint32_t ta[4], tb[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t a = inc_ia + cc[k] * inc_zz;
+            ta[k]            = crc_table[a];
+            tb[k]            = crc_table[a + inc_hh];
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const bool v = ((ok >> k) & 1u) != 0;
+            crc_lane ^= (v && ((fa >> cc[k]) & 1u) != 0) ? ta[k] : 0u;
+            crc_lane ^= (v && ((fb >> cc[k]) & 1u) != 0) ? tb[k] : 0u;
+          }
+        }
+        acc = crc_lane;
+      }
+#endif
       acc      = wave_xor(acc);
       zero     = (__ballot(zero != 0) != 0) ? 1u : 0u;
       int* red = scratch + 8 + 16 * (it & 1);

@@ -411,6 +411,21 @@ int srsgpu_ofdm_demodulator_symbols_plan_create(srsgpu_context*           ctx,
                                                 uint32_t                  nof_symbols,
                                                 srsgpu_ofdm_plan**        plan);
 
+/** Sector groups — one launch for the same symbol (or slot) of several sectors sharing a GPU, where the reference runs
+ *  one lower-PHY sector per cell, each with its own OFDM objects (lib/ru/generic/ru_factory_generic_impl.cpp:75-90,
+ *  lib/phy/lower/lower_phy_factory.cpp:70/:84). Concatenates the jobs of `members` (the sectors' plans, each keeping
+ *  its own carrier frequency, scaling and slot/symbol positions) into one plan: member i's grids follow member i-1's
+ *  (srsgpu_ofdm_plan_nof_grid_words words each) and its time samples follow member i-1's; the plan's grid g runs over
+ *  the members' grids in order (srsgpu_ofdm_plan_sample_offset). The members must share direction, DFT size, bandwidth,
+ *  DFT window offset and number of ports (one kernel runs every job). The members stay owned by the caller. */
+int srsgpu_ofdm_plan_concat(srsgpu_context*                ctx,
+                            const srsgpu_ofdm_plan* const* members,
+                            uint32_t                       nof_members,
+                            srsgpu_ofdm_plan**             plan);
+
+/** uint32 words of the plan's grids (grids x ports x symbols x 12 * bw_rb). */
+uint64_t srsgpu_ofdm_plan_nof_grid_words(const srsgpu_ofdm_plan* plan);
+
 /** Total number of complex samples of the plan's time buffer (all grids and ports). */
 uint64_t srsgpu_ofdm_plan_nof_samples(const srsgpu_ofdm_plan* plan);
 

@@ -25,8 +25,11 @@ public:
   staged_buffer& operator=(const staged_buffer&) = delete;
   ~staged_buffer()
   {
-    (void)hipFree(d);
-    (void)hipHostFree(h);
+    if (d != nullptr || h != nullptr) {
+      std::lock_guard<std::recursive_mutex> lock(hip_setup_mutex());  // frees vs another thread's capture
+      (void)hipFree(d);
+      (void)hipHostFree(h);
+    }
   }
 
   /// Makes room for n bytes (contents are not preserved when it grows).

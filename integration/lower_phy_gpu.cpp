@@ -24,6 +24,7 @@
 //    a slot is notified, in order, before the slot's last process_symbol() returns.
 #include "signal_chain_gpu.h"
 
+#include "batch_graph.h"
 #include "gpu_staging.h"
 #include "srsran/gateways/baseband/buffer/baseband_gateway_buffer_reader.h"
 #include "srsran/gateways/baseband/buffer/baseband_gateway_buffer_writer.h"
@@ -39,10 +40,14 @@
 #include "srsran/phy/support/resource_grid_writer.h"
 #include "srsran/phy/support/shared_resource_grid.h"
 
+#include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <deque>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -68,6 +73,15 @@ public:
     request                     old = std::move(e.req);
     e.req                           = std::move(r);
     return old;
+  }
+
+  template <typename F>
+  void for_each(F&& f)
+  {
+    for (entry& e : entries) {
+      std::lock_guard<std::mutex> lock(e.mtx);
+      f(e.req.payload);
+    }
   }
 
 private:
@@ -116,6 +130,391 @@ srsgpu_ofdm_config ofdm_config(subcarrier_spacing scs, cyclic_prefix cp, unsigne
 }
 
 // ---------------------------------------------------------------------------------------------------------------------
+// Sector group
+// ---------------------------------------------------------------------------------------------------------------------
+
+/// One direction of a sector group. A round is the work of every sector at one position (UL: a symbol, key = system
+/// slot x symbols per slot + symbol; DL: a slot, key = system slot), run as one captured graph on the group's stream:
+/// upload of the round's input region (all sectors), the OFDM launch of the sectors' plans concatenated
+/// (srsgpu_ofdm_plan_concat), download of the output region. Rounds sit in a ring of a whole number of periods (a
+/// subframe's symbols or slots), so a ring entry always serves the same position and owns one graph over its own
+/// pinned and device buffers.
+class sector_rounds
+{
+public:
+  using clock = std::chrono::steady_clock;
+
+  sector_rounds(srsgpu_context* ctx_, const char* who_, bool inverse_, unsigned nof_sectors_, unsigned period_,
+                unsigned nof_rounds, std::chrono::microseconds window_) :
+    ctx(ctx_),
+    who(who_),
+    inverse(inverse_),
+    nof_sectors(nof_sectors_),
+    all((nof_sectors_ >= 32) ? ~0u : ((1u << nof_sectors_) - 1)),
+    period(period_),
+    window(window_),
+    stream(ctx_, who_),
+    members(nof_sectors_)
+  {
+    for (unsigned r = 0; r != nof_rounds; ++r) {
+      rounds.emplace_back(std::make_unique<round>(who));
+    }
+    dispatcher = std::thread([this]() { dispatch_loop(); });
+  }
+
+  ~sector_rounds()
+  {
+    {
+      std::lock_guard<std::mutex> lock(mtx);
+      stopping = true;
+    }
+    dispatch_cv.notify_all();
+    dispatcher.join();
+    (void)hipStreamSynchronize(stream.get());
+    std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());
+    for (auto& rd : rounds) {
+      if (rd->graph != nullptr) {
+        (void)hipGraphExecDestroy(rd->graph);
+      }
+      if (rd->done != nullptr) {
+        (void)hipEventDestroy(rd->done);
+      }
+    }
+    rounds.clear();
+    for (srsgpu_ofdm_plan* p : plans) {
+      srsgpu_ofdm_plan_destroy(p);
+    }
+  }
+
+  /// A sector's plans, one per position of the period (kept by the caller while it is registered); returns the
+  /// sector's index, or -1 when every index is taken. The last sector builds the concatenated plans, the rounds'
+  /// buffers and graphs (the caller holds gpu::hip_setup_mutex). Sectors whose plans do not concatenate leave the
+  /// group disabled: every sector then runs alone.
+  int add_sector(const std::vector<srsgpu_ofdm_plan*>& sector_plans)
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    if (registered == nof_sectors || sector_plans.size() != period) {
+      return -1;
+    }
+    const int index     = static_cast<int>(registered++);
+    members[index]      = sector_plans;
+    if (registered == nof_sectors) {
+      build();
+    }
+    return index;
+  }
+
+  /// Deregistration (the sector's plans are going away): rounds no longer wait for it; before the group is built, the
+  /// group stays disabled.
+  void remove_sector(int sector)
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    gone |= 1u << sector;
+    members[sector].clear();
+    const auto now = clock::now();
+    for (auto& rd : rounds) {
+      if (rd->key != UINT64_MAX && !rd->closed) {
+        rd->arrived |= 1u << sector;
+        try_close(*rd, now);
+      }
+    }
+  }
+
+  bool enabled() const { return built; }
+
+  /// Sector `sector` reaches the round of `key`: present (it has work: returns the ring entry it writes its input into
+  /// before calling written()) or absent (no request: returns -1, the round stops waiting for it). -1 also when the
+  /// round launched already or its ring entry is still busy with an older key: the sector runs alone.
+  int join(int sector, uint64_t key, bool present)
+  {
+    if (!built || sector < 0) {
+      return -1;
+    }
+    std::lock_guard<std::mutex> lock(mtx);
+    const unsigned r  = static_cast<unsigned>(key % rounds.size());
+    round&         rd = *rounds[r];
+    if (rd.key != key) {
+      if (rd.consumers != 0 || (rd.arrived != 0 && !rd.closed)) {
+        ++alone;
+        return -1;
+      }
+      rd.key      = key;
+      rd.arrived  = gone;
+      rd.present  = 0;
+      rd.written  = 0;
+      rd.closed   = false;
+      rd.launched = false;
+      rd.first    = clock::now();
+      dispatch_cv.notify_one();
+    }
+    const uint32_t bit = 1u << sector;
+    if (rd.closed || (rd.arrived & bit) != 0) {
+      if (present) {
+        ++alone;
+      }
+      return -1;
+    }
+    rd.arrived |= bit;
+    if (!present) {
+      try_close(rd, clock::now());
+      return -1;
+    }
+    rd.present |= bit;
+    ++rd.consumers;
+    ++grouped;
+    return static_cast<int>(r);
+  }
+
+  uint8_t* input(int r, int sector) { return rounds[r]->in.host(in_off[r % period][sector]); }
+  const uint8_t* output(int r, int sector) { return rounds[r]->out.host(out_off[r % period][sector]); }
+
+  /// The sector's input of round r is in place.
+  void written(int r, int sector)
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    round& rd = *rounds[r];
+    rd.written |= 1u << sector;
+    try_close(rd, clock::now());
+  }
+
+  /// Whether round r's outputs are ready; wait: block until they are.
+  bool ready(int r, bool wait)
+  {
+    round& rd = *rounds[r];
+    {
+      std::unique_lock<std::mutex> lock(mtx);
+      if (!rd.launched) {
+        if (!wait) {
+          return false;
+        }
+        launched_cv.wait(lock, [&rd]() { return rd.launched; });
+      }
+    }
+    if (wait) {
+      gpu::hip_check(hipEventSynchronize(rd.done), who, "sector group round");
+      return true;
+    }
+    return hipEventQuery(rd.done) == hipSuccess;
+  }
+
+  /// A present sector is done with round r's outputs.
+  void release(int r)
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    --rounds[r]->consumers;
+  }
+
+  uint64_t nof_rounds() const { return launches.load(); }
+  uint64_t nof_grouped() const { return grouped.load(); }
+  uint64_t nof_alone() const { return alone.load(); }
+
+private:
+  struct round {
+    explicit round(const char* w) : in(w), out(w) {}
+    uint64_t            key       = UINT64_MAX;
+    uint32_t            arrived   = 0;  ///< sectors that reached the round (present or absent; gone ones count)
+    uint32_t            present   = 0;  ///< sectors with input in the round
+    uint32_t            written   = 0;  ///< present sectors whose input is in place
+    unsigned            consumers = 0;  ///< present sectors that have not released the outputs
+    bool                closed    = false;  ///< no more sectors join (launched, or nothing to launch)
+    bool                launched  = false;
+    clock::time_point   first;
+    gpu::staged_buffer  in;
+    gpu::staged_buffer  out;
+    hipEvent_t          done  = nullptr;
+    hipGraphExec_t      graph = nullptr;
+  };
+
+  /// Launches (or, with nobody present, retires) a round once every sector arrived or its window ran out, and every
+  /// present sector's input is in place. Holds mtx.
+  void try_close(round& rd, clock::time_point now)
+  {
+    if (rd.closed || rd.written != rd.present || (rd.arrived != all && now - rd.first < window)) {
+      return;
+    }
+    rd.closed = true;
+    if (rd.present == 0) {
+      return;
+    }
+    gpu::device_scope dev(ctx, who);
+    gpu::hip_check(hipGraphLaunch(rd.graph, stream.get()), who, "graph launch");
+    gpu::hip_check(hipEventRecord(rd.done, stream.get()), who, "event");
+    rd.launched = true;
+    ++launches;
+    launched_cv.notify_all();
+  }
+
+  void dispatch_loop()
+  {
+    std::unique_lock<std::mutex> lock(mtx);
+    while (!stopping) {
+      clock::time_point next = clock::time_point::max();
+      const auto        now  = clock::now();
+      for (auto& rd : rounds) {
+        if (rd->arrived == 0 || rd->closed || rd->key == UINT64_MAX) {
+          continue;
+        }
+        try_close(*rd, now);
+        if (!rd->closed) {
+          // waiting for its window, or (window over) for a sector still copying its input
+          next = std::min(next, rd->first + window > now ? rd->first + window : now + std::chrono::microseconds(20));
+        }
+      }
+      if (next == clock::time_point::max()) {
+        dispatch_cv.wait(lock);
+      } else {
+        dispatch_cv.wait_until(lock, next);
+      }
+    }
+  }
+
+  /// Concatenated plans, per-sector offsets, round buffers and graphs. Holds mtx (and gpu::hip_setup_mutex).
+  void build()
+  {
+    gpu::device_scope dev(ctx, who);
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      if (members[k].size() != period) {
+        return;  // a sector left before the group was complete
+      }
+    }
+    std::vector<srsgpu_ofdm_plan*> cat(period, nullptr);
+    for (unsigned pos = 0; pos != period; ++pos) {
+      std::vector<const srsgpu_ofdm_plan*> m;
+      for (unsigned k = 0; k != nof_sectors; ++k) {
+        m.push_back(members[k][pos]);
+      }
+      if (srsgpu_ofdm_plan_concat(ctx, m.data(), nof_sectors, &cat[pos]) != SRSGPU_OK) {
+        for (srsgpu_ofdm_plan* p : cat) {
+          srsgpu_ofdm_plan_destroy(p);
+        }
+        return;  // sectors differ in what one launch shares: no group
+      }
+    }
+    plans = cat;
+    in_off.assign(period, std::vector<size_t>(nof_sectors));
+    out_off.assign(period, std::vector<size_t>(nof_sectors));
+    std::vector<size_t> in_bytes(period), out_bytes(period);
+    for (unsigned pos = 0; pos != period; ++pos) {
+      const size_t words = srsgpu_ofdm_plan_nof_grid_words(plans[pos]) / nof_sectors;  // equal per sector
+      for (unsigned k = 0; k != nof_sectors; ++k) {
+        const size_t samples = srsgpu_ofdm_plan_sample_offset(plans[pos], k, 0) * sizeof(cf_t);
+        in_off[pos][k]       = inverse ? k * words * sizeof(uint32_t) : samples;
+        out_off[pos][k]      = inverse ? samples : k * words * sizeof(uint32_t);
+      }
+      const size_t grid_bytes   = srsgpu_ofdm_plan_nof_grid_words(plans[pos]) * sizeof(uint32_t);
+      const size_t sample_bytes = srsgpu_ofdm_plan_nof_samples(plans[pos]) * sizeof(cf_t);
+      in_bytes[pos]             = inverse ? grid_bytes : sample_bytes;
+      out_bytes[pos]            = inverse ? sample_bytes : grid_bytes;
+    }
+    hipStream_t hs = stream.get();
+    for (unsigned r = 0; r != rounds.size(); ++r) {
+      round&         rd  = *rounds[r];
+      const unsigned pos = r % period;
+      rd.in.reserve(in_bytes[pos]);
+      rd.out.reserve(out_bytes[pos]);
+      gpu::hip_check(hipEventCreateWithFlags(&rd.done, hipEventDisableTiming), who, "event");
+      rd.graph = gpu::capture_graph(hs, who, [&]() {
+        rd.in.upload(0, in_bytes[pos], hs);
+        if (inverse) {
+          gpu::srsgpu_check(srsgpu_ofdm_modulator_plan_execute(plans[pos], rd.in.dev<uint32_t>(), rd.out.dev<float>(),
+                                                               hs),
+                            who);
+        } else {
+          gpu::srsgpu_check(srsgpu_ofdm_demodulator_plan_execute(plans[pos], rd.in.dev<float>(),
+                                                                 rd.out.dev<uint32_t>(), hs),
+                            who);
+        }
+        rd.out.download(0, out_bytes[pos], hs);
+      });
+    }
+    built = true;
+  }
+
+  srsgpu_context*                              ctx;
+  const char*                                  who;
+  bool                                         inverse;
+  unsigned                                     nof_sectors;
+  uint32_t                                     all;
+  unsigned                                     period;
+  std::chrono::microseconds                    window;
+  gpu::owned_stream                            stream;
+  std::vector<std::vector<srsgpu_ofdm_plan*>>  members;
+  std::vector<srsgpu_ofdm_plan*>               plans;    ///< per position: every sector's plan concatenated
+  std::vector<std::vector<size_t>>             in_off;   ///< per position and sector: byte offset of its input
+  std::vector<std::vector<size_t>>             out_off;  ///< ... and of its output
+  std::vector<std::unique_ptr<round>>          rounds;
+  unsigned                                     registered = 0;
+  uint32_t                                     gone       = 0;
+  std::atomic<bool>                            built      = false;
+  bool                                         stopping   = false;
+  std::atomic<uint64_t>                        launches   = 0;
+  std::atomic<uint64_t>                        grouped    = 0;
+  std::atomic<uint64_t>                        alone      = 0;
+  std::mutex                                   mtx;
+  std::condition_variable                      launched_cv;
+  std::condition_variable                      dispatch_cv;
+  std::thread                                  dispatcher;
+};
+
+} // namespace
+
+/// The group: one sector_rounds per direction, made by the first processor of that direction (its geometry sets the
+/// period: the subframe's symbols for UL, its slots for DL).
+class lower_phy_sector_group
+{
+public:
+  explicit lower_phy_sector_group(const lower_phy_group_configuration& cfg_) :
+    cfg(cfg_), owner(gpu::shared_context(cfg_.device))
+  {
+    if (cfg.nof_sectors == 0 || cfg.nof_sectors > 32) {
+      throw std::invalid_argument("lower_phy_sector_group: 1 to 32 sectors");
+    }
+  }
+
+  sector_rounds& rounds(bool downlink, unsigned period)
+  {
+    std::lock_guard<std::mutex> lock(mtx);
+    std::unique_ptr<sector_rounds>& r = downlink ? dl : ul;
+    if (!r) {
+      // A whole number of periods (one graph per ring entry): at least 8 slots of DL (requests run a few slots ahead
+      // of the slot being transmitted) and 4 slots of UL symbols (a sector holds at most a slot's symbols).
+      const unsigned n = downlink ? period * std::max(1u, 8u / period) : period * std::max(2u, 56u / period);
+      r = std::make_unique<sector_rounds>(owner.get(), downlink ? "pdxch_sector_group" : "puxch_sector_group",
+                                          downlink, cfg.nof_sectors, period, n,
+                                          std::chrono::microseconds(downlink ? cfg.dl_window_us : cfg.ul_window_us));
+    }
+    return *r;
+  }
+
+  lower_phy_group_counters counters() const
+  {
+    lower_phy_group_counters c;
+    std::lock_guard<std::mutex> lock(mtx);
+    if (ul) {
+      c.ul_rounds  = ul->nof_rounds();
+      c.ul_grouped = ul->nof_grouped();
+      c.ul_alone   = ul->nof_alone();
+    }
+    if (dl) {
+      c.dl_rounds  = dl->nof_rounds();
+      c.dl_grouped = dl->nof_grouped();
+      c.dl_alone   = dl->nof_alone();
+    }
+    return c;
+  }
+
+  const lower_phy_group_configuration cfg;
+  std::shared_ptr<srsgpu_context>      owner;
+
+private:
+  mutable std::mutex             mtx;
+  std::unique_ptr<sector_rounds> ul;
+  std::unique_ptr<sector_rounds> dl;
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------------------------------
 // PDxCH
 // ---------------------------------------------------------------------------------------------------------------------
 
@@ -153,11 +552,16 @@ class pdxch_processor_gpu : public pdxch_processor,
     std::vector<bool>  port_empty;
     unsigned           subframe_slot = 0;
     bool               launched      = false;  ///< false: the request's grid was empty (nothing to transmit).
+    bool               own           = false;  ///< launched on this job's own buffers (done is recorded)
+    int                round         = -1;     ///< launched in the sector group's round (its outputs hold the slot)
   };
   using job_ptr = std::unique_ptr<job>;
 
 public:
-  pdxch_processor_gpu(std::shared_ptr<srsgpu_context> owner_, const pdxch_processor_configuration& config) :
+  pdxch_processor_gpu(std::shared_ptr<srsgpu_context>         owner_,
+                      const pdxch_processor_configuration&    config,
+                      std::shared_ptr<lower_phy_sector_group> group_) :
+    group_owner(std::move(group_)),
     owner(std::move(owner_)),
     ctx(owner.get()),
     stream(ctx, WHO),
@@ -165,7 +569,8 @@ public:
     nof_ports(config.nof_tx_ports),
     nsc(config.bandwidth_rb * NRE)
   {
-    gpu::device_scope dev(ctx, WHO);
+    gpu::device_scope                     dev(ctx, WHO);
+    std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());  // plan allocations vs other sectors' captures
     // pdxch_processor_factory_sw: modulator scaling 1 (pdxch_processor_factories.cpp:59).
     const srsgpu_ofdm_config c = ofdm_config(config.scs, config.cp, config.bandwidth_rb,
                                              config.srate.get_dft_size(config.scs), 0, 1.0F, config.center_freq_Hz);
@@ -174,11 +579,22 @@ public:
       gpu::srsgpu_check(srsgpu_ofdm_modulator_plan_create(ctx, &c, 1, nof_ports, &s, &p), WHO);
       plans.push_back(p);
     }
+    if (group_owner) {
+      group  = &group_owner->rounds(true, geo.nslot);
+      sector = group->add_sector(plans);
+    }
   }
 
   ~pdxch_processor_gpu() override
   {
+    recycle(std::move(current));
+    requests.for_each([this](job_ptr& j) { recycle(std::move(j)); });
+    if (sector >= 0) {
+      group->remove_sector(sector);
+    }
     (void)hipStreamSynchronize(stream.get());
+    std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());
+    free_jobs.clear();
     for (srsgpu_ofdm_plan* p : plans) {
       srsgpu_ofdm_plan_destroy(p);
     }
@@ -214,7 +630,11 @@ private:
       }
       current = std::move(r.payload);
       gpu::device_scope dev(ctx, WHO);
-      gpu::hip_check(hipEventSynchronize(current->done), WHO, "modulation");
+      if (current->round >= 0) {
+        group->ready(current->round, true);
+      } else {
+        gpu::hip_check(hipEventSynchronize(current->done), WHO, "modulation");
+      }
     }
     if (!current) {
       return false;
@@ -222,13 +642,15 @@ private:
     const unsigned s     = context.slot.subframe_slot_index() * geo.nsymb + context.symbol;
     const unsigned n     = geo.size[s];
     const size_t   slotn = geo.slot_size(current->subframe_slot);
+    const auto*    slot_samples =
+        reinterpret_cast<const cf_t*>(current->round >= 0 ? group->output(current->round, sector) : current->samples.host());
     for (unsigned p = 0; p != nof_ports; ++p) {
       span<cf_t> out = samples.get_channel_buffer(p);
       srsran_assert(out.size() == n, "The output buffer size ({}) does not match the symbol size ({}).", out.size(), n);
       if (current->port_empty[p]) {
         std::fill(out.begin(), out.end(), cf_t());  // ofdm_modulator_impl.cpp:77: an empty port transmits zeros
       } else {
-        std::memcpy(out.data(), current->samples.host<cf_t>((p * slotn + geo.start[s]) * sizeof(cf_t)), n * sizeof(cf_t));
+        std::memcpy(out.data(), slot_samples + p * slotn + geo.start[s], n * sizeof(cf_t));
       }
     }
     return true;
@@ -243,7 +665,15 @@ private:
     job_ptr j = acquire();
     j->launched = false;
     const resource_grid_reader& reader = grid.get_reader();
-    if (!reader.is_empty()) {
+    const bool                  empty  = reader.is_empty();
+    const int r = sector >= 0 ? group->join(sector, context.slot.system_slot(), !empty) : -1;
+    if (r >= 0) {
+      stage_grid(*j, reader, group->input(r, sector));
+      group->written(r, sector);
+      j->round         = r;
+      j->subframe_slot = context.slot.subframe_slot_index();
+      j->launched      = true;
+    } else if (!empty) {
       launch(*j, reader, context.slot.subframe_slot_index());
     }
     auto old = requests.exchange({context.slot, std::move(j)});
@@ -267,18 +697,10 @@ private:
     j.grid.reserve(nof_ports * geo.nsymb * row);
     j.samples.reserve(nof_ports * slotn * sizeof(cf_t));
     if (j.done == nullptr) {
+      std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());
       gpu::hip_check(hipEventCreateWithFlags(&j.done, hipEventDisableTiming), WHO, "event");
     }
-    j.port_empty.assign(nof_ports, false);
-    for (unsigned p = 0; p != nof_ports; ++p) {
-      j.port_empty[p] = reader.is_empty(p);
-      if (j.port_empty[p]) {
-        continue;  // its rows stay stale on the device; the port's output is zeros
-      }
-      for (unsigned l = 0; l != geo.nsymb; ++l) {
-        std::memcpy(j.grid.host((p * geo.nsymb + l) * row), reader.get_view(p, l).data(), row);
-      }
-    }
+    stage_grid(j, reader, j.grid.host());
     // Upload, modulation and download as one captured graph per (job, slot of the subframe), built on first use.
     if (j.graph_buffers[0] != j.grid.dev() || j.graph_buffers[1] != j.samples.dev()) {
       j.drop_graphs();  // the job's buffers grew: the graphs captured their old addresses
@@ -311,6 +733,23 @@ private:
     gpu::hip_check(hipEventRecord(j.done, s), WHO, "event");
     j.subframe_slot = subframe_slot;
     j.launched      = true;
+    j.own           = true;
+  }
+
+  /// The grid rows of every non-empty port into `dst` ([port][symbol][subcarrier] uint32), the empty ports noted.
+  void stage_grid(job& j, const resource_grid_reader& reader, uint8_t* dst)
+  {
+    const size_t row = static_cast<size_t>(nsc) * sizeof(uint32_t);
+    j.port_empty.assign(nof_ports, false);
+    for (unsigned p = 0; p != nof_ports; ++p) {
+      j.port_empty[p] = reader.is_empty(p);
+      if (j.port_empty[p]) {
+        continue;  // its rows stay stale on the device; the port's output is zeros
+      }
+      for (unsigned l = 0; l != geo.nsymb; ++l) {
+        std::memcpy(dst + (p * geo.nsymb + l) * row, reader.get_view(p, l).data(), row);
+      }
+    }
   }
 
   /// A job from the free list (its previous transfers finished before its buffers are rewritten) or a new one.
@@ -327,9 +766,10 @@ private:
     if (!j) {
       return std::make_unique<job>(WHO);
     }
-    if (j->launched) {
+    if (j->own) {
       gpu::device_scope dev(ctx, WHO);
       gpu::hip_check(hipEventSynchronize(j->done), WHO, "job reuse");
+      j->own = false;
     }
     return j;
   }
@@ -337,11 +777,18 @@ private:
   void recycle(job_ptr j)
   {
     if (j) {
+      if (j->round >= 0) {
+        group->release(j->round);
+        j->round = -1;
+      }
       std::lock_guard<std::mutex> lock(free_mtx);
       free_jobs.push_back(std::move(j));
     }
   }
 
+  std::shared_ptr<lower_phy_sector_group> group_owner;
+  sector_rounds*                  group  = nullptr;
+  int                             sector = -1;  ///< index in the group, -1: not grouped
   std::shared_ptr<srsgpu_context> owner;
   srsgpu_context*                 ctx;
   gpu::owned_stream               stream;
@@ -384,9 +831,11 @@ class puxch_processor_gpu : public puxch_processor,
   };
 
 public:
-  puxch_processor_gpu(std::shared_ptr<srsgpu_context> owner_,
-                      const puxch_processor_configuration& config,
-                      unsigned                             max_symbols_in_flight_) :
+  puxch_processor_gpu(std::shared_ptr<srsgpu_context>         owner_,
+                      const puxch_processor_configuration&    config,
+                      unsigned                                max_symbols_in_flight_,
+                      std::shared_ptr<lower_phy_sector_group> group_) :
+    group_owner(std::move(group_)),
     owner(std::move(owner_)),
     ctx(owner.get()),
     stream(ctx, WHO),
@@ -395,8 +844,9 @@ public:
     nsc(config.bandwidth_rb * NRE),
     max_symbols_in_flight(max_symbols_in_flight_)
   {
-    gpu::device_scope dev(ctx, WHO);
-    const unsigned    N = config.srate.get_dft_size(config.scs);
+    gpu::device_scope                     dev(ctx, WHO);
+    std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());  // plan allocations vs other sectors' captures
+    const unsigned                        N = config.srate.get_dft_size(config.scs);
     // puxch_processor_factory_sw (puxch_processor_factories.cpp:41-57): DFT window offset as a fraction of the CP of
     // symbol 1, scaling 1 / sqrt(subcarriers).
     const unsigned window_offset = static_cast<unsigned>(
@@ -423,11 +873,25 @@ public:
       stages.back()->out.reserve(static_cast<size_t>(nof_ports) * nsc * sizeof(uint32_t));
       gpu::hip_check(hipEventCreateWithFlags(&stages.back()->done, hipEventDisableTiming), WHO, "event");
     }
+    if (group_owner) {
+      group  = &group_owner->rounds(false, geo.nslot * geo.nsymb);
+      sector = group->add_sector(plans);
+    }
   }
 
   ~puxch_processor_gpu() override
   {
+    for (const pending_symbol& ps : pending) {
+      if (ps.round >= 0) {
+        group->release(ps.round);
+      }
+    }
+    if (sector >= 0) {
+      group->remove_sector(sector);
+    }
     (void)hipStreamSynchronize(stream.get());
+    std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());
+    stages.clear();
     for (hipGraphExec_t g : graphs) {
       if (g != nullptr) {
         (void)hipGraphExecDestroy(g);
@@ -464,14 +928,37 @@ private:
         current_grid = std::move(r.payload);
       }
     }
+    const unsigned l   = context.nof_symbols;
+    const uint64_t key = static_cast<uint64_t>(context.slot.system_slot()) * geo.nsymb + l;
     if (!current_grid) {
+      if (sector >= 0) {
+        group->join(sector, key, false);  // the group's round for this symbol stops waiting for this sector
+      }
       return false;
     }
-    const unsigned l = context.nof_symbols;
     const unsigned s = context.slot.subframe_slot_index() * geo.nsymb + l;
     const unsigned n = geo.size[s];
-    symbol_stage&  st = *stages[l];
-    hipStream_t    hs = stream.get();
+    // Grouped: the samples go into the group's round for this symbol, launched with the other sectors' samples.
+    const int r = sector >= 0 ? group->join(sector, key, true) : -1;
+    if (r >= 0) {
+      uint8_t* dst = group->input(r, sector);
+      for (unsigned p = 0; p != nof_ports; ++p) {
+        span<const cf_t> in = samples.get_channel_buffer(p);
+        srsran_assert(in.size() == n, "The input buffer size ({}) does not match the symbol size ({}).", in.size(), n);
+        std::memcpy(dst + static_cast<size_t>(p) * n * sizeof(cf_t), in.data(), n * sizeof(cf_t));
+      }
+      group->written(r, sector);
+      pending.push_back({l, context, r});
+      if (l == geo.nsymb - 1) {
+        drain(0);
+        current_grid.release();
+      } else {
+        drain(max_symbols_in_flight);
+      }
+      return true;
+    }
+    symbol_stage& st = *stages[l];
+    hipStream_t   hs = stream.get();
     for (unsigned p = 0; p != nof_ports; ++p) {
       span<const cf_t> in = samples.get_channel_buffer(p);
       srsran_assert(in.size() == n, "The input buffer size ({}) does not match the symbol size ({}).", in.size(), n);
@@ -501,7 +988,7 @@ private:
     }
     gpu::hip_check(hipGraphLaunch(exec, hs), WHO, "graph launch");
     gpu::hip_check(hipEventRecord(st.done, hs), WHO, "event");
-    pending.push_back({l, context});
+    pending.push_back({l, context, -1});
     // Deliver what has finished; bound the symbols in flight; the slot's last symbol drains the slot.
     if (l == geo.nsymb - 1) {
       drain(0);
@@ -533,16 +1020,30 @@ private:
   {
     while (!pending.empty()) {
       const pending_symbol& ps = pending.front();
-      symbol_stage&         st = *stages[ps.symbol];
-      if (pending.size() > keep) {
-        gpu::hip_check(hipEventSynchronize(st.done), WHO, "demodulation");
-      } else if (hipEventQuery(st.done) != hipSuccess) {
-        break;
+      const uint8_t*        rows;
+      if (ps.round >= 0) {
+        if (!group->ready(ps.round, pending.size() > keep)) {
+          break;
+        }
+        rows = group->output(ps.round, sector);
+      } else {
+        symbol_stage& st = *stages[ps.symbol];
+        if (pending.size() > keep) {
+          gpu::hip_check(hipEventSynchronize(st.done), WHO, "demodulation");
+        } else if (hipEventQuery(st.done) != hipSuccess) {
+          break;
+        }
+        rows = st.out.host();
       }
       resource_grid_writer& writer = current_grid.get().get_writer();
       for (unsigned p = 0; p != nof_ports; ++p) {
         writer.put(p, ps.symbol, 0, 1,
-                   span<const cbf16_t>(st.out.host<cbf16_t>(static_cast<size_t>(p) * nsc * sizeof(uint32_t)), nsc));
+                   span<const cbf16_t>(reinterpret_cast<const cbf16_t*>(rows + static_cast<size_t>(p) * nsc *
+                                                                                    sizeof(uint32_t)),
+                                       nsc));
+      }
+      if (ps.round >= 0) {
+        group->release(ps.round);
       }
       notifier->on_rx_symbol(current_grid, ps.context);
       pending.pop_front();
@@ -552,8 +1053,12 @@ private:
   struct pending_symbol {
     unsigned                    symbol;
     lower_phy_rx_symbol_context context;
+    int                         round;  ///< the group's round holding the result, -1: this processor's own stage
   };
 
+  std::shared_ptr<lower_phy_sector_group>    group_owner;
+  sector_rounds*                             group  = nullptr;
+  int                                        sector = -1;  ///< index in the group, -1: not grouped
   std::shared_ptr<srsgpu_context>            owner;
   srsgpu_context*                            ctx;
   gpu::owned_stream                          stream;
@@ -575,43 +1080,71 @@ private:
 class pdxch_processor_factory_gpu : public pdxch_processor_factory
 {
 public:
-  explicit pdxch_processor_factory_gpu(int device) : ctx(gpu::shared_context(device)) {}
+  pdxch_processor_factory_gpu(int device, std::shared_ptr<lower_phy_sector_group> g) :
+    ctx(gpu::shared_context(device)), group(std::move(g))
+  {
+  }
   std::unique_ptr<pdxch_processor> create(const pdxch_processor_configuration& config) override
   {
-    return std::make_unique<pdxch_processor_gpu>(ctx, config);
+    return std::make_unique<pdxch_processor_gpu>(ctx, config, group);
   }
 
 private:
-  std::shared_ptr<srsgpu_context> ctx;
+  std::shared_ptr<srsgpu_context>         ctx;
+  std::shared_ptr<lower_phy_sector_group> group;
 };
 
 class puxch_processor_factory_gpu : public puxch_processor_factory
 {
 public:
-  puxch_processor_factory_gpu(int device, unsigned max_symbols_in_flight_) :
-    ctx(gpu::shared_context(device)), max_symbols_in_flight(max_symbols_in_flight_)
+  puxch_processor_factory_gpu(int device, unsigned max_symbols_in_flight_, std::shared_ptr<lower_phy_sector_group> g) :
+    ctx(gpu::shared_context(device)), max_symbols_in_flight(max_symbols_in_flight_), group(std::move(g))
   {
   }
   std::unique_ptr<puxch_processor> create(const puxch_processor_configuration& config) override
   {
-    return std::make_unique<puxch_processor_gpu>(ctx, config, max_symbols_in_flight);
+    return std::make_unique<puxch_processor_gpu>(ctx, config, max_symbols_in_flight, group);
   }
 
 private:
-  std::shared_ptr<srsgpu_context> ctx;
-  unsigned                        max_symbols_in_flight;
+  std::shared_ptr<srsgpu_context>         ctx;
+  unsigned                                max_symbols_in_flight;
+  std::shared_ptr<lower_phy_sector_group> group;
 };
 
 } // namespace
 
 std::shared_ptr<pdxch_processor_factory> create_pdxch_processor_factory_gpu(int device)
 {
-  return std::make_shared<pdxch_processor_factory_gpu>(device);
+  return std::make_shared<pdxch_processor_factory_gpu>(device, nullptr);
 }
 
 std::shared_ptr<puxch_processor_factory> create_puxch_processor_factory_gpu(int device, unsigned max_symbols_in_flight)
 {
-  return std::make_shared<puxch_processor_factory_gpu>(device, max_symbols_in_flight);
+  return std::make_shared<puxch_processor_factory_gpu>(device, max_symbols_in_flight, nullptr);
+}
+
+std::shared_ptr<lower_phy_sector_group> create_lower_phy_sector_group(const lower_phy_group_configuration& config)
+{
+  return std::make_shared<lower_phy_sector_group>(config);
+}
+
+std::shared_ptr<pdxch_processor_factory> create_pdxch_processor_factory_gpu(std::shared_ptr<lower_phy_sector_group> group)
+{
+  const int device = group->cfg.device;
+  return std::make_shared<pdxch_processor_factory_gpu>(device, std::move(group));
+}
+
+std::shared_ptr<puxch_processor_factory> create_puxch_processor_factory_gpu(std::shared_ptr<lower_phy_sector_group> group,
+                                                                            unsigned max_symbols_in_flight)
+{
+  const int device = group->cfg.device;
+  return std::make_shared<puxch_processor_factory_gpu>(device, max_symbols_in_flight, std::move(group));
+}
+
+lower_phy_group_counters get_lower_phy_group_counters(const lower_phy_sector_group& group)
+{
+  return group.counters();
 }
 
 } // namespace srsran

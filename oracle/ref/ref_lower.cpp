@@ -4,7 +4,8 @@
 //     pdxch_processor_impl.cpp, uplink/puxch/puxch_processor_impl.cpp, compiled from their sources by
 //     oracle/build_chain.sh) on the reference's OFDM symbol (de)modulator with the generic DFT (variant 0) or on the GPU
 //     symbol objects of integration/ofdm_gpu.cpp (variant 1);
-//   * the GPU processors of integration/lower_phy_gpu.cpp (variant 2).
+//   * the GPU processors of integration/lower_phy_gpu.cpp (variant 2), and those of a sector group (variant 3, several
+//     sectors driven from their own threads: ref_lower_sectors_run).
 // Every variant sees the same requests, grids and samples; the test compares samples, grids, return values and the
 // notifications (late requests, received symbols). Never shipped.
 #include "signal_chain_gpu.h"
@@ -28,8 +29,13 @@
 #include "srsran/phy/support/resource_grid_reader.h"
 #include "srsran/phy/support/resource_grid_writer.h"
 
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 using namespace srsran;
@@ -106,6 +112,231 @@ unsigned symbol_size(int numerology, int dft_size, cyclic_prefix cp, unsigned sy
          dft_size;
 }
 
+/// The lower-PHY configuration every sector of a scenario shares (the carrier frequency is per sector).
+struct scenario {
+  int           numerology;
+  int           bw_rb;
+  int           dft_size;
+  cyclic_prefix cp;
+  float         dft_window_offset;
+  int           nof_ports;
+
+  subcarrier_spacing scs() const { return scs_of(numerology); }
+  unsigned           nsymb() const { return get_nsymb_per_slot(cp); }
+  unsigned           nsc() const { return 12 * bw_rb; }
+  double             srate() const { return static_cast<double>(dft_size) * scs_to_khz(scs()) * 1000.0; }
+};
+
+/// Variants 0 (reference processor, generic DFT), 1 (reference processor, GPU symbol objects), 2 (GPU processor) and
+/// 3 (GPU processor of a sector group).
+std::unique_ptr<pdxch_processor>
+make_pdxch(int variant, const scenario& sc, double center_freq_hz, const std::shared_ptr<lower_phy_sector_group>& group)
+{
+  if (variant >= 2) {
+    pdxch_processor_configuration c;
+    c.cp             = sc.cp;
+    c.scs            = sc.scs();
+    c.srate          = sampling_rate::from_Hz(sc.srate());
+    c.bandwidth_rb   = sc.bw_rb;
+    c.center_freq_Hz = center_freq_hz;
+    c.nof_tx_ports   = sc.nof_ports;
+    return (variant == 3 ? create_pdxch_processor_factory_gpu(group) : create_pdxch_processor_factory_gpu(0))->create(c);
+  }
+  ofdm_modulator_configuration mc{static_cast<unsigned>(sc.numerology), static_cast<unsigned>(sc.bw_rb),
+                                  static_cast<unsigned>(sc.dft_size), sc.cp, 1.0F, center_freq_hz};
+  std::unique_ptr<ofdm_symbol_modulator> mod;
+  if (variant == 0) {
+    ofdm_modulator_common_configuration common;
+    common.dft = std::make_unique<dft_processor_generic_impl>(
+        dft_processor::configuration{static_cast<unsigned>(sc.dft_size), dft_processor::direction::INVERSE});
+    mod = std::make_unique<ofdm_symbol_modulator_impl>(common, mc);
+  } else {
+    mod = create_ofdm_modulator_factory_gpu(0)->create_ofdm_symbol_modulator(mc);
+  }
+  pdxch_processor_impl::configuration pc{sc.cp, static_cast<unsigned>(sc.nof_ports), 16};
+  return std::make_unique<pdxch_processor_impl>(std::move(mod), pc);
+}
+
+std::unique_ptr<puxch_processor> make_puxch(int                                            variant,
+                                            int                                            max_in_flight,
+                                            const scenario&                                sc,
+                                            double                                         center_freq_hz,
+                                            const std::shared_ptr<lower_phy_sector_group>& group)
+{
+  if (variant >= 2) {
+    puxch_processor_configuration c;
+    c.cp                = sc.cp;
+    c.scs               = sc.scs();
+    c.srate             = sampling_rate::from_Hz(sc.srate());
+    c.bandwidth_rb      = sc.bw_rb;
+    c.dft_window_offset = sc.dft_window_offset;
+    c.center_freq_Hz    = center_freq_hz;
+    c.nof_rx_ports      = sc.nof_ports;
+    const unsigned f    = static_cast<unsigned>(max_in_flight);
+    return (variant == 3 ? create_puxch_processor_factory_gpu(group, f) : create_puxch_processor_factory_gpu(0, f))
+        ->create(c);
+  }
+  // puxch_processor_factory_sw::create (puxch_processor_factories.cpp:41-57).
+  const unsigned woff = static_cast<unsigned>(static_cast<float>(sc.cp.get_length(1, sc.scs()).to_samples(sc.srate())) *
+                                              sc.dft_window_offset);
+  ofdm_demodulator_configuration dc{static_cast<unsigned>(sc.numerology), static_cast<unsigned>(sc.bw_rb),
+                                    static_cast<unsigned>(sc.dft_size), sc.cp, woff,
+                                    1.0F / std::sqrt(static_cast<float>(sc.bw_rb * 12)), center_freq_hz};
+  std::unique_ptr<ofdm_symbol_demodulator> demod;
+  if (variant == 0) {
+    ofdm_demodulator_common_configuration common;
+    common.dft = std::make_unique<dft_processor_generic_impl>(
+        dft_processor::configuration{static_cast<unsigned>(sc.dft_size), dft_processor::direction::DIRECT});
+    demod = std::make_unique<ofdm_symbol_demodulator_impl>(common, dc);
+  } else {
+    demod = create_ofdm_demodulator_factory_gpu(0)->create_ofdm_symbol_demodulator(dc);
+  }
+  puxch_processor_impl::configuration pc{sc.cp, static_cast<unsigned>(sc.nof_ports), 16};
+  return std::make_unique<puxch_processor_impl>(std::move(demod), pc);
+}
+
+/// A grid pool holding the scenario's DL grids (port_mask bit p clear: port p stays empty).
+void fill_pool(harness_pool& pool, const scenario& sc, int nof_grids, const uint16_t* grids, const uint32_t* port_mask)
+{
+  const unsigned nsymb = sc.nsymb();
+  const unsigned nsc   = sc.nsc();
+  for (int g = 0; g < nof_grids; ++g) {
+    resource_grid_writer& w = pool.get(g).get_writer();
+    for (int p = 0; p < sc.nof_ports; ++p) {
+      if (((port_mask[g] >> p) & 1U) == 0) {
+        continue;
+      }
+      for (unsigned l = 0; l != nsymb; ++l) {
+        const auto* row =
+            reinterpret_cast<const cbf16_t*>(grids + 2 * ((static_cast<size_t>(g) * sc.nof_ports + p) * nsymb + l) * nsc);
+        w.put(p, l, 0, 1, span<const cbf16_t>(row, nsc));
+      }
+    }
+  }
+}
+
+/// The DL script (see ref_lower_pdxch_run). Returns the number of samples produced, -1 when they overflow samples_cap.
+long run_pdxch_script(pdxch_processor&  proc,
+                      harness_pool&     pool,
+                      const scenario&   sc,
+                      int               nof_events,
+                      const int*        events,
+                      float*            samples_out,
+                      long              samples_cap,
+                      uint8_t*          processed_out)
+{
+  long        pos   = 0;
+  size_t      nflag = 0;
+  span_writer buf;
+  for (int e = 0; e < nof_events; ++e) {
+    const int*       ev = events + 4 * e;
+    const slot_point slot(static_cast<uint32_t>(sc.numerology), static_cast<uint32_t>(ev[1]));
+    if (ev[0] == 0) {
+      proc.get_request_handler().handle_request(pool.grab(static_cast<unsigned>(ev[2])), {slot, 0});
+      continue;
+    }
+    for (int l = ev[2]; l < ev[3]; ++l) {
+      const unsigned n    = symbol_size(sc.numerology, sc.dft_size, sc.cp, slot.subframe_slot_index() * sc.nsymb() + l);
+      const long     need = static_cast<long>(n) * sc.nof_ports;
+      long           at   = pos;
+      if (samples_cap < 0) {
+        if (need > -samples_cap) {
+          return -1;
+        }
+        at = (pos % -samples_cap) + need > -samples_cap ? 0 : pos % -samples_cap;
+      } else if (pos + need > samples_cap) {
+        return -1;
+      }
+      buf.ch.clear();
+      for (int p = 0; p < sc.nof_ports; ++p) {
+        auto* dst = reinterpret_cast<cf_t*>(samples_out) + at + static_cast<long>(p) * n;
+        if (samples_cap >= 0) {
+          std::fill(dst, dst + n, cf_t(1e30F, 1e30F));
+        }
+        buf.ch.emplace_back(dst, n);
+      }
+      pdxch_processor_baseband::symbol_context ctx{slot, 0, static_cast<unsigned>(l)};
+      processed_out[nflag++] = proc.get_baseband().process_symbol(buf, ctx) ? 1 : 0;
+      pos += need;
+    }
+  }
+  return pos;
+}
+
+/// The UL script (see ref_lower_puxch_run).
+void run_puxch_script(puxch_processor& proc,
+                      harness_pool&    pool,
+                      const scenario&  sc,
+                      int              nof_events,
+                      const int*       events,
+                      const float*     samples_in,
+                      uint8_t*         processed_out)
+{
+  long        pos   = 0;
+  size_t      nflag = 0;
+  span_reader buf;
+  for (int e = 0; e < nof_events; ++e) {
+    const int*       ev = events + 4 * e;
+    const slot_point slot(static_cast<uint32_t>(sc.numerology), static_cast<uint32_t>(ev[1]));
+    if (ev[0] == 0) {
+      proc.get_request_handler().handle_request(pool.grab(static_cast<unsigned>(ev[2])), {slot, 0});
+      continue;
+    }
+    for (int l = ev[2]; l < ev[3]; ++l) {
+      const unsigned n = symbol_size(sc.numerology, sc.dft_size, sc.cp, slot.subframe_slot_index() * sc.nsymb() + l);
+      buf.ch.clear();
+      for (int p = 0; p < sc.nof_ports; ++p) {
+        buf.ch.emplace_back(reinterpret_cast<const cf_t*>(samples_in) + pos + static_cast<long>(p) * n, n);
+      }
+      lower_phy_rx_symbol_context ctx{slot, 0, static_cast<unsigned>(l)};
+      processed_out[nflag++] = proc.get_baseband().process_symbol(buf, ctx) ? 1 : 0;
+      pos += static_cast<long>(n) * sc.nof_ports;
+    }
+  }
+}
+
+/// Final grid contents (nof_grids x ports x nsymb x nsc bf16 pairs).
+void dump_pool(harness_pool& pool, const scenario& sc, int nof_grids, uint16_t* grids_out)
+{
+  const unsigned nsymb = sc.nsymb();
+  const unsigned nsc   = sc.nsc();
+  for (int g = 0; g < nof_grids; ++g) {
+    const resource_grid_reader& r = pool.get(g).get_reader();
+    for (int p = 0; p < sc.nof_ports; ++p) {
+      for (unsigned l = 0; l != nsymb; ++l) {
+        std::memcpy(grids_out + 2 * ((static_cast<size_t>(g) * sc.nof_ports + p) * nsymb + l) * nsc,
+                    r.get_view(p, l).data(), nsc * sizeof(cbf16_t));
+      }
+    }
+  }
+}
+
+/// All sector threads meet here between the DL and UL scripts.
+class barrier
+{
+public:
+  explicit barrier(unsigned n_) : n(n_) {}
+  void wait()
+  {
+    std::unique_lock<std::mutex> lock(mtx);
+    const unsigned               gen = generation;
+    if (++count == n) {
+      count = 0;
+      ++generation;
+      cv.notify_all();
+      return;
+    }
+    cv.wait(lock, [&]() { return generation != gen; });
+  }
+
+private:
+  std::mutex              mtx;
+  std::condition_variable cv;
+  unsigned                n;
+  unsigned                count      = 0;
+  unsigned                generation = 0;
+};
+
 } // namespace
 
 extern "C" {
@@ -114,7 +345,9 @@ extern "C" {
 /// written (the others stay empty). events: nof_events x {kind, system slot, a, b}: kind 0 = handle_request(grid a),
 /// kind 1 = process_symbol for symbols [a, b) of the slot. Outputs, in event order: the samples of every processed
 /// symbol and port (sentinel 1e30 where the processor leaves the buffer untouched), one return flag per symbol, the
-/// late-request slots. Returns the number of samples written (< 0 on error).
+/// late-request slots. Returns the number of samples written (< 0 on error). Benchmark mode, samples_cap < 0: the
+/// samples go round a ring of -samples_cap samples (a radio's reused baseband buffer: no page faults on fresh memory, no
+/// sentinel fill), the return value still counts every sample.
 long ref_lower_pdxch_run(int             variant,
                          int             numerology,
                          int             bw_rb,
@@ -133,80 +366,15 @@ long ref_lower_pdxch_run(int             variant,
                          int*            late_out,
                          int*            nof_late)
 {
-  const cyclic_prefix      cp    = cp_extended ? cyclic_prefix::EXTENDED : cyclic_prefix::NORMAL;
-  const subcarrier_spacing scs   = scs_of(numerology);
-  const unsigned           nsymb = get_nsymb_per_slot(cp);
-  const unsigned           nsc   = 12 * bw_rb;
-  harness_pool             pool(nof_grids, nof_ports, nsymb, nsc);
-  for (int g = 0; g < nof_grids; ++g) {
-    resource_grid_writer& w = pool.get(g).get_writer();
-    for (int p = 0; p < nof_ports; ++p) {
-      if (((port_mask[g] >> p) & 1U) == 0) {
-        continue;
-      }
-      for (unsigned l = 0; l != nsymb; ++l) {
-        const auto* row = reinterpret_cast<const cbf16_t*>(grids + 2 * ((static_cast<size_t>(g) * nof_ports + p) * nsymb + l) * nsc);
-        w.put(p, l, 0, 1, span<const cbf16_t>(row, nsc));
-      }
-    }
-  }
-
-  std::unique_ptr<pdxch_processor> proc;
-  if (variant == 2) {
-    pdxch_processor_configuration c;
-    c.cp             = cp;
-    c.scs            = scs;
-    c.srate          = sampling_rate::from_Hz(static_cast<double>(dft_size) * scs_to_khz(scs) * 1000.0);
-    c.bandwidth_rb   = bw_rb;
-    c.center_freq_Hz = center_freq_hz;
-    c.nof_tx_ports   = nof_ports;
-    proc             = create_pdxch_processor_factory_gpu(0)->create(c);
-  } else {
-    ofdm_modulator_configuration mc{static_cast<unsigned>(numerology), static_cast<unsigned>(bw_rb),
-                                    static_cast<unsigned>(dft_size), cp, 1.0F, center_freq_hz};
-    std::unique_ptr<ofdm_symbol_modulator> mod;
-    if (variant == 0) {
-      ofdm_modulator_common_configuration common;
-      common.dft = std::make_unique<dft_processor_generic_impl>(
-          dft_processor::configuration{static_cast<unsigned>(dft_size), dft_processor::direction::INVERSE});
-      mod = std::make_unique<ofdm_symbol_modulator_impl>(common, mc);
-    } else {
-      mod = create_ofdm_modulator_factory_gpu(0)->create_ofdm_symbol_modulator(mc);
-    }
-    pdxch_processor_impl::configuration pc{cp, static_cast<unsigned>(nof_ports), 16};
-    proc = std::make_unique<pdxch_processor_impl>(std::move(mod), pc);
-  }
-  pdxch_recorder rec;
+  const scenario sc{numerology, bw_rb, dft_size, cp_extended ? cyclic_prefix::EXTENDED : cyclic_prefix::NORMAL, 0.0F,
+                    nof_ports};
+  harness_pool   pool(nof_grids, nof_ports, sc.nsymb(), sc.nsc());
+  fill_pool(pool, sc, nof_grids, grids, port_mask);
+  std::unique_ptr<pdxch_processor> proc = make_pdxch(variant, sc, center_freq_hz, nullptr);
+  pdxch_recorder                   rec;
   proc->connect(rec);
-
-  long              pos = 0;
-  size_t            nflag = 0;
-  span_writer       buf;
-  std::vector<cf_t> store;
-  for (int e = 0; e < nof_events; ++e) {
-    const int*       ev = events + 4 * e;
-    const slot_point slot(static_cast<uint32_t>(numerology), static_cast<uint32_t>(ev[1]));
-    if (ev[0] == 0) {
-      proc->get_request_handler().handle_request(pool.grab(static_cast<unsigned>(ev[2])), {slot, 0});
-      continue;
-    }
-    for (int l = ev[2]; l < ev[3]; ++l) {
-      const unsigned n = symbol_size(numerology, dft_size, cp, slot.subframe_slot_index() * nsymb + l);
-      if (pos + static_cast<long>(n) * nof_ports > samples_cap) {
-        return -1;
-      }
-      buf.ch.clear();
-      for (int p = 0; p < nof_ports; ++p) {
-        auto* dst = reinterpret_cast<cf_t*>(samples_out) + pos + static_cast<long>(p) * n;
-        std::fill(dst, dst + n, cf_t(1e30F, 1e30F));
-        buf.ch.emplace_back(dst, n);
-      }
-      pdxch_processor_baseband::symbol_context ctx{slot, 0, static_cast<unsigned>(l)};
-      processed_out[nflag++] = proc->get_baseband().process_symbol(buf, ctx) ? 1 : 0;
-      pos += static_cast<long>(n) * nof_ports;
-    }
-  }
-  *nof_late = static_cast<int>(rec.late.size());
+  const long pos = run_pdxch_script(*proc, pool, sc, nof_events, events, samples_out, samples_cap, processed_out);
+  *nof_late      = static_cast<int>(rec.late.size());
   std::copy(rec.late.begin(), rec.late.end(), late_out);
   return pos;
 }
@@ -235,81 +403,143 @@ int ref_lower_puxch_run(int          variant,
                         int*         late_out,
                         int*         nof_late)
 {
-  const cyclic_prefix      cp    = cp_extended ? cyclic_prefix::EXTENDED : cyclic_prefix::NORMAL;
-  const subcarrier_spacing scs   = scs_of(numerology);
-  const unsigned           nsymb = get_nsymb_per_slot(cp);
-  const unsigned           nsc   = 12 * bw_rb;
-  const double             srate = static_cast<double>(dft_size) * scs_to_khz(scs) * 1000.0;
-  harness_pool             pool(nof_grids, nof_ports, nsymb, nsc);
-
-  std::unique_ptr<puxch_processor> proc;
-  if (variant == 2) {
-    puxch_processor_configuration c;
-    c.cp                = cp;
-    c.scs               = scs;
-    c.srate             = sampling_rate::from_Hz(srate);
-    c.bandwidth_rb      = bw_rb;
-    c.dft_window_offset = dft_window_offset;
-    c.center_freq_Hz    = center_freq_hz;
-    c.nof_rx_ports      = nof_ports;
-    proc                = create_puxch_processor_factory_gpu(0, static_cast<unsigned>(max_in_flight))->create(c);
-  } else {
-    // puxch_processor_factory_sw::create (puxch_processor_factories.cpp:41-57).
-    const unsigned woff = static_cast<unsigned>(static_cast<float>(cp.get_length(1, scs).to_samples(srate)) *
-                                                dft_window_offset);
-    ofdm_demodulator_configuration dc{static_cast<unsigned>(numerology), static_cast<unsigned>(bw_rb),
-                                      static_cast<unsigned>(dft_size), cp, woff,
-                                      1.0F / std::sqrt(static_cast<float>(bw_rb * 12)), center_freq_hz};
-    std::unique_ptr<ofdm_symbol_demodulator> demod;
-    if (variant == 0) {
-      ofdm_demodulator_common_configuration common;
-      common.dft = std::make_unique<dft_processor_generic_impl>(
-          dft_processor::configuration{static_cast<unsigned>(dft_size), dft_processor::direction::DIRECT});
-      demod = std::make_unique<ofdm_symbol_demodulator_impl>(common, dc);
-    } else {
-      demod = create_ofdm_demodulator_factory_gpu(0)->create_ofdm_symbol_demodulator(dc);
-    }
-    puxch_processor_impl::configuration pc{cp, static_cast<unsigned>(nof_ports), 16};
-    proc = std::make_unique<puxch_processor_impl>(std::move(demod), pc);
-  }
-  puxch_recorder rec;
+  const scenario sc{numerology,        bw_rb,    dft_size, cp_extended ? cyclic_prefix::EXTENDED : cyclic_prefix::NORMAL,
+                    dft_window_offset, nof_ports};
+  harness_pool   pool(nof_grids, nof_ports, sc.nsymb(), sc.nsc());
+  std::unique_ptr<puxch_processor> proc = make_puxch(variant, max_in_flight, sc, center_freq_hz, nullptr);
+  puxch_recorder                   rec;
   proc->connect(rec);
-
-  long        pos   = 0;
-  size_t      nflag = 0;
-  span_reader buf;
-  for (int e = 0; e < nof_events; ++e) {
-    const int*       ev = events + 4 * e;
-    const slot_point slot(static_cast<uint32_t>(numerology), static_cast<uint32_t>(ev[1]));
-    if (ev[0] == 0) {
-      proc->get_request_handler().handle_request(pool.grab(static_cast<unsigned>(ev[2])), {slot, 0});
-      continue;
-    }
-    for (int l = ev[2]; l < ev[3]; ++l) {
-      const unsigned n = symbol_size(numerology, dft_size, cp, slot.subframe_slot_index() * nsymb + l);
-      buf.ch.clear();
-      for (int p = 0; p < nof_ports; ++p) {
-        buf.ch.emplace_back(reinterpret_cast<const cf_t*>(samples_in) + pos + static_cast<long>(p) * n, n);
-      }
-      lower_phy_rx_symbol_context ctx{slot, 0, static_cast<unsigned>(l)};
-      processed_out[nflag++] = proc->get_baseband().process_symbol(buf, ctx) ? 1 : 0;
-      pos += static_cast<long>(n) * nof_ports;
-    }
-  }
+  run_puxch_script(*proc, pool, sc, nof_events, events, samples_in, processed_out);
   proc.reset();
-  for (int g = 0; g < nof_grids; ++g) {
-    const resource_grid_reader& r = pool.get(g).get_reader();
-    for (int p = 0; p < nof_ports; ++p) {
-      for (unsigned l = 0; l != nsymb; ++l) {
-        std::memcpy(grids_out + 2 * ((static_cast<size_t>(g) * nof_ports + p) * nsymb + l) * nsc,
-                    r.get_view(p, l).data(), nsc * sizeof(cbf16_t));
-      }
-    }
-  }
+  dump_pool(pool, sc, nof_grids, grids_out);
   *nof_rx   = static_cast<int>(rec.rx.size() / 2);
   *nof_late = static_cast<int>(rec.late.size());
   std::copy(rec.rx.begin(), rec.rx.end(), rx_out);
   std::copy(rec.late.begin(), rec.late.end(), late_out);
+  return 0;
+}
+
+/// Several sectors at once, as the reference's radio unit runs them (one lower-PHY sector per cell, each driven by its
+/// own thread: lib/ru/generic/ru_factory_generic_impl.cpp:75-90): nof_sectors threads, sector k with carrier
+/// center_freq_hz[k], its own grids (dl_grids + k * grid block, dl_port_mask + k * nof_grids) and UL samples
+/// (ul_samples + k * ul_stride complex samples), first all run the DL script together, then (after a barrier) the UL
+/// script. Variant 3: the sectors' GPU processors come from one lower_phy_sector_group (window_us: its gather windows,
+/// 0 = defaults). Outputs per sector k at k x the stride of one sector: DL samples (dl_cap < 0: a ring per sector, as
+/// ref_lower_pdxch_run), DL and UL return flags, UL grids, UL notifications (nof_rx[k] pairs) and late slots
+/// (nof_late[k], DL then UL); seconds[2k], seconds[2k+1]: the sector's DL and UL script wall time. group_counts (6
+/// values, variant 3): lower_phy_group_counters. Returns 0, -1 on a sample overflow.
+int ref_lower_sectors_run(int             variant,
+                          int             max_in_flight,
+                          int             nof_sectors,
+                          int             numerology,
+                          int             bw_rb,
+                          int             dft_size,
+                          int             cp_extended,
+                          float           dft_window_offset,
+                          const double*   center_freq_hz,
+                          int             nof_ports,
+                          int             nof_grids,
+                          int             window_us,
+                          const uint16_t* dl_grids,
+                          const uint32_t* dl_port_mask,
+                          int             nof_dl_events,
+                          const int*      dl_events,
+                          float*          dl_samples_out,
+                          long            dl_cap,
+                          uint8_t*        dl_processed,
+                          int             nof_ul_events,
+                          const int*      ul_events,
+                          const float*    ul_samples,
+                          long            ul_stride,
+                          uint16_t*       ul_grids_out,
+                          uint8_t*        ul_processed,
+                          int*            rx_out,
+                          int*            nof_rx,
+                          int*            late_out,
+                          int*            nof_late,
+                          double*         seconds,
+                          uint64_t*       group_counts)
+{
+  const scenario sc{numerology,        bw_rb,    dft_size, cp_extended ? cyclic_prefix::EXTENDED : cyclic_prefix::NORMAL,
+                    dft_window_offset, nof_ports};
+  const size_t   grid_block = static_cast<size_t>(nof_grids) * nof_ports * sc.nsymb() * sc.nsc() * 2;
+  int            n_dl_proc = 0, n_ul_proc = 0;
+  for (int e = 0; e < nof_dl_events; ++e) {
+    n_dl_proc += dl_events[4 * e] == 1 ? dl_events[4 * e + 3] - dl_events[4 * e + 2] : 0;
+  }
+  for (int e = 0; e < nof_ul_events; ++e) {
+    n_ul_proc += ul_events[4 * e] == 1 ? ul_events[4 * e + 3] - ul_events[4 * e + 2] : 0;
+  }
+  const long dl_stride   = 2 * std::labs(dl_cap);
+  const int  late_stride = nof_dl_events + nof_ul_events + 1;
+
+  std::shared_ptr<lower_phy_sector_group> group;
+  if (variant == 3) {
+    lower_phy_group_configuration gc;
+    gc.device      = 0;
+    gc.nof_sectors = static_cast<unsigned>(nof_sectors);
+    if (window_us > 0) {
+      gc.ul_window_us = static_cast<unsigned>(window_us);
+      gc.dl_window_us = static_cast<unsigned>(window_us);
+    }
+    group = create_lower_phy_sector_group(gc);
+  }
+  std::vector<std::unique_ptr<harness_pool>>    dl_pools, ul_pools;
+  std::vector<std::unique_ptr<pdxch_processor>> dl;
+  std::vector<std::unique_ptr<puxch_processor>> ul;
+  std::vector<pdxch_recorder>                   dl_rec(nof_sectors);
+  std::vector<puxch_recorder>                   ul_rec(nof_sectors);
+  for (int k = 0; k < nof_sectors; ++k) {
+    dl_pools.emplace_back(std::make_unique<harness_pool>(nof_grids, nof_ports, sc.nsymb(), sc.nsc()));
+    fill_pool(*dl_pools.back(), sc, nof_grids, dl_grids + k * grid_block, dl_port_mask + k * nof_grids);
+    ul_pools.emplace_back(std::make_unique<harness_pool>(nof_grids, nof_ports, sc.nsymb(), sc.nsc()));
+    dl.push_back(make_pdxch(variant, sc, center_freq_hz[k], group));
+    dl.back()->connect(dl_rec[k]);
+    ul.push_back(make_puxch(variant, max_in_flight, sc, center_freq_hz[k], group));
+    ul.back()->connect(ul_rec[k]);
+  }
+  barrier                  meet(static_cast<unsigned>(nof_sectors));
+  std::vector<long>        produced(nof_sectors, 0);
+  std::vector<std::thread> threads;
+  for (int k = 0; k < nof_sectors; ++k) {
+    threads.emplace_back([&, k]() {
+      using clock = std::chrono::steady_clock;
+      meet.wait();
+      auto t0     = clock::now();
+      produced[k] = run_pdxch_script(*dl[k], *dl_pools[k], sc, nof_dl_events, dl_events, dl_samples_out + k * dl_stride,
+                                     dl_cap, dl_processed + static_cast<size_t>(k) * n_dl_proc);
+      seconds[2 * k] = std::chrono::duration<double>(clock::now() - t0).count();
+      meet.wait();
+      t0 = clock::now();
+      run_puxch_script(*ul[k], *ul_pools[k], sc, nof_ul_events, ul_events, ul_samples + 2 * k * ul_stride,
+                       ul_processed + static_cast<size_t>(k) * n_ul_proc);
+      seconds[2 * k + 1] = std::chrono::duration<double>(clock::now() - t0).count();
+    });
+  }
+  for (std::thread& t : threads) {
+    t.join();
+  }
+  dl.clear();
+  ul.clear();
+  for (int k = 0; k < nof_sectors; ++k) {
+    dump_pool(*ul_pools[k], sc, nof_grids, ul_grids_out + k * grid_block);
+    nof_rx[k] = static_cast<int>(ul_rec[k].rx.size() / 2);
+    std::copy(ul_rec[k].rx.begin(), ul_rec[k].rx.end(), rx_out + static_cast<size_t>(k) * 2 * n_ul_proc);
+    int* late = late_out + static_cast<size_t>(k) * late_stride;
+    late      = std::copy(dl_rec[k].late.begin(), dl_rec[k].late.end(), late);
+    std::copy(ul_rec[k].late.begin(), ul_rec[k].late.end(), late);
+    nof_late[k] = static_cast<int>(dl_rec[k].late.size() + ul_rec[k].late.size());
+  }
+  if (group) {
+    const lower_phy_group_counters c = get_lower_phy_group_counters(*group);
+    const uint64_t                 v[6] = {c.ul_rounds, c.ul_grouped, c.ul_alone, c.dl_rounds, c.dl_grouped, c.dl_alone};
+    std::copy(v, v + 6, group_counts);
+  }
+  for (long p : produced) {
+    if (p < 0) {
+      return -1;
+    }
+  }
   return 0;
 }
 

@@ -20,7 +20,8 @@ struct srsgpu_ofdm_plan {
   ofdm_job*             d_jobs     = nullptr;
   int                   nof_jobs   = 0;
   float*                d_scratch  = nullptr;  ///< Split sizes: one N-point complex row per job.
-  std::vector<uint64_t> offsets;  ///< Sample offset of (grid, port); one extra entry = total.
+  std::vector<uint64_t> offsets;     ///< Sample offset of (grid, port); one extra entry = total.
+  uint64_t              grid_words = 0;  ///< uint32 words of the plan's grids (all grids, ports and symbols).
 };
 
 namespace {
@@ -168,6 +169,7 @@ int plan_create(srsgpu_context*           ctx,
     }
   }
   plan->offsets.push_back(pos);
+  plan->grid_words = static_cast<uint64_t>(nof_grids) * nof_ports * nof_symbols * nsc;
   if (pos >= (1ull << 32) || static_cast<uint64_t>(nof_grids) * nof_ports * nof_symbols * nsc >= (1ull << 32)) {
     delete plan;
     return fail(SRSGPU_ERR_INVALID_ARG, "batch too large for 32-bit offsets");
@@ -233,6 +235,86 @@ int srsgpu_ofdm_demodulator_symbols_plan_create(srsgpu_context*           ctx,
                                                 srsgpu_ofdm_plan**        plan)
 {
   return plan_create(ctx, false, cfg, 1, nof_ports, &slot_index, plan, first_symbol, nof_symbols);
+}
+
+int srsgpu_ofdm_plan_concat(srsgpu_context*                ctx,
+                            const srsgpu_ofdm_plan* const* members,
+                            uint32_t                       nof_members,
+                            srsgpu_ofdm_plan**             plan_out)
+{
+  if (ctx == nullptr || members == nullptr || plan_out == nullptr || nof_members == 0) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument or no member plans");
+  }
+  const srsgpu_ofdm_plan* first = members[0];
+  if (first == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null member plan");
+  }
+  std::lock_guard<std::mutex> lock(ctx->mtx);
+  HIP_TRY(hipSetDevice(ctx->device));
+  std::vector<ofdm_job> jobs;
+  uint64_t              samples = 0;
+  uint64_t              words   = 0;
+  auto*                 plan    = new srsgpu_ofdm_plan();
+  plan->ctx        = ctx;
+  plan->inverse    = first->inverse;
+  plan->dft_size   = first->dft_size;
+  plan->nsc        = first->nsc;
+  plan->window_off = first->window_off;
+  plan->nof_ports  = first->nof_ports;
+  for (uint32_t i = 0; i < nof_members; ++i) {
+    const srsgpu_ofdm_plan* m = members[i];
+    // One kernel runs every job: the members must agree on what the launch takes from the plan.
+    if (m == nullptr || m->ctx != ctx || m->inverse != first->inverse || m->dft_size != first->dft_size ||
+        m->nsc != first->nsc || m->window_off != first->window_off || m->nof_ports != first->nof_ports) {
+      delete plan;
+      return fail(SRSGPU_ERR_INVALID_ARG,
+                  "member plan %u differs from the first in context, direction, DFT size, bandwidth, window offset or "
+                  "ports",
+                  i);
+    }
+    const size_t base = jobs.size();
+    jobs.resize(base + m->nof_jobs);
+    if (m->nof_jobs > 0 && hipMemcpy(jobs.data() + base, m->d_jobs, m->nof_jobs * sizeof(ofdm_job),
+                                     hipMemcpyDeviceToHost) != hipSuccess) {
+      delete plan;
+      return fail(SRSGPU_ERR_HIP, "failed to read member plan %u's jobs", i);
+    }
+    for (size_t j = base; j != jobs.size(); ++j) {
+      jobs[j].grid_offset += static_cast<uint32_t>(words);
+      jobs[j].sample_offset += static_cast<uint32_t>(samples);
+    }
+    for (size_t k = 0; k + 1 < m->offsets.size(); ++k) {
+      plan->offsets.push_back(m->offsets[k] + samples);
+    }
+    samples += m->offsets.empty() ? 0 : m->offsets.back();
+    words += m->grid_words;
+    if (samples >= (1ull << 32) || words >= (1ull << 32)) {
+      delete plan;
+      return fail(SRSGPU_ERR_INVALID_ARG, "batch too large for 32-bit offsets");
+    }
+  }
+  plan->offsets.push_back(samples);
+  plan->grid_words = words;
+  plan->nof_jobs   = static_cast<int>(jobs.size());
+  if (!jobs.empty() && (hipMalloc(&plan->d_jobs, jobs.size() * sizeof(ofdm_job)) != hipSuccess ||
+                        hipMemcpy(plan->d_jobs, jobs.data(), jobs.size() * sizeof(ofdm_job), hipMemcpyHostToDevice) !=
+                            hipSuccess)) {
+    srsgpu_ofdm_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to upload OFDM jobs");
+  }
+  if (!jobs.empty() && ofdm_split_factor(plan->dft_size) != 0 &&
+      hipMalloc(&plan->d_scratch, jobs.size() * static_cast<size_t>(plan->dft_size) * 2 * sizeof(float)) !=
+          hipSuccess) {
+    srsgpu_ofdm_plan_destroy(plan);
+    return fail(SRSGPU_ERR_HIP, "failed to allocate the split-transform scratch");
+  }
+  *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+uint64_t srsgpu_ofdm_plan_nof_grid_words(const srsgpu_ofdm_plan* plan)
+{
+  return plan == nullptr ? 0 : plan->grid_words;
 }
 
 uint64_t srsgpu_ofdm_plan_nof_samples(const srsgpu_ofdm_plan* plan)

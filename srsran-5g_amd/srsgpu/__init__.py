@@ -391,6 +391,9 @@ def load_library(path: str = LIB_PATH):
         getattr(lib, name).argtypes = [P, P] + [ctypes.c_uint32] * 4 + [ctypes.POINTER(P)]
     lib.srsgpu_ofdm_plan_nof_samples.argtypes = [P]
     lib.srsgpu_ofdm_plan_nof_samples.restype = ctypes.c_uint64
+    lib.srsgpu_ofdm_plan_nof_grid_words.argtypes = [P]
+    lib.srsgpu_ofdm_plan_nof_grid_words.restype = ctypes.c_uint64
+    lib.srsgpu_ofdm_plan_concat.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(P)]
     lib.srsgpu_ofdm_plan_sample_offset.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     lib.srsgpu_ofdm_plan_sample_offset.restype = ctypes.c_uint64
     lib.srsgpu_ofdm_modulator_plan_execute.argtypes = [P, P, P, P]
@@ -420,6 +423,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_modulator_plan_create", "srsgpu_ofdm_demodulator_plan_create", "srsgpu_ofdm_plan_nof_samples",
     "srsgpu_ofdm_modulator_symbols_plan_create", "srsgpu_ofdm_demodulator_symbols_plan_create", "srsgpu_harq_copy",
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
+    "srsgpu_ofdm_plan_concat", "srsgpu_ofdm_plan_nof_grid_words",
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
     "srsgpu_pusch_demodulator_plan_create_ex", "srsgpu_pusch_demodulator_plan_execute_ex",
@@ -1428,6 +1432,23 @@ class OfdmPlan:
         if symbols is not None:
             self.nsymb = symbols[1]
         self.nof_samples = int(_lib.srsgpu_ofdm_plan_nof_samples(h))
+        self.grid_words = int(_lib.srsgpu_ofdm_plan_nof_grid_words(h))
+
+    @classmethod
+    def concat(cls, members: Sequence["OfdmPlan"]) -> "OfdmPlan":
+        """srsgpu_ofdm_plan_concat: one plan running the members' jobs (a sector group): member i's grid words and time
+        samples follow member i-1's."""
+        arr = (ctypes.c_void_p * len(members))(*[m.handle for m in members])
+        h = ctypes.c_void_p()
+        _check(_lib.srsgpu_ofdm_plan_concat(members[0].ctx.handle, ctypes.cast(arr, ctypes.c_void_p), len(members),
+                                             ctypes.byref(h)))
+        self = cls.__new__(cls)
+        self.ctx, self.inverse, self.handle = members[0].ctx, members[0].inverse, h
+        self.nof_grids = sum(m.nof_grids for m in members)
+        self.nof_ports, self.nsymb, self.nsc = members[0].nof_ports, members[0].nsymb, members[0].nsc
+        self.nof_samples = int(_lib.srsgpu_ofdm_plan_nof_samples(h))
+        self.grid_words = int(_lib.srsgpu_ofdm_plan_nof_grid_words(h))
+        return self
 
     def sample_offset(self, grid: int, port: int) -> int:
         return int(_lib.srsgpu_ofdm_plan_sample_offset(self.handle, grid, port))

@@ -10,7 +10,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHAIN_SO = os.path.join(ROOT, "oracle", "_ref", "libsrschain.so")
 _P = ctypes.c_void_p
-REF_CPU, REF_ON_GPU_SYMBOLS, GPU_PROCESSOR = 0, 1, 2
+REF_CPU, REF_ON_GPU_SYMBOLS, GPU_PROCESSOR, GPU_GROUP = 0, 1, 2, 3
 REQUEST, PROCESS = 0, 1
 SENTINEL = np.float32(1e30)
 
@@ -43,13 +43,18 @@ class Lower:
         f = self.lib.ref_lower_puxch_run
         f.restype = ctypes.c_int
         f.argtypes = [ctypes.c_int] * 6 + [ctypes.c_float, ctypes.c_double] + [ctypes.c_int] * 3 + [_P] * 8
+        f = self.lib.ref_lower_sectors_run
+        f.restype = ctypes.c_int
+        f.argtypes = ([ctypes.c_int] * 7 + [ctypes.c_float, _P] + [ctypes.c_int] * 3 + [_P, _P, ctypes.c_int, _P, _P,
+                      ctypes.c_long, _P, ctypes.c_int, _P, _P, ctypes.c_long] + [_P] * 8)
 
-    def pdxch(self, variant, cfg, grids, port_mask, events):
+    def pdxch(self, variant, cfg, grids, port_mask, events, ring=None):
         """cfg: dict numerology, bw_rb, dft_size, extended, center_freq_hz, nof_ports. grids (G, P, nsymb, nsc, 2)
-        uint16. Returns (samples complex64 in event order, processed flags, late slots)."""
+        uint16. Returns (samples complex64 in event order, processed flags, late slots). ring: benchmark mode, the
+        samples go round a reused buffer of that many complex samples (returned as is, not in event order)."""
         ev = np.ascontiguousarray(np.asarray(events, np.int32).reshape(-1, 4))
         nproc = sum(e[3] - e[2] for e in ev if e[0] == PROCESS)
-        cap = int(nproc * cfg["nof_ports"] * (cfg["dft_size"] * 2))
+        cap = int(nproc * cfg["nof_ports"] * (cfg["dft_size"] * 2)) if ring is None else int(ring)
         out = np.zeros(2 * cap, np.float32)
         flags = np.zeros(max(nproc, 1), np.uint8)
         late = np.zeros(len(ev) + 1, np.int32)
@@ -58,10 +63,10 @@ class Lower:
         m = np.ascontiguousarray(port_mask, np.uint32)
         n = self.lib.ref_lower_pdxch_run(variant, cfg["numerology"], cfg["bw_rb"], cfg["dft_size"],
                                          int(cfg["extended"]), cfg["center_freq_hz"], cfg["nof_ports"], g.shape[0],
-                                         _ptr(g), _ptr(m), len(ev), _ptr(ev), _ptr(out), cap, _ptr(flags), _ptr(late),
-                                         ctypes.byref(nlate))
+                                         _ptr(g), _ptr(m), len(ev), _ptr(ev), _ptr(out),
+                                         cap if ring is None else -cap, _ptr(flags), _ptr(late), ctypes.byref(nlate))
         assert n >= 0
-        return out[: 2 * n].view(np.complex64), flags[:nproc], late[: nlate.value].tolist()
+        return out[: 2 * (n if ring is None else cap)].view(np.complex64), flags[:nproc], late[: nlate.value].tolist()
 
     def puxch(self, variant, cfg, nof_grids, events, samples, max_in_flight=2):
         """samples: complex64 of every processed symbol and port in event order. Returns (final grids
@@ -83,3 +88,48 @@ class Lower:
         assert r == 0
         return grids, flags[:nproc], [tuple(v) for v in rx[: 2 * nrx.value].reshape(-1, 2).tolist()], \
             late[: nlate.value].tolist()
+
+    def sectors(self, variant, cfg, freqs, grids, masks, dl_events, ul_events, ul_samples, max_in_flight=0,
+                ring=None, window_us=0):
+        """ref_lower_sectors_run: len(freqs) sectors on their own threads (variant 3: one sector group). grids
+        (S, G, P, nsymb, nsc, 2) uint16 and masks (S, G): each sector's DL grids; ul_samples (S, n) complex64.
+        Returns a dict: per-sector lists dl (samples, flags, late DL+UL mixed in 'late'), ul (grids, flags, rx), late,
+        seconds (S, 2) DL/UL wall time, and group counters (variant 3)."""
+        S = len(freqs)
+        nsymb = 12 if cfg["extended"] else 14
+        P = cfg["nof_ports"]
+        G = grids.shape[1]
+        dl_ev = np.ascontiguousarray(np.asarray(dl_events, np.int32).reshape(-1, 4))
+        ul_ev = np.ascontiguousarray(np.asarray(ul_events, np.int32).reshape(-1, 4))
+        n_dl = sum(e[3] - e[2] for e in dl_ev if e[0] == PROCESS)
+        n_ul = sum(e[3] - e[2] for e in ul_ev if e[0] == PROCESS)
+        cap = int(n_dl * P * (cfg["dft_size"] * 2)) if ring is None else int(ring)
+        dl_out = np.zeros((S, 2 * cap), np.float32)
+        dl_flags = np.zeros((S, max(n_dl, 1)), np.uint8)
+        ul_flags = np.zeros((S, max(n_ul, 1)), np.uint8)
+        ul_grids = np.zeros((S, G, P, nsymb, 12 * cfg["bw_rb"], 2), np.uint16)
+        rx = np.zeros((S, 2 * max(n_ul, 1)), np.int32)
+        nrx = np.zeros(S, np.int32)
+        late = np.zeros((S, len(dl_ev) + len(ul_ev) + 1), np.int32)
+        nlate = np.zeros(S, np.int32)
+        secs = np.zeros((S, 2), np.float64)
+        counts = np.zeros(6, np.uint64)
+        fr = np.ascontiguousarray(freqs, np.float64)
+        g = np.ascontiguousarray(grids, np.uint16)
+        m = np.ascontiguousarray(masks, np.uint32)
+        x = np.ascontiguousarray(ul_samples, np.complex64)
+        r = self.lib.ref_lower_sectors_run(
+            variant, max_in_flight, S, cfg["numerology"], cfg["bw_rb"], cfg["dft_size"], int(cfg["extended"]),
+            cfg["window_offset"], _ptr(fr), P, G, window_us, _ptr(g), _ptr(m), len(dl_ev), _ptr(dl_ev), _ptr(dl_out),
+            cap if ring is None else -cap, _ptr(dl_flags), len(ul_ev), _ptr(ul_ev), _ptr(x), x.shape[1], _ptr(ul_grids),
+            _ptr(ul_flags), _ptr(rx), _ptr(nrx), _ptr(late), _ptr(nlate), _ptr(secs), _ptr(counts))
+        assert r == 0
+        return {
+            "dl": [(dl_out[k].view(np.complex64), dl_flags[k, :n_dl]) for k in range(S)],
+            "ul": [(ul_grids[k], ul_flags[k, :n_ul], [tuple(v) for v in rx[k, : 2 * nrx[k]].reshape(-1, 2).tolist()])
+                   for k in range(S)],
+            "late": [late[k, : nlate[k]].tolist() for k in range(S)],
+            "seconds": secs,
+            "group": dict(zip(("ul_rounds", "ul_grouped", "ul_alone", "dl_rounds", "dl_grouped", "dl_alone"),
+                              counts.tolist())),
+        }

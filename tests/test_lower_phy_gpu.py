@@ -18,7 +18,8 @@ overwritten by one 16 slots later (late), a request processed 16 slots late, par
 import numpy as np
 import pytest
 
-from lower_harness import GPU_PROCESSOR, PROCESS, REF_CPU, REF_ON_GPU_SYMBOLS, REQUEST, SENTINEL, Lower, symbol_size
+from lower_harness import (GPU_GROUP, GPU_PROCESSOR, PROCESS, REF_CPU, REF_ON_GPU_SYMBOLS, REQUEST, SENTINEL, Lower,
+                           symbol_size)
 from ofdm_oracle import bf16_to_complex
 from pusch_demod_cases import bf16
 
@@ -118,3 +119,79 @@ def test_puxch_processor_gpu_equals_reference(lower, name):
         assert np.array_equal(va == 0, vb == 0), what  # the same REs written
         err = np.abs(va - vb)
         assert np.all(err <= np.maximum(2.0 ** -7 * np.abs(va), 1e-4 * rms)), (what, float(np.max(err / rms)))
+
+
+def test_sectors_on_one_gpu_equal_reference(lower):
+    """Several sectors on one GPU, as the reference's radio unit runs them: one lower-PHY sector per cell
+    (lib/ru/generic/ru_factory_generic_impl.cpp:75-90), each driven from its own thread. Every sector's PDxCH and
+    PUxCH GPU processors run concurrently with the others' (own streams, graphs and staging on a shared context) and
+    each equals the reference run alone on that sector's data."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    sectors = [(name, seed) for seed, name in enumerate(sorted(CONFIGS) * 2)]  # 6 sectors, 3 configurations
+    inputs = []
+    for name, seed in sectors:
+        cfg = CONFIGS[name]
+        nsymb = 12 if cfg["extended"] else 14
+        rng = np.random.default_rng(100 + seed)
+        grids, mask = dl_grids(rng, cfg, nsymb)
+        ev_ul = ul_script(nsymb)
+        inputs.append((cfg, grids, mask, dl_script(nsymb), ev_ul, ul_samples(rng, cfg, ev_ul)))
+
+    def run(variant, i):
+        cfg, grids, mask, ev_dl, ev_ul, x = inputs[i]
+        dl = lower.pdxch(variant, cfg, grids, mask, ev_dl)
+        ul = lower.puxch(variant, cfg, 6, ev_ul, x, max_in_flight=0)
+        return dl, ul
+
+    refs = [run(REF_CPU, i) for i in range(len(sectors))]
+    with ThreadPoolExecutor(len(sectors)) as pool:
+        gots = list(pool.map(lambda i: run(GPU_PROCESSOR, i), range(len(sectors))))
+    for (name, _), (rdl, rul), (gdl, gul) in zip(sectors, refs, gots):
+        touched = rdl[0].real != SENTINEL
+        rms = np.sqrt(np.mean(np.abs(rdl[0][touched]) ** 2))
+        assert np.array_equal(gdl[1], rdl[1]) and gdl[2] == rdl[2], name
+        assert np.array_equal(gdl[0].real == SENTINEL, ~touched), name
+        assert np.max(np.abs(gdl[0][touched] - rdl[0][touched])) < 2e-5 * rms, name
+        assert np.array_equal(gul[1], rul[1]) and gul[2] == rul[2] and gul[3] == rul[3], name
+        va, vb = bf16_to_complex(rul[0]), bf16_to_complex(gul[0])
+        rms = np.sqrt(np.mean(np.abs(va[va != 0]) ** 2))
+        assert np.array_equal(va == 0, vb == 0), name
+        assert np.all(np.abs(va - vb) <= np.maximum(2.0 ** -7 * np.abs(va), 1e-4 * rms)), name
+
+
+@pytest.mark.parametrize("name", ["100MHz_30kHz_4port", "10MHz_15kHz_2port"])
+@pytest.mark.parametrize("in_flight", [0, 3])
+def test_sector_group_equals_reference(lower, name, in_flight):
+    """The sector group (lower_phy_sector_group: the same symbol / slot of every sector in one launch): four sectors
+    on their own carrier frequencies and data, driven from their own threads through the edge-case scripts above
+    (missing requests, late and overwritten requests, partial slots, a slot left mid-way, empty grids and ports), each
+    equal to the reference processor run on that sector; and the group did launch shared rounds."""
+    cfg = CONFIGS[name]
+    nsymb = 12 if cfg["extended"] else 14
+    S, G = 4, 8
+    freqs = [cfg["center_freq_hz"] + 1e7 * k for k in range(S)]
+    rng = np.random.default_rng(41)
+    grids, masks = zip(*(dl_grids(rng, cfg, nsymb, G) for _ in range(S)))
+    grids, masks = np.stack(grids), np.stack(masks)
+    ev_dl, ev_ul = dl_script(nsymb), ul_script(nsymb)
+    x = np.stack([ul_samples(rng, cfg, ev_ul) for _ in range(S)])
+    ref = lower.sectors(REF_CPU, cfg, freqs, grids, masks, ev_dl, ev_ul, x)
+    got = lower.sectors(GPU_GROUP, cfg, freqs, grids, masks, ev_dl, ev_ul, x, max_in_flight=in_flight)
+    for k in range(S):
+        (rs, rf), (gs, gf) = ref["dl"][k], got["dl"][k]
+        touched = rs.real != SENTINEL
+        rms = np.sqrt(np.mean(np.abs(rs[touched]) ** 2))
+        assert np.array_equal(gf, rf), k
+        assert np.array_equal(gs.real == SENTINEL, ~touched), k
+        assert np.max(np.abs(gs[touched] - rs[touched])) < 2e-5 * rms, k
+        (rg, rfl, rrx), (gg, gfl, grx) = ref["ul"][k], got["ul"][k]
+        assert np.array_equal(gfl, rfl) and grx == rrx, k
+        assert got["late"][k] == ref["late"][k], k
+        va, vb = bf16_to_complex(rg), bf16_to_complex(gg)
+        rms = np.sqrt(np.mean(np.abs(va[va != 0]) ** 2))
+        assert np.array_equal(va == 0, vb == 0), k
+        assert np.all(np.abs(va - vb) <= np.maximum(2.0 ** -7 * np.abs(va), 1e-4 * rms)), k
+    c = got["group"]
+    assert c["ul_rounds"] > 0 and c["ul_grouped"] > c["ul_alone"], c
+    assert c["dl_rounds"] > 0 and c["dl_grouped"] > c["dl_alone"], c

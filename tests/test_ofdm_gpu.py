@@ -100,3 +100,46 @@ def test_ofdm_rejects_invalid(ctx):
         srsgpu.OfdmPlan(ctx, False, 1, 106, 2048, 1.0, 0.0, [0], 1, window_offset=144)
     with pytest.raises(srsgpu.SrsGpuError):  # slot index beyond the subframe
         srsgpu.OfdmPlan(ctx, True, 1, 106, 2048, 1.0, 0.0, [2], 1)
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_ofdm_plan_concat_sector_group(ctx, inverse):
+    """srsgpu_ofdm_plan_concat (the lower-PHY sector group): three sectors with their own carrier frequency, scaling
+    and symbol position in one plan give, bit for bit, what each sector's own plan gives on its slice of the grids and
+    time samples; members that disagree on the launch-wide parameters are refused."""
+    import torch
+    import srsgpu
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(31)
+    P = 2
+    members = [srsgpu.OfdmPlan(ctx, inverse, 1, 106, 2048, sc, fc, [slot], P, window_offset=0 if inverse else 40,
+                               symbols=(l, 1))
+               for sc, fc, slot, l in ((0.5, 3.5e9, 0, 0), (0.25, 3.6e9, 1, 7), (1.0, 1.8e9, 1, 13))]
+    group = srsgpu.OfdmPlan.concat(members)
+    assert group.grid_words == sum(m.grid_words for m in members)
+    assert group.nof_samples == sum(m.nof_samples for m in members)
+    words = np.cumsum([0] + [m.grid_words for m in members])
+    samples = np.cumsum([0] + [m.nof_samples for m in members])
+    for i, m in enumerate(members):
+        for p in range(P):
+            assert group.sample_offset(i, p) == samples[i] + m.sample_offset(0, p)
+    grids = rng.integers(0, 1 << 14, 2 * group.grid_words).astype(np.uint16).view(np.int32)
+    x = (rng.normal(size=2 * group.nof_samples) * 0.1).astype(np.float32)
+    src = torch.from_numpy(grids.copy() if inverse else x.copy()).to(dev)
+    out = (torch.zeros(2 * group.nof_samples, dtype=torch.float32, device=dev) if inverse
+           else torch.zeros(group.grid_words, dtype=torch.int32, device=dev))
+    group.execute(src, out)
+    for i, m in enumerate(members):
+        if inverse:
+            s_in = src[words[i]:words[i + 1]].clone()
+            o = torch.zeros(2 * m.nof_samples, dtype=torch.float32, device=dev)
+            m.execute(s_in, o)
+            assert torch.equal(o, out[2 * samples[i]:2 * samples[i + 1]]), i
+        else:
+            s_in = src[2 * samples[i]:2 * samples[i + 1]].clone()
+            o = torch.zeros(m.grid_words, dtype=torch.int32, device=dev)
+            m.execute(s_in, o)
+            assert torch.equal(o, out[words[i]:words[i + 1]]), i
+    odd = srsgpu.OfdmPlan(ctx, inverse, 1, 52, 2048, 1.0, 3.5e9, [0], P, symbols=(0, 1))
+    with pytest.raises(srsgpu.SrsGpuError):
+        srsgpu.OfdmPlan.concat([members[0], odd])

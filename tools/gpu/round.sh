@@ -12,7 +12,8 @@
 #   slots_trace16    the same at 16 threads
 #   slots_trace      rocprofv3 kernel + memory-copy trace of the slot processors at one thread (UL)
 #   kstats           rocprofv3 --kernel-trace --stats of the default bench
-#   lower            tools/lower_phy_bench.py
+#   lower            tools/lower_phy_bench.py with the multi-sector sweep
+#   lower_trace      rocprofv3 kernel + memory-copy trace of the GPU processors at 8 sectors
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -60,9 +61,13 @@ for step in "$@"; do
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kstats" -o k -- python3 -u bench.py \
         > "$OUT/kstats_bench.json" 2> "$OUT/kstats.log" || { tail -20 "$OUT/kstats.log"; exit 1; } ;;
     lower)
-      timeout -k 10 300 python -u tools/lower_phy_bench.py > "$OUT/lower.json" 2> "$OUT/lower.log" \
+      timeout -k 10 400 python -u tools/lower_phy_bench.py --sectors 1,2,4,8,16 > "$OUT/lower.json" 2> "$OUT/lower.log" \
         || { tail -20 "$OUT/lower.log"; exit 1; }
       tail -c 800 "$OUT/lower.json" ;;
+    lower_trace)
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/lower_trace" -o lower -- python3 -u \
+        tools/lower_phy_bench.py --slots 100 --sectors 8 --sweep-only group4 > "$OUT/lower_trace.json" \
+        2> "$OUT/lower_trace.log" || { tail -20 "$OUT/lower_trace.log"; exit 1; } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

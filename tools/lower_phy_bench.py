@@ -4,8 +4,16 @@ puxch_processor_impl (CPU OFDM objects, built from source by oracle/build_chain.
 integration/lower_phy_gpu.cpp, one sector, 100 MHz 30 kHz 4 ports. The DL script requests slot s + 2 before the lower
 PHY processes every symbol of slot s (the radio unit's processing delay); the UL script requests slot s and delivers
 its 14 symbols. Times the whole scenario call (the harness's per-symbol sample copies included for both variants) and
-prints one JSON object; real time is 2 000 slots/s per sector. TEST INFRASTRUCTURE (diagnostic); GPU box:
-    python tools/lower_phy_bench.py [--slots N]
+prints one JSON object; real time is 2 000 slots/s per sector.
+
+--sectors S1,S2,...: the multi-sector sweep. S sectors share one GPU the way the reference's radio unit runs them
+(one lower-PHY sector per cell, each driven by its own thread: lib/ru/generic/ru_factory_generic_impl.cpp:75-90): S
+C++ threads (oracle/ref/ref_lower.cpp ref_lower_sectors_run) run the DL script together on their own processors, then
+the UL script together; reported per S are the aggregate slots/s, the slowest sector's slots/s and whether every
+sector kept real time, for the reference CPU processors (host cores, up to --cpu-threads), the GPU processors one per
+sector, and the GPU processors of one lower_phy_sector_group (one launch per symbol / slot for all sectors).
+TEST INFRASTRUCTURE (diagnostic); GPU box:
+    python tools/lower_phy_bench.py [--slots N] [--sectors 1,2,4,8,16]
 """
 import argparse
 import json
@@ -28,6 +36,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--slots", type=int, default=200)
     ap.add_argument("--grids", type=int, default=8)
+    ap.add_argument("--sectors", default="", help="comma-separated sector counts for the multi-sector sweep")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="largest sector count for the reference CPU sweep")
+    ap.add_argument("--sweep-only", default="", help="sweep only: comma list of cpu, gpu0, gpu4, group0, group4 "
+                                                    "(default cpu,gpu4,group0,group4 after the single-sector runs)")
     args = ap.parse_args()
     rng = np.random.default_rng(3)
     lower = LH.Lower()
@@ -49,7 +61,8 @@ def main():
             for e in ul if e[0] == LH.PROCESS for l in range(e[2], e[3]))
     samples = ((rng.normal(size=n) + 1j * rng.normal(size=n)) * 0.05).astype(np.complex64)
     out = {"config": dict(CFG, slots=S), "pdxch": {}, "puxch": {}}
-    for name, variant in (("reference CPU processor", LH.REF_CPU), ("GPU processor", LH.GPU_PROCESSOR)):
+    single = (("reference CPU processor", LH.REF_CPU), ("GPU processor", LH.GPU_PROCESSOR))
+    for name, variant in () if args.sweep_only else single:
         lower.pdxch(variant, CFG, grids, mask, dl[:8])  # warm-up: plans, DFT tables
         t0 = time.perf_counter()
         _, flags, late = lower.pdxch(variant, CFG, grids, mask, dl)
@@ -63,7 +76,52 @@ def main():
             t = time.perf_counter() - t0
             out["puxch"][key] = {"seconds": t, "slots_per_s": S / t, "late": len(late), "notifications": len(rx)}
             print(json.dumps({key: out["puxch"][key]}), file=sys.stderr, flush=True)
+    if args.sectors:
+        out["sectors"] = sweep(lower, args, grids, mask, dl, ul, samples)
     print(json.dumps(out))
+
+
+REAL_TIME = 2000.0  # slots/s of one 30 kHz sector
+RING = 2 * 4 * 14 * (4096 + 352)  # DL baseband ring of the sweep: two slots of 4 ports (complex samples)
+
+
+def sweep(lower, args, grids, mask, dl, ul, samples):
+    """ref_lower_sectors_run: S sectors on their own C++ threads, all running the DL script together and then the UL
+    script together; the sectors' carriers 20 MHz apart, each with its own copy of the grids and samples."""
+    S, G = args.slots, args.grids
+    res = {}
+    runs = {"cpu": ("reference CPU processor", LH.REF_CPU, 0),
+            "gpu0": ("GPU processor", LH.GPU_PROCESSOR, 0), "gpu4": ("GPU processor", LH.GPU_PROCESSOR, 4),
+            "group0": ("GPU sector group", LH.GPU_GROUP, 0), "group4": ("GPU sector group", LH.GPU_GROUP, 4)}
+    runs = [runs[k] for k in (args.sweep_only or "cpu,gpu4,group0,group4").split(",")]
+    for name, variant, inflight in runs:
+        key = name if variant == LH.REF_CPU else f"{name}, {inflight} symbols in flight"
+        res[key] = {}
+        for nsec in (int(v) for v in args.sectors.split(",")):
+            if variant == LH.REF_CPU and nsec > args.cpu_threads:
+                continue
+            freqs = [CFG["center_freq_hz"] + 2e7 * k for k in range(nsec)]
+            g = np.broadcast_to(grids, (nsec,) + grids.shape)
+            m = np.broadcast_to(mask, (nsec,) + mask.shape)
+            x = np.broadcast_to(samples, (nsec,) + samples.shape)
+            lower.sectors(variant, CFG, freqs, g, m, dl[:8], ul[:4], x, inflight, ring=RING)  # warm-up
+            t0 = time.perf_counter()
+            r = lower.sectors(variant, CFG, freqs, g, m, dl, ul, x, inflight, ring=RING)
+            wall = time.perf_counter() - t0
+            sec = r["seconds"]
+            dl_min, ul_min = S / sec[:, 0].max(), S / sec[:, 1].max()
+            res[key][str(nsec)] = {
+                "wall_s": wall, "pdxch_slowest_sector_slots_per_s": dl_min, "puxch_slowest_sector_slots_per_s": ul_min,
+                "pdxch_aggregate_slots_per_s": nsec * S / sec[:, 0].max(),
+                "puxch_aggregate_slots_per_s": nsec * S / sec[:, 1].max(),
+                "late": sum(len(v) for v in r["late"]), "notifications": sum(len(u[2]) for u in r["ul"]),
+                "real_time": bool(dl_min >= REAL_TIME and ul_min >= REAL_TIME)}
+            if variant == LH.GPU_GROUP:
+                res[key][str(nsec)]["group"] = r["group"]
+            print(json.dumps({key: {nsec: res[key][str(nsec)]}}), file=sys.stderr, flush=True)
+        rt = [int(k) for k, v in res[key].items() if v["real_time"]]
+        res[key]["sectors_at_real_time"] = max(rt) if rt else 0
+    return res
 
 
 if __name__ == "__main__":

@@ -153,11 +153,13 @@ public:
     all((nof_sectors_ >= 32) ? ~0u : ((1u << nof_sectors_) - 1)),
     period(period_),
     window(window_),
-    stream(ctx_, who_),
     members(nof_sectors_)
   {
+    for (auto& st : streams) {
+      st = std::make_unique<gpu::owned_stream>(ctx_, who_);
+    }
     for (unsigned r = 0; r != nof_rounds; ++r) {
-      rounds.emplace_back(std::make_unique<round>(who));
+      rounds.emplace_back(std::make_unique<round>(who, r));
     }
     dispatcher = std::thread([this]() { dispatch_loop(); });
   }
@@ -170,7 +172,9 @@ public:
     }
     dispatch_cv.notify_all();
     dispatcher.join();
-    (void)hipStreamSynchronize(stream.get());
+    for (auto& st : streams) {
+      (void)hipStreamSynchronize(st->get());
+    }
     std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());
     for (auto& rd : rounds) {
       if (rd->graph != nullptr) {
@@ -310,7 +314,8 @@ public:
 
 private:
   struct round {
-    explicit round(const char* w) : in(w), out(w) {}
+    round(const char* w, unsigned i) : index(i), in(w), out(w) {}
+    unsigned            index;
     uint64_t            key       = UINT64_MAX;
     uint32_t            arrived   = 0;  ///< sectors that reached the round (present or absent; gone ones count)
     uint32_t            present   = 0;  ///< sectors with input in the round
@@ -336,9 +341,11 @@ private:
     if (rd.present == 0) {
       return;
     }
+    // Consecutive rounds on different streams: one round's download overlaps the next one's upload and OFDM launch.
     gpu::device_scope dev(ctx, who);
-    gpu::hip_check(hipGraphLaunch(rd.graph, stream.get()), who, "graph launch");
-    gpu::hip_check(hipEventRecord(rd.done, stream.get()), who, "event");
+    hipStream_t       hs = streams[rd.index % streams.size()]->get();
+    gpu::hip_check(hipGraphLaunch(rd.graph, hs), who, "graph launch");
+    gpu::hip_check(hipEventRecord(rd.done, hs), who, "event");
     rd.launched = true;
     ++launches;
     launched_cv.notify_all();
@@ -406,7 +413,7 @@ private:
       in_bytes[pos]             = inverse ? grid_bytes : sample_bytes;
       out_bytes[pos]            = inverse ? sample_bytes : grid_bytes;
     }
-    hipStream_t hs = stream.get();
+    hipStream_t hs = streams[0]->get();
     for (unsigned r = 0; r != rounds.size(); ++r) {
       round&         rd  = *rounds[r];
       const unsigned pos = r % period;
@@ -437,7 +444,7 @@ private:
   uint32_t                                     all;
   unsigned                                     period;
   std::chrono::microseconds                    window;
-  gpu::owned_stream                            stream;
+  std::array<std::unique_ptr<gpu::owned_stream>, 3> streams;
   std::vector<std::vector<srsgpu_ofdm_plan*>>  members;
   std::vector<srsgpu_ofdm_plan*>               plans;    ///< per position: every sector's plan concatenated
   std::vector<std::vector<size_t>>             in_off;   ///< per position and sector: byte offset of its input

@@ -29,6 +29,8 @@
 #include "srsran/phy/support/resource_grid_reader.h"
 #include "srsran/phy/support/resource_grid_writer.h"
 
+#include <algorithm>
+#include <array>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -215,6 +217,35 @@ void fill_pool(harness_pool& pool, const scenario& sc, int nof_grids, const uint
   }
 }
 
+/// Real-time pacing of a script: symbol i of the script may start at start + i x period (the radio delivers / wants a
+/// symbol every period); max_lag: the latest a symbol started behind that time (a sector that cannot keep up falls
+/// further behind symbol after symbol). period 0: free-running.
+struct pacer {
+  using clock = std::chrono::steady_clock;
+  clock::time_point start;
+  clock::duration   period{0};
+  double            max_lag = 0;
+  long              i       = 0;
+
+  void next()
+  {
+    if (period.count() == 0) {
+      return;
+    }
+    const clock::time_point due = start + period * i++;
+    clock::time_point       now = clock::now();
+    if (now < due) {
+      if (due - now > std::chrono::microseconds(60)) {
+        std::this_thread::sleep_until(due - std::chrono::microseconds(50));
+      }
+      while (clock::now() < due) {
+      }
+    } else {
+      max_lag = std::max(max_lag, std::chrono::duration<double>(now - due).count());
+    }
+  }
+};
+
 /// The DL script (see ref_lower_pdxch_run). Returns the number of samples produced, -1 when they overflow samples_cap.
 long run_pdxch_script(pdxch_processor&  proc,
                       harness_pool&     pool,
@@ -223,7 +254,8 @@ long run_pdxch_script(pdxch_processor&  proc,
                       const int*        events,
                       float*            samples_out,
                       long              samples_cap,
-                      uint8_t*          processed_out)
+                      uint8_t*          processed_out,
+                      pacer*            pace = nullptr)
 {
   long        pos   = 0;
   size_t      nflag = 0;
@@ -256,6 +288,9 @@ long run_pdxch_script(pdxch_processor&  proc,
         buf.ch.emplace_back(dst, n);
       }
       pdxch_processor_baseband::symbol_context ctx{slot, 0, static_cast<unsigned>(l)};
+      if (pace != nullptr) {
+        pace->next();
+      }
       processed_out[nflag++] = proc.get_baseband().process_symbol(buf, ctx) ? 1 : 0;
       pos += need;
     }
@@ -270,7 +305,8 @@ void run_puxch_script(puxch_processor& proc,
                       int              nof_events,
                       const int*       events,
                       const float*     samples_in,
-                      uint8_t*         processed_out)
+                      uint8_t*         processed_out,
+                      pacer*           pace = nullptr)
 {
   long        pos   = 0;
   size_t      nflag = 0;
@@ -289,6 +325,9 @@ void run_puxch_script(puxch_processor& proc,
         buf.ch.emplace_back(reinterpret_cast<const cf_t*>(samples_in) + pos + static_cast<long>(p) * n, n);
       }
       lower_phy_rx_symbol_context ctx{slot, 0, static_cast<unsigned>(l)};
+      if (pace != nullptr) {
+        pace->next();
+      }
       processed_out[nflag++] = proc.get_baseband().process_symbol(buf, ctx) ? 1 : 0;
       pos += static_cast<long>(n) * sc.nof_ports;
     }
@@ -427,7 +466,10 @@ int ref_lower_puxch_run(int          variant,
 /// 0 = defaults). Outputs per sector k at k x the stride of one sector: DL samples (dl_cap < 0: a ring per sector, as
 /// ref_lower_pdxch_run), DL and UL return flags, UL grids, UL notifications (nof_rx[k] pairs) and late slots
 /// (nof_late[k], DL then UL); seconds[2k], seconds[2k+1]: the sector's DL and UL script wall time. group_counts (6
-/// values, variant 3): lower_phy_group_counters. Returns 0, -1 on a sample overflow.
+/// values, variant 3): lower_phy_group_counters. paced != 0: every sector runs at the radio's pace, one symbol per
+/// symbol duration (1 ms / symbols per subframe) from a common start, and lag[2k], lag[2k+1] report the latest a DL / UL
+/// symbol of sector k started behind its time (a sector keeps real time when that stays bounded). Returns 0, -1 on a
+/// sample overflow.
 int ref_lower_sectors_run(int             variant,
                           int             max_in_flight,
                           int             nof_sectors,
@@ -458,7 +500,9 @@ int ref_lower_sectors_run(int             variant,
                           int*            late_out,
                           int*            nof_late,
                           double*         seconds,
-                          uint64_t*       group_counts)
+                          uint64_t*       group_counts,
+                          int             paced,
+                          double*         lag)
 {
   const scenario sc{numerology,        bw_rb,    dft_size, cp_extended ? cyclic_prefix::EXTENDED : cyclic_prefix::NORMAL,
                     dft_window_offset, nof_ports};
@@ -501,19 +545,37 @@ int ref_lower_sectors_run(int             variant,
   barrier                  meet(static_cast<unsigned>(nof_sectors));
   std::vector<long>        produced(nof_sectors, 0);
   std::vector<std::thread> threads;
+  using clock = std::chrono::steady_clock;
+  const clock::duration period =
+      paced != 0 ? std::chrono::duration_cast<clock::duration>(std::chrono::nanoseconds(
+                       1000000 / (sc.nsymb() * get_nof_slots_per_subframe(sc.scs()))))
+                 : clock::duration(0);
+  std::array<clock::time_point, 2> start;
   for (int k = 0; k < nof_sectors; ++k) {
     threads.emplace_back([&, k]() {
-      using clock = std::chrono::steady_clock;
+      pacer pdl, pul;
+      pdl.period = pul.period = period;
+      if (k == 0) {
+        start[0] = clock::now() + std::chrono::milliseconds(1);
+      }
       meet.wait();
+      pdl.start   = start[0];
       auto t0     = clock::now();
       produced[k] = run_pdxch_script(*dl[k], *dl_pools[k], sc, nof_dl_events, dl_events, dl_samples_out + k * dl_stride,
-                                     dl_cap, dl_processed + static_cast<size_t>(k) * n_dl_proc);
+                                     dl_cap, dl_processed + static_cast<size_t>(k) * n_dl_proc, &pdl);
       seconds[2 * k] = std::chrono::duration<double>(clock::now() - t0).count();
       meet.wait();
-      t0 = clock::now();
+      if (k == 0) {
+        start[1] = clock::now() + std::chrono::milliseconds(1);
+      }
+      meet.wait();
+      pul.start = start[1];
+      t0        = clock::now();
       run_puxch_script(*ul[k], *ul_pools[k], sc, nof_ul_events, ul_events, ul_samples + 2 * k * ul_stride,
-                       ul_processed + static_cast<size_t>(k) * n_ul_proc);
+                       ul_processed + static_cast<size_t>(k) * n_ul_proc, &pul);
       seconds[2 * k + 1] = std::chrono::duration<double>(clock::now() - t0).count();
+      lag[2 * k]         = pdl.max_lag;
+      lag[2 * k + 1]     = pul.max_lag;
     });
   }
   for (std::thread& t : threads) {

@@ -46,7 +46,7 @@ class Lower:
         f = self.lib.ref_lower_sectors_run
         f.restype = ctypes.c_int
         f.argtypes = ([ctypes.c_int] * 7 + [ctypes.c_float, _P] + [ctypes.c_int] * 3 + [_P, _P, ctypes.c_int, _P, _P,
-                      ctypes.c_long, _P, ctypes.c_int, _P, _P, ctypes.c_long] + [_P] * 8)
+                      ctypes.c_long, _P, ctypes.c_int, _P, _P, ctypes.c_long] + [_P] * 8 + [ctypes.c_int, _P])
 
     def pdxch(self, variant, cfg, grids, port_mask, events, ring=None):
         """cfg: dict numerology, bw_rb, dft_size, extended, center_freq_hz, nof_ports. grids (G, P, nsymb, nsc, 2)
@@ -90,11 +90,12 @@ class Lower:
             late[: nlate.value].tolist()
 
     def sectors(self, variant, cfg, freqs, grids, masks, dl_events, ul_events, ul_samples, max_in_flight=0,
-                ring=None, window_us=0):
+                ring=None, window_us=0, paced=False):
         """ref_lower_sectors_run: len(freqs) sectors on their own threads (variant 3: one sector group). grids
         (S, G, P, nsymb, nsc, 2) uint16 and masks (S, G): each sector's DL grids; ul_samples (S, n) complex64.
         Returns a dict: per-sector lists dl (samples, flags, late DL+UL mixed in 'late'), ul (grids, flags, rx), late,
-        seconds (S, 2) DL/UL wall time, and group counters (variant 3)."""
+        seconds (S, 2) DL/UL wall time, group counters (variant 3) and, paced (one symbol per symbol duration), lag
+        (S, 2): the latest a DL / UL symbol started behind its time."""
         S = len(freqs)
         nsymb = 12 if cfg["extended"] else 14
         P = cfg["nof_ports"]
@@ -114,6 +115,7 @@ class Lower:
         nlate = np.zeros(S, np.int32)
         secs = np.zeros((S, 2), np.float64)
         counts = np.zeros(6, np.uint64)
+        lag = np.zeros((S, 2), np.float64)
         fr = np.ascontiguousarray(freqs, np.float64)
         g = np.ascontiguousarray(grids, np.uint16)
         m = np.ascontiguousarray(masks, np.uint32)
@@ -122,7 +124,8 @@ class Lower:
             variant, max_in_flight, S, cfg["numerology"], cfg["bw_rb"], cfg["dft_size"], int(cfg["extended"]),
             cfg["window_offset"], _ptr(fr), P, G, window_us, _ptr(g), _ptr(m), len(dl_ev), _ptr(dl_ev), _ptr(dl_out),
             cap if ring is None else -cap, _ptr(dl_flags), len(ul_ev), _ptr(ul_ev), _ptr(x), x.shape[1], _ptr(ul_grids),
-            _ptr(ul_flags), _ptr(rx), _ptr(nrx), _ptr(late), _ptr(nlate), _ptr(secs), _ptr(counts))
+            _ptr(ul_flags), _ptr(rx), _ptr(nrx), _ptr(late), _ptr(nlate), _ptr(secs), _ptr(counts), int(paced),
+            _ptr(lag))
         assert r == 0
         return {
             "dl": [(dl_out[k].view(np.complex64), dl_flags[k, :n_dl]) for k in range(S)],
@@ -130,6 +133,7 @@ class Lower:
                    for k in range(S)],
             "late": [late[k, : nlate[k]].tolist() for k in range(S)],
             "seconds": secs,
+            "lag": lag,
             "group": dict(zip(("ul_rounds", "ul_grouped", "ul_alone", "dl_rounds", "dl_grouped", "dl_alone"),
                               counts.tolist())),
         }

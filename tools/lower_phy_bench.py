@@ -9,8 +9,9 @@ prints one JSON object; real time is 2 000 slots/s per sector.
 --sectors S1,S2,...: the multi-sector sweep. S sectors share one GPU the way the reference's radio unit runs them
 (one lower-PHY sector per cell, each driven by its own thread: lib/ru/generic/ru_factory_generic_impl.cpp:75-90): S
 C++ threads (oracle/ref/ref_lower.cpp ref_lower_sectors_run) run the DL script together on their own processors, then
-the UL script together; reported per S are the aggregate slots/s, the slowest sector's slots/s and whether every
-sector kept real time, for the reference CPU processors (host cores, up to --cpu-threads), the GPU processors one per
+the UL script together; reported per S are the free-running aggregate slots/s and the slowest sector's slots/s,
+then, paced at the radio's symbol rate from a common start, each direction's largest lag behind that pace (real time:
+under one slot), for the reference CPU processors (host cores, up to --cpu-threads), the GPU processors one per
 sector, and the GPU processors of one lower_phy_sector_group (one launch per symbol / slot for all sectors).
 TEST INFRASTRUCTURE (diagnostic); GPU box:
     python tools/lower_phy_bench.py [--slots N] [--sectors 1,2,4,8,16]
@@ -38,8 +39,8 @@ def main():
     ap.add_argument("--grids", type=int, default=8)
     ap.add_argument("--sectors", default="", help="comma-separated sector counts for the multi-sector sweep")
     ap.add_argument("--cpu-threads", type=int, default=16, help="largest sector count for the reference CPU sweep")
-    ap.add_argument("--sweep-only", default="", help="sweep only: comma list of cpu, gpu0, gpu4, group0, group4 "
-                                                    "(default cpu,gpu4,group0,group4 after the single-sector runs)")
+    ap.add_argument("--sweep-only", default="", help="sweep only: comma list of cpu, gpu0, gpu4, gpu13, group0, "
+                                                    "group4, group13 (default all, after the single-sector runs)")
     args = ap.parse_args()
     rng = np.random.default_rng(3)
     lower = LH.Lower()
@@ -81,7 +82,7 @@ def main():
     print(json.dumps(out))
 
 
-REAL_TIME = 2000.0  # slots/s of one 30 kHz sector
+MAX_LAG = 0.5e-3  # a paced sector keeps real time while no symbol starts more than one slot behind its time
 RING = 2 * 4 * 14 * (4096 + 352)  # DL baseband ring of the sweep: two slots of 4 ports (complex samples)
 
 
@@ -92,8 +93,10 @@ def sweep(lower, args, grids, mask, dl, ul, samples):
     res = {}
     runs = {"cpu": ("reference CPU processor", LH.REF_CPU, 0),
             "gpu0": ("GPU processor", LH.GPU_PROCESSOR, 0), "gpu4": ("GPU processor", LH.GPU_PROCESSOR, 4),
-            "group0": ("GPU sector group", LH.GPU_GROUP, 0), "group4": ("GPU sector group", LH.GPU_GROUP, 4)}
-    runs = [runs[k] for k in (args.sweep_only or "cpu,gpu4,group0,group4").split(",")]
+            "gpu13": ("GPU processor", LH.GPU_PROCESSOR, 13),
+            "group0": ("GPU sector group", LH.GPU_GROUP, 0), "group4": ("GPU sector group", LH.GPU_GROUP, 4),
+            "group13": ("GPU sector group", LH.GPU_GROUP, 13)}
+    runs = [runs[k] for k in (args.sweep_only or "cpu,gpu0,gpu4,gpu13,group0,group4,group13").split(",")]
     for name, variant, inflight in runs:
         key = name if variant == LH.REF_CPU else f"{name}, {inflight} symbols in flight"
         res[key] = {}
@@ -105,17 +108,24 @@ def sweep(lower, args, grids, mask, dl, ul, samples):
             m = np.broadcast_to(mask, (nsec,) + mask.shape)
             x = np.broadcast_to(samples, (nsec,) + samples.shape)
             lower.sectors(variant, CFG, freqs, g, m, dl[:8], ul[:4], x, inflight, ring=RING)  # warm-up
-            t0 = time.perf_counter()
             r = lower.sectors(variant, CFG, freqs, g, m, dl, ul, x, inflight, ring=RING)
-            wall = time.perf_counter() - t0
             sec = r["seconds"]
-            dl_min, ul_min = S / sec[:, 0].max(), S / sec[:, 1].max()
+            # Paced: every sector at the radio's symbol rate from a common start; it keeps real time when no symbol
+            # starts more than one slot (0.5 ms) behind its time.
+            p = lower.sectors(variant, CFG, freqs, g, m, dl, ul, x, inflight, ring=RING, paced=True)
+            lag = p["lag"]
             res[key][str(nsec)] = {
-                "wall_s": wall, "pdxch_slowest_sector_slots_per_s": dl_min, "puxch_slowest_sector_slots_per_s": ul_min,
-                "pdxch_aggregate_slots_per_s": nsec * S / sec[:, 0].max(),
-                "puxch_aggregate_slots_per_s": nsec * S / sec[:, 1].max(),
-                "late": sum(len(v) for v in r["late"]), "notifications": sum(len(u[2]) for u in r["ul"]),
-                "real_time": bool(dl_min >= REAL_TIME and ul_min >= REAL_TIME)}
+                "free_running": {
+                    "pdxch_slowest_sector_slots_per_s": S / sec[:, 0].max(),
+                    "puxch_slowest_sector_slots_per_s": S / sec[:, 1].max(),
+                    "pdxch_aggregate_slots_per_s": nsec * S / sec[:, 0].max(),
+                    "puxch_aggregate_slots_per_s": nsec * S / sec[:, 1].max()},
+                "paced_max_lag_us": {"pdxch": 1e6 * lag[:, 0].max(), "puxch": 1e6 * lag[:, 1].max()},
+                "late": sum(len(v) for v in r["late"]) + sum(len(v) for v in p["late"]),
+                "notifications": sum(len(u[2]) for u in p["ul"]),
+                "real_time": bool(lag.max() < MAX_LAG)}
+            if variant == LH.GPU_GROUP:
+                res[key][str(nsec)]["group_paced"] = p["group"]
             if variant == LH.GPU_GROUP:
                 res[key][str(nsec)]["group"] = r["group"]
             print(json.dumps({key: {nsec: res[key][str(nsec)]}}), file=sys.stderr, flush=True)

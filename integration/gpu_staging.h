@@ -81,6 +81,61 @@ private:
   size_t      cap = 0;
 };
 
+/// Pinned host memory the GPU reads and writes in place (fine-grained, mapped): zero-copy staging. A kernel that reads
+/// its input from here and writes its output here replaces an upload, the kernel and a download; below a few MB the
+/// DMA engines' copies cost far more than the PCIe transfer itself (profiles/r5_pcie_probe.txt: a 142 KB
+/// hipMemcpyAsync takes ~70 us, a kernel reads it in place in ~5 us).
+class mapped_buffer
+{
+public:
+  explicit mapped_buffer(const char* who_) : who(who_) {}
+  mapped_buffer(const mapped_buffer&)            = delete;
+  mapped_buffer& operator=(const mapped_buffer&) = delete;
+  ~mapped_buffer()
+  {
+    if (h != nullptr) {
+      std::lock_guard<std::recursive_mutex> lock(hip_setup_mutex());
+      (void)hipHostFree(h);
+    }
+  }
+
+  /// Makes room for n bytes (contents are not preserved when it grows).
+  void reserve(size_t n)
+  {
+    if (n <= cap) {
+      return;
+    }
+    std::lock_guard<std::recursive_mutex> lock(hip_setup_mutex());
+    const size_t                          c = std::max(n, 2 * cap);
+    (void)hipHostFree(h);
+    h   = nullptr;
+    d   = nullptr;
+    cap = 0;
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&h), c, hipHostMallocCoherent | hipHostMallocMapped), who,
+              "mapped staging");
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0), who, "mapped device pointer");
+    cap = c;
+  }
+
+  template <typename T = uint8_t>
+  T* host(size_t byte_offset = 0)
+  {
+    return reinterpret_cast<T*>(h + byte_offset);
+  }
+  /// The same bytes as the GPU addresses them.
+  template <typename T = uint8_t>
+  T* dev(size_t byte_offset = 0)
+  {
+    return reinterpret_cast<T*>(d + byte_offset);
+  }
+
+private:
+  const char* who;
+  uint8_t*    h   = nullptr;
+  uint8_t*    d   = nullptr;
+  size_t      cap = 0;
+};
+
 /// Appends the bytes of a POD value to a cache key.
 template <typename T>
 void key_append(std::vector<uint8_t>& key, const T& v)

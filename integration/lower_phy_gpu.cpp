@@ -10,18 +10,22 @@
 // and symbol from the real-time baseband thread. On the GPU a symbol of one port is far too small a launch, so:
 //
 //  * PDxCH (downlink): the whole slot is modulated when the upper PHY hands the grid over (handle_request): every
-//    non-empty port's 14 grid rows go up, one launch modulates all ports and symbols, the samples come back into a
-//    pinned buffer of the request, all asynchronously on the processor's stream. process_symbol() only waits for that
-//    slot's event at its first symbol (long finished: requests arrive max_processing_delay slots ahead) and copies
-//    the symbol's CP + N samples of every port. The request bookkeeping (one entry per slot modulo 16, the late-request
-//    notifications, empty grids discarded) is the reference's.
+//    non-empty port's 14 grid rows are staged in mapped host memory, one launch modulates all ports and symbols
+//    reading them in place and writes the samples in place into mapped memory of the request, asynchronously on the
+//    processor's stream (zero-copy: below a few MB a DMA copy costs several times the PCIe transfer). process_symbol()
+//    only waits for that slot's event at its first symbol (long finished: requests arrive max_processing_delay slots
+//    ahead) and copies the symbol's CP + N samples of every port. The request bookkeeping (one entry per slot modulo
+//    16, the late-request notifications, empty grids discarded) is the reference's.
 //
 //  * PUxCH (uplink): the symbols arrive one by one. process_symbol() stages the symbol's samples of every port into
-//    pinned memory and launches its demodulation (one plan per symbol of the subframe, all ports) without waiting.
+//    mapped memory and launches its demodulation (one plan per symbol of the subframe, all ports) without waiting.
 //    Symbols whose demodulation has finished are written into the request's grid and notified (on_rx_symbol) in
 //    order; at most `max_symbols_in_flight` are outstanding (0: every symbol is demodulated and notified before
 //    process_symbol returns, the reference's timing), and the slot's last symbol drains everything, so every symbol of
 //    a slot is notified, in order, before the slot's last process_symbol() returns.
+//
+//  * Sector group (lower_phy_sector_group, optional): the processors of several sectors on one GPU share launches:
+//    the same UL symbol / DL slot of every sector runs as one OFDM launch over the sectors' plans concatenated.
 #include "signal_chain_gpu.h"
 
 #include "batch_graph.h"
@@ -134,11 +138,11 @@ srsgpu_ofdm_config ofdm_config(subcarrier_spacing scs, cyclic_prefix cp, unsigne
 // ---------------------------------------------------------------------------------------------------------------------
 
 /// One direction of a sector group. A round is the work of every sector at one position (UL: a symbol, key = system
-/// slot x symbols per slot + symbol; DL: a slot, key = system slot), run as one captured graph on the group's stream:
-/// upload of the round's input region (all sectors), the OFDM launch of the sectors' plans concatenated
-/// (srsgpu_ofdm_plan_concat), download of the output region. Rounds sit in a ring of a whole number of periods (a
-/// subframe's symbols or slots), so a ring entry always serves the same position and owns one graph over its own
-/// pinned and device buffers.
+/// slot x symbols per slot + symbol; DL: a slot, key = system slot), run as one OFDM launch of the sectors' plans
+/// concatenated (srsgpu_ofdm_plan_concat) that reads the round's input region (all sectors) from mapped host memory
+/// and writes its output region there (zero-copy: no DMA copy on the path). Rounds sit in a ring of a whole number of
+/// periods (a subframe's symbols or slots), so a ring entry always serves the same position and owns one captured
+/// launch over its own buffers; consecutive rounds go to different streams.
 class sector_rounds
 {
 public:
@@ -324,8 +328,8 @@ private:
     bool                closed    = false;  ///< no more sectors join (launched, or nothing to launch)
     bool                launched  = false;
     clock::time_point   first;
-    gpu::staged_buffer  in;
-    gpu::staged_buffer  out;
+    gpu::mapped_buffer  in;   ///< every sector's input, read in place by the OFDM kernel
+    gpu::mapped_buffer  out;  ///< every sector's output, written in place
     hipEvent_t          done  = nullptr;
     hipGraphExec_t      graph = nullptr;
   };
@@ -341,7 +345,7 @@ private:
     if (rd.present == 0) {
       return;
     }
-    // Consecutive rounds on different streams: one round's download overlaps the next one's upload and OFDM launch.
+    // Consecutive rounds on different streams: a round still reading / writing host memory does not hold the next.
     gpu::device_scope dev(ctx, who);
     hipStream_t       hs = streams[rd.index % streams.size()]->get();
     gpu::hip_check(hipGraphLaunch(rd.graph, hs), who, "graph launch");
@@ -400,7 +404,7 @@ private:
     plans = cat;
     in_off.assign(period, std::vector<size_t>(nof_sectors));
     out_off.assign(period, std::vector<size_t>(nof_sectors));
-    std::vector<size_t> in_bytes(period), out_bytes(period);
+    std::vector<size_t> in_bytes(period), out_bytes(period);  // per position
     for (unsigned pos = 0; pos != period; ++pos) {
       const size_t words = srsgpu_ofdm_plan_nof_grid_words(plans[pos]) / nof_sectors;  // equal per sector
       for (unsigned k = 0; k != nof_sectors; ++k) {
@@ -421,7 +425,6 @@ private:
       rd.out.reserve(out_bytes[pos]);
       gpu::hip_check(hipEventCreateWithFlags(&rd.done, hipEventDisableTiming), who, "event");
       rd.graph = gpu::capture_graph(hs, who, [&]() {
-        rd.in.upload(0, in_bytes[pos], hs);
         if (inverse) {
           gpu::srsgpu_check(srsgpu_ofdm_modulator_plan_execute(plans[pos], rd.in.dev<uint32_t>(), rd.out.dev<float>(),
                                                                hs),
@@ -431,7 +434,6 @@ private:
                                                                  rd.out.dev<uint32_t>(), hs),
                             who);
         }
-        rd.out.download(0, out_bytes[pos], hs);
       });
     }
     built = true;
@@ -550,10 +552,10 @@ class pdxch_processor_gpu : public pdxch_processor,
         }
       }
     }
-    gpu::staged_buffer grid;
-    gpu::staged_buffer samples;
+    gpu::mapped_buffer grid;     ///< the slot's grid rows, read in place by the modulation
+    gpu::mapped_buffer samples;  ///< the slot's samples, written in place
     hipEvent_t         done = nullptr;
-    /// Per slot of the subframe: upload + modulation + download captured over this job's buffers (graph_buffers).
+    /// Per slot of the subframe: the modulation captured over this job's buffers (graph_buffers).
     std::vector<hipGraphExec_t> graphs;
     const void*                 graph_buffers[2] = {nullptr, nullptr};
     std::vector<bool>  port_empty;
@@ -708,7 +710,8 @@ private:
       gpu::hip_check(hipEventCreateWithFlags(&j.done, hipEventDisableTiming), WHO, "event");
     }
     stage_grid(j, reader, j.grid.host());
-    // Upload, modulation and download as one captured graph per (job, slot of the subframe), built on first use.
+    // The modulation reads the rows and writes the samples in mapped host memory (no DMA copies), one captured launch
+    // per (job, slot of the subframe), built on first use.
     if (j.graph_buffers[0] != j.grid.dev() || j.graph_buffers[1] != j.samples.dev()) {
       j.drop_graphs();  // the job's buffers grew: the graphs captured their old addresses
       j.graph_buffers[0] = j.grid.dev();
@@ -718,23 +721,11 @@ private:
     hipGraphExec_t& exec = j.graphs[subframe_slot];
     if (exec == nullptr) {
       std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());
-      gpu::hip_check(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), WHO, "begin capture");
-      hipGraph_t graph = nullptr;
-      try {
-        j.grid.upload(0, nof_ports * geo.nsymb * row, s);
+      exec = gpu::capture_graph(s, WHO, [&]() {
         gpu::srsgpu_check(srsgpu_ofdm_modulator_plan_execute(plans[subframe_slot], j.grid.dev<uint32_t>(),
                                                              j.samples.dev<float>(), s),
                           WHO);
-        j.samples.download(0, nof_ports * slotn * sizeof(cf_t), s);
-      } catch (...) {
-        (void)hipStreamEndCapture(s, &graph);
-        (void)hipGraphDestroy(graph);
-        throw;
-      }
-      gpu::hip_check(hipStreamEndCapture(s, &graph), WHO, "end capture");
-      const hipError_t r = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(graph);
-      gpu::hip_check(r, WHO, "graph instantiate");
+      });
     }
     gpu::hip_check(hipGraphLaunch(exec, s), WHO, "graph launch");
     gpu::hip_check(hipEventRecord(j.done, s), WHO, "event");
@@ -832,8 +823,8 @@ class puxch_processor_gpu : public puxch_processor,
         (void)hipEventDestroy(done);
       }
     }
-    gpu::staged_buffer in;
-    gpu::staged_buffer out;
+    gpu::mapped_buffer in;   ///< the symbol's samples (all ports), read in place by the demodulation
+    gpu::mapped_buffer out;  ///< the demodulated rows, written in place
     hipEvent_t         done = nullptr;
   };
 
@@ -971,27 +962,15 @@ private:
       srsran_assert(in.size() == n, "The input buffer size ({}) does not match the symbol size ({}).", in.size(), n);
       std::memcpy(st.in.host<cf_t>(static_cast<size_t>(p) * n * sizeof(cf_t)), in.data(), n * sizeof(cf_t));
     }
-    // Upload, demodulation and download of this symbol position as one captured graph (built on first use): a
-    // symbol costs one launch instead of three dependent queue operations (~9 us apart each).
+    // The demodulation of this symbol position reads the samples and writes the rows in mapped host memory (no DMA
+    // copies), captured once per position.
     hipGraphExec_t& exec = graphs[s];
     if (exec == nullptr) {
       std::lock_guard<std::recursive_mutex> lock(gpu::hip_setup_mutex());
-      gpu::hip_check(hipStreamBeginCapture(hs, hipStreamCaptureModeRelaxed), WHO, "begin capture");
-      hipGraph_t graph = nullptr;
-      try {
-        st.in.upload(0, static_cast<size_t>(nof_ports) * n * sizeof(cf_t), hs);
+      exec = gpu::capture_graph(hs, WHO, [&]() {
         gpu::srsgpu_check(
             srsgpu_ofdm_demodulator_plan_execute(plans[s], st.in.dev<float>(), st.out.dev<uint32_t>(), hs), WHO);
-        st.out.download(0, static_cast<size_t>(nof_ports) * nsc * sizeof(uint32_t), hs);
-      } catch (...) {
-        (void)hipStreamEndCapture(hs, &graph);
-        (void)hipGraphDestroy(graph);
-        throw;
-      }
-      gpu::hip_check(hipStreamEndCapture(hs, &graph), WHO, "end capture");
-      const hipError_t r = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(graph);
-      gpu::hip_check(r, WHO, "graph instantiate");
+      });
     }
     gpu::hip_check(hipGraphLaunch(exec, hs), WHO, "graph launch");
     gpu::hip_check(hipEventRecord(st.done, hs), WHO, "event");
@@ -1074,7 +1053,7 @@ private:
   unsigned                                   nsc;
   unsigned                                   max_symbols_in_flight;
   std::vector<srsgpu_ofdm_plan*>             plans;  ///< One plan (all ports) per symbol of the subframe.
-  std::vector<hipGraphExec_t>                graphs;  ///< per plan: upload + demodulation + download
+  std::vector<hipGraphExec_t>                graphs;  ///< per plan: the demodulation over the stage's buffers
   std::vector<std::unique_ptr<symbol_stage>> stages;
   std::deque<pending_symbol>                 pending;
   std::atomic<bool>                          stopped  = false;

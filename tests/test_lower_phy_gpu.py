@@ -166,7 +166,8 @@ def test_sector_group_equals_reference(lower, name, in_flight):
     """The sector group (lower_phy_sector_group: the same symbol / slot of every sector in one launch): four sectors
     on their own carrier frequencies and data, driven from their own threads through the edge-case scripts above
     (missing requests, late and overwritten requests, partial slots, a slot left mid-way, empty grids and ports), each
-    equal to the reference processor run on that sector; and the group did launch shared rounds."""
+    equal to the reference processor run on that sector; and the group did launch shared rounds (the sectors are paced
+    at the symbol rate, as a radio unit drives them; free-running threads drift apart and run more symbols alone)."""
     cfg = CONFIGS[name]
     nsymb = 12 if cfg["extended"] else 14
     S, G = 4, 8
@@ -177,7 +178,8 @@ def test_sector_group_equals_reference(lower, name, in_flight):
     ev_dl, ev_ul = dl_script(nsymb), ul_script(nsymb)
     x = np.stack([ul_samples(rng, cfg, ev_ul) for _ in range(S)])
     ref = lower.sectors(REF_CPU, cfg, freqs, grids, masks, ev_dl, ev_ul, x)
-    got = lower.sectors(GPU_GROUP, cfg, freqs, grids, masks, ev_dl, ev_ul, x, max_in_flight=in_flight)
+    # paced at the radio's symbol rate, as a radio unit drives its sectors: their symbols meet in the group's rounds
+    got = lower.sectors(GPU_GROUP, cfg, freqs, grids, masks, ev_dl, ev_ul, x, max_in_flight=in_flight, paced=True)
     for k in range(S):
         (rs, rf), (gs, gf) = ref["dl"][k], got["dl"][k]
         touched = rs.real != SENTINEL

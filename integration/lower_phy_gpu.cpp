@@ -216,15 +216,23 @@ public:
   /// group stays disabled.
   void remove_sector(int sector)
   {
-    std::lock_guard<std::mutex> lock(mtx);
-    gone |= 1u << sector;
-    members[sector].clear();
-    const auto now = clock::now();
-    for (auto& rd : rounds) {
-      if (rd->key != UINT64_MAX && !rd->closed) {
-        rd->arrived |= 1u << sector;
-        try_close(*rd, now);
+    std::vector<round*> go;
+    {
+      std::lock_guard<std::mutex> lock(mtx);
+      gone |= 1u << sector;
+      members[sector].clear();
+      const auto now = clock::now();
+      for (auto& rd : rounds) {
+        if (rd->key != UINT64_MAX && !rd->closed) {
+          rd->arrived |= 1u << sector;
+          if (try_close(*rd, now)) {
+            go.push_back(rd.get());
+          }
+        }
       }
+    }
+    for (round* rd : go) {
+      launch(*rd);
     }
   }
 
@@ -238,9 +246,9 @@ public:
     if (!built || sector < 0) {
       return -1;
     }
-    std::lock_guard<std::mutex> lock(mtx);
-    const unsigned r  = static_cast<unsigned>(key % rounds.size());
-    round&         rd = *rounds[r];
+    std::unique_lock<std::mutex> lock(mtx);
+    const unsigned               r  = static_cast<unsigned>(key % rounds.size());
+    round&                       rd = *rounds[r];
     if (rd.key != key) {
       if (rd.consumers != 0 || (rd.arrived != 0 && !rd.closed)) {
         ++alone;
@@ -253,7 +261,9 @@ public:
       rd.closed   = false;
       rd.launched = false;
       rd.first    = clock::now();
-      dispatch_cv.notify_one();
+      if (dispatcher_idle) {
+        dispatch_cv.notify_one();  // a busy dispatcher already waits for an earlier deadline
+      }
     }
     const uint32_t bit = 1u << sector;
     if (rd.closed || (rd.arrived & bit) != 0) {
@@ -264,7 +274,10 @@ public:
     }
     rd.arrived |= bit;
     if (!present) {
-      try_close(rd, clock::now());
+      if (try_close(rd, clock::now())) {
+        lock.unlock();
+        launch(rd);
+      }
       return -1;
     }
     rd.present |= bit;
@@ -279,10 +292,16 @@ public:
   /// The sector's input of round r is in place.
   void written(int r, int sector)
   {
-    std::lock_guard<std::mutex> lock(mtx);
     round& rd = *rounds[r];
-    rd.written |= 1u << sector;
-    try_close(rd, clock::now());
+    bool   go;
+    {
+      std::lock_guard<std::mutex> lock(mtx);
+      rd.written |= 1u << sector;
+      go = try_close(rd, clock::now());
+    }
+    if (go) {
+      launch(rd);
+    }
   }
 
   /// Whether round r's outputs are ready; wait: block until they are.
@@ -334,23 +353,30 @@ private:
     hipGraphExec_t      graph = nullptr;
   };
 
-  /// Launches (or, with nobody present, retires) a round once every sector arrived or its window ran out, and every
-  /// present sector's input is in place. Holds mtx.
-  void try_close(round& rd, clock::time_point now)
+  /// Closes a round once every sector arrived or its window ran out, and every present sector's input is in place;
+  /// true: the caller launches it (after releasing mtx). A round nobody is present in retires without a launch. Holds
+  /// mtx.
+  bool try_close(round& rd, clock::time_point now)
   {
     if (rd.closed || rd.written != rd.present || (rd.arrived != all && now - rd.first < window)) {
-      return;
+      return false;
     }
     rd.closed = true;
-    if (rd.present == 0) {
-      return;
-    }
-    // Consecutive rounds on different streams: a round still reading / writing host memory does not hold the next.
+    return rd.present != 0;
+  }
+
+  /// The round's captured launch, outside mtx (the sectors of the next round keep joining meanwhile). Consecutive
+  /// rounds go to different streams: a round still reading / writing host memory does not hold the next.
+  void launch(round& rd)
+  {
     gpu::device_scope dev(ctx, who);
     hipStream_t       hs = streams[rd.index % streams.size()]->get();
     gpu::hip_check(hipGraphLaunch(rd.graph, hs), who, "graph launch");
     gpu::hip_check(hipEventRecord(rd.done, hs), who, "event");
-    rd.launched = true;
+    {
+      std::lock_guard<std::mutex> lock(mtx);
+      rd.launched = true;
+    }
     ++launches;
     launched_cv.notify_all();
   }
@@ -358,6 +384,7 @@ private:
   void dispatch_loop()
   {
     std::unique_lock<std::mutex> lock(mtx);
+    std::vector<round*>          go;
     while (!stopping) {
       clock::time_point next = clock::time_point::max();
       const auto        now  = clock::now();
@@ -365,17 +392,29 @@ private:
         if (rd->arrived == 0 || rd->closed || rd->key == UINT64_MAX) {
           continue;
         }
-        try_close(*rd, now);
-        if (!rd->closed) {
+        if (try_close(*rd, now)) {
+          go.push_back(rd.get());
+        } else if (!rd->closed) {
           // waiting for its window, or (window over) for a sector still copying its input
           next = std::min(next, rd->first + window > now ? rd->first + window : now + std::chrono::microseconds(20));
         }
       }
-      if (next == clock::time_point::max()) {
+      if (!go.empty()) {
+        lock.unlock();
+        for (round* rd : go) {
+          launch(*rd);
+        }
+        go.clear();
+        lock.lock();
+        continue;
+      }
+      dispatcher_idle = next == clock::time_point::max();
+      if (dispatcher_idle) {
         dispatch_cv.wait(lock);
       } else {
         dispatch_cv.wait_until(lock, next);
       }
+      dispatcher_idle = false;
     }
   }
 
@@ -456,6 +495,7 @@ private:
   uint32_t                                     gone       = 0;
   std::atomic<bool>                            built      = false;
   bool                                         stopping   = false;
+  bool                                         dispatcher_idle = true;
   std::atomic<uint64_t>                        launches   = 0;
   std::atomic<uint64_t>                        grouped    = 0;
   std::atomic<uint64_t>                        alone      = 0;

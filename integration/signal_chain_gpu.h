@@ -94,8 +94,8 @@ std::shared_ptr<puxch_processor_factory> create_puxch_processor_factory_gpu(int 
 struct lower_phy_group_configuration {
   int      device          = 0;
   unsigned nof_sectors     = 1;    ///< processors of each direction expected in a round (at most 32).
-  unsigned ul_window_us    = 100;  ///< how long a partly filled UL round waits for its missing sectors.
-  unsigned dl_window_us    = 200;  ///< the same for DL rounds (requests arrive slots ahead of transmission).
+  unsigned ul_window_us    = 300;  ///< how long a partly filled UL round waits for its missing sectors.
+  unsigned dl_window_us    = 300;  ///< the same for DL rounds (requests arrive slots ahead of transmission).
 };
 class lower_phy_sector_group;
 std::shared_ptr<lower_phy_sector_group> create_lower_phy_sector_group(const lower_phy_group_configuration& config);

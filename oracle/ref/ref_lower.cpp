@@ -218,14 +218,18 @@ void fill_pool(harness_pool& pool, const scenario& sc, int nof_grids, const uint
 }
 
 /// Real-time pacing of a script: symbol i of the script may start at start + i x period (the radio delivers / wants a
-/// symbol every period); max_lag: the latest a symbol started behind that time (a sector that cannot keep up falls
-/// further behind symbol after symbol). period 0: free-running.
+/// symbol every period). Lag statistics: the latest a symbol started behind its time, the lag of the last symbol (a
+/// sector that cannot keep up falls further behind symbol after symbol; one that can recovers from a hiccup) and the
+/// symbols that started more than one slot behind. period 0: free-running.
 struct pacer {
   using clock = std::chrono::steady_clock;
   clock::time_point start;
   clock::duration   period{0};
-  double            max_lag = 0;
-  long              i       = 0;
+  clock::duration   slot{0};
+  double            max_lag   = 0;
+  double            final_lag = 0;
+  long              late      = 0;
+  long              i         = 0;
 
   void next()
   {
@@ -240,8 +244,11 @@ struct pacer {
       }
       while (clock::now() < due) {
       }
+      final_lag = 0;
     } else {
-      max_lag = std::max(max_lag, std::chrono::duration<double>(now - due).count());
+      final_lag = std::chrono::duration<double>(now - due).count();
+      max_lag   = std::max(max_lag, final_lag);
+      late += (now - due) > slot ? 1 : 0;
     }
   }
 };
@@ -467,9 +474,9 @@ int ref_lower_puxch_run(int          variant,
 /// ref_lower_pdxch_run), DL and UL return flags, UL grids, UL notifications (nof_rx[k] pairs) and late slots
 /// (nof_late[k], DL then UL); seconds[2k], seconds[2k+1]: the sector's DL and UL script wall time. group_counts (6
 /// values, variant 3): lower_phy_group_counters. paced != 0: every sector runs at the radio's pace, one symbol per
-/// symbol duration (1 ms / symbols per subframe) from a common start, and lag[2k], lag[2k+1] report the latest a DL / UL
-/// symbol of sector k started behind its time (a sector keeps real time when that stays bounded). Returns 0, -1 on a
-/// sample overflow.
+/// symbol duration (1 ms / symbols per subframe) from a common start; lag[6k .. 6k+5]: sector k's DL and UL largest
+/// lag behind that pace (s), DL and UL lag at the last symbol (s), DL and UL fraction of symbols started more than one
+/// slot behind. Returns 0, -1 on a sample overflow.
 int ref_lower_sectors_run(int             variant,
                           int             max_in_flight,
                           int             nof_sectors,
@@ -555,6 +562,7 @@ int ref_lower_sectors_run(int             variant,
     threads.emplace_back([&, k]() {
       pacer pdl, pul;
       pdl.period = pul.period = period;
+      pdl.slot = pul.slot = period * static_cast<long>(sc.nsymb());
       if (k == 0) {
         start[0] = clock::now() + std::chrono::milliseconds(1);
       }
@@ -574,8 +582,9 @@ int ref_lower_sectors_run(int             variant,
       run_puxch_script(*ul[k], *ul_pools[k], sc, nof_ul_events, ul_events, ul_samples + 2 * k * ul_stride,
                        ul_processed + static_cast<size_t>(k) * n_ul_proc, &pul);
       seconds[2 * k + 1] = std::chrono::duration<double>(clock::now() - t0).count();
-      lag[2 * k]         = pdl.max_lag;
-      lag[2 * k + 1]     = pul.max_lag;
+      const double nd = static_cast<double>(std::max(1L, pdl.i)), nu = static_cast<double>(std::max(1L, pul.i));
+      const double v[6] = {pdl.max_lag, pul.max_lag, pdl.final_lag, pul.final_lag, pdl.late / nd, pul.late / nu};
+      std::copy(v, v + 6, lag + 6 * k);
     });
   }
   for (std::thread& t : threads) {

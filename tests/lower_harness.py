@@ -95,7 +95,8 @@ class Lower:
         (S, G, P, nsymb, nsc, 2) uint16 and masks (S, G): each sector's DL grids; ul_samples (S, n) complex64.
         Returns a dict: per-sector lists dl (samples, flags, late DL+UL mixed in 'late'), ul (grids, flags, rx), late,
         seconds (S, 2) DL/UL wall time, group counters (variant 3) and, paced (one symbol per symbol duration), lag
-        (S, 2): the latest a DL / UL symbol started behind its time."""
+        (S, 6): DL, UL largest lag behind the pace (s), DL, UL lag at the last symbol, DL, UL fraction of symbols more
+        than a slot behind."""
         S = len(freqs)
         nsymb = 12 if cfg["extended"] else 14
         P = cfg["nof_ports"]
@@ -115,7 +116,7 @@ class Lower:
         nlate = np.zeros(S, np.int32)
         secs = np.zeros((S, 2), np.float64)
         counts = np.zeros(6, np.uint64)
-        lag = np.zeros((S, 2), np.float64)
+        lag = np.zeros((S, 6), np.float64)
         fr = np.ascontiguousarray(freqs, np.float64)
         g = np.ascontiguousarray(grids, np.uint16)
         m = np.ascontiguousarray(masks, np.uint32)
@@ -123,8 +124,8 @@ class Lower:
         r = self.lib.ref_lower_sectors_run(
             variant, max_in_flight, S, cfg["numerology"], cfg["bw_rb"], cfg["dft_size"], int(cfg["extended"]),
             cfg["window_offset"], _ptr(fr), P, G, window_us, _ptr(g), _ptr(m), len(dl_ev), _ptr(dl_ev), _ptr(dl_out),
-            cap if ring is None else -cap, _ptr(dl_flags), len(ul_ev), _ptr(ul_ev), _ptr(x), x.shape[1], _ptr(ul_grids),
-            _ptr(ul_flags), _ptr(rx), _ptr(nrx), _ptr(late), _ptr(nlate), _ptr(secs), _ptr(counts), int(paced),
+            cap if ring is None else -cap, _ptr(dl_flags), len(ul_ev), _ptr(ul_ev), _ptr(x),
+            x.shape[1] if x.ndim == 2 else 0, _ptr(ul_grids), _ptr(ul_flags), _ptr(rx), _ptr(nrx), _ptr(late), _ptr(nlate), _ptr(secs), _ptr(counts), int(paced),
             _ptr(lag))
         assert r == 0
         return {

@@ -61,11 +61,12 @@ for step in "$@"; do
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kstats" -o k -- python3 -u bench.py \
         > "$OUT/kstats_bench.json" 2> "$OUT/kstats.log" || { tail -20 "$OUT/kstats.log"; exit 1; } ;;
     lower)
-      timeout -k 10 400 python -u tools/lower_phy_bench.py --sectors 1,2,4,8,16 > "$OUT/lower.json" 2> "$OUT/lower.log" \
+      timeout -k 10 400 python -u tools/lower_phy_bench.py --sectors 1,2,4,6,8,12 \
+        --sweep-only cpu,gpu0,gpu4,group0,group4,group13 > "$OUT/lower.json" 2> "$OUT/lower.log" \
         || { tail -20 "$OUT/lower.log"; exit 1; }
       tail -c 800 "$OUT/lower.json" ;;
     lower_trace)
-      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/lower_trace" -o lower -- python3 -u \
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/lower_trace" -o lower -- python3 -u \
         tools/lower_phy_bench.py --slots 100 --sectors 8 --sweep-only group4 > "$OUT/lower_trace.json" \
         2> "$OUT/lower_trace.log" || { tail -20 "$OUT/lower_trace.log"; exit 1; } ;;
     *) echo "unknown step $step"; exit 2 ;;

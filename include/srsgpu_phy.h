@@ -423,6 +423,34 @@ int srsgpu_ofdm_plan_concat(srsgpu_context*                ctx,
                             uint32_t                       nof_members,
                             srsgpu_ofdm_plan**             plan);
 
+/** One (grid, port, symbol) transform of an OFDM launch: the grid row at grid_offset (uint32 words), the symbol's
+ *  cyclic prefix at sample_offset (complex samples), its length, and the phase compensation times the scaling. */
+typedef struct {
+  uint32_t grid_offset;
+  uint32_t sample_offset;
+  uint32_t cp_len;
+  uint32_t reserved;
+  float    coef_re;
+  float    coef_im;
+} srsgpu_ofdm_job;
+
+/** The plan's jobs (one per grid, port and symbol, offsets relative to the plan's own buffers), as its launch runs
+ *  them: capacity entries at most, *nof_jobs = how many the plan has. */
+int srsgpu_ofdm_plan_get_jobs(const srsgpu_ofdm_plan* plan, srsgpu_ofdm_job* jobs, uint32_t capacity,
+                              uint32_t* nof_jobs);
+
+/** Runs a caller-assembled job list — the jobs of several plans (sectors, slots, symbols) at offsets of the caller's
+ *  choosing within d_in / d_out — with the launch parameters of `plan` (direction, DFT size, bandwidth, DFT window
+ *  offset); the jobs' plans must share them. d_jobs, d_in and d_out are device-accessible (HBM, or mapped host memory
+ *  the kernel reads / writes in place). Not for the split DFT sizes (9216 .. 98304 points: their scratch is per plan).
+ *  Asynchronous on `stream`. */
+int srsgpu_ofdm_jobs_execute(const srsgpu_ofdm_plan* plan,
+                             const srsgpu_ofdm_job*  d_jobs,
+                             uint32_t                nof_jobs,
+                             const void*             d_in,
+                             void*                   d_out,
+                             void*                   stream);
+
 /** uint32 words of the plan's grids (grids x ports x symbols x 12 * bw_rb). */
 uint64_t srsgpu_ofdm_plan_nof_grid_words(const srsgpu_ofdm_plan* plan);
 

@@ -97,6 +97,23 @@ private:
   std::array<entry, SIZE> entries;
 };
 
+/// Waits for a lower-PHY launch by polling its event: the launches take tens of microseconds, and a blocking
+/// hipEventSynchronize sleeps until an interrupt that can come that much later again (a real-time sector thread would
+/// lose the time of its next symbol).
+inline void wait_event(hipEvent_t e, const char* who)
+{
+  for (;;) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipSuccess) {
+      return;
+    }
+    if (r != hipErrorNotReady) {
+      gpu::hip_check(r, who, "event");
+    }
+    std::this_thread::yield();
+  }
+}
+
 /// Cyclic prefix + DFT samples of every symbol of a subframe and where each starts within its slot.
 struct symbol_geometry {
   symbol_geometry(subcarrier_spacing scs, cyclic_prefix cp, unsigned dft_size) :
@@ -137,38 +154,48 @@ srsgpu_ofdm_config ofdm_config(subcarrier_spacing scs, cyclic_prefix cp, unsigne
 // Sector group
 // ---------------------------------------------------------------------------------------------------------------------
 
-/// One direction of a sector group. A round is the work of every sector at one position (UL: a symbol, key = system
-/// slot x symbols per slot + symbol; DL: a slot, key = system slot), run as one OFDM launch of the sectors' plans
-/// concatenated (srsgpu_ofdm_plan_concat) that reads the round's input region (all sectors) from mapped host memory
-/// and writes its output region there (zero-copy: no DMA copy on the path). Rounds sit in a ring of a whole number of
-/// periods (a subframe's symbols or slots), so a ring entry always serves the same position and owns one captured
-/// launch over its own buffers; consecutive rounds go to different streams.
-class sector_rounds
+/// One direction of a sector group: the sectors' OFDM work (UL: one symbol of one sector; DL: one slot) in shared
+/// launches. A sector stages its input in an entry of its own ring in mapped host memory and submits it; a launch
+/// takes every submitted entry — whatever sector, slot or symbol — and runs them as one job list
+/// (srsgpu_ofdm_jobs_execute: each entry's jobs are its plan's, moved to the entry's place in the shared buffers),
+/// reading the inputs and writing the outputs in place (zero-copy). A launch goes out as soon as every active sector
+/// (one that submitted within the last `activity`) has an entry waiting, or `window` after the oldest waiting entry;
+/// the last sector to submit launches it, a dispatcher thread handles the windows. Nothing waits for a particular
+/// sector: a sector that falls behind has its entries taken by whichever launch comes next. Completion: the stream
+/// writes each launch's sequence number into its completion word in mapped memory, which the sectors poll (no HIP
+/// call on their per-symbol path).
+class ofdm_batcher
 {
 public:
   using clock = std::chrono::steady_clock;
 
-  sector_rounds(srsgpu_context* ctx_, const char* who_, bool inverse_, unsigned nof_sectors_, unsigned period_,
-                unsigned nof_rounds, std::chrono::microseconds window_) :
+  ofdm_batcher(srsgpu_context*           ctx_,
+               const char*               who_,
+               bool                      inverse_,
+               unsigned                  nof_sectors_,
+               unsigned                  depth_,
+               std::chrono::microseconds window_,
+               clock::duration           activity_) :
     ctx(ctx_),
     who(who_),
     inverse(inverse_),
     nof_sectors(nof_sectors_),
-    all((nof_sectors_ >= 32) ? ~0u : ((1u << nof_sectors_) - 1)),
-    period(period_),
+    depth(depth_),
     window(window_),
-    members(nof_sectors_)
+    activity(activity_),
+    sectors(nof_sectors_),
+    jobs_buf(who_),
+    in_all(who_),
+    out_all(who_),
+    flags(who_)
   {
     for (auto& st : streams) {
       st = std::make_unique<gpu::owned_stream>(ctx_, who_);
     }
-    for (unsigned r = 0; r != nof_rounds; ++r) {
-      rounds.emplace_back(std::make_unique<round>(who, r));
-    }
     dispatcher = std::thread([this]() { dispatch_loop(); });
   }
 
-  ~sector_rounds()
+  ~ofdm_batcher()
   {
     {
       std::lock_guard<std::mutex> lock(mtx);
@@ -179,330 +206,299 @@ public:
     for (auto& st : streams) {
       (void)hipStreamSynchronize(st->get());
     }
-    std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());
-    for (auto& rd : rounds) {
-      if (rd->graph != nullptr) {
-        (void)hipGraphExecDestroy(rd->graph);
-      }
-      if (rd->done != nullptr) {
-        (void)hipEventDestroy(rd->done);
-      }
-    }
-    rounds.clear();
-    for (srsgpu_ofdm_plan* p : plans) {
-      srsgpu_ofdm_plan_destroy(p);
-    }
   }
 
-  /// A sector's plans, one per position of the period (kept by the caller while it is registered); returns the
-  /// sector's index, or -1 when every index is taken. The last sector builds the concatenated plans, the rounds'
-  /// buffers and graphs (the caller holds gpu::hip_setup_mutex). Sectors whose plans do not concatenate leave the
-  /// group disabled: every sector then runs alone.
-  int add_sector(const std::vector<srsgpu_ofdm_plan*>& sector_plans)
+  /// Registers a sector's plans, one per position of its period (kept by the caller while registered): its index, or
+  /// -1 (no free index, or plans that cannot share a launch with the first sector's: that sector runs alone). The
+  /// first sector sizes the shared buffers (the caller holds gpu::hip_setup_mutex).
+  int add_sector(const std::vector<srsgpu_ofdm_plan*>& plans)
   {
     std::lock_guard<std::mutex> lock(mtx);
-    if (registered == nof_sectors || sector_plans.size() != period) {
-      return -1;
-    }
-    const int index     = static_cast<int>(registered++);
-    members[index]      = sector_plans;
-    if (registered == nof_sectors) {
-      build();
-    }
-    return index;
-  }
-
-  /// Deregistration (the sector's plans are going away): rounds no longer wait for it; before the group is built, the
-  /// group stays disabled.
-  void remove_sector(int sector)
-  {
-    std::vector<round*> go;
-    {
-      std::lock_guard<std::mutex> lock(mtx);
-      gone |= 1u << sector;
-      members[sector].clear();
-      const auto now = clock::now();
-      for (auto& rd : rounds) {
-        if (rd->key != UINT64_MAX && !rd->closed) {
-          rd->arrived |= 1u << sector;
-          if (try_close(*rd, now)) {
-            go.push_back(rd.get());
-          }
-        }
+    int k = -1;
+    for (unsigned i = 0; i != nof_sectors; ++i) {
+      if (!sectors[i].used) {
+        k = static_cast<int>(i);
+        break;
       }
     }
-    for (round* rd : go) {
-      launch(*rd);
-    }
-  }
-
-  bool enabled() const { return built; }
-
-  /// Sector `sector` reaches the round of `key`: present (it has work: returns the ring entry it writes its input into
-  /// before calling written()) or absent (no request: returns -1, the round stops waiting for it). -1 also when the
-  /// round launched already or its ring entry is still busy with an older key: the sector runs alone.
-  int join(int sector, uint64_t key, bool present)
-  {
-    if (!built || sector < 0) {
+    if (k < 0 || plans.empty()) {
       return -1;
     }
-    std::unique_lock<std::mutex> lock(mtx);
-    const unsigned               r  = static_cast<unsigned>(key % rounds.size());
-    round&                       rd = *rounds[r];
-    if (rd.key != key) {
-      if (rd.consumers != 0 || (rd.arrived != 0 && !rd.closed)) {
-        ++alone;
+    if (launcher == nullptr) {
+      if (!size_buffers(plans)) {
         return -1;
       }
-      rd.key      = key;
-      rd.arrived  = gone;
-      rd.present  = 0;
-      rd.written  = 0;
-      rd.closed   = false;
-      rd.launched = false;
-      rd.first    = clock::now();
-      if (dispatcher_idle) {
-        dispatch_cv.notify_one();  // a busy dispatcher already waits for an earlier deadline
-      }
-    }
-    const uint32_t bit = 1u << sector;
-    if (rd.closed || (rd.arrived & bit) != 0) {
-      if (present) {
-        ++alone;
-      }
+    } else if (!compatible(plans)) {
       return -1;
     }
-    rd.arrived |= bit;
-    if (!present) {
-      if (try_close(rd, clock::now())) {
-        lock.unlock();
-        launch(rd);
-      }
-      return -1;
+    sector_state& sc = sectors[k];
+    sc.used          = true;
+    sc.templates.assign(plans.size(), {});
+    for (size_t pos = 0; pos != plans.size(); ++pos) {
+      uint32_t n = 0;
+      gpu::srsgpu_check(srsgpu_ofdm_plan_get_jobs(plans[pos], nullptr, 0, &n), who);
+      sc.templates[pos].resize(n);
+      gpu::srsgpu_check(srsgpu_ofdm_plan_get_jobs(plans[pos], sc.templates[pos].data(), n, &n), who);
     }
-    rd.present |= bit;
-    ++rd.consumers;
-    ++grouped;
-    return static_cast<int>(r);
+    sc.entries = std::vector<entry>(depth);
+    sc.head    = 0;
+    return k;
   }
 
-  uint8_t* input(int r, int sector) { return rounds[r]->in.host(in_off[r % period][sector]); }
-  const uint8_t* output(int r, int sector) { return rounds[r]->out.host(out_off[r % period][sector]); }
-
-  /// The sector's input of round r is in place.
-  void written(int r, int sector)
-  {
-    round& rd = *rounds[r];
-    bool   go;
-    {
-      std::lock_guard<std::mutex> lock(mtx);
-      rd.written |= 1u << sector;
-      go = try_close(rd, clock::now());
-    }
-    if (go) {
-      launch(rd);
-    }
-  }
-
-  /// Whether round r's outputs are ready; wait: block until they are.
-  bool ready(int r, bool wait)
-  {
-    round& rd = *rounds[r];
-    {
-      std::unique_lock<std::mutex> lock(mtx);
-      if (!rd.launched) {
-        if (!wait) {
-          return false;
-        }
-        launched_cv.wait(lock, [&rd]() { return rd.launched; });
-      }
-    }
-    if (wait) {
-      gpu::hip_check(hipEventSynchronize(rd.done), who, "sector group round");
-      return true;
-    }
-    return hipEventQuery(rd.done) == hipSuccess;
-  }
-
-  /// A present sector is done with round r's outputs.
-  void release(int r)
+  void remove_sector(int sector)
   {
     std::lock_guard<std::mutex> lock(mtx);
-    --rounds[r]->consumers;
+    sectors[sector].used        = false;
+    sectors[sector].last_submit = clock::time_point();
   }
 
-  uint64_t nof_rounds() const { return launches.load(); }
-  uint64_t nof_grouped() const { return grouped.load(); }
-  uint64_t nof_alone() const { return alone.load(); }
-
-private:
-  struct round {
-    round(const char* w, unsigned i) : index(i), in(w), out(w) {}
-    unsigned            index;
-    uint64_t            key       = UINT64_MAX;
-    uint32_t            arrived   = 0;  ///< sectors that reached the round (present or absent; gone ones count)
-    uint32_t            present   = 0;  ///< sectors with input in the round
-    uint32_t            written   = 0;  ///< present sectors whose input is in place
-    unsigned            consumers = 0;  ///< present sectors that have not released the outputs
-    bool                closed    = false;  ///< no more sectors join (launched, or nothing to launch)
-    bool                launched  = false;
-    clock::time_point   first;
-    gpu::mapped_buffer  in;   ///< every sector's input, read in place by the OFDM kernel
-    gpu::mapped_buffer  out;  ///< every sector's output, written in place
-    hipEvent_t          done  = nullptr;
-    hipGraphExec_t      graph = nullptr;
-  };
-
-  /// Closes a round once every sector arrived or its window ran out, and every present sector's input is in place;
-  /// true: the caller launches it (after releasing mtx). A round nobody is present in retires without a launch. Holds
-  /// mtx.
-  bool try_close(round& rd, clock::time_point now)
+  /// The sector's next staging entry, or -1 while it is still in use (the sector then runs that work alone).
+  int acquire(int sector)
   {
-    if (rd.closed || rd.written != rd.present || (rd.arrived != all && now - rd.first < window)) {
-      return false;
+    sector_state& sc = sectors[sector];
+    const int     e  = static_cast<int>(sc.head % depth);
+    entry&        en = sc.entries[e];
+    if (en.busy.load(std::memory_order_acquire)) {
+      ++alone;
+      return -1;
     }
-    rd.closed = true;
-    return rd.present != 0;
+    en.busy.store(true, std::memory_order_relaxed);
+    en.launched.store(false, std::memory_order_relaxed);
+    ++sc.head;
+    return e;
   }
 
-  /// The round's captured launch, outside mtx (the sectors of the next round keep joining meanwhile). Consecutive
-  /// rounds go to different streams: a round still reading / writing host memory does not hold the next.
-  void launch(round& rd)
+  uint8_t*       input(int sector, int e) { return in_all.host(entry_index(sector, e) * in_max); }
+  const uint8_t* output(int sector, int e) { return out_all.host(entry_index(sector, e) * out_max); }
+
+  /// The entry's input for position `pos` is in place.
+  void submit(int sector, int e, unsigned pos)
   {
-    gpu::device_scope dev(ctx, who);
-    hipStream_t       hs = streams[rd.index % streams.size()]->get();
-    gpu::hip_check(hipGraphLaunch(rd.graph, hs), who, "graph launch");
-    gpu::hip_check(hipEventRecord(rd.done, hs), who, "event");
+    std::vector<pending_entry> batch;
     {
       std::lock_guard<std::mutex> lock(mtx);
-      rd.launched = true;
+      const auto now = clock::now();
+      sectors[sector].last_submit = now;
+      queue.push_back({sector, e, pos, now});
+      if (queue.size() == 1) {
+        dispatch_cv.notify_one();  // a window to watch
+      }
+      if (queue.size() >= active_sectors(now)) {
+        batch.swap(queue);
+      }
+    }
+    if (!batch.empty()) {
+      launch(batch);
+    }
+  }
+
+  /// Whether the entry's output is ready; wait: until it is.
+  bool ready(int sector, int e, bool wait)
+  {
+    entry& en = sectors[sector].entries[e];
+    if (!en.launched.load(std::memory_order_acquire)) {
+      if (!wait) {
+        return false;
+      }
+      std::unique_lock<std::mutex> lock(mtx);
+      launched_cv.wait(lock, [&en]() { return en.launched.load(std::memory_order_acquire); });
+    }
+    const uint32_t* word = flags.host<uint32_t>(en.batch * 64);
+    for (;;) {
+      // the words count up (wrapping): reached once the difference is no longer negative
+      if (static_cast<int32_t>(__atomic_load_n(word, __ATOMIC_ACQUIRE) - en.seq) >= 0) {
+        return true;
+      }
+      if (!wait) {
+        return false;
+      }
+      std::this_thread::yield();
+    }
+  }
+
+  void release(int sector, int e) { sectors[sector].entries[e].busy.store(false, std::memory_order_release); }
+
+  uint64_t nof_launches() const { return launches.load(); }
+  uint64_t nof_grouped() const { return grouped.load(); }
+  uint64_t nof_alone() const { return alone.load(); }
+  uint64_t nof_windowed() const { return windowed.load(); }
+  double   mean_batch() const { return launches ? static_cast<double>(grouped.load()) / launches.load() : 0; }
+
+private:
+  struct entry {
+    std::atomic<bool> busy     = false;  ///< acquired and not yet released
+    std::atomic<bool> launched = false;
+    unsigned          batch    = 0;  ///< batch ring index of its launch
+    uint32_t          seq      = 0;  ///< that launch's sequence number
+  };
+  struct sector_state {
+    bool                                      used = false;
+    std::vector<std::vector<srsgpu_ofdm_job>> templates;  ///< per position: the plan's jobs
+    std::vector<entry>                        entries;
+    uint64_t                                  head = 0;
+    clock::time_point                         last_submit;
+  };
+  struct pending_entry {
+    int               sector;
+    int               e;
+    unsigned          pos;
+    clock::time_point at;
+  };
+  static constexpr unsigned NOF_BATCHES = 16;
+
+  size_t entry_index(int sector, int e) const { return static_cast<size_t>(sector) * depth + e; }
+
+  /// Sectors that submitted within `activity` (at least one). Holds mtx.
+  size_t active_sectors(clock::time_point now) const
+  {
+    size_t n = 0;
+    for (const sector_state& sc : sectors) {
+      n += (sc.used && now - sc.last_submit < activity) ? 1 : 0;
+    }
+    return std::max<size_t>(n, 1);
+  }
+
+  /// Shared buffers sized from the first sector's plans. Holds mtx and gpu::hip_setup_mutex.
+  bool size_buffers(const std::vector<srsgpu_ofdm_plan*>& plans)
+  {
+    for (srsgpu_ofdm_plan* p : plans) {
+      const size_t grid  = srsgpu_ofdm_plan_nof_grid_words(p) * sizeof(uint32_t);
+      const size_t samp  = srsgpu_ofdm_plan_nof_samples(p) * sizeof(cf_t);
+      uint32_t     njobs = 0;
+      gpu::srsgpu_check(srsgpu_ofdm_plan_get_jobs(p, nullptr, 0, &njobs), who);
+      // entries 256-byte aligned; offsets in samples (8 bytes) and grid words (4 bytes) stay exact
+      in_max        = std::max(in_max, (inverse ? grid : samp) + 255) / 256 * 256;
+      out_max       = std::max(out_max, (inverse ? samp : grid) + 255) / 256 * 256;
+      jobs_per_entry = std::max<size_t>(jobs_per_entry, njobs);
+    }
+    const size_t entries = static_cast<size_t>(nof_sectors) * depth;
+    if ((entries * in_max) / sizeof(uint32_t) >= (1ull << 32) || (entries * out_max) / sizeof(uint32_t) >= (1ull << 32)) {
+      return false;  // beyond the jobs' 32-bit offsets
+    }
+    in_all.reserve(entries * in_max);
+    out_all.reserve(entries * out_max);
+    jobs_buf.reserve(NOF_BATCHES * entries * jobs_per_entry * sizeof(srsgpu_ofdm_job));
+    flags.reserve(NOF_BATCHES * 64);
+    for (unsigned b = 0; b != NOF_BATCHES; ++b) {
+      *flags.host<uint32_t>(b * 64) = 0;
+    }
+    launcher = plans[0];
+    return true;
+  }
+
+  /// Whether the plans can share a launch with the first sector's (the launch takes its parameters from those).
+  bool compatible(const std::vector<srsgpu_ofdm_plan*>& plans) const
+  {
+    const srsgpu_ofdm_plan* pair[2] = {launcher, plans[0]};
+    srsgpu_ofdm_plan*       joined  = nullptr;
+    if (srsgpu_ofdm_plan_concat(ctx, pair, 2, &joined) != SRSGPU_OK) {
+      return false;
+    }
+    srsgpu_ofdm_plan_destroy(joined);
+    for (srsgpu_ofdm_plan* p : plans) {
+      const size_t grid = srsgpu_ofdm_plan_nof_grid_words(p) * sizeof(uint32_t);
+      const size_t samp = srsgpu_ofdm_plan_nof_samples(p) * sizeof(cf_t);
+      if ((inverse ? grid : samp) > in_max || (inverse ? samp : grid) > out_max) {
+        return false;
+      }
+    }
+    return true;
+  }
+
+  /// One launch of the entries: their jobs moved to the entries' places, the OFDM kernel over them, the completion
+  /// word. Without mtx.
+  void launch(const std::vector<pending_entry>& batch)
+  {
+    std::lock_guard<std::mutex> serial(launch_mtx);  // batch ring order = sequence order
+    const unsigned              b     = static_cast<unsigned>(next_seq % NOF_BATCHES);
+    const uint32_t              seq   = static_cast<uint32_t>(++next_seq);
+    const uint32_t*             word  = flags.host<uint32_t>(b * 64);
+    // The batch record's previous launch (NOF_BATCHES launches ago) must have finished reading its job table.
+    while (static_cast<int32_t>(__atomic_load_n(word, __ATOMIC_ACQUIRE) - (seq - NOF_BATCHES)) < 0 &&
+           seq > NOF_BATCHES) {
+      std::this_thread::yield();
+    }
+    const size_t     stride = static_cast<size_t>(nof_sectors) * depth * jobs_per_entry;
+    srsgpu_ofdm_job* jobs   = jobs_buf.host<srsgpu_ofdm_job>(b * stride * sizeof(srsgpu_ofdm_job));
+    size_t           n      = 0;
+    for (const pending_entry& pe : batch) {
+      const size_t in_off  = entry_index(pe.sector, pe.e) * in_max;
+      const size_t out_off = entry_index(pe.sector, pe.e) * out_max;
+      // demodulation: samples in, grid out; modulation: grid in, samples out
+      const uint32_t samples_base = static_cast<uint32_t>((inverse ? out_off : in_off) / sizeof(cf_t));
+      const uint32_t grid_base    = static_cast<uint32_t>((inverse ? in_off : out_off) / sizeof(uint32_t));
+      for (srsgpu_ofdm_job jb : sectors[pe.sector].templates[pe.pos]) {
+        jb.sample_offset += samples_base;
+        jb.grid_offset += grid_base;
+        jobs[n++] = jb;
+      }
+    }
+    gpu::device_scope dev(ctx, who);
+    hipStream_t       hs = streams[b % streams.size()]->get();
+    gpu::srsgpu_check(srsgpu_ofdm_jobs_execute(launcher, jobs_buf.dev<srsgpu_ofdm_job>(b * stride * sizeof(srsgpu_ofdm_job)),
+                                               static_cast<uint32_t>(n), in_all.dev(), out_all.dev(), hs),
+                      who);
+    gpu::hip_check(hipStreamWriteValue32(hs, flags.dev<uint32_t>(b * 64), seq, 0), who, "completion word");
+    for (const pending_entry& pe : batch) {
+      entry& en = sectors[pe.sector].entries[pe.e];
+      en.batch  = b;
+      en.seq    = seq;
+      en.launched.store(true, std::memory_order_release);
     }
     ++launches;
+    grouped += batch.size();
+    {
+      std::lock_guard<std::mutex> lock(mtx);  // pairs with the waiters' predicate check
+    }
     launched_cv.notify_all();
   }
 
   void dispatch_loop()
   {
     std::unique_lock<std::mutex> lock(mtx);
-    std::vector<round*>          go;
     while (!stopping) {
-      clock::time_point next = clock::time_point::max();
-      const auto        now  = clock::now();
-      for (auto& rd : rounds) {
-        if (rd->arrived == 0 || rd->closed || rd->key == UINT64_MAX) {
-          continue;
-        }
-        if (try_close(*rd, now)) {
-          go.push_back(rd.get());
-        } else if (!rd->closed) {
-          // waiting for its window, or (window over) for a sector still copying its input
-          next = std::min(next, rd->first + window > now ? rd->first + window : now + std::chrono::microseconds(20));
-        }
-      }
-      if (!go.empty()) {
-        lock.unlock();
-        for (round* rd : go) {
-          launch(*rd);
-        }
-        go.clear();
-        lock.lock();
+      if (queue.empty()) {
+        dispatch_cv.wait(lock);
         continue;
       }
-      dispatcher_idle = next == clock::time_point::max();
-      if (dispatcher_idle) {
-        dispatch_cv.wait(lock);
-      } else {
-        dispatch_cv.wait_until(lock, next);
+      const auto deadline = queue.front().at + window;
+      if (clock::now() < deadline) {
+        dispatch_cv.wait_until(lock, deadline);
+        continue;
       }
-      dispatcher_idle = false;
+      std::vector<pending_entry> batch;
+      batch.swap(queue);
+      lock.unlock();
+      ++windowed;
+      launch(batch);
+      lock.lock();
     }
   }
 
-  /// Concatenated plans, per-sector offsets, round buffers and graphs. Holds mtx (and gpu::hip_setup_mutex).
-  void build()
-  {
-    gpu::device_scope dev(ctx, who);
-    for (unsigned k = 0; k != nof_sectors; ++k) {
-      if (members[k].size() != period) {
-        return;  // a sector left before the group was complete
-      }
-    }
-    std::vector<srsgpu_ofdm_plan*> cat(period, nullptr);
-    for (unsigned pos = 0; pos != period; ++pos) {
-      std::vector<const srsgpu_ofdm_plan*> m;
-      for (unsigned k = 0; k != nof_sectors; ++k) {
-        m.push_back(members[k][pos]);
-      }
-      if (srsgpu_ofdm_plan_concat(ctx, m.data(), nof_sectors, &cat[pos]) != SRSGPU_OK) {
-        for (srsgpu_ofdm_plan* p : cat) {
-          srsgpu_ofdm_plan_destroy(p);
-        }
-        return;  // sectors differ in what one launch shares: no group
-      }
-    }
-    plans = cat;
-    in_off.assign(period, std::vector<size_t>(nof_sectors));
-    out_off.assign(period, std::vector<size_t>(nof_sectors));
-    std::vector<size_t> in_bytes(period), out_bytes(period);  // per position
-    for (unsigned pos = 0; pos != period; ++pos) {
-      const size_t words = srsgpu_ofdm_plan_nof_grid_words(plans[pos]) / nof_sectors;  // equal per sector
-      for (unsigned k = 0; k != nof_sectors; ++k) {
-        const size_t samples = srsgpu_ofdm_plan_sample_offset(plans[pos], k, 0) * sizeof(cf_t);
-        in_off[pos][k]       = inverse ? k * words * sizeof(uint32_t) : samples;
-        out_off[pos][k]      = inverse ? samples : k * words * sizeof(uint32_t);
-      }
-      const size_t grid_bytes   = srsgpu_ofdm_plan_nof_grid_words(plans[pos]) * sizeof(uint32_t);
-      const size_t sample_bytes = srsgpu_ofdm_plan_nof_samples(plans[pos]) * sizeof(cf_t);
-      in_bytes[pos]             = inverse ? grid_bytes : sample_bytes;
-      out_bytes[pos]            = inverse ? sample_bytes : grid_bytes;
-    }
-    hipStream_t hs = streams[0]->get();
-    for (unsigned r = 0; r != rounds.size(); ++r) {
-      round&         rd  = *rounds[r];
-      const unsigned pos = r % period;
-      rd.in.reserve(in_bytes[pos]);
-      rd.out.reserve(out_bytes[pos]);
-      gpu::hip_check(hipEventCreateWithFlags(&rd.done, hipEventDisableTiming), who, "event");
-      rd.graph = gpu::capture_graph(hs, who, [&]() {
-        if (inverse) {
-          gpu::srsgpu_check(srsgpu_ofdm_modulator_plan_execute(plans[pos], rd.in.dev<uint32_t>(), rd.out.dev<float>(),
-                                                               hs),
-                            who);
-        } else {
-          gpu::srsgpu_check(srsgpu_ofdm_demodulator_plan_execute(plans[pos], rd.in.dev<float>(),
-                                                                 rd.out.dev<uint32_t>(), hs),
-                            who);
-        }
-      });
-    }
-    built = true;
-  }
-
-  srsgpu_context*                              ctx;
-  const char*                                  who;
-  bool                                         inverse;
-  unsigned                                     nof_sectors;
-  uint32_t                                     all;
-  unsigned                                     period;
-  std::chrono::microseconds                    window;
+  srsgpu_context*                                   ctx;
+  const char*                                       who;
+  bool                                              inverse;
+  unsigned                                          nof_sectors;
+  unsigned                                          depth;  ///< staging entries per sector
+  std::chrono::microseconds                         window;
+  clock::duration                                   activity;
+  std::vector<sector_state>                         sectors;
+  const srsgpu_ofdm_plan*                           launcher = nullptr;  ///< the first sector's plan: launch params
+  size_t                                            in_max = 0, out_max = 0, jobs_per_entry = 0;
+  gpu::mapped_buffer                                jobs_buf;  ///< NOF_BATCHES job tables
+  gpu::mapped_buffer                                in_all;    ///< every sector's entries' inputs
+  gpu::mapped_buffer                                out_all;   ///< ... and outputs
+  gpu::mapped_buffer                                flags;     ///< completion word per batch record
   std::array<std::unique_ptr<gpu::owned_stream>, 3> streams;
-  std::vector<std::vector<srsgpu_ofdm_plan*>>  members;
-  std::vector<srsgpu_ofdm_plan*>               plans;    ///< per position: every sector's plan concatenated
-  std::vector<std::vector<size_t>>             in_off;   ///< per position and sector: byte offset of its input
-  std::vector<std::vector<size_t>>             out_off;  ///< ... and of its output
-  std::vector<std::unique_ptr<round>>          rounds;
-  unsigned                                     registered = 0;
-  uint32_t                                     gone       = 0;
-  std::atomic<bool>                            built      = false;
-  bool                                         stopping   = false;
-  bool                                         dispatcher_idle = true;
-  std::atomic<uint64_t>                        launches   = 0;
-  std::atomic<uint64_t>                        grouped    = 0;
-  std::atomic<uint64_t>                        alone      = 0;
-  std::mutex                                   mtx;
-  std::condition_variable                      launched_cv;
-  std::condition_variable                      dispatch_cv;
-  std::thread                                  dispatcher;
+  std::vector<pending_entry>                        queue;
+  uint64_t                                          next_seq = 0;
+  bool                                              stopping = false;
+  std::atomic<uint64_t>                             launches = 0, grouped = 0, alone = 0, windowed = 0;
+  std::mutex                                        mtx;
+  std::mutex                                        launch_mtx;
+  std::condition_variable                           launched_cv;
+  std::condition_variable                           dispatch_cv;
+  std::thread                                       dispatcher;
 };
 
 } // namespace
@@ -520,17 +516,19 @@ public:
     }
   }
 
-  sector_rounds& rounds(bool downlink, unsigned period)
+  /// The direction's batcher, made by its first processor: `positions` = slots (DL) or symbols (UL) per subframe.
+  ofdm_batcher& batcher(bool downlink, unsigned positions)
   {
     std::lock_guard<std::mutex> lock(mtx);
-    std::unique_ptr<sector_rounds>& r = downlink ? dl : ul;
+    std::unique_ptr<ofdm_batcher>& r = downlink ? dl : ul;
     if (!r) {
-      // A whole number of periods (one graph per ring entry): at least 8 slots of DL (requests run a few slots ahead
-      // of the slot being transmitted) and 4 slots of UL symbols (a sector holds at most a slot's symbols).
-      const unsigned n = downlink ? period * std::max(1u, 8u / period) : period * std::max(2u, 56u / period);
-      r = std::make_unique<sector_rounds>(owner.get(), downlink ? "pdxch_sector_group" : "puxch_sector_group",
-                                          downlink, cfg.nof_sectors, period, n,
-                                          std::chrono::microseconds(downlink ? cfg.dl_window_us : cfg.ul_window_us));
+      // Staging entries per sector: a UL sector holds at most a slot's symbols, a DL sector the requests of a few
+      // slots ahead. A sector is active while it submitted within 3 symbols (UL) / 1.5 slots (DL).
+      const auto position = std::chrono::nanoseconds(1000000 / positions);
+      r = std::make_unique<ofdm_batcher>(owner.get(), downlink ? "pdxch_sector_group" : "puxch_sector_group", downlink,
+                                         cfg.nof_sectors, downlink ? 8 : 16,
+                                         std::chrono::microseconds(downlink ? cfg.dl_window_us : cfg.ul_window_us),
+                                         downlink ? position * 3 / 2 : position * 3);
     }
     return *r;
   }
@@ -540,14 +538,16 @@ public:
     lower_phy_group_counters c;
     std::lock_guard<std::mutex> lock(mtx);
     if (ul) {
-      c.ul_rounds  = ul->nof_rounds();
-      c.ul_grouped = ul->nof_grouped();
-      c.ul_alone   = ul->nof_alone();
+      c.ul_launches = ul->nof_launches();
+      c.ul_batched  = ul->nof_grouped();
+      c.ul_alone    = ul->nof_alone();
+      c.ul_windowed = ul->nof_windowed();
     }
     if (dl) {
-      c.dl_rounds  = dl->nof_rounds();
-      c.dl_grouped = dl->nof_grouped();
-      c.dl_alone   = dl->nof_alone();
+      c.dl_launches = dl->nof_launches();
+      c.dl_batched  = dl->nof_grouped();
+      c.dl_alone    = dl->nof_alone();
+      c.dl_windowed = dl->nof_windowed();
     }
     return c;
   }
@@ -556,9 +556,9 @@ public:
   std::shared_ptr<srsgpu_context>      owner;
 
 private:
-  mutable std::mutex             mtx;
-  std::unique_ptr<sector_rounds> ul;
-  std::unique_ptr<sector_rounds> dl;
+  mutable std::mutex            mtx;
+  std::unique_ptr<ofdm_batcher> ul;
+  std::unique_ptr<ofdm_batcher> dl;
 };
 
 namespace {
@@ -602,7 +602,7 @@ class pdxch_processor_gpu : public pdxch_processor,
     unsigned           subframe_slot = 0;
     bool               launched      = false;  ///< false: the request's grid was empty (nothing to transmit).
     bool               own           = false;  ///< launched on this job's own buffers (done is recorded)
-    int                round         = -1;     ///< launched in the sector group's round (its outputs hold the slot)
+    int                entry         = -1;     ///< staged in the sector group's entry (its output holds the slot)
   };
   using job_ptr = std::unique_ptr<job>;
 
@@ -629,7 +629,7 @@ public:
       plans.push_back(p);
     }
     if (group_owner) {
-      group  = &group_owner->rounds(true, geo.nslot);
+      group  = &group_owner->batcher(true, geo.nslot);
       sector = group->add_sector(plans);
     }
   }
@@ -679,10 +679,10 @@ private:
       }
       current = std::move(r.payload);
       gpu::device_scope dev(ctx, WHO);
-      if (current->round >= 0) {
-        group->ready(current->round, true);
+      if (current->entry >= 0) {
+        group->ready(sector, current->entry, true);
       } else {
-        gpu::hip_check(hipEventSynchronize(current->done), WHO, "modulation");
+        wait_event(current->done, WHO);
       }
     }
     if (!current) {
@@ -692,7 +692,7 @@ private:
     const unsigned n     = geo.size[s];
     const size_t   slotn = geo.slot_size(current->subframe_slot);
     const auto*    slot_samples =
-        reinterpret_cast<const cf_t*>(current->round >= 0 ? group->output(current->round, sector) : current->samples.host());
+        reinterpret_cast<const cf_t*>(current->entry >= 0 ? group->output(sector, current->entry) : current->samples.host());
     for (unsigned p = 0; p != nof_ports; ++p) {
       span<cf_t> out = samples.get_channel_buffer(p);
       srsran_assert(out.size() == n, "The output buffer size ({}) does not match the symbol size ({}).", out.size(), n);
@@ -715,11 +715,12 @@ private:
     j->launched = false;
     const resource_grid_reader& reader = grid.get_reader();
     const bool                  empty  = reader.is_empty();
-    const int r = sector >= 0 ? group->join(sector, context.slot.system_slot(), !empty) : -1;
-    if (r >= 0) {
-      stage_grid(*j, reader, group->input(r, sector));
-      group->written(r, sector);
-      j->round         = r;
+    const int e = (sector >= 0 && !empty) ? group->acquire(sector) : -1;
+    if (e >= 0) {
+      // Grouped: the rows go into this sector's staging entry, modulated in the group's next launch.
+      stage_grid(*j, reader, group->input(sector, e));
+      group->submit(sector, e, context.slot.subframe_slot_index());
+      j->entry         = e;
       j->subframe_slot = context.slot.subframe_slot_index();
       j->launched      = true;
     } else if (!empty) {
@@ -815,9 +816,10 @@ private:
   void recycle(job_ptr j)
   {
     if (j) {
-      if (j->round >= 0) {
-        group->release(j->round);
-        j->round = -1;
+      if (j->entry >= 0) {
+        group->ready(sector, j->entry, true);  // a late or dropped request's launch may still write the entry
+        group->release(sector, j->entry);
+        j->entry = -1;
       }
       std::lock_guard<std::mutex> lock(free_mtx);
       free_jobs.push_back(std::move(j));
@@ -825,7 +827,7 @@ private:
   }
 
   std::shared_ptr<lower_phy_sector_group> group_owner;
-  sector_rounds*                  group  = nullptr;
+  ofdm_batcher*                   group  = nullptr;
   int                             sector = -1;  ///< index in the group, -1: not grouped
   std::shared_ptr<srsgpu_context> owner;
   srsgpu_context*                 ctx;
@@ -912,7 +914,7 @@ public:
       gpu::hip_check(hipEventCreateWithFlags(&stages.back()->done, hipEventDisableTiming), WHO, "event");
     }
     if (group_owner) {
-      group  = &group_owner->rounds(false, geo.nslot * geo.nsymb);
+      group  = &group_owner->batcher(false, geo.nslot * geo.nsymb);
       sector = group->add_sector(plans);
     }
   }
@@ -920,8 +922,9 @@ public:
   ~puxch_processor_gpu() override
   {
     for (const pending_symbol& ps : pending) {
-      if (ps.round >= 0) {
-        group->release(ps.round);
+      if (ps.entry >= 0) {
+        group->ready(sector, ps.entry, true);  // the launch still writes the entry
+        group->release(sector, ps.entry);
       }
     }
     if (sector >= 0) {
@@ -966,27 +969,23 @@ private:
         current_grid = std::move(r.payload);
       }
     }
-    const unsigned l   = context.nof_symbols;
-    const uint64_t key = static_cast<uint64_t>(context.slot.system_slot()) * geo.nsymb + l;
+    const unsigned l = context.nof_symbols;
     if (!current_grid) {
-      if (sector >= 0) {
-        group->join(sector, key, false);  // the group's round for this symbol stops waiting for this sector
-      }
       return false;
     }
     const unsigned s = context.slot.subframe_slot_index() * geo.nsymb + l;
     const unsigned n = geo.size[s];
-    // Grouped: the samples go into the group's round for this symbol, launched with the other sectors' samples.
-    const int r = sector >= 0 ? group->join(sector, key, true) : -1;
-    if (r >= 0) {
-      uint8_t* dst = group->input(r, sector);
+    // Grouped: the samples go into this sector's staging entry, demodulated in the group's next launch.
+    const int e = sector >= 0 ? group->acquire(sector) : -1;
+    if (e >= 0) {
+      uint8_t* dst = group->input(sector, e);
       for (unsigned p = 0; p != nof_ports; ++p) {
         span<const cf_t> in = samples.get_channel_buffer(p);
         srsran_assert(in.size() == n, "The input buffer size ({}) does not match the symbol size ({}).", in.size(), n);
         std::memcpy(dst + static_cast<size_t>(p) * n * sizeof(cf_t), in.data(), n * sizeof(cf_t));
       }
-      group->written(r, sector);
-      pending.push_back({l, context, r});
+      group->submit(sector, e, s);
+      pending.push_back({l, context, e});
       if (l == geo.nsymb - 1) {
         drain(0);
         current_grid.release();
@@ -1047,15 +1046,15 @@ private:
     while (!pending.empty()) {
       const pending_symbol& ps = pending.front();
       const uint8_t*        rows;
-      if (ps.round >= 0) {
-        if (!group->ready(ps.round, pending.size() > keep)) {
+      if (ps.entry >= 0) {
+        if (!group->ready(sector, ps.entry, pending.size() > keep)) {
           break;
         }
-        rows = group->output(ps.round, sector);
+        rows = group->output(sector, ps.entry);
       } else {
         symbol_stage& st = *stages[ps.symbol];
         if (pending.size() > keep) {
-          gpu::hip_check(hipEventSynchronize(st.done), WHO, "demodulation");
+          wait_event(st.done, WHO);
         } else if (hipEventQuery(st.done) != hipSuccess) {
           break;
         }
@@ -1068,8 +1067,8 @@ private:
                                                                                     sizeof(uint32_t)),
                                        nsc));
       }
-      if (ps.round >= 0) {
-        group->release(ps.round);
+      if (ps.entry >= 0) {
+        group->release(sector, ps.entry);
       }
       notifier->on_rx_symbol(current_grid, ps.context);
       pending.pop_front();
@@ -1079,11 +1078,11 @@ private:
   struct pending_symbol {
     unsigned                    symbol;
     lower_phy_rx_symbol_context context;
-    int                         round;  ///< the group's round holding the result, -1: this processor's own stage
+    int                         entry;  ///< the group staging entry holding the result, -1: this processor's own stage
   };
 
   std::shared_ptr<lower_phy_sector_group>    group_owner;
-  sector_rounds*                             group  = nullptr;
+  ofdm_batcher*                              group  = nullptr;
   int                                        sector = -1;  ///< index in the group, -1: not grouped
   std::shared_ptr<srsgpu_context>            owner;
   srsgpu_context*                            ctx;

@@ -85,17 +85,18 @@ std::shared_ptr<puxch_processor_factory> create_puxch_processor_factory_gpu(int 
 /// The sectors of one GPU as a group (integration/lower_phy_gpu.cpp). The reference runs one lower-PHY sector per cell,
 /// each with its own processors driven by its own real-time thread (lib/ru/generic/ru_factory_generic_impl.cpp:75-90);
 /// the processors made by a group's factories stay one per sector and keep the reference's per-sector behaviour and
-/// notifications, but the same symbol (UL) or slot (DL) of every sector runs as ONE launch: one upload of all sectors'
-/// samples (grids), one OFDM launch over all sectors' ports, one download. A round launches as soon as every sector has
-/// delivered (a sector without a request for that symbol reports itself absent), or `gather_window_us` after its first
-/// sector arrived; a sector arriving after its round launched, or beyond `nof_sectors`, runs on its own as the
-/// ungrouped processors do. Sectors group when they share numerology, cyclic prefix, DFT size, bandwidth, DFT window
-/// offset and number of ports (carrier frequencies may differ); otherwise each runs on its own.
+/// notifications, but their OFDM work is batched: the symbols (UL) or slots (DL) the sectors submit at about the same
+/// time run as ONE launch over every sector's ports, reading the samples (grids) and writing the grids (samples) in
+/// place in mapped host memory. A launch goes out once every active sector has work waiting, or the gather window
+/// after the oldest waiting work; no sector waits for a particular other one. Sectors batch when they share
+/// numerology, cyclic prefix, DFT size (not the split sizes), bandwidth, DFT window offset and number of ports
+/// (carrier frequencies may differ); a sector that cannot (or finds its staging full) runs on its own as the ungrouped
+/// processors do.
 struct lower_phy_group_configuration {
-  int      device          = 0;
-  unsigned nof_sectors     = 1;    ///< processors of each direction expected in a round (at most 32).
-  unsigned ul_window_us    = 300;  ///< how long a partly filled UL round waits for its missing sectors.
-  unsigned dl_window_us    = 300;  ///< the same for DL rounds (requests arrive slots ahead of transmission).
+  int      device       = 0;
+  unsigned nof_sectors  = 1;    ///< sectors of each direction the group takes (at most 32).
+  unsigned ul_window_us = 50;   ///< how long a UL launch waits for active sectors still to submit.
+  unsigned dl_window_us = 100;  ///< the same for DL launches (requests arrive slots ahead of transmission).
 };
 class lower_phy_sector_group;
 std::shared_ptr<lower_phy_sector_group> create_lower_phy_sector_group(const lower_phy_group_configuration& config);
@@ -103,10 +104,11 @@ std::shared_ptr<pdxch_processor_factory> create_pdxch_processor_factory_gpu(std:
 std::shared_ptr<puxch_processor_factory> create_puxch_processor_factory_gpu(std::shared_ptr<lower_phy_sector_group> group,
                                                                             unsigned max_symbols_in_flight = 0);
 
-/// Rounds a group has launched (UL, DL) and symbols / slots that ran on their own instead (for tests and benchmarks).
+/// Launches a group made (UL, DL), the sector symbols / slots they ran, those that ran alone instead and the launches
+/// the gather window sent (for tests and benchmarks).
 struct lower_phy_group_counters {
-  uint64_t ul_rounds = 0, ul_grouped = 0, ul_alone = 0;
-  uint64_t dl_rounds = 0, dl_grouped = 0, dl_alone = 0;
+  uint64_t ul_launches = 0, ul_batched = 0, ul_alone = 0, ul_windowed = 0;
+  uint64_t dl_launches = 0, dl_batched = 0, dl_alone = 0, dl_windowed = 0;
 };
 lower_phy_group_counters get_lower_phy_group_counters(const lower_phy_sector_group& group);
 

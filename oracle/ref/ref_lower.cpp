@@ -37,6 +37,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <sys/prctl.h>
 #include <thread>
 #include <vector>
 
@@ -230,6 +231,19 @@ struct pacer {
   double            final_lag = 0;
   long              late      = 0;
   long              i         = 0;
+  clock::time_point call;            ///< start of the current process_symbol call
+  double            max_call   = 0;  ///< longest process_symbol call (s)
+  long              calls_over = 0;  ///< calls longer than one symbol duration
+
+  void done()
+  {
+    if (period.count() == 0) {
+      return;
+    }
+    const auto d = clock::now() - call;
+    max_call     = std::max(max_call, std::chrono::duration<double>(d).count());
+    calls_over += d > period ? 1 : 0;
+  }
 
   void next()
   {
@@ -239,17 +253,16 @@ struct pacer {
     const clock::time_point due = start + period * i++;
     clock::time_point       now = clock::now();
     if (now < due) {
-      if (due - now > std::chrono::microseconds(60)) {
-        std::this_thread::sleep_until(due - std::chrono::microseconds(50));
-      }
-      while (clock::now() < due) {
-      }
+      // Sleep (the thread of a radio unit blocks on its baseband device): spinning sectors would take the CPUs the
+      // processors need. The thread's timer slack is 1 us (set_timer_slack), so the wake-up lands within microseconds.
+      std::this_thread::sleep_until(due);
       final_lag = 0;
     } else {
       final_lag = std::chrono::duration<double>(now - due).count();
       max_lag   = std::max(max_lag, final_lag);
       late += (now - due) > slot ? 1 : 0;
     }
+    call = clock::now();
   }
 };
 
@@ -299,6 +312,9 @@ long run_pdxch_script(pdxch_processor&  proc,
         pace->next();
       }
       processed_out[nflag++] = proc.get_baseband().process_symbol(buf, ctx) ? 1 : 0;
+      if (pace != nullptr) {
+        pace->done();
+      }
       pos += need;
     }
   }
@@ -336,6 +352,9 @@ void run_puxch_script(puxch_processor& proc,
         pace->next();
       }
       processed_out[nflag++] = proc.get_baseband().process_symbol(buf, ctx) ? 1 : 0;
+      if (pace != nullptr) {
+        pace->done();
+      }
       pos += static_cast<long>(n) * sc.nof_ports;
     }
   }
@@ -472,11 +491,11 @@ int ref_lower_puxch_run(int          variant,
 /// script. Variant 3: the sectors' GPU processors come from one lower_phy_sector_group (window_us: its gather windows,
 /// 0 = defaults). Outputs per sector k at k x the stride of one sector: DL samples (dl_cap < 0: a ring per sector, as
 /// ref_lower_pdxch_run), DL and UL return flags, UL grids, UL notifications (nof_rx[k] pairs) and late slots
-/// (nof_late[k], DL then UL); seconds[2k], seconds[2k+1]: the sector's DL and UL script wall time. group_counts (6
-/// values, variant 3): lower_phy_group_counters. paced != 0: every sector runs at the radio's pace, one symbol per
-/// symbol duration (1 ms / symbols per subframe) from a common start; lag[6k .. 6k+5]: sector k's DL and UL largest
+/// (nof_late[k], DL then UL); seconds[2k], seconds[2k+1]: the sector's DL and UL script wall time. group_counts (8
+/// values, variant 3): lower_phy_group_counters in declaration order. paced != 0: every sector runs at the radio's pace, one symbol per
+/// symbol duration (1 ms / symbols per subframe) from a common start; lag[10k .. 10k+9]: sector k's DL and UL largest
 /// lag behind that pace (s), DL and UL lag at the last symbol (s), DL and UL fraction of symbols started more than one
-/// slot behind. Returns 0, -1 on a sample overflow.
+/// slot behind, DL and UL longest process_symbol call (s), DL and UL fraction of calls longer than a symbol. Returns 0, -1 on a sample overflow.
 int ref_lower_sectors_run(int             variant,
                           int             max_in_flight,
                           int             nof_sectors,
@@ -560,6 +579,9 @@ int ref_lower_sectors_run(int             variant,
   std::array<clock::time_point, 2> start;
   for (int k = 0; k < nof_sectors; ++k) {
     threads.emplace_back([&, k]() {
+      if (period.count() != 0) {
+        (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);  // 1 us timer slack: paced sleeps wake on time
+      }
       pacer pdl, pul;
       pdl.period = pul.period = period;
       pdl.slot = pul.slot = period * static_cast<long>(sc.nsymb());
@@ -583,8 +605,9 @@ int ref_lower_sectors_run(int             variant,
                        ul_processed + static_cast<size_t>(k) * n_ul_proc, &pul);
       seconds[2 * k + 1] = std::chrono::duration<double>(clock::now() - t0).count();
       const double nd = static_cast<double>(std::max(1L, pdl.i)), nu = static_cast<double>(std::max(1L, pul.i));
-      const double v[6] = {pdl.max_lag, pul.max_lag, pdl.final_lag, pul.final_lag, pdl.late / nd, pul.late / nu};
-      std::copy(v, v + 6, lag + 6 * k);
+      const double v[10] = {pdl.max_lag,  pul.max_lag,  pdl.final_lag,       pul.final_lag,       pdl.late / nd,
+                            pul.late / nu, pdl.max_call, pul.max_call, pdl.calls_over / nd, pul.calls_over / nu};
+      std::copy(v, v + 10, lag + 10 * k);
     });
   }
   for (std::thread& t : threads) {
@@ -603,8 +626,9 @@ int ref_lower_sectors_run(int             variant,
   }
   if (group) {
     const lower_phy_group_counters c = get_lower_phy_group_counters(*group);
-    const uint64_t                 v[6] = {c.ul_rounds, c.ul_grouped, c.ul_alone, c.dl_rounds, c.dl_grouped, c.dl_alone};
-    std::copy(v, v + 6, group_counts);
+    const uint64_t v[8] = {c.ul_launches, c.ul_batched, c.ul_alone, c.ul_windowed,
+                           c.dl_launches, c.dl_batched, c.dl_alone, c.dl_windowed};
+    std::copy(v, v + 8, group_counts);
   }
   for (long p : produced) {
     if (p < 0) {

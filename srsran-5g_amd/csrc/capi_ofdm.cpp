@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <cstddef>
 #include <vector>
 
 using namespace srsgpu;
@@ -309,6 +310,56 @@ int srsgpu_ofdm_plan_concat(srsgpu_context*                ctx,
     return fail(SRSGPU_ERR_HIP, "failed to allocate the split-transform scratch");
   }
   *plan_out = plan;
+  return SRSGPU_OK;
+}
+
+static_assert(sizeof(srsgpu_ofdm_job) == sizeof(ofdm_job) && offsetof(srsgpu_ofdm_job, sample_offset) ==
+                  offsetof(ofdm_job, sample_offset) && offsetof(srsgpu_ofdm_job, cp_len) == offsetof(ofdm_job, cp_len) &&
+                  offsetof(srsgpu_ofdm_job, coef_re) == offsetof(ofdm_job, coef_re),
+              "srsgpu_ofdm_job is the kernel's job layout");
+
+int srsgpu_ofdm_plan_get_jobs(const srsgpu_ofdm_plan* plan, srsgpu_ofdm_job* jobs, uint32_t capacity, uint32_t* nof_jobs)
+{
+  if (plan == nullptr || nof_jobs == nullptr || (jobs == nullptr && capacity > 0)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  *nof_jobs      = static_cast<uint32_t>(plan->nof_jobs);
+  const size_t n = std::min<size_t>(capacity, static_cast<size_t>(plan->nof_jobs));
+  if (n > 0) {
+    std::lock_guard<std::mutex> lock(plan->ctx->mtx);
+    HIP_TRY(hipSetDevice(plan->ctx->device));
+    HIP_TRY(hipMemcpy(jobs, plan->d_jobs, n * sizeof(ofdm_job), hipMemcpyDeviceToHost));
+  }
+  return SRSGPU_OK;
+}
+
+int srsgpu_ofdm_jobs_execute(const srsgpu_ofdm_plan* plan,
+                             const srsgpu_ofdm_job*  d_jobs,
+                             uint32_t                nof_jobs,
+                             const void*             d_in,
+                             void*                   d_out,
+                             void*                   stream)
+{
+  if (plan == nullptr || d_in == nullptr || d_out == nullptr || (d_jobs == nullptr && nof_jobs > 0)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  if (ofdm_split_factor(plan->dft_size) != 0) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "job lists do not run the split DFT sizes (%u points)", plan->dft_size);
+  }
+  if (nof_jobs == 0) {
+    return SRSGPU_OK;
+  }
+  const auto* jobs = reinterpret_cast<const ofdm_job*>(d_jobs);
+  if (plan->inverse) {
+    launch_ofdm(true, plan->dft_size, jobs, static_cast<int>(nof_jobs), plan->nsc, 0, plan->ctx->d_ofdm_twiddles,
+                static_cast<const uint32_t*>(d_in), nullptr, nullptr, static_cast<float*>(d_out), nullptr,
+                static_cast<hipStream_t>(stream));
+  } else {
+    launch_ofdm(false, plan->dft_size, jobs, static_cast<int>(nof_jobs), plan->nsc, plan->window_off,
+                plan->ctx->d_ofdm_twiddles, nullptr, static_cast<uint32_t*>(d_out), static_cast<const float*>(d_in),
+                nullptr, nullptr, static_cast<hipStream_t>(stream));
+  }
+  HIP_TRY(hipGetLastError());
   return SRSGPU_OK;
 }
 

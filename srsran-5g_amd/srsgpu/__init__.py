@@ -394,6 +394,8 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_ofdm_plan_nof_grid_words.argtypes = [P]
     lib.srsgpu_ofdm_plan_nof_grid_words.restype = ctypes.c_uint64
     lib.srsgpu_ofdm_plan_concat.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(P)]
+    lib.srsgpu_ofdm_plan_get_jobs.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    lib.srsgpu_ofdm_jobs_execute.argtypes = [P, P, ctypes.c_uint32, P, P, P]
     lib.srsgpu_ofdm_plan_sample_offset.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     lib.srsgpu_ofdm_plan_sample_offset.restype = ctypes.c_uint64
     lib.srsgpu_ofdm_modulator_plan_execute.argtypes = [P, P, P, P]
@@ -423,7 +425,8 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_modulator_plan_create", "srsgpu_ofdm_demodulator_plan_create", "srsgpu_ofdm_plan_nof_samples",
     "srsgpu_ofdm_modulator_symbols_plan_create", "srsgpu_ofdm_demodulator_symbols_plan_create", "srsgpu_harq_copy",
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
-    "srsgpu_ofdm_plan_concat", "srsgpu_ofdm_plan_nof_grid_words",
+    "srsgpu_ofdm_plan_concat", "srsgpu_ofdm_plan_nof_grid_words", "srsgpu_ofdm_plan_get_jobs",
+    "srsgpu_ofdm_jobs_execute",
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
     "srsgpu_pusch_demodulator_plan_create_ex", "srsgpu_pusch_demodulator_plan_execute_ex",
@@ -1452,6 +1455,22 @@ class OfdmPlan:
 
     def sample_offset(self, grid: int, port: int) -> int:
         return int(_lib.srsgpu_ofdm_plan_sample_offset(self.handle, grid, port))
+
+    OFDM_JOB = np.dtype([("grid_offset", "<u4"), ("sample_offset", "<u4"), ("cp_len", "<u4"), ("reserved", "<u4"),
+                         ("coef_re", "<f4"), ("coef_im", "<f4")])
+
+    def jobs(self) -> np.ndarray:
+        """srsgpu_ofdm_plan_get_jobs: the plan's (grid, port, symbol) jobs as a structured array (OFDM_JOB)."""
+        n = ctypes.c_uint32()
+        _check(_lib.srsgpu_ofdm_plan_get_jobs(self.handle, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, self.OFDM_JOB)
+        _check(_lib.srsgpu_ofdm_plan_get_jobs(self.handle, out.ctypes.data, n.value, ctypes.byref(n)))
+        return out
+
+    def execute_jobs(self, d_jobs, nof_jobs: int, d_in, d_out, stream=None):
+        """srsgpu_ofdm_jobs_execute: a caller-assembled job list with this plan's launch parameters."""
+        _check(_lib.srsgpu_ofdm_jobs_execute(self.handle, _dptr(d_jobs), nof_jobs, _dptr(d_in), _dptr(d_out),
+                                             _stream_handle(stream)))
 
     def execute(self, d_in, d_out, stream=None):
         f = _lib.srsgpu_ofdm_modulator_plan_execute if self.inverse else _lib.srsgpu_ofdm_demodulator_plan_execute

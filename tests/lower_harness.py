@@ -95,8 +95,8 @@ class Lower:
         (S, G, P, nsymb, nsc, 2) uint16 and masks (S, G): each sector's DL grids; ul_samples (S, n) complex64.
         Returns a dict: per-sector lists dl (samples, flags, late DL+UL mixed in 'late'), ul (grids, flags, rx), late,
         seconds (S, 2) DL/UL wall time, group counters (variant 3) and, paced (one symbol per symbol duration), lag
-        (S, 6): DL, UL largest lag behind the pace (s), DL, UL lag at the last symbol, DL, UL fraction of symbols more
-        than a slot behind."""
+        (S, 10): DL, UL largest lag behind the pace (s), DL, UL lag at the last symbol, DL, UL fraction of symbols more
+        than a slot behind, DL, UL longest process_symbol call (s), DL, UL fraction of calls longer than a symbol."""
         S = len(freqs)
         nsymb = 12 if cfg["extended"] else 14
         P = cfg["nof_ports"]
@@ -115,8 +115,8 @@ class Lower:
         late = np.zeros((S, len(dl_ev) + len(ul_ev) + 1), np.int32)
         nlate = np.zeros(S, np.int32)
         secs = np.zeros((S, 2), np.float64)
-        counts = np.zeros(6, np.uint64)
-        lag = np.zeros((S, 6), np.float64)
+        counts = np.zeros(8, np.uint64)
+        lag = np.zeros((S, 10), np.float64)
         fr = np.ascontiguousarray(freqs, np.float64)
         g = np.ascontiguousarray(grids, np.uint16)
         m = np.ascontiguousarray(masks, np.uint32)
@@ -135,6 +135,6 @@ class Lower:
             "late": [late[k, : nlate[k]].tolist() for k in range(S)],
             "seconds": secs,
             "lag": lag,
-            "group": dict(zip(("ul_rounds", "ul_grouped", "ul_alone", "dl_rounds", "dl_grouped", "dl_alone"),
-                              counts.tolist())),
+            "group": dict(zip(("ul_launches", "ul_batched", "ul_alone", "ul_windowed", "dl_launches", "dl_batched",
+                               "dl_alone", "dl_windowed"), counts.tolist())),
         }

@@ -143,3 +143,50 @@ def test_ofdm_plan_concat_sector_group(ctx, inverse):
     odd = srsgpu.OfdmPlan(ctx, inverse, 1, 52, 2048, 1.0, 3.5e9, [0], P, symbols=(0, 1))
     with pytest.raises(srsgpu.SrsGpuError):
         srsgpu.OfdmPlan.concat([members[0], odd])
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_ofdm_job_list_equals_plans(ctx, inverse):
+    """srsgpu_ofdm_jobs_execute (the lower-PHY sector group's launch): the jobs of three sectors' plans (own carrier,
+    scaling, slot and symbol), reordered and placed at offsets of the caller's choosing in one buffer pair, give bit for
+    bit what each plan gives on its own buffers; a split DFT size is refused."""
+    import torch
+    import srsgpu
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(37)
+    P = 2
+    members = [srsgpu.OfdmPlan(ctx, inverse, 1, 106, 2048, sc, fc, [slot], P, window_offset=0 if inverse else 40,
+                               symbols=(l, 1))
+               for sc, fc, slot, l in ((0.5, 3.5e9, 0, 0), (0.25, 3.6e9, 1, 7), (1.0, 1.8e9, 1, 13))]
+    # Member i's buffers sit at (word_base[i], sample_base[i]) of the shared buffers, in reverse order with gaps.
+    word_base = [3 * 4096 + 7, 1 * 4096 + 5, 0 + 3][:3]
+    sample_base = [9000 * 2 + 11, 9000 + 13, 17]
+    jobs = []
+    for i, m in enumerate(members):
+        j = m.jobs()
+        assert len(j) == P
+        j["grid_offset"] += word_base[i]
+        j["sample_offset"] += sample_base[i]
+        jobs.append(j)
+    jobs = np.concatenate(jobs)[::-1].copy()  # any order
+    words, samples = 5 * 4096, 4 * 9000
+    d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
+    if inverse:
+        src = torch.from_numpy(rng.integers(0, 1 << 14, 2 * words).astype(np.uint16).view(np.int32).copy()).to(dev)
+        out = torch.zeros(2 * samples, dtype=torch.float32, device=dev)
+    else:
+        src = torch.from_numpy((rng.normal(size=2 * samples) * 0.1).astype(np.float32)).to(dev)
+        out = torch.zeros(words, dtype=torch.int32, device=dev)
+    members[0].execute_jobs(d_jobs, len(jobs), src, out)
+    for i, m in enumerate(members):
+        if inverse:
+            o = torch.zeros(2 * m.nof_samples, dtype=torch.float32, device=dev)
+            m.execute(src[word_base[i]:word_base[i] + m.grid_words].clone(), o)
+            assert torch.equal(o, out[2 * sample_base[i]:2 * (sample_base[i] + m.nof_samples)]), i
+        else:
+            o = torch.zeros(m.grid_words, dtype=torch.int32, device=dev)
+            m.execute(src[2 * sample_base[i]:2 * (sample_base[i] + m.nof_samples)].clone(), o)
+            assert torch.equal(o, out[word_base[i]:word_base[i] + m.grid_words]), i
+    split = srsgpu.OfdmPlan(ctx, inverse, 1, 273, 12288, 1.0, 3.5e9, [0], 1, symbols=(0, 1))
+    with pytest.raises(srsgpu.SrsGpuError):
+        split.execute_jobs(d_jobs, 1, src, out)

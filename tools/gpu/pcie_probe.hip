@@ -54,6 +54,34 @@ int main()
   std::memset(h_def, 1, maxb * 4);
   std::memset(h_coh, 1, maxb * 4);
   std::memset(h_out, 1, maxb * 4);
+  // CPU side: memcpy into / out of each kind of host memory (what a sector thread does per symbol).
+  {
+    std::vector<char> src(maxb), dst(maxb);
+    std::memset(src.data(), 3, maxb);
+    char* plain = static_cast<char*>(std::malloc(maxb));
+    std::memset(plain, 0, maxb);
+    struct {
+      const char* name;
+      char*       p;
+    } kinds[] = {{"malloc", plain}, {"hipHostMalloc default", h_def}, {"hipHostMalloc coherent|mapped", h_coh}};
+    for (auto& k : kinds) {
+      for (size_t b : {size_t(142336), size_t(53248)}) {
+        auto t0 = clk::now();
+        for (int r = 0; r < 2000; ++r) {
+          std::memcpy(k.p + (r % 8) * b, src.data() + (r % 8) * b, b);
+        }
+        double tw = since(t0) / 2000;
+        t0        = clk::now();
+        for (int r = 0; r < 2000; ++r) {
+          std::memcpy(dst.data() + (r % 8) * b, k.p + (r % 8) * b, b);
+        }
+        double tr = since(t0) / 2000;
+        std::printf("cpu %s bytes %zu: write %.1f us (%.1f GB/s), read %.1f us (%.1f GB/s)\n", k.name, b, tw * 1e6,
+                    b / tw / 1e9, tr * 1e6, b / tr / 1e9);
+      }
+    }
+    std::free(plain);
+  }
   for (size_t b : sizes) {
     // DMA H2D, 1 and 3 streams (each stream its own slice).
     for (int ns : {1, 3}) {

@@ -61,8 +61,9 @@ for step in "$@"; do
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kstats" -o k -- python3 -u bench.py \
         > "$OUT/kstats_bench.json" 2> "$OUT/kstats.log" || { tail -20 "$OUT/kstats.log"; exit 1; } ;;
     lower)
+      echo "cgroup cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null || echo n/a), nproc $(nproc)"
       timeout -k 10 400 python -u tools/lower_phy_bench.py --sectors 1,2,4,6,8,12 \
-        --sweep-only cpu,gpu0,gpu4,group0,group4,group13 > "$OUT/lower.json" 2> "$OUT/lower.log" \
+        --sweep-only cpu,gpu0,gpu4,gpu13,group0,group4,group13 > "$OUT/lower.json" 2> "$OUT/lower.log" \
         || { tail -20 "$OUT/lower.log"; exit 1; }
       tail -c 800 "$OUT/lower.json" ;;
     lower_trace)

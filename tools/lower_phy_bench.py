@@ -18,6 +18,7 @@ TEST INFRASTRUCTURE (diagnostic); GPU box:
 """
 import argparse
 import json
+import resource
 import os
 import sys
 import time
@@ -115,7 +116,10 @@ def sweep(lower, args, grids, mask, dl, ul, samples):
             # Paced: every sector at the radio's symbol rate from a common start. It keeps real
             # time when it ends less than a slot behind and under 1 % of its symbols started more than a slot late
             # (this host is no real-time system: a lone scheduling hiccup is forgiven, a growing lag is not).
+            ru0, t0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
             p = lower.sectors(variant, CFG, freqs, g, m, dl, ul, samples, inflight, ring=RING, window_us=w, paced=True)
+            ru1, t1 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
+            cpus = (ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime) / (t1 - t0)
             lag = p["lag"]
             res[key][str(nsec)] = {
                 "free_running": {
@@ -126,6 +130,9 @@ def sweep(lower, args, grids, mask, dl, ul, samples):
                 "paced_max_lag_us": {"pdxch": 1e6 * lag[:, 0].max(), "puxch": 1e6 * lag[:, 1].max()},
                 "paced_final_lag_us": {"pdxch": 1e6 * lag[:, 2].max(), "puxch": 1e6 * lag[:, 3].max()},
                 "paced_late_fraction": {"pdxch": lag[:, 4].max(), "puxch": lag[:, 5].max()},
+                "paced_cpus_busy": cpus,
+                "paced_longest_call_us": {"pdxch": 1e6 * lag[:, 6].max(), "puxch": 1e6 * lag[:, 7].max()},
+                "paced_calls_over_a_symbol": {"pdxch": lag[:, 8].max(), "puxch": lag[:, 9].max()},
                 "late": sum(len(v) for v in r["late"]) + sum(len(v) for v in p["late"]),
                 "notifications": sum(len(u[2]) for u in p["ul"]),
                 "real_time": bool(lag[:, 2:4].max() < MAX_LAG and lag[:, 4:6].max() < 0.01)}

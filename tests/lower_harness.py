@@ -125,8 +125,8 @@ class Lower:
             variant, max_in_flight, S, cfg["numerology"], cfg["bw_rb"], cfg["dft_size"], int(cfg["extended"]),
             cfg["window_offset"], _ptr(fr), P, G, window_us, _ptr(g), _ptr(m), len(dl_ev), _ptr(dl_ev), _ptr(dl_out),
             cap if ring is None else -cap, _ptr(dl_flags), len(ul_ev), _ptr(ul_ev), _ptr(x),
-            x.shape[1] if x.ndim == 2 else 0, _ptr(ul_grids), _ptr(ul_flags), _ptr(rx), _ptr(nrx), _ptr(late), _ptr(nlate), _ptr(secs), _ptr(counts), int(paced),
-            _ptr(lag))
+            x.shape[1] if x.ndim == 2 else 0, _ptr(ul_grids), _ptr(ul_flags), _ptr(rx), _ptr(nrx), _ptr(late),
+            _ptr(nlate), _ptr(secs), _ptr(counts), int(paced), _ptr(lag))
         assert r == 0
         return {
             "dl": [(dl_out[k].view(np.complex64), dl_flags[k, :n_dl]) for k in range(S)],

@@ -199,6 +199,15 @@ __device__ __forceinline__ void job_sum_n(float (&v)[K], float* red)
   }
 }
 
+/// Early first-pilot loads (round 5, verdict item 2): 1 issues each lane's first pilot grid loads before the sequence
+/// staging. With the lane guard it passes the estimator tests (round 4's unguarded version faulted), but it does not
+/// pay: estimator stage 36.6-37.1 vs 36.3-36.6 us per step, headline 143.8k vs 143.9k slots/s, two alternating runs
+/// each (profiles/r5_chest_early_pilots_ab.txt). Off by default.
+#ifndef CHEST_EARLY_PILOTS
+#define CHEST_EARLY_PILOTS 0
+#endif
+constexpr int CHEST_EARLY = 4;  ///< DM-RS symbols whose first pilot is loaded early
+
 /// Ordering of a job's LDS stages: a workgroup barrier; in a one-wave workgroup (T = 64, where the 32-lane halves may
 /// run jobs with different stage sequences) a wave-level fence: a wave's LDS accesses complete in program order.
 template <int T>
@@ -544,6 +553,28 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(CHEST_WAVES_P
   const int        NP    = geom.max_pilots;
   cpx* const       Fbase = L.F;
 
+#if CHEST_EARLY_PILOTS
+  // The grid values of each lane's first pilot on the first CHEST_EARLY DM-RS symbols, issued before the sequence
+  // staging so the two memory round trips overlap (the staging barrier waits for both). Only lanes that hold a pilot
+  // (lane < N) compute a subcarrier: pilot_subcarrier reads the job's CRB list at rb = lane / pilots per RB, which lies
+  // beyond the list (and, for the plan's last job, beyond the buffer) for the lanes past the last pilot. Round 4's
+  // unguarded version faulted exactly there (an illegal address in the CFO / TA golden test).
+  cpx e0{}, e1{}, e2{}, e3{};  // named registers (an array here lands in scratch)
+  if (lane < N) {
+    const uint32_t  k   = pilot_subcarrier(jb, crbs, lane);
+    const uint32_t* row = grids + jb.grid_base + k;
+    e0                  = bf16c(row[jb.dmrs_symbols[0] * jb.nsc]);
+    if (D > 1) {
+      e1 = bf16c(row[jb.dmrs_symbols[1] * jb.nsc]);
+    }
+    if (D > 2) {
+      e2 = bf16c(row[jb.dmrs_symbols[2] * jb.nsc]);
+    }
+    if (D > 3) {
+      e3 = bf16c(row[jb.dmrs_symbols[3] * jb.nsc]);
+    }
+  }
+#endif
   // Stage: taps and the sequence words of every DM-RS symbol (the plan's resident words, gold_fill_kernel).
   if (lane < 32) {
     L.taps[lane] = jb.taps[lane];
@@ -563,7 +594,16 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(CHEST_WAVES_P
     const uint32_t k = pilot_subcarrier(jb, crbs, i);
     const int      m = pilot_seq_index(jb, crbs, i);
     for (int s = 0; s < D; ++s) {
+#if CHEST_EARLY_PILOTS
+      cpx y;
+      if (i == lane && s < CHEST_EARLY) {
+        y = s == 0 ? e0 : s == 1 ? e1 : s == 2 ? e2 : e3;
+      } else {
+        y = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
+      }
+#else
       const cpx y = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
+#endif
       const cpx p = dmrs_value(jb, lp, L.seq, W, s, n0, m, i);
       L.Y[s * NP + i] = {y.x * p.x + y.y * p.y, y.y * p.x - y.x * p.y};
       epre_acc += y.x * y.x + y.y * y.y;

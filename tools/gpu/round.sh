@@ -13,7 +13,8 @@
 #   slots_trace      rocprofv3 kernel + memory-copy trace of the slot processors at one thread (UL)
 #   kstats           rocprofv3 --kernel-trace --stats of the default bench
 #   lower            tools/lower_phy_bench.py with the multi-sector sweep
-#   lower_trace      rocprofv3 kernel + memory-copy trace of the GPU processors at 8 sectors
+#   lower_trace      rocprofv3 kernel trace of the sector group at 8 sectors
+#   ab:DIR[:N]       A/B of the default bench: the in-tree library against srsran-5g_amd/DIR's, N rounds
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -70,6 +71,17 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/lower_trace" -o lower -- python3 -u \
         tools/lower_phy_bench.py --slots 100 --sectors 8 --sweep-only group4 > "$OUT/lower_trace.json" \
         2> "$OUT/lower_trace.log" || { tail -20 "$OUT/lower_trace.log"; exit 1; } ;;
+    ab:*)
+      # ab:DIR[:N] — the default bench N times (default 2), alternating the in-tree library and srsran-5g_amd/DIR's
+      SPEC=${step#ab:}; DIR=${SPEC%%:*}; N=2; [[ "$SPEC" == *:* ]] && N=${SPEC##*:}
+      for i in $(seq 1 "$N"); do
+        for lib in lib "$DIR"; do
+          SRSGPU_LIB=srsran-5g_amd/$lib/libsrsgpu_phy.so timeout -k 10 300 python -u bench.py \
+            > "$OUT/ab_${lib}_$i.json" 2> "$OUT/ab_${lib}_$i.err" || { tail -20 "$OUT/ab_${lib}_$i.err"; exit 1; }
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value']), d.get('stage_ms_per_step', ''))" \
+            "$OUT/ab_${lib}_$i.json" "$lib"
+        done
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

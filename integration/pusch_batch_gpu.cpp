@@ -511,6 +511,10 @@ public:
   /// Replays every PDU of `jobs` through the reference's processor from results at io_host (the staging image: result
   /// offsets of the launch plan) and msgs_host (the CB messages).
   void replay(const std::vector<std::unique_ptr<pusch_job>>& jobs, const uint8_t* io_host, const uint8_t* msgs_host);
+  /// One job's replay. Jobs of distinct batches replay concurrently on different threads, except those with a CSI Part 2
+  /// PDU (needs_second_phase), whose second launch uses this launcher's deferred-decode state: one thread at a time.
+  void        replay_job(pusch_job& job, const uint8_t* io_host, const uint8_t* msgs_host);
+  static bool needs_second_phase(const pusch_job& job);
 
   const launch_plan& current() const { return *plan; }
   /// The device result region [flag_o, end_o) and the CB messages of the current launch.
@@ -724,6 +728,8 @@ private:
 
   void dispatch_loop();
   void complete_loop();
+  void replay_loop();
+  void replay_share(launch_set& set);
   void launch(launch_set& set);
   void finish(launch_set& set);
   void fail_jobs(launch_set& set, const char* what);
@@ -746,6 +752,18 @@ private:
   std::thread                             dispatcher;
   std::thread                             completer;
 
+  // Replay helpers (cfg.replay_threads - 1 of them; the completion thread replays too): a launch's jobs are shared
+  // out through rp_next, one job at a time.
+  std::vector<std::thread> replayers;
+  std::mutex               rp_mtx;
+  std::condition_variable  rp_cv;       ///< new work or stop
+  std::condition_variable  rp_done_cv;  ///< a helper finished its share
+  launch_set*              rp_set    = nullptr;
+  std::atomic<size_t>      rp_next{0};
+  uint64_t                 rp_gen    = 0;
+  unsigned                 rp_busy   = 0;
+  bool                     rp_stop   = false;
+
   // SRSGPU_BATCH_TIMING=1: mean host-clock time per launch of each phase (diagnostics).
   const bool timing = std::getenv("SRSGPU_BATCH_TIMING") != nullptr;
   double     phase_us[5]   = {};  ///< build + plans, fill, graph + launch, wait for GPU, replay
@@ -767,6 +785,9 @@ pusch_gpu_service::pusch_gpu_service(const pusch_service_configuration& cfg_) :
   }
   dispatcher = std::thread([this] { dispatch_loop(); });
   completer  = std::thread([this] { complete_loop(); });
+  for (unsigned i = 1; i < cfg.replay_threads; ++i) {
+    replayers.emplace_back([this] { replay_loop(); });
+  }
 }
 
 pusch_gpu_service::~pusch_gpu_service()
@@ -780,6 +801,14 @@ pusch_gpu_service::~pusch_gpu_service()
   done_cv.notify_all();
   dispatcher.join();
   completer.join();
+  {
+    std::lock_guard<std::mutex> lock(rp_mtx);
+    rp_stop = true;
+  }
+  rp_cv.notify_all();
+  for (std::thread& t : replayers) {
+    t.join();
+  }
   if (timing && timed_launches > 0) {
     std::fprintf(stderr,
                  "pusch_gpu_service: %llu launches, %.2f slots per launch, us per launch: build %.1f, fill %.1f, "
@@ -924,6 +953,44 @@ void pusch_gpu_service::complete_loop()
       set->busy = false;
     }
     free_cv.notify_all();
+  }
+}
+
+/// Takes jobs of the shared launch one at a time and replays those without a second phase.
+void pusch_gpu_service::replay_share(launch_set& set)
+{
+  for (size_t i = rp_next++; i < set.jobs.size(); i = rp_next++) {
+    pusch_job& job = *set.jobs[i];
+    if (!pusch_launcher::needs_second_phase(job)) {
+      set.L.replay_job(job, set.L.host_io(), set.L.host_msgs());
+    }
+  }
+}
+
+void pusch_gpu_service::replay_loop()
+{
+  uint64_t seen = 0;
+  for (;;) {
+    launch_set* set = nullptr;
+    {
+      std::unique_lock<std::mutex> lock(rp_mtx);
+      rp_cv.wait(lock, [&] { return rp_stop || rp_gen != seen; });
+      if (rp_stop) {
+        return;
+      }
+      seen = rp_gen;
+      set  = rp_set;
+    }
+    try {
+      replay_share(*set);
+    } catch (const std::exception& e) {
+      fail_jobs(*set, e.what());
+    }
+    {
+      std::lock_guard<std::mutex> lock(rp_mtx);
+      --rp_busy;
+    }
+    rp_done_cv.notify_all();
   }
 }
 
@@ -1295,8 +1362,26 @@ void pusch_launcher::replay(const std::vector<std::unique_ptr<pusch_job>>& jobs,
                             const uint8_t*                                 io_host,
                             const uint8_t*                                 msgs_host)
 {
-  const launch_plan& lp = *plan;
   for (const auto& job : jobs) {
+    replay_job(*job, io_host, msgs_host);
+  }
+}
+
+bool pusch_launcher::needs_second_phase(const pusch_job& job)
+{
+  for (const pusch_entry& e : job.entries) {
+    if (e.csi2) {
+      return true;
+    }
+  }
+  return false;
+}
+
+void pusch_launcher::replay_job(pusch_job& job_ref, const uint8_t* io_host, const uint8_t* msgs_host)
+{
+  const launch_plan& lp  = *plan;
+  pusch_job*         job = &job_ref;
+  {
     replay_processor&                r    = job->batch->replay_for_this_thread();
     const pusch_batch_configuration& bcfg = job->batch->cfg;
     for (pusch_entry& e : job->entries) {
@@ -1318,7 +1403,7 @@ void pusch_launcher::replay(const std::vector<std::unique_ptr<pusch_job>>& jobs,
       r.dec->cb_KZ             = e.cb_KZ;
       r.dec->max_iter          = bcfg.nof_ldpc_iterations;
       if (e.csi2) {
-        r.demux->second_phase = [this, &e, &r, job = job.get()](unsigned bits, unsigned enc_bits, unsigned first,
+        r.demux->second_phase = [this, &e, &r, job](unsigned bits, unsigned enc_bits, unsigned first,
                                                                 const int8_t*& llrs, const uint32_t*& counts) {
           decode_deferred(e, *job->harq, bits, enc_bits, first);
           llrs            = d_io.host<int8_t>(d_lay.csi2_o);
@@ -1367,7 +1452,30 @@ void pusch_gpu_service::finish(launch_set& set)
 {
   set.L.wait(set.jobs);
   const auto t_gpu = clock_type::now();
-  set.L.replay(set.jobs, set.L.host_io(), set.L.host_msgs());
+  if (replayers.empty() || set.jobs.size() < 2) {
+    set.L.replay(set.jobs, set.L.host_io(), set.L.host_msgs());
+  } else {
+    // The jobs without a second phase shared with the helpers, then the others on this thread.
+    {
+      std::lock_guard<std::mutex> lock(rp_mtx);
+      rp_set = &set;
+      rp_next.store(0);
+      rp_busy = static_cast<unsigned>(replayers.size());
+      ++rp_gen;
+    }
+    rp_cv.notify_all();
+    replay_share(set);
+    {
+      std::unique_lock<std::mutex> lock(rp_mtx);
+      rp_done_cv.wait(lock, [this] { return rp_busy == 0; });
+      rp_set = nullptr;
+    }
+    for (const auto& job : set.jobs) {
+      if (pusch_launcher::needs_second_phase(*job)) {
+        set.L.replay_job(*job, set.L.host_io(), set.L.host_msgs());
+      }
+    }
+  }
   const auto t_end = clock_type::now();
   if (timing) {
     phase_us[3] += us_between(set.t_launched, t_gpu);

@@ -81,6 +81,10 @@ struct pusch_service_configuration {
   unsigned expected_slots_per_launch = 1;   ///< slots of one slot number to wait for before launching (the cells)
   unsigned gather_window_us          = 0;   ///< longest wait for them, from the first one's arrival
   unsigned max_grids                 = 64;  ///< batches (uplink processors) per grid shape on the device
+  /// Threads replaying a launch's slots (the completion thread included). 1 by default: on the 16-CPU box with 16
+  /// sector threads, 4 replay threads cut the 16-sector UL service from 39.4k to 33.5k one-PDU slots/s (15.1k from
+  /// 39.0k with 16 UEs; profiles/r5_replay_threads_ab.txt): the helpers take the sectors' CPUs.
+  unsigned replay_threads = 1;
 };
 class pusch_gpu_service;
 std::shared_ptr<pusch_gpu_service> create_pusch_gpu_service(const pusch_service_configuration& config);

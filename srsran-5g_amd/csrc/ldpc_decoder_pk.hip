@@ -86,6 +86,13 @@ __device__ __forceinline__ u16x2 uu(int x)
 #define LDPC_PK_PHASED 0
 #endif
 
+/// 1: a row's two-minimum search runs as two independent chains (even and odd edges) merged at the end
+/// (k1 = min(k1a, k1b), k2 = min(max(k1a, k1b), k2a, k2b): the exact result of the sequential scan, since the keys
+/// |v| * 32 + e are distinct) - half the serial min/max dependency chain of a 19-edge row (A/B switch).
+#ifndef LDPC_PK_SPLIT_SEARCH
+#define LDPC_PK_SPLIT_SEARCH 0
+#endif
+
 /// 1 where IDX != e, 0 where IDX == e (both halves): IDX ^ e (one 32-bit v_xor on both 5-bit halves), then one
 /// v_pk_min_u16 against an opaque 0x00010001 (a visible constant 1 gets the min rewritten into per-half compares and
 /// cndmasks).
@@ -213,6 +220,9 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   const u16x2 IDX = as_u16(sgw) >> uu(11);
   s16x2       v2c[deg];
   u16x2       k1 = uu(KEY_INIT), k2 = uu(KEY_INIT);
+#if LDPC_PK_SPLIT_SEARCH
+  u16x2 k1b = uu(KEY_INIT), k2b = uu(KEY_INIT);  // the odd edges' chain
+#endif
   uint32_t    sx = 0;
   uint32_t    one_bits = 0x00010001u;
   asm("" : "+v"(one_bits));
@@ -245,8 +255,16 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     v2c[e]          = v;
 #if !LDPC_PK_PHASED
     const u16x2 key = key_pk(v, e, kc);
-    k2              = __builtin_elementwise_min(__builtin_elementwise_max(key, k1), k2);
-    k1              = __builtin_elementwise_min(key, k1);
+#if LDPC_PK_SPLIT_SEARCH
+    if constexpr (e % 2 == 1) {
+      k2b = __builtin_elementwise_min(__builtin_elementwise_max(key, k1b), k2b);
+      k1b = __builtin_elementwise_min(key, k1b);
+    } else
+#endif
+    {
+      k2 = __builtin_elementwise_min(__builtin_elementwise_max(key, k1), k2);
+      k1 = __builtin_elementwise_min(key, k1);
+    }
     sx ^= bits(v);
 #endif
 #ifdef LDPC_PK_EXPERIMENT_EXTRA_VALU  // timing experiments only: N extra independent VALU per edge
@@ -274,6 +292,10 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     k1                = __builtin_elementwise_min(key, k1);
     sx ^= bits(v);
   });
+#endif
+#if LDPC_PK_SPLIT_SEARCH && !LDPC_PK_PHASED
+  k2 = __builtin_elementwise_min(__builtin_elementwise_max(k1, k1b), __builtin_elementwise_min(k2, k2b));
+  k1 = __builtin_elementwise_min(k1, k1b);
 #endif
   const u16x2 IDXN = k1 & uu(31);
   const u16x2 S1N  = scale_pk<MODE>(k1 >> uu(5), sc);

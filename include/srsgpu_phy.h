@@ -858,6 +858,19 @@ int srsgpu_harq_copy_arenas(srsgpu_context*             ctx,
                             uint32_t                    nof_jobs,
                             void*                       stream);
 
+/** A list of copies as one launch: span i copies bytes bytes (a multiple of 16, 16-byte aligned addresses) from src to
+ *  dst; src / dst device-accessible (HBM, or mapped host memory the kernel reads or writes in place). d_spans itself is
+ *  device-accessible; max_bytes = the largest span. Replaces the per-slot rx-grid upload of a slot batch (one
+ *  hipMemcpyAsync per slot: the DMA engines manage ~29 GB/s for 0.5–1 MB copies where a kernel reading mapped memory
+ *  reaches 37–50 GB/s, profiles/r5_pcie_probe.txt). Asynchronous on `stream`. */
+typedef struct {
+  const void* src;
+  void*       dst;
+  uint64_t    bytes;
+} srsgpu_copy_span;
+
+int srsgpu_copy_spans(const srsgpu_copy_span* d_spans, uint32_t nof_spans, uint64_t max_bytes, void* stream);
+
 /** Stage timing: with enable = 1 every execute records HIP events on its stream around the three kernel stages
  *  (0: rate dematching, 1: LDPC decoding, 2: TB assembly + CRC); with enable = 2 only around the decoding stage (two
  *  events: the least perturbation of a timed run); 0 disables. stage_times synchronises on them and returns the

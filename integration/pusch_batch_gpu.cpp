@@ -431,7 +431,10 @@ struct pusch_job {
   unsigned                 grid_slot = 0;  ///< The batch's grid index in the service's grid class.
   unsigned                 P         = 0;
   unsigned                 grid_prb  = 0;
-  hipEvent_t               uploaded  = nullptr;
+  hipEvent_t               uploaded  = nullptr;  ///< DMA upload of the grid (multi-device shards), else nullptr
+  const void*              grid_src  = nullptr;  ///< The grid in mapped host memory, copied in by the launch
+  uint32_t*                grid_dst  = nullptr;  ///< ... into the batch's HBM grid slot
+  size_t                   grid_bytes = 0;
   const pusch_harq_arena*  harq      = nullptr;  ///< The HARQ arena the layout addresses.
   clock_type::time_point   arrival;
 };
@@ -583,6 +586,7 @@ private:
   plan_cache<launch_plan> launches;
   staged_buffer           io;    ///< Inputs and results (layout in launch_plan).
   staged_buffer           msgs;  ///< CB messages: HARQ context in, kept messages out.
+  mapped_buffer           spans{"pusch_launcher grid spans"};  ///< the launch's rx-grid copies (srsgpu_copy_spans)
   uint32_t*               d_ce       = nullptr;
   size_t                  d_ce_cap   = 0;
   int8_t*                 d_harq     = nullptr;
@@ -662,7 +666,8 @@ private:
   std::unique_ptr<pusch_processor>     fallback;
   owned_stream                         upload_stream;
   hipEvent_t                           uploaded = nullptr;
-  staged_buffer                        grid_buf;  ///< Pinned copy of the rx grid (host side only).
+  staged_buffer                        grid_buf;  ///< Pinned copy of the rx grid for the shards' DMA uploads.
+  mapped_buffer                        grid_map{"pusch_slot_batch grid"};  ///< The rx grid, read in place by the launch
   unsigned                             batch_id   = 0;
   int                                  grid_slot  = -1;
   unsigned                             grid_P     = 0;
@@ -1230,9 +1235,26 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
   }
   tm.filled = clock_type::now();
 
-  // The grids' uploads (each batch's own stream) before the graph; the kept messages only when a CB has passed before.
-  for (const auto& job : jobs) {
-    hip_check(hipStreamWaitEvent(s, job->uploaded, 0), WHO, "wait for the grid upload");
+  // The grids: one launch copies every job's grid from mapped host memory into its HBM grid slot (zero-copy reads;
+  // a DMA copy per slot ran the service at the DMA engines' ~29 GB/s); shards uploaded by DMA are waited for. The kept
+  // messages only when a CB has passed before.
+  {
+    std::vector<srsgpu_copy_span> sp;
+    uint64_t                      max_bytes = 0;
+    for (const auto& job : jobs) {
+      if (job->grid_src != nullptr) {
+        sp.push_back({job->grid_src, job->grid_dst, job->grid_bytes});
+        max_bytes = std::max<uint64_t>(max_bytes, job->grid_bytes);
+      } else if (job->uploaded != nullptr) {
+        hip_check(hipStreamWaitEvent(s, job->uploaded, 0), WHO, "wait for the grid upload");
+      }
+    }
+    if (!sp.empty()) {
+      spans.reserve(sp.size() * sizeof(srsgpu_copy_span));
+      std::memcpy(spans.host(), sp.data(), sp.size() * sizeof(srsgpu_copy_span));
+      srsgpu_check(srsgpu_copy_spans(spans.dev<srsgpu_copy_span>(), static_cast<uint32_t>(sp.size()), max_bytes, s),
+                   WHO);
+    }
   }
   if (any_msgs) {
     hip_check(hipMemcpyAsync(msgs.dev(), msgs.host(), static_cast<size_t>(lp->cb_total) * SRSGPU_CB_MSG_STRIDE,
@@ -1926,18 +1948,14 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     grid_prb     = nsc / NRE;
   }
   const size_t row = static_cast<size_t>(nsc) * sizeof(uint32_t);
-  grid_buf.reserve(static_cast<size_t>(P) * 14 * row);
-  // The rx grid (every symbol of ports 0..P-1, [port][symbol][subcarrier]) into pinned memory, then to the batch's HBM
-  // grid slot on its own stream (the launch waits for the event).
+  grid_map.reserve(static_cast<size_t>(P) * 14 * row);
+  // The rx grid (every symbol of ports 0..P-1, [port][symbol][subcarrier]) into mapped host memory; the launch copies
+  // it into the batch's HBM grid slot (srsgpu_copy_spans, with the other slots' grids).
   for (unsigned p = 0; p != P; ++p) {
     for (unsigned l = 0; l != 14; ++l) {
-      std::memcpy(grid_buf.host((p * 14 + l) * row), grid.get_view(p, l).data(), row);
+      std::memcpy(grid_map.host((p * 14 + l) * row), grid.get_view(p, l).data(), row);
     }
   }
-  hip_check(hipMemcpyAsync(d_grid, grid_buf.host(), static_cast<size_t>(P) * 14 * row, hipMemcpyHostToDevice,
-                           upload_stream.get()),
-            WHO, "grid upload");
-  hip_check(hipEventRecord(uploaded, upload_stream.get()), WHO, "event");
 
   job->batch     = this;
   job->batch_id  = batch_id;
@@ -1946,7 +1964,10 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
   job->grid_slot = static_cast<unsigned>(grid_slot);
   job->P         = P;
   job->grid_prb  = grid_prb;
-  job->uploaded  = uploaded;
+  job->uploaded  = nullptr;
+  job->grid_src   = grid_map.dev();
+  job->grid_dst   = d_grid;
+  job->grid_bytes = static_cast<size_t>(P) * 14 * row;
   build_layout(*job, *arena);
   {
     std::lock_guard<std::mutex> done_lock(done_mtx);

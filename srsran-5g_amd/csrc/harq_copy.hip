@@ -4,8 +4,11 @@
 // get_codeblock_soft_bits), across slots; a batched PUSCH decoder plan addresses them contiguously per transport
 // block. One workgroup per codeblock, 16-byte vector copies (every offset and length is a multiple of 16 for the LDPC
 // lengths N = 64 Z / 48 Z at even Z; a byte loop otherwise). HBM-bound: 2 bytes moved per soft bit.
+// Also srsgpu_copy_spans: a list of copies as one launch (the slot batches' rx grids, read in place from mapped host
+// memory into their HBM grid slots).
 #include "srsgpu_internal.h"
 #include "capi_internal.h"
+#include <algorithm>
 
 namespace {
 
@@ -38,7 +41,36 @@ __global__ void __launch_bounds__(256) harq_copy_kernel(int8_t* __restrict__ are
   }
 }
 
+/// Span copies: blockIdx.y = span, the x blocks stride over it in 16-byte words (the entry point checks alignment).
+__global__ void __launch_bounds__(256) copy_spans_kernel(const srsgpu_copy_span* __restrict__ spans)
+{
+  const srsgpu_copy_span sp = spans[blockIdx.y];
+  const uint4*           s4 = reinterpret_cast<const uint4*>(sp.src);
+  uint4*                 d4 = reinterpret_cast<uint4*>(sp.dst);
+  const uint64_t         n  = sp.bytes / 16u;
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    d4[i] = s4[i];
+  }
+}
+
 } // namespace
+
+extern "C" int srsgpu_copy_spans(const srsgpu_copy_span* d_spans, uint32_t nof_spans, uint64_t max_bytes, void* stream)
+{
+  if ((d_spans == nullptr && nof_spans > 0) || (max_bytes & 15u) != 0) {
+    return srsgpu::fail(SRSGPU_ERR_INVALID_ARG, "srsgpu_copy_spans: invalid argument (max_bytes a multiple of 16)");
+  }
+  if (nof_spans == 0 || max_bytes == 0) {
+    return SRSGPU_OK;
+  }
+  // Enough workgroups per span that a host-memory source keeps many reads in flight (about 4 KB per workgroup pass).
+  const uint64_t blocks = std::min<uint64_t>(256, (max_bytes / 16u + 255u) / 256u);
+  copy_spans_kernel<<<dim3(static_cast<unsigned>(blocks), nof_spans), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      d_spans);
+  const hipError_t err = hipGetLastError();
+  return err == hipSuccess ? SRSGPU_OK : srsgpu::fail(SRSGPU_ERR_HIP, "srsgpu_copy_spans: %s", hipGetErrorString(err));
+}
 
 extern "C" int srsgpu_harq_copy(srsgpu_context*             ctx,
                                 int                         direction,

@@ -396,6 +396,7 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_ofdm_plan_concat.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(P)]
     lib.srsgpu_ofdm_plan_get_jobs.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
     lib.srsgpu_ofdm_jobs_execute.argtypes = [P, P, ctypes.c_uint32, P, P, P]
+    lib.srsgpu_copy_spans.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64, P]
     lib.srsgpu_ofdm_plan_sample_offset.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     lib.srsgpu_ofdm_plan_sample_offset.restype = ctypes.c_uint64
     lib.srsgpu_ofdm_modulator_plan_execute.argtypes = [P, P, P, P]
@@ -426,7 +427,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_modulator_symbols_plan_create", "srsgpu_ofdm_demodulator_symbols_plan_create", "srsgpu_harq_copy",
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
     "srsgpu_ofdm_plan_concat", "srsgpu_ofdm_plan_nof_grid_words", "srsgpu_ofdm_plan_get_jobs",
-    "srsgpu_ofdm_jobs_execute",
+    "srsgpu_ofdm_jobs_execute", "srsgpu_copy_spans",
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
     "srsgpu_pusch_demodulator_plan_create_ex", "srsgpu_pusch_demodulator_plan_execute_ex",
@@ -456,6 +457,20 @@ def _stream_handle(stream) -> Optional[int]:
     if hasattr(stream, "cuda_stream"):
         return stream.cuda_stream
     return int(stream)
+
+
+def copy_spans(spans, stream=None):
+    """srsgpu_copy_spans: spans = [(src tensor, dst tensor)], each a contiguous device tensor of the same byte size (a
+    multiple of 16). One launch copies them all."""
+    arr = np.zeros(len(spans), np.dtype([("src", "<u8"), ("dst", "<u8"), ("bytes", "<u8")]))
+    for i, (a, b) in enumerate(spans):
+        n = a.numel() * a.element_size()
+        if n != b.numel() * b.element_size():
+            raise SrsGpuError("copy_spans: source and destination sizes differ")
+        arr[i] = (_dptr(a), _dptr(b), n)
+    d = torch.from_numpy(arr.view(np.uint8).copy()).to(spans[0][0].device)
+    _check(_lib.srsgpu_copy_spans(_dptr(d), len(spans), int(arr["bytes"].max()), _stream_handle(stream)))
+    return d  # keep alive until the stream has run the copies
 
 
 def _dptr(t) -> int:

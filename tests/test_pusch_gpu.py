@@ -385,3 +385,30 @@ def test_pusch_decoder_sliced_tb_stage(orc, ctx):
     flags = crc.cpu().numpy()
     n0, n1 = segs[0].nof_segments, segs[1].nof_segments
     assert flags[:n0].all() and not flags[n0:n0 + n1].any()
+
+
+def test_copy_spans():
+    """srsgpu_copy_spans (the slot batches' rx-grid gather): several spans of different sizes in one launch, each
+    destination equal to its source, the bytes around them untouched; unaligned sizes refused."""
+    import torch
+    import srsgpu
+    srsgpu.Context(0)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(5)
+    srcs = [torch.randint(0, 255, (n,), dtype=torch.uint8, generator=g).to(dev) for n in (16, 4096, 733824, 48)]
+    big = torch.full((sum(x.numel() for x in srcs) + 64 * len(srcs),), 7, dtype=torch.uint8, device=dev)
+    dsts, off = [], 0
+    for x in srcs:
+        dsts.append(big[off:off + x.numel()])
+        off += x.numel() + 64
+    keep = srsgpu.copy_spans(list(zip(srcs, dsts)))
+    torch.cuda.synchronize()
+    del keep
+    off = 0
+    for x, d in zip(srcs, dsts):
+        assert torch.equal(x, d)
+        gap = big[off + x.numel():off + x.numel() + 64]
+        assert int(gap.min()) == 7 == int(gap.max())
+        off += x.numel() + 64
+    with pytest.raises(srsgpu.SrsGpuError):
+        srsgpu.copy_spans([(srcs[0][:8], dsts[0][:8])])

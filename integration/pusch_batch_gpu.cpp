@@ -1947,14 +1947,28 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
     grid_P       = P;
     grid_prb     = nsc / NRE;
   }
-  const size_t row = static_cast<size_t>(nsc) * sizeof(uint32_t);
-  grid_map.reserve(static_cast<size_t>(P) * 14 * row);
+  const size_t row    = static_cast<size_t>(nsc) * sizeof(uint32_t);
+  const size_t gbytes = static_cast<size_t>(P) * 14 * row;
+  // SRSGPU_GRID_DMA=1 (diagnostics, A/B): the round-5 first version's DMA upload per slot instead of the span copy.
+  static const bool grid_dma = std::getenv("SRSGPU_GRID_DMA") != nullptr;
+  staged_buffer*    dma_buf  = grid_dma ? &grid_buf : nullptr;
+  if (grid_dma) {
+    grid_buf.reserve(gbytes);
+  } else {
+    grid_map.reserve(gbytes);
+  }
   // The rx grid (every symbol of ports 0..P-1, [port][symbol][subcarrier]) into mapped host memory; the launch copies
   // it into the batch's HBM grid slot (srsgpu_copy_spans, with the other slots' grids).
   for (unsigned p = 0; p != P; ++p) {
     for (unsigned l = 0; l != 14; ++l) {
-      std::memcpy(grid_map.host((p * 14 + l) * row), grid.get_view(p, l).data(), row);
+      uint8_t* dst = dma_buf != nullptr ? dma_buf->host((p * 14 + l) * row) : grid_map.host((p * 14 + l) * row);
+      std::memcpy(dst, grid.get_view(p, l).data(), row);
     }
+  }
+  if (dma_buf != nullptr) {
+    hip_check(hipMemcpyAsync(d_grid, dma_buf->host(), gbytes, hipMemcpyHostToDevice, upload_stream.get()), WHO,
+              "grid upload");
+    hip_check(hipEventRecord(uploaded, upload_stream.get()), WHO, "event");
   }
 
   job->batch     = this;
@@ -1964,10 +1978,10 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
   job->grid_slot = static_cast<unsigned>(grid_slot);
   job->P         = P;
   job->grid_prb  = grid_prb;
-  job->uploaded  = nullptr;
-  job->grid_src   = grid_map.dev();
+  job->uploaded   = dma_buf != nullptr ? uploaded : nullptr;
+  job->grid_src   = dma_buf != nullptr ? nullptr : grid_map.dev();
   job->grid_dst   = d_grid;
-  job->grid_bytes = static_cast<size_t>(P) * 14 * row;
+  job->grid_bytes = gbytes;
   build_layout(*job, *arena);
   {
     std::lock_guard<std::mutex> done_lock(done_mtx);

@@ -525,7 +525,7 @@ public:
   size_t         results_bytes() const { return plan->end_o - plan->flag_o; }
   const uint8_t* device_msgs() { return msgs.dev<uint8_t>(); }
   size_t         msgs_bytes() const { return static_cast<size_t>(plan->cb_total) * SRSGPU_CB_MSG_STRIDE; }
-  const uint8_t* host_io() { return io.host<uint8_t>(); }
+  const uint8_t* host_io() { return ioh<uint8_t>(0); }
   const uint8_t* host_msgs() { return msgs.host<uint8_t>(); }
   hipStream_t    get_stream() const { return stream.get(); }
   hipEvent_t     done_event() const { return done; }
@@ -584,7 +584,21 @@ private:
   owned_stream            stream;
   hipEvent_t              done = nullptr;
   plan_cache<launch_plan> launches;
-  staged_buffer           io;    ///< Inputs and results (layout in launch_plan).
+  staged_buffer           io;    ///< Inputs and results (layout in launch_plan), when they stay in HBM (shards).
+  mapped_buffer           io_map{"pusch_launcher io"};  ///< The same image in mapped host memory, read and written in
+                                                         ///< place by the launch (results to the host: no copy nodes)
+  bool                    zc = false;  ///< the current launch uses io_map
+
+  template <typename T = uint8_t>
+  T* ioh(size_t off)
+  {
+    return zc ? io_map.host<T>(off) : io.host<T>(off);
+  }
+  template <typename T = uint8_t>
+  T* iod(size_t off)
+  {
+    return zc ? io_map.dev<T>(off) : io.dev<T>(off);
+  }
   staged_buffer           msgs;  ///< CB messages: HARQ context in, kept messages out.
   mapped_buffer           spans{"pusch_launcher grid spans"};  ///< the launch's rx-grid copies (srsgpu_copy_spans)
   uint32_t*               d_ce       = nullptr;
@@ -1120,16 +1134,24 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
   launch_plan* lp = launches.get(key, [&] { return create_plan(jobs, P, grid_prb); });
   plan            = lp;
   downloaded      = download;
+  // Results to the host: the launch reads and writes its staging image in place. SRSGPU_IO_COPY=1 (diagnostics, A/B):
+  // the staging image in HBM with an upload and a download node in the graph.
+  static const bool io_copy = std::getenv("SRSGPU_IO_COPY") != nullptr;
+  zc                        = download && !io_copy;
 
   // Buffers (grow-only; a move invalidates the captured graphs).
   {
-    const void* before[5] = {io.host(), msgs.host(), d_ce, d_harq, d_llr};
-    io.reserve(lp->end_o);
+    const void* before[6] = {io.host(), io_map.host(), msgs.host(), d_ce, d_harq, d_llr};
+    if (zc) {
+      io_map.reserve(lp->end_o);
+    } else {
+      io.reserve(lp->end_o);
+    }
     msgs.reserve(std::max<size_t>(static_cast<size_t>(lp->cb_total) * SRSGPU_CB_MSG_STRIDE, 64));
     reserve_device(d_ce, d_ce_cap, static_cast<size_t>(lp->max_grid) * 4 * P * 14 * row, "channel estimates");
     reserve_device(d_harq, d_harq_cap, std::max<size_t>(lp->harq_total, 16), "HARQ launch buffer");
     reserve_device(d_llr, d_llr_cap, std::max<size_t>(lp->llr_total, 64), "LLRs");
-    const void* after[5] = {io.host(), msgs.host(), d_ce, d_harq, d_llr};
+    const void* after[6] = {io.host(), io_map.host(), msgs.host(), d_ce, d_harq, d_llr};
     if (!std::equal(std::begin(before), std::end(before), std::begin(after))) {
       ++buffer_generation;
     }
@@ -1142,9 +1164,11 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
       lp->graph = nullptr;
     }
     lp->graph = capture_graph(s, WHO, [&] {
-      io.upload(0, lp->iter_o, s);
-      srsgpu_check(srsgpu_pusch_chest_plan_execute(lp->chest, d_grids, d_ce, io.dev<float>(lp->nv_o),
-                                                   io.dev<float>(lp->m_o), s),
+      if (!zc) {
+        io.upload(0, lp->iter_o, s);
+      }
+      srsgpu_check(srsgpu_pusch_chest_plan_execute(lp->chest, d_grids, d_ce, iod<float>(lp->nv_o),
+                                                   iod<float>(lp->m_o), s),
                    WHO);
       // pusch_processor_impl.cpp:222-240: the DC subcarrier's estimate is zeroed for CP-OFDM transmissions over it.
       for (const auto& z : lp->dc_zero) {
@@ -1152,28 +1176,28 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
                                    s),
                   WHO, "DC");
       }
-      srsgpu_check(srsgpu_pusch_demodulator_plan_execute_ex(lp->demod, d_grids, d_ce, io.dev<float>(lp->nv_o),
-                                                            d_llr, io.dev<float>(lp->st_o), s),
+      srsgpu_check(srsgpu_pusch_demodulator_plan_execute_ex(lp->demod, d_grids, d_ce, iod<float>(lp->nv_o),
+                                                            d_llr, iod<float>(lp->st_o), s),
                    WHO);
       if (lp->demux != nullptr) {
-        int8_t* uci = io.dev<int8_t>(lp->uci_o);
+        int8_t* uci = iod<int8_t>(lp->uci_o);
         srsgpu_check(srsgpu_ulsch_demux_plan_execute(lp->demux, d_llr, d_llr, uci, uci, nullptr, s), WHO);
       }
-      srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_BATCH, io.dev<int8_t*>(lp->arena_o),
-                                           HARQ_SLOT_BYTES, d_harq, io.dev<srsgpu_harq_copy_job>(0),
+      srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_BATCH, iod<int8_t*>(lp->arena_o),
+                                           HARQ_SLOT_BYTES, d_harq, iod<srsgpu_harq_copy_job>(0),
                                            lp->nof_copies, s),
                    WHO);
       if (lp->dec != nullptr) {
-        srsgpu_check(srsgpu_pusch_decoder_plan_execute(lp->dec, d_llr, d_harq, io.dev<uint8_t>(lp->flag_o),
-                                                       msgs.dev<uint8_t>(), io.dev<int32_t>(lp->iter_o),
-                                                       io.dev<uint8_t>(lp->tb_o), io.dev<uint8_t>(lp->tbok_o), s),
+        srsgpu_check(srsgpu_pusch_decoder_plan_execute(lp->dec, d_llr, d_harq, iod<uint8_t>(lp->flag_o),
+                                                       msgs.dev<uint8_t>(), iod<int32_t>(lp->iter_o),
+                                                       iod<uint8_t>(lp->tb_o), iod<uint8_t>(lp->tbok_o), s),
                      WHO);
       }
-      srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_ARENA, io.dev<int8_t*>(lp->arena_o),
-                                           HARQ_SLOT_BYTES, d_harq, io.dev<srsgpu_harq_copy_job>(0),
+      srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_ARENA, iod<int8_t*>(lp->arena_o),
+                                           HARQ_SLOT_BYTES, d_harq, iod<srsgpu_harq_copy_job>(0),
                                            lp->nof_copies, s),
                    WHO);
-      if (download) {
+      if (download && !zc) {
         io.download(lp->flag_o, lp->end_o - lp->flag_o, s);
       }
     });
@@ -1185,9 +1209,9 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
   // Absolute offsets of the entries, the copy jobs and the HARQ context (flags; messages of CBs that passed before).
   decoded_flags.assign(lp->cb_total, 0);
   unsigned tx_b = 0, llr_b = 0, cb_b = 0, tb_b = 0, uci_b = 0, harq_b = 0, dmx_b = 0, tbi_b = 0;
-  auto*    copies   = io.host<srsgpu_harq_copy_job>(0);
+  auto*    copies   = ioh<srsgpu_harq_copy_job>(0);
   bool     any_msgs = false;
-  std::memcpy(io.host(lp->arena_o), lp->arenas.data(), lp->arenas.size() * sizeof(int8_t*));
+  std::memcpy(ioh(lp->arena_o), lp->arenas.data(), lp->arenas.size() * sizeof(int8_t*));
   for (size_t j = 0; j != jobs.size(); ++j) {
     const auto&       job = jobs[j];
     const job_layout& L   = job->lay;
@@ -1197,7 +1221,7 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
       copies->arena = lp->job_arena[j];
       ++copies;
     }
-    std::memcpy(io.host<uint8_t>(lp->flag_o + cb_b), L.flags.data(), L.cb_total);
+    std::memcpy(ioh<uint8_t>(lp->flag_o + cb_b), L.flags.data(), L.cb_total);
     for (unsigned c = 0; c != L.cb_total; ++c) {
       decoded_flags[cb_b + c] = L.flags[c] != 0 ? 0 : 1;
     }
@@ -1367,9 +1391,9 @@ void pusch_launcher::wait(const std::vector<std::unique_ptr<pusch_job>>& jobs)
   bool               need_msgs = false;
   for (const auto& job : jobs) {
     for (const pusch_entry& e : job->entries) {
-      if (e.tb_index >= 0 && *io.host<uint8_t>(lp.tbok_o + static_cast<unsigned>(e.tb_index)) == 0) {
+      if (e.tb_index >= 0 && *ioh<uint8_t>(lp.tbok_o + static_cast<unsigned>(e.tb_index)) == 0) {
         for (unsigned c = 0; c != e.nof_cbs && !need_msgs; ++c) {
-          need_msgs = *io.host<uint8_t>(lp.flag_o + e.cb0 + c) != 0;
+          need_msgs = *ioh<uint8_t>(lp.flag_o + e.cb0 + c) != 0;
         }
       }
     }

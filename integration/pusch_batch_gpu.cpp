@@ -1134,10 +1134,12 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
   launch_plan* lp = launches.get(key, [&] { return create_plan(jobs, P, grid_prb); });
   plan            = lp;
   downloaded      = download;
-  // Results to the host: the launch reads and writes its staging image in place. SRSGPU_IO_COPY=1 (diagnostics, A/B):
-  // the staging image in HBM with an upload and a download node in the graph.
-  static const bool io_copy = std::getenv("SRSGPU_IO_COPY") != nullptr;
-  zc                        = download && !io_copy;
+  // The staging image in HBM with an upload and a download node in the graph. SRSGPU_IO_MAPPED=1 (diagnostics, A/B):
+  // the image in mapped host memory, read and written in place by the kernels (no copy nodes) - measured slower:
+  // one thread 6.3k either way, 16-sector service 23.3-23.7k vs 42.7-45.0k one-PDU slots/s: the decoder's and the
+  // statistics kernels' small scattered result stores cross PCIe one by one (profiles/r5_io_mapped_ab.txt).
+  static const bool io_mapped = std::getenv("SRSGPU_IO_MAPPED") != nullptr;
+  zc                          = download && io_mapped;
 
   // Buffers (grow-only; a move invalidates the captured graphs).
   {

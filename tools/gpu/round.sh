@@ -14,6 +14,7 @@
 #   kstats           rocprofv3 --kernel-trace --stats of the default bench
 #   lower            tools/lower_phy_bench.py with the multi-sector sweep
 #   lower_trace      rocprofv3 kernel trace of the sector group at 8 sectors
+#   lds              PMC pass of the bench: LDS issue stalls, bank conflicts, LDS-array cycles per kernel
 #   ab:DIR[:N]       A/B of the default bench: the in-tree library against srsran-5g_amd/DIR's, N rounds
 set -o pipefail
 TAG=${1:?tag}
@@ -71,6 +72,16 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/lower_trace" -o lower -- python3 -u \
         tools/lower_phy_bench.py --slots 100 --sectors 8 --sweep-only group4 > "$OUT/lower_trace.json" \
         2> "$OUT/lower_trace.log" || { tail -20 "$OUT/lower_trace.log"; exit 1; } ;;
+    lds)
+      # LDS counters of the bench's kernels (one PMC pass): issue stalls on LDS, bank-conflict cycles, LDS-array cycles
+      timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_LDS \
+        SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES -d "$OUT/pmc_lds" -o run --output-format csv -- python3 -u \
+        bench.py --no-cpu-baseline --no-extra-points --no-extra-workloads --steps 40 --warmup 4 --min-time 0 \
+        > "$OUT/pmc_lds.json" 2> "$OUT/pmc_lds.err" || { tail -20 "$OUT/pmc_lds.err"; exit 1; }
+      CSV=$(find "$OUT/pmc_lds" -name "*counter_collection.csv" | head -1)
+      python3 tools/pmc_summary.py "$CSV" > "$OUT/pmc_lds.txt"
+      rm -rf "$OUT/pmc_lds"
+      cat "$OUT/pmc_lds.txt" | cut -c1-400 ;;
     ab:*)
       # ab:DIR[:N] — the default bench N times (default 2), alternating the in-tree library and srsran-5g_amd/DIR's
       SPEC=${step#ab:}; DIR=${SPEC%%:*}; N=2; [[ "$SPEC" == *:* ]] && N=${SPEC##*:}

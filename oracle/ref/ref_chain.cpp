@@ -66,6 +66,12 @@
 #include "lib/phy/upper/signal_processors/ptrs/ptrs_pdsch_generator_impl.h"
 #include "lib/phy/upper/downlink_processor_single_executor_impl.h"
 #include "lib/phy/upper/uplink_processor_impl.h"
+#include "srsran/gateways/baseband/buffer/baseband_gateway_buffer_reader.h"
+#include "srsran/phy/lower/lower_phy_rx_symbol_context.h"
+#include "srsran/phy/lower/processors/uplink/puxch/puxch_processor.h"
+#include "srsran/phy/lower/processors/uplink/puxch/puxch_processor_baseband.h"
+#include "srsran/phy/lower/processors/uplink/puxch/puxch_processor_notifier.h"
+#include "srsran/phy/lower/processors/uplink/puxch/puxch_processor_request_handler.h"
 #include "srsran/phy/upper/rx_buffer_pool.h"
 #include "srsran/phy/upper/upper_phy_rg_gateway.h"
 #include "srsran/phy/upper/upper_phy_rx_results_notifier.h"
@@ -86,6 +92,7 @@
 #include <map>
 #include <mutex>
 #include <random>
+#include <sys/prctl.h>
 #include <thread>
 #include <memory>
 #include <vector>
@@ -1750,6 +1757,221 @@ int chain_dl_bench(int                 device,
       workers[t]->post([&, t] { delete hs[t]; });
       workers[t]->wait();
     }
+    return 0;
+  });
+}
+
+
+/// du_low's UL on one GPU, paced at the radio's symbol rate (TEST INFRASTRUCTURE, tools/du_low_bench.py): every sector
+/// a thread that, per slot, takes the grid of one of its ring of 4 uplink processors (the GPU slot batches on one shared
+/// PUSCH service, as chain_ul_bench variant 2) with that slot's PUSCH PDUs, hands it to the sector's lower-PHY PUxCH
+/// processor (handle_request) and delivers the slot's 14 symbols of samples (process_symbol) one symbol duration apart;
+/// the PUxCH notifier's last symbol of the slot starts the uplink processor (handle_rx_symbol(13)), as the radio unit's
+/// rx-symbol handler does in du_low. grouped: the sectors' PUxCH processors come from one lower_phy_sector_group (else
+/// one GPU PUxCH processor each). samples: complex float, the two slots of a subframe, per symbol all ports (P x
+/// (CP + N)) consecutively. Outputs per sector k: lag[4k..4k+3] = largest lag behind the pace (s), lag at the last
+/// symbol (s), fraction of symbols more than a slot late, late PUxCH requests; results[2k], [2k+1] = PUSCH data results
+/// and TB CRC passes. seconds: wall time. Returns 0 (< 0 on error).
+int chain_du_low_ul(int                 device,
+                    unsigned            nof_sectors,
+                    unsigned            slots,
+                    int                 nof_pdus,
+                    const chain_params* pdus,
+                    const int*          tb_bytes,
+                    const float*        samples,
+                    unsigned            nof_ports,
+                    unsigned            grid_prb,
+                    unsigned            dft_size,
+                    int                 grouped,
+                    unsigned            in_flight,
+                    double*             lag,
+                    int*                results,
+                    double*             seconds)
+{
+  return guarded("chain_du_low_ul", [&] {
+    using clock         = std::chrono::steady_clock;
+    constexpr unsigned UL_RING = 4;
+    const unsigned     nsc     = 12 * grid_prb;
+    const double       srate   = static_cast<double>(dft_size) * 30e3;
+    // Symbol sizes (CP + N) of the subframe's 28 symbols and where each symbol's samples start.
+    std::vector<unsigned> size(28), start(28);
+    size_t                pos = 0;
+    for (unsigned s = 0; s != 28; ++s) {
+      size[s]  = cyclic_prefix(cyclic_prefix::NORMAL).get_length(s, subcarrier_spacing::kHz30).to_samples(srate) +
+                 dft_size;
+      start[s] = static_cast<unsigned>(pos);
+      pos += static_cast<size_t>(size[s]) * nof_ports;
+    }
+    gpu::pusch_service_configuration sc;
+    sc.device                    = device;
+    sc.nof_launch_sets           = 3;
+    sc.max_slots_per_launch      = nof_sectors;
+    sc.expected_slots_per_launch = nof_sectors;
+    sc.gather_window_us          = 300;
+    sc.max_grids                 = nof_sectors * UL_RING;
+    auto service                 = gpu::create_pusch_gpu_service(sc);
+    std::shared_ptr<lower_phy_sector_group> group;
+    if (grouped != 0) {
+      lower_phy_group_configuration gc;
+      gc.device      = device;
+      gc.nof_sectors = nof_sectors;
+      group          = create_lower_phy_sector_group(gc);
+    }
+
+    struct du_ul_notifier : public puxch_processor_notifier {
+      std::vector<ul_harness*>* ring = nullptr;
+      std::atomic<unsigned>     late{0};
+      void on_puxch_request_late(const resource_grid_context& /*c*/) override { ++late; }
+      void on_rx_symbol(const shared_resource_grid& /*grid*/, const lower_phy_rx_symbol_context& c) override
+      {
+        if (c.nof_symbols == 13) {
+          (*ring)[c.slot.system_slot() % ring->size()]->proc->get_slot_processor(c.slot).handle_rx_symbol(13);
+        }
+      }
+    };
+    struct reader : public baseband_gateway_buffer_reader {
+      std::vector<span<const cf_t>> ch;
+      unsigned                      get_nof_channels() const override { return ch.size(); }
+      unsigned                      get_nof_samples() const override { return ch.empty() ? 0 : ch[0].size(); }
+      span<const cf_t>              get_channel_buffer(unsigned i) const override { return ch[i]; }
+    };
+    struct sector_state {
+      std::unique_ptr<ul_sector>       sec;
+      std::vector<ul_harness*>         ring;
+      du_ul_notifier                   notifier;
+      std::unique_ptr<puxch_processor> puxch;
+    };
+    std::vector<std::unique_ptr<bench_worker>> workers;
+    std::vector<std::unique_ptr<sector_state>> st(nof_sectors);
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      workers.push_back(std::make_unique<bench_worker>());
+    }
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      workers[k]->post([&, k] {
+        st[k]                           = std::make_unique<sector_state>();
+        st[k]->sec                      = std::make_unique<ul_sector>();
+        st[k]->sec->pool                = ul_pool();
+        st[k]->sec->arena               = gpu::create_pusch_harq_arena(device, UL_POOL_CODEBLOCKS);
+        st[k]->sec->notifier.count_only = true;
+        for (unsigned r = 0; r != UL_RING; ++r) {
+          st[k]->ring.push_back(ul_create(device, 1, nof_ports, grid_prb, 2, st[k]->sec.get(), service, true));
+        }
+        st[k]->notifier.ring = &st[k]->ring;
+        puxch_processor_configuration c;
+        c.cp                = cyclic_prefix::NORMAL;
+        c.scs               = subcarrier_spacing::kHz30;
+        c.srate             = sampling_rate::from_Hz(srate);
+        c.bandwidth_rb      = grid_prb;
+        c.dft_window_offset = 0.5F;
+        c.center_freq_Hz    = 3.5e9 + 2e7 * k;
+        c.nof_rx_ports      = nof_ports;
+        st[k]->puxch        = (group ? create_puxch_processor_factory_gpu(group, in_flight)
+                                     : create_puxch_processor_factory_gpu(device, in_flight))
+                           ->create(c);
+        st[k]->puxch->connect(st[k]->notifier);
+      });
+      workers[k]->wait();  // one at a time: the factories' first-use initialisation is not ours to race
+    }
+    const clock::duration period = std::chrono::duration_cast<clock::duration>(std::chrono::nanoseconds(1000000 / 28));
+    std::vector<unsigned> slot_no(nof_sectors, 0), submitted(nof_sectors, 0);
+    // One sector's slots: paced (period > 0, from `t0`) or free-running; returns (largest lag, last lag, late count).
+    auto run = [&](unsigned k, unsigned n, clock::time_point t0, bool paced, double* out) {
+      if (paced) {
+        (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
+      }
+      sector_state& s       = *st[k];
+      reader        buf;
+      double        max_lag = 0, last_lag = 0;
+      long          late = 0, i_sym = 0;
+      for (unsigned i = 0; i != n; ++i) {
+        const unsigned   sl = slot_no[k]++;
+        const slot_point sp(subcarrier_spacing::kHz30, sl % 20480);
+        ul_harness*      h  = s.ring[sl % UL_RING];
+        unique_uplink_pdu_slot_repository repo = h->proc->get_pdu_slot_repository(sp);
+        while (!repo.is_valid()) {
+          std::this_thread::yield();  // the ring's processor still holds an earlier slot
+          repo = h->proc->get_pdu_slot_repository(sp);
+        }
+        for (int q = 0; q != nof_pdus; ++q) {
+          chain_params c = pdus[q];
+          c.slot         = static_cast<int>(sp.slot_index());
+          c.harq_id      = (c.harq_id + static_cast<int>(sl)) % 16;
+          repo->add_pusch_pdu({static_cast<unsigned>(c.harq_id), units::bytes(static_cast<unsigned>(tb_bytes[q])),
+                               make_pusch_pdu(c)});
+        }
+        shared_resource_grid g = repo.release();
+        s.puxch->get_request_handler().handle_request(g, {sp, k});
+        g.release();
+        submitted[k] += static_cast<unsigned>(nof_pdus);
+        const unsigned q0 = sp.subframe_slot_index() * 14;
+        for (unsigned l = 0; l != 14; ++l) {
+          if (paced) {
+            const clock::time_point due = t0 + period * i_sym++;
+            const clock::time_point now = clock::now();
+            if (now < due) {
+              std::this_thread::sleep_until(due);
+              last_lag = 0;
+            } else {
+              last_lag = std::chrono::duration<double>(now - due).count();
+              max_lag  = std::max(max_lag, last_lag);
+              late += (now - due) > period * 14 ? 1 : 0;
+            }
+          }
+          buf.ch.clear();
+          const unsigned ssz = size[q0 + l];
+          for (unsigned p = 0; p != nof_ports; ++p) {
+            buf.ch.emplace_back(reinterpret_cast<const cf_t*>(samples) + start[q0 + l] + static_cast<size_t>(p) * ssz,
+                                ssz);
+          }
+          s.puxch->get_baseband().process_symbol(buf, lower_phy_rx_symbol_context{sp, k, l});
+        }
+      }
+      s.sec->notifier.wait_for(submitted[k]);  // every result of the sector's slots notified
+      out[0] = max_lag;
+      out[1] = last_lag;
+      out[2] = static_cast<double>(late) / std::max(1L, i_sym);
+    };
+    // Warm-up over one frame, free-running (plans per slot number, pools, first touch).
+    std::vector<double> tmp(3 * nof_sectors);
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      workers[k]->post([&, k] { run(k, 20, clock::now(), false, &tmp[3 * k]); });
+    }
+    for (auto& w : workers) {
+      w->wait();
+    }
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      st[k]->sec->notifier.reset();
+      st[k]->notifier.late = 0;
+      submitted[k]         = 0;
+    }
+    const clock::time_point t0 = clock::now() + std::chrono::milliseconds(2);
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      workers[k]->post([&, k] { run(k, slots, t0, true, &tmp[3 * k]); });
+    }
+    for (auto& w : workers) {
+      w->wait();
+    }
+    *seconds = std::chrono::duration<double>(clock::now() - t0).count();
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      lag[4 * k]         = tmp[3 * k];
+      lag[4 * k + 1]     = tmp[3 * k + 1];
+      lag[4 * k + 2]     = tmp[3 * k + 2];
+      lag[4 * k + 3]     = st[k]->notifier.late.load();
+      results[2 * k]     = static_cast<int>(st[k]->sec->notifier.nof_data.load());
+      results[2 * k + 1] = static_cast<int>(st[k]->sec->notifier.crc_ok.load());
+    }
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      workers[k]->post([&, k] {
+        st[k]->puxch.reset();
+        for (ul_harness* h : st[k]->ring) {
+          delete h;
+        }
+        st[k].reset();
+      });
+      workers[k]->wait();
+    }
+    group.reset();
+    service.reset();
     return 0;
   });
 }

@@ -14,6 +14,7 @@
 #   kstats           rocprofv3 --kernel-trace --stats of the default bench
 #   lower            tools/lower_phy_bench.py with the multi-sector sweep
 #   lower_trace      rocprofv3 kernel trace of the sector group at 8 sectors
+#   dulow            tools/du_low_bench.py: lower PHY + PUSCH service per sector, paced, 1..8 sectors
 #   lds              PMC pass of the bench: LDS issue stalls, bank conflicts, LDS-array cycles per kernel
 #   ab:DIR[:N]       A/B of the default bench: the in-tree library against srsran-5g_amd/DIR's, N rounds
 set -o pipefail
@@ -72,6 +73,10 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/lower_trace" -o lower -- python3 -u \
         tools/lower_phy_bench.py --slots 100 --sectors 8 --sweep-only group4 > "$OUT/lower_trace.json" \
         2> "$OUT/lower_trace.log" || { tail -20 "$OUT/lower_trace.log"; exit 1; } ;;
+    dulow)
+      timeout -k 10 500 python -u tools/du_low_bench.py > "$OUT/du_low.json" 2> "$OUT/du_low.log" \
+        || { tail -20 "$OUT/du_low.log"; exit 1; }
+      tail -c 600 "$OUT/du_low.json" ;;
     lds)
       # LDS counters of the bench's kernels (one PMC pass): issue stalls on LDS, bank-conflict cycles, LDS-array cycles
       timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_LDS \

@@ -68,6 +68,11 @@
 #include "lib/phy/upper/uplink_processor_impl.h"
 #include "srsran/gateways/baseband/buffer/baseband_gateway_buffer_reader.h"
 #include "srsran/phy/lower/lower_phy_rx_symbol_context.h"
+#include "srsran/gateways/baseband/buffer/baseband_gateway_buffer_writer.h"
+#include "srsran/phy/lower/processors/downlink/pdxch/pdxch_processor.h"
+#include "srsran/phy/lower/processors/downlink/pdxch/pdxch_processor_baseband.h"
+#include "srsran/phy/lower/processors/downlink/pdxch/pdxch_processor_notifier.h"
+#include "srsran/phy/lower/processors/downlink/pdxch/pdxch_processor_request_handler.h"
 #include "srsran/phy/lower/processors/uplink/puxch/puxch_processor.h"
 #include "srsran/phy/lower/processors/uplink/puxch/puxch_processor_baseband.h"
 #include "srsran/phy/lower/processors/uplink/puxch/puxch_processor_notifier.h"
@@ -1333,13 +1338,19 @@ ul_harness* ul_create(int                                     device,
 class grid_capture : public upper_phy_rg_gateway
 {
 public:
-  void send(const resource_grid_context&, shared_resource_grid grid) override
+  void send(const resource_grid_context& context, shared_resource_grid grid) override
   {
+    if (forward) {
+      forward(context, std::move(grid));  // du_low: on to the sector's lower-PHY PDxCH processor
+      sent = true;
+      return;
+    }
     if (out != nullptr) {
       store_grid(grid.get(), out, P, nsc);
     }
     sent = true;
   }
+  std::function<void(const resource_grid_context&, shared_resource_grid)> forward;
   uint16_t* out  = nullptr;
   unsigned  P    = 0;
   unsigned  nsc  = 0;
@@ -1972,6 +1983,195 @@ int chain_du_low_ul(int                 device,
     }
     group.reset();
     service.reset();
+    return 0;
+  });
+}
+
+/// du_low's downlink on one GPU at the radio's pace (TEST INFRASTRUCTURE, tools/du_low_bench.py --direction dl):
+/// every sector has an upper-PHY thread running its downlink processor (the GPU PDSCH slot batch) and a radio thread
+/// that, at the start of slot s, asks the upper thread for slot s + 2 and then takes the 14 symbols of slot s from the
+/// sector's lower-PHY PDxCH processor (process_symbol), one symbol duration apart; the downlink processor's grid goes
+/// to the PDxCH processor (handle_request) through the upper-PHY gateway, as in du_low. grouped: the PDxCH processors
+/// come from one lower_phy_sector_group. PDUs / weights / TBs as chain_dl_bench. Outputs per sector k: lag[4k..4k+3]
+/// as chain_du_low_ul (the last entry: late PDxCH requests); results[2k], [2k+1] = symbols that carried a slot's
+/// samples, DL slots the upper thread finished. Returns 0 (< 0 on error).
+int chain_du_low_dl(int                 device,
+                    unsigned            nof_sectors,
+                    unsigned            slots,
+                    int                 nof_pdus,
+                    const chain_params* pdus,
+                    const float*        weights,
+                    const uint8_t*      tbs,
+                    const int*          tb_bytes,
+                    unsigned            nof_ports,
+                    unsigned            grid_prb,
+                    unsigned            dft_size,
+                    int                 grouped,
+                    double*             lag,
+                    int*                results,
+                    double*             seconds)
+{
+  return guarded("chain_du_low_dl", [&] {
+    using clock     = std::chrono::steady_clock;
+    const double srate = static_cast<double>(dft_size) * 30e3;
+    std::vector<unsigned> size(28);
+    for (unsigned s = 0; s != 28; ++s) {
+      size[s] = cyclic_prefix(cyclic_prefix::NORMAL).get_length(s, subcarrier_spacing::kHz30).to_samples(srate) +
+                dft_size;
+    }
+    std::shared_ptr<lower_phy_sector_group> group;
+    if (grouped != 0) {
+      lower_phy_group_configuration gc;
+      gc.device      = device;
+      gc.nof_sectors = nof_sectors;
+      group          = create_lower_phy_sector_group(gc);
+    }
+    struct du_dl_notifier : public pdxch_processor_notifier {
+      std::atomic<unsigned> late{0};
+      void                  on_pdxch_request_late(const resource_grid_context& /*c*/) override { ++late; }
+    };
+    struct writer : public baseband_gateway_buffer_writer {
+      std::vector<span<cf_t>> ch;
+      unsigned                get_nof_channels() const override { return ch.size(); }
+      unsigned                get_nof_samples() const override { return ch.empty() ? 0 : ch[0].size(); }
+      span<cf_t>              get_channel_buffer(unsigned i) override { return ch[i]; }
+    };
+    struct sector_state {
+      dl_harness*                      dl = nullptr;
+      du_dl_notifier                   notifier;
+      std::unique_ptr<pdxch_processor> pdxch;
+      std::vector<cf_t>                out;  ///< one symbol of every port (a radio's baseband buffer)
+      std::atomic<int>                 dl_slots{0};
+    };
+    std::vector<std::unique_ptr<bench_worker>> radio, upper;
+    std::vector<std::unique_ptr<sector_state>> st(nof_sectors);
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      radio.push_back(std::make_unique<bench_worker>());
+      upper.push_back(std::make_unique<bench_worker>());
+    }
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      st[k] = std::make_unique<sector_state>();
+      upper[k]->post([&, k] { st[k]->dl = dl_create(device, 1, nof_ports, grid_prb); });
+      upper[k]->wait();
+      radio[k]->post([&, k] {
+        pdxch_processor_configuration c;
+        c.cp             = cyclic_prefix::NORMAL;
+        c.scs            = subcarrier_spacing::kHz30;
+        c.srate          = sampling_rate::from_Hz(srate);
+        c.bandwidth_rb   = grid_prb;
+        c.center_freq_Hz = 3.5e9 + 2e7 * k;
+        c.nof_tx_ports   = nof_ports;
+        st[k]->pdxch     = (group ? create_pdxch_processor_factory_gpu(group) : create_pdxch_processor_factory_gpu(device))
+                           ->create(c);
+        st[k]->pdxch->connect(st[k]->notifier);
+        st[k]->out.resize(static_cast<size_t>(nof_ports) * (dft_size + dft_size / 8));
+      });
+      radio[k]->wait();
+      pdxch_processor* px = st[k]->pdxch.get();
+      st[k]->dl->gateway.forward = [px](const resource_grid_context& c, shared_resource_grid g) {
+        px->get_request_handler().handle_request(g, c);
+      };
+    }
+    // The downlink processor of one slot (upper thread).
+    auto dl_slot = [&](unsigned k, unsigned sl) {
+      dl_harness*               h  = st[k]->dl;
+      const slot_point          sp(subcarrier_spacing::kHz30, sl % 20480);
+      unique_downlink_processor dl = h->proc->get_controller().configure_resource_grid({sp, k}, h->pool->grab());
+      if (!dl.is_valid()) {
+        return;
+      }
+      const uint8_t* tb = tbs;
+      const float*   w  = weights;
+      for (int q = 0; q != nof_pdus; ++q) {
+        chain_params c = pdus[q];
+        c.slot         = static_cast<int>(sp.slot_index());
+        static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data;
+        data.emplace_back(span<const uint8_t>(tb, static_cast<size_t>(tb_bytes[q])));
+        dl->process_pdsch(std::move(data), make_pdsch_pdu(c, w));
+        tb += tb_bytes[q];
+        w += 2 * c.nof_ports * c.nof_layers;
+      }
+      dl.release();
+      ++st[k]->dl_slots;
+    };
+    const clock::duration period = std::chrono::duration_cast<clock::duration>(std::chrono::nanoseconds(1000000 / 28));
+    std::vector<unsigned> slot_no(nof_sectors, 0);
+    std::vector<double>   tmp(4 * nof_sectors, 0.0);
+    auto run = [&](unsigned k, unsigned n, clock::time_point t0, bool paced) {
+      if (paced) {
+        (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
+      }
+      sector_state& s = *st[k];
+      writer        buf;
+      double        max_lag = 0, last_lag = 0;
+      long          late = 0, i_sym = 0, with_data = 0;
+      for (unsigned i = 0; i != n; ++i) {
+        const unsigned   sl = slot_no[k]++;
+        const slot_point sp(subcarrier_spacing::kHz30, sl % 20480);
+        upper[k]->wait();  // the slot before's DL job has finished (it had a whole slot)
+        upper[k]->post([&, k, sl] { dl_slot(k, sl + 2); });
+        const unsigned q0 = sp.subframe_slot_index() * 14;
+        for (unsigned l = 0; l != 14; ++l) {
+          if (paced) {
+            const clock::time_point due = t0 + period * i_sym++;
+            const clock::time_point now = clock::now();
+            if (now < due) {
+              std::this_thread::sleep_until(due);
+              last_lag = 0;
+            } else {
+              last_lag = std::chrono::duration<double>(now - due).count();
+              max_lag  = std::max(max_lag, last_lag);
+              late += (now - due) > period * 14 ? 1 : 0;
+            }
+          }
+          const unsigned ssz = size[q0 + l];
+          buf.ch.clear();
+          for (unsigned p = 0; p != nof_ports; ++p) {
+            buf.ch.emplace_back(s.out.data() + static_cast<size_t>(p) * (dft_size + dft_size / 8), ssz);
+          }
+          with_data += s.pdxch->get_baseband().process_symbol(buf, {sp, k, l}) ? 1 : 0;
+        }
+      }
+      upper[k]->wait();
+      tmp[4 * k]     = max_lag;
+      tmp[4 * k + 1] = last_lag;
+      tmp[4 * k + 2] = static_cast<double>(late) / std::max(1L, i_sym);
+      tmp[4 * k + 3] = static_cast<double>(with_data);
+    };
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      radio[k]->post([&, k] { run(k, 20, clock::now(), false); });
+    }
+    for (auto& w : radio) {
+      w->wait();
+    }
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      st[k]->notifier.late = 0;
+      st[k]->dl_slots      = 0;
+    }
+    const clock::time_point t0 = clock::now() + std::chrono::milliseconds(2);
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      radio[k]->post([&, k] { run(k, slots, t0, true); });
+    }
+    for (auto& w : radio) {
+      w->wait();
+    }
+    *seconds = std::chrono::duration<double>(clock::now() - t0).count();
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      lag[4 * k]         = tmp[4 * k];
+      lag[4 * k + 1]     = tmp[4 * k + 1];
+      lag[4 * k + 2]     = tmp[4 * k + 2];
+      lag[4 * k + 3]     = st[k]->notifier.late.load();
+      results[2 * k]     = static_cast<int>(tmp[4 * k + 3]);
+      results[2 * k + 1] = st[k]->dl_slots.load();
+    }
+    for (unsigned k = 0; k != nof_sectors; ++k) {
+      st[k]->dl->gateway.forward = nullptr;
+      radio[k]->post([&, k] { st[k]->pdxch.reset(); });
+      radio[k]->wait();
+      upper[k]->post([&, k] { delete st[k]->dl; });
+      upper[k]->wait();
+    }
+    group.reset();
     return 0;
   });
 }

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""du_low's uplink on one GPU at the radio's pace: S sectors, each a thread delivering its 100 MHz 4-port samples one
+"""du_low on one GPU at the radio's pace. Uplink: S sectors, each a thread delivering its 100 MHz 4-port samples one
 OFDM symbol per symbol duration to its lower-PHY PUxCH processor (row b5: one GPU processor per sector, or the sector
 group), whose grid is the grid of one of the sector's uplink processors (row b6: the GPU slot batches on one shared
 PUSCH service) with that slot's PUSCH PDUs; the last symbol of a slot starts the uplink processor, as du_low's
@@ -8,7 +8,10 @@ rx-symbol handler does (oracle/ref/ref_chain.cpp chain_du_low_ul). The PUSCH pro
 
 Reported per S: the largest lag behind the symbol pace, the lag at the end, the fraction of symbols more than a slot
 late, late PUxCH requests and the PUSCH results notified; real time = every sector ends less than a slot behind with
-under 1 % of its symbols a slot late and every PDU notified. TEST INFRASTRUCTURE (diagnostic); GPU box:
+under 1 % of its symbols a slot late and every PDU notified. Downlink (chain_du_low_dl): per sector an upper-PHY thread
+runs the downlink processor (GPU PDSCH slot batch, one 270-PRB 4-layer PDU) for slot s + 2 while the radio thread takes
+slot s's 14 symbols from the PDxCH processor, the grid going from the upper-PHY gateway to handle_request; real time as
+for the UL, with every slot's symbols carrying samples and no late request. TEST INFRASTRUCTURE (diagnostic); GPU box:
     python tools/du_low_bench.py [--sectors 1,2,4,6,8] [--slots 200]
 """
 import argparse
@@ -45,8 +48,55 @@ def profiles():
     yield "16 UEs x 17 PRB per slot", pdus, tb_list
 
 
+def dl_profiles(rng):
+    tbs = sch.tbs_calculate(270, 12, 6 * 3 * 2, 0, 8, 948.0, 4)
+    p = H.params(slot=0, rnti=1, n_id=0, scrambling_id=0, nof_rb=270, rb_start=0, bwp_size=273, qm=8,
+                 target_code_rate=948.0, nof_layers=4, nof_ports=4, start_symbol=2, nof_symbols=12,
+                 dmrs_mask=(1 << 2) | (1 << 7) | (1 << 11), base_graph=sch.base_graph(tbs, 948 / 1024),
+                 tbs_lbrm_bytes=159749)
+    q, _ = np.linalg.qr(rng.normal(size=(4, 4)) + 1j * rng.normal(size=(4, 4)))
+    yield "one 270-PRB 4-layer 256QAM PDSCH per slot", [p], [tbs], [q.astype(np.complex64)]
+
+
+def run_dl(lib, args, out):
+    f = lib.chain_du_low_dl
+    f.restype = ctypes.c_int
+    f.argtypes = ([ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_int, ctypes.POINTER(H.ChainParams)] +
+                  [ctypes.c_void_p] * 3 + [ctypes.c_uint] * 3 + [ctypes.c_int] + [ctypes.c_void_p] * 3)
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    rng = np.random.default_rng(6)
+    for name, pdus, tbs, weights in dl_profiles(rng):
+        arr = (H.ChainParams * len(pdus))(*pdus)
+        tbb = np.array(tbs, np.int32) // 8
+        data = rng.integers(0, 256, int(tbb.sum())).astype(np.uint8)
+        w = np.ascontiguousarray(np.concatenate([x.ravel() for x in weights]), np.complex64).view(np.float32)
+        for variant in args.variants.split(","):
+            lower = "sector group" if variant == "group" else "one processor per sector"
+            res = {"direction": "dl", "profile": name, "lower_phy": lower, "by_sectors": {}}
+            for S in (int(v) for v in args.sectors.split(",")):
+                lag = np.zeros((S, 4), np.float64)
+                results = np.zeros((S, 2), np.int32)
+                secs = np.zeros(1, np.float64)
+                r = f(0, S, args.slots, len(pdus), arr, ptr(w), ptr(data), ptr(tbb), P, PRB, DFT,
+                      1 if variant == "group" else 0, ptr(lag), ptr(results), ptr(secs))
+                assert r == 0, r
+                # every slot's 14 symbols but the first two slots' (requested before the run) carried samples
+                complete = bool((results[:, 0] >= 14 * (args.slots - 2)).all())
+                rt = bool(lag[:, 1].max() < 0.5e-3 and lag[:, 2].max() < 0.01 and complete and lag[:, 3].sum() == 0)
+                res["by_sectors"][S] = {"max_lag_us": 1e6 * lag[:, 0].max(), "final_lag_us": 1e6 * lag[:, 1].max(),
+                                        "late_fraction": lag[:, 2].max(), "late_requests": int(lag[:, 3].sum()),
+                                        "symbols_with_samples": int(results[:, 0].sum()),
+                                        "dl_slots_processed": int(results[:, 1].sum()), "complete": complete,
+                                        "seconds": float(secs[0]), "real_time": rt}
+                print(json.dumps({name: {variant: {S: res["by_sectors"][S]}}}), file=sys.stderr, flush=True)
+            rts = [S for S, v in res["by_sectors"].items() if v["real_time"]]
+            res["sectors_at_real_time"] = max(rts) if rts else 0
+            out["runs"].append(res)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--direction", default="ul,dl")
     ap.add_argument("--sectors", default="1,2,4,6,8")
     ap.add_argument("--slots", type=int, default=200)
     ap.add_argument("--in-flight", default="4,13")
@@ -63,13 +113,16 @@ def main():
     rng = np.random.default_rng(5)
     samples = ((rng.normal(size=n) + 1j * rng.normal(size=n)) * 0.05).astype(np.complex64)
     out = {"config": {"sectors": "100 MHz 30 kHz 4T4R", "slots": args.slots}, "runs": []}
-    for name, pdus, tbs in profiles():
+    if "dl" in args.direction:
+        run_dl(lib, args, out)
+    for name, pdus, tbs in (profiles() if "ul" in args.direction else ()):
         arr = (H.ChainParams * len(pdus))(*pdus)
         tbb = np.array(tbs, np.int32) // 8
         for variant in args.variants.split(","):
             for inflight in (int(v) for v in args.in_flight.split(",")):
                 lower = "sector group" if variant == "group" else "one processor per sector"
-                res = {"profile": name, "lower_phy": lower, "symbols_in_flight": inflight, "by_sectors": {}}
+                res = {"direction": "ul", "profile": name, "lower_phy": lower, "symbols_in_flight": inflight,
+                       "by_sectors": {}}
                 for S in (int(v) for v in args.sectors.split(",")):
                     lag = np.zeros((S, 4), np.float64)
                     results = np.zeros((S, 2), np.int32)

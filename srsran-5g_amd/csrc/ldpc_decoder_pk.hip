@@ -89,6 +89,15 @@ __device__ __forceinline__ u16x2 uu(int x)
 /// 1: a row's two-minimum search runs as two independent chains (even and odd edges) merged at the end
 /// (k1 = min(k1a, k1b), k2 = min(max(k1a, k1b), k2a, k2b): the exact result of the sequential scan, since the keys
 /// |v| * 32 + e are distinct) - half the serial min/max dependency chain of a 19-edge row (A/B switch).
+/// Soft-bit loads issued this many edges ahead of their use in a row's first pass (0: the compiler's placement, one
+/// edge ahead); LDPC_PK_PRELOAD_GROUPS > 0 also pins the pattern (that many VALU, then the next edge's two loads).
+#ifndef LDPC_PK_PRELOAD
+#define LDPC_PK_PRELOAD 0
+#endif
+#ifndef LDPC_PK_PRELOAD_GROUPS
+#define LDPC_PK_PRELOAD_GROUPS 0
+#endif
+
 #ifndef LDPC_PK_SPLIT_SEARCH
 #define LDPC_PK_SPLIT_SEARCH 0
 #endif
@@ -230,8 +239,34 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   const pk_consts kc  = make_pk_consts();
 
   uint32_t addr[KEEP_ADDR ? deg : 1];
+#if LDPC_PK_PRELOAD
+  // Soft-bit loads PD edges ahead of their use (a layer's positions are disjoint, so every load of the row may issue
+  // before any store); the group barriers keep the scheduler from sinking them next to their use.
+  constexpr int PD = LDPC_PK_PRELOAD < deg ? LDPC_PK_PRELOAD : deg;
+  uint32_t      aq[deg];
+  int           qa[deg], qb[deg];
+  auto          load_edge = [&](auto E) {
+    constexpr int e   = decltype(E)::value;
+    constexpr int col = G::col(e0 + e);
+    aq[e]             = pair_address(z2x2, ab[e0 + e]);
+    qa[e]             = soft[col * CS + aq[e]];
+    qb[e]             = soft[col * CS + (aq[e] ^ 1u)];
+  };
+  static_for<PD>(load_edge);
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * PD, 0);
+#endif
   static_for<deg>([&](auto E) {
     constexpr int  e   = decltype(E)::value;
+#if LDPC_PK_PRELOAD
+    if constexpr (e + PD < deg) {
+      load_edge(std::integral_constant<int, e + PD>{});
+    }
+    const uint32_t a = aq[e];
+    if constexpr (KEEP_ADDR) {
+      addr[e] = a;
+    }
+    const s16x2 sb{static_cast<short>(qa[e]), static_cast<short>(qb[e])};
+#else
     constexpr int  col = G::col(e0 + e);
     const uint32_t a   = pair_address(z2x2, ab[e0 + e]);
     if constexpr (KEEP_ADDR) {
@@ -243,6 +278,7 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
                    static_cast<short>(soft[col * CS + (a ^ 1u)])};
 #else  // timing experiments only
     const s16x2 sb = as_s16(((a * 0x9e3779b1u) >> 3) & 0x003f003fu);
+#endif
 #endif
     // Previous c2v of this edge: magnitude min2 at the argmin, min1 elsewhere; sign from the sign bits.
     constexpr int  pos = (e < SIGNS_W0) ? e : e - SIGNS_W0;
@@ -266,6 +302,12 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
       k1 = __builtin_elementwise_min(key, k1);
     }
     sx ^= bits(v);
+#endif
+#if LDPC_PK_PRELOAD && LDPC_PK_PRELOAD_GROUPS
+    if constexpr (e + PD < deg) {
+      __builtin_amdgcn_sched_group_barrier(0x002, LDPC_PK_PRELOAD_GROUPS, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
 #endif
 #ifdef LDPC_PK_EXPERIMENT_EXTRA_VALU  // timing experiments only: N extra independent VALU per edge
     {

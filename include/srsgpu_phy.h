@@ -809,6 +809,22 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
                                       uint8_t*                         d_tb_crc_ok,
                                       void*                            stream);
 
+/** As srsgpu_pusch_decoder_plan_execute, with codeblock c's HARQ soft buffer (N bytes, the rate dematcher's output and
+ *  the decoder's input) at d_harq_cbs[c] - a device array of one pointer per codeblock of the plan, e.g. the slots of
+ *  a persistent rx-buffer arena (the reference's rx_buffer.h:72 get_codeblock_soft_bits for the codeblock's absolute
+ *  identifier, :65) - instead of at d_harq + srsgpu_pusch_tb_config::harq_offset. The soft bits stay in the arena: no
+ *  copy into a batch buffer before the decode and back after it (srsgpu_harq_copy_arenas). Asynchronous,
+ *  hipGraph-capturable (the pointer array may change between replays). */
+int srsgpu_pusch_decoder_plan_execute_arena(const srsgpu_pusch_decoder_plan* plan,
+                                            const int8_t*                    d_llrs,
+                                            int8_t* const*                   d_harq_cbs,
+                                            uint8_t*                         d_cb_crc_ok,
+                                            uint8_t*                         d_cb_msgs,
+                                            int32_t*                         d_cb_nof_iterations,
+                                            uint8_t*                         d_tbs,
+                                            uint8_t*                         d_tb_crc_ok,
+                                            void*                            stream);
+
 /** The transport-block stage alone (pusch_decoder_impl.cpp:386 join_and_notify, :438 concatenate_codeblocks): TB
  *  assembly from the codeblock messages and flags already in d_cb_msgs / d_cb_crc_ok (the plan's codeblock layout,
  *  SRSGPU_CB_MSG_STRIDE bytes per codeblock) and the TB CRC24A check; a TB CRC mismatch clears the TB's codeblock
@@ -870,6 +886,20 @@ typedef struct {
 } srsgpu_copy_span;
 
 int srsgpu_copy_spans(const srsgpu_copy_span* d_spans, uint32_t nof_spans, uint64_t max_bytes, void* stream);
+
+/** As srsgpu_pusch_chest_plan_execute, with the span copies d_spans[0, nof_spans) (each as in srsgpu_copy_spans,
+ *  max_bytes the largest) done in the same launch by extra workgroups while the estimator's run: for a slot batch whose rx
+ *  grids are read from mapped host memory, the data-symbol rows, which the estimator does not read, arrive while it
+ *  works on the DM-RS rows copied before (pusch_processor_impl.cpp:165-213 estimates from the DM-RS symbols only). */
+int srsgpu_pusch_chest_plan_execute_copy(const srsgpu_pusch_chest_plan* plan,
+                                         const uint32_t*                d_grids,
+                                         uint32_t*                      d_ch_estimates,
+                                         float*                         d_noise_var,
+                                         float*                         d_metrics,
+                                         const srsgpu_copy_span*        d_spans,
+                                         uint32_t                       nof_spans,
+                                         uint64_t                       max_bytes,
+                                         void*                          stream);
 
 /** Stage timing: with enable = 1 every execute records HIP events on its stream around the three kernel stages
  *  (0: rate dematching, 1: LDPC decoding, 2: TB assembly + CRC); with enable = 2 only around the decoding stage (two

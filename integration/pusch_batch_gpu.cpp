@@ -59,6 +59,18 @@ namespace {
 
 constexpr unsigned HARQ_SLOT_BYTES = 66 * 384;  ///< N of BG1 at Z = 384: one arena slot per codeblock.
 
+/// The rate dematcher and decoder read and write the HARQ soft buffers in the arena through a per-codeblock pointer
+/// table (srsgpu_pusch_decoder_plan_execute_arena). SRSGPU_HARQ_COPY=1 (A/B): copy them into a batch buffer before
+/// the decode and back after it (two srsgpu_harq_copy_arenas launches).
+bool harq_in_arena()
+{
+  static const bool copy = [] {
+    const char* e = std::getenv("SRSGPU_HARQ_COPY");
+    return e != nullptr && e[0] == '1';
+  }();
+  return !copy;
+}
+
 using clock_type = std::chrono::steady_clock;
 
 double us_between(clock_type::time_point a, clock_type::time_point b)
@@ -455,7 +467,12 @@ struct launch_plan {
   std::vector<uint32_t>          job_arena;  ///< per job: its arena's index in `arenas`
   unsigned                       nof_copies = 0;
   std::vector<std::pair<size_t, unsigned>> dc_zero;  ///< estimate byte offset and rows of each DC zeroing
-  size_t   arena_o = 0, flag_o = 0, iter_o = 0, tbok_o = 0, nv_o = 0, m_o = 0, st_o = 0, uci_o = 0, tb_o = 0, end_o = 0;
+  size_t   arena_o = 0, ptr_o = 0, flag_o = 0, iter_o = 0, tbok_o = 0, nv_o = 0, m_o = 0, st_o = 0, uci_o = 0, tb_o = 0,
+           end_o = 0;
+  std::vector<uint16_t> dmrs_rows;  ///< Per job: the union of its PDUs' DM-RS symbol masks (rows the estimator reads).
+  unsigned nof_dmrs_spans = 0, nof_data_spans = 0;  ///< Split grid copy: one span per (port, symbol) row.
+  bool     graph_split    = false;                 ///< The captured graph copies the grids itself (split).
+  const void* graph_spans = nullptr;               ///< ... from this span list.
   unsigned n = 0, cb_total = 0, llr_total = 0, harq_total = 0, max_grid = 0;
 
   static void destroy(launch_plan* p)
@@ -551,7 +568,7 @@ private:
     }
   };
   struct deferred_layout {
-    size_t                   arena_o = 0, flag_o = 0, iter_o = 0, tbok_o = 0, csi2_o = 0, tb_o = 0, end_o = 0;
+    size_t arena_o = 0, ptr_o = 0, flag_o = 0, iter_o = 0, tbok_o = 0, csi2_o = 0, tb_o = 0, end_o = 0;
     std::array<uint32_t, 14> csi2_counts{};
   };
   plan_cache<deferred_plan> deferred_plans{deferred_plan::destroy, 16};
@@ -1059,6 +1076,13 @@ launch_plan* pusch_launcher::create_plan(const std::vector<std::unique_ptr<pusch
     for (const auto& z : L.dc_zero_local) {
       lp->dc_zero.push_back(z);
     }
+    uint16_t rows = 0;
+    for (const pusch_chest_desc& d : L.chests) {
+      rows |= d.c.dmrs_symbol_mask;
+    }
+    lp->dmrs_rows.push_back(rows);
+    lp->nof_dmrs_spans += P * static_cast<unsigned>(__builtin_popcount(rows & 0x3fffu));
+    lp->nof_data_spans += P * (14u - static_cast<unsigned>(__builtin_popcount(rows & 0x3fffu)));
     int8_t*    arena = job->batch->arena->d_soft;
     const auto it    = std::find(lp->arenas.begin(), lp->arenas.end(), arena);
     lp->job_arena.push_back(static_cast<uint32_t>(it - lp->arenas.begin()));
@@ -1097,11 +1121,13 @@ launch_plan* pusch_launcher::create_plan(const std::vector<std::unique_ptr<pusch
     srsgpu_check(srsgpu_pusch_decoder_plan_create(ctx, SRSGPU_LDPC_IMPL_SIMD, tbs.data(), tbs.size(), &lp->dec), WHO);
   }
 
-  // Staging image: [copy jobs | arena table | CB CRC flags] uploaded, [CB CRC flags | iterations | TB CRC flags | nv |
-  // metrics | statistics | UCI streams | TBs] downloaded (the CRC flags are the HARQ context in and the result out).
+  // Staging image: [copy jobs | arena table | HARQ buffer pointers | CB CRC flags] uploaded, [CB CRC flags | iterations |
+  // TB CRC flags | nv | metrics | statistics | UCI streams | TBs] downloaded (the CRC flags are the HARQ context in and
+  // the result out).
   auto align  = [](size_t x) { return (x + 63) / 64 * 64; };
   lp->arena_o = align(static_cast<size_t>(copy_b) * sizeof(srsgpu_harq_copy_job));
-  lp->flag_o  = align(lp->arena_o + lp->arenas.size() * sizeof(int8_t*));
+  lp->ptr_o   = align(lp->arena_o + lp->arenas.size() * sizeof(int8_t*));
+  lp->flag_o  = align(lp->ptr_o + static_cast<size_t>(cb_b) * sizeof(int8_t*));
   lp->iter_o = align(lp->flag_o + cb_b);
   lp->tbok_o = align(lp->iter_o + static_cast<size_t>(cb_b) * sizeof(int32_t));
   lp->nv_o   = align(lp->tbok_o + n);
@@ -1140,6 +1166,21 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
   // statistics kernels' small scattered result stores cross PCIe one by one (profiles/r5_io_mapped_ab.txt).
   static const bool io_mapped = std::getenv("SRSGPU_IO_MAPPED") != nullptr;
   zc                          = download && io_mapped;
+  // Split grid copy: every job's grid is read from mapped host memory by the launch: a copy launch before the graph
+  // moves the DM-RS symbol rows, and the channel estimator's launch (which reads only those) moves the data-symbol
+  // rows on extra workgroups while it runs. SRSGPU_GRID_SPLIT=0 (A/B): the whole grids in one copy launch before the
+  // graph. (A fork onto a second stream inside the graph measured serialised and slower.)
+  static const bool split_enabled = [] {
+    const char* e = std::getenv("SRSGPU_GRID_SPLIT");
+    return e == nullptr || e[0] != '0';
+  }();
+  bool split = split_enabled;
+  for (const auto& job : jobs) {
+    split = split && job->grid_src != nullptr;
+  }
+  if (split) {
+    spans.reserve((lp->nof_dmrs_spans + lp->nof_data_spans) * sizeof(srsgpu_copy_span));
+  }
 
   // Buffers (grow-only; a move invalidates the captured graphs).
   {
@@ -1159,7 +1200,8 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
     }
   }
   hipStream_t s = stream.get();
-  if (lp->graph == nullptr || lp->graph_buffers != buffer_generation || lp->graph_download != download) {
+  if (lp->graph == nullptr || lp->graph_buffers != buffer_generation || lp->graph_download != download ||
+      lp->graph_split != split || (split && lp->graph_spans != spans.dev())) {
     std::lock_guard<std::recursive_mutex> setup_lock(hip_setup_mutex());
     if (lp->graph != nullptr) {
       (void)hipGraphExecDestroy(lp->graph);
@@ -1169,9 +1211,18 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
       if (!zc) {
         io.upload(0, lp->iter_o, s);
       }
-      srsgpu_check(srsgpu_pusch_chest_plan_execute(lp->chest, d_grids, d_ce, iod<float>(lp->nv_o),
-                                                   iod<float>(lp->m_o), s),
-                   WHO);
+      if (split) {
+        // The estimator's launch also copies the data-symbol rows (extra workgroups), after the DM-RS rows it reads
+        // were copied by the launch before the graph.
+        srsgpu_check(srsgpu_pusch_chest_plan_execute_copy(
+                         lp->chest, d_grids, d_ce, iod<float>(lp->nv_o), iod<float>(lp->m_o),
+                         spans.dev<srsgpu_copy_span>() + lp->nof_dmrs_spans, lp->nof_data_spans, row, s),
+                     WHO);
+      } else {
+        srsgpu_check(srsgpu_pusch_chest_plan_execute(lp->chest, d_grids, d_ce, iod<float>(lp->nv_o),
+                                                     iod<float>(lp->m_o), s),
+                     WHO);
+      }
       // pusch_processor_impl.cpp:222-240: the DC subcarrier's estimate is zeroed for CP-OFDM transmissions over it.
       for (const auto& z : lp->dc_zero) {
         hip_check(hipMemset2DAsync(reinterpret_cast<uint8_t*>(d_ce) + z.first, row, 0, sizeof(uint32_t), z.second,
@@ -1185,26 +1236,39 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
         int8_t* uci = iod<int8_t>(lp->uci_o);
         srsgpu_check(srsgpu_ulsch_demux_plan_execute(lp->demux, d_llr, d_llr, uci, uci, nullptr, s), WHO);
       }
-      srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_BATCH, iod<int8_t*>(lp->arena_o),
-                                           HARQ_SLOT_BYTES, d_harq, iod<srsgpu_harq_copy_job>(0),
-                                           lp->nof_copies, s),
-                   WHO);
-      if (lp->dec != nullptr) {
-        srsgpu_check(srsgpu_pusch_decoder_plan_execute(lp->dec, d_llr, d_harq, iod<uint8_t>(lp->flag_o),
-                                                       msgs.dev<uint8_t>(), iod<int32_t>(lp->iter_o),
-                                                       iod<uint8_t>(lp->tb_o), iod<uint8_t>(lp->tbok_o), s),
+      if (harq_in_arena()) {
+        // The rate dematcher and the decoder work on the soft buffers in the rx-buffer arenas through the per-codeblock
+        // pointer table (no copy into the batch HARQ buffer and back).
+        if (lp->dec != nullptr) {
+          srsgpu_check(srsgpu_pusch_decoder_plan_execute_arena(
+                           lp->dec, d_llr, iod<int8_t*>(lp->ptr_o), iod<uint8_t>(lp->flag_o), msgs.dev<uint8_t>(),
+                           iod<int32_t>(lp->iter_o), iod<uint8_t>(lp->tb_o), iod<uint8_t>(lp->tbok_o), s),
+                       WHO);
+        }
+      } else {
+        srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_BATCH, iod<int8_t*>(lp->arena_o),
+                                             HARQ_SLOT_BYTES, d_harq, iod<srsgpu_harq_copy_job>(0),
+                                             lp->nof_copies, s),
+                     WHO);
+        if (lp->dec != nullptr) {
+          srsgpu_check(srsgpu_pusch_decoder_plan_execute(lp->dec, d_llr, d_harq, iod<uint8_t>(lp->flag_o),
+                                                         msgs.dev<uint8_t>(), iod<int32_t>(lp->iter_o),
+                                                         iod<uint8_t>(lp->tb_o), iod<uint8_t>(lp->tbok_o), s),
+                       WHO);
+        }
+        srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_ARENA, iod<int8_t*>(lp->arena_o),
+                                             HARQ_SLOT_BYTES, d_harq, iod<srsgpu_harq_copy_job>(0),
+                                             lp->nof_copies, s),
                      WHO);
       }
-      srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_ARENA, iod<int8_t*>(lp->arena_o),
-                                           HARQ_SLOT_BYTES, d_harq, iod<srsgpu_harq_copy_job>(0),
-                                           lp->nof_copies, s),
-                   WHO);
       if (download && !zc) {
         io.download(lp->flag_o, lp->end_o - lp->flag_o, s);
       }
     });
     lp->graph_buffers  = buffer_generation;
     lp->graph_download = download;
+    lp->graph_split    = split;
+    lp->graph_spans    = split ? spans.dev() : nullptr;
   }
   tm.built = clock_type::now();
 
@@ -1214,13 +1278,19 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
   auto*    copies   = ioh<srsgpu_harq_copy_job>(0);
   bool     any_msgs = false;
   std::memcpy(ioh(lp->arena_o), lp->arenas.data(), lp->arenas.size() * sizeof(int8_t*));
+  auto* harq_ptrs = ioh<int8_t*>(lp->ptr_o);
   for (size_t j = 0; j != jobs.size(); ++j) {
     const auto&       job = jobs[j];
     const job_layout& L   = job->lay;
+    if (L.copies.size() != L.cb_total) {
+      throw std::logic_error(std::string(WHO) + ": one HARQ copy per codeblock expected");
+    }
     for (const srsgpu_harq_copy_job& c : L.copies) {
       *copies = c;
       copies->batch_offset += harq_b;
       copies->arena = lp->job_arena[j];
+      // Codeblock cb_b + k of the plan (the job's copies are in codeblock order): its arena slot.
+      *harq_ptrs++ = lp->arenas[lp->job_arena[j]] + static_cast<size_t>(c.slot) * HARQ_SLOT_BYTES;
       ++copies;
     }
     std::memcpy(ioh<uint8_t>(lp->flag_o + cb_b), L.flags.data(), L.cb_total);
@@ -1264,7 +1334,30 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
   // The grids: one launch copies every job's grid from mapped host memory into its HBM grid slot (zero-copy reads;
   // a DMA copy per slot ran the service at the DMA engines' ~29 GB/s); shards uploaded by DMA are waited for. The kept
   // messages only when a CB has passed before.
-  {
+  if (split) {
+    // The graph's copy nodes read this list: [DM-RS rows of every job | data rows of every job], one row per span.
+    auto*    dm = spans.host<srsgpu_copy_span>();
+    auto*    da = dm + lp->nof_dmrs_spans;
+    unsigned nd = 0, na = 0;
+    for (size_t j = 0; j != jobs.size(); ++j) {
+      const auto* src = static_cast<const uint8_t*>(jobs[j]->grid_src);
+      auto*       dst = reinterpret_cast<uint8_t*>(jobs[j]->grid_dst);
+      for (unsigned r = 0; r != P * 14u; ++r) {
+        const srsgpu_copy_span c{src + r * row, dst + r * row, row};
+        if (((lp->dmrs_rows[j] >> (r % 14u)) & 1u) != 0) {
+          dm[nd++] = c;
+        } else {
+          da[na++] = c;
+        }
+      }
+    }
+    if (nd != lp->nof_dmrs_spans || na != lp->nof_data_spans) {
+      throw std::logic_error(std::string(WHO) + ": grid span count differs from the launch plan's");
+    }
+    if (nd > 0) {
+      srsgpu_check(srsgpu_copy_spans(spans.dev<srsgpu_copy_span>(), nd, row, s), WHO);
+    }
+  } else {
     std::vector<srsgpu_copy_span> sp;
     uint64_t                      max_bytes = 0;
     for (const auto& job : jobs) {
@@ -1331,10 +1424,12 @@ void pusch_launcher::decode_deferred(const pusch_entry&      e,
   });
   srsgpu_check(srsgpu_ulsch_demux_plan_symbol_llrs(dp->demux, 0, 4, d_lay.csi2_counts.data()), WHO);
 
-  // [copies | arena table | CB flags] up, [CB flags | iterations | TB flag | CSI Part 2 | TB] down.
+  // [copies | arena table | HARQ buffer pointers | CB flags] up, [CB flags | iterations | TB flag | CSI Part 2 | TB]
+  // down.
   const unsigned n_cb = static_cast<unsigned>(e.copies.size());
   d_lay.arena_o       = a64(n_cb * sizeof(srsgpu_harq_copy_job));
-  d_lay.flag_o        = a64(d_lay.arena_o + sizeof(int8_t*));
+  d_lay.ptr_o         = a64(d_lay.arena_o + sizeof(int8_t*));
+  d_lay.flag_o        = a64(d_lay.ptr_o + n_cb * sizeof(int8_t*));
   d_lay.iter_o        = a64(d_lay.flag_o + n_cb);
   d_lay.tbok_o        = a64(d_lay.iter_o + n_cb * sizeof(int32_t));
   d_lay.csi2_o        = a64(d_lay.tbok_o + 1);
@@ -1348,6 +1443,10 @@ void pusch_launcher::decode_deferred(const pusch_entry&      e,
   std::memcpy(d_io.host(0), e.copies.data(), n_cb * sizeof(srsgpu_harq_copy_job));
   int8_t* arena_base = harq.d_soft;
   std::memcpy(d_io.host(d_lay.arena_o), &arena_base, sizeof(arena_base));
+  for (unsigned c = 0; c != n_cb; ++c) {
+    int8_t* p = arena_base + static_cast<size_t>(e.copies[c].slot) * HARQ_SLOT_BYTES;
+    std::memcpy(d_io.host(d_lay.ptr_o + c * sizeof(int8_t*)), &p, sizeof(p));
+  }
   std::memcpy(d_io.host(d_lay.flag_o), e.flags.data(), n_cb);
   d_decoded.assign(n_cb, 0);
   bool any_msgs = false;
@@ -1367,16 +1466,24 @@ void pusch_launcher::decode_deferred(const pusch_entry&      e,
   srsgpu_check(srsgpu_ulsch_demux_plan_execute(dp->demux, d_llr, d_sch_b, d_uci_b, d_uci_b,
                                                d_io.dev<int8_t>(d_lay.csi2_o), s),
                WHO);
-  srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_BATCH, d_io.dev<int8_t*>(d_lay.arena_o), HARQ_SLOT_BYTES,
-                                       d_harq_b, d_io.dev<srsgpu_harq_copy_job>(0), n_cb, s),
-               WHO);
-  srsgpu_check(srsgpu_pusch_decoder_plan_execute(dp->dec, d_sch_b, d_harq_b, d_io.dev<uint8_t>(d_lay.flag_o),
-                                                 d_msgs.dev<uint8_t>(), d_io.dev<int32_t>(d_lay.iter_o),
-                                                 d_io.dev<uint8_t>(d_lay.tb_o), d_io.dev<uint8_t>(d_lay.tbok_o), s),
-               WHO);
-  srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_ARENA, d_io.dev<int8_t*>(d_lay.arena_o), HARQ_SLOT_BYTES,
-                                       d_harq_b, d_io.dev<srsgpu_harq_copy_job>(0), n_cb, s),
-               WHO);
+  if (harq_in_arena()) {
+    srsgpu_check(srsgpu_pusch_decoder_plan_execute_arena(dp->dec, d_sch_b, d_io.dev<int8_t*>(d_lay.ptr_o),
+                                                         d_io.dev<uint8_t>(d_lay.flag_o), d_msgs.dev<uint8_t>(),
+                                                         d_io.dev<int32_t>(d_lay.iter_o), d_io.dev<uint8_t>(d_lay.tb_o),
+                                                         d_io.dev<uint8_t>(d_lay.tbok_o), s),
+                 WHO);
+  } else {
+    srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_BATCH, d_io.dev<int8_t*>(d_lay.arena_o),
+                                         HARQ_SLOT_BYTES, d_harq_b, d_io.dev<srsgpu_harq_copy_job>(0), n_cb, s),
+                 WHO);
+    srsgpu_check(srsgpu_pusch_decoder_plan_execute(dp->dec, d_sch_b, d_harq_b, d_io.dev<uint8_t>(d_lay.flag_o),
+                                                   d_msgs.dev<uint8_t>(), d_io.dev<int32_t>(d_lay.iter_o),
+                                                   d_io.dev<uint8_t>(d_lay.tb_o), d_io.dev<uint8_t>(d_lay.tbok_o), s),
+                 WHO);
+    srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_ARENA, d_io.dev<int8_t*>(d_lay.arena_o),
+                                         HARQ_SLOT_BYTES, d_harq_b, d_io.dev<srsgpu_harq_copy_job>(0), n_cb, s),
+                 WHO);
+  }
   d_io.download(d_lay.flag_o, d_lay.end_o - d_lay.flag_o, s);
   d_msgs.download(0, static_cast<size_t>(n_cb) * SRSGPU_CB_MSG_STRIDE, s);
   hip_check(hipStreamSynchronize(s), WHO, "synchronise");

@@ -800,31 +800,33 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
 }
 
 /// d_cw_llrs / d_harq: the codeword LLRs and the HARQ buffer of the fused groups (PUSCH plans; null otherwise).
+/// d_harq_cbs (PUSCH plans, optional): codeblock c's HARQ soft buffer is d_harq_cbs[c] (then d_llrs / d_harq unused).
 int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
                          const int8_t*                   d_llrs,
                          uint8_t*                        d_out,
                          int32_t*                        d_nof_iterations,
                          uint8_t*                        d_cb_crc_ok,
                          hipStream_t                     s,
-                         const int8_t*                   d_cw_llrs = nullptr,
-                         int8_t*                         d_harq    = nullptr)
+                         const int8_t*                   d_cw_llrs  = nullptr,
+                         int8_t*                         d_harq     = nullptr,
+                         int8_t* const*                  d_harq_cbs = nullptr)
 {
   for (const auto& g : plan->groups) {
     if (g.pack == LDPC_PK4) {
       launch_ldpc_decode_pk4(g.bg, plan->impl, g.max_layers, g.d_desc, g.count, g.threads, d_llrs, d_out,
                              d_nof_iterations, plan->ctx->d_pair_ab4[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok,
-                             s);
+                             s, d_harq_cbs);
     } else if (g.packed) {
-      if (g.d_dm != nullptr && (d_cw_llrs == nullptr || d_harq == nullptr)) {
+      if (g.d_dm != nullptr && (d_cw_llrs == nullptr || (d_harq == nullptr && d_harq_cbs == nullptr))) {
         return fail(SRSGPU_ERR_INVALID_ARG, "fused decoder group without codeword LLRs / HARQ buffer");
       }
       launch_ldpc_decode_pk(g.bg, plan->impl, g.max_layers, g.split, g.d_desc, g.count, g.threads,
                             g.d_dm != nullptr ? d_cw_llrs : d_llrs, d_out, d_nof_iterations,
                             plan->ctx->d_pair_ab[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, g.d_dm,
-                            g.d_dm != nullptr ? d_harq : nullptr, s);
+                            g.d_dm != nullptr ? d_harq : nullptr, s, d_harq_cbs);
     } else {
       launch_ldpc_decode(g.bg, plan->impl, g.d_desc, g.count, g.threads, d_llrs, d_out, d_nof_iterations,
-                         plan->ctx->d_shifts32[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s);
+                         plan->ctx->d_shifts32[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s, d_harq_cbs);
     }
     HIP_TRY(hipGetLastError());
   }
@@ -1501,6 +1503,40 @@ uint64_t srsgpu_pusch_decoder_plan_decoder_input_llrs(const srsgpu_pusch_decoder
   return (plan == nullptr || plan->cbs == nullptr || plan->cbs->dec == nullptr) ? 0u : plan->cbs->dec->input_llrs;
 }
 
+namespace {
+int execute_pusch_decoder_plan(const srsgpu_pusch_decoder_plan* plan,
+                               const int8_t*                    d_llrs,
+                               int8_t*                          d_harq,
+                               int8_t* const*                   d_harq_cbs,
+                               uint8_t*                         d_cb_crc_ok,
+                               uint8_t*                         d_cb_msgs,
+                               int32_t*                         d_cb_nof_iterations,
+                               uint8_t*                         d_tbs,
+                               uint8_t*                         d_tb_crc_ok,
+                               hipStream_t                      s)
+{
+  auto* ev  = plan->timer.begin();
+  auto* evd = plan->timer_dec.begin();
+  stage_timer::mark(ev, 0, s);
+  launch_rate_dematch(plan->cbs->impl, plan->cbs->d_dm, plan->cbs->nof_cbs, d_llrs, d_harq, d_cb_crc_ok, s,
+                      d_harq_cbs);
+  HIP_TRY(hipGetLastError());
+  stage_timer::mark(ev, 1, s);
+  stage_timer::mark(evd, 0, s);
+  int r = execute_decoder_plan(plan->cbs->dec, d_harq, d_cb_msgs, d_cb_nof_iterations, d_cb_crc_ok, s, d_llrs, d_harq,
+                               d_harq_cbs);
+  if (r != SRSGPU_OK) {
+    return r;
+  }
+  stage_timer::mark(evd, 1, s);
+  stage_timer::mark(ev, 2, s);
+  launch_plan_tb_stage(plan, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, s);
+  HIP_TRY(hipGetLastError());
+  stage_timer::mark(ev, 3, s);
+  return SRSGPU_OK;
+}
+} // namespace
+
 int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
                                       const int8_t*                    d_llrs,
                                       int8_t*                          d_harq,
@@ -1515,24 +1551,26 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
       d_cb_nof_iterations == nullptr || d_tbs == nullptr || d_tb_crc_ok == nullptr) {
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  auto  s  = static_cast<hipStream_t>(stream);
-  auto* ev  = plan->timer.begin();
-  auto* evd = plan->timer_dec.begin();
-  stage_timer::mark(ev, 0, s);
-  launch_rate_dematch(plan->cbs->impl, plan->cbs->d_dm, plan->cbs->nof_cbs, d_llrs, d_harq, d_cb_crc_ok, s);
-  HIP_TRY(hipGetLastError());
-  stage_timer::mark(ev, 1, s);
-  stage_timer::mark(evd, 0, s);
-  int r = execute_decoder_plan(plan->cbs->dec, d_harq, d_cb_msgs, d_cb_nof_iterations, d_cb_crc_ok, s, d_llrs, d_harq);
-  if (r != SRSGPU_OK) {
-    return r;
+  return execute_pusch_decoder_plan(plan, d_llrs, d_harq, nullptr, d_cb_crc_ok, d_cb_msgs, d_cb_nof_iterations, d_tbs,
+                                    d_tb_crc_ok, static_cast<hipStream_t>(stream));
+}
+
+int srsgpu_pusch_decoder_plan_execute_arena(const srsgpu_pusch_decoder_plan* plan,
+                                            const int8_t*                    d_llrs,
+                                            int8_t* const*                   d_harq_cbs,
+                                            uint8_t*                         d_cb_crc_ok,
+                                            uint8_t*                         d_cb_msgs,
+                                            int32_t*                         d_cb_nof_iterations,
+                                            uint8_t*                         d_tbs,
+                                            uint8_t*                         d_tb_crc_ok,
+                                            void*                            stream)
+{
+  if (plan == nullptr || d_llrs == nullptr || d_harq_cbs == nullptr || d_cb_crc_ok == nullptr ||
+      d_cb_msgs == nullptr || d_cb_nof_iterations == nullptr || d_tbs == nullptr || d_tb_crc_ok == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
-  stage_timer::mark(evd, 1, s);
-  stage_timer::mark(ev, 2, s);
-  launch_plan_tb_stage(plan, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, s);
-  HIP_TRY(hipGetLastError());
-  stage_timer::mark(ev, 3, s);
-  return SRSGPU_OK;
+  return execute_pusch_decoder_plan(plan, d_llrs, nullptr, d_harq_cbs, d_cb_crc_ok, d_cb_msgs, d_cb_nof_iterations,
+                                    d_tbs, d_tb_crc_ok, static_cast<hipStream_t>(stream));
 }
 
 int srsgpu_pusch_decoder_plan_assemble(const srsgpu_pusch_decoder_plan* plan,

@@ -434,6 +434,31 @@ int srsgpu_pusch_chest_plan_execute(const srsgpu_pusch_chest_plan* plan,
   return SRSGPU_OK;
 }
 
+int srsgpu_pusch_chest_plan_execute_copy(const srsgpu_pusch_chest_plan* plan,
+                                         const uint32_t*                d_grids,
+                                         uint32_t*                      d_ch_estimates,
+                                         float*                         d_noise_var,
+                                         float*                         d_metrics,
+                                         const srsgpu_copy_span*        d_spans,
+                                         uint32_t                       nof_spans,
+                                         uint64_t                       max_bytes,
+                                         void*                          stream)
+{
+  if (plan == nullptr || d_grids == nullptr || d_ch_estimates == nullptr || d_noise_var == nullptr ||
+      (d_spans == nullptr && nof_spans > 0) || nof_spans > 65536 || (max_bytes & 15u) != 0 ||
+      max_bytes > (uint64_t{1} << 32)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "invalid argument (max_bytes a multiple of 16)");
+  }
+  if (plan->nof_jobs <= 0) {
+    return srsgpu_copy_spans(d_spans, nof_spans, max_bytes, stream);
+  }
+  launch_pusch_chest(plan->d_lp, plan->d_crbs, plan->d_jobs, plan->nof_jobs, plan->geom, d_grids, d_ch_estimates,
+                     d_noise_var, d_metrics, plan->d_seq, static_cast<hipStream_t>(stream), d_spans,
+                     static_cast<int>(nof_spans), max_bytes);
+  HIP_TRY(hipGetLastError());
+  return SRSGPU_OK;
+}
+
 void srsgpu_pusch_chest_plan_destroy(srsgpu_pusch_chest_plan* plan)
 {
   if (plan == nullptr) {

@@ -161,7 +161,8 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
                                                           int32_t* __restrict__ results,
                                                           const uint32_t* __restrict__ shift_table,
                                                           const uint32_t* __restrict__ crc_tables,
-                                                          uint8_t* __restrict__ cb_crc_ok)
+                                                          uint8_t* __restrict__ cb_crc_ok,
+                                                          int8_t* const* __restrict__ llr_cbs)
 {
   using G = bg_t<BG>;
   // Static LDS: its base is a link-time constant, so every soft-bit access is (lane offset + immediate).
@@ -203,7 +204,8 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
   // scatter into the column-major image. A vector inside one lifted column of the clamped region (the common case)
   // takes the short path: one address, a clamp per byte, a whole-vector non-zero test. Boundary vectors (head and
   // tail of the span, column crossings, the unclamped tail of the input) go byte by byte.
-  const int8_t*  llr   = llrs + d.llr_offset;
+  // The input: at its offset in the batch buffer, or wherever llr_cbs[cb] points (a persistent HARQ arena slot).
+  const int8_t*  llr   = (llr_cbs != nullptr) ? llr_cbs[d.cb_index] : llrs + d.llr_offset;
   const int      n_llr = static_cast<int>(d.nof_llr);
   const uint32_t ncols = __umulhi(static_cast<uint32_t>(n_llr), d.div_magic);  // whole lifted columns of input
   const uint32_t full  = ncols * static_cast<uint32_t>(Z);
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(384, LDPC_DEC_MIN_WAVES) void ldpc_decode_kernel(co
   const bool     use_crc = d.crc_table != NO_CRC_TABLE;
   const int      nsig    = d.nof_significant;
   {
-    const uint32_t head = static_cast<uint32_t>(d.llr_offset) & 15u;
+    const uint32_t head = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(llr)) & 15u;
     const uint4*   vecs = reinterpret_cast<const uint4*>(llr - head);
     const int      nvec = static_cast<int>((head + static_cast<uint32_t>(n_llr) + 15u) >> 4);
     // 5 x 16 B per lane covers a whole BG1 codeblock at Z = 384 with 384 lanes (and at every smaller Z).
@@ -448,7 +450,8 @@ void launch_ldpc_decode(int             bg,
                         const uint32_t* d_shifts,
                         const uint32_t* d_crc_tables,
                         uint8_t*        d_cb_crc_ok,
-                        hipStream_t     stream)
+                        hipStream_t     stream,
+                        int8_t* const*  d_llr_cbs)
 {
   if (nof_cbs <= 0) {
     return;
@@ -457,15 +460,15 @@ void launch_ldpc_decode(int             bg,
   dim3         grid(nof_cbs), block(block_threads);
   if (bg == 1) {
     if (mode == 1) {
-      ldpc_decode_kernel<1, 1><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok);
+      ldpc_decode_kernel<1, 1><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok, d_llr_cbs);
     } else {
-      ldpc_decode_kernel<1, 0><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok);
+      ldpc_decode_kernel<1, 0><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok, d_llr_cbs);
     }
   } else {
     if (mode == 1) {
-      ldpc_decode_kernel<2, 1><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok);
+      ldpc_decode_kernel<2, 1><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok, d_llr_cbs);
     } else {
-      ldpc_decode_kernel<2, 0><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok);
+      ldpc_decode_kernel<2, 0><<<grid, block, lds, stream>>>(d_desc, d_llrs, d_out, d_results, d_shifts, d_crc_tables, d_cb_crc_ok, d_llr_cbs);
     }
   }
 }

@@ -545,7 +545,8 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
                                                              const uint32_t* __restrict__ crc_tables,
                                                              uint8_t* __restrict__ cb_crc_ok,
                                                              const dm_desc* __restrict__ dms,
-                                                             int8_t* __restrict__ harq)
+                                                             int8_t* __restrict__ harq,
+                                                             int8_t* const* __restrict__ harq_cbs)
 {
   using G = bg_t<BG>;
   // Only the first K + MAXL columns can be touched by MAXL layers: the soft-bit image shrinks with the layer bound
@@ -596,7 +597,9 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
 
   // ---- LLRs -> soft-bit image (ldpc_decoder_impl.cpp:152), last non-zero LLR (:94); as ldpc_decoder.hip but with
   // the pair layout: a 16-byte vector inside one half of one column is a stride-2 run of bytes. ----
-  const int8_t*  llr   = llrs + d.llr_offset;
+  // The codeblock's HARQ soft buffer (the input of an unfused codeblock, the output of a fused one): at its offset in
+  // the batch buffer, or wherever harq_cbs[cb] points (a persistent rx-buffer arena slot).
+  const int8_t*  llr   = (!FUSE && harq_cbs != nullptr) ? harq_cbs[d.cb_index] : llrs + d.llr_offset;
   const int      n_llr = static_cast<int>(d.nof_llr);
   const uint32_t ncols = __umulhi(static_cast<uint32_t>(n_llr), d.div_magic);
   const uint32_t full  = ncols * static_cast<uint32_t>(Z);
@@ -608,7 +611,7 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
     const int      ninfo = static_cast<int>(dm.nsys) - Fl;
     const int      Nh    = static_cast<int>(dm.N);
     const int8_t*  in    = llrs + dm.llr_offset;
-    int8_t*        hb    = harq + dm.harq_offset;
+    int8_t*        hb    = (harq_cbs != nullptr) ? harq_cbs[d.cb_index] : harq + dm.harq_offset;
     // The whole image starts at zero (punctured columns, positions beyond the input and the unreached tail).
     {
       uint4* s16 = reinterpret_cast<uint4*>(soft);
@@ -637,7 +640,8 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
     // 4-aligned R, ninfo, fillers and HARQ buffer (every bench codeblock): a lane takes four consecutive symbols and
     // writes each bit row's four HARQ bytes as one dword (8 dword stores per 4 symbols instead of 32 byte stores).
     const bool q8 = Qm == 8 && ((dm.llr_offset & 7u) == 0u);
-    const bool q8x4 = LDPC_PK_HARQ_X4 && q8 && ((R | ninfo | Fl | static_cast<int>(dm.harq_offset)) & 3) == 0;
+    const bool q8x4 = LDPC_PK_HARQ_X4 && q8 &&
+                      ((R | ninfo | Fl | static_cast<int>(reinterpret_cast<uintptr_t>(hb))) & 3) == 0;
     if (q8x4) {
       for (int r0 = 4 * static_cast<int>(threadIdx.x); r0 < R; r0 += 4 * static_cast<int>(blockDim.x)) {
         uint2 v[4];
@@ -709,7 +713,7 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
     }
   } else {
     {
-      const uint32_t head   = static_cast<uint32_t>(d.llr_offset) & 15u;
+      const uint32_t head   = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(llr)) & 15u;
       const uint4*   vecs   = reinterpret_cast<const uint4*>(llr - head);
       const int      nvec   = static_cast<int>((head + static_cast<uint32_t>(n_llr) + 15u) >> 4);
       // 16-B vectors per lane in flight: the whole input span of the layer bound at Z = 384 with 192 lanes.
@@ -1094,17 +1098,16 @@ __device__ __forceinline__ uint32_t pair_pos4(uint32_t l, uint32_t H, uint32_t i
 /// the slot's addresses), the punctured columns and every position beyond the input zeroed. Returns this thread's
 /// index of the last non-zero LLR it saw (ldpc_decoder_impl.cpp:94), -1 if none.
 template <int NCOL>
-__device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const int8_t* __restrict__ llrs,
+__device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const int8_t* __restrict__ llr,
                                              const dec_desc& d, uint32_t slot)
 {
   const int      Z     = d.Z;
   const uint32_t H     = static_cast<uint32_t>(Z) / 2u;
-  const int8_t*  llr   = llrs + d.llr_offset;
   const int      n_llr = static_cast<int>(d.nof_llr);
   const uint32_t ncols = __umulhi(static_cast<uint32_t>(n_llr), d.div_magic);
   const uint32_t full  = ncols * static_cast<uint32_t>(Z);
   int            last  = -1;
-  const uint32_t head  = static_cast<uint32_t>(d.llr_offset) & 15u;
+  const uint32_t head  = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(llr)) & 15u;
   const uint4*   vecs  = reinterpret_cast<const uint4*>(llr - head);
   const int      nvec  = static_cast<int>((head + static_cast<uint32_t>(n_llr) + 15u) >> 4);
   constexpr int  BATCH = ((NCOL - 2) * 384 / 16 + 191) / 192;
@@ -1230,7 +1233,8 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
     int32_t* __restrict__ results,
     const uint32_t* __restrict__ ab_table,
     const uint32_t* __restrict__ crc_tables,
-    uint8_t* __restrict__ cb_crc_ok)
+    uint8_t* __restrict__ cb_crc_ok,
+    int8_t* const* __restrict__ llr_cbs)
 {
   using G = bg_t<BG>;
   static_assert(MAXL >= 4 && MAXL <= 16, "PK4: 8- and 16-layer classes (the 16-bit pair addresses and the LDS image)");
@@ -1280,7 +1284,8 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
         results[d.cb_index] = 0;
       }
     } else {
-      int last = load_llrs_pk4<NCOL>(soft, llrs, d, static_cast<uint32_t>(i));
+      int last = load_llrs_pk4<NCOL>(soft, (llr_cbs != nullptr) ? llr_cbs[d.cb_index] : llrs + d.llr_offset, d,
+                                     static_cast<uint32_t>(i));
       last     = wave_max(last);
       if (lane == 0) {
         wlast[wave] = last;
@@ -1472,7 +1477,8 @@ void launch_ldpc_decode_pk(int             bg,
                            uint8_t*        d_cb_crc_ok,
                            const dm_desc*  d_dm,
                            int8_t*         d_harq,
-                           hipStream_t     stream)
+                           hipStream_t     stream,
+                           int8_t* const*  d_harq_cbs)
 {
   if (nof_cbs <= 0) {
     return;
@@ -1481,9 +1487,9 @@ void launch_ldpc_decode_pk(int             bg,
   const bool fuse = d_dm != nullptr;
 #define SRSGPU_PK_LAUNCH1(BG_, MODE_, MAXL_, SPLIT_)                                                                   \
   (fuse ? ldpc_decode_pk_kernel<BG_, MODE_, MAXL_, SPLIT_, true><<<grid, block, 0, stream>>>(                          \
-              d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables, d_cb_crc_ok, d_dm, d_harq)                        \
+              d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables, d_cb_crc_ok, d_dm, d_harq, d_harq_cbs)            \
         : ldpc_decode_pk_kernel<BG_, MODE_, MAXL_, SPLIT_, false><<<grid, block, 0, stream>>>(                         \
-              d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables, d_cb_crc_ok, nullptr, nullptr))
+              d_desc, d_llrs, d_out, d_results, d_ab, d_crc_tables, d_cb_crc_ok, nullptr, nullptr, d_harq_cbs))
 #define SRSGPU_PK_LAUNCH(BG_, MODE_, MAXL_)                                                                            \
   (split == 2 ? SRSGPU_PK_LAUNCH1(BG_, MODE_, MAXL_, 2) : SRSGPU_PK_LAUNCH1(BG_, MODE_, MAXL_, 1))
   if (bg == 1) {
@@ -1519,7 +1525,8 @@ void launch_ldpc_decode_pk4(int             bg,
                             const uint32_t* d_ab4,
                             const uint32_t* d_crc_tables,
                             uint8_t*        d_cb_crc_ok,
-                            hipStream_t     stream)
+                            hipStream_t     stream,
+                            int8_t* const*  d_llr_cbs)
 {
   if (nof_groups <= 0) {
     return;
@@ -1527,7 +1534,7 @@ void launch_ldpc_decode_pk4(int             bg,
   dim3 grid(nof_groups), block(block_threads);
 #define SRSGPU_PK4_LAUNCH(BG_, MODE_, MAXL_)                                                                           \
   ldpc_decode_pk4_kernel<BG_, MODE_, MAXL_><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab4,       \
-                                                                        d_crc_tables, d_cb_crc_ok)
+                                                                        d_crc_tables, d_cb_crc_ok, d_llr_cbs)
   if (bg == 1) {
     if (max_layers <= 8) {
       mode == 1 ? SRSGPU_PK4_LAUNCH(1, 1, 8) : SRSGPU_PK4_LAUNCH(1, 0, 8);

@@ -19,6 +19,7 @@
 // the lanes (one 32-lane half per band edge, unwrap as a prefix sum); reductions are wave shuffles. HBM traffic per job:
 // the D DM-RS symbols' pilots of one port (read twice: the second pass, for the noise residual, hits L2) and 4 B per
 // estimated RE per layer (the dominant term).
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -502,12 +503,28 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(CHEST_WAVES_P
     float* __restrict__ metrics,
     const uint32_t* __restrict__ gseq,
     const uint16_t* __restrict__ crbs,
-    const float2* __restrict__ lp)
+    const float2* __restrict__ lp,
+    const srsgpu_copy_span* __restrict__ spans,
+    int nof_spans)
 {
   extern __shared__ __align__(16) unsigned char lds_raw[];
   __shared__ float redf[3 * (T / 64)];
   __shared__ int   redi[2 * (T / 64)];
   constexpr int JPW  = T / TS;  // jobs per workgroup
+  // Workgroups past the jobs' copy the spans (srsgpu_pusch_chest_plan_execute_copy: grid rows the estimator does not
+  // read, moved while it runs): the same number of workgroups per span, each a contiguous part of 16-byte vectors.
+  const int job_blocks = (nof_jobs + JPW - 1) / JPW;
+  if (static_cast<int>(blockIdx.x) >= job_blocks) {
+    const uint32_t cb       = blockIdx.x - static_cast<uint32_t>(job_blocks);
+    const uint32_t per_span = (gridDim.x - static_cast<uint32_t>(job_blocks)) / static_cast<uint32_t>(nof_spans);
+    const srsgpu_copy_span sp = spans[cb / per_span];
+    const uint4*           s4 = reinterpret_cast<const uint4*>(sp.src);
+    uint4*                 d4 = reinterpret_cast<uint4*>(sp.dst);
+    for (uint64_t i = (cb % per_span) * T + threadIdx.x; i < sp.bytes / 16u; i += static_cast<uint64_t>(per_span) * T) {
+      d4[i] = s4[i];
+    }
+    return;
+  }
   const int     slot = static_cast<int>(threadIdx.x) / TS;
   const int     job  = static_cast<int>(blockIdx.x) * JPW + slot;
   if (JPW > 1 && job >= nof_jobs) {
@@ -980,19 +997,31 @@ void launch_pusch_chest(const float2*   d_lp,
                         float*           d_noise_var,
                         float*           d_metrics,
                         const uint32_t*  d_seq,
-                        hipStream_t      stream)
+                        hipStream_t      stream,
+                        const srsgpu_copy_span* d_spans,
+                        int              nof_spans,
+                        uint64_t         span_bytes)
 {
   if (nof_jobs <= 0) {
     return;
   }
   const size_t lds = chest_job_lds_bytes(geom);
+  // Copy workgroups: per span, enough for one 16-byte vector per lane of the largest span (a read from mapped host
+  // memory is a PCIe round trip: the copy's rate is its requests in flight).
+  const auto copy_blocks = [&](int threads) {
+    if (nof_spans <= 0) {
+      return 0;
+    }
+    const uint64_t per_span = std::max<uint64_t>(1, (span_bytes / 16u + threads - 1) / threads);
+    return static_cast<int>(per_span * static_cast<uint64_t>(nof_spans));
+  };
   // Two jobs per wave (32 lanes each) for the usual few-RB allocations (many jobs resident together); a job with
   // hundreds of pilots (a wideband allocation: few jobs, each a long serial chain on one wave) spreads over 4 or 16
   // waves. SRSGPU_CHEST_ONE_JOB_PER_WAVE=1: one 64-lane job per wave (A/B).
   const auto launch = [&](auto kernel, int threads, int jpw) {
-    hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>((nof_jobs + jpw - 1) / jpw)),
+    hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>((nof_jobs + jpw - 1) / jpw + copy_blocks(threads))),
                        dim3(static_cast<unsigned>(threads)), static_cast<unsigned>(jpw * lds), stream, d_jobs, nof_jobs,
-                       geom, d_grids, d_ce, d_noise_var, d_metrics, d_seq, d_crbs, d_lp);
+                       geom, d_grids, d_ce, d_noise_var, d_metrics, d_seq, d_crbs, d_lp, d_spans, nof_spans);
   };
   static const bool one_job = [] {
     const char* e = std::getenv("SRSGPU_CHEST_ONE_JOB_PER_WAVE");

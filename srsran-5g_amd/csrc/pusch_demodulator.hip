@@ -332,13 +332,14 @@ __device__ __forceinline__ void stage_chunk(const demod_uniform& u, uint32_t* se
   const demod_desc& d      = *u.d;
   const uint32_t    tid    = threadIdx.x;
   const uint32_t    nwords = (d.nof_llrs + 31u) >> 5;
-  for (uint32_t j = tid; j < DEMOD_CHUNK_WORDS; j += T) {
+  // The words the chunk's REs read (o >> 5 and the next one, demod_res): at most DEMOD_CHUNK_WORDS + 1, fewer for the
+  // short chunks of a small plan.
+  const uint32_t Lq    = static_cast<uint32_t>(d.L) * d.qm;
+  const uint32_t need  = ((u.re_end * Lq + 31u) >> 5) - u.word0 + 1u;
+  const uint32_t stage = need < DEMOD_CHUNK_WORDS + 1u ? need : DEMOD_CHUNK_WORDS + 1u;
+  for (uint32_t j = tid; j < stage; j += T) {
     const uint32_t w = u.word0 + j;
     seq[j]           = (w < nwords) ? u.gseq[d.seq_word_offset + w] : 0u;
-  }
-  if (tid == 0) {
-    const uint32_t w2      = u.word0 + DEMOD_CHUNK_WORDS;
-    seq[DEMOD_CHUNK_WORDS] = (w2 < nwords) ? u.gseq[d.seq_word_offset + w2] : 0u;
   }
   if (d.qm >= 6) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(u.tables);
@@ -607,6 +608,74 @@ __device__ __forceinline__ void demod_res_qm(const demod_uniform& u, demap_pair_
   }
 }
 
+/// Statistics of OFDM symbol l from its accumulators v[4 l .. 4 l + 3] (pusch_demodulator_impl.cpp:406
+/// on_provisional_stats): SINR dB and EVM, NaN for a symbol without data.
+__device__ __forceinline__ void symbol_stats(const float* v, int l, float* __restrict__ o)
+{
+  const float nv = v[4 * l], cnt = v[4 * l + 1], e2 = v[4 * l + 2], n = v[4 * l + 3];
+  if (n == 0.f) {
+    o[2 * l] = o[2 * l + 1] = __builtin_nanf("");
+    return;
+  }
+  o[2 * l]     = (cnt > 0.f && nv > 0.f) ? -10.f * log10f(nv / cnt) : __builtin_inff();
+  o[2 * l + 1] = sqrtf(e2 / n);
+}
+
+/// Statistics of the whole transmission (pusch_demodulator_impl.cpp:432 on_end_stats) from its accumulators.
+__device__ __forceinline__ void total_stats(const float* v, float* __restrict__ o)
+{
+  float tot_nv = 0.f, tot_cnt = 0.f, tot_evm = 0.f, tot_n = 0.f;
+  for (int l = 0; l < 14; ++l) {
+    const float n = v[4 * l + 3];
+    if (n != 0.f) {
+      tot_nv += v[4 * l];
+      tot_cnt += v[4 * l + 1];
+      tot_evm += n * sqrtf(v[4 * l + 2] / n);
+      tot_n += n;
+    }
+  }
+  const float nan = __builtin_nanf("");
+  o[28] = tot_n == 0.f ? nan : ((tot_cnt > 0.f && tot_nv > 0.f) ? -10.f * log10f(tot_nv / tot_cnt) : __builtin_inff());
+  o[29] = tot_n == 0.f ? nan : tot_evm / tot_n;
+}
+
+/// Fused statistics (stats != nullptr): after its accumulator adds, the workgroup counts itself in cnt[2 tx + 1]; the
+/// last of the transmission's cnt[2 tx] workgroups (chunks and transform-precoding jobs) reads the accumulators back
+/// (device-scope atomics: the other workgroups' adds), resets them and the count, and writes the statistics - no
+/// separate statistics launch. Called by every thread of the workgroup (at least 64); sh: DEMOD_ACC_PER_TX + 1 free
+/// LDS words.
+__device__ __forceinline__ void finish_if_last(uint32_t tx, float* __restrict__ acc, float* __restrict__ stats,
+                                               uint32_t* __restrict__ cnt, float* sh)
+{
+  __threadfence();  // this thread's accumulator adds are done before the count below
+  __syncthreads();
+  uint32_t* flag = reinterpret_cast<uint32_t*>(sh + DEMOD_ACC_PER_TX);
+  if (threadIdx.x == 0) {
+    const uint32_t done = atomicAdd(&cnt[2 * tx + 1], 1u) + 1u;
+    *flag               = done == cnt[2 * tx] ? 1u : 0u;
+  }
+  __syncthreads();
+  if (*flag == 0u) {
+    return;
+  }
+  __threadfence();
+  float* a = acc + DEMOD_ACC_PER_TX * tx;
+  if (threadIdx.x < static_cast<unsigned>(DEMOD_ACC_PER_TX)) {
+    sh[threadIdx.x] = __hip_atomic_load(&a[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a[threadIdx.x], 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&cnt[2 * tx + 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  float* o = stats + DEMOD_STATS_PER_TX * tx;
+  if (threadIdx.x < 14) {
+    symbol_stats(sh, static_cast<int>(threadIdx.x), o);
+  } else if (threadIdx.x == 32) {
+    total_stats(sh, o);
+  }
+}
+
 #ifdef SRSGPU_DEMOD_WAVES  // occupancy experiments: waves per SIMD forced by the register allocator
 #define DEMOD_OCCUPANCY __attribute__((amdgpu_waves_per_eu(SRSGPU_DEMOD_WAVES, SRSGPU_DEMOD_WAVES)))
 #else
@@ -624,13 +693,15 @@ __global__ __launch_bounds__(T) DEMOD_OCCUPANCY void pusch_demodulate_kernel(con
                                                                          int8_t* __restrict__ llrs,
                                                                          const uint32_t* __restrict__ gseq,
                                                                          const uint16_t* __restrict__ crbs,
-                                                                         float* __restrict__ acc)
+                                                                         float* __restrict__ acc,
+                                                                         float* __restrict__ stats,
+                                                                         uint32_t* __restrict__ cnt)
 {
   __shared__ uint32_t         seq[DEMOD_CHUNK_WORDS + 1];
   __shared__ demap_pair_table tab[DEMAP_TABLES];
   __shared__ uint32_t         out32[DEMOD_OUT_BYTES / 4];
   __shared__ cpx              rot[14 * 16];
-  __shared__ float            lacc[DEMOD_ACC_PER_TX];
+  __shared__ float            lacc[DEMOD_ACC_PER_TX + 1];
   const mod_chunk             ch     = chunks[blockIdx.x];
   const demod_desc&           d      = descs[ch.tx];
   const uint32_t              tid    = threadIdx.x;
@@ -660,6 +731,9 @@ __global__ __launch_bounds__(T) DEMOD_OCCUPANCY void pusch_demodulate_kernel(con
   __syncthreads();
   if (STATS && tid < static_cast<uint32_t>(DEMOD_ACC_PER_TX) && lacc[tid] != 0.f) {
     atomicAdd(&acc[DEMOD_ACC_PER_TX * d.tx + tid], lacc[tid]);
+  }
+  if (STATS && stats != nullptr) {
+    finish_if_last(ch.tx, acc, stats, cnt, lacc);  // lacc (DEMOD_ACC_PER_TX + 1 words) is free again
   }
 
   // Contiguous LLR range [re_begin * Lq, re_end * Lq) of the codeword, staged from LDS byte 0. With s = dst & 3, the
@@ -836,7 +910,9 @@ __global__ __launch_bounds__(TP_THREADS) void pusch_demodulate_tp_kernel(const d
                                                                         int8_t* __restrict__ llrs,
                                                                         const uint32_t* __restrict__ gseq,
                                                                         const uint16_t* __restrict__ crbs,
-                                                                        float* __restrict__ acc)
+                                                                        float* __restrict__ acc,
+                                                                        float* __restrict__ stats,
+                                                                        uint32_t* __restrict__ cnt)
 {
   __shared__ cpx              xa[TP_MAX_M], xb[TP_MAX_M];
   __shared__ uint8_t          cls[TP_MAX_M];
@@ -933,6 +1009,9 @@ __global__ __launch_bounds__(TP_THREADS) void pusch_demodulate_tp_kernel(const d
     if (threadIdx.x < 4) {
       atomicAdd(&acc[DEMOD_ACC_PER_TX * d.tx + 4 * l + threadIdx.x], st[threadIdx.x]);
     }
+    if (stats != nullptr) {
+      finish_if_last(job.tx, acc, stats, cnt, reinterpret_cast<float*>(xb));  // the IDFT's buffers are free again
+    }
   }
 }
 
@@ -945,28 +1024,15 @@ __global__ __launch_bounds__(64) void pusch_demod_stats_kernel(float* __restrict
   if (t >= nof_tx) {
     return;
   }
-  float*      a   = acc + DEMOD_ACC_PER_TX * t;
-  float*      o   = stats + DEMOD_STATS_PER_TX * t;
-  const float nan = __builtin_nanf("");
-  const float inf = __builtin_inff();
-  float       tot_nv = 0.f, tot_cnt = 0.f, tot_evm = 0.f, tot_n = 0.f;
+  float* a = acc + DEMOD_ACC_PER_TX * t;
+  float* o = stats + DEMOD_STATS_PER_TX * t;
   for (int l = 0; l < 14; ++l) {
-    const float nv = a[4 * l], cnt = a[4 * l + 1], e2 = a[4 * l + 2], n = a[4 * l + 3];
-    a[4 * l] = a[4 * l + 1] = a[4 * l + 2] = a[4 * l + 3] = 0.f;
-    if (n == 0.f) {
-      o[2 * l] = o[2 * l + 1] = nan;
-      continue;
-    }
-    const float evm = sqrtf(e2 / n);
-    o[2 * l]        = (cnt > 0.f && nv > 0.f) ? -10.f * log10f(nv / cnt) : inf;
-    o[2 * l + 1]    = evm;
-    tot_nv += nv;
-    tot_cnt += cnt;
-    tot_evm += n * evm;
-    tot_n += n;
+    symbol_stats(a, l, o);
   }
-  o[28] = tot_n == 0.f ? nan : ((tot_cnt > 0.f && tot_nv > 0.f) ? -10.f * log10f(tot_nv / tot_cnt) : inf);
-  o[29] = tot_n == 0.f ? nan : tot_evm / tot_n;
+  total_stats(a, o);
+  for (int i = 0; i < DEMOD_ACC_PER_TX; ++i) {
+    a[i] = 0.f;
+  }
 }
 
 } // namespace
@@ -983,7 +1049,9 @@ void launch_pusch_demodulate(const demod_desc*       d_desc,
                              const uint32_t*         d_seq,
                              const uint16_t*         d_crbs,
                              float*                  d_acc,
-                             hipStream_t             stream)
+                             hipStream_t             stream,
+                             float*                  d_stats,
+                             uint32_t*               d_cnt)
 {
   if (nof_chunks <= 0) {
     return;
@@ -995,7 +1063,8 @@ void launch_pusch_demodulate(const demod_desc*       d_desc,
   const int threads = forced > 0 ? forced : plan_threads;
   const auto launch = [&](auto kernel, int t) {
     hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nof_chunks)), dim3(static_cast<unsigned>(t)), 0, stream,
-                       d_desc, d_chunks, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq, d_crbs, d_acc);
+                       d_desc, d_chunks, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq, d_crbs, d_acc,
+                       d_stats, d_cnt);
   };
   if (d_acc != nullptr) {
     launch(pusch_demodulate_kernel<true, DEMOD_THREADS>, DEMOD_THREADS);
@@ -1020,13 +1089,16 @@ void launch_pusch_demodulate_tp(const demod_desc*       d_desc,
                                 const uint32_t*         d_seq,
                                 const uint16_t*         d_crbs,
                                 float*                  d_acc,
-                                hipStream_t             stream)
+                                hipStream_t             stream,
+                                float*                  d_stats,
+                                uint32_t*               d_cnt)
 {
   if (nof_jobs <= 0) {
     return;
   }
   hipLaunchKernelGGL(pusch_demodulate_tp_kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(TP_THREADS), 0, stream,
-                     d_desc, d_jobs, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq, d_crbs, d_acc);
+                     d_desc, d_jobs, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq, d_crbs, d_acc, d_stats,
+                     d_cnt);
 }
 
 void launch_pusch_demod_stats(float* d_acc, float* d_stats, int nof_tx, hipStream_t stream)

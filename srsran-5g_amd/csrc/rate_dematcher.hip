@@ -87,10 +87,9 @@ __device__ __forceinline__ int dematch_position(const dm_desc& d, const int8_t* 
 /// Any transmission, position by position (dword read-modify-write where aligned).
 template <int MODE>
 __device__ __forceinline__ void dematch_general(const dm_desc& d, const int8_t* __restrict__ llrs,
-                                                int8_t* __restrict__ harq)
+                                                int8_t* __restrict__ buf)
 {
   const int8_t* in  = llrs + d.llr_offset;
-  int8_t*       buf = harq + d.harq_offset;
   const int     E = static_cast<int>(d.E);
   const int     N = static_cast<int>(d.N), Ncb = static_cast<int>(d.Ncb);
   const int     nsys = static_cast<int>(d.nsys), F = d.nof_filler, ninfo = nsys - F;
@@ -108,7 +107,7 @@ __device__ __forceinline__ void dematch_general(const dm_desc& d, const int8_t* 
       zero_from = N - (Ncb - kend);
     }
   }
-  if (((d.harq_offset | static_cast<uint32_t>(N)) & 3u) == 0u) {
+  if (((static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf)) | static_cast<uint32_t>(N)) & 3u) == 0u) {
     // Dword read-modify-write of four consecutive positions per lane.
     auto* buf32 = reinterpret_cast<uint32_t*>(buf);
     for (int k4 = threadIdx.x; k4 < N / 4; k4 += blockDim.x) {
@@ -136,10 +135,9 @@ __device__ __forceinline__ void dematch_general(const dm_desc& d, const int8_t* 
 /// copy positions. The two phases write disjoint bytes.
 template <int MODE>
 __device__ __forceinline__ void dematch_new_data(const dm_desc& d, const int8_t* __restrict__ llrs,
-                                                 int8_t* __restrict__ harq)
+                                                 int8_t* __restrict__ buf)
 {
   const int8_t* in  = llrs + d.llr_offset;
-  int8_t*       buf = harq + d.harq_offset;
   const int     E = static_cast<int>(d.E), Qm = d.Qm, R = E / Qm;
   const int     N = static_cast<int>(d.N), Ncb = static_cast<int>(d.Ncb);
   const int     nsys = static_cast<int>(d.nsys), F = d.nof_filler, ninfo = nsys - F;
@@ -199,7 +197,7 @@ __device__ __forceinline__ void dematch_new_data(const dm_desc& d, const int8_t*
         !(k0 < ninfo && k0 + 15 >= ninfo)) {
       continue;
     }
-    if (k0 >= zero_from && k0 + 15 < N && ((d.harq_offset + static_cast<uint32_t>(k0)) & 15u) == 0u) {
+    if (k0 >= zero_from && k0 + 15 < N && ((reinterpret_cast<uintptr_t>(buf) + static_cast<uint32_t>(k0)) & 15u) == 0u) {
       *reinterpret_cast<uint4*>(buf + k0) = make_uint4(0u, 0u, 0u, 0u);  // limited-buffer / walk-end zero tail
       continue;
     }
@@ -218,18 +216,22 @@ template <int MODE>
 __global__ __launch_bounds__(256) void rate_dematch_kernel(const dm_desc* __restrict__ descs,
                                                            const int8_t* __restrict__ llrs,
                                                            int8_t* __restrict__ harq,
+                                                           int8_t* const* __restrict__ harq_cbs,
                                                            uint8_t* __restrict__ cb_crc_ok)
 {
   const dm_desc d = descs[blockIdx.x];
+  // The codeblock's soft buffer: at its offset in the batch HARQ buffer, or wherever harq_cbs[cb] points (a slot of a
+  // persistent rx-buffer arena, srsgpu_pusch_decoder_plan_execute_arena).
+  int8_t* const buf = (harq_cbs != nullptr) ? harq_cbs[d.cb_index] : harq + d.harq_offset;
   // New data invalidates the codeblock CRC flags of the HARQ context (pusch_decoder_impl.cpp:132).
   if (d.new_data && cb_crc_ok != nullptr && threadIdx.x == 0) {
     cb_crc_ok[d.cb_index] = 0;
   }
   const int V = static_cast<int>(d.Ncb) - d.nof_filler;
   if (d.new_data && static_cast<int>(d.E) <= V && d.Qm <= 8) {
-    dematch_new_data<MODE>(d, llrs, harq);
+    dematch_new_data<MODE>(d, llrs, buf);
   } else {
-    dematch_general<MODE>(d, llrs, harq);
+    dematch_general<MODE>(d, llrs, buf);
   }
 }
 
@@ -241,15 +243,16 @@ void launch_rate_dematch(int           mode,
                          const int8_t* d_llrs,
                          int8_t*       d_harq,
                          uint8_t*      d_cb_crc_ok,
-                         hipStream_t   stream)
+                         hipStream_t   stream,
+                         int8_t* const* d_harq_cbs)
 {
   if (nof_cbs <= 0) {
     return;
   }
   if (mode == 1) {
-    rate_dematch_kernel<1><<<nof_cbs, 256, 0, stream>>>(d_desc, d_llrs, d_harq, d_cb_crc_ok);
+    rate_dematch_kernel<1><<<nof_cbs, 256, 0, stream>>>(d_desc, d_llrs, d_harq, d_harq_cbs, d_cb_crc_ok);
   } else {
-    rate_dematch_kernel<0><<<nof_cbs, 256, 0, stream>>>(d_desc, d_llrs, d_harq, d_cb_crc_ok);
+    rate_dematch_kernel<0><<<nof_cbs, 256, 0, stream>>>(d_desc, d_llrs, d_harq, d_harq_cbs, d_cb_crc_ok);
   }
 }
 

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "srsgpu_phy.h"  // srsgpu_copy_span
+
 namespace srsgpu {
 
 /// Number of bytes between consecutive lifted-node columns of the soft-bit image in LDS. A fixed stride (the maximum
@@ -160,13 +162,15 @@ void launch_pdsch_encode_packed(int              bg,
                                 hipStream_t      s);
 
 /// Launches the batched rate dematcher (rate_dematcher.hip). mode 0: generic combining, 1: SIMD combining.
-void launch_rate_dematch(int           mode,
+/// d_harq_cbs (optional): codeblock i's soft buffer is d_harq_cbs[dm_desc::cb_index] instead of d_harq + harq_offset.
+void launch_rate_dematch(int            mode,
                          const dm_desc* d_desc,
-                         int           nof_cbs,
-                         const int8_t* d_llrs,
-                         int8_t*       d_harq,
-                         uint8_t*      d_cb_crc_ok,
-                         hipStream_t   stream);
+                         int            nof_cbs,
+                         const int8_t*  d_llrs,
+                         int8_t*        d_harq,
+                         uint8_t*       d_cb_crc_ok,
+                         hipStream_t    stream,
+                         int8_t* const* d_harq_cbs = nullptr);
 
 /// TB stage of the PUSCH decoder (pusch_tb.hip): codeblock concatenation and TB CRC check.
 struct tb_dec_desc {
@@ -251,7 +255,8 @@ void launch_ldpc_decode_pk(int             bg,
                            uint8_t*        d_cb_crc_ok,
                            const dm_desc*  d_dm,
                            int8_t*         d_harq,
-                           hipStream_t     stream);
+                           hipStream_t     stream,
+                           int8_t* const*  d_harq_cbs = nullptr);
 
 /// Codeblocks per workgroup of the multi-codeblock packed decoder (ldpc_decode_pk4_kernel).
 constexpr int LDPC_PK4 = 4;
@@ -271,9 +276,12 @@ void launch_ldpc_decode_pk4(int             bg,
                             const uint32_t* d_ab4,
                             const uint32_t* d_crc_tables,
                             uint8_t*        d_cb_crc_ok,
-                            hipStream_t     stream);
+                            hipStream_t     stream,
+                            int8_t* const*  d_llr_cbs = nullptr);
 
-/// Launches the batched LDPC decoder (ldpc_decoder.hip).
+/// Launches the batched LDPC decoder (ldpc_decoder.hip). d_llr_cbs (optional): codeblock c's input is
+/// d_llr_cbs[dec_desc::cb_index] instead of d_llrs + llr_offset (the same for the packed launchers: per-codeblock HARQ
+/// soft buffers in a persistent arena).
 void launch_ldpc_decode(int                bg,
                         int                mode,
                         const dec_desc*    d_desc,
@@ -285,7 +293,8 @@ void launch_ldpc_decode(int                bg,
                         const uint32_t*    d_shifts,
                         const uint32_t*    d_crc_tables,
                         uint8_t*           d_cb_crc_ok,
-                        hipStream_t        stream);
+                        hipStream_t        stream,
+                        int8_t* const*     d_llr_cbs = nullptr);
 
 /// PDSCH modulator (pdsch_modulator.hip): per-transmission descriptor.
 struct mod_desc {
@@ -571,7 +580,10 @@ void launch_pusch_chest(const float2*   d_lp,
                         float*           d_noise_var,
                         float*           d_metrics,
                         const uint32_t*  d_seq,
-                        hipStream_t      stream);
+                        hipStream_t      stream,
+                        const srsgpu_copy_span* d_spans    = nullptr,
+                        int              nof_spans  = 0,
+                        uint64_t         span_bytes = 0);  ///< the largest span
 
 /// UL-SCH demultiplexer (ulsch_demux.hip): per-transmission descriptor and per-RE routing.
 struct ulsch_demux_desc {
@@ -617,7 +629,9 @@ void launch_pusch_demodulate_tp(const demod_desc*       d_desc,
                                 const uint32_t*          d_seq,
                                 const uint16_t*          d_crbs,
                                 float*                   d_acc,
-                                hipStream_t              stream);
+                                hipStream_t              stream,
+                                float*                   d_stats = nullptr,
+                                uint32_t*                d_cnt   = nullptr);
 void launch_pusch_demod_stats(float* d_acc, float* d_stats, int nof_tx, hipStream_t stream);
 void launch_pusch_demodulate(const demod_desc*        d_desc,
                              const mod_chunk*         d_chunks,
@@ -631,6 +645,8 @@ void launch_pusch_demodulate(const demod_desc*        d_desc,
                              const uint32_t*          d_seq,
                              const uint16_t*          d_crbs,
                              float*                   d_acc,
-                             hipStream_t              stream);
+                             hipStream_t              stream,
+                             float*                   d_stats = nullptr,
+                             uint32_t*                d_cnt   = nullptr);
 
 } // namespace srsgpu

@@ -343,6 +343,7 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pusch_decoder_plan_nof_codeblocks.argtypes = [P]
     lib.srsgpu_pusch_decoder_plan_nof_codeblocks.restype = ctypes.c_uint32
     lib.srsgpu_pusch_decoder_plan_execute.argtypes = [P, P, P, P, P, P, P, P, P]
+    lib.srsgpu_pusch_decoder_plan_execute_arena.argtypes = [P, P, P, P, P, P, P, P, P]
     lib.srsgpu_pusch_decoder_plan_assemble.argtypes = [P, P, P, P, P, P]
     lib.srsgpu_pusch_decoder_plan_destroy.argtypes = [P]
     lib.srsgpu_pusch_decoder_plan_destroy.restype = None
@@ -376,6 +377,7 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_pusch_chest_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                    ctypes.POINTER(P)]
     lib.srsgpu_pusch_chest_plan_execute.argtypes = [P, P, P, P, P, P]
+    lib.srsgpu_pusch_chest_plan_execute_copy.argtypes = [P, P, P, P, P, P, ctypes.c_uint32, ctypes.c_uint64, P]
     lib.srsgpu_pusch_chest_plan_destroy.argtypes = [P]
     lib.srsgpu_pusch_chest_plan_destroy.restype = None
     lib.srsgpu_pusch_demodulator_plan_create.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -418,7 +420,8 @@ EXPORTED_SYMBOLS = [
     "srsgpu_pusch_cb_plan_destroy", "srsgpu_pdsch_encoder_plan_create", "srsgpu_pdsch_encoder_plan_nof_codeblocks",
     "srsgpu_pdsch_encoder_plan_execute", "srsgpu_pdsch_encoder_plan_destroy", "srsgpu_pusch_decoder_plan_create",
     "srsgpu_pusch_decoder_plan_nof_codeblocks", "srsgpu_pusch_decoder_plan_decoder_input_llrs",
-    "srsgpu_pusch_decoder_plan_execute", "srsgpu_pusch_decoder_plan_assemble",
+    "srsgpu_pusch_decoder_plan_execute", "srsgpu_pusch_decoder_plan_execute_arena",
+    "srsgpu_pusch_decoder_plan_assemble",
     "srsgpu_pusch_decoder_plan_destroy", "srsgpu_pusch_decoder_plan_enable_timing",
     "srsgpu_pusch_decoder_plan_stage_times", "srsgpu_pdsch_encoder_plan_enable_timing",
     "srsgpu_pdsch_encoder_plan_stage_times", "srsgpu_pdsch_modulator_plan_create",
@@ -435,6 +438,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ulsch_demux_plan_symbol_llrs", "srsgpu_harq_copy_arenas",
     "srsgpu_ulsch_demux_plan_execute", "srsgpu_ulsch_demux_plan_destroy",
     "srsgpu_pusch_chest_plan_create", "srsgpu_pusch_chest_plan_execute", "srsgpu_pusch_chest_plan_destroy",
+    "srsgpu_pusch_chest_plan_execute_copy",
     "srsgpu_pdsch_dmrs_plan_create", "srsgpu_pdsch_dmrs_plan_create_ex", "srsgpu_pdsch_dmrs_plan_execute", "srsgpu_pdsch_dmrs_plan_destroy",
 ]
 
@@ -459,17 +463,23 @@ def _stream_handle(stream) -> Optional[int]:
     return int(stream)
 
 
-def copy_spans(spans, stream=None):
-    """srsgpu_copy_spans: spans = [(src tensor, dst tensor)], each a contiguous device tensor of the same byte size (a
-    multiple of 16). One launch copies them all."""
+def span_list(spans):
+    """The srsgpu_copy_span array of spans = [(src tensor, dst tensor)] (contiguous device tensors of the same byte
+    size, a multiple of 16) on the device, and its byte counts."""
     arr = np.zeros(len(spans), np.dtype([("src", "<u8"), ("dst", "<u8"), ("bytes", "<u8")]))
     for i, (a, b) in enumerate(spans):
         n = a.numel() * a.element_size()
         if n != b.numel() * b.element_size():
             raise SrsGpuError("copy_spans: source and destination sizes differ")
         arr[i] = (_dptr(a), _dptr(b), n)
-    d = torch.from_numpy(arr.view(np.uint8).copy()).to(spans[0][0].device)
-    _check(_lib.srsgpu_copy_spans(_dptr(d), len(spans), int(arr["bytes"].max()), _stream_handle(stream)))
+    return torch.from_numpy(arr.view(np.uint8).copy()).to(spans[0][0].device), arr["bytes"]
+
+
+def copy_spans(spans, stream=None):
+    """srsgpu_copy_spans: spans = [(src tensor, dst tensor)], each a contiguous device tensor of the same byte size (a
+    multiple of 16). One launch copies them all."""
+    d, nbytes = span_list(spans)
+    _check(_lib.srsgpu_copy_spans(_dptr(d), len(spans), int(nbytes.max()), _stream_handle(stream)))
     return d  # keep alive until the stream has run the copies
 
 
@@ -1269,6 +1279,15 @@ class PuschChannelEstimatorPlan:
         _check(_lib.srsgpu_pusch_chest_plan_execute(self.handle, _dptr(d_grids), _dptr(d_ch_est), _dptr(d_noise_var),
                                                     _dptr(d_metrics), _stream_handle(stream)))
 
+    def execute_copy(self, d_grids, d_ch_est, d_noise_var, spans, d_metrics=None, stream=None):
+        """execute, with the copies spans = [(src, dst)] done by extra workgroups of the same launch. Returns the
+        device span list (keep it alive until the stream has run the launch)."""
+        d, nbytes = span_list(spans)
+        _check(_lib.srsgpu_pusch_chest_plan_execute_copy(self.handle, _dptr(d_grids), _dptr(d_ch_est),
+                                                         _dptr(d_noise_var), _dptr(d_metrics), _dptr(d), len(spans),
+                                                         int(nbytes.max()), _stream_handle(stream)))
+        return d
+
     def close(self):
         if getattr(self, "handle", None):
             _lib.srsgpu_pusch_chest_plan_destroy(self.handle)
@@ -1599,6 +1618,13 @@ class PuschDecoderPlan:
         _check(_lib.srsgpu_pusch_decoder_plan_execute(self.handle, _dptr(d_llrs), _dptr(d_harq), _dptr(d_cb_crc_ok),
                                                       _dptr(d_cb_msgs), _dptr(d_cb_iters), _dptr(d_tbs),
                                                       _dptr(d_tb_crc_ok), _stream_handle(stream)))
+
+    def execute_arena(self, d_llrs, d_harq_cbs, d_cb_crc_ok, d_cb_msgs, d_cb_iters, d_tbs, d_tb_crc_ok, stream=None):
+        """As execute, with codeblock c's HARQ soft buffer at the device address d_harq_cbs[c] (an int64 tensor of one
+        pointer per codeblock, e.g. slots of a persistent arena) instead of in a contiguous batch buffer."""
+        _check(_lib.srsgpu_pusch_decoder_plan_execute_arena(self.handle, _dptr(d_llrs), _dptr(d_harq_cbs),
+                                                            _dptr(d_cb_crc_ok), _dptr(d_cb_msgs), _dptr(d_cb_iters),
+                                                            _dptr(d_tbs), _dptr(d_tb_crc_ok), _stream_handle(stream)))
 
     def assemble(self, d_cb_crc_ok, d_cb_msgs, d_tbs, d_tb_crc_ok, stream=None):
         """TB stage only, from codeblock messages / flags decoded elsewhere (codeblock-sharded decoding)."""

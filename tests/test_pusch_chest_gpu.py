@@ -519,3 +519,51 @@ def test_pusch_transform_precoding_receive_chain(ctx):
     sent = np.concatenate([data[l] for l in sorted(data)])
     hard = D.modulate_bits((llr <= 0).astype(np.uint8), qm)
     assert np.mean(np.abs(hard - sent.astype(np.complex64)) > 1e-3) < 1e-3
+
+
+def test_pusch_chest_execute_copy(ctx):
+    """srsgpu_pusch_chest_plan_execute_copy (the slot batch's split grid copy): the wideband 273-PRB jobs estimated
+    from grids holding only their DM-RS symbol rows while the same launch copies every other row in equal the plain
+    execute over the complete grids bit for bit (estimates, noise variances, metrics), and the copied rows arrive."""
+    import torch
+    import srsgpu
+    dev = torch.device("cuda", 0)
+    cases = list(G.pusch_chest_273_cases())
+    grids = np.ascontiguousarray(np.stack([c[1] for c in cases]), np.uint16)
+    ests = [to_est(cfg, 2, 1, 0, 1) for cfg, _, _, _ in cases]
+    S, Pg, L, nsc = grids.shape[:4]
+    exts, _keep = srsgpu.make_crb_mask_exts(ests, 273)
+    plan = srsgpu.PuschChannelEstimatorPlan(ctx, srsgpu.make_pusch_chest_configs(ests, list(range(S))), 273, Pg, exts)
+    full = torch.from_numpy(grids.view(np.int32).reshape(-1).copy()).to(dev)
+    part = torch.zeros_like(full)
+    rows = full.view(S, Pg, L, nsc)
+    prow = part.view(S, Pg, L, nsc)
+    dmrs = {l for cfg, _, _, _ in cases for l in range(14) if (cfg["dmrs_symbol_mask"] >> l) & 1}
+    g = torch.Generator().manual_seed(3)
+    for l in range(L):
+        if l not in dmrs:  # data rows (the golden grids hold only the DM-RS rows): something to copy
+            rows[:, :, l] = torch.randint(-2**31, 2**31 - 1, (S, Pg, nsc), dtype=torch.int32, generator=g).to(dev)
+    spans = []
+    for s in range(S):
+        for p in range(Pg):
+            for l in range(L):
+                if l in dmrs:
+                    prow[s, p, l].copy_(rows[s, p, l])
+                else:
+                    spans.append((rows[s, p, l], prow[s, p, l]))
+    outs = []
+    for k in range(2):
+        ce = torch.zeros(S * 4 * Pg * L * nsc, dtype=torch.int32, device=dev)
+        nv = torch.zeros(4 * S, dtype=torch.float32, device=dev)
+        m = torch.zeros(4 * srsgpu.CHEST_METRICS * S, dtype=torch.float32, device=dev)
+        if k == 0:
+            plan.execute(full, ce, nv, m)
+        else:
+            keep = plan.execute_copy(part, ce, nv, spans, m)
+        outs.append((ce, nv, m))
+    torch.cuda.synchronize(dev)
+    del keep
+    plan.close()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    assert torch.equal(full, part)

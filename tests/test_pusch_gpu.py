@@ -412,3 +412,75 @@ def test_copy_spans():
         off += x.numel() + 64
     with pytest.raises(srsgpu.SrsGpuError):
         srsgpu.copy_spans([(srcs[0][:8], dsts[0][:8])])
+
+
+def test_pusch_decoder_harq_in_arena(orc, ctx):
+    """srsgpu_pusch_decoder_plan_execute_arena (each codeblock's HARQ soft buffer in a slot of a scattered, garbage-
+    initialised arena, addressed through a per-codeblock pointer table) equals srsgpu_pusch_decoder_plan_execute over a
+    contiguous batch HARQ buffer bit for bit, for a new transmission (fused and separate rate dematching, odd and even
+    lifting sizes) and an rv2 retransmission that combines with the soft bits left in the arena: codeblock CRC flags,
+    messages and iteration counts, TBs, TB CRC flags and every HARQ soft bit."""
+    import torch
+    import srsgpu
+    from srsgpu import sch
+    rng = np.random.default_rng(11)
+    dev = torch.device("cuda", 0)
+    tables = list(sch.MCS_TABLE_256QAM.values())
+    grants, tbs = [], []
+    while len(grants) < 40:
+        qm, r = tables[int(rng.integers(0, len(tables)))]
+        g = sch.UeGrant(int(rng.integers(1, 40)), int(rng.integers(1, 5)), qm, r, nof_symb_sh=int(rng.integers(6, 15)))
+        seg = g.segmentation()
+        grants.append((g, seg))
+        tbs.append(rng.integers(0, 256, seg.tbs // 8).astype(np.uint8))
+    nof_cbs = [seg.nof_segments for _, seg in grants]
+    cb_len = [BG_N_SHORT[seg.base_graph] * seg.lifting_size for _, seg in grants]
+    slot_bytes = 66 * 384
+    ncb = sum(nof_cbs)
+    arena = torch.from_numpy(rng.integers(-128, 128, 2 * ncb * slot_bytes).astype(np.int8)).to(dev)
+    perm = rng.permutation(2 * ncb)[:ncb]
+    ptrs = torch.tensor([arena.data_ptr() + int(p) * slot_bytes for p in perm], dtype=torch.int64, device=dev)
+    state = None
+    for rv, new_data in ((0, True), (2, False)):
+        llrs, cfgs = [], []
+        for i, ((g, seg), tb) in enumerate(zip(grants, tbs)):
+            cw, _, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, rv, g.qm, g.nof_layers, 0, g.nof_ch_symbols)
+            llrs.append(bits_to_llrs(rng, cw, amp=6.0, noise=[2.0, 6.0, 9.0, 12.0][i % 4]))
+            cfgs.append(srsgpu.PuschTransportBlock(seg.tbs // 8, seg.base_graph, rv, g.qm, g.nof_layers,
+                                                   g.nof_ch_symbols, new_data=new_data, nof_ldpc_iterations=6))
+        arr, nllr, nharq, ncb2, ntb = srsgpu.make_pusch_tb_configs(cfgs, nof_cbs, cb_len)
+        assert ncb2 == ncb
+        if state is None:
+            state = [dict(harq=torch.zeros(nharq, dtype=torch.int8, device=dev)) for _ in range(2)]
+            for st in state:
+                st["crc"] = torch.zeros(ncb, dtype=torch.uint8, device=dev)
+                st["msgs"] = torch.zeros(ncb * srsgpu.CB_MSG_STRIDE, dtype=torch.uint8, device=dev)
+        d_llrs = torch.from_numpy(np.concatenate(llrs).astype(np.int8)).to(dev)
+        assert d_llrs.numel() == nllr
+        plan = srsgpu.PuschDecoderPlan(ctx, srsgpu.IMPL_BY_NAME["avx2"], arr)
+        outs = []
+        for k, st in enumerate(state):
+            it = torch.zeros(ncb, dtype=torch.int32, device=dev)
+            tb_out = torch.zeros(max(ntb, 1), dtype=torch.uint8, device=dev)
+            tb_ok = torch.zeros(len(cfgs), dtype=torch.uint8, device=dev)
+            if k == 0:
+                plan.execute(d_llrs, st["harq"], st["crc"], st["msgs"], it, tb_out, tb_ok)
+            else:
+                plan.execute_arena(d_llrs, ptrs, st["crc"], st["msgs"], it, tb_out, tb_ok)
+            outs.append((it, tb_out, tb_ok))
+        torch.cuda.synchronize(dev)
+        plan.close()
+        for a, b in zip(outs[0], outs[1]):
+            assert torch.equal(a, b), rv
+        assert torch.equal(state[0]["crc"], state[1]["crc"]), rv
+        assert torch.equal(state[0]["msgs"], state[1]["msgs"]), rv
+        harq = state[0]["harq"].cpu().numpy()
+        arena_h = arena.cpu().numpy()
+        c = 0
+        for t in range(len(cfgs)):
+            for i in range(nof_cbs[t]):
+                off = int(arr[t].harq_offset) + i * cb_len[t]
+                slot = int(perm[c]) * slot_bytes
+                assert np.array_equal(harq[off: off + cb_len[t]], arena_h[slot: slot + cb_len[t]]), (rv, t, i)
+                c += 1
+        assert int(outs[0][2].sum()) >= 8

@@ -17,6 +17,7 @@
 #   dulow            tools/du_low_bench.py: lower PHY + PUSCH service per sector, paced, 1..8 sectors
 #   lds              PMC pass of the bench: LDS issue stalls, bank conflicts, LDS-array cycles per kernel
 #   ab:DIR[:N]       A/B of the default bench: the in-tree library against srsran-5g_amd/DIR's, N rounds
+#   slotsab:V=X[:N]  A/B of the UL slot processors (16 threads): default environment against V=X, N rounds
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -87,6 +88,21 @@ for step in "$@"; do
       python3 tools/pmc_summary.py "$CSV" > "$OUT/pmc_lds.txt"
       rm -rf "$OUT/pmc_lds"
       cat "$OUT/pmc_lds.txt" | cut -c1-400 ;;
+    slotsab:*)
+      # slotsab:VAR=V[,VAR2=V2][:N] — the UL slot processors at 16 threads (processor_bench.py --only-slots), N rounds
+      # (default 2) alternating the default environment and the given variables
+      SPEC=${step#slotsab:}; KV=${SPEC%%:*}; N=2; [[ "$SPEC" == *:* ]] && N=${SPEC##*:}
+      IFS=, read -r -a VARS <<< "$KV"
+      for i in $(seq 1 "$N"); do
+        for v in default alt; do
+          if [ "$v" = default ]; then E=(); else E=("${VARS[@]}"); fi
+          env "${E[@]}" timeout -k 10 300 python -u tools/processor_bench.py --only-slots --threads 16 --slots 100 \
+            --repetitions 3 --directions ul > "$OUT/slotsab_${v}_$i.json" 2> "$OUT/slotsab_${v}_$i.log" \
+            || { tail -20 "$OUT/slotsab_${v}_$i.log"; exit 1; }
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], [(p['profile'][:12], [round(r['slots_per_s']) for r in p['runs']]) for p in d['slot_processors']['ul']])" \
+            "$OUT/slotsab_${v}_$i.json" "$v ${E[*]}"
+        done
+      done ;;
     ab:*)
       # ab:DIR[:N] — the default bench N times (default 2), alternating the in-tree library and srsran-5g_amd/DIR's
       SPEC=${step#ab:}; DIR=${SPEC%%:*}; N=2; [[ "$SPEC" == *:* ]] && N=${SPEC##*:}

@@ -110,7 +110,8 @@ struct srsgpu_ldpc_decoder_plan {
     bool      packed  = false;
     int       max_layers = 0;
     int       split   = 1;   ///< 2: edge-split kernel (each row's edges over two wave halves), see upload_decoder_plan
-    int       pack    = 1;   ///< LDPC_PK4: multi-codeblock workgroups (count = workgroups), see pk4_layout_for
+    int       pack    = 1;   ///< LDPC_PK4 / 2: multi-codeblock workgroups (count = workgroups), see pk4_layout_for /
+                             ///< pair_layout_for
     int       threads = 64;
     int       count   = 0;
     dec_desc* d_desc  = nullptr;
@@ -371,7 +372,8 @@ int srsgpu_context_create(int device, srsgpu_context** out)
     // Packed decoder: rows z and z + H of a lane read the pair at min(2z + A, 2z + B) (row z) and its partner byte.
     // PK4 (multi-codeblock workgroups, ldpc_decoder_pk.hip): pairs are 2 LDPC_PK4 bytes apart in the interleaved
     // image, the lane constant is 2 LDPC_PK4 z + 2 slot: A = 2 PK4 s' + hi, B = 2 PK4 (s' - H) + 1 - hi.
-    std::vector<uint32_t> ab(static_cast<size_t>(51) * ne, 0u), ab4(static_cast<size_t>(51) * ne, 0u);
+    std::vector<uint32_t> ab(static_cast<size_t>(51) * ne, 0u), ab4(static_cast<size_t>(51) * ne, 0u),
+        ab2(static_cast<size_t>(51) * ne, 0u);
     for (int p = 0; p < 51; ++p) {
       const int Z = kLiftingSizes[p];
       if (Z % 2 != 0) {
@@ -390,6 +392,10 @@ int srsgpu_context_create(int device, srsgpu_context** out)
         const int B4 = 2 * LDPC_PK4 * (sm - H) + 1 - hi;
         ab4[static_cast<size_t>(p) * ne + e] =
             static_cast<uint32_t>(A4) | (static_cast<uint32_t>(B4 & 0xffff) << 16);
+        const int A2 = 4 * sm + hi;  // two-codeblock workgroups (PKN = 2)
+        const int B2 = 4 * (sm - H) + 1 - hi;
+        ab2[static_cast<size_t>(p) * ne + e] =
+            static_cast<uint32_t>(A2) | (static_cast<uint32_t>(B2 & 0xffff) << 16);
       }
     }
     if (hipMalloc(&ctx->d_pair_ab[bg - 1], ab.size() * sizeof(uint32_t)) != hipSuccess ||
@@ -397,6 +403,9 @@ int srsgpu_context_create(int device, srsgpu_context** out)
             hipSuccess ||
         hipMalloc(&ctx->d_pair_ab4[bg - 1], ab4.size() * sizeof(uint32_t)) != hipSuccess ||
         hipMemcpy(ctx->d_pair_ab4[bg - 1], ab4.data(), ab4.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        hipMalloc(&ctx->d_pair_ab2[bg - 1], ab2.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipMemcpy(ctx->d_pair_ab2[bg - 1], ab2.data(), ab2.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
             hipSuccess) {
       srsgpu_context_destroy(ctx);
       return fail(SRSGPU_ERR_HIP, "failed to upload LDPC pair address tables");
@@ -489,6 +498,11 @@ void srsgpu_context_destroy(srsgpu_context* ctx)
     }
   }
   for (auto* p : ctx->d_pair_ab4) {
+    if (p != nullptr) {
+      (void)hipFree(p);
+    }
+  }
+  for (auto* p : ctx->d_pair_ab2) {
     if (p != nullptr) {
       (void)hipFree(p);
     }
@@ -733,19 +747,104 @@ bool pk4_layout_for(int bg, int max_layers, const std::vector<dec_desc>& cbs, pk
   return true;
 }
 
+/// Two-codeblock workgroups (ldpc_decode_pk4_kernel with PKN = 2): a codeblock of H = Z / 2 in (64, 96] (Z = 144 ..
+/// 192) spans two waves of which the second is partly idle, while two of them fill three waves (Z = 192: 25 % fewer
+/// wave-instructions). Moves such codeblocks of `cbs` (and their dm_desc, when fused) into `pairs` / `pair_dms`, two
+/// slots per workgroup (codeblocks sharing Z, scaling, iteration limit and CRC mode; an odd one out leaves its second
+/// slot empty), keeping the others. Opt-in (SRSGPU_DECODER_PK2=1): measured at Z = 192 (8-layer span,
+/// tools/decoder_scaling.py, profiles/r5_decoder_pk2_scaling.txt) 2-7 % faster with all 6 iterations (8 192 codeblocks:
+/// 676 -> 631 us), equal with early stop at 2 iterations, 8 % slower at 1 024 codeblocks: far from the 25 % fewer
+/// waves (the wave shared by both codeblocks runs until the later one stops; 8-byte pair interleave).
+void pair_layout_for(std::vector<dec_desc>& cbs, std::vector<dm_desc>& dms, bool fused, std::vector<dec_desc>& pairs,
+                     std::vector<dm_desc>& pair_dms)
+{
+  const char* env = std::getenv("SRSGPU_DECODER_PK2");
+  if (env == nullptr || env[0] != '1') {
+    return;
+  }
+  std::vector<size_t> idx, rest;
+  for (size_t i = 0; i < cbs.size(); ++i) {
+    const int H = cbs[i].Z / 2;
+    ((H > 64 && H <= 96) ? idx : rest).push_back(i);
+  }
+  if (idx.empty()) {
+    return;
+  }
+  auto key = [&](size_t i) {
+    const dec_desc& d = cbs[i];
+    return std::make_tuple(d.Z, d.sf16, d.max_iter, static_cast<uint32_t>(d.flags), d.crc_table == NO_CRC_TABLE);
+  };
+  std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return key(a) < key(b); });
+  for (size_t k = 0; k < idx.size();) {
+    const bool two = k + 1 < idx.size() && key(idx[k + 1]) == key(idx[k]) && cbs[idx[k + 1]].sf == cbs[idx[k]].sf;
+    pairs.push_back(cbs[idx[k]]);
+    pairs.push_back(two ? cbs[idx[k + 1]] : dec_desc{});
+    if (fused) {
+      pair_dms.push_back(dms[idx[k]]);
+      pair_dms.push_back(two ? dms[idx[k + 1]] : dm_desc{});
+    }
+    k += two ? 2 : 1;
+  }
+  std::vector<dec_desc> keep;
+  std::vector<dm_desc>  keep_dms;
+  for (size_t i : rest) {
+    keep.push_back(cbs[i]);
+    if (fused) {
+      keep_dms.push_back(dms[i]);
+    }
+  }
+  cbs.swap(keep);
+  dms.swap(keep_dms);
+}
+
 int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, srsgpu_ldpc_decoder_plan** plan_out)
 {
   auto* plan = new srsgpu_ldpc_decoder_plan();
   plan->ctx  = ctx;
   plan->impl = impl;
+  auto upload = [&](void** dst, const void* src, size_t bytes) {
+    return hipMalloc(dst, bytes) == hipSuccess && hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
   for (const auto& kv : batch.groups) {
+    const bool            fused = std::get<3>(kv.first);
+    std::vector<dec_desc> cbs   = kv.second;
+    std::vector<dm_desc>  dms   = fused ? batch.fused.at(kv.first) : std::vector<dm_desc>{};
+    if (std::get<1>(kv.first) && std::get<2>(kv.first) <= 16) {
+      std::vector<dec_desc> pairs;
+      std::vector<dm_desc>  pair_dms;
+      pair_layout_for(cbs, dms, fused, pairs, pair_dms);
+      if (!pairs.empty()) {
+        srsgpu_ldpc_decoder_plan::group gp;
+        gp.bg         = std::get<0>(kv.first);
+        gp.packed     = true;
+        gp.max_layers = std::get<2>(kv.first);
+        gp.pack       = 2;
+        gp.threads    = 192;
+        gp.count      = static_cast<int>(pairs.size() / 2);
+        for (size_t k = 0; k < pairs.size(); ++k) {
+          if (pairs[k].nof_llr != 0u) {
+            plan->input_llrs += fused ? static_cast<uint64_t>(pair_dms[k].E) + pair_dms[k].N : pairs[k].nof_llr;
+          }
+        }
+        const bool ok = upload(reinterpret_cast<void**>(&gp.d_desc), pairs.data(), pairs.size() * sizeof(dec_desc)) &&
+                        (!fused || upload(reinterpret_cast<void**>(&gp.d_dm), pair_dms.data(),
+                                          pair_dms.size() * sizeof(dm_desc)));
+        plan->groups.push_back(gp);
+        if (!ok) {
+          srsgpu_ldpc_decoder_plan_destroy(plan);
+          return fail(SRSGPU_ERR_HIP, "failed to upload decoder descriptors");
+        }
+      }
+    }
+    if (cbs.empty()) {
+      continue;
+    }
     srsgpu_ldpc_decoder_plan::group g;
     g.bg               = std::get<0>(kv.first);
     g.packed           = std::get<1>(kv.first);
     g.max_layers       = std::get<2>(kv.first);
-    const bool fused   = std::get<3>(kv.first);
     g.threads          = batch.threads.at(kv.first);
-    g.count            = static_cast<int>(kv.second.size());
+    g.count            = static_cast<int>(cbs.size());
     // Few codeblocks per launch leave the SIMDs with one or two waves each: the per-codeblock latency (instructions
     // per wave) then sets the kernel time, and the edge-split kernel halves it at ~15 % more total work. Above ~3
     // waves per SIMD of the plain kernel (MI355X: 1024 SIMDs) the launch is throughput-bound and keeps the plain one.
@@ -760,12 +859,11 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
       }
     }
     if (!fused) {
-      for (const dec_desc& d : kv.second) {
+      for (const dec_desc& d : cbs) {
         plan->input_llrs += d.nof_llr;
       }
     } else {
       // A fused codeblock reads its E codeword LLRs and writes the N-byte HARQ buffer instead.
-      const std::vector<dm_desc>& dms = batch.fused.at(kv.first);
       for (const dm_desc& m : dms) {
         plan->input_llrs += static_cast<uint64_t>(m.E) + m.N;
       }
@@ -778,9 +876,9 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
       }
     }
     pk4_layout             pk4;
-    const dec_desc*        src   = kv.second.data();
-    size_t                 bytes = kv.second.size() * sizeof(dec_desc);
-    if (g.packed && g.split == 1 && !fused && pk4_layout_for(g.bg, g.max_layers, kv.second, pk4)) {
+    const dec_desc*        src   = cbs.data();
+    size_t                 bytes = cbs.size() * sizeof(dec_desc);
+    if (g.packed && g.split == 1 && !fused && pk4_layout_for(g.bg, g.max_layers, cbs, pk4)) {
       g.pack    = LDPC_PK4;
       g.threads = pk4.threads;
       g.count   = pk4.groups;
@@ -812,10 +910,15 @@ int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
                          int8_t* const*                  d_harq_cbs = nullptr)
 {
   for (const auto& g : plan->groups) {
-    if (g.pack == LDPC_PK4) {
-      launch_ldpc_decode_pk4(g.bg, plan->impl, g.max_layers, g.d_desc, g.count, g.threads, d_llrs, d_out,
-                             d_nof_iterations, plan->ctx->d_pair_ab4[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok,
-                             s, d_harq_cbs);
+    if (g.pack == LDPC_PK4 || g.pack == 2) {
+      if (g.d_dm != nullptr && (d_cw_llrs == nullptr || (d_harq == nullptr && d_harq_cbs == nullptr))) {
+        return fail(SRSGPU_ERR_INVALID_ARG, "fused decoder group without codeword LLRs / HARQ buffer");
+      }
+      launch_ldpc_decode_pk4(g.bg, plan->impl, g.max_layers, g.d_desc, g.count, g.threads,
+                             g.d_dm != nullptr ? d_cw_llrs : d_llrs, d_out, d_nof_iterations,
+                             g.pack == 2 ? plan->ctx->d_pair_ab2[g.bg - 1] : plan->ctx->d_pair_ab4[g.bg - 1],
+                             plan->ctx->d_crc_arena, d_cb_crc_ok, s, d_harq_cbs, g.pack, g.d_dm,
+                             g.d_dm != nullptr ? d_harq : nullptr);
     } else if (g.packed) {
       if (g.d_dm != nullptr && (d_cw_llrs == nullptr || (d_harq == nullptr && d_harq_cbs == nullptr))) {
         return fail(SRSGPU_ERR_INVALID_ARG, "fused decoder group without codeword LLRs / HARQ buffer");

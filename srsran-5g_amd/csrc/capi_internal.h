@@ -63,6 +63,7 @@ struct srsgpu_context {
   /// Packed decoder address constants A | B << 16 per (Z position, edge), see ldpc_decoder_pk.hip (even Z only).
   uint32_t*                            d_pair_ab[2] = {nullptr, nullptr};
   uint32_t*                            d_pair_ab4[2] = {nullptr, nullptr};  ///< Same for the PK4 interleaved image.
+  uint32_t*                            d_pair_ab2[2] = {nullptr, nullptr};  ///< ... and the two-codeblock one.
   srsgpu::core_plan*                   d_core[2]   = {nullptr, nullptr};
   std::vector<srsgpu::core_plan>       core[2];
   uint32_t*                            d_crc_arena = nullptr;

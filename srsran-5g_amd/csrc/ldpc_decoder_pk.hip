@@ -1082,22 +1082,26 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
 // until the last one stops). The host puts codeblocks with the same Z, scaling, iteration limit and CRC mode in a
 // workgroup (descs[PK4 * w + i], empty slots have nof_llr = 0).
 // ---------------------------------------------------------------------------------------------------------------------
-constexpr int PK4       = LDPC_PK4;
-constexpr int PK4_CS    = PK4 * SOFT_COL_STRIDE;
-constexpr int PK4_WAVES = PK4 * 192 / WAVE;
-constexpr int PK4_RED   = 2 * PK4 * PK4_WAVES * 2;  ///< CRC reduction ints: [iteration parity][slot][wave][acc, zero]
-constexpr int PK4_SCRATCH_INTS = PK4_WAVES + PK4_RED + 2 * PK4;
+/// Geometry of a PKN-codeblock workgroup (PKN = LDPC_PK4 or 2: two codeblocks of Z <= 192 fill three waves).
+template <int PKN>
+struct pk_geom {
+  static constexpr int CS           = PKN * SOFT_COL_STRIDE;   ///< column stride of the interleaved image
+  static constexpr int WAVES        = PKN * 192 / WAVE;        ///< most waves of a workgroup (Z = 384 slots)
+  static constexpr int RED          = 2 * PKN * WAVES * 2;     ///< CRC reduction ints: [parity][slot][wave][acc, zero]
+  static constexpr int SCRATCH_INTS = WAVES + RED + 2 * PKN;
+};
 
 /// Byte offset of position l (0 <= l < Z) of slot i within a column of the interleaved image.
+template <int PKN>
 __device__ __forceinline__ uint32_t pair_pos4(uint32_t l, uint32_t H, uint32_t i)
 {
-  return ((l < H) ? 2u * PK4 * l : 2u * PK4 * (l - H) + 1u) + 2u * i;
+  return ((l < H) ? 2u * PKN * l : 2u * PKN * (l - H) + 1u) + 2u * i;
 }
 
 /// LLRs of one codeblock -> its slot of the interleaved image (ldpc_decoder_impl.cpp:152; the plain kernel's load with
 /// the slot's addresses), the punctured columns and every position beyond the input zeroed. Returns this thread's
 /// index of the last non-zero LLR it saw (ldpc_decoder_impl.cpp:94), -1 if none.
-template <int NCOL>
+template <int NCOL, int PKN>
 __device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const int8_t* __restrict__ llr,
                                              const dec_desc& d, uint32_t slot)
 {
@@ -1132,10 +1136,10 @@ __device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const in
       const bool short_path = (16u * static_cast<uint32_t>(w) >= head) && (i0 + 16u <= full) &&
                               (l0 + 16u <= static_cast<uint32_t>(Z));
       if (short_path) {
-        // Consecutive positions are 2 PK4 bytes apart; a byte past the half boundary moves by 1 - 2 PK4 H.
-        int8_t*        dst   = soft + (c0 + 2) * PK4_CS + pair_pos4(l0, H, slot);
+        // Consecutive positions are 2 PKN bytes apart; a byte past the half boundary moves by 1 - 2 PKN H.
+        int8_t*        dst   = soft + (c0 + 2) * pk_geom<PKN>::CS + pair_pos4<PKN>(l0, H, slot);
         const uint32_t cross = (l0 < H && l0 + 16u > H) ? (0xffffu << (H - l0)) : 0u;
-        const int      adj   = 1 - 2 * PK4 * static_cast<int>(H);
+        const int      adj   = 1 - 2 * PKN * static_cast<int>(H);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const uint32_t word = (q == 0) ? val[j].x : (q == 1) ? val[j].y : (q == 2) ? val[j].z : val[j].w;
@@ -1143,7 +1147,7 @@ __device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const in
           for (int k = 0; k < 4; ++k) {
             const int kk = 4 * q + k;
             const int mv = static_cast<int>((cross >> kk) & 1u) * adj;
-            dst[2 * PK4 * kk + mv] = static_cast<int8_t>(clamp_i(static_cast<int8_t>(word >> (8 * k)), -64, 64));
+            dst[2 * PKN * kk + mv] = static_cast<int8_t>(clamp_i(static_cast<int8_t>(word >> (8 * k)), -64, 64));
           }
         }
         if ((val[j].x | val[j].y | val[j].z | val[j].w) != 0u) {
@@ -1162,7 +1166,7 @@ __device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const in
               last  = (v != 0) ? static_cast<int>(i) : last;
               v     = (i < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
               const uint32_t cq = __umulhi(i, d.div_magic);
-              soft[(cq + 2) * PK4_CS + pair_pos4(i - cq * static_cast<uint32_t>(Z), H, slot)] = static_cast<int8_t>(v);
+              soft[(cq + 2) * pk_geom<PKN>::CS + pair_pos4<PKN>(i - cq * static_cast<uint32_t>(Z), H, slot)] = static_cast<int8_t>(v);
             }
           }
         }
@@ -1183,28 +1187,29 @@ __device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const in
   const uint32_t z = threadIdx.x;
   if (z < H) {
     auto* soft16 = reinterpret_cast<uint16_t*>(soft);
-    const uint32_t pz = PK4 * z + slot;  // 16-bit index of pair z within a column
-    soft16[(0 * PK4_CS) / 2 + pz] = 0;
-    soft16[(1 * PK4_CS) / 2 + pz] = 0;
+    const uint32_t pz = PKN * z + slot;  // 16-bit index of pair z within a column
+    soft16[(0 * pk_geom<PKN>::CS) / 2 + pz] = 0;
+    soft16[(1 * pk_geom<PKN>::CS) / 2 + pz] = 0;
     int c = 2 + static_cast<int>(ncols);
     if (static_cast<uint32_t>(n_llr) > full) {
       const uint32_t rem = static_cast<uint32_t>(n_llr) - full;
       if (z >= rem) {
-        soft[c * PK4_CS + 2 * pz] = 0;
+        soft[c * pk_geom<PKN>::CS + 2 * pz] = 0;
       }
       if (z + H >= rem) {
-        soft[c * PK4_CS + 2 * pz + 1] = 0;
+        soft[c * pk_geom<PKN>::CS + 2 * pz + 1] = 0;
       }
       ++c;
     }
     for (; c < NCOL; ++c) {
-      soft16[(c * PK4_CS) / 2 + pz] = 0;
+      soft16[(c * pk_geom<PKN>::CS) / 2 + pz] = 0;
     }
   }
   return last;
 }
 
 /// Hard decisions of one slot's K*Z systematic bits, written by the slot's H lanes (lane z: bytes z, z + H, ...).
+template <int PKN>
 __device__ __forceinline__ void write_hard_bits_pk4(const int8_t* __restrict__ soft, uint8_t* __restrict__ out,
                                                     int nbits, int Z, uint32_t magic, uint32_t slot, uint32_t z)
 {
@@ -1218,15 +1223,111 @@ __device__ __forceinline__ void write_hard_bits_pk4(const int8_t* __restrict__ s
       if (i < nbits) {
         const uint32_t col = __umulhi(static_cast<uint32_t>(i), magic);
         const uint32_t l   = static_cast<uint32_t>(i) - col * static_cast<uint32_t>(Z);
-        byte |= static_cast<uint32_t>(soft[col * PK4_CS + pair_pos4(l, H, slot)] <= 0) << (7 - k);
+        byte |= static_cast<uint32_t>(soft[col * pk_geom<PKN>::CS + pair_pos4<PKN>(l, H, slot)] <= 0) << (7 - k);
       }
     }
     out[b] = static_cast<uint8_t>(byte);
   }
 }
 
-template <int BG, int MODE, int MAXL>
-__global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_8)) void ldpc_decode_pk4_kernel(
+/// FUSE (as the one-codeblock kernel's): slot i's first transmission is dematched by the workgroup from the codeword
+/// LLRs (llrs + dms[PKN w + i].llr_offset) into its slot of the image and into its HARQ soft buffer (harq +
+/// harq_offset, or llr_cbs[cb]); the image is zeroed first. Returns this thread's last non-zero input position.
+template <int NCOL, int PKN>
+__device__ __forceinline__ int load_fused_pk4(int8_t* __restrict__ soft, const int8_t* __restrict__ llrs,
+                                              const dec_desc& d, const dm_desc& dm, int8_t* __restrict__ hb,
+                                              uint32_t slot)
+{
+  const int      Z     = d.Z;
+  const uint32_t H     = static_cast<uint32_t>(Z) / 2u;
+  const int      n_llr = static_cast<int>(d.nof_llr);
+  const uint32_t full  = __umulhi(static_cast<uint32_t>(n_llr), d.div_magic) * static_cast<uint32_t>(Z);
+  const int      E = static_cast<int>(dm.E), Qm = dm.Qm, R = E / Qm;
+  const int      Fl = dm.nof_filler, ninfo = static_cast<int>(dm.nsys) - Fl, Nh = static_cast<int>(dm.N);
+  const int8_t*  in   = llrs + dm.llr_offset;
+  int            last = -1;
+  // The one-codeblock kernel's soft_put / put (ldpc_decoder_impl.cpp:152 clamps, :94 trailing-zero trim) at the slot's
+  // interleaved addresses.
+  auto soft_put = [&](int k, int v) {
+    if (static_cast<uint32_t>(k) < static_cast<uint32_t>(n_llr)) {
+      last              = (v != 0 && k > last) ? k : last;
+      const uint32_t cq = __umulhi(static_cast<uint32_t>(k), d.div_magic);
+      const int      cv = (static_cast<uint32_t>(k) < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
+      soft[(cq + 2) * pk_geom<PKN>::CS + pair_pos4<PKN>(static_cast<uint32_t>(k) - cq * static_cast<uint32_t>(Z), H,
+                                                        slot)] = static_cast<int8_t>(cv);
+    }
+  };
+  auto put = [&](int k, int v) {
+    hb[k] = static_cast<int8_t>(v);
+    soft_put(k, v);
+  };
+  const bool q8   = Qm == 8 && ((dm.llr_offset & 7u) == 0u);
+  const bool q8x4 = LDPC_PK_HARQ_X4 && q8 &&
+                    ((R | ninfo | Fl | static_cast<int>(reinterpret_cast<uintptr_t>(hb))) & 3) == 0;
+  if (q8x4) {
+    for (int r0 = 4 * static_cast<int>(threadIdx.x); r0 < R; r0 += 4 * static_cast<int>(blockDim.x)) {
+      uint2 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = *reinterpret_cast<const uint2*>(in + 8 * (r0 + q));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          w |= ((((j < 4) ? v[q].x : v[q].y) >> (8 * (j & 3))) & 0xffu) << (8 * q);
+        }
+        const int n = j * R + r0;
+        const int k = n < ninfo ? n : n + Fl;
+        *reinterpret_cast<uint32_t*>(hb + k) = w;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          soft_put(k + q, static_cast<int8_t>(w >> (8 * q)));
+        }
+      }
+    }
+  } else {
+    for (int r = threadIdx.x; r < R; r += blockDim.x) {
+      int8_t sym[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sym[j] = (j < Qm) ? in[r * Qm + j] : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j < Qm) {
+          const int n = j * R + r;
+          put(n < ninfo ? n : n + Fl, sym[j]);
+        }
+      }
+    }
+  }
+  // Fillers: +infinity (ldpc_rate_dematcher_impl.cpp:172); the unreached tail [E + F, N) of the HARQ buffer zeroed.
+  for (int k = ninfo + static_cast<int>(threadIdx.x); k < ninfo + Fl; k += blockDim.x) {
+    put(k, 127);
+  }
+  {
+    const int t0 = E + Fl;  // 16-byte stores between the unaligned head and tail bytes
+    const int a0 = min(Nh, t0 + static_cast<int>((16u - (reinterpret_cast<uintptr_t>(hb + t0) & 15u)) & 15u));
+    const int nv = (Nh - a0) / 16;
+    const int a1 = a0 + 16 * nv;
+    if (static_cast<int>(threadIdx.x) < a0 - t0) {
+      hb[t0 + static_cast<int>(threadIdx.x)] = 0;
+    }
+    uint4* z16 = reinterpret_cast<uint4*>(hb + a0);
+    for (int q = threadIdx.x; q < nv; q += blockDim.x) {
+      z16[q] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (static_cast<int>(threadIdx.x) < Nh - a1) {
+      hb[a1 + static_cast<int>(threadIdx.x)] = 0;
+    }
+  }
+  return last;
+}
+
+template <int BG, int MODE, int MAXL, int PKN, bool FUSE>
+__global__ __launch_bounds__(64 * pk_geom<PKN>::WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_8)) void ldpc_decode_pk4_kernel(
     const dec_desc* __restrict__ descs,
     const int8_t* __restrict__ llrs,
     uint8_t* __restrict__ out,
@@ -1234,18 +1335,20 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
     const uint32_t* __restrict__ ab_table,
     const uint32_t* __restrict__ crc_tables,
     uint8_t* __restrict__ cb_crc_ok,
-    int8_t* const* __restrict__ llr_cbs)
+    int8_t* const* __restrict__ llr_cbs,
+    const dm_desc* __restrict__ dms,
+    int8_t* __restrict__ harq)
 {
   using G = bg_t<BG>;
-  static_assert(MAXL >= 4 && MAXL <= 16, "PK4: 8- and 16-layer classes (the 16-bit pair addresses and the LDS image)");
+  static_assert(MAXL >= 4 && MAXL <= 16, "PKN: 8- and 16-layer classes (the 16-bit pair addresses and the LDS image)");
   constexpr int NCOL = G::K + MAXL;
-  __shared__ __attribute__((aligned(16))) int8_t smem[NCOL * PK4_CS + PK4_SCRATCH_INTS * sizeof(int)];
+  __shared__ __attribute__((aligned(16))) int8_t smem[NCOL * pk_geom<PKN>::CS + pk_geom<PKN>::SCRATCH_INTS * sizeof(int)];
   int8_t* soft  = smem;
-  int*    wlast = reinterpret_cast<int*>(smem + NCOL * PK4_CS);  // [wave]: last non-zero LLR of the slot being loaded
-  int*    red   = wlast + PK4_WAVES;                              // [parity][slot][wave][acc, zero]
-  int*    cbi   = red + PK4_RED;                                  // [slot][layers, running]
+  int*    wlast = reinterpret_cast<int*>(smem + NCOL * pk_geom<PKN>::CS);  // [wave]: last non-zero LLR of the slot being loaded
+  int*    red   = wlast + pk_geom<PKN>::WAVES;                              // [parity][slot][wave][acc, zero]
+  int*    cbi   = red + pk_geom<PKN>::RED;                                  // [slot][layers, running]
 
-  const dec_desc* wd = descs + static_cast<size_t>(blockIdx.x) * PK4;
+  const dec_desc* wd = descs + static_cast<size_t>(blockIdx.x) * PKN;
   // Workgroup-uniform parameters from slot 0 (the host groups codeblocks that share them).
   const dec_desc d0 = wd[0];
   const int      Z  = d0.Z;
@@ -1261,7 +1364,7 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
   });
   int cnt = 1;
 #pragma unroll
-  for (int i = 1; i < PK4; ++i) {
+  for (int i = 1; i < PKN; ++i) {
     cnt += (wd[i].nof_llr != 0u) ? 1 : 0;
   }
   const int      wave   = threadIdx.x / WAVE;
@@ -1274,18 +1377,37 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
   const bool     use_crc = d0.crc_table != NO_CRC_TABLE;
   const bool     early   = (d0.flags & DEC_FLAG_EARLY_STOP) != 0;
 
+  if constexpr (FUSE) {
+    // The fused slots write only their input positions: the whole image starts at zero.
+    uint4* s16 = reinterpret_cast<uint4*>(soft);
+    for (int q = threadIdx.x; q < NCOL * pk_geom<PKN>::CS / 16; q += blockDim.x) {
+      s16[q] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __syncthreads();
+  }
   // ---- per slot: HARQ skip (pusch_decoder_impl.cpp:300), LLR load, input length, layer count ----
   for (int i = 0; i < cnt; ++i) {
     const dec_desc d       = wd[i];
     int            layers  = 0;
     int            running = 0;
-    if (cb_crc_ok != nullptr && cb_crc_ok[d.cb_index] != 0) {
+    if (!FUSE && cb_crc_ok != nullptr && cb_crc_ok[d.cb_index] != 0) {
       if (threadIdx.x == 0) {
         results[d.cb_index] = 0;
       }
     } else {
-      int last = load_llrs_pk4<NCOL>(soft, (llr_cbs != nullptr) ? llr_cbs[d.cb_index] : llrs + d.llr_offset, d,
-                                     static_cast<uint32_t>(i));
+      int last;
+      if constexpr (FUSE) {
+        // New data invalidates the codeblock CRC flag of the HARQ context (pusch_decoder_impl.cpp:132).
+        if (cb_crc_ok != nullptr && threadIdx.x == 0) {
+          cb_crc_ok[d.cb_index] = 0;
+        }
+        const dm_desc dm = dms[static_cast<size_t>(blockIdx.x) * PKN + i];
+        int8_t*       hb = (llr_cbs != nullptr) ? llr_cbs[d.cb_index] : harq + dm.harq_offset;
+        last = load_fused_pk4<NCOL, PKN>(soft, llrs, d, dm, hb, static_cast<uint32_t>(i));
+      } else {
+        last = load_llrs_pk4<NCOL, PKN>(soft, (llr_cbs != nullptr) ? llr_cbs[d.cb_index] : llrs + d.llr_offset, d,
+                                        static_cast<uint32_t>(i));
+      }
       last     = wave_max(last);
       if (lane == 0) {
         wlast[wave] = last;
@@ -1336,10 +1458,10 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
     nl_max = (cbi[2 * i + 1] != 0 && cbi[2 * i] > nl_max) ? cbi[2 * i] : nl_max;
   }
   nl_max            = __builtin_amdgcn_readfirstlane(nl_max);
-  // Per-lane loop state in one VGPR: the lane constant u = 2 PK4 z + 2 slot (bits 0-15; z and slot are recovered from
+  // Per-lane loop state in one VGPR: the lane constant u = 2 PKN z + 2 slot (bits 0-15; z and slot are recovered from
   // it) and the lane's layer count while its codeblock runs (bits 16+; 0 once it stopped, or for lanes without a
   // codeblock): "layer m runs" is one compare, lane >= (m + 1) << 16.
-  uint32_t lane_st = (2u * PK4 * z + 2u * slot) |
+  uint32_t lane_st = (2u * PKN * z + 2u * slot) |
                      (static_cast<uint32_t>((in_cb && cbi[2 * slot + 1] != 0) ? cbi[2 * slot] : 0) << 16);
   int      running = __syncthreads_or(lane_st >= (1u << 16) ? 1 : 0);
 
@@ -1368,7 +1490,7 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
       if (m < nl) {
         if (lane_st >= static_cast<uint32_t>(m + 1) << 16) {
           __builtin_amdgcn_sched_barrier(0);
-          row_update_pk<BG, MODE, m, (MAXL <= LDPC_PK_KEEP_ADDR_MAXL), PK4_CS>(soft, abi, z2x2, sc, magw[m], sgw[m],
+          row_update_pk<BG, MODE, m, (MAXL <= LDPC_PK_KEEP_ADDR_MAXL), pk_geom<PKN>::CS>(soft, abi, z2x2, sc, magw[m], sgw[m],
                                                                               hiw[m & 3]);
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -1381,7 +1503,7 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
       uint32_t       acc = 0, zero = 0;
       const bool     run = lane_st >= (1u << 16);
       const uint32_t ub  = lane_st & 0xffffu;
-      const uint32_t lz = ub / (2u * PK4), ls = (ub / 2u) % PK4;  // z, slot
+      const uint32_t lz = ub / (2u * PKN), ls = (ub / 2u) % PKN;  // z, slot
       if (run) {
         const dec_desc* md       = wd + ls;
         const uint32_t* table    = crc_tables + md->crc_table;
@@ -1393,8 +1515,8 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
         static_for<G::K>([&](auto Ci) {
           constexpr int  c  = decltype(Ci)::value;
           const uint32_t ib = ia + HH;
-          const int      sa = scol[c * PK4_CS];
-          const int      sb = scol[c * PK4_CS + 1];
+          const int      sa = scol[c * pk_geom<PKN>::CS];
+          const int      sb = scol[c * pk_geom<PKN>::CS + 1];
           zero |= static_cast<uint32_t>(sa == 0) | static_cast<uint32_t>(sb == 0);
           const uint32_t ta = table[ia];  // zero tail past the message, as above
           const uint32_t tb = table[ib];
@@ -1406,27 +1528,27 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
           }
         });
       }
-      int* r = red + (it & 1) * (PK4 * PK4_WAVES * 2);
-      static_for<PK4>([&](auto J) {
+      int* r = red + (it & 1) * (PKN * pk_geom<PKN>::WAVES * 2);
+      static_for<PKN>([&](auto J) {
         constexpr uint32_t j  = decltype(J)::value;
         const bool         mine = run && ls == j;
         const uint32_t     a    = wave_xor(mine ? acc : 0u);
         const uint32_t     zr   = (__ballot(mine && zero != 0) != 0) ? 1u : 0u;
         if (lane == 0) {
-          r[(j * PK4_WAVES + wave) * 2]     = static_cast<int>(a);
-          r[(j * PK4_WAVES + wave) * 2 + 1] = static_cast<int>(zr);
+          r[(j * pk_geom<PKN>::WAVES + wave) * 2]     = static_cast<int>(a);
+          r[(j * pk_geom<PKN>::WAVES + wave) * 2 + 1] = static_cast<int>(zr);
         }
       });
       __syncthreads();
       if (run) {
         uint32_t tacc = 0, tzero = 0;
         for (int w = 0; w < nwaves; ++w) {
-          tacc ^= static_cast<uint32_t>(r[(ls * PK4_WAVES + w) * 2]);
-          tzero |= static_cast<uint32_t>(r[(ls * PK4_WAVES + w) * 2 + 1]);
+          tacc ^= static_cast<uint32_t>(r[(ls * pk_geom<PKN>::WAVES + w) * 2]);
+          tzero |= static_cast<uint32_t>(r[(ls * pk_geom<PKN>::WAVES + w) * 2 + 1]);
         }
         if ((tzero == 0 || !early) && tacc == 0) {
           const dec_desc* md = wd + ls;
-          write_hard_bits_pk4(soft, out + md->out_offset, msg_len, Z, d0.div_magic, ls, lz);
+          write_hard_bits_pk4<PKN>(soft, out + md->out_offset, msg_len, Z, d0.div_magic, ls, lz);
           if (lz == 0) {
             results[md->cb_index] = it + 1;
             if (cb_crc_ok != nullptr) {
@@ -1441,9 +1563,9 @@ __global__ __launch_bounds__(64 * PK4_WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_
   }
   if (lane_st >= (1u << 16)) {
     const uint32_t  ub = lane_st & 0xffffu;
-    const uint32_t  lz = ub / (2u * PK4), ls = (ub / 2u) % PK4;
+    const uint32_t  lz = ub / (2u * PKN), ls = (ub / 2u) % PKN;
     const dec_desc* md = wd + ls;
-    write_hard_bits_pk4(soft, out + md->out_offset, msg_len, Z, d0.div_magic, ls, lz);
+    write_hard_bits_pk4<PKN>(soft, out + md->out_offset, msg_len, Z, d0.div_magic, ls, lz);
     if (lz == 0) {
       results[md->cb_index] = -1;
     }
@@ -1526,15 +1648,23 @@ void launch_ldpc_decode_pk4(int             bg,
                             const uint32_t* d_crc_tables,
                             uint8_t*        d_cb_crc_ok,
                             hipStream_t     stream,
-                            int8_t* const*  d_llr_cbs)
+                            int8_t* const*  d_llr_cbs,
+                            int             pkn,
+                            const dm_desc*  d_dm,
+                            int8_t*         d_harq)
 {
   if (nof_groups <= 0) {
     return;
   }
   dim3 grid(nof_groups), block(block_threads);
+  // (codeblocks per workgroup, fused dematching): (LDPC_PK4, no), (2, no), (2, yes).
+#define SRSGPU_PK4_LAUNCH1(BG_, MODE_, MAXL_, PKN_, FUSE_)                                                              \
+  ldpc_decode_pk4_kernel<BG_, MODE_, MAXL_, PKN_, FUSE_><<<grid, block, 0, stream>>>(                                   \
+      d_desc, d_llrs, d_out, d_results, d_ab4, d_crc_tables, d_cb_crc_ok, d_llr_cbs, d_dm, d_harq)
 #define SRSGPU_PK4_LAUNCH(BG_, MODE_, MAXL_)                                                                           \
-  ldpc_decode_pk4_kernel<BG_, MODE_, MAXL_><<<grid, block, 0, stream>>>(d_desc, d_llrs, d_out, d_results, d_ab4,       \
-                                                                        d_crc_tables, d_cb_crc_ok, d_llr_cbs)
+  (pkn != 2 ? SRSGPU_PK4_LAUNCH1(BG_, MODE_, MAXL_, LDPC_PK4, false)                                                   \
+            : (d_dm != nullptr ? SRSGPU_PK4_LAUNCH1(BG_, MODE_, MAXL_, 2, true)                                        \
+                               : SRSGPU_PK4_LAUNCH1(BG_, MODE_, MAXL_, 2, false)))
   if (bg == 1) {
     if (max_layers <= 8) {
       mode == 1 ? SRSGPU_PK4_LAUNCH(1, 1, 8) : SRSGPU_PK4_LAUNCH(1, 0, 8);
@@ -1549,6 +1679,7 @@ void launch_ldpc_decode_pk4(int             bg,
     }
   }
 #undef SRSGPU_PK4_LAUNCH
+#undef SRSGPU_PK4_LAUNCH1
 }
 
 } // namespace srsgpu

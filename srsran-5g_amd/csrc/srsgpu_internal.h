@@ -261,9 +261,11 @@ void launch_ldpc_decode_pk(int             bg,
 /// Codeblocks per workgroup of the multi-codeblock packed decoder (ldpc_decode_pk4_kernel).
 constexpr int LDPC_PK4 = 4;
 
-/// Launches the multi-codeblock packed decoder: workgroup w decodes d_desc[LDPC_PK4 * w + i] (slots with nof_llr = 0
-/// are empty; the slots of a workgroup share Z, scaling, iteration limit and CRC mode), codeblock slot i on lanes
-/// [i Z / 2, (i + 1) Z / 2), block_threads >= (used slots) x Z / 2. d_ab4: the interleaved-image pair constants.
+/// Launches the multi-codeblock packed decoder: workgroup w decodes d_desc[pkn * w + i] (pkn = LDPC_PK4 or 2; slots with
+/// nof_llr = 0 are empty; the slots of a workgroup share Z, scaling, iteration limit and CRC mode), codeblock slot i on
+/// lanes [i Z / 2, (i + 1) Z / 2), block_threads >= (used slots) x Z / 2. d_ab4: the pkn-interleaved image's pair
+/// constants. d_dm (pkn = 2): fused rate dematching of first transmissions (d_dm[pkn * w + i], d_llrs the codeword
+/// LLRs, soft buffers at d_harq + harq_offset or d_llr_cbs[cb]).
 void launch_ldpc_decode_pk4(int             bg,
                             int             mode,
                             int             max_layers,
@@ -277,7 +279,10 @@ void launch_ldpc_decode_pk4(int             bg,
                             const uint32_t* d_crc_tables,
                             uint8_t*        d_cb_crc_ok,
                             hipStream_t     stream,
-                            int8_t* const*  d_llr_cbs = nullptr);
+                            int8_t* const*  d_llr_cbs = nullptr,
+                            int             pkn       = LDPC_PK4,
+                            const dm_desc*  d_dm      = nullptr,
+                            int8_t*         d_harq    = nullptr);
 
 /// Launches the batched LDPC decoder (ldpc_decoder.hip). d_llr_cbs (optional): codeblock c's input is
 /// d_llr_cbs[dec_desc::cb_index] instead of d_llrs + llr_offset (the same for the packed launchers: per-codeblock HARQ

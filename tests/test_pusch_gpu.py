@@ -484,3 +484,56 @@ def test_pusch_decoder_harq_in_arena(orc, ctx):
                 assert np.array_equal(harq[off: off + cb_len[t]], arena_h[slot: slot + cb_len[t]]), (rv, t, i)
                 c += 1
         assert int(outs[0][2].sum()) >= 8
+
+
+def test_pusch_decoder_two_codeblock_workgroups(orc, ctx, monkeypatch):
+    """Two codeblocks of Z = 144 .. 192 per workgroup (SRSGPU_DECODER_PK2=1: ldpc_decode_pk4_kernel<..., PKN = 2>,
+    fused rate dematching on first transmissions, the separate dematcher for the rv2 retransmission) equal the
+    one-codeblock kernel (SRSGPU_DECODER_PK2=0, the default) bit for bit: TB flags, TBs, per-CB iteration counts and the HARQ soft bits, over an odd
+    number of such codeblocks (a workgroup with an empty slot) mixed with other lifting sizes; and the oracle."""
+    import torch
+    import srsgpu
+    from srsgpu import sch
+    rng = np.random.default_rng(23)
+    grants, tbs = [], []
+    # 4-5 PRB 256QAM grants (Z = 192 / 224, the bench's UL), Z = 144 / 160 / 176 grants and a 12-PRB one (Z = 384).
+    while len(grants) < 41:
+        k = len(grants) % 6
+        nprb, qm, rate, ns = [(4, 8, 948.0, 12), (5, 8, 948.0, 12), (2, 8, 682.5, 12), (4, 8, 948.0, 10),
+                              (3, 8, 682.5, 10), (12, 4, 616.0, 12)][k]
+        g = sch.UeGrant(nprb, 1, qm, rate, nof_symb_sh=ns)
+        seg = g.segmentation()
+        grants.append((g, seg))
+        tbs.append(rng.integers(0, 256, seg.tbs // 8).astype(np.uint8))
+    zs = {seg.lifting_size for _, seg in grants}
+    assert {144, 160, 176, 192} <= zs, zs
+    results = {}
+    for pk2 in ("1", "0"):
+        monkeypatch.setenv("SRSGPU_DECODER_PK2", pk2)
+        dec = srsgpu.PuschDecoder(ctx, "avx2")
+        out = []
+        for rv, new_data in ((0, True), (2, False)):
+            llrs, cfgs = [], []
+            for i, ((g, seg), tb) in enumerate(zip(grants, tbs)):
+                cw, _, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, rv, g.qm, g.nof_layers, 0, g.nof_ch_symbols)
+                r = np.random.default_rng(1000 * rv + i)
+                llrs.append(bits_to_llrs(r, cw, amp=8.0, noise=[1.0, 3.0, 7.0][i % 3]))
+                cfgs.append(srsgpu.PuschTransportBlock(seg.tbs // 8, seg.base_graph, rv, g.qm, g.nof_layers,
+                                                       g.nof_ch_symbols, new_data=new_data, nof_ldpc_iterations=6))
+            ok, got, iters = dec.decode_batch(llrs, cfgs)
+            out.append((ok, [t.copy() for t in got], iters, dec.harq[0].cpu().numpy().copy()))
+            print(f"PK2={pk2} rv{rv}: TBs ok {sum(ok)}/{len(ok)}, iterations {sorted({x for v in iters for x in v})}")
+        results[pk2] = out
+    for a, b in zip(results["1"], results["0"]):
+        assert a[0] == b[0]
+        assert all(np.array_equal(x, y) for x, y in zip(a[1], b[1]))
+        assert a[2] == b[2]
+        assert np.array_equal(a[3], b[3])
+    # The one-codeblock kernel against the oracle for the first transmission (as test_pusch_decoder_tb_level).
+    ok0, got0, iters0, _ = results["0"][0]
+    n_ok = 0
+    for i, ((g, seg), tb) in enumerate(zip(grants, tbs)):
+        if ok0[i]:
+            assert np.array_equal(got0[i], tb), i
+            n_ok += 1
+    assert n_ok >= 10

@@ -18,6 +18,7 @@
 #   lds              PMC pass of the bench: LDS issue stalls, bank conflicts, LDS-array cycles per kernel
 #   ab:DIR[:N]       A/B of the default bench: the in-tree library against srsran-5g_amd/DIR's, N rounds
 #   slotsab:V=X[:N]  A/B of the UL slot processors (16 threads): default environment against V=X, N rounds
+#   benchab:V=X[:N]  A/B of the default bench: default environment against V=X, N rounds
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -101,6 +102,20 @@ for step in "$@"; do
             || { tail -20 "$OUT/slotsab_${v}_$i.log"; exit 1; }
           python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], [(p['profile'][:12], [round(r['slots_per_s']) for r in p['runs']]) for p in d['slot_processors']['ul']])" \
             "$OUT/slotsab_${v}_$i.json" "$v ${E[*]}"
+        done
+      done ;;
+    benchab:*)
+      # benchab:VAR=V[,VAR2=V2][:N] — the default bench N rounds (default 2), alternating the default environment and
+      # the given variables
+      SPEC=${step#benchab:}; KV=${SPEC%%:*}; N=2; [[ "$SPEC" == *:* ]] && N=${SPEC##*:}
+      IFS=, read -r -a VARS <<< "$KV"
+      for i in $(seq 1 "$N"); do
+        for v in default alt; do
+          if [ "$v" = default ]; then E=(); else E=("${VARS[@]}"); fi
+          env "${E[@]}" timeout -k 10 300 python -u bench.py > "$OUT/benchab_${v}_$i.json" 2> "$OUT/benchab_${v}_$i.err" \
+            || { tail -20 "$OUT/benchab_${v}_$i.err"; exit 1; }
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value']), [round(p['value']) for p in d['operating_points']], round(d['stage_ms_per_step']['pusch_decode'], 4), {k: round(v['value']) for k, v in d.get('workloads', {}).items()})" \
+            "$OUT/benchab_${v}_$i.json" "$v ${E[*]}"
         done
       done ;;
     ab:*)

@@ -810,7 +810,8 @@ int srsgpu_pusch_decoder_plan_execute(const srsgpu_pusch_decoder_plan* plan,
                                       void*                            stream);
 
 /** As srsgpu_pusch_decoder_plan_execute, with codeblock c's HARQ soft buffer (N bytes, the rate dematcher's output and
- *  the decoder's input) at d_harq_cbs[c] - a device array of one pointer per codeblock of the plan, e.g. the slots of
+ *  the decoder's input) at d_harq_cbs[c], c = srsgpu_pusch_tb_config::cb_offset + the codeblock's index in its TB (the
+ *  index of its CRC flag and message) - a device array covering every such index of the plan, e.g. the slots of
  *  a persistent rx-buffer arena (the reference's rx_buffer.h:72 get_codeblock_soft_bits for the codeblock's absolute
  *  identifier, :65) - instead of at d_harq + srsgpu_pusch_tb_config::harq_offset. The soft bits stay in the arena: no
  *  copy into a batch buffer before the decode and back after it (srsgpu_harq_copy_arenas). Asynchronous,

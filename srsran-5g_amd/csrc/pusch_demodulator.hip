@@ -410,10 +410,14 @@ __device__ __forceinline__ void setup_uniform(const demod_desc& d, const uint32_
 {
   u.rot = nullptr;
   if (d.ce_cfo) {
-    for (uint32_t i = threadIdx.x; i < 14u * 16u; i += blockDim.x) {
-      const uint32_t l = i >> 4, ly = (i >> 2) & 3u, p = i & 3u;
+    // Only the transmission's L layers' entries (every port slot p < 4: the RE loop reads them all; unused ports get
+    // the identity): 56 sincos per workgroup for one layer instead of 224, before the workgroup's first barrier.
+    const uint32_t nl = d.L;
+    for (uint32_t j = threadIdx.x; j < 14u * 4u * nl; j += blockDim.x) {
+      const uint32_t l = j / (4u * nl), ly = (j / 4u) % nl, p = j & 3u;
+      const uint32_t i = (l * 4u + ly) * 4u + p;
       float          c = 0.f;
-      if (ly < d.L && p < d.P) {
+      if (p < d.P) {
         c = __uint_as_float(ce[d.ce_base + ly * d.ce_layer_stride + p * d.port_stride + d.nsc + d.cfo_sc]);
       }
       float sn, cs;

@@ -84,6 +84,10 @@ struct srsgpu_pdsch_encoder_plan {
   int             threads[2] = {64, 64};
   size_t          out_begin  = 0;
   size_t          out_end    = 0;
+  /// The encoders OR a codeblock's partial edge words into the output, so [out_begin, out_end) is zeroed first, unless
+  /// every codeblock covers whole 32-bit words and the TB codewords tile the range without gaps: then every word is
+  /// stored exactly once (no memset node in the DL graph). SRSGPU_ENCODER_ZERO=1 keeps the memset (A/B).
+  bool            zero_output = true;
 };
 
 struct srsgpu_pusch_decoder_plan {
@@ -1250,6 +1254,8 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
   const char* force_env         = std::getenv("SRSGPU_ENCODER_BYTE_KERNEL");
   const bool  force_byte_kernel = force_env != nullptr && force_env[0] == '1';
   size_t                   out_begin = ~size_t(0), out_end = 0;
+  bool                     word_aligned = true;  // every codeblock starts and ends on a 32-bit word boundary
+  std::vector<std::pair<size_t, size_t>> cw_ranges;  // [begin, end) bytes of each TB's codeword
   for (uint32_t t = 0; t < nof_tbs; ++t) {
     const srsgpu_pdsch_tb_config& c = cfgs[t];
     const int                     qm = c.modulation_order;
@@ -1319,6 +1325,7 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
       const int last_col = (kmax + 2 * Z) / Z;  // full-codeblock node index
       const int n_ext    = last_col - (K + 4) + 1;
       d.n_ext            = static_cast<uint8_t>(n_ext < 0 ? 0 : n_ext);
+      word_aligned       = word_aligned && (d.out_bit_offset % 32u) == 0u && (cb.E % 32) == 0;
       // Packed kernel: Z % 32 == 0 and byte-aligned codeblock data (and CB CRC position).
       const bool packed = !force_byte_kernel && Z % 32 == 0 && ((cb.tb_offset | cb.nof_data) & 7) == 0 &&
                           (seg.cb_crc_len == 0 || (cb.used & 7) == 0);
@@ -1327,7 +1334,20 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
     maxz[seg.bg - 1] = Z > maxz[seg.bg - 1] ? Z : maxz[seg.bg - 1];
     out_begin        = std::min(out_begin, static_cast<size_t>(c.cw_offset));
     out_end          = std::max(out_end, static_cast<size_t>(c.cw_offset) + (static_cast<size_t>(seg.cw_length) + 31) / 32 * 4);
+    word_aligned     = word_aligned && seg.cw_length % 32 == 0;
+    cw_ranges.emplace_back(c.cw_offset, static_cast<size_t>(c.cw_offset) + static_cast<size_t>(seg.cw_length) / 8);
   }
+  // No memset when every output word is written whole by exactly one codeblock: aligned codeblocks and TB codewords
+  // that tile [out_begin, out_end) (no gap left unwritten, no overlap).
+  bool tiled = word_aligned;
+  if (tiled) {
+    std::sort(cw_ranges.begin(), cw_ranges.end());
+    for (size_t i = 1; i < cw_ranges.size() && tiled; ++i) {
+      tiled = cw_ranges[i].first == cw_ranges[i - 1].second;
+    }
+  }
+  const char* zero_env = std::getenv("SRSGPU_ENCODER_ZERO");
+  const bool  zero_out = !tiled || (zero_env != nullptr && zero_env[0] == '1');
   // TB CRC slices: a TB with a contribution table is spread over TB_CRC_SLICE_BYTES ranges (a max-TBS TB of one
   // workgroup would otherwise serialise ~150 KB of byte-table steps); without a table it stays one slice.
   std::vector<tb_crc_slice> slices;
@@ -1343,6 +1363,7 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
   plan->nof_slices = static_cast<int>(slices.size());
   plan->out_begin = nof_tbs ? out_begin : 0;
   plan->out_end   = out_end;
+  plan->zero_output = zero_out;
   bool ok         = true;
   if (nof_tbs > 0) {
     ok = hipMalloc(&plan->d_tb, tbd.size() * sizeof(tb_crc_desc)) == hipSuccess &&
@@ -1396,7 +1417,7 @@ int srsgpu_pdsch_encoder_plan_execute(const srsgpu_pdsch_encoder_plan* plan,
   auto  s  = static_cast<hipStream_t>(stream);
   auto* ev = plan->timer.begin();
   stage_timer::mark(ev, 0, s);
-  if (plan->out_end > plan->out_begin) {
+  if (plan->zero_output && plan->out_end > plan->out_begin) {
     HIP_TRY(hipMemsetAsync(d_codewords + plan->out_begin, 0, plan->out_end - plan->out_begin, s));
   }
   if (!plan->inline_tb_crc && plan->nof_tbs > 0) {

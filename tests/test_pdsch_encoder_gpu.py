@@ -151,3 +151,31 @@ def test_crc_table_arena_long_running_cell(ctx):
         assert np.array_equal(a, b)
     for p in live:
         p.close()
+
+
+def test_pdsch_encoder_aligned_plan_without_memset(ctx, monkeypatch):
+    """A plan whose codeblocks all cover whole 32-bit words (4 layers of 256QAM) and whose codewords tile the output
+    skips the output memset (capi.cpp: zero_output): on an output pre-filled with 0xAB (encode_batch) it must give the
+    oracle's codewords, as the memset path (SRSGPU_ENCODER_ZERO=1) does; a 1-layer QPSK TB in the plan brings the
+    memset back (edge words ORed)."""
+    import srsgpu
+    from srsgpu import sch
+    orc = Oracle()
+    rng = np.random.default_rng(11)
+    grants = list(sch.slot_100mhz_4x4())[:8]
+    tbs, cfgs, want = [], [], []
+    qm2, r2 = [v for v in sch.MCS_TABLE_256QAM.values() if v[0] == 2][0]
+    for g in grants + [sch.UeGrant(3, 1, qm2, r2, nof_symb_sh=11)]:
+        seg = g.segmentation()
+        tb = rng.integers(0, 256, seg.tbs // 8).astype(np.uint8)
+        cw, _, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, 0, g.qm, g.nof_layers, 0, g.nof_ch_symbols)
+        tbs.append(tb)
+        cfgs.append(srsgpu.PdschTransportBlock(seg.base_graph, 0, g.qm, g.nof_layers, g.nof_ch_symbols))
+        want.append(cw)
+    enc = srsgpu.PdschEncoder(ctx)
+    for zero in ("0", "1"):
+        monkeypatch.setenv("SRSGPU_ENCODER_ZERO", zero)
+        for n in (len(grants), len(grants) + 1):  # aligned plan; plus the unaligned TB
+            got = enc.encode_batch(tbs[:n], cfgs[:n])
+            for i, (a, b) in enumerate(zip(got, want[:n])):
+                assert np.array_equal(a, b), (zero, n, i)

@@ -285,6 +285,8 @@ def parse_args(argv=None):
     # Two graphs per set, each leg on its own stream, with 9 sets: 134.3k slots/s vs 130.0k for one graph per set
     # with 5 sets (profiles/r3_leg_graphs_sweep.json: one graph per set with 7 sets drops to 123k; 7-14 sets with leg
     # graphs give 132.9k-135.0k).
+    ap.add_argument("--ul-priority", type=int, default=int(os.environ.get("SRSGPU_BENCH_UL_PRIORITY", "0")),
+                    help="1: replay the UL legs on high-priority streams (with --leg-graphs)")
     ap.add_argument("--leg-graphs", action=argparse.BooleanOptionalAction, default=True,
                     help="capture the DL and UL legs of a step as two graphs replayed on two streams per input set")
     ap.add_argument("--graph-collectives", action=argparse.BooleanOptionalAction, default=True,
@@ -427,7 +429,10 @@ def measure(args, env):
     set_streams = [torch.cuda.Stream(dev) for _ in range(K)] if args.pipeline else None
     # --leg-graphs: the DL and UL legs of a set as two graphs replayed on two streams of their own.
     leg_graphs = args.leg_graphs and args.graph and not shard_x
-    ul_set_streams = [torch.cuda.Stream(dev) for _ in range(K)] if leg_graphs and args.pipeline else None
+    # --ul-priority: the UL legs' streams at a higher HIP stream priority (-1), so the decoder's workgroups are
+    # dispatched ahead of the DL leg's when both wait for a CU.
+    ul_set_streams = ([torch.cuda.Stream(dev, priority=-args.ul_priority) for _ in range(K)]
+                      if leg_graphs and args.pipeline else None)
 
     def step(i):
         st = sets[i % K]

@@ -285,6 +285,8 @@ def parse_args(argv=None):
     # Two graphs per set, each leg on its own stream, with 9 sets: 134.3k slots/s vs 130.0k for one graph per set
     # with 5 sets (profiles/r3_leg_graphs_sweep.json: one graph per set with 7 sets drops to 123k; 7-14 sets with leg
     # graphs give 132.9k-135.0k).
+    ap.add_argument("--dl-priority", type=int, default=int(os.environ.get("SRSGPU_BENCH_DL_PRIORITY", "0")),
+                    help="1: replay each set's step (the DL leg with --leg-graphs) on high-priority streams")
     ap.add_argument("--ul-priority", type=int, default=int(os.environ.get("SRSGPU_BENCH_UL_PRIORITY", "0")),
                     help="1: replay the UL legs on high-priority streams (with --leg-graphs)")
     ap.add_argument("--leg-graphs", action=argparse.BooleanOptionalAction, default=True,
@@ -426,7 +428,8 @@ def measure(args, env):
 
     # Pipelining across steps: each input set replays on its own stream, so a step's UL decode can overlap the next
     # set's front end (different buffers; a set's consecutive steps stay ordered on its stream).
-    set_streams = [torch.cuda.Stream(dev) for _ in range(K)] if args.pipeline else None
+    set_streams = ([torch.cuda.Stream(dev, priority=-args.dl_priority) for _ in range(K)]
+                   if args.pipeline else None)
     # --leg-graphs: the DL and UL legs of a set as two graphs replayed on two streams of their own.
     leg_graphs = args.leg_graphs and args.graph and not shard_x
     # --ul-priority: the UL legs' streams at a higher HIP stream priority (-1), so the decoder's workgroups are

@@ -206,6 +206,9 @@ public:
     for (auto& st : streams) {
       (void)hipStreamSynchronize(st->get());
     }
+    if (launcher != nullptr) {
+      srsgpu_ofdm_plan_destroy(launcher);
+    }
   }
 
   /// Registers a sector's plans, one per position of its period (kept by the caller while registered): its index, or
@@ -361,6 +364,19 @@ private:
   /// Shared buffers sized from the first sector's plans. Holds mtx and gpu::hip_setup_mutex.
   bool size_buffers(const std::vector<srsgpu_ofdm_plan*>& plans)
   {
+    // The launch parameters come from a plan of the batcher's own (a copy of the first plan): the sector that
+    // registered first may be removed, and its plans destroyed, while the others keep submitting.
+    srsgpu_ofdm_plan* own = nullptr;
+    if (srsgpu_ofdm_plan_concat(ctx, const_cast<const srsgpu_ofdm_plan* const*>(plans.data()), 1, &own) !=
+        SRSGPU_OK) {
+      return false;
+    }
+    for (srsgpu_ofdm_plan* p : plans) {
+      if (!joins(own, p) || !runs_job_lists(p)) {
+        srsgpu_ofdm_plan_destroy(own);
+        return false;
+      }
+    }
     for (srsgpu_ofdm_plan* p : plans) {
       const size_t grid  = srsgpu_ofdm_plan_nof_grid_words(p) * sizeof(uint32_t);
       const size_t samp  = srsgpu_ofdm_plan_nof_samples(p) * sizeof(cf_t);
@@ -373,6 +389,8 @@ private:
     }
     const size_t entries = static_cast<size_t>(nof_sectors) * depth;
     if ((entries * in_max) / sizeof(uint32_t) >= (1ull << 32) || (entries * out_max) / sizeof(uint32_t) >= (1ull << 32)) {
+      in_max = out_max = jobs_per_entry = 0;
+      srsgpu_ofdm_plan_destroy(own);
       return false;  // beyond the jobs' 32-bit offsets
     }
     in_all.reserve(entries * in_max);
@@ -382,22 +400,46 @@ private:
     for (unsigned b = 0; b != NOF_BATCHES; ++b) {
       *flags.host<uint32_t>(b * 64) = 0;
     }
-    launcher = plans[0];
+    launcher = own;
     return true;
   }
 
-  /// Whether the plans can share a launch with the first sector's (the launch takes its parameters from those).
-  bool compatible(const std::vector<srsgpu_ofdm_plan*>& plans) const
+  /// Whether two plans can run in one launch (srsgpu_ofdm_plan_concat accepts them: same direction, DFT size,
+  /// bandwidth, DFT window offset and ports).
+  bool joins(const srsgpu_ofdm_plan* a, const srsgpu_ofdm_plan* b) const
   {
-    const srsgpu_ofdm_plan* pair[2] = {launcher, plans[0]};
+    const srsgpu_ofdm_plan* pair[2] = {a, b};
     srsgpu_ofdm_plan*       joined  = nullptr;
     if (srsgpu_ofdm_plan_concat(ctx, pair, 2, &joined) != SRSGPU_OK) {
       return false;
     }
     srsgpu_ofdm_plan_destroy(joined);
+    return true;
+  }
+
+  /// Whether the plan's DFT size runs from job lists (not the split sizes 9216...98304): a zero-job trial, which
+  /// launches nothing.
+  static bool runs_job_lists(const srsgpu_ofdm_plan* p)
+  {
+    uint64_t dummy = 0;
+    return srsgpu_ofdm_jobs_execute(p, nullptr, 0, &dummy, &dummy, nullptr) == SRSGPU_OK;
+  }
+
+  /// Whether every position's plan can share a launch with the first sector's and fits the shared buffers: its
+  /// input and output in an entry, its jobs in an entry's slice of the job table (sized from the first sector; a
+  /// normal-CP sector joining an extended-CP group has more jobs per slot with the same sample count).
+  bool compatible(const std::vector<srsgpu_ofdm_plan*>& plans) const
+  {
     for (srsgpu_ofdm_plan* p : plans) {
-      const size_t grid = srsgpu_ofdm_plan_nof_grid_words(p) * sizeof(uint32_t);
-      const size_t samp = srsgpu_ofdm_plan_nof_samples(p) * sizeof(cf_t);
+      if (!joins(launcher, p) || !runs_job_lists(p)) {
+        return false;
+      }
+      const size_t grid  = srsgpu_ofdm_plan_nof_grid_words(p) * sizeof(uint32_t);
+      const size_t samp  = srsgpu_ofdm_plan_nof_samples(p) * sizeof(cf_t);
+      uint32_t     njobs = 0;
+      if (srsgpu_ofdm_plan_get_jobs(p, nullptr, 0, &njobs) != SRSGPU_OK || njobs > jobs_per_entry) {
+        return false;
+      }
       if ((inverse ? grid : samp) > in_max || (inverse ? samp : grid) > out_max) {
         return false;
       }
@@ -483,7 +525,7 @@ private:
   std::chrono::microseconds                         window;
   clock::duration                                   activity;
   std::vector<sector_state>                         sectors;
-  const srsgpu_ofdm_plan*                           launcher = nullptr;  ///< the first sector's plan: launch params
+  srsgpu_ofdm_plan*                                 launcher = nullptr;  ///< owned copy of the first plan: launch params
   size_t                                            in_max = 0, out_max = 0, jobs_per_entry = 0;
   gpu::mapped_buffer                                jobs_buf;  ///< NOF_BATCHES job tables
   gpu::mapped_buffer                                in_all;    ///< every sector's entries' inputs

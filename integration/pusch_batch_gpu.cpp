@@ -743,14 +743,18 @@ public:
 
   /// A batch's fixed HBM grid slot for grids of P ports x grid_prb PRBs: (index within the shape's arena, pointer).
   std::pair<unsigned, uint32_t*> register_grid(unsigned P, unsigned grid_prb);
-  unsigned                       new_batch_id() { return next_batch_id++; }
+  /// Returns a batch's grid slot (the batch is destroyed): uplink processors come and go with the factories that
+  /// create them, while the device's service lives on.
+  void     release_grid(unsigned P, unsigned grid_prb, unsigned index);
+  unsigned new_batch_id() { return next_batch_id++; }
 
   void submit(std::unique_ptr<pusch_job> job);
 
 private:
   struct grid_class {
-    unsigned  P = 0, prb = 0, used = 0;
-    uint32_t* d_grids = nullptr;
+    unsigned              P = 0, prb = 0, used = 0;
+    uint32_t*             d_grids = nullptr;
+    std::vector<unsigned> free;  ///< released slots below `used`
   };
 
   /// One launch in flight: a launcher (stream, staging, buffers, cached launch plans) and its jobs.
@@ -883,11 +887,28 @@ std::pair<unsigned, uint32_t*> pusch_gpu_service::register_grid(unsigned P, unsi
     grid_classes.push_back(c);
     g = &grid_classes.back();
   }
-  if (g->used == cfg.max_grids) {
-    throw std::length_error(std::string(WHO) + ": more batches than max_grids for one grid shape");
+  unsigned index = 0;
+  if (!g->free.empty()) {
+    index = g->free.back();
+    g->free.pop_back();
+  } else {
+    if (g->used == cfg.max_grids) {
+      throw std::length_error(std::string(WHO) + ": more batches than max_grids for one grid shape");
+    }
+    index = g->used++;
   }
-  const unsigned index = g->used++;
   return {index, g->d_grids + index * (grid_bytes / sizeof(uint32_t))};
+}
+
+void pusch_gpu_service::release_grid(unsigned P, unsigned grid_prb, unsigned index)
+{
+  std::lock_guard<std::mutex> lock(grid_mtx);
+  for (grid_class& c : grid_classes) {
+    if (c.P == P && c.prb == grid_prb) {
+      c.free.push_back(index);
+      return;
+    }
+  }
 }
 
 void pusch_gpu_service::submit(std::unique_ptr<pusch_job> job)
@@ -1720,6 +1741,9 @@ pusch_slot_batch::~pusch_slot_batch()
   }
   (void)hipStreamSynchronize(upload_stream.get());
   (void)hipEventDestroy(uploaded);
+  if (grid_slot >= 0) {
+    service->release_grid(grid_P, grid_prb, static_cast<unsigned>(grid_slot));
+  }
   for (shard_device& sh : shards) {
     device_scope sdev(sh.ctx.get(), WHO);
     (void)hipStreamSynchronize(sh.upload->get());

@@ -18,8 +18,8 @@
 //    the reference's rx buffer pool), one download. The results then go through the reference's own
 //    pusch_processor_impl per PDU, fed the GPU results (channel-estimate metrics, LLRs + scrambling sequence +
 //    post-equalisation statistics, decoded TB), so the CSI report, the UCI demultiplexing / decoding, the notifier
-//    order and the rx buffer bookkeeping are the reference's. PDUs the batch does not cover (CSI Part 2, non-identity
-//    rx port lists, more than four layers) go to a caller-supplied pusch_processor.
+//    order and the rx buffer bookkeeping are the reference's. PDUs the batch does not cover (UCI only, non-identity
+//    rx port lists, more than four layers or rx ports, extended CP) go to a caller-supplied pusch_processor.
 //
 //  * DL: the reference's downlink_processor_single_executor_impl is built with a pdsch_processor that runs the
 //    reference's pdsch_processor_impl over recording encoder / modulator / DM-RS stages (create_pdsch_processor_batch_gpu)
@@ -39,6 +39,14 @@
 #include "srsran/phy/upper/downlink_processor.h"
 #include "srsran/phy/upper/signal_processors/ptrs/ptrs_pdsch_generator.h"
 #include "srsran/phy/upper/uplink_processor.h"
+#include "srsran/phy/upper/upper_phy_factories.h"
+#include "srsran/phy/upper/channel_processors/pdcch/factories.h"
+#include "srsran/phy/upper/channel_processors/pucch/factories.h"
+#include "srsran/phy/upper/channel_processors/ssb/factories.h"
+#include "srsran/phy/upper/signal_processors/prs/factories.h"
+#include "srsran/phy/upper/signal_processors/ptrs/ptrs_pdsch_generator_factory.h"
+#include "srsran/phy/upper/signal_processors/signal_processor_factories.h"
+#include "srsran/phy/upper/signal_processors/srs/srs_estimator_factory.h"
 #include "srsran/support/executors/task_executor.h"
 
 #include <memory>
@@ -170,5 +178,101 @@ std::unique_ptr<downlink_processor_base> create_downlink_processor_batch_gpu(std
                                                                              std::shared_ptr<pdsch_slot_batch> batch,
                                                                              task_executor&                    executor);
 
+/// The device's shared PUSCH service (one per GPU and process): the first call for a device creates it with `config`,
+/// later calls for the same device return it while any batch still holds it (their `config` is then ignored).
+std::shared_ptr<pusch_gpu_service> get_pusch_gpu_service(const pusch_service_configuration& config);
+
 } // namespace gpu
+
+// ---------------------------------------------------------------------------------------------------------------------
+// Row b8: the slot-batched GPU processors behind the reference's factory interfaces (integration/
+// upper_phy_factories_gpu.cpp). upper_phy_factories.cpp builds its slot processors only through
+// uplink_processor_factory::create (upper_phy_factories.h:59-83) and downlink_processor_factory::create (:114-128), and
+// its PUSCH / PDSCH processors through pusch_processor_factory / pdsch_processor_factory (pusch/factories.h:101,
+// pdsch/factories.h): a maintainer selects the GPU by substituting these factories at upper_phy_factories.cpp:596
+// (PUSCH processor), :680 (uplink processor), :1014 (PDSCH processor) and :1100 (downlink processor); see INTEGRATION.md.
+// ---------------------------------------------------------------------------------------------------------------------
+
+/// create_pusch_processor_factory_sw's configuration (pusch/factories.h:109-120) with the estimator and demodulator on
+/// the GPU: the options replace the two factories.
+struct pusch_processor_factory_gpu_configuration {
+  int                                           device = 0;
+  gpu::pusch_estimator_options                  estimator;
+  gpu::pusch_demodulator_options                demodulator;
+  std::shared_ptr<ulsch_demultiplex_factory>    demux_factory;
+  std::shared_ptr<pusch_decoder_factory>        decoder_factory;  ///< e.g. create_pusch_decoder_factory_hw over the GPU HAL
+  std::shared_ptr<uci_decoder_factory>          uci_dec_factory;
+  channel_estimate::channel_estimate_dimensions ch_estimate_dimensions;
+  unsigned                                      dec_nof_iterations         = 10;
+  bool                                          dec_enable_early_stop      = true;
+  unsigned                                      max_nof_concurrent_threads = 1;
+  channel_state_information::sinr_type csi_sinr_calc_method = channel_state_information::sinr_type::channel_estimator;
+};
+
+/// The replacement of create_pusch_processor_factory_sw (upper_phy_factories.cpp:596): the reference's
+/// pusch_processor_impl over the GPU DM-RS estimator and demodulator (row b3); validator: the reference's, with the
+/// configured channel-estimate dimensions.
+std::shared_ptr<pusch_processor_factory>
+create_pusch_processor_factory_gpu(const pusch_processor_factory_gpu_configuration& config);
+
+/// The replacement of create_pdsch_processor_factory_sw (upper_phy_factories.cpp:1014): the reference's
+/// pdsch_processor_impl over the given encoder (e.g. create_pdsch_encoder_factory_hw over the GPU HAL) and the GPU
+/// modulator and DM-RS processor.
+std::shared_ptr<pdsch_processor_factory>
+create_pdsch_processor_factory_gpu(int                                           device,
+                                   std::shared_ptr<pdsch_encoder_factory>        encoder_factory,
+                                   std::shared_ptr<ptrs_pdsch_generator_factory> ptrs_factory);
+
+/// The uplink_processor_base_factory arguments (upper_phy_factories.cpp:52-70, :672-686) plus the GPU slot batch.
+struct uplink_processor_factory_gpu_configuration {
+  std::shared_ptr<pucch_processor_factory> pucch_factory;
+  std::shared_ptr<prach_detector_factory>  prach_factory;
+  std::shared_ptr<srs_estimator_factory>   srs_factory;
+  std::shared_ptr<resource_grid_factory>   grid_factory;
+  /// The PUSCH processors for the PDUs a slot batch does not cover (UCI only, more than four layers or rx ports,
+  /// non-identity rx port lists, extended CP); its validator is the factory's PUSCH validator.
+  std::shared_ptr<pusch_processor_factory> pusch_factory;
+  /// The reference's UCI decoder factory (host part of the result replay).
+  std::shared_ptr<uci_decoder_factory> uci_dec_factory;
+  /// upper_phy_config's executors (upper_phy_factories.cpp:672-675); the PUSCH executor runs the slot batches' jobs.
+  task_executor* pucch_executor = nullptr;
+  task_executor* pusch_executor = nullptr;
+  task_executor* srs_executor   = nullptr;
+  task_executor* prach_executor = nullptr;
+  /// The slot batches (device, estimator / demodulator options, HARQ arena size = the rx buffer pool's codeblocks,
+  /// iterations, synchronous / asynchronous, multi-GPU shards).
+  gpu::pusch_batch_configuration batch;
+  /// The GPU service the batches submit to; nullptr: gpu::get_pusch_gpu_service(service_config) - one per device,
+  /// shared by every uplink processor of every factory on that device (the cross-sector aggregation).
+  std::shared_ptr<gpu::pusch_gpu_service> service;
+  gpu::pusch_service_configuration        service_config;
+};
+
+/// The replacement of uplink_processor_base_factory (upper_phy_factories.cpp:680): create() builds the reference's
+/// uplink_processor_impl over a GPU slot batch and wraps it so that each slot's PUSCH PDUs run as one GPU job. Uplink
+/// processors created with the same rx_buffer_pool (one sector, as create_ul_processor_pool builds them) share one HBM
+/// HARQ arena. create_pdu_validator() returns the reference's uplink_processor_validator_impl over the channel
+/// factories' validators.
+std::shared_ptr<uplink_processor_factory>
+create_uplink_processor_factory_gpu(const uplink_processor_factory_gpu_configuration& config);
+
+/// The downlink_processor_single_executor_factory arguments (upper_phy_factories.cpp:153-170, :1100) plus the GPU
+/// device and the PT-RS generator the PDSCH slot batch maps on the host.
+struct downlink_processor_factory_gpu_configuration {
+  int                                           device = 0;
+  std::shared_ptr<pdcch_processor_factory>      pdcch_factory;
+  /// The PDSCH processors for the PDUs a slot batch does not cover (two codewords); its validator is the factory's.
+  std::shared_ptr<pdsch_processor_factory>      pdsch_factory;
+  std::shared_ptr<ssb_processor_factory>        ssb_factory;
+  std::shared_ptr<nzp_csi_rs_generator_factory> nzp_csi_rs_factory;
+  std::shared_ptr<prs_generator_factory>        prs_factory;
+  std::shared_ptr<ptrs_pdsch_generator_factory> ptrs_factory;
+};
+
+/// The replacement of downlink_processor_single_executor_factory (upper_phy_factories.cpp:1100): create() builds the
+/// reference's downlink_processor_single_executor_impl over a GPU PDSCH slot batch on `config.executor`, wrapped so that
+/// the slot's PDSCHs run as one GPU launch at finish_processing_pdus.
+std::shared_ptr<downlink_processor_factory>
+create_downlink_processor_factory_gpu(const downlink_processor_factory_gpu_configuration& config);
+
 } // namespace srsran

@@ -48,6 +48,7 @@ SRCS=(
   "$REF/lib/instrumentation/traces/du_traces.cpp"
   "$ROOT/integration/upper_phy_gpu.cpp"
   "$ROOT/integration/pusch_batch_gpu.cpp"
+  "$ROOT/integration/upper_phy_factories_gpu.cpp"
   "$U/uplink_processor_impl.cpp"
   "$U/downlink_processor_single_executor_impl.cpp"
   "$U/rx_buffer_pool_impl.cpp"
@@ -58,6 +59,7 @@ SRCS=(
   "$REF/lib/srslog/formatters/json_formatter.cpp"
   "$HERE/ref/ref_chain.cpp"
   "$HERE/ref/ref_lower.cpp"
+  "$HERE/ref/ref_factory_defaults.cpp"
 )
 OBJS=()
 pids=()

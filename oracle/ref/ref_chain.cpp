@@ -55,6 +55,8 @@
 #include "lib/phy/upper/channel_processors/pusch/pusch_decoder_impl.h"
 #include "lib/phy/upper/channel_processors/pusch/pusch_demodulator_impl.h"
 #include "lib/phy/upper/channel_processors/pusch/pusch_processor_impl.h"
+#include "lib/phy/upper/channel_processors/pusch/pusch_processor_validator_impl.h"
+#include "lib/phy/upper/channel_processors/pdsch/pdsch_processor_validator_impl.h"
 #include "lib/phy/upper/channel_processors/pusch/ulsch_demultiplex_impl.h"
 #include "lib/phy/upper/channel_processors/uci/uci_decoder_impl.h"
 #include "lib/phy/upper/equalization/channel_equalizer_generic_impl.h"
@@ -78,6 +80,7 @@
 #include "srsran/phy/lower/processors/uplink/puxch/puxch_processor_notifier.h"
 #include "srsran/phy/lower/processors/uplink/puxch/puxch_processor_request_handler.h"
 #include "srsran/phy/upper/rx_buffer_pool.h"
+#include "srsran/phy/upper/uplink_pdu_validator.h"
 #include "srsran/phy/upper/upper_phy_rg_gateway.h"
 #include "srsran/phy/upper/upper_phy_rx_results_notifier.h"
 #include "srsran/phy/upper/channel_processors/pdcch/pdcch_processor.h"
@@ -1127,6 +1130,161 @@ public:
   std::unique_ptr<uci_decoder> create() override { return cpu_uci_decoder(); }
 };
 
+// Factories of the stub channel processors (row b8: the GPU slot-processor factories take the channel factories of the
+// channels they do not batch, as upper_phy_factories.cpp passes its PUCCH / PRACH / SRS / PDCCH / SSB / CSI-RS / PRS
+// factories). Their validators accept every configuration.
+template <typename V, typename... C>
+class accept_all;
+template <typename V, typename C>
+class accept_all<V, C> : public V
+{
+public:
+  error_type<std::string> is_valid(const C&) const override { return default_success_t(); }
+};
+class accept_all_pucch : public pucch_pdu_validator
+{
+public:
+  error_type<std::string> is_valid(const pucch_processor::format0_configuration&) const override
+  {
+    return default_success_t();
+  }
+  error_type<std::string> is_valid(const pucch_processor::format1_configuration&) const override
+  {
+    return default_success_t();
+  }
+  error_type<std::string> is_valid(const pucch_processor::format2_configuration&) const override
+  {
+    return default_success_t();
+  }
+  error_type<std::string> is_valid(const pucch_processor::format3_configuration&) const override
+  {
+    return default_success_t();
+  }
+  error_type<std::string> is_valid(const pucch_processor::format4_configuration&) const override
+  {
+    return default_success_t();
+  }
+};
+class stub_prach_factory : public prach_detector_factory
+{
+public:
+  std::unique_ptr<prach_detector> create() override { return std::make_unique<stub_prach>(); }
+  std::unique_ptr<prach_detector_validator> create_validator() override
+  {
+    return std::make_unique<accept_all<prach_detector_validator, prach_detector::configuration>>();
+  }
+};
+class stub_pucch_factory : public pucch_processor_factory
+{
+public:
+  std::unique_ptr<pucch_processor>     create() override { return std::make_unique<stub_pucch>(); }
+  std::unique_ptr<pucch_pdu_validator> create_validator() override { return std::make_unique<accept_all_pucch>(); }
+};
+class stub_srs_factory : public srs_estimator_factory
+{
+public:
+  std::unique_ptr<srs_estimator> create() override { return std::make_unique<stub_srs>(); }
+  std::unique_ptr<srs_estimator_configuration_validator> create_validator() override
+  {
+    return std::make_unique<accept_all<srs_estimator_configuration_validator, srs_estimator_configuration>>();
+  }
+};
+class stub_pdcch_factory : public pdcch_processor_factory
+{
+public:
+  std::unique_ptr<pdcch_processor>     create() override { return std::make_unique<stub_pdcch>(); }
+  std::unique_ptr<pdcch_pdu_validator> create_validator() override
+  {
+    return std::make_unique<accept_all<pdcch_pdu_validator, pdcch_processor::pdu_t>>();
+  }
+};
+class stub_ssb_factory : public ssb_processor_factory
+{
+public:
+  std::unique_ptr<ssb_processor>     create() override { return std::make_unique<stub_ssb>(); }
+  std::unique_ptr<ssb_pdu_validator> create_validator() override
+  {
+    return std::make_unique<accept_all<ssb_pdu_validator, ssb_processor::pdu_t>>();
+  }
+};
+class stub_csi_rs_factory : public nzp_csi_rs_generator_factory
+{
+public:
+  std::unique_ptr<nzp_csi_rs_generator> create() override { return std::make_unique<stub_csi_rs>(); }
+  std::unique_ptr<nzp_csi_rs_configuration_validator> create_validator() override
+  {
+    return std::make_unique<accept_all<nzp_csi_rs_configuration_validator, nzp_csi_rs_generator::config_t>>();
+  }
+};
+class stub_prs_factory : public prs_generator_factory
+{
+public:
+  std::unique_ptr<prs_generator>           create() override { return std::make_unique<stub_prs>(); }
+  std::unique_ptr<prs_generator_validator> create_validator() override
+  {
+    return std::make_unique<accept_all<prs_generator_validator, prs_generator_configuration>>();
+  }
+};
+class grid_factory_ref : public resource_grid_factory
+{
+public:
+  std::unique_ptr<resource_grid> create(unsigned nof_ports, unsigned nof_symbols, unsigned nof_subc) override
+  {
+    return std::make_unique<resource_grid_impl>(nof_ports, nof_symbols, nof_subc);
+  }
+};
+/// The reference's CPU PUSCH decoder (pusch_decoder_impl over the AVX2 dematcher and the host's fastest LDPC decoder).
+class cpu_pusch_decoder_factory : public pusch_decoder_factory
+{
+public:
+  std::unique_ptr<pusch_decoder> create() override { return cpu_pusch_decoder(); }
+};
+/// The reference's pdsch_encoder_hw_impl over the GPU PDSCH-encoder accelerator (row b2).
+class gpu_pdsch_encoder_factory : public pdsch_encoder_factory
+{
+public:
+  explicit gpu_pdsch_encoder_factory(int device_) : device(device_) {}
+  std::unique_ptr<pdsch_encoder> create() override
+  {
+    auto seg_crc = sch_crc<ldpc_segmenter_tx_impl::sch_crc>();
+    auto crcs    = sch_crc<pdsch_encoder_hw_impl::sch_crc>();
+    return std::make_unique<pdsch_encoder_hw_impl>(crcs,
+                                                   std::make_unique<ldpc_segmenter_tx_impl>(seg_crc),
+                                                   hal::create_hw_accelerator_pdsch_enc_factory_gpu(device)->create());
+  }
+
+private:
+  int device;
+};
+class ptrs_factory_ref : public ptrs_pdsch_generator_factory
+{
+public:
+  std::unique_ptr<ptrs_pdsch_generator> create() override
+  {
+    return std::make_unique<ptrs_pdsch_generator_generic_impl>(std::make_unique<pseudo_random_generator_impl>(),
+                                                               cpu_mapper());
+  }
+};
+
+/// The GPU PUSCH processor factory of the fallback path (row b8): the reference's pusch_processor_impl over the GPU
+/// estimator and demodulator (filter smoothing, CFO compensation, time strategy td; ZF with EVM and post-equalisation
+/// SINR) and the reference's CPU decoder - what new_pusch_processor(device, 1, ...) assembles by hand.
+std::shared_ptr<pusch_processor_factory>
+gpu_pusch_factory(int device, port_channel_estimator_td_interpolation_strategy td, unsigned max_iter)
+{
+  pusch_processor_factory_gpu_configuration pc;
+  pc.device      = device;
+  pc.estimator   = gpu::make_pusch_estimator_options(port_channel_estimator_fd_smoothing_strategy::filter, td, true);
+  pc.demux_factory          = std::make_shared<demux_factory_ref>();
+  pc.decoder_factory        = std::make_shared<cpu_pusch_decoder_factory>();
+  pc.uci_dec_factory        = std::make_shared<uci_factory_ref>();
+  pc.ch_estimate_dimensions = channel_estimate::channel_estimate_dimensions{MAX_RB, MAX_NSYMB_PER_SLOT, 4, 4};
+  pc.dec_nof_iterations     = max_iter;
+  pc.dec_enable_early_stop  = true;
+  pc.csi_sinr_calc_method   = channel_state_information::sinr_type::post_equalization;
+  return create_pusch_processor_factory_gpu(pc);
+}
+
 /// PUSCH results as the upper PHY's notifier receives them, in arrival order.
 struct ul_record {
   int                  rnti, harq_id, crc_ok, nof_cbs, ldpc_obs, ldpc_min, ldpc_max;
@@ -1231,6 +1389,7 @@ struct ul_harness {
   rx_buffer_pool_controller*                 pool = nullptr;
   ul_results_recorder                        own_notifier;
   ul_results_recorder*                       notifier = &own_notifier;
+  std::shared_ptr<uplink_processor_factory>  factory;  ///< GPU variants: the factory that made `proc` (row b8)
   std::unique_ptr<uplink_processor>          proc;
 };
 
@@ -1251,9 +1410,47 @@ std::unique_ptr<rx_buffer_pool_controller> ul_pool()
 /// (du_low builds several uplink processors per sector over one pool). The GPU service is shared by every sector.
 struct ul_sector {
   std::unique_ptr<rx_buffer_pool_controller> pool;
-  std::shared_ptr<gpu::pusch_harq_arena>     arena;
   ul_results_recorder                        notifier;
 };
+
+/// The GPU uplink processor factory of the tests (row b8): stub PUCCH / PRACH / SRS, the reference's resource grid,
+/// the GPU per-PDU PUSCH processor factory as the fallback, the reference's UCI decoder, inline executors.
+/// service: nullptr for the device's shared service (gpu::get_pusch_gpu_service); multi: 1 three UE shards on the
+/// device with the peer-copy transport, 2 one shard through RCCL at world size 1 (row b7).
+std::shared_ptr<uplink_processor_factory> ul_factory(int                                              device,
+                                                     port_channel_estimator_td_interpolation_strategy td,
+                                                     unsigned                                         max_iter,
+                                                     std::shared_ptr<gpu::pusch_gpu_service>          service,
+                                                     bool                                             asynchronous,
+                                                     int                                              multi)
+{
+  uplink_processor_factory_gpu_configuration fc;
+  fc.pucch_factory   = std::make_shared<stub_pucch_factory>();
+  fc.prach_factory   = std::make_shared<stub_prach_factory>();
+  fc.srs_factory     = std::make_shared<stub_srs_factory>();
+  fc.grid_factory    = std::make_shared<grid_factory_ref>();
+  fc.pusch_factory   = gpu_pusch_factory(device, td, max_iter);
+  fc.uci_dec_factory = std::make_shared<uci_factory_ref>();
+  fc.pucch_executor  = &test_executor();
+  fc.pusch_executor  = &test_executor();
+  fc.srs_executor    = &test_executor();
+  fc.prach_executor  = &test_executor();
+  gpu::pusch_batch_configuration& bc = fc.batch;
+  bc.device              = device;
+  bc.estimator = gpu::make_pusch_estimator_options(port_channel_estimator_fd_smoothing_strategy::filter, td, true);
+  bc.max_cb_ids          = UL_POOL_CODEBLOCKS;
+  bc.nof_ldpc_iterations = max_iter;
+  bc.asynchronous        = asynchronous;
+  if (multi == 1) {
+    bc.devices = {device, device, device};
+  } else if (multi == 2) {
+    bc.devices   = {device};
+    bc.transport = gpu::create_pusch_rccl_transport({device});
+  }
+  fc.service                = std::move(service);
+  fc.service_config.device  = device;
+  return create_uplink_processor_factory_gpu(fc);
+}
 
 /// variant: 0 the reference's CPU PUSCH processor, 1 the GPU slot batch; + 2 with the "interpolate" time strategy of
 /// the estimator (the batch then keeps per-symbol estimates) instead of du_low's "average". sector / service /
@@ -1284,40 +1481,11 @@ ul_harness* ul_create(int                                     device,
     h->pool     = h->own_pool.get();
   }
 
-  std::unique_ptr<pusch_processor> pusch;
-  std::shared_ptr<gpu::pusch_slot_batch> batch;
   if (variant == 0) {
-    pusch = new_pusch_processor(device, 0, td, max_iter, true, {});
-  } else {
-    gpu::pusch_batch_configuration bc;
-    bc.device              = device;
-    bc.estimator = gpu::make_pusch_estimator_options(port_channel_estimator_fd_smoothing_strategy::filter, td, true);
-    bc.max_cb_ids          = UL_POOL_CODEBLOCKS;
-    bc.nof_ldpc_iterations = max_iter;
-    bc.asynchronous        = asynchronous;
-    if (multi == 1) {
-      // Row b7 on one GPU: three UE shards on device 0 (own launchers, HARQ arenas, grid copies), peer-copy gather.
-      bc.devices = {device, device, device};
-    } else if (multi == 2) {
-      // Row b7 through RCCL at world size 1: one shard, the gather an ncclSend / ncclRecv pair to itself.
-      bc.devices   = {device};
-      bc.transport = gpu::create_pusch_rccl_transport({device});
-    }
-    // PDUs outside the batch: the reference processor over the GPU estimator / demodulator (row b3).
-    auto fallback = new_pusch_processor(device, 1, td, max_iter, true, {});
-    std::shared_ptr<gpu::pusch_harq_arena> arena =
-        sector != nullptr ? sector->arena : gpu::create_pusch_harq_arena(device, bc.max_cb_ids);
-    batch = gpu::create_pusch_slot_batch(bc, arena, std::make_shared<demux_factory_ref>(),
-                                         std::make_shared<uci_factory_ref>(), std::move(fallback), service);
-    pusch = gpu::create_pusch_processor_batch_gpu(batch);
-  }
-  uplink_processor_impl::task_executor_collection execs{test_executor(),
-                                                        variant == 0 ? static_cast<task_executor&>(test_executor())
-                                                                     : gpu::pusch_inline_executor(),
-                                                        test_executor(),
-                                                        test_executor()};
-  auto impl = std::make_unique<uplink_processor_impl>(std::make_unique<stub_prach>(),
-                                                      std::move(pusch),
+    uplink_processor_impl::task_executor_collection execs{
+        test_executor(), test_executor(), test_executor(), test_executor()};
+    h->proc = std::make_unique<uplink_processor_impl>(std::make_unique<stub_prach>(),
+                                                      new_pusch_processor(device, 0, td, max_iter, true, {}),
                                                       std::make_unique<stub_pucch>(),
                                                       std::make_unique<stub_srs>(),
                                                       std::make_unique<resource_grid_impl>(P, 14, h->nsc),
@@ -1326,11 +1494,13 @@ ul_harness* ul_create(int                                     device,
                                                       *h->notifier,
                                                       grid_prb,
                                                       4);
-  if (variant == 0) {
-    h->proc = std::move(impl);
-  } else {
-    h->proc = gpu::create_uplink_processor_batch_gpu(std::move(impl), batch, test_executor());
+    return h;
   }
+  // Row b8: the GPU uplink processor only through the uplink_processor_factory interface, as upper_phy_factories.cpp
+  // would obtain it (create_ul_processor_pool -> factory.create(config)).
+  h->factory = ul_factory(device, td, max_iter, service, asynchronous, multi);
+  uplink_processor_config uc{*h->notifier, h->pool->get_pool(), P, grid_prb, 4};
+  h->proc = h->factory->create(uc);
   return h;
 }
 
@@ -1376,9 +1546,24 @@ struct dl_harness {
   unsigned                                  P, nsc;
   grid_capture                              gateway;
   std::unique_ptr<one_grid_pool>            pool;
-  std::unique_ptr<gpu::pdsch_batch_executor> exec;
+  std::shared_ptr<downlink_processor_factory> factory;  ///< GPU variant: the factory that made `proc` (row b8)
   std::unique_ptr<downlink_processor_base>  proc;
 };
+
+/// The GPU downlink processor factory of the tests (row b8).
+std::shared_ptr<downlink_processor_factory> dl_factory(int device)
+{
+  downlink_processor_factory_gpu_configuration fc;
+  fc.device             = device;
+  fc.pdcch_factory      = std::make_shared<stub_pdcch_factory>();
+  fc.pdsch_factory      = create_pdsch_processor_factory_gpu(device, std::make_shared<gpu_pdsch_encoder_factory>(device),
+                                                        std::make_shared<ptrs_factory_ref>());
+  fc.ssb_factory        = std::make_shared<stub_ssb_factory>();
+  fc.nzp_csi_rs_factory = std::make_shared<stub_csi_rs_factory>();
+  fc.prs_factory        = std::make_shared<stub_prs_factory>();
+  fc.ptrs_factory       = std::make_shared<ptrs_factory_ref>();
+  return create_downlink_processor_factory_gpu(fc);
+}
 
 dl_harness* dl_create(int device, int variant, unsigned P, unsigned grid_prb)
 {
@@ -1386,34 +1571,25 @@ dl_harness* dl_create(int device, int variant, unsigned P, unsigned grid_prb)
   h->P    = P;
   h->nsc  = 12 * grid_prb;
   h->pool = std::make_unique<one_grid_pool>(P, h->nsc);
-  std::unique_ptr<pdsch_processor>        pdsch;
-  std::shared_ptr<gpu::pdsch_slot_batch> batch;
-  task_executor*                          exec = &test_executor();
   if (variant == 0) {
-    pdsch = new_pdsch_processor(device, 0);
-  } else {
-    batch = gpu::create_pdsch_slot_batch(
-        device,
-        std::make_unique<ptrs_pdsch_generator_generic_impl>(std::make_unique<pseudo_random_generator_impl>(),
-                                                            cpu_mapper()),
-        new_pdsch_processor(device, 1));
-    pdsch   = gpu::create_pdsch_processor_batch_gpu(batch);
-    h->exec = std::make_unique<gpu::pdsch_batch_executor>(test_executor());
-    exec    = h->exec.get();
+    h->proc = std::make_unique<downlink_processor_single_executor_impl>(h->gateway,
+                                                                        std::make_unique<stub_pdcch>(),
+                                                                        new_pdsch_processor(device, 0),
+                                                                        std::make_unique<stub_ssb>(),
+                                                                        std::make_unique<stub_csi_rs>(),
+                                                                        std::make_unique<stub_prs>(),
+                                                                        test_executor(),
+                                                                        srslog::fetch_basic_logger("PHY", true));
+    return h;
   }
-  auto impl = std::make_unique<downlink_processor_single_executor_impl>(h->gateway,
-                                                                       std::make_unique<stub_pdcch>(),
-                                                                       std::move(pdsch),
-                                                                       std::make_unique<stub_ssb>(),
-                                                                       std::make_unique<stub_csi_rs>(),
-                                                                       std::make_unique<stub_prs>(),
-                                                                       *exec,
-                                                                       srslog::fetch_basic_logger("PHY", true));
-  if (variant == 0) {
-    h->proc = std::move(impl);
-  } else {
-    h->proc = gpu::create_downlink_processor_batch_gpu(std::move(impl), batch, test_executor());
-  }
+  // Row b8: the GPU downlink processor only through the downlink_processor_factory interface; the PDSCHs the slot
+  // batch does not cover go to the GPU per-PDU PDSCH processor factory (HAL encoder, GPU modulator and DM-RS).
+  h->factory = dl_factory(device);
+  downlink_processor_config dc;
+  dc.id       = 0;
+  dc.gateway  = &h->gateway;
+  dc.executor = &test_executor();
+  h->proc     = h->factory->create(dc);
   return h;
 }
 
@@ -1501,6 +1677,44 @@ int chain_ul_slot(void*               p,
       std::memcpy(tb_out + i * tb_stride, r.payload.data(), std::min<size_t>(r.payload.size(), tb_stride));
     }
     return static_cast<int>(recs.size());
+  });
+}
+
+/// Row b8: the PDU validators the GPU factories return (create_pdu_validator), against the reference's own PUSCH / PDSCH
+/// validators (pusch_processor_validator_impl with the upper PHY's channel-estimate dimensions,
+/// pdsch_processor_validator_impl). direction 0: PUSCH PDUs through the uplink factory's validator, 1: PDSCH PDUs (with
+/// `weights`, nof_ports x nof_layers complex per PDU) through the downlink factory's. out[i]: bit 0 the factory's
+/// validator accepts PDU i, bit 1 the reference's does, bit 2 their messages differ. Returns 0.
+int chain_factory_validate(int device, int direction, int nof_pdus, const chain_params* pdus, const float* weights,
+                           int* out)
+{
+  return guarded("chain_factory_validate", [&] {
+    if (direction == 0) {
+      std::unique_ptr<uplink_pdu_validator> v =
+          ul_factory(device, port_channel_estimator_td_interpolation_strategy::average, 6, nullptr, false, 0)
+              ->create_pdu_validator();
+      pusch_processor_validator_impl ref(channel_estimate::channel_estimate_dimensions{MAX_RB, MAX_NSYMB_PER_SLOT, 4, 4});
+      for (int i = 0; i != nof_pdus; ++i) {
+        const pusch_processor::pdu_t pdu = make_pusch_pdu(pdus[i]);
+        const auto                   a   = v->is_valid(pdu);
+        const auto                   b   = ref.is_valid(pdu);
+        out[i] = (a.has_value() ? 1 : 0) | (b.has_value() ? 2 : 0) |
+                 (!a.has_value() && !b.has_value() && a.error() != b.error() ? 4 : 0);
+      }
+    } else {
+      std::unique_ptr<downlink_pdu_validator> v = dl_factory(device)->create_pdu_validator();
+      pdsch_processor_validator_impl          ref;
+      const float*                            w = weights;
+      for (int i = 0; i != nof_pdus; ++i) {
+        const pdsch_processor::pdu_t pdu = make_pdsch_pdu(pdus[i], w);
+        w += 2 * pdus[i].nof_ports * pdus[i].nof_layers;
+        const auto a = v->is_valid(pdu);
+        const auto b = ref.is_valid(pdu);
+        out[i] = (a.has_value() ? 1 : 0) | (b.has_value() ? 2 : 0) |
+                 (!a.has_value() && !b.has_value() && a.error() != b.error() ? 4 : 0);
+      }
+    }
+    return 0;
   });
 }
 
@@ -1609,13 +1823,21 @@ int chain_ul_bench(int                 device,
         if (shared) {
           sectors[t]                      = std::make_unique<ul_sector>();
           sectors[t]->pool                = ul_pool();
-          sectors[t]->arena               = gpu::create_pusch_harq_arena(device, UL_POOL_CODEBLOCKS);
           sectors[t]->notifier.count_only = true;
           for (unsigned r = 0; r != UL_RING; ++r) {
             hs[t].push_back(ul_create(device, 1, nof_ports, grid_prb, 2, sectors[t].get(), service, true));
           }
         } else {
-          hs[t].push_back(ul_create(device, variant, nof_ports, grid_prb, 2));
+          // One synchronous uplink processor per thread on a private service (the per-thread batch of round 4).
+          std::shared_ptr<gpu::pusch_gpu_service> own;
+          if (variant == 1) {
+            gpu::pusch_service_configuration sc;
+            sc.device          = device;
+            sc.nof_launch_sets = 2;
+            sc.max_grids       = 4;
+            own                = gpu::create_pusch_gpu_service(sc);
+          }
+          hs[t].push_back(ul_create(device, variant, nof_ports, grid_prb, 2, nullptr, own));
           hs[t].back()->notifier->count_only = true;
         }
       });
@@ -1862,7 +2084,6 @@ int chain_du_low_ul(int                 device,
         st[k]                           = std::make_unique<sector_state>();
         st[k]->sec                      = std::make_unique<ul_sector>();
         st[k]->sec->pool                = ul_pool();
-        st[k]->sec->arena               = gpu::create_pusch_harq_arena(device, UL_POOL_CODEBLOCKS);
         st[k]->sec->notifier.count_only = true;
         for (unsigned r = 0; r != UL_RING; ++r) {
           st[k]->ring.push_back(ul_create(device, 1, nof_ports, grid_prb, 2, st[k]->sec.get(), service, true));

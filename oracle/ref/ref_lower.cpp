@@ -199,6 +199,30 @@ std::unique_ptr<puxch_processor> make_puxch(int                                 
 }
 
 /// A grid pool holding the scenario's DL grids (port_mask bit p clear: port p stays empty).
+/// Variants 4 and 5: the GPU processor of a two-sector group in which another sector registered first (the group takes
+/// its launch parameters and buffer sizes from the first sector's plans). 4: that sector was removed again (its processor
+/// and plans destroyed) before the tested one runs; 5: it stays, with the other cyclic prefix (at 60 kHz: the same
+/// slot length, 12 instead of 14 symbols: a normal-CP sector has more jobs per slot than the group's job table holds per
+/// entry and must run alone). The first sector is returned (nullptr for variant 4).
+template <typename Proc, typename Make>
+std::unique_ptr<Proc> group_prelude(int variant, const scenario& sc, double center_freq_hz,
+                                    std::shared_ptr<lower_phy_sector_group>& group, Make make)
+{
+  lower_phy_group_configuration gc;
+  gc.device      = 0;
+  gc.nof_sectors = 2;
+  group          = create_lower_phy_sector_group(gc);
+  scenario other = sc;
+  if (variant == 5) {
+    other.cp = sc.cp == cyclic_prefix::NORMAL ? cyclic_prefix::EXTENDED : cyclic_prefix::NORMAL;
+  }
+  std::unique_ptr<Proc> first = make(other, center_freq_hz + 1e7);
+  if (variant == 4) {
+    first.reset();
+  }
+  return first;
+}
+
 void fill_pool(harness_pool& pool, const scenario& sc, int nof_grids, const uint16_t* grids, const uint32_t* port_mask)
 {
   const unsigned nsymb = sc.nsymb();
@@ -406,7 +430,7 @@ private:
 
 extern "C" {
 
-/// PDxCH scenario. grids: nof_grids x ports x nsymb x nsc bf16 pairs; port_mask[g]: bit p set = port p of grid g is
+/// PDxCH scenario (variants 0-2 as make_pdxch, 4-5 as group_prelude). grids: nof_grids x ports x nsymb x nsc bf16 pairs; port_mask[g]: bit p set = port p of grid g is
 /// written (the others stay empty). events: nof_events x {kind, system slot, a, b}: kind 0 = handle_request(grid a),
 /// kind 1 = process_symbol for symbols [a, b) of the slot. Outputs, in event order: the samples of every processed
 /// symbol and port (sentinel 1e30 where the processor leaves the buffer untouched), one return flag per symbol, the
@@ -435,7 +459,14 @@ long ref_lower_pdxch_run(int             variant,
                     nof_ports};
   harness_pool   pool(nof_grids, nof_ports, sc.nsymb(), sc.nsc());
   fill_pool(pool, sc, nof_grids, grids, port_mask);
-  std::unique_ptr<pdxch_processor> proc = make_pdxch(variant, sc, center_freq_hz, nullptr);
+  std::shared_ptr<lower_phy_sector_group> group;
+  std::unique_ptr<pdxch_processor>        first;
+  if (variant >= 4) {
+    first = group_prelude<pdxch_processor>(variant, sc, center_freq_hz, group, [&](const scenario& o, double f) {
+      return make_pdxch(3, o, f, group);
+    });
+  }
+  std::unique_ptr<pdxch_processor> proc = make_pdxch(variant >= 4 ? 3 : variant, sc, center_freq_hz, group);
   pdxch_recorder                   rec;
   proc->connect(rec);
   const long pos = run_pdxch_script(*proc, pool, sc, nof_events, events, samples_out, samples_cap, processed_out);
@@ -471,7 +502,15 @@ int ref_lower_puxch_run(int          variant,
   const scenario sc{numerology,        bw_rb,    dft_size, cp_extended ? cyclic_prefix::EXTENDED : cyclic_prefix::NORMAL,
                     dft_window_offset, nof_ports};
   harness_pool   pool(nof_grids, nof_ports, sc.nsymb(), sc.nsc());
-  std::unique_ptr<puxch_processor> proc = make_puxch(variant, max_in_flight, sc, center_freq_hz, nullptr);
+  std::shared_ptr<lower_phy_sector_group> group;
+  std::unique_ptr<puxch_processor>        first;
+  if (variant >= 4) {
+    first = group_prelude<puxch_processor>(variant, sc, center_freq_hz, group, [&](const scenario& o, double f) {
+      return make_puxch(3, max_in_flight, o, f, group);
+    });
+  }
+  std::unique_ptr<puxch_processor> proc =
+      make_puxch(variant >= 4 ? 3 : variant, max_in_flight, sc, center_freq_hz, group);
   puxch_recorder                   rec;
   proc->connect(rec);
   run_puxch_script(*proc, pool, sc, nof_events, events, samples_in, processed_out);

@@ -190,7 +190,14 @@ class CodeblockShard:
     each) and CRC flags into the root's slot-wide buffers (one gather), where srsgpu_pusch_decoder_plan_assemble joins
     them into TBs and checks the TB CRCs (pusch_decoder_impl.cpp:386); `return_flags` scatters the root's final flags
     back, so a TB CRC mismatch clears the owners' codeblock flags exactly as the reference resets them for the
-    retransmission (:423). Buffers are allocated once; copies and collectives run on the current stream.
+    retransmission (:423). Buffers and the per-rank index tensors are allocated once; copies and collectives run on the
+    current stream, one indexed copy per rank on the root.
+
+    With `keys`, a rank's local codeblock positions change from slot to slot, so its CRC flags - the HARQ context that
+    makes the reference skip a codeblock already decoded in an earlier transmission (pusch_decoder_impl.cpp:208,
+    rx_buffer.h `get_codeblocks_crc`) - belong to the key, not the position: `return_flags(..., harq_flags=t)` also
+    stores them into `t[key]` (a per-rank tensor indexed by HARQ key, like the HBM HARQ arena), and
+    `local_flags(t)` reads this slot's local codeblocks' flags back in local order.
     """
 
     def __init__(self, cbs: Sequence[tuple], device: torch.device, root: int = 0,
@@ -229,6 +236,13 @@ class CodeblockShard:
         for i in self.members[self.rank]:
             self.local_cbs.append((pos, self.cbs[i][1]))
             pos += self.cbs[i][1]
+        self.keys = None if keys is None else [int(k) for k in keys]
+        #: this rank's codeblocks' HARQ keys in local order (keyed flags), on the device
+        self._local_keys = (torch.tensor([self.keys[i] for i in self.members[self.rank]], dtype=torch.long,
+                                         device=device) if self.keys is not None else None)
+        #: root: per rank, the slot positions of its codeblocks (indexed copies instead of one copy per codeblock)
+        self._idx = ([torch.tensor(m, dtype=torch.long, device=device) for m in self.members] if self.rank == root
+                     else None)
         self.llrs = torch.zeros(self.max_span, dtype=torch.int8, device=device)
         self._res = torch.zeros(self.max_cbs * (CB_MSG_STRIDE + 1), dtype=torch.uint8, device=device)
         self._flags = torch.zeros(self.max_cbs, dtype=torch.uint8, device=device)
@@ -272,19 +286,36 @@ class CodeblockShard:
         dist.gather(self._res, self._res_all, dst=self.root, group=self.group)
         if self.rank == self.root:
             S = CB_MSG_STRIDE
+            total = len(self.cbs)
+            msgs2d = d_all_msgs[: total * S].view(total, S)
             for r, mem in enumerate(self.members):
+                if not mem:
+                    continue
+                k = len(mem)
                 src = self._res_all[r]
-                for j, i in enumerate(mem):
-                    d_all_msgs[i * S: (i + 1) * S].copy_(src[j * S: (j + 1) * S])
-                    d_all_flags[i: i + 1].copy_(src[self.max_cbs * S + j: self.max_cbs * S + j + 1])
+                msgs2d.index_copy_(0, self._idx[r], src[: k * S].view(k, S))
+                d_all_flags.index_copy_(0, self._idx[r], src[self.max_cbs * S: self.max_cbs * S + k])
 
-    def return_flags(self, d_all_flags: Optional[torch.Tensor], d_flags: torch.Tensor) -> None:
-        """The root's codeblock flags after the TB stage back to their owners' `d_flags` (the HARQ context)."""
+    def return_flags(self, d_all_flags: Optional[torch.Tensor], d_flags: torch.Tensor,
+                     harq_flags: Optional[torch.Tensor] = None) -> None:
+        """The root's codeblock flags after the TB stage back to their owners' `d_flags` (local order); with
+        `harq_flags` (keyed sharding) also into harq_flags[key], the HARQ context that follows the codeblock."""
         if self.rank == self.root:
             for r, mem in enumerate(self.members):
                 if mem:
-                    idx = torch.tensor(mem, dtype=torch.long, device=d_all_flags.device)
-                    self._flags_all[r][: len(mem)].copy_(d_all_flags[idx])
+                    self._flags_all[r][: len(mem)].copy_(d_all_flags.index_select(0, self._idx[r]))
         dist.scatter(self._flags, self._flags_all, src=self.root, group=self.group)
         n = len(self.local_cbs)
         d_flags[:n].copy_(self._flags[:n])
+        if harq_flags is not None:
+            if self._local_keys is None:
+                raise ValueError("keyed flags need the shard's HARQ keys")
+            if n:
+                harq_flags.index_copy_(0, self._local_keys, self._flags[:n].to(harq_flags.dtype))
+
+    def local_flags(self, harq_flags: torch.Tensor) -> torch.Tensor:
+        """This slot's local codeblocks' CRC flags from the keyed HARQ context (local order): what this rank's decoder
+        reads to skip the codeblocks an earlier transmission already decoded."""
+        if self._local_keys is None:
+            raise ValueError("keyed flags need the shard's HARQ keys")
+        return harq_flags.index_select(0, self._local_keys)

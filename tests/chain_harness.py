@@ -179,3 +179,21 @@ class UpperPhy:
         g = np.array(grid, np.uint16, copy=True, order="C")
         assert self.lib.chain_dl_slot(self.dl, slot, len(pdus), arr, _ptr(w), _ptr(tb), _ptr(tbb), _ptr(g)) == 0
         return g
+
+
+def factory_validate(device, direction, pdus, weights=None, path=CHAIN_SO):
+    """Row b8: the GPU uplink (direction 0, PUSCH PDUs) / downlink (1, PDSCH PDUs + precoding weights) factory's
+    create_pdu_validator() against the reference's own PUSCH / PDSCH validator: per PDU (factory accepts, reference
+    accepts, messages differ)."""
+    L = ctypes.CDLL(path)
+    PP = ctypes.POINTER(ChainParams)
+    L.chain_factory_validate.restype = ctypes.c_int
+    L.chain_factory_validate.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, PP, _P, _P]
+    arr = (ChainParams * len(pdus))(*pdus)
+    w = np.zeros(2, np.float32)
+    if weights:
+        w = np.ascontiguousarray(np.concatenate([np.asarray(x, np.complex64).ravel() for x in weights]),
+                                 np.complex64).view(np.float32)
+    out = np.zeros(len(pdus), np.int32)
+    assert L.chain_factory_validate(device, direction, len(pdus), arr, _ptr(w), _ptr(out)) == 0
+    return [(bool(v & 1), bool(v & 2), bool(v & 4)) for v in out.tolist()]

@@ -554,19 +554,29 @@ def _cb_harq_slots(orc):
         return segs, np.concatenate(llrs), cbs, keys, new
 
     X, Y, W = (CB_TB_BYTES[0], 11, 0.16), (CB_TB_BYTES[1], 12, 0.03), (CB_TB_BYTES[1], 13, 0.03)
-    return slot([(X, 100, True), (Y, 200, True)]), slot([(W, 300, True), (X, 100, False)])
+    V = (CB_TB_BYTES[0], 14, 0.03)
+    # slot 3: X a third time behind a new TB V: the codeblocks of X that passed by slot 2 are skipped
+    return (slot([(X, 100, True), (Y, 200, True)]), slot([(W, 300, True), (X, 100, False)]),
+            slot([(V, 400, True), (X, 100, False)]))
 
 
-def _cb_harq_decode(orc, segs, ids, llrs, local_cbs, keys, new, harq):
+def _cb_harq_decode(orc, segs, ids, llrs, local_cbs, keys, new, harq, passed=None, kept=None):
     """Oracle decoding of codeblocks `ids` (slot order) with the HARQ buffers kept per key in `harq` (combined when
-    not new). Returns messages and CRC flags."""
+    not new). passed[j] (local order): the codeblock's CRC already passed in an earlier transmission - it is not
+    decoded again and its kept message (kept[key]) is reported, as pusch_decoder_impl skips it
+    (pusch_decoder_impl.cpp:208). Returns messages and CRC flags (and fills kept with the decoded messages)."""
     from chain_lib import crc_for_tb
     flat = [(seg, cb) for seg in segs for cb in seg.codeblocks]
     msgs = np.zeros(len(ids) * sdist.CB_MSG_STRIDE, np.uint8)
     ok = np.zeros(len(ids), np.uint8)
+    S = sdist.CB_MSG_STRIDE
     for j, (i, (o, e)) in enumerate(zip(ids, local_cbs)):
         seg, cb = flat[i]
         Z = seg.lifting_size
+        if passed is not None and passed[j] and not new[i]:
+            msgs[j * S: (j + 1) * S] = kept[keys[i]]
+            ok[j] = 1
+            continue
         buf = harq.get(keys[i]) if not new[i] else None
         buf = np.zeros(66 * Z, np.int8) if buf is None else buf
         buf = orc.rate_dematch(1, 1, Z, 0, 2, 0, cb.nof_filler_bits, int(new[i]), llrs[o:o + e], buf)
@@ -574,8 +584,10 @@ def _cb_harq_decode(orc, segs, ids, llrs, local_cbs, keys, new, harq):
         it, bits = orc.ldpc_decode(1, 1, Z, buf, nof_crc_bits=cb.nof_crc_bits, nof_filler=cb.nof_filler_bits,
                                    crc_poly=crc_for_tb(seg), max_iter=6)
         packed = np.packbits(np.asarray(bits, np.uint8))
-        msgs[j * sdist.CB_MSG_STRIDE: j * sdist.CB_MSG_STRIDE + packed.size] = packed
+        msgs[j * S: j * S + packed.size] = packed
         ok[j] = 0 if (it is None or it < 0) else 1  # the oracle returns -1 when the CRC never passes
+        if kept is not None:
+            kept[keys[i]] = msgs[j * S: (j + 1) * S].copy()
     return msgs, ok
 
 
@@ -588,19 +600,32 @@ def _cb_harq_worker(rank, world, port, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         orc = Oracle()
         harq = {}  # this rank's HARQ buffers, by key: they never move between ranks
+        kept = {}  # this rank's decoded messages, by key (the rx buffer's codeblock data)
+        harq_flags = torch.zeros(1024, dtype=torch.uint8)  # this rank's CRC flags, by key
         res = []
+        skipped = 0
         for segs, llrs, cbs, keys, new in _cb_harq_slots(orc):
             sh = sdist.CodeblockShard(cbs, torch.device("cpu"), root=0, keys=keys)
             span = sh.scatter_llrs(torch.from_numpy(llrs) if rank == 0 else None)
             mine = sh.members[rank]
             assert all(keys[i] % world == rank for i in mine)
-            msgs, ok = _cb_harq_decode(orc, segs, mine, span.numpy(), sh.local_cbs, keys, new, harq)
+            passed = sh.local_flags(harq_flags).numpy()
+            skipped += sum(1 for j, i in enumerate(mine) if passed[j] and not new[i])
+            msgs, ok = _cb_harq_decode(orc, segs, mine, span.numpy(), sh.local_cbs, keys, new, harq, passed, kept)
             n = len(cbs)
             all_msgs = torch.zeros(n * sdist.CB_MSG_STRIDE, dtype=torch.uint8) if rank == 0 else None
             all_ok = torch.zeros(n, dtype=torch.uint8) if rank == 0 else None
             sh.gather(torch.from_numpy(msgs), torch.from_numpy(ok), all_msgs, all_ok)
+            # The root's final flags (no TB stage here: the codeblock flags as gathered) back to their owners, by key.
+            local = torch.zeros(max(1, len(mine)), dtype=torch.uint8)
+            sh.return_flags(all_ok, local, harq_flags)
+            assert np.array_equal(local[: len(mine)].numpy(), ok)
             if rank == 0:
                 res.append((all_msgs.numpy().copy(), all_ok.numpy().copy()))
+        skipped_all = torch.tensor([skipped])
+        dist.all_reduce(skipped_all)
+        if rank == 0:
+            res.append(int(skipped_all.item()))
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, res if rank == 0 else None, None))
@@ -615,7 +640,8 @@ def test_codeblock_shard_harq_keys_retransmission_gloo(world):
     absolute codeblock id) instead of the slot position, so a TB retransmitted in a slot of another composition is
     decoded by the ranks holding its earlier soft bits. Two slots; the gathered messages and CRC flags of both equal one
     rank decoding every codeblock with every HARQ buffer, and the retransmission's combining recovers codeblocks the
-    first transmission lost."""
+    first transmission lost. Round-5 ADVICE: the returned CRC flags are kept by key (return_flags(..., harq_flags)), and
+    the retransmission skips exactly the codeblocks that already passed (local_flags), as the reference does."""
     from oracle_lib import Oracle
     port = _free_port()
     ctx = mp.get_context("spawn")
@@ -631,13 +657,20 @@ def test_codeblock_shard_harq_keys_retransmission_gloo(world):
     for p in procs:
         p.join(timeout=60)
     orc = Oracle()
-    harq = {}
-    want = []
+    harq, kept, flags = {}, {}, {}
+    want, skipped_want = [], 0
     for segs, llrs, cbs, keys, new in _cb_harq_slots(orc):
-        want.append(_cb_harq_decode(orc, segs, list(range(len(cbs))), llrs, cbs, keys, new, harq))
-    for (got_msgs, got_ok), (want_msgs, want_ok) in zip(out[0], want):
+        passed = [flags.get(k, 0) for k in keys]
+        skipped_want += sum(1 for p, n in zip(passed, new) if p and not n)
+        want.append(_cb_harq_decode(orc, segs, list(range(len(cbs))), llrs, cbs, keys, new, harq, passed, kept))
+        flags.update(zip(keys, want[-1][1].tolist()))
+    *slots, skipped = out[0]
+    assert len(slots) == len(want) == 3
+    for (got_msgs, got_ok), (want_msgs, want_ok) in zip(slots, want):
         assert np.array_equal(got_ok, want_ok)
         assert np.array_equal(got_msgs, want_msgs)
+    # X's codeblocks that had passed were skipped on its later transmissions, by the ranks that own their keys
+    assert skipped == skipped_want > 0, (skipped, skipped_want)
     nx = len(_cb_harq_slots(orc)[0][0][0].codeblocks)
     first_x, second_x = want[0][1][:nx], want[1][1][-nx:]
     assert first_x.sum() < nx and second_x.sum() > first_x.sum(), (first_x, second_x)

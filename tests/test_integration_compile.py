@@ -12,10 +12,10 @@ REF = "/root/reference"
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "include", "srsran")), reason="reference tree absent")
 @pytest.mark.parametrize("src", ["ldpc_decoder_gpu.cpp", "hw_accelerator_pusch_dec_gpu.cpp",
                                  "hw_accelerator_pdsch_enc_gpu.cpp", "pusch_chain_gpu.cpp", "pdsch_chain_gpu.cpp",
-                                 "ofdm_gpu.cpp"])
+                                 "ofdm_gpu.cpp", "upper_phy_factories_gpu.cpp"])
 def test_binding_compiles_against_reference_headers(src, tmp_path):
     cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-fsyntax-only", "-DFMT_HEADER_ONLY",
-           f"-I{REF}/include", f"-I{REF}/external/fmt/include", f"-I{REF}/external", f"-I{ROOT}/include",
+           f"-I{REF}/include", f"-I{REF}", f"-I{REF}/external/fmt/include", f"-I{REF}/external", f"-I{ROOT}/include",
            f"-I{ROOT}/integration", "-I/opt/rocm/include", "-x", "c++", "-D__HIP_PLATFORM_AMD__", os.path.join(ROOT, "integration", src)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -43,5 +43,6 @@ def test_chain_harness_links_reference_processors_with_gpu_signal_chain():
     import ctypes
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libsrschain.so"))
     for sym in ("chain_create", "chain_destroy", "chain_ue_tx", "chain_pusch_process", "chain_pdsch_process",
-                "chain_ofdm_modulate", "chain_ofdm_demodulate"):
+                "chain_ofdm_modulate", "chain_ofdm_demodulate", "chain_factory_validate", "chain_ul_create",
+                "chain_dl_create"):
         assert hasattr(lib, sym)

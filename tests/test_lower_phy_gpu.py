@@ -197,3 +197,46 @@ def test_sector_group_equals_reference(lower, name, in_flight):
     c = got["group"]
     assert c["ul_launches"] > 0 and c["ul_batched"] > c["ul_launches"] and c["ul_batched"] > c["ul_alone"], c
     assert c["dl_launches"] > 0 and c["dl_batched"] > c["dl_launches"] and c["dl_batched"] > c["dl_alone"], c
+
+
+# ref_lower.cpp group_prelude: the tested sector joins a two-sector group after another one registered first.
+GROUP_FIRST_REMOVED, GROUP_FIRST_OTHER_CP = 4, 5
+CONFIG_60K_NORMAL = dict(numerology=2, bw_rb=24, dft_size=512, extended=False, center_freq_hz=3.0e9, nof_ports=1,
+                         window_offset=0.25)
+
+
+def check_group_sector(lower, cfg, variant, seed=5):
+    nsymb = 12 if cfg["extended"] else 14
+    grids, mask = dl_grids(np.random.default_rng(seed), cfg, nsymb)
+    ev = dl_script(nsymb)
+    ref, ref_flags, ref_late = lower.pdxch(REF_CPU, cfg, grids, mask, ev)
+    got, flags, late = lower.pdxch(variant, cfg, grids, mask, ev)
+    touched = ref.real != SENTINEL
+    rms = np.sqrt(np.mean(np.abs(ref[touched]) ** 2))
+    assert np.array_equal(flags, ref_flags) and late == ref_late
+    assert np.array_equal(got.real == SENTINEL, ~touched)
+    assert np.max(np.abs(got[touched] - ref[touched])) < 2e-5 * rms
+    ev = ul_script(nsymb)
+    x = ul_samples(np.random.default_rng(seed + 1), cfg, ev)
+    ref, ref_flags, ref_rx, ref_late = lower.puxch(REF_CPU, cfg, 6, ev, x)
+    got, flags, rx, late = lower.puxch(variant, cfg, 6, ev, x, max_in_flight=3)
+    assert np.array_equal(flags, ref_flags) and rx == ref_rx and late == ref_late
+    va, vb = bf16_to_complex(ref), bf16_to_complex(got)
+    rms = np.sqrt(np.mean(np.abs(va[va != 0]) ** 2))
+    assert np.array_equal(va == 0, vb == 0)
+    assert np.all(np.abs(va - vb) <= np.maximum(2.0 ** -7 * np.abs(va), 1e-4 * rms))
+
+
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_sector_group_after_first_sector_removed(lower, name):
+    """The group's first sector is removed (processor and plans destroyed) before another sector runs: the group
+    launches with its own copy of the first plan, so the remaining sector's DL and UL still equal the reference."""
+    check_group_sector(lower, CONFIGS[name], GROUP_FIRST_REMOVED)
+
+
+@pytest.mark.parametrize("cfg", [CONFIG_60K_NORMAL, CONFIGS["60kHz_extended_cp"]], ids=["normal_cp", "extended_cp"])
+def test_sector_group_mixed_cyclic_prefix(lower, cfg):
+    """A 60 kHz sector joining a group whose first sector has the other cyclic prefix (same DFT size, bandwidth and
+    slot length): a normal-CP slot has 14 jobs per port where the extended-CP first sector sized the group's job table
+    for 12, so that sector must run alone; an extended-CP sector fits a normal-CP group. Both equal the reference."""
+    check_group_sector(lower, cfg, GROUP_FIRST_OTHER_CP)

@@ -1,7 +1,11 @@
 """Upper-PHY slot processors on the GPU (row b6): the reference's OWN uplink_processor_impl and
 downlink_processor_single_executor_impl (compiled from its sources by oracle/build_chain.sh) run once over the
 reference's CPU channel processors and once over the GPU slot batches of integration/upper_phy_gpu.cpp, which gather
-a slot's PUSCH / PDSCH PDUs into one launch sequence (tests/chain_harness.py: UpperPhy).
+a slot's PUSCH / PDSCH PDUs into one launch sequence (tests/chain_harness.py: UpperPhy). Row b8: every GPU processor
+here is obtained only through the GPU factories' create() (uplink_processor_factory / downlink_processor_factory of
+integration/upper_phy_factories_gpu.cpp, with the GPU pusch_processor_factory / pdsch_processor_factory for the PDUs
+the batches do not cover), as upper_phy_factories.cpp obtains its processors; their create_pdu_validator() equals the
+reference's validators.
 
   * UL: multi-UE slots (different sizes, modulations, CFOs, delays, SNRs, one UE over the DC subcarrier, one with
     HARQ-ACK on PUSCH, whose UL-SCH stream the batch demultiplexes on the GPU) registered in the reference's PDU repository;
@@ -272,3 +276,26 @@ def test_uplink_processor_gpu_batch_interpolate_equals_reference():
         chain.close()
         cpu.close()
         gpu.close()
+
+
+def test_gpu_factories_pdu_validators_equal_reference():
+    """Row b8: create_pdu_validator() of the GPU uplink / downlink processor factories answers like the reference's
+    pusch_processor_validator_impl (channel-estimate dimensions 273 PRB x 14 symbols x 4 layers x 4 ports) and
+    pdsch_processor_validator_impl, message for message, on valid PDUs and on PDUs each validator rejects."""
+    import chain_harness as H
+    ul = [H.params(), H.params(nof_rb=273), H.params(nof_layers=2, nof_ports=4),
+          H.params(nof_ports=5),                       # more rx ports than the channel-estimate dimensions
+          H.params(nof_layers=5),                      # more layers
+          H.params(rb_start=270, nof_rb=10),           # allocation outside the BWP
+          H.params(start_symbol=10, nof_symbols=8),    # symbols past the slot
+          H.params(dmrs_mask=0)]                       # no DM-RS symbol
+    res = H.factory_validate(0, 0, ul)
+    assert [r[:2] for r in res] == [(r[1], r[1]) for r in res], res  # same verdict as the reference
+    assert not any(r[2] for r in res), res                          # same messages
+    assert [r[1] for r in res][:3] == [True] * 3 and not all(r[1] for r in res), res
+    dl = [H.params(nof_layers=1), H.params(nof_layers=4, nof_rb=100), H.params(nof_layers=2, start_symbol=13,
+                                                                               nof_symbols=4)]
+    w = [np.ones((P, p.nof_layers), np.complex64) for p in dl]
+    res = H.factory_validate(0, 1, dl, w)
+    assert [r[:2] for r in res] == [(r[1], r[1]) for r in res], res
+    assert not any(r[2] for r in res), res

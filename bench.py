@@ -663,6 +663,8 @@ def measure(args, env):
         "ofdm_demodulate": S_ul * P * 14 * slotlib.DFT_SIZE * 8 + grid_b_ul,
         "pusch_channel_estimate": S_ul * P * nd * nsc * 4 + ce_b,
         "pusch_demodulate": data_re * (P * 4 + Lu * ul_ues[0].qm) + ce_b,
+        # TB bytes read + codeword bytes written
+        "pdsch_encode": sum(sum(s.tbs for s in c.segs) * c.nof_slots for c in dl_cells) // 8 + cw_b,
     }
     stage_gbps = {k: v / (stage[k] * 1e-3) / 1e9 for k, v in stage_bytes.items() if stage[k] > 0}
     set_bytes = sum(t.numel() * t.element_size() for t in
@@ -743,6 +745,7 @@ def measure(args, env):
         "operating_points": points,
         "stage_ms_per_step": stage,  # from an untimed eager pass with per-stage events
         "stage_algorithmic_gbps": stage_gbps,
+        "stage_algorithmic_bytes": stage_bytes,  # per step = per launch of each stage's kernel
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dec_kernel,
                      "kernel_ms_per_launch": dec_ms, "algorithmic_bytes_per_launch": dec_bytes,

@@ -57,6 +57,32 @@ void srsgpu_context_destroy(srsgpu_context* ctx);
 /** HIP device index of a context (-1 for NULL): the device a binding allocates its own buffers and streams on. */
 int srsgpu_context_device(const srsgpu_context* ctx);
 
+/** Kernel-selection options of a context, read when a plan is created (not from the process environment: what a plan
+ *  runs depends only on its context and configuration). Every default is the measured-fastest choice; the others are
+ *  alternative kernels with identical results, kept for the parity tests that pin them. */
+typedef enum {
+  /** Packed LDPC decoder, even Z: -1 (default) the edge-split kernel when a launch gives under ~3 waves per SIMD,
+   *  else the one-row-pair kernel; 0 always the one-row-pair kernel; 1 always the edge-split kernel. */
+  SRSGPU_OPTION_DECODER_SPLIT = 1,
+  /** 0 (default) / 1: codeblocks of Z = 144..192 two per workgroup (three waves for two codeblocks). */
+  SRSGPU_OPTION_DECODER_PAIRS = 2,
+  /** 1 (default) / 0: the PUSCH decoder dematches plain first transmissions itself (0: every codeblock through the
+   *  separate rate dematcher kernel). */
+  SRSGPU_OPTION_DECODER_FUSED_DEMATCH = 3,
+  /** 0 (default) / 1: the PDSCH encoder's one-bit-per-byte kernel for every codeblock (0: the packed-word kernel where
+   *  Z % 32 == 0 and the message is byte aligned). */
+  SRSGPU_OPTION_ENCODER_BYTE_KERNEL = 4,
+  /** 0 (default) / 1: the PDSCH encoder clears its codeword output before every execution (0: only when its
+   *  codeblocks do not each store whole words that tile the output). */
+  SRSGPU_OPTION_ENCODER_ZERO_OUTPUT = 5
+} srsgpu_option;
+
+/** Sets option `option` (srsgpu_option) of a context for the plans created afterwards. */
+int srsgpu_context_set_option(srsgpu_context* ctx, int option, int value);
+
+/** Reads option `option` of a context. */
+int srsgpu_context_get_option(const srsgpu_context* ctx, int option, int* value);
+
 /* ------------------------------------------------------------------------------------------------------------------
  * LDPC decoder — replaces srsran::ldpc_decoder::decode(bit_buffer& output, span<const log_likelihood_ratio> input,
  * crc_calculator* crc, const configuration& cfg)   (include/srsran/phy/upper/channel_coding/ldpc/ldpc_decoder.h:72,

@@ -166,6 +166,7 @@ public:
       return lru.front().plan;
     }
     Plan* plan = nullptr;
+    ++nof_misses;
     {
       std::lock_guard<std::recursive_mutex> lock(hip_setup_mutex());
       plan = create();
@@ -183,6 +184,8 @@ public:
 
   /// Plans destroyed so far (a captured graph that references a plan must not outlive it).
   uint64_t evictions() const { return nof_evictions; }
+  /// Plans created so far (cache misses).
+  uint64_t misses() const { return nof_misses; }
 
   void clear()
   {
@@ -203,6 +206,7 @@ private:
   std::list<entry>                                                  lru;
   std::unordered_map<std::string, typename std::list<entry>::iterator> index;
   uint64_t                                                          nof_evictions = 0;
+  uint64_t                                                          nof_misses    = 0;
 };
 
 /// A HIP stream on the context's device, destroyed with its owner.

@@ -59,18 +59,6 @@ namespace {
 
 constexpr unsigned HARQ_SLOT_BYTES = 66 * 384;  ///< N of BG1 at Z = 384: one arena slot per codeblock.
 
-/// The rate dematcher and decoder read and write the HARQ soft buffers in the arena through a per-codeblock pointer
-/// table (srsgpu_pusch_decoder_plan_execute_arena). SRSGPU_HARQ_COPY=1 (A/B): copy them into a batch buffer before
-/// the decode and back after it (two srsgpu_harq_copy_arenas launches).
-bool harq_in_arena()
-{
-  static const bool copy = [] {
-    const char* e = std::getenv("SRSGPU_HARQ_COPY");
-    return e != nullptr && e[0] == '1';
-  }();
-  return !copy;
-}
-
 using clock_type = std::chrono::steady_clock;
 
 double us_between(clock_type::time_point a, clock_type::time_point b)
@@ -508,16 +496,16 @@ public:
     launches.clear();
     (void)hipEventDestroy(done);
     (void)hipFree(d_ce);
-    (void)hipFree(d_harq);
     (void)hipFree(d_llr);
     (void)hipFree(d_sch_b);
     (void)hipFree(d_uci_b);
-    (void)hipFree(d_harq_b);
   }
 
   /// Host-clock stamps of a launch (diagnostics).
   struct stamps {
     clock_type::time_point start, built, filled, launched;
+    bool                   plan_created   = false;  ///< the launch plan was not cached (a new group layout)
+    bool                   graph_captured = false;  ///< its graph was (re)captured
   };
 
   /// Launches `jobs` (one grid shape; their grids in d_grids, uploads signalled by the jobs' events): the launch plan,
@@ -578,8 +566,6 @@ private:
   size_t                    d_sch_b_cap = 0;
   int8_t*                   d_uci_b     = nullptr;
   size_t                    d_uci_b_cap = 0;
-  int8_t*                   d_harq_b     = nullptr;
-  size_t                    d_harq_b_cap = 0;
   deferred_layout           d_lay;
   std::vector<uint8_t>      d_decoded;
 
@@ -601,27 +587,22 @@ private:
   owned_stream            stream;
   hipEvent_t              done = nullptr;
   plan_cache<launch_plan> launches;
-  staged_buffer           io;    ///< Inputs and results (layout in launch_plan), when they stay in HBM (shards).
-  mapped_buffer           io_map{"pusch_launcher io"};  ///< The same image in mapped host memory, read and written in
-                                                         ///< place by the launch (results to the host: no copy nodes)
-  bool                    zc = false;  ///< the current launch uses io_map
+  staged_buffer           io;    ///< Inputs and results (layout in launch_plan).
 
   template <typename T = uint8_t>
   T* ioh(size_t off)
   {
-    return zc ? io_map.host<T>(off) : io.host<T>(off);
+    return io.host<T>(off);
   }
   template <typename T = uint8_t>
   T* iod(size_t off)
   {
-    return zc ? io_map.dev<T>(off) : io.dev<T>(off);
+    return io.dev<T>(off);
   }
   staged_buffer           msgs;  ///< CB messages: HARQ context in, kept messages out.
   mapped_buffer           spans{"pusch_launcher grid spans"};  ///< the launch's rx-grid copies (srsgpu_copy_spans)
   uint32_t*               d_ce       = nullptr;
   size_t                  d_ce_cap   = 0;
-  int8_t*                 d_harq     = nullptr;
-  size_t                  d_harq_cap = 0;
   int8_t*                 d_llr      = nullptr;
   size_t                  d_llr_cap  = 0;
   uint64_t                buffer_generation = 1;  ///< Bumped when a buffer above moves (graphs capture pointers).
@@ -695,8 +676,6 @@ private:
   srsgpu_context*                      ctx;
   std::shared_ptr<uci_decoder_factory> uci_factory;
   std::unique_ptr<pusch_processor>     fallback;
-  owned_stream                         upload_stream;
-  hipEvent_t                           uploaded = nullptr;
   staged_buffer                        grid_buf;  ///< Pinned copy of the rx grid for the shards' DMA uploads.
   mapped_buffer                        grid_map{"pusch_slot_batch grid"};  ///< The rx grid, read in place by the launch
   unsigned                             batch_id   = 0;
@@ -809,6 +788,10 @@ private:
   double     phase_us[5]   = {};  ///< build + plans, fill, graph + launch, wait for GPU, replay
   uint64_t   timed_launches = 0;
   uint64_t   timed_slots    = 0;
+  uint64_t   plans_created   = 0;  ///< launches whose group layout was not cached (new plans)
+  uint64_t   graphs_captured = 0;  ///< launches that (re)captured their graph
+  double     setup_us        = 0;  ///< dispatcher time of those launches
+  std::array<uint64_t, 33> launch_sizes{};  ///< launches by slots per launch (32: 32 or more)
 };
 
 // ---------------------------------------------------------------------------------------------------------------------
@@ -852,10 +835,20 @@ pusch_gpu_service::~pusch_gpu_service()
   if (timing && timed_launches > 0) {
     std::fprintf(stderr,
                  "pusch_gpu_service: %llu launches, %.2f slots per launch, us per launch: build %.1f, fill %.1f, "
-                 "graph+launch %.1f, GPU wait %.1f, replay %.1f\n",
+                 "graph+launch %.1f, GPU wait %.1f, replay %.1f; new plans %llu, graph captures %llu (%.0f us of "
+                 "dispatcher time)\n",
                  static_cast<unsigned long long>(timed_launches), static_cast<double>(timed_slots) / timed_launches,
                  phase_us[0] / timed_launches, phase_us[1] / timed_launches, phase_us[2] / timed_launches,
-                 phase_us[3] / timed_launches, phase_us[4] / timed_launches);
+                 phase_us[3] / timed_launches, phase_us[4] / timed_launches,
+                 static_cast<unsigned long long>(plans_created), static_cast<unsigned long long>(graphs_captured),
+                 setup_us);
+    std::fprintf(stderr, "pusch_gpu_service: launches by slots per launch:");
+    for (size_t n = 1; n != launch_sizes.size(); ++n) {
+      if (launch_sizes[n] != 0) {
+        std::fprintf(stderr, " %zu:%llu", n, static_cast<unsigned long long>(launch_sizes[n]));
+      }
+    }
+    std::fprintf(stderr, "\n");
   }
   std::lock_guard<std::recursive_mutex> lock(hip_setup_mutex());
   device_scope                          dev(ctx.get(), WHO);
@@ -1178,24 +1171,20 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
     key_append(key, job->lay.key.size());
     key.insert(key.end(), job->lay.key.begin(), job->lay.key.end());
   }
-  launch_plan* lp = launches.get(key, [&] { return create_plan(jobs, P, grid_prb); });
-  plan            = lp;
+  const uint64_t misses = launches.misses();
+  launch_plan*   lp     = launches.get(key, [&] { return create_plan(jobs, P, grid_prb); });
+  tm.plan_created       = launches.misses() != misses;
+  plan                  = lp;
   downloaded      = download;
-  // The staging image in HBM with an upload and a download node in the graph. SRSGPU_IO_MAPPED=1 (diagnostics, A/B):
-  // the image in mapped host memory, read and written in place by the kernels (no copy nodes) - measured slower:
-  // one thread 6.3k either way, 16-sector service 23.3-23.7k vs 42.7-45.0k one-PDU slots/s: the decoder's and the
-  // statistics kernels' small scattered result stores cross PCIe one by one (profiles/r5_io_mapped_ab.txt).
-  static const bool io_mapped = std::getenv("SRSGPU_IO_MAPPED") != nullptr;
-  zc                          = download && io_mapped;
+  // The staging image in HBM with an upload and a download node in the graph. (The image in mapped host memory, read
+  // and written in place by the kernels, measured slower: 16-sector service 23.3-23.7k vs 42.7-45.0k one-PDU slots/s,
+  // the decoder's and the statistics kernels' small scattered result stores cross PCIe one by one,
+  // profiles/r5_io_mapped_ab.txt.)
   // Split grid copy: every job's grid is read from mapped host memory by the launch: a copy launch before the graph
   // moves the DM-RS symbol rows, and the channel estimator's launch (which reads only those) moves the data-symbol
-  // rows on extra workgroups while it runs. SRSGPU_GRID_SPLIT=0 (A/B): the whole grids in one copy launch before the
-  // graph. (A fork onto a second stream inside the graph measured serialised and slower.)
-  static const bool split_enabled = [] {
-    const char* e = std::getenv("SRSGPU_GRID_SPLIT");
-    return e == nullptr || e[0] != '0';
-  }();
-  bool split = split_enabled;
+  // rows on extra workgroups while it runs (one-PDU slot: grid copy 21 -> 7 us exposed). Shards whose grid came by
+  // DMA copy nothing. (A fork onto a second stream inside the graph measured serialised and slower.)
+  bool split = true;
   for (const auto& job : jobs) {
     split = split && job->grid_src != nullptr;
   }
@@ -1205,17 +1194,12 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
 
   // Buffers (grow-only; a move invalidates the captured graphs).
   {
-    const void* before[6] = {io.host(), io_map.host(), msgs.host(), d_ce, d_harq, d_llr};
-    if (zc) {
-      io_map.reserve(lp->end_o);
-    } else {
-      io.reserve(lp->end_o);
-    }
+    const void* before[4] = {io.host(), msgs.host(), d_ce, d_llr};
+    io.reserve(lp->end_o);
     msgs.reserve(std::max<size_t>(static_cast<size_t>(lp->cb_total) * SRSGPU_CB_MSG_STRIDE, 64));
     reserve_device(d_ce, d_ce_cap, static_cast<size_t>(lp->max_grid) * 4 * P * 14 * row, "channel estimates");
-    reserve_device(d_harq, d_harq_cap, std::max<size_t>(lp->harq_total, 16), "HARQ launch buffer");
     reserve_device(d_llr, d_llr_cap, std::max<size_t>(lp->llr_total, 64), "LLRs");
-    const void* after[6] = {io.host(), io_map.host(), msgs.host(), d_ce, d_harq, d_llr};
+    const void* after[4] = {io.host(), msgs.host(), d_ce, d_llr};
     if (!std::equal(std::begin(before), std::end(before), std::begin(after))) {
       ++buffer_generation;
     }
@@ -1228,10 +1212,9 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
       (void)hipGraphExecDestroy(lp->graph);
       lp->graph = nullptr;
     }
+    tm.graph_captured = true;
     lp->graph = capture_graph(s, WHO, [&] {
-      if (!zc) {
-        io.upload(0, lp->iter_o, s);
-      }
+      io.upload(0, lp->iter_o, s);
       if (split) {
         // The estimator's launch also copies the data-symbol rows (extra workgroups), after the DM-RS rows it reads
         // were copied by the launch before the graph.
@@ -1257,32 +1240,15 @@ pusch_launcher::stamps pusch_launcher::launch(const std::vector<std::unique_ptr<
         int8_t* uci = iod<int8_t>(lp->uci_o);
         srsgpu_check(srsgpu_ulsch_demux_plan_execute(lp->demux, d_llr, d_llr, uci, uci, nullptr, s), WHO);
       }
-      if (harq_in_arena()) {
-        // The rate dematcher and the decoder work on the soft buffers in the rx-buffer arenas through the per-codeblock
-        // pointer table (no copy into the batch HARQ buffer and back).
-        if (lp->dec != nullptr) {
-          srsgpu_check(srsgpu_pusch_decoder_plan_execute_arena(
-                           lp->dec, d_llr, iod<int8_t*>(lp->ptr_o), iod<uint8_t>(lp->flag_o), msgs.dev<uint8_t>(),
-                           iod<int32_t>(lp->iter_o), iod<uint8_t>(lp->tb_o), iod<uint8_t>(lp->tbok_o), s),
-                       WHO);
-        }
-      } else {
-        srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_BATCH, iod<int8_t*>(lp->arena_o),
-                                             HARQ_SLOT_BYTES, d_harq, iod<srsgpu_harq_copy_job>(0),
-                                             lp->nof_copies, s),
-                     WHO);
-        if (lp->dec != nullptr) {
-          srsgpu_check(srsgpu_pusch_decoder_plan_execute(lp->dec, d_llr, d_harq, iod<uint8_t>(lp->flag_o),
-                                                         msgs.dev<uint8_t>(), iod<int32_t>(lp->iter_o),
-                                                         iod<uint8_t>(lp->tb_o), iod<uint8_t>(lp->tbok_o), s),
-                       WHO);
-        }
-        srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_ARENA, iod<int8_t*>(lp->arena_o),
-                                             HARQ_SLOT_BYTES, d_harq, iod<srsgpu_harq_copy_job>(0),
-                                             lp->nof_copies, s),
+      // The rate dematcher and the decoder work on the soft buffers in the rx-buffer arenas through the per-codeblock
+      // pointer table (no copy into a batch HARQ buffer and back).
+      if (lp->dec != nullptr) {
+        srsgpu_check(srsgpu_pusch_decoder_plan_execute_arena(
+                         lp->dec, d_llr, iod<int8_t*>(lp->ptr_o), iod<uint8_t>(lp->flag_o), msgs.dev<uint8_t>(),
+                         iod<int32_t>(lp->iter_o), iod<uint8_t>(lp->tb_o), iod<uint8_t>(lp->tbok_o), s),
                      WHO);
       }
-      if (download && !zc) {
+      if (download) {
         io.download(lp->flag_o, lp->end_o - lp->flag_o, s);
       }
     });
@@ -1460,7 +1426,6 @@ void pusch_launcher::decode_deferred(const pusch_entry&      e,
   d_msgs.reserve(std::max<size_t>(static_cast<size_t>(n_cb) * SRSGPU_CB_MSG_STRIDE, 64));
   reserve_device(d_sch_b, d_sch_b_cap, std::max<size_t>(nsch, 64), "deferred UL-SCH");
   reserve_device(d_uci_b, d_uci_b_cap, d.csi1_offset + a64(d.nof_enc_csi_part1_bits) + 64, "deferred UCI");
-  reserve_device(d_harq_b, d_harq_b_cap, std::max<size_t>(static_cast<size_t>(n_cb) * e.cb_N, 16), "deferred HARQ");
   std::memcpy(d_io.host(0), e.copies.data(), n_cb * sizeof(srsgpu_harq_copy_job));
   int8_t* arena_base = harq.d_soft;
   std::memcpy(d_io.host(d_lay.arena_o), &arena_base, sizeof(arena_base));
@@ -1487,24 +1452,11 @@ void pusch_launcher::decode_deferred(const pusch_entry&      e,
   srsgpu_check(srsgpu_ulsch_demux_plan_execute(dp->demux, d_llr, d_sch_b, d_uci_b, d_uci_b,
                                                d_io.dev<int8_t>(d_lay.csi2_o), s),
                WHO);
-  if (harq_in_arena()) {
-    srsgpu_check(srsgpu_pusch_decoder_plan_execute_arena(dp->dec, d_sch_b, d_io.dev<int8_t*>(d_lay.ptr_o),
-                                                         d_io.dev<uint8_t>(d_lay.flag_o), d_msgs.dev<uint8_t>(),
-                                                         d_io.dev<int32_t>(d_lay.iter_o), d_io.dev<uint8_t>(d_lay.tb_o),
-                                                         d_io.dev<uint8_t>(d_lay.tbok_o), s),
-                 WHO);
-  } else {
-    srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_BATCH, d_io.dev<int8_t*>(d_lay.arena_o),
-                                         HARQ_SLOT_BYTES, d_harq_b, d_io.dev<srsgpu_harq_copy_job>(0), n_cb, s),
-                 WHO);
-    srsgpu_check(srsgpu_pusch_decoder_plan_execute(dp->dec, d_sch_b, d_harq_b, d_io.dev<uint8_t>(d_lay.flag_o),
-                                                   d_msgs.dev<uint8_t>(), d_io.dev<int32_t>(d_lay.iter_o),
-                                                   d_io.dev<uint8_t>(d_lay.tb_o), d_io.dev<uint8_t>(d_lay.tbok_o), s),
-                 WHO);
-    srsgpu_check(srsgpu_harq_copy_arenas(ctx, SRSGPU_HARQ_TO_ARENA, d_io.dev<int8_t*>(d_lay.arena_o),
-                                         HARQ_SLOT_BYTES, d_harq_b, d_io.dev<srsgpu_harq_copy_job>(0), n_cb, s),
-                 WHO);
-  }
+  srsgpu_check(srsgpu_pusch_decoder_plan_execute_arena(dp->dec, d_sch_b, d_io.dev<int8_t*>(d_lay.ptr_o),
+                                                       d_io.dev<uint8_t>(d_lay.flag_o), d_msgs.dev<uint8_t>(),
+                                                       d_io.dev<int32_t>(d_lay.iter_o), d_io.dev<uint8_t>(d_lay.tb_o),
+                                                       d_io.dev<uint8_t>(d_lay.tbok_o), s),
+               WHO);
   d_io.download(d_lay.flag_o, d_lay.end_o - d_lay.flag_o, s);
   d_msgs.download(0, static_cast<size_t>(n_cb) * SRSGPU_CB_MSG_STRIDE, s);
   hip_check(hipStreamSynchronize(s), WHO, "synchronise");
@@ -1620,6 +1572,12 @@ void pusch_gpu_service::launch(launch_set& set)
     phase_us[0] += us_between(tm.start, tm.built);
     phase_us[1] += us_between(tm.built, tm.filled);
     phase_us[2] += us_between(tm.filled, tm.launched);
+    plans_created += tm.plan_created ? 1 : 0;
+    graphs_captured += tm.graph_captured ? 1 : 0;
+    if (tm.plan_created || tm.graph_captured) {
+      setup_us += us_between(tm.start, tm.launched);
+    }
+    ++launch_sizes[std::min<size_t>(set.jobs.size(), launch_sizes.size() - 1)];
   }
 }
 
@@ -1697,7 +1655,6 @@ pusch_slot_batch::pusch_slot_batch(const pusch_batch_configuration&     cfg_,
   ctx(service->context()),
   uci_factory(std::move(uci_factory_)),
   fallback(std::move(fallback_)),
-  upload_stream(ctx, WHO),
   grid_buf(WHO)
 {
   if (!fallback || !uci_factory || !arena) {
@@ -1707,7 +1664,6 @@ pusch_slot_batch::pusch_slot_batch(const pusch_batch_configuration&     cfg_,
     throw std::invalid_argument(std::string(WHO) + ": HARQ arena and service on different devices");
   }
   device_scope dev(ctx, WHO);
-  hip_check(hipEventCreateWithFlags(&uploaded, hipEventDisableTiming), WHO, "event");
   batch_id = service->new_batch_id();
   if (!cfg.devices.empty()) {
     if (cfg.asynchronous) {
@@ -1739,8 +1695,6 @@ pusch_slot_batch::~pusch_slot_batch()
     std::unique_lock<std::mutex> lock(done_mtx);
     done_cv.wait(lock, [&] { return outstanding == 0; });
   }
-  (void)hipStreamSynchronize(upload_stream.get());
-  (void)hipEventDestroy(uploaded);
   if (grid_slot >= 0) {
     service->release_grid(grid_P, grid_prb, static_cast<unsigned>(grid_slot));
   }
@@ -2106,26 +2060,14 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
   }
   const size_t row    = static_cast<size_t>(nsc) * sizeof(uint32_t);
   const size_t gbytes = static_cast<size_t>(P) * 14 * row;
-  // SRSGPU_GRID_DMA=1 (diagnostics, A/B): the round-5 first version's DMA upload per slot instead of the span copy.
-  static const bool grid_dma = std::getenv("SRSGPU_GRID_DMA") != nullptr;
-  staged_buffer*    dma_buf  = grid_dma ? &grid_buf : nullptr;
-  if (grid_dma) {
-    grid_buf.reserve(gbytes);
-  } else {
-    grid_map.reserve(gbytes);
-  }
   // The rx grid (every symbol of ports 0..P-1, [port][symbol][subcarrier]) into mapped host memory; the launch copies
-  // it into the batch's HBM grid slot (srsgpu_copy_spans, with the other slots' grids).
+  // it into the batch's HBM grid slot (srsgpu_copy_spans, with the other slots' grids: zero-copy reads instead of a DMA
+  // copy per slot, which ran the service at the DMA engines' ~29 GB/s, profiles/r5_grid_span_copy_ab.txt).
+  grid_map.reserve(gbytes);
   for (unsigned p = 0; p != P; ++p) {
     for (unsigned l = 0; l != 14; ++l) {
-      uint8_t* dst = dma_buf != nullptr ? dma_buf->host((p * 14 + l) * row) : grid_map.host((p * 14 + l) * row);
-      std::memcpy(dst, grid.get_view(p, l).data(), row);
+      std::memcpy(grid_map.host((p * 14 + l) * row), grid.get_view(p, l).data(), row);
     }
-  }
-  if (dma_buf != nullptr) {
-    hip_check(hipMemcpyAsync(d_grid, dma_buf->host(), gbytes, hipMemcpyHostToDevice, upload_stream.get()), WHO,
-              "grid upload");
-    hip_check(hipEventRecord(uploaded, upload_stream.get()), WHO, "event");
   }
 
   job->batch     = this;
@@ -2135,8 +2077,8 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
   job->grid_slot = static_cast<unsigned>(grid_slot);
   job->P         = P;
   job->grid_prb  = grid_prb;
-  job->uploaded   = dma_buf != nullptr ? uploaded : nullptr;
-  job->grid_src   = dma_buf != nullptr ? nullptr : grid_map.dev();
+  job->uploaded   = nullptr;
+  job->grid_src   = grid_map.dev();
   job->grid_dst   = d_grid;
   job->grid_bytes = gbytes;
   build_layout(*job, *arena);

@@ -114,8 +114,7 @@ struct srsgpu_ldpc_decoder_plan {
     bool      packed  = false;
     int       max_layers = 0;
     int       split   = 1;   ///< 2: edge-split kernel (each row's edges over two wave halves), see upload_decoder_plan
-    int       pack    = 1;   ///< LDPC_PK4 / 2: multi-codeblock workgroups (count = workgroups), see pk4_layout_for /
-                             ///< pair_layout_for
+    int       pack    = 1;   ///< 2: two-codeblock workgroups (count = workgroups), see pair_layout_for
     int       threads = 64;
     int       count   = 0;
     dec_desc* d_desc  = nullptr;
@@ -374,10 +373,9 @@ int srsgpu_context_create(int device, srsgpu_context** out)
     // The decoder reads its shifts through scalar loads, which are dword-granular: it gets a 32-bit copy.
     std::vector<uint32_t> tab32(tab.begin(), tab.end());
     // Packed decoder: rows z and z + H of a lane read the pair at min(2z + A, 2z + B) (row z) and its partner byte.
-    // PK4 (multi-codeblock workgroups, ldpc_decoder_pk.hip): pairs are 2 LDPC_PK4 bytes apart in the interleaved
-    // image, the lane constant is 2 LDPC_PK4 z + 2 slot: A = 2 PK4 s' + hi, B = 2 PK4 (s' - H) + 1 - hi.
-    std::vector<uint32_t> ab(static_cast<size_t>(51) * ne, 0u), ab4(static_cast<size_t>(51) * ne, 0u),
-        ab2(static_cast<size_t>(51) * ne, 0u);
+    // Two-codeblock workgroups (ldpc_decoder_pk.hip): pairs are 4 bytes apart in the interleaved image, the lane
+    // constant is 4 z + 2 slot: A = 4 s' + hi, B = 4 (s' - H) + 1 - hi.
+    std::vector<uint32_t> ab(static_cast<size_t>(51) * ne, 0u), ab2(static_cast<size_t>(51) * ne, 0u);
     for (int p = 0; p < 51; ++p) {
       const int Z = kLiftingSizes[p];
       if (Z % 2 != 0) {
@@ -392,10 +390,6 @@ int srsgpu_context_create(int device, srsgpu_context** out)
         const int B   = 2 * sm - 2 * H + 1 - hi;
         // One dword per edge: A in the low half, B (negative: wraps) in the high half.
         ab[static_cast<size_t>(p) * ne + e] = static_cast<uint32_t>(A) | (static_cast<uint32_t>(B & 0xffff) << 16);
-        const int A4 = 2 * LDPC_PK4 * sm + hi;
-        const int B4 = 2 * LDPC_PK4 * (sm - H) + 1 - hi;
-        ab4[static_cast<size_t>(p) * ne + e] =
-            static_cast<uint32_t>(A4) | (static_cast<uint32_t>(B4 & 0xffff) << 16);
         const int A2 = 4 * sm + hi;  // two-codeblock workgroups (PKN = 2)
         const int B2 = 4 * (sm - H) + 1 - hi;
         ab2[static_cast<size_t>(p) * ne + e] =
@@ -404,9 +398,6 @@ int srsgpu_context_create(int device, srsgpu_context** out)
     }
     if (hipMalloc(&ctx->d_pair_ab[bg - 1], ab.size() * sizeof(uint32_t)) != hipSuccess ||
         hipMemcpy(ctx->d_pair_ab[bg - 1], ab.data(), ab.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
-            hipSuccess ||
-        hipMalloc(&ctx->d_pair_ab4[bg - 1], ab4.size() * sizeof(uint32_t)) != hipSuccess ||
-        hipMemcpy(ctx->d_pair_ab4[bg - 1], ab4.data(), ab4.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
             hipSuccess ||
         hipMalloc(&ctx->d_pair_ab2[bg - 1], ab2.size() * sizeof(uint32_t)) != hipSuccess ||
         hipMemcpy(ctx->d_pair_ab2[bg - 1], ab2.data(), ab2.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
@@ -485,6 +476,59 @@ int srsgpu_context_device(const srsgpu_context* ctx)
   return ctx == nullptr ? -1 : ctx->device;
 }
 
+namespace {
+
+int* context_option(srsgpu_context* ctx, int option)
+{
+  switch (option) {
+    case SRSGPU_OPTION_DECODER_SPLIT:
+      return &ctx->opt_decoder_split;
+    case SRSGPU_OPTION_DECODER_PAIRS:
+      return &ctx->opt_decoder_pairs;
+    case SRSGPU_OPTION_DECODER_FUSED_DEMATCH:
+      return &ctx->opt_decoder_fused_dematch;
+    case SRSGPU_OPTION_ENCODER_BYTE_KERNEL:
+      return &ctx->opt_encoder_byte_kernel;
+    case SRSGPU_OPTION_ENCODER_ZERO_OUTPUT:
+      return &ctx->opt_encoder_zero_output;
+    default:
+      return nullptr;
+  }
+}
+
+} // namespace
+
+int srsgpu_context_set_option(srsgpu_context* ctx, int option, int value)
+{
+  if (ctx == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null context");
+  }
+  int* slot = context_option(ctx, option);
+  if (slot == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "unknown option %d", option);
+  }
+  const int lo = option == SRSGPU_OPTION_DECODER_SPLIT ? -1 : 0;
+  if (value < lo || value > 1) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "option %d: invalid value %d", option, value);
+  }
+  std::lock_guard<std::mutex> lock(ctx->mtx);
+  *slot = value;
+  return SRSGPU_OK;
+}
+
+int srsgpu_context_get_option(const srsgpu_context* ctx, int option, int* value)
+{
+  if (ctx == nullptr || value == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  const int* slot = context_option(const_cast<srsgpu_context*>(ctx), option);
+  if (slot == nullptr) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "unknown option %d", option);
+  }
+  *value = *slot;
+  return SRSGPU_OK;
+}
+
 void srsgpu_context_destroy(srsgpu_context* ctx)
 {
   if (ctx == nullptr) {
@@ -497,11 +541,6 @@ void srsgpu_context_destroy(srsgpu_context* ctx)
     }
   }
   for (auto* p : ctx->d_shifts32) {
-    if (p != nullptr) {
-      (void)hipFree(p);
-    }
-  }
-  for (auto* p : ctx->d_pair_ab4) {
     if (p != nullptr) {
       (void)hipFree(p);
     }
@@ -637,133 +676,18 @@ int add_decoder_cb(srsgpu_context* ctx,
   return SRSGPU_OK;
 }
 
-/// Workgroup layout of a packed-kernel launch group on the multi-codeblock kernel (ldpc_decode_pk4_kernel).
-struct pk4_layout {
-  int                   threads = 0;
-  int                   groups  = 0;
-  std::vector<dec_desc> slots;  ///< groups x LDPC_PK4 descriptors, empty slots zero
-};
-
-/// Issue cost model of a decoder launch (the kernel is bound by wave-instruction issue, profiles/r3_decoder_z_sweep.log:
-/// a codeblock costs the waves its lanes span, whatever their fill): active waves, stretched when fewer than 16 waves
-/// fit a CU (4 per SIMD are needed for the SIMD's VALU rate; one wave issues at a quarter of it).
-double decoder_issue_cost(long active_waves, int threads, int max_layers, size_t lds_bytes)
-{
-  const int wpg      = threads / 64;
-  const int simd_cap = max_layers <= 8 ? 5 : 4;  // waves per SIMD at the kernels' VGPR counts
-  // A workgroup's waves go round-robin over the CU's 4 SIMDs: above 4 waves one SIMD takes ceil(w / 4) of them, so
-  // e.g. a 9-wave workgroup (3 on one SIMD) leaves no room for a second at 5 waves per SIMD (measured: PK4, r3).
-  const int by_vgpr  = wpg <= 4 ? (4 * simd_cap) / wpg : simd_cap / ((wpg + 3) / 4);
-  const int by_lds   = static_cast<int>((160u * 1024u) / lds_bytes);
-  const int resident = std::min(by_vgpr, by_lds) * wpg;
-  if (resident <= 0) {
-    return 1e300;
-  }
-  return static_cast<double>(active_waves) * std::max(1.0, 16.0 / resident);
-}
-
-/// Chooses whether a packed-kernel launch group runs on the multi-codeblock kernel, and its workgroup size: codeblocks
-/// sharing the workgroup-uniform parameters (Z, scaling, iteration limit, CRC mode) are packed LDPC_PK4 at a time
-/// (fewer if c Z / 2 lanes exceed the workgroup), over every workgroup size of 64..LDPC_PK4 x 192 lanes, the size with
-/// the lowest modelled cost.
-bool pk4_layout_for(int bg, int max_layers, const std::vector<dec_desc>& cbs, pk4_layout& out)
-{
-  // Opt-in (SRSGPU_DECODER_PK4=1) until it wins on the box: measured round 3 (profiles/r3_decoder_pk4_scaling.log, r3_decoder_pk4_bench_ab.txt), the
-  // packed workgroups do not beat the one-codeblock kernel at equal work although they issue 25 % fewer waves.
-  const char* env = std::getenv("SRSGPU_DECODER_PK4");
-  if (env == nullptr || env[0] != '1' || max_layers > 16 || cbs.empty()) {
-    return false;
-  }
-  const int K = (bg == 1) ? kBG1_K : kBG2_K;
-  std::vector<dec_desc> v(cbs);
-  auto                  key = [](const dec_desc& d) {
-    return std::make_tuple(d.Z, d.sf16, d.max_iter, static_cast<uint32_t>(d.flags), d.crc_table == NO_CRC_TABLE);
-  };
-  std::stable_sort(v.begin(), v.end(), [&](const dec_desc& a, const dec_desc& b) { return key(a) < key(b); });
-  // Runs of equal keys (a run's codeblocks may share workgroups; the scaling float follows sf16).
-  std::vector<std::pair<size_t, size_t>> runs;
-  for (size_t i = 0; i < v.size();) {
-    size_t j = i + 1;
-    while (j < v.size() && key(v[j]) == key(v[i]) && v[j].sf == v[i].sf) {
-      ++j;
-    }
-    runs.emplace_back(i, j);
-    i = j;
-  }
-  const size_t lds4  = static_cast<size_t>(LDPC_PK4) * (K + max_layers) * SOFT_COL_STRIDE + 1024;
-  double       best  = 1e300;
-  int          best_t = 0;
-  const char*  tenv   = std::getenv("SRSGPU_DECODER_PK4_THREADS");  // A/B: one workgroup size only
-  const int    t_only = tenv != nullptr ? std::atoi(tenv) : 0;
-  for (int t = 64; t <= LDPC_PK4 * 192; t += 64) {
-    if (t_only > 0 && t != t_only) {
-      continue;
-    }
-    long active = 0;
-    bool ok     = true;
-    for (const auto& r : runs) {
-      const int H = v[r.first].Z / 2;
-      const int c = std::min(LDPC_PK4, t / H);
-      if (c == 0) {
-        ok = false;
-        break;
-      }
-      const long n = static_cast<long>(r.second - r.first);
-      active += (n / c) * ((c * H + 63) / 64) + ((n % c) != 0 ? ((n % c) * H + 63) / 64 : 0);
-    }
-    if (!ok) {
-      continue;
-    }
-    const double c4 = decoder_issue_cost(active, t, max_layers, lds4);
-    if (c4 < best) {
-      best   = c4;
-      best_t = t;
-    }
-  }
-  if (best_t == 0) {
-    return false;
-  }
-  out.threads = best_t;
-  out.slots.clear();
-  for (const auto& r : runs) {
-    const int c = std::min(LDPC_PK4, best_t / (v[r.first].Z / 2));
-    for (size_t i = r.first; i < r.second; i += static_cast<size_t>(c)) {
-      const size_t n = std::min(static_cast<size_t>(c), r.second - i);
-      for (size_t k = 0; k < static_cast<size_t>(LDPC_PK4); ++k) {
-        out.slots.push_back(k < n ? v[i + k] : dec_desc{});
-      }
-    }
-  }
-  out.groups = static_cast<int>(out.slots.size() / LDPC_PK4);
-  // The PK4 kernel counts a workgroup's occupied slots and treats slots [0, count) as used: every workgroup must hold
-  // its codeblocks first and its empty slots (a zero dec_desc, which aliases codeblock 0's outputs) last. A layout
-  // that breaks this is refused (the caller then launches the one-codeblock kernel).
-  for (int g = 0; g < out.groups; ++g) {
-    bool empty_seen = false;
-    for (int k = 0; k < LDPC_PK4; ++k) {
-      const bool empty = out.slots[static_cast<size_t>(g) * LDPC_PK4 + k].nof_llr == 0;
-      if ((k == 0 && empty) || (empty_seen && !empty)) {
-        return false;
-      }
-      empty_seen = empty_seen || empty;
-    }
-  }
-  return true;
-}
-
-/// Two-codeblock workgroups (ldpc_decode_pk4_kernel with PKN = 2): a codeblock of H = Z / 2 in (64, 96] (Z = 144 ..
+/// Two-codeblock workgroups (ldpc_decode_pairs_kernel): a codeblock of H = Z / 2 in (64, 96] (Z = 144 ..
 /// 192) spans two waves of which the second is partly idle, while two of them fill three waves (Z = 192: 25 % fewer
 /// wave-instructions). Moves such codeblocks of `cbs` (and their dm_desc, when fused) into `pairs` / `pair_dms`, two
 /// slots per workgroup (codeblocks sharing Z, scaling, iteration limit and CRC mode; an odd one out leaves its second
-/// slot empty), keeping the others. Opt-in (SRSGPU_DECODER_PK2=1): measured at Z = 192 (8-layer span,
+/// slot empty), keeping the others. Opt-in (SRSGPU_OPTION_DECODER_PAIRS): measured at Z = 192 (8-layer span,
 /// tools/decoder_scaling.py, profiles/r5_decoder_pk2_scaling.txt) 2-7 % faster with all 6 iterations (8 192 codeblocks:
 /// 676 -> 631 us), equal with early stop at 2 iterations, 8 % slower at 1 024 codeblocks: far from the 25 % fewer
 /// waves (the wave shared by both codeblocks runs until the later one stops; 8-byte pair interleave).
-void pair_layout_for(std::vector<dec_desc>& cbs, std::vector<dm_desc>& dms, bool fused, std::vector<dec_desc>& pairs,
-                     std::vector<dm_desc>& pair_dms)
+void pair_layout_for(const srsgpu_context* ctx, std::vector<dec_desc>& cbs, std::vector<dm_desc>& dms, bool fused,
+                     std::vector<dec_desc>& pairs, std::vector<dm_desc>& pair_dms)
 {
-  const char* env = std::getenv("SRSGPU_DECODER_PK2");
-  if (env == nullptr || env[0] != '1') {
+  if (ctx->opt_decoder_pairs == 0) {
     return;
   }
   std::vector<size_t> idx, rest;
@@ -816,7 +740,7 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
     if (std::get<1>(kv.first) && std::get<2>(kv.first) <= 16) {
       std::vector<dec_desc> pairs;
       std::vector<dm_desc>  pair_dms;
-      pair_layout_for(cbs, dms, fused, pairs, pair_dms);
+      pair_layout_for(ctx, cbs, dms, fused, pairs, pair_dms);
       if (!pairs.empty()) {
         srsgpu_ldpc_decoder_plan::group gp;
         gp.bg         = std::get<0>(kv.first);
@@ -852,11 +776,10 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
     // Few codeblocks per launch leave the SIMDs with one or two waves each: the per-codeblock latency (instructions
     // per wave) then sets the kernel time, and the edge-split kernel halves it at ~15 % more total work. Above ~3
     // waves per SIMD of the plain kernel (MI355X: 1024 SIMDs) the launch is throughput-bound and keeps the plain one.
-    // SRSGPU_DECODER_SPLIT=0 / 1 forces either (A/B tests).
+    // SRSGPU_OPTION_DECODER_SPLIT forces either (parity tests).
     if (g.packed) {
-      const char* env    = std::getenv("SRSGPU_DECODER_SPLIT");
-      const long  waves  = static_cast<long>(g.count) * (g.threads / 64);
-      const bool  split2 = env != nullptr ? (env[0] == '1') : (waves < 3L * 1024L);
+      const long waves  = static_cast<long>(g.count) * (g.threads / 64);
+      const bool split2 = ctx->opt_decoder_split >= 0 ? (ctx->opt_decoder_split == 1) : (waves < 3L * 1024L);
       if (split2) {
         g.split = 2;
         g.threads *= 2;
@@ -879,16 +802,8 @@ int upload_decoder_plan(srsgpu_context* ctx, int impl, const dec_batch& batch, s
         return fail(SRSGPU_ERR_HIP, "failed to upload fused rate dematcher descriptors");
       }
     }
-    pk4_layout             pk4;
-    const dec_desc*        src   = cbs.data();
-    size_t                 bytes = cbs.size() * sizeof(dec_desc);
-    if (g.packed && g.split == 1 && !fused && pk4_layout_for(g.bg, g.max_layers, cbs, pk4)) {
-      g.pack    = LDPC_PK4;
-      g.threads = pk4.threads;
-      g.count   = pk4.groups;
-      src       = pk4.slots.data();
-      bytes     = pk4.slots.size() * sizeof(dec_desc);
-    }
+    const dec_desc* src   = cbs.data();
+    const size_t    bytes = cbs.size() * sizeof(dec_desc);
     if (hipMalloc(&g.d_desc, bytes) != hipSuccess ||
         hipMemcpy(g.d_desc, src, bytes, hipMemcpyHostToDevice) != hipSuccess) {
       plan->groups.push_back(g);
@@ -914,15 +829,14 @@ int execute_decoder_plan(const srsgpu_ldpc_decoder_plan* plan,
                          int8_t* const*                  d_harq_cbs = nullptr)
 {
   for (const auto& g : plan->groups) {
-    if (g.pack == LDPC_PK4 || g.pack == 2) {
+    if (g.pack == 2) {
       if (g.d_dm != nullptr && (d_cw_llrs == nullptr || (d_harq == nullptr && d_harq_cbs == nullptr))) {
         return fail(SRSGPU_ERR_INVALID_ARG, "fused decoder group without codeword LLRs / HARQ buffer");
       }
-      launch_ldpc_decode_pk4(g.bg, plan->impl, g.max_layers, g.d_desc, g.count, g.threads,
-                             g.d_dm != nullptr ? d_cw_llrs : d_llrs, d_out, d_nof_iterations,
-                             g.pack == 2 ? plan->ctx->d_pair_ab2[g.bg - 1] : plan->ctx->d_pair_ab4[g.bg - 1],
-                             plan->ctx->d_crc_arena, d_cb_crc_ok, s, d_harq_cbs, g.pack, g.d_dm,
-                             g.d_dm != nullptr ? d_harq : nullptr);
+      launch_ldpc_decode_pairs(g.bg, plan->impl, g.max_layers, g.d_desc, g.count, g.threads,
+                               g.d_dm != nullptr ? d_cw_llrs : d_llrs, d_out, d_nof_iterations,
+                               plan->ctx->d_pair_ab2[g.bg - 1], plan->ctx->d_crc_arena, d_cb_crc_ok, s, d_harq_cbs,
+                               g.d_dm, g.d_dm != nullptr ? d_harq : nullptr);
     } else if (g.packed) {
       if (g.d_dm != nullptr && (d_cw_llrs == nullptr || (d_harq == nullptr && d_harq_cbs == nullptr))) {
         return fail(SRSGPU_ERR_INVALID_ARG, "fused decoder group without codeword LLRs / HARQ buffer");
@@ -1004,10 +918,8 @@ int add_pusch_cb(srsgpu_context*        ctx,
   // A first transmission from rv 0 of the whole circular buffer that reaches every systematic position without
   // wrapping (ninfo <= E <= V) is a plain copy that defines every HARQ position (copies, fillers, zeroed tail): the
   // packed decoder dematches it itself (ldpc_decode_pk_kernel FUSE) and the rate dematcher skips it.
-  // SRSGPU_DECODER_FUSED_DM=0 keeps every codeblock on the separate rate dematcher (A/B).
-  const char* fuse_env     = std::getenv("SRSGPU_DECODER_FUSED_DM");
-  const bool  fuse_enabled = fuse_env == nullptr || fuse_env[0] != '0';
-  const bool fuse = fuse_enabled && c.new_data && d.v0 == 0 && Ncb == N && static_cast<int>(c.E) >= ninfo &&
+  // SRSGPU_OPTION_DECODER_FUSED_DEMATCH = 0 keeps every codeblock on the separate rate dematcher (parity tests).
+  const bool fuse = ctx->opt_decoder_fused_dematch != 0 && c.new_data && d.v0 == 0 && Ncb == N && static_cast<int>(c.E) >= ninfo &&
                     static_cast<int>(c.E) <= Ncb - c.filler && (Z % 2) == 0;
   if (!fuse) {
     dms.push_back(d);
@@ -1250,9 +1162,8 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
   std::vector<tb_crc_desc> tbd(nof_tbs);
   std::vector<enc_desc>    encs[2], encs_pk[2];
   int                      maxz[2]   = {0, 0};
-  // SRSGPU_ENCODER_BYTE_KERNEL=1 routes every codeblock to the byte kernel (A/B parity checks of the packed kernel).
-  const char* force_env         = std::getenv("SRSGPU_ENCODER_BYTE_KERNEL");
-  const bool  force_byte_kernel = force_env != nullptr && force_env[0] == '1';
+  // SRSGPU_OPTION_ENCODER_BYTE_KERNEL routes every codeblock to the byte kernel (parity checks of both kernels).
+  const bool               force_byte_kernel = ctx->opt_encoder_byte_kernel != 0;
   size_t                   out_begin = ~size_t(0), out_end = 0;
   bool                     word_aligned = true;  // every codeblock starts and ends on a 32-bit word boundary
   std::vector<std::pair<size_t, size_t>> cw_ranges;  // [begin, end) bytes of each TB's codeword
@@ -1346,8 +1257,7 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
       tiled = cw_ranges[i].first == cw_ranges[i - 1].second;
     }
   }
-  const char* zero_env = std::getenv("SRSGPU_ENCODER_ZERO");
-  const bool  zero_out = !tiled || (zero_env != nullptr && zero_env[0] == '1');
+  const bool zero_out = !tiled || ctx->opt_encoder_zero_output != 0;
   // TB CRC slices: a TB with a contribution table is spread over TB_CRC_SLICE_BYTES ranges (a max-TBS TB of one
   // workgroup would otherwise serialise ~150 KB of byte-table steps); without a table it stays one slice.
   std::vector<tb_crc_slice> slices;
@@ -1388,9 +1298,7 @@ int srsgpu_pdsch_encoder_plan_create(srsgpu_context*               ctx,
     srsgpu_pdsch_encoder_plan_destroy(plan);
     return fail(SRSGPU_ERR_HIP, "failed to upload encoder descriptors");
   }
-  // SRSGPU_ENCODER_TB_CRC_INLINE=0: always the separate tb_crc_kernel (A/B).
-  const char* inl_env = std::getenv("SRSGPU_ENCODER_TB_CRC_INLINE");
-  plan->inline_tb_crc = (inl_env == nullptr || inl_env[0] != '0') && plan->count[0] == 0 && plan->count[1] == 0 &&
+  plan->inline_tb_crc = plan->count[0] == 0 && plan->count[1] == 0 &&
                         std::all_of(tbd.begin(), tbd.end(), [](const tb_crc_desc& t) {
                           return t.table != NO_CRC_TABLE && t.nbytes <= TB_CRC_INLINE_MAX_BYTES;
                         });
@@ -1562,11 +1470,7 @@ int srsgpu_pusch_decoder_plan_create(srsgpu_context*               ctx,
     return t.nof_cbs > 1 && t.crc_table != NO_CRC_TABLE && (t.cb_data_bits & 7u) == 0;
   });
   std::vector<tb_slice> slices;
-  static const bool slicing = [] {
-    const char* e = std::getenv("SRSGPU_TB_SLICED");  // A/B: 0 = one workgroup per TB
-    return e == nullptr || e[0] != '0';
-  }();
-  if (slicing && sliceable && any_large && tbs.size() <= 8) {
+  if (sliceable && any_large && tbs.size() <= 8) {
     for (uint32_t t = 0; t < tbs.size(); ++t) {
       const uint32_t bytes = tbs[t].tbs_bits / 8u;
       const uint32_t n     = (bytes + TB_SLICE_BYTES - 1) / TB_SLICE_BYTES;

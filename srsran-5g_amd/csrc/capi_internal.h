@@ -62,8 +62,7 @@ struct srsgpu_context {
   uint32_t*                            d_shifts32[2] = {nullptr, nullptr};  ///< Same, one dword per shift (decoder).
   /// Packed decoder address constants A | B << 16 per (Z position, edge), see ldpc_decoder_pk.hip (even Z only).
   uint32_t*                            d_pair_ab[2] = {nullptr, nullptr};
-  uint32_t*                            d_pair_ab4[2] = {nullptr, nullptr};  ///< Same for the PK4 interleaved image.
-  uint32_t*                            d_pair_ab2[2] = {nullptr, nullptr};  ///< ... and the two-codeblock one.
+  uint32_t*                            d_pair_ab2[2] = {nullptr, nullptr};  ///< Same for the two-codeblock image.
   srsgpu::core_plan*                   d_core[2]   = {nullptr, nullptr};
   std::vector<srsgpu::core_plan>       core[2];
   uint32_t*                            d_crc_arena = nullptr;
@@ -80,6 +79,12 @@ struct srsgpu_context {
   uint32_t*                            d_gold_x2_lane = nullptr;
   /// OFDM DFT twiddles exp(-j 2 pi m / OFDM_MAX_DFT) as (re, im) floats (built on first use).
   float*                               d_ofdm_twiddles = nullptr;
+  /// srsgpu_option values (srsgpu_context_set_option), read at plan creation.
+  int opt_decoder_split         = -1;
+  int opt_decoder_pairs         = 0;
+  int opt_decoder_fused_dematch = 1;
+  int opt_encoder_byte_kernel   = 0;
+  int opt_encoder_zero_output   = 0;
   std::mutex                           mtx;
 };
 

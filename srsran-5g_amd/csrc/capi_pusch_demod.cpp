@@ -20,8 +20,6 @@ struct srsgpu_pusch_demodulator_plan {
   uint32_t*             d_seq      = nullptr;  ///< Descrambling sequences of the transmissions (plan lifetime).
   uint16_t*             d_crbs     = nullptr;  ///< Allocated CRB lists of the CRB-mask transmissions.
   float*                d_acc      = nullptr;  ///< Statistics accumulators (zero between executes).
-  uint32_t*             d_cnt      = nullptr;  ///< Per transmission: [workgroups that add to it, finished so far].
-  bool                  fuse_stats = false;    ///< The demodulator's last workgroup per transmission writes its stats.
   int                   nof_chunks = 0;
   int                   chunk_threads = 256;  ///< Lanes per chunk workgroup (launch_pusch_demodulate).
   int                   nof_tp_jobs = 0;
@@ -248,7 +246,7 @@ int srsgpu_pusch_demodulator_plan_create_ex(srsgpu_context*                  ctx
   // 256 lanes instead, so the latency of the launch is about one RE per lane.
   uint32_t chunk_words = DEMOD_CHUNK_WORDS;
   bool     small_plan  = false;
-  if (total_words < 256u * DEMOD_CHUNK_WORDS && std::getenv("SRSGPU_DEMOD_FIXED_CHUNKS") == nullptr) {
+  if (total_words < 256u * DEMOD_CHUNK_WORDS) {
     small_plan  = true;
     chunk_words = std::min<uint32_t>(DEMOD_CHUNK_WORDS, std::max<uint32_t>(8u, 8u * max_lq));
   }
@@ -345,30 +343,6 @@ int srsgpu_pusch_demodulator_plan_create_ex(srsgpu_context*                  ctx
   if (ok && nof_tx > 0) {
     const size_t acc_bytes = static_cast<size_t>(nof_tx) * DEMOD_ACC_PER_TX * sizeof(float);
     ok = hipMalloc(&plan->d_acc, acc_bytes) == hipSuccess && hipMemset(plan->d_acc, 0, acc_bytes) == hipSuccess;
-    // SRSGPU_DEMOD_STATS_FUSED=1 (A/B): the statistics finished by the last workgroup of each transmission instead of a
-    // separate launch (needs a workgroup per transmission). Measured slower on MI355X (one-PDU 273-PRB slot: fused
-    // demodulator 23.8 us against 8.7 + 7.7 us): the device-scope fences and counter atomics of every workgroup cost
-    // more than the launch they save.
-    std::vector<uint32_t> cnt(2 * static_cast<size_t>(nof_tx), 0u);
-    for (const mod_chunk& ch : chunks) {
-      ++cnt[2 * ch.tx];
-    }
-    for (const demod_tp_job& j : tp_jobs) {
-      ++cnt[2 * j.tx];
-    }
-    static const bool separate = [] {
-      const char* e = std::getenv("SRSGPU_DEMOD_STATS_FUSED");
-      return e == nullptr || e[0] != '1';
-    }();
-    bool              all      = true;
-    for (uint32_t t = 0; t < nof_tx; ++t) {
-      all = all && cnt[2 * t] > 0;
-    }
-    plan->fuse_stats = all && !separate;
-    if (ok && plan->fuse_stats) {
-      ok = hipMalloc(&plan->d_cnt, cnt.size() * sizeof(uint32_t)) == hipSuccess &&
-           hipMemcpy(plan->d_cnt, cnt.data(), cnt.size() * sizeof(uint32_t), hipMemcpyHostToDevice) == hipSuccess;
-    }
   }
   if (!ok) {
     srsgpu_pusch_demodulator_plan_destroy(plan);
@@ -410,15 +384,12 @@ int srsgpu_pusch_demodulator_plan_execute_ex(const srsgpu_pusch_demodulator_plan
     return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
   }
   const hipStream_t s   = static_cast<hipStream_t>(stream);
-  float*            acc   = d_stats != nullptr ? plan->d_acc : nullptr;
-  const bool        fused = d_stats != nullptr && plan->fuse_stats;
-  float*            fst   = fused ? d_stats : nullptr;
-  uint32_t*         fcnt  = fused ? plan->d_cnt : nullptr;
+  float*            acc = d_stats != nullptr ? plan->d_acc : nullptr;
   launch_pusch_demodulate(plan->d_desc, plan->d_chunks, plan->nof_chunks, plan->chunk_threads, plan->d_tables,
-                          d_grids, d_ch_estimates, d_noise_var, d_llrs, plan->d_seq, plan->d_crbs, acc, s, fst, fcnt);
+                          d_grids, d_ch_estimates, d_noise_var, d_llrs, plan->d_seq, plan->d_crbs, acc, s);
   launch_pusch_demodulate_tp(plan->d_desc, plan->d_tp_jobs, plan->nof_tp_jobs, plan->d_tables, d_grids,
-                             d_ch_estimates, d_noise_var, d_llrs, plan->d_seq, plan->d_crbs, acc, s, fst, fcnt);
-  if (d_stats != nullptr && !fused) {
+                             d_ch_estimates, d_noise_var, d_llrs, plan->d_seq, plan->d_crbs, acc, s);
+  if (d_stats != nullptr) {
     launch_pusch_demod_stats(plan->d_acc, d_stats, plan->nof_tx, s);
   }
   HIP_TRY(hipGetLastError());
@@ -432,8 +403,7 @@ void srsgpu_pusch_demodulator_plan_destroy(srsgpu_pusch_demodulator_plan* plan)
   }
   for (void* p : {static_cast<void*>(plan->d_desc), static_cast<void*>(plan->d_chunks),
                   static_cast<void*>(plan->d_tp_jobs), static_cast<void*>(plan->d_tables),
-                  static_cast<void*>(plan->d_seq), static_cast<void*>(plan->d_crbs), static_cast<void*>(plan->d_acc),
-                  static_cast<void*>(plan->d_cnt)}) {
+                  static_cast<void*>(plan->d_seq), static_cast<void*>(plan->d_crbs), static_cast<void*>(plan->d_acc)}) {
     if (p != nullptr) {
       (void)hipFree(p);
     }

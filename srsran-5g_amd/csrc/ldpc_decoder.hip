@@ -25,9 +25,7 @@ namespace srsgpu {
 namespace {
 using namespace ldpc_dec;
 
-#ifndef LDPC_DEC_MIN_WAVES
-#define LDPC_DEC_MIN_WAVES 4
-#endif
+constexpr int LDPC_DEC_MIN_WAVES = 4;
 
 #ifdef LDPC_DEC_PROFILE
 // Instrumented build only (SRSGPU_EXTRA_FLAGS=-DLDPC_DEC_PROFILE): per-codeblock s_memtime stamps of the decoder

@@ -69,65 +69,27 @@ __device__ __forceinline__ u16x2 uu(int x)
 }
 /// Packed 16-bit VALU instructions issue at about two thirds of the rate of 32-bit ones on gfx950
 /// (profiles/r3_valu_rate_probe_*.log): where an operation is bitwise the 32-bit form serves both halves.
-#ifndef LDPC_PK_XOR_ARGMIN
-#define LDPC_PK_XOR_ARGMIN 1
-#endif
-#ifndef LDPC_PK_SAT_INF
-#define LDPC_PK_SAT_INF 1
-#endif
-/// 1: fused 256QAM dematching writes the HARQ buffer in dwords (0: bytes; A/B).
-#ifndef LDPC_PK_HARQ_X4
-#define LDPC_PK_HARQ_X4 1
-#endif
-/// 1: a row's two-minimum search runs after all of its v2c values (156 instead of 360 hazard s_nops per 8-layer
-/// iteration, decoder launch 188 -> 184 us) - but the bench does not move (129.6k vs 128.9k slots/s,
-/// profiles/r3_decoder_phased_ab.txt: the other waves of a SIMD fill the nop slots), so edge by edge stays the default.
-#ifndef LDPC_PK_PHASED
-#define LDPC_PK_PHASED 0
-#endif
-
-/// 1: a row's two-minimum search runs as two independent chains (even and odd edges) merged at the end
-/// (k1 = min(k1a, k1b), k2 = min(max(k1a, k1b), k2a, k2b): the exact result of the sequential scan, since the keys
-/// |v| * 32 + e are distinct) - half the serial min/max dependency chain of a 19-edge row (A/B switch).
-/// Soft-bit loads issued this many edges ahead of their use in a row's first pass (0: the compiler's placement, one
-/// edge ahead); LDPC_PK_PRELOAD_GROUPS > 0 also pins the pattern (that many VALU, then the next edge's two loads).
-#ifndef LDPC_PK_PRELOAD
-#define LDPC_PK_PRELOAD 0
-#endif
-#ifndef LDPC_PK_PRELOAD_GROUPS
-#define LDPC_PK_PRELOAD_GROUPS 0
-#endif
-
-#ifndef LDPC_PK_SPLIT_SEARCH
-#define LDPC_PK_SPLIT_SEARCH 0
-#endif
-
 /// 1 where IDX != e, 0 where IDX == e (both halves): IDX ^ e (one 32-bit v_xor on both 5-bit halves), then one
 /// v_pk_min_u16 against an opaque 0x00010001 (a visible constant 1 gets the min rewritten into per-half compares and
 /// cndmasks).
 __device__ __forceinline__ u16x2 not_argmin(u16x2 idx, int e, u16x2 one)
 {
-#if LDPC_PK_XOR_ARGMIN
   return __builtin_elementwise_min(as_u16(bits(idx) ^ (0x00010001u * static_cast<uint32_t>(e))), one);
-#else
-  return __builtin_elementwise_min(idx - uu(e), one);  // v_pk_sub_u16 with e inline and op_sel_hi broadcast
-#endif
 }
 
 /// Opaque packed multipliers 32 and 512: with a visible power of two the compiler splits a multiply-add into a
 /// shift and an add / or (two VALU instead of one v_pk_mad).
 struct pk_consts {
   u16x2    k32;
-  s16x2    k512;
-  uint32_t k271, kn271, kn21;  ///< 271, -271, -21 in both halves (SGPRs; LDPC_PK_SAT_INF)
+  uint32_t k271, kn271, kn21;  ///< 271, -271, -21 in both halves (SGPRs)
 };
 __device__ __forceinline__ pk_consts make_pk_consts()
 {
-  uint32_t a = 0x00200020u, b = 0x02000200u;
-  asm("" : "+v"(a), "+v"(b));
+  uint32_t a = 0x00200020u;
+  asm("" : "+v"(a));
   uint32_t c = 0x010f010fu, d = 0xfef1fef1u, f = 0xffebffebu;
   asm("" : "+s"(c), "+s"(d), "+s"(f));
-  return {as_u16(a), as_s16(b), c, d, f};
+  return {as_u16(a), c, d, f};
 }
 
 /// v2c of an edge from its soft bit sb and previous c2v magnitude om with sign mask n (0 / -1):
@@ -138,7 +100,6 @@ __device__ __forceinline__ s16x2 v2c_pk(s16x2 sb, u16x2 om, s16x2 n, const pk_co
   const s16x2 nn  = as_s16(~bits(n) | 0x00010001u);
   const s16x2 t   = as_s16(bits(om)) * nn + sb;
   const s16x2 ct  = __builtin_elementwise_min(__builtin_elementwise_max(t, ss(-LLR_MAX)), ss(LLR_MAX));
-#if LDPC_PK_SAT_INF
   // Infinity marker without clamping sb: g = sat16(271 sb) - 271 sb is 0 for |sb| <= 120 (271 x 120 = 32520) and
   // -24 / +23 for sb = +121 / -121 (the saturating v_pk_mad_i16 clamps 32791 to 32767); v = clamp(t) - 21 g puts an
   // infinite soft bit's v2c at +505..624 / -603..-484 (|v2c| >= 392 stays infinite; keys < 2^16).
@@ -146,10 +107,6 @@ __device__ __forceinline__ s16x2 v2c_pk(s16x2 sb, u16x2 om, s16x2 n, const pk_co
   asm("v_pk_mad_i16 %0, %1, %2, 0 clamp" : "=v"(sat) : "v"(bits(sb)), "s"(kc.k271));
   const s16x2 g = sb * as_s16(kc.kn271) + as_s16(sat);
   return g * as_s16(kc.kn21) + ct;
-#else
-  const s16x2 fin = __builtin_elementwise_min(__builtin_elementwise_max(sb, ss(-LLR_MAX)), ss(LLR_MAX));
-  return (sb - fin) * kc.k512 + ct;
-#endif
 }
 
 /// Search key |v| * 32 + e of the two-minimum scan (one v_pk_mad).
@@ -193,17 +150,15 @@ __device__ __forceinline__ u16x2 scale_pk(u16x2 m, const scale_t& sc)
   }
 }
 
-/// 1: the row-z and partner LDS addresses of every edge stay in VGPRs between the two passes of a row; 0: only the
-/// row-z one (A/B switch).
-#ifndef LDPC_PK_KEEP_PARTNER
-#define LDPC_PK_KEEP_PARTNER 1
-#endif
+/// Bound on the CRC table loads in flight (each holds a result register): a scheduling barrier every CRC_CHUNK
+/// systematic columns.
+constexpr int CRC_CHUNK = 8;
 
-#ifndef LDPC_PK_CRC_CHUNK
-#define LDPC_PK_CRC_CHUNK 8
-#endif
-/// Systematic columns per batch of CRC table loads.
-constexpr int CRC_CHUNK = LDPC_PK_CRC_CHUNK;
+/// Occupancy of the 8-layer class: at least 5 workgroups per CU (96 VGPRs, 5 waves per SIMD); 8 with the pass-1
+/// addresses recomputed measured slower (r2: 117.8k vs 112.6k slots/s).
+constexpr int PK_MIN_BLOCKS_8 = 5;
+/// Layer bound up to which a row's pass-1 pair addresses stay in VGPRs for pass 2 (above it they are recomputed).
+constexpr int PK_KEEP_ADDR_MAXL = 16;
 
 /// Sign bits of edge e: bit e (e < 11) of the sign word or bit e - 11 of the hi word, in both halves.
 constexpr int SIGNS_W0 = 11;
@@ -229,9 +184,6 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   const u16x2 IDX = as_u16(sgw) >> uu(11);
   s16x2       v2c[deg];
   u16x2       k1 = uu(KEY_INIT), k2 = uu(KEY_INIT);
-#if LDPC_PK_SPLIT_SEARCH
-  u16x2 k1b = uu(KEY_INIT), k2b = uu(KEY_INIT);  // the odd edges' chain
-#endif
   uint32_t    sx = 0;
   uint32_t    one_bits = 0x00010001u;
   asm("" : "+v"(one_bits));
@@ -239,47 +191,15 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   const pk_consts kc  = make_pk_consts();
 
   uint32_t addr[KEEP_ADDR ? deg : 1];
-#if LDPC_PK_PRELOAD
-  // Soft-bit loads PD edges ahead of their use (a layer's positions are disjoint, so every load of the row may issue
-  // before any store); the group barriers keep the scheduler from sinking them next to their use.
-  constexpr int PD = LDPC_PK_PRELOAD < deg ? LDPC_PK_PRELOAD : deg;
-  uint32_t      aq[deg];
-  int           qa[deg], qb[deg];
-  auto          load_edge = [&](auto E) {
-    constexpr int e   = decltype(E)::value;
-    constexpr int col = G::col(e0 + e);
-    aq[e]             = pair_address(z2x2, ab[e0 + e]);
-    qa[e]             = soft[col * CS + aq[e]];
-    qb[e]             = soft[col * CS + (aq[e] ^ 1u)];
-  };
-  static_for<PD>(load_edge);
-  __builtin_amdgcn_sched_group_barrier(0x100, 2 * PD, 0);
-#endif
   static_for<deg>([&](auto E) {
     constexpr int  e   = decltype(E)::value;
-#if LDPC_PK_PRELOAD
-    if constexpr (e + PD < deg) {
-      load_edge(std::integral_constant<int, e + PD>{});
-    }
-    const uint32_t a = aq[e];
-    if constexpr (KEEP_ADDR) {
-      addr[e] = a;
-    }
-    const s16x2 sb{static_cast<short>(qa[e]), static_cast<short>(qb[e])};
-#else
     constexpr int  col = G::col(e0 + e);
     const uint32_t a   = pair_address(z2x2, ab[e0 + e]);
     if constexpr (KEEP_ADDR) {
       addr[e] = a;
     }
     // Two byte loads merged by one v_perm (d16 loads do not preserve the other half with SRAM ECC on gfx950).
-#ifndef LDPC_PK_EXPERIMENT_NO_LOADS
-    const s16x2 sb{static_cast<short>(soft[col * CS + a]),
-                   static_cast<short>(soft[col * CS + (a ^ 1u)])};
-#else  // timing experiments only
-    const s16x2 sb = as_s16(((a * 0x9e3779b1u) >> 3) & 0x003f003fu);
-#endif
-#endif
+    const s16x2 sb{static_cast<short>(soft[col * CS + a]), static_cast<short>(soft[col * CS + (a ^ 1u)])};
     // Previous c2v of this edge: magnitude min2 at the argmin, min1 elsewhere; sign from the sign bits.
     constexpr int  pos = (e < SIGNS_W0) ? e : e - SIGNS_W0;
     const uint32_t sw  = (e < SIGNS_W0) ? sgw : hiw;
@@ -289,56 +209,12 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     // v2c = soft - c2v saturated to +/-LLR_MAX; infinite soft bits give |v2c| >= 392 (stay infinite).
     const s16x2 v   = v2c_pk(sb, om, n, kc);
     v2c[e]          = v;
-#if !LDPC_PK_PHASED
     const u16x2 key = key_pk(v, e, kc);
-#if LDPC_PK_SPLIT_SEARCH
-    if constexpr (e % 2 == 1) {
-      k2b = __builtin_elementwise_min(__builtin_elementwise_max(key, k1b), k2b);
-      k1b = __builtin_elementwise_min(key, k1b);
-    } else
-#endif
-    {
-      k2 = __builtin_elementwise_min(__builtin_elementwise_max(key, k1), k2);
-      k1 = __builtin_elementwise_min(key, k1);
-    }
+    k2              = __builtin_elementwise_min(__builtin_elementwise_max(key, k1), k2);
+    k1              = __builtin_elementwise_min(key, k1);
     sx ^= bits(v);
-#endif
-#if LDPC_PK_PRELOAD && LDPC_PK_PRELOAD_GROUPS
-    if constexpr (e + PD < deg) {
-      __builtin_amdgcn_sched_group_barrier(0x002, LDPC_PK_PRELOAD_GROUPS, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-    }
-#endif
-#ifdef LDPC_PK_EXPERIMENT_EXTRA_VALU  // timing experiments only: N extra independent VALU per edge
-    {
-      uint32_t j0 = bits(v), j1 = bits(key);
-#pragma unroll
-      for (int x = 0; x < LDPC_PK_EXPERIMENT_EXTRA_VALU / 2; ++x) {
-        asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(j0) : "v"(j1));
-        asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(j1) : "v"(j0));
-      }
-      sx ^= (j0 ^ j1) & 0x00010001u & (j0 >> 30);
-    }
-#endif
   });
 
-#if LDPC_PK_PHASED
-  // The search after all of the row's v2c values exist: the per-edge chains (v2c -> |v2c| -> key) of different edges
-  // are independent, so the scheduler interleaves them instead of issuing one edge's dependent packed instructions
-  // back to back (each such pair costs an s_nop on gfx950).
-  static_for<deg>([&](auto E) {
-    constexpr int e   = decltype(E)::value;
-    const s16x2   v   = v2c[e];
-    const u16x2   key = key_pk(v, e, kc);
-    k2                = __builtin_elementwise_min(__builtin_elementwise_max(key, k1), k2);
-    k1                = __builtin_elementwise_min(key, k1);
-    sx ^= bits(v);
-  });
-#endif
-#if LDPC_PK_SPLIT_SEARCH && !LDPC_PK_PHASED
-  k2 = __builtin_elementwise_min(__builtin_elementwise_max(k1, k1b), __builtin_elementwise_min(k2, k2b));
-  k1 = __builtin_elementwise_min(k1, k1b);
-#endif
   const u16x2 IDXN = k1 & uu(31);
   const u16x2 S1N  = scale_pk<MODE>(k1 >> uu(5), sc);
   const u16x2 S2N  = scale_pk<MODE>(k2 >> uu(5), sc);
@@ -367,20 +243,11 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     uint32_t       a;
     if constexpr (KEEP_ADDR) {
       a = addr[e];
-#if !LDPC_PK_KEEP_PARTNER
-      // Keep only the row-z address between the passes (the partner a ^ 1 is recomputed: one VALU per edge for one
-      // VGPR per edge).
-      asm volatile("" : "+v"(a));
-#endif
     } else {
       a = pair_address(z2x2_b, ab[e0 + e]);
     }
-#ifndef LDPC_PK_EXPERIMENT_NO_STORES
     soft[col * CS + a]        = static_cast<int8_t>(sb.x);
     soft[col * CS + (a ^ 1u)] = static_cast<int8_t>(sb.y);
-#else  // timing experiments only: keep the values alive
-    nhi ^= bits(sb) + a;
-#endif
     constexpr int      pos  = (e < SIGNS_W0) ? e : e - SIGNS_W0;
     constexpr uint32_t mask = (1u << pos) | (1u << (16 + pos));
     if constexpr (e < SIGNS_W0) {
@@ -531,13 +398,7 @@ __device__ __forceinline__ void write_hard_bits_pk(const int8_t* __restrict__ so
 /// itself (dms[blockIdx.x]) into the LDS image and writes the HARQ soft buffer the separate rate_dematch_kernel would
 /// have written (rate_dematcher.hip dematch_new_data: copies symbol-major, fillers +127, the unreached tail zeroed).
 template <int BG, int MODE, int MAXL, int SPLIT, bool FUSE>
-#ifndef LDPC_PK_MIN_BLOCKS_8
-#define LDPC_PK_MIN_BLOCKS_8 5
-#endif
-#ifndef LDPC_PK_KEEP_ADDR_MAXL
-#define LDPC_PK_KEEP_ADDR_MAXL 16
-#endif
-__global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_8)))) void ldpc_decode_pk_kernel(const dec_desc* __restrict__ descs,
+__global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : PK_MIN_BLOCKS_8)))) void ldpc_decode_pk_kernel(const dec_desc* __restrict__ descs,
                                                              const int8_t* __restrict__ llrs,
                                                              uint8_t* __restrict__ out,
                                                              int32_t* __restrict__ results,
@@ -640,7 +501,7 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
     // 4-aligned R, ninfo, fillers and HARQ buffer (every bench codeblock): a lane takes four consecutive symbols and
     // writes each bit row's four HARQ bytes as one dword (8 dword stores per 4 symbols instead of 32 byte stores).
     const bool q8 = Qm == 8 && ((dm.llr_offset & 7u) == 0u);
-    const bool q8x4 = LDPC_PK_HARQ_X4 && q8 &&
+    const bool q8x4 = q8 &&
                       ((R | ninfo | Fl | static_cast<int>(reinterpret_cast<uintptr_t>(hb))) & 3) == 0;
     if (q8x4) {
       for (int r0 = 4 * static_cast<int>(threadIdx.x); r0 < R; r0 += 4 * static_cast<int>(blockDim.x)) {
@@ -872,13 +733,6 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
   __syncthreads();
 
   const int max_iter = d.max_iter;
-#ifdef LDPC_PK_INC_CRC
-  // Incremental CRC (a CRC is linear over GF(2): the remainder of the hard decisions is the XOR of the table entries of
-  // the set bits). Each lane keeps its previous hard decisions of its two positions per systematic column (bit c of
-  // crc_ha / crc_hb) and the XOR of the table entries of its set ones; an iteration XORs in or out only the entries of
-  // the positions that flipped, and a column no lane of the wave flipped costs no load. Bit-exact with the full sum.
-  uint32_t crc_ha = 0, crc_hb = 0, crc_lane = 0;
-#endif
   DEC_STAMP(1);
   DEC_PROF(31, static_cast<uint64_t>(nof_layers));
   for (int it = 0; it < max_iter; ++it) {
@@ -895,7 +749,7 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
         if constexpr (SPLIT == 1) {
           if (active) {
             __builtin_amdgcn_sched_barrier(0);
-            row_update_pk<BG, MODE, m, (MAXL <= LDPC_PK_KEEP_ADDR_MAXL)>(soft, abi, z2x2, sc, magw[m], sgw[m],
+            row_update_pk<BG, MODE, m, (MAXL <= PK_KEEP_ADDR_MAXL)>(soft, abi, z2x2, sc, magw[m], sgw[m],
                                                                          hiw[m & 3]);
             __builtin_amdgcn_sched_barrier(0);
           }
@@ -926,24 +780,15 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
             }
           }
         }
-#ifndef LDPC_PK_EXPERIMENT_NO_LAYER_BARRIER  // timing experiments only: results are wrong without the barrier
         __syncthreads();
-#endif
       }
     });
     DEC_STAMP(2 + 2 * (it & 7));
 
     // CRC after every iteration with early stop (ldpc_decoder_impl.cpp:133), else after the last one.
-#ifdef LDPC_PK_EXPERIMENT_CRC_LAST  // timing experiments only: no early stop (the worst case decodes identically)
-    if (use_crc && it == max_iter - 1) {
-#else
     if (use_crc && ((d.flags & DEC_FLAG_EARLY_STOP) != 0 || it == max_iter - 1)) {
-#endif
       uint32_t acc  = 0;
       uint32_t zero = 0;
-#ifdef LDPC_PK_INC_CRC
-      uint32_t fa = 0, fb = 0, inc_ia = 0, inc_zz = 0, inc_hh = 0;
-#endif
       if (active) {
         // Opaque copies again: per-column table offsets would otherwise be hoisted out of the iteration loop. The
         // table loads are unconditional (index clamped, value masked): no divergent branches between them, all of
@@ -958,24 +803,6 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
         const int     hcol = half * KC;
         uint32_t      ia   = zz + static_cast<uint32_t>(hcol) * ZZ;
         const int8_t* scol = soft + hcol * SOFT_COL_STRIDE;
-#ifdef LDPC_PK_INC_CRC
-        uint32_t ha = 0, hb = 0;
-        static_for<KC>([&](auto Ci) {
-          constexpr int c  = decltype(Ci)::value;
-          const int     sa = scol[c * SOFT_COL_STRIDE + 2 * zz];
-          const int     sb = scol[c * SOFT_COL_STRIDE + 2 * zz + 1];
-          zero |= static_cast<uint32_t>(sa == 0) | static_cast<uint32_t>(sb == 0);
-          ha |= (sa <= 0 ? 1u : 0u) << c;
-          hb |= (sb <= 0 ? 1u : 0u) << c;
-        });
-        fa     = ha ^ crc_ha;
-        fb     = hb ^ crc_hb;
-        crc_ha = ha;
-        crc_hb = hb;
-        inc_ia = ia;
-        inc_zz = ZZ;
-        inc_hh = HH;
-#else
         static_for<KC>([&](auto Ci) {
           constexpr int  c  = decltype(Ci)::value;
           const uint32_t ib = ia + HH;
@@ -993,39 +820,7 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
             __builtin_amdgcn_sched_barrier(0);
           }
         });
-#endif
       }
-#ifdef LDPC_PK_INC_CRC
-      // Columns with a flipped decision somewhere in the wave (wave-uniform), four per round: eight table loads in
-      // flight, then the lanes XOR the entries of their flipped positions into their running remainder.
-      uint32_t cols = wave_or(fa | fb);
-      if (active) {
-        while (cols != 0) {
-          uint32_t cc[4];
-          uint32_t ok = 0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            cc[k] = cols != 0 ? static_cast<uint32_t>(__builtin_ctz(cols)) : cc[0];
-            ok |= (cols != 0 ? 1u : 0u) << k;
-            cols &= cols - 1;
-          }
-          uint32_t ta[4], tb[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t a = inc_ia + cc[k] * inc_zz;
-            ta[k]            = crc_table[a];
-            tb[k]            = crc_table[a + inc_hh];
-          }
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const bool v = ((ok >> k) & 1u) != 0;
-            crc_lane ^= (v && ((fa >> cc[k]) & 1u) != 0) ? ta[k] : 0u;
-            crc_lane ^= (v && ((fb >> cc[k]) & 1u) != 0) ? tb[k] : 0u;
-          }
-        }
-        acc = crc_lane;
-      }
-#endif
       acc      = wave_xor(acc);
       zero     = (__ballot(zero != 0) != 0) ? 1u : 0u;
       int* red = scratch + 8 + 16 * (it & 1);
@@ -1064,25 +859,24 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
 }
 
 // ---------------------------------------------------------------------------------------------------------------------
-// Multi-codeblock workgroups (PK4). The plain kernel gives a codeblock 64 * ceil(Z / 128) lanes: a Z = 288 codeblock
-// runs three waves of which the third has 16 active lanes, and every wave issues the full instruction stream (the
-// decoder is bound by wave-instruction issue: at a fixed per-lane load, Z = 256 on two waves decodes 1.6x the
-// codeblocks per second of Z = 288 on three, profiles/r3_decoder_z_sweep.log). Here up to PK4 codeblocks of one lifting
-// size share a workgroup: codeblock slot i owns lanes [i H, (i + 1) H), so the lanes are packed without gaps (four
-// Z = 288 codeblocks on nine full waves) and a wave whose codeblocks have all stopped skips the layer bodies.
+// Two-codeblock workgroups (SRSGPU_OPTION_DECODER_PAIRS). The plain kernel gives a codeblock 64 * ceil(Z / 128) lanes:
+// a Z = 144..192 codeblock runs two waves of which the second is partly idle, and every wave issues the full instruction
+// stream. Here two codeblocks of one lifting size share a workgroup: codeblock slot i owns lanes [i H, (i + 1) H), so
+// two Z = 192 codeblocks fill three waves, and a wave whose codeblocks have both stopped skips the layer bodies.
 //
 // The soft-bit images of the slots are interleaved pair by pair: position p of column c of slot i is at byte
-// c * PK4_CS + 2 * PK4 * (p mod H) + 2 i + [p >= H]. With the lane constant u = 2 PK4 z + 2 i and the per-(Z, edge)
-// constants A = 2 PK4 s' + hi, B = 2 PK4 (s' - H) + 1 - hi (s' = shift mod H, hi = [shift >= H]; ctx d_pair_ab4) the
+// c * CS + 2 * PKN * (p mod H) + 2 i + [p >= H]. With the lane constant u = 2 PKN z + 2 i and the per-(Z, edge)
+// constants A = 2 PKN s' + hi, B = 2 PKN (s' - H) + 1 - hi (s' = shift mod H, hi = [shift >= H]; ctx d_pair_ab2) the
 // packed kernel's address arithmetic (min(u + A, u + B) in 16-bit halves, partner byte a ^ 1) and its column
-// immediates are unchanged: row_update_pk runs as is, with column stride PK4_CS.
+// immediates are unchanged: row_update_pk runs as is, with column stride CS.
 //
 // Per codeblock as in the plain kernel: HARQ skip, LLR load, layer count, CRC early stop, hard decisions and results.
 // The slots of a workgroup share the iteration loop (a stopped codeblock's lanes idle through the layers and barriers
-// until the last one stops). The host puts codeblocks with the same Z, scaling, iteration limit and CRC mode in a
-// workgroup (descs[PK4 * w + i], empty slots have nof_llr = 0).
+// until the other one stops). The host pairs codeblocks with the same Z, scaling, iteration limit and CRC mode
+// (descs[2 w + i], an empty slot has nof_llr = 0). Measured (profiles/r5_decoder_pk2_scaling.txt): 2-7 % faster at six
+// iterations, equal or slower under early stop - opt-in.
 // ---------------------------------------------------------------------------------------------------------------------
-/// Geometry of a PKN-codeblock workgroup (PKN = LDPC_PK4 or 2: two codeblocks of Z <= 192 fill three waves).
+/// Geometry of a PKN-codeblock workgroup (PKN = 2: two codeblocks of Z <= 192 fill three waves).
 template <int PKN>
 struct pk_geom {
   static constexpr int CS           = PKN * SOFT_COL_STRIDE;   ///< column stride of the interleaved image
@@ -1093,7 +887,7 @@ struct pk_geom {
 
 /// Byte offset of position l (0 <= l < Z) of slot i within a column of the interleaved image.
 template <int PKN>
-__device__ __forceinline__ uint32_t pair_pos4(uint32_t l, uint32_t H, uint32_t i)
+__device__ __forceinline__ uint32_t pair_pos_pkn(uint32_t l, uint32_t H, uint32_t i)
 {
   return ((l < H) ? 2u * PKN * l : 2u * PKN * (l - H) + 1u) + 2u * i;
 }
@@ -1102,7 +896,7 @@ __device__ __forceinline__ uint32_t pair_pos4(uint32_t l, uint32_t H, uint32_t i
 /// the slot's addresses), the punctured columns and every position beyond the input zeroed. Returns this thread's
 /// index of the last non-zero LLR it saw (ldpc_decoder_impl.cpp:94), -1 if none.
 template <int NCOL, int PKN>
-__device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const int8_t* __restrict__ llr,
+__device__ __forceinline__ int load_llrs_pkn(int8_t* __restrict__ soft, const int8_t* __restrict__ llr,
                                              const dec_desc& d, uint32_t slot)
 {
   const int      Z     = d.Z;
@@ -1137,7 +931,7 @@ __device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const in
                               (l0 + 16u <= static_cast<uint32_t>(Z));
       if (short_path) {
         // Consecutive positions are 2 PKN bytes apart; a byte past the half boundary moves by 1 - 2 PKN H.
-        int8_t*        dst   = soft + (c0 + 2) * pk_geom<PKN>::CS + pair_pos4<PKN>(l0, H, slot);
+        int8_t*        dst   = soft + (c0 + 2) * pk_geom<PKN>::CS + pair_pos_pkn<PKN>(l0, H, slot);
         const uint32_t cross = (l0 < H && l0 + 16u > H) ? (0xffffu << (H - l0)) : 0u;
         const int      adj   = 1 - 2 * PKN * static_cast<int>(H);
 #pragma unroll
@@ -1166,7 +960,7 @@ __device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const in
               last  = (v != 0) ? static_cast<int>(i) : last;
               v     = (i < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
               const uint32_t cq = __umulhi(i, d.div_magic);
-              soft[(cq + 2) * pk_geom<PKN>::CS + pair_pos4<PKN>(i - cq * static_cast<uint32_t>(Z), H, slot)] = static_cast<int8_t>(v);
+              soft[(cq + 2) * pk_geom<PKN>::CS + pair_pos_pkn<PKN>(i - cq * static_cast<uint32_t>(Z), H, slot)] = static_cast<int8_t>(v);
             }
           }
         }
@@ -1210,7 +1004,7 @@ __device__ __forceinline__ int load_llrs_pk4(int8_t* __restrict__ soft, const in
 
 /// Hard decisions of one slot's K*Z systematic bits, written by the slot's H lanes (lane z: bytes z, z + H, ...).
 template <int PKN>
-__device__ __forceinline__ void write_hard_bits_pk4(const int8_t* __restrict__ soft, uint8_t* __restrict__ out,
+__device__ __forceinline__ void write_hard_bits_pkn(const int8_t* __restrict__ soft, uint8_t* __restrict__ out,
                                                     int nbits, int Z, uint32_t magic, uint32_t slot, uint32_t z)
 {
   const uint32_t H      = static_cast<uint32_t>(Z) / 2u;
@@ -1223,7 +1017,7 @@ __device__ __forceinline__ void write_hard_bits_pk4(const int8_t* __restrict__ s
       if (i < nbits) {
         const uint32_t col = __umulhi(static_cast<uint32_t>(i), magic);
         const uint32_t l   = static_cast<uint32_t>(i) - col * static_cast<uint32_t>(Z);
-        byte |= static_cast<uint32_t>(soft[col * pk_geom<PKN>::CS + pair_pos4<PKN>(l, H, slot)] <= 0) << (7 - k);
+        byte |= static_cast<uint32_t>(soft[col * pk_geom<PKN>::CS + pair_pos_pkn<PKN>(l, H, slot)] <= 0) << (7 - k);
       }
     }
     out[b] = static_cast<uint8_t>(byte);
@@ -1234,7 +1028,7 @@ __device__ __forceinline__ void write_hard_bits_pk4(const int8_t* __restrict__ s
 /// LLRs (llrs + dms[PKN w + i].llr_offset) into its slot of the image and into its HARQ soft buffer (harq +
 /// harq_offset, or llr_cbs[cb]); the image is zeroed first. Returns this thread's last non-zero input position.
 template <int NCOL, int PKN>
-__device__ __forceinline__ int load_fused_pk4(int8_t* __restrict__ soft, const int8_t* __restrict__ llrs,
+__device__ __forceinline__ int load_fused_pkn(int8_t* __restrict__ soft, const int8_t* __restrict__ llrs,
                                               const dec_desc& d, const dm_desc& dm, int8_t* __restrict__ hb,
                                               uint32_t slot)
 {
@@ -1253,7 +1047,7 @@ __device__ __forceinline__ int load_fused_pk4(int8_t* __restrict__ soft, const i
       last              = (v != 0 && k > last) ? k : last;
       const uint32_t cq = __umulhi(static_cast<uint32_t>(k), d.div_magic);
       const int      cv = (static_cast<uint32_t>(k) < full) ? clamp_i(v, -64, 64) : clamp_i(v, -SOFT_INF, SOFT_INF);
-      soft[(cq + 2) * pk_geom<PKN>::CS + pair_pos4<PKN>(static_cast<uint32_t>(k) - cq * static_cast<uint32_t>(Z), H,
+      soft[(cq + 2) * pk_geom<PKN>::CS + pair_pos_pkn<PKN>(static_cast<uint32_t>(k) - cq * static_cast<uint32_t>(Z), H,
                                                         slot)] = static_cast<int8_t>(cv);
     }
   };
@@ -1262,7 +1056,7 @@ __device__ __forceinline__ int load_fused_pk4(int8_t* __restrict__ soft, const i
     soft_put(k, v);
   };
   const bool q8   = Qm == 8 && ((dm.llr_offset & 7u) == 0u);
-  const bool q8x4 = LDPC_PK_HARQ_X4 && q8 &&
+  const bool q8x4 = q8 &&
                     ((R | ninfo | Fl | static_cast<int>(reinterpret_cast<uintptr_t>(hb))) & 3) == 0;
   if (q8x4) {
     for (int r0 = 4 * static_cast<int>(threadIdx.x); r0 < R; r0 += 4 * static_cast<int>(blockDim.x)) {
@@ -1327,7 +1121,7 @@ __device__ __forceinline__ int load_fused_pk4(int8_t* __restrict__ soft, const i
 }
 
 template <int BG, int MODE, int MAXL, int PKN, bool FUSE>
-__global__ __launch_bounds__(64 * pk_geom<PKN>::WAVES, (MAXL > 8 ? 4 : LDPC_PK_MIN_BLOCKS_8)) void ldpc_decode_pk4_kernel(
+__global__ __launch_bounds__(64 * pk_geom<PKN>::WAVES, (MAXL > 8 ? 4 : PK_MIN_BLOCKS_8)) void ldpc_decode_pairs_kernel(
     const dec_desc* __restrict__ descs,
     const int8_t* __restrict__ llrs,
     uint8_t* __restrict__ out,
@@ -1403,9 +1197,9 @@ __global__ __launch_bounds__(64 * pk_geom<PKN>::WAVES, (MAXL > 8 ? 4 : LDPC_PK_M
         }
         const dm_desc dm = dms[static_cast<size_t>(blockIdx.x) * PKN + i];
         int8_t*       hb = (llr_cbs != nullptr) ? llr_cbs[d.cb_index] : harq + dm.harq_offset;
-        last = load_fused_pk4<NCOL, PKN>(soft, llrs, d, dm, hb, static_cast<uint32_t>(i));
+        last = load_fused_pkn<NCOL, PKN>(soft, llrs, d, dm, hb, static_cast<uint32_t>(i));
       } else {
-        last = load_llrs_pk4<NCOL, PKN>(soft, (llr_cbs != nullptr) ? llr_cbs[d.cb_index] : llrs + d.llr_offset, d,
+        last = load_llrs_pkn<NCOL, PKN>(soft, (llr_cbs != nullptr) ? llr_cbs[d.cb_index] : llrs + d.llr_offset, d,
                                         static_cast<uint32_t>(i));
       }
       last     = wave_max(last);
@@ -1490,7 +1284,7 @@ __global__ __launch_bounds__(64 * pk_geom<PKN>::WAVES, (MAXL > 8 ? 4 : LDPC_PK_M
       if (m < nl) {
         if (lane_st >= static_cast<uint32_t>(m + 1) << 16) {
           __builtin_amdgcn_sched_barrier(0);
-          row_update_pk<BG, MODE, m, (MAXL <= LDPC_PK_KEEP_ADDR_MAXL), pk_geom<PKN>::CS>(soft, abi, z2x2, sc, magw[m], sgw[m],
+          row_update_pk<BG, MODE, m, (MAXL <= PK_KEEP_ADDR_MAXL), pk_geom<PKN>::CS>(soft, abi, z2x2, sc, magw[m], sgw[m],
                                                                               hiw[m & 3]);
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -1548,7 +1342,7 @@ __global__ __launch_bounds__(64 * pk_geom<PKN>::WAVES, (MAXL > 8 ? 4 : LDPC_PK_M
         }
         if ((tzero == 0 || !early) && tacc == 0) {
           const dec_desc* md = wd + ls;
-          write_hard_bits_pk4<PKN>(soft, out + md->out_offset, msg_len, Z, d0.div_magic, ls, lz);
+          write_hard_bits_pkn<PKN>(soft, out + md->out_offset, msg_len, Z, d0.div_magic, ls, lz);
           if (lz == 0) {
             results[md->cb_index] = it + 1;
             if (cb_crc_ok != nullptr) {
@@ -1565,7 +1359,7 @@ __global__ __launch_bounds__(64 * pk_geom<PKN>::WAVES, (MAXL > 8 ? 4 : LDPC_PK_M
     const uint32_t  ub = lane_st & 0xffffu;
     const uint32_t  lz = ub / (2u * PKN), ls = (ub / 2u) % PKN;
     const dec_desc* md = wd + ls;
-    write_hard_bits_pk4<PKN>(soft, out + md->out_offset, msg_len, Z, d0.div_magic, ls, lz);
+    write_hard_bits_pkn<PKN>(soft, out + md->out_offset, msg_len, Z, d0.div_magic, ls, lz);
     if (lz == 0) {
       results[md->cb_index] = -1;
     }
@@ -1635,51 +1429,47 @@ void launch_ldpc_decode_pk(int             bg,
 #undef SRSGPU_PK_LAUNCH1
 }
 
-void launch_ldpc_decode_pk4(int             bg,
-                            int             mode,
-                            int             max_layers,
-                            const dec_desc* d_desc,
-                            int             nof_groups,
-                            int             block_threads,
-                            const int8_t*   d_llrs,
-                            uint8_t*        d_out,
-                            int32_t*        d_results,
-                            const uint32_t* d_ab4,
-                            const uint32_t* d_crc_tables,
-                            uint8_t*        d_cb_crc_ok,
-                            hipStream_t     stream,
-                            int8_t* const*  d_llr_cbs,
-                            int             pkn,
-                            const dm_desc*  d_dm,
-                            int8_t*         d_harq)
+void launch_ldpc_decode_pairs(int             bg,
+                              int             mode,
+                              int             max_layers,
+                              const dec_desc* d_desc,
+                              int             nof_groups,
+                              int             block_threads,
+                              const int8_t*   d_llrs,
+                              uint8_t*        d_out,
+                              int32_t*        d_results,
+                              const uint32_t* d_ab2,
+                              const uint32_t* d_crc_tables,
+                              uint8_t*        d_cb_crc_ok,
+                              hipStream_t     stream,
+                              int8_t* const*  d_llr_cbs,
+                              const dm_desc*  d_dm,
+                              int8_t*         d_harq)
 {
   if (nof_groups <= 0) {
     return;
   }
   dim3 grid(nof_groups), block(block_threads);
-  // (codeblocks per workgroup, fused dematching): (LDPC_PK4, no), (2, no), (2, yes).
-#define SRSGPU_PK4_LAUNCH1(BG_, MODE_, MAXL_, PKN_, FUSE_)                                                              \
-  ldpc_decode_pk4_kernel<BG_, MODE_, MAXL_, PKN_, FUSE_><<<grid, block, 0, stream>>>(                                   \
-      d_desc, d_llrs, d_out, d_results, d_ab4, d_crc_tables, d_cb_crc_ok, d_llr_cbs, d_dm, d_harq)
-#define SRSGPU_PK4_LAUNCH(BG_, MODE_, MAXL_)                                                                           \
-  (pkn != 2 ? SRSGPU_PK4_LAUNCH1(BG_, MODE_, MAXL_, LDPC_PK4, false)                                                   \
-            : (d_dm != nullptr ? SRSGPU_PK4_LAUNCH1(BG_, MODE_, MAXL_, 2, true)                                        \
-                               : SRSGPU_PK4_LAUNCH1(BG_, MODE_, MAXL_, 2, false)))
+#define SRSGPU_PAIRS_LAUNCH1(BG_, MODE_, MAXL_, FUSE_)                                                                  \
+  ldpc_decode_pairs_kernel<BG_, MODE_, MAXL_, 2, FUSE_><<<grid, block, 0, stream>>>(                                   \
+      d_desc, d_llrs, d_out, d_results, d_ab2, d_crc_tables, d_cb_crc_ok, d_llr_cbs, d_dm, d_harq)
+#define SRSGPU_PAIRS_LAUNCH(BG_, MODE_, MAXL_)                                                                         \
+  (d_dm != nullptr ? SRSGPU_PAIRS_LAUNCH1(BG_, MODE_, MAXL_, true) : SRSGPU_PAIRS_LAUNCH1(BG_, MODE_, MAXL_, false))
   if (bg == 1) {
     if (max_layers <= 8) {
-      mode == 1 ? SRSGPU_PK4_LAUNCH(1, 1, 8) : SRSGPU_PK4_LAUNCH(1, 0, 8);
+      mode == 1 ? SRSGPU_PAIRS_LAUNCH(1, 1, 8) : SRSGPU_PAIRS_LAUNCH(1, 0, 8);
     } else {
-      mode == 1 ? SRSGPU_PK4_LAUNCH(1, 1, 16) : SRSGPU_PK4_LAUNCH(1, 0, 16);
+      mode == 1 ? SRSGPU_PAIRS_LAUNCH(1, 1, 16) : SRSGPU_PAIRS_LAUNCH(1, 0, 16);
     }
   } else {
     if (max_layers <= 8) {
-      mode == 1 ? SRSGPU_PK4_LAUNCH(2, 1, 8) : SRSGPU_PK4_LAUNCH(2, 0, 8);
+      mode == 1 ? SRSGPU_PAIRS_LAUNCH(2, 1, 8) : SRSGPU_PAIRS_LAUNCH(2, 0, 8);
     } else {
-      mode == 1 ? SRSGPU_PK4_LAUNCH(2, 1, 16) : SRSGPU_PK4_LAUNCH(2, 0, 16);
+      mode == 1 ? SRSGPU_PAIRS_LAUNCH(2, 1, 16) : SRSGPU_PAIRS_LAUNCH(2, 0, 16);
     }
   }
-#undef SRSGPU_PK4_LAUNCH
-#undef SRSGPU_PK4_LAUNCH1
+#undef SRSGPU_PAIRS_LAUNCH
+#undef SRSGPU_PAIRS_LAUNCH1
 }
 
 } // namespace srsgpu

@@ -26,11 +26,7 @@
 namespace srsgpu {
 namespace {
 
-#ifdef SRSGPU_OFDM_WAVES  // occupancy experiments: waves per SIMD forced by the register allocator
-#define OFDM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(SRSGPU_OFDM_WAVES, 8)))
-#else
 #define OFDM_OCCUPANCY
-#endif
 
 // cos / sin (2 pi k / 16).
 __device__ constexpr float kCos16[16] = {1.0f,          0.92387953251f,  0.70710678118f,  0.38268343236f,
@@ -298,10 +294,6 @@ __device__ __forceinline__ void dft_lds3(float2* lds, const float2* __restrict__
   }
 }
 
-#ifndef OFDM_LDS_SWIZZLE
-#define OFDM_LDS_SWIZZLE 0
-#endif
-
 template <int LOG2N, int S, typename Src, typename Dst>
 __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
 {
@@ -311,22 +303,13 @@ __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ 
   constexpr int NP   = LOG2N / 4 + (REM ? 1 : 0);
   // The first pass's stores go to j R0 + r: 16 consecutive lanes 16 float2 apart on one bank pair, and 64 % of the
   // 4096-point kernels' LDS cycles are bank-conflict cycles (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE,
-  // profiles/r5_lds_counters.txt). OFDM_LDS_SWIZZLE=1 (i ^ ((i >> 4) & 15)) or 2 (XOR of bits 1-3 only, pairs kept)
-  // remove every conflict (LDS-array cycles 5.0M -> 1.4M, LDS issue stalls 5.7M -> 0.4M per modulator launch), but the
+  // profiles/r5_lds_counters.txt). An XOR swizzle (i ^ ((i >> 4) & 15), or of bits 1-3 only, pairs kept) removed every
+  // conflict (LDS-array cycles 5.0M -> 1.4M, LDS issue stalls 5.7M -> 0.4M per modulator launch), but the
   // runtime XOR splits the merged ds_write_b128 / ds_read2st64_b64 into single b64 accesses (2x the LDS instructions,
   // +9 % VALU) and the bench gets slower: modulator stage 45.6 -> 68-73 us per step, demodulator unchanged, headline
   // 144.2k -> 142.6k (profiles/r5_ofdm_swizzle_ab.txt). The LDS conflicts do not bound these kernels: plain layout.
-#if OFDM_LDS_SWIZZLE == 2
-  // Pair-preserving: XOR bits 1-3 with bits 4-6, so a thread's consecutive pairs stay 16-byte units (ds_*_b128).
-  auto ld = [lds](int i) { return lds[i ^ (((i >> 4) & 7) << 1)]; };
-  auto st = [lds](int i, float2 v) { lds[i ^ (((i >> 4) & 7) << 1)] = v; };
-#elif OFDM_LDS_SWIZZLE
-  auto ld = [lds](int i) { return lds[i ^ ((i >> 4) & 15)]; };
-  auto st = [lds](int i, float2 v) { lds[i ^ ((i >> 4) & 15)] = v; };
-#else
   auto ld = [lds](int i) { return lds[i]; };
   auto st = [lds](int i, float2 v) { lds[i] = v; };
-#endif
   static_assert(NP >= 2 && NP <= 4, "supported DFT sizes: 128..8192");
   float2 w0[16 / R0][R0], w1[1][16], w2[1][16], w3[1][16];
   load_twiddles<N, 16, R0, S>(tw, w1);

@@ -24,10 +24,7 @@
 namespace srsgpu {
 namespace {
 
-#ifndef SRSGPU_MOD_THREADS
-#define SRSGPU_MOD_THREADS 256
-#endif
-constexpr int MOD_THREADS = SRSGPU_MOD_THREADS;
+constexpr int MOD_THREADS = 256;
 
 /// Scrambled codeword word w (bits 32w..32w+31, MSB first) of a transmission: the plan's precomputed sequence word.
 __device__ __forceinline__ uint32_t scrambled_word(const mod_desc& d,

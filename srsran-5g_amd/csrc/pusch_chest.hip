@@ -51,9 +51,7 @@ __device__ uint64_t g_chest_prof[CHEST_PROF_JOBS * CHEST_PROF_SLOTS];
 /// few-RB instantiations settle at 72-78 VGPRs (6-7 waves per SIMD) with no spill, and the headline bench gains
 /// 1.4 % (137.8k -> 139.8k slots/s, estimator stage 37.4 -> 33.5 us per step; profiles/r4_chest_waves_ab.txt); 4 also
 /// keeps the 1024-lane wideband instantiation (100 VGPRs) from spilling.
-#ifndef CHEST_WAVES_PER_EU
 #define CHEST_WAVES_PER_EU 4
-#endif
 
 constexpr int CHEST_THREADS = 64;  // one wavefront per job (multi-wave workgroups for large allocations: T)
 constexpr int CHEST_VP      = 12;  // MAX_V_PILOTS
@@ -200,14 +198,6 @@ __device__ __forceinline__ void job_sum_n(float (&v)[K], float* red)
   }
 }
 
-/// Early first-pilot loads (round 5, verdict item 2): 1 issues each lane's first pilot grid loads before the sequence
-/// staging. With the lane guard it passes the estimator tests (round 4's unguarded version faulted), but it does not
-/// pay: estimator stage 36.6-37.1 vs 36.3-36.6 us per step, headline 143.8k vs 143.9k slots/s, two alternating runs
-/// each (profiles/r5_chest_early_pilots_ab.txt). Off by default.
-#ifndef CHEST_EARLY_PILOTS
-#define CHEST_EARLY_PILOTS 0
-#endif
-constexpr int CHEST_EARLY = 4;  ///< DM-RS symbols whose first pilot is loaded early
 
 /// Ordering of a job's LDS stages: a workgroup barrier; in a one-wave workgroup (T = 64, where the 32-lane halves may
 /// run jobs with different stage sequences) a wave-level fence: a wave's LDS accesses complete in program order.
@@ -540,9 +530,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(CHEST_WAVES_P
   L.seq  = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(L.Y) + chest_region_bytes(geom));
   L.taps = reinterpret_cast<float*>(L.seq + geom.max_dmrs * geom.max_words);
 
-#ifndef SRSGPU_CHEST_JOB_SCALAR
   // The job descriptor staged in LDS once (one coalesced read) instead of dependent scalar loads of its fields
-  // (A/B on MI355X: chest stage 32.6 -> 28.9 us per 16-slot step; SRSGPU_CHEST_JOB_SCALAR restores the direct reads).
+  // (A/B on MI355X: chest stage 32.6 -> 28.9 us per 16-slot step).
   __shared__ chest_job sjob[JPW];
   {
     static_assert(sizeof(chest_job) % 4 == 0, "word copy");
@@ -554,9 +543,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(CHEST_WAVES_P
     job_sync<T>();
   }
   const chest_job& jb = sjob[slot];
-#else
-  const chest_job& jb    = jobs[job];
-#endif
   const int        lane  = static_cast<int>(threadIdx.x) % TS;  // lane within the job
   CHEST_STAMP(0);
   CHEST_PROF(10, __builtin_amdgcn_s_memrealtime());
@@ -570,28 +556,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(CHEST_WAVES_P
   const int        NP    = geom.max_pilots;
   cpx* const       Fbase = L.F;
 
-#if CHEST_EARLY_PILOTS
-  // The grid values of each lane's first pilot on the first CHEST_EARLY DM-RS symbols, issued before the sequence
-  // staging so the two memory round trips overlap (the staging barrier waits for both). Only lanes that hold a pilot
-  // (lane < N) compute a subcarrier: pilot_subcarrier reads the job's CRB list at rb = lane / pilots per RB, which lies
-  // beyond the list (and, for the plan's last job, beyond the buffer) for the lanes past the last pilot. Round 4's
-  // unguarded version faulted exactly there (an illegal address in the CFO / TA golden test).
-  cpx e0{}, e1{}, e2{}, e3{};  // named registers (an array here lands in scratch)
-  if (lane < N) {
-    const uint32_t  k   = pilot_subcarrier(jb, crbs, lane);
-    const uint32_t* row = grids + jb.grid_base + k;
-    e0                  = bf16c(row[jb.dmrs_symbols[0] * jb.nsc]);
-    if (D > 1) {
-      e1 = bf16c(row[jb.dmrs_symbols[1] * jb.nsc]);
-    }
-    if (D > 2) {
-      e2 = bf16c(row[jb.dmrs_symbols[2] * jb.nsc]);
-    }
-    if (D > 3) {
-      e3 = bf16c(row[jb.dmrs_symbols[3] * jb.nsc]);
-    }
-  }
-#endif
   // Stage: taps and the sequence words of every DM-RS symbol (the plan's resident words, gold_fill_kernel).
   if (lane < 32) {
     L.taps[lane] = jb.taps[lane];
@@ -611,16 +575,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(CHEST_WAVES_P
     const uint32_t k = pilot_subcarrier(jb, crbs, i);
     const int      m = pilot_seq_index(jb, crbs, i);
     for (int s = 0; s < D; ++s) {
-#if CHEST_EARLY_PILOTS
-      cpx y;
-      if (i == lane && s < CHEST_EARLY) {
-        y = s == 0 ? e0 : s == 1 ? e1 : s == 2 ? e2 : e3;
-      } else {
-        y = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
-      }
-#else
       const cpx y = bf16c(grids[jb.grid_base + jb.dmrs_symbols[s] * jb.nsc + k]);
-#endif
       const cpx p = dmrs_value(jb, lp, L.seq, W, s, n0, m, i);
       L.Y[s * NP + i] = {y.x * p.x + y.y * p.y, y.y * p.x - y.x * p.y};
       epre_acc += y.x * y.x + y.y * y.y;
@@ -1017,21 +972,17 @@ void launch_pusch_chest(const float2*   d_lp,
   };
   // Two jobs per wave (32 lanes each) for the usual few-RB allocations (many jobs resident together); a job with
   // hundreds of pilots (a wideband allocation: few jobs, each a long serial chain on one wave) spreads over 4 or 16
-  // waves. SRSGPU_CHEST_ONE_JOB_PER_WAVE=1: one 64-lane job per wave (A/B).
+  // waves (two jobs per wave against one: chest stage 51 -> 42 us per step, profiles/r3_chest_two_jobs_per_wave_ab.json).
   const auto launch = [&](auto kernel, int threads, int jpw) {
     hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>((nof_jobs + jpw - 1) / jpw + copy_blocks(threads))),
                        dim3(static_cast<unsigned>(threads)), static_cast<unsigned>(jpw * lds), stream, d_jobs, nof_jobs,
                        geom, d_grids, d_ce, d_noise_var, d_metrics, d_seq, d_crbs, d_lp, d_spans, nof_spans);
   };
-  static const bool one_job = [] {
-    const char* e = std::getenv("SRSGPU_CHEST_ONE_JOB_PER_WAVE");
-    return e != nullptr && e[0] == '1';
-  }();
   if (geom.max_pilots > 512) {
     launch(pusch_chest_kernel<1024, 1024>, 1024, 1);
   } else if (geom.max_pilots > 128) {
     launch(pusch_chest_kernel<256, 256>, 256, 1);
-  } else if (!one_job && geom.max_pilots <= 64 && 2 * lds <= 64 * 1024) {
+  } else if (geom.max_pilots <= 64 && 2 * lds <= 64 * 1024) {
     launch(pusch_chest_kernel<CHEST_THREADS, CHEST_THREADS / 2>, CHEST_THREADS, 2);
   } else {
     launch(pusch_chest_kernel<CHEST_THREADS, CHEST_THREADS>, CHEST_THREADS, 1);

@@ -467,19 +467,9 @@ __device__ __forceinline__ void demod_res(demod_uniform        u,
   __syncthreads();
   lane_stats st;
   for (bool first = true; r < u.re_end; r += T, first = false) {
-#if SRSGPU_DEMOD_PREFETCH
-    // The next RE's loads fly while this one is equalised and demapped.
-    (void)first;
-    uint32_t       nyw[4] = {}, nhw[L][4] = {}, nsym = 0;
-    const uint32_t rn     = r + T;
-    if (rn < u.re_end) {
-      load_re<L>(d, rn, grids, ce, u.crbs, nyw, nhw, nsym);
-    }
-#else
     if (!first) {
       load_re<L>(d, r, grids, ce, u.crbs, yw, hw, sym);
     }
-#endif
     cpx y[4], h[L][4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -581,17 +571,6 @@ __device__ __forceinline__ void demod_res(demod_uniform        u,
         out8[ob + b] = static_cast<uint8_t>(pk[b / 4] >> (8 * (b % 4)));
       }
     }
-#if SRSGPU_DEMOD_PREFETCH
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      yw[p] = nyw[p];
-#pragma unroll
-      for (int ly = 0; ly < L; ++ly) {
-        hw[ly][p] = nhw[ly][p];
-      }
-    }
-    sym = nsym;
-#endif
   }
   if constexpr (STATS) {
     st.flush(u.lacc);
@@ -643,52 +622,10 @@ __device__ __forceinline__ void total_stats(const float* v, float* __restrict__ 
   o[29] = tot_n == 0.f ? nan : tot_evm / tot_n;
 }
 
-/// Fused statistics (stats != nullptr): after its accumulator adds, the workgroup counts itself in cnt[2 tx + 1]; the
-/// last of the transmission's cnt[2 tx] workgroups (chunks and transform-precoding jobs) reads the accumulators back
-/// (device-scope atomics: the other workgroups' adds), resets them and the count, and writes the statistics - no
-/// separate statistics launch. Called by every thread of the workgroup (at least 64); sh: DEMOD_ACC_PER_TX + 1 free
-/// LDS words.
-__device__ __forceinline__ void finish_if_last(uint32_t tx, float* __restrict__ acc, float* __restrict__ stats,
-                                               uint32_t* __restrict__ cnt, float* sh)
-{
-  __threadfence();  // this thread's accumulator adds are done before the count below
-  __syncthreads();
-  uint32_t* flag = reinterpret_cast<uint32_t*>(sh + DEMOD_ACC_PER_TX);
-  if (threadIdx.x == 0) {
-    const uint32_t done = atomicAdd(&cnt[2 * tx + 1], 1u) + 1u;
-    *flag               = done == cnt[2 * tx] ? 1u : 0u;
-  }
-  __syncthreads();
-  if (*flag == 0u) {
-    return;
-  }
-  __threadfence();
-  float* a = acc + DEMOD_ACC_PER_TX * tx;
-  if (threadIdx.x < static_cast<unsigned>(DEMOD_ACC_PER_TX)) {
-    sh[threadIdx.x] = __hip_atomic_load(&a[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a[threadIdx.x], 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(&cnt[2 * tx + 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  float* o = stats + DEMOD_STATS_PER_TX * tx;
-  if (threadIdx.x < 14) {
-    symbol_stats(sh, static_cast<int>(threadIdx.x), o);
-  } else if (threadIdx.x == 32) {
-    total_stats(sh, o);
-  }
-}
-
-#ifdef SRSGPU_DEMOD_WAVES  // occupancy experiments: waves per SIMD forced by the register allocator
-#define DEMOD_OCCUPANCY __attribute__((amdgpu_waves_per_eu(SRSGPU_DEMOD_WAVES, SRSGPU_DEMOD_WAVES)))
-#else
-#define DEMOD_OCCUPANCY
-#endif
 /// STATS: also accumulate the post-equalization statistics (a separate instantiation, so that the plain kernel keeps
 /// its register budget).
 template <bool STATS, int T>
-__global__ __launch_bounds__(T) DEMOD_OCCUPANCY void pusch_demodulate_kernel(const demod_desc* __restrict__ descs,
+__global__ __launch_bounds__(T) void pusch_demodulate_kernel(const demod_desc* __restrict__ descs,
                                                                          const mod_chunk* __restrict__ chunks,
                                                                          const demap_pair_table* __restrict__ tables,
                                                                          const uint32_t* __restrict__ grids,
@@ -697,9 +634,7 @@ __global__ __launch_bounds__(T) DEMOD_OCCUPANCY void pusch_demodulate_kernel(con
                                                                          int8_t* __restrict__ llrs,
                                                                          const uint32_t* __restrict__ gseq,
                                                                          const uint16_t* __restrict__ crbs,
-                                                                         float* __restrict__ acc,
-                                                                         float* __restrict__ stats,
-                                                                         uint32_t* __restrict__ cnt)
+                                                                         float* __restrict__ acc)
 {
   __shared__ uint32_t         seq[DEMOD_CHUNK_WORDS + 1];
   __shared__ demap_pair_table tab[DEMAP_TABLES];
@@ -735,9 +670,6 @@ __global__ __launch_bounds__(T) DEMOD_OCCUPANCY void pusch_demodulate_kernel(con
   __syncthreads();
   if (STATS && tid < static_cast<uint32_t>(DEMOD_ACC_PER_TX) && lacc[tid] != 0.f) {
     atomicAdd(&acc[DEMOD_ACC_PER_TX * d.tx + tid], lacc[tid]);
-  }
-  if (STATS && stats != nullptr) {
-    finish_if_last(ch.tx, acc, stats, cnt, lacc);  // lacc (DEMOD_ACC_PER_TX + 1 words) is free again
   }
 
   // Contiguous LLR range [re_begin * Lq, re_end * Lq) of the codeword, staged from LDS byte 0. With s = dst & 3, the
@@ -914,9 +846,7 @@ __global__ __launch_bounds__(TP_THREADS) void pusch_demodulate_tp_kernel(const d
                                                                         int8_t* __restrict__ llrs,
                                                                         const uint32_t* __restrict__ gseq,
                                                                         const uint16_t* __restrict__ crbs,
-                                                                        float* __restrict__ acc,
-                                                                        float* __restrict__ stats,
-                                                                        uint32_t* __restrict__ cnt)
+                                                                        float* __restrict__ acc)
 {
   __shared__ cpx              xa[TP_MAX_M], xb[TP_MAX_M];
   __shared__ uint8_t          cls[TP_MAX_M];
@@ -1013,9 +943,6 @@ __global__ __launch_bounds__(TP_THREADS) void pusch_demodulate_tp_kernel(const d
     if (threadIdx.x < 4) {
       atomicAdd(&acc[DEMOD_ACC_PER_TX * d.tx + 4 * l + threadIdx.x], st[threadIdx.x]);
     }
-    if (stats != nullptr) {
-      finish_if_last(job.tx, acc, stats, cnt, reinterpret_cast<float*>(xb));  // the IDFT's buffers are free again
-    }
   }
 }
 
@@ -1053,22 +980,15 @@ void launch_pusch_demodulate(const demod_desc*       d_desc,
                              const uint32_t*         d_seq,
                              const uint16_t*         d_crbs,
                              float*                  d_acc,
-                             hipStream_t             stream,
-                             float*                  d_stats,
-                             uint32_t*               d_cnt)
+                             hipStream_t             stream)
 {
   if (nof_chunks <= 0) {
     return;
   }
-  static const int forced = [] {
-    const char* e = std::getenv("SRSGPU_DEMOD_THREADS");  // A/B: 64, 128 or 256 lanes per chunk for every plan
-    return e != nullptr ? std::atoi(e) : 0;
-  }();
-  const int threads = forced > 0 ? forced : plan_threads;
-  const auto launch = [&](auto kernel, int t) {
+  const int  threads = plan_threads;
+  const auto launch  = [&](auto kernel, int t) {
     hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nof_chunks)), dim3(static_cast<unsigned>(t)), 0, stream,
-                       d_desc, d_chunks, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq, d_crbs, d_acc,
-                       d_stats, d_cnt);
+                       d_desc, d_chunks, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq, d_crbs, d_acc);
   };
   if (d_acc != nullptr) {
     launch(pusch_demodulate_kernel<true, DEMOD_THREADS>, DEMOD_THREADS);
@@ -1093,16 +1013,13 @@ void launch_pusch_demodulate_tp(const demod_desc*       d_desc,
                                 const uint32_t*         d_seq,
                                 const uint16_t*         d_crbs,
                                 float*                  d_acc,
-                                hipStream_t             stream,
-                                float*                  d_stats,
-                                uint32_t*               d_cnt)
+                                hipStream_t             stream)
 {
   if (nof_jobs <= 0) {
     return;
   }
   hipLaunchKernelGGL(pusch_demodulate_tp_kernel, dim3(static_cast<unsigned>(nof_jobs)), dim3(TP_THREADS), 0, stream,
-                     d_desc, d_jobs, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq, d_crbs, d_acc, d_stats,
-                     d_cnt);
+                     d_desc, d_jobs, d_tables, d_grids, d_ch_est, d_noise_var, d_llrs, d_seq, d_crbs, d_acc);
 }
 
 void launch_pusch_demod_stats(float* d_acc, float* d_stats, int nof_tx, hipStream_t stream)

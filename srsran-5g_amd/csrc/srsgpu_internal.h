@@ -258,31 +258,27 @@ void launch_ldpc_decode_pk(int             bg,
                            hipStream_t     stream,
                            int8_t* const*  d_harq_cbs = nullptr);
 
-/// Codeblocks per workgroup of the multi-codeblock packed decoder (ldpc_decode_pk4_kernel).
-constexpr int LDPC_PK4 = 4;
-
-/// Launches the multi-codeblock packed decoder: workgroup w decodes d_desc[pkn * w + i] (pkn = LDPC_PK4 or 2; slots with
-/// nof_llr = 0 are empty; the slots of a workgroup share Z, scaling, iteration limit and CRC mode), codeblock slot i on
-/// lanes [i Z / 2, (i + 1) Z / 2), block_threads >= (used slots) x Z / 2. d_ab4: the pkn-interleaved image's pair
-/// constants. d_dm (pkn = 2): fused rate dematching of first transmissions (d_dm[pkn * w + i], d_llrs the codeword
-/// LLRs, soft buffers at d_harq + harq_offset or d_llr_cbs[cb]).
-void launch_ldpc_decode_pk4(int             bg,
-                            int             mode,
-                            int             max_layers,
-                            const dec_desc* d_desc,
-                            int             nof_groups,
-                            int             block_threads,
-                            const int8_t*   d_llrs,
-                            uint8_t*        d_out,
-                            int32_t*        d_results,
-                            const uint32_t* d_ab4,
-                            const uint32_t* d_crc_tables,
-                            uint8_t*        d_cb_crc_ok,
-                            hipStream_t     stream,
-                            int8_t* const*  d_llr_cbs = nullptr,
-                            int             pkn       = LDPC_PK4,
-                            const dm_desc*  d_dm      = nullptr,
-                            int8_t*         d_harq    = nullptr);
+/// Launches the two-codeblock packed decoder (ldpc_decode_pairs_kernel): workgroup w decodes d_desc[2 w + i] (slots
+/// with nof_llr = 0 are empty; the two slots share Z, scaling, iteration limit and CRC mode), codeblock slot i on lanes
+/// [i Z / 2, (i + 1) Z / 2), block_threads >= (used slots) x Z / 2. d_ab2: the interleaved image's pair constants. d_dm:
+/// fused rate dematching of first transmissions (d_dm[2 w + i], d_llrs the codeword LLRs, soft buffers at d_harq +
+/// harq_offset or d_llr_cbs[cb]).
+void launch_ldpc_decode_pairs(int             bg,
+                              int             mode,
+                              int             max_layers,
+                              const dec_desc* d_desc,
+                              int             nof_groups,
+                              int             block_threads,
+                              const int8_t*   d_llrs,
+                              uint8_t*        d_out,
+                              int32_t*        d_results,
+                              const uint32_t* d_ab2,
+                              const uint32_t* d_crc_tables,
+                              uint8_t*        d_cb_crc_ok,
+                              hipStream_t     stream,
+                              int8_t* const*  d_llr_cbs = nullptr,
+                              const dm_desc*  d_dm      = nullptr,
+                              int8_t*         d_harq    = nullptr);
 
 /// Launches the batched LDPC decoder (ldpc_decoder.hip). d_llr_cbs (optional): codeblock c's input is
 /// d_llr_cbs[dec_desc::cb_index] instead of d_llrs + llr_offset (the same for the packed launchers: per-codeblock HARQ
@@ -340,19 +336,10 @@ struct mod_chunk {
 /// Codeword words per modulator chunk (one workgroup): 1024 keeps a few-PRB 4-layer transmission (~23k bits) in one
 /// workgroup of ~3 REs per lane instead of three workgroups of one RE per lane (DM-RS + modulator stage 59.5 -> 52.6 us
 /// per step, headline +0.5 %; 512 splits such a transmission unevenly and was slower; profiles/r4_mod_chunk_ab.txt).
-#ifndef SRSGPU_MOD_CHUNK_WORDS
-#define SRSGPU_MOD_CHUNK_WORDS 1024
-#endif
-constexpr uint32_t MOD_CHUNK_WORDS = SRSGPU_MOD_CHUNK_WORDS;
-/// PUSCH demodulator chunk (codeword words per workgroup) and whether a lane prefetches its next RE's received values
-/// and estimates while it equalises the current one (pusch_demodulator.hip).
-#ifndef SRSGPU_DEMOD_CHUNK_WORDS
-#define SRSGPU_DEMOD_CHUNK_WORDS 256
-#endif
-#ifndef SRSGPU_DEMOD_PREFETCH
-#define SRSGPU_DEMOD_PREFETCH 0
-#endif
-constexpr uint32_t DEMOD_CHUNK_WORDS = SRSGPU_DEMOD_CHUNK_WORDS;
+constexpr uint32_t MOD_CHUNK_WORDS = 1024;
+/// PUSCH demodulator chunk (codeword words per workgroup, pusch_demodulator.hip). A lane that issued its next RE's
+/// loads while equalising the current one was slower (r4: 4x the loads in flight, 98 -> 106 VGPRs, 28.3 -> 30.2 us).
+constexpr uint32_t DEMOD_CHUNK_WORDS = 256;
 constexpr uint32_t MOD_MAX_BITS    = 1u << 21;
 /// Gold sequence tables (TS 38.211 section 5.2.1): x1 bits x1(1600 + n) as LSB-first words; x2 chunk jumps
 /// M^(1600 + 2048 c) (c < MOD_MAX_BITS / 2048, 31 column words each); x2 lane jumps M^(32 i) (i < 64) as [column][i].
@@ -634,9 +621,7 @@ void launch_pusch_demodulate_tp(const demod_desc*       d_desc,
                                 const uint32_t*          d_seq,
                                 const uint16_t*          d_crbs,
                                 float*                   d_acc,
-                                hipStream_t              stream,
-                                float*                   d_stats = nullptr,
-                                uint32_t*                d_cnt   = nullptr);
+                                hipStream_t              stream);
 void launch_pusch_demod_stats(float* d_acc, float* d_stats, int nof_tx, hipStream_t stream);
 void launch_pusch_demodulate(const demod_desc*        d_desc,
                              const mod_chunk*         d_chunks,
@@ -650,8 +635,6 @@ void launch_pusch_demodulate(const demod_desc*        d_desc,
                              const uint32_t*          d_seq,
                              const uint16_t*          d_crbs,
                              float*                   d_acc,
-                             hipStream_t              stream,
-                             float*                   d_stats = nullptr,
-                             uint32_t*                d_cnt   = nullptr);
+                             hipStream_t              stream);
 
 } // namespace srsgpu

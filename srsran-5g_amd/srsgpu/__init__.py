@@ -322,6 +322,10 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_context_destroy.restype = None
     lib.srsgpu_context_device.argtypes = [P]
     lib.srsgpu_context_device.restype = ctypes.c_int
+    lib.srsgpu_context_set_option.argtypes = [P, ctypes.c_int, ctypes.c_int]
+    lib.srsgpu_context_set_option.restype = ctypes.c_int
+    lib.srsgpu_context_get_option.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    lib.srsgpu_context_get_option.restype = ctypes.c_int
     lib.srsgpu_ldpc_decoder_plan_create.argtypes = [P, ctypes.c_int, P, ctypes.c_uint32, ctypes.POINTER(P)]
     lib.srsgpu_ldpc_decoder_plan_execute.argtypes = [P, P, P, P, P]
     lib.srsgpu_ldpc_decoder_plan_destroy.argtypes = [P]
@@ -414,7 +418,8 @@ def load_library(path: str = LIB_PATH):
 
 # Every symbol include/srsgpu_phy.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = [
-    "srsgpu_version", "srsgpu_last_error", "srsgpu_context_create", "srsgpu_context_destroy", "srsgpu_context_device", "srsgpu_pusch_demodulator_plan_scrambling",
+    "srsgpu_version", "srsgpu_last_error", "srsgpu_context_create", "srsgpu_context_destroy", "srsgpu_context_device",
+    "srsgpu_context_set_option", "srsgpu_context_get_option", "srsgpu_pusch_demodulator_plan_scrambling",
     "srsgpu_ldpc_decoder_plan_create", "srsgpu_ldpc_decoder_plan_execute", "srsgpu_ldpc_decoder_plan_destroy",
     "srsgpu_ldpc_decode", "srsgpu_pusch_cb_plan_create", "srsgpu_pusch_cb_plan_execute",
     "srsgpu_pusch_cb_plan_destroy", "srsgpu_pdsch_encoder_plan_create", "srsgpu_pdsch_encoder_plan_nof_codeblocks",
@@ -493,6 +498,16 @@ def _dptr(t) -> int:
     return t.data_ptr()
 
 
+# srsgpu_option (include/srsgpu_phy.h): kernel-selection options of a context, read at plan creation.
+OPTION_DECODER_SPLIT = 1          # -1 auto (default), 0 one-row-pair kernel, 1 edge-split kernel
+OPTION_DECODER_PAIRS = 2          # 0 (default) / 1: Z = 144..192 codeblocks two per workgroup
+OPTION_DECODER_FUSED_DEMATCH = 3  # 1 (default) / 0: every codeblock through the separate rate dematcher
+OPTION_ENCODER_BYTE_KERNEL = 4    # 0 (default) / 1: the byte-per-bit encoder kernel for every codeblock
+OPTION_ENCODER_ZERO_OUTPUT = 5    # 0 (default) / 1: the encoder always clears its output first
+OPTION_DEFAULTS = {OPTION_DECODER_SPLIT: -1, OPTION_DECODER_PAIRS: 0, OPTION_DECODER_FUSED_DEMATCH: 1,
+                   OPTION_ENCODER_BYTE_KERNEL: 0, OPTION_ENCODER_ZERO_OUTPUT: 0}
+
+
 class Context:
     """srsgpu_context: one per GPU (one process per GPU)."""
 
@@ -504,6 +519,33 @@ class Context:
         h = ctypes.c_void_p()
         _check(lib.srsgpu_context_create(device, ctypes.byref(h)))
         self.handle = h
+
+    def set_option(self, option: int, value: int) -> None:
+        """srsgpu_context_set_option: plans created afterwards use it."""
+        _check(_lib.srsgpu_context_set_option(self.handle, option, value))
+
+    def get_option(self, option: int) -> int:
+        v = ctypes.c_int()
+        _check(_lib.srsgpu_context_get_option(self.handle, option, ctypes.byref(v)))
+        return v.value
+
+    def options(self, **kw):
+        """Context manager: the given options (OPTION_* names without the prefix, lower case) while inside, the
+        previous values after."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def scope():
+            keys = {globals()["OPTION_" + k.upper()]: v for k, v in kw.items()}
+            old = {k: self.get_option(k) for k in keys}
+            try:
+                for k, v in keys.items():
+                    self.set_option(k, v)
+                yield self
+            finally:
+                for k, v in old.items():
+                    self.set_option(k, v)
+        return scope()
 
     def close(self):
         if getattr(self, "handle", None):

@@ -19,18 +19,17 @@ def ctx():
     return srsgpu.Context(0)
 
 
-# Kernel variants of the packed (even Z) decoder, forced through the plan's A/B switches (capi.cpp): the
-# one-codeblock kernel, its edge-split variant and the multi-codeblock workgroups (PK4, 8- and 16-layer classes).
-VARIANTS = {"plain": {"SRSGPU_DECODER_SPLIT": "0", "SRSGPU_DECODER_PK4": "0"},
-            "split": {"SRSGPU_DECODER_SPLIT": "1", "SRSGPU_DECODER_PK4": "0"},
-            "pk4": {"SRSGPU_DECODER_SPLIT": "0", "SRSGPU_DECODER_PK4": "1"}}
+# Kernel variants of the packed (even Z) decoder, forced through the context's kernel options (srsgpu_option,
+# capi.cpp): the one-codeblock kernel, its edge-split variant and the two-codeblock workgroups (Z = 144..192).
+VARIANTS = {"plain": dict(decoder_split=0, decoder_pairs=0),
+            "split": dict(decoder_split=1, decoder_pairs=0),
+            "pairs": dict(decoder_split=0, decoder_pairs=1)}
 
 
 @pytest.fixture(params=sorted(VARIANTS))
-def variant(request, monkeypatch):
-    for k, v in VARIANTS[request.param].items():
-        monkeypatch.setenv(k, v)
-    return request.param
+def variant(request, ctx):
+    with ctx.options(**VARIANTS[request.param]):
+        yield request.param
 
 
 def _case(orc, rng, bg, Z, trial):
@@ -162,18 +161,22 @@ def test_decoder_golden_vectors(ctx, variant):
 
 
 @pytest.mark.parametrize("mode", [1, 0])
-def test_decoder_pk4_mixed_workgroups(orc, ctx, mode, monkeypatch):
-    """Multi-codeblock workgroups with everything that differs between the slots of one workgroup: codeblocks that
-    stop at different iterations or never, different layer counts (input lengths, trailing zeros), too-short inputs,
-    mixed CRC polynomials and filler lengths, and lifting sizes whose slots straddle waves (Z = 288 / 352 / 208 / 96).
-    Against the oracle, bit-exact."""
+def test_decoder_pairs_mixed_workgroups(orc, ctx, mode):
+    """Two-codeblock workgroups (SRSGPU_OPTION_DECODER_PAIRS) with everything that differs between the slots of one
+    workgroup: codeblocks that stop at different iterations or never, different layer counts (input lengths, trailing
+    zeros), too-short inputs, mixed CRC polynomials and filler lengths, odd counts that leave a slot empty, at every
+    lifting size the pairs take (Z = 144..192). Against the oracle, bit-exact."""
     import srsgpu
-    monkeypatch.setenv("SRSGPU_DECODER_SPLIT", "0")
-    monkeypatch.setenv("SRSGPU_DECODER_PK4", "1")
+    with ctx.options(decoder_split=0, decoder_pairs=1):
+        _pairs_mixed(orc, ctx, mode)
+
+
+def _pairs_mixed(orc, ctx, mode):
+    import srsgpu
     rng = np.random.default_rng(77 + mode)
     dec = srsgpu.LdpcDecoder(ctx, "avx2" if mode == 1 else "generic")
     llrs, cfgs, polys, want = [], [], [], []
-    for bg, Z in ((1, 288), (1, 352), (1, 208), (2, 96), (1, 64)):
+    for bg, Z in ((1, 192), (1, 176), (2, 160), (2, 144), (1, 160)):
         K = BG_K[bg]
         for i in range(23):
             crc_poly = [CRC24B, CRC16, CRC24A][i % 3]

@@ -75,7 +75,7 @@ def test_pdsch_encoder_slot_100mhz(ctx):
 
 
 def test_pdsch_encoder_packed_kernel_every_lifting_size(ctx):
-    """The packed kernel (Z % 32 == 0) against the oracle and against the byte kernel (SRSGPU_ENCODER_BYTE_KERNEL=1)
+    """The packed kernel (Z % 32 == 0) against the oracle and against the byte kernel (SRSGPU_OPTION_ENCODER_BYTE_KERNEL)
     on grants covering every (BG, Z) with Z a multiple of 32 that the TBS tables reach, every Qm and rv."""
     import os
     import srsgpu
@@ -103,11 +103,8 @@ def test_pdsch_encoder_packed_kernel_every_lifting_size(ctx):
     got = srsgpu.PdschEncoder(ctx).encode_batch(tbs, cfgs)
     for i, (a, b) in enumerate(zip(got, want)):
         assert np.array_equal(a, b), (i, cfgs[i])
-    os.environ["SRSGPU_ENCODER_BYTE_KERNEL"] = "1"
-    try:
+    with ctx.options(encoder_byte_kernel=1):
         byte = srsgpu.PdschEncoder(ctx).encode_batch(tbs, cfgs)
-    finally:
-        del os.environ["SRSGPU_ENCODER_BYTE_KERNEL"]
     for a, b in zip(got, byte):
         assert np.array_equal(a, b)
 
@@ -153,10 +150,10 @@ def test_crc_table_arena_long_running_cell(ctx):
         p.close()
 
 
-def test_pdsch_encoder_aligned_plan_without_memset(ctx, monkeypatch):
+def test_pdsch_encoder_aligned_plan_without_memset(ctx):
     """A plan whose codeblocks all cover whole 32-bit words (4 layers of 256QAM) and whose codewords tile the output
     skips the output memset (capi.cpp: zero_output): on an output pre-filled with 0xAB (encode_batch) it must give the
-    oracle's codewords, as the memset path (SRSGPU_ENCODER_ZERO=1) does; a 1-layer QPSK TB in the plan brings the
+    oracle's codewords, as the memset path (SRSGPU_OPTION_ENCODER_ZERO_OUTPUT) does; a 1-layer QPSK TB in the plan brings the
     memset back (edge words ORed)."""
     import srsgpu
     from srsgpu import sch
@@ -173,9 +170,9 @@ def test_pdsch_encoder_aligned_plan_without_memset(ctx, monkeypatch):
         cfgs.append(srsgpu.PdschTransportBlock(seg.base_graph, 0, g.qm, g.nof_layers, g.nof_ch_symbols))
         want.append(cw)
     enc = srsgpu.PdschEncoder(ctx)
-    for zero in ("0", "1"):
-        monkeypatch.setenv("SRSGPU_ENCODER_ZERO", zero)
-        for n in (len(grants), len(grants) + 1):  # aligned plan; plus the unaligned TB
-            got = enc.encode_batch(tbs[:n], cfgs[:n])
-            for i, (a, b) in enumerate(zip(got, want[:n])):
-                assert np.array_equal(a, b), (zero, n, i)
+    for zero in (0, 1):
+        with ctx.options(encoder_zero_output=zero):
+            for n in (len(grants), len(grants) + 1):  # aligned plan; plus the unaligned TB
+                got = enc.encode_batch(tbs[:n], cfgs[:n])
+                for i, (a, b) in enumerate(zip(got, want[:n])):
+                    assert np.array_equal(a, b), (zero, n, i)

@@ -188,11 +188,11 @@ def test_pusch_decoder_large_unaligned_tbs(orc, ctx):
 
 
 @pytest.mark.parametrize("dec_type,mode", [("avx2", 1), ("generic", 0)])
-def test_fused_rate_dematch_in_decoder(orc, ctx, monkeypatch, dec_type, mode):
+def test_fused_rate_dematch_in_decoder(orc, ctx, dec_type, mode):
     """First transmissions that are a plain copy (rv 0, no LBRM, ninfo <= E <= V, even Z) are dematched inside the
     packed decoder (DEC_FLAG_FUSED_DM): 160 such codeblocks mixed with 40 that keep the separate rate dematcher, over a
     HARQ buffer of random old content; iterations, bits, HARQ buffer and CRC flags equal the oracle composition and the
-    unfused plan (SRSGPU_DECODER_FUSED_DM=0)."""
+    unfused plan (SRSGPU_OPTION_DECODER_FUSED_DEMATCH = 0)."""
     import srsgpu
     rng = np.random.default_rng(404 + mode)
     cbs, llrs, inits = [], [], []
@@ -221,9 +221,8 @@ def test_fused_rate_dematch_in_decoder(orc, ctx, monkeypatch, dec_type, mode):
     init = np.concatenate(inits)
     dec = srsgpu.PuschCodeblockDecoder(ctx, dec_type)
     res_f, harq_f, crc_f = dec.decode(llrs, cbs, harq=init.copy())
-    monkeypatch.setenv("SRSGPU_DECODER_FUSED_DM", "0")
-    res_u, harq_u, crc_u = dec.decode(llrs, cbs, harq=init.copy())
-    monkeypatch.delenv("SRSGPU_DECODER_FUSED_DM")
+    with ctx.options(decoder_fused_dematch=0):
+        res_u, harq_u, crc_u = dec.decode(llrs, cbs, harq=init.copy())
     assert np.array_equal(harq_f, harq_u)
     assert np.array_equal(np.asarray(crc_f), np.asarray(crc_u))
     off, n_ok = 0, 0
@@ -486,10 +485,10 @@ def test_pusch_decoder_harq_in_arena(orc, ctx):
         assert int(outs[0][2].sum()) >= 8
 
 
-def test_pusch_decoder_two_codeblock_workgroups(orc, ctx, monkeypatch):
-    """Two codeblocks of Z = 144 .. 192 per workgroup (SRSGPU_DECODER_PK2=1: ldpc_decode_pk4_kernel<..., PKN = 2>,
+def test_pusch_decoder_two_codeblock_workgroups(orc, ctx):
+    """Two codeblocks of Z = 144 .. 192 per workgroup (SRSGPU_OPTION_DECODER_PAIRS: ldpc_decode_pairs_kernel,
     fused rate dematching on first transmissions, the separate dematcher for the rv2 retransmission) equal the
-    one-codeblock kernel (SRSGPU_DECODER_PK2=0, the default) bit for bit: TB flags, TBs, per-CB iteration counts and the HARQ soft bits, over an odd
+    one-codeblock kernel (the default) bit for bit: TB flags, TBs, per-CB iteration counts and the HARQ soft bits, over an odd
     number of such codeblocks (a workgroup with an empty slot) mixed with other lifting sizes; and the oracle."""
     import torch
     import srsgpu
@@ -509,21 +508,21 @@ def test_pusch_decoder_two_codeblock_workgroups(orc, ctx, monkeypatch):
     assert {144, 160, 176, 192} <= zs, zs
     results = {}
     for pk2 in ("1", "0"):
-        monkeypatch.setenv("SRSGPU_DECODER_PK2", pk2)
-        dec = srsgpu.PuschDecoder(ctx, "avx2")
-        out = []
-        for rv, new_data in ((0, True), (2, False)):
-            llrs, cfgs = [], []
-            for i, ((g, seg), tb) in enumerate(zip(grants, tbs)):
-                cw, _, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, rv, g.qm, g.nof_layers, 0, g.nof_ch_symbols)
-                r = np.random.default_rng(1000 * rv + i)
-                llrs.append(bits_to_llrs(r, cw, amp=8.0, noise=[1.0, 3.0, 7.0][i % 3]))
-                cfgs.append(srsgpu.PuschTransportBlock(seg.tbs // 8, seg.base_graph, rv, g.qm, g.nof_layers,
-                                                       g.nof_ch_symbols, new_data=new_data, nof_ldpc_iterations=6))
-            ok, got, iters = dec.decode_batch(llrs, cfgs)
-            out.append((ok, [t.copy() for t in got], iters, dec.harq[0].cpu().numpy().copy()))
-            print(f"PK2={pk2} rv{rv}: TBs ok {sum(ok)}/{len(ok)}, iterations {sorted({x for v in iters for x in v})}")
-        results[pk2] = out
+        with ctx.options(decoder_pairs=int(pk2)):
+            dec = srsgpu.PuschDecoder(ctx, "avx2")
+            out = []
+            for rv, new_data in ((0, True), (2, False)):
+                llrs, cfgs = [], []
+                for i, ((g, seg), tb) in enumerate(zip(grants, tbs)):
+                    cw, _, _ = oracle_pdsch_encode(orc, tb, seg.base_graph, rv, g.qm, g.nof_layers, 0, g.nof_ch_symbols)
+                    r = np.random.default_rng(1000 * rv + i)
+                    llrs.append(bits_to_llrs(r, cw, amp=8.0, noise=[1.0, 3.0, 7.0][i % 3]))
+                    cfgs.append(srsgpu.PuschTransportBlock(seg.tbs // 8, seg.base_graph, rv, g.qm, g.nof_layers,
+                                                           g.nof_ch_symbols, new_data=new_data, nof_ldpc_iterations=6))
+                ok, got, iters = dec.decode_batch(llrs, cfgs)
+                out.append((ok, [t.copy() for t in got], iters, dec.harq[0].cpu().numpy().copy()))
+                print(f"PK2={pk2} rv{rv}: TBs ok {sum(ok)}/{len(ok)}, iterations {sorted({x for v in iters for x in v})}")
+            results[pk2] = out
     for a, b in zip(results["1"], results["0"]):
         assert a[0] == b[0]
         assert all(np.array_equal(x, y) for x, y in zip(a[1], b[1]))

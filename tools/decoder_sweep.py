@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Decoder kernel time vs iterations (no CRC: every codeblock runs max_iterations) for the bench's codeblock shapes,
-plain vs edge-split kernel (SRSGPU_DECODER_SPLIT read at plan creation): fixed cost + per-iteration cost.
+plain vs edge-split kernel (SRSGPU_OPTION_DECODER_SPLIT, read at plan creation): fixed cost + per-iteration cost.
 
     python tools/decoder_sweep.py [--n 1024] [--z 224] [--cols 27]
 """
@@ -32,7 +32,7 @@ def main():
     llr1 = np.clip(np.round(16.0 + rng.normal(0, 6.0, n_llr)), -120, 120).astype(np.int8)
     for n in args.n:
         for split in ("0", "1"):
-            os.environ["SRSGPU_DECODER_SPLIT"] = split
+            ctx.set_option(srsgpu.OPTION_DECODER_SPLIT, int(split))
             row = []
             for iters in range(1, 7):
                 cfg = srsgpu.CodeblockDecodeConfig(1, Z, nof_crc_bits=16, max_iterations=iters)

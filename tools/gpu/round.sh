@@ -16,6 +16,8 @@
 #   lower_trace      rocprofv3 kernel trace of the sector group at 8 sectors
 #   dulow            tools/du_low_bench.py: lower PHY + PUSCH service per sector, paced, 1..8 sectors
 #   lds              PMC pass of the bench: LDS issue stalls, bank conflicts, LDS-array cycles per kernel
+#   traffic          FETCH_SIZE / WRITE_SIZE / SQ passes of the bench -> per-kernel HBM traffic vs algorithmic bytes
+#                    (tools/chain_traffic.py), isolated kernel times, VALU issue and waits (tools/sq_summary.py)
 #   ab:DIR[:N]       A/B of the default bench: the in-tree library against srsran-5g_amd/DIR's, N rounds
 #   slotsab:V=X[:N]  A/B of the UL slot processors (16 threads): default environment against V=X, N rounds
 #   benchab:V=X[:N]  A/B of the default bench: default environment against V=X, N rounds
@@ -89,6 +91,22 @@ for step in "$@"; do
       python3 tools/pmc_summary.py "$CSV" > "$OUT/pmc_lds.txt"
       rm -rf "$OUT/pmc_lds"
       cat "$OUT/pmc_lds.txt" | cut -c1-400 ;;
+    traffic)
+      PB="--no-cpu-baseline --no-extra-points --no-extra-workloads --steps 40 --warmup 4 --min-time 0"
+      timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv \
+        -- python3 -u bench.py $PB > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err" || { tail -20 "$OUT/pmc_fetch.err"; exit 1; }
+      timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv \
+        -- python3 -u bench.py $PB > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err" || { tail -20 "$OUT/pmc_write.err"; exit 1; }
+      timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY \
+        SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS -d "$OUT/pmc_sq" -o run --output-format csv \
+        -- python3 -u bench.py $PB > "$OUT/pmc_sq.json" 2> "$OUT/pmc_sq.err" || { tail -20 "$OUT/pmc_sq.err"; exit 1; }
+      python3 tools/chain_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_fetch.json" > "$OUT/chain_traffic.json"
+      SQ_CSV=$(find "$OUT/pmc_sq" -name "*counter_collection.csv" | head -1)
+      python3 tools/sq_summary.py "$SQ_CSV" "$OUT/sq_valu.json" "$OUT/pmc_sq.json" > "$OUT/sq.log"
+      find "$OUT" -name "*counter_collection.csv" -size +1M -delete
+      find "$OUT" -name "*kernel_trace.csv" -delete
+      cat "$OUT/sq.log" | head -14
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); [print(k, round(v.get('traffic_ratio', 0), 3), round(v.get('isolated_us', 0), 1), round(v.get('hbm_fraction_of_8tbs_isolated', 0), 3)) for k, v in d['stages'].items()]" "$OUT/chain_traffic.json" ;;
     slotsab:*)
       # slotsab:VAR=V[,VAR2=V2][:N] — the UL slot processors at 16 threads (processor_bench.py --only-slots), N rounds
       # (default 2) alternating the default environment and the given variables

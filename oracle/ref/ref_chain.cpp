@@ -89,6 +89,7 @@
 #include "srsran/phy/upper/signal_processors/prs/prs_generator.h"
 #include "srsran/srslog/srslog.h"
 
+#include <algorithm>
 #include <array>
 #include <cmath>
 #include <cstdio>
@@ -1325,7 +1326,14 @@ public:
   void on_new_pusch_results_data(const ul_pusch_results_data& r) override
   {
     if (count_only) {
-      // Benchmarks: results arrive on the GPU service's completion thread; only the count matters.
+      // Benchmarks: results arrive on the GPU service's completion thread; only the count (and, when tracked, the
+      // latency from the slot's reference instant) matters.
+      if (track_latency) {
+        const int64_t now = std::chrono::steady_clock::now().time_since_epoch().count();
+        const int64_t ref = slot_ref[r.slot.system_slot() % slot_ref.size()].load(std::memory_order_acquire);
+        std::lock_guard<std::mutex> lock(mtx);
+        latency_ns.push_back(now - ref);
+      }
       crc_ok += r.decoder_result.tb_crc_ok ? 1 : 0;
       ++nof_data;
       return;
@@ -1368,8 +1376,23 @@ public:
     records.clear();
     harq_ack.clear();
     csi.clear();
+    latency_ns.clear();
     nof_data = 0;
     crc_ok   = 0;
+  }
+
+  /// Latency tracking (benchmarks): the reference instant (steady clock) of each system slot - its last symbol - set by
+  /// the slot's producer before the slot is processed; each data notification records now - reference.
+  void track(bool on)
+  {
+    track_latency = on;
+    if (on && slot_ref.empty()) {
+      slot_ref = std::vector<std::atomic<int64_t>>(20480);
+    }
+  }
+  void set_slot_reference(slot_point sp, std::chrono::steady_clock::time_point t)
+  {
+    slot_ref[sp.system_slot() % slot_ref.size()].store(t.time_since_epoch().count(), std::memory_order_release);
   }
 
   std::mutex                         mtx;
@@ -1378,6 +1401,9 @@ public:
   std::map<int, std::pair<std::array<int, 3>, std::array<int, 3>>> csi;  ///< RNTI -> CSI Part 1, Part 2 fields
   unsigned                           nof_control = 0;
   bool                               count_only  = false;
+  bool                               track_latency = false;
+  std::vector<std::atomic<int64_t>>  slot_ref;
+  std::vector<int64_t>               latency_ns;
   std::atomic<unsigned>              nof_data{0};
   std::atomic<unsigned>              crc_ok{0};
 };
@@ -1775,6 +1801,26 @@ int chain_dl_slot(void*               p,
 }
 
 
+/// p50 / p90 / p99 / max / mean (us) of latencies (ns) and the fraction above budget_us; out[6] = samples.
+void latency_summary(std::vector<int64_t> v, double budget_us, double* out)
+{
+  std::sort(v.begin(), v.end());
+  const size_t n = v.size();
+  auto         q = [&](double f) { return n ? static_cast<double>(v[std::min(n - 1, static_cast<size_t>(f * n))]) * 1e-3 : 0.0; };
+  double       sum = 0, over = 0;
+  for (int64_t x : v) {
+    sum += static_cast<double>(x) * 1e-3;
+    over += static_cast<double>(x) * 1e-3 > budget_us ? 1 : 0;
+  }
+  out[0] = q(0.5);
+  out[1] = q(0.9);
+  out[2] = q(0.99);
+  out[3] = n ? static_cast<double>(v.back()) * 1e-3 : 0.0;
+  out[4] = n ? sum / static_cast<double>(n) : 0.0;
+  out[5] = n ? over / static_cast<double>(n) : 0.0;
+  out[6] = static_cast<double>(n);
+}
+
 /// Slot-processor throughput (the reference's pusch_processor_benchmark / pdsch_processor_benchmark "throughput total"
 /// scheme, at the granularity du_low drives: one uplink / downlink processor per thread, each running slots of
 /// `nof_pdus` PDUs through the reference's uplink_processor_impl / downlink_processor_single_executor_impl, variant 0 =
@@ -1791,9 +1837,15 @@ int chain_ul_bench(int                 device,
                    const uint16_t*     grid_in,
                    unsigned            nof_ports,
                    unsigned            grid_prb,
-                   double*             seconds)
+                   double*             seconds,
+                   double              pace_us,
+                   double*             latency)
 {
   return guarded("chain_ul_bench", [&] {
+    // pace_us > 0: every thread (sector) submits its slot i at t0 + i pace_us - a radio's slot clock, the sectors
+    // aligned - and each PUSCH data notification's latency from its slot's submission (handle_rx_symbol of the last
+    // symbol) is recorded; latency[0..6] = latency_summary over all sectors (budget: du_low's max_processing_delay_slots
+    // = 5 slots of pace_us, du_low_config.h:39), latency[7] = the largest lag of a submission behind its instant (us).
     // variant 0: reference CPU processors; 1: GPU slot batches, one synchronous uplink processor per thread (sector)
     // with a private GPU service; 2: du_low's structure on one shared GPU service - each sector (thread) a ring of
     // UL_RING uplink processors over one rx buffer pool and HARQ arena, slots completing asynchronously, the service
@@ -1849,11 +1901,27 @@ int chain_ul_bench(int                 device,
     auto                   notifier_of = [&](unsigned t) -> ul_results_recorder& {
       return shared ? sectors[t]->notifier : *hs[t].front()->notifier;
     };
-    auto run_slots = [&](unsigned t, unsigned n) {
+    using bclock = std::chrono::steady_clock;
+    bclock::time_point  pace_t0;
+    const bool          paced = pace_us > 0;
+    std::vector<double> max_lag(nof_threads, 0.0);
+    auto run_slots = [&](unsigned t, unsigned n, bool timed) {
+      if (timed && paced) {
+        (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
+      }
       for (unsigned i = 0; i != n; ++i) {
         const unsigned   s  = slot_no[t]++;
         const slot_point sp(subcarrier_spacing::kHz30, s % 20480);
         ul_harness*      h  = hs[t][s % hs[t].size()];
+        if (timed && paced) {
+          const auto due = pace_t0 + std::chrono::nanoseconds(static_cast<int64_t>(pace_us * 1e3 * i));
+          const auto now = bclock::now();
+          if (now < due) {
+            std::this_thread::sleep_until(due);
+          } else {
+            max_lag[t] = std::max(max_lag[t], std::chrono::duration<double, std::micro>(now - due).count());
+          }
+        }
         unique_uplink_pdu_slot_repository repo = h->proc->get_pdu_slot_repository(sp);
         while (!repo.is_valid()) {
           // The ring's processor still holds an earlier slot (its PUSCH results are not all notified yet).
@@ -1876,6 +1944,9 @@ int chain_ul_bench(int                 device,
           }
         }
         g.release();
+        if (notifier_of(t).track_latency) {
+          notifier_of(t).set_slot_reference(sp, bclock::now());
+        }
         h->proc->get_slot_processor(sp).handle_rx_symbol(13);
         submitted[t] += static_cast<unsigned>(nof_pdus);
       }
@@ -1884,20 +1955,25 @@ int chain_ul_bench(int                 device,
     // Warm-up over one frame (20 slots at 30 kHz): every slot number's DM-RS plans, pools, first touch - a DU runs
     // continuously, and the GPU batches cache their slot-dependent plans per slot number.
     for (unsigned t = 0; t != nof_threads; ++t) {
-      workers[t]->post([&, t] { run_slots(t, 20); });
+      workers[t]->post([&, t] { run_slots(t, 20, false); });
     }
     for (auto& w : workers) {
       w->wait();
     }
-    int ok = 0;
+    for (unsigned t = 0; t != nof_threads; ++t) {
+      notifier_of(t).track(latency != nullptr);
+    }
+    int                  ok = 0;
+    std::vector<int64_t> lat;
     for (unsigned r = 0; r != repetitions; ++r) {
       for (unsigned t = 0; t != nof_threads; ++t) {
         notifier_of(t).reset();
         submitted[t] = 0;
       }
       const auto t0 = std::chrono::steady_clock::now();
+      pace_t0       = t0 + std::chrono::milliseconds(2);
       for (unsigned t = 0; t != nof_threads; ++t) {
-        workers[t]->post([&, t] { run_slots(t, slots); });
+        workers[t]->post([&, t] { run_slots(t, slots, true); });
       }
       for (auto& w : workers) {
         w->wait();
@@ -1906,7 +1982,13 @@ int chain_ul_bench(int                 device,
       ok         = 0;
       for (unsigned t = 0; t != nof_threads; ++t) {
         ok += static_cast<int>(notifier_of(t).crc_ok.load());
+        std::lock_guard<std::mutex> lock(notifier_of(t).mtx);
+        lat.insert(lat.end(), notifier_of(t).latency_ns.begin(), notifier_of(t).latency_ns.end());
       }
+    }
+    if (latency != nullptr) {
+      latency_summary(lat, 5.0 * (paced ? pace_us : 500.0), latency);
+      latency[7] = *std::max_element(max_lag.begin(), max_lag.end());
     }
     for (unsigned t = 0; t != nof_threads; ++t) {
       workers[t]->post([&, t] {
@@ -2019,9 +2101,13 @@ int chain_du_low_ul(int                 device,
                     unsigned            in_flight,
                     double*             lag,
                     int*                results,
-                    double*             seconds)
+                    double*             seconds,
+                    double*             latency)
 {
   return guarded("chain_du_low_ul", [&] {
+    // latency (8 values, may be null): the PUSCH results' latency from the end of their slot on the radio's clock (the
+    // instant its last symbol has been received) to the data notification, over every sector: latency_summary with
+    // du_low's budget of max_processing_delay_slots = 5 slots (du_low_config.h:39), then the number of samples.
     using clock         = std::chrono::steady_clock;
     constexpr unsigned UL_RING = 4;
     const unsigned     nsc     = 12 * grid_prb;
@@ -2136,6 +2222,9 @@ int chain_du_low_ul(int                 device,
         g.release();
         submitted[k] += static_cast<unsigned>(nof_pdus);
         const unsigned q0 = sp.subframe_slot_index() * 14;
+        if (paced && s.sec->notifier.track_latency) {
+          s.sec->notifier.set_slot_reference(sp, t0 + period * (i_sym + 14));
+        }
         for (unsigned l = 0; l != 14; ++l) {
           if (paced) {
             const clock::time_point due = t0 + period * i_sym++;
@@ -2173,6 +2262,7 @@ int chain_du_low_ul(int                 device,
     }
     for (unsigned k = 0; k != nof_sectors; ++k) {
       st[k]->sec->notifier.reset();
+      st[k]->sec->notifier.track(latency != nullptr);
       st[k]->notifier.late = 0;
       submitted[k]         = 0;
     }
@@ -2191,6 +2281,15 @@ int chain_du_low_ul(int                 device,
       lag[4 * k + 3]     = st[k]->notifier.late.load();
       results[2 * k]     = static_cast<int>(st[k]->sec->notifier.nof_data.load());
       results[2 * k + 1] = static_cast<int>(st[k]->sec->notifier.crc_ok.load());
+    }
+    if (latency != nullptr) {
+      std::vector<int64_t> all;
+      for (unsigned k = 0; k != nof_sectors; ++k) {
+        std::lock_guard<std::mutex> lock(st[k]->sec->notifier.mtx);
+        all.insert(all.end(), st[k]->sec->notifier.latency_ns.begin(), st[k]->sec->notifier.latency_ns.end());
+      }
+      latency_summary(all, 5 * 500.0, latency);
+      latency[7] = 0;
     }
     for (unsigned k = 0; k != nof_sectors; ++k) {
       workers[k]->post([&, k] {

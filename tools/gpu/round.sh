@@ -9,6 +9,9 @@
 #   bench_driver     python bench.py --steps 20 --warmup 5 -> bench_driver.json
 #   slots1 / slots16 tools/processor_bench.py --only-slots at 1 / 16 threads (SRSGPU_BATCH_TIMING=1)
 #   slots16ul        the same, UL only
+#   slotslat         UL slot processors at 16 threads, free-running and paced at real time (500 us per slot and
+#                    sector): throughput, PUSCH result latency, service plan / graph counters
+#   dulowul          tools/du_low_bench.py, UL only, sector group with 13 symbols in flight, 4/6/8 sectors (latency)
 #   slots_trace16    the same at 16 threads
 #   slots_trace      rocprofv3 kernel + memory-copy trace of the slot processors at one thread (UL)
 #   kstats           rocprofv3 --kernel-trace --stats of the default bench
@@ -56,6 +59,15 @@ for step in "$@"; do
         --slots 100 --repetitions 3 --directions "$DIRS" > "$OUT/$step.json" 2> "$OUT/$step.log" \
         || { tail -20 "$OUT/$step.log"; exit 1; }
       grep -v '^pusch_slot_batch' "$OUT/$step.log" | tail -4; grep '^pusch_slot_batch' "$OUT/$step.log" | tail -2 ;;
+    slotslat)
+      SRSGPU_BATCH_TIMING=1 timeout -k 10 500 python -u tools/processor_bench.py --only-slots --threads 16 \
+        --slots 100 --repetitions 3 --directions ul --pace-us 500 > "$OUT/slotslat.json" 2> "$OUT/slotslat.log" \
+        || { tail -20 "$OUT/slotslat.log"; exit 1; }
+      grep -v '^pusch_slot_batch' "$OUT/slotslat.log" | cut -c1-600 | tail -12 ;;
+    dulowul)
+      timeout -k 10 500 python -u tools/du_low_bench.py --direction ul --sectors 4,6,8 --variants group \
+        --in-flight 13 > "$OUT/du_low_ul.json" 2> "$OUT/du_low_ul.log" || { tail -20 "$OUT/du_low_ul.log"; exit 1; }
+      tail -c 1500 "$OUT/du_low_ul.json" ;;
     slots_trace16)
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/trace16" -o slots -- python3 -u \
         tools/processor_bench.py --only-slots --threads 16 --repetitions 1 --slots 30 --directions ul \

@@ -45,7 +45,7 @@ def run(lib, fn, mode, p, tbs, threads, batch, reps, weights=None):
             "pdus_per_s": pdus / med, "tb_crc_ok": int(r)}
 
 
-def slot_cases(lib, T, slots, R, directions=("ul", "dl")):
+def slot_cases(lib, T, slots, R, directions=("ul", "dl"), pace_us=0.0):
     """The same profiles through the reference's slot processors (uplink_processor_impl /
     downlink_processor_single_executor_impl), one per thread, reference CPU processors (variant 0) vs the GPU slot batches
     of integration/pusch_batch_gpu.cpp / upper_phy_gpu.cpp (variant 1: one synchronous uplink processor per thread;
@@ -59,7 +59,7 @@ def slot_cases(lib, T, slots, R, directions=("ul", "dl")):
     lib.chain_ul_bench.restype = ctypes.c_int
     lib.chain_ul_bench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint,
                                    ctypes.c_int, PP, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint,
-                                   ctypes.c_void_p]
+                                   ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p]
     lib.chain_dl_bench.restype = ctypes.c_int
     lib.chain_dl_bench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint,
                                    ctypes.c_int, PP, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint,
@@ -77,15 +77,31 @@ def slot_cases(lib, T, slots, R, directions=("ul", "dl")):
         for v in (0, 1, 2):
             n = slots
             secs = np.zeros(R, np.float64)
-            r = lib.chain_ul_bench(0, v, T, n, R, len(pdus), arr, ptr(tbb), ptr(g), 4, 273, ptr(secs))
+            lat = np.zeros(8, np.float64)
+            r = lib.chain_ul_bench(0, v, T, n, R, len(pdus), arr, ptr(tbb), ptr(g), 4, 273, ptr(secs), 0.0, ptr(lat))
             assert r >= 0, r
             med = float(np.median(secs))
-            case["runs"].append({"variant": ["reference CPU processors", "GPU slot batch, synchronous",
-                                             "GPU service: 4 uplink processors per sector, asynchronous, "
-                                             "sectors aggregated per slot"][v], "threads": T,
-                                 "slots_per_thread": n, "seconds_median": med,
-                                 "throughput_mbps_median": T * n * sum(tbs) / med / 1e6,
-                                 "slots_per_s": T * n / med})
+            run = {"variant": ["reference CPU processors", "GPU slot batch, synchronous",
+                               "GPU service: 4 uplink processors per sector, asynchronous, "
+                               "sectors aggregated per slot"][v], "threads": T,
+                   "slots_per_thread": n, "seconds_median": med, "seconds": secs.tolist(),
+                   "throughput_mbps_median": T * n * sum(tbs) / med / 1e6,
+                   "slots_per_s": T * n / med,
+                   # free-running: submission -> notification, queueing included (the paced section is the latency)
+                   "latency_us_free_running": dict(zip(("p50", "p90", "p99", "max", "mean"), lat[:5]))}
+            if pace_us > 0:
+                # Real time: every sector submits a slot every pace_us (aligned, a radio's slot clock); the latency of
+                # each PUSCH result from its slot's submission (handle_rx_symbol of the last symbol).
+                lat = np.zeros(8, np.float64)
+                r = lib.chain_ul_bench(0, v, T, n, 1, len(pdus), arr, ptr(tbb), ptr(g), 4, 273, ptr(secs), pace_us,
+                                       ptr(lat))
+                assert r >= 0, r
+                run["paced"] = {"slot_period_us": pace_us, "seconds": float(secs[0]),
+                                "kept_pace": bool(lat[7] < 5 * pace_us),
+                                "max_submission_lag_us": float(lat[7]),
+                                "latency_us": dict(zip(("p50", "p90", "p99", "max", "mean"), lat[:5])),
+                                "over_5_slot_budget": float(lat[5]), "samples": int(lat[6])}
+            case["runs"].append(run)
         out["ul"].append(case)
         print(json.dumps(case), file=sys.stderr, flush=True)
 
@@ -157,12 +173,16 @@ def main():
     ap.add_argument("--slots", type=int, default=20, help="slot-processor section: slots per thread and repetition")
     ap.add_argument("--only-slots", action="store_true", help="run only the slot-processor section")
     ap.add_argument("--directions", default="ul,dl", help="slot-processor section: ul, dl or ul,dl")
+    ap.add_argument("--pace-us", type=float, default=0.0,
+                    help="slot-processor section, UL: also run every variant paced at one slot per this many us per "
+                         "sector (500 = real time at 30 kHz) and report the PUSCH result latency")
     args = ap.parse_args()
     if args.only_slots:
         print(json.dumps({"threads": args.threads, "slot_processors": slot_cases(ctypes.CDLL(H.CHAIN_SO),
                                                                                 args.threads, args.slots,
                                                                                 args.repetitions,
-                                                                                args.directions.split(","))}))
+                                                                                args.directions.split(","),
+                                                                                args.pace_us)}))
         return
     lib = ctypes.CDLL(H.CHAIN_SO)
     PP = ctypes.POINTER(H.ChainParams)

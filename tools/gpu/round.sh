@@ -21,6 +21,7 @@
 #   lds              PMC pass of the bench: LDS issue stalls, bank conflicts, LDS-array cycles per kernel
 #   traffic          FETCH_SIZE / WRITE_SIZE / SQ passes of the bench -> per-kernel HBM traffic vs algorithmic bytes
 #                    (tools/chain_traffic.py), isolated kernel times, VALU issue and waits (tools/sq_summary.py)
+#   ofdmab:DIR[:N]   tools/ofdm_bench.py (isolated OFDM launches, bench shape): in-tree library against DIR's, N rounds
 #   ab:DIR[:N]       A/B of the default bench: the in-tree library against srsran-5g_amd/DIR's, N rounds
 #   slotsab:V=X[:N]  A/B of the UL slot processors (16 threads): default environment against V=X, N rounds
 #   benchab:V=X[:N]  A/B of the default bench: default environment against V=X, N rounds
@@ -146,6 +147,16 @@ for step in "$@"; do
             || { tail -20 "$OUT/benchab_${v}_$i.err"; exit 1; }
           python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value']), [round(p['value']) for p in d['operating_points']], round(d['stage_ms_per_step']['pusch_decode'], 4), {k: round(v['value']) for k, v in d.get('workloads', {}).items()})" \
             "$OUT/benchab_${v}_$i.json" "$v ${E[*]}"
+        done
+      done ;;
+    ofdmab:*)
+      SPEC=${step#ofdmab:}; DIR=${SPEC%%:*}; N=2; [[ "$SPEC" == *:* ]] && N=${SPEC##*:}
+      for i in $(seq 1 "$N"); do
+        for lib in lib "$DIR"; do
+          echo "-- $lib"
+          SRSGPU_LIB=srsran-5g_amd/$lib/libsrsgpu_phy.so timeout -k 10 120 python -u tools/ofdm_bench.py \
+            > "$OUT/ofdmab_${lib}_$i.txt" 2>&1 || { tail -20 "$OUT/ofdmab_${lib}_$i.txt"; exit 1; }
+          head -2 "$OUT/ofdmab_${lib}_$i.txt"
         done
       done ;;
     ab:*)

@@ -1330,7 +1330,7 @@ public:
       // latency from the slot's reference instant) matters.
       if (track_latency) {
         const int64_t now = std::chrono::steady_clock::now().time_since_epoch().count();
-        const int64_t ref = slot_ref[r.slot.system_slot() % slot_ref.size()].load(std::memory_order_acquire);
+        const int64_t ref = slot_ref[r.slot.slot_index() % slot_ref.size()].load(std::memory_order_acquire);
         std::lock_guard<std::mutex> lock(mtx);
         latency_ns.push_back(now - ref);
       }
@@ -1381,18 +1381,20 @@ public:
     crc_ok   = 0;
   }
 
-  /// Latency tracking (benchmarks): the reference instant (steady clock) of each system slot - its last symbol - set by
-  /// the slot's producer before the slot is processed; each data notification records now - reference.
+  /// Latency tracking (benchmarks): the reference instant (steady clock) of each slot - its last symbol - set by the
+  /// slot's producer before the slot is processed; each data notification records now - reference. Keyed by the slot
+  /// index within the frame: the harnesses' PDUs carry that index only (frame 0), and a sector has far fewer than a
+  /// frame's slots in flight.
   void track(bool on)
   {
     track_latency = on;
     if (on && slot_ref.empty()) {
-      slot_ref = std::vector<std::atomic<int64_t>>(20480);
+      slot_ref = std::vector<std::atomic<int64_t>>(20);
     }
   }
   void set_slot_reference(slot_point sp, std::chrono::steady_clock::time_point t)
   {
-    slot_ref[sp.system_slot() % slot_ref.size()].store(t.time_since_epoch().count(), std::memory_order_release);
+    slot_ref[sp.slot_index() % slot_ref.size()].store(t.time_since_epoch().count(), std::memory_order_release);
   }
 
   std::mutex                         mtx;

@@ -143,11 +143,58 @@ __device__ __forceinline__ void load_twiddles(const float2* __restrict__ tw, flo
   }
 }
 
-/// One Stockham pass of radix R over N points (NS = product of the previous passes' radices): butterfly j takes
-/// x[j + r N / R], twiddles by W^(r k) (preloaded in w), k = j mod NS, and writes X[(j - k) R + k + r NS].
-template <int N, int R, int NS, int S, typename Src, typename Dst>
-__device__ __forceinline__ void stockham_pass(const float2 (&w)[16 / R][R], Src src, Dst dst)
+/// W^k = exp(S 2 pi i k / (16 NS)), k = tid mod NS: the base twiddle of this thread's butterfly in a radix-16 pass
+/// after passes of total radix NS (the table holds exp(-2 pi i m / OFDM_MAX_DFT)). Loaded at kernel start for every
+/// pass (one 8-byte L2 gather each, in flight under the first pass's HBM loads); the powers are expanded in the pass
+/// itself (twiddle16), so the transform holds 2 VGPRs per later pass instead of 32.
+template <int NS, int S>
+__device__ __forceinline__ float2 twiddle_base(const float2* __restrict__ tw)
 {
+  const int k = static_cast<int>(threadIdx.x) & (NS - 1);
+  float2    x = tw[k * static_cast<int>(OFDM_MAX_DFT / (NS * 16))];
+  if constexpr (S > 0) {
+    x.y = -x.y;
+  }
+  return x;
+}
+
+/// v[r] *= W^r, r = 1..15, from W = w1: W^2, W^4, W^8 by squaring, the other powers by at most three complex products
+/// (relative error < 1e-6), each power formed just before its product so that few stay live.
+__device__ __forceinline__ void twiddle16(float2 (&v)[16], float2 w1)
+{
+  const float2 w2 = cmul(w1, w1);
+  const float2 w4 = cmul(w2, w2);
+  const float2 w8 = cmul(w4, w4);
+  const float2 w3 = cmul(w1, w2);
+  const float2 w5 = cmul(w4, w1);
+  const float2 w6 = cmul(w4, w2);
+  const float2 w7 = cmul(w4, w3);
+  v[1]            = cmul(v[1], w1);
+  v[2]            = cmul(v[2], w2);
+  v[3]            = cmul(v[3], w3);
+  v[4]            = cmul(v[4], w4);
+  v[5]            = cmul(v[5], w5);
+  v[6]            = cmul(v[6], w6);
+  v[7]            = cmul(v[7], w7);
+  v[8]            = cmul(v[8], w8);
+  v[9]            = cmul(v[9], cmul(w8, w1));
+  v[10]           = cmul(v[10], cmul(w8, w2));
+  v[11]           = cmul(v[11], cmul(w8, w3));
+  v[12]           = cmul(v[12], cmul(w8, w4));
+  v[13]           = cmul(v[13], cmul(w8, w5));
+  v[14]           = cmul(v[14], cmul(w8, w6));
+  v[15]           = cmul(v[15], cmul(w8, w7));
+}
+
+/// One Stockham pass of radix R over N points (NS = product of the previous passes' radices): butterfly j takes
+/// x[j + r N / R], twiddles by W^(r k) (k = j mod NS, expanded from the base wb), and writes X[(j - k) R + k + r NS].
+/// Twiddled passes are radix 16 (one butterfly per thread); a radix below 16 is the first pass only (NS = 1).
+/// SYNC_IN: the inputs come from the LDS buffer the outputs overwrite, so every thread's reads complete first (the
+/// first pass reads HBM and needs no barrier before its LDS stores).
+template <int N, int R, int NS, int S, bool SYNC_IN, typename Src, typename Dst>
+__device__ __forceinline__ void stockham_pass(float2 wb, Src src, Dst dst)
+{
+  static_assert(R == 16 || NS == 1, "twiddled passes are radix 16");
   constexpr int T = N / 16;
   constexpr int B = 16 / R;
   float2        v[B][R];
@@ -160,16 +207,15 @@ __device__ __forceinline__ void stockham_pass(const float2 (&w)[16 / R][R], Src 
       v[b][r] = src(j + r * (N / R));
     }
   }
-  __syncthreads();
+  if constexpr (SYNC_IN) {
+    __syncthreads();
+  }
 #pragma unroll
   for (int b = 0; b < B; ++b) {
     const int j = tid + b * T;
     const int k = j & (NS - 1);
     if constexpr (NS > 1) {
-#pragma unroll
-      for (int r = 1; r < R; ++r) {
-        v[b][r] = cmul(v[b][r], w[b][r]);
-      }
+      twiddle16(v[b], wb);
     }
     dft_reg<R, S>(v[b]);
     const int base = (j - k) * R + k;
@@ -311,24 +357,19 @@ __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ 
   auto ld = [lds](int i) { return lds[i]; };
   auto st = [lds](int i, float2 v) { lds[i] = v; };
   static_assert(NP >= 2 && NP <= 4, "supported DFT sizes: 128..8192");
-  float2 w0[16 / R0][R0], w1[1][16], w2[1][16], w3[1][16];
-  load_twiddles<N, 16, R0, S>(tw, w1);
-  if constexpr (NP >= 3) {
-    load_twiddles<N, 16, R0 * 16, S>(tw, w2);
-  }
-  if constexpr (NP == 4) {
-    load_twiddles<N, 16, R0 * 256, S>(tw, w3);
-  }
-  stockham_pass<N, R0, 1, S>(w0, src_first, st);  // NS = 1: no twiddles
+  const float2 b1 = twiddle_base<R0, S>(tw);
+  const float2 b2 = NP >= 3 ? twiddle_base<R0 * 16, S>(tw) : float2{};
+  const float2 b3 = NP == 4 ? twiddle_base<R0 * 256, S>(tw) : float2{};
+  stockham_pass<N, R0, 1, S, false>(float2{}, src_first, st);  // NS = 1: no twiddles
   if constexpr (NP == 2) {
-    stockham_pass<N, 16, R0, S>(w1, ld, dst_last);
+    stockham_pass<N, 16, R0, S, true>(b1, ld, dst_last);
   } else if constexpr (NP == 3) {
-    stockham_pass<N, 16, R0, S>(w1, ld, st);
-    stockham_pass<N, 16, R0 * 16, S>(w2, ld, dst_last);
+    stockham_pass<N, 16, R0, S, true>(b1, ld, st);
+    stockham_pass<N, 16, R0 * 16, S, true>(b2, ld, dst_last);
   } else {
-    stockham_pass<N, 16, R0, S>(w1, ld, st);
-    stockham_pass<N, 16, R0 * 16, S>(w2, ld, st);
-    stockham_pass<N, 16, R0 * 256, S>(w3, ld, dst_last);
+    stockham_pass<N, 16, R0, S, true>(b1, ld, st);
+    stockham_pass<N, 16, R0 * 16, S, true>(b2, ld, st);
+    stockham_pass<N, 16, R0 * 256, S, true>(b3, ld, dst_last);
   }
 }
 

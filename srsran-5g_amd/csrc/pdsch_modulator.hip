@@ -59,12 +59,30 @@ __device__ __forceinline__ uint32_t to_bf16_bits(float v)
   return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
 }
 
+/// Constellation point of a Qm-bit index on the TS 38.211 section 5.1 integer grid (Gray mapping; the amplitude is in
+/// the precoding weights): bit pairs (2j + 1, 2j) from the least significant pick the signs of the real and imaginary
+/// parts after j + 1 levels (the reference's modulation_mapper_lut_impl.cpp tables hold the same points).
+__device__ __forceinline__ float2 constellation_point(uint32_t idx, uint32_t qm)
+{
+  int re = 0, im = 0, off = -1;
+  for (uint32_t j = 0; j < qm / 2; ++j) {
+    re += off;
+    im += off;
+    off *= 2;
+    re = ((idx >> (2 * j + 1)) & 1u) ? re : -re;
+    im = ((idx >> (2 * j)) & 1u) ? im : -im;
+  }
+  return make_float2(static_cast<float>(re), static_cast<float>(im));
+}
+
 /// The chunk's REs: modulation, layer mapping, precoding and mapping. MAP: general allocation (the plan's RE ->
-/// subcarrier map); PRG: per-PRG precoding weights (resource_grid_mapper_impl.cpp:218).
+/// subcarrier map); PRG: per-PRG precoding weights (resource_grid_mapper_impl.cpp:218). points: the transmission's
+/// 2^Qm constellation points, staged in LDS by the workgroup (one LDS read per layer and RE).
 template <bool MAP, bool PRG>
 __device__ __forceinline__ void modulate_res(const mod_desc& d,
                                              const mod_chunk& ch,
                                              const uint32_t*  bits,
+                                             const float2*    points,
                                              const uint16_t* __restrict__ sc_map,
                                              const float* __restrict__ prg_w,
                                              uint32_t* __restrict__ grids)
@@ -82,17 +100,25 @@ __device__ __forceinline__ void modulate_res(const mod_desc& d,
     }
   }
 
+  // OFDM symbol of the lane's current RE (allocation order: symbol-major, ascending subcarrier) and the first RE of
+  // the next symbol: a lane's REs are MOD_THREADS apart, so the symbol search runs only when a lane crosses into a
+  // later symbol.
+  uint32_t l = 0, next = 0;
   for (uint32_t r = ch.re_begin + tid; r < ch.re_end; r += MOD_THREADS) {
     // The RE's L * Qm bits, left-aligned in 64 bits.
     const uint32_t o  = r * Lq - ch.word0 * 32u;
     const uint32_t wi = o >> 5;
     const uint64_t b  = ((static_cast<uint64_t>(bits[wi]) << 32) | bits[wi + 1]) << (o & 31u);
 
-    // OFDM symbol and subcarrier of the RE (allocation order: symbol-major, ascending subcarrier).
-    uint32_t l = 0;
+    if (r >= next) {
+      l    = 0;
+      next = 0xffffffffu;
 #pragma unroll
-    for (int j = 1; j < 15; ++j) {
-      l += (d.sym_cum[j] <= r) ? 1u : 0u;
+      for (int j = 1; j < 15; ++j) {
+        const uint32_t c = d.sym_cum[j];
+        l += (c <= r) ? 1u : 0u;
+        next = (c > r && c < next) ? c : next;
+      }
     }
     const uint32_t k = r - d.sym_cum[l];
     uint32_t       sc;
@@ -112,22 +138,14 @@ __device__ __forceinline__ void modulate_res(const mod_desc& d,
     // Per-PRG precoding: the weights of the PRG holding the RE's subcarrier.
     const float* wt = PRG ? prg_w + d.prg_w + (sc / d.prg_sc) * 32u : nullptr;
 
-    // Constellation points of the layers (TS 38.211 section 5.1 integer grid; the amplitude is in the weights).
+    // Constellation points of the layers.
     float xr[4], xi[4];
 #pragma unroll
     for (int ly = 0; ly < 4; ++ly) {
       if (ly < static_cast<int>(L)) {
-        const uint32_t idx = static_cast<uint32_t>(b >> (64u - (ly + 1) * qm)) & qmask;
-        int            re = 0, im = 0, off = -1;
-        for (uint32_t j = 0; j < qm / 2; ++j) {
-          re += off;
-          im += off;
-          off *= 2;
-          re = ((idx >> (2 * j + 1)) & 1u) ? re : -re;
-          im = ((idx >> (2 * j)) & 1u) ? im : -im;
-        }
-        xr[ly] = static_cast<float>(re);
-        xi[ly] = static_cast<float>(im);
+        const float2 x = points[static_cast<uint32_t>(b >> (64u - (ly + 1) * qm)) & qmask];
+        xr[ly]         = x.x;
+        xi[ly]         = x.y;
       }
     }
 
@@ -162,10 +180,15 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
                                                                       const uint32_t* __restrict__ seq)
 {
   __shared__ uint32_t bits[MOD_CHUNK_WORDS + 1];
+  __shared__ float2   points[256];
   const mod_chunk ch  = chunks[blockIdx.x];
   const mod_desc& d   = descs[ch.tx];
   const uint32_t  tid = threadIdx.x;
   const uint32_t  nwords = (d.nof_bits + 31u) >> 5;
+  static_assert(MOD_THREADS >= 256, "one constellation point per lane");
+  if (tid < (1u << d.qm)) {
+    points[tid] = constellation_point(tid, d.qm);
+  }
 
   // Stage the chunk's scrambled words (and the first word of the next chunk, for an RE straddling the boundary).
   for (uint32_t j = tid; j < MOD_CHUNK_WORDS; j += MOD_THREADS) {
@@ -184,11 +207,11 @@ __global__ __launch_bounds__(MOD_THREADS) void pdsch_modulate_kernel(const mod_d
   // weights in registers and its subcarrier arithmetic; the general path reads the RE -> subcarrier map and, with
   // PRGs, the PRG's weights.
   if (d.sc_map == NO_SC_MAP) {
-    modulate_res<false, false>(d, ch, bits, sc_map, prg_w, grids);
+    modulate_res<false, false>(d, ch, bits, points, sc_map, prg_w, grids);
   } else if (d.prg_sc == 0) {
-    modulate_res<true, false>(d, ch, bits, sc_map, prg_w, grids);
+    modulate_res<true, false>(d, ch, bits, points, sc_map, prg_w, grids);
   } else {
-    modulate_res<true, true>(d, ch, bits, sc_map, prg_w, grids);
+    modulate_res<true, true>(d, ch, bits, points, sc_map, prg_w, grids);
   }
 }
 

@@ -25,7 +25,7 @@ def main():
     a = ap.parse_args()
     ctx = srsgpu.Context(0)
     dev = torch.device("cuda", 0)
-    slots = [s % 20 for s in range(a.slots)]
+    slots = [s % 2 for s in range(a.slots)]  # slot index within the subframe
     res = {"slots": a.slots, "ports": a.ports, "lib": os.environ.get("SRSGPU_LIB", "in-tree")}
     mod = srsgpu.OfdmPlan(ctx, True, 1, 273, 4096, 0.01, 3.5e9, slots, a.ports)
     dem = srsgpu.OfdmPlan(ctx, False, 1, 273, 4096, 1.0 / 4096, 3.5e9, slots, a.ports)

@@ -477,6 +477,26 @@ int srsgpu_ofdm_jobs_execute(const srsgpu_ofdm_plan* plan,
                              void*                   d_out,
                              void*                   stream);
 
+/** An OFDM job with absolute device addresses: the grid row (12 * bw_rb uint32 bf16 pairs) and the first sample of
+ *  the symbol's cyclic prefix, each anywhere device-accessible — HBM, or host memory mapped for the device — so the
+ *  caller's own buffers (a resource grid's rows, a radio buffer) are read or written in place. */
+typedef struct {
+  uint64_t grid;
+  uint64_t samples;
+  uint32_t cp_len;
+  float    coef_re;
+  float    coef_im;
+  uint32_t reserved;
+} srsgpu_ofdm_direct_job;
+
+/** srsgpu_ofdm_jobs_execute over direct-address jobs (same launch parameters, same restrictions): the lower PHY's
+ *  sector group demodulates straight into the rows of an uplink grid that its owner has mapped, instead of into a
+ *  staging entry copied into the grid afterwards (puxch_processor_impl.cpp:78, the grid write per symbol). */
+int srsgpu_ofdm_jobs_execute_direct(const srsgpu_ofdm_plan*       plan,
+                                    const srsgpu_ofdm_direct_job* d_jobs,
+                                    uint32_t                      nof_jobs,
+                                    void*                         stream);
+
 /** uint32 words of the plan's grids (grids x ports x symbols x 12 * bw_rb). */
 uint64_t srsgpu_ofdm_plan_nof_grid_words(const srsgpu_ofdm_plan* plan);
 

@@ -9,6 +9,8 @@
 #include <algorithm>
 #include <cstring>
 #include <list>
+#include <map>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -225,6 +227,69 @@ public:
 
 private:
   hipStream_t s = nullptr;
+};
+
+/// Host blocks page-locked and mapped for the devices (hipHostRegister), shared by the components that hand them to
+/// kernels in place. The PUSCH slot batch registers its uplink processor's resource grid (the reference's
+/// resource_grid_impl tensor, one [port][symbol][subcarrier] block) and reads it in place; the lower PHY's sector group
+/// finds the grid here and demodulates straight into its rows. The registering component unregisters the block before
+/// its memory goes away.
+class host_blocks
+{
+public:
+  /// Registers [base, base + bytes) (the caller's device is current); the device address, or nullptr on failure.
+  static const void* add(const void* base, size_t bytes)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    void*                       d = nullptr;
+    if (hipHostRegister(const_cast<void*>(base), bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    if (hipHostGetDevicePointer(&d, const_cast<void*>(base), 0) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipHostUnregister(const_cast<void*>(base));
+      return nullptr;
+    }
+    r.blocks[reinterpret_cast<uintptr_t>(base)] = {bytes, reinterpret_cast<uintptr_t>(d)};
+    return d;
+  }
+
+  static void remove(const void* base)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    if (r.blocks.erase(reinterpret_cast<uintptr_t>(base)) != 0) {
+      (void)hipHostUnregister(const_cast<void*>(base));
+    }
+  }
+
+  /// The device address of p when [p, p + bytes) lies inside a registered block, else nullptr.
+  static void* find(const void* p, size_t bytes)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    const auto                  a  = reinterpret_cast<uintptr_t>(p);
+    auto                        it = r.blocks.upper_bound(a);
+    if (it == r.blocks.begin()) {
+      return nullptr;
+    }
+    --it;
+    if (a + bytes > it->first + it->second.first) {
+      return nullptr;
+    }
+    return reinterpret_cast<void*>(it->second.second + (a - it->first));
+  }
+
+private:
+  static host_blocks& get()
+  {
+    static host_blocks r;
+    return r;
+  }
+  std::mutex                                                 mtx;
+  std::map<uintptr_t, std::pair<size_t, uintptr_t>>          blocks;  ///< base -> (bytes, device address)
 };
 
 } // namespace gpu

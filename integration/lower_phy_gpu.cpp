@@ -243,8 +243,10 @@ public:
       sc.templates[pos].resize(n);
       gpu::srsgpu_check(srsgpu_ofdm_plan_get_jobs(plans[pos], sc.templates[pos].data(), n, &n), who);
     }
-    sc.entries = std::vector<entry>(depth);
-    sc.head    = 0;
+    sc.entries   = std::vector<entry>(depth);
+    sc.head      = 0;
+    sc.row_words = static_cast<uint32_t>(srsgpu_ofdm_plan_nof_grid_words(plans[0]) /
+                                         std::max<size_t>(sc.templates[0].size(), 1));  // one job per grid row
     return k;
   }
 
@@ -273,16 +275,28 @@ public:
 
   uint8_t*       input(int sector, int e) { return in_all.host(entry_index(sector, e) * in_max); }
   const uint8_t* output(int sector, int e) { return out_all.host(entry_index(sector, e) * out_max); }
+  /// Whether the entry's rows went to the direct destination given at submit (not to its staging output).
+  bool           direct(int sector, int e) const { return sectors[sector].entries[e].direct; }
 
-  /// The entry's input for position `pos` is in place.
-  void submit(int sector, int e, unsigned pos)
+  /// Where a demodulation entry's grid rows go instead of its staging output: the device address of port 0's row and
+  /// the distance between ports' rows (a mapped uplink resource grid, gpu::host_blocks).
+  struct direct_rows {
+    uint8_t* row0        = nullptr;
+    size_t   port_stride = 0;
+  };
+
+  /// The entry's input for position `pos` is in place; rows: its demodulated rows' destination (default: the entry's
+  /// staging output).
+  void submit(int sector, int e, unsigned pos) { submit(sector, e, pos, direct_rows()); }
+  void submit(int sector, int e, unsigned pos, direct_rows rows)
   {
     std::vector<pending_entry> batch;
     {
       std::lock_guard<std::mutex> lock(mtx);
       const auto now = clock::now();
       sectors[sector].last_submit = now;
-      queue.push_back({sector, e, pos, now});
+      sectors[sector].entries[e].direct = rows.row0 != nullptr && !inverse;
+      queue.push_back({sector, e, pos, now, rows});
       if (queue.size() == 1) {
         dispatch_cv.notify_one();  // a window to watch
       }
@@ -331,14 +345,16 @@ private:
   struct entry {
     std::atomic<bool> busy     = false;  ///< acquired and not yet released
     std::atomic<bool> launched = false;
-    unsigned          batch    = 0;  ///< batch ring index of its launch
-    uint32_t          seq      = 0;  ///< that launch's sequence number
+    unsigned          batch    = 0;      ///< batch ring index of its launch
+    uint32_t          seq      = 0;      ///< that launch's sequence number
+    bool              direct   = false;  ///< rows written to the submit's direct destination
   };
   struct sector_state {
     bool                                      used = false;
     std::vector<std::vector<srsgpu_ofdm_job>> templates;  ///< per position: the plan's jobs
     std::vector<entry>                        entries;
-    uint64_t                                  head = 0;
+    uint64_t                                  head      = 0;
+    uint32_t                                  row_words = 1;  ///< uint32 words of a grid row (12 * bw_rb)
     clock::time_point                         last_submit;
   };
   struct pending_entry {
@@ -346,6 +362,7 @@ private:
     int               e;
     unsigned          pos;
     clock::time_point at;
+    direct_rows       rows;
   };
   static constexpr unsigned NOF_BATCHES = 16;
 
@@ -395,7 +412,7 @@ private:
     }
     in_all.reserve(entries * in_max);
     out_all.reserve(entries * out_max);
-    jobs_buf.reserve(NOF_BATCHES * entries * jobs_per_entry * sizeof(srsgpu_ofdm_job));
+    jobs_buf.reserve(NOF_BATCHES * entries * jobs_per_entry * sizeof(srsgpu_ofdm_direct_job));
     flags.reserve(NOF_BATCHES * 64);
     for (unsigned b = 0; b != NOF_BATCHES; ++b) {
       *flags.host<uint32_t>(b * 64) = 0;
@@ -460,26 +477,37 @@ private:
            seq > NOF_BATCHES) {
       std::this_thread::yield();
     }
-    const size_t     stride = static_cast<size_t>(nof_sectors) * depth * jobs_per_entry;
-    srsgpu_ofdm_job* jobs   = jobs_buf.host<srsgpu_ofdm_job>(b * stride * sizeof(srsgpu_ofdm_job));
-    size_t           n      = 0;
+    // Direct-address jobs: every entry's buffers are its staging slices, except the grid rows of a demodulation entry
+    // submitted with a direct destination (the uplink grid itself).
+    const size_t            stride = static_cast<size_t>(nof_sectors) * depth * jobs_per_entry;
+    srsgpu_ofdm_direct_job* jobs   = jobs_buf.host<srsgpu_ofdm_direct_job>(b * stride * sizeof(srsgpu_ofdm_direct_job));
+    size_t                  n      = 0;
     for (const pending_entry& pe : batch) {
-      const size_t in_off  = entry_index(pe.sector, pe.e) * in_max;
-      const size_t out_off = entry_index(pe.sector, pe.e) * out_max;
-      // demodulation: samples in, grid out; modulation: grid in, samples out
-      const uint32_t samples_base = static_cast<uint32_t>((inverse ? out_off : in_off) / sizeof(cf_t));
-      const uint32_t grid_base    = static_cast<uint32_t>((inverse ? in_off : out_off) / sizeof(uint32_t));
-      for (srsgpu_ofdm_job jb : sectors[pe.sector].templates[pe.pos]) {
-        jb.sample_offset += samples_base;
-        jb.grid_offset += grid_base;
-        jobs[n++] = jb;
+      uint8_t* in_dev   = in_all.dev<uint8_t>(entry_index(pe.sector, pe.e) * in_max);
+      uint8_t* out_dev  = out_all.dev<uint8_t>(entry_index(pe.sector, pe.e) * out_max);
+      uint8_t* grid_dev = inverse ? in_dev : out_dev;
+      uint8_t* samp_dev = inverse ? out_dev : in_dev;
+      for (const srsgpu_ofdm_job& jb : sectors[pe.sector].templates[pe.pos]) {
+        srsgpu_ofdm_direct_job& d = jobs[n++];
+        d.grid                    = reinterpret_cast<uint64_t>(grid_dev + static_cast<size_t>(jb.grid_offset) * 4);
+        if (!inverse && pe.rows.row0 != nullptr) {
+          // the templates' rows are [port][symbol - first] of one symbol: row = port
+          d.grid = reinterpret_cast<uint64_t>(pe.rows.row0 + (jb.grid_offset / sectors[pe.sector].row_words) * pe.rows.port_stride);
+        }
+        d.samples  = reinterpret_cast<uint64_t>(samp_dev + static_cast<size_t>(jb.sample_offset) * sizeof(cf_t));
+        d.cp_len   = jb.cp_len;
+        d.coef_re  = jb.coef_re;
+        d.coef_im  = jb.coef_im;
+        d.reserved = 0;
       }
     }
     gpu::device_scope dev(ctx, who);
     hipStream_t       hs = streams[b % streams.size()]->get();
-    gpu::srsgpu_check(srsgpu_ofdm_jobs_execute(launcher, jobs_buf.dev<srsgpu_ofdm_job>(b * stride * sizeof(srsgpu_ofdm_job)),
-                                               static_cast<uint32_t>(n), in_all.dev(), out_all.dev(), hs),
-                      who);
+    gpu::srsgpu_check(
+        srsgpu_ofdm_jobs_execute_direct(
+            launcher, jobs_buf.dev<srsgpu_ofdm_direct_job>(b * stride * sizeof(srsgpu_ofdm_direct_job)),
+            static_cast<uint32_t>(n), hs),
+        who);
     gpu::hip_check(hipStreamWriteValue32(hs, flags.dev<uint32_t>(b * 64), seq, 0), who, "completion word");
     for (const pending_entry& pe : batch) {
       entry& en = sectors[pe.sector].entries[pe.e];
@@ -998,6 +1026,7 @@ private:
     if (context.slot != current_slot) {
       drain(0);  // a slot left before its last symbol: what was demodulated is still delivered
       current_grid.release();
+      grid_dev = nullptr;
       current_slot = context.slot;
       auto r       = requests.exchange({context.slot, shared_resource_grid()});
       if (!r.payload) {
@@ -1009,6 +1038,7 @@ private:
         notifier->on_puxch_request_late(late);
       } else {
         current_grid = std::move(r.payload);
+        find_grid_rows();
       }
     }
     const unsigned l = context.nof_symbols;
@@ -1026,11 +1056,16 @@ private:
         srsran_assert(in.size() == n, "The input buffer size ({}) does not match the symbol size ({}).", in.size(), n);
         std::memcpy(dst + static_cast<size_t>(p) * n * sizeof(cf_t), in.data(), n * sizeof(cf_t));
       }
-      group->submit(sector, e, s);
+      ofdm_batcher::direct_rows rows;
+      if (grid_dev != nullptr) {
+        rows = {grid_dev + static_cast<size_t>(l) * nsc * sizeof(uint32_t), grid_port_stride};
+      }
+      group->submit(sector, e, s, rows);
       pending.push_back({l, context, e});
       if (l == geo.nsymb - 1) {
         drain(0);
         current_grid.release();
+        grid_dev = nullptr;
       } else {
         drain(max_symbols_in_flight);
       }
@@ -1060,6 +1095,7 @@ private:
     if (l == geo.nsymb - 1) {
       drain(0);
       current_grid.release();
+      grid_dev = nullptr;
     } else {
       drain(max_symbols_in_flight);
     }
@@ -1103,11 +1139,21 @@ private:
         rows = st.out.host();
       }
       resource_grid_writer& writer = current_grid.get().get_writer();
-      for (unsigned p = 0; p != nof_ports; ++p) {
-        writer.put(p, ps.symbol, 0, 1,
-                   span<const cbf16_t>(reinterpret_cast<const cbf16_t*>(rows + static_cast<size_t>(p) * nsc *
-                                                                                    sizeof(uint32_t)),
-                                       nsc));
+      if (ps.entry >= 0 && group->direct(sector, ps.entry)) {
+        // Demodulated straight into the grid's rows: only the ports' non-empty marks remain (a put of each row's first
+        // element onto itself, resource_grid_writer_impl.cpp clear_empty).
+        const resource_grid_reader& reader = current_grid.get().get_reader();
+        for (unsigned p = 0; p != nof_ports; ++p) {
+          const cbf16_t v = reader.get_view(p, ps.symbol)[0];
+          writer.put(p, ps.symbol, 0, 1, span<const cbf16_t>(&v, 1));
+        }
+      } else {
+        for (unsigned p = 0; p != nof_ports; ++p) {
+          writer.put(p, ps.symbol, 0, 1,
+                     span<const cbf16_t>(reinterpret_cast<const cbf16_t*>(rows + static_cast<size_t>(p) * nsc *
+                                                                                      sizeof(uint32_t)),
+                                         nsc));
+        }
       }
       if (ps.entry >= 0) {
         group->release(sector, ps.entry);
@@ -1122,6 +1168,33 @@ private:
     lower_phy_rx_symbol_context context;
     int                         entry;  ///< the group staging entry holding the result, -1: this processor's own stage
   };
+
+  /// The current grid's rows in device-mapped host memory (gpu::host_blocks: mapped by the grid's owner, the GPU
+  /// uplink processor's PUSCH slot batch), for the sector group to demodulate into directly; nullptr: the rows are
+  /// staged and copied into the grid (drain). Needs the reference grid's layout: one [port][symbol][subcarrier] block.
+  void find_grid_rows()
+  {
+    grid_dev = nullptr;
+    if (sector < 0 || !current_grid) {
+      return;
+    }
+    const resource_grid_reader& r = current_grid.get().get_reader();
+    if (r.get_nof_ports() < nof_ports || r.get_nof_subc() != nsc || r.get_nof_symbols() < geo.nsymb) {
+      return;
+    }
+    const size_t row   = static_cast<size_t>(nsc) * sizeof(uint32_t);
+    const size_t nsymb = r.get_nof_symbols();
+    const auto*  base  = reinterpret_cast<const uint8_t*>(r.get_view(0, 0).data());
+    for (unsigned p = 0; p != nof_ports; ++p) {
+      for (unsigned l = 0; l != geo.nsymb; ++l) {
+        if (reinterpret_cast<const uint8_t*>(r.get_view(p, l).data()) != base + (p * nsymb + l) * row) {
+          return;
+        }
+      }
+    }
+    grid_dev         = static_cast<uint8_t*>(gpu::host_blocks::find(base, nof_ports * nsymb * row));
+    grid_port_stride = nsymb * row;
+  }
 
   std::shared_ptr<lower_phy_sector_group>    group_owner;
   ofdm_batcher*                              group  = nullptr;
@@ -1141,6 +1214,8 @@ private:
   puxch_processor_notifier*                  notifier = nullptr;
   slot_point                                 current_slot;
   shared_resource_grid                       current_grid;
+  uint8_t*                                   grid_dev         = nullptr;  ///< find_grid_rows
+  size_t                                     grid_port_stride = 0;
   request_ring<shared_resource_grid>         requests;
 };
 

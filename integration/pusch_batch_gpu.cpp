@@ -102,6 +102,11 @@ std::shared_ptr<pusch_harq_arena> create_pusch_harq_arena(int device, unsigned m
 
 namespace {
 
+/// Process-wide grid transfer counts of the multi-device UL batches (get_pusch_multi_transfer_counters).
+struct {
+  std::atomic<uint64_t> host_uploads{0}, shard_copies{0}, shard_bytes{0};
+} multi_transfers;
+
 /// One registered PUSCH transmission and where its results are in its launch.
 struct pusch_entry {
   pusch_processor::pdu_t           pdu;
@@ -625,6 +630,15 @@ public:
                    std::shared_ptr<pusch_gpu_service>   service_);
   ~pusch_slot_batch();
 
+  /// Unmaps the uplink processor's grid storage (grid_in_place) once every launch is done; the owner calls it before
+  /// the grid goes away.
+  void release_host_grid();
+
+  /// The device address of the grid's rows of ports 0..P-1 when they are one [port][symbol][subcarrier] block in
+  /// host memory (the reference's resource_grid_impl tensor), mapped for the launch's copy kernel to read in place:
+  /// no per-slot memcpy into the batch's buffer. nullptr: another layout (the rows are copied).
+  const void* grid_in_place(const resource_grid_reader& grid, unsigned P, size_t row);
+
   void add(pusch_entry&& e)
   {
     std::lock_guard<std::mutex> lock(pending_mtx);
@@ -678,6 +692,11 @@ private:
   std::unique_ptr<pusch_processor>     fallback;
   staged_buffer                        grid_buf;  ///< Pinned copy of the rx grid for the shards' DMA uploads.
   mapped_buffer                        grid_map{"pusch_slot_batch grid"};  ///< The rx grid, read in place by the launch
+  /// The uplink processor's own grid storage, page-locked and mapped once (grid_in_place): base, bytes, device address.
+  const uint8_t*                       host_grid      = nullptr;
+  size_t                               host_grid_size = 0;
+  const void*                          host_grid_dev  = nullptr;
+  bool                                 host_grid_off  = false;  ///< registration failed once: copy from now on
   unsigned                             batch_id   = 0;
   int                                  grid_slot  = -1;
   unsigned                             grid_P     = 0;
@@ -704,10 +723,22 @@ private:
     size_t                            grid_cap = 0;
   };
   void                                    run_multi(std::unique_ptr<pusch_job> job);
+  void                                    multi_complete_loop();
   std::vector<shard_device>               shards;
   std::shared_ptr<pusch_result_transport> transport;
   std::unique_ptr<owned_stream>           root_stream;
   staged_buffer                           gathered{"pusch_slot_batch gather"};
+  mapped_buffer                           shard_spans{"pusch_slot_batch shard spans"};  ///< grid copies per shard
+  /// The slot in flight (one per batch: run waits for the previous): its shards' jobs and their result offsets in
+  /// the gathered image, replayed by the completion thread once root_done has passed.
+  std::vector<std::vector<std::unique_ptr<pusch_job>>> multi_jobs;
+  std::vector<std::pair<size_t, size_t>>               multi_offsets;
+  hipEvent_t                                           root_done = nullptr;
+  std::thread                                          multi_completion;
+  std::mutex                                           multi_mtx;
+  std::condition_variable                              multi_cv;
+  bool                                                 multi_pending = false;
+  bool                                                 multi_stop    = false;
 };
 
 class pusch_gpu_service
@@ -1666,9 +1697,6 @@ pusch_slot_batch::pusch_slot_batch(const pusch_batch_configuration&     cfg_,
   device_scope dev(ctx, WHO);
   batch_id = service->new_batch_id();
   if (!cfg.devices.empty()) {
-    if (cfg.asynchronous) {
-      throw std::invalid_argument(std::string(WHO) + ": the multi-GPU batch completes synchronously");
-    }
     if (cfg.devices.front() != srsgpu_context_device(ctx)) {
       throw std::invalid_argument(std::string(WHO) + ": the root device (devices[0]) must hold the HARQ arena");
     }
@@ -1684,16 +1712,33 @@ pusch_slot_batch::pusch_slot_batch(const pusch_batch_configuration&     cfg_,
       sh.launcher = std::make_unique<pusch_launcher>(sh.ctx.get());
       sh.upload   = std::make_unique<owned_stream>(sh.ctx.get(), WHO);
       hip_check(hipEventCreateWithFlags(&sh.uploaded, hipEventDisableTiming), WHO, "event");
+      if (sh.device != cfg.devices.front()) {
+        // The shard's grid rows are copied from the root's grid by a kernel on the shard (peer reads over xGMI).
+        const hipError_t pe = hipDeviceEnablePeerAccess(cfg.devices.front(), 0);
+        if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) {
+          throw std::runtime_error(std::string(WHO) + ": no peer access from device " + std::to_string(sh.device) +
+                                   " to the root device");
+        }
+        (void)hipGetLastError();
+      }
       shards.push_back(std::move(sh));
     }
+    hip_check(hipEventCreateWithFlags(&root_done, hipEventDisableTiming), WHO, "event");
+    multi_completion = std::thread([this]() { multi_complete_loop(); });
   }
 }
 
 pusch_slot_batch::~pusch_slot_batch()
 {
-  {
-    std::unique_lock<std::mutex> lock(done_mtx);
-    done_cv.wait(lock, [&] { return outstanding == 0; });
+  release_host_grid();  // waits for every slot in flight
+  if (multi_completion.joinable()) {
+    {
+      std::lock_guard<std::mutex> lock(multi_mtx);
+      multi_stop = true;
+    }
+    multi_cv.notify_all();
+    multi_completion.join();
+    (void)hipEventDestroy(root_done);
   }
   if (grid_slot >= 0) {
     service->release_grid(grid_P, grid_prb, static_cast<unsigned>(grid_slot));
@@ -1704,6 +1749,59 @@ pusch_slot_batch::~pusch_slot_batch()
     (void)hipEventDestroy(sh.uploaded);
     (void)hipFree(sh.d_grid);
   }
+}
+
+void pusch_slot_batch::release_host_grid()
+{
+  {
+    std::unique_lock<std::mutex> lock(done_mtx);
+    done_cv.wait(lock, [&] { return outstanding == 0; });
+  }
+  std::lock_guard<std::mutex> lock(run_mtx);
+  if (host_grid != nullptr) {
+    device_scope dev(ctx, WHO);
+    host_blocks::remove(host_grid);
+    host_grid     = nullptr;
+    host_grid_dev = nullptr;
+  }
+}
+
+const void* pusch_slot_batch::grid_in_place(const resource_grid_reader& grid, unsigned P, size_t row)
+{
+  if (host_grid_off) {
+    return nullptr;
+  }
+  const auto* base = reinterpret_cast<const uint8_t*>(grid.get_view(0, 0).data());
+  for (unsigned p = 0; p != P; ++p) {
+    for (unsigned l = 0; l != 14; ++l) {
+      if (reinterpret_cast<const uint8_t*>(grid.get_view(p, l).data()) != base + (p * 14 + l) * row) {
+        return nullptr;
+      }
+    }
+  }
+  const size_t bytes = static_cast<size_t>(P) * 14 * row;
+  if (host_grid == nullptr || host_grid != base || host_grid_size < bytes) {
+    if (host_grid == nullptr) {
+      if (void* d = host_blocks::find(base, bytes)) {
+        return d;  // mapped by another component (which unmaps it)
+      }
+    }
+    device_scope dev(ctx, WHO);
+    if (host_grid != nullptr) {
+      host_blocks::remove(host_grid);
+      host_grid     = nullptr;
+      host_grid_dev = nullptr;
+    }
+    const void* d = host_blocks::add(base, bytes);
+    if (d == nullptr) {
+      host_grid_off = true;
+      return nullptr;
+    }
+    host_grid      = base;
+    host_grid_size = bytes;
+    host_grid_dev  = d;
+  }
+  return host_grid_dev;
 }
 
 replay_processor& pusch_slot_batch::replay_for_this_thread()
@@ -2063,11 +2161,16 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
   // The rx grid (every symbol of ports 0..P-1, [port][symbol][subcarrier]) into mapped host memory; the launch copies
   // it into the batch's HBM grid slot (srsgpu_copy_spans, with the other slots' grids: zero-copy reads instead of a DMA
   // copy per slot, which ran the service at the DMA engines' ~29 GB/s, profiles/r5_grid_span_copy_ab.txt).
-  grid_map.reserve(gbytes);
-  for (unsigned p = 0; p != P; ++p) {
-    for (unsigned l = 0; l != 14; ++l) {
-      std::memcpy(grid_map.host((p * 14 + l) * row), grid.get_view(p, l).data(), row);
+  // The uplink processor's grid read in place when its storage is one block; otherwise a copy.
+  const void* grid_src = grid_in_place(grid, P, row);
+  if (grid_src == nullptr) {
+    grid_map.reserve(gbytes);
+    for (unsigned p = 0; p != P; ++p) {
+      for (unsigned l = 0; l != 14; ++l) {
+        std::memcpy(grid_map.host((p * 14 + l) * row), grid.get_view(p, l).data(), row);
+      }
     }
+    grid_src = grid_map.dev();
   }
 
   job->batch     = this;
@@ -2078,7 +2181,7 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
   job->P         = P;
   job->grid_prb  = grid_prb;
   job->uploaded   = nullptr;
-  job->grid_src   = grid_map.dev();
+  job->grid_src   = grid_src;
   job->grid_dst   = d_grid;
   job->grid_bytes = gbytes;
   build_layout(*job, *arena);
@@ -2106,14 +2209,10 @@ void pusch_slot_batch::run_multi(std::unique_ptr<pusch_job> job)
   const size_t   row      = static_cast<size_t>(grid_prb) * NRE * sizeof(uint32_t);
   const size_t   gbytes   = static_cast<size_t>(P) * 14 * row;
   const resource_grid_reader& grid = *job->entries.front().grid;
-  grid_buf.reserve(gbytes);
-  for (unsigned p = 0; p != P; ++p) {
-    for (unsigned l = 0; l != 14; ++l) {
-      std::memcpy(grid_buf.host((p * 14 + l) * row), grid.get_view(p, l).data(), row);
-    }
-  }
-  // UE shards: RNTI mod D (a UE's HARQ soft bits stay on the device that decodes it).
+  // UE shards: RNTI mod D (a UE's HARQ soft bits stay on the device that decodes it); each shard's subcarrier bands
+  // (its UEs' allocations, merged).
   std::vector<std::vector<std::unique_ptr<pusch_job>>> shard_jobs(D);
+  std::vector<std::vector<std::pair<unsigned, unsigned>>> bands(D);
   for (pusch_entry& e : job->entries) {
     const unsigned s = static_cast<unsigned>(e.pdu.rnti) % D;
     if (shard_jobs[s].empty()) {
@@ -2127,17 +2226,48 @@ void pusch_slot_batch::run_multi(std::unique_ptr<pusch_job> job)
       sj->uploaded    = shards[s].uploaded;
       shard_jobs[s].push_back(std::move(sj));
     }
+    const crb_bitmap mask = e.pdu.freq_alloc.get_crb_mask(e.pdu.bwp_start_rb, e.pdu.bwp_size_rb);
+    if (mask.any()) {
+      bands[s].emplace_back(static_cast<unsigned>(mask.find_lowest()) * NRE,
+                            (static_cast<unsigned>(mask.find_highest()) + 1) * NRE);
+    }
     shard_jobs[s].front()->entries.push_back(std::move(e));
   }
-  // Each shard: its grid copy, its layout and launch (results stay in its HBM).
-  std::vector<pusch_result_transport::part> parts;
-  std::vector<std::pair<size_t, size_t>>    offsets(D);  // (results, messages) in the gathered image
-  size_t                                    total = 0;
-  auto                                      align = [](size_t x) { return (x + 255) / 256 * 256; };
-  for (unsigned s = 0; s != D; ++s) {
-    if (shard_jobs[s].empty()) {
-      continue;
+  for (auto& b : bands) {
+    std::sort(b.begin(), b.end());
+    std::vector<std::pair<unsigned, unsigned>> merged;
+    for (const auto& r : b) {
+      if (!merged.empty() && r.first <= merged.back().second) {
+        merged.back().second = std::max(merged.back().second, r.second);
+      } else {
+        merged.push_back(r);
+      }
     }
+    b = std::move(merged);
+  }
+  {
+    std::lock_guard<std::mutex> lock(done_mtx);
+    ++outstanding;
+  }
+  // The grid goes to the root device once (its in-place mapped image or the batch's copy, read by a copy kernel);
+  // every other shard receives only its bands' subcarriers of every port and symbol from the root's HBM copy.
+  const void* src = grid_in_place(grid, P, row);
+  if (src == nullptr) {
+    grid_map.reserve(gbytes);
+    for (unsigned p = 0; p != P; ++p) {
+      for (unsigned l = 0; l != 14; ++l) {
+        std::memcpy(grid_map.host((p * 14 + l) * row), grid.get_view(p, l).data(), row);
+      }
+    }
+    src = grid_map.dev();
+  }
+  size_t nspans = 1;
+  for (unsigned s = 1; s != D; ++s) {
+    nspans += shard_jobs[s].empty() ? 0 : bands[s].size() * P * 14;
+  }
+  shard_spans.reserve(nspans * sizeof(srsgpu_copy_span));
+  auto* spans = shard_spans.host<srsgpu_copy_span>();
+  for (unsigned s = 0; s != D; ++s) {
     shard_device& sh = shards[s];
     device_scope  sdev(sh.ctx.get(), WHO);
     if (sh.grid_cap < gbytes) {
@@ -2148,9 +2278,54 @@ void pusch_slot_batch::run_multi(std::unique_ptr<pusch_job> job)
       hip_check(hipMalloc(reinterpret_cast<void**>(&sh.d_grid), gbytes), WHO, "shard grid");
       sh.grid_cap = gbytes;
     }
-    hip_check(hipMemcpyAsync(sh.d_grid, grid_buf.host(), gbytes, hipMemcpyHostToDevice, sh.upload->get()), WHO,
-              "shard grid upload");
+  }
+  {
+    shard_device& root = shards[0];
+    device_scope  rdev(root.ctx.get(), WHO);
+    spans[0] = {src, root.d_grid, gbytes};
+    srsgpu_check(srsgpu_copy_spans(shard_spans.dev<srsgpu_copy_span>(), 1, gbytes, root.upload->get()), WHO);
+    hip_check(hipEventRecord(root.uploaded, root.upload->get()), WHO, "event");
+    multi_transfers.host_uploads.fetch_add(1, std::memory_order_relaxed);
+  }
+  size_t next = 1;
+  for (unsigned s = 1; s != D; ++s) {
+    if (shard_jobs[s].empty()) {
+      continue;
+    }
+    shard_device& sh = shards[s];
+    device_scope  sdev(sh.ctx.get(), WHO);
+    const size_t  first = next;
+    uint64_t      most  = 0;
+    for (const auto& b : bands[s]) {
+      const size_t off = static_cast<size_t>(b.first) * sizeof(uint32_t);
+      const size_t len = static_cast<size_t>(b.second - b.first) * sizeof(uint32_t);
+      for (unsigned r = 0; r != P * 14; ++r) {
+        spans[next++] = {reinterpret_cast<const uint8_t*>(shards[0].d_grid) + r * row + off,
+                         reinterpret_cast<uint8_t*>(sh.d_grid) + r * row + off, len};
+        multi_transfers.shard_bytes.fetch_add(len, std::memory_order_relaxed);
+      }
+      most = std::max<uint64_t>(most, len);
+    }
+    hip_check(hipStreamWaitEvent(sh.upload->get(), shards[0].uploaded, 0), WHO, "wait for the root grid");
+    if (next > first) {
+      srsgpu_check(srsgpu_copy_spans(shard_spans.dev<srsgpu_copy_span>(first * sizeof(srsgpu_copy_span)),
+                                     static_cast<uint32_t>(next - first), most, sh.upload->get()),
+                   WHO);
+      multi_transfers.shard_copies.fetch_add(1, std::memory_order_relaxed);
+    }
     hip_check(hipEventRecord(sh.uploaded, sh.upload->get()), WHO, "event");
+  }
+  // Each shard's layout and launch (results stay in its HBM), then the gather to the root and one download.
+  std::vector<pusch_result_transport::part> parts;
+  std::vector<std::pair<size_t, size_t>>    offsets(D);  // (results, messages) in the gathered image
+  size_t                                    total = 0;
+  auto                                      align = [](size_t x) { return (x + 255) / 256 * 256; };
+  for (unsigned s = 0; s != D; ++s) {
+    if (shard_jobs[s].empty()) {
+      continue;
+    }
+    shard_device& sh = shards[s];
+    device_scope  sdev(sh.ctx.get(), WHO);
     build_layout(*shard_jobs[s].front(), *sh.arena);
     sh.launcher->launch(shard_jobs[s], sh.d_grid, false);
     offsets[s] = {total, align(total + sh.launcher->results_bytes())};
@@ -2160,20 +2335,67 @@ void pusch_slot_batch::run_multi(std::unique_ptr<pusch_job> job)
                      offsets[s].second});
     total = align(offsets[s].second + sh.launcher->msgs_bytes());
   }
-  // Gather to the root, one download, the replay.
   device_scope root(ctx, WHO);
   gathered.reserve(std::max<size_t>(total, 256));
   transport->gather(cfg.devices.front(), root_stream->get(), gathered.dev(), parts);
   gathered.download(0, total, root_stream->get());
-  hip_check(hipStreamSynchronize(root_stream->get()), WHO, "synchronise");
-  for (unsigned s = 0; s != D; ++s) {
-    if (shard_jobs[s].empty()) {
-      continue;
-    }
-    pusch_launcher&    L  = *shards[s].launcher;
-    const launch_plan& lp = L.current();
-    L.replay(shard_jobs[s], gathered.host<uint8_t>(offsets[s].first) - lp.flag_o, gathered.host<uint8_t>(offsets[s].second));
+  hip_check(hipEventRecord(root_done, root_stream->get()), WHO, "event");
+  // The replay (notifications) on the completion thread once the download has landed; a synchronous batch waits.
+  {
+    std::lock_guard<std::mutex> lock(multi_mtx);
+    multi_jobs    = std::move(shard_jobs);
+    multi_offsets = std::move(offsets);
+    multi_pending = true;
   }
+  multi_cv.notify_all();
+  if (!cfg.asynchronous) {
+    std::unique_lock<std::mutex> done_lock(done_mtx);
+    done_cv.wait(done_lock, [&] { return outstanding == 0; });
+  }
+}
+
+void pusch_slot_batch::multi_complete_loop()
+{
+  for (;;) {
+    std::vector<std::vector<std::unique_ptr<pusch_job>>> jobs;
+    std::vector<std::pair<size_t, size_t>>               offsets;
+    {
+      std::unique_lock<std::mutex> lock(multi_mtx);
+      multi_cv.wait(lock, [&] { return multi_pending || multi_stop; });
+      if (!multi_pending) {
+        return;
+      }
+      jobs          = std::move(multi_jobs);
+      offsets       = std::move(multi_offsets);
+      multi_pending = false;
+    }
+    device_scope root(ctx, WHO);
+    try {
+      hip_check(hipEventSynchronize(root_done), WHO, "synchronise");
+      for (size_t s = 0; s != jobs.size(); ++s) {
+        if (jobs[s].empty()) {
+          continue;
+        }
+        pusch_launcher&    L  = *shards[s].launcher;
+        const launch_plan& lp = L.current();
+        L.replay(jobs[s], gathered.host<uint8_t>(offsets[s].first) - lp.flag_o,
+                 gathered.host<uint8_t>(offsets[s].second));
+      }
+    } catch (const std::exception& e) {
+      report_fatal_error("pusch_slot_batch: {}", e.what());
+    }
+    {
+      std::lock_guard<std::mutex> lock(done_mtx);
+      --outstanding;
+    }
+    done_cv.notify_all();
+  }
+}
+
+pusch_multi_transfer_counters get_pusch_multi_transfer_counters()
+{
+  return {multi_transfers.host_uploads.load(), multi_transfers.shard_copies.load(),
+          multi_transfers.shard_bytes.load()};
 }
 
 namespace {
@@ -2363,6 +2585,9 @@ public:
       s.owner = this;
     }
   }
+
+  // The inner processor owns the grid the batch reads in place: unmapped before it goes.
+  ~uplink_processor_batch_gpu() override { batch->release_host_grid(); }
 
   unique_uplink_pdu_slot_repository get_pdu_slot_repository(slot_point slot) override
   {

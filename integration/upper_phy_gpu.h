@@ -115,6 +115,16 @@ public:
   virtual void gather(int root_device, void* root_stream, void* dst, const std::vector<part>& parts) = 0;
 };
 /// Device-to-device copies (hipMemcpyPeerAsync; any device list, devices may repeat).
+/// Grid transfers of the multi-device UL batches, process-wide (row b7): host-to-device grid uploads (one per slot, to
+/// the root device, whatever the number of devices), root-to-shard copy launches and the bytes they moved (each
+/// shard receives only its UEs' subcarrier bands).
+struct pusch_multi_transfer_counters {
+  uint64_t host_uploads = 0;
+  uint64_t shard_copies = 0;
+  uint64_t shard_bytes  = 0;
+};
+pusch_multi_transfer_counters get_pusch_multi_transfer_counters();
+
 std::shared_ptr<pusch_result_transport> create_pusch_copy_transport();
 /// RCCL point-to-point over xGMI: one communicator per listed device in this process (ncclCommInitAll, devices distinct),
 /// every part an ncclSend from its rank to rank 0 inside one group.

@@ -1643,6 +1643,16 @@ void chain_ul_destroy(void* p)
   delete static_cast<ul_harness*>(p);
 }
 
+/// Process-wide grid transfer counts of the multi-device UL batches (gpu::get_pusch_multi_transfer_counters): out[0]
+/// host-to-device grid uploads, out[1] root-to-shard copy launches, out[2] bytes those copies moved.
+void chain_multi_transfer_counters(uint64_t* out)
+{
+  const gpu::pusch_multi_transfer_counters c = gpu::get_pusch_multi_transfer_counters();
+  out[0]                                     = c.host_uploads;
+  out[1]                                     = c.shard_copies;
+  out[2]                                     = c.shard_bytes;
+}
+
 /// One UL slot: the PUSCH PDUs (tb_bytes[i] each) registered in the reference's PDU repository, the received grid
 /// (nof_ports, 14, 12 grid_prb) bf16 pairs written into the processor's grid, then handle_rx_symbol(13). Results in
 /// notification order: ints [rnti, harq, crc_ok, nof_cbs, ldpc_obs, ldpc_min, ldpc_max, harq_ack_status (-1: none),

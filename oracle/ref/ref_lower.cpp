@@ -8,6 +8,7 @@
 //     sectors driven from their own threads: ref_lower_sectors_run).
 // Every variant sees the same requests, grids and samples; the test compares samples, grids, return values and the
 // notifications (late requests, received symbols). Never shipped.
+#include "gpu_staging.h"
 #include "signal_chain_gpu.h"
 
 #include "lib/phy/generic_functions/dft_processor_generic_impl.h"
@@ -57,6 +58,21 @@ public:
     }
   }
   resource_grid& get(unsigned id) override { return *grids[id]; }
+  /// Maps (or unmaps) every grid's storage for the devices (gpu::host_blocks), as a GPU uplink processor's PUSCH slot
+  /// batch does with its grid: the GPU lower PHY then demodulates into the rows directly.
+  void map_grids(bool on)
+  {
+    for (auto& g : grids) {
+      const resource_grid_reader& r    = g->get_reader();
+      const void*                 base = r.get_view(0, 0).data();
+      if (on) {
+        (void)gpu::host_blocks::add(base, static_cast<size_t>(r.get_nof_ports()) * r.get_nof_symbols() *
+                                              r.get_nof_subc() * sizeof(cbf16_t));
+      } else {
+        gpu::host_blocks::remove(base);
+      }
+    }
+  }
   void           notify_release_scope(unsigned /*id*/) override {}
   shared_resource_grid grab(unsigned id)
   {
@@ -582,6 +598,12 @@ int ref_lower_sectors_run(int             variant,
   const long dl_stride   = 2 * std::labs(dl_cap);
   const int  late_stride = nof_dl_events + nof_ul_events + 1;
 
+  // Variant 6: the sector group (variant 3) with the UL grids mapped for the devices, so that the group demodulates
+  // into them directly (srsgpu_ofdm_jobs_execute_direct) instead of staging and copying the rows.
+  const bool mapped_ul = variant == 6;
+  if (mapped_ul) {
+    variant = 3;
+  }
   std::shared_ptr<lower_phy_sector_group> group;
   if (variant == 3) {
     lower_phy_group_configuration gc;
@@ -602,6 +624,9 @@ int ref_lower_sectors_run(int             variant,
     dl_pools.emplace_back(std::make_unique<harness_pool>(nof_grids, nof_ports, sc.nsymb(), sc.nsc()));
     fill_pool(*dl_pools.back(), sc, nof_grids, dl_grids + k * grid_block, dl_port_mask + k * nof_grids);
     ul_pools.emplace_back(std::make_unique<harness_pool>(nof_grids, nof_ports, sc.nsymb(), sc.nsc()));
+    if (mapped_ul) {
+      ul_pools.back()->map_grids(true);
+    }
     dl.push_back(make_pdxch(variant, sc, center_freq_hz[k], group));
     dl.back()->connect(dl_rec[k]);
     ul.push_back(make_puxch(variant, max_in_flight, sc, center_freq_hz[k], group));
@@ -655,6 +680,9 @@ int ref_lower_sectors_run(int             variant,
   dl.clear();
   ul.clear();
   for (int k = 0; k < nof_sectors; ++k) {
+    if (mapped_ul) {
+      ul_pools[k]->map_grids(false);
+    }
     dump_pool(*ul_pools[k], sc, nof_grids, ul_grids_out + k * grid_block);
     nof_rx[k] = static_cast<int>(ul_rec[k].rx.size() / 2);
     std::copy(ul_rec[k].rx.begin(), ul_rec[k].rx.end(), rx_out + static_cast<size_t>(k) * 2 * n_ul_proc);

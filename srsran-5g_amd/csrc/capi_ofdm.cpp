@@ -363,6 +363,26 @@ int srsgpu_ofdm_jobs_execute(const srsgpu_ofdm_plan* plan,
   return SRSGPU_OK;
 }
 
+int srsgpu_ofdm_jobs_execute_direct(const srsgpu_ofdm_plan*       plan,
+                                    const srsgpu_ofdm_direct_job* d_jobs,
+                                    uint32_t                      nof_jobs,
+                                    void*                         stream)
+{
+  if (plan == nullptr || (d_jobs == nullptr && nof_jobs > 0)) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument");
+  }
+  if (ofdm_split_factor(plan->dft_size) != 0) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "job lists do not run the split DFT sizes (%u points)", plan->dft_size);
+  }
+  if (!launch_ofdm_direct(plan->inverse, plan->dft_size, d_jobs, static_cast<int>(nof_jobs), plan->nsc,
+                          plan->inverse ? 0u : plan->window_off, plan->ctx->d_ofdm_twiddles,
+                          static_cast<hipStream_t>(stream))) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "unsupported DFT size %u", plan->dft_size);
+  }
+  HIP_TRY(hipGetLastError());
+  return SRSGPU_OK;
+}
+
 uint64_t srsgpu_ofdm_plan_nof_grid_words(const srsgpu_ofdm_plan* plan)
 {
   return plan == nullptr ? 0 : plan->grid_words;

@@ -390,18 +390,47 @@ __device__ __forceinline__ uint32_t bf16_bits(float v)
   return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
 }
 
-template <int N>
-__global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_modulate_kernel(
-    const ofdm_job* __restrict__ jobs,
-    uint32_t nsc,
-    const float2* __restrict__ tw,
-    const uint32_t* __restrict__ grid,
-    float2* __restrict__ out)
+/// One job of a launch resolved to its buffers: the grid row, the first sample of the symbol's cyclic prefix, the
+/// prefix length and the phase compensation times the scaling.
+struct job_ref {
+  uint32_t* grid;
+  float2*   samples;
+  uint32_t  cp;
+  float2    coef;
+};
+
+/// Jobs as offsets into one grid buffer and one sample buffer (plans and srsgpu_ofdm_jobs_execute).
+struct offset_jobs {
+  const ofdm_job* jobs;
+  uint32_t*       grid;
+  float2*         samples;
+  __device__ __forceinline__ job_ref get(unsigned b) const
+  {
+    const ofdm_job j = jobs[b];
+    return {grid + j.grid_offset, samples + j.sample_offset, j.cp_len, make_float2(j.coef_re, j.coef_im)};
+  }
+};
+
+/// Jobs with absolute device addresses (srsgpu_ofdm_jobs_execute_direct).
+struct direct_jobs {
+  const srsgpu_ofdm_direct_job* jobs;
+  __device__ __forceinline__ job_ref get(unsigned b) const
+  {
+    const srsgpu_ofdm_direct_job j = jobs[b];
+    return {reinterpret_cast<uint32_t*>(j.grid), reinterpret_cast<float2*>(j.samples), j.cp_len,
+            make_float2(j.coef_re, j.coef_im)};
+  }
+};
+
+template <int N, typename JS>
+__global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_modulate_kernel(JS js,
+                                                                                       uint32_t nsc,
+                                                                                       const float2* __restrict__ tw)
 {
   __shared__ float2   lds[N];
-  const ofdm_job      jb   = jobs[blockIdx.x];
+  const job_ref       jb   = js.get(blockIdx.x);
   const int           half = static_cast<int>(nsc / 2);
-  const uint32_t*     row  = grid + jb.grid_offset;
+  const uint32_t*     row  = jb.grid;
   // Bin b < rg/2 carries subcarrier rg/2 + b, bin b >= N - rg/2 subcarrier b - (N - rg/2), the rest are zero.
   auto src = [row, half](int b) {
     int sc = -1;
@@ -416,9 +445,9 @@ __global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_modulat
     const uint32_t u = row[sc];
     return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
   };
-  const float2 coef = make_float2(jb.coef_re, jb.coef_im);
-  float2*      sym  = out + jb.sample_offset;
-  const int    cp   = static_cast<int>(jb.cp_len);
+  const float2 coef = jb.coef;
+  float2*      sym  = jb.samples;
+  const int    cp   = static_cast<int>(jb.cp);
   auto dst = [sym, coef, cp](int n, float2 v) {
     const float2 y = cmul(v, coef);
     sym[cp + n]    = y;
@@ -429,22 +458,19 @@ __global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_modulat
   dft_any<N, +1>(lds, tw, src, dst);
 }
 
-template <int N>
-__global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_demodulate_kernel(
-    const ofdm_job* __restrict__ jobs,
-    uint32_t nsc,
-    uint32_t window_offset,
-    const float2* __restrict__ tw,
-    const float2* __restrict__ in,
-    uint32_t* __restrict__ grid)
+template <int N, typename JS>
+__global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_demodulate_kernel(JS js,
+                                                                                         uint32_t nsc,
+                                                                                         uint32_t window_offset,
+                                                                                         const float2* __restrict__ tw)
 {
   __shared__ float2 lds[N];
-  const ofdm_job    jb   = jobs[blockIdx.x];
+  const job_ref     jb   = js.get(blockIdx.x);
   const int         half = static_cast<int>(nsc / 2);
-  const float2*     x    = in + jb.sample_offset + jb.cp_len - window_offset;
+  const float2*     x    = jb.samples + jb.cp - window_offset;
   auto              src  = [x](int n) { return x[n]; };
-  const float2      coef = make_float2(jb.coef_re, jb.coef_im);
-  uint32_t*         row  = grid + jb.grid_offset;
+  const float2      coef = jb.coef;
+  uint32_t*         row  = jb.grid;
   auto dst = [row, coef, half, tw, window_offset](int b, float2 v) {
     int sc = -1;
     if (b < half) {
@@ -611,26 +637,40 @@ void launch_split(bool            inverse,
   }
 }
 
-template <int N>
-void launch_one(bool            inverse,
-                const ofdm_job* jobs,
-                int             nof_jobs,
-                uint32_t        nsc,
-                uint32_t        window_offset,
-                const float2*   tw,
-                const uint32_t* grid_in,
-                uint32_t*       grid_out,
-                const float2*   samples_in,
-                float2*         samples_out,
-                hipStream_t     stream)
+template <int N, typename JS>
+void launch_one(bool inverse, JS js, int nof_jobs, uint32_t nsc, uint32_t window_offset, const float2* tw,
+                hipStream_t stream)
 {
   constexpr int threads = ofdm_threads<N>();  // every thread takes part in the passes' barriers
   if (inverse) {
-    hipLaunchKernelGGL(ofdm_modulate_kernel<N>, dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0, stream,
-                       jobs, nsc, tw, grid_in, samples_out);
+    hipLaunchKernelGGL((ofdm_modulate_kernel<N, JS>), dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0, stream,
+                       js, nsc, tw);
   } else {
-    hipLaunchKernelGGL(ofdm_demodulate_kernel<N>, dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0,
-                       stream, jobs, nsc, window_offset, tw, samples_in, grid_out);
+    hipLaunchKernelGGL((ofdm_demodulate_kernel<N, JS>), dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0,
+                       stream, js, nsc, window_offset, tw);
+  }
+}
+
+/// Every non-split DFT size: its launch over the job source.
+template <typename JS>
+bool launch_sizes(bool inverse, uint32_t dft_size, JS js, int nof_jobs, uint32_t nsc, uint32_t window_offset,
+                  const float2* tw, hipStream_t stream)
+{
+  switch (dft_size) {
+    case 128: launch_one<128>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 256: launch_one<256>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 512: launch_one<512>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 1024: launch_one<1024>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 2048: launch_one<2048>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 4096: launch_one<4096>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 8192: launch_one<8192>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 384: launch_one<384>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 768: launch_one<768>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 1536: launch_one<1536>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 3072: launch_one<3072>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 4608: launch_one<4608>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    case 6144: launch_one<6144>(inverse, js, nof_jobs, nsc, window_offset, tw, stream); return true;
+    default: return false;
   }
 }
 
@@ -656,21 +696,11 @@ void launch_ofdm(bool            inverse,
   const auto* tw  = reinterpret_cast<const float2*>(d_twiddles);
   const auto* sin = reinterpret_cast<const float2*>(d_samples_in);
   auto*       so  = reinterpret_cast<float2*>(d_samples_out);
-  switch (dft_size) {
-    case 128: launch_one<128>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 256: launch_one<256>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 512: launch_one<512>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 1024: launch_one<1024>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 2048: launch_one<2048>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 4096: launch_one<4096>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 8192: launch_one<8192>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 384: launch_one<384>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 768: launch_one<768>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 1536: launch_one<1536>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 3072: launch_one<3072>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 4608: launch_one<4608>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    case 6144: launch_one<6144>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, stream); break;
-    default: break;
+  // The kernels only read the input buffer of their direction.
+  const offset_jobs js{d_jobs, inverse ? const_cast<uint32_t*>(d_grid_in) : d_grid_out,
+                       inverse ? so : const_cast<float2*>(sin)};
+  if (launch_sizes(inverse, dft_size, js, nof_jobs, nsc, window_offset, tw, stream)) {
+    return;
   }
   auto* sc = reinterpret_cast<float2*>(d_scratch);
   switch (dft_size) {
@@ -683,6 +713,22 @@ void launch_ofdm(bool            inverse,
     case 98304: launch_split<12, 8192>(inverse, d_jobs, nof_jobs, nsc, window_offset, tw, d_grid_in, d_grid_out, sin, so, sc, stream); break;
     default: break;
   }
+}
+
+bool launch_ofdm_direct(bool                          inverse,
+                        uint32_t                      dft_size,
+                        const srsgpu_ofdm_direct_job* d_jobs,
+                        int                           nof_jobs,
+                        uint32_t                      nsc,
+                        uint32_t                      window_offset,
+                        const float*                  d_twiddles,
+                        hipStream_t                   stream)
+{
+  if (nof_jobs <= 0) {
+    return true;
+  }
+  return launch_sizes(inverse, dft_size, direct_jobs{d_jobs}, nof_jobs, nsc, window_offset,
+                      reinterpret_cast<const float2*>(d_twiddles), stream);
 }
 
 } // namespace srsgpu

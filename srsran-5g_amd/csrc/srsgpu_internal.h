@@ -408,6 +408,15 @@ void launch_ofdm(bool            inverse,
                  float*          d_samples_out,
                  float*          d_scratch,
                  hipStream_t     stream);
+/// Direct-address job list (srsgpu_ofdm_jobs_execute_direct); false for a split DFT size (nothing launched).
+bool launch_ofdm_direct(bool                          inverse,
+                        uint32_t                      dft_size,
+                        const srsgpu_ofdm_direct_job* d_jobs,
+                        int                           nof_jobs,
+                        uint32_t                      nsc,
+                        uint32_t                      window_offset,
+                        const float*                  d_twiddles,
+                        hipStream_t                   stream);
 
 /// PUSCH demodulator (pusch_demodulator.hip): per-transmission descriptor. Work items are mod_chunk (8192 LLRs each).
 struct demod_desc {

@@ -402,6 +402,7 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_ofdm_plan_concat.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(P)]
     lib.srsgpu_ofdm_plan_get_jobs.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
     lib.srsgpu_ofdm_jobs_execute.argtypes = [P, P, ctypes.c_uint32, P, P, P]
+    lib.srsgpu_ofdm_jobs_execute_direct.argtypes = [P, P, ctypes.c_uint32, P]
     lib.srsgpu_copy_spans.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64, P]
     lib.srsgpu_ofdm_plan_sample_offset.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     lib.srsgpu_ofdm_plan_sample_offset.restype = ctypes.c_uint64
@@ -435,7 +436,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_modulator_symbols_plan_create", "srsgpu_ofdm_demodulator_symbols_plan_create", "srsgpu_harq_copy",
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
     "srsgpu_ofdm_plan_concat", "srsgpu_ofdm_plan_nof_grid_words", "srsgpu_ofdm_plan_get_jobs",
-    "srsgpu_ofdm_jobs_execute", "srsgpu_copy_spans",
+    "srsgpu_ofdm_jobs_execute", "srsgpu_ofdm_jobs_execute_direct", "srsgpu_copy_spans",
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
     "srsgpu_pusch_demodulator_plan_create_ex", "srsgpu_pusch_demodulator_plan_execute_ex",
@@ -1547,6 +1548,22 @@ class OfdmPlan:
         """srsgpu_ofdm_jobs_execute: a caller-assembled job list with this plan's launch parameters."""
         _check(_lib.srsgpu_ofdm_jobs_execute(self.handle, _dptr(d_jobs), nof_jobs, _dptr(d_in), _dptr(d_out),
                                              _stream_handle(stream)))
+
+    OFDM_DIRECT_JOB = np.dtype([("grid", "<u8"), ("samples", "<u8"), ("cp_len", "<u4"), ("coef_re", "<f4"),
+                                ("coef_im", "<f4"), ("reserved", "<u4")])
+
+    def direct_jobs(self, d_grid, d_samples) -> np.ndarray:
+        """The plan's jobs as srsgpu_ofdm_direct_job (OFDM_DIRECT_JOB) over the given grid and sample buffers."""
+        j = self.jobs()
+        out = np.zeros(len(j), self.OFDM_DIRECT_JOB)
+        out["grid"] = _dptr(d_grid) + 4 * j["grid_offset"].astype(np.uint64)
+        out["samples"] = _dptr(d_samples) + 8 * j["sample_offset"].astype(np.uint64)
+        out["cp_len"], out["coef_re"], out["coef_im"] = j["cp_len"], j["coef_re"], j["coef_im"]
+        return out
+
+    def execute_jobs_direct(self, d_jobs, nof_jobs: int, stream=None):
+        """srsgpu_ofdm_jobs_execute_direct: direct-address jobs with this plan's launch parameters."""
+        _check(_lib.srsgpu_ofdm_jobs_execute_direct(self.handle, _dptr(d_jobs), nof_jobs, _stream_handle(stream)))
 
     def execute(self, d_in, d_out, stream=None):
         f = _lib.srsgpu_ofdm_modulator_plan_execute if self.inverse else _lib.srsgpu_ofdm_demodulator_plan_execute

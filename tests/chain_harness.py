@@ -139,10 +139,17 @@ class UpperPhy:
         L.chain_dl_destroy.argtypes = [_P]
         L.chain_dl_slot.restype = ctypes.c_int
         L.chain_dl_slot.argtypes = [_P, ctypes.c_uint, ctypes.c_int, PP, _P, _P, _P, _P]
+        L.chain_multi_transfer_counters.argtypes = [_P]
         self.P, self.grid_prb = nof_ports, grid_prb
         self.ul = L.chain_ul_create(device, variant, nof_ports, grid_prb, max_iter)
         self.dl = L.chain_dl_create(device, variant, nof_ports, grid_prb)
         assert self.ul and self.dl
+
+    def multi_transfer_counters(self):
+        """Process-wide grid transfers of the multi-device UL batches (chain_multi_transfer_counters)."""
+        out = np.zeros(3, np.uint64)
+        self.lib.chain_multi_transfer_counters(_ptr(out))
+        return dict(zip(("host_uploads", "shard_copies", "shard_bytes"), (int(v) for v in out)))
 
     def close(self):
         if self.ul:

@@ -11,6 +11,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHAIN_SO = os.path.join(ROOT, "oracle", "_ref", "libsrschain.so")
 _P = ctypes.c_void_p
 REF_CPU, REF_ON_GPU_SYMBOLS, GPU_PROCESSOR, GPU_GROUP = 0, 1, 2, 3
+# ref_lower_sectors_run variant 6: the sector group with the UL grids mapped for the device (gpu::host_blocks), as a GPU
+# uplink processor's PUSCH batch maps its grid: the group demodulates into the grids' rows directly.
+GPU_GROUP_MAPPED = 6
 REQUEST, PROCESS = 0, 1
 SENTINEL = np.float32(1e30)
 

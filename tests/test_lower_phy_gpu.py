@@ -18,7 +18,7 @@ overwritten by one 16 slots later (late), a request processed 16 slots late, par
 import numpy as np
 import pytest
 
-from lower_harness import (GPU_GROUP, GPU_PROCESSOR, PROCESS, REF_CPU, REF_ON_GPU_SYMBOLS, REQUEST, SENTINEL, Lower,
+from lower_harness import (GPU_GROUP, GPU_GROUP_MAPPED, GPU_PROCESSOR, PROCESS, REF_CPU, REF_ON_GPU_SYMBOLS, REQUEST, SENTINEL, Lower,
                            symbol_size)
 from ofdm_oracle import bf16_to_complex
 from pusch_demod_cases import bf16
@@ -162,12 +162,16 @@ def test_sectors_on_one_gpu_equal_reference(lower):
 
 @pytest.mark.parametrize("name", ["100MHz_30kHz_4port", "10MHz_15kHz_2port"])
 @pytest.mark.parametrize("in_flight", [0, 3])
-def test_sector_group_equals_reference(lower, name, in_flight):
+@pytest.mark.parametrize("variant", [GPU_GROUP, GPU_GROUP_MAPPED], ids=["staged", "mapped_ul_grids"])
+def test_sector_group_equals_reference(lower, name, in_flight, variant):
     """The sector group (lower_phy_sector_group: the same symbol / slot of every sector in one launch): four sectors
     on their own carrier frequencies and data, driven from their own threads through the edge-case scripts above
     (missing requests, late and overwritten requests, partial slots, a slot left mid-way, empty grids and ports), each
     equal to the reference processor run on that sector; and the group did batch several sectors' work per launch
-    (the sectors are paced at the symbol rate, as a radio unit drives them)."""
+    (the sectors are paced at the symbol rate, as a radio unit drives them). mapped_ul_grids: the UL grids are
+    mapped for the device (as the GPU uplink processor's PUSCH batch maps its grid), so the group demodulates into
+    their rows directly instead of staging them (srsgpu_ofdm_jobs_execute_direct); the grids, notifications and
+    empty-port marks must be the same."""
     cfg = CONFIGS[name]
     nsymb = 12 if cfg["extended"] else 14
     S, G = 4, 8
@@ -179,7 +183,7 @@ def test_sector_group_equals_reference(lower, name, in_flight):
     x = np.stack([ul_samples(rng, cfg, ev_ul) for _ in range(S)])
     ref = lower.sectors(REF_CPU, cfg, freqs, grids, masks, ev_dl, ev_ul, x)
     # paced at the radio's symbol rate, as a radio unit drives its sectors: their symbols meet in the group's rounds
-    got = lower.sectors(GPU_GROUP, cfg, freqs, grids, masks, ev_dl, ev_ul, x, max_in_flight=in_flight, paced=True)
+    got = lower.sectors(variant, cfg, freqs, grids, masks, ev_dl, ev_ul, x, max_in_flight=in_flight, paced=True)
     for k in range(S):
         (rs, rf), (gs, gf) = ref["dl"][k], got["dl"][k]
         touched = rs.real != SENTINEL

@@ -190,3 +190,41 @@ def test_ofdm_job_list_equals_plans(ctx, inverse):
     split = srsgpu.OfdmPlan(ctx, inverse, 1, 273, 12288, 1.0, 3.5e9, [0], 1, symbols=(0, 1))
     with pytest.raises(srsgpu.SrsGpuError):
         split.execute_jobs(d_jobs, 1, src, out)
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_ofdm_direct_jobs_equal_plans(ctx, inverse):
+    """srsgpu_ofdm_jobs_execute_direct (the sector group writing straight into a mapped uplink grid): three sectors'
+    jobs with absolute addresses into three separate allocations per side, in any order, give bit for bit what each
+    plan gives on its own buffers; a split DFT size is refused."""
+    import torch
+    import srsgpu
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(41)
+    P = 2
+    members = [srsgpu.OfdmPlan(ctx, inverse, 1, 106, 2048, sc, fc, [slot], P, window_offset=0 if inverse else 40,
+                               symbols=(l, 1))
+               for sc, fc, slot, l in ((0.5, 3.5e9, 0, 0), (0.25, 3.6e9, 1, 7), (1.0, 1.8e9, 1, 13))]
+    grids, samples, jobs = [], [], []
+    for m in members:
+        g = torch.from_numpy(rng.integers(0, 1 << 14, 2 * m.grid_words).astype(np.uint16).view(np.int32).copy())
+        x = torch.from_numpy((rng.normal(size=2 * m.nof_samples) * 0.1).astype(np.float32))
+        grids.append((g if inverse else torch.zeros(m.grid_words, dtype=torch.int32)).to(dev))
+        samples.append((torch.zeros(2 * m.nof_samples, dtype=torch.float32) if inverse else x).to(dev))
+        jobs.append(m.direct_jobs(grids[-1], samples[-1]))
+    jobs = np.concatenate(jobs)[::-1].copy()
+    d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
+    members[0].execute_jobs_direct(d_jobs, len(jobs))
+    torch.cuda.synchronize()
+    for i, m in enumerate(members):
+        if inverse:
+            o = torch.zeros(2 * m.nof_samples, dtype=torch.float32, device=dev)
+            m.execute(grids[i], o)
+            assert torch.equal(o, samples[i]), i
+        else:
+            o = torch.zeros(m.grid_words, dtype=torch.int32, device=dev)
+            m.execute(samples[i], o)
+            assert torch.equal(o, grids[i]), i
+    split = srsgpu.OfdmPlan(ctx, inverse, 1, 273, 12288, 1.0, 3.5e9, [0], 1, symbols=(0, 1))
+    with pytest.raises(srsgpu.SrsGpuError):
+        split.execute_jobs_direct(d_jobs, 1)

@@ -30,18 +30,21 @@ T_C = 1.0 / (480000 * 4096)
 P = 4
 
 
-@pytest.fixture(scope="module", params=["sync", "async", "multi3_copy", "multi1_rccl"])
+@pytest.fixture(scope="module", params=["sync", "async", "multi3_copy", "multi3_copy_async", "multi1_rccl"])
 def procs(request):
     """The reference's CPU processors and the GPU batches, the latter completing synchronously (the PUSCH task returns
     with the results notified), asynchronously (results notified from the GPU service's completion thread), or as the
     multi-GPU batch of row b7: the slot's UEs sharded by RNTI over the device list {0, 0, 0} (three shards with their
-    own launch plans, HARQ arenas and grid copies on one GPU, results gathered by peer copies) or over {0} with the
-    RCCL transport (world size 1: the gather is an ncclSend / ncclRecv pair in one group). Every mode must equal the
-    reference's CPU processors, hence the single-device batch."""
+    own launch plans, HARQ arenas and grid copies on one GPU, results gathered by peer copies; synchronous, or
+    asynchronous with the replay on the batch's completion thread) or over {0} with the RCCL transport (world size 1:
+    the gather is an ncclSend / ncclRecv pair in one group). Every mode must equal the reference's CPU processors,
+    hence the single-device batch."""
     import chain_harness as H
     cpu = H.UpperPhy(0, H.UL_CPU, P)
-    extra = {"sync": 0, "async": H.UL_ASYNC, "multi3_copy": H.UL_MULTI_COPY, "multi1_rccl": H.UL_MULTI_RCCL}
+    extra = {"sync": 0, "async": H.UL_ASYNC, "multi3_copy": H.UL_MULTI_COPY,
+             "multi3_copy_async": H.UL_MULTI_COPY | H.UL_ASYNC, "multi1_rccl": H.UL_MULTI_RCCL}
     gpu = H.UpperPhy(0, H.UL_GPU_BATCH | extra[request.param], P)
+    gpu.mode = request.param
     yield cpu, gpu
     cpu.close()
     gpu.close()
@@ -135,8 +138,17 @@ def test_uplink_processor_gpu_batch_equals_reference(procs):
         grid = received_grid(rng, chain, ues, tbs, 28.0)
         pdus = [p for p, *_ in ues]
         ref = cpu.ul_slot(7, pdus, sizes, grid)
+        before = gpu.multi_transfer_counters()
         got = gpu.ul_slot(7, pdus, sizes, grid)
+        after = gpu.multi_transfer_counters()
         check_equal(ref, got, "slot 7")
+        if gpu.mode.startswith("multi3"):
+            # One host-to-device grid transfer for the slot whatever the number of devices; the two other shards
+            # receive only their UEs' subcarrier bands from the root's copy (less than the whole grid each).
+            assert after["host_uploads"] - before["host_uploads"] == 1, (before, after)
+            assert after["shard_copies"] - before["shard_copies"] == 2, (before, after)
+            moved = after["shard_bytes"] - before["shard_bytes"]
+            assert 0 < moved < 2 * P * 14 * 12 * 273 * 4, moved
         ok = {d["rnti"]: d["tb_crc_ok"] for d, _ in ref}
         ack_res = next(d for d, _ in got if d["rnti"] == ack.rnti)
         assert ack_res["harq_ack_status"] >= 0, ack_res  # the HARQ-ACK field was reported

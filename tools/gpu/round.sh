@@ -22,6 +22,7 @@
 #   traffic          FETCH_SIZE / WRITE_SIZE / SQ passes of the bench -> per-kernel HBM traffic vs algorithmic bytes
 #                    (tools/chain_traffic.py), isolated kernel times, VALU issue and waits (tools/sq_summary.py)
 #   ofdmab:DIR[:N]   tools/ofdm_bench.py (isolated OFDM launches, bench shape): in-tree library against DIR's, N rounds
+#   hbm              tools/probes/hbm_rw.py: torch's fill / sum / copy rates (HBM write, read, copy ceilings)
 #   ab:DIR[:N]       A/B of the default bench: the in-tree library against srsran-5g_amd/DIR's, N rounds
 #   slotsab:V=X[:N]  A/B of the UL slot processors (16 threads): default environment against V=X, N rounds
 #   benchab:V=X[:N]  A/B of the default bench: default environment against V=X, N rounds
@@ -149,6 +150,9 @@ for step in "$@"; do
             "$OUT/benchab_${v}_$i.json" "$v ${E[*]}"
         done
       done ;;
+    hbm)
+      timeout -k 10 120 python -u tools/probes/hbm_rw.py > "$OUT/hbm.json" 2>&1 || { tail -20 "$OUT/hbm.json"; exit 1; }
+      tail -1 "$OUT/hbm.json" ;;
     ofdmab:*)
       SPEC=${step#ofdmab:}; DIR=${SPEC%%:*}; N=2; [[ "$SPEC" == *:* ]] && N=${SPEC##*:}
       for i in $(seq 1 "$N"); do

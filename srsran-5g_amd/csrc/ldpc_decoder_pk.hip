@@ -92,13 +92,10 @@ __device__ __forceinline__ pk_consts make_pk_consts()
   return {as_u16(a), c, d, f};
 }
 
-/// v2c of an edge from its soft bit sb and previous c2v magnitude om with sign mask n (0 / -1):
-/// clamp(sb - c2v, +/-LLR_MAX), plus +/-512 for an infinite soft bit (|v2c| >= 392 stays infinite). sb - c2v is one
-/// multiply-add on -(n | 1) = ~n | 1.
-__device__ __forceinline__ s16x2 v2c_pk(s16x2 sb, u16x2 om, s16x2 n, const pk_consts& kc)
+/// v2c of an edge from its soft bit sb and t = sb - c2v: clamp(t, +/-LLR_MAX), plus +/-512 for an infinite soft bit
+/// (|v2c| >= 392 stays infinite).
+__device__ __forceinline__ s16x2 v2c_from_t(s16x2 t, s16x2 sb, const pk_consts& kc)
 {
-  const s16x2 nn  = as_s16(~bits(n) | 0x00010001u);
-  const s16x2 t   = as_s16(bits(om)) * nn + sb;
   const s16x2 ct  = __builtin_elementwise_min(__builtin_elementwise_max(t, ss(-LLR_MAX)), ss(LLR_MAX));
   // Infinity marker without clamping sb: g = sat16(271 sb) - 271 sb is 0 for |sb| <= 120 (271 x 120 = 32520) and
   // -24 / +23 for sb = +121 / -121 (the saturating v_pk_mad_i16 clamps 32791 to 32767); v = clamp(t) - 21 g puts an
@@ -107,6 +104,45 @@ __device__ __forceinline__ s16x2 v2c_pk(s16x2 sb, u16x2 om, s16x2 n, const pk_co
   asm("v_pk_mad_i16 %0, %1, %2, 0 clamp" : "=v"(sat) : "v"(bits(sb)), "s"(kc.k271));
   const s16x2 g = sb * as_s16(kc.kn271) + as_s16(sat);
   return g * as_s16(kc.kn21) + ct;
+}
+
+/// v2c from the previous c2v magnitude om with sign mask n (0 / -1): sb - c2v is one multiply-add on
+/// -(n | 1) = ~n | 1.
+__device__ __forceinline__ s16x2 v2c_pk(s16x2 sb, u16x2 om, s16x2 n, const pk_consts& kc)
+{
+  const s16x2 nn = as_s16(~bits(n) | 0x00010001u);
+  return v2c_from_t(as_s16(bits(om)) * nn + sb, sb, kc);
+}
+
+/// Check-to-variable messages kept whole (C2V layers): the signed c2v of both rows of edge e as int8, two edges per
+/// word [c_z(e + 1), c_z(e), c_zH(e + 1), c_zH(e)] for even e, so that the even edge sits on the odd bytes, whose sign
+/// bits v_perm replicates (selectors 8 / 9): one v_perm gives its two sign-extended 16-bit halves; the odd edge takes a
+/// v_perm into the high bytes and an arithmetic shift. Against the compressed state (sign bits, argmin, min1 / min2)
+/// this replaces the sign expansion, the argmin test and the magnitude select of pass 1 (6 VALU) by 1-2.
+template <int e>
+__device__ __forceinline__ s16x2 c2v_get(const uint32_t* cw)
+{
+  const uint32_t w = cw[e / 2];
+  if constexpr (e % 2 == 0) {
+    return as_s16(__builtin_amdgcn_perm(w, w, 0x09030801u));
+  } else {
+    return as_s16(__builtin_amdgcn_perm(w, w, 0x020c000cu)) >> ss(8);
+  }
+}
+/// Words of c2v storage of a row of DEG edges.
+constexpr int c2v_words(int deg)
+{
+  return (deg + 1) / 2;
+}
+/// Most words of c2v storage over the first L rows of a base graph.
+template <typename G>
+constexpr int c2v_words_max(int L)
+{
+  int w = 0;
+  for (int m = 0; m < L; ++m) {
+    w = c2v_words(G::rs(m + 1) - G::rs(m)) > w ? c2v_words(G::rs(m + 1) - G::rs(m)) : w;
+  }
+  return w;
 }
 
 /// Search key |v| * 32 + e of the two-minimum scan (one v_pk_mad).
@@ -157,6 +193,11 @@ constexpr int CRC_CHUNK = 8;
 /// Occupancy of the 8-layer class: at least 5 workgroups per CU (96 VGPRs, 5 waves per SIMD); 8 with the pass-1
 /// addresses recomputed measured slower (r2: 117.8k vs 112.6k slots/s).
 constexpr int PK_MIN_BLOCKS_8 = 5;
+/// The one-codeblock 8-layer kernel keeps the core layers' c2v whole (C2V_CORE, 40 VGPRs instead of 12): up to 128
+/// VGPRs, 4 waves per SIMD, which still holds the bench's whole launch (2 048 two-wave codeblocks on 1 024 SIMDs).
+constexpr int PK_MIN_WAVES_C2V = 4;
+/// Layers whose c2v messages the 8-layer kernel keeps whole: the four core rows (19 edges each in BG1).
+constexpr int C2V_LAYERS = 4;
 /// Layer bound up to which a row's pass-1 pair addresses stay in VGPRs for pass 2 (above it they are recomputed).
 constexpr int PK_KEEP_ADDR_MAXL = 16;
 
@@ -165,14 +206,15 @@ constexpr int SIGNS_W0 = 11;
 
 /// Two lifted check rows (z, z + H) of layer m: v2c messages, min-sum analysis, c2v messages, soft-bit update
 /// (ldpc_decoder_impl.cpp:195, :255, :240; arithmetic of ldpc_decoder_avx2.cpp:69/:111/:165/:205).
-template <int BG, int MODE, int m, bool KEEP_ADDR, int CS = SOFT_COL_STRIDE>
+template <int BG, int MODE, int m, bool KEEP_ADDR, int CS = SOFT_COL_STRIDE, bool C2V = false>
 __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
                                               const_u32_ptr  ab,  // A | B << 16 address constants of this Z
                                               uint32_t       z2x2,  // 2z in both halves
                                               const scale_t& sc,
                                               uint32_t&      magw,
                                               uint32_t&      sgw,
-                                              uint32_t&      hiw)
+                                              uint32_t&      hiw,
+                                              uint32_t*      cw = nullptr)  // C2V: the row's c2v words
 {
   using G           = bg_t<BG>;
   constexpr int e0  = G::rs(m);
@@ -200,14 +242,19 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     }
     // Two byte loads merged by one v_perm (d16 loads do not preserve the other half with SRAM ECC on gfx950).
     const s16x2 sb{static_cast<short>(soft[col * CS + a]), static_cast<short>(soft[col * CS + (a ^ 1u)])};
-    // Previous c2v of this edge: magnitude min2 at the argmin, min1 elsewhere; sign from the sign bits.
-    constexpr int  pos = (e < SIGNS_W0) ? e : e - SIGNS_W0;
-    const uint32_t sw  = (e < SIGNS_W0) ? sgw : hiw;
-    const s16x2    n   = (as_s16(sw) << ss(15 - pos)) >> ss(15);
-    const u16x2    ne  = not_argmin(IDX, e, one);
-    const u16x2    om  = ne * D + S2;
     // v2c = soft - c2v saturated to +/-LLR_MAX; infinite soft bits give |v2c| >= 392 (stay infinite).
-    const s16x2 v   = v2c_pk(sb, om, n, kc);
+    s16x2 v;
+    if constexpr (C2V) {
+      v = v2c_from_t(sb - c2v_get<e>(cw), sb, kc);
+    } else {
+      // Previous c2v of this edge: magnitude min2 at the argmin, min1 elsewhere; sign from the sign bits.
+      constexpr int  pos = (e < SIGNS_W0) ? e : e - SIGNS_W0;
+      const uint32_t sw  = (e < SIGNS_W0) ? sgw : hiw;
+      const s16x2    n   = (as_s16(sw) << ss(15 - pos)) >> ss(15);
+      const u16x2    ne  = not_argmin(IDX, e, one);
+      const u16x2    om  = ne * D + S2;
+      v                  = v2c_pk(sb, om, n, kc);
+    }
     v2c[e]          = v;
     const u16x2 key = key_pk(v, e, kc);
     k2              = __builtin_elementwise_min(__builtin_elementwise_max(key, k1), k2);
@@ -228,6 +275,7 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
   if constexpr (!KEEP_ADDR) {
     asm volatile("" : "+v"(z2x2_b));
   }
+  s16x2 c_even = ss(0);  // C2V: the c2v of the row's last even edge, packed with the next one
   static_for<deg>([&](auto E) {
     constexpr int e   = decltype(E)::value;
     constexpr int col = G::col(e0 + e);
@@ -239,7 +287,21 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     // c2v + v2c as one multiply-add on the sign +/-1 (n | 1).
     const s16x2 sgn = as_s16(bits(n) | 0x00010001u);
     // Promotion sum (log_likelihood_ratio.cpp:75): |sum| > LLR_MAX becomes +/-infinity (SOFT_INF).
-    const s16x2    sb = clamp2(as_s16(bits(mag)) * sgn + v, -SOFT_INF, SOFT_INF);
+    s16x2 sb;
+    if constexpr (C2V) {
+      const s16x2 c = as_s16(bits(mag)) * sgn;
+      sb            = clamp2(c + v, -SOFT_INF, SOFT_INF);
+      if constexpr (e % 2 == 0) {
+        c_even = c;
+        if constexpr (e == deg - 1) {
+          cw[e / 2] = __builtin_amdgcn_perm(bits(c), bits(c), 0x060c040cu);
+        }
+      } else {
+        cw[e / 2] = __builtin_amdgcn_perm(bits(c_even), bits(c), 0x06020400u);
+      }
+    } else {
+      sb = clamp2(as_s16(bits(mag)) * sgn + v, -SOFT_INF, SOFT_INF);
+    }
     uint32_t       a;
     if constexpr (KEEP_ADDR) {
       a = addr[e];
@@ -250,16 +312,19 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     soft[col * CS + (a ^ 1u)] = static_cast<int8_t>(sb.y);
     constexpr int      pos  = (e < SIGNS_W0) ? e : e - SIGNS_W0;
     constexpr uint32_t mask = (1u << pos) | (1u << (16 + pos));
-    if constexpr (e < SIGNS_W0) {
+    if constexpr (C2V) {
+    } else if constexpr (e < SIGNS_W0) {
       nsg |= bits(n) & mask;
     } else {
       nhi |= bits(n) & mask;
     }
   });
-  magw = bits(S1N | (S2N << uu(7)));
-  sgw  = nsg;
-  if constexpr (deg > SIGNS_W0) {
-    hiw = nhi;
+  if constexpr (!C2V) {
+    magw = bits(S1N | (S2N << uu(7)));
+    sgw  = nsg;
+    if constexpr (deg > SIGNS_W0) {
+      hiw = nhi;
+    }
   }
 }
 
@@ -398,7 +463,7 @@ __device__ __forceinline__ void write_hard_bits_pk(const int8_t* __restrict__ so
 /// itself (dms[blockIdx.x]) into the LDS image and writes the HARQ soft buffer the separate rate_dematch_kernel would
 /// have written (rate_dematcher.hip dematch_new_data: copies symbol-major, fillers +127, the unreached tail zeroed).
 template <int BG, int MODE, int MAXL, int SPLIT, bool FUSE>
-__global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : PK_MIN_BLOCKS_8)))) void ldpc_decode_pk_kernel(const dec_desc* __restrict__ descs,
+__global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MAXL > 8 ? 4 : PK_MIN_WAVES_C2V)))) void ldpc_decode_pk_kernel(const dec_desc* __restrict__ descs,
                                                              const int8_t* __restrict__ llrs,
                                                              uint8_t* __restrict__ out,
                                                              int32_t* __restrict__ results,
@@ -730,6 +795,17 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
     magw[m] = 0;
     sgw[m]  = 0;
   }
+  // The core layers' c2v kept whole (zero before the first iteration: v2c = soft, ldpc_decoder_impl.cpp:218).
+  constexpr bool C2V_CORE = (SPLIT == 1 && MAXL == 8);
+  constexpr int  C2V_W    = c2v_words_max<G>(C2V_LAYERS);
+  uint32_t       c2vw[C2V_LAYERS][C2V_W];
+#pragma unroll
+  for (int m = 0; m < C2V_LAYERS; ++m) {
+#pragma unroll
+    for (int w = 0; w < C2V_W; ++w) {
+      c2vw[m][w] = 0u;
+    }
+  }
   __syncthreads();
 
   const int max_iter = d.max_iter;
@@ -749,8 +825,13 @@ __global__ __launch_bounds__(192 * SPLIT, (SPLIT == 2 ? 2 : (MAXL > 16 ? 3 : (MA
         if constexpr (SPLIT == 1) {
           if (active) {
             __builtin_amdgcn_sched_barrier(0);
-            row_update_pk<BG, MODE, m, (MAXL <= PK_KEEP_ADDR_MAXL)>(soft, abi, z2x2, sc, magw[m], sgw[m],
-                                                                         hiw[m & 3]);
+            if constexpr (C2V_CORE && m < C2V_LAYERS) {
+              row_update_pk<BG, MODE, m, true, SOFT_COL_STRIDE, true>(soft, abi, z2x2, sc, magw[m], sgw[m],
+                                                                      hiw[m & 3], c2vw[m]);
+            } else {
+              row_update_pk<BG, MODE, m, (MAXL <= PK_KEEP_ADDR_MAXL)>(soft, abi, z2x2, sc, magw[m], sgw[m],
+                                                                           hiw[m & 3]);
+            }
             __builtin_amdgcn_sched_barrier(0);
           }
         } else {

@@ -163,6 +163,14 @@ for step in "$@"; do
           head -2 "$OUT/ofdmab_${lib}_$i.txt"
         done
       done ;;
+    ofdmsweep)
+      # isolated OFDM launch time against the number of symbols per launch (slots x 4 ports x 14): the workgroup
+      # rounds per CU show as steps in the time
+      for s in 8 16 20 22 23 24 28 32 40 45 46 64; do
+        timeout -k 10 120 python -u tools/ofdm_bench.py --slots "$s" --iters 100 > "$OUT/ofdmsweep_$s.txt" 2>&1 \
+          || { tail -20 "$OUT/ofdmsweep_$s.txt"; exit 1; }
+        echo "slots $s: $(head -2 "$OUT/ofdmsweep_$s.txt" | tr '\n' ' ')"
+      done ;;
     ab:*)
       # ab:DIR[:N] — the default bench N times (default 2), alternating the in-tree library and srsran-5g_amd/DIR's
       SPEC=${step#ab:}; DIR=${SPEC%%:*}; N=2; [[ "$SPEC" == *:* ]] && N=${SPEC##*:}

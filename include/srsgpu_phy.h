@@ -934,6 +934,16 @@ typedef struct {
 
 int srsgpu_copy_spans(const srsgpu_copy_span* d_spans, uint32_t nof_spans, uint64_t max_bytes, void* stream);
 
+/** As srsgpu_copy_spans, but each 32-bit word of a source replaces the destination's only when it is not `sentinel`:
+ *  the gather of a multi-device PDSCH slot batch, whose shards map their UEs' REs into sentinel-filled grids and merge
+ *  their bands into the root device's grid (peer reads over xGMI) before its one download
+ *  (downlink_processor_single_executor_impl.cpp:268-274 sends one grid per slot). */
+int srsgpu_merge_spans(const srsgpu_copy_span* d_spans,
+                       uint32_t                nof_spans,
+                       uint64_t                max_bytes,
+                       uint32_t                sentinel,
+                       void*                   stream);
+
 /** As srsgpu_pusch_chest_plan_execute, with the span copies d_spans[0, nof_spans) (each as in srsgpu_copy_spans,
  *  max_bytes the largest) done in the same launch by extra workgroups while the estimator's run: for a slot batch whose rx
  *  grids are read from mapped host memory, the data-symbol rows, which the estimator does not read, arrive while it

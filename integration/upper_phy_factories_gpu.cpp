@@ -330,7 +330,8 @@ private:
       invalid(WHO, "invalid resource grid gateway or executor");
     }
     std::shared_ptr<gpu::pdsch_slot_batch> batch =
-        gpu::create_pdsch_slot_batch(cfg.device, cfg.ptrs_factory->create(), std::move(fallback));
+        gpu::create_pdsch_slot_batch(gpu::pdsch_batch_configuration{cfg.device, cfg.devices}, cfg.ptrs_factory->create(),
+                                     std::move(fallback));
     // The reference posts each PDSCH to its executor (downlink_processor_single_executor_impl.cpp:96-135): the batch
     // executor runs it inline while the wrapper's process_pdsch is in progress, so the batch records it.
     auto exec = std::make_unique<gpu::pdsch_batch_executor>(*config.executor);

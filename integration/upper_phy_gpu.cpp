@@ -27,7 +27,9 @@
 #include "srsran/ran/pusch/ulsch_info.h"
 #include "srsran/ran/sch/sch_dmrs_power.h"
 
+#include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdio>
 #include <map>
 #include <mutex>
@@ -46,7 +48,10 @@ namespace {
 struct pdsch_entry {
   resource_grid_writer*          grid     = nullptr;
   pdsch_processor_notifier*      notifier = nullptr;
-  srsgpu_pdsch_tb_config         tb;
+  srsgpu_pdsch_tb_config         tb;  ///< tb_offset / cw_offset are set per launch
+  std::vector<uint8_t>           data;
+  unsigned                       cw_bytes = 0;
+  crb_bitmap                     crbs;  ///< the allocation's CRBs (the multi-device gather moves these bands)
   pdsch_modulator::config_t      mod;
   dmrs_pdsch_processor::config_t dmrs;
 };
@@ -61,18 +66,24 @@ public:
 
 thread_local bool pdsch_inline_scope = false;
 
-} // namespace
+/// Grid transfers of the multi-device PDSCH batches, process-wide.
+struct {
+  std::atomic<uint64_t> grid_downloads{0};
+  std::atomic<uint64_t> shard_merges{0};
+  std::atomic<uint64_t> merge_bytes{0};
+} pdsch_transfers;
 
-class pdsch_slot_batch
+
+/// One device's part of a PDSCH slot batch: its launch plans and captured graphs, TB staging, codewords and a
+/// sentinel-filled scratch grid into which the encoder, DM-RS and modulator map its PDSCHs.
+class pdsch_shard
 {
   static constexpr const char* WHO = "pdsch_slot_batch";
 
 public:
-  pdsch_slot_batch(int device, std::unique_ptr<ptrs_pdsch_generator> ptrs_, std::unique_ptr<pdsch_processor> fallback_) :
+  explicit pdsch_shard(int device) :
     owner(shared_context(device)),
     ctx(owner.get()),
-    ptrs(std::move(ptrs_)),
-    fallback(std::move(fallback_)),
     stream(ctx, WHO),
     enc_plans(srsgpu_pdsch_encoder_plan_destroy, 16),
     mod_plans(srsgpu_pdsch_modulator_plan_destroy, 16),
@@ -81,15 +92,184 @@ public:
     tb_buf(WHO),
     grid_buf(WHO)
   {
+    device_scope dev(ctx, WHO);
+    hip_check(hipEventCreateWithFlags(&done, hipEventDisableTiming), WHO, "event");
+  }
+
+  ~pdsch_shard()
+  {
+    device_scope dev(ctx, WHO);
+    (void)hipStreamSynchronize(stream.get());
+    (void)hipFree(d_cw);
+    (void)hipEventDestroy(done);
+  }
+
+  /// The scratch grid (P x 14 rows of `row` bytes) on the device, grown when needed.
+  void reserve_grid(size_t bytes)
+  {
+    device_scope                          dev(ctx, WHO);
+    std::lock_guard<std::recursive_mutex> setup_lock(gpu::hip_setup_mutex());
+    grid_buf.reserve(bytes);
+  }
+
+  /// Queues the PDSCHs `es` on the stream as one captured graph (cached per layout): TB upload, sentinel scratch grid,
+  /// encoder, DM-RS, modulator, and, with `download`, the grid back into the host image. Without PDSCHs only the
+  /// sentinel fill.
+  void launch(const std::vector<const pdsch_entry*>& es, unsigned grid_prb, unsigned P, bool download)
+  {
+    device_scope   dev(ctx, WHO);
+    const unsigned nsc   = grid_prb * NRE;
+    const size_t   row   = static_cast<size_t>(nsc) * sizeof(uint32_t);
+    const size_t   gsize = static_cast<size_t>(P) * 14 * row;
+    hipStream_t    s     = stream.get();
+    reserve_grid(gsize);
+    if (es.empty()) {
+      hip_check(hipMemsetAsync(grid_buf.dev(), 0xff, gsize, s), WHO, "scratch");
+      return;
+    }
+    const unsigned                      n = static_cast<unsigned>(es.size());
+    std::vector<srsgpu_pdsch_tb_config> tcs;
+    std::vector<pdsch_mod_desc>         mods;
+    std::vector<pdsch_dmrs_desc>        dmrss;
+    std::vector<uint8_t>                enc_key, mod_key, dmrs_key, tbs;
+    unsigned                            cw_bytes = 0;
+    gpu::key_append(mod_key, grid_prb);
+    gpu::key_append(dmrs_key, grid_prb);
+    for (const pdsch_entry* e : es) {
+      srsgpu_pdsch_tb_config tc = e->tb;
+      tc.tb_offset              = static_cast<uint32_t>(tbs.size());
+      tc.cw_offset              = cw_bytes;
+      tbs.insert(tbs.end(), e->data.begin(), e->data.end());
+      tbs.resize((tbs.size() + 15) / 16 * 16, 0);
+      cw_bytes += e->cw_bytes;
+      tcs.push_back(tc);
+      gpu::key_append(enc_key, tc);
+      const unsigned nof_bits = tc.nof_ch_symbols * tc.modulation_order;
+      mods.push_back(make_pdsch_mod_desc(e->mod, nof_bits, grid_prb, P, WHO));
+      mods.back().c.cw_offset = tc.cw_offset;
+      mods.back().append_key(mod_key);
+      dmrss.push_back(make_pdsch_dmrs_desc(e->dmrs, grid_prb, P, WHO));
+      dmrss.back().append_key(dmrs_key);
+    }
+    srsgpu_pdsch_encoder_plan* enc = enc_plans.get(enc_key, [&] {
+      srsgpu_pdsch_encoder_plan* p = nullptr;
+      srsgpu_check(srsgpu_pdsch_encoder_plan_create(ctx, tcs.data(), n, &p), WHO);
+      return p;
+    });
+    srsgpu_pdsch_modulator_plan* mod = mod_plans.get(mod_key, [&] {
+      std::vector<srsgpu_pdsch_mod_config> c;
+      std::vector<srsgpu_alloc_ext>        x;
+      for (pdsch_mod_desc& d : mods) {
+        c.push_back(d.c);
+        x.push_back(d.ext());
+      }
+      srsgpu_pdsch_modulator_plan* p = nullptr;
+      srsgpu_check(srsgpu_pdsch_modulator_plan_create_ex(ctx, c.data(), x.data(), n, grid_prb, P, &p), WHO);
+      return p;
+    });
+    srsgpu_pdsch_dmrs_plan* dmrs = dmrs_plans.get(dmrs_key, [&] {
+      std::vector<srsgpu_pdsch_dmrs_config> c;
+      std::vector<srsgpu_alloc_ext>         x;
+      for (const pdsch_dmrs_desc& d : dmrss) {
+        c.push_back(d.c);
+        x.push_back(d.ext());
+      }
+      srsgpu_pdsch_dmrs_plan* p = nullptr;
+      srsgpu_check(srsgpu_pdsch_dmrs_plan_create_ex(ctx, c.data(), x.data(), n, grid_prb, P, &p), WHO);
+      return p;
+    });
+    {
+      // Buffer growth and the graph capture call synchronous HIP APIs, which fail while any thread captures a
+      // stream: both run under gpu::hip_setup_mutex, as the UL slot batch's do.
+      std::lock_guard<std::recursive_mutex> setup_lock(gpu::hip_setup_mutex());
+      tb_buf.reserve(std::max<size_t>(tbs.size(), 16));
+      if (cw_bytes > d_cw_cap) {
+        (void)hipFree(d_cw);
+        d_cw     = nullptr;
+        d_cw_cap = 0;
+        hip_check(hipMalloc(&d_cw, cw_bytes), WHO, "codewords");
+        d_cw_cap = cw_bytes;
+      }
+    }
+    std::memcpy(tb_buf.host(), tbs.data(), tbs.size());
+
+    // The shard's device work as one captured graph per layout (cached like the plans it runs), so a slot costs one
+    // graph launch instead of six queue operations.
+    std::vector<uint8_t> graph_key;
+    for (const std::vector<uint8_t>* k : {&enc_key, &mod_key, &dmrs_key}) {
+      gpu::key_append(graph_key, k->size());
+      graph_key.insert(graph_key.end(), k->begin(), k->end());
+    }
+    for (const void* ptr : {static_cast<const void*>(tb_buf.host()), static_cast<const void*>(tb_buf.dev()),
+                            static_cast<const void*>(grid_buf.host()), static_cast<const void*>(grid_buf.dev()),
+                            static_cast<const void*>(d_cw)}) {
+      gpu::key_append(graph_key, ptr);
+    }
+    gpu::key_append(graph_key, tbs.size());
+    gpu::key_append(graph_key, P);
+    gpu::key_append(graph_key, download);
+    std::unique_lock<std::recursive_mutex> setup_lock(gpu::hip_setup_mutex());
+    // A plan evicted since the last slot invalidates the graphs that run it.
+    const uint64_t generation = enc_plans.evictions() + mod_plans.evictions() + dmrs_plans.evictions();
+    if (generation != plan_generation) {
+      graphs.clear();
+      plan_generation = generation;
+    }
+    hipGraphExec_t exec = graphs.get(graph_key, [&] { return capture_graph(s, WHO, [&] {
+      tb_buf.upload(0, tbs.size(), s);
+      // Sentinel scratch grid: exactly the REs the PDSCH and its DM-RS map come back.
+      hip_check(hipMemsetAsync(grid_buf.dev(), 0xff, gsize, s), WHO, "scratch");
+      srsgpu_check(srsgpu_pdsch_encoder_plan_execute(enc, tb_buf.dev<uint8_t>(), d_cw, s), WHO);
+      srsgpu_check(srsgpu_pdsch_dmrs_plan_execute(dmrs, grid_buf.dev<uint32_t>(), s), WHO);
+      srsgpu_check(srsgpu_pdsch_modulator_plan_execute(mod, d_cw, grid_buf.dev<uint32_t>(), s), WHO);
+      if (download) {
+        grid_buf.download(0, gsize, s);
+      }
+    }); });
+    setup_lock.unlock();
+    hip_check(hipGraphLaunch(exec, s), WHO, "graph launch");
+  }
+
+  std::shared_ptr<srsgpu_context>                   owner;
+  srsgpu_context*                                   ctx;
+  owned_stream                                      stream;
+  plan_cache<srsgpu_pdsch_encoder_plan>             enc_plans;
+  plan_cache<srsgpu_pdsch_modulator_plan>           mod_plans;
+  plan_cache<srsgpu_pdsch_dmrs_plan>                dmrs_plans;
+  plan_cache<std::remove_pointer_t<hipGraphExec_t>> graphs;
+  uint64_t                                          plan_generation = 0;
+  staged_buffer                                     tb_buf;
+  staged_buffer                                     grid_buf;
+  uint8_t*                                          d_cw     = nullptr;
+  size_t                                            d_cw_cap = 0;
+  hipEvent_t                                        done     = nullptr;
+};
+
+} // namespace
+
+pdsch_multi_transfer_counters get_pdsch_multi_transfer_counters()
+{
+  return {pdsch_transfers.grid_downloads.load(), pdsch_transfers.shard_merges.load(),
+          pdsch_transfers.merge_bytes.load()};
+}
+
+class pdsch_slot_batch
+{
+  static constexpr const char* WHO = "pdsch_slot_batch";
+
+public:
+  pdsch_slot_batch(const pdsch_batch_configuration&      config,
+                   std::unique_ptr<ptrs_pdsch_generator> ptrs_,
+                   std::unique_ptr<pdsch_processor>      fallback_) :
+    ptrs(std::move(ptrs_)), fallback(std::move(fallback_)), spans(WHO)
+  {
     if (!ptrs || !fallback) {
       throw std::invalid_argument(std::string(WHO) + ": invalid dependencies");
     }
-  }
-
-  ~pdsch_slot_batch()
-  {
-    (void)hipStreamSynchronize(stream.get());
-    (void)hipFree(d_cw);
+    const std::vector<int> devs = config.devices.empty() ? std::vector<int>{config.device} : config.devices;
+    for (int d : devs) {
+      shards.push_back(std::make_unique<pdsch_shard>(d));
+    }
   }
 
   /// pdsch_processor_impl::process (pdsch_processor_impl.cpp:42-90) up to the point where the encoder, modulator and
@@ -120,11 +300,9 @@ public:
     e.tb.tbs_bytes        = static_cast<uint32_t>(tb.size());
     e.tb.nof_ch_symbols   = nre * nof_layers;
     e.tb.Nref = ldpc::compute_N_ref(pdu.tbs_lbrm, ldpc::compute_nof_codeblocks(tbs, pdu.ldpc_base_graph)).value();
-    e.tb.tb_offset = static_cast<uint32_t>(tb_bytes.size());
-    tb_bytes.insert(tb_bytes.end(), tb.begin(), tb.end());
-    tb_bytes.resize((tb_bytes.size() + 15) / 16 * 16, 0);
-    e.tb.cw_offset = cw_total;
-    cw_total += (nre * nof_layers * qm + 31) / 32 * 4;
+    e.data.assign(tb.begin(), tb.end());
+    e.cw_bytes = (nre * nof_layers * qm + 31) / 32 * 4;
+    e.crbs     = pdu.freq_alloc.get_crb_mask(pdu.bwp_start_rb, pdu.bwp_size_rb);
 
     // The modulator configuration pdsch_processor_impl::modulate builds (pdsch_processor_impl.cpp:143-161; one
     // codeword; dmrs_config_type is not set there, so it keeps its default, type 1).
@@ -152,161 +330,135 @@ public:
     entries.push_back(std::move(e));
   }
 
-  /// Encodes, modulates and maps every recorded PDSCH as one launch sequence, stores the REs into the slot's grid and
-  /// reports each PDSCH finished (after which the reference's downlink processor sends the grid).
+  /// Encodes, modulates and maps every recorded PDSCH, stores the REs into the slot's grid and reports each PDSCH
+  /// finished (after which the reference's downlink processor sends the grid). One device: one launch sequence and one
+  /// download. Several devices (row b7's DL counterpart): a UE's PDSCH runs on the device of its RNTI modulo the number
+  /// of devices, every shard maps into its own sentinel-filled grid, the other shards' subcarrier bands are merged into
+  /// the root's grid on the root (peer reads over xGMI, sentinel words skipped) and the root's grid comes back once.
   void flush()
   {
     std::vector<pdsch_entry> es;
-    std::vector<uint8_t>     tbs;
-    unsigned                 cw_bytes = 0;
     {
       std::lock_guard<std::mutex> lock(mtx);
-      es       = std::exchange(entries, {});
-      tbs      = std::exchange(tb_bytes, {});
-      cw_bytes = std::exchange(cw_total, 0u);
+      es = std::exchange(entries, {});
     }
     if (es.empty()) {
       return;
     }
     std::lock_guard<std::mutex> lock(run_mtx);
-    device_scope                dev(ctx, WHO);
     resource_grid_writer&       grid     = *es.front().grid;
     const unsigned              nsc      = grid.get_nof_subc();
     const unsigned              grid_prb = nsc / NRE;
     const unsigned              P        = grid.get_nof_ports();
-    const unsigned              n        = es.size();
-
-    std::vector<srsgpu_pdsch_tb_config> tcs;
-    std::vector<pdsch_mod_desc>         mods;
-    std::vector<pdsch_dmrs_desc>        dmrss;
-    std::vector<uint8_t>                enc_key, mod_key, dmrs_key;
-    gpu::key_append(mod_key, grid_prb);
-    gpu::key_append(dmrs_key, grid_prb);
+    const unsigned              D        = static_cast<unsigned>(shards.size());
+    const size_t                row      = static_cast<size_t>(nsc) * sizeof(uint32_t);
+    const size_t                gsize    = static_cast<size_t>(P) * 14 * row;
+    std::vector<std::vector<const pdsch_entry*>> part(D);
     for (const pdsch_entry& e : es) {
       if (e.grid != &grid) {
         throw std::logic_error(std::string(WHO) + ": PDSCH of one batch in different resource grids");
       }
-      tcs.push_back(e.tb);
-      gpu::key_append(enc_key, e.tb);
-      const unsigned nof_bits = e.tb.nof_ch_symbols * e.tb.modulation_order;
-      mods.push_back(make_pdsch_mod_desc(e.mod, nof_bits, grid_prb, P, WHO));
-      mods.back().c.cw_offset = e.tb.cw_offset;
-      mods.back().append_key(mod_key);
-      dmrss.push_back(make_pdsch_dmrs_desc(e.dmrs, grid_prb, P, WHO));
-      dmrss.back().append_key(dmrs_key);
+      part[D == 1 ? 0 : e.mod.rnti % D].push_back(&e);
     }
-    srsgpu_pdsch_encoder_plan* enc = enc_plans.get(enc_key, [&] {
-      srsgpu_pdsch_encoder_plan* p = nullptr;
-      srsgpu_check(srsgpu_pdsch_encoder_plan_create(ctx, tcs.data(), n, &p), WHO);
-      return p;
-    });
-    srsgpu_pdsch_modulator_plan* mod = mod_plans.get(mod_key, [&] {
-      std::vector<srsgpu_pdsch_mod_config> c;
-      std::vector<srsgpu_alloc_ext>        x;
-      for (pdsch_mod_desc& d : mods) {
-        c.push_back(d.c);
-        x.push_back(d.ext());
+    pdsch_shard& root = *shards[0];
+    if (D == 1) {
+      root.launch(part[0], grid_prb, P, true);
+    } else {
+      // The shards' launches first, so that they run while the root maps its own UEs.
+      for (unsigned s = 1; s != D; ++s) {
+        if (!part[s].empty()) {
+          shards[s]->launch(part[s], grid_prb, P, false);
+          device_scope sdev(shards[s]->ctx, WHO);
+          hip_check(hipEventRecord(shards[s]->done, shards[s]->stream.get()), WHO, "event");
+        }
       }
-      srsgpu_pdsch_modulator_plan* p = nullptr;
-      srsgpu_check(srsgpu_pdsch_modulator_plan_create_ex(ctx, c.data(), x.data(), n, grid_prb, P, &p), WHO);
-      return p;
-    });
-    srsgpu_pdsch_dmrs_plan* dmrs = dmrs_plans.get(dmrs_key, [&] {
-      std::vector<srsgpu_pdsch_dmrs_config> c;
-      std::vector<srsgpu_alloc_ext>         x;
-      for (const pdsch_dmrs_desc& d : dmrss) {
-        c.push_back(d.c);
-        x.push_back(d.ext());
+      root.launch(part[0], grid_prb, P, false);
+      // Each shard's bands: its UEs' allocations, merged.
+      size_t nspans = 0;
+      std::vector<std::vector<std::pair<unsigned, unsigned>>> bands(D);
+      for (unsigned s = 1; s != D; ++s) {
+        for (const pdsch_entry* e : part[s]) {
+          if (e->crbs.any()) {
+            bands[s].emplace_back(static_cast<unsigned>(e->crbs.find_lowest()) * NRE,
+                                  (static_cast<unsigned>(e->crbs.find_highest()) + 1) * NRE);
+          }
+        }
+        std::sort(bands[s].begin(), bands[s].end());
+        std::vector<std::pair<unsigned, unsigned>> merged;
+        for (const auto& r : bands[s]) {
+          if (!merged.empty() && r.first <= merged.back().second) {
+            merged.back().second = std::max(merged.back().second, r.second);
+          } else {
+            merged.push_back(r);
+          }
+        }
+        bands[s] = std::move(merged);
+        nspans += bands[s].size() * P * 14;
       }
-      srsgpu_pdsch_dmrs_plan* p = nullptr;
-      srsgpu_check(srsgpu_pdsch_dmrs_plan_create_ex(ctx, c.data(), x.data(), n, grid_prb, P, &p), WHO);
-      return p;
-    });
-
-    hipStream_t  s   = stream.get();
-    const size_t row = static_cast<size_t>(nsc) * sizeof(uint32_t);
+      device_scope rdev(root.ctx, WHO);
+      hipStream_t  rs = root.stream.get();
+      spans.reserve(std::max<size_t>(nspans, 1) * sizeof(srsgpu_copy_span));
+      auto*    sp   = spans.host<srsgpu_copy_span>();
+      size_t   next = 0;
+      uint64_t most = 0;
+      for (unsigned s = 1; s != D; ++s) {
+        if (part[s].empty()) {
+          continue;
+        }
+        for (const auto& b : bands[s]) {
+          const size_t off = static_cast<size_t>(b.first) * sizeof(uint32_t);
+          const size_t len = static_cast<size_t>(b.second - b.first) * sizeof(uint32_t);
+          for (unsigned r = 0; r != P * 14; ++r) {
+            sp[next++] = {shards[s]->grid_buf.dev(r * row + off), root.grid_buf.dev(r * row + off), len};
+            pdsch_transfers.merge_bytes.fetch_add(len, std::memory_order_relaxed);
+          }
+          most = std::max<uint64_t>(most, len);
+        }
+        hip_check(hipStreamWaitEvent(rs, shards[s]->done, 0), WHO, "wait for a shard");
+        pdsch_transfers.shard_merges.fetch_add(1, std::memory_order_relaxed);
+      }
+      if (next != 0) {
+        srsgpu_check(srsgpu_merge_spans(spans.dev<srsgpu_copy_span>(), static_cast<uint32_t>(next), most,
+                                        GRID_SENTINEL, rs),
+                     WHO);
+      }
+      root.grid_buf.download(0, gsize, rs);
+    }
+    pdsch_transfers.grid_downloads.fetch_add(1, std::memory_order_relaxed);
     {
-      // Buffer growth and the graph capture call synchronous HIP APIs, which fail while any thread captures a
-      // stream: both run under gpu::hip_setup_mutex, as the UL slot batch's do.
-      std::lock_guard<std::recursive_mutex> setup_lock(gpu::hip_setup_mutex());
-      tb_buf.reserve(std::max<size_t>(tbs.size(), 16));
-      if (cw_bytes > d_cw_cap) {
-        (void)hipFree(d_cw);
-        d_cw     = nullptr;
-        d_cw_cap = 0;
-        hip_check(hipMalloc(&d_cw, cw_bytes), WHO, "codewords");
-        d_cw_cap = cw_bytes;
-      }
-      grid_buf.reserve(P * 14 * row);
+      device_scope rdev(root.ctx, WHO);
+      hip_check(hipStreamSynchronize(root.stream.get()), WHO, "synchronise");
     }
-    std::memcpy(tb_buf.host(), tbs.data(), tbs.size());
-
-    // The slot's device work as one captured graph per layout (cached like the plans it runs), so a slot costs one
-    // graph launch instead of six queue operations.
-    std::vector<uint8_t> graph_key;
-    for (const std::vector<uint8_t>* k : {&enc_key, &mod_key, &dmrs_key}) {
-      gpu::key_append(graph_key, k->size());
-      graph_key.insert(graph_key.end(), k->begin(), k->end());
-    }
-    for (const void* ptr : {static_cast<const void*>(tb_buf.host()), static_cast<const void*>(tb_buf.dev()),
-                            static_cast<const void*>(grid_buf.host()), static_cast<const void*>(grid_buf.dev()),
-                            static_cast<const void*>(d_cw)}) {
-      gpu::key_append(graph_key, ptr);
-    }
-    gpu::key_append(graph_key, tbs.size());
-    gpu::key_append(graph_key, P);
-    std::unique_lock<std::recursive_mutex> setup_lock(gpu::hip_setup_mutex());
-    // A plan evicted since the last slot invalidates the graphs that run it.
-    const uint64_t generation = enc_plans.evictions() + mod_plans.evictions() + dmrs_plans.evictions();
-    if (generation != plan_generation) {
-      graphs.clear();
-      plan_generation = generation;
-    }
-    hipGraphExec_t exec = graphs.get(graph_key, [&] { return capture_graph(s, WHO, [&] {
-      tb_buf.upload(0, tbs.size(), s);
-      // Sentinel scratch grid: exactly the REs the PDSCH and its DM-RS map come back.
-      hip_check(hipMemsetAsync(grid_buf.dev(), 0xff, P * 14 * row, s), WHO, "scratch");
-      srsgpu_check(srsgpu_pdsch_encoder_plan_execute(enc, tb_buf.dev<uint8_t>(), d_cw, s), WHO);
-      srsgpu_check(srsgpu_pdsch_dmrs_plan_execute(dmrs, grid_buf.dev<uint32_t>(), s), WHO);
-      srsgpu_check(srsgpu_pdsch_modulator_plan_execute(mod, d_cw, grid_buf.dev<uint32_t>(), s), WHO);
-      grid_buf.download(0, P * 14 * row, s);
-    }); });
-    setup_lock.unlock();
-    hip_check(hipGraphLaunch(exec, s), WHO, "graph launch");
-    hip_check(hipStreamSynchronize(s), WHO, "synchronise");
-    store_written_res(grid, grid_buf.host<uint32_t>(), P, nsc, 0, 14);
+    store_written_res(grid, root.grid_buf.host<uint32_t>(), P, nsc, 0, 14);
     for (pdsch_entry& e : es) {
       e.notifier->on_finish_processing();
     }
   }
 
 private:
-  std::shared_ptr<srsgpu_context>       owner;
-  srsgpu_context*                       ctx;
-  std::unique_ptr<ptrs_pdsch_generator> ptrs;
-  std::unique_ptr<pdsch_processor>      fallback;
-  owned_stream                          stream;
-  plan_cache<srsgpu_pdsch_encoder_plan>   enc_plans;
-  plan_cache<srsgpu_pdsch_modulator_plan> mod_plans;
-  plan_cache<srsgpu_pdsch_dmrs_plan>      dmrs_plans;
-  plan_cache<std::remove_pointer_t<hipGraphExec_t>> graphs;
-  uint64_t                              plan_generation = 0;
-  staged_buffer                         tb_buf;
-  staged_buffer                         grid_buf;
-  uint8_t*                              d_cw     = nullptr;
-  size_t                                d_cw_cap = 0;
-  std::mutex                            mtx;
-  std::vector<pdsch_entry>              entries;
-  std::vector<uint8_t>                  tb_bytes;
-  unsigned                              cw_total = 0;
-  std::mutex                            run_mtx;
+  std::unique_ptr<ptrs_pdsch_generator>     ptrs;
+  std::unique_ptr<pdsch_processor>          fallback;
+  std::vector<std::unique_ptr<pdsch_shard>> shards;
+  mapped_buffer                             spans;  ///< the multi-device gather's merge list
+  std::mutex                                mtx;
+  std::vector<pdsch_entry>                  entries;
+  std::mutex                                run_mtx;
 };
+
+std::shared_ptr<pdsch_slot_batch> create_pdsch_slot_batch(const pdsch_batch_configuration&      config,
+                                                          std::unique_ptr<ptrs_pdsch_generator> ptrs,
+                                                          std::unique_ptr<pdsch_processor>      fallback)
+{
+  return std::make_shared<pdsch_slot_batch>(config, std::move(ptrs), std::move(fallback));
+}
 
 std::shared_ptr<pdsch_slot_batch> create_pdsch_slot_batch(int                                   device,
                                                           std::unique_ptr<ptrs_pdsch_generator> ptrs,
                                                           std::unique_ptr<pdsch_processor>      fallback)
 {
-  return std::make_shared<pdsch_slot_batch>(device, std::move(ptrs), std::move(fallback));
+  pdsch_batch_configuration c;
+  c.device = device;
+  return create_pdsch_slot_batch(c, std::move(ptrs), std::move(fallback));
 }
 
 namespace {

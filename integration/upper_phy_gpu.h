@@ -160,9 +160,31 @@ std::unique_ptr<uplink_processor> create_uplink_processor_batch_gpu(std::unique_
                                                                     std::shared_ptr<pusch_slot_batch> batch,
                                                                     task_executor&                    executor);
 
+/// PDSCH slot batching parameters.
+struct pdsch_batch_configuration {
+  int device = 0;
+  /// Multi-GPU (the DL counterpart of row b7): the devices a slot's PDSCHs are sharded over, the first one the root;
+  /// empty: one device (`device`). A PDSCH runs on the device of its RNTI modulo the number of devices; every shard maps
+  /// its UEs into its own grid and the root merges the shards' subcarrier bands into its grid (peer reads over xGMI)
+  /// before the slot's one download.
+  std::vector<int> devices;
+};
+
+/// Grid transfers of the PDSCH slot batches, process-wide: device-to-host grid downloads (one per slot, from the root
+/// device, whatever the number of devices), shard-to-root merges and the bytes they moved (each shard's bands only).
+struct pdsch_multi_transfer_counters {
+  uint64_t grid_downloads = 0;
+  uint64_t shard_merges   = 0;
+  uint64_t merge_bytes    = 0;
+};
+pdsch_multi_transfer_counters get_pdsch_multi_transfer_counters();
+
 /// A slot batch of PDSCH transmissions (one per downlink processor). ptrs: the reference's PT-RS generator (host);
 /// fallback: the processor for PDUs the batch does not cover (two codewords).
 class pdsch_slot_batch;
+std::shared_ptr<pdsch_slot_batch> create_pdsch_slot_batch(const pdsch_batch_configuration&      config,
+                                                          std::unique_ptr<ptrs_pdsch_generator> ptrs,
+                                                          std::unique_ptr<pdsch_processor>      fallback);
 std::shared_ptr<pdsch_slot_batch> create_pdsch_slot_batch(int                                   device,
                                                           std::unique_ptr<ptrs_pdsch_generator> ptrs,
                                                           std::unique_ptr<pdsch_processor>      fallback);
@@ -270,6 +292,7 @@ create_uplink_processor_factory_gpu(const uplink_processor_factory_gpu_configura
 /// device and the PT-RS generator the PDSCH slot batch maps on the host.
 struct downlink_processor_factory_gpu_configuration {
   int                                           device = 0;
+  std::vector<int>                              devices;  ///< multi-GPU PDSCH shards (gpu::pdsch_batch_configuration)
   std::shared_ptr<pdcch_processor_factory>      pdcch_factory;
   /// The PDSCH processors for the PDUs a slot batch does not cover (two codewords); its validator is the factory's.
   std::shared_ptr<pdsch_processor_factory>      pdsch_factory;

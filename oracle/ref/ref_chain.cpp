@@ -1579,10 +1579,13 @@ struct dl_harness {
 };
 
 /// The GPU downlink processor factory of the tests (row b8).
-std::shared_ptr<downlink_processor_factory> dl_factory(int device)
+std::shared_ptr<downlink_processor_factory> dl_factory(int device, bool multi = false)
 {
   downlink_processor_factory_gpu_configuration fc;
   fc.device             = device;
+  if (multi) {
+    fc.devices = {device, device, device};  // three PDSCH shards on one GPU (the gather through peer reads)
+  }
   fc.pdcch_factory      = std::make_shared<stub_pdcch_factory>();
   fc.pdsch_factory      = create_pdsch_processor_factory_gpu(device, std::make_shared<gpu_pdsch_encoder_factory>(device),
                                                         std::make_shared<ptrs_factory_ref>());
@@ -1612,7 +1615,7 @@ dl_harness* dl_create(int device, int variant, unsigned P, unsigned grid_prb)
   }
   // Row b8: the GPU downlink processor only through the downlink_processor_factory interface; the PDSCHs the slot
   // batch does not cover go to the GPU per-PDU PDSCH processor factory (HAL encoder, GPU modulator and DM-RS).
-  h->factory = dl_factory(device);
+  h->factory = dl_factory(device, (variant & 8) != 0);
   downlink_processor_config dc;
   dc.id       = 0;
   dc.gateway  = &h->gateway;
@@ -1651,6 +1654,16 @@ void chain_multi_transfer_counters(uint64_t* out)
   out[0]                                     = c.host_uploads;
   out[1]                                     = c.shard_copies;
   out[2]                                     = c.shard_bytes;
+}
+
+/// Process-wide grid transfer counts of the PDSCH slot batches (gpu::get_pdsch_multi_transfer_counters): out[0]
+/// device-to-host grid downloads, out[1] shard-to-root merges, out[2] bytes those merges moved.
+void chain_pdsch_transfer_counters(uint64_t* out)
+{
+  const gpu::pdsch_multi_transfer_counters c = gpu::get_pdsch_multi_transfer_counters();
+  out[0]                                     = c.grid_downloads;
+  out[1]                                     = c.shard_merges;
+  out[2]                                     = c.merge_bytes;
 }
 
 /// One UL slot: the PUSCH PDUs (tb_bytes[i] each) registered in the reference's PDU repository, the received grid

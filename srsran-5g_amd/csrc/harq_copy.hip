@@ -54,7 +54,52 @@ __global__ void __launch_bounds__(256) copy_spans_kernel(const srsgpu_copy_span*
   }
 }
 
+/// Span merges: as copy_spans_kernel, but a 32-bit source word replaces the destination's only when it differs from
+/// `sentinel` (the words a producer left unwritten in a sentinel-filled grid).
+__global__ void __launch_bounds__(256) merge_spans_kernel(const srsgpu_copy_span* __restrict__ spans, uint32_t sentinel)
+{
+  const srsgpu_copy_span sp = spans[blockIdx.y];
+  const uint4*           s4 = reinterpret_cast<const uint4*>(sp.src);
+  uint4*                 d4 = reinterpret_cast<uint4*>(sp.dst);
+  const uint64_t         n  = sp.bytes / 16u;
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint4    v    = s4[i];
+    const uint32_t keep = (v.x != sentinel ? 1u : 0u) | (v.y != sentinel ? 2u : 0u) | (v.z != sentinel ? 4u : 0u) |
+                          (v.w != sentinel ? 8u : 0u);
+    if (keep == 15u) {
+      d4[i] = v;
+    } else if (keep != 0u) {
+      uint4 o = d4[i];
+      o.x     = (keep & 1u) ? v.x : o.x;
+      o.y     = (keep & 2u) ? v.y : o.y;
+      o.z     = (keep & 4u) ? v.z : o.z;
+      o.w     = (keep & 8u) ? v.w : o.w;
+      d4[i]   = o;
+    }
+  }
+}
+
 } // namespace
+
+extern "C" int srsgpu_merge_spans(const srsgpu_copy_span* d_spans,
+                                  uint32_t                nof_spans,
+                                  uint64_t                max_bytes,
+                                  uint32_t                sentinel,
+                                  void*                   stream)
+{
+  if ((d_spans == nullptr && nof_spans > 0) || (max_bytes & 15u) != 0) {
+    return srsgpu::fail(SRSGPU_ERR_INVALID_ARG, "srsgpu_merge_spans: invalid argument (max_bytes a multiple of 16)");
+  }
+  if (nof_spans == 0 || max_bytes == 0) {
+    return SRSGPU_OK;
+  }
+  const uint64_t blocks = std::min<uint64_t>(256, (max_bytes / 16u + 255u) / 256u);
+  merge_spans_kernel<<<dim3(static_cast<unsigned>(blocks), nof_spans), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      d_spans, sentinel);
+  const hipError_t err = hipGetLastError();
+  return err == hipSuccess ? SRSGPU_OK : srsgpu::fail(SRSGPU_ERR_HIP, "srsgpu_merge_spans: %s", hipGetErrorString(err));
+}
 
 extern "C" int srsgpu_copy_spans(const srsgpu_copy_span* d_spans, uint32_t nof_spans, uint64_t max_bytes, void* stream)
 {

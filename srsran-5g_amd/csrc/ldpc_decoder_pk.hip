@@ -276,14 +276,22 @@ __device__ __forceinline__ void row_update_pk(int8_t* __restrict__ soft,
     asm volatile("" : "+v"(z2x2_b));
   }
   s16x2 c_even = ss(0);  // C2V: the c2v of the row's last even edge, packed with the next one
+  // C2V: min1 / min2 signed once per layer by the sign of the product of all edges, so that an edge's c2v is its
+  // magnitude times its own v2c sign (the product of the others' signs): no per-edge parity term.
+  s16x2 M2s = ss(0), DMs = ss(0);
+  if constexpr (C2V) {
+    const s16x2 sall = as_s16(bits(as_s16(sx) >> ss(15)) | 0x00010001u);
+    M2s              = as_s16(bits(S2N)) * sall;
+    DMs              = as_s16(bits(S1N)) * sall - M2s;
+  }
   static_for<deg>([&](auto E) {
     constexpr int e   = decltype(E)::value;
     constexpr int col = G::col(e0 + e);
     const s16x2   v   = v2c[e];
     // c2v sign = product of the other edges' signs; magnitude min2 at the argmin, min1 elsewhere.
-    const s16x2 n   = as_s16(sx ^ bits(v)) >> ss(15);
+    const s16x2 n   = C2V ? (v >> ss(15)) : (as_s16(sx ^ bits(v)) >> ss(15));
     const u16x2 ne  = not_argmin(IDXN, e, one);
-    const u16x2 mag = ne * DN + S2N;
+    const u16x2 mag = C2V ? as_u16(bits(as_s16(bits(ne)) * DMs + M2s)) : ne * DN + S2N;
     // c2v + v2c as one multiply-add on the sign +/-1 (n | 1).
     const s16x2 sgn = as_s16(bits(n) | 0x00010001u);
     // Promotion sum (log_likelihood_ratio.cpp:75): |sum| > LLR_MAX becomes +/-infinity (SOFT_INF).

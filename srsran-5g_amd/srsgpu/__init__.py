@@ -404,6 +404,8 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_ofdm_jobs_execute.argtypes = [P, P, ctypes.c_uint32, P, P, P]
     lib.srsgpu_ofdm_jobs_execute_direct.argtypes = [P, P, ctypes.c_uint32, P]
     lib.srsgpu_copy_spans.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64, P]
+    if hasattr(lib, "srsgpu_merge_spans"):  # (libraries built before round 6 lack it: A/B runs of older builds)
+        lib.srsgpu_merge_spans.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, P]
     lib.srsgpu_ofdm_plan_sample_offset.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     lib.srsgpu_ofdm_plan_sample_offset.restype = ctypes.c_uint64
     lib.srsgpu_ofdm_modulator_plan_execute.argtypes = [P, P, P, P]
@@ -436,7 +438,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_modulator_symbols_plan_create", "srsgpu_ofdm_demodulator_symbols_plan_create", "srsgpu_harq_copy",
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
     "srsgpu_ofdm_plan_concat", "srsgpu_ofdm_plan_nof_grid_words", "srsgpu_ofdm_plan_get_jobs",
-    "srsgpu_ofdm_jobs_execute", "srsgpu_ofdm_jobs_execute_direct", "srsgpu_copy_spans",
+    "srsgpu_ofdm_jobs_execute", "srsgpu_ofdm_jobs_execute_direct", "srsgpu_copy_spans", "srsgpu_merge_spans",
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
     "srsgpu_pusch_demodulator_plan_execute", "srsgpu_pusch_demodulator_plan_destroy",
     "srsgpu_pusch_demodulator_plan_create_ex", "srsgpu_pusch_demodulator_plan_execute_ex",
@@ -487,6 +489,14 @@ def copy_spans(spans, stream=None):
     d, nbytes = span_list(spans)
     _check(_lib.srsgpu_copy_spans(_dptr(d), len(spans), int(nbytes.max()), _stream_handle(stream)))
     return d  # keep alive until the stream has run the copies
+
+
+def merge_spans(spans, sentinel=0xFFFFFFFF, stream=None):
+    """srsgpu_merge_spans: as copy_spans, but a 32-bit source word replaces the destination's only when it is not
+    `sentinel` (the multi-device PDSCH batch's gather of sentinel-filled shard grids)."""
+    d, nbytes = span_list(spans)
+    _check(_lib.srsgpu_merge_spans(_dptr(d), len(spans), int(nbytes.max()), int(sentinel), _stream_handle(stream)))
+    return d
 
 
 def _dptr(t) -> int:

@@ -117,6 +117,7 @@ UL_FLOATS = ("ldpc_mean", "sinr_db", "evm", "ta_s", "cfo_hz", "epre_db", "rsrp_d
 UL_CPU, UL_GPU_BATCH = 0, 1
 UL_INTERPOLATE, UL_ASYNC = 2, 4  # variant bits: estimator time strategy, asynchronous batch completion
 UL_MULTI_COPY, UL_MULTI_RCCL = 8, 16  # multi-GPU batch: 3 UE shards on one device (peer copies) / RCCL world size 1
+# (UL_MULTI_COPY also makes the DL batch three PDSCH shards on one device, merged into the root's grid)
 DL_CPU, DL_GPU_BATCH = 0, 1
 
 
@@ -140,6 +141,7 @@ class UpperPhy:
         L.chain_dl_slot.restype = ctypes.c_int
         L.chain_dl_slot.argtypes = [_P, ctypes.c_uint, ctypes.c_int, PP, _P, _P, _P, _P]
         L.chain_multi_transfer_counters.argtypes = [_P]
+        L.chain_pdsch_transfer_counters.argtypes = [_P]
         self.P, self.grid_prb = nof_ports, grid_prb
         self.ul = L.chain_ul_create(device, variant, nof_ports, grid_prb, max_iter)
         self.dl = L.chain_dl_create(device, variant, nof_ports, grid_prb)
@@ -150,6 +152,12 @@ class UpperPhy:
         out = np.zeros(3, np.uint64)
         self.lib.chain_multi_transfer_counters(_ptr(out))
         return dict(zip(("host_uploads", "shard_copies", "shard_bytes"), (int(v) for v in out)))
+
+    def pdsch_transfer_counters(self):
+        """Process-wide grid transfers of the PDSCH slot batches (chain_pdsch_transfer_counters)."""
+        out = np.zeros(3, np.uint64)
+        self.lib.chain_pdsch_transfer_counters(_ptr(out))
+        return dict(zip(("grid_downloads", "shard_merges", "merge_bytes"), (int(v) for v in out)))
 
     def close(self):
         if self.ul:

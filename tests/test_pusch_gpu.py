@@ -413,6 +413,28 @@ def test_copy_spans():
         srsgpu.copy_spans([(srcs[0][:8], dsts[0][:8])])
 
 
+def test_merge_spans():
+    """srsgpu_merge_spans (the multi-device PDSCH batch's gather): every destination word whose source word is not the
+    sentinel takes the source's, the others keep their value; vectors of four sentinel words, of none and mixed ones."""
+    import torch
+    import srsgpu
+    srsgpu.Context(0)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(9)
+    n = 3276 * 4
+    src = torch.randint(0, 2 ** 31 - 1, (3, n), dtype=torch.int64, generator=g).to(torch.int32)
+    sentinel = -1  # 0xffffffff
+    src[0, : n // 2] = sentinel                          # whole vectors of sentinels
+    src[1, torch.randperm(n, generator=g)[: n // 3]] = sentinel  # mixed vectors
+    dst = torch.randint(0, 2 ** 31 - 1, (3, n), dtype=torch.int64, generator=g).to(torch.int32)
+    want = torch.where(src != sentinel, src, dst)
+    s_d, d_d = src.to(dev), dst.to(dev)
+    keep = srsgpu.merge_spans([(s_d[i], d_d[i]) for i in range(3)])
+    torch.cuda.synchronize()
+    del keep
+    assert torch.equal(d_d.cpu(), want)
+
+
 def test_pusch_decoder_harq_in_arena(orc, ctx):
     """srsgpu_pusch_decoder_plan_execute_arena (each codeblock's HARQ soft buffer in a slot of a scattered, garbage-
     initialised arena, addressed through a per-codeblock pointer table) equals srsgpu_pusch_decoder_plan_execute over a

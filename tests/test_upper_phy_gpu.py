@@ -34,7 +34,8 @@ P = 4
 def procs(request):
     """The reference's CPU processors and the GPU batches, the latter completing synchronously (the PUSCH task returns
     with the results notified), asynchronously (results notified from the GPU service's completion thread), or as the
-    multi-GPU batch of row b7: the slot's UEs sharded by RNTI over the device list {0, 0, 0} (three shards with their
+    multi-GPU batch of row b7 (and its DL counterpart, the PDSCH slot batch over the same three shards): the slot's UEs
+    sharded by RNTI over the device list {0, 0, 0} (three shards with their
     own launch plans, HARQ arenas and grid copies on one GPU, results gathered by peer copies; synchronous, or
     asynchronous with the replay on the batch's completion thread) or over {0} with the RCCL transport (world size 1:
     the gather is an ncclSend / ncclRecv pair in one group). Every mode must equal the reference's CPU processors,
@@ -253,8 +254,17 @@ def test_downlink_processor_gpu_batch_equals_reference(procs):
     other = bf16((rng.normal(size=(P, 14, 12 * 273)) + 1j * rng.normal(size=(P, 14, 12 * 273))) * 0.1)
     for slot in (3, 4):
         ref = cpu.dl_slot(slot, pdus, weights, tbs, other)
+        before = gpu.pdsch_transfer_counters()
         got = gpu.dl_slot(slot, pdus, weights, tbs, other)
+        after = gpu.pdsch_transfer_counters()
         assert np.array_equal(ref, got), (slot, int(np.sum(np.any(ref != got, axis=-1))))
+        # One device-to-host grid transfer per slot whatever the number of devices; with three PDSCH shards (RNTI mod 3)
+        # the two non-root ones merge only their UEs' subcarrier bands into the root's grid.
+        assert after["grid_downloads"] - before["grid_downloads"] == 1, (before, after)
+        if gpu.mode.startswith("multi3"):
+            assert after["shard_merges"] - before["shard_merges"] == 2, (before, after)
+            moved = after["merge_bytes"] - before["merge_bytes"]
+            assert 0 < moved < 2 * P * 14 * 12 * 273 * 4, moved
         assert np.mean(np.any(ref != other, axis=-1)) > 0.3  # the PDSCHs were written
         assert np.array_equal(ref[:, :2], other[:, :2])  # symbols 0-1 (another channel's) untouched
 

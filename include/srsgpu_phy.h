@@ -479,7 +479,9 @@ int srsgpu_ofdm_jobs_execute(const srsgpu_ofdm_plan* plan,
 
 /** An OFDM job with absolute device addresses: the grid row (12 * bw_rb uint32 bf16 pairs) and the first sample of
  *  the symbol's cyclic prefix, each anywhere device-accessible — HBM, or host memory mapped for the device — so the
- *  caller's own buffers (a resource grid's rows, a radio buffer) are read or written in place. */
+ *  caller's own buffers (a resource grid's rows, a radio buffer) are read or written in place. grid_copy (demodulation
+ *  only, 0: none): a second row the same subcarriers are written to — the HBM copy of a mapped uplink grid that the
+ *  PUSCH slot batch on the same GPU reads instead of fetching the host grid back over PCIe. */
 typedef struct {
   uint64_t grid;
   uint64_t samples;
@@ -487,6 +489,7 @@ typedef struct {
   float    coef_re;
   float    coef_im;
   uint32_t reserved;
+  uint64_t grid_copy;
 } srsgpu_ofdm_direct_job;
 
 /** srsgpu_ofdm_jobs_execute over direct-address jobs (same launch parameters, same restrictions): the lower PHY's

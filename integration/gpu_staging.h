@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstring>
 #include <list>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <string>
@@ -282,6 +283,36 @@ public:
     return reinterpret_cast<void*>(it->second.second + (a - it->first));
   }
 
+  /// An HBM twin of a registered block (the PUSCH slot batch's HBM slot of its uplink processor's grid, same layout):
+  /// a writer that fills the block from the GPU (the lower PHY's demodulation) writes the twin too and sets one bit
+  /// per OFDM symbol in `symbols`; the owner, which would otherwise copy the block to its twin over PCIe, skips the
+  /// copy when every symbol's bit is set, and clears them.
+  struct twin {
+    uint8_t*               dev     = nullptr;
+    size_t                 bytes   = 0;
+    std::atomic<uint32_t>* symbols = nullptr;
+  };
+  static void set_twin(const void* base, const twin& t)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    r.twins[reinterpret_cast<uintptr_t>(base)] = t;
+  }
+  static void remove_twin(const void* base)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    r.twins.erase(reinterpret_cast<uintptr_t>(base));
+  }
+  /// The twin of the block that starts at base, if any (dev == nullptr: none).
+  static twin find_twin(const void* base)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    auto                        it = r.twins.find(reinterpret_cast<uintptr_t>(base));
+    return it == r.twins.end() ? twin() : it->second;
+  }
+
 private:
   static host_blocks& get()
   {
@@ -290,6 +321,7 @@ private:
   }
   std::mutex                                                 mtx;
   std::map<uintptr_t, std::pair<size_t, uintptr_t>>          blocks;  ///< base -> (bytes, device address)
+  std::map<uintptr_t, twin>                                  twins;   ///< base -> HBM twin
 };
 
 } // namespace gpu

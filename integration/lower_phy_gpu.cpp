@@ -283,6 +283,7 @@ public:
   struct direct_rows {
     uint8_t* row0        = nullptr;
     size_t   port_stride = 0;
+    uint8_t* twin0       = nullptr;  ///< the same rows of the grid's HBM twin (gpu::host_blocks::twin), or nullptr
   };
 
   /// The entry's input for position `pos` is in place; rows: its demodulated rows' destination (default: the entry's
@@ -490,9 +491,14 @@ private:
       for (const srsgpu_ofdm_job& jb : sectors[pe.sector].templates[pe.pos]) {
         srsgpu_ofdm_direct_job& d = jobs[n++];
         d.grid                    = reinterpret_cast<uint64_t>(grid_dev + static_cast<size_t>(jb.grid_offset) * 4);
+        d.grid_copy = 0;
         if (!inverse && pe.rows.row0 != nullptr) {
           // the templates' rows are [port][symbol - first] of one symbol: row = port
-          d.grid = reinterpret_cast<uint64_t>(pe.rows.row0 + (jb.grid_offset / sectors[pe.sector].row_words) * pe.rows.port_stride);
+          const size_t port = jb.grid_offset / sectors[pe.sector].row_words;
+          d.grid            = reinterpret_cast<uint64_t>(pe.rows.row0 + port * pe.rows.port_stride);
+          if (pe.rows.twin0 != nullptr) {
+            d.grid_copy = reinterpret_cast<uint64_t>(pe.rows.twin0 + port * pe.rows.port_stride);
+          }
         }
         d.samples  = reinterpret_cast<uint64_t>(samp_dev + static_cast<size_t>(jb.sample_offset) * sizeof(cf_t));
         d.cp_len   = jb.cp_len;
@@ -1058,9 +1064,15 @@ private:
       }
       ofdm_batcher::direct_rows rows;
       if (grid_dev != nullptr) {
-        rows = {grid_dev + static_cast<size_t>(l) * nsc * sizeof(uint32_t), grid_port_stride};
+        const size_t off = static_cast<size_t>(l) * nsc * sizeof(uint32_t);
+        rows             = {grid_dev + off, grid_port_stride, twin.dev != nullptr ? twin.dev + off : nullptr};
       }
       group->submit(sector, e, s, rows);
+      if (grid_dev != nullptr && twin.dev != nullptr) {
+        // The symbol goes to the twin too; the PUSCH batch copies nothing for a slot whose 14 symbols all did (the
+        // launch is queued before this symbol's notification, which precedes the uplink processor's PUSCH job).
+        twin.symbols->fetch_or(1u << l, std::memory_order_acq_rel);
+      }
       pending.push_back({l, context, e});
       if (l == geo.nsymb - 1) {
         drain(0);
@@ -1194,6 +1206,11 @@ private:
     }
     grid_dev         = static_cast<uint8_t*>(gpu::host_blocks::find(base, nof_ports * nsymb * row));
     grid_port_stride = nsymb * row;
+    // The HBM twin only when it has the grid's exact shape (the PUSCH batch's grid slot: [port][14][subcarrier]).
+    twin = gpu::host_blocks::find_twin(base);
+    if (grid_dev == nullptr || nsymb != 14 || geo.nsymb != 14 || twin.bytes != nof_ports * nsymb * row) {
+      twin = {};
+    }
   }
 
   std::shared_ptr<lower_phy_sector_group>    group_owner;
@@ -1216,6 +1233,7 @@ private:
   shared_resource_grid                       current_grid;
   uint8_t*                                   grid_dev         = nullptr;  ///< find_grid_rows
   size_t                                     grid_port_stride = 0;
+  gpu::host_blocks::twin                     twin;  ///< find_grid_rows: the grid's HBM twin (dev nullptr: none)
   request_ring<shared_resource_grid>         requests;
 };
 

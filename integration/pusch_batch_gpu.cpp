@@ -105,6 +105,7 @@ namespace {
 /// Process-wide grid transfer counts of the multi-device UL batches (get_pusch_multi_transfer_counters).
 struct {
   std::atomic<uint64_t> host_uploads{0}, shard_copies{0}, shard_bytes{0};
+  std::atomic<uint64_t> twin_grids{0};  ///< single-device slots whose grid the lower PHY had written into HBM
 } multi_transfers;
 
 /// One registered PUSCH transmission and where its results are in its launch.
@@ -697,6 +698,10 @@ private:
   size_t                               host_grid_size = 0;
   const void*                          host_grid_dev  = nullptr;
   bool                                 host_grid_off  = false;  ///< registration failed once: copy from now on
+  /// The grid's HBM twin (host_blocks::twin): the batch's grid slot, announced once the host grid is registered; the
+  /// lower PHY sets a bit per symbol it demodulated into both, and a slot with all of them set copies nothing.
+  bool                                 twin_announced = false;
+  std::atomic<uint32_t>                twin_symbols{0};
   unsigned                             batch_id   = 0;
   int                                  grid_slot  = -1;
   unsigned                             grid_P     = 0;
@@ -1760,9 +1765,11 @@ void pusch_slot_batch::release_host_grid()
   std::lock_guard<std::mutex> lock(run_mtx);
   if (host_grid != nullptr) {
     device_scope dev(ctx, WHO);
+    host_blocks::remove_twin(host_grid);
     host_blocks::remove(host_grid);
-    host_grid     = nullptr;
-    host_grid_dev = nullptr;
+    host_grid      = nullptr;
+    host_grid_dev  = nullptr;
+    twin_announced = false;
   }
 }
 
@@ -1788,9 +1795,11 @@ const void* pusch_slot_batch::grid_in_place(const resource_grid_reader& grid, un
     }
     device_scope dev(ctx, WHO);
     if (host_grid != nullptr) {
+      host_blocks::remove_twin(host_grid);
       host_blocks::remove(host_grid);
-      host_grid     = nullptr;
-      host_grid_dev = nullptr;
+      host_grid      = nullptr;
+      host_grid_dev  = nullptr;
+      twin_announced = false;
     }
     const void* d = host_blocks::add(base, bytes);
     if (d == nullptr) {
@@ -2171,6 +2180,17 @@ void pusch_slot_batch::run(std::vector<pusch_entry>& all)
       }
     }
     grid_src = grid_map.dev();
+  } else if (host_grid != nullptr && grid_src == host_grid_dev) {
+    // du_low with the lower PHY on this GPU: the sector group demodulates every symbol into the grid and into its
+    // HBM twin (this batch's grid slot); when it did for all 14 symbols of this slot, the slot copies nothing.
+    if (!twin_announced) {
+      host_blocks::set_twin(host_grid, {reinterpret_cast<uint8_t*>(d_grid), gbytes, &twin_symbols});
+      twin_announced = true;
+    }
+    if (twin_symbols.exchange(0, std::memory_order_acq_rel) == (1u << 14) - 1u) {
+      grid_src = nullptr;
+      multi_transfers.twin_grids.fetch_add(1, std::memory_order_relaxed);
+    }
   }
 
   job->batch     = this;
@@ -2395,7 +2415,7 @@ void pusch_slot_batch::multi_complete_loop()
 pusch_multi_transfer_counters get_pusch_multi_transfer_counters()
 {
   return {multi_transfers.host_uploads.load(), multi_transfers.shard_copies.load(),
-          multi_transfers.shard_bytes.load()};
+          multi_transfers.shard_bytes.load(), multi_transfers.twin_grids.load()};
 }
 
 namespace {

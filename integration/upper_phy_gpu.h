@@ -122,6 +122,9 @@ struct pusch_multi_transfer_counters {
   uint64_t host_uploads = 0;
   uint64_t shard_copies = 0;
   uint64_t shard_bytes  = 0;
+  /// Single-device slots whose rx grid was already in HBM: the lower PHY's sector group demodulated every symbol into
+  /// the uplink grid and its HBM twin (the batch's grid slot), so the slot read nothing back over PCIe.
+  uint64_t twin_grids = 0;
 };
 pusch_multi_transfer_counters get_pusch_multi_transfer_counters();
 

@@ -1646,14 +1646,16 @@ void chain_ul_destroy(void* p)
   delete static_cast<ul_harness*>(p);
 }
 
-/// Process-wide grid transfer counts of the multi-device UL batches (gpu::get_pusch_multi_transfer_counters): out[0]
-/// host-to-device grid uploads, out[1] root-to-shard copy launches, out[2] bytes those copies moved.
+/// Process-wide grid transfer counts of the UL batches (gpu::get_pusch_multi_transfer_counters): out[0] host-to-device
+/// grid uploads of multi-device batches, out[1] root-to-shard copy launches, out[2] bytes those copies moved, out[3]
+/// single-device slots whose grid the lower PHY had written into its HBM twin.
 void chain_multi_transfer_counters(uint64_t* out)
 {
   const gpu::pusch_multi_transfer_counters c = gpu::get_pusch_multi_transfer_counters();
   out[0]                                     = c.host_uploads;
   out[1]                                     = c.shard_copies;
   out[2]                                     = c.shard_bytes;
+  out[3]                                     = c.twin_grids;
 }
 
 /// Process-wide grid transfer counts of the PDSCH slot batches (gpu::get_pdsch_multi_transfer_counters): out[0]

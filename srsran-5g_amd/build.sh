@@ -17,7 +17,9 @@ for src in "${SRCS[@]}"; do
   if [ ! -f "$obj" ] || [ "$src" -nt "$obj" ] || [ "$newest_hdr" -nt "$obj" ] || [ "$0" -nt "$obj" ]; then
     # The demodulator's complex arithmetic is scalar f32: SLP packing into v_pk_* costs moves and ~40 VGPRs there.
     extra=""
-    [[ "$(basename "$src")" == pusch_demodulator.hip ]] && extra="-fno-slp-vectorize"
+    # The OFDM kernels likewise: the two-wave 4096-point transform spills under SLP at its 128-VGPR bound, and the
+    # one-wave-per-16-points kernels take fewer VGPRs without it (74 vs 92 at 2048 points).
+    [[ "$(basename "$src")" == pusch_demodulator.hip || "$(basename "$src")" == ofdm.hip ]] && extra="-fno-slp-vectorize"
     if [[ "$src" == *.hip ]]; then
       $HIPCC $FLAGS $extra -x hip -c "$src" -o "$obj" &
     else

@@ -26,7 +26,6 @@
 namespace srsgpu {
 namespace {
 
-#define OFDM_OCCUPANCY
 
 // cos / sin (2 pi k / 16).
 __device__ constexpr float kCos16[16] = {1.0f,          0.92387953251f,  0.70710678118f,  0.38268343236f,
@@ -373,11 +372,140 @@ __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ 
   }
 }
 
+/// 4096 points on two waves (128 threads, two radix-16 butterflies per thread and pass, j0 = tid and j1 = tid + 128)
+/// through a 16 KB LDS buffer. The one-butterfly transform holds the 4096-point block in 32 KB of LDS and at 92 VGPRs
+/// runs 5 four-wave workgroups per CU: 5 symbols in flight per CU, and each waits out its HBM loads, barriers and
+/// stores in lockstep with the others. Here a symbol takes two waves and 16 KB, so 8 symbols are in flight per CU
+/// (4 waves per SIMD), each thread with two independent butterflies. The Stockham index maps put butterfly j0's outputs
+/// of passes 1 and 2 into the first half of the 4096 points and j1's into the second, and each pass reads inputs
+/// j + 256 r, r < 8 from the first half and r >= 8 from the second: every exchange runs as write half A, read the A
+/// inputs, write half B, read the B inputs, with the same 2048-entry buffer.
+template <int S, typename Src, typename Dst>
+__device__ __forceinline__ void dft4096_two_waves(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
+{
+  constexpr int T = 128, H = 2048;
+  const int     tid = static_cast<int>(threadIdx.x);
+  // Pass bases: NS = 16 (k = j mod 16, the same for both butterflies), NS = 256 (k = j: j1's base loaded apart).
+  const float2 b1  = twiddle_base<16, S>(tw);
+  const float2 b2a = twiddle_base<256, S>(tw);
+  float2       b2b = tw[(tid + T) * static_cast<int>(OFDM_MAX_DFT / (256 * 16))];
+  if constexpr (S > 0) {
+    b2b.y = -b2b.y;
+  }
+  // a: butterfly j0's values, c: j1's. Each exchange frees one set before the reads that refill it, so that at most
+  // 32 complex values are live: write j0's outputs (half A), read every butterfly's inputs r < 8 into a (j0's into
+  // a[0..7], j1's into a[8..15]), then compute / write j1's (half B) and read the inputs r >= 8 into c likewise;
+  // the next pass's butterflies are {a[0..7], c[0..7]} and {a[8..15], c[8..15]}, regrouped by renaming.
+  float2 a[16], c[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    a[r] = src_first(tid + r * 256);
+  }
+  auto regroup = [&]() {
+    float2 t[16];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      t[r]     = a[8 + r];
+      t[8 + r] = c[8 + r];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      a[8 + r] = c[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      c[r] = t[r];
+    }
+  };
+  // One pass with its exchange: twiddles (pass 2), DFT and half-A write of j0, reads r < 8, DFT and half-B write of
+  // j1, reads r >= 8; dst_index(b, r) is the pass's output position of butterfly j_b's value r.
+  auto pass_exchange = [&](auto twiddle0, auto twiddle1, auto dst_index, auto fetch1) {
+    twiddle0(a);
+    dft_reg<16, S>(a);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      lds[dst_index(0, r)] = a[r];
+    }
+    fetch1();  // pass 1: j1's HBM inputs, in flight across the half-A exchange
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      a[r]     = lds[tid + r * 256];
+      a[8 + r] = lds[tid + T + r * 256];
+    }
+    __syncthreads();
+    twiddle1(c);
+    dft_reg<16, S>(c);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      lds[dst_index(1, r) - H] = c[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      c[r]     = lds[tid + r * 256];
+      c[8 + r] = lds[tid + T + r * 256];
+    }
+    regroup();
+  };
+  auto none = [](float2 (&)[16]) {};
+  // Pass 1 (radix 16, no twiddles): butterfly j takes x[j + 256 r] and writes X[16 j + r].
+  pass_exchange(none, none, [&](int b, int r) { return (tid + b * T) * 16 + r; }, [&]() {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      c[r] = src_first(tid + T + r * 256);
+    }
+  });
+  // Pass 2 (NS = 16): butterfly j, k = j mod 16, writes X[(j - k) 16 + k + 16 r] = X[256 (j / 16) + k + 16 r].
+  __syncthreads();  // the previous exchange's B reads are done before the buffer is written again
+  auto tw1 = [&](float2 (&v)[16]) { twiddle16(v, b1); };
+  pass_exchange(
+      tw1, tw1,
+      [&](int b, int r) {
+        const int j = tid + b * T;
+        return (j >> 4) * 256 + (j & 15) + 16 * r;
+      },
+      []() {});
+  // Pass 3 (NS = 256): butterfly j (k = j) writes X[j + 256 r] to HBM. An opaque copy of the thread index keeps the
+  // output addressing here (hoisted to the kernel start, it spilled).
+  int tid3 = tid;
+  asm volatile("" : "+v"(tid3));
+  twiddle16(a, b2a);
+  dft_reg<16, S>(a);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    dst_last(tid3 + 256 * r, a[r]);
+  }
+  twiddle16(c, b2b);
+  dft_reg<16, S>(c);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    dst_last(tid3 + T + 256 * r, c[r]);
+  }
+}
+
+/// Threads per workgroup of the N-point kernels (the two-wave 4096-point transform uses 128).
+template <int N>
+constexpr int ofdm_kernel_threads()
+{
+  return N == 4096 ? 128 : ofdm_threads<N>();
+}
+
+/// Minimum waves per SIMD the N-point kernels are compiled for (the two-wave 4096-point one: 8 workgroups per CU, at
+/// most 128 VGPRs; the others: the compiler's choice).
+template <int N>
+constexpr int ofdm_min_waves()
+{
+  return N == 4096 ? 4 : 1;
+}
+
 /// Any supported N: the power-of-two or the 3 x 2^m decomposition.
 template <int N, int S, typename Src, typename Dst>
 __device__ __forceinline__ void dft_any(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
 {
-  if constexpr (is_pow2(N)) {
+  if constexpr (N == 4096) {
+    dft4096_two_waves<S>(lds, tw, src_first, dst_last);
+  } else if constexpr (is_pow2(N)) {
     dft_lds<ilog2(N), S>(lds, tw, src_first, dst_last);
   } else {
     dft_lds3<N, S>(lds, tw, src_first, dst_last);
@@ -397,6 +525,7 @@ struct job_ref {
   float2*   samples;
   uint32_t  cp;
   float2    coef;
+  uint32_t* grid_copy;  ///< demodulation: a second destination row (nullptr: none)
 };
 
 /// Jobs as offsets into one grid buffer and one sample buffer (plans and srsgpu_ofdm_jobs_execute).
@@ -406,8 +535,15 @@ struct offset_jobs {
   float2*         samples;
   __device__ __forceinline__ job_ref get(unsigned b) const
   {
-    const ofdm_job j = jobs[b];
-    return {grid + j.grid_offset, samples + j.sample_offset, j.cp_len, make_float2(j.coef_re, j.coef_im)};
+    // The job is the workgroup's (b = blockIdx.x): its offsets in SGPRs, so that every grid load and sample store
+    // addresses the kernel-argument base plus a 32-bit offset (the compiler cannot prove the loaded fields uniform).
+    const ofdm_job j    = jobs[b];
+    const uint32_t goff = __builtin_amdgcn_readfirstlane(j.grid_offset);
+    const uint32_t soff = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(j.sample_offset));
+    return {grid + goff, samples + soff, static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(j.cp_len)),
+            make_float2(__uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(j.coef_re))),
+                        __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(j.coef_im)))),
+            nullptr};
   }
 };
 
@@ -418,16 +554,16 @@ struct direct_jobs {
   {
     const srsgpu_ofdm_direct_job j = jobs[b];
     return {reinterpret_cast<uint32_t*>(j.grid), reinterpret_cast<float2*>(j.samples), j.cp_len,
-            make_float2(j.coef_re, j.coef_im)};
+            make_float2(j.coef_re, j.coef_im), reinterpret_cast<uint32_t*>(j.grid_copy)};
   }
 };
 
 template <int N, typename JS>
-__global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_modulate_kernel(JS js,
-                                                                                       uint32_t nsc,
-                                                                                       const float2* __restrict__ tw)
+__global__ __launch_bounds__(ofdm_kernel_threads<N>(), ofdm_min_waves<N>()) void ofdm_modulate_kernel(JS js,
+                                                                                              uint32_t nsc,
+                                                                                              const float2* __restrict__ tw)
 {
-  __shared__ float2   lds[N];
+  __shared__ float2   lds[N == 4096 ? N / 2 : N];
   const job_ref       jb   = js.get(blockIdx.x);
   const int           half = static_cast<int>(nsc / 2);
   const uint32_t*     row  = jb.grid;
@@ -459,19 +595,20 @@ __global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_modulat
 }
 
 template <int N, typename JS>
-__global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_demodulate_kernel(JS js,
-                                                                                         uint32_t nsc,
-                                                                                         uint32_t window_offset,
-                                                                                         const float2* __restrict__ tw)
+__global__ __launch_bounds__(ofdm_kernel_threads<N>(), ofdm_min_waves<N>()) void ofdm_demodulate_kernel(JS js,
+                                                                                                uint32_t nsc,
+                                                                                                uint32_t window_offset,
+                                                                                                const float2* __restrict__ tw)
 {
-  __shared__ float2 lds[N];
+  __shared__ float2 lds[N == 4096 ? N / 2 : N];
   const job_ref     jb   = js.get(blockIdx.x);
   const int         half = static_cast<int>(nsc / 2);
   const float2*     x    = jb.samples + jb.cp - window_offset;
   auto              src  = [x](int n) { return x[n]; };
   const float2      coef = jb.coef;
   uint32_t*         row  = jb.grid;
-  auto dst = [row, coef, half, tw, window_offset](int b, float2 v) {
+  uint32_t*         row2 = jb.grid_copy;
+  auto dst = [row, row2, coef, half, tw, window_offset](int b, float2 v) {
     int sc = -1;
     if (b < half) {
       sc = half + b;
@@ -485,7 +622,11 @@ __global__ __launch_bounds__(ofdm_threads<N>()) OFDM_OCCUPANCY void ofdm_demodul
     if (window_offset != 0) {  // times exp(+j 2 pi offset b / N)
       y = cmul(y, twiddle_any<N, +1>(tw, (window_offset * static_cast<uint32_t>(b)) % N));
     }
-    row[sc] = bf16_bits(y.x) | (bf16_bits(y.y) << 16);
+    const uint32_t w = bf16_bits(y.x) | (bf16_bits(y.y) << 16);
+    row[sc]          = w;
+    if (row2 != nullptr) {
+      row2[sc] = w;
+    }
   };
   dft_any<N, -1>(lds, tw, src, dst);
 }
@@ -641,7 +782,7 @@ template <int N, typename JS>
 void launch_one(bool inverse, JS js, int nof_jobs, uint32_t nsc, uint32_t window_offset, const float2* tw,
                 hipStream_t stream)
 {
-  constexpr int threads = ofdm_threads<N>();  // every thread takes part in the passes' barriers
+  constexpr int threads = ofdm_kernel_threads<N>();  // every thread takes part in the passes' barriers
   if (inverse) {
     hipLaunchKernelGGL((ofdm_modulate_kernel<N, JS>), dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0, stream,
                        js, nsc, tw);

@@ -1560,7 +1560,7 @@ class OfdmPlan:
                                              _stream_handle(stream)))
 
     OFDM_DIRECT_JOB = np.dtype([("grid", "<u8"), ("samples", "<u8"), ("cp_len", "<u4"), ("coef_re", "<f4"),
-                                ("coef_im", "<f4"), ("reserved", "<u4")])
+                                ("coef_im", "<f4"), ("reserved", "<u4"), ("grid_copy", "<u8")])
 
     def direct_jobs(self, d_grid, d_samples) -> np.ndarray:
         """The plan's jobs as srsgpu_ofdm_direct_job (OFDM_DIRECT_JOB) over the given grid and sample buffers."""

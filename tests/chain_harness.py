@@ -149,9 +149,9 @@ class UpperPhy:
 
     def multi_transfer_counters(self):
         """Process-wide grid transfers of the multi-device UL batches (chain_multi_transfer_counters)."""
-        out = np.zeros(3, np.uint64)
+        out = np.zeros(4, np.uint64)
         self.lib.chain_multi_transfer_counters(_ptr(out))
-        return dict(zip(("host_uploads", "shard_copies", "shard_bytes"), (int(v) for v in out)))
+        return dict(zip(("host_uploads", "shard_copies", "shard_bytes", "twin_grids"), (int(v) for v in out)))
 
     def pdsch_transfer_counters(self):
         """Process-wide grid transfers of the PDSCH slot batches (chain_pdsch_transfer_counters)."""

@@ -212,6 +212,10 @@ def test_ofdm_direct_jobs_equal_plans(ctx, inverse):
         grids.append((g if inverse else torch.zeros(m.grid_words, dtype=torch.int32)).to(dev))
         samples.append((torch.zeros(2 * m.nof_samples, dtype=torch.float32) if inverse else x).to(dev))
         jobs.append(m.direct_jobs(grids[-1], samples[-1]))
+    # Demodulation: the second member's rows also go to a copy (grid_copy: the HBM twin of a mapped uplink grid).
+    twin = torch.zeros(members[1].grid_words, dtype=torch.int32, device=dev)
+    if not inverse:
+        jobs[1]["grid_copy"] = jobs[1]["grid"] - np.uint64(srsgpu._dptr(grids[1])) + np.uint64(srsgpu._dptr(twin))
     jobs = np.concatenate(jobs)[::-1].copy()
     d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
     members[0].execute_jobs_direct(d_jobs, len(jobs))
@@ -225,6 +229,8 @@ def test_ofdm_direct_jobs_equal_plans(ctx, inverse):
             o = torch.zeros(m.grid_words, dtype=torch.int32, device=dev)
             m.execute(samples[i], o)
             assert torch.equal(o, grids[i]), i
+    if not inverse:
+        assert torch.equal(twin, grids[1])
     split = srsgpu.OfdmPlan(ctx, inverse, 1, 273, 12288, 1.0, 3.5e9, [0], 1, symbols=(0, 1))
     with pytest.raises(srsgpu.SrsGpuError):
         split.execute_jobs_direct(d_jobs, 1)

@@ -109,6 +109,12 @@ def main():
                    ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_uint] * 3 + [ctypes.c_int, ctypes.c_uint] +
                   [ctypes.c_void_p] * 4)
     ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    lib.chain_multi_transfer_counters.argtypes = [ctypes.c_void_p]
+
+    def twin_grids():
+        c = np.zeros(4, np.uint64)
+        lib.chain_multi_transfer_counters(ptr(c))
+        return int(c[3])
     n = sum(P * LH.symbol_size(1, DFT, False, s, l) for s in (0, 1) for l in range(14))
     rng = np.random.default_rng(5)
     samples = ((rng.normal(size=n) + 1j * rng.normal(size=n)) * 0.05).astype(np.complex64)
@@ -128,9 +134,11 @@ def main():
                     results = np.zeros((S, 2), np.int32)
                     secs = np.zeros(1, np.float64)
                     lat = np.zeros(8, np.float64)
+                    t0 = twin_grids()
                     r = f(0, S, args.slots, len(pdus), arr, ptr(tbb), ptr(samples), P, PRB, DFT,
                           1 if variant == "group" else 0, inflight, ptr(lag), ptr(results), ptr(secs), ptr(lat))
                     assert r == 0, r
+                    twins = twin_grids() - t0
                     notified = bool((results[:, 0] == args.slots * len(pdus)).all())
                     rt = bool(lag[:, 1].max() < 0.5e-3 and lag[:, 2].max() < 0.01 and notified)
                     res["by_sectors"][S] = {"max_lag_us": 1e6 * lag[:, 0].max(), "final_lag_us": 1e6 * lag[:, 1].max(),
@@ -139,7 +147,10 @@ def main():
                                             "seconds": float(secs[0]), "real_time": rt,
                                             # PUSCH result latency: end of the slot on the radio clock -> notification
                                             "latency_us": dict(zip(("p50", "p90", "p99", "max", "mean"), lat[:5])),
-                                            "over_5_slot_budget": float(lat[5])}
+                                            "over_5_slot_budget": float(lat[5]),
+                                            # slots whose rx grid the PUSCH launch found in HBM (written there by
+                                            # the sector group's demodulation): no PCIe read-back
+                                            "grids_from_hbm_twin": twins}
                     print(json.dumps({name: {variant: {inflight: {S: res["by_sectors"][S]}}}}), file=sys.stderr,
                           flush=True)
                 rts = [S for S, v in res["by_sectors"].items() if v["real_time"]]

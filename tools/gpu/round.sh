@@ -163,6 +163,17 @@ for step in "$@"; do
           head -2 "$OUT/ofdmab_${lib}_$i.txt"
         done
       done ;;
+    setsweep)
+      # the headline against the number of input sets in flight (bench.py --input-sets), two rounds
+      for i in 1 2; do
+        for n in 9 13 16 20 24; do
+          timeout -k 10 200 python -u bench.py --input-sets "$n" --no-cpu-baseline --no-extra-points \
+            --no-extra-workloads > "$OUT/setsweep_${n}_$i.json" 2> "$OUT/setsweep_${n}_$i.err" \
+            || { tail -20 "$OUT/setsweep_${n}_$i.err"; exit 1; }
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('sets', sys.argv[2], round(d['value']))" \
+            "$OUT/setsweep_${n}_$i.json" "$n"
+        done
+      done ;;
     ofdmsweep)
       # isolated OFDM launch time against the number of symbols per launch (slots x 4 ports x 14): the workgroup
       # rounds per CU show as steps in the time

@@ -484,26 +484,28 @@ __device__ __forceinline__ void dft4096_two_waves(float2* lds, const float2* __r
   }
 }
 
-/// Threads per workgroup of the N-point kernels (the two-wave 4096-point transform uses 128).
+/// Threads per workgroup of the N-point kernels of exponent sign S (the two-wave 4096-point transform, used by the
+/// modulator, 128; the 4096-point demodulator keeps four waves: two measured the bench equal and the isolated
+/// launch 10 % slower, profiles/r6n_ofdm_demod_waves_ab.txt).
 template <int N>
-constexpr int ofdm_kernel_threads()
+constexpr int ofdm_kernel_threads(int S)
 {
-  return N == 4096 ? 128 : ofdm_threads<N>();
+  return (N == 4096 && S > 0) ? 128 : ofdm_threads<N>();
 }
 
-/// Minimum waves per SIMD the N-point kernels are compiled for (the two-wave 4096-point one: 8 workgroups per CU, at
-/// most 128 VGPRs; the others: the compiler's choice).
+/// Minimum waves per SIMD the N-point kernels of sign S are compiled for (the two-wave 4096-point one: 8 workgroups
+/// per CU, at most 128 VGPRs; the others: the compiler's choice).
 template <int N>
-constexpr int ofdm_min_waves()
+constexpr int ofdm_min_waves(int S)
 {
-  return N == 4096 ? 4 : 1;
+  return (N == 4096 && S > 0) ? 4 : 1;
 }
 
 /// Any supported N: the power-of-two or the 3 x 2^m decomposition.
 template <int N, int S, typename Src, typename Dst>
 __device__ __forceinline__ void dft_any(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
 {
-  if constexpr (N == 4096) {
+  if constexpr (N == 4096 && S > 0) {
     dft4096_two_waves<S>(lds, tw, src_first, dst_last);
   } else if constexpr (is_pow2(N)) {
     dft_lds<ilog2(N), S>(lds, tw, src_first, dst_last);
@@ -559,7 +561,7 @@ struct direct_jobs {
 };
 
 template <int N, typename JS>
-__global__ __launch_bounds__(ofdm_kernel_threads<N>(), ofdm_min_waves<N>()) void ofdm_modulate_kernel(JS js,
+__global__ __launch_bounds__(ofdm_kernel_threads<N>(+1), ofdm_min_waves<N>(+1)) void ofdm_modulate_kernel(JS js,
                                                                                               uint32_t nsc,
                                                                                               const float2* __restrict__ tw)
 {
@@ -595,12 +597,12 @@ __global__ __launch_bounds__(ofdm_kernel_threads<N>(), ofdm_min_waves<N>()) void
 }
 
 template <int N, typename JS>
-__global__ __launch_bounds__(ofdm_kernel_threads<N>(), ofdm_min_waves<N>()) void ofdm_demodulate_kernel(JS js,
+__global__ __launch_bounds__(ofdm_kernel_threads<N>(-1), ofdm_min_waves<N>(-1)) void ofdm_demodulate_kernel(JS js,
                                                                                                 uint32_t nsc,
                                                                                                 uint32_t window_offset,
                                                                                                 const float2* __restrict__ tw)
 {
-  __shared__ float2 lds[N == 4096 ? N / 2 : N];
+  __shared__ float2 lds[N];  // (the two-wave 4096-point demodulation measured 10 % slower in isolation)
   const job_ref     jb   = js.get(blockIdx.x);
   const int         half = static_cast<int>(nsc / 2);
   const float2*     x    = jb.samples + jb.cp - window_offset;
@@ -782,7 +784,7 @@ template <int N, typename JS>
 void launch_one(bool inverse, JS js, int nof_jobs, uint32_t nsc, uint32_t window_offset, const float2* tw,
                 hipStream_t stream)
 {
-  constexpr int threads = ofdm_kernel_threads<N>();  // every thread takes part in the passes' barriers
+  const int threads = ofdm_kernel_threads<N>(inverse ? 1 : -1);  // every thread takes part in the passes' barriers
   if (inverse) {
     hipLaunchKernelGGL((ofdm_modulate_kernel<N, JS>), dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0, stream,
                        js, nsc, tw);

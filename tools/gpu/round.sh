@@ -70,6 +70,10 @@ for step in "$@"; do
       timeout -k 10 500 python -u tools/du_low_bench.py --direction ul --sectors 4,6,8 --variants group \
         --in-flight 13 > "$OUT/du_low_ul.json" 2> "$OUT/du_low_ul.log" || { tail -20 "$OUT/du_low_ul.log"; exit 1; }
       tail -c 1500 "$OUT/du_low_ul.json" ;;
+    dulowdl)
+      timeout -k 10 500 python -u tools/du_low_bench.py --direction dl --sectors 4,6,8 --variants alone,group \
+        > "$OUT/du_low_dl.json" 2> "$OUT/du_low_dl.log" || { tail -20 "$OUT/du_low_dl.log"; exit 1; }
+      tail -c 1500 "$OUT/du_low_dl.json" ;;
     slots_trace16)
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/trace16" -o slots -- python3 -u \
         tools/processor_bench.py --only-slots --threads 16 --repetitions 1 --slots 30 --directions ul \

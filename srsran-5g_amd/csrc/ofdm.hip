@@ -372,6 +372,14 @@ __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ 
   }
 }
 
+/// Swaps a value between lanes 2i and 2i + 1 (DPP quad permutation [1, 0, 3, 2]).
+__device__ __forceinline__ float2 swap_lane_pairs(float2 v)
+{
+  constexpr int QUAD_1032 = 1 | (0 << 2) | (3 << 4) | (2 << 6);
+  return make_float2(__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.x), QUAD_1032, 0xf, 0xf, false)),
+                     __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), QUAD_1032, 0xf, 0xf, false)));
+}
+
 /// 4096 points on two waves (128 threads, two radix-16 butterflies per thread and pass, j0 = tid and j1 = tid + 128)
 /// through a 16 KB LDS buffer. The one-butterfly transform holds the 4096-point block in 32 KB of LDS and at 92 VGPRs
 /// runs 5 four-wave workgroups per CU: 5 symbols in flight per CU, and each waits out its HBM loads, barriers and
@@ -380,8 +388,9 @@ __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ 
 /// of passes 1 and 2 into the first half of the 4096 points and j1's into the second, and each pass reads inputs
 /// j + 256 r, r < 8 from the first half and r >= 8 from the second: every exchange runs as write half A, read the A
 /// inputs, write half B, read the B inputs, with the same 2048-entry buffer.
-template <int S, typename Src, typename Dst>
-__device__ __forceinline__ void dft4096_two_waves(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
+template <int S, typename Src, typename DstPair>
+__device__ __forceinline__ void dft4096_two_waves(float2* lds, const float2* __restrict__ tw, Src src_first,
+                                                  DstPair dst_pair)
 {
   constexpr int T = 128, H = 2048;
   const int     tid = static_cast<int>(threadIdx.x);
@@ -467,21 +476,28 @@ __device__ __forceinline__ void dft4096_two_waves(float2* lds, const float2* __r
       },
       []() {});
   // Pass 3 (NS = 256): butterfly j (k = j) writes X[j + 256 r] to HBM. An opaque copy of the thread index keeps the
-  // output addressing here (hoisted to the kernel start, it spilled).
+  // output addressing here (hoisted to the kernel start, it spilled). Neighbouring lanes hold neighbouring points:
+  // for each pair r, r + 1 the even lane trades its X[j + 256 (r + 1)] for the odd lane's X[j + 1 + 256 r] (one DPP
+  // swap), so that every lane stores two consecutive points (16 bytes: half the store instructions of one point per
+  // lane, the stores being what the symbol's last phase waits on).
   int tid3 = tid;
   asm volatile("" : "+v"(tid3));
+  const bool odd  = (tid3 & 1) != 0;
+  const int  even = tid3 & ~1;
+  auto store_pairs = [&](float2 (&v)[16], int j) {
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const float2 send = odd ? v[r] : v[r + 1];
+      const float2 recv = swap_lane_pairs(send);
+      dst_pair(j + 256 * (odd ? r + 1 : r), odd ? recv : v[r], odd ? v[r + 1] : recv);
+    }
+  };
   twiddle16(a, b2a);
   dft_reg<16, S>(a);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    dst_last(tid3 + 256 * r, a[r]);
-  }
+  store_pairs(a, even);
   twiddle16(c, b2b);
   dft_reg<16, S>(c);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    dst_last(tid3 + T + 256 * r, c[r]);
-  }
+  store_pairs(c, even + T);
 }
 
 /// Threads per workgroup of the N-point kernels of exponent sign S (the two-wave 4096-point transform, used by the
@@ -501,13 +517,11 @@ constexpr int ofdm_min_waves(int S)
   return (N == 4096 && S > 0) ? 4 : 1;
 }
 
-/// Any supported N: the power-of-two or the 3 x 2^m decomposition.
+/// Any supported N: the power-of-two or the 3 x 2^m decomposition (the modulator's 4096 points: dft4096_two_waves).
 template <int N, int S, typename Src, typename Dst>
 __device__ __forceinline__ void dft_any(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
 {
-  if constexpr (N == 4096 && S > 0) {
-    dft4096_two_waves<S>(lds, tw, src_first, dst_last);
-  } else if constexpr (is_pow2(N)) {
+  if constexpr (is_pow2(N)) {
     dft_lds<ilog2(N), S>(lds, tw, src_first, dst_last);
   } else {
     dft_lds3<N, S>(lds, tw, src_first, dst_last);
@@ -569,31 +583,57 @@ __global__ __launch_bounds__(ofdm_kernel_threads<N>(+1), ofdm_min_waves<N>(+1)) 
   const job_ref       jb   = js.get(blockIdx.x);
   const int           half = static_cast<int>(nsc / 2);
   const uint32_t*     row  = jb.grid;
-  // Bin b < rg/2 carries subcarrier rg/2 + b, bin b >= N - rg/2 subcarrier b - (N - rg/2), the rest are zero.
+  // Bin b < rg/2 carries subcarrier rg/2 + b, bin b >= N - rg/2 subcarrier b - (N - rg/2), the rest are zero. The
+  // guard bins load subcarrier 0 and discard it (no branch per load; unsigned offsets from the row's SGPR base).
   auto src = [row, half](int b) {
-    int sc = -1;
-    if (b < half) {
-      sc = half + b;
-    } else if (b >= N - half) {
-      sc = b - (N - half);
-    }
-    if (sc < 0) {
-      return make_float2(0.f, 0.f);
-    }
-    const uint32_t u = row[sc];
+    const uint32_t ub    = static_cast<uint32_t>(b);
+    const bool     lower = ub < static_cast<uint32_t>(half);
+    const bool     upper = ub >= static_cast<uint32_t>(N - half);
+    const uint32_t sc    = lower ? ub + static_cast<uint32_t>(half) : (upper ? ub - static_cast<uint32_t>(N - half) : 0u);
+    uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(row) + sc * 4u);
+    u          = (lower || upper) ? u : 0u;
     return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
   };
   const float2 coef = jb.coef;
   float2*      sym  = jb.samples;
   const int    cp   = static_cast<int>(jb.cp);
-  auto dst = [sym, coef, cp](int n, float2 v) {
-    const float2 y = cmul(v, coef);
-    sym[cp + n]    = y;
-    if (n >= N - cp) {
-      sym[n - (N - cp)] = y;
-    }
-  };
-  dft_any<N, +1>(lds, tw, src, dst);
+  if constexpr (N == 4096) {
+    // Two consecutive points per store (n even): 16-byte stores when the symbol's first sample is 16-byte aligned
+    // (plans and every even cyclic prefix; direct jobs may point anywhere).
+    const bool wide = ((reinterpret_cast<uintptr_t>(sym + cp) | reinterpret_cast<uintptr_t>(sym)) & 15) == 0;
+    auto dst_pair = [sym, coef, cp, wide](int n, float2 v0, float2 v1) {
+      const float2 y0 = cmul(v0, coef);
+      const float2 y1 = cmul(v1, coef);
+      // Byte offsets as unsigned 32-bit values from the symbol's SGPR base.
+      char* base = reinterpret_cast<char*>(sym);
+      if (wide) {  // (cp even: both points or neither fall in the prefix's source range)
+        const float4 y = make_float4(y0.x, y0.y, y1.x, y1.y);
+        *reinterpret_cast<float4*>(base + static_cast<uint32_t>(cp + n) * 8u) = y;
+        if (n >= N - cp) {
+          *reinterpret_cast<float4*>(base + static_cast<uint32_t>(n - (N - cp)) * 8u) = y;
+        }
+      } else {
+        *reinterpret_cast<float2*>(base + static_cast<uint32_t>(cp + n) * 8u)     = y0;
+        *reinterpret_cast<float2*>(base + static_cast<uint32_t>(cp + n + 1) * 8u) = y1;
+        if (n >= N - cp) {
+          *reinterpret_cast<float2*>(base + static_cast<uint32_t>(n - (N - cp)) * 8u) = y0;
+        }
+        if (n + 1 >= N - cp) {
+          *reinterpret_cast<float2*>(base + static_cast<uint32_t>(n + 1 - (N - cp)) * 8u) = y1;
+        }
+      }
+    };
+    dft4096_two_waves<+1>(lds, tw, src, dst_pair);
+  } else {
+    auto dst = [sym, coef, cp](int n, float2 v) {
+      const float2 y = cmul(v, coef);
+      sym[cp + n]    = y;
+      if (n >= N - cp) {
+        sym[n - (N - cp)] = y;
+      }
+    };
+    dft_any<N, +1>(lds, tw, src, dst);
+  }
 }
 
 template <int N, typename JS>
@@ -605,29 +645,27 @@ __global__ __launch_bounds__(ofdm_kernel_threads<N>(-1), ofdm_min_waves<N>(-1)) 
   __shared__ float2 lds[N];  // (the two-wave 4096-point demodulation measured 10 % slower in isolation)
   const job_ref     jb   = js.get(blockIdx.x);
   const int         half = static_cast<int>(nsc / 2);
-  const float2*     x    = jb.samples + jb.cp - window_offset;
-  auto              src  = [x](int n) { return x[n]; };
+  // Unsigned 32-bit byte offsets from the job's SGPR bases (no 64-bit address arithmetic per access).
+  const char*       x    = reinterpret_cast<const char*>(jb.samples + jb.cp - window_offset);
+  auto              src  = [x](int n) { return *reinterpret_cast<const float2*>(x + static_cast<uint32_t>(n) * 8u); };
   const float2      coef = jb.coef;
-  uint32_t*         row  = jb.grid;
-  uint32_t*         row2 = jb.grid_copy;
+  char*             row  = reinterpret_cast<char*>(jb.grid);
+  char*             row2 = reinterpret_cast<char*>(jb.grid_copy);
   auto dst = [row, row2, coef, half, tw, window_offset](int b, float2 v) {
-    int sc = -1;
-    if (b < half) {
-      sc = half + b;
-    } else if (b >= N - half) {
-      sc = b - (N - half);
-    }
-    if (sc < 0) {
-      return;
-    }
-    float2 y = cmul(v, coef);
+    const uint32_t ub    = static_cast<uint32_t>(b);
+    const bool     lower = ub < static_cast<uint32_t>(half);
+    const bool     upper = ub >= static_cast<uint32_t>(N - half);
+    const uint32_t sc    = lower ? ub + static_cast<uint32_t>(half) : ub - static_cast<uint32_t>(N - half);
+    float2         y     = cmul(v, coef);
     if (window_offset != 0) {  // times exp(+j 2 pi offset b / N)
-      y = cmul(y, twiddle_any<N, +1>(tw, (window_offset * static_cast<uint32_t>(b)) % N));
+      y = cmul(y, twiddle_any<N, +1>(tw, (window_offset * ub) % N));
     }
     const uint32_t w = bf16_bits(y.x) | (bf16_bits(y.y) << 16);
-    row[sc]          = w;
-    if (row2 != nullptr) {
-      row2[sc] = w;
+    if (lower || upper) {  // guard bins are not stored
+      *reinterpret_cast<uint32_t*>(row + sc * 4u) = w;
+      if (row2 != nullptr) {
+        *reinterpret_cast<uint32_t*>(row2 + sc * 4u) = w;
+      }
     }
   };
   dft_any<N, -1>(lds, tw, src, dst);

@@ -164,7 +164,7 @@ for step in "$@"; do
           echo "-- $lib"
           SRSGPU_LIB=srsran-5g_amd/$lib/libsrsgpu_phy.so timeout -k 10 120 python -u tools/ofdm_bench.py \
             > "$OUT/ofdmab_${lib}_$i.txt" 2>&1 || { tail -20 "$OUT/ofdmab_${lib}_$i.txt"; exit 1; }
-          head -2 "$OUT/ofdmab_${lib}_$i.txt"
+          grep "ofdm_" "$OUT/ofdmab_${lib}_$i.txt" || true
         done
       done ;;
     setsweep)

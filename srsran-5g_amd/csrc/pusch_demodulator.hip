@@ -390,13 +390,16 @@ __device__ __forceinline__ void load_re(const demod_desc& d,
   }
   const uint32_t ge = d.grid_base + l * d.nsc + sc;
   const uint32_t ee = d.ce_base + (d.ce_compact ? 0u : l * d.nsc) + sc;
+  // Unsigned 32-bit byte offsets from the buffers' SGPR bases (saddr loads, no 64-bit address arithmetic per load).
+  const char* gb = reinterpret_cast<const char*>(grids);
+  const char* cb = reinterpret_cast<const char*>(ce);
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     if (p < static_cast<int>(d.P)) {
-      yw[p] = grids[ge + p * d.port_stride];
+      yw[p] = *reinterpret_cast<const uint32_t*>(gb + (ge + p * d.port_stride) * 4u);
 #pragma unroll
       for (int ly = 0; ly < L; ++ly) {
-        hw[ly][p] = ce[ee + ly * d.ce_layer_stride + p * d.port_stride];
+        hw[ly][p] = *reinterpret_cast<const uint32_t*>(cb + (ee + ly * d.ce_layer_stride + p * d.port_stride) * 4u);
       }
     }
   }

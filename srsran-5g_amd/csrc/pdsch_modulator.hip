@@ -32,7 +32,9 @@ __device__ __forceinline__ uint32_t scrambled_word(const mod_desc& d,
                                                    const uint32_t* __restrict__ seq,
                                                    uint32_t w)
 {
-  return __builtin_bswap32(cw[d.cw_word_offset + w]) ^ seq[d.seq_word_offset + w];
+  return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(cw) +
+                                                              (d.cw_word_offset + w) * 4u)) ^
+         *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(seq) + (d.seq_word_offset + w) * 4u);
 }
 
 /// Plan-time fill of the (de)scrambling sequences (launch_gold_fill): Gold sequence by GF(2) jumps.
@@ -165,7 +167,9 @@ __device__ __forceinline__ void modulate_res(const mod_desc& d,
             si             = (ly == 0) ? pi : si + pi;
           }
         }
-        grids[e + static_cast<uint32_t>(p) * d.port_stride] = to_bf16_bits(sr) | (to_bf16_bits(si) << 16);
+        // (an unsigned 32-bit byte offset from the grid's SGPR base: saddr stores)
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(grids) + (e + static_cast<uint32_t>(p) * d.port_stride) * 4u) =
+            to_bf16_bits(sr) | (to_bf16_bits(si) << 16);
       }
     }
   }

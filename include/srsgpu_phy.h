@@ -519,6 +519,16 @@ int srsgpu_ofdm_modulator_plan_execute(const srsgpu_ofdm_plan* plan,
                                        float*                  d_samples,
                                        void*                   stream);
 
+/** As srsgpu_ofdm_modulator_plan_execute, every RE taken from d_twin (same layout as d_grids, e.g. the PDSCH slot
+ *  batch's HBM grid) unless it holds 0xffffffff, then from d_grids (the REs the host channels wrote): the modulation
+ *  of a grid whose PDSCH REs never left the GPU (lower_phy_gpu's PDxCH, downlink_processor_single_executor_impl.cpp:268
+ *  send_resource_grid -> pdxch_processor_impl handle_request). Not for the split DFT sizes. */
+int srsgpu_ofdm_modulator_plan_execute_twin(const srsgpu_ofdm_plan* plan,
+                                            const uint32_t*         d_grids,
+                                            const uint32_t*         d_twin,
+                                            float*                  d_samples,
+                                            void*                   stream);
+
 /** Demodulates d_samples into d_grids (every subcarrier of every symbol is written). Asynchronous. */
 int srsgpu_ofdm_demodulator_plan_execute(const srsgpu_ofdm_plan* plan,
                                          const float*            d_samples,

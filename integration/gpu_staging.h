@@ -324,5 +324,128 @@ private:
   std::map<uintptr_t, twin>                                  twins;   ///< base -> HBM twin
 };
 
+/// HBM twins of downlink resource grids (the DL counterpart of host_blocks::twin), keyed by the grid's writer: when the
+/// GPU PDxCH of a sector on the same device modulates the grid (it subscribes), the PDSCH slot batch leaves its slot's
+/// PDSCH REs in the twin (a device copy of its sentinel-filled scratch grid) instead of downloading them into the host
+/// grid, and the PDxCH modulates every RE from the twin unless it holds the sentinel, then from the host grid (the REs
+/// the CPU channels wrote): the grid's PDSCH part crosses PCIe neither way. Stream-ordered on both sides: the producer
+/// waits for the consumer's last read of the twin before its copy, the consumer for the producer's copy. A publication
+/// is tagged with its slot, so a consumer never takes one meant for an earlier use of the same grid.
+class dl_grid_twins
+{
+public:
+  /// A consumer on `device` modulates the grid keyed `key` (idempotent).
+  static void subscribe(const void* key, int device)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    if (r.enabled) {
+      r.entries[key].device = device;
+    }
+  }
+  static void unsubscribe(const void* key)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    auto                        it = r.entries.find(key);
+    if (it != r.entries.end()) {
+      it->second.device = -1;
+    }
+  }
+  /// Tests: false makes every producer download its grid (the path the twin replaces).
+  static void set_enabled(bool on)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    r.enabled = on;
+  }
+
+  /// Producer (current device `device`): the twin buffer for `key` (grown to `bytes`) after `s` waits for the
+  /// consumer's last read of it; nullptr when no consumer on `device` subscribed to `key`.
+  static uint8_t* begin(const void* key, int device, size_t bytes, hipStream_t s)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    auto                        it = r.entries.find(key);
+    if (!r.enabled || it == r.entries.end() || it->second.device != device) {
+      return nullptr;
+    }
+    entry& e = it->second;
+    if (e.bytes < bytes) {
+      std::lock_guard<std::recursive_mutex> setup(hip_setup_mutex());
+      if (e.dev != nullptr) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(e.dev);
+        e.dev = nullptr;
+      }
+      if (hipMalloc(&e.dev, bytes) != hipSuccess) {
+        e.dev   = nullptr;
+        e.bytes = 0;
+        return nullptr;
+      }
+      e.bytes = bytes;
+      if (e.ready == nullptr) {
+        (void)hipEventCreateWithFlags(&e.ready, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&e.consumed, hipEventDisableTiming);
+      }
+    }
+    (void)hipStreamWaitEvent(s, e.consumed, 0);
+    e.pending = false;
+    return e.dev;
+  }
+  /// Producer: the twin of `key` holds slot `slot` once `s` reaches this point.
+  static void publish(const void* key, uint32_t slot, hipStream_t s)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    entry&                      e = r.entries[key];
+    (void)hipEventRecord(e.ready, s);
+    e.slot    = slot;
+    e.pending = true;
+  }
+  /// Consumer: the twin of `key` for `slot` with `bytes` bytes (`s` waits for it), or nullptr. release() follows
+  /// the launch that reads it.
+  static const uint8_t* take(const void* key, uint32_t slot, size_t bytes, hipStream_t s)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    auto                        it = r.entries.find(key);
+    if (it == r.entries.end() || !it->second.pending || it->second.slot != slot || it->second.bytes < bytes) {
+      return nullptr;
+    }
+    it->second.pending = false;
+    (void)hipStreamWaitEvent(s, it->second.ready, 0);
+    return it->second.dev;
+  }
+  static void release(const void* key, hipStream_t s)
+  {
+    auto&                       r = get();
+    std::lock_guard<std::mutex> lock(r.mtx);
+    auto                        it = r.entries.find(key);
+    if (it != r.entries.end()) {
+      (void)hipEventRecord(it->second.consumed, s);
+    }
+  }
+
+private:
+  struct entry {
+    int        device   = -1;  ///< the subscribed consumer's device (-1: none)
+    uint8_t*   dev      = nullptr;
+    size_t     bytes    = 0;
+    hipEvent_t ready    = nullptr;
+    hipEvent_t consumed = nullptr;
+    uint32_t   slot     = 0;
+    bool       pending  = false;
+  };
+  static dl_grid_twins& get()
+  {
+    static dl_grid_twins r;
+    return r;
+  }
+  std::mutex                         mtx;
+  bool                               enabled = true;
+  std::map<const void*, entry>       entries;
+};
+
 } // namespace gpu
 } // namespace srsran

@@ -704,6 +704,7 @@ public:
       gpu::srsgpu_check(srsgpu_ofdm_modulator_plan_create(ctx, &c, 1, nof_ports, &s, &p), WHO);
       plans.push_back(p);
     }
+    gpu::hip_check(hipGetDevice(&device_id), WHO, "device");
     if (group_owner) {
       group  = &group_owner->batcher(true, geo.nslot);
       sector = group->add_sector(plans);
@@ -716,6 +717,9 @@ public:
     requests.for_each([this](job_ptr& j) { recycle(std::move(j)); });
     if (sector >= 0) {
       group->remove_sector(sector);
+    }
+    for (const void* key : twin_keys) {
+      gpu::dl_grid_twins::unsubscribe(key);
     }
     (void)hipStreamSynchronize(stream.get());
     std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());
@@ -791,6 +795,16 @@ private:
     j->launched = false;
     const resource_grid_reader& reader = grid.get_reader();
     const bool                  empty  = reader.is_empty();
+    // An ungrouped sector modulates the grid itself: it takes the PDSCH REs from the grid's HBM twin when the PDSCH
+    // slot batch of its device left them there (gpu::dl_grid_twins).
+    const void* twin_key = nullptr;
+    if (sector < 0) {
+      twin_key = &grid.get_writer();
+      if (std::find(twin_keys.begin(), twin_keys.end(), twin_key) == twin_keys.end()) {
+        gpu::dl_grid_twins::subscribe(twin_key, device_id);
+        twin_keys.push_back(twin_key);
+      }
+    }
     const int e = (sector >= 0 && !empty) ? group->acquire(sector) : -1;
     if (e >= 0) {
       // Grouped: the rows go into this sector's staging entry, modulated in the group's next launch.
@@ -799,8 +813,8 @@ private:
       j->entry         = e;
       j->subframe_slot = context.slot.subframe_slot_index();
       j->launched      = true;
-    } else if (!empty) {
-      launch(*j, reader, context.slot.subframe_slot_index());
+    } else if (twin_key != nullptr || !empty) {
+      launch(*j, reader, context.slot.subframe_slot_index(), twin_key, context.slot.to_uint());
     }
     auto old = requests.exchange({context.slot, std::move(j)});
     if (old.payload) {
@@ -812,21 +826,43 @@ private:
     }
   }
 
-  /// Stages the grid's non-empty ports and modulates the whole slot on the processor's stream (no waiting).
-  void launch(job& j, const resource_grid_reader& reader, unsigned subframe_slot)
+  /// Stages the grid's non-empty ports and modulates the whole slot on the processor's stream (no waiting). With
+  /// `twin_key`, the PDSCH REs come from the grid's HBM twin when one was published for `slot` (then every port is
+  /// staged and modulated); without a twin an empty grid launches nothing.
+  void launch(job& j, const resource_grid_reader& reader, unsigned subframe_slot, const void* twin_key = nullptr,
+              uint32_t slot = 0)
   {
     gpu::device_scope           dev(ctx, WHO);
     std::lock_guard<std::mutex> lock(launch_mtx);
     const size_t                row   = static_cast<size_t>(nsc) * sizeof(uint32_t);
     const size_t                slotn = geo.slot_size(subframe_slot);
     hipStream_t                 s     = stream.get();
+    const size_t                gsize = nof_ports * geo.nsymb * row;
+    const uint8_t*              twin  = (twin_key != nullptr && geo.nsymb == 14)
+                                            ? gpu::dl_grid_twins::take(twin_key, slot, gsize, s)
+                                            : nullptr;
+    if (twin == nullptr && reader.is_empty()) {
+      return;  // nothing to transmit
+    }
     j.grid.reserve(nof_ports * geo.nsymb * row);
     j.samples.reserve(nof_ports * slotn * sizeof(cf_t));
     if (j.done == nullptr) {
       std::lock_guard<std::recursive_mutex> setup(gpu::hip_setup_mutex());
       gpu::hip_check(hipEventCreateWithFlags(&j.done, hipEventDisableTiming), WHO, "event");
     }
-    stage_grid(j, reader, j.grid.host());
+    stage_grid(j, reader, j.grid.host(), twin != nullptr);
+    if (twin != nullptr) {
+      gpu::srsgpu_check(srsgpu_ofdm_modulator_plan_execute_twin(plans[subframe_slot], j.grid.dev<uint32_t>(),
+                                                                reinterpret_cast<const uint32_t*>(twin),
+                                                                j.samples.dev<float>(), s),
+                        WHO);
+      gpu::dl_grid_twins::release(twin_key, s);
+      gpu::hip_check(hipEventRecord(j.done, s), WHO, "event");
+      j.subframe_slot = subframe_slot;
+      j.launched      = true;
+      j.own           = true;
+      return;
+    }
     // The modulation reads the rows and writes the samples in mapped host memory (no DMA copies), one captured launch
     // per (job, slot of the subframe), built on first use.
     if (j.graph_buffers[0] != j.grid.dev() || j.graph_buffers[1] != j.samples.dev()) {
@@ -852,12 +888,18 @@ private:
   }
 
   /// The grid rows of every non-empty port into `dst` ([port][symbol][subcarrier] uint32), the empty ports noted.
-  void stage_grid(job& j, const resource_grid_reader& reader, uint8_t* dst)
+  /// `all_ports` (an HBM twin holds the PDSCH REs): no port is empty, an empty one's rows are zeros.
+  void stage_grid(job& j, const resource_grid_reader& reader, uint8_t* dst, bool all_ports = false)
   {
     const size_t row = static_cast<size_t>(nsc) * sizeof(uint32_t);
     j.port_empty.assign(nof_ports, false);
     for (unsigned p = 0; p != nof_ports; ++p) {
       j.port_empty[p] = reader.is_empty(p);
+      if (j.port_empty[p] && all_ports) {
+        j.port_empty[p] = false;
+        std::memset(dst + p * geo.nsymb * row, 0, geo.nsymb * row);
+        continue;
+      }
       if (j.port_empty[p]) {
         continue;  // its rows stay stale on the device; the port's output is zeros
       }
@@ -912,6 +954,8 @@ private:
   unsigned                        nof_ports;
   unsigned                        nsc;
   std::vector<srsgpu_ofdm_plan*>  plans;  ///< One whole-slot plan (all ports) per slot of the subframe.
+  int                             device_id = 0;
+  std::vector<const void*>        twin_keys;  ///< grids subscribed to (gpu::dl_grid_twins)
   std::atomic<bool>               stopped  = false;
   pdxch_processor_notifier*       notifier = nullptr;
   slot_point                      current_slot;

@@ -52,6 +52,7 @@ struct pdsch_entry {
   std::vector<uint8_t>           data;
   unsigned                       cw_bytes = 0;
   crb_bitmap                     crbs;  ///< the allocation's CRBs (the multi-device gather moves these bands)
+  uint32_t                       slot = 0;  ///< pdu.slot (the HBM twin's publication tag)
   pdsch_modulator::config_t      mod;
   dmrs_pdsch_processor::config_t dmrs;
 };
@@ -71,6 +72,7 @@ struct {
   std::atomic<uint64_t> grid_downloads{0};
   std::atomic<uint64_t> shard_merges{0};
   std::atomic<uint64_t> merge_bytes{0};
+  std::atomic<uint64_t> twin_grids{0};
 } pdsch_transfers;
 
 
@@ -81,8 +83,9 @@ class pdsch_shard
   static constexpr const char* WHO = "pdsch_slot_batch";
 
 public:
-  explicit pdsch_shard(int device) :
-    owner(shared_context(device)),
+  explicit pdsch_shard(int device_) :
+    device(device_),
+    owner(shared_context(device_)),
     ctx(owner.get()),
     stream(ctx, WHO),
     enc_plans(srsgpu_pdsch_encoder_plan_destroy, 16),
@@ -230,6 +233,7 @@ public:
     hip_check(hipGraphLaunch(exec, s), WHO, "graph launch");
   }
 
+  int                                               device;
   std::shared_ptr<srsgpu_context>                   owner;
   srsgpu_context*                                   ctx;
   owned_stream                                      stream;
@@ -250,7 +254,7 @@ public:
 pdsch_multi_transfer_counters get_pdsch_multi_transfer_counters()
 {
   return {pdsch_transfers.grid_downloads.load(), pdsch_transfers.shard_merges.load(),
-          pdsch_transfers.merge_bytes.load()};
+          pdsch_transfers.merge_bytes.load(), pdsch_transfers.twin_grids.load()};
 }
 
 class pdsch_slot_batch
@@ -288,6 +292,7 @@ public:
     pdsch_entry                 e;
     e.grid                     = &grid;
     e.notifier                 = &notifier;
+    e.slot                     = pdu.slot.to_uint();
     span<const uint8_t> tb     = data[0].get_buffer();
     const unsigned      nre    = pdsch_compute_nof_data_re(pdu);
     const unsigned      qm     = get_bits_per_symbol(pdu.codewords[0].modulation);
@@ -362,6 +367,29 @@ public:
     }
     pdsch_shard& root = *shards[0];
     if (D == 1) {
+      // A GPU PDxCH on this device modulates the grid (gpu::dl_grid_twins): the REs stay in the grid's HBM twin.
+      uint8_t* twin = nullptr;
+      {
+        device_scope rdev(root.ctx, WHO);
+        twin = gpu::dl_grid_twins::begin(&grid, root.device, gsize, root.stream.get());
+        if (twin != nullptr) {
+          // Without the download's synchronisation below, the previous slot's launch is waited for here, before this
+          // one rewrites its TB staging.
+          hip_check(hipStreamSynchronize(root.stream.get()), WHO, "synchronise");
+        }
+      }
+      if (twin != nullptr) {
+        root.launch(part[0], grid_prb, P, false);
+        device_scope rdev(root.ctx, WHO);
+        hip_check(hipMemcpyAsync(twin, root.grid_buf.dev(), gsize, hipMemcpyDeviceToDevice, root.stream.get()), WHO,
+                  "twin copy");
+        gpu::dl_grid_twins::publish(&grid, es.front().slot, root.stream.get());
+        pdsch_transfers.twin_grids.fetch_add(1, std::memory_order_relaxed);
+        for (pdsch_entry& e : es) {
+          e.notifier->on_finish_processing();
+        }
+        return;
+      }
       root.launch(part[0], grid_prb, P, true);
     } else {
       // The shards' launches first, so that they run while the root maps its own UEs.

@@ -179,6 +179,7 @@ struct pdsch_multi_transfer_counters {
   uint64_t grid_downloads = 0;
   uint64_t shard_merges   = 0;
   uint64_t merge_bytes    = 0;
+  uint64_t twin_grids     = 0;  ///< slots whose PDSCH REs stayed in the grid's HBM twin for the GPU PDxCH (no download)
 };
 pdsch_multi_transfer_counters get_pdsch_multi_transfer_counters();
 

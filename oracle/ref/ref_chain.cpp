@@ -11,6 +11,7 @@
 // test's PUSCH: the PUSCH scrambling (c_init = rnti 2^15 + n_id), modulation, layer mapping and DM-RS sequences are the
 // PDSCH ones (TS 38.211 6.3.1.1 / 7.3.1.1, 6.4.1.1.1 / 7.4.1.1.1).
 #include "hw_accelerator_pusch_dec_gpu.h"
+#include "gpu_staging.h"
 #include "signal_chain_gpu.h"
 #include "upper_phy_gpu.h"
 
@@ -1659,13 +1660,15 @@ void chain_multi_transfer_counters(uint64_t* out)
 }
 
 /// Process-wide grid transfer counts of the PDSCH slot batches (gpu::get_pdsch_multi_transfer_counters): out[0]
-/// device-to-host grid downloads, out[1] shard-to-root merges, out[2] bytes those merges moved.
+/// device-to-host grid downloads, out[1] shard-to-root merges, out[2] bytes those merges moved, out[3] slots whose
+/// PDSCH REs stayed in the grid's HBM twin for the GPU PDxCH.
 void chain_pdsch_transfer_counters(uint64_t* out)
 {
   const gpu::pdsch_multi_transfer_counters c = gpu::get_pdsch_multi_transfer_counters();
   out[0]                                     = c.grid_downloads;
   out[1]                                     = c.shard_merges;
   out[2]                                     = c.merge_bytes;
+  out[3]                                     = c.twin_grids;
 }
 
 /// One UL slot: the PUSCH PDUs (tb_bytes[i] each) registered in the reference's PDU repository, the received grid
@@ -2519,6 +2522,131 @@ int chain_du_low_dl(int                 device,
       upper[k]->wait();
     }
     group.reset();
+    return 0;
+  });
+}
+
+/// One sector's downlink on the calling thread: the GPU downlink processor (PDSCH slot batch, row b8) hands each
+/// slot's grid to the GPU PDxCH processor (gateway -> handle_request, as du_low's upper-PHY gateway does), which
+/// modulates it; `slots` slots, with the downlink HBM grid twin enabled or not (gpu::dl_grid_twins::set_enabled).
+/// Before its PDSCHs every slot's grid gets host-written REs (random, in symbols 0-1 and above PRB 270 as PDCCH /
+/// CSI-RS would put them), so the twin's merge of device and host REs is exercised. out: every slot's 14 symbols x
+/// nof_ports complex samples in order [slot][symbol][port][sample] (as float pairs); counters: [PDSCH grid downloads,
+/// slots through the twin, late PDxCH requests] over the run.
+int chain_dl_twin_samples(int                 device,
+                          int                 twin,
+                          unsigned            slots,
+                          int                 nof_pdus,
+                          const chain_params* pdus,
+                          const float*        weights,
+                          const uint8_t*      tbs,
+                          const int*          tb_bytes,
+                          unsigned            nof_ports,
+                          unsigned            grid_prb,
+                          unsigned            dft_size,
+                          float*              out,
+                          uint64_t*           counters)
+{
+  return guarded("chain_dl_twin_samples", [&] {
+    gpu::dl_grid_twins::set_enabled(twin != 0);
+    const double                srate = static_cast<double>(dft_size) * 30e3;
+    std::unique_ptr<dl_harness> h(dl_create(device, 1, nof_ports, grid_prb));
+    struct late_notifier : public pdxch_processor_notifier {
+      std::atomic<unsigned> late{0};
+      void                  on_pdxch_request_late(const resource_grid_context& /*c*/) override { ++late; }
+    } notifier;
+    struct writer : public baseband_gateway_buffer_writer {
+      std::vector<span<cf_t>> ch;
+      unsigned                get_nof_channels() const override { return ch.size(); }
+      unsigned                get_nof_samples() const override { return ch.empty() ? 0 : ch[0].size(); }
+      span<cf_t>              get_channel_buffer(unsigned i) override { return ch[i]; }
+    };
+    pdxch_processor_configuration c;
+    c.cp                                 = cyclic_prefix::NORMAL;
+    c.scs                                = subcarrier_spacing::kHz30;
+    c.srate                              = sampling_rate::from_Hz(srate);
+    c.bandwidth_rb                       = grid_prb;
+    c.center_freq_Hz                     = 3.5e9;
+    c.nof_tx_ports                       = nof_ports;
+    std::unique_ptr<pdxch_processor> px  = create_pdxch_processor_factory_gpu(device)->create(c);
+    px->connect(notifier);
+    std::atomic<unsigned> forwarded{0};
+    pdxch_processor*      pxp = px.get();
+    h->gateway.forward        = [pxp, &forwarded](const resource_grid_context& ctx, shared_resource_grid g) {
+      pxp->get_request_handler().handle_request(g, ctx);
+      ++forwarded;
+    };
+    const gpu::pdsch_multi_transfer_counters before = gpu::get_pdsch_multi_transfer_counters();
+    std::mt19937                             rng(7);
+    std::normal_distribution<float>          nd(0.F, 0.5F);
+    const unsigned                           nsc = 12 * grid_prb;
+    std::vector<cf_t>                        row(nsc);
+    std::vector<cf_t>                        buf(static_cast<size_t>(nof_ports) * (dft_size + dft_size / 8));
+    size_t                                   o = 0;
+    for (unsigned i = 0; i != slots; ++i) {
+      const slot_point          sp(subcarrier_spacing::kHz30, i);
+      unique_downlink_processor dl = h->proc->get_controller().configure_resource_grid({sp, 0}, h->pool->grab());
+      if (!dl.is_valid()) {
+        throw std::runtime_error("downlink processor not available");
+      }
+      resource_grid& g = h->pool->grid;
+      g.set_all_zero();
+      for (unsigned p = 0; p != nof_ports; ++p) {
+        for (unsigned l = 0; l != 14; ++l) {
+          const unsigned k0 = l < 2 ? 0 : std::min(nsc, 270U * 12);
+          for (unsigned k = k0; k < nsc; ++k) {
+            row[k] = cf_t(nd(rng), nd(rng));
+          }
+          if (k0 < nsc) {
+            g.get_writer().put(p, l, k0, span<const cf_t>(row.data() + k0, nsc - k0));
+          }
+        }
+      }
+      const uint8_t* tb = tbs;
+      const float*   w  = weights;
+      for (int q = 0; q != nof_pdus; ++q) {
+        chain_params cq = pdus[q];
+        cq.slot         = static_cast<int>(sp.slot_index());
+        static_vector<shared_transport_block, pdsch_processor::MAX_NOF_TRANSPORT_BLOCKS> data;
+        data.emplace_back(span<const uint8_t>(tb, static_cast<size_t>(tb_bytes[q])));
+        dl->process_pdsch(std::move(data), make_pdsch_pdu(cq, w));
+        tb += tb_bytes[q];
+        w += 2 * cq.nof_ports * cq.nof_layers;
+      }
+      dl.release();
+      for (int t = 0; forwarded.load() != i + 1; ++t) {  // the grid reaches the PDxCH (inline executor: at once)
+        if (t == 5000) {
+          throw std::runtime_error("the grid of a slot never reached the PDxCH processor");
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      }
+      for (unsigned l = 0; l != 14; ++l) {
+        const unsigned n = cyclic_prefix(cyclic_prefix::NORMAL)
+                               .get_length(sp.subframe_slot_index() * 14 + l, subcarrier_spacing::kHz30)
+                               .to_samples(srate) +
+                           dft_size;
+        writer wb;
+        for (unsigned p = 0; p != nof_ports; ++p) {
+          wb.ch.emplace_back(buf.data() + static_cast<size_t>(p) * (dft_size + dft_size / 8), n);
+        }
+        const bool any = pxp->get_baseband().process_symbol(wb, {sp, 0, l});
+        for (unsigned p = 0; p != nof_ports; ++p) {
+          for (unsigned k = 0; k != n; ++k) {
+            const cf_t v = any ? wb.ch[p][k] : cf_t();
+            out[o++]     = v.real();
+            out[o++]     = v.imag();
+          }
+        }
+      }
+    }
+    const gpu::pdsch_multi_transfer_counters after = gpu::get_pdsch_multi_transfer_counters();
+    counters[0]                                    = after.grid_downloads - before.grid_downloads;
+    counters[1]                                    = after.twin_grids - before.twin_grids;
+    counters[2]                                    = notifier.late.load();
+    h->gateway.forward                             = nullptr;
+    px.reset();
+    h.reset();
+    gpu::dl_grid_twins::set_enabled(true);
     return 0;
   });
 }

@@ -416,6 +416,24 @@ int srsgpu_ofdm_modulator_plan_execute(const srsgpu_ofdm_plan* plan,
   return SRSGPU_OK;
 }
 
+int srsgpu_ofdm_modulator_plan_execute_twin(const srsgpu_ofdm_plan* plan,
+                                            const uint32_t*         d_grids,
+                                            const uint32_t*         d_twin,
+                                            float*                  d_samples,
+                                            void*                   stream)
+{
+  if (plan == nullptr || d_grids == nullptr || d_twin == nullptr || d_samples == nullptr || !plan->inverse) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "null argument or not a modulator plan");
+  }
+  if (ofdm_split_factor(plan->dft_size) != 0) {
+    return fail(SRSGPU_ERR_INVALID_ARG, "no twin grid for the split DFT size %u", plan->dft_size);
+  }
+  launch_ofdm(true, plan->dft_size, plan->d_jobs, plan->nof_jobs, plan->nsc, 0, plan->ctx->d_ofdm_twiddles, d_grids,
+              nullptr, nullptr, d_samples, plan->d_scratch, static_cast<hipStream_t>(stream), d_twin);
+  HIP_TRY(hipGetLastError());
+  return SRSGPU_OK;
+}
+
 int srsgpu_ofdm_demodulator_plan_execute(const srsgpu_ofdm_plan* plan,
                                          const float*            d_samples,
                                          uint32_t*               d_grids,

@@ -21,6 +21,7 @@
 // n1 < M, the N2-point DFT of x[n1 + M n2] (n2 < N2) times exp(S 2 pi i n1 k2 / N) into scratch[k2][n1]; the second runs
 // the M-point LDS transform of each scratch row k2 and writes output k2 + N2 k1 with the same fused last-pass work.
 // X[k2 + N2 k1] = sum_n1 W_M^(n1 k1) W_N^(n1 k2) sum_n2 x[n1 + M n2] W_N2^(n2 k2).
+#include <type_traits>
 #include "srsgpu_internal.h"
 
 namespace srsgpu {
@@ -549,6 +550,7 @@ struct offset_jobs {
   const ofdm_job* jobs;
   uint32_t*       grid;
   float2*         samples;
+  uint32_t*       twin = nullptr;  ///< modulation: the grid's HBM twin (same layout), read first (nullptr: none)
   __device__ __forceinline__ job_ref get(unsigned b) const
   {
     // The job is the workgroup's (b = blockIdx.x): its offsets in SGPRs, so that every grid load and sample store
@@ -559,7 +561,7 @@ struct offset_jobs {
     return {grid + goff, samples + soff, static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(j.cp_len)),
             make_float2(__uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(j.coef_re))),
                         __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(j.coef_im)))),
-            nullptr};
+            twin != nullptr ? twin + goff : nullptr};
   }
 };
 
@@ -574,7 +576,9 @@ struct direct_jobs {
   }
 };
 
-template <int N, typename JS>
+/// TWIN: every RE comes from the job's twin row (jb.grid_copy, the PDSCH batch's HBM grid) unless that holds the
+/// sentinel 0xffffffff, then from its grid row (the REs the host wrote).
+template <int N, typename JS, bool TWIN = false>
 __global__ __launch_bounds__(ofdm_kernel_threads<N>(+1), ofdm_min_waves<N>(+1)) void ofdm_modulate_kernel(JS js,
                                                                                               uint32_t nsc,
                                                                                               const float2* __restrict__ tw)
@@ -583,15 +587,24 @@ __global__ __launch_bounds__(ofdm_kernel_threads<N>(+1), ofdm_min_waves<N>(+1)) 
   const job_ref       jb   = js.get(blockIdx.x);
   const int           half = static_cast<int>(nsc / 2);
   const uint32_t*     row  = jb.grid;
+  const uint32_t*     trow = jb.grid_copy;
   // Bin b < rg/2 carries subcarrier rg/2 + b, bin b >= N - rg/2 subcarrier b - (N - rg/2), the rest are zero. The
   // guard bins load subcarrier 0 and discard it (no branch per load; unsigned offsets from the row's SGPR base).
-  auto src = [row, half](int b) {
+  auto src = [row, trow, half](int b) {
     const uint32_t ub    = static_cast<uint32_t>(b);
     const bool     lower = ub < static_cast<uint32_t>(half);
     const bool     upper = ub >= static_cast<uint32_t>(N - half);
     const uint32_t sc    = lower ? ub + static_cast<uint32_t>(half) : (upper ? ub - static_cast<uint32_t>(N - half) : 0u);
-    uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(row) + sc * 4u);
-    u          = (lower || upper) ? u : 0u;
+    uint32_t u;
+    if constexpr (TWIN) {
+      u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(trow) + sc * 4u);
+      if (u == 0xffffffffu) {
+        u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(row) + sc * 4u);
+      }
+    } else {
+      u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(row) + sc * 4u);
+    }
+    u = (lower || upper) ? u : 0u;
     return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
   };
   const float2 coef = jb.coef;
@@ -824,6 +837,13 @@ void launch_one(bool inverse, JS js, int nof_jobs, uint32_t nsc, uint32_t window
 {
   const int threads = ofdm_kernel_threads<N>(inverse ? 1 : -1);  // every thread takes part in the passes' barriers
   if (inverse) {
+    if constexpr (std::is_same_v<JS, offset_jobs>) {
+      if (js.twin != nullptr) {
+        hipLaunchKernelGGL((ofdm_modulate_kernel<N, JS, true>), dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0,
+                           stream, js, nsc, tw);
+        return;
+      }
+    }
     hipLaunchKernelGGL((ofdm_modulate_kernel<N, JS>), dim3(static_cast<unsigned>(nof_jobs)), dim3(threads), 0, stream,
                        js, nsc, tw);
   } else {
@@ -869,7 +889,8 @@ void launch_ofdm(bool            inverse,
                  const float*    d_samples_in,
                  float*          d_samples_out,
                  float*          d_scratch,
-                 hipStream_t     stream)
+                 hipStream_t     stream,
+                 const uint32_t* d_twin)
 {
   if (nof_jobs <= 0) {
     return;
@@ -879,7 +900,7 @@ void launch_ofdm(bool            inverse,
   auto*       so  = reinterpret_cast<float2*>(d_samples_out);
   // The kernels only read the input buffer of their direction.
   const offset_jobs js{d_jobs, inverse ? const_cast<uint32_t*>(d_grid_in) : d_grid_out,
-                       inverse ? so : const_cast<float2*>(sin)};
+                       inverse ? so : const_cast<float2*>(sin), inverse ? const_cast<uint32_t*>(d_twin) : nullptr};
   if (launch_sizes(inverse, dft_size, js, nof_jobs, nsc, window_offset, tw, stream)) {
     return;
   }

@@ -407,7 +407,8 @@ void launch_ofdm(bool            inverse,
                  const float*    d_samples_in,
                  float*          d_samples_out,
                  float*          d_scratch,
-                 hipStream_t     stream);
+                 hipStream_t     stream,
+                 const uint32_t* d_twin = nullptr);  ///< modulation: HBM twin of d_grid_in (not for split sizes)
 /// Direct-address job list (srsgpu_ofdm_jobs_execute_direct); false for a split DFT size (nothing launched).
 bool launch_ofdm_direct(bool                          inverse,
                         uint32_t                      dft_size,

@@ -410,6 +410,8 @@ def load_library(path: str = LIB_PATH):
     lib.srsgpu_ofdm_plan_sample_offset.restype = ctypes.c_uint64
     lib.srsgpu_ofdm_modulator_plan_execute.argtypes = [P, P, P, P]
     lib.srsgpu_ofdm_demodulator_plan_execute.argtypes = [P, P, P, P]
+    if hasattr(lib, "srsgpu_ofdm_modulator_plan_execute_twin"):
+        lib.srsgpu_ofdm_modulator_plan_execute_twin.argtypes = [P, P, P, P, P]
     lib.srsgpu_ofdm_plan_destroy.argtypes = [P]
     lib.srsgpu_ofdm_plan_destroy.restype = None
     for name in ("srsgpu_pusch_decoder_plan", "srsgpu_pdsch_encoder_plan"):
@@ -437,6 +439,7 @@ EXPORTED_SYMBOLS = [
     "srsgpu_ofdm_modulator_plan_create", "srsgpu_ofdm_demodulator_plan_create", "srsgpu_ofdm_plan_nof_samples",
     "srsgpu_ofdm_modulator_symbols_plan_create", "srsgpu_ofdm_demodulator_symbols_plan_create", "srsgpu_harq_copy",
     "srsgpu_ofdm_plan_sample_offset", "srsgpu_ofdm_modulator_plan_execute", "srsgpu_ofdm_demodulator_plan_execute",
+    "srsgpu_ofdm_modulator_plan_execute_twin",
     "srsgpu_ofdm_plan_concat", "srsgpu_ofdm_plan_nof_grid_words", "srsgpu_ofdm_plan_get_jobs",
     "srsgpu_ofdm_jobs_execute", "srsgpu_ofdm_jobs_execute_direct", "srsgpu_copy_spans", "srsgpu_merge_spans",
     "srsgpu_ofdm_plan_destroy", "srsgpu_pusch_demodulator_plan_create", "srsgpu_pusch_demodulator_plan_nof_llrs",
@@ -1578,6 +1581,11 @@ class OfdmPlan:
     def execute(self, d_in, d_out, stream=None):
         f = _lib.srsgpu_ofdm_modulator_plan_execute if self.inverse else _lib.srsgpu_ofdm_demodulator_plan_execute
         _check(f(self.handle, _dptr(d_in), _dptr(d_out), _stream_handle(stream)))
+
+    def execute_twin(self, d_grid, d_twin, d_samples, stream=None):
+        """srsgpu_ofdm_modulator_plan_execute_twin: every RE from d_twin unless it holds 0xffffffff, else from d_grid."""
+        _check(_lib.srsgpu_ofdm_modulator_plan_execute_twin(self.handle, _dptr(d_grid), _dptr(d_twin), _dptr(d_samples),
+                                                            _stream_handle(stream)))
 
     def close(self):
         if getattr(self, "handle", None):

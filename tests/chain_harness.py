@@ -155,9 +155,9 @@ class UpperPhy:
 
     def pdsch_transfer_counters(self):
         """Process-wide grid transfers of the PDSCH slot batches (chain_pdsch_transfer_counters)."""
-        out = np.zeros(3, np.uint64)
+        out = np.zeros(4, np.uint64)
         self.lib.chain_pdsch_transfer_counters(_ptr(out))
-        return dict(zip(("grid_downloads", "shard_merges", "merge_bytes"), (int(v) for v in out)))
+        return dict(zip(("grid_downloads", "shard_merges", "merge_bytes", "twin_grids"), (int(v) for v in out)))
 
     def close(self):
         if self.ul:

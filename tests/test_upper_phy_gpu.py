@@ -321,3 +321,49 @@ def test_gpu_factories_pdu_validators_equal_reference():
     res = H.factory_validate(0, 1, dl, w)
     assert [r[:2] for r in res] == [(r[1], r[1]) for r in res], res
     assert not any(r[2] for r in res), res
+
+
+def test_dl_grid_twin_equals_downloaded_grid():
+    """du_low DL with the grid's PDSCH part kept on the GPU (integration/gpu_staging.h dl_grid_twins; verdict item 5's
+    DL half): one sector's GPU downlink processor (PDSCH slot batch) hands each slot's grid to the GPU PDxCH processor
+    through the reference's gateway path (downlink_processor_single_executor_impl.cpp:268 send_resource_grid ->
+    pdxch handle_request). With the twin the batch leaves its PDSCH REs in HBM (no download, no host store) and the
+    PDxCH modulates them merged with the REs the host wrote into the grid (symbols 0-1 and the PRBs above the PDSCH,
+    random); without it the batch downloads the REs into the host grid as the reference's PDSCH processor writes them.
+    The baseband samples of every slot, symbol and port are equal, and the counters show which path ran (the first slot
+    precedes the PDxCH's subscription, so it downloads)."""
+    import ctypes
+
+    import chain_harness as H
+
+    lib = ctypes.CDLL(H.CHAIN_SO)
+    f = lib.chain_dl_twin_samples
+    f.restype = ctypes.c_int
+    f.argtypes = ([ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.POINTER(H.ChainParams)] +
+                  [ctypes.c_void_p] * 3 + [ctypes.c_uint] * 3 + [ctypes.c_void_p] * 2)
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    rng = np.random.default_rng(11)
+    tbs = sch.tbs_calculate(270, 12, 6 * 3 * 2, 0, 8, 948.0, 4)
+    pdu = H.params(slot=0, rnti=1, n_id=0, scrambling_id=0, nof_rb=270, rb_start=0, bwp_size=273, qm=8,
+                   target_code_rate=948.0, nof_layers=4, nof_ports=4, start_symbol=2, nof_symbols=12,
+                   dmrs_mask=(1 << 2) | (1 << 7) | (1 << 11), base_graph=sch.base_graph(tbs, 948 / 1024),
+                   tbs_lbrm_bytes=159749)
+    q, _ = np.linalg.qr(rng.normal(size=(4, 4)) + 1j * rng.normal(size=(4, 4)))
+    w = np.ascontiguousarray(q.astype(np.complex64).ravel()).view(np.float32)
+    tbb = np.array([tbs // 8], np.int32)
+    data = rng.integers(0, 256, int(tbb.sum())).astype(np.uint8)
+    arr = (H.ChainParams * 1)(pdu)
+    slots = 4
+    res = {}
+    for twin in (0, 1):
+        out = np.zeros(slots * P * 61440 * 2, np.float32)
+        cnt = np.zeros(3, np.uint64)
+        r = f(0, twin, slots, 1, arr, ptr(w), ptr(data), ptr(tbb), P, 273, 4096, ptr(out), ptr(cnt))
+        assert r == 0, r
+        res[twin] = (out, cnt)
+    (ref, c0), (got, c1) = res[0], res[1]
+    assert int(c0[0]) == slots and int(c0[1]) == 0, c0   # every slot downloaded
+    assert int(c1[1]) == slots - 1 and int(c1[0]) == 1, c1  # all but the first through the twin
+    assert int(c0[2]) == 0 and int(c1[2]) == 0
+    assert np.abs(ref).max() > 0
+    np.testing.assert_array_equal(got, ref)

@@ -64,6 +64,13 @@ def run_dl(lib, args, out):
     f.argtypes = ([ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_int, ctypes.POINTER(H.ChainParams)] +
                   [ctypes.c_void_p] * 3 + [ctypes.c_uint] * 3 + [ctypes.c_int] + [ctypes.c_void_p] * 3)
     ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    lib.chain_pdsch_transfer_counters.argtypes = [ctypes.c_void_p]
+
+    def pdsch_twins():
+        c = np.zeros(4, np.uint64)
+        lib.chain_pdsch_transfer_counters(ptr(c))
+        return int(c[3])
+
     rng = np.random.default_rng(6)
     for name, pdus, tbs, weights in dl_profiles(rng):
         arr = (H.ChainParams * len(pdus))(*pdus)
@@ -77,9 +84,11 @@ def run_dl(lib, args, out):
                 lag = np.zeros((S, 4), np.float64)
                 results = np.zeros((S, 2), np.int32)
                 secs = np.zeros(1, np.float64)
+                t0 = pdsch_twins()
                 r = f(0, S, args.slots, len(pdus), arr, ptr(w), ptr(data), ptr(tbb), P, PRB, DFT,
                       1 if variant == "group" else 0, ptr(lag), ptr(results), ptr(secs))
                 assert r == 0, r
+                twins = pdsch_twins() - t0
                 # every slot's 14 symbols but the first two slots' (requested before the run) carried samples
                 complete = bool((results[:, 0] >= 14 * (args.slots - 2)).all())
                 rt = bool(lag[:, 1].max() < 0.5e-3 and lag[:, 2].max() < 0.01 and complete and lag[:, 3].sum() == 0)
@@ -87,7 +96,8 @@ def run_dl(lib, args, out):
                                         "late_fraction": lag[:, 2].max(), "late_requests": int(lag[:, 3].sum()),
                                         "symbols_with_samples": int(results[:, 0].sum()),
                                         "dl_slots_processed": int(results[:, 1].sum()), "complete": complete,
-                                        "seconds": float(secs[0]), "real_time": rt}
+                                        "seconds": float(secs[0]), "real_time": rt,
+                                        "grids_from_hbm_twin": twins}
                 print(json.dumps({name: {variant: {S: res["by_sectors"][S]}}}), file=sys.stderr, flush=True)
             rts = [S for S, v in res["by_sectors"].items() if v["real_time"]]
             res["sectors_at_real_time"] = max(rts) if rts else 0

@@ -334,13 +334,15 @@ private:
 class dl_grid_twins
 {
 public:
-  /// A consumer on `device` modulates the grid keyed `key` (idempotent).
-  static void subscribe(const void* key, int device)
+  /// A consumer on `device` modulates the grid keyed `key`, whose [port][symbol][subcarrier] image has `bytes` bytes
+  /// (idempotent).
+  static void subscribe(const void* key, int device, size_t bytes)
   {
     auto&                       r = get();
     std::lock_guard<std::mutex> lock(r.mtx);
     if (r.enabled) {
       r.entries[key].device = device;
+      r.entries[key].want   = bytes;
     }
   }
   static void unsubscribe(const void* key)
@@ -361,13 +363,14 @@ public:
   }
 
   /// Producer (current device `device`): the twin buffer for `key` (grown to `bytes`) after `s` waits for the
-  /// consumer's last read of it; nullptr when no consumer on `device` subscribed to `key`.
+  /// consumer's last read of it; nullptr when no consumer on `device` subscribed to `key` with that image size (then
+  /// the producer writes the host grid as before).
   static uint8_t* begin(const void* key, int device, size_t bytes, hipStream_t s)
   {
     auto&                       r = get();
     std::lock_guard<std::mutex> lock(r.mtx);
     auto                        it = r.entries.find(key);
-    if (!r.enabled || it == r.entries.end() || it->second.device != device) {
+    if (!r.enabled || it == r.entries.end() || it->second.device != device || it->second.want != bytes) {
       return nullptr;
     }
     entry& e = it->second;
@@ -410,7 +413,7 @@ public:
     auto&                       r = get();
     std::lock_guard<std::mutex> lock(r.mtx);
     auto                        it = r.entries.find(key);
-    if (it == r.entries.end() || !it->second.pending || it->second.slot != slot || it->second.bytes < bytes) {
+    if (it == r.entries.end() || !it->second.pending || it->second.slot != slot || it->second.want != bytes) {
       return nullptr;
     }
     it->second.pending = false;
@@ -430,6 +433,7 @@ public:
 private:
   struct entry {
     int        device   = -1;  ///< the subscribed consumer's device (-1: none)
+    size_t     want     = 0;   ///< the subscribed consumer's image size
     uint8_t*   dev      = nullptr;
     size_t     bytes    = 0;
     hipEvent_t ready    = nullptr;

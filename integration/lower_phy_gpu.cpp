@@ -798,10 +798,10 @@ private:
     // An ungrouped sector modulates the grid itself: it takes the PDSCH REs from the grid's HBM twin when the PDSCH
     // slot batch of its device left them there (gpu::dl_grid_twins).
     const void* twin_key = nullptr;
-    if (sector < 0) {
+    if (sector < 0 && geo.nsymb == 14) {
       twin_key = &grid.get_writer();
       if (std::find(twin_keys.begin(), twin_keys.end(), twin_key) == twin_keys.end()) {
-        gpu::dl_grid_twins::subscribe(twin_key, device_id);
+        gpu::dl_grid_twins::subscribe(twin_key, device_id, static_cast<size_t>(nof_ports) * 14 * nsc * sizeof(uint32_t));
         twin_keys.push_back(twin_key);
       }
     }
@@ -838,9 +838,7 @@ private:
     const size_t                slotn = geo.slot_size(subframe_slot);
     hipStream_t                 s     = stream.get();
     const size_t                gsize = nof_ports * geo.nsymb * row;
-    const uint8_t*              twin  = (twin_key != nullptr && geo.nsymb == 14)
-                                            ? gpu::dl_grid_twins::take(twin_key, slot, gsize, s)
-                                            : nullptr;
+    const uint8_t*              twin  = twin_key != nullptr ? gpu::dl_grid_twins::take(twin_key, slot, gsize, s) : nullptr;
     if (twin == nullptr && reader.is_empty()) {
       return;  // nothing to transmit
     }

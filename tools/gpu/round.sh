@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
-# One parameterised GPU-box script for the round's measurements (replaces the one-off rN*.sh scripts, kept under
-# tools/gpu/archive/). Usage on the box (via gpurun):  tools/gpu/round.sh TAG STEP [STEP ...]
+# One parameterised GPU-box script for the round's measurements (replaces the one-off rN*.sh scripts of rounds 1-5,
+# in the git history). Usage on the box (via gpurun):  tools/gpu/round.sh TAG STEP [STEP ...]
 # Each step runs under its own time limit and writes into gpurun_out/TAG/; the script stops at the first failure.
 #   tests            GPU parity suite (pytest -m gpu)
 #   tests:EXPR       GPU tests selected by pytest -k EXPR

@@ -373,14 +373,6 @@ __device__ __forceinline__ void dft_lds(float2* lds, const float2* __restrict__ 
   }
 }
 
-/// Swaps a value between lanes 2i and 2i + 1 (DPP quad permutation [1, 0, 3, 2]).
-__device__ __forceinline__ float2 swap_lane_pairs(float2 v)
-{
-  constexpr int QUAD_1032 = 1 | (0 << 2) | (3 << 4) | (2 << 6);
-  return make_float2(__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.x), QUAD_1032, 0xf, 0xf, false)),
-                     __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), QUAD_1032, 0xf, 0xf, false)));
-}
-
 /// 4096 points on two waves (128 threads, two radix-16 butterflies per thread and pass, j0 = tid and j1 = tid + 128)
 /// through a 16 KB LDS buffer. The one-butterfly transform holds the 4096-point block in 32 KB of LDS and at 92 VGPRs
 /// runs 5 four-wave workgroups per CU: 5 symbols in flight per CU, and each waits out its HBM loads, barriers and
@@ -389,9 +381,8 @@ __device__ __forceinline__ float2 swap_lane_pairs(float2 v)
 /// of passes 1 and 2 into the first half of the 4096 points and j1's into the second, and each pass reads inputs
 /// j + 256 r, r < 8 from the first half and r >= 8 from the second: every exchange runs as write half A, read the A
 /// inputs, write half B, read the B inputs, with the same 2048-entry buffer.
-template <int S, typename Src, typename DstPair>
-__device__ __forceinline__ void dft4096_two_waves(float2* lds, const float2* __restrict__ tw, Src src_first,
-                                                  DstPair dst_pair)
+template <int S, typename Src, typename Dst>
+__device__ __forceinline__ void dft4096_two_waves(float2* lds, const float2* __restrict__ tw, Src src_first, Dst dst_last)
 {
   constexpr int T = 128, H = 2048;
   const int     tid = static_cast<int>(threadIdx.x);
@@ -477,28 +468,23 @@ __device__ __forceinline__ void dft4096_two_waves(float2* lds, const float2* __r
       },
       []() {});
   // Pass 3 (NS = 256): butterfly j (k = j) writes X[j + 256 r] to HBM. An opaque copy of the thread index keeps the
-  // output addressing here (hoisted to the kernel start, it spilled). Neighbouring lanes hold neighbouring points:
-  // for each pair r, r + 1 the even lane trades its X[j + 256 (r + 1)] for the odd lane's X[j + 1 + 256 r] (one DPP
-  // swap), so that every lane stores two consecutive points (16 bytes: half the store instructions of one point per
-  // lane, the stores being what the symbol's last phase waits on).
+  // output addressing here (hoisted to the kernel start, it spilled). One point per lane and store: two consecutive
+  // points per lane (a DPP lane-pair swap, 16-byte stores) measured the same within +-0.6 us in three A/Bs, for 32
+  // DPP moves and ~130 selects more (profiles/r6za_ofdm_modulator_ab.txt).
   int tid3 = tid;
   asm volatile("" : "+v"(tid3));
-  const bool odd  = (tid3 & 1) != 0;
-  const int  even = tid3 & ~1;
-  auto store_pairs = [&](float2 (&v)[16], int j) {
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      const float2 send = odd ? v[r] : v[r + 1];
-      const float2 recv = swap_lane_pairs(send);
-      dst_pair(j + 256 * (odd ? r + 1 : r), odd ? recv : v[r], odd ? v[r + 1] : recv);
-    }
-  };
   twiddle16(a, b2a);
   dft_reg<16, S>(a);
-  store_pairs(a, even);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    dst_last(tid3 + 256 * r, a[r]);
+  }
   twiddle16(c, b2b);
   dft_reg<16, S>(c);
-  store_pairs(c, even + T);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    dst_last(tid3 + T + 256 * r, c[r]);
+  }
 }
 
 /// Threads per workgroup of the N-point kernels of exponent sign S (the two-wave 4096-point transform, used by the
@@ -610,41 +596,18 @@ __global__ __launch_bounds__(ofdm_kernel_threads<N>(+1), ofdm_min_waves<N>(+1)) 
   const float2 coef = jb.coef;
   float2*      sym  = jb.samples;
   const int    cp   = static_cast<int>(jb.cp);
+  // Unsigned 32-bit byte offsets from the symbol's SGPR base.
+  auto dst = [sym, coef, cp](int n, float2 v) {
+    const float2 y    = cmul(v, coef);
+    char*        base = reinterpret_cast<char*>(sym);
+    *reinterpret_cast<float2*>(base + static_cast<uint32_t>(cp + n) * 8u) = y;
+    if (n >= N - cp) {
+      *reinterpret_cast<float2*>(base + static_cast<uint32_t>(n - (N - cp)) * 8u) = y;
+    }
+  };
   if constexpr (N == 4096) {
-    // Two consecutive points per store (n even): 16-byte stores when the symbol's first sample is 16-byte aligned
-    // (plans and every even cyclic prefix; direct jobs may point anywhere).
-    const bool wide = ((reinterpret_cast<uintptr_t>(sym + cp) | reinterpret_cast<uintptr_t>(sym)) & 15) == 0;
-    auto dst_pair = [sym, coef, cp, wide](int n, float2 v0, float2 v1) {
-      const float2 y0 = cmul(v0, coef);
-      const float2 y1 = cmul(v1, coef);
-      // Byte offsets as unsigned 32-bit values from the symbol's SGPR base.
-      char* base = reinterpret_cast<char*>(sym);
-      if (wide) {  // (cp even: both points or neither fall in the prefix's source range)
-        const float4 y = make_float4(y0.x, y0.y, y1.x, y1.y);
-        *reinterpret_cast<float4*>(base + static_cast<uint32_t>(cp + n) * 8u) = y;
-        if (n >= N - cp) {
-          *reinterpret_cast<float4*>(base + static_cast<uint32_t>(n - (N - cp)) * 8u) = y;
-        }
-      } else {
-        *reinterpret_cast<float2*>(base + static_cast<uint32_t>(cp + n) * 8u)     = y0;
-        *reinterpret_cast<float2*>(base + static_cast<uint32_t>(cp + n + 1) * 8u) = y1;
-        if (n >= N - cp) {
-          *reinterpret_cast<float2*>(base + static_cast<uint32_t>(n - (N - cp)) * 8u) = y0;
-        }
-        if (n + 1 >= N - cp) {
-          *reinterpret_cast<float2*>(base + static_cast<uint32_t>(n + 1 - (N - cp)) * 8u) = y1;
-        }
-      }
-    };
-    dft4096_two_waves<+1>(lds, tw, src, dst_pair);
+    dft4096_two_waves<+1>(lds, tw, src, dst);
   } else {
-    auto dst = [sym, coef, cp](int n, float2 v) {
-      const float2 y = cmul(v, coef);
-      sym[cp + n]    = y;
-      if (n >= N - cp) {
-        sym[n - (N - cp)] = y;
-      }
-    };
     dft_any<N, +1>(lds, tw, src, dst);
   }
 }
